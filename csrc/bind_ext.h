@@ -1,0 +1,6 @@
+// Binding entry points of the network (RTSP/RTP) and muxer (FLV/RTMP/MP4) layers.
+#pragma once
+#include <pybind11/pybind11.h>
+
+void bind_net(pybind11::module_& m);
+void bind_mux(pybind11::module_& m);

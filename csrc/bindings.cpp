@@ -1,0 +1,435 @@
+// pybind11 bindings of the vep native data plane (module `video_edge_ai_proxy_amd._vep`).
+// Every call that can block (decode, D2H, network) releases the GIL.
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "vep/bench_driver.h"
+#include "vep/codec.h"
+#include "vep/gpu.h"
+#include "vep/h264.h"
+#include "bind_ext.h"
+#include "vep/runtime.h"
+#include "vep/synth.h"
+
+namespace py = pybind11;
+using namespace vep;
+
+static py::bytes to_bytes(const u8* p, size_t n) {
+  return py::bytes(reinterpret_cast<const char*>(p), n);
+}
+
+static py::dict meta_dict(const FrameMeta& m) {
+  py::dict d;
+  d["width"] = m.width;
+  d["height"] = m.height;
+  d["timestamp"] = m.timestamp;
+  d["pts"] = m.pts;
+  d["dts"] = m.dts;
+  d["packet"] = m.packet;
+  d["keyframe"] = m.keyframe;
+  d["is_keyframe"] = m.is_keyframe;
+  d["is_corrupt"] = m.is_corrupt;
+  d["frame_type"] = std::string(1, m.frame_type);
+  d["time_base"] = m.time_base;
+  d["seq"] = m.seq;
+  d["decoded_us"] = m.decoded_us;
+  d["arrival_ms"] = m.arrival_ms;
+  return d;
+}
+
+static py::dict pic_dict(const PictureInfo& p) {
+  py::dict d;
+  d["width"] = p.width;
+  d["height"] = p.height;
+  d["coded_width"] = p.coded_width;
+  d["coded_height"] = p.coded_height;
+  d["pict_type"] = std::string(1, p.pict_type);
+  d["idr"] = p.idr;
+  d["frame_num"] = p.frame_num;
+  d["coded_mbs"] = p.coded_mbs;
+  d["fps"] = p.fps;
+  return d;
+}
+
+static Camera& cam_of(Worker& w, int idx) {
+  Camera* c = w.camera(idx);
+  if (!c) throw py::index_error("no camera with index " + std::to_string(idx));
+  return *c;
+}
+
+// Stateful oracle: parse + CPU reconstruct a sequence of AUs, return the final BGR picture.
+struct CpuDecoder {
+  H264Parser parser;
+  MbUpdate upd;
+  HostSurface surf;
+  PictureInfo last;
+  py::object decode(const AccessUnit& au) {
+    upd.slot.assign(upd.slot.size(), -1);
+    upd.nslots = 0;
+    upd.payload.clear();
+    last = parser.parse(au, upd);
+    if (surf.coded_w != last.coded_width || surf.coded_h != last.coded_height)
+      surf.alloc(last.coded_width, last.coded_height);
+    cpu_apply_update(upd, surf);
+    py::array_t<uint8_t> out({last.height, last.width, 3});
+    cpu_nv12_to_bgr(surf, last.crop_left, last.crop_top, last.width, last.height,
+                    out.mutable_data());
+    return out;
+  }
+};
+
+PYBIND11_MODULE(_vep, m) {
+  m.doc() = "vep native data plane (gfx950 HIP kernels, H.264 subset decoder, RTSP/RTP, muxers)";
+  py::register_exception<Error>(m, "NativeError");
+  py::register_exception<UnsupportedStream>(m, "UnsupportedStream");
+
+  m.def("device_count", &gpu::device_count);
+
+  py::class_<SynthConfig>(m, "SynthConfig")
+      .def(py::init<>())
+      .def_readwrite("width", &SynthConfig::width)
+      .def_readwrite("height", &SynthConfig::height)
+      .def_readwrite("fps", &SynthConfig::fps)
+      .def_readwrite("gop", &SynthConfig::gop)
+      .def_readwrite("motion", &SynthConfig::motion)
+      .def_readwrite("seed", &SynthConfig::seed)
+      .def_readwrite("slices", &SynthConfig::slices)
+      .def_readwrite("zero_samples", &SynthConfig::zero_samples);
+
+  py::class_<AccessUnit, std::shared_ptr<AccessUnit>>(m, "AccessUnit")
+      .def(py::init<>())
+      .def_property_readonly("codec", [](const AccessUnit& a) { return int(a.codec); })
+      .def_readwrite("pts", &AccessUnit::pts)
+      .def_readwrite("dts", &AccessUnit::dts)
+      .def_readwrite("duration", &AccessUnit::duration)
+      .def_readwrite("keyframe", &AccessUnit::keyframe)
+      .def_readwrite("corrupt", &AccessUnit::corrupt)
+      .def_readwrite("arrival_ms", &AccessUnit::arrival_ms)
+      .def_readwrite("seq", &AccessUnit::seq)
+      .def_property_readonly("size", &AccessUnit::bytes)
+      .def("nals",
+           [](const AccessUnit& a) {
+             py::list l;
+             for (size_t i = 0; i < a.nals.size(); ++i) l.append(to_bytes(a.nal(i), a.nal_size(i)));
+             return l;
+           })
+      .def("annexb",
+           [](const AccessUnit& a) {
+             std::string s;
+             for (size_t i = 0; i < a.nals.size(); ++i) {
+               s.append("\x00\x00\x00\x01", 4);
+               s.append(reinterpret_cast<const char*>(a.nal(i)), a.nal_size(i));
+             }
+             return py::bytes(s);
+           })
+      .def_static(
+          "from_nals",
+          [](const std::vector<std::string>& nals, i64 pts, i64 dts, bool key, int codec) {
+            auto a = std::make_shared<AccessUnit>();
+            a->codec = Codec(codec);
+            for (auto& n : nals) a->add_nal(reinterpret_cast<const u8*>(n.data()), n.size());
+            a->pts = pts;
+            a->dts = dts;
+            a->keyframe = key;
+            a->arrival_ms = now_ms();
+            return a;
+          },
+          py::arg("nals"), py::arg("pts") = 0, py::arg("dts") = 0, py::arg("keyframe") = false,
+          py::arg("codec") = 0);
+
+  py::class_<SynthH264>(m, "SynthH264")
+      .def(py::init<const SynthConfig&>())
+      .def("next", [](SynthH264& s) { return std::shared_ptr<AccessUnit>(s.next()); },
+           py::call_guard<py::gil_scoped_release>())
+      .def("picture",
+           [](const SynthH264& s) {
+             const HostSurface& p = s.picture();
+             py::array_t<uint8_t> y({p.coded_h, p.coded_w});
+             py::array_t<uint8_t> uv({p.coded_h / 2, p.coded_w});
+             std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
+             std::memcpy(uv.mutable_data(), p.uv.data(), p.uv.size());
+             return py::make_tuple(y, uv);
+           })
+      .def_property_readonly("sps_nal", [](const SynthH264& s) { return to_bytes(s.sps_nal().data(), s.sps_nal().size()); })
+      .def_property_readonly("pps_nal", [](const SynthH264& s) { return to_bytes(s.pps_nal().data(), s.pps_nal().size()); })
+      .def_property_readonly("frame_index", &SynthH264::frame_index);
+
+  py::class_<CpuDecoder>(m, "CpuDecoder")
+      .def(py::init<>())
+      .def("decode", &CpuDecoder::decode)
+      .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
+      .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.upd.nslots; })
+      .def("surface", [](const CpuDecoder& d) {
+        py::array_t<uint8_t> y({d.surf.coded_h, d.surf.coded_w});
+        py::array_t<uint8_t> uv({d.surf.coded_h / 2, d.surf.coded_w});
+        std::memcpy(y.mutable_data(), d.surf.y.data(), d.surf.y.size());
+        std::memcpy(uv.mutable_data(), d.surf.uv.data(), d.surf.uv.size());
+        return py::make_tuple(y, uv);
+      });
+
+  m.def("parse_sps", [](const std::string& nal) {
+    std::vector<u8> r(nal.size());
+    size_t n = ebsp_to_rbsp(reinterpret_cast<const u8*>(nal.data()), nal.size(), r.data());
+    h264::Sps s = h264::parse_sps(r.data(), n);
+    py::dict d;
+    d["profile_idc"] = s.profile_idc;
+    d["level_idc"] = s.level_idc;
+    d["width"] = s.width();
+    d["height"] = s.height();
+    d["coded_width"] = s.coded_width();
+    d["coded_height"] = s.coded_height();
+    d["fps"] = s.fps();
+    d["poc_type"] = s.poc_type;
+    d["max_num_ref_frames"] = s.max_num_ref_frames;
+    return d;
+  });
+  m.def("rbsp_to_ebsp", [](const std::string& r) {
+    std::vector<u8> out;
+    rbsp_to_ebsp(reinterpret_cast<const u8*>(r.data()), r.size(), out);
+    return to_bytes(out.data(), out.size());
+  });
+  m.def("ebsp_to_rbsp", [](const std::string& e) {
+    std::vector<u8> out(e.size());
+    size_t n = ebsp_to_rbsp(reinterpret_cast<const u8*>(e.data()), e.size(), out.data());
+    return to_bytes(out.data(), n);
+  });
+  m.def("find_epb", [](const std::string& e) {
+    std::vector<u32> out;
+    find_epb(reinterpret_cast<const u8*>(e.data()), e.size(), out);
+    return out;
+  });
+  m.def("split_annexb", [](const std::string& b) {
+    auto v = h264::split_annexb(reinterpret_cast<const u8*>(b.data()), b.size());
+    py::list l;
+    for (auto& [o, n] : v) l.append(py::bytes(b.data() + o, n));
+    return l;
+  });
+  m.def("bitwriter_roundtrip", [](const std::vector<u32>& ue_vals, const std::vector<i32>& se_vals) {
+    BitWriter bw;
+    for (u32 v : ue_vals) bw.ue(v);
+    for (i32 v : se_vals) bw.se(v);
+    bw.trailing();
+    BitReader br(bw.buf().data(), bw.buf().size());
+    std::vector<u32> u;
+    std::vector<i32> s;
+    for (size_t i = 0; i < ue_vals.size(); ++i) u.push_back(br.ue());
+    for (size_t i = 0; i < se_vals.size(); ++i) s.push_back(br.se());
+    bool at_stop = br.bitpos() == br.stop_bit_pos();
+    return py::make_tuple(u, s, at_stop);
+  });
+
+  py::class_<Worker>(m, "Worker")
+      .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
+                       std::vector<float> stdv, int max_cameras) {
+             WorkerOptions o;
+             o.device = device;
+             o.letterbox_size = letterbox_size;
+             o.chw_dtype = chw_dtype;
+             for (int k = 0; k < 3; ++k) {
+               o.mean[k] = mean.size() == 3 ? mean[size_t(k)] : 0.f;
+               o.std[k] = stdv.size() == 3 ? stdv[size_t(k)] : 1.f;
+             }
+             o.max_cameras = max_cameras;
+             return std::make_unique<Worker>(o);
+           }),
+           py::arg("device") = 0, py::arg("letterbox_size") = 0, py::arg("chw_dtype") = 0,
+           py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
+           py::arg("max_cameras") = 256)
+      .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
+      .def("add_camera", &Worker::add_camera, py::arg("name"), py::arg("ring_slots") = 2)
+      .def("remove_camera", &Worker::remove_camera, py::call_guard<py::gil_scoped_release>())
+      .def("find", [](Worker& w, const std::string& n) { Camera* c = w.find(n); return c ? c->index() : -1; })
+      .def("num_cameras", &Worker::num_cameras)
+      .def("start", &Worker::start)
+      .def("stop", &Worker::stop, py::call_guard<py::gil_scoped_release>())
+      .def("flush", &Worker::flush, py::call_guard<py::gil_scoped_release>())
+      .def("set_last_query", [](Worker& w, int i, i64 ms) { cam_of(w, i).last_query_ms.store(ms); })
+      .def("last_query", [](Worker& w, int i) { return cam_of(w, i).last_query_ms.load(); })
+      .def("set_keyframe_only", [](Worker& w, int i, bool v) { cam_of(w, i).keyframe_only.store(v); })
+      .def("keyframe_only", [](Worker& w, int i) { return cam_of(w, i).keyframe_only.load(); })
+      .def("set_proxy", [](Worker& w, int i, bool v) { cam_of(w, i).proxy_rtmp.store(v); })
+      .def("proxy", [](Worker& w, int i) { return cam_of(w, i).proxy_rtmp.load(); })
+      .def("set_idle_cutoff_ms", [](Worker& w, int i, i64 v) { cam_of(w, i).idle_cutoff_ms.store(v); })
+      .def("submit_au",
+           [](Worker& w, int i, std::shared_ptr<AccessUnit> au) {
+             Camera& c = cam_of(w, i);
+             py::gil_scoped_release r;
+             return c.on_access_unit(au);
+           })
+      .def("decode_now",
+           [](Worker& w, int i, std::shared_ptr<AccessUnit> au) {
+             Camera& c = cam_of(w, i);
+             py::gil_scoped_release r;
+             DecodeJob job;
+             if (!c.make_job(au, job)) return false;
+             std::vector<DecodeJob> v;
+             v.push_back(std::move(job));
+             w.run_batch(v);
+             return true;
+           })
+      .def("stats",
+           [](Worker& w, int i) {
+             Camera& c = cam_of(w, i);
+             py::dict d;
+             d["packets"] = c.packets.load();
+             d["decoded"] = c.decoded.load();
+             d["skipped"] = c.skipped.load();
+             d["errors"] = c.errors.load();
+             d["bytes_in"] = c.bytes_in.load();
+             d["last_packet_ms"] = c.last_packet_ms.load();
+             d["published"] = c.ring() ? c.ring()->published() : 0;
+             d["width"] = c.ring() ? c.ring()->width() : 0;
+             d["height"] = c.ring() ? c.ring()->height() : 0;
+             d["ring_slots"] = c.ring() ? c.ring()->slots() : c.ring_slots_cfg;
+             return d;
+           })
+      .def("log", [](Worker& w, int i, bool err, const std::string& line) { cam_of(w, i).logs.add(err, line); })
+      .def("logs", [](Worker& w, int i, bool err, int last) { return cam_of(w, i).logs.dump(err, size_t(last)); },
+           py::arg("idx"), py::arg("err") = false, py::arg("last") = 100)
+      .def("read_latest",
+           [](Worker& w, int i, i64 after) -> py::object {
+             Camera& c = cam_of(w, i);
+             if (!c.ring()) return py::none();
+             size_t n = c.ring()->slot_bytes();
+             py::array_t<uint8_t> out({c.ring()->height(), c.ring()->width(), 3});
+             FrameMeta m;
+             bool ok;
+             u8* dst = out.mutable_data();
+             {
+               py::gil_scoped_release r;
+               ok = w.read_latest(i, after, &m, dst, n);
+             }
+             if (!ok) return py::none();
+             return py::make_tuple(meta_dict(m), out);
+           },
+           py::arg("idx"), py::arg("after") = 0)
+      .def("video_frame",
+           // Serialized VideoFrame proto built in one buffer: header, D2H'd pixels, trailer.
+           [](Worker& w, int i, i64 after, const std::string& device_id) -> py::object {
+             Camera& c = cam_of(w, i);
+             if (!c.ring()) return py::none();
+             size_t n = c.ring()->slot_bytes();
+             FrameMeta probe;
+             int slot;
+             if (!c.ring()->latest(after, &probe, &slot)) return py::none();
+             auto [pre0, suf0] = encode_video_frame(probe, n, device_id);
+             size_t total = pre0.size() + n + suf0.size() + 64;
+             PyObject* b = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(total));
+             if (!b) throw py::error_already_set();
+             py::object holder = py::reinterpret_steal<py::object>(b);
+             char* buf = PyBytes_AS_STRING(b);
+             FrameMeta m;
+             bool ok;
+             {
+               py::gil_scoped_release r;
+               ok = w.read_latest(i, after, &m, reinterpret_cast<u8*>(buf) + 32 + pre0.size(), n);
+             }
+             if (!ok) return py::none();
+             auto [pre, suf] = encode_video_frame(m, n, device_id);
+             // header may differ in length from the probe: place it right before the data
+             char* data = buf + 32 + pre0.size();
+             char* start = data - pre.size();
+             std::memcpy(start, pre.data(), pre.size());
+             std::memcpy(data + n, suf.data(), suf.size());
+             size_t len = pre.size() + n + suf.size();
+             py::bytes res(start, len);  // one host copy into an exact-size object
+             return py::make_tuple(m.seq, res, meta_dict(m));
+           },
+           py::arg("idx"), py::arg("after") = 0, py::arg("device_id") = "")
+      .def("set_consumer_buffers",
+           [](Worker& w, uintptr_t hwc, uintptr_t chw, int rows) {
+             w.set_consumer_buffers(reinterpret_cast<u8*>(hwc), reinterpret_cast<void*>(chw), rows);
+           })
+      .def("consumer_hwc_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.consumer_hwc()); })
+      .def("consumer_chw_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.consumer_chw()); })
+      .def("ring_slot_ptr", [](Worker& w, int i, int s) {
+        Camera& c = cam_of(w, i);
+        if (!c.ring()) return uintptr_t(0);
+        return reinterpret_cast<uintptr_t>(c.ring()->slot_ptr(s));
+      })
+      .def("latest_slot", [](Worker& w, int i) -> py::object {
+        Camera& c = cam_of(w, i);
+        FrameMeta m;
+        int slot;
+        if (!c.ring() || !c.ring()->latest(0, &m, &slot)) return py::none();
+        return py::make_tuple(slot, meta_dict(m));
+      })
+      .def_property_readonly("batches", &Worker::batches)
+      .def_property_readonly("frames", &Worker::frames)
+      .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
+      .def("compute_stream_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.compute_stream()); });
+
+  py::class_<ReplayBench>(m, "ReplayBench")
+      .def(py::init([](Worker& w, int ncams, const SynthConfig& cfg, int cached, int threads,
+                       int ring_slots, const std::string& prefix) {
+             py::gil_scoped_release r;
+             return std::make_unique<ReplayBench>(w, ncams, cfg, cached, threads, ring_slots, prefix);
+           }),
+           py::arg("worker"), py::arg("ncams"), py::arg("cfg"), py::arg("cached_frames") = 30,
+           py::arg("threads") = 8, py::arg("ring_slots") = 2, py::arg("prefix") = "cam",
+           py::keep_alive<1, 2>())
+      .def("step", &ReplayBench::step, py::call_guard<py::gil_scoped_release>())
+      .def("drain", &ReplayBench::drain, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("frames", &ReplayBench::frames)
+      .def_property_readonly("payload_bytes", &ReplayBench::bitstream_bytes)
+      .def_property_readonly("parse_ms", &ReplayBench::parse_ms)
+      .def_property_readonly("batch_ms", &ReplayBench::batch_ms)
+      .def_property_readonly("cameras", &ReplayBench::cameras);
+
+  // ---- op API on caller-owned device buffers (torch tensors pass data_ptr / stream) ----
+  m.def("nv12_to_bgr",
+        [](uintptr_t y, uintptr_t uv, uintptr_t map, uintptr_t payload, int wmbs, int hmbs,
+           int out_w, int out_h, int crop_left, int crop_top, uintptr_t out, uintptr_t stream) {
+          gpu::DecodeDesc d{};
+          d.y = reinterpret_cast<u8*>(y);
+          d.uv = reinterpret_cast<u8*>(uv);
+          d.map = reinterpret_cast<const i32*>(map);
+          d.payload = reinterpret_cast<const u8*>(payload);
+          d.bgr = reinterpret_cast<u8*>(out);
+          d.wmbs = wmbs;
+          d.hmbs = hmbs;
+          d.out_w = out_w;
+          d.out_h = out_h;
+          d.crop_left = crop_left;
+          d.crop_top = crop_top;
+          d.tiles_x = (wmbs + gpu::kTileMbW - 1) / gpu::kTileMbW;
+          d.tile_begin = 0;
+          gpu::launch_decode_convert_one(d, reinterpret_cast<hipStream_t>(stream));
+        });
+  m.def("letterbox",
+        [](uintptr_t y, uintptr_t uv, int pitch, int src_w, int src_h, int crop_left, int crop_top,
+           int size, uintptr_t out_hwc, uintptr_t out_chw, int chw_dtype, std::vector<float> mean,
+           std::vector<float> stdv, int pad, uintptr_t stream) {
+          gpu::LetterboxDesc d{};
+          d.y = reinterpret_cast<const u8*>(y);
+          d.uv = reinterpret_cast<const u8*>(uv);
+          d.pitch = pitch;
+          d.src_w = src_w;
+          d.src_h = src_h;
+          d.crop_left = crop_left;
+          d.crop_top = crop_top;
+          d.out_hwc = reinterpret_cast<u8*>(out_hwc);
+          d.out_chw = reinterpret_cast<void*>(out_chw);
+          gpu::fill_letterbox_geometry(d, size);
+          gpu::LetterboxParams p{};
+          p.size = size;
+          p.chw_dtype = chw_dtype;
+          for (int k = 0; k < 3; ++k) {
+            p.mean[k] = mean.size() == 3 ? mean[size_t(k)] : 0.f;
+            p.inv_std[k] = 1.f / (stdv.size() == 3 ? stdv[size_t(k)] : 1.f);
+          }
+          p.pad_value = u8(pad);
+          gpu::launch_letterbox_one(d, p, reinterpret_cast<hipStream_t>(stream));
+        });
+  m.def("letterbox_geometry", [](int src_w, int src_h, int size) {
+    gpu::LetterboxDesc d{};
+    d.src_w = src_w;
+    d.src_h = src_h;
+    gpu::fill_letterbox_geometry(d, size);
+    return py::make_tuple(d.nw, d.nh, d.pad_x, d.pad_y);
+  });
+
+  bind_net(m);
+  bind_mux(m);
+}

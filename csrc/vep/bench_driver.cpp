@@ -1,0 +1,106 @@
+// Replay driver implementation. See bench_driver.h.
+#include "bench_driver.h"
+
+namespace vep {
+
+ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cached_frames,
+                         int threads, int ring_slots, const std::string& prefix)
+    : w_(w), pool_(threads) {
+  VEP_CHECK(ncams > 0, "bench needs at least one camera");
+  const int gop = std::max(1, base.gop);
+  const int nframes = std::max(gop, (cached_frames + gop - 1) / gop * gop);
+  aus_.resize(size_t(ncams));
+  pos_.assign(size_t(ncams), 0);
+  for (int i = 0; i < ncams; ++i)
+    cams_.push_back(w_.add_camera(prefix + std::to_string(i), ring_slots));
+  pool_.parallel_for(ncams, [&](int i) {
+    SynthConfig c = base;
+    c.seed = base.seed + u64(i) * 7919u;
+    SynthH264 enc(c);
+    auto& v = aus_[size_t(i)];
+    v.reserve(size_t(nframes));
+    for (int f = 0; f < nframes; ++f) v.push_back(enc.next());
+  });
+  pf_ = std::thread([this] { prefetch_loop(); });
+}
+
+ReplayBench::~ReplayBench() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (pf_.joinable()) pf_.join();
+}
+
+void ReplayBench::parse_tick(std::vector<DecodeJob>& out) {
+  const int n = int(cams_.size());
+  out.clear();
+  out.resize(size_t(n));
+  std::vector<char> ok(size_t(n), 0);
+  pool_.parallel_for(n, [&](int i) {
+    auto& v = aus_[size_t(i)];
+    const AuPtr& au = v[pos_[size_t(i)]];
+    pos_[size_t(i)] = (pos_[size_t(i)] + 1) % v.size();
+    Camera* c = w_.camera(cams_[size_t(i)]);
+    ok[size_t(i)] = c && c->make_job(au, out[size_t(i)]);
+  });
+  size_t k = 0;
+  for (int i = 0; i < n; ++i) {
+    if (!ok[size_t(i)]) continue;
+    if (size_t(i) != k) out[k] = std::move(out[size_t(i)]);
+    ++k;
+  }
+  out.resize(k);
+}
+
+void ReplayBench::prefetch_loop() {
+  std::vector<DecodeJob> jobs;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [&] { return stop_ || want_; });
+      if (stop_) return;
+    }
+    const i64 t0 = mono_us();
+    parse_tick(jobs);
+    const i64 t1 = mono_us();
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      parse_us_ += double(t1 - t0);
+      ready_.swap(jobs);
+      have_ready_ = true;
+      want_ = false;
+    }
+    cv_.notify_all();
+  }
+}
+
+void ReplayBench::step() {
+  std::vector<DecodeJob> jobs;
+  {
+    std::unique_lock<std::mutex> g(mu_);
+    if (!have_ready_ && !want_) {
+      want_ = true;
+      cv_.notify_all();
+    }
+    cv_.wait(g, [&] { return have_ready_; });
+    jobs.swap(ready_);
+    have_ready_ = false;
+    want_ = true;  // start parsing tick t+1 while tick t runs on the GPU
+  }
+  cv_.notify_all();
+  for (auto& j : jobs) bytes_ += u64(j.upd.nslots) * kPcmMbBytes;
+  const i64 t0 = mono_us();
+  const size_t n = jobs.size();
+  w_.run_batch(jobs);
+  batch_us_ += double(mono_us() - t0);
+  frames_ += n;
+}
+
+void ReplayBench::drain() {
+  std::unique_lock<std::mutex> g(mu_);
+  cv_.wait(g, [&] { return !want_; });
+}
+
+}  // namespace vep

@@ -1,0 +1,136 @@
+// Access units, the native H.264 macroblock-layer parser and the CPU reference reconstructor.
+//
+// Split of work (MI355X-first): the CPU does what is inherently serial — NAL parsing and the
+// CAVLC macroblock-layer walk — and emits a compact, 16-byte-aligned *MB update list*
+// (dense per-MB slot map + 384-byte sample slots). Reconstruction + colour conversion run as
+// one batched HIP kernel over all cameras of a GPU (gpu_kernels.hip).
+//
+// Native subset decoder: I_PCM macroblocks in I/P slices and P_Skip (zero-MV, single
+// reference, every picture a reference picture). This is the decodable subset emitted by the
+// synthetic camera farm (synth.h). Anything else is reported as unsupported so a
+// RocDecode/VCN backend can take the stream (SURVEY.md §7.4 hard part 1).
+//
+// Reference parity: python/read_image.py:47-133 (decode loop), :70-85 (GOP catch-up).
+#pragma once
+
+#include <map>
+#include <memory>
+
+#include "common.h"
+#include "h264.h"
+
+namespace vep {
+
+enum class Codec : int { kH264 = 0, kH265 = 1 };
+
+// One demuxed packet ≈ PyAV Packet (python/rtsp_to_rtmp.py:92).
+struct AccessUnit {
+  Codec codec = Codec::kH264;
+  std::vector<u8> data;                         // escaped NAL payloads, back to back
+  std::vector<std::pair<u32, u32>> nals;        // (offset, size) into data, no start codes
+  i64 pts = 0, dts = 0, duration = 0;           // 90 kHz
+  bool keyframe = false;
+  bool corrupt = false;
+  i64 arrival_ms = 0;
+  u64 seq = 0;                                  // per-camera packet counter
+
+  void add_nal(const u8* p, size_t n) {
+    nals.emplace_back(u32(data.size()), u32(n));
+    data.insert(data.end(), p, p + n);
+  }
+  const u8* nal(size_t i) const { return data.data() + nals[i].first; }
+  size_t nal_size(size_t i) const { return nals[i].second; }
+  size_t bytes() const { return data.size(); }
+};
+using AuPtr = std::shared_ptr<const AccessUnit>;
+
+// Accumulated macroblock updates for one camera surface; several AUs of a GOP can be
+// collapsed into one update (latest writer wins), which is how GOP catch-up
+// (read_image.py:80-85) becomes a single batched GPU launch.
+struct MbUpdate {
+  int width_mbs = 0, height_mbs = 0;
+  std::vector<i32> slot;   // per MB: payload slot or -1 (keep reference sample)
+  AlignedBuf payload;      // nslots * 384 B, 16-B aligned slots
+  int nslots = 0;
+  int frames = 0;          // AUs folded in
+
+  void reset(int wmbs, int hmbs) {
+    width_mbs = wmbs;
+    height_mbs = hmbs;
+    slot.assign(size_t(wmbs) * hmbs, -1);
+    payload.clear();
+    nslots = 0;
+    frames = 0;
+  }
+  int mbs() const { return width_mbs * height_mbs; }
+  u8* slot_for(int mb) {
+    int s = slot[mb];
+    if (s < 0) {
+      s = nslots++;
+      slot[mb] = s;
+      payload.resize(size_t(nslots) * kPcmMbBytes);
+    }
+    return payload.data() + size_t(s) * kPcmMbBytes;
+  }
+};
+
+// Picture-level metadata produced by the parser (fills VideoFrame fields).
+struct PictureInfo {
+  int width = 0, height = 0;          // cropped output size
+  int coded_width = 0, coded_height = 0;
+  int crop_left = 0, crop_top = 0;
+  char pict_type = '?';
+  bool idr = false;
+  int frame_num = 0;
+  int coded_mbs = 0;                  // non-skipped MBs in this AU
+  double fps = 0;
+};
+
+class UnsupportedStream : public Error {
+ public:
+  using Error::Error;
+};
+
+// Stateful H.264 AU parser (keeps SPS/PPS tables across AUs).
+class H264Parser {
+ public:
+  // Parse one AU; macroblock updates are folded into `upd` (which must be sized for the
+  // stream, see need_reset()). Throws UnsupportedStream for syntax outside the subset.
+  PictureInfo parse(const AccessUnit& au, MbUpdate& upd);
+  // Parameter sets only (no slice walk) — cheap keyframe/size probe.
+  void absorb_parameter_sets(const AccessUnit& au);
+  bool has_sps() const { return !sps_.empty(); }
+  const h264::Sps& active_sps() const;
+  const std::vector<u8>& last_sps_nal() const { return sps_nal_; }
+  const std::vector<u8>& last_pps_nal() const { return pps_nal_; }
+
+ private:
+  void walk_slice(const u8* rbsp, size_t n, const h264::SliceHeader& sh, BitReader& br,
+                  const h264::Sps& sps, MbUpdate& upd, int& coded);
+  std::map<int, h264::Sps> sps_;
+  std::map<int, h264::Pps> pps_;
+  int active_sps_id_ = -1;
+  std::vector<u8> sps_nal_, pps_nal_;
+  std::vector<u8> rbsp_scratch_;
+  std::vector<u32> epb_;
+};
+
+// Host NV12 surface (CPU backend / test oracle).
+struct HostSurface {
+  int coded_w = 0, coded_h = 0;
+  std::vector<u8> y, uv;  // NV12
+  void alloc(int w, int h) {
+    coded_w = w;
+    coded_h = h;
+    y.assign(size_t(w) * h, 16);
+    uv.assign(size_t(w) * h / 2, 128);
+  }
+};
+
+// CPU reference of the fused GPU kernel: apply MB update to the NV12 surface, then convert the
+// cropped picture to packed BGR24 (out must hold width*height*3 bytes).
+void cpu_apply_update(const MbUpdate& upd, HostSurface& s);
+void cpu_nv12_to_bgr(const HostSurface& s, int crop_left, int crop_top, int width, int height,
+                     u8* out);
+
+}  // namespace vep

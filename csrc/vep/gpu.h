@@ -1,0 +1,74 @@
+// gfx950 device layer: memory, streams and the batched HIP kernels of the data plane.
+//
+// Kernels (gpu_kernels.hip):
+//  * decode_convert — fused I_PCM macroblock reconstruction into the per-camera NV12 reference
+//    surface + BT.601 NV12->BGR24 conversion into the camera's HBM ring slot. One launch per
+//    worker step covers every camera of the GPU (block -> (camera, 8x2-MB tile)).
+//    Replaces libavcodec reconstruction + libswscale (read_image.py:87,94).
+//  * letterbox — NV12 surface -> letterboxed model input (HWC u8 and/or normalised CHW
+//    fp16/bf16/fp32), batched over cameras.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace vep::gpu {
+
+#define VEP_HIP(expr)                                                                    \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw ::vep::Error(std::string("HIP error ") + hipGetErrorString(_e) + " at " +     \
+                         __FILE__ + ":" + std::to_string(__LINE__) + ": " #expr);        \
+  } while (0)
+
+int device_count();  // 0 when no GPU / no driver
+
+// One camera-frame of a batched decode_convert launch (lives in device memory).
+struct DecodeDesc {
+  u8* y;              // NV12 luma plane, pitch = wmbs*16
+  u8* uv;             // NV12 interleaved chroma plane, pitch = wmbs*16
+  u8* bgr;            // output slot: out_h x out_w x 3 (packed BGR24); may be null
+  const i32* map;     // per-MB payload slot or -1; null = no update (pure conversion)
+  const u8* payload;  // 384-B PCM slots
+  i32 wmbs, hmbs;
+  i32 out_w, out_h;
+  i32 crop_left, crop_top;
+  i32 tile_begin;     // exclusive prefix sum of tiles over the batch
+  i32 tiles_x;
+};
+constexpr int kTileMbW = 8, kTileMbH = 2;  // 256 threads: 32 pixel rows x 8 MB columns
+inline int tiles_for(int wmbs, int hmbs) {
+  return ((wmbs + kTileMbW - 1) / kTileMbW) * ((hmbs + kTileMbH - 1) / kTileMbH);
+}
+
+void launch_decode_convert(const DecodeDesc* d_descs, int n, int total_tiles, hipStream_t s);
+// Single-frame variant: descriptor passed by value (op API on caller-owned buffers).
+void launch_decode_convert_one(const DecodeDesc& d, hipStream_t s);
+
+enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
+
+struct LetterboxDesc {
+  const u8* y;
+  const u8* uv;
+  i32 pitch;
+  i32 src_w, src_h, crop_left, crop_top;
+  u8* out_hwc;      // S*S*3 BGR u8, or null
+  void* out_chw;    // 3*S*S RGB normalised, or null
+  i32 nw, nh, pad_x, pad_y;
+  float rx, ry;     // src/dst scale per axis
+};
+struct LetterboxParams {
+  i32 size;          // S
+  i32 chw_dtype;     // ChwDtype
+  float mean[3];     // RGB
+  float inv_std[3];  // RGB
+  u8 pad_value;
+};
+void fill_letterbox_geometry(LetterboxDesc& d, int size);
+void launch_letterbox(const LetterboxDesc* d_descs, int n, const LetterboxParams& p,
+                      hipStream_t s);
+void launch_letterbox_one(const LetterboxDesc& d, const LetterboxParams& p, hipStream_t s);
+
+}  // namespace vep::gpu

@@ -1,0 +1,279 @@
+// gfx950 (CDNA4) kernels of the vep data plane. See gpu.h for the contracts.
+//
+// Design notes (MI355X):
+//  * Both kernels are HBM-bound streaming kernels (≈9.3 MB moved per 1080p frame for
+//    decode_convert), so the levers are 16-B vector accesses, full 64-lane waves with
+//    contiguous per-wave output, and >>256 workgroups per launch: one launch covers every
+//    camera on the GPU (32 x 1080p = 16,320 workgroups).
+//  * decode_convert maps a 256-thread workgroup onto an 8x2-macroblock tile, lane = one
+//    16-pixel row segment: 8 consecutive lanes write 8 x 48 B = 384 contiguous bytes of one
+//    BGR row, a wave covers 8 rows (no LDS needed — there is no intra-tile reuse).
+//  * PCM slots are 384 = 24 x 16 B, so every payload read is an aligned dwordx4 / dwordx2.
+//  * letterbox reads the NV12 surface (1.5 B/px) instead of the BGR slot (3 B/px).
+#include <algorithm>
+#include <cmath>
+
+#include "color.h"
+#include "gpu.h"
+
+namespace vep::gpu {
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+__device__ __forceinline__ uint32_t pack4(uint8_t a, uint8_t b, uint8_t c, uint8_t d) {
+  return uint32_t(a) | (uint32_t(b) << 8) | (uint32_t(c) << 16) | (uint32_t(d) << 24);
+}
+
+// 16 luma bytes + 8 interleaved (Cb,Cr) pairs -> 48 BGR bytes as 12 dwords.
+__device__ __forceinline__ void convert16(const uint4 yv, const uint4 uvv, uint32_t out[12]) {
+  const uint32_t yw[4] = {yv.x, yv.y, yv.z, yv.w};
+  const uint32_t cw[4] = {uvv.x, uvv.y, uvv.z, uvv.w};
+  uint8_t px[48];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    int y = (yw[i >> 2] >> (8 * (i & 3))) & 0xff;
+    int pair = i >> 1;  // chroma sample index 0..7: word pair>>1, byte (pair&1)*2
+    uint32_t w = cw[pair >> 1];
+    int u = (w >> (16 * (pair & 1))) & 0xff;
+    int v = (w >> (16 * (pair & 1) + 8)) & 0xff;
+    int c = (y - 16) * kCy + 32768;
+    int d = u - 128, e = v - 128;
+    px[3 * i + 0] = clip_u8((c + kCbu * d) >> 16);
+    px[3 * i + 1] = clip_u8((c - kCgu * d - kCgv * e) >> 16);
+    px[3 * i + 2] = clip_u8((c + kCrv * e) >> 16);
+  }
+#pragma unroll
+  for (int k = 0; k < 12; ++k)
+    out[k] = pack4(px[4 * k], px[4 * k + 1], px[4 * k + 2], px[4 * k + 3]);
+}
+
+__device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const int tile) {
+  const int tx = tile % d.tiles_x, ty = tile / d.tiles_x;
+  const int t = threadIdx.x;
+  const int r = t >> 3, c = t & 7;
+  const int mbx = tx * kTileMbW + c;
+  const int mby = ty * kTileMbH + (r >> 4);
+  const int row = r & 15;
+  if (mbx >= d.wmbs || mby >= d.hmbs) return;
+  const int pitch = d.wmbs * 16;
+  const int mb = mby * d.wmbs + mbx;
+  const int slot = d.map ? d.map[mb] : -1;
+  uint8_t* yp = d.y + size_t(mby * 16 + row) * pitch + mbx * 16;
+  uint8_t* uvp = d.uv + size_t(mby * 8 + (row >> 1)) * pitch + mbx * 16;
+  uint4 yv, uvv;
+  if (slot >= 0) {
+    const uint8_t* src = d.payload + size_t(slot) * 384;
+    yv = *reinterpret_cast<const uint4*>(src + row * 16);
+    const uint2 cb = *reinterpret_cast<const uint2*>(src + 256 + (row >> 1) * 8);
+    const uint2 cr = *reinterpret_cast<const uint2*>(src + 320 + (row >> 1) * 8);
+    // interleave Cb/Cr bytes: (cb0 cr0 cb1 cr1) ...
+    uvv.x = __builtin_amdgcn_perm(cr.x, cb.x, 0x05010400u);
+    uvv.y = __builtin_amdgcn_perm(cr.x, cb.x, 0x07030602u);
+    uvv.z = __builtin_amdgcn_perm(cr.y, cb.y, 0x05010400u);
+    uvv.w = __builtin_amdgcn_perm(cr.y, cb.y, 0x07030602u);
+    *reinterpret_cast<uint4*>(yp) = yv;
+    if ((row & 1) == 0) *reinterpret_cast<uint4*>(uvp) = uvv;
+  } else {
+    yv = *reinterpret_cast<const uint4*>(yp);
+    uvv = *reinterpret_cast<const uint4*>(uvp);
+  }
+  if (!d.bgr) return;
+  const int oy = mby * 16 + row - d.crop_top;
+  const int ox = mbx * 16 - d.crop_left;
+  if (oy < 0 || oy >= d.out_h || ox + 16 <= 0 || ox >= d.out_w) return;
+  uint32_t o[12];
+  convert16(yv, uvv, o);
+  uint8_t* dst = d.bgr + (size_t(oy) * d.out_w + ox) * 3;
+  if (ox >= 0 && ox + 16 <= d.out_w) {
+    // 48 contiguous bytes; 16-B aligned whenever out_w % 16 == 0 and crop_left % 16 == 0
+    uint4 a = make_uint4(o[0], o[1], o[2], o[3]), bq = make_uint4(o[4], o[5], o[6], o[7]),
+          cq = make_uint4(o[8], o[9], o[10], o[11]);
+    __builtin_memcpy(dst, &a, 16);
+    __builtin_memcpy(dst + 16, &bq, 16);
+    __builtin_memcpy(dst + 32, &cq, 16);
+  } else {  // ragged left/right crop edge
+    for (int i = 0; i < 16; ++i) {
+      int x = ox + i;
+      if (x < 0 || x >= d.out_w) continue;
+      for (int k = 0; k < 3; ++k) {
+        int bi = 3 * i + k;
+        d.bgr[(size_t(oy) * d.out_w + x) * 3 + k] = uint8_t(o[bi >> 2] >> (8 * (bi & 3)));
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void decode_convert_kernel(const DecodeDesc* __restrict__ descs,
+                                                             int n) {
+  // block -> job: binary search over the tile prefix (wave-uniform, scalar loads)
+  const int b = blockIdx.x;
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    int mid = (lo + hi + 1) >> 1;
+    if (descs[mid].tile_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const DecodeDesc d = descs[lo];
+  decode_convert_tile(d, b - d.tile_begin);
+}
+
+__global__ __launch_bounds__(256) void decode_convert_one_kernel(const DecodeDesc d) {
+  decode_convert_tile(d, blockIdx.x);
+}
+
+void launch_decode_convert_one(const DecodeDesc& d, hipStream_t s) {
+  hipLaunchKernelGGL(decode_convert_one_kernel, dim3(tiles_for(d.wmbs, d.hmbs)), dim3(256), 0, s,
+                     d);
+  VEP_HIP(hipGetLastError());
+}
+
+void launch_decode_convert(const DecodeDesc* d_descs, int n, int total_tiles, hipStream_t s) {
+  if (n <= 0 || total_tiles <= 0) return;
+  hipLaunchKernelGGL(decode_convert_kernel, dim3(total_tiles), dim3(256), 0, s, d_descs, n);
+  VEP_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
+// Letterbox: bilinear (align_corners=False, as torch F.interpolate / cv2 INTER_LINEAR) resize of
+// the BT.601-converted picture into an S x S canvas, centred, padded with pad_value.
+
+__device__ __forceinline__ void bgr_at(const uint8_t* __restrict__ y,
+                                       const uint8_t* __restrict__ uv, int pitch, int x, int yy,
+                                       float& b, float& g, float& r) {
+  int Y = y[size_t(yy) * pitch + x];
+  const uint8_t* c = uv + size_t(yy >> 1) * pitch + (x & ~1);
+  uint8_t bb, gg, rr;
+  yuv_to_bgr(Y, c[0], c[1], &bb, &gg, &rr);
+  b = bb;
+  g = gg;
+  r = rr;
+}
+
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+__device__ __forceinline__ void letterbox_quad(const LetterboxDesc& d, const LetterboxParams& p) {
+  const int S = p.size;
+  const int q = blockIdx.x * 256 + threadIdx.x;  // quad index (4 px)
+  const int pix0 = q * 4;
+  if (pix0 >= S * S) return;
+  const int oy = pix0 / S, ox0 = pix0 % S;
+  float vb[4], vg[4], vr[4];
+  bool inside_row = (oy >= d.pad_y && oy < d.pad_y + d.nh);
+  float sy = 0.f, ly = 0.f;
+  int y0 = 0, y1 = 0;
+  if (inside_row) {
+    sy = fmaxf((float(oy - d.pad_y) + 0.5f) * d.ry - 0.5f, 0.f);
+    y0 = int(sy);
+    y1 = y0 + (y0 < d.src_h - 1 ? 1 : 0);
+    ly = sy - float(y0);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int ox = ox0 + i;
+    if (!inside_row || ox < d.pad_x || ox >= d.pad_x + d.nw) {
+      vb[i] = vg[i] = vr[i] = float(p.pad_value);
+      continue;
+    }
+    float sx = fmaxf((float(ox - d.pad_x) + 0.5f) * d.rx - 0.5f, 0.f);
+    int x0 = int(sx);
+    int x1 = x0 + (x0 < d.src_w - 1 ? 1 : 0);
+    float lx = sx - float(x0);
+    float b00, g00, r00, b01, g01, r01, b10, g10, r10, b11, g11, r11;
+    const int X0 = x0 + d.crop_left, X1 = x1 + d.crop_left;
+    const int Y0 = y0 + d.crop_top, Y1 = y1 + d.crop_top;
+    bgr_at(d.y, d.uv, d.pitch, X0, Y0, b00, g00, r00);
+    bgr_at(d.y, d.uv, d.pitch, X1, Y0, b01, g01, r01);
+    bgr_at(d.y, d.uv, d.pitch, X0, Y1, b10, g10, r10);
+    bgr_at(d.y, d.uv, d.pitch, X1, Y1, b11, g11, r11);
+    const float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx),
+                w11 = ly * lx;
+    vb[i] = w00 * b00 + w01 * b01 + w10 * b10 + w11 * b11;
+    vg[i] = w00 * g00 + w01 * g01 + w10 * g10 + w11 * g11;
+    vr[i] = w00 * r00 + w01 * r01 + w10 * r10 + w11 * r11;
+  }
+  if (d.out_hwc) {
+    uint8_t o[12];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      o[3 * i + 0] = uint8_t(fminf(fmaxf(vb[i] + 0.5f, 0.f), 255.f));
+      o[3 * i + 1] = uint8_t(fminf(fmaxf(vg[i] + 0.5f, 0.f), 255.f));
+      o[3 * i + 2] = uint8_t(fminf(fmaxf(vr[i] + 0.5f, 0.f), 255.f));
+    }
+    __builtin_memcpy(d.out_hwc + size_t(pix0) * 3, o, 12);
+  }
+  if (p.chw_dtype != kChwNone && d.out_chw) {
+    const size_t plane = size_t(S) * S;
+    float ch[3][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {  // RGB planes
+      ch[0][i] = (vr[i] * (1.f / 255.f) - p.mean[0]) * p.inv_std[0];
+      ch[1][i] = (vg[i] * (1.f / 255.f) - p.mean[1]) * p.inv_std[1];
+      ch[2][i] = (vb[i] * (1.f / 255.f) - p.mean[2]) * p.inv_std[2];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      if (p.chw_dtype == kChwF32) {
+        float4 v = make_float4(ch[k][0], ch[k][1], ch[k][2], ch[k][3]);
+        *reinterpret_cast<float4*>(static_cast<float*>(d.out_chw) + k * plane + pix0) = v;
+      } else if (p.chw_dtype == kChwF16) {
+        _Float16 h[4] = {(_Float16)ch[k][0], (_Float16)ch[k][1], (_Float16)ch[k][2],
+                         (_Float16)ch[k][3]};
+        __builtin_memcpy(static_cast<_Float16*>(d.out_chw) + k * plane + pix0, h, 8);
+      } else {
+        uint16_t h[4] = {f32_to_bf16(ch[k][0]), f32_to_bf16(ch[k][1]), f32_to_bf16(ch[k][2]),
+                         f32_to_bf16(ch[k][3])};
+        __builtin_memcpy(static_cast<uint16_t*>(d.out_chw) + k * plane + pix0, h, 8);
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void letterbox_kernel(const LetterboxDesc* __restrict__ descs,
+                                                        LetterboxParams p) {
+  const LetterboxDesc d = descs[blockIdx.y];
+  letterbox_quad(d, p);
+}
+
+__global__ __launch_bounds__(256) void letterbox_one_kernel(const LetterboxDesc d,
+                                                            LetterboxParams p) {
+  letterbox_quad(d, p);
+}
+
+void launch_letterbox_one(const LetterboxDesc& d, const LetterboxParams& p, hipStream_t s) {
+  VEP_CHECK(p.size % 4 == 0, "letterbox size must be a multiple of 4");
+  int quads = p.size * p.size / 4;
+  hipLaunchKernelGGL(letterbox_one_kernel, dim3((quads + 255) / 256), dim3(256), 0, s, d, p);
+  VEP_HIP(hipGetLastError());
+}
+
+void fill_letterbox_geometry(LetterboxDesc& d, int size) {
+  float scale = std::min(float(size) / float(d.src_w), float(size) / float(d.src_h));
+  d.nw = std::max(1, std::min(size, int(std::lround(d.src_w * scale))));
+  d.nh = std::max(1, std::min(size, int(std::lround(d.src_h * scale))));
+  d.pad_x = (size - d.nw) / 2;
+  d.pad_y = (size - d.nh) / 2;
+  d.rx = float(d.src_w) / float(d.nw);
+  d.ry = float(d.src_h) / float(d.nh);
+}
+
+void launch_letterbox(const LetterboxDesc* d_descs, int n, const LetterboxParams& p,
+                      hipStream_t s) {
+  if (n <= 0) return;
+  VEP_CHECK(p.size % 4 == 0, "letterbox size must be a multiple of 4");
+  int quads = p.size * p.size / 4;
+  hipLaunchKernelGGL(letterbox_kernel, dim3((quads + 255) / 256, n), dim3(256), 0, s, d_descs,
+                     p);
+  VEP_HIP(hipGetLastError());
+}
+
+}  // namespace vep::gpu

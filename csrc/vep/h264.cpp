@@ -1,0 +1,348 @@
+// H.264 parameter-set / slice-header parsing and writing (ITU-T H.264 §7.3.2.1, §7.3.2.2, §7.3.3).
+#include "h264.h"
+
+namespace vep::h264 {
+
+static void skip_scaling_list(BitReader& br, int size) {
+  int last = 8, next = 8;
+  for (int j = 0; j < size; ++j) {
+    if (next != 0) {
+      int delta = br.se();
+      next = (last + delta + 256) % 256;
+    }
+    last = (next == 0) ? last : next;
+  }
+}
+
+Sps parse_sps(const u8* rbsp, size_t n) {
+  VEP_CHECK(n >= 4 && nal_type(rbsp[0]) == kNalSps, "not an SPS NAL");
+  BitReader br(rbsp + 1, n - 1);
+  Sps s;
+  s.profile_idc = br.u(8);
+  s.constraint_flags = br.u(8);
+  s.level_idc = br.u(8);
+  s.sps_id = br.ue();
+  VEP_CHECK(s.sps_id < 32, "sps_id out of range");
+  switch (s.profile_idc) {
+    case 100: case 110: case 122: case 244: case 44: case 83: case 86: case 118:
+    case 128: case 138: case 139: case 134: case 135: {
+      s.chroma_format_idc = br.ue();
+      if (s.chroma_format_idc == 3) br.u1();  // separate_colour_plane_flag
+      s.bit_depth_luma = 8 + br.ue();
+      s.bit_depth_chroma = 8 + br.ue();
+      br.u1();  // qpprime_y_zero_transform_bypass_flag
+      if (br.u1()) {  // seq_scaling_matrix_present_flag
+        int cnt = (s.chroma_format_idc != 3) ? 8 : 12;
+        for (int i = 0; i < cnt; ++i)
+          if (br.u1()) skip_scaling_list(br, i < 6 ? 16 : 64);
+      }
+      break;
+    }
+    default: break;
+  }
+  s.log2_max_frame_num = br.ue() + 4;
+  s.poc_type = br.ue();
+  if (s.poc_type == 0) {
+    s.log2_max_poc_lsb = br.ue() + 4;
+  } else if (s.poc_type == 1) {
+    s.delta_pic_order_always_zero = br.u1();
+    br.se();
+    br.se();
+    int cyc = br.ue();
+    VEP_CHECK(cyc < 256, "poc cycle too long");
+    for (int i = 0; i < cyc; ++i) br.se();
+  }
+  s.max_num_ref_frames = br.ue();
+  br.u1();  // gaps_in_frame_num_value_allowed_flag
+  s.width_mbs = br.ue() + 1;
+  s.height_map_units = br.ue() + 1;
+  s.frame_mbs_only = br.u1();
+  if (!s.frame_mbs_only) br.u1();  // mb_adaptive_frame_field_flag
+  s.direct_8x8 = br.u1();
+  if (br.u1()) {  // frame_cropping_flag
+    int cx = (s.chroma_format_idc == 0 || s.chroma_format_idc == 3) ? 1 : 2;
+    int cy = ((s.chroma_format_idc == 1) ? 2 : 1) * (s.frame_mbs_only ? 1 : 2);
+    if (s.chroma_format_idc == 0) cy = s.frame_mbs_only ? 1 : 2;
+    s.crop_left = br.ue() * cx;
+    s.crop_right = br.ue() * cx;
+    s.crop_top = br.ue() * cy;
+    s.crop_bottom = br.ue() * cy;
+  }
+  if (br.u1()) {  // vui_parameters_present_flag
+    if (br.u1()) {  // aspect_ratio_info_present_flag
+      if (br.u(8) == 255) br.u(32);
+    }
+    if (br.u1()) br.u1();  // overscan
+    if (br.u1()) {         // video_signal_type_present_flag
+      br.u(4);
+      if (br.u1()) br.u(24);
+    }
+    if (br.u1()) {  // chroma_loc_info_present_flag
+      br.ue();
+      br.ue();
+    }
+    s.timing_info = br.u1();
+    if (s.timing_info) {
+      s.num_units_in_tick = br.u(32);
+      s.time_scale = br.u(32);
+      br.u1();
+    }
+  }
+  VEP_CHECK(s.width_mbs > 0 && s.width_mbs <= 1024 && s.height_mbs() <= 1024, "bad SPS size");
+  return s;
+}
+
+Pps parse_pps(const u8* rbsp, size_t n) {
+  VEP_CHECK(n >= 2 && nal_type(rbsp[0]) == kNalPps, "not a PPS NAL");
+  BitReader br(rbsp + 1, n - 1);
+  Pps p;
+  p.pps_id = br.ue();
+  p.sps_id = br.ue();
+  VEP_CHECK(p.pps_id < 256 && p.sps_id < 32, "pps ids out of range");
+  p.cabac = br.u1();
+  p.bottom_field_pic_order = br.u1();
+  p.num_slice_groups = br.ue() + 1;
+  VEP_CHECK(p.num_slice_groups == 1, "FMO slice groups are not supported");
+  p.num_ref_idx_l0_default = br.ue() + 1;
+  p.num_ref_idx_l1_default = br.ue() + 1;
+  p.weighted_pred = br.u1();
+  p.weighted_bipred_idc = br.u(2);
+  p.pic_init_qp = 26 + br.se();
+  p.pic_init_qs = 26 + br.se();
+  p.chroma_qp_index_offset = br.se();
+  p.deblocking_filter_control = br.u1();
+  p.constrained_intra_pred = br.u1();
+  p.redundant_pic_cnt_present = br.u1();
+  return p;
+}
+
+SliceHeader parse_slice_header(BitReader& br, u8 nal_hdr, const Sps& sps, const Pps& pps) {
+  SliceHeader sh;
+  sh.nal_type = nal_type(nal_hdr);
+  sh.nal_ref_idc = nal_ref_idc(nal_hdr);
+  sh.first_mb = br.ue();
+  sh.slice_type = br.ue();
+  sh.pps_id = br.ue();
+  sh.frame_num = br.u(sps.log2_max_frame_num);
+  if (!sps.frame_mbs_only) {
+    VEP_CHECK(br.u1() == 0, "field pictures are not supported");
+  }
+  if (sh.idr()) sh.idr_pic_id = br.ue();
+  if (sps.poc_type == 0) {
+    sh.poc_lsb = br.u(sps.log2_max_poc_lsb);
+    if (pps.bottom_field_pic_order) br.se();
+  } else if (sps.poc_type == 1 && !sps.delta_pic_order_always_zero) {
+    br.se();
+    if (pps.bottom_field_pic_order) br.se();
+  }
+  if (pps.redundant_pic_cnt_present) br.ue();
+  int st = sh.slice_type % 5;
+  if (st == kB) br.u1();  // direct_spatial_mv_pred_flag
+  sh.num_ref_idx_l0 = pps.num_ref_idx_l0_default;
+  if (st == kP || st == kSP || st == kB) {
+    if (br.u1()) {
+      sh.num_ref_idx_l0 = br.ue() + 1;
+      if (st == kB) br.ue();
+    }
+  }
+  // ref_pic_list_modification()
+  if (st != kI && st != kSI) {
+    if (br.u1()) {
+      for (;;) {
+        u32 idc = br.ue();
+        if (idc == 3) break;
+        VEP_CHECK(idc <= 5, "bad modification_of_pic_nums_idc");
+        br.ue();
+      }
+    }
+  }
+  if (st == kB) {
+    if (br.u1()) {
+      for (;;) {
+        u32 idc = br.ue();
+        if (idc == 3) break;
+        br.ue();
+      }
+    }
+  }
+  VEP_CHECK(!((pps.weighted_pred && (st == kP || st == kSP)) ||
+              (pps.weighted_bipred_idc == 1 && st == kB)),
+            "weighted prediction is not supported");
+  if (sh.nal_ref_idc != 0) {  // dec_ref_pic_marking()
+    if (sh.idr()) {
+      br.u1();
+      br.u1();
+    } else if (br.u1()) {
+      for (;;) {
+        u32 op = br.ue();
+        if (op == 0) break;
+        if (op == 1 || op == 3) br.ue();
+        if (op == 2) br.ue();
+        if (op == 3 || op == 6) br.ue();
+        if (op == 4) br.ue();
+      }
+    }
+  }
+  if (pps.cabac && st != kI && st != kSI) br.ue();
+  sh.slice_qp_delta = br.se();
+  if (st == kSP || st == kSI) {
+    if (st == kSP) br.u1();
+    br.se();
+  }
+  if (pps.deblocking_filter_control) {
+    sh.disable_deblocking = br.ue();
+    if (sh.disable_deblocking != 1) {
+      br.se();
+      br.se();
+    }
+  }
+  sh.data_bitpos = br.bitpos();
+  return sh;
+}
+
+std::vector<u8> write_sps(const Sps& s) {
+  BitWriter bw;
+  bw.u(8, (0 << 7) | (3 << 5) | kNalSps);
+  bw.u(8, s.profile_idc);
+  bw.u(8, s.constraint_flags);
+  bw.u(8, s.level_idc);
+  bw.ue(s.sps_id);
+  bw.ue(s.log2_max_frame_num - 4);
+  bw.ue(s.poc_type);
+  if (s.poc_type == 0) bw.ue(s.log2_max_poc_lsb - 4);
+  bw.ue(s.max_num_ref_frames);
+  bw.u1(0);
+  bw.ue(s.width_mbs - 1);
+  bw.ue(s.height_map_units - 1);
+  bw.u1(1);  // frame_mbs_only
+  bw.u1(1);  // direct_8x8_inference
+  bool crop = s.crop_left || s.crop_right || s.crop_top || s.crop_bottom;
+  bw.u1(crop);
+  if (crop) {
+    bw.ue(s.crop_left / 2);
+    bw.ue(s.crop_right / 2);
+    bw.ue(s.crop_top / 2);
+    bw.ue(s.crop_bottom / 2);
+  }
+  bw.u1(1);  // vui
+  bw.u1(0);  // aspect ratio
+  bw.u1(0);  // overscan
+  bw.u1(1);  // video_signal_type_present: BT.601 limited range (SMPTE 170M)
+  bw.u(3, 5);
+  bw.u1(0);
+  bw.u1(1);
+  bw.u(8, 6);
+  bw.u(8, 6);
+  bw.u(8, 6);
+  bw.u1(0);  // chroma loc
+  bw.u1(s.timing_info);
+  if (s.timing_info) {
+    bw.u(32, s.num_units_in_tick);
+    bw.u(32, s.time_scale);
+    bw.u1(1);
+  }
+  bw.u1(0);  // nal hrd
+  bw.u1(0);  // vcl hrd
+  bw.u1(0);  // pic_struct_present
+  bw.u1(0);  // bitstream_restriction
+  bw.trailing();
+  return bw.buf();
+}
+
+std::vector<u8> write_pps(const Pps& p) {
+  BitWriter bw;
+  bw.u(8, (0 << 7) | (3 << 5) | kNalPps);
+  bw.ue(p.pps_id);
+  bw.ue(p.sps_id);
+  bw.u1(0);  // CAVLC
+  bw.u1(0);
+  bw.ue(0);
+  bw.ue(p.num_ref_idx_l0_default - 1);
+  bw.ue(p.num_ref_idx_l1_default - 1);
+  bw.u1(0);
+  bw.u(2, 0);
+  bw.se(p.pic_init_qp - 26);
+  bw.se(p.pic_init_qs - 26);
+  bw.se(p.chroma_qp_index_offset);
+  bw.u1(p.deblocking_filter_control);
+  bw.u1(0);
+  bw.u1(0);
+  bw.trailing();
+  return bw.buf();
+}
+
+void write_slice_header(BitWriter& bw, const SliceHeader& sh, const Sps& sps, const Pps& pps) {
+  bw.u(8, (0 << 7) | (u32(sh.nal_ref_idc) << 5) | u32(sh.nal_type));
+  bw.ue(sh.first_mb);
+  bw.ue(sh.slice_type);
+  bw.ue(sh.pps_id);
+  bw.u(sps.log2_max_frame_num, sh.frame_num);
+  if (sh.idr()) bw.ue(sh.idr_pic_id);
+  if (sps.poc_type == 0) bw.u(sps.log2_max_poc_lsb, sh.poc_lsb);
+  int st = sh.slice_type % 5;
+  if (st == kP) {
+    bw.u1(0);  // num_ref_idx_active_override_flag
+    bw.u1(0);  // ref_pic_list_modification_flag_l0
+  }
+  if (sh.nal_ref_idc) {
+    if (sh.idr()) {
+      bw.u1(0);
+      bw.u1(0);
+    } else {
+      bw.u1(0);
+    }
+  }
+  bw.se(sh.slice_qp_delta);
+  if (pps.deblocking_filter_control) {
+    bw.ue(sh.disable_deblocking);
+    if (sh.disable_deblocking != 1) {
+      bw.se(0);
+      bw.se(0);
+    }
+  }
+}
+
+std::vector<std::pair<size_t, size_t>> split_annexb(const u8* p, size_t n) {
+  std::vector<std::pair<size_t, size_t>> out;
+  size_t i = 0, start = SIZE_MAX;
+  while (i + 2 < n) {
+    if (p[i] == 0 && p[i + 1] == 0 && p[i + 2] == 1) {
+      if (start != SIZE_MAX) {
+        size_t end = i;
+        while (end > start && p[end - 1] == 0) --end;  // trailing_zero_8bits / 4-byte code
+        out.emplace_back(start, end - start);
+      }
+      i += 3;
+      start = i;
+    } else {
+      ++i;
+    }
+  }
+  if (start != SIZE_MAX && start < n) {
+    size_t end = n;
+    while (end > start && p[end - 1] == 0) --end;  // trailing_zero_8bits
+    if (end > start) out.emplace_back(start, end - start);
+  }
+  return out;
+}
+
+std::vector<u8> avcc_record(const std::vector<u8>& sps, const std::vector<u8>& pps) {
+  VEP_CHECK(sps.size() >= 4 && !pps.empty(), "avcC needs SPS and PPS");
+  std::vector<u8> r;
+  r.push_back(1);
+  r.push_back(sps[1]);
+  r.push_back(sps[2]);
+  r.push_back(sps[3]);
+  r.push_back(0xFF);  // lengthSizeMinusOne = 3
+  r.push_back(0xE1);  // 1 SPS
+  r.push_back(u8(sps.size() >> 8));
+  r.push_back(u8(sps.size()));
+  r.insert(r.end(), sps.begin(), sps.end());
+  r.push_back(1);
+  r.push_back(u8(pps.size() >> 8));
+  r.push_back(u8(pps.size()));
+  r.insert(r.end(), pps.begin(), pps.end());
+  return r;
+}
+
+}  // namespace vep::h264

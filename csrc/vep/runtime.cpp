@@ -1,0 +1,741 @@
+// Data-plane runtime implementation. See runtime.h.
+#include "runtime.h"
+
+#include <algorithm>
+#include <cmath>
+
+#include "color.h"
+
+namespace vep {
+
+// ------------------------------------------------------------------------------------ Device
+
+Device::Device(int id) : id_(id) {
+  if (id_ >= 0) {
+    int n = gpu::device_count();
+    VEP_CHECK(id_ < n, "GPU " + std::to_string(id_) + " not present (" + std::to_string(n) +
+                           " visible)");
+    bind();
+  }
+}
+Device::~Device() = default;
+
+void Device::bind() const {
+  if (id_ >= 0) VEP_HIP(hipSetDevice(id_));
+}
+
+void* Device::alloc(size_t n) {
+  n = std::max<size_t>(n, 256);
+  if (!gpu()) {
+    void* p = std::aligned_alloc(256, (n + 255) & ~size_t(255));
+    VEP_CHECK(p, "host alloc failed");
+    return p;
+  }
+  void* p = nullptr;
+  VEP_HIP(hipMalloc(&p, n));
+  return p;
+}
+void Device::free(void* p) {
+  if (!p) return;
+  if (!gpu()) std::free(p);
+  else (void)hipFree(p);
+}
+void* Device::alloc_pinned(size_t n) {
+  n = std::max<size_t>(n, 256);
+  if (!gpu()) return alloc(n);
+  void* p = nullptr;
+  VEP_HIP(hipHostMalloc(&p, n, hipHostMallocDefault));
+  return p;
+}
+void Device::free_pinned(void* p) {
+  if (!p) return;
+  if (!gpu()) std::free(p);
+  else (void)hipHostFree(p);
+}
+
+// --------------------------------------------------------------------------------- FrameRing
+
+FrameRing::FrameRing(Device& dev, int slots, int width, int height)
+    : dev_(dev), w_(width), h_(height) {
+  VEP_CHECK(slots >= 1 && slots <= 4096, "ring slots out of range");
+  base_ = static_cast<u8*>(dev_.alloc(slot_bytes() * size_t(slots)));
+  for (int i = 0; i < slots; ++i) slots_.emplace_back(std::make_unique<Slot>());
+}
+FrameRing::~FrameRing() { dev_.free(base_); }
+
+int FrameRing::begin_write() {
+  std::lock_guard<std::mutex> g(meta_mu_);
+  int s = next_;
+  next_ = (next_ + 1) % int(slots_.size());
+  if (int(slots_.size()) > 1 && s == latest_.load()) {  // never overwrite the newest frame
+    s = next_;
+    next_ = (next_ + 1) % int(slots_.size());
+  }
+  slots_[s]->version.fetch_add(1, std::memory_order_acq_rel);  // odd: being written
+  return s;
+}
+
+void FrameRing::commit(int slot, FrameMeta meta) {
+  std::lock_guard<std::mutex> g(meta_mu_);
+  meta.seq = published_.load() + 1;
+  slots_[slot]->meta = meta;
+  slots_[slot]->version.fetch_add(1, std::memory_order_acq_rel);  // even: stable
+  latest_.store(slot, std::memory_order_release);
+  published_.store(meta.seq, std::memory_order_release);
+}
+
+bool FrameRing::latest(i64 after, FrameMeta* meta, int* slot) const {
+  std::lock_guard<std::mutex> g(meta_mu_);
+  int s = latest_.load();
+  if (s < 0) return false;
+  const Slot& sl = *slots_[s];
+  if ((sl.version.load() & 1) || sl.meta.seq <= after) return false;
+  *meta = sl.meta;
+  *slot = s;
+  return true;
+}
+
+bool FrameRing::still_valid(int slot, i64 seq) const {
+  std::lock_guard<std::mutex> g(meta_mu_);
+  const Slot& sl = *slots_[slot];
+  return !(sl.version.load() & 1) && sl.meta.seq == seq;
+}
+
+// ----------------------------------------------------------------------------------- LogRing
+
+void LogRing::add(bool err, std::string line) {
+  std::lock_guard<std::mutex> g(mu_);
+  auto& q = err ? err_ : out_;
+  q.push_back(std::move(line));
+  while (q.size() > 1000) q.pop_front();
+}
+
+std::string LogRing::dump(bool err, size_t last) const {
+  std::lock_guard<std::mutex> g(mu_);
+  const auto& q = err ? err_ : out_;
+  std::string s;
+  size_t start = q.size() > last ? q.size() - last : 0;
+  for (size_t i = start; i < q.size(); ++i) {
+    s += q[i];
+    s += '\n';
+  }
+  return s;
+}
+
+// ------------------------------------------------------------------------------------ Camera
+
+Camera::Camera(Worker& w, int index, std::string name, int ring_slots)
+    : ring_slots_cfg(ring_slots), w_(w), index_(index), name_(std::move(name)) {}
+
+std::vector<AuPtr> Camera::gop_snapshot() {
+  std::lock_guard<std::mutex> g(mu_);
+  return gop_;
+}
+
+bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
+  job.cam = index_;
+  job.refresh = refresh;
+  const AccessUnit* last = nullptr;
+  try {
+    for (size_t i = from; i < to; ++i) {
+      job.pic = parser_.parse(*gop_[i], job.upd);
+      last = gop_[i].get();
+    }
+  } catch (const std::exception& e) {
+    errors.fetch_add(1);
+    logs.add(true, std::string("failed to decode packet: ") + e.what());
+    decoded_upto_ = gop_.size();  // give up on this GOP; wait for the next keyframe
+    return false;
+  }
+  FrameMeta& m = job.meta;
+  m.width = job.pic.width;
+  m.height = job.pic.height;
+  m.pts = last->pts;
+  m.dts = last->dts;
+  m.timestamp = last->pts;  // int(frame.time * time_base.denominator) with tb = 1/90000
+  m.packet = i64(to - 1);
+  m.keyframe = keyframes_;
+  m.is_keyframe = last->keyframe;
+  m.is_corrupt = last->corrupt;
+  m.frame_type = job.pic.pict_type;
+  m.arrival_ms = last->arrival_ms;
+  decoded_upto_ = to;
+  return true;
+}
+
+bool Camera::on_access_unit(const AuPtr& au) {
+  DecodeJob job;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    packets.fetch_add(1, std::memory_order_relaxed);
+    bytes_in.fetch_add(au->bytes(), std::memory_order_relaxed);
+    last_packet_ms.store(au->arrival_ms ? au->arrival_ms : now_ms());
+    if (au->keyframe) {
+      gop_.clear();
+      decoded_upto_ = 0;
+      ++keyframes_;
+    }
+    if (gop_.empty() && !au->keyframe) {  // rtsp_to_rtmp.py:111-114 "skipping, since not a keyframe"
+      skipped.fetch_add(1, std::memory_order_relaxed);
+      if (parser_.has_sps() == false) parser_.absorb_parameter_sets(*au);
+      return false;
+    }
+    gop_.push_back(au);
+    const i64 lq = last_query_ms.load();
+    if (lq == 0) return false;                            // no last_query yet
+    if (now_ms() - lq >= idle_cutoff_ms.load()) return false;  // idle > 10 s: stop decoding
+    size_t to = gop_.size();
+    if (keyframe_only.load()) {
+      if (decoded_upto_ > 0) return false;  // keyframe already reconstructed
+      to = 1;
+    }
+    if (decoded_upto_ >= to) return false;
+    const size_t from = decoded_upto_;
+    if (!build_job(job, from, to, from == 0 && gop_[0]->keyframe)) return false;
+  }
+  w_.submit(std::move(job));
+  return true;
+}
+
+void Camera::decode_now(const AuPtr& au) {
+  DecodeJob job;
+  if (make_job(au, job)) w_.submit(std::move(job));
+}
+
+bool Camera::make_job(const AuPtr& au, DecodeJob& job) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    packets.fetch_add(1, std::memory_order_relaxed);
+    bytes_in.fetch_add(au->bytes(), std::memory_order_relaxed);
+    if (au->keyframe) {
+      gop_.clear();
+      decoded_upto_ = 0;
+      ++keyframes_;
+    }
+    if (gop_.empty() && !au->keyframe) return false;
+    gop_.push_back(au);
+    size_t from = decoded_upto_, to = gop_.size();
+    return build_job(job, from, to, from == 0);
+  }
+}
+
+// ------------------------------------------------------------------------------------ Worker
+
+Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
+  if (dev_.gpu()) {
+    dev_.bind();
+    VEP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    VEP_HIP(hipStreamCreateWithFlags(&serve_stream_, hipStreamNonBlocking));
+    VEP_HIP(hipEventCreate(&ev0_));
+    VEP_HIP(hipEventCreate(&ev1_));
+  }
+  cams_.reserve(size_t(opt_.max_cameras));
+  if (opt_.letterbox_size > 0) {
+    const size_t S = size_t(opt_.letterbox_size);
+    cons_hwc_ = static_cast<u8*>(dev_.alloc(size_t(opt_.max_cameras) * S * S * 3));
+    size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
+    if (opt_.chw_dtype != gpu::kChwNone)
+      cons_chw_ = dev_.alloc(size_t(opt_.max_cameras) * 3 * S * S * es);
+    cons_rows_ = opt_.max_cameras;
+  }
+}
+
+void Worker::set_consumer_buffers(u8* hwc, void* chw, int rows) {
+  std::lock_guard<std::mutex> lg(launch_mu_);
+  VEP_CHECK(opt_.letterbox_size > 0, "worker was built without a letterbox consumer batch");
+  if (owns_cons_) {
+    dev_.free(cons_hwc_);
+    dev_.free(cons_chw_);
+  }
+  owns_cons_ = false;
+  cons_hwc_ = hwc;
+  cons_chw_ = chw;
+  cons_rows_ = rows;
+}
+
+Worker::~Worker() {
+  stop();
+  std::lock_guard<std::mutex> g(cams_mu_);
+  for (auto& c : cams_) {
+    if (!c) continue;
+    dev_.free(c->surface.y);
+    dev_.free(c->surface.uv);
+    c->ring_.reset();
+  }
+  if (owns_cons_) {
+    dev_.free(cons_hwc_);
+    dev_.free(cons_chw_);
+  }
+  dev_.free(d_stage_);
+  dev_.free_pinned(h_stage_);
+  dev_.free_pinned(h_serve_);
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (serve_stream_) (void)hipStreamDestroy(serve_stream_);
+  if (ev0_) (void)hipEventDestroy(ev0_);
+  if (ev1_) (void)hipEventDestroy(ev1_);
+}
+
+int Worker::add_camera(const std::string& name, int ring_slots) {
+  std::lock_guard<std::mutex> g(cams_mu_);
+  for (auto& c : cams_)
+    VEP_CHECK(!c || c->name() != name, "camera already registered: " + name);
+  int idx = -1;
+  for (size_t i = 0; i < cams_.size(); ++i)
+    if (!cams_[i]) { idx = int(i); break; }
+  if (idx < 0) {
+    VEP_CHECK(int(cams_.size()) < opt_.max_cameras, "worker camera capacity exhausted");
+    idx = int(cams_.size());
+    cams_.emplace_back();
+  }
+  cams_[size_t(idx)] = std::make_unique<Camera>(*this, idx, name, std::max(1, ring_slots));
+  return idx;
+}
+
+void Worker::remove_camera(int idx) {
+  flush();
+  std::lock_guard<std::mutex> lg(launch_mu_);
+  std::lock_guard<std::mutex> g(cams_mu_);
+  VEP_CHECK(idx >= 0 && idx < int(cams_.size()) && cams_[size_t(idx)], "no such camera");
+  auto& c = cams_[size_t(idx)];
+  dev_.free(c->surface.y);
+  dev_.free(c->surface.uv);
+  c.reset();
+}
+
+Camera* Worker::camera(int idx) {
+  std::lock_guard<std::mutex> g(cams_mu_);
+  if (idx < 0 || idx >= int(cams_.size())) return nullptr;
+  return cams_[size_t(idx)].get();
+}
+
+Camera* Worker::find(const std::string& name) {
+  std::lock_guard<std::mutex> g(cams_mu_);
+  for (auto& c : cams_)
+    if (c && c->name() == name) return c.get();
+  return nullptr;
+}
+
+int Worker::num_cameras() const {
+  std::lock_guard<std::mutex> g(cams_mu_);
+  int n = 0;
+  for (auto& c : cams_) n += c ? 1 : 0;
+  return n;
+}
+
+void Worker::start() {
+  std::lock_guard<std::mutex> g(q_mu_);
+  if (running_) return;
+  running_ = true;
+  stop_ = false;
+  th_ = std::thread([this] { loop(); });
+}
+
+void Worker::stop() {
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    if (!running_) return;
+    stop_ = true;
+  }
+  q_cv_.notify_all();
+  if (th_.joinable()) th_.join();
+  std::lock_guard<std::mutex> g(q_mu_);
+  running_ = false;
+}
+
+static void fold_update(MbUpdate& into, const MbUpdate& from) {
+  VEP_CHECK(into.width_mbs == from.width_mbs && into.height_mbs == from.height_mbs,
+            "fold size mismatch");
+  for (int mb = 0; mb < from.mbs(); ++mb) {
+    int s = from.slot[size_t(mb)];
+    if (s < 0) continue;
+    std::memcpy(into.slot_for(mb), from.payload.data() + size_t(s) * kPcmMbBytes, kPcmMbBytes);
+  }
+  into.frames += from.frames;
+}
+
+void Worker::submit(DecodeJob&& job) {
+  {
+    std::lock_guard<std::mutex> g(q_mu_);
+    for (auto& p : pending_) {
+      if (p.cam != job.cam) continue;
+      // collapse into the not-yet-launched job: latest writer wins per macroblock
+      if (job.refresh || p.upd.width_mbs != job.upd.width_mbs ||
+          p.upd.height_mbs != job.upd.height_mbs) {
+        p = std::move(job);
+      } else {
+        fold_update(p.upd, job.upd);
+        p.pic = job.pic;
+        p.meta = job.meta;
+      }
+      q_cv_.notify_one();
+      return;
+    }
+    pending_.push_back(std::move(job));
+  }
+  q_cv_.notify_one();
+}
+
+void Worker::flush() {
+  std::unique_lock<std::mutex> g(q_mu_);
+  if (!running_) return;
+  idle_cv_.wait(g, [this] { return pending_.empty() && !busy_; });
+}
+
+void Worker::loop() {
+  dev_.bind();
+  std::vector<DecodeJob> batch;
+  for (;;) {
+    {
+      std::unique_lock<std::mutex> g(q_mu_);
+      q_cv_.wait(g, [this] { return stop_ || !pending_.empty(); });
+      if (stop_ && pending_.empty()) break;
+      batch.swap(pending_);
+      busy_ = true;
+    }
+    try {
+      run_batch(batch);
+    } catch (const std::exception& e) {
+      for (auto& j : batch)
+        if (Camera* c = camera(j.cam)) {
+          c->errors.fetch_add(1);
+          c->logs.add(true, std::string("decode batch failed: ") + e.what());
+        }
+    }
+    batch.clear();
+    {
+      std::lock_guard<std::mutex> g(q_mu_);
+      busy_ = false;
+    }
+    idle_cv_.notify_all();
+  }
+}
+
+void Worker::ensure_surface(Camera& c, const PictureInfo& pi) {
+  const int wmbs = pi.coded_width / 16, hmbs = pi.coded_height / 16;
+  auto& s = c.surface;
+  if (s.wmbs == wmbs && s.hmbs == hmbs && c.ring_ && c.ring_->width() == pi.width &&
+      c.ring_->height() == pi.height)
+    return;
+  dev_.free(s.y);
+  dev_.free(s.uv);
+  s.y = s.uv = nullptr;
+  s.wmbs = wmbs;
+  s.hmbs = hmbs;
+  const size_t ysz = size_t(wmbs) * 16 * hmbs * 16;
+  if (dev_.gpu()) {
+    s.y = static_cast<u8*>(dev_.alloc(ysz));
+    s.uv = static_cast<u8*>(dev_.alloc(ysz / 2));
+    VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
+    VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
+  } else {
+    s.host.alloc(wmbs * 16, hmbs * 16);
+  }
+  c.ring_ = std::make_unique<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height);
+}
+
+static inline size_t al(size_t x, size_t a = 256) { return (x + a - 1) & ~(a - 1); }
+
+static void cpu_letterbox(const HostSurface& s, const gpu::LetterboxDesc& d,
+                          const gpu::LetterboxParams& p) {
+  const int S = p.size;
+  for (int oy = 0; oy < S; ++oy) {
+    for (int ox = 0; ox < S; ++ox) {
+      float v[3];
+      bool in = oy >= d.pad_y && oy < d.pad_y + d.nh && ox >= d.pad_x && ox < d.pad_x + d.nw;
+      if (!in) {
+        v[0] = v[1] = v[2] = float(p.pad_value);
+      } else {
+        float sy = std::max((float(oy - d.pad_y) + 0.5f) * d.ry - 0.5f, 0.f);
+        float sx = std::max((float(ox - d.pad_x) + 0.5f) * d.rx - 0.5f, 0.f);
+        int y0 = int(sy), x0 = int(sx);
+        int y1 = y0 + (y0 < d.src_h - 1 ? 1 : 0), x1 = x0 + (x0 < d.src_w - 1 ? 1 : 0);
+        float ly = sy - float(y0), lx = sx - float(x0);
+        auto px = [&](int x, int y, float* o) {
+          x += d.crop_left;
+          y += d.crop_top;
+          const u8* c = &s.uv[size_t(y >> 1) * s.coded_w + (x & ~1)];
+          u8 b, g, r;
+          yuv_to_bgr(s.y[size_t(y) * s.coded_w + x], c[0], c[1], &b, &g, &r);
+          o[0] = b;
+          o[1] = g;
+          o[2] = r;
+        };
+        float a[3], b[3], c[3], e[3];
+        px(x0, y0, a);
+        px(x1, y0, b);
+        px(x0, y1, c);
+        px(x1, y1, e);
+        float w00 = (1.f - ly) * (1.f - lx), w01 = (1.f - ly) * lx, w10 = ly * (1.f - lx),
+              w11 = ly * lx;
+        for (int k = 0; k < 3; ++k) v[k] = w00 * a[k] + w01 * b[k] + w10 * c[k] + w11 * e[k];
+      }
+      size_t pix = size_t(oy) * S + ox;
+      if (d.out_hwc)
+        for (int k = 0; k < 3; ++k)
+          d.out_hwc[pix * 3 + k] = u8(std::min(std::max(v[k] + 0.5f, 0.f), 255.f));
+      if (d.out_chw && p.chw_dtype == gpu::kChwF32) {
+        float* o = static_cast<float*>(d.out_chw);
+        const size_t plane = size_t(S) * S;
+        for (int k = 0; k < 3; ++k)  // RGB planes from BGR values
+          o[k * plane + pix] = (v[2 - k] * (1.f / 255.f) - p.mean[k]) * p.inv_std[k];
+      }
+    }
+  }
+}
+
+void Worker::launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
+  const int n = int(jobs.size());
+  // staging layout: [descs][letterbox descs][maps][payloads]
+  size_t off_desc = 0;
+  size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
+  size_t off_map = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
+  size_t need = off_map;
+  std::vector<size_t> map_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
+  for (int i = 0; i < n; ++i) {
+    map_off[size_t(i)] = need;
+    need += al(sizeof(i32) * jobs[size_t(i)].upd.slot.size(), 16);
+  }
+  need = al(need);
+  for (int i = 0; i < n; ++i) {
+    pay_off[size_t(i)] = need;
+    need += size_t(jobs[size_t(i)].upd.nslots) * kPcmMbBytes;
+  }
+  need = al(need);
+  if (need > stage_cap_) {
+    dev_.free(d_stage_);
+    dev_.free_pinned(h_stage_);
+    stage_cap_ = std::max(need + need / 2, size_t(1) << 20);
+    h_stage_ = static_cast<u8*>(dev_.alloc_pinned(stage_cap_));
+    d_stage_ = static_cast<u8*>(dev_.alloc(stage_cap_));
+  }
+  auto* hd = reinterpret_cast<gpu::DecodeDesc*>(h_stage_ + off_desc);
+  auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(h_stage_ + off_lb);
+  int tiles = 0;
+  for (int i = 0; i < n; ++i) {
+    DecodeJob& j = jobs[size_t(i)];
+    Camera* c = cams_[size_t(j.cam)].get();
+    std::memcpy(h_stage_ + map_off[size_t(i)], j.upd.slot.data(), sizeof(i32) * j.upd.slot.size());
+    std::memcpy(h_stage_ + pay_off[size_t(i)], j.upd.payload.data(),
+                size_t(j.upd.nslots) * kPcmMbBytes);
+    gpu::DecodeDesc& d = hd[i];
+    d.y = c->surface.y;
+    d.uv = c->surface.uv;
+    d.bgr = c->ring_->slot_ptr(slots[size_t(i)]);
+    d.map = reinterpret_cast<const i32*>(d_stage_ + map_off[size_t(i)]);
+    d.payload = d_stage_ + pay_off[size_t(i)];
+    d.wmbs = j.upd.width_mbs;
+    d.hmbs = j.upd.height_mbs;
+    d.out_w = j.pic.width;
+    d.out_h = j.pic.height;
+    d.crop_left = j.pic.crop_left;
+    d.crop_top = j.pic.crop_top;
+    d.tiles_x = (d.wmbs + gpu::kTileMbW - 1) / gpu::kTileMbW;
+    d.tile_begin = tiles;
+    tiles += gpu::tiles_for(d.wmbs, d.hmbs);
+    if (opt_.letterbox_size > 0) {
+      gpu::LetterboxDesc& l = hl[i];
+      const size_t S = size_t(opt_.letterbox_size);
+      l.y = c->surface.y;
+      l.uv = c->surface.uv;
+      l.pitch = d.wmbs * 16;
+      l.src_w = j.pic.width;
+      l.src_h = j.pic.height;
+      l.crop_left = j.pic.crop_left;
+      l.crop_top = j.pic.crop_top;
+      VEP_CHECK(j.cam < cons_rows_, "camera index exceeds consumer batch rows");
+      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(j.cam) * S * S * 3 : nullptr;
+      size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
+      l.out_chw = cons_chw_ ? static_cast<u8*>(cons_chw_) + size_t(j.cam) * 3 * S * S * es
+                            : nullptr;
+      gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
+    }
+  }
+  VEP_HIP(hipMemcpyAsync(d_stage_, h_stage_, need, hipMemcpyHostToDevice, stream_));
+  VEP_HIP(hipEventRecord(ev0_, stream_));
+  gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(d_stage_ + off_desc), n,
+                             tiles, stream_);
+  if (opt_.letterbox_size > 0) {
+    gpu::LetterboxParams p{};
+    p.size = opt_.letterbox_size;
+    p.chw_dtype = opt_.chw_dtype;
+    for (int k = 0; k < 3; ++k) {
+      p.mean[k] = opt_.mean[k];
+      p.inv_std[k] = 1.f / opt_.std[k];
+    }
+    p.pad_value = 114;
+    gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(d_stage_ + off_lb), n, p,
+                          stream_);
+  }
+  VEP_HIP(hipEventRecord(ev1_, stream_));
+  VEP_HIP(hipEventSynchronize(ev1_));
+  float ms = 0;
+  VEP_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
+  gpu_ms_total_ += ms;
+}
+
+void Worker::run_batch(std::vector<DecodeJob>& jobs) {
+  if (jobs.empty()) return;
+  std::lock_guard<std::mutex> lg(launch_mu_);
+  dev_.bind();
+  std::vector<int> slots(jobs.size());
+  {
+    std::lock_guard<std::mutex> g(cams_mu_);
+    // drop jobs whose camera vanished
+    jobs.erase(std::remove_if(jobs.begin(), jobs.end(),
+                              [&](const DecodeJob& j) {
+                                return j.cam < 0 || j.cam >= int(cams_.size()) ||
+                                       !cams_[size_t(j.cam)];
+                              }),
+               jobs.end());
+    for (size_t i = 0; i < jobs.size(); ++i) {
+      Camera& c = *cams_[size_t(jobs[i].cam)];
+      ensure_surface(c, jobs[i].pic);
+      slots[i] = c.ring_->begin_write();
+    }
+  }
+  slots.resize(jobs.size());
+  if (jobs.empty()) return;
+  if (dev_.gpu()) {
+    launch(jobs, slots);
+  } else {
+    for (size_t i = 0; i < jobs.size(); ++i) {
+      Camera& c = *cams_[size_t(jobs[i].cam)];
+      cpu_apply_update(jobs[i].upd, c.surface.host);
+      cpu_nv12_to_bgr(c.surface.host, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
+                      jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
+      if (opt_.letterbox_size > 0) {
+        gpu::LetterboxDesc l{};
+        const size_t S = size_t(opt_.letterbox_size);
+        l.src_w = jobs[i].pic.width;
+        l.src_h = jobs[i].pic.height;
+        l.crop_left = jobs[i].pic.crop_left;
+        l.crop_top = jobs[i].pic.crop_top;
+        l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(jobs[i].cam) * S * S * 3 : nullptr;
+        l.out_chw = (cons_chw_ && opt_.chw_dtype == gpu::kChwF32)
+                        ? static_cast<u8*>(cons_chw_) + size_t(jobs[i].cam) * 3 * S * S * 4
+                        : nullptr;
+        gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
+        gpu::LetterboxParams p{};
+        p.size = opt_.letterbox_size;
+        p.chw_dtype = opt_.chw_dtype;
+        for (int k = 0; k < 3; ++k) {
+          p.mean[k] = opt_.mean[k];
+          p.inv_std[k] = 1.f / opt_.std[k];
+        }
+        p.pad_value = 114;
+        cpu_letterbox(c.surface.host, l, p);
+      }
+    }
+  }
+  const i64 t = mono_us();
+  std::lock_guard<std::mutex> g(cams_mu_);
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    Camera& c = *cams_[size_t(jobs[i].cam)];
+    jobs[i].meta.decoded_us = t;
+    c.ring_->commit(slots[i], jobs[i].meta);
+    c.decoded.fetch_add(1, std::memory_order_relaxed);
+  }
+  frames_.fetch_add(jobs.size());
+  batches_.fetch_add(1);
+}
+
+bool Worker::read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap) {
+  Camera* c = camera(cam);
+  if (!c || !c->ring_) return false;
+  FrameRing* ring = c->ring_.get();
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    int slot;
+    if (!ring->latest(after, meta, &slot)) return false;
+    const size_t n = ring->slot_bytes();
+    VEP_CHECK(cap >= n, "read_latest destination too small");
+    if (dev_.gpu()) {
+      std::lock_guard<std::mutex> g(serve_mu_);
+      if (n > serve_cap_) {
+        dev_.free_pinned(h_serve_);
+        serve_cap_ = n;
+        h_serve_ = static_cast<u8*>(dev_.alloc_pinned(n));
+      }
+      dev_.bind();
+      VEP_HIP(hipMemcpyAsync(h_serve_, ring->slot_ptr(slot), n, hipMemcpyDeviceToHost,
+                             serve_stream_));
+      VEP_HIP(hipStreamSynchronize(serve_stream_));
+      if (!ring->still_valid(slot, meta->seq)) continue;
+      std::memcpy(dst, h_serve_, n);
+      return true;
+    }
+    std::memcpy(dst, ring->slot_ptr(slot), n);
+    if (ring->still_valid(slot, meta->seq)) return true;
+  }
+  return false;
+}
+
+// --------------------------------------------------------------------------- proto encoding
+
+static void put_varint(std::string& s, u64 v) {
+  while (v >= 0x80) {
+    s.push_back(char((v & 0x7f) | 0x80));
+    v >>= 7;
+  }
+  s.push_back(char(v));
+}
+static void put_tag(std::string& s, int field, int wt) { put_varint(s, u64(field) << 3 | u64(wt)); }
+static void put_i64(std::string& s, int field, i64 v) {
+  if (v == 0) return;
+  put_tag(s, field, 0);
+  put_varint(s, u64(v));
+}
+static void put_bool(std::string& s, int field, bool v) {
+  if (!v) return;
+  put_tag(s, field, 0);
+  s.push_back(1);
+}
+static void put_str(std::string& s, int field, const std::string& v) {
+  if (v.empty()) return;
+  put_tag(s, field, 2);
+  put_varint(s, v.size());
+  s += v;
+}
+
+std::pair<std::string, std::string> encode_video_frame(const FrameMeta& m, size_t data_len,
+                                                       const std::string& device_id) {
+  std::string pre, suf;
+  put_i64(pre, 1, m.width);
+  put_i64(pre, 2, m.height);
+  if (data_len) {
+    put_tag(pre, 3, 2);
+    put_varint(pre, data_len);
+  }
+  put_i64(suf, 4, m.timestamp);
+  put_bool(suf, 5, m.is_keyframe);
+  put_i64(suf, 6, m.pts);
+  put_i64(suf, 7, m.dts);
+  if (m.frame_type != '?' && m.frame_type != 0) put_str(suf, 8, std::string(1, m.frame_type));
+  put_bool(suf, 9, m.is_corrupt);
+  if (m.time_base != 0.0) {
+    put_tag(suf, 10, 1);
+    u64 bits;
+    std::memcpy(&bits, &m.time_base, 8);
+    for (int i = 0; i < 8; ++i) suf.push_back(char((bits >> (8 * i)) & 0xff));
+  }
+  if (m.width > 0) {  // ShapeProto{dim: [(H,"0"), (W,"1"), (3,"2")]}
+    std::string shape;
+    const i64 dims[3] = {m.height, m.width, 3};
+    for (int k = 0; k < 3; ++k) {
+      std::string dim;
+      put_i64(dim, 1, dims[k]);
+      put_str(dim, 2, std::string(1, char('0' + k)));
+      put_tag(shape, 2, 2);
+      put_varint(shape, dim.size());
+      shape += dim;
+    }
+    put_tag(suf, 11, 2);
+    put_varint(suf, shape.size());
+    suf += shape;
+  }
+  put_str(suf, 12, device_id);
+  put_i64(suf, 13, m.packet);
+  put_i64(suf, 14, m.keyframe);
+  return {pre, suf};
+}
+
+}  // namespace vep

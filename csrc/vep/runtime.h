@@ -1,0 +1,248 @@
+// Data-plane runtime: per-camera HBM frame rings, lazy-decode camera state and the per-GPU
+// worker that batches every camera's decode into one HIP launch.
+//
+// Reference parity:
+//  * FrameRing replaces the Redis stream `XADD <device> MAXLEN n` / `XREAD` frame cache
+//    (python/read_image.py:121, server/grpcapi/grpc_api.go:186-231).
+//  * Camera's control atomics replace the Redis keys `last_access_time_<dev>`
+//    {last_query, proxy_rtmp} and `is_key_frame_only_<dev>`.
+//  * Camera::on_access_unit implements the lazy decode / keyframe-only / GOP catch-up rules of
+//    rtsp_to_rtmp.py:94-160 and read_image.py:57-128.
+#pragma once
+
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
+#include <mutex>
+#include <thread>
+
+#include "codec.h"
+#include "gpu.h"
+
+namespace vep {
+
+// VideoFrame metadata (proto/video_streaming.proto VideoFrame; read_image.py:99-117).
+struct FrameMeta {
+  i64 width = 0, height = 0;
+  i64 timestamp = 0, pts = 0, dts = 0;
+  i64 packet = 0, keyframe = 0;  // index in GOP, GOP counter
+  bool is_keyframe = false, is_corrupt = false;
+  char frame_type = '?';
+  double time_base = 1.0 / 90000.0;
+  i64 seq = 0;            // ring publish counter (per-client cursor, XREAD lastId analog)
+  i64 decoded_us = 0;     // monotonic time the frame became readable
+  i64 arrival_ms = 0;     // packet arrival wall clock
+};
+
+// Device (or host) memory owner. id < 0 selects the CPU backend.
+class Device {
+ public:
+  explicit Device(int id);
+  ~Device();
+  bool gpu() const { return id_ >= 0; }
+  int id() const { return id_; }
+  void* alloc(size_t n);
+  void free(void* p);
+  void* alloc_pinned(size_t n);
+  void free_pinned(void* p);
+  void bind() const;  // hipSetDevice on the calling thread
+
+ private:
+  int id_;
+};
+
+// Ring of N decoded BGR24 frames for one camera, seqlock-published.
+class FrameRing {
+ public:
+  FrameRing(Device& dev, int slots, int width, int height);
+  ~FrameRing();
+  int slots() const { return int(slots_.size()); }
+  int width() const { return w_; }
+  int height() const { return h_; }
+  size_t slot_bytes() const { return size_t(w_) * h_ * 3; }
+  u8* slot_ptr(int i) const { return base_ + size_t(i) * slot_bytes(); }
+  // writer side (single writer: the worker thread)
+  int begin_write();
+  void commit(int slot, FrameMeta meta);
+  // reader side: newest committed frame with seq > after (false if none)
+  bool latest(i64 after, FrameMeta* meta, int* slot) const;
+  // true if `slot` still holds the frame with publish counter `seq`
+  bool still_valid(int slot, i64 seq) const;
+  i64 published() const { return published_.load(std::memory_order_acquire); }
+
+ private:
+  struct Slot {
+    std::atomic<u64> version{0};  // odd while being written
+    FrameMeta meta;
+  };
+  Device& dev_;
+  int w_, h_;
+  u8* base_ = nullptr;
+  std::vector<std::unique_ptr<Slot>> slots_;
+  mutable std::mutex meta_mu_;
+  std::atomic<int> latest_{-1};
+  std::atomic<i64> published_{0};
+  int next_ = 0;
+};
+
+struct DecodeJob {
+  int cam = -1;
+  MbUpdate upd;
+  PictureInfo pic;
+  FrameMeta meta;
+  bool refresh = false;  // IDR: every MB is covered
+};
+
+class Worker;
+
+// Bounded log ring (docker json-file analog, rtsp_process_manager.go:72-75; Info returns 100).
+class LogRing {
+ public:
+  void add(bool err, std::string line);
+  std::string dump(bool err, size_t last = 100) const;
+
+ private:
+  mutable std::mutex mu_;
+  std::deque<std::string> out_, err_;
+};
+
+// Camera data-plane state (one per registered RTSP process).
+class Camera {
+ public:
+  Camera(Worker& w, int index, std::string name, int ring_slots);
+  const std::string& name() const { return name_; }
+  int index() const { return index_; }
+
+  // --- control (atomics; replaces Redis control keys) ---
+  std::atomic<i64> last_query_ms{0};   // 0 = never queried ("no last_query" in the hash)
+  std::atomic<bool> keyframe_only{false};
+  std::atomic<bool> proxy_rtmp{false};
+  std::atomic<i64> idle_cutoff_ms{10000};  // rtsp_to_rtmp.py:144-145
+
+  // --- ingest entry point (called from the camera's network thread) ---
+  // Returns true if the AU triggered a decode submission.
+  bool on_access_unit(const AuPtr& au);
+  // Force-decode (used by bench/tests): parse au and submit regardless of query state.
+  void decode_now(const AuPtr& au);
+  // Same as decode_now but hands the job back (bench driver batches jobs itself).
+  bool make_job(const AuPtr& au, DecodeJob& job);
+
+  // --- stats ---
+  std::atomic<u64> packets{0}, decoded{0}, skipped{0}, errors{0}, bytes_in{0};
+  std::atomic<i64> last_packet_ms{0};
+  LogRing logs;
+
+  FrameRing* ring() const { return ring_.get(); }
+  H264Parser& parser() { return parser_; }
+  std::mutex& gop_mutex() { return mu_; }
+  std::vector<AuPtr> gop_snapshot();   // current GOP packets (for RTMP flush / archive)
+
+  // worker-owned GPU state
+  struct Surface {
+    int wmbs = 0, hmbs = 0;
+    u8* y = nullptr;
+    u8* uv = nullptr;
+    HostSurface host;  // CPU backend
+  } surface;
+  std::unique_ptr<FrameRing> ring_;
+  int ring_slots_cfg;
+
+ private:
+  friend class Worker;
+  bool build_job(DecodeJob& job, size_t from, size_t to, bool refresh);
+  Worker& w_;
+  int index_;
+  std::string name_;
+  std::mutex mu_;
+  std::vector<AuPtr> gop_;
+  size_t decoded_upto_ = 0;  // gop_[0, decoded_upto_) are reconstructed on the surface
+  i64 keyframes_ = 0;
+  H264Parser parser_;
+};
+
+struct WorkerOptions {
+  int device = 0;             // -1 = CPU backend
+  int letterbox_size = 0;     // 0 = no consumer batch
+  int chw_dtype = 0;          // gpu::ChwDtype for the normalised CHW consumer tensor
+  float mean[3] = {0.f, 0.f, 0.f};
+  float std[3] = {1.f, 1.f, 1.f};
+  int max_cameras = 256;
+};
+
+class Worker {
+ public:
+  explicit Worker(const WorkerOptions& o);
+  ~Worker();
+  Device& device() { return dev_; }
+  const WorkerOptions& options() const { return opt_; }
+
+  int add_camera(const std::string& name, int ring_slots);
+  void remove_camera(int idx);
+  Camera* camera(int idx);
+  Camera* find(const std::string& name);
+  int num_cameras() const;
+
+  // Live mode: a background thread drains submitted jobs in batches.
+  void start();
+  void stop();
+  void submit(DecodeJob&& job);  // merges with a not-yet-launched job of the same camera
+
+  // Synchronous batched decode (bench / tests). Jobs are consumed.
+  void run_batch(std::vector<DecodeJob>& jobs);
+  // Wait until every submitted job is published.
+  void flush();
+
+  // Serving: copy the newest frame with seq > after into dst (host). Returns false if none.
+  bool read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap);
+
+  // Consumer batch (letterbox): device pointers of [max_cameras, S, S, 3] u8 and CHW tensor.
+  // Point the consumer batch at caller-owned device buffers (e.g. torch tensors that feed an
+  // RCCL all-gather); row r belongs to camera index r. Takes effect from the next batch.
+  void set_consumer_buffers(u8* hwc, void* chw, int rows);
+  u8* consumer_hwc() const { return cons_hwc_; }
+  void* consumer_chw() const { return cons_chw_; }
+  hipStream_t compute_stream() const { return stream_; }
+  u64 batches() const { return batches_.load(); }
+  u64 frames() const { return frames_.load(); }
+  double gpu_ms_total() const { return gpu_ms_total_; }
+
+ private:
+  void loop();
+  void ensure_surface(Camera& c, const PictureInfo& pi);
+  void launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
+  WorkerOptions opt_;
+  Device dev_;
+  hipStream_t stream_ = nullptr, serve_stream_ = nullptr;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  mutable std::mutex cams_mu_;
+  std::vector<std::unique_ptr<Camera>> cams_;
+  // staging
+  u8* h_stage_ = nullptr;
+  u8* d_stage_ = nullptr;
+  size_t stage_cap_ = 0;
+  u8* h_serve_ = nullptr;
+  size_t serve_cap_ = 0;
+  std::mutex serve_mu_;
+  u8* cons_hwc_ = nullptr;
+  void* cons_chw_ = nullptr;
+  bool owns_cons_ = true;
+  int cons_rows_ = 0;
+  // live queue
+  std::mutex q_mu_;
+  std::condition_variable q_cv_, idle_cv_;
+  std::vector<DecodeJob> pending_;
+  bool running_ = false, stop_ = false, busy_ = false;
+  std::thread th_;
+  std::mutex launch_mu_;
+  std::atomic<u64> batches_{0}, frames_{0};
+  double gpu_ms_total_ = 0;
+};
+
+// Protobuf wire encoding of chrys.cloud.videostreaming.v1beta1.VideoFrame
+// (field numbers from proto/video_streaming.proto). `data` bytes are supplied separately so
+// the payload can be DMA'd straight into the output buffer: returns (prefix, suffix).
+std::pair<std::string, std::string> encode_video_frame(const FrameMeta& m, size_t data_len,
+                                                       const std::string& device_id);
+
+}  // namespace vep

@@ -1,0 +1,205 @@
+// Synthetic H.264 camera encoder (I_PCM / P_Skip). See synth.h.
+#include "synth.h"
+
+#include <algorithm>
+#include <cmath>
+
+namespace vep {
+
+using namespace h264;
+
+SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
+  VEP_CHECK(cfg.width >= 16 && cfg.height >= 16 && cfg.width % 2 == 0 && cfg.height % 2 == 0,
+            "synthetic size must be even and >= 16");
+  wmbs_ = (cfg.width + 15) / 16;
+  hmbs_ = (cfg.height + 15) / 16;
+  sps_.profile_idc = 66;
+  sps_.constraint_flags = 0xC0;
+  sps_.level_idc = 51;
+  sps_.log2_max_frame_num = 8;
+  sps_.poc_type = 2;
+  sps_.max_num_ref_frames = 1;
+  sps_.width_mbs = wmbs_;
+  sps_.height_map_units = hmbs_;
+  sps_.crop_right = wmbs_ * 16 - cfg.width;
+  sps_.crop_bottom = hmbs_ * 16 - cfg.height;
+  sps_.timing_info = true;
+  sps_.num_units_in_tick = 1;
+  sps_.time_scale = u32(2 * cfg.fps);
+  pps_.deblocking_filter_control = true;
+  std::vector<u8> r = write_sps(sps_);
+  rbsp_to_ebsp(r.data(), r.size(), sps_nal_);
+  r = write_pps(pps_);
+  rbsp_to_ebsp(r.data(), r.size(), pps_nal_);
+  pic_.alloc(wmbs_ * 16, hmbs_ * 16);
+  bg_.alloc(wmbs_ * 16, hmbs_ * 16);
+  state_ = cfg.seed * 0x9E3779B97F4A7C15ull + 0x1234567ull;
+  double area = std::max(1.0, cfg.motion * wmbs_ * hmbs_);
+  bw_ = std::clamp(int(std::lround(std::sqrt(area * 4.0 / 3.0))), 1, wmbs_);
+  bh_ = std::clamp(int(std::lround(area / bw_)), 1, hmbs_);
+  if (cfg.motion <= 0) bw_ = bh_ = 0;
+}
+
+u64 SynthH264::rnd() {
+  u64 x = state_;
+  x ^= x << 13;
+  x ^= x >> 7;
+  x ^= x << 17;
+  return state_ = x;
+}
+
+void SynthH264::paint_background() {
+  const int W = bg_.coded_w, H = bg_.coded_h;
+  const int lo = cfg_.zero_samples ? 0 : 16;
+  for (int y = 0; y < H; ++y) {
+    u8* row = &bg_.y[size_t(y) * W];
+    for (int x = 0; x < W; x += 8) {
+      u64 r = rnd();
+      for (int k = 0; k < 8; ++k) {
+        int v = 16 + ((x + k) * 3 + y * 2) % 160 + int((r >> (8 * k)) & 63);
+        row[x + k] = u8(std::clamp(v, lo, 235));
+      }
+    }
+  }
+  for (int y = 0; y < H / 2; ++y) {
+    u8* row = &bg_.uv[size_t(y) * W];
+    for (int x = 0; x < W; x += 8) {
+      u64 r = rnd();
+      for (int k = 0; k < 8; ++k) {
+        int base = (k & 1) ? 96 + (y % 64) : 96 + ((x / 2) % 64);
+        row[x + k] = u8(std::clamp(base + int((r >> (8 * k)) & 15), lo, 240));
+      }
+    }
+  }
+  if (cfg_.zero_samples) {  // plant explicit 00 00 runs so EPBs appear in the NAL
+    for (int y = 0; y < H; y += 7) bg_.y[size_t(y) * W + (y % W)] = 0, bg_.y[size_t(y) * W + ((y + 1) % W)] = 0;
+  }
+}
+
+SynthH264::Rect SynthH264::box_at(i64 f) const {
+  if (bw_ == 0) return {0, 0, 0, 0};
+  int span_x = std::max(1, wmbs_ - bw_ + 1), span_y = std::max(1, hmbs_ - bh_ + 1);
+  i64 px = f % (2 * span_x);
+  int x = int(px < span_x ? px : 2 * span_x - 1 - px);
+  i64 py = (f / 2) % (2 * span_y);
+  int y = int(py < span_y ? py : 2 * span_y - 1 - py);
+  return {x, y, x + bw_, y + bh_};
+}
+
+void SynthH264::paint_box(const Rect& r) {
+  const int W = pic_.coded_w;
+  u8 cb = u8(64 + (rnd() & 127)), cr = u8(64 + (rnd() & 127));
+  for (int y = r.y0 * 16; y < r.y1 * 16; ++y) {
+    u8* row = &pic_.y[size_t(y) * W];
+    for (int x = r.x0 * 16; x < r.x1 * 16; x += 8) {
+      u64 q = rnd();
+      for (int k = 0; k < 8; ++k) row[x + k] = u8(180 + ((q >> (8 * k)) & 31));
+    }
+  }
+  for (int y = r.y0 * 8; y < r.y1 * 8; ++y) {
+    u8* row = &pic_.uv[size_t(y) * W];
+    for (int x = r.x0 * 16; x < r.x1 * 16; x += 2) {
+      row[x] = cb;
+      row[x + 1] = cr;
+    }
+  }
+}
+
+void SynthH264::pcm_payload(int mb, u8* out) const {
+  const int W = pic_.coded_w;
+  int mx = mb % wmbs_, my = mb / wmbs_;
+  for (int r = 0; r < 16; ++r)
+    std::memcpy(out + r * 16, &pic_.y[size_t(my * 16 + r) * W + mx * 16], 16);
+  for (int r = 0; r < 8; ++r) {
+    const u8* s = &pic_.uv[size_t(my * 8 + r) * W + mx * 16];
+    for (int c = 0; c < 8; ++c) {
+      out[256 + r * 8 + c] = s[2 * c];
+      out[320 + r * 8 + c] = s[2 * c + 1];
+    }
+  }
+}
+
+std::vector<u8> SynthH264::encode_slice(bool idr, int mb0, int mb1,
+                                        const std::vector<u8>& coded) {
+  BitWriter bw;
+  SliceHeader sh;
+  sh.nal_type = idr ? kNalIdr : kNalSlice;
+  sh.nal_ref_idc = 3;
+  sh.first_mb = mb0;
+  sh.slice_type = idr ? 7 : 5;
+  sh.frame_num = frame_num_;
+  sh.idr_pic_id = idr_id_;
+  sh.disable_deblocking = 1;
+  write_slice_header(bw, sh, sps_, pps_);
+  u8 buf[kPcmMbBytes];
+  int run = 0;
+  for (int mb = mb0; mb < mb1; ++mb) {
+    if (!idr && !coded[mb]) {
+      ++run;
+      continue;
+    }
+    if (!idr) {
+      bw.ue(u32(run));
+      run = 0;
+    }
+    bw.ue(idr ? 25u : 30u);
+    bw.align_zero();
+    pcm_payload(mb, buf);
+    bw.bytes(buf, kPcmMbBytes);
+  }
+  if (!idr && run > 0) bw.ue(u32(run));
+  bw.trailing();
+  std::vector<u8> nal;
+  rbsp_to_ebsp(bw.buf().data(), bw.buf().size(), nal);
+  return nal;
+}
+
+std::shared_ptr<AccessUnit> SynthH264::next() {
+  ++frame_;
+  const bool idr = (frame_ % cfg_.gop) == 0;
+  auto au = std::make_shared<AccessUnit>();
+  au->codec = Codec::kH264;
+  au->pts = au->dts = frame_ * 90000 / cfg_.fps;
+  au->duration = 90000 / cfg_.fps;
+  au->keyframe = idr;
+  au->seq = u64(frame_);
+  au->arrival_ms = now_ms();
+  const int total = wmbs_ * hmbs_;
+  std::vector<u8> coded(size_t(total), 0);
+  Rect box = box_at(frame_);
+  if (idr) {
+    paint_background();
+    pic_.y = bg_.y;
+    pic_.uv = bg_.uv;
+    if (bw_) paint_box(box);
+    frame_num_ = 0;
+    idr_id_ = (idr_id_ + 1) & 0xffff;
+    au->add_nal(sps_nal_.data(), sps_nal_.size());
+    au->add_nal(pps_nal_.data(), pps_nal_.size());
+  } else {
+    frame_num_ = (frame_num_ + 1) % (1 << sps_.log2_max_frame_num);
+    // restore background under the previous box, paint the new one
+    const int W = pic_.coded_w;
+    const Rect& o = prev_box_;
+    for (int y = o.y0 * 16; y < o.y1 * 16; ++y)
+      std::memcpy(&pic_.y[size_t(y) * W + o.x0 * 16], &bg_.y[size_t(y) * W + o.x0 * 16],
+                  size_t(o.x1 - o.x0) * 16);
+    for (int y = o.y0 * 8; y < o.y1 * 8; ++y)
+      std::memcpy(&pic_.uv[size_t(y) * W + o.x0 * 16], &bg_.uv[size_t(y) * W + o.x0 * 16],
+                  size_t(o.x1 - o.x0) * 16);
+    if (bw_) paint_box(box);
+    for (const Rect& r : {o, box})
+      for (int y = r.y0; y < r.y1; ++y)
+        for (int x = r.x0; x < r.x1; ++x) coded[size_t(y) * wmbs_ + x] = 1;
+  }
+  prev_box_ = box;
+  const int ns = std::max(1, std::min(cfg_.slices, hmbs_));
+  for (int s = 0; s < ns; ++s) {
+    int r0 = hmbs_ * s / ns, r1 = hmbs_ * (s + 1) / ns;
+    std::vector<u8> nal = encode_slice(idr, r0 * wmbs_, r1 * wmbs_, coded);
+    au->add_nal(nal.data(), nal.size());
+  }
+  return au;
+}
+
+}  // namespace vep

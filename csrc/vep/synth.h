@@ -1,0 +1,54 @@
+// Synthetic camera: a conformant H.264 Baseline encoder emitting IDR pictures of I_PCM
+// macroblocks and P pictures of P_Skip + I_PCM macroblocks (a moving object over a static
+// random background). Lets every BASELINE.json config run without cameras or network.
+//
+// The reference had no synthetic source at all — its tests used real cameras
+// (README.md:117-239).
+#pragma once
+
+#include "codec.h"
+
+namespace vep {
+
+struct SynthConfig {
+  int width = 640, height = 480;
+  int fps = 30;
+  int gop = 30;            // IDR period in frames
+  double motion = 0.05;    // fraction of the picture covered by the moving object
+  u64 seed = 1;
+  int slices = 1;          // slices per picture (MB-row aligned)
+  bool zero_samples = false;  // allow 0x00 PCM samples (forces emulation-prevention bytes)
+};
+
+class SynthH264 {
+ public:
+  explicit SynthH264(const SynthConfig& cfg);
+  std::shared_ptr<AccessUnit> next();
+  const HostSurface& picture() const { return pic_; }  // ground truth of the last AU
+  const std::vector<u8>& sps_nal() const { return sps_nal_; }
+  const std::vector<u8>& pps_nal() const { return pps_nal_; }
+  const SynthConfig& config() const { return cfg_; }
+  i64 frame_index() const { return frame_; }
+
+ private:
+  struct Rect { int x0, y0, x1, y1; };
+  u64 rnd();
+  void paint_background();
+  void paint_box(const Rect& r);
+  Rect box_at(i64 f) const;
+  void pcm_payload(int mb, u8* out) const;
+  std::vector<u8> encode_slice(bool idr, int mb0, int mb1, const std::vector<u8>& coded);
+
+  SynthConfig cfg_;
+  h264::Sps sps_;
+  h264::Pps pps_;
+  std::vector<u8> sps_nal_, pps_nal_;
+  HostSurface pic_, bg_;
+  int wmbs_, hmbs_, bw_, bh_;
+  i64 frame_ = -1;
+  int idr_id_ = 0, frame_num_ = 0;
+  u64 state_;
+  Rect prev_box_{0, 0, 0, 0};
+};
+
+}  // namespace vep

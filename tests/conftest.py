@@ -1,0 +1,45 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+def _gpu_count():
+    try:
+        from video_edge_ai_proxy_amd import native
+
+        return native.device_count()
+    except Exception:
+        return 0
+
+
+def pytest_collection_modifyitems(config, items):
+    if _gpu_count() > 0:
+        return
+    skip = pytest.mark.skip(reason="no GPU visible")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
+
+
+@pytest.fixture(scope="session")
+def native():
+    from video_edge_ai_proxy_amd import native as n
+
+    return n
+
+
+def synth(native, w=640, h=480, gop=10, motion=0.05, seed=1, slices=1, zero=False, fps=30):
+    c = native.SynthConfig()
+    c.width, c.height, c.gop, c.motion, c.seed, c.slices, c.fps = w, h, gop, motion, seed, slices, fps
+    c.zero_samples = zero
+    return native.SynthH264(c)
