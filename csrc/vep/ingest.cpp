@@ -1,0 +1,211 @@
+// Ingest session / supervisor implementation. See ingest.h.
+#include "ingest.h"
+
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include <algorithm>
+
+namespace vep {
+
+IngestSession::IngestSession(Worker& w, int cam, IngestConfig cfg,
+                             std::shared_ptr<mux::Archiver> archiver)
+    : w_(w), cam_(cam), cfg_(std::move(cfg)), archiver_(std::move(archiver)) {}
+
+IngestSession::~IngestSession() { stop(); }
+
+void IngestSession::log(bool err, const std::string& s) {
+  if (Camera* c = w_.camera(cam_)) c->logs.add(err, s);
+}
+
+void IngestSession::start() {
+  stop_ = false;
+  th_ = std::thread([this] { run(); });
+}
+
+void IngestSession::stop() {
+  stop_ = true;
+  if (th_.joinable()) th_.join();
+  std::lock_guard<std::mutex> g(mu_);
+  if (st_.status != "created") {
+    st_.status = "exited";
+    st_.running = st_.restarting = false;
+    st_.finished_at_ms = now_ms();
+  }
+}
+
+SessionState IngestSession::state() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return st_;
+}
+
+bool IngestSession::sleep_interruptible(int ms) {
+  for (int t = 0; t < ms && !stop_.load(); t += 20)
+    std::this_thread::sleep_for(std::chrono::milliseconds(std::min(20, ms - t)));
+  return !stop_.load();
+}
+
+void IngestSession::on_au(const AuPtr& au) {
+  Camera* cam = w_.camera(cam_);
+  if (!cam) return;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.aus++;
+  }
+  if (au->codec == Codec::kH264) {
+    for (size_t i = 0; i < au->nals.size(); ++i) {
+      int t = au->nal(i)[0] & 0x1f;
+      if (t == h264::kNalSps) sps_.assign(au->nal(i), au->nal(i) + au->nal_size(i));
+      if (t == h264::kNalPps) pps_.assign(au->nal(i), au->nal(i) + au->nal_size(i));
+    }
+  }
+  // --- archive: previous GOP goes to the archiver on every keyframe (rtsp_to_rtmp.py:97-110)
+  if (au->keyframe) {
+    if (!gop_.empty() && archiver_ && !cfg_.disk_path.empty() && !sps_.empty() && !pps_.empty()) {
+      mux::Mp4Info info;
+      if (cam->ring()) {
+        info.width = cam->ring()->width();
+        info.height = cam->ring()->height();
+      }
+      if (info.width == 0 && !sps_.empty()) {
+        std::vector<u8> r(sps_.size());
+        size_t n = ebsp_to_rbsp(sps_.data(), sps_.size(), r.data());
+        try {
+          h264::Sps s = h264::parse_sps(r.data(), n);
+          info.width = s.width();
+          info.height = s.height();
+        } catch (...) {
+        }
+      }
+      info.sps = sps_;
+      info.pps = pps_;
+      archiver_->enqueue(cfg_.disk_path, cfg_.name, gop_start_ms_, std::move(gop_), info);
+    }
+    gop_.clear();
+    gop_start_ms_ = now_ms();
+    seen_key_ = true;
+  }
+  if (seen_key_) gop_.push_back(au);
+
+  // --- decode scheduling (lazy / keyframe-only / catch-up) lives in the camera
+  cam->on_access_unit(au);
+
+  // --- RTMP pass-through (rtsp_to_rtmp.py:127-139, :162-182)
+  const bool want = cam->proxy_rtmp.load() && !cfg_.rtmp_url.empty();
+  const bool rising = want && !prev_proxy_;
+  prev_proxy_ = want;
+  if (!want) {
+    if (pub_) {
+      pub_->close();
+      pub_.reset();
+      pub_ts0_ = -1;
+    }
+    return;
+  }
+  if (!seen_key_) return;
+  try {
+    if (!pub_ || !pub_->connected()) {
+      if (mono_us() / 1000 < pub_retry_at_) return;
+      pub_ = std::make_unique<mux::RtmpPublisher>(cfg_.rtmp_url, cfg_.timeout_ms);
+      pub_->connect();
+      log(false, "rtmp publishing to " + cfg_.rtmp_url);
+      pub_ts0_ = -1;
+    }
+    auto ts_ms = [&](const AccessUnit& a) {
+      if (pub_ts0_ < 0) pub_ts0_ = a.dts;
+      return u32(std::max<i64>(0, (a.dts - pub_ts0_) / 90));
+    };
+    if (rising || pub_->messages() == 0) {
+      // start the stream at a keyframe: sequence header + the whole current GOP
+      if (!sps_.empty() && !pps_.empty()) pub_->send_sequence_header(sps_, pps_);
+      for (auto& p : gop_) pub_->send_au(*p, ts_ms(*p));
+    } else {
+      pub_->send_au(*au, ts_ms(*au));
+    }
+    std::lock_guard<std::mutex> g(mu_);
+    st_.rtmp_messages = pub_->messages();
+    st_.rtmp_error.clear();
+  } catch (const std::exception& e) {
+    log(true, std::string("failed muxing: ") + e.what());
+    pub_.reset();
+    pub_retry_at_ = mono_us() / 1000 + 2000;
+    std::lock_guard<std::mutex> g(mu_);
+    st_.rtmp_error = e.what();
+  }
+}
+
+void IngestSession::run() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.pid = int(::syscall(SYS_gettid));
+  }
+  net::RtspClientOptions opt;
+  opt.timeout_ms = cfg_.timeout_ms;
+  while (!stop_.load()) {
+    int delay = cfg_.reconnect_delay_ms;
+    try {
+      net::RtspClient client(cfg_.rtsp_url, opt);
+      net::RtspStreamInfo info = client.open();
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        st_.status = "running";
+        st_.running = true;
+        st_.restarting = false;
+        st_.dead = false;
+        st_.exit_code = 0;
+        st_.error.clear();
+        st_.started_at_ms = now_ms();
+        st_.failing_streak = 0;
+        st_.health = "healthy";
+        st_.fps = info.framerate;
+      }
+      for (auto& ps : info.param_sets) {
+        if (ps.empty()) continue;
+        int t = ps[0] & 0x1f;
+        if (t == h264::kNalSps) sps_ = ps;
+        if (t == h264::kNalPps) pps_ = ps;
+      }
+      log(false, "connected to " + cfg_.name + " (" +
+                     (info.codec == Codec::kH264 ? "H.264" : "H.265") + ")");
+      std::string why = client.run([this](const AuPtr& au) { on_au(au); }, stop_);
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        st_.bytes += client.bytes();
+        st_.lost += client.lost();
+      }
+      if (stop_.load()) break;
+      log(false, "rtsp stopped streaming (" + why + ")...waiting for camera to reappear");
+      std::lock_guard<std::mutex> g(mu_);
+      st_.status = "restarting";
+      st_.running = false;
+      st_.restarting = true;
+      st_.finished_at_ms = now_ms();
+      st_.restart_count++;
+      st_.failing_streak++;
+      st_.health = st_.failing_streak >= 3 ? "unhealthy" : "starting";
+      st_.error = why;
+      delay = cfg_.reconnect_delay_ms;
+    } catch (const std::exception& e) {
+      log(true, std::string("failed to connect to RTSP camera ") + e.what());
+      std::lock_guard<std::mutex> g(mu_);
+      st_.status = "restarting";
+      st_.running = false;
+      st_.restarting = true;
+      st_.exit_code = 1;  // rtsp_to_rtmp.py:76-78 os._exit(1)
+      st_.error = e.what();
+      st_.finished_at_ms = now_ms();
+      st_.restart_count++;
+      st_.failing_streak++;
+      st_.health = st_.failing_streak >= 3 ? "unhealthy" : "starting";
+      int shift = std::min(st_.failing_streak - 1, 5);
+      delay = std::min(cfg_.max_backoff_ms, cfg_.reconnect_delay_ms << shift);
+    }
+    gop_.clear();
+    seen_key_ = false;
+    prev_proxy_ = false;
+    pub_.reset();
+    if (!sleep_interruptible(delay)) break;
+  }
+}
+
+}  // namespace vep

@@ -1,0 +1,85 @@
+// Per-camera ingest session + supervisor: RTSP client thread that feeds the camera's lazy
+// decoder, the RTMP pass-through (proxy) and the per-GOP MP4 archiver, with restart-always
+// semantics and container-like state for ListStreams / REST Info.
+//
+// Reference parity (one Docker container + Python worker per camera):
+//  * connect / demux / reconnect-after-1 s: python/rtsp_to_rtmp.py:49-187
+//  * proxy rising edge flushes the current GOP, then muxes every packet: :127-139, :162-182
+//  * GOP -> archiver queue on every keyframe: :97-110; archive.py
+//  * Docker `restart: always` + ContainerState (Status/Running/Restarting/ExitCode/Error/Pid/
+//    StartedAt/FinishedAt/Health.FailingStreak): services/rtsp_process_manager.go:70-81, :283-335
+#pragma once
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+
+#include "mux.h"
+#include "net.h"
+#include "runtime.h"
+
+namespace vep {
+
+struct IngestConfig {
+  std::string name;
+  std::string rtsp_url;
+  std::string rtmp_url;     // empty: no pass-through possible
+  std::string disk_path;    // empty: no archive
+  int timeout_ms = 5000;
+  int reconnect_delay_ms = 1000;
+  int max_backoff_ms = 30000;
+};
+
+struct SessionState {
+  std::string status = "created";  // created | running | restarting | exited | dead
+  bool running = false, restarting = false, dead = false, paused = false, oomkilled = false;
+  int pid = 0;
+  int exit_code = 0;
+  std::string error;
+  i64 started_at_ms = 0, finished_at_ms = 0;
+  int restart_count = 0;
+  int failing_streak = 0;
+  std::string health = "starting";
+  u64 aus = 0, bytes = 0, lost = 0;
+  u64 rtmp_messages = 0;
+  std::string rtmp_error;
+  double fps = 0;
+  int width = 0, height = 0;
+};
+
+class IngestSession {
+ public:
+  IngestSession(Worker& w, int cam, IngestConfig cfg, std::shared_ptr<mux::Archiver> archiver);
+  ~IngestSession();
+  void start();
+  void stop();  // joins the thread
+  SessionState state() const;
+  const IngestConfig& config() const { return cfg_; }
+  void log(bool err, const std::string& s);
+
+ private:
+  void run();
+  void on_au(const AuPtr& au);
+  bool sleep_interruptible(int ms);
+  Worker& w_;
+  int cam_;
+  IngestConfig cfg_;
+  std::shared_ptr<mux::Archiver> archiver_;
+  std::atomic<bool> stop_{false};
+  std::thread th_;
+  mutable std::mutex mu_;
+  SessionState st_;
+  // pass-through / archive state (ingest thread only)
+  std::unique_ptr<mux::RtmpPublisher> pub_;
+  bool prev_proxy_ = false;
+  i64 pub_retry_at_ = 0;
+  i64 pub_ts0_ = -1;
+  std::vector<u8> sps_, pps_;
+  std::vector<AuPtr> gop_;
+  i64 gop_start_ms_ = 0;
+  bool seen_key_ = false;
+};
+
+}  // namespace vep
