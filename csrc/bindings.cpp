@@ -341,6 +341,24 @@ PYBIND11_MODULE(_vep, m) {
            [](Worker& w, uintptr_t hwc, uintptr_t chw, int rows) {
              w.set_consumer_buffers(reinterpret_cast<u8*>(hwc), reinterpret_cast<void*>(chw), rows);
            })
+      .def("wait_frame",
+           // Block (GIL released) until the camera publishes a frame with seq > after.
+           [](Worker& w, int i, i64 after, int timeout_ms) {
+             Camera& c = cam_of(w, i);
+             py::gil_scoped_release r;
+             const i64 deadline = mono_us() + i64(timeout_ms) * 1000;
+             while (!c.ring()) {  // ring appears with the first decoded frame
+               if (mono_us() >= deadline) return false;
+               std::this_thread::sleep_for(std::chrono::milliseconds(2));
+             }
+             int left = int(std::max<i64>(0, (deadline - mono_us()) / 1000));
+             return c.ring()->wait_newer(after, left);
+           },
+           py::arg("idx"), py::arg("after"), py::arg("timeout_ms"))
+      .def("published", [](Worker& w, int i) {
+        Camera& c = cam_of(w, i);
+        return c.ring() ? c.ring()->published() : i64(0);
+      })
       .def("consumer_hwc_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.consumer_hwc()); })
       .def("consumer_chw_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.consumer_chw()); })
       .def("ring_slot_ptr", [](Worker& w, int i, int s) {

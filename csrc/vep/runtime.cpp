@@ -76,12 +76,21 @@ int FrameRing::begin_write() {
 }
 
 void FrameRing::commit(int slot, FrameMeta meta) {
-  std::lock_guard<std::mutex> g(meta_mu_);
-  meta.seq = published_.load() + 1;
-  slots_[slot]->meta = meta;
-  slots_[slot]->version.fetch_add(1, std::memory_order_acq_rel);  // even: stable
-  latest_.store(slot, std::memory_order_release);
-  published_.store(meta.seq, std::memory_order_release);
+  {
+    std::lock_guard<std::mutex> g(meta_mu_);
+    meta.seq = published_.load() + 1;
+    slots_[slot]->meta = meta;
+    slots_[slot]->version.fetch_add(1, std::memory_order_acq_rel);  // even: stable
+    latest_.store(slot, std::memory_order_release);
+    published_.store(meta.seq, std::memory_order_release);
+  }
+  cv_.notify_all();
+}
+
+bool FrameRing::wait_newer(i64 after, int timeout_ms) const {
+  std::unique_lock<std::mutex> g(meta_mu_);
+  return cv_.wait_for(g, std::chrono::milliseconds(timeout_ms),
+                      [&] { return published_.load() > after; });
 }
 
 bool FrameRing::latest(i64 after, FrameMeta* meta, int* slot) const {

@@ -70,8 +70,11 @@ class FrameRing {
   // true if `slot` still holds the frame with publish counter `seq`
   bool still_valid(int slot, i64 seq) const;
   i64 published() const { return published_.load(std::memory_order_acquire); }
+  // Block until a frame with seq > after is published (XREAD ... BLOCK analog).
+  bool wait_newer(i64 after, int timeout_ms) const;
 
  private:
+  mutable std::condition_variable cv_;
   struct Slot {
     std::atomic<u64> version{0};  // odd while being written
     FrameMeta meta;

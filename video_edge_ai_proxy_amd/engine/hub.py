@@ -1,0 +1,189 @@
+"""Hub: the node-level data-plane owner (one native Worker per local GPU, camera placement,
+ingest sessions, archiver, latest-frame access).
+
+Reference parity: replaces the per-camera Docker container + Redis pair
+(services/rtsp_process_manager.go:50-150 starts a container per camera; python/ workers publish
+frames to Redis). Here every camera is a native IngestSession thread feeding a Camera on the GPU
+Worker chosen by the placement policy (camera data parallelism inside one process; across
+processes/nodes see ``video_edge_ai_proxy_amd.parallel``).
+"""
+from __future__ import annotations
+
+import hashlib
+import logging
+import os
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Optional
+
+from .._native import gpu_count, native
+from ..config import Config
+from ..utils import now_ms
+
+log = logging.getLogger("vep.hub")
+
+_CHW = {"none": 0, "fp16": 1, "bf16": 2, "fp32": 3}
+
+
+class CameraNotFound(KeyError):
+    pass
+
+
+class CameraExists(ValueError):
+    pass
+
+
+@dataclass
+class CameraHandle:
+    name: str
+    worker_index: int
+    cam: int
+    rtsp: str
+    rtmp: str = ""
+    session: Optional[object] = None
+    created_ms: int = field(default_factory=now_ms)
+
+
+def place_camera(name: str, loads: list[int], policy: str = "least_loaded") -> int:
+    """Camera -> worker index. ``hash`` is stable across restarts; ``least_loaded`` balances."""
+    if not loads:
+        raise RuntimeError("no workers")
+    if policy == "hash":
+        h = int(hashlib.md5(name.encode()).hexdigest(), 16)
+        return h % len(loads)
+    return min(range(len(loads)), key=lambda i: (loads[i], i))
+
+
+class Hub:
+    def __init__(self, cfg: Config, devices: Optional[list[int]] = None):
+        self.cfg = cfg
+        if devices is None:
+            devices = list(cfg.gpu.devices) if cfg.gpu.devices else list(range(gpu_count()))
+        if not devices:
+            devices = [-1]  # CPU backend (no GPU visible)
+        self.devices = devices
+        g = cfg.gpu
+        self.workers = []
+        for d in devices:
+            w = native.Worker(device=d, letterbox_size=int(g.letterbox_size),
+                              chw_dtype=_CHW.get(g.letterbox_dtype, 0), mean=list(g.mean),
+                              std=list(g.std), max_cameras=int(g.max_cameras_per_gpu))
+            w.start()
+            self.workers.append(w)
+        self.archiver = native.Archiver()
+        self.cameras: dict[str, CameraHandle] = {}
+        self._lock = threading.RLock()
+        log.info("hub up: devices=%s", devices)
+
+    # ------------------------------------------------------------------ lifecycle
+    def _loads(self) -> list[int]:
+        loads = [0] * len(self.workers)
+        for h in self.cameras.values():
+            loads[h.worker_index] += 1
+        return loads
+
+    def archive_dir(self) -> str:
+        if not self.cfg.buffer.on_disk:
+            return ""
+        return self.cfg.buffer.on_disk_folder or os.path.join(self.cfg.data_dir, "archive")
+
+    def start_camera(self, name: str, rtsp: str, rtmp: str = "", disk_path: Optional[str] = None,
+                     timeout_ms: int = 5000, reconnect_delay_ms: int = 1000) -> CameraHandle:
+        with self._lock:
+            if name in self.cameras:
+                raise CameraExists(f"camera {name!r} already running")
+            wi = place_camera(name, self._loads(), self.cfg.gpu.placement)
+            w = self.workers[wi]
+            cam = w.add_camera(name, self.cfg.ring_slots)
+            w.set_idle_cutoff_ms(cam, int(self.cfg.gpu.idle_cutoff_ms))
+            h = CameraHandle(name, wi, cam, rtsp, rtmp)
+            disk = self.archive_dir() if disk_path is None else disk_path
+            h.session = native.IngestSession(w, cam, name, rtsp, rtmp or "", disk or "",
+                                             self.archiver, timeout_ms, reconnect_delay_ms, 30000)
+            h.session.start()
+            self.cameras[name] = h
+            log.info("camera %s -> worker %d (device %s) slot %d", name, wi, self.devices[wi], cam)
+            return h
+
+    def stop_camera(self, name: str) -> None:
+        with self._lock:
+            h = self.cameras.pop(name, None)
+        if h is None:
+            raise CameraNotFound(name)
+        h.session.stop()
+        self.workers[h.worker_index].remove_camera(h.cam)
+
+    def has(self, name: str) -> bool:
+        return name in self.cameras
+
+    def handle(self, name: str) -> CameraHandle:
+        h = self.cameras.get(name)
+        if h is None:
+            raise CameraNotFound(name)
+        return h
+
+    def worker_of(self, name: str):
+        h = self.handle(name)
+        return self.workers[h.worker_index], h.cam
+
+    def shutdown(self) -> None:
+        for name in list(self.cameras):
+            try:
+                self.stop_camera(name)
+            except CameraNotFound:
+                pass
+        for w in self.workers:
+            w.stop()
+        self.archiver.flush()
+
+    # ------------------------------------------------------------------ state
+    def state(self, name: str) -> dict:
+        h = self.handle(name)
+        w = self.workers[h.worker_index]
+        st = h.session.state()
+        st.update(w.stats(h.cam))
+        st["device"] = self.devices[h.worker_index]
+        return st
+
+    def logs(self, name: str, last: int = 100) -> tuple[str, str]:
+        w, cam = self.worker_of(name)
+        return w.logs(cam, False, last), w.logs(cam, True, last)
+
+    # ------------------------------------------------------------------ control
+    def touch(self, name: str, keyframe_only: Optional[bool] = None) -> None:
+        """A client asked for a frame: refresh last_query (and keyframe-only mode)."""
+        w, cam = self.worker_of(name)
+        if keyframe_only is not None:
+            w.set_keyframe_only(cam, bool(keyframe_only))
+        w.set_last_query(cam, now_ms())
+
+    def set_proxy(self, name: str, on: bool) -> None:
+        w, cam = self.worker_of(name)
+        w.set_proxy(cam, bool(on))
+        w.set_last_query(cam, now_ms())
+
+    def proxy(self, name: str) -> bool:
+        w, cam = self.worker_of(name)
+        return bool(w.proxy(cam))
+
+    # ------------------------------------------------------------------ frames
+    def latest_frame_bytes(self, name: str, after: int = 0, wait_ms: int = 0):
+        """(seq, serialized VideoFrame, meta) of the newest frame with seq > after, or None."""
+        w, cam = self.worker_of(name)
+        if wait_ms > 0 and w.published(cam) <= after:
+            w.wait_frame(cam, after, wait_ms)
+        return w.video_frame(cam, after, name)
+
+    def latest_frame(self, name: str, after: int = 0):
+        w, cam = self.worker_of(name)
+        return w.read_latest(cam, after)
+
+    def wait_decoded(self, name: str, n: int = 1, timeout_s: float = 10.0) -> bool:
+        w, cam = self.worker_of(name)
+        deadline = time.time() + timeout_s
+        while time.time() < deadline:
+            if w.published(cam) >= n:
+                return True
+            w.wait_frame(cam, w.published(cam), 50)
+        return False

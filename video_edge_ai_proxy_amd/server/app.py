@@ -1,0 +1,129 @@
+"""Hub daemon bootstrap (``vep serve``).
+
+Reference parity: server/main.go:44-164 — load conf.yaml or defaults, open the registry store,
+build services, start cron jobs, REST on :8080 and gRPC on :50001, graceful shutdown on SIGINT.
+Differences: no Redis (frames/control in native memory), stored cameras are re-spawned at boot.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import signal
+import threading
+from dataclasses import dataclass
+from typing import Optional
+
+from ..config import Config, load_config
+from ..engine.hub import Hub
+from ..services.annotation import AnnotationConsumer, AnnotationQueue
+from ..services.cron import start_cron_jobs
+from ..services.edge import EdgeService
+from ..services.process_manager import ProcessManager
+from ..services.settings import SettingsManager
+from ..services.storage import Storage
+from .grpc_server import ImageService, serve
+from .metrics import Metrics
+from .rest import create_app
+
+log = logging.getLogger("vep.app")
+
+
+@dataclass
+class HubApp:
+    cfg: Config
+    storage: Storage
+    hub: Hub
+    pm: ProcessManager
+    settings: SettingsManager
+    edge: EdgeService
+    queue: AnnotationQueue
+    consumer: AnnotationConsumer
+    image: ImageService
+    grpc_server: object
+    rest_server: Optional[object]
+    rest_thread: Optional[threading.Thread]
+    cron: list
+    metrics: Metrics
+
+    @property
+    def grpc_port(self) -> int:
+        return self.grpc_server.bound_port
+
+    @property
+    def rest_port(self) -> int:
+        return self._rest_port
+
+    def stop(self):
+        log.info("shutting down")
+        try:
+            self.grpc_server.stop(grace=2).wait(5)
+        except Exception:
+            pass
+        if self.rest_server is not None:
+            self.rest_server.should_exit = True
+            if self.rest_thread:
+                self.rest_thread.join(timeout=5)
+        for j in self.cron:
+            j.stop()
+        self.queue.stop()
+        self.hub.shutdown()
+        self.storage.close()
+
+
+def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = None,
+              grpc_port: Optional[int] = None, devices=None, start_rest: bool = True,
+              restore: bool = True) -> HubApp:
+    os.makedirs(cfg.data_dir, exist_ok=True)
+    storage = Storage(os.path.join(cfg.data_dir, "registry.db"))
+    hub = Hub(cfg, devices)
+    pm = ProcessManager(storage, hub)
+    settings = SettingsManager(storage)
+    edge = EdgeService()
+    queue = AnnotationQueue(os.path.join(cfg.data_dir, "annotations.db"))
+    consumer = AnnotationConsumer(settings, edge, cfg.annotation.endpoint)
+    queue.start_consuming(consumer, cfg.annotation.unacked_limit, cfg.annotation.poll_duration_ms,
+                          cfg.annotation.max_batch_size)
+    image = ImageService(pm, settings, edge, queue, cfg.api.endpoint)
+    gport = cfg.grpc_port if grpc_port is None else grpc_port
+    gsrv = serve(image, f"{host}:{gport}")
+    cron = start_cron_jobs(cfg)
+    metrics = Metrics(hub, image)
+    rest_server = rest_thread = None
+    rport = cfg.port if rest_port is None else rest_port
+    if start_rest:
+        import socket
+
+        import uvicorn
+
+        app = create_app(pm, settings, metrics)
+        sock = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+        sock.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+        sock.bind((host, rport))
+        rport = sock.getsockname()[1]
+        ucfg = uvicorn.Config(app, log_level="warning", lifespan="off")
+        rest_server = uvicorn.Server(ucfg)
+        rest_thread = threading.Thread(target=rest_server.run, kwargs={"sockets": [sock]},
+                                       daemon=True, name="vep-rest")
+        rest_thread.start()
+    happ = HubApp(cfg, storage, hub, pm, settings, edge, queue, consumer, image, gsrv,
+                  rest_server, rest_thread, cron, metrics)
+    happ._rest_port = rport  # type: ignore[attr-defined]
+    if restore:
+        restored = pm.restore()
+        if restored:
+            log.info("restored %d cameras from the registry", len(restored))
+    log.info("vep ready: REST :%s gRPC :%s devices=%s", rport, gsrv.bound_port, hub.devices)
+    return happ
+
+
+def run_forever(cfg: Config, **kw) -> None:
+    app = build_app(cfg, **kw)
+    done = threading.Event()
+
+    def on_sig(*_):
+        done.set()
+
+    signal.signal(signal.SIGINT, on_sig)
+    signal.signal(signal.SIGTERM, on_sig)
+    done.wait()
+    app.stop()

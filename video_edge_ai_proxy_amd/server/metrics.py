@@ -1,0 +1,68 @@
+"""Prometheus metrics (new: the reference exposed none — SURVEY.md §5 observability row).
+
+Scraped lazily from the native counters: per-camera packets / decoded frames / errors / bytes /
+published frames / ingest state, per-worker batches and GPU kernel time, gRPC frame latency.
+"""
+from __future__ import annotations
+
+import statistics
+
+from prometheus_client import CONTENT_TYPE_LATEST, CollectorRegistry, generate_latest
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
+
+
+class HubCollector:
+    def __init__(self, hub, image_service=None):
+        self.hub = hub
+        self.svc = image_service
+
+    def collect(self):
+        labels = ["camera", "device"]
+        pk = CounterMetricFamily("vep_packets", "access units received", labels=labels)
+        dec = CounterMetricFamily("vep_decoded_frames", "frames reconstructed + converted", labels=labels)
+        errs = CounterMetricFamily("vep_decode_errors", "decode errors", labels=labels)
+        byt = CounterMetricFamily("vep_ingest_bytes", "bitstream bytes received", labels=labels)
+        run = GaugeMetricFamily("vep_camera_running", "ingest session connected", labels=labels)
+        rst = CounterMetricFamily("vep_camera_restarts", "ingest reconnects", labels=labels)
+        for name in list(self.hub.cameras):
+            try:
+                st = self.hub.state(name)
+            except KeyError:
+                continue
+            lv = [name, str(st.get("device"))]
+            pk.add_metric(lv, st.get("packets", 0))
+            dec.add_metric(lv, st.get("decoded", 0))
+            errs.add_metric(lv, st.get("errors", 0))
+            byt.add_metric(lv, st.get("bytes_in", 0))
+            run.add_metric(lv, 1.0 if st.get("running") else 0.0)
+            rst.add_metric(lv, st.get("restart_count", 0))
+        yield from (pk, dec, errs, byt, run, rst)
+        wb = CounterMetricFamily("vep_worker_batches", "batched decode launches", labels=["device"])
+        wf = CounterMetricFamily("vep_worker_frames", "frames decoded by the worker", labels=["device"])
+        wg = CounterMetricFamily("vep_worker_gpu_ms", "GPU time of decode batches (ms)", labels=["device"])
+        for d, w in zip(self.hub.devices, self.hub.workers):
+            wb.add_metric([str(d)], w.batches)
+            wf.add_metric([str(d)], w.frames)
+            wg.add_metric([str(d)], w.gpu_ms_total)
+        yield from (wb, wf, wg)
+        if self.svc is not None:
+            served = CounterMetricFamily("vep_grpc_frames_served", "VideoLatestImage frames sent")
+            served.add_metric([], self.svc.frames_served)
+            yield served
+            lat = list(self.svc.latencies_ms)
+            if lat:
+                g = GaugeMetricFamily("vep_grpc_frame_latency_ms", "server-side frame latency",
+                                      labels=["quantile"])
+                s = sorted(lat)
+                g.add_metric(["0.5"], statistics.median(s))
+                g.add_metric(["0.99"], s[max(0, int(len(s) * 0.99) - 1)])
+                yield g
+
+
+class Metrics:
+    def __init__(self, hub, image_service=None):
+        self.registry = CollectorRegistry()
+        self.registry.register(HubCollector(hub, image_service))
+
+    def render(self):
+        return generate_latest(self.registry), CONTENT_TYPE_LATEST
