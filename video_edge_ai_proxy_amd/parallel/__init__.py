@@ -1,1 +1,132 @@
+"""Camera data parallelism across GPUs and processes.
 
+* :func:`shard_cameras` — deterministic camera -> rank/GPU placement (rendezvous hashing: adding
+  a camera or a GPU moves only the cameras that must move).
+* :func:`init_distributed` — one process per GPU, ``torch.distributed`` over RCCL ("nccl") on
+  ROCm, gloo on CPU hosts; rendezvous on 127.0.0.1 by default.
+* :class:`ConsumerBatch` — the batched, letterboxed frame tensor every worker maintains for
+  annotation / inference consumers; ``gather()`` assembles the node-wide batch either with one
+  RCCL all-gather over xGMI (multi-process) or with peer copies (single process, many GPUs).
+
+The reference scaled by running one Docker container per camera on one host with no GPU and no
+collective communication at all (0 NCCL/MPI/Gloo call sites); camera-level data
+parallelism is the only parallelism that applies (no model is trained, there is no tensor /
+sequence dimension to split — a GOP must be decoded serially).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+from typing import Iterable, Optional
+
+import torch
+import torch.distributed as dist
+
+
+def shard_cameras(names: Iterable[str], world: int, capacity: Optional[int] = None) -> dict[str, int]:
+    """Rendezvous (highest-random-weight) hashing with an optional per-rank capacity.
+
+    Deterministic across processes and restarts; with ``capacity`` the overflow spills to the
+    next-best rank so load stays within ``capacity`` cameras per rank."""
+    names = list(names)
+    if world <= 0:
+        raise ValueError("world must be positive")
+    if capacity is not None and capacity * world < len(names):
+        raise ValueError(f"{len(names)} cameras exceed {world} x {capacity} capacity")
+    load = [0] * world
+    out: dict[str, int] = {}
+    for n in sorted(names):
+        scores = sorted(range(world), key=lambda r: hashlib.sha1(f"{n}|{r}".encode()).digest(),
+                        reverse=True)
+        for r in scores:
+            if capacity is None or load[r] < capacity:
+                out[n] = r
+                load[r] += 1
+                break
+    return out
+
+
+def balanced_shard(n_cameras: int, world: int) -> list[range]:
+    """Contiguous equal split used by the benchmark (weak scaling: fixed cameras per rank)."""
+    per, rem = divmod(n_cameras, world)
+    out, start = [], 0
+    for r in range(world):
+        k = per + (1 if r < rem else 0)
+        out.append(range(start, start + k))
+        start += k
+    return out
+
+
+def init_distributed(backend: Optional[str] = None) -> tuple[int, int, int]:
+    """Initialise torch.distributed from the torchrun environment. Returns (rank, world, local)."""
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29500")
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+        dist.init_process_group(backend=backend)
+    return rank, world, local
+
+
+class ConsumerBatch:
+    """Double-buffered ``[cams, S, S, 3]`` uint8 letterboxed batch owned by torch, written by a
+    native Worker's letterbox kernel, gathered across ranks with one RCCL all-gather.
+
+    Gathering the uint8 HWC tensor (1.2 MB per 640x640 camera) instead of the normalised
+    fp16/bf16 CHW tensor halves the xGMI bytes; consumers normalise after the gather (fused into
+    their first op, or via :func:`video_edge_ai_proxy_amd.ops.letterbox` style kernels)."""
+
+    def __init__(self, worker, cams: int, size: int, device: torch.device, world: int = 1):
+        self.worker = worker
+        self.cams, self.size, self.world = cams, size, world
+        self.bufs = [torch.zeros((cams, size, size, 3), dtype=torch.uint8, device=device)
+                     for _ in range(2)]
+        self.out = [torch.zeros((world * cams, size, size, 3), dtype=torch.uint8, device=device)
+                    for _ in range(2)] if world > 1 else None
+        self.handles = [None, None]
+        self.tick = 0
+
+    def prepare(self) -> torch.Tensor:
+        """Point the worker at the buffer for the next tick (waits if it still feeds a gather)."""
+        b = self.tick & 1
+        h = self.handles[b]
+        if h is not None:
+            h.wait()
+            self.handles[b] = None
+            if self.bufs[b].is_cuda:
+                torch.cuda.current_stream(self.bufs[b].device).synchronize()
+        self.worker.set_consumer_buffers(self.bufs[b].data_ptr(), 0, self.cams)
+        return self.bufs[b]
+
+    def gather(self, async_op: bool = True):
+        """All-gather the tick's batch (after the worker published it). Returns (tensor, work)."""
+        b = self.tick & 1
+        self.tick += 1
+        if self.world == 1:
+            return self.bufs[b], None
+        w = dist.all_gather_into_tensor(self.out[b], self.bufs[b], async_op=async_op)
+        self.handles[b] = w if async_op else None
+        return self.out[b], w
+
+    def drain(self):
+        for k in range(2):
+            if self.handles[k] is not None:
+                self.handles[k].wait()
+                self.handles[k] = None
+
+
+def gather_to_device(batches: list[torch.Tensor], device: torch.device) -> torch.Tensor:
+    """Single-process multi-GPU: concatenate per-GPU consumer batches on one device with peer
+    copies over xGMI (non_blocking copies on the destination's current stream)."""
+    total = sum(b.shape[0] for b in batches)
+    out = torch.empty((total, *batches[0].shape[1:]), dtype=batches[0].dtype, device=device)
+    off = 0
+    for b in batches:
+        out[off:off + b.shape[0]].copy_(b, non_blocking=True)
+        off += b.shape[0]
+    return out
