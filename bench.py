@@ -89,29 +89,42 @@ def main():
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam")
 
-    bufs = [torch.empty((cams, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(2)]
+    # The native worker keeps two ticks in flight (tick t's frames are published while tick
+    # t+2 is being launched), and one all-gather may still be reading an older tick: 4 buffers.
+    NB = 4
+    bufs = [torch.empty((cams, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
     gather = world > 1 and not a.no_gather
     gathered = [torch.empty((world * cams, S, S, 3), dtype=torch.uint8, device=dev)
-                for _ in range(2)] if gather else None
-    handles = [None, None]
+                for _ in range(NB)] if gather else None
+    handles = [None] * NB
+    pending = []  # ticks launched whose consumer batch has not been handed to the gather yet
 
     def sync():
         if use_gpu:
             torch.cuda.synchronize()
 
+    def issue_gather(t):
+        k = t % NB
+        if gather:
+            handles[k] = dist.all_gather_into_tensor(gathered[k], bufs[k], async_op=True)
+
     def step(i):
-        b = i & 1
-        if handles[b] is not None:  # buffer b may still feed the all-gather of tick i-2
+        b = i % NB
+        if handles[b] is not None:  # buffer b may still feed the all-gather of tick i-4
             handles[b].wait()
             handles[b] = None
             sync()
         worker.set_consumer_buffers(bufs[b].data_ptr(), 0, cams)
-        rb.step()  # returns once the tick's frames + consumer batch are published
-        if gather:
-            handles[b] = dist.all_gather_into_tensor(gathered[b], bufs[b], async_op=True)
+        rb.step()  # enqueues tick i; ticks <= i-2 are published when it returns
+        pending.append(i)
+        while pending and pending[0] <= i - 2:
+            issue_gather(pending.pop(0))
 
     def drain():
-        for k in range(2):
+        rb.drain()  # publishes every launched tick
+        while pending:
+            issue_gather(pending.pop(0))
+        for k in range(NB):
             if handles[k] is not None:
                 handles[k].wait()
                 handles[k] = None
@@ -148,7 +161,7 @@ def main():
         # the single-process tick must not touch the collective: decode-only ticks here
         worker.set_consumer_buffers(bufs[0].data_ptr(), 0, cams)
         serve_lat, next_lat, nlat = measure_latency(worker, list(rb.cameras), a.latency_samples,
-                                                    rb.step, float(a.fps))
+                                                    lambda: (rb.step(), rb.drain()), float(a.fps))
     if world > 1:
         dist.barrier()
 

@@ -244,6 +244,7 @@ PYBIND11_MODULE(_vep, m) {
       .def("start", &Worker::start)
       .def("stop", &Worker::stop, py::call_guard<py::gil_scoped_release>())
       .def("flush", &Worker::flush, py::call_guard<py::gil_scoped_release>())
+      .def("complete_all", &Worker::complete_all, py::call_guard<py::gil_scoped_release>())
       .def("set_last_query", [](Worker& w, int i, i64 ms) { cam_of(w, i).last_query_ms.store(ms); })
       .def("last_query", [](Worker& w, int i) { return cam_of(w, i).last_query_ms.load(); })
       .def("set_keyframe_only", [](Worker& w, int i, bool v) { cam_of(w, i).keyframe_only.store(v); })
@@ -397,12 +398,14 @@ PYBIND11_MODULE(_vep, m) {
 
   // ---- op API on caller-owned device buffers (torch tensors pass data_ptr / stream) ----
   m.def("nv12_to_bgr",
-        [](uintptr_t y, uintptr_t uv, uintptr_t map, uintptr_t payload, int wmbs, int hmbs,
-           int out_w, int out_h, int crop_left, int crop_top, uintptr_t out, uintptr_t stream) {
+        [](uintptr_t y, uintptr_t uv, uintptr_t mask, uintptr_t prefix, uintptr_t payload, int wmbs,
+           int hmbs, int out_w, int out_h, int crop_left, int crop_top, uintptr_t out,
+           uintptr_t stream) {
           gpu::DecodeDesc d{};
           d.y = reinterpret_cast<u8*>(y);
           d.uv = reinterpret_cast<u8*>(uv);
-          d.map = reinterpret_cast<const i32*>(map);
+          d.mask = reinterpret_cast<const u32*>(mask);
+          d.prefix = reinterpret_cast<const u32*>(prefix);
           d.payload = reinterpret_cast<const u8*>(payload);
           d.bgr = reinterpret_cast<u8*>(out);
           d.wmbs = wmbs;

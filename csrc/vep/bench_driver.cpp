@@ -16,6 +16,7 @@ ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cach
   pool_.parallel_for(ncams, [&](int i) {
     SynthConfig c = base;
     c.seed = base.seed + u64(i) * 7919u;
+    c.idr_phase = base.idr_phase + (i * gop) / ncams;  // unsynchronised cameras
     SynthH264 enc(c);
     auto& v = aus_[size_t(i)];
     v.reserve(size_t(nframes));
@@ -93,14 +94,17 @@ void ReplayBench::step() {
   for (auto& j : jobs) bytes_ += u64(j.upd.nslots) * kPcmMbBytes;
   const i64 t0 = mono_us();
   const size_t n = jobs.size();
-  w_.run_batch(jobs);
+  w_.launch_async(jobs);  // publishes tick t-2; ticks t-1 and t stay in flight
   batch_us_ += double(mono_us() - t0);
   frames_ += n;
 }
 
 void ReplayBench::drain() {
-  std::unique_lock<std::mutex> g(mu_);
-  cv_.wait(g, [&] { return !want_; });
+  {
+    std::unique_lock<std::mutex> g(mu_);
+    cv_.wait(g, [&] { return !want_; });
+  }
+  w_.complete_all();
 }
 
 }  // namespace vep

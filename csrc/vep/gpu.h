@@ -30,8 +30,12 @@ struct DecodeDesc {
   u8* y;              // NV12 luma plane, pitch = wmbs*16
   u8* uv;             // NV12 interleaved chroma plane, pitch = wmbs*16
   u8* bgr;            // output slot: out_h x out_w x 3 (packed BGR24); may be null
-  const i32* map;     // per-MB payload slot or -1; null = no update (pure conversion)
-  const u8* payload;  // 384-B PCM slots
+  // Coded-MB bitmask (bit mb of word mb/32) + exclusive per-word popcount prefix: the payload
+  // slot of a coded MB is prefix[w] + popc(mask[w] & below(mb)), slots in raster order.
+  // null mask = no update (pure conversion). 2 bits/MB of H2D instead of a 32-bit map.
+  const u32* mask;
+  const u32* prefix;
+  const u8* payload;  // 384-B PCM slots, raster order of the coded MBs
   i32 wmbs, hmbs;
   i32 out_w, out_h;
   i32 crop_left, crop_top;

@@ -64,7 +64,12 @@ __device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const i
   if (mbx >= d.wmbs || mby >= d.hmbs) return;
   const int pitch = d.wmbs * 16;
   const int mb = mby * d.wmbs + mbx;
-  const int slot = d.map ? d.map[mb] : -1;
+  int slot = -1;
+  if (d.mask) {
+    const uint32_t w = d.mask[mb >> 5];
+    const uint32_t bit = 1u << (mb & 31);
+    if (w & bit) slot = int(d.prefix[mb >> 5] + __builtin_popcount(w & (bit - 1u)));
+  }
   uint8_t* yp = d.y + size_t(mby * 16 + row) * pitch + mbx * 16;
   uint8_t* uvp = d.uv + size_t(mby * 8 + (row >> 1)) * pitch + mbx * 16;
   uint4 yv, uvv;

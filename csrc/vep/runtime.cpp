@@ -65,12 +65,17 @@ FrameRing::~FrameRing() { dev_.free(base_); }
 
 int FrameRing::begin_write() {
   std::lock_guard<std::mutex> g(meta_mu_);
+  // never overwrite the newest committed frame or a slot an in-flight batch is writing
+  const int n = int(slots_.size());
   int s = next_;
-  next_ = (next_ + 1) % int(slots_.size());
-  if (int(slots_.size()) > 1 && s == latest_.load()) {  // never overwrite the newest frame
-    s = next_;
-    next_ = (next_ + 1) % int(slots_.size());
+  for (int k = 0; k < n; ++k) {
+    const int c = (next_ + k) % n;
+    if ((n == 1 || c != latest_.load()) && !(slots_[c]->version.load() & 1)) {
+      s = c;
+      break;
+    }
   }
+  next_ = (s + 1) % n;
   slots_[s]->version.fetch_add(1, std::memory_order_acq_rel);  // odd: being written
   return s;
 }
@@ -234,10 +239,15 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (dev_.gpu()) {
     dev_.bind();
     VEP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    VEP_HIP(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
     VEP_HIP(hipStreamCreateWithFlags(&serve_stream_, hipStreamNonBlocking));
-    VEP_HIP(hipEventCreate(&ev0_));
-    VEP_HIP(hipEventCreate(&ev1_));
+    for (Stage& st : stage_) {
+      VEP_HIP(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
+      VEP_HIP(hipEventCreate(&st.e0));
+      VEP_HIP(hipEventCreate(&st.e1));
+    }
   }
+  if (opt_.pack_threads > 0) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads);
   cams_.reserve(size_t(opt_.max_cameras));
   if (opt_.letterbox_size > 0) {
     const size_t S = size_t(opt_.letterbox_size);
@@ -264,6 +274,10 @@ void Worker::set_consumer_buffers(u8* hwc, void* chw, int rows) {
 
 Worker::~Worker() {
   stop();
+  try {
+    complete_all();
+  } catch (...) {
+  }
   std::lock_guard<std::mutex> g(cams_mu_);
   for (auto& c : cams_) {
     if (!c) continue;
@@ -275,13 +289,17 @@ Worker::~Worker() {
     dev_.free(cons_hwc_);
     dev_.free(cons_chw_);
   }
-  dev_.free(d_stage_);
-  dev_.free_pinned(h_stage_);
+  for (Stage& st : stage_) {
+    dev_.free(st.d);
+    dev_.free_pinned(st.h);
+    if (st.copied) (void)hipEventDestroy(st.copied);
+    if (st.e0) (void)hipEventDestroy(st.e0);
+    if (st.e1) (void)hipEventDestroy(st.e1);
+  }
   dev_.free_pinned(h_serve_);
   if (stream_) (void)hipStreamDestroy(stream_);
+  if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (serve_stream_) (void)hipStreamDestroy(serve_stream_);
-  if (ev0_) (void)hipEventDestroy(ev0_);
-  if (ev1_) (void)hipEventDestroy(ev1_);
 }
 
 int Worker::add_camera(const std::string& name, int ring_slots) {
@@ -296,12 +314,15 @@ int Worker::add_camera(const std::string& name, int ring_slots) {
     idx = int(cams_.size());
     cams_.emplace_back();
   }
-  cams_[size_t(idx)] = std::make_unique<Camera>(*this, idx, name, std::max(1, ring_slots));
+  // two batches may be in flight on the GPU: keep >= 3 slots so a committed frame stays readable
+  cams_[size_t(idx)] =
+      std::make_unique<Camera>(*this, idx, name, std::max(dev_.gpu() ? 3 : 1, ring_slots));
   return idx;
 }
 
 void Worker::remove_camera(int idx) {
   flush();
+  complete_all();
   std::lock_guard<std::mutex> lg(launch_mu_);
   std::lock_guard<std::mutex> g(cams_mu_);
   VEP_CHECK(idx >= 0 && idx < int(cams_.size()) && cams_[size_t(idx)], "no such camera");
@@ -385,9 +406,14 @@ void Worker::submit(DecodeJob&& job) {
 }
 
 void Worker::flush() {
-  std::unique_lock<std::mutex> g(q_mu_);
-  if (!running_) return;
-  idle_cv_.wait(g, [this] { return pending_.empty() && !busy_; });
+  {
+    std::unique_lock<std::mutex> g(q_mu_);
+    if (running_) {
+      idle_cv_.wait(g, [this] { return pending_.empty() && !busy_; });
+      return;
+    }
+  }
+  complete_all();
 }
 
 void Worker::loop() {
@@ -402,7 +428,7 @@ void Worker::loop() {
       busy_ = true;
     }
     try {
-      run_batch(batch);
+      launch_async(batch);
     } catch (const std::exception& e) {
       for (auto& j : batch)
         if (Camera* c = camera(j.cam)) {
@@ -413,9 +439,21 @@ void Worker::loop() {
     batch.clear();
     {
       std::lock_guard<std::mutex> g(q_mu_);
-      busy_ = false;
+      if (!pending_.empty()) continue;  // keep the pipeline two batches deep
+    }
+    try {
+      complete_all();
+    } catch (const std::exception&) {
+    }
+    {
+      std::lock_guard<std::mutex> g(q_mu_);
+      if (pending_.empty()) busy_ = false;
     }
     idle_cv_.notify_all();
+  }
+  try {
+    complete_all();
+  } catch (const std::exception&) {
   }
 }
 
@@ -492,17 +530,87 @@ static void cpu_letterbox(const HostSurface& s, const gpu::LetterboxDesc& d,
   }
 }
 
-void Worker::launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
+// Drop jobs of vanished cameras, (re)allocate surfaces/rings, reserve ring slots.
+void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
+  bool resize = false;
+  {
+    std::lock_guard<std::mutex> g(cams_mu_);
+    jobs.erase(std::remove_if(jobs.begin(), jobs.end(),
+                              [&](const DecodeJob& j) {
+                                return j.cam < 0 || j.cam >= int(cams_.size()) ||
+                                       !cams_[size_t(j.cam)];
+                              }),
+               jobs.end());
+    for (auto& j : jobs) {
+      Camera& c = *cams_[size_t(j.cam)];
+      const bool have = c.ring_ != nullptr;
+      if (have && (c.surface.wmbs * 16 != j.pic.coded_width ||
+                   c.surface.hmbs * 16 != j.pic.coded_height || c.ring_->width() != j.pic.width ||
+                   c.ring_->height() != j.pic.height))
+        resize = true;
+    }
+  }
+  if (resize) complete_locked();  // never free a surface an in-flight batch still writes
+  std::lock_guard<std::mutex> g(cams_mu_);
+  slots.resize(jobs.size());
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    Camera& c = *cams_[size_t(jobs[i].cam)];
+    ensure_surface(c, jobs[i].pic);
+    slots[i] = c.ring_->begin_write();
+  }
+}
+
+namespace {
+
+// Coded-MB bitmask + per-word exclusive prefix, payload packed in raster order.
+void pack_job(const MbUpdate& u, u32* mask, u32* prefix, u8* payload) {
+  const int mbs = u.mbs();
+  const int words = (mbs + 31) / 32;
+  const i32* slot = u.slot.data();
+  bool raster = true;  // slots assigned in raster order (no GOP collapse): one memcpy
+  int expect = 0;
+  u32 run = 0;
+  for (int w = 0; w < words; ++w) {
+    u32 m = 0;
+    const int lim = std::min(32, mbs - w * 32);
+    for (int b = 0; b < lim; ++b) {
+      const i32 s = slot[w * 32 + b];
+      if (s >= 0) {
+        m |= 1u << b;
+        raster &= (s == expect);
+        ++expect;
+      }
+    }
+    mask[w] = m;
+    prefix[w] = run;
+    run += u32(__builtin_popcount(m));
+  }
+  if (raster) {
+    std::memcpy(payload, u.payload.data(), size_t(u.nslots) * kPcmMbBytes);
+    return;
+  }
+  u8* o = payload;
+  for (int mb = 0; mb < mbs; ++mb) {
+    if (slot[mb] < 0) continue;
+    std::memcpy(o, u.payload.data() + size_t(slot[mb]) * kPcmMbBytes, kPcmMbBytes);
+    o += kPcmMbBytes;
+  }
+}
+
+}  // namespace
+
+void Worker::launch_gpu(Stage& st) {
+  std::vector<DecodeJob>& jobs = st.jobs;
   const int n = int(jobs.size());
-  // staging layout: [descs][letterbox descs][maps][payloads]
-  size_t off_desc = 0;
-  size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
-  size_t off_map = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
-  size_t need = off_map;
-  std::vector<size_t> map_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
+  // staging layout: [descs][letterbox descs][per job: mask, prefix][payloads]
+  const size_t off_desc = 0;
+  const size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
+  size_t need = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
+  std::vector<size_t> mask_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
   for (int i = 0; i < n; ++i) {
-    map_off[size_t(i)] = need;
-    need += al(sizeof(i32) * jobs[size_t(i)].upd.slot.size(), 16);
+    mask_off[size_t(i)] = need;
+    const size_t words = size_t(jobs[size_t(i)].upd.mbs() + 31) / 32;
+    need += 2 * al(words * sizeof(u32), 16);
   }
   need = al(need);
   for (int i = 0; i < n; ++i) {
@@ -510,28 +618,37 @@ void Worker::launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
     need += size_t(jobs[size_t(i)].upd.nslots) * kPcmMbBytes;
   }
   need = al(need);
-  if (need > stage_cap_) {
-    dev_.free(d_stage_);
-    dev_.free_pinned(h_stage_);
-    stage_cap_ = std::max(need + need / 2, size_t(1) << 20);
-    h_stage_ = static_cast<u8*>(dev_.alloc_pinned(stage_cap_));
-    d_stage_ = static_cast<u8*>(dev_.alloc(stage_cap_));
+  if (need > st.cap) {
+    dev_.free(st.d);
+    dev_.free_pinned(st.h);
+    st.cap = std::max(need + need / 2, size_t(4) << 20);
+    st.h = static_cast<u8*>(dev_.alloc_pinned(st.cap));
+    st.d = static_cast<u8*>(dev_.alloc(st.cap));
   }
-  auto* hd = reinterpret_cast<gpu::DecodeDesc*>(h_stage_ + off_desc);
-  auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(h_stage_ + off_lb);
+  auto pack = [&](int i) {
+    const DecodeJob& j = jobs[size_t(i)];
+    const size_t words = size_t(j.upd.mbs() + 31) / 32;
+    u32* m = reinterpret_cast<u32*>(st.h + mask_off[size_t(i)]);
+    u32* p = reinterpret_cast<u32*>(st.h + mask_off[size_t(i)] + al(words * sizeof(u32), 16));
+    pack_job(j.upd, m, p, st.h + pay_off[size_t(i)]);
+  };
+  if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, pack);
+  else for (int i = 0; i < n; ++i) pack(i);
+
+  auto* hd = reinterpret_cast<gpu::DecodeDesc*>(st.h + off_desc);
+  auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(st.h + off_lb);
   int tiles = 0;
   for (int i = 0; i < n; ++i) {
-    DecodeJob& j = jobs[size_t(i)];
+    const DecodeJob& j = jobs[size_t(i)];
     Camera* c = cams_[size_t(j.cam)].get();
-    std::memcpy(h_stage_ + map_off[size_t(i)], j.upd.slot.data(), sizeof(i32) * j.upd.slot.size());
-    std::memcpy(h_stage_ + pay_off[size_t(i)], j.upd.payload.data(),
-                size_t(j.upd.nslots) * kPcmMbBytes);
+    const size_t words = size_t(j.upd.mbs() + 31) / 32;
     gpu::DecodeDesc& d = hd[i];
     d.y = c->surface.y;
     d.uv = c->surface.uv;
-    d.bgr = c->ring_->slot_ptr(slots[size_t(i)]);
-    d.map = reinterpret_cast<const i32*>(d_stage_ + map_off[size_t(i)]);
-    d.payload = d_stage_ + pay_off[size_t(i)];
+    d.bgr = c->ring_->slot_ptr(st.slots[size_t(i)]);
+    d.mask = reinterpret_cast<const u32*>(st.d + mask_off[size_t(i)]);
+    d.prefix = reinterpret_cast<const u32*>(st.d + mask_off[size_t(i)] + al(words * sizeof(u32), 16));
+    d.payload = st.d + pay_off[size_t(i)];
     d.wmbs = j.upd.width_mbs;
     d.hmbs = j.upd.height_mbs;
     d.out_w = j.pic.width;
@@ -553,16 +670,19 @@ void Worker::launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       l.crop_top = j.pic.crop_top;
       VEP_CHECK(j.cam < cons_rows_, "camera index exceeds consumer batch rows");
       l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(j.cam) * S * S * 3 : nullptr;
-      size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
+      const size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
       l.out_chw = cons_chw_ ? static_cast<u8*>(cons_chw_) + size_t(j.cam) * 3 * S * S * es
                             : nullptr;
       gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
     }
   }
-  VEP_HIP(hipMemcpyAsync(d_stage_, h_stage_, need, hipMemcpyHostToDevice, stream_));
-  VEP_HIP(hipEventRecord(ev0_, stream_));
-  gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(d_stage_ + off_desc), n,
-                             tiles, stream_);
+  // H2D on the copy stream overlaps the previous batch's kernels on the compute stream
+  VEP_HIP(hipMemcpyAsync(st.d, st.h, need, hipMemcpyHostToDevice, copy_stream_));
+  VEP_HIP(hipEventRecord(st.copied, copy_stream_));
+  VEP_HIP(hipStreamWaitEvent(stream_, st.copied, 0));
+  VEP_HIP(hipEventRecord(st.e0, stream_));
+  gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), n, tiles,
+                             stream_);
   if (opt_.letterbox_size > 0) {
     gpu::LetterboxParams p{};
     p.size = opt_.letterbox_size;
@@ -572,80 +692,112 @@ void Worker::launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       p.inv_std[k] = 1.f / opt_.std[k];
     }
     p.pad_value = 114;
-    gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(d_stage_ + off_lb), n, p,
+    gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(st.d + off_lb), n, p,
                           stream_);
   }
-  VEP_HIP(hipEventRecord(ev1_, stream_));
-  VEP_HIP(hipEventSynchronize(ev1_));
-  float ms = 0;
-  VEP_HIP(hipEventElapsedTime(&ms, ev0_, ev1_));
-  gpu_ms_total_ += ms;
+  VEP_HIP(hipEventRecord(st.e1, stream_));
 }
 
-void Worker::run_batch(std::vector<DecodeJob>& jobs) {
-  if (jobs.empty()) return;
-  std::lock_guard<std::mutex> lg(launch_mu_);
-  dev_.bind();
-  std::vector<int> slots(jobs.size());
-  {
-    std::lock_guard<std::mutex> g(cams_mu_);
-    // drop jobs whose camera vanished
-    jobs.erase(std::remove_if(jobs.begin(), jobs.end(),
-                              [&](const DecodeJob& j) {
-                                return j.cam < 0 || j.cam >= int(cams_.size()) ||
-                                       !cams_[size_t(j.cam)];
-                              }),
-               jobs.end());
-    for (size_t i = 0; i < jobs.size(); ++i) {
-      Camera& c = *cams_[size_t(jobs[i].cam)];
-      ensure_surface(c, jobs[i].pic);
-      slots[i] = c.ring_->begin_write();
-    }
-  }
-  slots.resize(jobs.size());
-  if (jobs.empty()) return;
-  if (dev_.gpu()) {
-    launch(jobs, slots);
-  } else {
-    for (size_t i = 0; i < jobs.size(); ++i) {
-      Camera& c = *cams_[size_t(jobs[i].cam)];
-      cpu_apply_update(jobs[i].upd, c.surface.host);
-      cpu_nv12_to_bgr(c.surface.host, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
-                      jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
-      if (opt_.letterbox_size > 0) {
-        gpu::LetterboxDesc l{};
-        const size_t S = size_t(opt_.letterbox_size);
-        l.src_w = jobs[i].pic.width;
-        l.src_h = jobs[i].pic.height;
-        l.crop_left = jobs[i].pic.crop_left;
-        l.crop_top = jobs[i].pic.crop_top;
-        l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(jobs[i].cam) * S * S * 3 : nullptr;
-        l.out_chw = (cons_chw_ && opt_.chw_dtype == gpu::kChwF32)
-                        ? static_cast<u8*>(cons_chw_) + size_t(jobs[i].cam) * 3 * S * S * 4
-                        : nullptr;
-        gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
-        gpu::LetterboxParams p{};
-        p.size = opt_.letterbox_size;
-        p.chw_dtype = opt_.chw_dtype;
-        for (int k = 0; k < 3; ++k) {
-          p.mean[k] = opt_.mean[k];
-          p.inv_std[k] = 1.f / opt_.std[k];
-        }
-        p.pad_value = 114;
-        cpu_letterbox(c.surface.host, l, p);
+void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    Camera& c = *cams_[size_t(jobs[i].cam)];
+    cpu_apply_update(jobs[i].upd, c.surface.host);
+    cpu_nv12_to_bgr(c.surface.host, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
+                    jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
+    if (opt_.letterbox_size > 0) {
+      gpu::LetterboxDesc l{};
+      const size_t S = size_t(opt_.letterbox_size);
+      l.src_w = jobs[i].pic.width;
+      l.src_h = jobs[i].pic.height;
+      l.crop_left = jobs[i].pic.crop_left;
+      l.crop_top = jobs[i].pic.crop_top;
+      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(jobs[i].cam) * S * S * 3 : nullptr;
+      l.out_chw = (cons_chw_ && opt_.chw_dtype == gpu::kChwF32)
+                      ? static_cast<u8*>(cons_chw_) + size_t(jobs[i].cam) * 3 * S * S * 4
+                      : nullptr;
+      gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
+      gpu::LetterboxParams p{};
+      p.size = opt_.letterbox_size;
+      p.chw_dtype = opt_.chw_dtype;
+      for (int k = 0; k < 3; ++k) {
+        p.mean[k] = opt_.mean[k];
+        p.inv_std[k] = 1.f / opt_.std[k];
       }
+      p.pad_value = 114;
+      cpu_letterbox(c.surface.host, l, p);
     }
   }
+}
+
+void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
   const i64 t = mono_us();
   std::lock_guard<std::mutex> g(cams_mu_);
   for (size_t i = 0; i < jobs.size(); ++i) {
-    Camera& c = *cams_[size_t(jobs[i].cam)];
+    auto& cp = cams_[size_t(jobs[i].cam)];
+    if (!cp || !cp->ring_) continue;
     jobs[i].meta.decoded_us = t;
-    c.ring_->commit(slots[i], jobs[i].meta);
-    c.decoded.fetch_add(1, std::memory_order_relaxed);
+    cp->ring_->commit(slots[i], jobs[i].meta);
+    cp->decoded.fetch_add(1, std::memory_order_relaxed);
   }
   frames_.fetch_add(jobs.size());
   batches_.fetch_add(1);
+}
+
+void Worker::complete(Stage& st) {
+  if (!st.active) return;
+  st.active = false;
+  VEP_HIP(hipEventSynchronize(st.e1));
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) gpu_ms_total_ += ms;
+  publish(st.jobs, st.slots);
+  st.jobs.clear();
+  st.slots.clear();
+}
+
+void Worker::complete_locked() {
+  // oldest first: next_stage_ names the stage that will be reused next, i.e. the older batch
+  complete(stage_[next_stage_]);
+  complete(stage_[next_stage_ ^ 1]);
+}
+
+void Worker::complete_all() {
+  std::lock_guard<std::mutex> lg(launch_mu_);
+  if (dev_.gpu()) dev_.bind();
+  complete_locked();
+}
+
+void Worker::launch_async(std::vector<DecodeJob>& jobs) {
+  if (jobs.empty()) return;
+  std::lock_guard<std::mutex> lg(launch_mu_);
+  dev_.bind();
+  std::vector<int> slots;
+  prepare(jobs, slots);
+  if (jobs.empty()) return;
+  if (!dev_.gpu()) {
+    run_cpu(jobs, slots);
+    publish(jobs, slots);
+    jobs.clear();
+    return;
+  }
+  Stage& st = stage_[next_stage_];
+  next_stage_ ^= 1;
+  complete(st);  // the batch from two launches ago: its staging buffer is reused now
+  st.jobs.swap(jobs);
+  st.slots.swap(slots);
+  jobs.clear();
+  try {
+    launch_gpu(st);
+  } catch (...) {
+    st.jobs.clear();
+    st.slots.clear();
+    throw;
+  }
+  st.active = true;
+}
+
+void Worker::run_batch(std::vector<DecodeJob>& jobs) {
+  launch_async(jobs);
+  complete_all();
 }
 
 bool Worker::read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap) {

@@ -19,6 +19,7 @@
 
 #include "codec.h"
 #include "gpu.h"
+#include "pool.h"
 
 namespace vep {
 
@@ -171,6 +172,7 @@ struct WorkerOptions {
   float mean[3] = {0.f, 0.f, 0.f};
   float std[3] = {1.f, 1.f, 1.f};
   int max_cameras = 256;
+  int pack_threads = 4;       // host threads packing MB payloads into pinned staging
 };
 
 class Worker {
@@ -193,6 +195,12 @@ class Worker {
 
   // Synchronous batched decode (bench / tests). Jobs are consumed.
   void run_batch(std::vector<DecodeJob>& jobs);
+  // Asynchronous pipeline (two batches in flight, double-buffered staging, H2D on a copy
+  // stream overlapping the previous batch's kernels). launch_async returns once the batch is
+  // enqueued; its frames are published by a later launch_async (when its staging buffer is
+  // reused) or by complete_all().
+  void launch_async(std::vector<DecodeJob>& jobs);
+  void complete_all();
   // Wait until every submitted job is published.
   void flush();
 
@@ -211,19 +219,31 @@ class Worker {
   double gpu_ms_total() const { return gpu_ms_total_; }
 
  private:
+  struct Stage {  // one pinned + device staging pair and the batch that uses it
+    u8* h = nullptr;
+    u8* d = nullptr;
+    size_t cap = 0;
+    hipEvent_t copied = nullptr, e0 = nullptr, e1 = nullptr;
+    std::vector<DecodeJob> jobs;
+    std::vector<int> slots;
+    bool active = false;
+  };
   void loop();
   void ensure_surface(Camera& c, const PictureInfo& pi);
-  void launch(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
+  void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
+  void launch_gpu(Stage& st);
+  void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
+  void publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
+  void complete(Stage& st);
+  void complete_locked();
   WorkerOptions opt_;
   Device dev_;
-  hipStream_t stream_ = nullptr, serve_stream_ = nullptr;
-  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  hipStream_t stream_ = nullptr, copy_stream_ = nullptr, serve_stream_ = nullptr;
   mutable std::mutex cams_mu_;
   std::vector<std::unique_ptr<Camera>> cams_;
-  // staging
-  u8* h_stage_ = nullptr;
-  u8* d_stage_ = nullptr;
-  size_t stage_cap_ = 0;
+  Stage stage_[2];
+  int next_stage_ = 0;
+  std::unique_ptr<ThreadPool> pack_pool_;
   u8* h_serve_ = nullptr;
   size_t serve_cap_ = 0;
   std::mutex serve_mu_;

@@ -156,7 +156,9 @@ std::vector<u8> SynthH264::encode_slice(bool idr, int mb0, int mb1,
 
 std::shared_ptr<AccessUnit> SynthH264::next() {
   ++frame_;
-  const bool idr = (frame_ % cfg_.gop) == 0;
+  // frame 0 is always an IDR; later IDRs fall where (frame + phase) % gop == 0 so that a fleet
+  // of cameras does not refresh in lock-step
+  const bool idr = frame_ == 0 || ((frame_ + cfg_.idr_phase) % cfg_.gop) == 0;
   auto au = std::make_shared<AccessUnit>();
   au->codec = Codec::kH264;
   au->pts = au->dts = frame_ * 90000 / cfg_.fps;

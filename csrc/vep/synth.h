@@ -18,6 +18,7 @@ struct SynthConfig {
   u64 seed = 1;
   int slices = 1;          // slices per picture (MB-row aligned)
   bool zero_samples = false;  // allow 0x00 PCM samples (forces emulation-prevention bytes)
+  int idr_phase = 0;       // GOP phase offset (IDR when (frame + phase) % gop == 0, and frame 0)
 };
 
 class SynthH264 {

@@ -47,9 +47,26 @@ def nv12_to_bgr(y: torch.Tensor, uv: torch.Tensor, width: int | None = None,
     if out is None:
         out = torch.empty((height, width, 3), dtype=torch.uint8, device=y.device)
     assert out.is_contiguous() and tuple(out.shape) == (height, width, 3)
-    native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), 0, 0, W // 16, H // 16, width, height,
+    native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), 0, 0, 0, W // 16, H // 16, width, height,
                        crop_left, crop_top, out.data_ptr(), _stream_ptr(y))
     return out
+
+
+def mb_mask_prefix(mb_slot: torch.Tensor):
+    """Dense per-MB slot map -> (coded-MB bitmask words, exclusive per-word popcount prefix,
+    raster-order permutation of the payload slots) — the compact form the kernel consumes."""
+    s = mb_slot.detach().to("cpu", torch.int64)
+    n = s.numel()
+    words = (n + 31) // 32
+    coded = torch.zeros(words * 32, dtype=torch.int64)
+    coded[:n] = (s >= 0).to(torch.int64)
+    bits = coded.view(words, 32) << torch.arange(32, dtype=torch.int64)
+    mask = bits.sum(1)
+    counts = coded.view(words, 32).sum(1)
+    prefix = torch.cumsum(counts, 0) - counts
+    order = s[s >= 0]
+    to_i32 = lambda t: torch.where(t >= 2**31, t - 2**32, t).to(torch.int32)
+    return to_i32(mask), prefix.to(torch.int32), order
 
 
 def pcm_decode_bgr(y: torch.Tensor, uv: torch.Tensor, mb_slot: torch.Tensor,
@@ -68,9 +85,14 @@ def pcm_decode_bgr(y: torch.Tensor, uv: torch.Tensor, mb_slot: torch.Tensor,
         raise ValueError("mb_slot references a payload slot out of range")
     width = W if width is None else width
     height = H if height is None else height
+    mask, prefix, order = mb_mask_prefix(mb_slot)
+    slots = payload.view(-1, 384)[order.to(payload.device)].contiguous()
+    mask, prefix = mask.to(y.device), prefix.to(y.device)
     out = torch.empty((height, width, 3), dtype=torch.uint8, device=y.device)
-    native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), mb_slot.data_ptr(), payload.data_ptr(),
-                       W // 16, H // 16, width, height, 0, 0, out.data_ptr(), _stream_ptr(y))
+    native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), mask.data_ptr(), prefix.data_ptr(),
+                       slots.data_ptr(), W // 16, H // 16, width, height, 0, 0, out.data_ptr(),
+                       _stream_ptr(y))
+    torch.cuda.current_stream(y.device).synchronize()  # host-built index tensors go out of scope
     return out
 
 

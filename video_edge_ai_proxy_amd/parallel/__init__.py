@@ -104,7 +104,8 @@ class ConsumerBatch:
         return self.bufs[b]
 
     def gather(self, async_op: bool = True):
-        """All-gather the tick's batch (after the worker published it). Returns (tensor, work)."""
+        """All-gather the tick's batch. Returns (tensor, work)."""
+        self.worker.complete_all()  # the tick's letterbox kernels must have finished
         b = self.tick & 1
         self.tick += 1
         if self.world == 1:
