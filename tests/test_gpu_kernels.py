@@ -132,6 +132,7 @@ def test_replay_bench_runs(native):
     rb = native.ReplayBench(wk, 8, cfg, cached_frames=10, threads=4)
     for _ in range(12):
         rb.step()
+    rb.drain()  # two ticks stay in flight until drained
     assert rb.frames == 96
     for c in rb.cameras:
         st = wk.stats(c)
