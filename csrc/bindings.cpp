@@ -65,9 +65,7 @@ struct CpuDecoder {
   HostSurface surf;
   PictureInfo last;
   py::object decode(const AccessUnit& au) {
-    upd.slot.assign(upd.slot.size(), -1);
-    upd.nslots = 0;
-    upd.payload.clear();
+    upd.clear_payload();  // `au` outlives this call: src pointers into it are safe
     last = parser.parse(au, upd);
     if (surf.coded_w != last.coded_width || surf.coded_h != last.coded_height)
       surf.alloc(last.coded_width, last.coded_height);

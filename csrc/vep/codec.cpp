@@ -57,9 +57,29 @@ void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, Bit
   const bool is_i = (st == kI);
   VEP_CHECK(is_i || st == kP, "only I and P slices are supported by the native decoder");
   const u32 pcm_type = is_i ? 25u : 30u;  // I_PCM (Table 7-11) / offset by 5 in P slices
+  // Byte-aligned fast path: after a PCM macroblock the reader is byte aligned, and the next
+  // macroblock header is a fixed 2-byte pattern — I slice: ue(25) + 7 alignment zeros = 0D 00;
+  // P slice: ue(0) skip run + ue(30) + 6 zeros = 87 C0. Peeking two bytes replaces the bit-level
+  // Exp-Golomb walk for the common case; anything else takes the general path below.
+  const u8 f0 = is_i ? 0x0D : 0x87, f1 = is_i ? 0x00 : 0xC0;
+  const u8* base = br.data();
+  const size_t nbytes = br.size();
   int mb = sh.first_mb;
   bool more = true;
   do {
+    if (br.byte_aligned()) {
+      size_t off = br.bytepos();
+      while (off + 2 + kPcmMbBytes <= nbytes && base[off] == f0 && base[off + 1] == f1 &&
+             (off + 2) * 8 < stop) {
+        VEP_CHECK(mb < total, "macroblock address past end of picture");
+        upd.set(mb, base + off + 2);
+        ++coded;
+        ++mb;
+        off += 2 + kPcmMbBytes;
+      }
+      br.seek_byte(off);
+      if (br.bitpos() >= stop) break;
+    }
     int run = 0;
     if (!is_i) {
       run = int(br.ue());
@@ -76,7 +96,7 @@ void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, Bit
       br.align();
       size_t off = br.bytepos();
       VEP_CHECK(off + kPcmMbBytes <= br.size(), "truncated PCM macroblock");
-      std::memcpy(upd.slot_for(mb), br.data() + off, kPcmMbBytes);
+      upd.set(mb, base + off);
       br.skip(kPcmMbBytes * 8);
       ++coded;
     }
@@ -110,6 +130,13 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
     if (t != kNalSlice && t != kNalIdr) continue;
     size_t rn;
     const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn);
+    std::shared_ptr<std::vector<u8>> owned;
+    if (r != p) {
+      // emulation-prevention bytes present: the MB samples are referenced from an owned
+      // unescaped copy (kept alive by the update) instead of the shared parser scratch
+      owned = std::make_shared<std::vector<u8>>(r, r + rn);
+      r = owned->data();
+    }
     BitReader br(r + 1, rn - 1);
     // peek pps id to locate parameter sets
     BitReader peek(r + 1, rn - 1);
@@ -141,9 +168,8 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
       if (upd.width_mbs != sps.width_mbs || upd.height_mbs != sps.height_mbs())
         upd.reset(sps.width_mbs, sps.height_mbs());
       got_slice = true;
-    } else if (sh.pict_char() == 'I' && pi.pict_type == 'P') {
-      // mixed-slice picture: PyAV reports the first slice's type; keep it
-    }
+    }  // mixed-slice pictures report the first slice's type, as PyAV's pict_type does
+    if (owned) upd.own.push_back(owned);
     walk_slice(r, rn, sh, br, sps, upd, pi.coded_mbs);
   }
   VEP_CHECK(got_slice, "access unit has no slice");
@@ -157,7 +183,7 @@ void cpu_apply_update(const MbUpdate& upd, HostSurface& s) {
   for (int mb = 0; mb < upd.mbs(); ++mb) {
     int sl = upd.slot[mb];
     if (sl < 0) continue;
-    const u8* src = upd.payload.data() + size_t(sl) * kPcmMbBytes;
+    const u8* src = upd.block(sl);
     int mx = mb % W, my = mb / W;
     for (int r = 0; r < 16; ++r)
       std::memcpy(&s.y[size_t(my * 16 + r) * s.coded_w + mx * 16], src + r * 16, 16);

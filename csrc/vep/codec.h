@@ -49,29 +49,40 @@ using AuPtr = std::shared_ptr<const AccessUnit>;
 // (read_image.py:80-85) becomes a single batched GPU launch.
 struct MbUpdate {
   int width_mbs = 0, height_mbs = 0;
-  std::vector<i32> slot;   // per MB: payload slot or -1 (keep reference sample)
-  AlignedBuf payload;      // nslots * 384 B, 16-B aligned slots
+  std::vector<i32> slot;          // per MB: payload slot or -1 (keep reference sample)
+  std::vector<const u8*> src;     // per slot: the MB's 384 sample bytes, *in place* in the AU
+                                  // bitstream (no parse-time copy) or in an unescaped RBSP
+  std::vector<AuPtr> keep;        // AUs that `src` points into
+  std::vector<std::shared_ptr<const std::vector<u8>>> own;  // unescaped RBSPs `src` points into
   int nslots = 0;
-  int frames = 0;          // AUs folded in
+  int frames = 0;                 // AUs folded in
 
   void reset(int wmbs, int hmbs) {
     width_mbs = wmbs;
     height_mbs = hmbs;
     slot.assign(size_t(wmbs) * hmbs, -1);
-    payload.clear();
+    clear_payload();
+  }
+  void clear_payload() {
+    std::fill(slot.begin(), slot.end(), -1);
+    src.clear();
+    keep.clear();
+    own.clear();
     nslots = 0;
     frames = 0;
   }
   int mbs() const { return width_mbs * height_mbs; }
-  u8* slot_for(int mb) {
-    int s = slot[mb];
+  // Latest writer wins: a MB coded again later in a collapsed GOP re-points its slot.
+  void set(int mb, const u8* p) {
+    int s = slot[size_t(mb)];
     if (s < 0) {
-      s = nslots++;
-      slot[mb] = s;
-      payload.resize(size_t(nslots) * kPcmMbBytes);
+      slot[size_t(mb)] = nslots++;
+      src.push_back(p);
+    } else {
+      src[size_t(s)] = p;
     }
-    return payload.data() + size_t(s) * kPcmMbBytes;
   }
+  const u8* block(int s) const { return src[size_t(s)]; }
 };
 
 // Picture-level metadata produced by the parser (fills VideoFrame fields).
@@ -94,8 +105,9 @@ class UnsupportedStream : public Error {
 // Stateful H.264 AU parser (keeps SPS/PPS tables across AUs).
 class H264Parser {
  public:
-  // Parse one AU; macroblock updates are folded into `upd` (which must be sized for the
-  // stream, see need_reset()). Throws UnsupportedStream for syntax outside the subset.
+  // Parse one AU; macroblock updates are folded into `upd` (resized to the stream when
+  // needed). `upd.src` points into `au`'s bytes: the caller keeps the AU alive (upd.keep).
+  // Throws UnsupportedStream for syntax outside the subset.
   PictureInfo parse(const AccessUnit& au, MbUpdate& upd);
   // Parameter sets only (no slice walk) — cheap keyframe/size probe.
   void absorb_parameter_sets(const AccessUnit& au);

@@ -153,6 +153,7 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
   try {
     for (size_t i = from; i < to; ++i) {
       job.pic = parser_.parse(*gop_[i], job.upd);
+      job.upd.keep.push_back(gop_[i]);  // MB samples are referenced in place
       last = gop_[i].get();
     }
   } catch (const std::exception& e) {
@@ -378,8 +379,10 @@ static void fold_update(MbUpdate& into, const MbUpdate& from) {
   for (int mb = 0; mb < from.mbs(); ++mb) {
     int s = from.slot[size_t(mb)];
     if (s < 0) continue;
-    std::memcpy(into.slot_for(mb), from.payload.data() + size_t(s) * kPcmMbBytes, kPcmMbBytes);
+    into.set(mb, from.block(s));
   }
+  into.keep.insert(into.keep.end(), from.keep.begin(), from.keep.end());
+  into.own.insert(into.own.end(), from.own.begin(), from.own.end());
   into.frames += from.frames;
 }
 
@@ -562,13 +565,11 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
 
 namespace {
 
-// Coded-MB bitmask + per-word exclusive prefix, payload packed in raster order.
-void pack_job(const MbUpdate& u, u32* mask, u32* prefix, u8* payload) {
+// Coded-MB bitmask + per-word exclusive prefix, and the raster-order list of sample blocks.
+void build_index(const MbUpdate& u, u32* mask, u32* prefix, const u8** order) {
   const int mbs = u.mbs();
   const int words = (mbs + 31) / 32;
   const i32* slot = u.slot.data();
-  bool raster = true;  // slots assigned in raster order (no GOP collapse): one memcpy
-  int expect = 0;
   u32 run = 0;
   for (int w = 0; w < words; ++w) {
     u32 m = 0;
@@ -577,25 +578,16 @@ void pack_job(const MbUpdate& u, u32* mask, u32* prefix, u8* payload) {
       const i32 s = slot[w * 32 + b];
       if (s >= 0) {
         m |= 1u << b;
-        raster &= (s == expect);
-        ++expect;
+        order[run + u32(__builtin_popcount(m)) - 1] = u.block(s);
       }
     }
     mask[w] = m;
     prefix[w] = run;
     run += u32(__builtin_popcount(m));
   }
-  if (raster) {
-    std::memcpy(payload, u.payload.data(), size_t(u.nslots) * kPcmMbBytes);
-    return;
-  }
-  u8* o = payload;
-  for (int mb = 0; mb < mbs; ++mb) {
-    if (slot[mb] < 0) continue;
-    std::memcpy(o, u.payload.data() + size_t(slot[mb]) * kPcmMbBytes, kPcmMbBytes);
-    o += kPcmMbBytes;
-  }
 }
+
+constexpr int kPackChunk = 1024;  // MB blocks per copy task (384 KiB)
 
 }  // namespace
 
@@ -625,15 +617,32 @@ void Worker::launch_gpu(Stage& st) {
     st.h = static_cast<u8*>(dev_.alloc_pinned(st.cap));
     st.d = static_cast<u8*>(dev_.alloc(st.cap));
   }
-  auto pack = [&](int i) {
+  // Phase 1 (per job): bitmask/prefix + raster-order block list. Phase 2 (chunked across the
+  // pack threads, so one IDR does not serialise on a single core): the only host copy of the
+  // samples, straight from the AU bitstream into pinned staging.
+  std::vector<std::vector<const u8*>> order(static_cast<size_t>(n));
+  auto index = [&](int i) {
     const DecodeJob& j = jobs[size_t(i)];
     const size_t words = size_t(j.upd.mbs() + 31) / 32;
     u32* m = reinterpret_cast<u32*>(st.h + mask_off[size_t(i)]);
     u32* p = reinterpret_cast<u32*>(st.h + mask_off[size_t(i)] + al(words * sizeof(u32), 16));
-    pack_job(j.upd, m, p, st.h + pay_off[size_t(i)]);
+    order[size_t(i)].resize(size_t(j.upd.nslots));
+    build_index(j.upd, m, p, order[size_t(i)].data());
   };
-  if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, pack);
-  else for (int i = 0; i < n; ++i) pack(i);
+  if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
+  else for (int i = 0; i < n; ++i) index(i);
+  std::vector<std::pair<int, int>> tasks;  // (job, first block)
+  for (int i = 0; i < n; ++i)
+    for (int b = 0; b < jobs[size_t(i)].upd.nslots; b += kPackChunk) tasks.emplace_back(i, b);
+  auto copy = [&](int t) {
+    const auto [i, b0] = tasks[size_t(t)];
+    const auto& ord = order[size_t(i)];
+    const int b1 = std::min<int>(int(ord.size()), b0 + kPackChunk);
+    u8* dst = st.h + pay_off[size_t(i)] + size_t(b0) * kPcmMbBytes;
+    for (int b = b0; b < b1; ++b, dst += kPcmMbBytes) std::memcpy(dst, ord[size_t(b)], kPcmMbBytes);
+  };
+  if (pack_pool_ && tasks.size() > 1) pack_pool_->parallel_for(int(tasks.size()), copy);
+  else for (int t = 0; t < int(tasks.size()); ++t) copy(t);
 
   auto* hd = reinterpret_cast<gpu::DecodeDesc*>(st.h + off_desc);
   auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(st.h + off_lb);
