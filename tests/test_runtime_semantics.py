@@ -1,0 +1,108 @@
+"""Lazy decode / keyframe-only / GOP catch-up / idle cutoff / frame ring (CPU backend).
+
+Reference semantics: python/rtsp_to_rtmp.py:94-160 and python/read_image.py:47-133."""
+import time
+
+import numpy as np
+import pytest
+
+from conftest import synth
+
+
+@pytest.fixture
+def live(native):
+    w = native.Worker(device=-1)
+    w.start()
+    yield w
+    w.stop()
+
+
+def _now():
+    return int(time.time() * 1000)
+
+
+def test_no_query_no_decode(native, live):
+    cam = live.add_camera("idle", 2)
+    enc = synth(native, 64, 48, gop=4)
+    for _ in range(6):
+        assert live.submit_au(cam, enc.next()) is False
+    live.flush()
+    st = live.stats(cam)
+    assert st["packets"] == 6 and st["decoded"] == 0 and st["published"] == 0
+
+
+def test_packets_before_first_keyframe_are_skipped(native, live):
+    cam = live.add_camera("late", 2)
+    enc = synth(native, 64, 48, gop=4)
+    aus = [enc.next() for _ in range(8)]
+    live.set_last_query(cam, _now())
+    for au in aus[1:4]:  # joined mid-GOP: P frames without their IDR
+        assert live.submit_au(cam, au) is False
+    assert live.stats(cam)["skipped"] == 3
+    assert live.submit_au(cam, aus[4])  # next IDR starts decoding
+    live.flush()
+    assert live.stats(cam)["decoded"] == 1
+
+
+def test_catch_up_reconstructs_current_frame(native, live):
+    """P frames that arrived while nobody was watching are folded into one GPU update when a
+    query arrives; the published picture equals a full sequential decode."""
+    cam = live.add_camera("catchup", 2)
+    enc = synth(native, 128, 96, gop=20, motion=0.2)
+    ref = native.CpuDecoder()
+    for _ in range(7):  # IDR + 6 P, no viewer
+        au = enc.next()
+        want = ref.decode(au)
+        live.submit_au(cam, au)
+    live.flush()
+    assert live.stats(cam)["decoded"] == 0
+    live.set_last_query(cam, _now())
+    au = enc.next()
+    want = ref.decode(au)
+    assert live.submit_au(cam, au)
+    live.flush()
+    meta, got = live.read_latest(cam, 0)
+    assert np.array_equal(got, want)
+    assert meta["packet"] == 7 and meta["frame_type"] == "P" and meta["keyframe"] == 1
+    assert live.stats(cam)["decoded"] == 1
+
+
+def test_keyframe_only_mode(native, live):
+    cam = live.add_camera("kf", 2)
+    live.set_keyframe_only(cam, True)
+    live.set_last_query(cam, _now())
+    enc = synth(native, 64, 48, gop=5)
+    types = []
+    for i in range(15):
+        live.submit_au(cam, enc.next())
+        live.flush()
+        r = live.read_latest(cam, 0)
+        if r:
+            types.append(r[0]["frame_type"])
+    assert live.stats(cam)["decoded"] == 3  # the three IDRs only
+    assert set(types) == {"I"}
+
+
+def test_idle_cutoff(native, live):
+    cam = live.add_camera("cut", 2)
+    enc = synth(native, 64, 48, gop=3)
+    live.set_last_query(cam, _now() - 11_000)  # last viewer left 11 s ago
+    for _ in range(3):
+        assert live.submit_au(cam, enc.next()) is False
+    live.set_idle_cutoff_ms(cam, 60_000)
+    assert live.submit_au(cam, enc.next())
+
+
+def test_ring_cursor_semantics(native):
+    w = native.Worker(device=-1)
+    cam = w.add_camera("ring", 3)
+    enc = synth(native, 64, 48, gop=10)
+    w.decode_now(cam, enc.next())
+    m1, _ = w.read_latest(cam, 0)
+    assert w.read_latest(cam, m1["seq"]) is None  # nothing newer than the cursor
+    assert w.wait_frame(cam, m1["seq"], 50) is False
+    w.decode_now(cam, enc.next())
+    assert w.wait_frame(cam, m1["seq"], 50) is True
+    m2, _ = w.read_latest(cam, m1["seq"])
+    assert m2["seq"] == m1["seq"] + 1 and m2["pts"] == 3000
+    assert w.published(cam) == 2
