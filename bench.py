@@ -43,6 +43,7 @@ def parse_args():
     ap.add_argument("--gop", type=int, default=30)
     ap.add_argument("--motion", type=float, default=0.05)
     ap.add_argument("--threads", type=int, default=8, help="host parse threads per rank")
+    ap.add_argument("--pack-threads", type=int, default=8, help="host staging-pack threads per rank")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--ring-slots", type=int, default=2)
@@ -82,7 +83,7 @@ def main():
     cams = a.cams_per_gpu
     S = a.letterbox
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
-                        max_cameras=cams)
+                        max_cameras=cams, pack_threads=a.pack_threads)
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
     cfg.seed = 1 + rank * 100003
@@ -137,6 +138,7 @@ def main():
         dist.barrier()
     sync()
     f0, p0, b0, g0 = rb.frames, rb.parse_ms, rb.batch_ms, worker.gpu_ms_total
+    tm0 = worker.timings()
     t0 = time.perf_counter()
     for i in range(a.steps):
         step(a.warmup + i)
@@ -147,6 +149,7 @@ def main():
     elapsed = t1 - t0
     frames = rb.frames - f0
     parse_ms, batch_ms, gpu_ms = rb.parse_ms - p0, rb.batch_ms - b0, worker.gpu_ms_total - g0
+    tm1 = worker.timings()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -209,6 +212,8 @@ def main():
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "rank0_launch_breakdown_ms_per_step": {
+                k: round((v - tm0[k]) / a.steps, 4) for k, v in tm1.items()},
         }
         print(json.dumps(res), flush=True)
     if world > 1:

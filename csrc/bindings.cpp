@@ -219,9 +219,10 @@ PYBIND11_MODULE(_vep, m) {
 
   py::class_<Worker>(m, "Worker")
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
-                       std::vector<float> stdv, int max_cameras) {
+                       std::vector<float> stdv, int max_cameras, int pack_threads) {
              WorkerOptions o;
              o.device = device;
+             o.pack_threads = pack_threads;
              o.letterbox_size = letterbox_size;
              o.chw_dtype = chw_dtype;
              for (int k = 0; k < 3; ++k) {
@@ -233,7 +234,7 @@ PYBIND11_MODULE(_vep, m) {
            }),
            py::arg("device") = 0, py::arg("letterbox_size") = 0, py::arg("chw_dtype") = 0,
            py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
-           py::arg("max_cameras") = 256)
+           py::arg("max_cameras") = 256, py::arg("pack_threads") = 4)
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def("add_camera", &Worker::add_camera, py::arg("name"), py::arg("ring_slots") = 2)
       .def("remove_camera", &Worker::remove_camera, py::call_guard<py::gil_scoped_release>())
@@ -372,6 +373,16 @@ PYBIND11_MODULE(_vep, m) {
         if (!c.ring() || !c.ring()->latest(0, &m, &slot)) return py::none();
         return py::make_tuple(slot, meta_dict(m));
       })
+      .def("timings",
+           [](Worker& w) {
+             py::dict d;
+             d["prepare_ms"] = w.timers.prepare / 1000.0;
+             d["index_ms"] = w.timers.index / 1000.0;
+             d["copy_ms"] = w.timers.copy / 1000.0;
+             d["enqueue_ms"] = w.timers.enqueue / 1000.0;
+             d["wait_ms"] = w.timers.wait / 1000.0;
+             return d;
+           })
       .def_property_readonly("batches", &Worker::batches)
       .def_property_readonly("frames", &Worker::frames)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)

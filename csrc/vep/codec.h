@@ -54,6 +54,7 @@ struct MbUpdate {
                                   // bitstream (no parse-time copy) or in an unescaped RBSP
   std::vector<AuPtr> keep;        // AUs that `src` points into
   std::vector<std::shared_ptr<const std::vector<u8>>> own;  // unescaped RBSPs `src` points into
+  std::vector<i32> coded;         // MBs with a slot, in first-coded order (raster per AU)
   int nslots = 0;
   int frames = 0;                 // AUs folded in
 
@@ -64,10 +65,15 @@ struct MbUpdate {
     clear_payload();
   }
   void clear_payload() {
-    std::fill(slot.begin(), slot.end(), -1);
+    if (coded.size() * 8 < slot.size()) {
+      for (i32 mb : coded) slot[size_t(mb)] = -1;  // sparse reset
+    } else {
+      std::fill(slot.begin(), slot.end(), -1);
+    }
     src.clear();
     keep.clear();
     own.clear();
+    coded.clear();
     nslots = 0;
     frames = 0;
   }
@@ -78,6 +84,7 @@ struct MbUpdate {
     if (s < 0) {
       slot[size_t(mb)] = nslots++;
       src.push_back(p);
+      coded.push_back(mb);
     } else {
       src[size_t(s)] = p;
     }

@@ -566,24 +566,26 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
 namespace {
 
 // Coded-MB bitmask + per-word exclusive prefix, and the raster-order list of sample blocks.
+// O(coded MBs), not O(picture MBs): a P frame touches a few hundred of 8,160 MBs.
 void build_index(const MbUpdate& u, u32* mask, u32* prefix, const u8** order) {
-  const int mbs = u.mbs();
-  const int words = (mbs + 31) / 32;
-  const i32* slot = u.slot.data();
+  const int words = (u.mbs() + 31) / 32;
+  std::memset(mask, 0, size_t(words) * sizeof(u32));
+  const std::vector<i32>* list = &u.coded;
+  std::vector<i32> sorted;
+  if (!std::is_sorted(u.coded.begin(), u.coded.end())) {  // GOP collapse re-ordered slots
+    sorted = u.coded;
+    std::sort(sorted.begin(), sorted.end());
+    list = &sorted;
+  }
+  size_t k = 0;
+  for (i32 mb : *list) {
+    mask[mb >> 5] |= 1u << (mb & 31);
+    order[k++] = u.block(u.slot[size_t(mb)]);
+  }
   u32 run = 0;
   for (int w = 0; w < words; ++w) {
-    u32 m = 0;
-    const int lim = std::min(32, mbs - w * 32);
-    for (int b = 0; b < lim; ++b) {
-      const i32 s = slot[w * 32 + b];
-      if (s >= 0) {
-        m |= 1u << b;
-        order[run + u32(__builtin_popcount(m)) - 1] = u.block(s);
-      }
-    }
-    mask[w] = m;
     prefix[w] = run;
-    run += u32(__builtin_popcount(m));
+    run += u32(__builtin_popcount(mask[w]));
   }
 }
 
@@ -629,8 +631,11 @@ void Worker::launch_gpu(Stage& st) {
     order[size_t(i)].resize(size_t(j.upd.nslots));
     build_index(j.upd, m, p, order[size_t(i)].data());
   };
+  const i64 t_index0 = mono_us();
   if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
   else for (int i = 0; i < n; ++i) index(i);
+  const i64 t_copy0 = mono_us();
+  timers.index += double(t_copy0 - t_index0);
   std::vector<std::pair<int, int>> tasks;  // (job, first block)
   for (int i = 0; i < n; ++i)
     for (int b = 0; b < jobs[size_t(i)].upd.nslots; b += kPackChunk) tasks.emplace_back(i, b);
@@ -643,6 +648,8 @@ void Worker::launch_gpu(Stage& st) {
   };
   if (pack_pool_ && tasks.size() > 1) pack_pool_->parallel_for(int(tasks.size()), copy);
   else for (int t = 0; t < int(tasks.size()); ++t) copy(t);
+  const i64 t_enq0 = mono_us();
+  timers.copy += double(t_enq0 - t_copy0);
 
   auto* hd = reinterpret_cast<gpu::DecodeDesc*>(st.h + off_desc);
   auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(st.h + off_lb);
@@ -705,6 +712,7 @@ void Worker::launch_gpu(Stage& st) {
                           stream_);
   }
   VEP_HIP(hipEventRecord(st.e1, stream_));
+  timers.enqueue += double(mono_us() - t_enq0);
 }
 
 void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
@@ -755,7 +763,9 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
 void Worker::complete(Stage& st) {
   if (!st.active) return;
   st.active = false;
+  const i64 t0 = mono_us();
   VEP_HIP(hipEventSynchronize(st.e1));
+  timers.wait += double(mono_us() - t0);
   float ms = 0;
   if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) gpu_ms_total_ += ms;
   publish(st.jobs, st.slots);
@@ -780,7 +790,9 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
   std::lock_guard<std::mutex> lg(launch_mu_);
   dev_.bind();
   std::vector<int> slots;
+  const i64 t0 = mono_us();
   prepare(jobs, slots);
+  timers.prepare += double(mono_us() - t0);
   if (jobs.empty()) return;
   if (!dev_.gpu()) {
     run_cpu(jobs, slots);

@@ -244,6 +244,14 @@ class Worker {
   Stage stage_[2];
   int next_stage_ = 0;
   std::unique_ptr<ThreadPool> pack_pool_;
+
+ public:
+  // host-side launch path timers (µs, cumulative): where a batch's CPU time goes
+  struct Timers {
+    double prepare = 0, index = 0, copy = 0, enqueue = 0, wait = 0;
+  } timers;
+
+ private:
   u8* h_serve_ = nullptr;
   size_t serve_cap_ = 0;
   std::mutex serve_mu_;
