@@ -407,14 +407,15 @@ PYBIND11_MODULE(_vep, m) {
 
   // ---- op API on caller-owned device buffers (torch tensors pass data_ptr / stream) ----
   m.def("nv12_to_bgr",
-        [](uintptr_t y, uintptr_t uv, uintptr_t mask, uintptr_t prefix, uintptr_t payload, int wmbs,
-           int hmbs, int out_w, int out_h, int crop_left, int crop_top, uintptr_t out,
-           uintptr_t stream) {
+        [](uintptr_t y, uintptr_t uv, uintptr_t mask, uintptr_t prefix, uintptr_t offsets,
+           uintptr_t payload, int wmbs, int hmbs, int out_w, int out_h, int crop_left,
+           int crop_top, uintptr_t out, uintptr_t stream) {
           gpu::DecodeDesc d{};
           d.y = reinterpret_cast<u8*>(y);
           d.uv = reinterpret_cast<u8*>(uv);
           d.mask = reinterpret_cast<const u32*>(mask);
           d.prefix = reinterpret_cast<const u32*>(prefix);
+          d.offsets = reinterpret_cast<const u32*>(offsets);
           d.payload = reinterpret_cast<const u8*>(payload);
           d.bgr = reinterpret_cast<u8*>(out);
           d.wmbs = wmbs;

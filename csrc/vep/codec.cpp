@@ -170,6 +170,7 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
       got_slice = true;
     }  // mixed-slice pictures report the first slice's type, as PyAV's pict_type does
     if (owned) upd.own.push_back(owned);
+    upd.begin_segment(r, rn);
     walk_slice(r, rn, sh, br, sps, upd, pi.coded_mbs);
   }
   VEP_CHECK(got_slice, "access unit has no slice");

@@ -55,6 +55,14 @@ struct MbUpdate {
   std::vector<AuPtr> keep;        // AUs that `src` points into
   std::vector<std::shared_ptr<const std::vector<u8>>> own;  // unescaped RBSPs `src` points into
   std::vector<i32> coded;         // MBs with a slot, in first-coded order (raster per AU)
+  // Contiguous byte ranges (slice RBSPs) the blocks live in: the GPU path ships whole
+  // segments (one large copy each) plus a per-MB offset table instead of gathering blocks.
+  struct Segment {
+    const u8* base;
+    size_t len;
+  };
+  std::vector<Segment> segs;
+  std::vector<u32> slot_seg;      // per slot: index into segs
   int nslots = 0;
   int frames = 0;                 // AUs folded in
 
@@ -74,19 +82,26 @@ struct MbUpdate {
     keep.clear();
     own.clear();
     coded.clear();
+    segs.clear();
+    slot_seg.clear();
     nslots = 0;
     frames = 0;
   }
   int mbs() const { return width_mbs * height_mbs; }
+  void begin_segment(const u8* base, size_t len) { segs.push_back({base, len}); }
   // Latest writer wins: a MB coded again later in a collapsed GOP re-points its slot.
-  void set(int mb, const u8* p) {
+  // `p` must lie in the most recently begun segment.
+  void set(int mb, const u8* p) { set_in(mb, p, u32(segs.size() - 1)); }
+  void set_in(int mb, const u8* p, u32 seg) {
     int s = slot[size_t(mb)];
     if (s < 0) {
       slot[size_t(mb)] = nslots++;
       src.push_back(p);
+      slot_seg.push_back(seg);
       coded.push_back(mb);
     } else {
       src[size_t(s)] = p;
+      slot_seg[size_t(s)] = seg;
     }
   }
   const u8* block(int s) const { return src[size_t(s)]; }

@@ -35,7 +35,8 @@ struct DecodeDesc {
   // null mask = no update (pure conversion). 2 bits/MB of H2D instead of a 32-bit map.
   const u32* mask;
   const u32* prefix;
-  const u8* payload;  // 384-B PCM slots, raster order of the coded MBs
+  const u32* offsets;  // per coded MB (raster order): byte offset of its 384 samples in payload
+  const u8* payload;   // the slices' bytes as received (samples read in place, unaligned)
   i32 wmbs, hmbs;
   i32 out_w, out_h;
   i32 crop_left, crop_top;

@@ -74,10 +74,13 @@ __device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const i
   uint8_t* uvp = d.uv + size_t(mby * 8 + (row >> 1)) * pitch + mbx * 16;
   uint4 yv, uvv;
   if (slot >= 0) {
-    const uint8_t* src = d.payload + size_t(slot) * 384;
-    yv = *reinterpret_cast<const uint4*>(src + row * 16);
-    const uint2 cb = *reinterpret_cast<const uint2*>(src + 256 + (row >> 1) * 8);
-    const uint2 cr = *reinterpret_cast<const uint2*>(src + 320 + (row >> 1) * 8);
+    // samples are read in place from the slice bytes: 2-byte aligned in general (PCM blocks
+    // sit at a 386-byte stride after their header), so these are unaligned dwordx4/x2 loads
+    const uint8_t* src = d.payload + d.offsets[slot];
+    uint2 cb, cr;
+    __builtin_memcpy(&yv, src + row * 16, 16);
+    __builtin_memcpy(&cb, src + 256 + (row >> 1) * 8, 8);
+    __builtin_memcpy(&cr, src + 320 + (row >> 1) * 8, 8);
     // interleave Cb/Cr bytes: (cb0 cr0 cb1 cr1) ...
     uvv.x = __builtin_amdgcn_perm(cr.x, cb.x, 0x05010400u);
     uvv.y = __builtin_amdgcn_perm(cr.x, cb.x, 0x07030602u);

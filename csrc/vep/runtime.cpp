@@ -379,8 +379,9 @@ static void fold_update(MbUpdate& into, const MbUpdate& from) {
   for (int mb = 0; mb < from.mbs(); ++mb) {
     int s = from.slot[size_t(mb)];
     if (s < 0) continue;
-    into.set(mb, from.block(s));
+    into.set_in(mb, from.block(s), u32(into.segs.size()) + from.slot_seg[size_t(s)]);
   }
+  into.segs.insert(into.segs.end(), from.segs.begin(), from.segs.end());
   into.keep.insert(into.keep.end(), from.keep.begin(), from.keep.end());
   into.own.insert(into.own.end(), from.own.begin(), from.own.end());
   into.frames += from.frames;
@@ -567,7 +568,9 @@ namespace {
 
 // Coded-MB bitmask + per-word exclusive prefix, and the raster-order list of sample blocks.
 // O(coded MBs), not O(picture MBs): a P frame touches a few hundred of 8,160 MBs.
-void build_index(const MbUpdate& u, u32* mask, u32* prefix, const u8** order) {
+// seg_off[s] = staging byte offset (relative to the job's payload base) of segment s.
+void build_index(const MbUpdate& u, const std::vector<size_t>& seg_off, u32* mask, u32* prefix,
+                 u32* offsets) {
   const int words = (u.mbs() + 31) / 32;
   std::memset(mask, 0, size_t(words) * sizeof(u32));
   const std::vector<i32>* list = &u.coded;
@@ -580,7 +583,9 @@ void build_index(const MbUpdate& u, u32* mask, u32* prefix, const u8** order) {
   size_t k = 0;
   for (i32 mb : *list) {
     mask[mb >> 5] |= 1u << (mb & 31);
-    order[k++] = u.block(u.slot[size_t(mb)]);
+    const int s = u.slot[size_t(mb)];
+    const u32 g = u.slot_seg[size_t(s)];
+    offsets[k++] = u32(seg_off[g] + size_t(u.block(s) - u.segs[g].base));
   }
   u32 run = 0;
   for (int w = 0; w < words; ++w) {
@@ -589,27 +594,34 @@ void build_index(const MbUpdate& u, u32* mask, u32* prefix, const u8** order) {
   }
 }
 
-constexpr int kPackChunk = 1024;  // MB blocks per copy task (384 KiB)
+constexpr size_t kPackChunk = size_t(1) << 20;  // bytes per copy task
 
 }  // namespace
 
 void Worker::launch_gpu(Stage& st) {
   std::vector<DecodeJob>& jobs = st.jobs;
   const int n = int(jobs.size());
-  // staging layout: [descs][letterbox descs][per job: mask, prefix][payloads]
+  // staging layout: [descs][letterbox descs][per job: mask, prefix, offsets][per job: segments]
   const size_t off_desc = 0;
   const size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
   size_t need = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
   std::vector<size_t> mask_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
+  std::vector<std::vector<size_t>> seg_off(static_cast<size_t>(n));
+  auto words_of = [&](int i) { return size_t(jobs[size_t(i)].upd.mbs() + 31) / 32; };
   for (int i = 0; i < n; ++i) {
     mask_off[size_t(i)] = need;
-    const size_t words = size_t(jobs[size_t(i)].upd.mbs() + 31) / 32;
-    need += 2 * al(words * sizeof(u32), 16);
+    need += 2 * al(words_of(i) * sizeof(u32), 16) +
+            al(size_t(jobs[size_t(i)].upd.nslots) * sizeof(u32), 16);
   }
   need = al(need);
   for (int i = 0; i < n; ++i) {
     pay_off[size_t(i)] = need;
-    need += size_t(jobs[size_t(i)].upd.nslots) * kPcmMbBytes;
+    size_t rel = 0;
+    for (const auto& sg : jobs[size_t(i)].upd.segs) {
+      seg_off[size_t(i)].push_back(rel);
+      rel += al(sg.len, 16);
+    }
+    need += rel;
   }
   need = al(need);
   if (need > st.cap) {
@@ -619,33 +631,39 @@ void Worker::launch_gpu(Stage& st) {
     st.h = static_cast<u8*>(dev_.alloc_pinned(st.cap));
     st.d = static_cast<u8*>(dev_.alloc(st.cap));
   }
-  // Phase 1 (per job): bitmask/prefix + raster-order block list. Phase 2 (chunked across the
-  // pack threads, so one IDR does not serialise on a single core): the only host copy of the
-  // samples, straight from the AU bitstream into pinned staging.
-  std::vector<std::vector<const u8*>> order(static_cast<size_t>(n));
+  auto mask_ptr = [&](u8* base, int i) { return reinterpret_cast<u32*>(base + mask_off[size_t(i)]); };
+  auto prefix_ptr = [&](u8* base, int i) {
+    return reinterpret_cast<u32*>(base + mask_off[size_t(i)] + al(words_of(i) * sizeof(u32), 16));
+  };
+  auto offsets_ptr = [&](u8* base, int i) {
+    return reinterpret_cast<u32*>(base + mask_off[size_t(i)] + 2 * al(words_of(i) * sizeof(u32), 16));
+  };
+  // Phase 1 (per job): bitmask/prefix + per-MB sample offsets. Phase 2 (1 MiB chunks across
+  // the pack threads): the slices' bytes are copied as received — one large memcpy per slice,
+  // the only host copy — and the kernel reads the PCM samples in place.
   auto index = [&](int i) {
-    const DecodeJob& j = jobs[size_t(i)];
-    const size_t words = size_t(j.upd.mbs() + 31) / 32;
-    u32* m = reinterpret_cast<u32*>(st.h + mask_off[size_t(i)]);
-    u32* p = reinterpret_cast<u32*>(st.h + mask_off[size_t(i)] + al(words * sizeof(u32), 16));
-    order[size_t(i)].resize(size_t(j.upd.nslots));
-    build_index(j.upd, m, p, order[size_t(i)].data());
+    build_index(jobs[size_t(i)].upd, seg_off[size_t(i)], mask_ptr(st.h, i), prefix_ptr(st.h, i),
+                offsets_ptr(st.h, i));
   };
   const i64 t_index0 = mono_us();
   if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
   else for (int i = 0; i < n; ++i) index(i);
   const i64 t_copy0 = mono_us();
   timers.index += double(t_copy0 - t_index0);
-  std::vector<std::pair<int, int>> tasks;  // (job, first block)
-  for (int i = 0; i < n; ++i)
-    for (int b = 0; b < jobs[size_t(i)].upd.nslots; b += kPackChunk) tasks.emplace_back(i, b);
-  auto copy = [&](int t) {
-    const auto [i, b0] = tasks[size_t(t)];
-    const auto& ord = order[size_t(i)];
-    const int b1 = std::min<int>(int(ord.size()), b0 + kPackChunk);
-    u8* dst = st.h + pay_off[size_t(i)] + size_t(b0) * kPcmMbBytes;
-    for (int b = b0; b < b1; ++b, dst += kPcmMbBytes) std::memcpy(dst, ord[size_t(b)], kPcmMbBytes);
+  struct CopyTask {
+    const u8* src;
+    u8* dst;
+    size_t len;
   };
+  std::vector<CopyTask> tasks;
+  for (int i = 0; i < n; ++i) {
+    const auto& segs = jobs[size_t(i)].upd.segs;
+    for (size_t g = 0; g < segs.size(); ++g)
+      for (size_t o = 0; o < segs[g].len; o += kPackChunk)
+        tasks.push_back({segs[g].base + o, st.h + pay_off[size_t(i)] + seg_off[size_t(i)][g] + o,
+                         std::min(kPackChunk, segs[g].len - o)});
+  }
+  auto copy = [&](int t) { std::memcpy(tasks[size_t(t)].dst, tasks[size_t(t)].src, tasks[size_t(t)].len); };
   if (pack_pool_ && tasks.size() > 1) pack_pool_->parallel_for(int(tasks.size()), copy);
   else for (int t = 0; t < int(tasks.size()); ++t) copy(t);
   const i64 t_enq0 = mono_us();
@@ -662,8 +680,10 @@ void Worker::launch_gpu(Stage& st) {
     d.y = c->surface.y;
     d.uv = c->surface.uv;
     d.bgr = c->ring_->slot_ptr(st.slots[size_t(i)]);
-    d.mask = reinterpret_cast<const u32*>(st.d + mask_off[size_t(i)]);
-    d.prefix = reinterpret_cast<const u32*>(st.d + mask_off[size_t(i)] + al(words * sizeof(u32), 16));
+    (void)words;
+    d.mask = mask_ptr(st.d, i);
+    d.prefix = prefix_ptr(st.d, i);
+    d.offsets = offsets_ptr(st.d, i);
     d.payload = st.d + pay_off[size_t(i)];
     d.wmbs = j.upd.width_mbs;
     d.hmbs = j.upd.height_mbs;

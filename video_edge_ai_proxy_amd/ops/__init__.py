@@ -47,8 +47,8 @@ def nv12_to_bgr(y: torch.Tensor, uv: torch.Tensor, width: int | None = None,
     if out is None:
         out = torch.empty((height, width, 3), dtype=torch.uint8, device=y.device)
     assert out.is_contiguous() and tuple(out.shape) == (height, width, 3)
-    native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), 0, 0, 0, W // 16, H // 16, width, height,
-                       crop_left, crop_top, out.data_ptr(), _stream_ptr(y))
+    native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), 0, 0, 0, 0, W // 16, H // 16, width,
+                       height, crop_left, crop_top, out.data_ptr(), _stream_ptr(y))
     return out
 
 
@@ -86,12 +86,13 @@ def pcm_decode_bgr(y: torch.Tensor, uv: torch.Tensor, mb_slot: torch.Tensor,
     width = W if width is None else width
     height = H if height is None else height
     mask, prefix, order = mb_mask_prefix(mb_slot)
-    slots = payload.view(-1, 384)[order.to(payload.device)].contiguous()
+    offsets = (order * 384).to(torch.int32).to(y.device)  # samples read in place from payload
     mask, prefix = mask.to(y.device), prefix.to(y.device)
+    payload = payload.to(y.device).contiguous()
     out = torch.empty((height, width, 3), dtype=torch.uint8, device=y.device)
     native.nv12_to_bgr(y.data_ptr(), uv.data_ptr(), mask.data_ptr(), prefix.data_ptr(),
-                       slots.data_ptr(), W // 16, H // 16, width, height, 0, 0, out.data_ptr(),
-                       _stream_ptr(y))
+                       offsets.data_ptr(), payload.data_ptr(), W // 16, H // 16, width, height,
+                       0, 0, out.data_ptr(), _stream_ptr(y))
     torch.cuda.current_stream(y.device).synchronize()  # host-built index tensors go out of scope
     return out
 
