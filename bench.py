@@ -46,6 +46,8 @@ def parse_args():
     ap.add_argument("--pack-threads", type=int, default=8, help="host staging-pack threads per rank")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
+    ap.add_argument("--consumer-format", choices=["nv12", "bgr"], default="nv12",
+                    help="letterboxed consumer batch layout gathered over xGMI (nv12 = 1.5 B/px)")
     ap.add_argument("--ring-slots", type=int, default=2)
     ap.add_argument("--latency-samples", type=int, default=100)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (plumbing check, no GPU)")
@@ -83,7 +85,9 @@ def main():
     cams = a.cams_per_gpu
     S = a.letterbox
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
-                        max_cameras=cams, pack_threads=a.pack_threads)
+                        max_cameras=cams, pack_threads=a.pack_threads,
+                        letterbox_format=1 if a.consumer_format == "nv12" else 0)
+    row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
     cfg.seed = 1 + rank * 100003
@@ -93,9 +97,9 @@ def main():
     # The native worker keeps two ticks in flight (tick t's frames are published while tick
     # t+2 is being launched), and one all-gather may still be reading an older tick: 4 buffers.
     NB = 4
-    bufs = [torch.empty((cams, S, S, 3), dtype=torch.uint8, device=dev) for _ in range(NB)]
+    bufs = [torch.empty((cams, row), dtype=torch.uint8, device=dev) for _ in range(NB)]
     gather = world > 1 and not a.no_gather
-    gathered = [torch.empty((world * cams, S, S, 3), dtype=torch.uint8, device=dev)
+    gathered = [torch.empty((world * cams, row), dtype=torch.uint8, device=dev)
                 for _ in range(NB)] if gather else None
     handles = [None] * NB
     pending = []  # ticks launched whose consumer batch has not been handed to the gather yet
@@ -194,6 +198,8 @@ def main():
                 "parallelism": f"camera-dp{max(world, 1)}",
                 "cams_per_gpu": cams,
                 "letterbox": S,
+                "consumer_format": a.consumer_format,
+                "gathered_bytes_per_rank_per_step": cams * row if gather else 0,
                 "all_gather": gather,
             },
             "p50_latency_ms": r3(serve_lat[0]),

@@ -93,7 +93,8 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("motion", &SynthConfig::motion)
       .def_readwrite("seed", &SynthConfig::seed)
       .def_readwrite("slices", &SynthConfig::slices)
-      .def_readwrite("zero_samples", &SynthConfig::zero_samples);
+      .def_readwrite("zero_samples", &SynthConfig::zero_samples)
+      .def_readwrite("idr_phase", &SynthConfig::idr_phase);
 
   py::class_<AccessUnit, std::shared_ptr<AccessUnit>>(m, "AccessUnit")
       .def(py::init<>())
@@ -219,10 +220,12 @@ PYBIND11_MODULE(_vep, m) {
 
   py::class_<Worker>(m, "Worker")
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
-                       std::vector<float> stdv, int max_cameras, int pack_threads) {
+                       std::vector<float> stdv, int max_cameras, int pack_threads,
+                       int letterbox_format) {
              WorkerOptions o;
              o.device = device;
              o.pack_threads = pack_threads;
+             o.letterbox_format = letterbox_format;
              o.letterbox_size = letterbox_size;
              o.chw_dtype = chw_dtype;
              for (int k = 0; k < 3; ++k) {
@@ -234,7 +237,8 @@ PYBIND11_MODULE(_vep, m) {
            }),
            py::arg("device") = 0, py::arg("letterbox_size") = 0, py::arg("chw_dtype") = 0,
            py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
-           py::arg("max_cameras") = 256, py::arg("pack_threads") = 4)
+           py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
+           py::arg("letterbox_format") = 0)
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def("add_camera", &Worker::add_camera, py::arg("name"), py::arg("ring_slots") = 2)
       .def("remove_camera", &Worker::remove_camera, py::call_guard<py::gil_scoped_release>())
@@ -431,7 +435,7 @@ PYBIND11_MODULE(_vep, m) {
   m.def("letterbox",
         [](uintptr_t y, uintptr_t uv, int pitch, int src_w, int src_h, int crop_left, int crop_top,
            int size, uintptr_t out_hwc, uintptr_t out_chw, int chw_dtype, std::vector<float> mean,
-           std::vector<float> stdv, int pad, uintptr_t stream) {
+           std::vector<float> stdv, int pad, uintptr_t stream, int format) {
           gpu::LetterboxDesc d{};
           d.y = reinterpret_cast<const u8*>(y);
           d.uv = reinterpret_cast<const u8*>(uv);
@@ -442,8 +446,9 @@ PYBIND11_MODULE(_vep, m) {
           d.crop_top = crop_top;
           d.out_hwc = reinterpret_cast<u8*>(out_hwc);
           d.out_chw = reinterpret_cast<void*>(out_chw);
-          gpu::fill_letterbox_geometry(d, size);
+          gpu::fill_letterbox_geometry(d, size, format == gpu::kLbNV12);
           gpu::LetterboxParams p{};
+          p.format = format;
           p.size = size;
           p.chw_dtype = chw_dtype;
           for (int k = 0; k < 3; ++k) {
@@ -452,14 +457,29 @@ PYBIND11_MODULE(_vep, m) {
           }
           p.pad_value = u8(pad);
           gpu::launch_letterbox_one(d, p, reinterpret_cast<hipStream_t>(stream));
+        },
+        py::arg("y"), py::arg("uv"), py::arg("pitch"), py::arg("src_w"), py::arg("src_h"),
+        py::arg("crop_left"), py::arg("crop_top"), py::arg("size"), py::arg("out_hwc"),
+        py::arg("out_chw"), py::arg("chw_dtype"), py::arg("mean"), py::arg("std"), py::arg("pad"),
+        py::arg("stream"), py::arg("format") = 0);
+  m.def("nv12_to_chw",
+        [](uintptr_t in, uintptr_t out, int n, int size, int chw_dtype, std::vector<float> mean,
+           std::vector<float> stdv, uintptr_t stream) {
+          float m3[3], is3[3];
+          for (int k = 0; k < 3; ++k) {
+            m3[k] = mean.size() == 3 ? mean[size_t(k)] : 0.f;
+            is3[k] = 1.f / (stdv.size() == 3 ? stdv[size_t(k)] : 1.f);
+          }
+          gpu::launch_nv12_to_chw(reinterpret_cast<const u8*>(in), reinterpret_cast<void*>(out), n,
+                                  size, chw_dtype, m3, is3, reinterpret_cast<hipStream_t>(stream));
         });
-  m.def("letterbox_geometry", [](int src_w, int src_h, int size) {
+  m.def("letterbox_geometry", [](int src_w, int src_h, int size, bool even) {
     gpu::LetterboxDesc d{};
     d.src_w = src_w;
     d.src_h = src_h;
-    gpu::fill_letterbox_geometry(d, size);
+    gpu::fill_letterbox_geometry(d, size, even);
     return py::make_tuple(d.nw, d.nh, d.pad_x, d.pad_y);
-  });
+  }, py::arg("src_w"), py::arg("src_h"), py::arg("size"), py::arg("even") = false);
 
   bind_net(m);
   bind_mux(m);

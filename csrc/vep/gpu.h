@@ -64,14 +64,26 @@ struct LetterboxDesc {
   i32 nw, nh, pad_x, pad_y;
   float rx, ry;     // src/dst scale per axis
 };
+enum LetterboxFormat : int {
+  kLbBGR = 0,   // out_hwc = S*S*3 packed BGR (+ optional normalised CHW)
+  kLbNV12 = 1,  // out_hwc = S*S*3/2 NV12 (Y plane then interleaved UV): half the bytes on xGMI
+};
 struct LetterboxParams {
   i32 size;          // S
   i32 chw_dtype;     // ChwDtype
   float mean[3];     // RGB
   float inv_std[3];  // RGB
   u8 pad_value;
+  i32 format = kLbBGR;
 };
-void fill_letterbox_geometry(LetterboxDesc& d, int size);
+// even = true keeps the fitted size and padding on chroma-sample boundaries (NV12 output)
+void fill_letterbox_geometry(LetterboxDesc& d, int size, bool even = false);
+inline size_t letterbox_bytes(int size, int format) {
+  return format == kLbNV12 ? size_t(size) * size * 3 / 2 : size_t(size) * size * 3;
+}
+// Consumer side: NV12 letterboxed batch [n][S*S*3/2] -> normalised RGB CHW [n][3][S][S].
+void launch_nv12_to_chw(const u8* in, void* out, int n, int size, int chw_dtype,
+                        const float mean[3], const float inv_std[3], hipStream_t s);
 void launch_letterbox(const LetterboxDesc* d_descs, int n, const LetterboxParams& p,
                       hipStream_t s);
 void launch_letterbox_one(const LetterboxDesc& d, const LetterboxParams& p, hipStream_t s);

@@ -257,30 +257,206 @@ __global__ __launch_bounds__(256) void letterbox_one_kernel(const LetterboxDesc 
   letterbox_quad(d, p);
 }
 
+static inline u8 pad_luma(u8 pad);
+__global__ void letterbox_nv12_one_kernel(const LetterboxDesc d, int size, uint8_t pad_y);
+
 void launch_letterbox_one(const LetterboxDesc& d, const LetterboxParams& p, hipStream_t s) {
-  VEP_CHECK(p.size % 4 == 0, "letterbox size must be a multiple of 4");
-  int quads = p.size * p.size / 4;
-  hipLaunchKernelGGL(letterbox_one_kernel, dim3((quads + 255) / 256), dim3(256), 0, s, d, p);
+  VEP_CHECK(p.size % 8 == 0, "letterbox size must be a multiple of 8");
+  if (p.format == kLbNV12) {
+    const int work = p.size * p.size / 4 + p.size * p.size / 8;
+    hipLaunchKernelGGL(letterbox_nv12_one_kernel, dim3((work + 255) / 256), dim3(256), 0, s, d,
+                       p.size, pad_luma(p.pad_value));
+  } else {
+    int quads = p.size * p.size / 4;
+    hipLaunchKernelGGL(letterbox_one_kernel, dim3((quads + 255) / 256), dim3(256), 0, s, d, p);
+  }
   VEP_HIP(hipGetLastError());
 }
 
-void fill_letterbox_geometry(LetterboxDesc& d, int size) {
+void fill_letterbox_geometry(LetterboxDesc& d, int size, bool even) {
   float scale = std::min(float(size) / float(d.src_w), float(size) / float(d.src_h));
   d.nw = std::max(1, std::min(size, int(std::lround(d.src_w * scale))));
   d.nh = std::max(1, std::min(size, int(std::lround(d.src_h * scale))));
   d.pad_x = (size - d.nw) / 2;
   d.pad_y = (size - d.nh) / 2;
+  if (even) {
+    d.nw = std::max(2, d.nw & ~1);
+    d.nh = std::max(2, d.nh & ~1);
+    d.pad_x = ((size - d.nw) / 2) & ~1;
+    d.pad_y = ((size - d.nh) / 2) & ~1;
+  }
   d.rx = float(d.src_w) / float(d.nw);
   d.ry = float(d.src_h) / float(d.nh);
 }
 
+// ---------------------------------------------------------------------------------------------
+// NV12 letterbox: the Y and the interleaved UV planes are resized independently (bilinear,
+// align_corners=False) into an S x S NV12 canvas. Threads [0, S*S/4) produce 4 luma bytes each,
+// threads [S*S/4, S*S/4 + S*S/8) produce 2 chroma pairs (4 bytes) each; one dword store per
+// thread, consecutive lanes on consecutive dwords.
+
+__device__ __forceinline__ float bilerp(const uint8_t* __restrict__ p, int pitch, int step,
+                                        int x0, int x1, int y0, int y1, float lx, float ly) {
+  const float a = p[size_t(y0) * pitch + x0 * step], b = p[size_t(y0) * pitch + x1 * step];
+  const float c = p[size_t(y1) * pitch + x0 * step], e = p[size_t(y1) * pitch + x1 * step];
+  return (1.f - ly) * ((1.f - lx) * a + lx * b) + ly * ((1.f - lx) * c + lx * e);
+}
+
+__device__ __forceinline__ void axis(int o, int pad, int n, float r, int src, int& i0, int& i1,
+                                     float& l) {
+  const float s = fmaxf((float(o - pad) + 0.5f) * r - 0.5f, 0.f);
+  i0 = int(s);
+  i1 = i0 + (i0 < src - 1 ? 1 : 0);
+  l = s - float(i0);
+}
+
+__device__ __forceinline__ void letterbox_nv12_body(const LetterboxDesc& d, const int size,
+                                                    const uint8_t pad_y) {
+  const int S = size;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  const int ny = S * S / 4, nuv = S * S / 8;
+  if (t >= ny + nuv) return;
+  uint8_t o[4];
+  uint8_t* dst;
+  if (t < ny) {  // luma
+    const int pix0 = t * 4, oy = pix0 / S, ox0 = pix0 % S;
+    const bool row_in = oy >= d.pad_y && oy < d.pad_y + d.nh;
+    int y0 = 0, y1 = 0;
+    float ly = 0.f;
+    if (row_in) axis(oy, d.pad_y, d.nh, d.ry, d.src_h, y0, y1, ly);
+    const uint8_t* Y = d.y + size_t(d.crop_top) * d.pitch + d.crop_left;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ox = ox0 + i;
+      if (!row_in || ox < d.pad_x || ox >= d.pad_x + d.nw) {
+        o[i] = pad_y;
+        continue;
+      }
+      int x0, x1;
+      float lx;
+      axis(ox, d.pad_x, d.nw, d.rx, d.src_w, x0, x1, lx);
+      o[i] = uint8_t(fminf(bilerp(Y, d.pitch, 1, x0, x1, y0, y1, lx, ly) + 0.5f, 255.f));
+    }
+    dst = d.out_hwc + size_t(pix0);
+  } else {  // chroma: 2 (U,V) pairs
+    const int q = t - ny;
+    const int c0 = q * 2, Sc = S / 2, cy = c0 / Sc, cx0 = c0 % Sc;
+    const int px = d.pad_x / 2, py = d.pad_y / 2, nwc = d.nw / 2, nhc = d.nh / 2;
+    const int sw = (d.src_w + 1) / 2, sh = (d.src_h + 1) / 2;
+    const bool row_in = cy >= py && cy < py + nhc;
+    int y0 = 0, y1 = 0;
+    float ly = 0.f;
+    if (row_in) axis(cy, py, nhc, d.ry, sh, y0, y1, ly);
+    const uint8_t* UV = d.uv + size_t(d.crop_top / 2) * d.pitch + (d.crop_left & ~1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int cx = cx0 + i;
+      if (!row_in || cx < px || cx >= px + nwc) {
+        o[2 * i] = o[2 * i + 1] = 128;
+        continue;
+      }
+      int x0, x1;
+      float lx;
+      axis(cx, px, nwc, d.rx, sw, x0, x1, lx);
+      o[2 * i] = uint8_t(fminf(bilerp(UV, d.pitch, 2, x0, x1, y0, y1, lx, ly) + 0.5f, 255.f));
+      o[2 * i + 1] = uint8_t(fminf(bilerp(UV + 1, d.pitch, 2, x0, x1, y0, y1, lx, ly) + 0.5f, 255.f));
+    }
+    dst = d.out_hwc + size_t(S) * S + size_t(c0) * 2;
+  }
+  __builtin_memcpy(dst, o, 4);
+}
+
+__global__ __launch_bounds__(256) void letterbox_nv12_kernel(const LetterboxDesc* __restrict__ descs,
+                                                             int size, uint8_t pad_y) {
+  const LetterboxDesc d = descs[blockIdx.y];
+  letterbox_nv12_body(d, size, pad_y);
+}
+
+__global__ __launch_bounds__(256) void letterbox_nv12_one_kernel(const LetterboxDesc d, int size,
+                                                                 uint8_t pad_y) {
+  letterbox_nv12_body(d, size, pad_y);
+}
+
+// Consumer: NV12 [n][S*S*3/2] -> RGB CHW normalised, 4 pixels of a row per thread.
+template <int DT>
+__global__ __launch_bounds__(256) void nv12_to_chw_kernel(const uint8_t* __restrict__ in,
+                                                          void* __restrict__ out, int size,
+                                                          LetterboxParams p) {
+  const int S = size;
+  const int cam = blockIdx.y;
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q * 4 >= S * S) return;
+  const int pix0 = q * 4, oy = pix0 / S, ox0 = pix0 % S;
+  const uint8_t* base = in + size_t(cam) * (size_t(S) * S * 3 / 2);
+  uint32_t yw, cw;
+  __builtin_memcpy(&yw, base + pix0, 4);
+  __builtin_memcpy(&cw, base + size_t(S) * S + size_t(oy >> 1) * S + ox0, 4);  // 2 UV pairs
+  float ch[3][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int pair = i >> 1;
+    uint8_t b, g, r;
+    yuv_to_bgr(int((yw >> (8 * i)) & 0xff), int((cw >> (16 * pair)) & 0xff),
+               int((cw >> (16 * pair + 8)) & 0xff), &b, &g, &r);
+    ch[0][i] = (float(r) * (1.f / 255.f) - p.mean[0]) * p.inv_std[0];
+    ch[1][i] = (float(g) * (1.f / 255.f) - p.mean[1]) * p.inv_std[1];
+    ch[2][i] = (float(b) * (1.f / 255.f) - p.mean[2]) * p.inv_std[2];
+  }
+  const size_t plane = size_t(S) * S;
+  const size_t obase = size_t(cam) * 3 * plane + size_t(pix0);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    if constexpr (DT == kChwF32) {
+      float4 v = make_float4(ch[k][0], ch[k][1], ch[k][2], ch[k][3]);
+      *reinterpret_cast<float4*>(static_cast<float*>(out) + obase + k * plane) = v;
+    } else if constexpr (DT == kChwF16) {
+      _Float16 h[4] = {(_Float16)ch[k][0], (_Float16)ch[k][1], (_Float16)ch[k][2], (_Float16)ch[k][3]};
+      __builtin_memcpy(static_cast<_Float16*>(out) + obase + k * plane, h, 8);
+    } else {
+      uint16_t h[4] = {f32_to_bf16(ch[k][0]), f32_to_bf16(ch[k][1]), f32_to_bf16(ch[k][2]),
+                       f32_to_bf16(ch[k][3])};
+      __builtin_memcpy(static_cast<uint16_t*>(out) + obase + k * plane, h, 8);
+    }
+  }
+}
+
+void launch_nv12_to_chw(const u8* in, void* out, int n, int size, int chw_dtype,
+                        const float mean[3], const float inv_std[3], hipStream_t s) {
+  if (n <= 0) return;
+  VEP_CHECK(size % 4 == 0, "size must be a multiple of 4");
+  LetterboxParams p{};
+  p.size = size;
+  for (int k = 0; k < 3; ++k) {
+    p.mean[k] = mean[k];
+    p.inv_std[k] = inv_std[k];
+  }
+  dim3 grid((size * size / 4 + 255) / 256, n);
+  if (chw_dtype == kChwF32)
+    hipLaunchKernelGGL(nv12_to_chw_kernel<kChwF32>, grid, dim3(256), 0, s, in, out, size, p);
+  else if (chw_dtype == kChwF16)
+    hipLaunchKernelGGL(nv12_to_chw_kernel<kChwF16>, grid, dim3(256), 0, s, in, out, size, p);
+  else if (chw_dtype == kChwBF16)
+    hipLaunchKernelGGL(nv12_to_chw_kernel<kChwBF16>, grid, dim3(256), 0, s, in, out, size, p);
+  else
+    throw Error("nv12_to_chw: unsupported dtype");
+  VEP_HIP(hipGetLastError());
+}
+
+static inline u8 pad_luma(u8 pad) { return u8(std::lround(16.0 + pad * 219.0 / 255.0)); }
+
 void launch_letterbox(const LetterboxDesc* d_descs, int n, const LetterboxParams& p,
                       hipStream_t s) {
   if (n <= 0) return;
-  VEP_CHECK(p.size % 4 == 0, "letterbox size must be a multiple of 4");
-  int quads = p.size * p.size / 4;
-  hipLaunchKernelGGL(letterbox_kernel, dim3((quads + 255) / 256, n), dim3(256), 0, s, d_descs,
-                     p);
+  VEP_CHECK(p.size % 8 == 0, "letterbox size must be a multiple of 8");
+  if (p.format == kLbNV12) {
+    const int work = p.size * p.size / 4 + p.size * p.size / 8;
+    hipLaunchKernelGGL(letterbox_nv12_kernel, dim3((work + 255) / 256, n), dim3(256), 0, s,
+                       d_descs, p.size, pad_luma(p.pad_value));
+  } else {
+    int quads = p.size * p.size / 4;
+    hipLaunchKernelGGL(letterbox_kernel, dim3((quads + 255) / 256, n), dim3(256), 0, s, d_descs,
+                       p);
+  }
   VEP_HIP(hipGetLastError());
 }
 

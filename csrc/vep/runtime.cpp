@@ -252,7 +252,9 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   cams_.reserve(size_t(opt_.max_cameras));
   if (opt_.letterbox_size > 0) {
     const size_t S = size_t(opt_.letterbox_size);
-    cons_hwc_ = static_cast<u8*>(dev_.alloc(size_t(opt_.max_cameras) * S * S * 3));
+    (void)S;
+    cons_hwc_ = static_cast<u8*>(dev_.alloc(
+        size_t(opt_.max_cameras) * gpu::letterbox_bytes(opt_.letterbox_size, opt_.letterbox_format)));
     size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
     if (opt_.chw_dtype != gpu::kChwNone)
       cons_chw_ = dev_.alloc(size_t(opt_.max_cameras) * 3 * S * S * es);
@@ -486,6 +488,54 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi) {
 
 static inline size_t al(size_t x, size_t a = 256) { return (x + a - 1) & ~(a - 1); }
 
+// CPU mirror of letterbox_nv12_kernel (same float math, same rounding).
+static void cpu_letterbox_nv12(const HostSurface& s, const gpu::LetterboxDesc& d, int S, u8 pad) {
+  const u8 pad_y = u8(std::lround(16.0 + pad * 219.0 / 255.0));
+  auto axis = [](int o, int p, float r, int src, int& i0, int& i1, float& l) {
+    const float v = std::max((float(o - p) + 0.5f) * r - 0.5f, 0.f);
+    i0 = int(v);
+    i1 = i0 + (i0 < src - 1 ? 1 : 0);
+    l = v - float(i0);
+  };
+  auto lerp = [](const u8* p, int pitch, int step, int x0, int x1, int y0, int y1, float lx, float ly) {
+    const float a = p[size_t(y0) * pitch + x0 * step], b = p[size_t(y0) * pitch + x1 * step];
+    const float c = p[size_t(y1) * pitch + x0 * step], e = p[size_t(y1) * pitch + x1 * step];
+    return (1.f - ly) * ((1.f - lx) * a + lx * b) + ly * ((1.f - lx) * c + lx * e);
+  };
+  const int pitch = s.coded_w;
+  const u8* Y = s.y.data() + size_t(d.crop_top) * pitch + d.crop_left;
+  for (int oy = 0; oy < S; ++oy)
+    for (int ox = 0; ox < S; ++ox) {
+      u8 v = pad_y;
+      if (oy >= d.pad_y && oy < d.pad_y + d.nh && ox >= d.pad_x && ox < d.pad_x + d.nw) {
+        int x0, x1, y0, y1;
+        float lx, ly;
+        axis(oy, d.pad_y, d.ry, d.src_h, y0, y1, ly);
+        axis(ox, d.pad_x, d.rx, d.src_w, x0, x1, lx);
+        v = u8(std::min(lerp(Y, pitch, 1, x0, x1, y0, y1, lx, ly) + 0.5f, 255.f));
+      }
+      d.out_hwc[size_t(oy) * S + ox] = v;
+    }
+  const u8* UV = s.uv.data() + size_t(d.crop_top / 2) * pitch + (d.crop_left & ~1);
+  const int px = d.pad_x / 2, py = d.pad_y / 2, nwc = d.nw / 2, nhc = d.nh / 2;
+  const int sw = (d.src_w + 1) / 2, sh = (d.src_h + 1) / 2;
+  u8* out = d.out_hwc + size_t(S) * S;
+  for (int cy = 0; cy < S / 2; ++cy)
+    for (int cx = 0; cx < S / 2; ++cx) {
+      u8 u = 128, w = 128;
+      if (cy >= py && cy < py + nhc && cx >= px && cx < px + nwc) {
+        int x0, x1, y0, y1;
+        float lx, ly;
+        axis(cy, py, d.ry, sh, y0, y1, ly);
+        axis(cx, px, d.rx, sw, x0, x1, lx);
+        u = u8(std::min(lerp(UV, pitch, 2, x0, x1, y0, y1, lx, ly) + 0.5f, 255.f));
+        w = u8(std::min(lerp(UV + 1, pitch, 2, x0, x1, y0, y1, lx, ly) + 0.5f, 255.f));
+      }
+      out[size_t(cy) * S + 2 * cx] = u;
+      out[size_t(cy) * S + 2 * cx + 1] = w;
+    }
+}
+
 static void cpu_letterbox(const HostSurface& s, const gpu::LetterboxDesc& d,
                           const gpu::LetterboxParams& p) {
   const int S = p.size;
@@ -705,11 +755,12 @@ void Worker::launch_gpu(Stage& st) {
       l.crop_left = j.pic.crop_left;
       l.crop_top = j.pic.crop_top;
       VEP_CHECK(j.cam < cons_rows_, "camera index exceeds consumer batch rows");
-      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(j.cam) * S * S * 3 : nullptr;
+      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(j.cam) * gpu::letterbox_bytes(int(S), opt_.letterbox_format)
+                            : nullptr;
       const size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
       l.out_chw = cons_chw_ ? static_cast<u8*>(cons_chw_) + size_t(j.cam) * 3 * S * S * es
                             : nullptr;
-      gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
+      gpu::fill_letterbox_geometry(l, opt_.letterbox_size, opt_.letterbox_format == gpu::kLbNV12);
     }
   }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream
@@ -728,6 +779,7 @@ void Worker::launch_gpu(Stage& st) {
       p.inv_std[k] = 1.f / opt_.std[k];
     }
     p.pad_value = 114;
+    p.format = opt_.letterbox_format;
     gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(st.d + off_lb), n, p,
                           stream_);
   }
@@ -748,11 +800,18 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       l.src_h = jobs[i].pic.height;
       l.crop_left = jobs[i].pic.crop_left;
       l.crop_top = jobs[i].pic.crop_top;
-      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(jobs[i].cam) * S * S * 3 : nullptr;
+      const bool nv12 = opt_.letterbox_format == gpu::kLbNV12;
+      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(jobs[i].cam) *
+                                              gpu::letterbox_bytes(int(S), opt_.letterbox_format)
+                            : nullptr;
       l.out_chw = (cons_chw_ && opt_.chw_dtype == gpu::kChwF32)
                       ? static_cast<u8*>(cons_chw_) + size_t(jobs[i].cam) * 3 * S * S * 4
                       : nullptr;
-      gpu::fill_letterbox_geometry(l, opt_.letterbox_size);
+      gpu::fill_letterbox_geometry(l, opt_.letterbox_size, nv12);
+      if (nv12) {
+        cpu_letterbox_nv12(c.surface.host, l, opt_.letterbox_size, 114);
+        continue;
+      }
       gpu::LetterboxParams p{};
       p.size = opt_.letterbox_size;
       p.chw_dtype = opt_.chw_dtype;

@@ -168,6 +168,7 @@ class Camera {
 struct WorkerOptions {
   int device = 0;             // -1 = CPU backend
   int letterbox_size = 0;     // 0 = no consumer batch
+  int letterbox_format = 0;   // gpu::LetterboxFormat (BGR HWC or NV12)
   int chw_dtype = 0;          // gpu::ChwDtype for the normalised CHW consumer tensor
   float mean[3] = {0.f, 0.f, 0.f};
   float std[3] = {1.f, 1.f, 1.f};

@@ -137,3 +137,59 @@ def test_replay_bench_runs(native):
     for c in rb.cameras:
         st = wk.stats(c)
         assert st["decoded"] == 12 and st["errors"] == 0
+
+
+@pytest.mark.parametrize("src", [(1920, 1080), (640, 480), (352, 288)])
+def test_letterbox_nv12_vs_reference(src):
+    from video_edge_ai_proxy_amd import ops
+
+    w, h = src
+    H, W = (h + 15) // 16 * 16, (w + 15) // 16 * 16
+    g = torch.Generator().manual_seed(2)
+    y = torch.randint(16, 236, (H, W), dtype=torch.uint8, generator=g).cuda()
+    uv = torch.randint(16, 241, (H // 2, W), dtype=torch.uint8, generator=g).cuda()
+    got = ops.letterbox_nv12(y, uv, 640, w, h)
+    want = ops.letterbox_nv12_reference(y, uv, 640, w, h)
+    torch.cuda.synchronize()
+    d = (got.int() - want.int()).abs()
+    assert d.max().item() <= 1 and (d > 0).float().mean().item() < 0.01
+
+
+def test_nv12_to_chw_vs_reference():
+    from video_edge_ai_proxy_amd import ops
+
+    S, n = 64, 3
+    g = torch.Generator().manual_seed(3)
+    batch = torch.randint(0, 256, (n, S * S * 3 // 2), dtype=torch.uint8, generator=g)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    got = ops.nv12_to_chw(batch.cuda(), S, torch.float32, mean, std)
+    got16 = ops.nv12_to_chw(batch.cuda(), S, torch.bfloat16, mean, std)
+    torch.cuda.synchronize()
+    for i in range(n):
+        yp = batch[i, :S * S].view(S, S)
+        uvp = batch[i, S * S:].view(S // 2, S)
+        bgr = ops.nv12_to_bgr_reference(yp, uvp).float() / 255.0
+        rgb = bgr.flip(-1).permute(2, 0, 1)
+        ref = (rgb - torch.tensor(mean).view(3, 1, 1)) / torch.tensor(std).view(3, 1, 1)
+        assert torch.allclose(got[i].cpu(), ref, atol=1e-5)
+        assert torch.allclose(got16[i].float().cpu(), ref, atol=0.03)
+
+
+def test_worker_nv12_consumer_batch(native):
+    from video_edge_ai_proxy_amd import ops
+
+    S = 320
+    wk = native.Worker(device=0, letterbox_size=S, max_cameras=2, letterbox_format=1)
+    buf = torch.zeros((2, S * S * 3 // 2), dtype=torch.uint8, device="cuda")
+    wk.set_consumer_buffers(buf.data_ptr(), 0, 2)
+    enc = synth(native, 640, 480, gop=5)
+    ref = native.CpuDecoder()
+    cam = wk.add_camera("c", 3)
+    for _ in range(3):
+        au = enc.next()
+        ref.decode(au)
+        wk.decode_now(cam, au)
+    yh, uvh = ref.surface()
+    want = ops.letterbox_nv12_reference(torch.from_numpy(yh), torch.from_numpy(uvh), S, 640, 480)
+    d = (buf[cam].cpu().int() - want.int()).abs()
+    assert d.max().item() <= 1

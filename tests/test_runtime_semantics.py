@@ -106,3 +106,23 @@ def test_ring_cursor_semantics(native):
     m2, _ = w.read_latest(cam, m1["seq"])
     assert m2["seq"] == m1["seq"] + 1 and m2["pts"] == 3000
     assert w.published(cam) == 2
+
+
+def test_cpu_worker_nv12_consumer_matches_reference(native):
+    import torch
+
+    from video_edge_ai_proxy_amd import ops
+
+    S = 64
+    w = native.Worker(device=-1, letterbox_size=S, max_cameras=1, letterbox_format=1)
+    buf = torch.zeros((1, S * S * 3 // 2), dtype=torch.uint8)
+    w.set_consumer_buffers(buf.data_ptr(), 0, 1)
+    cam = w.add_camera("c", 2)
+    enc = synth(native, 96, 64, gop=4)
+    ref = native.CpuDecoder()
+    au = enc.next()
+    ref.decode(au)
+    w.decode_now(cam, au)
+    yh, uvh = ref.surface()
+    want = ops.letterbox_nv12_reference(torch.from_numpy(yh), torch.from_numpy(uvh), S, 96, 64)
+    assert (buf[0].int() - want.int()).abs().max().item() <= 1

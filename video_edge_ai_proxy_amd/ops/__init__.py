@@ -97,9 +97,62 @@ def pcm_decode_bgr(y: torch.Tensor, uv: torch.Tensor, mb_slot: torch.Tensor,
     return out
 
 
-def letterbox_geometry(src_w: int, src_h: int, size: int):
-    """(new_w, new_h, pad_x, pad_y) of the centred aspect-preserving fit."""
-    return tuple(native.letterbox_geometry(src_w, src_h, size))
+def letterbox_geometry(src_w: int, src_h: int, size: int, even: bool = False):
+    """(new_w, new_h, pad_x, pad_y) of the centred aspect-preserving fit (even: NV12-aligned)."""
+    return tuple(native.letterbox_geometry(src_w, src_h, size, even))
+
+
+def letterbox_nv12(y: torch.Tensor, uv: torch.Tensor, size: int = 640, width: int | None = None,
+                   height: int | None = None, crop_left: int = 0, crop_top: int = 0,
+                   pad_value: int = 114) -> torch.Tensor:
+    """NV12 -> letterboxed NV12 ``[S*S*3/2]`` uint8 (Y and UV planes resized independently):
+    the compact consumer format that crosses xGMI in the all-gather."""
+    require_gpu()
+    H, W = _check_nv12(y, uv)
+    width = W - crop_left if width is None else width
+    height = H - crop_top if height is None else height
+    if size % 8:
+        raise ValueError("size must be a multiple of 8")
+    out = torch.empty((size * size * 3 // 2,), dtype=torch.uint8, device=y.device)
+    native.letterbox(y.data_ptr(), uv.data_ptr(), W, width, height, crop_left, crop_top, size,
+                     out.data_ptr(), 0, 0, [0.0] * 3, [1.0] * 3, int(pad_value), _stream_ptr(y), 1)
+    return out
+
+
+def nv12_to_chw(batch: torch.Tensor, size: int, dtype: torch.dtype = torch.bfloat16,
+                mean=(0.0, 0.0, 0.0), std=(1.0, 1.0, 1.0)) -> torch.Tensor:
+    """Consumer-side: ``[N, S*S*3/2]`` NV12 batch -> ``[N, 3, S, S]`` normalised RGB (BT.601)."""
+    require_gpu()
+    if batch.dtype != torch.uint8 or not batch.is_contiguous():
+        raise ValueError("batch must be contiguous uint8")
+    n = batch.numel() // (size * size * 3 // 2)
+    if n * size * size * 3 // 2 != batch.numel():
+        raise ValueError("batch size is not a whole number of S x S NV12 pictures")
+    out = torch.empty((n, 3, size, size), dtype=dtype, device=batch.device)
+    native.nv12_to_chw(batch.data_ptr(), out.data_ptr(), n, size, _CHW_DTYPES[dtype],
+                       list(map(float, mean)), list(map(float, std)), _stream_ptr(batch))
+    return out
+
+
+def letterbox_nv12_reference(y: torch.Tensor, uv: torch.Tensor, size: int, width: int,
+                             height: int, pad_value: int = 114) -> torch.Tensor:
+    """fp32 torch reference of :func:`letterbox_nv12` (per-plane bilinear, align_corners=False)."""
+    import torch.nn.functional as F
+
+    nw, nh, px, py = letterbox_geometry(width, height, size, even=True)
+    ypad = round(16 + pad_value * 219 / 255)
+    Y = y[:height, :width].float()[None, None]
+    yo = torch.full((size, size), float(ypad), device=y.device)
+    yo[py:py + nh, px:px + nw] = F.interpolate(Y, size=(nh, nw), mode="bilinear",
+                                               align_corners=False)[0, 0]
+    cw, chh = (width + 1) // 2, (height + 1) // 2
+    C = uv[:chh, :cw * 2].float().view(chh, cw, 2).permute(2, 0, 1)[None]
+    co = torch.full((2, size // 2, size // 2), 128.0, device=y.device)
+    co[:, py // 2:py // 2 + nh // 2, px // 2:px // 2 + nw // 2] = F.interpolate(
+        C, size=(nh // 2, nw // 2), mode="bilinear", align_corners=False)[0]
+    out_y = (yo + 0.5).clamp(0, 255).floor().to(torch.uint8).flatten()
+    out_c = (co + 0.5).clamp(0, 255).floor().to(torch.uint8).permute(1, 2, 0).flatten()
+    return torch.cat([out_y, out_c])
 
 
 def letterbox(y: torch.Tensor, uv: torch.Tensor, size: int = 640, width: int | None = None,
