@@ -59,6 +59,7 @@ class GpuConfig:
     ring_slots: int = 0                          # 0 = max(2, buffer.in_memory)
     letterbox_size: int = 0                      # >0: maintain a batched consumer tensor
     letterbox_dtype: str = "none"                # none | fp16 | bf16 | fp32
+    letterbox_format: str = "bgr"                # bgr (HWC u8) | nv12 (gather-friendly)
     mean: list = field(default_factory=lambda: [0.0, 0.0, 0.0])
     std: list = field(default_factory=lambda: [1.0, 1.0, 1.0])
     idle_cutoff_ms: int = 10000                  # rtsp_to_rtmp.py:144-145

@@ -68,7 +68,8 @@ class Hub:
         for d in devices:
             w = native.Worker(device=d, letterbox_size=int(g.letterbox_size),
                               chw_dtype=_CHW.get(g.letterbox_dtype, 0), mean=list(g.mean),
-                              std=list(g.std), max_cameras=int(g.max_cameras_per_gpu))
+                              std=list(g.std), max_cameras=int(g.max_cameras_per_gpu),
+                              letterbox_format=1 if g.letterbox_format == "nv12" else 0)
             w.start()
             self.workers.append(w)
         self.archiver = native.Archiver()

@@ -81,12 +81,14 @@ class ConsumerBatch:
     fp16/bf16 CHW tensor halves the xGMI bytes; consumers normalise after the gather (fused into
     their first op, or via :func:`video_edge_ai_proxy_amd.ops.letterbox` style kernels)."""
 
-    def __init__(self, worker, cams: int, size: int, device: torch.device, world: int = 1):
+    def __init__(self, worker, cams: int, size: int, device: torch.device, world: int = 1,
+                 fmt: str = "bgr"):
         self.worker = worker
-        self.cams, self.size, self.world = cams, size, world
-        self.bufs = [torch.zeros((cams, size, size, 3), dtype=torch.uint8, device=device)
+        self.cams, self.size, self.world, self.fmt = cams, size, world, fmt
+        shape = (size * size * 3 // 2,) if fmt == "nv12" else (size, size, 3)
+        self.bufs = [torch.zeros((cams, *shape), dtype=torch.uint8, device=device)
                      for _ in range(2)]
-        self.out = [torch.zeros((world * cams, size, size, 3), dtype=torch.uint8, device=device)
+        self.out = [torch.zeros((world * cams, *shape), dtype=torch.uint8, device=device)
                     for _ in range(2)] if world > 1 else None
         self.handles = [None, None]
         self.tick = 0
