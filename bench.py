@@ -29,6 +29,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "decoded FPS (whole node) + p50 VideoLatestImage latency, 256×1080p RTSP"
+CODEC = {"h264": "H.264", "h265": "H.265"}
+ENTROPY = {"h264": "CAVLC macroblock-layer", "h265": "CABAC coding-tree"}
 
 
 def parse_args():
@@ -42,6 +44,8 @@ def parse_args():
     ap.add_argument("--fps", type=int, default=30)
     ap.add_argument("--gop", type=int, default=30)
     ap.add_argument("--motion", type=float, default=0.05)
+    ap.add_argument("--codec", choices=["h264", "h265"], default="h264",
+                    help="h265 = BASELINE config 5 codec (e.g. --width 3840 --height 2160)")
     ap.add_argument("--threads", type=int, default=8, help="host parse threads per rank")
     ap.add_argument("--pack-threads", type=int, default=8, help="host staging-pack threads per rank")
     ap.add_argument("--letterbox", type=int, default=640)
@@ -90,6 +94,7 @@ def main():
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
+    cfg.codec = a.codec
     cfg.seed = 1 + rank * 100003
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam")
@@ -189,10 +194,10 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8 (BGR24 frames; bf16-capable consumer path)",
-            "data": "synthetic H.264 Baseline streams (random-noise background + moving object, "
+            "data": f"synthetic {CODEC[a.codec]} streams (random-noise background + moving object, "
                     f"GOP {a.gop}, {a.motion:.0%} motion), pre-encoded per camera and replayed",
             "config": {
-                "model": f"{cams * max(world, 1)}x{a.width}x{a.height}p{a.fps} H.264 cameras",
+                "model": f"{cams * max(world, 1)}x{a.width}x{a.height}p{a.fps} {CODEC[a.codec]} cameras",
                 "global_batch": cams * max(world, 1),
                 "seq_len": a.gop,
                 "parallelism": f"camera-dp{max(world, 1)}",
@@ -212,8 +217,8 @@ def main():
             "next_frame_latency_definition": "back-to-back requests on one stream/channel (the "
                                              "reference clients' pattern): includes waiting for "
                                              "the camera's next decoded frame",
-            "decoder_backend": "native subset decoder: CPU CAVLC MB-layer parse + gfx950 HIP "
-                               "I_PCM reconstruct/NV12->BGR24 (rocDecode absent in image)",
+            "decoder_backend": "native subset decoder: CPU " + ENTROPY[a.codec] + " parse + gfx950 "
+                               "HIP PCM reconstruct/NV12->BGR24 (rocDecode absent in image)",
             "per_gpu_fps": round(fps / max(world, 1), 2),
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),

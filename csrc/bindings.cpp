@@ -5,6 +5,7 @@
 #include <pybind11/stl.h>
 
 #include "vep/bench_driver.h"
+#include "vep/cabac.h"
 #include "vep/codec.h"
 #include "vep/gpu.h"
 #include "vep/h264.h"
@@ -60,7 +61,7 @@ static Camera& cam_of(Worker& w, int idx) {
 
 // Stateful oracle: parse + CPU reconstruct a sequence of AUs, return the final BGR picture.
 struct CpuDecoder {
-  H264Parser parser;
+  StreamParser parser;
   MbUpdate upd;
   HostSurface surf;
   PictureInfo last;
@@ -94,7 +95,15 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("seed", &SynthConfig::seed)
       .def_readwrite("slices", &SynthConfig::slices)
       .def_readwrite("zero_samples", &SynthConfig::zero_samples)
-      .def_readwrite("idr_phase", &SynthConfig::idr_phase);
+      .def_readwrite("idr_phase", &SynthConfig::idr_phase)
+      .def_readwrite("merge_cands", &SynthConfig::merge_cands)
+      .def_property(
+          "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
+          [](SynthConfig& c, const std::string& v) {
+            if (v == "h264" || v == "avc") c.codec = Codec::kH264;
+            else if (v == "h265" || v == "hevc") c.codec = Codec::kH265;
+            else throw Error("codec must be h264 or h265");
+          });
 
   py::class_<AccessUnit, std::shared_ptr<AccessUnit>>(m, "AccessUnit")
       .def(py::init<>())
@@ -152,7 +161,9 @@ PYBIND11_MODULE(_vep, m) {
            })
       .def_property_readonly("sps_nal", [](const SynthH264& s) { return to_bytes(s.sps_nal().data(), s.sps_nal().size()); })
       .def_property_readonly("pps_nal", [](const SynthH264& s) { return to_bytes(s.pps_nal().data(), s.pps_nal().size()); })
+      .def_property_readonly("vps_nal", [](const SynthH264& s) { return to_bytes(s.vps_nal().data(), s.vps_nal().size()); })
       .def_property_readonly("frame_index", &SynthH264::frame_index);
+  m.attr("SynthEncoder") = m.attr("SynthH264");
 
   py::class_<CpuDecoder>(m, "CpuDecoder")
       .def(py::init<>())
@@ -182,6 +193,68 @@ PYBIND11_MODULE(_vep, m) {
     d["poc_type"] = s.poc_type;
     d["max_num_ref_frames"] = s.max_num_ref_frames;
     return d;
+  });
+  m.def("parse_hevc_sps", [](const std::string& nal) {
+    std::vector<u8> r(nal.size());
+    size_t n = ebsp_to_rbsp(reinterpret_cast<const u8*>(nal.data()), nal.size(), r.data());
+    hevc::Sps s = hevc::parse_sps(r.data(), n);
+    py::dict d;
+    d["profile_idc"] = s.ptl.profile_idc;
+    d["level_idc"] = s.ptl.level_idc;
+    d["width"] = s.out_width();
+    d["height"] = s.out_height();
+    d["coded_width"] = s.width;
+    d["coded_height"] = s.height;
+    d["fps"] = s.fps();
+    d["ctb_size"] = s.ctb_size();
+    d["pcm"] = s.pcm;
+    d["num_short_term_rps"] = int(s.st_rps.size());
+    return d;
+  });
+  // Random-bin CABAC engine round trip (context-coded with skewed and flipping statistics,
+  // bypass, terminate-0 and a final terminate-1 flush). Returns (ok, coded_bytes).
+  m.def("cabac_roundtrip", [](u64 seed, int n, int qp) {
+    u64 st = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() { st ^= st << 13; st ^= st >> 7; st ^= st << 17; return st; };
+    const size_t nn = static_cast<size_t>(n);
+    std::vector<u8> kind(nn), ctx(nn), bin(nn);
+    for (int i = 0; i < n; ++i) {
+      u64 r = rnd();
+      kind[size_t(i)] = u8((r & 15) == 0 ? 1 : ((r & 63) == 1 ? 2 : 0));  // 0 ctx, 1 bypass, 2 term0
+      ctx[size_t(i)] = u8((r >> 8) % 4);
+      const int p = ctx[size_t(i)] == 0 ? 2 : ctx[size_t(i)] == 1 ? 50 : ctx[size_t(i)] == 2 ? 97 : ((i / 500) & 1) ? 90 : 10;
+      bin[size_t(i)] = kind[size_t(i)] == 2 ? 0 : u8(int((r >> 20) % 100) < p);
+    }
+    std::vector<u8> buf;
+    cabac::Ctx ce[4], cd[4];
+    const int init[4] = {197, 154, 122, 139};
+    for (int k = 0; k < 4; ++k) ce[k].init(init[k], qp), cd[k].init(init[k], qp);
+    {
+      cabac::Encoder e(buf);
+      for (int i = 0; i < n; ++i) {
+        if (kind[size_t(i)] == 0) e.decision(ce[ctx[size_t(i)]], bin[size_t(i)]);
+        else if (kind[size_t(i)] == 1) e.bypass(bin[size_t(i)]);
+        else e.terminate(0);
+      }
+      e.terminate(1);
+      e.align_zero();
+    }
+    cabac::Decoder d(buf.data(), buf.size(), 0);
+    bool ok = true;
+    for (int i = 0; i < n && ok; ++i) {
+      u32 b;
+      if (kind[size_t(i)] == 0) b = d.decision(cd[ctx[size_t(i)]]);
+      else if (kind[size_t(i)] == 1) b = d.bypass();
+      else b = d.terminate();
+      ok = b == bin[size_t(i)];
+    }
+    ok = ok && d.terminate() == 1 && d.aligned_bytepos() == buf.size();
+    return py::make_tuple(ok, buf.size());
+  });
+  m.def("hvcc_record", [](const std::string& vps, const std::string& sps, const std::string& pps) {
+    auto v = [](const std::string& x) { return std::vector<u8>(x.begin(), x.end()); };
+    std::vector<u8> r = hevc::hvcc_record(v(vps), v(sps), v(pps));
+    return to_bytes(r.data(), r.size());
   });
   m.def("rbsp_to_ebsp", [](const std::string& r) {
     std::vector<u8> out;

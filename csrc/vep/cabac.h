@@ -1,0 +1,234 @@
+// CABAC arithmetic coding engine (H.265 §9.3.4.3 / §9.3.5; identical engine to H.264 §9.3.3.2):
+// 9-bit-offset decoder, 10-bit-low encoder with outstanding-bit carry resolution, the 64-state
+// probability model and the slice-QP-dependent context initialisation.
+//
+// Used by the native HEVC subset codec (hevc.h) for the handful of context-coded syntax elements
+// a PCM/skip picture needs (cu_skip_flag, pred_mode_flag, part_mode) plus the terminating bins
+// (pcm_flag, end_of_slice_segment_flag). Replaces libavcodec's CABAC inside PyAV in the reference
+// (python/read_image.py:87 `p.decode()`).
+#pragma once
+
+#include "common.h"
+
+namespace vep::cabac {
+
+// rangeTabLPS[pStateIdx][qRangeIdx] (H.265 Table 9-52 / H.264 Table 9-44).
+inline constexpr u8 kRangeLps[64][4] = {
+    {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205},
+    {116, 142, 169, 195}, {111, 135, 160, 185}, {105, 128, 152, 175}, {100, 122, 144, 166},
+    {95, 116, 137, 158},  {90, 110, 130, 150},  {85, 104, 123, 142},  {81, 99, 117, 135},
+    {77, 94, 111, 128},   {73, 89, 105, 122},   {69, 85, 100, 116},   {66, 80, 95, 110},
+    {62, 76, 90, 104},    {59, 72, 86, 99},     {56, 69, 81, 94},     {53, 65, 77, 89},
+    {51, 62, 73, 85},     {48, 59, 69, 80},     {46, 56, 66, 76},     {43, 53, 63, 72},
+    {41, 50, 59, 69},     {39, 48, 56, 65},     {37, 45, 54, 62},     {35, 43, 51, 59},
+    {33, 41, 48, 56},     {32, 39, 46, 53},     {30, 37, 43, 50},     {29, 35, 41, 48},
+    {27, 33, 39, 45},     {26, 31, 37, 43},     {24, 30, 35, 41},     {23, 28, 33, 39},
+    {22, 27, 32, 37},     {21, 26, 30, 35},     {20, 24, 29, 33},     {19, 23, 27, 31},
+    {18, 22, 26, 30},     {17, 21, 25, 28},     {16, 20, 23, 27},     {15, 19, 22, 25},
+    {14, 18, 21, 24},     {14, 17, 20, 23},     {13, 16, 19, 22},     {12, 15, 18, 21},
+    {12, 14, 17, 20},     {11, 14, 16, 19},     {11, 13, 15, 18},     {10, 12, 15, 17},
+    {10, 12, 14, 16},     {9, 11, 13, 15},      {9, 11, 12, 14},      {8, 10, 12, 14},
+    {8, 9, 11, 13},       {7, 9, 11, 12},       {7, 9, 10, 12},       {7, 8, 10, 11},
+    {6, 8, 9, 11},        {6, 7, 9, 10},        {6, 7, 8, 9},         {2, 2, 2, 2},
+};
+
+// transIdxLps (Table 9-53); transIdxMps is min(s + 1, 62) (63 is the terminate state).
+inline constexpr u8 kNextLps[64] = {
+    0,  0,  1,  2,  2,  4,  4,  5,  6,  7,  8,  9,  9,  11, 11, 12, 13, 13, 15, 15, 16, 16,
+    18, 18, 19, 19, 21, 21, 22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30,
+    31, 32, 32, 33, 33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63,
+};
+
+struct Ctx {
+  u8 state = 0;  // pStateIdx
+  u8 mps = 0;    // valMps
+
+  // §9.3.2.2: initValue -> (pStateIdx, valMps) for SliceQpY.
+  void init(int init_value, int qp) {
+    const int slope = init_value >> 4, offset = init_value & 15;
+    const int m = slope * 5 - 45, n = (offset << 3) - 16;
+    const int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
+    int pre = ((m * q) >> 4) + n;
+    pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
+    mps = pre <= 63 ? 0 : 1;
+    state = u8(mps ? pre - 64 : 63 - pre);
+  }
+};
+
+// Arithmetic decoder over an RBSP (byte positions are RBSP offsets).
+class Decoder {
+ public:
+  Decoder(const u8* p, size_t n, size_t bytepos) : p_(p), n_(n) { start(bytepos); }
+
+  // §9.3.2.5: (re)initialise at a byte position (slice data start, or after PCM samples).
+  void start(size_t bytepos) {
+    pos_ = bytepos * 8;
+    range_ = 510;
+    offset_ = read(9);
+  }
+  u32 decision(Ctx& c) {
+    const u32 lps = kRangeLps[c.state][(range_ >> 6) & 3];
+    range_ -= lps;
+    u32 bin;
+    if (offset_ >= range_) {
+      bin = c.mps ^ 1u;
+      offset_ -= range_;
+      range_ = lps;
+      if (c.state == 0) c.mps ^= 1;
+      c.state = kNextLps[c.state];
+    } else {
+      bin = c.mps;
+      if (c.state < 62) ++c.state;
+    }
+    renorm();
+    return bin;
+  }
+  // §9.3.4.3.5. After a 1 (pcm_flag / end_of_slice_segment_flag) the bit position is exactly
+  // the end of the encoder's flush (the flush's final 1 bit included).
+  u32 terminate() {
+    range_ -= 2;
+    if (offset_ >= range_) return 1;
+    renorm();
+    return 0;
+  }
+  u32 bypass() {
+    offset_ = (offset_ << 1) | read(1);
+    if (offset_ >= range_) {
+      offset_ -= range_;
+      return 1;
+    }
+    return 0;
+  }
+  size_t bitpos() const { return pos_; }
+  size_t aligned_bytepos() const { return (pos_ + 7) >> 3; }
+
+ private:
+  void renorm() {
+    while (range_ < 256) {
+      range_ <<= 1;
+      offset_ = (offset_ << 1) | read(1);
+    }
+  }
+  u32 read(int nbits) {
+    u32 v = 0;
+    for (int i = 0; i < nbits; ++i, ++pos_) {
+      // reading past the end yields zeros (the trailing bits); the caller bounds the walk
+      const u32 b = pos_ < n_ * 8 ? (p_[pos_ >> 3] >> (7 - (pos_ & 7))) & 1u : 0u;
+      v = (v << 1) | b;
+    }
+    return v;
+  }
+  const u8* p_;
+  size_t n_;
+  size_t pos_ = 0;
+  u32 range_ = 510, offset_ = 0;
+};
+
+// Arithmetic encoder appending to a byte-aligned RBSP buffer (§9.3.5).
+class Encoder {
+ public:
+  explicit Encoder(std::vector<u8>& out) : out_(out) { start(); }
+
+  void start() {  // InitEncoder: must be at a byte boundary
+    VEP_CHECK(nbits_ == 0, "CABAC encoder must start byte aligned");
+    low_ = 0;
+    range_ = 510;
+    first_ = true;
+    outstanding_ = 0;
+  }
+  void decision(Ctx& c, u32 bin) {
+    const u32 lps = kRangeLps[c.state][(range_ >> 6) & 3];
+    range_ -= lps;
+    if (bin != c.mps) {
+      low_ += range_;
+      range_ = lps;
+      if (c.state == 0) c.mps ^= 1;
+      c.state = kNextLps[c.state];
+    } else if (c.state < 62) {
+      ++c.state;
+    }
+    renorm();
+  }
+  void terminate(u32 bin) {
+    range_ -= 2;
+    if (bin) {
+      low_ += range_;
+      flush();
+    } else {
+      renorm();
+    }
+  }
+  void bypass(u32 bin) {
+    low_ <<= 1;
+    if (bin) low_ += range_;
+    if (low_ >= 1024) {
+      put(1);
+      low_ -= 1024;
+    } else if (low_ < 512) {
+      put(0);
+    } else {
+      low_ -= 512;
+      ++outstanding_;
+    }
+  }
+  // Raw bits after a flush (pcm_alignment_zero_bit, byte_alignment()).
+  void align_zero() {
+    while (nbits_ != 0) bit(0);
+  }
+  void raw_bytes(const u8* p, size_t n) {
+    VEP_CHECK(nbits_ == 0, "raw bytes must be byte aligned");
+    out_.insert(out_.end(), p, p + n);
+  }
+  bool byte_aligned() const { return nbits_ == 0; }
+
+ private:
+  void flush() {  // EncodeFlush: the final written bit is 1 (rbsp_stop_one_bit at slice end)
+    range_ = 2;
+    renorm();
+    put((low_ >> 9) & 1);
+    bit(((low_ >> 8) & 1));
+    bit(1);
+  }
+  void renorm() {
+    while (range_ < 256) {
+      if (low_ < 256) {
+        put(0);
+      } else if (low_ >= 512) {
+        low_ -= 512;
+        put(1);
+      } else {
+        low_ -= 256;
+        ++outstanding_;
+      }
+      range_ <<= 1;
+      low_ <<= 1;
+    }
+  }
+  void put(u32 b) {
+    if (first_) {
+      first_ = false;
+    } else {
+      bit(b);
+    }
+    while (outstanding_ > 0) {
+      bit(1 - b);
+      --outstanding_;
+    }
+  }
+  void bit(u32 b) {
+    cur_ = (cur_ << 1) | (b & 1u);
+    if (++nbits_ == 8) {
+      out_.push_back(u8(cur_));
+      cur_ = 0;
+      nbits_ = 0;
+    }
+  }
+  std::vector<u8>& out_;
+  u32 low_ = 0, range_ = 510;
+  bool first_ = true;
+  u32 outstanding_ = 0;
+  u32 cur_ = 0;
+  int nbits_ = 0;
+};
+
+}  // namespace vep::cabac

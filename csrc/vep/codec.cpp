@@ -2,6 +2,7 @@
 // reconstruction. See codec.h for the CPU/GPU split.
 #include "codec.h"
 
+#include "cabac.h"
 #include "color.h"
 
 namespace vep {
@@ -176,6 +177,205 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
   VEP_CHECK(got_slice, "access unit has no slice");
   upd.frames += 1;
   return pi;
+}
+
+// ------------------------------------------------------------------------------------ H.265
+
+void H265Parser::store_parameter_set(int t, const u8* p, size_t n) {
+  size_t rn;
+  const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn);
+  if (t == hevc::kVps) {
+    hevc::Vps v = hevc::parse_vps(r, rn);
+    vps_[v.vps_id] = v;
+  } else if (t == hevc::kSps) {
+    hevc::Sps s = hevc::parse_sps(r, rn);
+    sps_[s.sps_id] = s;
+  } else {
+    hevc::Pps q = hevc::parse_pps(r, rn);
+    pps_[q.pps_id] = q;
+  }
+}
+
+void H265Parser::absorb_parameter_sets(const AccessUnit& au) {
+  for (size_t i = 0; i < au.nals.size(); ++i) {
+    const u8* p = au.nal(i);
+    size_t n = au.nal_size(i);
+    if (n < 3) continue;
+    int t = hevc::nal_type(p);
+    if (t == hevc::kVps || t == hevc::kSps || t == hevc::kPps) store_parameter_set(t, p, n);
+  }
+}
+
+const hevc::Sps& H265Parser::active_sps() const {
+  VEP_CHECK(!sps_.empty(), "no active SPS");
+  auto it = sps_.find(active_sps_id_ < 0 ? sps_.begin()->first : active_sps_id_);
+  VEP_CHECK(it != sps_.end(), "no active SPS");
+  return it->second;
+}
+
+// Coding-tree walk of one slice segment (H.265 §7.3.8). With CtbLog2SizeY == MinCbLog2SizeY
+// every CTB is one CU and split_cu_flag is absent; per CU:
+//   P/B: cu_skip_flag (ctxInc = left skip + above skip, §9.3.4.2.2)
+//        skip -> merge_idx (TR, first bin context-coded) — every merge candidate is the zero
+//        MV on reference 0 in this subset, so a skipped CU keeps the reference samples;
+//        else pred_mode_flag must be MODE_INTRA
+//   part_mode bin 0 must be PART_2Nx2N, then pcm_flag (terminating bin) must be 1;
+//   PCM: alignment zeros, 384 raw sample bytes (16x16 Y, 8x8 Cb, 8x8 Cr), CABAC re-init;
+//   end_of_slice_segment_flag (terminating bin).
+void H265Parser::walk_slice(const u8* rbsp, size_t n, const hevc::SliceHeader& sh,
+                            const hevc::Sps& sps, const hevc::Pps& pps, MbUpdate& upd,
+                            int& coded) {
+  const int wctb = sps.width_ctbs(), total = wctb * sps.height_ctbs();
+  const bool inter = sh.slice_type != hevc::kI;
+  const int init_type = !inter ? 0 : (sh.slice_type == hevc::kP ? (sh.cabac_init ? 2 : 1)
+                                                                 : (sh.cabac_init ? 1 : 2));
+  const int qp = pps.init_qp + sh.qp_delta;
+  cabac::Ctx skip_ctx[3], pred_ctx, part_ctx, merge_ctx;
+  for (auto& c : skip_ctx) c.init(0, qp);
+  if (inter) {
+    const int skip_init[3] = {197, 185, 201};
+    for (int k = 0; k < 3; ++k) skip_ctx[k].init(skip_init[k], qp);
+    pred_ctx.init(init_type == 1 ? 149 : 134, qp);
+    merge_ctx.init(init_type == 1 ? 122 : 137, qp);
+  }
+  part_ctx.init(init_type == 0 ? 184 : 154, qp);
+  const int slice_addr = sh.segment_address;  // no dependent segments: slice == segment
+  cabac::Decoder dec(rbsp, n, sh.data_bytepos);
+  for (int ctb = sh.segment_address;; ++ctb) {
+    VEP_CHECK(ctb < total, "coding tree unit past end of picture");
+    bool skip = false;
+    if (inter) {
+      const int x = ctb % wctb;
+      const int l = (x > 0 && ctb - 1 >= slice_addr) ? skip_[size_t(ctb - 1)] : 0;
+      const int a = (ctb - wctb >= slice_addr) ? skip_[size_t(ctb - wctb)] : 0;
+      skip = dec.decision(skip_ctx[l + a]);
+    }
+    skip_[size_t(ctb)] = u8(skip);
+    if (skip) {
+      if (sh.max_num_merge_cand > 1 && dec.decision(merge_ctx))
+        for (int k = 1; k < sh.max_num_merge_cand - 1 && dec.bypass(); ++k) {
+        }
+    } else {
+      if (inter && !dec.decision(pred_ctx))
+        throw UnsupportedStream("inter-coded HEVC CU (native subset decodes PCM + skip only)");
+      if (!dec.decision(part_ctx)) throw UnsupportedStream("intra NxN HEVC CU is not supported");
+      if (!dec.terminate())
+        throw UnsupportedStream("regular intra HEVC CU (native subset decodes PCM + skip only)");
+      const size_t off = dec.aligned_bytepos();
+      VEP_CHECK(off + kPcmMbBytes <= n, "truncated PCM coding unit");
+      upd.set(ctb, rbsp + off);
+      ++coded;
+      dec.start(off + kPcmMbBytes);
+    }
+    if (dec.terminate()) break;  // end_of_slice_segment_flag
+  }
+}
+
+PictureInfo H265Parser::parse(const AccessUnit& au, MbUpdate& upd) {
+  PictureInfo pi;
+  bool got_slice = false;
+  for (size_t i = 0; i < au.nals.size(); ++i) {
+    const u8* p = au.nal(i);
+    size_t n = au.nal_size(i);
+    if (n < 3) continue;
+    const int t = hevc::nal_type(p);
+    if (t == hevc::kVps || t == hevc::kSps || t == hevc::kPps) {
+      store_parameter_set(t, p, n);
+      continue;
+    }
+    if (!hevc::is_vcl(t)) continue;
+    if (t > hevc::kTrailR && t < hevc::kBlaWLp)
+      throw UnsupportedStream("HEVC leading / sub-layer pictures are not supported");
+    size_t rn;
+    const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn);
+    std::shared_ptr<std::vector<u8>> owned;
+    if (r != p) {
+      owned = std::make_shared<std::vector<u8>>(r, r + rn);
+      r = owned->data();
+    }
+    const int pps_id = hevc::peek_slice_pps_id(r, rn);
+    auto pit = pps_.find(pps_id);
+    if (pit == pps_.end()) throw UnsupportedStream("slice references unknown PPS");
+    auto sit = sps_.find(pit->second.sps_id);
+    if (sit == sps_.end()) throw UnsupportedStream("slice references unknown SPS");
+    const hevc::Sps& sps = sit->second;
+    const hevc::Pps& pps = pit->second;
+    if (sps.chroma_format_idc != 1 || sps.bit_depth_luma != 8 || sps.bit_depth_chroma != 8)
+      throw UnsupportedStream("only 8-bit 4:2:0 HEVC is supported");
+    if (sps.log2_ctb != 4 || sps.log2_min_cb != 4 || !sps.pcm || sps.log2_min_pcm > 4 ||
+        sps.log2_max_pcm < 4 || sps.pcm_bit_depth_luma != 8 || sps.pcm_bit_depth_chroma != 8)
+      throw UnsupportedStream("native HEVC subset needs 16x16 CTBs coded as 8-bit PCM CUs");
+    if (pps.transquant_bypass || pps.tiles || pps.entropy_coding_sync)
+      throw UnsupportedStream("HEVC tiles / WPP / transquant bypass are not supported");
+    hevc::SliceHeader sh;
+    try {
+      sh = hevc::parse_slice_header(r, rn, sps, pps);
+    } catch (const UnsupportedStream&) {
+      throw;
+    } catch (const Error& e) {
+      throw UnsupportedStream(e.what());
+    }
+    if (sh.slice_type == hevc::kB) throw UnsupportedStream("HEVC B slices are not supported");
+    if (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled)
+      throw UnsupportedStream("HEVC in-loop filters (SAO / deblocking) are not supported");
+    if (sh.slice_type == hevc::kP && sh.num_ref_idx_l0 != 1)
+      throw UnsupportedStream("HEVC P slices with more than one reference are not supported");
+    active_sps_id_ = sps.sps_id;
+    if (!got_slice) {
+      pi.coded_width = sps.width;
+      pi.coded_height = sps.height;
+      pi.width = sps.out_width();
+      pi.height = sps.out_height();
+      pi.crop_left = sps.conf_left;
+      pi.crop_top = sps.conf_top;
+      pi.pict_type = sh.pict_char();
+      pi.idr = hevc::is_irap(t);
+      pi.frame_num = sh.poc_lsb;
+      pi.fps = sps.fps();
+      const int w = sps.width_ctbs(), h = sps.height_ctbs();
+      if (upd.width_mbs != w || upd.height_mbs != h) upd.reset(w, h);
+      skip_.assign(size_t(w) * h, 0);
+      got_slice = true;
+    }
+    if (owned) upd.own.push_back(owned);
+    upd.begin_segment(r, rn);
+    walk_slice(r, rn, sh, sps, pps, upd, pi.coded_mbs);
+  }
+  VEP_CHECK(got_slice, "access unit has no slice");
+  upd.frames += 1;
+  return pi;
+}
+
+// ------------------------------------------------------------------------------ ParamSets
+
+void ParamSets::absorb(const u8* p, size_t n) {
+  if (n < 2) return;
+  if (codec == Codec::kH264) {
+    const int t = nal_type(p[0]);
+    if (t == kNalSps) sps.assign(p, p + n);
+    else if (t == kNalPps) pps.assign(p, p + n);
+  } else {
+    const int t = hevc::nal_type(p);
+    if (t == hevc::kVps) vps.assign(p, p + n);
+    else if (t == hevc::kSps) sps.assign(p, p + n);
+    else if (t == hevc::kPps) pps.assign(p, p + n);
+  }
+}
+
+std::pair<int, int> ParamSets::size() const {
+  if (sps.empty()) return {0, 0};
+  std::vector<u8> r(sps.size());
+  const size_t n = ebsp_to_rbsp(sps.data(), sps.size(), r.data());
+  try {
+    if (codec == Codec::kH264) {
+      const Sps s = parse_sps(r.data(), n);
+      return {s.width(), s.height()};
+    }
+    const hevc::Sps s = hevc::parse_sps(r.data(), n);
+    return {s.out_width(), s.out_height()};
+  } catch (const std::exception&) {
+    return {0, 0};
+  }
 }
 
 void cpu_apply_update(const MbUpdate& upd, HostSurface& s) {

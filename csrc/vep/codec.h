@@ -18,6 +18,7 @@
 
 #include "common.h"
 #include "h264.h"
+#include "hevc.h"
 
 namespace vep {
 
@@ -43,6 +44,23 @@ struct AccessUnit {
   size_t bytes() const { return data.size(); }
 };
 using AuPtr = std::shared_ptr<const AccessUnit>;
+
+// Latest escaped parameter-set NALs of a stream (VPS only for H.265): what the muxers need for
+// avcC / hvcC and the FLV / enhanced-RTMP sequence header.
+struct ParamSets {
+  Codec codec = Codec::kH264;
+  std::vector<u8> vps, sps, pps;
+  void absorb(const u8* nal, size_t n);  // no-op for non-parameter-set NALs
+  void absorb(const AccessUnit& au) {
+    codec = au.codec;
+    for (size_t i = 0; i < au.nals.size(); ++i) absorb(au.nal(i), au.nal_size(i));
+  }
+  bool complete() const {
+    return !sps.empty() && !pps.empty() && (codec == Codec::kH264 || !vps.empty());
+  }
+  // Cropped output size from the SPS ({0, 0} if absent or unparsable).
+  std::pair<int, int> size() const;
+};
 
 // Accumulated macroblock updates for one camera surface; several AUs of a GOP can be
 // collapsed into one update (latest writer wins), which is how GOP catch-up
@@ -147,6 +165,54 @@ class H264Parser {
   std::vector<u8> sps_nal_, pps_nal_;
   std::vector<u8> rbsp_scratch_;
   std::vector<u32> epb_;
+};
+
+// Stateful H.265 AU parser: the CABAC coding-tree walk of the native HEVC subset — 16x16 CTBs
+// (= minimum CU = PCM CU size), PCM intra CUs, skipped inter CUs with a single reference and
+// zero merge candidates, no SAO/deblocking. PCM CU samples are laid out exactly like an H.264
+// I_PCM macroblock (256 luma, 64 Cb, 64 Cr), so the same MbUpdate / GPU kernel reconstructs
+// both codecs. Everything else throws UnsupportedStream.
+class H265Parser {
+ public:
+  PictureInfo parse(const AccessUnit& au, MbUpdate& upd);
+  void absorb_parameter_sets(const AccessUnit& au);
+  bool has_sps() const { return !sps_.empty(); }
+  const hevc::Sps& active_sps() const;
+
+ private:
+  void store_parameter_set(int type, const u8* p, size_t n);
+  void walk_slice(const u8* rbsp, size_t n, const hevc::SliceHeader& sh, const hevc::Sps& sps,
+                  const hevc::Pps& pps, MbUpdate& upd, int& coded);
+  std::map<int, hevc::Vps> vps_;
+  std::map<int, hevc::Sps> sps_;
+  std::map<int, hevc::Pps> pps_;
+  int active_sps_id_ = -1;
+  std::vector<u8> rbsp_scratch_;
+  std::vector<u32> epb_;
+  std::vector<u8> skip_;  // per-CTB cu_skip_flag of the current picture (ctxInc derivation)
+};
+
+// Codec dispatcher used by cameras (the codec comes from the SDP / AU).
+class StreamParser {
+ public:
+  PictureInfo parse(const AccessUnit& au, MbUpdate& upd) {
+    codec_ = au.codec;
+    return au.codec == Codec::kH265 ? h265_.parse(au, upd) : h264_.parse(au, upd);
+  }
+  void absorb_parameter_sets(const AccessUnit& au) {
+    codec_ = au.codec;
+    if (au.codec == Codec::kH265) h265_.absorb_parameter_sets(au);
+    else h264_.absorb_parameter_sets(au);
+  }
+  bool has_sps() const { return codec_ == Codec::kH265 ? h265_.has_sps() : h264_.has_sps(); }
+  Codec codec() const { return codec_; }
+  H264Parser& h264() { return h264_; }
+  H265Parser& h265() { return h265_; }
+
+ private:
+  Codec codec_ = Codec::kH264;
+  H264Parser h264_;
+  H265Parser h265_;
 };
 
 // Host NV12 surface (CPU backend / test oracle).

@@ -2,6 +2,7 @@
 #include <algorithm>
 
 #include "h264.h"
+#include "hevc.h"
 #include "mux.h"
 #include "net.h"
 #include "sock.h"
@@ -42,6 +43,24 @@ std::vector<u8> flv_avc_sequence_header(const std::vector<u8>& sps, const std::v
 
 std::vector<u8> flv_avc_nalu(const AccessUnit& au) {
   std::vector<u8> b = {u8(au.keyframe ? 0x17 : 0x27), 0x01, 0x00, 0x00, 0x00};
+  std::vector<u8> a = au_to_avcc(au);
+  b.insert(b.end(), a.begin(), a.end());
+  return b;
+}
+
+std::vector<u8> flv_sequence_header(const ParamSets& ps) {
+  if (ps.codec == Codec::kH264) return flv_avc_sequence_header(ps.sps, ps.pps);
+  // IsExHeader | FrameType 1 (key) | PacketType 0 (SequenceStart), FourCC, hvcC
+  std::vector<u8> b = {u8(0x80 | (1 << 4) | 0), 'h', 'v', 'c', '1'};
+  std::vector<u8> rec = hevc::hvcc_record(ps.vps, ps.sps, ps.pps);
+  b.insert(b.end(), rec.begin(), rec.end());
+  return b;
+}
+
+std::vector<u8> flv_video(const AccessUnit& au) {
+  if (au.codec == Codec::kH264) return flv_avc_nalu(au);
+  // PacketType 3 (CodedFramesX: composition time 0 implied), length-prefixed NAL units
+  std::vector<u8> b = {u8(0x80 | ((au.keyframe ? 1 : 2) << 4) | 3), 'h', 'v', 'c', '1'};
   std::vector<u8> a = au_to_avcc(au);
   b.insert(b.end(), a.begin(), a.end());
   return b;
@@ -401,12 +420,12 @@ void RtmpPublisher::connect() {
   wait_for("onStatus", nullptr);
 }
 
-void RtmpPublisher::send_sequence_header(const std::vector<u8>& sps, const std::vector<u8>& pps) {
-  send_message(6, 9, stream_id_, 0, flv_avc_sequence_header(sps, pps));
+void RtmpPublisher::send_sequence_header(const ParamSets& ps) {
+  send_message(6, 9, stream_id_, 0, flv_sequence_header(ps));
 }
 
 void RtmpPublisher::send_au(const AccessUnit& au, u32 ts_ms) {
-  send_message(6, 9, stream_id_, ts_ms, flv_avc_nalu(au));
+  send_message(6, 9, stream_id_, ts_ms, flv_video(au));
 }
 
 // ---------------------------------------------------------------------------------- sink
@@ -473,7 +492,15 @@ void RtmpSink::serve(int fd) {
       }
       if (type == 9) {
         std::lock_guard<std::mutex> g(mu_);
-        if (body.size() >= 2) {
+        if (body.size() >= 5 && (body[0] & 0x80)) {  // enhanced RTMP
+          const int pkt = body[0] & 0x0f, ftype = (body[0] >> 4) & 7;
+          if (std::memcmp(&body[1], "hvc1", 4) == 0) hevc_.fetch_add(1);
+          if (pkt == 0) seqhdr_.fetch_add(1);
+          else if (pkt == 1 || pkt == 3) {
+            video_.fetch_add(1);
+            if (ftype == 1) keys_.fetch_add(1);
+          }
+        } else if (body.size() >= 2) {
           if (body[1] == 0) seqhdr_.fetch_add(1);
           else {
             video_.fetch_add(1);

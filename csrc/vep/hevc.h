@@ -1,0 +1,163 @@
+// H.265/HEVC NAL, parameter-set and slice-segment-header layer (ITU-T H.265 §7.3) plus the
+// HEVCDecoderConfigurationRecord (ISO/IEC 14496-15 §8.3.3) used by MP4 (hvcC) and enhanced-RTMP.
+//
+// The parsers read the general syntax (profile_tier_level with sub-layers, scaling lists,
+// inter-predicted short-term RPS, long-term refs, VUI timing) so any real camera's parameter
+// sets can be probed for size / frame rate; the native subset *decoder* (H265Parser in codec.h)
+// then accepts the subset the synthetic farm emits and reports everything else as
+// UnsupportedStream (the RocDecode/VCN backend's job — SURVEY.md §7.4 hard part 1).
+//
+// Reference parity: libavcodec hevc parser/decoder behind PyAV (python/read_image.py:87,
+// python/rtsp_to_rtmp.py:92); BASELINE.json config 5 ("64x 4K30 H.265").
+#pragma once
+
+#include "bits.h"
+#include "common.h"
+
+namespace vep::hevc {
+
+enum NalType : int {
+  kTrailN = 0,
+  kTrailR = 1,
+  kBlaWLp = 16,
+  kIdrWRadl = 19,
+  kIdrNLp = 20,
+  kCra = 21,
+  kRsvIrap23 = 23,
+  kVps = 32,
+  kSps = 33,
+  kPps = 34,
+  kAud = 35,
+  kSeiPrefix = 39,
+  kSeiSuffix = 40,
+  kAp = 48,  // RTP aggregation packet (RFC 7798)
+  kFu = 49,  // RTP fragmentation unit (RFC 7798)
+};
+
+inline int nal_type(const u8* hdr) { return (hdr[0] >> 1) & 0x3f; }
+inline bool is_irap(int t) { return t >= kBlaWLp && t <= kRsvIrap23; }
+inline bool is_idr(int t) { return t == kIdrWRadl || t == kIdrNLp; }
+inline bool is_vcl(int t) { return t < 32; }
+
+struct ProfileTierLevel {
+  int profile_space = 0, tier = 0, profile_idc = 1;
+  u32 compat_flags = 0x60000000;     // Main + Main-compatible bits (1 and 2)
+  u64 constraint_flags = 0x900000000000ull;  // 48 bits: progressive_source + frame_only
+  int level_idc = 153;               // level 5.1 (x30)
+};
+
+struct ShortTermRps {
+  int num_negative = 0, num_positive = 0;
+  int delta_poc[32] = {};            // negatives then positives
+  bool used[32] = {};
+  int num_delta() const { return num_negative + num_positive; }
+};
+
+struct Vps {
+  int vps_id = 0;
+  int max_sub_layers = 1;
+  ProfileTierLevel ptl;
+  bool timing_info = false;
+  u32 num_units_in_tick = 0, time_scale = 0;
+};
+
+struct Sps {
+  int vps_id = 0, sps_id = 0, max_sub_layers = 1;
+  ProfileTierLevel ptl;
+  int chroma_format_idc = 1;
+  bool separate_colour_plane = false;
+  int width = 0, height = 0;                 // pic_{width,height}_in_luma_samples (coded)
+  int conf_left = 0, conf_right = 0, conf_top = 0, conf_bottom = 0;  // in luma samples
+  int bit_depth_luma = 8, bit_depth_chroma = 8;
+  int log2_max_poc_lsb = 8;
+  int max_dec_pic_buffering = 2, max_num_reorder = 0, max_latency_increase_plus1 = 0;
+  int log2_min_cb = 4, log2_ctb = 4;
+  int log2_min_tb = 2, log2_max_tb = 4;
+  int max_th_depth_inter = 0, max_th_depth_intra = 0;
+  bool scaling_list = false, amp = false, sao = false;
+  bool pcm = true;
+  int pcm_bit_depth_luma = 8, pcm_bit_depth_chroma = 8;
+  int log2_min_pcm = 4, log2_max_pcm = 4;
+  bool pcm_loop_filter_disabled = true;
+  std::vector<ShortTermRps> st_rps;
+  bool long_term_refs = false;
+  int num_long_term_ref_pics_sps = 0;
+  bool temporal_mvp = false, strong_intra_smoothing = false;
+  bool vui = false, video_signal_type = false;
+  int video_format = 5, matrix_coeffs = 6;
+  bool full_range = false;
+  bool timing_info = false;
+  u32 num_units_in_tick = 0, time_scale = 0;
+
+  int ctb_size() const { return 1 << log2_ctb; }
+  int width_ctbs() const { return (width + ctb_size() - 1) >> log2_ctb; }
+  int height_ctbs() const { return (height + ctb_size() - 1) >> log2_ctb; }
+  int out_width() const { return width - conf_left - conf_right; }
+  int out_height() const { return height - conf_top - conf_bottom; }
+  double fps() const {
+    return (timing_info && num_units_in_tick) ? double(time_scale) / num_units_in_tick : 0.0;
+  }
+};
+
+struct Pps {
+  int pps_id = 0, sps_id = 0;
+  bool dependent_slice_segments = false, output_flag_present = false;
+  int num_extra_slice_header_bits = 0;
+  bool sign_data_hiding = false, cabac_init_present = false;
+  int num_ref_idx_l0_default = 1, num_ref_idx_l1_default = 1;
+  int init_qp = 26;
+  bool constrained_intra_pred = false, transform_skip = false, cu_qp_delta = false;
+  int cb_qp_offset = 0, cr_qp_offset = 0;
+  bool slice_chroma_qp_offsets_present = false;
+  bool weighted_pred = false, weighted_bipred = false, transquant_bypass = false;
+  bool tiles = false, entropy_coding_sync = false;
+  bool loop_filter_across_slices = false;
+  bool deblocking_control = true, deblocking_override_enabled = false, deblocking_disabled = true;
+  bool scaling_list = false, lists_modification = false;
+  int log2_parallel_merge_level = 2;
+  bool slice_header_extension = false;
+};
+
+enum SliceType : int { kB = 0, kP = 1, kI = 2 };
+
+struct SliceHeader {
+  int nal_type = 0;
+  bool first_slice_in_pic = true;
+  int pps_id = 0;
+  bool dependent = false;
+  int segment_address = 0;                   // CTB raster address
+  int slice_type = kI;
+  int poc_lsb = 0;
+  int num_ref_idx_l0 = 1;
+  bool cabac_init = false;
+  int max_num_merge_cand = 5;
+  int qp_delta = 0;
+  bool deblocking_disabled = true;
+  bool sao_luma = false, sao_chroma = false;
+  bool temporal_mvp = false;
+  int num_entry_points = 0;
+  size_t data_bytepos = 0;                   // slice_segment_data() start within the RBSP
+  char pict_char() const { return slice_type == kI ? 'I' : slice_type == kP ? 'P' : 'B'; }
+};
+
+// Parsers take the RBSP *including* the 2-byte NAL header.
+Vps parse_vps(const u8* rbsp, size_t n);
+Sps parse_sps(const u8* rbsp, size_t n);
+Pps parse_pps(const u8* rbsp, size_t n);
+// pps_id of a slice segment (first fields of the header) without full parsing.
+int peek_slice_pps_id(const u8* rbsp, size_t n);
+SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const Pps& pps);
+
+// Writers (RBSP including the NAL header) for the synthetic encoder.
+std::vector<u8> write_vps(const Vps& v);
+std::vector<u8> write_sps(const Sps& s);
+std::vector<u8> write_pps(const Pps& p);
+// Writes the slice segment header through byte_alignment(); CABAC data follows.
+void write_slice_header(BitWriter& bw, const SliceHeader& sh, const Sps& sps, const Pps& pps);
+std::vector<u8> nal_header(int type, int tid_plus1 = 1);
+
+// HEVCDecoderConfigurationRecord from escaped VPS/SPS/PPS NALs (MP4 hvcC, enhanced-RTMP).
+std::vector<u8> hvcc_record(const std::vector<u8>& vps, const std::vector<u8>& sps,
+                            const std::vector<u8>& pps);
+
+}  // namespace vep::hevc

@@ -1,6 +1,8 @@
 // Ingest session / supervisor implementation. See ingest.h.
 #include "ingest.h"
 
+#include <tuple>
+
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -52,33 +54,17 @@ void IngestSession::on_au(const AuPtr& au) {
     std::lock_guard<std::mutex> g(mu_);
     st_.aus++;
   }
-  if (au->codec == Codec::kH264) {
-    for (size_t i = 0; i < au->nals.size(); ++i) {
-      int t = au->nal(i)[0] & 0x1f;
-      if (t == h264::kNalSps) sps_.assign(au->nal(i), au->nal(i) + au->nal_size(i));
-      if (t == h264::kNalPps) pps_.assign(au->nal(i), au->nal(i) + au->nal_size(i));
-    }
-  }
+  ps_.absorb(*au);
   // --- archive: previous GOP goes to the archiver on every keyframe (rtsp_to_rtmp.py:97-110)
   if (au->keyframe) {
-    if (!gop_.empty() && archiver_ && !cfg_.disk_path.empty() && !sps_.empty() && !pps_.empty()) {
+    if (!gop_.empty() && archiver_ && !cfg_.disk_path.empty() && ps_.complete()) {
       mux::Mp4Info info;
       if (cam->ring()) {
         info.width = cam->ring()->width();
         info.height = cam->ring()->height();
       }
-      if (info.width == 0 && !sps_.empty()) {
-        std::vector<u8> r(sps_.size());
-        size_t n = ebsp_to_rbsp(sps_.data(), sps_.size(), r.data());
-        try {
-          h264::Sps s = h264::parse_sps(r.data(), n);
-          info.width = s.width();
-          info.height = s.height();
-        } catch (...) {
-        }
-      }
-      info.sps = sps_;
-      info.pps = pps_;
+      if (info.width == 0) std::tie(info.width, info.height) = ps_.size();
+      info.ps = ps_;
       archiver_->enqueue(cfg_.disk_path, cfg_.name, gop_start_ms_, std::move(gop_), info);
     }
     gop_.clear();
@@ -117,7 +103,7 @@ void IngestSession::on_au(const AuPtr& au) {
     };
     if (rising || pub_->messages() == 0) {
       // start the stream at a keyframe: sequence header + the whole current GOP
-      if (!sps_.empty() && !pps_.empty()) pub_->send_sequence_header(sps_, pps_);
+      if (ps_.complete()) pub_->send_sequence_header(ps_);
       for (auto& p : gop_) pub_->send_au(*p, ts_ms(*p));
     } else {
       pub_->send_au(*au, ts_ms(*au));
@@ -159,12 +145,8 @@ void IngestSession::run() {
         st_.health = "healthy";
         st_.fps = info.framerate;
       }
-      for (auto& ps : info.param_sets) {
-        if (ps.empty()) continue;
-        int t = ps[0] & 0x1f;
-        if (t == h264::kNalSps) sps_ = ps;
-        if (t == h264::kNalPps) pps_ = ps;
-      }
+      ps_.codec = info.codec;
+      for (auto& ps : info.param_sets) ps_.absorb(ps.data(), ps.size());
       log(false, "connected to " + cfg_.name + " (" +
                      (info.codec == Codec::kH264 ? "H.264" : "H.265") + ")");
       std::string why = client.run([this](const AuPtr& au) { on_au(au); }, stop_);

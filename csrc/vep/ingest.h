@@ -76,7 +76,7 @@ class IngestSession {
   bool prev_proxy_ = false;
   i64 pub_retry_at_ = 0;
   i64 pub_ts0_ = -1;
-  std::vector<u8> sps_, pps_;
+  ParamSets ps_;
   std::vector<AuPtr> gop_;
   i64 gop_start_ms_ = 0;
   bool seen_key_ = false;

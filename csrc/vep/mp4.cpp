@@ -10,6 +10,7 @@
 #include <cstdio>
 
 #include "h264.h"
+#include "hevc.h"
 #include "mux.h"
 
 namespace vep::mux {
@@ -63,7 +64,8 @@ i64 segment_duration_ms(const std::vector<AuPtr>& aus) {
 
 std::vector<u8> build_mp4(const std::vector<AuPtr>& aus, const Mp4Info& info) {
   VEP_CHECK(!aus.empty(), "empty GOP");
-  VEP_CHECK(!info.sps.empty() && !info.pps.empty(), "MP4 needs SPS/PPS");
+  VEP_CHECK(info.ps.complete(), "MP4 needs the stream's parameter sets");
+  const bool hevc = info.ps.codec == Codec::kH265;
   const u32 ts = 90000;
   const i64 base = aus.front()->dts;
   std::vector<std::vector<u8>> samples;
@@ -83,7 +85,7 @@ std::vector<u8> build_mp4(const std::vector<AuPtr>& aus, const Mp4Info& info) {
   Box ftyp("ftyp");
   ftyp.bytes("isom", 4);
   ftyp.u32_(0x200);
-  ftyp.bytes("isomiso2avc1mp41", 16);
+  ftyp.bytes(hevc ? "isomiso2hvc1mp41" : "isomiso2avc1mp41", 16);
 
   auto build_moov = [&](u32 chunk_offset) {
     Box mvhd("mvhd");
@@ -145,10 +147,11 @@ std::vector<u8> build_mp4(const std::vector<AuPtr>& aus, const Mp4Info& info) {
     Box dinf("dinf");
     dinf.add(dref);
 
-    Box avcc("avcC");
-    std::vector<u8> rec = h264::avcc_record(info.sps, info.pps);
+    Box avcc(hevc ? "hvcC" : "avcC");
+    std::vector<u8> rec = hevc ? hevc::hvcc_record(info.ps.vps, info.ps.sps, info.ps.pps)
+                               : h264::avcc_record(info.ps.sps, info.ps.pps);
     avcc.bytes(rec.data(), rec.size());
-    Box avc1("avc1");
+    Box avc1(hevc ? "hvc1" : "avc1");
     avc1.zeros(6);
     avc1.u16_(1);
     avc1.zeros(16);

@@ -21,9 +21,13 @@ namespace vep::mux {
 // NAL units of an AU re-framed as 4-byte-length AVCC, dropping SPS/PPS/AUD (carried in avcC).
 std::vector<u8> au_to_avcc(const AccessUnit& au);
 
-// FLV VIDEODATA bodies (without the 11-byte tag header).
+// FLV VIDEODATA bodies (without the 11-byte tag header). H.264 uses the classic AVC tags
+// (CodecID 7); H.265 uses enhanced RTMP (IsExHeader, FourCC 'hvc1', SequenceStart /
+// CodedFramesX), which FFmpeg >= 6.1, OBS and the major ingest services accept.
 std::vector<u8> flv_avc_sequence_header(const std::vector<u8>& sps, const std::vector<u8>& pps);
 std::vector<u8> flv_avc_nalu(const AccessUnit& au);
+std::vector<u8> flv_sequence_header(const ParamSets& ps);
+std::vector<u8> flv_video(const AccessUnit& au);
 // Complete FLV tag (header + body + PreviousTagSize).
 std::vector<u8> flv_tag(u8 type, u32 ts_ms, const std::vector<u8>& body);
 std::vector<u8> flv_file_header();
@@ -35,7 +39,7 @@ class RtmpPublisher {
   ~RtmpPublisher();
   void connect();
   bool connected() const { return fd_ >= 0; }
-  void send_sequence_header(const std::vector<u8>& sps, const std::vector<u8>& pps);
+  void send_sequence_header(const ParamSets& ps);
   void send_au(const AccessUnit& au, u32 ts_ms);
   void close();
   u64 bytes_sent() const { return sent_; }
@@ -63,6 +67,7 @@ class RtmpSink {
   u64 video_messages() const { return video_.load(); }
   u64 keyframes() const { return keys_.load(); }
   u64 sequence_headers() const { return seqhdr_.load(); }
+  u64 hevc_messages() const { return hevc_.load(); }  // enhanced-RTMP 'hvc1' video messages
   std::string last_stream_key() const;
   std::vector<std::vector<u8>> video_bodies() const;  // FLV VIDEODATA bodies in arrival order
 
@@ -73,7 +78,7 @@ class RtmpSink {
   std::atomic<bool> stop_{false};
   std::thread acc_;
   std::atomic<int> live_{0};
-  std::atomic<u64> video_{0}, keys_{0}, seqhdr_{0};
+  std::atomic<u64> video_{0}, keys_{0}, seqhdr_{0}, hevc_{0};
   mutable std::mutex mu_;
   std::string key_;
   std::vector<std::vector<u8>> bodies_;
@@ -82,7 +87,7 @@ class RtmpSink {
 // One MP4 file for a GOP of access units (timestamps rebased to the first DTS).
 struct Mp4Info {
   int width = 0, height = 0;
-  std::vector<u8> sps, pps;
+  ParamSets ps;  // avc1/avcC for H.264, hvc1/hvcC for H.265
 };
 std::vector<u8> build_mp4(const std::vector<AuPtr>& aus, const Mp4Info& info);
 // Segment length in ms per archive.py:45-73 (sum of durations, else DTS span).

@@ -161,7 +161,7 @@ class RtspServer {
   struct Stream {
     ServedStream cfg;
     std::vector<AuPtr> cache;
-    std::vector<u8> sps, pps;
+    std::vector<u8> sps, pps, vps;
     std::atomic<int> fault{0};
   };
   void accept_loop();

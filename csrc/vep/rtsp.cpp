@@ -400,6 +400,7 @@ void RtspServer::add_stream(const std::string& path, const ServedStream& s) {
   SynthH264 enc(s.cfg);
   st->sps = enc.sps_nal();
   st->pps = enc.pps_nal();
+  st->vps = enc.vps_nal();
   if (s.cached_frames > 0)
     for (int i = 0; i < s.cached_frames; ++i) st->cache.push_back(enc.next());
   std::lock_guard<std::mutex> g(mu_);
@@ -529,13 +530,21 @@ void RtspServer::serve(int fd) {
     if (method == "DESCRIBE") {
       std::string sps64 = base64_encode(st->sps.data(), st->sps.size());
       std::string pps64 = base64_encode(st->pps.data(), st->pps.size());
-      char pli[8];
-      snprintf(pli, sizeof(pli), "%02X%02X%02X", st->sps[1], st->sps[2], st->sps[3]);
-      std::string sdp = "v=0\r\no=- 0 0 IN IP4 " + bind_ + "\r\ns=vep synthetic camera\r\nt=0 0\r\n"
-                        "m=video 0 RTP/AVP 96\r\na=rtpmap:96 H264/90000\r\n"
-                        "a=fmtp:96 packetization-mode=1;profile-level-id=" + std::string(pli) +
-                        ";sprop-parameter-sets=" + sps64 + "," + pps64 + "\r\n"
-                        "a=control:trackID=0\r\na=framerate:" + std::to_string(st->cfg.cfg.fps) + "\r\n";
+      std::string media;
+      if (st->cfg.cfg.codec == Codec::kH265) {  // RFC 7798 §7.1
+        std::string vps64 = base64_encode(st->vps.data(), st->vps.size());
+        media = "m=video 0 RTP/AVP 96\r\na=rtpmap:96 H265/90000\r\n"
+                "a=fmtp:96 sprop-vps=" + vps64 + ";sprop-sps=" + sps64 + ";sprop-pps=" + pps64 + "\r\n";
+      } else {  // RFC 6184 §8.1
+        char pli[8];
+        snprintf(pli, sizeof(pli), "%02X%02X%02X", st->sps[1], st->sps[2], st->sps[3]);
+        media = "m=video 0 RTP/AVP 96\r\na=rtpmap:96 H264/90000\r\n"
+                "a=fmtp:96 packetization-mode=1;profile-level-id=" + std::string(pli) +
+                ";sprop-parameter-sets=" + sps64 + "," + pps64 + "\r\n";
+      }
+      std::string sdp = "v=0\r\no=- 0 0 IN IP4 " + bind_ + "\r\ns=vep synthetic camera\r\nt=0 0\r\n" +
+                        media + "a=control:trackID=0\r\na=framerate:" +
+                        std::to_string(st->cfg.cfg.fps) + "\r\n";
       std::string base = "rtsp://" + bind_ + ":" + std::to_string(port_) + path + "/";
       reply(200, "OK", cseq, "Content-Type: application/sdp\r\nContent-Base: " + base + "\r\n", sdp);
     } else if (method == "SETUP") {
@@ -560,6 +569,7 @@ void RtspServer::serve(int fd) {
     std::unique_ptr<SynthH264> enc;
     if (st->cache.empty()) enc = std::make_unique<SynthH264>(st->cfg.cfg);
     const int fps = std::max(1, st->cfg.cfg.fps);
+    const Codec codec = st->cfg.cfg.codec;
     RtpHeader h;
     h.ssrc = 0x5ee0000u ^ u32(fd);
     h.seq = u16(fd * 7919);
@@ -611,14 +621,15 @@ void RtspServer::serve(int fd) {
       for (size_t i = 0; i < au->nals.size(); ++i) {
         pk.clear();
         std::vector<u8> nal(au->nal(i), au->nal(i) + au->nal_size(i));
-        if (fault == int(Fault::kCorruptNal) && ((nal[0] & 0x1f) == 1 || (nal[0] & 0x1f) == 5) &&
-            nal.size() > 16) {
+        const bool vcl = codec == Codec::kH264 ? ((nal[0] & 0x1f) == 1 || (nal[0] & 0x1f) == 5)
+                                               : ((nal[0] >> 1) & 0x3f) < 32;
+        if (fault == int(Fault::kCorruptNal) && vcl && nal.size() > 16) {
           for (size_t j = 4; j < nal.size(); j += 97) nal[j] ^= 0x5a;
           nal[4] = 0x00;  // break the slice header / mb_type
           nal[5] = 0x00;
           nal[6] = 0x01;  // embedded start code: an emulation-prevention violation
         }
-        packetize_nal(Codec::kH264, nal.data(), nal.size(), 1400, pk);
+        packetize_nal(codec, nal.data(), nal.size(), 1400, pk);
         for (size_t j = 0; j < pk.size(); ++j) {
           h.marker = (i + 1 == au->nals.size()) && (j + 1 == pk.size());
           size_t len = kRtpHeader + pk[j].size();

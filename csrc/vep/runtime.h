@@ -138,7 +138,7 @@ class Camera {
   LogRing logs;
 
   FrameRing* ring() const { return ring_.get(); }
-  H264Parser& parser() { return parser_; }
+  StreamParser& parser() { return parser_; }
   std::mutex& gop_mutex() { return mu_; }
   std::vector<AuPtr> gop_snapshot();   // current GOP packets (for RTMP flush / archive)
 
@@ -162,7 +162,7 @@ class Camera {
   std::vector<AuPtr> gop_;
   size_t decoded_upto_ = 0;  // gop_[0, decoded_upto_) are reconstructed on the surface
   i64 keyframes_ = 0;
-  H264Parser parser_;
+  StreamParser parser_;
 };
 
 struct WorkerOptions {

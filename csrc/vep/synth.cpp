@@ -4,6 +4,8 @@
 #include <algorithm>
 #include <cmath>
 
+#include "cabac.h"
+
 namespace vep {
 
 using namespace h264;
@@ -27,10 +29,40 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
   sps_.num_units_in_tick = 1;
   sps_.time_scale = u32(2 * cfg.fps);
   pps_.deblocking_filter_control = true;
-  std::vector<u8> r = write_sps(sps_);
-  rbsp_to_ebsp(r.data(), r.size(), sps_nal_);
-  r = write_pps(pps_);
-  rbsp_to_ebsp(r.data(), r.size(), pps_nal_);
+  if (cfg.codec == Codec::kH265) {
+    VEP_CHECK(cfg.merge_cands >= 1 && cfg.merge_cands <= 5, "merge_cands must be 1..5");
+    hvps_.timing_info = true;
+    hvps_.num_units_in_tick = 1;
+    hvps_.time_scale = u32(cfg.fps);
+    hsps_.width = wmbs_ * 16;
+    hsps_.height = hmbs_ * 16;
+    hsps_.conf_right = wmbs_ * 16 - cfg.width;
+    hsps_.conf_bottom = hmbs_ * 16 - cfg.height;
+    hsps_.ptl.level_idc = (cfg.width * cfg.height > 2228224) ? 153 : 123;  // 5.1 / 4.1
+    hevc::ShortTermRps rps;
+    rps.num_negative = 1;
+    rps.delta_poc[0] = -1;
+    rps.used[0] = true;
+    hsps_.st_rps = {rps};
+    hsps_.vui = true;
+    hsps_.video_signal_type = true;
+    hsps_.timing_info = true;
+    hsps_.num_units_in_tick = 1;
+    hsps_.time_scale = u32(cfg.fps);
+    for (auto* pr : {&vps_nal_, &sps_nal_, &pps_nal_}) pr->clear();
+    std::vector<u8> r = hevc::write_vps(hvps_);
+    rbsp_to_ebsp(r.data(), r.size(), vps_nal_);
+    r = hevc::write_sps(hsps_);
+    rbsp_to_ebsp(r.data(), r.size(), sps_nal_);
+    r = hevc::write_pps(hpps_);
+    rbsp_to_ebsp(r.data(), r.size(), pps_nal_);
+    skip_.assign(size_t(wmbs_) * hmbs_, 0);
+  } else {
+    std::vector<u8> r = write_sps(sps_);
+    rbsp_to_ebsp(r.data(), r.size(), sps_nal_);
+    r = write_pps(pps_);
+    rbsp_to_ebsp(r.data(), r.size(), pps_nal_);
+  }
   pic_.alloc(wmbs_ * 16, hmbs_ * 16);
   bg_.alloc(wmbs_ * 16, hmbs_ * 16);
   state_ = cfg.seed * 0x9E3779B97F4A7C15ull + 0x1234567ull;
@@ -154,13 +186,70 @@ std::vector<u8> SynthH264::encode_slice(bool idr, int mb0, int mb1,
   return nal;
 }
 
+// HEVC slice segment: one CU per 16x16 CTB; see H265Parser::walk_slice for the syntax.
+std::vector<u8> SynthH264::encode_slice_hevc(bool idr, int ctb0, int ctb1,
+                                             const std::vector<u8>& coded) {
+  BitWriter bw;
+  hevc::SliceHeader sh;
+  sh.nal_type = idr ? hevc::kIdrWRadl : hevc::kTrailR;
+  sh.first_slice_in_pic = ctb0 == 0;
+  sh.segment_address = ctb0;
+  sh.slice_type = idr ? hevc::kI : hevc::kP;
+  sh.poc_lsb = poc_;
+  sh.max_num_merge_cand = cfg_.merge_cands;
+  hevc::write_slice_header(bw, sh, hsps_, hpps_);
+  std::vector<u8> out = std::move(bw.buf());
+  const int qp = hpps_.init_qp + sh.qp_delta;
+  cabac::Ctx skip_ctx[3], pred_ctx, part_ctx, merge_ctx;
+  const int skip_init[3] = {197, 185, 201};
+  for (int k = 0; k < 3; ++k) skip_ctx[k].init(skip_init[k], qp);
+  pred_ctx.init(149, qp);
+  merge_ctx.init(122, qp);
+  part_ctx.init(idr ? 184 : 154, qp);
+  cabac::Encoder enc(out);
+  u8 buf[kPcmMbBytes];
+  for (int ctb = ctb0; ctb < ctb1; ++ctb) {
+    const bool pcm = idr || coded[size_t(ctb)];
+    if (!idr) {
+      const int x = ctb % wmbs_;
+      const int l = (x > 0 && ctb - 1 >= ctb0) ? skip_[size_t(ctb - 1)] : 0;
+      const int a = (ctb - wmbs_ >= ctb0) ? skip_[size_t(ctb - wmbs_)] : 0;
+      enc.decision(skip_ctx[l + a], pcm ? 0 : 1);
+      skip_[size_t(ctb)] = u8(!pcm);
+      if (!pcm && cfg_.merge_cands > 1) {
+        const int idx = ctb % cfg_.merge_cands;  // any candidate: all are the zero MV
+        enc.decision(merge_ctx, idx > 0);
+        for (int k = 1; k < cfg_.merge_cands - 1 && idx > 0; ++k) {
+          enc.bypass(idx > k);
+          if (idx <= k) break;
+        }
+      }
+      if (pcm) enc.decision(pred_ctx, 1);  // MODE_INTRA
+    }
+    if (pcm) {
+      enc.decision(part_ctx, 1);  // PART_2Nx2N
+      enc.terminate(1);           // pcm_flag
+      enc.align_zero();           // pcm_alignment_zero_bit
+      pcm_payload(ctb, buf);
+      enc.raw_bytes(buf, kPcmMbBytes);
+      enc.start();
+    }
+    enc.terminate(ctb + 1 == ctb1 ? 1 : 0);  // end_of_slice_segment_flag
+  }
+  enc.align_zero();  // rbsp_slice_segment_trailing_bits (the stop bit ends the flush)
+  std::vector<u8> nal;
+  rbsp_to_ebsp(out.data(), out.size(), nal);
+  return nal;
+}
+
 std::shared_ptr<AccessUnit> SynthH264::next() {
   ++frame_;
   // frame 0 is always an IDR; later IDRs fall where (frame + phase) % gop == 0 so that a fleet
   // of cameras does not refresh in lock-step
   const bool idr = frame_ == 0 || ((frame_ + cfg_.idr_phase) % cfg_.gop) == 0;
   auto au = std::make_shared<AccessUnit>();
-  au->codec = Codec::kH264;
+  const bool h265 = cfg_.codec == Codec::kH265;
+  au->codec = cfg_.codec;
   au->pts = au->dts = frame_ * 90000 / cfg_.fps;
   au->duration = 90000 / cfg_.fps;
   au->keyframe = idr;
@@ -175,11 +264,14 @@ std::shared_ptr<AccessUnit> SynthH264::next() {
     pic_.uv = bg_.uv;
     if (bw_) paint_box(box);
     frame_num_ = 0;
+    poc_ = 0;
     idr_id_ = (idr_id_ + 1) & 0xffff;
+    if (h265) au->add_nal(vps_nal_.data(), vps_nal_.size());
     au->add_nal(sps_nal_.data(), sps_nal_.size());
     au->add_nal(pps_nal_.data(), pps_nal_.size());
   } else {
     frame_num_ = (frame_num_ + 1) % (1 << sps_.log2_max_frame_num);
+    ++poc_;
     // restore background under the previous box, paint the new one
     const int W = pic_.coded_w;
     const Rect& o = prev_box_;
@@ -198,7 +290,8 @@ std::shared_ptr<AccessUnit> SynthH264::next() {
   const int ns = std::max(1, std::min(cfg_.slices, hmbs_));
   for (int s = 0; s < ns; ++s) {
     int r0 = hmbs_ * s / ns, r1 = hmbs_ * (s + 1) / ns;
-    std::vector<u8> nal = encode_slice(idr, r0 * wmbs_, r1 * wmbs_, coded);
+    std::vector<u8> nal = h265 ? encode_slice_hevc(idr, r0 * wmbs_, r1 * wmbs_, coded)
+                               : encode_slice(idr, r0 * wmbs_, r1 * wmbs_, coded);
     au->add_nal(nal.data(), nal.size());
   }
   return au;

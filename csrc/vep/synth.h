@@ -1,6 +1,8 @@
 // Synthetic camera: a conformant H.264 Baseline encoder emitting IDR pictures of I_PCM
 // macroblocks and P pictures of P_Skip + I_PCM macroblocks (a moving object over a static
-// random background). Lets every BASELINE.json config run without cameras or network.
+// random background) — or, with `codec = kH265`, a conformant HEVC Main encoder (CABAC) emitting
+// the same pictures as 16x16 CTBs of PCM CUs (IDR_W_RADL) and skip + PCM CUs (TRAIL_R).
+// Lets every BASELINE.json config run without cameras or network.
 //
 // The reference had no synthetic source at all — its tests used real cameras
 // (README.md:117-239).
@@ -19,15 +21,18 @@ struct SynthConfig {
   int slices = 1;          // slices per picture (MB-row aligned)
   bool zero_samples = false;  // allow 0x00 PCM samples (forces emulation-prevention bytes)
   int idr_phase = 0;       // GOP phase offset (IDR when (frame + phase) % gop == 0, and frame 0)
+  Codec codec = Codec::kH264;
+  int merge_cands = 1;     // HEVC MaxNumMergeCand (merge_idx coded when > 1)
 };
 
-class SynthH264 {
+class SynthH264 {  // (both codecs; the name predates H.265 support)
  public:
   explicit SynthH264(const SynthConfig& cfg);
   std::shared_ptr<AccessUnit> next();
   const HostSurface& picture() const { return pic_; }  // ground truth of the last AU
   const std::vector<u8>& sps_nal() const { return sps_nal_; }
   const std::vector<u8>& pps_nal() const { return pps_nal_; }
+  const std::vector<u8>& vps_nal() const { return vps_nal_; }  // H.265 only
   const SynthConfig& config() const { return cfg_; }
   i64 frame_index() const { return frame_; }
 
@@ -39,11 +44,17 @@ class SynthH264 {
   Rect box_at(i64 f) const;
   void pcm_payload(int mb, u8* out) const;
   std::vector<u8> encode_slice(bool idr, int mb0, int mb1, const std::vector<u8>& coded);
+  std::vector<u8> encode_slice_hevc(bool idr, int ctb0, int ctb1, const std::vector<u8>& coded);
 
   SynthConfig cfg_;
   h264::Sps sps_;
   h264::Pps pps_;
-  std::vector<u8> sps_nal_, pps_nal_;
+  hevc::Vps hvps_;
+  hevc::Sps hsps_;
+  hevc::Pps hpps_;
+  std::vector<u8> sps_nal_, pps_nal_, vps_nal_;
+  std::vector<u8> skip_;  // HEVC per-CTB cu_skip_flag of the picture being encoded
+  int poc_ = 0;
   HostSurface pic_, bg_;
   int wmbs_, hmbs_, bw_, bh_;
   i64 frame_ = -1;

@@ -38,8 +38,11 @@ def native():
     return n
 
 
-def synth(native, w=640, h=480, gop=10, motion=0.05, seed=1, slices=1, zero=False, fps=30):
+def synth(native, w=640, h=480, gop=10, motion=0.05, seed=1, slices=1, zero=False, fps=30,
+          codec="h264", merge_cands=1):
     c = native.SynthConfig()
     c.width, c.height, c.gop, c.motion, c.seed, c.slices, c.fps = w, h, gop, motion, seed, slices, fps
     c.zero_samples = zero
+    c.codec = codec
+    c.merge_cands = merge_cands
     return native.SynthH264(c)

@@ -268,3 +268,46 @@ def test_registry_restore(native, farm, tmp_path):
         assert b.hub.has("keepme")
     finally:
         b.stop()
+
+
+def test_hevc_camera_end_to_end(native, hubapp):
+    """H.265 RTSP camera -> hub -> gRPC frame, hvc1 MP4 archive and enhanced-RTMP pass-through."""
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
+    srv = native.RtspServer("127.0.0.1", 0)
+    cfg = native.SynthConfig()
+    cfg.width, cfg.height, cfg.gop, cfg.fps, cfg.seed, cfg.codec = 320, 240, 10, 30, 21, "h265"
+    srv.add_stream("/hevc", cfg, realtime=True, cached_frames=20)
+    srv.start()
+    sink = native.RtmpSink("127.0.0.1", 0)
+    sink.start()
+    rest = _rest(hubapp)
+    cli = ImageClient(f"127.0.0.1:{hubapp.grpc_port}")
+    try:
+        r = rest.post("/api/v1/process", json={
+            "name": "hevc_cam", "rtsp_endpoint": f"rtsp://127.0.0.1:{srv.port}/hevc",
+            "rtmp_endpoint": f"rtmp://127.0.0.1:{sink.port}/live/hevc42"})
+        assert r.status_code == 200, r.text
+        deadline, vf = time.time() + 15, None
+        while time.time() < deadline:
+            vf = cli.latest_frame("hevc_cam")
+            if vf is not None and vf.width:
+                break
+            time.sleep(0.1)
+        assert vf is not None and (vf.width, vf.height) == (320, 240)
+        img = np.frombuffer(vf.data, np.uint8).reshape(240, 320, 3)
+        ref = synth(native, 320, 240, gop=10, seed=21, codec="h265")
+        dec = native.CpuDecoder()
+        assert any(np.array_equal(img, dec.decode(ref.next())) for _ in range(20))
+        t0 = time.time()
+        while (sink.video_messages < 12 or hubapp.hub.archiver.written == 0) and time.time() - t0 < 10:
+            time.sleep(0.05)
+        assert sink.sequence_headers >= 1 and sink.hevc_messages >= 12 and sink.keyframes >= 1
+        p = hubapp.hub.archiver.last_path
+        with open(p, "rb") as f:
+            mp4 = f.read()
+        assert b"hvc1" in mp4 and b"hvcC" in mp4
+    finally:
+        cli.close()
+        sink.stop()
+        srv.stop()
