@@ -210,7 +210,7 @@ def main():
             "p50_latency_ms": r3(serve_lat[0]),
             "p99_latency_ms": r3(serve_lat[1]),
             "latency_definition": "client-observed gRPC VideoLatestImage (loopback, connected "
-                                  "channel): request sent -> 1080p BGR24 VideoFrame received and "
+                                  f"channel): request sent -> {a.width}x{a.height} BGR24 VideoFrame received and "
                                   "parsed; newest frame already in the HBM ring; cameras decoding "
                                   f"at {a.fps} fps meanwhile; {nlat} samples",
             "p50_next_frame_latency_ms": r3(next_lat[0]),
