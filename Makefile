@@ -1,0 +1,49 @@
+# vep build / test entry points. GPU code targets gfx950 (MI355X) only.
+PY      ?= python
+HIPCC   ?= hipcc
+ARCH    ?= gfx950
+SRCS     = $(wildcard csrc/vep/*.cpp)
+TSAN_DIR = build/tsan
+ASAN_DIR = build/asan
+
+.PHONY: build test test-gpu bench bench-h265 smoke tsan asan clean
+
+build:                     ## compile the extension in-tree (video_edge_ai_proxy_amd/_vep*.so)
+	$(PY) csrc/build.py
+
+test: build                ## CPU test suite
+	$(PY) -m pytest tests -x -q -m "not gpu"
+
+test-gpu: build            ## GPU tests (needs an MI355X)
+	$(PY) -m pytest tests -x -q -m gpu
+
+smoke: build
+	$(PY) -c "import __graft_entry__ as g; g.smoke()"
+
+bench: build               ## headline benchmark, 1 GPU (torchrun for N > 1)
+	$(PY) bench.py
+
+bench-h265: build          ## BASELINE config 5 shape on one GPU: 8 x 4K30 H.265
+	$(PY) bench.py --codec h265 --width 3840 --height 2160 --cams-per-gpu 8
+
+# ThreadSanitizer / AddressSanitizer builds of the native stress driver. Sanitizers apply to
+# host code only (-Xarch_host); the driver runs the CPU backend, so no GPU is needed.
+$(TSAN_DIR)/native_stress: $(SRCS) csrc/vep/gpu_kernels.hip csrc/tests/native_stress.cpp $(wildcard csrc/vep/*.h)
+	mkdir -p $(TSAN_DIR)
+	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O1 -g -Xarch_host -fsanitize=thread \
+	  $(SRCS) csrc/tests/native_stress.cpp -x hip csrc/vep/gpu_kernels.hip -o $@ -lpthread
+
+$(ASAN_DIR)/native_stress: $(SRCS) csrc/vep/gpu_kernels.hip csrc/tests/native_stress.cpp $(wildcard csrc/vep/*.h)
+	mkdir -p $(ASAN_DIR)
+	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O1 -g -Xarch_host -fsanitize=address \
+	  -Xarch_host -fno-omit-frame-pointer \
+	  $(SRCS) csrc/tests/native_stress.cpp -x hip csrc/vep/gpu_kernels.hip -o $@ -lpthread
+
+tsan: $(TSAN_DIR)/native_stress
+	cd /tmp && TSAN_OPTIONS="halt_on_error=1" $(CURDIR)/$(TSAN_DIR)/native_stress
+
+asan: $(ASAN_DIR)/native_stress
+	cd /tmp && ASAN_OPTIONS="detect_leaks=1" $(CURDIR)/$(ASAN_DIR)/native_stress
+
+clean:
+	rm -rf build video_edge_ai_proxy_amd/_vep*.so

@@ -53,11 +53,14 @@ static py::dict pic_dict(const PictureInfo& p) {
   return d;
 }
 
-static Camera& cam_of(Worker& w, int idx) {
-  Camera* c = w.camera(idx);
+// Callers bind the result to a local (`auto cp = cam_ref(w, i)`) when the camera must outlive
+// a GIL-released section; short accessors use cam_of.
+static std::shared_ptr<Camera> cam_ref(Worker& w, int idx) {
+  std::shared_ptr<Camera> c = w.camera(idx);
   if (!c) throw py::index_error("no camera with index " + std::to_string(idx));
-  return *c;
+  return c;
 }
+static Camera& cam_of(Worker& w, int idx) { return *cam_ref(w, idx); }
 
 // Stateful oracle: parse + CPU reconstruct a sequence of AUs, return the final BGR picture.
 struct CpuDecoder {
@@ -315,7 +318,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def("add_camera", &Worker::add_camera, py::arg("name"), py::arg("ring_slots") = 2)
       .def("remove_camera", &Worker::remove_camera, py::call_guard<py::gil_scoped_release>())
-      .def("find", [](Worker& w, const std::string& n) { Camera* c = w.find(n); return c ? c->index() : -1; })
+      .def("find", [](Worker& w, const std::string& n) { auto c = w.find(n); return c ? c->index() : -1; })
       .def("num_cameras", &Worker::num_cameras)
       .def("start", &Worker::start)
       .def("stop", &Worker::stop, py::call_guard<py::gil_scoped_release>())
@@ -355,10 +358,11 @@ PYBIND11_MODULE(_vep, m) {
              d["errors"] = c.errors.load();
              d["bytes_in"] = c.bytes_in.load();
              d["last_packet_ms"] = c.last_packet_ms.load();
-             d["published"] = c.ring() ? c.ring()->published() : 0;
-             d["width"] = c.ring() ? c.ring()->width() : 0;
-             d["height"] = c.ring() ? c.ring()->height() : 0;
-             d["ring_slots"] = c.ring() ? c.ring()->slots() : c.ring_slots_cfg;
+             auto ring = c.ring();
+             d["published"] = ring ? ring->published() : 0;
+             d["width"] = ring ? ring->width() : 0;
+             d["height"] = ring ? ring->height() : 0;
+             d["ring_slots"] = ring ? ring->slots() : c.ring_slots_cfg;
              return d;
            })
       .def("log", [](Worker& w, int i, bool err, const std::string& line) { cam_of(w, i).logs.add(err, line); })
@@ -366,16 +370,16 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("idx"), py::arg("err") = false, py::arg("last") = 100)
       .def("read_latest",
            [](Worker& w, int i, i64 after) -> py::object {
-             Camera& c = cam_of(w, i);
-             if (!c.ring()) return py::none();
-             size_t n = c.ring()->slot_bytes();
-             py::array_t<uint8_t> out({c.ring()->height(), c.ring()->width(), 3});
+             std::shared_ptr<FrameRing> ring = cam_of(w, i).ring();
+             if (!ring) return py::none();
+             size_t n = ring->slot_bytes();
+             py::array_t<uint8_t> out({ring->height(), ring->width(), 3});
              FrameMeta m;
              bool ok;
              u8* dst = out.mutable_data();
              {
                py::gil_scoped_release r;
-               ok = w.read_latest(i, after, &m, dst, n);
+               ok = w.read_latest(*ring, after, &m, dst, n);
              }
              if (!ok) return py::none();
              return py::make_tuple(meta_dict(m), out);
@@ -385,11 +389,12 @@ PYBIND11_MODULE(_vep, m) {
            // Serialized VideoFrame proto built in one buffer: header, D2H'd pixels, trailer.
            [](Worker& w, int i, i64 after, const std::string& device_id) -> py::object {
              Camera& c = cam_of(w, i);
-             if (!c.ring()) return py::none();
-             size_t n = c.ring()->slot_bytes();
+             std::shared_ptr<FrameRing> ring = c.ring();
+             if (!ring) return py::none();
+             size_t n = ring->slot_bytes();
              FrameMeta probe;
              int slot;
-             if (!c.ring()->latest(after, &probe, &slot)) return py::none();
+             if (!ring->latest(after, &probe, &slot)) return py::none();
              auto [pre0, suf0] = encode_video_frame(probe, n, device_id);
              size_t total = pre0.size() + n + suf0.size() + 64;
              PyObject* b = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(total));
@@ -400,7 +405,7 @@ PYBIND11_MODULE(_vep, m) {
              bool ok;
              {
                py::gil_scoped_release r;
-               ok = w.read_latest(i, after, &m, reinterpret_cast<u8*>(buf) + 32 + pre0.size(), n);
+               ok = w.read_latest(*ring, after, &m, reinterpret_cast<u8*>(buf) + 32 + pre0.size(), n);
              }
              if (!ok) return py::none();
              auto [pre, suf] = encode_video_frame(m, n, device_id);
@@ -421,33 +426,35 @@ PYBIND11_MODULE(_vep, m) {
       .def("wait_frame",
            // Block (GIL released) until the camera publishes a frame with seq > after.
            [](Worker& w, int i, i64 after, int timeout_ms) {
-             Camera& c = cam_of(w, i);
+             std::shared_ptr<Camera> cp = cam_ref(w, i);
+             Camera& c = *cp;
              py::gil_scoped_release r;
              const i64 deadline = mono_us() + i64(timeout_ms) * 1000;
-             while (!c.ring()) {  // ring appears with the first decoded frame
+             std::shared_ptr<FrameRing> ring;
+             while (!(ring = c.ring())) {  // ring appears with the first decoded frame
                if (mono_us() >= deadline) return false;
                std::this_thread::sleep_for(std::chrono::milliseconds(2));
              }
              int left = int(std::max<i64>(0, (deadline - mono_us()) / 1000));
-             return c.ring()->wait_newer(after, left);
+             return ring->wait_newer(after, left);
            },
            py::arg("idx"), py::arg("after"), py::arg("timeout_ms"))
       .def("published", [](Worker& w, int i) {
-        Camera& c = cam_of(w, i);
-        return c.ring() ? c.ring()->published() : i64(0);
+        auto ring = cam_of(w, i).ring();
+        return ring ? ring->published() : i64(0);
       })
       .def("consumer_hwc_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.consumer_hwc()); })
       .def("consumer_chw_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.consumer_chw()); })
       .def("ring_slot_ptr", [](Worker& w, int i, int s) {
-        Camera& c = cam_of(w, i);
-        if (!c.ring()) return uintptr_t(0);
-        return reinterpret_cast<uintptr_t>(c.ring()->slot_ptr(s));
+        auto ring = cam_of(w, i).ring();
+        if (!ring) return uintptr_t(0);
+        return reinterpret_cast<uintptr_t>(ring->slot_ptr(s));
       })
       .def("latest_slot", [](Worker& w, int i) -> py::object {
-        Camera& c = cam_of(w, i);
+        auto ring = cam_of(w, i).ring();
         FrameMeta m;
         int slot;
-        if (!c.ring() || !c.ring()->latest(0, &m, &slot)) return py::none();
+        if (!ring || !ring->latest(0, &m, &slot)) return py::none();
         return py::make_tuple(slot, meta_dict(m));
       })
       .def("timings",

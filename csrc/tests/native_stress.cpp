@@ -1,0 +1,172 @@
+// Multi-threaded stress driver for the native data plane, built under ThreadSanitizer by
+// `make tsan` (host code only: `-Xarch_host -fsanitize=thread`; the CPU backend runs, so no GPU
+// is needed). Exercises every cross-thread hand-off of the runtime:
+//   * live Worker (device -1): producer threads feeding cameras (on_access_unit + lazy-decode
+//     control atomics) while reader threads poll rings, wait for frames and encode VideoFrames;
+//   * ring replacement on a resolution change while readers hold the old ring;
+//   * remove_camera while readers still hold the camera;
+//   * RTSP server with concurrent clients; IngestSession supervisor start/stop against it.
+// Reference: SURVEY.md §5 "Race detection / sanitizers" (the reference had none and real races:
+// read_image.py:48,71-74 vs rtsp_to_rtmp.py:147-151; grpc_api.go:181-184).
+#include <atomic>
+#include <cstdio>
+#include <thread>
+#include <vector>
+
+#include "../vep/ingest.h"
+#include "../vep/runtime.h"
+#include "../vep/synth.h"
+
+using namespace vep;
+
+#define CHECK(c)                                                              \
+  do {                                                                        \
+    if (!(c)) {                                                               \
+      std::fprintf(stderr, "CHECK failed %s:%d: %s\n", __FILE__, __LINE__, #c); \
+      std::exit(1);                                                           \
+    }                                                                         \
+  } while (0)
+
+static void live_worker_stress() {
+  WorkerOptions o;
+  o.device = -1;
+  o.letterbox_size = 64;
+  o.max_cameras = 8;
+  Worker w(o);
+  w.start();
+  const int ncam = 4;
+  std::vector<int> cams;
+  for (int i = 0; i < ncam; ++i) cams.push_back(w.add_camera("c" + std::to_string(i), 3));
+  std::atomic<bool> stop{false};
+  std::atomic<u64> served{0};
+  std::vector<std::thread> th;
+  for (int i = 0; i < ncam; ++i) {
+    th.emplace_back([&, i] {
+      SynthConfig c;
+      c.width = (i == 0) ? 96 : 160;
+      c.height = (i == 0) ? 64 : 96;
+      c.gop = 5;
+      c.seed = u64(i + 1);
+      c.codec = (i & 1) ? Codec::kH265 : Codec::kH264;
+      SynthH264 enc(c);
+      auto cam = w.camera(cams[size_t(i)]);
+      for (int f = 0; f < 120; ++f) {
+        if (i == 0 && f == 60) {  // resolution change mid-stream: the ring is replaced
+          c.width = 128;
+          c.height = 80;
+          enc = SynthH264(c);
+        }
+        cam->last_query_ms.store(now_ms());
+        cam->keyframe_only.store(f % 40 > 30);
+        cam->on_access_unit(enc.next());
+        if (f % 7 == 0) std::this_thread::sleep_for(std::chrono::microseconds(200));
+      }
+    });
+  }
+  for (int r = 0; r < 3; ++r) {
+    th.emplace_back([&, r] {
+      std::vector<u8> buf(size_t(160) * 96 * 3);
+      i64 cursor[8] = {};
+      while (!stop.load()) {
+        for (int i = 0; i < ncam; ++i) {
+          auto cam = w.camera(cams[size_t(i)]);
+          if (!cam) continue;
+          auto ring = cam->ring();
+          if (!ring) continue;
+          if (r == 0) {
+            ring->wait_newer(cursor[i], 2);
+          }
+          FrameMeta m;
+          if (ring->slot_bytes() <= buf.size() &&
+              w.read_latest(*ring, cursor[i], &m, buf.data(), buf.size())) {
+            CHECK(m.seq > cursor[i]);
+            cursor[i] = m.seq;
+            auto enc = encode_video_frame(m, ring->slot_bytes(), cam->name());
+            CHECK(!enc.first.empty());
+            served.fetch_add(1);
+          }
+        }
+      }
+    });
+  }
+  for (int i = 0; i < ncam; ++i) th[size_t(i)].join();
+  w.flush();
+  stop.store(true);
+  for (size_t i = ncam; i < th.size(); ++i) th[i].join();
+  for (int i = 0; i < ncam; ++i) CHECK(w.camera(cams[size_t(i)])->decoded.load() > 0);
+  // remove a camera while a reader still holds it
+  auto held = w.camera(cams[1]);
+  w.remove_camera(cams[1]);
+  CHECK(held->name() == "c1" && !w.camera(cams[1]));
+  w.stop();
+  std::printf("live worker: served %llu frames\n", (unsigned long long)served.load());
+}
+
+static void rtsp_stress() {
+  net::RtspServer srv("127.0.0.1", 0);
+  net::ServedStream s;
+  s.cfg.width = 128;
+  s.cfg.height = 96;
+  s.cfg.gop = 6;
+  s.realtime = false;
+  s.cached_frames = 12;
+  srv.add_stream("/a", s);
+  s.cfg.codec = Codec::kH265;
+  srv.add_stream("/b", s);
+  srv.start();
+  std::vector<std::thread> th;
+  std::atomic<int> got{0};
+  for (int k = 0; k < 4; ++k) {
+    th.emplace_back([&, k] {
+      net::RtspClient c("rtsp://127.0.0.1:" + std::to_string(srv.port()) + ((k & 1) ? "/b" : "/a"));
+      c.open();
+      std::atomic<bool> stop{false};
+      int n = 0;
+      c.run([&](const AuPtr&) { if (++n >= 30) stop.store(true); }, stop);
+      got.fetch_add(n);
+    });
+  }
+  for (auto& t : th) t.join();
+  CHECK(got.load() >= 120);
+
+  // supervisor against the farm, with live decode, RTMP pass-through and per-GOP archive
+  mux::RtmpSink sink("127.0.0.1", 0);
+  sink.start();
+  WorkerOptions o;
+  o.device = -1;
+  Worker w(o);
+  w.start();
+  int cam = w.add_camera("ingest", 2);
+  w.camera(cam)->last_query_ms.store(now_ms());
+  IngestConfig ic;
+  ic.name = "ingest";
+  ic.rtsp_url = "rtsp://127.0.0.1:" + std::to_string(srv.port()) + "/b";
+  ic.rtmp_url = "rtmp://127.0.0.1:" + std::to_string(sink.port()) + "/live/stress";
+  ic.disk_path = "/tmp/vep_native_stress";
+  w.camera(cam)->proxy_rtmp.store(true);
+  auto arch = std::make_shared<mux::Archiver>();
+  IngestSession sess(w, cam, ic, arch);
+  sess.start();
+  for (int i = 0; i < 100 && w.camera(cam)->decoded.load() < 5; ++i) {
+    w.camera(cam)->last_query_ms.store(now_ms());
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    (void)sess.state();
+  }
+  sess.stop();
+  w.flush();
+  CHECK(w.camera(cam)->decoded.load() >= 5);
+  arch->flush();
+  CHECK(sink.video_messages() > 0);
+  w.stop();
+  sink.stop();
+  srv.stop();
+  std::printf("rtsp: %d AUs over 4 clients; ingest decoded %llu\n", got.load(),
+              (unsigned long long)w.camera(cam)->decoded.load());
+}
+
+int main() {
+  live_worker_stress();
+  rtsp_stress();
+  std::printf("native_stress ok\n");
+  return 0;
+}

@@ -43,7 +43,7 @@ void ReplayBench::parse_tick(std::vector<DecodeJob>& out) {
     auto& v = aus_[size_t(i)];
     const AuPtr& au = v[pos_[size_t(i)]];
     pos_[size_t(i)] = (pos_[size_t(i)] + 1) % v.size();
-    Camera* c = w_.camera(cams_[size_t(i)]);
+    auto c = w_.camera(cams_[size_t(i)]);
     ok[size_t(i)] = c && c->make_job(au, out[size_t(i)]);
   });
   size_t k = 0;

@@ -450,12 +450,12 @@ void RtmpSink::start() {
 
 void RtmpSink::stop() {
   if (stop_.exchange(true)) return;
+  if (lfd_ >= 0) ::shutdown(lfd_, SHUT_RDWR);  // wake the accept loop; close after the join
+  if (acc_.joinable()) acc_.join();
   if (lfd_ >= 0) {
-    ::shutdown(lfd_, SHUT_RDWR);
     ::close(lfd_);
     lfd_ = -1;
   }
-  if (acc_.joinable()) acc_.join();
   for (int i = 0; i < 200 && live_.load() > 0; ++i)
     std::this_thread::sleep_for(std::chrono::milliseconds(25));
 }

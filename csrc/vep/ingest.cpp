@@ -17,7 +17,7 @@ IngestSession::IngestSession(Worker& w, int cam, IngestConfig cfg,
 IngestSession::~IngestSession() { stop(); }
 
 void IngestSession::log(bool err, const std::string& s) {
-  if (Camera* c = w_.camera(cam_)) c->logs.add(err, s);
+  if (auto c = w_.camera(cam_)) c->logs.add(err, s);
 }
 
 void IngestSession::start() {
@@ -48,7 +48,7 @@ bool IngestSession::sleep_interruptible(int ms) {
 }
 
 void IngestSession::on_au(const AuPtr& au) {
-  Camera* cam = w_.camera(cam_);
+  std::shared_ptr<Camera> cam = w_.camera(cam_);
   if (!cam) return;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -59,9 +59,9 @@ void IngestSession::on_au(const AuPtr& au) {
   if (au->keyframe) {
     if (!gop_.empty() && archiver_ && !cfg_.disk_path.empty() && ps_.complete()) {
       mux::Mp4Info info;
-      if (cam->ring()) {
-        info.width = cam->ring()->width();
-        info.height = cam->ring()->height();
+      if (auto ring = cam->ring()) {
+        info.width = ring->width();
+        info.height = ring->height();
       }
       if (info.width == 0) std::tie(info.width, info.height) = ps_.size();
       info.ps = ps_;

@@ -435,12 +435,14 @@ void RtspServer::start() {
 
 void RtspServer::stop() {
   if (stop_.exchange(true)) return;
+  // wake the accept loop, join it, and only then close: the fd number must not be reused while
+  // the loop may still poll it
+  if (lfd_ >= 0) ::shutdown(lfd_, SHUT_RDWR);
+  if (acc_.joinable()) acc_.join();
   if (lfd_ >= 0) {
-    ::shutdown(lfd_, SHUT_RDWR);
     ::close(lfd_);
     lfd_ = -1;
   }
-  if (acc_.joinable()) acc_.join();
   {
     std::lock_guard<std::mutex> g(mu_);
     for (int fd : conn_fds_) ::shutdown(fd, SHUT_RDWR);

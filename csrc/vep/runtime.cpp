@@ -286,7 +286,7 @@ Worker::~Worker() {
     if (!c) continue;
     dev_.free(c->surface.y);
     dev_.free(c->surface.uv);
-    c->ring_.reset();
+    c->set_ring(nullptr);
   }
   if (owns_cons_) {
     dev_.free(cons_hwc_);
@@ -319,7 +319,7 @@ int Worker::add_camera(const std::string& name, int ring_slots) {
   }
   // two batches may be in flight on the GPU: keep >= 3 slots so a committed frame stays readable
   cams_[size_t(idx)] =
-      std::make_unique<Camera>(*this, idx, name, std::max(dev_.gpu() ? 3 : 1, ring_slots));
+      std::make_shared<Camera>(*this, idx, name, std::max(dev_.gpu() ? 3 : 1, ring_slots));
   return idx;
 }
 
@@ -335,16 +335,16 @@ void Worker::remove_camera(int idx) {
   c.reset();
 }
 
-Camera* Worker::camera(int idx) {
+std::shared_ptr<Camera> Worker::camera(int idx) {
   std::lock_guard<std::mutex> g(cams_mu_);
   if (idx < 0 || idx >= int(cams_.size())) return nullptr;
-  return cams_[size_t(idx)].get();
+  return cams_[size_t(idx)];
 }
 
-Camera* Worker::find(const std::string& name) {
+std::shared_ptr<Camera> Worker::find(const std::string& name) {
   std::lock_guard<std::mutex> g(cams_mu_);
   for (auto& c : cams_)
-    if (c && c->name() == name) return c.get();
+    if (c && c->name() == name) return c;
   return nullptr;
 }
 
@@ -437,7 +437,7 @@ void Worker::loop() {
       launch_async(batch);
     } catch (const std::exception& e) {
       for (auto& j : batch)
-        if (Camera* c = camera(j.cam)) {
+        if (auto c = camera(j.cam)) {
           c->errors.fetch_add(1);
           c->logs.add(true, std::string("decode batch failed: ") + e.what());
         }
@@ -483,7 +483,7 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi) {
   } else {
     s.host.alloc(wmbs * 16, hmbs * 16);
   }
-  c.ring_ = std::make_unique<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height);
+  c.set_ring(std::make_shared<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height));
 }
 
 static inline size_t al(size_t x, size_t a = 256) { return (x + a - 1) & ~(a - 1); }
@@ -901,9 +901,14 @@ void Worker::run_batch(std::vector<DecodeJob>& jobs) {
 }
 
 bool Worker::read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap) {
-  Camera* c = camera(cam);
-  if (!c || !c->ring_) return false;
-  FrameRing* ring = c->ring_.get();
+  std::shared_ptr<Camera> c = camera(cam);
+  if (!c) return false;
+  std::shared_ptr<FrameRing> r = c->ring();
+  return r && read_latest(*r, after, meta, dst, cap);
+}
+
+bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, size_t cap) {
+  FrameRing* ring = &rg;
   for (int attempt = 0; attempt < 4; ++attempt) {
     int slot;
     if (!ring->latest(after, meta, &slot)) return false;

@@ -137,7 +137,9 @@ class Camera {
   std::atomic<i64> last_packet_ms{0};
   LogRing logs;
 
-  FrameRing* ring() const { return ring_.get(); }
+  // The ring is replaced on a resolution change: readers hold their own reference.
+  std::shared_ptr<FrameRing> ring() const { return std::atomic_load(&ring_); }
+  void set_ring(std::shared_ptr<FrameRing> r) { std::atomic_store(&ring_, std::move(r)); }
   StreamParser& parser() { return parser_; }
   std::mutex& gop_mutex() { return mu_; }
   std::vector<AuPtr> gop_snapshot();   // current GOP packets (for RTMP flush / archive)
@@ -149,7 +151,7 @@ class Camera {
     u8* uv = nullptr;
     HostSurface host;  // CPU backend
   } surface;
-  std::unique_ptr<FrameRing> ring_;
+  std::shared_ptr<FrameRing> ring_;  // written by the worker via set_ring(); read via ring()
   int ring_slots_cfg;
 
  private:
@@ -185,8 +187,9 @@ class Worker {
 
   int add_camera(const std::string& name, int ring_slots);
   void remove_camera(int idx);
-  Camera* camera(int idx);
-  Camera* find(const std::string& name);
+  // Shared ownership: a reader (gRPC thread) keeps the camera alive across remove_camera().
+  std::shared_ptr<Camera> camera(int idx);
+  std::shared_ptr<Camera> find(const std::string& name);
   int num_cameras() const;
 
   // Live mode: a background thread drains submitted jobs in batches.
@@ -207,6 +210,7 @@ class Worker {
 
   // Serving: copy the newest frame with seq > after into dst (host). Returns false if none.
   bool read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap);
+  bool read_latest(FrameRing& ring, i64 after, FrameMeta* meta, u8* dst, size_t cap);
 
   // Consumer batch (letterbox): device pointers of [max_cameras, S, S, 3] u8 and CHW tensor.
   // Point the consumer batch at caller-owned device buffers (e.g. torch tensors that feed an
@@ -241,7 +245,7 @@ class Worker {
   Device dev_;
   hipStream_t stream_ = nullptr, copy_stream_ = nullptr, serve_stream_ = nullptr;
   mutable std::mutex cams_mu_;
-  std::vector<std::unique_ptr<Camera>> cams_;
+  std::vector<std::shared_ptr<Camera>> cams_;
   Stage stage_[2];
   int next_stage_ = 0;
   std::unique_ptr<ThreadPool> pack_pool_;

@@ -63,6 +63,7 @@ def cmd_farm(a):
         c = native.SynthConfig()
         c.width, c.height, c.fps, c.gop, c.motion = a.width, a.height, a.fps, a.gop, a.motion
         c.seed = 1 + i
+        c.codec = a.codec
         c.idr_phase = (i * a.gop) // max(1, a.cams)
         srv.add_stream(f"/cam{i}", c, realtime=not a.unpaced, cached_frames=a.cached_frames)
     srv.start()
@@ -166,6 +167,7 @@ def main(argv=None):
     f.add_argument("--fps", type=int, default=30)
     f.add_argument("--gop", type=int, default=30)
     f.add_argument("--motion", type=float, default=0.05)
+    f.add_argument("--codec", choices=["h264", "h265"], default="h264")
     f.add_argument("--bind", default="127.0.0.1")
     f.add_argument("--port", type=int, default=8554)
     f.add_argument("--unpaced", action="store_true")
