@@ -147,6 +147,7 @@ def main():
         dist.barrier()
     sync()
     f0, p0, b0, g0 = rb.frames, rb.parse_ms, rb.batch_ms, worker.gpu_ms_total
+    ip0, sg0 = worker.bytes_inplace, worker.bytes_staged
     tm0 = worker.timings()
     t0 = time.perf_counter()
     for i in range(a.steps):
@@ -223,6 +224,9 @@ def main():
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "rank0_slice_bytes_per_step": {
+                "gpu_read_in_place_from_pinned": (worker.bytes_inplace - ip0) // a.steps,
+                "host_staged": (worker.bytes_staged - sg0) // a.steps},
             "rank0_launch_breakdown_ms_per_step": {
                 k: round((v - tm0[k]) / a.steps, 4) for k, v in tm1.items()},
         }

@@ -119,6 +119,8 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("arrival_ms", &AccessUnit::arrival_ms)
       .def_readwrite("seq", &AccessUnit::seq)
       .def_property_readonly("size", &AccessUnit::bytes)
+      .def("pin", &AccessUnit::pin)
+      .def_property_readonly("pinned", &AccessUnit::pinned)
       .def("nals",
            [](const AccessUnit& a) {
              py::list l;
@@ -253,6 +255,37 @@ PYBIND11_MODULE(_vep, m) {
     }
     ok = ok && d.terminate() == 1 && d.aligned_bytepos() == buf.size();
     return py::make_tuple(ok, buf.size());
+  });
+  // Host parse cost of one AU (µs, mean over iters) and of its emulation-prevention scan alone.
+  m.def("parse_cost_us", [](const AccessUnit& au, int iters, std::shared_ptr<AccessUnit> prime) {
+    py::gil_scoped_release r;
+    StreamParser p;
+    MbUpdate u;
+    if (prime) p.absorb_parameter_sets(*prime);
+    p.parse(au, u);
+    i64 t0 = mono_us();
+    for (int k = 0; k < iters; ++k) {
+      u.clear_payload();
+      p.parse(au, u);
+    }
+    const double parse_us = double(mono_us() - t0) / iters;
+    std::vector<u32> epb;
+    t0 = mono_us();
+    for (int k = 0; k < iters; ++k)
+      for (size_t i = 0; i < au.nals.size(); ++i) find_epb(au.nal(i), au.nal_size(i), epb);
+    const double scan_us = double(mono_us() - t0) / iters;
+    return std::make_pair(parse_us, scan_us);
+  }, py::arg("au"), py::arg("iters") = 100, py::arg("prime") = nullptr);
+  m.def("pinned_pool_stats", [] {
+    hostmem::PoolStats st = hostmem::pool_stats();
+    py::dict d;
+    d["enabled"] = hostmem::pool_enabled();
+    d["chunks"] = st.chunks;
+    d["bytes_reserved"] = st.bytes_reserved;
+    d["blocks_live"] = st.blocks_live;
+    d["blocks_reused"] = st.blocks_reused;
+    d["fallbacks"] = st.fallbacks;
+    return d;
   });
   m.def("hvcc_record", [](const std::string& vps, const std::string& sps, const std::string& pps) {
     auto v = [](const std::string& x) { return std::vector<u8>(x.begin(), x.end()); };
@@ -470,6 +503,8 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("batches", &Worker::batches)
       .def_property_readonly("frames", &Worker::frames)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
+      .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)
+      .def_property_readonly("bytes_staged", &Worker::bytes_staged)
       .def("compute_stream_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.compute_stream()); });
 
   py::class_<ReplayBench>(m, "ReplayBench")

@@ -1,6 +1,8 @@
 // Replay driver implementation. See bench_driver.h.
 #include "bench_driver.h"
 
+#include <algorithm>
+
 namespace vep {
 
 ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cached_frames,
@@ -20,7 +22,11 @@ ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cach
     SynthH264 enc(c);
     auto& v = aus_[size_t(i)];
     v.reserve(size_t(nframes));
-    for (int f = 0; f < nframes; ++f) v.push_back(enc.next());
+    for (int f = 0; f < nframes; ++f) {
+      auto au = enc.next();
+      au->pin();  // as the RTSP depacketizer does: ingest-side copy into the pinned pool
+      v.push_back(au);
+    }
   });
   pf_ = std::thread([this] { prefetch_loop(); });
 }
@@ -39,7 +45,14 @@ void ReplayBench::parse_tick(std::vector<DecodeJob>& out) {
   out.clear();
   out.resize(size_t(n));
   std::vector<char> ok(size_t(n), 0);
-  pool_.parallel_for(n, [&](int i) {
+  // largest-first (LPT) order: a keyframe's parse starts at once instead of trailing the tick
+  std::vector<int> order(static_cast<size_t>(n));
+  for (int i = 0; i < n; ++i) order[size_t(i)] = i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return aus_[size_t(a)][pos_[size_t(a)]]->bytes() > aus_[size_t(b)][pos_[size_t(b)]]->bytes();
+  });
+  pool_.parallel_for(n, [&](int t) {
+    const int i = order[size_t(t)];
     auto& v = aus_[size_t(i)];
     const AuPtr& au = v[pos_[size_t(i)]];
     pos_[size_t(i)] = (pos_[size_t(i)] + 1) % v.size();

@@ -55,16 +55,20 @@ struct Ctx {
   }
 };
 
-// Arithmetic decoder over an RBSP (byte positions are RBSP offsets).
+// Arithmetic decoder over an RBSP (byte positions are RBSP offsets). Bits are pulled from a
+// 64-bit MSB-aligned cache and renormalisation is one clz + shift, so a bin costs a handful of
+// instructions (a 1080p skip picture is ~16k bins).
 class Decoder {
  public:
   Decoder(const u8* p, size_t n, size_t bytepos) : p_(p), n_(n) { start(bytepos); }
 
   // §9.3.2.5: (re)initialise at a byte position (slice data start, or after PCM samples).
   void start(size_t bytepos) {
-    pos_ = bytepos * 8;
+    byte_ = bytepos;
+    cache_ = 0;
+    cbits_ = 0;
     range_ = 510;
-    offset_ = read(9);
+    offset_ = bits(9);
   }
   u32 decision(Ctx& c) {
     const u32 lps = kRangeLps[c.state][(range_ >> 6) & 3];
@@ -92,35 +96,45 @@ class Decoder {
     return 0;
   }
   u32 bypass() {
-    offset_ = (offset_ << 1) | read(1);
+    offset_ = (offset_ << 1) | bits(1);
     if (offset_ >= range_) {
       offset_ -= range_;
       return 1;
     }
     return 0;
   }
-  size_t bitpos() const { return pos_; }
-  size_t aligned_bytepos() const { return (pos_ + 7) >> 3; }
+  size_t bitpos() const { return byte_ * 8 - size_t(cbits_); }
+  size_t aligned_bytepos() const { return (bitpos() + 7) >> 3; }
 
  private:
   void renorm() {
-    while (range_ < 256) {
-      range_ <<= 1;
-      offset_ = (offset_ << 1) | read(1);
+    if (range_ < 256) {
+      const int sh = __builtin_clz(range_) - 23;  // range_ in [2, 255] -> shift to >= 256
+      range_ <<= sh;
+      offset_ = (offset_ << sh) | bits(sh);
     }
   }
-  u32 read(int nbits) {
-    u32 v = 0;
-    for (int i = 0; i < nbits; ++i, ++pos_) {
-      // reading past the end yields zeros (the trailing bits); the caller bounds the walk
-      const u32 b = pos_ < n_ * 8 ? (p_[pos_ >> 3] >> (7 - (pos_ & 7))) & 1u : 0u;
-      v = (v << 1) | b;
-    }
+  u32 bits(int k) {  // 1 <= k <= 9
+    if (cbits_ < k) refill();
+    const u32 v = u32(cache_ >> (64 - k));
+    cache_ <<= k;
+    cbits_ -= k;
     return v;
+  }
+  void refill() {
+    // reading past the end yields zeros (the trailing bits); the caller bounds the walk
+    while (cbits_ <= 56) {
+      const u64 b = byte_ < n_ ? p_[byte_] : 0;
+      ++byte_;
+      cache_ |= b << (56 - cbits_);
+      cbits_ += 8;
+    }
   }
   const u8* p_;
   size_t n_;
-  size_t pos_ = 0;
+  size_t byte_ = 0;
+  u64 cache_ = 0;
+  int cbits_ = 0;
   u32 range_ = 510, offset_ = 0;
 };
 

@@ -9,17 +9,109 @@ namespace vep {
 
 using namespace h264;
 
+// ------------------------------------------------------------------------------ AccessUnit
+
+bool AccessUnit::pin() {
+  if (pinned_) return true;
+  std::shared_ptr<u8> b = hostmem::pinned_block(data.size());
+  u8* dst = b ? b.get() : nullptr;
+  constexpr size_t kChunk = size_t(256) << 10;
+  std::vector<u32> tmp;
+  epb_.clear();
+  epb_idx_.assign(1, 0);
+  for (size_t i = 0; i < nals.size(); ++i) {
+    const size_t off = nals[i].first, n = nals[i].second;
+    for (size_t c = 0; c < n; c += kChunk) {
+      const size_t len = std::min(kChunk, n - c);
+      const u8* src = data.data() + off + c;
+      if (dst) std::memcpy(dst + off + c, src, len);
+      // window reaches 2 bytes back so a 00 00 03 split by the chunk edge is still seen; an
+      // EPB needs its two zero bytes right before it, so windows cannot disagree with a
+      // sequential scan
+      const size_t back = std::min<size_t>(c, 2);
+      find_epb(data.data() + off + c - back, len + back, tmp);
+      for (u32 e : tmp)
+        if (e >= back) epb_.push_back(u32(c + e - back));
+    }
+    epb_idx_.push_back(u32(epb_.size()));
+  }
+  if (!b) return false;
+  pinned_len_ = data.size();
+  pinned_ = std::move(b);
+  std::vector<u8>().swap(data);
+  return true;
+}
+
 static const u8* rbsp_of(const u8* nal, size_t n, std::vector<u32>& epb,
-                         std::vector<u8>& scratch, size_t& out_n) {
-  find_epb(nal, n, epb);
+                         std::vector<u8>& scratch, size_t& out_n, const u32* known_b = nullptr,
+                         const u32* known_e = nullptr) {
+  if (known_b) epb.assign(known_b, known_e);  // scanned at ingest (AccessUnit::pin)
+  else find_epb(nal, n, epb);
   if (epb.empty()) {
     out_n = n;
     return nal;
   }
+  // unescape with one memcpy per run between emulation-prevention bytes
   scratch.resize(n);
-  out_n = ebsp_to_rbsp(nal, n, scratch.data());
+  size_t o = 0, from = 0;
+  for (u32 e : epb) {
+    std::memcpy(scratch.data() + o, nal + from, e - from);
+    o += e - from;
+    from = size_t(e) + 1;
+  }
+  std::memcpy(scratch.data() + o, nal + from, n - from);
+  out_n = o + (n - from);
   return scratch.data();
 }
+
+// Collects the PCM blocks of one slice NAL. Without emulation-prevention bytes the RBSP is the
+// NAL itself and blocks are referenced in place. With EPBs the walk runs on the unescaped
+// scratch copy; resolve() maps each block back into the escaped NAL (RBSP offset + number of
+// EPBs before it) — still in place — unless an EPB falls inside the block, in which case its
+// 384 bytes go to a small owned buffer. No whole-slice copy survives the parse.
+struct BlockSink {
+  MbUpdate& upd;
+  const u8* rbsp;
+  bool direct;
+  std::vector<std::pair<int, u32>> pending;  // (mb, RBSP offset), increasing offsets
+
+  void add(int mb, const u8* p) {
+    if (direct) upd.set(mb, p);
+    else pending.emplace_back(mb, u32(p - rbsp));
+  }
+  void resolve(const u8* nal, const std::vector<u32>& epb) {
+    if (direct || pending.empty()) return;
+    const u32 seg = u32(upd.segs.size() - 1);  // the NAL's segment (begun by the caller)
+    size_t k = 0, straddle = 0;
+    // pass 1: count blocks an EPB splits (their RBSP bytes are not contiguous in the NAL)
+    auto q = [&](size_t i) { return size_t(epb[i]) - i; };  // RBSP position after EPB i
+    for (auto& [mb, off] : pending) {
+      while (k < epb.size() && q(k) <= off) ++k;
+      if (k < epb.size() && q(k) < size_t(off) + kPcmMbBytes) ++straddle;
+    }
+    std::shared_ptr<std::vector<u8>> own;
+    u32 own_seg = 0;
+    if (straddle) {
+      own = std::make_shared<std::vector<u8>>(straddle * kPcmMbBytes);
+      upd.own.push_back(own);
+      upd.begin_segment(own->data(), own->size());
+      own_seg = u32(upd.segs.size() - 1);
+    }
+    k = 0;
+    size_t o = 0;
+    for (auto& [mb, off] : pending) {
+      while (k < epb.size() && q(k) <= off) ++k;
+      if (k < epb.size() && q(k) < size_t(off) + kPcmMbBytes) {
+        u8* dst = own->data() + o * kPcmMbBytes;
+        std::memcpy(dst, rbsp + off, kPcmMbBytes);
+        upd.set_in(mb, dst, own_seg);
+        ++o;
+      } else {
+        upd.set_in(mb, nal + off + k, seg);
+      }
+    }
+  }
+};
 
 void H264Parser::absorb_parameter_sets(const AccessUnit& au) {
   for (size_t i = 0; i < au.nals.size(); ++i) {
@@ -49,7 +141,7 @@ const Sps& H264Parser::active_sps() const {
 }
 
 void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, BitReader& br,
-                            const Sps& sps, MbUpdate& upd, int& coded) {
+                            const Sps& sps, BlockSink& upd, int& coded) {
   (void)rbsp;
   (void)n;
   const int total = sps.width_mbs * sps.height_mbs();
@@ -73,7 +165,7 @@ void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, Bit
       while (off + 2 + kPcmMbBytes <= nbytes && base[off] == f0 && base[off + 1] == f1 &&
              (off + 2) * 8 < stop) {
         VEP_CHECK(mb < total, "macroblock address past end of picture");
-        upd.set(mb, base + off + 2);
+        upd.add(mb, base + off + 2);
         ++coded;
         ++mb;
         off += 2 + kPcmMbBytes;
@@ -97,7 +189,7 @@ void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, Bit
       br.align();
       size_t off = br.bytepos();
       VEP_CHECK(off + kPcmMbBytes <= br.size(), "truncated PCM macroblock");
-      upd.set(mb, base + off);
+      upd.add(mb, base + off);
       br.skip(kPcmMbBytes * 8);
       ++coded;
     }
@@ -130,14 +222,9 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
     }
     if (t != kNalSlice && t != kNalIdr) continue;
     size_t rn;
-    const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn);
-    std::shared_ptr<std::vector<u8>> owned;
-    if (r != p) {
-      // emulation-prevention bytes present: the MB samples are referenced from an owned
-      // unescaped copy (kept alive by the update) instead of the shared parser scratch
-      owned = std::make_shared<std::vector<u8>>(r, r + rn);
-      r = owned->data();
-    }
+    const u32 *kb = nullptr, *ke = nullptr;
+    au.epb_of(i, &kb, &ke);
+    const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn, kb, ke);
     BitReader br(r + 1, rn - 1);
     // peek pps id to locate parameter sets
     BitReader peek(r + 1, rn - 1);
@@ -170,9 +257,10 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
         upd.reset(sps.width_mbs, sps.height_mbs());
       got_slice = true;
     }  // mixed-slice pictures report the first slice's type, as PyAV's pict_type does
-    if (owned) upd.own.push_back(owned);
-    upd.begin_segment(r, rn);
-    walk_slice(r, rn, sh, br, sps, upd, pi.coded_mbs);
+    upd.begin_segment(p, n);
+    BlockSink sink{upd, r, r == p, {}};
+    walk_slice(r, rn, sh, br, sps, sink, pi.coded_mbs);
+    sink.resolve(p, epb_);
   }
   VEP_CHECK(got_slice, "access unit has no slice");
   upd.frames += 1;
@@ -223,7 +311,7 @@ const hevc::Sps& H265Parser::active_sps() const {
 //   PCM: alignment zeros, 384 raw sample bytes (16x16 Y, 8x8 Cb, 8x8 Cr), CABAC re-init;
 //   end_of_slice_segment_flag (terminating bin).
 void H265Parser::walk_slice(const u8* rbsp, size_t n, const hevc::SliceHeader& sh,
-                            const hevc::Sps& sps, const hevc::Pps& pps, MbUpdate& upd,
+                            const hevc::Sps& sps, const hevc::Pps& pps, BlockSink& upd,
                             int& coded) {
   const int wctb = sps.width_ctbs(), total = wctb * sps.height_ctbs();
   const bool inter = sh.slice_type != hevc::kI;
@@ -263,7 +351,7 @@ void H265Parser::walk_slice(const u8* rbsp, size_t n, const hevc::SliceHeader& s
         throw UnsupportedStream("regular intra HEVC CU (native subset decodes PCM + skip only)");
       const size_t off = dec.aligned_bytepos();
       VEP_CHECK(off + kPcmMbBytes <= n, "truncated PCM coding unit");
-      upd.set(ctb, rbsp + off);
+      upd.add(ctb, rbsp + off);
       ++coded;
       dec.start(off + kPcmMbBytes);
     }
@@ -287,12 +375,9 @@ PictureInfo H265Parser::parse(const AccessUnit& au, MbUpdate& upd) {
     if (t > hevc::kTrailR && t < hevc::kBlaWLp)
       throw UnsupportedStream("HEVC leading / sub-layer pictures are not supported");
     size_t rn;
-    const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn);
-    std::shared_ptr<std::vector<u8>> owned;
-    if (r != p) {
-      owned = std::make_shared<std::vector<u8>>(r, r + rn);
-      r = owned->data();
-    }
+    const u32 *kb = nullptr, *ke = nullptr;
+    au.epb_of(i, &kb, &ke);
+    const u8* r = rbsp_of(p, n, epb_, rbsp_scratch_, rn, kb, ke);
     const int pps_id = hevc::peek_slice_pps_id(r, rn);
     auto pit = pps_.find(pps_id);
     if (pit == pps_.end()) throw UnsupportedStream("slice references unknown PPS");
@@ -337,9 +422,10 @@ PictureInfo H265Parser::parse(const AccessUnit& au, MbUpdate& upd) {
       skip_.assign(size_t(w) * h, 0);
       got_slice = true;
     }
-    if (owned) upd.own.push_back(owned);
-    upd.begin_segment(r, rn);
-    walk_slice(r, rn, sh, sps, pps, upd, pi.coded_mbs);
+    upd.begin_segment(p, n);
+    BlockSink sink{upd, r, r == p, {}};
+    walk_slice(r, rn, sh, sps, pps, sink, pi.coded_mbs);
+    sink.resolve(p, epb_);
   }
   VEP_CHECK(got_slice, "access unit has no slice");
   upd.frames += 1;

@@ -19,6 +19,7 @@
 #include "common.h"
 #include "h264.h"
 #include "hevc.h"
+#include "hostmem.h"
 
 namespace vep {
 
@@ -36,12 +37,33 @@ struct AccessUnit {
   u64 seq = 0;                                  // per-camera packet counter
 
   void add_nal(const u8* p, size_t n) {
+    VEP_CHECK(!pinned_, "access unit is finalised");
     nals.emplace_back(u32(data.size()), u32(n));
     data.insert(data.end(), p, p + n);
   }
-  const u8* nal(size_t i) const { return data.data() + nals[i].first; }
+  const u8* base() const { return pinned_ ? pinned_.get() : data.data(); }
+  const u8* nal(size_t i) const { return base() + nals[i].first; }
   size_t nal_size(size_t i) const { return nals[i].second; }
-  size_t bytes() const { return data.size(); }
+  size_t bytes() const { return pinned_ ? pinned_len_ : data.size(); }
+  // Finalise into device-accessible pinned memory (hostmem.h) so the GPU can read the slice
+  // bytes in place; the emulation-prevention scan is fused into the copy (each chunk is scanned
+  // while hot in cache), so the parser never makes its own pass over the bytes. Call before the
+  // AU is shared with other threads. Without a pool only the scan is done.
+  bool pin();
+  bool pinned() const { return bool(pinned_); }
+  // EPB positions (indices of the 0x03 bytes, relative to the NAL) recorded by pin(); false if
+  // the AU was never scanned.
+  bool epb_of(size_t i, const u32** begin, const u32** end) const {
+    if (epb_idx_.empty()) return false;
+    *begin = epb_.data() + epb_idx_[i];
+    *end = epb_.data() + epb_idx_[i + 1];
+    return true;
+  }
+
+ private:
+  std::shared_ptr<u8> pinned_;
+  size_t pinned_len_ = 0;
+  std::vector<u32> epb_, epb_idx_;
 };
 using AuPtr = std::shared_ptr<const AccessUnit>;
 
@@ -142,6 +164,8 @@ class UnsupportedStream : public Error {
   using Error::Error;
 };
 
+struct BlockSink;  // per-slice PCM block collector (codec.cpp)
+
 // Stateful H.264 AU parser (keeps SPS/PPS tables across AUs).
 class H264Parser {
  public:
@@ -158,7 +182,7 @@ class H264Parser {
 
  private:
   void walk_slice(const u8* rbsp, size_t n, const h264::SliceHeader& sh, BitReader& br,
-                  const h264::Sps& sps, MbUpdate& upd, int& coded);
+                  const h264::Sps& sps, BlockSink& upd, int& coded);
   std::map<int, h264::Sps> sps_;
   std::map<int, h264::Pps> pps_;
   int active_sps_id_ = -1;
@@ -182,7 +206,7 @@ class H265Parser {
  private:
   void store_parameter_set(int type, const u8* p, size_t n);
   void walk_slice(const u8* rbsp, size_t n, const hevc::SliceHeader& sh, const hevc::Sps& sps,
-                  const hevc::Pps& pps, MbUpdate& upd, int& coded);
+                  const hevc::Pps& pps, BlockSink& upd, int& coded);
   std::map<int, hevc::Vps> vps_;
   std::map<int, hevc::Sps> sps_;
   std::map<int, hevc::Pps> pps_;

@@ -52,6 +52,18 @@ void launch_decode_convert(const DecodeDesc* d_descs, int n, int total_tiles, hi
 // Single-frame variant: descriptor passed by value (op API on caller-owned buffers).
 void launch_decode_convert_one(const DecodeDesc& d, hipStream_t s);
 
+// Gather: copy byte ranges from device-accessible (pinned, mapped) host memory into device
+// memory over PCIe — one workgroup per chunk, 16-byte loads per lane. Replaces a host memcpy
+// into staging + SDMA copy when the slice bytes already live in the pinned ingest pool.
+struct GatherChunk {
+  const u8* src;  // device address of pinned host memory (any alignment)
+  u8* dst;        // device memory, 16-byte aligned
+  u32 len;
+  u32 pad;
+};
+constexpr u32 kGatherChunk = 32u << 10;
+void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s);
+
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
 
 struct LetterboxDesc {

@@ -148,6 +148,28 @@ void launch_decode_convert(const DecodeDesc* d_descs, int n, int total_tiles, hi
 }
 
 // ---------------------------------------------------------------------------------------------
+// Gather (pinned host -> device). The source is read once over PCIe: 256 lanes x 16 B per
+// iteration keeps 4 KiB in flight per workgroup; dst offsets are 16-byte aligned.
+
+__global__ __launch_bounds__(256) void gather_kernel(const GatherChunk* __restrict__ chunks) {
+  const GatherChunk c = chunks[blockIdx.x];
+  const u32 full = c.len & ~15u;
+  for (u32 o = threadIdx.x * 16u; o < full; o += 256u * 16u) {
+    uint4 v;
+    __builtin_memcpy(&v, c.src + o, 16);
+    *reinterpret_cast<uint4*>(c.dst + o) = v;
+  }
+  const u32 tail = c.len - full;
+  if (threadIdx.x < tail) c.dst[full + threadIdx.x] = c.src[full + threadIdx.x];
+}
+
+void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(gather_kernel, dim3(n), dim3(256), 0, s, d_chunks);
+  VEP_HIP(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------------------------
 // Letterbox: bilinear (align_corners=False, as torch F.interpolate / cv2 INTER_LINEAR) resize of
 // the BT.601-converted picture into an S x S canvas, centred, padded with pad_value.
 

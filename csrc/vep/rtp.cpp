@@ -136,6 +136,7 @@ void Depacketizer::finish(std::vector<AuPtr>& out) {
   cur_->corrupt = corrupt_;
   cur_->arrival_ms = now_ms();
   cur_->seq = seq_counter_++;
+  cur_->pin();  // into device-accessible pinned memory when a GPU worker enabled the pool
   out.push_back(cur_);
   cur_.reset();
   corrupt_ = false;

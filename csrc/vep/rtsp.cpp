@@ -343,11 +343,18 @@ std::string RtspClient::run(const AuCallback& cb, const std::atomic<bool>& stop)
           has_sps |= (info_.codec == Codec::kH264) ? t == 7 : t == 33;
         }
         if (!has_sps) {
-          auto a2 = std::make_shared<AccessUnit>(*au);
-          a2->data.clear();
-          a2->nals.clear();
+          auto a2 = std::make_shared<AccessUnit>();
+          a2->codec = au->codec;
+          a2->pts = au->pts;
+          a2->dts = au->dts;
+          a2->duration = au->duration;
+          a2->keyframe = au->keyframe;
+          a2->corrupt = au->corrupt;
+          a2->arrival_ms = au->arrival_ms;
+          a2->seq = au->seq;
           for (auto& ps : info_.param_sets) a2->add_nal(ps.data(), ps.size());
           for (size_t i = 0; i < au->nals.size(); ++i) a2->add_nal(au->nal(i), au->nal_size(i));
+          a2->pin();
           cb(a2);
           params_sent = true;
           continue;

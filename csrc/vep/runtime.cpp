@@ -247,6 +247,7 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       VEP_HIP(hipEventCreate(&st.e0));
       VEP_HIP(hipEventCreate(&st.e1));
     }
+    hostmem::enable_pool();  // AUs finalised from here on are GPU-readable in place
   }
   if (opt_.pack_threads > 0) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads);
   cams_.reserve(size_t(opt_.max_cameras));
@@ -293,6 +294,7 @@ Worker::~Worker() {
     dev_.free(cons_chw_);
   }
   for (Stage& st : stage_) {
+    if (st.h) hostmem::unregister_range(st.h);
     dev_.free(st.d);
     dev_.free_pinned(st.h);
     if (st.copied) (void)hipEventDestroy(st.copied);
@@ -651,10 +653,17 @@ constexpr size_t kPackChunk = size_t(1) << 20;  // bytes per copy task
 void Worker::launch_gpu(Stage& st) {
   std::vector<DecodeJob>& jobs = st.jobs;
   const int n = int(jobs.size());
-  // staging layout: [descs][letterbox descs][per job: mask, prefix, offsets][per job: segments]
+  // staging layout: [descs][letterbox descs][gather chunks][per job: mask, prefix, offsets]
+  // | [per job: segments]. The header part goes over with one small SDMA copy; the payload
+  // (slice bytes) is pulled by the gather kernel, straight from the AU's pinned block when the
+  // AU was finalised into the ingest pool, else from this staging buffer after a host memcpy.
   const size_t off_desc = 0;
   const size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
-  size_t need = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
+  size_t nchunks = 0;
+  for (const auto& j : jobs)
+    for (const auto& sg : j.upd.segs) nchunks += (sg.len + gpu::kGatherChunk - 1) / gpu::kGatherChunk;
+  const size_t off_gather = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
+  size_t need = off_gather + al(sizeof(gpu::GatherChunk) * nchunks);
   std::vector<size_t> mask_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
   std::vector<std::vector<size_t>> seg_off(static_cast<size_t>(n));
   auto words_of = [&](int i) { return size_t(jobs[size_t(i)].upd.mbs() + 31) / 32; };
@@ -664,6 +673,7 @@ void Worker::launch_gpu(Stage& st) {
             al(size_t(jobs[size_t(i)].upd.nslots) * sizeof(u32), 16);
   }
   need = al(need);
+  const size_t header_bytes = need;
   for (int i = 0; i < n; ++i) {
     pay_off[size_t(i)] = need;
     size_t rel = 0;
@@ -675,11 +685,15 @@ void Worker::launch_gpu(Stage& st) {
   }
   need = al(need);
   if (need > st.cap) {
+    if (st.h) hostmem::unregister_range(st.h);
     dev_.free(st.d);
     dev_.free_pinned(st.h);
     st.cap = std::max(need + need / 2, size_t(4) << 20);
     st.h = static_cast<u8*>(dev_.alloc_pinned(st.cap));
     st.d = static_cast<u8*>(dev_.alloc(st.cap));
+    void* hd_ptr = nullptr;
+    if (hipHostGetDevicePointer(&hd_ptr, st.h, 0) != hipSuccess) hd_ptr = st.h;
+    hostmem::register_range(st.h, st.cap, static_cast<u8*>(hd_ptr));
   }
   auto mask_ptr = [&](u8* base, int i) { return reinterpret_cast<u32*>(base + mask_off[size_t(i)]); };
   auto prefix_ptr = [&](u8* base, int i) {
@@ -688,9 +702,9 @@ void Worker::launch_gpu(Stage& st) {
   auto offsets_ptr = [&](u8* base, int i) {
     return reinterpret_cast<u32*>(base + mask_off[size_t(i)] + 2 * al(words_of(i) * sizeof(u32), 16));
   };
-  // Phase 1 (per job): bitmask/prefix + per-MB sample offsets. Phase 2 (1 MiB chunks across
-  // the pack threads): the slices' bytes are copied as received — one large memcpy per slice,
-  // the only host copy — and the kernel reads the PCM samples in place.
+  // Phase 1 (per job): bitmask/prefix + per-MB sample offsets. Phase 2: gather descriptors —
+  // slices already in pinned memory are read in place by the GPU; the rest are copied as
+  // received (1 MiB chunks across the pack threads) into staging first.
   auto index = [&](int i) {
     build_index(jobs[size_t(i)].upd, seg_off[size_t(i)], mask_ptr(st.h, i), prefix_ptr(st.h, i),
                 offsets_ptr(st.h, i));
@@ -706,13 +720,29 @@ void Worker::launch_gpu(Stage& st) {
     size_t len;
   };
   std::vector<CopyTask> tasks;
+  auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
+  size_t ng = 0;
   for (int i = 0; i < n; ++i) {
     const auto& segs = jobs[size_t(i)].upd.segs;
-    for (size_t g = 0; g < segs.size(); ++g)
-      for (size_t o = 0; o < segs[g].len; o += kPackChunk)
-        tasks.push_back({segs[g].base + o, st.h + pay_off[size_t(i)] + seg_off[size_t(i)][g] + o,
-                         std::min(kPackChunk, segs[g].len - o)});
+    for (size_t g = 0; g < segs.size(); ++g) {
+      const size_t dst_off = pay_off[size_t(i)] + seg_off[size_t(i)][g];
+      const u8* src = hostmem::device_address(segs[g].base, segs[g].len);
+      if (!src) {  // pageable AU bytes: stage them
+        for (size_t o = 0; o < segs[g].len; o += kPackChunk)
+          tasks.push_back({segs[g].base + o, st.h + dst_off + o,
+                           std::min(kPackChunk, segs[g].len - o)});
+        src = hostmem::device_address(st.h + dst_off, segs[g].len);
+        VEP_CHECK(src, "staging buffer is not registered");
+        pinned_bytes_staged_ += segs[g].len;
+      } else {
+        pinned_bytes_inplace_ += segs[g].len;
+      }
+      for (size_t o = 0; o < segs[g].len; o += gpu::kGatherChunk)
+        gc[ng++] = {src + o, st.d + dst_off + o,
+                    u32(std::min<size_t>(gpu::kGatherChunk, segs[g].len - o)), 0};
+    }
   }
+  VEP_CHECK(ng == nchunks, "gather chunk count mismatch");
   auto copy = [&](int t) { std::memcpy(tasks[size_t(t)].dst, tasks[size_t(t)].src, tasks[size_t(t)].len); };
   if (pack_pool_ && tasks.size() > 1) pack_pool_->parallel_for(int(tasks.size()), copy);
   else for (int t = 0; t < int(tasks.size()); ++t) copy(t);
@@ -763,8 +793,11 @@ void Worker::launch_gpu(Stage& st) {
       gpu::fill_letterbox_geometry(l, opt_.letterbox_size, opt_.letterbox_format == gpu::kLbNV12);
     }
   }
-  // H2D on the copy stream overlaps the previous batch's kernels on the compute stream
-  VEP_HIP(hipMemcpyAsync(st.d, st.h, need, hipMemcpyHostToDevice, copy_stream_));
+  // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
+  // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
+  VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, copy_stream_));
+  gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather), int(nchunks),
+                     copy_stream_);
   VEP_HIP(hipEventRecord(st.copied, copy_stream_));
   VEP_HIP(hipStreamWaitEvent(stream_, st.copied, 0));
   VEP_HIP(hipEventRecord(st.e0, stream_));

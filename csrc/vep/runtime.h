@@ -220,6 +220,9 @@ class Worker {
   void* consumer_chw() const { return cons_chw_; }
   hipStream_t compute_stream() const { return stream_; }
   u64 batches() const { return batches_.load(); }
+  // slice bytes the GPU read in place from pinned AU blocks vs. staged by a host memcpy
+  u64 bytes_inplace() const { return pinned_bytes_inplace_; }
+  u64 bytes_staged() const { return pinned_bytes_staged_; }
   u64 frames() const { return frames_.load(); }
   double gpu_ms_total() const { return gpu_ms_total_; }
 
@@ -273,6 +276,7 @@ class Worker {
   std::mutex launch_mu_;
   std::atomic<u64> batches_{0}, frames_{0};
   double gpu_ms_total_ = 0;
+  u64 pinned_bytes_inplace_ = 0, pinned_bytes_staged_ = 0;
 };
 
 // Protobuf wire encoding of chrys.cloud.videostreaming.v1beta1.VideoFrame

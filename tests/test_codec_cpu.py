@@ -105,3 +105,18 @@ def test_bt601_reference_matches_numpy(native):
     # sanity vs float BT.601 matrix within 1 LSB
     rf = 1.164383 * (Y - 16) + 1.596027 * (V - 128)
     assert np.abs(np.clip(np.round(rf), 0, 255) - r).max() <= 1
+
+
+@pytest.mark.parametrize("codec", ["h264", "h265"])
+def test_ingest_scan_matches_parser_scan(native, codec):
+    """AccessUnit.pin() records emulation-prevention bytes at ingest (fused into the pinned copy,
+    or scan-only without a GPU); parsing with the recorded positions must decode identically to
+    parsing with the parser's own scan."""
+    enc = synth(native, 320, 240, gop=3, zero=True, codec=codec)
+    a, b = native.CpuDecoder(), native.CpuDecoder()
+    for _ in range(5):
+        au = enc.next()
+        want = a.decode(au)
+        au.pin()
+        assert np.array_equal(b.decode(au), want)
+        assert np.array_equal(b.surface()[0], enc.picture()[0])

@@ -210,3 +210,21 @@ def test_hevc_decode_on_gpu_bit_exact_vs_cpu(native, w, h, slices):
         assert got.shape == (h, w, 3)
         assert np.array_equal(got, want), f"frame {i} mismatch"
         assert meta["frame_type"] == ("I" if i % 4 == 0 else "P")
+
+
+def test_pinned_aus_are_read_in_place(native):
+    """AUs finalised into the pinned ingest pool are gathered by the GPU without a host copy."""
+    wk = native.Worker(device=0)
+    assert native.pinned_pool_stats()["enabled"]
+    cam = wk.add_camera("pin", 3)
+    enc = synth(native, 640, 480, gop=4, motion=0.2)
+    ref = native.CpuDecoder()
+    for i in range(6):
+        au = enc.next()
+        want = ref.decode(au)
+        if i % 2 == 0:
+            assert au.pin() and au.pinned
+        wk.decode_now(cam, au)
+        _, got = wk.read_latest(cam, 0)
+        assert np.array_equal(got, want), i
+    assert wk.bytes_inplace > 0 and wk.bytes_staged > 0
