@@ -46,8 +46,8 @@ def parse_args():
     ap.add_argument("--motion", type=float, default=0.05)
     ap.add_argument("--codec", choices=["h264", "h265"], default="h264",
                     help="h265 = BASELINE config 5 codec (e.g. --width 3840 --height 2160)")
-    ap.add_argument("--threads", type=int, default=8, help="host parse threads per rank")
-    ap.add_argument("--pack-threads", type=int, default=8, help="host staging-pack threads per rank")
+    ap.add_argument("--threads", type=int, default=12, help="host parse threads per rank")
+    ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--consumer-format", choices=["nv12", "bgr"], default="nv12",

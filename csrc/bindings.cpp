@@ -517,6 +517,7 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("threads") = 8, py::arg("ring_slots") = 2, py::arg("prefix") = "cam",
            py::keep_alive<1, 2>())
       .def("step", &ReplayBench::step, py::call_guard<py::gil_scoped_release>())
+      .def("parse_only_ms", &ReplayBench::parse_only_ms, py::call_guard<py::gil_scoped_release>())
       .def("drain", &ReplayBench::drain, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("frames", &ReplayBench::frames)
       .def_property_readonly("payload_bytes", &ReplayBench::bitstream_bytes)

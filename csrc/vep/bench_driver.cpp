@@ -68,6 +68,15 @@ void ReplayBench::parse_tick(std::vector<DecodeJob>& out) {
   out.resize(k);
 }
 
+double ReplayBench::parse_only_ms(int ticks) {
+  drain();
+  std::lock_guard<std::mutex> g(mu_);  // keeps the prefetch thread idle
+  std::vector<DecodeJob> jobs;
+  const i64 t0 = mono_us();
+  for (int t = 0; t < ticks; ++t) parse_tick(jobs);
+  return double(mono_us() - t0) / 1000.0 / std::max(1, ticks);
+}
+
 void ReplayBench::prefetch_loop() {
   std::vector<DecodeJob> jobs;
   for (;;) {

@@ -23,6 +23,9 @@ class ReplayBench {
   ~ReplayBench();
   void step();      // blocks until the tick's frames are published
   void drain();     // wait for any prefetch in flight
+  // Host parse cost alone: run `ticks` parse ticks (no GPU work, jobs dropped) and return the
+  // mean wall ms per tick, split into the parallel parse and the job-vector compaction.
+  double parse_only_ms(int ticks);
   u64 frames() const { return frames_; }
   u64 bitstream_bytes() const { return bytes_; }
   double parse_ms() const { return parse_us_ / 1000.0; }

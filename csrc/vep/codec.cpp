@@ -79,6 +79,13 @@ struct BlockSink {
     if (direct) upd.set(mb, p);
     else pending.emplace_back(mb, u32(p - rbsp));
   }
+  void add_run(int mb0, int count, const u8* p, size_t stride) {
+    if (direct) {
+      upd.set_run(mb0, count, p, stride, u32(upd.segs.size() - 1));
+    } else {
+      for (int k = 0; k < count; ++k) add(mb0 + k, p + size_t(k) * stride);
+    }
+  }
   void resolve(const u8* nal, const std::vector<u32>& epb) {
     if (direct || pending.empty()) return;
     const u32 seg = u32(upd.segs.size() - 1);  // the NAL's segment (begun by the caller)
@@ -162,9 +169,33 @@ void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, Bit
   do {
     if (br.byte_aligned()) {
       size_t off = br.bytepos();
+      // Speculative walk: an I slice whose remaining bytes are exactly k I_PCM records plus
+      // the one-byte trailing 0x80 is taken as k PCM MBs without touching the 2-byte headers
+      // in between (each would be a cold cache miss). Only the first and last headers are
+      // read here; the consumer checks every other one (spec_lo/spec_hi) before publishing.
+      constexpr size_t rec = 2 + kPcmMbBytes;
+      if (is_i && speculate_ && upd.direct && spec_hi_ == spec_lo_ && (stop & 7) == 0) {
+        const size_t end = stop >> 3;
+        if (end > off && (end - off) % rec == 0 && base[end] == 0x80 && base[off] == f0 &&
+            base[off + 1] == f1 && base[end - rec] == f0 && base[end - rec + 1] == f1) {
+          const int k = int((end - off) / rec);
+          VEP_CHECK(mb + k <= total, "macroblock address past end of picture");
+          spec_lo_ = upd.upd.nslots;
+          upd.add_run(mb, k, base + off + 2, rec);
+          spec_hi_ = upd.upd.nslots;
+          if (spec_hi_ - spec_lo_ != k)  // a slice re-coding MBs of an earlier slice
+            throw UnsupportedStream("overlapping slices in one picture");
+          coded += k;
+          br.seek_byte(end);
+          break;
+        }
+      }
       while (off + 2 + kPcmMbBytes <= nbytes && base[off] == f0 && base[off + 1] == f1 &&
              (off + 2) * 8 < stop) {
         VEP_CHECK(mb < total, "macroblock address past end of picture");
+        // the headers sit 386 B apart: a cold slice is one DRAM miss per MB, so keep ~16 in
+        // flight (prefetch past the end of the buffer is harmless on x86 and never faults)
+        __builtin_prefetch(base + off + 64 * (2 + kPcmMbBytes));
         upd.add(mb, base + off + 2);
         ++coded;
         ++mb;
@@ -201,6 +232,7 @@ void H264Parser::walk_slice(const u8* rbsp, size_t n, const SliceHeader& sh, Bit
 PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
   PictureInfo pi;
   bool got_slice = false;
+  spec_lo_ = spec_hi_ = 0;
   for (size_t i = 0; i < au.nals.size(); ++i) {
     const u8* p = au.nal(i);
     size_t n = au.nal_size(i);
@@ -258,10 +290,14 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
       got_slice = true;
     }  // mixed-slice pictures report the first slice's type, as PyAV's pict_type does
     upd.begin_segment(p, n);
+    upd.reserve_blocks(n / kPcmMbBytes + 1);
     BlockSink sink{upd, r, r == p, {}};
     walk_slice(r, rn, sh, br, sps, sink, pi.coded_mbs);
     sink.resolve(p, epb_);
   }
+  pi.spec_lo = spec_lo_;
+  pi.spec_hi = spec_hi_;
+  speculate_ = false;  // one parse only
   VEP_CHECK(got_slice, "access unit has no slice");
   upd.frames += 1;
   return pi;
@@ -423,6 +459,7 @@ PictureInfo H265Parser::parse(const AccessUnit& au, MbUpdate& upd) {
       got_slice = true;
     }
     upd.begin_segment(p, n);
+    upd.reserve_blocks(n / kPcmMbBytes + 1);
     BlockSink sink{upd, r, r == p, {}};
     walk_slice(r, rn, sh, sps, pps, sink, pi.coded_mbs);
     sink.resolve(p, epb_);

@@ -128,10 +128,37 @@ struct MbUpdate {
     frames = 0;
   }
   int mbs() const { return width_mbs * height_mbs; }
+  // Pre-size the per-slot arrays (a slice of n bytes holds at most n / 384 PCM blocks) so a
+  // keyframe's 8k+ blocks do not go through a chain of reallocations.
+  void reserve_blocks(size_t n) {
+    n = std::min(n, size_t(mbs()));
+    src.reserve(src.size() + n);
+    slot_seg.reserve(slot_seg.size() + n);
+    coded.reserve(coded.size() + n);
+  }
   void begin_segment(const u8* base, size_t len) { segs.push_back({base, len}); }
   // Latest writer wins: a MB coded again later in a collapsed GOP re-points its slot.
   // `p` must lie in the most recently begun segment.
   void set(int mb, const u8* p) { set_in(mb, p, u32(segs.size() - 1)); }
+  // A run of blocks of consecutive MBs at a fixed stride (all in segment `seg`).
+  void set_run(int mb0, int count, const u8* p, size_t stride, u32 seg) {
+    bool fresh = true;  // common case (a keyframe slice): no MB of the run coded yet
+    for (int k = 0; k < count && fresh; ++k) fresh = slot[size_t(mb0 + k)] < 0;
+    if (!fresh) {
+      for (int k = 0; k < count; ++k) set_in(mb0 + k, p + size_t(k) * stride, seg);
+      return;
+    }
+    const size_t base = src.size();
+    src.resize(base + size_t(count));
+    slot_seg.resize(base + size_t(count), seg);
+    coded.resize(base + size_t(count));
+    for (int k = 0; k < count; ++k) {
+      slot[size_t(mb0 + k)] = nslots + k;
+      src[base + size_t(k)] = p + size_t(k) * stride;
+      coded[base + size_t(k)] = mb0 + k;
+    }
+    nslots += count;
+  }
   void set_in(int mb, const u8* p, u32 seg) {
     int s = slot[size_t(mb)];
     if (s < 0) {
@@ -157,6 +184,12 @@ struct PictureInfo {
   int frame_num = 0;
   int coded_mbs = 0;                  // non-skipped MBs in this AU
   double fps = 0;
+  // Speculative I-slice walk (H264Parser::set_speculate): payload slots [spec_lo, spec_hi) were
+  // placed by arithmetic (uniform 386-byte I_PCM records, byte-exact slice length) without
+  // reading their headers; the consumer (GPU kernel / CPU path) must check that each such
+  // block is preceded by the I_PCM header bytes 0D 00 before the frame is published.
+  int spec_lo = 0, spec_hi = 0;
+  bool speculative() const { return spec_hi > spec_lo; }
 };
 
 class UnsupportedStream : public Error {
@@ -179,8 +212,13 @@ class H264Parser {
   const h264::Sps& active_sps() const;
   const std::vector<u8>& last_sps_nal() const { return sps_nal_; }
   const std::vector<u8>& last_pps_nal() const { return pps_nal_; }
+  // Allow the header-free I-slice walk for the next parse (single-AU jobs whose consumer
+  // verifies the headers, see PictureInfo::spec_lo).
+  void set_speculate(bool on) { speculate_ = on; }
 
  private:
+  bool speculate_ = false;
+  int spec_lo_ = 0, spec_hi_ = 0;
   void walk_slice(const u8* rbsp, size_t n, const h264::SliceHeader& sh, BitReader& br,
                   const h264::Sps& sps, BlockSink& upd, int& coded);
   std::map<int, h264::Sps> sps_;
@@ -219,9 +257,11 @@ class H265Parser {
 // Codec dispatcher used by cameras (the codec comes from the SDP / AU).
 class StreamParser {
  public:
-  PictureInfo parse(const AccessUnit& au, MbUpdate& upd) {
+  PictureInfo parse(const AccessUnit& au, MbUpdate& upd, bool speculate = false) {
     codec_ = au.codec;
-    return au.codec == Codec::kH265 ? h265_.parse(au, upd) : h264_.parse(au, upd);
+    if (au.codec == Codec::kH265) return h265_.parse(au, upd);
+    h264_.set_speculate(speculate);
+    return h264_.parse(au, upd);
   }
   void absorb_parameter_sets(const AccessUnit& au) {
     codec_ = au.codec;

@@ -42,6 +42,12 @@ struct DecodeDesc {
   i32 crop_left, crop_top;
   i32 tile_begin;     // exclusive prefix sum of tiles over the batch
   i32 tiles_x;
+  // Speculatively placed blocks (PictureInfo::spec_lo/hi): payload slots [chk_lo, chk_hi) must
+  // be preceded by the 2 header bytes chk_pat (little-endian); a mismatch sets *err (pinned
+  // host memory) and the worker drops the frame.
+  i32 chk_lo, chk_hi;
+  u32 chk_pat;
+  u32* err;
 };
 constexpr int kTileMbW = 8, kTileMbH = 2;  // 256 threads: 32 pixel rows x 8 MB columns
 inline int tiles_for(int wmbs, int hmbs) {

@@ -77,6 +77,9 @@ __device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const i
     // samples are read in place from the slice bytes: 2-byte aligned in general (PCM blocks
     // sit at a 386-byte stride after their header), so these are unaligned dwordx4/x2 loads
     const uint8_t* src = d.payload + d.offsets[slot];
+    if (row == 0 && slot >= d.chk_lo && slot < d.chk_hi &&
+        (uint32_t(src[-2]) | (uint32_t(src[-1]) << 8)) != d.chk_pat)
+      __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     uint2 cb, cr;
     __builtin_memcpy(&yv, src + row * 16, 16);
     __builtin_memcpy(&cb, src + 256 + (row >> 1) * 8, 8);

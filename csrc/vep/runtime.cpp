@@ -92,6 +92,11 @@ void FrameRing::commit(int slot, FrameMeta meta) {
   cv_.notify_all();
 }
 
+void FrameRing::abort(int slot) {
+  std::lock_guard<std::mutex> g(meta_mu_);
+  if (slots_[slot]->version.load() & 1) slots_[slot]->version.fetch_add(1, std::memory_order_acq_rel);
+}
+
 bool FrameRing::wait_newer(i64 after, int timeout_ms) const {
   std::unique_lock<std::mutex> g(meta_mu_);
   return cv_.wait_for(g, std::chrono::milliseconds(timeout_ms),
@@ -152,7 +157,9 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
   const AccessUnit* last = nullptr;
   try {
     for (size_t i = from; i < to; ++i) {
-      job.pic = parser_.parse(*gop_[i], job.upd);
+      // single-AU jobs may take the header-free I-slice walk: the worker verifies the skipped
+      // headers on the GPU (or CPU) before it publishes the frame
+      job.pic = parser_.parse(*gop_[i], job.upd, to - from == 1);
       job.upd.keep.push_back(gop_[i]);  // MB samples are referenced in place
       last = gop_[i].get();
     }
@@ -294,6 +301,7 @@ Worker::~Worker() {
     dev_.free(cons_chw_);
   }
   for (Stage& st : stage_) {
+    dev_.free_pinned(st.err);
     if (st.h) hostmem::unregister_range(st.h);
     dev_.free(st.d);
     dev_.free_pinned(st.h);
@@ -749,6 +757,15 @@ void Worker::launch_gpu(Stage& st) {
   const i64 t_enq0 = mono_us();
   timers.copy += double(t_enq0 - t_copy0);
 
+  if (st.err_cap < size_t(n)) {
+    if (st.err) dev_.free_pinned(st.err);
+    st.err_cap = std::max<size_t>(size_t(n), 64);
+    st.err = static_cast<u32*>(dev_.alloc_pinned(st.err_cap * sizeof(u32)));
+    void* ed = nullptr;
+    if (hipHostGetDevicePointer(&ed, st.err, 0) != hipSuccess) ed = st.err;
+    st.err_dev = static_cast<const u32*>(ed);
+  }
+  std::memset(st.err, 0, size_t(n) * sizeof(u32));
   auto* hd = reinterpret_cast<gpu::DecodeDesc*>(st.h + off_desc);
   auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(st.h + off_lb);
   int tiles = 0;
@@ -773,6 +790,10 @@ void Worker::launch_gpu(Stage& st) {
     d.crop_top = j.pic.crop_top;
     d.tiles_x = (d.wmbs + gpu::kTileMbW - 1) / gpu::kTileMbW;
     d.tile_begin = tiles;
+    d.chk_lo = j.pic.spec_lo;
+    d.chk_hi = j.pic.spec_hi;
+    d.chk_pat = 0x000Du;  // I_PCM header bytes 0D 00
+    d.err = const_cast<u32*>(st.err_dev) + i;
     tiles += gpu::tiles_for(d.wmbs, d.hmbs);
     if (opt_.letterbox_size > 0) {
       gpu::LetterboxDesc& l = hl[i];
@@ -820,9 +841,17 @@ void Worker::launch_gpu(Stage& st) {
   timers.enqueue += double(mono_us() - t_enq0);
 }
 
-void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
+void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
+                     std::vector<u32>& err) {
+  err.assign(jobs.size(), 0);
   for (size_t i = 0; i < jobs.size(); ++i) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
+    const PictureInfo& pi = jobs[i].pic;
+    for (int sl = pi.spec_lo; sl < pi.spec_hi && !err[i]; ++sl) {  // speculative headers
+      const u8* b = jobs[i].upd.block(sl);
+      err[i] = (b[-2] != 0x0D || b[-1] != 0x00) ? 1u : 0u;
+    }
+    if (err[i]) continue;
     cpu_apply_update(jobs[i].upd, c.surface.host);
     cpu_nv12_to_bgr(c.surface.host, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
                     jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
@@ -858,12 +887,26 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
   }
 }
 
-void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
+void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, const u32* err) {
   const i64 t = mono_us();
   std::lock_guard<std::mutex> g(cams_mu_);
   for (size_t i = 0; i < jobs.size(); ++i) {
     auto& cp = cams_[size_t(jobs[i].cam)];
     if (!cp || !cp->ring_) continue;
+    if (err && err[i]) {
+      cp->errors.fetch_add(1, std::memory_order_relaxed);
+      cp->logs.add(true, "corrupt keyframe: I_PCM header check failed; waiting for the next keyframe");
+      cp->broken_ = true;
+      cp->ring_->abort(slots[i]);
+      continue;
+    }
+    if (cp->broken_) {  // surfaces are garbage until a keyframe rewrites every MB
+      if (!jobs[i].refresh) {
+        cp->ring_->abort(slots[i]);
+        continue;
+      }
+      cp->broken_ = false;
+    }
     jobs[i].meta.decoded_us = t;
     cp->ring_->commit(slots[i], jobs[i].meta);
     cp->decoded.fetch_add(1, std::memory_order_relaxed);
@@ -880,7 +923,7 @@ void Worker::complete(Stage& st) {
   timers.wait += double(mono_us() - t0);
   float ms = 0;
   if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) gpu_ms_total_ += ms;
-  publish(st.jobs, st.slots);
+  publish(st.jobs, st.slots, st.err);
   st.jobs.clear();
   st.slots.clear();
 }
@@ -907,8 +950,9 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
   timers.prepare += double(mono_us() - t0);
   if (jobs.empty()) return;
   if (!dev_.gpu()) {
-    run_cpu(jobs, slots);
-    publish(jobs, slots);
+    std::vector<u32> err;
+    run_cpu(jobs, slots, err);
+    publish(jobs, slots, err.data());
     jobs.clear();
     return;
   }

@@ -66,6 +66,8 @@ class FrameRing {
   // writer side (single writer: the worker thread)
   int begin_write();
   void commit(int slot, FrameMeta meta);
+  // Release a slot from begin_write() without publishing (frame dropped after a failed check).
+  void abort(int slot);
   // reader side: newest committed frame with seq > after (false if none)
   bool latest(i64 after, FrameMeta* meta, int* slot) const;
   // true if `slot` still holds the frame with publish counter `seq`
@@ -163,6 +165,7 @@ class Camera {
   std::mutex mu_;
   std::vector<AuPtr> gop_;
   size_t decoded_upto_ = 0;  // gop_[0, decoded_upto_) are reconstructed on the surface
+  bool broken_ = false;      // worker thread: a published frame failed its check; drop until IDR
   i64 keyframes_ = 0;
   StreamParser parser_;
 };
@@ -235,13 +238,18 @@ class Worker {
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;
     bool active = false;
+    u32* err = nullptr;        // pinned per-job check flags (written by the kernel)
+    const u32* err_dev = nullptr;
+    size_t err_cap = 0;
   };
   void loop();
   void ensure_surface(Camera& c, const PictureInfo& pi);
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
   void launch_gpu(Stage& st);
-  void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
-  void publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
+  void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err);
+  // err[i] != 0: job i failed its speculative-header check (dropped, camera waits for the
+  // next keyframe)
+  void publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, const u32* err = nullptr);
   void complete(Stage& st);
   void complete_locked();
   WorkerOptions opt_;

@@ -228,3 +228,9 @@ def test_pinned_aus_are_read_in_place(native):
         _, got = wk.read_latest(cam, 0)
         assert np.array_equal(got, want), i
     assert wk.bytes_inplace > 0 and wk.bytes_staged > 0
+
+
+def test_speculative_keyframe_walk_is_verified_gpu(native):
+    from test_runtime_semantics import run_speculation_check
+
+    run_speculation_check(native, 0)

@@ -126,3 +126,42 @@ def test_cpu_worker_nv12_consumer_matches_reference(native):
     yh, uvh = ref.surface()
     want = ops.letterbox_nv12_reference(torch.from_numpy(yh), torch.from_numpy(uvh), S, 96, 64)
     assert (buf[0].int() - want.int()).abs().max().item() <= 1
+
+
+def corrupt_inner_pcm_header(native, au, records_from_end=100):
+    """Same length, but one I_PCM MB header deep inside the slice is wrong: only the worker's
+    speculative-header check can see it (the host walk does not read those bytes)."""
+    nals = au.nals()
+    sl = bytearray(nals[-1])
+    pos = len(sl) - 1 - 386 * records_from_end
+    assert sl[pos] == 0x0D and sl[pos + 1] == 0x00
+    sl[pos] = 0x0E
+    return native.AccessUnit.from_nals(nals[:-1] + [bytes(sl)], pts=au.pts, dts=au.dts,
+                                       keyframe=True)
+
+
+def run_speculation_check(native, device):
+    wk = native.Worker(device=device)
+    cam = wk.add_camera("spec", 3)
+    enc = synth(native, 640, 480, gop=3, motion=0.2)
+    ref = native.CpuDecoder()
+    aus = [enc.next() for _ in range(7)]  # I P P I P P I
+    wk.decode_now(cam, aus[0])
+    wk.decode_now(cam, aus[1])
+    assert wk.published(cam) == 2
+    bad = corrupt_inner_pcm_header(native, aus[3])
+    wk.decode_now(cam, bad)
+    wk.decode_now(cam, aus[4])  # reference is garbage: suppressed until the next keyframe
+    wk.decode_now(cam, aus[5])
+    assert wk.published(cam) == 2 and wk.stats(cam)["errors"] == 1
+    assert "I_PCM header check failed" in wk.logs(cam, True)
+    wk.decode_now(cam, aus[6])
+    assert wk.published(cam) == 3
+    for a in aus:
+        want = ref.decode(a)
+    _, got = wk.read_latest(cam, 0)
+    assert np.array_equal(got, want)
+
+
+def test_speculative_keyframe_walk_is_verified_cpu(native):
+    run_speculation_check(native, -1)
