@@ -247,7 +247,11 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (dev_.gpu()) {
     dev_.bind();
     VEP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    VEP_HIP(hipStreamCreateWithFlags(&copy_stream_, hipStreamNonBlocking));
+    // The copy stream's gather kernel is PCIe-latency bound and must keep its waves resident
+    // while the previous batch's decode kernel floods the CUs: give it dispatch priority.
+    int prio_lo = 0, prio_hi = 0;
+    VEP_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    VEP_HIP(hipStreamCreateWithPriority(&copy_stream_, hipStreamNonBlocking, prio_hi));
     VEP_HIP(hipStreamCreateWithFlags(&serve_stream_, hipStreamNonBlocking));
     for (Stage& st : stage_) {
       VEP_HIP(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
