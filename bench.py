@@ -224,6 +224,9 @@ def main():
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "payload_path": ("decode kernel reads slice bytes from pinned host memory over PCIe"
+                             if getattr(worker, "direct_reads", False) else
+                             "gather kernel pulls slice bytes into HBM, decode reads HBM"),
             "rank0_slice_bytes_per_step": {
                 "gpu_read_in_place_from_pinned": (worker.bytes_inplace - ip0) // a.steps,
                 "host_staged": (worker.bytes_staged - sg0) // a.steps},

@@ -504,6 +504,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("frames", &Worker::frames)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
       .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)
+      .def_property_readonly("direct_reads", &Worker::direct_reads)
       .def_property_readonly("bytes_staged", &Worker::bytes_staged)
       .def("compute_stream_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.compute_stream()); });
 

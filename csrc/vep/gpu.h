@@ -37,6 +37,8 @@ struct DecodeDesc {
   const u32* prefix;
   const u32* offsets;  // per coded MB (raster order): byte offset of its 384 samples in payload
   const u8* payload;   // the slices' bytes as received (samples read in place, unaligned)
+  const u64* ptrs;     // direct mode (non-null): per coded MB, device address of its samples in
+                       // pinned host memory — read over PCIe; offsets/payload unused
   i32 wmbs, hmbs;
   i32 out_w, out_h;
   i32 crop_left, crop_top;

@@ -76,7 +76,8 @@ __device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const i
   if (slot >= 0) {
     // samples are read in place from the slice bytes: 2-byte aligned in general (PCM blocks
     // sit at a 386-byte stride after their header), so these are unaligned dwordx4/x2 loads
-    const uint8_t* src = d.payload + d.offsets[slot];
+    const uint8_t* src = d.ptrs ? reinterpret_cast<const uint8_t*>(d.ptrs[slot])
+                                : d.payload + d.offsets[slot];
     if (row == 0 && slot >= d.chk_lo && slot < d.chk_hi &&
         (uint32_t(src[-2]) | (uint32_t(src[-1]) << 8)) != d.chk_pat)
       __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

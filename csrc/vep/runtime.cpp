@@ -259,6 +259,8 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       VEP_HIP(hipEventCreate(&st.e1));
     }
     hostmem::enable_pool();  // AUs finalised from here on are GPU-readable in place
+    const char* dr = std::getenv("VEP_DIRECT_READS");
+    direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
   if (opt_.pack_threads > 0) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads);
   cams_.reserve(size_t(opt_.max_cameras));
@@ -658,6 +660,33 @@ void build_index(const MbUpdate& u, const std::vector<size_t>& seg_off, u32* mas
   }
 }
 
+// Direct mode: per coded MB the device address of its samples inside host memory (pinned AU
+// block or staging), instead of an offset into a device-side copy.
+void build_index_ptrs(const MbUpdate& u, const std::vector<const u8*>& seg_dev, u32* mask,
+                      u32* prefix, u64* ptrs) {
+  const int words = (u.mbs() + 31) / 32;
+  std::memset(mask, 0, size_t(words) * sizeof(u32));
+  const std::vector<i32>* list = &u.coded;
+  std::vector<i32> sorted;
+  if (!std::is_sorted(u.coded.begin(), u.coded.end())) {
+    sorted = u.coded;
+    std::sort(sorted.begin(), sorted.end());
+    list = &sorted;
+  }
+  size_t k = 0;
+  for (i32 mb : *list) {
+    mask[mb >> 5] |= 1u << (mb & 31);
+    const int s = u.slot[size_t(mb)];
+    const u32 g = u.slot_seg[size_t(s)];
+    ptrs[k++] = reinterpret_cast<u64>(seg_dev[g] + (u.block(s) - u.segs[g].base));
+  }
+  u32 run = 0;
+  for (int w = 0; w < words; ++w) {
+    prefix[w] = run;
+    run += u32(__builtin_popcount(mask[w]));
+  }
+}
+
 constexpr size_t kPackChunk = size_t(1) << 20;  // bytes per copy task
 
 }  // namespace
@@ -665,24 +694,32 @@ constexpr size_t kPackChunk = size_t(1) << 20;  // bytes per copy task
 void Worker::launch_gpu(Stage& st) {
   std::vector<DecodeJob>& jobs = st.jobs;
   const int n = int(jobs.size());
-  // staging layout: [descs][letterbox descs][gather chunks][per job: mask, prefix, offsets]
-  // | [per job: segments]. The header part goes over with one small SDMA copy; the payload
-  // (slice bytes) is pulled by the gather kernel, straight from the AU's pinned block when the
-  // AU was finalised into the ingest pool, else from this staging buffer after a host memcpy.
+  // Slice bytes stay in host memory: pinned AU blocks as received (hostmem.h), or this stage's
+  // pinned staging buffer for pageable AUs (one host memcpy). Two ways to the GPU:
+  //  * direct (default): decode_convert reads each block straight over PCIe from its host
+  //    address (per-MB 64-bit pointer table) — no device copy of the payload at all;
+  //  * gather: a gather kernel on the copy stream first pulls the slices into device staging,
+  //    and the kernel reads per-MB offsets into that copy.
+  // Layout: [descs][letterbox descs][gather chunks][per job: mask, prefix, offsets|ptrs]
+  // | [per job: staged payload]. Only the header part is copied by SDMA.
+  const bool direct = direct_reads_;
   const size_t off_desc = 0;
   const size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
   size_t nchunks = 0;
-  for (const auto& j : jobs)
-    for (const auto& sg : j.upd.segs) nchunks += (sg.len + gpu::kGatherChunk - 1) / gpu::kGatherChunk;
+  if (!direct)
+    for (const auto& j : jobs)
+      for (const auto& sg : j.upd.segs)
+        nchunks += (sg.len + gpu::kGatherChunk - 1) / gpu::kGatherChunk;
   const size_t off_gather = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
   size_t need = off_gather + al(sizeof(gpu::GatherChunk) * nchunks);
   std::vector<size_t> mask_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
   std::vector<std::vector<size_t>> seg_off(static_cast<size_t>(n));
   auto words_of = [&](int i) { return size_t(jobs[size_t(i)].upd.mbs() + 31) / 32; };
+  const size_t ent = direct ? sizeof(u64) : sizeof(u32);
   for (int i = 0; i < n; ++i) {
     mask_off[size_t(i)] = need;
     need += 2 * al(words_of(i) * sizeof(u32), 16) +
-            al(size_t(jobs[size_t(i)].upd.nslots) * sizeof(u32), 16);
+            al(size_t(jobs[size_t(i)].upd.nslots) * ent, 16);
   }
   need = al(need);
   const size_t header_bytes = need;
@@ -711,27 +748,17 @@ void Worker::launch_gpu(Stage& st) {
   auto prefix_ptr = [&](u8* base, int i) {
     return reinterpret_cast<u32*>(base + mask_off[size_t(i)] + al(words_of(i) * sizeof(u32), 16));
   };
-  auto offsets_ptr = [&](u8* base, int i) {
-    return reinterpret_cast<u32*>(base + mask_off[size_t(i)] + 2 * al(words_of(i) * sizeof(u32), 16));
+  auto table_ptr = [&](u8* base, int i) {
+    return base + mask_off[size_t(i)] + 2 * al(words_of(i) * sizeof(u32), 16);
   };
-  // Phase 1 (per job): bitmask/prefix + per-MB sample offsets. Phase 2: gather descriptors —
-  // slices already in pinned memory are read in place by the GPU; the rest are copied as
-  // received (1 MiB chunks across the pack threads) into staging first.
-  auto index = [&](int i) {
-    build_index(jobs[size_t(i)].upd, seg_off[size_t(i)], mask_ptr(st.h, i), prefix_ptr(st.h, i),
-                offsets_ptr(st.h, i));
-  };
-  const i64 t_index0 = mono_us();
-  if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
-  else for (int i = 0; i < n; ++i) index(i);
-  const i64 t_copy0 = mono_us();
-  timers.index += double(t_copy0 - t_index0);
+  // Phase 1: where each segment's bytes are readable by the GPU (staging pageable ones).
   struct CopyTask {
     const u8* src;
     u8* dst;
     size_t len;
   };
   std::vector<CopyTask> tasks;
+  std::vector<std::vector<const u8*>> seg_dev(static_cast<size_t>(n));
   auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
   size_t ng = 0;
   for (int i = 0; i < n; ++i) {
@@ -749,12 +776,28 @@ void Worker::launch_gpu(Stage& st) {
       } else {
         pinned_bytes_inplace_ += segs[g].len;
       }
-      for (size_t o = 0; o < segs[g].len; o += gpu::kGatherChunk)
-        gc[ng++] = {src + o, st.d + dst_off + o,
-                    u32(std::min<size_t>(gpu::kGatherChunk, segs[g].len - o)), 0};
+      seg_dev[size_t(i)].push_back(src);
+      if (!direct)
+        for (size_t o = 0; o < segs[g].len; o += gpu::kGatherChunk)
+          gc[ng++] = {src + o, st.d + dst_off + o,
+                      u32(std::min<size_t>(gpu::kGatherChunk, segs[g].len - o)), 0};
     }
   }
   VEP_CHECK(ng == nchunks, "gather chunk count mismatch");
+  // Phase 2 (per job, pack threads): coded-MB bitmask/prefix + per-MB offsets or pointers.
+  auto index = [&](int i) {
+    if (direct)
+      build_index_ptrs(jobs[size_t(i)].upd, seg_dev[size_t(i)], mask_ptr(st.h, i),
+                       prefix_ptr(st.h, i), reinterpret_cast<u64*>(table_ptr(st.h, i)));
+    else
+      build_index(jobs[size_t(i)].upd, seg_off[size_t(i)], mask_ptr(st.h, i), prefix_ptr(st.h, i),
+                  reinterpret_cast<u32*>(table_ptr(st.h, i)));
+  };
+  const i64 t_index0 = mono_us();
+  if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
+  else for (int i = 0; i < n; ++i) index(i);
+  const i64 t_copy0 = mono_us();
+  timers.index += double(t_copy0 - t_index0);
   auto copy = [&](int t) { std::memcpy(tasks[size_t(t)].dst, tasks[size_t(t)].src, tasks[size_t(t)].len); };
   if (pack_pool_ && tasks.size() > 1) pack_pool_->parallel_for(int(tasks.size()), copy);
   else for (int t = 0; t < int(tasks.size()); ++t) copy(t);
@@ -784,8 +827,15 @@ void Worker::launch_gpu(Stage& st) {
     (void)words;
     d.mask = mask_ptr(st.d, i);
     d.prefix = prefix_ptr(st.d, i);
-    d.offsets = offsets_ptr(st.d, i);
-    d.payload = st.d + pay_off[size_t(i)];
+    if (direct) {
+      d.ptrs = reinterpret_cast<const u64*>(table_ptr(st.d, i));
+      d.offsets = nullptr;
+      d.payload = nullptr;
+    } else {
+      d.ptrs = nullptr;
+      d.offsets = reinterpret_cast<const u32*>(table_ptr(st.d, i));
+      d.payload = st.d + pay_off[size_t(i)];
+    }
     d.wmbs = j.upd.width_mbs;
     d.hmbs = j.upd.height_mbs;
     d.out_w = j.pic.width;
@@ -821,8 +871,9 @@ void Worker::launch_gpu(Stage& st) {
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
   VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, copy_stream_));
-  gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather), int(nchunks),
-                     copy_stream_);
+  if (!direct)
+    gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
+                       int(nchunks), copy_stream_);
   VEP_HIP(hipEventRecord(st.copied, copy_stream_));
   VEP_HIP(hipStreamWaitEvent(stream_, st.copied, 0));
   VEP_HIP(hipEventRecord(st.e0, stream_));

@@ -179,6 +179,7 @@ struct WorkerOptions {
   float std[3] = {1.f, 1.f, 1.f};
   int max_cameras = 256;
   int pack_threads = 4;       // host threads packing MB payloads into pinned staging
+  bool direct_reads = true;   // decode kernel reads slice bytes from host memory (else gather)
 };
 
 class Worker {
@@ -285,6 +286,10 @@ class Worker {
   std::atomic<u64> batches_{0}, frames_{0};
   double gpu_ms_total_ = 0;
   u64 pinned_bytes_inplace_ = 0, pinned_bytes_staged_ = 0;
+  bool direct_reads_ = false;
+
+ public:
+  bool direct_reads() const { return direct_reads_; }
 };
 
 // Protobuf wire encoding of chrys.cloud.videostreaming.v1beta1.VideoFrame
