@@ -54,37 +54,56 @@ __device__ __forceinline__ void convert16(const uint4 yv, const uint4 uvv, uint3
     out[k] = pack4(px[4 * k], px[4 * k + 1], px[4 * k + 2], px[4 * k + 3]);
 }
 
-__device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const int tile) {
+// One 8x2-MB tile per 256-thread workgroup. Phase 1 stages the tile's coded PCM blocks into LDS
+// with coalesced loads: 24 lanes x 16 B cover one block's 384 contiguous bytes, so a block is a
+// few full PCIe read requests when the bytes live in pinned host memory (direct mode) and full
+// cache lines otherwise. Phase 2: each lane owns one 16-pixel row of one MB — reconstructs it
+// into the NV12 reference surfaces and converts it to 48 bytes of BGR24.
+__device__ __forceinline__ void decode_convert_tile(const DecodeDesc& d, const int tile,
+                                                   uint8_t (*blk)[kPcmMbBytes]) {
   const int tx = tile % d.tiles_x, ty = tile / d.tiles_x;
   const int t = threadIdx.x;
+  auto slot_of = [&](int mbx, int mby) {
+    if (!d.mask || mbx >= d.wmbs || mby >= d.hmbs) return -1;
+    const int mb = mby * d.wmbs + mbx;
+    const uint32_t w = d.mask[mb >> 5];
+    const uint32_t bit = 1u << (mb & 31);
+    return (w & bit) ? int(d.prefix[mb >> 5] + __builtin_popcount(w & (bit - 1u))) : -1;
+  };
+  auto src_of = [&](int slot) {
+    return d.ptrs ? reinterpret_cast<const uint8_t*>(d.ptrs[slot]) : d.payload + d.offsets[slot];
+  };
+  // phase 1: LDS staging (MB i of the tile = column i & 7, MB row i >> 3)
+  constexpr int kParts = kPcmMbBytes / 16;  // 24
+  for (int idx = t; idx < kTileMbW * kTileMbH * kParts; idx += 256) {
+    const int i = idx / kParts, part = idx - i * kParts;
+    const int slot = slot_of(tx * kTileMbW + (i & 7), ty * kTileMbH + (i >> 3));
+    if (slot < 0) continue;
+    const uint8_t* src = src_of(slot);
+    uint4 v;
+    __builtin_memcpy(&v, src + part * 16, 16);
+    *reinterpret_cast<uint4*>(&blk[i][part * 16]) = v;
+    if (part == 0 && slot >= d.chk_lo && slot < d.chk_hi &&
+        (uint32_t(src[-2]) | (uint32_t(src[-1]) << 8)) != d.chk_pat)
+      __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  // phase 2
   const int r = t >> 3, c = t & 7;
   const int mbx = tx * kTileMbW + c;
   const int mby = ty * kTileMbH + (r >> 4);
   const int row = r & 15;
   if (mbx >= d.wmbs || mby >= d.hmbs) return;
   const int pitch = d.wmbs * 16;
-  const int mb = mby * d.wmbs + mbx;
-  int slot = -1;
-  if (d.mask) {
-    const uint32_t w = d.mask[mb >> 5];
-    const uint32_t bit = 1u << (mb & 31);
-    if (w & bit) slot = int(d.prefix[mb >> 5] + __builtin_popcount(w & (bit - 1u)));
-  }
+  const int slot = slot_of(mbx, mby);
   uint8_t* yp = d.y + size_t(mby * 16 + row) * pitch + mbx * 16;
   uint8_t* uvp = d.uv + size_t(mby * 8 + (row >> 1)) * pitch + mbx * 16;
   uint4 yv, uvv;
   if (slot >= 0) {
-    // samples are read in place from the slice bytes: 2-byte aligned in general (PCM blocks
-    // sit at a 386-byte stride after their header), so these are unaligned dwordx4/x2 loads
-    const uint8_t* src = d.ptrs ? reinterpret_cast<const uint8_t*>(d.ptrs[slot])
-                                : d.payload + d.offsets[slot];
-    if (row == 0 && slot >= d.chk_lo && slot < d.chk_hi &&
-        (uint32_t(src[-2]) | (uint32_t(src[-1]) << 8)) != d.chk_pat)
-      __hip_atomic_store(d.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    uint2 cb, cr;
-    __builtin_memcpy(&yv, src + row * 16, 16);
-    __builtin_memcpy(&cb, src + 256 + (row >> 1) * 8, 8);
-    __builtin_memcpy(&cr, src + 320 + (row >> 1) * 8, 8);
+    const uint8_t* b = blk[(r >> 4) * kTileMbW + c];
+    yv = *reinterpret_cast<const uint4*>(b + row * 16);
+    const uint2 cb = *reinterpret_cast<const uint2*>(b + 256 + (row >> 1) * 8);
+    const uint2 cr = *reinterpret_cast<const uint2*>(b + 320 + (row >> 1) * 8);
     // interleave Cb/Cr bytes: (cb0 cr0 cb1 cr1) ...
     uvv.x = __builtin_amdgcn_perm(cr.x, cb.x, 0x05010400u);
     uvv.y = __builtin_amdgcn_perm(cr.x, cb.x, 0x07030602u);
@@ -132,11 +151,13 @@ __global__ __launch_bounds__(256) void decode_convert_kernel(const DecodeDesc* _
     if (descs[mid].tile_begin <= b) lo = mid; else hi = mid - 1;
   }
   const DecodeDesc d = descs[lo];
-  decode_convert_tile(d, b - d.tile_begin);
+  __shared__ __attribute__((aligned(16))) uint8_t blk[kTileMbW * kTileMbH][kPcmMbBytes];
+  decode_convert_tile(d, b - d.tile_begin, blk);
 }
 
 __global__ __launch_bounds__(256) void decode_convert_one_kernel(const DecodeDesc d) {
-  decode_convert_tile(d, blockIdx.x);
+  __shared__ __attribute__((aligned(16))) uint8_t blk[kTileMbW * kTileMbH][kPcmMbBytes];
+  decode_convert_tile(d, blockIdx.x, blk);
 }
 
 void launch_decode_convert_one(const DecodeDesc& d, hipStream_t s) {
