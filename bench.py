@@ -218,6 +218,7 @@ def main():
             "next_frame_latency_definition": "back-to-back requests on one stream/channel (the "
                                              "reference clients' pattern): includes waiting for "
                                              "the camera's next decoded frame",
+            "rocdecode_available": bool(vep.rocdecode_available()),
             "decoder_backend": "native subset decoder: CPU " + ENTROPY[a.codec] + " parse + gfx950 "
                                "HIP PCM reconstruct/NV12->BGR24 (rocDecode absent in image)",
             "per_gpu_fps": round(fps / max(world, 1), 2),

@@ -276,6 +276,7 @@ PYBIND11_MODULE(_vep, m) {
     const double scan_us = double(mono_us() - t0) / iters;
     return std::make_pair(parse_us, scan_us);
   }, py::arg("au"), py::arg("iters") = 100, py::arg("prime") = nullptr);
+  m.def("rocdecode_available", [] { return gpu::rocdecode_available(); });
   m.def("pinned_pool_stats", [] {
     hostmem::PoolStats st = hostmem::pool_stats();
     py::dict d;
@@ -396,6 +397,13 @@ PYBIND11_MODULE(_vep, m) {
              d["width"] = ring ? ring->width() : 0;
              d["height"] = ring ? ring->height() : 0;
              d["ring_slots"] = ring ? ring->slots() : c.ring_slots_cfg;
+             py::list hist;
+             for (auto& h : c.lat_hist) hist.append(h.load());
+             d["latency_hist"] = hist;
+             d["latency_sum_ms"] = c.lat_sum_ms.load();
+             py::list bounds;
+             for (double b : Camera::kLatBucketsMs) bounds.append(b);
+             d["latency_bounds_ms"] = bounds;
              return d;
            })
       .def("log", [](Worker& w, int i, bool err, const std::string& line) { cam_of(w, i).logs.add(err, line); })

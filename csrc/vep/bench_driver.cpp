@@ -3,6 +3,8 @@
 
 #include <algorithm>
 
+#include "trace.h"
+
 namespace vep {
 
 ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cached_frames,
@@ -41,6 +43,7 @@ ReplayBench::~ReplayBench() {
 }
 
 void ReplayBench::parse_tick(std::vector<DecodeJob>& out) {
+  trace::Range tr("vep.parse_tick");
   const int n = int(cams_.size());
   out.clear();
   out.resize(size_t(n));

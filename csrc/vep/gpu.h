@@ -24,6 +24,7 @@ namespace vep::gpu {
   } while (0)
 
 int device_count();  // 0 when no GPU / no driver
+bool rocdecode_available();  // VCN backend library present (backend.cpp)
 
 // One camera-frame of a batched decode_convert launch (lives in device memory).
 struct DecodeDesc {

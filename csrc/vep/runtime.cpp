@@ -5,6 +5,7 @@
 #include <cmath>
 
 #include "color.h"
+#include "trace.h"
 
 namespace vep {
 
@@ -794,8 +795,11 @@ void Worker::launch_gpu(Stage& st) {
                   reinterpret_cast<u32*>(table_ptr(st.h, i)));
   };
   const i64 t_index0 = mono_us();
-  if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
-  else for (int i = 0; i < n; ++i) index(i);
+  {
+    trace::Range tr("vep.index");
+    if (pack_pool_ && n > 1) pack_pool_->parallel_for(n, index);
+    else for (int i = 0; i < n; ++i) index(i);
+  }
   const i64 t_copy0 = mono_us();
   timers.index += double(t_copy0 - t_index0);
   auto copy = [&](int t) { std::memcpy(tasks[size_t(t)].dst, tasks[size_t(t)].src, tasks[size_t(t)].len); };
@@ -943,7 +947,9 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
 }
 
 void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, const u32* err) {
+  trace::Range tr("vep.publish");
   const i64 t = mono_us();
+  const i64 wall = now_ms();
   std::lock_guard<std::mutex> g(cams_mu_);
   for (size_t i = 0; i < jobs.size(); ++i) {
     auto& cp = cams_[size_t(jobs[i].cam)];
@@ -963,6 +969,13 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       cp->broken_ = false;
     }
     jobs[i].meta.decoded_us = t;
+    if (jobs[i].meta.arrival_ms > 0) {
+      const i64 lat = std::max<i64>(0, wall - jobs[i].meta.arrival_ms);
+      int b = 0;
+      while (b < Camera::kLatBuckets - 1 && double(lat) > Camera::kLatBucketsMs[b]) ++b;
+      cp->lat_hist[b].fetch_add(1, std::memory_order_relaxed);
+      cp->lat_sum_ms.fetch_add(u64(lat), std::memory_order_relaxed);
+    }
     cp->ring_->commit(slots[i], jobs[i].meta);
     cp->decoded.fetch_add(1, std::memory_order_relaxed);
   }
@@ -974,7 +987,10 @@ void Worker::complete(Stage& st) {
   if (!st.active) return;
   st.active = false;
   const i64 t0 = mono_us();
-  VEP_HIP(hipEventSynchronize(st.e1));
+  {
+    trace::Range tr("vep.wait_gpu");
+    VEP_HIP(hipEventSynchronize(st.e1));
+  }
   timers.wait += double(mono_us() - t0);
   float ms = 0;
   if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) gpu_ms_total_ += ms;
@@ -996,6 +1012,7 @@ void Worker::complete_all() {
 }
 
 void Worker::launch_async(std::vector<DecodeJob>& jobs) {
+  trace::Range tr("vep.launch_async");
   if (jobs.empty()) return;
   std::lock_guard<std::mutex> lg(launch_mu_);
   dev_.bind();

@@ -136,6 +136,11 @@ class Camera {
 
   // --- stats ---
   std::atomic<u64> packets{0}, decoded{0}, skipped{0}, errors{0}, bytes_in{0};
+  // packet arrival -> frame published (ms) histogram, upper bounds kLatBucketsMs (+inf last)
+  static constexpr int kLatBuckets = 12;
+  static constexpr double kLatBucketsMs[kLatBuckets - 1] = {1, 2, 5, 10, 20, 35, 50, 100, 250, 500, 1000};
+  std::atomic<u64> lat_hist[kLatBuckets] = {};
+  std::atomic<u64> lat_sum_ms{0};
   std::atomic<i64> last_packet_ms{0};
   LogRing logs;
 

@@ -1,5 +1,6 @@
 #!/bin/bash
-# One gpurun call: GPU tests, smoke, 1-GPU bench, rocprofv3 kernel stats. Stops at first failure.
+# One gpurun call: GPU tests, smoke, 1-GPU bench, rocprofv3 kernel stats + roctx marker trace.
+# Stops at the first failure.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -14,8 +15,12 @@ tail -1 gpurun_out/smoke.log
 echo "[gpu_check] bench"
 timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
-echo "[gpu_check] rocprofv3"
+echo "[gpu_check] rocprofv3 kernel stats"
 export TMPDIR=/tmp
-cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 30 --warmup 5 > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/prof.log"; exit 1; }
-find "$R/gpurun_out/prof" -name "*stats*" | head
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$R/gpurun_out/prof" -o run -- python3 "$R/bench.py" --steps 30 --warmup 5 --latency-samples 0 > "$R/gpurun_out/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$R/gpurun_out/prof.log"; exit 1; }
+echo "[gpu_check] rocprofv3 roctx marker trace (host stages next to kernels)"
+export VEP_ROCTX=1
+cd /tmp && timeout -k 10 300 rocprofv3 --marker-trace --kernel-trace --output-format csv -d "$R/gpurun_out/prof_markers" -o run -- python3 "$R/bench.py" --steps 20 --warmup 5 --latency-samples 0 > "$R/gpurun_out/prof_markers.log" 2>&1 || { echo "marker trace failed"; tail -20 "$R/gpurun_out/prof_markers.log"; exit 1; }
+unset VEP_ROCTX
+find "$R/gpurun_out/prof" "$R/gpurun_out/prof_markers" -name "*.csv" | head
 echo "[gpu_check] done"

@@ -132,6 +132,16 @@ def cmd_proxy(a):
     print(ImageClient(_addr(a)).Proxy(pb.ProxyRequest(device_id=a.device, passthrough=_bool(a.on))))
 
 
+def cmd_bench(a, rest):
+    """``vep bench ...`` = the repo's bench.py (headline benchmark) with the same flags."""
+    import subprocess
+
+    bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+    if not os.path.exists(bench):
+        raise SystemExit("bench.py not found next to the package")
+    raise SystemExit(subprocess.call([sys.executable, bench, *rest]))
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser(prog="vep", description=__doc__,
                                  formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -191,7 +201,14 @@ def main(argv=None):
             p.add_argument("--on", required=True)
         p.set_defaults(fn=fn)
 
-    a = ap.parse_args(argv)
+    b = sub.add_parser("bench", help="run bench.py (flags passed through, e.g. --codec h265)")
+    b.set_defaults(fn=None)
+
+    a, rest = ap.parse_known_args(argv)
+    if a.cmd == "bench":
+        cmd_bench(a, rest)
+    if rest:
+        ap.error(f"unrecognized arguments: {' '.join(rest)}")
     a.fn(a)
 
 

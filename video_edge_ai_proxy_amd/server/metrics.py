@@ -8,7 +8,7 @@ from __future__ import annotations
 import statistics
 
 from prometheus_client import CONTENT_TYPE_LATEST, CollectorRegistry, generate_latest
-from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily
+from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, HistogramMetricFamily
 
 
 class HubCollector:
@@ -24,6 +24,8 @@ class HubCollector:
         byt = CounterMetricFamily("vep_ingest_bytes", "bitstream bytes received", labels=labels)
         run = GaugeMetricFamily("vep_camera_running", "ingest session connected", labels=labels)
         rst = CounterMetricFamily("vep_camera_restarts", "ingest reconnects", labels=labels)
+        lat = HistogramMetricFamily("vep_decode_latency_seconds",
+                                    "packet arrival -> decoded frame published", labels=labels)
         for name in list(self.hub.cameras):
             try:
                 st = self.hub.state(name)
@@ -36,7 +38,14 @@ class HubCollector:
             byt.add_metric(lv, st.get("bytes_in", 0))
             run.add_metric(lv, 1.0 if st.get("running") else 0.0)
             rst.add_metric(lv, st.get("restart_count", 0))
-        yield from (pk, dec, errs, byt, run, rst)
+            hist, bounds = st.get("latency_hist"), st.get("latency_bounds_ms")
+            if hist and bounds:
+                acc, buckets = 0, []
+                for b, c in zip(list(bounds) + [float("inf")], hist):
+                    acc += c
+                    buckets.append((str(b / 1000.0) if b != float("inf") else "+Inf", acc))
+                lat.add_metric(lv, buckets, st.get("latency_sum_ms", 0) / 1000.0)
+        yield from (pk, dec, errs, byt, run, rst, lat)
         wb = CounterMetricFamily("vep_worker_batches", "batched decode launches", labels=["device"])
         wf = CounterMetricFamily("vep_worker_frames", "frames decoded by the worker", labels=["device"])
         wg = CounterMetricFamily("vep_worker_gpu_ms", "GPU time of decode batches (ms)", labels=["device"])
@@ -45,6 +54,15 @@ class HubCollector:
             wf.add_metric([str(d)], w.frames)
             wg.add_metric([str(d)], w.gpu_ms_total)
         yield from (wb, wf, wg)
+        try:
+            from .._native import native
+
+            ps = native.pinned_pool_stats()
+            pool = GaugeMetricFamily("vep_pinned_pool_bytes", "pinned ingest pool reserved bytes")
+            pool.add_metric([], ps["bytes_reserved"])
+            yield pool
+        except Exception:  # noqa: BLE001 — metrics must never fail a scrape
+            pass
         if self.svc is not None:
             served = CounterMetricFamily("vep_grpc_frames_served", "VideoLatestImage frames sent")
             served.add_metric([], self.svc.frames_served)

@@ -126,7 +126,11 @@ def create_app(pm: ProcessManager, sm: SettingsManager, metrics=None) -> FastAPI
 
     @app.get("/healthz")
     def healthz():
-        return {"ok": True, "cameras": len(pm.hub.cameras), "devices": pm.hub.devices}
+        from .._native import native
+
+        return {"ok": True, "cameras": len(pm.hub.cameras), "devices": pm.hub.devices,
+                "decoder_backend": "rocdecode" if native.rocdecode_available() else "native-subset",
+                "direct_host_reads": [bool(w.direct_reads) for w in pm.hub.workers]}
 
     @app.get("/metrics")
     def prom():
