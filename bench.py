@@ -48,6 +48,8 @@ def parse_args():
                     help="h265 = BASELINE config 5 codec (e.g. --width 3840 --height 2160)")
     ap.add_argument("--threads", type=int, default=12, help="host parse threads per rank")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
+    ap.add_argument("--cache-gops", type=int, default=1,
+                    help="distinct pre-encoded GOPs replayed per camera (working-set size)")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--consumer-format", choices=["nv12", "bgr"], default="nv12",
@@ -96,7 +98,7 @@ def main():
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
     cfg.codec = a.codec
     cfg.seed = 1 + rank * 100003
-    rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop, threads=a.threads,
+    rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam")
 
     # The native worker keeps two ticks in flight (tick t's frames are published while tick
