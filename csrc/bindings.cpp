@@ -4,6 +4,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "vep/avc_cavlc.h"
 #include "vep/bench_driver.h"
 #include "vep/cabac.h"
 #include "vep/codec.h"
@@ -63,21 +64,51 @@ static std::shared_ptr<Camera> cam_ref(Worker& w, int idx) {
 static Camera& cam_of(Worker& w, int idx) { return *cam_ref(w, idx); }
 
 // Stateful oracle: parse + CPU reconstruct a sequence of AUs, return the final BGR picture.
+// Streams inside the I_PCM / P_Skip subset take the fast-path parser; anything else switches to
+// the general H.264 decoder (avc.h) for good, like a Camera does.
 struct CpuDecoder {
   StreamParser parser;
   MbUpdate upd;
   HostSurface surf;
   PictureInfo last;
+  avc::Decoder avc;
+  std::vector<HostSurface> slots;
+  bool general = false;
+  int target = 0;
+  int coded = 0;
+  const HostSurface& out() const { return general ? slots[size_t(target)] : surf; }
   py::object decode(const AccessUnit& au) {
-    upd.clear_payload();  // `au` outlives this call: src pointers into it are safe
-    last = parser.parse(au, upd);
-    if (surf.coded_w != last.coded_width || surf.coded_h != last.coded_height)
-      surf.alloc(last.coded_width, last.coded_height);
-    cpu_apply_update(upd, surf);
-    py::array_t<uint8_t> out({last.height, last.width, 3});
-    cpu_nv12_to_bgr(surf, last.crop_left, last.crop_top, last.width, last.height,
-                    out.mutable_data());
-    return out;
+    {
+      py::gil_scoped_release nogil;
+      bool done = false;
+      if (!general) {
+        try {
+          upd.clear_payload();  // `au` outlives this call: src pointers into it are safe
+          last = parser.parse(au, upd);
+          if (surf.coded_w != last.coded_width || surf.coded_h != last.coded_height)
+            surf.alloc(last.coded_width, last.coded_height);
+          cpu_apply_update(upd, surf);
+          coded = upd.nslots;
+          done = true;
+        } catch (const UnsupportedStream&) {
+          if (au.codec != Codec::kH264) throw;
+          general = true;
+        }
+      }
+      if (!done) {
+        avc::PicturePtr pic = avc.parse(au);
+        if (slots.size() < size_t(pic->dpb_slots)) slots.resize(size_t(pic->dpb_slots));
+        for (auto& h : slots)
+          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16) h.alloc(pic->wmbs * 16, pic->hmbs * 16);
+        avc::cpu_reconstruct(*pic, slots);
+        last = pic->info;
+        target = pic->target;
+        coded = pic->info.coded_mbs;
+      }
+    }
+    py::array_t<uint8_t> o({last.height, last.width, 3});
+    cpu_nv12_to_bgr(out(), last.crop_left, last.crop_top, last.width, last.height, o.mutable_data());
+    return o;
   }
 };
 
@@ -100,6 +131,12 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("zero_samples", &SynthConfig::zero_samples)
       .def_readwrite("idr_phase", &SynthConfig::idr_phase)
       .def_readwrite("merge_cands", &SynthConfig::merge_cands)
+      .def_readwrite("compressed", &SynthConfig::compressed)
+      .def_readwrite("qp", &SynthConfig::qp)
+      .def_readwrite("refs", &SynthConfig::refs)
+      .def_readwrite("objects", &SynthConfig::objects)
+      .def_readwrite("deblock_idc", &SynthConfig::deblock_idc)
+      .def_readwrite("coverage", &SynthConfig::coverage)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -174,15 +211,36 @@ PYBIND11_MODULE(_vep, m) {
       .def(py::init<>())
       .def("decode", &CpuDecoder::decode)
       .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
-      .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.upd.nslots; })
+      .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.coded; })
+      .def_property_readonly("general", [](const CpuDecoder& d) { return d.general; })
       .def("surface", [](const CpuDecoder& d) {
-        py::array_t<uint8_t> y({d.surf.coded_h, d.surf.coded_w});
-        py::array_t<uint8_t> uv({d.surf.coded_h / 2, d.surf.coded_w});
-        std::memcpy(y.mutable_data(), d.surf.y.data(), d.surf.y.size());
-        std::memcpy(uv.mutable_data(), d.surf.uv.data(), d.surf.uv.size());
+        const HostSurface& s = d.out();
+        py::array_t<uint8_t> y({s.coded_h, s.coded_w});
+        py::array_t<uint8_t> uv({s.coded_h / 2, s.coded_w});
+        std::memcpy(y.mutable_data(), s.y.data(), s.y.size());
+        std::memcpy(uv.mutable_data(), s.uv.data(), s.uv.size());
         return py::make_tuple(y, uv);
       });
 
+  m.def("cavlc_roundtrip", [](int nc, int max_coeff, const std::vector<int>& c) {
+    // write_residual_block -> read_residual_block (table self-consistency, tests only)
+    VEP_CHECK(int(c.size()) == max_coeff, "coefficient count mismatch");
+    BitWriter bw;
+    avc::write_residual_block(bw, nc, max_coeff, c.data());
+    bw.u1(1);
+    bw.align_zero();
+    avc::Bits br(bw.buf().data(), bw.buf().size());
+    std::vector<int> out(16, 0);
+    const int total = avc::read_residual_block(br, nc, max_coeff, out.data());
+    out.resize(size_t(max_coeff));
+    return py::make_tuple(out, total);
+  });
+  m.def("avc_source_luma", [](const SynthH264& s) {
+    const HostSurface& p = s.source();
+    py::array_t<uint8_t> y({p.coded_h, p.coded_w});
+    std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
+    return y;
+  });
   m.def("parse_sps", [](const std::string& nal) {
     std::vector<u8> r(nal.size());
     size_t n = ebsp_to_rbsp(reinterpret_cast<const u8*>(nal.data()), nal.size(), r.data());
@@ -382,6 +440,29 @@ PYBIND11_MODULE(_vep, m) {
              w.run_batch(v);
              return true;
            })
+      .def("decode_many",
+           [](Worker& w, const std::vector<std::pair<int, std::vector<std::shared_ptr<AccessUnit>>>>& work) {
+             // one batch: per camera all given AUs (merged into one job, GOP catch-up style)
+             std::vector<std::shared_ptr<Camera>> keep;
+             for (auto& [idx, aus] : work) keep.push_back(cam_ref(w, idx));
+             py::gil_scoped_release r;
+             std::vector<DecodeJob> jobs;
+             for (size_t k = 0; k < work.size(); ++k) {
+               DecodeJob merged;
+               bool have = false;
+               for (auto& au : work[k].second) {
+                 DecodeJob j;
+                 if (!keep[k]->make_job(au, j)) continue;
+                 if (!have) merged = std::move(j);
+                 else merge_job(merged, std::move(j));
+                 have = true;
+               }
+               if (have) jobs.push_back(std::move(merged));
+             }
+             const size_t n = jobs.size();
+             w.run_batch(jobs);
+             return n;
+           })
       .def("stats",
            [](Worker& w, int i) {
              Camera& c = cam_of(w, i);
@@ -392,6 +473,7 @@ PYBIND11_MODULE(_vep, m) {
              d["errors"] = c.errors.load();
              d["bytes_in"] = c.bytes_in.load();
              d["last_packet_ms"] = c.last_packet_ms.load();
+             d["decoder"] = c.general_decoder() ? "general" : "fast";
              auto ring = c.ring();
              d["published"] = ring ? ring->published() : 0;
              d["width"] = ring ? ring->width() : 0;

@@ -1,0 +1,1203 @@
+// General H.264 decoding path: slice headers, CAVLC macroblock layer, neighbour derivations,
+// DPB / reference lists and the CPU reference reconstruction. See avc.h for the CPU/GPU split.
+#include "avc.h"
+
+#include <algorithm>
+
+#include "avc_cavlc.h"
+
+namespace vep::avc {
+
+using h264::Pps;
+using h264::Sps;
+
+// ------------------------------------------------------------------------- MbNeighbours
+
+void MbNeighbours::reset(int wmbs, int hmbs) {
+  w_ = wmbs;
+  h_ = hmbs;
+  st_.assign(size_t(wmbs) * hmbs, MbState{});
+}
+
+int MbNeighbours::mb_at(int mb, int x, int y) const {
+  if (y >= 16) return -1;
+  const int dx = x < 0 ? -1 : (x >= 16 ? 1 : 0);
+  const int dy = y < 0 ? -1 : 0;
+  if (dx == 0 && dy == 0) return mb;
+  if (dx > 0 && dy == 0) return -1;  // right neighbour: later in decoding order
+  const int nx = mb % w_ + dx, ny = mb / w_ + dy;
+  if (nx < 0 || nx >= w_ || ny < 0) return -1;
+  const int nb = ny * w_ + nx;
+  return mb_available(mb, nb) ? nb : -1;
+}
+
+static int coded_count(const MbState& s, int blk) {
+  if (s.kind == kSkip) return 0;
+  if (s.kind == kIPcm) return 16;
+  return s.tc[blk];
+}
+
+int MbNeighbours::nc_luma(int mb, int blk) const {
+  const int bx = blk & 3, by = blk >> 2;
+  int na = -1, nb = -1;
+  const int am = mb_at(mb, bx * 4 - 1, by * 4);
+  if (am >= 0) na = coded_count(st_[size_t(am)], bx > 0 ? blk - 1 : blk + 3);
+  const int bm = mb_at(mb, bx * 4, by * 4 - 1);
+  if (bm >= 0) nb = coded_count(st_[size_t(bm)], by > 0 ? blk - 4 : blk + 12);
+  if (na >= 0 && nb >= 0) return (na + nb + 1) >> 1;
+  if (na >= 0) return na;
+  if (nb >= 0) return nb;
+  return 0;
+}
+
+int MbNeighbours::nc_chroma(int mb, int c, int blk) const {
+  const int bx = blk & 1, by = blk >> 1;
+  auto count = [&](int m, int b) {
+    const MbState& s = st_[size_t(m)];
+    if (s.kind == kSkip) return 0;
+    if (s.kind == kIPcm) return 16;
+    return int(s.tcc[c][b]);
+  };
+  int na = -1, nb = -1;
+  const int am = bx > 0 ? mb : mb_at(mb, -1, 0);
+  if (am >= 0) na = count(am, bx > 0 ? blk - 1 : blk + 1);
+  const int bm = by > 0 ? mb : mb_at(mb, 0, -1);
+  if (bm >= 0) nb = count(bm, by > 0 ? blk - 2 : blk + 2);
+  if (na >= 0 && nb >= 0) return (na + nb + 1) >> 1;
+  if (na >= 0) return na;
+  if (nb >= 0) return nb;
+  return 0;
+}
+
+int MbNeighbours::pred_intra4x4(int mb, int blk, bool constrained) const {
+  const int bx = blk & 3, by = blk >> 2;
+  const int am = mb_at(mb, bx * 4 - 1, by * 4), bm = mb_at(mb, bx * 4, by * 4 - 1);
+  if (am < 0 || bm < 0) return 2;
+  const MbState& a = st_[size_t(am)];
+  const MbState& b = st_[size_t(bm)];
+  if (constrained && (!is_intra(a.kind) || !is_intra(b.kind))) return 2;
+  const int ma = a.kind == kI4x4 ? a.i4[bx > 0 ? blk - 1 : blk + 3] : 2;
+  const int mbm = b.kind == kI4x4 ? b.i4[by > 0 ? blk - 4 : blk + 12] : 2;
+  return ma < mbm ? ma : mbm;
+}
+
+MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done) const {
+  Nb r{false, -1, {0, 0}};
+  const int m = mb_at(mb, x, y);
+  if (m < 0) return r;
+  const int blk = ((y & 15) >> 2) * 4 + ((x & 15) >> 2);
+  if (m == mb && !((done >> blk) & 1)) return r;  // partition not yet decoded
+  r.avail = true;
+  const MbState& s = st_[size_t(m)];
+  if (is_intra(s.kind)) return r;
+  r.ref = s.ref[((blk >> 3) << 1) | ((blk & 3) >> 1)];
+  r.mv[0] = s.mv[blk][0];
+  r.mv[1] = s.mv[blk][1];
+  return r;
+}
+
+static int median3(int a, int b, int c) { return a + b + c - std::min({a, b, c}) - std::max({a, b, c}); }
+
+void MbNeighbours::pred_mv(int mb, int x4, int y4, int w4, int h4, int ref, u16 done, int shape,
+                           int out[2]) const {
+  (void)h4;
+  const int x = x4 * 4, y = y4 * 4, w = w4 * 4;
+  Nb A = motion_at(mb, x - 1, y, done);
+  Nb B = motion_at(mb, x, y - 1, done);
+  Nb C = motion_at(mb, x + w, y - 1, done);
+  if (!C.avail) C = motion_at(mb, x - 1, y - 1, done);  // D replaces an unavailable C
+  auto take = [&](const Nb& n) {
+    out[0] = n.mv[0];
+    out[1] = n.mv[1];
+  };
+  if (shape == 1) {  // 16x8
+    if (y4 == 0 && B.ref == ref) return take(B);
+    if (y4 != 0 && A.ref == ref) return take(A);
+  } else if (shape == 2) {  // 8x16
+    if (x4 == 0 && A.ref == ref) return take(A);
+    if (x4 != 0 && C.ref == ref) return take(C);
+  }
+  if (!B.avail && !C.avail && A.avail) B = C = A;
+  const int match = (A.ref == ref) + (B.ref == ref) + (C.ref == ref);
+  if (match == 1) return take(A.ref == ref ? A : B.ref == ref ? B : C);
+  out[0] = median3(A.mv[0], B.mv[0], C.mv[0]);
+  out[1] = median3(A.mv[1], B.mv[1], C.mv[1]);
+}
+
+void MbNeighbours::pskip_mv(int mb, int out[2]) const {
+  out[0] = out[1] = 0;
+  if (mb_at(mb, -1, 0) < 0 || mb_at(mb, 0, -1) < 0) return;
+  const Nb A = motion_at(mb, -1, 0, 0), B = motion_at(mb, 0, -1, 0);
+  if ((A.ref == 0 && A.mv[0] == 0 && A.mv[1] == 0) || (B.ref == 0 && B.mv[0] == 0 && B.mv[1] == 0))
+    return;
+  pred_mv(mb, 0, 0, 4, 4, 0, 0, 0, out);
+}
+
+// ------------------------------------------------------------------------- parameter sets
+
+namespace {
+
+// Profile features outside the CAVLC 4:2:0 8-bit flat-scaling subset.
+void check_sps_supported(const u8* rbsp, size_t n, const Sps& s) {
+  if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
+    throw UnsupportedStream("only 8-bit 4:2:0 H.264 is supported");
+  if (!s.frame_mbs_only) throw UnsupportedStream("interlaced H.264 (field / MBAFF) is not supported");
+  switch (s.profile_idc) {
+    case 100: case 110: case 122: case 244: case 44: case 83: case 86: case 118: case 128:
+    case 138: case 139: case 134: case 135: {
+      Bits br(rbsp + 1, n - 1);
+      br.u(24);
+      br.ue();
+      const u32 cf = br.ue();
+      if (cf == 3) br.u1();
+      br.ue();
+      br.ue();
+      if (br.u1()) throw UnsupportedStream("lossless (transform bypass) H.264 is not supported");
+      if (br.u1()) throw UnsupportedStream("H.264 scaling matrices are not supported");
+      break;
+    }
+    default: break;
+  }
+}
+
+void check_pps_supported(const u8* rbsp, size_t n, const Pps& p) {
+  if (p.cabac) throw UnsupportedStream("CABAC H.264 (Main/High entropy coding) needs the VCN backend");
+  if (p.weighted_pred) throw UnsupportedStream("H.264 weighted prediction is not supported");
+  // Re-walk to the optional High-profile tail (transform_8x8_mode_flag, scaling matrix).
+  Bits br(rbsp + 1, n - 1);
+  br.ue();
+  br.ue();
+  br.u(2);
+  br.ue();
+  br.ue();
+  br.ue();
+  br.u(3);
+  br.se();
+  br.se();
+  br.se();
+  br.u(3);
+  size_t stop = BitReader(rbsp + 1, n - 1).stop_bit_pos();
+  if (br.pos() < stop) {
+    if (br.u1()) throw UnsupportedStream("H.264 8x8 transforms (High profile) are not supported");
+    if (br.u1()) throw UnsupportedStream("H.264 scaling matrices are not supported");
+  }
+}
+
+const u8* unescape(const u8* p, size_t n, std::vector<u32>& epb, std::vector<u8>& scratch,
+                   size_t& out_n, const u32* kb = nullptr, const u32* ke = nullptr) {
+  if (kb) epb.assign(kb, ke);
+  else find_epb(p, n, epb);
+  if (epb.empty()) {
+    out_n = n;
+    return p;
+  }
+  scratch.resize(n);
+  size_t o = 0, from = 0;
+  for (u32 e : epb) {
+    std::memcpy(scratch.data() + o, p + from, e - from);
+    o += e - from;
+    from = size_t(e) + 1;
+  }
+  std::memcpy(scratch.data() + o, p + from, n - from);
+  out_n = o + (n - from);
+  return scratch.data();
+}
+
+// Slice-level context of the macroblock walk.
+struct SliceCtx {
+  const SliceHdr& sh;
+  const Pps& pps;
+  int slice;
+  bool is_p;
+  int qp;
+  const std::vector<int>& list0;
+};
+
+void h16(int c[16]) {  // 4x4 Hadamard, in place: f = H c H
+  int t[16];
+  for (int i = 0; i < 4; ++i) {
+    const int a = c[i * 4], b = c[i * 4 + 1], d = c[i * 4 + 2], e = c[i * 4 + 3];
+    t[i * 4] = a + b + d + e;
+    t[i * 4 + 1] = a + b - d - e;
+    t[i * 4 + 2] = a - b - d + e;
+    t[i * 4 + 3] = a - b + d - e;
+  }
+  for (int j = 0; j < 4; ++j) {
+    const int a = t[j], b = t[4 + j], d = t[8 + j], e = t[12 + j];
+    c[j] = a + b + d + e;
+    c[4 + j] = a + b - d - e;
+    c[8 + j] = a - b - d + e;
+    c[12 + j] = a - b + d - e;
+  }
+}
+
+i16 sat16(int v) { return i16(v < -32768 ? -32768 : v > 32767 ? 32767 : v); }
+
+}  // namespace
+
+// ------------------------------------------------------------------------- slice header
+
+static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pps& pps) {
+  SliceHdr sh;
+  sh.nal_type = h264::nal_type(nal_hdr);
+  sh.nal_ref_idc = h264::nal_ref_idc(nal_hdr);
+  sh.first_mb = int(br.ue());
+  sh.slice_type = int(br.ue());
+  VEP_CHECK(sh.slice_type <= 9, "bad slice_type");
+  sh.pps_id = int(br.ue());
+  sh.frame_num = int(br.u(sps.log2_max_frame_num));
+  if (sh.idr()) sh.idr_pic_id = int(br.ue());
+  if (sps.poc_type == 0) {
+    sh.poc_lsb = int(br.u(sps.log2_max_poc_lsb));
+    if (pps.bottom_field_pic_order) br.se();
+  } else if (sps.poc_type == 1 && !sps.delta_pic_order_always_zero) {
+    br.se();
+    if (pps.bottom_field_pic_order) br.se();
+  }
+  if (pps.redundant_pic_cnt_present) {
+    if (br.ue() != 0) throw UnsupportedStream("redundant H.264 pictures are not supported");
+  }
+  const int st = sh.slice_type % 5;
+  if (st == h264::kB || st == h264::kSP || st == h264::kSI)
+    throw UnsupportedStream("H.264 B / SP / SI slices are not supported");
+  sh.num_ref_idx_l0 = pps.num_ref_idx_l0_default;
+  if (st == h264::kP) {
+    if (br.u1()) sh.num_ref_idx_l0 = int(br.ue()) + 1;
+    VEP_CHECK(sh.num_ref_idx_l0 <= 32, "num_ref_idx_l0 out of range");
+    if (br.u1()) {  // ref_pic_list_modification_flag_l0
+      for (;;) {
+        const int idc = int(br.ue());
+        if (idc == 3) break;
+        VEP_CHECK(idc <= 2, "bad modification_of_pic_nums_idc");
+        sh.ref_mods.push_back({idc, int(br.ue())});
+        VEP_CHECK(sh.ref_mods.size() <= 33, "too many reference list modifications");
+      }
+    }
+  }
+  if (sh.nal_ref_idc != 0) {
+    if (sh.idr()) {
+      sh.no_output_of_prior_pics = br.u1();
+      sh.long_term_reference = br.u1();
+    } else if ((sh.adaptive_marking = br.u1())) {
+      for (;;) {
+        const int op = int(br.ue());
+        if (op == 0) break;
+        VEP_CHECK(op <= 6, "bad memory_management_control_operation");
+        SliceHdr::Mmco m{op, 0, 0};
+        if (op == 1 || op == 3) m.a = int(br.ue());
+        if (op == 2) m.a = int(br.ue());
+        if (op == 3 || op == 6) (op == 3 ? m.b : m.a) = int(br.ue());
+        if (op == 4) m.a = int(br.ue());
+        sh.mmcos.push_back(m);
+        VEP_CHECK(sh.mmcos.size() <= 66, "too many MMCO operations");
+      }
+    }
+  }
+  sh.qp = pps.pic_init_qp + br.se();
+  VEP_CHECK(sh.qp >= 0 && sh.qp <= 51, "slice QP out of range");
+  if (pps.deblocking_filter_control) {
+    sh.disable_deblocking = int(br.ue());
+    VEP_CHECK(sh.disable_deblocking <= 2, "bad disable_deblocking_filter_idc");
+    if (sh.disable_deblocking != 1) {
+      sh.alpha_off = 2 * br.se();
+      sh.beta_off = 2 * br.se();
+      VEP_CHECK(sh.alpha_off >= -12 && sh.alpha_off <= 12 && sh.beta_off >= -12 && sh.beta_off <= 12,
+                "deblocking offsets out of range");
+    }
+  }
+  return sh;
+}
+
+// ------------------------------------------------------------------------- DPB
+
+void Decoder::reset_references() {
+  dpb_.clear();
+  have_idr_ = false;
+  max_lt_idx_ = -1;
+}
+
+int Decoder::pick_slot() const {
+  for (int s = 0; s < dpb_slots_; ++s) {
+    bool used = false;
+    for (const auto& r : dpb_) used |= r.slot == s;
+    if (!used) return s;
+  }
+  throw Error("vep: decoded picture buffer overflow");
+}
+
+void Decoder::build_ref_list(const SliceHdr& sh, const Sps& sps) {
+  const int max_fn = 1 << sps.log2_max_frame_num;
+  std::vector<RefPic*> st, lt;
+  for (auto& r : dpb_) {
+    if (r.long_term) {
+      lt.push_back(&r);
+    } else {
+      r.frame_num_wrap = r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num;
+      st.push_back(&r);
+    }
+  }
+  std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
+  std::sort(lt.begin(), lt.end(), [](RefPic* a, RefPic* b) { return a->lt_idx < b->lt_idx; });
+  std::vector<RefPic*> list = st;
+  list.insert(list.end(), lt.begin(), lt.end());
+  int pred = sh.frame_num;
+  size_t idx = 0;
+  for (const auto& m : sh.ref_mods) {
+    RefPic* pick = nullptr;
+    if (m.idc < 2) {
+      const int d = m.val + 1;
+      int nw = m.idc == 0 ? pred - d : pred + d;
+      if (nw < 0) nw += max_fn;
+      if (nw >= max_fn) nw -= max_fn;
+      pred = nw;
+      const int pic_num = nw > sh.frame_num ? nw - max_fn : nw;
+      for (RefPic* r : st)
+        if (r->frame_num_wrap == pic_num) pick = r;
+    } else {
+      for (RefPic* r : lt)
+        if (r->lt_idx == m.val) pick = r;
+    }
+    if (!pick) throw Error("vep: reference list modification names a missing picture");
+    list.insert(list.begin() + long(std::min(idx, list.size())), pick);
+    for (size_t k = idx + 1; k < list.size(); ++k)
+      if (list[k] == pick) {
+        list.erase(list.begin() + long(k));
+        break;
+      }
+    ++idx;
+  }
+  list0_.assign(size_t(sh.num_ref_idx_l0), -1);
+  for (size_t i = 0; i < list0_.size() && i < list.size(); ++i) list0_[i] = list[i]->slot;
+}
+
+void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot) {
+  const int max_fn = 1 << sps.log2_max_frame_num;
+  const int max_refs = std::max(1, sps.max_num_ref_frames);
+  if (sh.idr()) {
+    dpb_.clear();
+    RefPic r;
+    r.slot = slot;
+    r.frame_num = sh.frame_num;
+    if (sh.long_term_reference) {
+      r.long_term = true;
+      r.lt_idx = 0;
+      max_lt_idx_ = 0;
+    } else {
+      max_lt_idx_ = -1;
+    }
+    dpb_.push_back(r);
+    return;
+  }
+  auto wrap = [&](const RefPic& r) { return r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num; };
+  auto erase_if = [&](auto pred) { dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), pred), dpb_.end()); };
+  bool cur_long = false, mmco5 = false;
+  int cur_lt = 0;
+  if (sh.adaptive_marking) {
+    for (const auto& m : sh.mmcos) {
+      switch (m.op) {
+        case 1: {
+          const int pn = sh.frame_num - (m.a + 1);
+          erase_if([&](const RefPic& r) { return !r.long_term && wrap(r) == pn; });
+          break;
+        }
+        case 2:
+          erase_if([&](const RefPic& r) { return r.long_term && r.lt_idx == m.a; });
+          break;
+        case 3: {
+          const int pn = sh.frame_num - (m.a + 1);
+          erase_if([&](const RefPic& r) { return r.long_term && r.lt_idx == m.b; });
+          for (auto& r : dpb_)
+            if (!r.long_term && wrap(r) == pn) {
+              r.long_term = true;
+              r.lt_idx = m.b;
+            }
+          break;
+        }
+        case 4:
+          max_lt_idx_ = m.a - 1;
+          erase_if([&](const RefPic& r) { return r.long_term && r.lt_idx > max_lt_idx_; });
+          break;
+        case 5:
+          dpb_.clear();
+          max_lt_idx_ = -1;
+          mmco5 = true;
+          break;
+        case 6:
+          erase_if([&](const RefPic& r) { return r.long_term && r.lt_idx == m.a; });
+          cur_long = true;
+          cur_lt = m.a;
+          break;
+        default: break;
+      }
+    }
+  } else {
+    int n_short = 0;
+    for (const auto& r : dpb_) n_short += !r.long_term;
+    if (int(dpb_.size()) >= max_refs && n_short > 0) {  // sliding window
+      auto it = std::min_element(dpb_.begin(), dpb_.end(), [&](const RefPic& a, const RefPic& b) {
+        if (a.long_term != b.long_term) return !a.long_term;
+        return wrap(a) < wrap(b);
+      });
+      dpb_.erase(it);
+    }
+  }
+  RefPic r;
+  r.slot = slot;
+  r.frame_num = mmco5 ? 0 : sh.frame_num;
+  r.long_term = cur_long;
+  r.lt_idx = cur_lt;
+  dpb_.push_back(r);
+  while (int(dpb_.size()) > max_refs) {  // non-conforming stream: drop the oldest short-term
+    auto it = std::min_element(dpb_.begin(), dpb_.end(), [&](const RefPic& a, const RefPic& b) {
+      if (a.long_term != b.long_term) return !a.long_term;
+      return wrap(a) < wrap(b);
+    });
+    dpb_.erase(it);
+  }
+}
+
+// ------------------------------------------------------------------------- macroblock layer
+
+void Decoder::absorb_parameter_sets(const AccessUnit& au) {
+  std::vector<u8> scratch;
+  for (size_t i = 0; i < au.nals.size(); ++i) {
+    const u8* p = au.nal(i);
+    const size_t n = au.nal_size(i);
+    if (n < 2) continue;
+    const int t = h264::nal_type(p[0]);
+    if (t != h264::kNalSps && t != h264::kNalPps) continue;
+    size_t rn;
+    const u8* r = unescape(p, n, epb_, scratch, rn);
+    if (t == h264::kNalSps) {
+      Sps s = h264::parse_sps(r, rn);
+      sps_[s.sps_id] = s;
+    } else {
+      Pps q = h264::parse_pps(r, rn);
+      pps_[q.pps_id] = q;
+    }
+  }
+}
+
+namespace {
+
+class MbDecoder {
+ public:
+  MbDecoder(MbNeighbours& nb, Picture& pic, const SliceCtx& sc) : nb_(nb), pic_(pic), sc_(sc) {}
+
+  void skip(int mb) {
+    MbState& s = nb_.at(mb);
+    s = MbState{};
+    s.kind = kSkip;
+    s.slice = u16(sc_.slice);
+    s.qp = u8(sc_.qp);
+    for (int k = 0; k < 4; ++k) s.ref[k] = 0;
+    int mv[2];
+    nb_.pskip_mv(mb, mv);
+    for (auto& v : s.mv) {
+      v[0] = i16(mv[0]);
+      v[1] = i16(mv[1]);
+    }
+    MbResidual res;
+    emit(mb, s, res, 0, 0);
+  }
+
+  void macroblock(Bits& br, int mb) {
+    const u32 mbt = br.ue();
+    int it = -1;  // I-slice mb_type of an intra MB
+    if (sc_.is_p) {
+      VEP_CHECK(mbt <= 30, "bad P mb_type");
+      if (mbt >= 5) it = int(mbt) - 5;
+    } else {
+      VEP_CHECK(mbt <= 25, "bad I mb_type");
+      it = int(mbt);
+    }
+    MbState& s = nb_.at(mb);
+    s = MbState{};
+    s.slice = u16(sc_.slice);
+    MbResidual res;
+    if (it == 25) {  // I_PCM
+      s.kind = kIPcm;
+      std::fill(std::begin(s.tc), std::end(s.tc), u8(16));
+      for (auto& c : s.tcc) std::fill(std::begin(c), std::end(c), u8(16));
+      s.qp = u8(sc_.qp);
+      br.align();
+      const size_t off = br.pos() >> 3;
+      VEP_CHECK(off + kPcmMbBytes <= br.size(), "truncated I_PCM macroblock");
+      pcm_ = br.data() + off;
+      br.skip(kPcmMbBytes * 8);
+      emit(mb, s, res, 0, 0);
+      pcm_ = nullptr;
+      return;
+    }
+    int cbp_luma = 0, cbp_chroma = 0, i16_mode = 0, chroma_mode = 0;
+    if (it == 0) {
+      s.kind = kI4x4;
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        const bool prev = br.u1();
+        const int rem = prev ? 0 : int(br.u(3));
+        const int pred = nb_.pred_intra4x4(mb, r, sc_.pps.constrained_intra_pred);
+        s.i4[r] = u8(prev ? pred : (rem < pred ? rem : rem + 1));
+      }
+      chroma_mode = int(br.ue());
+    } else if (it > 0) {
+      s.kind = kI16x16;
+      i16_mode = (it - 1) % 4;
+      cbp_chroma = ((it - 1) / 4) % 3;
+      cbp_luma = it >= 13 ? 15 : 0;
+      std::fill(std::begin(s.i4), std::end(s.i4), u8(2));
+      chroma_mode = int(br.ue());
+    } else {
+      s.kind = kInter;
+      inter_pred(br, mb, s, int(mbt));
+    }
+    VEP_CHECK(chroma_mode <= 3, "bad intra_chroma_pred_mode");
+    if (s.kind != kI16x16) {
+      const u32 me = br.ue();
+      VEP_CHECK(me < 48, "bad coded_block_pattern");
+      const int cbp = s.kind == kI4x4 ? kCbpIntra[me] : kCbpInter[me];
+      cbp_luma = cbp & 15;
+      cbp_chroma = cbp >> 4;
+    }
+    int qp = sc_.qp;
+    if (cbp_luma || cbp_chroma || s.kind == kI16x16) {
+      const int dqp = br.se();
+      VEP_CHECK(dqp >= -26 && dqp <= 25, "mb_qp_delta out of range");
+      qp = (qp + dqp + 52) % 52;
+      qp_out_ = qp;
+    }
+    s.qp = u8(qp);
+    residual(br, mb, s, res, cbp_luma, cbp_chroma, qp);
+    emit(mb, s, res, i16_mode, chroma_mode);
+  }
+
+  int qp_out_ = -1;  // updated QP_Y (the next MB's QP_Y,PRED), -1 = unchanged
+
+ private:
+  int read_ref(Bits& br) {
+    const int n = sc_.sh.num_ref_idx_l0;
+    int r = 0;
+    if (n == 2) r = int(br.u1() ^ 1u);
+    else if (n > 2) r = int(br.ue());
+    VEP_CHECK(r < n && sc_.list0[size_t(r)] >= 0, "ref_idx_l0 names a missing reference picture");
+    return r;
+  }
+
+  void set_part(MbState& s, int x4, int y4, int w4, int h4, const int mv[2]) {
+    for (int y = y4; y < y4 + h4; ++y)
+      for (int x = x4; x < x4 + w4; ++x) {
+        s.mv[y * 4 + x][0] = i16(mv[0]);
+        s.mv[y * 4 + x][1] = i16(mv[1]);
+      }
+  }
+  static u16 part_mask(int x4, int y4, int w4, int h4) {
+    u16 m = 0;
+    for (int y = y4; y < y4 + h4; ++y)
+      for (int x = x4; x < x4 + w4; ++x) m |= u16(1u << (y * 4 + x));
+    return m;
+  }
+
+  void inter_pred(Bits& br, int mb, MbState& s, int mbt) {
+    struct Part {
+      int x4, y4, w4, h4, ref, shape;
+      int mvd[2];
+    };
+    Part parts[16];
+    int np = 0;
+    if (mbt <= 2) {
+      const int n = mbt == 0 ? 1 : 2;
+      int refs[2] = {0, 0};
+      for (int i = 0; i < n; ++i) refs[i] = read_ref(br);
+      for (int i = 0; i < n; ++i) {
+        Part& p = parts[np++];
+        p.ref = refs[i];
+        p.mvd[0] = br.se();
+        p.mvd[1] = br.se();
+        if (mbt == 0) p.x4 = 0, p.y4 = 0, p.w4 = 4, p.h4 = 4, p.shape = 0;
+        else if (mbt == 1) p.x4 = 0, p.y4 = 2 * i, p.w4 = 4, p.h4 = 2, p.shape = 1;
+        else p.x4 = 2 * i, p.y4 = 0, p.w4 = 2, p.h4 = 4, p.shape = 2;
+      }
+      for (int i = 0; i < n; ++i) {
+        const Part& p = parts[i];
+        for (int y = p.y4 / 2; y < (p.y4 + p.h4) / 2; ++y)
+          for (int x = p.x4 / 2; x < (p.x4 + p.w4) / 2; ++x) s.ref[y * 2 + x] = i8(p.ref);
+      }
+    } else {
+      int sub[4], refs[4];
+      for (int& t : sub) {
+        t = int(br.ue());
+        VEP_CHECK(t <= 3, "bad P sub_mb_type");
+      }
+      for (int i = 0; i < 4; ++i) refs[i] = mbt == 4 ? 0 : read_ref(br);
+      for (int i = 0; i < 4; ++i) {
+        s.ref[i] = i8(refs[i]);
+        const int x8 = (i & 1) * 2, y8 = (i >> 1) * 2;
+        const int cnt = sub[i] == 0 ? 1 : sub[i] == 3 ? 4 : 2;
+        for (int j = 0; j < cnt; ++j) {
+          Part& p = parts[np++];
+          p.ref = refs[i];
+          p.shape = 0;
+          p.mvd[0] = br.se();
+          p.mvd[1] = br.se();
+          switch (sub[i]) {
+            case 0: p.x4 = x8, p.y4 = y8, p.w4 = 2, p.h4 = 2; break;
+            case 1: p.x4 = x8, p.y4 = y8 + j, p.w4 = 2, p.h4 = 1; break;
+            case 2: p.x4 = x8 + j, p.y4 = y8, p.w4 = 1, p.h4 = 2; break;
+            default: p.x4 = x8 + (j & 1), p.y4 = y8 + (j >> 1), p.w4 = 1, p.h4 = 1; break;
+          }
+        }
+      }
+    }
+    u16 done = 0;
+    for (int i = 0; i < np; ++i) {
+      const Part& p = parts[i];
+      int mvp[2];
+      nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, p.ref, done, p.shape, mvp);
+      int mv[2] = {mvp[0] + p.mvd[0], mvp[1] + p.mvd[1]};
+      VEP_CHECK(mv[0] >= -32768 && mv[0] <= 32767 && mv[1] >= -32768 && mv[1] <= 32767,
+                "motion vector out of range");
+      set_part(s, p.x4, p.y4, p.w4, p.h4, mv);
+      done |= part_mask(p.x4, p.y4, p.w4, p.h4);
+    }
+  }
+
+  void residual(Bits& br, int mb, MbState& s, MbResidual& res, int cbp_luma, int cbp_chroma, int qp) {
+    MbLevels lv{};
+    if (s.kind == kI16x16) {
+      read_residual_block(br, nb_.nc_luma(mb, 0), 16, lv.dc);
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        if (cbp_luma) s.tc[r] = u8(read_residual_block(br, nb_.nc_luma(mb, r), 15, lv.luma[r] + 1));
+      }
+    } else {
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        if ((cbp_luma >> (idx >> 2)) & 1)
+          s.tc[r] = u8(read_residual_block(br, nb_.nc_luma(mb, r), 16, lv.luma[r]));
+      }
+    }
+    if (cbp_chroma) {
+      for (int c = 0; c < 2; ++c) {
+        int dc[16] = {};
+        read_residual_block(br, -1, 4, dc);
+        for (int k = 0; k < 4; ++k) lv.cdc[c][k] = dc[k];
+      }
+      if (cbp_chroma & 2)
+        for (int c = 0; c < 2; ++c)
+          for (int b = 0; b < 4; ++b)
+            s.tcc[c][b] = u8(read_residual_block(br, nb_.nc_chroma(mb, c, b), 15, lv.cac[c][b] + 1));
+    }
+    VEP_CHECK(!br.overrun(), "slice data overrun");
+    dequantize_mb(lv, s.kind == kI16x16, qp, chroma_qp(qp, sc_.pps.chroma_qp_index_offset), res);
+  }
+
+  void emit(int mb, const MbState& s, const MbResidual& res, int i16_mode, int chroma_mode) {
+    MbRec m{};
+    m.kind = s.kind;
+    m.qp = s.kind == kIPcm ? 0 : s.qp;
+    m.qpc = u8(chroma_qp(m.qp, sc_.pps.chroma_qp_index_offset));
+    m.i16_mode = u8(i16_mode);
+    m.chroma_mode = u8(chroma_mode);
+    m.dbk = u8((sc_.sh.disable_deblocking == 1 ? 1 : 0) | (sc_.sh.disable_deblocking == 2 ? 2 : 0));
+    m.alpha_off = i8(sc_.sh.alpha_off);
+    m.beta_off = i8(sc_.sh.beta_off);
+    m.slice = s.slice;
+    for (int k = 0; k < 4; ++k)
+      m.ref[k] = s.ref[k] >= 0 ? u8(sc_.list0[size_t(s.ref[k])]) : u8(0xFF);
+    for (int r = 0; r < 16; ++r) m.i4[r >> 1] |= u8((s.kind == kI4x4 ? s.i4[r] : 0) << ((r & 1) * 4));
+    store_mb(pic_, mb, m, s, &res, pcm_);
+  }
+
+  MbNeighbours& nb_;
+  Picture& pic_;
+  const SliceCtx& sc_;
+  const u8* pcm_ = nullptr;
+};
+
+}  // namespace
+
+PicturePtr Decoder::parse(const AccessUnit& au) {
+  auto pic = std::make_shared<Picture>();
+  bool got = false;
+  int slice_idx = 0;
+  SliceHdr first;
+  const Sps* act_sps = nullptr;
+  std::vector<u8> scratch;
+  for (size_t i = 0; i < au.nals.size(); ++i) {
+    const u8* p = au.nal(i);
+    const size_t n = au.nal_size(i);
+    if (n < 2) continue;
+    const int t = h264::nal_type(p[0]);
+    if (t == h264::kNalSps || t == h264::kNalPps) {
+      size_t rn;
+      const u8* r = unescape(p, n, epb_, scratch, rn);
+      if (t == h264::kNalSps) {
+        Sps s = h264::parse_sps(r, rn);
+        check_sps_supported(r, rn, s);
+        sps_[s.sps_id] = s;
+      } else {
+        Pps q = h264::parse_pps(r, rn);
+        check_pps_supported(r, rn, q);
+        pps_[q.pps_id] = q;
+      }
+      continue;
+    }
+    if (t >= 2 && t <= 4) throw UnsupportedStream("H.264 data partitioning is not supported");
+    if (t != h264::kNalSlice && t != h264::kNalIdr) continue;
+    size_t rn;
+    const u32 *kb = nullptr, *ke = nullptr;
+    au.epb_of(i, &kb, &ke);
+    const u8* r = unescape(p, n, epb_, rbsp_, rn, kb, ke);
+    Bits peek(r + 1, rn - 1);
+    peek.ue();
+    peek.ue();
+    const int pps_id = int(peek.ue());
+    auto pit = pps_.find(pps_id);
+    if (pit == pps_.end()) throw UnsupportedStream("slice references unknown PPS");
+    auto sit = sps_.find(pit->second.sps_id);
+    if (sit == sps_.end()) throw UnsupportedStream("slice references unknown SPS");
+    const Sps& sps = sit->second;
+    const Pps& pps = pit->second;
+    Bits br(r + 1, rn - 1);
+    const SliceHdr sh = read_slice_header(br, p[0], sps, pps);
+    if (!got) {
+      first = sh;
+      act_sps = &sps;
+      const int slots = std::max(1, sps.max_num_ref_frames) + 1;
+      VEP_CHECK(slots <= kMaxDpbSlots, "max_num_ref_frames out of range");
+      if (sh.idr()) {
+        dpb_.clear();
+        have_idr_ = true;
+        dpb_slots_ = slots;
+      } else {
+        if (!have_idr_) throw Error("vep: H.264 stream does not start with an IDR picture");
+        VEP_CHECK(slots == dpb_slots_, "SPS changed without an IDR picture");
+      }
+      const int W = sps.width_mbs, H = sps.height_mbs();
+      pic->wmbs = W;
+      pic->hmbs = H;
+      pic->mbs.assign(size_t(W) * H, MbRec{});
+      pic->coefs.reserve(size_t(W) * H * 16);
+      pic->dpb_slots = dpb_slots_;
+      pic->constrained_intra = pps.constrained_intra_pred;
+      pic->idr = sh.idr();
+      PictureInfo& pi = pic->info;
+      pi.coded_width = sps.coded_width();
+      pi.coded_height = sps.coded_height();
+      pi.width = sps.width();
+      pi.height = sps.height();
+      pi.crop_left = sps.crop_left;
+      pi.crop_top = sps.crop_top;
+      pi.pict_type = "PBISi"[sh.slice_type % 5];
+      pi.idr = sh.idr();
+      pi.frame_num = sh.frame_num;
+      pi.fps = sps.fps();
+      nb_.reset(W, H);
+      pic->target = pick_slot();
+      got = true;
+    } else {
+      VEP_CHECK(&sps == act_sps, "slices of one picture reference different SPSs");
+    }
+    if (sh.slice_type % 5 == h264::kP) build_ref_list(sh, sps);
+    else list0_.clear();
+    // skip the slice header bits already consumed: decode from the current position
+    const size_t stop = BitReader(r + 1, rn - 1).stop_bit_pos();
+    SliceCtx sc{sh, pps, slice_idx, sh.slice_type % 5 == h264::kP, sh.qp, list0_};
+    const int total = pic->nmbs();
+    int mb = sh.first_mb;
+    VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
+    bool more = true;
+    while (more) {
+      if (sc.is_p) {
+        const u32 run = br.ue();
+        VEP_CHECK(u32(total - mb) >= run, "mb_skip_run past end of picture");
+        MbDecoder d(nb_, *pic, sc);
+        for (u32 k = 0; k < run; ++k) d.skip(mb++);
+        if (run > 0) {
+          more = br.pos() < stop;
+          if (!more) break;
+        }
+      }
+      VEP_CHECK(mb < total, "macroblock address past end of picture");
+      MbDecoder d(nb_, *pic, sc);
+      d.macroblock(br, mb);
+      if (d.qp_out_ >= 0) sc.qp = d.qp_out_;
+      VEP_CHECK(!br.overrun(), "slice data overrun");
+      more = br.pos() < stop;
+      ++mb;
+    }
+    ++slice_idx;
+    VEP_CHECK(slice_idx < 65535, "too many slices");
+  }
+  VEP_CHECK(got, "access unit has no slice");
+  // conceal macroblocks no slice covered (lost slices): copy from the first reference, or grey
+  int missing = 0;
+  for (int mb = 0; mb < pic->nmbs(); ++mb) {
+    MbRec& m = pic->mbs[size_t(mb)];
+    if (nb_.at(mb).kind != 0xFF) continue;
+    ++missing;
+    m = MbRec{};
+    m.dbk = 1;
+    m.slice = u16(0xFFFF);
+    if (!dpb_.empty()) {
+      m.kind = kSkip;
+      for (auto& rf : m.ref) rf = u8(dpb_.front().slot);
+      m.mv = u32(pic->mvs.size() / 32);
+      pic->mvs.resize(pic->mvs.size() + 32, 0);
+      ++pic->inter_mbs;
+    } else {
+      m.kind = kI16x16;
+      m.i16_mode = 2;
+      std::fill(std::begin(m.ref), std::end(m.ref), u8(0xFF));
+      ++pic->intra_mbs;
+    }
+  }
+  pic->info.coded_mbs = pic->nmbs() - missing;
+  if (first.nal_ref_idc != 0) mark_references(first, *act_sps, pic->target);
+  return pic;
+}
+
+// ------------------------------------------------------------------------- shared internals
+
+void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& res) {
+  // (§8.5.6 - §8.5.12.1) scan-order levels -> dequantised raster 4x4 blocks
+  int dcy[16] = {};
+  if (i16x16) {
+    int c[16] = {};
+    for (int k = 0; k < 16; ++k) c[kZigzag4x4[k]] = lv.dc[k];
+    h16(c);
+    const int ls = 16 * kNormAdjust[qp % 6][0];
+    for (int k = 0; k < 16; ++k)
+      dcy[k] = qp >= 36 ? c[k] * ls * (1 << (qp / 6 - 6)) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+  }
+  res.luma = 0;
+  res.chroma = 0;
+  for (int r = 0; r < 16; ++r) {
+    i16* d = res.blk[r];
+    bool nz = false;
+    for (int k = 0; k < 16; ++k) {
+      const int pos = kZigzag4x4[k];
+      int v = 0;
+      if (k == 0 && i16x16) v = dcy[r];  // the DC matrix is spatial (row by, column bx)
+      else if (lv.luma[r][k]) v = dequant4x4(lv.luma[r][k], qp, pos >> 2, pos & 3);
+      d[pos] = sat16(v);
+      nz |= v != 0;
+    }
+    if (nz) res.luma |= u16(1u << r);
+  }
+  const int ls = 16 * kNormAdjust[qpc % 6][0];
+  for (int c = 0; c < 2; ++c) {
+    const int c0 = lv.cdc[c][0], c1 = lv.cdc[c][1], c2 = lv.cdc[c][2], c3 = lv.cdc[c][3];
+    const int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+    for (int b = 0; b < 4; ++b) {
+      i16* d = res.blk[16 + c * 4 + b];
+      bool nz = false;
+      for (int k = 0; k < 16; ++k) {
+        const int pos = kZigzag4x4[k];
+        int v = 0;
+        if (k == 0) v = ((f[b] * ls) * (1 << (qpc / 6))) >> 5;
+        else if (lv.cac[c][b][k]) v = dequant4x4(lv.cac[c][b][k], qpc, pos >> 2, pos & 3);
+        d[pos] = sat16(v);
+        nz |= v != 0;
+      }
+      if (nz) res.chroma |= u8(1u << (c * 4 + b));
+    }
+  }
+}
+
+void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm) {
+  m.nz = 0;
+  for (int r = 0; r < 16; ++r)
+    if (s.tc[r]) m.nz |= u16(1u << r);
+  m.coef = u32(pic.coefs.size() / 16);
+  m.luma_coded = 0;
+  m.chroma_coded = 0;
+  if (m.kind == kIPcm) {
+    VEP_CHECK(pcm, "I_PCM macroblock without samples");
+    const size_t o = pic.coefs.size();
+    pic.coefs.resize(o + kPcmMbBytes / 2);
+    std::memcpy(pic.coefs.data() + o, pcm, kPcmMbBytes);
+  } else if (res) {
+    m.luma_coded = res->luma;
+    m.chroma_coded = res->chroma;
+    for (int r = 0; r < 16; ++r)
+      if ((res->luma >> r) & 1) pic.coefs.insert(pic.coefs.end(), res->blk[r], res->blk[r] + 16);
+    for (int k = 0; k < 8; ++k)
+      if ((res->chroma >> k) & 1) pic.coefs.insert(pic.coefs.end(), res->blk[16 + k], res->blk[16 + k] + 16);
+  }
+  m.mv = 0;
+  if (m.kind == kSkip || m.kind == kInter) {
+    m.mv = u32(pic.mvs.size() / 32);
+    for (int b = 0; b < 16; ++b) {
+      pic.mvs.push_back(s.mv[b][0]);
+      pic.mvs.push_back(s.mv[b][1]);
+    }
+    ++pic.inter_mbs;
+  } else if (m.kind == kIPcm) {
+    ++pic.inter_mbs;  // no neighbour dependency: reconstructed in the parallel pass
+  } else {
+    ++pic.intra_mbs;
+  }
+  if (!(m.dbk & 1)) pic.deblock = true;
+  pic.mbs[size_t(mb)] = m;
+}
+
+// ------------------------------------------------------------------------- CPU reconstruction
+
+namespace {
+
+// Intra availability of MB (nx, ny) for the current MB m (§6.4.11 + constrained_intra_pred).
+bool intra_avail(const Picture& pic, const MbRec& m, int nx, int ny) {
+  if (nx < 0 || ny < 0 || nx >= pic.wmbs) return false;
+  const MbRec& n = pic.mbs[size_t(ny) * pic.wmbs + nx];
+  if (n.slice != m.slice) return false;
+  return !(pic.constrained_intra && !is_intra(n.kind));
+}
+
+const i16* luma_res(const Picture& pic, const MbRec& m, int r) {
+  if (!((m.luma_coded >> r) & 1)) return nullptr;
+  return pic.block(m.coef + u32(__builtin_popcount(m.luma_coded & ((1u << r) - 1))));
+}
+
+const i16* chroma_res(const Picture& pic, const MbRec& m, int c, int b) {
+  const int k = c * 4 + b;
+  if (!((m.chroma_coded >> k) & 1)) return nullptr;
+  return pic.block(m.coef + u32(__builtin_popcount(m.luma_coded)) +
+                   u32(__builtin_popcount(m.chroma_coded & ((1u << k) - 1))));
+}
+
+struct Recon {
+  const Picture& pic;
+  std::vector<HostSurface>& slots;
+  HostSurface& T;
+  int pitch, wpx, hpx;
+
+  u8& Y(int x, int y) { return T.y[size_t(y) * pitch + x]; }
+  u8& C(int x, int y, int c) { return T.uv[size_t(y) * pitch + 2 * x + c]; }
+
+  void add_luma_block(const MbRec& m, int r, int x0, int y0, const int* pred) {
+    const i16* d = luma_res(pic, m, r);
+    int res[16] = {};
+    if (d) idct4x4(d, res);
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) Y(x0 + j, y0 + i) = u8(clip1(pred[i * 4 + j] + res[i * 4 + j]));
+  }
+
+  void chroma_store(const MbRec& m, int mx, int my, int c, const int* pred /*8x8*/) {
+    for (int b = 0; b < 4; ++b) {
+      const i16* d = chroma_res(pic, m, c, b);
+      int res[16] = {};
+      if (d) idct4x4(d, res);
+      const int bx = (b & 1) * 4, by = (b >> 1) * 4;
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+          C(mx * 8 + bx + j, my * 8 + by + i, c) = u8(clip1(pred[(by + i) * 8 + bx + j] + res[i * 4 + j]));
+    }
+  }
+
+  void inter(const MbRec& m, int mx, int my) {
+    const i16* mv = &pic.mvs[size_t(m.mv) * 32];
+    int pred[16];
+    for (int r = 0; r < 16; ++r) {
+      const int bx = r & 3, by = r >> 2;
+      const HostSurface& R = slots[m.ref[((by >> 1) << 1) | (bx >> 1)]];
+      const int mvx = mv[2 * r], mvy = mv[2 * r + 1];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+          pred[i * 4 + j] = luma_qpel(R.y.data(), pitch, wpx, hpx, mx * 16 + bx * 4 + j + (mvx >> 2),
+                                      my * 16 + by * 4 + i + (mvy >> 2), mvx & 3, mvy & 3);
+      add_luma_block(m, r, mx * 16 + bx * 4, my * 16 + by * 4, pred);
+    }
+    for (int c = 0; c < 2; ++c) {
+      int cp[64];
+      for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) {
+          const int r = (y >> 1) * 4 + (x >> 1);
+          const HostSurface& R = slots[m.ref[((r >> 3) << 1) | ((r & 3) >> 1)]];
+          const int mvx = mv[2 * r], mvy = mv[2 * r + 1];
+          cp[y * 8 + x] = chroma_epel(R.uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mvx >> 3),
+                                      my * 8 + y + (mvy >> 3), mvx & 7, mvy & 7);
+        }
+      chroma_store(m, mx, my, c, cp);
+    }
+  }
+
+  void pcm(const MbRec& m, int mx, int my) {
+    const u8* s = reinterpret_cast<const u8*>(pic.block(m.coef));
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = s[y * 16 + x];
+    for (int c = 0; c < 2; ++c)
+      for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) C(mx * 8 + x, my * 8 + y, c) = s[256 + c * 64 + y * 8 + x];
+  }
+
+  void intra_chroma(const MbRec& m, int mb, int mx, int my) {
+    for (int c = 0; c < 2; ++c) {
+      IntraChromaNb n;
+      chroma_neighbours(pic, mb, c, T, n);
+      const PredConst k = m.chroma_mode == 3 ? chroma_plane_const(n) : PredConst{0, 0, 0, 0};
+      int cp[64];
+      for (int y = 0; y < 8; ++y)
+        for (int x = 0; x < 8; ++x) cp[y * 8 + x] = chroma_pred(n, k, m.chroma_mode, x, y);
+      chroma_store(m, mx, my, c, cp);
+    }
+  }
+
+  void intra16(const MbRec& m, int mb, int mx, int my) {
+    Intra16Nb n;
+    intra16_neighbours(pic, mb, T, n);
+    const PredConst k = intra16x16_const(n, m.i16_mode);
+    int pred[16];
+    for (int r = 0; r < 16; ++r) {
+      const int bx = r & 3, by = r >> 2;
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) pred[i * 4 + j] = intra16x16_pred(n, k, m.i16_mode, bx * 4 + j, by * 4 + i);
+      add_luma_block(m, r, mx * 16 + bx * 4, my * 16 + by * 4, pred);
+    }
+  }
+
+  void intra4(const MbRec& m, int mb, int mx, int my) {
+    for (int idx = 0; idx < 16; ++idx) {
+      const int r = blk_to_raster(idx), bx = r & 3, by = r >> 2;
+      Intra4Nb n;
+      intra4x4_neighbours(pic, mb, idx, T, n);
+      const int mode = i4_mode(m, r);
+      int pred[16];
+      for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j) pred[i * 4 + j] = intra4x4_pred(n, mode, j, i);
+      add_luma_block(m, r, mx * 16 + bx * 4, my * 16 + by * 4, pred);
+    }
+  }
+};
+
+}  // namespace
+
+void intra4x4_neighbours(const Picture& pic, int mb, int idx, const HostSurface& T, Intra4Nb& n) {
+  const MbRec& m = pic.mbs[size_t(mb)];
+  const int mx = mb % pic.wmbs, my = mb / pic.wmbs, pitch = T.coded_w;
+  const bool A = intra_avail(pic, m, mx - 1, my), B = intra_avail(pic, m, mx, my - 1),
+             Cm = intra_avail(pic, m, mx + 1, my - 1), D = intra_avail(pic, m, mx - 1, my - 1);
+  const int r = blk_to_raster(idx), bx = r & 3, by = r >> 2;
+  const int x0 = mx * 16 + bx * 4, y0 = my * 16 + by * 4;
+  auto P = [&](int x, int y) { return int(T.y[size_t(y) * pitch + x]); };
+  n.has_top = by > 0 || B;
+  n.has_left = bx > 0 || A;
+  n.has_tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+  const bool tr = by == 0 ? (bx < 3 ? B : Cm) : (bx < 3 && raster_to_blk((by - 1) * 4 + bx + 1) < idx);
+  n.t[0] = n.has_tl ? P(x0 - 1, y0 - 1) : 128;
+  for (int k = 0; k < 4; ++k) {
+    n.t[1 + k] = n.has_top ? P(x0 + k, y0 - 1) : 128;
+    n.l[k] = n.has_left ? P(x0 - 1, y0 + k) : 128;
+  }
+  for (int k = 0; k < 4; ++k) n.t[5 + k] = tr ? P(x0 + 4 + k, y0 - 1) : n.t[4];
+}
+
+void intra16_neighbours(const Picture& pic, int mb, const HostSurface& T, Intra16Nb& n) {
+  const MbRec& m = pic.mbs[size_t(mb)];
+  const int mx = mb % pic.wmbs, my = mb / pic.wmbs, pitch = T.coded_w;
+  auto P = [&](int x, int y) { return int(T.y[size_t(y) * pitch + x]); };
+  n.has_left = intra_avail(pic, m, mx - 1, my);
+  n.has_top = intra_avail(pic, m, mx, my - 1);
+  n.has_tl = intra_avail(pic, m, mx - 1, my - 1);
+  n.top[0] = n.has_tl ? P(mx * 16 - 1, my * 16 - 1) : 128;
+  for (int k = 0; k < 16; ++k) {
+    n.top[k + 1] = n.has_top ? P(mx * 16 + k, my * 16 - 1) : 128;
+    n.left[k] = n.has_left ? P(mx * 16 - 1, my * 16 + k) : 128;
+  }
+}
+
+void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, IntraChromaNb& n) {
+  const MbRec& m = pic.mbs[size_t(mb)];
+  const int mx = mb % pic.wmbs, my = mb / pic.wmbs, pitch = T.coded_w;
+  auto P = [&](int x, int y) { return int(T.uv[size_t(y) * pitch + 2 * x + c]); };
+  n.has_left = intra_avail(pic, m, mx - 1, my);
+  n.has_top = intra_avail(pic, m, mx, my - 1);
+  n.has_tl = intra_avail(pic, m, mx - 1, my - 1);
+  n.top[0] = n.has_tl ? P(mx * 8 - 1, my * 8 - 1) : 128;
+  for (int k = 0; k < 8; ++k) {
+    n.top[k + 1] = n.has_top ? P(mx * 8 + k, my * 8 - 1) : 128;
+    n.left[k] = n.has_left ? P(mx * 8 - 1, my * 8 + k) : 128;
+  }
+}
+
+void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots) {
+  HostSurface& T = slots[size_t(pic.target)];
+  const int wpx = pic.wmbs * 16, hpx = pic.hmbs * 16;
+  Recon r{pic, slots, T, wpx, wpx, hpx};
+  const MbRec& m = pic.mbs[size_t(mb)];
+  const int mx = mb % pic.wmbs, my = mb / pic.wmbs;
+  switch (m.kind) {
+    case kSkip:
+    case kInter:
+      for (u8 s : m.ref)
+        VEP_CHECK(s < slots.size() && slots[s].coded_w == wpx && slots[s].coded_h == hpx,
+                  "missing reference surface");
+      r.inter(m, mx, my);
+      break;
+    case kIPcm: r.pcm(m, mx, my); break;
+    case kI16x16:
+      r.intra16(m, mb, mx, my);
+      r.intra_chroma(m, mb, mx, my);
+      break;
+    default:
+      r.intra4(m, mb, mx, my);
+      r.intra_chroma(m, mb, mx, my);
+      break;
+  }
+}
+
+void cpu_deblock(const Picture& pic, HostSurface& T) {
+  static const i16 kZeroMv[32] = {};
+  const int W = pic.wmbs, pitch = T.coded_w;
+  u8* Yp = T.y.data();
+  u8* UV = T.uv.data();
+  auto mvs = [&](const MbRec& r) { return is_intra(r.kind) ? kZeroMv : &pic.mvs[size_t(r.mv) * 32]; };
+  for (int mb = 0; mb < pic.nmbs(); ++mb) {
+    const MbRec& q = pic.mbs[size_t(mb)];
+    if (q.dbk & 1) continue;
+    const int mx = mb % W, my = mb / W;
+    const bool left = mx > 0 && !((q.dbk & 2) && pic.mbs[size_t(mb - 1)].slice != q.slice);
+    const bool top = my > 0 && !((q.dbk & 2) && pic.mbs[size_t(mb - W)].slice != q.slice);
+    const i16* mq = mvs(q);
+    for (int dir = 0; dir < 2; ++dir) {  // 0: vertical edges, 1: horizontal edges
+      for (int e = 0; e < 4; ++e) {
+        if (e == 0 && !(dir == 0 ? left : top)) continue;
+        const MbRec& p = e > 0 ? q : pic.mbs[size_t(dir == 0 ? mb - 1 : mb - W)];
+        const i16* mp = mvs(p);
+        const EdgeParams ep = edge_params(p.qp, q.qp, q.alpha_off, q.beta_off);
+        const EdgeParams epc = edge_params(p.qpc, q.qpc, q.alpha_off, q.beta_off);
+        int bs[16];
+        for (int k = 0; k < 16; ++k) {
+          const int bq = dir == 0 ? (k >> 2) * 4 + e : e * 4 + (k >> 2);
+          const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
+          bs[k] = boundary_strength(p, bp, mp + 2 * bp, q, bq, mq + 2 * bq, e == 0);
+        }
+        for (int k = 0; k < 16; ++k) {
+          if (!bs[k]) continue;
+          if (dir == 0) filter_line(Yp + size_t(my * 16 + k) * pitch + mx * 16 + 4 * e, 1, bs[k], ep, false);
+          else filter_line(Yp + size_t(my * 16 + 4 * e) * pitch + mx * 16 + k, long(pitch), bs[k], ep, false);
+        }
+        if (e & 1) continue;  // chroma edges at chroma sample 0 and 4 (luma edges 0 and 2)
+        for (int c = 0; c < 2; ++c)
+          for (int k = 0; k < 8; ++k) {
+            const int b = bs[2 * k];
+            if (!b) continue;
+            if (dir == 0)
+              filter_line(UV + size_t(my * 8 + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, b, epc, true);
+            else
+              filter_line(UV + size_t(my * 8 + 2 * e) * pitch + (mx * 8 + k) * 2 + c, long(pitch), b, epc, true);
+          }
+      }
+    }
+  }
+}
+
+void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots) {
+  VEP_CHECK(pic.target >= 0 && pic.target < int(slots.size()), "target slot out of range");
+  HostSurface& T = slots[size_t(pic.target)];
+  VEP_CHECK(T.coded_w == pic.wmbs * 16 && T.coded_h == pic.hmbs * 16, "surface size mismatch");
+  for (int mb = 0; mb < pic.nmbs(); ++mb) cpu_reconstruct_mb(pic, mb, slots);
+  if (pic.deblock) cpu_deblock(pic, T);
+}
+
+}  // namespace vep::avc

@@ -1,0 +1,237 @@
+// General H.264 decoding path: CAVLC macroblock layer of I and P slices (Baseline /
+// Constrained Baseline / CAVLC Main without B slices), reference picture management, the CPU
+// reference reconstruction and a closed-loop synthetic encoder that emits the same syntax.
+//
+// Split of work (MI355X-first):
+//  * CPU (`Decoder::parse`): the inherently serial entropy layer — slice headers, mb_type,
+//    prediction modes, motion-vector prediction, CAVLC residual levels and dequantisation —
+//    into a compact per-picture record array (`Picture`: 40-byte MbRec per MB + a pool of
+//    dequantised 4x4 coefficient blocks + a motion-vector pool), and the DPB / reference-list
+//    bookkeeping (which GPU surface holds which reference picture).
+//  * GPU (gpu_avc.hip): everything that touches samples — motion compensation + residual for
+//    all inter MBs of all cameras in one launch, intra prediction in a row-ticketed wavefront,
+//    the deblocking filter in a second wavefront, then the NV12->BGR24 conversion.
+//  * `cpu_reconstruct` is the bit-exact CPU reference (and the CPU backend) built from the same
+//    primitives (avc_recon.h).
+//
+// Reference parity: this is the libavcodec h264 decoder the reference calls through PyAV
+// (python/read_image.py:87 `p.decode()`, :94 `to_ndarray('bgr24')`; SURVEY.md §2.2 N2 and
+// §2.3 K1). CABAC (Main/High profile entropy coding), B slices, interlace, 8x8 transforms,
+// weighted prediction and scaling matrices are reported as UnsupportedStream (the VCN
+// backend's job).
+#pragma once
+
+#include <map>
+#include <memory>
+
+#include "avc_recon.h"
+#include "codec.h"
+
+namespace vep::avc {
+
+constexpr int kMaxDpbSlots = 17;  // 16 references + the picture being decoded
+
+// One parsed picture, ready for reconstruction into DPB slot `target`.
+struct Picture {
+  int wmbs = 0, hmbs = 0;
+  std::vector<MbRec> mbs;     // raster order
+  std::vector<i16> coefs;     // 16-entry blocks (dequantised, row-major); I_PCM raw samples
+  std::vector<i16> mvs;       // 32 entries (16 x (mvx, mvy), quarter samples) per inter MB
+  int target = 0;             // DPB slot this picture is reconstructed into
+  int dpb_slots = 1;          // surfaces the camera needs for this stream
+  bool constrained_intra = false;
+  int intra_mbs = 0;          // I4x4 / I16x16 MBs (need the wavefront pass)
+  int inter_mbs = 0;          // skip / inter / I_PCM MBs (the parallel pass)
+  bool deblock = false;       // any MB with the loop filter enabled
+  bool idr = false;
+  PictureInfo info;
+
+  int nmbs() const { return wmbs * hmbs; }
+  const i16* block(u32 b) const { return coefs.data() + size_t(b) * 16; }
+};
+using PicturePtr = std::shared_ptr<const Picture>;
+
+// Full slice header (the fields reconstruction needs).
+struct SliceHdr {
+  int nal_type = 0, nal_ref_idc = 0;
+  int first_mb = 0, slice_type = 0, pps_id = 0, frame_num = 0, idr_pic_id = 0;
+  int poc_lsb = 0;
+  int num_ref_idx_l0 = 1;
+  struct RefMod {
+    int idc, val;
+  };
+  std::vector<RefMod> ref_mods;  // ref_pic_list_modification (list 0)
+  bool no_output_of_prior_pics = false, long_term_reference = false;
+  bool adaptive_marking = false;
+  struct Mmco {
+    int op, a, b;
+  };
+  std::vector<Mmco> mmcos;
+  int qp = 26;                   // SliceQP_Y
+  int disable_deblocking = 0, alpha_off = 0, beta_off = 0;  // offsets already doubled
+  bool idr() const { return nal_type == h264::kNalIdr; }
+};
+
+// Parse-time state of one MB of the current picture (neighbour derivations).
+struct MbState {
+  u8 kind = 0xFF;   // MbKind; 0xFF = not decoded in this picture
+  u16 slice = 0;
+  i8 ref[4] = {-1, -1, -1, -1};  // ref_idx_l0 per 8x8 (-1: intra)
+  i16 mv[16][2] = {};
+  u8 tc[16] = {};     // luma total_coeff (raster)
+  u8 tcc[2][4] = {};  // chroma AC total_coeff per component (raster 2x2)
+  u8 i4[16] = {};     // Intra4x4PredMode (raster)
+  u8 qp = 0;
+};
+
+// Neighbour derivations shared by the decoder and the encoder (§6.4.11, §8.3.1.1, §8.4.1.3,
+// §9.2.1): availability is "same slice and already decoded".
+class MbNeighbours {
+ public:
+  void reset(int wmbs, int hmbs);
+  MbState& at(int mb) { return st_[size_t(mb)]; }
+  const MbState& at(int mb) const { return st_[size_t(mb)]; }
+  int wmbs() const { return w_; }
+  int hmbs() const { return h_; }
+  // MB containing luma location (x, y) relative to MB `mb` (x, y may be -1 or >= 16); -1 if not
+  // available. For locations inside `mb` itself returns mb.
+  int mb_at(int mb, int x, int y) const;
+  bool mb_available(int mb, int nb) const {
+    return nb >= 0 && st_[size_t(nb)].kind != 0xFF && st_[size_t(nb)].slice == st_[size_t(mb)].slice;
+  }
+  // nC for luma block (raster) `blk` / chroma component c block `blk` (§9.2.1).
+  int nc_luma(int mb, int blk) const;
+  int nc_chroma(int mb, int c, int blk) const;
+  // predIntra4x4PredMode for raster block `blk`.
+  int pred_intra4x4(int mb, int blk, bool constrained_intra) const;
+  // Motion-vector predictor for partition (x, y, w, h) in 4x4 units with reference `ref`;
+  // `done` = 4x4 blocks of the current MB whose motion is already set; shape: 0 generic,
+  // 1 16x8, 2 8x16.
+  void pred_mv(int mb, int x4, int y4, int w4, int h4, int ref, u16 done, int shape, int out[2]) const;
+  void pskip_mv(int mb, int out[2]) const;
+
+ private:
+  struct Nb {
+    bool avail;
+    int ref;
+    int mv[2];
+  };
+  Nb motion_at(int mb, int x, int y, u16 done) const;  // x, y in luma samples rel. to mb
+  int w_ = 0, h_ = 0;
+  std::vector<MbState> st_;
+};
+
+// Reference picture (DPB entry).
+struct RefPic {
+  int slot = -1;
+  int frame_num = 0;
+  int frame_num_wrap = 0;
+  bool long_term = false;
+  int lt_idx = 0;
+};
+
+// Stateful decoder of one H.264 stream (parameter sets, DPB marking, neighbour state).
+class Decoder {
+ public:
+  // Parse one access unit into a Picture (decode order). Throws UnsupportedStream for syntax
+  // outside the supported profile subset and Error for corrupt data.
+  PicturePtr parse(const AccessUnit& au);
+  void absorb_parameter_sets(const AccessUnit& au);
+  bool has_sps() const { return !sps_.empty(); }
+  // Forget the DPB (e.g. after a failed picture): the next picture must be an IDR.
+  void reset_references();
+  int dpb_slots() const { return dpb_slots_; }
+
+ private:
+  void build_ref_list(const SliceHdr& sh, const h264::Sps& sps);
+  void mark_references(const SliceHdr& sh, const h264::Sps& sps, int slot);
+  int pick_slot() const;
+
+  std::map<int, h264::Sps> sps_;
+  std::map<int, h264::Pps> pps_;
+  std::vector<u8> rbsp_;
+  std::vector<u32> epb_;
+  MbNeighbours nb_;
+  std::vector<RefPic> dpb_;
+  std::vector<int> list0_;  // ref_idx -> DPB slot of the current slice
+  int max_lt_idx_ = -1;     // MaxLongTermFrameIdx ("no long-term frame indices" = -1)
+  int dpb_slots_ = 2;
+  bool have_idr_ = false;
+};
+
+// CPU reference reconstruction of `pic` into DPB surfaces `slots` (coded size; references are
+// read from the slots named by the MbRecs). Bit-exact with the GPU kernels.
+void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots);
+
+// ---- internals shared by the decoder and the encoder -------------------------------------
+// Levels of one MB in scan order (luma per raster block; I16x16 AC at index 1..15 with the DC
+// levels in `dc`; chroma AC at index 1..15).
+struct MbLevels {
+  int luma[16][16];
+  int dc[16];
+  int cdc[2][4];
+  int cac[2][4][16];
+};
+// Dequantised residual blocks of one MB (16 luma raster, 4 Cb, 4 Cr) and their coded masks.
+struct MbResidual {
+  i16 blk[24][16];
+  u16 luma = 0;
+  u8 chroma = 0;
+};
+void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& out);
+// Append MB `mb` to `pic`: coefficient blocks (or I_PCM samples), motion vectors and the
+// bookkeeping fields of `m` (coef, mv, coded masks, nz from s.tc); stores pic.mbs[mb] = m.
+void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm);
+void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots);
+void cpu_deblock(const Picture& pic, HostSurface& target);
+// Neighbour samples for intra prediction from the surface being reconstructed.
+void intra4x4_neighbours(const Picture& pic, int mb, int idx, const HostSurface& T, Intra4Nb& n);
+void intra16_neighbours(const Picture& pic, int mb, const HostSurface& T, Intra16Nb& n);
+void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, IntraChromaNb& n);
+
+// ------------------------------------------------------------------------------ encoder
+// Closed-loop synthetic H.264 encoder (CAVLC I/P): intra 16x16 / 4x4 and chroma prediction,
+// motion-compensated P macroblocks (16x16, 16x8, 8x16, 8x8 with sub-partitions, P_Skip),
+// multiple reference frames, residual coding and the deblocking filter — a real compressed
+// stream for the camera farm and for decoder coverage. The scene is a static textured
+// background with moving textured objects (known motion seeds the motion search).
+struct AvcEncConfig {
+  int width = 640, height = 480;
+  int fps = 30, gop = 30;
+  int idr_phase = 0;         // IDR when frame 0 or (frame + idr_phase) % gop == 0
+  int qp = 28;
+  int slices = 1;            // per picture (MB-row aligned)
+  int refs = 1;              // max_num_ref_frames
+  int objects = 3;
+  u64 seed = 1;
+  int deblock_idc = 0;       // disable_deblocking_filter_idc for every slice
+  int alpha_off = 0, beta_off = 0;  // slice_alpha_c0_offset_div2 / slice_beta_offset_div2
+  bool constrained_intra = false;
+  int chroma_qp_offset = 0;
+  bool coverage = false;     // randomised mode decisions: every MB type / partition / mode
+  int pcm_rate = 0;          // percent of I_PCM macroblocks in coverage mode
+  int nonref_rate = 0;       // percent of non-reference P pictures in coverage mode
+  double noise = 3.0;        // background texture amplitude
+};
+
+class AvcEncoder {
+ public:
+  explicit AvcEncoder(const AvcEncConfig& cfg);
+  ~AvcEncoder();
+  std::shared_ptr<AccessUnit> next();
+  // Encoder's own reconstruction of the last picture (what a conformant decoder must output).
+  const HostSurface& reconstruction() const;
+  // The source picture that was encoded (for PSNR).
+  const HostSurface& source() const;
+  const AvcEncConfig& config() const { return cfg_; }
+  // Escaped parameter-set NALs (what the muxers put in avcC / the FLV sequence header).
+  const std::vector<u8>& sps_nal() const;
+  const std::vector<u8>& pps_nal() const;
+
+ private:
+  struct Impl;
+  AvcEncConfig cfg_;
+  std::unique_ptr<Impl> p_;
+};
+
+}  // namespace vep::avc

@@ -1,0 +1,476 @@
+// H.264 reconstruction primitives shared by the CPU reference decoder, the synthetic encoder's
+// closed loop and the gfx950 reconstruction kernels (gpu_avc.hip): dequantisation tables, the
+// 4x4 inverse transform, intra prediction, quarter-sample motion compensation and the in-loop
+// deblocking filter (ITU-T H.264 §8.3, §8.4.2.2, §8.5, §8.7).
+//
+// Everything here is plain integer arithmetic with no state, compiled for both host and device,
+// so the GPU path is bit-exact with the CPU path by construction; the numerics tests still
+// compare the two on real bitstreams.
+//
+// Reference parity: replaces libavcodec's h264 reconstruction behind PyAV `packet.decode()`
+// (python/read_image.py:87; SURVEY.md §2.2 N2, §2.3 K1 idct4x4_dequant / intra_pred /
+// inter_mc_qpel / deblock_edge).
+#pragma once
+
+#include "common.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define VEP_HD __host__ __device__ inline
+#else
+#define VEP_HD inline
+#endif
+// Lookup tables live in constant memory in the device pass and in ordinary host memory in the
+// host pass (a __constant__ object's host shadow is not initialised).
+#if defined(__HIP_DEVICE_COMPILE__)
+#define VEP_CONST __constant__
+#else
+#define VEP_CONST
+#endif
+
+namespace vep::avc {
+
+using i16 = int16_t;
+using i8 = int8_t;
+
+// ------------------------------------------------------------------------------ MB records
+// One macroblock of a parsed picture, as shipped to the GPU (48 bytes).
+enum MbKind : u8 { kSkip = 0, kInter = 1, kI4x4 = 2, kI16x16 = 3, kIPcm = 4 };
+VEP_HD bool is_intra(u8 k) { return k >= kI4x4; }
+
+struct MbRec {
+  u8 kind;          // MbKind
+  u8 qp;            // QP_Y (0 for I_PCM)
+  u8 qpc;           // QP_C of QP_Y (chroma_qp_index_offset applied)
+  u8 i16_mode;      // Intra16x16PredMode
+  u8 chroma_mode;   // intra_chroma_pred_mode
+  u8 dbk;           // deblocking: bit0 filter disabled (idc 1), bit1 slice-edge mode (idc 2)
+  i8 alpha_off;     // FilterOffsetA
+  i8 beta_off;      // FilterOffsetB
+  u16 nz;           // luma 4x4 blocks (raster) with total_coeff != 0 (deblocking bS 2)
+  u16 luma_coded;   // luma 4x4 blocks (raster) with residual samples to add
+  u8 chroma_coded;  // bits 0-3 Cb, 4-7 Cr 4x4 blocks (raster) with residual
+  u8 pad0;
+  u16 slice;        // slice index within the picture (neighbour availability)
+  u8 ref[4];        // per 8x8 (raster): DPB slot of the reference picture (0xFF = none)
+  u32 coef;         // first 16-coefficient block in the picture's coefficient pool (I_PCM:
+                    // 384 raw sample bytes = 12 blocks)
+  u32 mv;           // first of 16 (x, y) motion vectors (raster 4x4) in the mv pool
+  u8 i4[8];         // Intra4x4PredMode per raster 4x4 block, 4 bits each (low nibble first)
+  u32 pad1;
+};
+static_assert(sizeof(MbRec) == 40, "MbRec layout");
+
+VEP_HD int i4_mode(const MbRec& m, int blk) { return (m.i4[blk >> 1] >> ((blk & 1) * 4)) & 15; }
+
+// Coding order of the 4x4 luma blocks (luma4x4BlkIdx) <-> raster position within the MB.
+VEP_HD int blk_to_raster(int idx) {
+  return ((idx >> 3) << 3) | (((idx >> 1) & 1) << 2) | (((idx >> 2) & 1) << 1) | (idx & 1);
+}
+VEP_HD int raster_to_blk(int r) {  // r = by*4 + bx
+  const int bx = r & 3, by = r >> 2;
+  return ((by >> 1) << 3) | ((bx >> 1) << 2) | ((by & 1) << 1) | (bx & 1);
+}
+
+// ------------------------------------------------------------------------------ tables
+// normAdjust4x4 (§8.5.9): v[m][0] even/even positions, [1] odd/odd, [2] mixed.
+VEP_CONST static const u8 kNormAdjust[6][3] = {
+    {10, 16, 13}, {11, 18, 14}, {13, 20, 16}, {14, 23, 18}, {16, 25, 20}, {18, 29, 23}};
+
+VEP_HD int norm_adjust(int m, int i, int j) {
+  const int cls = ((i & 1) == 0 && (j & 1) == 0) ? 0 : ((i & 1) && (j & 1)) ? 1 : 2;
+  return kNormAdjust[m][cls];
+}
+
+// QP_C as a function of qPI (Table 8-15), qPI in [0, 51].
+VEP_CONST static const u8 kChromaQp[52] = {
+    0,  1,  2,  3,  4,  5,  6,  7,  8,  9,  10, 11, 12, 13, 14, 15, 16, 17,
+    18, 19, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 29, 30, 31, 32, 32, 33,
+    34, 34, 35, 35, 36, 36, 37, 37, 37, 38, 38, 38, 39, 39, 39, 39};
+
+VEP_HD int chroma_qp(int qpy, int offset) {
+  int q = qpy + offset;
+  q = q < 0 ? 0 : q > 51 ? 51 : q;
+  return kChromaQp[q];
+}
+
+// Zig-zag scan (frame macroblocks): scan index -> raster position in the 4x4 block.
+VEP_CONST static const u8 kZigzag4x4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+
+// Deblocking thresholds (Table 8-16 / 8-17), indexed by indexA / indexB.
+VEP_CONST static const u8 kAlpha[52] = {
+    0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,   0,   0,   0,   0,   4,   4,
+    5,  6,  7,  8,  9,  10, 12, 13, 15, 17, 20, 22,  25,  28,  32,  36,  40,  45,
+    50, 56, 63, 71, 80, 90, 101, 113, 127, 144, 162, 182, 203, 226, 255, 255};
+VEP_CONST static const u8 kBeta[52] = {
+    0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0,  0,  0,  0,  2,  2,  2,  3,  3,  3,  3,  4,  4,  4,
+    6, 6, 7, 7, 8, 8, 9, 9, 10, 10, 11, 11, 12, 12, 13, 13, 14, 14, 15, 15, 16, 16, 17, 17, 18, 18};
+VEP_CONST static const u8 kTc0[52][3] = {
+    {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},    {0, 0, 0},    {0, 0, 0},
+    {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 0},    {0, 0, 0},    {0, 0, 0},
+    {0, 0, 0},   {0, 0, 0},   {0, 0, 0},   {0, 0, 1},   {0, 0, 1},    {0, 0, 1},    {0, 0, 1},
+    {0, 1, 1},   {0, 1, 1},   {1, 1, 1},   {1, 1, 1},   {1, 1, 1},    {1, 1, 1},    {1, 1, 2},
+    {1, 1, 2},   {1, 1, 2},   {1, 1, 2},   {1, 2, 3},   {1, 2, 3},    {2, 2, 3},    {2, 2, 4},
+    {2, 3, 4},   {2, 3, 4},   {3, 3, 5},   {3, 4, 6},   {3, 4, 6},    {4, 5, 7},    {4, 5, 8},
+    {4, 6, 9},   {5, 7, 10},  {6, 8, 11},  {6, 8, 13},  {7, 10, 14},  {8, 11, 16},  {9, 12, 18},
+    {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
+
+// ------------------------------------------------------------------------------ helpers
+VEP_HD int clip1(int x) { return x < 0 ? 0 : (x > 255 ? 255 : x); }
+VEP_HD int clip3(int lo, int hi, int x) { return x < lo ? lo : (x > hi ? hi : x); }
+VEP_HD int iabs(int x) { return x < 0 ? -x : x; }
+VEP_HD int imin(int a, int b) { return a < b ? a : b; }
+VEP_HD int imax(int a, int b) { return a > b ? a : b; }
+
+// ------------------------------------------------------------------------------ transform
+// Scale one parsed 4x4 coefficient level at raster position (i = row, j = column) (§8.5.12.1,
+// flat weight matrices: LevelScale4x4 = 16 * normAdjust4x4).
+VEP_HD int dequant4x4(int c, int qp, int i, int j) {
+  const int ls = 16 * norm_adjust(qp % 6, i, j);
+  if (qp >= 24) return c * ls * (1 << (qp / 6 - 4));
+  return (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+}
+
+// Inverse 4x4 transform (§8.5.12.2) of one block, d row-major (d[i*4+j]); r receives the
+// residual samples (h + 32) >> 6.
+VEP_HD void idct4x4(const i16* d, int* r) {
+  int f[16];
+  for (int i = 0; i < 4; ++i) {
+    const int d0 = d[i * 4], d1 = d[i * 4 + 1], d2 = d[i * 4 + 2], d3 = d[i * 4 + 3];
+    const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+    f[i * 4] = e0 + e3;
+    f[i * 4 + 1] = e1 + e2;
+    f[i * 4 + 2] = e1 - e2;
+    f[i * 4 + 3] = e0 - e3;
+  }
+  for (int j = 0; j < 4; ++j) {
+    const int f0 = f[j], f1 = f[4 + j], f2 = f[8 + j], f3 = f[12 + j];
+    const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
+    r[j] = (g0 + g3 + 32) >> 6;
+    r[4 + j] = (g1 + g2 + 32) >> 6;
+    r[8 + j] = (g1 - g2 + 32) >> 6;
+    r[12 + j] = (g0 - g3 + 32) >> 6;
+  }
+}
+
+// One residual sample (row i, column j) of the same transform: identical integer operations,
+// one output per GPU lane.
+VEP_HD int idct4x4_at(const i16* d, int i, int j) {
+  int f[4];
+  for (int k = 0; k < 4; ++k) {
+    const int d0 = d[k * 4], d1 = d[k * 4 + 1], d2 = d[k * 4 + 2], d3 = d[k * 4 + 3];
+    const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+    f[k] = j == 0 ? e0 + e3 : j == 1 ? e1 + e2 : j == 2 ? e1 - e2 : e0 - e3;
+  }
+  const int g0 = f[0] + f[2], g1 = f[0] - f[2], g2 = (f[1] >> 1) - f[3], g3 = f[1] + (f[3] >> 1);
+  const int h = i == 0 ? g0 + g3 : i == 1 ? g1 + g2 : i == 2 ? g1 - g2 : g0 - g3;
+  return (h + 32) >> 6;
+}
+
+// ------------------------------------------------------------------------------ intra 4x4
+// Neighbour samples of a 4x4 block: t[0] = p[-1,-1], t[1..8] = p[0..7,-1], l[0..3] = p[-1,0..3].
+// Unavailable top-right samples must already be substituted by p[3,-1] (§8.3.1.2).
+struct Intra4Nb {
+  int t[9];
+  int l[4];
+  bool has_top, has_left, has_tl;
+};
+
+VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y) {
+  auto T = [&](int xx) { return n.t[xx + 1]; };       // p[xx, -1], xx in -1..7
+  auto L = [&](int yy) { return yy < 0 ? n.t[0] : n.l[yy]; };  // p[-1, yy], yy in -1..3
+  switch (mode) {
+    case 0: return T(x);
+    case 1: return L(y);
+    case 2: {
+      int s = 0;
+      if (n.has_top && n.has_left) {
+        for (int k = 0; k < 4; ++k) s += T(k) + L(k);
+        return (s + 4) >> 3;
+      }
+      if (n.has_left) {
+        for (int k = 0; k < 4; ++k) s += L(k);
+        return (s + 2) >> 2;
+      }
+      if (n.has_top) {
+        for (int k = 0; k < 4; ++k) s += T(k);
+        return (s + 2) >> 2;
+      }
+      return 128;
+    }
+    case 3:
+      if (x == 3 && y == 3) return (T(6) + 3 * T(7) + 2) >> 2;
+      return (T(x + y) + 2 * T(x + y + 1) + T(x + y + 2) + 2) >> 2;
+    case 4:
+      if (x > y) return (T(x - y - 2) + 2 * T(x - y - 1) + T(x - y) + 2) >> 2;
+      if (x < y) return (L(y - x - 2) + 2 * L(y - x - 1) + L(y - x) + 2) >> 2;
+      return (T(0) + 2 * T(-1) + L(0) + 2) >> 2;
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0 && (z & 1) == 0) return (T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 1) >> 1;
+      if (z >= 0) return (T(x - (y >> 1) - 2) + 2 * T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 2) >> 2;
+      if (z == -1) return (L(0) + 2 * L(-1) + T(0) + 2) >> 2;
+      return (L(y - 1) + 2 * L(y - 2) + L(y - 3) + 2) >> 2;
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0 && (z & 1) == 0) return (L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 1) >> 1;
+      if (z >= 0) return (L(y - (x >> 1) - 2) + 2 * L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 2) >> 2;
+      if (z == -1) return (L(0) + 2 * L(-1) + T(0) + 2) >> 2;
+      return (T(x - 1) + 2 * T(x - 2) + T(x - 3) + 2) >> 2;
+    }
+    case 7:
+      if ((y & 1) == 0) return (T(x + (y >> 1)) + T(x + (y >> 1) + 1) + 1) >> 1;
+      return (T(x + (y >> 1)) + 2 * T(x + (y >> 1) + 1) + T(x + (y >> 1) + 2) + 2) >> 2;
+    default: {  // 8: Horizontal_Up
+      const int z = x + 2 * y;
+      if (z > 5) return L(3);
+      if (z == 5) return (L(2) + 3 * L(3) + 2) >> 2;
+      if ((z & 1) == 0) return (L(y + (x >> 1)) + L(y + (x >> 1) + 1) + 1) >> 1;
+      return (L(y + (x >> 1)) + 2 * L(y + (x >> 1) + 1) + L(y + (x >> 1) + 2) + 2) >> 2;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------ intra 16x16
+// top[0] = p[-1,-1], top[1..16] = p[0..15,-1]; left[0..15] = p[-1,0..15].
+struct Intra16Nb {
+  int top[17];
+  int left[16];
+  bool has_top, has_left, has_tl;
+};
+
+// Per-MB constants of a 16x16 / chroma prediction (DC value or plane a, b, c).
+struct PredConst {
+  int dc, a, b, c;
+};
+
+VEP_HD PredConst intra16x16_const(const Intra16Nb& n, int mode) {
+  PredConst k{128, 0, 0, 0};
+  if (mode == 2) {
+    int s = 0;
+    if (n.has_top && n.has_left) {
+      for (int i = 0; i < 16; ++i) s += n.top[i + 1] + n.left[i];
+      k.dc = (s + 16) >> 5;
+    } else if (n.has_left) {
+      for (int i = 0; i < 16; ++i) s += n.left[i];
+      k.dc = (s + 8) >> 4;
+    } else if (n.has_top) {
+      for (int i = 0; i < 16; ++i) s += n.top[i + 1];
+      k.dc = (s + 8) >> 4;
+    }
+  } else if (mode == 3) {
+    int H = 0, V = 0;
+    for (int i = 0; i < 8; ++i) {
+      H += (i + 1) * (n.top[8 + i + 1] - n.top[6 - i + 1]);
+      V += (i + 1) * (n.left[8 + i] - (6 - i >= 0 ? n.left[6 - i] : n.top[0]));
+    }
+    k.a = 16 * (n.left[15] + n.top[16]);
+    k.b = (5 * H + 32) >> 6;
+    k.c = (5 * V + 32) >> 6;
+  }
+  return k;
+}
+
+VEP_HD int intra16x16_pred(const Intra16Nb& n, const PredConst& k, int mode, int x, int y) {
+  switch (mode) {
+    case 0: return n.top[x + 1];
+    case 1: return n.left[y];
+    case 2: return k.dc;
+    default: return clip1((k.a + k.b * (x - 7) + k.c * (y - 7) + 16) >> 5);
+  }
+}
+
+// Chroma (4:2:0, 8x8 per component): top[0] = p[-1,-1], top[1..8]; left[0..7].
+struct IntraChromaNb {
+  int top[9];
+  int left[8];
+  bool has_top, has_left, has_tl;
+};
+
+// DC of chroma 4x4 block (bx, by) (§8.3.4.1-3).
+VEP_HD int chroma_dc(const IntraChromaNb& n, int bx, int by) {
+  int st = 0, sl = 0;
+  for (int i = 0; i < 4; ++i) {
+    st += n.top[1 + bx * 4 + i];
+    sl += n.left[by * 4 + i];
+  }
+  const bool corner_rule = (bx == 0 && by == 0) || (bx > 0 && by > 0);
+  if (corner_rule) {
+    if (n.has_top && n.has_left) return (st + sl + 4) >> 3;
+    if (n.has_left) return (sl + 2) >> 2;
+    if (n.has_top) return (st + 2) >> 2;
+    return 128;
+  }
+  if (bx > 0) {  // top-right block: top first
+    if (n.has_top) return (st + 2) >> 2;
+    if (n.has_left) return (sl + 2) >> 2;
+    return 128;
+  }
+  if (n.has_left) return (sl + 2) >> 2;  // bottom-left block: left first
+  if (n.has_top) return (st + 2) >> 2;
+  return 128;
+}
+
+VEP_HD PredConst chroma_plane_const(const IntraChromaNb& n) {
+  int H = 0, V = 0;
+  for (int i = 0; i < 4; ++i) {
+    H += (i + 1) * (n.top[4 + i + 1] - n.top[2 - i + 1]);
+    V += (i + 1) * (n.left[4 + i] - (2 - i >= 0 ? n.left[2 - i] : n.top[0]));
+  }
+  PredConst k{0, 16 * (n.left[7] + n.top[8]), (34 * H + 32) >> 6, (34 * V + 32) >> 6};
+  return k;
+}
+
+// mode: 0 DC, 1 horizontal, 2 vertical, 3 plane
+VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y) {
+  switch (mode) {
+    case 0: return chroma_dc(n, x >> 2, y >> 2);
+    case 1: return n.left[y];
+    case 2: return n.top[x + 1];
+    default: return clip1((k.a + k.b * (x - 3) + k.c * (y - 3) + 16) >> 5);
+  }
+}
+
+// ------------------------------------------------------------------------------ inter
+// Reference sample fetch with edge clamping (§8.4.2.2.1 Clip3 on xInt/yInt).
+VEP_HD int ref_px(const u8* p, int pitch, int w, int h, int x, int y) {
+  x = clip3(0, w - 1, x);
+  y = clip3(0, h - 1, y);
+  return p[size_t(y) * pitch + x];
+}
+
+VEP_HD int tap6(int a, int b, int c, int d, int e, int f) {
+  return a - 5 * b + 20 * c + 20 * d - 5 * e + f;
+}
+
+// Luma sample prediction at integer (xi, yi) with fractional offset (fx, fy) in quarter samples
+// (Table 8-12).
+VEP_HD int luma_qpel(const u8* p, int pitch, int w, int h, int xi, int yi, int fx, int fy) {
+  auto G = [&](int dx, int dy) { return ref_px(p, pitch, w, h, xi + dx, yi + dy); };
+  // unrounded half-sample intermediates
+  auto b1 = [&](int dy) {  // horizontal half sample between (0,dy) and (1,dy)
+    return tap6(G(-2, dy), G(-1, dy), G(0, dy), G(1, dy), G(2, dy), G(3, dy));
+  };
+  auto h1 = [&](int dx) {  // vertical half sample between (dx,0) and (dx,1)
+    return tap6(G(dx, -2), G(dx, -1), G(dx, 0), G(dx, 1), G(dx, 2), G(dx, 3));
+  };
+  auto rb = [&](int v) { return clip1((v + 16) >> 5); };
+  if (fx == 0 && fy == 0) return G(0, 0);
+  if (fy == 0) {
+    const int b = rb(b1(0));
+    if (fx == 2) return b;
+    return (b + G(fx == 1 ? 0 : 1, 0) + 1) >> 1;  // a / c
+  }
+  if (fx == 0) {
+    const int hh = rb(h1(0));
+    if (fy == 2) return hh;
+    return (hh + G(0, fy == 1 ? 0 : 1) + 1) >> 1;  // d / n
+  }
+  if (fx == 2 || fy == 2) {
+    // j from the vertical 6-tap over horizontal intermediates
+    const int j1 = tap6(b1(-2), b1(-1), b1(0), b1(1), b1(2), b1(3));
+    const int j = clip1((j1 + 512) >> 10);
+    if (fx == 2 && fy == 2) return j;
+    if (fx == 2) {  // f (fy 1) / q (fy 3): with b (row 0) or s (row 1)
+      const int o = rb(b1(fy == 1 ? 0 : 1));
+      return (o + j + 1) >> 1;
+    }
+    // i (fx 1) / k (fx 3): with h (column 0) or m (column 1)
+    const int o = rb(h1(fx == 1 ? 0 : 1));
+    return (o + j + 1) >> 1;
+  }
+  // diagonal quarter positions e, g, p, r: average of a horizontal and a vertical half sample
+  const int hb = rb(b1(fy == 1 ? 0 : 1));  // b (row 0) or s (row 1)
+  const int hv = rb(h1(fx == 1 ? 0 : 1));  // h (column 0) or m (column 1)
+  return (hb + hv + 1) >> 1;
+}
+
+// Chroma sample prediction (§8.4.2.2.2) at integer (xi, yi) with eighth-sample (fx, fy) in one
+// component of an interleaved NV12 plane (component c in {0, 1}); w, h in chroma samples.
+VEP_HD int chroma_epel(const u8* uv, int pitch, int w, int h, int c, int xi, int yi, int fx,
+                       int fy) {
+  auto S = [&](int x, int y) {
+    x = clip3(0, w - 1, x);
+    y = clip3(0, h - 1, y);
+    return int(uv[size_t(y) * pitch + 2 * x + c]);
+  };
+  const int A = S(xi, yi), B = S(xi + 1, yi), C = S(xi, yi + 1), D = S(xi + 1, yi + 1);
+  return ((8 - fx) * (8 - fy) * A + fx * (8 - fy) * B + (8 - fx) * fy * C + fx * fy * D + 32) >> 6;
+}
+
+// ------------------------------------------------------------------------------ deblocking
+// Boundary strength of the edge between 4x4 luma blocks P (in MB mp, raster block bp) and Q (in
+// MB mq, block bq) (§8.7.2.1, frame macroblocks, no 8x8 transform). mv_p / mv_q point at the
+// blocks' (x, y) motion vectors.
+VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
+                             const i16* mv_q, bool mb_edge) {
+  if (is_intra(mp.kind) || is_intra(mq.kind)) return mb_edge ? 4 : 3;
+  if (((mp.nz >> bp) & 1) || ((mq.nz >> bq) & 1)) return 2;
+  const int rp = mp.ref[((bp >> 3) << 1) | ((bp & 3) >> 1)];
+  const int rq = mq.ref[((bq >> 3) << 1) | ((bq & 3) >> 1)];
+  if (rp != rq) return 1;
+  if (iabs(mv_p[0] - mv_q[0]) >= 4 || iabs(mv_p[1] - mv_q[1]) >= 4) return 1;
+  return 0;
+}
+
+struct EdgeParams {
+  int alpha, beta, index_a;
+};
+
+VEP_HD EdgeParams edge_params(int qp_p, int qp_q, int off_a, int off_b) {
+  const int qav = (qp_p + qp_q + 1) >> 1;
+  const int ia = clip3(0, 51, qav + off_a), ib = clip3(0, 51, qav + off_b);
+  return EdgeParams{kAlpha[ia], kBeta[ib], ia};
+}
+
+// Filter one line of samples across an edge: s points at q0, `step` is the distance between
+// successive samples across the edge (1 for a vertical edge, pitch for a horizontal one).
+// chroma lines use the two-sample filters (§8.7.2.3 / §8.7.2.4).
+template <typename Px>
+VEP_HD void filter_line(Px* s, long step, int bs, const EdgeParams& e, bool chroma) {
+  const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
+  if (!(iabs(p0 - q0) < e.alpha && iabs(p1 - p0) < e.beta && iabs(q1 - q0) < e.beta)) return;
+  if (chroma) {
+    if (bs < 4) {
+      const int tc = kTc0[e.index_a][bs - 1] + 1;
+      const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+      s[-step] = Px(clip1(p0 + d));
+      s[0] = Px(clip1(q0 - d));
+    } else {
+      s[-step] = Px((2 * p1 + p0 + q1 + 2) >> 2);
+      s[0] = Px((2 * q1 + q0 + p1 + 2) >> 2);
+    }
+    return;
+  }
+  const int p2 = s[-3 * step], q2 = s[2 * step];
+  const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
+  if (bs < 4) {
+    const int tc0 = kTc0[e.index_a][bs - 1];
+    const int tc = tc0 + (ap < e.beta) + (aq < e.beta);
+    const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+    s[-step] = Px(clip1(p0 + d));
+    s[0] = Px(clip1(q0 - d));
+    if (ap < e.beta) s[-2 * step] = Px(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+    if (aq < e.beta) s[step] = Px(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+    return;
+  }
+  const int p3 = s[-4 * step], q3 = s[3 * step];
+  const bool strong = iabs(p0 - q0) < ((e.alpha >> 2) + 2);
+  if (ap < e.beta && strong) {
+    s[-step] = Px((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
+    s[-2 * step] = Px((p2 + p1 + p0 + q0 + 2) >> 2);
+    s[-3 * step] = Px((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+  } else {
+    s[-step] = Px((2 * p1 + p0 + q1 + 2) >> 2);
+  }
+  if (aq < e.beta && strong) {
+    s[0] = Px((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
+    s[step] = Px((p0 + q0 + q1 + q2 + 2) >> 2);
+    s[2 * step] = Px((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+  } else {
+    s[0] = Px((2 * q1 + q0 + p1 + 2) >> 2);
+  }
+}
+
+}  // namespace vep::avc

@@ -73,6 +73,31 @@ struct GatherChunk {
 constexpr u32 kGatherChunk = 32u << 10;
 void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s);
 
+// ---- general H.264 reconstruction (gpu_avc.hip; records from avc::Decoder, avc.h) ----------
+// One picture of a batched reconstruction round (device memory). DPB slot k of the camera
+// lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = wmbs * 16).
+struct AvcDesc {
+  const void* mbs;     // avc::MbRec[wmbs * hmbs]
+  const i16* coefs;    // dequantised 4x4 blocks (16 x i16) / I_PCM samples
+  const i16* mvs;      // 32 x i16 per inter MB
+  u8* y;
+  u8* uv;
+  u64 slot_y, slot_uv;
+  i32 wmbs, hmbs;
+  i32 target;          // DPB slot reconstructed into
+  i32 constrained;     // constrained_intra_pred_flag
+  i32 mb_begin;        // exclusive prefix of MBs over the round (inter kernel block -> picture)
+  i32 pad;
+  u32* err;            // pinned flag: wavefront timeout (frame dropped)
+};
+constexpr int kAvcMaxRows = 512;  // MB rows per picture the wavefront kernels support (8K)
+// Inter / skip / I_PCM macroblocks of every picture of the round: one 256-lane workgroup per MB.
+void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
+// Intra 4x4 / 16x16 macroblocks in a wavefront, then the deblocking filter in a wavefront: one
+// 1024-lane workgroup (16 wave64s) per picture, rows synchronised through LDS counters.
+void launch_avc_intra(const AvcDesc* d_descs, int n, hipStream_t s);
+void launch_avc_deblock(const AvcDesc* d_descs, int n, hipStream_t s);
+
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
 
 struct LetterboxDesc {

@@ -157,16 +157,38 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
   job.refresh = refresh;
   const AccessUnit* last = nullptr;
   try {
-    for (size_t i = from; i < to; ++i) {
-      // single-AU jobs may take the header-free I-slice walk: the worker verifies the skipped
-      // headers on the GPU (or CPU) before it publishes the frame
-      job.pic = parser_.parse(*gop_[i], job.upd, to - from == 1);
-      job.upd.keep.push_back(gop_[i]);  // MB samples are referenced in place
-      last = gop_[i].get();
+    if (!full_) {
+      try {
+        for (size_t i = from; i < to; ++i) {
+          // single-AU jobs may take the header-free I-slice walk: the worker verifies the
+          // skipped headers on the GPU (or CPU) before it publishes the frame
+          job.pic = parser_.parse(*gop_[i], job.upd, to - from == 1);
+          job.upd.keep.push_back(gop_[i]);  // MB samples are referenced in place
+          last = gop_[i].get();
+        }
+      } catch (const UnsupportedStream& e) {
+        if (gop_[from]->codec != Codec::kH264 || !gop_[0]->keyframe) throw;
+        // The stream uses H.264 syntax beyond the I_PCM / P_Skip fast path: switch this camera
+        // to the general decoder for good and rebuild the job from the GOP's keyframe (the
+        // general decoder needs the whole reference history of the GOP).
+        full_ = true;
+        logs.add(false, std::string("general H.264 decoder enabled (") + e.what() + ")");
+        job.upd = MbUpdate{};
+        from = 0;
+        job.refresh = true;
+      }
+    }
+    if (full_) {
+      for (size_t i = from; i < to; ++i) {
+        job.avc.push_back(avc_.parse(*gop_[i]));
+        last = gop_[i].get();
+      }
+      job.pic = job.avc.back()->info;
     }
   } catch (const std::exception& e) {
     errors.fetch_add(1);
     logs.add(true, std::string("failed to decode packet: ") + e.what());
+    if (full_) avc_.reset_references();
     decoded_upto_ = gop_.size();  // give up on this GOP; wait for the next keyframe
     return false;
   }
@@ -406,20 +428,30 @@ static void fold_update(MbUpdate& into, const MbUpdate& from) {
   into.frames += from.frames;
 }
 
+void merge_job(DecodeJob& p, DecodeJob&& job) {
+  VEP_CHECK(p.cam == job.cam, "merge_job: different cameras");
+  // collapse into the not-yet-launched job: latest writer wins per macroblock (fast path);
+  // general-path pictures are appended (each references the previous ones)
+  if (job.general() && p.general() && !job.refresh) {
+    p.avc.insert(p.avc.end(), job.avc.begin(), job.avc.end());
+    p.pic = job.pic;
+    p.meta = job.meta;
+  } else if (job.refresh || job.general() != p.general() || p.upd.width_mbs != job.upd.width_mbs ||
+             p.upd.height_mbs != job.upd.height_mbs) {
+    p = std::move(job);
+  } else {
+    fold_update(p.upd, job.upd);
+    p.pic = job.pic;
+    p.meta = job.meta;
+  }
+}
+
 void Worker::submit(DecodeJob&& job) {
   {
     std::lock_guard<std::mutex> g(q_mu_);
     for (auto& p : pending_) {
       if (p.cam != job.cam) continue;
-      // collapse into the not-yet-launched job: latest writer wins per macroblock
-      if (job.refresh || p.upd.width_mbs != job.upd.width_mbs ||
-          p.upd.height_mbs != job.upd.height_mbs) {
-        p = std::move(job);
-      } else {
-        fold_update(p.upd, job.upd);
-        p.pic = job.pic;
-        p.meta = job.meta;
-      }
+      merge_job(p, std::move(job));
       q_cv_.notify_one();
       return;
     }
@@ -480,25 +512,27 @@ void Worker::loop() {
   }
 }
 
-void Worker::ensure_surface(Camera& c, const PictureInfo& pi) {
+void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots) {
   const int wmbs = pi.coded_width / 16, hmbs = pi.coded_height / 16;
   auto& s = c.surface;
-  if (s.wmbs == wmbs && s.hmbs == hmbs && c.ring_ && c.ring_->width() == pi.width &&
-      c.ring_->height() == pi.height)
+  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && c.ring_ &&
+      c.ring_->width() == pi.width && c.ring_->height() == pi.height)
     return;
   dev_.free(s.y);
   dev_.free(s.uv);
   s.y = s.uv = nullptr;
   s.wmbs = wmbs;
   s.hmbs = hmbs;
-  const size_t ysz = size_t(wmbs) * 16 * hmbs * 16;
+  s.slots = std::max(1, slots);
+  const size_t ysz = s.slot_y() * size_t(s.slots);
   if (dev_.gpu()) {
     s.y = static_cast<u8*>(dev_.alloc(ysz));
     s.uv = static_cast<u8*>(dev_.alloc(ysz / 2));
     VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
     VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
   } else {
-    s.host.alloc(wmbs * 16, hmbs * 16);
+    s.host.assign(size_t(s.slots), HostSurface{});
+    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16);
   }
   c.set_ring(std::make_shared<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height));
 }
@@ -617,7 +651,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       const bool have = c.ring_ != nullptr;
       if (have && (c.surface.wmbs * 16 != j.pic.coded_width ||
                    c.surface.hmbs * 16 != j.pic.coded_height || c.ring_->width() != j.pic.width ||
-                   c.ring_->height() != j.pic.height))
+                   c.ring_->height() != j.pic.height || c.surface.slots < j.dpb_slots()))
         resize = true;
     }
   }
@@ -626,7 +660,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
   slots.resize(jobs.size());
   for (size_t i = 0; i < jobs.size(); ++i) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
-    ensure_surface(c, jobs[i].pic);
+    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots());
     slots[i] = c.ring_->begin_write();
   }
 }
@@ -722,6 +756,37 @@ void Worker::launch_gpu(Stage& st) {
     need += 2 * al(words_of(i) * sizeof(u32), 16) +
             al(size_t(jobs[size_t(i)].upd.nslots) * ent, 16);
   }
+  // General H.264 pictures: MB records, coefficient blocks and motion vectors of every picture,
+  // plus one AvcDesc array per reconstruction round (round r = r-th picture of each job).
+  struct AvcPic {
+    const avc::Picture* p;
+    int job;
+    size_t off_mbs, off_coef, off_mv;
+  };
+  std::vector<AvcPic> apics;
+  int rounds = 0;
+  for (int i = 0; i < n; ++i) rounds = std::max(rounds, int(jobs[size_t(i)].avc.size()));
+  std::vector<size_t> off_round(static_cast<size_t>(rounds));
+  std::vector<std::vector<int>> round_pics(static_cast<size_t>(rounds));
+  for (int r = 0; r < rounds; ++r) {
+    for (int i = 0; i < n; ++i) {
+      const auto& v = jobs[size_t(i)].avc;
+      if (int(v.size()) <= r) continue;
+      const avc::Picture& p = *v[size_t(r)];
+      VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows, "picture too tall for the wavefront kernels");
+      AvcPic a{&p, i, 0, 0, 0};
+      a.off_mbs = need;
+      need += al(p.mbs.size() * sizeof(avc::MbRec));
+      a.off_coef = need;
+      need += al(p.coefs.size() * sizeof(i16));
+      a.off_mv = need;
+      need += al(p.mvs.size() * sizeof(i16));
+      round_pics[size_t(r)].push_back(int(apics.size()));
+      apics.push_back(a);
+    }
+    off_round[size_t(r)] = need;
+    need += al(round_pics[size_t(r)].size() * sizeof(gpu::AvcDesc));
+  }
   need = al(need);
   const size_t header_bytes = need;
   for (int i = 0; i < n; ++i) {
@@ -759,6 +824,15 @@ void Worker::launch_gpu(Stage& st) {
     size_t len;
   };
   std::vector<CopyTask> tasks;
+  for (const AvcPic& a : apics) {
+    auto add = [&](const void* src, size_t len, size_t off) {
+      for (size_t o = 0; o < len; o += kPackChunk)
+        tasks.push_back({static_cast<const u8*>(src) + o, st.h + off + o, std::min(kPackChunk, len - o)});
+    };
+    add(a.p->mbs.data(), a.p->mbs.size() * sizeof(avc::MbRec), a.off_mbs);
+    add(a.p->coefs.data(), a.p->coefs.size() * sizeof(i16), a.off_coef);
+    add(a.p->mvs.data(), a.p->mvs.size() * sizeof(i16), a.off_mv);
+  }
   std::vector<std::vector<const u8*>> seg_dev(static_cast<size_t>(n));
   auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
   size_t ng = 0;
@@ -825,8 +899,9 @@ void Worker::launch_gpu(Stage& st) {
     Camera* c = cams_[size_t(j.cam)].get();
     const size_t words = size_t(j.upd.mbs() + 31) / 32;
     gpu::DecodeDesc& d = hd[i];
-    d.y = c->surface.y;
-    d.uv = c->surface.uv;
+    const size_t tgt = size_t(j.target());
+    d.y = c->surface.y + tgt * c->surface.slot_y();
+    d.uv = c->surface.uv + tgt * c->surface.slot_uv();
     d.bgr = c->ring_->slot_ptr(st.slots[size_t(i)]);
     (void)words;
     d.mask = mask_ptr(st.d, i);
@@ -840,8 +915,9 @@ void Worker::launch_gpu(Stage& st) {
       d.offsets = reinterpret_cast<const u32*>(table_ptr(st.d, i));
       d.payload = st.d + pay_off[size_t(i)];
     }
-    d.wmbs = j.upd.width_mbs;
-    d.hmbs = j.upd.height_mbs;
+    d.wmbs = j.general() ? j.pic.coded_width / 16 : j.upd.width_mbs;
+    d.hmbs = j.general() ? j.pic.coded_height / 16 : j.upd.height_mbs;
+    if (j.general()) d.mask = d.prefix = nullptr;  // pure conversion of the reconstructed slot
     d.out_w = j.pic.width;
     d.out_h = j.pic.height;
     d.crop_left = j.pic.crop_left;
@@ -856,8 +932,8 @@ void Worker::launch_gpu(Stage& st) {
     if (opt_.letterbox_size > 0) {
       gpu::LetterboxDesc& l = hl[i];
       const size_t S = size_t(opt_.letterbox_size);
-      l.y = c->surface.y;
-      l.uv = c->surface.uv;
+      l.y = d.y;
+      l.uv = d.uv;
       l.pitch = d.wmbs * 16;
       l.src_w = j.pic.width;
       l.src_h = j.pic.height;
@@ -872,6 +948,31 @@ void Worker::launch_gpu(Stage& st) {
       gpu::fill_letterbox_geometry(l, opt_.letterbox_size, opt_.letterbox_format == gpu::kLbNV12);
     }
   }
+  // AVC descriptors (device addresses known only now)
+  for (int r = 0; r < rounds; ++r) {
+    auto* ad = reinterpret_cast<gpu::AvcDesc*>(st.h + off_round[size_t(r)]);
+    int mbs = 0;
+    for (size_t k = 0; k < round_pics[size_t(r)].size(); ++k) {
+      const AvcPic& a = apics[size_t(round_pics[size_t(r)][k])];
+      const Camera* c = cams_[size_t(jobs[size_t(a.job)].cam)].get();
+      gpu::AvcDesc& g = ad[k];
+      g.mbs = st.d + a.off_mbs;
+      g.coefs = reinterpret_cast<const i16*>(st.d + a.off_coef);
+      g.mvs = reinterpret_cast<const i16*>(st.d + a.off_mv);
+      g.y = c->surface.y;
+      g.uv = c->surface.uv;
+      g.slot_y = c->surface.slot_y();
+      g.slot_uv = c->surface.slot_uv();
+      g.wmbs = a.p->wmbs;
+      g.hmbs = a.p->hmbs;
+      g.target = a.p->target;
+      g.constrained = a.p->constrained_intra ? 1 : 0;
+      g.mb_begin = mbs;
+      g.pad = 0;
+      g.err = const_cast<u32*>(st.err_dev) + a.job;
+      mbs += a.p->nmbs();
+    }
+  }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
   VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, copy_stream_));
@@ -881,6 +982,20 @@ void Worker::launch_gpu(Stage& st) {
   VEP_HIP(hipEventRecord(st.copied, copy_stream_));
   VEP_HIP(hipStreamWaitEvent(stream_, st.copied, 0));
   VEP_HIP(hipEventRecord(st.e0, stream_));
+  for (int r = 0; r < rounds; ++r) {
+    const auto* ad = reinterpret_cast<const gpu::AvcDesc*>(st.d + off_round[size_t(r)]);
+    const int np = int(round_pics[size_t(r)].size());
+    int mbs = 0;
+    bool intra = false, dbk = false;
+    for (int k : round_pics[size_t(r)]) {
+      mbs += apics[size_t(k)].p->nmbs();
+      intra |= apics[size_t(k)].p->intra_mbs > 0;
+      dbk |= apics[size_t(k)].p->deblock;
+    }
+    gpu::launch_avc_inter(ad, np, mbs, stream_);
+    if (intra) gpu::launch_avc_intra(ad, np, stream_);
+    if (dbk) gpu::launch_avc_deblock(ad, np, stream_);
+  }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), n, tiles,
                              stream_);
   if (opt_.letterbox_size > 0) {
@@ -911,8 +1026,13 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
       err[i] = (b[-2] != 0x0D || b[-1] != 0x00) ? 1u : 0u;
     }
     if (err[i]) continue;
-    cpu_apply_update(jobs[i].upd, c.surface.host);
-    cpu_nv12_to_bgr(c.surface.host, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
+    if (jobs[i].general()) {
+      for (const auto& pic : jobs[i].avc) avc::cpu_reconstruct(*pic, c.surface.host);
+    } else {
+      cpu_apply_update(jobs[i].upd, c.surface.host[0]);
+    }
+    const HostSurface& src = c.surface.host[size_t(jobs[i].target())];
+    cpu_nv12_to_bgr(src, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
                     jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
     if (opt_.letterbox_size > 0) {
       gpu::LetterboxDesc l{};
@@ -930,7 +1050,7 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
                       : nullptr;
       gpu::fill_letterbox_geometry(l, opt_.letterbox_size, nv12);
       if (nv12) {
-        cpu_letterbox_nv12(c.surface.host, l, opt_.letterbox_size, 114);
+        cpu_letterbox_nv12(src, l, opt_.letterbox_size, 114);
         continue;
       }
       gpu::LetterboxParams p{};
@@ -941,7 +1061,7 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
         p.inv_std[k] = 1.f / opt_.std[k];
       }
       p.pad_value = 114;
-      cpu_letterbox(c.surface.host, l, p);
+      cpu_letterbox(src, l, p);
     }
   }
 }

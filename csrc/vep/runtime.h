@@ -17,6 +17,7 @@
 #include <mutex>
 #include <thread>
 
+#include "avc.h"
 #include "codec.h"
 #include "gpu.h"
 #include "pool.h"
@@ -94,11 +95,18 @@ class FrameRing {
 
 struct DecodeJob {
   int cam = -1;
-  MbUpdate upd;
+  MbUpdate upd;                        // PCM / skip fast path (collapsible)
+  std::vector<avc::PicturePtr> avc;    // general H.264 path: pictures in decoding order
   PictureInfo pic;
   FrameMeta meta;
   bool refresh = false;  // IDR: every MB is covered
+  bool general() const { return !avc.empty(); }
+  int dpb_slots() const { return avc.empty() ? 1 : avc.back()->dpb_slots; }
+  int target() const { return avc.empty() ? 0 : avc.back()->target; }
 };
+
+// Fold `job` into the not-yet-launched job `p` of the same camera (GOP catch-up collapse).
+void merge_job(DecodeJob& p, DecodeJob&& job);
 
 class Worker;
 
@@ -148,15 +156,20 @@ class Camera {
   std::shared_ptr<FrameRing> ring() const { return std::atomic_load(&ring_); }
   void set_ring(std::shared_ptr<FrameRing> r) { std::atomic_store(&ring_, std::move(r)); }
   StreamParser& parser() { return parser_; }
+  // true once the stream left the I_PCM / P_Skip fast path (general H.264 decoder in use)
+  bool general_decoder() const { return full_; }
   std::mutex& gop_mutex() { return mu_; }
   std::vector<AuPtr> gop_snapshot();   // current GOP packets (for RTMP flush / archive)
 
   // worker-owned GPU state
   struct Surface {
     int wmbs = 0, hmbs = 0;
+    int slots = 1;                 // DPB surfaces (general H.264 path); slot k at y + k * bytes
     u8* y = nullptr;
     u8* uv = nullptr;
-    HostSurface host;  // CPU backend
+    size_t slot_y() const { return size_t(wmbs) * 16 * hmbs * 16; }
+    size_t slot_uv() const { return slot_y() / 2; }
+    std::vector<HostSurface> host;  // CPU backend: one per slot
   } surface;
   std::shared_ptr<FrameRing> ring_;  // written by the worker via set_ring(); read via ring()
   int ring_slots_cfg;
@@ -173,6 +186,8 @@ class Camera {
   bool broken_ = false;      // worker thread: a published frame failed its check; drop until IDR
   i64 keyframes_ = 0;
   StreamParser parser_;
+  avc::Decoder avc_;
+  bool full_ = false;
 };
 
 struct WorkerOptions {
@@ -249,7 +264,8 @@ class Worker {
     size_t err_cap = 0;
   };
   void loop();
-  void ensure_surface(Camera& c, const PictureInfo& pi);
+  void ensure_surface(Camera& c, const PictureInfo& pi, int slots);
+  void launch_avc(Stage& st, size_t& need, size_t off);
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
   void launch_gpu(Stage& st);
   void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err);

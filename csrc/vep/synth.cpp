@@ -70,6 +70,29 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
   bw_ = std::clamp(int(std::lround(std::sqrt(area * 4.0 / 3.0))), 1, wmbs_);
   bh_ = std::clamp(int(std::lround(area / bw_)), 1, hmbs_);
   if (cfg.motion <= 0) bw_ = bh_ = 0;
+  if (cfg.compressed) {
+    VEP_CHECK(cfg.codec == Codec::kH264, "compressed synthetic streams are H.264 only");
+    avc::AvcEncConfig ac;
+    ac.width = cfg.width;
+    ac.height = cfg.height;
+    ac.fps = cfg.fps;
+    ac.gop = cfg.gop;
+    ac.idr_phase = cfg.idr_phase;
+    ac.qp = cfg.qp;
+    ac.slices = cfg.slices;
+    ac.refs = cfg.refs;
+    ac.objects = cfg.objects;
+    ac.seed = cfg.seed;
+    ac.deblock_idc = cfg.deblock_idc;
+    ac.coverage = cfg.coverage;
+    if (cfg.coverage) {
+      ac.pcm_rate = 3;
+      ac.nonref_rate = 15;
+    }
+    avc_ = std::make_unique<avc::AvcEncoder>(ac);
+    sps_nal_ = avc_->sps_nal();
+    pps_nal_ = avc_->pps_nal();
+  }
 }
 
 u64 SynthH264::rnd() {
@@ -244,6 +267,11 @@ std::vector<u8> SynthH264::encode_slice_hevc(bool idr, int ctb0, int ctb1,
 
 std::shared_ptr<AccessUnit> SynthH264::next() {
   ++frame_;
+  if (avc_) {
+    auto au = avc_->next();
+    au->arrival_ms = now_ms();
+    return au;
+  }
   // frame 0 is always an IDR; later IDRs fall where (frame + phase) % gop == 0 so that a fleet
   // of cameras does not refresh in lock-step
   const bool idr = frame_ == 0 || ((frame_ + cfg_.idr_phase) % cfg_.gop) == 0;

@@ -8,6 +8,7 @@
 // (README.md:117-239).
 #pragma once
 
+#include "avc.h"
 #include "codec.h"
 
 namespace vep {
@@ -23,13 +24,25 @@ struct SynthConfig {
   int idr_phase = 0;       // GOP phase offset (IDR when (frame + phase) % gop == 0, and frame 0)
   Codec codec = Codec::kH264;
   int merge_cands = 1;     // HEVC MaxNumMergeCand (merge_idx coded when > 1)
+  // H.264 only: emit a real compressed stream (CAVLC intra/inter prediction + residual +
+  // deblocking, avc::AvcEncoder) instead of the I_PCM / P_Skip fast-path subset.
+  bool compressed = false;
+  int qp = 28;
+  int refs = 1;            // max_num_ref_frames
+  int objects = 3;         // moving textured objects in the compressed scene
+  int deblock_idc = 0;     // disable_deblocking_filter_idc
+  bool coverage = false;   // randomised mode decisions (decoder coverage streams)
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)
  public:
   explicit SynthH264(const SynthConfig& cfg);
   std::shared_ptr<AccessUnit> next();
-  const HostSurface& picture() const { return pic_; }  // ground truth of the last AU
+  // ground truth of the last AU (compressed streams: the encoder's reconstruction, i.e. what a
+  // conforming decoder outputs)
+  const HostSurface& picture() const { return avc_ ? avc_->reconstruction() : pic_; }
+  // the scene that was encoded (compressed streams: the encoder's source picture)
+  const HostSurface& source() const { return avc_ ? avc_->source() : pic_; }
   const std::vector<u8>& sps_nal() const { return sps_nal_; }
   const std::vector<u8>& pps_nal() const { return pps_nal_; }
   const std::vector<u8>& vps_nal() const { return vps_nal_; }  // H.265 only
@@ -61,6 +74,7 @@ class SynthH264 {  // (both codecs; the name predates H.265 support)
   int idr_id_ = 0, frame_num_ = 0;
   u64 state_;
   Rect prev_box_{0, 0, 0, 0};
+  std::unique_ptr<avc::AvcEncoder> avc_;  // compressed H.264 streams
 };
 
 }  // namespace vep

@@ -39,10 +39,13 @@ def native():
 
 
 def synth(native, w=640, h=480, gop=10, motion=0.05, seed=1, slices=1, zero=False, fps=30,
-          codec="h264", merge_cands=1):
+          codec="h264", merge_cands=1, compressed=False, coverage=False, refs=1, qp=28,
+          deblock_idc=0, objects=3):
     c = native.SynthConfig()
     c.width, c.height, c.gop, c.motion, c.seed, c.slices, c.fps = w, h, gop, motion, seed, slices, fps
     c.zero_samples = zero
     c.codec = codec
     c.merge_cands = merge_cands
+    c.compressed, c.coverage, c.refs, c.qp = compressed, coverage, refs, qp
+    c.deblock_idc, c.objects = deblock_idc, objects
     return native.SynthH264(c)
