@@ -137,6 +137,8 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("objects", &SynthConfig::objects)
       .def_readwrite("deblock_idc", &SynthConfig::deblock_idc)
       .def_readwrite("coverage", &SynthConfig::coverage)
+      .def_readwrite("noise", &SynthConfig::noise)
+      .def_readwrite("temporal_noise", &SynthConfig::temporal_noise)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -612,6 +614,8 @@ PYBIND11_MODULE(_vep, m) {
       .def("drain", &ReplayBench::drain, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("frames", &ReplayBench::frames)
       .def_property_readonly("payload_bytes", &ReplayBench::bitstream_bytes)
+      .def_property_readonly("stream_bytes", &ReplayBench::stream_bytes)
+      .def_property_readonly("stream_frames", &ReplayBench::stream_frames)
       .def_property_readonly("parse_ms", &ReplayBench::parse_ms)
       .def_property_readonly("batch_ms", &ReplayBench::batch_ms)
       .def_property_readonly("cameras", &ReplayBench::cameras);

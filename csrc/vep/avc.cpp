@@ -19,16 +19,35 @@ void MbNeighbours::reset(int wmbs, int hmbs) {
   st_.assign(size_t(wmbs) * hmbs, MbState{});
 }
 
+void MbNeighbours::begin(int mb) {
+  cur_ = mb;
+  const int mx = mb % w_, my = mb / w_;
+  auto nb = [&](int nx, int ny) {
+    if (nx < 0 || nx >= w_ || ny < 0) return -1;
+    const int n = ny * w_ + nx;
+    return mb_available(mb, n) ? n : -1;
+  };
+  a_ = nb(mx - 1, my);
+  b_ = nb(mx, my - 1);
+  c_ = nb(mx + 1, my - 1);
+  d_ = nb(mx - 1, my - 1);
+}
+
 int MbNeighbours::mb_at(int mb, int x, int y) const {
   if (y >= 16) return -1;
-  const int dx = x < 0 ? -1 : (x >= 16 ? 1 : 0);
-  const int dy = y < 0 ? -1 : 0;
-  if (dx == 0 && dy == 0) return mb;
-  if (dx > 0 && dy == 0) return -1;  // right neighbour: later in decoding order
-  const int nx = mb % w_ + dx, ny = mb / w_ + dy;
-  if (nx < 0 || nx >= w_ || ny < 0) return -1;
-  const int nb = ny * w_ + nx;
-  return mb_available(mb, nb) ? nb : -1;
+  if (mb != cur_) {  // slow path (not the MB announced by begin())
+    const int dx = x < 0 ? -1 : (x >= 16 ? 1 : 0);
+    const int dy = y < 0 ? -1 : 0;
+    if (dx == 0 && dy == 0) return mb;
+    if (dx > 0 && dy == 0) return -1;
+    const int nx = mb % w_ + dx, ny = mb / w_ + dy;
+    if (nx < 0 || nx >= w_ || ny < 0) return -1;
+    const int n = ny * w_ + nx;
+    return mb_available(mb, n) ? n : -1;
+  }
+  if (y < 0) return x < 0 ? d_ : (x < 16 ? b_ : c_);
+  if (x < 0) return a_;
+  return x < 16 ? mb : -1;  // right neighbour: later in decoding order
 }
 
 static int coded_count(const MbState& s, int blk) {
@@ -489,6 +508,7 @@ class MbDecoder {
     s = MbState{};
     s.kind = kSkip;
     s.slice = u16(sc_.slice);
+    nb_.begin(mb);
     s.qp = u8(sc_.qp);
     for (int k = 0; k < 4; ++k) s.ref[k] = 0;
     int mv[2];
@@ -514,6 +534,7 @@ class MbDecoder {
     MbState& s = nb_.at(mb);
     s = MbState{};
     s.slice = u16(sc_.slice);
+    nb_.begin(mb);
     MbResidual res;
     if (it == 25) {  // I_PCM
       s.kind = kIPcm;
@@ -662,30 +683,43 @@ class MbDecoder {
   }
 
   void residual(Bits& br, int mb, MbState& s, MbResidual& res, int cbp_luma, int cbp_chroma, int qp) {
-    MbLevels lv{};
+    MbLevels& lv = lv_;
+    lv.lmask = lv.cmask = lv.dcmask = 0;
     if (s.kind == kI16x16) {
-      read_residual_block(br, nb_.nc_luma(mb, 0), 16, lv.dc);
-      for (int idx = 0; idx < 16; ++idx) {
-        const int r = blk_to_raster(idx);
-        if (cbp_luma) s.tc[r] = u8(read_residual_block(br, nb_.nc_luma(mb, r), 15, lv.luma[r] + 1));
-      }
+      std::memset(lv.dc, 0, sizeof lv.dc);
+      if (read_residual_block(br, nb_.nc_luma(mb, 0), 16, lv.dc)) lv.dcmask |= 1;
+      if (cbp_luma)
+        for (int idx = 0; idx < 16; ++idx) {
+          const int r = blk_to_raster(idx);
+          std::memset(lv.luma[r], 0, sizeof lv.luma[r]);
+          const int tc = read_residual_block(br, nb_.nc_luma(mb, r), 15, lv.luma[r] + 1);
+          s.tc[r] = u8(tc);
+          if (tc) lv.lmask |= u16(1u << r);
+        }
     } else {
       for (int idx = 0; idx < 16; ++idx) {
+        if (!((cbp_luma >> (idx >> 2)) & 1)) continue;
         const int r = blk_to_raster(idx);
-        if ((cbp_luma >> (idx >> 2)) & 1)
-          s.tc[r] = u8(read_residual_block(br, nb_.nc_luma(mb, r), 16, lv.luma[r]));
+        std::memset(lv.luma[r], 0, sizeof lv.luma[r]);
+        const int tc = read_residual_block(br, nb_.nc_luma(mb, r), 16, lv.luma[r]);
+        s.tc[r] = u8(tc);
+        if (tc) lv.lmask |= u16(1u << r);
       }
     }
     if (cbp_chroma) {
       for (int c = 0; c < 2; ++c) {
         int dc[16] = {};
-        read_residual_block(br, -1, 4, dc);
+        if (read_residual_block(br, -1, 4, dc)) lv.dcmask |= u8(2 << c);
         for (int k = 0; k < 4; ++k) lv.cdc[c][k] = dc[k];
       }
       if (cbp_chroma & 2)
         for (int c = 0; c < 2; ++c)
-          for (int b = 0; b < 4; ++b)
-            s.tcc[c][b] = u8(read_residual_block(br, nb_.nc_chroma(mb, c, b), 15, lv.cac[c][b] + 1));
+          for (int b = 0; b < 4; ++b) {
+            std::memset(lv.cac[c][b], 0, sizeof lv.cac[c][b]);
+            const int tc = read_residual_block(br, nb_.nc_chroma(mb, c, b), 15, lv.cac[c][b] + 1);
+            s.tcc[c][b] = u8(tc);
+            if (tc) lv.cmask |= u8(1u << (c * 4 + b));
+          }
     }
     VEP_CHECK(!br.overrun(), "slice data overrun");
     dequantize_mb(lv, s.kind == kI16x16, qp, chroma_qp(qp, sc_.pps.chroma_qp_index_offset), res);
@@ -712,6 +746,7 @@ class MbDecoder {
   Picture& pic_;
   const SliceCtx& sc_;
   const u8* pcm_ = nullptr;
+  MbLevels lv_;
 };
 
 }  // namespace
@@ -777,7 +812,8 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
       pic->wmbs = W;
       pic->hmbs = H;
       pic->mbs.assign(size_t(W) * H, MbRec{});
-      pic->coefs.reserve(size_t(W) * H * 16);
+      pic->coefs.reserve(size_t(W) * H * 32);
+      pic->mvs.reserve(size_t(W) * H * 32);
       pic->dpb_slots = dpb_slots_;
       pic->constrained_intra = pps.constrained_intra_pred;
       pic->idr = sh.idr();
@@ -860,9 +896,13 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
 // ------------------------------------------------------------------------- shared internals
 
 void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& res) {
-  // (§8.5.6 - §8.5.12.1) scan-order levels -> dequantised raster 4x4 blocks
-  int dcy[16] = {};
-  if (i16x16) {
+  // (§8.5.6 - §8.5.12.1) scan-order levels -> dequantised raster 4x4 blocks; blocks without
+  // levels are skipped (their res.blk entries are left unwritten and masked out)
+  res.luma = 0;
+  res.chroma = 0;
+  int dcy[16];
+  const bool have_dc = i16x16 && (lv.dcmask & 1);
+  if (have_dc) {
     int c[16] = {};
     for (int k = 0; k < 16; ++k) c[kZigzag4x4[k]] = lv.dc[k];
     h16(c);
@@ -870,35 +910,59 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
     for (int k = 0; k < 16; ++k)
       dcy[k] = qp >= 36 ? c[k] * ls * (1 << (qp / 6 - 6)) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
   }
-  res.luma = 0;
-  res.chroma = 0;
+  const int q6 = qp / 6, qm = qp % 6;
   for (int r = 0; r < 16; ++r) {
+    const bool ac = (lv.lmask >> r) & 1;
+    const int dcv = have_dc ? dcy[r] : 0;
+    if (!ac && dcv == 0) continue;
     i16* d = res.blk[r];
-    bool nz = false;
-    for (int k = 0; k < 16; ++k) {
-      const int pos = kZigzag4x4[k];
-      int v = 0;
-      if (k == 0 && i16x16) v = dcy[r];  // the DC matrix is spatial (row by, column bx)
-      else if (lv.luma[r][k]) v = dequant4x4(lv.luma[r][k], qp, pos >> 2, pos & 3);
-      d[pos] = sat16(v);
-      nz |= v != 0;
+    std::memset(d, 0, 16 * sizeof(i16));
+    bool nz = dcv != 0;
+    d[0] = sat16(dcv);
+    if (ac) {
+      for (int k = i16x16 ? 1 : 0; k < 16; ++k) {
+        const int l = lv.luma[r][k];
+        if (!l) continue;
+        const int pos = kZigzag4x4[k];
+        const int v = dequant4x4(l, qp, pos >> 2, pos & 3);
+        d[pos] = sat16(v);
+        nz |= v != 0;
+      }
     }
     if (nz) res.luma |= u16(1u << r);
   }
+  (void)q6;
+  (void)qm;
   const int ls = 16 * kNormAdjust[qpc % 6][0];
   for (int c = 0; c < 2; ++c) {
-    const int c0 = lv.cdc[c][0], c1 = lv.cdc[c][1], c2 = lv.cdc[c][2], c3 = lv.cdc[c][3];
-    const int f[4] = {c0 + c1 + c2 + c3, c0 - c1 + c2 - c3, c0 + c1 - c2 - c3, c0 - c1 - c2 + c3};
+    const bool has_dc = (lv.dcmask >> (1 + c)) & 1;
+    const int acm = (lv.cmask >> (c * 4)) & 15;
+    if (!has_dc && !acm) continue;
+    int f[4] = {0, 0, 0, 0};
+    if (has_dc) {
+      const int c0 = lv.cdc[c][0], c1 = lv.cdc[c][1], c2 = lv.cdc[c][2], c3 = lv.cdc[c][3];
+      f[0] = c0 + c1 + c2 + c3;
+      f[1] = c0 - c1 + c2 - c3;
+      f[2] = c0 + c1 - c2 - c3;
+      f[3] = c0 - c1 - c2 + c3;
+    }
     for (int b = 0; b < 4; ++b) {
+      const int dcv = ((f[b] * ls) * (1 << (qpc / 6))) >> 5;
+      const bool ac = (acm >> b) & 1;
+      if (!ac && dcv == 0) continue;
       i16* d = res.blk[16 + c * 4 + b];
-      bool nz = false;
-      for (int k = 0; k < 16; ++k) {
-        const int pos = kZigzag4x4[k];
-        int v = 0;
-        if (k == 0) v = ((f[b] * ls) * (1 << (qpc / 6))) >> 5;
-        else if (lv.cac[c][b][k]) v = dequant4x4(lv.cac[c][b][k], qpc, pos >> 2, pos & 3);
-        d[pos] = sat16(v);
-        nz |= v != 0;
+      std::memset(d, 0, 16 * sizeof(i16));
+      d[0] = sat16(dcv);
+      bool nz = dcv != 0;
+      if (ac) {
+        for (int k = 1; k < 16; ++k) {
+          const int l = lv.cac[c][b][k];
+          if (!l) continue;
+          const int pos = kZigzag4x4[k];
+          const int v = dequant4x4(l, qpc, pos >> 2, pos & 3);
+          d[pos] = sat16(v);
+          nz |= v != 0;
+        }
       }
       if (nz) res.chroma |= u8(1u << (c * 4 + b));
     }
@@ -907,8 +971,7 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
 
 void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm) {
   m.nz = 0;
-  for (int r = 0; r < 16; ++r)
-    if (s.tc[r]) m.nz |= u16(1u << r);
+  for (int r = 0; r < 16; ++r) m.nz |= u16(s.tc[r] ? 1u << r : 0u);
   m.coef = u32(pic.coefs.size() / 16);
   m.luma_coded = 0;
   m.chroma_coded = 0;
@@ -917,21 +980,22 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
     const size_t o = pic.coefs.size();
     pic.coefs.resize(o + kPcmMbBytes / 2);
     std::memcpy(pic.coefs.data() + o, pcm, kPcmMbBytes);
-  } else if (res) {
+  } else if (res && (res->luma | res->chroma)) {
     m.luma_coded = res->luma;
     m.chroma_coded = res->chroma;
-    for (int r = 0; r < 16; ++r)
-      if ((res->luma >> r) & 1) pic.coefs.insert(pic.coefs.end(), res->blk[r], res->blk[r] + 16);
-    for (int k = 0; k < 8; ++k)
-      if ((res->chroma >> k) & 1) pic.coefs.insert(pic.coefs.end(), res->blk[16 + k], res->blk[16 + k] + 16);
+    const int nb = __builtin_popcount(res->luma) + __builtin_popcount(res->chroma);
+    size_t o = pic.coefs.size();
+    pic.coefs.resize(o + size_t(nb) * 16);
+    i16* dst = pic.coefs.data() + o;
+    for (u32 w = res->luma; w; w &= w - 1, dst += 16) std::memcpy(dst, res->blk[__builtin_ctz(w)], 32);
+    for (u32 w = res->chroma; w; w &= w - 1, dst += 16) std::memcpy(dst, res->blk[16 + __builtin_ctz(w)], 32);
   }
   m.mv = 0;
   if (m.kind == kSkip || m.kind == kInter) {
     m.mv = u32(pic.mvs.size() / 32);
-    for (int b = 0; b < 16; ++b) {
-      pic.mvs.push_back(s.mv[b][0]);
-      pic.mvs.push_back(s.mv[b][1]);
-    }
+    const size_t o = pic.mvs.size();
+    pic.mvs.resize(o + 32);
+    std::memcpy(pic.mvs.data() + o, s.mv, 64);
     ++pic.inter_mbs;
   } else if (m.kind == kIPcm) {
     ++pic.inter_mbs;  // no neighbour dependency: reconstructed in the parallel pass

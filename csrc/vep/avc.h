@@ -89,6 +89,9 @@ struct MbState {
 class MbNeighbours {
  public:
   void reset(int wmbs, int hmbs);
+  // Announce the MB being decoded (after its kind and slice are set): caches the A/B/C/D
+  // neighbour availability so the per-block derivations below need no division or lookup.
+  void begin(int mb);
   MbState& at(int mb) { return st_[size_t(mb)]; }
   const MbState& at(int mb) const { return st_[size_t(mb)]; }
   int wmbs() const { return w_; }
@@ -118,6 +121,7 @@ class MbNeighbours {
   };
   Nb motion_at(int mb, int x, int y, u16 done) const;  // x, y in luma samples rel. to mb
   int w_ = 0, h_ = 0;
+  int cur_ = -1, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
   std::vector<MbState> st_;
 };
 
@@ -166,11 +170,30 @@ void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots);
 // ---- internals shared by the decoder and the encoder -------------------------------------
 // Levels of one MB in scan order (luma per raster block; I16x16 AC at index 1..15 with the DC
 // levels in `dc`; chroma AC at index 1..15).
+// Only the blocks named by the masks are read (the decoder zeroes a block just before parsing
+// into it, so nothing else needs initialising); update_masks() derives them from the arrays.
 struct MbLevels {
   int luma[16][16];
   int dc[16];
   int cdc[2][4];
   int cac[2][4][16];
+  u16 lmask = 0;   // luma blocks (raster) with levels in `luma`
+  u8 cmask = 0;    // chroma AC blocks (c * 4 + b) with levels in `cac`
+  u8 dcmask = 0;   // bit 0: Intra16x16 DC levels; bits 1-2: chroma DC of Cb / Cr
+  void update_masks() {
+    lmask = cmask = dcmask = 0;
+    for (int r = 0; r < 16; ++r)
+      for (int k = 0; k < 16; ++k)
+        if (luma[r][k]) lmask |= u16(1u << r);
+    for (int k = 0; k < 16; ++k)
+      if (dc[k]) dcmask |= 1;
+    for (int c = 0; c < 2; ++c)
+      for (int b = 0; b < 4; ++b) {
+        if (cdc[c][b]) dcmask |= u8(2 << c);
+        for (int k = 0; k < 16; ++k)
+          if (cac[c][b][k]) cmask |= u8(1u << (c * 4 + b));
+      }
+  }
 };
 // Dequantised residual blocks of one MB (16 luma raster, 4 Cb, 4 Cr) and their coded masks.
 struct MbResidual {
@@ -212,6 +235,7 @@ struct AvcEncConfig {
   int pcm_rate = 0;          // percent of I_PCM macroblocks in coverage mode
   int nonref_rate = 0;       // percent of non-reference P pictures in coverage mode
   double noise = 3.0;        // background texture amplitude
+  double temporal_noise = 0; // per-frame sensor noise amplitude (drives P-picture residual bits)
 };
 
 class AvcEncoder {

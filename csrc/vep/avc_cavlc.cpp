@@ -127,10 +127,8 @@ struct Tables {
   }
 };
 
-const Tables& tables() {
-  static const Tables t;
-  return t;
-}
+const Tables kTables;  // built at load time: no guard check on the hot path
+inline const Tables& tables() { return kTables; }
 
 }  // namespace
 

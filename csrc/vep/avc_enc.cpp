@@ -223,6 +223,18 @@ struct AvcEncoder::Impl {
     }
   }
 
+  void add_sensor_noise() {
+    if (cfg.temporal_noise <= 0) return;
+    const u32 seed = u32(frame * 0x9E3779B1u) ^ u32(cfg.seed);
+    const int amp = int(cfg.temporal_noise * 2) + 1;
+    for (int y = 0; y < hpx; ++y)
+      for (int x = 0; x < wpx; ++x) {
+        u8& p = src.y[size_t(y) * wpx + x];
+        const int n = int(hash2(u32(x), u32(y), seed) % u32(amp)) - amp / 2;
+        p = u8(std::min(255, std::max(0, p + n)));
+      }
+  }
+
   void advance_scene() {
     for (Obj& o : objs) {
       o.x += o.vx;
@@ -413,7 +425,11 @@ struct AvcEncoder::Impl {
     m.qpc = u8(chroma_qp(m.qp, cfg.chroma_qp_offset));
     s.qp = u8(qp);
     MbResidual res;
-    if (lv) dequantize_mb(*lv, i16, qp, chroma_qp(qp, cfg.chroma_qp_offset), res);
+    if (lv) {
+      MbLevels l = *lv;
+      l.update_masks();
+      dequantize_mb(l, i16, qp, chroma_qp(qp, cfg.chroma_qp_offset), res);
+    }
     for (int r = 0; r < 16; ++r) m.i4[r >> 1] |= u8((m.kind == kI4x4 ? s.i4[r] : 0) << ((r & 1) * 4));
     store_mb(pic, mb, m, s, lv ? &res : nullptr, pcm);
     cpu_reconstruct_mb(pic, mb, slots);
@@ -832,6 +848,7 @@ struct AvcEncoder::Impl {
     ++frame;
     if (frame > 0) advance_scene();
     render();
+    add_sensor_noise();
     const bool idr = frame == 0 || (frame + cfg.idr_phase) % std::max(1, cfg.gop) == 0;
     gop_pos = idr ? 1 : gop_pos + 1;
     if (idr) {
@@ -906,6 +923,7 @@ struct AvcEncoder::Impl {
         MbState& s = nb.at(mb);
         s = MbState{};
         s.slice = u16(slice);
+        nb.begin(mb);
         if (!is_p) {
           if (cfg.coverage && rng.chance(cfg.pcm_rate)) encode_pcm(mb, s);
           else encode_intra(mb, s);

@@ -176,23 +176,25 @@ struct Intra4Nb {
   bool has_top, has_left, has_tl;
 };
 
-VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y) {
-  auto T = [&](int xx) { return n.t[xx + 1]; };       // p[xx, -1], xx in -1..7
-  auto L = [&](int yy) { return yy < 0 ? n.t[0] : n.l[yy]; };  // p[-1, yy], yy in -1..3
+// Generic form: T(xx) = p[xx, -1] for xx in -1..7 (top-right already substituted), L(yy) =
+// p[-1, yy] for yy in -1..3. The GPU passes LDS accessors, the CPU the Intra4Nb arrays; the
+// arithmetic is shared.
+template <class TF, class LF>
+VEP_HD int intra4x4_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, int x, int y) {
   switch (mode) {
     case 0: return T(x);
     case 1: return L(y);
     case 2: {
       int s = 0;
-      if (n.has_top && n.has_left) {
+      if (has_top && has_left) {
         for (int k = 0; k < 4; ++k) s += T(k) + L(k);
         return (s + 4) >> 3;
       }
-      if (n.has_left) {
+      if (has_left) {
         for (int k = 0; k < 4; ++k) s += L(k);
         return (s + 2) >> 2;
       }
-      if (n.has_top) {
+      if (has_top) {
         for (int k = 0; k < 4; ++k) s += T(k);
         return (s + 2) >> 2;
       }
@@ -232,6 +234,12 @@ VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y) {
   }
 }
 
+VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y) {
+  return intra4x4_pred_g([&](int xx) { return n.t[xx + 1]; },
+                         [&](int yy) { return yy < 0 ? n.t[0] : n.l[yy]; }, n.has_top, n.has_left,
+                         mode, x, y);
+}
+
 // ------------------------------------------------------------------------------ intra 16x16
 // top[0] = p[-1,-1], top[1..16] = p[0..15,-1]; left[0..15] = p[-1,0..15].
 struct Intra16Nb {
@@ -245,40 +253,53 @@ struct PredConst {
   int dc, a, b, c;
 };
 
-VEP_HD PredConst intra16x16_const(const Intra16Nb& n, int mode) {
+// Generic forms: T(x) = p[x, -1] for x in -1..15, L(y) = p[-1, y] for y in 0..15.
+template <class TF, class LF>
+VEP_HD PredConst intra16x16_const_g(TF T, LF L, bool has_top, bool has_left, int mode) {
   PredConst k{128, 0, 0, 0};
   if (mode == 2) {
     int s = 0;
-    if (n.has_top && n.has_left) {
-      for (int i = 0; i < 16; ++i) s += n.top[i + 1] + n.left[i];
+    if (has_top && has_left) {
+      for (int i = 0; i < 16; ++i) s += T(i) + L(i);
       k.dc = (s + 16) >> 5;
-    } else if (n.has_left) {
-      for (int i = 0; i < 16; ++i) s += n.left[i];
+    } else if (has_left) {
+      for (int i = 0; i < 16; ++i) s += L(i);
       k.dc = (s + 8) >> 4;
-    } else if (n.has_top) {
-      for (int i = 0; i < 16; ++i) s += n.top[i + 1];
+    } else if (has_top) {
+      for (int i = 0; i < 16; ++i) s += T(i);
       k.dc = (s + 8) >> 4;
     }
   } else if (mode == 3) {
     int H = 0, V = 0;
     for (int i = 0; i < 8; ++i) {
-      H += (i + 1) * (n.top[8 + i + 1] - n.top[6 - i + 1]);
-      V += (i + 1) * (n.left[8 + i] - (6 - i >= 0 ? n.left[6 - i] : n.top[0]));
+      H += (i + 1) * (T(8 + i) - T(6 - i));
+      V += (i + 1) * (L(8 + i) - (6 - i >= 0 ? L(6 - i) : T(-1)));
     }
-    k.a = 16 * (n.left[15] + n.top[16]);
+    k.a = 16 * (L(15) + T(15));
     k.b = (5 * H + 32) >> 6;
     k.c = (5 * V + 32) >> 6;
   }
   return k;
 }
 
-VEP_HD int intra16x16_pred(const Intra16Nb& n, const PredConst& k, int mode, int x, int y) {
+template <class TF, class LF>
+VEP_HD int intra16x16_pred_g(TF T, LF L, const PredConst& k, int mode, int x, int y) {
   switch (mode) {
-    case 0: return n.top[x + 1];
-    case 1: return n.left[y];
+    case 0: return T(x);
+    case 1: return L(y);
     case 2: return k.dc;
     default: return clip1((k.a + k.b * (x - 7) + k.c * (y - 7) + 16) >> 5);
   }
+}
+
+VEP_HD PredConst intra16x16_const(const Intra16Nb& n, int mode) {
+  return intra16x16_const_g([&](int x) { return n.top[x + 1]; }, [&](int y) { return n.left[y]; },
+                            n.has_top, n.has_left, mode);
+}
+
+VEP_HD int intra16x16_pred(const Intra16Nb& n, const PredConst& k, int mode, int x, int y) {
+  return intra16x16_pred_g([&](int xx) { return n.top[xx + 1]; }, [&](int yy) { return n.left[yy]; },
+                           k, mode, x, y);
 }
 
 // Chroma (4:2:0, 8x8 per component): top[0] = p[-1,-1], top[1..8]; left[0..7].
@@ -288,48 +309,62 @@ struct IntraChromaNb {
   bool has_top, has_left, has_tl;
 };
 
-// DC of chroma 4x4 block (bx, by) (§8.3.4.1-3).
-VEP_HD int chroma_dc(const IntraChromaNb& n, int bx, int by) {
+// DC of chroma 4x4 block (bx, by) (§8.3.4.1-3). Generic: T(x) = p[x, -1] (x in -1..7),
+// L(y) = p[-1, y] (y in 0..7).
+template <class TF, class LF>
+VEP_HD int chroma_dc_g(TF T, LF L, bool has_top, bool has_left, int bx, int by) {
   int st = 0, sl = 0;
   for (int i = 0; i < 4; ++i) {
-    st += n.top[1 + bx * 4 + i];
-    sl += n.left[by * 4 + i];
+    st += T(bx * 4 + i);
+    sl += L(by * 4 + i);
   }
   const bool corner_rule = (bx == 0 && by == 0) || (bx > 0 && by > 0);
   if (corner_rule) {
-    if (n.has_top && n.has_left) return (st + sl + 4) >> 3;
-    if (n.has_left) return (sl + 2) >> 2;
-    if (n.has_top) return (st + 2) >> 2;
+    if (has_top && has_left) return (st + sl + 4) >> 3;
+    if (has_left) return (sl + 2) >> 2;
+    if (has_top) return (st + 2) >> 2;
     return 128;
   }
   if (bx > 0) {  // top-right block: top first
-    if (n.has_top) return (st + 2) >> 2;
-    if (n.has_left) return (sl + 2) >> 2;
+    if (has_top) return (st + 2) >> 2;
+    if (has_left) return (sl + 2) >> 2;
     return 128;
   }
-  if (n.has_left) return (sl + 2) >> 2;  // bottom-left block: left first
-  if (n.has_top) return (st + 2) >> 2;
+  if (has_left) return (sl + 2) >> 2;  // bottom-left block: left first
+  if (has_top) return (st + 2) >> 2;
   return 128;
 }
 
-VEP_HD PredConst chroma_plane_const(const IntraChromaNb& n) {
+template <class TF, class LF>
+VEP_HD PredConst chroma_plane_const_g(TF T, LF L) {
   int H = 0, V = 0;
   for (int i = 0; i < 4; ++i) {
-    H += (i + 1) * (n.top[4 + i + 1] - n.top[2 - i + 1]);
-    V += (i + 1) * (n.left[4 + i] - (2 - i >= 0 ? n.left[2 - i] : n.top[0]));
+    H += (i + 1) * (T(4 + i) - T(2 - i));
+    V += (i + 1) * (L(4 + i) - (2 - i >= 0 ? L(2 - i) : T(-1)));
   }
-  PredConst k{0, 16 * (n.left[7] + n.top[8]), (34 * H + 32) >> 6, (34 * V + 32) >> 6};
+  PredConst k{0, 16 * (L(7) + T(7)), (34 * H + 32) >> 6, (34 * V + 32) >> 6};
   return k;
 }
 
 // mode: 0 DC, 1 horizontal, 2 vertical, 3 plane
-VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y) {
+template <class TF, class LF>
+VEP_HD int chroma_pred_g(TF T, LF L, bool has_top, bool has_left, const PredConst& k, int mode, int x,
+                         int y) {
   switch (mode) {
-    case 0: return chroma_dc(n, x >> 2, y >> 2);
-    case 1: return n.left[y];
-    case 2: return n.top[x + 1];
+    case 0: return chroma_dc_g(T, L, has_top, has_left, x >> 2, y >> 2);
+    case 1: return L(y);
+    case 2: return T(x);
     default: return clip1((k.a + k.b * (x - 3) + k.c * (y - 3) + 16) >> 5);
   }
+}
+
+VEP_HD PredConst chroma_plane_const(const IntraChromaNb& n) {
+  return chroma_plane_const_g([&](int x) { return n.top[x + 1]; }, [&](int y) { return n.left[y]; });
+}
+
+VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y) {
+  return chroma_pred_g([&](int xx) { return n.top[xx + 1]; }, [&](int yy) { return n.left[yy]; },
+                       n.has_top, n.has_left, k, mode, x, y);
 }
 
 // ------------------------------------------------------------------------------ inter

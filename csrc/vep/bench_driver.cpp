@@ -27,6 +27,8 @@ ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cach
     for (int f = 0; f < nframes; ++f) {
       auto au = enc.next();
       au->pin();  // as the RTSP depacketizer does: ingest-side copy into the pinned pool
+      stream_bytes_ += au->bytes();
+      stream_frames_ += 1;
       v.push_back(au);
     }
   });
@@ -116,7 +118,10 @@ void ReplayBench::step() {
     want_ = true;  // start parsing tick t+1 while tick t runs on the GPU
   }
   cv_.notify_all();
-  for (auto& j : jobs) bytes_ += u64(j.upd.nslots) * kPcmMbBytes;
+  for (auto& j : jobs) {
+    bytes_ += u64(j.upd.nslots) * kPcmMbBytes;
+    for (const auto& p : j.avc) bytes_ += u64(p->coefs.size()) * 2 + p->mbs.size() * sizeof(avc::MbRec);
+  }
   const i64 t0 = mono_us();
   const size_t n = jobs.size();
   w_.launch_async(jobs);  // publishes tick t-2; ticks t-1 and t stay in flight

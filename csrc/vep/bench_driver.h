@@ -28,6 +28,9 @@ class ReplayBench {
   double parse_only_ms(int ticks);
   u64 frames() const { return frames_; }
   u64 bitstream_bytes() const { return bytes_; }
+  // size of the replayed streams (all cameras' cached AUs)
+  u64 stream_bytes() const { return stream_bytes_; }
+  u64 stream_frames() const { return stream_frames_; }
   double parse_ms() const { return parse_us_ / 1000.0; }
   double batch_ms() const { return batch_us_ / 1000.0; }
   const std::vector<int>& cameras() const { return cams_; }
@@ -46,6 +49,7 @@ class ReplayBench {
   std::condition_variable cv_;
   std::thread pf_;
   u64 frames_ = 0, bytes_ = 0;
+  std::atomic<u64> stream_bytes_{0}, stream_frames_{0};
   double parse_us_ = 0, batch_us_ = 0;
 };
 

@@ -89,13 +89,26 @@ struct AvcDesc {
   i32 mb_begin;        // exclusive prefix of MBs over the round (inter kernel block -> picture)
   i32 pad;
   u32* err;            // pinned flag: wavefront timeout (frame dropped)
+  void* dbk;           // device scratch: AvcDbkInfo[wmbs * hmbs] (avc_bs_kernel -> deblock)
 };
+// Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.
+struct AvcDbkInfo {
+  u32 bs[4];      // 32 x 4-bit bS: nibble dir * 16 + edge * 4 + segment (0 = edge not filtered)
+  u8 alpha[6], beta[6], ia[6];  // [left, top, internal] luma, then [left, top, internal] chroma
+  u8 any;         // any bS != 0
+  u8 pad[13];
+};
+static_assert(sizeof(AvcDbkInfo) == 48, "AvcDbkInfo layout");
 constexpr int kAvcMaxRows = 512;  // MB rows per picture the wavefront kernels support (8K)
+constexpr int kAvcMaxCols = 512;  // MB columns
 // Inter / skip / I_PCM macroblocks of every picture of the round: one 256-lane workgroup per MB.
 void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
 // Intra 4x4 / 16x16 macroblocks in a wavefront, then the deblocking filter in a wavefront: one
 // 1024-lane workgroup (16 wave64s) per picture, rows synchronised through LDS counters.
 void launch_avc_intra(const AvcDesc* d_descs, int n, hipStream_t s);
+// Boundary strengths + edge thresholds of every MB of the round (fully parallel), then the
+// deblocking wavefront over them.
+void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
 void launch_avc_deblock(const AvcDesc* d_descs, int n, hipStream_t s);
 
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };

@@ -761,7 +761,7 @@ void Worker::launch_gpu(Stage& st) {
   struct AvcPic {
     const avc::Picture* p;
     int job;
-    size_t off_mbs, off_coef, off_mv;
+    size_t off_mbs, off_coef, off_mv, off_dbk;
   };
   std::vector<AvcPic> apics;
   int rounds = 0;
@@ -774,7 +774,7 @@ void Worker::launch_gpu(Stage& st) {
       if (int(v.size()) <= r) continue;
       const avc::Picture& p = *v[size_t(r)];
       VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows, "picture too tall for the wavefront kernels");
-      AvcPic a{&p, i, 0, 0, 0};
+      AvcPic a{&p, i, 0, 0, 0, 0};
       a.off_mbs = need;
       need += al(p.mbs.size() * sizeof(avc::MbRec));
       a.off_coef = need;
@@ -797,6 +797,11 @@ void Worker::launch_gpu(Stage& st) {
       rel += al(sg.len, 16);
     }
     need += rel;
+  }
+  need = al(need);
+  for (AvcPic& a : apics) {  // device-only scratch (never copied): per-MB loop-filter inputs
+    a.off_dbk = need;
+    need += al(size_t(a.p->nmbs()) * sizeof(gpu::AvcDbkInfo));
   }
   need = al(need);
   if (need > st.cap) {
@@ -970,6 +975,7 @@ void Worker::launch_gpu(Stage& st) {
       g.mb_begin = mbs;
       g.pad = 0;
       g.err = const_cast<u32*>(st.err_dev) + a.job;
+      g.dbk = st.d + a.off_dbk;
       mbs += a.p->nmbs();
     }
   }
@@ -994,7 +1000,10 @@ void Worker::launch_gpu(Stage& st) {
     }
     gpu::launch_avc_inter(ad, np, mbs, stream_);
     if (intra) gpu::launch_avc_intra(ad, np, stream_);
-    if (dbk) gpu::launch_avc_deblock(ad, np, stream_);
+    if (dbk) {
+      gpu::launch_avc_bs(ad, np, mbs, stream_);
+      gpu::launch_avc_deblock(ad, np, stream_);
+    }
   }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), n, tiles,
                              stream_);

@@ -85,6 +85,8 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
     ac.seed = cfg.seed;
     ac.deblock_idc = cfg.deblock_idc;
     ac.coverage = cfg.coverage;
+    ac.noise = cfg.noise;
+    ac.temporal_noise = cfg.temporal_noise;
     if (cfg.coverage) {
       ac.pcm_rate = 3;
       ac.nonref_rate = 15;

@@ -32,6 +32,8 @@ struct SynthConfig {
   int objects = 3;         // moving textured objects in the compressed scene
   int deblock_idc = 0;     // disable_deblocking_filter_idc
   bool coverage = false;   // randomised mode decisions (decoder coverage streams)
+  double noise = 3.0;      // static texture amplitude of the compressed scene
+  double temporal_noise = 0.0;  // per-frame sensor noise (P-picture residual, bitrate)
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)
