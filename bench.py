@@ -259,6 +259,12 @@ def main():
             "rank0_launch_breakdown_ms_per_step": {
                 k: round((v - tm0[k]) / a.steps, 4) for k, v in tm1.items()},
         }
+        if os.environ.get("VEP_AVC_PROF") == "1":
+            pr = worker.avc_profile()
+            for ph in ("intra", "dbk"):
+                n = max(1, pr[f"{ph}_mbs"])
+                res[f"{ph}_cycles_per_mb"] = {k[len(ph) + 1:]: round(v / n, 1) for k, v in pr.items()
+                                              if k.startswith(ph) and not k.endswith("mbs")}
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -465,6 +465,15 @@ PYBIND11_MODULE(_vep, m) {
              w.run_batch(jobs);
              return n;
            })
+      .def("avc_profile", [](Worker& w) {
+        static const char* kNames[gpu::kAvcProfSlots] = {
+            "intra_wait", "intra_load", "intra_luma", "intra_chroma", "intra_store", "intra_mbs",
+            "dbk_wait", "dbk_load", "dbk_filter", "dbk_store", "dbk_mbs", "intra_residual"};
+        const std::vector<u64> v = w.avc_profile();
+        py::dict d;
+        for (int i = 0; i < gpu::kAvcProfSlots; ++i) d[kNames[i]] = v[size_t(i)];
+        return d;
+      })
       .def("stats",
            [](Worker& w, int i) {
              Camera& c = cam_of(w, i);

@@ -234,6 +234,102 @@ VEP_HD int intra4x4_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, in
   }
 }
 
+// Tap form of the non-DC Intra_4x4 predictors (same formulas as intra4x4_pred_g): the sample
+// is (sum_k w[k] * N[idx[k]] + add) >> shift over the 13 neighbours
+// N = {p[-1,-1], p[0..7,-1], p[-1,0..3]}. The GPU evaluates it with all LDS reads issued at
+// once; tests pin it to intra4x4_pred_g for every mode and position.
+struct Taps4 {
+  u8 idx[3], w[3];
+  u8 n, add, shift;
+};
+VEP_HD Taps4 intra4x4_taps(int mode, int x, int y) {
+  auto T = [](int xx) { return u8(xx + 1); };
+  auto L = [](int yy) { return u8(yy < 0 ? 0 : 9 + yy); };
+  Taps4 t{{0, 0, 0}, {1, 2, 1}, 3, 2, 2};
+  auto set3 = [&](u8 a, u8 b, u8 c) {
+    t.idx[0] = a;
+    t.idx[1] = b;
+    t.idx[2] = c;
+  };
+  auto set2 = [&](u8 a, u8 b) {  // (a + b + 1) >> 1
+    t.idx[0] = a;
+    t.idx[1] = b;
+    t.idx[2] = a;
+    t.w[0] = 1;
+    t.w[1] = 1;
+    t.w[2] = 0;
+    t.n = 2;
+    t.add = 1;
+    t.shift = 1;
+  };
+  auto set1 = [&](u8 a) {
+    t.idx[0] = t.idx[1] = t.idx[2] = a;
+    t.w[0] = 1;
+    t.w[1] = 0;
+    t.w[2] = 0;
+    t.n = 1;
+    t.add = 0;
+    t.shift = 0;
+  };
+  switch (mode) {
+    case 0: set1(T(x)); break;
+    case 1: set1(L(y)); break;
+    case 3:
+      if (x == 3 && y == 3) {
+        set3(T(6), T(7), T(7));
+        t.w[0] = 1, t.w[1] = 3, t.w[2] = 0;
+      } else {
+        set3(T(x + y), T(x + y + 1), T(x + y + 2));
+      }
+      break;
+    case 4:
+      if (x > y) set3(T(x - y - 2), T(x - y - 1), T(x - y));
+      else if (x < y) set3(L(y - x - 2), L(y - x - 1), L(y - x));
+      else set3(T(0), T(-1), L(0));
+      break;
+    case 5: {
+      const int z = 2 * x - y, b = x - (y >> 1);
+      if (z >= 0 && (z & 1) == 0) set2(T(b - 1), T(b));
+      else if (z >= 0) set3(T(b - 2), T(b - 1), T(b));
+      else if (z == -1) set3(L(0), L(-1), T(0));
+      else set3(L(y - 1), L(y - 2), L(y - 3));
+      break;
+    }
+    case 6: {
+      const int z = 2 * y - x, b = y - (x >> 1);
+      if (z >= 0 && (z & 1) == 0) set2(L(b - 1), L(b));
+      else if (z >= 0) set3(L(b - 2), L(b - 1), L(b));
+      else if (z == -1) set3(L(0), L(-1), T(0));
+      else set3(T(x - 1), T(x - 2), T(x - 3));
+      break;
+    }
+    case 7: {
+      const int b = x + (y >> 1);
+      if ((y & 1) == 0) set2(T(b), T(b + 1));
+      else set3(T(b), T(b + 1), T(b + 2));
+      break;
+    }
+    default: {  // 8
+      const int z = x + 2 * y, b = y + (x >> 1);
+      if (z > 5) set1(L(3));
+      else if (z == 5) {
+        set3(L(2), L(3), L(3));
+        t.w[0] = 1, t.w[1] = 3, t.w[2] = 0;
+      } else if ((z & 1) == 0) set2(L(b), L(b + 1));
+      else set3(L(b), L(b + 1), L(b + 2));
+      break;
+    }
+  }
+  return t;
+}
+
+// Packed tap word (GPU LDS): idx0..2 (4 bits each), w0..2 (2 bits), add (2), shift (2), dc (1).
+constexpr u32 kTapDc = 1u << 24;
+VEP_HD u32 pack_taps(const Taps4& t) {
+  return u32(t.idx[0]) | u32(t.idx[1]) << 4 | u32(t.idx[2]) << 8 | u32(t.w[0]) << 12 |
+         u32(t.w[1]) << 14 | u32(t.w[2]) << 16 | u32(t.add) << 18 | u32(t.shift) << 20;
+}
+
 VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y) {
   return intra4x4_pred_g([&](int xx) { return n.t[xx + 1]; },
                          [&](int yy) { return yy < 0 ? n.t[0] : n.l[yy]; }, n.has_top, n.has_left,
@@ -254,32 +350,36 @@ struct PredConst {
 };
 
 // Generic forms: T(x) = p[x, -1] for x in -1..15, L(y) = p[-1, y] for y in 0..15.
-template <class TF, class LF>
-VEP_HD PredConst intra16x16_const_g(TF T, LF L, bool has_top, bool has_left, int mode) {
+// Final step of the 16x16 constants from the neighbour sums (the GPU computes the sums with a
+// wave reduction): st / sl = sum of the 16 top / left samples, H / V the plane gradients.
+VEP_HD PredConst intra16x16_const_from_sums(int mode, bool has_top, bool has_left, int st, int sl,
+                                            int H, int V, int top15, int left15) {
   PredConst k{128, 0, 0, 0};
   if (mode == 2) {
-    int s = 0;
-    if (has_top && has_left) {
-      for (int i = 0; i < 16; ++i) s += T(i) + L(i);
-      k.dc = (s + 16) >> 5;
-    } else if (has_left) {
-      for (int i = 0; i < 16; ++i) s += L(i);
-      k.dc = (s + 8) >> 4;
-    } else if (has_top) {
-      for (int i = 0; i < 16; ++i) s += T(i);
-      k.dc = (s + 8) >> 4;
-    }
+    if (has_top && has_left) k.dc = (st + sl + 16) >> 5;
+    else if (has_left) k.dc = (sl + 8) >> 4;
+    else if (has_top) k.dc = (st + 8) >> 4;
   } else if (mode == 3) {
-    int H = 0, V = 0;
-    for (int i = 0; i < 8; ++i) {
-      H += (i + 1) * (T(8 + i) - T(6 - i));
-      V += (i + 1) * (L(8 + i) - (6 - i >= 0 ? L(6 - i) : T(-1)));
-    }
-    k.a = 16 * (L(15) + T(15));
+    k.a = 16 * (left15 + top15);
     k.b = (5 * H + 32) >> 6;
     k.c = (5 * V + 32) >> 6;
   }
   return k;
+}
+
+// Generic forms: T(x) = p[x, -1] for x in -1..15, L(y) = p[-1, y] for y in 0..15.
+template <class TF, class LF>
+VEP_HD PredConst intra16x16_const_g(TF T, LF L, bool has_top, bool has_left, int mode) {
+  int st = 0, sl = 0, H = 0, V = 0;
+  for (int i = 0; i < 16; ++i) {
+    st += T(i);
+    sl += L(i);
+  }
+  for (int i = 0; i < 8; ++i) {
+    H += (i + 1) * (T(8 + i) - T(6 - i));
+    V += (i + 1) * (L(8 + i) - (6 - i >= 0 ? L(6 - i) : T(-1)));
+  }
+  return intra16x16_const_from_sums(mode, has_top, has_left, st, sl, H, V, T(15), L(15));
 }
 
 template <class TF, class LF>

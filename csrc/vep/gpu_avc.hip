@@ -52,7 +52,7 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     if (descs[mid].mb_begin <= g) lo = mid;
     else hi = mid - 1;
   }
-  const AvcDesc& d = descs[lo];
+  const AvcDesc d = descs[lo];
   const int mb = g - d.mb_begin;
   const MbRec m = rec(d, mb);
   if (m.kind != avc::kSkip && m.kind != avc::kInter && m.kind != avc::kIPcm) return;
@@ -140,167 +140,315 @@ __device__ inline void wave_sync() {
 
 // --------------------------------------------------------------------------------- intra
 
+constexpr int kTp = 24;  // luma tile pitch: row 0 = p[-1..19, -1], rows 1..16 = p[-1..15, y]
+constexpr int kCp = 12;  // chroma tile pitch: row 0 = p[-1..7, -1], rows 1..8 = p[-1..7, y]
+
 struct alignas(16) IntraWave {
-  u64 mask[kAvcMaxCols / 64];  // intra MBs (I4x4 / I16x16) of the current row
+  MbRec rec[64];      // records of the current 64-MB chunk of the row
   i16 coef[24 * 16];  // the MB's dequantised residual blocks (coded blocks only, pool order)
-  u8 mb[256];
-  u8 mbc[2][64];
-  u8 top[21];      // [0] top-left, [1..16] above, [17..20] above-right
-  u8 left[16];
-  u8 ctop[2][9];   // [0] top-left, [1..8] above
-  u8 cleft[2][8];
-  u8 carry[16];    // right luma column of the previous MB of this row (if this wave built it)
+  i16 res[384];       // residual samples: 256 luma (raster) + 2 x 64 chroma
+  int ftmp[24 * 16];  // inverse transform: row-pass intermediates
+  u32 taps[256];      // Intra_4x4 tap words of the MB's samples
+  u8 tile[17 * kTp];  // luma neighbours + the MB being reconstructed (branch-free addressing)
+  u8 ctile[2][9 * kCp];
+  u8 carry[16];       // right luma column of the previous MB of this row (if this wave built it)
   u8 ccarry[2][8];
 };
 
-// One intra MB, whole wave. Every global load of the MB (coefficients, neighbour samples) is
-// issued in one batch so the MB costs one memory round trip plus LDS work.
+__device__ inline bool avail_hdr(const AvcDesc& d, const uint4& h, bool in_pic, u16 slice) {
+  if (!in_pic) return false;
+  const u8 kind = u8(h.x & 0xff);
+  if (u16(h.w >> 16) != slice) return false;  // MbRec.slice lives in bytes 14..15
+  return !(d.constrained && !avc::is_intra(kind));
+}
+
+// One intra MB, whole wave: one round trip of global loads (all issued before any is used),
+// a parallel residual pass, then prediction out of LDS.
 __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, int row, bool carry,
-                         int lane) {
+                         int lane, u64 t_start, u64* acc) {
   const int W = d.wmbs, pitch = W * 16;
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
-  const bool A = intra_avail(d, m, x - 1, row), B = intra_avail(d, m, x, row - 1),
-             C = intra_avail(d, m, x + 1, row - 1), D = intra_avail(d, m, x - 1, row - 1);
   const int x0 = x * 16, y0 = row * 16;
-  // ---- batch: residual blocks (16 B per lane) + neighbour samples
+  const bool up = row > 0, lf = x > 0;
+  const MbRec* recs = static_cast<const MbRec*>(d.mbs);
+  // ---- issue every load
   const int nblk = __popc(m.luma_coded) + __popc(m.chroma_coded);
-  const uint4* src = reinterpret_cast<const uint4*>(d.coefs + size_t(m.coef) * 16);
-  uint4* dst = reinterpret_cast<uint4*>(L.coef);
-  if (lane < 2 * nblk) dst[lane] = src[lane];
+  uint4 cv = make_uint4(0, 0, 0, 0);
+  if (lane < 2 * nblk) cv = reinterpret_cast<const uint4*>(d.coefs + size_t(m.coef) * 16)[lane];
+  u32 a = 128, b = 128;
+  if (lane < 21) {  // luma row above: x0-1 .. x0+19
+    const int px = x0 - 1 + lane;
+    if (up && px >= 0 && px < pitch) a = Y[size_t(y0 - 1) * pitch + px];
+  } else if (lane < 37) {  // luma left column
+    if (lf && !carry) a = Y[size_t(y0 + lane - 21) * pitch + x0 - 1];
+  } else if (lane < 55) {  // chroma row above: x*8-1 .. x*8+7 per component
+    const int c = (lane - 37) / 9, k = (lane - 37) % 9, px = x * 8 - 1 + k;
+    if (up && px >= 0) a = UV[size_t(row * 8 - 1) * pitch + px * 2 + c];
+  }
+  if (lane >= 48) {  // chroma left columns
+    const int c = (lane - 48) >> 3, k = (lane - 48) & 7;
+    if (lf && !carry) b = UV[size_t(row * 8 + k) * pitch + (x * 8 - 1) * 2 + c];
+  }
+  uint4 h = make_uint4(0, 0, 0, 0);  // neighbour record headers: B, C, D, A
+  bool in_pic = false;
+  if (lane == 56) in_pic = up;
+  else if (lane == 57) in_pic = up && x + 1 < W;
+  else if (lane == 58) in_pic = up && lf;
+  else if (lane == 59) in_pic = lf;
+  if (in_pic) {
+    const int nx = lane == 56 ? x : lane == 57 ? x + 1 : x - 1, ny = lane == 59 ? row : row - 1;
+    h = *reinterpret_cast<const uint4*>(&recs[ny * W + nx]);
+  }
+  // ---- availability (B, C, D, A) and the LDS neighbour tiles
+  const bool av = avail_hdr(d, h, in_pic, m.slice);
+  const bool B = __builtin_amdgcn_readlane(int(av), 56) != 0;
+  const bool C = __builtin_amdgcn_readlane(int(av), 57) != 0;
+  const bool D = __builtin_amdgcn_readlane(int(av), 58) != 0;
+  const bool A = __builtin_amdgcn_readlane(int(av), 59) != 0;
+  if (lane < 2 * nblk) reinterpret_cast<uint4*>(L.coef)[lane] = cv;
   if (lane < 21) {
-    u8 v = 128;
-    if (lane == 0) { if (D) v = Y[size_t(y0 - 1) * pitch + x0 - 1]; }
-    else if (lane <= 16) { if (B) v = Y[size_t(y0 - 1) * pitch + x0 + lane - 1]; }
-    else if (C) v = Y[size_t(y0 - 1) * pitch + x0 + lane - 1];
-    L.top[lane] = v;
+    L.tile[lane] = u8((lane == 0 ? D : lane <= 16 ? B : C) ? a : 128u);
   } else if (lane < 37) {
     const int k = lane - 21;
-    L.left[k] = !A ? u8(128) : carry ? L.carry[k] : Y[size_t(y0 + k) * pitch + x0 - 1];
+    L.tile[(k + 1) * kTp] = !A ? u8(128) : carry ? L.carry[k] : u8(a);
   } else if (lane < 55) {
     const int c = (lane - 37) / 9, k = (lane - 37) % 9;
-    u8 v = 128;
-    if (k == 0) { if (D) v = UV[size_t(row * 8 - 1) * pitch + (x * 8 - 1) * 2 + c]; }
-    else if (B) v = UV[size_t(row * 8 - 1) * pitch + (x * 8 + k - 1) * 2 + c];
-    L.ctop[c][k] = v;
+    L.ctile[c][k] = u8((k == 0 ? D : B) ? a : 128u);
   }
   if (lane >= 48) {
     const int c = (lane - 48) >> 3, k = (lane - 48) & 7;
-    L.cleft[c][k] = !A ? u8(128) : carry ? L.ccarry[c][k] : UV[size_t(row * 8 + k) * pitch + (x * 8 - 1) * 2 + c];
+    L.ctile[c][(k + 1) * kCp] = !A ? u8(128) : carry ? L.ccarry[c][k] : u8(b);
   }
   wave_sync();
-  auto lblk = [&](int r) { return L.coef + __popc(m.luma_coded & ((1u << r) - 1)) * 16; };
-  // ---- luma (predictors read LDS through accessors: no private arrays, no scratch)
+  const u64 t_loaded = d.prof ? clock64() : 0;
+  // ---- residual samples of every coded block (independent of prediction), as the two passes
+  // of the inverse transform: 24 blocks x 4 rows, then 24 blocks x 4 columns, 2 tasks per lane.
+  // Same integer operations as avc::idct4x4 (bit-exact).
+  auto coded = [&](int blk) {
+    return blk < 16 ? (m.luma_coded >> blk) & 1 : (m.chroma_coded >> (blk - 16)) & 1;
+  };
+  auto pool = [&](int blk) {
+    return blk < 16 ? __popc(m.luma_coded & ((1u << blk) - 1))
+                    : __popc(m.luma_coded) + __popc(m.chroma_coded & ((1u << (blk - 16)) - 1));
+  };
+#pragma unroll 1
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k, blk = t >> 2, i = t & 3;
+    if (blk < 24 && coded(blk)) {
+      const i16* dq = L.coef + pool(blk) * 16 + i * 4;
+      const int d0 = dq[0], d1 = dq[1], d2 = dq[2], d3 = dq[3];
+      const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
+      int* f = L.ftmp + blk * 16 + i * 4;
+      f[0] = e0 + e3;
+      f[1] = e1 + e2;
+      f[2] = e1 - e2;
+      f[3] = e0 - e3;
+    }
+  }
+  wave_sync();
+#pragma unroll 1
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k, blk = t >> 2, j = t & 3;
+    if (blk >= 24) continue;
+    int r[4] = {0, 0, 0, 0};
+    if (coded(blk)) {
+      const int* f = L.ftmp + blk * 16 + j;
+      const int f0 = f[0], f1 = f[4], f2 = f[8], f3 = f[12];
+      const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
+      r[0] = (g0 + g3 + 32) >> 6;
+      r[1] = (g1 + g2 + 32) >> 6;
+      r[2] = (g1 - g2 + 32) >> 6;
+      r[3] = (g0 - g3 + 32) >> 6;
+    }
+    if (blk < 16) {
+      const int bx = blk & 3, by = blk >> 2;
+      for (int i = 0; i < 4; ++i) L.res[(by * 4 + i) * 16 + bx * 4 + j] = i16(r[i]);
+    } else {
+      const int c = (blk - 16) >> 2, cb = (blk - 16) & 3, bx = cb & 1, by = cb >> 1;
+      for (int i = 0; i < 4; ++i) L.res[256 + c * 64 + (by * 4 + i) * 8 + bx * 4 + j] = i16(r[i]);
+    }
+  }
+  wave_sync();
+  const u64 t_res = d.prof ? clock64() : 0;
+  // ---- luma prediction
+  auto P = [&](int ax, int ay) -> int { return L.tile[(ay + 1) * kTp + ax + 1]; };
   if (m.kind == avc::kI16x16) {
-    auto T = [&](int xx) { return int(L.top[xx + 1]); };
-    auto Lf = [&](int yy) { return int(L.left[yy]); };
-    const avc::PredConst pk = avc::intra16x16_const_g(T, Lf, B, A, m.i16_mode);
+    // DC / plane constants: the neighbour sums by a wave reduction instead of 32 reads per lane
+    int st = 0, sl = 0, H = 0, V = 0;
+    if (lane < 16) st = P(lane, -1);
+    else if (lane < 32) sl = P(-1, lane - 16);
+    else if (lane < 40) H = (lane - 31) * (P(8 + lane - 32, -1) - P(6 - (lane - 32), -1));
+    else if (lane < 48) {
+      const int i = lane - 40;
+      V = (i + 1) * (P(-1, 8 + i) - (6 - i >= 0 ? P(-1, 6 - i) : P(-1, -1)));
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      st += __shfl_xor(st, off);
+      sl += __shfl_xor(sl, off);
+      H += __shfl_xor(H, off);
+      V += __shfl_xor(V, off);
+    }
+    const avc::PredConst pk =
+        avc::intra16x16_const_from_sums(m.i16_mode, B, A, st, sl, H, V, P(15, -1), P(-1, 15));
+    auto T = [&](int xx) { return P(xx, -1); };
+    auto Lf = [&](int yy) { return P(-1, yy); };
+    u8 out[4];
     for (int k = 0; k < 4; ++k) {
       const int p = lane + 64 * k, px = p & 15, py = p >> 4;
-      int v = avc::intra16x16_pred_g(T, Lf, pk, m.i16_mode, px, py);
-      const int blk = (py >> 2) * 4 + (px >> 2);
-      if ((m.luma_coded >> blk) & 1) v += avc::idct4x4_at(lblk(blk), py & 3, px & 3);
-      L.mb[p] = u8(avc::clip1(v));
+      out[k] = u8(avc::clip1(avc::intra16x16_pred_g(T, Lf, pk, m.i16_mode, px, py) + L.res[p]));
+    }
+    wave_sync();  // every lane has read the neighbours before the MB is written over them
+    for (int k = 0; k < 4; ++k) {
+      const int p = lane + 64 * k;
+      L.tile[((p >> 4) + 1) * kTp + (p & 15) + 1] = out[k];
     }
   } else {
+    // Tap words of all 256 samples in one parallel pass (the mode divergence is paid once)
+#pragma unroll 1
+    for (int k = 0; k < 4; ++k) {
+      const int p = lane + 64 * k, px = p & 15, py = p >> 4;
+      const int mode = avc::i4_mode(m, (py >> 2) * 4 + (px >> 2));
+      L.taps[p] = mode == 2 ? avc::kTapDc : avc::pack_taps(avc::intra4x4_taps(mode, px & 3, py & 3));
+    }
+    wave_sync();
     // Diagonal schedule: block (bx, by) only reads left / top / top-left / (when available in
-    // coding order) top-right neighbours, all on earlier diagonals s = bx + 2 * by, so the 16
-    // blocks run in 10 steps, up to 4 blocks (16 lanes each) at a time.
+    // coding order) top-right neighbours, all on earlier diagonals s = bx + 2 * by: 10 steps of
+    // at most 2 blocks (lanes 0-15 and 16-31).
     const int g = lane >> 4, i = (lane >> 2) & 3, j = lane & 3;
+#pragma unroll 1
     for (int st = 0; st < 10; ++st) {
-      int bx = -1, by = -1, cnt = 0;
-      for (int yy = 0; yy < 4; ++yy) {
-        const int xx = st - 2 * yy;
-        if (xx >= 0 && xx < 4) {
-          if (cnt == g) bx = xx, by = yy;
-          ++cnt;
-        }
-      }
-      if (bx >= 0) {
-        const int r = by * 4 + bx, idx = avc::raster_to_blk(r);
-        const bool tr = by == 0 ? (bx < 3 ? B : C) : (bx < 3 && avc::raster_to_blk((by - 1) * 4 + bx + 1) < idx);
-        auto P = [&](int ax, int ay) -> int {  // MB-relative, ax in -1..19, ay in -1..15
-          if (ay < 0) return L.top[ax + 1];
-          if (ax < 0) return L.left[ay];
-          return L.mb[ay * 16 + ax];
+      const int by = g == 0 ? (st >= 6 ? st / 2 - 1 : st / 2 - (st >= 2 ? 0 : 0)) : 0;
+      // blocks of diagonal st: (st - 2*yy, yy) for yy = max(0, (st - 3 + 1) / 2) .. min(3, st / 2)
+      const int y_lo = st > 3 ? (st - 2) / 2 : 0, y_hi = st / 2 < 3 ? st / 2 : 3;
+      const int yy = y_lo + g;
+      (void)by;
+      if (g < 2 && yy <= y_hi) {
+        const int bx = st - 2 * yy, byy = yy;
+        const int r = byy * 4 + bx, idx = avc::raster_to_blk(r);
+        const bool tr = byy == 0 ? (bx < 3 ? B : C) : (bx < 3 && avc::raster_to_blk((byy - 1) * 4 + bx + 1) < idx);
+        const bool ht = byy > 0 || B, hl = bx > 0 || A;
+        // tile index of neighbour N[k] of this block (top-right substitution folded in)
+        auto nidx = [&](int k) {
+          if (k == 0) return (byy * 4) * kTp + bx * 4;
+          if (k <= 8) return (byy * 4) * kTp + bx * 4 + 1 + (k - 1 >= 4 && !tr ? 3 : k - 1);
+          return (byy * 4 + k - 8) * kTp + bx * 4;
         };
-        auto T = [&](int xx) { return P(bx * 4 + (xx >= 4 && !tr ? 3 : xx), by * 4 - 1); };
-        auto Lf = [&](int yy) { return P(bx * 4 - 1, by * 4 + yy); };
-        int v = avc::intra4x4_pred_g(T, Lf, by > 0 || B, bx > 0 || A, avc::i4_mode(m, r), j, i);
-        if ((m.luma_coded >> r) & 1) v += avc::idct4x4_at(lblk(r), i, j);
-        L.mb[(by * 4 + i) * 16 + bx * 4 + j] = u8(avc::clip1(v));
+        const int p = (byy * 4 + i) * 16 + bx * 4 + j;
+        const u32 tp = L.taps[p];
+        int v;
+        if (tp & avc::kTapDc) {
+          int st4 = 0, sl4 = 0;
+          for (int q = 0; q < 4; ++q) {
+            st4 += L.tile[nidx(1 + q)];
+            sl4 += L.tile[nidx(9 + q)];
+          }
+          v = ht && hl ? (st4 + sl4 + 4) >> 3 : hl ? (sl4 + 2) >> 2 : ht ? (st4 + 2) >> 2 : 128;
+        } else {
+          const int n0 = L.tile[nidx(int(tp & 15))], n1 = L.tile[nidx(int((tp >> 4) & 15))],
+                    n2 = L.tile[nidx(int((tp >> 8) & 15))];
+          v = (int((tp >> 12) & 3) * n0 + int((tp >> 14) & 3) * n1 + int((tp >> 16) & 3) * n2 +
+               int((tp >> 18) & 3)) >> int((tp >> 20) & 3);
+        }
+        v += L.res[p];
+        L.tile[(byy * 4 + i + 1) * kTp + bx * 4 + j + 1] = u8(avc::clip1(v));
       }
       wave_sync();
     }
   }
+  const u64 t_luma = d.prof ? clock64() : 0;
   // ---- chroma (2 samples per lane)
-  const i16* cbase = L.coef + __popc(m.luma_coded) * 16;
-  for (int k = 0; k < 2; ++k) {
-    const int p = lane + 64 * k, c = p >> 6, q = p & 63, px = q & 7, py = q >> 3;
-    auto T = [&](int xx) { return int(L.ctop[c][xx + 1]); };
-    auto Lf = [&](int yy) { return int(L.cleft[c][yy]); };
-    const avc::PredConst pk =
-        m.chroma_mode == 3 ? avc::chroma_plane_const_g(T, Lf) : avc::PredConst{0, 0, 0, 0};
-    int v = avc::chroma_pred_g(T, Lf, B, A, pk, m.chroma_mode, px, py);
-    const int kk = c * 4 + (py >> 2) * 2 + (px >> 2);
-    if ((m.chroma_coded >> kk) & 1)
-      v += avc::idct4x4_at(cbase + __popc(m.chroma_coded & ((1u << kk) - 1)) * 16, py & 3, px & 3);
-    L.mbc[c][q] = u8(avc::clip1(v));
+  {
+    u8 out[2];
+    for (int k = 0; k < 2; ++k) {
+      const int p = lane + 64 * k, c = p >> 6, q = p & 63, px = q & 7, py = q >> 3;
+      const u8* t = L.ctile[c];
+      auto T = [&](int xx) { return int(t[xx + 1]); };
+      auto Lf = [&](int yy) { return int(t[(yy + 1) * kCp]); };
+      const avc::PredConst pk =
+          m.chroma_mode == 3 ? avc::chroma_plane_const_g(T, Lf) : avc::PredConst{0, 0, 0, 0};
+      out[k] = u8(avc::clip1(avc::chroma_pred_g(T, Lf, B, A, pk, m.chroma_mode, px, py) + L.res[256 + p]));
+    }
+    wave_sync();
+    for (int k = 0; k < 2; ++k) {
+      const int p = lane + 64 * k, c = p >> 6, q = p & 63;
+      L.ctile[c][((q >> 3) + 1) * kCp + (q & 7) + 1] = out[k];
+    }
   }
   wave_sync();
+  const u64 t_chroma = d.prof ? clock64() : 0;
   // ---- write back + carry the right column for the next MB of this row
   {
     const int ry = lane >> 2, rx = (lane & 3) * 4;
-    u32 w = 0;
-    for (int b = 0; b < 4; ++b) w |= u32(L.mb[ry * 16 + rx + b]) << (8 * b);
+    const u8* src = &L.tile[(ry + 1) * kTp + rx + 1];
+    const u32 w = u32(src[0]) | u32(src[1]) << 8 | u32(src[2]) << 16 | u32(src[3]) << 24;
     *reinterpret_cast<u32*>(Y + size_t(y0 + ry) * pitch + x0 + rx) = w;
     if (lane < 32) {  // NV12: 8 rows x 16 bytes
       const int cyr = lane >> 2, cxb = (lane & 3) * 2;
-      u32 cw = 0;
-      for (int b = 0; b < 2; ++b)
-        cw |= (u32(L.mbc[0][cyr * 8 + cxb + b]) | u32(L.mbc[1][cyr * 8 + cxb + b]) << 8) << (16 * b);
+      const u8* c0 = &L.ctile[0][(cyr + 1) * kCp + cxb + 1];
+      const u8* c1 = &L.ctile[1][(cyr + 1) * kCp + cxb + 1];
+      const u32 cw = u32(c0[0]) | u32(c1[0]) << 8 | u32(c0[1]) << 16 | u32(c1[1]) << 24;
       *reinterpret_cast<u32*>(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cxb) * 2) = cw;
     }
-    if (lane < 16) L.carry[lane] = L.mb[lane * 16 + 15];
-    if (lane < 16) L.ccarry[lane >> 3][lane & 7] = L.mbc[lane >> 3][(lane & 7) * 8 + 7];
+    if (lane < 16) L.carry[lane] = L.tile[(lane + 1) * kTp + 16];
+    if (lane < 16) L.ccarry[lane >> 3][lane & 7] = L.ctile[lane >> 3][((lane & 7) + 1) * kCp + 8];
   }
   wave_sync();
+  if (d.prof) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // count the store drain here
+    const u64 t_end = clock64();
+    acc[1] += t_loaded - t_start;
+    acc[2] += t_luma - t_res;
+    acc[6] += t_res - t_loaded;
+    acc[3] += t_chroma - t_luma;
+    acc[4] += t_end - t_chroma;
+    acc[5] += 1;
+  }
 }
 
 __global__ __launch_bounds__(1024) void avc_intra_kernel(const AvcDesc* __restrict__ descs) {
   __shared__ Sync sync;
   __shared__ IntraWave lds[kWaves];
-  const AvcDesc& d = descs[blockIdx.x];
+  const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs;
   sync_init(sync, H);
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   IntraWave& L = lds[wave];
-  const int words = (W + 63) / 64;
+  const MbRec* recs = static_cast<const MbRec*>(d.mbs);
+  u64 acc[7] = {0, 0, 0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
   for (int row = wave; row < H; row += kWaves) {
-    // ---- which MBs of this row need the wavefront (one parallel scan, ballot per 64 MBs)
-    for (int wd = 0; wd < words; ++wd) {
-      const int x = wd * 64 + lane;
+    int prev = -2;
+    for (int base = 0; base < W; base += 64) {
+      // ---- the chunk's records into LDS (one round trip) and its intra MBs by ballot
+      const int x = base + lane;
       bool intra = false;
       if (x < W) {
-        const u8 k = rec(d, row * W + x).kind;
-        intra = k == avc::kI4x4 || k == avc::kI16x16;
+        const uint2* src = reinterpret_cast<const uint2*>(&recs[row * W + x]);
+        uint2* dst = reinterpret_cast<uint2*>(&L.rec[lane]);
+        uint2 q[5];
+        for (int k = 0; k < 5; ++k) q[k] = src[k];
+        for (int k = 0; k < 5; ++k) dst[k] = q[k];
+        const u8 kd = u8(q[0].x & 0xff);
+        intra = kd == avc::kI4x4 || kd == avc::kI16x16;
       }
-      const u64 b = __ballot(intra);
-      if (lane == 0) L.mask[wd] = b;
-    }
-    wave_sync();
-    int prev = -2;
-    for (int wd = 0; wd < words; ++wd) {
-      for (u64 b = L.mask[wd]; b; b &= b - 1) {
-        const int x = wd * 64 + __ffsll(static_cast<unsigned long long>(b)) - 1;
-        publish_row(sync, row, u32(x));  // every MB left of x is final
-        if (row > 0) wait_row(sync, row - 1, u32(x + 2 < W ? x + 2 : W), d.err);
-        const MbRec m = rec(d, row * W + x);
-        intra_mb(d, L, m, x, row, prev == x - 1, lane);
-        prev = x;
+      const u64 mask = __ballot(intra);
+      wave_sync();
+      for (u64 bits = mask; bits; bits &= bits - 1) {
+        const int xx = base + __ffsll(static_cast<unsigned long long>(bits)) - 1;
+        const u64 t0 = d.prof ? clock64() : 0;
+        publish_row(sync, row, u32(xx));  // every MB left of xx is final
+        if (row > 0) wait_row(sync, row - 1, u32(xx + 2 < W ? xx + 2 : W), d.err);
+        const u64 t1 = d.prof ? clock64() : 0;
+        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, t1, acc);
+        prev = xx;
+        acc[0] += t1 - t0;
       }
     }
     publish_row(sync, row, u32(W));
+  }
+  if (d.prof && lane == 0) {
+    for (int k = 0; k < 6; ++k) atomicAdd(&d.prof[k], acc[k]);
+    atomicAdd(&d.prof[11], acc[6]);
   }
 }
 
@@ -316,7 +464,7 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
     if (descs[mid].mb_begin <= g) lo = mid;
     else hi = mid - 1;
   }
-  const AvcDesc& d = descs[lo];
+  const AvcDesc d = descs[lo];
   const int mb = g - d.mb_begin, W = d.wmbs, x = mb % W, row = mb / W;
   const MbRec q = rec(d, mb);
   AvcDbkInfo info{};
@@ -376,7 +524,7 @@ __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
 __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __restrict__ descs) {
   __shared__ Sync sync;
   __shared__ DbkWave lds[kWaves];
-  const AvcDesc& d = descs[blockIdx.x];
+  const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, pitch = W * 16;
   sync_init(sync, H);
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
@@ -384,45 +532,62 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
+  u64 acc[5] = {0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
   for (int row = wave; row < H; row += kWaves) {
     bool carry = false;
     for (int x = 0; x < W; ++x) {
       const int mb = row * W + x;
+      const u64 t0 = d.prof ? clock64() : 0;
       if (row > 0) wait_row(sync, row - 1, u32(x + 2 < W ? x + 2 : W), d.err);
+      const u64 t1 = d.prof ? clock64() : 0;
       const int x0 = x * 16, y0 = row * 16;
-      // ---- batch: filter inputs, MB samples, left columns, top rows (luma + chroma)
-      if (lane < 12) reinterpret_cast<u32*>(&L.info)[lane] = reinterpret_cast<const u32*>(&infos[mb])[lane];
-      {
-        const int ry = lane >> 2, rw = (lane & 3) * 4;
-        const u32 w = *reinterpret_cast<const u32*>(Y + size_t(y0 + ry) * pitch + x0 + rw);
-        for (int b = 0; b < 4; ++b) L.y[(ry + 4) * 20 + 4 + rw + b] = u8(w >> (8 * b));
+      // ---- batch: every global load first (filter inputs, MB samples, left columns, top rows),
+      // then the LDS stores — one memory round trip per MB
+      const int ry = lane >> 2, rw = (lane & 3) * 4;
+      u32 vinfo = 0;
+      if (lane < 12) vinfo = reinterpret_cast<const u32*>(&infos[mb])[lane];
+      const u32 vmb = *reinterpret_cast<const u32*>(Y + size_t(y0 + ry) * pitch + x0 + rw);
+      u32 v2 = 0, v3 = 0;
+      if (lane < 16) {  // luma left columns -4..-1 of row `lane`
+        if (x > 0 && !carry) v2 = *reinterpret_cast<const u32*>(Y + size_t(y0 + lane) * pitch + x0 - 4);
+      } else if (lane < 32) {  // luma top rows -4..-1
+        const int k = lane - 16;
+        if (row > 0) v2 = *reinterpret_cast<const u32*>(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4);
+      } else {  // chroma MB: 8 rows x 16 bytes NV12
+        const int k = lane - 32;
+        v2 = *reinterpret_cast<const u32*>(UV + size_t(row * 8 + (k >> 2)) * pitch + (x * 8 + (k & 3) * 2) * 2);
       }
-      if (lane < 16) {  // left columns -4..-1 of row `lane`
+      if (lane >= 16 && lane < 24) {  // chroma left 2 columns of row `lane - 16`
+        if (x > 0 && !carry) v3 = *reinterpret_cast<const u32*>(UV + size_t(row * 8 + lane - 16) * pitch + (x * 8 - 2) * 2);
+      } else if (lane >= 24 && lane < 32) {  // chroma top 2 rows
+        const int k = lane - 24;
+        if (row > 0) v3 = *reinterpret_cast<const u32*>(UV + size_t(row * 8 - 2 + (k >> 2)) * pitch + (x * 8 + (k & 3) * 2) * 2);
+      }
+      // ---- LDS stores
+      if (lane < 12) reinterpret_cast<u32*>(&L.info)[lane] = vinfo;
+      for (int b = 0; b < 4; ++b) L.y[(ry + 4) * 20 + 4 + rw + b] = u8(vmb >> (8 * b));
+      if (lane < 16) {
         if (x > 0) {
-          u32 lw;
+          u32 lw = v2;
           if (carry) {
             lw = 0;
             for (int b = 0; b < 4; ++b) lw |= u32(L.carry[lane * 4 + b]) << (8 * b);
-          } else {
-            lw = *reinterpret_cast<const u32*>(Y + size_t(y0 + lane) * pitch + x0 - 4);
           }
           for (int b = 0; b < 4; ++b) L.y[(lane + 4) * 20 + b] = u8(lw >> (8 * b));
         }
-      } else if (lane < 32) {  // top rows -4..-1
+      } else if (lane < 32) {
         if (row > 0) {
           const int k = lane - 16, tr = k >> 2, tw = (k & 3) * 4;
-          const u32 tw32 = *reinterpret_cast<const u32*>(Y + size_t(y0 - 4 + tr) * pitch + x0 + tw);
-          for (int b = 0; b < 4; ++b) L.y[tr * 20 + 4 + tw + b] = u8(tw32 >> (8 * b));
+          for (int b = 0; b < 4; ++b) L.y[tr * 20 + 4 + tw + b] = u8(v2 >> (8 * b));
         }
-      } else {  // chroma MB: 8 rows x 16 bytes NV12
+      } else {
         const int k = lane - 32, cyr = k >> 2, cb = (k & 3) * 2;
-        const u32 cw = *reinterpret_cast<const u32*>(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cb) * 2);
         for (int b = 0; b < 2; ++b) {
-          L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(cw >> (16 * b));
-          L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(cw >> (16 * b + 8));
+          L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(v2 >> (16 * b));
+          L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(v2 >> (16 * b + 8));
         }
       }
-      if (lane >= 16 && lane < 24 && x > 0) {  // chroma left 2 columns of row `lane - 16`
+      if (lane >= 16 && lane < 24 && x > 0) {
         const int k = lane - 16;
         u8 v[4];
         if (carry) {
@@ -431,22 +596,22 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
           v[2] = L.ccarry[0][k * 2 + 1];
           v[3] = L.ccarry[1][k * 2 + 1];
         } else {
-          const u32 cw = *reinterpret_cast<const u32*>(UV + size_t(row * 8 + k) * pitch + (x * 8 - 2) * 2);
-          for (int b = 0; b < 4; ++b) v[b] = u8(cw >> (8 * b));
+          for (int b = 0; b < 4; ++b) v[b] = u8(v3 >> (8 * b));
         }
         L.c[0][(k + 2) * 10 + 0] = v[0];
         L.c[1][(k + 2) * 10 + 0] = v[1];
         L.c[0][(k + 2) * 10 + 1] = v[2];
         L.c[1][(k + 2) * 10 + 1] = v[3];
-      } else if (lane >= 24 && lane < 32 && row > 0) {  // chroma top 2 rows
+      } else if (lane >= 24 && lane < 32 && row > 0) {
         const int k = lane - 24, tr = k >> 2, cb = (k & 3) * 2;
-        const u32 cw = *reinterpret_cast<const u32*>(UV + size_t(row * 8 - 2 + tr) * pitch + (x * 8 + cb) * 2);
         for (int b = 0; b < 2; ++b) {
-          L.c[0][tr * 10 + 2 + cb + b] = u8(cw >> (16 * b));
-          L.c[1][tr * 10 + 2 + cb + b] = u8(cw >> (16 * b + 8));
+          L.c[0][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b));
+          L.c[1][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b + 8));
         }
       }
       wave_sync();
+      const u64 t2 = d.prof ? clock64() : 0;
+      u64 t3 = t2;
       if (L.info.any) {
         // ---- filter: vertical edges then horizontal edges (luma lanes 0-15, chroma 16-31)
         for (int dir = 0; dir < 2; ++dir) {
@@ -471,6 +636,7 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
             wave_sync();
           }
         }
+        t3 = d.prof ? clock64() : 0;
         // ---- write back (MB, left columns, top rows)
         const bool left = (L.info.bs[0] & 0xFFFFu) != 0;   // dir 0, edge 0 nibbles
         const bool top = (L.info.bs[2] & 0xFFFFu) != 0;    // dir 1, edge 0 nibbles
@@ -525,8 +691,18 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
       wave_sync();
       carry = true;
       publish_row(sync, row, u32(x + 1));
+      if (d.prof) {
+        const u64 t4 = clock64();
+        acc[0] += t1 - t0;
+        acc[1] += t2 - t1;
+        acc[2] += t3 - t2;
+        acc[3] += t4 - t3;
+        acc[4] += 1;
+      }
     }
   }
+  if (d.prof && lane == 0)
+    for (int k = 0; k < 5; ++k) atomicAdd(&d.prof[6 + k], acc[k]);
 }
 
 }  // namespace

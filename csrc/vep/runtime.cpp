@@ -282,6 +282,11 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       VEP_HIP(hipEventCreate(&st.e1));
     }
     hostmem::enable_pool();  // AUs finalised from here on are GPU-readable in place
+    const char* ap = std::getenv("VEP_AVC_PROF");
+    if (ap && ap[0] == '1') {
+      avc_prof_ = static_cast<u64*>(dev_.alloc(gpu::kAvcProfSlots * sizeof(u64)));
+      VEP_HIP(hipMemset(avc_prof_, 0, gpu::kAvcProfSlots * sizeof(u64)));
+    }
     const char* dr = std::getenv("VEP_DIRECT_READS");
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
@@ -339,6 +344,7 @@ Worker::~Worker() {
     if (st.e1) (void)hipEventDestroy(st.e1);
   }
   dev_.free_pinned(h_serve_);
+  dev_.free(avc_prof_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
   if (serve_stream_) (void)hipStreamDestroy(serve_stream_);
@@ -976,6 +982,7 @@ void Worker::launch_gpu(Stage& st) {
       g.pad = 0;
       g.err = const_cast<u32*>(st.err_dev) + a.job;
       g.dbk = st.d + a.off_dbk;
+      g.prof = avc_prof_;
       mbs += a.p->nmbs();
     }
   }
@@ -1171,6 +1178,14 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
     throw;
   }
   st.active = true;
+}
+
+std::vector<u64> Worker::avc_profile() {
+  std::vector<u64> v(gpu::kAvcProfSlots, 0);
+  if (!avc_prof_) return v;
+  complete_all();
+  VEP_HIP(hipMemcpy(v.data(), avc_prof_, v.size() * sizeof(u64), hipMemcpyDeviceToHost));
+  return v;
 }
 
 void Worker::run_batch(std::vector<DecodeJob>& jobs) {

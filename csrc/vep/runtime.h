@@ -249,6 +249,8 @@ class Worker {
   u64 bytes_staged() const { return pinned_bytes_staged_; }
   u64 frames() const { return frames_.load(); }
   double gpu_ms_total() const { return gpu_ms_total_; }
+  // clock64() phase accumulators of the wavefront kernels (VEP_AVC_PROF=1; gpu::kAvcProfSlots)
+  std::vector<u64> avc_profile();
 
  private:
   struct Stage {  // one pinned + device staging pair and the batch that uses it
@@ -308,6 +310,7 @@ class Worker {
   double gpu_ms_total_ = 0;
   u64 pinned_bytes_inplace_ = 0, pinned_bytes_staged_ = 0;
   bool direct_reads_ = false;
+  u64* avc_prof_ = nullptr;
 
  public:
   bool direct_reads() const { return direct_reads_; }
