@@ -61,6 +61,8 @@ def parse_args():
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
     ap.add_argument("--cache-gops", type=int, default=1,
                     help="distinct pre-encoded GOPs replayed per camera (working-set size)")
+    ap.add_argument("--lanes", type=int, default=0,
+                    help="independent GPU pipelines per worker (0 = runtime default)")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--consumer-format", choices=["nv12", "bgr"], default="nv12",
@@ -103,7 +105,7 @@ def main():
     S = a.letterbox
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
                         max_cameras=cams, pack_threads=a.pack_threads,
-                        letterbox_format=1 if a.consumer_format == "nv12" else 0)
+                        letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes)
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
@@ -250,6 +252,7 @@ def main():
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "gpu_lanes": worker.lanes,
             "payload_path": ("decode kernel reads slice bytes from pinned host memory over PCIe"
                              if getattr(worker, "direct_reads", False) else
                              "gather kernel pulls slice bytes into HBM, decode reads HBM"),

@@ -266,20 +266,39 @@ bool Camera::make_job(const AuPtr& au, DecodeJob& job) {
 
 // ------------------------------------------------------------------------------------ Worker
 
+// Lanes per GPU worker (WorkerOptions::lanes): lane streams + the serving stream fit the
+// default 4 hardware queues per process.
+constexpr int kDefaultLanes = 3;
+
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (dev_.gpu()) {
     dev_.bind();
-    VEP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-    // The copy stream's gather kernel is PCIe-latency bound and must keep its waves resident
-    // while the previous batch's decode kernel floods the CUs: give it dispatch priority.
-    int prio_lo = 0, prio_hi = 0;
-    VEP_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-    VEP_HIP(hipStreamCreateWithPriority(&copy_stream_, hipStreamNonBlocking, prio_hi));
+    int nl = opt_.lanes;
+    if (nl <= 0) {
+      const char* le = std::getenv("VEP_LANES");
+      nl = le ? std::atoi(le) : kDefaultLanes;
+    }
+    lanes_.resize(size_t(std::clamp(nl, 1, 8)));
+    // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES): create only the
+    // ones in use, serving first so its D2H never queues behind a lane's kernels.
     VEP_HIP(hipStreamCreateWithFlags(&serve_stream_, hipStreamNonBlocking));
-    for (Stage& st : stage_) {
-      VEP_HIP(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
-      VEP_HIP(hipEventCreate(&st.e0));
-      VEP_HIP(hipEventCreate(&st.e1));
+    VEP_HIP(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+    if (lanes_.size() == 1) {
+      // The copy stream's gather kernel is PCIe-latency bound and must keep its waves resident
+      // while the previous batch's decode kernel floods the CUs: give it dispatch priority.
+      int prio_lo = 0, prio_hi = 0;
+      VEP_HIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+      VEP_HIP(hipStreamCreateWithPriority(&copy_stream_, hipStreamNonBlocking, prio_hi));
+    }
+    for (size_t g = 0; g < lanes_.size(); ++g) {
+      Lane& ln = lanes_[g];
+      if (g == 0) ln.stream = stream_;
+      else VEP_HIP(hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
+      for (Stage& st : ln.stage) {
+        VEP_HIP(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
+        VEP_HIP(hipEventCreate(&st.e0));
+        VEP_HIP(hipEventCreate(&st.e1));
+      }
     }
     hostmem::enable_pool();  // AUs finalised from here on are GPU-readable in place
     const char* ap = std::getenv("VEP_AVC_PROF");
@@ -334,14 +353,17 @@ Worker::~Worker() {
     dev_.free(cons_hwc_);
     dev_.free(cons_chw_);
   }
-  for (Stage& st : stage_) {
-    dev_.free_pinned(st.err);
-    if (st.h) hostmem::unregister_range(st.h);
-    dev_.free(st.d);
-    dev_.free_pinned(st.h);
-    if (st.copied) (void)hipEventDestroy(st.copied);
-    if (st.e0) (void)hipEventDestroy(st.e0);
-    if (st.e1) (void)hipEventDestroy(st.e1);
+  for (Lane& ln : lanes_) {
+    for (Stage& st : ln.stage) {
+      dev_.free_pinned(st.err);
+      if (st.h) hostmem::unregister_range(st.h);
+      dev_.free(st.d);
+      dev_.free_pinned(st.h);
+      if (st.copied) (void)hipEventDestroy(st.copied);
+      if (st.e0) (void)hipEventDestroy(st.e0);
+      if (st.e1) (void)hipEventDestroy(st.e1);
+    }
+    if (ln.stream && ln.stream != stream_) (void)hipStreamDestroy(ln.stream);
   }
   dev_.free_pinned(h_serve_);
   dev_.free(avc_prof_);
@@ -536,6 +558,8 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots) {
     s.uv = static_cast<u8*>(dev_.alloc(ysz / 2));
     VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
     VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
+    // the camera's lane may be another stream: the fill must land before its first kernel
+    if (lanes_.size() > 1) VEP_HIP(hipStreamSynchronize(stream_));
   } else {
     s.host.assign(size_t(s.slots), HostSurface{});
     for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16);
@@ -732,7 +756,8 @@ constexpr size_t kPackChunk = size_t(1) << 20;  // bytes per copy task
 
 }  // namespace
 
-void Worker::launch_gpu(Stage& st) {
+void Worker::launch_gpu(Lane& ln, Stage& st) {
+  const hipStream_t cs = ln.stream;
   std::vector<DecodeJob>& jobs = st.jobs;
   const int n = int(jobs.size());
   // Slice bytes stay in host memory: pinned AU blocks as received (hostmem.h), or this stage's
@@ -988,13 +1013,24 @@ void Worker::launch_gpu(Stage& st) {
   }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
-  VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, copy_stream_));
-  if (!direct)
-    gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
-                       int(nchunks), copy_stream_);
-  VEP_HIP(hipEventRecord(st.copied, copy_stream_));
-  VEP_HIP(hipStreamWaitEvent(stream_, st.copied, 0));
-  VEP_HIP(hipEventRecord(st.e0, stream_));
+  // With several lanes the copy goes on the lane's own stream instead: it then waits for the
+  // lane's previous kernels, while the other lanes keep the GPU busy, and no lane ever waits
+  // on a queue another lane shares.
+  if (lanes_.size() > 1) {
+    VEP_HIP(hipEventRecord(st.e0, cs));
+    VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, cs));
+    if (!direct)
+      gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
+                         int(nchunks), cs);
+  } else {
+    VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, copy_stream_));
+    if (!direct)
+      gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
+                         int(nchunks), copy_stream_);
+    VEP_HIP(hipEventRecord(st.copied, copy_stream_));
+    VEP_HIP(hipStreamWaitEvent(cs, st.copied, 0));
+    VEP_HIP(hipEventRecord(st.e0, cs));
+  }
   for (int r = 0; r < rounds; ++r) {
     const auto* ad = reinterpret_cast<const gpu::AvcDesc*>(st.d + off_round[size_t(r)]);
     const int np = int(round_pics[size_t(r)].size());
@@ -1005,15 +1041,15 @@ void Worker::launch_gpu(Stage& st) {
       intra |= apics[size_t(k)].p->intra_mbs > 0;
       dbk |= apics[size_t(k)].p->deblock;
     }
-    gpu::launch_avc_inter(ad, np, mbs, stream_);
-    if (intra) gpu::launch_avc_intra(ad, np, stream_);
+    gpu::launch_avc_inter(ad, np, mbs, cs);
+    if (intra) gpu::launch_avc_intra(ad, np, cs);
     if (dbk) {
-      gpu::launch_avc_bs(ad, np, mbs, stream_);
-      gpu::launch_avc_deblock(ad, np, stream_);
+      gpu::launch_avc_bs(ad, np, mbs, cs);
+      gpu::launch_avc_deblock(ad, np, cs);
     }
   }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), n, tiles,
-                             stream_);
+                             cs);
   if (opt_.letterbox_size > 0) {
     gpu::LetterboxParams p{};
     p.size = opt_.letterbox_size;
@@ -1025,9 +1061,9 @@ void Worker::launch_gpu(Stage& st) {
     p.pad_value = 114;
     p.format = opt_.letterbox_format;
     gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(st.d + off_lb), n, p,
-                          stream_);
+                          cs);
   }
-  VEP_HIP(hipEventRecord(st.e1, stream_));
+  VEP_HIP(hipEventRecord(st.e1, cs));
   timers.enqueue += double(mono_us() - t_enq0);
 }
 
@@ -1119,7 +1155,13 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
   batches_.fetch_add(1);
 }
 
-void Worker::complete(Stage& st) {
+double Worker::gpu_ms_total() const {
+  double m = 0;
+  for (const Lane& ln : lanes_) m = std::max(m, ln.gpu_ms);
+  return m;
+}
+
+void Worker::complete(Lane& ln, Stage& st) {
   if (!st.active) return;
   st.active = false;
   const i64 t0 = mono_us();
@@ -1129,16 +1171,18 @@ void Worker::complete(Stage& st) {
   }
   timers.wait += double(mono_us() - t0);
   float ms = 0;
-  if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) gpu_ms_total_ += ms;
+  if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) ln.gpu_ms += ms;
   publish(st.jobs, st.slots, st.err);
   st.jobs.clear();
   st.slots.clear();
 }
 
 void Worker::complete_locked() {
-  // oldest first: next_stage_ names the stage that will be reused next, i.e. the older batch
-  complete(stage_[next_stage_]);
-  complete(stage_[next_stage_ ^ 1]);
+  // oldest first: Lane::next names the stage that will be reused next, i.e. the older batch
+  for (Lane& ln : lanes_) {
+    complete(ln, ln.stage[ln.next]);
+    complete(ln, ln.stage[ln.next ^ 1]);
+  }
 }
 
 void Worker::complete_all() {
@@ -1164,20 +1208,32 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
     jobs.clear();
     return;
   }
-  Stage& st = stage_[next_stage_];
-  next_stage_ ^= 1;
-  complete(st);  // the batch from two launches ago: its staging buffer is reused now
-  st.jobs.swap(jobs);
-  st.slots.swap(slots);
-  jobs.clear();
-  try {
-    launch_gpu(st);
-  } catch (...) {
-    st.jobs.clear();
-    st.slots.clear();
-    throw;
+  const size_t nl = lanes_.size();
+  std::vector<std::vector<DecodeJob>> lj(nl);
+  std::vector<std::vector<int>> ls(nl);
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    const size_t g = size_t(jobs[i].cam) % nl;  // a camera's surfaces are ordered by its lane
+    lj[g].push_back(std::move(jobs[i]));
+    ls[g].push_back(slots[i]);
   }
-  st.active = true;
+  jobs.clear();
+  for (size_t g = 0; g < nl; ++g) {
+    if (lj[g].empty()) continue;
+    Lane& ln = lanes_[g];
+    Stage& st = ln.stage[ln.next];
+    ln.next ^= 1;
+    complete(ln, st);  // this lane's batch from two launches ago: its staging is reused now
+    st.jobs.swap(lj[g]);
+    st.slots.swap(ls[g]);
+    try {
+      launch_gpu(ln, st);
+    } catch (...) {
+      st.jobs.clear();
+      st.slots.clear();
+      throw;
+    }
+    st.active = true;
+  }
 }
 
 std::vector<u64> Worker::avc_profile() {

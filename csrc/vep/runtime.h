@@ -200,6 +200,10 @@ struct WorkerOptions {
   int max_cameras = 256;
   int pack_threads = 4;       // host threads packing MB payloads into pinned staging
   bool direct_reads = true;   // decode kernel reads slice bytes from host memory (else gather)
+  // Independent GPU pipelines ("lanes"): camera c always runs on lane c % lanes, each lane with
+  // its own stream and staging. A keyframe's long intra wavefront then delays only its lane's
+  // cameras instead of the whole tick. 0 = VEP_LANES or the default.
+  int lanes = 0;
 };
 
 class Worker {
@@ -242,13 +246,15 @@ class Worker {
   void set_consumer_buffers(u8* hwc, void* chw, int rows);
   u8* consumer_hwc() const { return cons_hwc_; }
   void* consumer_chw() const { return cons_chw_; }
-  hipStream_t compute_stream() const { return stream_; }
+  hipStream_t compute_stream() const { return stream_; }  // lane 0
+  int lanes() const { return int(lanes_.size()); }
   u64 batches() const { return batches_.load(); }
   // slice bytes the GPU read in place from pinned AU blocks vs. staged by a host memcpy
   u64 bytes_inplace() const { return pinned_bytes_inplace_; }
   u64 bytes_staged() const { return pinned_bytes_staged_; }
   u64 frames() const { return frames_.load(); }
-  double gpu_ms_total() const { return gpu_ms_total_; }
+  // GPU time of the batches (first event to last, per lane; the busiest lane's total)
+  double gpu_ms_total() const;
   // clock64() phase accumulators of the wavefront kernels (VEP_AVC_PROF=1; gpu::kAvcProfSlots)
   std::vector<u64> avc_profile();
 
@@ -267,22 +273,26 @@ class Worker {
   };
   void loop();
   void ensure_surface(Camera& c, const PictureInfo& pi, int slots);
-  void launch_avc(Stage& st, size_t& need, size_t off);
+  struct Lane {
+    hipStream_t stream = nullptr;  // lane 0 uses Worker::stream_
+    Stage stage[2];
+    int next = 0;                  // the stage reused next (the older in-flight batch)
+    double gpu_ms = 0;             // cumulative batch time on this lane
+  };
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
-  void launch_gpu(Stage& st);
+  void launch_gpu(Lane& ln, Stage& st);
   void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err);
   // err[i] != 0: job i failed its speculative-header check (dropped, camera waits for the
   // next keyframe)
   void publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, const u32* err = nullptr);
-  void complete(Stage& st);
+  void complete(Lane& ln, Stage& st);
   void complete_locked();
   WorkerOptions opt_;
   Device dev_;
   hipStream_t stream_ = nullptr, copy_stream_ = nullptr, serve_stream_ = nullptr;
   mutable std::mutex cams_mu_;
   std::vector<std::shared_ptr<Camera>> cams_;
-  Stage stage_[2];
-  int next_stage_ = 0;
+  std::vector<Lane> lanes_;
   std::unique_ptr<ThreadPool> pack_pool_;
 
  public:
@@ -307,7 +317,6 @@ class Worker {
   std::thread th_;
   std::mutex launch_mu_;
   std::atomic<u64> batches_{0}, frames_{0};
-  double gpu_ms_total_ = 0;
   u64 pinned_bytes_inplace_ = 0, pinned_bytes_staged_ = 0;
   bool direct_reads_ = false;
   u64* avc_prof_ = nullptr;
