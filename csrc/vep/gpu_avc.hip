@@ -516,6 +516,15 @@ struct DbkWave {
   u8 ccarry[2][8 * 2];
 };
 
+// A wave filters two adjacent MB rows at once: lanes 0-31 row 2p, lanes 32-63 row 2p+1, the
+// second trailing by kDbkLag columns. Row 2p+1 at column x needs row 2p finished up to x+1,
+// which this wave completed in an earlier iteration, so only the first row ever waits on
+// another wave. 32 rows in flight per picture instead of 16, and all 64 lanes filter.
+constexpr int kDbkLag = 3;
+
+__device__ inline void st4(u8* p, u32 v) { *reinterpret_cast<u32*>(p) = v; }
+__device__ inline u32 ld4(const u8* p) { return *reinterpret_cast<const u32*>(p); }
+
 __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
   const int i = dir * 16 + e * 4 + sg;
   return int((in.bs[i >> 3] >> (4 * (i & 7))) & 15u);
@@ -523,114 +532,116 @@ __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
 
 __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __restrict__ descs) {
   __shared__ Sync sync;
-  __shared__ DbkWave lds[kWaves];
+  __shared__ DbkWave lds[kWaves][2];
   const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, pitch = W * 16;
   sync_init(sync, H);
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
-  DbkWave& L = lds[wave];
+  const int h = lane >> 5, l = lane & 31;  // row of the pair / lane within the half-wave
+  DbkWave& L = lds[wave][h];
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
   u64 acc[5] = {0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
-  for (int row = wave; row < H; row += kWaves) {
+  for (int r0 = 2 * wave; r0 < H; r0 += 2 * kWaves) {
+    const int row = r0 + h;
     bool carry = false;
-    for (int x = 0; x < W; ++x) {
-      const int mb = row * W + x;
+    for (int i = 0; i < W + kDbkLag; ++i) {
+      const int x = i - h * kDbkLag;
+      const bool act = row < H && x >= 0 && x < W;
       const u64 t0 = d.prof ? clock64() : 0;
-      if (row > 0) wait_row(sync, row - 1, u32(x + 2 < W ? x + 2 : W), d.err);
+      if (r0 > 0 && i < W) wait_row(sync, r0 - 1, u32(i + 2 < W ? i + 2 : W), d.err);
       const u64 t1 = d.prof ? clock64() : 0;
       const int x0 = x * 16, y0 = row * 16;
+      const size_t mb = size_t(row) * W + x;
       // ---- batch: every global load first (filter inputs, MB samples, left columns, top rows),
       // then the LDS stores — one memory round trip per MB
-      const int ry = lane >> 2, rw = (lane & 3) * 4;
-      u32 vinfo = 0;
-      if (lane < 12) vinfo = reinterpret_cast<const u32*>(&infos[mb])[lane];
-      const u32 vmb = *reinterpret_cast<const u32*>(Y + size_t(y0 + ry) * pitch + x0 + rw);
-      u32 v2 = 0, v3 = 0;
-      if (lane < 16) {  // luma left columns -4..-1 of row `lane`
-        if (x > 0 && !carry) v2 = *reinterpret_cast<const u32*>(Y + size_t(y0 + lane) * pitch + x0 - 4);
-      } else if (lane < 32) {  // luma top rows -4..-1
-        const int k = lane - 16;
-        if (row > 0) v2 = *reinterpret_cast<const u32*>(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4);
-      } else {  // chroma MB: 8 rows x 16 bytes NV12
-        const int k = lane - 32;
-        v2 = *reinterpret_cast<const u32*>(UV + size_t(row * 8 + (k >> 2)) * pitch + (x * 8 + (k & 3) * 2) * 2);
-      }
-      if (lane >= 16 && lane < 24) {  // chroma left 2 columns of row `lane - 16`
-        if (x > 0 && !carry) v3 = *reinterpret_cast<const u32*>(UV + size_t(row * 8 + lane - 16) * pitch + (x * 8 - 2) * 2);
-      } else if (lane >= 24 && lane < 32) {  // chroma top 2 rows
-        const int k = lane - 24;
-        if (row > 0) v3 = *reinterpret_cast<const u32*>(UV + size_t(row * 8 - 2 + (k >> 2)) * pitch + (x * 8 + (k & 3) * 2) * 2);
-      }
-      // ---- LDS stores
-      if (lane < 12) reinterpret_cast<u32*>(&L.info)[lane] = vinfo;
-      for (int b = 0; b < 4; ++b) L.y[(ry + 4) * 20 + 4 + rw + b] = u8(vmb >> (8 * b));
-      if (lane < 16) {
-        if (x > 0) {
-          u32 lw = v2;
-          if (carry) {
-            lw = 0;
-            for (int b = 0; b < 4; ++b) lw |= u32(L.carry[lane * 4 + b]) << (8 * b);
+      u32 vinfo = 0, vm0 = 0, vm1 = 0, v2 = 0, vc = 0, v3 = 0;
+      if (act) {
+        if (l < 12) vinfo = reinterpret_cast<const u32*>(&infos[mb])[l];
+        const u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
+        vm0 = ld4(ym);                       // MB rows 0..7
+        vm1 = ld4(ym + size_t(8) * pitch);   // MB rows 8..15
+        if (l < 16) {  // luma left columns -4..-1 of MB row l
+          if (x > 0 && !carry) v2 = ld4(Y + size_t(y0 + l) * pitch + x0 - 4);
+        } else if (row > 0) {  // luma top rows -4..-1
+          const int k = l - 16;
+          v2 = ld4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4);
+        }
+        vc = ld4(UV + size_t(row * 8 + (l >> 2)) * pitch + x0 + (l & 3) * 4);  // NV12 8 x 16 B
+        if (l < 8) {  // chroma left 2 columns (4 B NV12) of chroma row l
+          if (x > 0 && !carry) v3 = ld4(UV + size_t(row * 8 + l) * pitch + x0 - 4);
+        } else if (l < 16 && row > 0) {  // chroma top 2 rows
+          const int k = l - 8;
+          v3 = ld4(UV + size_t(row * 8 - 2 + (k >> 2)) * pitch + x0 + (k & 3) * 4);
+        }
+        // ---- LDS stores
+        if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = vinfo;
+        st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], vm0);
+        st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], vm1);
+        if (l < 16) {
+          if (x > 0) st4(&L.y[(l + 4) * 20], carry ? ld4(&L.carry[l * 4]) : v2);
+        } else if (row > 0) {
+          const int k = l - 16;
+          st4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4], v2);
+        }
+        {
+          const int cyr = l >> 2, cb = (l & 3) * 2;
+          for (int b = 0; b < 2; ++b) {
+            L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(vc >> (16 * b));
+            L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(vc >> (16 * b + 8));
           }
-          for (int b = 0; b < 4; ++b) L.y[(lane + 4) * 20 + b] = u8(lw >> (8 * b));
         }
-      } else if (lane < 32) {
-        if (row > 0) {
-          const int k = lane - 16, tr = k >> 2, tw = (k & 3) * 4;
-          for (int b = 0; b < 4; ++b) L.y[tr * 20 + 4 + tw + b] = u8(v2 >> (8 * b));
-        }
-      } else {
-        const int k = lane - 32, cyr = k >> 2, cb = (k & 3) * 2;
-        for (int b = 0; b < 2; ++b) {
-          L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(v2 >> (16 * b));
-          L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(v2 >> (16 * b + 8));
-        }
-      }
-      if (lane >= 16 && lane < 24 && x > 0) {
-        const int k = lane - 16;
-        u8 v[4];
-        if (carry) {
-          v[0] = L.ccarry[0][k * 2];
-          v[1] = L.ccarry[1][k * 2];
-          v[2] = L.ccarry[0][k * 2 + 1];
-          v[3] = L.ccarry[1][k * 2 + 1];
-        } else {
-          for (int b = 0; b < 4; ++b) v[b] = u8(v3 >> (8 * b));
-        }
-        L.c[0][(k + 2) * 10 + 0] = v[0];
-        L.c[1][(k + 2) * 10 + 0] = v[1];
-        L.c[0][(k + 2) * 10 + 1] = v[2];
-        L.c[1][(k + 2) * 10 + 1] = v[3];
-      } else if (lane >= 24 && lane < 32 && row > 0) {
-        const int k = lane - 24, tr = k >> 2, cb = (k & 3) * 2;
-        for (int b = 0; b < 2; ++b) {
-          L.c[0][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b));
-          L.c[1][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b + 8));
+        if (l < 8) {
+          if (x > 0) {
+            u8 v[4];
+            if (carry) {
+              v[0] = L.ccarry[0][l * 2];
+              v[1] = L.ccarry[1][l * 2];
+              v[2] = L.ccarry[0][l * 2 + 1];
+              v[3] = L.ccarry[1][l * 2 + 1];
+            } else {
+              for (int b = 0; b < 4; ++b) v[b] = u8(v3 >> (8 * b));
+            }
+            L.c[0][(l + 2) * 10 + 0] = v[0];
+            L.c[1][(l + 2) * 10 + 0] = v[1];
+            L.c[0][(l + 2) * 10 + 1] = v[2];
+            L.c[1][(l + 2) * 10 + 1] = v[3];
+          }
+        } else if (l < 16 && row > 0) {
+          const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+          for (int b = 0; b < 2; ++b) {
+            L.c[0][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b));
+            L.c[1][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b + 8));
+          }
         }
       }
       wave_sync();
       const u64 t2 = d.prof ? clock64() : 0;
       u64 t3 = t2;
-      if (L.info.any) {
-        // ---- filter: vertical edges then horizontal edges (luma lanes 0-15, chroma 16-31)
+      const bool any = act && L.info.any;
+      if (__ballot(any)) {
+        // ---- filter: vertical edges then horizontal edges (per half: luma lanes 0-15,
+        // chroma 16-31)
         for (int dir = 0; dir < 2; ++dir) {
           for (int e = 0; e < 4; ++e) {
             const int pk = e > 0 ? 2 : dir;  // edge params: left / top / internal
-            if (lane < 16) {
-              const int bs = bs_of(L.info, dir, e, lane >> 2);
-              if (bs) {
-                const avc::EdgeParams ep{L.info.alpha[pk], L.info.beta[pk], L.info.ia[pk]};
-                if (dir == 0) avc::filter_line(&L.y[(4 + lane) * 20 + 4 + 4 * e], 1, bs, ep, false);
-                else avc::filter_line(&L.y[(4 + 4 * e) * 20 + 4 + lane], 20, bs, ep, false);
-              }
-            } else if (lane < 32 && !(e & 1)) {
-              const int c = (lane - 16) >> 3, k = (lane - 16) & 7;
-              const int bs = bs_of(L.info, dir, e, k >> 1);
-              if (bs) {
-                const avc::EdgeParams ep{L.info.alpha[3 + pk], L.info.beta[3 + pk], L.info.ia[3 + pk]};
-                if (dir == 0) avc::filter_line(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, ep, true);
-                else avc::filter_line(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, ep, true);
+            if (any) {
+              if (l < 16) {
+                const int bs = bs_of(L.info, dir, e, l >> 2);
+                if (bs) {
+                  const avc::EdgeParams ep{L.info.alpha[pk], L.info.beta[pk], L.info.ia[pk]};
+                  if (dir == 0) avc::filter_line(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, ep, false);
+                  else avc::filter_line(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, ep, false);
+                }
+              } else if (!(e & 1)) {
+                const int c = (l - 16) >> 3, k = (l - 16) & 7;
+                const int bs = bs_of(L.info, dir, e, k >> 1);
+                if (bs) {
+                  const avc::EdgeParams ep{L.info.alpha[3 + pk], L.info.beta[3 + pk], L.info.ia[3 + pk]};
+                  if (dir == 0) avc::filter_line(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, ep, true);
+                  else avc::filter_line(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, ep, true);
+                }
               }
             }
             wave_sync();
@@ -638,66 +649,66 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
         }
         t3 = d.prof ? clock64() : 0;
         // ---- write back (MB, left columns, top rows)
-        const bool left = (L.info.bs[0] & 0xFFFFu) != 0;   // dir 0, edge 0 nibbles
-        const bool top = (L.info.bs[2] & 0xFFFFu) != 0;    // dir 1, edge 0 nibbles
-        {
-          const int ry = lane >> 2, rw = (lane & 3) * 4;
-          u32 w = 0;
-          for (int b = 0; b < 4; ++b) w |= u32(L.y[(ry + 4) * 20 + 4 + rw + b]) << (8 * b);
-          *reinterpret_cast<u32*>(Y + size_t(y0 + ry) * pitch + x0 + rw) = w;
+        if (any) {
+          const bool left = (L.info.bs[0] & 0xFFFFu) != 0;  // dir 0, edge 0 nibbles
+          const bool top = (L.info.bs[2] & 0xFFFFu) != 0;   // dir 1, edge 0 nibbles
+          u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
+          st4(ym, ld4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4]));
+          st4(ym + size_t(8) * pitch, ld4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4]));
+          if (l < 16) {
+            if (left) st4(Y + size_t(y0 + l) * pitch + x0 - 4, ld4(&L.y[(l + 4) * 20]));
+          } else if (top) {
+            const int k = l - 16;
+            st4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4,
+                ld4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4]));
+          }
+          {
+            const int cyr = l >> 2, cb = (l & 3) * 2;
+            u32 cw = 0;
+            for (int b = 0; b < 2; ++b)
+              cw |= (u32(L.c[0][(cyr + 2) * 10 + 2 + cb + b]) | u32(L.c[1][(cyr + 2) * 10 + 2 + cb + b]) << 8)
+                    << (16 * b);
+            st4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
+          }
+          if (l < 8) {
+            if (left) {
+              const u32 cw = u32(L.c[0][(l + 2) * 10]) | u32(L.c[1][(l + 2) * 10]) << 8 |
+                             u32(L.c[0][(l + 2) * 10 + 1]) << 16 | u32(L.c[1][(l + 2) * 10 + 1]) << 24;
+              st4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
+            }
+          } else if (l < 16 && top) {
+            const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+            u32 cw = 0;
+            for (int b = 0; b < 2; ++b)
+              cw |= (u32(L.c[0][tr * 10 + 2 + cb + b]) | u32(L.c[1][tr * 10 + 2 + cb + b]) << 8) << (16 * b);
+            st4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
+          }
         }
-        if (lane < 16) {
-          if (left) {
-            u32 lw = 0;
-            for (int b = 0; b < 4; ++b) lw |= u32(L.y[(lane + 4) * 20 + b]) << (8 * b);
-            *reinterpret_cast<u32*>(Y + size_t(y0 + lane) * pitch + x0 - 4) = lw;
-          }
-        } else if (lane < 32) {
-          if (top) {
-            const int k = lane - 16, tr = k >> 2, tw = (k & 3) * 4;
-            u32 t32 = 0;
-            for (int b = 0; b < 4; ++b) t32 |= u32(L.y[tr * 20 + 4 + tw + b]) << (8 * b);
-            *reinterpret_cast<u32*>(Y + size_t(y0 - 4 + tr) * pitch + x0 + tw) = t32;
-          }
+      }
+      // carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
+      if (act) {
+        if (l < 16) {
+          st4(&L.carry[l * 4], ld4(&L.y[(l + 4) * 20 + 16]));
         } else {
-          const int k = lane - 32, cyr = k >> 2, cb = (k & 3) * 2;
-          u32 cw = 0;
-          for (int b = 0; b < 2; ++b)
-            cw |= (u32(L.c[0][(cyr + 2) * 10 + 2 + cb + b]) | u32(L.c[1][(cyr + 2) * 10 + 2 + cb + b]) << 8)
-                  << (16 * b);
-          *reinterpret_cast<u32*>(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cb) * 2) = cw;
-        }
-        if (lane >= 16 && lane < 24 && left) {
-          const int k = lane - 16;
-          const u32 cw = u32(L.c[0][(k + 2) * 10]) | u32(L.c[1][(k + 2) * 10]) << 8 |
-                         u32(L.c[0][(k + 2) * 10 + 1]) << 16 | u32(L.c[1][(k + 2) * 10 + 1]) << 24;
-          *reinterpret_cast<u32*>(UV + size_t(row * 8 + k) * pitch + (x * 8 - 2) * 2) = cw;
-        } else if (lane >= 24 && lane < 32 && top) {
-          const int k = lane - 24, tr = k >> 2, cb = (k & 3) * 2;
-          u32 cw = 0;
-          for (int b = 0; b < 2; ++b)
-            cw |= (u32(L.c[0][tr * 10 + 2 + cb + b]) | u32(L.c[1][tr * 10 + 2 + cb + b]) << 8) << (16 * b);
-          *reinterpret_cast<u32*>(UV + size_t(row * 8 - 2 + tr) * pitch + (x * 8 + cb) * 2) = cw;
+          const int c = (l - 16) >> 3, k = (l - 16) & 7;
+          L.ccarry[c][k * 2] = L.c[c][(k + 2) * 10 + 8];
+          L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 10 + 9];
         }
       }
-      // carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one
-      if (lane < 16)
-        for (int b = 0; b < 4; ++b) L.carry[lane * 4 + b] = L.y[(lane + 4) * 20 + 16 + b];
-      if (lane >= 16 && lane < 32) {
-        const int c = (lane - 16) >> 3, k = (lane - 16) & 7;
-        L.ccarry[c][k * 2] = L.c[c][(k + 2) * 10 + 8];
-        L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 10 + 9];
-      }
+      carry = carry || act;
+      // publish both rows: this wave's global stores happen-before the new progress values
+      // (row 2p's stores are also what the second half reads in its next iterations)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (l == 0 && act)
+        __hip_atomic_store(&sync.progress[row], u32(x + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       wave_sync();
-      carry = true;
-      publish_row(sync, row, u32(x + 1));
       if (d.prof) {
         const u64 t4 = clock64();
         acc[0] += t1 - t0;
         acc[1] += t2 - t1;
         acc[2] += t3 - t2;
         acc[3] += t4 - t3;
-        acc[4] += 1;
+        acc[4] += u64(__popcll(__ballot(act) & 0x100000001ull));
       }
     }
   }
