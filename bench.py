@@ -57,7 +57,7 @@ def parse_args():
     ap.add_argument("--noise", type=float, default=8.0, help="static scene texture amplitude")
     ap.add_argument("--temporal-noise", type=float, default=1.0, help="per-frame sensor noise")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
-    ap.add_argument("--threads", type=int, default=12, help="host parse threads per rank")
+    ap.add_argument("--threads", type=int, default=14, help="host parse threads per rank")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
     ap.add_argument("--cache-gops", type=int, default=1,
                     help="distinct pre-encoded GOPs replayed per camera (working-set size)")

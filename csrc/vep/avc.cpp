@@ -252,6 +252,17 @@ void h16(int c[16]) {  // 4x4 Hadamard, in place: f = H c H
 
 i16 sat16(int v) { return i16(v < -32768 ? -32768 : v > 32767 ? 32767 : v); }
 
+// LevelScale4x4 with flat weight matrices (16 * normAdjust4x4), per qP % 6 and raster position.
+struct LevelScaleTable {
+  int v[6][16];
+  LevelScaleTable() {
+    for (int m = 0; m < 6; ++m)
+      for (int p = 0; p < 16; ++p) v[m][p] = 16 * norm_adjust(m, p >> 2, p & 3);
+  }
+};
+const LevelScaleTable kLevelScaleTable;
+const int (&kLevelScale)[6][16] = kLevelScaleTable.v;
+
 }  // namespace
 
 // ------------------------------------------------------------------------- slice header
@@ -682,47 +693,141 @@ class MbDecoder {
     }
   }
 
-  void residual(Bits& br, int mb, MbState& s, MbResidual& res, int cbp_luma, int cbp_chroma, int qp) {
-    MbLevels& lv = lv_;
-    lv.lmask = lv.cmask = lv.dcmask = 0;
-    if (s.kind == kI16x16) {
-      std::memset(lv.dc, 0, sizeof lv.dc);
-      if (read_residual_block(br, nb_.nc_luma(mb, 0), 16, lv.dc)) lv.dcmask |= 1;
-      if (cbp_luma)
-        for (int idx = 0; idx < 16; ++idx) {
-          const int r = blk_to_raster(idx);
-          std::memset(lv.luma[r], 0, sizeof lv.luma[r]);
-          const int tc = read_residual_block(br, nb_.nc_luma(mb, r), 15, lv.luma[r] + 1);
-          s.tc[r] = u8(tc);
-          if (tc) lv.lmask |= u16(1u << r);
-        }
-    } else {
-      for (int idx = 0; idx < 16; ++idx) {
-        if (!((cbp_luma >> (idx >> 2)) & 1)) continue;
-        const int r = blk_to_raster(idx);
-        std::memset(lv.luma[r], 0, sizeof lv.luma[r]);
-        const int tc = read_residual_block(br, nb_.nc_luma(mb, r), 16, lv.luma[r]);
-        s.tc[r] = u8(tc);
-        if (tc) lv.lmask |= u16(1u << r);
+  // nC contexts (§9.2.1) of the current MB: total_coeff of the 4x4 blocks left of and above
+  // every block (luma [(by + 1) * 5 + bx + 1], chroma [c][(by + 1) * 3 + bx + 1]), filled from
+  // the A/B neighbours once and updated as blocks are parsed; kNa = not available.
+  static constexpr u8 kNa = 0xFF;
+  u8 ncl_[25];
+  u8 ncc_[2][9];
+
+  void nc_setup(int mb) {
+    std::memset(ncl_, 0, sizeof ncl_);
+    std::memset(ncc_, 0, sizeof ncc_);
+    const int am = nb_.mb_at(mb, -1, 0), bm = nb_.mb_at(mb, 0, -1);
+    const MbState* a = am >= 0 ? &nb_.at(am) : nullptr;
+    const MbState* b = bm >= 0 ? &nb_.at(bm) : nullptr;
+    for (int k = 0; k < 4; ++k) {
+      ncl_[1 + k] = b ? b->tc[12 + k] : kNa;
+      ncl_[(k + 1) * 5] = a ? a->tc[k * 4 + 3] : kNa;
+    }
+    ncl_[0] = kNa;
+    for (int c = 0; c < 2; ++c) {
+      for (int k = 0; k < 2; ++k) {
+        ncc_[c][1 + k] = b ? b->tcc[c][2 + k] : kNa;
+        ncc_[c][(k + 1) * 3] = a ? a->tcc[c][k * 2 + 1] : kNa;
       }
+      ncc_[c][0] = kNa;
+    }
+  }
+  static int nc_of(u8 na, u8 nb) {
+    if (na != kNa && nb != kNa) return (na + nb + 1) >> 1;
+    if (na != kNa) return na;
+    if (nb != kNa) return nb;
+    return 0;
+  }
+  int ncl(int r) const {
+    const int i = ((r >> 2) + 1) * 5 + (r & 3) + 1;
+    return nc_of(ncl_[i - 1], ncl_[i - 5]);
+  }
+  int ncc(int c, int b) const {
+    const int i = ((b >> 1) + 1) * 3 + (b & 1) + 1;
+    return nc_of(ncc_[c][i - 1], ncc_[c][i - 3]);
+  }
+
+  struct Scale {  // v = (level * ls[pos] * mul + add) >> sh  (§8.5.12.1)
+    const int* ls;
+    int mul, add, sh;
+  };
+
+  // Residual syntax with the scaling (§8.5.12.1, flat LevelScale) fused in: each level is
+  // dequantised as it is placed into its raster position, so no level arrays or second pass.
+  // Same output as dequantize_mb over MbLevels (the encoder's path).
+  void residual(Bits& br, int mb, MbState& s, MbResidual& res, int cbp_luma, int cbp_chroma, int qp) {
+    res.luma = 0;
+    res.chroma = 0;
+    nc_setup(mb);
+    const bool intra16 = s.kind == kI16x16;
+    auto scaler = [](int q) {
+      return Scale{kLevelScale[q % 6], q >= 24 ? 1 << (q / 6 - 4) : 1, q >= 24 ? 0 : 1 << (3 - q / 6),
+                   q >= 24 ? 0 : 4 - q / 6};
+    };
+    const auto dl = scaler(qp);
+    auto luma_block = [&](int r, int start, int max_coeff, int dcv) {
+      i16* d = res.blk[r];
+      std::memset(d, 0, 16 * sizeof(i16));
+      bool nz = dcv != 0;
+      d[0] = sat16(dcv);
+      const int tc = read_residual_block_cb(br, ncl(r), max_coeff, [&](int k, int l) {
+        const int pos = kZigzag4x4[k + start];
+        const int v = (l * dl.ls[pos] * dl.mul + dl.add) >> dl.sh;
+        d[pos] = sat16(v);
+        nz |= v != 0;
+      });
+      s.tc[r] = u8(tc);
+      ncl_[((r >> 2) + 1) * 5 + (r & 3) + 1] = u8(tc);
+      if (nz) res.luma |= u16(1u << r);
+    };
+    if (intra16) {
+      int c[16] = {};
+      const bool have_dc =
+          read_residual_block_cb(br, ncl(0), 16, [&](int k, int l) { c[kZigzag4x4[k]] = l; }) > 0;
+      int dcy[16] = {};
+      if (have_dc) {
+        h16(c);
+        const int ls = 16 * kNormAdjust[qp % 6][0];
+        for (int k = 0; k < 16; ++k)
+          dcy[k] = qp >= 36 ? c[k] * ls * (1 << (qp / 6 - 6)) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+      }
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        if (cbp_luma) {
+          luma_block(r, 1, 15, dcy[r]);
+        } else if (dcy[r] != 0) {
+          i16* d = res.blk[r];
+          std::memset(d, 0, 16 * sizeof(i16));
+          d[0] = sat16(dcy[r]);
+          res.luma |= u16(1u << r);
+        }
+      }
+    } else {
+      for (int idx = 0; idx < 16; ++idx)
+        if ((cbp_luma >> (idx >> 2)) & 1) luma_block(blk_to_raster(idx), 0, 16, 0);
     }
     if (cbp_chroma) {
+      const int qpc = chroma_qp(qp, sc_.pps.chroma_qp_index_offset);
+      const auto dc = scaler(qpc);
+      const int ls = 16 * kNormAdjust[qpc % 6][0];
+      int dcv[2][4];
       for (int c = 0; c < 2; ++c) {
-        int dc[16] = {};
-        if (read_residual_block(br, -1, 4, dc)) lv.dcmask |= u8(2 << c);
-        for (int k = 0; k < 4; ++k) lv.cdc[c][k] = dc[k];
+        int v[4] = {0, 0, 0, 0};
+        read_residual_block_cb(br, -1, 4, [&](int k, int l) { v[k] = l; });
+        const int f[4] = {v[0] + v[1] + v[2] + v[3], v[0] - v[1] + v[2] - v[3],
+                          v[0] + v[1] - v[2] - v[3], v[0] - v[1] - v[2] + v[3]};
+        for (int b = 0; b < 4; ++b) dcv[c][b] = ((f[b] * ls) * (1 << (qpc / 6))) >> 5;
       }
-      if (cbp_chroma & 2)
-        for (int c = 0; c < 2; ++c)
-          for (int b = 0; b < 4; ++b) {
-            std::memset(lv.cac[c][b], 0, sizeof lv.cac[c][b]);
-            const int tc = read_residual_block(br, nb_.nc_chroma(mb, c, b), 15, lv.cac[c][b] + 1);
+      for (int c = 0; c < 2; ++c)
+        for (int b = 0; b < 4; ++b) {
+          i16* d = res.blk[16 + c * 4 + b];
+          bool nz = dcv[c][b] != 0;
+          if (cbp_chroma & 2) {
+            std::memset(d, 0, 16 * sizeof(i16));
+            d[0] = sat16(dcv[c][b]);
+            const int tc = read_residual_block_cb(br, ncc(c, b), 15, [&](int k, int l) {
+              const int pos = kZigzag4x4[k + 1];
+              const int v = (l * dc.ls[pos] * dc.mul + dc.add) >> dc.sh;
+              d[pos] = sat16(v);
+              nz |= v != 0;
+            });
             s.tcc[c][b] = u8(tc);
-            if (tc) lv.cmask |= u8(1u << (c * 4 + b));
+            ncc_[c][((b >> 1) + 1) * 3 + (b & 1) + 1] = u8(tc);
+          } else if (nz) {
+            std::memset(d, 0, 16 * sizeof(i16));
+            d[0] = sat16(dcv[c][b]);
           }
+          if (nz) res.chroma |= u8(1u << (c * 4 + b));
+        }
     }
     VEP_CHECK(!br.overrun(), "slice data overrun");
-    dequantize_mb(lv, s.kind == kI16x16, qp, chroma_qp(qp, sc_.pps.chroma_qp_index_offset), res);
   }
 
   void emit(int mb, const MbState& s, const MbResidual& res, int i16_mode, int chroma_mode) {
@@ -746,7 +851,6 @@ class MbDecoder {
   Picture& pic_;
   const SliceCtx& sc_;
   const u8* pcm_ = nullptr;
-  MbLevels lv_;
 };
 
 }  // namespace
@@ -983,19 +1087,20 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   } else if (res && (res->luma | res->chroma)) {
     m.luma_coded = res->luma;
     m.chroma_coded = res->chroma;
-    const int nb = __builtin_popcount(res->luma) + __builtin_popcount(res->chroma);
-    size_t o = pic.coefs.size();
-    pic.coefs.resize(o + size_t(nb) * 16);
-    i16* dst = pic.coefs.data() + o;
-    for (u32 w = res->luma; w; w &= w - 1, dst += 16) std::memcpy(dst, res->blk[__builtin_ctz(w)], 32);
-    for (u32 w = res->chroma; w; w &= w - 1, dst += 16) std::memcpy(dst, res->blk[16 + __builtin_ctz(w)], 32);
+    // appended without a zero-filling resize (the pool is reserved per picture)
+    for (u32 w = res->luma; w; w &= w - 1) {
+      const i16* b = res->blk[__builtin_ctz(w)];
+      pic.coefs.insert(pic.coefs.end(), b, b + 16);
+    }
+    for (u32 w = res->chroma; w; w &= w - 1) {
+      const i16* b = res->blk[16 + __builtin_ctz(w)];
+      pic.coefs.insert(pic.coefs.end(), b, b + 16);
+    }
   }
   m.mv = 0;
   if (m.kind == kSkip || m.kind == kInter) {
     m.mv = u32(pic.mvs.size() / 32);
-    const size_t o = pic.mvs.size();
-    pic.mvs.resize(o + 32);
-    std::memcpy(pic.mvs.data() + o, s.mv, 64);
+    pic.mvs.insert(pic.mvs.end(), &s.mv[0][0], &s.mv[0][0] + 32);
     ++pic.inter_mbs;
   } else if (m.kind == kIPcm) {
     ++pic.inter_mbs;  // no neighbour dependency: reconstructed in the parallel pass

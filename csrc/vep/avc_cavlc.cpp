@@ -152,55 +152,6 @@ int read_run_before(Bits& br, int zeros_left) {
   return tables().run[(zeros_left < 7 ? zeros_left : 7) - 1].read(br);
 }
 
-int read_residual_block(Bits& br, int nc, int max_coeff, int* coeff) {
-  const CoeffToken t = read_coeff_token(br, coeff_token_class(nc));
-  if (t.total == 0) return 0;
-  VEP_CHECK(t.total <= max_coeff, "TotalCoeff exceeds maxNumCoeff");
-  int level[16];
-  int suffix_len = (t.total > 10 && t.trailing < 3) ? 1 : 0;
-  for (int i = 0; i < t.total; ++i) {
-    if (i < t.trailing) {
-      level[i] = br.u1() ? -1 : 1;
-      continue;
-    }
-    const u32 w = br.peek32();
-    VEP_CHECK(w != 0, "level_prefix too long");
-    const int prefix = __builtin_clz(w);
-    br.skip(size_t(prefix) + 1);
-    int code = (prefix < 15 ? prefix : 15) << suffix_len;
-    const int ssize = (prefix == 14 && suffix_len == 0) ? 4 : (prefix >= 15 ? prefix - 3 : suffix_len);
-    if (ssize > 0) code += int(br.u(ssize));
-    if (prefix >= 15 && suffix_len == 0) code += 15;
-    if (prefix >= 16) code += (1 << (prefix - 3)) - 4096;
-    if (i == t.trailing && t.trailing < 3) code += 2;
-    level[i] = (code % 2 == 0) ? (code + 2) >> 1 : (-code - 1) >> 1;
-    if (suffix_len == 0) suffix_len = 1;
-    const int a = level[i] < 0 ? -level[i] : level[i];
-    if (a > (3 << (suffix_len - 1)) && suffix_len < 6) ++suffix_len;
-  }
-  int zeros = 0;
-  if (t.total < max_coeff) zeros = read_total_zeros(br, t.total, max_coeff == 4);
-  VEP_CHECK(t.total + zeros <= max_coeff, "total_zeros out of range");
-  int run[16];
-  int left = zeros;
-  for (int i = 0; i < t.total - 1; ++i) {
-    if (left > 0) {
-      run[i] = read_run_before(br, left);
-      left -= run[i];
-      VEP_CHECK(left >= 0, "run_before exceeds zerosLeft");
-    } else {
-      run[i] = 0;
-    }
-  }
-  run[t.total - 1] = left;
-  int pos = -1;
-  for (int i = t.total - 1; i >= 0; --i) {
-    pos += run[i] + 1;
-    coeff[pos] = level[i];
-  }
-  return t.total;
-}
-
 // --------------------------------------------------------------------------------- writer
 
 int write_residual_block(BitWriter& bw, int nc, int max_coeff, const int* coeff) {

@@ -82,9 +82,59 @@ CoeffToken read_coeff_token(Bits& br, int cls);
 int read_total_zeros(Bits& br, int total_coeff, bool chroma_dc);
 int read_run_before(Bits& br, int zeros_left);
 
+// Parse one residual_block_cavlc (§7.3.5.3.3), handing every nonzero coefficient to
+// put(scan_index, level) (scan_index in [0, max_coeff)). Returns TotalCoeff.
+template <class Put>
+inline int read_residual_block_cb(Bits& br, int nc, int max_coeff, Put&& put) {
+  const CoeffToken t = read_coeff_token(br, coeff_token_class(nc));
+  if (t.total == 0) return 0;
+  VEP_CHECK(t.total <= max_coeff, "TotalCoeff exceeds maxNumCoeff");
+  int level[16];
+  int suffix_len = (t.total > 10 && t.trailing < 3) ? 1 : 0;
+  for (int i = 0; i < t.total; ++i) {
+    if (i < t.trailing) {
+      level[i] = br.u1() ? -1 : 1;
+      continue;
+    }
+    const u32 w = br.peek32();
+    VEP_CHECK(w != 0, "level_prefix too long");
+    const int prefix = __builtin_clz(w);
+    br.skip(size_t(prefix) + 1);
+    int code = (prefix < 15 ? prefix : 15) << suffix_len;
+    const int ssize = (prefix == 14 && suffix_len == 0) ? 4 : (prefix >= 15 ? prefix - 3 : suffix_len);
+    if (ssize > 0) code += int(br.u(ssize));
+    if (prefix >= 15 && suffix_len == 0) code += 15;
+    if (prefix >= 16) code += (1 << (prefix - 3)) - 4096;
+    if (i == t.trailing && t.trailing < 3) code += 2;
+    level[i] = (code % 2 == 0) ? (code + 2) >> 1 : (-code - 1) >> 1;
+    if (suffix_len == 0) suffix_len = 1;
+    const int a = level[i] < 0 ? -level[i] : level[i];
+    if (a > (3 << (suffix_len - 1)) && suffix_len < 6) ++suffix_len;
+  }
+  int left = 0;
+  if (t.total < max_coeff) left = read_total_zeros(br, t.total, max_coeff == 4);
+  VEP_CHECK(t.total + left <= max_coeff, "total_zeros out of range");
+  // levels arrive highest frequency first: walk scan positions downwards from the last one
+  int pos = t.total + left - 1;
+  for (int i = 0; i < t.total - 1; ++i) {
+    put(pos, level[i]);
+    int run = 0;
+    if (left > 0) {
+      run = read_run_before(br, left);
+      left -= run;
+      VEP_CHECK(left >= 0, "run_before exceeds zerosLeft");
+    }
+    pos -= run + 1;
+  }
+  put(pos, level[t.total - 1]);
+  return t.total;
+}
+
 // Parse one residual_block_cavlc (§7.3.5.3.3) into coeff[0 .. max_coeff-1] (scan order; the
 // caller zeroes coeff). Returns TotalCoeff.
-int read_residual_block(Bits& br, int nc, int max_coeff, int* coeff);
+inline int read_residual_block(Bits& br, int nc, int max_coeff, int* coeff) {
+  return read_residual_block_cb(br, nc, max_coeff, [coeff](int k, int v) { coeff[k] = v; });
+}
 
 // Encoder side: coeff[0 .. max_coeff-1] in scan order; levels must satisfy |level| <= 2047.
 // Returns TotalCoeff.
