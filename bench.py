@@ -58,6 +58,8 @@ def parse_args():
     ap.add_argument("--temporal-noise", type=float, default=1.0, help="per-frame sensor noise")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
     ap.add_argument("--threads", type=int, default=14, help="host parse threads per rank")
+    ap.add_argument("--parse-window", type=int, default=3,
+                    help="ticks a camera's parse may run ahead of the tick being launched")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
     ap.add_argument("--cache-gops", type=int, default=1,
                     help="distinct pre-encoded GOPs replayed per camera (working-set size)")
@@ -116,7 +118,7 @@ def main():
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
-                         ring_slots=a.ring_slots, prefix=f"r{rank}cam")
+                         ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
 
     # The native worker keeps two ticks in flight (tick t's frames are published while tick
     # t+2 is being launched), and one all-gather may still be reading an older tick: 4 buffers.
@@ -166,6 +168,7 @@ def main():
         dist.barrier()
     sync()
     f0, p0, b0, g0 = rb.frames, rb.parse_ms, rb.batch_ms, worker.gpu_ms_total
+    pw0 = rb.parse_wait_ms
     ip0, sg0 = worker.bytes_inplace, worker.bytes_staged
     tm0 = worker.timings()
     t0 = time.perf_counter()
@@ -178,6 +181,7 @@ def main():
     elapsed = t1 - t0
     frames = rb.frames - f0
     parse_ms, batch_ms, gpu_ms = rb.parse_ms - p0, rb.batch_ms - b0, worker.gpu_ms_total - g0
+    parse_wait_ms = rb.parse_wait_ms - pw0
     tm1 = worker.timings()
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -250,6 +254,7 @@ def main():
                                 "HIP PCM reconstruct/NV12->BGR24 (rocDecode absent in image)"),
             "per_gpu_fps": round(fps / max(world, 1), 2),
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
+            "rank0_parse_wait_ms_per_step": round(parse_wait_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
             "gpu_lanes": worker.lanes,

@@ -613,13 +613,14 @@ PYBIND11_MODULE(_vep, m) {
 
   py::class_<ReplayBench>(m, "ReplayBench")
       .def(py::init([](Worker& w, int ncams, const SynthConfig& cfg, int cached, int threads,
-                       int ring_slots, const std::string& prefix) {
+                       int ring_slots, const std::string& prefix, int window) {
              py::gil_scoped_release r;
-             return std::make_unique<ReplayBench>(w, ncams, cfg, cached, threads, ring_slots, prefix);
+             return std::make_unique<ReplayBench>(w, ncams, cfg, cached, threads, ring_slots, prefix,
+                                                  window);
            }),
            py::arg("worker"), py::arg("ncams"), py::arg("cfg"), py::arg("cached_frames") = 30,
            py::arg("threads") = 8, py::arg("ring_slots") = 2, py::arg("prefix") = "cam",
-           py::keep_alive<1, 2>())
+           py::arg("window") = 2, py::keep_alive<1, 2>())
       .def("step", &ReplayBench::step, py::call_guard<py::gil_scoped_release>())
       .def("parse_only_ms", &ReplayBench::parse_only_ms, py::call_guard<py::gil_scoped_release>())
       .def("drain", &ReplayBench::drain, py::call_guard<py::gil_scoped_release>())
@@ -628,6 +629,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("stream_bytes", &ReplayBench::stream_bytes)
       .def_property_readonly("stream_frames", &ReplayBench::stream_frames)
       .def_property_readonly("parse_ms", &ReplayBench::parse_ms)
+      .def_property_readonly("parse_wait_ms", &ReplayBench::parse_wait_ms)
       .def_property_readonly("batch_ms", &ReplayBench::batch_ms)
       .def_property_readonly("cameras", &ReplayBench::cameras);
 
