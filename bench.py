@@ -65,6 +65,8 @@ def parse_args():
                     help="distinct pre-encoded GOPs replayed per camera (working-set size)")
     ap.add_argument("--lanes", type=int, default=0,
                     help="independent GPU pipelines per worker (0 = runtime default)")
+    ap.add_argument("--stages", type=int, default=0,
+                    help="ticks in flight per GPU lane (0 = runtime default)")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--consumer-format", choices=["nv12", "bgr"], default="nv12",
@@ -107,7 +109,8 @@ def main():
     S = a.letterbox
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
                         max_cameras=cams, pack_threads=a.pack_threads,
-                        letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes)
+                        letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes,
+                        stages=a.stages)
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
@@ -120,9 +123,11 @@ def main():
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
 
-    # The native worker keeps two ticks in flight (tick t's frames are published while tick
-    # t+2 is being launched), and one all-gather may still be reading an older tick: 4 buffers.
-    NB = 4
+    # The native worker keeps `worker.stages` ticks in flight (tick t's frames are published
+    # while tick t + stages is being launched), and one all-gather may still be reading an
+    # older tick: stages + 2 consumer buffers.
+    LAG = worker.stages if use_gpu else 0
+    NB = LAG + 2
     bufs = [torch.empty((cams, row), dtype=torch.uint8, device=dev) for _ in range(NB)]
     gather = world > 1 and not a.no_gather
     gathered = [torch.empty((world * cams, row), dtype=torch.uint8, device=dev)
@@ -141,14 +146,14 @@ def main():
 
     def step(i):
         b = i % NB
-        if handles[b] is not None:  # buffer b may still feed the all-gather of tick i-4
+        if handles[b] is not None:  # buffer b may still feed the all-gather of tick i - NB
             handles[b].wait()
             handles[b] = None
             sync()
         worker.set_consumer_buffers(bufs[b].data_ptr(), 0, cams)
-        rb.step()  # enqueues tick i; ticks <= i-2 are published when it returns
+        rb.step()  # enqueues tick i; ticks <= i - LAG are published when it returns
         pending.append(i)
-        while pending and pending[0] <= i - 2:
+        while pending and pending[0] <= i - LAG:
             issue_gather(pending.pop(0))
 
     def drain():
@@ -258,6 +263,7 @@ def main():
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
             "gpu_lanes": worker.lanes,
+            "gpu_stages": worker.stages,
             "payload_path": ("decode kernel reads slice bytes from pinned host memory over PCIe"
                              if getattr(worker, "direct_reads", False) else
                              "gather kernel pulls slice bytes into HBM, decode reads HBM"),

@@ -391,10 +391,11 @@ PYBIND11_MODULE(_vep, m) {
   py::class_<Worker>(m, "Worker")
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
                        std::vector<float> stdv, int max_cameras, int pack_threads,
-                       int letterbox_format, int lanes) {
+                       int letterbox_format, int lanes, int stages) {
              WorkerOptions o;
              o.device = device;
              o.lanes = lanes;
+             o.stages = stages;
              o.pack_threads = pack_threads;
              o.letterbox_format = letterbox_format;
              o.letterbox_size = letterbox_size;
@@ -409,9 +410,10 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("device") = 0, py::arg("letterbox_size") = 0, py::arg("chw_dtype") = 0,
            py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
            py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
-           py::arg("letterbox_format") = 0, py::arg("lanes") = 0)
+           py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0)
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def_property_readonly("lanes", &Worker::lanes)
+      .def_property_readonly("stages", &Worker::stages)
       .def("add_camera", &Worker::add_camera, py::arg("name"), py::arg("ring_slots") = 2)
       .def("remove_camera", &Worker::remove_camera, py::call_guard<py::gil_scoped_release>())
       .def("find", [](Worker& w, const std::string& n) { auto c = w.find(n); return c ? c->index() : -1; })

@@ -550,25 +550,28 @@ VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbR
 }
 
 struct EdgeParams {
-  int alpha, beta, index_a;
+  int alpha, beta;
+  int tc0[3];  // tC0 for bS 1..3 (Table 8-17), resolved once per edge, not per sample line
 };
 
 VEP_HD EdgeParams edge_params(int qp_p, int qp_q, int off_a, int off_b) {
   const int qav = (qp_p + qp_q + 1) >> 1;
   const int ia = clip3(0, 51, qav + off_a), ib = clip3(0, 51, qav + off_b);
-  return EdgeParams{kAlpha[ia], kBeta[ib], ia};
+  return EdgeParams{kAlpha[ia], kBeta[ib], {kTc0[ia][0], kTc0[ia][1], kTc0[ia][2]}};
 }
 
 // Filter one line of samples across an edge: s points at q0, `step` is the distance between
 // successive samples across the edge (1 for a vertical edge, pitch for a horizontal one).
 // chroma lines use the two-sample filters (§8.7.2.3 / §8.7.2.4).
+// Core of filter_line with the edge's thresholds as scalars: tc0 = tC0 of this line's bS
+// (ignored for bS 4).
 template <typename Px>
-VEP_HD void filter_line(Px* s, long step, int bs, const EdgeParams& e, bool chroma) {
+VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0, bool chroma) {
   const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
-  if (!(iabs(p0 - q0) < e.alpha && iabs(p1 - p0) < e.beta && iabs(q1 - q0) < e.beta)) return;
+  if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
   if (chroma) {
     if (bs < 4) {
-      const int tc = kTc0[e.index_a][bs - 1] + 1;
+      const int tc = tc0 + 1;
       const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
       s[-step] = Px(clip1(p0 + d));
       s[0] = Px(clip1(q0 - d));
@@ -581,31 +584,35 @@ VEP_HD void filter_line(Px* s, long step, int bs, const EdgeParams& e, bool chro
   const int p2 = s[-3 * step], q2 = s[2 * step];
   const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
   if (bs < 4) {
-    const int tc0 = kTc0[e.index_a][bs - 1];
-    const int tc = tc0 + (ap < e.beta) + (aq < e.beta);
+    const int tc = tc0 + (ap < beta) + (aq < beta);
     const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
     s[-step] = Px(clip1(p0 + d));
     s[0] = Px(clip1(q0 - d));
-    if (ap < e.beta) s[-2 * step] = Px(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-    if (aq < e.beta) s[step] = Px(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
+    if (ap < beta) s[-2 * step] = Px(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
+    if (aq < beta) s[step] = Px(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
     return;
   }
   const int p3 = s[-4 * step], q3 = s[3 * step];
-  const bool strong = iabs(p0 - q0) < ((e.alpha >> 2) + 2);
-  if (ap < e.beta && strong) {
+  const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
+  if (ap < beta && strong) {
     s[-step] = Px((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
     s[-2 * step] = Px((p2 + p1 + p0 + q0 + 2) >> 2);
     s[-3 * step] = Px((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
   } else {
     s[-step] = Px((2 * p1 + p0 + q1 + 2) >> 2);
   }
-  if (aq < e.beta && strong) {
+  if (aq < beta && strong) {
     s[0] = Px((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
     s[step] = Px((p0 + q0 + q1 + q2 + 2) >> 2);
     s[2 * step] = Px((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
   } else {
     s[0] = Px((2 * q1 + q0 + p1 + 2) >> 2);
   }
+}
+
+template <typename Px>
+VEP_HD void filter_line(Px* s, long step, int bs, const EdgeParams& e, bool chroma) {
+  filter_line_t(s, step, bs, e.alpha, e.beta, bs < 4 ? e.tc0[bs - 1] : 0, chroma);
 }
 
 }  // namespace vep::avc

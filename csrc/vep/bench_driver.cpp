@@ -140,7 +140,7 @@ void ReplayBench::step() {
   }
   const i64 t0 = mono_us();
   const size_t n = jobs.size();
-  w_.launch_async(jobs);  // publishes tick t-2; ticks t-1 and t stay in flight
+  w_.launch_async(jobs);  // publishes tick t - stages; the ticks after it stay in flight
   batch_us_ += double(mono_us() - t0);
   frames_ += n;
 }

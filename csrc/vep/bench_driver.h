@@ -23,7 +23,7 @@ class ReplayBench {
   ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cached_frames, int threads,
               int ring_slots, const std::string& prefix, int window = 2);
   ~ReplayBench();
-  void step();      // takes the next parsed tick and launches it (publishes tick t-2)
+  void step();      // takes the next parsed tick and launches it (publishes tick t - stages)
   void drain();     // publish every launched tick
   // Host parse throughput alone: consume `ticks` parsed ticks without GPU work (jobs dropped)
   // and return the mean wall ms per tick.

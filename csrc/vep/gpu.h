@@ -98,9 +98,10 @@ constexpr int kAvcProfSlots = 12;  // + [11] intra residual pass
 // Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.
 struct AvcDbkInfo {
   u32 bs[4];      // 32 x 4-bit bS: nibble dir * 16 + edge * 4 + segment (0 = edge not filtered)
-  u8 alpha[6], beta[6], ia[6];  // [left, top, internal] luma, then [left, top, internal] chroma
+  u8 alpha[6], beta[6];  // [left, top, internal] luma, then [left, top, internal] chroma
+  u8 tc0[6][3];   // tC0 for bS 1..3, same edge order
   u8 any;         // any bS != 0
-  u8 pad[13];
+  u8 pad[1];
 };
 static_assert(sizeof(AvcDbkInfo) == 48, "AvcDbkInfo layout");
 constexpr int kAvcMaxRows = 512;  // MB rows per picture the wavefront kernels support (8K)

@@ -497,10 +497,10 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
       const avc::EdgeParams ec = avc::edge_params(ps[k]->qpc, q.qpc, q.alpha_off, q.beta_off);
       info.alpha[k] = u8(el.alpha);
       info.beta[k] = u8(el.beta);
-      info.ia[k] = u8(el.index_a);
+      for (int j = 0; j < 3; ++j) info.tc0[k][j] = u8(el.tc0[j]);
       info.alpha[3 + k] = u8(ec.alpha);
       info.beta[3 + k] = u8(ec.beta);
-      info.ia[3 + k] = u8(ec.index_a);
+      for (int j = 0; j < 3; ++j) info.tc0[3 + k][j] = u8(ec.tc0[j]);
     }
   }
   static_cast<AvcDbkInfo*>(d.dbk)[mb] = info;
@@ -516,23 +516,69 @@ struct DbkWave {
   u8 ccarry[2][8 * 2];
 };
 
+// Final bottom rows of one MB of a row, handed to the row below through LDS: luma rows 12..15
+// and NV12 chroma rows 6..7 (the only samples of a row that the row below reads or filters).
+struct alignas(16) DbkXch {
+  u8 y[4 * 16];
+  u8 c[2 * 16];
+};
+
 // A wave filters two adjacent MB rows at once: lanes 0-31 row 2p, lanes 32-63 row 2p+1, the
-// second trailing by kDbkLag columns. Row 2p+1 at column x needs row 2p finished up to x+1,
-// which this wave completed in an earlier iteration, so only the first row ever waits on
-// another wave. 32 rows in flight per picture instead of 16, and all 64 lanes filter.
+// second trailing by kDbkLag columns. 32 rows in flight per picture, all 64 lanes filtering.
+//
+// Rows talk only through LDS, so the per-MB handshake never waits on global memory:
+//  * a row passes its final bottom rows to the row below in an exchange ring of kDbkDepth
+//    columns (the producer waits when the consumer falls that far behind); the row pair that
+//    crosses from one pass to the next (row % 32 == 31 -> wave 0 of the next pass) uses a
+//    whole-row buffer instead, so no wait ever points from one pass to the next;
+//  * each sample is written to the picture by exactly one wave: a row stores rows 0..11 of its
+//    MBs, the row below stores rows 12..15 (from the exchange, after its own top-edge filter),
+//    so no global store ever needs to be ordered against another wave's;
+//  * the MB's own samples are prefetched one column ahead (no wave writes them before the row
+//    that owns the MB has filtered it).
 constexpr int kDbkLag = 3;
+constexpr int kDbkDepth = 8;
+constexpr int kDbkSlots = 2 * kWaves + 2;  // >= 33: a ring slot is reused only by a row whose
+                                           // wave has finished every row that could still read it
 
 __device__ inline void st4(u8* p, u32 v) { *reinterpret_cast<u32*>(p) = v; }
 __device__ inline u32 ld4(const u8* p) { return *reinterpret_cast<const u32*>(p); }
+// Global-memory accesses through address-space-1 pointers: global_load/global_store count only
+// against vmcnt. Generic (flat) accesses also count against lgkmcnt, so every LDS wait would
+// stall on them too — prefetches and fire-and-forget stores would serialise with the LDS work.
+#define VEP_GLOBAL __attribute__((address_space(1)))
+__device__ inline u32 gld4(const void* p) { return *(const VEP_GLOBAL u32*)(p); }
+__device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
+
+// LDS-only handshake: progress counters and the data they guard both live in LDS.
+__device__ inline void wait_row_lds(Sync& s, int r, u32 need, u32* err) {
+  u32 spins = 0;
+  while (__hip_atomic_load(&s.progress[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
+    if (__hip_atomic_load(&s.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+    if (++spins > kSpinLimit) {
+      __hip_atomic_store(&s.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if ((threadIdx.x & 63) == 0) atomicOr(err, 2u);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
   const int i = dir * 16 + e * 4 + sg;
   return int((in.bs[i >> 3] >> (4 * (i & 7))) & 15u);
 }
 
+struct DbkRegs {  // one MB's inputs as loaded from global memory (per lane of a half-wave)
+  u32 info, m0, m1, c;
+};
+
 __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __restrict__ descs) {
   __shared__ Sync sync;
   __shared__ DbkWave lds[kWaves][2];
+  __shared__ DbkXch xring[kDbkSlots][kDbkDepth];
+  __shared__ DbkXch xwrap[kAvcMaxCols];
   const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, pitch = W * 16;
   sync_init(sync, H);
@@ -542,83 +588,79 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
+  constexpr int kPass = 2 * kWaves;
+  auto xch = [&](int r, int x) -> DbkXch& {
+    return r % kPass == kPass - 1 ? xwrap[x] : xring[r % kDbkSlots][x % kDbkDepth];
+  };
+  // Branch-free (row / column clamped, the result unused when out of range): a conditional
+  // load would merge with a default at the join and force an immediate vmcnt wait.
+  auto load_mb = [&](int row, int x) {
+    row = row < H ? row : H - 1;
+    x = x < 0 ? 0 : (x < W ? x : W - 1);
+    DbkRegs v;
+    v.info = gld4(reinterpret_cast<const u32*>(&infos[size_t(row) * W + x]) + (l < 12 ? l : 0));
+    const u8* ym = Y + size_t(row * 16 + (l >> 2)) * pitch + x * 16 + (l & 3) * 4;
+    v.m0 = gld4(ym);                      // MB rows 0..7
+    v.m1 = gld4(ym + size_t(8) * pitch);  // MB rows 8..15
+    v.c = gld4(UV + size_t(row * 8 + (l >> 2)) * pitch + x * 16 + (l & 3) * 4);  // 8 x 16 B
+    return v;
+  };
   u64 acc[5] = {0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
-  for (int r0 = 2 * wave; r0 < H; r0 += 2 * kWaves) {
+  for (int r0 = 2 * wave; r0 < H; r0 += kPass) {
     const int row = r0 + h;
+    const bool last = row == H - 1;
+    const bool prod = row + 1 < H;  // this row hands its bottom rows to the row below
     bool carry = false;
+    DbkRegs cur = load_mb(row, -kDbkLag * h);
     for (int i = 0; i < W + kDbkLag; ++i) {
       const int x = i - h * kDbkLag;
       const bool act = row < H && x >= 0 && x < W;
       const u64 t0 = d.prof ? clock64() : 0;
-      if (r0 > 0 && i < W) wait_row(sync, r0 - 1, u32(i + 2 < W ? i + 2 : W), d.err);
+      const DbkRegs nxt = load_mb(row, x + 1);  // prefetch: in flight across this MB's work
+      if (r0 > 0 && i < W) wait_row_lds(sync, r0 - 1, u32(i + 2 < W ? i + 2 : W), d.err);
+      {  // back-pressure: the pair's second row feeds the next wave through an 8-column ring
+        const int x1 = i - kDbkLag;
+        if (r0 + 2 < H && (r0 + 1) % kPass != kPass - 1 && x1 < W && x1 - kDbkDepth + 1 > 0)
+          wait_row_lds(sync, r0 + 2, u32(x1 - kDbkDepth + 1), d.err);
+      }
       const u64 t1 = d.prof ? clock64() : 0;
       const int x0 = x * 16, y0 = row * 16;
-      const size_t mb = size_t(row) * W + x;
-      // ---- batch: every global load first (filter inputs, MB samples, left columns, top rows),
-      // then the LDS stores — one memory round trip per MB
-      u32 vinfo = 0, vm0 = 0, vm1 = 0, v2 = 0, vc = 0, v3 = 0;
+      // ---- LDS: MB samples, left columns (carried), top rows (the row above's exchange)
       if (act) {
-        if (l < 12) vinfo = reinterpret_cast<const u32*>(&infos[mb])[l];
-        const u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
-        vm0 = ld4(ym);                       // MB rows 0..7
-        vm1 = ld4(ym + size_t(8) * pitch);   // MB rows 8..15
-        if (l < 16) {  // luma left columns -4..-1 of MB row l
-          if (x > 0 && !carry) v2 = ld4(Y + size_t(y0 + l) * pitch + x0 - 4);
-        } else if (row > 0) {  // luma top rows -4..-1
-          const int k = l - 16;
-          v2 = ld4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4);
-        }
-        vc = ld4(UV + size_t(row * 8 + (l >> 2)) * pitch + x0 + (l & 3) * 4);  // NV12 8 x 16 B
-        if (l < 8) {  // chroma left 2 columns (4 B NV12) of chroma row l
-          if (x > 0 && !carry) v3 = ld4(UV + size_t(row * 8 + l) * pitch + x0 - 4);
-        } else if (l < 16 && row > 0) {  // chroma top 2 rows
-          const int k = l - 8;
-          v3 = ld4(UV + size_t(row * 8 - 2 + (k >> 2)) * pitch + x0 + (k & 3) * 4);
-        }
-        // ---- LDS stores
-        if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = vinfo;
-        st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], vm0);
-        st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], vm1);
+        if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
+        st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
+        st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
         if (l < 16) {
-          if (x > 0) st4(&L.y[(l + 4) * 20], carry ? ld4(&L.carry[l * 4]) : v2);
+          if (x > 0) st4(&L.y[(l + 4) * 20], ld4(&L.carry[l * 4]));
         } else if (row > 0) {
           const int k = l - 16;
-          st4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4], v2);
+          st4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4], ld4(&xch(row - 1, x).y[k * 4]));
         }
         {
           const int cyr = l >> 2, cb = (l & 3) * 2;
           for (int b = 0; b < 2; ++b) {
-            L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(vc >> (16 * b));
-            L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(vc >> (16 * b + 8));
+            L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(cur.c >> (16 * b));
+            L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(cur.c >> (16 * b + 8));
           }
         }
         if (l < 8) {
           if (x > 0) {
-            u8 v[4];
-            if (carry) {
-              v[0] = L.ccarry[0][l * 2];
-              v[1] = L.ccarry[1][l * 2];
-              v[2] = L.ccarry[0][l * 2 + 1];
-              v[3] = L.ccarry[1][l * 2 + 1];
-            } else {
-              for (int b = 0; b < 4; ++b) v[b] = u8(v3 >> (8 * b));
-            }
-            L.c[0][(l + 2) * 10 + 0] = v[0];
-            L.c[1][(l + 2) * 10 + 0] = v[1];
-            L.c[0][(l + 2) * 10 + 1] = v[2];
-            L.c[1][(l + 2) * 10 + 1] = v[3];
+            L.c[0][(l + 2) * 10 + 0] = L.ccarry[0][l * 2];
+            L.c[1][(l + 2) * 10 + 0] = L.ccarry[1][l * 2];
+            L.c[0][(l + 2) * 10 + 1] = L.ccarry[0][l * 2 + 1];
+            L.c[1][(l + 2) * 10 + 1] = L.ccarry[1][l * 2 + 1];
           }
         } else if (l < 16 && row > 0) {
           const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+          const u32 v = ld4(&xch(row - 1, x).c[k * 4]);
           for (int b = 0; b < 2; ++b) {
-            L.c[0][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b));
-            L.c[1][tr * 10 + 2 + cb + b] = u8(v3 >> (16 * b + 8));
+            L.c[0][tr * 10 + 2 + cb + b] = u8(v >> (16 * b));
+            L.c[1][tr * 10 + 2 + cb + b] = u8(v >> (16 * b + 8));
           }
         }
       }
       wave_sync();
       const u64 t2 = d.prof ? clock64() : 0;
-      u64 t3 = t2;
       const bool any = act && L.info.any;
       if (__ballot(any)) {
         // ---- filter: vertical edges then horizontal edges (per half: luma lanes 0-15,
@@ -630,63 +672,92 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
               if (l < 16) {
                 const int bs = bs_of(L.info, dir, e, l >> 2);
                 if (bs) {
-                  const avc::EdgeParams ep{L.info.alpha[pk], L.info.beta[pk], L.info.ia[pk]};
-                  if (dir == 0) avc::filter_line(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, ep, false);
-                  else avc::filter_line(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, ep, false);
+                  const int al = L.info.alpha[pk], be = L.info.beta[pk];
+                  const int tc = bs < 4 ? L.info.tc0[pk][bs - 1] : 0;
+                  if (dir == 0) avc::filter_line_t(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, al, be, tc, false);
+                  else avc::filter_line_t(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, al, be, tc, false);
                 }
               } else if (!(e & 1)) {
                 const int c = (l - 16) >> 3, k = (l - 16) & 7;
                 const int bs = bs_of(L.info, dir, e, k >> 1);
                 if (bs) {
-                  const avc::EdgeParams ep{L.info.alpha[3 + pk], L.info.beta[3 + pk], L.info.ia[3 + pk]};
-                  if (dir == 0) avc::filter_line(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, ep, true);
-                  else avc::filter_line(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, ep, true);
+                  const int al = L.info.alpha[3 + pk], be = L.info.beta[3 + pk];
+                  const int tc = bs < 4 ? L.info.tc0[3 + pk][bs - 1] : 0;
+                  if (dir == 0) avc::filter_line_t(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, al, be, tc, true);
+                  else avc::filter_line_t(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, al, be, tc, true);
                 }
               }
             }
             wave_sync();
           }
         }
-        t3 = d.prof ? clock64() : 0;
-        // ---- write back (MB, left columns, top rows)
+      }
+      const u64 t3 = d.prof ? clock64() : 0;
+      if (act) {
+        // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left
+        // neighbour's columns 12..15 if the left edge was filtered, and always the MB above's
+        // final rows 12..15 (this wave is their only writer)
+        const bool left = any && (L.info.bs[0] & 0xFFFFu) != 0;  // dir 0, edge 0 nibbles
         if (any) {
-          const bool left = (L.info.bs[0] & 0xFFFFu) != 0;  // dir 0, edge 0 nibbles
-          const bool top = (L.info.bs[2] & 0xFFFFu) != 0;   // dir 1, edge 0 nibbles
           u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
-          st4(ym, ld4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4]));
-          st4(ym + size_t(8) * pitch, ld4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4]));
-          if (l < 16) {
-            if (left) st4(Y + size_t(y0 + l) * pitch + x0 - 4, ld4(&L.y[(l + 4) * 20]));
-          } else if (top) {
-            const int k = l - 16;
-            st4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4,
-                ld4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4]));
-          }
-          {
-            const int cyr = l >> 2, cb = (l & 3) * 2;
+          gst4(ym, ld4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4]));
+          if ((l >> 2) < 4 || last)
+            gst4(ym + size_t(8) * pitch, ld4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4]));
+          const int cyr = l >> 2, cb = (l & 3) * 2;
+          if (cyr < 6 || last) {
             u32 cw = 0;
             for (int b = 0; b < 2; ++b)
               cw |= (u32(L.c[0][(cyr + 2) * 10 + 2 + cb + b]) | u32(L.c[1][(cyr + 2) * 10 + 2 + cb + b]) << 8)
                     << (16 * b);
-            st4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
-          }
-          if (l < 8) {
-            if (left) {
-              const u32 cw = u32(L.c[0][(l + 2) * 10]) | u32(L.c[1][(l + 2) * 10]) << 8 |
-                             u32(L.c[0][(l + 2) * 10 + 1]) << 16 | u32(L.c[1][(l + 2) * 10 + 1]) << 24;
-              st4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
-            }
-          } else if (l < 16 && top) {
-            const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
-            u32 cw = 0;
-            for (int b = 0; b < 2; ++b)
-              cw |= (u32(L.c[0][tr * 10 + 2 + cb + b]) | u32(L.c[1][tr * 10 + 2 + cb + b]) << 8) << (16 * b);
-            st4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
+            gst4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
           }
         }
-      }
-      // carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
-      if (act) {
+        if (l < 16) {
+          if (left && (l < 12 || last)) gst4(Y + size_t(y0 + l) * pitch + x0 - 4, ld4(&L.y[(l + 4) * 20]));
+        } else if (row > 0) {
+          const int k = l - 16;
+          gst4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4,
+              ld4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4]));
+        }
+        if (l < 8) {
+          if (left && (l < 6 || last)) {
+            const u32 cw = u32(L.c[0][(l + 2) * 10]) | u32(L.c[1][(l + 2) * 10]) << 8 |
+                           u32(L.c[0][(l + 2) * 10 + 1]) << 16 | u32(L.c[1][(l + 2) * 10 + 1]) << 24;
+            gst4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
+          }
+        } else if (l < 16 && row > 0) {
+          const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+          u32 cw = 0;
+          for (int b = 0; b < 2; ++b)
+            cw |= (u32(L.c[0][tr * 10 + 2 + cb + b]) | u32(L.c[1][tr * 10 + 2 + cb + b]) << 8) << (16 * b);
+          gst4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
+        }
+        // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (columns
+        // 12..15 / 6..7 final only after the next MB's left edge) and the previous MB's now
+        // final columns 12..15 / 6..7
+        if (prod) {
+          DbkXch& xo = xch(row, x);
+          if (l < 16) {
+            st4(&xo.y[l * 4], ld4(&L.y[(16 + (l >> 2)) * 20 + 4 + (l & 3) * 4]));
+          } else if (l < 24) {
+            const int k = l - 16, cr = 8 + (k >> 2), cb = (k & 3) * 2;
+            const u32 cw = u32(L.c[0][cr * 10 + 2 + cb]) | u32(L.c[1][cr * 10 + 2 + cb]) << 8 |
+                           u32(L.c[0][cr * 10 + 3 + cb]) << 16 | u32(L.c[1][cr * 10 + 3 + cb]) << 24;
+            st4(&xo.c[k * 4], cw);
+          } else if (x > 0) {
+            DbkXch& xp = xch(row, x - 1);
+            if (l < 28) {
+              const int k = l - 24;
+              st4(&xp.y[k * 16 + 12], ld4(&L.y[(16 + k) * 20]));
+            } else if (l < 30) {
+              const int k = l - 28, cr = 8 + k;
+              const u32 cw = u32(L.c[0][cr * 10]) | u32(L.c[1][cr * 10]) << 8 |
+                             u32(L.c[0][cr * 10 + 1]) << 16 | u32(L.c[1][cr * 10 + 1]) << 24;
+              st4(&xp.c[k * 16 + 12], cw);
+            }
+          }
+        }
+        // ---- carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
         if (l < 16) {
           st4(&L.carry[l * 4], ld4(&L.y[(l + 4) * 20 + 16]));
         } else {
@@ -696,12 +767,13 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
         }
       }
       carry = carry || act;
-      // publish both rows: this wave's global stores happen-before the new progress values
-      // (row 2p's stores are also what the second half reads in its next iterations)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      // publish both rows (LDS release: the exchange and carries are LDS; global stores are
+      // never read back in this kernel and have a single writer)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if (l == 0 && act)
         __hip_atomic_store(&sync.progress[row], u32(x + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       wave_sync();
+      cur = nxt;
       if (d.prof) {
         const u64 t4 = clock64();
         acc[0] += t1 - t0;

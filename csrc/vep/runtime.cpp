@@ -269,6 +269,9 @@ bool Camera::make_job(const AuPtr& au, DecodeJob& job) {
 // Lanes per GPU worker (WorkerOptions::lanes): lane streams + the serving stream fit the
 // default 4 hardware queues per process.
 constexpr int kDefaultLanes = 3;
+// Batches in flight per lane: one slow batch (a keyframe's intra wavefront) then blocks the
+// launching thread only after the other lanes have this many batches queued.
+constexpr int kDefaultStages = 3;
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (dev_.gpu()) {
@@ -279,6 +282,12 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       nl = le ? std::atoi(le) : kDefaultLanes;
     }
     lanes_.resize(size_t(std::clamp(nl, 1, 8)));
+    int ns = opt_.stages;
+    if (ns <= 0) {
+      const char* se = std::getenv("VEP_STAGES");
+      ns = se ? std::atoi(se) : kDefaultStages;
+    }
+    stages_ = std::clamp(ns, 2, 8);
     // Streams map onto the process's few hardware queues (GPU_MAX_HW_QUEUES): create only the
     // ones in use, serving first so its D2H never queues behind a lane's kernels.
     VEP_HIP(hipStreamCreateWithFlags(&serve_stream_, hipStreamNonBlocking));
@@ -294,6 +303,7 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       Lane& ln = lanes_[g];
       if (g == 0) ln.stream = stream_;
       else VEP_HIP(hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
+      ln.stage.resize(size_t(stages_));
       for (Stage& st : ln.stage) {
         VEP_HIP(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
         VEP_HIP(hipEventCreate(&st.e0));
@@ -384,9 +394,10 @@ int Worker::add_camera(const std::string& name, int ring_slots) {
     idx = int(cams_.size());
     cams_.emplace_back();
   }
-  // two batches may be in flight on the GPU: keep >= 3 slots so a committed frame stays readable
+  // `stages` batches may be in flight on the GPU: keep one more slot so the newest committed
+  // frame stays readable while they are written
   cams_[size_t(idx)] =
-      std::make_shared<Camera>(*this, idx, name, std::max(dev_.gpu() ? 3 : 1, ring_slots));
+      std::make_shared<Camera>(*this, idx, name, std::max(dev_.gpu() ? stages_ + 1 : 1, ring_slots));
   return idx;
 }
 
@@ -522,7 +533,7 @@ void Worker::loop() {
     batch.clear();
     {
       std::lock_guard<std::mutex> g(q_mu_);
-      if (!pending_.empty()) continue;  // keep the pipeline two batches deep
+      if (!pending_.empty()) continue;  // keep the pipeline full while work keeps arriving
     }
     try {
       complete_all();
@@ -804,7 +815,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       const auto& v = jobs[size_t(i)].avc;
       if (int(v.size()) <= r) continue;
       const avc::Picture& p = *v[size_t(r)];
-      VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows, "picture too tall for the wavefront kernels");
+      VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows && p.wmbs <= gpu::kAvcMaxCols,
+                "picture too large for the wavefront kernels");
       AvcPic a{&p, i, 0, 0, 0, 0};
       a.off_mbs = need;
       need += al(p.mbs.size() * sizeof(avc::MbRec));
@@ -1178,11 +1190,10 @@ void Worker::complete(Lane& ln, Stage& st) {
 }
 
 void Worker::complete_locked() {
-  // oldest first: Lane::next names the stage that will be reused next, i.e. the older batch
-  for (Lane& ln : lanes_) {
-    complete(ln, ln.stage[ln.next]);
-    complete(ln, ln.stage[ln.next ^ 1]);
-  }
+  // oldest first: Lane::next names the stage that will be reused next, i.e. the oldest batch
+  for (Lane& ln : lanes_)
+    for (size_t k = 0; k < ln.stage.size(); ++k)
+      complete(ln, ln.stage[(size_t(ln.next) + k) % ln.stage.size()]);
 }
 
 void Worker::complete_all() {
@@ -1220,9 +1231,9 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
   for (size_t g = 0; g < nl; ++g) {
     if (lj[g].empty()) continue;
     Lane& ln = lanes_[g];
-    Stage& st = ln.stage[ln.next];
-    ln.next ^= 1;
-    complete(ln, st);  // this lane's batch from two launches ago: its staging is reused now
+    Stage& st = ln.stage[size_t(ln.next)];
+    ln.next = (ln.next + 1) % int(ln.stage.size());
+    complete(ln, st);  // this lane's oldest batch (`stages` launches ago): its staging is reused
     st.jobs.swap(lj[g]);
     st.slots.swap(ls[g]);
     try {

@@ -204,6 +204,9 @@ struct WorkerOptions {
   // its own stream and staging. A keyframe's long intra wavefront then delays only its lane's
   // cameras instead of the whole tick. 0 = VEP_LANES or the default.
   int lanes = 0;
+  // Batches in flight per lane (staging buffers): launch_async blocks only when its lane still
+  // runs the batch from `stages` launches ago. 0 = VEP_STAGES or the default.
+  int stages = 0;
 };
 
 class Worker {
@@ -227,10 +230,10 @@ class Worker {
 
   // Synchronous batched decode (bench / tests). Jobs are consumed.
   void run_batch(std::vector<DecodeJob>& jobs);
-  // Asynchronous pipeline (two batches in flight, double-buffered staging, H2D on a copy
-  // stream overlapping the previous batch's kernels). launch_async returns once the batch is
-  // enqueued; its frames are published by a later launch_async (when its staging buffer is
-  // reused) or by complete_all().
+  // Asynchronous pipeline (per lane `stages()` batches in flight, one staging buffer each; with
+  // one lane the H2D runs on a copy stream overlapping the previous batch's kernels).
+  // launch_async returns once the batch is enqueued; its frames are published by a later
+  // launch_async (when its staging buffer is reused) or by complete_all().
   void launch_async(std::vector<DecodeJob>& jobs);
   void complete_all();
   // Wait until every submitted job is published.
@@ -248,6 +251,8 @@ class Worker {
   void* consumer_chw() const { return cons_chw_; }
   hipStream_t compute_stream() const { return stream_; }  // lane 0
   int lanes() const { return int(lanes_.size()); }
+  // batches in flight per lane: a launch publishes the batch from this many launches ago
+  int stages() const { return stages_; }
   u64 batches() const { return batches_.load(); }
   // slice bytes the GPU read in place from pinned AU blocks vs. staged by a host memcpy
   u64 bytes_inplace() const { return pinned_bytes_inplace_; }
@@ -275,8 +280,8 @@ class Worker {
   void ensure_surface(Camera& c, const PictureInfo& pi, int slots);
   struct Lane {
     hipStream_t stream = nullptr;  // lane 0 uses Worker::stream_
-    Stage stage[2];
-    int next = 0;                  // the stage reused next (the older in-flight batch)
+    std::vector<Stage> stage;      // ring of staging buffers (Worker::stages() deep)
+    int next = 0;                  // the stage reused next (the oldest in-flight batch)
     double gpu_ms = 0;             // cumulative batch time on this lane
   };
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
@@ -293,6 +298,7 @@ class Worker {
   mutable std::mutex cams_mu_;
   std::vector<std::shared_ptr<Camera>> cams_;
   std::vector<Lane> lanes_;
+  int stages_ = 2;
   std::unique_ptr<ThreadPool> pack_pool_;
 
  public:
