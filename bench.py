@@ -67,6 +67,8 @@ def parse_args():
                     help="independent GPU pipelines per worker (0 = runtime default)")
     ap.add_argument("--stages", type=int, default=0,
                     help="ticks in flight per GPU lane (0 = runtime default)")
+    ap.add_argument("--lane-queue", type=int, default=0,
+                    help="batches queued per GPU lane launcher thread (0 = runtime default)")
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--no-gather", action="store_true")
     ap.add_argument("--consumer-format", choices=["nv12", "bgr"], default="nv12",
@@ -110,7 +112,7 @@ def main():
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
                         max_cameras=cams, pack_threads=a.pack_threads,
                         letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes,
-                        stages=a.stages)
+                        stages=a.stages, queue=a.lane_queue)
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
@@ -123,10 +125,9 @@ def main():
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
 
-    # The native worker keeps `worker.stages` ticks in flight (tick t's frames are published
-    # while tick t + stages is being launched), and one all-gather may still be reading an
-    # older tick: stages + 2 consumer buffers.
-    LAG = worker.stages if use_gpu else 0
+    # The native worker keeps up to `worker.inflight` ticks per lane launched but unpublished,
+    # and one all-gather may still be reading an older tick: inflight + 2 consumer buffers.
+    LAG = worker.inflight if use_gpu else 0
     NB = LAG + 2
     bufs = [torch.empty((cams, row), dtype=torch.uint8, device=dev) for _ in range(NB)]
     gather = world > 1 and not a.no_gather
@@ -134,6 +135,7 @@ def main():
                 for _ in range(NB)] if gather else None
     handles = [None] * NB
     pending = []  # ticks launched whose consumer batch has not been handed to the gather yet
+    seq_of = {}   # tick -> the worker's launch sequence (lane threads publish asynchronously)
 
     def sync():
         if use_gpu:
@@ -141,7 +143,9 @@ def main():
 
     def issue_gather(t):
         k = t % NB
+        seq = seq_of.pop(t)
         if gather:
+            worker.wait_published(seq)  # every lane has written tick t's letterbox rows
             handles[k] = dist.all_gather_into_tensor(gathered[k], bufs[k], async_op=True)
 
     def step(i):
@@ -151,7 +155,8 @@ def main():
             handles[b] = None
             sync()
         worker.set_consumer_buffers(bufs[b].data_ptr(), 0, cams)
-        rb.step()  # enqueues tick i; ticks <= i - LAG are published when it returns
+        rb.step()  # enqueues tick i
+        seq_of[i] = worker.launch_seq if use_gpu else 0
         pending.append(i)
         while pending and pending[0] <= i - LAG:
             issue_gather(pending.pop(0))
@@ -264,6 +269,7 @@ def main():
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
             "gpu_lanes": worker.lanes,
             "gpu_stages": worker.stages,
+            "gpu_inflight_per_lane": worker.inflight,
             "payload_path": ("decode kernel reads slice bytes from pinned host memory over PCIe"
                              if getattr(worker, "direct_reads", False) else
                              "gather kernel pulls slice bytes into HBM, decode reads HBM"),

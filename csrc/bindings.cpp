@@ -391,11 +391,13 @@ PYBIND11_MODULE(_vep, m) {
   py::class_<Worker>(m, "Worker")
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
                        std::vector<float> stdv, int max_cameras, int pack_threads,
-                       int letterbox_format, int lanes, int stages) {
+                       int letterbox_format, int lanes, int stages, int queue, bool lane_threads) {
              WorkerOptions o;
              o.device = device;
              o.lanes = lanes;
              o.stages = stages;
+             o.queue = queue;
+             o.lane_threads = lane_threads;
              o.pack_threads = pack_threads;
              o.letterbox_format = letterbox_format;
              o.letterbox_size = letterbox_size;
@@ -410,10 +412,15 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("device") = 0, py::arg("letterbox_size") = 0, py::arg("chw_dtype") = 0,
            py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
            py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
-           py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0)
+           py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0,
+           py::arg("queue") = 0, py::arg("lane_threads") = false)
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def_property_readonly("lanes", &Worker::lanes)
       .def_property_readonly("stages", &Worker::stages)
+      .def_property_readonly("inflight", &Worker::inflight)
+      .def_property_readonly("launch_seq", &Worker::launch_seq)
+      .def("wait_published", &Worker::wait_published, py::arg("seq"),
+           py::call_guard<py::gil_scoped_release>())
       .def("add_camera", &Worker::add_camera, py::arg("name"), py::arg("ring_slots") = 2)
       .def("remove_camera", &Worker::remove_camera, py::call_guard<py::gil_scoped_release>())
       .def("find", [](Worker& w, const std::string& n) { auto c = w.find(n); return c ? c->index() : -1; })
@@ -447,7 +454,8 @@ PYBIND11_MODULE(_vep, m) {
              return true;
            })
       .def("decode_many",
-           [](Worker& w, const std::vector<std::pair<int, std::vector<std::shared_ptr<AccessUnit>>>>& work) {
+           [](Worker& w, const std::vector<std::pair<int, std::vector<std::shared_ptr<AccessUnit>>>>& work,
+              bool sync) {
              // one batch: per camera all given AUs (merged into one job, GOP catch-up style)
              std::vector<std::shared_ptr<Camera>> keep;
              for (auto& [idx, aus] : work) keep.push_back(cam_ref(w, idx));
@@ -466,9 +474,11 @@ PYBIND11_MODULE(_vep, m) {
                if (have) jobs.push_back(std::move(merged));
              }
              const size_t n = jobs.size();
-             w.run_batch(jobs);
+             if (sync) w.run_batch(jobs);
+             else w.launch_async(jobs);  // published later (launch_seq / wait_published)
              return n;
-           })
+           },
+           py::arg("work"), py::arg("sync") = true)
       .def("avc_profile", [](Worker& w) {
         static const char* kNames[gpu::kAvcProfSlots] = {
             "intra_wait", "intra_load", "intra_luma", "intra_chroma", "intra_store", "intra_mbs",

@@ -272,6 +272,8 @@ constexpr int kDefaultLanes = 3;
 // Batches in flight per lane: one slow batch (a keyframe's intra wavefront) then blocks the
 // launching thread only after the other lanes have this many batches queued.
 constexpr int kDefaultStages = 3;
+// Batches queued per lane launcher thread behind the in-flight ones.
+constexpr int kDefaultLaneQueue = 2;
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (dev_.gpu()) {
@@ -281,7 +283,18 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       const char* le = std::getenv("VEP_LANES");
       nl = le ? std::atoi(le) : kDefaultLanes;
     }
-    lanes_.resize(size_t(std::clamp(nl, 1, 8)));
+    nl = std::clamp(nl, 1, 16);
+    for (int g = 0; g < nl; ++g) lanes_.push_back(std::make_unique<Lane>());
+    // Launcher thread per lane: opt-in (measured no steadier than the single launching thread
+    // at the default 3 lanes, whose batches are bound by per-picture wavefront latency).
+    const char* lt = std::getenv("VEP_LANE_THREADS");
+    threaded_ = nl > 1 && (opt_.lane_threads || (lt && lt[0] == '1'));
+    int nq = opt_.queue;
+    if (nq <= 0) {
+      const char* qe = std::getenv("VEP_LANE_QUEUE");
+      nq = qe ? std::atoi(qe) : kDefaultLaneQueue;
+    }
+    queue_ = std::clamp(nq, 1, 16);
     int ns = opt_.stages;
     if (ns <= 0) {
       const char* se = std::getenv("VEP_STAGES");
@@ -300,14 +313,16 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       VEP_HIP(hipStreamCreateWithPriority(&copy_stream_, hipStreamNonBlocking, prio_hi));
     }
     for (size_t g = 0; g < lanes_.size(); ++g) {
-      Lane& ln = lanes_[g];
+      Lane& ln = *lanes_[g];
       if (g == 0) ln.stream = stream_;
       else VEP_HIP(hipStreamCreateWithFlags(&ln.stream, hipStreamNonBlocking));
       ln.stage.resize(size_t(stages_));
       for (Stage& st : ln.stage) {
         VEP_HIP(hipEventCreateWithFlags(&st.copied, hipEventDisableTiming));
         VEP_HIP(hipEventCreate(&st.e0));
-        VEP_HIP(hipEventCreate(&st.e1));
+        // waiters sleep instead of spinning: several lane threads wait at once and share the
+        // CPUs with the parse threads
+        VEP_HIP(hipEventCreateWithFlags(&st.e1, threaded_ ? hipEventBlockingSync : hipEventDefault));
       }
     }
     hostmem::enable_pool();  // AUs finalised from here on are GPU-readable in place
@@ -319,7 +334,12 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     const char* dr = std::getenv("VEP_DIRECT_READS");
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
-  if (opt_.pack_threads > 0) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads);
+  if (opt_.pack_threads > 0 && !threaded_) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads);
+  if (threaded_)
+    for (auto& lp : lanes_) {
+      Lane* ln = lp.get();
+      ln->th = std::thread([this, ln] { lane_loop(*ln); });
+    }
   cams_.reserve(size_t(opt_.max_cameras));
   if (opt_.letterbox_size > 0) {
     const size_t S = size_t(opt_.letterbox_size);
@@ -337,6 +357,10 @@ void Worker::set_consumer_buffers(u8* hwc, void* chw, int rows) {
   std::lock_guard<std::mutex> lg(launch_mu_);
   VEP_CHECK(opt_.letterbox_size > 0, "worker was built without a letterbox consumer batch");
   if (owns_cons_) {
+    if (dev_.gpu()) {
+      dev_.bind();
+      complete_locked();  // batches in flight still write the worker-owned buffers
+    }
     dev_.free(cons_hwc_);
     dev_.free(cons_chw_);
   }
@@ -363,7 +387,17 @@ Worker::~Worker() {
     dev_.free(cons_hwc_);
     dev_.free(cons_chw_);
   }
-  for (Lane& ln : lanes_) {
+  for (auto& lp : lanes_) {
+    Lane& ln = *lp;
+    {
+      std::lock_guard<std::mutex> g(ln.mu);
+      ln.stop = true;
+    }
+    ln.cv.notify_all();
+    if (ln.th.joinable()) ln.th.join();
+  }
+  for (auto& lp : lanes_) {
+    Lane& ln = *lp;
     for (Stage& st : ln.stage) {
       dev_.free_pinned(st.err);
       if (st.h) hostmem::unregister_range(st.h);
@@ -394,10 +428,10 @@ int Worker::add_camera(const std::string& name, int ring_slots) {
     idx = int(cams_.size());
     cams_.emplace_back();
   }
-  // `stages` batches may be in flight on the GPU: keep one more slot so the newest committed
-  // frame stays readable while they are written
-  cams_[size_t(idx)] =
-      std::make_shared<Camera>(*this, idx, name, std::max(dev_.gpu() ? stages_ + 1 : 1, ring_slots));
+  // `stages` batches may be in flight on the GPU (+ the lane thread's queue and the batch it is
+  // launching): keep one more slot so the newest committed frame stays readable meanwhile
+  const int min_slots = dev_.gpu() ? inflight() + (threaded_ ? 2 : 1) : 1;
+  cams_[size_t(idx)] = std::make_shared<Camera>(*this, idx, name, std::max(min_slots, ring_slots));
   return idx;
 }
 
@@ -895,9 +929,9 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
                            std::min(kPackChunk, segs[g].len - o)});
         src = hostmem::device_address(st.h + dst_off, segs[g].len);
         VEP_CHECK(src, "staging buffer is not registered");
-        pinned_bytes_staged_ += segs[g].len;
+        pinned_bytes_staged_ += u64(segs[g].len);
       } else {
-        pinned_bytes_inplace_ += segs[g].len;
+        pinned_bytes_inplace_ += u64(segs[g].len);
       }
       seg_dev[size_t(i)].push_back(src);
       if (!direct)
@@ -923,12 +957,12 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     else for (int i = 0; i < n; ++i) index(i);
   }
   const i64 t_copy0 = mono_us();
-  timers.index += double(t_copy0 - t_index0);
+  add_time(&Timers::index, double(t_copy0 - t_index0));
   auto copy = [&](int t) { std::memcpy(tasks[size_t(t)].dst, tasks[size_t(t)].src, tasks[size_t(t)].len); };
   if (pack_pool_ && tasks.size() > 1) pack_pool_->parallel_for(int(tasks.size()), copy);
   else for (int t = 0; t < int(tasks.size()); ++t) copy(t);
   const i64 t_enq0 = mono_us();
-  timers.copy += double(t_enq0 - t_copy0);
+  add_time(&Timers::copy, double(t_enq0 - t_copy0));
 
   if (st.err_cap < size_t(n)) {
     if (st.err) dev_.free_pinned(st.err);
@@ -987,11 +1021,11 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       l.src_h = j.pic.height;
       l.crop_left = j.pic.crop_left;
       l.crop_top = j.pic.crop_top;
-      VEP_CHECK(j.cam < cons_rows_, "camera index exceeds consumer batch rows");
-      l.out_hwc = cons_hwc_ ? cons_hwc_ + size_t(j.cam) * gpu::letterbox_bytes(int(S), opt_.letterbox_format)
+      VEP_CHECK(j.cam < st.cons_rows, "camera index exceeds consumer batch rows");
+      l.out_hwc = st.cons_hwc ? st.cons_hwc + size_t(j.cam) * gpu::letterbox_bytes(int(S), opt_.letterbox_format)
                             : nullptr;
       const size_t es = opt_.chw_dtype == gpu::kChwF32 ? 4 : 2;
-      l.out_chw = cons_chw_ ? static_cast<u8*>(cons_chw_) + size_t(j.cam) * 3 * S * S * es
+      l.out_chw = st.cons_chw ? static_cast<u8*>(st.cons_chw) + size_t(j.cam) * 3 * S * S * es
                             : nullptr;
       gpu::fill_letterbox_geometry(l, opt_.letterbox_size, opt_.letterbox_format == gpu::kLbNV12);
     }
@@ -1076,7 +1110,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
                           cs);
   }
   VEP_HIP(hipEventRecord(st.e1, cs));
-  timers.enqueue += double(mono_us() - t_enq0);
+  add_time(&Timers::enqueue, double(mono_us() - t_enq0));
 }
 
 void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
@@ -1169,8 +1203,13 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
 
 double Worker::gpu_ms_total() const {
   double m = 0;
-  for (const Lane& ln : lanes_) m = std::max(m, ln.gpu_ms);
+  for (const auto& lp : lanes_) m = std::max(m, lp->gpu_ms.load());
   return m;
+}
+
+void Worker::add_time(double Timers::*f, double us) {
+  std::lock_guard<std::mutex> g(timers_mu_);
+  timers.*f += us;
 }
 
 void Worker::complete(Lane& ln, Stage& st) {
@@ -1181,25 +1220,140 @@ void Worker::complete(Lane& ln, Stage& st) {
     trace::Range tr("vep.wait_gpu");
     VEP_HIP(hipEventSynchronize(st.e1));
   }
-  timers.wait += double(mono_us() - t0);
+  add_time(&Timers::wait, double(mono_us() - t0));
   float ms = 0;
-  if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) ln.gpu_ms += ms;
+  if (hipEventElapsedTime(&ms, st.e0, st.e1) == hipSuccess) ln.gpu_ms.store(ln.gpu_ms.load() + ms);
   publish(st.jobs, st.slots, st.err);
   st.jobs.clear();
   st.slots.clear();
+  {
+    std::lock_guard<std::mutex> g(pub_mu_);
+    if (!ln.unpublished.empty() && ln.unpublished.front() == st.seq) ln.unpublished.pop_front();
+  }
+  pub_cv_.notify_all();
+}
+
+void Worker::launch_on(Lane& ln, Batch&& b) {
+  Stage& st = ln.stage[size_t(ln.next)];
+  ln.next = (ln.next + 1) % int(ln.stage.size());
+  complete(ln, st);  // this lane's oldest batch (`stages` launches ago): its staging is reused
+  st.jobs.swap(b.jobs);
+  st.slots.swap(b.slots);
+  st.seq = b.seq;
+  st.cons_hwc = b.cons_hwc;
+  st.cons_chw = b.cons_chw;
+  st.cons_rows = b.cons_rows;
+  try {
+    launch_gpu(ln, st);
+  } catch (...) {
+    // the batch is dropped: give its ring slots back and count it as published
+    {
+      std::lock_guard<std::mutex> g(cams_mu_);
+      for (size_t i = 0; i < st.jobs.size(); ++i) {
+        auto& cp = cams_[size_t(st.jobs[i].cam)];
+        if (cp && cp->ring_) cp->ring_->abort(st.slots[i]);
+      }
+    }
+    st.jobs.clear();
+    st.slots.clear();
+    {
+      std::lock_guard<std::mutex> g(pub_mu_);
+      if (!ln.unpublished.empty() && ln.unpublished.front() == st.seq) ln.unpublished.pop_front();
+    }
+    pub_cv_.notify_all();
+    throw;
+  }
+  st.active = true;
+}
+
+// Launcher thread of one lane: launches the batches handed over by launch_async, each after
+// its staging buffer's previous batch is complete and published, so a lane waiting on a slow
+// batch (a keyframe's intra wavefront) never holds back the other lanes.
+void Worker::lane_loop(Lane& ln) {
+  dev_.bind();
+  auto keep_error = [&] {
+    std::lock_guard<std::mutex> g(pub_mu_);
+    if (!lane_err_) lane_err_ = std::current_exception();
+  };
+  std::unique_lock<std::mutex> lk(ln.mu);
+  for (;;) {
+    ln.cv.wait(lk, [&] { return ln.stop || ln.drain || !ln.q.empty(); });
+    if (!ln.q.empty()) {
+      Batch b = std::move(ln.q.front());
+      ln.q.pop_front();
+      ln.busy = true;
+      lk.unlock();
+      ln.cv.notify_all();  // room for the next batch
+      try {
+        launch_on(ln, std::move(b));
+      } catch (...) {
+        keep_error();
+      }
+      lk.lock();
+      ln.busy = false;
+      ln.cv.notify_all();
+      continue;
+    }
+    if (ln.drain) {
+      lk.unlock();
+      try {
+        for (size_t k = 0; k < ln.stage.size(); ++k)
+          complete(ln, ln.stage[(size_t(ln.next) + k) % ln.stage.size()]);
+      } catch (...) {
+        keep_error();
+      }
+      lk.lock();
+      ln.drain = false;
+      ln.cv.notify_all();
+      continue;
+    }
+    if (ln.stop) return;
+  }
+}
+
+void Worker::drain_lanes() {
+  for (auto& lp : lanes_) {
+    std::lock_guard<std::mutex> g(lp->mu);
+    lp->drain = true;
+  }
+  for (auto& lp : lanes_) lp->cv.notify_all();
+  for (auto& lp : lanes_) {
+    Lane& ln = *lp;
+    std::unique_lock<std::mutex> lk(ln.mu);
+    ln.cv.wait(lk, [&] { return !ln.drain && ln.q.empty() && !ln.busy; });
+  }
+  std::exception_ptr e;
+  {
+    std::lock_guard<std::mutex> g(pub_mu_);
+    std::swap(e, lane_err_);
+  }
+  if (e) std::rethrow_exception(e);
 }
 
 void Worker::complete_locked() {
+  if (threaded_) {
+    drain_lanes();
+    return;
+  }
   // oldest first: Lane::next names the stage that will be reused next, i.e. the oldest batch
-  for (Lane& ln : lanes_)
-    for (size_t k = 0; k < ln.stage.size(); ++k)
-      complete(ln, ln.stage[(size_t(ln.next) + k) % ln.stage.size()]);
+  for (auto& lp : lanes_)
+    for (size_t k = 0; k < lp->stage.size(); ++k)
+      complete(*lp, lp->stage[(size_t(lp->next) + k) % lp->stage.size()]);
 }
 
 void Worker::complete_all() {
   std::lock_guard<std::mutex> lg(launch_mu_);
   if (dev_.gpu()) dev_.bind();
   complete_locked();
+}
+
+void Worker::wait_published(u64 seq) {
+  std::unique_lock<std::mutex> g(pub_mu_);
+  pub_cv_.wait(g, [&] {
+    for (const auto& lp : lanes_)
+      if (!lp->unpublished.empty() && lp->unpublished.front() <= seq) return false;
+    return true;
+  });
 }
 
 void Worker::launch_async(std::vector<DecodeJob>& jobs) {
@@ -1210,7 +1364,7 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
   std::vector<int> slots;
   const i64 t0 = mono_us();
   prepare(jobs, slots);
-  timers.prepare += double(mono_us() - t0);
+  add_time(&Timers::prepare, double(mono_us() - t0));
   if (jobs.empty()) return;
   if (!dev_.gpu()) {
     std::vector<u32> err;
@@ -1228,22 +1382,32 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
     ls[g].push_back(slots[i]);
   }
   jobs.clear();
+  const u64 seq = ++launch_seq_;
   for (size_t g = 0; g < nl; ++g) {
     if (lj[g].empty()) continue;
-    Lane& ln = lanes_[g];
-    Stage& st = ln.stage[size_t(ln.next)];
-    ln.next = (ln.next + 1) % int(ln.stage.size());
-    complete(ln, st);  // this lane's oldest batch (`stages` launches ago): its staging is reused
-    st.jobs.swap(lj[g]);
-    st.slots.swap(ls[g]);
-    try {
-      launch_gpu(ln, st);
-    } catch (...) {
-      st.jobs.clear();
-      st.slots.clear();
-      throw;
+    Lane& ln = *lanes_[g];
+    {
+      std::lock_guard<std::mutex> pg(pub_mu_);
+      ln.unpublished.push_back(seq);
     }
-    st.active = true;
+    Batch b{std::move(lj[g]), std::move(ls[g]), seq, cons_hwc_, cons_chw_, cons_rows_};
+    if (!threaded_) {
+      launch_on(ln, std::move(b));
+      continue;
+    }
+    std::unique_lock<std::mutex> lk(ln.mu);
+    ln.cv.wait(lk, [&] { return int(ln.q.size()) < queue_; });  // bounded per-lane backlog
+    ln.q.push_back(std::move(b));
+    lk.unlock();
+    ln.cv.notify_all();
+  }
+  if (threaded_) {
+    std::exception_ptr e;
+    {
+      std::lock_guard<std::mutex> g(pub_mu_);
+      std::swap(e, lane_err_);
+    }
+    if (e) std::rethrow_exception(e);
   }
 }
 

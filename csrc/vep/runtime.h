@@ -12,6 +12,7 @@
 
 #include <condition_variable>
 #include <deque>
+#include <exception>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -207,6 +208,11 @@ struct WorkerOptions {
   // Batches in flight per lane (staging buffers): launch_async blocks only when its lane still
   // runs the batch from `stages` launches ago. 0 = VEP_STAGES or the default.
   int stages = 0;
+  // Batches a lane's launcher thread may have queued behind its in-flight ones (several lanes):
+  // how far the other lanes can run ahead of one held up by a slow batch. 0 = VEP_LANE_QUEUE or
+  // the default.
+  int queue = 0;
+  bool lane_threads = false;  // one launcher thread per lane (also VEP_LANE_THREADS=1)
 };
 
 class Worker {
@@ -253,10 +259,17 @@ class Worker {
   int lanes() const { return int(lanes_.size()); }
   // batches in flight per lane: a launch publishes the batch from this many launches ago
   int stages() const { return stages_; }
+  // batches launch_async may have handed over but not yet published, per lane
+  int inflight() const { return stages_ + (threaded_ ? queue_ : 0); }
+  // Every launch_async() with work gets a sequence number (launch_seq() after it returns).
+  // With several lanes each lane has its own launcher thread, so a batch's frames are published
+  // asynchronously: wait_published(s) blocks until every batch with sequence <= s is published.
+  u64 launch_seq() const { return launch_seq_.load(); }
+  void wait_published(u64 seq);
   u64 batches() const { return batches_.load(); }
   // slice bytes the GPU read in place from pinned AU blocks vs. staged by a host memcpy
-  u64 bytes_inplace() const { return pinned_bytes_inplace_; }
-  u64 bytes_staged() const { return pinned_bytes_staged_; }
+  u64 bytes_inplace() const { return pinned_bytes_inplace_.load(); }
+  u64 bytes_staged() const { return pinned_bytes_staged_.load(); }
   u64 frames() const { return frames_.load(); }
   // GPU time of the batches (first event to last, per lane; the busiest lane's total)
   double gpu_ms_total() const;
@@ -271,6 +284,10 @@ class Worker {
     hipEvent_t copied = nullptr, e0 = nullptr, e1 = nullptr;
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;
+    u64 seq = 0;               // launch sequence of the batch
+    u8* cons_hwc = nullptr;    // consumer batch at launch time (set_consumer_buffers may move on)
+    void* cons_chw = nullptr;
+    int cons_rows = 0;
     bool active = false;
     u32* err = nullptr;        // pinned per-job check flags (written by the kernel)
     const u32* err_dev = nullptr;
@@ -278,14 +295,32 @@ class Worker {
   };
   void loop();
   void ensure_surface(Camera& c, const PictureInfo& pi, int slots);
+  struct Batch {
+    std::vector<DecodeJob> jobs;
+    std::vector<int> slots;
+    u64 seq = 0;
+    u8* cons_hwc = nullptr;
+    void* cons_chw = nullptr;
+    int cons_rows = 0;
+  };
   struct Lane {
     hipStream_t stream = nullptr;  // lane 0 uses Worker::stream_
     std::vector<Stage> stage;      // ring of staging buffers (Worker::stages() deep)
     int next = 0;                  // the stage reused next (the oldest in-flight batch)
-    double gpu_ms = 0;             // cumulative batch time on this lane
+    std::atomic<double> gpu_ms{0}; // cumulative batch time on this lane
+    // launcher thread (several lanes): batches handed over by launch_async
+    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<Batch> q;
+    bool busy = false, drain = false, stop = false;
+    std::deque<u64> unpublished;   // sequences given to this lane, not yet published (pub_mu_)
   };
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
   void launch_gpu(Lane& ln, Stage& st);
+  void lane_loop(Lane& ln);
+  void launch_on(Lane& ln, Batch&& b);  // reuse the lane's oldest stage for batch b
+  void drain_lanes();
   void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err);
   // err[i] != 0: job i failed its speculative-header check (dropped, camera waits for the
   // next keyframe)
@@ -297,17 +332,27 @@ class Worker {
   hipStream_t stream_ = nullptr, copy_stream_ = nullptr, serve_stream_ = nullptr;
   mutable std::mutex cams_mu_;
   std::vector<std::shared_ptr<Camera>> cams_;
-  std::vector<Lane> lanes_;
+  std::vector<std::unique_ptr<Lane>> lanes_;
   int stages_ = 2;
+  bool threaded_ = false;        // one launcher thread per lane
+  int queue_ = 0;                // lane queue depth (threaded)
+  std::atomic<u64> launch_seq_{0};
+  std::mutex pub_mu_;
+  std::condition_variable pub_cv_;
+  std::exception_ptr lane_err_;  // first error of a lane thread, rethrown to the launcher
   std::unique_ptr<ThreadPool> pack_pool_;
 
  public:
-  // host-side launch path timers (µs, cumulative): where a batch's CPU time goes
-  struct Timers {
+  // host-side launch path timers (µs, cumulative): where a batch's CPU time goes (summed over
+  // lane threads)
+  struct Timers_ {
     double prepare = 0, index = 0, copy = 0, enqueue = 0, wait = 0;
-  } timers;
+  };
+  using Timers = Timers_;
+  Timers timers;
 
  private:
+  void add_time(double Timers_::*f, double us);
   u8* h_serve_ = nullptr;
   size_t serve_cap_ = 0;
   std::mutex serve_mu_;
@@ -323,7 +368,8 @@ class Worker {
   std::thread th_;
   std::mutex launch_mu_;
   std::atomic<u64> batches_{0}, frames_{0};
-  u64 pinned_bytes_inplace_ = 0, pinned_bytes_staged_ = 0;
+  std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0};
+  std::mutex timers_mu_;
   bool direct_reads_ = false;
   u64* avc_prof_ = nullptr;
 
