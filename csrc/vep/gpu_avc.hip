@@ -165,7 +165,7 @@ __device__ inline bool avail_hdr(const AvcDesc& d, const uint4& h, bool in_pic, 
 // One intra MB, whole wave: one round trip of global loads (all issued before any is used),
 // a parallel residual pass, then prediction out of LDS.
 __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, int row, bool carry,
-                         int lane, u64 t_start, u64* acc) {
+                         int lane, const u32* tap_lut, u64 t_start, u64* acc) {
   const int W = d.wmbs, pitch = W * 16;
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
@@ -304,12 +304,11 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       L.tile[((p >> 4) + 1) * kTp + (p & 15) + 1] = out[k];
     }
   } else {
-    // Tap words of all 256 samples in one parallel pass (the mode divergence is paid once)
-#pragma unroll 1
+    // Tap words of all 256 samples: one lookup each in the per-workgroup (mode, x, y) table
     for (int k = 0; k < 4; ++k) {
       const int p = lane + 64 * k, px = p & 15, py = p >> 4;
       const int mode = avc::i4_mode(m, (py >> 2) * 4 + (px >> 2));
-      L.taps[p] = mode == 2 ? avc::kTapDc : avc::pack_taps(avc::intra4x4_taps(mode, px & 3, py & 3));
+      L.taps[p] = tap_lut[mode * 16 + (py & 3) * 4 + (px & 3)];
     }
     wave_sync();
     // Diagonal schedule: block (bx, by) only reads left / top / top-left / (when available in
@@ -409,9 +408,14 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
 __global__ __launch_bounds__(1024) void avc_intra_kernel(const AvcDesc* __restrict__ descs) {
   __shared__ Sync sync;
   __shared__ IntraWave lds[kWaves];
+  __shared__ u32 tap_lut[9 * 16];  // Intra_4x4 tap word per (mode, y, x) of a 4x4 block
   const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs;
-  sync_init(sync, H);
+  for (int t = int(threadIdx.x); t < 9 * 16; t += int(blockDim.x)) {
+    const int mode = t >> 4, y = (t >> 2) & 3, x = t & 3;
+    tap_lut[t] = mode == 2 ? avc::kTapDc : avc::pack_taps(avc::intra4x4_taps(mode, x, y));
+  }
+  sync_init(sync, H);  // (its barrier also publishes the table)
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   IntraWave& L = lds[wave];
   const MbRec* recs = static_cast<const MbRec*>(d.mbs);
@@ -439,7 +443,7 @@ __global__ __launch_bounds__(1024) void avc_intra_kernel(const AvcDesc* __restri
         publish_row(sync, row, u32(xx));  // every MB left of xx is final
         if (row > 0) wait_row(sync, row - 1, u32(xx + 2 < W ? xx + 2 : W), d.err);
         const u64 t1 = d.prof ? clock64() : 0;
-        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, t1, acc);
+        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, t1, acc);
         prev = xx;
         acc[0] += t1 - t0;
       }
