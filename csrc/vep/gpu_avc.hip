@@ -304,11 +304,27 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       L.tile[((p >> 4) + 1) * kTp + (p & 15) + 1] = out[k];
     }
   } else {
-    // Tap words of all 256 samples: one lookup each in the per-workgroup (mode, x, y) table
+    // Tap words of all 256 samples: the (mode, y, x) table entry with its neighbour indices
+    // resolved to tile offsets from the block's top-left neighbour (top-right substitution and
+    // availability folded in), so the dependent steps below are plain loads + one multiply-add.
+    //   non-DC: bits 0-6 / 7-13 / 14-20 offsets, 21-30 weights/add/shift; DC: bit 31, 21 top
+    //   available, 22 left available
     for (int k = 0; k < 4; ++k) {
-      const int p = lane + 64 * k, px = p & 15, py = p >> 4;
-      const int mode = avc::i4_mode(m, (py >> 2) * 4 + (px >> 2));
-      L.taps[p] = tap_lut[mode * 16 + (py & 3) * 4 + (px & 3)];
+      const int p = lane + 64 * k, px = p & 15, py = p >> 4, bx = px >> 2, byy = py >> 2;
+      const int r = byy * 4 + bx;
+      const u32 tw = tap_lut[avc::i4_mode(m, r) * 16 + (py & 3) * 4 + (px & 3)];
+      u32 word;
+      if (tw & avc::kTapDc) {
+        word = 1u << 31 | u32(byy > 0 || B) << 21 | u32(bx > 0 || A) << 22;
+      } else {
+        const bool tr = byy == 0 ? (bx < 3 ? B : C)
+                                 : (bx < 3 && avc::raster_to_blk((byy - 1) * 4 + bx + 1) < avc::raster_to_blk(r));
+        auto rel = [&](u32 n) -> u32 {
+          return n == 0 ? 0u : n <= 8 ? 1u + ((n - 1 >= 4 && !tr) ? 3u : n - 1) : (n - 8) * u32(kTp);
+        };
+        word = rel(tw & 15) | rel((tw >> 4) & 15) << 7 | rel((tw >> 8) & 15) << 14 | ((tw >> 12) & 1023u) << 21;
+      }
+      L.taps[p] = word;
     }
     wave_sync();
     // Diagonal schedule: block (bx, by) only reads left / top / top-left / (when available in
@@ -317,40 +333,30 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     const int g = lane >> 4, i = (lane >> 2) & 3, j = lane & 3;
 #pragma unroll 1
     for (int st = 0; st < 10; ++st) {
-      const int by = g == 0 ? (st >= 6 ? st / 2 - 1 : st / 2 - (st >= 2 ? 0 : 0)) : 0;
       // blocks of diagonal st: (st - 2*yy, yy) for yy = max(0, (st - 3 + 1) / 2) .. min(3, st / 2)
       const int y_lo = st > 3 ? (st - 2) / 2 : 0, y_hi = st / 2 < 3 ? st / 2 : 3;
       const int yy = y_lo + g;
-      (void)by;
       if (g < 2 && yy <= y_hi) {
-        const int bx = st - 2 * yy, byy = yy;
-        const int r = byy * 4 + bx, idx = avc::raster_to_blk(r);
-        const bool tr = byy == 0 ? (bx < 3 ? B : C) : (bx < 3 && avc::raster_to_blk((byy - 1) * 4 + bx + 1) < idx);
-        const bool ht = byy > 0 || B, hl = bx > 0 || A;
-        // tile index of neighbour N[k] of this block (top-right substitution folded in)
-        auto nidx = [&](int k) {
-          if (k == 0) return (byy * 4) * kTp + bx * 4;
-          if (k <= 8) return (byy * 4) * kTp + bx * 4 + 1 + (k - 1 >= 4 && !tr ? 3 : k - 1);
-          return (byy * 4 + k - 8) * kTp + bx * 4;
-        };
-        const int p = (byy * 4 + i) * 16 + bx * 4 + j;
-        const u32 tp = L.taps[p];
+        const int bx = st - 2 * yy;
+        const int p = (yy * 4 + i) * 16 + bx * 4 + j;
+        const u32 tw = L.taps[p];
+        const u8* nb = &L.tile[(yy * 4) * kTp + bx * 4];  // neighbour N[0] (top-left) of the block
         int v;
-        if (tp & avc::kTapDc) {
+        if (tw >> 31) {
           int st4 = 0, sl4 = 0;
           for (int q = 0; q < 4; ++q) {
-            st4 += L.tile[nidx(1 + q)];
-            sl4 += L.tile[nidx(9 + q)];
+            st4 += nb[1 + q];
+            sl4 += nb[(q + 1) * kTp];
           }
+          const bool ht = (tw >> 21) & 1, hl = (tw >> 22) & 1;
           v = ht && hl ? (st4 + sl4 + 4) >> 3 : hl ? (sl4 + 2) >> 2 : ht ? (st4 + 2) >> 2 : 128;
         } else {
-          const int n0 = L.tile[nidx(int(tp & 15))], n1 = L.tile[nidx(int((tp >> 4) & 15))],
-                    n2 = L.tile[nidx(int((tp >> 8) & 15))];
-          v = (int((tp >> 12) & 3) * n0 + int((tp >> 14) & 3) * n1 + int((tp >> 16) & 3) * n2 +
-               int((tp >> 18) & 3)) >> int((tp >> 20) & 3);
+          const int n0 = nb[tw & 127], n1 = nb[(tw >> 7) & 127], n2 = nb[(tw >> 14) & 127];
+          v = (int((tw >> 21) & 3) * n0 + int((tw >> 23) & 3) * n1 + int((tw >> 25) & 3) * n2 +
+               int((tw >> 27) & 3)) >> int((tw >> 29) & 3);
         }
         v += L.res[p];
-        L.tile[(byy * 4 + i + 1) * kTp + bx * 4 + j + 1] = u8(avc::clip1(v));
+        L.tile[(yy * 4 + i + 1) * kTp + bx * 4 + j + 1] = u8(avc::clip1(v));
       }
       wave_sync();
     }
