@@ -563,50 +563,68 @@ VEP_HD EdgeParams edge_params(int qp_p, int qp_q, int off_a, int off_b) {
 // Filter one line of samples across an edge: s points at q0, `step` is the distance between
 // successive samples across the edge (1 for a vertical edge, pitch for a horizontal one).
 // chroma lines use the two-sample filters (§8.7.2.3 / §8.7.2.4).
-// Core of filter_line with the edge's thresholds as scalars: tc0 = tC0 of this line's bS
-// (ignored for bS 4).
-template <typename Px>
-VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0, bool chroma) {
-  const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
-  if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return;
+// Filter one sample line in registers: p[k] = p_k, q[k] = q_k (k = 0..3; chroma uses k < 2).
+// Returns false (nothing changed) when the edge is not filtered at this line. tc0 = tC0 of
+// the line's bS (ignored for bS 4).
+VEP_HD bool filter_samples(int* p, int* q, int bs, int alpha, int beta, int tc0, bool chroma) {
+  const int p0 = p[0], p1 = p[1], q0 = q[0], q1 = q[1];
+  if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return false;
   if (chroma) {
     if (bs < 4) {
       const int tc = tc0 + 1;
       const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-      s[-step] = Px(clip1(p0 + d));
-      s[0] = Px(clip1(q0 - d));
+      p[0] = clip1(p0 + d);
+      q[0] = clip1(q0 - d);
     } else {
-      s[-step] = Px((2 * p1 + p0 + q1 + 2) >> 2);
-      s[0] = Px((2 * q1 + q0 + p1 + 2) >> 2);
+      p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
+      q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
     }
-    return;
+    return true;
   }
-  const int p2 = s[-3 * step], q2 = s[2 * step];
+  const int p2 = p[2], q2 = q[2];
   const int ap = iabs(p2 - p0), aq = iabs(q2 - q0);
   if (bs < 4) {
     const int tc = tc0 + (ap < beta) + (aq < beta);
     const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-    s[-step] = Px(clip1(p0 + d));
-    s[0] = Px(clip1(q0 - d));
-    if (ap < beta) s[-2 * step] = Px(p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1));
-    if (aq < beta) s[step] = Px(q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1));
-    return;
+    p[0] = clip1(p0 + d);
+    q[0] = clip1(q0 - d);
+    if (ap < beta) p[1] = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
+    if (aq < beta) q[1] = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
+    return true;
   }
-  const int p3 = s[-4 * step], q3 = s[3 * step];
+  const int p3 = p[3], q3 = q[3];
   const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
   if (ap < beta && strong) {
-    s[-step] = Px((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3);
-    s[-2 * step] = Px((p2 + p1 + p0 + q0 + 2) >> 2);
-    s[-3 * step] = Px((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3);
+    p[0] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+    p[1] = (p2 + p1 + p0 + q0 + 2) >> 2;
+    p[2] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
   } else {
-    s[-step] = Px((2 * p1 + p0 + q1 + 2) >> 2);
+    p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
   }
   if (aq < beta && strong) {
-    s[0] = Px((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3);
-    s[step] = Px((p0 + q0 + q1 + q2 + 2) >> 2);
-    s[2 * step] = Px((2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3);
+    q[0] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+    q[1] = (p0 + q0 + q1 + q2 + 2) >> 2;
+    q[2] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
   } else {
-    s[0] = Px((2 * q1 + q0 + p1 + 2) >> 2);
+    q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
+  }
+  return true;
+}
+
+// filter_samples on samples in memory (stride `step` across the edge; s = q0).
+template <typename Px>
+VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0, bool chroma) {
+  const int n = chroma ? 2 : 4;
+  int p[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
+  for (int k = 0; k < n; ++k) {
+    p[k] = s[-(k + 1) * step];
+    q[k] = s[k * step];
+  }
+  if (!filter_samples(p, q, bs, alpha, beta, tc0, chroma)) return;
+  const int m = chroma ? 1 : 3;
+  for (int k = 0; k < m; ++k) {
+    s[-(k + 1) * step] = Px(p[k]);
+    s[k * step] = Px(q[k]);
   }
 }
 
