@@ -994,7 +994,32 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
   }
   pic->info.coded_mbs = pic->nmbs() - missing;
   if (first.nal_ref_idc != 0) mark_references(first, *act_sps, pic->target);
+  validate(*pic);
   return pic;
+}
+
+void validate(const Picture& p) {
+  VEP_CHECK(p.dpb_slots >= 1 && p.dpb_slots <= kMaxDpbSlots && p.target >= 0 && p.target < p.dpb_slots,
+            "picture DPB slots out of range");
+  VEP_CHECK(p.wmbs > 0 && p.hmbs > 0 && p.mbs.size() == size_t(p.nmbs()), "picture size mismatch");
+  const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size() / 32;
+  for (const MbRec& m : p.mbs) {
+    VEP_CHECK(m.kind <= kIPcm, "macroblock kind out of range");
+    VEP_CHECK(m.qp <= 51 && m.qpc <= 51, "macroblock QP out of range");
+    if (m.kind == kIPcm) {
+      VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 32 <= nblocks, "I_PCM samples outside the pool");
+      continue;
+    }
+    const size_t nb = size_t(__builtin_popcount(m.luma_coded)) + size_t(__builtin_popcount(m.chroma_coded));
+    VEP_CHECK(size_t(m.coef) + nb <= nblocks, "coefficient blocks outside the pool");
+    VEP_CHECK(m.chroma_mode <= 3 && m.i16_mode <= 3, "intra prediction mode out of range");
+    if (m.kind == kSkip || m.kind == kInter) {
+      VEP_CHECK(size_t(m.mv) + 1 <= nmv, "motion vectors outside the pool");
+      for (u8 r : m.ref) VEP_CHECK(int(r) < p.dpb_slots, "reference slot outside the DPB");
+    } else if (m.kind == kI4x4) {
+      for (u8 b : m.i4) VEP_CHECK((b & 15) <= 8 && (b >> 4) <= 8, "Intra_4x4 mode out of range");
+    }
+  }
 }
 
 // ------------------------------------------------------------------------- shared internals

@@ -51,6 +51,12 @@ struct Picture {
 };
 using PicturePtr = std::shared_ptr<const Picture>;
 
+// Structural invariants the reconstruction kernels rely on: every record's coefficient-pool and
+// motion-vector indices lie inside the picture's pools, reference / target slots inside the
+// DPB, modes in range. Throws Error otherwise (defence in depth against a parser bug on hostile
+// input: the GPU kernels index with these values unchecked).
+void validate(const Picture& p);
+
 // Full slice header (the fields reconstruction needs).
 struct SliceHdr {
   int nal_type = 0, nal_ref_idc = 0;

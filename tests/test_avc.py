@@ -89,3 +89,45 @@ def test_cabac_stream_reports_unsupported(native):
     bad = native.AccessUnit.from_nals([nals[0], bytes(pps)] + nals[2:], keyframe=True)
     with pytest.raises(native.UnsupportedStream):
         native.CpuDecoder().decode(bad)
+
+
+def test_corrupt_slices_never_crash_and_recover_at_idr(native):
+    """Bit errors in slice data (as on a lossy RTSP link): every corrupted access unit either
+    raises (the camera drops it and waits for a keyframe) or yields a picture that passed
+    avc::validate (all pool / DPB indices the GPU kernels use are in range); decoding is bit-exact
+    again from the next IDR on."""
+    import random
+
+    rnd = random.Random(7)
+    gop = 6
+    clean = synth(native, 176, 144, gop=gop, seed=11, compressed=True, coverage=True, refs=2, slices=2)
+    aus = [clean.next() for _ in range(4 * gop)]
+    ref = native.CpuDecoder()
+    want = [ref.decode(a) for a in aus]
+    raised = decoded = 0
+    for trial in range(24):
+        dec = native.CpuDecoder()
+        bad_at = rnd.randrange(1, 3 * gop)
+        for i, au in enumerate(aus):
+            if i == bad_at:
+                nals = [bytearray(n) for n in au.nals()]
+                slice_ix = [k for k, n in enumerate(nals) if (n[0] & 0x1F) in (1, 5)]
+                n = nals[rnd.choice(slice_ix)]
+                for _ in range(rnd.randint(1, 6)):
+                    pos = rnd.randrange(2, len(n))
+                    n[pos] ^= 1 << rnd.randrange(8)
+                au = native.AccessUnit.from_nals([bytes(x) for x in nals], keyframe=au.keyframe)
+            try:
+                got = dec.decode(au)
+            except Exception:  # corrupt picture rejected
+                if i == bad_at:
+                    raised += 1
+                    continue
+                if i > bad_at and i % gop != 0:
+                    continue  # references poisoned until the next IDR
+                raise
+            if i == bad_at:
+                decoded += 1
+            if i >= (bad_at // gop + 1) * gop:  # from the next IDR on: bit-exact again
+                assert np.array_equal(got, want[i]), f"trial {trial}: frame {i} after IDR differs"
+    assert raised + decoded == 24
