@@ -977,6 +977,7 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
     if (nb_.at(mb).kind != 0xFF) continue;
     ++missing;
     m = MbRec{};
+    m.res = kNoRes;
     m.dbk = 1;
     m.slice = u16(0xFFFF);
     if (!dpb_.empty()) {
@@ -1019,6 +1020,7 @@ void validate(const Picture& p) {
     } else if (m.kind == kI4x4) {
       for (u8 b : m.i4) VEP_CHECK((b & 15) <= 8 && (b >> 4) <= 8, "Intra_4x4 mode out of range");
     }
+    VEP_CHECK(m.res == kNoRes || (is_intra(m.kind) && m.res < u32(p.intra_res)), "residual slot out of range");
   }
 }
 
@@ -1132,6 +1134,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   } else {
     ++pic.intra_mbs;
   }
+  m.res = is_intra(m.kind) && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
   if (!(m.dbk & 1)) pic.deblock = true;
   pic.mbs[size_t(mb)] = m;
 }

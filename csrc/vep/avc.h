@@ -41,6 +41,7 @@ struct Picture {
   int dpb_slots = 1;          // surfaces the camera needs for this stream
   bool constrained_intra = false;
   int intra_mbs = 0;          // I4x4 / I16x16 MBs (need the wavefront pass)
+  int intra_res = 0;          // intra MBs with residual samples (MbRec::res slots)
   int inter_mbs = 0;          // skip / inter / I_PCM MBs (the parallel pass)
   bool deblock = false;       // any MB with the loop filter enabled
   bool idr = false;

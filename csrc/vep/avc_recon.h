@@ -57,9 +57,11 @@ struct MbRec {
                     // 384 raw sample bytes = 12 blocks)
   u32 mv;           // first of 16 (x, y) motion vectors (raster 4x4) in the mv pool
   u8 i4[8];         // Intra4x4PredMode per raster 4x4 block, 4 bits each (low nibble first)
-  u32 pad1;
+  u32 res;          // intra MBs with residual: slot of their 384 residual samples (GPU scratch,
+                    // filled by the parallel pass); kNoRes otherwise
 };
 static_assert(sizeof(MbRec) == 40, "MbRec layout");
+constexpr u32 kNoRes = 0xFFFFFFFFu;
 
 VEP_HD int i4_mode(const MbRec& m, int blk) { return (m.i4[blk >> 1] >> ((blk & 1) * 4)) & 15; }
 

@@ -90,11 +90,15 @@ struct AvcDesc {
   i32 pad;
   u32* err;            // pinned flag: wavefront timeout (frame dropped)
   void* dbk;           // device scratch: AvcDbkInfo[wmbs * hmbs] (avc_bs_kernel -> deblock)
+  i16* res;            // device scratch: kAvcResSamples per intra MB with residual (MbRec::res
+                       // slot; avc_inter_kernel -> avc_intra_kernel)
   u64* prof;           // optional (VEP_AVC_PROF=1): kAvcProfSlots clock64() phase accumulators
 };
 // Phase accumulators of the wavefront kernels (summed over waves): intra wait / load / luma /
 // chroma / store+publish / MBs, deblock wait / load / filter / store+publish / MBs.
 constexpr int kAvcProfSlots = 12;  // + [11] intra residual pass
+// Residual samples of one intra MB: 256 luma (raster) + 2 x 64 chroma, as i16.
+constexpr int kAvcResSamples = 384;
 // Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.
 struct AvcDbkInfo {
   u32 bs[4];      // 32 x 4-bit bS: nibble dir * 16 + edge * 4 + segment (0 = edge not filtered)

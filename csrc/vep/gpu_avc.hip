@@ -55,13 +55,26 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   const AvcDesc d = descs[lo];
   const int mb = g - d.mb_begin;
   const MbRec m = rec(d, mb);
+  const int t = int(threadIdx.x), x = t & 15, y = t >> 4;
+  const int cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;  // chroma lane (t < 128)
+  if (avc::is_intra(m.kind) && m.kind != avc::kIPcm) {
+    // Intra MB: its residual samples do not depend on the prediction, so they are computed here
+    // in parallel and the intra wavefront only adds them (same layout as IntraWave::res).
+    if (m.res == avc::kNoRes) return;
+    i16* r = d.res + size_t(m.res) * kAvcResSamples;
+    const int blk = (y >> 2) * 4 + (x >> 2);
+    r[t] = i16((m.luma_coded >> blk) & 1 ? avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3) : 0);
+    if (t < 128) {
+      const int k = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
+      r[256 + t] = i16((m.chroma_coded >> k) & 1 ? avc::idct4x4_at(chroma_block(d, m, k), cy & 3, cx & 3) : 0);
+    }
+    return;
+  }
   if (m.kind != avc::kSkip && m.kind != avc::kInter && m.kind != avc::kIPcm) return;
   const int W = d.wmbs, wpx = W * 16, hpx = d.hmbs * 16, pitch = wpx;
   const int mx = mb % W, my = mb / W;
   u8* ty = d.y + d.slot_y * u64(d.target);
   u8* tuv = d.uv + d.slot_uv * u64(d.target);
-  const int t = int(threadIdx.x), x = t & 15, y = t >> 4;
-  const int cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;  // chroma lane (t < 128)
   if (m.kind == avc::kIPcm) {
     const u8* s = reinterpret_cast<const u8*>(d.coefs + size_t(m.coef) * 16);
     ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = s[t];
@@ -145,9 +158,7 @@ constexpr int kCp = 12;  // chroma tile pitch: row 0 = p[-1..7, -1], rows 1..8 =
 
 struct alignas(16) IntraWave {
   MbRec rec[64];      // records of the current 64-MB chunk of the row
-  i16 coef[24 * 16];  // the MB's dequantised residual blocks (coded blocks only, pool order)
-  i16 res[384];       // residual samples: 256 luma (raster) + 2 x 64 chroma
-  int ftmp[24 * 16];  // inverse transform: row-pass intermediates
+  i16 res[384];       // residual samples: 256 luma (raster) + 2 x 64 chroma (from the inter pass)
   u32 taps[256];      // Intra_4x4 tap words of the MB's samples
   u8 tile[17 * kTp];  // luma neighbours + the MB being reconstructed (branch-free addressing)
   u8 ctile[2][9 * kCp];
@@ -173,9 +184,10 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   const bool up = row > 0, lf = x > 0;
   const MbRec* recs = static_cast<const MbRec*>(d.mbs);
   // ---- issue every load
-  const int nblk = __popc(m.luma_coded) + __popc(m.chroma_coded);
+  // residual samples (768 B = 48 lanes x 16 B), computed by the parallel inter pass
   uint4 cv = make_uint4(0, 0, 0, 0);
-  if (lane < 2 * nblk) cv = reinterpret_cast<const uint4*>(d.coefs + size_t(m.coef) * 16)[lane];
+  if (m.res != avc::kNoRes && lane < 48)
+    cv = reinterpret_cast<const uint4*>(d.res + size_t(m.res) * kAvcResSamples)[lane];
   u32 a = 128, b = 128;
   if (lane < 21) {  // luma row above: x0-1 .. x0+19
     const int px = x0 - 1 + lane;
@@ -206,7 +218,7 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   const bool C = __builtin_amdgcn_readlane(int(av), 57) != 0;
   const bool D = __builtin_amdgcn_readlane(int(av), 58) != 0;
   const bool A = __builtin_amdgcn_readlane(int(av), 59) != 0;
-  if (lane < 2 * nblk) reinterpret_cast<uint4*>(L.coef)[lane] = cv;
+  if (lane < 48) reinterpret_cast<uint4*>(L.res)[lane] = cv;  // zeros without residual
   if (lane < 21) {
     L.tile[lane] = u8((lane == 0 ? D : lane <= 16 ? B : C) ? a : 128u);
   } else if (lane < 37) {
@@ -222,54 +234,6 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   }
   wave_sync();
   const u64 t_loaded = d.prof ? clock64() : 0;
-  // ---- residual samples of every coded block (independent of prediction), as the two passes
-  // of the inverse transform: 24 blocks x 4 rows, then 24 blocks x 4 columns, 2 tasks per lane.
-  // Same integer operations as avc::idct4x4 (bit-exact).
-  auto coded = [&](int blk) {
-    return blk < 16 ? (m.luma_coded >> blk) & 1 : (m.chroma_coded >> (blk - 16)) & 1;
-  };
-  auto pool = [&](int blk) {
-    return blk < 16 ? __popc(m.luma_coded & ((1u << blk) - 1))
-                    : __popc(m.luma_coded) + __popc(m.chroma_coded & ((1u << (blk - 16)) - 1));
-  };
-#pragma unroll 1
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k, blk = t >> 2, i = t & 3;
-    if (blk < 24 && coded(blk)) {
-      const i16* dq = L.coef + pool(blk) * 16 + i * 4;
-      const int d0 = dq[0], d1 = dq[1], d2 = dq[2], d3 = dq[3];
-      const int e0 = d0 + d2, e1 = d0 - d2, e2 = (d1 >> 1) - d3, e3 = d1 + (d3 >> 1);
-      int* f = L.ftmp + blk * 16 + i * 4;
-      f[0] = e0 + e3;
-      f[1] = e1 + e2;
-      f[2] = e1 - e2;
-      f[3] = e0 - e3;
-    }
-  }
-  wave_sync();
-#pragma unroll 1
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k, blk = t >> 2, j = t & 3;
-    if (blk >= 24) continue;
-    int r[4] = {0, 0, 0, 0};
-    if (coded(blk)) {
-      const int* f = L.ftmp + blk * 16 + j;
-      const int f0 = f[0], f1 = f[4], f2 = f[8], f3 = f[12];
-      const int g0 = f0 + f2, g1 = f0 - f2, g2 = (f1 >> 1) - f3, g3 = f1 + (f3 >> 1);
-      r[0] = (g0 + g3 + 32) >> 6;
-      r[1] = (g1 + g2 + 32) >> 6;
-      r[2] = (g1 - g2 + 32) >> 6;
-      r[3] = (g0 - g3 + 32) >> 6;
-    }
-    if (blk < 16) {
-      const int bx = blk & 3, by = blk >> 2;
-      for (int i = 0; i < 4; ++i) L.res[(by * 4 + i) * 16 + bx * 4 + j] = i16(r[i]);
-    } else {
-      const int c = (blk - 16) >> 2, cb = (blk - 16) & 3, bx = cb & 1, by = cb >> 1;
-      for (int i = 0; i < 4; ++i) L.res[256 + c * 64 + (by * 4 + i) * 8 + bx * 4 + j] = i16(r[i]);
-    }
-  }
-  wave_sync();
   const u64 t_res = d.prof ? clock64() : 0;
   // ---- luma prediction
   auto P = [&](int ax, int ay) -> int { return L.tile[(ay + 1) * kTp + ax + 1]; };

@@ -837,7 +837,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   struct AvcPic {
     const avc::Picture* p;
     int job;
-    size_t off_mbs, off_coef, off_mv, off_dbk;
+    size_t off_mbs, off_coef, off_mv, off_dbk, off_res;
   };
   std::vector<AvcPic> apics;
   int rounds = 0;
@@ -851,7 +851,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       const avc::Picture& p = *v[size_t(r)];
       VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows && p.wmbs <= gpu::kAvcMaxCols,
                 "picture too large for the wavefront kernels");
-      AvcPic a{&p, i, 0, 0, 0, 0};
+      AvcPic a{&p, i, 0, 0, 0, 0, 0};
       a.off_mbs = need;
       need += al(p.mbs.size() * sizeof(avc::MbRec));
       a.off_coef = need;
@@ -876,9 +876,11 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     need += rel;
   }
   need = al(need);
-  for (AvcPic& a : apics) {  // device-only scratch (never copied): per-MB loop-filter inputs
-    a.off_dbk = need;
+  for (AvcPic& a : apics) {  // device-only scratch (never copied): per-MB loop-filter inputs,
+    a.off_dbk = need;         // intra MBs' residual samples (inter kernel -> intra wavefront)
     need += al(size_t(a.p->nmbs()) * sizeof(gpu::AvcDbkInfo));
+    a.off_res = need;
+    need += al(size_t(a.p->intra_res) * gpu::kAvcResSamples * sizeof(i16));
   }
   need = al(need);
   if (need > st.cap) {
@@ -1053,6 +1055,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.pad = 0;
       g.err = const_cast<u32*>(st.err_dev) + a.job;
       g.dbk = st.d + a.off_dbk;
+      g.res = reinterpret_cast<i16*>(st.d + a.off_res);
       g.prof = avc_prof_;
       mbs += a.p->nmbs();
     }
