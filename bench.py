@@ -47,8 +47,9 @@ ENTROPY = {"h264": "CAVLC macroblock-layer", "h265": "CABAC coding-tree"}
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=60)
-    ap.add_argument("--warmup", type=int, default=10)
+    # a tick takes ~4-5 ms: 300 timed ticks (10 GOPs of every camera) keep the number steady
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--cams-per-gpu", type=int, default=32)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)

@@ -5,7 +5,7 @@ set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 mkdir -p gpurun_out
-STEPS=${STEPS:-60}
+STEPS=${STEPS:-300}
 echo "[gpu_check] pytest -m gpu"
 timeout -k 10 420 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
@@ -13,7 +13,7 @@ echo "[gpu_check] smoke"
 timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
 tail -1 gpurun_out/smoke.log
 echo "[gpu_check] bench"
-timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
+timeout -k 10 300 python bench.py --steps $STEPS --warmup 30 > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -20 gpurun_out/bench.log; exit 1; }
 tail -1 gpurun_out/bench.log
 echo "[gpu_check] rocprofv3 kernel stats"
 export TMPDIR=/tmp
