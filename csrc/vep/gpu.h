@@ -93,6 +93,10 @@ struct AvcDesc {
   i16* res;            // device scratch: kAvcResSamples per intra MB with residual (MbRec::res
                        // slot; avc_inter_kernel -> avc_intra_kernel)
   u64* prof;           // optional (VEP_AVC_PROF=1): kAvcProfSlots clock64() phase accumulators
+  u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
+                       // tagged words per MB of every workgroup's last row (intra wavefront:
+                       // words 0..7, zeroed by avc_inter_kernel; deblocking: all, zeroed by
+                       // avc_bs_kernel)
 };
 // Phase accumulators of the wavefront kernels (summed over waves): intra wait / load / luma /
 // chroma / store+publish / MBs, deblock wait / load / filter / store+publish / MBs.
@@ -108,17 +112,29 @@ struct AvcDbkInfo {
   u8 pad[1];
 };
 static_assert(sizeof(AvcDbkInfo) == 48, "AvcDbkInfo layout");
+// The deblocking wavefront runs kAvcDbkWgRows MB rows per workgroup (two per wave64), several
+// workgroups per picture; a workgroup's last row hands its final bottom samples to the next
+// workgroup through `xg`: 16 luma + 8 NV12 chroma u32 words per MB, each tagged (high half) with
+// 2 once final (1 = columns 12..15 still to be filtered by the next MB's left edge).
+constexpr int kAvcDbkWgRows = 8;
+constexpr int kAvcXgWords = 24;
+inline int avc_dbk_groups(int hmbs) { return (hmbs + kAvcDbkWgRows - 1) / kAvcDbkWgRows; }
+inline size_t avc_xg_bytes(int wmbs, int hmbs) {
+  return size_t(avc_dbk_groups(hmbs) - 1) * size_t(wmbs) * kAvcXgWords * sizeof(u64);
+}
 constexpr int kAvcMaxRows = 512;  // MB rows per picture the wavefront kernels support (8K)
 constexpr int kAvcMaxCols = 512;  // MB columns
 // Inter / skip / I_PCM macroblocks of every picture of the round: one 256-lane workgroup per MB.
 void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
-// Intra 4x4 / 16x16 macroblocks in a wavefront, then the deblocking filter in a wavefront: one
-// 1024-lane workgroup (16 wave64s) per picture, rows synchronised through LDS counters.
-void launch_avc_intra(const AvcDesc* d_descs, int n, hipStream_t s);
+// Intra 4x4 / 16x16 macroblocks in a wavefront: avc_dbk_groups(hmbs) workgroups of
+// kAvcDbkWgRows wave64s (one row each) per picture; rows synchronised through LDS counters
+// inside a workgroup and tagged exchange words (AvcDesc::xg) between workgroups.
+void launch_avc_intra(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s);
 // Boundary strengths + edge thresholds of every MB of the round (fully parallel), then the
-// deblocking wavefront over them.
+// deblocking wavefront over them: avc_dbk_groups(hmbs) workgroups of kAvcDbkWgRows / 2 wave64s
+// per picture, spread over the XCDs picture-wise (a picture's workgroups share one L2).
 void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
-void launch_avc_deblock(const AvcDesc* d_descs, int n, hipStream_t s);
+void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s);
 
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
 

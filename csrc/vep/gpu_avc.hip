@@ -27,7 +27,9 @@ using avc::MbRec;
 
 namespace {
 
-constexpr int kWaves = 16;
+constexpr int kIntraWaves = kAvcDbkWgRows;  // intra wavefront: one row per wave, one workgroup
+                                             // per kAvcDbkWgRows rows (shares AvcDesc::xg)
+constexpr int kIntraXgWords = 8;  // intra exchange: 4 luma + 4 NV12 words of an MB's last line
 constexpr u32 kSpinLimit = 1u << 24;
 
 __device__ inline const MbRec& rec(const AvcDesc& d, int mb) {
@@ -58,6 +60,9 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   const int t = int(threadIdx.x), x = t & 15, y = t >> 4;
   const int cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;  // chroma lane (t < 128)
   if (avc::is_intra(m.kind) && m.kind != avc::kIPcm) {
+    const int row = mb / d.wmbs;  // clear the intra wavefront's exchange tags of this MB
+    if (t < kIntraXgWords && row % kAvcDbkWgRows == kAvcDbkWgRows - 1 && row + 1 < d.hmbs)
+      d.xg[(size_t(row / kAvcDbkWgRows) * d.wmbs + mb % d.wmbs) * kAvcXgWords + t] = 0;
     // Intra MB: its residual samples do not depend on the prediction, so they are computed here
     // in parallel and the intra wavefront only adds them (same layout as IntraWave::res).
     if (m.res == avc::kNoRes) return;
@@ -144,6 +149,13 @@ __device__ inline bool intra_avail(const AvcDesc& d, const MbRec& m, int nx, int
   return !(d.constrained && !avc::is_intra(n.kind));
 }
 
+// Tagged exchange words between the workgroups of one picture's wavefront (AvcDesc::xg): device-scope relaxed atomics (global_{load,store}_dwordx2 sc1, past
+// the per-CU L1), single-copy atomic, so a reader sees a word's data and tag together.
+__device__ inline void xg_put(u64* p, u32 v, u32 tag) {
+  __hip_atomic_store(p, u64(tag) << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline u64 xg_get(u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
 // wave-local barrier (one wave64 per "group" here: LDS ordering + compiler fence)
 __device__ inline void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -164,6 +176,7 @@ struct alignas(16) IntraWave {
   u8 ctile[2][9 * kCp];
   u8 carry[16];       // right luma column of the previous MB of this row (if this wave built it)
   u8 ccarry[2][8];
+  u8 up[68];          // row above, MBs base-1 .. base+64 of the chunk: intra (published in xg)?
 };
 
 __device__ inline bool avail_hdr(const AvcDesc& d, const uint4& h, bool in_pic, u16 slice) {
@@ -175,8 +188,14 @@ __device__ inline bool avail_hdr(const AvcDesc& d, const uint4& h, bool in_pic, 
 
 // One intra MB, whole wave: one round trip of global loads (all issued before any is used),
 // a parallel residual pass, then prediction out of LDS.
+//
+// The first row of a workgroup reads the row above's intra MBs (reconstructed by the previous
+// workgroup in this same launch) from `xi_in` (tag 1 = final), polled per sample word;
+// `up_intra[n]` says whether MB n of the row above is such an MB. The last row of a workgroup
+// publishes its bottom lines to `xi_out`.
 __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, int row, bool carry,
-                         int lane, const u32* tap_lut, u64 t_start, u64* acc) {
+                         int lane, const u32* tap_lut, u64 t_start, u64* acc, Sync& sync,
+                         u64* xi_in, const u8* up_intra, u64* xi_out) {
   const int W = d.wmbs, pitch = W * 16;
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
@@ -189,14 +208,45 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   if (m.res != avc::kNoRes && lane < 48)
     cv = reinterpret_cast<const uint4*>(d.res + size_t(m.res) * kAvcResSamples)[lane];
   u32 a = 128, b = 128;
+  int xw = -1, xsh = 0;  // tagged word of the previous workgroup's exchange holding sample `a`
   if (lane < 21) {  // luma row above: x0-1 .. x0+19
     const int px = x0 - 1 + lane;
-    if (up && px >= 0 && px < pitch) a = Y[size_t(y0 - 1) * pitch + px];
+    if (up && px >= 0 && px < pitch) {
+      if (xi_in && up_intra[px >> 4]) {
+        xw = (px >> 4) * kAvcXgWords + ((px & 15) >> 2);
+        xsh = (px & 3) * 8;
+      } else {
+        a = Y[size_t(y0 - 1) * pitch + px];
+      }
+    }
   } else if (lane < 37) {  // luma left column
     if (lf && !carry) a = Y[size_t(y0 + lane - 21) * pitch + x0 - 1];
   } else if (lane < 55) {  // chroma row above: x*8-1 .. x*8+7 per component
     const int c = (lane - 37) / 9, k = (lane - 37) % 9, px = x * 8 - 1 + k;
-    if (up && px >= 0) a = UV[size_t(row * 8 - 1) * pitch + px * 2 + c];
+    if (up && px >= 0) {
+      if (xi_in && up_intra[px >> 3]) {
+        const int bo = (px & 7) * 2 + c;  // byte of the MB's NV12 bottom line
+        xw = (px >> 3) * kAvcXgWords + 4 + (bo >> 2);
+        xsh = (bo & 3) * 8;
+      } else {
+        a = UV[size_t(row * 8 - 1) * pitch + px * 2 + c];
+      }
+    }
+  }
+  if (xi_in) {  // (wave-uniform) poll the published words until every one is final
+    u64 v = xw >= 0 ? xg_get(xi_in + xw) : 0;
+    u32 spins = 0;
+    while (__ballot(xw >= 0 && u32(v >> 32) != 1u)) {
+      if (__hip_atomic_load(&sync.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      if (++spins > (kSpinLimit >> 4)) {
+        __hip_atomic_store(&sync.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) atomicOr(d.err, 2u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (xw >= 0) v = xg_get(xi_in + xw);
+    }
+    if (xw >= 0) a = u32(v >> xsh) & 0xffu;
   }
   if (lane >= 48) {  // chroma left columns
     const int c = (lane - 48) >> 3, k = (lane - 48) & 7;
@@ -352,12 +402,14 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     const u8* src = &L.tile[(ry + 1) * kTp + rx + 1];
     const u32 w = u32(src[0]) | u32(src[1]) << 8 | u32(src[2]) << 16 | u32(src[3]) << 24;
     *reinterpret_cast<u32*>(Y + size_t(y0 + ry) * pitch + x0 + rx) = w;
+    if (xi_out && lane >= 60) xg_put(xi_out + size_t(x) * kAvcXgWords + (lane - 60), w, 1u);
     if (lane < 32) {  // NV12: 8 rows x 16 bytes
       const int cyr = lane >> 2, cxb = (lane & 3) * 2;
       const u8* c0 = &L.ctile[0][(cyr + 1) * kCp + cxb + 1];
       const u8* c1 = &L.ctile[1][(cyr + 1) * kCp + cxb + 1];
       const u32 cw = u32(c0[0]) | u32(c1[0]) << 8 | u32(c0[1]) << 16 | u32(c1[1]) << 24;
       *reinterpret_cast<u32*>(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cxb) * 2) = cw;
+      if (xi_out && lane >= 28) xg_put(xi_out + size_t(x) * kAvcXgWords + 4 + (lane - 28), cw, 1u);
     }
     if (lane < 16) L.carry[lane] = L.tile[(lane + 1) * kTp + 16];
     if (lane < 16) L.ccarry[lane >> 3][lane & 7] = L.ctile[lane >> 3][((lane & 7) + 1) * kCp + 8];
@@ -375,22 +427,34 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   }
 }
 
-__global__ __launch_bounds__(1024) void avc_intra_kernel(const AvcDesc* __restrict__ descs) {
+// One row per wave, kIntraWaves rows per workgroup, avc_dbk_groups(H) workgroups per picture
+// (same XCD-aware grid order as the deblocking wavefront): rows of a workgroup synchronise
+// through LDS counters, a workgroup's first row polls the previous workgroup's published lines.
+__global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDesc* __restrict__ descs,
+                                                                      int n, int groups) {
+  const int b = int(blockIdx.x), j = b >> 3;
+  const int pic = (j / groups) * 8 + (b & 7), grp = j % groups;
+  if (pic >= n) return;
+  const AvcDesc d = descs[pic];  // by value: SGPRs, no reloads after stores
+  const int W = d.wmbs, H = d.hmbs, g0 = grp * kIntraWaves;
+  if (g0 >= H) return;  // (uniform over the workgroup, before any barrier)
   __shared__ Sync sync;
-  __shared__ IntraWave lds[kWaves];
+  __shared__ IntraWave lds[kIntraWaves];
   __shared__ u32 tap_lut[9 * 16];  // Intra_4x4 tap word per (mode, y, x) of a 4x4 block
-  const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
-  const int W = d.wmbs, H = d.hmbs;
   for (int t = int(threadIdx.x); t < 9 * 16; t += int(blockDim.x)) {
     const int mode = t >> 4, y = (t >> 2) & 3, x = t & 3;
     tap_lut[t] = mode == 2 ? avc::kTapDc : avc::pack_taps(avc::intra4x4_taps(mode, x, y));
   }
-  sync_init(sync, H);  // (its barrier also publishes the table)
+  sync_init(sync, kIntraWaves);  // (its barrier also publishes the table)
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   IntraWave& L = lds[wave];
   const MbRec* recs = static_cast<const MbRec*>(d.mbs);
+  const int row = g0 + wave;
+  const bool xin = grp > 0 && wave == 0;
+  u64* xi_in = xin ? d.xg + size_t(grp - 1) * W * kAvcXgWords : nullptr;
+  u64* xi_out = wave == kIntraWaves - 1 && row + 1 < H ? d.xg + size_t(grp) * W * kAvcXgWords : nullptr;
   u64 acc[7] = {0, 0, 0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
-  for (int row = wave; row < H; row += kWaves) {
+  if (row < H) {
     int prev = -2;
     for (int base = 0; base < W; base += 64) {
       // ---- the chunk's records into LDS (one round trip) and its intra MBs by ballot
@@ -405,20 +469,31 @@ __global__ __launch_bounds__(1024) void avc_intra_kernel(const AvcDesc* __restri
         const u8 kd = u8(q[0].x & 0xff);
         intra = kd == avc::kI4x4 || kd == avc::kI16x16;
       }
+      if (xin)  // which MBs base-1 .. base+64 of the row above come through xi_in
+        for (int q = lane; q < 66; q += 64) {
+          const int ax = base - 1 + q;
+          u8 v = 0;
+          if (ax >= 0 && ax < W) {
+            const u8 kd = recs[(row - 1) * W + ax].kind;
+            v = kd == avc::kI4x4 || kd == avc::kI16x16;
+          }
+          L.up[q] = v;
+        }
       const u64 mask = __ballot(intra);
       wave_sync();
       for (u64 bits = mask; bits; bits &= bits - 1) {
         const int xx = base + __ffsll(static_cast<unsigned long long>(bits)) - 1;
         const u64 t0 = d.prof ? clock64() : 0;
-        publish_row(sync, row, u32(xx));  // every MB left of xx is final
-        if (row > 0) wait_row(sync, row - 1, u32(xx + 2 < W ? xx + 2 : W), d.err);
+        publish_row(sync, wave, u32(xx));  // every MB left of xx is final
+        if (wave > 0) wait_row(sync, wave - 1, u32(xx + 2 < W ? xx + 2 : W), d.err);
         const u64 t1 = d.prof ? clock64() : 0;
-        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, t1, acc);
+        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, t1, acc, sync, xi_in,
+                 xin ? &L.up[1] - base : nullptr, xi_out);
         prev = xx;
         acc[0] += t1 - t0;
       }
     }
-    publish_row(sync, row, u32(W));
+    publish_row(sync, wave, u32(W));
   }
   if (d.prof && lane == 0) {
     for (int k = 0; k < 6; ++k) atomicAdd(&d.prof[k], acc[k]);
@@ -440,6 +515,11 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
   }
   const AvcDesc d = descs[lo];
   const int mb = g - d.mb_begin, W = d.wmbs, x = mb % W, row = mb / W;
+  if (row % kAvcDbkWgRows == kAvcDbkWgRows - 1 && row + 1 < d.hmbs) {  // clear the deblock
+    uint4* z = reinterpret_cast<uint4*>(                                  // exchange tags
+        d.xg + (size_t(row / kAvcDbkWgRows) * W + x) * kAvcXgWords);
+    for (int k = 0; k < kAvcXgWords / 2; ++k) z[k] = make_uint4(0, 0, 0, 0);
+  }
   const MbRec q = rec(d, mb);
   AvcDbkInfo info{};
   if (!(q.dbk & 1)) {
@@ -498,22 +578,37 @@ struct alignas(16) DbkXch {
 };
 
 // A wave filters two adjacent MB rows at once: lanes 0-31 row 2p, lanes 32-63 row 2p+1, the
-// second trailing by kDbkLag columns. 32 rows in flight per picture, all 64 lanes filtering.
+// second trailing by kDbkLag columns, all 64 lanes filtering. A workgroup of kDbkWaves waves
+// owns kAvcDbkWgRows consecutive rows, and a picture runs avc_dbk_groups(H) workgroups at once
+// (68 rows of 1080p: 9 workgroups, 34 waves, every row in flight), so each wave gets most of a
+// SIMD to itself instead of sharing one CU with the whole picture.
 //
-// Rows talk only through LDS, so the per-MB handshake never waits on global memory:
-//  * a row passes its final bottom rows to the row below in an exchange ring of kDbkDepth
-//    columns (the producer waits when the consumer falls that far behind); the row pair that
-//    crosses from one pass to the next (row % 32 == 31 -> wave 0 of the next pass) uses a
-//    whole-row buffer instead, so no wait ever points from one pass to the next;
+// Rows hand their final bottom samples to the row below; the per-MB handshake never waits on
+// the picture in global memory:
+//  * inside a workgroup through an LDS exchange ring of kDbkDepth columns (the producer waits
+//    when the consumer falls that far behind) guarded by LDS progress counters;
+//  * from a workgroup's last row to the next workgroup's first row through `xg`, a whole-row
+//    buffer of device-coherent (sc1) 64-bit words whose high half tags the word as final, so
+//    the data is its own flag: no counter, no release fence, no L2 writeback; the consumer
+//    prefetches the next MB's words one step ahead and re-polls only when they are not final;
 //  * each sample is written to the picture by exactly one wave: a row stores rows 0..11 of its
 //    MBs, the row below stores rows 12..15 (from the exchange, after its own top-edge filter),
 //    so no global store ever needs to be ordered against another wave's;
 //  * the MB's own samples are prefetched one column ahead (no wave writes them before the row
 //    that owns the MB has filtered it).
-constexpr int kDbkLag = 3;
+// Workgroups wait only on the previous workgroup of their picture, which the XCD-aware grid
+// order (launch_avc_deblock) dispatches first, so every wait is on a resident workgroup.
+constexpr int kDbkLag = 2;  // the second row needs MB x + 1 of the first row filtered
 constexpr int kDbkDepth = 8;
-constexpr int kDbkSlots = 2 * kWaves + 2;  // >= 33: a ring slot is reused only by a row whose
-                                           // wave has finished every row that could still read it
+constexpr int kDbkRows = kAvcDbkWgRows;
+constexpr int kDbkWaves = kDbkRows / 2;
+constexpr u32 kXgFinal = 2u, kXgPartial = 1u;
+static_assert(kDbkRows % 2 == 0 && kDbkDepth > kDbkLag, "deblock wavefront geometry");
+
+struct DbkSync {
+  u32 progress[kDbkRows];  // MBs finished per row of the workgroup
+  u32 abort;
+};
 
 __device__ inline void st4(u8* p, u32 v) { *reinterpret_cast<u32*>(p) = v; }
 __device__ inline u32 ld4(const u8* p) { return *reinterpret_cast<const u32*>(p); }
@@ -525,7 +620,7 @@ __device__ inline u32 gld4(const void* p) { return *(const VEP_GLOBAL u32*)(p); 
 __device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
 
 // LDS-only handshake: progress counters and the data they guard both live in LDS.
-__device__ inline void wait_row_lds(Sync& s, int r, u32 need, u32* err) {
+__device__ inline void wait_row_lds(DbkSync& s, int r, u32 need, u32* err) {
   u32 spins = 0;
   while (__hip_atomic_load(&s.progress[r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need) {
     if (__hip_atomic_load(&s.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
@@ -548,24 +643,30 @@ struct DbkRegs {  // one MB's inputs as loaded from global memory (per lane of a
   u32 info, m0, m1, c;
 };
 
-__global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __restrict__ descs) {
-  __shared__ Sync sync;
-  __shared__ DbkWave lds[kWaves][2];
-  __shared__ DbkXch xring[kDbkSlots][kDbkDepth];
-  __shared__ DbkXch xwrap[kAvcMaxCols];
-  const AvcDesc d = descs[blockIdx.x];  // by value: SGPRs, no reloads after stores
+__global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDesc* __restrict__ descs,
+                                                                      int n, int groups) {
+  // grid order: workgroup b runs on XCD b % 8; picture p's group k is b = ((p / 8) * groups +
+  // k) * 8 + p % 8, so a picture stays on one XCD and its groups dispatch in order
+  const int b = int(blockIdx.x), j = b >> 3;
+  const int pic = (j / groups) * 8 + (b & 7), grp = j % groups;
+  if (pic >= n) return;
+  const AvcDesc d = descs[pic];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, pitch = W * 16;
-  sync_init(sync, H);
+  const int g0 = grp * kDbkRows;  // first row of this workgroup
+  if (g0 >= H) return;            // (uniform over the workgroup, before any barrier)
+  __shared__ DbkSync sync;
+  __shared__ DbkWave lds[kDbkWaves][2];
+  __shared__ DbkXch xring[kDbkRows - 1][kDbkDepth];
+  if (threadIdx.x < kDbkRows) sync.progress[threadIdx.x] = 0;
+  if (threadIdx.x == 0) sync.abort = 0;
+  __syncthreads();
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int h = lane >> 5, l = lane & 31;  // row of the pair / lane within the half-wave
   DbkWave& L = lds[wave][h];
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
-  constexpr int kPass = 2 * kWaves;
-  auto xch = [&](int r, int x) -> DbkXch& {
-    return r % kPass == kPass - 1 ? xwrap[x] : xring[r % kDbkSlots][x % kDbkDepth];
-  };
+  auto xch = [&](int r, int x) -> DbkXch& { return xring[r - g0][x % kDbkDepth]; };
   // Branch-free (row / column clamped, the result unused when out of range): a conditional
   // load would merge with a default at the join and force an immediate vmcnt wait.
   auto load_mb = [&](int row, int x) {
@@ -579,183 +680,222 @@ __global__ __launch_bounds__(1024) void avc_deblock_kernel(const AvcDesc* __rest
     v.c = gld4(UV + size_t(row * 8 + (l >> 2)) * pitch + x * 16 + (l & 3) * 4);  // 8 x 16 B
     return v;
   };
+  const int r0 = g0 + 2 * wave, row = r0 + h, lrow = row - g0;
+  const bool last = row == H - 1;
+  const bool prod = row + 1 < H;                          // hands its bottom rows down
+  const bool xout = prod && lrow == kDbkRows - 1;          // ... to the next workgroup
+  const bool xin = grp > 0 && wave == 0;                   // row r0 reads the previous group's
+  // exchange word this lane of row r0 reads: luma lanes 16..31 -> words 0..15, chroma lanes
+  // 8..15 -> words 16..23
+  const int xw = l >= 16 ? l - 16 : (l >= 8 ? 16 + (l - 8) : -1);
+  const bool xneed = xin && h == 0 && xw >= 0;
+  u64* xg_in = xin ? d.xg + size_t(grp - 1) * W * kAvcXgWords : nullptr;
+  u64* xg_out = d.xg + size_t(grp) * W * kAvcXgWords;
+  u64 gx = 0;  // row r0's exchange word of the current MB (prefetched one step ahead)
+  if (xneed) gx = xg_get(xg_in + xw);
   u64 acc[5] = {0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
-  for (int r0 = 2 * wave; r0 < H; r0 += kPass) {
-    const int row = r0 + h;
-    const bool last = row == H - 1;
-    const bool prod = row + 1 < H;  // this row hands its bottom rows to the row below
-    bool carry = false;
-    DbkRegs cur = load_mb(row, -kDbkLag * h);
-    for (int i = 0; i < W + kDbkLag; ++i) {
-      const int x = i - h * kDbkLag;
-      const bool act = row < H && x >= 0 && x < W;
-      const u64 t0 = d.prof ? clock64() : 0;
-      const DbkRegs nxt = load_mb(row, x + 1);  // prefetch: in flight across this MB's work
-      if (r0 > 0 && i < W) wait_row_lds(sync, r0 - 1, u32(i + 2 < W ? i + 2 : W), d.err);
-      {  // back-pressure: the pair's second row feeds the next wave through an 8-column ring
-        const int x1 = i - kDbkLag;
-        if (r0 + 2 < H && (r0 + 1) % kPass != kPass - 1 && x1 < W && x1 - kDbkDepth + 1 > 0)
-          wait_row_lds(sync, r0 + 2, u32(x1 - kDbkDepth + 1), d.err);
+  DbkRegs cur = load_mb(row, -kDbkLag * h);
+  for (int i = 0; r0 < H && i < W + kDbkLag; ++i) {
+    const int x = i - h * kDbkLag;
+    const bool act = row < H && x >= 0 && x < W;
+    const u64 t0 = d.prof ? clock64() : 0;
+    if (xin && i < W) {  // previous workgroup's bottom samples of MB i: poll until final
+      u32 spins = 0;
+      while (__ballot(xneed && u32(gx >> 32) != kXgFinal)) {
+        if (__hip_atomic_load(&sync.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        if (++spins > (kSpinLimit >> 4)) {
+          __hip_atomic_store(&sync.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          if (lane == 0) atomicOr(d.err, 2u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        if (xneed) gx = xg_get(xg_in + size_t(i) * kAvcXgWords + xw);
       }
-      const u64 t1 = d.prof ? clock64() : 0;
-      const int x0 = x * 16, y0 = row * 16;
-      // ---- LDS: MB samples, left columns (carried), top rows (the row above's exchange)
-      if (act) {
-        if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
-        st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
-        st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
-        if (l < 16) {
-          if (x > 0) st4(&L.y[(l + 4) * 20], ld4(&L.carry[l * 4]));
-        } else if (row > 0) {
-          const int k = l - 16;
-          st4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4], ld4(&xch(row - 1, x).y[k * 4]));
-        }
-        {
-          const int cyr = l >> 2, cb = (l & 3) * 2;
-          for (int b = 0; b < 2; ++b) {
-            L.c[0][(cyr + 2) * 10 + 2 + cb + b] = u8(cur.c >> (16 * b));
-            L.c[1][(cyr + 2) * 10 + 2 + cb + b] = u8(cur.c >> (16 * b + 8));
-          }
-        }
-        if (l < 8) {
-          if (x > 0) {
-            L.c[0][(l + 2) * 10 + 0] = L.ccarry[0][l * 2];
-            L.c[1][(l + 2) * 10 + 0] = L.ccarry[1][l * 2];
-            L.c[0][(l + 2) * 10 + 1] = L.ccarry[0][l * 2 + 1];
-            L.c[1][(l + 2) * 10 + 1] = L.ccarry[1][l * 2 + 1];
-          }
-        } else if (l < 16 && row > 0) {
-          const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
-          const u32 v = ld4(&xch(row - 1, x).c[k * 4]);
-          for (int b = 0; b < 2; ++b) {
-            L.c[0][tr * 10 + 2 + cb + b] = u8(v >> (16 * b));
-            L.c[1][tr * 10 + 2 + cb + b] = u8(v >> (16 * b + 8));
-          }
+    }
+    const u32 gv = u32(gx);
+    if (xneed && i + 1 < W) gx = xg_get(xg_in + size_t(i + 1) * kAvcXgWords + xw);  // prefetch
+    const DbkRegs nxt = load_mb(row, x + 1);  // prefetch: in flight across this MB's work
+    if (wave > 0 && i < W) wait_row_lds(sync, 2 * wave - 1, u32(i + 2 < W ? i + 2 : W), d.err);
+    {  // back-pressure: the pair's second row feeds the next wave through a kDbkDepth ring
+      const int x1 = i - kDbkLag;
+      if (r0 + 2 < H && wave + 1 < kDbkWaves && x1 < W && x1 - kDbkDepth + 1 > 0)
+        wait_row_lds(sync, 2 * wave + 2, u32(x1 - kDbkDepth + 1), d.err);
+    }
+    const u64 t1 = d.prof ? clock64() : 0;
+    const int x0 = x * 16, y0 = row * 16;
+    const bool top_g = xin && h == 0;  // this row's top samples come from xg
+    // ---- LDS: MB samples, left columns (carried), top rows (the row above's exchange)
+    if (act) {
+      if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
+      st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
+      st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
+      if (l < 16) {
+        if (x > 0) st4(&L.y[(l + 4) * 20], ld4(&L.carry[l * 4]));
+      } else if (row > 0) {
+        const int k = l - 16;
+        st4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4], top_g ? gv : ld4(&xch(row - 1, x).y[k * 4]));
+      }
+      {
+        const int cyr = l >> 2, cb = (l & 3) * 2;
+        for (int q = 0; q < 2; ++q) {
+          L.c[0][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q));
+          L.c[1][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q + 8));
         }
       }
-      wave_sync();
-      const u64 t2 = d.prof ? clock64() : 0;
-      const bool any = act && L.info.any;
-      if (__ballot(any)) {
-        // ---- filter: vertical edges then horizontal edges (per half: luma lanes 0-15,
-        // chroma 16-31)
-        for (int dir = 0; dir < 2; ++dir) {
-          for (int e = 0; e < 4; ++e) {
-            const int pk = e > 0 ? 2 : dir;  // edge params: left / top / internal
-            if (any) {
-              if (l < 16) {
-                const int bs = bs_of(L.info, dir, e, l >> 2);
-                if (bs) {
-                  const int al = L.info.alpha[pk], be = L.info.beta[pk];
-                  const int tc = bs < 4 ? L.info.tc0[pk][bs - 1] : 0;
-                  if (dir == 0) avc::filter_line_t(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, al, be, tc, false);
-                  else avc::filter_line_t(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, al, be, tc, false);
-                }
-              } else if (!(e & 1)) {
-                const int c = (l - 16) >> 3, k = (l - 16) & 7;
-                const int bs = bs_of(L.info, dir, e, k >> 1);
-                if (bs) {
-                  const int al = L.info.alpha[3 + pk], be = L.info.beta[3 + pk];
-                  const int tc = bs < 4 ? L.info.tc0[3 + pk][bs - 1] : 0;
-                  if (dir == 0) avc::filter_line_t(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, al, be, tc, true);
-                  else avc::filter_line_t(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, al, be, tc, true);
-                }
+      if (l < 8) {
+        if (x > 0) {
+          L.c[0][(l + 2) * 10 + 0] = L.ccarry[0][l * 2];
+          L.c[1][(l + 2) * 10 + 0] = L.ccarry[1][l * 2];
+          L.c[0][(l + 2) * 10 + 1] = L.ccarry[0][l * 2 + 1];
+          L.c[1][(l + 2) * 10 + 1] = L.ccarry[1][l * 2 + 1];
+        }
+      } else if (l < 16 && row > 0) {
+        const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+        const u32 v = top_g ? gv : ld4(&xch(row - 1, x).c[k * 4]);
+        for (int q = 0; q < 2; ++q) {
+          L.c[0][tr * 10 + 2 + cb + q] = u8(v >> (16 * q));
+          L.c[1][tr * 10 + 2 + cb + q] = u8(v >> (16 * q + 8));
+        }
+      }
+    }
+    wave_sync();
+    const u64 t2 = d.prof ? clock64() : 0;
+    const bool any = act && L.info.any;
+    if (__ballot(any)) {
+      // ---- filter: vertical edges then horizontal edges (per half: luma lanes 0-15,
+      // chroma 16-31)
+      for (int dir = 0; dir < 2; ++dir) {
+        for (int e = 0; e < 4; ++e) {
+          const int pk = e > 0 ? 2 : dir;  // edge params: left / top / internal
+          if (any) {
+            if (l < 16) {
+              const int bs = bs_of(L.info, dir, e, l >> 2);
+              if (bs) {
+                const int al = L.info.alpha[pk], be = L.info.beta[pk];
+                const int tc = bs < 4 ? L.info.tc0[pk][bs - 1] : 0;
+                if (dir == 0) avc::filter_line_t(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, al, be, tc, false);
+                else avc::filter_line_t(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, al, be, tc, false);
+              }
+            } else if (!(e & 1)) {
+              const int c = (l - 16) >> 3, k = (l - 16) & 7;
+              const int bs = bs_of(L.info, dir, e, k >> 1);
+              if (bs) {
+                const int al = L.info.alpha[3 + pk], be = L.info.beta[3 + pk];
+                const int tc = bs < 4 ? L.info.tc0[3 + pk][bs - 1] : 0;
+                if (dir == 0) avc::filter_line_t(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, al, be, tc, true);
+                else avc::filter_line_t(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, al, be, tc, true);
               }
             }
-            wave_sync();
           }
+          wave_sync();
         }
       }
-      const u64 t3 = d.prof ? clock64() : 0;
-      if (act) {
-        // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left
-        // neighbour's columns 12..15 if the left edge was filtered, and always the MB above's
-        // final rows 12..15 (this wave is their only writer)
-        const bool left = any && (L.info.bs[0] & 0xFFFFu) != 0;  // dir 0, edge 0 nibbles
-        if (any) {
-          u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
-          gst4(ym, ld4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4]));
-          if ((l >> 2) < 4 || last)
-            gst4(ym + size_t(8) * pitch, ld4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4]));
-          const int cyr = l >> 2, cb = (l & 3) * 2;
-          if (cyr < 6 || last) {
-            u32 cw = 0;
-            for (int b = 0; b < 2; ++b)
-              cw |= (u32(L.c[0][(cyr + 2) * 10 + 2 + cb + b]) | u32(L.c[1][(cyr + 2) * 10 + 2 + cb + b]) << 8)
-                    << (16 * b);
-            gst4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
-          }
-        }
-        if (l < 16) {
-          if (left && (l < 12 || last)) gst4(Y + size_t(y0 + l) * pitch + x0 - 4, ld4(&L.y[(l + 4) * 20]));
-        } else if (row > 0) {
-          const int k = l - 16;
-          gst4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4,
-              ld4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4]));
-        }
-        if (l < 8) {
-          if (left && (l < 6 || last)) {
-            const u32 cw = u32(L.c[0][(l + 2) * 10]) | u32(L.c[1][(l + 2) * 10]) << 8 |
-                           u32(L.c[0][(l + 2) * 10 + 1]) << 16 | u32(L.c[1][(l + 2) * 10 + 1]) << 24;
-            gst4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
-          }
-        } else if (l < 16 && row > 0) {
-          const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+    }
+    const u64 t3 = d.prof ? clock64() : 0;
+    if (act) {
+      // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left
+      // neighbour's columns 12..15 if the left edge was filtered, and always the MB above's
+      // final rows 12..15 (this wave is their only writer)
+      const bool left = any && (L.info.bs[0] & 0xFFFFu) != 0;  // dir 0, edge 0 nibbles
+      if (any) {
+        u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
+        gst4(ym, ld4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4]));
+        if ((l >> 2) < 4 || last)
+          gst4(ym + size_t(8) * pitch, ld4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4]));
+        const int cyr = l >> 2, cb = (l & 3) * 2;
+        if (cyr < 6 || last) {
           u32 cw = 0;
-          for (int b = 0; b < 2; ++b)
-            cw |= (u32(L.c[0][tr * 10 + 2 + cb + b]) | u32(L.c[1][tr * 10 + 2 + cb + b]) << 8) << (16 * b);
-          gst4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
+          for (int q = 0; q < 2; ++q)
+            cw |= (u32(L.c[0][(cyr + 2) * 10 + 2 + cb + q]) | u32(L.c[1][(cyr + 2) * 10 + 2 + cb + q]) << 8)
+                  << (16 * q);
+          gst4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
         }
-        // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (columns
-        // 12..15 / 6..7 final only after the next MB's left edge) and the previous MB's now
-        // final columns 12..15 / 6..7
-        if (prod) {
-          DbkXch& xo = xch(row, x);
-          if (l < 16) {
-            st4(&xo.y[l * 4], ld4(&L.y[(16 + (l >> 2)) * 20 + 4 + (l & 3) * 4]));
-          } else if (l < 24) {
-            const int k = l - 16, cr = 8 + (k >> 2), cb = (k & 3) * 2;
-            const u32 cw = u32(L.c[0][cr * 10 + 2 + cb]) | u32(L.c[1][cr * 10 + 2 + cb]) << 8 |
-                           u32(L.c[0][cr * 10 + 3 + cb]) << 16 | u32(L.c[1][cr * 10 + 3 + cb]) << 24;
-            st4(&xo.c[k * 4], cw);
-          } else if (x > 0) {
-            DbkXch& xp = xch(row, x - 1);
-            if (l < 28) {
-              const int k = l - 24;
-              st4(&xp.y[k * 16 + 12], ld4(&L.y[(16 + k) * 20]));
-            } else if (l < 30) {
-              const int k = l - 28, cr = 8 + k;
-              const u32 cw = u32(L.c[0][cr * 10]) | u32(L.c[1][cr * 10]) << 8 |
-                             u32(L.c[0][cr * 10 + 1]) << 16 | u32(L.c[1][cr * 10 + 1]) << 24;
-              st4(&xp.c[k * 16 + 12], cw);
-            }
+      }
+      if (l < 16) {
+        if (left && (l < 12 || last)) gst4(Y + size_t(y0 + l) * pitch + x0 - 4, ld4(&L.y[(l + 4) * 20]));
+      } else if (row > 0) {
+        const int k = l - 16;
+        gst4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4,
+             ld4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4]));
+      }
+      if (l < 8) {
+        if (left && (l < 6 || last)) {
+          const u32 cw = u32(L.c[0][(l + 2) * 10]) | u32(L.c[1][(l + 2) * 10]) << 8 |
+                         u32(L.c[0][(l + 2) * 10 + 1]) << 16 | u32(L.c[1][(l + 2) * 10 + 1]) << 24;
+          gst4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
+        }
+      } else if (l < 16 && row > 0) {
+        const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
+        u32 cw = 0;
+        for (int q = 0; q < 2; ++q)
+          cw |= (u32(L.c[0][tr * 10 + 2 + cb + q]) | u32(L.c[1][tr * 10 + 2 + cb + q]) << 8) << (16 * q);
+        gst4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
+      }
+      // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (columns
+      // 12..15 / 6..7 final only after the next MB's left edge) and the previous MB's now
+      // final columns 12..15 / 6..7
+      if (prod) {
+        // words in exchange order: luma 0..15 (row k >> 2, columns (k & 3) * 4..+3), chroma
+        // 16..23; the last word of each 4-word row is final only after the next MB
+        u32 w = 0;
+        int wi = -1;
+        if (l < 16) {
+          w = ld4(&L.y[(16 + (l >> 2)) * 20 + 4 + (l & 3) * 4]);
+          wi = l;
+        } else if (l < 24) {
+          const int k = l - 16, cr = 8 + (k >> 2), cb = (k & 3) * 2;
+          w = u32(L.c[0][cr * 10 + 2 + cb]) | u32(L.c[1][cr * 10 + 2 + cb]) << 8 |
+              u32(L.c[0][cr * 10 + 3 + cb]) << 16 | u32(L.c[1][cr * 10 + 3 + cb]) << 24;
+          wi = l;
+        }
+        u32 fw = 0;
+        int fi = -1;  // fix-up of the previous MB's right columns
+        if (x > 0) {
+          if (l >= 24 && l < 28) {
+            const int k = l - 24;
+            fw = ld4(&L.y[(16 + k) * 20]);
+            fi = k * 4 + 3;
+          } else if (l >= 28 && l < 30) {
+            const int k = l - 28, cr = 8 + k;
+            fw = u32(L.c[0][cr * 10]) | u32(L.c[1][cr * 10]) << 8 | u32(L.c[0][cr * 10 + 1]) << 16 |
+                 u32(L.c[1][cr * 10 + 1]) << 24;
+            fi = 16 + k * 4 + 3;
           }
         }
-        // ---- carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
-        if (l < 16) {
-          st4(&L.carry[l * 4], ld4(&L.y[(l + 4) * 20 + 16]));
+        if (xout) {
+          if (wi >= 0)
+            xg_put(xg_out + size_t(x) * kAvcXgWords + wi, w,
+                   (wi & 3) == 3 && x + 1 < W ? kXgPartial : kXgFinal);
+          if (fi >= 0) xg_put(xg_out + size_t(x - 1) * kAvcXgWords + fi, fw, kXgFinal);
         } else {
-          const int c = (l - 16) >> 3, k = (l - 16) & 7;
-          L.ccarry[c][k * 2] = L.c[c][(k + 2) * 10 + 8];
-          L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 10 + 9];
+          if (wi >= 0) st4(wi < 16 ? &xch(row, x).y[wi * 4] : &xch(row, x).c[(wi - 16) * 4], w);
+          if (fi >= 0)
+            st4(fi < 16 ? &xch(row, x - 1).y[fi * 4] : &xch(row, x - 1).c[(fi - 16) * 4], fw);
         }
       }
-      carry = carry || act;
-      // publish both rows (LDS release: the exchange and carries are LDS; global stores are
-      // never read back in this kernel and have a single writer)
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (l == 0 && act)
-        __hip_atomic_store(&sync.progress[row], u32(x + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      wave_sync();
-      cur = nxt;
-      if (d.prof) {
-        const u64 t4 = clock64();
-        acc[0] += t1 - t0;
-        acc[1] += t2 - t1;
-        acc[2] += t3 - t2;
-        acc[3] += t4 - t3;
-        acc[4] += u64(__popcll(__ballot(act) & 0x100000001ull));
+      // ---- carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
+      if (l < 16) {
+        st4(&L.carry[l * 4], ld4(&L.y[(l + 4) * 20 + 16]));
+      } else {
+        const int c = (l - 16) >> 3, k = (l - 16) & 7;
+        L.ccarry[c][k * 2] = L.c[c][(k + 2) * 10 + 8];
+        L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 10 + 9];
       }
+    }
+    // publish both rows (LDS release: the exchange and carries are LDS; global stores are
+    // never read back in this kernel and have a single writer)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (l == 0 && act)
+      __hip_atomic_store(&sync.progress[lrow], u32(x + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    wave_sync();
+    cur = nxt;
+    if (d.prof) {
+      const u64 t4 = clock64();
+      acc[0] += t1 - t0;
+      acc[1] += t2 - t1;
+      acc[2] += t3 - t2;
+      acc[3] += t4 - t3;
+      acc[4] += u64(__popcll(__ballot(act) & 0x100000001ull));
     }
   }
   if (d.prof && lane == 0)
@@ -770,9 +910,11 @@ void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t 
   VEP_HIP(hipGetLastError());
 }
 
-void launch_avc_intra(const AvcDesc* d_descs, int n, hipStream_t s) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(avc_intra_kernel, dim3(unsigned(n)), dim3(64 * kWaves), 0, s, d_descs);
+void launch_avc_intra(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s) {
+  if (n <= 0 || max_hmbs <= 0) return;
+  const int groups = avc_dbk_groups(max_hmbs);
+  const unsigned blocks = unsigned((n + 7) / 8) * unsigned(groups) * 8u;
+  hipLaunchKernelGGL(avc_intra_kernel, dim3(blocks), dim3(64 * kIntraWaves), 0, s, d_descs, n, groups);
   VEP_HIP(hipGetLastError());
 }
 
@@ -783,9 +925,11 @@ void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s) 
   VEP_HIP(hipGetLastError());
 }
 
-void launch_avc_deblock(const AvcDesc* d_descs, int n, hipStream_t s) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(avc_deblock_kernel, dim3(unsigned(n)), dim3(64 * kWaves), 0, s, d_descs);
+void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s) {
+  if (n <= 0 || max_hmbs <= 0) return;
+  const int groups = avc_dbk_groups(max_hmbs);
+  const unsigned blocks = unsigned((n + 7) / 8) * unsigned(groups) * 8u;
+  hipLaunchKernelGGL(avc_deblock_kernel, dim3(blocks), dim3(64 * kDbkWaves), 0, s, d_descs, n, groups);
   VEP_HIP(hipGetLastError());
 }
 

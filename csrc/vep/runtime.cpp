@@ -837,7 +837,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   struct AvcPic {
     const avc::Picture* p;
     int job;
-    size_t off_mbs, off_coef, off_mv, off_dbk, off_res;
+    size_t off_mbs, off_coef, off_mv, off_dbk, off_res, off_xg;
   };
   std::vector<AvcPic> apics;
   int rounds = 0;
@@ -851,7 +851,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       const avc::Picture& p = *v[size_t(r)];
       VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows && p.wmbs <= gpu::kAvcMaxCols,
                 "picture too large for the wavefront kernels");
-      AvcPic a{&p, i, 0, 0, 0, 0, 0};
+      AvcPic a{&p, i, 0, 0, 0, 0, 0, 0};
       a.off_mbs = need;
       need += al(p.mbs.size() * sizeof(avc::MbRec));
       a.off_coef = need;
@@ -881,6 +881,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     need += al(size_t(a.p->nmbs()) * sizeof(gpu::AvcDbkInfo));
     a.off_res = need;
     need += al(size_t(a.p->intra_res) * gpu::kAvcResSamples * sizeof(i16));
+    a.off_xg = need;  // deblock exchange between the wavefront's workgroups
+    need += al(gpu::avc_xg_bytes(a.p->wmbs, a.p->hmbs));
   }
   need = al(need);
   if (need > st.cap) {
@@ -1056,6 +1058,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.err = const_cast<u32*>(st.err_dev) + a.job;
       g.dbk = st.d + a.off_dbk;
       g.res = reinterpret_cast<i16*>(st.d + a.off_res);
+      g.xg = reinterpret_cast<u64*>(st.d + a.off_xg);
       g.prof = avc_prof_;
       mbs += a.p->nmbs();
     }
@@ -1085,16 +1088,18 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const int np = int(round_pics[size_t(r)].size());
     int mbs = 0;
     bool intra = false, dbk = false;
+    int max_h = 0;
     for (int k : round_pics[size_t(r)]) {
       mbs += apics[size_t(k)].p->nmbs();
+      max_h = std::max(max_h, apics[size_t(k)].p->hmbs);
       intra |= apics[size_t(k)].p->intra_mbs > 0;
       dbk |= apics[size_t(k)].p->deblock;
     }
     gpu::launch_avc_inter(ad, np, mbs, cs);
-    if (intra) gpu::launch_avc_intra(ad, np, cs);
+    if (intra) gpu::launch_avc_intra(ad, np, max_h, cs);
     if (dbk) {
       gpu::launch_avc_bs(ad, np, mbs, cs);
-      gpu::launch_avc_deblock(ad, np, cs);
+      gpu::launch_avc_deblock(ad, np, max_h, cs);
     }
   }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), n, tiles,
