@@ -30,11 +30,10 @@ import os
 import sys
 import time
 
-# Multi-rank runs add torch's and RCCL's streams to the worker's serving stream + 3 decode lanes:
-# give the process 8 hardware queues (HIP's default is 4) so a long-running all-gather kernel
-# never shares a queue with a decode lane. Must be set before HIP initialises.
-if int(os.environ.get("WORLD_SIZE", "1")) > 1:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# The worker's serving stream + 3 decode lanes + their 3 copy streams (and, multi-rank, torch's
+# and RCCL's streams): give the process 8 hardware queues (HIP's default is 4) so no decode lane
+# or all-gather shares a queue with another. Must be set before HIP initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

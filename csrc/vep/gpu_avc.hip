@@ -598,7 +598,8 @@ struct alignas(16) DbkXch {
 //    that owns the MB has filtered it).
 // Workgroups wait only on the previous workgroup of their picture, which the XCD-aware grid
 // order (launch_avc_deblock) dispatches first, so every wait is on a resident workgroup.
-constexpr int kDbkLag = 2;  // the second row needs MB x + 1 of the first row filtered
+constexpr int kDbkLag = 1;  // the second row filters MB x's top edge after the first row's
+                            // vertical edges of MB x + 1, in the same step
 constexpr int kDbkDepth = 8;
 constexpr int kDbkRows = kAvcDbkWgRows;
 constexpr int kDbkWaves = kDbkRows / 2;
@@ -637,6 +638,36 @@ __device__ inline void wait_row_lds(DbkSync& s, int r, u32 need, u32* err) {
 __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
   const int i = dir * 16 + e * 4 + sg;
   return int((in.bs[i >> 3] >> (4 * (i & 7))) & 15u);
+}
+
+// One direction of an MB's edges, whole wave (lanes of a half-wave: luma lines 0-15, chroma
+// lines 16-31, `any` = this half's MB has an edge to filter): 4 edges in order, each line by
+// filter_line_t (the CPU decoder's core) on the LDS tile.
+__device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
+  for (int e = 0; e < 4; ++e) {
+    const int pk = e > 0 ? 2 : dir;  // edge params: left / top / internal
+    if (any) {
+      if (l < 16) {
+        const int bs = bs_of(L.info, dir, e, l >> 2);
+        if (bs) {
+          const int al = L.info.alpha[pk], be = L.info.beta[pk];
+          const int tc = bs < 4 ? L.info.tc0[pk][bs - 1] : 0;
+          if (dir == 0) avc::filter_line_t(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, al, be, tc, false);
+          else avc::filter_line_t(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, al, be, tc, false);
+        }
+      } else if (!(e & 1)) {
+        const int c = (l - 16) >> 3, k = (l - 16) & 7;
+        const int bs = bs_of(L.info, dir, e, k >> 1);
+        if (bs) {
+          const int al = L.info.alpha[3 + pk], be = L.info.beta[3 + pk];
+          const int tc = bs < 4 ? L.info.tc0[3 + pk][bs - 1] : 0;
+          if (dir == 0) avc::filter_line_t(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, al, be, tc, true);
+          else avc::filter_line_t(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, al, be, tc, true);
+        }
+      }
+    }
+    wave_sync();
+  }
 }
 
 struct DbkRegs {  // one MB's inputs as loaded from global memory (per lane of a half-wave)
@@ -699,6 +730,71 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     const int x = i - h * kDbkLag;
     const bool act = row < H && x >= 0 && x < W;
     const u64 t0 = d.prof ? clock64() : 0;
+    const DbkRegs nxt = load_mb(row, x + 1);  // prefetch: in flight across this MB's work
+    {  // back-pressure: the pair's second row feeds the next wave through a kDbkDepth ring
+      // (the consumer has read column c once its progress reaches c + 2)
+      const int x1 = i - kDbkLag;
+      if (r0 + 2 < H && wave + 1 < kDbkWaves && x1 < W && x1 - kDbkDepth + 2 > 0)
+        wait_row_lds(sync, 2 * wave + 2, u32(x1 - kDbkDepth + 2), d.err);
+    }
+    const u64 t1 = d.prof ? clock64() : 0;
+    const int x0 = x * 16, y0 = row * 16;
+    // ---- LDS: MB samples and left columns (carried)
+    if (act) {
+      if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
+      st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
+      st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
+      if (l < 16) {
+        if (x > 0) st4(&L.y[(l + 4) * 20], ld4(&L.carry[l * 4]));
+      }
+      {
+        const int cyr = l >> 2, cb = (l & 3) * 2;
+        for (int q = 0; q < 2; ++q) {
+          L.c[0][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q));
+          L.c[1][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q + 8));
+        }
+      }
+      if (l < 8 && x > 0) {
+        L.c[0][(l + 2) * 10 + 0] = L.ccarry[0][l * 2];
+        L.c[1][(l + 2) * 10 + 0] = L.ccarry[1][l * 2];
+        L.c[0][(l + 2) * 10 + 1] = L.ccarry[0][l * 2 + 1];
+        L.c[1][(l + 2) * 10 + 1] = L.ccarry[1][l * 2 + 1];
+      }
+    }
+    wave_sync();
+    const u64 t2 = d.prof ? clock64() : 0;
+    const bool any = act && L.info.any;
+    const bool wany = __ballot(any) != 0;
+    // ---- vertical edges (per half: luma lanes 0-15, chroma 16-31): they touch only this MB's
+    // rows, so they need nothing from the row above
+    if (wany) dbk_dir(L, any, l, 0);
+    // ---- the previous MB's right columns are final now (this MB's left edge was the last
+    // filter to touch them): complete its exchange entry for the row below, then publish
+    // "vertical edges of MB x done" (the row below may filter MB x - 1's top edge)
+    if (act && prod && x > 0) {
+      u32 fw = 0;
+      int fi = -1;  // exchange word: luma rows 12..15 columns 12..15 / NV12 rows 6..7 bytes 12..15
+      if (l >= 24 && l < 28) {
+        const int k = l - 24;
+        fw = ld4(&L.y[(16 + k) * 20]);
+        fi = k * 4 + 3;
+      } else if (l >= 28 && l < 30) {
+        const int k = l - 28, cr = 8 + k;
+        fw = u32(L.c[0][cr * 10]) | u32(L.c[1][cr * 10]) << 8 | u32(L.c[0][cr * 10 + 1]) << 16 |
+             u32(L.c[1][cr * 10 + 1]) << 24;
+        fi = 16 + k * 4 + 3;
+      }
+      if (fi >= 0) {
+        if (xout) xg_put(xg_out + size_t(x - 1) * kAvcXgWords + fi, fw, kXgFinal);
+        else st4(fi < 16 ? &xch(row, x - 1).y[fi * 4] : &xch(row, x - 1).c[(fi - 16) * 4], fw);
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (l == 0 && act)
+      __hip_atomic_store(&sync.progress[lrow], u32(x + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    const u64 t3 = d.prof ? clock64() : 0;
+    // ---- wait for the row above: its exchange entry of MB x is complete once it has done the
+    // vertical edges of MB x + 1 (progress x + 2; W + 1 after its last MB)
     if (xin && i < W) {  // previous workgroup's bottom samples of MB i: poll until final
       u32 spins = 0;
       while (__ballot(xneed && u32(gx >> 32) != kXgFinal)) {
@@ -714,42 +810,16 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     }
     const u32 gv = u32(gx);
     if (xneed && i + 1 < W) gx = xg_get(xg_in + size_t(i + 1) * kAvcXgWords + xw);  // prefetch
-    const DbkRegs nxt = load_mb(row, x + 1);  // prefetch: in flight across this MB's work
-    if (wave > 0 && i < W) wait_row_lds(sync, 2 * wave - 1, u32(i + 2 < W ? i + 2 : W), d.err);
-    {  // back-pressure: the pair's second row feeds the next wave through a kDbkDepth ring
-      const int x1 = i - kDbkLag;
-      if (r0 + 2 < H && wave + 1 < kDbkWaves && x1 < W && x1 - kDbkDepth + 1 > 0)
-        wait_row_lds(sync, 2 * wave + 2, u32(x1 - kDbkDepth + 1), d.err);
-    }
-    const u64 t1 = d.prof ? clock64() : 0;
-    const int x0 = x * 16, y0 = row * 16;
+    if (wave > 0 && i < W) wait_row_lds(sync, 2 * wave - 1, u32(i + 2), d.err);
+    wave_sync();  // (the pair's second row reads what the first row completed just above)
+    const u64 t4 = d.prof ? clock64() : 0;
+    // ---- LDS: top rows (the row above's exchange)
     const bool top_g = xin && h == 0;  // this row's top samples come from xg
-    // ---- LDS: MB samples, left columns (carried), top rows (the row above's exchange)
-    if (act) {
-      if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
-      st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
-      st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
-      if (l < 16) {
-        if (x > 0) st4(&L.y[(l + 4) * 20], ld4(&L.carry[l * 4]));
-      } else if (row > 0) {
+    if (act && row > 0) {
+      if (l >= 16) {
         const int k = l - 16;
         st4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4], top_g ? gv : ld4(&xch(row - 1, x).y[k * 4]));
-      }
-      {
-        const int cyr = l >> 2, cb = (l & 3) * 2;
-        for (int q = 0; q < 2; ++q) {
-          L.c[0][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q));
-          L.c[1][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q + 8));
-        }
-      }
-      if (l < 8) {
-        if (x > 0) {
-          L.c[0][(l + 2) * 10 + 0] = L.ccarry[0][l * 2];
-          L.c[1][(l + 2) * 10 + 0] = L.ccarry[1][l * 2];
-          L.c[0][(l + 2) * 10 + 1] = L.ccarry[0][l * 2 + 1];
-          L.c[1][(l + 2) * 10 + 1] = L.ccarry[1][l * 2 + 1];
-        }
-      } else if (l < 16 && row > 0) {
+      } else if (l >= 8) {
         const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
         const u32 v = top_g ? gv : ld4(&xch(row - 1, x).c[k * 4]);
         for (int q = 0; q < 2; ++q) {
@@ -759,39 +829,10 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
       }
     }
     wave_sync();
-    const u64 t2 = d.prof ? clock64() : 0;
-    const bool any = act && L.info.any;
-    if (__ballot(any)) {
-      // ---- filter: vertical edges then horizontal edges (per half: luma lanes 0-15,
-      // chroma 16-31)
-      for (int dir = 0; dir < 2; ++dir) {
-        for (int e = 0; e < 4; ++e) {
-          const int pk = e > 0 ? 2 : dir;  // edge params: left / top / internal
-          if (any) {
-            if (l < 16) {
-              const int bs = bs_of(L.info, dir, e, l >> 2);
-              if (bs) {
-                const int al = L.info.alpha[pk], be = L.info.beta[pk];
-                const int tc = bs < 4 ? L.info.tc0[pk][bs - 1] : 0;
-                if (dir == 0) avc::filter_line_t(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, al, be, tc, false);
-                else avc::filter_line_t(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, al, be, tc, false);
-              }
-            } else if (!(e & 1)) {
-              const int c = (l - 16) >> 3, k = (l - 16) & 7;
-              const int bs = bs_of(L.info, dir, e, k >> 1);
-              if (bs) {
-                const int al = L.info.alpha[3 + pk], be = L.info.beta[3 + pk];
-                const int tc = bs < 4 ? L.info.tc0[3 + pk][bs - 1] : 0;
-                if (dir == 0) avc::filter_line_t(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, al, be, tc, true);
-                else avc::filter_line_t(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, al, be, tc, true);
-              }
-            }
-          }
-          wave_sync();
-        }
-      }
-    }
-    const u64 t3 = d.prof ? clock64() : 0;
+    const u64 t5 = d.prof ? clock64() : 0;
+    // ---- horizontal edges
+    if (wany) dbk_dir(L, any, l, 1);
+    const u64 t6 = d.prof ? clock64() : 0;
     if (act) {
       // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left
       // neighbour's columns 12..15 if the left edge was filtered, and always the MB above's
@@ -831,47 +872,22 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
           cw |= (u32(L.c[0][tr * 10 + 2 + cb + q]) | u32(L.c[1][tr * 10 + 2 + cb + q]) << 8) << (16 * q);
         gst4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
       }
-      // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (columns
-      // 12..15 / 6..7 final only after the next MB's left edge) and the previous MB's now
-      // final columns 12..15 / 6..7
-      if (prod) {
-        // words in exchange order: luma 0..15 (row k >> 2, columns (k & 3) * 4..+3), chroma
-        // 16..23; the last word of each 4-word row is final only after the next MB
-        u32 w = 0;
-        int wi = -1;
+      // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (the last
+      // word of each 4-word row, columns 12..15 / 6..7, is completed by the next MB's vertical
+      // edges above)
+      if (prod && l < 24) {
+        u32 w;
         if (l < 16) {
           w = ld4(&L.y[(16 + (l >> 2)) * 20 + 4 + (l & 3) * 4]);
-          wi = l;
-        } else if (l < 24) {
+        } else {
           const int k = l - 16, cr = 8 + (k >> 2), cb = (k & 3) * 2;
           w = u32(L.c[0][cr * 10 + 2 + cb]) | u32(L.c[1][cr * 10 + 2 + cb]) << 8 |
               u32(L.c[0][cr * 10 + 3 + cb]) << 16 | u32(L.c[1][cr * 10 + 3 + cb]) << 24;
-          wi = l;
         }
-        u32 fw = 0;
-        int fi = -1;  // fix-up of the previous MB's right columns
-        if (x > 0) {
-          if (l >= 24 && l < 28) {
-            const int k = l - 24;
-            fw = ld4(&L.y[(16 + k) * 20]);
-            fi = k * 4 + 3;
-          } else if (l >= 28 && l < 30) {
-            const int k = l - 28, cr = 8 + k;
-            fw = u32(L.c[0][cr * 10]) | u32(L.c[1][cr * 10]) << 8 | u32(L.c[0][cr * 10 + 1]) << 16 |
-                 u32(L.c[1][cr * 10 + 1]) << 24;
-            fi = 16 + k * 4 + 3;
-          }
-        }
-        if (xout) {
-          if (wi >= 0)
-            xg_put(xg_out + size_t(x) * kAvcXgWords + wi, w,
-                   (wi & 3) == 3 && x + 1 < W ? kXgPartial : kXgFinal);
-          if (fi >= 0) xg_put(xg_out + size_t(x - 1) * kAvcXgWords + fi, fw, kXgFinal);
-        } else {
-          if (wi >= 0) st4(wi < 16 ? &xch(row, x).y[wi * 4] : &xch(row, x).c[(wi - 16) * 4], w);
-          if (fi >= 0)
-            st4(fi < 16 ? &xch(row, x - 1).y[fi * 4] : &xch(row, x - 1).c[(fi - 16) * 4], fw);
-        }
+        if (xout)
+          xg_put(xg_out + size_t(x) * kAvcXgWords + l, w, (l & 3) == 3 && x + 1 < W ? kXgPartial : kXgFinal);
+        else
+          st4(l < 16 ? &xch(row, x).y[l * 4] : &xch(row, x).c[(l - 16) * 4], w);
       }
       // ---- carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
       if (l < 16) {
@@ -882,19 +898,19 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
         L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 10 + 9];
       }
     }
-    // publish both rows (LDS release: the exchange and carries are LDS; global stores are
-    // never read back in this kernel and have a single writer)
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (l == 0 && act)
-      __hip_atomic_store(&sync.progress[lrow], u32(x + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (x == W - 1) {  // the row's exchange is complete (no MB to its right)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (l == 0 && act)
+        __hip_atomic_store(&sync.progress[lrow], u32(W + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
     wave_sync();
     cur = nxt;
     if (d.prof) {
-      const u64 t4 = clock64();
-      acc[0] += t1 - t0;
-      acc[1] += t2 - t1;
-      acc[2] += t3 - t2;
-      acc[3] += t4 - t3;
+      const u64 t7 = clock64();
+      acc[0] += (t1 - t0) + (t4 - t3);
+      acc[1] += (t2 - t1) + (t5 - t4);
+      acc[2] += (t3 - t2) + (t6 - t5);
+      acc[3] += t7 - t6;
       acc[4] += u64(__popcll(__ballot(act) & 0x100000001ull));
     }
   }

@@ -305,6 +305,7 @@ class Worker {
   };
   struct Lane {
     hipStream_t stream = nullptr;  // lane 0 uses Worker::stream_
+    hipStream_t copy = nullptr;    // H2D of the next batch's MB data while this one decodes
     std::vector<Stage> stage;      // ring of staging buffers (Worker::stages() deep)
     int next = 0;                  // the stage reused next (the oldest in-flight batch)
     std::atomic<double> gpu_ms{0}; // cumulative batch time on this lane

@@ -9,4 +9,11 @@ frame rings and camera-data-parallel sharding over RCCL/xGMI.
 
 __version__ = "0.1.0"
 
+import os as _os
+
+# A GPU worker runs a serving stream plus, per decode lane, a kernel stream and a copy stream
+# (7 for the default 3 lanes): 8 hardware queues instead of HIP's 4, so none of them shares a
+# queue with another. Read once when HIP initialises, so it must be set before that.
+_os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 from ._native import gpu_count, native  # noqa: F401
