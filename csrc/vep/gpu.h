@@ -124,7 +124,8 @@ inline size_t avc_xg_bytes(int wmbs, int hmbs) {
 }
 constexpr int kAvcMaxRows = 512;  // MB rows per picture the wavefront kernels support (8K)
 constexpr int kAvcMaxCols = 512;  // MB columns
-// Inter / skip / I_PCM macroblocks of every picture of the round: one 256-lane workgroup per MB.
+// Inter / skip / I_PCM macroblocks of every picture of the round (and intra MBs' residuals): one
+// wave64 per MB, four per workgroup.
 void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
 // Intra 4x4 / 16x16 macroblocks in a wavefront: avc_dbk_groups(hmbs) workgroups of
 // kAvcDbkWgRows wave64s (one row each) per picture; rows synchronised through LDS counters

@@ -46,8 +46,14 @@ __device__ inline const i16* chroma_block(const AvcDesc& d, const MbRec& m, int 
 
 // --------------------------------------------------------------------------------- inter
 
-__global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restrict__ descs, int n) {
-  const int g = int(blockIdx.x);
+// One wave64 per MB, four MBs per workgroup: each lane reconstructs 4 luma samples (one per
+// 4x4-block row) and 2 chroma samples, so a lane has all of its reference loads in flight at
+// once and the picture lookup / record / MV loads are paid once per wave instead of per
+// 64 samples.
+__global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restrict__ descs, int n,
+                                                         int total) {
+  const int g = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + (int(threadIdx.x) >> 6));
+  if (g >= total) return;  // (wave-uniform; the kernel has no barrier)
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -57,21 +63,26 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   const AvcDesc d = descs[lo];
   const int mb = g - d.mb_begin;
   const MbRec m = rec(d, mb);
-  const int t = int(threadIdx.x), x = t & 15, y = t >> 4;
-  const int cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;  // chroma lane (t < 128)
+  const int lane = int(threadIdx.x) & 63;
+  const int x = lane & 15, y0 = lane >> 4;  // luma sample (x, y0 + 4k), block row k
   if (avc::is_intra(m.kind) && m.kind != avc::kIPcm) {
     const int row = mb / d.wmbs;  // clear the intra wavefront's exchange tags of this MB
-    if (t < kIntraXgWords && row % kAvcDbkWgRows == kAvcDbkWgRows - 1 && row + 1 < d.hmbs)
-      d.xg[(size_t(row / kAvcDbkWgRows) * d.wmbs + mb % d.wmbs) * kAvcXgWords + t] = 0;
+    if (lane < kIntraXgWords && row % kAvcDbkWgRows == kAvcDbkWgRows - 1 && row + 1 < d.hmbs)
+      d.xg[(size_t(row / kAvcDbkWgRows) * d.wmbs + mb % d.wmbs) * kAvcXgWords + lane] = 0;
     // Intra MB: its residual samples do not depend on the prediction, so they are computed here
     // in parallel and the intra wavefront only adds them (same layout as IntraWave::res).
     if (m.res == avc::kNoRes) return;
     i16* r = d.res + size_t(m.res) * kAvcResSamples;
-    const int blk = (y >> 2) * 4 + (x >> 2);
-    r[t] = i16((m.luma_coded >> blk) & 1 ? avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3) : 0);
-    if (t < 128) {
-      const int k = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
-      r[256 + t] = i16((m.chroma_coded >> k) & 1 ? avc::idct4x4_at(chroma_block(d, m, k), cy & 3, cx & 3) : 0);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
+      r[y * 16 + x] = i16((m.luma_coded >> blk) & 1 ? avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3) : 0);
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
+      const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
+      r[256 + t] = i16((m.chroma_coded >> kb) & 1 ? avc::idct4x4_at(chroma_block(d, m, kb), cy & 3, cx & 3) : 0);
     }
     return;
   }
@@ -82,27 +93,49 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   u8* tuv = d.uv + d.slot_uv * u64(d.target);
   if (m.kind == avc::kIPcm) {
     const u8* s = reinterpret_cast<const u8*>(d.coefs + size_t(m.coef) * 16);
-    ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = s[t];
-    if (t < 128) tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = s[256 + t];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ty[size_t(my * 16 + y0 + 4 * k) * pitch + mx * 16 + x] = s[(y0 + 4 * k) * 16 + x];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
+      tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = s[256 + t];
+    }
     return;
   }
   const i16* mv = d.mvs + size_t(m.mv) * 32;
-  const int blk = (y >> 2) * 4 + (x >> 2);
-  const int mvx = mv[2 * blk], mvy = mv[2 * blk + 1];
-  const int ref = m.ref[((blk >> 3) << 1) | ((blk & 3) >> 1)];
-  int v = avc::luma_qpel(d.y + d.slot_y * u64(ref), pitch, wpx, hpx, mx * 16 + x + (mvx >> 2),
-                         my * 16 + y + (mvy >> 2), mvx & 3, mvy & 3);
-  if ((m.luma_coded >> blk) & 1) v += avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3);
-  ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = u8(avc::clip1(v));
-  if (t < 128) {
+  int v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
+    const int mvx = mv[2 * blk], mvy = mv[2 * blk + 1];
+    const int ref = m.ref[((blk >> 3) << 1) | ((blk & 3) >> 1)];
+    v[k] = avc::luma_qpel(d.y + d.slot_y * u64(ref), pitch, wpx, hpx, mx * 16 + x + (mvx >> 2),
+                          my * 16 + y + (mvy >> 2), mvx & 3, mvy & 3);
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
+    int o = v[k];
+    if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3);
+    ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = u8(avc::clip1(o));
+  }
+  int u[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
     const int r = (cy >> 1) * 4 + (cx >> 1);
     const int c_mvx = mv[2 * r], c_mvy = mv[2 * r + 1];
     const int cref = m.ref[((r >> 3) << 1) | ((r & 3) >> 1)];
-    int u = avc::chroma_epel(d.uv + d.slot_uv * u64(cref), pitch, wpx / 2, hpx / 2, cc,
-                             mx * 8 + cx + (c_mvx >> 3), my * 8 + cy + (c_mvy >> 3), c_mvx & 7, c_mvy & 7);
-    const int k = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
-    if ((m.chroma_coded >> k) & 1) u += avc::idct4x4_at(chroma_block(d, m, k), cy & 3, cx & 3);
-    tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = u8(avc::clip1(u));
+    u[k] = avc::chroma_epel(d.uv + d.slot_uv * u64(cref), pitch, wpx / 2, hpx / 2, cc,
+                            mx * 8 + cx + (c_mvx >> 3), my * 8 + cy + (c_mvy >> 3), c_mvx & 7, c_mvy & 7);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
+    const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
+    int o = u[k];
+    if ((m.chroma_coded >> kb) & 1) o += avc::idct4x4_at(chroma_block(d, m, kb), cy & 3, cx & 3);
+    tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = u8(avc::clip1(o));
   }
 }
 
@@ -922,7 +955,8 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
 
 void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s) {
   if (n <= 0 || total_mbs <= 0) return;
-  hipLaunchKernelGGL(avc_inter_kernel, dim3(unsigned(total_mbs)), dim3(256), 0, s, d_descs, n);
+  hipLaunchKernelGGL(avc_inter_kernel, dim3(unsigned((total_mbs + 3) / 4)), dim3(256), 0, s, d_descs, n,
+                     total_mbs);
   VEP_HIP(hipGetLastError());
 }
 
