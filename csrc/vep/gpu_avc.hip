@@ -30,6 +30,8 @@ namespace {
 constexpr int kIntraWaves = kAvcDbkWgRows;  // intra wavefront: one row per wave, one workgroup
                                              // per kAvcDbkWgRows rows (shares AvcDesc::xg)
 constexpr int kIntraXgWords = 8;  // intra exchange: 4 luma + 4 NV12 words of an MB's last line
+constexpr int kIntraLine = 32;    // bytes of an MB's bottom line in LDS: 16 luma + 16 NV12
+constexpr int kIntraLineCols = 240;  // LDS lines cover pictures up to 3840 samples wide
 constexpr u32 kSpinLimit = 1u << 24;
 
 __device__ inline const MbRec& rec(const AvcDesc& d, int mb) {
@@ -227,59 +229,55 @@ __device__ inline bool avail_hdr(const AvcDesc& d, const uint4& h, bool in_pic, 
 // `up_intra[n]` says whether MB n of the row above is such an MB. The last row of a workgroup
 // publishes its bottom lines to `xi_out`.
 __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, int row, bool carry,
-                         int lane, const u32* tap_lut, u64 t_start, u64* acc, Sync& sync,
-                         u64* xi_in, const u8* up_intra, u64* xi_out) {
+                         int lane, const u32* tap_lut, u64 t_start, u64* acc, Sync& sync, int wave,
+                         u32 wait_need, u64* xi_in, const u8* up_intra, const u8* line_in, u8* line_out,
+                         u64* xi_out) {
   const int W = d.wmbs, pitch = W * 16;
   u8* Y = d.y + d.slot_y * u64(d.target);
   u8* UV = d.uv + d.slot_uv * u64(d.target);
   const int x0 = x * 16, y0 = row * 16;
   const bool up = row > 0, lf = x > 0;
   const MbRec* recs = static_cast<const MbRec*>(d.mbs);
-  // ---- issue every load
+  // ---- loads that do not depend on the row above, issued before waiting for it: residual
+  // samples, the left column (a left MB that is not carried is inter / I_PCM, final since the
+  // inter kernel), neighbour headers, and top samples of non-intra MBs above
   // residual samples (768 B = 48 lanes x 16 B), computed by the parallel inter pass
   uint4 cv = make_uint4(0, 0, 0, 0);
   if (m.res != avc::kNoRes && lane < 48)
     cv = reinterpret_cast<const uint4*>(d.res + size_t(m.res) * kAvcResSamples)[lane];
   u32 a = 128, b = 128;
-  int xw = -1, xsh = 0;  // tagged word of the previous workgroup's exchange holding sample `a`
+  // where sample `a` of a top lane comes from once the row above is ready: 0 = already loaded
+  // (or none), 1 = previous workgroup's exchange word, 2 = this workgroup's LDS line of the row
+  // above, 3 = the picture (the row above's intra MBs, no LDS line)
+  int src = 0, xw = -1, xsh = 0, lo = 0;
+  const u8* gp = nullptr;
+  auto top = [&](int n, const u8* g, int word, int sh, int lo_off) {
+    if (!up_intra || !up_intra[n]) {
+      a = *g;
+    } else if (xi_in) {
+      src = 1;
+      xw = n * kAvcXgWords + word;
+      xsh = sh;
+    } else if (line_in) {
+      src = 2;
+      lo = n * kIntraLine + lo_off;
+    } else {
+      src = 3;
+      gp = g;
+    }
+  };
   if (lane < 21) {  // luma row above: x0-1 .. x0+19
     const int px = x0 - 1 + lane;
-    if (up && px >= 0 && px < pitch) {
-      if (xi_in && up_intra[px >> 4]) {
-        xw = (px >> 4) * kAvcXgWords + ((px & 15) >> 2);
-        xsh = (px & 3) * 8;
-      } else {
-        a = Y[size_t(y0 - 1) * pitch + px];
-      }
-    }
+    if (up && px >= 0 && px < pitch)
+      top(px >> 4, &Y[size_t(y0 - 1) * pitch + px], (px & 15) >> 2, (px & 3) * 8, px & 15);
   } else if (lane < 37) {  // luma left column
     if (lf && !carry) a = Y[size_t(y0 + lane - 21) * pitch + x0 - 1];
   } else if (lane < 55) {  // chroma row above: x*8-1 .. x*8+7 per component
     const int c = (lane - 37) / 9, k = (lane - 37) % 9, px = x * 8 - 1 + k;
     if (up && px >= 0) {
-      if (xi_in && up_intra[px >> 3]) {
-        const int bo = (px & 7) * 2 + c;  // byte of the MB's NV12 bottom line
-        xw = (px >> 3) * kAvcXgWords + 4 + (bo >> 2);
-        xsh = (bo & 3) * 8;
-      } else {
-        a = UV[size_t(row * 8 - 1) * pitch + px * 2 + c];
-      }
+      const int bo = (px & 7) * 2 + c;  // byte of the MB's NV12 bottom line
+      top(px >> 3, &UV[size_t(row * 8 - 1) * pitch + px * 2 + c], 4 + (bo >> 2), (bo & 3) * 8, 16 + bo);
     }
-  }
-  if (xi_in) {  // (wave-uniform) poll the published words until every one is final
-    u64 v = xw >= 0 ? xg_get(xi_in + xw) : 0;
-    u32 spins = 0;
-    while (__ballot(xw >= 0 && u32(v >> 32) != 1u)) {
-      if (__hip_atomic_load(&sync.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
-      if (++spins > (kSpinLimit >> 4)) {
-        __hip_atomic_store(&sync.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (lane == 0) atomicOr(d.err, 2u);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      if (xw >= 0) v = xg_get(xi_in + xw);
-    }
-    if (xw >= 0) a = u32(v >> xsh) & 0xffu;
   }
   if (lane >= 48) {  // chroma left columns
     const int c = (lane - 48) >> 3, k = (lane - 48) & 7;
@@ -295,6 +293,29 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     const int nx = lane == 56 ? x : lane == 57 ? x + 1 : x - 1, ny = lane == 59 ? row : row - 1;
     h = *reinterpret_cast<const uint4*>(&recs[ny * W + nx]);
   }
+  // ---- the row above: this workgroup's (LDS counter, then LDS line / picture) or the
+  // previous workgroup's (exchange words, polled)
+  const u64 t_wait = d.prof ? clock64() : 0;
+  if (wait_need) wait_row(sync, wave - 1, wait_need, d.err);
+  if (xi_in) {  // (wave-uniform) poll the published words until every one is final
+    u64 v = src == 1 ? xg_get(xi_in + xw) : 0;
+    u32 spins = 0;
+    while (__ballot(src == 1 && u32(v >> 32) != 1u)) {
+      if (__hip_atomic_load(&sync.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+      if (++spins > (kSpinLimit >> 4)) {
+        __hip_atomic_store(&sync.abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) atomicOr(d.err, 2u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (src == 1) v = xg_get(xi_in + xw);
+    }
+    if (src == 1) a = u32(v >> xsh) & 0xffu;
+  }
+  if (src == 2) a = line_in[lo];
+  else if (src == 3) a = *gp;
+  const u64 waited = d.prof ? clock64() - t_wait : 0;
+  acc[0] += waited;
   // ---- availability (B, C, D, A) and the LDS neighbour tiles
   const bool av = avail_hdr(d, h, in_pic, m.slice);
   const bool B = __builtin_amdgcn_readlane(int(av), 56) != 0;
@@ -436,6 +457,7 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     const u32 w = u32(src[0]) | u32(src[1]) << 8 | u32(src[2]) << 16 | u32(src[3]) << 24;
     *reinterpret_cast<u32*>(Y + size_t(y0 + ry) * pitch + x0 + rx) = w;
     if (xi_out && lane >= 60) xg_put(xi_out + size_t(x) * kAvcXgWords + (lane - 60), w, 1u);
+    if (line_out && lane >= 60) *reinterpret_cast<u32*>(line_out + x * kIntraLine + (lane - 60) * 4) = w;
     if (lane < 32) {  // NV12: 8 rows x 16 bytes
       const int cyr = lane >> 2, cxb = (lane & 3) * 2;
       const u8* c0 = &L.ctile[0][(cyr + 1) * kCp + cxb + 1];
@@ -443,6 +465,7 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       const u32 cw = u32(c0[0]) | u32(c1[0]) << 8 | u32(c0[1]) << 16 | u32(c1[1]) << 24;
       *reinterpret_cast<u32*>(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cxb) * 2) = cw;
       if (xi_out && lane >= 28) xg_put(xi_out + size_t(x) * kAvcXgWords + 4 + (lane - 28), cw, 1u);
+      if (line_out && lane >= 28) *reinterpret_cast<u32*>(line_out + x * kIntraLine + 16 + (lane - 28) * 4) = cw;
     }
     if (lane < 16) L.carry[lane] = L.tile[(lane + 1) * kTp + 16];
     if (lane < 16) L.ccarry[lane >> 3][lane & 7] = L.ctile[lane >> 3][((lane & 7) + 1) * kCp + 8];
@@ -451,7 +474,7 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   if (d.prof) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // count the store drain here
     const u64 t_end = clock64();
-    acc[1] += t_loaded - t_start;
+    acc[1] += t_loaded - t_start - waited;
     acc[2] += t_luma - t_res;
     acc[6] += t_res - t_loaded;
     acc[3] += t_chroma - t_luma;
@@ -474,6 +497,9 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
   __shared__ Sync sync;
   __shared__ IntraWave lds[kIntraWaves];
   __shared__ u32 tap_lut[9 * 16];  // Intra_4x4 tap word per (mode, y, x) of a 4x4 block
+  // bottom lines of the intra MBs of rows 0..6 for the row below (pictures up to kIntraLineCols
+  // MBs wide; wider ones read the picture)
+  __shared__ u8 lines[kIntraWaves - 1][kIntraLineCols * kIntraLine];
   for (int t = int(threadIdx.x); t < 9 * 16; t += int(blockDim.x)) {
     const int mode = t >> 4, y = (t >> 2) & 3, x = t & 3;
     tap_lut[t] = mode == 2 ? avc::kTapDc : avc::pack_taps(avc::intra4x4_taps(mode, x, y));
@@ -486,6 +512,9 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
   const bool xin = grp > 0 && wave == 0;
   u64* xi_in = xin ? d.xg + size_t(grp - 1) * W * kAvcXgWords : nullptr;
   u64* xi_out = wave == kIntraWaves - 1 && row + 1 < H ? d.xg + size_t(grp) * W * kAvcXgWords : nullptr;
+  const bool use_lines = W <= kIntraLineCols;
+  const u8* line_in = use_lines && wave > 0 ? lines[wave - 1] : nullptr;
+  u8* line_out = use_lines && wave + 1 < kIntraWaves ? lines[wave] : nullptr;
   u64 acc[7] = {0, 0, 0, 0, 0, 0, 0};  // phase clocks of this wave (flushed once at the end)
   if (row < H) {
     int prev = -2;
@@ -502,7 +531,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
         const u8 kd = u8(q[0].x & 0xff);
         intra = kd == avc::kI4x4 || kd == avc::kI16x16;
       }
-      if (xin)  // which MBs base-1 .. base+64 of the row above come through xi_in
+      if (row > 0)  // which MBs base-1 .. base+64 of the row above are intra (this wavefront's)
         for (int q = lane; q < 66; q += 64) {
           const int ax = base - 1 + q;
           u8 v = 0;
@@ -518,12 +547,11 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
         const int xx = base + __ffsll(static_cast<unsigned long long>(bits)) - 1;
         const u64 t0 = d.prof ? clock64() : 0;
         publish_row(sync, wave, u32(xx));  // every MB left of xx is final
-        if (wave > 0) wait_row(sync, wave - 1, u32(xx + 2 < W ? xx + 2 : W), d.err);
-        const u64 t1 = d.prof ? clock64() : 0;
-        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, t1, acc, sync, xi_in,
-                 xin ? &L.up[1] - base : nullptr, xi_out);
+        // (intra_mb waits for the row above itself, after issuing the loads that do not need it)
+        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, t0, acc, sync, wave,
+                 wave > 0 ? u32(xx + 2 < W ? xx + 2 : W) : 0u, xi_in, row > 0 ? &L.up[1] - base : nullptr,
+                 line_in, line_out, xi_out);
         prev = xx;
-        acc[0] += t1 - t0;
       }
     }
     publish_row(sync, wave, u32(W));
