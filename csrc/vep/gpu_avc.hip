@@ -397,17 +397,29 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     wave_sync();
     // Diagonal schedule: block (bx, by) only reads left / top / top-left / (when available in
     // coding order) top-right neighbours, all on earlier diagonals s = bx + 2 * by: 10 steps of
-    // at most 2 blocks (lanes 0-15 and 16-31).
+    // at most 2 blocks (lanes 0-15 and 16-31). Every step's tap word and residual sample are
+    // loaded up front, so a step is only its neighbour reads, a multiply-add and one store.
     const int g = lane >> 4, i = (lane >> 2) & 3, j = lane & 3;
-#pragma unroll 1
-    for (int st = 0; st < 10; ++st) {
+    auto slot = [&](int st) -> int {  // sample of this lane at step st, -1 if none
       // blocks of diagonal st: (st - 2*yy, yy) for yy = max(0, (st - 3 + 1) / 2) .. min(3, st / 2)
       const int y_lo = st > 3 ? (st - 2) / 2 : 0, y_hi = st / 2 < 3 ? st / 2 : 3;
       const int yy = y_lo + g;
-      if (g < 2 && yy <= y_hi) {
-        const int bx = st - 2 * yy;
-        const int p = (yy * 4 + i) * 16 + bx * 4 + j;
-        const u32 tw = L.taps[p];
+      return g < 2 && yy <= y_hi ? (yy * 4 + i) * 16 + (st - 2 * yy) * 4 + j : -1;
+    };
+    u32 tws[10];
+    int rss[10];
+#pragma unroll
+    for (int st = 0; st < 10; ++st) {
+      const int p = slot(st);
+      tws[st] = p >= 0 ? L.taps[p] : 0u;
+      rss[st] = p >= 0 ? L.res[p] : 0;
+    }
+#pragma unroll
+    for (int st = 0; st < 10; ++st) {
+      const int p = slot(st);
+      if (p >= 0) {
+        const int yy = p >> 6, bx = (p & 15) >> 2;
+        const u32 tw = tws[st];
         const u8* nb = &L.tile[(yy * 4) * kTp + bx * 4];  // neighbour N[0] (top-left) of the block
         int v;
         if (tw >> 31) {
@@ -423,7 +435,7 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
           v = (int((tw >> 21) & 3) * n0 + int((tw >> 23) & 3) * n1 + int((tw >> 25) & 3) * n2 +
                int((tw >> 27) & 3)) >> int((tw >> 29) & 3);
         }
-        v += L.res[p];
+        v += rss[st];
         L.tile[(yy * 4 + i + 1) * kTp + bx * 4 + j + 1] = u8(avc::clip1(v));
       }
       wave_sync();
