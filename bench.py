@@ -64,7 +64,7 @@ def parse_args():
     ap.add_argument("--temporal-noise", type=float, default=1.0, help="per-frame sensor noise")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
     ap.add_argument("--threads", type=int, default=14, help="host parse threads per rank")
-    ap.add_argument("--parse-window", type=int, default=3,
+    ap.add_argument("--parse-window", type=int, default=8,
                     help="ticks a camera's parse may run ahead of the tick being launched")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
     ap.add_argument("--cache-gops", type=int, default=1,
