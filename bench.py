@@ -63,7 +63,8 @@ def parse_args():
     ap.add_argument("--noise", type=float, default=8.0, help="static scene texture amplitude")
     ap.add_argument("--temporal-noise", type=float, default=1.0, help="per-frame sensor noise")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
-    ap.add_argument("--threads", type=int, default=14, help="host parse threads per rank")
+    ap.add_argument("--threads", type=int, default=0,
+                    help="host parse threads per rank (0 = CPU budget / local ranks - 2, at most 14)")
     ap.add_argument("--parse-window", type=int, default=8,
                     help="ticks a camera's parse may run ahead of the tick being launched")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
@@ -112,7 +113,10 @@ def main():
         torch.cuda.set_device(local)
 
     from video_edge_ai_proxy_amd import native as vep
+    from video_edge_ai_proxy_amd.utils import parse_threads_per_rank
 
+    if a.threads <= 0:
+        a.threads = parse_threads_per_rank(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
     cams = a.cams_per_gpu
     S = a.letterbox
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
@@ -274,6 +278,7 @@ def main():
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
             "gpu_lanes": worker.lanes,
+            "parse_threads_per_rank": a.threads,
             "gpu_stages": worker.stages,
             "gpu_inflight_per_lane": worker.inflight,
             "payload_path": ("decode kernel reads slice bytes from pinned host memory over PCIe"

@@ -94,3 +94,17 @@ def test_bench_two_ranks_gloo():
     d = json.loads(line)
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4 and d["config"]["all_gather"]
     assert d["value"] > 0 and d["config"]["parallelism"] == "camera-dp2"
+
+
+def test_parse_threads_split_cpu_budget(monkeypatch):
+    from video_edge_ai_proxy_amd import utils
+
+    monkeypatch.setattr(utils, "host_cpu_budget", lambda: 16)
+    assert utils.parse_threads_per_rank(1) == 14      # single-GPU share: the measured optimum
+    monkeypatch.setattr(utils, "host_cpu_budget", lambda: 128)
+    assert utils.parse_threads_per_rank(8) == 14      # 16 CPUs per rank
+    monkeypatch.setattr(utils, "host_cpu_budget", lambda: 64)
+    assert utils.parse_threads_per_rank(8) == 6       # 8 per rank, 2 left for launch/lanes
+    monkeypatch.setattr(utils, "host_cpu_budget", lambda: 4)
+    assert utils.parse_threads_per_rank(8) == 2       # floor
+    assert utils.host_cpu_budget.__call__() >= 1

@@ -46,3 +46,42 @@ def setup_logging(level: str = "info", json_logs: bool = True) -> logging.Logger
 
 
 log = logging.getLogger("vep")
+
+
+def host_cpu_budget() -> int:
+    """CPUs this process may actually run on: the smaller of its affinity mask and the cgroup
+    CPU quota (cgroup v2 ``cpu.max`` or v1 ``cfs_quota_us``). ``os.cpu_count()`` reports the
+    whole machine, which on a shared GPU node is many times the share a rank gets."""
+    import os
+
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()[:2]
+            if q != "max":
+                quota = int(q) / int(p)
+    except (OSError, ValueError):
+        try:
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+                q = int(f.read())
+            with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+                p = int(f.read())
+            if q > 0 and p > 0:
+                quota = q / p
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        n = min(n, max(1, int(quota)))
+    return max(1, n)
+
+
+def parse_threads_per_rank(local_world: int, cap: int = 14, reserve: int = 2) -> int:
+    """Host CAVLC parse threads for one rank: the node's CPU budget split over the ranks that
+    share it, minus ``reserve`` for the rank's launcher / lane / gRPC threads, capped at ``cap``
+    (14 on a 16-CPU single-GPU share: the measured optimum, profiles/r1_sweep_threads_v17.txt)."""
+    share = host_cpu_budget() // max(1, local_world)
+    return max(2, min(cap, share - reserve))
