@@ -713,30 +713,74 @@ __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
   return int((in.bs[i >> 3] >> (4 * (i & 7))) & 15u);
 }
 
+// filter_samples (avc_recon.h) for a luma or a chroma line in one instruction stream, so the
+// luma lanes (0-15) and chroma lanes (16-31) of a half-wave run one filter body together instead
+// of the two type-specialised copies back to back. p2/p3/q2/q3 are read for chroma lines too
+// (in-bounds LDS of the DbkWave tile, values unused) and only p0/q0 are stored for them.
+__device__ inline void filter_line_any(u8* s, int step, int bs, int alpha, int beta, int tc0, bool chroma) {
+  const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
+  const int p2 = s[-3 * step], p3 = s[-4 * step], q2 = s[2 * step], q3 = s[3 * step];
+  if (!(avc::iabs(p0 - q0) < alpha && avc::iabs(p1 - p0) < beta && avc::iabs(q1 - q0) < beta)) return;
+  const int ap = avc::iabs(p2 - p0), aq = avc::iabs(q2 - q0);
+  const bool lp = !chroma && ap < beta, lq = !chroma && aq < beta;
+  int np0, nq0, np1 = p1, nq1 = q1, np2 = p2, nq2 = q2;
+  if (bs < 4) {
+    const int tc = chroma ? tc0 + 1 : tc0 + int(lp) + int(lq);
+    const int dl = avc::clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+    np0 = avc::clip1(p0 + dl);
+    nq0 = avc::clip1(q0 - dl);
+    if (lp) np1 = p1 + avc::clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
+    if (lq) nq1 = q1 + avc::clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
+  } else {
+    const bool strong = !chroma && avc::iabs(p0 - q0) < ((alpha >> 2) + 2);
+    if (lp && strong) {
+      np0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+      np1 = (p2 + p1 + p0 + q0 + 2) >> 2;
+      np2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+    } else {
+      np0 = (2 * p1 + p0 + q1 + 2) >> 2;
+    }
+    if (lq && strong) {
+      nq0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+      nq1 = (p0 + q0 + q1 + q2 + 2) >> 2;
+      nq2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+    } else {
+      nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
+    }
+  }
+  s[-step] = u8(np0);
+  s[0] = u8(nq0);
+  if (!chroma) {
+    s[-2 * step] = u8(np1);
+    s[step] = u8(nq1);
+    s[-3 * step] = u8(np2);
+    s[2 * step] = u8(nq2);
+  }
+}
+
 // One direction of an MB's edges, whole wave (lanes of a half-wave: luma lines 0-15, chroma
 // lines 16-31, `any` = this half's MB has an edge to filter): 4 edges in order, each line by
-// filter_line_t (the CPU decoder's core) on the LDS tile.
+// filter_line_any on the LDS tile (chroma lines on the even edges only).
 __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
+  const bool ch = l >= 16;
+  const int c = (l - 16) >> 3, k = (l - 16) & 7;
   for (int e = 0; e < 4; ++e) {
-    const int pk = e > 0 ? 2 : dir;  // edge params: left / top / internal
-    if (any) {
-      if (l < 16) {
-        const int bs = bs_of(L.info, dir, e, l >> 2);
-        if (bs) {
-          const int al = L.info.alpha[pk], be = L.info.beta[pk];
-          const int tc = bs < 4 ? L.info.tc0[pk][bs - 1] : 0;
-          if (dir == 0) avc::filter_line_t(&L.y[(4 + l) * 20 + 4 + 4 * e], 1, bs, al, be, tc, false);
-          else avc::filter_line_t(&L.y[(4 + 4 * e) * 20 + 4 + l], 20, bs, al, be, tc, false);
+    if (any && (!ch || !(e & 1))) {
+      const int bs = bs_of(L.info, dir, e, ch ? k >> 1 : l >> 2);
+      if (bs) {
+        const int pi = (e > 0 ? 2 : dir) + (ch ? 3 : 0);  // edge params: left / top / internal
+        const int al = L.info.alpha[pi], be = L.info.beta[pi];
+        const int tc = bs < 4 ? L.info.tc0[pi][bs - 1] : 0;
+        u8* sp;
+        int step;
+        if (!ch) {
+          sp = dir == 0 ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.y[(4 + 4 * e) * 20 + 4 + l];
+          step = dir == 0 ? 1 : 20;
+        } else {
+          sp = dir == 0 ? &L.c[c][(2 + k) * 10 + 2 + 2 * e] : &L.c[c][(2 + 2 * e) * 10 + 2 + k];
+          step = dir == 0 ? 1 : 10;
         }
-      } else if (!(e & 1)) {
-        const int c = (l - 16) >> 3, k = (l - 16) & 7;
-        const int bs = bs_of(L.info, dir, e, k >> 1);
-        if (bs) {
-          const int al = L.info.alpha[3 + pk], be = L.info.beta[3 + pk];
-          const int tc = bs < 4 ? L.info.tc0[3 + pk][bs - 1] : 0;
-          if (dir == 0) avc::filter_line_t(&L.c[c][(2 + k) * 10 + 2 + 2 * e], 1, bs, al, be, tc, true);
-          else avc::filter_line_t(&L.c[c][(2 + 2 * e) * 10 + 2 + k], 10, bs, al, be, tc, true);
-        }
+        filter_line_any(sp, step, bs, al, be, tc, ch);
       }
     }
     wave_sync();
