@@ -3,10 +3,11 @@ PY      ?= python
 HIPCC   ?= hipcc
 ARCH    ?= gfx950
 SRCS     = $(wildcard csrc/vep/*.cpp)
+HIP_SRCS = $(wildcard csrc/vep/*.hip)
 TSAN_DIR = build/tsan
 ASAN_DIR = build/asan
 
-.PHONY: build test test-gpu bench bench-h265 smoke tsan asan clean
+.PHONY: build test test-gpu bench bench-h265 smoke tsan asan link-check clean
 
 build:                     ## compile the extension in-tree (video_edge_ai_proxy_amd/_vep*.so)
 	$(PY) csrc/build.py
@@ -28,16 +29,27 @@ bench-h265: build          ## BASELINE config 5 shape on one GPU: 8 x 4K30 H.265
 
 # ThreadSanitizer / AddressSanitizer builds of the native stress driver. Sanitizers apply to
 # host code only (-Xarch_host); the driver runs the CPU backend, so no GPU is needed.
-$(TSAN_DIR)/native_stress: $(SRCS) csrc/vep/gpu_kernels.hip csrc/tests/native_stress.cpp $(wildcard csrc/vep/*.h)
+# Every data-plane source goes in (all csrc/vep/*.cpp host code and every csrc/vep/*.hip kernel
+# file, as csrc/build.py does), so the sanitizer binaries link exactly what the module links.
+$(TSAN_DIR)/native_stress: $(SRCS) $(HIP_SRCS) csrc/tests/native_stress.cpp $(wildcard csrc/vep/*.h)
 	mkdir -p $(TSAN_DIR)
 	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O1 -g -Xarch_host -fsanitize=thread \
-	  $(SRCS) csrc/tests/native_stress.cpp -x hip csrc/vep/gpu_kernels.hip -o $@ -lpthread
+	  $(SRCS) csrc/tests/native_stress.cpp -x hip $(HIP_SRCS) -o $@ -lpthread
 
-$(ASAN_DIR)/native_stress: $(SRCS) csrc/vep/gpu_kernels.hip csrc/tests/native_stress.cpp $(wildcard csrc/vep/*.h)
+$(ASAN_DIR)/native_stress: $(SRCS) $(HIP_SRCS) csrc/tests/native_stress.cpp $(wildcard csrc/vep/*.h)
 	mkdir -p $(ASAN_DIR)
 	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O1 -g -Xarch_host -fsanitize=address \
 	  -Xarch_host -fno-omit-frame-pointer \
-	  $(SRCS) csrc/tests/native_stress.cpp -x hip csrc/vep/gpu_kernels.hip -o $@ -lpthread
+	  $(SRCS) csrc/tests/native_stress.cpp -x hip $(HIP_SRCS) -o $@ -lpthread
+
+# Cheap link check of the sanitizer target's source set (default CPU suite): the stress driver
+# against the data-plane objects csrc/build.py already compiled (no sanitizer instrumentation).
+link-check: build
+	mkdir -p build/linkcheck
+	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O0 -c csrc/tests/native_stress.cpp -Icsrc \
+	  -o build/linkcheck/native_stress.o
+	$(HIPCC) --offload-arch=$(ARCH) build/linkcheck/native_stress.o build/obj/vep__*.o \
+	  -o build/linkcheck/native_stress -lpthread
 
 tsan: $(TSAN_DIR)/native_stress
 	cd /tmp && TSAN_OPTIONS="halt_on_error=1" $(CURDIR)/$(TSAN_DIR)/native_stress

@@ -95,8 +95,26 @@ def measure_latency(worker, cams, samples, tick, fps):
     return summarize(serve_ms), summarize(next_ms), len(serve_ms)
 
 
+def spawn_ranks(n: int) -> int:
+    """`--gpus N` without a torch.distributed environment: run N fresh rank processes (one per
+    GPU) through torch.distributed.run and return their exit code. Called before this process
+    touches the GPU, so the parent never holds a device context while its children run."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__),
+           *sys.argv[1:]]
+    return subprocess.call(cmd)
+
+
 def main():
     a = parse_args()
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.cpu:
+        sys.exit(spawn_ranks(a.gpus))
     import torch
     import torch.distributed as dist
 
@@ -183,11 +201,15 @@ def main():
 
     for i in range(a.warmup):
         step(i)
+    # the parse pipeline runs ahead of the launched tick: launch what it has already parsed and
+    # stop it, so every tick of the timed region is parsed inside the timed region
+    rb.quiesce()
     drain()
     if world > 1:
         dist.barrier()
     sync()
-    f0, p0, b0, g0 = rb.frames, rb.parse_ms, rb.batch_ms, worker.gpu_ms_total
+    f0, p0, b0, g0 = worker.frames, rb.parse_ms, rb.batch_ms, worker.gpu_ms_total
+    d0, pf0, l0 = worker.dropped, rb.parse_failures, rb.frames
     pw0 = rb.parse_wait_ms
     ip0, sg0 = worker.bytes_inplace, worker.bytes_staged
     tm0 = worker.timings()
@@ -199,7 +221,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
-    frames = rb.frames - f0
+    # frames committed to the camera rings (readable by clients), not jobs launched
+    frames = worker.frames - f0
+    launched = rb.frames - l0
+    dropped = (worker.dropped - d0) + (rb.parse_failures - pf0)
     parse_ms, batch_ms, gpu_ms = rb.parse_ms - p0, rb.batch_ms - b0, worker.gpu_ms_total - g0
     parse_wait_ms = rb.parse_wait_ms - pw0
     tm1 = worker.timings()
@@ -207,9 +232,9 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        fr = torch.tensor([frames], dtype=torch.float64, device=dev)
+        fr = torch.tensor([frames, dropped, launched], dtype=torch.float64, device=dev)
         dist.all_reduce(fr, op=dist.ReduceOp.SUM)
-        frames = int(fr.item())
+        frames, dropped, launched = (int(v) for v in fr.tolist())
 
     serve_lat = next_lat = (None, None)
     nlat = 0
@@ -231,7 +256,8 @@ def main():
             "metric": METRIC,
             "value": round(fps, 2),
             "unit": "frames/s",
-            "n_gpus": world if world > 1 else a.gpus if use_gpu else 0,
+            "n_gpus": world if use_gpu else 0,
+            "n_ranks": world,
             "steps": a.steps,
             "warmup": a.warmup,
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
@@ -273,6 +299,12 @@ def main():
                                 "native subset decoder: CPU " + ENTROPY[a.codec] + " parse + gfx950 "
                                 "HIP PCM reconstruct/NV12->BGR24 (rocDecode absent in image)"),
             "per_gpu_fps": round(fps / max(world, 1), 2),
+            "frames_published": frames,
+            "frames_launched": launched,
+            "frames_dropped": dropped,
+            "frame_count_definition": "frames committed to camera HBM rings during the timed "
+                                      "region (parse -> GPU reconstruct -> BGR24 -> ring publish); "
+                                      "dropped = parse failures + frames the worker did not publish",
             "rank0_host_parse_ms_per_step": round(parse_ms / a.steps, 4),
             "rank0_parse_wait_ms_per_step": round(parse_wait_ms / a.steps, 4),
             "rank0_batch_ms_per_step": round(batch_ms / a.steps, 4),
@@ -299,6 +331,9 @@ def main():
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if dropped:
+        print(f"bench: {dropped} frames dropped in the timed region", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

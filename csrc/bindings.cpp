@@ -617,6 +617,7 @@ PYBIND11_MODULE(_vep, m) {
            })
       .def_property_readonly("batches", &Worker::batches)
       .def_property_readonly("frames", &Worker::frames)
+      .def_property_readonly("dropped", &Worker::dropped)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
       .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)
       .def_property_readonly("direct_reads", &Worker::direct_reads)
@@ -636,6 +637,8 @@ PYBIND11_MODULE(_vep, m) {
       .def("step", &ReplayBench::step, py::call_guard<py::gil_scoped_release>())
       .def("parse_only_ms", &ReplayBench::parse_only_ms, py::call_guard<py::gil_scoped_release>())
       .def("drain", &ReplayBench::drain, py::call_guard<py::gil_scoped_release>())
+      .def("quiesce", &ReplayBench::quiesce, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("parse_failures", &ReplayBench::parse_failures)
       .def_property_readonly("frames", &ReplayBench::frames)
       .def_property_readonly("payload_bytes", &ReplayBench::bitstream_bytes)
       .def_property_readonly("stream_bytes", &ReplayBench::stream_bytes)

@@ -59,7 +59,9 @@ int ReplayBench::pick_locked() const {
   // oldest tick first; within a tick the largest AU first (a keyframe starts at once)
   int best = -1;
   for (int c = 0; c < int(cams_.size()); ++c) {
-    if (cam_busy_[size_t(c)] || cam_tick_[size_t(c)] >= consume_ + window_) continue;
+    if (cam_busy_[size_t(c)] || cam_tick_[size_t(c)] >= consume_ + window_ ||
+        cam_tick_[size_t(c)] >= gate_)
+      continue;
     if (best < 0 || cam_tick_[size_t(c)] < cam_tick_[size_t(best)] ||
         (cam_tick_[size_t(c)] == cam_tick_[size_t(best)] &&
          aus_[size_t(c)][pos_[size_t(c)]]->bytes() > aus_[size_t(best)][pos_[size_t(best)]]->bytes()))
@@ -101,7 +103,7 @@ void ReplayBench::parse_loop() {
     k.ok[size_t(c)] = ok ? 1 : 0;
     cam_tick_[size_t(c)] = t + 1;
     cam_busy_[size_t(c)] = 0;
-    if (++k.done == int(cams_.size())) ready_cv_.notify_all();
+    if (++k.done == int(cams_.size()) || gate_ != INT64_MAX) ready_cv_.notify_all();
   }
 }
 
@@ -115,6 +117,7 @@ std::vector<DecodeJob> ReplayBench::take(bool timed) {
   out.reserve(cams_.size());
   for (size_t i = 0; i < cams_.size(); ++i) {
     if (k.ok[i]) out.push_back(std::move(k.jobs[i]));
+    else ++parse_fail_;
     k.jobs[i] = DecodeJob{};
     k.ok[i] = 0;
   }
@@ -132,7 +135,40 @@ double ReplayBench::parse_only_ms(int ticks) {
   return double(mono_us() - t0) / 1000.0 / std::max(1, ticks);
 }
 
+void ReplayBench::quiesce() {
+  i64 upto;
+  {
+    std::unique_lock<std::mutex> g(mu_);
+    upto = consume_;
+    for (size_t c = 0; c < cams_.size(); ++c) upto = std::max(upto, cam_tick_[c] + (cam_busy_[c] ? 1 : 0));
+    gate_ = upto;  // no camera starts a tick >= upto; the ones behind catch up to it
+  }
+  work_cv_.notify_all();
+  while (true) {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      if (consume_ >= upto) break;
+    }
+    std::vector<DecodeJob> jobs = take(false);
+    w_.launch_async(jobs);
+  }
+  {
+    std::unique_lock<std::mutex> g(mu_);
+    ready_cv_.wait(g, [&] {
+      for (size_t c = 0; c < cams_.size(); ++c)
+        if (cam_busy_[c]) return false;
+      return true;
+    });
+  }
+  w_.complete_all();
+}
+
 void ReplayBench::step() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (gate_ != INT64_MAX) gate_ = INT64_MAX;  // re-open parsing (after quiesce)
+  }
+  work_cv_.notify_all();
   std::vector<DecodeJob> jobs = take(true);
   for (auto& j : jobs) {
     bytes_ += u64(j.upd.nslots) * kPcmMbBytes;

@@ -25,6 +25,13 @@ class ReplayBench {
   ~ReplayBench();
   void step();      // takes the next parsed tick and launches it (publishes tick t - stages)
   void drain();     // publish every launched tick
+  // Bring the parse pipeline to rest before a timed region: stop parse threads from starting
+  // new ticks, let every camera finish the ticks already started, launch (untimed) every tick
+  // parsed so far and drain the GPU. The next step() re-opens parsing, so no tick of the timed
+  // region is parsed before it starts.
+  void quiesce();
+  // jobs whose parse failed (dropped before the GPU); the worker counts its own drops
+  u64 parse_failures() const { return parse_fail_; }
   // Host parse throughput alone: consume `ticks` parsed ticks without GPU work (jobs dropped)
   // and return the mean wall ms per tick.
   double parse_only_ms(int ticks);
@@ -55,13 +62,14 @@ class ReplayBench {
   const int window_;
   std::vector<Tick> ring_;      // tick T in slot T % window_
   i64 consume_ = 0;             // next tick step() takes
+  i64 gate_ = INT64_MAX;        // parse threads start only ticks < gate_ (quiesce)
   std::vector<i64> cam_tick_;   // next tick each camera parses
   std::vector<char> cam_busy_;
   bool stop_ = false;
   std::mutex mu_;
   std::condition_variable work_cv_, ready_cv_;
   std::vector<std::thread> workers_;
-  u64 frames_ = 0, bytes_ = 0;
+  u64 frames_ = 0, bytes_ = 0, parse_fail_ = 0;
   std::atomic<u64> stream_bytes_{0}, stream_frames_{0}, parse_ns_{0};
   double wait_us_ = 0, batch_us_ = 0;
 };

@@ -8,12 +8,15 @@
 //  * avc_intra_kernel / avc_deblock_kernel — the two inherently ordered passes. Intra
 //    prediction reads reconstructed neighbours (left, top, top-right) and the loop filter reads
 //    the left/top neighbours' filtered samples, so both run as a 2-MB-skewed wavefront over
-//    MB rows. One 1024-lane workgroup (16 wave64s) per picture: wave w walks rows w, w+16, ...,
-//    row r waits until row r-1 has finished MB x+1 via an LDS progress counter. Keeping a
-//    picture's wavefront inside one workgroup (one CU) makes every hand-off a workgroup-scope
-//    release/acquire: no cross-XCD L2 write-back / invalidate per macroblock (MI355X has one L2
-//    per XCD), and no inter-workgroup spin that could deadlock. Pictures of different cameras
-//    are different workgroups, spread over the XCDs by the dispatcher.
+//    MB rows. A picture runs avc_dbk_groups(H) workgroups of kAvcDbkWgRows rows each (one or
+//    two rows per wave64): inside a workgroup row r waits until row r-1 has finished MB x+1 via
+//    LDS progress counters (workgroup-scope release/acquire); a workgroup's first row polls the
+//    previous workgroup's last row through tagged device-coherent exchange words (AvcDesc::xg).
+//    That cross-workgroup spin relies on in-order dispatch: the grid order in launch_avc_*
+//    puts a picture's workgroups on one XCD (one L2) in row order, so every workgroup a spin
+//    waits on was dispatched earlier and is resident. Every spin is bounded (kSpinLimit): a
+//    timeout sets AvcDesc::err bit 1, aborts the picture's waits so all waves drain, and the
+//    worker drops the frame (logged as a wavefront timeout).
 //    Per wave the MB under reconstruction lives in LDS; the left neighbour's edge columns are
 //    carried in LDS (same-wave read-after-write never goes through global memory).
 //

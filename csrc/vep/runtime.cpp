@@ -1196,10 +1196,19 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
   std::lock_guard<std::mutex> g(cams_mu_);
   for (size_t i = 0; i < jobs.size(); ++i) {
     auto& cp = cams_[size_t(jobs[i].cam)];
-    if (!cp || !cp->ring_) continue;
+    if (!cp || !cp->ring_) {
+      dropped_.fetch_add(1, std::memory_order_relaxed);
+      continue;
+    }
     if (err && err[i]) {
+      dropped_.fetch_add(1, std::memory_order_relaxed);
       cp->errors.fetch_add(1, std::memory_order_relaxed);
-      cp->logs.add(true, "corrupt keyframe: I_PCM header check failed; waiting for the next keyframe");
+      // err bit 0: a speculatively placed I_PCM block failed its header check (decode_convert);
+      // bit 1: a reconstruction wavefront timed out waiting for a neighbour (gpu_avc.hip)
+      if (err[i] & 2u)
+        cp->logs.add(true, "GPU reconstruction wavefront timed out; frame dropped, waiting for the next keyframe");
+      if (err[i] & ~2u)
+        cp->logs.add(true, "corrupt keyframe: I_PCM header check failed; waiting for the next keyframe");
       cp->broken_ = true;
       cp->ring_->abort(slots[i]);
       continue;
@@ -1207,6 +1216,7 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
     if (cp->broken_) {  // surfaces are garbage until a keyframe rewrites every MB
       if (!jobs[i].refresh) {
         cp->ring_->abort(slots[i]);
+        dropped_.fetch_add(1, std::memory_order_relaxed);
         continue;
       }
       cp->broken_ = false;
@@ -1221,8 +1231,8 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
     }
     cp->ring_->commit(slots[i], jobs[i].meta);
     cp->decoded.fetch_add(1, std::memory_order_relaxed);
+    frames_.fetch_add(1, std::memory_order_relaxed);
   }
-  frames_.fetch_add(jobs.size());
   batches_.fetch_add(1);
 }
 
@@ -1278,6 +1288,7 @@ void Worker::launch_on(Lane& ln, Batch&& b) {
         auto& cp = cams_[size_t(st.jobs[i].cam)];
         if (cp && cp->ring_) cp->ring_->abort(st.slots[i]);
       }
+      dropped_.fetch_add(st.jobs.size(), std::memory_order_relaxed);
     }
     st.jobs.clear();
     st.slots.clear();

@@ -270,7 +270,11 @@ class Worker {
   // slice bytes the GPU read in place from pinned AU blocks vs. staged by a host memcpy
   u64 bytes_inplace() const { return pinned_bytes_inplace_.load(); }
   u64 bytes_staged() const { return pinned_bytes_staged_.load(); }
+  // frames committed to camera rings (what a client can read) / frames a batch produced but the
+  // worker did not publish (GPU check failure, wavefront timeout, camera waiting for a keyframe
+  // after an error, camera removed)
   u64 frames() const { return frames_.load(); }
+  u64 dropped() const { return dropped_.load(); }
   // GPU time of the batches (first event to last, per lane; the busiest lane's total)
   double gpu_ms_total() const;
   // clock64() phase accumulators of the wavefront kernels (VEP_AVC_PROF=1; gpu::kAvcProfSlots)
@@ -368,7 +372,7 @@ class Worker {
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;
-  std::atomic<u64> batches_{0}, frames_{0};
+  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0};
   std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0};
   std::mutex timers_mu_;
   bool direct_reads_ = false;

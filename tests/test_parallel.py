@@ -92,7 +92,7 @@ def test_bench_two_ranks_gloo():
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 4 and d["config"]["all_gather"]
+    assert d["n_ranks"] == 2 and d["n_gpus"] == 0 and d["config"]["global_batch"] == 4 and d["config"]["all_gather"]
     assert d["value"] > 0 and d["config"]["parallelism"] == "camera-dp2"
 
 

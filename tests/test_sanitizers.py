@@ -20,3 +20,12 @@ def test_native_stress_under_sanitizer(target):
     assert r.returncode == 0, out[-4000:]
     assert "native_stress ok" in out
     assert "WARNING: ThreadSanitizer" not in out and "ERROR: AddressSanitizer" not in out
+
+
+def test_sanitizer_target_links():
+    """The sanitizer binaries' source set links (every csrc/vep/*.cpp + *.hip): a cheap check
+    that runs in the default CPU suite, so a missing kernel file breaks here, not only under
+    VEP_SANITIZERS=1."""
+    r = subprocess.run(["make", "-C", ROOT, "link-check"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-4000:]
+    assert os.path.exists(os.path.join(ROOT, "build", "linkcheck", "native_stress"))

@@ -88,8 +88,11 @@ class ConsumerBatch:
         shape = (size * size * 3 // 2,) if fmt == "nv12" else (size, size, 3)
         self.bufs = [torch.zeros((cams, *shape), dtype=torch.uint8, device=device)
                      for _ in range(2)]
+        # a process group of any size (a 1-rank RCCL group included) gathers through the
+        # collective; without one the local batch is the node batch
+        self.collective = world > 1 or (dist.is_available() and dist.is_initialized())
         self.out = [torch.zeros((world * cams, *shape), dtype=torch.uint8, device=device)
-                    for _ in range(2)] if world > 1 else None
+                    for _ in range(2)] if self.collective else None
         self.handles = [None, None]
         self.tick = 0
 
@@ -110,7 +113,7 @@ class ConsumerBatch:
         self.worker.complete_all()  # the tick's letterbox kernels must have finished
         b = self.tick & 1
         self.tick += 1
-        if self.world == 1:
+        if not self.collective:
             return self.bufs[b], None
         w = dist.all_gather_into_tensor(self.out[b], self.bufs[b], async_op=async_op)
         self.handles[b] = w if async_op else None
