@@ -101,15 +101,34 @@ struct CpuDecoder {
         for (auto& h : slots)
           if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16) h.alloc(pic->wmbs * 16, pic->hmbs * 16);
         avc::cpu_reconstruct(*pic, slots);
-        last = pic->info;
-        target = pic->target;
         coded = pic->info.coded_mbs;
+        pictures.push_back(pic->info);
+        // B-frame reordering: the newest frame that left the reorder buffer, if any
+        if (pic->outputs.empty()) return py::none();
+        last = pic->outputs.back().info;
+        target = pic->outputs.back().slot;
+        last_poc = pic->outputs.back().poc;
+        pending_outputs = pic->outputs;
       }
     }
     py::array_t<uint8_t> o({last.height, last.width, 3});
     cpu_nv12_to_bgr(out(), last.crop_left, last.crop_top, last.width, last.height, o.mutable_data());
     return o;
   }
+  // Frames still in the reorder buffer (end of stream), oldest first.
+  py::list flush() {
+    py::list out_list;
+    for (const auto& f : avc.flush_output()) {
+      py::array_t<uint8_t> o({f.info.height, f.info.width, 3});
+      cpu_nv12_to_bgr(slots[size_t(f.slot)], f.info.crop_left, f.info.crop_top, f.info.width, f.info.height,
+                      o.mutable_data());
+      out_list.append(o);
+    }
+    return out_list;
+  }
+  std::vector<PictureInfo> pictures;      // every decoded picture (decoding order)
+  std::vector<avc::OutFrame> pending_outputs;  // outputs of the last decode() (output order)
+  int last_poc = 0;
 };
 
 PYBIND11_MODULE(_vep, m) {
@@ -212,6 +231,9 @@ PYBIND11_MODULE(_vep, m) {
   py::class_<CpuDecoder>(m, "CpuDecoder")
       .def(py::init<>())
       .def("decode", &CpuDecoder::decode)
+      .def("flush", &CpuDecoder::flush)
+      .def_property_readonly("last_poc", [](const CpuDecoder& d) { return d.last_poc; })
+      .def_property_readonly("outputs_last", [](const CpuDecoder& d) { return int(d.pending_outputs.size()); })
       .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
       .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.coded; })
       .def_property_readonly("general", [](const CpuDecoder& d) { return d.general; })

@@ -3,8 +3,10 @@
 #include "avc.h"
 
 #include <algorithm>
+#include <array>
 
 #include "avc_cavlc.h"
+#include "avc_internal.h"
 
 namespace vep::avc {
 
@@ -100,7 +102,30 @@ int MbNeighbours::pred_intra4x4(int mb, int blk, bool constrained) const {
   return ma < mbm ? ma : mbm;
 }
 
-MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done) const {
+int MbNeighbours::pred_intra8x8(int mb, int b8, bool constrained) const {
+  // §8.3.2.1: neighbour 8x8 blocks A / B; an Intra_4x4 neighbour contributes the 4x4 block
+  // n = 1 (A) / 2 (B) of its 8x8 — exactly the 4x4 block left of / above the 8x8's top-left
+  // block, which is what MbState::i4 holds (8x8 modes are replicated over their four blocks)
+  const int blk = (b8 & 1) * 2 + (b8 >> 1) * 8;
+  const int bx = blk & 3, by = blk >> 2;
+  const int am = mb_at(mb, bx * 4 - 1, by * 4), bm = mb_at(mb, bx * 4, by * 4 - 1);
+  if (am < 0 || bm < 0) return 2;
+  const MbState& a = st_[size_t(am)];
+  const MbState& b = st_[size_t(bm)];
+  if (constrained && (!is_intra(a.kind) || !is_intra(b.kind))) return 2;
+  auto mode = [](const MbState& n, int r, int b8n) -> int {
+    if (n.kind == kI8x8) return n.i4[(b8n & 1) * 2 + (b8n >> 1) * 8];
+    if (n.kind == kI4x4) return n.i4[r];
+    return 2;
+  };
+  // A: the 4x4 block left of the top-left block (right column of the left 8x8), B: above
+  const int ra = bx > 0 ? blk - 1 : blk + 3, rb = by > 0 ? blk - 4 : blk + 12;
+  const int b8a = ((ra >> 3) << 1) | ((ra & 3) >> 1), b8b = ((rb >> 3) << 1) | ((rb & 3) >> 1);
+  const int ma = mode(a, ra, b8a), mbm = mode(b, rb, b8b);
+  return ma < mbm ? ma : mbm;
+}
+
+MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done, int list) const {
   Nb r{false, -1, {0, 0}};
   const int m = mb_at(mb, x, y);
   if (m < 0) return r;
@@ -109,22 +134,23 @@ MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done) const {
   r.avail = true;
   const MbState& s = st_[size_t(m)];
   if (is_intra(s.kind)) return r;
-  r.ref = s.ref[((blk >> 3) << 1) | ((blk & 3) >> 1)];
-  r.mv[0] = s.mv[blk][0];
-  r.mv[1] = s.mv[blk][1];
+  r.ref = s.ref[list][((blk >> 3) << 1) | ((blk & 3) >> 1)];
+  if (r.ref < 0) return r;  // list unused: refIdx -1, mv 0
+  r.mv[0] = s.mv[list][blk][0];
+  r.mv[1] = s.mv[list][blk][1];
   return r;
 }
 
 static int median3(int a, int b, int c) { return a + b + c - std::min({a, b, c}) - std::max({a, b, c}); }
 
-void MbNeighbours::pred_mv(int mb, int x4, int y4, int w4, int h4, int ref, u16 done, int shape,
+void MbNeighbours::pred_mv(int mb, int x4, int y4, int w4, int h4, int list, int ref, u16 done, int shape,
                            int out[2]) const {
   (void)h4;
   const int x = x4 * 4, y = y4 * 4, w = w4 * 4;
-  Nb A = motion_at(mb, x - 1, y, done);
-  Nb B = motion_at(mb, x, y - 1, done);
-  Nb C = motion_at(mb, x + w, y - 1, done);
-  if (!C.avail) C = motion_at(mb, x - 1, y - 1, done);  // D replaces an unavailable C
+  Nb A = motion_at(mb, x - 1, y, done, list);
+  Nb B = motion_at(mb, x, y - 1, done, list);
+  Nb C = motion_at(mb, x + w, y - 1, done, list);
+  if (!C.avail) C = motion_at(mb, x - 1, y - 1, done, list);  // D replaces an unavailable C
   auto take = [&](const Nb& n) {
     out[0] = n.mv[0];
     out[1] = n.mv[1];
@@ -146,60 +172,31 @@ void MbNeighbours::pred_mv(int mb, int x4, int y4, int w4, int h4, int ref, u16 
 void MbNeighbours::pskip_mv(int mb, int out[2]) const {
   out[0] = out[1] = 0;
   if (mb_at(mb, -1, 0) < 0 || mb_at(mb, 0, -1) < 0) return;
-  const Nb A = motion_at(mb, -1, 0, 0), B = motion_at(mb, 0, -1, 0);
+  const Nb A = motion_at(mb, -1, 0, 0, 0), B = motion_at(mb, 0, -1, 0, 0);
   if ((A.ref == 0 && A.mv[0] == 0 && A.mv[1] == 0) || (B.ref == 0 && B.mv[0] == 0 && B.mv[1] == 0))
     return;
-  pred_mv(mb, 0, 0, 4, 4, 0, 0, 0, out);
+  pred_mv(mb, 0, 0, 4, 4, 0, 0, 0, 0, out);
+}
+
+void MbNeighbours::mb_neighbour_refs(int mb, int list, int ref[3]) const {
+  const Nb A = motion_at(mb, -1, 0, 0, list), B = motion_at(mb, 0, -1, 0, list);
+  Nb C = motion_at(mb, 16, -1, 0, list);
+  if (!C.avail) C = motion_at(mb, -1, -1, 0, list);
+  ref[0] = A.ref;
+  ref[1] = B.ref;
+  ref[2] = C.ref;
 }
 
 // ------------------------------------------------------------------------- parameter sets
 
 namespace {
 
-// Profile features outside the CAVLC 4:2:0 8-bit flat-scaling subset.
-void check_sps_supported(const u8* rbsp, size_t n, const Sps& s) {
+// Stream features outside the supported subset (progressive 8-bit 4:2:0, no lossless).
+void check_sps_supported(const Sps& s) {
   if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
     throw UnsupportedStream("only 8-bit 4:2:0 H.264 is supported");
   if (!s.frame_mbs_only) throw UnsupportedStream("interlaced H.264 (field / MBAFF) is not supported");
-  switch (s.profile_idc) {
-    case 100: case 110: case 122: case 244: case 44: case 83: case 86: case 118: case 128:
-    case 138: case 139: case 134: case 135: {
-      Bits br(rbsp + 1, n - 1);
-      br.u(24);
-      br.ue();
-      const u32 cf = br.ue();
-      if (cf == 3) br.u1();
-      br.ue();
-      br.ue();
-      if (br.u1()) throw UnsupportedStream("lossless (transform bypass) H.264 is not supported");
-      if (br.u1()) throw UnsupportedStream("H.264 scaling matrices are not supported");
-      break;
-    }
-    default: break;
-  }
-}
-
-void check_pps_supported(const u8* rbsp, size_t n, const Pps& p) {
-  if (p.cabac) throw UnsupportedStream("CABAC H.264 (Main/High entropy coding) needs the VCN backend");
-  if (p.weighted_pred) throw UnsupportedStream("H.264 weighted prediction is not supported");
-  // Re-walk to the optional High-profile tail (transform_8x8_mode_flag, scaling matrix).
-  Bits br(rbsp + 1, n - 1);
-  br.ue();
-  br.ue();
-  br.u(2);
-  br.ue();
-  br.ue();
-  br.ue();
-  br.u(3);
-  br.se();
-  br.se();
-  br.se();
-  br.u(3);
-  size_t stop = BitReader(rbsp + 1, n - 1).stop_bit_pos();
-  if (br.pos() < stop) {
-    if (br.u1()) throw UnsupportedStream("H.264 8x8 transforms (High profile) are not supported");
-    if (br.u1()) throw UnsupportedStream("H.264 scaling matrices are not supported");
-  }
+  if (s.transform_bypass) throw UnsupportedStream("lossless (transform bypass) H.264 is not supported");
 }
 
 const u8* unescape(const u8* p, size_t n, std::vector<u32>& epb, std::vector<u8>& scratch,
@@ -229,28 +226,8 @@ struct SliceCtx {
   int slice;
   bool is_p;
   int qp;
-  const std::vector<int>& list0;
+  const std::vector<ListEntry>& list0;
 };
-
-void h16(int c[16]) {  // 4x4 Hadamard, in place: f = H c H
-  int t[16];
-  for (int i = 0; i < 4; ++i) {
-    const int a = c[i * 4], b = c[i * 4 + 1], d = c[i * 4 + 2], e = c[i * 4 + 3];
-    t[i * 4] = a + b + d + e;
-    t[i * 4 + 1] = a + b - d - e;
-    t[i * 4 + 2] = a - b - d + e;
-    t[i * 4 + 3] = a - b + d - e;
-  }
-  for (int j = 0; j < 4; ++j) {
-    const int a = t[j], b = t[4 + j], d = t[8 + j], e = t[12 + j];
-    c[j] = a + b + d + e;
-    c[4 + j] = a + b - d - e;
-    c[8 + j] = a - b - d + e;
-    c[12 + j] = a - b + d - e;
-  }
-}
-
-i16 sat16(int v) { return i16(v < -32768 ? -32768 : v > 32767 ? 32767 : v); }
 
 // LevelScale4x4 with flat weight matrices (16 * normAdjust4x4), per qP % 6 and raster position.
 struct LevelScaleTable {
@@ -267,6 +244,17 @@ const int (&kLevelScale)[6][16] = kLevelScaleTable.v;
 
 // ------------------------------------------------------------------------- slice header
 
+static void read_ref_mods(Bits& br, std::vector<SliceHdr::RefMod>& mods) {
+  if (!br.u1()) return;  // ref_pic_list_modification_flag_lX
+  for (;;) {
+    const int idc = int(br.ue());
+    if (idc == 3) break;
+    VEP_CHECK(idc <= 2, "bad modification_of_pic_nums_idc");
+    mods.push_back({idc, int(br.ue())});
+    VEP_CHECK(mods.size() <= 33, "too many reference list modifications");
+  }
+}
+
 static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pps& pps) {
   SliceHdr sh;
   sh.nal_type = h264::nal_type(nal_hdr);
@@ -279,28 +267,53 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
   if (sh.idr()) sh.idr_pic_id = int(br.ue());
   if (sps.poc_type == 0) {
     sh.poc_lsb = int(br.u(sps.log2_max_poc_lsb));
-    if (pps.bottom_field_pic_order) br.se();
+    if (pps.bottom_field_pic_order) sh.delta_poc_bottom = br.se();
   } else if (sps.poc_type == 1 && !sps.delta_pic_order_always_zero) {
-    br.se();
-    if (pps.bottom_field_pic_order) br.se();
+    sh.delta_poc[0] = br.se();
+    if (pps.bottom_field_pic_order) sh.delta_poc[1] = br.se();
   }
   if (pps.redundant_pic_cnt_present) {
     if (br.ue() != 0) throw UnsupportedStream("redundant H.264 pictures are not supported");
   }
-  const int st = sh.slice_type % 5;
-  if (st == h264::kB || st == h264::kSP || st == h264::kSI)
-    throw UnsupportedStream("H.264 B / SP / SI slices are not supported");
-  sh.num_ref_idx_l0 = pps.num_ref_idx_l0_default;
-  if (st == h264::kP) {
-    if (br.u1()) sh.num_ref_idx_l0 = int(br.ue()) + 1;
-    VEP_CHECK(sh.num_ref_idx_l0 <= 32, "num_ref_idx_l0 out of range");
-    if (br.u1()) {  // ref_pic_list_modification_flag_l0
-      for (;;) {
-        const int idc = int(br.ue());
-        if (idc == 3) break;
-        VEP_CHECK(idc <= 2, "bad modification_of_pic_nums_idc");
-        sh.ref_mods.push_back({idc, int(br.ue())});
-        VEP_CHECK(sh.ref_mods.size() <= 33, "too many reference list modifications");
+  const int st = sh.type();
+  if (st == h264::kSP || st == h264::kSI) throw UnsupportedStream("H.264 SP / SI slices are not supported");
+  if (st == h264::kB) sh.direct_spatial = br.u1();
+  sh.num_ref_idx[0] = pps.num_ref_idx_l0_default;
+  sh.num_ref_idx[1] = pps.num_ref_idx_l1_default;
+  if (st == h264::kP || st == h264::kB) {
+    if (br.u1()) {  // num_ref_idx_active_override_flag
+      sh.num_ref_idx[0] = int(br.ue()) + 1;
+      if (st == h264::kB) sh.num_ref_idx[1] = int(br.ue()) + 1;
+    }
+    VEP_CHECK(sh.num_ref_idx[0] <= 32 && sh.num_ref_idx[1] <= 32, "num_ref_idx out of range");
+    read_ref_mods(br, sh.ref_mods[0]);
+    if (st == h264::kB) read_ref_mods(br, sh.ref_mods[1]);
+  }
+  if (st == h264::kP) sh.num_ref_idx[1] = 0;
+  if (st == h264::kI) sh.num_ref_idx[0] = sh.num_ref_idx[1] = 0;
+  if ((pps.weighted_pred && st == h264::kP) || (pps.weighted_bipred_idc == 1 && st == h264::kB)) {
+    sh.explicit_wp = true;  // pred_weight_table()
+    sh.luma_lwd = int(br.ue());
+    sh.chroma_lwd = int(br.ue());
+    VEP_CHECK(sh.luma_lwd <= 7 && sh.chroma_lwd <= 7, "weight denominator out of range");
+    for (int l = 0; l < (st == h264::kB ? 2 : 1); ++l) {
+      sh.wt[l].resize(size_t(sh.num_ref_idx[l]));
+      for (auto& w : sh.wt[l]) {
+        w.w[0] = i16(1 << sh.luma_lwd);
+        w.w[1] = w.w[2] = i16(1 << sh.chroma_lwd);
+        w.o[0] = w.o[1] = w.o[2] = 0;
+        if (br.u1()) {
+          w.w[0] = i16(br.se());
+          w.o[0] = i16(br.se());
+          VEP_CHECK(w.w[0] >= -128 && w.w[0] <= 127 && w.o[0] >= -128 && w.o[0] <= 127, "luma weight out of range");
+        }
+        if (br.u1())
+          for (int c = 1; c < 3; ++c) {
+            w.w[c] = i16(br.se());
+            w.o[c] = i16(br.se());
+            VEP_CHECK(w.w[c] >= -128 && w.w[c] <= 127 && w.o[c] >= -128 && w.o[c] <= 127,
+                      "chroma weight out of range");
+          }
       }
     }
   }
@@ -323,6 +336,10 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
       }
     }
   }
+  if (pps.cabac && st != h264::kI) {
+    sh.cabac_init_idc = int(br.ue());
+    VEP_CHECK(sh.cabac_init_idc <= 2, "bad cabac_init_idc");
+  }
   sh.qp = pps.pic_init_qp + br.se();
   VEP_CHECK(sh.qp >= 0 && sh.qp <= 51, "slice QP out of range");
   if (pps.deblocking_filter_control) {
@@ -342,21 +359,80 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
 
 void Decoder::reset_references() {
   dpb_.clear();
+  pending_.clear();
   have_idr_ = false;
   max_lt_idx_ = -1;
+  pinned_slot_ = -1;
 }
 
 int Decoder::pick_slot() const {
   for (int s = 0; s < dpb_slots_; ++s) {
-    bool used = false;
+    bool used = s == pinned_slot_;
     for (const auto& r : dpb_) used |= r.slot == s;
+    for (const auto& p : pending_) used |= p.f.slot == s;
     if (!used) return s;
   }
   throw Error("vep: decoded picture buffer overflow");
 }
 
-void Decoder::build_ref_list(const SliceHdr& sh, const Sps& sps) {
+// §8.2.1: picture order count of the current picture (frame: min(top, bottom)).
+int Decoder::compute_poc(const SliceHdr& sh, const Sps& sps) {
   const int max_fn = 1 << sps.log2_max_frame_num;
+  if (sps.poc_type == 0) {
+    if (sh.idr()) prev_poc_msb_ = prev_poc_lsb_ = 0;
+    const int max_lsb = 1 << sps.log2_max_poc_lsb;
+    int msb = prev_poc_msb_;
+    if (sh.poc_lsb < prev_poc_lsb_ && prev_poc_lsb_ - sh.poc_lsb >= max_lsb / 2) msb = prev_poc_msb_ + max_lsb;
+    else if (sh.poc_lsb > prev_poc_lsb_ && sh.poc_lsb - prev_poc_lsb_ > max_lsb / 2) msb = prev_poc_msb_ - max_lsb;
+    const int top = msb + sh.poc_lsb, bot = top + sh.delta_poc_bottom;
+    if (sh.nal_ref_idc != 0) {
+      if (sh.has_mmco5()) {
+        prev_poc_msb_ = 0;
+        prev_poc_lsb_ = top - std::min(top, bot);
+      } else {
+        prev_poc_msb_ = msb;
+        prev_poc_lsb_ = sh.poc_lsb;
+      }
+    }
+    return std::min(top, bot);
+  }
+  // types 1 and 2: FrameNumOffset
+  int fno;
+  if (sh.idr()) fno = 0;
+  else if (prev_frame_num_ > sh.frame_num) fno = prev_frame_num_offset_ + max_fn;
+  else fno = prev_frame_num_offset_;
+  int poc;
+  if (sps.poc_type == 1) {
+    const int n = int(sps.offset_for_ref_frame.size());
+    int abs_fn = n != 0 ? fno + sh.frame_num : 0;
+    if (sh.nal_ref_idc == 0 && abs_fn > 0) --abs_fn;
+    int expected = 0;
+    if (abs_fn > 0) {
+      int per_cycle = 0;
+      for (int v : sps.offset_for_ref_frame) per_cycle += v;
+      const int cnt = (abs_fn - 1) / n, in_cycle = (abs_fn - 1) % n;
+      expected = cnt * per_cycle;
+      for (int i = 0; i <= in_cycle; ++i) expected += sps.offset_for_ref_frame[size_t(i)];
+    }
+    if (sh.nal_ref_idc == 0) expected += sps.offset_for_non_ref_pic;
+    const int top = expected + sh.delta_poc[0];
+    const int bot = top + sps.offset_for_top_to_bottom_field + sh.delta_poc[1];
+    poc = std::min(top, bot);
+  } else {
+    poc = sh.idr() ? 0 : (sh.nal_ref_idc == 0 ? 2 * (fno + sh.frame_num) - 1 : 2 * (fno + sh.frame_num));
+  }
+  const bool mmco5 = sh.has_mmco5();
+  prev_frame_num_offset_ = mmco5 ? 0 : fno;
+  prev_frame_num_ = mmco5 ? 0 : sh.frame_num;
+  return poc;
+}
+
+// §8.2.4.2 / §8.2.4.3: reference picture lists of the current slice.
+void Decoder::build_lists(const SliceHdr& sh, const Sps& sps, int cur_poc) {
+  const int max_fn = 1 << sps.log2_max_frame_num;
+  list_[0].clear();
+  list_[1].clear();
+  if (sh.type() == h264::kI) return;
   std::vector<RefPic*> st, lt;
   for (auto& r : dpb_) {
     if (r.long_term) {
@@ -366,56 +442,81 @@ void Decoder::build_ref_list(const SliceHdr& sh, const Sps& sps) {
       st.push_back(&r);
     }
   }
-  std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
   std::sort(lt.begin(), lt.end(), [](RefPic* a, RefPic* b) { return a->lt_idx < b->lt_idx; });
-  std::vector<RefPic*> list = st;
-  list.insert(list.end(), lt.begin(), lt.end());
-  int pred = sh.frame_num;
-  size_t idx = 0;
-  for (const auto& m : sh.ref_mods) {
-    RefPic* pick = nullptr;
-    if (m.idc < 2) {
-      const int d = m.val + 1;
-      int nw = m.idc == 0 ? pred - d : pred + d;
-      if (nw < 0) nw += max_fn;
-      if (nw >= max_fn) nw -= max_fn;
-      pred = nw;
-      const int pic_num = nw > sh.frame_num ? nw - max_fn : nw;
-      for (RefPic* r : st)
-        if (r->frame_num_wrap == pic_num) pick = r;
-    } else {
-      for (RefPic* r : lt)
-        if (r->lt_idx == m.val) pick = r;
-    }
-    if (!pick) throw Error("vep: reference list modification names a missing picture");
-    list.insert(list.begin() + long(std::min(idx, list.size())), pick);
-    for (size_t k = idx + 1; k < list.size(); ++k)
-      if (list[k] == pick) {
-        list.erase(list.begin() + long(k));
-        break;
-      }
-    ++idx;
+  std::vector<RefPic*> init[2];
+  if (sh.type() == h264::kP) {
+    std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
+    init[0] = st;
+    init[0].insert(init[0].end(), lt.begin(), lt.end());
+  } else {
+    std::vector<RefPic*> before, after;
+    for (RefPic* r : st) (r->poc < cur_poc ? before : after).push_back(r);
+    std::sort(before.begin(), before.end(), [](RefPic* a, RefPic* b) { return a->poc > b->poc; });
+    std::sort(after.begin(), after.end(), [](RefPic* a, RefPic* b) { return a->poc < b->poc; });
+    init[0] = before;
+    init[0].insert(init[0].end(), after.begin(), after.end());
+    init[0].insert(init[0].end(), lt.begin(), lt.end());
+    init[1] = after;
+    init[1].insert(init[1].end(), before.begin(), before.end());
+    init[1].insert(init[1].end(), lt.begin(), lt.end());
+    if (init[1].size() > 1 && init[1] == init[0]) std::swap(init[1][0], init[1][1]);
   }
-  list0_.assign(size_t(sh.num_ref_idx_l0), -1);
-  for (size_t i = 0; i < list0_.size() && i < list.size(); ++i) list0_[i] = list[i]->slot;
+  for (int l = 0; l < (sh.type() == h264::kB ? 2 : 1); ++l) {
+    std::vector<RefPic*> list = init[l];
+    int pred = sh.frame_num;
+    size_t idx = 0;
+    for (const auto& m : sh.ref_mods[l]) {
+      RefPic* pick = nullptr;
+      if (m.idc < 2) {
+        const int d = m.val + 1;
+        int nw = m.idc == 0 ? pred - d : pred + d;
+        if (nw < 0) nw += max_fn;
+        if (nw >= max_fn) nw -= max_fn;
+        pred = nw;
+        const int pic_num = nw > sh.frame_num ? nw - max_fn : nw;
+        for (RefPic* r : st)
+          if (r->frame_num_wrap == pic_num) pick = r;
+      } else {
+        for (RefPic* r : lt)
+          if (r->lt_idx == m.val) pick = r;
+      }
+      if (!pick) throw Error("vep: reference list modification names a missing picture");
+      list.insert(list.begin() + long(std::min(idx, list.size())), pick);
+      for (size_t k = idx + 1; k < list.size(); ++k)
+        if (list[k] == pick) {
+          list.erase(list.begin() + long(k));
+          break;
+        }
+      ++idx;
+    }
+    list_[l].assign(size_t(sh.num_ref_idx[l]), ListEntry{});
+    for (size_t i = 0; i < list_[l].size() && i < list.size(); ++i) {
+      const RefPic& r = *list[i];
+      list_[l][i] = ListEntry{r.slot, r.poc, r.long_term, r.uid, r.col.get()};
+    }
+  }
 }
 
-void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot) {
+void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int poc, u32 uid,
+                              std::shared_ptr<const ColMotion> col) {
   const int max_fn = 1 << sps.log2_max_frame_num;
   const int max_refs = std::max(1, sps.max_num_ref_frames);
+  RefPic cur;
+  cur.slot = slot;
+  cur.frame_num = sh.frame_num;
+  cur.poc = poc;
+  cur.uid = uid;
+  cur.col = std::move(col);
   if (sh.idr()) {
     dpb_.clear();
-    RefPic r;
-    r.slot = slot;
-    r.frame_num = sh.frame_num;
     if (sh.long_term_reference) {
-      r.long_term = true;
-      r.lt_idx = 0;
+      cur.long_term = true;
+      cur.lt_idx = 0;
       max_lt_idx_ = 0;
     } else {
       max_lt_idx_ = -1;
     }
-    dpb_.push_back(r);
+    dpb_.push_back(cur);
     return;
   }
   auto wrap = [&](const RefPic& r) { return r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num; };
@@ -471,12 +572,11 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot) {
       dpb_.erase(it);
     }
   }
-  RefPic r;
-  r.slot = slot;
-  r.frame_num = mmco5 ? 0 : sh.frame_num;
-  r.long_term = cur_long;
-  r.lt_idx = cur_lt;
-  dpb_.push_back(r);
+  cur.frame_num = mmco5 ? 0 : sh.frame_num;
+  if (mmco5) cur.poc = 0;
+  cur.long_term = cur_long;
+  cur.lt_idx = cur_lt;
+  dpb_.push_back(cur);
   while (int(dpb_.size()) > max_refs) {  // non-conforming stream: drop the oldest short-term
     auto it = std::min_element(dpb_.begin(), dpb_.end(), [&](const RefPic& a, const RefPic& b) {
       if (a.long_term != b.long_term) return !a.long_term;
@@ -486,7 +586,59 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot) {
   }
 }
 
-// ------------------------------------------------------------------------- macroblock layer
+int Decoder::reorder_depth(const Sps& sps) const {
+  if (sps.max_num_reorder_frames >= 0) return sps.max_num_reorder_frames;
+  if (sps.poc_type == 2 || sps.profile_idc == 66) return 0;  // output order = decoding order
+  return adaptive_reorder_;
+}
+
+// C.4.5.3-style bumping in POC order: an IDR / MMCO5 picture first outputs everything still
+// waiting (and itself: nothing after it can precede it); otherwise the smallest POC leaves once
+// more than reorder_depth() pictures wait. A picture whose POC is below the last output one
+// arrived too late for its turn: it is not output, and (without a VUI reorder depth) the
+// depth learnt from the stream grows.
+void Decoder::bump(Picture& pic, bool flush_all) {
+  auto take_min = [&] {
+    auto it = std::min_element(pending_.begin(), pending_.end(),
+                               [](const Pending& a, const Pending& b) { return a.f.poc < b.f.poc; });
+    pic.outputs.push_back(it->f);
+    last_out_poc_ = it->f.poc;
+    out_since_idr_ = true;
+    pending_.erase(it);
+  };
+  if (flush_all) {
+    while (!pending_.empty()) take_min();
+    out_since_idr_ = false;
+  }
+  OutFrame f;
+  f.slot = pic.target;
+  f.info = pic.info;
+  f.au = pic.au;
+  f.poc = pic.poc;
+  if (flush_all) {
+    pic.outputs.push_back(f);
+    last_out_poc_ = f.poc;
+    out_since_idr_ = true;
+  } else if (out_since_idr_ && f.poc < last_out_poc_) {
+    if (adaptive_reorder_ < 16) ++adaptive_reorder_;  // late: dropped from output
+  } else {
+    pending_.push_back({f, 0});
+    while (int(pending_.size()) > reorder_cur_) take_min();
+  }
+  if (!pic.outputs.empty()) pinned_slot_ = pic.outputs.back().slot;
+}
+
+std::vector<OutFrame> Decoder::flush_output() {
+  Picture tmp;
+  while (!pending_.empty()) {
+    auto it = std::min_element(pending_.begin(), pending_.end(),
+                               [](const Pending& a, const Pending& b) { return a.f.poc < b.f.poc; });
+    tmp.outputs.push_back(it->f);
+    pending_.erase(it);
+  }
+  if (!tmp.outputs.empty()) pinned_slot_ = tmp.outputs.back().slot;
+  return tmp.outputs;
+}
 
 void Decoder::absorb_parameter_sets(const AccessUnit& au) {
   std::vector<u8> scratch;
@@ -521,10 +673,10 @@ class MbDecoder {
     s.slice = u16(sc_.slice);
     nb_.begin(mb);
     s.qp = u8(sc_.qp);
-    for (int k = 0; k < 4; ++k) s.ref[k] = 0;
+    for (int k = 0; k < 4; ++k) s.ref[0][k] = 0;
     int mv[2];
     nb_.pskip_mv(mb, mv);
-    for (auto& v : s.mv) {
+    for (auto& v : s.mv[0]) {
       v[0] = i16(mv[0]);
       v[1] = i16(mv[1]);
     }
@@ -607,19 +759,19 @@ class MbDecoder {
 
  private:
   int read_ref(Bits& br) {
-    const int n = sc_.sh.num_ref_idx_l0;
+    const int n = sc_.sh.num_ref_idx[0];
     int r = 0;
     if (n == 2) r = int(br.u1() ^ 1u);
     else if (n > 2) r = int(br.ue());
-    VEP_CHECK(r < n && sc_.list0[size_t(r)] >= 0, "ref_idx_l0 names a missing reference picture");
+    VEP_CHECK(r < n && sc_.list0[size_t(r)].slot >= 0, "ref_idx_l0 names a missing reference picture");
     return r;
   }
 
   void set_part(MbState& s, int x4, int y4, int w4, int h4, const int mv[2]) {
     for (int y = y4; y < y4 + h4; ++y)
       for (int x = x4; x < x4 + w4; ++x) {
-        s.mv[y * 4 + x][0] = i16(mv[0]);
-        s.mv[y * 4 + x][1] = i16(mv[1]);
+        s.mv[0][y * 4 + x][0] = i16(mv[0]);
+        s.mv[0][y * 4 + x][1] = i16(mv[1]);
       }
   }
   static u16 part_mask(int x4, int y4, int w4, int h4) {
@@ -652,7 +804,7 @@ class MbDecoder {
       for (int i = 0; i < n; ++i) {
         const Part& p = parts[i];
         for (int y = p.y4 / 2; y < (p.y4 + p.h4) / 2; ++y)
-          for (int x = p.x4 / 2; x < (p.x4 + p.w4) / 2; ++x) s.ref[y * 2 + x] = i8(p.ref);
+          for (int x = p.x4 / 2; x < (p.x4 + p.w4) / 2; ++x) s.ref[0][y * 2 + x] = i8(p.ref);
       }
     } else {
       int sub[4], refs[4];
@@ -662,7 +814,7 @@ class MbDecoder {
       }
       for (int i = 0; i < 4; ++i) refs[i] = mbt == 4 ? 0 : read_ref(br);
       for (int i = 0; i < 4; ++i) {
-        s.ref[i] = i8(refs[i]);
+        s.ref[0][i] = i8(refs[i]);
         const int x8 = (i & 1) * 2, y8 = (i >> 1) * 2;
         const int cnt = sub[i] == 0 ? 1 : sub[i] == 3 ? 4 : 2;
         for (int j = 0; j < cnt; ++j) {
@@ -684,7 +836,7 @@ class MbDecoder {
     for (int i = 0; i < np; ++i) {
       const Part& p = parts[i];
       int mvp[2];
-      nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, p.ref, done, p.shape, mvp);
+      nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, 0, p.ref, done, p.shape, mvp);
       int mv[2] = {mvp[0] + p.mvd[0], mvp[1] + p.mvd[1]};
       VEP_CHECK(mv[0] >= -32768 && mv[0] <= 32767 && mv[1] >= -32768 && mv[1] <= 32767,
                 "motion vector out of range");
@@ -773,7 +925,7 @@ class MbDecoder {
           read_residual_block_cb(br, ncl(0), 16, [&](int k, int l) { c[kZigzag4x4[k]] = l; }) > 0;
       int dcy[16] = {};
       if (have_dc) {
-        h16(c);
+        hadamard4x4(c);
         const int ls = 16 * kNormAdjust[qp % 6][0];
         for (int k = 0; k < 16; ++k)
           dcy[k] = qp >= 36 ? c[k] * ls * (1 << (qp / 6 - 6)) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
@@ -835,16 +987,20 @@ class MbDecoder {
     m.kind = s.kind;
     m.qp = s.kind == kIPcm ? 0 : s.qp;
     m.qpc = u8(chroma_qp(m.qp, sc_.pps.chroma_qp_index_offset));
+    m.qpc2 = m.qpc;  // (the fast path runs only when both chroma offsets are equal)
     m.i16_mode = u8(i16_mode);
     m.chroma_mode = u8(chroma_mode);
     m.dbk = u8((sc_.sh.disable_deblocking == 1 ? 1 : 0) | (sc_.sh.disable_deblocking == 2 ? 2 : 0));
     m.alpha_off = i8(sc_.sh.alpha_off);
     m.beta_off = i8(sc_.sh.beta_off);
     m.slice = s.slice;
-    for (int k = 0; k < 4; ++k)
-      m.ref[k] = s.ref[k] >= 0 ? u8(sc_.list0[size_t(s.ref[k])]) : u8(0xFF);
+    for (int k = 0; k < 4; ++k) {
+      m.ref[k] = s.ref[0][k] >= 0 ? u8(sc_.list0[size_t(s.ref[0][k])].slot) : u8(0xFF);
+      m.ref1[k] = u8(0xFF);
+    }
     for (int r = 0; r < 16; ++r) m.i4[r >> 1] |= u8((s.kind == kI4x4 ? s.i4[r] : 0) << ((r & 1) * 4));
-    store_mb(pic_, mb, m, s, &res, pcm_);
+    for (int r = 0; r < 16; ++r) m.nz |= u16(s.tc[r] ? 1u << r : 0u);
+    store_mb(pic_, mb, m, s, &res, pcm_, nullptr);
   }
 
   MbNeighbours& nb_;
@@ -855,13 +1011,37 @@ class MbDecoder {
 
 }  // namespace
 
-PicturePtr Decoder::parse(const AccessUnit& au) {
+namespace {
+
+// The fast CAVLC MbDecoder above covers a slice when nothing beyond Baseline-style syntax is in
+// use (the default synthetic camera streams); everything else goes to decode_slice_generic.
+bool legacy_slice(const SliceHdr& sh, const Sps& sps, const Pps& pps) {
+  return !pps.cabac && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
+         !sps.scaling_matrix_present && !pps.scaling_matrix_present && !sh.explicit_wp &&
+         pps.chroma_qp_index_offset == pps.second_chroma_qp_index_offset;
+}
+
+// Surfaces a stream needs: references + pictures waiting for output + the picture being decoded
+// + the newest output (kept until a newer one replaces it).
+int dpb_slots_for(const Sps& sps) {
+  int bound;
+  if (sps.max_num_reorder_frames >= 0) bound = sps.max_num_reorder_frames;
+  else if (sps.poc_type == 2 || sps.profile_idc == 66) bound = 0;
+  else bound = sps.max_dpb_frames();
+  return std::min(kMaxDpbSlots, std::max(1, sps.max_num_ref_frames) + bound + 2);
+}
+
+}  // namespace
+
+PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   auto pic = std::make_shared<Picture>();
   bool got = false;
   int slice_idx = 0;
   SliceHdr first;
   const Sps* act_sps = nullptr;
+  const Pps* act_pps = nullptr;
   std::vector<u8> scratch;
+  std::vector<std::array<std::vector<u32>, 2>> slice_uids;  // list uids per slice (colocated motion)
   for (size_t i = 0; i < au.nals.size(); ++i) {
     const u8* p = au.nal(i);
     const size_t n = au.nal_size(i);
@@ -872,11 +1052,10 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
       const u8* r = unescape(p, n, epb_, scratch, rn);
       if (t == h264::kNalSps) {
         Sps s = h264::parse_sps(r, rn);
-        check_sps_supported(r, rn, s);
+        check_sps_supported(s);
         sps_[s.sps_id] = s;
       } else {
         Pps q = h264::parse_pps(r, rn);
-        check_pps_supported(r, rn, q);
         pps_[q.pps_id] = q;
       }
       continue;
@@ -897,22 +1076,35 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
     if (sit == sps_.end()) throw UnsupportedStream("slice references unknown SPS");
     const Sps& sps = sit->second;
     const Pps& pps = pit->second;
+    check_sps_supported(sps);
     Bits br(r + 1, rn - 1);
     const SliceHdr sh = read_slice_header(br, p[0], sps, pps);
     if (!got) {
       first = sh;
       act_sps = &sps;
-      const int slots = std::max(1, sps.max_num_ref_frames) + 1;
+      act_pps = &pps;
+      const int slots = dpb_slots_for(sps);
       VEP_CHECK(slots <= kMaxDpbSlots, "max_num_ref_frames out of range");
+      const int W = sps.width_mbs, H = sps.height_mbs();
       if (sh.idr()) {
-        dpb_.clear();
         have_idr_ = true;
         dpb_slots_ = slots;
+        wmbs_ = W;
+        hmbs_ = H;
+        reorder_cur_ = reorder_depth(sps);
       } else {
         if (!have_idr_) throw Error("vep: H.264 stream does not start with an IDR picture");
-        VEP_CHECK(slots == dpb_slots_, "SPS changed without an IDR picture");
+        // a non-IDR picture may not change the picture size or the DPB (a mid-GOP SPS that
+        // does would make earlier pictures of a batch write outside the surfaces)
+        VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_, "SPS changed without an IDR picture");
       }
-      const int W = sps.width_mbs, H = sps.height_mbs();
+      if (sh.idr()) {
+        // IDR: the previous pictures leave the reorder buffer first (no_output_of_prior_pics
+        // is not honoured: a viewer wants the newest frame), then the DPB is emptied
+        dpb_.clear();
+        max_lt_idx_ = -1;
+      }
+      pic->poc = compute_poc(sh, sps);
       pic->wmbs = W;
       pic->hmbs = H;
       pic->mbs.assign(size_t(W) * H, MbRec{});
@@ -928,48 +1120,71 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
       pi.height = sps.height();
       pi.crop_left = sps.crop_left;
       pi.crop_top = sps.crop_top;
-      pi.pict_type = "PBISi"[sh.slice_type % 5];
+      pi.pict_type = "PBISi"[sh.type()];
       pi.idr = sh.idr();
       pi.frame_num = sh.frame_num;
       pi.fps = sps.fps();
+      pic->au.pts = au.pts;
+      pic->au.dts = au.dts;
+      pic->au.arrival_ms = au.arrival_ms;
+      pic->au.keyframe = au.keyframe;
+      pic->au.corrupt = au.corrupt;
+      pic->au.tag = tag;
       nb_.reset(W, H);
-      pic->target = pick_slot();
+      pic->target = pick_slot();  // (pictures waiting for output keep their slots until bump)
       got = true;
     } else {
       VEP_CHECK(&sps == act_sps, "slices of one picture reference different SPSs");
+      if (sh.type() == h264::kB || pic->info.pict_type == 'I') pic->info.pict_type = "PBISi"[sh.type()];
     }
-    if (sh.slice_type % 5 == h264::kP) build_ref_list(sh, sps);
-    else list0_.clear();
-    // skip the slice header bits already consumed: decode from the current position
-    const size_t stop = BitReader(r + 1, rn - 1).stop_bit_pos();
-    SliceCtx sc{sh, pps, slice_idx, sh.slice_type % 5 == h264::kP, sh.qp, list0_};
-    const int total = pic->nmbs();
-    int mb = sh.first_mb;
-    VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
-    bool more = true;
-    while (more) {
-      if (sc.is_p) {
-        const u32 run = br.ue();
-        VEP_CHECK(u32(total - mb) >= run, "mb_skip_run past end of picture");
-        MbDecoder d(nb_, *pic, sc);
-        for (u32 k = 0; k < run; ++k) d.skip(mb++);
-        if (run > 0) {
-          more = br.pos() < stop;
-          if (!more) break;
+    build_lists(sh, sps, pic->poc);
+    std::array<std::vector<u32>, 2> uids;
+    for (int l = 0; l < 2; ++l)
+      for (const auto& e : list_[l]) uids[size_t(l)].push_back(e.uid);
+    slice_uids.push_back(std::move(uids));
+    if (legacy_slice(sh, sps, pps)) {
+      const size_t stop = BitReader(r + 1, rn - 1).stop_bit_pos();
+      SliceCtx sc{sh, pps, slice_idx, sh.type() == h264::kP, sh.qp, list_[0]};
+      const int total = pic->nmbs();
+      int mb = sh.first_mb;
+      VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
+      bool more = true;
+      while (more) {
+        if (sc.is_p) {
+          const u32 run = br.ue();
+          VEP_CHECK(u32(total - mb) >= run, "mb_skip_run past end of picture");
+          MbDecoder d(nb_, *pic, sc);
+          for (u32 k = 0; k < run; ++k) d.skip(mb++);
+          if (run > 0) {
+            more = br.pos() < stop;
+            if (!more) break;
+          }
         }
+        VEP_CHECK(mb < total, "macroblock address past end of picture");
+        MbDecoder d(nb_, *pic, sc);
+        d.macroblock(br, mb);
+        if (d.qp_out_ >= 0) sc.qp = d.qp_out_;
+        VEP_CHECK(!br.overrun(), "slice data overrun");
+        more = br.pos() < stop;
+        ++mb;
       }
-      VEP_CHECK(mb < total, "macroblock address past end of picture");
-      MbDecoder d(nb_, *pic, sc);
-      d.macroblock(br, mb);
-      if (d.qp_out_ >= 0) sc.qp = d.qp_out_;
-      VEP_CHECK(!br.overrun(), "slice data overrun");
-      more = br.pos() < stop;
-      ++mb;
+    } else {
+      SliceEnv env;
+      env.sh = &sh;
+      env.sps = &sps;
+      env.pps = &pps;
+      env.slice = slice_idx;
+      env.list[0] = &list_[0];
+      env.list[1] = &list_[1];
+      env.cur_poc = pic->poc;
+      env.scaling = h264::resolve_scaling(sps, pps);
+      decode_slice_generic(nb_, *pic, env, r + 1, rn - 1, br.pos());
     }
     ++slice_idx;
     VEP_CHECK(slice_idx < 65535, "too many slices");
   }
   VEP_CHECK(got, "access unit has no slice");
+  (void)act_pps;
   // conceal macroblocks no slice covered (lost slices): copy from the first reference, or grey
   int missing = 0;
   for (int mb = 0; mb < pic->nmbs(); ++mb) {
@@ -980,6 +1195,7 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
     m.res = kNoRes;
     m.dbk = 1;
     m.slice = u16(0xFFFF);
+    std::fill(std::begin(m.ref1), std::end(m.ref1), u8(0xFF));
     if (!dpb_.empty()) {
       m.kind = kSkip;
       for (auto& rf : m.ref) rf = u8(dpb_.front().slot);
@@ -994,7 +1210,37 @@ PicturePtr Decoder::parse(const AccessUnit& au) {
     }
   }
   pic->info.coded_mbs = pic->nmbs() - missing;
-  if (first.nal_ref_idc != 0) mark_references(first, *act_sps, pic->target);
+  const u32 uid = next_uid_++;
+  if (first.nal_ref_idc != 0) {
+    std::shared_ptr<ColMotion> col;
+    if (act_sps->profile_idc != 66) {  // B slices possible: keep the motion for direct prediction
+      col = std::make_shared<ColMotion>();
+      col->wmbs = pic->wmbs;
+      col->hmbs = pic->hmbs;
+      const size_t nb = size_t(pic->nmbs()) * 16;
+      col->mv.assign(nb * 2, 0);
+      col->ref.assign(nb, i8(-1));
+      col->pid.assign(nb, 0u);
+      for (int mb = 0; mb < pic->nmbs(); ++mb) {
+        const MbState& st = nb_.at(mb);
+        if (st.kind == 0xFF || is_intra(st.kind)) continue;
+        const auto& lu = slice_uids[std::min<size_t>(st.slice, slice_uids.size() - 1)];
+        for (int blk = 0; blk < 16; ++blk) {
+          const int b8 = ((blk >> 3) << 1) | ((blk & 3) >> 1);
+          const int l = st.ref[0][b8] >= 0 ? 0 : 1;
+          const int ri = st.ref[l][b8];
+          if (ri < 0) continue;
+          const size_t k = size_t(mb) * 16 + size_t(blk);
+          col->mv[k * 2] = st.mv[l][blk][0];
+          col->mv[k * 2 + 1] = st.mv[l][blk][1];
+          col->ref[k] = i8(ri);
+          col->pid[k] = size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u;
+        }
+      }
+    }
+    mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col));
+  }
+  bump(*pic, first.idr() || first.has_mmco5());
   validate(*pic);
   return pic;
 }
@@ -1005,8 +1251,8 @@ void validate(const Picture& p) {
   VEP_CHECK(p.wmbs > 0 && p.hmbs > 0 && p.mbs.size() == size_t(p.nmbs()), "picture size mismatch");
   const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size() / 32;
   for (const MbRec& m : p.mbs) {
-    VEP_CHECK(m.kind <= kIPcm, "macroblock kind out of range");
-    VEP_CHECK(m.qp <= 51 && m.qpc <= 51, "macroblock QP out of range");
+    VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
+    VEP_CHECK(m.qp <= 51 && m.qpc <= 51 && m.qpc2 <= 51, "macroblock QP out of range");
     if (m.kind == kIPcm) {
       VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 32 <= nblocks, "I_PCM samples outside the pool");
       continue;
@@ -1014,11 +1260,27 @@ void validate(const Picture& p) {
     const size_t nb = size_t(__builtin_popcount(m.luma_coded)) + size_t(__builtin_popcount(m.chroma_coded));
     VEP_CHECK(size_t(m.coef) + nb <= nblocks, "coefficient blocks outside the pool");
     VEP_CHECK(m.chroma_mode <= 3 && m.i16_mode <= 3, "intra prediction mode out of range");
+    if (m.flags & kMbT8x8)
+      for (int q = 0; q < 4; ++q) {
+        const u32 g = (u32(m.luma_coded) >> ((q & 1) * 2 + (q >> 1) * 8)) & 0x33u;
+        VEP_CHECK(g == 0 || g == 0x33u, "8x8 residual block partially coded");
+      }
     if (m.kind == kSkip || m.kind == kInter) {
-      VEP_CHECK(size_t(m.mv) + 1 <= nmv, "motion vectors outside the pool");
-      for (u8 r : m.ref) VEP_CHECK(int(r) < p.dpb_slots, "reference slot outside the DPB");
+      VEP_CHECK(size_t(m.mv) + ((m.flags & kMbL1) ? 2 : 1) <= nmv, "motion vectors outside the pool");
+      for (int k = 0; k < 4; ++k) {
+        const int r0 = m.ref[k], r1 = m.ref1[k];
+        VEP_CHECK(r0 != 0xFF || r1 != 0xFF, "inter partition without a reference");
+        VEP_CHECK((r0 == 0xFF || r0 < p.dpb_slots) && (r1 == 0xFF || r1 < p.dpb_slots),
+                  "reference slot outside the DPB");
+        VEP_CHECK(r1 == 0xFF || (m.flags & kMbL1), "list-1 reference without list-1 motion");
+      }
+      if (m.flags & kMbWp) VEP_CHECK(size_t(m.wp) + 4 <= p.wps.size(), "weights outside the pool");
     } else if (m.kind == kI4x4) {
       for (u8 b : m.i4) VEP_CHECK((b & 15) <= 8 && (b >> 4) <= 8, "Intra_4x4 mode out of range");
+    } else if (m.kind == kI8x8) {
+      VEP_CHECK((m.flags & kMbT8x8) && (m.i4[0] & 15) <= 8 && (m.i4[0] >> 4) <= 8 && (m.i4[1] & 15) <= 8 &&
+                    (m.i4[1] >> 4) <= 8,
+                "Intra_8x8 mode out of range");
     }
     VEP_CHECK(m.res == kNoRes || (is_intra(m.kind) && m.res < u32(p.intra_res)), "residual slot out of range");
   }
@@ -1036,7 +1298,7 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
   if (have_dc) {
     int c[16] = {};
     for (int k = 0; k < 16; ++k) c[kZigzag4x4[k]] = lv.dc[k];
-    h16(c);
+    hadamard4x4(c);
     const int ls = 16 * kNormAdjust[qp % 6][0];
     for (int k = 0; k < 16; ++k)
       dcy[k] = qp >= 36 ? c[k] * ls * (1 << (qp / 6 - 6)) : (c[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
@@ -1100,9 +1362,8 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
   }
 }
 
-void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm) {
-  m.nz = 0;
-  for (int r = 0; r < 16; ++r) m.nz |= u16(s.tc[r] ? 1u << r : 0u);
+void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm,
+              const WpEntry* wp) {
   m.coef = u32(pic.coefs.size() / 16);
   m.luma_coded = 0;
   m.chroma_coded = 0;
@@ -1115,9 +1376,15 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
     m.luma_coded = res->luma;
     m.chroma_coded = res->chroma;
     // appended without a zero-filling resize (the pool is reserved per picture)
-    for (u32 w = res->luma; w; w &= w - 1) {
-      const i16* b = res->blk[__builtin_ctz(w)];
-      pic.coefs.insert(pic.coefs.end(), b, b + 16);
+    if (res->t8) {
+      m.flags |= kMbT8x8;
+      for (int q = 0; q < 4; ++q)
+        if ((res->luma >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) pic.coefs.insert(pic.coefs.end(), res->b8[q], res->b8[q] + 64);
+    } else {
+      for (u32 w = res->luma; w; w &= w - 1) {
+        const i16* b = res->blk[__builtin_ctz(w)];
+        pic.coefs.insert(pic.coefs.end(), b, b + 16);
+      }
     }
     for (u32 w = res->chroma; w; w &= w - 1) {
       const i16* b = res->blk[16 + __builtin_ctz(w)];
@@ -1125,16 +1392,24 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
     }
   }
   m.mv = 0;
+  m.wp = 0;
   if (m.kind == kSkip || m.kind == kInter) {
     m.mv = u32(pic.mvs.size() / 32);
-    pic.mvs.insert(pic.mvs.end(), &s.mv[0][0], &s.mv[0][0] + 32);
+    pic.mvs.insert(pic.mvs.end(), &s.mv[0][0][0], &s.mv[0][0][0] + 32);
+    if (m.flags & kMbL1) pic.mvs.insert(pic.mvs.end(), &s.mv[1][0][0], &s.mv[1][0][0] + 32);
+    if (wp && (m.flags & kMbWp)) {
+      m.wp = u32(pic.wps.size());
+      pic.wps.insert(pic.wps.end(), wp, wp + 4);
+    } else {
+      m.flags &= u8(~kMbWp);
+    }
     ++pic.inter_mbs;
   } else if (m.kind == kIPcm) {
     ++pic.inter_mbs;  // no neighbour dependency: reconstructed in the parallel pass
   } else {
     ++pic.intra_mbs;
   }
-  m.res = is_intra(m.kind) && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
+  m.res = is_intra(m.kind) && m.kind != kIPcm && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
   if (!(m.dbk & 1)) pic.deblock = true;
   pic.mbs[size_t(mb)] = m;
 }
@@ -1163,6 +1438,29 @@ const i16* chroma_res(const Picture& pic, const MbRec& m, int c, int b) {
                    u32(__builtin_popcount(m.chroma_coded & ((1u << k) - 1))));
 }
 
+// Luma residual samples of the whole MB (raster 16x16), from 4x4 or 8x8 transform blocks.
+void luma_residual(const Picture& pic, const MbRec& m, int* out) {
+  std::memset(out, 0, 256 * sizeof(int));
+  if (m.flags & kMbT8x8) {
+    for (int q = 0; q < 4; ++q) {
+      if (!((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1)) continue;
+      int r[64];
+      idct8x8(pic.block(luma8_block_index(m, q)), r);
+      for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) out[((q >> 1) * 8 + i) * 16 + (q & 1) * 8 + j] = r[i * 8 + j];
+    }
+    return;
+  }
+  for (int blk = 0; blk < 16; ++blk) {
+    const i16* d = luma_res(pic, m, blk);
+    if (!d) continue;
+    int r[16];
+    idct4x4(d, r);
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 4; ++j) out[((blk >> 2) * 4 + i) * 16 + (blk & 3) * 4 + j] = r[i * 4 + j];
+  }
+}
+
 struct Recon {
   const Picture& pic;
   std::vector<HostSurface>& slots;
@@ -1171,14 +1469,6 @@ struct Recon {
 
   u8& Y(int x, int y) { return T.y[size_t(y) * pitch + x]; }
   u8& C(int x, int y, int c) { return T.uv[size_t(y) * pitch + 2 * x + c]; }
-
-  void add_luma_block(const MbRec& m, int r, int x0, int y0, const int* pred) {
-    const i16* d = luma_res(pic, m, r);
-    int res[16] = {};
-    if (d) idct4x4(d, res);
-    for (int i = 0; i < 4; ++i)
-      for (int j = 0; j < 4; ++j) Y(x0 + j, y0 + i) = u8(clip1(pred[i * 4 + j] + res[i * 4 + j]));
-  }
 
   void chroma_store(const MbRec& m, int mx, int my, int c, const int* pred /*8x8*/) {
     for (int b = 0; b < 4; ++b) {
@@ -1193,27 +1483,39 @@ struct Recon {
   }
 
   void inter(const MbRec& m, int mx, int my) {
-    const i16* mv = &pic.mvs[size_t(m.mv) * 32];
-    int pred[16];
-    for (int r = 0; r < 16; ++r) {
-      const int bx = r & 3, by = r >> 2;
-      const HostSurface& R = slots[m.ref[((by >> 1) << 1) | (bx >> 1)]];
-      const int mvx = mv[2 * r], mvy = mv[2 * r + 1];
-      for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j)
-          pred[i * 4 + j] = luma_qpel(R.y.data(), pitch, wpx, hpx, mx * 16 + bx * 4 + j + (mvx >> 2),
-                                      my * 16 + by * 4 + i + (mvy >> 2), mvx & 3, mvy & 3);
-      add_luma_block(m, r, mx * 16 + bx * 4, my * 16 + by * 4, pred);
-    }
+    const i16* mv0 = &pic.mvs[size_t(m.mv) * 32];
+    const i16* mv1 = (m.flags & kMbL1) ? mv0 + 32 : nullptr;
+    const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
+    int res[256];
+    luma_residual(pic, m, res);
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) {
+        const int r = (y >> 2) * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
+        const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+        int p0 = 0, p1 = 0;
+        if (s0 != 0xFF)
+          p0 = luma_qpel(slots[size_t(s0)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * r] >> 2),
+                         my * 16 + y + (mv0[2 * r + 1] >> 2), mv0[2 * r] & 3, mv0[2 * r + 1] & 3);
+        if (s1 != 0xFF)
+          p1 = luma_qpel(slots[size_t(s1)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * r] >> 2),
+                         my * 16 + y + (mv1[2 * r + 1] >> 2), mv1[2 * r] & 3, mv1[2 * r + 1] & 3);
+        const int pr = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 0);
+        Y(mx * 16 + x, my * 16 + y) = u8(clip1(pr + res[y * 16 + x]));
+      }
     for (int c = 0; c < 2; ++c) {
       int cp[64];
       for (int y = 0; y < 8; ++y)
         for (int x = 0; x < 8; ++x) {
-          const int r = (y >> 1) * 4 + (x >> 1);
-          const HostSurface& R = slots[m.ref[((r >> 3) << 1) | ((r & 3) >> 1)]];
-          const int mvx = mv[2 * r], mvy = mv[2 * r + 1];
-          cp[y * 8 + x] = chroma_epel(R.uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mvx >> 3),
-                                      my * 8 + y + (mvy >> 3), mvx & 7, mvy & 7);
+          const int r = (y >> 1) * 4 + (x >> 1), b8 = ((y >> 2) << 1) | (x >> 2);
+          const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+          int p0 = 0, p1 = 0;
+          if (s0 != 0xFF)
+            p0 = chroma_epel(slots[size_t(s0)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
+                             my * 8 + y + (mv0[2 * r + 1] >> 3), mv0[2 * r] & 7, mv0[2 * r + 1] & 7);
+          if (s1 != 0xFF)
+            p1 = chroma_epel(slots[size_t(s1)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
+                             my * 8 + y + (mv1[2 * r + 1] >> 3), mv1[2 * r] & 7, mv1[2 * r + 1] & 7);
+          cp[y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c);
         }
       chroma_store(m, mx, my, c, cp);
     }
@@ -1244,13 +1546,11 @@ struct Recon {
     Intra16Nb n;
     intra16_neighbours(pic, mb, T, n);
     const PredConst k = intra16x16_const(n, m.i16_mode);
-    int pred[16];
-    for (int r = 0; r < 16; ++r) {
-      const int bx = r & 3, by = r >> 2;
-      for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) pred[i * 4 + j] = intra16x16_pred(n, k, m.i16_mode, bx * 4 + j, by * 4 + i);
-      add_luma_block(m, r, mx * 16 + bx * 4, my * 16 + by * 4, pred);
-    }
+    int res[256];
+    luma_residual(pic, m, res);
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x)
+        Y(mx * 16 + x, my * 16 + y) = u8(clip1(intra16x16_pred(n, k, m.i16_mode, x, y) + res[y * 16 + x]));
   }
 
   void intra4(const MbRec& m, int mb, int mx, int my) {
@@ -1259,15 +1559,57 @@ struct Recon {
       Intra4Nb n;
       intra4x4_neighbours(pic, mb, idx, T, n);
       const int mode = i4_mode(m, r);
-      int pred[16];
+      const i16* d = luma_res(pic, m, r);
+      int res[16] = {};
+      if (d) idct4x4(d, res);
       for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j) pred[i * 4 + j] = intra4x4_pred(n, mode, j, i);
-      add_luma_block(m, r, mx * 16 + bx * 4, my * 16 + by * 4, pred);
+        for (int j = 0; j < 4; ++j)
+          Y(mx * 16 + bx * 4 + j, my * 16 + by * 4 + i) = u8(clip1(intra4x4_pred(n, mode, j, i) + res[i * 4 + j]));
+    }
+  }
+
+  void intra8(const MbRec& m, int mb, int mx, int my) {
+    for (int q = 0; q < 4; ++q) {
+      int f[25];
+      bool top, left;
+      intra8x8_neighbours(pic, mb, q, T, f, top, left);
+      const int mode = i4_mode(m, q);
+      int res[64] = {};
+      if ((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) idct8x8(pic.block(luma8_block_index(m, q)), res);
+      const int x0 = mx * 16 + (q & 1) * 8, y0 = my * 16 + (q >> 1) * 8;
+      for (int i = 0; i < 8; ++i)
+        for (int j = 0; j < 8; ++j) Y(x0 + j, y0 + i) = u8(clip1(intra8x8_pred(f, top, left, mode, j, i) + res[i * 8 + j]));
     }
   }
 };
 
 }  // namespace
+
+// Filtered Intra_8x8 reference samples of 8x8 block q (§8.3.2.2, §8.3.2.2.1) from the surface
+// being reconstructed.
+void intra8x8_neighbours(const Picture& pic, int mb, int q, const HostSurface& T, int* f, bool& has_top,
+                         bool& has_left) {
+  const MbRec& m = pic.mbs[size_t(mb)];
+  const int mx = mb % pic.wmbs, my = mb / pic.wmbs, pitch = T.coded_w;
+  const bool A = intra_avail(pic, m, mx - 1, my), B = intra_avail(pic, m, mx, my - 1),
+             Cm = intra_avail(pic, m, mx + 1, my - 1), D = intra_avail(pic, m, mx - 1, my - 1);
+  const int bx = q & 1, by = q >> 1;
+  const int x0 = mx * 16 + bx * 8, y0 = my * 16 + by * 8;
+  has_top = by > 0 || B;
+  has_left = bx > 0 || A;
+  const bool has_tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+  const bool has_tr = by == 0 ? (bx == 0 ? B : Cm) : (bx == 0);  // block 2's top-right is block 1
+  auto P = [&](int x, int y) { return int(T.y[size_t(y) * pitch + x]); };
+  int t[17], l[8];  // t[0] = p[-1,-1], t[1 + x] = p[x,-1]
+  t[0] = has_tl ? P(x0 - 1, y0 - 1) : 128;
+  for (int k = 0; k < 8; ++k) {
+    t[1 + k] = has_top ? P(x0 + k, y0 - 1) : 128;
+    l[k] = has_left ? P(x0 - 1, y0 + k) : 128;
+  }
+  for (int k = 8; k < 16; ++k) t[1 + k] = has_tr ? P(x0 + k, y0 - 1) : t[8];
+  for (int k = 0; k < 25; ++k) f[k] = 128;
+  intra8x8_filter([&](int x) { return t[1 + x]; }, [&](int y) { return l[y]; }, has_top, has_left, has_tl, f);
+}
 
 void intra4x4_neighbours(const Picture& pic, int mb, int idx, const HostSurface& T, Intra4Nb& n) {
   const MbRec& m = pic.mbs[size_t(mb)];
@@ -1326,14 +1668,20 @@ void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& sl
   switch (m.kind) {
     case kSkip:
     case kInter:
-      for (u8 s : m.ref)
-        VEP_CHECK(s < slots.size() && slots[s].coded_w == wpx && slots[s].coded_h == hpx,
+      for (int k = 0; k < 8; ++k) {
+        const u8 s = k < 4 ? m.ref[k] : ((m.flags & kMbL1) ? m.ref1[k - 4] : u8(0xFF));
+        VEP_CHECK(s == 0xFF || (s < slots.size() && slots[s].coded_w == wpx && slots[s].coded_h == hpx),
                   "missing reference surface");
+      }
       r.inter(m, mx, my);
       break;
     case kIPcm: r.pcm(m, mx, my); break;
     case kI16x16:
       r.intra16(m, mb, mx, my);
+      r.intra_chroma(m, mb, mx, my);
+      break;
+    case kI8x8:
+      r.intra8(m, mb, mx, my);
       r.intra_chroma(m, mb, mx, my);
       break;
     default:
@@ -1344,7 +1692,7 @@ void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& sl
 }
 
 void cpu_deblock(const Picture& pic, HostSurface& T) {
-  static const i16 kZeroMv[32] = {};
+  static const i16 kZeroMv[64] = {};
   const int W = pic.wmbs, pitch = T.coded_w;
   u8* Yp = T.y.data();
   u8* UV = T.uv.data();
@@ -1361,13 +1709,15 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
         if (e == 0 && !(dir == 0 ? left : top)) continue;
         const MbRec& p = e > 0 ? q : pic.mbs[size_t(dir == 0 ? mb - 1 : mb - W)];
         const i16* mp = mvs(p);
+        if ((e & 1) && (q.flags & kMbT8x8)) continue;  // no 4x4 edges inside 8x8 transform blocks
         const EdgeParams ep = edge_params(p.qp, q.qp, q.alpha_off, q.beta_off);
-        const EdgeParams epc = edge_params(p.qpc, q.qpc, q.alpha_off, q.beta_off);
+        const EdgeParams epcs[2] = {edge_params(p.qpc, q.qpc, q.alpha_off, q.beta_off),
+                                    edge_params(p.qpc2, q.qpc2, q.alpha_off, q.beta_off)};
         int bs[16];
         for (int k = 0; k < 16; ++k) {
           const int bq = dir == 0 ? (k >> 2) * 4 + e : e * 4 + (k >> 2);
           const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
-          bs[k] = boundary_strength(p, bp, mp + 2 * bp, q, bq, mq + 2 * bq, e == 0);
+          bs[k] = boundary_strength(p, bp, mp, q, bq, mq, e == 0);
         }
         for (int k = 0; k < 16; ++k) {
           if (!bs[k]) continue;
@@ -1377,6 +1727,7 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
         if (e & 1) continue;  // chroma edges at chroma sample 0 and 4 (luma edges 0 and 2)
         for (int c = 0; c < 2; ++c)
           for (int k = 0; k < 8; ++k) {
+            const EdgeParams& epc = epcs[c];
             const int b = bs[2 * k];
             if (!b) continue;
             if (dir == 0)

@@ -1,24 +1,29 @@
-// General H.264 decoding path: CAVLC macroblock layer of I and P slices (Baseline /
-// Constrained Baseline / CAVLC Main without B slices), reference picture management, the CPU
-// reference reconstruction and a closed-loop synthetic encoder that emits the same syntax.
+// General H.264 decoding path: the macroblock layer of I, P and B slices in both entropy modes
+// (CAVLC and CABAC; Baseline / Main / High profile, progressive 8-bit 4:2:0), 4x4 and 8x8
+// transforms, scaling matrices, explicit and implicit weighted prediction, spatial and temporal
+// direct prediction, reference picture management with picture-order-count output reordering,
+// the CPU reference reconstruction and a closed-loop synthetic encoder that emits the same
+// syntax.
 //
 // Split of work (MI355X-first):
 //  * CPU (`Decoder::parse`): the inherently serial entropy layer — slice headers, mb_type,
-//    prediction modes, motion-vector prediction, CAVLC residual levels and dequantisation —
-//    into a compact per-picture record array (`Picture`: 40-byte MbRec per MB + a pool of
-//    dequantised 4x4 coefficient blocks + a motion-vector pool), and the DPB / reference-list
-//    bookkeeping (which GPU surface holds which reference picture).
-//  * GPU (gpu_avc.hip): everything that touches samples — motion compensation + residual for
-//    all inter MBs of all cameras in one launch, intra prediction in a row-ticketed wavefront,
-//    the deblocking filter in a second wavefront, then the NV12->BGR24 conversion.
+//    prediction modes, motion-vector prediction (incl. direct modes), residual levels and
+//    dequantisation — into a compact per-picture record array (`Picture`: 56-byte MbRec per MB
+//    + a pool of dequantised coefficient blocks + a motion-vector pool + a weight pool), and the
+//    DPB / reference-list / output-order bookkeeping (which GPU surface holds which picture).
+//  * GPU (gpu_avc.hip): everything that touches samples — motion compensation (bi-predictive and
+//    weighted) + residual for all inter MBs of all cameras in one launch, intra prediction
+//    (4x4 / 8x8 / 16x16) in a row-ticketed wavefront, the deblocking filter in a second
+//    wavefront, then the NV12->BGR24 conversion of each camera's newest output picture.
 //  * `cpu_reconstruct` is the bit-exact CPU reference (and the CPU backend) built from the same
 //    primitives (avc_recon.h).
 //
 // Reference parity: this is the libavcodec h264 decoder the reference calls through PyAV
 // (python/read_image.py:87 `p.decode()`, :94 `to_ndarray('bgr24')`; SURVEY.md §2.2 N2 and
-// §2.3 K1). CABAC (Main/High profile entropy coding), B slices, interlace, 8x8 transforms,
-// weighted prediction and scaling matrices are reported as UnsupportedStream (the VCN
-// backend's job).
+// §2.3 K1), including its output order (frames leave in picture-order-count order). Interlaced
+// coding (field pictures / MBAFF), 4:2:2 / 4:4:4, high bit depth, lossless, data partitioning,
+// FMO/ASO, SP/SI slices and CABAC streams with cabac_init_idc 1 or 2 are reported as
+// UnsupportedStream (the VCN backend's job).
 #pragma once
 
 #include <map>
@@ -29,66 +34,113 @@
 
 namespace vep::avc {
 
-constexpr int kMaxDpbSlots = 17;  // 16 references + the picture being decoded
+constexpr int kMaxDpbSlots = 34;  // 16 references + 16 pictures waiting for output + current + pin
+
+// Access-unit metadata a picture carries to its output (VideoFrame fields).
+struct AuMeta {
+  i64 pts = 0, dts = 0, arrival_ms = 0;
+  i64 tag = 0;  // caller's tag (the camera passes the packet's index in its GOP)
+  bool keyframe = false, corrupt = false;
+};
+
+// A decoded picture leaving the reorder buffer (output order).
+struct OutFrame {
+  int slot = -1;     // DPB slot holding its samples
+  PictureInfo info;  // size, crop, picture type
+  AuMeta au;
+  int poc = 0;
+};
 
 // One parsed picture, ready for reconstruction into DPB slot `target`.
 struct Picture {
   int wmbs = 0, hmbs = 0;
   std::vector<MbRec> mbs;     // raster order
   std::vector<i16> coefs;     // 16-entry blocks (dequantised, row-major); I_PCM raw samples
-  std::vector<i16> mvs;       // 32 entries (16 x (mvx, mvy), quarter samples) per inter MB
+  std::vector<i16> mvs;       // 32 entries (16 x (mvx, mvy), quarter samples) per list per MB
+  std::vector<WpEntry> wps;   // weighted-prediction entries (4 per weighted MB)
   int target = 0;             // DPB slot this picture is reconstructed into
   int dpb_slots = 1;          // surfaces the camera needs for this stream
   bool constrained_intra = false;
-  int intra_mbs = 0;          // I4x4 / I16x16 MBs (need the wavefront pass)
+  int intra_mbs = 0;          // I4x4 / I8x8 / I16x16 MBs (need the wavefront pass)
   int intra_res = 0;          // intra MBs with residual samples (MbRec::res slots)
   int inter_mbs = 0;          // skip / inter / I_PCM MBs (the parallel pass)
   bool deblock = false;       // any MB with the loop filter enabled
   bool idr = false;
+  int poc = 0;
   PictureInfo info;
+  AuMeta au;
+  // Pictures that left the reorder buffer when this one was decoded, in output order (the last
+  // one is the newest frame a client can be shown after this picture).
+  std::vector<OutFrame> outputs;
 
   int nmbs() const { return wmbs * hmbs; }
   const i16* block(u32 b) const { return coefs.data() + size_t(b) * 16; }
 };
 using PicturePtr = std::shared_ptr<const Picture>;
 
-// Structural invariants the reconstruction kernels rely on: every record's coefficient-pool and
-// motion-vector indices lie inside the picture's pools, reference / target slots inside the
-// DPB, modes in range. Throws Error otherwise (defence in depth against a parser bug on hostile
-// input: the GPU kernels index with these values unchecked).
+// Structural invariants the reconstruction kernels rely on: every record's coefficient-pool,
+// motion-vector and weight indices lie inside the picture's pools, reference / target slots
+// inside the DPB, modes in range. Throws Error otherwise (defence in depth against a parser bug
+// on hostile input: the GPU kernels index with these values unchecked).
 void validate(const Picture& p);
 
 // Full slice header (the fields reconstruction needs).
 struct SliceHdr {
   int nal_type = 0, nal_ref_idc = 0;
   int first_mb = 0, slice_type = 0, pps_id = 0, frame_num = 0, idr_pic_id = 0;
-  int poc_lsb = 0;
-  int num_ref_idx_l0 = 1;
+  int poc_lsb = 0, delta_poc_bottom = 0, delta_poc[2] = {0, 0};
+  bool direct_spatial = true;
+  int num_ref_idx[2] = {1, 1};
   struct RefMod {
     int idc, val;
   };
-  std::vector<RefMod> ref_mods;  // ref_pic_list_modification (list 0)
+  std::vector<RefMod> ref_mods[2];  // ref_pic_list_modification per list
+  // pred_weight_table (explicit weighted prediction); weights default to 1 << log2_denom
+  bool explicit_wp = false;
+  int luma_lwd = 0, chroma_lwd = 0;
+  struct Weight {
+    i16 w[3], o[3];  // Y, Cb, Cr
+  };
+  std::vector<Weight> wt[2];
   bool no_output_of_prior_pics = false, long_term_reference = false;
   bool adaptive_marking = false;
   struct Mmco {
     int op, a, b;
   };
   std::vector<Mmco> mmcos;
+  int cabac_init_idc = 0;
   int qp = 26;                   // SliceQP_Y
   int disable_deblocking = 0, alpha_off = 0, beta_off = 0;  // offsets already doubled
   bool idr() const { return nal_type == h264::kNalIdr; }
+  int type() const { return slice_type % 5; }
+  bool has_mmco5() const {
+    for (const auto& m : mmcos)
+      if (m.op == 5) return true;
+    return false;
+  }
 };
 
-// Parse-time state of one MB of the current picture (neighbour derivations).
+// Parse-time state of one MB of the current picture (neighbour derivations of both entropy
+// modes, direct prediction of later B pictures).
 struct MbState {
-  u8 kind = 0xFF;   // MbKind; 0xFF = not decoded in this picture
-  u16 slice = 0;
-  i8 ref[4] = {-1, -1, -1, -1};  // ref_idx_l0 per 8x8 (-1: intra)
-  i16 mv[16][2] = {};
-  u8 tc[16] = {};     // luma total_coeff (raster)
-  u8 tcc[2][4] = {};  // chroma AC total_coeff per component (raster 2x2)
-  u8 i4[16] = {};     // Intra4x4PredMode (raster)
+  u8 kind = 0xFF;    // MbKind; 0xFF = not decoded in this picture
+  u8 skip = 0;       // P_Skip / B_Skip (mb_skip_flag context)
+  u8 direct16 = 0;   // B_Skip / B_Direct_16x16 (B mb_type context)
+  u8 direct8 = 0;    // bit per 8x8: predicted by direct mode (ref_idx context)
+  u8 t8x8 = 0;       // transform_size_8x8_flag
+  u8 cbp = 0;        // CodedBlockPatternLuma | CodedBlockPatternChroma << 4 (I_PCM: 0x2F)
+  u8 chroma_mode = 0;
   u8 qp = 0;
+  u16 slice = 0;
+  u16 cbf = 0;       // coded_block_flag of the luma 4x4 blocks (raster)
+  u8 cbf_dc = 0;     // bit 0 luma DC (Intra16x16), bits 1-2 Cb / Cr DC
+  u8 cbf_cac[2] = {0, 0};  // chroma AC blocks (raster 2x2) per component
+  i8 ref[2][4] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}};  // refIdx per list per 8x8 (-1: unused)
+  i16 mv[2][16][2] = {};
+  u8 mvd[2][16][2] = {};  // min(|mvd|, 127) per 4x4 (CABAC mvd context)
+  u8 tc[16] = {};     // CAVLC luma total_coeff (raster)
+  u8 tcc[2][4] = {};  // CAVLC chroma AC total_coeff per component (raster 2x2)
+  u8 i4[16] = {};     // Intra4x4PredMode (raster; Intra8x8PredMode replicated over its 4 blocks)
 };
 
 // Neighbour derivations shared by the decoder and the encoder (§6.4.11, §8.3.1.1, §8.4.1.3,
@@ -112,13 +164,28 @@ class MbNeighbours {
   // nC for luma block (raster) `blk` / chroma component c block `blk` (§9.2.1).
   int nc_luma(int mb, int blk) const;
   int nc_chroma(int mb, int c, int blk) const;
-  // predIntra4x4PredMode for raster block `blk`.
+  // predIntra4x4PredMode for raster block `blk` (also predIntra8x8PredMode with blk = the
+  // 8x8's top-left 4x4 block and n8 = true: §8.3.2.1's neighbour block choice).
   int pred_intra4x4(int mb, int blk, bool constrained_intra) const;
-  // Motion-vector predictor for partition (x, y, w, h) in 4x4 units with reference `ref`;
-  // `done` = 4x4 blocks of the current MB whose motion is already set; shape: 0 generic,
+  int pred_intra8x8(int mb, int b8, bool constrained_intra) const;
+  // Motion-vector predictor of list `list` for partition (x, y, w, h) in 4x4 units with reference
+  // `ref`; `done` = 4x4 blocks of the current MB whose motion is already set; shape: 0 generic,
   // 1 16x8, 2 8x16.
-  void pred_mv(int mb, int x4, int y4, int w4, int h4, int ref, u16 done, int shape, int out[2]) const;
+  void pred_mv(int mb, int x4, int y4, int w4, int h4, int list, int ref, u16 done, int shape,
+               int out[2]) const;
+  void pred_mv(int mb, int x4, int y4, int w4, int h4, int ref, u16 done, int shape, int out[2]) const {
+    pred_mv(mb, x4, y4, w4, h4, 0, ref, done, shape, out);
+  }
   void pskip_mv(int mb, int out[2]) const;
+  // Neighbour A/B/C(D) motion of the whole MB for list `list` (direct spatial prediction):
+  // ref[k] = refIdx (-1 unavailable / intra / list unused).
+  void mb_neighbour_refs(int mb, int list, int ref[3]) const;
+  // Swap the state array out (kept as the colocated picture's motion) and start a fresh one.
+  std::vector<MbState> take_state() {
+    std::vector<MbState> v;
+    v.swap(st_);
+    return v;
+  }
 
  private:
   struct Nb {
@@ -126,10 +193,20 @@ class MbNeighbours {
     int ref;
     int mv[2];
   };
-  Nb motion_at(int mb, int x, int y, u16 done) const;  // x, y in luma samples rel. to mb
+  Nb motion_at(int mb, int x, int y, u16 done, int list) const;  // x, y in luma samples rel. to mb
   int w_ = 0, h_ = 0;
   int cur_ = -1, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
   std::vector<MbState> st_;
+};
+
+// Motion of a reference picture as the colocated picture of direct prediction (§8.4.1.2.1):
+// per 4x4 block the vector and reference index of list 0 if the block used it, else of list 1,
+// and the identity of the referenced picture.
+struct ColMotion {
+  int wmbs = 0, hmbs = 0;
+  std::vector<i16> mv;   // 2 per 4x4 block (raster blocks of raster MBs: mb * 16 + blk)
+  std::vector<i8> ref;   // refIdxCol (-1: intra)
+  std::vector<u32> pid;  // Picture uid the block references
 };
 
 // Reference picture (DPB entry).
@@ -139,24 +216,50 @@ struct RefPic {
   int frame_num_wrap = 0;
   bool long_term = false;
   int lt_idx = 0;
+  int poc = 0;
+  u32 uid = 0;
+  std::shared_ptr<const ColMotion> col;
 };
 
-// Stateful decoder of one H.264 stream (parameter sets, DPB marking, neighbour state).
+// Per-slice list entry (a RefPic snapshot).
+struct ListEntry {
+  int slot = -1;
+  int poc = 0;
+  bool long_term = false;
+  u32 uid = 0;
+  const ColMotion* col = nullptr;
+};
+
+// Stateful decoder of one H.264 stream (parameter sets, DPB marking, output order, neighbour
+// state).
 class Decoder {
  public:
   // Parse one access unit into a Picture (decode order). Throws UnsupportedStream for syntax
-  // outside the supported profile subset and Error for corrupt data.
-  PicturePtr parse(const AccessUnit& au);
+  // outside the supported subset and Error for corrupt data. `tag` is carried to the output.
+  PicturePtr parse(const AccessUnit& au, i64 tag = 0);
   void absorb_parameter_sets(const AccessUnit& au);
   bool has_sps() const { return !sps_.empty(); }
-  // Forget the DPB (e.g. after a failed picture): the next picture must be an IDR.
+  // Forget the DPB and the reorder buffer (e.g. after a failed picture): the next picture must
+  // be an IDR.
   void reset_references();
   int dpb_slots() const { return dpb_slots_; }
+  // Frames still waiting in the reorder buffer (flushed by the next IDR / end of stream).
+  int pending_output() const { return int(pending_.size()); }
+  // Output every pending frame now (end of stream); returns them in output order.
+  std::vector<OutFrame> flush_output();
 
  private:
-  void build_ref_list(const SliceHdr& sh, const h264::Sps& sps);
-  void mark_references(const SliceHdr& sh, const h264::Sps& sps, int slot);
+  struct Pending {
+    OutFrame f;
+    u32 uid;
+  };
+  void build_lists(const SliceHdr& sh, const h264::Sps& sps, int cur_poc);
+  void mark_references(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid,
+                       std::shared_ptr<const ColMotion> col);
   int pick_slot() const;
+  int compute_poc(const SliceHdr& sh, const h264::Sps& sps);
+  void bump(Picture& pic, bool flush_all);
+  int reorder_depth(const h264::Sps& sps) const;
 
   std::map<int, h264::Sps> sps_;
   std::map<int, h264::Pps> pps_;
@@ -164,10 +267,23 @@ class Decoder {
   std::vector<u32> epb_;
   MbNeighbours nb_;
   std::vector<RefPic> dpb_;
-  std::vector<int> list0_;  // ref_idx -> DPB slot of the current slice
+  std::vector<Pending> pending_;  // decoded, not yet output (POC order decides)
+  std::vector<ListEntry> list_[2];  // refIdx -> entry of the current slice
   int max_lt_idx_ = -1;     // MaxLongTermFrameIdx ("no long-term frame indices" = -1)
   int dpb_slots_ = 2;
+  int wmbs_ = 0, hmbs_ = 0;  // active picture size (changes only at an IDR)
   bool have_idr_ = false;
+  int pinned_slot_ = -1;    // newest output: kept until a newer one leaves the reorder buffer
+  int last_out_poc_ = 0;
+  bool out_since_idr_ = false;
+  int adaptive_reorder_ = 0;  // reorder depth learnt from the stream when the SPS gives none
+  int reorder_cur_ = 0;       // reorder depth in force for the active SPS
+  u32 next_uid_ = 1;
+  // picture order count state (§8.2.1)
+  int prev_poc_msb_ = 0, prev_poc_lsb_ = 0;
+  int prev_frame_num_ = 0, prev_frame_num_offset_ = 0;
+  bool prev_ref_mmco5_ = false;
+  std::vector<std::vector<MbState>> spare_;  // recycled MbState arrays
 };
 
 // CPU reference reconstruction of `pic` into DPB surfaces `slots` (coded size; references are
@@ -204,20 +320,28 @@ struct MbLevels {
 };
 // Dequantised residual blocks of one MB (16 luma raster, 4 Cb, 4 Cr) and their coded masks.
 struct MbResidual {
-  i16 blk[24][16];
-  u16 luma = 0;
+  i16 blk[24][16];  // 16 luma 4x4 (raster), 4 Cb, 4 Cr
+  i16 b8[4][64];    // 8x8-transform luma blocks (raster 8x8 in each; t8 MBs)
+  u16 luma = 0;     // coded luma 4x4 blocks (t8: all four blocks of each coded 8x8)
   u8 chroma = 0;
+  bool t8 = false;
 };
 void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& out);
 // Append MB `mb` to `pic`: coefficient blocks (or I_PCM samples), motion vectors and the
 // bookkeeping fields of `m` (coef, mv, coded masks, nz from s.tc); stores pic.mbs[mb] = m.
-void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm);
+// (m.nz is the caller's; wp = 4 WpEntry when m.flags has kMbWp)
+void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm,
+              const WpEntry* wp = nullptr);
 void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots);
 void cpu_deblock(const Picture& pic, HostSurface& target);
 // Neighbour samples for intra prediction from the surface being reconstructed.
 void intra4x4_neighbours(const Picture& pic, int mb, int idx, const HostSurface& T, Intra4Nb& n);
 void intra16_neighbours(const Picture& pic, int mb, const HostSurface& T, Intra16Nb& n);
 void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, IntraChromaNb& n);
+// Filtered Intra_8x8 references of 8x8 block q: f[0] = p'[-1,-1], f[1..16] = p'[0..15,-1],
+// f[17..24] = p'[-1,0..7].
+void intra8x8_neighbours(const Picture& pic, int mb, int q, const HostSurface& T, int* f, bool& has_top,
+                         bool& has_left);
 
 // ------------------------------------------------------------------------------ encoder
 // Closed-loop synthetic H.264 encoder (CAVLC I/P): intra 16x16 / 4x4 and chroma prediction,

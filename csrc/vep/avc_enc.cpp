@@ -417,12 +417,14 @@ struct AvcEncoder::Impl {
     m.alpha_off = i8(2 * cfg.alpha_off);
     m.beta_off = i8(2 * cfg.beta_off);
     std::fill(std::begin(m.ref), std::end(m.ref), u8(0xFF));
+    std::fill(std::begin(m.ref1), std::end(m.ref1), u8(0xFF));
     return m;
   }
 
   void finish_mb(int mb, MbRec m, MbState& s, const MbLevels* lv, bool i16, int qp, const u8* pcm) {
     m.qp = m.kind == kIPcm ? 0 : u8(qp);
     m.qpc = u8(chroma_qp(m.qp, cfg.chroma_qp_offset));
+    m.qpc2 = m.qpc;
     s.qp = u8(qp);
     MbResidual res;
     if (lv) {
@@ -431,6 +433,8 @@ struct AvcEncoder::Impl {
       dequantize_mb(l, i16, qp, chroma_qp(qp, cfg.chroma_qp_offset), res);
     }
     for (int r = 0; r < 16; ++r) m.i4[r >> 1] |= u8((m.kind == kI4x4 ? s.i4[r] : 0) << ((r & 1) * 4));
+    m.nz = 0;
+    for (int r = 0; r < 16; ++r) m.nz |= u16(s.tc[r] ? 1u << r : 0u);
     store_mb(pic, mb, m, s, lv ? &res : nullptr, pcm);
     cpu_reconstruct_mb(pic, mb, slots);
   }
@@ -668,7 +672,7 @@ struct AvcEncoder::Impl {
     out.clear();
     out.push_back({0, 0});
     int p[2];
-    nb.pred_mv(mb, 0, 0, 4, 4, ref, 0, 0, p);
+    nb.pred_mv(mb, 0, 0, 4, 4, 0, ref, 0, 0, p);
     out.push_back({p[0], p[1]});
     for (const Obj& o : objs) {
       if (o.x > mx * 16 + 16 || o.x + o.w < mx * 16 || o.y > my * 16 + 16 || o.y + o.h < my * 16) continue;
@@ -752,20 +756,20 @@ struct AvcEncoder::Impl {
       }
     }
     // ---- motion vectors in decoding order (predictors depend on earlier partitions)
-    for (int i = 0; i < 4; ++i) s.ref[i] = i8(ref8[i]);
+    for (int i = 0; i < 4; ++i) s.ref[0][i] = i8(ref8[i]);
     int mvd[16][2];
     u16 done = 0;
     int mvs[16][2];
     for (int i = 0; i < np; ++i) {
       Part& p = parts[i];
       int mvp[2];
-      nb.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, p.ref, done, p.shape, mvp);
+      nb.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, 0, p.ref, done, p.shape, mvp);
       mvd[i][0] = p.mv[0] - mvp[0];
       mvd[i][1] = p.mv[1] - mvp[1];
       for (int y = p.y4; y < p.y4 + p.h4; ++y)
         for (int x = p.x4; x < p.x4 + p.w4; ++x) {
-          s.mv[y * 4 + x][0] = i16(p.mv[0]);
-          s.mv[y * 4 + x][1] = i16(p.mv[1]);
+          s.mv[0][y * 4 + x][0] = i16(p.mv[0]);
+          s.mv[0][y * 4 + x][1] = i16(p.mv[1]);
           mvs[y * 4 + x][0] = p.mv[0];
           mvs[y * 4 + x][1] = p.mv[1];
           done |= u16(1u << (y * 4 + x));

@@ -1,0 +1,1014 @@
+// Generic H.264 macroblock layer (§7.3.5, §7.4.5, §8.4.1, §8.4.2.3, §8.5, §9.2, §9.3): I, P and B
+// macroblocks in CAVLC and CABAC slices, Intra 4x4 / 8x8 / 16x16 and I_PCM, every inter
+// partition and sub-partition shape, spatial and temporal direct prediction (B_Skip,
+// B_Direct_16x16, B_Direct_8x8), explicit and implicit weighted prediction, 4x4 and 8x8
+// transforms with scaling matrices. Output: MbState (neighbour / colocated state) and the
+// MbRec + dequantised coefficient blocks + motion vectors + weights the reconstruction kernels
+// consume (avc.h).
+//
+// The fast CAVLC path for Baseline-style slices (avc.cpp MbDecoder, fused nC cache) stays the
+// default for those; this layer takes every slice that needs anything beyond it.
+//
+// Reference parity: libavcodec's h264 macroblock decoding behind PyAV `packet.decode()`
+// (python/read_image.py:87).
+#include <algorithm>
+
+#include "avc_cabac.h"
+#include "avc_cavlc.h"
+#include "avc_internal.h"
+
+namespace vep::avc {
+
+namespace {
+
+// LevelScale4x4 / LevelScale8x8 (§8.5.9, §8.5.13.1): weightScale (scaling list, raster) times
+// normAdjust, per list and qP % 6.
+struct Dequant {
+  int ls4[6][6][16];  // [Intra Y, Cb, Cr, Inter Y, Cb, Cr][m][raster]
+  int ls8[2][6][64];  // [Intra Y, Inter Y][m][raster]
+  explicit Dequant(const h264::ScalingLists& sl) {
+    for (int l = 0; l < 6; ++l)
+      for (int m = 0; m < 6; ++m)
+        for (int k = 0; k < 16; ++k) {
+          const int pos = kZigzag4x4[k];
+          ls4[l][m][pos] = int(sl.l4[l][k]) * norm_adjust(m, pos >> 2, pos & 3);
+        }
+    for (int l = 0; l < 2; ++l)
+      for (int m = 0; m < 6; ++m)
+        for (int k = 0; k < 64; ++k) {
+          const int pos = kZigzag8x8[k];
+          ls8[l][m][pos] = int(sl.l8[l][k]) * norm_adjust8(m, pos >> 3, pos & 7);
+        }
+  }
+};
+
+inline int scale4(int c, int ls, int qp) {
+  return qp >= 24 ? (c * ls) * (1 << (qp / 6 - 4)) : (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
+}
+inline int scale8(int c, int ls, int qp) {
+  return qp >= 36 ? (c * ls) * (1 << (qp / 6 - 6)) : (c * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+}
+
+// B mb_type 0..22 (Table 7-14): prediction flags (bit 0 list 0, bit 1 list 1) per partition.
+constexpr u8 kBPart[23][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {1, 1}, {1, 1}, {2, 2}, {2, 2},
+                              {1, 2}, {1, 2}, {2, 1}, {2, 1}, {1, 3}, {1, 3}, {2, 3}, {2, 3},
+                              {3, 1}, {3, 1}, {3, 2}, {3, 2}, {3, 3}, {3, 3}, {0, 0}};
+// B sub_mb_type 0..12 (Table 7-18): prediction flags, sub-partition shape (0 8x8, 1 8x4, 2 4x8,
+// 3 4x4). P sub_mb_type 0..3 is list 0 with shape = value.
+constexpr u8 kBSub[13][2] = {{0, 0}, {1, 0}, {2, 0}, {3, 0}, {1, 1}, {1, 2}, {2, 1},
+                             {2, 2}, {3, 1}, {3, 2}, {1, 3}, {2, 3}, {3, 3}};
+constexpr int kSubParts[4] = {1, 2, 2, 4};
+
+inline int raster_b8(int blk) { return ((blk >> 3) << 1) | ((blk & 3) >> 1); }
+inline u16 b8_blocks(int b8) { return u16(0x33u << ((b8 & 1) * 2 + (b8 >> 1) * 8)); }
+inline int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
+
+template <bool kCabac>
+class MbLayer {
+ public:
+  MbLayer(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const Dequant& dq)
+      : nb_(nb), pic_(pic), env_(env), sh_(*env.sh), pps_(*env.pps), sps_(*env.sps), dq_(dq) {
+    type_ = sh_.type();
+    qp_ = sh_.qp;
+    weighted_ = (type_ == h264::kP && pps_.weighted_pred) || (type_ == h264::kB && pps_.weighted_bipred_idc != 0);
+    implicit_ = type_ == h264::kB && pps_.weighted_bipred_idc == 2;
+  }
+
+  // entropy sources (one of them is used)
+  Bits* br = nullptr;
+  AvcBins<BinDecoder>* bins = nullptr;
+  cabac::Decoder* cabac = nullptr;
+  int prev_qpd_nz = 0;  // mb_qp_delta of the previous MB in decoding order != 0 (CABAC context)
+
+  int qp() const { return qp_; }
+
+  bool read_skip_flag(int mb) {
+    MbState& s = nb_.at(mb);
+    s = MbState{};
+    s.slice = u16(env_.slice);
+    nb_.begin(mb);
+    auto cond = [&](int m) { return m >= 0 && !nb_.at(m).skip ? 1 : 0; };
+    const int inc = cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1));
+    return bins->mb_skip(type_ == h264::kB, inc, false) != 0;
+  }
+
+  void skip_mb(int mb, bool fresh) {
+    MbState& s = nb_.at(mb);
+    if (fresh) {
+      s = MbState{};
+      s.slice = u16(env_.slice);
+      nb_.begin(mb);
+    }
+    s.kind = kSkip;
+    s.skip = 1;
+    s.qp = u8(qp_);
+    MbResidual res;
+    res.luma = 0;
+    res.chroma = 0;
+    if (type_ == h264::kP) {
+      s.ref[0][0] = s.ref[0][1] = s.ref[0][2] = s.ref[0][3] = 0;
+      need_ref(0, 0);
+      int mv[2];
+      nb_.pskip_mv(mb, mv);
+      for (auto& v : s.mv[0]) {
+        v[0] = i16(mv[0]);
+        v[1] = i16(mv[1]);
+      }
+    } else {
+      s.direct16 = 1;
+      s.direct8 = 0xF;
+      direct(mb, s, 0xF);
+    }
+    prev_qpd_nz = 0;
+    emit(mb, s, res, 0, 0, nullptr);
+  }
+
+  void coded_mb(int mb, bool fresh) {
+    MbState& s = nb_.at(mb);
+    if (fresh) {
+      s = MbState{};
+      s.slice = u16(env_.slice);
+      nb_.begin(mb);
+    }
+    int mbt = read_mb_type(mb);
+    int itype = -1;
+    if (type_ == h264::kI) {
+      itype = mbt;
+    } else if (type_ == h264::kP) {
+      VEP_CHECK(mbt <= 30, "bad P mb_type");
+      if (mbt >= 5) itype = mbt - 5;
+    } else {
+      VEP_CHECK(mbt <= 48, "bad B mb_type");
+      if (mbt >= 23) itype = mbt - 23;
+    }
+    VEP_CHECK(itype <= 25, "bad intra mb_type");
+    MbResidual res;
+    res.luma = 0;
+    res.chroma = 0;
+    if (itype == 25) {
+      pcm_mb(mb, s, res);
+      return;
+    }
+    int cbp = 0, i16_mode = 0;
+    const bool intra = itype >= 0;
+    bool no_small = true;  // noSubMbPartSizeLessThan8x8Flag
+    if (itype == 0) {
+      if (pps_.transform_8x8_mode) s.t8x8 = u8(read_t8x8(mb));
+      s.kind = s.t8x8 ? kI8x8 : kI4x4;
+      intra_modes(mb, s);
+      s.chroma_mode = u8(read_chroma_mode(mb));
+    } else if (itype > 0) {
+      s.kind = kI16x16;
+      i16_mode = (itype - 1) % 4;
+      cbp = (((itype - 1) / 4) % 3) << 4 | (itype >= 13 ? 15 : 0);
+      std::fill(std::begin(s.i4), std::end(s.i4), u8(2));
+      s.chroma_mode = u8(read_chroma_mode(mb));
+    } else {
+      s.kind = kInter;
+      no_small = inter_pred(mb, s, mbt);
+    }
+    VEP_CHECK(s.chroma_mode <= 3, "bad intra_chroma_pred_mode");
+    if (s.kind != kI16x16) cbp = read_cbp(mb, s, intra);
+    s.cbp = u8(cbp);
+    if (s.kind == kInter && (cbp & 15) && pps_.transform_8x8_mode && no_small &&
+        !(type_ == h264::kB && mbt == 0 && !sps_.direct_8x8))
+      s.t8x8 = u8(read_t8x8(mb));
+    int qp = qp_;
+    if ((cbp & 15) || (cbp >> 4) || s.kind == kI16x16) {
+      const int dqp = read_qp_delta();
+      VEP_CHECK(dqp >= -26 && dqp <= 25, "mb_qp_delta out of range");
+      qp = (qp + dqp + 52) % 52;
+      prev_qpd_nz = dqp != 0;
+    } else {
+      prev_qpd_nz = 0;
+    }
+    qp_ = qp;
+    s.qp = u8(qp);
+    residual(mb, s, res, cbp & 15, cbp >> 4, qp, intra);
+    emit(mb, s, res, i16_mode, s.chroma_mode, nullptr);
+  }
+
+  // Pictures the slice's MBs reference (list entries that must exist).
+  void need_ref(int list, int idx) {
+    const auto* l = env_.list[list];
+    VEP_CHECK(l && idx >= 0 && idx < int(l->size()) && (*l)[size_t(idx)].slot >= 0,
+              "ref_idx names a missing reference picture");
+  }
+
+ private:
+  // ------------------------------------------------------------------ syntax elements
+  int read_mb_type(int mb) {
+    if constexpr (kCabac) {
+      if (type_ == h264::kI) {
+        auto cond = [&](int m) {
+          if (m < 0) return 0;
+          const u8 k = nb_.at(m).kind;
+          return (k == kI4x4 || k == kI8x8) ? 0 : 1;
+        };
+        return bins->mb_type_i(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), 0);
+      }
+      if (type_ == h264::kP) return bins->mb_type_p(0);
+      auto cond = [&](int m) { return m >= 0 && !nb_.at(m).direct16 ? 1 : 0; };
+      return bins->mb_type_b(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), 0);
+    } else {
+      return int(br->ue());
+    }
+  }
+  int read_t8x8(int mb) {
+    if constexpr (kCabac) {
+      auto cond = [&](int m) { return m >= 0 && nb_.at(m).t8x8 ? 1 : 0; };
+      return int(bins->transform_8x8(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), false));
+    } else {
+      return int(br->u1());
+    }
+  }
+  int read_chroma_mode(int mb) {
+    if constexpr (kCabac) {
+      auto cond = [&](int m) {
+        if (m < 0) return 0;
+        const MbState& n = nb_.at(m);
+        return is_intra(n.kind) && n.kind != kIPcm && n.chroma_mode != 0 ? 1 : 0;
+      };
+      return bins->chroma_mode(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), 0);
+    } else {
+      return int(br->ue());
+    }
+  }
+  int read_mode(int pred) {  // prev_intra{4x4,8x8}_pred_mode_flag + rem
+    if constexpr (kCabac) {
+      if (bins->prev_intra_flag(false)) return pred;
+      const int rem = bins->rem_intra_mode(0);
+      return rem < pred ? rem : rem + 1;
+    } else {
+      if (br->u1()) return pred;
+      const int rem = int(br->u(3));
+      return rem < pred ? rem : rem + 1;
+    }
+  }
+  int read_sub_type() {
+    if constexpr (kCabac) return type_ == h264::kB ? bins->sub_mb_type_b(0) : bins->sub_mb_type_p(0);
+    else return int(br->ue());
+  }
+  int read_ref(int mb, int list, int x4, int y4) {
+    const int n = sh_.num_ref_idx[list];
+    if (n <= 1) return 0;
+    int r;
+    if constexpr (kCabac) {
+      auto cond = [&](int x, int y) {
+        const int m = nb_.mb_at(mb, x, y);
+        if (m < 0) return 0;
+        const MbState& nbs = nb_.at(m);
+        if (m != mb && (nbs.skip || is_intra(nbs.kind))) return 0;
+        const int b8 = (((y & 15) >> 3) << 1) | ((x & 15) >> 3);
+        if ((nbs.direct8 >> b8) & 1) return 0;
+        return nbs.ref[list][b8] > 0 ? 1 : 0;
+      };
+      r = bins->ref_idx(cond(x4 * 4 - 1, y4 * 4) + 2 * cond(x4 * 4, y4 * 4 - 1), 0);
+    } else {
+      r = n == 2 ? int(br->u1() ^ 1u) : int(br->ue());
+    }
+    VEP_CHECK(r < n, "ref_idx out of range");
+    need_ref(list, r);
+    return r;
+  }
+  int read_mvd(int mb, int list, int x4, int y4, int comp) {
+    if constexpr (kCabac) {
+      auto am = [&](int x, int y) -> int {
+        const int m = nb_.mb_at(mb, x, y);
+        if (m < 0) return 0;
+        const MbState& n = nb_.at(m);
+        return n.mvd[list][((y & 15) >> 2) * 4 + ((x & 15) >> 2)][comp];
+      };
+      const int sum = am(x4 * 4 - 1, y4 * 4) + am(x4 * 4, y4 * 4 - 1);
+      return bins->mvd(comp ? 47 : 40, sum < 3 ? 0 : (sum > 32 ? 2 : 1), 0);
+    } else {
+      return br->se();
+    }
+  }
+  int read_cbp(int mb, const MbState& s, bool intra) {
+    if constexpr (kCabac) {
+      const int am = nb_.mb_at(mb, -1, 0), bm = nb_.mb_at(mb, 0, -1);
+      int luma = 0;
+      for (int b8 = 0; b8 < 4; ++b8) {
+        auto cond = [&](int m, int nb8, bool cur) {
+          if (cur) return ((luma >> nb8) & 1) ? 0 : 1;
+          if (m < 0) return 0;
+          return ((nb_.at(m).cbp >> nb8) & 1) ? 0 : 1;
+        };
+        const int ca = (b8 & 1) ? cond(mb, b8 - 1, true) : cond(am, b8 + 1, false);
+        const int cb = (b8 & 2) ? cond(mb, b8 - 2, true) : cond(bm, b8 + 2, false);
+        luma |= int(bins->cbp_luma_bin(ca + 2 * cb, false)) << b8;
+      }
+      auto cc = [&](int m, int thr) { return m >= 0 && (nb_.at(m).cbp >> 4) >= thr ? 1 : 0; };
+      int chroma = 0;
+      if (bins->cbp_chroma_bin(cc(am, 1) + 2 * cc(bm, 1), false))
+        chroma = 1 + int(bins->cbp_chroma_bin(4 + cc(am, 2) + 2 * cc(bm, 2), false));
+      (void)s;
+      (void)intra;
+      return luma | chroma << 4;
+    } else {
+      const u32 me = br->ue();
+      VEP_CHECK(me < 48, "bad coded_block_pattern");
+      (void)mb;
+      (void)s;
+      return intra ? kCbpIntra[me] : kCbpInter[me];
+    }
+  }
+  int read_qp_delta() {
+    if constexpr (kCabac) return bins->qp_delta(prev_qpd_nz ? 1 : 0, 0);
+    else return br->se();
+  }
+
+  // ------------------------------------------------------------------ I_PCM
+  void pcm_mb(int mb, MbState& s, MbResidual& res) {
+    s.kind = kIPcm;
+    s.cbp = 0x2F;
+    s.cbf = 0xFFFF;
+    s.cbf_dc = 7;
+    s.cbf_cac[0] = s.cbf_cac[1] = 0xF;
+    std::fill(std::begin(s.tc), std::end(s.tc), u8(16));
+    for (auto& c : s.tcc) std::fill(std::begin(c), std::end(c), u8(16));
+    s.qp = u8(qp_);
+    const u8* pcm;
+    if constexpr (kCabac) {
+      const size_t off = cabac->aligned_bytepos();
+      VEP_CHECK(off + kPcmMbBytes <= data_n, "truncated I_PCM macroblock");
+      pcm = data + off;
+      cabac->start(off + kPcmMbBytes);
+    } else {
+      br->align();
+      const size_t off = br->pos() >> 3;
+      VEP_CHECK(off + kPcmMbBytes <= br->size(), "truncated I_PCM macroblock");
+      pcm = br->data() + off;
+      br->skip(kPcmMbBytes * 8);
+    }
+    prev_qpd_nz = 0;
+    emit(mb, s, res, 0, 0, pcm);
+  }
+
+ public:
+  const u8* data = nullptr;  // CABAC: slice RBSP (I_PCM samples are read in place)
+  size_t data_n = 0;
+
+ private:
+  // ------------------------------------------------------------------ intra modes
+  void intra_modes(int mb, MbState& s) {
+    const bool ci = pps_.constrained_intra_pred;
+    if (s.t8x8) {
+      for (int b8 = 0; b8 < 4; ++b8) {
+        const int m = read_mode(nb_.pred_intra8x8(mb, b8, ci));
+        for (u16 w = b8_blocks(b8); w; w &= w - 1) s.i4[__builtin_ctz(w)] = u8(m);
+      }
+    } else {
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        s.i4[r] = u8(read_mode(nb_.pred_intra4x4(mb, r, ci)));
+      }
+    }
+  }
+
+  // ------------------------------------------------------------------ inter prediction
+  struct Part {
+    int x4, y4, w4, h4, shape;
+  };
+  static u16 part_mask(const Part& p) {
+    u16 m = 0;
+    for (int y = p.y4; y < p.y4 + p.h4; ++y)
+      for (int x = p.x4; x < p.x4 + p.w4; ++x) m |= u16(1u << (y * 4 + x));
+    return m;
+  }
+  static void set_mvd(MbState& s, int list, const Part& p, int dx, int dy) {
+    const u8 ax = u8(std::min(dx < 0 ? -dx : dx, 127)), ay = u8(std::min(dy < 0 ? -dy : dy, 127));
+    for (int y = p.y4; y < p.y4 + p.h4; ++y)
+      for (int x = p.x4; x < p.x4 + p.w4; ++x) {
+        s.mvd[list][y * 4 + x][0] = ax;
+        s.mvd[list][y * 4 + x][1] = ay;
+      }
+  }
+  static void set_mv(MbState& s, int list, const Part& p, int mx, int my) {
+    VEP_CHECK(mx >= -32768 && mx <= 32767 && my >= -32768 && my <= 32767, "motion vector out of range");
+    for (int y = p.y4; y < p.y4 + p.h4; ++y)
+      for (int x = p.x4; x < p.x4 + p.w4; ++x) {
+        s.mv[list][y * 4 + x][0] = i16(mx);
+        s.mv[list][y * 4 + x][1] = i16(my);
+      }
+  }
+
+  // Returns noSubMbPartSizeLessThan8x8Flag.
+  bool inter_pred(int mb, MbState& s, int mbt) {
+    const bool b = type_ == h264::kB;
+    if (b && mbt == 0) {  // B_Direct_16x16
+      s.direct16 = 1;
+      s.direct8 = 0xF;
+      direct(mb, s, 0xF);
+      return true;
+    }
+    if ((!b && mbt <= 2) || (b && mbt <= 21)) {
+      Part parts[2];
+      int np;
+      u8 pred[2];
+      int shape;
+      if (!b) {
+        shape = mbt;  // 0 16x16, 1 16x8, 2 8x16
+        pred[0] = pred[1] = 1;
+      } else {
+        shape = mbt <= 3 ? 0 : ((mbt & 1) ? 2 : 1);
+        pred[0] = kBPart[mbt][0];
+        pred[1] = kBPart[mbt][1];
+      }
+      np = shape == 0 ? 1 : 2;
+      for (int i = 0; i < np; ++i) {
+        if (shape == 0) parts[i] = {0, 0, 4, 4, 0};
+        else if (shape == 1) parts[i] = {0, 2 * i, 4, 2, 1};
+        else parts[i] = {2 * i, 0, 2, 4, 2};
+      }
+      int refs[2][2] = {{-1, -1}, {-1, -1}};
+      for (int l = 0; l < 2; ++l)
+        for (int i = 0; i < np; ++i) {
+          if (!((pred[i] >> l) & 1)) continue;
+          refs[l][i] = read_ref(mb, l, parts[i].x4, parts[i].y4);
+          const Part& p = parts[i];
+          for (int y = p.y4 / 2; y < (p.y4 + p.h4) / 2; ++y)
+            for (int x = p.x4 / 2; x < (p.x4 + p.w4) / 2; ++x) s.ref[l][y * 2 + x] = i8(refs[l][i]);
+        }
+      int mvd[2][2][2] = {};
+      for (int l = 0; l < 2; ++l)
+        for (int i = 0; i < np; ++i) {
+          if (!((pred[i] >> l) & 1)) continue;
+          mvd[l][i][0] = read_mvd(mb, l, parts[i].x4, parts[i].y4, 0);
+          mvd[l][i][1] = read_mvd(mb, l, parts[i].x4, parts[i].y4, 1);
+          set_mvd(s, l, parts[i], mvd[l][i][0], mvd[l][i][1]);
+        }
+      for (int l = 0; l < 2; ++l) {
+        u16 done = 0;
+        for (int i = 0; i < np; ++i) {
+          if (!((pred[i] >> l) & 1)) continue;
+          const Part& p = parts[i];
+          int mvp[2];
+          nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, refs[l][i], done, p.shape, mvp);
+          set_mv(s, l, p, mvp[0] + mvd[l][i][0], mvp[1] + mvd[l][i][1]);
+          done |= part_mask(p);
+        }
+      }
+      return true;
+    }
+    // P_8x8 / P_8x8ref0 / B_8x8
+    int sub[4];
+    bool no_small = true;
+    for (int& t : sub) {
+      t = read_sub_type();
+      VEP_CHECK(t <= (b ? 12 : 3), "bad sub_mb_type");
+    }
+    u8 spred[4], sshape[4];
+    for (int i = 0; i < 4; ++i) {
+      if (b) {
+        spred[i] = kBSub[sub[i]][0];
+        sshape[i] = kBSub[sub[i]][1];
+        if (sub[i] == 0) {
+          s.direct8 |= u8(1u << i);
+          if (!sps_.direct_8x8) no_small = false;
+        }
+      } else {
+        spred[i] = 1;
+        sshape[i] = u8(sub[i]);
+      }
+      if (sshape[i] != 0) no_small = false;
+    }
+    for (int l = 0; l < 2; ++l)
+      for (int i = 0; i < 4; ++i) {
+        if (!((spred[i] >> l) & 1)) continue;
+        const int r = (!b && mbt == 4) ? 0 : read_ref(mb, l, (i & 1) * 2, (i >> 1) * 2);
+        if (!b && mbt == 4) need_ref(0, 0);
+        s.ref[l][i] = i8(r);
+      }
+    int mvd[2][4][4][2] = {};
+    auto sub_part = [&](int i, int j) -> Part {
+      const int x8 = (i & 1) * 2, y8 = (i >> 1) * 2;
+      switch (sshape[i]) {
+        case 0: return {x8, y8, 2, 2, 0};
+        case 1: return {x8, y8 + j, 2, 1, 0};
+        case 2: return {x8 + j, y8, 1, 2, 0};
+        default: return {x8 + (j & 1), y8 + (j >> 1), 1, 1, 0};
+      }
+    };
+    for (int l = 0; l < 2; ++l)
+      for (int i = 0; i < 4; ++i) {
+        if (!((spred[i] >> l) & 1)) continue;
+        for (int j = 0; j < kSubParts[sshape[i]]; ++j) {
+          const Part p = sub_part(i, j);
+          mvd[l][i][j][0] = read_mvd(mb, l, p.x4, p.y4, 0);
+          mvd[l][i][j][1] = read_mvd(mb, l, p.x4, p.y4, 1);
+          set_mvd(s, l, p, mvd[l][i][j][0], mvd[l][i][j][1]);
+        }
+      }
+    // motion in 8x8 order (direct 8x8s included, so later sub-partitions predict from them)
+    if (s.direct8) direct(mb, s, s.direct8);
+    u16 done[2] = {0, 0};
+    for (int i = 0; i < 4; ++i) {
+      if ((s.direct8 >> i) & 1) {
+        done[0] |= b8_blocks(i);
+        done[1] |= b8_blocks(i);
+        continue;
+      }
+      for (int l = 0; l < 2; ++l) {
+        if (!((spred[i] >> l) & 1)) continue;
+        for (int j = 0; j < kSubParts[sshape[i]]; ++j) {
+          const Part p = sub_part(i, j);
+          int mvp[2];
+          nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, s.ref[l][i], done[l], 0, mvp);
+          set_mv(s, l, p, mvp[0] + mvd[l][i][j][0], mvp[1] + mvd[l][i][j][1]);
+          done[l] |= part_mask(p);
+        }
+      }
+      done[0] |= b8_blocks(i);
+      done[1] |= b8_blocks(i);
+    }
+    return no_small;
+  }
+
+  // ------------------------------------------------------------------ direct prediction
+  // Motion of the 8x8 blocks in `mask` by the slice's direct mode (§8.4.1.2). Spatial mode uses
+  // the whole MB's neighbours (identical for every 8x8), temporal mode the colocated picture.
+  void direct(int mb, MbState& s, int mask) {
+    VEP_CHECK(env_.list[1] && !env_.list[1]->empty() && (*env_.list[1])[0].slot >= 0,
+              "direct prediction without a list-1 reference");
+    const ListEntry& c1 = (*env_.list[1])[0];
+    const ColMotion* col = c1.col;
+    VEP_CHECK(col && col->wmbs == nb_.wmbs() && col->hmbs == nb_.hmbs(), "colocated picture motion missing");
+    const bool infer = sps_.direct_8x8;
+    auto col_blk = [&](int blk) {  // colocated 4x4 block of raster block blk
+      if (infer) {
+        const int b8 = raster_b8(blk);
+        blk = (b8 & 1 ? 3 : 0) + (b8 & 2 ? 12 : 0);  // the 8x8's outer corner
+      }
+      return size_t(mb) * 16 + size_t(blk);
+    };
+    if (sh_.direct_spatial) {
+      int ref[2];
+      for (int l = 0; l < 2; ++l) {
+        int n[3];
+        nb_.mb_neighbour_refs(mb, l, n);
+        auto minpos = [](int a, int b2) { return (a >= 0 && b2 >= 0) ? std::min(a, b2) : std::max(a, b2); };
+        ref[l] = minpos(n[0], minpos(n[1], n[2]));
+      }
+      const bool zero = ref[0] < 0 && ref[1] < 0;
+      if (zero) ref[0] = ref[1] = 0;
+      int mvp[2][2] = {{0, 0}, {0, 0}};
+      for (int l = 0; l < 2; ++l) {
+        if (ref[l] < 0 || zero) continue;
+        need_ref(l, ref[l]);
+        nb_.pred_mv(mb, 0, 0, 4, 4, l, ref[l], 0, 0, mvp[l]);
+      }
+      if (zero) {
+        need_ref(0, 0);
+        need_ref(1, 0);
+      }
+      for (int b8 = 0; b8 < 4; ++b8) {
+        if (!((mask >> b8) & 1)) continue;
+        for (int l = 0; l < 2; ++l) s.ref[l][b8] = i8(ref[l]);
+        for (u16 w = b8_blocks(b8); w; w &= w - 1) {
+          const int blk = __builtin_ctz(w);
+          const size_t cb = col_blk(blk);
+          const bool col_zero = !c1.long_term && col->ref[cb] == 0 && col->mv[cb * 2] >= -1 &&
+                                col->mv[cb * 2] <= 1 && col->mv[cb * 2 + 1] >= -1 && col->mv[cb * 2 + 1] <= 1;
+          for (int l = 0; l < 2; ++l) {
+            int mx = 0, my = 0;
+            if (ref[l] >= 0 && !zero && !(ref[l] == 0 && col_zero)) {
+              mx = mvp[l][0];
+              my = mvp[l][1];
+            }
+            s.mv[l][blk][0] = i16(ref[l] >= 0 ? mx : 0);
+            s.mv[l][blk][1] = i16(ref[l] >= 0 ? my : 0);
+          }
+        }
+      }
+      return;
+    }
+    // temporal (§8.4.1.2.3)
+    const auto& l0 = *env_.list[0];
+    for (int b8 = 0; b8 < 4; ++b8) {
+      if (!((mask >> b8) & 1)) continue;
+      int r0 = 0;
+      for (u16 w = b8_blocks(b8); w; w &= w - 1) {
+        const int blk = __builtin_ctz(w);
+        const size_t cb = col_blk(blk);
+        int mvc[2] = {0, 0};
+        r0 = 0;
+        if (col->ref[cb] >= 0) {
+          mvc[0] = col->mv[cb * 2];
+          mvc[1] = col->mv[cb * 2 + 1];
+          const u32 pid = col->pid[cb];
+          r0 = -1;
+          for (size_t k = 0; k < l0.size() && r0 < 0; ++k)
+            if (l0[k].slot >= 0 && l0[k].uid == pid) r0 = int(k);
+          if (r0 < 0) r0 = 0;  // the colocated reference is gone (non-conforming): conceal
+        }
+        need_ref(0, r0);
+        const ListEntry& p0 = l0[size_t(r0)];
+        int m0[2], m1[2];
+        const int td = clip3i(-128, 127, c1.poc - p0.poc);
+        if (td == 0 || p0.long_term) {
+          m0[0] = mvc[0];
+          m0[1] = mvc[1];
+          m1[0] = m1[1] = 0;
+        } else {
+          const int tb = clip3i(-128, 127, env_.cur_poc - p0.poc);
+          const int tx = (16384 + std::abs(td / 2)) / td;
+          const int dsf = clip3i(-1024, 1023, (tb * tx + 32) >> 6);
+          for (int k = 0; k < 2; ++k) {
+            m0[k] = (dsf * mvc[k] + 128) >> 8;
+            m1[k] = m0[k] - mvc[k];
+          }
+        }
+        s.mv[0][blk][0] = i16(clip3i(-32768, 32767, m0[0]));
+        s.mv[0][blk][1] = i16(clip3i(-32768, 32767, m0[1]));
+        s.mv[1][blk][0] = i16(clip3i(-32768, 32767, m1[0]));
+        s.mv[1][blk][1] = i16(clip3i(-32768, 32767, m1[1]));
+      }
+      s.ref[0][b8] = i8(r0);
+      s.ref[1][b8] = 0;
+    }
+  }
+
+  // ------------------------------------------------------------------ weighted prediction
+  // WpEntry of an 8x8 partition with reference indices (r0, r1) (-1 = list unused).
+  WpEntry weights(int r0, int r1) {
+    WpEntry e{};
+    for (int c = 0; c < 3; ++c) {
+      e.w0[c] = e.w1[c] = 1;
+      e.o[c] = 0;
+      e.lwd[c] = 0;
+    }
+    if (implicit_) {
+      if (r0 < 0 || r1 < 0) return e;
+      const ListEntry& p0 = (*env_.list[0])[size_t(r0)];
+      const ListEntry& p1 = (*env_.list[1])[size_t(r1)];
+      int w0 = 32, w1 = 32;
+      const int td = clip3i(-128, 127, p1.poc - p0.poc);
+      if (td != 0 && !p0.long_term && !p1.long_term) {
+        const int tb = clip3i(-128, 127, env_.cur_poc - p0.poc);
+        const int tx = (16384 + std::abs(td / 2)) / td;
+        const int dsf = clip3i(-1024, 1023, (tb * tx + 32) >> 6);
+        if ((dsf >> 2) >= -64 && (dsf >> 2) <= 128) {
+          w1 = dsf >> 2;
+          w0 = 64 - w1;
+        }
+      }
+      for (int c = 0; c < 3; ++c) {
+        e.w0[c] = i16(w0);
+        e.w1[c] = i16(w1);
+        e.lwd[c] = 5;
+      }
+      return e;
+    }
+    // explicit
+    for (int c = 0; c < 3; ++c) e.lwd[c] = u8(c == 0 ? sh_.luma_lwd : sh_.chroma_lwd);
+    int o0[3] = {0, 0, 0}, o1[3] = {0, 0, 0};
+    if (r0 >= 0) {
+      const auto& w = sh_.wt[0][size_t(r0)];
+      for (int c = 0; c < 3; ++c) {
+        e.w0[c] = w.w[c];
+        o0[c] = w.o[c];
+      }
+    }
+    if (r1 >= 0) {
+      const auto& w = sh_.wt[1][size_t(r1)];
+      for (int c = 0; c < 3; ++c) {
+        e.w1[c] = w.w[c];
+        o1[c] = w.o[c];
+      }
+    }
+    for (int c = 0; c < 3; ++c)
+      e.o[c] = i16(r0 >= 0 && r1 >= 0 ? (o0[c] + o1[c] + 1) >> 1 : (r0 >= 0 ? o0[c] : o1[c]));
+    return e;
+  }
+
+  // ------------------------------------------------------------------ residual
+  // coded_block_flag context increments (§9.3.3.1.1.9).
+  int cbf_luma_inc(int mb, int blk, bool intra) {
+    auto cond = [&](int m, int nblk) -> int {
+      if (m < 0) return intra ? 1 : 0;
+      const MbState& n = nb_.at(m);
+      if (n.kind == kIPcm) return 1;
+      if (n.skip) return 0;
+      if (!((n.cbp >> raster_b8(nblk)) & 1)) return 0;
+      if (n.t8x8) return 1;
+      return (n.cbf >> nblk) & 1;
+    };
+    const int bx = blk & 3, by = blk >> 2;
+    const int a = bx > 0 ? cond(mb, blk - 1) : cond(nb_.mb_at(mb, -1, 0), blk + 3);
+    const int b = by > 0 ? cond(mb, blk - 4) : cond(nb_.mb_at(mb, 0, -1), blk + 12);
+    return a + 2 * b;
+  }
+  int cbf_dc_inc(int mb, int bit, bool intra) {  // bit 0 luma DC, 1 Cb DC, 2 Cr DC
+    auto cond = [&](int m) -> int {
+      if (m < 0) return intra ? 1 : 0;
+      const MbState& n = nb_.at(m);
+      if (n.kind == kIPcm) return 1;
+      if (bit == 0) return n.kind == kI16x16 ? (n.cbf_dc & 1) : 0;
+      if (n.skip || (n.cbp >> 4) == 0) return 0;
+      return (n.cbf_dc >> bit) & 1;
+    };
+    return cond(nb_.mb_at(mb, -1, 0)) + 2 * cond(nb_.mb_at(mb, 0, -1));
+  }
+  int cbf_cac_inc(int mb, int c, int b, bool intra) {
+    auto cond = [&](int m, int nb2, bool cur) -> int {
+      if (cur) return (nb_.at(mb).cbf_cac[c] >> nb2) & 1;
+      if (m < 0) return intra ? 1 : 0;
+      const MbState& n = nb_.at(m);
+      if (n.kind == kIPcm) return 1;
+      if (n.skip || (n.cbp >> 4) != 2) return 0;
+      return (n.cbf_cac[c] >> nb2) & 1;
+    };
+    const int bx = b & 1, by = b >> 1;
+    const int a = bx ? cond(mb, b - 1, true) : cond(nb_.mb_at(mb, -1, 0), b + 1, false);
+    const int bb = by ? cond(mb, b - 2, true) : cond(nb_.mb_at(mb, 0, -1), b + 2, false);
+    return a + 2 * bb;
+  }
+
+  // One residual block's levels (scan order) into lv[0..n-1]; returns TotalCoeff.
+  int read_block(int cat, int cbf_inc, int nc, int n, int* lv) {
+    std::memset(lv, 0, size_t(n) * sizeof(int));
+    if constexpr (kCabac) {
+      (void)nc;
+      return bins->residual(cat, cbf_inc, n, lv);
+    } else {
+      (void)cat;
+      (void)cbf_inc;
+      return read_residual_block_cb(*br, nc, n, [lv](int k, int l) { lv[k] = l; });
+    }
+  }
+
+  void residual(int mb, MbState& s, MbResidual& res, int cbp_luma, int cbp_chroma, int qp, bool intra) {
+    const int ly = intra ? 0 : 3;
+    const int q6 = qp / 6, qm = qp % 6;
+    int lv[64];
+    if (s.kind == kI16x16) {
+      const int inc = kCabac ? cbf_dc_inc(mb, 0, true) : 0;
+      const int nc = kCabac ? 0 : nb_.nc_luma(mb, 0);
+      int dcy[16] = {};
+      if (read_block(kCatLumaDc, inc, nc, 16, lv) > 0) {
+        s.cbf_dc |= 1;
+        int c[16];
+        for (int k = 0; k < 16; ++k) c[kZigzag4x4[k]] = lv[k];
+        hadamard4x4(c);
+        const int ls = dq_.ls4[ly][qm][0];
+        for (int k = 0; k < 16; ++k)
+          dcy[k] = qp >= 36 ? c[k] * ls * (1 << (q6 - 6)) : (c[k] * ls + (1 << (5 - q6))) >> (6 - q6);
+      }
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        i16* d = res.blk[r];
+        bool nz = dcy[r] != 0;
+        int tc = 0;
+        std::memset(d, 0, 16 * sizeof(i16));
+        d[0] = sat16(dcy[r]);
+        if (cbp_luma) {
+          const int binc = kCabac ? cbf_luma_inc(mb, r, true) : 0;
+          const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
+          tc = read_block(kCatLumaAc, binc, bnc, 15, lv);
+          for (int k = 0; k < 15; ++k) {
+            if (!lv[k]) continue;
+            const int pos = kZigzag4x4[k + 1];
+            const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
+            d[pos] = sat16(v);
+            nz |= v != 0;
+          }
+          s.tc[r] = u8(tc);
+          if (tc) s.cbf |= u16(1u << r);
+        }
+        if (nz) res.luma |= u16(1u << r);
+      }
+    } else if (s.t8x8) {
+      res.t8 = true;
+      const int l8 = intra ? 0 : 1;
+      for (int b8 = 0; b8 < 4; ++b8) {
+        if (!((cbp_luma >> b8) & 1)) continue;
+        int c64[64] = {};
+        int total = 0;
+        if constexpr (kCabac) {
+          total = read_block(kCatLuma8x8, -1, 0, 64, c64);
+          for (u16 w = b8_blocks(b8); w; w &= w - 1) s.tc[__builtin_ctz(w)] = u8(std::min(total, 16));
+        } else {
+          for (int i4 = 0; i4 < 4; ++i4) {
+            const int r = blk_to_raster(b8 * 4 + i4);
+            const int tc = read_block(kCatLuma4x4, 0, nb_.nc_luma(mb, r), 16, lv);
+            s.tc[r] = u8(tc);
+            total += tc;
+            for (int k = 0; k < 16; ++k) c64[4 * k + i4] = lv[k];
+          }
+        }
+        i16* d = res.b8[b8];
+        std::memset(d, 0, 64 * sizeof(i16));
+        bool nz = false;
+        for (int k = 0; k < 64; ++k) {
+          if (!c64[k]) continue;
+          const int pos = kZigzag8x8[k];
+          const int v = scale8(c64[k], dq_.ls8[l8][qm][pos], qp);
+          d[pos] = sat16(v);
+          nz |= v != 0;
+        }
+        if (total) {
+          s.cbf |= b8_blocks(b8);
+          nz8_ |= b8_blocks(b8);
+        }
+        if (nz) res.luma |= b8_blocks(b8);
+      }
+    } else {
+      for (int idx = 0; idx < 16; ++idx) {
+        const int r = blk_to_raster(idx);
+        if (!((cbp_luma >> (idx >> 2)) & 1)) continue;
+        const int binc = kCabac ? cbf_luma_inc(mb, r, intra) : 0;
+        const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
+        const int tc = read_block(kCatLuma4x4, binc, bnc, 16, lv);
+        s.tc[r] = u8(tc);
+        if (tc) s.cbf |= u16(1u << r);
+        if (!tc) continue;
+        i16* d = res.blk[r];
+        std::memset(d, 0, 16 * sizeof(i16));
+        bool nz = false;
+        for (int k = 0; k < 16; ++k) {
+          if (!lv[k]) continue;
+          const int pos = kZigzag4x4[k];
+          const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
+          d[pos] = sat16(v);
+          nz |= v != 0;
+        }
+        if (nz) res.luma |= u16(1u << r);
+      }
+    }
+    if (cbp_chroma) {
+      const int qpc[2] = {chroma_qp(qp, pps_.chroma_qp_index_offset),
+                          chroma_qp(qp, pps_.second_chroma_qp_index_offset)};
+      int dcv[2][4] = {};
+      for (int c = 0; c < 2; ++c) {
+        const int inc = kCabac ? cbf_dc_inc(mb, 1 + c, intra) : 0;
+        int v4[4];
+        if (read_block(kCatChromaDc, inc, -1, 4, v4) > 0) {
+          s.cbf_dc |= u8(2 << c);
+          const int f[4] = {v4[0] + v4[1] + v4[2] + v4[3], v4[0] - v4[1] + v4[2] - v4[3],
+                            v4[0] + v4[1] - v4[2] - v4[3], v4[0] - v4[1] - v4[2] + v4[3]};
+          const int ls = dq_.ls4[ly + 1 + c][qpc[c] % 6][0];
+          for (int b = 0; b < 4; ++b) dcv[c][b] = ((f[b] * ls) * (1 << (qpc[c] / 6))) >> 5;
+        }
+      }
+      for (int c = 0; c < 2; ++c) {
+        const int lc = ly + 1 + c;
+        for (int b = 0; b < 4; ++b) {
+          i16* d = res.blk[16 + c * 4 + b];
+          bool nz = dcv[c][b] != 0;
+          std::memset(d, 0, 16 * sizeof(i16));
+          d[0] = sat16(dcv[c][b]);
+          if (cbp_chroma & 2) {
+            const int binc = kCabac ? cbf_cac_inc(mb, c, b, intra) : 0;
+            const int bnc = kCabac ? 0 : nb_.nc_chroma(mb, c, b);
+            const int tc = read_block(kCatChromaAc, binc, bnc, 15, lv);
+            s.tcc[c][b] = u8(tc);
+            if (tc) s.cbf_cac[c] |= u8(1u << b);
+            for (int k = 0; k < 15; ++k) {
+              if (!lv[k]) continue;
+              const int pos = kZigzag4x4[k + 1];
+              const int v = scale4(lv[k], dq_.ls4[lc][qpc[c] % 6][pos], qpc[c]);
+              d[pos] = sat16(v);
+              nz |= v != 0;
+            }
+          }
+          if (nz) res.chroma |= u8(1u << (c * 4 + b));
+        }
+      }
+    }
+    if constexpr (!kCabac) VEP_CHECK(!br->overrun(), "slice data overrun");
+  }
+
+  // ------------------------------------------------------------------ MbRec
+  void emit(int mb, const MbState& s, const MbResidual& res, int i16_mode, int chroma_mode, const u8* pcm) {
+    MbRec m{};
+    m.kind = s.kind;
+    m.qp = s.kind == kIPcm ? 0 : s.qp;
+    m.qpc = u8(chroma_qp(m.qp, pps_.chroma_qp_index_offset));
+    m.qpc2 = u8(chroma_qp(m.qp, pps_.second_chroma_qp_index_offset));
+    m.i16_mode = u8(i16_mode);
+    m.chroma_mode = u8(chroma_mode);
+    m.dbk = u8((sh_.disable_deblocking == 1 ? 1 : 0) | (sh_.disable_deblocking == 2 ? 2 : 0));
+    m.alpha_off = i8(sh_.alpha_off);
+    m.beta_off = i8(sh_.beta_off);
+    m.slice = s.slice;
+    m.flags = s.t8x8 && s.kind != kI8x8 ? kMbT8x8 : 0;
+    if (s.kind == kI8x8) m.flags = kMbT8x8;
+    bool l1 = false;
+    for (int k = 0; k < 4; ++k) {
+      m.ref[k] = u8(0xFF);
+      m.ref1[k] = u8(0xFF);
+      if (is_intra(s.kind)) continue;
+      if (s.ref[0][k] >= 0) m.ref[k] = u8((*env_.list[0])[size_t(s.ref[0][k])].slot);
+      if (s.ref[1][k] >= 0) {
+        m.ref1[k] = u8((*env_.list[1])[size_t(s.ref[1][k])].slot);
+        l1 = true;
+      }
+    }
+    if (l1) m.flags |= kMbL1;
+    // deblocking bS 2: 4x4 blocks with coefficients (8x8 transform: all blocks of the 8x8)
+    u16 nz = 0;
+    if (s.t8x8) {
+      nz = nz8_;
+      if (!kCabac)
+        for (int b8 = 0; b8 < 4; ++b8) {
+          bool any = false;
+          for (u16 w = b8_blocks(b8); w; w &= w - 1) any |= s.tc[__builtin_ctz(w)] != 0;
+          if (any) nz |= b8_blocks(b8);
+        }
+    } else {
+      for (int r = 0; r < 16; ++r) nz |= u16(s.tc[r] ? 1u << r : 0u);
+    }
+    nz8_ = 0;
+    m.nz = nz;
+    if (s.kind == kI4x4)
+      for (int r = 0; r < 16; ++r) m.i4[r >> 1] |= u8(s.i4[r] << ((r & 1) * 4));
+    if (s.kind == kI8x8)
+      for (int b8 = 0; b8 < 4; ++b8) m.i4[b8 >> 1] |= u8(s.i4[(b8 & 1) * 2 + (b8 >> 1) * 8] << ((b8 & 1) * 4));
+    WpEntry wp[4];
+    bool use_wp = false;
+    if (weighted_ && !is_intra(s.kind)) {
+      for (int k = 0; k < 4; ++k) {
+        wp[k] = weights(s.ref[0][k], s.ref[1][k]);
+        const WpEntry& e = wp[k];
+        for (int c = 0; c < 3; ++c)
+          use_wp |= !(e.lwd[c] == 0 && e.w0[c] == 1 && e.w1[c] == 1 && e.o[c] == 0) &&
+                    !(e.w0[c] == (1 << e.lwd[c]) && e.w1[c] == (1 << e.lwd[c]) && e.o[c] == 0);
+      }
+      if (use_wp) m.flags |= kMbWp;
+    }
+    store_mb(pic_, mb, m, s, &res, pcm, use_wp ? wp : nullptr);
+  }
+
+  MbNeighbours& nb_;
+  Picture& pic_;
+  const SliceEnv& env_;
+  const SliceHdr& sh_;
+  const h264::Pps& pps_;
+  const h264::Sps& sps_;
+  const Dequant& dq_;
+  int type_ = 0;
+  int qp_ = 26;
+  bool weighted_ = false, implicit_ = false;
+  u16 nz8_ = 0;  // CABAC 8x8 blocks with coefficients (current MB)
+};
+
+}  // namespace
+
+void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const u8* data, size_t n,
+                          size_t bitpos) {
+  const SliceHdr& sh = *env.sh;
+  const Dequant dq(env.scaling);
+  const int total = pic.nmbs();
+  int mb = sh.first_mb;
+  VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
+  if (env.pps->cabac) {
+    if (sh.type() != h264::kI && sh.cabac_init_idc != 0)
+      throw UnsupportedStream("CABAC cabac_init_idc " + std::to_string(sh.cabac_init_idc) + " is not supported");
+    const size_t start = (bitpos + 7) >> 3;  // cabac_alignment_one_bit
+    VEP_CHECK(start <= n, "slice data overrun");
+    cabac::Ctx ctx[kCabacCtx];
+    cabac_init_contexts(ctx, sh.type() == h264::kI ? -1 : 0, sh.qp);
+    cabac::Decoder dec(data, n, start);
+    BinDecoder bd{dec, ctx};
+    AvcBins<BinDecoder> bins{bd};
+    MbLayer<true> L(nb, pic, env, dq);
+    L.bins = &bins;
+    L.cabac = &dec;
+    L.data = data;
+    L.data_n = n;
+    for (;;) {
+      VEP_CHECK(mb < total, "macroblock address past end of picture");
+      if (sh.type() != h264::kI && L.read_skip_flag(mb)) L.skip_mb(mb, false);
+      else L.coded_mb(mb, sh.type() == h264::kI);
+      ++mb;
+      if (bins.end_of_slice(false)) break;
+      VEP_CHECK(dec.bitpos() <= n * 8 + 16, "slice data overrun");
+    }
+    return;
+  }
+  Bits br(data, n, bitpos);
+  const size_t stop = BitReader(data, n).stop_bit_pos();
+  MbLayer<false> L(nb, pic, env, dq);
+  L.br = &br;
+  bool more = true;
+  while (more) {
+    if (sh.type() != h264::kI) {
+      const u32 run = br.ue();
+      VEP_CHECK(u32(total - mb) >= run, "mb_skip_run past end of picture");
+      for (u32 k = 0; k < run; ++k) L.skip_mb(mb++, true);
+      if (run > 0) {
+        more = br.pos() < stop;
+        if (!more) break;
+      }
+    }
+    VEP_CHECK(mb < total, "macroblock address past end of picture");
+    L.coded_mb(mb, true);
+    VEP_CHECK(!br.overrun(), "slice data overrun");
+    more = br.pos() < stop;
+    ++mb;
+  }
+}
+
+}  // namespace vep::avc

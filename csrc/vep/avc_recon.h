@@ -34,34 +34,84 @@ using i16 = int16_t;
 using i8 = int8_t;
 
 // ------------------------------------------------------------------------------ MB records
-// One macroblock of a parsed picture, as shipped to the GPU (48 bytes).
-enum MbKind : u8 { kSkip = 0, kInter = 1, kI4x4 = 2, kI16x16 = 3, kIPcm = 4 };
+// One macroblock of a parsed picture, as shipped to the GPU (56 bytes).
+enum MbKind : u8 { kSkip = 0, kInter = 1, kI4x4 = 2, kI16x16 = 3, kIPcm = 4, kI8x8 = 5 };
 VEP_HD bool is_intra(u8 k) { return k >= kI4x4; }
+// intra MBs reconstructed by the wavefront (prediction from reconstructed neighbours)
+VEP_HD bool is_wave_intra(u8 k) { return k == kI4x4 || k == kI16x16 || k == kI8x8; }
+
+// MbRec::flags
+constexpr u8 kMbT8x8 = 1;  // luma residual in 8x8 transform blocks (4 pool blocks each: 64
+                           // coefficients, raster 8x8); deblocking skips internal 4x4 edges
+constexpr u8 kMbL1 = 2;    // list-1 motion present: 32 more mv entries follow the list-0 ones
+constexpr u8 kMbWp = 4;    // weighted prediction: MbRec::wp names 4 WpEntry (one per 8x8)
 
 struct MbRec {
   u8 kind;          // MbKind
   u8 qp;            // QP_Y (0 for I_PCM)
-  u8 qpc;           // QP_C of QP_Y (chroma_qp_index_offset applied)
+  u8 qpc;           // QP_C of Cb (chroma_qp_index_offset applied)
+  u8 qpc2;          // QP_C of Cr (second_chroma_qp_index_offset applied)
   u8 i16_mode;      // Intra16x16PredMode
   u8 chroma_mode;   // intra_chroma_pred_mode
   u8 dbk;           // deblocking: bit0 filter disabled (idc 1), bit1 slice-edge mode (idc 2)
+  u8 flags;         // kMbT8x8 | kMbL1 | kMbWp
+  u16 nz;           // luma 4x4 blocks (raster) with non-zero coefficients (deblocking bS 2; for
+                    // 8x8-transform MBs all four blocks of a coded 8x8)
+  u16 luma_coded;   // luma 4x4 blocks (raster) with residual samples to add (8x8 transform: all
+                    // four blocks of a coded 8x8 set)
   i8 alpha_off;     // FilterOffsetA
   i8 beta_off;      // FilterOffsetB
-  u16 nz;           // luma 4x4 blocks (raster) with total_coeff != 0 (deblocking bS 2)
-  u16 luma_coded;   // luma 4x4 blocks (raster) with residual samples to add
+  u16 slice;        // slice index within the picture (neighbour availability); bytes 14..15
   u8 chroma_coded;  // bits 0-3 Cb, 4-7 Cr 4x4 blocks (raster) with residual
   u8 pad0;
-  u16 slice;        // slice index within the picture (neighbour availability)
-  u8 ref[4];        // per 8x8 (raster): DPB slot of the reference picture (0xFF = none)
+  u16 pad1;
+  u8 ref[4];        // per 8x8 (raster): DPB slot of the list-0 reference picture (0xFF = none)
+  u8 ref1[4];       // per 8x8: DPB slot of the list-1 reference picture (0xFF = none)
   u32 coef;         // first 16-coefficient block in the picture's coefficient pool (I_PCM:
                     // 384 raw sample bytes = 12 blocks)
-  u32 mv;           // first of 16 (x, y) motion vectors (raster 4x4) in the mv pool
-  u8 i4[8];         // Intra4x4PredMode per raster 4x4 block, 4 bits each (low nibble first)
+  u32 mv;           // first of 16 (x, y) motion vectors (raster 4x4) in the mv pool (units of
+                    // 32 i16); kMbL1: the list-1 vectors are the next unit
+  u8 i4[8];         // Intra4x4PredMode per raster 4x4 block / Intra8x8PredMode per raster 8x8
+                    // block (nibbles 0..3), 4 bits each (low nibble first)
   u32 res;          // intra MBs with residual: slot of their 384 residual samples (GPU scratch,
                     // filled by the parallel pass); kNoRes otherwise
+  u32 wp;           // kMbWp: first of 4 WpEntry in the picture's weight pool
+  u32 pad2;
 };
-static_assert(sizeof(MbRec) == 40, "MbRec layout");
+static_assert(sizeof(MbRec) == 56, "MbRec layout");
 constexpr u32 kNoRes = 0xFFFFFFFFu;
+
+// Weighted sample prediction of one 8x8 partition (§8.4.2.3), per component (Y, Cb, Cr):
+// explicit (pred_weight_table) or implicit (POC distances) weights resolved on the host.
+struct WpEntry {
+  i16 w0[3], w1[3];  // list-0 / list-1 weights
+  i16 o[3];          // single-list: that list's offset; bi-prediction: (o0 + o1 + 1) >> 1
+  u8 lwd[3];         // logWD
+  u8 pad[11];
+};
+static_assert(sizeof(WpEntry) == 32, "WpEntry layout");
+
+// Final prediction sample from the list-0 / list-1 predictions (§8.4.2.3.1 default, §8.4.2.3.2
+// weighted); c = component.
+VEP_HD int wp_sample(int p0, int p1, bool has0, bool has1, const WpEntry* w, int c) {
+  if (!w) return has0 && has1 ? (p0 + p1 + 1) >> 1 : (has0 ? p0 : p1);
+  const int lwd = w->lwd[c];
+  if (has0 && has1) {
+    const int v = ((p0 * w->w0[c] + p1 * w->w1[c] + (1 << lwd)) >> (lwd + 1)) + w->o[c];
+    return v < 0 ? 0 : (v > 255 ? 255 : v);
+  }
+  const int p = has0 ? p0 : p1, ww = has0 ? w->w0[c] : w->w1[c];
+  const int v = lwd >= 1 ? ((p * ww + (1 << (lwd - 1))) >> lwd) + w->o[c] : p * ww + w->o[c];
+  return v < 0 ? 0 : (v > 255 ? 255 : v);
+}
+
+// Pool block index of 8x8 luma block q (raster 8x8) of an 8x8-transform MB: its four blocks are
+// contiguous (64 coefficients, raster 8x8), coded 8x8s in raster order.
+VEP_HD u32 luma8_block_index(const MbRec& m, int q) {
+  const u32 lc = m.luma_coded;
+  const u32 qm = (lc & 1u) | ((lc >> 1) & 2u) | ((lc >> 6) & 4u) | ((lc >> 7) & 8u);
+  return m.coef + 4u * u32(__builtin_popcount(qm & ((1u << q) - 1u)));
+}
 
 VEP_HD int i4_mode(const MbRec& m, int blk) { return (m.i4[blk >> 1] >> ((blk & 1) * 4)) & 15; }
 
@@ -167,6 +217,163 @@ VEP_HD int idct4x4_at(const i16* d, int i, int j) {
   const int g0 = f[0] + f[2], g1 = f[0] - f[2], g2 = (f[1] >> 1) - f[3], g3 = f[1] + (f[3] >> 1);
   const int h = i == 0 ? g0 + g3 : i == 1 ? g1 + g2 : i == 2 ? g1 - g2 : g0 - g3;
   return (h + 32) >> 6;
+}
+
+// 8x8 zig-zag scan (frame macroblocks): scan index -> raster position (row * 8 + column).
+VEP_CONST static const u8 kZigzag8x8[64] = {
+    0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
+    41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
+    30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
+
+// normAdjust8x8 (§8.5.13.1): v[m][class] with the six position classes below.
+VEP_CONST static const u8 kNormAdjust8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26},
+                                                {26, 23, 42, 24, 33, 31}, {28, 25, 45, 26, 35, 33},
+                                                {32, 28, 51, 30, 40, 38}, {36, 32, 58, 34, 46, 43}};
+VEP_HD int norm_adjust8(int m, int i, int j) {
+  int cls;
+  if ((i & 3) == 0 && (j & 3) == 0) cls = 0;
+  else if ((i & 1) && (j & 1)) cls = 1;
+  else if ((i & 3) == 2 && (j & 3) == 2) cls = 2;
+  else if (((i & 3) == 0 && (j & 1)) || ((i & 1) && (j & 3) == 0)) cls = 3;
+  else if (((i & 3) == 0 && (j & 3) == 2) || ((i & 3) == 2 && (j & 3) == 0)) cls = 4;
+  else cls = 5;
+  return kNormAdjust8[m][cls];
+}
+
+// One 8-point inverse transform butterfly (§8.5.13.2), in place on x[0..7].
+VEP_HD void idct8_1d(int* x) {
+  const int a0 = x[0] + x[4], a4 = x[0] - x[4];
+  const int a2 = (x[2] >> 1) - x[6], a6 = x[2] + (x[6] >> 1);
+  const int b0 = a0 + a6, b2 = a4 + a2, b4 = a4 - a2, b6 = a0 - a6;
+  const int a1 = -x[3] + x[5] - x[7] - (x[7] >> 1);
+  const int a3 = x[1] + x[7] - x[3] - (x[3] >> 1);
+  const int a5 = -x[1] + x[7] + x[5] + (x[5] >> 1);
+  const int a7 = x[3] + x[5] + x[1] + (x[1] >> 1);
+  const int b1 = a1 + (a7 >> 2), b7 = a7 - (a1 >> 2), b3 = a3 + (a5 >> 2), b5 = (a3 >> 2) - a5;
+  x[0] = b0 + b7;
+  x[1] = b2 + b5;
+  x[2] = b4 + b3;
+  x[3] = b6 + b1;
+  x[4] = b6 - b1;
+  x[5] = b4 - b3;
+  x[6] = b2 - b5;
+  x[7] = b0 - b7;
+}
+
+// Inverse 8x8 transform of one block (d raster 8x8); r receives (h + 32) >> 6.
+VEP_HD void idct8x8(const i16* d, int* r) {
+  int t[64];
+  for (int i = 0; i < 8; ++i) {
+    int x[8];
+    for (int k = 0; k < 8; ++k) x[k] = d[i * 8 + k];
+    idct8_1d(x);
+    for (int k = 0; k < 8; ++k) t[i * 8 + k] = x[k];
+  }
+  for (int j = 0; j < 8; ++j) {
+    int x[8];
+    for (int k = 0; k < 8; ++k) x[k] = t[k * 8 + j];
+    idct8_1d(x);
+    for (int k = 0; k < 8; ++k) r[k * 8 + j] = (x[k] + 32) >> 6;
+  }
+}
+
+// ------------------------------------------------------------------------------ intra 8x8
+// Reference sample filtering (§8.3.2.2.1). Inputs (after the top-right substitution of
+// §8.3.2.2): T(x) = p[x, -1] for x in -1..15, L(y) = p[-1, y] for y in 0..7. Output
+// f[0] = p'[-1,-1], f[1 + x] = p'[x,-1] (x 0..15), f[17 + y] = p'[-1,y] (y 0..7).
+// One filtered reference sample: k = 0 -> p'[-1,-1], 1..16 -> p'[k-1,-1], 17..24 -> p'[-1,k-17]
+// (128 where the side is unavailable; such samples are never used by a prediction mode).
+template <class TF, class LF>
+VEP_HD int intra8x8_filter_at(TF T, LF L, bool has_top, bool has_left, bool has_tl, int k) {
+  if (k == 0) {
+    if (!has_tl) return 128;
+    if (has_top && has_left) return (T(0) + 2 * T(-1) + L(0) + 2) >> 2;
+    if (has_top) return (3 * T(-1) + T(0) + 2) >> 2;
+    if (has_left) return (3 * T(-1) + L(0) + 2) >> 2;
+    return T(-1);
+  }
+  if (k <= 16) {
+    if (!has_top) return 128;
+    const int x = k - 1;
+    if (x == 0) return has_tl ? (T(-1) + 2 * T(0) + T(1) + 2) >> 2 : (3 * T(0) + T(1) + 2) >> 2;
+    if (x == 15) return (T(14) + 3 * T(15) + 2) >> 2;
+    return (T(x - 1) + 2 * T(x) + T(x + 1) + 2) >> 2;
+  }
+  if (!has_left) return 128;
+  const int y = k - 17;
+  if (y == 0) return has_tl ? (T(-1) + 2 * L(0) + L(1) + 2) >> 2 : (3 * L(0) + L(1) + 2) >> 2;
+  if (y == 7) return (L(6) + 3 * L(7) + 2) >> 2;
+  return (L(y - 1) + 2 * L(y) + L(y + 1) + 2) >> 2;
+}
+
+// Reference sample filtering (§8.3.2.2.1). Inputs (after the top-right substitution of
+// §8.3.2.2): T(x) = p[x, -1] for x in -1..15, L(y) = p[-1, y] for y in 0..7. Output
+// f[0] = p'[-1,-1], f[1 + x] = p'[x,-1] (x 0..15), f[17 + y] = p'[-1,y] (y 0..7).
+template <class TF, class LF>
+VEP_HD void intra8x8_filter(TF T, LF L, bool has_top, bool has_left, bool has_tl, int* f) {
+  for (int k = 0; k < 25; ++k) f[k] = intra8x8_filter_at(T, L, has_top, has_left, has_tl, k);
+}
+
+// Intra_8x8 sample prediction (§8.3.2.2.2 - 8.3.2.2.10) from the filtered references.
+// Generic: T(x) = p'[x,-1] for x in -1..15, L(y) = p'[-1,y] for y in -1..7 (L(-1) = T(-1)).
+template <class TF, class LF>
+VEP_HD int intra8x8_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, int x, int y) {
+  switch (mode) {
+    case 0: return T(x);
+    case 1: return L(y);
+    case 2: {
+      int s = 0;
+      if (has_top && has_left) {
+        for (int k = 0; k < 8; ++k) s += T(k) + L(k);
+        return (s + 8) >> 4;
+      }
+      if (has_left) {
+        for (int k = 0; k < 8; ++k) s += L(k);
+        return (s + 4) >> 3;
+      }
+      if (has_top) {
+        for (int k = 0; k < 8; ++k) s += T(k);
+        return (s + 4) >> 3;
+      }
+      return 128;
+    }
+    case 3:
+      if (x == 7 && y == 7) return (T(14) + 3 * T(15) + 2) >> 2;
+      return (T(x + y) + 2 * T(x + y + 1) + T(x + y + 2) + 2) >> 2;
+    case 4:
+      if (x > y) return (T(x - y - 2) + 2 * T(x - y - 1) + T(x - y) + 2) >> 2;
+      if (x < y) return (L(y - x - 2) + 2 * L(y - x - 1) + L(y - x) + 2) >> 2;
+      return (T(0) + 2 * T(-1) + L(0) + 2) >> 2;
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0 && (z & 1) == 0) return (T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 1) >> 1;
+      if (z >= 0) return (T(x - (y >> 1) - 2) + 2 * T(x - (y >> 1) - 1) + T(x - (y >> 1)) + 2) >> 2;
+      if (z == -1) return (L(0) + 2 * L(-1) + T(0) + 2) >> 2;
+      return (L(y - 2 * x - 1) + 2 * L(y - 2 * x - 2) + L(y - 2 * x - 3) + 2) >> 2;
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0 && (z & 1) == 0) return (L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 1) >> 1;
+      if (z >= 0) return (L(y - (x >> 1) - 2) + 2 * L(y - (x >> 1) - 1) + L(y - (x >> 1)) + 2) >> 2;
+      if (z == -1) return (L(0) + 2 * L(-1) + T(0) + 2) >> 2;
+      return (T(x - 2 * y - 1) + 2 * T(x - 2 * y - 2) + T(x - 2 * y - 3) + 2) >> 2;
+    }
+    case 7:
+      if ((y & 1) == 0) return (T(x + (y >> 1)) + T(x + (y >> 1) + 1) + 1) >> 1;
+      return (T(x + (y >> 1)) + 2 * T(x + (y >> 1) + 1) + T(x + (y >> 1) + 2) + 2) >> 2;
+    default: {  // 8: Horizontal_Up
+      const int z = x + 2 * y;
+      if (z > 13) return L(7);
+      if (z == 13) return (L(6) + 3 * L(7) + 2) >> 2;
+      if ((z & 1) == 0) return (L(y + (x >> 1)) + L(y + (x >> 1) + 1) + 1) >> 1;
+      return (L(y + (x >> 1)) + 2 * L(y + (x >> 1) + 1) + L(y + (x >> 1) + 2) + 2) >> 2;
+    }
+  }
+}
+
+VEP_HD int intra8x8_pred(const int* f, bool has_top, bool has_left, int mode, int x, int y) {
+  return intra8x8_pred_g([&](int xx) { return f[1 + xx]; }, [&](int yy) { return yy < 0 ? f[0] : f[17 + yy]; },
+                         has_top, has_left, mode, x, y);
 }
 
 // ------------------------------------------------------------------------------ intra 4x4
@@ -538,17 +745,36 @@ VEP_HD int chroma_epel(const u8* uv, int pitch, int w, int h, int c, int xi, int
 
 // ------------------------------------------------------------------------------ deblocking
 // Boundary strength of the edge between 4x4 luma blocks P (in MB mp, raster block bp) and Q (in
-// MB mq, block bq) (§8.7.2.1, frame macroblocks, no 8x8 transform). mv_p / mv_q point at the
-// blocks' (x, y) motion vectors.
+// MB mq, block bq) (§8.7.2.1, frame macroblocks). mv_p / mv_q point at the MBs' motion vector
+// units (list 0 at [0..31], list 1 at [32..63] when kMbL1); nullptr for intra MBs. Reference
+// pictures are compared by DPB slot (= picture identity within one picture's decode), so a
+// picture reached through list 0 and list 1 counts as the same picture.
+VEP_HD bool mv_far(const i16* a, const i16* b) { return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= 4; }
 VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
                              const i16* mv_q, bool mb_edge) {
   if (is_intra(mp.kind) || is_intra(mq.kind)) return mb_edge ? 4 : 3;
   if (((mp.nz >> bp) & 1) || ((mq.nz >> bq) & 1)) return 2;
-  const int rp = mp.ref[((bp >> 3) << 1) | ((bp & 3) >> 1)];
-  const int rq = mq.ref[((bq >> 3) << 1) | ((bq & 3) >> 1)];
-  if (rp != rq) return 1;
-  if (iabs(mv_p[0] - mv_q[0]) >= 4 || iabs(mv_p[1] - mv_q[1]) >= 4) return 1;
-  return 0;
+  const int p8 = ((bp >> 3) << 1) | ((bp & 3) >> 1), q8 = ((bq >> 3) << 1) | ((bq & 3) >> 1);
+  const int p0 = mp.ref[p8], p1 = (mp.flags & kMbL1) ? mp.ref1[p8] : 0xFF;
+  const int q0 = mq.ref[q8], q1 = (mq.flags & kMbL1) ? mq.ref1[q8] : 0xFF;
+  const int np = (p0 != 0xFF) + (p1 != 0xFF), nq = (q0 != 0xFF) + (q1 != 0xFF);
+  if (np != nq) return 1;
+  const i16* pa = mv_p + 2 * bp;        // list 0 of P
+  const i16* pb = mv_p + 32 + 2 * bp;   // list 1 of P (valid when p1 used)
+  const i16* qa = mv_q + 2 * bq;
+  const i16* qb = mv_q + 32 + 2 * bq;
+  if (np == 1) {
+    const int rp = p0 != 0xFF ? p0 : p1, rq = q0 != 0xFF ? q0 : q1;
+    if (rp != rq) return 1;
+    return mv_far(p0 != 0xFF ? pa : pb, q0 != 0xFF ? qa : qb) ? 1 : 0;
+  }
+  if (!((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))) return 1;
+  if (p0 != p1) {  // two different reference pictures: compare the vectors of the same picture
+    if (p0 == q0) return (mv_far(pa, qa) || mv_far(pb, qb)) ? 1 : 0;
+    return (mv_far(pa, qb) || mv_far(pb, qa)) ? 1 : 0;
+  }
+  // both vectors of both blocks reference the same picture
+  return ((mv_far(pa, qa) || mv_far(pb, qb)) && (mv_far(pa, qb) || mv_far(pb, qa))) ? 1 : 0;
 }
 
 struct EdgeParams {

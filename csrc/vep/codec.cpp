@@ -269,7 +269,11 @@ PictureInfo H264Parser::parse(const AccessUnit& au, MbUpdate& upd) {
     if (sit == sps_.end()) throw UnsupportedStream("slice references unknown SPS");
     const Sps& sps = sit->second;
     const Pps& pps = pit->second;
-    if (pps.cabac) throw UnsupportedStream("CABAC streams need the RocDecode backend");
+    // anything beyond the I_PCM / P_Skip subset goes to the general decoder (avc.h)
+    if (pps.cabac) throw UnsupportedStream("CABAC slices (general decoder)");
+    if (pps.transform_8x8_mode || sps.scaling_matrix_present || pps.scaling_matrix_present)
+      throw UnsupportedStream("High-profile tools (general decoder)");
+    if (!sps.frame_mbs_only) throw UnsupportedStream("interlaced H.264 is not supported");
     if (sps.chroma_format_idc != 1 || sps.bit_depth_luma != 8 || sps.bit_depth_chroma != 8)
       throw UnsupportedStream("only 8-bit 4:2:0 is supported");
     active_sps_id_ = sps.sps_id;

@@ -79,7 +79,8 @@ void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s);
 struct AvcDesc {
   const void* mbs;     // avc::MbRec[wmbs * hmbs]
   const i16* coefs;    // dequantised 4x4 blocks (16 x i16) / I_PCM samples
-  const i16* mvs;      // 32 x i16 per inter MB
+  const i16* mvs;      // 32 x i16 per list per inter MB
+  const void* wps;     // avc::WpEntry pool (weighted prediction)
   u8* y;
   u8* uv;
   u64 slot_y, slot_uv;
@@ -106,12 +107,12 @@ constexpr int kAvcResSamples = 384;
 // Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.
 struct AvcDbkInfo {
   u32 bs[4];      // 32 x 4-bit bS: nibble dir * 16 + edge * 4 + segment (0 = edge not filtered)
-  u8 alpha[6], beta[6];  // [left, top, internal] luma, then [left, top, internal] chroma
-  u8 tc0[6][3];   // tC0 for bS 1..3, same edge order
+  u8 alpha[9], beta[9];  // [left, top, internal] for luma, Cb, Cr (component * 3 + edge kind)
+  u8 tc0[9][3];   // tC0 for bS 1..3, same order
   u8 any;         // any bS != 0
   u8 pad[1];
 };
-static_assert(sizeof(AvcDbkInfo) == 48, "AvcDbkInfo layout");
+static_assert(sizeof(AvcDbkInfo) == 64, "AvcDbkInfo layout");
 // The deblocking wavefront runs kAvcDbkWgRows MB rows per workgroup (two per wave64), several
 // workgroups per picture; a workgroup's last row hands its final bottom samples to the next
 // workgroup through `xg`: 16 luma + 8 NV12 chroma u32 words per MB, each tagged (high half) with

@@ -49,16 +49,62 @@ __device__ inline const i16* chroma_block(const AvcDesc& d, const MbRec& m, int 
                           u32(__popc(m.chroma_coded & ((1u << k) - 1)))) * 16;
 }
 
+// wave-local barrier (one wave64 per "group" here: LDS ordering + compiler fence)
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 // --------------------------------------------------------------------------------- inter
+
+// Luma residual of an 8x8-transform MB, whole wave: the four 8x8 inverse transforms as 32 row
+// butterflies then 32 column butterflies (lanes 0-31, one 8-point transform each) through the
+// wave's LDS buffer `T` (256 ints); afterwards T holds the MB's 16x16 residual (raster).
+__device__ inline void luma8_residual(const AvcDesc& d, const MbRec& m, int lane, int* T) {
+  if (lane < 32) {
+    const int q = lane >> 3, i = lane & 7;
+    int v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if ((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) {
+      const uint4 w = *reinterpret_cast<const uint4*>(d.coefs + size_t(avc::luma8_block_index(m, q)) * 16 + i * 8);
+      const u32 ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] = int(i16(ws[k] & 0xffff));
+        v[2 * k + 1] = int(i16(ws[k] >> 16));
+      }
+      avc::idct8_1d(v);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) T[q * 64 + i * 8 + k] = v[k];
+  }
+  wave_sync();
+  int c[8];
+  const int q = (lane >> 3) & 3, j = lane & 7;
+  if (lane < 32) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c[k] = T[q * 64 + k * 8 + j];
+    avc::idct8_1d(c);
+  }
+  wave_sync();  // every lane has read the row pass before the buffer is overwritten
+  if (lane < 32) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) T[((q >> 1) * 8 + k) * 16 + (q & 1) * 8 + j] = (c[k] + 32) >> 6;
+  }
+  wave_sync();
+}
 
 // One wave64 per MB, four MBs per workgroup: each lane reconstructs 4 luma samples (one per
 // 4x4-block row) and 2 chroma samples, so a lane has all of its reference loads in flight at
 // once and the picture lookup / record / MV loads are paid once per wave instead of per
-// 64 samples.
+// 64 samples. List-0 / list-1 predictions are combined by avc::wp_sample (default average or
+// the MB's weighted-prediction entries); 8x8-transform residuals go through LDS.
 __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restrict__ descs, int n,
                                                          int total) {
-  const int g = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + (int(threadIdx.x) >> 6));
-  if (g >= total) return;  // (wave-uniform; the kernel has no barrier)
+  __shared__ int lres[4][256];
+  const int wv = int(threadIdx.x) >> 6;
+  const int g = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
+  if (g >= total) return;  // (wave-uniform; the kernel has no workgroup barrier)
   int lo = 0, hi = n - 1;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
@@ -70,7 +116,9 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   const MbRec m = rec(d, mb);
   const int lane = int(threadIdx.x) & 63;
   const int x = lane & 15, y0 = lane >> 4;  // luma sample (x, y0 + 4k), block row k
-  if (avc::is_intra(m.kind) && m.kind != avc::kIPcm) {
+  int* T = lres[wv];
+  const bool t8 = (m.flags & avc::kMbT8x8) && m.luma_coded;
+  if (avc::is_wave_intra(m.kind)) {
     const int row = mb / d.wmbs;  // clear the intra wavefront's exchange tags of this MB
     if (lane < kIntraXgWords && row % kAvcDbkWgRows == kAvcDbkWgRows - 1 && row + 1 < d.hmbs)
       d.xg[(size_t(row / kAvcDbkWgRows) * d.wmbs + mb % d.wmbs) * kAvcXgWords + lane] = 0;
@@ -78,10 +126,14 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     // in parallel and the intra wavefront only adds them (same layout as IntraWave::res).
     if (m.res == avc::kNoRes) return;
     i16* r = d.res + size_t(m.res) * kAvcResSamples;
+    if (t8) luma8_residual(d, m, lane, T);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
-      r[y * 16 + x] = i16((m.luma_coded >> blk) & 1 ? avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3) : 0);
+      int v;
+      if (t8) v = T[y * 16 + x];
+      else v = (m.luma_coded >> blk) & 1 ? avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3) : 0;
+      r[y * 16 + x] = i16(v);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -107,32 +159,47 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     }
     return;
   }
-  const i16* mv = d.mvs + size_t(m.mv) * 32;
+  const i16* mv0 = d.mvs + size_t(m.mv) * 32;
+  const i16* mv1 = (m.flags & avc::kMbL1) ? mv0 + 32 : nullptr;
+  const avc::WpEntry* wpp =
+      (m.flags & avc::kMbWp) ? static_cast<const avc::WpEntry*>(d.wps) + m.wp : nullptr;
   int v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
-    const int mvx = mv[2 * blk], mvy = mv[2 * blk + 1];
-    const int ref = m.ref[((blk >> 3) << 1) | ((blk & 3) >> 1)];
-    v[k] = avc::luma_qpel(d.y + d.slot_y * u64(ref), pitch, wpx, hpx, mx * 16 + x + (mvx >> 2),
-                          my * 16 + y + (mvy >> 2), mvx & 3, mvy & 3);
+    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
+    const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+    int p0 = 0, p1 = 0;
+    if (s0 != 0xFF)
+      p0 = avc::luma_qpel(d.y + d.slot_y * u64(s0), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * blk] >> 2),
+                          my * 16 + y + (mv0[2 * blk + 1] >> 2), mv0[2 * blk] & 3, mv0[2 * blk + 1] & 3);
+    if (s1 != 0xFF)
+      p1 = avc::luma_qpel(d.y + d.slot_y * u64(s1), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * blk] >> 2),
+                          my * 16 + y + (mv1[2 * blk + 1] >> 2), mv1[2 * blk] & 3, mv1[2 * blk + 1] & 3);
+    v[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 0);
   }
+  if (t8) luma8_residual(d, m, lane, T);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
     int o = v[k];
-    if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3);
+    if (t8) o += T[y * 16 + x];
+    else if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3);
     ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = u8(avc::clip1(o));
   }
   int u[2];
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
     const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-    const int r = (cy >> 1) * 4 + (cx >> 1);
-    const int c_mvx = mv[2 * r], c_mvy = mv[2 * r + 1];
-    const int cref = m.ref[((r >> 3) << 1) | ((r & 3) >> 1)];
-    u[k] = avc::chroma_epel(d.uv + d.slot_uv * u64(cref), pitch, wpx / 2, hpx / 2, cc,
-                            mx * 8 + cx + (c_mvx >> 3), my * 8 + cy + (c_mvy >> 3), c_mvx & 7, c_mvy & 7);
+    const int r = (cy >> 1) * 4 + (cx >> 1), b8 = ((cy >> 2) << 1) | (cx >> 2);
+    const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+    int p0 = 0, p1 = 0;
+    if (s0 != 0xFF)
+      p0 = avc::chroma_epel(d.uv + d.slot_uv * u64(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (mv0[2 * r] >> 3),
+                            my * 8 + cy + (mv0[2 * r + 1] >> 3), mv0[2 * r] & 7, mv0[2 * r + 1] & 7);
+    if (s1 != 0xFF)
+      p1 = avc::chroma_epel(d.uv + d.slot_uv * u64(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (mv1[2 * r] >> 3),
+                            my * 8 + cy + (mv1[2 * r + 1] >> 3), mv1[2 * r] & 7, mv1[2 * r + 1] & 7);
+    u[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 1 + cc);
   }
 #pragma unroll
   for (int k = 0; k < 2; ++k) {
@@ -194,22 +261,18 @@ __device__ inline void xg_put(u64* p, u32 v, u32 tag) {
 }
 __device__ inline u64 xg_get(u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-// wave-local barrier (one wave64 per "group" here: LDS ordering + compiler fence)
-__device__ inline void wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // --------------------------------------------------------------------------------- intra
 
-constexpr int kTp = 24;  // luma tile pitch: row 0 = p[-1..19, -1], rows 1..16 = p[-1..15, y]
+constexpr int kTp = 28;  // luma tile pitch: row 0 = p[-1..23, -1] (Intra_8x8 top-right reaches
+                         // p[23,-1]), rows 1..16 = p[-1..15, y]; 4 * kTp must fit the 7-bit
+                         // Intra_4x4 tap offsets
 constexpr int kCp = 12;  // chroma tile pitch: row 0 = p[-1..7, -1], rows 1..8 = p[-1..7, y]
 
 struct alignas(16) IntraWave {
   MbRec rec[64];      // records of the current 64-MB chunk of the row
   i16 res[384];       // residual samples: 256 luma (raster) + 2 x 64 chroma (from the inter pass)
   u32 taps[256];      // Intra_4x4 tap words of the MB's samples
+  u8 pf[32];          // Intra_8x8 filtered references of the current 8x8 block
   u8 tile[17 * kTp];  // luma neighbours + the MB being reconstructed (branch-free addressing)
   u8 ctile[2][9 * kCp];
   u8 carry[16];       // right luma column of the previous MB of this row (if this wave built it)
@@ -269,14 +332,14 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       gp = g;
     }
   };
-  if (lane < 21) {  // luma row above: x0-1 .. x0+19
+  if (lane < 25) {  // luma row above: x0-1 .. x0+23
     const int px = x0 - 1 + lane;
     if (up && px >= 0 && px < pitch)
       top(px >> 4, &Y[size_t(y0 - 1) * pitch + px], (px & 15) >> 2, (px & 3) * 8, px & 15);
-  } else if (lane < 37) {  // luma left column
-    if (lf && !carry) a = Y[size_t(y0 + lane - 21) * pitch + x0 - 1];
-  } else if (lane < 55) {  // chroma row above: x*8-1 .. x*8+7 per component
-    const int c = (lane - 37) / 9, k = (lane - 37) % 9, px = x * 8 - 1 + k;
+  } else if (lane < 41) {  // luma left column
+    if (lf && !carry) a = Y[size_t(y0 + lane - 25) * pitch + x0 - 1];
+  } else if (lane < 59) {  // chroma row above: x*8-1 .. x*8+7 per component
+    const int c = (lane - 41) / 9, k = (lane - 41) % 9, px = x * 8 - 1 + k;
     if (up && px >= 0) {
       const int bo = (px & 7) * 2 + c;  // byte of the MB's NV12 bottom line
       top(px >> 3, &UV[size_t(row * 8 - 1) * pitch + px * 2 + c], 4 + (bo >> 2), (bo & 3) * 8, 16 + bo);
@@ -326,13 +389,13 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   const bool D = __builtin_amdgcn_readlane(int(av), 58) != 0;
   const bool A = __builtin_amdgcn_readlane(int(av), 59) != 0;
   if (lane < 48) reinterpret_cast<uint4*>(L.res)[lane] = cv;  // zeros without residual
-  if (lane < 21) {
+  if (lane < 25) {
     L.tile[lane] = u8((lane == 0 ? D : lane <= 16 ? B : C) ? a : 128u);
-  } else if (lane < 37) {
-    const int k = lane - 21;
+  } else if (lane < 41) {
+    const int k = lane - 25;
     L.tile[(k + 1) * kTp] = !A ? u8(128) : carry ? L.carry[k] : u8(a);
-  } else if (lane < 55) {
-    const int c = (lane - 37) / 9, k = (lane - 37) % 9;
+  } else if (lane < 59) {
+    const int c = (lane - 41) / 9, k = (lane - 41) % 9;
     L.ctile[c][k] = u8((k == 0 ? D : B) ? a : 128u);
   }
   if (lane >= 48) {
@@ -373,6 +436,27 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     for (int k = 0; k < 4; ++k) {
       const int p = lane + 64 * k;
       L.tile[((p >> 4) + 1) * kTp + (p & 15) + 1] = out[k];
+    }
+  } else if (m.kind == avc::kI8x8) {
+    // Intra_8x8: four blocks in order; per block lanes 0-24 filter the 25 reference samples
+    // (§8.3.2.2.1) into LDS, then every lane predicts one sample and adds its residual.
+    for (int q = 0; q < 4; ++q) {
+      const int bx = q & 1, by = q >> 1;
+      const bool top = by > 0 || B, left = bx > 0 || A;
+      const bool tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+      const bool tr = by == 0 ? (bx == 0 ? B : C) : (bx == 0);
+      const u8* nb = &L.tile[(by * 8) * kTp + bx * 8];  // p[-1,-1] of the block
+      auto Tr = [&](int xx) -> int { return nb[1 + (xx >= 8 && !tr ? 7 : xx)]; };
+      auto Lr = [&](int yy) -> int { return nb[(yy + 1) * kTp]; };
+      if (lane < 25) L.pf[lane] = u8(avc::intra8x8_filter_at(Tr, Lr, top, left, tl, lane));
+      wave_sync();
+      const int px = lane & 7, py = lane >> 3;
+      auto Tf = [&](int xx) -> int { return L.pf[1 + xx]; };
+      auto Lf = [&](int yy) -> int { return yy < 0 ? L.pf[0] : L.pf[17 + yy]; };
+      const int v = avc::intra8x8_pred_g(Tf, Lf, top, left, avc::i4_mode(m, q), px, py) +
+                    L.res[(by * 8 + py) * 16 + bx * 8 + px];
+      L.tile[(by * 8 + py + 1) * kTp + bx * 8 + px + 1] = u8(avc::clip1(v));
+      wave_sync();
     }
   } else {
     // Tap words of all 256 samples: the (mode, y, x) table entry with its neighbour indices
@@ -538,21 +622,20 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
       const int x = base + lane;
       bool intra = false;
       if (x < W) {
+        constexpr int kWords = int(sizeof(MbRec) / sizeof(uint2));
         const uint2* src = reinterpret_cast<const uint2*>(&recs[row * W + x]);
         uint2* dst = reinterpret_cast<uint2*>(&L.rec[lane]);
-        uint2 q[5];
-        for (int k = 0; k < 5; ++k) q[k] = src[k];
-        for (int k = 0; k < 5; ++k) dst[k] = q[k];
-        const u8 kd = u8(q[0].x & 0xff);
-        intra = kd == avc::kI4x4 || kd == avc::kI16x16;
+        uint2 q[kWords];
+        for (int k = 0; k < kWords; ++k) q[k] = src[k];
+        for (int k = 0; k < kWords; ++k) dst[k] = q[k];
+        intra = avc::is_wave_intra(u8(q[0].x & 0xff));
       }
       if (row > 0)  // which MBs base-1 .. base+64 of the row above are intra (this wavefront's)
         for (int q = lane; q < 66; q += 64) {
           const int ax = base - 1 + q;
           u8 v = 0;
           if (ax >= 0 && ax < W) {
-            const u8 kd = recs[(row - 1) * W + ax].kind;
-            v = kd == avc::kI4x4 || kd == avc::kI16x16;
+            v = avc::is_wave_intra(recs[(row - 1) * W + ax].kind);
           }
           L.up[q] = v;
         }
@@ -606,16 +689,17 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
     const i16* mq = avc::is_intra(q.kind) ? nullptr : d.mvs + size_t(q.mv) * 32;
     const i16* ml = avc::is_intra(lm.kind) ? nullptr : d.mvs + size_t(lm.mv) * 32;
     const i16* mt = avc::is_intra(tm.kind) ? nullptr : d.mvs + size_t(tm.mv) * 32;
+    const bool t8 = (q.flags & avc::kMbT8x8) != 0;
     for (int dir = 0; dir < 2; ++dir)
       for (int e = 0; e < 4; ++e) {
         if (e == 0 && !(dir == 0 ? left : top)) continue;
+        if ((e & 1) && t8) continue;  // no 4x4 edges inside 8x8 transform blocks
         const MbRec& p = e > 0 ? q : (dir == 0 ? lm : tm);
         const i16* mp = e > 0 ? mq : (dir == 0 ? ml : mt);
         for (int sg = 0; sg < 4; ++sg) {
           const int bq = dir == 0 ? sg * 4 + e : e * 4 + sg;
           const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
-          const int bs = avc::boundary_strength(p, bp, mp ? mp + 2 * bp : nullptr, q, bq,
-                                                mq ? mq + 2 * bq : nullptr, e == 0);
+          const int bs = avc::boundary_strength(p, bp, mp, q, bq, mq, e == 0);
           const int i = dir * 16 + e * 4 + sg;
           info.bs[i >> 3] |= u32(bs) << (4 * (i & 7));
         }
@@ -623,14 +707,14 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
     info.any = (info.bs[0] | info.bs[1] | info.bs[2] | info.bs[3]) ? 1 : 0;
     const MbRec* ps[3] = {&lm, &tm, &q};
     for (int k = 0; k < 3; ++k) {
-      const avc::EdgeParams el = avc::edge_params(ps[k]->qp, q.qp, q.alpha_off, q.beta_off);
-      const avc::EdgeParams ec = avc::edge_params(ps[k]->qpc, q.qpc, q.alpha_off, q.beta_off);
-      info.alpha[k] = u8(el.alpha);
-      info.beta[k] = u8(el.beta);
-      for (int j = 0; j < 3; ++j) info.tc0[k][j] = u8(el.tc0[j]);
-      info.alpha[3 + k] = u8(ec.alpha);
-      info.beta[3 + k] = u8(ec.beta);
-      for (int j = 0; j < 3; ++j) info.tc0[3 + k][j] = u8(ec.tc0[j]);
+      const avc::EdgeParams ep[3] = {avc::edge_params(ps[k]->qp, q.qp, q.alpha_off, q.beta_off),
+                                     avc::edge_params(ps[k]->qpc, q.qpc, q.alpha_off, q.beta_off),
+                                     avc::edge_params(ps[k]->qpc2, q.qpc2, q.alpha_off, q.beta_off)};
+      for (int c = 0; c < 3; ++c) {
+        info.alpha[c * 3 + k] = u8(ep[c].alpha);
+        info.beta[c * 3 + k] = u8(ep[c].beta);
+        for (int j = 0; j < 3; ++j) info.tc0[c * 3 + k][j] = u8(ep[c].tc0[j]);
+      }
     }
   }
   static_cast<AvcDbkInfo*>(d.dbk)[mb] = info;
@@ -771,7 +855,7 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
     if (any && (!ch || !(e & 1))) {
       const int bs = bs_of(L.info, dir, e, ch ? k >> 1 : l >> 2);
       if (bs) {
-        const int pi = (e > 0 ? 2 : dir) + (ch ? 3 : 0);  // edge params: left / top / internal
+        const int pi = (e > 0 ? 2 : dir) + (ch ? 3 + 3 * c : 0);  // component, then left / top / internal
         const int al = L.info.alpha[pi], be = L.info.beta[pi];
         const int tc = bs < 4 ? L.info.tc0[pi][bs - 1] : 0;
         u8* sp;
@@ -824,7 +908,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     row = row < H ? row : H - 1;
     x = x < 0 ? 0 : (x < W ? x : W - 1);
     DbkRegs v;
-    v.info = gld4(reinterpret_cast<const u32*>(&infos[size_t(row) * W + x]) + (l < 12 ? l : 0));
+    v.info = gld4(reinterpret_cast<const u32*>(&infos[size_t(row) * W + x]) + (l < 16 ? l : 0));
     const u8* ym = Y + size_t(row * 16 + (l >> 2)) * pitch + x * 16 + (l & 3) * 4;
     v.m0 = gld4(ym);                      // MB rows 0..7
     v.m1 = gld4(ym + size_t(8) * pitch);  // MB rows 8..15
@@ -861,7 +945,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     const int x0 = x * 16, y0 = row * 16;
     // ---- LDS: MB samples and left columns (carried)
     if (act) {
-      if (l < 12) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
+      if (l < 16) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
       st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
       st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
       if (l < 16) {

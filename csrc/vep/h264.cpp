@@ -1,23 +1,103 @@
 // H.264 parameter-set / slice-header parsing and writing (ITU-T H.264 §7.3.2.1, §7.3.2.2, §7.3.3).
 #include "h264.h"
 
+#include <algorithm>
+
 namespace vep::h264 {
 
-static void skip_scaling_list(BitReader& br, int size) {
+const u8 kDefault4x4[2][16] = {
+    {6, 13, 13, 20, 20, 20, 28, 28, 28, 28, 32, 32, 32, 37, 37, 42},
+    {10, 14, 14, 20, 20, 20, 24, 24, 24, 24, 27, 27, 27, 30, 30, 34}};
+const u8 kDefault8x8[2][64] = {
+    {6,  10, 10, 13, 11, 13, 16, 16, 16, 16, 18, 18, 18, 18, 18, 23, 23, 23, 23, 23, 23, 25,
+     25, 25, 25, 25, 25, 25, 27, 27, 27, 27, 27, 27, 27, 27, 29, 29, 29, 29, 29, 29, 29, 31,
+     31, 31, 31, 31, 31, 33, 33, 33, 33, 33, 36, 36, 36, 36, 38, 38, 38, 40, 40, 42},
+    {9,  13, 13, 15, 13, 15, 17, 17, 17, 17, 19, 19, 19, 19, 19, 21, 21, 21, 21, 21, 21, 22,
+     22, 22, 22, 22, 22, 22, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 27,
+     27, 27, 27, 27, 27, 28, 28, 28, 28, 28, 30, 30, 30, 30, 32, 32, 32, 33, 33, 35}};
+
+// scaling_list() (§7.3.2.1.1.1): returns useDefaultScalingMatrixFlag.
+static bool read_scaling_list(BitReader& br, u8* list, int size) {
   int last = 8, next = 8;
+  bool use_default = false;
   for (int j = 0; j < size; ++j) {
     if (next != 0) {
-      int delta = br.se();
+      const int delta = br.se();
+      VEP_CHECK(delta >= -128 && delta <= 127, "delta_scale out of range");
       next = (last + delta + 256) % 256;
+      use_default = j == 0 && next == 0;
     }
-    last = (next == 0) ? last : next;
+    list[j] = u8(next == 0 ? last : next);
+    last = list[j];
   }
+  return use_default;
+}
+
+// Parse up to `count` lists with the fall-back rule: rule A (SPS, `base` = nullptr) falls back
+// to the defaults, rule B (PPS) to the SPS's lists for lists 0, 3, 6, 7.
+static void read_scaling_matrix(BitReader& br, int count, ScalingLists& out, const ScalingLists* base,
+                                bool* present, bool* use_default) {
+  for (int i = 0; i < 8; ++i) {
+    const bool pr = i < count && br.u1();
+    if (present) present[i] = pr;
+    bool def = false;
+    if (pr) def = read_scaling_list(br, i < 6 ? out.l4[i] : out.l8[i - 6], i < 6 ? 16 : 64);
+    if (use_default) use_default[i] = def;
+    if (pr && !def) continue;
+    if (i < 6) {
+      u8* l = out.l4[i];
+      if (pr && def) std::memcpy(l, kDefault4x4[i >= 3], 16);
+      else if (i == 0 || i == 3) std::memcpy(l, base ? base->l4[i] : kDefault4x4[i >= 3], 16);
+      else std::memcpy(l, out.l4[i - 1], 16);
+    } else {
+      u8* l = out.l8[i - 6];
+      if (pr && def) std::memcpy(l, kDefault8x8[i - 6], 64);
+      else std::memcpy(l, base ? base->l8[i - 6] : kDefault8x8[i - 6], 64);
+    }
+  }
+}
+
+static void read_hrd(BitReader& br) {
+  const u32 cnt = br.ue() + 1;
+  VEP_CHECK(cnt <= 32, "cpb_cnt out of range");
+  br.u(4);
+  br.u(4);
+  for (u32 i = 0; i < cnt; ++i) {
+    br.ue();
+    br.ue();
+    br.u1();
+  }
+  br.u(5);
+  br.u(5);
+  br.u(5);
+  br.u(5);
+}
+
+int Sps::max_dpb_frames() const {
+  int mbs;  // MaxDpbMbs (Table A-1)
+  switch (level_idc) {
+    case 9: case 10: mbs = 396; break;
+    case 11: mbs = (constraint_flags & 0x10) && profile_idc != 100 ? 396 : 900; break;
+    case 12: case 13: case 20: mbs = 2376; break;
+    case 21: mbs = 4752; break;
+    case 22: case 30: mbs = 8100; break;
+    case 31: mbs = 18000; break;
+    case 32: mbs = 20480; break;
+    case 40: case 41: mbs = 32768; break;
+    case 42: mbs = 34816; break;
+    case 50: mbs = 110400; break;
+    case 51: case 52: mbs = 184320; break;
+    default: mbs = 696320; break;
+  }
+  const int pic = width_mbs * height_mbs();
+  return std::max(1, std::min(16, pic > 0 ? mbs / pic : 16));
 }
 
 Sps parse_sps(const u8* rbsp, size_t n) {
   VEP_CHECK(n >= 4 && nal_type(rbsp[0]) == kNalSps, "not an SPS NAL");
   BitReader br(rbsp + 1, n - 1);
   Sps s;
+  s.scaling.flat();
   s.profile_idc = br.u(8);
   s.constraint_flags = br.u(8);
   s.level_idc = br.u(8);
@@ -27,37 +107,41 @@ Sps parse_sps(const u8* rbsp, size_t n) {
     case 100: case 110: case 122: case 244: case 44: case 83: case 86: case 118:
     case 128: case 138: case 139: case 134: case 135: {
       s.chroma_format_idc = br.ue();
+      VEP_CHECK(s.chroma_format_idc <= 3, "bad chroma_format_idc");
       if (s.chroma_format_idc == 3) br.u1();  // separate_colour_plane_flag
       s.bit_depth_luma = 8 + br.ue();
       s.bit_depth_chroma = 8 + br.ue();
-      br.u1();  // qpprime_y_zero_transform_bypass_flag
-      if (br.u1()) {  // seq_scaling_matrix_present_flag
-        int cnt = (s.chroma_format_idc != 3) ? 8 : 12;
-        for (int i = 0; i < cnt; ++i)
-          if (br.u1()) skip_scaling_list(br, i < 6 ? 16 : 64);
-      }
+      VEP_CHECK(s.bit_depth_luma <= 14 && s.bit_depth_chroma <= 14, "bad bit depth");
+      s.transform_bypass = br.u1();
+      s.scaling_matrix_present = br.u1();
+      if (s.scaling_matrix_present)
+        read_scaling_matrix(br, s.chroma_format_idc != 3 ? 8 : 12, s.scaling, nullptr, nullptr, nullptr);
       break;
     }
     default: break;
   }
   s.log2_max_frame_num = br.ue() + 4;
+  VEP_CHECK(s.log2_max_frame_num <= 16, "log2_max_frame_num out of range");
   s.poc_type = br.ue();
+  VEP_CHECK(s.poc_type <= 2, "bad pic_order_cnt_type");
   if (s.poc_type == 0) {
     s.log2_max_poc_lsb = br.ue() + 4;
+    VEP_CHECK(s.log2_max_poc_lsb <= 16, "log2_max_pic_order_cnt_lsb out of range");
   } else if (s.poc_type == 1) {
     s.delta_pic_order_always_zero = br.u1();
-    br.se();
-    br.se();
-    int cyc = br.ue();
+    s.offset_for_non_ref_pic = br.se();
+    s.offset_for_top_to_bottom_field = br.se();
+    const u32 cyc = br.ue();
     VEP_CHECK(cyc < 256, "poc cycle too long");
-    for (int i = 0; i < cyc; ++i) br.se();
+    for (u32 i = 0; i < cyc; ++i) s.offset_for_ref_frame.push_back(br.se());
   }
   s.max_num_ref_frames = br.ue();
-  br.u1();  // gaps_in_frame_num_value_allowed_flag
+  VEP_CHECK(s.max_num_ref_frames <= 16, "max_num_ref_frames out of range");
+  s.gaps_in_frame_num_allowed = br.u1();
   s.width_mbs = br.ue() + 1;
   s.height_map_units = br.ue() + 1;
   s.frame_mbs_only = br.u1();
-  if (!s.frame_mbs_only) br.u1();  // mb_adaptive_frame_field_flag
+  if (!s.frame_mbs_only) s.mbaff = br.u1();
   s.direct_8x8 = br.u1();
   if (br.u1()) {  // frame_cropping_flag
     int cx = (s.chroma_format_idc == 0 || s.chroma_format_idc == 3) ? 1 : 2;
@@ -68,7 +152,7 @@ Sps parse_sps(const u8* rbsp, size_t n) {
     s.crop_top = br.ue() * cy;
     s.crop_bottom = br.ue() * cy;
   }
-  if (br.u1()) {  // vui_parameters_present_flag
+  if (br.bits_left() > 0 && br.u1()) {  // vui_parameters_present_flag
     if (br.u1()) {  // aspect_ratio_info_present_flag
       if (br.u(8) == 255) br.u(32);
     }
@@ -86,6 +170,23 @@ Sps parse_sps(const u8* rbsp, size_t n) {
       s.num_units_in_tick = br.u(32);
       s.time_scale = br.u(32);
       br.u1();
+    }
+    const bool nal_hrd = br.u1();
+    if (nal_hrd) read_hrd(br);
+    const bool vcl_hrd = br.u1();
+    if (vcl_hrd) read_hrd(br);
+    if (nal_hrd || vcl_hrd) br.u1();  // low_delay_hrd_flag
+    br.u1();                          // pic_struct_present_flag
+    if (br.u1()) {                    // bitstream_restriction_flag
+      br.u1();
+      br.ue();
+      br.ue();
+      br.ue();
+      br.ue();
+      s.max_num_reorder_frames = int(br.ue());
+      s.max_dec_frame_buffering = int(br.ue());
+      VEP_CHECK(s.max_num_reorder_frames <= 16 && s.max_dec_frame_buffering <= 16,
+                "bitstream_restriction out of range");
     }
   }
   VEP_CHECK(s.width_mbs > 0 && s.width_mbs <= 1024 && s.height_mbs() <= 1024, "bad SPS size");
@@ -105,15 +206,55 @@ Pps parse_pps(const u8* rbsp, size_t n) {
   VEP_CHECK(p.num_slice_groups == 1, "FMO slice groups are not supported");
   p.num_ref_idx_l0_default = br.ue() + 1;
   p.num_ref_idx_l1_default = br.ue() + 1;
+  VEP_CHECK(p.num_ref_idx_l0_default <= 32 && p.num_ref_idx_l1_default <= 32, "num_ref_idx out of range");
   p.weighted_pred = br.u1();
   p.weighted_bipred_idc = br.u(2);
+  VEP_CHECK(p.weighted_bipred_idc <= 2, "bad weighted_bipred_idc");
   p.pic_init_qp = 26 + br.se();
   p.pic_init_qs = 26 + br.se();
   p.chroma_qp_index_offset = br.se();
+  VEP_CHECK(p.chroma_qp_index_offset >= -12 && p.chroma_qp_index_offset <= 12, "chroma_qp_index_offset out of range");
   p.deblocking_filter_control = br.u1();
   p.constrained_intra_pred = br.u1();
   p.redundant_pic_cnt_present = br.u1();
+  p.second_chroma_qp_index_offset = p.chroma_qp_index_offset;
+  p.scaling.flat();
+  if (br.bitpos() < br.stop_bit_pos()) {  // more_rbsp_data(): the High-profile tail
+    p.transform_8x8_mode = br.u1();
+    p.scaling_matrix_present = br.u1();
+    if (p.scaling_matrix_present)
+      for (int i = 0; i < 6 + 2 * int(p.transform_8x8_mode); ++i) {
+        p.scaling_list_present[i] = br.u1();
+        if (p.scaling_list_present[i])
+          p.scaling_use_default[i] = read_scaling_list(br, i < 6 ? p.scaling.l4[i] : p.scaling.l8[i - 6], i < 6 ? 16 : 64);
+      }
+    p.second_chroma_qp_index_offset = br.se();
+    VEP_CHECK(p.second_chroma_qp_index_offset >= -12 && p.second_chroma_qp_index_offset <= 12,
+              "second_chroma_qp_index_offset out of range");
+  }
   return p;
+}
+
+ScalingLists resolve_scaling(const Sps& sps, const Pps& pps) {
+  if (!pps.scaling_matrix_present) return sps.scaling;  // flat when the SPS has none
+  // rule B when the SPS carries a matrix, rule A otherwise
+  const ScalingLists* base = sps.scaling_matrix_present ? &sps.scaling : nullptr;
+  ScalingLists out = pps.scaling;
+  for (int i = 0; i < 8; ++i) {
+    const bool pr = pps.scaling_list_present[i], def = pps.scaling_use_default[i];
+    if (pr && !def) continue;
+    if (i < 6) {
+      u8* l = out.l4[i];
+      if (pr && def) std::memcpy(l, kDefault4x4[i >= 3], 16);
+      else if (i == 0 || i == 3) std::memcpy(l, base ? base->l4[i] : kDefault4x4[i >= 3], 16);
+      else std::memcpy(l, out.l4[i - 1], 16);
+    } else {
+      u8* l = out.l8[i - 6];
+      if (pr && def) std::memcpy(l, kDefault8x8[i - 6], 64);
+      else std::memcpy(l, base ? base->l8[i - 6] : kDefault8x8[i - 6], 64);
+    }
+  }
+  return out;
 }
 
 SliceHeader parse_slice_header(BitReader& br, u8 nal_hdr, const Sps& sps, const Pps& pps) {
@@ -139,12 +280,14 @@ SliceHeader parse_slice_header(BitReader& br, u8 nal_hdr, const Sps& sps, const 
   int st = sh.slice_type % 5;
   if (st == kB) br.u1();  // direct_spatial_mv_pred_flag
   sh.num_ref_idx_l0 = pps.num_ref_idx_l0_default;
+  int num_l1 = pps.num_ref_idx_l1_default;
   if (st == kP || st == kSP || st == kB) {
     if (br.u1()) {
       sh.num_ref_idx_l0 = br.ue() + 1;
-      if (st == kB) br.ue();
+      if (st == kB) num_l1 = int(br.ue()) + 1;
     }
   }
+  VEP_CHECK(sh.num_ref_idx_l0 <= 32 && num_l1 <= 32, "num_ref_idx out of range");
   // ref_pic_list_modification()
   if (st != kI && st != kSI) {
     if (br.u1()) {
@@ -165,9 +308,22 @@ SliceHeader parse_slice_header(BitReader& br, u8 nal_hdr, const Sps& sps, const 
       }
     }
   }
-  VEP_CHECK(!((pps.weighted_pred && (st == kP || st == kSP)) ||
-              (pps.weighted_bipred_idc == 1 && st == kB)),
-            "weighted prediction is not supported");
+  if ((pps.weighted_pred && (st == kP || st == kSP)) || (pps.weighted_bipred_idc == 1 && st == kB)) {
+    // pred_weight_table(): skipped here (the general decoder, avc.cpp, applies it)
+    br.ue();
+    if (sps.chroma_format_idc != 0) br.ue();
+    for (int l = 0; l < (st == kB ? 2 : 1); ++l) {
+      const int nref = l == 0 ? sh.num_ref_idx_l0 : num_l1;
+      for (int i = 0; i < nref; ++i) {
+        if (br.u1()) {
+          br.se();
+          br.se();
+        }
+        if (sps.chroma_format_idc != 0 && br.u1())
+          for (int k = 0; k < 4; ++k) br.se();
+      }
+    }
+  }
   if (sh.nal_ref_idc != 0) {  // dec_ref_pic_marking()
     if (sh.idr()) {
       br.u1();
@@ -207,6 +363,13 @@ std::vector<u8> write_sps(const Sps& s) {
   bw.u(8, s.constraint_flags);
   bw.u(8, s.level_idc);
   bw.ue(s.sps_id);
+  if (s.profile_idc >= 100) {
+    bw.ue(1);   // chroma_format_idc 4:2:0
+    bw.ue(0);   // bit_depth_luma_minus8
+    bw.ue(0);   // bit_depth_chroma_minus8
+    bw.u1(0);   // qpprime_y_zero_transform_bypass_flag
+    bw.u1(0);   // seq_scaling_matrix_present_flag
+  }
   bw.ue(s.log2_max_frame_num - 4);
   bw.ue(s.poc_type);
   if (s.poc_type == 0) bw.ue(s.log2_max_poc_lsb - 4);
@@ -244,7 +407,17 @@ std::vector<u8> write_sps(const Sps& s) {
   bw.u1(0);  // nal hrd
   bw.u1(0);  // vcl hrd
   bw.u1(0);  // pic_struct_present
-  bw.u1(0);  // bitstream_restriction
+  const bool restrict = s.max_num_reorder_frames >= 0;
+  bw.u1(restrict);  // bitstream_restriction
+  if (restrict) {
+    bw.u1(1);   // motion_vectors_over_pic_boundaries_flag
+    bw.ue(0);   // max_bytes_per_pic_denom
+    bw.ue(0);   // max_bits_per_mb_denom
+    bw.ue(16);  // log2_max_mv_length_horizontal
+    bw.ue(16);  // log2_max_mv_length_vertical
+    bw.ue(u32(s.max_num_reorder_frames));
+    bw.ue(u32(std::max(s.max_dec_frame_buffering, s.max_num_ref_frames)));
+  }
   bw.trailing();
   return bw.buf();
 }
@@ -254,19 +427,24 @@ std::vector<u8> write_pps(const Pps& p) {
   bw.u(8, (0 << 7) | (3 << 5) | kNalPps);
   bw.ue(p.pps_id);
   bw.ue(p.sps_id);
-  bw.u1(0);  // CAVLC
+  bw.u1(p.cabac);
   bw.u1(0);
   bw.ue(0);
   bw.ue(p.num_ref_idx_l0_default - 1);
   bw.ue(p.num_ref_idx_l1_default - 1);
-  bw.u1(0);
-  bw.u(2, 0);
+  bw.u1(p.weighted_pred);
+  bw.u(2, u32(p.weighted_bipred_idc));
   bw.se(p.pic_init_qp - 26);
   bw.se(p.pic_init_qs - 26);
   bw.se(p.chroma_qp_index_offset);
   bw.u1(p.deblocking_filter_control);
+  bw.u1(p.constrained_intra_pred);
   bw.u1(0);
-  bw.u1(0);
+  if (p.transform_8x8_mode || p.second_chroma_qp_index_offset != p.chroma_qp_index_offset) {
+    bw.u1(p.transform_8x8_mode);
+    bw.u1(0);  // pic_scaling_matrix_present_flag
+    bw.se(p.second_chroma_qp_index_offset);
+  }
   bw.trailing();
   return bw.buf();
 }

@@ -180,10 +180,32 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
     }
     if (full_) {
       for (size_t i = from; i < to; ++i) {
-        job.avc.push_back(avc_.parse(*gop_[i]));
+        job.avc.push_back(avc_.parse(*gop_[i], i64(i)));
         last = gop_[i].get();
       }
       job.pic = job.avc.back()->info;
+      // the newest picture that left the reorder buffer during this job is the one published
+      const avc::OutFrame* of = nullptr;
+      for (const auto& p : job.avc)
+        if (!p->outputs.empty()) of = &p->outputs.back();
+      job.out_slot = of ? of->slot : -1;
+      if (of) {
+        job.pic = of->info;
+        FrameMeta& m = job.meta;
+        m.width = of->info.width;
+        m.height = of->info.height;
+        m.pts = of->au.pts;
+        m.dts = of->au.dts;
+        m.timestamp = of->au.pts;
+        m.packet = of->au.tag;
+        m.keyframe = keyframes_;
+        m.is_keyframe = of->au.keyframe;
+        m.is_corrupt = of->au.corrupt;
+        m.frame_type = of->info.pict_type;
+        m.arrival_ms = last->arrival_ms;  // latency: from the packet that completed the output
+        decoded_upto_ = to;
+        return true;
+      }
     }
   } catch (const std::exception& e) {
     errors.fetch_add(1);
@@ -516,8 +538,11 @@ void merge_job(DecodeJob& p, DecodeJob&& job) {
   // general-path pictures are appended (each references the previous ones)
   if (job.general() && p.general() && !job.refresh) {
     p.avc.insert(p.avc.end(), job.avc.begin(), job.avc.end());
-    p.pic = job.pic;
-    p.meta = job.meta;
+    if (job.out_slot >= 0 || p.out_slot < 0) {  // the newer output wins; none keeps the older
+      p.pic = job.pic;
+      p.meta = job.meta;
+      p.out_slot = job.out_slot;
+    }
   } else if (job.refresh || job.general() != p.general() || p.upd.width_mbs != job.upd.width_mbs ||
              p.upd.height_mbs != job.upd.height_mbs) {
     p = std::move(job);
@@ -745,7 +770,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
   for (size_t i = 0; i < jobs.size(); ++i) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
     ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots());
-    slots[i] = c.ring_->begin_write();
+    slots[i] = jobs[i].has_output() ? c.ring_->begin_write() : -1;
   }
 }
 
@@ -846,7 +871,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   struct AvcPic {
     const avc::Picture* p;
     int job;
-    size_t off_mbs, off_coef, off_mv, off_dbk, off_res, off_xg;
+    size_t off_mbs, off_coef, off_mv, off_wp, off_dbk, off_res, off_xg;
   };
   std::vector<AvcPic> apics;
   int rounds = 0;
@@ -860,13 +885,17 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       const avc::Picture& p = *v[size_t(r)];
       VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows && p.wmbs <= gpu::kAvcMaxCols,
                 "picture too large for the wavefront kernels");
-      AvcPic a{&p, i, 0, 0, 0, 0, 0, 0};
+      VEP_CHECK(p.wmbs * 16 == jobs[size_t(i)].pic.coded_width && p.hmbs * 16 == jobs[size_t(i)].pic.coded_height,
+                "picture size differs from the camera's surfaces");
+      AvcPic a{&p, i, 0, 0, 0, 0, 0, 0, 0};
       a.off_mbs = need;
       need += al(p.mbs.size() * sizeof(avc::MbRec));
       a.off_coef = need;
       need += al(p.coefs.size() * sizeof(i16));
       a.off_mv = need;
       need += al(p.mvs.size() * sizeof(i16));
+      a.off_wp = need;
+      need += al(p.wps.size() * sizeof(avc::WpEntry));
       round_pics[size_t(r)].push_back(int(apics.size()));
       apics.push_back(a);
     }
@@ -927,6 +956,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     add(a.p->mbs.data(), a.p->mbs.size() * sizeof(avc::MbRec), a.off_mbs);
     add(a.p->coefs.data(), a.p->coefs.size() * sizeof(i16), a.off_coef);
     add(a.p->mvs.data(), a.p->mvs.size() * sizeof(i16), a.off_mv);
+    add(a.p->wps.data(), a.p->wps.size() * sizeof(avc::WpEntry), a.off_wp);
   }
   std::vector<std::vector<const u8*>> seg_dev(static_cast<size_t>(n));
   auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
@@ -989,11 +1019,18 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   auto* hd = reinterpret_cast<gpu::DecodeDesc*>(st.h + off_desc);
   auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(st.h + off_lb);
   int tiles = 0;
-  for (int i = 0; i < n; ++i) {
+  // conversion / letterbox descriptors only for jobs that publish a frame (a general-path job
+  // whose pictures all wait in the reorder buffer only reconstructs)
+  std::vector<int> outs;
+  for (int i = 0; i < n; ++i)
+    if (jobs[size_t(i)].has_output()) outs.push_back(i);
+  const int nout = int(outs.size());
+  for (int k = 0; k < nout; ++k) {
+    const int i = outs[size_t(k)];
     const DecodeJob& j = jobs[size_t(i)];
     Camera* c = cams_[size_t(j.cam)].get();
     const size_t words = size_t(j.upd.mbs() + 31) / 32;
-    gpu::DecodeDesc& d = hd[i];
+    gpu::DecodeDesc& d = hd[k];
     const size_t tgt = size_t(j.target());
     d.y = c->surface.y + tgt * c->surface.slot_y();
     d.uv = c->surface.uv + tgt * c->surface.slot_uv();
@@ -1025,7 +1062,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     d.err = const_cast<u32*>(st.err_dev) + i;
     tiles += gpu::tiles_for(d.wmbs, d.hmbs);
     if (opt_.letterbox_size > 0) {
-      gpu::LetterboxDesc& l = hl[i];
+      gpu::LetterboxDesc& l = hl[k];
       const size_t S = size_t(opt_.letterbox_size);
       l.y = d.y;
       l.uv = d.uv;
@@ -1054,6 +1091,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.mbs = st.d + a.off_mbs;
       g.coefs = reinterpret_cast<const i16*>(st.d + a.off_coef);
       g.mvs = reinterpret_cast<const i16*>(st.d + a.off_mv);
+      g.wps = st.d + a.off_wp;
       g.y = c->surface.y;
       g.uv = c->surface.uv;
       g.slot_y = c->surface.slot_y();
@@ -1119,7 +1157,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       gpu::launch_avc_deblock(ad, np, max_h, cs);
     }
   }
-  gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), n, tiles,
+  gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), nout, tiles,
                              cs);
   if (opt_.letterbox_size > 0) {
     gpu::LetterboxParams p{};
@@ -1131,7 +1169,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     }
     p.pad_value = 114;
     p.format = opt_.letterbox_format;
-    gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(st.d + off_lb), n, p,
+    gpu::launch_letterbox(reinterpret_cast<const gpu::LetterboxDesc*>(st.d + off_lb), nout, p,
                           cs);
   }
   VEP_HIP(hipEventRecord(st.e1, cs));
@@ -1154,6 +1192,7 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
     } else {
       cpu_apply_update(jobs[i].upd, c.surface.host[0]);
     }
+    if (!jobs[i].has_output()) continue;
     const HostSurface& src = c.surface.host[size_t(jobs[i].target())];
     cpu_nv12_to_bgr(src, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
                     jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
@@ -1196,8 +1235,22 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
   std::lock_guard<std::mutex> g(cams_mu_);
   for (size_t i = 0; i < jobs.size(); ++i) {
     auto& cp = cams_[size_t(jobs[i].cam)];
+    const bool out = jobs[i].has_output();
     if (!cp || !cp->ring_) {
-      dropped_.fetch_add(1, std::memory_order_relaxed);
+      if (out) dropped_.fetch_add(1, std::memory_order_relaxed);
+      continue;
+    }
+    if (!(err && err[i]) && !cp->broken_) {
+      const u64 np = jobs[i].general() ? jobs[i].avc.size() : 1;
+      pictures_.fetch_add(np, std::memory_order_relaxed);
+      cp->pictures.fetch_add(np, std::memory_order_relaxed);
+    }
+    if (!out) {  // reconstruction only (its pictures wait in the reorder buffer)
+      if (err && err[i]) {
+        cp->errors.fetch_add(1, std::memory_order_relaxed);
+        cp->logs.add(true, "GPU reconstruction wavefront timed out; waiting for the next keyframe");
+        cp->broken_ = true;
+      }
       continue;
     }
     if (err && err[i]) {
@@ -1286,9 +1339,9 @@ void Worker::launch_on(Lane& ln, Batch&& b) {
       std::lock_guard<std::mutex> g(cams_mu_);
       for (size_t i = 0; i < st.jobs.size(); ++i) {
         auto& cp = cams_[size_t(st.jobs[i].cam)];
-        if (cp && cp->ring_) cp->ring_->abort(st.slots[i]);
+        if (cp && cp->ring_ && st.slots[i] >= 0) cp->ring_->abort(st.slots[i]);
       }
-      dropped_.fetch_add(st.jobs.size(), std::memory_order_relaxed);
+      for (const auto& j : st.jobs) dropped_.fetch_add(j.has_output() ? 1 : 0, std::memory_order_relaxed);
     }
     st.jobs.clear();
     st.slots.clear();

@@ -98,12 +98,17 @@ struct DecodeJob {
   int cam = -1;
   MbUpdate upd;                        // PCM / skip fast path (collapsible)
   std::vector<avc::PicturePtr> avc;    // general H.264 path: pictures in decoding order
-  PictureInfo pic;
+  PictureInfo pic;                     // the published frame's picture (sizes of the surfaces)
   FrameMeta meta;
   bool refresh = false;  // IDR: every MB is covered
+  // General path: DPB slot of the newest picture that left the reorder buffer in this job (it is
+  // converted and published), -1 when every picture of the job is still waiting for output
+  // (B-frame reordering): the job then only reconstructs.
+  int out_slot = -1;
   bool general() const { return !avc.empty(); }
+  bool has_output() const { return !general() || out_slot >= 0; }
   int dpb_slots() const { return avc.empty() ? 1 : avc.back()->dpb_slots; }
-  int target() const { return avc.empty() ? 0 : avc.back()->target; }
+  int target() const { return avc.empty() ? 0 : out_slot; }
 };
 
 // Fold `job` into the not-yet-launched job `p` of the same camera (GOP catch-up collapse).
@@ -144,7 +149,9 @@ class Camera {
   bool make_job(const AuPtr& au, DecodeJob& job);
 
   // --- stats ---
-  std::atomic<u64> packets{0}, decoded{0}, skipped{0}, errors{0}, bytes_in{0};
+  // decoded = frames published to the ring; pictures = pictures reconstructed (general path: a
+  // picture can be reconstructed in one job and output by a later one)
+  std::atomic<u64> packets{0}, decoded{0}, skipped{0}, errors{0}, bytes_in{0}, pictures{0};
   // packet arrival -> frame published (ms) histogram, upper bounds kLatBucketsMs (+inf last)
   static constexpr int kLatBuckets = 12;
   static constexpr double kLatBucketsMs[kLatBuckets - 1] = {1, 2, 5, 10, 20, 35, 50, 100, 250, 500, 1000};
@@ -275,6 +282,7 @@ class Worker {
   // after an error, camera removed)
   u64 frames() const { return frames_.load(); }
   u64 dropped() const { return dropped_.load(); }
+  u64 pictures() const { return pictures_.load(); }  // pictures reconstructed
   // GPU time of the batches (first event to last, per lane; the busiest lane's total)
   double gpu_ms_total() const;
   // clock64() phase accumulators of the wavefront kernels (VEP_AVC_PROF=1; gpu::kAvcProfSlots)
@@ -372,7 +380,7 @@ class Worker {
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;
-  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0};
+  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0};
   std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0};
   std::mutex timers_mu_;
   bool direct_reads_ = false;

@@ -79,7 +79,9 @@ def test_worker_cpu_lazy_catch_up_matches_oracle(native):
     assert np.array_equal(got, wants[-1])
 
 
-def test_cabac_stream_reports_unsupported(native):
+def test_cavlc_slices_read_as_cabac_fail_cleanly(native):
+    """A PPS flipped to entropy_coding_mode_flag = 1 makes the CAVLC slice data garbage for the
+    CABAC decoder: it must be reported as an error (never a crash or a silent bad picture)."""
     enc = synth(native, 64, 64, compressed=True)
     au = enc.next()
     nals = au.nals()
@@ -87,7 +89,7 @@ def test_cabac_stream_reports_unsupported(native):
     # entropy_coding_mode_flag is the bit after pps_id ue(0)='1' and sps_id ue(0)='1'
     pps[1] |= 0x20
     bad = native.AccessUnit.from_nals([nals[0], bytes(pps)] + nals[2:], keyframe=True)
-    with pytest.raises(native.UnsupportedStream):
+    with pytest.raises((native.UnsupportedStream, native.NativeError)):
         native.CpuDecoder().decode(bad)
 
 

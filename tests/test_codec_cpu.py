@@ -76,15 +76,43 @@ def test_emulation_prevention_in_stream(native):
     assert seen > 0
 
 
+def _sps_interlaced():
+    """An SPS RBSP (with NAL header) for an interlaced (field-coded) 64x64 Main-profile stream."""
+    bits = []
+
+    def u(n, v):
+        bits.extend((v >> (n - 1 - i)) & 1 for i in range(n))
+
+    def ue(v):
+        x = v + 1
+        n = x.bit_length()
+        u(n - 1, 0)
+        u(n, x)
+
+    u(8, 0x67)
+    u(8, 77), u(8, 0), u(8, 40)
+    ue(0)           # sps_id
+    ue(0)           # log2_max_frame_num - 4
+    ue(2)           # pic_order_cnt_type
+    ue(1)           # max_num_ref_frames
+    u(1, 0)         # gaps
+    ue(3), ue(1)    # 4 MBs wide, 2 map units (64x64 frame)
+    u(1, 0)         # frame_mbs_only_flag = 0 -> interlaced
+    u(1, 0)         # mb_adaptive_frame_field_flag
+    u(1, 1)         # direct_8x8_inference
+    u(1, 0), u(1, 0)  # no crop, no VUI
+    u(1, 1)
+    while len(bits) % 8:
+        bits.append(0)
+    return bytes(int("".join(map(str, bits[i:i + 8])), 2) for i in range(0, len(bits), 8))
+
+
 def test_unsupported_stream_is_reported(native):
-    # CABAC PPS: entropy_coding_mode_flag = 1 -> the native subset decoder must refuse loudly
+    # interlaced coding is outside the native decoder: it must refuse loudly (VCN backend's job)
     enc = synth(native, 64, 48)
     au = enc.next()
     nals = au.nals()
-    pps = bytearray(nals[1])
-    # pps_id ue(0)=1, sps_id ue(0)=1, next bit = entropy_coding_mode_flag
-    pps[1] |= 0x20
-    bad = native.AccessUnit.from_nals([nals[0], bytes(pps), nals[2]], keyframe=True)
+    bad = native.AccessUnit.from_nals([_sps_interlaced(), nals[1], nals[2]], keyframe=True)
     with pytest.raises(native.UnsupportedStream):
         native.CpuDecoder().decode(bad)
 
