@@ -103,6 +103,20 @@ struct CpuDecoder {
         avc::cpu_reconstruct(*pic, slots);
         coded = pic->info.coded_mbs;
         pictures.push_back(pic->info);
+        for (const avc::MbRec& m : pic->mbs) {
+          ++kinds[m.kind];
+          if (m.flags & avc::kMbT8x8) ++t8x8;
+          if (m.flags & avc::kMbWp) ++weighted;
+          if (m.kind <= avc::kInter) {
+            bool bi = false, l1only = false;
+            for (int k = 0; k < 4; ++k) {
+              bi |= m.ref[k] != 0xFF && m.ref1[k] != 0xFF;
+              l1only |= m.ref[k] == 0xFF && m.ref1[k] != 0xFF;
+            }
+            bipred += bi;
+            list1_only += l1only;
+          }
+        }
         // B-frame reordering: the newest frame that left the reorder buffer, if any
         if (pic->outputs.empty()) return py::none();
         last = pic->outputs.back().info;
@@ -127,6 +141,9 @@ struct CpuDecoder {
     return out_list;
   }
   std::vector<PictureInfo> pictures;      // every decoded picture (decoding order)
+  // macroblock statistics over every decoded picture (coverage checks)
+  u64 kinds[6] = {0, 0, 0, 0, 0, 0};
+  u64 t8x8 = 0, weighted = 0, bipred = 0, list1_only = 0;
   std::vector<avc::OutFrame> pending_outputs;  // outputs of the last decode() (output order)
   int last_poc = 0;
 };
@@ -233,6 +250,19 @@ PYBIND11_MODULE(_vep, m) {
       .def("decode", &CpuDecoder::decode)
       .def("flush", &CpuDecoder::flush)
       .def_property_readonly("last_poc", [](const CpuDecoder& d) { return d.last_poc; })
+      .def_property_readonly("mb_stats", [](const CpuDecoder& d) {
+        py::dict r;
+        const char* names[6] = {"skip", "inter", "i4x4", "i16x16", "pcm", "i8x8"};
+        for (int k = 0; k < 6; ++k) r[names[k]] = d.kinds[k];
+        r["t8x8"] = d.t8x8;
+        r["weighted"] = d.weighted;
+        r["bipred"] = d.bipred;
+        r["list1_only"] = d.list1_only;
+        std::string types;
+        for (const auto& p : d.pictures) types += p.pict_type;
+        r["types"] = types;
+        return r;
+      })
       .def_property_readonly("outputs_last", [](const CpuDecoder& d) { return int(d.pending_outputs.size()); })
       .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
       .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.coded; })

@@ -130,3 +130,28 @@ def test_corrupt_slices_on_gpu_recover_at_idr(native):
                 assert ok, f"trial {trial}: frame {i} after the IDR was dropped"
                 _, got = wk.read_latest(cam, 0)
                 assert np.array_equal(got, want[i]), f"trial {trial}: frame {i} differs"
+
+
+CLIP = "/opt/conda/lib/python3.9/site-packages/imageio/resources/images/realshort.mp4"
+
+
+@pytest.mark.skipif(not __import__("os").path.exists(CLIP), reason="imageio sample clip not in this image")
+def test_third_party_high_profile_clip_bit_exact_vs_cpu(native):
+    """A real High-profile CABAC clip (8x8 transform, Intra_8x8 / 4x4, P pictures): every frame
+    the GPU worker publishes equals the CPU reference decoder's, bit-exact."""
+    from video_edge_ai_proxy_amd.utils import mp4
+
+    buf = open(CLIP, "rb").read()
+    tr = mp4.parse(buf)
+    ref = native.CpuDecoder()
+    wk = native.Worker(device=0)
+    cam = wk.add_camera("clip", 3)
+    for i, (nals, key, dts, pts) in enumerate(mp4.samples(buf, tr)):
+        au = native.AccessUnit.from_nals((tr.param_sets if i == 0 else []) + nals, keyframe=key, pts=pts, dts=dts)
+        want = ref.decode(au)
+        assert wk.decode_now(cam, au)
+        _, got = wk.read_latest(cam, 0)
+        assert np.array_equal(got, want), f"frame {i} differs in {int((got != want).sum())} samples"
+    st = ref.mb_stats
+    assert st["i8x8"] > 0 and st["t8x8"] > 0
+    assert wk.stats(cam)["decoder"] == "general"
