@@ -78,6 +78,7 @@ struct CpuDecoder {
   int coded = 0;
   const HostSurface& out() const { return general ? slots[size_t(target)] : surf; }
   py::object decode(const AccessUnit& au) {
+    bool no_output = false;
     {
       py::gil_scoped_release nogil;
       bool done = false;
@@ -118,16 +119,34 @@ struct CpuDecoder {
           }
         }
         // B-frame reordering: the newest frame that left the reorder buffer, if any
-        if (pic->outputs.empty()) return py::none();
-        last = pic->outputs.back().info;
-        target = pic->outputs.back().slot;
-        last_poc = pic->outputs.back().poc;
         pending_outputs = pic->outputs;
+        no_output = pic->outputs.empty();
+        if (!no_output) {
+          last = pic->outputs.back().info;
+          target = pic->outputs.back().slot;
+          last_poc = pic->outputs.back().poc;
+          last_pts = pic->outputs.back().au.pts;
+        }
       }
     }
+    if (no_output) return py::none();
     py::array_t<uint8_t> o({last.height, last.width, 3});
     cpu_nv12_to_bgr(out(), last.crop_left, last.crop_top, last.width, last.height, o.mutable_data());
     return o;
+  }
+  // Every frame that left the reorder buffer with the last decode() (or, after flush_frames(),
+  // at end of stream): [(pts, (Y, UV) coded NV12 planes)] in output order.
+  py::list frames_of(const std::vector<avc::OutFrame>& fs) const {
+    py::list l;
+    for (const auto& f : fs) {
+      const HostSurface& s = slots[size_t(f.slot)];
+      py::array_t<uint8_t> y({s.coded_h, s.coded_w});
+      py::array_t<uint8_t> uv({s.coded_h / 2, s.coded_w});
+      std::memcpy(y.mutable_data(), s.y.data(), s.y.size());
+      std::memcpy(uv.mutable_data(), s.uv.data(), s.uv.size());
+      l.append(py::make_tuple(f.au.pts, py::make_tuple(y, uv)));
+    }
+    return l;
   }
   // Frames still in the reorder buffer (end of stream), oldest first.
   py::list flush() {
@@ -146,6 +165,7 @@ struct CpuDecoder {
   u64 t8x8 = 0, weighted = 0, bipred = 0, list1_only = 0;
   std::vector<avc::OutFrame> pending_outputs;  // outputs of the last decode() (output order)
   int last_poc = 0;
+  i64 last_pts = 0;
 };
 
 PYBIND11_MODULE(_vep, m) {
@@ -175,6 +195,12 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("coverage", &SynthConfig::coverage)
       .def_readwrite("noise", &SynthConfig::noise)
       .def_readwrite("temporal_noise", &SynthConfig::temporal_noise)
+      .def_readwrite("profile", &SynthConfig::profile)
+      .def_readwrite("bframes", &SynthConfig::bframes)
+      .def_readwrite("cabac", &SynthConfig::cabac)
+      .def_readwrite("weighted_p", &SynthConfig::weighted_p)
+      .def_readwrite("weighted_b", &SynthConfig::weighted_b)
+      .def_readwrite("direct_spatial", &SynthConfig::direct_spatial)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -242,14 +268,62 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("sps_nal", [](const SynthH264& s) { return to_bytes(s.sps_nal().data(), s.sps_nal().size()); })
       .def_property_readonly("pps_nal", [](const SynthH264& s) { return to_bytes(s.pps_nal().data(), s.pps_nal().size()); })
       .def_property_readonly("vps_nal", [](const SynthH264& s) { return to_bytes(s.vps_nal().data(), s.vps_nal().size()); })
-      .def_property_readonly("frame_index", &SynthH264::frame_index);
+      .def_property_readonly("frame_index", &SynthH264::frame_index)
+      .def_property_readonly("last_pts", &SynthH264::last_pts);
   m.attr("SynthEncoder") = m.attr("SynthH264");
+
+  auto surface_tuple = [](const HostSurface& p) {
+    py::array_t<uint8_t> y({p.coded_h, p.coded_w});
+    py::array_t<uint8_t> uv({p.coded_h / 2, p.coded_w});
+    std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
+    std::memcpy(uv.mutable_data(), p.uv.data(), p.uv.size());
+    return py::make_tuple(y, uv);
+  };
+  py::class_<avc::AvcHighConfig>(m, "AvcHighConfig")
+      .def(py::init<>())
+      .def_readwrite("width", &avc::AvcHighConfig::width)
+      .def_readwrite("height", &avc::AvcHighConfig::height)
+      .def_readwrite("fps", &avc::AvcHighConfig::fps)
+      .def_readwrite("gop", &avc::AvcHighConfig::gop)
+      .def_readwrite("idr_phase", &avc::AvcHighConfig::idr_phase)
+      .def_readwrite("bframes", &avc::AvcHighConfig::bframes)
+      .def_readwrite("pyramid", &avc::AvcHighConfig::pyramid)
+      .def_readwrite("refs", &avc::AvcHighConfig::refs)
+      .def_readwrite("qp", &avc::AvcHighConfig::qp)
+      .def_readwrite("cabac", &avc::AvcHighConfig::cabac)
+      .def_readwrite("t8x8", &avc::AvcHighConfig::t8x8)
+      .def_readwrite("weighted_p", &avc::AvcHighConfig::weighted_p)
+      .def_readwrite("weighted_b", &avc::AvcHighConfig::weighted_b)
+      .def_readwrite("direct_spatial", &avc::AvcHighConfig::direct_spatial)
+      .def_readwrite("scaling", &avc::AvcHighConfig::scaling)
+      .def_readwrite("slices", &avc::AvcHighConfig::slices)
+      .def_readwrite("deblock_idc", &avc::AvcHighConfig::deblock_idc)
+      .def_readwrite("chroma_qp_offset", &avc::AvcHighConfig::chroma_qp_offset)
+      .def_readwrite("second_chroma_qp_offset", &avc::AvcHighConfig::second_chroma_qp_offset)
+      .def_readwrite("coverage", &avc::AvcHighConfig::coverage)
+      .def_readwrite("objects", &avc::AvcHighConfig::objects)
+      .def_readwrite("noise", &avc::AvcHighConfig::noise)
+      .def_readwrite("temporal_noise", &avc::AvcHighConfig::temporal_noise)
+      .def_readwrite("seed", &avc::AvcHighConfig::seed);
+  py::class_<avc::AvcHighEncoder>(m, "AvcHighEncoder")
+      .def(py::init<const avc::AvcHighConfig&>())
+      .def("next", &avc::AvcHighEncoder::next, py::call_guard<py::gil_scoped_release>())
+      .def("picture", [surface_tuple](const avc::AvcHighEncoder& e) { return surface_tuple(e.reconstruction()); })
+      .def("source", [surface_tuple](const avc::AvcHighEncoder& e) { return surface_tuple(e.source()); })
+      .def_property_readonly("last_pts", &avc::AvcHighEncoder::last_pts)
+      .def_property_readonly("last_type", [](const avc::AvcHighEncoder& e) { return std::string(1, e.last_type()); })
+      .def_property_readonly("last_display_index", &avc::AvcHighEncoder::last_display_index)
+      .def_property_readonly("sps_nal", [](const avc::AvcHighEncoder& e) { return to_bytes(e.sps_nal().data(), e.sps_nal().size()); })
+      .def_property_readonly("pps_nal", [](const avc::AvcHighEncoder& e) { return to_bytes(e.pps_nal().data(), e.pps_nal().size()); });
 
   py::class_<CpuDecoder>(m, "CpuDecoder")
       .def(py::init<>())
       .def("decode", &CpuDecoder::decode)
       .def("flush", &CpuDecoder::flush)
+      .def("frames", [](CpuDecoder& d) { return d.general ? d.frames_of(d.pending_outputs) : py::list(); })
+      .def("flush_frames", [](CpuDecoder& d) { return d.frames_of(d.avc.flush_output()); })
       .def_property_readonly("last_poc", [](const CpuDecoder& d) { return d.last_poc; })
+      .def_property_readonly("last_pts", [](const CpuDecoder& d) { return d.last_pts; })
       .def_property_readonly("mb_stats", [](const CpuDecoder& d) {
         py::dict r;
         const char* names[6] = {"skip", "inter", "i4x4", "i16x16", "pcm", "i8x8"};

@@ -1213,31 +1213,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   const u32 uid = next_uid_++;
   if (first.nal_ref_idc != 0) {
     std::shared_ptr<ColMotion> col;
-    if (act_sps->profile_idc != 66) {  // B slices possible: keep the motion for direct prediction
-      col = std::make_shared<ColMotion>();
-      col->wmbs = pic->wmbs;
-      col->hmbs = pic->hmbs;
-      const size_t nb = size_t(pic->nmbs()) * 16;
-      col->mv.assign(nb * 2, 0);
-      col->ref.assign(nb, i8(-1));
-      col->pid.assign(nb, 0u);
-      for (int mb = 0; mb < pic->nmbs(); ++mb) {
-        const MbState& st = nb_.at(mb);
-        if (st.kind == 0xFF || is_intra(st.kind)) continue;
-        const auto& lu = slice_uids[std::min<size_t>(st.slice, slice_uids.size() - 1)];
-        for (int blk = 0; blk < 16; ++blk) {
-          const int b8 = ((blk >> 3) << 1) | ((blk & 3) >> 1);
-          const int l = st.ref[0][b8] >= 0 ? 0 : 1;
-          const int ri = st.ref[l][b8];
-          if (ri < 0) continue;
-          const size_t k = size_t(mb) * 16 + size_t(blk);
-          col->mv[k * 2] = st.mv[l][blk][0];
-          col->mv[k * 2 + 1] = st.mv[l][blk][1];
-          col->ref[k] = i8(ri);
-          col->pid[k] = size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u;
-        }
-      }
-    }
+    if (act_sps->profile_idc != 66)  // B slices possible: keep the motion for direct prediction
+      col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids);
     mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col));
   }
   bump(*pic, first.idr() || first.has_mmco5());
@@ -1287,6 +1264,66 @@ void validate(const Picture& p) {
 }
 
 // ------------------------------------------------------------------------- shared internals
+
+std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, int hmbs,
+                                            const std::vector<std::array<std::vector<u32>, 2>>& slice_uids) {
+  auto col = std::make_shared<ColMotion>();
+  col->wmbs = wmbs;
+  col->hmbs = hmbs;
+  const size_t n = size_t(wmbs) * hmbs * 16;
+  col->mv.assign(n * 2, 0);
+  col->ref.assign(n, i8(-1));
+  col->pid.assign(n, 0u);
+  for (int mb = 0; mb < wmbs * hmbs; ++mb) {
+    const MbState& st = nb.at(mb);
+    if (st.kind == 0xFF || is_intra(st.kind) || slice_uids.empty()) continue;
+    const auto& lu = slice_uids[std::min<size_t>(st.slice, slice_uids.size() - 1)];
+    for (int blk = 0; blk < 16; ++blk) {
+      const int b8 = ((blk >> 3) << 1) | ((blk & 3) >> 1);
+      const int l = st.ref[0][b8] >= 0 ? 0 : 1;
+      const int ri = st.ref[l][b8];
+      if (ri < 0) continue;
+      const size_t k = size_t(mb) * 16 + size_t(blk);
+      col->mv[k * 2] = st.mv[l][blk][0];
+      col->mv[k * 2 + 1] = st.mv[l][blk][1];
+      col->ref[k] = i8(ri);
+      col->pid[k] = size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u;
+    }
+  }
+  return col;
+}
+
+void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
+                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64]) {
+  const int pitch = slots[0].coded_w, wpx = pitch, hpx = slots[0].coded_h;
+  for (int y = 0; y < 16; ++y)
+    for (int x = 0; x < 16; ++x) {
+      const int r = (y >> 2) * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
+      const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+      int p0 = 0, p1 = 0;
+      if (s0 != 0xFF)
+        p0 = luma_qpel(slots[size_t(s0)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * r] >> 2),
+                       my * 16 + y + (mv0[2 * r + 1] >> 2), mv0[2 * r] & 3, mv0[2 * r + 1] & 3);
+      if (s1 != 0xFF)
+        p1 = luma_qpel(slots[size_t(s1)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * r] >> 2),
+                       my * 16 + y + (mv1[2 * r + 1] >> 2), mv1[2 * r] & 3, mv1[2 * r + 1] & 3);
+      py[y * 16 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 0);
+    }
+  for (int c = 0; c < 2; ++c)
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x) {
+        const int r = (y >> 1) * 4 + (x >> 1), b8 = ((y >> 2) << 1) | (x >> 2);
+        const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+        int p0 = 0, p1 = 0;
+        if (s0 != 0xFF)
+          p0 = chroma_epel(slots[size_t(s0)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
+                           my * 8 + y + (mv0[2 * r + 1] >> 3), mv0[2 * r] & 7, mv0[2 * r + 1] & 7);
+        if (s1 != 0xFF)
+          p1 = chroma_epel(slots[size_t(s1)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
+                           my * 8 + y + (mv1[2 * r + 1] >> 3), mv1[2 * r] & 7, mv1[2 * r + 1] & 7);
+        pc[c][y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c);
+      }
+}
 
 void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& res) {
   // (§8.5.6 - §8.5.12.1) scan-order levels -> dequantised raster 4x4 blocks; blocks without
@@ -1486,39 +1523,12 @@ struct Recon {
     const i16* mv0 = &pic.mvs[size_t(m.mv) * 32];
     const i16* mv1 = (m.flags & kMbL1) ? mv0 + 32 : nullptr;
     const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
-    int res[256];
+    int py[256], pc[2][64], res[256];
+    predict_inter(slots, m, mv0, mv1, wp, mx, my, py, pc);
     luma_residual(pic, m, res);
     for (int y = 0; y < 16; ++y)
-      for (int x = 0; x < 16; ++x) {
-        const int r = (y >> 2) * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
-        const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
-        int p0 = 0, p1 = 0;
-        if (s0 != 0xFF)
-          p0 = luma_qpel(slots[size_t(s0)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * r] >> 2),
-                         my * 16 + y + (mv0[2 * r + 1] >> 2), mv0[2 * r] & 3, mv0[2 * r + 1] & 3);
-        if (s1 != 0xFF)
-          p1 = luma_qpel(slots[size_t(s1)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * r] >> 2),
-                         my * 16 + y + (mv1[2 * r + 1] >> 2), mv1[2 * r] & 3, mv1[2 * r + 1] & 3);
-        const int pr = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 0);
-        Y(mx * 16 + x, my * 16 + y) = u8(clip1(pr + res[y * 16 + x]));
-      }
-    for (int c = 0; c < 2; ++c) {
-      int cp[64];
-      for (int y = 0; y < 8; ++y)
-        for (int x = 0; x < 8; ++x) {
-          const int r = (y >> 1) * 4 + (x >> 1), b8 = ((y >> 2) << 1) | (x >> 2);
-          const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
-          int p0 = 0, p1 = 0;
-          if (s0 != 0xFF)
-            p0 = chroma_epel(slots[size_t(s0)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
-                             my * 8 + y + (mv0[2 * r + 1] >> 3), mv0[2 * r] & 7, mv0[2 * r + 1] & 7);
-          if (s1 != 0xFF)
-            p1 = chroma_epel(slots[size_t(s1)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
-                             my * 8 + y + (mv1[2 * r + 1] >> 3), mv1[2 * r] & 7, mv1[2 * r + 1] & 7);
-          cp[y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c);
-        }
-      chroma_store(m, mx, my, c, cp);
-    }
+      for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = u8(clip1(py[y * 16 + x] + res[y * 16 + x]));
+    for (int c = 0; c < 2; ++c) chroma_store(m, mx, my, c, pc[c]);
   }
 
   void pcm(const MbRec& m, int mx, int my) {

@@ -343,7 +343,22 @@ void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, 
 void intra8x8_neighbours(const Picture& pic, int mb, int q, const HostSurface& T, int* f, bool& has_top,
                          bool& has_left);
 
-// ------------------------------------------------------------------------------ encoder
+// ------------------------------------------------------------------------------ encoders
+// What the synthetic camera (synth.h) needs from an encoder.
+class StreamEncoder {
+ public:
+  virtual ~StreamEncoder() = default;
+  virtual std::shared_ptr<AccessUnit> next() = 0;
+  // Encoder's own reconstruction of the last coded picture (what a conformant decoder must
+  // output for it) and the source picture that was encoded (for PSNR).
+  virtual const HostSurface& reconstruction() const = 0;
+  virtual const HostSurface& source() const = 0;
+  virtual i64 last_pts() const = 0;  // pts of the last access unit (B pictures: display time)
+  // Escaped parameter-set NALs (what the muxers put in avcC / the FLV sequence header).
+  virtual const std::vector<u8>& sps_nal() const = 0;
+  virtual const std::vector<u8>& pps_nal() const = 0;
+};
+
 // Closed-loop synthetic H.264 encoder (CAVLC I/P): intra 16x16 / 4x4 and chroma prediction,
 // motion-compensated P macroblocks (16x16, 16x8, 8x16, 8x8 with sub-partitions, P_Skip),
 // multiple reference frames, residual coding and the deblocking filter — a real compressed
@@ -369,23 +384,70 @@ struct AvcEncConfig {
   double temporal_noise = 0; // per-frame sensor noise amplitude (drives P-picture residual bits)
 };
 
-class AvcEncoder {
+class AvcEncoder : public StreamEncoder {
  public:
   explicit AvcEncoder(const AvcEncConfig& cfg);
-  ~AvcEncoder();
-  std::shared_ptr<AccessUnit> next();
-  // Encoder's own reconstruction of the last picture (what a conformant decoder must output).
-  const HostSurface& reconstruction() const;
-  // The source picture that was encoded (for PSNR).
-  const HostSurface& source() const;
+  ~AvcEncoder() override;
+  std::shared_ptr<AccessUnit> next() override;
+  const HostSurface& reconstruction() const override;
+  const HostSurface& source() const override;
+  i64 last_pts() const override;
   const AvcEncConfig& config() const { return cfg_; }
-  // Escaped parameter-set NALs (what the muxers put in avcC / the FLV sequence header).
-  const std::vector<u8>& sps_nal() const;
-  const std::vector<u8>& pps_nal() const;
+  const std::vector<u8>& sps_nal() const override;
+  const std::vector<u8>& pps_nal() const override;
 
  private:
   struct Impl;
   AvcEncConfig cfg_;
+  std::unique_ptr<Impl> p_;
+};
+
+// Closed-loop synthetic H.264 Main / High-profile encoder (avc_enc_high.cpp): CABAC or CAVLC;
+// I, P and B pictures in mini-GOPs (anchor P, then the B pictures, the middle one a reference
+// when `pyramid`); 8x8 transform with Intra_8x8; spatial / temporal direct; explicit (P and B)
+// or implicit (B) weighted prediction; explicit scaling matrices. Every macroblock is written
+// by the decoder's own macroblock layer and reconstructed by its reconstruction, so the
+// encoder's pictures are what a conforming decoder outputs.
+struct AvcHighConfig {
+  int width = 640, height = 480;
+  int fps = 30, gop = 30;
+  int idr_phase = 0;          // IDR when display index 0 or (index + idr_phase) % gop == 0
+  int bframes = 2;            // B pictures between anchors (0..4)
+  bool pyramid = true;        // middle B of each mini-GOP is a reference (bframes >= 2)
+  int refs = 2;               // P reference pictures searched / listed (1..8)
+  int qp = 28;                // I / P; B pictures +1 (reference) / +2
+  bool cabac = true;
+  bool t8x8 = true;           // High profile: transform_8x8_mode + Intra_8x8
+  bool weighted_p = false;    // explicit weighted prediction in P slices
+  int weighted_b = 0;         // weighted_bipred_idc: 0 default, 1 explicit, 2 implicit
+  bool direct_spatial = true; // B direct mode (false: temporal)
+  bool scaling = false;       // explicit (non-flat) sequence scaling matrices
+  int slices = 1;             // per picture (MB-row aligned)
+  int deblock_idc = 0;
+  int chroma_qp_offset = 0, second_chroma_qp_offset = 0;
+  bool coverage = false;      // randomised decisions: every MB / sub-MB type, mode, transform
+  int objects = 3;
+  double noise = 3.0, temporal_noise = 0.0;
+  u64 seed = 1;
+};
+
+class AvcHighEncoder : public StreamEncoder {
+ public:
+  explicit AvcHighEncoder(const AvcHighConfig& cfg);
+  ~AvcHighEncoder() override;
+  std::shared_ptr<AccessUnit> next() override;  // coding order
+  const HostSurface& reconstruction() const override;
+  const HostSurface& source() const override;
+  i64 last_pts() const override;
+  i64 last_display_index() const;
+  char last_type() const;  // 'I' / 'P' / 'B'
+  const AvcHighConfig& config() const { return cfg_; }
+  const std::vector<u8>& sps_nal() const override;
+  const std::vector<u8>& pps_nal() const override;
+
+ private:
+  struct Impl;
+  AvcHighConfig cfg_;
   std::unique_ptr<Impl> p_;
 };
 

@@ -10,70 +10,12 @@
 
 #include "avc.h"
 #include "avc_cavlc.h"
+#include "avc_scene.h"
 #include "h264.h"
 
 namespace vep::avc {
 
 namespace {
-
-const int kMF[6][3] = {{13107, 5243, 8066}, {11916, 4660, 7490}, {10082, 4194, 6554},
-                       {9362, 3647, 5825},  {8192, 3355, 5243},  {7282, 2893, 4559}};
-
-int mf_class(int pos) {
-  const int i = pos >> 2, j = pos & 3;
-  return (!(i & 1) && !(j & 1)) ? 0 : ((i & 1) && (j & 1)) ? 1 : 2;
-}
-
-// Forward core transform W = Cf X Cf^T (raster in, raster out).
-void fwd4x4(const int* x, int* w) {
-  int t[16];
-  for (int i = 0; i < 4; ++i) {
-    const int a = x[i * 4], b = x[i * 4 + 1], c = x[i * 4 + 2], d = x[i * 4 + 3];
-    const int s03 = a + d, d03 = a - d, s12 = b + c, d12 = b - c;
-    t[i * 4] = s03 + s12;
-    t[i * 4 + 1] = 2 * d03 + d12;
-    t[i * 4 + 2] = s03 - s12;
-    t[i * 4 + 3] = d03 - 2 * d12;
-  }
-  for (int j = 0; j < 4; ++j) {
-    const int a = t[j], b = t[4 + j], c = t[8 + j], d = t[12 + j];
-    const int s03 = a + d, d03 = a - d, s12 = b + c, d12 = b - c;
-    w[j] = s03 + s12;
-    w[4 + j] = 2 * d03 + d12;
-    w[8 + j] = s03 - s12;
-    w[12 + j] = d03 - 2 * d12;
-  }
-}
-
-int quant(int w, int qp, int cls, bool intra, int extra_shift = 0) {
-  const int qbits = 15 + qp / 6 + extra_shift;
-  const int f = (1 << qbits) / (intra ? 3 : 6);
-  const long long a = (static_cast<long long>(w < 0 ? -w : w) * kMF[qp % 6][cls] + f) >> qbits;
-  const int l = int(a > 2047 ? 2047 : a);
-  return w < 0 ? -l : l;
-}
-
-struct Rng {
-  u64 s;
-  u64 next() {
-    s ^= s << 13;
-    s ^= s >> 7;
-    s ^= s << 17;
-    return s;
-  }
-  int uni(int n) { return int(next() % u64(n)); }
-  bool chance(int pct) { return uni(100) < pct; }
-};
-
-u32 hash2(u32 x, u32 y, u32 seed) {
-  u32 h = x * 0x8da6b343u ^ y * 0xd8163841u ^ seed * 0xcb1ab31fu;
-  h ^= h >> 13;
-  h *= 0x5bd1e995u;
-  h ^= h >> 15;
-  return h;
-}
-
-u8 sat8(double v) { return u8(v < 0 ? 0 : v > 255 ? 255 : int(v + 0.5)); }
 
 }  // namespace
 
@@ -83,7 +25,8 @@ struct AvcEncoder::Impl {
   h264::Sps sps;
   std::vector<u8> sps_nal, pps_nal;
   int W = 0, H = 0, wpx = 0, hpx = 0;
-  HostSurface bg, src;
+  Scene scene;
+  const HostSurface& src = scene.src;
   std::vector<HostSurface> slots;
   struct Ref {
     int slot;
@@ -92,14 +35,6 @@ struct AvcEncoder::Impl {
   std::vector<Ref> refs;  // most recent first (= list 0 order without modifications)
   Picture pic;
   MbNeighbours nb;
-  struct Obj {
-    double x, y, vx, vy;
-    int w, h;
-    bool ellipse;
-    double p1, p2, p3;
-    int by, bu, bv;
-  };
-  std::vector<Obj> objs;
   i64 frame = -1;
   int next_fn = 0, idr_id = -1, gop_pos = 0;
   // per-slice state
@@ -153,95 +88,7 @@ struct AvcEncoder::Impl {
     rbsp_to_ebsp(pw.buf().data(), pw.buf().size(), pps_nal);
     slots.resize(size_t(c.refs) + 1);
     for (auto& s : slots) s.alloc(wpx, hpx);
-    make_scene();
-  }
-
-  // ------------------------------------------------------------------ scene
-  void make_scene() {
-    bg.alloc(wpx, hpx);
-    src.alloc(wpx, hpx);
-    const u32 seed = u32(cfg.seed * 2654435761u);
-    for (int y = 0; y < hpx; ++y)
-      for (int x = 0; x < wpx; ++x) {
-        const double v = 70 + 60 * (0.5 + 0.5 * std::sin(x * 0.011 + y * 0.004 + seed % 7)) +
-                         40.0 * y / hpx + cfg.noise * ((hash2(u32(x), u32(y), seed) & 255) / 128.0 - 1.0);
-        bg.y[size_t(y) * wpx + x] = sat8(v);
-      }
-    for (int y = 0; y < hpx / 2; ++y)
-      for (int x = 0; x < wpx / 2; ++x) {
-        bg.uv[size_t(y) * wpx + 2 * x] = sat8(128 + 25 * std::sin(x * 0.02 + seed % 5));
-        bg.uv[size_t(y) * wpx + 2 * x + 1] = sat8(128 + 25 * std::cos(y * 0.017 + seed % 3));
-      }
-    const double speeds[] = {0.75, 1.25, 2.0, 2.5, 3.25, 1.0, 4.5};
-    for (int i = 0; i < cfg.objects; ++i) {
-      Obj o;
-      o.w = std::max(16, cfg.width / (4 + rng.uni(5)));
-      o.h = std::max(16, cfg.height / (4 + rng.uni(5)));
-      o.x = rng.uni(std::max(1, cfg.width - o.w));
-      o.y = rng.uni(std::max(1, cfg.height - o.h));
-      o.vx = speeds[rng.uni(7)] * (rng.uni(2) ? 1 : -1);
-      o.vy = speeds[rng.uni(7)] * (rng.uni(2) ? 1 : -1) * 0.5;
-      o.ellipse = rng.uni(2);
-      o.p1 = 0.05 + rng.uni(100) * 0.003;
-      o.p2 = 0.04 + rng.uni(100) * 0.003;
-      o.p3 = 0.02 + rng.uni(100) * 0.002;
-      o.by = 60 + rng.uni(140);
-      o.bu = 90 + rng.uni(80);
-      o.bv = 90 + rng.uni(80);
-      objs.push_back(o);
-    }
-  }
-
-  bool inside(const Obj& o, double lx, double ly) const {
-    if (lx < 0 || ly < 0 || lx >= o.w || ly >= o.h) return false;
-    if (!o.ellipse) return true;
-    const double dx = (lx - o.w / 2.0) / (o.w / 2.0), dy = (ly - o.h / 2.0) / (o.h / 2.0);
-    return dx * dx + dy * dy <= 1.0;
-  }
-
-  void render() {
-    src.y = bg.y;
-    src.uv = bg.uv;
-    for (const Obj& o : objs) {
-      const int x0 = std::max(0, int(std::floor(o.x))), y0 = std::max(0, int(std::floor(o.y)));
-      const int x1 = std::min(cfg.width, int(std::ceil(o.x + o.w)) + 1);
-      const int y1 = std::min(cfg.height, int(std::ceil(o.y + o.h)) + 1);
-      for (int y = y0; y < y1; ++y)
-        for (int x = x0; x < x1; ++x) {
-          const double lx = x - o.x, ly = y - o.y;
-          if (!inside(o, lx, ly)) continue;
-          src.y[size_t(y) * wpx + x] =
-              sat8(o.by + 50 * std::sin(lx * o.p1) * std::cos(ly * o.p2) + 25 * std::sin((lx + ly) * o.p3));
-        }
-      for (int y = y0 / 2; y < (y1 + 1) / 2; ++y)
-        for (int x = x0 / 2; x < (x1 + 1) / 2; ++x) {
-          const double lx = 2 * x - o.x, ly = 2 * y - o.y;
-          if (!inside(o, lx, ly)) continue;
-          src.uv[size_t(y) * wpx + 2 * x] = sat8(o.bu + 20 * std::sin(lx * o.p2));
-          src.uv[size_t(y) * wpx + 2 * x + 1] = sat8(o.bv + 20 * std::cos(ly * o.p1));
-        }
-    }
-  }
-
-  void add_sensor_noise() {
-    if (cfg.temporal_noise <= 0) return;
-    const u32 seed = u32(frame * 0x9E3779B1u) ^ u32(cfg.seed);
-    const int amp = int(cfg.temporal_noise * 2) + 1;
-    for (int y = 0; y < hpx; ++y)
-      for (int x = 0; x < wpx; ++x) {
-        u8& p = src.y[size_t(y) * wpx + x];
-        const int n = int(hash2(u32(x), u32(y), seed) % u32(amp)) - amp / 2;
-        p = u8(std::min(255, std::max(0, p + n)));
-      }
-  }
-
-  void advance_scene() {
-    for (Obj& o : objs) {
-      o.x += o.vx;
-      o.y += o.vy;
-      if (o.x < -o.w / 2.0 || o.x + o.w / 2.0 > cfg.width) o.vx = -o.vx;
-      if (o.y < -o.h / 2.0 || o.y + o.h / 2.0 > cfg.height) o.vy = -o.vy;
-    }
+    scene.make(SceneConfig{c.width, c.height, wpx, hpx, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
   }
 
   // ------------------------------------------------------------------ helpers
@@ -674,7 +521,7 @@ struct AvcEncoder::Impl {
     int p[2];
     nb.pred_mv(mb, 0, 0, 4, 4, 0, ref, 0, 0, p);
     out.push_back({p[0], p[1]});
-    for (const Obj& o : objs) {
+    for (const Scene::Obj& o : scene.objs) {
       if (o.x > mx * 16 + 16 || o.x + o.w < mx * 16 || o.y > my * 16 + 16 || o.y + o.h < my * 16) continue;
       const int k = ref + 1;  // reference k pictures back (ref pictures are consecutive)
       out.push_back({int(std::lround(-o.vx * 4 * k)), int(std::lround(-o.vy * 4 * k))});
@@ -850,9 +697,9 @@ struct AvcEncoder::Impl {
   // ------------------------------------------------------------------ picture
   std::shared_ptr<AccessUnit> next() {
     ++frame;
-    if (frame > 0) advance_scene();
-    render();
-    add_sensor_noise();
+    if (frame > 0) scene.advance();
+    scene.render();
+    scene.add_sensor_noise(frame);
     const bool idr = frame == 0 || (frame + cfg.idr_phase) % std::max(1, cfg.gop) == 0;
     gop_pos = idr ? 1 : gop_pos + 1;
     if (idr) {
@@ -963,6 +810,7 @@ AvcEncoder::~AvcEncoder() = default;
 std::shared_ptr<AccessUnit> AvcEncoder::next() { return p_->next(); }
 const HostSurface& AvcEncoder::reconstruction() const { return p_->slots[size_t(p_->last_target)]; }
 const HostSurface& AvcEncoder::source() const { return p_->src; }
+i64 AvcEncoder::last_pts() const { return p_->frame * (90000 / std::max(1, cfg_.fps)); }
 const std::vector<u8>& AvcEncoder::sps_nal() const { return p_->sps_nal; }
 const std::vector<u8>& AvcEncoder::pps_nal() const { return p_->pps_nal; }
 

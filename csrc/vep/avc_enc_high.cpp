@@ -1,0 +1,1029 @@
+// Closed-loop synthetic H.264 Main / High-profile encoder: CABAC or CAVLC, I / P / B pictures
+// with B-pyramids, 8x8 transform + Intra_8x8, spatial or temporal direct prediction, explicit
+// and implicit weighted prediction, optional scaling matrices. See avc.h (AvcHighEncoder).
+//
+// Every macroblock goes through the decoder's own macroblock layer in write mode
+// (SliceWriter, avc_mb.cpp): the syntax, its context selection, motion-vector prediction, direct
+// derivation, dequantisation and the per-MB records are the decoder's code, and each MB is then
+// reconstructed with the decoder's reconstruction (cpu_reconstruct_mb), so the encoder's
+// reference pictures are by construction what a conforming decoder of the emitted stream
+// reconstructs. Mode decision is SAD-driven with a motion search seeded by the scene's known
+// object motion; `coverage` randomises every decision (all MB / sub-MB types, prediction
+// modes, reference indices, motion phases, transform sizes, levels) for decoder coverage.
+#include <cmath>
+#include <deque>
+#include <map>
+
+#include "avc.h"
+#include "avc_internal.h"
+#include "avc_scene.h"
+#include "h264.h"
+
+namespace vep::avc {
+
+namespace {
+
+// Exact 1-D 8x8 inverse transform matrix (idct8_1d on unit vectors) and its inverse: the 8x8
+// quantiser inverts the decoder's transform numerically, so levels reconstruct to the residual.
+struct Idct8Inverse {
+  double inv[8][8];
+  Idct8Inverse() {
+    double m[8][8];
+    for (int k = 0; k < 8; ++k) {
+      int x[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      x[k] = 1024;
+      idct8_1d(x);
+      for (int i = 0; i < 8; ++i) m[i][k] = x[i] / 1024.0;
+    }
+    double a[8][16];
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 16; ++j) a[i][j] = j < 8 ? m[i][j] : (j - 8 == i ? 1.0 : 0.0);
+    for (int c = 0; c < 8; ++c) {
+      int piv = c;
+      for (int r = c + 1; r < 8; ++r)
+        if (std::fabs(a[r][c]) > std::fabs(a[piv][c])) piv = r;
+      for (int j = 0; j < 16; ++j) std::swap(a[c][j], a[piv][j]);
+      const double d = a[c][c];
+      for (int j = 0; j < 16; ++j) a[c][j] /= d;
+      for (int r = 0; r < 8; ++r) {
+        if (r == c) continue;
+        const double f = a[r][c];
+        for (int j = 0; j < 16; ++j) a[r][j] -= f * a[c][j];
+      }
+    }
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 8; ++j) inv[i][j] = a[i][8 + j];
+  }
+};
+const Idct8Inverse kInv8;
+
+// Levels (8x8 scan order) of residual x (raster 8x8) at qp with flat matrices.
+void quant8x8(const int* x, int qp, bool intra, int* lv) {
+  double t[64], d[64];
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) {
+      double s = 0;
+      for (int k = 0; k < 8; ++k) s += kInv8.inv[i][k] * x[k * 8 + j];
+      t[i * 8 + j] = s;
+    }
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) {
+      double s = 0;
+      for (int k = 0; k < 8; ++k) s += t[i * 8 + k] * kInv8.inv[j][k];
+      d[i * 8 + j] = s * 64.0;  // coefficient d with r = (M d M^T) / 64
+    }
+  const double f = intra ? 1.0 / 3 : 1.0 / 6;
+  for (int k = 0; k < 64; ++k) {
+    const int pos = kZigzag8x8[k], i = pos >> 3, j = pos & 7;
+    const double step = 16.0 * norm_adjust8(qp % 6, i, j) * std::ldexp(1.0, qp / 6) / 64.0;
+    const double v = d[pos] / step;
+    const int a = int(std::fabs(v) + f);
+    lv[k] = v < 0 ? -std::min(a, 2047) : std::min(a, 2047);
+  }
+}
+
+// Decoder-exact 8x8 dequantisation + inverse transform (flat matrices): residual samples.
+void recon8x8(const int* lv, int qp, int* r) {
+  i16 d[64] = {};
+  for (int k = 0; k < 64; ++k) {
+    if (!lv[k]) continue;
+    const int pos = kZigzag8x8[k];
+    const int ls = 16 * norm_adjust8(qp % 6, pos >> 3, pos & 7);
+    const int v = qp >= 36 ? (lv[k] * ls) * (1 << (qp / 6 - 6)) : (lv[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
+    d[pos] = sat16(v);
+  }
+  idct8x8(d, r);
+}
+
+}  // namespace
+
+struct AvcHighEncoder::Impl {
+  AvcHighConfig cfg;
+  Rng rng;
+  Scene scene;
+  h264::Sps sps;
+  h264::Pps pps;
+  std::vector<u8> sps_nal, pps_nal;
+  int W = 0, H = 0, wpx = 0, hpx = 0, max_fn = 1 << 16;
+  std::vector<HostSurface> slots;
+  struct Ref {
+    int slot, frame_num, poc;
+    u32 uid;
+    std::shared_ptr<const ColMotion> col;
+  };
+  std::vector<Ref> dpb;
+  struct Job {
+    i64 disp;
+    int type;  // h264::kI / kP / kB
+    bool ref;
+    bool idr;
+  };
+  std::deque<Job> plan;
+  std::map<i64, HostSurface> sources;
+  i64 next_disp = 0, gop_start = 0, rendered = -1, coded = 0;
+  int prev_ref_fn = 0, idr_id = -1;
+  u32 next_uid = 1;
+  Picture pic;
+  MbNeighbours nb;
+  HostSurface recon, src_out;
+  i64 last_disp = 0, last_pts = 0;
+  char last_type = 'I';
+  const HostSurface* cur_src = nullptr;
+
+  explicit Impl(const AvcHighConfig& c) : cfg(c), rng{c.seed * 0x9E3779B97F4A7C15ull + 777} {
+    VEP_CHECK(c.width >= 16 && c.height >= 16 && c.width % 2 == 0 && c.height % 2 == 0,
+              "encoder size must be even and >= 16");
+    VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.refs >= 1 && c.refs <= 8, "bframes 0..4, refs 1..8");
+    VEP_CHECK(c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
+    W = (c.width + 15) / 16;
+    H = (c.height + 15) / 16;
+    wpx = W * 16;
+    hpx = H * 16;
+    sps.profile_idc = (c.t8x8 || c.scaling) ? 100 : 77;
+    sps.constraint_flags = 0;
+    sps.level_idc = W * H > 8192 ? 51 : 40;
+    sps.log2_max_frame_num = 16;
+    sps.poc_type = 0;
+    sps.log2_max_poc_lsb = 16;
+    const int pyr = c.pyramid && c.bframes >= 2 ? 1 : 0;
+    sps.max_num_ref_frames = std::max(c.refs, c.bframes > 0 ? 2 : 1) + pyr;
+    sps.width_mbs = W;
+    sps.height_map_units = H;
+    sps.crop_right = wpx - c.width;
+    sps.crop_bottom = hpx - c.height;
+    sps.timing_info = true;
+    sps.num_units_in_tick = 1;
+    sps.time_scale = u32(2 * c.fps);
+    sps.max_num_reorder_frames = c.bframes > 0 ? (pyr ? 2 : 1) : 0;
+    sps.max_dec_frame_buffering = sps.max_num_ref_frames;
+    sps.scaling_matrix_present = c.scaling;
+    if (c.scaling) {  // non-flat matrices, coded explicitly: the defaults perturbed per entry
+      for (int l = 0; l < 6; ++l)
+        for (int k = 0; k < 16; ++k) sps.scaling.l4[l][k] = u8(h264::kDefault4x4[l >= 3][k] + rng.uni(9) - 4);
+      for (int l = 0; l < 2; ++l)
+        for (int k = 0; k < 64; ++k) sps.scaling.l8[l][k] = u8(h264::kDefault8x8[l][k] + rng.uni(9) - 4);
+    } else {
+      sps.scaling.flat();
+    }
+    pps.cabac = c.cabac;
+    pps.weighted_pred = c.weighted_p;
+    pps.weighted_bipred_idc = c.weighted_b;
+    pps.chroma_qp_index_offset = c.chroma_qp_offset;
+    pps.second_chroma_qp_index_offset = c.second_chroma_qp_offset;
+    pps.deblocking_filter_control = true;
+    pps.transform_8x8_mode = c.t8x8;
+    pps.scaling.flat();
+    auto nal = [](const std::vector<u8>& rbsp, std::vector<u8>& out) { rbsp_to_ebsp(rbsp.data(), rbsp.size(), out); };
+    nal(h264::write_sps(sps), sps_nal);
+    nal(h264::write_pps(pps), pps_nal);
+    slots.resize(size_t(sps.max_num_ref_frames) + 2);
+    for (auto& s : slots) s.alloc(wpx, hpx);
+    scene.make(SceneConfig{c.width, c.height, wpx, hpx, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
+  }
+
+  bool is_idr_pos(i64 d) const { return d == 0 || (d + cfg.idr_phase) % cfg.gop == 0; }
+
+  const HostSurface& source_of(i64 d) {
+    while (rendered < d) {
+      ++rendered;
+      if (rendered > 0) scene.advance();
+      scene.render();
+      scene.add_sensor_noise(rendered);
+      sources[rendered] = scene.src;
+    }
+    return sources.at(d);
+  }
+
+  void plan_next() {
+    if (is_idr_pos(next_disp)) {
+      plan.push_back({next_disp, h264::kI, true, true});
+      gop_start = next_disp;
+      ++next_disp;
+      return;
+    }
+    i64 next_idr = next_disp + 1;
+    while (!is_idr_pos(next_idr)) ++next_idr;
+    const i64 anchor = std::min<i64>(next_disp + cfg.bframes, next_idr - 1);
+    const int nb_ = int(anchor - next_disp);
+    plan.push_back({anchor, h264::kP, true, false});
+    const bool pyr = cfg.pyramid && nb_ >= 2;
+    const i64 mid = next_disp + nb_ / 2;
+    if (pyr) plan.push_back({mid, h264::kB, true, false});
+    for (i64 d = next_disp; d < anchor; ++d)
+      if (!(pyr && d == mid)) plan.push_back({d, h264::kB, false, false});
+    next_disp = anchor + 1;
+  }
+
+  // ---------------------------------------------------------------- reference lists
+  void build_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* lists) {
+    std::vector<const Ref*> st;
+    for (const Ref& r : dpb) st.push_back(&r);
+    std::vector<const Ref*> init[2];
+    if (sh.type() == h264::kP) {
+      auto wrap = [&](const Ref* r) { return r->frame_num > sh.frame_num ? r->frame_num - max_fn : r->frame_num; };
+      std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap(a) > wrap(b); });
+      init[0] = st;
+    } else if (sh.type() == h264::kB) {
+      std::vector<const Ref*> before, after;
+      for (const Ref* r : st) (r->poc < cur_poc ? before : after).push_back(r);
+      std::sort(before.begin(), before.end(), [](const Ref* a, const Ref* b) { return a->poc > b->poc; });
+      std::sort(after.begin(), after.end(), [](const Ref* a, const Ref* b) { return a->poc < b->poc; });
+      init[0] = before;
+      init[0].insert(init[0].end(), after.begin(), after.end());
+      init[1] = after;
+      init[1].insert(init[1].end(), before.begin(), before.end());
+      if (init[1].size() > 1 && init[1] == init[0]) std::swap(init[1][0], init[1][1]);
+    }
+    for (int l = 0; l < 2; ++l) {
+      lists[l].clear();
+      for (int i = 0; i < sh.num_ref_idx[l] && i < int(init[l].size()); ++i) {
+        const Ref& r = *init[l][size_t(i)];
+        lists[l].push_back(ListEntry{r.slot, r.poc, false, r.uid, r.col.get()});
+      }
+    }
+  }
+
+  int pick_slot() const {
+    for (int s = 0; s < int(slots.size()); ++s) {
+      bool used = false;
+      for (const Ref& r : dpb) used |= r.slot == s;
+      if (!used) return s;
+    }
+    throw Error("vep: encoder DPB overflow");
+  }
+
+  // ---------------------------------------------------------------- slice header
+  void write_header(BitWriter& bw, const SliceHdr& sh) {
+    bw.u(8, u32(sh.nal_ref_idc) << 5 | u32(sh.nal_type));
+    bw.ue(u32(sh.first_mb));
+    bw.ue(u32(sh.slice_type));
+    bw.ue(0);
+    bw.u(sps.log2_max_frame_num, u32(sh.frame_num));
+    if (sh.idr()) bw.ue(u32(sh.idr_pic_id));
+    bw.u(sps.log2_max_poc_lsb, u32(sh.poc_lsb));
+    const int st = sh.type();
+    if (st == h264::kB) bw.u1(sh.direct_spatial);
+    if (st != h264::kI) {
+      bw.u1(1);  // num_ref_idx_active_override_flag
+      bw.ue(u32(sh.num_ref_idx[0] - 1));
+      if (st == h264::kB) bw.ue(u32(sh.num_ref_idx[1] - 1));
+      bw.u1(0);  // ref_pic_list_modification_flag_l0
+      if (st == h264::kB) bw.u1(0);
+    }
+    if (sh.explicit_wp) {
+      bw.ue(u32(sh.luma_lwd));
+      bw.ue(u32(sh.chroma_lwd));
+      for (int l = 0; l < (st == h264::kB ? 2 : 1); ++l)
+        for (const auto& w : sh.wt[l]) {
+          const bool lf = w.w[0] != (1 << sh.luma_lwd) || w.o[0] != 0;
+          bw.u1(lf);
+          if (lf) {
+            bw.se(w.w[0]);
+            bw.se(w.o[0]);
+          }
+          const bool cf = w.w[1] != (1 << sh.chroma_lwd) || w.o[1] != 0 || w.w[2] != (1 << sh.chroma_lwd) || w.o[2] != 0;
+          bw.u1(cf);
+          if (cf)
+            for (int c = 1; c < 3; ++c) {
+              bw.se(w.w[c]);
+              bw.se(w.o[c]);
+            }
+        }
+    }
+    if (sh.nal_ref_idc != 0) {
+      if (sh.idr()) {
+        bw.u1(0);
+        bw.u1(0);
+      } else {
+        bw.u1(0);  // sliding window
+      }
+    }
+    if (pps.cabac && st != h264::kI) bw.ue(0);  // cabac_init_idc
+    bw.se(sh.qp - pps.pic_init_qp);
+    bw.ue(u32(sh.disable_deblocking));
+    if (sh.disable_deblocking != 1) {
+      bw.se(sh.alpha_off / 2);
+      bw.se(sh.beta_off / 2);
+    }
+  }
+
+  // ---------------------------------------------------------------- helpers
+  int S(int x, int y) const { return cur_src->y[size_t(y) * wpx + x]; }
+  int SC(int x, int y, int c) const { return cur_src->uv[size_t(y) * wpx + 2 * x + c]; }
+  HostSurface& T() { return slots[size_t(pic.target)]; }
+
+  // Neighbour MB (dx, dy) of `mb` coded in the current slice (intra availability).
+  bool avail(int mb, int dx, int dy) const {
+    const int mx = mb % W + dx, my = mb / W + dy;
+    if (mx < 0 || mx >= W || my < 0) return false;
+    const int n = my * W + mx;
+    return n < mb && pic.mbs[size_t(n)].slice == cur_slice;
+  }
+  int cur_slice = 0;
+
+  // Luma / chroma residual levels of a prediction into `d` (t8: 8x8 transform), cbp returned.
+  int code_residual(int mb, const int* py, const int (*pc)[64], bool intra, bool t8, bool i16, int qp, MbDesc& d) {
+    const int mx = mb % W, my = mb / W;
+    int cl = 0;
+    if (t8) {
+      for (int q = 0; q < 4; ++q) {
+        int x[64];
+        for (int i = 0; i < 8; ++i)
+          for (int j = 0; j < 8; ++j) {
+            const int yy = (q >> 1) * 8 + i, xx = (q & 1) * 8 + j;
+            x[i * 8 + j] = S(mx * 16 + xx, my * 16 + yy) - py[yy * 16 + xx];
+          }
+        quant8x8(x, qp, intra, d.l8[q]);
+        for (int k = 0; k < 64; ++k)
+          if (d.l8[q][k]) cl |= 1 << q;
+      }
+    } else {
+      int dcw[16];
+      for (int r = 0; r < 16; ++r) {
+        const int bx = r & 3, by = r >> 2;
+        int x[16], w[16];
+        for (int i = 0; i < 4; ++i)
+          for (int j = 0; j < 4; ++j)
+            x[i * 4 + j] = S(mx * 16 + bx * 4 + j, my * 16 + by * 4 + i) - py[(by * 4 + i) * 16 + bx * 4 + j];
+        fwd4x4(x, w);
+        dcw[r] = w[0];
+        for (int k = i16 ? 1 : 0; k < 16; ++k) {
+          const int pos = kZigzag4x4[k];
+          const int l = quant(w[pos], qp, mf_class(pos), intra);
+          d.ac[r][i16 ? k - 1 : k] = l;
+          if (l) cl |= 1 << (raster_to_blk(r) >> 2);
+        }
+      }
+      if (i16) {
+        int f[16], g[16];
+        for (int i = 0; i < 4; ++i) {
+          const int a = dcw[i * 4], b = dcw[i * 4 + 1], c = dcw[i * 4 + 2], e = dcw[i * 4 + 3];
+          f[i * 4] = a + b + c + e;
+          f[i * 4 + 1] = a + b - c - e;
+          f[i * 4 + 2] = a - b - c + e;
+          f[i * 4 + 3] = a - b + c - e;
+        }
+        for (int j = 0; j < 4; ++j) {
+          const int a = f[j], b = f[4 + j], c = f[8 + j], e = f[12 + j];
+          g[j] = a + b + c + e;
+          g[4 + j] = a + b - c - e;
+          g[8 + j] = a - b - c + e;
+          g[12 + j] = a - b + c - e;
+        }
+        for (int k = 0; k < 16; ++k) d.dc[k] = quant(g[kZigzag4x4[k]] / 2, qp, 0, true, 1);
+        cl = cl ? 15 : 0;
+      }
+    }
+    int cc = 0;
+    const int qpc[2] = {chroma_qp(qp, pps.chroma_qp_index_offset), chroma_qp(qp, pps.second_chroma_qp_index_offset)};
+    for (int c = 0; c < 2; ++c) {
+      int cw[4];
+      for (int b = 0; b < 4; ++b) {
+        const int bx = (b & 1) * 4, by = (b >> 1) * 4;
+        int x[16], w[16];
+        for (int i = 0; i < 4; ++i)
+          for (int j = 0; j < 4; ++j)
+            x[i * 4 + j] = SC(mx * 8 + bx + j, my * 8 + by + i, c) - pc[c][(by + i) * 8 + bx + j];
+        fwd4x4(x, w);
+        cw[b] = w[0];
+        for (int k = 1; k < 16; ++k) {
+          const int pos = kZigzag4x4[k];
+          d.cac[c][b][k - 1] = quant(w[pos], qpc[c], mf_class(pos), intra);
+          if (d.cac[c][b][k - 1]) cc = 2;
+        }
+      }
+      const int f[4] = {cw[0] + cw[1] + cw[2] + cw[3], cw[0] - cw[1] + cw[2] - cw[3],
+                        cw[0] + cw[1] - cw[2] - cw[3], cw[0] - cw[1] - cw[2] + cw[3]};
+      for (int b = 0; b < 4; ++b) {
+        d.cdc[c][b] = quant(f[b], qpc[c], 0, intra, 1);
+        if (d.cdc[c][b]) cc = std::max(cc, 1);
+      }
+    }
+    if (cc < 2)
+      for (auto& c : d.cac)
+        for (auto& b : c)
+          for (int& v : b) v = 0;
+    return cl | cc << 4;
+  }
+
+  int sad_pred(int mb, const int* py) const {
+    const int mx = mb % W, my = mb / W;
+    int s = 0;
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) s += std::abs(S(mx * 16 + x, my * 16 + y) - py[y * 16 + x]);
+    return s;
+  }
+
+  // Inter prediction of a whole MB from per-8x8 list entries and per-4x4 motion.
+  void predict(const SliceEnv& env, int mb, const int r0[4], const int r1[4], const i16 (*mv)[16][2], int* py,
+               int (*pc)[64], bool weighted) {
+    MbRec m{};
+    bool l1 = false;
+    WpEntry wp[4];
+    for (int k = 0; k < 4; ++k) {
+      m.ref[k] = r0[k] >= 0 ? u8((*env.list[0])[size_t(r0[k])].slot) : u8(0xFF);
+      m.ref1[k] = r1[k] >= 0 ? u8((*env.list[1])[size_t(r1[k])].slot) : u8(0xFF);
+      l1 |= r1[k] >= 0;
+      if (weighted) wp[k] = wp_entry(env, r0[k], r1[k]);
+    }
+    predict_inter(slots, m, &mv[0][0][0], l1 ? &mv[1][0][0] : nullptr, weighted ? wp : nullptr, mb % W, mb / W, py, pc);
+  }
+
+  // 16x16 motion search in one list for reference r: candidates (zero, predictor, the scene's
+  // object motion) refined by full-, half- and quarter-sample steps.
+  void search(const SliceEnv& env, int mb, int list, int r, const int pmv[2], int best[2], int& best_sad) {
+    const ListEntry& e = (*env.list[list])[size_t(r)];
+    const HostSurface& R = slots[size_t(e.slot)];
+    const double dist = (e.poc - env.cur_poc) / 2.0;  // display frames from here to the reference
+    const int mx = mb % W, my = mb / W;
+    auto cost = [&](int vx, int vy) {
+      int s = 0;
+      for (int i = 0; i < 16; i += 2)
+        for (int j = 0; j < 16; j += 2) {
+          const int x = mx * 16 + j, y = my * 16 + i;
+          s += std::abs(S(x, y) - luma_qpel(R.y.data(), wpx, wpx, hpx, x + (vx >> 2), y + (vy >> 2), vx & 3, vy & 3));
+        }
+      return s * 4 + 4 * (std::abs(vx - pmv[0]) + std::abs(vy - pmv[1]));
+    };
+    std::vector<std::pair<int, int>> cand = {{0, 0}, {pmv[0], pmv[1]}};
+    for (const Scene::Obj& o : scene.objs) {
+      if (o.x > mx * 16 + 24 || o.x + o.w < mx * 16 - 8 || o.y > my * 16 + 24 || o.y + o.h < my * 16 - 8) continue;
+      cand.push_back({int(std::lround(o.vx * 4 * dist)), int(std::lround(o.vy * 4 * dist))});
+    }
+    best_sad = 1 << 30;
+    for (auto [vx, vy] : cand) {
+      const int c = cost(vx, vy);
+      if (c < best_sad) {
+        best_sad = c;
+        best[0] = vx;
+        best[1] = vy;
+      }
+    }
+    for (int step : {4, 2, 1}) {
+      bool moved = true;
+      for (int it = 0; moved && it < 4; ++it) {
+        moved = false;
+        const int cx = best[0], cy = best[1];
+        for (int k = 0; k < 8; ++k) {
+          static const int dx[8] = {-1, 1, 0, 0, -1, -1, 1, 1}, dy[8] = {0, 0, -1, 1, -1, 1, -1, 1};
+          const int vx = cx + dx[k] * step, vy = cy + dy[k] * step;
+          if (std::abs(vx) > 2048 || std::abs(vy) > 512) continue;
+          const int c = cost(vx, vy);
+          if (c < best_sad) {
+            best_sad = c;
+            best[0] = vx;
+            best[1] = vy;
+            moved = true;
+          }
+        }
+      }
+    }
+  }
+
+  // ---------------------------------------------------------------- intra decisions
+  // Intra_16x16 (no 8x8 transform) or Intra_8x8 with per-block closed-loop mode choice.
+  void decide_intra(int mb, int qp, MbDesc& d, int& sad) {
+    const int mx = mb % W, my = mb / W;
+    const bool A = avail(mb, -1, 0), B = avail(mb, 0, -1), D = avail(mb, -1, -1);
+    const int itype_base = 0;
+    (void)itype_base;
+    int cp[2][64];
+    {  // chroma: DC
+      for (int c = 0; c < 2; ++c) {
+        IntraChromaNb n;
+        chroma_neighbours(pic, mb, c, T(), n);
+        for (int y = 0; y < 8; ++y)
+          for (int x = 0; x < 8; ++x) cp[c][y * 8 + x] = chroma_pred(n, PredConst{0, 0, 0, 0}, 0, x, y);
+      }
+      d.chroma_mode = 0;
+    }
+    if (cfg.t8x8) {
+      // Intra_8x8: each block predicted from the (closed-loop) reconstruction of the previous ones
+      int py[256];
+      HostSurface& t = T();
+      sad = 0;
+      for (int q = 0; q < 4; ++q) {
+        int f[25];
+        bool top, left;
+        intra8x8_neighbours(pic, mb, q, t, f, top, left);
+        const int bx = q & 1, by = q >> 1;
+        const bool tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+        int best = 2, best_s = 1 << 30;
+        for (int mode = 0; mode < 9; ++mode) {
+          const bool ok = mode == 2 || ((mode == 0 || mode == 3 || mode == 7) && top) || ((mode == 1 || mode == 8) && left) ||
+                          ((mode >= 4 && mode <= 6) && top && left && tl);
+          if (!ok) continue;
+          int s = 0;
+          for (int i = 0; i < 8; ++i)
+            for (int j = 0; j < 8; ++j)
+              s += std::abs(S(mx * 16 + bx * 8 + j, my * 16 + by * 8 + i) - intra8x8_pred(f, top, left, mode, j, i));
+          if (s < best_s) {
+            best_s = s;
+            best = mode;
+          }
+        }
+        d.ipred[q] = u8(best);
+        int x[64], pb[64];
+        for (int i = 0; i < 8; ++i)
+          for (int j = 0; j < 8; ++j) {
+            pb[i * 8 + j] = intra8x8_pred(f, top, left, best, j, i);
+            py[(by * 8 + i) * 16 + bx * 8 + j] = pb[i * 8 + j];
+            x[i * 8 + j] = S(mx * 16 + bx * 8 + j, my * 16 + by * 8 + i) - pb[i * 8 + j];
+          }
+        quant8x8(x, qp, true, d.l8[q]);
+        int r[64];
+        recon8x8(d.l8[q], qp, r);
+        for (int i = 0; i < 8; ++i)
+          for (int j = 0; j < 8; ++j)
+            t.y[size_t(my * 16 + by * 8 + i) * wpx + mx * 16 + bx * 8 + j] = u8(clip1(pb[i * 8 + j] + r[i * 8 + j]));
+        sad += best_s;
+      }
+      MbDesc tmp;
+      const int cbp = code_residual(mb, py, cp, true, true, false, qp, tmp);
+      for (int c = 0; c < 2; ++c) {  // keep the closed-loop luma levels, take the chroma ones
+        std::memcpy(d.cdc[c], tmp.cdc[c], sizeof d.cdc[c]);
+        std::memcpy(d.cac[c], tmp.cac[c], sizeof d.cac[c]);
+      }
+      int cl = 0;
+      for (int q = 0; q < 4; ++q)
+        for (int k = 0; k < 64; ++k)
+          if (d.l8[q][k]) cl |= 1 << q;
+      d.t8x8 = true;
+      d.cbp = cl | (cbp & 0x30);
+      d.mb_type = 0;  // I_NxN (+ transform_size_8x8_flag)
+      return;
+    }
+    Intra16Nb n;
+    intra16_neighbours(pic, mb, T(), n);
+    int best = 2, best_s = 1 << 30;
+    int py[256];
+    for (int mode = 0; mode < 4; ++mode) {
+      if ((mode == 0 && !B) || (mode == 1 && !A) || (mode == 3 && !(A && B && D))) continue;
+      const PredConst k = intra16x16_const(n, mode);
+      int s = 0;
+      for (int y = 0; y < 16; ++y)
+        for (int x = 0; x < 16; ++x) s += std::abs(S(mx * 16 + x, my * 16 + y) - intra16x16_pred(n, k, mode, x, y));
+      if (s < best_s) {
+        best_s = s;
+        best = mode;
+      }
+    }
+    const PredConst k = intra16x16_const(n, best);
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) py[y * 16 + x] = intra16x16_pred(n, k, best, x, y);
+    const int cbp = code_residual(mb, py, cp, true, false, true, qp, d);
+    d.mb_type = 1 + best + 4 * (cbp >> 4) + 12 * ((cbp & 15) ? 1 : 0);
+    if (!(cbp & 15))
+      for (auto& b : d.ac)
+        for (int& v : b) v = 0;
+    sad = best_s;
+  }
+
+  // ---------------------------------------------------------------- coverage decisions
+  void random_levels(MbDesc& d, bool t8, bool i16) {
+    auto lvl = [&]() {
+      const int r = rng.uni(100);
+      if (r < 70) return 0;
+      int a = r < 95 ? 1 + rng.uni(3) : 1 + rng.uni(r < 99 ? 40 : 600);
+      return rng.uni(2) ? a : -a;
+    };
+    if (t8)
+      for (auto& b : d.l8)
+        for (int k = 0; k < 64; ++k) b[k] = k < 20 ? lvl() : (rng.chance(5) ? lvl() : 0);
+    else
+      for (auto& b : d.ac)
+        for (int k = 0; k < (i16 ? 15 : 16); ++k) b[k] = lvl();
+    if (i16)
+      for (int& v : d.dc) v = lvl();
+    for (auto& c : d.cdc)
+      for (int& v : c) v = lvl();
+    for (auto& c : d.cac)
+      for (auto& b : c)
+        for (int& v : b) v = rng.chance(30) ? lvl() : 0;
+  }
+
+  void random_intra(int mb, bool islice_pcm_ok, MbDesc& d, int& base_type) {
+    const bool A = avail(mb, -1, 0), B = avail(mb, 0, -1), D = avail(mb, -1, -1);
+    const int r = rng.uni(100);
+    auto chroma = [&]() {
+      int m;
+      do m = rng.uni(4);
+      while ((m == 1 && !A) || (m == 2 && !B) || (m == 3 && !(A && B && D)));
+      return m;
+    };
+    if (islice_pcm_ok && r < 5) {
+      static thread_local u8 pcm[kPcmMbBytes];
+      for (auto& p : pcm) p = u8(16 + rng.uni(220));
+      d.pcm = pcm;
+      base_type = 25;
+      return;
+    }
+    d.chroma_mode = chroma();
+    if (r < 40) {  // Intra_16x16
+      int m;
+      do m = rng.uni(4);
+      while ((m == 0 && !B) || (m == 1 && !A) || (m == 3 && !(A && B && D)));
+      random_levels(d, false, true);
+      const int cl = rng.chance(50) ? 15 : 0, cc = rng.uni(3);
+      if (!cl)
+        for (auto& b : d.ac)
+          for (int& v : b) v = 0;
+      if (cc < 2)
+        for (auto& c : d.cac)
+          for (auto& b : c)
+            for (int& v : b) v = 0;
+      if (cc < 1)
+        for (auto& c : d.cdc)
+          for (int& v : c) v = 0;
+      base_type = 1 + m + 4 * cc + 12 * (cl ? 1 : 0);
+      return;
+    }
+    base_type = 0;
+    d.t8x8 = cfg.t8x8 && rng.chance(50);
+    const int mx = mb % W, my = mb / W;
+    (void)mx;
+    (void)my;
+    if (d.t8x8) {
+      for (int q = 0; q < 4; ++q) {
+        const int bx = q & 1, by = q >> 1;
+        const bool top = by > 0 || B, left = bx > 0 || A;
+        const bool tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+        int m;
+        do m = rng.uni(9);
+        while (!(m == 2 || ((m == 0 || m == 3 || m == 7) && top) || ((m == 1 || m == 8) && left) ||
+                 ((m >= 4 && m <= 6) && top && left && tl)));
+        d.ipred[q] = u8(m);
+      }
+    } else {
+      for (int rb = 0; rb < 16; ++rb) {
+        const int bx = rb & 3, by = rb >> 2;
+        const bool top = by > 0 || B, left = bx > 0 || A;
+        const bool tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+        int m;
+        do m = rng.uni(9);
+        while (!(m == 2 || ((m == 0 || m == 3 || m == 7) && top) || ((m == 1 || m == 8) && left) ||
+                 ((m >= 4 && m <= 6) && top && left && tl)));
+        d.ipred[rb] = u8(m);
+      }
+    }
+    random_levels(d, d.t8x8, false);
+    d.cbp = rng.uni(16) | rng.uni(3) << 4;
+  }
+
+  // ---------------------------------------------------------------- picture
+  std::shared_ptr<AccessUnit> encode(const Job& job) {
+    cur_src = &source_of(job.disp);
+    const bool idr = job.idr;
+    if (idr) {
+      dpb.clear();
+      ++idr_id;
+    }
+    SliceHdr sh;
+    sh.nal_type = idr ? h264::kNalIdr : h264::kNalSlice;
+    sh.nal_ref_idc = job.ref ? (job.type == h264::kB ? 2 : 3) : 0;
+    sh.slice_type = job.type;
+    sh.frame_num = idr ? 0 : (prev_ref_fn + 1) % max_fn;
+    sh.idr_pic_id = idr_id & 0xFFFF;
+    const int poc = int(2 * (job.disp - gop_start));
+    sh.poc_lsb = poc & ((1 << sps.log2_max_poc_lsb) - 1);
+    sh.direct_spatial = cfg.direct_spatial;
+    int n0 = 0, n1 = 0;
+    if (job.type == h264::kP) n0 = std::min<int>(cfg.refs, int(dpb.size()));
+    if (job.type == h264::kB) {
+      int before = 0, after = 0;
+      for (const Ref& r : dpb) (r.poc < poc ? before : after) += 1;
+      // every reference in list 0: temporal direct needs the colocated picture's references
+      n0 = int(dpb.size());
+      n1 = std::min<int>(cfg.coverage ? 2 : 1, int(dpb.size()));
+      VEP_CHECK(before > 0 && after > 0, "B picture without references on both sides");
+    }
+    sh.num_ref_idx[0] = std::max(1, n0);
+    sh.num_ref_idx[1] = std::max(1, n1);
+    const bool wp_p = job.type == h264::kP && cfg.weighted_p;
+    const bool wp_b = job.type == h264::kB && cfg.weighted_b == 1;
+    sh.explicit_wp = wp_p || wp_b;
+    if (sh.explicit_wp) {
+      sh.luma_lwd = 5;
+      sh.chroma_lwd = 4;
+      for (int l = 0; l < (job.type == h264::kB ? 2 : 1); ++l) {
+        sh.wt[l].resize(size_t(sh.num_ref_idx[l]));
+        for (auto& w : sh.wt[l]) {
+          w.w[0] = i16(32 + (cfg.coverage ? rng.uni(9) - 4 : 1));
+          w.o[0] = i16(cfg.coverage ? rng.uni(9) - 4 : -2);
+          w.w[1] = w.w[2] = i16(16);
+          w.o[1] = w.o[2] = i16(cfg.coverage ? rng.uni(5) - 2 : 0);
+        }
+      }
+    }
+    sh.cabac_init_idc = 0;
+    sh.qp = std::clamp(cfg.qp + (job.type == h264::kB ? (job.ref ? 1 : 2) : 0), 0, 51);
+    sh.disable_deblocking = cfg.deblock_idc;
+    const bool weighted = sh.explicit_wp || (job.type == h264::kB && cfg.weighted_b == 2);
+
+    pic = Picture{};
+    pic.wmbs = W;
+    pic.hmbs = H;
+    pic.mbs.assign(size_t(W) * H, MbRec{});
+    pic.coefs.reserve(size_t(W) * H * 64);
+    pic.mvs.reserve(size_t(W) * H * 64);
+    pic.dpb_slots = int(slots.size());
+    pic.target = pick_slot();
+    pic.idr = idr;
+    pic.poc = poc;
+    nb.reset(W, H);
+    std::vector<ListEntry> lists[2];
+    auto au = std::make_shared<AccessUnit>();
+    au->codec = Codec::kH264;
+    au->keyframe = idr;
+    // decoding timestamps run `reorder depth` frames behind the display timestamps
+    const i64 dur = 90000 / std::max(1, cfg.fps);
+    au->pts = (job.disp + std::max(0, sps.max_num_reorder_frames)) * dur;
+    au->dts = coded * dur;
+    au->duration = dur;
+    au->seq = u64(coded);
+    last_pts = au->pts;
+    last_type = job.type == h264::kI ? 'I' : job.type == h264::kP ? 'P' : 'B';
+    if (idr) {
+      au->add_nal(sps_nal.data(), sps_nal.size());
+      au->add_nal(pps_nal.data(), pps_nal.size());
+    }
+    std::vector<std::array<std::vector<u32>, 2>> slice_uids;
+    const int nslices = std::max(1, std::min(cfg.slices, H));
+    for (int si = 0; si < nslices; ++si) {
+      const int row0 = si * H / nslices, row1 = (si + 1) * H / nslices;
+      sh.first_mb = row0 * W;
+      build_lists(sh, poc, lists);
+      std::array<std::vector<u32>, 2> uids;
+      for (int l = 0; l < 2; ++l)
+        for (const auto& e : lists[l]) uids[size_t(l)].push_back(e.uid);
+      slice_uids.push_back(uids);
+      SliceEnv env;
+      env.sh = &sh;
+      env.sps = &sps;
+      env.pps = &pps;
+      env.slice = si;
+      env.list[0] = &lists[0];
+      env.list[1] = &lists[1];
+      env.cur_poc = poc;
+      env.scaling = h264::resolve_scaling(sps, pps);
+      BitWriter bw;
+      write_header(bw, sh);
+      SliceWriter sw(nb, pic, env, bw);
+      cur_slice = si;
+      for (int mb = row0 * W; mb < row1 * W; ++mb) {
+        pic.mbs[size_t(mb)].slice = decltype(MbRec::slice)(si);  // intra availability of this MB
+        MbDesc d;
+        decide(env, sw, mb, job, sh, weighted, d);
+        sw.write_mb(mb, d);
+        cpu_reconstruct_mb(pic, mb, slots);
+      }
+      sw.finish();
+      std::vector<u8> nal;
+      rbsp_to_ebsp(bw.buf().data(), bw.buf().size(), nal);
+      au->add_nal(nal.data(), nal.size());
+    }
+    if (pic.deblock) cpu_deblock(pic, T());
+    if (job.ref) {
+      Ref r{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids)};
+      if (int(dpb.size()) >= sps.max_num_ref_frames) {  // sliding window (§8.2.5.3)
+        auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
+          auto wrap = [&](const Ref& x) { return x.frame_num > sh.frame_num ? x.frame_num - max_fn : x.frame_num; };
+          return wrap(a) < wrap(b);
+        });
+        dpb.erase(it);
+      }
+      dpb.push_back(r);
+      prev_ref_fn = sh.frame_num;
+    }
+    ++next_uid;
+    recon = T();
+    src_out = *cur_src;
+    last_disp = job.disp;
+    ++coded;
+    // sources of pictures coded and no longer needed
+    sources.erase(job.disp);
+    return au;
+  }
+
+  void decide(const SliceEnv& env, SliceWriter& sw, int mb, const Job& job, const SliceHdr& sh, bool weighted,
+              MbDesc& d) {
+    const int qp = sh.qp;
+    const int t = job.type;
+    if (cfg.coverage) {
+      decide_random(env, sw, mb, t, d);
+      return;
+    }
+    if (t == h264::kI) {
+      int sad;
+      decide_intra(mb, qp, d, sad);
+      return;
+    }
+    const int mx = mb % W, my = mb / W;
+    (void)mx;
+    (void)my;
+    MbState skip;
+    sw.skip_motion(mb, skip);
+    int r0[4], r1[4];
+    for (int k = 0; k < 4; ++k) {
+      r0[k] = skip.ref[0][k];
+      r1[k] = skip.ref[1][k];
+    }
+    int py[256], pc[2][64];
+    predict(env, mb, r0, r1, skip.mv, py, pc, weighted);
+    const int skip_sad = sad_pred(mb, py);
+    MbDesc sd;
+    const int skip_cbp = code_residual(mb, py, pc, false, cfg.t8x8, false, qp, sd);
+    if (skip_cbp == 0 && skip_sad < 256 * 6) {
+      d.skip = true;
+      return;
+    }
+    // 16x16 motion search: list 0 (P: the first two references) and list 1 (B: reference 0)
+    int best[2][2] = {{0, 0}, {0, 0}}, bsad[2] = {1 << 30, 1 << 30}, bref[2] = {0, 0};
+    for (int l = 0; l < (t == h264::kB ? 2 : 1); ++l) {
+      const int nr = t == h264::kP ? std::min(2, int(env.list[l]->size())) : 1;
+      for (int r = 0; r < nr; ++r) {
+        int pmv[2], mv[2], s;
+        nb.pred_mv(mb, 0, 0, 4, 4, l, r, 0, 0, pmv);
+        search(env, mb, l, r, pmv, mv, s);
+        if (s < bsad[l]) {
+          bsad[l] = s;
+          best[l][0] = mv[0];
+          best[l][1] = mv[1];
+          bref[l] = r;
+        }
+      }
+    }
+    // candidate predictions: 0 L0, 1 L1, 2 Bi (B) ; direct (with residual)
+    int cands = t == h264::kB ? 3 : 1;
+    int best_c = -1, best_cost = skip_sad + 256 * 2;  // direct / skip-motion with residual
+    int cpy[3][256], cpc[3][2][64];
+    for (int c = 0; c < cands; ++c) {
+      int a0[4], a1[4];
+      i16 mv[2][16][2];
+      for (int k = 0; k < 4; ++k) {
+        a0[k] = (c == 0 || c == 2) ? bref[0] : -1;
+        a1[k] = (c == 1 || c == 2) ? bref[1] : -1;
+      }
+      for (int l = 0; l < 2; ++l)
+        for (int b = 0; b < 16; ++b) {
+          mv[l][b][0] = i16(best[l][0]);
+          mv[l][b][1] = i16(best[l][1]);
+        }
+      predict(env, mb, a0, a1, mv, cpy[c], cpc[c], weighted);
+      const int s = sad_pred(mb, cpy[c]);
+      if (s < best_cost) {
+        best_cost = s;
+        best_c = c;
+      }
+    }
+    // intra fallback
+    if (best_cost > 256 * 22) {
+      MbDesc id;
+      int isad;
+      HostSurface& T0 = T();
+      std::vector<u8> save;
+      if (cfg.t8x8) {  // decide_intra's closed loop writes samples: keep them to undo
+        save.resize(16 * 16);
+        for (int y = 0; y < 16; ++y) std::memcpy(&save[size_t(y) * 16], &T0.y[size_t(mb / W * 16 + y) * wpx + mb % W * 16], 16);
+      }
+      decide_intra(mb, qp, id, isad);
+      if (isad + 256 * 4 < best_cost) {
+        d = id;
+        d.mb_type += t == h264::kP ? 5 : 23;
+        return;
+      }
+      if (cfg.t8x8)
+        for (int y = 0; y < 16; ++y) std::memcpy(&T0.y[size_t(mb / W * 16 + y) * wpx + mb % W * 16], &save[size_t(y) * 16], 16);
+    }
+    if (best_c < 0) {  // the skip / direct motion with residual
+      if (t == h264::kP) {
+        d.mb_type = 0;
+        d.ref[0][0] = 0;
+        for (int b = 0; b < 16; ++b) {
+          d.mv[0][b][0] = skip.mv[0][b][0];
+          d.mv[0][b][1] = skip.mv[0][b][1];
+        }
+      } else {
+        d.mb_type = 0;  // B_Direct_16x16
+      }
+      d.t8x8 = cfg.t8x8 && (t == h264::kP || sps.direct_8x8);
+      const int cbp = code_residual(mb, py, pc, false, d.t8x8, false, qp, d);
+      d.cbp = cbp;
+      return;
+    }
+    d.mb_type = t == h264::kP ? 0 : 1 + best_c;  // P_L0_16x16 / B_L0, B_L1, B_Bi _16x16
+    for (int l = 0; l < 2; ++l) {
+      d.ref[l][0] = bref[l];
+      for (int b = 0; b < 16; ++b) {
+        d.mv[l][b][0] = i16(best[l][0]);
+        d.mv[l][b][1] = i16(best[l][1]);
+      }
+    }
+    d.t8x8 = cfg.t8x8;
+    d.cbp = code_residual(mb, cpy[best_c], cpc[best_c], false, d.t8x8, false, qp, d);
+  }
+
+  void decide_random(const SliceEnv& env, SliceWriter& sw, int mb, int t, MbDesc& d) {
+    (void)sw;
+    const int r = rng.uni(100);
+    auto rmv = [&]() { return i16(rng.uni(100) < 20 ? 0 : rng.uni(161) - 80); };
+    if (t == h264::kI || r < 12) {
+      int base;
+      random_intra(mb, true, d, base);
+      d.mb_type = base + (t == h264::kI ? 0 : (t == h264::kP ? 5 : 23));
+      if (base > 0 && base < 25) d.cbp = 0;
+      d.qp_delta = rng.chance(20) ? rng.uni(9) - 4 : 0;
+      return;
+    }
+    if (r < 25) {
+      d.skip = true;
+      return;
+    }
+    const bool b = t == h264::kB;
+    const int n0 = sh_num(env, 0), n1 = sh_num(env, 1);
+    int mbt;
+    if (b) mbt = rng.uni(23);
+    else mbt = rng.uni(4);
+    d.mb_type = mbt;
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < 4; ++k) d.ref[l][k] = rng.uni(l == 0 ? n0 : n1);
+    for (int l = 0; l < 2; ++l)
+      for (int k = 0; k < 16; ++k) {
+        d.mv[l][k][0] = rmv();
+        d.mv[l][k][1] = rmv();
+      }
+    // sub-macroblock shapes: 0 8x8, 1 8x4, 2 4x8, 3 4x4 (B_Direct_8x8 counts as 8x8: the SPS
+    // sets direct_8x8_inference)
+    static const u8 kBShape[13] = {0, 0, 0, 0, 1, 2, 1, 2, 1, 2, 3, 3, 3};
+    bool small = false;
+    const bool eight = (!b && mbt == 3) || (b && mbt == 22);
+    if (eight)
+      for (int i = 0; i < 4; ++i) {
+        d.sub[i] = b ? rng.uni(13) : rng.uni(4);
+        small |= (b ? kBShape[d.sub[i]] : d.sub[i]) != 0;
+      }
+    // uniform motion inside each partition (the layer reads the partition's top-left block)
+    auto fill = [&](int l, int x4, int y4, int w4, int h4) {
+      const i16 vx = d.mv[l][y4 * 4 + x4][0], vy = d.mv[l][y4 * 4 + x4][1];
+      for (int y = y4; y < y4 + h4; ++y)
+        for (int x = x4; x < x4 + w4; ++x) {
+          d.mv[l][y * 4 + x][0] = vx;
+          d.mv[l][y * 4 + x][1] = vy;
+        }
+    };
+    for (int l = 0; l < 2; ++l) {
+      if (!eight) {
+        const int shape = (!b ? mbt : (mbt <= 3 ? 0 : ((mbt & 1) ? 2 : 1)));
+        if (shape == 0) fill(l, 0, 0, 4, 4);
+        else if (shape == 1) {
+          fill(l, 0, 0, 4, 2);
+          fill(l, 0, 2, 4, 2);
+        } else {
+          fill(l, 0, 0, 2, 4);
+          fill(l, 2, 0, 2, 4);
+        }
+      } else {
+        for (int i = 0; i < 4; ++i) {
+          const int x8 = (i & 1) * 2, y8 = (i >> 1) * 2;
+          const int shape = b ? kBShape[d.sub[i]] : d.sub[i];
+          if (shape == 0) fill(l, x8, y8, 2, 2);
+          else if (shape == 1) {
+            fill(l, x8, y8, 2, 1);
+            fill(l, x8, y8 + 1, 2, 1);
+          } else if (shape == 2) {
+            fill(l, x8, y8, 1, 2);
+            fill(l, x8 + 1, y8, 1, 2);
+          }
+        }
+      }
+    }
+    const bool direct16 = b && mbt == 0;
+    const bool t8_ok = cfg.t8x8 && !small && (!direct16 || sps.direct_8x8);
+    d.t8x8 = t8_ok && rng.chance(50);
+    random_levels(d, d.t8x8, false);
+    d.cbp = rng.uni(16) | rng.uni(3) << 4;
+    d.qp_delta = rng.chance(20) ? rng.uni(9) - 4 : 0;
+  }
+
+  static int sh_num(const SliceEnv& env, int l) { return std::max(1, int(env.list[l]->size())); }
+
+  std::shared_ptr<AccessUnit> next() {
+    if (plan.empty()) plan_next();
+    const Job j = plan.front();
+    plan.pop_front();
+    return encode(j);
+  }
+};
+
+AvcHighEncoder::AvcHighEncoder(const AvcHighConfig& cfg) : cfg_(cfg), p_(std::make_unique<Impl>(cfg)) {}
+AvcHighEncoder::~AvcHighEncoder() = default;
+std::shared_ptr<AccessUnit> AvcHighEncoder::next() { return p_->next(); }
+const HostSurface& AvcHighEncoder::reconstruction() const { return p_->recon; }
+const HostSurface& AvcHighEncoder::source() const { return p_->src_out; }
+i64 AvcHighEncoder::last_display_index() const { return p_->last_disp; }
+i64 AvcHighEncoder::last_pts() const { return p_->last_pts; }
+char AvcHighEncoder::last_type() const { return p_->last_type; }
+const std::vector<u8>& AvcHighEncoder::sps_nal() const { return p_->sps_nal; }
+const std::vector<u8>& AvcHighEncoder::pps_nal() const { return p_->pps_nal; }
+
+}  // namespace vep::avc

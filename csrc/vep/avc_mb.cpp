@@ -63,8 +63,12 @@ inline int raster_b8(int blk) { return ((blk >> 3) << 1) | ((blk & 3) >> 1); }
 inline u16 b8_blocks(int b8) { return u16(0x33u << ((b8 & 1) * 2 + (b8 >> 1) * 8)); }
 inline int clip3i(int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); }
 
-template <bool kCabac>
+// kCabac: entropy mode; kWrite: encoder direction (values come from `want` and are written;
+// every context derivation, predictor and record is the decoder's).
+template <bool kCabac, bool kWrite>
 class MbLayer {
+  using Bins = std::conditional_t<kWrite, AvcBins<BinEncoder>, AvcBins<BinDecoder>>;
+
  public:
   MbLayer(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const Dequant& dq)
       : nb_(nb), pic_(pic), env_(env), sh_(*env.sh), pps_(*env.pps), sps_(*env.sps), dq_(dq) {
@@ -74,22 +78,51 @@ class MbLayer {
     implicit_ = type_ == h264::kB && pps_.weighted_bipred_idc == 2;
   }
 
-  // entropy sources (one of them is used)
-  Bits* br = nullptr;
-  AvcBins<BinDecoder>* bins = nullptr;
-  cabac::Decoder* cabac = nullptr;
+  // entropy sources / sinks (the ones of the mode are used)
+  Bits* br = nullptr;            // CAVLC read
+  BitWriter* bw = nullptr;       // CAVLC write
+  Bins* bins = nullptr;          // CABAC
+  cabac::Decoder* cabac = nullptr;  // CABAC read (I_PCM repositioning)
+  cabac::Encoder* cenc = nullptr;   // CABAC write (I_PCM raw bytes)
+  const MbDesc* want = nullptr;     // write mode: the macroblock being written
   int prev_qpd_nz = 0;  // mb_qp_delta of the previous MB in decoding order != 0 (CABAC context)
 
   int qp() const { return qp_; }
 
-  bool read_skip_flag(int mb) {
+  // CAVLC primitives in both directions
+  int ue(u32 v) {
+    if constexpr (kWrite) {
+      bw->ue(v);
+      return int(v);
+    } else {
+      return int(br->ue());
+    }
+  }
+  int se(int v) {
+    if constexpr (kWrite) {
+      bw->se(v);
+      return v;
+    } else {
+      return br->se();
+    }
+  }
+  int u(int n, u32 v) {
+    if constexpr (kWrite) {
+      bw->u(n, v);
+      return int(v);
+    } else {
+      return int(br->u(n));
+    }
+  }
+
+  bool read_skip_flag(int mb, bool v = false) {
     MbState& s = nb_.at(mb);
     s = MbState{};
     s.slice = u16(env_.slice);
     nb_.begin(mb);
     auto cond = [&](int m) { return m >= 0 && !nb_.at(m).skip ? 1 : 0; };
     const int inc = cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1));
-    return bins->mb_skip(type_ == h264::kB, inc, false) != 0;
+    return bins->mb_skip(type_ == h264::kB, inc, v) != 0;
   }
 
   void skip_mb(int mb, bool fresh) {
@@ -130,7 +163,7 @@ class MbLayer {
       s.slice = u16(env_.slice);
       nb_.begin(mb);
     }
-    int mbt = read_mb_type(mb);
+    int mbt = read_mb_type(mb, kWrite ? want->mb_type : 0);
     int itype = -1;
     if (type_ == h264::kI) {
       itype = mbt;
@@ -153,29 +186,29 @@ class MbLayer {
     const bool intra = itype >= 0;
     bool no_small = true;  // noSubMbPartSizeLessThan8x8Flag
     if (itype == 0) {
-      if (pps_.transform_8x8_mode) s.t8x8 = u8(read_t8x8(mb));
+      if (pps_.transform_8x8_mode) s.t8x8 = u8(read_t8x8(mb, kWrite && want->t8x8));
       s.kind = s.t8x8 ? kI8x8 : kI4x4;
       intra_modes(mb, s);
-      s.chroma_mode = u8(read_chroma_mode(mb));
+      s.chroma_mode = u8(read_chroma_mode(mb, kWrite ? want->chroma_mode : 0));
     } else if (itype > 0) {
       s.kind = kI16x16;
       i16_mode = (itype - 1) % 4;
       cbp = (((itype - 1) / 4) % 3) << 4 | (itype >= 13 ? 15 : 0);
       std::fill(std::begin(s.i4), std::end(s.i4), u8(2));
-      s.chroma_mode = u8(read_chroma_mode(mb));
+      s.chroma_mode = u8(read_chroma_mode(mb, kWrite ? want->chroma_mode : 0));
     } else {
       s.kind = kInter;
       no_small = inter_pred(mb, s, mbt);
     }
     VEP_CHECK(s.chroma_mode <= 3, "bad intra_chroma_pred_mode");
-    if (s.kind != kI16x16) cbp = read_cbp(mb, s, intra);
+    if (s.kind != kI16x16) cbp = read_cbp(mb, s, intra, kWrite ? want->cbp : 0);
     s.cbp = u8(cbp);
     if (s.kind == kInter && (cbp & 15) && pps_.transform_8x8_mode && no_small &&
         !(type_ == h264::kB && mbt == 0 && !sps_.direct_8x8))
-      s.t8x8 = u8(read_t8x8(mb));
+      s.t8x8 = u8(read_t8x8(mb, kWrite && want->t8x8));
     int qp = qp_;
     if ((cbp & 15) || (cbp >> 4) || s.kind == kI16x16) {
-      const int dqp = read_qp_delta();
+      const int dqp = read_qp_delta(kWrite ? want->qp_delta : 0);
       VEP_CHECK(dqp >= -26 && dqp <= 25, "mb_qp_delta out of range");
       qp = (qp + dqp + 52) % 52;
       prev_qpd_nz = dqp != 0;
@@ -188,6 +221,28 @@ class MbLayer {
     emit(mb, s, res, i16_mode, s.chroma_mode, nullptr);
   }
 
+  // Motion a skipped MB at `mb` would get (encoder decisions): P_Skip or B_Skip / direct.
+  void skip_motion(int mb, MbState& out) {
+    MbState& s = nb_.at(mb);
+    s = MbState{};
+    s.slice = u16(env_.slice);
+    nb_.begin(mb);
+    out = MbState{};
+    out.slice = s.slice;
+    if (type_ == h264::kP) {
+      for (int k = 0; k < 4; ++k) out.ref[0][k] = 0;
+      int mv[2];
+      nb_.pskip_mv(mb, mv);
+      for (auto& v : out.mv[0]) {
+        v[0] = i16(mv[0]);
+        v[1] = i16(mv[1]);
+      }
+    } else {
+      direct(mb, out, 0xF);
+    }
+    s = MbState{};  // (the MB is written later)
+  }
+
   // Pictures the slice's MBs reference (list entries that must exist).
   void need_ref(int list, int idx) {
     const auto* l = env_.list[list];
@@ -197,7 +252,7 @@ class MbLayer {
 
  private:
   // ------------------------------------------------------------------ syntax elements
-  int read_mb_type(int mb) {
+  int read_mb_type(int mb, int v) {
     if constexpr (kCabac) {
       if (type_ == h264::kI) {
         auto cond = [&](int m) {
@@ -205,51 +260,53 @@ class MbLayer {
           const u8 k = nb_.at(m).kind;
           return (k == kI4x4 || k == kI8x8) ? 0 : 1;
         };
-        return bins->mb_type_i(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), 0);
+        return bins->mb_type_i(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), v);
       }
-      if (type_ == h264::kP) return bins->mb_type_p(0);
+      if (type_ == h264::kP) return bins->mb_type_p(v);
       auto cond = [&](int m) { return m >= 0 && !nb_.at(m).direct16 ? 1 : 0; };
-      return bins->mb_type_b(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), 0);
+      return bins->mb_type_b(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), v);
     } else {
-      return int(br->ue());
+      return ue(u32(v));
     }
   }
-  int read_t8x8(int mb) {
+  int read_t8x8(int mb, bool v) {
     if constexpr (kCabac) {
       auto cond = [&](int m) { return m >= 0 && nb_.at(m).t8x8 ? 1 : 0; };
-      return int(bins->transform_8x8(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), false));
+      return int(bins->transform_8x8(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), v));
     } else {
-      return int(br->u1());
+      return u(1, v ? 1u : 0u);
     }
   }
-  int read_chroma_mode(int mb) {
+  int read_chroma_mode(int mb, int v) {
     if constexpr (kCabac) {
       auto cond = [&](int m) {
         if (m < 0) return 0;
         const MbState& n = nb_.at(m);
         return is_intra(n.kind) && n.kind != kIPcm && n.chroma_mode != 0 ? 1 : 0;
       };
-      return bins->chroma_mode(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), 0);
+      return bins->chroma_mode(cond(nb_.mb_at(mb, -1, 0)) + cond(nb_.mb_at(mb, 0, -1)), v);
     } else {
-      return int(br->ue());
+      return ue(u32(v));
     }
   }
-  int read_mode(int pred) {  // prev_intra{4x4,8x8}_pred_mode_flag + rem
+  int read_mode(int pred, int v) {  // prev_intra{4x4,8x8}_pred_mode_flag + rem
+    const bool same = v == pred;
+    const int rem_v = v < pred ? v : v - 1;
     if constexpr (kCabac) {
-      if (bins->prev_intra_flag(false)) return pred;
-      const int rem = bins->rem_intra_mode(0);
+      if (bins->prev_intra_flag(same)) return pred;
+      const int rem = bins->rem_intra_mode(rem_v);
       return rem < pred ? rem : rem + 1;
     } else {
-      if (br->u1()) return pred;
-      const int rem = int(br->u(3));
+      if (u(1, same ? 1u : 0u)) return pred;
+      const int rem = u(3, u32(rem_v));
       return rem < pred ? rem : rem + 1;
     }
   }
-  int read_sub_type() {
-    if constexpr (kCabac) return type_ == h264::kB ? bins->sub_mb_type_b(0) : bins->sub_mb_type_p(0);
-    else return int(br->ue());
+  int read_sub_type(int v) {
+    if constexpr (kCabac) return type_ == h264::kB ? bins->sub_mb_type_b(v) : bins->sub_mb_type_p(v);
+    else return ue(u32(v));
   }
-  int read_ref(int mb, int list, int x4, int y4) {
+  int read_ref(int mb, int list, int x4, int y4, int v) {
     const int n = sh_.num_ref_idx[list];
     if (n <= 1) return 0;
     int r;
@@ -263,15 +320,16 @@ class MbLayer {
         if ((nbs.direct8 >> b8) & 1) return 0;
         return nbs.ref[list][b8] > 0 ? 1 : 0;
       };
-      r = bins->ref_idx(cond(x4 * 4 - 1, y4 * 4) + 2 * cond(x4 * 4, y4 * 4 - 1), 0);
+      r = bins->ref_idx(cond(x4 * 4 - 1, y4 * 4) + 2 * cond(x4 * 4, y4 * 4 - 1), v);
     } else {
-      r = n == 2 ? int(br->u1() ^ 1u) : int(br->ue());
+      if (n == 2) r = u(1, v ? 0u : 1u) ^ 1;
+      else r = ue(u32(v));
     }
     VEP_CHECK(r < n, "ref_idx out of range");
     need_ref(list, r);
     return r;
   }
-  int read_mvd(int mb, int list, int x4, int y4, int comp) {
+  int read_mvd(int mb, int list, int x4, int y4, int comp, int v) {
     if constexpr (kCabac) {
       auto am = [&](int x, int y) -> int {
         const int m = nb_.mb_at(mb, x, y);
@@ -280,12 +338,12 @@ class MbLayer {
         return n.mvd[list][((y & 15) >> 2) * 4 + ((x & 15) >> 2)][comp];
       };
       const int sum = am(x4 * 4 - 1, y4 * 4) + am(x4 * 4, y4 * 4 - 1);
-      return bins->mvd(comp ? 47 : 40, sum < 3 ? 0 : (sum > 32 ? 2 : 1), 0);
+      return bins->mvd(comp ? 47 : 40, sum < 3 ? 0 : (sum > 32 ? 2 : 1), v);
     } else {
-      return br->se();
+      return se(v);
     }
   }
-  int read_cbp(int mb, const MbState& s, bool intra) {
+  int read_cbp(int mb, const MbState& s, bool intra, int v) {
     if constexpr (kCabac) {
       const int am = nb_.mb_at(mb, -1, 0), bm = nb_.mb_at(mb, 0, -1);
       int luma = 0;
@@ -297,26 +355,31 @@ class MbLayer {
         };
         const int ca = (b8 & 1) ? cond(mb, b8 - 1, true) : cond(am, b8 + 1, false);
         const int cb = (b8 & 2) ? cond(mb, b8 - 2, true) : cond(bm, b8 + 2, false);
-        luma |= int(bins->cbp_luma_bin(ca + 2 * cb, false)) << b8;
+        luma |= int(bins->cbp_luma_bin(ca + 2 * cb, (v >> b8) & 1)) << b8;
       }
       auto cc = [&](int m, int thr) { return m >= 0 && (nb_.at(m).cbp >> 4) >= thr ? 1 : 0; };
+      const int vc = v >> 4;
       int chroma = 0;
-      if (bins->cbp_chroma_bin(cc(am, 1) + 2 * cc(bm, 1), false))
-        chroma = 1 + int(bins->cbp_chroma_bin(4 + cc(am, 2) + 2 * cc(bm, 2), false));
+      if (bins->cbp_chroma_bin(cc(am, 1) + 2 * cc(bm, 1), vc != 0))
+        chroma = 1 + int(bins->cbp_chroma_bin(4 + cc(am, 2) + 2 * cc(bm, 2), vc == 2));
       (void)s;
       (void)intra;
       return luma | chroma << 4;
     } else {
-      const u32 me = br->ue();
-      VEP_CHECK(me < 48, "bad coded_block_pattern");
       (void)mb;
       (void)s;
-      return intra ? kCbpIntra[me] : kCbpInter[me];
+      const u8* tab = intra ? kCbpIntra : kCbpInter;
+      u32 code = 0;
+      if constexpr (kWrite)
+        while (code < 48 && tab[code] != v) ++code;
+      const u32 me = u32(ue(code));
+      VEP_CHECK(me < 48, "bad coded_block_pattern");
+      return tab[me];
     }
   }
-  int read_qp_delta() {
-    if constexpr (kCabac) return bins->qp_delta(prev_qpd_nz ? 1 : 0, 0);
-    else return br->se();
+  int read_qp_delta(int v) {
+    if constexpr (kCabac) return bins->qp_delta(prev_qpd_nz ? 1 : 0, v);
+    else return se(v);
   }
 
   // ------------------------------------------------------------------ I_PCM
@@ -330,7 +393,18 @@ class MbLayer {
     for (auto& c : s.tcc) std::fill(std::begin(c), std::end(c), u8(16));
     s.qp = u8(qp_);
     const u8* pcm;
-    if constexpr (kCabac) {
+    if constexpr (kWrite) {
+      pcm = want->pcm;
+      VEP_CHECK(pcm, "I_PCM macroblock without samples");
+      if constexpr (kCabac) {
+        cenc->align_zero();  // pcm_alignment_zero_bit (the terminate bin flushed the engine)
+        cenc->raw_bytes(pcm, kPcmMbBytes);
+        cenc->start();
+      } else {
+        bw->align_zero();
+        bw->bytes(pcm, kPcmMbBytes);
+      }
+    } else if constexpr (kCabac) {
       const size_t off = cabac->aligned_bytepos();
       VEP_CHECK(off + kPcmMbBytes <= data_n, "truncated I_PCM macroblock");
       pcm = data + off;
@@ -356,13 +430,15 @@ class MbLayer {
     const bool ci = pps_.constrained_intra_pred;
     if (s.t8x8) {
       for (int b8 = 0; b8 < 4; ++b8) {
-        const int m = read_mode(nb_.pred_intra8x8(mb, b8, ci));
+        const int m = read_mode(nb_.pred_intra8x8(mb, b8, ci), kWrite ? want->ipred[b8] : 0);
+        VEP_CHECK(m <= 8, "Intra_8x8 mode out of range");
         for (u16 w = b8_blocks(b8); w; w &= w - 1) s.i4[__builtin_ctz(w)] = u8(m);
       }
     } else {
       for (int idx = 0; idx < 16; ++idx) {
         const int r = blk_to_raster(idx);
-        s.i4[r] = u8(read_mode(nb_.pred_intra4x4(mb, r, ci)));
+        s.i4[r] = u8(read_mode(nb_.pred_intra4x4(mb, r, ci), kWrite ? want->ipred[r] : 0));
+        VEP_CHECK(s.i4[r] <= 8, "Intra_4x4 mode out of range");
       }
     }
   }
@@ -426,28 +502,46 @@ class MbLayer {
       for (int l = 0; l < 2; ++l)
         for (int i = 0; i < np; ++i) {
           if (!((pred[i] >> l) & 1)) continue;
-          refs[l][i] = read_ref(mb, l, parts[i].x4, parts[i].y4);
+          refs[l][i] = read_ref(mb, l, parts[i].x4, parts[i].y4, kWrite ? want->ref[l][i] : 0);
           const Part& p = parts[i];
           for (int y = p.y4 / 2; y < (p.y4 + p.h4) / 2; ++y)
             for (int x = p.x4 / 2; x < (p.x4 + p.w4) / 2; ++x) s.ref[l][y * 2 + x] = i8(refs[l][i]);
         }
       int mvd[2][2][2] = {};
+      if constexpr (kWrite) {  // the decoder's predictors in decoding order give the mvds to code
+        for (int l = 0; l < 2; ++l) {
+          u16 done = 0;
+          for (int i = 0; i < np; ++i) {
+            if (!((pred[i] >> l) & 1)) continue;
+            const Part& p = parts[i];
+            int mvp[2];
+            nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, refs[l][i], done, p.shape, mvp);
+            const i16* w = want->mv[l][p.y4 * 4 + p.x4];
+            mvd[l][i][0] = w[0] - mvp[0];
+            mvd[l][i][1] = w[1] - mvp[1];
+            set_mv(s, l, p, w[0], w[1]);
+            done |= part_mask(p);
+          }
+        }
+      }
       for (int l = 0; l < 2; ++l)
         for (int i = 0; i < np; ++i) {
           if (!((pred[i] >> l) & 1)) continue;
-          mvd[l][i][0] = read_mvd(mb, l, parts[i].x4, parts[i].y4, 0);
-          mvd[l][i][1] = read_mvd(mb, l, parts[i].x4, parts[i].y4, 1);
+          mvd[l][i][0] = read_mvd(mb, l, parts[i].x4, parts[i].y4, 0, mvd[l][i][0]);
+          mvd[l][i][1] = read_mvd(mb, l, parts[i].x4, parts[i].y4, 1, mvd[l][i][1]);
           set_mvd(s, l, parts[i], mvd[l][i][0], mvd[l][i][1]);
         }
-      for (int l = 0; l < 2; ++l) {
-        u16 done = 0;
-        for (int i = 0; i < np; ++i) {
-          if (!((pred[i] >> l) & 1)) continue;
-          const Part& p = parts[i];
-          int mvp[2];
-          nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, refs[l][i], done, p.shape, mvp);
-          set_mv(s, l, p, mvp[0] + mvd[l][i][0], mvp[1] + mvd[l][i][1]);
-          done |= part_mask(p);
+      if constexpr (!kWrite) {
+        for (int l = 0; l < 2; ++l) {
+          u16 done = 0;
+          for (int i = 0; i < np; ++i) {
+            if (!((pred[i] >> l) & 1)) continue;
+            const Part& p = parts[i];
+            int mvp[2];
+            nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, refs[l][i], done, p.shape, mvp);
+            set_mv(s, l, p, mvp[0] + mvd[l][i][0], mvp[1] + mvd[l][i][1]);
+            done |= part_mask(p);
+          }
         }
       }
       return true;
@@ -455,9 +549,9 @@ class MbLayer {
     // P_8x8 / P_8x8ref0 / B_8x8
     int sub[4];
     bool no_small = true;
-    for (int& t : sub) {
-      t = read_sub_type();
-      VEP_CHECK(t <= (b ? 12 : 3), "bad sub_mb_type");
+    for (int i = 0; i < 4; ++i) {
+      sub[i] = read_sub_type(kWrite ? want->sub[i] : 0);
+      VEP_CHECK(sub[i] <= (b ? 12 : 3), "bad sub_mb_type");
     }
     u8 spred[4], sshape[4];
     for (int i = 0; i < 4; ++i) {
@@ -477,7 +571,7 @@ class MbLayer {
     for (int l = 0; l < 2; ++l)
       for (int i = 0; i < 4; ++i) {
         if (!((spred[i] >> l) & 1)) continue;
-        const int r = (!b && mbt == 4) ? 0 : read_ref(mb, l, (i & 1) * 2, (i >> 1) * 2);
+        const int r = (!b && mbt == 4) ? 0 : read_ref(mb, l, (i & 1) * 2, (i >> 1) * 2, kWrite ? want->ref[l][i] : 0);
         if (!b && mbt == 4) need_ref(0, 0);
         s.ref[l][i] = i8(r);
       }
@@ -491,38 +585,48 @@ class MbLayer {
         default: return {x8 + (j & 1), y8 + (j >> 1), 1, 1, 0};
       }
     };
+    // motion in 8x8 order (direct 8x8s included, so later sub-partitions predict from them);
+    // write mode derives the mvds to code here, before the mvd syntax
+    auto derive = [&](bool write) {
+      if (s.direct8) direct(mb, s, s.direct8);
+      u16 done[2] = {0, 0};
+      for (int i = 0; i < 4; ++i) {
+        if ((s.direct8 >> i) & 1) {
+          done[0] |= b8_blocks(i);
+          done[1] |= b8_blocks(i);
+          continue;
+        }
+        for (int l = 0; l < 2; ++l) {
+          if (!((spred[i] >> l) & 1)) continue;
+          for (int j = 0; j < kSubParts[sshape[i]]; ++j) {
+            const Part p = sub_part(i, j);
+            int mvp[2];
+            nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, s.ref[l][i], done[l], 0, mvp);
+            if (write) {
+              const i16* w = want->mv[l][p.y4 * 4 + p.x4];
+              mvd[l][i][j][0] = w[0] - mvp[0];
+              mvd[l][i][j][1] = w[1] - mvp[1];
+            }
+            set_mv(s, l, p, mvp[0] + mvd[l][i][j][0], mvp[1] + mvd[l][i][j][1]);
+            done[l] |= part_mask(p);
+          }
+        }
+        done[0] |= b8_blocks(i);
+        done[1] |= b8_blocks(i);
+      }
+    };
+    if constexpr (kWrite) derive(true);
     for (int l = 0; l < 2; ++l)
       for (int i = 0; i < 4; ++i) {
         if (!((spred[i] >> l) & 1)) continue;
         for (int j = 0; j < kSubParts[sshape[i]]; ++j) {
           const Part p = sub_part(i, j);
-          mvd[l][i][j][0] = read_mvd(mb, l, p.x4, p.y4, 0);
-          mvd[l][i][j][1] = read_mvd(mb, l, p.x4, p.y4, 1);
+          mvd[l][i][j][0] = read_mvd(mb, l, p.x4, p.y4, 0, mvd[l][i][j][0]);
+          mvd[l][i][j][1] = read_mvd(mb, l, p.x4, p.y4, 1, mvd[l][i][j][1]);
           set_mvd(s, l, p, mvd[l][i][j][0], mvd[l][i][j][1]);
         }
       }
-    // motion in 8x8 order (direct 8x8s included, so later sub-partitions predict from them)
-    if (s.direct8) direct(mb, s, s.direct8);
-    u16 done[2] = {0, 0};
-    for (int i = 0; i < 4; ++i) {
-      if ((s.direct8 >> i) & 1) {
-        done[0] |= b8_blocks(i);
-        done[1] |= b8_blocks(i);
-        continue;
-      }
-      for (int l = 0; l < 2; ++l) {
-        if (!((spred[i] >> l) & 1)) continue;
-        for (int j = 0; j < kSubParts[sshape[i]]; ++j) {
-          const Part p = sub_part(i, j);
-          int mvp[2];
-          nb_.pred_mv(mb, p.x4, p.y4, p.w4, p.h4, l, s.ref[l][i], done[l], 0, mvp);
-          set_mv(s, l, p, mvp[0] + mvd[l][i][j][0], mvp[1] + mvd[l][i][j][1]);
-          done[l] |= part_mask(p);
-        }
-      }
-      done[0] |= b8_blocks(i);
-      done[1] |= b8_blocks(i);
-    }
+    if constexpr (!kWrite) derive(false);
     return no_small;
   }
 
@@ -631,57 +735,7 @@ class MbLayer {
   }
 
   // ------------------------------------------------------------------ weighted prediction
-  // WpEntry of an 8x8 partition with reference indices (r0, r1) (-1 = list unused).
-  WpEntry weights(int r0, int r1) {
-    WpEntry e{};
-    for (int c = 0; c < 3; ++c) {
-      e.w0[c] = e.w1[c] = 1;
-      e.o[c] = 0;
-      e.lwd[c] = 0;
-    }
-    if (implicit_) {
-      if (r0 < 0 || r1 < 0) return e;
-      const ListEntry& p0 = (*env_.list[0])[size_t(r0)];
-      const ListEntry& p1 = (*env_.list[1])[size_t(r1)];
-      int w0 = 32, w1 = 32;
-      const int td = clip3i(-128, 127, p1.poc - p0.poc);
-      if (td != 0 && !p0.long_term && !p1.long_term) {
-        const int tb = clip3i(-128, 127, env_.cur_poc - p0.poc);
-        const int tx = (16384 + std::abs(td / 2)) / td;
-        const int dsf = clip3i(-1024, 1023, (tb * tx + 32) >> 6);
-        if ((dsf >> 2) >= -64 && (dsf >> 2) <= 128) {
-          w1 = dsf >> 2;
-          w0 = 64 - w1;
-        }
-      }
-      for (int c = 0; c < 3; ++c) {
-        e.w0[c] = i16(w0);
-        e.w1[c] = i16(w1);
-        e.lwd[c] = 5;
-      }
-      return e;
-    }
-    // explicit
-    for (int c = 0; c < 3; ++c) e.lwd[c] = u8(c == 0 ? sh_.luma_lwd : sh_.chroma_lwd);
-    int o0[3] = {0, 0, 0}, o1[3] = {0, 0, 0};
-    if (r0 >= 0) {
-      const auto& w = sh_.wt[0][size_t(r0)];
-      for (int c = 0; c < 3; ++c) {
-        e.w0[c] = w.w[c];
-        o0[c] = w.o[c];
-      }
-    }
-    if (r1 >= 0) {
-      const auto& w = sh_.wt[1][size_t(r1)];
-      for (int c = 0; c < 3; ++c) {
-        e.w1[c] = w.w[c];
-        o1[c] = w.o[c];
-      }
-    }
-    for (int c = 0; c < 3; ++c)
-      e.o[c] = i16(r0 >= 0 && r1 >= 0 ? (o0[c] + o1[c] + 1) >> 1 : (r0 >= 0 ? o0[c] : o1[c]));
-    return e;
-  }
+  WpEntry weights(int r0, int r1) { return wp_entry(env_, r0, r1); }
 
   // ------------------------------------------------------------------ residual
   // coded_block_flag context increments (§9.3.3.1.1.9).
@@ -726,16 +780,20 @@ class MbLayer {
     return a + 2 * bb;
   }
 
-  // One residual block's levels (scan order) into lv[0..n-1]; returns TotalCoeff.
-  int read_block(int cat, int cbf_inc, int nc, int n, int* lv) {
-    std::memset(lv, 0, size_t(n) * sizeof(int));
+  // One residual block's levels (scan order) into lv[0..n-1] (write mode: the levels of `src`
+  // are coded); returns TotalCoeff.
+  int read_block(int cat, int cbf_inc, int nc, int n, int* lv, const int* src) {
+    if constexpr (kWrite) std::memcpy(lv, src, size_t(n) * sizeof(int));
+    else std::memset(lv, 0, size_t(n) * sizeof(int));
+    (void)src;
     if constexpr (kCabac) {
       (void)nc;
       return bins->residual(cat, cbf_inc, n, lv);
     } else {
       (void)cat;
       (void)cbf_inc;
-      return read_residual_block_cb(*br, nc, n, [lv](int k, int l) { lv[k] = l; });
+      if constexpr (kWrite) return write_residual_block(*bw, nc, n, lv);
+      else return read_residual_block_cb(*br, nc, n, [lv](int k, int l) { lv[k] = l; });
     }
   }
 
@@ -747,7 +805,7 @@ class MbLayer {
       const int inc = kCabac ? cbf_dc_inc(mb, 0, true) : 0;
       const int nc = kCabac ? 0 : nb_.nc_luma(mb, 0);
       int dcy[16] = {};
-      if (read_block(kCatLumaDc, inc, nc, 16, lv) > 0) {
+      if (read_block(kCatLumaDc, inc, nc, 16, lv, kWrite ? want->dc : nullptr) > 0) {
         s.cbf_dc |= 1;
         int c[16];
         for (int k = 0; k < 16; ++k) c[kZigzag4x4[k]] = lv[k];
@@ -766,7 +824,7 @@ class MbLayer {
         if (cbp_luma) {
           const int binc = kCabac ? cbf_luma_inc(mb, r, true) : 0;
           const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
-          tc = read_block(kCatLumaAc, binc, bnc, 15, lv);
+          tc = read_block(kCatLumaAc, binc, bnc, 15, lv, kWrite ? want->ac[r] : nullptr);
           for (int k = 0; k < 15; ++k) {
             if (!lv[k]) continue;
             const int pos = kZigzag4x4[k + 1];
@@ -787,12 +845,15 @@ class MbLayer {
         int c64[64] = {};
         int total = 0;
         if constexpr (kCabac) {
-          total = read_block(kCatLuma8x8, -1, 0, 64, c64);
+          total = read_block(kCatLuma8x8, -1, 0, 64, c64, kWrite ? want->l8[b8] : nullptr);
           for (u16 w = b8_blocks(b8); w; w &= w - 1) s.tc[__builtin_ctz(w)] = u8(std::min(total, 16));
         } else {
           for (int i4 = 0; i4 < 4; ++i4) {
             const int r = blk_to_raster(b8 * 4 + i4);
-            const int tc = read_block(kCatLuma4x4, 0, nb_.nc_luma(mb, r), 16, lv);
+            int part[16] = {};
+            if constexpr (kWrite)
+              for (int k = 0; k < 16; ++k) part[k] = want->l8[b8][4 * k + i4];
+            const int tc = read_block(kCatLuma4x4, 0, nb_.nc_luma(mb, r), 16, lv, part);
             s.tc[r] = u8(tc);
             total += tc;
             for (int k = 0; k < 16; ++k) c64[4 * k + i4] = lv[k];
@@ -820,7 +881,7 @@ class MbLayer {
         if (!((cbp_luma >> (idx >> 2)) & 1)) continue;
         const int binc = kCabac ? cbf_luma_inc(mb, r, intra) : 0;
         const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
-        const int tc = read_block(kCatLuma4x4, binc, bnc, 16, lv);
+        const int tc = read_block(kCatLuma4x4, binc, bnc, 16, lv, kWrite ? want->ac[r] : nullptr);
         s.tc[r] = u8(tc);
         if (tc) s.cbf |= u16(1u << r);
         if (!tc) continue;
@@ -844,7 +905,7 @@ class MbLayer {
       for (int c = 0; c < 2; ++c) {
         const int inc = kCabac ? cbf_dc_inc(mb, 1 + c, intra) : 0;
         int v4[4];
-        if (read_block(kCatChromaDc, inc, -1, 4, v4) > 0) {
+        if (read_block(kCatChromaDc, inc, -1, 4, v4, kWrite ? want->cdc[c] : nullptr) > 0) {
           s.cbf_dc |= u8(2 << c);
           const int f[4] = {v4[0] + v4[1] + v4[2] + v4[3], v4[0] - v4[1] + v4[2] - v4[3],
                             v4[0] + v4[1] - v4[2] - v4[3], v4[0] - v4[1] - v4[2] + v4[3]};
@@ -862,7 +923,7 @@ class MbLayer {
           if (cbp_chroma & 2) {
             const int binc = kCabac ? cbf_cac_inc(mb, c, b, intra) : 0;
             const int bnc = kCabac ? 0 : nb_.nc_chroma(mb, c, b);
-            const int tc = read_block(kCatChromaAc, binc, bnc, 15, lv);
+            const int tc = read_block(kCatChromaAc, binc, bnc, 15, lv, kWrite ? want->cac[c][b] : nullptr);
             s.tcc[c][b] = u8(tc);
             if (tc) s.cbf_cac[c] |= u8(1u << b);
             for (int k = 0; k < 15; ++k) {
@@ -877,7 +938,7 @@ class MbLayer {
         }
       }
     }
-    if constexpr (!kCabac) VEP_CHECK(!br->overrun(), "slice data overrun");
+    if constexpr (!kCabac && !kWrite) VEP_CHECK(!br->overrun(), "slice data overrun");
   }
 
   // ------------------------------------------------------------------ MbRec
@@ -956,6 +1017,60 @@ class MbLayer {
 
 }  // namespace
 
+// WpEntry of an 8x8 partition with reference indices (r0, r1) (-1 = list unused): explicit
+// weights from the slice header, implicit weights from POC distances (§8.4.2.3).
+WpEntry wp_entry(const SliceEnv& env, int r0, int r1) {
+  const SliceHdr& sh = *env.sh;
+  const bool implicit = sh.type() == h264::kB && env.pps->weighted_bipred_idc == 2;
+  WpEntry e{};
+  for (int c = 0; c < 3; ++c) {
+    e.w0[c] = e.w1[c] = 1;
+    e.o[c] = 0;
+    e.lwd[c] = 0;
+  }
+  if (implicit) {
+    if (r0 < 0 || r1 < 0) return e;
+    const ListEntry& p0 = (*env.list[0])[size_t(r0)];
+    const ListEntry& p1 = (*env.list[1])[size_t(r1)];
+    int w0 = 32, w1 = 32;
+    const int td = clip3i(-128, 127, p1.poc - p0.poc);
+    if (td != 0 && !p0.long_term && !p1.long_term) {
+      const int tb = clip3i(-128, 127, env.cur_poc - p0.poc);
+      const int tx = (16384 + std::abs(td / 2)) / td;
+      const int dsf = clip3i(-1024, 1023, (tb * tx + 32) >> 6);
+      if ((dsf >> 2) >= -64 && (dsf >> 2) <= 128) {
+        w1 = dsf >> 2;
+        w0 = 64 - w1;
+      }
+    }
+    for (int c = 0; c < 3; ++c) {
+      e.w0[c] = i16(w0);
+      e.w1[c] = i16(w1);
+      e.lwd[c] = 5;
+    }
+    return e;
+  }
+  for (int c = 0; c < 3; ++c) e.lwd[c] = u8(c == 0 ? sh.luma_lwd : sh.chroma_lwd);
+  int o0[3] = {0, 0, 0}, o1[3] = {0, 0, 0};
+  if (r0 >= 0) {
+    const auto& w = sh.wt[0][size_t(r0)];
+    for (int c = 0; c < 3; ++c) {
+      e.w0[c] = w.w[c];
+      o0[c] = w.o[c];
+    }
+  }
+  if (r1 >= 0) {
+    const auto& w = sh.wt[1][size_t(r1)];
+    for (int c = 0; c < 3; ++c) {
+      e.w1[c] = w.w[c];
+      o1[c] = w.o[c];
+    }
+  }
+  for (int c = 0; c < 3; ++c)
+    e.o[c] = i16(r0 >= 0 && r1 >= 0 ? (o0[c] + o1[c] + 1) >> 1 : (r0 >= 0 ? o0[c] : o1[c]));
+  return e;
+}
+
 void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const u8* data, size_t n,
                           size_t bitpos) {
   const SliceHdr& sh = *env.sh;
@@ -973,7 +1088,7 @@ void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, c
     cabac::Decoder dec(data, n, start);
     BinDecoder bd{dec, ctx};
     AvcBins<BinDecoder> bins{bd};
-    MbLayer<true> L(nb, pic, env, dq);
+    MbLayer<true, false> L(nb, pic, env, dq);
     L.bins = &bins;
     L.cabac = &dec;
     L.data = data;
@@ -990,7 +1105,7 @@ void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, c
   }
   Bits br(data, n, bitpos);
   const size_t stop = BitReader(data, n).stop_bit_pos();
-  MbLayer<false> L(nb, pic, env, dq);
+  MbLayer<false, false> L(nb, pic, env, dq);
   L.br = &br;
   bool more = true;
   while (more) {
@@ -1010,5 +1125,85 @@ void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, c
     ++mb;
   }
 }
+
+// ---------------------------------------------------------------------------- SliceWriter
+
+struct SliceWriter::Impl {
+  const SliceEnv& env;
+  BitWriter& bw;
+  Dequant dq;
+  bool cabac;
+  bool is_i;
+  int run = 0;      // CAVLC mb_skip_run
+  bool first = true;
+  cabac::Ctx ctx[kCabacCtx];
+  std::unique_ptr<cabac::Encoder> enc;
+  std::unique_ptr<BinEncoder> be;
+  std::unique_ptr<AvcBins<BinEncoder>> bins;
+  std::unique_ptr<MbLayer<true, true>> lc;
+  std::unique_ptr<MbLayer<false, true>> lv;
+  Impl(MbNeighbours& nb, Picture& pic, const SliceEnv& e, BitWriter& w)
+      : env(e), bw(w), dq(e.scaling), cabac(e.pps->cabac), is_i(e.sh->type() == h264::kI) {
+    if (cabac) {
+      while (!bw.byte_aligned()) bw.u1(1);  // cabac_alignment_one_bit
+      cabac_init_contexts(ctx, is_i ? -1 : 0, e.sh->qp);
+      enc = std::make_unique<cabac::Encoder>(bw.buf());
+      be = std::make_unique<BinEncoder>(BinEncoder{*enc, ctx});
+      bins = std::make_unique<AvcBins<BinEncoder>>(AvcBins<BinEncoder>{*be});
+      lc = std::make_unique<MbLayer<true, true>>(nb, pic, env, dq);
+      lc->bins = bins.get();
+      lc->cenc = enc.get();
+    } else {
+      lv = std::make_unique<MbLayer<false, true>>(nb, pic, env, dq);
+      lv->bw = &bw;
+    }
+  }
+};
+
+SliceWriter::SliceWriter(MbNeighbours& nb, Picture& pic, const SliceEnv& env, BitWriter& bw)
+    : p_(std::make_unique<Impl>(nb, pic, env, bw)) {}
+SliceWriter::~SliceWriter() = default;
+
+void SliceWriter::write_mb(int mb, const MbDesc& d) {
+  Impl& p = *p_;
+  VEP_CHECK(!(d.skip && p.is_i), "skipped macroblock in an I slice");
+  if (p.cabac) {
+    if (!p.first) p.bins->end_of_slice(false);
+    p.first = false;
+    p.lc->want = &d;
+    if (!p.is_i && p.lc->read_skip_flag(mb, d.skip)) p.lc->skip_mb(mb, false);
+    else p.lc->coded_mb(mb, p.is_i);
+    return;
+  }
+  p.lv->want = &d;
+  if (d.skip) {
+    p.lv->skip_mb(mb, true);
+    ++p.run;
+    return;
+  }
+  if (!p.is_i) {
+    p.bw.ue(u32(p.run));
+    p.run = 0;
+  }
+  p.lv->coded_mb(mb, true);
+}
+
+void SliceWriter::finish() {
+  Impl& p = *p_;
+  if (p.cabac) {
+    p.bins->end_of_slice(true);  // terminate + flush: the flush ends with the rbsp_stop_one_bit
+    p.enc->align_zero();
+    return;
+  }
+  if (p.run > 0) p.bw.ue(u32(p.run));
+  p.bw.trailing();
+}
+
+void SliceWriter::skip_motion(int mb, MbState& out) {
+  if (p_->cabac) p_->lc->skip_motion(mb, out);
+  else p_->lv->skip_motion(mb, out);
+}
+
+int SliceWriter::qp() const { return p_->cabac ? p_->lc->qp() : p_->lv->qp(); }
 
 }  // namespace vep::avc

@@ -368,7 +368,21 @@ std::vector<u8> write_sps(const Sps& s) {
     bw.ue(0);   // bit_depth_luma_minus8
     bw.ue(0);   // bit_depth_chroma_minus8
     bw.u1(0);   // qpprime_y_zero_transform_bypass_flag
-    bw.u1(0);   // seq_scaling_matrix_present_flag
+    bw.u1(s.scaling_matrix_present);
+    if (s.scaling_matrix_present) {  // all eight lists explicit (delta-coded, §7.3.2.1.1.1)
+      auto list = [&](const u8* v, int n) {
+        bw.u1(1);
+        int last = 8;
+        for (int k = 0; k < n; ++k) {
+          int d = (int(v[k]) - last + 256) % 256;
+          if (d > 127) d -= 256;
+          bw.se(d);
+          last = v[k];
+        }
+      };
+      for (int l = 0; l < 6; ++l) list(s.scaling.l4[l], 16);
+      for (int l = 0; l < 2; ++l) list(s.scaling.l8[l], 64);
+    }
   }
   bw.ue(s.log2_max_frame_num - 4);
   bw.ue(s.poc_type);

@@ -72,26 +72,52 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
   if (cfg.motion <= 0) bw_ = bh_ = 0;
   if (cfg.compressed) {
     VEP_CHECK(cfg.codec == Codec::kH264, "compressed synthetic streams are H.264 only");
-    avc::AvcEncConfig ac;
-    ac.width = cfg.width;
-    ac.height = cfg.height;
-    ac.fps = cfg.fps;
-    ac.gop = cfg.gop;
-    ac.idr_phase = cfg.idr_phase;
-    ac.qp = cfg.qp;
-    ac.slices = cfg.slices;
-    ac.refs = cfg.refs;
-    ac.objects = cfg.objects;
-    ac.seed = cfg.seed;
-    ac.deblock_idc = cfg.deblock_idc;
-    ac.coverage = cfg.coverage;
-    ac.noise = cfg.noise;
-    ac.temporal_noise = cfg.temporal_noise;
-    if (cfg.coverage) {
-      ac.pcm_rate = 3;
-      ac.nonref_rate = 15;
+    if (cfg.profile == "main" || cfg.profile == "high") {
+      avc::AvcHighConfig hc;
+      hc.width = cfg.width;
+      hc.height = cfg.height;
+      hc.fps = cfg.fps;
+      hc.gop = cfg.gop;
+      hc.idr_phase = cfg.idr_phase;
+      hc.qp = cfg.qp;
+      hc.slices = cfg.slices;
+      hc.refs = cfg.refs;
+      hc.bframes = cfg.bframes;
+      hc.cabac = cfg.cabac;
+      hc.t8x8 = cfg.profile == "high";
+      hc.weighted_p = cfg.weighted_p;
+      hc.weighted_b = cfg.weighted_b;
+      hc.direct_spatial = cfg.direct_spatial;
+      hc.objects = cfg.objects;
+      hc.seed = cfg.seed;
+      hc.deblock_idc = cfg.deblock_idc;
+      hc.coverage = cfg.coverage;
+      hc.noise = cfg.noise;
+      hc.temporal_noise = cfg.temporal_noise;
+      avc_ = std::make_unique<avc::AvcHighEncoder>(hc);
+    } else {
+      VEP_CHECK(cfg.profile == "baseline", "profile must be baseline, main or high");
+      avc::AvcEncConfig ac;
+      ac.width = cfg.width;
+      ac.height = cfg.height;
+      ac.fps = cfg.fps;
+      ac.gop = cfg.gop;
+      ac.idr_phase = cfg.idr_phase;
+      ac.qp = cfg.qp;
+      ac.slices = cfg.slices;
+      ac.refs = cfg.refs;
+      ac.objects = cfg.objects;
+      ac.seed = cfg.seed;
+      ac.deblock_idc = cfg.deblock_idc;
+      ac.coverage = cfg.coverage;
+      ac.noise = cfg.noise;
+      ac.temporal_noise = cfg.temporal_noise;
+      if (cfg.coverage) {
+        ac.pcm_rate = 3;
+        ac.nonref_rate = 15;
+      }
+      avc_ = std::make_unique<avc::AvcEncoder>(ac);
     }
-    avc_ = std::make_unique<avc::AvcEncoder>(ac);
     sps_nal_ = avc_->sps_nal();
     pps_nal_ = avc_->pps_nal();
   }

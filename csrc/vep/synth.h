@@ -34,6 +34,14 @@ struct SynthConfig {
   bool coverage = false;   // randomised mode decisions (decoder coverage streams)
   double noise = 3.0;      // static texture amplitude of the compressed scene
   double temporal_noise = 0.0;  // per-frame sensor noise (P-picture residual, bitrate)
+  // Compressed H.264 profile: "baseline" (CAVLC I/P, avc::AvcEncoder), "main" (CABAC, B
+  // pictures) or "high" (main + 8x8 transform / Intra_8x8) — avc::AvcHighEncoder.
+  std::string profile = "baseline";
+  int bframes = 2;           // main / high: B pictures between anchors (pyramid when >= 2)
+  bool cabac = true;         // main / high entropy coder (false: CAVLC)
+  bool weighted_p = false;   // main / high: explicit weighted prediction in P slices
+  int weighted_b = 0;        // main / high: weighted_bipred_idc
+  bool direct_spatial = true;
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)
@@ -45,6 +53,8 @@ class SynthH264 {  // (both codecs; the name predates H.265 support)
   const HostSurface& picture() const { return avc_ ? avc_->reconstruction() : pic_; }
   // the scene that was encoded (compressed streams: the encoder's source picture)
   const HostSurface& source() const { return avc_ ? avc_->source() : pic_; }
+  // pts of the last AU (compressed streams with B pictures: the display time of `picture()`)
+  i64 last_pts() const { return avc_ ? avc_->last_pts() : frame_ * 90000 / cfg_.fps; }
   const std::vector<u8>& sps_nal() const { return sps_nal_; }
   const std::vector<u8>& pps_nal() const { return pps_nal_; }
   const std::vector<u8>& vps_nal() const { return vps_nal_; }  // H.265 only
@@ -76,7 +86,7 @@ class SynthH264 {  // (both codecs; the name predates H.265 support)
   int idr_id_ = 0, frame_num_ = 0;
   u64 state_;
   Rect prev_box_{0, 0, 0, 0};
-  std::unique_ptr<avc::AvcEncoder> avc_;  // compressed H.264 streams
+  std::unique_ptr<avc::StreamEncoder> avc_;  // compressed H.264 streams
 };
 
 }  // namespace vep

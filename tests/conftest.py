@@ -49,3 +49,32 @@ def synth(native, w=640, h=480, gop=10, motion=0.05, seed=1, slices=1, zero=Fals
     c.compressed, c.coverage, c.refs, c.qp = compressed, coverage, refs, qp
     c.deblock_idc, c.objects = deblock_idc, objects
     return native.SynthH264(c)
+
+
+def high_encoder(native, w=176, h=144, **kw):
+    """Main / High-profile synthetic encoder (avc::AvcHighEncoder); kw = AvcHighConfig fields."""
+    c = native.AvcHighConfig()
+    c.width, c.height = w, h
+    for k, v in kw.items():
+        if not hasattr(c, k):
+            raise AttributeError(k)
+        setattr(c, k, v)
+    return native.AvcHighEncoder(c)
+
+
+def roundtrip(native, enc, n):
+    """Encode n pictures and decode them on the CPU: ({pts: encoder NV12}, {pts: decoder NV12},
+    decoder, access units). Decoder frames are collected from every reorder-buffer output."""
+    dec = native.CpuDecoder()
+    rec, got, aus = {}, {}, []
+    for _ in range(n):
+        au = enc.next()
+        aus.append(au)
+        y, uv = enc.picture()
+        rec[enc.last_pts] = (y.copy(), uv.copy())
+        dec.decode(au)
+        for pts, planes in dec.frames():
+            got[pts] = planes
+    for pts, planes in dec.flush_frames():
+        got[pts] = planes
+    return rec, got, dec, aus

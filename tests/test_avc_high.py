@@ -88,3 +88,129 @@ def test_third_party_clip_corruption_never_crashes(native):
             if i >= 30:
                 assert got is not None and np.array_equal(got, want[i]), f"trial {trial}: frame {i}"
         assert isinstance(broken, bool)
+
+
+# ---------------------------------------------------------------------------------------------
+# Closed-loop Main / High encoder (avc::AvcHighEncoder) <-> CPU decoder. The encoder writes
+# every macroblock through the decoder's own macroblock layer (write mode) and reconstructs it
+# with the decoder's reconstruction, so these round trips pin that both directions of the
+# symmetric layer agree and that the slice / DPB / reference-list / output-order layers of the
+# encoder and the decoder match. (The spec conformance of the B-slice CABAC syntax itself is
+# pinned by no third-party stream available here: parity unpinned beyond this closed loop and
+# the spec-derived table tests.)
+from conftest import high_encoder, roundtrip  # noqa: E402
+
+HIGH_CONFIGS = {
+    "high-cabac-ibbp-pyramid": dict(bframes=2),
+    "high-cabac-ibbbp-temporal": dict(bframes=3, direct_spatial=False),
+    "high-cavlc-ibp": dict(bframes=1, cabac=False),
+    "main-cabac-ibbp": dict(bframes=2, t8x8=False),
+    "high-weighted-explicit": dict(bframes=2, weighted_p=True, weighted_b=1),
+    "high-weighted-implicit-temporal": dict(bframes=3, weighted_b=2, direct_spatial=False),
+    "cov-cabac": dict(bframes=2, coverage=True),
+    "cov-cavlc-temporal": dict(bframes=2, coverage=True, cabac=False, direct_spatial=False),
+    "cov-scaling-slices-wp": dict(bframes=3, coverage=True, scaling=True, slices=3, weighted_b=1,
+                                  weighted_p=True, chroma_qp_offset=-2, second_chroma_qp_offset=3),
+    "cov-implicit-dbk2": dict(bframes=2, coverage=True, direct_spatial=False, weighted_b=2,
+                              slices=2, deblock_idc=2),
+    "cov-refs4-nopyramid": dict(bframes=2, pyramid=False, refs=4, coverage=True, gop=7),
+}
+
+
+@pytest.mark.parametrize("name", sorted(HIGH_CONFIGS))
+def test_high_encoder_roundtrip_bit_exact(native, name):
+    kw = HIGH_CONFIGS[name]
+    enc = high_encoder(native, 176, 144, gop=kw.pop("gop", 12), seed=7, **kw)
+    rec, got, dec, _ = roundtrip(native, enc, 20)
+    assert len(rec) == 20 and set(got) == set(rec)
+    for pts in sorted(rec):
+        ey, euv = rec[pts]
+        gy, guv = got[pts]
+        assert np.array_equal(ey, gy) and np.array_equal(euv, guv), f"{name}: pts {pts} differs"
+    st = dec.mb_stats
+    bf = HIGH_CONFIGS[name].get("bframes", 2)
+    assert "B" in st["types"] if bf else "B" not in st["types"]
+    if bf:
+        assert st["bipred"] > 0 and st["list1_only"] > 0
+    if HIGH_CONFIGS[name].get("t8x8", True):
+        assert st["t8x8"] > 0 and st["i8x8"] > 0
+    if HIGH_CONFIGS[name].get("weighted_b") or HIGH_CONFIGS[name].get("weighted_p"):
+        assert st["weighted"] > 0
+    if HIGH_CONFIGS[name].get("coverage"):
+        assert st["i4x4"] > 0 and st["i16x16"] > 0 and st["pcm"] > 0 and st["skip"] > 0
+
+
+def test_high_encoder_output_order_and_quality(native):
+    """Realistic (non-coverage) High CABAC IBBP: frames leave the decoder in display order, one
+    per access unit overall, and the reconstruction is close to the source scene."""
+    enc = high_encoder(native, 320, 240, bframes=3, gop=16, seed=2, qp=26)
+    dec = native.CpuDecoder()
+    order, src = [], {}
+    for _ in range(24):
+        au = enc.next()
+        src[enc.last_pts] = enc.source()[0].copy()
+        dec.decode(au)
+        order += [pts for pts, _ in dec.frames()]
+        rec = enc.picture()[0]
+        err = rec[:240, :320].astype(float) - src[enc.last_pts][:240, :320]
+        assert 10 * np.log10(255.0 ** 2 / max(1e-9, (err ** 2).mean())) > 33
+    order += [pts for pts, _ in dec.flush_frames()]
+    assert order == sorted(order) and len(order) == 24
+
+
+def test_high_profile_synth_camera(native):
+    """SynthConfig.profile routes the synthetic camera to the High encoder (what the camera farm
+    and bench --profile high stream)."""
+    c = native.SynthConfig()
+    c.width, c.height, c.gop, c.compressed, c.profile, c.bframes = 176, 144, 8, True, "high", 2
+    s = native.SynthH264(c)
+    nal_types = []
+    dec = native.CpuDecoder()
+    outs = 0
+    for _ in range(10):
+        au = s.next()
+        nal_types += [n[0] & 0x1F for n in au.nals()]
+        outs += dec.decode(au) is not None
+    assert nal_types[:2] == [7, 8] and 5 in nal_types
+    sps = native.parse_sps(s.sps_nal)
+    assert sps["profile_idc"] == 100
+    assert "B" in dec.mb_stats["types"] and outs >= 7  # (reorder depth 2 still holds some)
+    c.profile = "bogus"
+    with pytest.raises(native.NativeError):
+        native.SynthH264(c)
+
+
+def test_high_stream_corruption_never_crashes(native):
+    """Bit flips in CABAC B / P slices: the decoder raises or decodes, never crashes, and
+    recovers bit-exact at the next IDR."""
+    import random
+
+    rnd = random.Random(5)
+    enc = high_encoder(native, 176, 144, bframes=2, gop=8, seed=9, coverage=True)
+    aus = [enc.next() for _ in range(24)]
+    clean = native.CpuDecoder()
+    want = {}
+    for a in aus:
+        clean.decode(a)
+        for pts, (y, uv) in clean.frames():
+            want[pts] = y
+    for trial in range(12):
+        dec = native.CpuDecoder()
+        bad = rnd.randrange(1, 14)
+        for i, a in enumerate(aus):
+            if i == bad:
+                nals = [bytearray(n) for n in a.nals()]
+                sl = [k for k, x in enumerate(nals) if (x[0] & 0x1F) in (1, 5)][0]
+                for _ in range(rnd.randint(1, 5)):
+                    pos = rnd.randrange(3, len(nals[sl]))
+                    nals[sl][pos] ^= 1 << rnd.randrange(8)
+                a = native.AccessUnit.from_nals([bytes(x) for x in nals], pts=a.pts, dts=a.dts, keyframe=a.keyframe)
+            try:
+                dec.decode(a)
+            except (native.NativeError, native.UnsupportedStream):
+                continue
+            if i >= 16:  # pictures from the IDR at display 16 on equal the clean stream's
+                for pts, (y, uv) in dec.frames():
+                    if pts < 18 * 3000:  # (pts = (display + reorder depth 2) * 3000)
+                        continue
+                    assert np.array_equal(y, want[pts]), f"trial {trial} pts {pts}"
