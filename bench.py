@@ -4,7 +4,7 @@
 One rank per GPU (torch.distributed over RCCL when WORLD_SIZE > 1). Each rank owns
 ``--cams-per-gpu`` synthetic 1080p30 H.264 cameras (camera data parallelism, weak scaling). One
 *step* is one frame tick: every camera on the rank decodes one access unit —
-  host:  CAVLC macroblock-layer parse of the real H.264 AU (thread pool, pipelined one tick ahead)
+  host:  CABAC/CAVLC macroblock-layer parse of the real H.264 AU (thread pool, pipelined one tick ahead)
   GPU:   one batched gfx950 launch: I_PCM reconstruction into the NV12 reference surfaces +
          BT.601 NV12->BGR24 into each camera's HBM ring slot, then a batched letterbox kernel
          writing the 640x640 consumer batch
@@ -14,13 +14,15 @@ One rank per GPU (torch.distributed over RCCL when WORLD_SIZE > 1). Each rank ow
 p50 latency: after the timed loop rank 0 issues VideoLatestImage requests through the real gRPC
 server (in-process, loopback) and reports the client-observed request->frame-received median.
 
-Data (default ``--content avc``): real compressed synthetic H.264 camera streams — CAVLC intra
-4x4/16x16 + motion-compensated P pictures with residuals and the in-loop deblocking filter,
-~5.6 Mbit/s at 1080p30 (a textured static scene, moving textured objects and per-frame sensor
-noise) — pre-encoded per camera and replayed. Host: CAVLC macroblock-layer parse +
-dequantisation into per-MB records; GPU: motion compensation, intra wavefront, deblocking
-wavefront, NV12->BGR24, letterbox. ``--content pcm`` replays the I_PCM / P_Skip fast-path
-streams instead (raw samples in an H.264 wrapper; decode = a PCIe copy).
+Data (default ``--content avc --profile high``): real compressed synthetic H.264 camera streams
+of the kind IP cameras send — High profile, CABAC, I/P/B with B pyramids (2 B pictures per
+mini-GOP), 8x8 transform + Intra_8x8 and 4x4 / 16x16 intra, motion-compensated P/B macroblocks
+with residuals and the in-loop deblocking filter (a textured static scene, moving textured
+objects and per-frame sensor noise) — pre-encoded per camera and replayed. Host: CABAC
+macroblock-layer parse + dequantisation into per-MB records; GPU: motion compensation
+(bi-predictive), intra wavefront, deblocking wavefront, NV12->BGR24, letterbox. ``--profile
+baseline`` streams CAVLC I/P instead; ``--content pcm`` replays the I_PCM / P_Skip fast-path
+streams (raw samples in an H.264 wrapper; decode = a PCIe copy).
 """
 from __future__ import annotations
 
@@ -59,9 +61,17 @@ def parse_args():
                     help="h265 = BASELINE config 5 codec (e.g. --width 3840 --height 2160)")
     ap.add_argument("--content", choices=["avc", "pcm"], default="avc",
                     help="avc = compressed CAVLC streams (general decoder); pcm = I_PCM/P_Skip fast path")
-    ap.add_argument("--qp", type=int, default=27, help="encoder QP of the compressed streams")
+    ap.add_argument("--profile", choices=["baseline", "main", "high"], default="high",
+                    help="H.264 profile of the compressed streams: baseline = CAVLC I/P; main = CABAC "
+                         "I/P/B; high = main + 8x8 transform / Intra_8x8 (what IP cameras send)")
+    ap.add_argument("--bframes", type=int, default=2, help="main/high: B pictures per mini-GOP (pyramid)")
+    ap.add_argument("--cavlc", action="store_true", help="main/high: CAVLC instead of CABAC")
+    ap.add_argument("--qp", type=int, default=None,
+                    help="encoder QP of the compressed streams (default: 25 main/high, 27 baseline)")
     ap.add_argument("--noise", type=float, default=8.0, help="static scene texture amplitude")
-    ap.add_argument("--temporal-noise", type=float, default=1.0, help="per-frame sensor noise")
+    ap.add_argument("--temporal-noise", type=float, default=None,
+                    help="per-frame sensor noise (default: 1.5 main/high -> ~3.9 Mbit/s at 1080p30, "
+                         "1.0 baseline -> ~4.5 Mbit/s)")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
     ap.add_argument("--threads", type=int, default=0,
                     help="host parse threads per rank (0 = CPU budget / local ranks - 2, at most 14)")
@@ -83,7 +93,12 @@ def parse_args():
     ap.add_argument("--ring-slots", type=int, default=2)
     ap.add_argument("--latency-samples", type=int, default=100)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (plumbing check, no GPU)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    if a.qp is None:
+        a.qp = 27 if a.profile == "baseline" else 25
+    if a.temporal_noise is None:
+        a.temporal_noise = 1.0 if a.profile == "baseline" else 1.5
+    return a
 
 
 def measure_latency(worker, cams, samples, tick, fps):
@@ -150,6 +165,13 @@ def main():
     if compressed:
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
+        cfg.profile, cfg.bframes, cfg.cabac = a.profile, a.bframes, not a.cavlc
+    if compressed and a.profile == "baseline":
+        stream_desc = "Baseline CAVLC I/P"
+    elif compressed:
+        stream_desc = (f"{a.profile.capitalize()} profile {'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
+                       f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"
+                       f"{', 8x8 transform + Intra_8x8' if a.profile == 'high' else ''}")
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
 
@@ -265,7 +287,7 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "uint8 (BGR24 frames; bf16-capable consumer path)",
-            "data": (f"synthetic compressed {CODEC[a.codec]} camera streams (CAVLC I/P, QP {a.qp}, GOP "
+            "data": (f"synthetic compressed {CODEC[a.codec]} camera streams ({stream_desc}, QP {a.qp}, GOP "
                      f"{a.gop}, {bitrate_mbps:.1f} Mbit/s per camera: textured scene, moving objects, "
                      "sensor noise), pre-encoded per camera and replayed" if compressed else
                      f"synthetic {CODEC[a.codec]} I_PCM/P_Skip fast-path streams (random-noise "
@@ -293,7 +315,8 @@ def main():
                                              "reference clients' pattern): includes waiting for "
                                              "the camera's next decoded frame",
             "rocdecode_available": bool(vep.rocdecode_available()),
-            "decoder_backend": ("native H.264 decoder: CPU CAVLC macroblock-layer parse + dequant; "
+            "decoder_backend": ("native H.264 decoder: CPU " + ("CAVLC" if a.profile == "baseline" or a.cavlc
+                                                               else "CABAC") + " macroblock-layer parse + dequant; "
                                 "gfx950 HIP motion compensation, intra + deblocking wavefronts, "
                                 "NV12->BGR24 (rocDecode absent in image)" if compressed else
                                 "native subset decoder: CPU " + ENTROPY[a.codec] + " parse + gfx950 "

@@ -1,0 +1,69 @@
+// Host-only H.264 parse benchmark: encodes a synthetic 1080p stream with the closed-loop encoder
+// (High: CABAC IBBP + 8x8; baseline: CAVLC I/P), then times avc::Decoder::parse (entropy layer +
+// dequantisation + MB records, no sample reconstruction) over it. Used with gprof
+// (`make parse-prof`) to find the parse hot spots that bound the bench.
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+
+#include "vep/avc.h"
+
+using namespace vep;
+
+
+int main(int argc, char** argv) {
+  const bool high = argc < 2 || std::strcmp(argv[1], "baseline") != 0;
+  const int frames = argc > 2 ? std::atoi(argv[2]) : 30;
+  const int reps = argc > 3 ? std::atoi(argv[3]) : 5;
+  std::vector<std::shared_ptr<AccessUnit>> aus;
+  if (high) {
+    avc::AvcHighConfig c;
+    c.width = 1920;
+    c.height = 1080;
+    c.qp = 25;
+    c.noise = 8.0;
+    c.temporal_noise = 1.5;
+    avc::AvcHighEncoder e(c);
+    for (int i = 0; i < frames; ++i) aus.push_back(e.next());
+  } else {
+    avc::AvcEncConfig c;
+    c.width = 1920;
+    c.height = 1080;
+    c.qp = 27;
+    c.noise = 8.0;
+    c.temporal_noise = 1.0;
+    avc::AvcEncoder e(c);
+    for (int i = 0; i < frames; ++i) aus.push_back(e.next());
+  }
+  size_t bytes = 0;
+  for (auto& a : aus) bytes += a->bytes();
+  const auto t0 = std::chrono::steady_clock::now();
+  size_t mbs = 0;
+  double by_type[3] = {0, 0, 0};  // P, B, I
+  int n_type[3] = {0, 0, 0};
+  u64 kinds[8] = {};
+  for (int r = 0; r < reps; ++r) {
+    avc::Decoder d;
+    for (auto& a : aus) {
+      const auto p0 = std::chrono::steady_clock::now();
+      auto pic = d.parse(*a);
+      const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - p0).count();
+      const int t = pic->info.pict_type == 'P' ? 0 : pic->info.pict_type == 'B' ? 1 : 2;
+      by_type[t] += dt;
+      n_type[t] += 1;
+      mbs += size_t(pic->nmbs());
+      if (r == 0)
+        for (const auto& m : pic->mbs) ++kinds[m.kind & 7];
+    }
+  }
+  const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  for (int t = 0; t < 3; ++t)
+    if (n_type[t])
+      std::printf("  %c: %d pictures, %.3f ms/picture\n", "PBI"[t], n_type[t] / reps, by_type[t] * 1e3 / n_type[t]);
+  std::printf("  MB kinds (skip inter i4 i16 pcm i8): %llu %llu %llu %llu %llu %llu\n", (unsigned long long)kinds[0],
+              (unsigned long long)kinds[1], (unsigned long long)kinds[2], (unsigned long long)kinds[3],
+              (unsigned long long)kinds[4], (unsigned long long)kinds[5]);
+  std::printf("%s: %d frames x %d, %.1f kB/frame, parse %.3f ms/frame (%.1f ns/MB)\n", high ? "high" : "baseline",
+              frames, reps, bytes / 1e3 / frames, s * 1e3 / (frames * reps), s * 1e9 / double(mbs));
+  return 0;
+}

@@ -597,32 +597,35 @@ int Decoder::reorder_depth(const Sps& sps) const {
 // more than reorder_depth() pictures wait. A picture whose POC is below the last output one
 // arrived too late for its turn: it is not output, and (without a VUI reorder depth) the
 // depth learnt from the stream grows.
-void Decoder::bump(Picture& pic, bool flush_all) {
+// Output ("bumping", C.4.5.3): pictures leave in (epoch, POC) order once more than the reorder
+// depth are waiting. An IDR / MMCO5 picture starts a new epoch: the previous pictures still leave
+// first (as no_output_of_prior_pics_flag = 0 requires) but one per decoded picture, like the
+// steady state, so a stream with B pictures outputs one frame per access unit across GOPs
+// instead of a burst at every IDR. `hard` (new picture geometry, or no reordering) outputs every
+// waiting picture at once.
+void Decoder::bump(Picture& pic, bool new_epoch, bool hard) {
+  auto before = [](const Pending& a, const Pending& b) {
+    return a.epoch != b.epoch ? a.epoch < b.epoch : a.f.poc < b.f.poc;
+  };
   auto take_min = [&] {
-    auto it = std::min_element(pending_.begin(), pending_.end(),
-                               [](const Pending& a, const Pending& b) { return a.f.poc < b.f.poc; });
+    auto it = std::min_element(pending_.begin(), pending_.end(), before);
     pic.outputs.push_back(it->f);
     last_out_poc_ = it->f.poc;
-    out_since_idr_ = true;
+    last_out_epoch_ = i64(it->epoch);
     pending_.erase(it);
   };
-  if (flush_all) {
+  if (new_epoch) ++epoch_;
+  if (hard)
     while (!pending_.empty()) take_min();
-    out_since_idr_ = false;
-  }
   OutFrame f;
   f.slot = pic.target;
   f.info = pic.info;
   f.au = pic.au;
   f.poc = pic.poc;
-  if (flush_all) {
-    pic.outputs.push_back(f);
-    last_out_poc_ = f.poc;
-    out_since_idr_ = true;
-  } else if (out_since_idr_ && f.poc < last_out_poc_) {
+  if (last_out_epoch_ == i64(epoch_) && f.poc < last_out_poc_) {
     if (adaptive_reorder_ < 16) ++adaptive_reorder_;  // late: dropped from output
   } else {
-    pending_.push_back({f, 0});
+    pending_.push_back({f, epoch_});
     while (int(pending_.size()) > reorder_cur_) take_min();
   }
   if (!pic.outputs.empty()) pinned_slot_ = pic.outputs.back().slot;
@@ -631,8 +634,9 @@ void Decoder::bump(Picture& pic, bool flush_all) {
 std::vector<OutFrame> Decoder::flush_output() {
   Picture tmp;
   while (!pending_.empty()) {
-    auto it = std::min_element(pending_.begin(), pending_.end(),
-                               [](const Pending& a, const Pending& b) { return a.f.poc < b.f.poc; });
+    auto it = std::min_element(pending_.begin(), pending_.end(), [](const Pending& a, const Pending& b) {
+      return a.epoch != b.epoch ? a.epoch < b.epoch : a.f.poc < b.f.poc;
+    });
     tmp.outputs.push_back(it->f);
     pending_.erase(it);
   }
@@ -1036,6 +1040,7 @@ int dpb_slots_for(const Sps& sps) {
 PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   auto pic = std::make_shared<Picture>();
   bool got = false;
+  bool hard_flush = false;  // IDR with a new picture geometry: waiting pictures leave at once
   int slice_idx = 0;
   SliceHdr first;
   const Sps* act_sps = nullptr;
@@ -1087,6 +1092,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       VEP_CHECK(slots <= kMaxDpbSlots, "max_num_ref_frames out of range");
       const int W = sps.width_mbs, H = sps.height_mbs();
       if (sh.idr()) {
+        hard_flush = slots != dpb_slots_ || W != wmbs_ || H != hmbs_;
         have_idr_ = true;
         dpb_slots_ = slots;
         wmbs_ = W;
@@ -1099,8 +1105,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
         VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_, "SPS changed without an IDR picture");
       }
       if (sh.idr()) {
-        // IDR: the previous pictures leave the reorder buffer first (no_output_of_prior_pics
-        // is not honoured: a viewer wants the newest frame), then the DPB is emptied
+        // IDR: the DPB is emptied; pictures waiting for output stay (they leave before the
+        // IDR's, bump(); no_output_of_prior_pics is not honoured: a viewer wants every frame)
         dpb_.clear();
         max_lt_idx_ = -1;
       }
@@ -1217,7 +1223,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids);
     mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col));
   }
-  bump(*pic, first.idr() || first.has_mmco5());
+  const bool boundary = first.idr() || first.has_mmco5();
+  bump(*pic, boundary, boundary && (hard_flush || reorder_cur_ == 0));
   validate(*pic);
   return pic;
 }

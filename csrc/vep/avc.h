@@ -251,14 +251,14 @@ class Decoder {
  private:
   struct Pending {
     OutFrame f;
-    u32 uid;
+    u32 epoch;  // IDR / MMCO5 period the picture belongs to (output order: epoch, then POC)
   };
   void build_lists(const SliceHdr& sh, const h264::Sps& sps, int cur_poc);
   void mark_references(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid,
                        std::shared_ptr<const ColMotion> col);
   int pick_slot() const;
   int compute_poc(const SliceHdr& sh, const h264::Sps& sps);
-  void bump(Picture& pic, bool flush_all);
+  void bump(Picture& pic, bool new_epoch, bool hard);
   int reorder_depth(const h264::Sps& sps) const;
 
   std::map<int, h264::Sps> sps_;
@@ -275,7 +275,8 @@ class Decoder {
   bool have_idr_ = false;
   int pinned_slot_ = -1;    // newest output: kept until a newer one leaves the reorder buffer
   int last_out_poc_ = 0;
-  bool out_since_idr_ = false;
+  i64 last_out_epoch_ = -1;
+  u32 epoch_ = 0;
   int adaptive_reorder_ = 0;  // reorder depth learnt from the stream when the SPS gives none
   int reorder_cur_ = 0;       // reorder depth in force for the active SPS
   u32 next_uid_ = 1;
