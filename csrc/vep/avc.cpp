@@ -187,6 +187,27 @@ void MbNeighbours::mb_neighbour_refs(int mb, int list, int ref[3]) const {
   ref[2] = C.ref;
 }
 
+void MbNeighbours::direct_spatial_pred(int mb, int list, int& ref, int mv[2]) const {
+  Nb A = motion_at(mb, -1, 0, 0, list), B = motion_at(mb, 0, -1, 0, list);
+  Nb C = motion_at(mb, 16, -1, 0, list);
+  if (!C.avail) C = motion_at(mb, -1, -1, 0, list);
+  auto minpos = [](int a, int b) { return (a >= 0 && b >= 0) ? std::min(a, b) : std::max(a, b); };
+  ref = minpos(A.ref, minpos(B.ref, C.ref));
+  mv[0] = mv[1] = 0;
+  if (ref < 0) return;
+  // the 16x16 predictor of pred_mv() for `ref` from the same A, B, C
+  if (!B.avail && !C.avail && A.avail) B = C = A;
+  const int match = (A.ref == ref) + (B.ref == ref) + (C.ref == ref);
+  if (match == 1) {
+    const Nb& n = A.ref == ref ? A : B.ref == ref ? B : C;
+    mv[0] = n.mv[0];
+    mv[1] = n.mv[1];
+    return;
+  }
+  mv[0] = median3(A.mv[0], B.mv[0], C.mv[0]);
+  mv[1] = median3(A.mv[1], B.mv[1], C.mv[1]);
+}
+
 // ------------------------------------------------------------------------- parameter sets
 
 namespace {
@@ -1220,7 +1241,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   if (first.nal_ref_idc != 0) {
     std::shared_ptr<ColMotion> col;
     if (act_sps->profile_idc != 66)  // B slices possible: keep the motion for direct prediction
-      col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids);
+      col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids, act_sps->direct_8x8);
     mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col));
   }
   const bool boundary = first.idr() || first.has_mmco5();
@@ -1273,28 +1294,34 @@ void validate(const Picture& p) {
 // ------------------------------------------------------------------------- shared internals
 
 std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, int hmbs,
-                                            const std::vector<std::array<std::vector<u32>, 2>>& slice_uids) {
+                                            const std::vector<std::array<std::vector<u32>, 2>>& slice_uids,
+                                            bool corners) {
   auto col = std::make_shared<ColMotion>();
   col->wmbs = wmbs;
   col->hmbs = hmbs;
-  const size_t n = size_t(wmbs) * hmbs * 16;
-  col->mv.assign(n * 2, 0);
-  col->ref.assign(n, i8(-1));
-  col->pid.assign(n, 0u);
+  col->corners = corners;
+  const int per = corners ? 4 : 16;
+  col->b.resize(size_t(wmbs) * hmbs * size_t(per));
+  static constexpr u8 kCorner[4] = {0, 3, 12, 15};  // outer corner 4x4 block of each 8x8
   for (int mb = 0; mb < wmbs * hmbs; ++mb) {
     const MbState& st = nb.at(mb);
-    if (st.kind == 0xFF || is_intra(st.kind) || slice_uids.empty()) continue;
+    ColMotion::Blk* out = &col->b[size_t(mb) * size_t(per)];
+    if (st.kind == 0xFF || is_intra(st.kind) || slice_uids.empty()) {
+      for (int k = 0; k < per; ++k) out[k] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
+      continue;
+    }
     const auto& lu = slice_uids[std::min<size_t>(st.slice, slice_uids.size() - 1)];
-    for (int blk = 0; blk < 16; ++blk) {
+    for (int k = 0; k < per; ++k) {
+      const int blk = corners ? kCorner[k] : k;
       const int b8 = ((blk >> 3) << 1) | ((blk & 3) >> 1);
       const int l = st.ref[0][b8] >= 0 ? 0 : 1;
       const int ri = st.ref[l][b8];
-      if (ri < 0) continue;
-      const size_t k = size_t(mb) * 16 + size_t(blk);
-      col->mv[k * 2] = st.mv[l][blk][0];
-      col->mv[k * 2 + 1] = st.mv[l][blk][1];
-      col->ref[k] = i8(ri);
-      col->pid[k] = size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u;
+      if (ri < 0) {
+        out[k] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
+        continue;
+      }
+      out[k] = ColMotion::Blk{{st.mv[l][blk][0], st.mv[l][blk][1]},
+                              size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u, i8(ri)};
     }
   }
   return col;

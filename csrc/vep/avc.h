@@ -180,6 +180,9 @@ class MbNeighbours {
   // Neighbour A/B/C(D) motion of the whole MB for list `list` (direct spatial prediction):
   // ref[k] = refIdx (-1 unavailable / intra / list unused).
   void mb_neighbour_refs(int mb, int list, int ref[3]) const;
+  // Spatial direct (§8.4.1.2.2) for list `list`: refIdx = MinPositive over A, B, C and the
+  // 16x16 motion-vector predictor for it (mv = 0 when ref < 0), from one neighbour fetch.
+  void direct_spatial_pred(int mb, int list, int& ref, int mv[2]) const;
   // Swap the state array out (kept as the colocated picture's motion) and start a fresh one.
   std::vector<MbState> take_state() {
     std::vector<MbState> v;
@@ -201,12 +204,22 @@ class MbNeighbours {
 
 // Motion of a reference picture as the colocated picture of direct prediction (§8.4.1.2.1):
 // per 4x4 block the vector and reference index of list 0 if the block used it, else of list 1,
-// and the identity of the referenced picture.
+// and the identity of the referenced picture. With direct_8x8_inference (every stream this
+// decoder accepts that has B slices sets it in practice) only the outer corner block of each 8x8
+// is ever read, so only those four blocks per MB are kept.
 struct ColMotion {
+  struct Blk {
+    i16 mv[2];
+    u32 pid;  // uid of the picture the block references
+    i8 ref;   // refIdxCol (-1: intra / not available)
+  };
   int wmbs = 0, hmbs = 0;
-  std::vector<i16> mv;   // 2 per 4x4 block (raster blocks of raster MBs: mb * 16 + blk)
-  std::vector<i8> ref;   // refIdxCol (-1: intra)
-  std::vector<u32> pid;  // Picture uid the block references
+  bool corners = false;  // 4 entries per MB (8x8 outer corners), else 16 (raster 4x4 blocks)
+  std::vector<Blk> b;
+  // entry of raster 4x4 block `blk` of MB `mb` (corners: the block's 8x8)
+  size_t index(int mb, int blk) const {
+    return corners ? size_t(mb) * 4 + size_t(((blk >> 3) << 1) | ((blk & 3) >> 1)) : size_t(mb) * 16 + size_t(blk);
+  }
 };
 
 // Reference picture (DPB entry).

@@ -43,6 +43,7 @@ void cabac_init_contexts(cabac::Ctx* ctx, int model, int qp);
 
 // Decoder adapter: bins are read; the value arguments are ignored.
 struct BinDecoder {
+  static constexpr bool kWrite = false;
   cabac::Decoder& d;
   cabac::Ctx* ctx;
   u32 bin(int i, u32) { return d.decision(ctx[i]); }
@@ -52,6 +53,7 @@ struct BinDecoder {
 
 // Encoder adapter: the value arguments are written and returned.
 struct BinEncoder {
+  static constexpr bool kWrite = true;
   cabac::Encoder& e;
   cabac::Ctx* ctx;
   u32 bin(int i, u32 v) {
@@ -202,38 +204,43 @@ struct AvcBins {
   u32 cbp_luma_bin(int inc, bool v) { return bin(73 + inc, v); }
   u32 cbp_chroma_bin(int inc, bool v) { return bin(77 + inc, v); }
 
-  // residual_block_cabac (§7.3.5.3.3): coef[0 .. n-1] levels in scan order (read: must be zeroed
-  // by the caller; write: the levels to code). cbf_inc < 0: coded_block_flag not coded (8x8
-  // luma blocks of 4:2:0). Returns the number of non-zero levels.
-  int residual(int cat, int cbf_inc, int n, int* coef) {
-    if (cbf_inc >= 0) {
-      bool any = false;
-      for (int i = 0; i < n && !any; ++i) any = coef[i] != 0;
-      if (!bin(85 + kCbfCatOff[cat] + cbf_inc, any)) return 0;
-    }
+  // residual_block_cabac (§7.3.5.3.3): coef[0 .. n-1] levels in scan order. Read: only the
+  // non-zero entries are written (the caller need not clear `coef`); write: the levels to code.
+  // `nzpos` receives the scan positions of the non-zero levels (ascending). cbf_inc < 0:
+  // coded_block_flag not coded (8x8 luma blocks of 4:2:0). Returns the number of non-zero levels.
+  int residual(int cat, int cbf_inc, int n, int* coef, u8* nzpos) {
     int last_nz = -1;
-    for (int i = 0; i < n; ++i)
-      if (coef[i]) last_nz = i;
+    if constexpr (E::kWrite)
+      for (int i = 0; i < n; ++i)
+        if (coef[i]) last_nz = i;
+    if (cbf_inc >= 0 && !bin(85 + kCbfCatOff[cat] + cbf_inc, last_nz >= 0)) return 0;
     const bool b8 = cat == kCatLuma8x8;
-    const int sig_base = b8 ? 402 : 105 + kSigCatOff[cat];
-    const int last_base = b8 ? 417 : 166 + kSigCatOff[cat];
-    int pos[64];
     int num = 0, i = 0;
-    for (; i < n - 1; ++i) {
-      const int si = b8 ? kSig8x8Frame[i] : (cat == kCatChromaDc ? (i < 2 ? i : 2) : i);
-      if (bin(sig_base + si, coef[i] != 0)) {
-        pos[num++] = i;
-        const int li = b8 ? kLast8x8[i] : si;
-        if (bin(last_base + li, i == last_nz)) break;
+    if (b8) {
+      for (; i < 63; ++i) {
+        if (bin(402 + kSig8x8Frame[i], E::kWrite && coef[i] != 0)) {
+          nzpos[num++] = u8(i);
+          if (bin(417 + kLast8x8[i], i == last_nz)) break;
+        }
+      }
+    } else {
+      const int sig_base = 105 + kSigCatOff[cat], last_base = 166 + kSigCatOff[cat];
+      const bool cdc = cat == kCatChromaDc;
+      for (; i < n - 1; ++i) {
+        const int si = cdc ? (i < 2 ? i : 2) : i;
+        if (bin(sig_base + si, E::kWrite && coef[i] != 0)) {
+          nzpos[num++] = u8(i);
+          if (bin(last_base + si, i == last_nz)) break;
+        }
       }
     }
-    if (i == n - 1) pos[num++] = n - 1;
+    if (i == n - 1) nzpos[num++] = u8(n - 1);
     const int abs_base = b8 ? 426 : 227 + kAbsCatOff[cat];
     const int gt1_max = cat == kCatChromaDc ? 3 : 4;
     int gt1 = 0, eq1 = 0;
     for (int k = num - 1; k >= 0; --k) {
-      const int p = pos[k];
-      const int c = coef[p];
+      const int p = nzpos[k];
+      const int c = E::kWrite ? coef[p] : 0;
       const int a = (c < 0 ? -c : c) - 1;
       int v = 0;
       if (bin(abs_base + (gt1 != 0 ? 0 : (eq1 + 1 < 4 ? eq1 + 1 : 4)), a > 0)) {

@@ -784,7 +784,7 @@ struct AvcHighEncoder::Impl {
     }
     if (pic.deblock) cpu_deblock(pic, T());
     if (job.ref) {
-      Ref r{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids)};
+      Ref r{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)};
       if (int(dpb.size()) >= sps.max_num_ref_frames) {  // sliding window (§8.2.5.3)
         auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
           auto wrap = [&](const Ref& x) { return x.frame_num > sh.frame_num ? x.frame_num - max_fn : x.frame_num; };

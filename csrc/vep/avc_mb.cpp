@@ -638,51 +638,41 @@ class MbLayer {
               "direct prediction without a list-1 reference");
     const ListEntry& c1 = (*env_.list[1])[0];
     const ColMotion* col = c1.col;
-    VEP_CHECK(col && col->wmbs == nb_.wmbs() && col->hmbs == nb_.hmbs(), "colocated picture motion missing");
+    VEP_CHECK(col && col->wmbs == nb_.wmbs() && col->hmbs == nb_.hmbs() && col->corners == sps_.direct_8x8,
+              "colocated picture motion missing");
+    // direct_8x8_inference: every 4x4 block of an 8x8 takes the motion derived from the 8x8's
+    // outer corner block of the colocated MB, i.e. one derivation per 8x8
     const bool infer = sps_.direct_8x8;
-    auto col_blk = [&](int blk) {  // colocated 4x4 block of raster block blk
-      if (infer) {
-        const int b8 = raster_b8(blk);
-        blk = (b8 & 1 ? 3 : 0) + (b8 & 2 ? 12 : 0);  // the 8x8's outer corner
+    auto fill = [&](int l, int b8, int blk, int mx, int my) {
+      if (!infer) {
+        s.mv[l][blk][0] = i16(mx);
+        s.mv[l][blk][1] = i16(my);
+        return;
       }
-      return size_t(mb) * 16 + size_t(blk);
+      for (u16 w = b8_blocks(b8); w; w &= w - 1) {
+        const int k = __builtin_ctz(w);
+        s.mv[l][k][0] = i16(mx);
+        s.mv[l][k][1] = i16(my);
+      }
     };
     if (sh_.direct_spatial) {
-      int ref[2];
-      for (int l = 0; l < 2; ++l) {
-        int n[3];
-        nb_.mb_neighbour_refs(mb, l, n);
-        auto minpos = [](int a, int b2) { return (a >= 0 && b2 >= 0) ? std::min(a, b2) : std::max(a, b2); };
-        ref[l] = minpos(n[0], minpos(n[1], n[2]));
-      }
+      int ref[2], mvp[2][2];
+      for (int l = 0; l < 2; ++l) nb_.direct_spatial_pred(mb, l, ref[l], mvp[l]);
       const bool zero = ref[0] < 0 && ref[1] < 0;
       if (zero) ref[0] = ref[1] = 0;
-      int mvp[2][2] = {{0, 0}, {0, 0}};
-      for (int l = 0; l < 2; ++l) {
-        if (ref[l] < 0 || zero) continue;
-        need_ref(l, ref[l]);
-        nb_.pred_mv(mb, 0, 0, 4, 4, l, ref[l], 0, 0, mvp[l]);
-      }
-      if (zero) {
-        need_ref(0, 0);
-        need_ref(1, 0);
-      }
+      for (int l = 0; l < 2; ++l)
+        if (ref[l] >= 0) need_ref(l, ref[l]);
       for (int b8 = 0; b8 < 4; ++b8) {
         if (!((mask >> b8) & 1)) continue;
         for (int l = 0; l < 2; ++l) s.ref[l][b8] = i8(ref[l]);
-        for (u16 w = b8_blocks(b8); w; w &= w - 1) {
+        for (u16 w = infer ? u16(1u << ((b8 & 1) * 2 + (b8 >> 1) * 8)) : b8_blocks(b8); w; w &= w - 1) {
           const int blk = __builtin_ctz(w);
-          const size_t cb = col_blk(blk);
-          const bool col_zero = !c1.long_term && col->ref[cb] == 0 && col->mv[cb * 2] >= -1 &&
-                                col->mv[cb * 2] <= 1 && col->mv[cb * 2 + 1] >= -1 && col->mv[cb * 2 + 1] <= 1;
+          const ColMotion::Blk& cb = col->b[col->index(mb, blk)];
+          const bool col_zero = !c1.long_term && cb.ref == 0 && cb.mv[0] >= -1 && cb.mv[0] <= 1 && cb.mv[1] >= -1 &&
+                                cb.mv[1] <= 1;
           for (int l = 0; l < 2; ++l) {
-            int mx = 0, my = 0;
-            if (ref[l] >= 0 && !zero && !(ref[l] == 0 && col_zero)) {
-              mx = mvp[l][0];
-              my = mvp[l][1];
-            }
-            s.mv[l][blk][0] = i16(ref[l] >= 0 ? mx : 0);
-            s.mv[l][blk][1] = i16(ref[l] >= 0 ? my : 0);
+            const bool use = ref[l] >= 0 && !zero && !(ref[l] == 0 && col_zero);
+            fill(l, b8, blk, use ? mvp[l][0] : 0, use ? mvp[l][1] : 0);
           }
         }
       }
@@ -693,18 +683,17 @@ class MbLayer {
     for (int b8 = 0; b8 < 4; ++b8) {
       if (!((mask >> b8) & 1)) continue;
       int r0 = 0;
-      for (u16 w = b8_blocks(b8); w; w &= w - 1) {
+      for (u16 w = infer ? u16(1u << ((b8 & 1) * 2 + (b8 >> 1) * 8)) : b8_blocks(b8); w; w &= w - 1) {
         const int blk = __builtin_ctz(w);
-        const size_t cb = col_blk(blk);
+        const ColMotion::Blk& cb = col->b[col->index(mb, blk)];
         int mvc[2] = {0, 0};
         r0 = 0;
-        if (col->ref[cb] >= 0) {
-          mvc[0] = col->mv[cb * 2];
-          mvc[1] = col->mv[cb * 2 + 1];
-          const u32 pid = col->pid[cb];
+        if (cb.ref >= 0) {
+          mvc[0] = cb.mv[0];
+          mvc[1] = cb.mv[1];
           r0 = -1;
           for (size_t k = 0; k < l0.size() && r0 < 0; ++k)
-            if (l0[k].slot >= 0 && l0[k].uid == pid) r0 = int(k);
+            if (l0[k].slot >= 0 && l0[k].uid == cb.pid) r0 = int(k);
           if (r0 < 0) r0 = 0;  // the colocated reference is gone (non-conforming): conceal
         }
         need_ref(0, r0);
@@ -724,10 +713,8 @@ class MbLayer {
             m1[k] = m0[k] - mvc[k];
           }
         }
-        s.mv[0][blk][0] = i16(clip3i(-32768, 32767, m0[0]));
-        s.mv[0][blk][1] = i16(clip3i(-32768, 32767, m0[1]));
-        s.mv[1][blk][0] = i16(clip3i(-32768, 32767, m1[0]));
-        s.mv[1][blk][1] = i16(clip3i(-32768, 32767, m1[1]));
+        fill(0, b8, blk, clip3i(-32768, 32767, m0[0]), clip3i(-32768, 32767, m0[1]));
+        fill(1, b8, blk, clip3i(-32768, 32767, m1[0]), clip3i(-32768, 32767, m1[1]));
       }
       s.ref[0][b8] = i8(r0);
       s.ref[1][b8] = 0;
@@ -780,20 +767,31 @@ class MbLayer {
     return a + 2 * bb;
   }
 
-  // One residual block's levels (scan order) into lv[0..n-1] (write mode: the levels of `src`
-  // are coded); returns TotalCoeff.
-  int read_block(int cat, int cbf_inc, int nc, int n, int* lv, const int* src) {
+  // One residual block: its non-zero levels lv[nzpos[j]] (scan order positions, j < the
+  // returned TotalCoeff; other entries of lv are unspecified when reading). Write mode: the
+  // levels of `src` are coded.
+  int read_block(int cat, int cbf_inc, int nc, int n, int* lv, u8* nzpos, const int* src) {
     if constexpr (kWrite) std::memcpy(lv, src, size_t(n) * sizeof(int));
-    else std::memset(lv, 0, size_t(n) * sizeof(int));
     (void)src;
     if constexpr (kCabac) {
       (void)nc;
-      return bins->residual(cat, cbf_inc, n, lv);
+      return bins->residual(cat, cbf_inc, n, lv, nzpos);
     } else {
       (void)cat;
       (void)cbf_inc;
-      if constexpr (kWrite) return write_residual_block(*bw, nc, n, lv);
-      else return read_residual_block_cb(*br, nc, n, [lv](int k, int l) { lv[k] = l; });
+      int t = 0;
+      if constexpr (kWrite) {
+        for (int k = 0; k < n; ++k)
+          if (lv[k]) nzpos[t++] = u8(k);
+        write_residual_block(*bw, nc, n, lv);
+        return t;
+      } else {
+        read_residual_block_cb(*br, nc, n, [&](int k, int l) {
+          lv[k] = l;
+          nzpos[t++] = u8(k);
+        });
+        return t;
+      }
     }
   }
 
@@ -801,14 +799,16 @@ class MbLayer {
     const int ly = intra ? 0 : 3;
     const int q6 = qp / 6, qm = qp % 6;
     int lv[64];
+    u8 nzp[64];
     if (s.kind == kI16x16) {
       const int inc = kCabac ? cbf_dc_inc(mb, 0, true) : 0;
       const int nc = kCabac ? 0 : nb_.nc_luma(mb, 0);
       int dcy[16] = {};
-      if (read_block(kCatLumaDc, inc, nc, 16, lv, kWrite ? want->dc : nullptr) > 0) {
+      const int tdc = read_block(kCatLumaDc, inc, nc, 16, lv, nzp, kWrite ? want->dc : nullptr);
+      if (tdc > 0) {
         s.cbf_dc |= 1;
-        int c[16];
-        for (int k = 0; k < 16; ++k) c[kZigzag4x4[k]] = lv[k];
+        int c[16] = {};
+        for (int j = 0; j < tdc; ++j) c[kZigzag4x4[nzp[j]]] = lv[nzp[j]];
         hadamard4x4(c);
         const int ls = dq_.ls4[ly][qm][0];
         for (int k = 0; k < 16; ++k)
@@ -818,15 +818,14 @@ class MbLayer {
         const int r = blk_to_raster(idx);
         i16* d = res.blk[r];
         bool nz = dcy[r] != 0;
-        int tc = 0;
         std::memset(d, 0, 16 * sizeof(i16));
         d[0] = sat16(dcy[r]);
         if (cbp_luma) {
           const int binc = kCabac ? cbf_luma_inc(mb, r, true) : 0;
           const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
-          tc = read_block(kCatLumaAc, binc, bnc, 15, lv, kWrite ? want->ac[r] : nullptr);
-          for (int k = 0; k < 15; ++k) {
-            if (!lv[k]) continue;
+          const int tc = read_block(kCatLumaAc, binc, bnc, 15, lv, nzp, kWrite ? want->ac[r] : nullptr);
+          for (int j = 0; j < tc; ++j) {
+            const int k = nzp[j];
             const int pos = kZigzag4x4[k + 1];
             const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
             d[pos] = sat16(v);
@@ -842,32 +841,31 @@ class MbLayer {
       const int l8 = intra ? 0 : 1;
       for (int b8 = 0; b8 < 4; ++b8) {
         if (!((cbp_luma >> b8) & 1)) continue;
-        int c64[64] = {};
+        i16* d = res.b8[b8];
+        std::memset(d, 0, 64 * sizeof(i16));
+        bool nz = false;
         int total = 0;
+        auto put = [&](int k, int level) {  // k: 8x8 scan position
+          const int pos = kZigzag8x8[k];
+          const int v = scale8(level, dq_.ls8[l8][qm][pos], qp);
+          d[pos] = sat16(v);
+          nz |= v != 0;
+        };
         if constexpr (kCabac) {
-          total = read_block(kCatLuma8x8, -1, 0, 64, c64, kWrite ? want->l8[b8] : nullptr);
+          total = read_block(kCatLuma8x8, -1, 0, 64, lv, nzp, kWrite ? want->l8[b8] : nullptr);
+          for (int j = 0; j < total; ++j) put(nzp[j], lv[nzp[j]]);
           for (u16 w = b8_blocks(b8); w; w &= w - 1) s.tc[__builtin_ctz(w)] = u8(std::min(total, 16));
         } else {
-          for (int i4 = 0; i4 < 4; ++i4) {
+          for (int i4 = 0; i4 < 4; ++i4) {  // CAVLC: four interleaved 4x4 scans
             const int r = blk_to_raster(b8 * 4 + i4);
             int part[16] = {};
             if constexpr (kWrite)
               for (int k = 0; k < 16; ++k) part[k] = want->l8[b8][4 * k + i4];
-            const int tc = read_block(kCatLuma4x4, 0, nb_.nc_luma(mb, r), 16, lv, part);
+            const int tc = read_block(kCatLuma4x4, 0, nb_.nc_luma(mb, r), 16, lv, nzp, part);
             s.tc[r] = u8(tc);
             total += tc;
-            for (int k = 0; k < 16; ++k) c64[4 * k + i4] = lv[k];
+            for (int j = 0; j < tc; ++j) put(4 * nzp[j] + i4, lv[nzp[j]]);
           }
-        }
-        i16* d = res.b8[b8];
-        std::memset(d, 0, 64 * sizeof(i16));
-        bool nz = false;
-        for (int k = 0; k < 64; ++k) {
-          if (!c64[k]) continue;
-          const int pos = kZigzag8x8[k];
-          const int v = scale8(c64[k], dq_.ls8[l8][qm][pos], qp);
-          d[pos] = sat16(v);
-          nz |= v != 0;
         }
         if (total) {
           s.cbf |= b8_blocks(b8);
@@ -881,15 +879,15 @@ class MbLayer {
         if (!((cbp_luma >> (idx >> 2)) & 1)) continue;
         const int binc = kCabac ? cbf_luma_inc(mb, r, intra) : 0;
         const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
-        const int tc = read_block(kCatLuma4x4, binc, bnc, 16, lv, kWrite ? want->ac[r] : nullptr);
+        const int tc = read_block(kCatLuma4x4, binc, bnc, 16, lv, nzp, kWrite ? want->ac[r] : nullptr);
         s.tc[r] = u8(tc);
-        if (tc) s.cbf |= u16(1u << r);
         if (!tc) continue;
+        s.cbf |= u16(1u << r);
         i16* d = res.blk[r];
         std::memset(d, 0, 16 * sizeof(i16));
         bool nz = false;
-        for (int k = 0; k < 16; ++k) {
-          if (!lv[k]) continue;
+        for (int j = 0; j < tc; ++j) {
+          const int k = nzp[j];
           const int pos = kZigzag4x4[k];
           const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
           d[pos] = sat16(v);
@@ -905,10 +903,13 @@ class MbLayer {
       for (int c = 0; c < 2; ++c) {
         const int inc = kCabac ? cbf_dc_inc(mb, 1 + c, intra) : 0;
         int v4[4];
-        if (read_block(kCatChromaDc, inc, -1, 4, v4, kWrite ? want->cdc[c] : nullptr) > 0) {
+        const int t = read_block(kCatChromaDc, inc, -1, 4, v4, nzp, kWrite ? want->cdc[c] : nullptr);
+        if (t > 0) {
           s.cbf_dc |= u8(2 << c);
-          const int f[4] = {v4[0] + v4[1] + v4[2] + v4[3], v4[0] - v4[1] + v4[2] - v4[3],
-                            v4[0] + v4[1] - v4[2] - v4[3], v4[0] - v4[1] - v4[2] + v4[3]};
+          int u[4] = {0, 0, 0, 0};
+          for (int j = 0; j < t; ++j) u[nzp[j]] = v4[nzp[j]];
+          const int f[4] = {u[0] + u[1] + u[2] + u[3], u[0] - u[1] + u[2] - u[3], u[0] + u[1] - u[2] - u[3],
+                            u[0] - u[1] - u[2] + u[3]};
           const int ls = dq_.ls4[ly + 1 + c][qpc[c] % 6][0];
           for (int b = 0; b < 4; ++b) dcv[c][b] = ((f[b] * ls) * (1 << (qpc[c] / 6))) >> 5;
         }
@@ -923,11 +924,11 @@ class MbLayer {
           if (cbp_chroma & 2) {
             const int binc = kCabac ? cbf_cac_inc(mb, c, b, intra) : 0;
             const int bnc = kCabac ? 0 : nb_.nc_chroma(mb, c, b);
-            const int tc = read_block(kCatChromaAc, binc, bnc, 15, lv, kWrite ? want->cac[c][b] : nullptr);
+            const int tc = read_block(kCatChromaAc, binc, bnc, 15, lv, nzp, kWrite ? want->cac[c][b] : nullptr);
             s.tcc[c][b] = u8(tc);
             if (tc) s.cbf_cac[c] |= u8(1u << b);
-            for (int k = 0; k < 15; ++k) {
-              if (!lv[k]) continue;
+            for (int j = 0; j < tc; ++j) {
+              const int k = nzp[j];
               const int pos = kZigzag4x4[k + 1];
               const int v = scale4(lv[k], dq_.ls4[lc][qpc[c] % 6][pos], qpc[c]);
               d[pos] = sat16(v);
