@@ -21,37 +21,6 @@ void MbNeighbours::reset(int wmbs, int hmbs) {
   st_.assign(size_t(wmbs) * hmbs, MbState{});
 }
 
-void MbNeighbours::begin(int mb) {
-  cur_ = mb;
-  const int mx = mb % w_, my = mb / w_;
-  auto nb = [&](int nx, int ny) {
-    if (nx < 0 || nx >= w_ || ny < 0) return -1;
-    const int n = ny * w_ + nx;
-    return mb_available(mb, n) ? n : -1;
-  };
-  a_ = nb(mx - 1, my);
-  b_ = nb(mx, my - 1);
-  c_ = nb(mx + 1, my - 1);
-  d_ = nb(mx - 1, my - 1);
-}
-
-int MbNeighbours::mb_at(int mb, int x, int y) const {
-  if (y >= 16) return -1;
-  if (mb != cur_) {  // slow path (not the MB announced by begin())
-    const int dx = x < 0 ? -1 : (x >= 16 ? 1 : 0);
-    const int dy = y < 0 ? -1 : 0;
-    if (dx == 0 && dy == 0) return mb;
-    if (dx > 0 && dy == 0) return -1;
-    const int nx = mb % w_ + dx, ny = mb / w_ + dy;
-    if (nx < 0 || nx >= w_ || ny < 0) return -1;
-    const int n = ny * w_ + nx;
-    return mb_available(mb, n) ? n : -1;
-  }
-  if (y < 0) return x < 0 ? d_ : (x < 16 ? b_ : c_);
-  if (x < 0) return a_;
-  return x < 16 ? mb : -1;  // right neighbour: later in decoding order
-}
-
 static int coded_count(const MbState& s, int blk) {
   if (s.kind == kSkip) return 0;
   if (s.kind == kIPcm) return 16;
@@ -123,22 +92,6 @@ int MbNeighbours::pred_intra8x8(int mb, int b8, bool constrained) const {
   const int b8a = ((ra >> 3) << 1) | ((ra & 3) >> 1), b8b = ((rb >> 3) << 1) | ((rb & 3) >> 1);
   const int ma = mode(a, ra, b8a), mbm = mode(b, rb, b8b);
   return ma < mbm ? ma : mbm;
-}
-
-MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done, int list) const {
-  Nb r{false, -1, {0, 0}};
-  const int m = mb_at(mb, x, y);
-  if (m < 0) return r;
-  const int blk = ((y & 15) >> 2) * 4 + ((x & 15) >> 2);
-  if (m == mb && !((done >> blk) & 1)) return r;  // partition not yet decoded
-  r.avail = true;
-  const MbState& s = st_[size_t(m)];
-  if (is_intra(s.kind)) return r;
-  r.ref = s.ref[list][((blk >> 3) << 1) | ((blk & 3) >> 1)];
-  if (r.ref < 0) return r;  // list unused: refIdx -1, mv 0
-  r.mv[0] = s.mv[list][blk][0];
-  r.mv[1] = s.mv[list][blk][1];
-  return r;
 }
 
 static int median3(int a, int b, int c) { return a + b + c - std::min({a, b, c}) - std::max({a, b, c}); }

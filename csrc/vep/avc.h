@@ -198,9 +198,73 @@ class MbNeighbours {
   };
   Nb motion_at(int mb, int x, int y, u16 done, int list) const;  // x, y in luma samples rel. to mb
   int w_ = 0, h_ = 0;
-  int cur_ = -1, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
+  int cur_ = -1, cx_ = 0, cy_ = 0, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
   std::vector<MbState> st_;
 };
+
+// Hot neighbour derivations, inline (called several times per macroblock).
+inline void MbNeighbours::begin(int mb) {
+  int mx, my;
+  if (mb == cur_) {
+    mx = cx_;
+    my = cy_;
+  } else if (mb == cur_ + 1 && cur_ >= 0) {  // raster order: no division
+    mx = cx_ + 1;
+    my = cy_;
+    if (mx == w_) {
+      mx = 0;
+      ++my;
+    }
+  } else {
+    mx = mb % w_;
+    my = mb / w_;
+  }
+  cur_ = mb;
+  cx_ = mx;
+  cy_ = my;
+  auto nb = [&](int nx, int ny) {
+    if (nx < 0 || nx >= w_ || ny < 0) return -1;
+    const int n = ny * w_ + nx;
+    return mb_available(mb, n) ? n : -1;
+  };
+  a_ = nb(mx - 1, my);
+  b_ = nb(mx, my - 1);
+  c_ = nb(mx + 1, my - 1);
+  d_ = nb(mx - 1, my - 1);
+}
+
+inline int MbNeighbours::mb_at(int mb, int x, int y) const {
+  if (y >= 16) return -1;
+  if (mb != cur_) {  // slow path (not the MB announced by begin())
+    const int dx = x < 0 ? -1 : (x >= 16 ? 1 : 0);
+    const int dy = y < 0 ? -1 : 0;
+    if (dx == 0 && dy == 0) return mb;
+    if (dx > 0 && dy == 0) return -1;
+    const int nx = mb % w_ + dx, ny = mb / w_ + dy;
+    if (nx < 0 || nx >= w_ || ny < 0) return -1;
+    const int n = ny * w_ + nx;
+    return mb_available(mb, n) ? n : -1;
+  }
+  if (y < 0) return x < 0 ? d_ : (x < 16 ? b_ : c_);
+  if (x < 0) return a_;
+  return x < 16 ? mb : -1;  // right neighbour: later in decoding order
+}
+
+inline MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done, int list) const {
+  Nb r{false, -1, {0, 0}};
+  const int m = mb_at(mb, x, y);
+  if (m < 0) return r;
+  const int blk = ((y & 15) >> 2) * 4 + ((x & 15) >> 2);
+  if (m == mb && !((done >> blk) & 1)) return r;  // partition not yet decoded
+  r.avail = true;
+  const MbState& s = st_[size_t(m)];
+  if (is_intra(s.kind)) return r;
+  r.ref = s.ref[list][((blk >> 3) << 1) | ((blk & 3) >> 1)];
+  if (r.ref < 0) return r;  // list unused: refIdx -1, mv 0
+  r.mv[0] = s.mv[list][blk][0];
+  r.mv[1] = s.mv[list][blk][1];
+  return r;
+}
 
 // Motion of a reference picture as the colocated picture of direct prediction (§8.4.1.2.1):
 // per 4x4 block the vector and reference index of list 0 if the block used it, else of list 1,
