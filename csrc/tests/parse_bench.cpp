@@ -46,6 +46,21 @@ int main(int argc, char** argv) {
     best = std::min(best, std::chrono::duration<double>(std::chrono::steady_clock::now() - b0).count());
   }
   std::printf("best of 3 passes: %.3f ms/frame\n", best * 1e3 / frames);
+  // several cameras interleaved on one thread (cold decoder state between pictures, as in the
+  // bench's parse pool)
+  const int ncam = argc > 4 ? std::atoi(argv[4]) : 0;
+  if (ncam > 0) {
+    double bestm = 1e30;
+    for (int round = 0; round < 3; ++round) {
+      std::vector<avc::Decoder> decs(static_cast<size_t>(ncam));
+      std::vector<avc::PicturePtr> keep(static_cast<size_t>(ncam) * 3);
+      const auto b0 = std::chrono::steady_clock::now();
+      for (auto& a : aus)
+        for (int c = 0; c < ncam; ++c) keep[size_t(c) * 3 + size_t(&a - &aus[0]) % 3] = decs[size_t(c)].parse(*a);
+      bestm = std::min(bestm, std::chrono::duration<double>(std::chrono::steady_clock::now() - b0).count());
+    }
+    std::printf("%d cameras interleaved: %.3f ms/frame\n", ncam, bestm * 1e3 / (frames * ncam));
+  }
   const auto t0 = std::chrono::steady_clock::now();
   size_t mbs = 0;
   double by_type[3] = {0, 0, 0};  // P, B, I

@@ -18,7 +18,15 @@ using h264::Sps;
 void MbNeighbours::reset(int wmbs, int hmbs) {
   w_ = wmbs;
   h_ = hmbs;
-  st_.assign(size_t(wmbs) * hmbs, MbState{});
+  cur_ = -1;
+  const size_t n = size_t(wmbs) * hmbs;
+  if (st_.size() != n) {
+    st_.assign(n, MbState{});
+    return;
+  }
+  // Only `kind` marks "not decoded in this picture": every other field is rewritten when the MB
+  // is decoded (MbState{} first), so one byte per MB is enough (a 1080p state array is 2 MB).
+  for (MbState& st : st_) st.kind = 0xFF;
 }
 
 static int coded_count(const MbState& s, int blk) {
@@ -1089,7 +1097,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       pic->hmbs = H;
       pic->mbs.assign(size_t(W) * H, MbRec{});
       pic->coefs.reserve(size_t(W) * H * 32);
-      pic->mvs.reserve(size_t(W) * H * 32);
+      pic->mvs.reserve(size_t(W) * H * 16);
       pic->dpb_slots = dpb_slots_;
       pic->constrained_intra = pps.constrained_intra_pred;
       pic->idr = sh.idr();
@@ -1179,8 +1187,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
     if (!dpb_.empty()) {
       m.kind = kSkip;
       for (auto& rf : m.ref) rf = u8(dpb_.front().slot);
-      m.mv = u32(pic->mvs.size() / 32);
-      pic->mvs.resize(pic->mvs.size() + 32, 0);
+      m.mv = u32(pic->mvs.size());
+      m.flags |= kMbMv16;
+      pic->mvs.resize(pic->mvs.size() + 2, 0);
       ++pic->inter_mbs;
     } else {
       m.kind = kI16x16;
@@ -1207,7 +1216,7 @@ void validate(const Picture& p) {
   VEP_CHECK(p.dpb_slots >= 1 && p.dpb_slots <= kMaxDpbSlots && p.target >= 0 && p.target < p.dpb_slots,
             "picture DPB slots out of range");
   VEP_CHECK(p.wmbs > 0 && p.hmbs > 0 && p.mbs.size() == size_t(p.nmbs()), "picture size mismatch");
-  const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size() / 32;
+  const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size();
   for (const MbRec& m : p.mbs) {
     VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
     VEP_CHECK(m.qp <= 51 && m.qpc <= 51 && m.qpc2 <= 51, "macroblock QP out of range");
@@ -1224,7 +1233,8 @@ void validate(const Picture& p) {
         VEP_CHECK(g == 0 || g == 0x33u, "8x8 residual block partially coded");
       }
     if (m.kind == kSkip || m.kind == kInter) {
-      VEP_CHECK(size_t(m.mv) + ((m.flags & kMbL1) ? 2 : 1) <= nmv, "motion vectors outside the pool");
+      VEP_CHECK(size_t(m.mv) + size_t(mv_per_list(m.flags)) * ((m.flags & kMbL1) ? 2 : 1) <= nmv,
+                "motion vectors outside the pool");
       for (int k = 0; k < 4; ++k) {
         const int r0 = m.ref[k], r1 = m.ref1[k];
         VEP_CHECK(r0 != 0xFF || r1 != 0xFF, "inter partition without a reference");
@@ -1417,10 +1427,35 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   }
   m.mv = 0;
   m.wp = 0;
+  m.flags &= u8(~(kMbMv8x8 | kMbMv16));
   if (m.kind == kSkip || m.kind == kInter) {
-    m.mv = u32(pic.mvs.size() / 32);
-    pic.mvs.insert(pic.mvs.end(), &s.mv[0][0][0], &s.mv[0][0][0] + 32);
-    if (m.flags & kMbL1) pic.mvs.insert(pic.mvs.end(), &s.mv[1][0][0], &s.mv[1][0][0] + 32);
+    // the coarsest granularity that represents the motion of every list used exactly
+    const int nl = (m.flags & kMbL1) ? 2 : 1;
+    bool u16 = true, u8x8 = true;
+    for (int l = 0; l < nl; ++l) {
+      u32 v[16];
+      std::memcpy(v, &s.mv[l][0][0], sizeof v);
+      for (int b = 1; b < 16; ++b) u16 &= v[b] == v[0];
+      for (int b = 0; b < 16; ++b) {
+        const int c = ((b >> 3) << 3) | (b & 2);  // top-left block of b's 8x8
+        u8x8 &= v[b] == v[c];
+      }
+    }
+    m.flags |= u16 ? kMbMv16 : (u8x8 ? kMbMv8x8 : 0);
+    m.mv = u32(pic.mvs.size());
+    for (int l = 0; l < nl; ++l) {
+      const i16* v = &s.mv[l][0][0];
+      if (u16) {
+        pic.mvs.insert(pic.mvs.end(), v, v + 2);
+      } else if (u8x8) {
+        for (int q = 0; q < 4; ++q) {
+          const int b = (q & 1) * 2 + (q >> 1) * 8;
+          pic.mvs.insert(pic.mvs.end(), v + 2 * b, v + 2 * b + 2);
+        }
+      } else {
+        pic.mvs.insert(pic.mvs.end(), v, v + 32);
+      }
+    }
     if (wp && (m.flags & kMbWp)) {
       m.wp = u32(pic.wps.size());
       pic.wps.insert(pic.wps.end(), wp, wp + 4);
@@ -1507,8 +1542,16 @@ struct Recon {
   }
 
   void inter(const MbRec& m, int mx, int my) {
-    const i16* mv0 = &pic.mvs[size_t(m.mv) * 32];
-    const i16* mv1 = (m.flags & kMbL1) ? mv0 + 32 : nullptr;
+    i16 e[2][32];  // expanded to one vector per 4x4 block
+    const i16* base = &pic.mvs[size_t(m.mv)];
+    for (int l = 0; l < ((m.flags & kMbL1) ? 2 : 1); ++l)
+      for (int b = 0; b < 16; ++b) {
+        const i16* v = base + mv_sub(m.flags, l, b);
+        e[l][2 * b] = v[0];
+        e[l][2 * b + 1] = v[1];
+      }
+    const i16* mv0 = e[0];
+    const i16* mv1 = (m.flags & kMbL1) ? e[1] : nullptr;
     const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
     int py[256], pc[2][64], res[256];
     predict_inter(slots, m, mv0, mv1, wp, mx, my, py, pc);
@@ -1693,7 +1736,7 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
   const int W = pic.wmbs, pitch = T.coded_w;
   u8* Yp = T.y.data();
   u8* UV = T.uv.data();
-  auto mvs = [&](const MbRec& r) { return is_intra(r.kind) ? kZeroMv : &pic.mvs[size_t(r.mv) * 32]; };
+  auto mvs = [&](const MbRec& r) { return is_intra(r.kind) ? kZeroMv : &pic.mvs[size_t(r.mv)]; };
   for (int mb = 0; mb < pic.nmbs(); ++mb) {
     const MbRec& q = pic.mbs[size_t(mb)];
     if (q.dbk & 1) continue;

@@ -43,8 +43,13 @@ VEP_HD bool is_wave_intra(u8 k) { return k == kI4x4 || k == kI16x16 || k == kI8x
 // MbRec::flags
 constexpr u8 kMbT8x8 = 1;  // luma residual in 8x8 transform blocks (4 pool blocks each: 64
                            // coefficients, raster 8x8); deblocking skips internal 4x4 edges
-constexpr u8 kMbL1 = 2;    // list-1 motion present: 32 more mv entries follow the list-0 ones
+constexpr u8 kMbL1 = 2;    // list-1 motion present: its vectors follow the list-0 ones
 constexpr u8 kMbWp = 4;    // weighted prediction: MbRec::wp names 4 WpEntry (one per 8x8)
+// Motion granularity in the mv pool (neither: 16 vectors per list, raster 4x4). Skip / direct /
+// 16x16 macroblocks are uniform per 8x8 or per MB, so a B picture's pool shrinks ~8x (host
+// memory traffic and the per-tick upload).
+constexpr u8 kMbMv8x8 = 8;   // 4 vectors per list (raster 8x8)
+constexpr u8 kMbMv16 = 16;   // 1 vector per list
 
 struct MbRec {
   u8 kind;          // MbKind
@@ -54,7 +59,7 @@ struct MbRec {
   u8 i16_mode;      // Intra16x16PredMode
   u8 chroma_mode;   // intra_chroma_pred_mode
   u8 dbk;           // deblocking: bit0 filter disabled (idc 1), bit1 slice-edge mode (idc 2)
-  u8 flags;         // kMbT8x8 | kMbL1 | kMbWp
+  u8 flags;         // kMbT8x8 | kMbL1 | kMbWp | kMbMv8x8 | kMbMv16
   u16 nz;           // luma 4x4 blocks (raster) with non-zero coefficients (deblocking bS 2; for
                     // 8x8-transform MBs all four blocks of a coded 8x8)
   u16 luma_coded;   // luma 4x4 blocks (raster) with residual samples to add (8x8 transform: all
@@ -69,8 +74,8 @@ struct MbRec {
   u8 ref1[4];       // per 8x8: DPB slot of the list-1 reference picture (0xFF = none)
   u32 coef;         // first 16-coefficient block in the picture's coefficient pool (I_PCM:
                     // 384 raw sample bytes = 12 blocks)
-  u32 mv;           // first of 16 (x, y) motion vectors (raster 4x4) in the mv pool (units of
-                    // 32 i16); kMbL1: the list-1 vectors are the next unit
+  u32 mv;           // i16 offset of the MB's motion vectors in the mv pool: (x, y) per vector,
+                    // list 0 then (kMbL1) list 1; see mv_sub()
   u8 i4[8];         // Intra4x4PredMode per raster 4x4 block / Intra8x8PredMode per raster 8x8
                     // block (nibbles 0..3), 4 bits each (low nibble first)
   u32 res;          // intra MBs with residual: slot of their 384 residual samples (GPU scratch,
@@ -80,6 +85,15 @@ struct MbRec {
 };
 static_assert(sizeof(MbRec) == 56, "MbRec layout");
 constexpr u32 kNoRes = 0xFFFFFFFFu;
+
+// i16 entries per list of an MB's motion (2, 8 or 32).
+VEP_HD int mv_per_list(u8 flags) { return (flags & kMbMv16) ? 2 : ((flags & kMbMv8x8) ? 8 : 32); }
+// Offset (i16 units, from the MB's pool base) of the (x, y) vector of raster 4x4 block `blk` in
+// list `list`.
+VEP_HD int mv_sub(u8 flags, int list, int blk) {
+  const int k = (flags & kMbMv16) ? 0 : ((flags & kMbMv8x8) ? 2 * (((blk >> 3) << 1) | ((blk & 3) >> 1)) : 2 * blk);
+  return list * mv_per_list(flags) + k;
+}
 
 // Weighted sample prediction of one 8x8 partition (§8.4.2.3), per component (Y, Cb, Cr):
 // explicit (pred_weight_table) or implicit (POC distances) weights resolved on the host.
@@ -759,10 +773,10 @@ VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbR
   const int q0 = mq.ref[q8], q1 = (mq.flags & kMbL1) ? mq.ref1[q8] : 0xFF;
   const int np = (p0 != 0xFF) + (p1 != 0xFF), nq = (q0 != 0xFF) + (q1 != 0xFF);
   if (np != nq) return 1;
-  const i16* pa = mv_p + 2 * bp;        // list 0 of P
-  const i16* pb = mv_p + 32 + 2 * bp;   // list 1 of P (valid when p1 used)
-  const i16* qa = mv_q + 2 * bq;
-  const i16* qb = mv_q + 32 + 2 * bq;
+  const i16* pa = mv_p + mv_sub(mp.flags, 0, bp);  // list 0 of P
+  const i16* pb = mv_p + mv_sub(mp.flags, 1, bp);  // list 1 of P (valid when p1 used)
+  const i16* qa = mv_q + mv_sub(mq.flags, 0, bq);
+  const i16* qb = mv_q + mv_sub(mq.flags, 1, bq);
   if (np == 1) {
     const int rp = p0 != 0xFF ? p0 : p1, rq = q0 != 0xFF ? q0 : q1;
     if (rp != rq) return 1;

@@ -159,22 +159,26 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     }
     return;
   }
-  const i16* mv0 = d.mvs + size_t(m.mv) * 32;
-  const i16* mv1 = (m.flags & avc::kMbL1) ? mv0 + 32 : nullptr;
+  const i16* mvb = d.mvs + size_t(m.mv);  // the MB's vectors (granularity: m.flags)
+  const bool l1 = (m.flags & avc::kMbL1) != 0;
   const avc::WpEntry* wpp =
       (m.flags & avc::kMbWp) ? static_cast<const avc::WpEntry*>(d.wps) + m.wp : nullptr;
   int v[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int y = y0 + 4 * k, blk = k * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
-    const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
     int p0 = 0, p1 = 0;
-    if (s0 != 0xFF)
-      p0 = avc::luma_qpel(d.y + d.slot_y * u64(s0), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * blk] >> 2),
-                          my * 16 + y + (mv0[2 * blk + 1] >> 2), mv0[2 * blk] & 3, mv0[2 * blk + 1] & 3);
-    if (s1 != 0xFF)
-      p1 = avc::luma_qpel(d.y + d.slot_y * u64(s1), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * blk] >> 2),
-                          my * 16 + y + (mv1[2 * blk + 1] >> 2), mv1[2 * blk] & 3, mv1[2 * blk + 1] & 3);
+    if (s0 != 0xFF) {
+      const i16* v0 = mvb + avc::mv_sub(m.flags, 0, blk);
+      p0 = avc::luma_qpel(d.y + d.slot_y * u64(s0), pitch, wpx, hpx, mx * 16 + x + (v0[0] >> 2),
+                          my * 16 + y + (v0[1] >> 2), v0[0] & 3, v0[1] & 3);
+    }
+    if (s1 != 0xFF) {
+      const i16* v1 = mvb + avc::mv_sub(m.flags, 1, blk);
+      p1 = avc::luma_qpel(d.y + d.slot_y * u64(s1), pitch, wpx, hpx, mx * 16 + x + (v1[0] >> 2),
+                          my * 16 + y + (v1[1] >> 2), v1[0] & 3, v1[1] & 3);
+    }
     v[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 0);
   }
   if (t8) luma8_residual(d, m, lane, T);
@@ -191,14 +195,18 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   for (int k = 0; k < 2; ++k) {
     const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
     const int r = (cy >> 1) * 4 + (cx >> 1), b8 = ((cy >> 2) << 1) | (cx >> 2);
-    const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
+    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
     int p0 = 0, p1 = 0;
-    if (s0 != 0xFF)
-      p0 = avc::chroma_epel(d.uv + d.slot_uv * u64(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (mv0[2 * r] >> 3),
-                            my * 8 + cy + (mv0[2 * r + 1] >> 3), mv0[2 * r] & 7, mv0[2 * r + 1] & 7);
-    if (s1 != 0xFF)
-      p1 = avc::chroma_epel(d.uv + d.slot_uv * u64(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (mv1[2 * r] >> 3),
-                            my * 8 + cy + (mv1[2 * r + 1] >> 3), mv1[2 * r] & 7, mv1[2 * r + 1] & 7);
+    if (s0 != 0xFF) {
+      const i16* v0 = mvb + avc::mv_sub(m.flags, 0, r);
+      p0 = avc::chroma_epel(d.uv + d.slot_uv * u64(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v0[0] >> 3),
+                            my * 8 + cy + (v0[1] >> 3), v0[0] & 7, v0[1] & 7);
+    }
+    if (s1 != 0xFF) {
+      const i16* v1 = mvb + avc::mv_sub(m.flags, 1, r);
+      p1 = avc::chroma_epel(d.uv + d.slot_uv * u64(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v1[0] >> 3),
+                            my * 8 + cy + (v1[1] >> 3), v1[0] & 7, v1[1] & 7);
+    }
     u[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 1 + cc);
   }
 #pragma unroll
@@ -686,9 +694,9 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
     const MbRec tm = row > 0 ? rec(d, mb - W) : q;
     const bool left = x > 0 && !((q.dbk & 2) && lm.slice != q.slice);
     const bool top = row > 0 && !((q.dbk & 2) && tm.slice != q.slice);
-    const i16* mq = avc::is_intra(q.kind) ? nullptr : d.mvs + size_t(q.mv) * 32;
-    const i16* ml = avc::is_intra(lm.kind) ? nullptr : d.mvs + size_t(lm.mv) * 32;
-    const i16* mt = avc::is_intra(tm.kind) ? nullptr : d.mvs + size_t(tm.mv) * 32;
+    const i16* mq = avc::is_intra(q.kind) ? nullptr : d.mvs + size_t(q.mv);
+    const i16* ml = avc::is_intra(lm.kind) ? nullptr : d.mvs + size_t(lm.mv);
+    const i16* mt = avc::is_intra(tm.kind) ? nullptr : d.mvs + size_t(tm.mv);
     const bool t8 = (q.flags & avc::kMbT8x8) != 0;
     for (int dir = 0; dir < 2; ++dir)
       for (int e = 0; e < 4; ++e) {
