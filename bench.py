@@ -93,6 +93,12 @@ def parse_args():
     ap.add_argument("--ring-slots", type=int, default=2)
     ap.add_argument("--latency-samples", type=int, default=100)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (plumbing check, no GPU)")
+    ap.add_argument("--source", choices=["replay", "rtsp"], default="replay",
+                    help="replay = pre-encoded AUs fed to the decode pipeline (decode-only); rtsp = an "
+                         "in-process loopback RTSP camera farm, unthrottled, with the production "
+                         "ingest (RtspClient + RTP depacketizer + lazy decoder) inside the timed loop")
+    ap.add_argument("--clients", type=int, default=32,
+                    help="concurrent gRPC clients for the latency run (one stream each)")
     a = ap.parse_args()
     if a.qp is None:
         a.qp = 27 if a.profile == "baseline" else 25
@@ -126,6 +132,206 @@ def spawn_ranks(n: int) -> int:
     return subprocess.call(cmd)
 
 
+def describe_streams(a, compressed):
+    if compressed and a.profile == "baseline":
+        return "Baseline CAVLC I/P"
+    if compressed:
+        return (f"{a.profile.capitalize()} profile {'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
+                f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"
+                f"{', 8x8 transform + Intra_8x8' if a.profile == 'high' else ''}")
+    return "I_PCM/P_Skip fast path"
+
+
+def make_cfg(vep, a, rank, compressed):
+    cfg = vep.SynthConfig()
+    cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
+    cfg.codec = a.codec
+    cfg.seed = 1 + rank * 100003
+    if compressed:
+        cfg.compressed = True
+        cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
+        cfg.profile, cfg.bframes, cfg.cabac = a.profile, a.bframes, not a.cavlc
+    return cfg
+
+
+class RtspFarm:
+    """`--source rtsp`: a loopback RTSP camera farm (one served stream per camera, pre-encoded
+    GOPs looped, unthrottled) and one production IngestSession per camera (RTSP client + RTP
+    depacketizer + Camera::on_access_unit lazy decoder -> Worker batches). Every picture of the
+    timed region crossed the network stack, the depacketizer and the host parse inside it."""
+
+    def __init__(self, vep, worker, a, rank, compressed):
+        import threading
+
+        self.worker = worker
+        self.srv = vep.RtspServer("127.0.0.1", 0)
+        self.cams = a.cams_per_gpu
+        self.stream_bytes = 0
+        for i in range(self.cams):
+            c = make_cfg(vep, a, rank, compressed)
+            c.seed = c.seed + i * 7919
+            c.idr_phase = (i * a.gop) // self.cams  # unsynchronised cameras
+            self.srv.add_stream(f"/cam{i}", c, realtime=False, cached_frames=a.gop * a.cache_gops)
+        self.srv.start()
+        worker.start()
+        self.idx = [worker.add_camera(f"r{rank}rtsp{i}", a.ring_slots) for i in range(self.cams)]
+        self._touch()
+        self.sessions = []
+        for i, cam in enumerate(self.idx):
+            sess = vep.IngestSession(worker, cam, f"r{rank}rtsp{i}", f"rtsp://127.0.0.1:{self.srv.port}/cam{i}")
+            sess.start()
+            self.sessions.append(sess)
+        self.stop_evt = threading.Event()
+        self.toucher = threading.Thread(target=self._touch_loop, daemon=True)
+        self.toucher.start()
+
+    def _touch(self):  # a client is watching every camera (the lazy decoder's last_query)
+        now = int(time.time() * 1000)
+        for cam in self.idx:
+            self.worker.set_last_query(cam, now)
+
+    def _touch_loop(self):
+        while not self.stop_evt.wait(0.5):
+            self._touch()
+
+    def wait_pictures(self, target, timeout_s=120.0):
+        deadline = time.perf_counter() + timeout_s
+        while self.worker.pictures < target:
+            if time.perf_counter() > deadline:
+                raise RuntimeError(f"rtsp farm stalled at {self.worker.pictures}/{target} pictures")
+            time.sleep(0.0002)
+
+    def stats(self):
+        st = [self.worker.stats(c) for c in self.idx]
+        return {"packets": sum(x["packets"] for x in st), "bytes_in": sum(x["bytes_in"] for x in st),
+                "errors": sum(x["errors"] for x in st), "decoded": sum(x["decoded"] for x in st)}
+
+    def close(self):
+        self.stop_evt.set()
+        for sess in self.sessions:
+            sess.stop()
+        self.srv.stop()
+        self.worker.stop()
+
+
+def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed):
+    """`--source rtsp`: the timed loop waits for the live pipeline (loopback RTSP farm ->
+    IngestSession -> lazy decoder -> Worker batches) to decode `cams` more pictures per step."""
+    from video_edge_ai_proxy_amd.server.bench_latency import grpc_concurrent_latency, summarize
+
+    cams = a.cams_per_gpu
+    buf = torch.empty((cams, row), dtype=torch.uint8, device=dev)
+    gather = world > 1 and not a.no_gather
+    gathered = torch.empty((world * cams, row), dtype=torch.uint8, device=dev) if gather else None
+    worker.set_consumer_buffers(buf.data_ptr(), 0, cams)
+
+    def sync():
+        if use_gpu:
+            torch.cuda.synchronize()
+
+    farm = RtspFarm(vep, worker, a, rank, compressed)
+    try:
+        farm.wait_pictures(cams * max(1, a.warmup), timeout_s=300.0)
+        if world > 1:
+            dist.barrier()
+        sync()
+        p0, f0, d0, s0 = worker.pictures, worker.frames, worker.dropped, farm.stats()
+        g0 = worker.gpu_ms_total
+        handle = None
+        t0 = time.perf_counter()
+        for i in range(a.steps):
+            farm.wait_pictures(p0 + cams * (i + 1))
+            if gather:  # RCCL all-gather of the letterboxed consumer batch, overlapped with decode
+                if handle is not None:
+                    handle.wait()
+                handle = dist.all_gather_into_tensor(gathered, buf, async_op=True)
+        if handle is not None:
+            handle.wait()
+        sync()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        elapsed = t1 - t0
+        pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
+        s1 = farm.stats()
+        gpu_ms = worker.gpu_ms_total - g0
+        wire_bytes = s1["bytes_in"] - s0["bytes_in"]
+        errors = s1["errors"] - s0["errors"]
+        if world > 1:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes], dtype=torch.float64, device=dev)
+            dist.all_reduce(fr, op=dist.ReduceOp.SUM)
+            pictures, frames, dropped, errors, wire_bytes = (int(v) for v in fr.tolist())
+        conc = (None, None)
+        nconc = 0
+        if rank == 0 and a.latency_samples > 0 and a.clients > 0:
+            xs = grpc_concurrent_latency(worker, farm.idx, a.clients, duration_s=3.0)
+            conc, nconc = summarize(xs), len(xs)
+        if world > 1:
+            dist.barrier()
+    finally:
+        farm.close()
+    if rank == 0:
+        fps = pictures / elapsed
+        res = {
+            "metric": METRIC,
+            "value": round(fps, 2),
+            "unit": "frames/s",
+            "n_gpus": world if use_gpu else 0,
+            "n_ranks": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "uint8 (BGR24 frames; bf16-capable consumer path)",
+            "data": (f"synthetic {CODEC[a.codec]} camera streams ({describe_streams(a, compressed)}, QP {a.qp}, "
+                     f"GOP {a.gop}) served by an in-process loopback RTSP farm (RTP/TCP interleaved, "
+                     f"FU-A), unthrottled; {wire_bytes * 8 / max(1, pictures) * a.fps / 1e6:.1f} Mbit/s per "
+                     f"camera at {a.fps} fps (wire bytes per decoded picture)"),
+            "source": "rtsp",
+            "config": {
+                "model": f"{cams * max(world, 1)}x{a.width}x{a.height}p{a.fps} {CODEC[a.codec]} cameras",
+                "global_batch": cams * max(world, 1),
+                "seq_len": a.gop,
+                "parallelism": f"camera-dp{max(world, 1)}",
+                "cams_per_gpu": cams,
+                "letterbox": a.letterbox,
+                "consumer_format": a.consumer_format,
+                "all_gather": gather,
+            },
+            "frame_count_definition": "pictures the live pipeline decoded (RTSP receive -> RTP "
+                                      "depacketize -> host parse -> GPU reconstruct) during the timed "
+                                      "region; the newest of each camera's batch is converted to BGR24 "
+                                      "and committed to its HBM ring (frames_published); older ones of "
+                                      "a catch-up batch are superseded before any client could read them",
+            "frames_decoded": pictures,
+            "frames_published": frames,
+            "frames_dropped": dropped,
+            "decode_errors": errors,
+            "concurrent_clients": a.clients,
+            "p50_latency_ms": round(conc[0], 3) if conc[0] is not None else None,
+            "p99_latency_ms": round(conc[1], 3) if conc[1] is not None else None,
+            "latency_definition": f"{a.clients} concurrent gRPC clients (one connected channel and camera "
+                                  "each) issuing back-to-back VideoLatestImage requests while every "
+                                  "camera decodes live: request sent -> the camera's next "
+                                  f"{a.width}x{a.height} BGR24 VideoFrame received and parsed; {nconc} samples",
+            "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "rocdecode_available": bool(vep.rocdecode_available()),
+            "per_gpu_fps": round(fps / max(world, 1), 2),
+        }
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if dropped or errors:
+        print(f"bench: {dropped} frames dropped, {errors} decode errors in the timed region", file=sys.stderr,
+              flush=True)
+        sys.exit(3)
+
+
 def main():
     a = parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.cpu:
@@ -157,21 +363,11 @@ def main():
                         letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes,
                         stages=a.stages, queue=a.lane_queue)
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
-    cfg = vep.SynthConfig()
-    cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
-    cfg.codec = a.codec
-    cfg.seed = 1 + rank * 100003
     compressed = a.content == "avc" and a.codec == "h264"
-    if compressed:
-        cfg.compressed = True
-        cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
-        cfg.profile, cfg.bframes, cfg.cabac = a.profile, a.bframes, not a.cavlc
-    if compressed and a.profile == "baseline":
-        stream_desc = "Baseline CAVLC I/P"
-    elif compressed:
-        stream_desc = (f"{a.profile.capitalize()} profile {'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
-                       f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"
-                       f"{', 8x8 transform + Intra_8x8' if a.profile == 'high' else ''}")
+    cfg = make_cfg(vep, a, rank, compressed)
+    stream_desc = describe_streams(a, compressed)
+    if a.source == "rtsp":
+        return run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed)
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
 
@@ -258,13 +454,19 @@ def main():
         dist.all_reduce(fr, op=dist.ReduceOp.SUM)
         frames, dropped, launched = (int(v) for v in fr.tolist())
 
-    serve_lat = next_lat = (None, None)
-    nlat = 0
+    serve_lat = next_lat = conc_lat = (None, None)
+    nlat = nconc = 0
     if rank == 0 and a.latency_samples > 0:
+        from video_edge_ai_proxy_amd.server.bench_latency import grpc_concurrent_latency, summarize
+
         # the single-process tick must not touch the collective: decode-only ticks here
         worker.set_consumer_buffers(bufs[0].data_ptr(), 0, cams)
         serve_lat, next_lat, nlat = measure_latency(worker, list(rb.cameras), a.latency_samples,
                                                     lambda: (rb.step(), rb.drain()), float(a.fps))
+        if a.clients > 0:
+            xs = grpc_concurrent_latency(worker, list(rb.cameras), a.clients, duration_s=3.0,
+                                         tick=lambda: (rb.step(), rb.drain()), fps=float(a.fps))
+            conc_lat, nconc = summarize(xs), len(xs)
     if world > 1:
         dist.barrier()
 
@@ -311,6 +513,14 @@ def main():
                                   "parsed; newest frame already in the HBM ring; cameras decoding "
                                   f"at {a.fps} fps meanwhile; {nlat} samples",
             "p50_next_frame_latency_ms": r3(next_lat[0]),
+            "concurrent_clients": a.clients,
+            "concurrent_p50_latency_ms": r3(conc_lat[0]),
+            "concurrent_p99_latency_ms": r3(conc_lat[1]),
+            "concurrent_latency_definition": f"{a.clients} concurrent gRPC clients (one connected channel and "
+                                             "camera each) issuing back-to-back VideoLatestImage requests "
+                                             f"while every camera decodes at {a.fps} fps: request sent -> "
+                                             "the camera's next frame received and parsed (includes waiting "
+                                             f"for it, up to one frame interval); {nconc} samples",
             "next_frame_latency_definition": "back-to-back requests on one stream/channel (the "
                                              "reference clients' pattern): includes waiting for "
                                              "the camera's next decoded frame",

@@ -744,6 +744,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("batches", &Worker::batches)
       .def_property_readonly("frames", &Worker::frames)
       .def_property_readonly("dropped", &Worker::dropped)
+      .def_property_readonly("pictures", &Worker::pictures)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
       .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)
       .def_property_readonly("direct_reads", &Worker::direct_reads)

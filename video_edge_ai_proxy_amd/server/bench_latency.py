@@ -99,6 +99,69 @@ def grpc_latency(worker, cams, samples: int, tick=None, fps: float = 30.0):
     return serve_ms, next_ms
 
 
+def grpc_concurrent_latency(worker, cams, clients: int, duration_s: float = 3.0, tick=None,
+                            fps: float = 30.0):
+    """``clients`` concurrent gRPC clients, each on its own connected channel and camera
+    (round-robin), issuing back-to-back VideoLatestImage requests for ``duration_s`` — the
+    reference clients' pattern, all at once. Each answer is a frame newer than the client's
+    previous one, so a sample is request sent -> the camera's next frame received and parsed.
+    ``tick()`` (replay mode) decodes one frame per camera at ``fps``; None when the cameras decode
+    live (RTSP farm). Returns the per-request latencies in ms."""
+    import grpc
+
+    hub = _WorkerHub(worker, cams)
+    svc = ImageService(_PM(hub))
+    server = serve(svc, "127.0.0.1:0", workers=max(16, 2 * clients))
+    stop = threading.Event()
+    ticker_th = None
+    if tick is not None:
+        def ticker():
+            nxt = time.perf_counter()
+            while not stop.is_set():
+                tick()
+                nxt += 1.0 / fps
+                time.sleep(max(0.0, nxt - time.perf_counter()))
+
+        ticker_th = threading.Thread(target=ticker, daemon=True)
+        ticker_th.start()
+    target = f"127.0.0.1:{server.bound_port}"
+    names = list(hub.map)
+    lat: list[list[float]] = [[] for _ in range(clients)]
+    go = threading.Event()
+
+    def client(k):
+        cli = ImageClient(target)
+        try:
+            grpc.channel_ready_future(cli.channel).result(timeout=10)
+            name = names[k % len(names)]
+            cli.latest_frame(name)  # cursor at the current frame
+            go.wait()
+            end = time.perf_counter() + duration_s
+            while time.perf_counter() < end:
+                t0 = time.perf_counter()
+                vf = cli.latest_frame(name)
+                t1 = time.perf_counter()
+                if vf is not None and vf.width:
+                    lat[k].append((t1 - t0) * 1e3)
+        finally:
+            cli.close()
+
+    threads = [threading.Thread(target=client, args=(k,), daemon=True) for k in range(clients)]
+    try:
+        for t in threads:
+            t.start()
+        time.sleep(0.5)
+        go.set()
+        for t in threads:
+            t.join(timeout=duration_s + 30)
+    finally:
+        stop.set()
+        if ticker_th is not None:
+            ticker_th.join(timeout=5)
+        server.stop(0)
+    return [x for xs in lat for x in xs]
+
+
 def grpc_latency_samples(worker, cams, samples, tick=None):
     serve_ms, _ = grpc_latency(worker, cams, samples, tick)
     return serve_ms

@@ -16,6 +16,7 @@ from __future__ import annotations
 import logging
 import threading
 import time
+from collections import OrderedDict
 from concurrent import futures
 from typing import Optional
 
@@ -33,6 +34,7 @@ log = logging.getLogger("vep.grpc")
 MAX_MSG = 256 * 1024 * 1024  # 4K BGR24 frames are 24.9 MB; grpcio's default is 4 MiB
 STREAM_DEADLINE_S = 15.0
 WAIT_ATTEMPTS, WAIT_BLOCK_MS = 3, 1000
+MAX_CURSORS = 65536  # (client, camera) cursors kept, least recently used evicted first
 _EMPTY = b""  # serialized empty VideoFrame
 
 
@@ -45,7 +47,9 @@ class ImageService:
         self.edge = edge_service
         self.queue = annotation_queue
         self.api_endpoint = api_endpoint
-        self._cursors: dict[tuple[str, str], int] = {}
+        # per (client peer, camera) sequence of the last frame sent; least recently used entries
+        # are evicted one at a time past MAX_CURSORS (no wholesale reset of every client)
+        self._cursors: "OrderedDict[tuple[str, str], int]" = OrderedDict()
         self._cur_lock = threading.Lock()
         self._edge_key: Optional[str] = None
         self.frames_served = 0
@@ -58,9 +62,11 @@ class ImageService:
 
     def _set_cursor(self, peer: str, dev: str, seq: int) -> None:
         with self._cur_lock:
-            if len(self._cursors) > 65536:
-                self._cursors.clear()
-            self._cursors[(peer, dev)] = seq
+            key = (peer, dev)
+            self._cursors[key] = seq
+            self._cursors.move_to_end(key)
+            while len(self._cursors) > MAX_CURSORS:
+                self._cursors.popitem(last=False)
 
     def frame_for(self, dev: str, key_frame_only: bool, peer: str = "") -> bytes:
         t0 = time.perf_counter()
