@@ -49,3 +49,23 @@ def test_live_rtsp_to_grpc_on_gpu(native, tmp_path):
     finally:
         app.stop()
         srv.stop()
+
+
+@pytest.mark.parametrize("profile", ["baseline", "high"])
+def test_live_compressed_rtsp_on_gpu(native, profile):
+    """Compressed live cameras (CAVLC Baseline, CABAC IBBP High) through RTSP ingest on the
+    gfx950 path: every published frame equals the CPU reference decoder's (test_live_compressed
+    is the CPU-backend twin)."""
+    from test_live_compressed import FPS, Live, check_frames, reference, stream_cfg
+
+    n = 20
+    cfg = stream_cfg(native, profile, w=640, h=360)
+    ref, _ = reference(native, cfg, n, loops=4)
+    live = Live(native, cfg, n, device=0)
+    try:
+        got = live.frames(1.5)
+        st = live.w.stats(live.cam)
+    finally:
+        live.close()
+    check_frames(got, ref, n, 90000 // FPS)
+    assert len(got) >= 15 and st["decoder"] == "general" and st["errors"] == 0
