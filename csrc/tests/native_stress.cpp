@@ -6,6 +6,11 @@
 //   * ring replacement on a resolution change while readers hold the old ring;
 //   * remove_camera while readers still hold the camera;
 //   * RTSP server with concurrent clients; IngestSession supervisor start/stop against it.
+//   * the general H.264 decoder (Baseline CAVLC and High CABAC IBBP streams) under concurrent
+//     producers and readers, with GOP catch-up merges and keyframe-only toggling;
+//   * the replay bench driver: parse pool threads + quiesce + step/drain (launch_async,
+//     wait_published, complete_all) against readers;
+//   * live ingest of a compressed High-profile camera with RTMP pass-through and the archiver.
 // Reference: SURVEY.md §5 "Race detection / sanitizers" (the reference had none and real races:
 // read_image.py:48,71-74 vs rtsp_to_rtmp.py:147-151; grpc_api.go:181-184).
 #include <atomic>
@@ -13,6 +18,7 @@
 #include <thread>
 #include <vector>
 
+#include "../vep/bench_driver.h"
 #include "../vep/ingest.h"
 #include "../vep/runtime.h"
 #include "../vep/synth.h"
@@ -164,9 +170,158 @@ static void rtsp_stress() {
               (unsigned long long)w.camera(cam)->decoded.load());
 }
 
+static SynthConfig compressed_cfg(const char* profile, u64 seed, int w, int h) {
+  SynthConfig c;
+  c.width = w;
+  c.height = h;
+  c.gop = 8;
+  c.seed = seed;
+  c.compressed = true;
+  c.profile = profile;
+  c.bframes = 2;
+  c.coverage = seed % 2 == 0;  // every MB / sub-MB type on half the cameras
+  return c;
+}
+
+static void general_decoder_stress() {
+  WorkerOptions o;
+  o.device = -1;
+  o.letterbox_size = 64;
+  o.max_cameras = 8;
+  Worker w(o);
+  w.start();
+  const int ncam = 4;
+  std::vector<int> cams;
+  for (int i = 0; i < ncam; ++i) cams.push_back(w.add_camera("g" + std::to_string(i), 3));
+  std::atomic<bool> stop{false};
+  std::atomic<u64> served{0};
+  std::vector<std::thread> th;
+  for (int i = 0; i < ncam; ++i) {
+    th.emplace_back([&, i] {
+      SynthH264 enc(compressed_cfg(i < 2 ? "high" : "baseline", u64(i + 1), 96 + 16 * i, 64));
+      auto cam = w.camera(cams[size_t(i)]);
+      for (int f = 0; f < 48; ++f) {
+        cam->last_query_ms.store(now_ms());
+        cam->keyframe_only.store(i == 3 && f % 24 > 16);
+        cam->on_access_unit(enc.next());
+        if (f % 5 == 0) std::this_thread::sleep_for(std::chrono::microseconds(300));  // catch-up merges
+      }
+    });
+  }
+  for (int r = 0; r < 2; ++r) {
+    th.emplace_back([&] {
+      std::vector<u8> buf(size_t(160) * 64 * 3);
+      i64 cursor[8] = {};
+      while (!stop.load()) {
+        for (int i = 0; i < ncam; ++i) {
+          auto cam = w.camera(cams[size_t(i)]);
+          auto ring = cam ? cam->ring() : nullptr;
+          if (!ring) continue;
+          FrameMeta m;
+          if (ring->slot_bytes() <= buf.size() && w.read_latest(*ring, cursor[i], &m, buf.data(), buf.size())) {
+            CHECK(m.seq > cursor[i]);
+            cursor[i] = m.seq;
+            served.fetch_add(1);
+          }
+        }
+      }
+    });
+  }
+  for (int i = 0; i < ncam; ++i) th[size_t(i)].join();
+  w.flush();
+  stop.store(true);
+  for (size_t i = ncam; i < th.size(); ++i) th[i].join();
+  for (int i = 0; i < ncam; ++i) {
+    CHECK(w.camera(cams[size_t(i)])->decoded.load() > 0);
+    CHECK(w.camera(cams[size_t(i)])->errors.load() == 0);
+  }
+  w.stop();
+  std::printf("general decoder: served %llu frames, %llu pictures\n", (unsigned long long)served.load(),
+              (unsigned long long)w.pictures());
+}
+
+static void replay_bench_stress() {
+  WorkerOptions o;
+  o.device = -1;
+  o.letterbox_size = 32;
+  o.max_cameras = 6;
+  Worker w(o);
+  SynthConfig c = compressed_cfg("high", 7, 96, 64);
+  c.coverage = false;
+  ReplayBench rb(w, 6, c, 16, 3, 2, "rb", 4);
+  std::atomic<bool> stop{false};
+  std::thread reader([&] {
+    std::vector<u8> buf(size_t(96) * 64 * 3);
+    i64 cursor = 0;
+    while (!stop.load()) {
+      auto cam = w.camera(rb.cameras()[0]);
+      auto ring = cam ? cam->ring() : nullptr;
+      FrameMeta m;
+      if (ring && ring->slot_bytes() <= buf.size() && w.read_latest(*ring, cursor, &m, buf.data(), buf.size()))
+        cursor = m.seq;
+    }
+  });
+  for (int i = 0; i < 10; ++i) rb.step();
+  rb.quiesce();
+  const u64 f0 = w.frames();
+  for (int i = 0; i < 30; ++i) rb.step();
+  rb.drain();
+  stop.store(true);
+  reader.join();
+  CHECK(rb.parse_failures() == 0 && w.dropped() == 0);
+  CHECK(w.frames() - f0 >= 30 * 6 - 12);
+  std::printf("replay bench: %llu frames published, %llu pictures\n", (unsigned long long)w.frames(),
+              (unsigned long long)w.pictures());
+}
+
+static void compressed_ingest_stress() {
+  net::RtspServer srv("127.0.0.1", 0);
+  net::ServedStream s;
+  s.cfg = compressed_cfg("high", 11, 160, 96);
+  s.cfg.coverage = false;
+  s.realtime = false;
+  s.cached_frames = 16;
+  srv.add_stream("/hi", s);
+  srv.start();
+  mux::RtmpSink sink("127.0.0.1", 0);
+  sink.start();
+  WorkerOptions o;
+  o.device = -1;
+  Worker w(o);
+  w.start();
+  int cam = w.add_camera("hi", 2);
+  w.camera(cam)->last_query_ms.store(now_ms());
+  w.camera(cam)->proxy_rtmp.store(true);
+  IngestConfig ic;
+  ic.name = "hi";
+  ic.rtsp_url = "rtsp://127.0.0.1:" + std::to_string(srv.port()) + "/hi";
+  ic.rtmp_url = "rtmp://127.0.0.1:" + std::to_string(sink.port()) + "/live/hi";
+  ic.disk_path = "/tmp/vep_native_stress_hi";
+  auto arch = std::make_shared<mux::Archiver>();
+  IngestSession sess(w, cam, ic, arch);
+  sess.start();
+  for (int i = 0; i < 200 && w.camera(cam)->decoded.load() < 20; ++i) {
+    w.camera(cam)->last_query_ms.store(now_ms());
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    (void)sess.state();
+  }
+  sess.stop();
+  w.flush();
+  CHECK(w.camera(cam)->decoded.load() >= 20 && w.camera(cam)->errors.load() == 0);
+  arch->flush();
+  CHECK(sink.video_messages() > 0);
+  w.stop();
+  sink.stop();
+  srv.stop();
+  std::printf("compressed ingest: decoded %llu\n", (unsigned long long)w.camera(cam)->decoded.load());
+}
+
 int main() {
   live_worker_stress();
   rtsp_stress();
+  general_decoder_stress();
+  replay_bench_stress();
+  compressed_ingest_stress();
   std::printf("native_stress ok\n");
   return 0;
 }

@@ -76,48 +76,141 @@ void IngestSession::on_au(const AuPtr& au) {
   // --- decode scheduling (lazy / keyframe-only / catch-up) lives in the camera
   cam->on_access_unit(au);
 
-  // --- RTMP pass-through (rtsp_to_rtmp.py:127-139, :162-182)
+  // --- RTMP pass-through (rtsp_to_rtmp.py:127-139, :162-182), sent off this thread
   const bool want = cam->proxy_rtmp.load() && !cfg_.rtmp_url.empty();
   const bool rising = want && !prev_proxy_;
   prev_proxy_ = want;
   if (!want) {
     if (pub_) {
-      pub_->close();
-      pub_.reset();
-      pub_ts0_ = -1;
+      pub_.reset();  // joins the sender; closes the connection
+      log(false, "rtmp publishing stopped");
     }
     return;
   }
   if (!seen_key_) return;
-  try {
-    if (!pub_ || !pub_->connected()) {
-      if (mono_us() / 1000 < pub_retry_at_) return;
-      pub_ = std::make_unique<mux::RtmpPublisher>(cfg_.rtmp_url, cfg_.timeout_ms);
-      pub_->connect();
-      log(false, "rtmp publishing to " + cfg_.rtmp_url);
-      pub_ts0_ = -1;
-    }
-    auto ts_ms = [&](const AccessUnit& a) {
-      if (pub_ts0_ < 0) pub_ts0_ = a.dts;
-      return u32(std::max<i64>(0, (a.dts - pub_ts0_) / 90));
-    };
-    if (rising || pub_->messages() == 0) {
-      // start the stream at a keyframe: sequence header + the whole current GOP
-      if (ps_.complete()) pub_->send_sequence_header(ps_);
-      for (auto& p : gop_) pub_->send_au(*p, ts_ms(*p));
-    } else {
-      pub_->send_au(*au, ts_ms(*au));
-    }
-    std::lock_guard<std::mutex> g(mu_);
-    st_.rtmp_messages = pub_->messages();
-    st_.rtmp_error.clear();
-  } catch (const std::exception& e) {
-    log(true, std::string("failed muxing: ") + e.what());
-    pub_.reset();
-    pub_retry_at_ = mono_us() / 1000 + 2000;
-    std::lock_guard<std::mutex> g(mu_);
-    st_.rtmp_error = e.what();
+  if (rising || !pub_) {
+    pub_ = std::make_unique<RtmpSender>(cfg_.rtmp_url, cfg_.timeout_ms);
+    log(false, "rtmp publishing to " + cfg_.rtmp_url);
+    pub_->start_gop(ps_, gop_);
+  } else if (pub_->needs_keyframe()) {
+    if (au->keyframe) pub_->start_gop(ps_, gop_);  // resume after an overflow / error
+  } else {
+    pub_->push(au);
   }
+  std::string err = pub_->error();
+  if (err != last_rtmp_err_) {
+    if (!err.empty()) log(true, "failed muxing: " + err);
+    last_rtmp_err_ = err;
+  }
+  std::lock_guard<std::mutex> g(mu_);
+  st_.rtmp_messages = pub_->messages();
+  st_.rtmp_error = err;
+}
+
+// ------------------------------------------------------------------------------ RtmpSender
+
+RtmpSender::RtmpSender(std::string url, int timeout_ms, size_t max_bytes)
+    : url_(std::move(url)), timeout_ms_(timeout_ms), max_bytes_(max_bytes) {
+  th_ = std::thread([this] { run(); });
+}
+
+RtmpSender::~RtmpSender() {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    stop_ = true;
+  }
+  cv_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+std::string RtmpSender::error() const {
+  std::lock_guard<std::mutex> g(mu_);
+  return err_;
+}
+
+void RtmpSender::drop_all_locked() {
+  dropped_.fetch_add(q_.size());
+  q_.clear();
+  q_bytes_ = 0;
+  need_key_.store(true);
+}
+
+void RtmpSender::start_gop(const ParamSets& ps, const std::vector<AuPtr>& gop) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    drop_all_locked();  // whatever is still queued belongs to the stream being restarted
+    if (ps.complete()) q_.push_back(Item{nullptr, ps});
+    for (const auto& a : gop) {
+      q_.push_back(Item{a, {}});
+      q_bytes_ += a->bytes();
+    }
+    need_key_.store(false);
+  }
+  cv_.notify_one();
+}
+
+void RtmpSender::push(const AuPtr& au) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (need_key_.load()) {
+      dropped_.fetch_add(1);
+      return;
+    }
+    if (q_bytes_ + au->bytes() > max_bytes_) {  // the server cannot keep up: resume at a keyframe
+      drop_all_locked();
+      dropped_.fetch_add(1);
+      err_ = "rtmp send queue overflow: dropped to the next keyframe";
+      return;
+    }
+    q_.push_back(Item{au, {}});
+    q_bytes_ += au->bytes();
+  }
+  cv_.notify_one();
+}
+
+void RtmpSender::run() {
+  std::unique_ptr<mux::RtmpPublisher> pub;
+  i64 retry_at = 0;
+  for (;;) {
+    Item it;
+    {
+      std::unique_lock<std::mutex> g(mu_);
+      cv_.wait(g, [this] { return stop_ || !q_.empty(); });
+      if (stop_) break;
+      it = std::move(q_.front());
+      q_.pop_front();
+      if (it.au) q_bytes_ -= it.au->bytes();
+    }
+    try {
+      if (!pub || !pub->connected()) {
+        if (mono_us() / 1000 < retry_at) {  // still backing off: this AU is lost
+          std::lock_guard<std::mutex> g(mu_);
+          drop_all_locked();
+          dropped_.fetch_add(1);
+          continue;
+        }
+        pub = std::make_unique<mux::RtmpPublisher>(url_, timeout_ms_);
+        pub->connect();
+        ts0_ = -1;
+      }
+      if (!it.au) {
+        pub->send_sequence_header(it.ps);
+      } else {
+        if (ts0_ < 0) ts0_ = it.au->dts;
+        pub->send_au(*it.au, u32(std::max<i64>(0, (it.au->dts - ts0_) / 90)));
+      }
+      msgs_.store(pub->messages());
+      std::lock_guard<std::mutex> g(mu_);
+      if (err_.rfind("rtmp send queue overflow", 0) != 0) err_.clear();
+    } catch (const std::exception& e) {
+      pub.reset();
+      retry_at = mono_us() / 1000 + 2000;
+      std::lock_guard<std::mutex> g(mu_);
+      err_ = e.what();
+      drop_all_locked();  // a new connection must start at a keyframe
+    }
+  }
+  if (pub) pub->close();
 }
 
 void IngestSession::run() {

@@ -11,6 +11,8 @@
 #pragma once
 
 #include <atomic>
+#include <condition_variable>
+#include <deque>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -49,6 +51,45 @@ struct SessionState {
   int width = 0, height = 0;
 };
 
+// RTMP pass-through off the ingest thread: the ingest thread enqueues access units, a sender
+// thread owns the connection (connect / retry every 2 s / send). The queue is bounded: when the
+// RTMP server is slow or dead it overflows, everything queued is dropped and sending resumes at
+// the next keyframe (with the sequence header), so ingest and decode never wait on RTMP.
+class RtmpSender {
+ public:
+  RtmpSender(std::string url, int timeout_ms, size_t max_bytes = size_t(32) << 20);
+  ~RtmpSender();
+  // Start (or restart after an overflow / error) at a keyframe: the parameter sets and the
+  // current GOP (rtsp_to_rtmp.py:127-139 flushes the GOP on the proxy's rising edge).
+  void start_gop(const ParamSets& ps, const std::vector<AuPtr>& gop);
+  void push(const AuPtr& au);  // one more AU of the running stream (dropped until a keyframe)
+  u64 messages() const { return msgs_.load(); }
+  u64 dropped() const { return dropped_.load(); }
+  bool needs_keyframe() const { return need_key_.load(); }
+  std::string error() const;
+
+ private:
+  struct Item {
+    AuPtr au;          // null: sequence header
+    ParamSets ps;
+  };
+  void run();
+  void drop_all_locked();
+  const std::string url_;
+  const int timeout_ms_;
+  const size_t max_bytes_;
+  std::thread th_;
+  mutable std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Item> q_;
+  size_t q_bytes_ = 0;
+  bool stop_ = false;
+  std::atomic<bool> need_key_{true};
+  std::atomic<u64> msgs_{0}, dropped_{0};
+  std::string err_;
+  i64 ts0_ = -1;
+};
+
 class IngestSession {
  public:
   IngestSession(Worker& w, int cam, IngestConfig cfg, std::shared_ptr<mux::Archiver> archiver);
@@ -72,10 +113,9 @@ class IngestSession {
   mutable std::mutex mu_;
   SessionState st_;
   // pass-through / archive state (ingest thread only)
-  std::unique_ptr<mux::RtmpPublisher> pub_;
+  std::unique_ptr<RtmpSender> pub_;
   bool prev_proxy_ = false;
-  i64 pub_retry_at_ = 0;
-  i64 pub_ts0_ = -1;
+  std::string last_rtmp_err_;
   ParamSets ps_;
   std::vector<AuPtr> gop_;
   i64 gop_start_ms_ = 0;

@@ -241,3 +241,44 @@ def test_live_1080p_fu_a_idr(native):
     for k, img in got:
         want = ref[k if k < 2 * n else n + (k - n) % n]
         assert np.array_equal(img, want), f"AU {k} differs"
+
+
+def test_rtmp_passthrough_never_stalls_ingest(native):
+    """RTMP pass-through runs on its own sender thread with a bounded queue: a server that
+    accepts the TCP connection and then never answers the handshake (the worst case: every send
+    blocks until the timeout) does not slow the camera's ingest or decoding."""
+    import socket
+
+    hang = socket.socket()
+    hang.bind(("127.0.0.1", 0))
+    hang.listen(4)
+    port = hang.getsockname()[1]
+    accepted = []
+    threading.Thread(target=lambda: accepted.append(hang.accept()), daemon=True).start()
+    n = 20
+    cfg = stream_cfg(native, "baseline")
+    srv = native.RtspServer("127.0.0.1", 0)
+    srv.add_stream("/cam", cfg, realtime=True, cached_frames=n)
+    srv.start()
+    w = native.Worker(device=-1)
+    w.start()
+    cam = w.add_camera("px", 2)
+    w.set_last_query(cam, int(time.time() * 1000) + 60000)
+    w.set_proxy(cam, True)
+    sess = native.IngestSession(w, cam, "px", f"rtsp://127.0.0.1:{srv.port}/cam",
+                                rtmp_url=f"rtmp://127.0.0.1:{port}/live/px", timeout_ms=4000)
+    sess.start()
+    try:
+        time.sleep(0.4)
+        d0 = w.stats(cam)["decoded"]
+        time.sleep(1.0)  # the RTMP handshake is hanging all this time
+        d1 = w.stats(cam)["decoded"]
+        aus = sess.state()["aus"]
+    finally:
+        sess.stop()
+        srv.stop()
+        w.stop()
+        hang.close()
+    assert accepted, "the pass-through never tried to connect"
+    assert d1 - d0 >= 40, f"decoding stalled behind RTMP: {d1 - d0} frames in 1 s at {FPS} fps"
+    assert aus >= 60
