@@ -350,6 +350,105 @@ PYBIND11_MODULE(_vep, m) {
         return py::make_tuple(y, uv);
       });
 
+  // Reconstruction primitives of avc_recon.h (shared by the CPU decoder, the gfx950 kernels and
+  // the encoders), exposed one by one for tests/test_spec_oracle.py, which checks them against
+  // independent implementations written from the H.264 text.
+  auto rc = m.def_submodule("recon", "H.264 reconstruction primitives (avc_recon.h)");
+  rc.def("idct4", [](std::vector<int> d) {
+    VEP_CHECK(d.size() == 16, "16 coefficients");
+    i16 c[16];
+    for (int k = 0; k < 16; ++k) c[k] = i16(d[size_t(k)]);
+    std::vector<int> r(16);
+    avc::idct4x4(c, r.data());
+    return r;
+  });
+  rc.def("idct8", [](std::vector<int> d) {
+    VEP_CHECK(d.size() == 64, "64 coefficients");
+    i16 c[64];
+    for (int k = 0; k < 64; ++k) c[k] = i16(d[size_t(k)]);
+    std::vector<int> r(64);
+    avc::idct8x8(c, r.data());
+    return r;
+  });
+  rc.def("dequant4", [](int c, int qp, int i, int j) { return avc::dequant4x4(c, qp, i, j); });
+  // top = p[-1..7, -1] (9, top-right already substituted), left = p[-1, 0..3]
+  rc.def("intra4x4", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode) {
+    VEP_CHECK(top.size() == 9 && left.size() == 4, "9 top + 4 left samples");
+    avc::Intra4Nb n{};
+    for (int k = 0; k < 9; ++k) n.t[k] = top[size_t(k)];
+    for (int k = 0; k < 4; ++k) n.l[k] = left[size_t(k)];
+    n.has_top = has_top;
+    n.has_left = has_left;
+    std::vector<int> r(16);
+    for (int y = 0; y < 4; ++y)
+      for (int x = 0; x < 4; ++x) r[size_t(y * 4 + x)] = avc::intra4x4_pred(n, mode, x, y);
+    return r;
+  });
+  // top = p[-1..15, -1] (17, top-right substituted), left = p[-1, 0..7]: reference filtering +
+  // prediction
+  rc.def("intra8x8", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, bool has_tl,
+                        int mode) {
+    VEP_CHECK(top.size() == 17 && left.size() == 8, "17 top + 8 left samples");
+    int f[25];
+    avc::intra8x8_filter([&](int x) { return top[size_t(x + 1)]; }, [&](int y) { return left[size_t(y)]; },
+                         has_top, has_left, has_tl, f);
+    std::vector<int> r(64);
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::intra8x8_pred(f, has_top, has_left, mode, x, y);
+    return r;
+  });
+  rc.def("intra16x16", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode) {
+    VEP_CHECK(top.size() == 17 && left.size() == 16, "17 top + 16 left samples");
+    avc::Intra16Nb n{};
+    for (int k = 0; k < 17; ++k) n.top[k] = top[size_t(k)];
+    for (int k = 0; k < 16; ++k) n.left[k] = left[size_t(k)];
+    n.has_top = has_top;
+    n.has_left = has_left;
+    n.has_tl = has_top && has_left;
+    const avc::PredConst k = avc::intra16x16_const(n, mode);
+    std::vector<int> r(256);
+    for (int y = 0; y < 16; ++y)
+      for (int x = 0; x < 16; ++x) r[size_t(y * 16 + x)] = avc::intra16x16_pred(n, k, mode, x, y);
+    return r;
+  });
+  rc.def("intra_chroma", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode) {
+    VEP_CHECK(top.size() == 9 && left.size() == 8, "9 top + 8 left samples");
+    avc::IntraChromaNb n{};
+    for (int k = 0; k < 9; ++k) n.top[k] = top[size_t(k)];
+    for (int k = 0; k < 8; ++k) n.left[k] = left[size_t(k)];
+    n.has_top = has_top;
+    n.has_left = has_left;
+    n.has_tl = has_top && has_left;
+    const avc::PredConst k = mode == 3 ? avc::chroma_plane_const(n) : avc::PredConst{0, 0, 0, 0};
+    std::vector<int> r(64);
+    for (int y = 0; y < 8; ++y)
+      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::chroma_pred(n, k, mode, x, y);
+    return r;
+  });
+  rc.def("luma_qpel", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> plane, int xi, int yi,
+                         int fx, int fy) {
+    VEP_CHECK(plane.ndim() == 2, "2-D plane");
+    const int h = int(plane.shape(0)), w = int(plane.shape(1));
+    return avc::luma_qpel(plane.data(), w, w, h, xi, yi, fx, fy);
+  });
+  rc.def("chroma_epel", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> uv, int c, int xi,
+                           int yi, int fx, int fy) {
+    VEP_CHECK(uv.ndim() == 2 && uv.shape(1) % 2 == 0, "interleaved UV plane");
+    const int h = int(uv.shape(0)), pitch = int(uv.shape(1));
+    return avc::chroma_epel(uv.data(), pitch, pitch / 2, h, c, xi, yi, fx, fy);
+  });
+  rc.def("edge_params", [](int qp_p, int qp_q, int off_a, int off_b) {
+    const avc::EdgeParams e = avc::edge_params(qp_p, qp_q, off_a, off_b);
+    return py::make_tuple(e.alpha, e.beta, std::vector<int>{e.tc0[0], e.tc0[1], e.tc0[2]});
+  });
+  // one sample line across an edge: p = p0..p3, q = q0..q3 -> filtered (p, q)
+  rc.def("filter_line", [](std::vector<int> p, std::vector<int> q, int bs, int alpha, int beta, int tc0,
+                           bool chroma) {
+    VEP_CHECK(p.size() == 4 && q.size() == 4, "4 + 4 samples");
+    avc::filter_samples(p.data(), q.data(), bs, alpha, beta, tc0, chroma);
+    return py::make_tuple(p, q);
+  });
+
   m.def("cavlc_roundtrip", [](int nc, int max_coeff, const std::vector<int>& c) {
     // write_residual_block -> read_residual_block (table self-consistency, tests only)
     VEP_CHECK(int(c.size()) == max_coeff, "coefficient count mismatch");

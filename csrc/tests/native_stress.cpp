@@ -153,10 +153,10 @@ static void rtsp_stress() {
   auto arch = std::make_shared<mux::Archiver>();
   IngestSession sess(w, cam, ic, arch);
   sess.start();
-  for (int i = 0; i < 100 && w.camera(cam)->decoded.load() < 5; ++i) {
+  // the RTMP sender connects and sends on its own thread: also wait for its first messages
+  for (int i = 0; i < 500 && (w.camera(cam)->decoded.load() < 5 || sess.state().rtmp_messages < 3); ++i) {
     w.camera(cam)->last_query_ms.store(now_ms());
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
-    (void)sess.state();
   }
   sess.stop();
   w.flush();
@@ -300,10 +300,9 @@ static void compressed_ingest_stress() {
   auto arch = std::make_shared<mux::Archiver>();
   IngestSession sess(w, cam, ic, arch);
   sess.start();
-  for (int i = 0; i < 200 && w.camera(cam)->decoded.load() < 20; ++i) {
+  for (int i = 0; i < 500 && (w.camera(cam)->decoded.load() < 20 || sess.state().rtmp_messages < 3); ++i) {
     w.camera(cam)->last_query_ms.store(now_ms());
     std::this_thread::sleep_for(std::chrono::milliseconds(20));
-    (void)sess.state();
   }
   sess.stop();
   w.flush();

@@ -759,8 +759,8 @@ VEP_HD int chroma_epel(const u8* uv, int pitch, int w, int h, int c, int xi, int
 
 // ------------------------------------------------------------------------------ deblocking
 // Boundary strength of the edge between 4x4 luma blocks P (in MB mp, raster block bp) and Q (in
-// MB mq, block bq) (§8.7.2.1, frame macroblocks). mv_p / mv_q point at the MBs' motion vector
-// units (list 0 at [0..31], list 1 at [32..63] when kMbL1); nullptr for intra MBs. Reference
+// MB mq, block bq) (§8.7.2.1, frame macroblocks). mv_p / mv_q point at the MBs' vectors in the
+// mv pool (granularity by the MbRec flags, see mv_sub()); unused for intra MBs. Reference
 // pictures are compared by DPB slot (= picture identity within one picture's decode), so a
 // picture reached through list 0 and list 1 counts as the same picture.
 VEP_HD bool mv_far(const i16* a, const i16* b) { return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= 4; }
