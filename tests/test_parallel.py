@@ -108,3 +108,57 @@ def test_parse_threads_split_cpu_budget(monkeypatch):
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 4)
     assert utils.parse_threads_per_rank(8) == 2       # floor
     assert utils.host_cpu_budget.__call__() >= 1
+
+
+def test_hub_consumer_batch_cpu(native, tmp_path):
+    """`vep serve`'s consumer API: every worker letterboxes each published frame into its
+    torch-owned consumer tensor; Hub.consumer_batch() returns the node-wide batch in the
+    requested camera order (rows compared with the fp32 letterbox reference of the camera's
+    latest frame, within rounding)."""
+    import time
+
+    import torch
+
+    from video_edge_ai_proxy_amd.config import Config
+    from video_edge_ai_proxy_amd.engine.hub import Hub
+    from video_edge_ai_proxy_amd.ops import letterbox_reference
+
+    srv = native.RtspServer("127.0.0.1", 0)
+    for i, (w, h) in enumerate([(320, 240), (256, 144)]):
+        c = native.SynthConfig()
+        c.width, c.height, c.gop, c.fps, c.seed = w, h, 10, 30, 3 + i
+        srv.add_stream(f"/c{i}", c, realtime=True, cached_frames=20)
+    srv.start()
+    cfg = Config()
+    cfg.data_dir = str(tmp_path)
+    cfg.gpu.devices = [-1, -1]  # two CPU-backend workers: the multi-worker assembly path
+    cfg.gpu.letterbox_size = 64
+    cfg.gpu.max_cameras_per_gpu = 4
+    hub = Hub(cfg)
+    try:
+        for i in range(2):
+            hub.start_camera(f"c{i}", f"rtsp://127.0.0.1:{srv.port}/c{i}", disk_path="")
+        assert {hub.handle("c0").worker_index, hub.handle("c1").worker_index} == {0, 1}
+        deadline = time.time() + 10
+        while time.time() < deadline:
+            for n in ("c0", "c1"):
+                w, cam = hub.worker_of(n)
+                w.set_last_query(cam, int(time.time() * 1000))
+            if all(hub.worker_of(n)[0].published(hub.worker_of(n)[1]) >= 3 for n in ("c0", "c1")):
+                break
+            time.sleep(0.05)
+        # freeze decoding (no more queries) so the rows and the latest frames stay put
+        for n in ("c0", "c1"):
+            w, cam = hub.worker_of(n)
+            w.set_idle_cutoff_ms(cam, 1)
+        time.sleep(0.3)
+        batch, names = hub.consumer_batch(names=["c1", "c0"])
+        assert names == ["c1", "c0"] and tuple(batch.shape) == (2, 64, 64, 3)
+        for row, n in zip(batch, names):
+            w, cam = hub.worker_of(n)
+            meta, img = w.read_latest(cam, 0)
+            ref, _ = letterbox_reference(torch.from_numpy(img), 64)
+            assert (row.int() - ref.int()).abs().max().item() <= 1, n
+    finally:
+        hub.shutdown()
+        srv.stop()

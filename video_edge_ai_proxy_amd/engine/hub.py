@@ -72,6 +72,20 @@ class Hub:
                               letterbox_format=1 if g.letterbox_format == "nv12" else 0)
             w.start()
             self.workers.append(w)
+        # Consumer batch: with letterbox_size > 0 every worker letterboxes each frame it publishes
+        # into row <camera slot> of a torch-owned tensor on its own GPU; consumer_batch() assembles
+        # the node-wide batch from them.
+        self.consumer: list = []
+        if int(g.letterbox_size) > 0:
+            import torch
+
+            S = int(g.letterbox_size)
+            shape = (S * S * 3 // 2,) if g.letterbox_format == "nv12" else (S, S, 3)
+            for w, d in zip(self.workers, devices):
+                dev = torch.device("cuda", d) if d >= 0 else torch.device("cpu")
+                t = torch.zeros((int(g.max_cameras_per_gpu), *shape), dtype=torch.uint8, device=dev)
+                w.set_consumer_buffers(t.data_ptr(), 0, int(g.max_cameras_per_gpu))
+                self.consumer.append(t)
         self.archiver = native.Archiver()
         self.cameras: dict[str, CameraHandle] = {}
         self._lock = threading.RLock()
@@ -127,6 +141,44 @@ class Hub:
     def worker_of(self, name: str):
         h = self.handle(name)
         return self.workers[h.worker_index], h.cam
+
+    def consumer_batch(self, device=None, names: Optional[list[str]] = None):
+        """Node-wide letterboxed batch of the newest frame of every running camera (or of
+        ``names``, in that order): ``(tensor [N, S, S, 3] uint8 (or NV12 rows), names)`` on
+        ``device`` (default: the first worker's device). Each GPU's rows are gathered from its own
+        consumer tensor and the per-GPU slices are concatenated on the destination with peer
+        copies over xGMI (one process, many GPUs; the multi-process form is
+        ``parallel.ConsumerBatch``, one RCCL all-gather). Rows of cameras that have not published
+        a frame yet are zero."""
+        import torch
+
+        from ..parallel import gather_to_device
+
+        if not self.consumer:
+            raise RuntimeError("consumer batch disabled (gpu.letterbox_size is 0)")
+        with self._lock:
+            order = list(names) if names is not None else sorted(self.cameras)
+            hs = [self.handle(n) for n in order]
+        if device is None:
+            device = self.consumer[0].device
+        # the letterbox kernels of every frame published so far have finished on each GPU
+        for t in self.consumer:
+            if t.is_cuda:
+                torch.cuda.synchronize(t.device)
+        parts, where = [], []
+        for wi, t in enumerate(self.consumer):
+            mine = [(k, h.cam) for k, h in enumerate(hs) if h.worker_index == wi]
+            if not mine:
+                continue
+            idx = torch.tensor([c for _, c in mine], dtype=torch.long, device=t.device)
+            parts.append(t.index_select(0, idx))
+            where += [k for k, _ in mine]
+        if not parts:
+            return torch.zeros((0, *self.consumer[0].shape[1:]), dtype=torch.uint8, device=device), []
+        cat = gather_to_device(parts, torch.device(device))
+        inv = torch.empty(len(where), dtype=torch.long)
+        inv[torch.tensor(where, dtype=torch.long)] = torch.arange(len(where))
+        return cat.index_select(0, inv.to(cat.device)), order
 
     def shutdown(self) -> None:
         for name in list(self.cameras):
