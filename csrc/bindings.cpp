@@ -10,6 +10,7 @@
 #include "vep/codec.h"
 #include "vep/gpu.h"
 #include "vep/h264.h"
+#include "vep/hevc_dec.h"
 #include "bind_ext.h"
 #include "vep/runtime.h"
 #include "vep/synth.h"
@@ -315,6 +316,74 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("last_display_index", &avc::AvcHighEncoder::last_display_index)
       .def_property_readonly("sps_nal", [](const avc::AvcHighEncoder& e) { return to_bytes(e.sps_nal().data(), e.sps_nal().size()); })
       .def_property_readonly("pps_nal", [](const avc::AvcHighEncoder& e) { return to_bytes(e.pps_nal().data(), e.pps_nal().size()); });
+
+  py::class_<hevc::HevcEncConfig>(m, "HevcEncConfig")
+      .def(py::init<>())
+      .def_readwrite("width", &hevc::HevcEncConfig::width)
+      .def_readwrite("height", &hevc::HevcEncConfig::height)
+      .def_readwrite("fps", &hevc::HevcEncConfig::fps)
+      .def_readwrite("gop", &hevc::HevcEncConfig::gop)
+      .def_readwrite("bframes", &hevc::HevcEncConfig::bframes)
+      .def_readwrite("qp", &hevc::HevcEncConfig::qp)
+      .def_readwrite("log2_ctb", &hevc::HevcEncConfig::log2_ctb)
+      .def_readwrite("log2_min_cb", &hevc::HevcEncConfig::log2_min_cb)
+      .def_readwrite("amp", &hevc::HevcEncConfig::amp)
+      .def_readwrite("sao", &hevc::HevcEncConfig::sao)
+      .def_readwrite("deblock", &hevc::HevcEncConfig::deblock)
+      .def_readwrite("tskip", &hevc::HevcEncConfig::tskip)
+      .def_readwrite("sign_hiding", &hevc::HevcEncConfig::sign_hiding)
+      .def_readwrite("cu_qp_delta", &hevc::HevcEncConfig::cu_qp_delta)
+      .def_readwrite("pcm", &hevc::HevcEncConfig::pcm)
+      .def_readwrite("tmvp", &hevc::HevcEncConfig::tmvp)
+      .def_readwrite("slices", &hevc::HevcEncConfig::slices)
+      .def_readwrite("coverage", &hevc::HevcEncConfig::coverage)
+      .def_readwrite("objects", &hevc::HevcEncConfig::objects)
+      .def_readwrite("noise", &hevc::HevcEncConfig::noise)
+      .def_readwrite("temporal_noise", &hevc::HevcEncConfig::temporal_noise)
+      .def_readwrite("seed", &hevc::HevcEncConfig::seed);
+  py::class_<hevc::HevcEncoder>(m, "HevcEncoder")
+      .def(py::init<const hevc::HevcEncConfig&>())
+      .def("next", &hevc::HevcEncoder::next, py::call_guard<py::gil_scoped_release>())
+      .def("picture", [surface_tuple](const hevc::HevcEncoder& e) { return surface_tuple(e.reconstruction()); })
+      .def("source", [surface_tuple](const hevc::HevcEncoder& e) { return surface_tuple(e.source()); })
+      .def_property_readonly("last_pts", &hevc::HevcEncoder::last_pts)
+      .def_property_readonly("last_type", [](const hevc::HevcEncoder& e) { return std::string(1, e.last_type()); })
+      .def_property_readonly("vps_nal", [](const hevc::HevcEncoder& e) { return to_bytes(e.vps_nal().data(), e.vps_nal().size()); })
+      .def_property_readonly("sps_nal", [](const hevc::HevcEncoder& e) { return to_bytes(e.sps_nal().data(), e.sps_nal().size()); })
+      .def_property_readonly("pps_nal", [](const hevc::HevcEncoder& e) { return to_bytes(e.pps_nal().data(), e.pps_nal().size()); });
+  // General H.265 Main decoder (CPU): decode() / flush() return the frames leaving the output
+  // queue as [(pts, poc, type, (Y, UV) coded NV12 planes)] in output order.
+  py::class_<hevc::Decoder>(m, "HevcDecoder")
+      .def(py::init<>())
+      .def("decode",
+           [surface_tuple](hevc::Decoder& d, const AccessUnit& au) {
+             std::vector<hevc::FramePtr> fs;
+             {
+               py::gil_scoped_release nogil;
+               fs = d.decode(au, 0);
+             }
+             py::list l;
+             for (const auto& f : fs) l.append(py::make_tuple(f->pts, f->poc, std::string(1, f->type), surface_tuple(f->s)));
+             return l;
+           })
+      .def("flush",
+           [surface_tuple](hevc::Decoder& d) {
+             py::list l;
+             for (const auto& f : d.flush()) l.append(py::make_tuple(f->pts, f->poc, std::string(1, f->type), surface_tuple(f->s)));
+             return l;
+           })
+      .def_property_readonly("stats", [](const hevc::Decoder& d) {
+        py::dict s;
+        s["intra"] = d.stats.intra;
+        s["inter"] = d.stats.inter;
+        s["skip"] = d.stats.skip;
+        s["pcm"] = d.stats.pcm;
+        s["merge"] = d.stats.merge;
+        s["bi"] = d.stats.bi;
+        s["tskip"] = d.stats.tskip;
+        s["amp"] = d.stats.amp;
+        return s;
+      });
 
   py::class_<CpuDecoder>(m, "CpuDecoder")
       .def(py::init<>())

@@ -292,7 +292,7 @@ Pps parse_pps(const u8* rbsp, size_t n) {
   p.constrained_intra_pred = br.u1();
   p.transform_skip = br.u1();
   p.cu_qp_delta = br.u1();
-  if (p.cu_qp_delta) br.ue();
+  if (p.cu_qp_delta) p.diff_cu_qp_delta_depth = int(br.ue());
   p.cb_qp_offset = br.se();
   p.cr_qp_offset = br.se();
   p.slice_chroma_qp_offsets_present = br.u1();
@@ -317,8 +317,8 @@ Pps parse_pps(const u8* rbsp, size_t n) {
     p.deblocking_override_enabled = br.u1();
     p.deblocking_disabled = br.u1();
     if (!p.deblocking_disabled) {
-      br.se();
-      br.se();
+      p.beta_offset = br.se() * 2;
+      p.tc_offset = br.se() * 2;
     }
   }
   p.scaling_list = br.u1();
@@ -343,7 +343,7 @@ SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const P
   SliceHeader sh;
   sh.nal_type = nal_type(rbsp);
   sh.first_slice_in_pic = br.u1();
-  if (is_irap(sh.nal_type)) br.u1();
+  if (is_irap(sh.nal_type)) sh.no_output_of_prior_pics = br.u1();
   sh.pps_id = int(br.ue());
   if (!sh.first_slice_in_pic) {
     if (pps.dependent_slice_segments) sh.dependent = br.u1();
@@ -371,11 +371,13 @@ SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const P
       VEP_CHECK(idx < nsets, "short_term_ref_pic_set_idx out of range");
       rps = sps.st_rps[size_t(idx)];
     }
+    sh.rps = rps;
     for (int i = 0; i < rps.num_delta(); ++i) num_pic_total_curr += rps.used[i];
     if (sps.long_term_refs) {
       int num_lt_sps = 0;
       if (sps.num_long_term_ref_pics_sps > 0) num_lt_sps = int(br.ue());
       const int num_lt = num_lt_sps + int(br.ue());
+      sh.num_long_term = num_lt;
       for (int i = 0; i < num_lt; ++i) {
         bool used;
         if (i < num_lt_sps) {
@@ -402,19 +404,27 @@ SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const P
       sh.num_ref_idx_l0 = int(br.ue()) + 1;
       if (sh.slice_type == kB) l1 = int(br.ue()) + 1;
     }
+    VEP_CHECK(sh.num_ref_idx_l0 <= 15 && l1 <= 15, "num_ref_idx out of range");
+    sh.num_ref_idx_l1 = sh.slice_type == kB ? l1 : 0;
     if (pps.lists_modification && num_pic_total_curr > 1) {
       const int bits = ceil_log2(num_pic_total_curr);
-      if (br.u1())
-        for (int i = 0; i < sh.num_ref_idx_l0; ++i) br.skip(size_t(bits));
-      if (sh.slice_type == kB && br.u1())
-        for (int i = 0; i < l1; ++i) br.skip(size_t(bits));
+      sh.list_mod[0] = br.u1();
+      if (sh.list_mod[0])
+        for (int i = 0; i < sh.num_ref_idx_l0; ++i) sh.list_entry[0][i] = int(br.u(bits));
+      if (sh.slice_type == kB) {
+        sh.list_mod[1] = br.u1();
+        if (sh.list_mod[1])
+          for (int i = 0; i < l1; ++i) sh.list_entry[1][i] = int(br.u(bits));
+      }
     }
-    if (sh.slice_type == kB) br.u1();  // mvd_l1_zero_flag
+    if (sh.slice_type == kB) sh.mvd_l1_zero = br.u1();
     if (pps.cabac_init_present) sh.cabac_init = br.u1();
     if (sh.temporal_mvp) {
       bool from_l0 = true;
       if (sh.slice_type == kB) from_l0 = br.u1();
-      if ((from_l0 && sh.num_ref_idx_l0 > 1) || (!from_l0 && l1 > 1)) br.ue();
+      sh.collocated_from_l0 = from_l0;
+      if ((from_l0 && sh.num_ref_idx_l0 > 1) || (!from_l0 && l1 > 1)) sh.collocated_ref_idx = int(br.ue());
+      VEP_CHECK(sh.collocated_ref_idx < (from_l0 ? sh.num_ref_idx_l0 : l1), "collocated_ref_idx out of range");
     }
     if ((pps.weighted_pred && sh.slice_type == kP) || (pps.weighted_bipred && sh.slice_type == kB))
       throw Error("weighted prediction is not supported");
@@ -423,20 +433,23 @@ SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const P
   }
   sh.qp_delta = br.se();
   if (pps.slice_chroma_qp_offsets_present) {
-    br.se();
-    br.se();
+    sh.cb_qp_offset = br.se();
+    sh.cr_qp_offset = br.se();
   }
+  sh.beta_offset = pps.beta_offset;
+  sh.tc_offset = pps.tc_offset;
   bool override_flag = false;
   if (pps.deblocking_override_enabled) override_flag = br.u1();
   if (override_flag) {
     sh.deblocking_disabled = br.u1();
     if (!sh.deblocking_disabled) {
-      br.se();
-      br.se();
+      sh.beta_offset = br.se() * 2;
+      sh.tc_offset = br.se() * 2;
     }
   }
+  sh.loop_filter_across_slices = pps.loop_filter_across_slices;
   if (pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled))
-    br.u1();
+    sh.loop_filter_across_slices = br.u1();
   if (pps.tiles || pps.entropy_coding_sync) {
     sh.num_entry_points = int(br.ue());
     if (sh.num_entry_points > 0) {
@@ -570,17 +583,18 @@ std::vector<u8> write_pps(const Pps& p) {
   bw.u1(0);  // dependent_slice_segments
   bw.u1(0);  // output_flag_present
   bw.u(3, 0);
-  bw.u1(0);  // sign_data_hiding
+  bw.u1(p.sign_data_hiding);
   bw.u1(p.cabac_init_present);
   bw.ue(u32(p.num_ref_idx_l0_default - 1));
   bw.ue(u32(p.num_ref_idx_l1_default - 1));
   bw.se(p.init_qp - 26);
-  bw.u1(0);  // constrained_intra_pred
-  bw.u1(0);  // transform_skip
-  bw.u1(0);  // cu_qp_delta
-  bw.se(0);
-  bw.se(0);
-  bw.u1(0);  // slice_chroma_qp_offsets_present
+  bw.u1(p.constrained_intra_pred);
+  bw.u1(p.transform_skip);
+  bw.u1(p.cu_qp_delta);
+  if (p.cu_qp_delta) bw.ue(u32(p.diff_cu_qp_delta_depth));
+  bw.se(p.cb_qp_offset);
+  bw.se(p.cr_qp_offset);
+  bw.u1(p.slice_chroma_qp_offsets_present);
   bw.u1(0);  // weighted_pred
   bw.u1(0);  // weighted_bipred
   bw.u1(0);  // transquant_bypass
@@ -588,11 +602,11 @@ std::vector<u8> write_pps(const Pps& p) {
   bw.u1(0);  // entropy_coding_sync
   bw.u1(p.loop_filter_across_slices);
   bw.u1(1);  // deblocking_filter_control_present
-  bw.u1(0);  // override enabled
+  bw.u1(p.deblocking_override_enabled);
   bw.u1(p.deblocking_disabled);
   if (!p.deblocking_disabled) {
-    bw.se(0);
-    bw.se(0);
+    bw.se(p.beta_offset / 2);
+    bw.se(p.tc_offset / 2);
   }
   bw.u1(0);  // pps_scaling_list_data_present
   bw.u1(0);  // lists_modification_present
@@ -628,6 +642,65 @@ void write_slice_header(BitWriter& bw, const SliceHeader& sh, const Sps& sps, co
   }
   bw.se(sh.qp_delta);
   if (pps.loop_filter_across_slices && !pps.deblocking_disabled) bw.u1(0);
+  bw.u1(1);  // byte_alignment()
+  bw.align_zero();
+}
+
+void write_slice_header_full(BitWriter& bw, const SliceHeader& sh, const Sps& sps, const Pps& pps) {
+  for (u8 b : nal_header(sh.nal_type)) bw.u(8, b);
+  bw.u1(sh.first_slice_in_pic);
+  if (is_irap(sh.nal_type)) bw.u1(sh.no_output_of_prior_pics);
+  bw.ue(u32(sh.pps_id));
+  if (!sh.first_slice_in_pic)
+    bw.u(ceil_log2(sps.width_ctbs() * sps.height_ctbs()), u32(sh.segment_address));
+  bw.ue(u32(sh.slice_type));
+  if (!is_idr(sh.nal_type)) {
+    bw.u(sps.log2_max_poc_lsb, u32(sh.poc_lsb) & ((1u << sps.log2_max_poc_lsb) - 1));
+    bw.u1(0);  // short_term_ref_pic_set_sps_flag: the RPS is coded in the header
+    write_st_rps(bw, int(sps.st_rps.size()), sh.rps);
+    if (sps.temporal_mvp) bw.u1(sh.temporal_mvp);
+  }
+  if (sps.sao) {
+    bw.u1(sh.sao_luma);
+    bw.u1(sh.sao_chroma);
+  }
+  if (sh.slice_type != kI) {
+    const bool override_refs = sh.num_ref_idx_l0 != pps.num_ref_idx_l0_default ||
+                               (sh.slice_type == kB && sh.num_ref_idx_l1 != pps.num_ref_idx_l1_default);
+    bw.u1(override_refs);
+    if (override_refs) {
+      bw.ue(u32(sh.num_ref_idx_l0 - 1));
+      if (sh.slice_type == kB) bw.ue(u32(sh.num_ref_idx_l1 - 1));
+    }
+    if (sh.slice_type == kB) bw.u1(sh.mvd_l1_zero);
+    if (pps.cabac_init_present) bw.u1(sh.cabac_init);
+    if (sh.temporal_mvp) {
+      if (sh.slice_type == kB) bw.u1(sh.collocated_from_l0);
+      const int n = sh.collocated_from_l0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+      if (n > 1) bw.ue(u32(sh.collocated_ref_idx));
+    }
+    bw.ue(u32(5 - sh.max_num_merge_cand));
+  }
+  bw.se(sh.qp_delta);
+  if (pps.slice_chroma_qp_offsets_present) {
+    bw.se(sh.cb_qp_offset);
+    bw.se(sh.cr_qp_offset);
+  }
+  bool override_flag = false;
+  if (pps.deblocking_override_enabled) {
+    override_flag = sh.deblocking_disabled != pps.deblocking_disabled || sh.beta_offset != pps.beta_offset ||
+                    sh.tc_offset != pps.tc_offset;
+    bw.u1(override_flag);
+  }
+  if (override_flag) {
+    bw.u1(sh.deblocking_disabled);
+    if (!sh.deblocking_disabled) {
+      bw.se(sh.beta_offset / 2);
+      bw.se(sh.tc_offset / 2);
+    }
+  }
+  if (pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled))
+    bw.u1(sh.loop_filter_across_slices);
   bw.u1(1);  // byte_alignment()
   bw.align_zero();
 }

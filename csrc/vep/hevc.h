@@ -107,6 +107,8 @@ struct Pps {
   int num_ref_idx_l0_default = 1, num_ref_idx_l1_default = 1;
   int init_qp = 26;
   bool constrained_intra_pred = false, transform_skip = false, cu_qp_delta = false;
+  int diff_cu_qp_delta_depth = 0;
+  int beta_offset = 0, tc_offset = 0;        // pps_{beta,tc}_offset_div2 * 2
   int cb_qp_offset = 0, cr_qp_offset = 0;
   bool slice_chroma_qp_offsets_present = false;
   bool weighted_pred = false, weighted_bipred = false, transquant_bypass = false;
@@ -123,16 +125,27 @@ enum SliceType : int { kB = 0, kP = 1, kI = 2 };
 struct SliceHeader {
   int nal_type = 0;
   bool first_slice_in_pic = true;
+  bool no_output_of_prior_pics = false;
   int pps_id = 0;
   bool dependent = false;
   int segment_address = 0;                   // CTB raster address
   int slice_type = kI;
   int poc_lsb = 0;
-  int num_ref_idx_l0 = 1;
+  ShortTermRps rps;                          // the picture's short-term RPS (non-IDR)
+  int num_long_term = 0;                     // long-term entries (rejected by the decoder)
+  int num_ref_idx_l0 = 1, num_ref_idx_l1 = 1;
+  bool list_mod[2] = {false, false};
+  int list_entry[2][16] = {};                // ref_pic_list_modification entries
+  bool mvd_l1_zero = false;
   bool cabac_init = false;
+  bool collocated_from_l0 = true;
+  int collocated_ref_idx = 0;
   int max_num_merge_cand = 5;
   int qp_delta = 0;
+  int cb_qp_offset = 0, cr_qp_offset = 0;
   bool deblocking_disabled = true;
+  int beta_offset = 0, tc_offset = 0;        // slice_{beta,tc}_offset_div2 * 2
+  bool loop_filter_across_slices = false;
   bool sao_luma = false, sao_chroma = false;
   bool temporal_mvp = false;
   int num_entry_points = 0;
@@ -154,6 +167,9 @@ std::vector<u8> write_sps(const Sps& s);
 std::vector<u8> write_pps(const Pps& p);
 // Writes the slice segment header through byte_alignment(); CABAC data follows.
 void write_slice_header(BitWriter& bw, const SliceHeader& sh, const Sps& sps, const Pps& pps);
+// General form (any slice type, explicit short-term RPS, SAO / reference / deblocking fields)
+// for the closed-loop Main encoder.
+void write_slice_header_full(BitWriter& bw, const SliceHeader& sh, const Sps& sps, const Pps& pps);
 std::vector<u8> nal_header(int type, int tid_plus1 = 1);
 
 // HEVCDecoderConfigurationRecord from escaped VPS/SPS/PPS NALs (MP4 hvcC, enhanced-RTMP).

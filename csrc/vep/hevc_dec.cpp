@@ -1,0 +1,289 @@
+// General H.265 Main decoder: parameter sets, picture order count (§8.3.1), reference picture
+// set marking (§8.3.2), reference list construction (§8.3.4), slice decoding through the CTU
+// layer (hevc_ctu.cpp), the in-loop filters and output in POC order with the bumping process of
+// C.5.2. See hevc_dec.h for the supported feature set.
+#include <algorithm>
+
+#include "bits.h"
+#include "hevc_ctu.h"
+#include "hevc_recon.h"
+
+namespace vep::hevc {
+
+namespace {
+bool is_rasl(int t) { return t == 8 || t == 9; }
+bool is_radl(int t) { return t == 6 || t == 7; }
+bool is_sub_layer_non_ref(int t) { return t <= 14 && (t % 2) == 0; }
+bool is_bla(int t) { return t >= 16 && t <= 18; }
+
+void check_supported(const Sps& sps, const Pps& pps) {
+  if (sps.chroma_format_idc != 1 || sps.separate_colour_plane) throw UnsupportedStream("HEVC: only 4:2:0 is supported");
+  if (sps.bit_depth_luma != 8 || sps.bit_depth_chroma != 8) throw UnsupportedStream("HEVC: only 8-bit (Main) is supported");
+  if (sps.scaling_list || pps.scaling_list) throw UnsupportedStream("HEVC: scaling lists are not supported");
+  if (pps.tiles || pps.entropy_coding_sync) throw UnsupportedStream("HEVC: tiles / wavefront entry points are not supported");
+  if (pps.transquant_bypass) throw UnsupportedStream("HEVC: transquant bypass is not supported");
+  if (pps.weighted_pred || pps.weighted_bipred) throw UnsupportedStream("HEVC: weighted prediction is not supported");
+  if (sps.pcm && (sps.pcm_bit_depth_luma != 8 || sps.pcm_bit_depth_chroma != 8))
+    throw UnsupportedStream("HEVC: PCM bit depth below 8 is not supported");
+  VEP_CHECK(sps.width > 0 && sps.height > 0 && sps.width % (1 << sps.log2_min_cb) == 0 &&
+                sps.height % (1 << sps.log2_min_cb) == 0,
+            "HEVC: picture size must be a multiple of the minimum CU");
+  VEP_CHECK(sps.log2_ctb >= 4 && sps.log2_ctb <= 6 && sps.log2_min_cb >= 3 && sps.log2_min_cb <= sps.log2_ctb,
+            "HEVC: CTB / CU sizes out of range");
+  VEP_CHECK(sps.log2_min_tb >= 2 && sps.log2_max_tb <= 5 && sps.log2_min_tb < sps.log2_min_cb &&
+                sps.log2_max_tb <= sps.log2_ctb,
+            "HEVC: transform sizes out of range");
+}
+}  // namespace
+
+Decoder::Decoder() : pc_(std::make_unique<PicCtx>()) {}
+Decoder::~Decoder() = default;
+
+void Decoder::bump(std::vector<FramePtr>& out) {
+  FramePtr best;
+  for (const FramePtr& f : dpb_)
+    if (f->needed_for_output && (!best || f->poc < best->poc)) best = f;
+  if (!best) return;
+  best->needed_for_output = false;
+  out.push_back(best);
+  dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const FramePtr& f) { return !f->is_ref && !f->needed_for_output; }),
+             dpb_.end());
+}
+
+void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, const Pps& pps, const AccessUnit& au,
+                            i64 tag, std::vector<FramePtr>& out) {
+  check_supported(sps, pps);
+  const int t = sh.nal_type;
+  const bool irap = is_irap(t);
+  if (irap) no_rasl_output_ = is_idr(t) || is_bla(t) || first_;
+  skip_pic_ = false;
+  if (is_rasl(t) && no_rasl_output_) {  // leading pictures of a CRA we started at: not decodable
+    skip_pic_ = true;
+    return;
+  }
+  if (sh.num_long_term > 0) throw UnsupportedStream("HEVC: long-term reference pictures are not supported");
+  // picture order count (§8.3.1)
+  const int max_lsb = 1 << sps.log2_max_poc_lsb;
+  int msb = 0;
+  if (!(irap && no_rasl_output_)) {
+    const int prev_lsb = prev_tid0_poc_ & (max_lsb - 1);
+    const int prev_msb = prev_tid0_poc_ - prev_lsb;
+    if (sh.poc_lsb < prev_lsb && prev_lsb - sh.poc_lsb >= max_lsb / 2) msb = prev_msb + max_lsb;
+    else if (sh.poc_lsb > prev_lsb && sh.poc_lsb - prev_lsb > max_lsb / 2) msb = prev_msb - max_lsb;
+    else msb = prev_msb;
+  }
+  const int poc = msb + (is_idr(t) ? 0 : sh.poc_lsb);
+  if (tid == 0 && !is_rasl(t) && !is_radl(t) && !is_sub_layer_non_ref(t)) prev_tid0_poc_ = poc;
+  // reference picture set (§8.3.2)
+  st_before_.clear();
+  st_after_.clear();
+  if (is_idr(t)) {
+    for (FramePtr& f : dpb_) f->is_ref = false;
+  } else {
+    std::vector<FramePtr> keep;
+    const ShortTermRps& r = sh.rps;
+    for (int i = 0; i < r.num_delta(); ++i) {
+      FramePtr hit;
+      for (const FramePtr& f : dpb_)
+        if (f->is_ref && f->poc == poc + r.delta_poc[i]) hit = f;
+      if (hit) keep.push_back(hit);
+      if (!r.used[i]) continue;
+      if (!hit) {
+        if (irap && no_rasl_output_) continue;  // (CRA / BLA start: references are not needed)
+        throw Error("HEVC: missing reference picture (poc " + std::to_string(poc + r.delta_poc[i]) + ")");
+      }
+      (i < r.num_negative ? st_before_ : st_after_).push_back(hit);
+    }
+    for (FramePtr& f : dpb_)
+      if (std::find(keep.begin(), keep.end(), f) == keep.end()) f->is_ref = false;
+  }
+  // output and removal of pictures from the DPB (C.5.2.2)
+  if (irap && no_rasl_output_ && !first_) {
+    if (!sh.no_output_of_prior_pics) {
+      while (true) {
+        const size_t before = out.size();
+        bump(out);
+        if (out.size() == before) break;
+      }
+    }
+    dpb_.clear();
+  } else {
+    dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const FramePtr& f) { return !f->is_ref && !f->needed_for_output; }),
+               dpb_.end());
+    while (true) {
+      int waiting = 0;
+      bool late = false;
+      const int max_latency = sps.max_latency_increase_plus1 ? sps.max_num_reorder + sps.max_latency_increase_plus1 - 1 : 0;
+      for (const FramePtr& f : dpb_)
+        if (f->needed_for_output) {
+          ++waiting;
+          if (sps.max_latency_increase_plus1 && f->latency >= max_latency) late = true;
+        }
+      if (!(waiting > sps.max_num_reorder || late || int(dpb_.size()) >= sps.max_dec_pic_buffering) || !waiting) break;
+      bump(out);
+    }
+  }
+  first_ = false;
+  // the new picture
+  cur_ = std::make_shared<HevcFrame>();
+  cur_->s.alloc(sps.width, sps.height);
+  cur_->poc = poc;
+  cur_->uid = next_uid_++;
+  cur_->pts = au.pts;
+  cur_->dts = au.dts;
+  cur_->tag = tag;
+  cur_->keyframe = irap;
+  cur_->type = sh.pict_char();
+  cur_->width = sps.out_width();
+  cur_->height = sps.out_height();
+  cur_->crop_left = sps.conf_left;
+  cur_->crop_top = sps.conf_top;
+  sps_act_ = &sps;
+  pps_act_ = &pps;
+  pc_->init(sps, pps, &cur_->s);
+  pc_->poc = poc;
+}
+
+void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
+  SliceInfo si;
+  si.sh = sh;
+  si.qp = pps_act_->init_qp + sh.qp_delta;
+  VEP_CHECK(si.qp >= 0 && si.qp <= 51, "HEVC: slice QP out of range");
+  if (sh.slice_type != kI) {
+    std::vector<FramePtr> all = st_before_;
+    all.insert(all.end(), st_after_.begin(), st_after_.end());
+    const int total = int(all.size());
+    VEP_CHECK(total > 0, "HEVC: inter slice without reference pictures");
+    for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
+      std::vector<FramePtr> temp;
+      const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+      const std::vector<FramePtr>& a = l == 0 ? st_before_ : st_after_;
+      const std::vector<FramePtr>& b = l == 0 ? st_after_ : st_before_;
+      while (int(temp.size()) < std::max(nref, total)) {
+        for (const FramePtr& f : a) temp.push_back(f);
+        for (const FramePtr& f : b) temp.push_back(f);
+      }
+      for (int i = 0; i < nref; ++i) {
+        const int e = sh.list_mod[l] ? sh.list_entry[l][i] : i;
+        VEP_CHECK(e < int(temp.size()), "HEVC: list_entry out of range");
+        si.list[l].push_back(temp[size_t(e)]);
+        si.list_poc[l].push_back(temp[size_t(e)]->poc);
+      }
+    }
+  }
+  if (!sh.first_slice_in_pic) {
+    const int prev_end = pc_->slices.empty() ? 0 : 1;
+    VEP_CHECK(prev_end, "HEVC: slice segment before the first slice of the picture");
+    VEP_CHECK(pc_->slice[size_t(sh.segment_address)] == 0xFFFF, "HEVC: slice segment overlaps decoded CTUs");
+  }
+  pc_->slices.push_back(std::move(si));
+  decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
+}
+
+void Decoder::finish_picture(std::vector<FramePtr>& out) {
+  FramePtr f = cur_;
+  cur_ = nullptr;
+  for (int k = 0; k < pc_->wctb * pc_->hctb; ++k)
+    VEP_CHECK(pc_->slice[size_t(k)] != 0xFFFF, "HEVC: picture has undecoded CTUs");
+  bool deblock = false, sao = false;
+  for (const SliceInfo& s : pc_->slices) {
+    deblock |= !s.sh.deblocking_disabled;
+    sao |= s.sh.sao_luma || s.sh.sao_chroma;
+  }
+  if (deblock) deblock_picture(*pc_);
+  if (sao) sao_picture(*pc_);
+  if (sps_act_->temporal_mvp) f->col = build_col(*pc_, f->col_w);
+  stats = pc_->stats;
+  // C.5.2.3: the current picture is a short-term reference and waits for output
+  for (FramePtr& d : dpb_)
+    if (d->needed_for_output) ++d->latency;
+  f->is_ref = true;
+  f->needed_for_output = true;
+  f->latency = 0;
+  dpb_.push_back(f);
+  last_ = f;
+  const Sps& sps = *sps_act_;
+  const int max_latency = sps.max_latency_increase_plus1 ? sps.max_num_reorder + sps.max_latency_increase_plus1 - 1 : 0;
+  while (true) {
+    int waiting = 0;
+    bool late = false;
+    for (const FramePtr& d : dpb_)
+      if (d->needed_for_output) {
+        ++waiting;
+        if (sps.max_latency_increase_plus1 && d->latency >= max_latency) late = true;
+      }
+    if (!waiting || !(waiting > sps.max_num_reorder || late)) break;
+    bump(out);
+  }
+}
+
+std::vector<FramePtr> Decoder::decode(const AccessUnit& au, i64 tag) {
+  std::vector<FramePtr> out;
+  for (size_t i = 0; i < au.nals.size(); ++i) {
+    const u8* p = au.nal(i);
+    const size_t n = au.nal_size(i);
+    if (n < 2) continue;
+    const int t = nal_type(p);
+    const int tid = (p[1] & 7) - 1;
+    if (t == 36 || t == 37) {  // end of sequence / bitstream: the next IRAP starts afresh
+      if (cur_) finish_picture(out);
+      first_ = true;
+      continue;
+    }
+    if (!(t < 22 || (t >= kVps && t <= kPps))) continue;  // AUD, SEI, reserved
+    if (t < 22 && t > 9 && t < 16) continue;              // reserved VCL types
+    rbsp_.resize(n);
+    const size_t rn = ebsp_to_rbsp(p, n, rbsp_.data());
+    if (t == kVps) {
+      Vps v = parse_vps(rbsp_.data(), rn);
+      vps_[v.vps_id] = v;
+      continue;
+    }
+    if (t == kSps) {
+      Sps s = parse_sps(rbsp_.data(), rn);
+      sps_[s.sps_id] = std::move(s);
+      continue;
+    }
+    if (t == kPps) {
+      Pps q = parse_pps(rbsp_.data(), rn);
+      pps_[q.pps_id] = q;
+      continue;
+    }
+    const int pps_id = peek_slice_pps_id(rbsp_.data(), rn);
+    auto pit = pps_.find(pps_id);
+    if (pit == pps_.end()) throw Error("HEVC: slice refers to a missing PPS");
+    auto sit = sps_.find(pit->second.sps_id);
+    if (sit == sps_.end()) throw Error("HEVC: PPS refers to a missing SPS");
+    const SliceHeader sh = parse_slice_header(rbsp_.data(), rn, sit->second, pit->second);
+    try {
+      if (sh.first_slice_in_pic) {
+        if (cur_) finish_picture(out);
+        start_picture(sh, tid, sit->second, pit->second, au, tag, out);
+      } else if (!cur_ && !skip_pic_) {
+        throw Error("HEVC: slice segment without the start of its picture");
+      }
+      if (skip_pic_) continue;
+      decode_slice(sh, rbsp_.data(), rn);
+    } catch (...) {
+      cur_ = nullptr;  // the damaged picture is dropped
+      throw;
+    }
+  }
+  if (cur_) finish_picture(out);
+  return out;
+}
+
+std::vector<FramePtr> Decoder::flush() {
+  std::vector<FramePtr> out;
+  if (cur_) finish_picture(out);
+  while (true) {
+    const size_t before = out.size();
+    bump(out);
+    if (out.size() == before) break;
+  }
+  dpb_.clear();
+  first_ = true;
+  return out;
+}
+
+}  // namespace vep::hevc

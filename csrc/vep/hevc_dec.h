@@ -1,0 +1,166 @@
+// General H.265/HEVC Main-profile decoder (8-bit 4:2:0, progressive): I, P and B slices with
+// CABAC coding quadtrees (CTB 16..64, CU 8..64, all partition modes incl. AMP), intra prediction
+// (35 modes, reference substitution / smoothing, strong intra smoothing), PCM, transform trees
+// (4..32 DCT, 4x4 DST, transform skip, sign data hiding, cu_qp_delta), merge / AMVP with
+// temporal motion-vector prediction, 8-tap / 4-tap motion compensation with bi-prediction,
+// the deblocking filter and SAO; short-term reference picture sets and output in POC order.
+//
+// Split of work: one `CtuLayer` walks the CTU syntax and reconstructs as it goes (intra
+// prediction needs the reconstructed neighbours), in read mode for the decoder and in write
+// mode for the closed-loop synthetic encoder (hevc_enc.cpp), so both share the binarizations,
+// the context selection, the candidate derivations and the reconstruction; the loop filters run
+// over the finished picture. This is the CPU reference of the H.265 path (bit-exact oracle for
+// GPU reconstruction kernels); streams using tiles, wavefront entry points, long-term
+// references, weighted prediction, scaling lists, transquant bypass or range extensions are
+// reported as UnsupportedStream.
+//
+// Reference parity: libavcodec's hevc decoder behind PyAV (python/read_image.py:87
+// `p.decode()`), BASELINE config 5 (H.265 cameras). No third-party HEVC stream exists in this
+// image: conformance beyond the closed loop and the spec oracle tests is unpinned.
+#pragma once
+
+#include <functional>
+#include <map>
+#include <memory>
+
+#include "codec.h"
+#include "hevc.h"
+#include "hevc_tables.h"
+
+namespace vep::hevc {
+
+// Motion of one 4x4 block (also the TMVP store of a reference picture, at 16x16 granularity).
+struct MvField {
+  i16 mv[2][2] = {{0, 0}, {0, 0}};
+  i8 ref[2] = {-1, -1};  // refIdx per list (-1: list unused)
+  u8 pred = 0;           // bit 0 list 0, bit 1 list 1; 0 = intra / not available
+};
+
+struct ColMv {  // a reference picture's motion as seen by TMVP
+  i16 mv[2][2];
+  i32 poc[2];    // POC of the picture each list's vector points at
+  u8 pred;       // 0 = intra
+};
+
+// A decoded picture.
+struct HevcFrame {
+  HostSurface s;
+  int poc = 0;
+  bool is_ref = false, needed_for_output = false;
+  u32 uid = 0;
+  i64 pts = 0, dts = 0, tag = 0;
+  bool keyframe = false;
+  char type = 'I';
+  std::shared_ptr<std::vector<ColMv>> col;  // 16x16 grid
+  int col_w = 0;
+  int width = 0, height = 0, crop_left = 0, crop_top = 0;  // conformance window (output size)
+  int latency = 0;                                          // (output bumping, C.5.2.3)
+};
+using FramePtr = std::shared_ptr<HevcFrame>;
+
+// Encoder side of the CTU layer: the decisions of one coding unit. Residual levels are asked
+// for once the prediction of each transform block is known (`residual`).
+struct CuDesc {
+  bool skip = false;
+  bool intra = false;
+  int part = 0;               // PartMode: 0 2Nx2N 1 2NxN 2 Nx2N 3 NxN 4 2NxnU 5 2NxnD 6 nLx2N 7 nRx2N
+  bool pcm = false;
+  const u8* pcm_samples = nullptr;  // (2N)^2 luma then 2 * N^2 chroma
+  int luma_mode[4] = {1, 1, 1, 1};  // IntraPredModeY per partition
+  int chroma_mode = 4;              // intra_chroma_pred_mode (4 = DM)
+  struct Pu {
+    bool merge = false;
+    int merge_idx = 0;
+    int dir = 1;              // 1 L0, 2 L1, 3 bi
+    int ref[2] = {0, 0};
+    int mvp[2] = {0, 0};      // mvp_lX_flag
+    i16 mv[2][2] = {{0, 0}, {0, 0}};  // wanted vectors (mvd = mv - predictor)
+  } pu[4];
+  int tu_log2 = 5;            // split the transform tree down to this size (clamped to limits)
+  int qp_delta = 0;
+  bool tskip = false;         // transform_skip_flag for 4x4 TUs
+};
+
+// Supplies levels for one transform block in write mode: `pred` is the prediction (stride
+// `pstride`), `src` the source samples, the levels go to `lv` (raster n x n). Returns whether the
+// block is coded with transform skip (4x4 only).
+using ResidualFn = std::function<void(int c, int x0, int y0, int log2, const u8* pred, int pstride, int qp,
+                                      bool tskip_allowed, bool intra, int* lv, bool& tskip)>;
+
+struct PicCtx;
+
+class Decoder {
+ public:
+  Decoder();
+  ~Decoder();
+  // Parse + reconstruct one access unit. Returns the frames that leave the output queue (POC
+  // order), possibly none; throws UnsupportedStream / Error.
+  std::vector<FramePtr> decode(const AccessUnit& au, i64 tag = 0);
+  std::vector<FramePtr> flush();  // end of stream
+  bool has_sps() const { return !sps_.empty(); }
+  FramePtr last_decoded() const { return last_; }
+  // statistics of the last picture (tests): CU counts by kind
+  struct Stats {
+    int intra = 0, inter = 0, skip = 0, pcm = 0, merge = 0, bi = 0, tskip = 0, amp = 0;
+  } stats;
+
+ private:
+  void start_picture(const SliceHeader& sh, int tid, const Sps& sps, const Pps& pps, const AccessUnit& au, i64 tag,
+                     std::vector<FramePtr>& out);
+  void finish_picture(std::vector<FramePtr>& out);
+  void bump(std::vector<FramePtr>& out);
+  void decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n);
+  std::map<int, Vps> vps_;
+  std::map<int, Sps> sps_;
+  std::map<int, Pps> pps_;
+  std::vector<FramePtr> dpb_;
+  FramePtr cur_, last_;
+  std::vector<FramePtr> st_before_, st_after_;  // RefPicSetStCurrBefore / After of the picture
+  std::unique_ptr<PicCtx> pc_;
+  const Sps* sps_act_ = nullptr;
+  const Pps* pps_act_ = nullptr;
+  std::vector<u8> rbsp_;
+  int prev_tid0_poc_ = 0;
+  bool first_ = true, no_rasl_output_ = true, skip_pic_ = false;
+  u32 next_uid_ = 1;
+};
+
+// Closed-loop synthetic HEVC Main encoder (tests, camera farm): I / P / B pictures over the
+// shared CTU layer; `coverage` randomises every decision (all CU sizes, partition modes incl.
+// AMP, intra modes, merge candidates, AMVP, bi-prediction, transform trees, transform skip, PCM,
+// QP deltas, SAO types), otherwise decisions come from a simple SAD search on the synthetic
+// scene.
+struct HevcEncConfig {
+  int width = 416, height = 240;
+  int fps = 30, gop = 16;
+  int bframes = 0;           // B pictures between anchors (0 = IPPP)
+  int qp = 30;
+  int log2_ctb = 5, log2_min_cb = 3;
+  bool amp = true, sao = true, deblock = true, tskip = true, sign_hiding = true, cu_qp_delta = true;
+  bool pcm = true, tmvp = true;
+  int slices = 1;
+  bool coverage = false;
+  int objects = 3;
+  double noise = 3.0, temporal_noise = 0.0;
+  u64 seed = 1;
+};
+
+class HevcEncoder {
+ public:
+  explicit HevcEncoder(const HevcEncConfig& cfg);
+  ~HevcEncoder();
+  std::shared_ptr<AccessUnit> next();
+  const HostSurface& reconstruction() const;
+  const HostSurface& source() const;
+  i64 last_pts() const;
+  char last_type() const;
+  const std::vector<u8>& vps_nal() const;
+  const std::vector<u8>& sps_nal() const;
+  const std::vector<u8>& pps_nal() const;
+
+ private:
+  struct Impl;
+  std::unique_ptr<Impl> p_;
+};
+
+}  // namespace vep::hevc

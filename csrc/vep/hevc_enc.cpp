@@ -1,0 +1,541 @@
+// Closed-loop synthetic H.265 Main encoder over the shared CTU layer (hevc_ctu.cpp, write mode):
+// the layer writes the CABAC syntax for the decisions made here and reconstructs exactly like
+// the decoder, so the decoder must reproduce `reconstruction()` bit for bit.
+//
+// Two decision modes: `coverage` randomises every decision the syntax allows (CU / TU trees,
+// all partition modes incl. AMP, the 35 intra modes and 5 chroma modes, PCM, merge indices, AMVP
+// predictors and vectors, bi-prediction, transform skip, QP deltas, SAO types and offsets,
+// per-slice deblocking / SAO / CABAC-init / merge-list settings), which is what the round-trip
+// tests run; otherwise a simple camera encoder (16x16 CUs, SAD motion search seeded with the
+// scene's object motion, skip / merge / AMVP / intra choice) for the synthetic camera farm.
+#include <cmath>
+#include <deque>
+
+#include "avc_scene.h"
+#include "bits.h"
+#include "hevc_ctu.h"
+#include "hevc_recon.h"
+
+namespace vep::hevc {
+
+namespace {
+
+using avc::Rng;
+using avc::Scene;
+using avc::SceneConfig;
+
+// Orthonormal basis rows of the n-point transform used by the encoder's forward transform.
+struct Basis {
+  double u[32][32];
+};
+const Basis& dct_basis(int log2) {
+  static Basis b[4];
+  static bool init = false;
+  if (!init) {
+    for (int l = 0; l < 4; ++l) {
+      const int n = 4 << l, step = 32 / n;
+      const double s = 1.0 / (64.0 * std::sqrt(double(n)));
+      for (int k = 0; k < n; ++k)
+        for (int j = 0; j < n; ++j) b[l].u[k][j] = kDct.m[k * step][j] * s;
+    }
+    init = true;
+  }
+  return b[log2 - 2];
+}
+
+// Forward transform + dead-zone quantisation (level = C / Qstep, Qstep = 2^((qp - 4) / 6)).
+void quantise(const int* res, int log2, bool dst, bool tskip, int qp, bool intra, int* lv) {
+  const int n = 1 << log2;
+  const double qstep = std::pow(2.0, (qp - 4) / 6.0);
+  const double f = intra ? 1.0 / 3 : 1.0 / 6;
+  std::vector<double> c(size_t(n) * n);
+  if (tskip) {
+    for (int k = 0; k < n * n; ++k) c[size_t(k)] = res[k];
+  } else {
+    double u[32][32];
+    if (dst) {
+      for (int k = 0; k < 4; ++k)
+        for (int j = 0; j < 4; ++j) u[k][j] = kDst4[k][j] / 128.0;
+    } else {
+      const Basis& b = dct_basis(log2);
+      for (int k = 0; k < n; ++k)
+        for (int j = 0; j < n; ++j) u[k][j] = b.u[k][j];
+    }
+    std::vector<double> t(size_t(n) * n);
+    for (int k = 0; k < n; ++k)  // t = U R (columns)
+      for (int x = 0; x < n; ++x) {
+        double a = 0;
+        for (int y = 0; y < n; ++y) a += u[k][y] * res[y * n + x];
+        t[size_t(k) * n + x] = a;
+      }
+    for (int k = 0; k < n; ++k)  // C = t U^T (rows: vertical frequency k, horizontal m)
+      for (int m = 0; m < n; ++m) {
+        double a = 0;
+        for (int x = 0; x < n; ++x) a += t[size_t(k) * n + x] * u[m][x];
+        c[size_t(k) * n + m] = a;
+      }
+  }
+  for (int k = 0; k < n * n; ++k) {
+    const double a = std::fabs(c[size_t(k)]) / qstep + f;
+    int l = int(std::min(a, 32767.0));
+    lv[k] = c[size_t(k)] < 0 ? -l : l;
+  }
+}
+
+}  // namespace
+
+struct HevcEncoder::Impl : CtuDecider {
+  HevcEncConfig cfg;
+  Rng rng;
+  Scene scene;
+  Vps vps;
+  Sps sps;
+  Pps pps;
+  std::vector<u8> vps_nal, sps_nal, pps_nal;
+  int W = 0, H = 0;  // coded size
+  struct Job {
+    i64 disp;
+    int type;
+    bool ref, idr;
+  };
+  std::deque<Job> plan;
+  std::map<i64, HostSurface> sources;
+  i64 next_disp = 0, rendered = -1, coded = 0, idr_disp = 0;
+  std::vector<FramePtr> anchors;  // kept reference pictures (coding order)
+  int keep_refs = 2;
+  PicCtx pc;
+  FramePtr cur;
+  const HostSurface* cur_src = nullptr;
+  int cur_slice = 0, cur_type = kI, cur_qp = 30;
+  i64 last_pts = 0;
+  char last_type = 'I';
+  HostSurface recon_out, src_out;
+  std::vector<u8> pcm_buf;
+
+  explicit Impl(const HevcEncConfig& c) : cfg(c), rng{c.seed * 0x9E3779B97F4A7C15ull + 4242} {
+    VEP_CHECK(c.width >= 16 && c.height >= 16 && c.width % 2 == 0 && c.height % 2 == 0,
+              "encoder size must be even and >= 16");
+    VEP_CHECK(c.log2_ctb >= 4 && c.log2_ctb <= 6 && c.log2_min_cb == 3, "log2_ctb 4..6, log2_min_cb 3");
+    VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
+    W = (c.width + 7) & ~7;
+    H = (c.height + 7) & ~7;
+    const bool cov = c.coverage;
+    sps.width = W;
+    sps.height = H;
+    sps.conf_right = W - c.width;
+    sps.conf_bottom = H - c.height;
+    sps.log2_max_poc_lsb = 8;
+    sps.log2_ctb = c.log2_ctb;
+    sps.log2_min_cb = 3;
+    sps.log2_min_tb = 2;
+    sps.log2_max_tb = std::min(5, c.log2_ctb);
+    sps.max_th_depth_inter = cov ? rng.uni(4) : 1;
+    sps.max_th_depth_intra = cov ? rng.uni(4) : 1;
+    sps.amp = c.amp;
+    sps.sao = c.sao;
+    sps.pcm = c.pcm;
+    sps.log2_min_pcm = 3;
+    sps.log2_max_pcm = std::min(5, c.log2_ctb);
+    sps.pcm_loop_filter_disabled = cov ? rng.chance(50) : true;
+    sps.temporal_mvp = c.tmvp;
+    sps.strong_intra_smoothing = true;
+    keep_refs = 2;
+    sps.max_dec_pic_buffering = keep_refs + 2;
+    sps.max_num_reorder = c.bframes > 0 ? 1 : 0;
+    sps.vui = true;
+    sps.timing_info = true;
+    sps.num_units_in_tick = 1;
+    sps.time_scale = u32(c.fps);
+    vps.timing_info = true;
+    vps.num_units_in_tick = 1;
+    vps.time_scale = u32(c.fps);
+    pps.sign_data_hiding = c.sign_hiding;
+    pps.cabac_init_present = true;
+    pps.init_qp = c.qp;
+    pps.constrained_intra_pred = cov ? rng.chance(30) : false;
+    pps.transform_skip = c.tskip;
+    pps.cu_qp_delta = c.cu_qp_delta;
+    pps.diff_cu_qp_delta_depth = c.cu_qp_delta ? std::min(1, c.log2_ctb - 3) : 0;
+    pps.cb_qp_offset = cov ? rng.uni(7) - 3 : 0;
+    pps.cr_qp_offset = cov ? rng.uni(7) - 3 : 0;
+    pps.slice_chroma_qp_offsets_present = cov;
+    pps.loop_filter_across_slices = true;
+    pps.deblocking_override_enabled = cov;
+    pps.deblocking_disabled = !c.deblock;
+    pps.beta_offset = cov ? 2 * (rng.uni(5) - 2) : 0;
+    pps.tc_offset = cov ? 2 * (rng.uni(5) - 2) : 0;
+    pps.log2_parallel_merge_level = cov && rng.chance(40) ? 3 : 2;
+    auto nal = [](const std::vector<u8>& rbsp, std::vector<u8>& out) { rbsp_to_ebsp(rbsp.data(), rbsp.size(), out); };
+    nal(write_vps(vps), vps_nal);
+    nal(write_sps(sps), sps_nal);
+    nal(write_pps(pps), pps_nal);
+    scene.make(SceneConfig{c.width, c.height, W, H, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
+    residual = [this](int ci, int x0, int y0, int log2, const u8* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
+                      bool& ts) { this->make_residual(ci, x0, y0, log2, pred, ps, qp, ts_ok, intra, lv, ts); };
+  }
+
+  bool is_idr_pos(i64 d) const { return d % cfg.gop == 0; }
+
+  const HostSurface& source_of(i64 d) {
+    while (rendered < d) {
+      ++rendered;
+      if (rendered > 0) scene.advance();
+      scene.render();
+      scene.add_sensor_noise(rendered);
+      sources[rendered] = scene.src;
+    }
+    return sources.at(d);
+  }
+
+  void plan_next() {
+    if (is_idr_pos(next_disp)) {
+      plan.push_back({next_disp, kI, true, true});
+      ++next_disp;
+      return;
+    }
+    i64 next_idr = next_disp + 1;
+    while (!is_idr_pos(next_idr)) ++next_idr;
+    const i64 anchor = std::min<i64>(next_disp + cfg.bframes, next_idr - 1);
+    plan.push_back({anchor, kP, true, false});
+    for (i64 d = next_disp; d < anchor; ++d) plan.push_back({d, kB, false, false});
+    next_disp = anchor + 1;
+  }
+
+  // ------------------------------------------------------------------ decisions (CtuDecider)
+  bool split(int x0, int y0, int log2) override {
+    (void)x0, (void)y0;
+    if (cfg.coverage) return rng.chance(log2 == 6 ? 80 : 50);
+    return log2 > 4;
+  }
+
+  void sao(int rx, int ry, SaoParams& p, bool& ml, bool& mu) override {
+    (void)rx, (void)ry;
+    p = SaoParams{};
+    ml = cfg.coverage && rng.chance(20);
+    mu = cfg.coverage && rng.chance(20);
+    if (!cfg.coverage) return;
+    for (int c = 0; c < 3; ++c) {
+      p.type[c] = u8(c == 2 ? p.type[1] : rng.uni(3));
+      p.band[c] = u8(rng.uni(32));
+      p.eo[c] = u8(c == 2 ? p.eo[1] : rng.uni(4));
+      for (int i = 0; i < 4; ++i) {
+        const int a = rng.uni(8);
+        p.off[c][i] = i8(p.type[c] == 1 && rng.chance(50) ? -a : a);
+      }
+    }
+  }
+
+  int sad_block(const HostSurface& ref, int x0, int y0, int n, int mvx, int mvy) const {
+    int s = 0;
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) {
+        const int rx = std::clamp(x0 + i + mvx, 0, W - 1), ry = std::clamp(y0 + j + mvy, 0, H - 1);
+        s += std::abs(int(cur_src->y[size_t(y0 + j) * W + size_t(x0 + i)]) - int(ref.y[size_t(ry) * W + size_t(rx)]));
+      }
+    return s;
+  }
+
+  void cu(int x0, int y0, int log2, CuDesc& d) override {
+    d = CuDesc{};
+    const int n = 1 << log2;
+    const SliceInfo& sl = pc.slices[size_t(cur_slice)];
+    const SliceHeader& sh = sl.sh;
+    if (cfg.coverage) {
+      coverage_cu(x0, y0, log2, d, sl);
+      return;
+    }
+    d.tu_log2 = log2;
+    d.chroma_mode = 4;
+    d.luma_mode[0] = 0;  // planar
+    if (sh.slice_type == kI) {
+      d.intra = true;
+      return;
+    }
+    // merge candidates first (skip), then a small motion search per list
+    MergeCand mc[5];
+    const int nm = merge_candidates(pc, cur_slice, x0, y0, n, x0, y0, n, n, 0, 0, mc);
+    int best = INT32_MAX, best_m = -1;
+    for (int k = 0; k < nm; ++k) {
+      int s = 0;
+      if (mc[k].pred == 3) continue;
+      const int l = mc[k].pred == 1 ? 0 : 1;
+      if (mc[k].mv[l][0] & 3 || mc[k].mv[l][1] & 3) continue;
+      s = sad_block(sl.list[l][size_t(mc[k].ref[l])]->s, x0, y0, n, mc[k].mv[l][0] >> 2, mc[k].mv[l][1] >> 2);
+      if (s < best) best = s, best_m = k;
+    }
+    const double qstep = std::pow(2.0, (cur_qp - 4) / 6.0);
+    if (best_m >= 0 && best < int(n * n * std::max(1.0, qstep * 0.6))) {
+      d.skip = true;
+      d.pu[0].merge = true;
+      d.pu[0].merge_idx = best_m;
+      return;
+    }
+    int bl = 0, bmv[2] = {0, 0}, bs = INT32_MAX;
+    const int nl = sh.slice_type == kB ? 2 : 1;
+    for (int l = 0; l < nl; ++l) {
+      const HevcFrame& rf = *sl.list[l][0];
+      const int dist = pc.poc - rf.poc;
+      std::vector<std::pair<int, int>> cands = {{0, 0}};
+      for (const Scene::Obj& o : scene.objs) cands.push_back({-int(std::lround(o.vx * dist)), -int(std::lround(o.vy * dist))});
+      for (auto [cx, cy] : cands)
+        for (int dy = -1; dy <= 1; ++dy)
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int s = sad_block(rf.s, x0, y0, n, cx + dx, cy + dy);
+            if (s < bs) bs = s, bl = l, bmv[0] = cx + dx, bmv[1] = cy + dy;
+          }
+    }
+    if (best_m >= 0 && best <= bs) {
+      d.pu[0].merge = true;
+      d.pu[0].merge_idx = best_m;
+      d.tu_log2 = std::min(log2, 4);
+      return;
+    }
+    if (bs > n * n * 40) {  // nothing matches: intra
+      d.intra = true;
+      return;
+    }
+    d.pu[0].dir = bl + 1;
+    d.pu[0].ref[bl] = 0;
+    d.pu[0].mv[bl][0] = i16(bmv[0] * 4);
+    d.pu[0].mv[bl][1] = i16(bmv[1] * 4);
+    d.tu_log2 = std::min(log2, 4);
+  }
+
+  void coverage_cu(int x0, int y0, int log2, CuDesc& d, const SliceInfo& sl) {
+    const SliceHeader& sh = sl.sh;
+    const int n = 1 << log2;
+    d.tu_log2 = 2 + rng.uni(log2 - 1);
+    d.qp_delta = rng.uni(7) - 3;
+    d.tskip = rng.chance(30);
+    d.chroma_mode = rng.uni(5);
+    for (int k = 0; k < 4; ++k) d.luma_mode[k] = rng.uni(35);
+    const bool inter_slice = sh.slice_type != kI;
+    if (inter_slice && rng.chance(15)) {
+      d.skip = true;
+      d.pu[0].merge = true;
+      d.pu[0].merge_idx = rng.uni(sh.max_num_merge_cand);
+      return;
+    }
+    d.intra = !inter_slice || rng.chance(25);
+    if (d.intra) {
+      d.part = (log2 == sps.log2_min_cb && rng.chance(40)) ? 3 : 0;
+      if (d.part == 0 && sps.pcm && log2 >= sps.log2_min_pcm && log2 <= sps.log2_max_pcm && rng.chance(6)) {
+        d.pcm = true;
+        pcm_buf.clear();
+        for (int j = 0; j < n; ++j)
+          for (int i = 0; i < n; ++i) pcm_buf.push_back(cur_src->y[size_t(y0 + j) * W + size_t(x0 + i)]);
+        for (int c = 0; c < 2; ++c)
+          for (int j = 0; j < n / 2; ++j)
+            for (int i = 0; i < n / 2; ++i)
+              pcm_buf.push_back(cur_src->uv[size_t(y0 / 2 + j) * W + size_t(x0 + 2 * i + c)]);
+        d.pcm_samples = pcm_buf.data();
+      }
+      return;
+    }
+    // inter partition
+    const bool min = log2 == sps.log2_min_cb;
+    int opts[8], no = 0;
+    opts[no++] = 0;
+    opts[no++] = 1;
+    opts[no++] = 2;
+    if (sps.amp && !min)
+      for (int p = 4; p < 8; ++p) opts[no++] = p;
+    d.part = opts[rng.uni(no)];
+    const int npu = d.part == 0 ? 1 : (d.part == 3 ? 4 : 2);
+    const int w = n, h = n;
+    for (int k = 0; k < npu; ++k) {
+      CuDesc::Pu& p = d.pu[k];
+      int pw = w, ph = h;
+      if (d.part == 1) ph = h / 2;
+      if (d.part == 2) pw = w / 2;
+      if (d.part >= 4 && d.part <= 5) ph = (k == 0) == (d.part == 4) ? h / 4 : 3 * h / 4;
+      if (d.part >= 6) pw = (k == 0) == (d.part == 6) ? w / 4 : 3 * w / 4;
+      p.merge = rng.chance(35);
+      p.merge_idx = rng.uni(sh.max_num_merge_cand);
+      p.dir = 1;
+      if (sh.slice_type == kB) p.dir = (pw + ph == 12) ? 1 + rng.uni(2) : 1 + rng.uni(3);
+      for (int l = 0; l < 2; ++l) {
+        const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+        p.ref[l] = nref > 0 ? rng.uni(nref) : 0;
+        p.mvp[l] = rng.uni(2);
+        const Scene::Obj* o = scene.objs.empty() ? nullptr : &scene.objs[size_t(rng.uni(int(scene.objs.size())))];
+        const int base_x = o ? int(-o->vx * 4) : 0, base_y = o ? int(-o->vy * 4) : 0;
+        p.mv[l][0] = i16(rng.chance(20) ? rng.uni(513) - 256 : base_x + rng.uni(17) - 8);
+        p.mv[l][1] = i16(rng.chance(20) ? rng.uni(257) - 128 : base_y + rng.uni(17) - 8);
+      }
+    }
+  }
+
+  void make_residual(int c, int x0, int y0, int log2, const u8* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
+                     bool& ts) {
+    const int n = 1 << log2;
+    std::vector<int> res(size_t(n) * n);
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) {
+        const int s = c == 0 ? cur_src->y[size_t(y0 + j) * W + size_t(x0 + i)]
+                             : cur_src->uv[size_t(y0 + j) * W + size_t(2 * (x0 + i) + c - 1)];
+        res[size_t(j) * n + i] = s - int(pred[size_t(j) * ps + i]);
+      }
+    if (!cfg.coverage) ts = false;
+    ts = ts && ts_ok;
+    quantise(res.data(), log2, c == 0 && log2 == 2 && intra, ts, qp, intra, lv);
+  }
+
+  // ------------------------------------------------------------------ pictures
+  std::shared_ptr<AccessUnit> encode(const Job& job) {
+    const int dur = 90000 / std::max(1, cfg.fps);
+    if (job.idr) {
+      idr_disp = job.disp;
+      anchors.clear();
+    }
+    const int poc = int(job.disp - idr_disp);
+    cur_src = &source_of(job.disp);
+    cur_type = job.type;
+    cur = std::make_shared<HevcFrame>();
+    cur->s.alloc(W, H);
+    cur->poc = poc;
+    cur->is_ref = job.ref;
+    // reference picture set: every kept anchor; used = the ones this picture predicts from
+    std::vector<FramePtr> before, after;
+    for (const FramePtr& f : anchors) (f->poc < poc ? before : after).push_back(f);
+    std::sort(before.begin(), before.end(), [](const FramePtr& a, const FramePtr& b) { return a->poc > b->poc; });
+    std::sort(after.begin(), after.end(), [](const FramePtr& a, const FramePtr& b) { return a->poc < b->poc; });
+    ShortTermRps rps;
+    rps.num_negative = int(before.size());
+    rps.num_positive = int(after.size());
+    for (size_t i = 0; i < before.size(); ++i) rps.delta_poc[i] = before[i]->poc - poc, rps.used[i] = true;
+    for (size_t i = 0; i < after.size(); ++i)
+      rps.delta_poc[before.size() + i] = after[i]->poc - poc, rps.used[before.size() + i] = true;
+    const int total = rps.num_delta();
+    // slices
+    pc.init(sps, pps, &cur->s);
+    pc.poc = poc;
+    auto au = std::make_shared<AccessUnit>();
+    au->codec = Codec::kH265;
+    if (job.idr) {
+      au->add_nal(vps_nal.data(), vps_nal.size());
+      au->add_nal(sps_nal.data(), sps_nal.size());
+      au->add_nal(pps_nal.data(), pps_nal.size());
+    }
+    const int nctb = pc.wctb * pc.hctb;
+    const int nsl = std::clamp(cfg.slices, 1, nctb);
+    const bool cov = cfg.coverage;
+    const int pic_qp = cov ? std::clamp(cfg.qp + rng.uni(21) - 10, 5, 51) : cfg.qp;
+    for (int s = 0; s < nsl; ++s) {
+      const int first = s * nctb / nsl, end = (s + 1) * nctb / nsl;
+      SliceHeader sh;
+      sh.nal_type = job.idr ? kIdrWRadl : (job.ref ? kTrailR : kTrailN);
+      sh.first_slice_in_pic = s == 0;
+      sh.segment_address = first;
+      sh.slice_type = job.type;
+      sh.poc_lsb = poc & 255;
+      sh.rps = rps;
+      sh.temporal_mvp = sps.temporal_mvp && job.type != kI;
+      sh.sao_luma = sps.sao && (!cov || rng.chance(70));
+      sh.sao_chroma = sps.sao && (!cov || rng.chance(70));
+      if (!cov) sh.sao_luma = sh.sao_chroma = false;
+      if (job.type != kI) {
+        sh.num_ref_idx_l0 = cov ? 1 + rng.uni(std::max(1, std::min(total, 3))) : 1;
+        sh.num_ref_idx_l1 = job.type == kB ? (cov ? 1 + rng.uni(2) : 1) : 0;
+        sh.mvd_l1_zero = job.type == kB && cov && rng.chance(30);
+        sh.cabac_init = cov && rng.chance(50);
+        sh.collocated_from_l0 = job.type != kB || !cov || rng.chance(50);
+        const int ncol = sh.collocated_from_l0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+        sh.collocated_ref_idx = cov ? rng.uni(ncol) : 0;
+        sh.max_num_merge_cand = cov ? 1 + rng.uni(5) : 5;
+      }
+      sh.qp_delta = pic_qp - pps.init_qp;
+      sh.cb_qp_offset = cov ? rng.uni(5) - 2 : 0;
+      sh.cr_qp_offset = cov ? rng.uni(5) - 2 : 0;
+      sh.deblocking_disabled = pps.deblocking_disabled;
+      sh.beta_offset = pps.beta_offset;
+      sh.tc_offset = pps.tc_offset;
+      if (cov && pps.deblocking_override_enabled && rng.chance(40)) {
+        sh.deblocking_disabled = rng.chance(30);
+        sh.beta_offset = sh.deblocking_disabled ? pps.beta_offset : 2 * (rng.uni(13) - 6);
+        sh.tc_offset = sh.deblocking_disabled ? pps.tc_offset : 2 * (rng.uni(13) - 6);
+      }
+      sh.loop_filter_across_slices = !cov || rng.chance(50);
+      if (!(pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled)))
+        sh.loop_filter_across_slices = pps.loop_filter_across_slices;
+      SliceInfo si;
+      si.sh = sh;
+      si.qp = pic_qp;
+      if (job.type != kI) build_lists(sh, before, after, si);
+      pc.slices.push_back(std::move(si));
+      cur_slice = s;
+      cur_qp = pic_qp;
+      BitWriter bw;
+      write_slice_header_full(bw, sh, sps, pps);
+      std::vector<u8> rb = std::move(bw.buf());
+      encode_slice_data(pc, s, rb, *this, first, end);
+      std::vector<u8> ebsp;
+      rbsp_to_ebsp(rb.data(), rb.size(), ebsp);
+      au->add_nal(ebsp.data(), ebsp.size());
+    }
+    bool deblock = false, sao_on = false;
+    for (const SliceInfo& s : pc.slices) {
+      deblock |= !s.sh.deblocking_disabled;
+      sao_on |= s.sh.sao_luma || s.sh.sao_chroma;
+    }
+    if (deblock) deblock_picture(pc);
+    if (sao_on) sao_picture(pc);
+    if (sps.temporal_mvp) cur->col = build_col(pc, cur->col_w);
+    if (job.ref) {
+      anchors.push_back(cur);
+      if (int(anchors.size()) > keep_refs) anchors.erase(anchors.begin());
+    }
+    au->pts = job.disp * dur;
+    au->dts = coded * dur - (cfg.bframes > 0 ? dur : 0);
+    au->duration = dur;
+    au->keyframe = job.idr;
+    ++coded;
+    last_pts = au->pts;
+    last_type = job.type == kI ? 'I' : job.type == kP ? 'P' : 'B';
+    recon_out = cur->s;
+    src_out = *cur_src;
+    // sources no longer needed
+    while (!sources.empty() && sources.begin()->first < job.disp - 8) sources.erase(sources.begin());
+    return au;
+  }
+
+  void build_lists(const SliceHeader& sh, const std::vector<FramePtr>& before, const std::vector<FramePtr>& after,
+                   SliceInfo& si) {
+    const int total = int(before.size() + after.size());
+    VEP_CHECK(total > 0, "inter picture without references");
+    for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
+      const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+      std::vector<FramePtr> temp;
+      const auto& a = l == 0 ? before : after;
+      const auto& b = l == 0 ? after : before;
+      while (int(temp.size()) < std::max(nref, total)) {
+        temp.insert(temp.end(), a.begin(), a.end());
+        temp.insert(temp.end(), b.begin(), b.end());
+      }
+      for (int i = 0; i < nref; ++i) {
+        si.list[l].push_back(temp[size_t(i)]);
+        si.list_poc[l].push_back(temp[size_t(i)]->poc);
+      }
+    }
+  }
+
+  std::shared_ptr<AccessUnit> next() {
+    if (plan.empty()) plan_next();
+    const Job j = plan.front();
+    plan.pop_front();
+    return encode(j);
+  }
+};
+
+HevcEncoder::HevcEncoder(const HevcEncConfig& cfg) : p_(std::make_unique<Impl>(cfg)) {}
+HevcEncoder::~HevcEncoder() = default;
+std::shared_ptr<AccessUnit> HevcEncoder::next() { return p_->next(); }
+const HostSurface& HevcEncoder::reconstruction() const { return p_->recon_out; }
+const HostSurface& HevcEncoder::source() const { return p_->src_out; }
+i64 HevcEncoder::last_pts() const { return p_->last_pts; }
+char HevcEncoder::last_type() const { return p_->last_type; }
+const std::vector<u8>& HevcEncoder::vps_nal() const { return p_->vps_nal; }
+const std::vector<u8>& HevcEncoder::sps_nal() const { return p_->sps_nal; }
+const std::vector<u8>& HevcEncoder::pps_nal() const { return p_->pps_nal; }
+
+}  // namespace vep::hevc
