@@ -323,6 +323,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("height", &hevc::HevcEncConfig::height)
       .def_readwrite("fps", &hevc::HevcEncConfig::fps)
       .def_readwrite("gop", &hevc::HevcEncConfig::gop)
+      .def_readwrite("idr_phase", &hevc::HevcEncConfig::idr_phase)
       .def_readwrite("bframes", &hevc::HevcEncConfig::bframes)
       .def_readwrite("qp", &hevc::HevcEncConfig::qp)
       .def_readwrite("log2_ctb", &hevc::HevcEncConfig::log2_ctb)
@@ -942,6 +943,22 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("parse_wait_ms", &ReplayBench::parse_wait_ms)
       .def_property_readonly("batch_ms", &ReplayBench::batch_ms)
       .def_property_readonly("cameras", &ReplayBench::cameras);
+
+  // CPU reference of the colour conversion (coded NV12 planes -> cropped BGR24).
+  m.def("nv12_to_bgr_cpu", [](py::array_t<uint8_t, py::array::c_style> y, py::array_t<uint8_t, py::array::c_style> uv,
+                              int crop_left, int crop_top, int width, int height) {
+    VEP_CHECK(y.ndim() == 2 && uv.ndim() == 2 && uv.shape(0) * 2 == y.shape(0) && uv.shape(1) == y.shape(1),
+              "nv12_to_bgr_cpu: Y (H, W) and UV (H / 2, W) planes expected");
+    VEP_CHECK(crop_left + width <= y.shape(1) && crop_top + height <= y.shape(0), "crop window outside the planes");
+    HostSurface s;
+    s.coded_w = int(y.shape(1));
+    s.coded_h = int(y.shape(0));
+    s.y.assign(y.data(), y.data() + y.size());
+    s.uv.assign(uv.data(), uv.data() + uv.size());
+    py::array_t<uint8_t> o({height, width, 3});
+    cpu_nv12_to_bgr(s, crop_left, crop_top, width, height, o.mutable_data());
+    return o;
+  });
 
   // ---- op API on caller-owned device buffers (torch tensors pass data_ptr / stream) ----
   m.def("nv12_to_bgr",

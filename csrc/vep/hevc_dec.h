@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 
+#include "avc.h"
 #include "codec.h"
 #include "hevc.h"
 #include "hevc_tables.h"
@@ -133,6 +134,7 @@ class Decoder {
 struct HevcEncConfig {
   int width = 416, height = 240;
   int fps = 30, gop = 16;
+  int idr_phase = 0;         // IDR when display index d == 0 or (d + idr_phase) % gop == 0
   int bframes = 0;           // B pictures between anchors (0 = IPPP)
   int qp = 30;
   int log2_ctb = 5, log2_min_cb = 3;
@@ -145,18 +147,18 @@ struct HevcEncConfig {
   u64 seed = 1;
 };
 
-class HevcEncoder {
+class HevcEncoder : public avc::StreamEncoder {
  public:
   explicit HevcEncoder(const HevcEncConfig& cfg);
-  ~HevcEncoder();
-  std::shared_ptr<AccessUnit> next();
-  const HostSurface& reconstruction() const;
-  const HostSurface& source() const;
-  i64 last_pts() const;
+  ~HevcEncoder() override;
+  std::shared_ptr<AccessUnit> next() override;
+  const HostSurface& reconstruction() const override;
+  const HostSurface& source() const override;
+  i64 last_pts() const override;
   char last_type() const;
   const std::vector<u8>& vps_nal() const;
-  const std::vector<u8>& sps_nal() const;
-  const std::vector<u8>& pps_nal() const;
+  const std::vector<u8>& sps_nal() const override;
+  const std::vector<u8>& pps_nal() const override;
 
  private:
   struct Impl;

@@ -174,7 +174,7 @@ struct HevcEncoder::Impl : CtuDecider {
                       bool& ts) { this->make_residual(ci, x0, y0, log2, pred, ps, qp, ts_ok, intra, lv, ts); };
   }
 
-  bool is_idr_pos(i64 d) const { return d % cfg.gop == 0; }
+  bool is_idr_pos(i64 d) const { return d == 0 || (d + cfg.idr_phase) % cfg.gop == 0; }
 
   const HostSurface& source_of(i64 d) {
     while (rendered < d) {
@@ -264,7 +264,7 @@ struct HevcEncoder::Impl : CtuDecider {
       if (s < best) best = s, best_m = k;
     }
     const double qstep = std::pow(2.0, (cur_qp - 4) / 6.0);
-    if (best_m >= 0 && best < int(n * n * std::max(1.0, qstep * 0.6))) {
+    if (best_m >= 0 && best < int(n * n * std::max(1.5, qstep * 0.15))) {
       d.skip = true;
       d.pu[0].merge = true;
       d.pu[0].merge_idx = best_m;

@@ -157,7 +157,7 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
   job.refresh = refresh;
   const AccessUnit* last = nullptr;
   try {
-    if (!full_) {
+    if (!full_ && !hevc_full_) {
       try {
         for (size_t i = from; i < to; ++i) {
           // single-AU jobs may take the header-free I-slice walk: the worker verifies the
@@ -167,16 +167,50 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
           last = gop_[i].get();
         }
       } catch (const UnsupportedStream& e) {
-        if (gop_[from]->codec != Codec::kH264 || !gop_[0]->keyframe) throw;
-        // The stream uses H.264 syntax beyond the I_PCM / P_Skip fast path: switch this camera
-        // to the general decoder for good and rebuild the job from the GOP's keyframe (the
-        // general decoder needs the whole reference history of the GOP).
-        full_ = true;
-        logs.add(false, std::string("general H.264 decoder enabled (") + e.what() + ")");
+        if (!gop_[0]->keyframe) throw;
+        // The stream uses syntax beyond the I_PCM / P_Skip fast path: switch this camera to the
+        // general decoder for good and rebuild the job from the GOP's keyframe (the general
+        // decoder needs the whole reference history of the GOP).
+        const bool h264 = gop_[from]->codec == Codec::kH264;
+        (h264 ? full_ : hevc_full_) = true;
+        logs.add(false, std::string(h264 ? "general H.264" : "general H.265") + " decoder enabled (" + e.what() + ")");
         job.upd = MbUpdate{};
         from = 0;
         job.refresh = true;
       }
+    }
+    if (hevc_full_) {
+      hevc::FramePtr of;
+      const bool key_only = keyframe_only.load() && to - from == 1 && gop_[from]->keyframe;
+      for (size_t i = from; i < to; ++i) {
+        std::vector<hevc::FramePtr> outs = hevc_.decode(*gop_[i], i64(i));
+        if (key_only) {  // nothing else of the GOP is decoded: take the picture out right away
+          std::vector<hevc::FramePtr> rest = hevc_.flush();
+          outs.insert(outs.end(), rest.begin(), rest.end());
+        }
+        if (!outs.empty()) of = outs.back();
+        last = gop_[i].get();
+      }
+      hevc_pics_ += int(to - from);
+      decoded_upto_ = to;
+      if (!of) return false;  // reordering: every picture still waits for output
+      hevc_publish(*of, job);
+      job.cpu_recon = true;
+      job.upd.frames = hevc_pics_;  // pictures reconstructed since the last published job
+      hevc_pics_ = 0;
+      FrameMeta& m = job.meta;
+      m.width = of->width;
+      m.height = of->height;
+      m.pts = of->pts;
+      m.dts = of->dts;
+      m.timestamp = of->pts;
+      m.packet = of->tag;
+      m.keyframe = keyframes_;
+      m.is_keyframe = of->keyframe;
+      m.is_corrupt = false;
+      m.frame_type = of->type;
+      m.arrival_ms = last->arrival_ms;
+      return true;
     }
     if (full_) {
       for (size_t i = from; i < to; ++i) {
@@ -211,6 +245,7 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
     errors.fetch_add(1);
     logs.add(true, std::string("failed to decode packet: ") + e.what());
     if (full_) avc_.reset_references();
+    if (hevc_full_) hevc_shown_.clear();  // the surface may hold a partial update
     decoded_upto_ = gop_.size();  // give up on this GOP; wait for the next keyframe
     return false;
   }
@@ -228,6 +263,64 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
   m.arrival_ms = last->arrival_ms;
   decoded_upto_ = to;
   return true;
+}
+
+bool Camera::hevc_publish(const hevc::HevcFrame& f, DecodeJob& job) {
+  const int W = f.s.coded_w, H = f.s.coded_h;
+  const int wmbs = (W + 15) / 16, hmbs = (H + 15) / 16;
+  if (job.upd.width_mbs != wmbs || job.upd.height_mbs != hmbs) job.upd.reset(wmbs, hmbs);
+  const size_t nmb = size_t(wmbs) * hmbs;
+  const bool full = hevc_shown_.size() != nmb * 384 || hevc_shown_wmbs_ != wmbs || hevc_shown_hmbs_ != hmbs;
+  if (full) {
+    hevc_shown_.assign(nmb * 384, 0);
+    hevc_shown_wmbs_ = wmbs;
+    hevc_shown_hmbs_ = hmbs;
+  }
+  auto buf = std::make_shared<std::vector<u8>>();
+  buf->reserve(full ? nmb * 384 : 64 * 384);
+  std::vector<i32> changed;
+  u8 blk[384];
+  for (int my = 0; my < hmbs; ++my)
+    for (int mx = 0; mx < wmbs; ++mx) {
+      // gather the macroblock in I_PCM order (16x16 Y, 8x8 Cb, 8x8 Cr), clamping at the edges of
+      // the coded picture (HEVC sizes are multiples of 8)
+      for (int y = 0; y < 16; ++y) {
+        const size_t row = size_t(std::min(my * 16 + y, H - 1)) * size_t(W);
+        for (int x = 0; x < 16; ++x) blk[y * 16 + x] = f.s.y[row + size_t(std::min(mx * 16 + x, W - 1))];
+      }
+      for (int y = 0; y < 8; ++y) {
+        const size_t row = size_t(std::min(my * 8 + y, H / 2 - 1)) * size_t(W);
+        for (int x = 0; x < 8; ++x) {
+          const size_t c = row + 2 * size_t(std::min(mx * 8 + x, W / 2 - 1));
+          blk[256 + y * 8 + x] = f.s.uv[c];
+          blk[320 + y * 8 + x] = f.s.uv[c + 1];
+        }
+      }
+      u8* shown = hevc_shown_.data() + (size_t(my) * wmbs + size_t(mx)) * 384;
+      if (!full && std::memcmp(shown, blk, 384) == 0) continue;
+      std::memcpy(shown, blk, 384);
+      buf->insert(buf->end(), blk, blk + 384);
+      changed.push_back(my * wmbs + mx);
+    }
+  job.refresh = full;
+  if (!changed.empty()) {
+    job.upd.begin_segment(buf->data(), buf->size());
+    job.upd.reserve_blocks(changed.size());
+    for (size_t k = 0; k < changed.size(); ++k) job.upd.set(changed[k], buf->data() + 384 * k);
+    job.upd.own.push_back(std::move(buf));
+  }
+  PictureInfo& p = job.pic;
+  p = PictureInfo{};
+  p.width = f.width;
+  p.height = f.height;
+  p.coded_width = wmbs * 16;
+  p.coded_height = hmbs * 16;
+  p.crop_left = f.crop_left;
+  p.crop_top = f.crop_top;
+  p.pict_type = f.type;
+  p.idr = f.keyframe;
+  p.coded_mbs = int(changed.size());
+  return full;
 }
 
 bool Camera::on_access_unit(const AuPtr& au) {
@@ -1241,7 +1334,7 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       continue;
     }
     if (!(err && err[i]) && !cp->broken_) {
-      const u64 np = jobs[i].general() ? jobs[i].avc.size() : 1;
+      const u64 np = jobs[i].general() ? jobs[i].avc.size() : jobs[i].cpu_recon ? u64(std::max(1, jobs[i].upd.frames)) : 1;
       pictures_.fetch_add(np, std::memory_order_relaxed);
       cp->pictures.fetch_add(np, std::memory_order_relaxed);
     }

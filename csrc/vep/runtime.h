@@ -20,6 +20,7 @@
 
 #include "avc.h"
 #include "codec.h"
+#include "hevc_dec.h"
 #include "gpu.h"
 #include "pool.h"
 
@@ -101,6 +102,7 @@ struct DecodeJob {
   PictureInfo pic;                     // the published frame's picture (sizes of the surfaces)
   FrameMeta meta;
   bool refresh = false;  // IDR: every MB is covered
+  bool cpu_recon = false;  // blocks reconstructed on the CPU (general H.265 path); upd.frames counts them
   // General path: DPB slot of the newest picture that left the reorder buffer in this job (it is
   // converted and published), -1 when every picture of the job is still waiting for output
   // (B-frame reordering): the job then only reconstructs.
@@ -164,8 +166,8 @@ class Camera {
   std::shared_ptr<FrameRing> ring() const { return std::atomic_load(&ring_); }
   void set_ring(std::shared_ptr<FrameRing> r) { std::atomic_store(&ring_, std::move(r)); }
   StreamParser& parser() { return parser_; }
-  // true once the stream left the I_PCM / P_Skip fast path (general H.264 decoder in use)
-  bool general_decoder() const { return full_; }
+  // true once the stream left the I_PCM / P_Skip fast path (general H.264 / H.265 decoder in use)
+  bool general_decoder() const { return full_ || hevc_full_; }
   std::mutex& gop_mutex() { return mu_; }
   std::vector<AuPtr> gop_snapshot();   // current GOP packets (for RTMP flush / archive)
 
@@ -196,6 +198,16 @@ class Camera {
   StreamParser parser_;
   avc::Decoder avc_;
   bool full_ = false;
+  // General H.265 path: the CPU decoder reconstructs (hevc_dec.h) and each published picture
+  // goes to the surface as an update of the 16x16 blocks that changed since the last one, in the
+  // I_PCM block layout of the fast path (so the GPU apply / convert / letterbox kernels, job
+  // collapsing and the CPU backend are shared).
+  bool hevc_publish(const hevc::HevcFrame& f, DecodeJob& job);
+  bool hevc_full_ = false;
+  hevc::Decoder hevc_;
+  std::vector<u8> hevc_shown_;  // the blocks the surface holds (384 B each), empty = unknown
+  int hevc_shown_wmbs_ = 0, hevc_shown_hmbs_ = 0;
+  int hevc_pics_ = 0;           // pictures reconstructed since the last published job
 };
 
 struct WorkerOptions {

@@ -1,6 +1,8 @@
 // Synthetic H.264 camera encoder (I_PCM / P_Skip). See synth.h.
 #include "synth.h"
 
+#include "hevc_dec.h"
+
 #include <algorithm>
 #include <cmath>
 
@@ -70,8 +72,28 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
   bw_ = std::clamp(int(std::lround(std::sqrt(area * 4.0 / 3.0))), 1, wmbs_);
   bh_ = std::clamp(int(std::lround(area / bw_)), 1, hmbs_);
   if (cfg.motion <= 0) bw_ = bh_ = 0;
-  if (cfg.compressed) {
-    VEP_CHECK(cfg.codec == Codec::kH264, "compressed synthetic streams are H.264 only");
+  if (cfg.compressed && cfg.codec == Codec::kH265) {  // general HEVC Main stream
+    hevc::HevcEncConfig hc;
+    hc.width = cfg.width;
+    hc.height = cfg.height;
+    hc.fps = cfg.fps;
+    hc.gop = cfg.gop;
+    hc.idr_phase = cfg.idr_phase;
+    hc.qp = cfg.qp;
+    hc.slices = cfg.slices;
+    hc.bframes = cfg.bframes;
+    hc.objects = cfg.objects;
+    hc.seed = cfg.seed;
+    hc.deblock = cfg.deblock_idc != 1;
+    hc.coverage = cfg.coverage;
+    hc.noise = cfg.noise;
+    hc.temporal_noise = cfg.temporal_noise;
+    auto enc = std::make_unique<hevc::HevcEncoder>(hc);
+    vps_nal_ = enc->vps_nal();
+    avc_ = std::move(enc);
+    sps_nal_ = avc_->sps_nal();
+    pps_nal_ = avc_->pps_nal();
+  } else if (cfg.compressed) {
     if (cfg.profile == "main" || cfg.profile == "high") {
       avc::AvcHighConfig hc;
       hc.width = cfg.width;

@@ -24,8 +24,9 @@ struct SynthConfig {
   int idr_phase = 0;       // GOP phase offset (IDR when (frame + phase) % gop == 0, and frame 0)
   Codec codec = Codec::kH264;
   int merge_cands = 1;     // HEVC MaxNumMergeCand (merge_idx coded when > 1)
-  // H.264 only: emit a real compressed stream (CAVLC intra/inter prediction + residual +
-  // deblocking, avc::AvcEncoder) instead of the I_PCM / P_Skip fast-path subset.
+  // Emit a real compressed stream instead of the I_PCM / P_Skip fast-path subset: H.264 per
+  // `profile` below, H.265 Main (CABAC CTU trees, intra / merge / AMVP / B, deblocking, SAO:
+  // hevc::HevcEncoder).
   bool compressed = false;
   int qp = 28;
   int refs = 1;            // max_num_ref_frames
