@@ -16,27 +16,39 @@ void inverse_transform(const i32* d, int log2, bool dst, bool tskip, i32* r) {
     for (int k = 0; k < n * n; ++k) r[k] = ((d[k] << 7) + (1 << 11)) >> 12;
     return;
   }
-  i32 e[32 * 32], g[32 * 32];
-  auto coef = [&](int j, int i) -> int {  // basis j (frequency) at sample i
-    return dst ? kDst4[j][i] : kDct.m[j << (5 - log2)][i];
-  };
-  // columns: e[x][y] = sum_j coef(j, y) * d[x][j] (d row-major: d[y * n + x])
-  for (int x = 0; x < n; ++x)
-    for (int y = 0; y < n; ++y) {
-      i64 s = 0;
-      for (int j = 0; j < n; ++j) {
-        const i32 v = d[j * n + x];
-        if (v) s += i64(coef(j, y)) * v;
-      }
-      e[y * n + x] = i32(s);
-    }
-  for (int k = 0; k < n * n; ++k) g[k] = std::clamp((e[k] + 64) >> 7, -32768, 32767);
+  // basis rows (frequency j, sample i): the n-point DCT is every (32 / n)-th row of the 32-point
+  // matrix; |coef| <= 90 and |d| < 2^15, so 32-term sums fit in 32 bits
+  const i8* basis[32];
+  for (int j = 0; j < n; ++j) basis[j] = dst ? kDst4[j] : kDct.m[j << (5 - log2)];
+  // the coded coefficients sit in the top-left corner: bound the work by their extent
+  int mx = -1, my = -1;
   for (int y = 0; y < n; ++y)
-    for (int x = 0; x < n; ++x) {
-      i64 s = 0;
-      for (int j = 0; j < n; ++j) s += i64(coef(j, x)) * g[y * n + j];
-      r[y * n + x] = i32((s + (1 << 11)) >> 12);
+    for (int x = 0; x < n; ++x)
+      if (d[y * n + x]) {
+        mx = std::max(mx, x);
+        my = y;
+      }
+  if (mx < 0) {
+    std::fill(r, r + n * n, 0);
+    return;
+  }
+  i32 g[32 * 32];
+  // first stage (vertical): g[y][x] = clip((sum_j basis[j][y] * d[j][x] + 64) >> 7), columns <= mx
+  for (int y = 0; y < n; ++y)
+    for (int x = 0; x <= mx; ++x) {
+      i32 s = 0;
+      for (int j = 0; j <= my; ++j) s += basis[j][y] * d[j * n + x];
+      g[y * n + x] = std::clamp((s + 64) >> 7, -32768, 32767);
     }
+  // second stage (horizontal): r[y][x] = (sum_j basis[j][x] * g[y][j] + 2^11) >> 12
+  for (int y = 0; y < n; ++y) {
+    const i32* gr = g + y * n;
+    for (int x = 0; x < n; ++x) {
+      i32 s = 0;
+      for (int j = 0; j <= mx; ++j) s += basis[j][x] * gr[j];
+      r[y * n + x] = (s + (1 << 11)) >> 12;
+    }
+  }
 }
 
 int dequant_level(int level, int qp, int log2) {
@@ -194,6 +206,111 @@ int chroma_inter_sample(const HostSurface& r, int c, int xi, int yi, int fx, int
   return s >> 6;
 }
 
+// 14-bit intermediate prediction of a w x h luma block at integer position (x0, y0) with
+// fraction (fx, fy), separable (§8.5.3.3.3.1): the (w + 7) x (h + 7) source window is read in
+// place when it lies inside the picture, else gathered with edge clamping.
+static void mc_luma(const HostSurface& r, int x0, int y0, int w, int h, int fx, int fy, i16* dst) {
+  const int W = r.coded_w, H = r.coded_h;
+  u8 win[71 * 71];
+  const u8* src;
+  int ss;
+  if (x0 - 3 >= 0 && y0 - 3 >= 0 && x0 + w + 4 <= W && y0 + h + 4 <= H) {
+    src = &r.y[size_t(y0 - 3) * W + size_t(x0 - 3)];
+    ss = W;
+  } else {
+    ss = w + 7;
+    for (int j = 0; j < h + 7; ++j) {
+      const size_t row = size_t(std::clamp(y0 - 3 + j, 0, H - 1)) * W;
+      for (int i = 0; i < w + 7; ++i) win[j * ss + i] = r.y[row + size_t(std::clamp(x0 - 3 + i, 0, W - 1))];
+    }
+    src = win;
+  }
+  const i8* fh = kLumaFilter[fx];
+  const i8* fv = kLumaFilter[fy];
+  if (!fx && !fy) {
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) dst[j * w + i] = i16(src[(j + 3) * ss + i + 3] << 6);
+  } else if (!fy) {
+    for (int j = 0; j < h; ++j) {
+      const u8* p = src + (j + 3) * ss;
+      for (int i = 0; i < w; ++i) {
+        int s = 0;
+        for (int k = 0; k < 8; ++k) s += fh[k] * p[i + k];
+        dst[j * w + i] = i16(s);
+      }
+    }
+  } else if (!fx) {
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        int s = 0;
+        for (int k = 0; k < 8; ++k) s += fv[k] * src[(j + k) * ss + i + 3];
+        dst[j * w + i] = i16(s);
+      }
+  } else {
+    i16 tmp[71 * 64];
+    for (int j = 0; j < h + 7; ++j) {
+      const u8* p = src + j * ss;
+      for (int i = 0; i < w; ++i) {
+        int s = 0;
+        for (int k = 0; k < 8; ++k) s += fh[k] * p[i + k];
+        tmp[j * w + i] = i16(s);
+      }
+    }
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        int s = 0;
+        for (int k = 0; k < 8; ++k) s += fv[k] * tmp[(j + k) * w + i];
+        dst[j * w + i] = i16(s >> 6);
+      }
+  }
+}
+
+// Same for one chroma component (4-tap, eighth-sample fraction) of the NV12 plane.
+static void mc_chroma(const HostSurface& r, int c, int x0, int y0, int w, int h, int fx, int fy, i16* dst) {
+  const int W = r.coded_w / 2, H = r.coded_h / 2, st = r.coded_w;
+  u8 win[35 * 35];
+  const int ss = w + 3;
+  for (int j = 0; j < h + 3; ++j) {
+    const size_t row = size_t(std::clamp(y0 - 1 + j, 0, H - 1)) * st;
+    if (x0 - 1 >= 0 && x0 + w + 2 <= W) {
+      const u8* p = &r.uv[row + 2 * size_t(x0 - 1) + size_t(c)];
+      for (int i = 0; i < w + 3; ++i) win[j * ss + i] = p[2 * i];
+    } else {
+      for (int i = 0; i < w + 3; ++i) win[j * ss + i] = r.uv[row + 2 * size_t(std::clamp(x0 - 1 + i, 0, W - 1)) + size_t(c)];
+    }
+  }
+  const i8* fh = kChromaFilter[fx];
+  const i8* fv = kChromaFilter[fy];
+  if (!fx && !fy) {
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) dst[j * w + i] = i16(win[(j + 1) * ss + i + 1] << 6);
+  } else if (!fy) {
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        const u8* p = win + (j + 1) * ss + i;
+        dst[j * w + i] = i16(fh[0] * p[0] + fh[1] * p[1] + fh[2] * p[2] + fh[3] * p[3]);
+      }
+  } else if (!fx) {
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        const u8* p = win + j * ss + i + 1;
+        dst[j * w + i] = i16(fv[0] * p[0] + fv[1] * p[ss] + fv[2] * p[2 * ss] + fv[3] * p[3 * ss]);
+      }
+  } else {
+    i16 tmp[35 * 32];
+    for (int j = 0; j < h + 3; ++j)
+      for (int i = 0; i < w; ++i) {
+        const u8* p = win + j * ss + i;
+        tmp[j * w + i] = i16(fh[0] * p[0] + fh[1] * p[1] + fh[2] * p[2] + fh[3] * p[3]);
+      }
+    for (int j = 0; j < h; ++j)
+      for (int i = 0; i < w; ++i) {
+        const i16* p = tmp + j * w + i;
+        dst[j * w + i] = i16((fv[0] * p[0] + fv[1] * p[w] + fv[2] * p[2 * w] + fv[3] * p[3 * w]) >> 6);
+      }
+  }
+}
+
 void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const MvField& m, u8* y, int ys, u8* cb,
                 u8* cr, int cs) {
   const SliceInfo& sl = pc.slices[size_t(si)];
@@ -205,27 +322,44 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
       r[l] = &sl.list[l][size_t(m.ref[l])]->s;
     }
   const bool bi = r[0] && r[1];
+  if (!bi) {  // uni-prediction with a full-sample vector inside the picture: a plain copy
+    const int l = r[0] ? 0 : 1;
+    const HostSurface& s = *r[l];
+    const int mx = m.mv[l][0], my = m.mv[l][1];
+    const int xi = xPb + (mx >> 2), yi = yPb + (my >> 2);
+    if (!(mx & 7) && !(my & 7) && xi >= 0 && yi >= 0 && xi + w <= s.coded_w && yi + h <= s.coded_h) {
+      const int st = s.coded_w;
+      for (int j = 0; j < h; ++j) std::memcpy(y + j * ys, &s.y[size_t(yi + j) * st + size_t(xi)], size_t(w));
+      for (int j = 0; j < h / 2; ++j) {
+        const u8* src = &s.uv[size_t(yi / 2 + j) * st + size_t(xi)];
+        for (int i = 0; i < w / 2; ++i) {
+          cb[j * cs + i] = src[2 * i];
+          cr[j * cs + i] = src[2 * i + 1];
+        }
+      }
+      return;
+    }
+  }
+  i16 p[2][64 * 64];
+  int np = 0;
+  for (int l = 0; l < 2; ++l)
+    if (r[l]) mc_luma(*r[l], xPb + (m.mv[l][0] >> 2), yPb + (m.mv[l][1] >> 2), w, h, m.mv[l][0] & 3, m.mv[l][1] & 3, p[np++]);
   for (int j = 0; j < h; ++j)
     for (int i = 0; i < w; ++i) {
-      int p[2] = {0, 0};
-      for (int l = 0; l < 2; ++l)
-        if (r[l])
-          p[l] = luma_inter_sample(*r[l], xPb + i + (m.mv[l][0] >> 2), yPb + j + (m.mv[l][1] >> 2), m.mv[l][0] & 3,
-                                   m.mv[l][1] & 3);
-      const int v = bi ? (p[0] + p[1] + 64) >> 7 : ((r[0] ? p[0] : p[1]) + 32) >> 6;
+      const int v = bi ? (p[0][j * w + i] + p[1][j * w + i] + 64) >> 7 : (p[0][j * w + i] + 32) >> 6;
       y[j * ys + i] = u8(std::clamp(v, 0, 255));
     }
   const int xc = xPb / 2, yc = yPb / 2, wc = w / 2, hc = h / 2;
   for (int c = 0; c < 2; ++c) {
+    np = 0;
+    for (int l = 0; l < 2; ++l)
+      if (r[l])
+        mc_chroma(*r[l], c, xc + (m.mv[l][0] >> 3), yc + (m.mv[l][1] >> 3), wc, hc, m.mv[l][0] & 7, m.mv[l][1] & 7,
+                  p[np++]);
     u8* out = c == 0 ? cb : cr;
     for (int j = 0; j < hc; ++j)
       for (int i = 0; i < wc; ++i) {
-        int p[2] = {0, 0};
-        for (int l = 0; l < 2; ++l)
-          if (r[l])
-            p[l] = chroma_inter_sample(*r[l], c, xc + i + (m.mv[l][0] >> 3), yc + j + (m.mv[l][1] >> 3),
-                                       m.mv[l][0] & 7, m.mv[l][1] & 7);
-        const int v = bi ? (p[0] + p[1] + 64) >> 7 : ((r[0] ? p[0] : p[1]) + 32) >> 6;
+        const int v = bi ? (p[0][j * wc + i] + p[1][j * wc + i] + 64) >> 7 : (p[0][j * wc + i] + 32) >> 6;
         out[j * cs + i] = u8(std::clamp(v, 0, 255));
       }
   }
