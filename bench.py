@@ -133,6 +133,9 @@ def spawn_ranks(n: int) -> int:
 
 
 def describe_streams(a, compressed):
+    if compressed and a.codec == "h265":
+        return (f"HEVC Main CABAC I/P/B, {a.bframes} B per mini-GOP, CTB 32, merge/AMVP/TMVP, "
+                "deblocking; CPU reconstruction (general H.265 decoder) + gfx950 block update / NV12->BGR24")
     if compressed and a.profile == "baseline":
         return "Baseline CAVLC I/P"
     if compressed:
@@ -363,7 +366,7 @@ def main():
                         letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes,
                         stages=a.stages, queue=a.lane_queue)
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
-    compressed = a.content == "avc" and a.codec == "h264"
+    compressed = a.content == "avc"  # (h265: general HEVC Main streams, CPU reconstruction)
     cfg = make_cfg(vep, a, rank, compressed)
     stream_desc = describe_streams(a, compressed)
     if a.source == "rtsp":
@@ -525,7 +528,10 @@ def main():
                                              "reference clients' pattern): includes waiting for "
                                              "the camera's next decoded frame",
             "rocdecode_available": bool(vep.rocdecode_available()),
-            "decoder_backend": ("native H.264 decoder: CPU " + ("CAVLC" if a.profile == "baseline" or a.cavlc
+            "decoder_backend": ("native H.265 Main decoder: CPU CABAC coding-tree parse + reconstruction "
+                                "(intra, merge/AMVP MC, transforms, deblocking, SAO); gfx950 changed-block "
+                                "update + NV12->BGR24 (rocDecode absent in image)" if compressed and a.codec == "h265" else
+                                "native H.264 decoder: CPU " + ("CAVLC" if a.profile == "baseline" or a.cavlc
                                                                else "CABAC") + " macroblock-layer parse + dequant; "
                                 "gfx950 HIP motion compensation, intra + deblocking wavefronts, "
                                 "NV12->BGR24 (rocDecode absent in image)" if compressed else
