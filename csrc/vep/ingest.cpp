@@ -1,6 +1,7 @@
 // Ingest session / supervisor implementation. See ingest.h.
 #include "ingest.h"
 
+#include <cstdlib>
 #include <tuple>
 
 #include <sys/syscall.h>
@@ -9,6 +10,51 @@
 #include <algorithm>
 
 namespace vep {
+
+// Liveness token of the pooled mode: timers and connector tasks enter() before touching the
+// session and leave() after; stop() waits for the ones inside and turns later ones away.
+struct IngestSession::Guard {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool stopped = false;
+  int busy = 0;
+  bool enter() {
+    std::lock_guard<std::mutex> g(mu);
+    if (stopped) return false;
+    ++busy;
+    return true;
+  }
+  void leave() {
+    std::lock_guard<std::mutex> g(mu);
+    --busy;
+    cv.notify_all();
+  }
+  void stop() {
+    std::unique_lock<std::mutex> g(mu);
+    stopped = true;
+    cv.wait(g, [this] { return busy == 0; });
+  }
+};
+
+// The session's socket on the shared epoll loop.
+class IngestSession::Handler : public IoHandler {
+ public:
+  Handler(IngestSession* s, std::shared_ptr<net::RtspClient> c) : s_(s), c_(std::move(c)) {}
+  bool on_readable() override {
+    return c_->read_available([this](const AuPtr& au) { s_->on_au(au); }, why_);
+  }
+  bool on_tick() override { return c_->maintain(why_); }
+  void on_closed() override { s_->on_stream_end(why_, c_->bytes(), c_->lost()); }
+  const net::RtspClient& client() const { return *c_; }
+
+ private:
+  IngestSession* s_;
+  std::shared_ptr<net::RtspClient> c_;
+  std::string why_;
+};
+
+// AUs a camera's parse strand may hold before ingest drops to the next keyframe (~8 s at 30 fps).
+constexpr size_t kMaxParseBacklog = 256;
 
 IngestSession::IngestSession(Worker& w, int cam, IngestConfig cfg,
                              std::shared_ptr<mux::Archiver> archiver)
@@ -22,18 +68,186 @@ void IngestSession::log(bool err, const std::string& s) {
 
 void IngestSession::start() {
   stop_ = false;
-  th_ = std::thread([this] { run(); });
+  const char* th = std::getenv("VEP_INGEST_THREADS");
+  pooled_ = !(th && th[0] == '1');
+  if (!pooled_) {
+    th_ = std::thread([this] { run(); });
+    return;
+  }
+  svc_ = IngestServices::acquire();
+  guard_ = std::make_shared<Guard>();
+  drop_to_key_ = false;
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.pid = int(::getpid());  // (no thread of its own: the hub process)
+  }
+  schedule_connect(0);
 }
 
 void IngestSession::stop() {
   stop_ = true;
   if (th_.joinable()) th_.join();
+  if (guard_) guard_->stop();  // no timer / connector task of this session runs from here on
+  std::shared_ptr<Handler> h;
+  {
+    std::lock_guard<std::mutex> g(handler_mu_);
+    h.swap(handler_);
+  }
+  if (h) {
+    svc_->io.remove(h);  // synchronous: no socket callback runs after this
+    std::lock_guard<std::mutex> g(mu_);
+    st_.bytes += h->client().bytes();
+    st_.lost += h->client().lost();
+  }
+  pub_.reset();
+  gop_.clear();
+  seen_key_ = false;
+  prev_proxy_ = false;
   std::lock_guard<std::mutex> g(mu_);
   if (st_.status != "created") {
     st_.status = "exited";
     st_.running = st_.restarting = false;
     st_.finished_at_ms = now_ms();
   }
+}
+
+void IngestSession::schedule_connect(int delay_ms) {
+  std::weak_ptr<Guard> wg = guard_;
+  svc_->timers.at(mono_us() / 1000 + delay_ms, [this, wg] {
+    auto g = wg.lock();
+    if (!g || !g->enter()) return;
+    try {
+      connect_once();
+    } catch (...) {
+    }
+    g->leave();
+  });
+}
+
+void IngestSession::mark_failed(const std::string& err, bool connect_error) {
+  std::lock_guard<std::mutex> g(mu_);
+  st_.status = "restarting";
+  st_.running = false;
+  st_.restarting = true;
+  if (connect_error) st_.exit_code = 1;  // rtsp_to_rtmp.py:76-78 os._exit(1)
+  st_.error = err;
+  st_.finished_at_ms = now_ms();
+  st_.restart_count++;
+  st_.failing_streak++;
+  st_.health = st_.failing_streak >= 3 ? "unhealthy" : "starting";
+}
+
+void IngestSession::connect_once() {
+  if (stop_.load()) return;
+  net::RtspClientOptions opt;
+  opt.timeout_ms = cfg_.timeout_ms;
+  auto client = std::make_shared<net::RtspClient>(cfg_.rtsp_url, opt);
+  net::RtspStreamInfo info;
+  try {
+    info = client->open();
+  } catch (const std::exception& e) {
+    log(true, std::string("failed to connect to RTSP camera ") + e.what());
+    mark_failed(e.what(), true);
+    int streak;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      streak = st_.failing_streak;
+    }
+    const int shift = std::min(streak - 1, 5);
+    schedule_connect(std::min(cfg_.max_backoff_ms, cfg_.reconnect_delay_ms << shift));
+    return;
+  }
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.status = "running";
+    st_.running = true;
+    st_.restarting = false;
+    st_.dead = false;
+    st_.exit_code = 0;
+    st_.error.clear();
+    st_.started_at_ms = now_ms();
+    st_.failing_streak = 0;
+    st_.health = "healthy";
+    st_.fps = info.framerate;
+  }
+  ps_ = ParamSets{};
+  ps_.codec = info.codec;
+  for (auto& ps : info.param_sets) ps_.absorb(ps.data(), ps.size());
+  gop_.clear();
+  seen_key_ = false;
+  prev_proxy_ = false;
+  drop_to_key_ = false;
+  log(false, "connected to " + cfg_.name + " (" + (info.codec == Codec::kH264 ? "H.264" : "H.265") + ")");
+  auto h = std::make_shared<Handler>(this, client);
+  {
+    std::lock_guard<std::mutex> g(handler_mu_);
+    handler_ = h;
+  }
+  svc_->io.add(client->fd(), h);
+}
+
+// Socket loop thread, inside the handler's callback: record the end, then clean up and schedule
+// the reconnect on the connector pool (the RTMP sender join must not stall the loop).
+void IngestSession::on_stream_end(const std::string& why, u64 bytes, u64 lost) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    st_.bytes += bytes;
+    st_.lost += lost;
+  }
+  if (stop_.load()) return;
+  log(false, "rtsp stopped streaming (" + why + ")...waiting for camera to reappear");
+  mark_failed(why, false);
+  std::weak_ptr<Guard> wg = guard_;
+  svc_->connect.post([this, wg] {
+    auto g = wg.lock();
+    if (!g || !g->enter()) return;
+    try {
+      after_stream_end();
+    } catch (...) {
+    }
+    g->leave();
+  });
+}
+
+void IngestSession::after_stream_end() {
+  {
+    std::lock_guard<std::mutex> g(handler_mu_);
+    handler_.reset();
+  }
+  pub_.reset();
+  gop_.clear();
+  seen_key_ = false;
+  prev_proxy_ = false;
+  schedule_connect(cfg_.reconnect_delay_ms);
+}
+
+void IngestSession::decode(const std::shared_ptr<Camera>& cam, const AuPtr& au) {
+  if (!pooled_) {
+    cam->on_access_unit(au);
+    return;
+  }
+  // parse off the socket thread, in order, on the camera's strand of the shared parse pool
+  const u64 key = u64(reinterpret_cast<uintptr_t>(cam.get()));
+  if (drop_to_key_) {
+    if (!au->keyframe) {
+      cam->skipped.fetch_add(1, std::memory_order_relaxed);
+      return;
+    }
+    drop_to_key_ = false;
+  } else if (svc_->parse.depth(key) >= kMaxParseBacklog) {
+    drop_to_key_ = true;
+    cam->skipped.fetch_add(1, std::memory_order_relaxed);
+    log(true, "parse backlog full: dropping packets until the next keyframe");
+    return;
+  }
+  svc_->parse.post(key, [cam, au] {
+    try {
+      cam->on_access_unit(au);
+    } catch (const std::exception& e) {
+      cam->errors.fetch_add(1);
+      cam->logs.add(true, std::string("failed to decode packet: ") + e.what());
+    }
+  });
 }
 
 SessionState IngestSession::state() const {
@@ -74,7 +288,7 @@ void IngestSession::on_au(const AuPtr& au) {
   if (seen_key_) gop_.push_back(au);
 
   // --- decode scheduling (lazy / keyframe-only / catch-up) lives in the camera
-  cam->on_access_unit(au);
+  decode(cam, au);
 
   // --- RTMP pass-through (rtsp_to_rtmp.py:127-139, :162-182), sent off this thread
   const bool want = cam->proxy_rtmp.load() && !cfg_.rtmp_url.empty();

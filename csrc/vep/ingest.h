@@ -18,6 +18,7 @@
 #include <string>
 #include <thread>
 
+#include "ioloop.h"
 #include "mux.h"
 #include "net.h"
 #include "runtime.h"
@@ -90,20 +91,41 @@ class RtmpSender {
   i64 ts0_ = -1;
 };
 
+// Two execution modes. Pooled (the default): the RTSP handshake runs on the shared connector
+// pool, the socket is then served by the shared epoll loop (IngestServices::io) and access units
+// are parsed on the camera's strand of the shared parse pool; reconnect back-off is a timer, so a
+// session owns no thread. Threaded (VEP_INGEST_THREADS=1): one blocking thread per camera that
+// receives and parses, as in round 1.
 class IngestSession {
  public:
   IngestSession(Worker& w, int cam, IngestConfig cfg, std::shared_ptr<mux::Archiver> archiver);
   ~IngestSession();
   void start();
-  void stop();  // joins the thread
+  void stop();  // synchronous: no callback of this session runs after it returns
   SessionState state() const;
   const IngestConfig& config() const { return cfg_; }
   void log(bool err, const std::string& s);
+  bool pooled() const { return pooled_; }
 
  private:
+  struct Guard;  // liveness token of the pooled mode's timers / connector tasks
+  class Handler;
   void run();
   void on_au(const AuPtr& au);
+  void decode(const std::shared_ptr<Camera>& cam, const AuPtr& au);
   bool sleep_interruptible(int ms);
+  // pooled mode
+  void schedule_connect(int delay_ms);
+  void connect_once();
+  void on_stream_end(const std::string& why, u64 bytes, u64 lost);
+  void after_stream_end();
+  void mark_failed(const std::string& err, bool connect_error);
+  bool pooled_ = true;
+  std::shared_ptr<IngestServices> svc_;
+  std::shared_ptr<Guard> guard_;
+  std::shared_ptr<Handler> handler_;
+  std::mutex handler_mu_;
+  bool drop_to_key_ = false;  // parse backlog overflowed: skip until the next keyframe
   Worker& w_;
   int cam_;
   IngestConfig cfg_;

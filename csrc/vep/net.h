@@ -109,11 +109,21 @@ class RtspClient {
   RtspStreamInfo open();
   // Read loop; returns the reason the stream ended.
   std::string run(const AuCallback& cb, const std::atomic<bool>& stop);
+  // Event-driven use (IoLoop): after open(), read whatever the socket holds without blocking and
+  // deliver the completed access units; false (with the reason) when the stream ended.
+  bool read_available(const AuCallback& cb, std::string& why);
+  // Periodic upkeep between reads: session keep-alive, stall timeout (false = timed out).
+  bool maintain(std::string& why);
+  int fd() const { return fd_; }
   void close();
   u64 bytes() const { return bytes_; }
   u64 lost() const { return dep_ ? dep_->lost() : 0; }
 
  private:
+  bool parse_buffer(std::vector<AuPtr>& aus, std::string& why);
+  void emit(std::vector<AuPtr>& aus, const AuCallback& cb);
+  bool params_sent_ = false;
+  i64 last_ka_us_ = 0;
   std::string request(const std::string& method, const std::string& uri,
                       const std::string& extra, std::string* body);
   std::string url_;

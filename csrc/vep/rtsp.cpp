@@ -227,7 +227,8 @@ RtspStreamInfo RtspClient::open() {
   session_.clear();
   cseq_ = 0;
   fd_ = connect_tcp(u_.host, u_.port, opt_.timeout_ms);
-  last_rx_us_ = mono_us();
+  last_rx_us_ = last_ka_us_ = mono_us();
+  params_sent_ = false;
   const std::string url = clean_url(u_);
   std::string sdp;
   request("OPTIONS", url, "", nullptr);
@@ -294,103 +295,134 @@ RtspStreamInfo RtspClient::open() {
   return info;
 }
 
-std::string RtspClient::run(const AuCallback& cb, const std::atomic<bool>& stop) {
-  VEP_CHECK(fd_ >= 0 && dep_, "RtspClient::run before open()");
+// Parse every complete interleaved frame / RTSP message in the receive buffer; access units go
+// to `aus`. Returns false (with the reason) on a framing error.
+bool RtspClient::parse_buffer(std::vector<AuPtr>& aus, std::string& why) {
+  for (;;) {
+    size_t avail = rbuf_.size() - rpos_;
+    if (avail < 4) break;
+    const u8* p = rbuf_.data() + rpos_;
+    if (p[0] == '$') {
+      size_t len = size_t(p[2]) << 8 | p[3];
+      if (avail < 4 + len) break;
+      if (p[1] == 0) {
+        RtpHeader h;
+        const u8* pl;
+        size_t pn;
+        if (parse_rtp(p + 4, len, h, &pl, &pn) && h.pt == info_.payload_type) dep_->push(h, pl, pn, aus);
+      }
+      rpos_ += 4 + len;
+    } else {
+      std::string view(reinterpret_cast<const char*>(p), avail);
+      size_t he = view.find("\r\n\r\n");
+      if (he == std::string::npos) {
+        if (avail > 8192) {
+          why = "protocol error: unframed data";
+          return false;
+        }
+        break;
+      }
+      Message m = parse_head(view.substr(0, he + 2));
+      size_t cl = m.hdr.count("content-length") ? size_t(std::atol(m.hdr["content-length"].c_str())) : 0;
+      if (avail < he + 4 + cl) break;
+      rpos_ += he + 4 + cl;  // keep-alive response or server request: ignore
+    }
+  }
+  if (rpos_ > (1u << 20) || rpos_ == rbuf_.size()) {
+    rbuf_.erase(rbuf_.begin(), rbuf_.begin() + long(rpos_));
+    rpos_ = 0;
+  }
+  return true;
+}
+
+// Deliver access units; the first keyframe gets the SDP parameter sets prepended when it does
+// not carry its own.
+void RtspClient::emit(std::vector<AuPtr>& aus, const AuCallback& cb) {
+  for (auto& au : aus) {
+    if (!params_sent_ && au->keyframe && !info_.param_sets.empty()) {
+      bool has_sps = false;
+      for (size_t i = 0; i < au->nals.size(); ++i) {
+        int t = info_.codec == Codec::kH264 ? (au->nal(i)[0] & 0x1f) : ((au->nal(i)[0] >> 1) & 0x3f);
+        has_sps |= (info_.codec == Codec::kH264) ? t == 7 : t == 33;
+      }
+      params_sent_ = true;
+      if (!has_sps) {
+        auto a2 = std::make_shared<AccessUnit>();
+        a2->codec = au->codec;
+        a2->pts = au->pts;
+        a2->dts = au->dts;
+        a2->duration = au->duration;
+        a2->keyframe = au->keyframe;
+        a2->corrupt = au->corrupt;
+        a2->arrival_ms = au->arrival_ms;
+        a2->seq = au->seq;
+        for (auto& ps : info_.param_sets) a2->add_nal(ps.data(), ps.size());
+        for (size_t i = 0; i < au->nals.size(); ++i) a2->add_nal(au->nal(i), au->nal_size(i));
+        a2->pin();
+        cb(a2);
+        continue;
+      }
+    }
+    cb(au);
+  }
+  aus.clear();
+}
+
+bool RtspClient::maintain(std::string& why) {
+  const i64 now = mono_us();
+  if (now - last_ka_us_ > 25'000'000) {  // session keep-alive
+    std::string ka = "GET_PARAMETER " + clean_url(u_) + " RTSP/1.0\r\nCSeq: " + std::to_string(++cseq_) +
+                     "\r\nSession: " + session_ + "\r\n\r\n";
+    send_all(fd_, reinterpret_cast<const u8*>(ka.data()), ka.size(), opt_.timeout_ms);
+    last_ka_us_ = now;
+  }
+  if ((now - last_rx_us_) / 1000 >= opt_.timeout_ms) {  // socket stall: nothing for timeout_ms
+    why = "timeout";
+    return false;
+  }
+  return true;
+}
+
+bool RtspClient::read_available(const AuCallback& cb, std::string& why) {
+  VEP_CHECK(fd_ >= 0 && dep_, "RtspClient::read_available before open()");
   std::vector<AuPtr> aus;
-  bool params_sent = false;
-  i64 last_ka = mono_us();
   u8 tmp[1 << 16];
-  while (!stop.load()) {
-    // parse everything buffered
-    for (;;) {
-      size_t avail = rbuf_.size() - rpos_;
-      if (avail < 4) break;
-      const u8* p = rbuf_.data() + rpos_;
-      if (p[0] == '$') {
-        size_t len = size_t(p[2]) << 8 | p[3];
-        if (avail < 4 + len) break;
-        if (p[1] == 0) {
-          RtpHeader h;
-          const u8* pl;
-          size_t pn;
-          if (parse_rtp(p + 4, len, h, &pl, &pn) && h.pt == info_.payload_type)
-            dep_->push(h, pl, pn, aus);
-        }
-        rpos_ += 4 + len;
-      } else {
-        std::string view(reinterpret_cast<const char*>(p), avail);
-        size_t he = view.find("\r\n\r\n");
-        if (he == std::string::npos) {
-          if (avail > 8192) return "protocol error: unframed data";
-          break;
-        }
-        Message m = parse_head(view.substr(0, he + 2));
-        size_t cl = m.hdr.count("content-length") ? size_t(std::atol(m.hdr["content-length"].c_str())) : 0;
-        if (avail < he + 4 + cl) break;
-        rpos_ += he + 4 + cl;  // keep-alive response or server request: ignore
-      }
-    }
-    if (rpos_ > (1u << 20) || rpos_ == rbuf_.size()) {
-      rbuf_.erase(rbuf_.begin(), rbuf_.begin() + long(rpos_));
-      rpos_ = 0;
-    }
-    for (auto& au : aus) {
-      if (!params_sent && au->keyframe && !info_.param_sets.empty()) {
-        // make sure the first keyframe carries SPS/PPS from the SDP
-        bool has_sps = false;
-        for (size_t i = 0; i < au->nals.size(); ++i) {
-          int t = info_.codec == Codec::kH264 ? (au->nal(i)[0] & 0x1f) : ((au->nal(i)[0] >> 1) & 0x3f);
-          has_sps |= (info_.codec == Codec::kH264) ? t == 7 : t == 33;
-        }
-        if (!has_sps) {
-          auto a2 = std::make_shared<AccessUnit>();
-          a2->codec = au->codec;
-          a2->pts = au->pts;
-          a2->dts = au->dts;
-          a2->duration = au->duration;
-          a2->keyframe = au->keyframe;
-          a2->corrupt = au->corrupt;
-          a2->arrival_ms = au->arrival_ms;
-          a2->seq = au->seq;
-          for (auto& ps : info_.param_sets) a2->add_nal(ps.data(), ps.size());
-          for (size_t i = 0; i < au->nals.size(); ++i) a2->add_nal(au->nal(i), au->nal_size(i));
-          a2->pin();
-          cb(a2);
-          params_sent = true;
-          continue;
-        }
-        params_sent = true;
-      }
-      cb(au);
-    }
-    aus.clear();
-    if (mono_us() - last_ka > 25'000'000) {  // session keep-alive
-      std::string ka = "GET_PARAMETER " + clean_url(u_) + " RTSP/1.0\r\nCSeq: " +
-                       std::to_string(++cseq_) + "\r\nSession: " + session_ + "\r\n\r\n";
-      send_all(fd_, reinterpret_cast<const u8*>(ka.data()), ka.size(), opt_.timeout_ms);
-      last_ka = mono_us();
-    }
-    pollfd p{fd_, POLLIN, 0};
-    int pr = ::poll(&p, 1, std::min(opt_.timeout_ms, 200));
-    if (pr == 0) {
-      // detect socket stall: nothing for timeout_ms
-      i64 quiet = (mono_us() - last_rx_us_) / 1000;
-      if (quiet >= opt_.timeout_ms) return "timeout";
-      continue;
-    }
-    if (pr < 0) {
-      if (errno == EINTR) continue;
-      return "poll error";
-    }
-    ssize_t k = ::recv(fd_, tmp, sizeof(tmp), 0);
+  for (;;) {
+    ssize_t k = ::recv(fd_, tmp, sizeof(tmp), MSG_DONTWAIT);
+    if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
+    if (k < 0 && errno == EINTR) continue;
     if (k <= 0) {
+      std::string perr;
+      parse_buffer(aus, perr);
       dep_->flush(aus);
-      for (auto& au : aus) cb(au);
-      return k == 0 ? "eof" : "recv error";
+      emit(aus, cb);
+      why = k == 0 ? "eof" : "recv error";
+      return false;
     }
     last_rx_us_ = mono_us();
     bytes_ += u64(k);
     rbuf_.insert(rbuf_.end(), tmp, tmp + k);
+    if (!parse_buffer(aus, why)) return false;
+    emit(aus, cb);
+    if (size_t(k) < sizeof(tmp)) break;  // drained
+  }
+  return true;
+}
+
+std::string RtspClient::run(const AuCallback& cb, const std::atomic<bool>& stop) {
+  VEP_CHECK(fd_ >= 0 && dep_, "RtspClient::run before open()");
+  last_ka_us_ = mono_us();
+  std::string why;
+  while (!stop.load()) {
+    if (!maintain(why)) return why;
+    pollfd p{fd_, POLLIN, 0};
+    int pr = ::poll(&p, 1, std::min(opt_.timeout_ms, 200));
+    if (pr == 0) continue;
+    if (pr < 0) {
+      if (errno == EINTR) continue;
+      return "poll error";
+    }
+    if (!read_available(cb, why)) return why;
   }
   return "stopped";
 }
