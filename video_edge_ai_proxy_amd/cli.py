@@ -29,6 +29,8 @@ def cmd_serve(a):
         cfg.port = a.port
     if a.grpc_port is not None:
         cfg.grpc_port = a.grpc_port
+    if a.isolate:
+        cfg.gpu.isolation = "process"
     devices = [int(x) for x in a.devices.split(",")] if a.devices else None
     run_forever(cfg, host=a.bind, devices=devices)
 
@@ -155,6 +157,9 @@ def main(argv=None):
     s.add_argument("--grpc-port", type=int, default=None)
     s.add_argument("--devices", default="", help="comma-separated GPU ids; -1 = CPU backend")
     s.add_argument("--log-level", default="info")
+    s.add_argument("--isolate", action="store_true",
+                   help="one supervised worker process per GPU (gpu.isolation: process): a native "
+                        "fault restarts that GPU's process, the other cameras keep running")
     s.set_defaults(fn=cmd_serve)
 
     c = sub.add_parser("camera")

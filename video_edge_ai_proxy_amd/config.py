@@ -63,6 +63,8 @@ class GpuConfig:
     mean: list = field(default_factory=lambda: [0.0, 0.0, 0.0])
     std: list = field(default_factory=lambda: [1.0, 1.0, 1.0])
     idle_cutoff_ms: int = 10000                  # rtsp_to_rtmp.py:144-145
+    isolation: str = "thread"                    # thread (one process) | process (a supervised
+                                                 # worker process per GPU, engine/isolated.py)
 
 
 @dataclass

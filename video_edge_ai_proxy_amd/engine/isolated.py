@@ -1,0 +1,310 @@
+"""Isolated hub: one supervised worker process per GPU (``gpu.isolation: process``).
+
+The in-process :class:`Hub` runs every camera of the node in one process, so a native fault in
+any camera's bitstream parse or a GPU error takes all cameras down. ``ProcessHub`` keeps the same
+interface for the servers and services but places each GPU's cameras in a child process
+(``engine/child.py``, started as a fresh interpreter, never by exec from a GPU process) and
+supervises them: when a child dies, its cameras report ``restarting``, a fresh child is started
+for the device and the cameras are re-added with their pass-through state — the reference's
+per-camera ``restart: always`` containers (server/services/rtsp_process_manager.go:70-81,
+:106-115) at per-GPU granularity, without one process per camera.
+
+Calls travel over authenticated local connections (a small pool per child, so a blocking
+``latest_frame_bytes`` does not hold the others up). The batched consumer tensor of the
+in-process hub is not offered here; the multi-process form of it is ``parallel.ConsumerBatch``
+(one RCCL all-gather across rank processes).
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import logging
+import os
+import queue
+import secrets
+import select
+import subprocess
+import sys
+import threading
+import time
+from multiprocessing.connection import Client
+from typing import Optional
+
+from ..config import Config
+from .hub import CameraExists, CameraHandle, CameraNotFound, place_camera
+
+log = logging.getLogger("vep.isolated")
+
+_PKG_PARENT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+class WorkerRestarting(RuntimeError):
+    """The camera's worker process died and is being restarted."""
+
+
+_ERRORS = {"CameraNotFound": CameraNotFound, "CameraExists": CameraExists, "KeyError": KeyError,
+           "ValueError": ValueError}
+
+
+class _Child:
+    def __init__(self, device: int, cfg_json: str, nconn: int = 8, start_timeout_s: float = 180.0):
+        self.device = device
+        key = secrets.token_bytes(16)
+        env = dict(os.environ, VEP_CHILD_KEY=key.hex())
+        env["PYTHONPATH"] = _PKG_PARENT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        self.proc = subprocess.Popen(
+            [sys.executable, "-m", "video_edge_ai_proxy_amd.engine.child", "--device", str(device),
+             "--config", cfg_json],
+            stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env)
+        line = b""
+        deadline = time.time() + start_timeout_s
+        while not line.endswith(b"\n"):
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"worker process for device {device} exited during start "
+                                   f"(code {self.proc.returncode})")
+            r, _, _ = select.select([self.proc.stdout], [], [], 0.5)
+            if r:
+                ch = os.read(self.proc.stdout.fileno(), 1)
+                if not ch:
+                    raise RuntimeError(f"worker process for device {device} closed its output")
+                line += ch
+            if time.time() > deadline:
+                self.proc.kill()
+                raise RuntimeError(f"worker process for device {device} did not start in time")
+        hello = json.loads(line)
+        self.pid = int(hello["pid"])
+        self.port = int(hello["port"])
+        self.free: queue.Queue = queue.Queue()
+        for _ in range(nconn):
+            self.free.put(Client(("127.0.0.1", self.port), authkey=key))
+        threading.Thread(target=self._drain, daemon=True).start()  # stray stdout never blocks it
+
+    def _drain(self) -> None:
+        try:
+            while self.proc.stdout.read(4096):
+                pass
+        except Exception:  # noqa: BLE001
+            pass
+
+    def alive(self) -> bool:
+        return self.proc.poll() is None
+
+    def call(self, method: str, *args, **kwargs):
+        if not self.alive():
+            raise WorkerRestarting(f"worker process for device {self.device} is restarting")
+        conn = self.free.get(timeout=60)
+        try:
+            conn.send((method, args, kwargs))
+            r = conn.recv()
+        except (EOFError, OSError) as e:
+            raise WorkerRestarting(f"worker process for device {self.device} died: {e}") from e
+        self.free.put(conn)
+        if r[0] == "ok":
+            return r[1]
+        raise _ERRORS.get(r[1], RuntimeError)(r[2])
+
+    def close(self, timeout_s: float = 20.0) -> None:
+        try:
+            self.proc.stdin.close()  # the child shuts its hub down and exits
+        except Exception:  # noqa: BLE001
+            pass
+        try:
+            self.proc.wait(timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            self.proc.kill()
+            self.proc.wait()
+
+
+class _WorkerView:
+    """Worker statistics of one child (what /metrics and /health read from hub.workers)."""
+
+    def __init__(self, hub: "ProcessHub", index: int):
+        self._hub, self._i = hub, index
+
+    def _stats(self) -> dict:
+        try:
+            return self._hub._child(self._i).call("worker_stats")
+        except Exception:  # noqa: BLE001 — a restarting child reports zeros
+            return {"batches": 0, "frames": 0, "gpu_ms_total": 0.0, "direct_reads": False}
+
+    @property
+    def batches(self):
+        return self._stats()["batches"]
+
+    @property
+    def frames(self):
+        return self._stats()["frames"]
+
+    @property
+    def gpu_ms_total(self):
+        return self._stats()["gpu_ms_total"]
+
+    @property
+    def direct_reads(self):
+        return self._stats()["direct_reads"]
+
+
+class ProcessHub:
+    def __init__(self, cfg: Config, devices: Optional[list[int]] = None, supervise_interval_s: float = 0.5):
+        self.cfg = cfg
+        if devices is None:
+            devices = list(cfg.gpu.devices) if cfg.gpu.devices else _count_gpus()
+        self.devices = devices or [-1]
+        self._cfg_json = json.dumps(dataclasses.asdict(cfg))
+        self._children = [_Child(d, self._cfg_json) for d in self.devices]
+        self.workers = [_WorkerView(self, i) for i in range(len(self.devices))]
+        self.cameras: dict[str, CameraHandle] = {}
+        self._specs: dict[str, dict] = {}
+        self._proxy: dict[str, bool] = {}
+        self.child_restarts = [0] * len(self.devices)
+        self._lock = threading.RLock()
+        self._stop = threading.Event()
+        self._sup = threading.Thread(target=self._supervise, args=(supervise_interval_s,), daemon=True,
+                                     name="vep-supervisor")
+        self._sup.start()
+        log.info("isolated hub up: devices=%s pids=%s", self.devices, [c.pid for c in self._children])
+
+    # ------------------------------------------------------------------ supervision
+    def _child(self, i: int) -> _Child:
+        return self._children[i]
+
+    def _supervise(self, interval: float) -> None:
+        while not self._stop.wait(interval):
+            for i in range(len(self._children)):
+                if self._stop.is_set() or self._children[i].alive():
+                    continue
+                code = self._children[i].proc.returncode
+                log.error("worker process for device %s (pid %d) exited with %s: restarting",
+                          self.devices[i], self._children[i].pid, code)
+                try:
+                    self._restart(i)
+                except Exception as e:  # noqa: BLE001 — try again at the next interval
+                    log.error("restart of device %s failed: %s", self.devices[i], e)
+
+    def _restart(self, i: int) -> None:
+        child = _Child(self.devices[i], self._cfg_json)
+        with self._lock:
+            mine = [n for n, h in self.cameras.items() if h.worker_index == i]
+            for n in mine:  # re-add before the fresh child takes calls (until then: restarting)
+                spec = self._specs[n]
+                res = child.call("start_camera", *spec["args"])
+                self.cameras[n].cam = res["cam"]
+                if self._proxy.get(n):
+                    child.call("set_proxy", n, True)
+            self._children[i] = child
+            self.child_restarts[i] += 1
+        log.info("device %s: fresh worker process pid %d, %d cameras re-added", self.devices[i], child.pid, len(mine))
+
+    # ------------------------------------------------------------------ lifecycle (Hub API)
+    def _loads(self) -> list[int]:
+        loads = [0] * len(self._children)
+        for h in self.cameras.values():
+            loads[h.worker_index] += 1
+        return loads
+
+    def archive_dir(self) -> str:
+        if not self.cfg.buffer.on_disk:
+            return ""
+        return self.cfg.buffer.on_disk_folder or os.path.join(self.cfg.data_dir, "archive")
+
+    def start_camera(self, name: str, rtsp: str, rtmp: str = "", disk_path: Optional[str] = None,
+                     timeout_ms: int = 5000, reconnect_delay_ms: int = 1000) -> CameraHandle:
+        with self._lock:
+            if name in self.cameras:
+                raise CameraExists(f"camera {name!r} already running")
+            wi = place_camera(name, self._loads(), self.cfg.gpu.placement)
+            args = (name, rtsp, rtmp or "", self.archive_dir() if disk_path is None else disk_path, timeout_ms,
+                    reconnect_delay_ms)
+            res = self._children[wi].call("start_camera", *args)
+            h = CameraHandle(name, wi, res["cam"], rtsp, rtmp)
+            self.cameras[name] = h
+            self._specs[name] = {"args": args}
+            return h
+
+    def stop_camera(self, name: str) -> None:
+        with self._lock:
+            h = self.cameras.pop(name, None)
+            self._specs.pop(name, None)
+            self._proxy.pop(name, None)
+        if h is None:
+            raise CameraNotFound(name)
+        try:
+            self._children[h.worker_index].call("stop_camera", name)
+        except WorkerRestarting:
+            pass  # the fresh child will not re-add it
+
+    def has(self, name: str) -> bool:
+        return name in self.cameras
+
+    def handle(self, name: str) -> CameraHandle:
+        h = self.cameras.get(name)
+        if h is None:
+            raise CameraNotFound(name)
+        return h
+
+    def _call(self, name: str, method: str, *args, **kwargs):
+        h = self.handle(name)
+        return self._children[h.worker_index].call(method, name, *args, **kwargs)
+
+    def consumer_batch(self, device=None, names=None):
+        raise RuntimeError("the batched consumer tensor is in-process only; with gpu.isolation: process "
+                           "use parallel.ConsumerBatch (RCCL all-gather across rank processes)")
+
+    def shutdown(self) -> None:
+        self._stop.set()
+        self._sup.join(timeout=5)
+        for name in list(self.cameras):
+            try:
+                self.stop_camera(name)
+            except (CameraNotFound, WorkerRestarting):
+                pass
+        for c in self._children:
+            c.close()
+
+    # ------------------------------------------------------------------ state / control / frames
+    def state(self, name: str) -> dict:
+        h = self.handle(name)
+        child = self._children[h.worker_index]
+        try:
+            st = self._call(name, "state")
+        except WorkerRestarting as e:
+            st = {"status": "restarting", "running": False, "restarting": True, "error": str(e),
+                  "health": "starting"}
+        st["device"] = self.devices[h.worker_index]
+        st["worker_pid"] = child.pid
+        st["worker_restarts"] = self.child_restarts[h.worker_index]
+        return st
+
+    def logs(self, name: str, last: int = 100) -> tuple[str, str]:
+        try:
+            return tuple(self._call(name, "logs", last))
+        except WorkerRestarting as e:
+            return "", str(e)
+
+    def touch(self, name: str, keyframe_only: Optional[bool] = None) -> None:
+        self._call(name, "touch", keyframe_only)
+
+    def set_proxy(self, name: str, on: bool) -> None:
+        self._proxy[name] = bool(on)
+        self._call(name, "set_proxy", bool(on))
+
+    def proxy(self, name: str) -> bool:
+        return bool(self._call(name, "proxy"))
+
+    def latest_frame_bytes(self, name: str, after: int = 0, wait_ms: int = 0):
+        return self._call(name, "latest_frame_bytes", after, wait_ms)
+
+    def latest_frame(self, name: str, after: int = 0):
+        return self._call(name, "latest_frame", after)
+
+    def wait_decoded(self, name: str, n: int = 1, timeout_s: float = 10.0) -> bool:
+        return bool(self._call(name, "wait_decoded", n, timeout_s))
+
+
+def _count_gpus() -> list[int]:
+    try:
+        import torch
+
+        return list(range(torch.cuda.device_count()))  # (does not initialise the GPU here)
+    except Exception:  # noqa: BLE001
+        return []

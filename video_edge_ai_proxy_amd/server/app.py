@@ -75,7 +75,12 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
               restore: bool = True) -> HubApp:
     os.makedirs(cfg.data_dir, exist_ok=True)
     storage = Storage(os.path.join(cfg.data_dir, "registry.db"))
-    hub = Hub(cfg, devices)
+    if cfg.gpu.isolation == "process":
+        from ..engine.isolated import ProcessHub
+
+        hub = ProcessHub(cfg, devices)
+    else:
+        hub = Hub(cfg, devices)
     pm = ProcessManager(storage, hub)
     settings = SettingsManager(storage)
     edge = EdgeService()
