@@ -10,6 +10,7 @@
 #include "vep/codec.h"
 #include "vep/gpu.h"
 #include "vep/h264.h"
+#include "vep/hevc_ctu.h"
 #include "vep/hevc_dec.h"
 #include "bind_ext.h"
 #include "vep/runtime.h"
@@ -383,6 +384,80 @@ PYBIND11_MODULE(_vep, m) {
         s["bi"] = d.stats.bi;
         s["tskip"] = d.stats.tskip;
         s["amp"] = d.stats.amp;
+        return s;
+      });
+
+  // General H.265 decoder in records mode + the CPU mirror of the GPU reconstruction (tests):
+  // same outputs as HevcDecoder, reconstructed from the GPU work lists.
+  struct HevcRecords {
+    hevc::Decoder d;
+    std::vector<HostSurface> slots;
+    u64 pictures = 0, pus = 0, tus = 0, intra_tus = 0, max_level = 0;
+    HevcRecords() { d.set_gpu_mode(true); }
+    py::list frames(const std::vector<hevc::FramePtr>& fs) {
+      py::list l;
+      for (const auto& f : fs) {
+        const HostSurface& s = slots[size_t(f->slot)];
+        const int W = f->width + f->crop_left, H = f->height + f->crop_top;
+        (void)W;
+        (void)H;
+        const int cw = s.coded_w, ch = s.coded_h;
+        (void)ch;
+        // the coded picture (the decoder's surfaces are coded_w x coded_h, slots are 16-aligned)
+        const int pw = coded_w_, ph = coded_h_;
+        py::array_t<uint8_t> y({ph, pw});
+        py::array_t<uint8_t> uv({ph / 2, pw});
+        for (int r = 0; r < ph; ++r) std::memcpy(y.mutable_data() + size_t(r) * pw, &s.y[size_t(r) * cw], size_t(pw));
+        for (int r = 0; r < ph / 2; ++r)
+          std::memcpy(uv.mutable_data() + size_t(r) * pw, &s.uv[size_t(r) * cw], size_t(pw));
+        l.append(py::make_tuple(f->pts, f->poc, std::string(1, f->type), py::make_tuple(y, uv), f->slot));
+      }
+      return l;
+    }
+    void run(std::vector<std::shared_ptr<hevc::GpuPicture>> ps) {
+      for (auto& p : ps) {
+        coded_w_ = p->width;
+        coded_h_ = p->height;
+        const int sw = (p->width + 15) & ~15, sh = (p->height + 15) & ~15;
+        if (slots.size() < size_t(d.gpu_slots())) slots.resize(size_t(d.gpu_slots()));
+        for (auto& h : slots)
+          if (h.coded_w != sw || h.coded_h != sh) h.alloc(sw, sh);
+        hevc::cpu_execute(*p, slots);
+        ++pictures;
+        pus += p->pus.size();
+        tus += p->tus.size();
+        for (const auto& t : p->tus) intra_tus += (t.flags & hevc::kTuIntra) ? 1 : 0;
+        max_level = std::max<u64>(max_level, p->level_begin.empty() ? 0 : p->level_begin.size() - 1);
+      }
+    }
+    int coded_w_ = 0, coded_h_ = 0;
+  };
+  py::class_<HevcRecords>(m, "HevcRecordsDecoder")
+      .def(py::init<>())
+      .def("decode",
+           [](HevcRecords& r, const AccessUnit& au) {
+             std::vector<hevc::FramePtr> fs;
+             {
+               py::gil_scoped_release nogil;
+               fs = r.d.decode(au, 0);
+               r.run(r.d.take_gpu_pictures());
+             }
+             return r.frames(fs);
+           })
+      .def("flush",
+           [](HevcRecords& r) {
+             auto fs = r.d.flush();
+             r.run(r.d.take_gpu_pictures());
+             return r.frames(fs);
+           })
+      .def_property_readonly("stats", [](const HevcRecords& r) {
+        py::dict s;
+        s["pictures"] = r.pictures;
+        s["pus"] = r.pus;
+        s["tus"] = r.tus;
+        s["intra_tus"] = r.intra_tus;
+        s["max_levels"] = r.max_level;
+        s["slots"] = r.d.gpu_slots();
         return s;
       });
 

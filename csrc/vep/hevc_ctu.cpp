@@ -337,6 +337,17 @@ class CtuLayer {
       VEP_CHECK(pos + bytes <= data_n, "PCM samples past the end of the slice");
       src = data + pos;
       rd->start(pos + bytes);
+      if (GpuPicture* g = pc_.gpu) {  // records mode: the GPU copies the samples (level 0)
+        GpuTu t{};
+        t.x = u16(x0);
+        t.y = u16(y0);
+        t.log2 = u8(log2);
+        t.flags = kTuPcm;
+        t.data = u32(g->pcm.size());
+        g->pcm.insert(g->pcm.end(), src, src + bytes);
+        g->tus.push_back(t);
+        return;
+      }
     }
     for (int y = 0; y < n; ++y) std::memcpy(&s.y[size_t(y0 + y) * s.coded_w + size_t(x0)], src + size_t(y) * n, size_t(n));
     const u8* cb = src + size_t(n) * n;
@@ -545,6 +556,29 @@ class CtuLayer {
   }
 
   void predict_inter_cu() {
+    if (GpuPicture* g = pc_.gpu) {  // records mode: one record per prediction block
+      for (int k = 0; k < cu_.npu; ++k) {
+        const int x = cu_.pus[k][0], y = cu_.pus[k][1];
+        const MvField& m = pc_.mf[pc_.i4(x, y)];
+        GpuPu u{};
+        u.x = u16(x);
+        u.y = u16(y);
+        u.w = u8(cu_.pus[k][2]);
+        u.h = u8(cu_.pus[k][3]);
+        u.pred = m.pred;
+        for (int l = 0; l < 2; ++l) {
+          u.slot[l] = -1;
+          if ((m.pred >> l) & 1) {
+            VEP_CHECK(m.ref[l] >= 0 && size_t(m.ref[l]) < sl_.list[l].size(), "reference index outside the list");
+            u.slot[l] = i8(sl_.list[l][size_t(m.ref[l])]->slot);
+          }
+          u.mv[l][0] = m.mv[l][0];
+          u.mv[l][1] = m.mv[l][1];
+        }
+        g->pus.push_back(u);
+      }
+      return;
+    }
     HostSurface& s = *pc_.s;
     const int st = s.coded_w;
     for (int k = 0; k < cu_.npu; ++k) {
@@ -716,6 +750,10 @@ class CtuLayer {
   // -------------------------------------------------------------------- intra prediction
   void intra_pred_block(int c, int x0, int y0, int log2) {
     // x0, y0 in the component's samples
+    if (pc_.gpu) {
+      gpu_intra_refs(c, x0, y0, log2);
+      return;
+    }
     HostSurface& s = *pc_.s;
     const int st = s.coded_w;
     const int n = 1 << log2, sub = c ? 1 : 0;
@@ -770,6 +808,30 @@ class CtuLayer {
       }
   }
 
+  // Records mode: which reference units of the block are available (hk_prepare_refs mask) and
+  // the block's intra dependency level (1 + the highest level among the intra blocks it reads).
+  void gpu_intra_refs(int c, int x0, int y0, int log2) {
+    const int n = 1 << log2, sub = c ? 1 : 0, g = c ? 2 : 4;
+    const int lx = x0 << sub, ly = y0 << sub;
+    std::vector<u16>& lvl = c ? pc_.lvl_c : pc_.lvl_y;
+    u64 mask = 0;
+    int level = 0;
+    auto probe = [&](int x, int y, int bit) {  // component location of the unit's first sample
+      const int xl = x << sub, yl = y << sub;
+      if (!pc_.avail(lx, ly, xl, yl, pc_.rec)) return;
+      if (pps_.constrained_intra_pred && !pc_.intra[pc_.i4(xl, yl)]) return;
+      mask |= u64(1) << bit;
+      level = std::max(level, int(lvl[pc_.i4(xl, yl)]));
+    };
+    probe(x0 - 1, y0 - 1, 0);
+    for (int k = 0; k < 2 * n / g; ++k) {
+      probe(x0 - 1, y0 + k * g, 1 + k);
+      probe(x0 + k * g, y0 - 1, 17 + k);
+    }
+    gpu_avail_ = mask;
+    gpu_level_ = level + 1;
+  }
+
   // -------------------------------------------------------------------- residual
   int scan_idx(int c, int log2) const {
     if (!cu_.intra) return 0;
@@ -822,6 +884,35 @@ class CtuLayer {
     }
     bool nz = false;
     for (int v : lv) nz |= v != 0;
+    if (GpuPicture* g = pc_.gpu) {  // records mode: the GPU predicts / transforms / adds
+      if (nz) cbf_nonzero_ = true;
+      if (!nz && !cu_.intra) return;
+      GpuTu t{};
+      t.x = u16(x0);
+      t.y = u16(y0);
+      t.log2 = u8(log2);
+      t.c = u8(c);
+      if (cu_.intra) {
+        t.flags |= kTuIntra;
+        t.mode = u8(c == 0 ? block_luma_mode_ : cu_.ipmc);
+        t.avail = gpu_avail_;
+        t.level = u16(gpu_level_);
+        t.strong = u8(sps_.strong_intra_smoothing);
+        if (c == 0 && log2 == 2) t.flags |= kTuDst;
+        // the block's samples are level `gpu_level_` output from here on
+        const int sub = c ? 1 : 0;
+        std::vector<u16>& lvl = c ? pc_.lvl_c : pc_.lvl_y;
+        for4(x0 << sub, y0 << sub, n << sub, n << sub, [&](size_t k) { lvl[k] = u16(gpu_level_); });
+      }
+      if (tskip) t.flags |= kTuSkip;
+      if (nz) {
+        t.flags |= kTuCoef;
+        t.data = u32(g->coefs.size());
+        for (int v : lv) g->coefs.push_back(i16(v ? dequant_level(v, qp, log2) : 0));
+      }
+      g->tus.push_back(t);
+      return;
+    }
     if (!nz) return;
     cbf_nonzero_ = true;
     std::vector<i32> d(size_t(n) * n), r(size_t(n) * n);
@@ -1107,6 +1198,8 @@ class CtuLayer {
   bool dry_tskip_ = false;
   bool cbf_nonzero_ = false;
   int block_luma_mode_ = 1;
+  u64 gpu_avail_ = 0;
+  int gpu_level_ = 1;
   std::map<TuKey, TuLevels> levels_;
 };
 

@@ -6,6 +6,7 @@
 
 #include "cabac.h"
 #include "hevc_dec.h"
+#include "hevc_kern.h"
 #include "hevc_tables.h"
 
 namespace vep::hevc {
@@ -41,6 +42,9 @@ struct PicCtx {
   std::vector<SaoParams> sao; // per CTB
   std::vector<SliceInfo> slices;
   Decoder::Stats stats;
+  // records mode (GPU reconstruction): the CTU layer emits work instead of samples
+  GpuPicture* gpu = nullptr;
+  std::vector<u16> lvl_y, lvl_c;  // intra dependency level of each 4x4 block's samples
 
   void init(const Sps& sp, const Pps& pp, HostSurface* surf) {
     sps = &sp;
@@ -70,6 +74,12 @@ struct PicCtx {
     sao.assign(size_t(wctb) * hctb, SaoParams{});
     slices.clear();
     stats = {};
+    gpu = nullptr;
+  }
+  void init_gpu(GpuPicture* g) {
+    gpu = g;
+    lvl_y.assign(size_t(w4) * h4, 0);
+    lvl_c.assign(size_t(w4) * h4, 0);
   }
   size_t i4(int x, int y) const { return size_t(y >> 2) * w4 + size_t(x >> 2); }
   int ctb_of(int x, int y) const { return (y >> log2ctb) * wctb + (x >> log2ctb); }
@@ -104,6 +114,13 @@ void encode_slice_data(PicCtx& pc, int slice_idx, std::vector<u8>& out, CtuDecid
 
 // Loop filters over the finished picture.
 void deblock_picture(PicCtx& pc);
+// Boundary strength of the left / top edge of every 4x4 block (0 where the edge is not filtered).
+void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& bsh);
+// Records mode: the loop-filter inputs of the finished picture into pc.gpu.
+void finish_gpu_picture(PicCtx& pc);
+// CPU mirror of the GPU reconstruction of one picture (hevc_gpu.cpp): executes the records on
+// the DPB surfaces `slots` with the kernels' per-sample math (tests; CPU backend).
+void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots);
 void sao_picture(PicCtx& pc);
 
 // TMVP store of a decoded picture.

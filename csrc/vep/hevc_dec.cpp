@@ -45,6 +45,7 @@ void Decoder::bump(std::vector<FramePtr>& out) {
     if (f->needed_for_output && (!best || f->poc < best->poc)) best = f;
   if (!best) return;
   best->needed_for_output = false;
+  last_out_slot_ = best->slot;  // (its surface is converted after the job: not reused before)
   out.push_back(best);
   dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const FramePtr& f) { return !f->is_ref && !f->needed_for_output; }),
              dpb_.end());
@@ -126,7 +127,18 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   first_ = false;
   // the new picture
   cur_ = std::make_shared<HevcFrame>();
-  cur_->s.alloc(sps.width, sps.height);
+  if (gpu_mode_) {  // a DPB surface slot no kept or just-output picture uses
+    gpu_slots_ = std::max(gpu_slots_, sps.max_dec_pic_buffering + 2);
+    std::vector<bool> used(size_t(gpu_slots_), false);
+    for (const FramePtr& f : dpb_) used[size_t(f->slot)] = true;
+    if (last_out_slot_ >= 0 && last_out_slot_ < gpu_slots_) used[size_t(last_out_slot_)] = true;
+    int slot = 0;
+    while (slot < gpu_slots_ && used[size_t(slot)]) ++slot;
+    VEP_CHECK(slot < gpu_slots_, "HEVC: no free DPB surface");
+    cur_->slot = slot;
+  } else {
+    cur_->s.alloc(sps.width, sps.height);
+  }
   cur_->poc = poc;
   cur_->uid = next_uid_++;
   cur_->pts = au.pts;
@@ -142,6 +154,17 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   pps_act_ = &pps;
   pc_->init(sps, pps, &cur_->s);
   pc_->poc = poc;
+  if (gpu_mode_) {
+    cur_gpu_ = std::make_shared<GpuPicture>();
+    cur_gpu_->target = cur_->slot;
+    pc_->init_gpu(cur_gpu_.get());
+  }
+}
+
+std::vector<std::shared_ptr<GpuPicture>> Decoder::take_gpu_pictures() {
+  std::vector<std::shared_ptr<GpuPicture>> v;
+  v.swap(gpu_out_);
+  return v;
 }
 
 void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
@@ -190,8 +213,13 @@ void Decoder::finish_picture(std::vector<FramePtr>& out) {
     deblock |= !s.sh.deblocking_disabled;
     sao |= s.sh.sao_luma || s.sh.sao_chroma;
   }
-  if (deblock) deblock_picture(*pc_);
-  if (sao) sao_picture(*pc_);
+  if (gpu_mode_) {
+    finish_gpu_picture(*pc_);
+    gpu_out_.push_back(std::move(cur_gpu_));
+  } else {
+    if (deblock) deblock_picture(*pc_);
+    if (sao) sao_picture(*pc_);
+  }
   if (sps_act_->temporal_mvp) f->col = build_col(*pc_, f->col_w);
   stats = pc_->stats;
   // C.5.2.3: the current picture is a short-term reference and waits for output
@@ -266,6 +294,7 @@ std::vector<FramePtr> Decoder::decode(const AccessUnit& au, i64 tag) {
       decode_slice(sh, rbsp_.data(), rn);
     } catch (...) {
       cur_ = nullptr;  // the damaged picture is dropped
+      cur_gpu_ = nullptr;
       throw;
     }
   }

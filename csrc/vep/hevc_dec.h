@@ -55,6 +55,7 @@ struct HevcFrame {
   std::shared_ptr<std::vector<ColMv>> col;  // 16x16 grid
   int col_w = 0;
   int width = 0, height = 0, crop_left = 0, crop_top = 0;  // conformance window (output size)
+  int slot = 0;                                             // DPB surface slot (GPU mode)
   int latency = 0;                                          // (output bumping, C.5.2.3)
 };
 using FramePtr = std::shared_ptr<HevcFrame>;
@@ -99,6 +100,13 @@ class Decoder {
   std::vector<FramePtr> decode(const AccessUnit& au, i64 tag = 0);
   std::vector<FramePtr> flush();  // end of stream
   bool has_sps() const { return !sps_.empty(); }
+  // Records mode (GPU reconstruction): pictures are parsed into GpuPicture work lists instead of
+  // being reconstructed; frames carry their DPB surface slot. take_gpu_pictures() hands over the
+  // pictures parsed since the last call, in decoding order.
+  void set_gpu_mode(bool on) { gpu_mode_ = on; }
+  bool gpu_mode() const { return gpu_mode_; }
+  std::vector<std::shared_ptr<struct GpuPicture>> take_gpu_pictures();
+  int gpu_slots() const { return gpu_slots_; }  // surfaces a camera needs (max DPB + 2)
   FramePtr last_decoded() const { return last_; }
   // statistics of the last picture (tests): CU counts by kind
   struct Stats {
@@ -124,6 +132,10 @@ class Decoder {
   int prev_tid0_poc_ = 0;
   bool first_ = true, no_rasl_output_ = true, skip_pic_ = false;
   u32 next_uid_ = 1;
+  bool gpu_mode_ = false;
+  int gpu_slots_ = 0, last_out_slot_ = -1;
+  std::shared_ptr<struct GpuPicture> cur_gpu_;
+  std::vector<std::shared_ptr<struct GpuPicture>> gpu_out_;
 };
 
 // Closed-loop synthetic HEVC Main encoder (tests, camera farm): I / P / B pictures over the

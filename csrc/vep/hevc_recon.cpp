@@ -683,12 +683,10 @@ static int bs_of(const PicCtx& pc, int xp, int yp, int xq, int yq, bool tu_edge)
   return ((far(ma[0], mb[0]) || far(ma[1], mb[1])) && (far(ma[0], mb[1]) || far(ma[1], mb[0]))) ? 1 : 0;
 }
 
-void deblock_picture(PicCtx& pc) {
-  HostSurface& s = *pc.s;
-  const int stride = s.coded_w;
+void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& bsh) {
   const int W = pc.W, H = pc.H;
-  // bS for every 4-sample edge segment on the 8x8 grid, both directions, before filtering
-  std::vector<u8> bsv(size_t(pc.w4) * pc.h4, 0), bsh(size_t(pc.w4) * pc.h4, 0);
+  bsv.assign(size_t(pc.w4) * pc.h4, 0);
+  bsh.assign(size_t(pc.w4) * pc.h4, 0);
   for (int y = 0; y < H; y += 4)
     for (int x = 0; x < W; x += 4) {
       const size_t k = pc.i4(x, y);
@@ -707,6 +705,15 @@ void deblock_picture(PicCtx& pc) {
         (dir == 0 ? bsv : bsh)[k] = u8(bs_of(pc, xp, yp, x, y, tu));
       }
     }
+}
+
+void deblock_picture(PicCtx& pc) {
+  HostSurface& s = *pc.s;
+  const int stride = s.coded_w;
+  const int W = pc.W, H = pc.H;
+  // bS for every 4-sample edge segment on the 8x8 grid, both directions, before filtering
+  std::vector<u8> bsv, bsh;
+  deblock_strengths(pc, bsv, bsh);
   auto qpc = [&](int qpi, int c) {
     return hevc_chroma_qp(std::clamp(qpi + (c == 0 ? pc.pps->cb_qp_offset : pc.pps->cr_qp_offset), 0, 57));
   };
