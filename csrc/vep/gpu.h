@@ -73,6 +73,49 @@ struct GatherChunk {
 constexpr u32 kGatherChunk = 32u << 10;
 void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s);
 
+// ---- general H.265 reconstruction (gpu_hevc.hip; records from hevc::Decoder, hevc_kern.h) ----
+// One picture of a batched reconstruction round (device memory). DPB slot k of the camera
+// lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = `stride`).
+struct HevcDesc {
+  u8* y;
+  u8* uv;
+  u64 slot_y, slot_uv;
+  i32 stride, width, height;
+  i32 log2ctb, wctb, hctb;
+  i32 target;
+  i32 cb_qp_offset, cr_qp_offset;
+  i32 flags;             // bit 0 deblock, bit 1 SAO, bit 2 PCM samples not loop-filtered
+  const void* pus;       // hevc::GpuPu[npu]
+  const void* tus;       // hevc::GpuTu (level-sorted)
+  const i16* coefs;
+  const u8* pcm;
+  const u8* bs_v;
+  const u8* bs_h;
+  const signed char* qp;
+  const u8* pcm_map;
+  const u16* ctb_slice;
+  const void* slices;    // hevc::GpuSlice
+  const void* sao;       // hevc::GpuSao per CTB
+  u8* sao_y;             // device scratch: the deblocked picture (SAO input)
+  u8* sao_uv;
+  i32 npu, pu_begin;     // exclusive prefix of PUs over the round
+  i32 blk_begin;         // exclusive prefix of 4x4 blocks over the round
+  i32 pad;
+};
+// One level's transform blocks of one picture: tus[first .. first + count) of descs[desc].
+struct HevcTuRange {
+  i32 desc, first, count, begin;  // begin: exclusive prefix of counts within the level
+};
+// Motion compensation of every prediction block of the round (one workgroup per block).
+void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s);
+// Transform blocks of one dependency level (level 0: inter residual + PCM; >= 1: intra
+// prediction + residual), one workgroup per block.
+void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, hipStream_t s);
+// Deblocking of every vertical (dir 0) or horizontal (dir 1) edge of the round, one thread per
+// 4-line edge segment; then SAO (copy of the deblocked picture, one thread per sample).
+void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s);
+void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream_t s);
+
 // ---- general H.264 reconstruction (gpu_avc.hip; records from avc::Decoder, avc.h) ----------
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera
 // lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = wmbs * 16).

@@ -1,0 +1,264 @@
+// gfx950 reconstruction kernels of the general H.265 path (records from hevc::Decoder in
+// records mode, hevc_kern.h). Per reconstruction round (round r = the r-th picture of each
+// camera's job):
+//
+//  * hevc_mc_kernel — every prediction block of the round, one 256-lane workgroup per block:
+//    8-tap luma / 4-tap chroma motion compensation from the camera's DPB surfaces with uni- or
+//    bi-prediction. No neighbour dependency: the launch is as wide as the round.
+//  * hevc_tu_kernel, once per dependency level — level 0 adds the inter residuals and copies
+//    PCM blocks; level L >= 1 reconstructs the intra transform blocks whose references were
+//    completed by levels < L (the CPU parser derives the levels from the blocks' reference
+//    areas). One workgroup per block: lane 0 prepares the substituted / filtered references in
+//    LDS, the block's 4..32-point inverse transform runs as two LDS passes, and every lane then
+//    writes prediction + residual for its samples. An I picture's wavefront of blocks therefore
+//    becomes a short sequence of wide launches instead of a serial walk.
+//  * hevc_deblock_kernel — HEVC filters every vertical edge of the picture before any
+//    horizontal one, and edges 8 samples apart never touch the same samples: one launch per
+//    direction, one lane per 4-line edge segment, no wavefront.
+//  * hevc_sao_copy_kernel + hevc_sao_kernel — SAO reads the deblocked picture: a copy, then one
+//    lane per 4x4 block (16 luma + 2 x 4 chroma samples).
+//
+// All sample arithmetic comes from hevc_kern.h, shared with the CPU mirror (hevc_gpu.cpp) that
+// is tested bit-exact against the reference decoder.
+#include "gpu.h"
+#include "hevc_kern.h"
+
+namespace vep::gpu {
+
+using hevc::GpuPu;
+using hevc::GpuSao;
+using hevc::GpuSlice;
+using hevc::GpuTu;
+
+namespace {
+
+__device__ inline int pick_pu(const HevcDesc* d, int n, int b) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].pu_begin <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ inline int pick_blk(const HevcDesc* d, int n, int b) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d[mid].blk_begin <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+__device__ inline int pick_range(const HevcTuRange* r, int n, int b) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (r[mid].begin <= b) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// ------------------------------------------------------------------------------ MC
+__global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict__ descs, int n) {
+  const int b = int(blockIdx.x);
+  const HevcDesc& d = descs[pick_pu(descs, n, b)];
+  const GpuPu u = static_cast<const GpuPu*>(d.pus)[b - d.pu_begin];
+  const int stride = d.stride, W = d.width, H = d.height;
+  u8* y = d.y + size_t(d.target) * d.slot_y;
+  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  const u8* ry[2] = {nullptr, nullptr};
+  const u8* ruv[2] = {nullptr, nullptr};
+  for (int l = 0; l < 2; ++l)
+    if ((u.pred >> l) & 1) {
+      ry[l] = d.y + size_t(u.slot[l]) * d.slot_y;
+      ruv[l] = d.uv + size_t(u.slot[l]) * d.slot_uv;
+    }
+  const bool bi = u.pred == 3;
+  const int nl = u.w * u.h;
+  for (int s = int(threadIdx.x); s < nl; s += 256) {
+    const int i = s % u.w, j = s / u.w;
+    int v[2] = {0, 0}, k = 0;
+    for (int l = 0; l < 2; ++l)
+      if (ry[l])
+        v[k++] = hevc::hk_luma_mc(ry[l], stride, W, H, u.x + i + (u.mv[l][0] >> 2), u.y + j + (u.mv[l][1] >> 2),
+                                  u.mv[l][0] & 3, u.mv[l][1] & 3);
+    y[(u.y + j) * stride + u.x + i] = hevc::hk_weight(v[0], v[1], bi);
+  }
+  const int wc = u.w >> 1, hc = u.h >> 1, nc = wc * hc;
+  for (int s = int(threadIdx.x); s < 2 * nc; s += 256) {
+    const int c = s / nc, r = s - c * nc, i = r % wc, j = r / wc;
+    int v[2] = {0, 0}, k = 0;
+    for (int l = 0; l < 2; ++l)
+      if (ruv[l])
+        v[k++] = hevc::hk_chroma_mc(ruv[l], stride, W >> 1, H >> 1, c, (u.x >> 1) + i + (u.mv[l][0] >> 3),
+                                    (u.y >> 1) + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7);
+    uv[((u.y >> 1) + j) * stride + u.x + 2 * i + c] = hevc::hk_weight(v[0], v[1], bi);
+  }
+}
+
+// ------------------------------------------------------------------------------ TUs
+__global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict__ descs,
+                                                     const HevcTuRange* __restrict__ ranges, int nranges) {
+  __shared__ int g[32 * 32];
+  __shared__ int top[129];
+  __shared__ int left[128];
+  const int b = int(blockIdx.x);
+  const HevcTuRange& rg = ranges[pick_range(ranges, nranges, b)];
+  const HevcDesc& d = descs[rg.desc];
+  const GpuTu t = static_cast<const GpuTu*>(d.tus)[rg.first + (b - rg.begin)];
+  const int stride = d.stride;
+  u8* y = d.y + size_t(d.target) * d.slot_y;
+  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  const int tid = int(threadIdx.x);
+  if (t.flags & hevc::kTuPcm) {
+    const int n = 1 << t.log2, nc = n >> 1;
+    const u8* src = d.pcm + t.data;
+    for (int s = tid; s < n * n; s += 256) y[(t.y + s / n) * stride + t.x + s % n] = src[s];
+    for (int s = tid; s < 2 * nc * nc; s += 256) {
+      const int c = s / (nc * nc), r = s - c * nc * nc;
+      uv[((t.y >> 1) + r / nc) * stride + t.x + 2 * (r % nc) + c] = src[n * n + s];
+    }
+    return;
+  }
+  const int log2 = t.log2, n = 1 << log2;
+  u8* plane = t.c == 0 ? y : uv + (t.c - 1);
+  const int step = t.c == 0 ? 1 : 2;
+  const bool intra = t.flags & hevc::kTuIntra;
+  const bool coef = t.flags & hevc::kTuCoef;
+  const bool tskip = t.flags & hevc::kTuSkip;
+  const bool dst = t.flags & hevc::kTuDst;
+  const i16* dq = d.coefs + t.data;
+  if (intra && tid == 0)
+    hevc::hk_prepare_refs(plane, stride, step, t.x, t.y, log2, t.c == 0, t.avail, t.mode,
+                          (t.flags & hevc::kTuStrong) != 0, top, left);
+  const int mx = t.ext_x, my = t.ext_y;
+  if (coef && !tskip)
+    for (int s = tid; s < n * (mx + 1); s += 256) {
+      const int yy = s / (mx + 1), xx = s - yy * (mx + 1);
+      g[yy * n + xx] = hevc::hk_itx_col(dq, log2, dst, yy, xx, my);
+    }
+  __syncthreads();
+  for (int s = tid; s < n * n; s += 256) {
+    const int yy = s >> log2, xx = s & (n - 1);
+    u8& q = plane[(t.y + yy) * stride + (t.x + xx) * step];
+    int v = intra ? int(hevc::hk_intra_sample(top, left, log2, t.mode, t.c == 0, xx, yy)) : int(q);
+    if (coef) v += tskip ? hevc::hk_tskip(dq[s]) : hevc::hk_itx_row(&g[yy * n], log2, dst, xx, mx);
+    q = hevc::hk_clip8(v);
+  }
+}
+
+// ------------------------------------------------------------------------------ deblocking
+__global__ __launch_bounds__(256) void hevc_deblock_kernel(const HevcDesc* __restrict__ descs, int n, int total,
+                                                          int dir) {
+  const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= total) return;
+  const HevcDesc& d = descs[pick_blk(descs, n, b)];
+  if (!(d.flags & 1)) return;
+  const int w4 = d.width >> 2, k = b - d.blk_begin;
+  const int x = (k % w4) << 2, yy = (k / w4) << 2;
+  const u8* bsm = dir == 0 ? d.bs_v : d.bs_h;
+  const int bs = bsm[k];
+  if (!bs) return;
+  const int stride = d.stride;
+  u8* y = d.y + size_t(d.target) * d.slot_y;
+  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? yy : yy - 1;
+  const int kp = (yp >> 2) * w4 + (xp >> 2);
+  const GpuSlice& sl =
+      static_cast<const GpuSlice*>(d.slices)[d.ctb_slice[(yy >> d.log2ctb) * d.wctb + (x >> d.log2ctb)]];
+  const bool nof = d.flags & 4;
+  const bool nfp = nof && d.pcm_map[kp], nfq = nof && d.pcm_map[k];
+  // (bS is non-zero only on the 8x8 grid)
+  hevc::HkLumaEdge e{y + yy * stride + x, dir == 0 ? stride : 1, dir == 0 ? 1 : stride};
+  hevc::hk_deblock_luma(e, bs, (d.qp[kp] + d.qp[k] + 1) >> 1, sl.beta_offset, sl.tc_offset, nfp, nfq);
+  if (bs == 2 && ((dir == 0 ? x : yy) & 15) == 0)
+    for (int c = 0; c < 2; ++c)
+      hevc::hk_deblock_chroma(uv + (yy >> 1) * stride + x + c, dir == 0 ? stride : 2, dir == 0 ? 2 : stride,
+                              d.qp[kp], d.qp[k], c == 0 ? d.cb_qp_offset : d.cr_qp_offset, sl.tc_offset, nfp,
+                              nfq);
+}
+
+// ------------------------------------------------------------------------------ SAO
+__global__ __launch_bounds__(256) void hevc_sao_copy_kernel(const HevcDesc* __restrict__ descs, int n, int total) {
+  const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= total) return;
+  const HevcDesc& d = descs[pick_blk(descs, n, b)];
+  if (!(d.flags & 2)) return;
+  const int w4 = d.width >> 2, k = b - d.blk_begin;
+  const int x = (k % w4) << 2, yy = (k / w4) << 2;
+  const int stride = d.stride;
+  const u8* y = d.y + size_t(d.target) * d.slot_y;
+  const u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  for (int j = 0; j < 4; ++j)
+    *reinterpret_cast<u32*>(d.sao_y + (yy + j) * stride + x) = *reinterpret_cast<const u32*>(y + (yy + j) * stride + x);
+  for (int j = 0; j < 2; ++j)
+    *reinterpret_cast<u32*>(d.sao_uv + ((yy >> 1) + j) * stride + x) =
+        *reinterpret_cast<const u32*>(uv + ((yy >> 1) + j) * stride + x);
+}
+
+__global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restrict__ descs, int n, int total) {
+  const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= total) return;
+  const HevcDesc& d = descs[pick_blk(descs, n, b)];
+  if (!(d.flags & 2)) return;
+  const int w4 = d.width >> 2, k = b - d.blk_begin;
+  const int x4 = (k % w4) << 2, y4 = (k / w4) << 2;
+  if ((d.flags & 4) && d.pcm_map[k]) return;
+  const int ci = (y4 >> d.log2ctb) * d.wctb + (x4 >> d.log2ctb);
+  const GpuSao sp = static_cast<const GpuSao*>(d.sao)[ci];
+  const int si = d.ctb_slice[ci];
+  const GpuSlice* slices = static_cast<const GpuSlice*>(d.slices);
+  const GpuSlice sl = slices[si];
+  const int stride = d.stride;
+  u8* y = d.y + size_t(d.target) * d.slot_y;
+  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  for (int c = 0; c < 3; ++c) {
+    if (!sp.type[c] || (c == 0 ? !sl.sao_luma : !sl.sao_chroma)) continue;
+    const int sub = c ? 1 : 0, step = c ? 2 : 1;
+    const u8* src = c == 0 ? d.sao_y : d.sao_uv + (c - 1);
+    u8* dst = c == 0 ? y : uv + (c - 1);
+    const int pw = d.width >> sub, ph = d.height >> sub;
+    auto nb_ok = [&](int nx, int ny) {
+      if (nx < 0 || ny < 0 || nx >= pw || ny >= ph) return false;
+      const int nsi = d.ctb_slice[((ny << sub) >> d.log2ctb) * d.wctb + ((nx << sub) >> d.log2ctb)];
+      if (nsi == si) return true;
+      return nsi > si ? slices[nsi].across != 0 : sl.across != 0;
+    };
+    const int sz = 4 >> sub, x0 = x4 >> sub, y0 = y4 >> sub;
+    for (int j = 0; j < sz; ++j)
+      for (int i = 0; i < sz; ++i)
+        dst[(y0 + j) * stride + (x0 + i) * step] =
+            u8(hevc::hk_sao_sample(src, stride, step, sp, c, x0 + i, y0 + j, nb_ok));
+  }
+}
+
+}  // namespace
+
+void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s) {
+  if (n <= 0 || total_pus <= 0) return;
+  hipLaunchKernelGGL(hevc_mc_kernel, dim3(total_pus), dim3(256), 0, s, d_descs, n);
+}
+
+void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, hipStream_t s) {
+  if (nranges <= 0 || total_tus <= 0) return;
+  hipLaunchKernelGGL(hevc_tu_kernel, dim3(total_tus), dim3(256), 0, s, d_descs, d_ranges, nranges);
+}
+
+void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s) {
+  if (n <= 0 || total_blocks <= 0) return;
+  hipLaunchKernelGGL(hevc_deblock_kernel, dim3((total_blocks + 255) / 256), dim3(256), 0, s, d_descs, n,
+                     total_blocks, dir);
+}
+
+void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream_t s) {
+  if (n <= 0 || total_blocks <= 0) return;
+  const dim3 grid((total_blocks + 255) / 256);
+  hipLaunchKernelGGL(hevc_sao_copy_kernel, grid, dim3(256), 0, s, d_descs, n, total_blocks);
+  hipLaunchKernelGGL(hevc_sao_kernel, grid, dim3(256), 0, s, d_descs, n, total_blocks);
+}
+
+}  // namespace vep::gpu

@@ -897,7 +897,7 @@ class CtuLayer {
         t.mode = u8(c == 0 ? block_luma_mode_ : cu_.ipmc);
         t.avail = gpu_avail_;
         t.level = u16(gpu_level_);
-        t.strong = u8(sps_.strong_intra_smoothing);
+        if (sps_.strong_intra_smoothing) t.flags |= kTuStrong;
         if (c == 0 && log2 == 2) t.flags |= kTuDst;
         // the block's samples are level `gpu_level_` output from here on
         const int sub = c ? 1 : 0;
@@ -908,7 +908,14 @@ class CtuLayer {
       if (nz) {
         t.flags |= kTuCoef;
         t.data = u32(g->coefs.size());
-        for (int v : lv) g->coefs.push_back(i16(v ? dequant_level(v, qp, log2) : 0));
+        int ex = 0, ey = 0;
+        for (int k = 0; k < n * n; ++k) {
+          const int v = lv[size_t(k)];
+          g->coefs.push_back(i16(v ? dequant_level(v, qp, log2) : 0));
+          if (v) ex = std::max(ex, k & (n - 1)), ey = k >> log2;
+        }
+        t.ext_x = u8(ex);
+        t.ext_y = u8(ey);
       }
       g->tus.push_back(t);
       return;

@@ -118,9 +118,7 @@ void deblock_picture(PicCtx& pc);
 void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& bsh);
 // Records mode: the loop-filter inputs of the finished picture into pc.gpu.
 void finish_gpu_picture(PicCtx& pc);
-// CPU mirror of the GPU reconstruction of one picture (hevc_gpu.cpp): executes the records on
-// the DPB surfaces `slots` with the kernels' per-sample math (tests; CPU backend).
-void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots);
+
 void sao_picture(PicCtx& pc);
 
 // TMVP store of a decoded picture.

@@ -138,6 +138,12 @@ class Decoder {
   std::vector<std::shared_ptr<struct GpuPicture>> gpu_out_;
 };
 
+// CPU mirror of the GPU reconstruction of one picture (hevc_gpu.cpp): executes the records of a
+// records-mode picture on the DPB surfaces `slots` with the kernels' per-sample math (CPU
+// backend of the records path; the oracle of gpu_hevc.hip).
+void cpu_execute(const struct GpuPicture& p, std::vector<HostSurface>& slots);
+
+
 // Closed-loop synthetic HEVC Main encoder (tests, camera farm): I / P / B pictures over the
 // shared CTU layer; `coverage` randomises every decision (all CU sizes, partition modes incl.
 // AMP, intra modes, merge candidates, AMVP, bi-prediction, transform trees, transform skip, PCM,

@@ -68,14 +68,7 @@ void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
     for (int k = 0; k < n * n; ++k) res[k] = hk_tskip(d[k]);
     return;
   }
-  int mx = -1, my = -1;
-  for (int y = 0; y < n; ++y)
-    for (int x = 0; x < n; ++x)
-      if (d[y * n + x]) mx = std::max(mx, x), my = y;
-  if (mx < 0) {
-    std::fill(res, res + n * n, 0);
-    return;
-  }
+  const int mx = t.ext_x, my = t.ext_y;
   const bool dst = t.flags & kTuDst;
   int g[32 * 32];
   for (int y = 0; y < n; ++y)
@@ -137,7 +130,7 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
     const int step = t.c == 0 ? 1 : 2;
     if (t.flags & kTuIntra) {
       int top[129], left[128];
-      hk_prepare_refs(plane, stride, step, t.x, t.y, t.log2, t.c == 0, t.avail, t.mode, t.strong, top, left);
+      hk_prepare_refs(plane, stride, step, t.x, t.y, t.log2, t.c == 0, t.avail, t.mode, t.flags & kTuStrong, top, left);
       for (int y = 0; y < n; ++y)
         for (int x = 0; x < n; ++x)
           plane[(t.y + y) * stride + (t.x + x) * step] = hk_intra_sample(top, left, t.log2, t.mode, t.c == 0, x, y);

@@ -33,7 +33,7 @@ struct GpuPu {    // one prediction block
 };
 static_assert(sizeof(GpuPu) == 18, "GpuPu layout");
 
-enum : u8 { kTuIntra = 1, kTuDst = 2, kTuSkip = 4, kTuCoef = 8, kTuPcm = 16 };
+enum : u8 { kTuIntra = 1, kTuDst = 2, kTuSkip = 4, kTuCoef = 8, kTuPcm = 16, kTuStrong = 32 };
 
 struct GpuTu {    // one transform block of one component (or one PCM coding block)
   u16 x, y;       // position in the component's samples
@@ -43,8 +43,7 @@ struct GpuTu {    // one transform block of one component (or one PCM coding blo
   u8 mode;        // intra prediction mode (component's)
   u32 data;       // kTuCoef: offset of the n x n dequantised coefficients (i16); kTuPcm: byte offset
   u16 level;      // intra dependency level (0: inter residual / PCM)
-  u8 strong;      // intra: strong intra smoothing enabled (luma)
-  u8 pad;
+  u8 ext_x, ext_y;  // kTuCoef: last column / row holding a non-zero coefficient
   u64 avail;      // intra: reference availability, see hk_prepare_refs
 };
 static_assert(sizeof(GpuTu) == 24, "GpuTu layout");

@@ -17,6 +17,13 @@ namespace vep::hevc {
 
 using i8 = std::int8_t;
 
+// Tables the gfx950 kernels read live in constant memory in the device pass.
+#if defined(__HIP_DEVICE_COMPILE__)
+#define HK_TABLE __constant__ constexpr
+#else
+#define HK_TABLE inline constexpr
+#endif
+
 // ---------------------------------------------------------------------------- CABAC contexts
 // Context index layout (one array per slice): every syntax element's contexts for the slice's
 // initialisation type are copied to these offsets.
@@ -152,9 +159,9 @@ inline constexpr ScanDiag8 kScanDiag{};
 
 // ---------------------------------------------------------------------------- intra
 // intraPredAngle for modes 2..34 (index mode - 2) and invAngle for modes 11..25.
-inline constexpr i8 kIntraAngle[33] = {32,  26,  21,  17,  13,  9,  5,  2,  0,  -2, -5, -9, -13, -17, -21, -26, -32,
+HK_TABLE i8 kIntraAngle[33] = {32,  26,  21,  17,  13,  9,  5,  2,  0,  -2, -5, -9, -13, -17, -21, -26, -32,
                                        -26, -21, -17, -13, -9, -5, -2, 0,   2,  5,  9,  13,  17,  21,  26,  32};
-inline constexpr i16 kInvAngle[15] = {-4096, -1638, -910, -630, -482, -390, -315, -256,
+HK_TABLE i16 kInvAngle[15] = {-4096, -1638, -910, -630, -482, -390, -315, -256,
                                       -315,  -390,  -482, -630, -910, -1638, -4096};
 
 // ---------------------------------------------------------------------------- transform
@@ -177,22 +184,22 @@ struct DctMatrix {
       }
   }
 };
-inline constexpr DctMatrix kDct{};
+HK_TABLE DctMatrix kDct{};
 // 4x4 DST-VII (intra luma 4x4).
-inline constexpr i8 kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
+HK_TABLE i8 kDst4[4][4] = {{29, 55, 74, 84}, {74, 74, 0, -74}, {84, -29, -74, 55}, {55, -84, 74, -29}};
 
 // ---------------------------------------------------------------------------- interpolation
-inline constexpr i8 kLumaFilter[4][8] = {
+HK_TABLE i8 kLumaFilter[4][8] = {
     {0, 0, 0, 64, 0, 0, 0, 0}, {-1, 4, -10, 58, 17, -5, 1, 0}, {-1, 4, -11, 40, 40, -11, 4, -1},
     {0, 1, -5, 17, 58, -10, 4, -1}};
-inline constexpr i8 kChromaFilter[8][4] = {{0, 64, 0, 0},     {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
+HK_TABLE i8 kChromaFilter[8][4] = {{0, 64, 0, 0},     {-2, 58, 10, -2}, {-4, 54, 16, -2}, {-6, 46, 28, -4},
                                            {-4, 36, 36, -4},  {-4, 28, 46, -6}, {-2, 16, 54, -4}, {-2, 10, 58, -2}};
 
 // ---------------------------------------------------------------------------- deblocking
-inline constexpr u8 kBetaTable[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
+HK_TABLE u8 kBetaTable[52] = {0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  0,  6,  7,
                                       8,  9,  10, 11, 12, 13, 14, 15, 16, 17, 18, 20, 22, 24, 26, 28, 30, 32,
                                       34, 36, 38, 40, 42, 44, 46, 48, 50, 52, 54, 56, 58, 60, 62, 64};
-inline constexpr u8 kTcTable[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
+HK_TABLE u8 kTcTable[54] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 1, 1, 1, 1, 1, 1, 1, 1, 1,
                                     2, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 6, 6, 7, 8, 9, 10, 11, 13, 14, 16, 18, 20, 22, 24};
 // QpC as a function of qPi for 4:2:0 (Table 8-10).
 inline int hevc_chroma_qp(int qpi) {

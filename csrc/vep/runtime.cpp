@@ -2,6 +2,7 @@
 #include "runtime.h"
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 
 #include "color.h"
@@ -180,6 +181,7 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
       }
     }
     if (hevc_full_) {
+      hevc_.set_gpu_mode(true);
       hevc::FramePtr of;
       const bool key_only = keyframe_only.load() && to - from == 1 && gop_[from]->keyframe;
       for (size_t i = from; i < to; ++i) {
@@ -188,16 +190,26 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
           std::vector<hevc::FramePtr> rest = hevc_.flush();
           outs.insert(outs.end(), rest.begin(), rest.end());
         }
+        for (auto& p : hevc_.take_gpu_pictures()) job.hevc.push_back(std::move(p));
         if (!outs.empty()) of = outs.back();
         last = gop_[i].get();
       }
-      hevc_pics_ += int(to - from);
       decoded_upto_ = to;
-      if (!of) return false;  // reordering: every picture still waits for output
-      hevc_publish(*of, job);
-      job.cpu_recon = true;
-      job.upd.frames = hevc_pics_;  // pictures reconstructed since the last published job
-      hevc_pics_ = 0;
+      if (job.hevc.empty()) return false;
+      job.hevc_slots = hevc_.gpu_slots();
+      const hevc::GpuPicture& gp = *job.hevc.back();
+      PictureInfo& pi = job.pic;
+      pi = PictureInfo{};
+      pi.coded_width = (gp.width + 15) & ~15;  // surfaces keep the 16-aligned pitch of the convert kernels
+      pi.coded_height = (gp.height + 15) & ~15;
+      pi.width = of ? of->width : gp.width;
+      pi.height = of ? of->height : gp.height;
+      job.out_slot = of ? of->slot : -1;
+      if (!of) return true;  // reordering: reconstruct only, nothing leaves the DPB yet
+      pi.crop_left = of->crop_left;
+      pi.crop_top = of->crop_top;
+      pi.pict_type = of->type;
+      pi.idr = of->keyframe;
       FrameMeta& m = job.meta;
       m.width = of->width;
       m.height = of->height;
@@ -245,7 +257,6 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
     errors.fetch_add(1);
     logs.add(true, std::string("failed to decode packet: ") + e.what());
     if (full_) avc_.reset_references();
-    if (hevc_full_) hevc_shown_.clear();  // the surface may hold a partial update
     decoded_upto_ = gop_.size();  // give up on this GOP; wait for the next keyframe
     return false;
   }
@@ -263,64 +274,6 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
   m.arrival_ms = last->arrival_ms;
   decoded_upto_ = to;
   return true;
-}
-
-bool Camera::hevc_publish(const hevc::HevcFrame& f, DecodeJob& job) {
-  const int W = f.s.coded_w, H = f.s.coded_h;
-  const int wmbs = (W + 15) / 16, hmbs = (H + 15) / 16;
-  if (job.upd.width_mbs != wmbs || job.upd.height_mbs != hmbs) job.upd.reset(wmbs, hmbs);
-  const size_t nmb = size_t(wmbs) * hmbs;
-  const bool full = hevc_shown_.size() != nmb * 384 || hevc_shown_wmbs_ != wmbs || hevc_shown_hmbs_ != hmbs;
-  if (full) {
-    hevc_shown_.assign(nmb * 384, 0);
-    hevc_shown_wmbs_ = wmbs;
-    hevc_shown_hmbs_ = hmbs;
-  }
-  auto buf = std::make_shared<std::vector<u8>>();
-  buf->reserve(full ? nmb * 384 : 64 * 384);
-  std::vector<i32> changed;
-  u8 blk[384];
-  for (int my = 0; my < hmbs; ++my)
-    for (int mx = 0; mx < wmbs; ++mx) {
-      // gather the macroblock in I_PCM order (16x16 Y, 8x8 Cb, 8x8 Cr), clamping at the edges of
-      // the coded picture (HEVC sizes are multiples of 8)
-      for (int y = 0; y < 16; ++y) {
-        const size_t row = size_t(std::min(my * 16 + y, H - 1)) * size_t(W);
-        for (int x = 0; x < 16; ++x) blk[y * 16 + x] = f.s.y[row + size_t(std::min(mx * 16 + x, W - 1))];
-      }
-      for (int y = 0; y < 8; ++y) {
-        const size_t row = size_t(std::min(my * 8 + y, H / 2 - 1)) * size_t(W);
-        for (int x = 0; x < 8; ++x) {
-          const size_t c = row + 2 * size_t(std::min(mx * 8 + x, W / 2 - 1));
-          blk[256 + y * 8 + x] = f.s.uv[c];
-          blk[320 + y * 8 + x] = f.s.uv[c + 1];
-        }
-      }
-      u8* shown = hevc_shown_.data() + (size_t(my) * wmbs + size_t(mx)) * 384;
-      if (!full && std::memcmp(shown, blk, 384) == 0) continue;
-      std::memcpy(shown, blk, 384);
-      buf->insert(buf->end(), blk, blk + 384);
-      changed.push_back(my * wmbs + mx);
-    }
-  job.refresh = full;
-  if (!changed.empty()) {
-    job.upd.begin_segment(buf->data(), buf->size());
-    job.upd.reserve_blocks(changed.size());
-    for (size_t k = 0; k < changed.size(); ++k) job.upd.set(changed[k], buf->data() + 384 * k);
-    job.upd.own.push_back(std::move(buf));
-  }
-  PictureInfo& p = job.pic;
-  p = PictureInfo{};
-  p.width = f.width;
-  p.height = f.height;
-  p.coded_width = wmbs * 16;
-  p.coded_height = hmbs * 16;
-  p.crop_left = f.crop_left;
-  p.crop_top = f.crop_top;
-  p.pict_type = f.type;
-  p.idr = f.keyframe;
-  p.coded_mbs = int(changed.size());
-  return full;
 }
 
 bool Camera::on_access_unit(const AuPtr& au) {
@@ -631,6 +584,8 @@ void merge_job(DecodeJob& p, DecodeJob&& job) {
   // general-path pictures are appended (each references the previous ones)
   if (job.general() && p.general() && !job.refresh) {
     p.avc.insert(p.avc.end(), job.avc.begin(), job.avc.end());
+    p.hevc.insert(p.hevc.end(), job.hevc.begin(), job.hevc.end());
+    p.hevc_slots = std::max(p.hevc_slots, job.hevc_slots);
     if (job.out_slot >= 0 || p.out_slot < 0) {  // the newer output wins; none keeps the older
       p.pic = job.pic;
       p.meta = job.meta;
@@ -995,6 +950,68 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     off_round[size_t(r)] = need;
     need += al(round_pics[size_t(r)].size() * sizeof(gpu::AvcDesc));
   }
+  // General H.265 pictures: reconstruction records of every picture, one HevcDesc array and one
+  // level-range table per round.
+  struct HevcPic {
+    const hevc::GpuPicture* p;
+    int job;
+    size_t off_pu, off_tu, off_coef, off_pcm, off_bsv, off_bsh, off_qp, off_pcmmap, off_cslice, off_slices, off_sao;
+  };
+  std::vector<HevcPic> hpics;
+  int hrounds = 0;
+  for (int i = 0; i < n; ++i) hrounds = std::max(hrounds, int(jobs[size_t(i)].hevc.size()));
+  std::vector<size_t> off_hround(static_cast<size_t>(hrounds)), off_hranges(static_cast<size_t>(hrounds));
+  std::vector<std::vector<int>> hround_pics(static_cast<size_t>(hrounds));
+  std::vector<std::vector<gpu::HevcTuRange>> hranges(static_cast<size_t>(hrounds));
+  std::vector<std::vector<std::array<int, 3>>> hlevels(static_cast<size_t>(hrounds));  // first range, ranges, tus
+  for (int r = 0; r < hrounds; ++r) {
+    int maxl = 0;
+    for (int i = 0; i < n; ++i) {
+      const auto& v = jobs[size_t(i)].hevc;
+      if (int(v.size()) <= r) continue;
+      const hevc::GpuPicture& p = *v[size_t(r)];
+      VEP_CHECK(((p.width + 15) & ~15) == jobs[size_t(i)].pic.coded_width &&
+                    ((p.height + 15) & ~15) == jobs[size_t(i)].pic.coded_height,
+                "picture size differs from the camera's surfaces");
+      HevcPic a{&p, i, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      auto put = [&](size_t bytes) {
+        const size_t o = need;
+        need += al(std::max<size_t>(bytes, 16));
+        return o;
+      };
+      a.off_pu = put(p.pus.size() * sizeof(hevc::GpuPu));
+      a.off_tu = put(p.tus.size() * sizeof(hevc::GpuTu));
+      a.off_coef = put(p.coefs.size() * sizeof(i16));
+      a.off_pcm = put(p.pcm.size());
+      a.off_bsv = put(p.bs_v.size());
+      a.off_bsh = put(p.bs_h.size());
+      a.off_qp = put(p.qp.size());
+      a.off_pcmmap = put(p.pcm_map.size());
+      a.off_cslice = put(p.ctb_slice.size() * sizeof(u16));
+      a.off_slices = put(p.slices.size() * sizeof(hevc::GpuSlice));
+      a.off_sao = put(p.sao_params.size() * sizeof(hevc::GpuSao));
+      maxl = std::max(maxl, int(p.level_begin.size()) - 1);
+      hround_pics[size_t(r)].push_back(int(hpics.size()));
+      hpics.push_back(a);
+    }
+    off_hround[size_t(r)] = need;
+    need += al(hround_pics[size_t(r)].size() * sizeof(gpu::HevcDesc));
+    for (int l = 0; l < maxl; ++l) {  // level l: one range per picture that has blocks at l
+      const int first = int(hranges[size_t(r)].size());
+      int tus = 0;
+      for (size_t k = 0; k < hround_pics[size_t(r)].size(); ++k) {
+        const hevc::GpuPicture& p = *hpics[size_t(hround_pics[size_t(r)][k])].p;
+        if (int(p.level_begin.size()) - 1 <= l) continue;
+        const int b = int(p.level_begin[size_t(l)]), e = int(p.level_begin[size_t(l) + 1]);
+        if (e <= b) continue;
+        hranges[size_t(r)].push_back({int(k), b, e - b, tus});
+        tus += e - b;
+      }
+      hlevels[size_t(r)].push_back({first, int(hranges[size_t(r)].size()) - first, tus});
+    }
+    off_hranges[size_t(r)] = need;
+    need += al(std::max<size_t>(hranges[size_t(r)].size(), 1) * sizeof(gpu::HevcTuRange));
+  }
   need = al(need);
   const size_t header_bytes = need;
   for (int i = 0; i < n; ++i) {
@@ -1050,6 +1067,24 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     add(a.p->coefs.data(), a.p->coefs.size() * sizeof(i16), a.off_coef);
     add(a.p->mvs.data(), a.p->mvs.size() * sizeof(i16), a.off_mv);
     add(a.p->wps.data(), a.p->wps.size() * sizeof(avc::WpEntry), a.off_wp);
+  }
+  for (const HevcPic& a : hpics) {
+    auto add = [&](const void* src, size_t len, size_t off) {
+      for (size_t o = 0; o < len; o += kPackChunk)
+        tasks.push_back({static_cast<const u8*>(src) + o, st.h + off + o, std::min(kPackChunk, len - o)});
+    };
+    const hevc::GpuPicture& p = *a.p;
+    add(p.pus.data(), p.pus.size() * sizeof(hevc::GpuPu), a.off_pu);
+    add(p.tus.data(), p.tus.size() * sizeof(hevc::GpuTu), a.off_tu);
+    add(p.coefs.data(), p.coefs.size() * sizeof(i16), a.off_coef);
+    add(p.pcm.data(), p.pcm.size(), a.off_pcm);
+    add(p.bs_v.data(), p.bs_v.size(), a.off_bsv);
+    add(p.bs_h.data(), p.bs_h.size(), a.off_bsh);
+    add(p.qp.data(), p.qp.size(), a.off_qp);
+    add(p.pcm_map.data(), p.pcm_map.size(), a.off_pcmmap);
+    add(p.ctb_slice.data(), p.ctb_slice.size() * sizeof(u16), a.off_cslice);
+    add(p.slices.data(), p.slices.size() * sizeof(hevc::GpuSlice), a.off_slices);
+    add(p.sao_params.data(), p.sao_params.size() * sizeof(hevc::GpuSao), a.off_sao);
   }
   std::vector<std::vector<const u8*>> seg_dev(static_cast<size_t>(n));
   auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
@@ -1203,6 +1238,57 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       mbs += a.p->nmbs();
     }
   }
+  // HEVC descriptors and level ranges
+  std::vector<std::array<int, 2>> hround_work(static_cast<size_t>(hrounds));  // PUs, 4x4 blocks
+  for (int r = 0; r < hrounds; ++r) {
+    auto* hd2 = reinterpret_cast<gpu::HevcDesc*>(st.h + off_hround[size_t(r)]);
+    int pus = 0, blks = 0;
+    for (size_t k = 0; k < hround_pics[size_t(r)].size(); ++k) {
+      const HevcPic& a = hpics[size_t(hround_pics[size_t(r)][k])];
+      const hevc::GpuPicture& p = *a.p;
+      const DecodeJob& j = jobs[size_t(a.job)];
+      const Camera* c = cams_[size_t(j.cam)].get();
+      gpu::HevcDesc& g = hd2[k];
+      g = gpu::HevcDesc{};
+      g.y = c->surface.y;
+      g.uv = c->surface.uv;
+      g.slot_y = c->surface.slot_y();
+      g.slot_uv = c->surface.slot_uv();
+      g.stride = c->surface.wmbs * 16;
+      g.width = p.width;
+      g.height = p.height;
+      g.log2ctb = p.log2ctb;
+      g.wctb = p.wctb;
+      g.hctb = p.hctb;
+      g.target = p.target;
+      g.cb_qp_offset = p.cb_qp_offset;
+      g.cr_qp_offset = p.cr_qp_offset;
+      g.flags = (p.deblock ? 1 : 0) | (p.sao ? 2 : 0) | (p.pcm_nofilter ? 4 : 0);
+      g.pus = st.d + a.off_pu;
+      g.tus = st.d + a.off_tu;
+      g.coefs = reinterpret_cast<const i16*>(st.d + a.off_coef);
+      g.pcm = st.d + a.off_pcm;
+      g.bs_v = st.d + a.off_bsv;
+      g.bs_h = st.d + a.off_bsh;
+      g.qp = reinterpret_cast<const signed char*>(st.d + a.off_qp);
+      g.pcm_map = st.d + a.off_pcmmap;
+      g.ctb_slice = reinterpret_cast<const u16*>(st.d + a.off_cslice);
+      g.slices = st.d + a.off_slices;
+      g.sao = st.d + a.off_sao;
+      const size_t scratch = size_t(j.hevc_slots);  // the extra surface after the DPB slots
+      VEP_CHECK(c->surface.slots > j.hevc_slots, "camera surfaces lack the SAO scratch slot");
+      g.sao_y = c->surface.y + scratch * c->surface.slot_y();
+      g.sao_uv = c->surface.uv + scratch * c->surface.slot_uv();
+      g.npu = int(p.pus.size());
+      g.pu_begin = pus;
+      g.blk_begin = blks;
+      pus += g.npu;
+      blks += p.w4() * p.h4();
+    }
+    hround_work[size_t(r)] = {pus, blks};
+    auto* hr = reinterpret_cast<gpu::HevcTuRange*>(st.h + off_hranges[size_t(r)]);
+    for (size_t k = 0; k < hranges[size_t(r)].size(); ++k) hr[k] = hranges[size_t(r)][k];
+  }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
   // With several lanes the copy goes on the lane's own stream instead: it then waits for the
@@ -1250,6 +1336,23 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       gpu::launch_avc_deblock(ad, np, max_h, cs);
     }
   }
+  for (int r = 0; r < hrounds; ++r) {
+    const auto* hd2 = reinterpret_cast<const gpu::HevcDesc*>(st.d + off_hround[size_t(r)]);
+    const auto* hr = reinterpret_cast<const gpu::HevcTuRange*>(st.d + off_hranges[size_t(r)]);
+    const int np = int(hround_pics[size_t(r)].size());
+    bool dbk = false, sao = false;
+    for (int k : hround_pics[size_t(r)]) {
+      dbk |= hpics[size_t(k)].p->deblock;
+      sao |= hpics[size_t(k)].p->sao;
+    }
+    gpu::launch_hevc_mc(hd2, np, hround_work[size_t(r)][0], cs);
+    for (const auto& lv : hlevels[size_t(r)]) gpu::launch_hevc_tu(hd2, hr + lv[0], lv[1], lv[2], cs);
+    if (dbk) {
+      gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 0, cs);
+      gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 1, cs);
+    }
+    if (sao) gpu::launch_hevc_sao(hd2, np, hround_work[size_t(r)][1], cs);
+  }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), nout, tiles,
                              cs);
   if (opt_.letterbox_size > 0) {
@@ -1282,6 +1385,7 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
     if (err[i]) continue;
     if (jobs[i].general()) {
       for (const auto& pic : jobs[i].avc) avc::cpu_reconstruct(*pic, c.surface.host);
+      for (const auto& pic : jobs[i].hevc) hevc::cpu_execute(*pic, c.surface.host);
     } else {
       cpu_apply_update(jobs[i].upd, c.surface.host[0]);
     }
@@ -1334,7 +1438,7 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       continue;
     }
     if (!(err && err[i]) && !cp->broken_) {
-      const u64 np = jobs[i].general() ? jobs[i].avc.size() : jobs[i].cpu_recon ? u64(std::max(1, jobs[i].upd.frames)) : 1;
+      const u64 np = jobs[i].general() ? jobs[i].avc.size() + jobs[i].hevc.size() : 1;
       pictures_.fetch_add(np, std::memory_order_relaxed);
       cp->pictures.fetch_add(np, std::memory_order_relaxed);
     }

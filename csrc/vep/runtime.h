@@ -21,6 +21,7 @@
 #include "avc.h"
 #include "codec.h"
 #include "hevc_dec.h"
+#include "hevc_kern.h"
 #include "gpu.h"
 #include "pool.h"
 
@@ -99,18 +100,21 @@ struct DecodeJob {
   int cam = -1;
   MbUpdate upd;                        // PCM / skip fast path (collapsible)
   std::vector<avc::PicturePtr> avc;    // general H.264 path: pictures in decoding order
+  std::vector<hevc::GpuPicturePtr> hevc;  // general H.265 path: reconstruction records
+  int hevc_slots = 0;                  // DPB surfaces the H.265 pictures use
   PictureInfo pic;                     // the published frame's picture (sizes of the surfaces)
   FrameMeta meta;
   bool refresh = false;  // IDR: every MB is covered
-  bool cpu_recon = false;  // blocks reconstructed on the CPU (general H.265 path); upd.frames counts them
+
   // General path: DPB slot of the newest picture that left the reorder buffer in this job (it is
   // converted and published), -1 when every picture of the job is still waiting for output
   // (B-frame reordering): the job then only reconstructs.
   int out_slot = -1;
-  bool general() const { return !avc.empty(); }
+  bool general() const { return !avc.empty() || !hevc.empty(); }
   bool has_output() const { return !general() || out_slot >= 0; }
-  int dpb_slots() const { return avc.empty() ? 1 : avc.back()->dpb_slots; }
-  int target() const { return avc.empty() ? 0 : out_slot; }
+  // (H.265: the DPB slots plus one scratch surface, the SAO input copy)
+  int dpb_slots() const { return !avc.empty() ? avc.back()->dpb_slots : (!hevc.empty() ? hevc_slots + 1 : 1); }
+  int target() const { return general() ? out_slot : 0; }
 };
 
 // Fold `job` into the not-yet-launched job `p` of the same camera (GOP catch-up collapse).
@@ -198,16 +202,10 @@ class Camera {
   StreamParser parser_;
   avc::Decoder avc_;
   bool full_ = false;
-  // General H.265 path: the CPU decoder reconstructs (hevc_dec.h) and each published picture
-  // goes to the surface as an update of the 16x16 blocks that changed since the last one, in the
-  // I_PCM block layout of the fast path (so the GPU apply / convert / letterbox kernels, job
-  // collapsing and the CPU backend are shared).
-  bool hevc_publish(const hevc::HevcFrame& f, DecodeJob& job);
+  // General H.265 path: the CPU parses into reconstruction records (hevc_dec.h records mode);
+  // the worker reconstructs them on the GPU (gpu_hevc.hip) or with the CPU mirror.
   bool hevc_full_ = false;
   hevc::Decoder hevc_;
-  std::vector<u8> hevc_shown_;  // the blocks the surface holds (384 B each), empty = unknown
-  int hevc_shown_wmbs_ = 0, hevc_shown_hmbs_ = 0;
-  int hevc_pics_ = 0;           // pictures reconstructed since the last published job
 };
 
 struct WorkerOptions {

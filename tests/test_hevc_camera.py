@@ -23,13 +23,17 @@ def run_camera(native, device, w, h, n, **kw):
     cam = wk.add_camera("hevc", 4)
     want = {}
     published = 0
+    seq = 0
     for _ in range(n):
         au = s.next()
         y, uv = s.picture()
         want[s.last_pts] = native.nv12_to_bgr_cpu(y, uv, 0, 0, w, h)
-        if not wk.decode_now(cam, au):
-            continue
-        meta, got = wk.read_latest(cam, 0)
+        wk.decode_now(cam, au)
+        r = wk.read_latest(cam, seq)
+        if r is None:
+            continue  # reordering: the picture was reconstructed, nothing left the DPB
+        meta, got = r
+        seq = meta["seq"]
         assert got.shape == (h, w, 3)
         ref = want[meta["pts"]]
         assert np.array_equal(got, ref), f"pts {meta['pts']}: {int((got != ref).sum())} samples differ"
