@@ -135,7 +135,7 @@ def spawn_ranks(n: int) -> int:
 def describe_streams(a, compressed):
     if compressed and a.codec == "h265":
         return (f"HEVC Main CABAC I/P/B, {a.bframes} B per mini-GOP, CTB 32, merge/AMVP/TMVP, "
-                "deblocking; CPU reconstruction (general H.265 decoder) + gfx950 block update / NV12->BGR24")
+                "deblocking")
     if compressed and a.profile == "baseline":
         return "Baseline CAVLC I/P"
     if compressed:
@@ -528,9 +528,10 @@ def main():
                                              "reference clients' pattern): includes waiting for "
                                              "the camera's next decoded frame",
             "rocdecode_available": bool(vep.rocdecode_available()),
-            "decoder_backend": ("native H.265 Main decoder: CPU CABAC coding-tree parse + reconstruction "
-                                "(intra, merge/AMVP MC, transforms, deblocking, SAO); gfx950 changed-block "
-                                "update + NV12->BGR24 (rocDecode absent in image)" if compressed and a.codec == "h265" else
+            "decoder_backend": ("native H.265 Main decoder: CPU CABAC coding-tree parse + merge/AMVP into "
+                                "reconstruction records; gfx950 HIP motion compensation, level-scheduled intra + "
+                                "residual transform blocks, deblocking, SAO, NV12->BGR24 (rocDecode absent in "
+                                "image)" if compressed and a.codec == "h265" else
                                 "native H.264 decoder: CPU " + ("CAVLC" if a.profile == "baseline" or a.cavlc
                                                                else "CABAC") + " macroblock-layer parse + dequant; "
                                 "gfx950 HIP motion compensation, intra + deblocking wavefronts, "

@@ -1,9 +1,10 @@
 // Host benchmark of the general HEVC decoder: encodes a synthetic camera stream once, then
 // decodes it several times and reports ms per picture (best pass) and the phase split.
-//   hevc_bench [width] [height] [frames] [bframes] [qp]
+//   hevc_bench [width] [height] [frames] [bframes] [qp] [records]
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 #include "vep/hevc_dec.h"
 
@@ -25,11 +26,16 @@ int main(int argc, char** argv) {
     aus.push_back(enc.next());
     bytes += aus.back()->bytes();
   }
+  const bool records = argc > 6 && std::string(argv[6]) == "records";  // parse only (GPU mode)
   double best = 1e30;
   for (int pass = 0; pass < 5; ++pass) {
     hevc::Decoder d;
+    d.set_gpu_mode(records);
     const auto t0 = std::chrono::steady_clock::now();
-    for (auto& a : aus) d.decode(*a);
+    for (auto& a : aus) {
+      d.decode(*a);
+      d.take_gpu_pictures();
+    }
     d.flush();
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     best = std::min(best, ms);

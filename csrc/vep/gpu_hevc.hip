@@ -101,11 +101,85 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
 }
 
 // ------------------------------------------------------------------------------ TUs
+// Reference samples of an intra block with every lane of the workgroup (the parallel form of
+// hk_prepare_refs, same result): gather by availability, substitution as "nearest available
+// sample before, else the first available one", then the [1 2 1] / strong filters. All lanes
+// must call it (it synchronises).
+__device__ void prepare_refs_par(const u8* plane, int stride, int step, int x0, int y0, int log2, bool luma, u64 avail,
+                                 int mode, bool strong, int* sbuf, u8* sav, int* sref, int* top, int* left) {
+  const int n = 1 << log2, g = luma ? 4 : 2, last = 4 * n;
+  const int tid = int(threadIdx.x), nt = int(blockDim.x);
+  for (int k = tid; k <= last; k += nt) {  // scan order: p[-1][2n-1] .. p[-1][-1] .. p[2n-1][-1]
+    bool a;
+    int v = 0;
+    if (k < 2 * n) {
+      const int y = 2 * n - 1 - k;
+      a = (avail >> (1 + y / g)) & 1;
+      if (a) v = plane[(y0 + y) * stride + (x0 - 1) * step];
+    } else if (k == 2 * n) {
+      a = avail & 1;
+      if (a) v = plane[(y0 - 1) * stride + (x0 - 1) * step];
+    } else {
+      const int x = k - 2 * n - 1;
+      a = (avail >> (17 + x / g)) & 1;
+      if (a) v = plane[(y0 - 1) * stride + (x0 + x) * step];
+    }
+    sbuf[k] = v;
+    sav[k] = a ? 1 : 0;
+  }
+  __syncthreads();
+  for (int k = tid; k <= last; k += nt) {
+    int src = -1;
+    for (int j = k; j >= 0 && src < 0; --j)
+      if (sav[j]) src = j;
+    for (int j = k + 1; j <= last && src < 0; ++j)
+      if (sav[j]) src = j;
+    sref[k] = src >= 0 ? sbuf[src] : 128;
+  }
+  __syncthreads();
+  // filtering decision (luma): same rule as hk_prepare_refs
+  bool filt = false, strong_f = false;
+  if (luma && mode != 1 && n != 4) {
+    const int dm = mode - 26 < 0 ? 26 - mode : mode - 26, dh = mode - 10 < 0 ? 10 - mode : mode - 10;
+    const int dist = dm < dh ? dm : dh;
+    const int thres = n == 8 ? 7 : (n == 16 ? 1 : 0);
+    filt = dist > thres;
+    if (filt && strong && n == 32) {
+      // tl = ref[2n], top[2n] = ref[4n], top[n] = ref[3n], left[2n-1] = ref[0], left[n-1] = ref[n]
+      const int tl = sref[2 * n];
+      const int a1 = tl + sref[4 * n] - 2 * sref[3 * n], a2 = tl + sref[0] - 2 * sref[n];
+      strong_f = (a1 < 0 ? -a1 : a1) < 8 && (a2 < 0 ? -a2 : a2) < 8;
+    }
+  }
+  for (int k = tid; k <= last; k += nt) {
+    int v = sref[k];
+    if (filt) {
+      if (strong_f) {  // bilinear between the corner and the far ends
+        const int tl = sref[2 * n];
+        if (k < 2 * n) {
+          const int y = 2 * n - 1 - k;
+          if (y < 63) v = ((63 - y) * tl + (y + 1) * sref[0] + 32) >> 6;
+        } else if (k > 2 * n) {
+          const int x = k - 2 * n - 1;
+          if (x < 63) v = ((63 - x) * tl + (x + 1) * sref[last] + 32) >> 6;
+        }
+      } else if (k > 0 && k < last) {
+        v = (sref[k - 1] + 2 * sref[k] + sref[k + 1] + 2) >> 2;
+      }
+    }
+    if (k < 2 * n) left[2 * n - 1 - k] = v;
+    else top[k - 2 * n] = v;
+  }
+  __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict__ descs,
                                                      const HevcTuRange* __restrict__ ranges, int nranges) {
   __shared__ int g[32 * 32];
   __shared__ int top[129];
   __shared__ int left[128];
+  __shared__ int sbuf[129], sref[129];
+  __shared__ u8 sav[129];
   const int b = int(blockIdx.x);
   const HevcTuRange& rg = ranges[pick_range(ranges, nranges, b)];
   const HevcDesc& d = descs[rg.desc];
@@ -132,9 +206,9 @@ __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict
   const bool tskip = t.flags & hevc::kTuSkip;
   const bool dst = t.flags & hevc::kTuDst;
   const i16* dq = d.coefs + t.data;
-  if (intra && tid == 0)
-    hevc::hk_prepare_refs(plane, stride, step, t.x, t.y, log2, t.c == 0, t.avail, t.mode,
-                          (t.flags & hevc::kTuStrong) != 0, top, left);
+  if (intra)  // (uniform per block)
+    prepare_refs_par(plane, stride, step, t.x, t.y, log2, t.c == 0, t.avail, t.mode, (t.flags & hevc::kTuStrong) != 0,
+                     sbuf, sav, sref, top, left);
   const int mx = t.ext_x, my = t.ext_y;
   if (coef && !tskip)
     for (int s = tid; s < n * (mx + 1); s += 256) {
