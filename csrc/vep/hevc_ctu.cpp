@@ -855,7 +855,10 @@ class CtuLayer {
     auto px = [&](int i, int j) -> u8& {
       return c == 0 ? s.y[size_t(y0 + j) * st + size_t(x0 + i)] : s.uv[size_t(y0 + j) * st + size_t(2 * (x0 + i) + c - 1)];
     };
-    std::vector<int> lv(size_t(n) * n, 0);
+    if (lvbuf_.size() < 1024) lvbuf_.resize(1024);
+    int* lv = lvbuf_.data();
+    const int nn = n * n;
+    std::fill(lv, lv + nn, 0);
     bool tskip = false;
     const TuKey key{c, x0, y0};
     if (dry_) {
@@ -865,25 +868,26 @@ class CtuLayer {
           for (int i = 0; i < n; ++i) pred[size_t(j) * n + i] = px(i, j);
         const bool ts_ok = pps_.transform_skip && log2 == 2;
         bool ts = dry_tskip_ && ts_ok;
-        dec_->residual(c, x0, y0, log2, pred.data(), n, qp, ts_ok, cu_.intra, lv.data(), ts);
+        dec_->residual(c, x0, y0, log2, pred.data(), n, qp, ts_ok, cu_.intra, lv, ts);
         tskip = ts && ts_ok;
-        if (pps_.sign_data_hiding) hide_signs(lv.data(), log2, scan_idx(c, log2));
+        if (pps_.sign_data_hiding) hide_signs(lv, log2, scan_idx(c, log2));
         TuLevels& t = levels_[key];
-        t.lv = lv;
+        t.lv.assign(lv, lv + nn);
         t.tskip = tskip;
-        t.any = std::any_of(lv.begin(), lv.end(), [](int v) { return v != 0; });
+        t.any = std::any_of(lv, lv + nn, [](int v) { return v != 0; });
       }
     } else if (coded) {
       if constexpr (kWrite) {
         const TuLevels& t = levels_[key];
-        lv = t.lv;
+        std::copy(t.lv.begin(), t.lv.end(), lv);
         tskip = t.tskip;
       }
-      residual_coding(c, log2, lv.data(), tskip);
+      residual_coding(c, log2, lv, tskip);
       if (tskip) ++pc_.stats.tskip;
     }
     bool nz = false;
-    for (int v : lv) nz |= v != 0;
+    if (coded || dry_)
+      for (int k = 0; k < nn; ++k) nz |= lv[k] != 0;
     if (GpuPicture* g = pc_.gpu) {  // records mode: the GPU predicts / transforms / adds
       if (nz) cbf_nonzero_ = true;
       if (!nz && !cu_.intra) return;
@@ -1206,6 +1210,7 @@ class CtuLayer {
   bool cbf_nonzero_ = false;
   int block_luma_mode_ = 1;
   u64 gpu_avail_ = 0;
+  std::vector<int> lvbuf_;  // one transform block's levels
   int gpu_level_ = 1;
   std::map<TuKey, TuLevels> levels_;
 };

@@ -650,6 +650,10 @@ static int bs_of(const PicCtx& pc, int xp, int yp, int xq, int yq, bool tu_edge)
   if (tu_edge && (pc.cbf[p] || pc.cbf[q])) return 1;
   const MvField& a = pc.mf[p];
   const MvField& b = pc.mf[q];
+  // the same motion in one slice (same lists): same pictures and vectors
+  if (std::memcmp(&a, &b, sizeof(MvField)) == 0 &&
+      pc.slice[size_t(pc.ctb_of(xp, yp))] == pc.slice[size_t(pc.ctb_of(xq, yq))])
+    return 0;
   const SliceInfo& sa = pc.slices[pc.slice[size_t(pc.ctb_of(xp, yp))]];
   const SliceInfo& sb = pc.slices[pc.slice[size_t(pc.ctb_of(xq, yq))]];
   const HevcFrame* ra[2] = {nullptr, nullptr};
@@ -687,24 +691,24 @@ void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& 
   const int W = pc.W, H = pc.H;
   bsv.assign(size_t(pc.w4) * pc.h4, 0);
   bsh.assign(size_t(pc.w4) * pc.h4, 0);
-  for (int y = 0; y < H; y += 4)
-    for (int x = 0; x < W; x += 4) {
-      const size_t k = pc.i4(x, y);
-      const int si = pc.slice[size_t(pc.ctb_of(x, y))];
-      const SliceHeader& sh = pc.slices[size_t(si)].sh;
-      if (sh.deblocking_disabled) continue;
-      for (int dir = 0; dir < 2; ++dir) {
-        const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
-        if ((dir == 0 ? x : y) % 8 != 0 || xp < 0 || yp < 0) continue;
+  // edges lie on the 8x8 grid: vertical ones in every 8th column, horizontal ones in every 8th row
+  for (int dir = 0; dir < 2; ++dir) {
+    const u8 tu_flag = dir == 0 ? kEdgeTuV : kEdgeTuH, pu_flag = dir == 0 ? kEdgePuV : kEdgePuH;
+    std::vector<u8>& out = dir == 0 ? bsv : bsh;
+    for (int y = dir == 0 ? 0 : 8; y < H; y += dir == 0 ? 4 : 8)
+      for (int x = dir == 0 ? 8 : 0; x < W; x += dir == 0 ? 8 : 4) {
+        const size_t k = pc.i4(x, y);
         const u8 e = pc.edge[k];
-        const bool tu = e & (dir == 0 ? kEdgeTuV : kEdgeTuH);
-        const bool pu = e & (dir == 0 ? kEdgePuV : kEdgePuH);
-        if (!tu && !pu) continue;
+        if (!(e & (tu_flag | pu_flag))) continue;
+        const int si = pc.slice[size_t(pc.ctb_of(x, y))];
+        const SliceHeader& sh = pc.slices[size_t(si)].sh;
+        if (sh.deblocking_disabled) continue;
+        const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
         const int sp = pc.slice[size_t(pc.ctb_of(xp, yp))];
         if (sp != si && !sh.loop_filter_across_slices) continue;
-        (dir == 0 ? bsv : bsh)[k] = u8(bs_of(pc, xp, yp, x, y, tu));
+        out[k] = u8(bs_of(pc, xp, yp, x, y, (e & tu_flag) != 0));
       }
-    }
+  }
 }
 
 void deblock_picture(PicCtx& pc) {
