@@ -316,6 +316,7 @@ static void compressed_ingest_stress() {
 }
 
 int main() {
+  std::setvbuf(stdout, nullptr, _IONBF, 0);  // progress is visible even if a run is cut short
   live_worker_stress();
   rtsp_stress();
   general_decoder_stress();

@@ -7,6 +7,15 @@ from __future__ import annotations
 
 import functools
 
+# PyTorch-ROCm ships its own HIP/HSA runtime next to the /opt/rocm one the extension links. When
+# the extension's runtime initialises the GPU first, torch's later initialisation finds no device
+# ("No HIP GPUs are available", seen on the MI355X boxes); loading torch first keeps both working
+# (consumer tensors, RCCL) in every import order.
+try:
+    import torch  # noqa: F401
+except ImportError:  # pragma: no cover - torch-less deployments still get the data plane
+    pass
+
 try:
     from . import _vep as native  # type: ignore[attr-defined]
 except ImportError as e:  # pragma: no cover - exercised only on a broken checkout
