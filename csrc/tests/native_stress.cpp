@@ -190,7 +190,7 @@ static void general_decoder_stress() {
   o.max_cameras = 8;
   Worker w(o);
   w.start();
-  const int ncam = 4;
+  const int ncam = 6;  // 2 High, 2 Baseline, 2 H.265 Main (records path + CPU mirror)
   std::vector<int> cams;
   for (int i = 0; i < ncam; ++i) cams.push_back(w.add_camera("g" + std::to_string(i), 3));
   std::atomic<bool> stop{false};
@@ -198,7 +198,9 @@ static void general_decoder_stress() {
   std::vector<std::thread> th;
   for (int i = 0; i < ncam; ++i) {
     th.emplace_back([&, i] {
-      SynthH264 enc(compressed_cfg(i < 2 ? "high" : "baseline", u64(i + 1), 96 + 16 * i, 64));
+      SynthConfig cfg = compressed_cfg(i < 2 ? "high" : "baseline", u64(i + 1), 96 + 16 * (i % 4), 64);
+      if (i >= 4) cfg.codec = Codec::kH265;
+      SynthH264 enc(cfg);
       auto cam = w.camera(cams[size_t(i)]);
       for (int f = 0; f < 48; ++f) {
         cam->last_query_ms.store(now_ms());
@@ -212,6 +214,7 @@ static void general_decoder_stress() {
     th.emplace_back([&] {
       std::vector<u8> buf(size_t(160) * 64 * 3);
       i64 cursor[8] = {};
+
       while (!stop.load()) {
         for (int i = 0; i < ncam; ++i) {
           auto cam = w.camera(cams[size_t(i)]);

@@ -238,6 +238,7 @@ class CtuLayer {
     int part = 0;
     if (skip) {
       cu_.intra = false;
+      for4(x0, y0, n, n, [&](size_t k) { pc_.intra[k] = 0; });
       prediction_unit(x0, y0, n, n, 0, 0, want.pu[0], true);
       ++pc_.stats.skip;
     } else {

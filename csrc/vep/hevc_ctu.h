@@ -35,7 +35,7 @@ struct PicCtx {
   int poc = 0;
   HostSurface* s = nullptr;   // target surface (reconstruction, then loop filters)
   // per 4x4 block
-  std::vector<u8> depth, skip, intra, ipm, done, rec, pcm, cbf, edge, tq;
+  std::vector<u8> depth, skip, intra, ipm, done, rec, pcm, cbf, edge;
   std::vector<i8> qp;
   std::vector<MvField> mf;
   std::vector<u16> slice;     // slice index per CTB (not per 4x4)
@@ -58,18 +58,19 @@ struct PicCtx {
     hctb = sp.height_ctbs();
     s = surf;
     const size_t n = size_t(w4) * h4;
-    depth.assign(n, 0);
-    skip.assign(n, 0);
-    intra.assign(n, 0);
-    ipm.assign(n, 1);
+    if (depth.size() != n) {  // (every other per-4x4 array is written by the CU covering it
+      depth.assign(n, 0);     // before anything reads it: only the decoded flags are reset)
+      skip.assign(n, 0);
+      intra.assign(n, 0);
+      ipm.assign(n, 1);
+      pcm.assign(n, 0);
+      cbf.assign(n, 0);
+      edge.assign(n, 0);
+      qp.assign(n, 0);
+      mf.assign(n, MvField{});
+    }
     done.assign(n, 0);
     rec.assign(n, 0);
-    pcm.assign(n, 0);
-    cbf.assign(n, 0);
-    edge.assign(n, 0);
-    tq.assign(n, 0);
-    qp.assign(n, 0);
-    mf.assign(n, MvField{});
     slice.assign(size_t(wctb) * hctb, 0xFFFF);
     sao.assign(size_t(wctb) * hctb, SaoParams{});
     slices.clear();
