@@ -63,6 +63,12 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
     return;
   }
   if (sh.num_long_term > 0) throw UnsupportedStream("HEVC: long-term reference pictures are not supported");
+  // only a picture that starts a new coded video sequence may change the picture size (a mid-GOP
+  // SPS with another size would have the picture predict from surfaces of the old size)
+  if (!(irap && no_rasl_output_) && act_w_ && (sps.width != act_w_ || sps.height != act_h_))
+    throw Error("HEVC: picture size changed outside an IRAP picture");
+  act_w_ = sps.width;  // (by value: a repeated SPS NAL replaces the map entry sps_act_ points at)
+  act_h_ = sps.height;
   // picture order count (§8.3.1)
   const int max_lsb = 1 << sps.log2_max_poc_lsb;
   int msb = 0;

@@ -130,6 +130,7 @@ class Decoder {
   const Pps* pps_act_ = nullptr;
   std::vector<u8> rbsp_;
   int prev_tid0_poc_ = 0;
+  int act_w_ = 0, act_h_ = 0;  // picture size of the active coded video sequence
   bool first_ = true, no_rasl_output_ = true, skip_pic_ = false;
   u32 next_uid_ = 1;
   bool gpu_mode_ = false;

@@ -387,7 +387,9 @@ bool RtspClient::read_available(const AuCallback& cb, std::string& why) {
   VEP_CHECK(fd_ >= 0 && dep_, "RtspClient::read_available before open()");
   std::vector<AuPtr> aus;
   u8 tmp[1 << 16];
-  for (;;) {
+  // at most 8 reads per call: a camera that sends faster than we read must not hold the event
+  // loop (or a stop() waiting for this callback) forever; the level-triggered loop comes back
+  for (int reads = 0; reads < 8; ++reads) {
     ssize_t k = ::recv(fd_, tmp, sizeof(tmp), MSG_DONTWAIT);
     if (k < 0 && (errno == EAGAIN || errno == EWOULDBLOCK)) break;
     if (k < 0 && errno == EINTR) continue;

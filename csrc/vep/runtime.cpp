@@ -196,6 +196,9 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
       }
       decoded_upto_ = to;
       if (job.hevc.empty()) return false;
+      for (const auto& p : job.hevc)  // (a size change starts a new coded video sequence)
+        VEP_CHECK(p->width == job.hevc.back()->width && p->height == job.hevc.back()->height,
+                  "HEVC: pictures of different sizes in one decode job");
       job.hevc_slots = hevc_.gpu_slots();
       const hevc::GpuPicture& gp = *job.hevc.back();
       PictureInfo& pi = job.pic;

@@ -124,3 +124,17 @@ def test_hevc_stream_starting_mid_gop_is_rejected_until_idr():
         out += d.decode(au)
     out += d.flush()
     assert len(out) == 2
+
+
+def test_hevc_mid_gop_size_change_is_rejected():
+    """A repeated SPS with another picture size before a P picture (corrupt / spliced stream)
+    must not make the P picture predict from surfaces of the old size."""
+    a = encoder(width=128, height=96)
+    b = encoder(width=160, height=96)
+    aus = [a.next() for _ in range(3)]
+    d = v.HevcDecoder()
+    for au in aus[:2]:
+        d.decode(au)
+    bad = v.AccessUnit.from_nals([b.sps_nal] + aus[2].nals(), pts=aus[2].pts, codec=1)
+    with pytest.raises(Exception, match="size"):
+        d.decode(bad)
