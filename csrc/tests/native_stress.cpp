@@ -235,8 +235,12 @@ static void general_decoder_stress() {
   stop.store(true);
   for (size_t i = ncam; i < th.size(); ++i) th[i].join();
   for (int i = 0; i < ncam; ++i) {
-    CHECK(w.camera(cams[size_t(i)])->decoded.load() > 0);
-    CHECK(w.camera(cams[size_t(i)])->errors.load() == 0);
+    auto c = w.camera(cams[size_t(i)]);
+    if (c->decoded.load() == 0 || c->errors.load() != 0)
+      std::printf("camera %d: decoded %llu errors %llu\n%s", i, (unsigned long long)c->decoded.load(),
+                  (unsigned long long)c->errors.load(), c->logs.dump(true).c_str());
+    CHECK(c->decoded.load() > 0);
+    CHECK(c->errors.load() == 0);
   }
   w.stop();
   std::printf("general decoder: served %llu frames, %llu pictures\n", (unsigned long long)served.load(),

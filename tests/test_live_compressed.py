@@ -282,3 +282,37 @@ def test_rtmp_passthrough_never_stalls_ingest(native):
     assert accepted, "the pass-through never tried to connect"
     assert d1 - d0 >= 40, f"decoding stalled behind RTMP: {d1 - d0} frames in 1 s at {FPS} fps"
     assert aus >= 60
+
+
+def hevc_reference(native, cfg, n_cached, loops=4):
+    """H.265 twin of reference(): newest output frame (BGR) per coding index of the looped cache."""
+    enc = native.SynthH264(cfg)
+    aus = [enc.next() for _ in range(n_cached)]
+    dec = native.HevcDecoder()
+    ref = {}
+    step = 90000 // cfg.fps
+    for k in range(n_cached * loops):
+        a = aus[k % n_cached]
+        au = native.AccessUnit.from_nals(a.nals(), pts=k * step, dts=k * step, keyframe=a.keyframe, codec=1)
+        for pts, poc, t, (y, uv) in dec.decode(au):
+            ref[pts // step] = native.nv12_to_bgr_cpu(y, uv, 0, 0, cfg.width, cfg.height)
+    return ref
+
+
+def test_live_hevc_stream_bit_exact(native):
+    """A compressed H.265 Main camera (CABAC I/P/B) through the live path: RTSP (RFC 7798 FU
+    fragmentation) -> fast-path attempt -> general HEVC decoder in records mode -> worker (CPU
+    mirror here, gfx950 kernels in the GPU twin) -> ring; every published frame equals the
+    reference decoder's."""
+    n = 20
+    cfg = stream_cfg(native, "main", w=320, h=240)
+    cfg.codec = "h265"
+    ref = hevc_reference(native, cfg, n)
+    live = Live(native, cfg, n)
+    try:
+        got = live.frames(1.5)
+        st = live.w.stats(live.cam)
+    finally:
+        live.close()
+    check_frames(got, ref, n, 90000 // FPS)
+    assert len(got) >= 15 and st["decoder"] == "general" and st["errors"] == 0
