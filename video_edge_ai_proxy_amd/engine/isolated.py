@@ -9,6 +9,12 @@ for the device and the cameras are re-added with their pass-through state — th
 per-camera ``restart: always`` containers (server/services/rtsp_process_manager.go:70-81,
 :106-115) at per-GPU granularity, without one process per camera.
 
+The supervising process never initialises the GPU itself (devices are counted through
+``torch.cuda.device_count()``, which does not): starting a child from a process that holds a GPU
+context is what the children are for, not something the parent may do. The GPU tests therefore
+do not drive this class (their pytest process holds a context); tests/test_isolated_hub.py does,
+with CPU-backend children.
+
 Calls travel over authenticated local connections (a small pool per child, so a blocking
 ``latest_frame_bytes`` does not hold the others up). The batched consumer tensor of the
 in-process hub is not offered here; the multi-process form of it is ``parallel.ConsumerBatch``
