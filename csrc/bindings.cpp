@@ -707,6 +707,10 @@ PYBIND11_MODULE(_vep, m) {
     return std::make_pair(parse_us, scan_us);
   }, py::arg("au"), py::arg("iters") = 100, py::arg("prime") = nullptr);
   m.def("rocdecode_available", [] { return gpu::rocdecode_available(); });
+  // VCN backend (vcn.h): which librocdecode is loaded, why none is, load a specific build
+  m.def("vcn_library", [] { return vcn::library(); });
+  m.def("vcn_load_error", [] { return vcn::load_error(); });
+  m.def("vcn_load", [](const std::string& path) { return vcn::load(path); }, py::arg("path"));
   m.def("pinned_pool_stats", [] {
     hostmem::PoolStats st = hostmem::pool_stats();
     py::dict d;
@@ -761,9 +765,14 @@ PYBIND11_MODULE(_vep, m) {
   py::class_<Worker>(m, "Worker")
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
                        std::vector<float> stdv, int max_cameras, int pack_threads,
-                       int letterbox_format, int lanes, int stages, int queue, bool lane_threads) {
+                       int letterbox_format, int lanes, int stages, int queue, bool lane_threads,
+                       const std::string& decoder) {
              WorkerOptions o;
              o.device = device;
+             if (decoder == "native") o.decoder = kDecoderNative;
+             else if (decoder == "vcn") o.decoder = kDecoderVcn;
+             else if (decoder == "auto") o.decoder = kDecoderAuto;
+             else throw Error("decoder must be native, vcn or auto (got '" + decoder + "')");
              o.lanes = lanes;
              o.stages = stages;
              o.queue = queue;
@@ -783,8 +792,9 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
            py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
            py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0,
-           py::arg("queue") = 0, py::arg("lane_threads") = false)
+           py::arg("queue") = 0, py::arg("lane_threads") = false, py::arg("decoder") = "native")
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
+      .def_property_readonly("decoder", [](Worker& w) { return std::string(w.vcn() ? "vcn" : "native"); })
       .def_property_readonly("lanes", &Worker::lanes)
       .def_property_readonly("stages", &Worker::stages)
       .def_property_readonly("inflight", &Worker::inflight)
@@ -869,6 +879,7 @@ PYBIND11_MODULE(_vep, m) {
              d["bytes_in"] = c.bytes_in.load();
              d["last_packet_ms"] = c.last_packet_ms.load();
              d["decoder"] = c.general_decoder() ? "general" : "fast";
+             d["backend"] = c.backend();
              auto ring = c.ring();
              d["published"] = ring ? ring->published() : 0;
              d["width"] = ring ? ring->width() : 0;

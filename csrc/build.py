@@ -107,6 +107,32 @@ def build(jobs: int | None = None, debug: bool = False, verbose: bool = False) -
     return out
 
 
+STUB_SRC = CSRC / "tests" / "rocdec_stub.cpp"
+STUB = ROOT / "tests" / "native" / "libvep_rocdec_stub.so"
+
+
+def build_rocdec_stub() -> Path:
+    """Test double of librocdecode (csrc/tests/rocdec_stub.cpp) for the VCN backend tests, linked
+    against the data-plane objects of build(); kept in-tree so GPU boxes receive it."""
+    flags = _flags(False)
+    obj = OBJ / "tests__rocdec_stub.cpp.o"
+    vep_objs = [OBJ / (s.relative_to(CSRC).as_posix().replace("/", "__") + ".o")
+                for s in sources() if s.parent.name == "vep"]
+    if not obj.exists() or obj.stat().st_mtime < max(STUB_SRC.stat().st_mtime, _newest_header()):
+        _compile(STUB_SRC, obj, flags)
+    newest = max(o.stat().st_mtime for o in [obj, *vep_objs])
+    if not STUB.exists() or STUB.stat().st_mtime < newest:
+        STUB.parent.mkdir(parents=True, exist_ok=True)
+        tmp = STUB.with_suffix(".tmp.so")
+        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", str(obj), *map(str, vep_objs), "-o", str(tmp),
+               "-lpthread", "-Wl,--no-undefined"]
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise RuntimeError(f"stub link failed\n{' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+        os.replace(tmp, STUB)
+    return STUB
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--clean", action="store_true")
@@ -119,6 +145,7 @@ def main() -> None:
         module_path().unlink(missing_ok=True)
     p = build(a.j, a.debug, a.v)
     print(p)
+    print(build_rocdec_stub())
 
 
 if __name__ == "__main__":

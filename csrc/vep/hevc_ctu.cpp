@@ -859,7 +859,7 @@ class CtuLayer {
     if (lvbuf_.size() < 1024) lvbuf_.resize(1024);
     int* lv = lvbuf_.data();
     const int nn = n * n;
-    std::fill(lv, lv + nn, 0);
+    if (kWrite) std::fill(lv, lv + nn, 0);  // (read mode: residual_coding clears what it reads)
     bool tskip = false;
     const TuKey key{c, x0, y0};
     if (dry_) {
@@ -914,10 +914,15 @@ class CtuLayer {
         t.flags |= kTuCoef;
         t.data = u32(g->coefs.size());
         int ex = 0, ey = 0;
-        for (int k = 0; k < n * n; ++k) {
-          const int v = lv[size_t(k)];
-          g->coefs.push_back(i16(v ? dequant_level(v, qp, log2) : 0));
-          if (v) ex = std::max(ex, k & (n - 1)), ey = k >> log2;
+        const size_t off = g->coefs.size();
+        g->coefs.resize(off + size_t(nn));
+        i16* dq = g->coefs.data() + off;
+        for (int k = 0; k < nn; ++k) {
+          const int v = lv[k];
+          if (!v) continue;
+          dq[k] = i16(dequant_level(v, qp, log2));
+          ex = std::max(ex, k & (n - 1));
+          ey = k >> log2;
         }
         t.ext_x = u8(ex);
         t.ext_y = u8(ey);

@@ -29,18 +29,19 @@ struct Basis {
   double u[32][32];
 };
 const Basis& dct_basis(int log2) {
-  static Basis b[4];
-  static bool init = false;
-  if (!init) {
-    for (int l = 0; l < 4; ++l) {
-      const int n = 4 << l, step = 32 / n;
-      const double s = 1.0 / (64.0 * std::sqrt(double(n)));
-      for (int k = 0; k < n; ++k)
-        for (int j = 0; j < n; ++j) b[l].u[k][j] = kDct.m[k * step][j] * s;
+  struct Table {
+    Basis b[4];
+    Table() {
+      for (int l = 0; l < 4; ++l) {
+        const int n = 4 << l, step = 32 / n;
+        const double s = 1.0 / (64.0 * std::sqrt(double(n)));
+        for (int k = 0; k < n; ++k)
+          for (int j = 0; j < n; ++j) b[l].u[k][j] = kDct.m[k * step][j] * s;
+      }
     }
-    init = true;
-  }
-  return b[log2 - 2];
+  };
+  static const Table t;  // (thread-safe one-time initialisation: encoders run on many threads)
+  return t.b[log2 - 2];
 }
 
 // Forward transform + dead-zone quantisation (level = C / Qstep, Qstep = 2^((qp - 4) / 6)).

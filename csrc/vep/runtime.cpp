@@ -146,14 +146,76 @@ std::string LogRing::dump(bool err, size_t last) const {
 // ------------------------------------------------------------------------------------ Camera
 
 Camera::Camera(Worker& w, int index, std::string name, int ring_slots)
-    : ring_slots_cfg(ring_slots), w_(w), index_(index), name_(std::move(name)) {}
+    : ring_slots_cfg(ring_slots), w_(w), index_(index), name_(std::move(name)), use_vcn_(w.vcn()) {}
 
 std::vector<AuPtr> Camera::gop_snapshot() {
   std::lock_guard<std::mutex> g(mu_);
   return gop_;
 }
 
+// VCN backend: the AUs go to the camera's rocDecode session; the newest picture that reached
+// display order is published (older ones of a catch-up run are released at once, as the native
+// path collapses them).
+bool Camera::build_vcn_job(DecodeJob& job, size_t from, size_t to) {
+  job.cam = index_;
+  job.refresh = true;  // a complete picture: the surface is rewritten whole
+  vcn::FramePtr out;
+  try {
+    if (!vcn_) {
+      const int dev = w_.device().gpu() ? w_.device().id() : 0;
+      vcn_ = std::make_unique<vcn::Session>(gop_[from]->codec, dev);
+      logs.add(false, std::string("VCN decoder session opened (") + vcn::library() + ")");
+    }
+    const bool key_only = keyframe_only.load() && to - from == 1 && gop_[from]->keyframe;
+    for (size_t i = from; i < to; ++i) {
+      std::vector<vcn::FramePtr> fs = vcn_->decode(*gop_[i], i64(i));
+      if (!fs.empty()) out = fs.back();
+    }
+    if (key_only) {  // nothing else of the GOP is decoded: drain the reorder queue
+      std::vector<vcn::FramePtr> fs = vcn_->flush();
+      if (!fs.empty()) out = fs.back();
+    }
+  } catch (const std::exception& e) {
+    errors.fetch_add(1);
+    logs.add(true, std::string("VCN decode failed: ") + e.what());
+    decoded_upto_ = gop_.size();  // wait for the next keyframe
+    if (vcn_) {
+      try {
+        vcn_->flush();
+      } catch (const std::exception&) {
+        vcn_.reset();  // a fresh session at the next keyframe
+      }
+    }
+    return false;
+  }
+  decoded_upto_ = to;
+  if (!out) return false;  // reordering: nothing reached display order yet
+  job.ext = out;
+  PictureInfo& pi = job.pic;
+  pi = PictureInfo{};
+  pi.width = out->width;
+  pi.height = out->height;
+  pi.coded_width = (out->width + 15) & ~15;
+  pi.coded_height = (out->height + 15) & ~15;
+  pi.pict_type = out->type;
+  pi.idr = out->keyframe;
+  FrameMeta& m = job.meta;
+  m.width = out->width;
+  m.height = out->height;
+  m.pts = out->pts;
+  m.dts = out->dts;
+  m.timestamp = out->pts;
+  m.packet = out->tag;
+  m.keyframe = keyframes_;
+  m.is_keyframe = out->keyframe;
+  m.is_corrupt = out->corrupt;
+  m.frame_type = out->type;
+  m.arrival_ms = gop_[to - 1]->arrival_ms;
+  return true;
+}
+
 bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
+  if (use_vcn_) return build_vcn_job(job, from, to);
   job.cam = index_;
   job.refresh = refresh;
   const AccessUnit* last = nullptr;
@@ -347,6 +409,9 @@ constexpr int kDefaultStages = 3;
 constexpr int kDefaultLaneQueue = 2;
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
+  if (opt_.decoder == kDecoderVcn)
+    VEP_CHECK(vcn::available(), "decoder backend 'vcn' requested but rocDecode is unavailable: " + vcn::load_error());
+  vcn_ = opt_.decoder == kDecoderVcn || (opt_.decoder == kDecoderAuto && vcn::available());
   if (dev_.gpu()) {
     dev_.bind();
     int nl = opt_.lanes;
@@ -1178,9 +1243,10 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       d.offsets = reinterpret_cast<const u32*>(table_ptr(st.d, i));
       d.payload = st.d + pay_off[size_t(i)];
     }
-    d.wmbs = j.general() ? j.pic.coded_width / 16 : j.upd.width_mbs;
-    d.hmbs = j.general() ? j.pic.coded_height / 16 : j.upd.height_mbs;
-    if (j.general()) d.mask = d.prefix = nullptr;  // pure conversion of the reconstructed slot
+    const bool whole = j.general() || j.ext;  // the slot already holds the picture
+    d.wmbs = whole ? j.pic.coded_width / 16 : j.upd.width_mbs;
+    d.hmbs = whole ? j.pic.coded_height / 16 : j.upd.height_mbs;
+    if (whole) d.mask = d.prefix = nullptr;  // pure conversion of the reconstructed slot
     d.out_w = j.pic.width;
     d.out_h = j.pic.height;
     d.crop_left = j.pic.crop_left;
@@ -1356,6 +1422,21 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     }
     if (sao) gpu::launch_hevc_sao(hd2, np, hround_work[size_t(r)][1], cs);
   }
+  // VCN pictures: the video core's surfaces -> the cameras' NV12 surfaces (device copies on the
+  // lane stream, ordered before the conversion; the surfaces return to rocDecode when the batch
+  // completes and its jobs are dropped)
+  for (int i = 0; i < n; ++i) {
+    const DecodeJob& j = jobs[size_t(i)];
+    if (!j.ext) continue;
+    const Camera* c = cams_[size_t(j.cam)].get();
+    const vcn::Frame& f = *j.ext;
+    const size_t pitch = size_t(c->surface.wmbs) * 16;
+    VEP_CHECK(size_t(f.width) <= pitch && f.height <= c->surface.hmbs * 16, "VCN picture exceeds the camera surface");
+    VEP_HIP(hipMemcpy2DAsync(c->surface.y, pitch, f.y, f.pitch_y, size_t(f.width), size_t(f.height),
+                             hipMemcpyDefault, cs));
+    VEP_HIP(hipMemcpy2DAsync(c->surface.uv, pitch, f.uv, f.pitch_uv, size_t(f.width), size_t(f.height / 2),
+                             hipMemcpyDefault, cs));
+  }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), nout, tiles,
                              cs);
   if (opt_.letterbox_size > 0) {
@@ -1386,7 +1467,15 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
       err[i] = (b[-2] != 0x0D || b[-1] != 0x00) ? 1u : 0u;
     }
     if (err[i]) continue;
-    if (jobs[i].general()) {
+    if (jobs[i].ext) {  // VCN picture (host-visible planes on the CPU backend)
+      const vcn::Frame& f = *jobs[i].ext;
+      HostSurface& hs = c.surface.host[0];
+      VEP_CHECK(f.width <= hs.coded_w && f.height <= hs.coded_h, "VCN picture exceeds the camera surface");
+      for (int r = 0; r < f.height; ++r)
+        std::memcpy(&hs.y[size_t(r) * size_t(hs.coded_w)], f.y + size_t(r) * f.pitch_y, size_t(f.width));
+      for (int r = 0; r < f.height / 2; ++r)
+        std::memcpy(&hs.uv[size_t(r) * size_t(hs.coded_w)], f.uv + size_t(r) * f.pitch_uv, size_t(f.width));
+    } else if (jobs[i].general()) {
       for (const auto& pic : jobs[i].avc) avc::cpu_reconstruct(*pic, c.surface.host);
       for (const auto& pic : jobs[i].hevc) hevc::cpu_execute(*pic, c.surface.host);
     } else {

@@ -24,6 +24,7 @@
 #include "hevc_kern.h"
 #include "gpu.h"
 #include "pool.h"
+#include "vcn.h"
 
 namespace vep {
 
@@ -110,6 +111,9 @@ struct DecodeJob {
   // converted and published), -1 when every picture of the job is still waiting for output
   // (B-frame reordering): the job then only reconstructs.
   int out_slot = -1;
+  // VCN backend (vcn.h): a picture decoded by the video core; the worker copies its planes into
+  // the camera's surface, then converts / letterboxes / publishes it like any other frame.
+  vcn::FramePtr ext;
   bool general() const { return !avc.empty() || !hevc.empty(); }
   bool has_output() const { return !general() || out_slot >= 0; }
   // (H.265: the DPB slots plus one scratch surface, the SAO input copy)
@@ -172,6 +176,8 @@ class Camera {
   StreamParser& parser() { return parser_; }
   // true once the stream left the I_PCM / P_Skip fast path (general H.264 / H.265 decoder in use)
   bool general_decoder() const { return full_ || hevc_full_; }
+  // decoder backend serving this camera: "vcn" (rocDecode) or "native" (CPU parse + gfx950)
+  const char* backend() const { return use_vcn_ ? "vcn" : "native"; }
   std::mutex& gop_mutex() { return mu_; }
   std::vector<AuPtr> gop_snapshot();   // current GOP packets (for RTMP flush / archive)
 
@@ -191,6 +197,7 @@ class Camera {
  private:
   friend class Worker;
   bool build_job(DecodeJob& job, size_t from, size_t to, bool refresh);
+  bool build_vcn_job(DecodeJob& job, size_t from, size_t to);
   Worker& w_;
   int index_;
   std::string name_;
@@ -206,6 +213,9 @@ class Camera {
   // the worker reconstructs them on the GPU (gpu_hevc.hip) or with the CPU mirror.
   bool hevc_full_ = false;
   hevc::Decoder hevc_;
+  // VCN backend: one rocDecode session per camera, created on the first keyframe
+  bool use_vcn_ = false;
+  std::unique_ptr<vcn::Session> vcn_;
 };
 
 struct WorkerOptions {
@@ -230,7 +240,11 @@ struct WorkerOptions {
   // the default.
   int queue = 0;
   bool lane_threads = false;  // one launcher thread per lane (also VEP_LANE_THREADS=1)
+  // Decoder backend: kDecoderNative (CPU parse + gfx950 reconstruction), kDecoderVcn (rocDecode
+  // on the video core; fails when librocdecode is missing) or kDecoderAuto (VCN when present).
+  int decoder = 0;
 };
+enum DecoderBackend : int { kDecoderNative = 0, kDecoderVcn = 1, kDecoderAuto = 2 };
 
 class Worker {
  public:
@@ -398,6 +412,11 @@ class Worker {
 
  public:
   bool direct_reads() const { return direct_reads_; }
+  // cameras decode through rocDecode / VCN (WorkerOptions::decoder)
+  bool vcn() const { return vcn_; }
+
+ private:
+  bool vcn_ = false;
 };
 
 // Protobuf wire encoding of chrys.cloud.videostreaming.v1beta1.VideoFrame

@@ -140,7 +140,7 @@ def test_end_to_end_serving(native, farm, hubapp):
     assert "vep_decoded_frames_total" in m and 'camera="front_door"' in m
     assert "vep_decode_latency_seconds_bucket" in m and "vep_pinned_pool_bytes" in m
     h = rest.get("/healthz").json()
-    assert h["decoder_backend"] == "native-subset"
+    assert h["decoder_backends"] == ["native"]
 
     # per-GOP archive on disk: <dir>/<device>/<start_ms>_<dur_ms>.mp4
     t0 = time.time()

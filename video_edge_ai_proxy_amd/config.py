@@ -65,6 +65,8 @@ class GpuConfig:
     idle_cutoff_ms: int = 10000                  # rtsp_to_rtmp.py:144-145
     isolation: str = "thread"                    # thread (one process) | process (a supervised
                                                  # worker process per GPU, engine/isolated.py)
+    decoder: str = "native"                      # native (CPU parse + gfx950 reconstruction) |
+                                                 # vcn (rocDecode on the video core) | auto
 
 
 @dataclass

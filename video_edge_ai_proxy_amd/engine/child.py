@@ -39,7 +39,7 @@ def _serve(hub, conn, lock_stop: threading.Event) -> None:
             elif method == "worker_stats":
                 w = hub.workers[0]
                 res = {"batches": w.batches, "frames": w.frames, "gpu_ms_total": w.gpu_ms_total,
-                       "direct_reads": bool(w.direct_reads)}
+                       "direct_reads": bool(w.direct_reads), "decoder": str(w.decoder)}
             elif method == "start_camera":
                 h = hub.start_camera(*args, **kwargs)
                 res = {"cam": h.cam}

@@ -69,7 +69,8 @@ class Hub:
             w = native.Worker(device=d, letterbox_size=int(g.letterbox_size),
                               chw_dtype=_CHW.get(g.letterbox_dtype, 0), mean=list(g.mean),
                               std=list(g.std), max_cameras=int(g.max_cameras_per_gpu),
-                              letterbox_format=1 if g.letterbox_format == "nv12" else 0)
+                              letterbox_format=1 if g.letterbox_format == "nv12" else 0,
+                              decoder=str(getattr(g, "decoder", "native")))
             w.start()
             self.workers.append(w)
         # Consumer batch: with letterbox_size > 0 every worker letterboxes each frame it publishes

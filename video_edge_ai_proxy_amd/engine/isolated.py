@@ -131,7 +131,8 @@ class _WorkerView:
         try:
             return self._hub._child(self._i).call("worker_stats")
         except Exception:  # noqa: BLE001 — a restarting child reports zeros
-            return {"batches": 0, "frames": 0, "gpu_ms_total": 0.0, "direct_reads": False}
+            return {"batches": 0, "frames": 0, "gpu_ms_total": 0.0, "direct_reads": False,
+                    "decoder": self._hub.cfg.gpu.decoder}
 
     @property
     def batches(self):
@@ -148,6 +149,10 @@ class _WorkerView:
     @property
     def direct_reads(self):
         return self._stats()["direct_reads"]
+
+    @property
+    def decoder(self):
+        return self._stats()["decoder"]
 
 
 class ProcessHub:

@@ -129,7 +129,8 @@ def create_app(pm: ProcessManager, sm: SettingsManager, metrics=None) -> FastAPI
         from .._native import native
 
         return {"ok": True, "cameras": len(pm.hub.cameras), "devices": pm.hub.devices,
-                "decoder_backend": "rocdecode" if native.rocdecode_available() else "native-subset",
+                "decoder_backends": [w.decoder for w in pm.hub.workers],
+                "vcn_available": bool(native.rocdecode_available()),
                 "direct_host_reads": [bool(w.direct_reads) for w in pm.hub.workers]}
 
     @app.get("/metrics")
