@@ -97,9 +97,15 @@ def parse_args():
                     help="replay = pre-encoded AUs fed to the decode pipeline (decode-only); rtsp = an "
                          "in-process loopback RTSP camera farm, unthrottled, with the production "
                          "ingest (RtspClient + RTP depacketizer + lazy decoder) inside the timed loop")
+    ap.add_argument("--keyframe-only", action="store_true",
+                    help="BASELINE config 3 (selective I-frame decode): every camera in keyframe-only "
+                         "mode (the reference's read_image.py --keyframe_only); needs --source rtsp so "
+                         "every access unit still crosses ingest and only IDR pictures are decoded")
     ap.add_argument("--clients", type=int, default=32,
                     help="concurrent gRPC clients for the latency run (one stream each)")
     a = ap.parse_args()
+    if a.keyframe_only and a.source != "rtsp":
+        ap.error("--keyframe-only needs --source rtsp (the ingest filters the access units)")
     if a.qp is None:
         a.qp = 27 if a.profile == "baseline" else 25
     if a.temporal_noise is None:
@@ -178,6 +184,8 @@ class RtspFarm:
         self.srv.start()
         worker.start()
         self.idx = [worker.add_camera(f"r{rank}rtsp{i}", a.ring_slots) for i in range(self.cams)]
+        for cam in self.idx:
+            worker.set_keyframe_only(cam, a.keyframe_only)
         self._touch()
         self.sessions = []
         for i, cam in enumerate(self.idx):
@@ -260,13 +268,14 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         gpu_ms = worker.gpu_ms_total - g0
         wire_bytes = s1["bytes_in"] - s0["bytes_in"]
         errors = s1["errors"] - s0["errors"]
+        aus = s1["packets"] - s0["packets"]  # access units through Camera::on_access_unit
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes], dtype=torch.float64, device=dev)
+            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes, aus], dtype=torch.float64, device=dev)
             dist.all_reduce(fr, op=dist.ReduceOp.SUM)
-            pictures, frames, dropped, errors, wire_bytes = (int(v) for v in fr.tolist())
+            pictures, frames, dropped, errors, wire_bytes, aus = (int(v) for v in fr.tolist())
         conc = (None, None)
         nconc = 0
         if rank == 0 and a.latency_samples > 0 and a.clients > 0:
@@ -296,6 +305,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                      f"FU-A), unthrottled; {wire_bytes * 8 / max(1, pictures) * a.fps / 1e6:.1f} Mbit/s per "
                      f"camera at {a.fps} fps (wire bytes per decoded picture)"),
             "source": "rtsp",
+            "keyframe_only": a.keyframe_only,
             "config": {
                 "model": f"{cams * max(world, 1)}x{a.width}x{a.height}p{a.fps} {CODEC[a.codec]} cameras",
                 "global_batch": cams * max(world, 1),
@@ -313,6 +323,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                                       "a catch-up batch are superseded before any client could read them",
             "frames_decoded": pictures,
             "frames_published": frames,
+            "access_units_ingested": aus,
+            "access_units_per_s": round(aus / elapsed, 1),
             "frames_dropped": dropped,
             "decode_errors": errors,
             "concurrent_clients": a.clients,

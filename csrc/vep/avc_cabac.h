@@ -258,4 +258,104 @@ struct AvcBins {
   }
 };
 
+// Decoder direction of residual_block_cabac, the parse hot loop (most bins of a High-profile
+// picture): same bins, same context selection as the generic body above, with the arithmetic
+// decoder held in a local copy so range/offset/bit cache stay in registers across the context
+// byte updates (see cabac.h).
+template <>
+inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef, u8* nzpos) {
+  cabac::Ctx* const ctx = e.ctx;
+  cabac::Decoder d = e.d;
+  if (cbf_inc >= 0 && !d.decision(ctx[85 + kCbfCatOff[cat] + cbf_inc])) {
+    e.d = d;
+    return 0;
+  }
+  int num = 0, i = 0;
+  const bool b8 = cat == kCatLuma8x8;
+  if (b8) {
+    cabac::Ctx* const sig = ctx + 402;
+    cabac::Ctx* const last = ctx + 417;
+    for (; i < 63; ++i)
+      if (d.decision(sig[kSig8x8Frame[i]])) {
+        nzpos[num++] = u8(i);
+        if (d.decision(last[kLast8x8[i]])) break;
+      }
+  } else {
+    cabac::Ctx* const sig = ctx + 105 + kSigCatOff[cat];
+    cabac::Ctx* const last = ctx + 166 + kSigCatOff[cat];
+    if (cat == kCatChromaDc) {
+      for (; i < n - 1; ++i) {
+        const int si = i < 2 ? i : 2;
+        if (d.decision(sig[si])) {
+          nzpos[num++] = u8(i);
+          if (d.decision(last[si])) break;
+        }
+      }
+    } else {
+      for (; i < n - 1; ++i)
+        if (d.decision(sig[i])) {
+          nzpos[num++] = u8(i);
+          if (d.decision(last[i])) break;
+        }
+    }
+  }
+  if (i == n - 1) nzpos[num++] = u8(n - 1);
+  cabac::Ctx* const absc = ctx + (b8 ? 426 : 227 + kAbsCatOff[cat]);
+  const int gt1_max = cat == kCatChromaDc ? 3 : 4;
+  int gt1 = 0, eq1 = 0;
+  for (int k = num - 1; k >= 0; --k) {
+    int level = 1;
+    if (d.decision(absc[gt1 != 0 ? 0 : (eq1 < 3 ? eq1 + 1 : 4)])) {
+      cabac::Ctx& cx = absc[5 + (gt1 < gt1_max ? gt1 : gt1_max)];
+      int v = 1;
+      while (v < 14 && d.decision(cx)) ++v;
+      if (v >= 14) {  // UEG0 suffix
+        int kk = 0;
+        while (d.bypass()) {
+          v += 1 << kk;
+          ++kk;
+          VEP_CHECK(kk < 24, "CABAC Exp-Golomb suffix too long");
+        }
+        while (kk--) v += int(d.bypass()) << kk;
+      }
+      level = v + 1;
+      ++gt1;
+    } else {
+      ++eq1;
+    }
+    coef[nzpos[k]] = d.bypass() ? -level : level;
+  }
+  e.d = d;
+  return num;
+}
+
+// Decoder direction of mvd_lX (UEG3, signed, uCoff 9), the second-largest bin consumer of P/B
+// pictures; local engine copy as above.
+template <>
+inline int AvcBins<BinDecoder>::mvd(int base, int inc, int) {
+  cabac::Ctx* const ctx = e.ctx;
+  cabac::Decoder d = e.d;
+  if (!d.decision(ctx[base + inc])) {
+    e.d = d;
+    return 0;
+  }
+  int k = 1, c = base + 3;
+  while (k < 9 && d.decision(ctx[c])) {
+    ++k;
+    if (c < base + 6) ++c;
+  }
+  if (k >= 9) {  // UEG3 suffix
+    int kk = 3;
+    while (d.bypass()) {
+      k += 1 << kk;
+      ++kk;
+      VEP_CHECK(kk < 24, "CABAC Exp-Golomb suffix too long");
+    }
+    while (kk--) k += int(d.bypass()) << kk;
+  }
+  const int r = d.bypass() ? -k : k;
+  e.d = d;
+  return r;
+}
+
 }  // namespace vep::avc

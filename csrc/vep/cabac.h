@@ -74,6 +74,13 @@ struct Ctx {
 // unpredictable on residual data). (A variant keeping the offset scaled with a 16-bit look-ahead
 // window and a marker bit measured 13% slower on the parse benchmark: the extra shift sits on
 // the range -> offset dependency chain.)
+//
+// Hot loops (residual blocks) work on a local copy of the decoder (`Decoder d = engine; ...;
+// engine = d;`): Ctx is a pair of u8, and u8 stores may alias any object, so with the engine
+// reached through a pointer every context update would force range/offset/cache back to memory
+// and reload them on the next bin. A local copy whose address never escapes (every member is
+// force-inlined) stays in registers.
+#define VEP_CABAC_INLINE inline __attribute__((always_inline))
 class Decoder {
  public:
   Decoder(const u8* p, size_t n, size_t bytepos) : p_(p), n_(n) { start(bytepos); }
@@ -86,7 +93,7 @@ class Decoder {
     range_ = 510;
     offset_ = bits(9);
   }
-  u32 decision(Ctx& c) {
+  VEP_CABAC_INLINE u32 decision(Ctx& c) {
     const u32 st = c.state;
     const u32 lps = kRangeLps[st][(range_ >> 6) & 3];
     const u32 rmps = range_ - lps;
@@ -107,7 +114,7 @@ class Decoder {
     renorm();
     return 0;
   }
-  u32 bypass() {
+  VEP_CABAC_INLINE u32 bypass() {
     offset_ = (offset_ << 1) | bits(1);
     if (offset_ >= range_) {
       offset_ -= range_;
@@ -118,26 +125,26 @@ class Decoder {
   size_t bitpos() const { return byte_ * 8 - size_t(cbits_); }
   size_t aligned_bytepos() const { return (bitpos() + 7) >> 3; }
  private:
-  void renorm() {  // range_ in [2, 510]: shift it back to >= 256 (0 when it already is)
+  VEP_CABAC_INLINE void renorm() {  // range_ in [2, 510]: shift it back to >= 256 (0 when it already is)
     const int sh = __builtin_clz(range_) - 23;
     range_ <<= sh;
     offset_ = (offset_ << sh) | bits0(sh);
   }
-  u32 bits(int k) {  // 1 <= k <= 9
+  VEP_CABAC_INLINE u32 bits(int k) {  // 1 <= k <= 9
     if (cbits_ < k) refill();
     const u32 v = u32(cache_ >> (64 - k));
     cache_ <<= k;
     cbits_ -= k;
     return v;
   }
-  u32 bits0(int k) {  // 0 <= k <= 8 (k = 0 reads nothing)
+  VEP_CABAC_INLINE u32 bits0(int k) {  // 0 <= k <= 8 (k = 0 reads nothing)
     if (cbits_ < k) refill();
     const u32 v = u32((cache_ >> 1) >> (63 - k));
     cache_ <<= k;
     cbits_ -= k;
     return v;
   }
-  void refill() {
+  VEP_CABAC_INLINE void refill() {
     if (byte_ + 8 <= n_) {  // whole bytes that fit behind the cached bits, one load
       u64 w;
       std::memcpy(&w, p_ + byte_, 8);

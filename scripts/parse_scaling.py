@@ -1,4 +1,4 @@
-"""Host CAVLC parse throughput vs thread count (no GPU work): the replay bench's parse stage
+"""Host H.264 parse throughput (PROFILE=baseline|main|high) vs thread count (no GPU work): the replay bench's parse stage
 alone, on synthetic 1080p camera streams. Usage: python scripts/parse_scaling.py [cams] [threads...]"""
 import os
 import sys
@@ -13,7 +13,12 @@ def main():
     cfg = vep.SynthConfig()
     cfg.width, cfg.height, cfg.fps, cfg.gop = 1920, 1080, 30, 30
     cfg.compressed = True
-    cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = 27, 8.0, 1.0, 1
+    profile = os.environ.get("PROFILE", "baseline")
+    if profile == "baseline":
+        cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = 27, 8.0, 1.0, 1
+    else:  # bench.py's default High CABAC IBBP streams
+        cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = 25, 8.0, 1.5, 1
+        cfg.profile, cfg.bframes, cfg.cabac = profile, 2, True
     w = vep.Worker(device=-1, max_cameras=cams * len(threads))
     for th in threads:
         rb = vep.ReplayBench(w, cams, cfg, cached_frames=30, threads=th, ring_slots=2,
