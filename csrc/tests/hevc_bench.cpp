@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <string>
 
+#include "sampler.h"
 #include "vep/hevc_dec.h"
 
 using namespace vep;
@@ -27,6 +28,18 @@ int main(int argc, char** argv) {
     bytes += aus.back()->bytes();
   }
   const bool records = argc > 6 && std::string(argv[6]) == "records";  // parse only (GPU mode)
+  if (const char* p = std::getenv("PROF")) {
+    sampler::run(std::atof(p), [&] {
+      hevc::Decoder d;
+      d.set_gpu_mode(records);
+      for (auto& a : aus) {
+        d.decode(*a);
+        d.take_gpu_pictures();
+      }
+      d.flush();
+    });
+    return 0;
+  }
   double best = 1e30;
   for (int pass = 0; pass < 5; ++pass) {
     hevc::Decoder d;

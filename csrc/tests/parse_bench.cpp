@@ -14,44 +14,11 @@
 #include <algorithm>
 #include <cstring>
 
+#include "sampler.h"
 #include "vep/avc.h"
 
 using namespace vep;
 
-// Sampling profiler (`PROF=<seconds>`): SIGPROF every ms of CPU time records the interrupted
-// instruction address; the histogram is written to parse_prof.txt for llvm-symbolizer.
-namespace {
-constexpr int kMaxSamples = 1 << 20;
-uintptr_t g_samples[kMaxSamples];
-std::atomic<int> g_nsamples{0};
-void on_prof(int, siginfo_t*, void* uc) {
-  const int i = g_nsamples.fetch_add(1, std::memory_order_relaxed);
-  if (i < kMaxSamples) g_samples[i] = uintptr_t(static_cast<ucontext_t*>(uc)->uc_mcontext.gregs[REG_RIP]);
-}
-void run_profile(const std::vector<std::shared_ptr<AccessUnit>>& aus, double seconds) {
-  struct sigaction sa {};
-  sa.sa_sigaction = on_prof;
-  sa.sa_flags = SA_SIGINFO | SA_RESTART;
-  sigaction(SIGPROF, &sa, nullptr);
-  itimerval it{{0, 1000}, {0, 1000}};
-  setitimer(ITIMER_PROF, &it, nullptr);
-  const auto t0 = std::chrono::steady_clock::now();
-  while (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() < seconds) {
-    avc::Decoder d;
-    for (auto& a : aus) (void)d.parse(*a);
-  }
-  itimerval off{};
-  setitimer(ITIMER_PROF, &off, nullptr);
-  std::map<uintptr_t, int> hist;
-  const int n = std::min(g_nsamples.load(), kMaxSamples);
-  for (int i = 0; i < n; ++i) ++hist[g_samples[i]];
-  // absolute addresses: build the profiling binary with -no-pie
-  FILE* f = std::fopen("parse_prof.txt", "w");
-  for (auto& [a, c] : hist) std::fprintf(f, "%d 0x%lx\n", c, (unsigned long)a);
-  std::fclose(f);
-  std::printf("profile: %d samples -> parse_prof.txt\n", n);
-}
-}  // namespace
 
 
 int main(int argc, char** argv) {
@@ -81,7 +48,10 @@ int main(int argc, char** argv) {
   size_t bytes = 0;
   for (auto& a : aus) bytes += a->bytes();
   if (const char* p = std::getenv("PROF")) {
-    run_profile(aus, std::atof(p));
+    sampler::run(std::atof(p), [&] {
+      avc::Decoder d;
+      for (auto& a : aus) (void)d.parse(*a);
+    });
     return 0;
   }
   double best = 1e30;

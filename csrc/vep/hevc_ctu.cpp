@@ -202,10 +202,18 @@ class CtuLayer {
   }
   int qp_y() const { return ((qp_pred_ + cu_qp_delta_ + 52) % 52); }
 
+  // f(k) for every 4x4 block index of the rectangle clipped to the picture: row by row over
+  // consecutive indices (the per-block bookkeeping of skip-heavy pictures is a large share of
+  // the parse, so no per-block index arithmetic or bound checks).
   template <class F>
   void for4(int x0, int y0, int w, int h, F f) {
-    for (int y = y0; y < y0 + h && y < pc_.H; y += 4)
-      for (int x = x0; x < x0 + w && x < pc_.W; x += 4) f(pc_.i4(x, y));
+    const int xe = std::min(x0 + w, pc_.W), ye = std::min(y0 + h, pc_.H);
+    if (xe <= x0) return;
+    const size_t cnt = size_t((xe - x0 + 3) >> 2);
+    for (int y = y0; y < ye; y += 4) {
+      const size_t k0 = pc_.i4(x0, y);
+      for (size_t k = k0; k < k0 + cnt; ++k) f(k);
+    }
   }
 
   // -------------------------------------------------------------------- coding unit

@@ -89,7 +89,8 @@ struct PicCtx {
   bool avail(int x, int y, int xn, int yn, const std::vector<u8>& flag) const {
     if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
     if (!flag[i4(xn, yn)]) return false;
-    return slice[size_t(ctb_of(xn, yn))] == slice[size_t(ctb_of(x, y))];
+    // a decoded block of a single-slice picture is in the current block's slice
+    return slices.size() == 1 || slice[size_t(ctb_of(xn, yn))] == slice[size_t(ctb_of(x, y))];
   }
 };
 
