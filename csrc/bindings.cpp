@@ -4,6 +4,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "vep/hostprof.h"
 #include "vep/avc_cavlc.h"
 #include "vep/bench_driver.h"
 #include "vep/cabac.h"
@@ -707,6 +708,9 @@ PYBIND11_MODULE(_vep, m) {
     return std::make_pair(parse_us, scan_us);
   }, py::arg("au"), py::arg("iters") = 100, py::arg("prime") = nullptr);
   m.def("rocdecode_available", [] { return gpu::rocdecode_available(); });
+  m.def("hostprof_start", &hostprof::start, py::arg("interval_us") = 1000,
+        "start sampling host CPU time (SIGPROF, every thread of the process)");
+  m.def("hostprof_stop", &hostprof::stop, py::arg("path"), "stop sampling; write 'count object offset symbol' lines");
   // VCN backend (vcn.h): which librocdecode is loaded, why none is, load a specific build
   m.def("vcn_library", [] { return vcn::library(); });
   m.def("vcn_load_error", [] { return vcn::load_error(); });

@@ -47,7 +47,7 @@ def _flags(debug: bool) -> list[str]:
         f"-I{pybind11.get_include()}",
         f"-I{sysconfig.get_paths()['include']}",
     ]
-    opt = ["-O1", "-g"] if debug else ["-O3"]
+    opt = ["-O1", "-g"] if debug else ["-O3", "-gline-tables-only"]  # line tables: hostprof symbolisation
     return [
         f"--offload-arch={ARCH}",
         "-std=c++17",
