@@ -1020,7 +1020,22 @@ int dpb_slots_for(const Sps& sps) {
 }  // namespace
 
 PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
-  auto pic = std::make_shared<Picture>();
+  auto pic = pic_pool_->acquire([](Picture& p) {  // default state, pool capacities kept
+    std::vector<MbRec> mbs = std::move(p.mbs);
+    std::vector<i16> coefs = std::move(p.coefs), mvs = std::move(p.mvs);
+    std::vector<WpEntry> wps = std::move(p.wps);
+    std::vector<OutFrame> outputs = std::move(p.outputs);
+    p = Picture{};
+    coefs.clear();
+    mvs.clear();
+    wps.clear();
+    outputs.clear();
+    p.mbs = std::move(mbs);
+    p.coefs = std::move(coefs);
+    p.mvs = std::move(mvs);
+    p.wps = std::move(wps);
+    p.outputs = std::move(outputs);
+  });
   bool got = false;
   bool hard_flush = false;  // IDR with a new picture geometry: waiting pictures leave at once
   int slice_idx = 0;
@@ -1203,7 +1218,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   if (first.nal_ref_idc != 0) {
     std::shared_ptr<ColMotion> col;
     if (act_sps->profile_idc != 66)  // B slices possible: keep the motion for direct prediction
-      col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids, act_sps->direct_8x8);
+      col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids, act_sps->direct_8x8, col_pool_.get());
     mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col));
   }
   const bool boundary = first.idr() || first.has_mmco5();
@@ -1258,8 +1273,8 @@ void validate(const Picture& p) {
 
 std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, int hmbs,
                                             const std::vector<std::array<std::vector<u32>, 2>>& slice_uids,
-                                            bool corners) {
-  auto col = std::make_shared<ColMotion>();
+                                            bool corners, Recycler<ColMotion>* pool) {
+  auto col = pool ? pool->acquire([](ColMotion& c) { c.b.clear(); }) : std::make_shared<ColMotion>();
   col->wmbs = wmbs;
   col->hmbs = hmbs;
   col->corners = corners;

@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 
+#include "recycle.h"
 #include "avc_recon.h"
 #include "codec.h"
 
@@ -344,6 +345,9 @@ class Decoder {
   std::vector<u32> epb_;
   MbNeighbours nb_;
   std::vector<RefPic> dpb_;
+  // buffer recycling (recycle.h): pictures in flight per camera (parse window + GPU stages)
+  std::shared_ptr<Recycler<Picture>> pic_pool_ = Recycler<Picture>::make(12);
+  std::shared_ptr<Recycler<ColMotion>> col_pool_ = Recycler<ColMotion>::make(8);
   std::vector<Pending> pending_;  // decoded, not yet output (POC order decides)
   std::vector<ListEntry> list_[2];  // refIdx -> entry of the current slice
   int max_lt_idx_ = -1;     // MaxLongTermFrameIdx ("no long-term frame indices" = -1)

@@ -35,7 +35,7 @@ WpEntry wp_entry(const SliceEnv& env, int r0, int r1);
 // `corners`: direct_8x8_inference is on, keep only each 8x8's outer corner block.
 std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, int hmbs,
                                             const std::vector<std::array<std::vector<u32>, 2>>& slice_uids,
-                                            bool corners);
+                                            bool corners, Recycler<ColMotion>* pool = nullptr);
 
 // Inter prediction of one MB (list-0 / list-1 + weights), exactly the reconstruction's: py 16x16
 // luma, pc 2 x 8x8 chroma. mv0 / mv1: 16 (x, y) per list (mv1 may be null).
