@@ -36,7 +36,7 @@ void check_supported(const Sps& sps, const Pps& pps) {
 }
 }  // namespace
 
-Decoder::Decoder() : pc_(std::make_unique<PicCtx>()) {}
+Decoder::Decoder() : pc_(std::make_unique<PicCtx>()), gpu_pool_(Recycler<GpuPicture>::make(12)) {}
 Decoder::~Decoder() = default;
 
 void Decoder::bump(std::vector<FramePtr>& out) {
@@ -161,7 +161,28 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   pc_->init(sps, pps, &cur_->s);
   pc_->poc = poc;
   if (gpu_mode_) {
-    cur_gpu_ = std::make_shared<GpuPicture>();
+    cur_gpu_ = gpu_pool_->acquire([](GpuPicture& g) {  // default state, capacities kept
+      GpuPicture fresh;
+      auto keep = [](auto& from, auto& to) {
+        from.clear();
+        to.swap(from);
+      };
+      keep(g.pus, fresh.pus);
+      keep(g.tus, fresh.tus);
+      keep(g.level_begin, fresh.level_begin);
+      keep(g.coefs, fresh.coefs);
+      keep(g.pcm, fresh.pcm);
+      keep(g.bs_v, fresh.bs_v);
+      keep(g.bs_h, fresh.bs_h);
+      keep(g.qp, fresh.qp);
+      keep(g.pcm_map, fresh.pcm_map);
+      keep(g.intra_map, fresh.intra_map);
+      keep(g.avail, fresh.avail);
+      keep(g.ctb_slice, fresh.ctb_slice);
+      keep(g.slices, fresh.slices);
+      keep(g.sao_params, fresh.sao_params);
+      g = std::move(fresh);
+    });
     cur_gpu_->target = cur_->slot;
     pc_->init_gpu(cur_gpu_.get());
   }

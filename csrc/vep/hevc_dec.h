@@ -23,6 +23,7 @@
 #include <map>
 #include <memory>
 
+#include "recycle.h"
 #include "avc.h"
 #include "codec.h"
 #include "hevc.h"
@@ -136,6 +137,8 @@ class Decoder {
   bool gpu_mode_ = false;
   int gpu_slots_ = 0, last_out_slot_ = -1;
   std::shared_ptr<struct GpuPicture> cur_gpu_;
+  // records-mode pictures recycled per decoder (recycle.h: resident buffers, no page faults)
+  std::shared_ptr<Recycler<struct GpuPicture>> gpu_pool_;
   std::vector<std::shared_ptr<struct GpuPicture>> gpu_out_;
 };
 
