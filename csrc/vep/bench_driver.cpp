@@ -43,7 +43,8 @@ ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cach
   }
   cam_tick_.assign(size_t(ncams), 0);
   cam_busy_.assign(size_t(ncams), 0);
-  for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this] { parse_loop(); });
+  cam_thread_.assign(size_t(ncams), -1);
+  for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this, i] { parse_loop(i); });
 }
 
 ReplayBench::~ReplayBench() {
@@ -55,29 +56,39 @@ ReplayBench::~ReplayBench() {
   for (auto& t : workers_) t.join();
 }
 
-int ReplayBench::pick_locked() const {
-  // oldest tick first; within a tick the largest AU first (a keyframe starts at once)
-  int best = -1;
+int ReplayBench::pick_locked(int me) const {
+  // A camera's decoder state (neighbour state, record pools: a few MB per 1080p camera) stays
+  // in the caches of the core that parsed its last picture; taking it on another core costs a
+  // cross-core transfer of every line it touches. So: a camera at the oldest tick (the one the
+  // launcher waits for) first, preferring this thread's own; then this thread's cameras; then
+  // any other, oldest tick first; within equal rank the largest AU first (a keyframe starts at
+  // once).
+  int best = -1, best_rank = 0;
   for (int c = 0; c < int(cams_.size()); ++c) {
-    if (cam_busy_[size_t(c)] || cam_tick_[size_t(c)] >= consume_ + window_ ||
-        cam_tick_[size_t(c)] >= gate_)
-      continue;
-    if (best < 0 || cam_tick_[size_t(c)] < cam_tick_[size_t(best)] ||
-        (cam_tick_[size_t(c)] == cam_tick_[size_t(best)] &&
-         aus_[size_t(c)][pos_[size_t(c)]]->bytes() > aus_[size_t(best)][pos_[size_t(best)]]->bytes()))
+    const size_t k = size_t(c);
+    if (cam_busy_[k] || cam_tick_[k] >= consume_ + window_ || cam_tick_[k] >= gate_) continue;
+    const bool mine = cam_thread_[k] == me || cam_thread_[k] < 0;
+    const int rank = (cam_tick_[k] == consume_ ? 0 : 2) + (mine ? 0 : 1);
+    if (best < 0 || rank < best_rank ||
+        (rank == best_rank && (cam_tick_[k] < cam_tick_[size_t(best)] ||
+                               (cam_tick_[k] == cam_tick_[size_t(best)] &&
+                                aus_[k][pos_[k]]->bytes() > aus_[size_t(best)][pos_[size_t(best)]]->bytes())))) {
       best = c;
+      best_rank = rank;
+    }
   }
   return best;
 }
 
-void ReplayBench::parse_loop() {
+void ReplayBench::parse_loop(int me) {
   std::unique_lock<std::mutex> g(mu_);
   for (;;) {
     int c = -1;
-    work_cv_.wait(g, [&] { return stop_ || (c = pick_locked()) >= 0; });
+    work_cv_.wait(g, [&] { return stop_ || (c = pick_locked(me)) >= 0; });
     if (stop_) return;
     const i64 t = cam_tick_[size_t(c)];
     cam_busy_[size_t(c)] = 1;
+    cam_thread_[size_t(c)] = me;
     auto& v = aus_[size_t(c)];
     const AuPtr au = v[pos_[size_t(c)]];
     pos_[size_t(c)] = (pos_[size_t(c)] + 1) % v.size();

@@ -52,8 +52,8 @@ class ReplayBench {
     std::vector<char> ok;
     int done = 0;
   };
-  void parse_loop();
-  int pick_locked() const;  // a camera allowed to parse its next tick, or -1
+  void parse_loop(int me);
+  int pick_locked(int me) const;  // a camera allowed to parse its next tick, or -1
   std::vector<DecodeJob> take(bool timed);
   Worker& w_;
   std::vector<int> cams_;
@@ -65,6 +65,7 @@ class ReplayBench {
   i64 gate_ = INT64_MAX;        // parse threads start only ticks < gate_ (quiesce)
   std::vector<i64> cam_tick_;   // next tick each camera parses
   std::vector<char> cam_busy_;
+  std::vector<int> cam_thread_;  // parse thread that last parsed each camera (cache affinity)
   bool stop_ = false;
   std::mutex mu_;
   std::condition_variable work_cv_, ready_cv_;

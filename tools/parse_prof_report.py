@@ -62,8 +62,11 @@ def main():
         objs = collections.Counter()
         for obj, items in by_obj.items():
             objs[os.path.basename(obj)] += sum(c for c, _, _ in items)
-            if "_vep" in os.path.basename(obj) and os.path.exists(obj):
-                for (c, _, _), frames in zip(items, symbolize(obj, [o for _, o, _ in items])):
+            local = obj if os.path.exists(obj) else os.path.join(
+                os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "video_edge_ai_proxy_amd",
+                os.path.basename(obj))  # a profile taken on the GPU box: the same .so in this tree
+            if "_vep" in os.path.basename(obj) and os.path.exists(local):
+                for (c, _, _), frames in zip(items, symbolize(local, [o for _, o, _ in items])):
                     samples.append((c, frames))
             else:
                 for c, off, sym in items:
