@@ -55,7 +55,7 @@ void TaskQueue::run() {
 // ------------------------------------------------------------------------------ StrandPool
 
 StrandPool::StrandPool(int threads) {
-  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this] { run(); });
+  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this, i] { run(i); });
 }
 
 StrandPool::~StrandPool() {
@@ -94,13 +94,23 @@ void StrandPool::drain(u64 key) {
   });
 }
 
-void StrandPool::run() {
+void StrandPool::run(int me) {
+  constexpr size_t kAffinityScan = 8;  // ready keys considered beyond the oldest
   std::unique_lock<std::mutex> g(mu_);
   for (;;) {
     cv_.wait(g, [this] { return stop_ || !ready_.empty(); });
     if (stop_) return;
-    const u64 key = ready_.front();
-    ready_.pop_front();
+    size_t pick = 0;
+    for (size_t i = 0; i < ready_.size() && i < kAffinityScan; ++i) {
+      auto o = owner_.find(ready_[i]);
+      if (o != owner_.end() && o->second == me) {
+        pick = i;
+        break;
+      }
+    }
+    const u64 key = ready_[pick];
+    ready_.erase(ready_.begin() + std::ptrdiff_t(pick));
+    owner_[key] = me;
     Strand& s = strands_[key];
     if (s.q.empty()) continue;
     s.running = true;

@@ -39,7 +39,8 @@ class TaskQueue {
 };
 
 // Per-key serial execution on a shared pool: tasks of one key run in posting order, never two at
-// once; different keys run in parallel.
+// once; different keys run in parallel. A free thread prefers a ready key it ran last (the
+// camera's decoder state is still in that core's caches) among the oldest few ready keys.
 class StrandPool {
  public:
   explicit StrandPool(int threads);
@@ -56,11 +57,12 @@ class StrandPool {
     std::deque<std::function<void()>> q;
     bool running = false;  // a thread owns the strand (running its front task)
   };
-  void run();
+  void run(int me);
   std::vector<std::thread> th_;
   mutable std::mutex mu_;
   std::condition_variable cv_, idle_cv_;
   std::map<u64, Strand> strands_;
+  std::map<u64, int> owner_;  // thread that last ran each key
   std::deque<u64> ready_;  // keys with queued tasks and no owner
   bool stop_ = false;
 };
