@@ -1110,7 +1110,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       pic->poc = compute_poc(sh, sps);
       pic->wmbs = W;
       pic->hmbs = H;
-      pic->mbs.assign(size_t(W) * H, MbRec{});
+      // every record is written by store_mb or by the concealment pass below: a recycled
+      // picture of the same size needs no clearing
+      if (pic->mbs.size() != size_t(W) * H) pic->mbs.assign(size_t(W) * H, MbRec{});
       pic->coefs.reserve(size_t(W) * H * 32);
       pic->mvs.reserve(size_t(W) * H * 16);
       pic->dpb_slots = dpb_slots_;
@@ -1274,7 +1276,8 @@ void validate(const Picture& p) {
 std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, int hmbs,
                                             const std::vector<std::array<std::vector<u32>, 2>>& slice_uids,
                                             bool corners, Recycler<ColMotion>* pool) {
-  auto col = pool ? pool->acquire([](ColMotion& c) { c.b.clear(); }) : std::make_shared<ColMotion>();
+  // (a recycled buffer keeps its entries: the loop below writes every one of them)
+  auto col = pool ? pool->acquire([](ColMotion&) {}) : std::make_shared<ColMotion>();
   col->wmbs = wmbs;
   col->hmbs = hmbs;
   col->corners = corners;
