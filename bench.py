@@ -240,6 +240,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         if use_gpu:
             torch.cuda.synchronize()
 
+    # the live ingest's parse strands get the rank's parse-thread budget (as the replay pool does)
+    os.environ.setdefault("VEP_INGEST_PARSE_THREADS", str(a.threads))
     farm = RtspFarm(vep, worker, a, rank, compressed)
     try:
         farm.wait_pictures(cams * max(1, a.warmup), timeout_s=300.0)

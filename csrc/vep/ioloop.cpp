@@ -2,9 +2,12 @@
 #include "ioloop.h"
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/epoll.h>
 #include <sys/eventfd.h>
 #include <unistd.h>
@@ -95,7 +98,11 @@ void StrandPool::drain(u64 key) {
 }
 
 void StrandPool::run(int me) {
-  constexpr size_t kAffinityScan = 8;  // ready keys considered beyond the oldest
+  // ready keys considered for affinity (VEP_STRAND_AFFINITY=0: plain FIFO)
+  static const size_t kAffinityScan = [] {
+    const char* e = std::getenv("VEP_STRAND_AFFINITY");
+    return e && e[0] == '0' ? size_t(0) : size_t(8);
+  }();
   std::unique_lock<std::mutex> g(mu_);
   for (;;) {
     cv_.wait(g, [this] { return stop_ || !ready_.empty(); });
@@ -336,12 +343,31 @@ static int env_int(const char* name, int dflt) {
 IngestServices::IngestServices(int io_threads, int parse_threads, int connect_threads)
     : io(io_threads), parse(parse_threads), connect(connect_threads), timers(connect) {}
 
+// Host CPUs this process may use: its affinity mask, bounded by a cgroup v2 CPU quota.
+static int cpu_budget() {
+  int n = 1;
+  cpu_set_t set;
+  CPU_ZERO(&set);
+  if (sched_getaffinity(0, sizeof set, &set) == 0) n = std::max(1, CPU_COUNT(&set));
+  if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long period = 0;
+    if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0)
+      n = std::min(n, int(std::max(1L, (std::atol(quota) + period - 1) / period)));
+    std::fclose(f);
+  }
+  return n;
+}
+
 std::shared_ptr<IngestServices> IngestServices::acquire() {
   static std::mutex mu;
   static std::weak_ptr<IngestServices> cur;
   std::lock_guard<std::mutex> g(mu);
   if (auto s = cur.lock()) return s;
-  auto s = std::make_shared<IngestServices>(env_int("VEP_IO_THREADS", 2), env_int("VEP_INGEST_PARSE_THREADS", 4),
+  // parse strands: the process's CPU budget minus the socket loops and the GPU launcher
+  const int parse_default = std::max(2, std::min(32, cpu_budget() - 2));
+  auto s = std::make_shared<IngestServices>(env_int("VEP_IO_THREADS", 2),
+                                            env_int("VEP_INGEST_PARSE_THREADS", parse_default),
                                             env_int("VEP_CONNECT_THREADS", 4));
   cur = s;
   return s;
