@@ -869,6 +869,7 @@ class CtuLayer {
     const int nn = n * n;
     if (kWrite) std::fill(lv, lv + nn, 0);  // (read mode: residual_coding clears what it reads)
     bool tskip = false;
+    int nnz = 0;  // read mode: non-zero levels, raster positions in nzbuf_
     const TuKey key{c, x0, y0};
     if (dry_) {
       if constexpr (kWrite) {
@@ -891,12 +892,17 @@ class CtuLayer {
         std::copy(t.lv.begin(), t.lv.end(), lv);
         tskip = t.tskip;
       }
-      residual_coding(c, log2, lv, tskip);
+      if constexpr (kWrite) residual_coding(c, log2, lv, tskip);
+      else nnz = residual_coding_rd(c, log2, lv, tskip, nzbuf_);
       if (tskip) ++pc_.stats.tskip;
     }
     bool nz = false;
-    if (coded || dry_)
-      for (int k = 0; k < nn; ++k) nz |= lv[k] != 0;
+    if constexpr (kWrite) {
+      if (coded || dry_)
+        for (int k = 0; k < nn; ++k) nz |= lv[k] != 0;
+    } else {
+      nz = nnz > 0;
+    }
     if (GpuPicture* g = pc_.gpu) {  // records mode: the GPU predicts / transforms / adds
       if (nz) cbf_nonzero_ = true;
       if (!nz && !cu_.intra) return;
@@ -925,12 +931,16 @@ class CtuLayer {
         const size_t off = g->coefs.size();
         g->coefs.resize(off + size_t(nn));
         i16* dq = g->coefs.data() + off;
-        for (int k = 0; k < nn; ++k) {
-          const int v = lv[k];
-          if (!v) continue;
-          dq[k] = i16(dequant_level(v, qp, log2));
+        auto put = [&](int k) {
+          dq[k] = i16(dequant_level(lv[k], qp, log2));
           ex = std::max(ex, k & (n - 1));
-          ey = k >> log2;
+          ey = std::max(ey, k >> log2);
+        };
+        if constexpr (kWrite) {
+          for (int k = 0; k < nn; ++k)
+            if (lv[k]) put(k);
+        } else {
+          for (int j = 0; j < nnz; ++j) put(nzbuf_[j]);
         }
         t.ext_x = u8(ex);
         t.ext_y = u8(ey);
@@ -1147,6 +1157,161 @@ class CtuLayer {
     }
   }
 
+  // Decoder direction of residual_coding (the parse hot spot of coded pictures): the same bins
+  // and context selection as the generic body above, with the arithmetic decoder held in a local
+  // copy (registers across the context updates, see cabac.h), the significance context of a
+  // position from per-sub-block tables, and the non-zero levels listed (raster positions in
+  // `nzp`) so the caller never scans the whole block. Returns the number of non-zero levels.
+  int residual_coding_rd(int c, int log2, int* lv, bool& tskip, u16* nzp) {
+    // sigCtx patterns by coded_sub_block_flag of the right / lower sub-blocks (prev_csbf) at
+    // position p = x | y << 2 inside a sub-block, and the 4x4-TU map (§9.3.4.2.5)
+    static constexpr u8 kPat[4][16] = {{2, 1, 1, 0, 1, 1, 0, 0, 1, 0, 0, 0, 0, 0, 0, 0},
+                                       {2, 2, 2, 2, 1, 1, 1, 1, 0, 0, 0, 0, 0, 0, 0, 0},
+                                       {2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0, 2, 1, 0, 0},
+                                       {2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2, 2}};
+    static constexpr u8 kMap4[16] = {0, 1, 4, 5, 2, 3, 4, 5, 6, 6, 8, 8, 7, 7, 8, 8};
+    cabac::Ctx* const ctx = e_.c;
+    cabac::Decoder d = e_.d;
+    auto bits = [&d](int nb) {  // fixed length, bypass, MSB first
+      u32 r = 0;
+      for (int i = nb - 1; i >= 0; --i) r |= d.bypass() << i;
+      return int(r);
+    };
+    const int n = 1 << log2;
+    tskip = false;
+    if (pps_.transform_skip && log2 == 2) tskip = d.decision(ctx[kCtxTransformSkip + (c ? 1 : 0)]) != 0;
+    const int scan = scan_idx(c, log2);
+    const int nsb = log2 - 2;
+    const int off = c ? 15 : 3 * (log2 - 2) + ((log2 - 1) >> 2), shift = c ? log2 - 2 : (log2 + 1) >> 2;
+    const int cmax = (log2 << 1) - 1;
+    int pre[2], pos[2];
+    for (int a = 0; a < 2; ++a) {  // both prefixes, then both suffixes
+      cabac::Ctx* const base = ctx + (a == 0 ? kCtxLastX : kCtxLastY) + off;
+      int v = 0;
+      while (v < cmax && d.decision(base[v >> shift])) ++v;
+      pre[a] = pos[a] = v;
+    }
+    for (int a = 0; a < 2; ++a)
+      if (pre[a] > 3) {
+        const int nb = (pre[a] >> 1) - 1;
+        pos[a] = (1 << nb) * (2 + (pre[a] & 1)) + bits(nb);
+      }
+    if (scan == 2) std::swap(pos[0], pos[1]);
+    const int lx = pos[0], ly = pos[1];
+    VEP_CHECK(lx < n && ly < n, "last significant coefficient outside the block");
+    int last_sb = 0, last_pos = 0;
+    {
+      bool ok = false;
+      for (int i = (1 << (2 * nsb)) - 1; i >= 0 && !ok; --i) {
+        int xs, ys;
+        scan_pos(scan, nsb, i, xs, ys);
+        if (xs != (lx >> 2) || ys != (ly >> 2)) continue;
+        const int want = (lx & 3) | ((ly & 3) << 2);
+        for (int k = 15; k >= 0; --k)
+          if (kScan4.s[scan][k] == want) {
+            last_sb = i, last_pos = k, ok = true;
+            break;
+          }
+      }
+    }
+    std::fill(lv, lv + n * n, 0);
+    const u8* const sc4 = kScan4.s[scan];
+    const int cofs = c ? 27 : 0;
+    u8 csbf[8][8] = {};
+    int greater1_ctx = 1;  // c1 carried between sub-blocks
+    bool first_sb = true;
+    int nnz = 0;
+    for (int i = last_sb; i >= 0; --i) {
+      int xs, ys;
+      scan_pos(scan, nsb, i, xs, ys);
+      const int right = xs + 1 < (1 << nsb) ? csbf[xs + 1][ys] : 0;
+      const int below = ys + 1 < (1 << nsb) ? csbf[xs][ys + 1] : 0;
+      bool infer_dc = false, sb_coded = true;
+      if (i < last_sb && i > 0) {
+        sb_coded = d.decision(ctx[kCtxCsbf + std::min(right + below, 1) + (c ? 2 : 0)]) != 0;
+        infer_dc = true;
+      }
+      csbf[xs][ys] = u8(sb_coded);
+      if (!sb_coded) continue;
+      // significance: ctxInc = sig_off + pattern[p] (the DC of a larger TU: cofs; 4x4 TU: map)
+      const u8* pat = log2 == 2 ? kMap4 : kPat[right | (below << 1)];
+      const int sig_off = log2 == 2 ? cofs
+                          : cofs + (c == 0 ? ((xs | ys) ? 3 : 0) + (log2 == 3 ? (scan == 0 ? 9 : 15) : 21)
+                                           : (log2 == 3 ? 9 : 12));
+      cabac::Ctx* const sigc = ctx + kCtxSig + sig_off;
+      const bool dc_sb = log2 > 2 && i == 0;
+      u32 sig = i == last_sb ? 1u << last_pos : 0u;
+      for (int k = i == last_sb ? last_pos - 1 : 15; k >= 0; --k) {
+        if (k > 0 || !infer_dc) {
+          const int p = sc4[k];
+          cabac::Ctx& cx = (dc_sb && p == 0) ? ctx[kCtxSig + cofs] : sigc[pat[p]];
+          if (d.decision(cx)) {
+            sig |= 1u << k;
+            infer_dc = false;
+          }
+        } else {
+          sig |= 1u;  // DC of a coded sub-block with no other significant coefficient
+        }
+      }
+      // levels: greater1 (first 8), greater2 (first greater1), signs, remaining
+      int ctx_set = (i == 0 || c > 0) ? 0 : 2;
+      if (!first_sb && greater1_ctx == 0) ++ctx_set;
+      first_sb = false;
+      greater1_ctx = 1;
+      if (!sig) continue;  // (the DC sub-block of a larger TU may have no significant level)
+      cabac::Ctx* const g1c = ctx + kCtxGt1 + ctx_set * 4 + (c ? 16 : 0);
+      u32 gt1 = 0;
+      int ngt1 = 0, last_gt1 = -1;
+      const int last_sig = 31 - __builtin_clz(sig), first_sig = __builtin_ctz(sig);
+      for (u32 w = sig; w && ngt1 < 8; ++ngt1) {
+        const int k = 31 - __builtin_clz(w);
+        w &= ~(1u << k);
+        if (d.decision(g1c[greater1_ctx])) {
+          gt1 |= 1u << k;
+          greater1_ctx = 0;
+          if (last_gt1 < 0) last_gt1 = k;
+        } else if (greater1_ctx > 0 && greater1_ctx < 3) {
+          ++greater1_ctx;
+        }
+      }
+      const bool hidden = pps_.sign_data_hiding && last_sig - first_sig > 3;
+      const bool gt2 = last_gt1 >= 0 && d.decision(ctx[kCtxGt2 + ctx_set + (c ? 4 : 0)]);
+      u32 neg = 0;
+      for (u32 w = sig; w;) {
+        const int k = 31 - __builtin_clz(w);
+        w &= ~(1u << k);
+        if ((!hidden || k != first_sig) && d.bypass()) neg |= 1u << k;
+      }
+      int nsig = 0, sum = 0, rice = 0;
+      for (u32 w = sig; w; ++nsig) {
+        const int k = 31 - __builtin_clz(w);
+        w &= ~(1u << k);
+        const int base = 1 + int((gt1 >> k) & 1) + (gt2 && k == last_gt1 ? 1 : 0);
+        int absv = base;
+        if (base == ((nsig < 8) ? ((k == last_gt1) ? 3 : 2) : 1)) {  // coeff_abs_level_remaining
+          int prefix = 0;
+          while (d.bypass()) {
+            ++prefix;
+            VEP_CHECK(prefix < 32, "coeff_abs_level_remaining prefix too long");
+          }
+          const int rem = prefix < 3 ? (prefix << rice) + bits(rice)
+                                     : (((1 << (prefix - 3)) + 2) << rice) + bits(prefix - 3 + rice);
+          absv = base + rem;
+          if (absv > 3 * (1 << rice)) rice = std::min(rice + 1, 4);
+        }
+        int v = (neg >> k) & 1 ? -absv : absv;
+        sum += absv;
+        if (hidden && k == first_sig && (sum & 1)) v = -v;
+        const int p = sc4[k];
+        const int r = ((ys << 2) + (p >> 2)) * n + (xs << 2) + (p & 3);
+        lv[r] = v;
+        nzp[nnz++] = u16(r);
+      }
+    }
+    e_.d = d;
+    return nnz;
+  }
+
   int coeff_remaining(int rice, int v) {  // §9.3.3.11 (prefix threshold 3, suffix EG(rice + 1))
     int prefix = 0;
     if constexpr (kWrite) {
@@ -1221,6 +1386,7 @@ class CtuLayer {
   bool dry_ = false;
   int dry_qp_delta_ = 0;
   bool dry_tskip_ = false;
+  u16 nzbuf_[1024];  // read mode: raster positions of a block's non-zero levels
   bool cbf_nonzero_ = false;
   int block_luma_mode_ = 1;
   u64 gpu_avail_ = 0;
