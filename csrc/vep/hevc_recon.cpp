@@ -644,18 +644,18 @@ std::shared_ptr<std::vector<ColMv>> build_col(const PicCtx& pc, int& col_w) {
 }
 
 // ------------------------------------------------------------------------------ deblocking
-static int bs_of(const PicCtx& pc, int xp, int yp, int xq, int yq, bool tu_edge) {
+static int bs_of(const PicCtx& pc, int xp, int yp, int xq, int yq, bool tu_edge, bool one_slice) {
   const size_t p = pc.i4(xp, yp), q = pc.i4(xq, yq);
   if (pc.intra[p] || pc.intra[q]) return 2;
   if (tu_edge && (pc.cbf[p] || pc.cbf[q])) return 1;
   const MvField& a = pc.mf[p];
   const MvField& b = pc.mf[q];
   // the same motion in one slice (same lists): same pictures and vectors
-  if (std::memcmp(&a, &b, sizeof(MvField)) == 0 &&
-      pc.slice[size_t(pc.ctb_of(xp, yp))] == pc.slice[size_t(pc.ctb_of(xq, yq))])
-    return 0;
-  const SliceInfo& sa = pc.slices[pc.slice[size_t(pc.ctb_of(xp, yp))]];
-  const SliceInfo& sb = pc.slices[pc.slice[size_t(pc.ctb_of(xq, yq))]];
+  const int slp = one_slice ? 0 : pc.slice[size_t(pc.ctb_of(xp, yp))];
+  const int slq = one_slice ? 0 : pc.slice[size_t(pc.ctb_of(xq, yq))];
+  if (std::memcmp(&a, &b, sizeof(MvField)) == 0 && slp == slq) return 0;
+  const SliceInfo& sa = pc.slices[size_t(slp)];
+  const SliceInfo& sb = pc.slices[size_t(slq)];
   const HevcFrame* ra[2] = {nullptr, nullptr};
   const HevcFrame* rb[2] = {nullptr, nullptr};
   int na = 0, nb = 0;
@@ -691,23 +691,30 @@ void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& 
   const int W = pc.W, H = pc.H;
   bsv.assign(size_t(pc.w4) * pc.h4, 0);
   bsh.assign(size_t(pc.w4) * pc.h4, 0);
+  // single-slice pictures (the common case) skip every per-edge slice lookup
+  const bool one = pc.slices.size() == 1;
+  if (one && pc.slices[0].sh.deblocking_disabled) return;
   // edges lie on the 8x8 grid: vertical ones in every 8th column, horizontal ones in every 8th row
   for (int dir = 0; dir < 2; ++dir) {
     const u8 tu_flag = dir == 0 ? kEdgeTuV : kEdgeTuH, pu_flag = dir == 0 ? kEdgePuV : kEdgePuH;
     std::vector<u8>& out = dir == 0 ? bsv : bsh;
-    for (int y = dir == 0 ? 0 : 8; y < H; y += dir == 0 ? 4 : 8)
+    for (int y = dir == 0 ? 0 : 8; y < H; y += dir == 0 ? 4 : 8) {
+      const size_t row = size_t(y >> 2) * size_t(pc.w4);
+      const u8* erow = pc.edge.data() + row;
       for (int x = dir == 0 ? 8 : 0; x < W; x += dir == 0 ? 8 : 4) {
-        const size_t k = pc.i4(x, y);
-        const u8 e = pc.edge[k];
+        const u8 e = erow[x >> 2];
         if (!(e & (tu_flag | pu_flag))) continue;
-        const int si = pc.slice[size_t(pc.ctb_of(x, y))];
-        const SliceHeader& sh = pc.slices[size_t(si)].sh;
-        if (sh.deblocking_disabled) continue;
         const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
-        const int sp = pc.slice[size_t(pc.ctb_of(xp, yp))];
-        if (sp != si && !sh.loop_filter_across_slices) continue;
-        out[k] = u8(bs_of(pc, xp, yp, x, y, (e & tu_flag) != 0));
+        if (!one) {
+          const int si = pc.slice[size_t(pc.ctb_of(x, y))];
+          const SliceHeader& sh = pc.slices[size_t(si)].sh;
+          if (sh.deblocking_disabled) continue;
+          const int sp = pc.slice[size_t(pc.ctb_of(xp, yp))];
+          if (sp != si && !sh.loop_filter_across_slices) continue;
+        }
+        out[row + size_t(x >> 2)] = u8(bs_of(pc, xp, yp, x, y, (e & tu_flag) != 0, one));
       }
+    }
   }
 }
 
