@@ -74,7 +74,7 @@ def parse_args():
                          "1.0 baseline -> ~4.5 Mbit/s)")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
     ap.add_argument("--threads", type=int, default=0,
-                    help="host parse threads per rank (0 = CPU budget / local ranks - 2, at most 14)")
+                    help="host parse threads per rank (0 = CPU budget / local ranks - 1, at most 15)")
     ap.add_argument("--parse-window", type=int, default=8,
                     help="ticks a camera's parse may run ahead of the tick being launched")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")

@@ -100,11 +100,11 @@ def test_parse_threads_split_cpu_budget(monkeypatch):
     from video_edge_ai_proxy_amd import utils
 
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 16)
-    assert utils.parse_threads_per_rank(1) == 14      # single-GPU share: the measured optimum
+    assert utils.parse_threads_per_rank(1) == 15      # single-GPU share: the measured optimum
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 128)
-    assert utils.parse_threads_per_rank(8) == 14      # 16 CPUs per rank
+    assert utils.parse_threads_per_rank(8) == 15      # 16 CPUs per rank
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 64)
-    assert utils.parse_threads_per_rank(8) == 6       # 8 per rank, 2 left for launch/lanes
+    assert utils.parse_threads_per_rank(8) == 7       # 8 per rank, 1 left for launch/lanes
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 4)
     assert utils.parse_threads_per_rank(8) == 2       # floor
     assert utils.host_cpu_budget.__call__() >= 1

@@ -79,9 +79,10 @@ def host_cpu_budget() -> int:
     return max(1, n)
 
 
-def parse_threads_per_rank(local_world: int, cap: int = 14, reserve: int = 2) -> int:
-    """Host CAVLC parse threads for one rank: the node's CPU budget split over the ranks that
-    share it, minus ``reserve`` for the rank's launcher / lane / gRPC threads, capped at ``cap``
-    (14 on a 16-CPU single-GPU share: the measured optimum, profiles/r1_sweep_threads_v17.txt)."""
+def parse_threads_per_rank(local_world: int, cap: int = 15, reserve: int = 1) -> int:
+    """Host parse threads for one rank: the node's CPU budget split over the ranks that share
+    it, minus ``reserve`` for the rank's launcher / lane / gRPC threads, capped at ``cap``
+    (15 on a 16-CPU single-GPU share: the measured optimum with cache-affine parse pools,
+    profiles/r2/sweep_threads_s2.txt; 14 before them, profiles/r1_sweep_threads_v17.txt)."""
     share = host_cpu_budget() // max(1, local_world)
     return max(2, min(cap, share - reserve))
