@@ -162,3 +162,38 @@ def test_hub_consumer_batch_cpu(native, tmp_path):
     finally:
         hub.shutdown()
         srv.stop()
+
+
+def test_bench_keyframe_only_rtsp_cpu():
+    """BASELINE config 3 shape: every access unit crosses the live ingest, only IDR pictures are
+    decoded (keyframe-only cameras); the JSON reports both rates."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--source", "rtsp", "--keyframe-only",
+           "--steps", "2", "--warmup", "1", "--width", "96", "--height", "64", "--cams-per-gpu", "2",
+           "--gop", "6", "--letterbox", "32", "--latency-samples", "0", "--threads", "1"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["keyframe_only"] and d["source"] == "rtsp" and d["frames_dropped"] == 0
+    # only keyframes decode: about one picture per GOP of ingested access units
+    assert 0 < d["frames_decoded"] < d["access_units_ingested"]
+
+
+def test_hostprof_samples_native_threads(native, tmp_path):
+    """The extension's SIGPROF sampler records where host CPU time goes (parse hot spots)."""
+    import time
+
+    out = tmp_path / "prof.txt"
+    cfg = native.SynthConfig()
+    cfg.width, cfg.height, cfg.compressed = 320, 240, True
+    enc = native.SynthH264(cfg)
+    aus = [enc.next() for _ in range(10)]
+    native.hostprof_start(200)
+    t0 = time.time()
+    while time.time() - t0 < 1.0:
+        dec = native.CpuDecoder()
+        for au in aus:
+            dec.decode(au)
+    n = native.hostprof_stop(str(out))
+    rows = [l.split(maxsplit=3) for l in out.read_text().splitlines()]
+    assert n > 0 and sum(int(r[0]) for r in rows) == min(n, 1 << 21)
+    assert any("_vep" in r[1] for r in rows)  # samples inside the extension, with offsets
