@@ -40,22 +40,30 @@ inline constexpr u8 kNextLps[64] = {
     18, 18, 19, 19, 21, 21, 22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30,
     31, 32, 32, 33, 33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63,
 };
-// Both transitions in one table for the branch-free decoder: kTrans[is_lps][pStateIdx].
+// A context is one u16: pStateIdx << 1 | valMps. (Not a pair of u8: u8 stores may alias any
+// object, so every context update would force the arithmetic decoder's range / offset / bit
+// cache back to memory when the decoder is reached through a pointer.)
+// Both transitions of the packed value in one table for the branch-free decoder:
+// kTrans[is_lps][s] = the next packed value (an LPS in state 0 flips valMps).
 struct StateTrans {
-  u8 t[2][64];
+  u16 t[2][128];
   constexpr StateTrans() : t{} {
-    for (int s = 0; s < 64; ++s) {
-      t[0][s] = u8(s < 62 ? s + 1 : s);
-      t[1][s] = kNextLps[s];
-    }
+    for (int st = 0; st < 64; ++st)
+      for (int m = 0; m < 2; ++m) {
+        const int s = st << 1 | m;
+        t[0][s] = u16((st < 62 ? st + 1 : st) << 1 | m);
+        t[1][s] = u16(kNextLps[st] << 1 | (st == 0 ? m ^ 1 : m));
+      }
   }
 };
 inline constexpr StateTrans kTrans{};
 
 struct Ctx {
-  u8 state = 0;  // pStateIdx
-  u8 mps = 0;    // valMps
+  u16 s = 0;  // pStateIdx << 1 | valMps
 
+  int state() const { return s >> 1; }
+  int mps() const { return s & 1; }
+  void set(int state, int mps) { s = u16(state << 1 | mps); }
   // §9.3.2.2: initValue -> (pStateIdx, valMps) for SliceQpY.
   void init(int init_value, int qp) {
     const int slope = init_value >> 4, offset = init_value & 15;
@@ -63,8 +71,8 @@ struct Ctx {
     const int q = qp < 0 ? 0 : (qp > 51 ? 51 : qp);
     int pre = ((m * q) >> 4) + n;
     pre = pre < 1 ? 1 : (pre > 126 ? 126 : pre);
-    mps = pre <= 63 ? 0 : 1;
-    state = u8(mps ? pre - 64 : 63 - pre);
+    const int mp = pre <= 63 ? 0 : 1;
+    set(mp ? pre - 64 : 63 - pre, mp);
   }
 };
 
@@ -75,11 +83,9 @@ struct Ctx {
 // window and a marker bit measured 13% slower on the parse benchmark: the extra shift sits on
 // the range -> offset dependency chain.)
 //
-// Hot loops (residual blocks) work on a local copy of the decoder (`Decoder d = engine; ...;
-// engine = d;`): Ctx is a pair of u8, and u8 stores may alias any object, so with the engine
-// reached through a pointer every context update would force range/offset/cache back to memory
-// and reload them on the next bin. A local copy whose address never escapes (every member is
-// force-inlined) stays in registers.
+// Hot loops (residual blocks) also work on a local copy of the decoder (`Decoder d = engine;
+// ...; engine = d;`): a copy whose address never escapes (every member is force-inlined) stays
+// in registers for the whole block.
 #define VEP_CABAC_INLINE inline __attribute__((always_inline))
 class Decoder {
  public:
@@ -94,17 +100,15 @@ class Decoder {
     offset_ = bits(9);
   }
   VEP_CABAC_INLINE u32 decision(Ctx& c) {
-    const u32 st = c.state;
-    const u32 lps = kRangeLps[st][(range_ >> 6) & 3];
+    const u32 s = c.s;
+    const u32 lps = kRangeLps[s >> 1][(range_ >> 6) & 3];
     const u32 rmps = range_ - lps;
     const u32 is_lps = offset_ >= rmps ? 1u : 0u;
     offset_ -= rmps & (0u - is_lps);
     range_ = is_lps ? lps : rmps;
-    const u32 bin = c.mps ^ is_lps;
-    c.mps = u8(c.mps ^ (is_lps & (st == 0 ? 1u : 0u)));
-    c.state = kTrans.t[is_lps][st];
+    c.s = kTrans.t[is_lps][s];
     renorm();
-    return bin;
+    return (s & 1u) ^ is_lps;
   }
   // §9.3.3.2.2.3. After a 1 (pcm_flag / end_of_slice_flag) the bit position is exactly the end
   // of the encoder's flush (the flush's final 1 bit included).
@@ -185,16 +189,14 @@ class Encoder {
     outstanding_ = 0;
   }
   void decision(Ctx& c, u32 bin) {
-    const u32 lps = kRangeLps[c.state][(range_ >> 6) & 3];
+    const u32 lps = kRangeLps[c.s >> 1][(range_ >> 6) & 3];
     range_ -= lps;
-    if (bin != c.mps) {
+    const u32 is_lps = bin != u32(c.s & 1) ? 1u : 0u;
+    if (is_lps) {
       low_ += range_;
       range_ = lps;
-      if (c.state == 0) c.mps ^= 1;
-      c.state = kNextLps[c.state];
-    } else if (c.state < 62) {
-      ++c.state;
     }
+    c.s = kTrans.t[is_lps][c.s];
     renorm();
   }
   void terminate(u32 bin) {
