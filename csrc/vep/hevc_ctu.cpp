@@ -225,15 +225,21 @@ class CtuLayer {
     cu_.x0 = x0;
     cu_.y0 = y0;
     cu_.log2 = log2;
-    for4(x0, y0, n, n, [&](size_t k) {
-      pc_.depth[k] = u8(depth);
-      pc_.edge[k] = 0;
-      pc_.cbf[k] = 0;
-      pc_.pcm[k] = 0;
+    // (raw pointers held in locals: a u8 store through pc_.X[k] may alias the vectors' own data
+    // pointers, which would otherwise be reloaded after every store of these per-4x4 loops)
+    u8* const m_depth = pc_.depth.data();
+    u8* const m_edge = pc_.edge.data();
+    u8* const m_cbf = pc_.cbf.data();
+    u8* const m_pcm = pc_.pcm.data();
+    for4(x0, y0, n, n, [=](size_t k) {
+      m_depth[k] = u8(depth);
+      m_edge[k] = 0;
+      m_cbf[k] = 0;
+      m_pcm[k] = 0;
     });
     // CU boundaries are transform and prediction block edges
-    for4(x0, y0, 4, n, [&](size_t k) { pc_.edge[k] |= kEdgeTuV | kEdgePuV; });
-    for4(x0, y0, n, 4, [&](size_t k) { pc_.edge[k] |= kEdgeTuH | kEdgePuH; });
+    for4(x0, y0, 4, n, [=](size_t k) { m_edge[k] |= kEdgeTuV | kEdgePuV; });
+    for4(x0, y0, n, 4, [=](size_t k) { m_edge[k] |= kEdgeTuH | kEdgePuH; });
     bool skip = false;
     if (sh_.slice_type != kI) {
       int inc = 0;
@@ -241,12 +247,14 @@ class CtuLayer {
       if (pc_.avail(x0, y0, x0, y0 - 1, pc_.done) && pc_.skip[pc_.i4(x0, y0 - 1)]) ++inc;
       skip = bin(kCtxSkip + inc, want.skip);
     }
-    for4(x0, y0, n, n, [&](size_t k) { pc_.skip[k] = u8(skip); });
+    u8* const m_skip = pc_.skip.data();
+    for4(x0, y0, n, n, [=](size_t k) { m_skip[k] = u8(skip); });
     bool intra = false, pcm = false;
     int part = 0;
     if (skip) {
       cu_.intra = false;
-      for4(x0, y0, n, n, [&](size_t k) { pc_.intra[k] = 0; });
+      u8* const m_intra = pc_.intra.data();
+      for4(x0, y0, n, n, [=](size_t k) { m_intra[k] = 0; });
       prediction_unit(x0, y0, n, n, 0, 0, want.pu[0], true);
       ++pc_.stats.skip;
     } else {
@@ -269,7 +277,8 @@ class CtuLayer {
           ++pc_.stats.intra;
         }
       } else {
-        for4(x0, y0, n, n, [&](size_t k) { pc_.intra[k] = 0; });
+        u8* const m_intra = pc_.intra.data();
+        for4(x0, y0, n, n, [=](size_t k) { m_intra[k] = 0; });
         int r[4][4];
         const int np = pu_rects(part, n, r);
         for (int k = 0; k < np; ++k) prediction_unit(x0 + r[k][0], y0 + r[k][1], r[k][2], r[k][3], k, part, want.pu[k], false);
@@ -299,11 +308,14 @@ class CtuLayer {
       }
     }
     const int q = qp_y();
-    for4(x0, y0, n, n, [&](size_t k) {
-      pc_.qp[k] = i8(q);
-      pc_.done[k] = 1;
-      pc_.rec[k] = 1;
-      pc_.pcm[k] = u8(pcm);
+    i8* const m_qp = pc_.qp.data();
+    u8* const m_done = pc_.done.data();
+    u8* const m_rec = pc_.rec.data();
+    for4(x0, y0, n, n, [=](size_t k) {
+      m_qp[k] = i8(q);
+      m_done[k] = 1;
+      m_rec[k] = 1;
+      m_pcm[k] = u8(pcm);
     });
     qp_last_ = q;
   }
@@ -536,12 +548,17 @@ class CtuLayer {
       }
       if (dir == 3) ++pc_.stats.bi;
     }
-    for4(x, y, w, h, [&](size_t k) {
-      pc_.mf[k] = m;
-      pc_.done[k] = 1;
-    });
-    for4(x, y, 4, h, [&](size_t k) { pc_.edge[k] |= kEdgePuV; });
-    for4(x, y, w, 4, [&](size_t k) { pc_.edge[k] |= kEdgePuH; });
+    {
+      MvField* const m_mf = pc_.mf.data();
+      u8* const m_done = pc_.done.data();
+      u8* const m_edge = pc_.edge.data();
+      for4(x, y, w, h, [=](size_t k) {
+        m_mf[k] = m;
+        m_done[k] = 1;
+      });
+      for4(x, y, 4, h, [=](size_t k) { m_edge[k] |= kEdgePuV; });
+      for4(x, y, w, 4, [=](size_t k) { m_edge[k] |= kEdgePuH; });
+    }
     cu_.pus[cu_.npu][0] = x, cu_.pus[cu_.npu][1] = y, cu_.pus[cu_.npu][2] = w, cu_.pus[cu_.npu][3] = h;
     ++cu_.npu;
   }
@@ -710,8 +727,11 @@ class CtuLayer {
     const bool chroma_at_parent = !chroma_here && blk == 3;
     const int xc = chroma_here ? x0 : xb, yc = chroma_here ? y0 : yb, log2c = chroma_here ? log2 - 1 : 2;
     // TU edges (deblocking) and the luma cbf map
-    for4(x0, y0, 4, n, [&](size_t k) { pc_.edge[k] |= kEdgeTuV; });
-    for4(x0, y0, n, 4, [&](size_t k) { pc_.edge[k] |= kEdgeTuH; });
+    {
+      u8* const m_edge = pc_.edge.data();
+      for4(x0, y0, 4, n, [=](size_t k) { m_edge[k] |= kEdgeTuV; });
+      for4(x0, y0, n, 4, [=](size_t k) { m_edge[k] |= kEdgeTuH; });
+    }
     const bool chroma_coded = cb || cr;  // (4x4 luma blocks: the parent's chroma flags, all four)
     if (dry_) {
       // quantisation parameter as the real pass will see it: the CU's delta is coded at the
@@ -739,10 +759,16 @@ class CtuLayer {
     // luma
     if (cu_.intra) intra_pred_block(0, x0, y0, log2);
     residual_block(0, x0, y0, log2, cl, qp);
-    for4(x0, y0, n, n, [&](size_t k) {
-      pc_.cbf[k] = u8(cl && !dry_ ? cbf_nonzero_ : 0);
-      if (cu_.intra) pc_.rec[k] = 1;
-    });
+    {
+      u8* const m_cbf = pc_.cbf.data();
+      u8* const m_rec = pc_.rec.data();
+      const u8 cbfv = u8(cl && !dry_ ? cbf_nonzero_ : 0);
+      const bool intra = cu_.intra;
+      for4(x0, y0, n, n, [=](size_t k) {
+        m_cbf[k] = cbfv;
+        if (intra) m_rec[k] = 1;
+      });
+    }
     // chroma
     if (chroma_here || chroma_at_parent) {
       const int qpi_cb = std::clamp(qp + pps_.cb_qp_offset + sh_.cb_qp_offset, -0, 57);
