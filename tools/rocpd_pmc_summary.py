@@ -8,7 +8,7 @@ import sys
 
 
 def short(k):
-    m = re.search(r"(avc_\w+_kernel|decode_convert_kernel|letterbox\w*_kernel|nv12_\w+_kernel|__amd_rocclr_\w+)", k)
+    m = re.search(r"(avc_\w+_kernel|hevc_\w+_kernel|decode_convert_kernel|letterbox\w*_kernel|nv12_\w+_kernel|__amd_rocclr_\w+)", k)
     return m.group(1) if m else k[:40]
 
 
