@@ -2,27 +2,26 @@
 """Headline benchmark: decoded FPS (whole node) + p50 VideoLatestImage latency, 256x1080p RTSP.
 
 One rank per GPU (torch.distributed over RCCL when WORLD_SIZE > 1). Each rank owns
-``--cams-per-gpu`` synthetic 1080p30 H.264 cameras (camera data parallelism, weak scaling). One
-*step* is one frame tick: every camera on the rank decodes one access unit —
-  host:  CABAC/CAVLC macroblock-layer parse of the real H.264 AU (thread pool, pipelined one tick ahead)
-  GPU:   one batched gfx950 launch: I_PCM reconstruction into the NV12 reference surfaces +
-         BT.601 NV12->BGR24 into each camera's HBM ring slot, then a batched letterbox kernel
-         writing the 640x640 consumer batch
-  RCCL:  all-gather of the letterboxed uint8 consumer batch over xGMI (N > 1), overlapped with
-         the next tick's decode (double-buffered)
-``value`` = decoded frames per second summed over all ranks (time = max over ranks).
-p50 latency: after the timed loop rank 0 issues VideoLatestImage requests through the real gRPC
-server (in-process, loopback) and reports the client-observed request->frame-received median.
+``--cams-per-gpu`` synthetic 1080p30 H.264 cameras (camera data parallelism, weak scaling).
 
-Data (default ``--content avc --profile high``): real compressed synthetic H.264 camera streams
-of the kind IP cameras send — High profile, CABAC, I/P/B with B pyramids (2 B pictures per
-mini-GOP), 8x8 transform + Intra_8x8 and 4x4 / 16x16 intra, motion-compensated P/B macroblocks
-with residuals and the in-loop deblocking filter (a textured static scene, moving textured
-objects and per-frame sensor noise) — pre-encoded per camera and replayed. Host: CABAC
-macroblock-layer parse + dequantisation into per-MB records; GPU: motion compensation
-(bi-predictive), intra wavefront, deblocking wavefront, NV12->BGR24, letterbox. ``--profile
-baseline`` streams CAVLC I/P instead; ``--content pcm`` replays the I_PCM / P_Skip fast-path
-streams (raw samples in an H.264 wrapper; decode = a PCIe copy).
+Default ``--source rtsp`` (the stated metric): every rank serves its cameras from an in-process
+loopback RTSP camera farm (RTP over TCP-interleaved, FU-A), and the production ingest — RtspClient
++ RTP depacketizer on the epoll loops, the lazy decoder's CABAC/CAVLC host parse on the parse
+strands, the GPU worker's batched gfx950 reconstruction + NV12->BGR24 into each camera's HBM ring
++ letterbox into the consumer batch — decodes them. One *step* is ``cams-per-gpu`` decoded
+pictures; the farm is unthrottled during the timed region, so ``value`` is the node's decode
+capacity (decoded pictures / s summed over ranks, time = max over ranks). With N > 1 the
+letterboxed consumer batch is all-gathered over RCCL once per step, overlapped with decode.
+
+Latency (headline ``p50_latency_ms`` / ``p99_latency_ms``): after the timed loop the farm switches
+to real time (``--fps``), and ``--clients`` concurrent gRPC clients running in separate processes
+(started before this process touches the GPU) each issue back-to-back VideoLatestImage requests
+for their own live camera through the production gRPC server: request sent -> the camera's next
+BGR24 VideoFrame received and parsed. ``serve_p50_latency_ms`` is one request on a fresh
+connected channel (the newest frame already in the ring).
+
+``--source replay`` is the decode-only capacity (pre-encoded AUs fed straight to the parse pool,
+no network stack), labelled as such in the JSON.
 """
 from __future__ import annotations
 
@@ -93,7 +92,7 @@ def parse_args():
     ap.add_argument("--ring-slots", type=int, default=2)
     ap.add_argument("--latency-samples", type=int, default=100)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (plumbing check, no GPU)")
-    ap.add_argument("--source", choices=["replay", "rtsp"], default="replay",
+    ap.add_argument("--source", choices=["replay", "rtsp"], default="rtsp",
                     help="replay = pre-encoded AUs fed to the decode pipeline (decode-only); rtsp = an "
                          "in-process loopback RTSP camera farm, unthrottled, with the production "
                          "ingest (RtspClient + RTP depacketizer + lazy decoder) inside the timed loop")
@@ -102,7 +101,11 @@ def parse_args():
                          "mode (the reference's read_image.py --keyframe_only); needs --source rtsp so "
                          "every access unit still crosses ingest and only IDR pictures are decoded")
     ap.add_argument("--clients", type=int, default=32,
-                    help="concurrent gRPC clients for the latency run (one stream each)")
+                    help="concurrent gRPC clients for the latency run (one camera each)")
+    ap.add_argument("--client-procs", type=int, default=0,
+                    help="processes the latency clients run in (0 = half the rank's CPU budget)")
+    ap.add_argument("--latency-seconds", type=float, default=4.0,
+                    help="duration of the concurrent-client latency run")
     a = ap.parse_args()
     if a.keyframe_only and a.source != "rtsp":
         ap.error("--keyframe-only needs --source rtsp (the ingest filters the access units)")
@@ -113,13 +116,48 @@ def parse_args():
     return a
 
 
-def measure_latency(worker, cams, samples, tick, fps):
-    """Client-observed VideoLatestImage latency through the production gRPC path while the
-    cameras keep decoding at their frame rate (see server/bench_latency.py for definitions)."""
-    from video_edge_ai_proxy_amd.server.bench_latency import grpc_latency, summarize
+def start_client_pool(a):
+    """Latency clients in fresh processes, started before this process touches the GPU."""
+    from video_edge_ai_proxy_amd.server.latency_clients import ClientPool
+    from video_edge_ai_proxy_amd.utils import host_cpu_budget
 
-    serve_ms, next_ms = grpc_latency(worker, cams, samples, tick=tick, fps=fps)
-    return summarize(serve_ms), summarize(next_ms), len(serve_ms)
+    if a.clients <= 0 and a.latency_samples <= 0:
+        return None
+    n = max(1, a.clients)
+    procs = a.client_procs or max(1, min(n, host_cpu_budget() // 2))
+    return ClientPool(procs, (n + procs - 1) // procs)
+
+
+def latency_fields(a, lat, live_fps=None):
+    """The JSON latency block of bench_latency.measure() results."""
+    from video_edge_ai_proxy_amd.server.bench_latency import summarize
+
+    def r3(x):
+        return round(x, 3) if x is not None else None
+
+    nx, sv, srv = summarize(lat["next"]), summarize(lat["serve"]), summarize(lat["server_ms"])
+    out = {
+        "p50_latency_ms": r3(nx[0]),
+        "p99_latency_ms": r3(nx[1]),
+        "latency_definition": (f"{a.clients} concurrent gRPC clients in separate processes (one connected "
+                               "channel and one live camera each), back-to-back VideoLatestImage requests "
+                               f"while every camera streams at {a.fps} fps: request sent -> the camera's next "
+                               f"{a.width}x{a.height} BGR24 VideoFrame received and parsed (includes waiting for "
+                               f"it, up to one frame interval); {len(lat['next'])} samples over "
+                               f"{a.latency_seconds:g} s"),
+        "latency_frames_served_per_s": round(lat["frames_served"] / a.latency_seconds, 1),
+        "server_p50_ms": r3(srv[0]),
+        "server_p99_ms": r3(srv[1]),
+        "server_latency_definition": "server side: request received -> serialized frame handed to grpcio "
+                                     "(includes waiting for the next frame)",
+        "serve_p50_latency_ms": r3(sv[0]),
+        "serve_p99_latency_ms": r3(sv[1]),
+        "serve_latency_definition": "one request per fresh connected channel, no concurrent clients: the "
+                                    f"newest frame already in the HBM ring; {len(lat['serve'])} samples",
+    }
+    if live_fps is not None:
+        out["latency_live_fps_per_camera"] = round(live_fps, 2)
+    return out
 
 
 def spawn_ranks(n: int) -> int:
@@ -189,7 +227,10 @@ class RtspFarm:
         self._touch()
         self.sessions = []
         for i, cam in enumerate(self.idx):
-            sess = vep.IngestSession(worker, cam, f"r{rank}rtsp{i}", f"rtsp://127.0.0.1:{self.srv.port}/cam{i}")
+            # lossless: while a camera's parse backlog is deep its socket is paused (TCP
+            # back-pressure on the unthrottled farm) instead of dropping AUs to the next keyframe
+            sess = vep.IngestSession(worker, cam, f"r{rank}rtsp{i}", f"rtsp://127.0.0.1:{self.srv.port}/cam{i}",
+                                     lossless=True)
             sess.start()
             self.sessions.append(sess)
         self.stop_evt = threading.Event()
@@ -215,7 +256,21 @@ class RtspFarm:
     def stats(self):
         st = [self.worker.stats(c) for c in self.idx]
         return {"packets": sum(x["packets"] for x in st), "bytes_in": sum(x["bytes_in"] for x in st),
-                "errors": sum(x["errors"] for x in st), "decoded": sum(x["decoded"] for x in st)}
+                "errors": sum(x["errors"] for x in st), "decoded": sum(x["decoded"] for x in st),
+                "skipped": sum(x["skipped"] for x in st)}
+
+    def go_live(self, fps, timeout_s=20.0):
+        """Switch the farm to real time and wait until the ingest backlog of the unthrottled run has
+        drained (the decode rate has fallen to the cameras' frame rate)."""
+        self.srv.set_pacing(1)
+        deadline = time.perf_counter() + timeout_s
+        target = self.cams * fps * 1.25
+        while time.perf_counter() < deadline:
+            p0 = self.worker.pictures
+            time.sleep(0.5)
+            if (self.worker.pictures - p0) / 0.5 <= target:
+                return True
+        return False
 
     def close(self):
         self.stop_evt.set()
@@ -225,10 +280,10 @@ class RtspFarm:
         self.worker.stop()
 
 
-def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed):
+def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed, pool):
     """`--source rtsp`: the timed loop waits for the live pipeline (loopback RTSP farm ->
     IngestSession -> lazy decoder -> Worker batches) to decode `cams` more pictures per step."""
-    from video_edge_ai_proxy_amd.server.bench_latency import grpc_concurrent_latency, summarize
+    from video_edge_ai_proxy_amd.server.bench_latency import measure
 
     cams = a.cams_per_gpu
     buf = torch.empty((cams, row), dtype=torch.uint8, device=dev)
@@ -243,6 +298,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
     # the live ingest's parse strands get the rank's parse-thread budget (as the replay pool does)
     os.environ.setdefault("VEP_INGEST_PARSE_THREADS", str(a.threads))
     farm = RtspFarm(vep, worker, a, rank, compressed)
+    lat = None
+    live_fps = None
     try:
         farm.wait_pictures(cams * max(1, a.warmup), timeout_s=300.0)
         if world > 1:
@@ -271,22 +328,32 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         wire_bytes = s1["bytes_in"] - s0["bytes_in"]
         errors = s1["errors"] - s0["errors"]
         aus = s1["packets"] - s0["packets"]  # access units through Camera::on_access_unit
+        skipped = s1["skipped"] - s0["skipped"]  # AUs the ingest dropped (parse backlog full)
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes, aus], dtype=torch.float64, device=dev)
+            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes, aus, skipped], dtype=torch.float64,
+                              device=dev)
             dist.all_reduce(fr, op=dist.ReduceOp.SUM)
-            pictures, frames, dropped, errors, wire_bytes, aus = (int(v) for v in fr.tolist())
-        conc = (None, None)
-        nconc = 0
-        if rank == 0 and a.latency_samples > 0 and a.clients > 0:
-            xs = grpc_concurrent_latency(worker, farm.idx, a.clients, duration_s=3.0)
-            conc, nconc = summarize(xs), len(xs)
-        if world > 1:
-            dist.barrier()
+            pictures, frames, dropped, errors, wire_bytes, aus, skipped = (int(v) for v in fr.tolist())
+        # latency: every rank's cameras go live (real-time farm), rank 0 measures
+        if pool is not None or world > 1:
+            settled = farm.go_live(a.fps)
+            if world > 1:
+                dist.barrier()
+            if pool is not None:
+                lp0, lt0 = worker.pictures, time.perf_counter()
+                lat = measure(pool, worker, farm.idx, duration_s=a.latency_seconds,
+                              serve_samples=a.latency_samples)
+                live_fps = (worker.pictures - lp0) / (time.perf_counter() - lt0) / cams
+                lat["settled"] = settled
+            if world > 1:
+                dist.barrier()
     finally:
         farm.close()
+        if pool is not None:
+            pool.close()
     if rank == 0:
         fps = pictures / elapsed
         res = {
@@ -304,8 +371,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "dtype": "uint8 (BGR24 frames; bf16-capable consumer path)",
             "data": (f"synthetic {CODEC[a.codec]} camera streams ({describe_streams(a, compressed)}, QP {a.qp}, "
                      f"GOP {a.gop}) served by an in-process loopback RTSP farm (RTP/TCP interleaved, "
-                     f"FU-A), unthrottled; {wire_bytes * 8 / max(1, pictures) * a.fps / 1e6:.1f} Mbit/s per "
-                     f"camera at {a.fps} fps (wire bytes per decoded picture)"),
+                     f"FU-A), unthrottled in the timed region; {wire_bytes * 8 / max(1, aus) * a.fps / 1e6:.1f} "
+                     f"Mbit/s per camera at {a.fps} fps"),
             "source": "rtsp",
             "keyframe_only": a.keyframe_only,
             "config": {
@@ -317,6 +384,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                 "letterbox": a.letterbox,
                 "consumer_format": a.consumer_format,
                 "all_gather": gather,
+                "gathered_bytes_per_rank_per_step": cams * row if gather else 0,
             },
             "frame_count_definition": "pictures the live pipeline decoded (RTSP receive -> RTP "
                                       "depacketize -> host parse -> GPU reconstruct) during the timed "
@@ -327,19 +395,19 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "frames_published": frames,
             "access_units_ingested": aus,
             "access_units_per_s": round(aus / elapsed, 1),
+            "access_units_skipped": skipped,
             "frames_dropped": dropped,
             "decode_errors": errors,
             "concurrent_clients": a.clients,
-            "p50_latency_ms": round(conc[0], 3) if conc[0] is not None else None,
-            "p99_latency_ms": round(conc[1], 3) if conc[1] is not None else None,
-            "latency_definition": f"{a.clients} concurrent gRPC clients (one connected channel and camera "
-                                  "each) issuing back-to-back VideoLatestImage requests while every "
-                                  "camera decodes live: request sent -> the camera's next "
-                                  f"{a.width}x{a.height} BGR24 VideoFrame received and parsed; {nconc} samples",
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "parse_threads_per_rank": a.threads,
             "rocdecode_available": bool(vep.rocdecode_available()),
+            "decoder_backend": decoder_backend(a, compressed),
             "per_gpu_fps": round(fps / max(world, 1), 2),
         }
+        if lat is not None:
+            res.update(latency_fields(a, lat, live_fps))
+            res["latency_farm_settled"] = lat["settled"]
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -349,10 +417,39 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         sys.exit(3)
 
 
+def payload_path(a, compressed, worker, ip0, sg0):
+    """What reaches the GPU per picture, from the worker's own byte counters."""
+    inplace = (worker.bytes_inplace - ip0) // max(1, a.steps)
+    staged = (worker.bytes_staged - sg0) // max(1, a.steps)
+    if compressed:
+        return {"gpu_input": "per-macroblock reconstruction records (modes, motion vectors, dequantised "
+                             "coefficients) built by the host parse and copied H2D per batch; slice bytes "
+                             "never reach the GPU",
+                "slice_bytes_read_in_place_per_step": inplace, "slice_bytes_staged_per_step": staged}
+    return {"gpu_input": "I_PCM slice bytes: the decode kernel reads them from pinned host memory over PCIe"
+                         if worker.direct_reads else "I_PCM slice bytes gathered into HBM, decode reads HBM",
+            "slice_bytes_read_in_place_per_step": inplace, "slice_bytes_staged_per_step": staged}
+
+
+def decoder_backend(a, compressed):
+    if compressed and a.codec == "h265":
+        return ("native H.265 Main decoder: CPU CABAC coding-tree parse + merge/AMVP into reconstruction "
+                "records; gfx950 HIP motion compensation, level-scheduled intra + residual transform blocks, "
+                "deblocking, SAO, NV12->BGR24 (rocDecode absent in image)")
+    if compressed:
+        return ("native H.264 decoder: CPU " + ("CAVLC" if a.profile == "baseline" or a.cavlc else "CABAC") +
+                " macroblock-layer parse + dequant; gfx950 HIP motion compensation, intra + deblocking "
+                "wavefronts, NV12->BGR24 (rocDecode absent in image)")
+    return ("native subset decoder: CPU " + ENTROPY[a.codec] + " parse + gfx950 HIP PCM reconstruct/"
+            "NV12->BGR24 (rocDecode absent in image)")
+
+
 def main():
     a = parse_args()
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ and not a.cpu:
         sys.exit(spawn_ranks(a.gpus))
+    # rank 0's latency clients: fresh processes, started before this process touches the GPU
+    pool = start_client_pool(a) if int(os.environ.get("RANK", "0")) == 0 else None
     import torch
     import torch.distributed as dist
 
@@ -384,7 +481,7 @@ def main():
     cfg = make_cfg(vep, a, rank, compressed)
     stream_desc = describe_streams(a, compressed)
     if a.source == "rtsp":
-        return run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed)
+        return run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed, pool)
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
                          ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
 
@@ -471,24 +568,20 @@ def main():
         dist.all_reduce(fr, op=dist.ReduceOp.SUM)
         frames, dropped, launched = (int(v) for v in fr.tolist())
 
-    serve_lat = next_lat = conc_lat = (None, None)
-    nlat = nconc = 0
-    if rank == 0 and a.latency_samples > 0:
-        from video_edge_ai_proxy_amd.server.bench_latency import grpc_concurrent_latency, summarize
+    lat = None
+    if pool is not None:
+        from video_edge_ai_proxy_amd.server.bench_latency import measure, ticking
 
-        # the single-process tick must not touch the collective: decode-only ticks here
+        # cameras decode at their frame rate meanwhile; the single-process tick must not touch
+        # the collective: decode-only ticks here
         worker.set_consumer_buffers(bufs[0].data_ptr(), 0, cams)
-        serve_lat, next_lat, nlat = measure_latency(worker, list(rb.cameras), a.latency_samples,
-                                                    lambda: (rb.step(), rb.drain()), float(a.fps))
-        if a.clients > 0:
-            xs = grpc_concurrent_latency(worker, list(rb.cameras), a.clients, duration_s=3.0,
-                                         tick=lambda: (rb.step(), rb.drain()), fps=float(a.fps))
-            conc_lat, nconc = summarize(xs), len(xs)
+        with ticking(lambda: (rb.step(), rb.drain()), float(a.fps)):
+            time.sleep(0.5)
+            lat = measure(pool, worker, list(rb.cameras), duration_s=a.latency_seconds,
+                          serve_samples=a.latency_samples)
+        pool.close()
     if world > 1:
         dist.barrier()
-
-    def r3(x):
-        return round(x, 3) if x is not None else None
 
     bitrate_mbps = rb.stream_bytes * 8 / max(1, rb.stream_frames) * a.fps / 1e6
     if rank == 0:
@@ -523,35 +616,10 @@ def main():
                 "gathered_bytes_per_rank_per_step": cams * row if gather else 0,
                 "all_gather": gather,
             },
-            "p50_latency_ms": r3(serve_lat[0]),
-            "p99_latency_ms": r3(serve_lat[1]),
-            "latency_definition": "client-observed gRPC VideoLatestImage (loopback, connected "
-                                  f"channel): request sent -> {a.width}x{a.height} BGR24 VideoFrame received and "
-                                  "parsed; newest frame already in the HBM ring; cameras decoding "
-                                  f"at {a.fps} fps meanwhile; {nlat} samples",
-            "p50_next_frame_latency_ms": r3(next_lat[0]),
-            "concurrent_clients": a.clients,
-            "concurrent_p50_latency_ms": r3(conc_lat[0]),
-            "concurrent_p99_latency_ms": r3(conc_lat[1]),
-            "concurrent_latency_definition": f"{a.clients} concurrent gRPC clients (one connected channel and "
-                                             "camera each) issuing back-to-back VideoLatestImage requests "
-                                             f"while every camera decodes at {a.fps} fps: request sent -> "
-                                             "the camera's next frame received and parsed (includes waiting "
-                                             f"for it, up to one frame interval); {nconc} samples",
-            "next_frame_latency_definition": "back-to-back requests on one stream/channel (the "
-                                             "reference clients' pattern): includes waiting for "
-                                             "the camera's next decoded frame",
             "rocdecode_available": bool(vep.rocdecode_available()),
-            "decoder_backend": ("native H.265 Main decoder: CPU CABAC coding-tree parse + merge/AMVP into "
-                                "reconstruction records; gfx950 HIP motion compensation, level-scheduled intra + "
-                                "residual transform blocks, deblocking, SAO, NV12->BGR24 (rocDecode absent in "
-                                "image)" if compressed and a.codec == "h265" else
-                                "native H.264 decoder: CPU " + ("CAVLC" if a.profile == "baseline" or a.cavlc
-                                                               else "CABAC") + " macroblock-layer parse + dequant; "
-                                "gfx950 HIP motion compensation, intra + deblocking wavefronts, "
-                                "NV12->BGR24 (rocDecode absent in image)" if compressed else
-                                "native subset decoder: CPU " + ENTROPY[a.codec] + " parse + gfx950 "
-                                "HIP PCM reconstruct/NV12->BGR24 (rocDecode absent in image)"),
+            "decoder_backend": decoder_backend(a, compressed),
+            "source": "replay (decode-only: pre-encoded access units fed to the parse pool; no RTSP "
+                      "receive / depacketization in the timed region)",
             "per_gpu_fps": round(fps / max(world, 1), 2),
             "frames_published": frames,
             "frames_launched": launched,
@@ -567,12 +635,7 @@ def main():
             "parse_threads_per_rank": a.threads,
             "gpu_stages": worker.stages,
             "gpu_inflight_per_lane": worker.inflight,
-            "payload_path": ("decode kernel reads slice bytes from pinned host memory over PCIe"
-                             if getattr(worker, "direct_reads", False) else
-                             "gather kernel pulls slice bytes into HBM, decode reads HBM"),
-            "rank0_slice_bytes_per_step": {
-                "gpu_read_in_place_from_pinned": (worker.bytes_inplace - ip0) // a.steps,
-                "host_staged": (worker.bytes_staged - sg0) // a.steps},
+            "payload_path": payload_path(a, compressed, worker, ip0, sg0),
             "rank0_launch_breakdown_ms_per_step": {
                 k: round((v - tm0[k]) / a.steps, 4) for k, v in tm1.items()},
         }
@@ -582,6 +645,8 @@ def main():
                 n = max(1, pr[f"{ph}_mbs"])
                 res[f"{ph}_cycles_per_mb"] = {k[len(ph) + 1:]: round(v / n, 1) for k, v in pr.items()
                                               if k.startswith(ph) and not k.endswith("mbs")}
+        if lat is not None:
+            res.update(latency_fields(a, lat))
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -136,6 +136,7 @@ void bind_net(py::module_& m) {
       .def("stop", &net::RtspServer::stop, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("port", &net::RtspServer::port)
       .def("inject", &net::RtspServer::inject)
+      .def("set_pacing", &net::RtspServer::set_pacing, py::arg("mode"))
       .def_property_readonly("sessions", &net::RtspServer::sessions)
       .def_property_readonly("aus_sent", &net::RtspServer::aus_sent);
 
@@ -197,8 +198,9 @@ void bind_net(py::module_& m) {
       .def(py::init([](Worker& w, int cam, const std::string& name, const std::string& rtsp,
                        const std::string& rtmp, const std::string& disk,
                        std::shared_ptr<mux::Archiver> arch, int timeout_ms, int reconnect_ms,
-                       int max_backoff_ms) {
+                       int max_backoff_ms, bool lossless) {
              IngestConfig c;
+             c.lossless = lossless;
              c.name = name;
              c.rtsp_url = rtsp;
              c.rtmp_url = rtmp;
@@ -211,7 +213,7 @@ void bind_net(py::module_& m) {
            py::arg("worker"), py::arg("cam"), py::arg("name"), py::arg("rtsp_url"),
            py::arg("rtmp_url") = "", py::arg("disk_path") = "", py::arg("archiver") = nullptr,
            py::arg("timeout_ms") = 5000, py::arg("reconnect_delay_ms") = 1000,
-           py::arg("max_backoff_ms") = 30000, py::keep_alive<1, 2>())
+           py::arg("max_backoff_ms") = 30000, py::arg("lossless") = false, py::keep_alive<1, 2>())
       .def("start", &IngestSession::start)
       .def("stop", &IngestSession::stop, py::call_guard<py::gil_scoped_release>())
       .def("state", [](IngestSession& s) { return state_dict(s.state()); })

@@ -1,5 +1,7 @@
 // pybind11 bindings of the vep native data plane (module `video_edge_ai_proxy_amd._vep`).
 // Every call that can block (decode, D2H, network) releases the GIL.
+#include <malloc.h>
+
 #include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
@@ -177,6 +179,14 @@ PYBIND11_MODULE(_vep, m) {
   py::register_exception<UnsupportedStream>(m, "UnsupportedStream");
 
   m.def("device_count", &gpu::device_count);
+  // Frame servers and clients allocate a new multi-MB buffer per frame: glibc would mmap each
+  // one and the first touch of its pages then costs more than the copy itself. Keep such blocks
+  // in the (per-thread) heaps instead, so freed frame buffers are reused without page faults.
+  m.def("tune_malloc_for_frames", [](int mmap_threshold_mb) {
+    const int thr = std::max(1, mmap_threshold_mb) << 20;
+    return mallopt(M_MMAP_THRESHOLD, thr) == 1 && mallopt(M_TRIM_THRESHOLD, 4 * thr) == 1 &&
+           mallopt(M_TOP_PAD, thr) == 1;
+  }, py::arg("mmap_threshold_mb") = 64);
 
   py::class_<SynthConfig>(m, "SynthConfig")
       .def(py::init<>())
@@ -919,36 +929,47 @@ PYBIND11_MODULE(_vep, m) {
            },
            py::arg("idx"), py::arg("after") = 0)
       .def("video_frame",
-           // Serialized VideoFrame proto built in one buffer: header, D2H'd pixels, trailer.
+           // Serialized VideoFrame proto, built in place in its final bytes object: header, the
+           // slot's pixels (D2H through a pinned pool buffer, GIL released), trailer; the object
+           // is then shrunk to the exact length (no second copy of the frame).
            [](Worker& w, int i, i64 after, const std::string& device_id) -> py::object {
              Camera& c = cam_of(w, i);
              std::shared_ptr<FrameRing> ring = c.ring();
              if (!ring) return py::none();
-             size_t n = ring->slot_bytes();
+             const size_t n = ring->slot_bytes();
              FrameMeta probe;
              int slot;
              if (!ring->latest(after, &probe, &slot)) return py::none();
-             auto [pre0, suf0] = encode_video_frame(probe, n, device_id);
-             size_t total = pre0.size() + n + suf0.size() + 64;
-             PyObject* b = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(total));
+             // the prefix holds width, height and the data length: fixed for this ring
+             const std::string pre = encode_video_frame(probe, n, device_id).first;
+             // the trailer's worst case: 7 varint fields (<= 11 B each), 2 bools, frame_type,
+             // time_base, shape, device_id
+             const size_t suf_max = 7 * 11 + 2 * 2 + 3 + 9 + 48 + 12 + device_id.size();
+             PyObject* b = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(pre.size() + n + suf_max));
              if (!b) throw py::error_already_set();
-             py::object holder = py::reinterpret_steal<py::object>(b);
              char* buf = PyBytes_AS_STRING(b);
+             std::memcpy(buf, pre.data(), pre.size());
              FrameMeta m;
              bool ok;
              {
                py::gil_scoped_release r;
-               ok = w.read_latest(*ring, after, &m, reinterpret_cast<u8*>(buf) + 32 + pre0.size(), n);
+               try {
+                 ok = w.read_latest(*ring, after, &m, reinterpret_cast<u8*>(buf) + pre.size(), n);
+               } catch (...) {
+                 py::gil_scoped_acquire a;
+                 Py_DECREF(b);
+                 throw;
+               }
              }
-             if (!ok) return py::none();
-             auto [pre, suf] = encode_video_frame(m, n, device_id);
-             // header may differ in length from the probe: place it right before the data
-             char* data = buf + 32 + pre0.size();
-             char* start = data - pre.size();
-             std::memcpy(start, pre.data(), pre.size());
-             std::memcpy(data + n, suf.data(), suf.size());
-             size_t len = pre.size() + n + suf.size();
-             py::bytes res(start, len);  // one host copy into an exact-size object
+             if (!ok) {
+               Py_DECREF(b);
+               return py::none();
+             }
+             auto [pre2, suf] = encode_video_frame(m, n, device_id);
+             VEP_CHECK(pre2 == pre && suf.size() <= suf_max, "VideoFrame header changed while serving");
+             std::memcpy(buf + pre.size() + n, suf.data(), suf.size());
+             if (_PyBytes_Resize(&b, Py_ssize_t(pre.size() + n + suf.size())) != 0) throw py::error_already_set();
+             py::object res = py::reinterpret_steal<py::object>(b);
              return py::make_tuple(m.seq, res, meta_dict(m));
            },
            py::arg("idx"), py::arg("after") = 0, py::arg("device_id") = "")

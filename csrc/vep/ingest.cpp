@@ -41,13 +41,42 @@ class IngestSession::Handler : public IoHandler {
  public:
   Handler(IngestSession* s, std::shared_ptr<net::RtspClient> c) : s_(s), c_(std::move(c)) {}
   bool on_readable() override {
-    return c_->read_available([this](const AuPtr& au) { s_->on_au(au); }, why_);
+    if (!c_->read_available([this](const AuPtr& au) { s_->on_au(au); }, why_)) return false;
+    if (s_->backlogged()) {  // lossless mode: hold the socket until the parse strand drains
+      paused_.store(true);
+      s_->svc_->io.pause_reading(*this);
+    }
+    return true;
   }
-  bool on_tick() override { return c_->maintain(why_); }
+  bool on_tick() override {
+    if (paused_.load()) {
+      c_->touch_rx();  // held back on purpose: not a stalled camera
+      if (s_->drained() && paused_.exchange(false)) {  // (safety net for a missed resume)
+        epoll_resume_in_callback();
+      }
+    }
+    return c_->maintain(why_);
+  }
+  // Parse strand side: the backlog has drained, read again.
+  void resume(const std::shared_ptr<Handler>& self) {
+    if (paused_.exchange(false)) s_->svc_->io.resume_reading(self);
+  }
   void on_closed() override { s_->on_stream_end(why_, c_->bytes(), c_->lost()); }
   const net::RtspClient& client() const { return *c_; }
+  bool paused() const { return paused_.load(); }
 
  private:
+  void epoll_resume_in_callback() {
+    // on_tick runs with this handler's lock held: re-arm through a task on the connector pool
+    std::weak_ptr<IoHandler> wh = self_;
+    auto svc = s_->svc_;
+    svc->connect.post([svc, wh] {
+      if (auto h = wh.lock()) svc->io.resume_reading(h);
+    });
+  }
+  friend class IngestSession;
+  std::weak_ptr<IoHandler> self_;
+  std::atomic<bool> paused_{false};
   IngestSession* s_;
   std::shared_ptr<net::RtspClient> c_;
   std::string why_;
@@ -55,6 +84,18 @@ class IngestSession::Handler : public IoHandler {
 
 // AUs a camera's parse strand may hold before ingest drops to the next keyframe (~8 s at 30 fps).
 constexpr size_t kMaxParseBacklog = 256;
+// Lossless mode: the socket is paused above kHighWater queued AUs and resumed at kLowWater.
+constexpr size_t kHighWater = 32, kLowWater = 8;
+
+bool IngestSession::backlogged() const {
+  const u64 key = parse_key_.load(std::memory_order_relaxed);
+  return cfg_.lossless && pooled_ && key && svc_->parse.depth(key) >= kHighWater;
+}
+
+bool IngestSession::drained() const {
+  const u64 key = parse_key_.load(std::memory_order_relaxed);
+  return !key || svc_->parse.depth(key) <= kLowWater;
+}
 
 IngestSession::IngestSession(Worker& w, int cam, IngestConfig cfg,
                              std::shared_ptr<mux::Archiver> archiver)
@@ -76,6 +117,7 @@ void IngestSession::start() {
   }
   svc_ = IngestServices::acquire();
   guard_ = std::make_shared<Guard>();
+  parse_live_ = std::make_shared<std::atomic<bool>>(true);
   drop_to_key_ = false;
   {
     std::lock_guard<std::mutex> g(mu_);
@@ -99,6 +141,11 @@ void IngestSession::stop() {
     st_.bytes += h->client().bytes();
     st_.lost += h->client().lost();
   }
+  // No socket callback runs any more, so nothing posts new parse work: cancel what is queued on
+  // the camera's strand and wait for the task that may be running. After this the Worker may
+  // remove the camera and reuse its slot without a stale task reaching the new camera.
+  if (parse_live_) parse_live_->store(false);
+  if (const u64 key = parse_key_.exchange(0); key && svc_) svc_->parse.drain(key);
   pub_.reset();
   gop_.clear();
   seen_key_ = false;
@@ -179,6 +226,7 @@ void IngestSession::connect_once() {
   drop_to_key_ = false;
   log(false, "connected to " + cfg_.name + " (" + (info.codec == Codec::kH264 ? "H.264" : "H.265") + ")");
   auto h = std::make_shared<Handler>(this, client);
+  h->self_ = h;
   {
     std::lock_guard<std::mutex> g(handler_mu_);
     handler_ = h;
@@ -228,7 +276,9 @@ void IngestSession::decode(const std::shared_ptr<Camera>& cam, const AuPtr& au) 
   }
   // parse off the socket thread, in order, on the camera's strand of the shared parse pool
   const u64 key = u64(reinterpret_cast<uintptr_t>(cam.get()));
-  if (drop_to_key_) {
+  if (cfg_.lossless) {
+    // never drop: on_readable pauses the socket above the high-water mark
+  } else if (drop_to_key_) {
     if (!au->keyframe) {
       cam->skipped.fetch_add(1, std::memory_order_relaxed);
       return;
@@ -240,13 +290,22 @@ void IngestSession::decode(const std::shared_ptr<Camera>& cam, const AuPtr& au) 
     log(true, "parse backlog full: dropping packets until the next keyframe");
     return;
   }
-  svc_->parse.post(key, [cam, au] {
+  parse_key_.store(key, std::memory_order_relaxed);
+  std::weak_ptr<Handler> wh;
+  if (cfg_.lossless) {
+    std::lock_guard<std::mutex> g(handler_mu_);
+    wh = handler_;
+  }
+  svc_->parse.post(key, [cam, au, live = parse_live_, wh, svc = svc_, key] {
+    if (!live->load(std::memory_order_acquire)) return;  // session stopped: cancelled
     try {
       cam->on_access_unit(au);
     } catch (const std::exception& e) {
       cam->errors.fetch_add(1);
       cam->logs.add(true, std::string("failed to decode packet: ") + e.what());
     }
+    if (auto h = wh.lock())  // lossless: the socket was paused and the backlog has drained
+      if (h->paused() && svc->parse.depth(key) <= kLowWater + 1) h->resume(h);
   });
 }
 

@@ -33,6 +33,11 @@ struct IngestConfig {
   int timeout_ms = 5000;
   int reconnect_delay_ms = 1000;
   int max_backoff_ms = 30000;
+  // Lossless ingest: while the camera's parse backlog is deep, stop reading its socket (TCP
+  // back-pressure to the camera) instead of dropping access units until the next keyframe.
+  // For sources that can be slowed down (files, replay farms, benchmarks); a live camera that
+  // outruns the decoder is better served by the default, which stays at the live edge.
+  bool lossless = false;
 };
 
 struct SessionState {
@@ -101,7 +106,10 @@ class IngestSession {
   IngestSession(Worker& w, int cam, IngestConfig cfg, std::shared_ptr<mux::Archiver> archiver);
   ~IngestSession();
   void start();
-  void stop();  // synchronous: no callback of this session runs after it returns
+  // Synchronous: when it returns no callback of this session runs, and every parse task it
+  // posted to the shared strand pool has finished or been cancelled (so the camera slot can be
+  // removed and reused).
+  void stop();
   SessionState state() const;
   const IngestConfig& config() const { return cfg_; }
   void log(bool err, const std::string& s);
@@ -110,6 +118,8 @@ class IngestSession {
  private:
   struct Guard;  // liveness token of the pooled mode's timers / connector tasks
   class Handler;
+  bool backlogged() const;  // lossless mode: parse backlog above the high-water mark
+  bool drained() const;     // parse backlog at or below the low-water mark
   void run();
   void on_au(const AuPtr& au);
   void decode(const std::shared_ptr<Camera>& cam, const AuPtr& au);
@@ -126,6 +136,10 @@ class IngestSession {
   std::shared_ptr<Handler> handler_;
   std::mutex handler_mu_;
   bool drop_to_key_ = false;  // parse backlog overflowed: skip until the next keyframe
+  // Cancellation token of the parse tasks this session posted (checked by each task before it
+  // touches the camera) and the strand key they were posted under.
+  std::shared_ptr<std::atomic<bool>> parse_live_;
+  std::atomic<u64> parse_key_{0};
   Worker& w_;
   int cam_;
   IngestConfig cfg_;

@@ -136,6 +136,7 @@ void StrandPool::run(int me) {
       cv_.notify_one();
     } else {
       strands_.erase(key);
+      owner_.erase(key);  // an idle key keeps no affinity (camera addresses get reused)
       idle_cv_.notify_all();
     }
   }
@@ -265,6 +266,24 @@ void IoLoop::remove(const std::shared_ptr<IoHandler>& h) {
   Loop& l = *loops_[size_t(k)];
   std::lock_guard<std::mutex> g(l.mu);
   l.live.erase(h.get());
+}
+
+void IoLoop::pause_reading(IoHandler& h) {  // (the loop thread holds h.mu_)
+  if (h.gone_ || h.fd_ < 0) return;
+  epoll_event ev{};
+  ev.events = EPOLLRDHUP;  // still told when the peer goes away
+  ev.data.ptr = &h;
+  ::epoll_ctl(loops_[size_t(h.loop_)]->ep, EPOLL_CTL_MOD, h.fd_, &ev);
+}
+
+void IoLoop::resume_reading(const std::shared_ptr<IoHandler>& h) {
+  if (!h) return;
+  std::lock_guard<std::mutex> hg(h->mu_);
+  if (h->gone_ || h->fd_ < 0) return;  // removed: the fd may already belong to someone else
+  epoll_event ev{};
+  ev.events = EPOLLIN | EPOLLRDHUP;
+  ev.data.ptr = h.get();
+  ::epoll_ctl(loops_[size_t(h->loop_)]->ep, EPOLL_CTL_MOD, h->fd_, &ev);
 }
 
 void IoLoop::dispatch(Loop& l, const std::shared_ptr<IoHandler>& h, bool readable) {

@@ -113,6 +113,10 @@ class IoLoop {
   void add(int fd, const std::shared_ptr<IoHandler>& h);
   // Synchronous: when it returns no callback of `h` is running or will run.
   void remove(const std::shared_ptr<IoHandler>& h);
+  // Flow control: stop / restart read notifications of `h` (ticks continue). pause_reading()
+  // may only be called from inside a callback of `h`; resume_reading() from any other thread.
+  void pause_reading(IoHandler& h);
+  void resume_reading(const std::shared_ptr<IoHandler>& h);
   int threads() const { return int(loops_.size()); }
   size_t handlers() const;
 

@@ -102,6 +102,7 @@ struct RtspClientOptions {
 // access units until `stop` is set, the server closes, or the socket times out.
 class RtspClient {
  public:
+  void touch_rx() { last_rx_us_ = mono_us(); }  // reading paused on purpose (flow control)
   using AuCallback = std::function<void(const AuPtr&)>;
   RtspClient(std::string url, RtspClientOptions opt = {});
   ~RtspClient();
@@ -166,11 +167,16 @@ class RtspServer {
   void inject(const std::string& path, Fault f);  // applies to the stream's live sessions
   int sessions() const { return live_.load(); }
   u64 aus_sent() const { return aus_sent_.load(); }
+  // Override every stream's pacing: 1 = real time at cfg.fps, 0 = as fast as the socket
+  // drains, -1 = each stream's own ServedStream::realtime. Takes effect at the next frame.
+  void set_pacing(int mode) { pace_.store(mode); }
 
  private:
   struct Stream {
     ServedStream cfg;
     std::vector<AuPtr> cache;
+    // RTP payloads (FU-A / single NAL) of each cached AU, packetized once: (payload, marker)
+    std::vector<std::vector<std::pair<std::vector<u8>, bool>>> cache_pk;
     std::vector<u8> sps, pps, vps;
     std::atomic<int> fault{0};
   };
@@ -186,6 +192,7 @@ class RtspServer {
   std::vector<int> conn_fds_;
   std::atomic<int> live_{0};
   std::atomic<u64> aus_sent_{0};
+  std::atomic<int> pace_{-1};
 };
 
 }  // namespace vep::net

@@ -444,6 +444,17 @@ void RtspServer::add_stream(const std::string& path, const ServedStream& s) {
   st->vps = enc.vps_nal();
   if (s.cached_frames > 0)
     for (int i = 0; i < s.cached_frames; ++i) st->cache.push_back(enc.next());
+  const Codec codec = s.cfg.codec;
+  for (const AuPtr& au : st->cache) {
+    auto& pks = st->cache_pk.emplace_back();
+    std::vector<std::vector<u8>> pk;
+    for (size_t i = 0; i < au->nals.size(); ++i) {
+      pk.clear();
+      packetize_nal(codec, au->nal(i), au->nal_size(i), 1400, pk);
+      for (size_t j = 0; j < pk.size(); ++j)
+        pks.emplace_back(std::move(pk[j]), (i + 1 == au->nals.size()) && (j + 1 == pk.size()));
+    }
+  }
   std::lock_guard<std::mutex> g(mu_);
   streams_[path.empty() || path[0] != '/' ? "/" + path : path] = st;
 }
@@ -617,7 +628,7 @@ void RtspServer::serve(int fd) {
     h.ssrc = 0x5ee0000u ^ u32(fd);
     h.seq = u16(fd * 7919);
     i64 frame = 0;
-    const i64 t0 = mono_us();
+    i64 pace_t0 = -1, pace_f0 = 0;
     std::vector<u8> out;
     std::vector<std::vector<u8>> pk;
     bool skip_gop = false;
@@ -654,14 +665,37 @@ void RtspServer::serve(int fd) {
         ++frame;
         continue;
       }
-      if (st->cfg.realtime) {
-        i64 due = t0 + frame * 1000000 / fps;
+      const int pace = pace_.load();
+      if (pace == 1 || (pace < 0 && st->cfg.realtime)) {
+        if (pace_t0 < 0) {  // (re)start pacing from this frame on
+          pace_t0 = mono_us();
+          pace_f0 = frame;
+        }
+        i64 due = pace_t0 + (frame - pace_f0) * 1000000 / fps;
         i64 now = mono_us();
         if (due > now) std::this_thread::sleep_for(std::chrono::microseconds(due - now));
+      } else {
+        pace_t0 = -1;
       }
       h.ts = u32(frame * 90000 / fps);
       out.clear();
-      for (size_t i = 0; i < au->nals.size(); ++i) {
+      const bool cached = !enc && fault != int(Fault::kCorruptNal);
+      if (cached) {  // cached AU: payloads packetized once
+        for (const auto& [pl, marker] : st->cache_pk[size_t(frame % i64(st->cache.size()))]) {
+          h.marker = marker;
+          const size_t len = kRtpHeader + pl.size();
+          const size_t o = out.size();
+          out.resize(o + 4 + len);
+          out[o] = '$';
+          out[o + 1] = 0;
+          out[o + 2] = u8(len >> 8);
+          out[o + 3] = u8(len);
+          write_rtp_header(&out[o + 4], h);
+          std::memcpy(&out[o + 4 + kRtpHeader], pl.data(), pl.size());
+          ++h.seq;
+        }
+      }
+      for (size_t i = 0; !cached && i < au->nals.size(); ++i) {
         pk.clear();
         std::vector<u8> nal(au->nal(i), au->nal(i) + au->nal_size(i));
         const bool vcl = codec == Codec::kH264 ? ((nal[0] & 0x1f) == 1 || (nal[0] & 0x1f) == 5)

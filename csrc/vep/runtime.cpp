@@ -554,7 +554,11 @@ Worker::~Worker() {
     if (ln.stream && ln.stream != stream_) (void)hipStreamDestroy(ln.stream);
     if (ln.copy) (void)hipStreamDestroy(ln.copy);
   }
-  dev_.free_pinned(h_serve_);
+  for (auto& b : serve_all_) {
+    dev_.free_pinned(b->h);
+    for (hipEvent_t e : b->ev)
+      if (e) (void)hipEventDestroy(e);
+  }
   dev_.free(avc_prof_);
   if (stream_) (void)hipStreamDestroy(stream_);
   if (copy_stream_) (void)hipStreamDestroy(copy_stream_);
@@ -1809,6 +1813,37 @@ bool Worker::read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t ca
   return r && read_latest(*r, after, meta, dst, cap);
 }
 
+Worker::ServeBuf* Worker::acquire_serve(size_t n) {
+  ServeBuf* b = nullptr;
+  {
+    std::unique_lock<std::mutex> g(serve_mu_);
+    if (serve_free_.empty() && serve_all_.size() < size_t(kServeBufs)) {
+      serve_all_.push_back(std::make_unique<ServeBuf>());
+      serve_free_.push_back(serve_all_.back().get());
+    }
+    serve_cv_.wait(g, [&] { return !serve_free_.empty(); });
+    b = serve_free_.back();
+    serve_free_.pop_back();
+  }
+  if (b->cap < n) {  // first use, or a larger ring (resolution change)
+    dev_.free_pinned(b->h);
+    b->h = static_cast<u8*>(dev_.alloc_pinned(n));
+    b->cap = n;
+  }
+  if (!b->ev[0])
+    for (hipEvent_t& e : b->ev)  // waiters sleep: several server threads wait at once
+      VEP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
+  return b;
+}
+
+void Worker::release_serve(ServeBuf* b) {
+  {
+    std::lock_guard<std::mutex> g(serve_mu_);
+    serve_free_.push_back(b);
+  }
+  serve_cv_.notify_one();
+}
+
 bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, size_t cap) {
   FrameRing* ring = &rg;
   for (int attempt = 0; attempt < 4; ++attempt) {
@@ -1817,18 +1852,30 @@ bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, siz
     const size_t n = ring->slot_bytes();
     VEP_CHECK(cap >= n, "read_latest destination too small");
     if (dev_.gpu()) {
-      std::lock_guard<std::mutex> g(serve_mu_);
-      if (n > serve_cap_) {
-        dev_.free_pinned(h_serve_);
-        serve_cap_ = n;
-        h_serve_ = static_cast<u8*>(dev_.alloc_pinned(n));
-      }
       dev_.bind();
-      VEP_HIP(hipMemcpyAsync(h_serve_, ring->slot_ptr(slot), n, hipMemcpyDeviceToHost,
-                             serve_stream_));
-      VEP_HIP(hipStreamSynchronize(serve_stream_));
+      ServeBuf* b = acquire_serve(n);
+      const u8* src = ring->slot_ptr(slot);
+      const size_t chunk = (n + kServeChunks - 1) / kServeChunks;
+      try {
+        for (int k = 0; k < kServeChunks; ++k) {
+          const size_t off = size_t(k) * chunk;
+          if (off >= n) break;
+          VEP_HIP(hipMemcpyAsync(b->h + off, src + off, std::min(chunk, n - off), hipMemcpyDeviceToHost,
+                                 serve_stream_));
+          VEP_HIP(hipEventRecord(b->ev[k], serve_stream_));
+        }
+        for (int k = 0; k < kServeChunks; ++k) {
+          const size_t off = size_t(k) * chunk;
+          if (off >= n) break;
+          VEP_HIP(hipEventSynchronize(b->ev[k]));
+          std::memcpy(dst + off, b->h + off, std::min(chunk, n - off));
+        }
+      } catch (...) {
+        release_serve(b);
+        throw;
+      }
+      release_serve(b);
       if (!ring->still_valid(slot, meta->seq)) continue;
-      std::memcpy(dst, h_serve_, n);
       return true;
     }
     std::memcpy(dst, ring->slot_ptr(slot), n);

@@ -390,9 +390,22 @@ class Worker {
 
  private:
   void add_time(double Timers_::*f, double us);
-  u8* h_serve_ = nullptr;
-  size_t serve_cap_ = 0;
+  // Serving: a pool of pinned host buffers, one per in-flight read_latest(), so concurrent
+  // requests DMA in parallel instead of queueing on one buffer. Each read streams the slot in
+  // kServeChunks pieces: the host copy of chunk k overlaps the DMA of chunk k+1.
+  static constexpr int kServeBufs = 8;
+  static constexpr int kServeChunks = 4;
+  struct ServeBuf {
+    u8* h = nullptr;
+    size_t cap = 0;
+    hipEvent_t ev[kServeChunks] = {};
+  };
+  ServeBuf* acquire_serve(size_t n);
+  void release_serve(ServeBuf* b);
   std::mutex serve_mu_;
+  std::condition_variable serve_cv_;
+  std::vector<std::unique_ptr<ServeBuf>> serve_all_;
+  std::vector<ServeBuf*> serve_free_;
   u8* cons_hwc_ = nullptr;
   void* cons_chw_ = nullptr;
   bool owns_cons_ = true;

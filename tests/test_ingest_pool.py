@@ -82,3 +82,41 @@ def test_pooled_session_restarts_after_server_loss(native):
     s.stop()
     assert s.state()["status"] == "exited"
     w.stop()
+
+
+def test_stop_cancels_parse_backlog_before_slot_reuse(native, monkeypatch):
+    # One parse thread and an unthrottled 640x480 compressed camera: the camera's parse strand
+    # holds a backlog when the session stops. stop() must cancel/drain it, so after the slot is
+    # removed and reused by a new camera, no stale access unit of the old stream reaches it
+    # (ingest.cpp stop() left queued strand tasks running against the reused index).
+    monkeypatch.setenv("VEP_INGEST_PARSE_THREADS", "1")
+    srv = native.RtspServer("127.0.0.1", 0)
+    c = native.SynthConfig()
+    c.width, c.height, c.gop, c.seed = 640, 480, 30, 7
+    c.compressed = True
+    srv.add_stream("/fast", c, realtime=False, cached_frames=30)
+    srv.start()
+    w = native.Worker(device=-1)
+    w.start()
+    try:
+        for _ in range(3):
+            cam = w.add_camera("old", 2)
+            w.set_last_query(cam, int(time.time() * 1000))
+            s = native.IngestSession(w, cam, "old", f"rtsp://127.0.0.1:{srv.port}/fast")
+            s.start()
+            t = time.time()
+            while time.time() - t < 10 and w.stats(cam)["decoded"] < 3:
+                time.sleep(0.02)
+            assert w.stats(cam)["decoded"] >= 3
+            s.stop()
+            w.remove_camera(cam)
+            new = w.add_camera("new", 2)
+            assert new == cam  # the slot is reused
+            w.set_last_query(new, int(time.time() * 1000))
+            time.sleep(0.5)
+            st = w.stats(new)
+            assert st["decoded"] == 0 and st["published"] == 0 and st["packets"] == 0, st
+            w.remove_camera(new)
+    finally:
+        w.stop()
+        srv.stop()

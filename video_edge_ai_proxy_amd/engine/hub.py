@@ -225,7 +225,12 @@ class Hub:
     def latest_frame_bytes(self, name: str, after: int = 0, wait_ms: int = 0):
         """(seq, serialized VideoFrame, meta) of the newest frame with seq > after, or None."""
         w, cam = self.worker_of(name)
-        if wait_ms > 0 and w.published(cam) <= after:
+        pub = w.published(cam)
+        if pub < after:
+            # the caller's cursor belongs to an older ring of this camera (a restarted worker
+            # process or a resolution change starts a new ring at 0): start over
+            after = 0
+        if wait_ms > 0 and pub <= after:
             w.wait_frame(cam, after, wait_ms)
         return w.video_frame(cam, after, name)
 

@@ -109,6 +109,14 @@ class _Child:
             return r[1]
         raise _ERRORS.get(r[1], RuntimeError)(r[2])
 
+    def close_pipes(self) -> None:
+        for f in (self.proc.stdin, self.proc.stdout):
+            try:
+                if f is not None:
+                    f.close()
+            except Exception:  # noqa: BLE001
+                pass
+
     def close(self, timeout_s: float = 20.0) -> None:
         try:
             self.proc.stdin.close()  # the child shuts its hub down and exits
@@ -119,6 +127,7 @@ class _Child:
         except subprocess.TimeoutExpired:
             self.proc.kill()
             self.proc.wait()
+        self.close_pipes()
 
 
 class _WorkerView:
@@ -193,17 +202,24 @@ class ProcessHub:
                     log.error("restart of device %s failed: %s", self.devices[i], e)
 
     def _restart(self, i: int) -> None:
+        self._children[i].close_pipes()  # the dead child's pipes
         child = _Child(self.devices[i], self._cfg_json)
-        with self._lock:
-            mine = [n for n, h in self.cameras.items() if h.worker_index == i]
-            for n in mine:  # re-add before the fresh child takes calls (until then: restarting)
-                spec = self._specs[n]
-                res = child.call("start_camera", *spec["args"])
-                self.cameras[n].cam = res["cam"]
-                if self._proxy.get(n):
-                    child.call("set_proxy", n, True)
-            self._children[i] = child
-            self.child_restarts[i] += 1
+        try:
+            with self._lock:
+                mine = [n for n, h in self.cameras.items() if h.worker_index == i]
+                for n in mine:  # re-add before the fresh child takes calls (until then: restarting)
+                    spec = self._specs[n]
+                    res = child.call("start_camera", *spec["args"])
+                    self.cameras[n].cam = res["cam"]
+                    if self._proxy.get(n):
+                        child.call("set_proxy", n, True)
+                self._children[i] = child
+                self.child_restarts[i] += 1
+        except BaseException:
+            # a half-initialised child must not survive (the next supervision round starts
+            # another one): it holds a GPU context and some of the cameras
+            child.close(timeout_s=5.0)
+            raise
         log.info("device %s: fresh worker process pid %d, %d cameras re-added", self.devices[i], child.pid, len(mine))
 
     # ------------------------------------------------------------------ lifecycle (Hub API)

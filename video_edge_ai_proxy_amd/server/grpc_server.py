@@ -23,6 +23,7 @@ from typing import Optional
 import grpc
 
 from ..engine.hub import CameraNotFound
+from ..engine.isolated import WorkerRestarting
 from ..models import RTMPStreamStatus
 from ..proto import SERVICE, pb
 from ..services.edge import Forbidden
@@ -32,6 +33,14 @@ from ..utils import now_ms, parse_rtmp_key
 log = logging.getLogger("vep.grpc")
 
 MAX_MSG = 256 * 1024 * 1024  # 4K BGR24 frames are 24.9 MB; grpcio's default is 4 MiB
+# Multi-MB frame messages: let the peer send 16 MB HTTP/2 frames, read the socket in large
+# chunks and keep a deep flow-control lookahead (measured: the Python client's receive CPU per
+# 1080p frame drops from ~14 ms to ~9 ms on loopback).
+FRAME_CHANNEL_OPTS = [("grpc.max_receive_message_length", MAX_MSG), ("grpc.max_send_message_length", MAX_MSG),
+                      ("grpc.http2.max_frame_size", 16777215), ("grpc.http2.lookahead_bytes", 64 << 20),
+                      ("grpc.experimental.tcp_read_chunk_size", 4 << 20),
+                      ("grpc.experimental.tcp_min_read_chunk_size", 256 << 10),
+                      ("grpc.experimental.tcp_max_read_chunk_size", 8 << 20)]
 STREAM_DEADLINE_S = 15.0
 WAIT_ATTEMPTS, WAIT_BLOCK_MS = 3, 1000
 MAX_CURSORS = 65536  # (client, camera) cursors kept, least recently used evicted first
@@ -86,8 +95,8 @@ class ImageService:
                         del self.latencies_ms[:5000]
                     return data
                 time.sleep(0.016)
-        except CameraNotFound:
-            pass
+        except (CameraNotFound, WorkerRestarting):
+            pass  # removed meanwhile / its worker process is being restarted: an empty frame
         return _EMPTY
 
     def VideoLatestImage(self, request_iterator, context):
@@ -213,9 +222,12 @@ def make_handler(svc: ImageService) -> grpc.GenericRpcHandler:
     return grpc.method_handlers_generic_handler(SERVICE.full_name, handlers)
 
 
-def serve(svc: ImageService, address: str = "0.0.0.0:50001", workers: int = 64) -> grpc.Server:
-    opts = [("grpc.max_send_message_length", MAX_MSG), ("grpc.max_receive_message_length", MAX_MSG),
-            ("grpc.so_reuseport", 0)]
+def serve(svc: ImageService, address: str = "0.0.0.0:50001", workers: int = 64,
+          reuseport: bool = False) -> grpc.Server:
+    from .._native import native
+
+    native.tune_malloc_for_frames(64)  # every response allocates a frame-sized bytes object
+    opts = FRAME_CHANNEL_OPTS + [("grpc.so_reuseport", 1 if reuseport else 0)]
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers), options=opts,
                          maximum_concurrent_rpcs=None)
     server.add_generic_rpc_handlers((make_handler(svc),))
@@ -231,8 +243,7 @@ class ImageClient:
     """Client stub (the reference used protoc-generated ``ImageStub``)."""
 
     def __init__(self, target: str):
-        self.channel = grpc.insecure_channel(target, options=[
-            ("grpc.max_receive_message_length", MAX_MSG), ("grpc.max_send_message_length", MAX_MSG)])
+        self.channel = grpc.insecure_channel(target, options=FRAME_CHANNEL_OPTS)
         p = SERVICE.path
         self.VideoLatestImage = self.channel.stream_stream(
             p("VideoLatestImage"), request_serializer=pb.VideoFrameRequest.SerializeToString,
