@@ -214,6 +214,13 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("weighted_p", &SynthConfig::weighted_p)
       .def_readwrite("weighted_b", &SynthConfig::weighted_b)
       .def_readwrite("direct_spatial", &SynthConfig::direct_spatial)
+      .def_readwrite("tile_cols", &SynthConfig::tile_cols)
+      .def_readwrite("tile_rows", &SynthConfig::tile_rows)
+      .def_readwrite("wpp", &SynthConfig::wpp)
+      .def_readwrite("segments", &SynthConfig::segments)
+      .def_readwrite("scaling_lists", &SynthConfig::scaling_lists)
+      .def_readwrite("long_term", &SynthConfig::long_term)
+      .def_readwrite("lossless", &SynthConfig::lossless)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -349,6 +356,14 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("pcm", &hevc::HevcEncConfig::pcm)
       .def_readwrite("tmvp", &hevc::HevcEncConfig::tmvp)
       .def_readwrite("slices", &hevc::HevcEncConfig::slices)
+      .def_readwrite("tile_cols", &hevc::HevcEncConfig::tile_cols)
+      .def_readwrite("tile_rows", &hevc::HevcEncConfig::tile_rows)
+      .def_readwrite("wpp", &hevc::HevcEncConfig::wpp)
+      .def_readwrite("segments", &hevc::HevcEncConfig::segments)
+      .def_readwrite("scaling_lists", &hevc::HevcEncConfig::scaling_lists)
+      .def_readwrite("weighted", &hevc::HevcEncConfig::weighted)
+      .def_readwrite("long_term", &hevc::HevcEncConfig::long_term)
+      .def_readwrite("lossless", &hevc::HevcEncConfig::lossless)
       .def_readwrite("coverage", &hevc::HevcEncConfig::coverage)
       .def_readwrite("objects", &hevc::HevcEncConfig::objects)
       .def_readwrite("noise", &hevc::HevcEncConfig::noise)
@@ -655,6 +670,80 @@ PYBIND11_MODULE(_vep, m) {
     d["ctb_size"] = s.ctb_size();
     d["pcm"] = s.pcm;
     d["num_short_term_rps"] = int(s.st_rps.size());
+    d["scaling_list"] = s.scaling_list;
+    d["scaling_list_data"] = s.scaling_list_data;
+    d["long_term_refs"] = s.long_term_refs;
+    d["num_long_term_ref_pics_sps"] = s.num_long_term_ref_pics_sps;
+    return d;
+  });
+  auto hevc_rbsp = [](const std::string& nal) {
+    std::vector<u8> r(nal.size());
+    r.resize(ebsp_to_rbsp(reinterpret_cast<const u8*>(nal.data()), nal.size(), r.data()));
+    return r;
+  };
+  m.def("parse_hevc_pps", [hevc_rbsp](const std::string& nal) {
+    const std::vector<u8> r = hevc_rbsp(nal);
+    hevc::Pps p = hevc::parse_pps(r.data(), r.size());
+    py::dict d;
+    d["tiles"] = p.tiles;
+    d["tile_cols"] = p.tile_cols;
+    d["tile_rows"] = p.tile_rows;
+    d["uniform_spacing"] = p.uniform_spacing;
+    d["loop_filter_across_tiles"] = p.loop_filter_across_tiles;
+    d["entropy_coding_sync"] = p.entropy_coding_sync;
+    d["dependent_slice_segments"] = p.dependent_slice_segments;
+    d["weighted_pred"] = p.weighted_pred;
+    d["weighted_bipred"] = p.weighted_bipred;
+    d["transquant_bypass"] = p.transquant_bypass;
+    d["scaling_list"] = p.scaling_list;
+    return d;
+  });
+  // ScalingFactor matrix (raster n x n, n = 4 << size_id) of the default lists, or of the lists an
+  // SPS / PPS carries (the PPS ones win, as in decoding).
+  m.def("hevc_scaling_factors", [hevc_rbsp](int size_id, int matrix_id, py::object sps_nal, py::object pps_nal) {
+    VEP_CHECK(size_id >= 0 && size_id < 4 && matrix_id >= 0 && matrix_id < 6, "bad sizeId / matrixId");
+    hevc::ScalingList sl;
+    if (!sps_nal.is_none()) {
+      const std::vector<u8> r = hevc_rbsp(sps_nal.cast<std::string>());
+      sl = hevc::parse_sps(r.data(), r.size()).sl;
+    }
+    if (!pps_nal.is_none()) {
+      const std::vector<u8> r = hevc_rbsp(pps_nal.cast<std::string>());
+      hevc::Pps p = hevc::parse_pps(r.data(), r.size());
+      if (p.scaling_list) sl = p.sl;
+    }
+    const int n = 4 << size_id;
+    std::vector<u8> f(size_t(n) * n);
+    sl.factors(size_id, matrix_id, f.data());
+    return std::vector<int>(f.begin(), f.end());
+  }, py::arg("size_id"), py::arg("matrix_id"), py::arg("sps_nal") = py::none(), py::arg("pps_nal") = py::none());
+  // Slice segment header fields of an escaped slice NAL: entry point offsets and the byte offset
+  // of slice_segment_data() within the escaped NAL.
+  m.def("hevc_slice_entry_points", [hevc_rbsp](const std::string& nal, const std::string& sps_nal,
+                                               const std::string& pps_nal) {
+    const std::vector<u8> rs = hevc_rbsp(sps_nal), rp = hevc_rbsp(pps_nal), r = hevc_rbsp(nal);
+    const hevc::Sps sps = hevc::parse_sps(rs.data(), rs.size());
+    const hevc::Pps pps = hevc::parse_pps(rp.data(), rp.size());
+    const hevc::SliceHeader prev;  // (a dependent segment's slice fields are not needed here)
+    const hevc::SliceHeader sh = hevc::parse_slice_header(r.data(), r.size(), sps, pps, &prev);
+    // RBSP offset -> escaped offset: count the emulation prevention bytes before it
+    size_t ebsp = 0, rbsp = 0;
+    int zeros = 0;
+    const u8* p = reinterpret_cast<const u8*>(nal.data());
+    while (rbsp < sh.data_bytepos && ebsp < nal.size()) {
+      const u8 b = p[ebsp++];
+      if (zeros >= 2 && b == 3) {
+        zeros = 0;
+        continue;
+      }
+      ++rbsp;
+      zeros = b == 0 ? zeros + 1 : 0;
+    }
+    py::dict d;
+    d["entry_points"] = std::vector<u32>(sh.entry_points.begin(), sh.entry_points.end());
+    d["data_offset_ebsp"] = ebsp;
+    d["dependent"] = sh.dependent;
+    d["segment_address"] = sh.segment_address;
     return d;
   });
   // Random-bin CABAC engine round trip (context-coded with skewed and flipping statistics,

@@ -84,7 +84,8 @@ struct HevcDesc {
   i32 log2ctb, wctb, hctb;
   i32 target;
   i32 cb_qp_offset, cr_qp_offset;
-  i32 flags;             // bit 0 deblock, bit 1 SAO, bit 2 PCM samples not loop-filtered
+  i32 flags;             // bit 0 deblock, bit 1 SAO, bit 2 samples not loop-filtered (pcm_map),
+                         // bit 3 SAO does not cross tile boundaries
   const void* pus;       // hevc::GpuPu[npu]
   const void* tus;       // hevc::GpuTu (level-sorted)
   const i16* coefs;
@@ -98,6 +99,8 @@ struct HevcDesc {
   const void* sao;       // hevc::GpuSao per CTB
   u8* sao_y;             // device scratch: the deblocked picture (SAO input)
   u8* sao_uv;
+  const void* wp;        // hevc::GpuWp (explicit weighted prediction, GpuPu::wp - 1)
+  const u16* ctb_tile;   // tile id per CTB
   i32 npu, pu_begin;     // exclusive prefix of PUs over the round
   i32 blk_begin;         // exclusive prefix of 4x4 blocks over the round
   i32 pad;

@@ -78,6 +78,9 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
       ruv[l] = d.uv + size_t(u.slot[l]) * d.slot_uv;
     }
   const bool bi = u.pred == 3;
+  // explicit weighted prediction: the PU's weights / offsets (uniform per workgroup)
+  const hevc::GpuWp* wp = u.wp ? static_cast<const hevc::GpuWp*>(d.wp) + (u.wp - 1) : nullptr;
+  const int ul = (u.pred & 1) ? 0 : 1;
   const int nl = u.w * u.h;
   for (int s = int(threadIdx.x); s < nl; s += 256) {
     const int i = s % u.w, j = s / u.w;
@@ -86,7 +89,8 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
       if (ry[l])
         v[k++] = hevc::hk_luma_mc(ry[l], stride, W, H, u.x + i + (u.mv[l][0] >> 2), u.y + j + (u.mv[l][1] >> 2),
                                   u.mv[l][0] & 3, u.mv[l][1] & 3);
-    y[(u.y + j) * stride + u.x + i] = hevc::hk_weight(v[0], v[1], bi);
+    y[(u.y + j) * stride + u.x + i] =
+        wp ? hevc::hk_weight_explicit(*wp, 0, v[0], v[1], bi, ul) : hevc::hk_weight(v[0], v[1], bi);
   }
   const int wc = u.w >> 1, hc = u.h >> 1, nc = wc * hc;
   for (int s = int(threadIdx.x); s < 2 * nc; s += 256) {
@@ -96,7 +100,8 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
       if (ruv[l])
         v[k++] = hevc::hk_chroma_mc(ruv[l], stride, W >> 1, H >> 1, c, (u.x >> 1) + i + (u.mv[l][0] >> 3),
                                     (u.y >> 1) + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7);
-    uv[((u.y >> 1) + j) * stride + u.x + 2 * i + c] = hevc::hk_weight(v[0], v[1], bi);
+    uv[((u.y >> 1) + j) * stride + u.x + 2 * i + c] =
+        wp ? hevc::hk_weight_explicit(*wp, 1 + c, v[0], v[1], bi, ul) : hevc::hk_weight(v[0], v[1], bi);
   }
 }
 
@@ -204,13 +209,14 @@ __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict
   const bool intra = t.flags & hevc::kTuIntra;
   const bool coef = t.flags & hevc::kTuCoef;
   const bool tskip = t.flags & hevc::kTuSkip;
+  const bool bypass = t.flags & hevc::kTuBypass;  // lossless CU: the coefficients are the residual
   const bool dst = t.flags & hevc::kTuDst;
   const i16* dq = d.coefs + t.data;
   if (intra)  // (uniform per block)
     prepare_refs_par(plane, stride, step, t.x, t.y, log2, t.c == 0, t.avail, t.mode, (t.flags & hevc::kTuStrong) != 0,
                      sbuf, sav, sref, top, left);
   const int mx = t.ext_x, my = t.ext_y;
-  if (coef && !tskip)
+  if (coef && !tskip && !bypass)
     for (int s = tid; s < n * (mx + 1); s += 256) {
       const int yy = s / (mx + 1), xx = s - yy * (mx + 1);
       g[yy * n + xx] = hevc::hk_itx_col(dq, log2, dst, yy, xx, my);
@@ -220,7 +226,7 @@ __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict
     const int yy = s >> log2, xx = s & (n - 1);
     u8& q = plane[(t.y + yy) * stride + (t.x + xx) * step];
     int v = intra ? int(hevc::hk_intra_sample(top, left, log2, t.mode, t.c == 0, xx, yy)) : int(q);
-    if (coef) v += tskip ? hevc::hk_tskip(dq[s]) : hevc::hk_itx_row(&g[yy * n], log2, dst, xx, mx);
+    if (coef) v += bypass ? int(dq[s]) : (tskip ? hevc::hk_tskip(dq[s]) : hevc::hk_itx_row(&g[yy * n], log2, dst, xx, mx));
     q = hevc::hk_clip8(v);
   }
 }
@@ -298,7 +304,9 @@ __global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restric
     const int pw = d.width >> sub, ph = d.height >> sub;
     auto nb_ok = [&](int nx, int ny) {
       if (nx < 0 || ny < 0 || nx >= pw || ny >= ph) return false;
-      const int nsi = d.ctb_slice[((ny << sub) >> d.log2ctb) * d.wctb + ((nx << sub) >> d.log2ctb)];
+      const int nci = ((ny << sub) >> d.log2ctb) * d.wctb + ((nx << sub) >> d.log2ctb);
+      if ((d.flags & 8) && d.ctb_tile[nci] != d.ctb_tile[ci]) return false;
+      const int nsi = d.ctb_slice[nci];
       if (nsi == si) return true;
       return nsi > si ? slices[nsi].across != 0 : sl.across != 0;
     };

@@ -1,6 +1,9 @@
 // H.265 parameter sets / slice segment header: parsers, writers and the hvcC record. See hevc.h.
 #include "hevc.h"
 
+#include <algorithm>
+#include <cstring>
+
 namespace vep::hevc {
 
 namespace {
@@ -41,17 +44,103 @@ void write_ptl(BitWriter& bw, const ProfileTierLevel& p) {
   bw.u(8, u32(p.level_idc));
 }
 
-void skip_scaling_list_data(BitReader& br) {
+// Table 7-6: default 8x8 (and up-sampled 16x16 / 32x32) lists, up-right diagonal order.
+constexpr u8 kSlIntra[64] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 16, 17, 16, 17, 18, 17, 18, 18, 17, 18, 21,
+                             19, 20, 21, 20, 19, 21, 24, 22, 22, 24, 24, 22, 22, 24, 25, 25, 27, 30, 27, 25, 25, 29,
+                             31, 35, 35, 31, 29, 36, 41, 44, 41, 36, 47, 54, 54, 47, 65, 70, 65, 88, 88, 115};
+constexpr u8 kSlInter[64] = {16, 16, 16, 16, 16, 16, 16, 16, 16, 16, 17, 17, 17, 17, 17, 18, 18, 18, 18, 18, 18, 20,
+                             20, 20, 20, 20, 20, 20, 24, 24, 24, 24, 24, 24, 24, 24, 25, 25, 25, 25, 25, 25, 25, 28,
+                             28, 28, 28, 28, 28, 33, 33, 33, 33, 33, 41, 41, 41, 41, 54, 54, 54, 71, 71, 91};
+
+void set_default_list(ScalingList& sl, int size_id, int matrix_id) {
+  for (int i = 0; i < 64; ++i)
+    sl.list[size_id][matrix_id][i] = size_id == 0 ? 16 : (matrix_id < 3 ? kSlIntra[i] : kSlInter[i]);
+  sl.dc[size_id][matrix_id] = 16;
+}
+
+// §7.3.4 (matrixId numbering of the range extensions: sizeId 3 uses 0 and 3)
+void parse_scaling_list_data(BitReader& br, ScalingList& sl) {
   for (int size_id = 0; size_id < 4; ++size_id) {
-    for (int matrix_id = 0; matrix_id < 6; matrix_id += (size_id == 3) ? 3 : 1) {
-      if (!br.u1()) {
-        br.ue();  // scaling_list_pred_matrix_id_delta
+    const int step = size_id == 3 ? 3 : 1;
+    for (int matrix_id = 0; matrix_id < 6; matrix_id += step) {
+      if (!br.u1()) {  // scaling_list_pred_mode_flag
+        const int delta = int(br.ue());
+        if (delta == 0) {
+          set_default_list(sl, size_id, matrix_id);
+        } else {
+          const int ref = matrix_id - delta * step;
+          VEP_CHECK(ref >= 0, "bad scaling_list_pred_matrix_id_delta");
+          std::memcpy(sl.list[size_id][matrix_id], sl.list[size_id][ref], 64);
+          sl.dc[size_id][matrix_id] = sl.dc[size_id][ref];
+        }
       } else {
-        const int coef_num = std::min(64, 1 << (4 + (size_id << 1)));
-        if (size_id > 1) br.se();
-        for (int i = 0; i < coef_num; ++i) br.se();
+        int next = 8;
+        const int num = std::min(64, 1 << (4 + (size_id << 1)));
+        if (size_id > 1) {
+          const int dc = br.se() + 8;
+          VEP_CHECK(dc >= 1 && dc <= 255, "bad scaling_list_dc_coef_minus8");
+          next = dc;
+          sl.dc[size_id][matrix_id] = u8(dc);
+        }
+        for (int i = 0; i < num; ++i) {
+          const int delta = br.se();
+          VEP_CHECK(delta >= -128 && delta <= 127, "bad scaling_list_delta_coef");
+          next = (next + delta + 256) % 256;
+          VEP_CHECK(next > 0, "scaling list entry 0");
+          sl.list[size_id][matrix_id][i] = u8(next);
+        }
       }
     }
+  }
+  for (int m = 0; m < 6; ++m)  // (4:2:0 never uses the 32x32 chroma matrices: keep them defined)
+    if (m % 3) {
+      std::memcpy(sl.list[3][m], sl.list[2][m], 64);
+      sl.dc[3][m] = sl.dc[2][m];
+    }
+}
+
+// Writes every list explicitly (pred_mode_flag 1), or as "default" when it is the default.
+void write_scaling_list_data(BitWriter& bw, const ScalingList& sl) {
+  ScalingList def;
+  for (int size_id = 0; size_id < 4; ++size_id) {
+    const int step = size_id == 3 ? 3 : 1;
+    for (int matrix_id = 0; matrix_id < 6; matrix_id += step) {
+      const int num = std::min(64, 1 << (4 + (size_id << 1)));
+      const bool is_def = std::memcmp(sl.list[size_id][matrix_id], def.list[size_id][matrix_id], size_t(num)) == 0 &&
+                          (size_id < 2 || sl.dc[size_id][matrix_id] == 16);
+      if (is_def) {
+        bw.u1(0);
+        bw.ue(0);
+        continue;
+      }
+      bw.u1(1);
+      int next = 8;
+      if (size_id > 1) {
+        bw.se(sl.dc[size_id][matrix_id] - 8);
+        next = sl.dc[size_id][matrix_id];
+      }
+      for (int i = 0; i < num; ++i) {
+        int d = int(sl.list[size_id][matrix_id][i]) - next;
+        if (d > 127) d -= 256;
+        if (d < -128) d += 256;
+        bw.se(d);
+        next = sl.list[size_id][matrix_id][i];
+      }
+    }
+  }
+}
+
+// Up-right diagonal scan of a blk x blk block (§6.5.3): (x, y) of scan position i.
+void diag_scan(int blk, int* xs, int* ys) {
+  int i = 0, x = 0, y = 0;
+  while (i < blk * blk) {
+    while (y >= 0) {
+      if (x < blk && y < blk) xs[i] = x, ys[i] = y, ++i;
+      --y;
+      ++x;
+    }
+    y = x;
+    x = 0;
   }
 }
 
@@ -139,12 +228,107 @@ void write_st_rps(BitWriter& bw, int idx, const ShortTermRps& r) {
   }
 }
 
+void parse_pred_weights(BitReader& br, SliceHeader& sh) {
+  PredWeights& w = sh.pwt;
+  w = PredWeights{};
+  w.luma_log2_denom = int(br.ue());
+  VEP_CHECK(w.luma_log2_denom <= 7, "bad luma_log2_weight_denom");
+  w.chroma_log2_denom = w.luma_log2_denom + br.se();
+  VEP_CHECK(w.chroma_log2_denom >= 0 && w.chroma_log2_denom <= 7, "bad delta_chroma_log2_weight_denom");
+  for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
+    const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+    for (int i = 0; i < nref; ++i) w.luma_flag[l][i] = br.u1();
+    for (int i = 0; i < nref; ++i) w.chroma_flag[l][i] = br.u1();
+    for (int i = 0; i < nref; ++i) {
+      w.w[l][i][0] = 1 << w.luma_log2_denom;
+      w.o[l][i][0] = 0;
+      if (w.luma_flag[l][i]) {
+        const int dw = br.se(), off = br.se();
+        VEP_CHECK(dw >= -128 && dw <= 127 && off >= -128 && off <= 127, "bad luma weight / offset");
+        w.w[l][i][0] += dw;
+        w.o[l][i][0] = off;
+      }
+      for (int c = 1; c <= 2; ++c) {
+        w.w[l][i][c] = 1 << w.chroma_log2_denom;
+        w.o[l][i][c] = 0;
+        if (w.chroma_flag[l][i]) {
+          const int dw = br.se(), doff = br.se();
+          VEP_CHECK(dw >= -128 && dw <= 127 && doff >= -512 && doff <= 511, "bad chroma weight / offset");
+          w.w[l][i][c] += dw;
+          w.o[l][i][c] = std::clamp(128 + doff - ((128 * w.w[l][i][c]) >> w.chroma_log2_denom), -128, 127);
+        }
+      }
+    }
+  }
+}
+
+void write_pred_weights(BitWriter& bw, const SliceHeader& sh) {
+  const PredWeights& w = sh.pwt;
+  bw.ue(u32(w.luma_log2_denom));
+  bw.se(w.chroma_log2_denom - w.luma_log2_denom);
+  for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
+    const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+    for (int i = 0; i < nref; ++i) bw.u1(w.luma_flag[l][i]);
+    for (int i = 0; i < nref; ++i) bw.u1(w.chroma_flag[l][i]);
+    for (int i = 0; i < nref; ++i) {
+      if (w.luma_flag[l][i]) {
+        bw.se(w.w[l][i][0] - (1 << w.luma_log2_denom));
+        bw.se(w.o[l][i][0]);
+      }
+      if (w.chroma_flag[l][i])
+        for (int c = 1; c <= 2; ++c) {
+          bw.se(w.w[l][i][c] - (1 << w.chroma_log2_denom));
+          const int doff = w.o[l][i][c] - 128 + ((128 * w.w[l][i][c]) >> w.chroma_log2_denom);
+          VEP_CHECK(doff >= -512 && doff <= 511, "chroma offset not codable with this weight");
+          bw.se(doff);
+        }
+    }
+  }
+}
+
 void check_nal(const u8* rbsp, size_t n, int want) {
   VEP_CHECK(n >= 3, "NAL too short");
   VEP_CHECK(nal_type(rbsp) == want, "unexpected HEVC NAL type");
 }
 
 }  // namespace
+
+void ScalingList::set_default() {
+  for (int size_id = 0; size_id < 4; ++size_id)
+    for (int m = 0; m < 6; ++m) set_default_list(*this, size_id, m);
+}
+
+bool ScalingList::operator==(const ScalingList& o) const {
+  return std::memcmp(list, o.list, sizeof list) == 0 && std::memcmp(dc, o.dc, sizeof dc) == 0;
+}
+
+void ScalingList::factors(int size_id, int matrix_id, u8* out) const {
+  const int n = 4 << size_id;
+  const int blk = size_id == 0 ? 4 : 8, rep = n / blk;
+  int xs[64], ys[64];
+  diag_scan(blk, xs, ys);
+  for (int i = 0; i < blk * blk; ++i)
+    for (int j = 0; j < rep; ++j)
+      for (int k = 0; k < rep; ++k) out[(ys[i] * rep + j) * n + xs[i] * rep + k] = list[size_id][matrix_id][i];
+  if (size_id >= 2) out[0] = dc[size_id][matrix_id];
+}
+
+void Pps::tile_bounds(int wctbs, int hctbs, std::vector<int>& col_bd, std::vector<int>& row_bd) const {
+  auto make = [&](int count, int total, const std::vector<int>& sizes, std::vector<int>& bd) {
+    bd.assign(size_t(count) + 1, 0);
+    for (int i = 0; i < count; ++i) {
+      int size;
+      if (!tiles || count == 1) size = total;
+      else if (uniform_spacing) size = ((i + 1) * total) / count - (i * total) / count;
+      else size = i < count - 1 ? sizes[size_t(i)] : total - bd[size_t(i)];
+      VEP_CHECK(size > 0, "HEVC: empty tile column / row");
+      bd[size_t(i) + 1] = bd[size_t(i)] + size;
+    }
+    VEP_CHECK(bd[size_t(count)] == total, "HEVC: tile sizes do not cover the picture");
+  };
+  make(tiles ? tile_cols : 1, wctbs, col_width, col_bd);
+  make(tiles ? tile_rows : 1, hctbs, row_height, row_bd);
+}
 
 std::vector<u8> nal_header(int type, int tid_plus1) {
   return {u8((type & 0x3f) << 1), u8(tid_plus1 & 7)};
@@ -219,7 +403,10 @@ Sps parse_sps(const u8* rbsp, size_t n) {
   s.max_th_depth_inter = int(br.ue());
   s.max_th_depth_intra = int(br.ue());
   s.scaling_list = br.u1();
-  if (s.scaling_list && br.u1()) skip_scaling_list_data(br);
+  if (s.scaling_list) {
+    s.scaling_list_data = br.u1();
+    if (s.scaling_list_data) parse_scaling_list_data(br, s.sl);
+  }
   s.amp = br.u1();
   s.sao = br.u1();
   s.pcm = br.u1();
@@ -237,7 +424,11 @@ Sps parse_sps(const u8* rbsp, size_t n) {
   s.long_term_refs = br.u1();
   if (s.long_term_refs) {
     s.num_long_term_ref_pics_sps = int(br.ue());
-    for (int i = 0; i < s.num_long_term_ref_pics_sps; ++i) br.skip(size_t(s.log2_max_poc_lsb) + 1);
+    VEP_CHECK(s.num_long_term_ref_pics_sps <= 32, "too many SPS long-term pictures");
+    for (int i = 0; i < s.num_long_term_ref_pics_sps; ++i) {
+      s.lt_poc_lsb_sps.push_back(int(br.u(s.log2_max_poc_lsb)));
+      s.lt_used_sps.push_back(br.u1());
+    }
   }
   s.temporal_mvp = br.u1();
   s.strong_intra_smoothing = br.u1();
@@ -302,12 +493,15 @@ Pps parse_pps(const u8* rbsp, size_t n) {
   p.tiles = br.u1();
   p.entropy_coding_sync = br.u1();
   if (p.tiles) {
-    const int cols = int(br.ue()) + 1, rows = int(br.ue()) + 1;
-    if (!br.u1()) {  // not uniform spacing
-      for (int i = 0; i < cols - 1; ++i) br.ue();
-      for (int i = 0; i < rows - 1; ++i) br.ue();
+    p.tile_cols = int(br.ue()) + 1;
+    p.tile_rows = int(br.ue()) + 1;
+    VEP_CHECK(p.tile_cols <= 64 && p.tile_rows <= 64, "too many tiles");
+    p.uniform_spacing = br.u1();
+    if (!p.uniform_spacing) {
+      for (int i = 0; i < p.tile_cols - 1; ++i) p.col_width.push_back(int(br.ue()) + 1);
+      for (int i = 0; i < p.tile_rows - 1; ++i) p.row_height.push_back(int(br.ue()) + 1);
     }
-    br.u1();  // loop_filter_across_tiles
+    p.loop_filter_across_tiles = br.u1();
   }
   p.loop_filter_across_slices = br.u1();
   p.deblocking_control = br.u1();
@@ -322,7 +516,7 @@ Pps parse_pps(const u8* rbsp, size_t n) {
     }
   }
   p.scaling_list = br.u1();
-  if (p.scaling_list) skip_scaling_list_data(br);
+  if (p.scaling_list) parse_scaling_list_data(br, p.sl);
   p.lists_modification = br.u1();
   p.log2_parallel_merge_level = int(br.ue()) + 2;
   p.slice_header_extension = br.u1();
@@ -337,7 +531,7 @@ int peek_slice_pps_id(const u8* rbsp, size_t n) {
   return int(br.ue());
 }
 
-SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const Pps& pps) {
+SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const Pps& pps, const SliceHeader* prev) {
   VEP_CHECK(n >= 3, "slice NAL too short");
   BitReader br(rbsp + 2, n - 2);
   SliceHeader sh;
@@ -351,111 +545,131 @@ SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const P
     sh.segment_address = int(br.u(ceil_log2(ctbs)));
     VEP_CHECK(sh.segment_address < ctbs, "slice_segment_address out of range");
   }
-  if (sh.dependent) throw Error("dependent slice segments are not supported");
-  br.skip(size_t(pps.num_extra_slice_header_bits));
-  sh.slice_type = int(br.ue());
-  VEP_CHECK(sh.slice_type <= 2, "bad slice_type");
-  if (pps.output_flag_present) br.u1();
-  if (sps.separate_colour_plane) br.skip(2);
-  int num_pic_total_curr = 0;
-  sh.deblocking_disabled = pps.deblocking_disabled;
-  if (!is_idr(sh.nal_type)) {
-    sh.poc_lsb = int(br.u(sps.log2_max_poc_lsb));
-    const int nsets = int(sps.st_rps.size());
-    ShortTermRps rps;
-    if (!br.u1()) {
-      rps = parse_st_rps(br, nsets, sps.st_rps);
-    } else {
-      VEP_CHECK(nsets > 0, "slice selects an SPS RPS but the SPS has none");
-      int idx = nsets > 1 ? int(br.u(ceil_log2(nsets))) : 0;
-      VEP_CHECK(idx < nsets, "short_term_ref_pic_set_idx out of range");
-      rps = sps.st_rps[size_t(idx)];
-    }
-    sh.rps = rps;
-    for (int i = 0; i < rps.num_delta(); ++i) num_pic_total_curr += rps.used[i];
-    if (sps.long_term_refs) {
-      int num_lt_sps = 0;
-      if (sps.num_long_term_ref_pics_sps > 0) num_lt_sps = int(br.ue());
-      const int num_lt = num_lt_sps + int(br.ue());
-      sh.num_long_term = num_lt;
-      for (int i = 0; i < num_lt; ++i) {
-        bool used;
-        if (i < num_lt_sps) {
-          if (sps.num_long_term_ref_pics_sps > 1) br.skip(size_t(ceil_log2(sps.num_long_term_ref_pics_sps)));
-          used = true;  // (per-SPS flag; counted conservatively)
-        } else {
-          br.skip(size_t(sps.log2_max_poc_lsb));
-          used = br.u1();
+  if (sh.dependent) {  // every slice-level field comes from the slice's independent segment
+    VEP_CHECK(prev != nullptr, "dependent slice segment without a preceding slice segment");
+    SliceHeader d = *prev;
+    d.nal_type = sh.nal_type;
+    d.first_slice_in_pic = false;
+    d.pps_id = sh.pps_id;
+    d.dependent = true;
+    d.segment_address = sh.segment_address;
+    d.num_entry_points = 0;
+    d.entry_points.clear();
+    sh = std::move(d);
+  } else {
+    br.skip(size_t(pps.num_extra_slice_header_bits));
+    sh.slice_type = int(br.ue());
+    VEP_CHECK(sh.slice_type <= 2, "bad slice_type");
+    if (pps.output_flag_present) br.u1();
+    if (sps.separate_colour_plane) br.skip(2);
+    int num_pic_total_curr = 0;
+    sh.deblocking_disabled = pps.deblocking_disabled;
+    if (!is_idr(sh.nal_type)) {
+      sh.poc_lsb = int(br.u(sps.log2_max_poc_lsb));
+      const int nsets = int(sps.st_rps.size());
+      ShortTermRps rps;
+      if (!br.u1()) {
+        rps = parse_st_rps(br, nsets, sps.st_rps);
+      } else {
+        VEP_CHECK(nsets > 0, "slice selects an SPS RPS but the SPS has none");
+        int idx = nsets > 1 ? int(br.u(ceil_log2(nsets))) : 0;
+        VEP_CHECK(idx < nsets, "short_term_ref_pic_set_idx out of range");
+        rps = sps.st_rps[size_t(idx)];
+        sh.short_term_rps_idx = idx;
+      }
+      sh.rps = rps;
+      for (int i = 0; i < rps.num_delta(); ++i) num_pic_total_curr += rps.used[i];
+      if (sps.long_term_refs) {  // §7.3.6.1 long-term entries, §7.4.7.1 derivations
+        if (sps.num_long_term_ref_pics_sps > 0) sh.num_long_term_sps = int(br.ue());
+        VEP_CHECK(sh.num_long_term_sps <= sps.num_long_term_ref_pics_sps, "num_long_term_sps out of range");
+        sh.num_long_term = sh.num_long_term_sps + int(br.ue());
+        VEP_CHECK(sh.num_long_term + rps.num_delta() <= 32, "too many reference pictures");
+        for (int i = 0; i < sh.num_long_term; ++i) {
+          if (i < sh.num_long_term_sps) {
+            int idx = 0;
+            if (sps.num_long_term_ref_pics_sps > 1) idx = int(br.u(ceil_log2(sps.num_long_term_ref_pics_sps)));
+            VEP_CHECK(idx < sps.num_long_term_ref_pics_sps, "lt_idx_sps out of range");
+            sh.lt_idx_sps[i] = idx;
+            sh.lt_poc_lsb[i] = sps.lt_poc_lsb_sps[size_t(idx)];
+            sh.lt_used[i] = sps.lt_used_sps[size_t(idx)];
+          } else {
+            sh.lt_poc_lsb[i] = int(br.u(sps.log2_max_poc_lsb));
+            sh.lt_used[i] = br.u1();
+          }
+          sh.lt_msb_present[i] = br.u1();
+          const int cycle = sh.lt_msb_present[i] ? int(br.ue()) : 0;
+          sh.lt_msb_cycle[i] = (i == 0 || i == sh.num_long_term_sps) ? cycle : cycle + sh.lt_msb_cycle[i - 1];
+          num_pic_total_curr += sh.lt_used[i];
         }
-        if (br.u1()) br.ue();  // delta_poc_msb_cycle_lt
-        num_pic_total_curr += used;
+      }
+      if (sps.temporal_mvp) sh.temporal_mvp = br.u1();
+    }
+    sh.num_pic_total_curr = num_pic_total_curr;
+    if (sps.sao) {
+      sh.sao_luma = br.u1();
+      if (sps.chroma_format_idc != 0) sh.sao_chroma = br.u1();
+    }
+    if (sh.slice_type != kI) {
+      sh.num_ref_idx_l0 = pps.num_ref_idx_l0_default;
+      int l1 = pps.num_ref_idx_l1_default;
+      if (br.u1()) {
+        sh.num_ref_idx_l0 = int(br.ue()) + 1;
+        if (sh.slice_type == kB) l1 = int(br.ue()) + 1;
+      }
+      VEP_CHECK(sh.num_ref_idx_l0 <= 15 && l1 <= 15, "num_ref_idx out of range");
+      sh.num_ref_idx_l1 = sh.slice_type == kB ? l1 : 0;
+      if (pps.lists_modification && num_pic_total_curr > 1) {
+        const int bits = ceil_log2(num_pic_total_curr);
+        sh.list_mod[0] = br.u1();
+        if (sh.list_mod[0])
+          for (int i = 0; i < sh.num_ref_idx_l0; ++i) sh.list_entry[0][i] = int(br.u(bits));
+        if (sh.slice_type == kB) {
+          sh.list_mod[1] = br.u1();
+          if (sh.list_mod[1])
+            for (int i = 0; i < l1; ++i) sh.list_entry[1][i] = int(br.u(bits));
+        }
+      }
+      if (sh.slice_type == kB) sh.mvd_l1_zero = br.u1();
+      if (pps.cabac_init_present) sh.cabac_init = br.u1();
+      if (sh.temporal_mvp) {
+        bool from_l0 = true;
+        if (sh.slice_type == kB) from_l0 = br.u1();
+        sh.collocated_from_l0 = from_l0;
+        if ((from_l0 && sh.num_ref_idx_l0 > 1) || (!from_l0 && l1 > 1)) sh.collocated_ref_idx = int(br.ue());
+        VEP_CHECK(sh.collocated_ref_idx < (from_l0 ? sh.num_ref_idx_l0 : l1), "collocated_ref_idx out of range");
+      }
+      sh.weighted = (pps.weighted_pred && sh.slice_type == kP) || (pps.weighted_bipred && sh.slice_type == kB);
+      if (sh.weighted) parse_pred_weights(br, sh);
+      sh.max_num_merge_cand = 5 - int(br.ue());
+      VEP_CHECK(sh.max_num_merge_cand >= 1 && sh.max_num_merge_cand <= 5, "bad merge candidates");
+    }
+    sh.qp_delta = br.se();
+    if (pps.slice_chroma_qp_offsets_present) {
+      sh.cb_qp_offset = br.se();
+      sh.cr_qp_offset = br.se();
+    }
+    sh.beta_offset = pps.beta_offset;
+    sh.tc_offset = pps.tc_offset;
+    bool override_flag = false;
+    if (pps.deblocking_override_enabled) override_flag = br.u1();
+    if (override_flag) {
+      sh.deblocking_disabled = br.u1();
+      if (!sh.deblocking_disabled) {
+        sh.beta_offset = br.se() * 2;
+        sh.tc_offset = br.se() * 2;
       }
     }
-    if (sps.temporal_mvp) sh.temporal_mvp = br.u1();
+    sh.loop_filter_across_slices = pps.loop_filter_across_slices;
+    if (pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled))
+      sh.loop_filter_across_slices = br.u1();
   }
-  if (sps.sao) {
-    sh.sao_luma = br.u1();
-    if (sps.chroma_format_idc != 0) sh.sao_chroma = br.u1();
-  }
-  if (sh.slice_type != kI) {
-    sh.num_ref_idx_l0 = pps.num_ref_idx_l0_default;
-    int l1 = pps.num_ref_idx_l1_default;
-    if (br.u1()) {
-      sh.num_ref_idx_l0 = int(br.ue()) + 1;
-      if (sh.slice_type == kB) l1 = int(br.ue()) + 1;
-    }
-    VEP_CHECK(sh.num_ref_idx_l0 <= 15 && l1 <= 15, "num_ref_idx out of range");
-    sh.num_ref_idx_l1 = sh.slice_type == kB ? l1 : 0;
-    if (pps.lists_modification && num_pic_total_curr > 1) {
-      const int bits = ceil_log2(num_pic_total_curr);
-      sh.list_mod[0] = br.u1();
-      if (sh.list_mod[0])
-        for (int i = 0; i < sh.num_ref_idx_l0; ++i) sh.list_entry[0][i] = int(br.u(bits));
-      if (sh.slice_type == kB) {
-        sh.list_mod[1] = br.u1();
-        if (sh.list_mod[1])
-          for (int i = 0; i < l1; ++i) sh.list_entry[1][i] = int(br.u(bits));
-      }
-    }
-    if (sh.slice_type == kB) sh.mvd_l1_zero = br.u1();
-    if (pps.cabac_init_present) sh.cabac_init = br.u1();
-    if (sh.temporal_mvp) {
-      bool from_l0 = true;
-      if (sh.slice_type == kB) from_l0 = br.u1();
-      sh.collocated_from_l0 = from_l0;
-      if ((from_l0 && sh.num_ref_idx_l0 > 1) || (!from_l0 && l1 > 1)) sh.collocated_ref_idx = int(br.ue());
-      VEP_CHECK(sh.collocated_ref_idx < (from_l0 ? sh.num_ref_idx_l0 : l1), "collocated_ref_idx out of range");
-    }
-    if ((pps.weighted_pred && sh.slice_type == kP) || (pps.weighted_bipred && sh.slice_type == kB))
-      throw Error("weighted prediction is not supported");
-    sh.max_num_merge_cand = 5 - int(br.ue());
-    VEP_CHECK(sh.max_num_merge_cand >= 1 && sh.max_num_merge_cand <= 5, "bad merge candidates");
-  }
-  sh.qp_delta = br.se();
-  if (pps.slice_chroma_qp_offsets_present) {
-    sh.cb_qp_offset = br.se();
-    sh.cr_qp_offset = br.se();
-  }
-  sh.beta_offset = pps.beta_offset;
-  sh.tc_offset = pps.tc_offset;
-  bool override_flag = false;
-  if (pps.deblocking_override_enabled) override_flag = br.u1();
-  if (override_flag) {
-    sh.deblocking_disabled = br.u1();
-    if (!sh.deblocking_disabled) {
-      sh.beta_offset = br.se() * 2;
-      sh.tc_offset = br.se() * 2;
-    }
-  }
-  sh.loop_filter_across_slices = pps.loop_filter_across_slices;
-  if (pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled))
-    sh.loop_filter_across_slices = br.u1();
   if (pps.tiles || pps.entropy_coding_sync) {
     sh.num_entry_points = int(br.ue());
+    VEP_CHECK(sh.num_entry_points <= 4096, "too many entry points");
     if (sh.num_entry_points > 0) {
       const int len = int(br.ue()) + 1;
       VEP_CHECK(len <= 32, "bad entry point offset length");
-      for (int i = 0; i < sh.num_entry_points; ++i) br.skip(size_t(len));
+      for (int i = 0; i < sh.num_entry_points; ++i) sh.entry_points.push_back(br.u(len) + 1);
     }
   }
   if (pps.slice_header_extension) {
@@ -529,7 +743,11 @@ std::vector<u8> write_sps(const Sps& s) {
   bw.ue(u32(s.log2_max_tb - s.log2_min_tb));
   bw.ue(u32(s.max_th_depth_inter));
   bw.ue(u32(s.max_th_depth_intra));
-  bw.u1(0);  // scaling_list_enabled
+  bw.u1(s.scaling_list);
+  if (s.scaling_list) {
+    bw.u1(s.scaling_list_data);
+    if (s.scaling_list_data) write_scaling_list_data(bw, s.sl);
+  }
   bw.u1(s.amp);
   bw.u1(s.sao);
   bw.u1(s.pcm);
@@ -542,7 +760,14 @@ std::vector<u8> write_sps(const Sps& s) {
   }
   bw.ue(u32(s.st_rps.size()));
   for (size_t i = 0; i < s.st_rps.size(); ++i) write_st_rps(bw, int(i), s.st_rps[i]);
-  bw.u1(0);  // long_term_ref_pics_present
+  bw.u1(s.long_term_refs);
+  if (s.long_term_refs) {
+    bw.ue(u32(s.lt_poc_lsb_sps.size()));
+    for (size_t i = 0; i < s.lt_poc_lsb_sps.size(); ++i) {
+      bw.u(s.log2_max_poc_lsb, u32(s.lt_poc_lsb_sps[i]));
+      bw.u1(s.lt_used_sps[i]);
+    }
+  }
   bw.u1(s.temporal_mvp);
   bw.u1(s.strong_intra_smoothing);
   bw.u1(s.vui);
@@ -580,7 +805,7 @@ std::vector<u8> write_pps(const Pps& p) {
   for (u8 b : nal_header(kPps)) bw.u(8, b);
   bw.ue(u32(p.pps_id));
   bw.ue(u32(p.sps_id));
-  bw.u1(0);  // dependent_slice_segments
+  bw.u1(p.dependent_slice_segments);
   bw.u1(0);  // output_flag_present
   bw.u(3, 0);
   bw.u1(p.sign_data_hiding);
@@ -595,11 +820,21 @@ std::vector<u8> write_pps(const Pps& p) {
   bw.se(p.cb_qp_offset);
   bw.se(p.cr_qp_offset);
   bw.u1(p.slice_chroma_qp_offsets_present);
-  bw.u1(0);  // weighted_pred
-  bw.u1(0);  // weighted_bipred
-  bw.u1(0);  // transquant_bypass
-  bw.u1(0);  // tiles
-  bw.u1(0);  // entropy_coding_sync
+  bw.u1(p.weighted_pred);
+  bw.u1(p.weighted_bipred);
+  bw.u1(p.transquant_bypass);
+  bw.u1(p.tiles);
+  bw.u1(p.entropy_coding_sync);
+  if (p.tiles) {
+    bw.ue(u32(p.tile_cols - 1));
+    bw.ue(u32(p.tile_rows - 1));
+    bw.u1(p.uniform_spacing);
+    if (!p.uniform_spacing) {
+      for (int i = 0; i < p.tile_cols - 1; ++i) bw.ue(u32(p.col_width[size_t(i)] - 1));
+      for (int i = 0; i < p.tile_rows - 1; ++i) bw.ue(u32(p.row_height[size_t(i)] - 1));
+    }
+    bw.u1(p.loop_filter_across_tiles);
+  }
   bw.u1(p.loop_filter_across_slices);
   bw.u1(1);  // deblocking_filter_control_present
   bw.u1(p.deblocking_override_enabled);
@@ -608,7 +843,8 @@ std::vector<u8> write_pps(const Pps& p) {
     bw.se(p.beta_offset / 2);
     bw.se(p.tc_offset / 2);
   }
-  bw.u1(0);  // pps_scaling_list_data_present
+  bw.u1(p.scaling_list);
+  if (p.scaling_list) write_scaling_list_data(bw, p.sl);
   bw.u1(0);  // lists_modification_present
   bw.ue(u32(p.log2_parallel_merge_level - 2));
   bw.u1(0);  // slice_segment_header_extension_present
@@ -651,56 +887,91 @@ void write_slice_header_full(BitWriter& bw, const SliceHeader& sh, const Sps& sp
   bw.u1(sh.first_slice_in_pic);
   if (is_irap(sh.nal_type)) bw.u1(sh.no_output_of_prior_pics);
   bw.ue(u32(sh.pps_id));
-  if (!sh.first_slice_in_pic)
+  if (!sh.first_slice_in_pic) {
+    if (pps.dependent_slice_segments) bw.u1(sh.dependent);
     bw.u(ceil_log2(sps.width_ctbs() * sps.height_ctbs()), u32(sh.segment_address));
-  bw.ue(u32(sh.slice_type));
-  if (!is_idr(sh.nal_type)) {
-    bw.u(sps.log2_max_poc_lsb, u32(sh.poc_lsb) & ((1u << sps.log2_max_poc_lsb) - 1));
-    bw.u1(0);  // short_term_ref_pic_set_sps_flag: the RPS is coded in the header
-    write_st_rps(bw, int(sps.st_rps.size()), sh.rps);
-    if (sps.temporal_mvp) bw.u1(sh.temporal_mvp);
   }
-  if (sps.sao) {
-    bw.u1(sh.sao_luma);
-    bw.u1(sh.sao_chroma);
-  }
-  if (sh.slice_type != kI) {
-    const bool override_refs = sh.num_ref_idx_l0 != pps.num_ref_idx_l0_default ||
-                               (sh.slice_type == kB && sh.num_ref_idx_l1 != pps.num_ref_idx_l1_default);
-    bw.u1(override_refs);
-    if (override_refs) {
-      bw.ue(u32(sh.num_ref_idx_l0 - 1));
-      if (sh.slice_type == kB) bw.ue(u32(sh.num_ref_idx_l1 - 1));
+  if (!sh.dependent) {
+    bw.ue(u32(sh.slice_type));
+    if (!is_idr(sh.nal_type)) {
+      bw.u(sps.log2_max_poc_lsb, u32(sh.poc_lsb) & ((1u << sps.log2_max_poc_lsb) - 1));
+      bw.u1(0);  // short_term_ref_pic_set_sps_flag: the RPS is coded in the header
+      write_st_rps(bw, int(sps.st_rps.size()), sh.rps);
+      if (sps.long_term_refs) {
+        if (sps.num_long_term_ref_pics_sps > 0) bw.ue(u32(sh.num_long_term_sps));
+        bw.ue(u32(sh.num_long_term - sh.num_long_term_sps));
+        for (int i = 0; i < sh.num_long_term; ++i) {
+          if (i < sh.num_long_term_sps) {
+            if (sps.num_long_term_ref_pics_sps > 1)
+              bw.u(ceil_log2(sps.num_long_term_ref_pics_sps), u32(sh.lt_idx_sps[i]));
+          } else {
+            bw.u(sps.log2_max_poc_lsb, u32(sh.lt_poc_lsb[i]));
+            bw.u1(sh.lt_used[i]);
+          }
+          bw.u1(sh.lt_msb_present[i]);
+          if (sh.lt_msb_present[i]) {
+            const int prev = (i == 0 || i == sh.num_long_term_sps) ? 0 : sh.lt_msb_cycle[i - 1];
+            VEP_CHECK(sh.lt_msb_cycle[i] >= prev, "DeltaPocMsbCycleLt must not decrease");
+            bw.ue(u32(sh.lt_msb_cycle[i] - prev));
+          }
+        }
+      }
+      if (sps.temporal_mvp) bw.u1(sh.temporal_mvp);
     }
-    if (sh.slice_type == kB) bw.u1(sh.mvd_l1_zero);
-    if (pps.cabac_init_present) bw.u1(sh.cabac_init);
-    if (sh.temporal_mvp) {
-      if (sh.slice_type == kB) bw.u1(sh.collocated_from_l0);
-      const int n = sh.collocated_from_l0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
-      if (n > 1) bw.ue(u32(sh.collocated_ref_idx));
+    if (sps.sao) {
+      bw.u1(sh.sao_luma);
+      bw.u1(sh.sao_chroma);
     }
-    bw.ue(u32(5 - sh.max_num_merge_cand));
+    if (sh.slice_type != kI) {
+      const bool override_refs = sh.num_ref_idx_l0 != pps.num_ref_idx_l0_default ||
+                                 (sh.slice_type == kB && sh.num_ref_idx_l1 != pps.num_ref_idx_l1_default);
+      bw.u1(override_refs);
+      if (override_refs) {
+        bw.ue(u32(sh.num_ref_idx_l0 - 1));
+        if (sh.slice_type == kB) bw.ue(u32(sh.num_ref_idx_l1 - 1));
+      }
+      if (sh.slice_type == kB) bw.u1(sh.mvd_l1_zero);
+      if (pps.cabac_init_present) bw.u1(sh.cabac_init);
+      if (sh.temporal_mvp) {
+        if (sh.slice_type == kB) bw.u1(sh.collocated_from_l0);
+        const int n = sh.collocated_from_l0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+        if (n > 1) bw.ue(u32(sh.collocated_ref_idx));
+      }
+      if ((pps.weighted_pred && sh.slice_type == kP) || (pps.weighted_bipred && sh.slice_type == kB))
+        write_pred_weights(bw, sh);
+      bw.ue(u32(5 - sh.max_num_merge_cand));
+    }
+    bw.se(sh.qp_delta);
+    if (pps.slice_chroma_qp_offsets_present) {
+      bw.se(sh.cb_qp_offset);
+      bw.se(sh.cr_qp_offset);
+    }
+    bool override_flag = false;
+    if (pps.deblocking_override_enabled) {
+      override_flag = sh.deblocking_disabled != pps.deblocking_disabled || sh.beta_offset != pps.beta_offset ||
+                      sh.tc_offset != pps.tc_offset;
+      bw.u1(override_flag);
+    }
+    if (override_flag) {
+      bw.u1(sh.deblocking_disabled);
+      if (!sh.deblocking_disabled) {
+        bw.se(sh.beta_offset / 2);
+        bw.se(sh.tc_offset / 2);
+      }
+    }
+    if (pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled))
+      bw.u1(sh.loop_filter_across_slices);
   }
-  bw.se(sh.qp_delta);
-  if (pps.slice_chroma_qp_offsets_present) {
-    bw.se(sh.cb_qp_offset);
-    bw.se(sh.cr_qp_offset);
-  }
-  bool override_flag = false;
-  if (pps.deblocking_override_enabled) {
-    override_flag = sh.deblocking_disabled != pps.deblocking_disabled || sh.beta_offset != pps.beta_offset ||
-                    sh.tc_offset != pps.tc_offset;
-    bw.u1(override_flag);
-  }
-  if (override_flag) {
-    bw.u1(sh.deblocking_disabled);
-    if (!sh.deblocking_disabled) {
-      bw.se(sh.beta_offset / 2);
-      bw.se(sh.tc_offset / 2);
+  if (pps.tiles || pps.entropy_coding_sync) {
+    bw.ue(u32(sh.entry_points.size()));
+    if (!sh.entry_points.empty()) {
+      u32 mx = 1;
+      for (u32 e : sh.entry_points) mx = std::max(mx, e - 1);
+      const int len = std::max(1, 32 - __builtin_clz(mx));
+      bw.ue(u32(len - 1));
+      for (u32 e : sh.entry_points) bw.u(len, e - 1);
     }
   }
-  if (pps.loop_filter_across_slices && (sh.sao_luma || sh.sao_chroma || !sh.deblocking_disabled))
-    bw.u1(sh.loop_filter_across_slices);
   bw.u1(1);  // byte_alignment()
   bw.align_zero();
 }

@@ -53,6 +53,18 @@ struct ShortTermRps {
   int num_delta() const { return num_negative + num_positive; }
 };
 
+// Scaling lists (§7.3.4 scaling_list_data, §7.4.5): the coded lists in up-right diagonal order.
+// matrixId 0..2 intra Y / Cb / Cr, 3..5 inter; sizeId 3 (32x32) uses matrixId 0 and 3 only.
+struct ScalingList {
+  u8 list[4][6][64] = {};
+  u8 dc[4][6] = {};  // sizeId 2, 3: scaling_list_dc_coef_minus8 + 8
+  ScalingList() { set_default(); }
+  void set_default();  // Table 7-5 / 7-6 (flat 16 for 4x4)
+  // ScalingFactor m of an n x n block (n = 4 << size_id), raster: out[y * n + x] = m[x][y].
+  void factors(int size_id, int matrix_id, u8* out) const;
+  bool operator==(const ScalingList& o) const;
+};
+
 struct Vps {
   int vps_id = 0;
   int max_sub_layers = 1;
@@ -75,6 +87,8 @@ struct Sps {
   int log2_min_tb = 2, log2_max_tb = 4;
   int max_th_depth_inter = 0, max_th_depth_intra = 0;
   bool scaling_list = false, amp = false, sao = false;
+  bool scaling_list_data = false;  // sps_scaling_list_data_present_flag (else the default lists)
+  ScalingList sl;
   bool pcm = true;
   int pcm_bit_depth_luma = 8, pcm_bit_depth_chroma = 8;
   int log2_min_pcm = 4, log2_max_pcm = 4;
@@ -82,6 +96,8 @@ struct Sps {
   std::vector<ShortTermRps> st_rps;
   bool long_term_refs = false;
   int num_long_term_ref_pics_sps = 0;
+  std::vector<int> lt_poc_lsb_sps;    // lt_ref_pic_poc_lsb_sps[]
+  std::vector<bool> lt_used_sps;      // used_by_curr_pic_lt_sps_flag[]
   bool temporal_mvp = false, strong_intra_smoothing = false;
   bool vui = false, video_signal_type = false;
   int video_format = 5, matrix_coeffs = 6;
@@ -113,11 +129,27 @@ struct Pps {
   bool slice_chroma_qp_offsets_present = false;
   bool weighted_pred = false, weighted_bipred = false, transquant_bypass = false;
   bool tiles = false, entropy_coding_sync = false;
+  int tile_cols = 1, tile_rows = 1;   // num_tile_{columns,rows}_minus1 + 1
+  bool uniform_spacing = true;
+  std::vector<int> col_width, row_height;  // explicit spacing: column_width_minus1 + 1 (cols - 1 entries)
+  bool loop_filter_across_tiles = true;
   bool loop_filter_across_slices = false;
   bool deblocking_control = true, deblocking_override_enabled = false, deblocking_disabled = true;
-  bool scaling_list = false, lists_modification = false;
+  bool scaling_list = false, lists_modification = false;  // scaling_list: pps_scaling_list_data_present
+  ScalingList sl;
   int log2_parallel_merge_level = 2;
   bool slice_header_extension = false;
+  // Tile column / row boundaries in CTBs (§6.5.1, size cols + 1 / rows + 1).
+  void tile_bounds(int wctbs, int hctbs, std::vector<int>& col_bd, std::vector<int>& row_bd) const;
+};
+
+// pred_weight_table (§7.3.6.3) with the derived weights / offsets (§7.4.7.3) per list and
+// reference index: [list][ref][0 luma, 1 Cb, 2 Cr].
+struct PredWeights {
+  int luma_log2_denom = 0, chroma_log2_denom = 0;
+  bool luma_flag[2][16] = {}, chroma_flag[2][16] = {};
+  int w[2][16][3] = {}, o[2][16][3] = {};
+  int log2_denom(int c) const { return c ? chroma_log2_denom : luma_log2_denom; }
 };
 
 enum SliceType : int { kB = 0, kP = 1, kI = 2 };
@@ -132,7 +164,17 @@ struct SliceHeader {
   int slice_type = kI;
   int poc_lsb = 0;
   ShortTermRps rps;                          // the picture's short-term RPS (non-IDR)
-  int num_long_term = 0;                     // long-term entries (rejected by the decoder)
+  int short_term_rps_idx = -1;               // -1: coded in the header, else the SPS set used
+  // long-term entries (§7.3.6.1, derived per §7.4.7.1): num_long_term_sps come first
+  int num_long_term = 0, num_long_term_sps = 0;
+  int lt_idx_sps[32] = {};
+  int lt_poc_lsb[32] = {};                   // PocLsbLt
+  bool lt_used[32] = {};                     // UsedByCurrPicLt
+  bool lt_msb_present[32] = {};              // delta_poc_msb_present_flag
+  int lt_msb_cycle[32] = {};                 // DeltaPocMsbCycleLt (accumulated)
+  int num_pic_total_curr = 0;
+  bool weighted = false;                     // explicit weighted prediction in this slice
+  PredWeights pwt;
   int num_ref_idx_l0 = 1, num_ref_idx_l1 = 1;
   bool list_mod[2] = {false, false};
   int list_entry[2][16] = {};                // ref_pic_list_modification entries
@@ -149,6 +191,7 @@ struct SliceHeader {
   bool sao_luma = false, sao_chroma = false;
   bool temporal_mvp = false;
   int num_entry_points = 0;
+  std::vector<u32> entry_points;             // entry_point_offset_minus1 + 1 (bytes incl. emulation prevention)
   size_t data_bytepos = 0;                   // slice_segment_data() start within the RBSP
   char pict_char() const { return slice_type == kI ? 'I' : slice_type == kP ? 'P' : 'B'; }
 };
@@ -159,7 +202,10 @@ Sps parse_sps(const u8* rbsp, size_t n);
 Pps parse_pps(const u8* rbsp, size_t n);
 // pps_id of a slice segment (first fields of the header) without full parsing.
 int peek_slice_pps_id(const u8* rbsp, size_t n);
-SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const Pps& pps);
+// `prev`: the header of the picture's previous slice segment (a dependent slice segment takes
+// every slice-level field from it); may be null when the segment is independent.
+SliceHeader parse_slice_header(const u8* rbsp, size_t n, const Sps& sps, const Pps& pps,
+                               const SliceHeader* prev = nullptr);
 
 // Writers (RBSP including the NAL header) for the synthetic encoder.
 std::vector<u8> write_vps(const Vps& v);

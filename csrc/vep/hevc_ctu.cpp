@@ -10,6 +10,39 @@
 
 namespace vep::hevc {
 
+void PicCtx::init_tiles() {
+  pps->tile_bounds(wctb, hctb, col_bd, row_bd);
+  const size_t nctb = size_t(wctb) * size_t(hctb);
+  rs2ts.resize(nctb);
+  ts2rs.resize(nctb);
+  tile.resize(nctb);
+  const int tc = int(col_bd.size()) - 1, tr = int(row_bd.size()) - 1;
+  int ts = 0;
+  for (int ty = 0; ty < tr; ++ty)  // tiles in raster order, CTBs in raster order inside a tile
+    for (int tx = 0; tx < tc; ++tx)
+      for (int y = row_bd[size_t(ty)]; y < row_bd[size_t(ty) + 1]; ++y)
+        for (int x = col_bd[size_t(tx)]; x < col_bd[size_t(tx) + 1]; ++x) {
+          const int rs = y * wctb + x;
+          rs2ts[size_t(rs)] = ts;
+          ts2rs[size_t(ts)] = rs;
+          tile[size_t(rs)] = u16(ty * tc + tx);
+          ++ts;
+        }
+}
+
+void PicCtx::init_scaling() {
+  scaling = sps->scaling_list;
+  if (!scaling) return;
+  // PPS lists replace the SPS ones; an SPS without explicit data uses the default lists
+  const ScalingList& sl = pps->scaling_list ? pps->sl : sps->sl;
+  for (int size_id = 0; size_id < 4; ++size_id)
+    for (int m = 0; m < 6; ++m) {
+      const int n = 4 << size_id;
+      sf[size_id][m].resize(size_t(n) * n);
+      sl.factors(size_id, m, sf[size_id][m].data());
+    }
+}
+
 namespace {
 
 struct RD {
@@ -78,12 +111,21 @@ class CtuLayer {
     const int rx = addr % pc_.wctb, ry = addr / pc_.wctb;
     const int x0 = rx << sps_.log2_ctb, y0 = ry << sps_.log2_ctb;
     pc_.slice[size_t(addr)] = u16(si_);
+    pc_.sord[size_t(addr)] = u16(sl_.ord);
     if (sh_.sao_luma || sh_.sao_chroma) sao(rx, ry);
     quadtree(x0, y0, sps_.log2_ctb, 0);
     const u32 end = e_.term(last ? 1u : 0u);
     if constexpr (!kWrite) last_read_ = end != 0;
   }
   bool end_of_slice() const { return last_read_; }
+  // qPY_PREV: SliceQpY again for the next quantization group (first QG of a tile, or of a CTB
+  // row with WPP), or the QP of the previous segment's last CU (dependent slice segment)
+  void reset_qp_prediction() { first_qg_ = true; }
+  void continue_qp_prediction(int qp_last) {
+    first_qg_ = false;
+    qp_last_ = qp_last;
+  }
+  int qp_last() const { return qp_last_; }
 
  private:
   u32 bin(int ctx, u32 v) { return e_.bin(ctx, v); }
@@ -112,8 +154,11 @@ class CtuLayer {
     if constexpr (kWrite) dec_->sao(rx, ry, want, ml, mu);
     const int addr = ry * pc_.wctb + rx;
     bool merge_left = false, merge_up = false;
-    if (rx > 0 && pc_.slice[size_t(addr - 1)] == si_) merge_left = bin(kCtxSaoMerge, ml);
-    if (ry > 0 && !merge_left && pc_.slice[size_t(addr - pc_.wctb)] == si_) merge_up = bin(kCtxSaoMerge, mu);
+    // §7.3.8.3: the left / up CTB must be in the slice (address >= SliceAddrRs) and the tile
+    const auto same_tile = [&](int a) { return pc_.tile[size_t(a)] == pc_.tile[size_t(addr)]; };
+    if (rx > 0 && addr - 1 >= sl_.addr_rs && same_tile(addr - 1)) merge_left = bin(kCtxSaoMerge, ml);
+    if (ry > 0 && !merge_left && addr - pc_.wctb >= sl_.addr_rs && same_tile(addr - pc_.wctb))
+      merge_up = bin(kCtxSaoMerge, mu);
     SaoParams& p = pc_.sao[size_t(addr)];
     if (merge_left) {
       p = pc_.sao[size_t(addr - 1)];
@@ -240,6 +285,14 @@ class CtuLayer {
     // CU boundaries are transform and prediction block edges
     for4(x0, y0, 4, n, [=](size_t k) { m_edge[k] |= kEdgeTuV | kEdgePuV; });
     for4(x0, y0, n, 4, [=](size_t k) { m_edge[k] |= kEdgeTuH | kEdgePuH; });
+    cu_.bypass = false;
+    if (pps_.transquant_bypass) {
+      cu_.bypass = bin(kCtxTransquantBypass, want.bypass) != 0;
+      u8* const m_byp = pc_.bypass.data();
+      const u8 bv = u8(cu_.bypass);
+      for4(x0, y0, n, n, [=](size_t k) { m_byp[k] = bv; });
+      if (cu_.bypass) pc_.any_bypass = true;
+    }
     bool skip = false;
     if (sh_.slice_type != kI) {
       int inc = 0;
@@ -581,6 +634,27 @@ class CtuLayer {
     }
   }
 
+  // Records mode: index + 1 of the explicit weighting of a PU in the picture's weight table
+  // (entries are shared by every PU with the same weights / offsets / shifts).
+  u8 gpu_wp_index(const MvField& m) {
+    GpuWp e{};
+    const PredWeights& w = sh_.pwt;
+    for (int c = 0; c < 3; ++c) {
+      e.shift[c] = u8(w.log2_denom(c) + 6);  // log2WD = denom + shift1 (14 - bitDepth)
+      for (int l = 0; l < 2; ++l)
+        if ((m.pred >> l) & 1) {
+          e.w[l][c] = i16(w.w[l][m.ref[l]][c]);
+          e.o[l][c] = i16(w.o[l][m.ref[l]][c]);
+        }
+    }
+    std::vector<GpuWp>& tab = pc_.gpu->wp;
+    for (size_t i = 0; i < tab.size(); ++i)
+      if (std::memcmp(&tab[i], &e, sizeof e) == 0) return u8(i + 1);
+    VEP_CHECK(tab.size() < 255, "HEVC: more than 255 distinct prediction weights in one picture");
+    tab.push_back(e);
+    return u8(tab.size());
+  }
+
   void predict_inter_cu() {
     if (GpuPicture* g = pc_.gpu) {  // records mode: one record per prediction block
       for (int k = 0; k < cu_.npu; ++k) {
@@ -592,6 +666,7 @@ class CtuLayer {
         u.w = u8(cu_.pus[k][2]);
         u.h = u8(cu_.pus[k][3]);
         u.pred = m.pred;
+        u.wp = sh_.weighted ? gpu_wp_index(m) : 0;
         for (int l = 0; l < 2; ++l) {
           u.slot[l] = -1;
           if ((m.pred >> l) & 1) {
@@ -902,11 +977,11 @@ class CtuLayer {
         std::vector<u8> pred(size_t(n) * n);
         for (int j = 0; j < n; ++j)
           for (int i = 0; i < n; ++i) pred[size_t(j) * n + i] = px(i, j);
-        const bool ts_ok = pps_.transform_skip && log2 == 2;
+        const bool ts_ok = pps_.transform_skip && log2 == 2 && !cu_.bypass;
         bool ts = dry_tskip_ && ts_ok;
         dec_->residual(c, x0, y0, log2, pred.data(), n, qp, ts_ok, cu_.intra, lv, ts);
         tskip = ts && ts_ok;
-        if (pps_.sign_data_hiding) hide_signs(lv, log2, scan_idx(c, log2));
+        if (pps_.sign_data_hiding && !cu_.bypass) hide_signs(lv, log2, scan_idx(c, log2));
         TuLevels& t = levels_[key];
         t.lv.assign(lv, lv + nn);
         t.tskip = tskip;
@@ -950,6 +1025,7 @@ class CtuLayer {
         for4(x0 << sub, y0 << sub, n << sub, n << sub, [&](size_t k) { lvl[k] = u16(gpu_level_); });
       }
       if (tskip) t.flags |= kTuSkip;
+      if (cu_.bypass) t.flags |= kTuBypass;
       if (nz) {
         t.flags |= kTuCoef;
         t.data = u32(g->coefs.size());
@@ -957,8 +1033,10 @@ class CtuLayer {
         const size_t off = g->coefs.size();
         g->coefs.resize(off + size_t(nn));
         i16* dq = g->coefs.data() + off;
+        const u8* m = scale_matrix(c, log2);
+        const bool byp = cu_.bypass;
         auto put = [&](int k) {
-          dq[k] = i16(dequant_level(lv[k], qp, log2));
+          dq[k] = byp ? i16(std::clamp(lv[k], -32768, 32767)) : i16(dequant_level(lv[k], qp, log2, m ? m[k] : 16));
           ex = std::max(ex, k & (n - 1));
           ey = std::max(ey, k >> log2);
         };
@@ -977,13 +1055,24 @@ class CtuLayer {
     if (!nz) return;
     cbf_nonzero_ = true;
     std::vector<i32> d(size_t(n) * n), r(size_t(n) * n);
-    for (size_t k = 0; k < d.size(); ++k) d[k] = lv[k] ? dequant_level(lv[k], qp, log2) : 0;
-    inverse_transform(d.data(), log2, c == 0 && log2 == 2 && cu_.intra, tskip, r.data());
+    if (cu_.bypass) {  // §8.6.2: the residual is the coded levels themselves
+      for (size_t k = 0; k < d.size(); ++k) r[k] = lv[k];
+    } else {
+      const u8* m = scale_matrix(c, log2);
+      for (size_t k = 0; k < d.size(); ++k) d[k] = lv[k] ? dequant_level(lv[k], qp, log2, m ? m[k] : 16) : 0;
+      inverse_transform(d.data(), log2, c == 0 && log2 == 2 && cu_.intra, tskip, r.data());
+    }
     for (int j = 0; j < n; ++j)
       for (int i = 0; i < n; ++i) {
         u8& p = px(i, j);
         p = u8(std::clamp(int(p) + r[size_t(j) * n + i], 0, 255));
       }
+  }
+
+  // ScalingFactor of the block (raster n x n) or null when scaling lists are off (m = 16)
+  const u8* scale_matrix(int c, int log2) const {
+    if (!pc_.scaling) return nullptr;
+    return pc_.sf[log2 - 2][(cu_.intra ? 0 : 3) + c].data();
   }
 
   // scan position k of a 4x4 sub-block / the sub-block grid
@@ -1025,7 +1114,7 @@ class CtuLayer {
 
   void residual_coding(int c, int log2, int* lv, bool& tskip) {
     const int n = 1 << log2;
-    if (pps_.transform_skip && log2 == 2) tskip = bin(kCtxTransformSkip + (c ? 1 : 0), tskip) != 0;
+    if (pps_.transform_skip && log2 == 2 && !cu_.bypass) tskip = bin(kCtxTransformSkip + (c ? 1 : 0), tskip) != 0;
     const int scan = scan_idx(c, log2);
     const int nsb = log2 - 2;
     // last significant position (write: the last non-zero level in scan order)
@@ -1152,7 +1241,7 @@ class CtuLayer {
         if (last_sig < 0) last_sig = k;
         first_sig = k;
       }
-      const bool hidden = pps_.sign_data_hiding && last_sig - first_sig > 3;
+      const bool hidden = pps_.sign_data_hiding && !cu_.bypass && last_sig - first_sig > 3;
       if (last_gt1 >= 0)
         gt2[last_gt1] = bin(kCtxGt2 + ctx_set + (c ? 4 : 0), kWrite && std::abs(at(last_gt1)) > 2) != 0;
       bool neg[16] = {};
@@ -1205,7 +1294,7 @@ class CtuLayer {
     };
     const int n = 1 << log2;
     tskip = false;
-    if (pps_.transform_skip && log2 == 2) tskip = d.decision(ctx[kCtxTransformSkip + (c ? 1 : 0)]) != 0;
+    if (pps_.transform_skip && log2 == 2 && !cu_.bypass) tskip = d.decision(ctx[kCtxTransformSkip + (c ? 1 : 0)]) != 0;
     const int scan = scan_idx(c, log2);
     const int nsb = log2 - 2;
     const int off = c ? 15 : 3 * (log2 - 2) + ((log2 - 1) >> 2), shift = c ? log2 - 2 : (log2 + 1) >> 2;
@@ -1300,7 +1389,7 @@ class CtuLayer {
           ++greater1_ctx;
         }
       }
-      const bool hidden = pps_.sign_data_hiding && last_sig - first_sig > 3;
+      const bool hidden = pps_.sign_data_hiding && !cu_.bypass && last_sig - first_sig > 3;
       const bool gt2 = last_gt1 >= 0 && d.decision(ctx[kCtxGt2 + ctx_set + (c ? 4 : 0)]);
       u32 neg = 0;
       for (u32 w = sig; w;) {
@@ -1388,7 +1477,7 @@ class CtuLayer {
 
   struct CuState {
     int x0 = 0, y0 = 0, log2 = 3;
-    bool intra = false, merge0 = false;
+    bool intra = false, merge0 = false, bypass = false;
     int part = 0;
     int ipm[4] = {1, 1, 1, 1}, ipmc = 1;
     int npu = 0;
@@ -1428,12 +1517,58 @@ void init_ctx(cabac::Ctx* ctx, const SliceHeader& sh, int qp) {
   for (int i = 0; i < kCtxCount; ++i) ctx[i].init(kCtxInit[type][i], qp);
 }
 
+// Context variables at the start of the CTU at `rs` (§9.3.1, §9.3.2.1): initialised at a tile
+// start; WPP rows synchronise from the storage after the 2nd CTB of the row above when its
+// top-right CTB is available; a dependent slice segment continues from the previous segment.
+// The qPY_PREV reset (§8.6.1) follows the same boundaries.
+template <class L>
+void start_ctu_state(PicCtx& pc, const SliceInfo& sl, cabac::Ctx* ctx, L& layer, int rs, bool segment_start) {
+  const bool wpp = pc.pps->entropy_coding_sync;
+  if (pc.first_ctb_in_tile(rs)) {
+    init_ctx(ctx, sl.sh, sl.qp);
+    layer.reset_qp_prediction();
+    return;
+  }
+  if (wpp && pc.ctb_row_start(rs)) {
+    const int rx = rs % pc.wctb, ry = rs / pc.wctb;
+    const int tr = rs - pc.wctb + 1;
+    const bool avail = ry > 0 && rx + 1 < pc.wctb && pc.slice[size_t(tr)] != 0xFFFF &&
+                       pc.sord[size_t(tr)] == sl.ord && pc.tile[size_t(tr)] == pc.tile[size_t(rs)];
+    if (avail) std::copy(pc.wpp_ctx, pc.wpp_ctx + kCtxCount, ctx);
+    else init_ctx(ctx, sl.sh, sl.qp);
+    layer.reset_qp_prediction();
+    return;
+  }
+  if (segment_start && sl.sh.dependent) {
+    std::copy(pc.ds_ctx, pc.ds_ctx + kCtxCount, ctx);
+    layer.continue_qp_prediction(pc.ds_qp);
+    return;
+  }
+  if (segment_start) init_ctx(ctx, sl.sh, sl.qp);
+}
+
+// After the CTU at `rs`: WPP storage and the end-of-segment storage (dependent segments).
+template <class L>
+void end_ctu_state(PicCtx& pc, const cabac::Ctx* ctx, const L& layer, int rs, bool segment_end) {
+  if (pc.pps->entropy_coding_sync && rs % pc.wctb == pc.tile_col_start(rs % pc.wctb) + 1)
+    std::copy(ctx, ctx + kCtxCount, pc.wpp_ctx);
+  if (segment_end && pc.pps->dependent_slice_segments) {
+    std::copy(ctx, ctx + kCtxCount, pc.ds_ctx);
+    pc.ds_qp = layer.qp_last();
+  }
+}
+
+// The next CTU starts a new substream (new tile, or new CTB row of a tile with WPP).
+bool substream_boundary(const PicCtx& pc, int rs, int next_rs) {
+  return (pc.pps->tiles && pc.tile[size_t(next_rs)] != pc.tile[size_t(rs)]) ||
+         (pc.pps->entropy_coding_sync && pc.ctb_row_start(next_rs));
+}
+
 }  // namespace
 
 void decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos) {
   SliceInfo& sl = pc.slices[size_t(slice_idx)];
   cabac::Ctx ctx[kCtxCount];
-  init_ctx(ctx, sl.sh, sl.qp);
   cabac::Decoder dec(data, n, bytepos);
   RD e{dec, ctx};
   CtuLayer<RD> L(pc, slice_idx, e, nullptr);
@@ -1441,24 +1576,51 @@ void decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size
   L.data = data;
   L.data_n = n;
   const int total = pc.wctb * pc.hctb;
-  for (int addr = sl.sh.segment_address;; ++addr) {
-    VEP_CHECK(addr < total, "slice data past the last CTU");
-    L.ctu(addr, false);
-    if (L.end_of_slice()) break;
+  int ts = pc.rs2ts[size_t(sl.sh.segment_address)];
+  start_ctu_state(pc, sl, ctx, L, sl.sh.segment_address, true);
+  for (;;) {
+    const int rs = pc.ts2rs[size_t(ts)];
+    VEP_CHECK(pc.slice[size_t(rs)] == 0xFFFF, "HEVC: CTU decoded twice");
+    L.ctu(rs, false);
+    const bool end = L.end_of_slice();
+    end_ctu_state(pc, ctx, L, rs, end);
+    if (end) break;
     VEP_CHECK(dec.bitpos() <= n * 8 + 16, "slice data overrun");
+    ++ts;
+    VEP_CHECK(ts < total, "slice data past the last CTU");
+    const int next = pc.ts2rs[size_t(ts)];
+    if (substream_boundary(pc, rs, next)) {
+      VEP_CHECK(dec.terminate() == 1, "HEVC: end_of_subset_one_bit must be 1");
+      dec.start(dec.aligned_bytepos());  // byte_alignment(), then a new arithmetic decoder
+      start_ctu_state(pc, sl, ctx, L, next, false);
+    }
   }
 }
 
-void encode_slice_data(PicCtx& pc, int slice_idx, std::vector<u8>& out, CtuDecider& dec, int first_ctb,
-                       int end_ctb) {
+void encode_slice_data(PicCtx& pc, int slice_idx, std::vector<u8>& out, CtuDecider& dec, int first_ts, int end_ts,
+                       std::vector<size_t>* substreams) {
   SliceInfo& sl = pc.slices[size_t(slice_idx)];
   cabac::Ctx ctx[kCtxCount];
-  init_ctx(ctx, sl.sh, sl.qp);
   cabac::Encoder enc(out);
   WR e{enc, ctx};
   CtuLayer<WR> L(pc, slice_idx, e, &dec);
   L.wr = &enc;
-  for (int addr = first_ctb; addr < end_ctb; ++addr) L.ctu(addr, addr + 1 == end_ctb);
+  start_ctu_state(pc, sl, ctx, L, pc.ts2rs[size_t(first_ts)], true);
+  for (int ts = first_ts; ts < end_ts; ++ts) {
+    const int rs = pc.ts2rs[size_t(ts)];
+    const bool last = ts + 1 == end_ts;
+    L.ctu(rs, last);
+    end_ctu_state(pc, ctx, L, rs, last);
+    if (last) break;
+    const int next = pc.ts2rs[size_t(ts) + 1];
+    if (substream_boundary(pc, rs, next)) {
+      enc.terminate(1);  // end_of_subset_one_bit
+      enc.align_zero();  // byte_alignment() (the flush wrote its 1 bit)
+      if (substreams) substreams->push_back(out.size());
+      enc.start();
+      start_ctu_state(pc, sl, ctx, L, next, false);
+    }
+  }
   enc.align_zero();
 }
 

@@ -18,12 +18,16 @@ struct SaoParams {
   i8 off[3][4] = {};        // SaoOffsetVal[1..4]
 };
 
-// Per-slice state needed after parsing (loop filters, TMVP).
+// Per-slice-segment state needed after parsing (loop filters, TMVP). The segments of one slice
+// (an independent segment and its dependent ones) share `ord` and the slice-level fields.
 struct SliceInfo {
   SliceHeader sh;
   int qp = 26;
+  int ord = 0;       // ordinal of the slice in the picture (decoding order)
+  int addr_rs = 0;   // SliceAddrRs: raster address of the slice's first CTB
   std::vector<FramePtr> list[2];
   std::vector<int> list_poc[2];
+  std::vector<u8> list_lt[2];  // the entry is a long-term reference picture
 };
 
 struct PicCtx {
@@ -38,9 +42,25 @@ struct PicCtx {
   std::vector<u8> depth, skip, intra, ipm, done, rec, pcm, cbf, edge;
   std::vector<i8> qp;
   std::vector<MvField> mf;
-  std::vector<u16> slice;     // slice index per CTB (not per 4x4)
+  std::vector<u16> slice;     // slice segment index per CTB (not per 4x4)
+  std::vector<u16> sord;      // slice ordinal per CTB
   std::vector<SaoParams> sao; // per CTB
   std::vector<SliceInfo> slices;
+  // tiles (§6.5.1): column / row boundaries in CTBs, CTB address conversions, tile id per CTB
+  std::vector<int> col_bd, row_bd, rs2ts, ts2rs;
+  std::vector<u16> tile;
+  bool multi = false;         // several slices or tiles: availability consults sord / tile
+  // per 4x4: CU coded with cu_transquant_bypass_flag (loop filters leave its samples alone)
+  std::vector<u8> bypass;
+  bool any_bypass = false;
+  // scaling factors m[x][y] per sizeId / matrixId (raster, n x n) when scaling lists are on
+  bool scaling = false;
+  std::vector<u8> sf[4][6];
+  // CABAC state carried across CTUs / segments: WPP storage (after the 2nd CTB of a row) and
+  // the end of the previous slice segment (dependent slice segments)
+  cabac::Ctx wpp_ctx[kCtxCount];
+  cabac::Ctx ds_ctx[kCtxCount];
+  int ds_qp = 26;
   Decoder::Stats stats;
   // records mode (GPU reconstruction): the CTU layer emits work instead of samples
   GpuPicture* gpu = nullptr;
@@ -72,10 +92,31 @@ struct PicCtx {
     done.assign(n, 0);
     rec.assign(n, 0);
     slice.assign(size_t(wctb) * hctb, 0xFFFF);
+    sord.assign(size_t(wctb) * hctb, 0xFFFF);
     sao.assign(size_t(wctb) * hctb, SaoParams{});
     slices.clear();
     stats = {};
     gpu = nullptr;
+    init_tiles();
+    multi = col_bd.size() > 2 || row_bd.size() > 2;
+    any_bypass = false;
+    if (pp.transquant_bypass) bypass.assign(n, 0);
+    init_scaling();
+  }
+  void init_tiles();
+  void init_scaling();
+  int tile_col_start(int rx) const {  // first CTB column of the tile column containing rx
+    int s = 0;
+    for (size_t i = 0; i + 1 < col_bd.size() && col_bd[i] <= rx; ++i) s = col_bd[i];
+    return s;
+  }
+  bool first_ctb_in_tile(int rs) const {
+    const int ts = rs2ts[size_t(rs)];
+    return ts == 0 || tile[size_t(ts2rs[size_t(ts) - 1])] != tile[size_t(rs)];
+  }
+  bool ctb_row_start(int rs) const { return rs % wctb == tile_col_start(rs % wctb); }
+  bool nofilter(size_t k) const {  // loop filters must not modify the 4x4 block's samples
+    return (sps->pcm_loop_filter_disabled && pcm[k]) || (any_bypass && bypass[k]);
   }
   void init_gpu(GpuPicture* g) {
     gpu = g;
@@ -89,8 +130,10 @@ struct PicCtx {
   bool avail(int x, int y, int xn, int yn, const std::vector<u8>& flag) const {
     if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
     if (!flag[i4(xn, yn)]) return false;
-    // a decoded block of a single-slice picture is in the current block's slice
-    return slices.size() == 1 || slice[size_t(ctb_of(xn, yn))] == slice[size_t(ctb_of(x, y))];
+    // a decoded block of a single-slice, single-tile picture is in the current block's slice
+    if (!multi) return true;
+    const size_t a = size_t(ctb_of(xn, yn)), b = size_t(ctb_of(x, y));
+    return sord[a] == sord[b] && tile[a] == tile[b];
   }
 };
 
@@ -111,8 +154,11 @@ struct CtuDecider {
 // NAL RBSP (read mode); `out`: the RBSP being written (write mode, slice header already in it,
 // byte aligned).
 void decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos);
-void encode_slice_data(PicCtx& pc, int slice_idx, std::vector<u8>& out, CtuDecider& dec, int first_ctb,
-                       int end_ctb);
+// Write mode: CTUs [first_ts, end_ts) in tile scan. `out` receives the slice segment data only;
+// `substreams` (when given) the byte offsets in `out` where each further WPP row / tile
+// substream starts (entry points, before emulation prevention).
+void encode_slice_data(PicCtx& pc, int slice_idx, std::vector<u8>& out, CtuDecider& dec, int first_ts, int end_ts,
+                       std::vector<size_t>* substreams = nullptr);
 
 // Loop filters over the finished picture.
 void deblock_picture(PicCtx& pc);

@@ -19,10 +19,6 @@ bool is_bla(int t) { return t >= 16 && t <= 18; }
 void check_supported(const Sps& sps, const Pps& pps) {
   if (sps.chroma_format_idc != 1 || sps.separate_colour_plane) throw UnsupportedStream("HEVC: only 4:2:0 is supported");
   if (sps.bit_depth_luma != 8 || sps.bit_depth_chroma != 8) throw UnsupportedStream("HEVC: only 8-bit (Main) is supported");
-  if (sps.scaling_list || pps.scaling_list) throw UnsupportedStream("HEVC: scaling lists are not supported");
-  if (pps.tiles || pps.entropy_coding_sync) throw UnsupportedStream("HEVC: tiles / wavefront entry points are not supported");
-  if (pps.transquant_bypass) throw UnsupportedStream("HEVC: transquant bypass is not supported");
-  if (pps.weighted_pred || pps.weighted_bipred) throw UnsupportedStream("HEVC: weighted prediction is not supported");
   if (sps.pcm && (sps.pcm_bit_depth_luma != 8 || sps.pcm_bit_depth_chroma != 8))
     throw UnsupportedStream("HEVC: PCM bit depth below 8 is not supported");
   VEP_CHECK(sps.width > 0 && sps.height > 0 && sps.width % (1 << sps.log2_min_cb) == 0 &&
@@ -62,7 +58,6 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
     skip_pic_ = true;
     return;
   }
-  if (sh.num_long_term > 0) throw UnsupportedStream("HEVC: long-term reference pictures are not supported");
   // only a picture that starts a new coded video sequence may change the picture size (a mid-GOP
   // SPS with another size would have the picture predict from surfaces of the old size)
   if (!(irap && no_rasl_output_) && act_w_ && (sps.width != act_w_ || sps.height != act_h_))
@@ -81,28 +76,45 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   }
   const int poc = msb + (is_idr(t) ? 0 : sh.poc_lsb);
   if (tid == 0 && !is_rasl(t) && !is_radl(t) && !is_sub_layer_non_ref(t)) prev_tid0_poc_ = poc;
-  // reference picture set (§8.3.2)
+  // reference picture set (§8.3.2): long-term entries first (any reference picture, by POC LSBs
+  // or full POC), then the short-term ones (short-term reference pictures only)
   st_before_.clear();
   st_after_.clear();
+  lt_curr_.clear();
   if (is_idr(t)) {
-    for (FramePtr& f : dpb_) f->is_ref = false;
+    for (FramePtr& f : dpb_) f->is_ref = f->long_term = false;
   } else {
     std::vector<FramePtr> keep;
+    const bool tolerate = irap && no_rasl_output_;  // (CRA / BLA start: references are not needed)
+    for (int i = 0; i < sh.num_long_term; ++i) {
+      int plt = sh.lt_poc_lsb[i];
+      if (sh.lt_msb_present[i]) plt += poc - sh.lt_msb_cycle[i] * max_lsb - (poc & (max_lsb - 1));
+      FramePtr hit;
+      for (const FramePtr& f : dpb_)
+        if (f->is_ref && (sh.lt_msb_present[i] ? f->poc == plt : (f->poc & (max_lsb - 1)) == plt)) hit = f;
+      if (hit) {
+        keep.push_back(hit);
+        if (sh.lt_used[i]) lt_curr_.push_back(hit);
+      } else if (sh.lt_used[i] && !tolerate) {
+        throw Error("HEVC: missing long-term reference picture (poc " + std::to_string(plt) + ")");
+      }
+    }
+    for (const FramePtr& f : keep) f->long_term = true;
     const ShortTermRps& r = sh.rps;
     for (int i = 0; i < r.num_delta(); ++i) {
       FramePtr hit;
       for (const FramePtr& f : dpb_)
-        if (f->is_ref && f->poc == poc + r.delta_poc[i]) hit = f;
+        if (f->is_ref && !f->long_term && f->poc == poc + r.delta_poc[i]) hit = f;
       if (hit) keep.push_back(hit);
       if (!r.used[i]) continue;
       if (!hit) {
-        if (irap && no_rasl_output_) continue;  // (CRA / BLA start: references are not needed)
+        if (tolerate) continue;
         throw Error("HEVC: missing reference picture (poc " + std::to_string(poc + r.delta_poc[i]) + ")");
       }
       (i < r.num_negative ? st_before_ : st_after_).push_back(hit);
     }
     for (FramePtr& f : dpb_)
-      if (std::find(keep.begin(), keep.end(), f) == keep.end()) f->is_ref = false;
+      if (std::find(keep.begin(), keep.end(), f) == keep.end()) f->is_ref = f->long_term = false;
   }
   // output and removal of pictures from the DPB (C.5.2.2)
   if (irap && no_rasl_output_ && !first_) {
@@ -179,6 +191,8 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
       keep(g.intra_map, fresh.intra_map);
       keep(g.avail, fresh.avail);
       keep(g.ctb_slice, fresh.ctb_slice);
+      keep(g.ctb_tile, fresh.ctb_tile);
+      keep(g.wp, fresh.wp);
       keep(g.slices, fresh.slices);
       keep(g.sao_params, fresh.sao_params);
       g = std::move(fresh);
@@ -197,34 +211,50 @@ std::vector<std::shared_ptr<GpuPicture>> Decoder::take_gpu_pictures() {
 void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
   SliceInfo si;
   si.sh = sh;
+  if (!sh.first_slice_in_pic) {
+    VEP_CHECK(!pc_->slices.empty(), "HEVC: slice segment before the first slice of the picture");
+    VEP_CHECK(pc_->slice[size_t(sh.segment_address)] == 0xFFFF, "HEVC: slice segment overlaps decoded CTUs");
+  }
+  if (sh.dependent) {  // a further segment of the previous slice: its lists, QP and identity
+    const SliceInfo& p = pc_->slices.back();
+    si.qp = p.qp;
+    si.ord = p.ord;
+    si.addr_rs = p.addr_rs;
+    for (int l = 0; l < 2; ++l) {
+      si.list[l] = p.list[l];
+      si.list_poc[l] = p.list_poc[l];
+      si.list_lt[l] = p.list_lt[l];
+    }
+    pc_->slices.push_back(std::move(si));
+    decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
+    return;
+  }
   si.qp = pps_act_->init_qp + sh.qp_delta;
   VEP_CHECK(si.qp >= 0 && si.qp <= 51, "HEVC: slice QP out of range");
-  if (sh.slice_type != kI) {
-    std::vector<FramePtr> all = st_before_;
-    all.insert(all.end(), st_after_.begin(), st_after_.end());
-    const int total = int(all.size());
+  si.ord = pc_->slices.empty() ? 0 : pc_->slices.back().ord + 1;
+  si.addr_rs = sh.segment_address;
+  if (si.ord > 0) pc_->multi = true;
+  if (sh.slice_type != kI) {  // reference picture lists (§8.3.4)
+    const int total = int(st_before_.size() + st_after_.size() + lt_curr_.size());
     VEP_CHECK(total > 0, "HEVC: inter slice without reference pictures");
     for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
-      std::vector<FramePtr> temp;
+      std::vector<std::pair<FramePtr, bool>> temp;  // (picture, long-term)
       const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
       const std::vector<FramePtr>& a = l == 0 ? st_before_ : st_after_;
       const std::vector<FramePtr>& b = l == 0 ? st_after_ : st_before_;
       while (int(temp.size()) < std::max(nref, total)) {
-        for (const FramePtr& f : a) temp.push_back(f);
-        for (const FramePtr& f : b) temp.push_back(f);
+        for (const FramePtr& f : a) temp.push_back({f, false});
+        for (const FramePtr& f : b) temp.push_back({f, false});
+        for (const FramePtr& f : lt_curr_) temp.push_back({f, true});
       }
       for (int i = 0; i < nref; ++i) {
         const int e = sh.list_mod[l] ? sh.list_entry[l][i] : i;
         VEP_CHECK(e < int(temp.size()), "HEVC: list_entry out of range");
-        si.list[l].push_back(temp[size_t(e)]);
-        si.list_poc[l].push_back(temp[size_t(e)]->poc);
+        si.list[l].push_back(temp[size_t(e)].first);
+        si.list_poc[l].push_back(temp[size_t(e)].first->poc);
+        si.list_lt[l].push_back(u8(temp[size_t(e)].second));
       }
     }
-  }
-  if (!sh.first_slice_in_pic) {
-    const int prev_end = pc_->slices.empty() ? 0 : 1;
-    VEP_CHECK(prev_end, "HEVC: slice segment before the first slice of the picture");
-    VEP_CHECK(pc_->slice[size_t(sh.segment_address)] == 0xFFFF, "HEVC: slice segment overlaps decoded CTUs");
   }
   pc_->slices.push_back(std::move(si));
   decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
@@ -309,7 +339,9 @@ std::vector<FramePtr> Decoder::decode(const AccessUnit& au, i64 tag) {
     if (pit == pps_.end()) throw Error("HEVC: slice refers to a missing PPS");
     auto sit = sps_.find(pit->second.sps_id);
     if (sit == sps_.end()) throw Error("HEVC: PPS refers to a missing SPS");
-    const SliceHeader sh = parse_slice_header(rbsp_.data(), rn, sit->second, pit->second);
+    const SliceHeader sh = parse_slice_header(rbsp_.data(), rn, sit->second, pit->second, have_prev_sh_ ? &prev_sh_ : nullptr);
+    prev_sh_ = sh;  // (a dependent segment of the next NAL takes its slice fields from here)
+    have_prev_sh_ = true;
     try {
       if (sh.first_slice_in_pic) {
         if (cur_) finish_picture(out);

@@ -10,9 +10,10 @@
 // mode for the closed-loop synthetic encoder (hevc_enc.cpp), so both share the binarizations,
 // the context selection, the candidate derivations and the reconstruction; the loop filters run
 // over the finished picture. This is the CPU reference of the H.265 path (bit-exact oracle for
-// GPU reconstruction kernels); streams using tiles, wavefront entry points, long-term
-// references, weighted prediction, scaling lists, transquant bypass or range extensions are
-// reported as UnsupportedStream.
+// GPU reconstruction kernels). Also: tiles, wavefront (WPP) substreams, dependent slice
+// segments, long-term reference pictures, explicit weighted prediction, scaling lists and
+// transquant-bypass (lossless) CUs. Range extensions (non-4:2:0, > 8 bit) are reported as
+// UnsupportedStream.
 //
 // Reference parity: libavcodec's hevc decoder behind PyAV (python/read_image.py:87
 // `p.decode()`), BASELINE config 5 (H.265 cameras). No third-party HEVC stream exists in this
@@ -42,6 +43,7 @@ struct ColMv {  // a reference picture's motion as seen by TMVP
   i16 mv[2][2];
   i32 poc[2];    // POC of the picture each list's vector points at
   u8 pred;       // 0 = intra
+  u8 lt;         // bit l: that reference was a long-term picture when this picture was decoded
 };
 
 // A decoded picture.
@@ -49,6 +51,7 @@ struct HevcFrame {
   HostSurface s;
   int poc = 0;
   bool is_ref = false, needed_for_output = false;
+  bool long_term = false;  // marked "used for long-term reference"
   u32 uid = 0;
   i64 pts = 0, dts = 0, tag = 0;
   bool keyframe = false;
@@ -66,6 +69,7 @@ using FramePtr = std::shared_ptr<HevcFrame>;
 struct CuDesc {
   bool skip = false;
   bool intra = false;
+  bool bypass = false;        // cu_transquant_bypass_flag (lossless CU)
   int part = 0;               // PartMode: 0 2Nx2N 1 2NxN 2 Nx2N 3 NxN 4 2NxnU 5 2NxnD 6 nLx2N 7 nRx2N
   bool pcm = false;
   const u8* pcm_samples = nullptr;  // (2N)^2 luma then 2 * N^2 chroma
@@ -126,6 +130,9 @@ class Decoder {
   std::vector<FramePtr> dpb_;
   FramePtr cur_, last_;
   std::vector<FramePtr> st_before_, st_after_;  // RefPicSetStCurrBefore / After of the picture
+  std::vector<FramePtr> lt_curr_;               // RefPicSetLtCurr
+  SliceHeader prev_sh_;                         // the picture's previous slice segment header
+  bool have_prev_sh_ = false;
   std::unique_ptr<PicCtx> pc_;
   const Sps* sps_act_ = nullptr;
   const Pps* pps_act_ = nullptr;
@@ -163,6 +170,14 @@ struct HevcEncConfig {
   bool amp = true, sao = true, deblock = true, tskip = true, sign_hiding = true, cu_qp_delta = true;
   bool pcm = true, tmvp = true;
   int slices = 1;
+  // stream structure / coding tools beyond the basic Main stream
+  int tile_cols = 1, tile_rows = 1;  // tiles (coverage: explicit, non-uniform spacing at random)
+  bool wpp = false;                  // entropy_coding_sync (one substream per CTB row)
+  int segments = 1;                  // slice segments per slice: the 2nd.. are dependent
+  bool scaling_lists = false;        // scaling lists (coverage: custom SPS / PPS lists)
+  bool weighted = false;             // explicit weighted prediction in P and B slices
+  bool long_term = false;            // each GOP's IDR stays referenced as a long-term picture
+  bool lossless = false;             // transquant bypass enabled (coverage: lossless CUs)
   bool coverage = false;
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;

@@ -44,8 +44,9 @@ const Basis& dct_basis(int log2) {
   return t.b[log2 - 2];
 }
 
-// Forward transform + dead-zone quantisation (level = C / Qstep, Qstep = 2^((qp - 4) / 6)).
-void quantise(const int* res, int log2, bool dst, bool tskip, int qp, bool intra, int* lv) {
+// Forward transform + dead-zone quantisation (level = C / Qstep, Qstep = 2^((qp - 4) / 6), times
+// m / 16 with a scaling matrix m).
+void quantise(const int* res, int log2, bool dst, bool tskip, int qp, bool intra, int* lv, const u8* m) {
   const int n = 1 << log2;
   const double qstep = std::pow(2.0, (qp - 4) / 6.0);
   const double f = intra ? 1.0 / 3 : 1.0 / 6;
@@ -77,7 +78,7 @@ void quantise(const int* res, int log2, bool dst, bool tskip, int qp, bool intra
       }
   }
   for (int k = 0; k < n * n; ++k) {
-    const double a = std::fabs(c[size_t(k)]) / qstep + f;
+    const double a = std::fabs(c[size_t(k)]) / (qstep * (m ? m[k] / 16.0 : 1.0)) + f;
     int l = int(std::min(a, 32767.0));
     lv[k] = c[size_t(k)] < 0 ? -l : l;
   }
@@ -112,6 +113,8 @@ struct HevcEncoder::Impl : CtuDecider {
   char last_type = 'I';
   HostSurface recon_out, src_out;
   std::vector<u8> pcm_buf;
+  FramePtr lt_pic;         // long_term: the GOP's IDR, referenced as a long-term picture
+  bool cur_bypass = false; // the CU being coded is lossless (transquant bypass)
 
   explicit Impl(const HevcEncConfig& c) : cfg(c), rng{c.seed * 0x9E3779B97F4A7C15ull + 4242} {
     VEP_CHECK(c.width >= 16 && c.height >= 16 && c.width % 2 == 0 && c.height % 2 == 0,
@@ -166,6 +169,7 @@ struct HevcEncoder::Impl : CtuDecider {
     pps.beta_offset = cov ? 2 * (rng.uni(5) - 2) : 0;
     pps.tc_offset = cov ? 2 * (rng.uni(5) - 2) : 0;
     pps.log2_parallel_merge_level = cov && rng.chance(40) ? 3 : 2;
+    setup_tools(c);
     auto nal = [](const std::vector<u8>& rbsp, std::vector<u8>& out) { rbsp_to_ebsp(rbsp.data(), rbsp.size(), out); };
     nal(write_vps(vps), vps_nal);
     nal(write_sps(sps), sps_nal);
@@ -173,6 +177,67 @@ struct HevcEncoder::Impl : CtuDecider {
     scene.make(SceneConfig{c.width, c.height, W, H, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
     residual = [this](int ci, int x0, int y0, int log2, const u8* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
                       bool& ts) { this->make_residual(ci, x0, y0, log2, pred, ps, qp, ts_ok, intra, lv, ts); };
+  }
+
+  // Tiles, WPP, dependent segments, scaling lists, weighted prediction, long-term references,
+  // transquant bypass (HevcEncConfig); coverage randomises their parameters.
+  void setup_tools(const HevcEncConfig& c) {
+    const bool cov = c.coverage;
+    const int ctb = 1 << c.log2_ctb;
+    const int wct = (W + ctb - 1) / ctb, hct = (H + ctb - 1) / ctb;
+    pps.tile_cols = std::clamp(c.tile_cols, 1, wct);
+    pps.tile_rows = std::clamp(c.tile_rows, 1, hct);
+    pps.tiles = pps.tile_cols * pps.tile_rows > 1;
+    if (pps.tiles) {
+      pps.uniform_spacing = !cov || rng.chance(50);
+      if (!pps.uniform_spacing) {
+        auto sizes = [&](int count, int total) {
+          std::vector<int> v(size_t(count), total / count);
+          v.back() += total % count;
+          for (int k = 0; k < 2 * count; ++k) {  // move single CTB columns / rows around
+            const int a = rng.uni(count), b = rng.uni(count);
+            if (a != b && v[size_t(a)] > 1) --v[size_t(a)], ++v[size_t(b)];
+          }
+          v.pop_back();  // (the last size is implied)
+          return v;
+        };
+        pps.col_width = sizes(pps.tile_cols, wct);
+        pps.row_height = sizes(pps.tile_rows, hct);
+      }
+      pps.loop_filter_across_tiles = !cov || rng.chance(50);
+    }
+    pps.entropy_coding_sync = c.wpp;
+    pps.dependent_slice_segments = c.segments > 1;
+    pps.weighted_pred = pps.weighted_bipred = c.weighted;
+    pps.transquant_bypass = c.lossless;
+    if (c.scaling_lists) {
+      sps.scaling_list = true;
+      if (cov) {
+        auto custom = [&](ScalingList& sl) {
+          for (int si = 0; si < 4; ++si)
+            for (int m = 0; m < 6; ++m) {
+              const int base = 8 + rng.uni(16);
+              for (int i = 0; i < 64; ++i) sl.list[si][m][i] = u8(std::clamp(base + i / 3 + rng.uni(9) - 4, 1, 255));
+              sl.dc[si][m] = u8(8 + rng.uni(24));
+            }
+          for (int m = 0; m < 6; ++m)  // (the 32x32 chroma lists are not coded for 4:2:0)
+            if (m % 3) std::memcpy(sl.list[3][m], sl.list[2][m], 64), sl.dc[3][m] = sl.dc[2][m];
+        };
+        sps.scaling_list_data = rng.chance(50);
+        if (sps.scaling_list_data) custom(sps.sl);
+        pps.scaling_list = rng.chance(50);
+        if (pps.scaling_list) custom(pps.sl);
+      }
+    }
+    if (c.long_term) {
+      sps.long_term_refs = true;
+      if (cov) {  // an SPS candidate list: the IDR (POC 0) and an unused entry
+        sps.lt_poc_lsb_sps = {0, 5};
+        sps.lt_used_sps = {true, false};
+      }
+      sps.num_long_term_ref_pics_sps = int(sps.lt_poc_lsb_sps.size());
+      sps.max_dec_pic_buffering += 1;
+    }
   }
 
   bool is_idr_pos(i64 d) const { return d == 0 || (d + cfg.idr_phase) % cfg.gop == 0; }
@@ -243,8 +308,11 @@ struct HevcEncoder::Impl : CtuDecider {
     const SliceHeader& sh = sl.sh;
     if (cfg.coverage) {
       coverage_cu(x0, y0, log2, d, sl);
+      d.bypass = pps.transquant_bypass && rng.chance(15);
+      cur_bypass = d.bypass;
       return;
     }
+    cur_bypass = false;
     d.tu_log2 = log2;
     d.chroma_mode = 4;
     d.luma_mode[0] = 0;  // planar
@@ -377,17 +445,140 @@ struct HevcEncoder::Impl : CtuDecider {
                              : cur_src->uv[size_t(y0 + j) * W + size_t(2 * (x0 + i) + c - 1)];
         res[size_t(j) * n + i] = s - int(pred[size_t(j) * ps + i]);
       }
+    if (cur_bypass) {  // lossless CU: the levels are the residual
+      ts = false;
+      for (int k = 0; k < n * n; ++k) lv[k] = res[size_t(k)];
+      return;
+    }
     if (!cfg.coverage) ts = false;
     ts = ts && ts_ok;
-    quantise(res.data(), log2, c == 0 && log2 == 2 && intra, ts, qp, intra, lv);
+    const u8* m = pc.scaling ? pc.sf[log2 - 2][(intra ? 0 : 3) + c].data() : nullptr;
+    quantise(res.data(), log2, c == 0 && log2 == 2 && intra, ts, qp, intra, lv, m);
   }
 
   // ------------------------------------------------------------------ pictures
+  // Slice ranges in tile scan: one slice per tile, or slices within the picture (CTB-row
+  // aligned with WPP, as §7.4.7.1 requires of a slice that does not start a row).
+  std::vector<std::pair<int, int>> plan_slices(int nctb) {
+    std::vector<std::pair<int, int>> out;
+    if (pps.tiles) {
+      if (cfg.slices > 1 || (cfg.coverage && rng.chance(50))) {
+        int a = 0;
+        for (int ts = 1; ts <= nctb; ++ts)
+          if (ts == nctb || pc.first_ctb_in_tile(pc.ts2rs[size_t(ts)])) {
+            out.push_back({a, ts});
+            a = ts;
+          }
+      } else {
+        out.push_back({0, nctb});
+      }
+      return out;
+    }
+    if (pps.entropy_coding_sync) {
+      const int nsl = std::clamp(cfg.slices, 1, pc.hctb);
+      for (int s = 0; s < nsl; ++s) out.push_back({s * pc.hctb / nsl * pc.wctb, (s + 1) * pc.hctb / nsl * pc.wctb});
+      return out;
+    }
+    const int nsl = std::clamp(cfg.slices, 1, nctb);
+    for (int s = 0; s < nsl; ++s) out.push_back({s * nctb / nsl, (s + 1) * nctb / nsl});
+    return out;
+  }
+
+  // Slice segments of the slice [a, b): the first independent, the others dependent. A segment
+  // spanning several tiles holds whole tiles; with WPP segments start at CTB rows.
+  std::vector<std::pair<int, int>> plan_segments(int a, int b) {
+    const bool multi_tile = pps.tiles && pc.tile[size_t(pc.ts2rs[size_t(a)])] != pc.tile[size_t(pc.ts2rs[size_t(b - 1)])];
+    std::vector<int> cand;
+    for (int ts = a + 1; ts < b; ++ts) {
+      const int rs = pc.ts2rs[size_t(ts)];
+      if (multi_tile ? pc.first_ctb_in_tile(rs) : (!pps.entropy_coding_sync || pc.ctb_row_start(rs))) cand.push_back(ts);
+    }
+    const int k = std::min(cfg.segments - 1, int(cand.size()));
+    std::vector<std::pair<int, int>> out;
+    int prev = a;
+    for (int i = 1; i <= k; ++i) {
+      const int cut = cand[size_t(i * int(cand.size()) / (k + 1))];
+      if (cut <= prev) continue;
+      out.push_back({prev, cut});
+      prev = cut;
+    }
+    out.push_back({prev, b});
+    return out;
+  }
+
+  void make_weights(SliceHeader& sh) {
+    const bool cov = cfg.coverage;
+    PredWeights& w = sh.pwt;
+    w = PredWeights{};
+    w.luma_log2_denom = cov ? rng.uni(8) : 6;
+    w.chroma_log2_denom = cov ? rng.uni(8) : 6;
+    for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
+      const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
+      for (int i = 0; i < nref; ++i) {
+        w.luma_flag[l][i] = !cov || rng.chance(70);
+        w.chroma_flag[l][i] = !cov || rng.chance(60);
+        const int dl = w.luma_log2_denom, dc = w.chroma_log2_denom;
+        w.w[l][i][0] = (1 << dl) + (w.luma_flag[l][i] && cov ? rng.uni(25) - 12 : 0);
+        w.o[l][i][0] = w.luma_flag[l][i] && cov ? rng.uni(21) - 10 : 0;
+        for (int c = 1; c <= 2; ++c) {
+          int wc = (1 << dc) + (w.chroma_flag[l][i] && cov ? rng.uni(17) - 8 : 0);
+          const int oc = w.chroma_flag[l][i] && cov ? rng.uni(11) - 5 : 0;
+          const int doff = oc - 128 + ((128 * wc) >> dc);
+          if (doff < -512 || doff > 511) wc = 1 << dc;  // keep delta_chroma_offset codable
+          w.w[l][i][c] = wc;
+          w.o[l][i][c] = oc;
+        }
+      }
+    }
+  }
+
+  // Emulation-prevented NAL of a slice segment: header (with entry points) + data. The entry
+  // point offsets count emulation prevention bytes (§7.4.7.1), which depend on the header: the
+  // offsets are iterated to a fixed point.
+  std::vector<u8> segment_nal(SliceHeader& sh, const std::vector<u8>& data, const std::vector<size_t>& subs) {
+    std::vector<u32> ep;
+    for (size_t k = 0; k < subs.size(); ++k) ep.push_back(u32(subs[k] - (k ? subs[k - 1] : 0)));
+    std::vector<u8> ebsp;
+    for (int iter = 0; iter < 8; ++iter) {
+      sh.entry_points = ep;
+      BitWriter bw;
+      write_slice_header_full(bw, sh, sps, pps);
+      std::vector<u8> rb = std::move(bw.buf());
+      const size_t hdr = rb.size();
+      rb.insert(rb.end(), data.begin(), data.end());
+      ebsp.clear();
+      std::vector<size_t> pos(rb.size() + 1);
+      int zeros = 0;
+      for (size_t i = 0; i < rb.size(); ++i) {
+        if (zeros >= 2 && rb[i] <= 3) {
+          ebsp.push_back(3);
+          zeros = 0;
+        }
+        pos[i] = ebsp.size();
+        ebsp.push_back(rb[i]);
+        zeros = rb[i] == 0 ? zeros + 1 : 0;
+      }
+      pos[rb.size()] = ebsp.size();
+      std::vector<u32> ep2;
+      size_t prev = pos[hdr];
+      for (size_t k = 0; k < subs.size(); ++k) {
+        const size_t at = pos[hdr + subs[k]];
+        ep2.push_back(u32(at - prev));
+        prev = at;
+      }
+      if (ep2 == ep) return ebsp;
+      ep = ep2;
+    }
+    VEP_CHECK(false, "entry point offsets did not converge");
+    return ebsp;
+  }
+
   std::shared_ptr<AccessUnit> encode(const Job& job) {
     const int dur = 90000 / std::max(1, cfg.fps);
     if (job.idr) {
       idr_disp = job.disp;
       anchors.clear();
+      lt_pic = nullptr;
     }
     const int poc = int(job.disp - idr_disp);
     cur_src = &source_of(job.disp);
@@ -407,7 +598,26 @@ struct HevcEncoder::Impl : CtuDecider {
     for (size_t i = 0; i < before.size(); ++i) rps.delta_poc[i] = before[i]->poc - poc, rps.used[i] = true;
     for (size_t i = 0; i < after.size(); ++i)
       rps.delta_poc[before.size() + i] = after[i]->poc - poc, rps.used[before.size() + i] = true;
-    const int total = rps.num_delta();
+    const bool cov = cfg.coverage;
+    // the GOP's long-term picture (used unless coverage leaves it in LtFoll for a while)
+    std::vector<FramePtr> lt;
+    SliceHeader lth;  // long-term fields shared by the picture's slices
+    if (lt_pic && !job.idr) {
+      const bool used = rps.num_delta() == 0 || !cov || rng.chance(75);
+      if (used) lt.push_back(lt_pic);
+      const int max_lsb = 1 << sps.log2_max_poc_lsb;
+      lth.num_long_term = 1;
+      lth.lt_poc_lsb[0] = lt_pic->poc & (max_lsb - 1);
+      lth.lt_used[0] = used;
+      if (cov && used && sps.num_long_term_ref_pics_sps > 0 && rng.chance(50) &&
+          sps.lt_poc_lsb_sps[0] == lth.lt_poc_lsb[0]) {
+        lth.num_long_term_sps = 1;
+        lth.lt_idx_sps[0] = 0;
+      }
+      lth.lt_msb_present[0] = cov && rng.chance(50);
+      lth.lt_msb_cycle[0] = lth.lt_msb_present[0] ? ((poc - (poc & (max_lsb - 1))) - (lt_pic->poc - lth.lt_poc_lsb[0])) / max_lsb : 0;
+    }
+    const int total = rps.num_delta() + int(lt.size());
     // slices
     pc.init(sps, pps, &cur->s);
     pc.poc = poc;
@@ -419,15 +629,15 @@ struct HevcEncoder::Impl : CtuDecider {
       au->add_nal(pps_nal.data(), pps_nal.size());
     }
     const int nctb = pc.wctb * pc.hctb;
-    const int nsl = std::clamp(cfg.slices, 1, nctb);
-    const bool cov = cfg.coverage;
+    const std::vector<std::pair<int, int>> slice_ranges = plan_slices(nctb);
+    if (slice_ranges.size() > 1) pc.multi = true;
     const int pic_qp = cov ? std::clamp(cfg.qp + rng.uni(21) - 10, 5, 51) : cfg.qp;
-    for (int s = 0; s < nsl; ++s) {
-      const int first = s * nctb / nsl, end = (s + 1) * nctb / nsl;
-      SliceHeader sh;
+    for (size_t s = 0; s < slice_ranges.size(); ++s) {
+      const auto [first_ts, end_ts] = slice_ranges[s];
+      SliceHeader sh = lth;
       sh.nal_type = job.idr ? kIdrWRadl : (job.ref ? kTrailR : kTrailN);
       sh.first_slice_in_pic = s == 0;
-      sh.segment_address = first;
+      sh.segment_address = pc.ts2rs[size_t(first_ts)];
       sh.slice_type = job.type;
       sh.poc_lsb = poc & 255;
       sh.rps = rps;
@@ -444,6 +654,8 @@ struct HevcEncoder::Impl : CtuDecider {
         const int ncol = sh.collocated_from_l0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
         sh.collocated_ref_idx = cov ? rng.uni(ncol) : 0;
         sh.max_num_merge_cand = cov ? 1 + rng.uni(5) : 5;
+        sh.weighted = pps.weighted_pred;  // (weighted_bipred is set alike)
+        if (sh.weighted) make_weights(sh);
       }
       sh.qp_delta = pic_qp - pps.init_qp;
       sh.cb_qp_offset = cov ? rng.uni(5) - 2 : 0;
@@ -462,17 +674,23 @@ struct HevcEncoder::Impl : CtuDecider {
       SliceInfo si;
       si.sh = sh;
       si.qp = pic_qp;
-      if (job.type != kI) build_lists(sh, before, after, si);
-      pc.slices.push_back(std::move(si));
-      cur_slice = s;
-      cur_qp = pic_qp;
-      BitWriter bw;
-      write_slice_header_full(bw, sh, sps, pps);
-      std::vector<u8> rb = std::move(bw.buf());
-      encode_slice_data(pc, s, rb, *this, first, end);
-      std::vector<u8> ebsp;
-      rbsp_to_ebsp(rb.data(), rb.size(), ebsp);
-      au->add_nal(ebsp.data(), ebsp.size());
+      si.ord = int(s);
+      si.addr_rs = sh.segment_address;
+      if (job.type != kI) build_lists(sh, before, after, lt, si);
+      for (const auto& [sa, sb] : plan_segments(first_ts, end_ts)) {
+        SliceInfo seg = si;
+        seg.sh.dependent = sa != first_ts;
+        seg.sh.segment_address = pc.ts2rs[size_t(sa)];
+        seg.sh.first_slice_in_pic = s == 0 && sa == first_ts;
+        pc.slices.push_back(seg);
+        cur_slice = int(pc.slices.size()) - 1;
+        cur_qp = pic_qp;
+        std::vector<u8> data;
+        std::vector<size_t> subs;
+        encode_slice_data(pc, cur_slice, data, *this, sa, sb, &subs);
+        const std::vector<u8> nal = segment_nal(pc.slices.back().sh, data, subs);
+        au->add_nal(nal.data(), nal.size());
+      }
     }
     bool deblock = false, sao_on = false;
     for (const SliceInfo& s : pc.slices) {
@@ -483,8 +701,12 @@ struct HevcEncoder::Impl : CtuDecider {
     if (sao_on) sao_picture(pc);
     if (sps.temporal_mvp) cur->col = build_col(pc, cur->col_w);
     if (job.ref) {
-      anchors.push_back(cur);
-      if (int(anchors.size()) > keep_refs) anchors.erase(anchors.begin());
+      if (cfg.long_term && job.idr) {
+        lt_pic = cur;
+      } else {
+        anchors.push_back(cur);
+        if (int(anchors.size()) > keep_refs) anchors.erase(anchors.begin());
+      }
     }
     au->pts = job.disp * dur;
     au->dts = coded * dur - (cfg.bframes > 0 ? dur : 0);
@@ -501,21 +723,23 @@ struct HevcEncoder::Impl : CtuDecider {
   }
 
   void build_lists(const SliceHeader& sh, const std::vector<FramePtr>& before, const std::vector<FramePtr>& after,
-                   SliceInfo& si) {
-    const int total = int(before.size() + after.size());
+                   const std::vector<FramePtr>& lt, SliceInfo& si) {
+    const int total = int(before.size() + after.size() + lt.size());
     VEP_CHECK(total > 0, "inter picture without references");
     for (int l = 0; l < (sh.slice_type == kB ? 2 : 1); ++l) {
       const int nref = l == 0 ? sh.num_ref_idx_l0 : sh.num_ref_idx_l1;
-      std::vector<FramePtr> temp;
+      std::vector<std::pair<FramePtr, bool>> temp;
       const auto& a = l == 0 ? before : after;
       const auto& b = l == 0 ? after : before;
       while (int(temp.size()) < std::max(nref, total)) {
-        temp.insert(temp.end(), a.begin(), a.end());
-        temp.insert(temp.end(), b.begin(), b.end());
+        for (const FramePtr& f : a) temp.push_back({f, false});
+        for (const FramePtr& f : b) temp.push_back({f, false});
+        for (const FramePtr& f : lt) temp.push_back({f, true});
       }
       for (int i = 0; i < nref; ++i) {
-        si.list[l].push_back(temp[size_t(i)]);
-        si.list_poc[l].push_back(temp[size_t(i)]->poc);
+        si.list[l].push_back(temp[size_t(i)].first);
+        si.list_poc[l].push_back(temp[size_t(i)].first->poc);
+        si.list_lt[l].push_back(u8(temp[size_t(i)].second));
       }
     }
   }

@@ -19,11 +19,11 @@ void finish_gpu_picture(PicCtx& pc) {
   g.hctb = pc.hctb;
   g.cb_qp_offset = pc.pps->cb_qp_offset;
   g.cr_qp_offset = pc.pps->cr_qp_offset;
-  g.pcm_nofilter = pc.sps->pcm_loop_filter_disabled;
   g.constrained_intra = pc.pps->constrained_intra_pred;
   g.deblock = g.sao = false;
   g.slices.clear();
-  for (const SliceInfo& s : pc.slices) {
+  for (const SliceInfo& s : pc.slices) {  // one entry per slice (its segments share the fields)
+    if (s.ord < int(g.slices.size())) continue;
     g.deblock |= !s.sh.deblocking_disabled;
     g.sao |= s.sh.sao_luma || s.sh.sao_chroma;
     GpuSlice gs{};
@@ -36,8 +36,13 @@ void finish_gpu_picture(PicCtx& pc) {
   }
   if (g.deblock) deblock_strengths(pc, g.bs_v, g.bs_h);
   g.qp.assign(pc.qp.begin(), pc.qp.end());
-  g.pcm_map.assign(pc.pcm.begin(), pc.pcm.end());
-  g.ctb_slice.assign(pc.slice.begin(), pc.slice.end());
+  // samples the loop filters leave alone: PCM (pcm_loop_filter_disabled) and lossless CUs
+  g.pcm_nofilter = pc.sps->pcm_loop_filter_disabled || pc.any_bypass;
+  g.pcm_map.resize(pc.pcm.size());
+  for (size_t k = 0; k < pc.pcm.size(); ++k) g.pcm_map[k] = u8(pc.nofilter(k));
+  g.ctb_slice.assign(pc.sord.begin(), pc.sord.end());
+  g.ctb_tile.assign(pc.tile.begin(), pc.tile.end());
+  g.tiles_block_sao = (pc.col_bd.size() > 2 || pc.row_bd.size() > 2) && !pc.pps->loop_filter_across_tiles;
   g.sao_params.resize(pc.sao.size());
   for (size_t k = 0; k < pc.sao.size(); ++k) {
     const SaoParams& p = pc.sao[k];
@@ -64,6 +69,10 @@ namespace {
 void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
   const int log2 = t.log2, n = 1 << log2;
   const i16* d = p.coefs.data() + t.data;
+  if (t.flags & kTuBypass) {
+    for (int k = 0; k < n * n; ++k) res[k] = d[k];
+    return;
+  }
   if (t.flags & kTuSkip) {
     for (int k = 0; k < n * n; ++k) res[k] = hk_tskip(d[k]);
     return;
@@ -85,6 +94,9 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
   // pass 1: motion compensation
   for (const GpuPu& u : p.pus) {
     const bool bi = u.pred == 3;
+    const GpuWp* wp = u.wp ? &p.wp[size_t(u.wp) - 1] : nullptr;
+    const int ul = (u.pred & 1) ? 0 : 1;
+    auto fin = [&](int c, int p0, int p1) { return wp ? hk_weight_explicit(*wp, c, p0, p1, bi, ul) : hk_weight(p0, p1, bi); };
     for (int j = 0; j < u.h; ++j)
       for (int i = 0; i < u.w; ++i) {
         int v[2] = {0, 0}, nv = 0;
@@ -94,7 +106,7 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
           v[nv++] = hk_luma_mc(r.y.data(), stride, W, H, u.x + i + (u.mv[l][0] >> 2), u.y + j + (u.mv[l][1] >> 2),
                                u.mv[l][0] & 3, u.mv[l][1] & 3);
         }
-        s.y[size_t(u.y + j) * stride + size_t(u.x + i)] = hk_weight(v[0], v[1], bi);
+        s.y[size_t(u.y + j) * stride + size_t(u.x + i)] = fin(0, v[0], v[1]);
       }
     for (int c = 0; c < 2; ++c)
       for (int j = 0; j < u.h / 2; ++j)
@@ -106,7 +118,7 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
             v[nv++] = hk_chroma_mc(r.uv.data(), stride, W / 2, H / 2, c, u.x / 2 + i + (u.mv[l][0] >> 3),
                                    u.y / 2 + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7);
           }
-          s.uv[size_t(u.y / 2 + j) * stride + size_t(u.x + 2 * i + c)] = hk_weight(v[0], v[1], bi);
+          s.uv[size_t(u.y / 2 + j) * stride + size_t(u.x + 2 * i + c)] = fin(1 + c, v[0], v[1]);
         }
   }
   // pass 2+: transform blocks by level (0: inter residual and PCM; then intra levels)
@@ -201,7 +213,9 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
               if (p.pcm_nofilter && p.pcm_map[size_t((y << sub) >> 2) * p.w4() + size_t((x << sub) >> 2)]) continue;
               auto nb_ok = [&](int nx, int ny) {
                 if (nx < 0 || ny < 0 || nx >= pw || ny >= ph) return false;
-                const int nsi = p.ctb_slice[size_t((((ny << sub) >> p.log2ctb) * p.wctb) + ((nx << sub) >> p.log2ctb))];
+                const size_t nci = size_t((((ny << sub) >> p.log2ctb) * p.wctb) + ((nx << sub) >> p.log2ctb));
+                if (p.tiles_block_sao && p.ctb_tile[nci] != p.ctb_tile[size_t(ci)]) return false;
+                const int nsi = p.ctb_slice[nci];
                 if (nsi == si) return true;
                 return nsi > si ? bool(p.slices[size_t(nsi)].across) : bool(sl.across);
               };

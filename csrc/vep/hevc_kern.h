@@ -27,13 +27,22 @@ struct GpuPu {    // one prediction block
   u16 x, y;       // luma position
   u8 w, h;        // luma size (4..64)
   u8 pred;        // bit 0 list 0, bit 1 list 1
-  u8 pad;
+  u8 wp;          // 0: default weighting, else 1 + index into GpuPicture::wp (explicit weights)
   i8 slot[2];     // DPB surface slot per list (-1 unused)
   i16 mv[2][2];   // quarter-sample luma vectors
 };
 static_assert(sizeof(GpuPu) == 18, "GpuPu layout");
 
-enum : u8 { kTuIntra = 1, kTuDst = 2, kTuSkip = 4, kTuCoef = 8, kTuPcm = 16, kTuStrong = 32 };
+enum : u8 { kTuIntra = 1, kTuDst = 2, kTuSkip = 4, kTuCoef = 8, kTuPcm = 16, kTuStrong = 32, kTuBypass = 64 };
+
+// Explicit weighted sample prediction of one PU (§8.5.3.3.4.3): per list / component weight and
+// offset, log2WD per component.
+struct GpuWp {
+  i16 w[2][3], o[2][3];
+  u8 shift[3];
+  u8 pad;
+};
+static_assert(sizeof(GpuWp) == 28, "GpuWp layout");
 
 struct GpuTu {    // one transform block of one component (or one PCM coding block)
   u16 x, y;       // position in the component's samples
@@ -41,7 +50,8 @@ struct GpuTu {    // one transform block of one component (or one PCM coding blo
   u8 c;           // 0 Y, 1 Cb, 2 Cr (PCM: 0, covers all three)
   u8 flags;       // kTu*
   u8 mode;        // intra prediction mode (component's)
-  u32 data;       // kTuCoef: offset of the n x n dequantised coefficients (i16); kTuPcm: byte offset
+  u32 data;       // kTuCoef: offset of the n x n dequantised coefficients (i16; kTuBypass: the
+                  // residual itself); kTuPcm: byte offset
   u16 level;      // intra dependency level (0: inter residual / PCM)
   u8 ext_x, ext_y;  // kTuCoef: last column / row holding a non-zero coefficient
   u64 avail;      // intra: reference availability, see hk_prepare_refs
@@ -74,11 +84,15 @@ struct GpuPicture {
   // per 4x4 luma block
   std::vector<u8> bs_v, bs_h;         // boundary strength of the left / top edge (0..2)
   std::vector<i8> qp;
-  std::vector<u8> pcm_map;            // PCM block whose samples the loop filters must not change
+  std::vector<u8> pcm_map;            // block whose samples the loop filters must not change
+                                      // (PCM with pcm_loop_filter_disabled, transquant bypass)
   std::vector<u8> intra_map;          // (constrained intra prediction) intra block
   std::vector<u8> avail;              // decoded-before flags: see intra reference availability
-  std::vector<u16> ctb_slice;         // slice index per CTB
-  std::vector<GpuSlice> slices;
+  std::vector<u16> ctb_slice;         // slice ordinal per CTB
+  std::vector<u16> ctb_tile;          // tile id per CTB (SAO across tile boundaries)
+  bool tiles_block_sao = false;       // several tiles and loop_filter_across_tiles_enabled_flag 0
+  std::vector<GpuSlice> slices;       // per slice ordinal
+  std::vector<GpuWp> wp;              // explicit prediction weights (GpuPu::wp)
   std::vector<GpuSao> sao_params;     // per CTB
   int w4() const { return width >> 2; }
   int h4() const { return height >> 2; }
@@ -147,6 +161,15 @@ VEP_HD u8 hk_clip8(int v) { return u8(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
 // Final prediction sample from the 14-bit intermediates (uni: (p + 32) >> 6, bi: (p0 + p1 + 64) >> 7).
 VEP_HD u8 hk_weight(int p0, int p1, bool bi) { return hk_clip8(bi ? (p0 + p1 + 64) >> 7 : (p0 + 32) >> 6); }
+
+// Explicit weighting (§8.5.3.3.4.3, 8-bit) of component c; `l` is the list of a uni-predicted
+// sample (p0), ignored for bi-prediction (p0 list 0, p1 list 1).
+VEP_HD u8 hk_weight_explicit(const GpuWp& e, int c, int p0, int p1, bool bi, int l) {
+  const int sh = e.shift[c];
+  if (bi) return hk_clip8((p0 * e.w[0][c] + p1 * e.w[1][c] + ((e.o[0][c] + e.o[1][c] + 1) << sh)) >> (sh + 1));
+  const int v = sh >= 1 ? ((p0 * e.w[l][c] + (1 << (sh - 1))) >> sh) + e.o[l][c] : p0 * e.w[l][c] + e.o[l][c];
+  return hk_clip8(v);
+}
 
 // ---------------------------------------------------------------------------- transform
 VEP_HD int hk_basis(int log2, bool dst, int j, int i) {  // basis j (frequency) at sample i

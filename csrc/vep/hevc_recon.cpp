@@ -51,10 +51,10 @@ void inverse_transform(const i32* d, int log2, bool dst, bool tskip, i32* r) {
   }
 }
 
-int dequant_level(int level, int qp, int log2) {
+int dequant_level(int level, int qp, int log2, int m) {
   static constexpr int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
   const int bd = 8 + log2 - 5;
-  const i64 v = ((i64(level) * 16 * kLevelScale[qp % 6]) << (qp / 6)) + (i64(1) << (bd - 1));
+  const i64 v = ((i64(level) * m * kLevelScale[qp % 6]) << (qp / 6)) + (i64(1) << (bd - 1));
   return int(std::clamp<i64>(v >> bd, -32768, 32767));
 }
 
@@ -322,7 +322,24 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
       r[l] = &sl.list[l][size_t(m.ref[l])]->s;
     }
   const bool bi = r[0] && r[1];
-  if (!bi) {  // uni-prediction with a full-sample vector inside the picture: a plain copy
+  // explicit weighted prediction (§8.5.3.3.4.3): the slice's weights of the PU's references
+  const bool wt = sl.sh.weighted;
+  GpuWp e{};
+  if (wt) {
+    for (int c = 0; c < 3; ++c) {
+      e.shift[c] = u8(sl.sh.pwt.log2_denom(c) + 6);
+      for (int l = 0; l < 2; ++l)
+        if (r[l]) {
+          e.w[l][c] = i16(sl.sh.pwt.w[l][m.ref[l]][c]);
+          e.o[l][c] = i16(sl.sh.pwt.o[l][m.ref[l]][c]);
+        }
+    }
+  }
+  const int ul = r[0] ? 0 : 1;  // the list of a uni-predicted PU
+  auto fin = [&](int c, int p0, int p1) -> u8 {
+    return wt ? hk_weight_explicit(e, c, p0, p1, bi, ul) : hk_weight(p0, p1, bi);
+  };
+  if (!bi && !wt) {  // uni-prediction with a full-sample vector inside the picture: a plain copy
     const int l = r[0] ? 0 : 1;
     const HostSurface& s = *r[l];
     const int mx = m.mv[l][0], my = m.mv[l][1];
@@ -345,10 +362,7 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
   for (int l = 0; l < 2; ++l)
     if (r[l]) mc_luma(*r[l], xPb + (m.mv[l][0] >> 2), yPb + (m.mv[l][1] >> 2), w, h, m.mv[l][0] & 3, m.mv[l][1] & 3, p[np++]);
   for (int j = 0; j < h; ++j)
-    for (int i = 0; i < w; ++i) {
-      const int v = bi ? (p[0][j * w + i] + p[1][j * w + i] + 64) >> 7 : (p[0][j * w + i] + 32) >> 6;
-      y[j * ys + i] = u8(std::clamp(v, 0, 255));
-    }
+    for (int i = 0; i < w; ++i) y[j * ys + i] = fin(0, p[0][j * w + i], bi ? p[1][j * w + i] : 0);
   const int xc = xPb / 2, yc = yPb / 2, wc = w / 2, hc = h / 2;
   for (int c = 0; c < 2; ++c) {
     np = 0;
@@ -358,10 +372,7 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
                   p[np++]);
     u8* out = c == 0 ? cb : cr;
     for (int j = 0; j < hc; ++j)
-      for (int i = 0; i < wc; ++i) {
-        const int v = bi ? (p[0][j * wc + i] + p[1][j * wc + i] + 64) >> 7 : (p[0][j * wc + i] + 32) >> 6;
-        out[j * cs + i] = u8(std::clamp(v, 0, 255));
-      }
+      for (int i = 0; i < wc; ++i) out[j * cs + i] = fin(1 + c, p[0][j * wc + i], bi ? p[1][j * wc + i] : 0);
   }
 }
 
@@ -433,9 +444,13 @@ static bool temporal_mv(const PicCtx& pc, int si, int xPb, int yPb, int nPbW, in
       for (int p : sl.list_poc[l]) no_backward &= p <= pc.poc;
     lc = no_backward ? X : (sh.collocated_from_l0 ? 1 : 0);
   }
+  // LongTermRefPic of the target and of the collocated vector's reference must agree; a
+  // long-term target takes the vector unscaled (§8.5.3.2.8)
+  const bool cur_lt = sl.list_lt[X][size_t(refIdx)] != 0;
+  if (cur_lt != (((c.lt >> lc) & 1) != 0)) return false;
   const int col_diff = col->poc - c.poc[lc];
   const int cur_diff = pc.poc - sl.list_poc[X][size_t(refIdx)];
-  if (col_diff == cur_diff || col_diff == 0) {
+  if (cur_lt || col_diff == cur_diff || col_diff == 0) {
     mv[0] = c.mv[lc][0];
     mv[1] = c.mv[lc][1];
   } else {
@@ -549,13 +564,16 @@ void amvp_candidates(const PicCtx& pc, int si, int xCb, int yCb, int nCbS, int x
     }
     return false;
   };
+  const bool tlt = sl.list_lt[X][size_t(refIdx)] != 0;
   auto second_pass = [&](const MvField& m, i16 mv[2]) {
+    // a neighbour vector qualifies when its reference's LongTermRefPic equals the target's;
+    // only short-term pairs are scaled (§8.5.3.2.7 steps 7 / 8)
     int l = -1;
-    if ((m.pred >> X) & 1) l = X;
-    else if ((m.pred >> Y) & 1) l = Y;
+    if ((m.pred >> X) & 1 && (sl.list_lt[X][size_t(m.ref[X])] != 0) == tlt) l = X;
+    else if ((m.pred >> Y) & 1 && (sl.list_lt[Y][size_t(m.ref[Y])] != 0) == tlt) l = Y;
     if (l < 0) return false;
     const int rpoc = sl.list_poc[l][size_t(m.ref[l])];
-    if (rpoc == tpoc) {
+    if (tlt || rpoc == tpoc) {
       mv[0] = m.mv[l][0];
       mv[1] = m.mv[l][1];
     } else {
@@ -627,7 +645,7 @@ std::shared_ptr<std::vector<ColMv>> build_col(const PicCtx& pc, int& col_w) {
       ColMv& c = (*col)[size_t(y) * size_t(col_w) + size_t(x)];
       const int px = x << 4, py = y << 4;
       const MvField& m = pc.mf[pc.i4(px, py)];
-      c = ColMv{{{0, 0}, {0, 0}}, {0, 0}, 0};
+      c = ColMv{{{0, 0}, {0, 0}}, {0, 0}, 0, 0};
       if (pc.intra[pc.i4(px, py)] || !m.pred) continue;
       const int si = pc.slice[size_t(pc.ctb_of(px, py))];
       if (si >= int(pc.slices.size())) continue;
@@ -638,6 +656,7 @@ std::shared_ptr<std::vector<ColMv>> build_col(const PicCtx& pc, int& col_w) {
           c.mv[l][0] = m.mv[l][0];
           c.mv[l][1] = m.mv[l][1];
           c.poc[l] = sl.list_poc[l][size_t(m.ref[l])];
+          if (sl.list_lt[l][size_t(m.ref[l])]) c.lt |= u8(1 << l);
         }
     }
   return col;
@@ -650,7 +669,7 @@ static int bs_of(const PicCtx& pc, int xp, int yp, int xq, int yq, bool tu_edge,
   if (tu_edge && (pc.cbf[p] || pc.cbf[q])) return 1;
   const MvField& a = pc.mf[p];
   const MvField& b = pc.mf[q];
-  // the same motion in one slice (same lists): same pictures and vectors
+  // the same motion in one slice segment (same lists): same pictures and vectors
   const int slp = one_slice ? 0 : pc.slice[size_t(pc.ctb_of(xp, yp))];
   const int slq = one_slice ? 0 : pc.slice[size_t(pc.ctb_of(xq, yq))];
   if (std::memcmp(&a, &b, sizeof(MvField)) == 0 && slp == slq) return 0;
@@ -691,9 +710,11 @@ void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& 
   const int W = pc.W, H = pc.H;
   bsv.assign(size_t(pc.w4) * pc.h4, 0);
   bsh.assign(size_t(pc.w4) * pc.h4, 0);
-  // single-slice pictures (the common case) skip every per-edge slice lookup
-  const bool one = pc.slices.size() == 1;
+  // single-slice, single-tile pictures (the common case) skip every per-edge slice lookup
+  const bool one = !pc.multi && pc.slices.size() == 1;
   if (one && pc.slices[0].sh.deblocking_disabled) return;
+  const bool tile_edges = pc.col_bd.size() > 2 || pc.row_bd.size() > 2;
+  const bool across_tiles = pc.pps->loop_filter_across_tiles;
   // edges lie on the 8x8 grid: vertical ones in every 8th column, horizontal ones in every 8th row
   for (int dir = 0; dir < 2; ++dir) {
     const u8 tu_flag = dir == 0 ? kEdgeTuV : kEdgeTuH, pu_flag = dir == 0 ? kEdgePuV : kEdgePuH;
@@ -706,11 +727,12 @@ void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& 
         if (!(e & (tu_flag | pu_flag))) continue;
         const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
         if (!one) {
-          const int si = pc.slice[size_t(pc.ctb_of(x, y))];
-          const SliceHeader& sh = pc.slices[size_t(si)].sh;
+          const size_t cq = size_t(pc.ctb_of(x, y)), cp = size_t(pc.ctb_of(xp, yp));
+          const SliceHeader& sh = pc.slices[size_t(pc.slice[cq])].sh;
           if (sh.deblocking_disabled) continue;
-          const int sp = pc.slice[size_t(pc.ctb_of(xp, yp))];
-          if (sp != si && !sh.loop_filter_across_slices) continue;
+          // slice boundary: the current (q) slice's flag decides (§8.7.2.3)
+          if (pc.sord[cp] != pc.sord[cq] && !sh.loop_filter_across_slices) continue;
+          if (tile_edges && !across_tiles && pc.tile[cp] != pc.tile[cq]) continue;
         }
         out[row + size_t(x >> 2)] = u8(bs_of(pc, xp, yp, x, y, (e & tu_flag) != 0, one));
       }
@@ -741,8 +763,8 @@ void deblock_picture(PicCtx& pc) {
         const int qpl = (qpP + qpQ + 1) >> 1;
         const int beta = kBetaTable[std::clamp(qpl + sh.beta_offset, 0, 51)];
         const int tc = kTcTable[std::clamp(qpl + 2 * (b - 1) + sh.tc_offset, 0, 53)];
-        const bool nfp = pc.sps->pcm_loop_filter_disabled && pc.pcm[pc.i4(xp, yp)];
-        const bool nfq = pc.sps->pcm_loop_filter_disabled && pc.pcm[pc.i4(x, y)];
+        const bool nfp = pc.nofilter(pc.i4(xp, yp));
+        const bool nfq = pc.nofilter(pc.i4(x, y));
         // sample access: line k (0..3) along the edge, i = distance from the edge (p: -1-i, q: i)
         auto at = [&](int k, int i) -> u8& {
           return dir == 0 ? s.y[size_t(y + k) * stride + size_t(x + i)] : s.y[size_t(y + i) * stride + size_t(x + k)];
@@ -799,8 +821,8 @@ void deblock_picture(PicCtx& pc) {
         const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? y : y - 1;
         const int qpP = pc.qp[pc.i4(xp, yp)], qpQ = pc.qp[pc.i4(x, y)];
         const SliceHeader& sh = pc.slices[pc.slice[size_t(pc.ctb_of(x, y))]].sh;
-        const bool nfp = pc.sps->pcm_loop_filter_disabled && pc.pcm[pc.i4(xp, yp)];
-        const bool nfq = pc.sps->pcm_loop_filter_disabled && pc.pcm[pc.i4(x, y)];
+        const bool nfp = pc.nofilter(pc.i4(xp, yp));
+        const bool nfq = pc.nofilter(pc.i4(x, y));
         for (int c = 0; c < 2; ++c) {
           const int qc = qpc((qpP + qpQ + 1) >> 1, c);
           const int tc = kTcTable[std::clamp(qc + 2 + sh.tc_offset, 0, 53)];
@@ -835,6 +857,8 @@ void sao_picture(PicCtx& pc) {
       const int si = pc.slice[size_t(ci)];
       if (si == 0xFFFF) continue;
       const SliceHeader& sh = pc.slices[size_t(si)].sh;
+      const int so = pc.sord[size_t(ci)];
+      const bool tiles_cut = (pc.col_bd.size() > 2 || pc.row_bd.size() > 2) && !pc.pps->loop_filter_across_tiles;
       for (int c = 0; c < 3; ++c) {
         if (!sp.type[c] || (c == 0 ? !sh.sao_luma : !sh.sao_chroma)) continue;
         const int sub = c ? 1 : 0;
@@ -851,7 +875,7 @@ void sao_picture(PicCtx& pc) {
         for (int y = y0; y < y0 + h; ++y)
           for (int x = x0; x < x0 + w; ++x) {
             const int lx = x << sub, ly = y << sub;  // luma location of the sample
-            if (pc.sps->pcm_loop_filter_disabled && pc.pcm[pc.i4(lx, ly)]) continue;
+            if (pc.nofilter(pc.i4(lx, ly))) continue;
             const int v = get(src, x, y);
             int off = 0;
             if (sp.type[c] == 1) {
@@ -868,16 +892,21 @@ void sao_picture(PicCtx& pc) {
                   ok = false;
                   break;
                 }
-                const int nsi = pc.slice[size_t(pc.ctb_of(nx << sub, ny << sub))];
-                if (nsi != si) {
+                const size_t nc = size_t(pc.ctb_of(nx << sub, ny << sub));
+                const int nso = pc.sord[nc];
+                if (nso != so) {
                   // the sample that comes later in decoding order decides by its slice's flag
-                  const bool nb_later = nsi > si;
-                  const bool across = nb_later ? pc.slices[size_t(nsi)].sh.loop_filter_across_slices
+                  const bool nb_later = nso > so;
+                  const bool across = nb_later ? pc.slices[size_t(pc.slice[nc])].sh.loop_filter_across_slices
                                                : sh.loop_filter_across_slices;
                   if (!across) {
                     ok = false;
                     break;
                   }
+                }
+                if (tiles_cut && pc.tile[nc] != pc.tile[size_t(ci)]) {
+                  ok = false;
+                  break;
                 }
                 const int nv = get(src, nx, ny);
                 sgn += (v > nv) - (v < nv);

@@ -10,7 +10,7 @@ namespace vep::hevc {
 // residual samples r (§8.6.4): DCT, 4x4 DST (intra luma) or transform skip.
 void inverse_transform(const i32* d, int log2, bool dst, bool tskip, i32* r);
 // Scaling of one coefficient level (§8.6.3, flat scaling: m = 16).
-int dequant_level(int level, int qp, int log2);
+int dequant_level(int level, int qp, int log2, int m = 16);  // m: ScalingFactor (16 = flat)
 // Intra sample prediction (§8.4.4.2.4-6) of an n x n block from the (substituted, filtered)
 // references: top[x + 1] = p[x][-1] for x = -1 .. 2n-1, left[y] = p[-1][y] for y = 0 .. 2n-1.
 void intra_predict(const int* top, const int* left, int log2, int mode, bool luma, u8* out, int stride,

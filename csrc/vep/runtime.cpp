@@ -1028,6 +1028,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const hevc::GpuPicture* p;
     int job;
     size_t off_pu, off_tu, off_coef, off_pcm, off_bsv, off_bsh, off_qp, off_pcmmap, off_cslice, off_slices, off_sao;
+    size_t off_wp, off_ctile;
   };
   std::vector<HevcPic> hpics;
   int hrounds = 0;
@@ -1045,7 +1046,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       VEP_CHECK(((p.width + 15) & ~15) == jobs[size_t(i)].pic.coded_width &&
                     ((p.height + 15) & ~15) == jobs[size_t(i)].pic.coded_height,
                 "picture size differs from the camera's surfaces");
-      HevcPic a{&p, i, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+      HevcPic a{&p, i, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
       auto put = [&](size_t bytes) {
         const size_t o = need;
         need += al(std::max<size_t>(bytes, 16));
@@ -1062,6 +1063,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       a.off_cslice = put(p.ctb_slice.size() * sizeof(u16));
       a.off_slices = put(p.slices.size() * sizeof(hevc::GpuSlice));
       a.off_sao = put(p.sao_params.size() * sizeof(hevc::GpuSao));
+      a.off_wp = put(p.wp.size() * sizeof(hevc::GpuWp));
+      a.off_ctile = put(p.ctb_tile.size() * sizeof(u16));
       maxl = std::max(maxl, int(p.level_begin.size()) - 1);
       hround_pics[size_t(r)].push_back(int(hpics.size()));
       hpics.push_back(a);
@@ -1157,6 +1160,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     add(p.ctb_slice.data(), p.ctb_slice.size() * sizeof(u16), a.off_cslice);
     add(p.slices.data(), p.slices.size() * sizeof(hevc::GpuSlice), a.off_slices);
     add(p.sao_params.data(), p.sao_params.size() * sizeof(hevc::GpuSao), a.off_sao);
+    add(p.wp.data(), p.wp.size() * sizeof(hevc::GpuWp), a.off_wp);
+    add(p.ctb_tile.data(), p.ctb_tile.size() * sizeof(u16), a.off_ctile);
   }
   std::vector<std::vector<const u8*>> seg_dev(static_cast<size_t>(n));
   auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
@@ -1336,7 +1341,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.target = p.target;
       g.cb_qp_offset = p.cb_qp_offset;
       g.cr_qp_offset = p.cr_qp_offset;
-      g.flags = (p.deblock ? 1 : 0) | (p.sao ? 2 : 0) | (p.pcm_nofilter ? 4 : 0);
+      g.flags = (p.deblock ? 1 : 0) | (p.sao ? 2 : 0) | (p.pcm_nofilter ? 4 : 0) | (p.tiles_block_sao ? 8 : 0);
       g.pus = st.d + a.off_pu;
       g.tus = st.d + a.off_tu;
       g.coefs = reinterpret_cast<const i16*>(st.d + a.off_coef);
@@ -1348,6 +1353,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.ctb_slice = reinterpret_cast<const u16*>(st.d + a.off_cslice);
       g.slices = st.d + a.off_slices;
       g.sao = st.d + a.off_sao;
+      g.wp = st.d + a.off_wp;
+      g.ctb_tile = reinterpret_cast<const u16*>(st.d + a.off_ctile);
       const size_t scratch = size_t(j.hevc_slots);  // the extra surface after the DPB slots
       VEP_CHECK(c->surface.slots > j.hevc_slots, "camera surfaces lack the SAO scratch slot");
       g.sao_y = c->surface.y + scratch * c->surface.slot_y();

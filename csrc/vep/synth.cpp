@@ -88,6 +88,14 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
     hc.coverage = cfg.coverage;
     hc.noise = cfg.noise;
     hc.temporal_noise = cfg.temporal_noise;
+    hc.tile_cols = cfg.tile_cols;
+    hc.tile_rows = cfg.tile_rows;
+    hc.wpp = cfg.wpp;
+    hc.segments = cfg.segments;
+    hc.scaling_lists = cfg.scaling_lists;
+    hc.weighted = cfg.weighted_p || cfg.weighted_b;
+    hc.long_term = cfg.long_term;
+    hc.lossless = cfg.lossless;
     auto enc = std::make_unique<hevc::HevcEncoder>(hc);
     vps_nal_ = enc->vps_nal();
     avc_ = std::move(enc);

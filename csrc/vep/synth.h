@@ -43,6 +43,14 @@ struct SynthConfig {
   bool weighted_p = false;   // main / high: explicit weighted prediction in P slices
   int weighted_b = 0;        // main / high: weighted_bipred_idc
   bool direct_spatial = true;
+  // H.265 stream structure / tools (hevc::HevcEncConfig; weighted_p turns on HEVC weighted
+  // prediction in P and B slices)
+  int tile_cols = 1, tile_rows = 1;
+  bool wpp = false;
+  int segments = 1;
+  bool scaling_lists = false;
+  bool long_term = false;
+  bool lossless = false;
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)
