@@ -1234,4 +1234,5 @@ PYBIND11_MODULE(_vep, m) {
 
   bind_net(m);
   bind_mux(m);
+  bind_hevc(m);
 }

@@ -371,8 +371,8 @@ VEP_HD int hk_chroma_qp(int qpi) {
 // Chroma filtering of the 2 chroma lines of one 4-luma-line segment (bS 2 edges only).
 VEP_HD void hk_deblock_chroma(u8* base, int along, int across, int qpP, int qpQ, int cqp_offset, int tc_offset,
                               bool nfp, bool nfq) {
-  int qpi = ((qpP + qpQ + 1) >> 1) + cqp_offset;
-  qpi = qpi < 0 ? 0 : (qpi > 57 ? 57 : qpi);
+  // §8.7.2.5.5: QpC from Table 8-10 of qPi (no clipping of qPi: that is the CU-level rule)
+  const int qpi = ((qpP + qpQ + 1) >> 1) + cqp_offset;
   int ti = hk_chroma_qp(qpi) + 2 + tc_offset;
   const int tc = kTcTable[ti < 0 ? 0 : (ti > 53 ? 53 : ti)];
   for (int k = 0; k < 2; ++k) {

@@ -748,7 +748,7 @@ void deblock_picture(PicCtx& pc) {
   std::vector<u8> bsv, bsh;
   deblock_strengths(pc, bsv, bsh);
   auto qpc = [&](int qpi, int c) {
-    return hevc_chroma_qp(std::clamp(qpi + (c == 0 ? pc.pps->cb_qp_offset : pc.pps->cr_qp_offset), 0, 57));
+    return hevc_chroma_qp(qpi + (c == 0 ? pc.pps->cb_qp_offset : pc.pps->cr_qp_offset));  // (no qPi clipping)
   };
   for (int dir = 0; dir < 2; ++dir) {
     const std::vector<u8>& bs = dir == 0 ? bsv : bsh;
