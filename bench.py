@@ -96,6 +96,13 @@ def parse_args():
                     help="replay = pre-encoded AUs fed to the decode pipeline (decode-only); rtsp = an "
                          "in-process loopback RTSP camera farm, unthrottled, with the production "
                          "ingest (RtspClient + RTP depacketizer + lazy decoder) inside the timed loop")
+    ap.add_argument("--rtmp", action="store_true",
+                    help="BASELINE config 5: every camera's RTMP pass-through on, to a loopback RTMP server "
+                         "(rtsp source)")
+    ap.add_argument("--annotate", action="store_true",
+                    help="BASELINE config 5: Annotate RPCs during the timed region, uploaded by the production "
+                         "queue + batch consumer to a loopback cloud endpoint (rtsp source)")
+    ap.add_argument("--annotate-rate", type=float, default=5.0, help="annotations per camera per second")
     ap.add_argument("--keyframe-only", action="store_true",
                     help="BASELINE config 3 (selective I-frame decode): every camera in keyframe-only "
                          "mode (the reference's read_image.py --keyframe_only); needs --source rtsp so "
@@ -109,6 +116,8 @@ def parse_args():
     a = ap.parse_args()
     if a.keyframe_only and a.source != "rtsp":
         ap.error("--keyframe-only needs --source rtsp (the ingest filters the access units)")
+    if (a.rtmp or a.annotate) and a.source != "rtsp":
+        ap.error("--rtmp / --annotate need --source rtsp")
     if a.qp is None:
         a.qp = 27 if a.profile == "baseline" else 25
     if a.temporal_noise is None:
@@ -214,23 +223,38 @@ class RtspFarm:
         self.srv = vep.RtspServer("127.0.0.1", 0)
         self.cams = a.cams_per_gpu
         self.stream_bytes = 0
-        for i in range(self.cams):
+
+        def add(i):  # (the farm pre-encodes each camera's GOPs: in parallel, GIL released)
             c = make_cfg(vep, a, rank, compressed)
             c.seed = c.seed + i * 7919
             c.idr_phase = (i * a.gop) // self.cams  # unsynchronised cameras
             self.srv.add_stream(f"/cam{i}", c, realtime=False, cached_frames=a.gop * a.cache_gops)
+
+        from concurrent.futures import ThreadPoolExecutor
+
+        with ThreadPoolExecutor(max(1, min(self.cams, (os.cpu_count() or 4), 16))) as ex:
+            list(ex.map(add, range(self.cams)))
         self.srv.start()
+        # BASELINE config 5: RTMP pass-through of every camera to a loopback RTMP server
+        self.sink = None
+        if a.rtmp:
+            self.sink = vep.RtmpSink("127.0.0.1", 0)
+            self.sink.set_keep_bodies(False)
+            self.sink.start()
         worker.start()
         self.idx = [worker.add_camera(f"r{rank}rtsp{i}", a.ring_slots) for i in range(self.cams)]
         for cam in self.idx:
             worker.set_keyframe_only(cam, a.keyframe_only)
+            if self.sink is not None:
+                worker.set_proxy(cam, True)
         self._touch()
         self.sessions = []
         for i, cam in enumerate(self.idx):
             # lossless: while a camera's parse backlog is deep its socket is paused (TCP
             # back-pressure on the unthrottled farm) instead of dropping AUs to the next keyframe
+            rtmp = f"rtmp://127.0.0.1:{self.sink.port}/live/r{rank}cam{i}" if self.sink is not None else ""
             sess = vep.IngestSession(worker, cam, f"r{rank}rtsp{i}", f"rtsp://127.0.0.1:{self.srv.port}/cam{i}",
-                                     lossless=True)
+                                     rtmp_url=rtmp, lossless=True)
             sess.start()
             self.sessions.append(sess)
         self.stop_evt = threading.Event()
@@ -255,9 +279,14 @@ class RtspFarm:
 
     def stats(self):
         st = [self.worker.stats(c) for c in self.idx]
-        return {"packets": sum(x["packets"] for x in st), "bytes_in": sum(x["bytes_in"] for x in st),
-                "errors": sum(x["errors"] for x in st), "decoded": sum(x["decoded"] for x in st),
-                "skipped": sum(x["skipped"] for x in st)}
+        out = {"packets": sum(x["packets"] for x in st), "bytes_in": sum(x["bytes_in"] for x in st),
+               "errors": sum(x["errors"] for x in st), "decoded": sum(x["decoded"] for x in st),
+               "skipped": sum(x["skipped"] for x in st)}
+        if self.sink is not None:
+            out["rtmp_messages"] = self.sink.video_messages
+            out["rtmp_bytes"] = self.sink.video_bytes
+            out["rtmp_keyframes"] = self.sink.keyframes
+        return out
 
     def go_live(self, fps, timeout_s=20.0):
         """Switch the farm to real time and wait until the ingest backlog of the unthrottled run has
@@ -277,6 +306,8 @@ class RtspFarm:
         for sess in self.sessions:
             sess.stop()
         self.srv.stop()
+        if self.sink is not None:
+            self.sink.stop()
         self.worker.stop()
 
 
@@ -300,7 +331,14 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
     farm = RtspFarm(vep, worker, a, rank, compressed)
     lat = None
     live_fps = None
+    annot = None
+    side = {}
     try:
+        if a.annotate:  # (runs from the warmup on: the counts cover warmup + timed region)
+            from video_edge_ai_proxy_amd.server.bench_pipeline import AnnotationLoad
+
+            annot = AnnotationLoad([f"r{rank}rtsp{i}" for i in range(cams)], rate=a.annotate_rate)
+            annot.start()
         farm.wait_pictures(cams * max(1, a.warmup), timeout_s=300.0)
         if world > 1:
             dist.barrier()
@@ -329,6 +367,19 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         errors = s1["errors"] - s0["errors"]
         aus = s1["packets"] - s0["packets"]  # access units through Camera::on_access_unit
         skipped = s1["skipped"] - s0["skipped"]  # AUs the ingest dropped (parse backlog full)
+        if farm.sink is not None:
+            side["rtmp_passthrough"] = {
+                "video_messages": s1["rtmp_messages"] - s0["rtmp_messages"],
+                "video_bytes": s1["rtmp_bytes"] - s0["rtmp_bytes"],
+                "keyframes": s1["rtmp_keyframes"] - s0["rtmp_keyframes"],
+                "messages_per_s": round((s1["rtmp_messages"] - s0["rtmp_messages"]) / elapsed, 1),
+                "definition": "FLV video messages the loopback RTMP server received from the cameras' pass-through "
+                              "senders during the timed region (packet copy, no transcode)"}
+        if annot is not None:
+            side["annotation"] = annot.stop()
+            side["annotation"]["rate_per_camera_per_s"] = a.annotate_rate
+            annot.close()
+            annot = None
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -351,6 +402,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             if world > 1:
                 dist.barrier()
     finally:
+        if annot is not None:
+            annot.close()
         farm.close()
         if pool is not None:
             pool.close()
@@ -408,6 +461,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         if lat is not None:
             res.update(latency_fields(a, lat, live_fps))
             res["latency_farm_settled"] = lat["settled"]
+        res.update(side)  # (rank 0's side loads)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -78,6 +78,8 @@ void bind_mux(py::module_& m) {
       .def_property_readonly("hevc_messages", &mux::RtmpSink::hevc_messages)
       .def_property_readonly("sequence_headers", &mux::RtmpSink::sequence_headers)
       .def_property_readonly("stream_key", &mux::RtmpSink::last_stream_key)
+      .def_property_readonly("video_bytes", &mux::RtmpSink::video_bytes)
+      .def("set_keep_bodies", &mux::RtmpSink::set_keep_bodies)
       .def("video_bodies", [](const mux::RtmpSink& s) {
         py::list l;
         for (auto& b : s.video_bodies()) l.append(B(b));

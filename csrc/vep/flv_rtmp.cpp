@@ -507,7 +507,8 @@ void RtmpSink::serve(int fd) {
             if ((body[0] >> 4) == 1) keys_.fetch_add(1);
           }
         }
-        bodies_.push_back(std::move(body));
+        bytes_.fetch_add(body.size());
+        if (keep_bodies_) bodies_.push_back(std::move(body));
         continue;
       }
       if (type != 20) continue;

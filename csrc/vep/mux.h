@@ -70,6 +70,9 @@ class RtmpSink {
   u64 hevc_messages() const { return hevc_.load(); }  // enhanced-RTMP 'hvc1' video messages
   std::string last_stream_key() const;
   std::vector<std::vector<u8>> video_bodies() const;  // FLV VIDEODATA bodies in arrival order
+  u64 video_bytes() const { return bytes_.load(); }
+  // false: count the video messages only (long-running loads; bodies are not retained)
+  void set_keep_bodies(bool on) { keep_bodies_ = on; }
 
  private:
   void serve(int fd);
@@ -78,7 +81,8 @@ class RtmpSink {
   std::atomic<bool> stop_{false};
   std::thread acc_;
   std::atomic<int> live_{0};
-  std::atomic<u64> video_{0}, keys_{0}, seqhdr_{0}, hevc_{0};
+  std::atomic<u64> video_{0}, keys_{0}, seqhdr_{0}, hevc_{0}, bytes_{0};
+  std::atomic<bool> keep_bodies_{true};
   mutable std::mutex mu_;
   std::string key_;
   std::vector<std::vector<u8>> bodies_;

@@ -197,3 +197,39 @@ def test_hostprof_samples_native_threads(native, tmp_path):
     rows = [l.split(maxsplit=3) for l in out.read_text().splitlines()]
     assert n > 0 and sum(int(r[0]) for r in rows) == min(n, 1 << 21)
     assert any("_vep" in r[1] for r in rows)  # samples inside the extension, with offsets
+
+
+def test_bench_config5_rtmp_annotation_cpu():
+    """BASELINE config 5 shape on the CPU backend: H.265 cameras through the live ingest with RTMP
+    pass-through to a loopback RTMP server and Annotate RPCs uploaded by the production queue +
+    batch consumer to a loopback cloud endpoint; the JSON reports all three."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--codec", "h265", "--rtmp", "--annotate",
+           "--annotate-rate", "20", "--steps", "6", "--warmup", "2", "--width", "128", "--height", "96",
+           "--cams-per-gpu", "2", "--gop", "8", "--letterbox", "32", "--clients", "2", "--client-procs", "1",
+           "--latency-seconds", "1", "--latency-samples", "5", "--threads", "2"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["source"] == "rtsp" and d["frames_dropped"] == 0 and d["decode_errors"] == 0
+    assert d["access_units_skipped"] == 0
+    assert d["rtmp_passthrough"]["video_messages"] > 0 and d["rtmp_passthrough"]["video_bytes"] > 0
+    ann = d["annotation"]
+    assert ann["annotate_rpcs"] > 0 and ann["annotate_rpc_errors"] == 0 and not ann["error"]
+    assert ann["annotations_uploaded"] == ann["annotate_rpcs"] and ann["unsigned_posts"] == 0
+    assert d["p50_latency_ms"] is not None and d["serve_p50_latency_ms"] is not None
+
+
+def test_bench_eight_ranks_gloo():
+    """World = 8 rehearsal of the camera-DP bench (gloo, CPU backend): rank spawn, barriers, the
+    all-gather of the consumer batch every step, the MAX / SUM reductions and rank 0's JSON."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--steps", "3", "--warmup", "1", "--cpu", "--width", "64", "--height", "48",
+           "--cams-per-gpu", "1", "--letterbox", "16", "--latency-samples", "2", "--clients", "1",
+           "--client-procs", "1", "--latency-seconds", "1", "--threads", "1", "--gop", "6"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=600, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["n_ranks"] == 8 and d["config"]["global_batch"] == 8 and d["config"]["all_gather"]
+    assert d["config"]["parallelism"] == "camera-dp8" and d["frames_dropped"] == 0 and d["value"] > 0
