@@ -311,6 +311,18 @@ class RtspFarm:
         self.worker.stop()
 
 
+def avc_cycles_per_mb(worker) -> dict:
+    """VEP_AVC_PROF=1: the H.264 wavefront kernels' per-phase clocks, per macroblock."""
+    pr = worker.avc_profile()
+    out = {}
+    for ph in ("intra", "dbk"):
+        n = max(1, pr[f"{ph}_mbs"])
+        out[f"{ph}_cycles_per_mb"] = {k[len(ph) + 1:]: round(v / n, 1) for k, v in pr.items()
+                                      if k.startswith(ph) and not k.endswith("mbs")}
+        out[f"{ph}_mbs"] = pr[f"{ph}_mbs"]
+    return out
+
+
 def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed, pool):
     """`--source rtsp`: the timed loop waits for the live pipeline (loopback RTSP farm ->
     IngestSession -> lazy decoder -> Worker batches) to decode `cams` more pictures per step."""
@@ -344,6 +356,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             dist.barrier()
         sync()
         p0, f0, d0, s0 = worker.pictures, worker.frames, worker.dropped, farm.stats()
+        rg0 = worker.records_gathered
         g0 = worker.gpu_ms_total
         handle = None
         t0 = time.perf_counter()
@@ -453,11 +466,15 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "decode_errors": errors,
             "concurrent_clients": a.clients,
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "rank0_record_bytes_gathered_per_step": (worker.records_gathered - rg0) // max(1, a.steps),
+            "keyframe_coalesce_window_us": worker.kf_window_us if a.keyframe_only else None,
             "parse_threads_per_rank": a.threads,
             "rocdecode_available": bool(vep.rocdecode_available()),
             "decoder_backend": decoder_backend(a, compressed),
             "per_gpu_fps": round(fps / max(world, 1), 2),
         }
+        if os.environ.get("VEP_AVC_PROF") == "1":
+            res.update(avc_cycles_per_mb(worker))
         if lat is not None:
             res.update(latency_fields(a, lat, live_fps))
             res["latency_farm_settled"] = lat["settled"]
@@ -471,14 +488,18 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         sys.exit(3)
 
 
-def payload_path(a, compressed, worker, ip0, sg0):
+def payload_path(a, compressed, worker, ip0, sg0, rg0=0):
     """What reaches the GPU per picture, from the worker's own byte counters."""
     inplace = (worker.bytes_inplace - ip0) // max(1, a.steps)
     staged = (worker.bytes_staged - sg0) // max(1, a.steps)
     if compressed:
+        gathered = (worker.records_gathered - rg0) // max(1, a.steps)
+        how = ("the H.264 records sit in pinned pool memory and a gather kernel pulls them over PCIe "
+               "(no host copy); the H.265 records are copied into the pinned staging buffer and sent H2D"
+               if gathered else "copied into the pinned staging buffer by the host and sent H2D per batch")
         return {"gpu_input": "per-macroblock reconstruction records (modes, motion vectors, dequantised "
-                             "coefficients) built by the host parse and copied H2D per batch; slice bytes "
-                             "never reach the GPU",
+                             "coefficients) built by the host parse; " + how + "; slice bytes never reach the GPU",
+                "record_bytes_gathered_per_step": gathered,
                 "slice_bytes_read_in_place_per_step": inplace, "slice_bytes_staged_per_step": staged}
     return {"gpu_input": "I_PCM slice bytes: the decode kernel reads them from pinned host memory over PCIe"
                          if worker.direct_reads else "I_PCM slice bytes gathered into HBM, decode reads HBM",
@@ -597,7 +618,7 @@ def main():
     f0, p0, b0, g0 = worker.frames, rb.parse_ms, rb.batch_ms, worker.gpu_ms_total
     d0, pf0, l0 = worker.dropped, rb.parse_failures, rb.frames
     pw0 = rb.parse_wait_ms
-    ip0, sg0 = worker.bytes_inplace, worker.bytes_staged
+    ip0, sg0, rg0 = worker.bytes_inplace, worker.bytes_staged, worker.records_gathered
     tm0 = worker.timings()
     t0 = time.perf_counter()
     for i in range(a.steps):
@@ -689,16 +710,12 @@ def main():
             "parse_threads_per_rank": a.threads,
             "gpu_stages": worker.stages,
             "gpu_inflight_per_lane": worker.inflight,
-            "payload_path": payload_path(a, compressed, worker, ip0, sg0),
+            "payload_path": payload_path(a, compressed, worker, ip0, sg0, rg0),
             "rank0_launch_breakdown_ms_per_step": {
                 k: round((v - tm0[k]) / a.steps, 4) for k, v in tm1.items()},
         }
         if os.environ.get("VEP_AVC_PROF") == "1":
-            pr = worker.avc_profile()
-            for ph in ("intra", "dbk"):
-                n = max(1, pr[f"{ph}_mbs"])
-                res[f"{ph}_cycles_per_mb"] = {k[len(ph) + 1:]: round(v / n, 1) for k, v in pr.items()
-                                              if k.startswith(ph) and not k.endswith("mbs")}
+            res.update(avc_cycles_per_mb(worker))
         if lat is not None:
             res.update(latency_fields(a, lat))
         print(json.dumps(res), flush=True)

@@ -45,6 +45,12 @@ static py::dict meta_dict(const FrameMeta& m) {
   return d;
 }
 
+// Worst case of a VideoFrame's trailer (everything after the pixel data): 7 varint fields
+// (<= 11 B each), 2 bools, frame_type, time_base, shape, device_id.
+static size_t video_frame_suffix_max(const std::string& device_id) {
+  return 7 * 11 + 2 * 2 + 3 + 9 + 48 + 12 + device_id.size();
+}
+
 static py::dict pic_dict(const PictureInfo& p) {
   py::dict d;
   d["width"] = p.width;
@@ -418,7 +424,7 @@ PYBIND11_MODULE(_vep, m) {
   struct HevcRecords {
     hevc::Decoder d;
     std::vector<HostSurface> slots;
-    u64 pictures = 0, pus = 0, tus = 0, intra_tus = 0, max_level = 0;
+    u64 pictures = 0, pus = 0, tus = 0, intra_tus = 0, max_level = 0, exchange_violations = 0;
     HevcRecords() { d.set_gpu_mode(true); }
     py::list frames(const std::vector<hevc::FramePtr>& fs) {
       py::list l;
@@ -453,6 +459,7 @@ PYBIND11_MODULE(_vep, m) {
         pus += p->pus.size();
         tus += p->tus.size();
         for (const auto& t : p->tus) intra_tus += (t.flags & hevc::kTuIntra) ? 1 : 0;
+        exchange_violations += hevc::exchange_violations(*p);
         max_level = std::max<u64>(max_level, p->level_begin.empty() ? 0 : p->level_begin.size() - 1);
       }
     }
@@ -483,6 +490,7 @@ PYBIND11_MODULE(_vep, m) {
         s["tus"] = r.tus;
         s["intra_tus"] = r.intra_tus;
         s["max_levels"] = r.max_level;
+        s["exchange_violations"] = r.exchange_violations;
         s["slots"] = r.d.gpu_slots();
         return s;
       });
@@ -869,7 +877,7 @@ PYBIND11_MODULE(_vep, m) {
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
                        std::vector<float> stdv, int max_cameras, int pack_threads,
                        int letterbox_format, int lanes, int stages, int queue, bool lane_threads,
-                       const std::string& decoder) {
+                       const std::string& decoder, int kf_window_us) {
              WorkerOptions o;
              o.device = device;
              if (decoder == "native") o.decoder = kDecoderNative;
@@ -880,6 +888,7 @@ PYBIND11_MODULE(_vep, m) {
              o.stages = stages;
              o.queue = queue;
              o.lane_threads = lane_threads;
+             o.kf_window_us = kf_window_us;
              o.pack_threads = pack_threads;
              o.letterbox_format = letterbox_format;
              o.letterbox_size = letterbox_size;
@@ -895,7 +904,9 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("mean") = std::vector<float>{}, py::arg("std") = std::vector<float>{},
            py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
            py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0,
-           py::arg("queue") = 0, py::arg("lane_threads") = false, py::arg("decoder") = "native")
+           py::arg("queue") = 0, py::arg("lane_threads") = false, py::arg("decoder") = "native",
+           py::arg("kf_window_us") = -1)
+      .def_property_readonly("kf_window_us", &Worker::kf_window_us)
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def_property_readonly("decoder", [](Worker& w) { return std::string(w.vcn() ? "vcn" : "native"); })
       .def_property_readonly("lanes", &Worker::lanes)
@@ -1017,6 +1028,55 @@ PYBIND11_MODULE(_vep, m) {
              return py::make_tuple(meta_dict(m), out);
            },
            py::arg("idx"), py::arg("after") = 0)
+      .def("video_frame_bound",
+           // Upper bound of the serialized VideoFrame of this camera's current ring (0: no ring).
+           [](Worker& w, int i, const std::string& device_id) -> size_t {
+             std::shared_ptr<FrameRing> ring = cam_of(w, i).ring();
+             if (!ring) return 0;
+             FrameMeta probe{};
+             probe.width = ring->width();
+             probe.height = ring->height();
+             return encode_video_frame(probe, ring->slot_bytes(), device_id).first.size() +
+                    ring->slot_bytes() + video_frame_suffix_max(device_id);
+           },
+           py::arg("idx"), py::arg("device_id") = "")
+      .def("video_frame_into",
+           // The serialized VideoFrame written into caller memory at `addr` (e.g. a shared-memory
+           // segment the front-end process maps): (seq, length, meta), None if no newer frame, or
+           // the needed size (int) if `cap` is too small. pinned: the range is register_host()ed,
+           // so the pixels arrive by one DMA with no staging copy.
+           [](Worker& w, int i, i64 after, const std::string& device_id, uintptr_t addr, size_t cap,
+              bool pinned) -> py::object {
+             std::shared_ptr<Camera> cp = cam_ref(w, i);
+             std::shared_ptr<FrameRing> ring = cp->ring();
+             if (!ring) return py::none();
+             const size_t n = ring->slot_bytes();
+             FrameMeta probe;
+             int slot;
+             if (!ring->latest(after, &probe, &slot)) return py::none();
+             const std::string pre = encode_video_frame(probe, n, device_id).first;
+             const size_t need = pre.size() + n + video_frame_suffix_max(device_id);
+             if (cap < need) return py::int_(need);
+             char* buf = reinterpret_cast<char*>(addr);
+             std::memcpy(buf, pre.data(), pre.size());
+             FrameMeta m;
+             bool ok;
+             {
+               py::gil_scoped_release r;
+               ok = w.read_latest(*ring, after, &m, reinterpret_cast<u8*>(buf) + pre.size(), n, pinned);
+             }
+             if (!ok) return py::none();
+             auto [pre2, suf] = encode_video_frame(m, n, device_id);
+             VEP_CHECK(pre2 == pre && suf.size() <= video_frame_suffix_max(device_id),
+                       "VideoFrame header changed while serving");
+             std::memcpy(buf + pre.size() + n, suf.data(), suf.size());
+             return py::make_tuple(m.seq, pre.size() + n + suf.size(), meta_dict(m));
+           },
+           py::arg("idx"), py::arg("after"), py::arg("device_id"), py::arg("addr"), py::arg("cap"),
+           py::arg("pinned") = false)
+      .def("register_host",
+           [](Worker& w, uintptr_t addr, size_t n) { return w.register_host(reinterpret_cast<void*>(addr), n); })
+      .def("unregister_host", [](Worker& w, uintptr_t addr) { w.unregister_host(reinterpret_cast<void*>(addr)); })
       .def("video_frame",
            // Serialized VideoFrame proto, built in place in its final bytes object: header, the
            // slot's pixels (D2H through a pinned pool buffer, GIL released), trailer; the object
@@ -1031,9 +1091,7 @@ PYBIND11_MODULE(_vep, m) {
              if (!ring->latest(after, &probe, &slot)) return py::none();
              // the prefix holds width, height and the data length: fixed for this ring
              const std::string pre = encode_video_frame(probe, n, device_id).first;
-             // the trailer's worst case: 7 varint fields (<= 11 B each), 2 bools, frame_type,
-             // time_base, shape, device_id
-             const size_t suf_max = 7 * 11 + 2 * 2 + 3 + 9 + 48 + 12 + device_id.size();
+             const size_t suf_max = video_frame_suffix_max(device_id);
              PyObject* b = PyBytes_FromStringAndSize(nullptr, Py_ssize_t(pre.size() + n + suf_max));
              if (!b) throw py::error_already_set();
              char* buf = PyBytes_AS_STRING(b);
@@ -1116,6 +1174,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("pictures", &Worker::pictures)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
       .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)
+      .def_property_readonly("records_gathered", &Worker::records_gathered)
       .def_property_readonly("direct_reads", &Worker::direct_reads)
       .def_property_readonly("bytes_staged", &Worker::bytes_staged)
       .def("compute_stream_ptr", [](Worker& w) { return reinterpret_cast<uintptr_t>(w.compute_stream()); });

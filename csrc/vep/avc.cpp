@@ -1021,9 +1021,9 @@ int dpb_slots_for(const Sps& sps) {
 
 PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   auto pic = pic_pool_->acquire([](Picture& p) {  // default state, pool capacities kept
-    std::vector<MbRec> mbs = std::move(p.mbs);
-    std::vector<i16> coefs = std::move(p.coefs), mvs = std::move(p.mvs);
-    std::vector<WpEntry> wps = std::move(p.wps);
+    auto mbs = std::move(p.mbs);
+    auto coefs = std::move(p.coefs), mvs = std::move(p.mvs);
+    auto wps = std::move(p.wps);
     std::vector<OutFrame> outputs = std::move(p.outputs);
     p = Picture{};
     coefs.clear();

@@ -29,6 +29,7 @@
 #include <map>
 #include <memory>
 
+#include "hostmem.h"
 #include "recycle.h"
 #include "avc_recon.h"
 #include "codec.h"
@@ -55,10 +56,12 @@ struct OutFrame {
 // One parsed picture, ready for reconstruction into DPB slot `target`.
 struct Picture {
   int wmbs = 0, hmbs = 0;
-  std::vector<MbRec> mbs;     // raster order
-  std::vector<i16> coefs;     // 16-entry blocks (dequantised, row-major); I_PCM raw samples
-  std::vector<i16> mvs;       // 32 entries (16 x (mvx, mvy), quarter samples) per list per MB
-  std::vector<WpEntry> wps;   // weighted-prediction entries (4 per weighted MB)
+  // Records in pinned pool memory once a GPU worker exists (hostmem::PinnedAllocator): the
+  // worker's gather kernel pulls them over PCIe, no host copy into its staging buffer.
+  hostmem::pinned_vector<MbRec> mbs;     // raster order
+  hostmem::pinned_vector<i16> coefs;     // 16-entry blocks (dequantised, row-major); I_PCM raw samples
+  hostmem::pinned_vector<i16> mvs;       // 32 entries (16 x (mvx, mvy), quarter samples) per list per MB
+  hostmem::pinned_vector<WpEntry> wps;   // weighted-prediction entries (4 per weighted MB)
   int target = 0;             // DPB slot this picture is reconstructed into
   int dpb_slots = 1;          // surfaces the camera needs for this stream
   bool constrained_intra = false;

@@ -101,19 +101,35 @@ struct HevcDesc {
   u8* sao_uv;
   const void* wp;        // hevc::GpuWp (explicit weighted prediction, GpuPu::wp - 1)
   const u16* ctb_tile;   // tile id per CTB
+  u32* err;              // the job's error word (bit 1: a dependency wait timed out)
+  // Intra edge exchange (hevc_tu_queue_kernel): the camera's words, tagged with this round's
+  // epoch, holding the right column / bottom row samples of every intra transform block.
+  u64* xg;
+  i32 xg_h;              // coded height of the exchange's luma plane (width = stride)
+  u32 epoch;             // tag of this round's words (never 0)
   i32 npu, pu_begin;     // exclusive prefix of PUs over the round
   i32 blk_begin;         // exclusive prefix of 4x4 blocks over the round
-  i32 pad;
 };
-// One level's transform blocks of one picture: tus[first .. first + count) of descs[desc].
+// Exchange words of a stride x h picture: luma columns (x % 4 == 3) and rows (y % 4 == 3), then
+// the same for Cb and Cr. 3/4 word per luma sample.
+inline size_t hevc_xg_words(int stride, int h) { return size_t(stride) * size_t(h) * 3 / 4; }
+// Transform blocks tus[first .. first + count) of descs[desc], at tickets begin .. begin + count
+// of their launch (intra queue: level-major, so a block's producers hold lower tickets).
 struct HevcTuRange {
-  i32 desc, first, count, begin;  // begin: exclusive prefix of counts within the level
+  i32 desc, first, count, begin;
 };
 // Motion compensation of every prediction block of the round (one workgroup per block).
 void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s);
-// Transform blocks of one dependency level (level 0: inter residual + PCM; >= 1: intra
-// prediction + residual), one workgroup per block.
-void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, hipStream_t s);
+// Independent transform blocks (level 0: inter residual + PCM; or the blocks of one intra level
+// at tickets base .. base + count of the queue's ranges), one wave per block.
+void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
+                    hipStream_t s);
+// Every intra transform block of the round in ONE launch: persistent waves take tickets in
+// level order from ctr[0] (zero at launch); a block reads the reference samples other intra
+// blocks of the launch write (GpuTu::pend) from their epoch-tagged edge words (HevcDesc::xg),
+// polled until current, and publishes its own right column / bottom row the same way.
+void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, u32* ctr,
+                          hipStream_t s);
 // Deblocking of every vertical (dir 0) or horizontal (dir 1) edge of the round, one thread per
 // 4-line edge segment; then SAO (copy of the deblocked picture, one thread per sample).
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s);

@@ -60,7 +60,12 @@ __device__ inline void wave_sync() {
 
 // Luma residual of an 8x8-transform MB, whole wave: the four 8x8 inverse transforms as 32 row
 // butterflies then 32 column butterflies (lanes 0-31, one 8-point transform each) through the
-// wave's LDS buffer `T` (256 ints); afterwards T holds the MB's 16x16 residual (raster).
+// wave's LDS buffer `T` (kT8Ints ints); afterwards T holds the MB's 16x16 residual (raster).
+// The transpose runs at a row pitch of 9 (and a block pitch of 72): lane (q, i) writes row i of
+// block q, so with pitch 8 the 32 lanes' stores fell on 4 banks (8-way conflicts); with 9 they
+// fall on 32 distinct banks, and the column reads stay conflict-free.
+constexpr int kT8Pitch = 9, kT8Block = 8 * kT8Pitch, kT8Ints = 4 * kT8Block;
+static_assert(kT8Ints >= 256, "the transpose buffer also holds the 16x16 raster result");
 __device__ inline void luma8_residual(const AvcDesc& d, const MbRec& m, int lane, int* T) {
   if (lane < 32) {
     const int q = lane >> 3, i = lane & 7;
@@ -76,14 +81,14 @@ __device__ inline void luma8_residual(const AvcDesc& d, const MbRec& m, int lane
       avc::idct8_1d(v);
     }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) T[q * 64 + i * 8 + k] = v[k];
+    for (int k = 0; k < 8; ++k) T[q * kT8Block + i * kT8Pitch + k] = v[k];
   }
   wave_sync();
   int c[8];
   const int q = (lane >> 3) & 3, j = lane & 7;
   if (lane < 32) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k) c[k] = T[q * 64 + k * 8 + j];
+    for (int k = 0; k < 8; ++k) c[k] = T[q * kT8Block + k * kT8Pitch + j];
     avc::idct8_1d(c);
   }
   wave_sync();  // every lane has read the row pass before the buffer is overwritten
@@ -101,7 +106,7 @@ __device__ inline void luma8_residual(const AvcDesc& d, const MbRec& m, int lane
 // the MB's weighted-prediction entries); 8x8-transform residuals go through LDS.
 __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restrict__ descs, int n,
                                                          int total) {
-  __shared__ int lres[4][256];
+  __shared__ int lres[4][kT8Ints];
   const int wv = int(threadIdx.x) >> 6;
   const int g = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
   if (g >= total) return;  // (wave-uniform; the kernel has no workgroup barrier)

@@ -5,13 +5,15 @@
 //  * hevc_mc_kernel — every prediction block of the round, one 256-lane workgroup per block:
 //    8-tap luma / 4-tap chroma motion compensation from the camera's DPB surfaces with uni- or
 //    bi-prediction. No neighbour dependency: the launch is as wide as the round.
-//  * hevc_tu_kernel, once per dependency level — level 0 adds the inter residuals and copies
-//    PCM blocks; level L >= 1 reconstructs the intra transform blocks whose references were
-//    completed by levels < L (the CPU parser derives the levels from the blocks' reference
-//    areas). One workgroup per block: lane 0 prepares the substituted / filtered references in
-//    LDS, the block's 4..32-point inverse transform runs as two LDS passes, and every lane then
-//    writes prediction + residual for its samples. An I picture's wavefront of blocks therefore
-//    becomes a short sequence of wide launches instead of a serial walk.
+//  * hevc_tu_kernel — level 0: the inter residuals and PCM blocks (independent), one wave per
+//    block, four per workgroup.
+//  * hevc_tu_queue_kernel — every intra transform block of the round in ONE launch. The CPU
+//    parser gives each block a dependency level (1 + the highest level among the intra blocks
+//    its references read); persistent waves take blocks in level order from a ticket counter and
+//    wait on a done counter only when they cross into a new level. Per block the wave prepares
+//    the substituted / filtered references in its LDS, runs the 4..32-point inverse transform as
+//    two LDS passes and writes prediction + residual. An I picture's ~190 dependency levels no
+//    longer cost ~190 launches.
 //  * hevc_deblock_kernel — HEVC filters every vertical edge of the picture before any
 //    horizontal one, and edges 8 samples apart never touch the same samples: one launch per
 //    direction, one lane per 4-line edge segment, no wavefront.
@@ -20,6 +22,8 @@
 //
 // All sample arithmetic comes from hevc_kern.h, shared with the CPU mirror (hevc_gpu.cpp) that
 // is tested bit-exact against the reference decoder.
+#include <algorithm>
+
 #include "gpu.h"
 #include "hevc_kern.h"
 
@@ -106,43 +110,116 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
 }
 
 // ------------------------------------------------------------------------------ TUs
-// Reference samples of an intra block with every lane of the workgroup (the parallel form of
+// One wave per transform block: LDS of the wave (the block's column pass, references and their
+// substitution scratch). Blocks are at most 32x32 = 16 samples per lane.
+struct TuWave {
+  int g[32 * 32];
+  int top[129];
+  int left[128];
+  int sbuf[129], sref[129];
+  u8 sav[132];
+};
+
+__device__ inline void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Intra edge exchange of the queue kernel: 64-bit words (epoch << 32 | sample) accessed with
+// device-scope relaxed atomics, coherent across the XCDs' L2s without fences. Word of component
+// c's sample (x, y) in a column x % 4 == 3 / a row y % 4 == 3 (see gpu::hevc_xg_words).
+__device__ inline u64* xg_col(const HevcDesc& d, int c, int x, int y) {
+  const size_t W = size_t(d.stride), H = size_t(d.xg_h);
+  if (c == 0) return d.xg + size_t(y) * (W >> 2) + size_t(x >> 2);
+  const size_t Wc = W >> 1, Hc = H >> 1, comp = Hc * (Wc >> 2) + (Hc >> 2) * Wc;
+  return d.xg + (W * H >> 1) + size_t(c - 1) * comp + size_t(y) * (Wc >> 2) + size_t(x >> 2);
+}
+__device__ inline u64* xg_row(const HevcDesc& d, int c, int x, int y) {
+  const size_t W = size_t(d.stride), H = size_t(d.xg_h);
+  if (c == 0) return d.xg + H * (W >> 2) + size_t(y >> 2) * W + size_t(x);
+  const size_t Wc = W >> 1, Hc = H >> 1, comp = Hc * (Wc >> 2) + (Hc >> 2) * Wc;
+  return d.xg + (W * H >> 1) + size_t(c - 1) * comp + Hc * (Wc >> 2) + size_t(y >> 2) * Wc + size_t(x);
+}
+__device__ inline void xg_put(u64* p, u32 epoch, u32 v) {
+  __hip_atomic_store(p, u64(epoch) << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline u64 xg_get(const u64* p) {
+  return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr u32 kXgSpinLimit = 1u << 20;  // x s_sleep 1: well under a second per wait
+
+// Reference samples of an intra block with the 64 lanes of a wave (the parallel form of
 // hk_prepare_refs, same result): gather by availability, substitution as "nearest available
-// sample before, else the first available one", then the [1 2 1] / strong filters. All lanes
-// must call it (it synchronises).
-__device__ void prepare_refs_par(const u8* plane, int stride, int step, int x0, int y0, int log2, bool luma, u64 avail,
-                                 int mode, bool strong, int* sbuf, u8* sav, int* sref, int* top, int* left) {
+// sample before, else the first available one", then the [1 2 1] / strong filters. Units in
+// `pend` (queue kernel only) come from the epoch-tagged edge words, polled until current.
+__device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* plane, int stride, int step, int lane,
+                                  TuWave& L) {
+  const int x0 = t.x, y0 = t.y, log2 = t.log2;
+  const bool luma = t.c == 0;
+  const u64 avail = t.avail, pend = d.xg ? t.pend : 0;
   const int n = 1 << log2, g = luma ? 4 : 2, last = 4 * n;
-  const int tid = int(threadIdx.x), nt = int(blockDim.x);
-  for (int k = tid; k <= last; k += nt) {  // scan order: p[-1][2n-1] .. p[-1][-1] .. p[2n-1][-1]
-    bool a;
-    int v = 0;
+  for (int k = lane; k <= last; k += 64) {  // scan order: p[-1][2n-1] .. p[-1][-1] .. p[2n-1][-1]
+    int bit, px, py;
     if (k < 2 * n) {
       const int y = 2 * n - 1 - k;
-      a = (avail >> (1 + y / g)) & 1;
-      if (a) v = plane[(y0 + y) * stride + (x0 - 1) * step];
+      bit = 1 + y / g;
+      px = x0 - 1;
+      py = y0 + y;
     } else if (k == 2 * n) {
-      a = avail & 1;
-      if (a) v = plane[(y0 - 1) * stride + (x0 - 1) * step];
+      bit = 0;
+      px = x0 - 1;
+      py = y0 - 1;
     } else {
       const int x = k - 2 * n - 1;
-      a = (avail >> (17 + x / g)) & 1;
-      if (a) v = plane[(y0 - 1) * stride + (x0 + x) * step];
+      bit = 17 + x / g;
+      px = x0 + x;
+      py = y0 - 1;
     }
-    sbuf[k] = v;
-    sav[k] = a ? 1 : 0;
+    const bool a = (avail >> bit) & 1;
+    const bool xq = a && ((pend >> bit) & 1);  // produced in this launch: poll its edge word
+    int v = 0;
+    if (a && !xq) v = plane[py * stride + px * step];
+    // the corner is on the right column or on the bottom row of the block covering it (a block
+    // reaching right of it / below it): only that block writes either word, so poll both
+    const u64* wp = nullptr;
+    const u64* wp2 = nullptr;
+    u64 w = 0;
+    if (xq) {
+      wp = k <= 2 * n ? xg_col(d, t.c, px, py) : xg_row(d, t.c, px, py);
+      if (k == 2 * n) wp2 = xg_row(d, t.c, px, py);
+      w = xg_get(wp);
+      if (wp2 && u32(w >> 32) != d.epoch) w = xg_get(wp2);
+    }
+    u32 spins = 0;
+    while (__ballot(xq && u32(w >> 32) != d.epoch)) {
+      if (++spins > kXgSpinLimit) {
+        if (xq && u32(w >> 32) != d.epoch) atomicOr(d.err, 2u);  // (the frame is dropped)
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      if (xq && u32(w >> 32) != d.epoch) {
+        w = xg_get(wp);
+        if (wp2 && u32(w >> 32) != d.epoch) w = xg_get(wp2);
+      }
+    }
+    if (xq) v = int(u32(w) & 0xffu);
+    L.sbuf[k] = v;
+    L.sav[k] = a ? 1 : 0;
   }
-  __syncthreads();
-  for (int k = tid; k <= last; k += nt) {
+  wave_sync();
+  for (int k = lane; k <= last; k += 64) {
     int src = -1;
     for (int j = k; j >= 0 && src < 0; --j)
-      if (sav[j]) src = j;
+      if (L.sav[j]) src = j;
     for (int j = k + 1; j <= last && src < 0; ++j)
-      if (sav[j]) src = j;
-    sref[k] = src >= 0 ? sbuf[src] : 128;
+      if (L.sav[j]) src = j;
+    L.sref[k] = src >= 0 ? L.sbuf[src] : 128;
   }
-  __syncthreads();
+  wave_sync();
   // filtering decision (luma): same rule as hk_prepare_refs
+  const int mode = t.mode;
+  const bool strong = (t.flags & hevc::kTuStrong) != 0;
   bool filt = false, strong_f = false;
   if (luma && mode != 1 && n != 4) {
     const int dm = mode - 26 < 0 ? 26 - mode : mode - 26, dh = mode - 10 < 0 ? 10 - mode : mode - 10;
@@ -151,53 +228,45 @@ __device__ void prepare_refs_par(const u8* plane, int stride, int step, int x0, 
     filt = dist > thres;
     if (filt && strong && n == 32) {
       // tl = ref[2n], top[2n] = ref[4n], top[n] = ref[3n], left[2n-1] = ref[0], left[n-1] = ref[n]
-      const int tl = sref[2 * n];
-      const int a1 = tl + sref[4 * n] - 2 * sref[3 * n], a2 = tl + sref[0] - 2 * sref[n];
+      const int tl = L.sref[2 * n];
+      const int a1 = tl + L.sref[4 * n] - 2 * L.sref[3 * n], a2 = tl + L.sref[0] - 2 * L.sref[n];
       strong_f = (a1 < 0 ? -a1 : a1) < 8 && (a2 < 0 ? -a2 : a2) < 8;
     }
   }
-  for (int k = tid; k <= last; k += nt) {
-    int v = sref[k];
+  for (int k = lane; k <= last; k += 64) {
+    int v = L.sref[k];
     if (filt) {
       if (strong_f) {  // bilinear between the corner and the far ends
-        const int tl = sref[2 * n];
+        const int tl = L.sref[2 * n];
         if (k < 2 * n) {
           const int y = 2 * n - 1 - k;
-          if (y < 63) v = ((63 - y) * tl + (y + 1) * sref[0] + 32) >> 6;
+          if (y < 63) v = ((63 - y) * tl + (y + 1) * L.sref[0] + 32) >> 6;
         } else if (k > 2 * n) {
           const int x = k - 2 * n - 1;
-          if (x < 63) v = ((63 - x) * tl + (x + 1) * sref[last] + 32) >> 6;
+          if (x < 63) v = ((63 - x) * tl + (x + 1) * L.sref[last] + 32) >> 6;
         }
       } else if (k > 0 && k < last) {
-        v = (sref[k - 1] + 2 * sref[k] + sref[k + 1] + 2) >> 2;
+        v = (L.sref[k - 1] + 2 * L.sref[k] + L.sref[k + 1] + 2) >> 2;
       }
     }
-    if (k < 2 * n) left[2 * n - 1 - k] = v;
-    else top[k - 2 * n] = v;
+    if (k < 2 * n) L.left[2 * n - 1 - k] = v;
+    else L.top[k - 2 * n] = v;
   }
-  __syncthreads();
+  wave_sync();
 }
 
-__global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict__ descs,
-                                                     const HevcTuRange* __restrict__ ranges, int nranges) {
-  __shared__ int g[32 * 32];
-  __shared__ int top[129];
-  __shared__ int left[128];
-  __shared__ int sbuf[129], sref[129];
-  __shared__ u8 sav[129];
-  const int b = int(blockIdx.x);
-  const HevcTuRange& rg = ranges[pick_range(ranges, nranges, b)];
-  const HevcDesc& d = descs[rg.desc];
-  const GpuTu t = static_cast<const GpuTu*>(d.tus)[rg.first + (b - rg.begin)];
+// One transform block with one wave: PCM copy, or (intra prediction +) inverse transform +
+// reconstruction into the picture.
+__device__ void tu_wave(const HevcDesc& d, const GpuTu& t, int lane, TuWave& L, bool publish) {
   const int stride = d.stride;
   u8* y = d.y + size_t(d.target) * d.slot_y;
   u8* uv = d.uv + size_t(d.target) * d.slot_uv;
-  const int tid = int(threadIdx.x);
+  wave_sync();  // the wave's previous block has finished reading its LDS
   if (t.flags & hevc::kTuPcm) {
     const int n = 1 << t.log2, nc = n >> 1;
     const u8* src = d.pcm + t.data;
-    for (int s = tid; s < n * n; s += 256) y[(t.y + s / n) * stride + t.x + s % n] = src[s];
-    for (int s = tid; s < 2 * nc * nc; s += 256) {
+    for (int s = lane; s < n * n; s += 64) y[(t.y + s / n) * stride + t.x + s % n] = src[s];
+    for (int s = lane; s < 2 * nc * nc; s += 64) {
       const int c = s / (nc * nc), r = s - c * nc * nc;
       uv[((t.y >> 1) + r / nc) * stride + t.x + 2 * (r % nc) + c] = src[n * n + s];
     }
@@ -212,22 +281,65 @@ __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict
   const bool bypass = t.flags & hevc::kTuBypass;  // lossless CU: the coefficients are the residual
   const bool dst = t.flags & hevc::kTuDst;
   const i16* dq = d.coefs + t.data;
-  if (intra)  // (uniform per block)
-    prepare_refs_par(plane, stride, step, t.x, t.y, log2, t.c == 0, t.avail, t.mode, (t.flags & hevc::kTuStrong) != 0,
-                     sbuf, sav, sref, top, left);
+  if (intra)  // (uniform per wave)
+    prepare_refs_wave(d, t, plane, stride, step, lane, L);
   const int mx = t.ext_x, my = t.ext_y;
-  if (coef && !tskip && !bypass)
-    for (int s = tid; s < n * (mx + 1); s += 256) {
+  if (coef && !tskip && !bypass) {
+    for (int s = lane; s < n * (mx + 1); s += 64) {
       const int yy = s / (mx + 1), xx = s - yy * (mx + 1);
-      g[yy * n + xx] = hevc::hk_itx_col(dq, log2, dst, yy, xx, my);
+      L.g[yy * n + xx] = hevc::hk_itx_col(dq, log2, dst, yy, xx, my);
     }
-  __syncthreads();
-  for (int s = tid; s < n * n; s += 256) {
+    wave_sync();
+  }
+  for (int s = lane; s < n * n; s += 64) {
     const int yy = s >> log2, xx = s & (n - 1);
     u8& q = plane[(t.y + yy) * stride + (t.x + xx) * step];
-    int v = intra ? int(hevc::hk_intra_sample(top, left, log2, t.mode, t.c == 0, xx, yy)) : int(q);
-    if (coef) v += bypass ? int(dq[s]) : (tskip ? hevc::hk_tskip(dq[s]) : hevc::hk_itx_row(&g[yy * n], log2, dst, xx, mx));
-    q = hevc::hk_clip8(v);
+    int v = intra ? int(hevc::hk_intra_sample(L.top, L.left, log2, t.mode, t.c == 0, xx, yy)) : int(q);
+    if (coef) v += bypass ? int(dq[s]) : (tskip ? hevc::hk_tskip(dq[s]) : hevc::hk_itx_row(&L.g[yy * n], log2, dst, xx, mx));
+    const u8 o = hevc::hk_clip8(v);
+    q = o;
+    if (publish) {  // the right column / bottom row other intra blocks of the launch may read
+      if (xx == n - 1) xg_put(xg_col(d, t.c, t.x + xx, t.y + yy), d.epoch, o);
+      if (yy == n - 1) xg_put(xg_row(d, t.c, t.x + xx, t.y + yy), d.epoch, o);
+    }
+  }
+}
+
+// Independent blocks (level 0, or one intra level when levels are launched one by one):
+// tickets base .. end, four blocks per workgroup, one per wave.
+__global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict__ descs,
+                                                     const HevcTuRange* __restrict__ ranges, int nranges, int base,
+                                                     int end) {
+  __shared__ TuWave lds[4];
+  const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
+  const int b = base + int(blockIdx.x) * 4 + wave;
+  if (b >= end) return;  // (uniform per wave; no workgroup barrier below)
+  const HevcTuRange& rg = ranges[pick_range(ranges, nranges, b)];
+  const HevcDesc& d = descs[rg.desc];
+  tu_wave(d, static_cast<const GpuTu*>(d.tus)[rg.first + (b - rg.begin)], lane, lds[wave], false);
+}
+
+// Intra levels: every intra block of the round in ONE launch. Waves take tickets in level order
+// until the queue is empty, so a block's producers (lower levels) were taken earlier by running
+// waves and the lowest unfinished ticket can always proceed (no co-residency assumption). A block
+// reads its references from the picture, except the units written in this launch (GpuTu::pend),
+// which it polls from the producers' epoch-tagged edge words: the data is its own flag, so there
+// is no completion counter, no release fence and no L2 writeback. A wait that exceeds the spin
+// limit marks the picture's error word (the frame is dropped) and goes on, so the grid drains.
+__global__ __launch_bounds__(256) void hevc_tu_queue_kernel(const HevcDesc* __restrict__ descs,
+                                                           const HevcTuRange* __restrict__ ranges, int nranges,
+                                                           int total, u32* __restrict__ ctr) {
+  __shared__ TuWave lds[4];
+  const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
+  TuWave& L = lds[wave];
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    t = __shfl(t, 0);
+    if (t >= total) break;
+    const HevcTuRange& rg = ranges[pick_range(ranges, nranges, t)];
+    const HevcDesc& d = descs[rg.desc];
+    tu_wave(d, static_cast<const GpuTu*>(d.tus)[rg.first + (t - rg.begin)], lane, L, true);
   }
 }
 
@@ -325,9 +437,19 @@ void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s
   hipLaunchKernelGGL(hevc_mc_kernel, dim3(total_pus), dim3(256), 0, s, d_descs, n);
 }
 
-void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, hipStream_t s) {
+void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
+                    hipStream_t s) {
+  if (nranges <= 0 || count <= 0) return;
+  hipLaunchKernelGGL(hevc_tu_kernel, dim3((count + 3) / 4), dim3(256), 0, s, d_descs, d_ranges, nranges, base,
+                     base + count);
+}
+
+void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, u32* ctr,
+                          hipStream_t s) {
   if (nranges <= 0 || total_tus <= 0) return;
-  hipLaunchKernelGGL(hevc_tu_kernel, dim3(total_tus), dim3(256), 0, s, d_descs, d_ranges, nranges);
+  // persistent waves: enough to fill the chip (4 per workgroup), never more than blocks
+  const int wgs = std::min((total_tus + 3) / 4, 1024);
+  hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, total_tus, ctr);
 }
 
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s) {

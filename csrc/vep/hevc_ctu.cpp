@@ -924,14 +924,16 @@ class CtuLayer {
     const int n = 1 << log2, sub = c ? 1 : 0, g = c ? 2 : 4;
     const int lx = x0 << sub, ly = y0 << sub;
     std::vector<u16>& lvl = c ? pc_.lvl_c : pc_.lvl_y;
-    u64 mask = 0;
+    u64 mask = 0, pend = 0;
     int level = 0;
     auto probe = [&](int x, int y, int bit) {  // component location of the unit's first sample
       const int xl = x << sub, yl = y << sub;
       if (!pc_.avail(lx, ly, xl, yl, pc_.rec)) return;
       if (pps_.constrained_intra_pred && !pc_.intra[pc_.i4(xl, yl)]) return;
       mask |= u64(1) << bit;
-      level = std::max(level, int(lvl[pc_.i4(xl, yl)]));
+      const int l = int(lvl[pc_.i4(xl, yl)]);
+      if (l > 0) pend |= u64(1) << bit;  // written by an intra block of the same launch
+      level = std::max(level, l);
     };
     probe(x0 - 1, y0 - 1, 0);
     for (int k = 0; k < 2 * n / g; ++k) {
@@ -939,6 +941,7 @@ class CtuLayer {
       probe(x0 + k * g, y0 - 1, 17 + k);
     }
     gpu_avail_ = mask;
+    gpu_pend_ = pend;
     gpu_level_ = level + 1;
   }
 
@@ -1016,6 +1019,7 @@ class CtuLayer {
         t.flags |= kTuIntra;
         t.mode = u8(c == 0 ? block_luma_mode_ : cu_.ipmc);
         t.avail = gpu_avail_;
+        t.pend = gpu_pend_;
         t.level = u16(gpu_level_);
         if (sps_.strong_intra_smoothing) t.flags |= kTuStrong;
         if (c == 0 && log2 == 2) t.flags |= kTuDst;
@@ -1505,6 +1509,7 @@ class CtuLayer {
   bool cbf_nonzero_ = false;
   int block_luma_mode_ = 1;
   u64 gpu_avail_ = 0;
+  u64 gpu_pend_ = 0;  // reference units the GPU reads from the intra blocks' edge exchange
   std::vector<int> lvbuf_;  // one transform block's levels
   int gpu_level_ = 1;
   std::map<TuKey, TuLevels> levels_;

@@ -153,6 +153,10 @@ class Decoder {
 // records-mode picture on the DPB surfaces `slots` with the kernels' per-sample math (CPU
 // backend of the records path; the oracle of gpu_hevc.hip).
 void cpu_execute(const struct GpuPicture& p, std::vector<HostSurface>& slots);
+// The queue kernel's edge exchange, checked on the records: every reference sample an intra
+// block polls (GpuTu::pend) must be on the right column / bottom row of an intra block of a
+// lower level. Returns the number of samples that are not (0 for a consistent picture).
+u64 exchange_violations(const struct GpuPicture& p);
 
 
 // Closed-loop synthetic HEVC Main encoder (tests, camera farm): I / P / B pictures over the

@@ -3,7 +3,10 @@
 // kernels' per-sample functions, in the kernels' pass order. The mirror is the CPU backend of
 // the records path and the oracle the kernels are checked against.
 #include <algorithm>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <unordered_map>
 
 #include "hevc_ctu.h"
 #include "hevc_recon.h"
@@ -87,6 +90,44 @@ void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
 }
 
 }  // namespace
+
+u64 exchange_violations(const GpuPicture& p) {
+  auto key = [](int c, int x, int y) { return u64(c) << 40 | u64(u32(y)) << 20 | u64(u32(x)); };
+  std::unordered_map<u64, int> col, row;  // edge word -> level of the block publishing it
+  for (const GpuTu& t : p.tus) {
+    if (!(t.flags & kTuIntra) || (t.flags & kTuPcm)) continue;
+    const int n = 1 << t.log2;
+    for (int k = 0; k < n; ++k) {
+      col[key(t.c, t.x + n - 1, t.y + k)] = t.level;
+      row[key(t.c, t.x + k, t.y + n - 1)] = t.level;
+    }
+  }
+  u64 bad = 0;
+  for (const GpuTu& t : p.tus) {
+    if (!(t.flags & kTuIntra) || (t.flags & kTuPcm) || !t.pend) continue;
+    const int n = 1 << t.log2, g = t.c == 0 ? 4 : 2;
+    auto need = [&](const std::unordered_map<u64, int>& m, int x, int y) {
+      auto it = m.find(key(t.c, x, y));
+      if (it == m.end() || it->second >= t.level) {
+        if (bad < 8 && std::getenv("VEP_XG_DEBUG"))
+          std::fprintf(stderr, "tu c%d (%d,%d) n%d lvl%d mode%d pend=%llx avail=%llx: word (%d,%d) %s %s lvl %d\n",
+                       t.c, t.x, t.y, n, t.level, t.mode, (unsigned long long)t.pend, (unsigned long long)t.avail, x, y,
+                       &m == &col ? "col" : "row", it == m.end() ? "missing" : "late", it == m.end() ? -1 : it->second);
+        ++bad;
+      }
+    };
+    if (t.pend & 1) {  // the corner: on the covering block's right column or bottom row
+      auto a = col.find(key(t.c, t.x - 1, t.y - 1)), b = row.find(key(t.c, t.x - 1, t.y - 1));
+      const bool ok = (a != col.end() && a->second < t.level) || (b != row.end() && b->second < t.level);
+      if (!ok) need(col, t.x - 1, t.y - 1);
+    }
+    for (int k = 0; k < 2 * n; ++k) {
+      if ((t.pend >> (1 + k / g)) & 1) need(col, t.x - 1, t.y + k);
+      if ((t.pend >> (17 + k / g)) & 1) need(row, t.x + k, t.y - 1);
+    }
+  }
+  return bad;
+}
 
 void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
   HostSurface& s = slots[size_t(p.target)];

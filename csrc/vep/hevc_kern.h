@@ -55,8 +55,10 @@ struct GpuTu {    // one transform block of one component (or one PCM coding blo
   u16 level;      // intra dependency level (0: inter residual / PCM)
   u8 ext_x, ext_y;  // kTuCoef: last column / row holding a non-zero coefficient
   u64 avail;      // intra: reference availability, see hk_prepare_refs
+  u64 pend;       // intra: the available units another intra block (level >= 1) writes, which
+                  // the GPU reads from that block's published edge (same bit layout as avail)
 };
-static_assert(sizeof(GpuTu) == 24, "GpuTu layout");
+static_assert(sizeof(GpuTu) == 32, "GpuTu layout");
 
 struct GpuSlice {  // per-slice loop-filter parameters
   i8 beta_offset, tc_offset;  // *2 values

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <new>
 #include <map>
 #include <shared_mutex>
 
@@ -106,6 +108,48 @@ std::shared_ptr<u8> pinned_block(size_t n) {
     // top-class block (it is at least that large)
     q.free_[cls >= 0 ? cls : kMaxShift].push_back(b);
   });
+}
+
+namespace {
+struct Live {  // pool blocks handed to containers, keyed by address
+  std::mutex mu;
+  std::map<void*, std::shared_ptr<u8>> blocks;
+};
+Live& live() {
+  static Live* l = new Live();  // leaked like the pool
+  return *l;
+}
+}  // namespace
+
+void* alloc_bytes(size_t n) {
+  n = std::max<size_t>(n, 1);
+  if (pool_enabled()) {
+    if (std::shared_ptr<u8> b = pinned_block(n)) {
+      void* p = b.get();
+      Live& l = live();
+      std::lock_guard<std::mutex> g(l.mu);
+      l.blocks.emplace(p, std::move(b));
+      return p;
+    }
+  }
+  void* p = std::malloc(n);
+  if (!p) throw std::bad_alloc();
+  return p;
+}
+
+void free_bytes(void* p) {
+  if (!p) return;
+  std::shared_ptr<u8> keep;  // released outside the lock (its deleter takes the pool lock)
+  {
+    Live& l = live();
+    std::lock_guard<std::mutex> g(l.mu);
+    auto it = l.blocks.find(p);
+    if (it != l.blocks.end()) {
+      keep = std::move(it->second);
+      l.blocks.erase(it);
+    }
+  }
+  if (!keep) std::free(p);
 }
 
 const u8* device_address(const u8* p, size_t n) {

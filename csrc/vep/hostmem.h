@@ -10,8 +10,12 @@
 // ndarray/tobytes/SerializeToString/Redis copy chain (python/read_image.py:94-121).
 #pragma once
 
+#include <algorithm>
+#include <cstring>
 #include <memory>
 #include <mutex>
+#include <type_traits>
+#include <vector>
 
 #include "common.h"
 
@@ -32,6 +36,96 @@ const u8* device_address(const u8* p, size_t n);
 // Register / unregister externally allocated pinned memory (e.g. a staging buffer).
 void register_range(const u8* host, size_t n, const u8* dev);
 void unregister_range(const u8* host);
+
+// Raw allocation for containers: from the pinned pool when it is enabled (so the GPU can read
+// the memory in place, see device_address), else from the heap. free_bytes tells them apart.
+void* alloc_bytes(size_t n);
+void free_bytes(void* p);
+
+// Growable array of trivially copyable per-picture reconstruction records in pool memory (the
+// std::vector subset the parser uses). Pictures are recycled with their capacity, so after
+// warm-up nothing is allocated; the worker gathers the records to the GPU over PCIe instead of
+// copying them into its staging buffer on the host. Appends are plain memcpy (a std::vector with
+// a custom allocator would construct element by element).
+template <class T>
+class PodVec {
+  static_assert(std::is_trivially_copyable_v<T>, "PodVec holds plain records");
+
+ public:
+  PodVec() = default;
+  PodVec(const PodVec& o) { append(o.p_, o.n_); }
+  PodVec(PodVec&& o) noexcept : p_(o.p_), n_(o.n_), cap_(o.cap_) { o.p_ = nullptr, o.n_ = o.cap_ = 0; }
+  PodVec& operator=(const PodVec& o) {
+    if (this != &o) {
+      n_ = 0;
+      append(o.p_, o.n_);
+    }
+    return *this;
+  }
+  PodVec& operator=(PodVec&& o) noexcept {
+    if (this != &o) {
+      free_bytes(p_);
+      p_ = o.p_, n_ = o.n_, cap_ = o.cap_;
+      o.p_ = nullptr, o.n_ = o.cap_ = 0;
+    }
+    return *this;
+  }
+  ~PodVec() { free_bytes(p_); }
+
+  size_t size() const { return n_; }
+  size_t capacity() const { return cap_; }
+  bool empty() const { return n_ == 0; }
+  T* data() { return p_; }
+  const T* data() const { return p_; }
+  T& operator[](size_t i) { return p_[i]; }
+  const T& operator[](size_t i) const { return p_[i]; }
+  T* begin() { return p_; }
+  T* end() { return p_ + n_; }
+  const T* begin() const { return p_; }
+  const T* end() const { return p_ + n_; }
+  T& back() { return p_[n_ - 1]; }
+
+  void clear() { n_ = 0; }
+  void reserve(size_t c) {
+    if (c > cap_) grow(c);
+  }
+  void resize(size_t n) { resize(n, T{}); }
+  void resize(size_t n, const T& v) {
+    if (n > cap_) grow(std::max(n, 2 * cap_));
+    for (size_t i = n_; i < n; ++i) p_[i] = v;
+    n_ = n;
+  }
+  void assign(size_t n, const T& v) {
+    n_ = 0;
+    resize(n, v);
+  }
+  void append(const T* src, size_t k) {
+    if (n_ + k > cap_) grow(std::max(n_ + k, 2 * cap_));
+    if (k) std::memcpy(static_cast<void*>(p_ + n_), src, k * sizeof(T));
+    n_ += k;
+  }
+  void push_back(const T& v) { append(&v, 1); }
+  // (std::vector's range insert, at the end only)
+  T* insert(T* pos, const T* first, const T* last) {
+    const size_t at = size_t(pos - p_);
+    VEP_CHECK(at == n_, "PodVec inserts append only");
+    append(first, size_t(last - first));
+    return p_ + at;
+  }
+
+ private:
+  void grow(size_t c) {
+    T* q = static_cast<T*>(alloc_bytes(c * sizeof(T)));
+    if (n_) std::memcpy(static_cast<void*>(q), p_, n_ * sizeof(T));
+    free_bytes(p_);
+    p_ = q;
+    cap_ = c;
+  }
+  T* p_ = nullptr;
+  size_t n_ = 0, cap_ = 0;
+};
+template <class T>
+using pinned_vector = PodVec<T>;
 
 struct PoolStats {
   u64 chunks = 0, bytes_reserved = 0, blocks_live = 0, blocks_reused = 0, fallbacks = 0;

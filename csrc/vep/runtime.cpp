@@ -215,6 +215,7 @@ bool Camera::build_vcn_job(DecodeJob& job, size_t from, size_t to) {
 }
 
 bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
+  job.keyframe_only = keyframe_only.load(std::memory_order_relaxed);
   if (use_vcn_) return build_vcn_job(job, from, to);
   job.cam = index_;
   job.refresh = refresh;
@@ -407,6 +408,7 @@ constexpr int kDefaultLanes = 3;
 constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
+constexpr int kDefaultKfWindowUs = 8000;  // keyframe-only coalescing window (see WorkerOptions)
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (opt_.decoder == kDecoderVcn)
@@ -431,6 +433,14 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       nq = qe ? std::atoi(qe) : kDefaultLaneQueue;
     }
     queue_ = std::clamp(nq, 1, 16);
+    int kw = opt_.kf_window_us;
+    if (kw < 0) {
+      const char* ke = std::getenv("VEP_KF_WINDOW_US");
+      kw = ke ? std::atoi(ke) : kDefaultKfWindowUs;
+    }
+    kf_window_us_ = std::clamp(kw, 0, 100000);
+    const char* tl = std::getenv("VEP_HEVC_TU_LEVELS");  // 1: one intra TU launch per level
+    hevc_tu_levels_ = tl && tl[0] == '1';
     int ns = opt_.stages;
     if (ns <= 0) {
       const char* se = std::getenv("VEP_STAGES");
@@ -525,6 +535,7 @@ Worker::~Worker() {
     if (!c) continue;
     dev_.free(c->surface.y);
     dev_.free(c->surface.uv);
+    dev_.free(c->surface.hevc_xg);
     c->set_ring(nullptr);
   }
   if (owns_cons_) {
@@ -593,6 +604,7 @@ void Worker::remove_camera(int idx) {
   auto& c = cams_[size_t(idx)];
   dev_.free(c->surface.y);
   dev_.free(c->surface.uv);
+  dev_.free(c->surface.hevc_xg);
   c.reset();
 }
 
@@ -706,6 +718,17 @@ void Worker::loop() {
       std::unique_lock<std::mutex> g(q_mu_);
       q_cv_.wait(g, [this] { return stop_ || !pending_.empty(); });
       if (stop_ && pending_.empty()) break;
+      if (kf_window_us_ > 0) {  // keyframe-only pictures: gather a few per wavefront launch
+        auto all_kf = [this] {
+          for (const DecodeJob& j : pending_)
+            if (!j.keyframe_only) return false;
+          return true;
+        };
+        const size_t enough = 4 * lanes_.size();
+        const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(kf_window_us_);
+        while (!stop_ && pending_.size() < enough && all_kf())
+          if (q_cv_.wait_until(g, deadline) == std::cv_status::timeout) break;
+      }
       batch.swap(pending_);
       busy_ = true;
     }
@@ -971,12 +994,16 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   const size_t off_desc = 0;
   const size_t off_lb = al(sizeof(gpu::DecodeDesc) * size_t(n));
   size_t nchunks = 0;
+  auto chunks_of = [](size_t len) { return (len + gpu::kGatherChunk - 1) / gpu::kGatherChunk; };
   if (!direct)
     for (const auto& j : jobs)
-      for (const auto& sg : j.upd.segs)
-        nchunks += (sg.len + gpu::kGatherChunk - 1) / gpu::kGatherChunk;
-  const size_t off_gather = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
-  size_t need = off_gather + al(sizeof(gpu::GatherChunk) * nchunks);
+      for (const auto& sg : j.upd.segs) nchunks += chunks_of(sg.len);
+  // record arrays already in pinned pool memory (hostmem::PinnedAllocator) are gathered by the
+  // GPU over PCIe instead of being copied into the staging buffer by the host
+  auto pinned = [](const void* p, size_t len) {
+    return len > 0 && hostmem::device_address(static_cast<const u8*>(p), len) != nullptr;
+  };
+  size_t need = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
   std::vector<size_t> mask_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
   std::vector<std::vector<size_t>> seg_off(static_cast<size_t>(n));
   auto words_of = [&](int i) { return size_t(jobs[size_t(i)].upd.mbs() + 31) / 32; };
@@ -1008,14 +1035,16 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       VEP_CHECK(p.wmbs * 16 == jobs[size_t(i)].pic.coded_width && p.hmbs * 16 == jobs[size_t(i)].pic.coded_height,
                 "picture size differs from the camera's surfaces");
       AvcPic a{&p, i, 0, 0, 0, 0, 0, 0, 0};
-      a.off_mbs = need;
-      need += al(p.mbs.size() * sizeof(avc::MbRec));
-      a.off_coef = need;
-      need += al(p.coefs.size() * sizeof(i16));
-      a.off_mv = need;
-      need += al(p.mvs.size() * sizeof(i16));
-      a.off_wp = need;
-      need += al(p.wps.size() * sizeof(avc::WpEntry));
+      auto put = [&](const void* src, size_t bytes) {
+        const size_t o = need;
+        need += al(bytes);
+        if (pinned(src, bytes)) nchunks += chunks_of(bytes);
+        return o;
+      };
+      a.off_mbs = put(p.mbs.data(), p.mbs.size() * sizeof(avc::MbRec));
+      a.off_coef = put(p.coefs.data(), p.coefs.size() * sizeof(i16));
+      a.off_mv = put(p.mvs.data(), p.mvs.size() * sizeof(i16));
+      a.off_wp = put(p.wps.data(), p.wps.size() * sizeof(avc::WpEntry));
       round_pics[size_t(r)].push_back(int(apics.size()));
       apics.push_back(a);
     }
@@ -1036,7 +1065,11 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   std::vector<size_t> off_hround(static_cast<size_t>(hrounds)), off_hranges(static_cast<size_t>(hrounds));
   std::vector<std::vector<int>> hround_pics(static_cast<size_t>(hrounds));
   std::vector<std::vector<gpu::HevcTuRange>> hranges(static_cast<size_t>(hrounds));
-  std::vector<std::vector<std::array<int, 3>>> hlevels(static_cast<size_t>(hrounds));  // first range, ranges, tus
+  // per round: level-0 ranges, level-0 blocks, intra (queue) ranges, intra blocks
+  std::vector<std::array<int, 4>> hwork(static_cast<size_t>(hrounds), std::array<int, 4>{0, 0, 0, 0});
+  std::vector<size_t> off_hctr(static_cast<size_t>(hrounds));
+  // per round and intra level: first ticket, blocks (the one-launch-per-level mode)
+  std::vector<std::vector<std::array<int, 2>>> hlevels(static_cast<size_t>(hrounds));
   for (int r = 0; r < hrounds; ++r) {
     int maxl = 0;
     for (int i = 0; i < n; ++i) {
@@ -1071,22 +1104,37 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     }
     off_hround[size_t(r)] = need;
     need += al(hround_pics[size_t(r)].size() * sizeof(gpu::HevcDesc));
-    for (int l = 0; l < maxl; ++l) {  // level l: one range per picture that has blocks at l
-      const int first = int(hranges[size_t(r)].size());
-      int tus = 0;
+    // level 0 (inter residual + PCM, independent blocks): one range per picture, one wide
+    // launch. Intra levels >= 1: one ticket queue for the whole round, level-major (a block's
+    // producers are at lower levels, so they hold lower tickets).
+    int tickets = 0;
+    for (int l = 0; l < maxl; ++l) {
+      if (l > 0) hlevels[size_t(r)].push_back({tickets, 0});
       for (size_t k = 0; k < hround_pics[size_t(r)].size(); ++k) {
         const hevc::GpuPicture& p = *hpics[size_t(hround_pics[size_t(r)][k])].p;
         if (int(p.level_begin.size()) - 1 <= l) continue;
         const int b = int(p.level_begin[size_t(l)]), e = int(p.level_begin[size_t(l) + 1]);
         if (e <= b) continue;
-        hranges[size_t(r)].push_back({int(k), b, e - b, tus});
-        tus += e - b;
+        if (l == 0) {
+          hranges[size_t(r)].push_back({int(k), b, e - b, hwork[size_t(r)][1]});
+          hwork[size_t(r)][0] += 1;
+          hwork[size_t(r)][1] += e - b;
+        } else {
+          hranges[size_t(r)].push_back({int(k), b, e - b, tickets});
+          hwork[size_t(r)][2] += 1;
+          tickets += e - b;
+          hlevels[size_t(r)].back()[1] += e - b;
+        }
       }
-      hlevels[size_t(r)].push_back({first, int(hranges[size_t(r)].size()) - first, tus});
     }
+    hwork[size_t(r)][3] = tickets;
     off_hranges[size_t(r)] = need;
     need += al(std::max<size_t>(hranges[size_t(r)].size(), 1) * sizeof(gpu::HevcTuRange));
+    off_hctr[size_t(r)] = need;  // the queue's ticket / done counters (zero in the upload)
+    need += al(4 * sizeof(u32));
   }
+  const size_t off_gather = need;  // gather chunks: pinned records (+ slices without direct reads)
+  need += al(sizeof(gpu::GatherChunk) * std::max<size_t>(nchunks, 1));
   need = al(need);
   const size_t header_bytes = need;
   for (int i = 0; i < n; ++i) {
@@ -1133,8 +1181,17 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     size_t len;
   };
   std::vector<CopyTask> tasks;
+  auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
+  size_t ng = 0;
   for (const AvcPic& a : apics) {
     auto add = [&](const void* src, size_t len, size_t off) {
+      if (pinned(src, len)) {  // the GPU pulls it (gather kernel after the header copy)
+        const u8* dv = hostmem::device_address(static_cast<const u8*>(src), len);
+        for (size_t o = 0; o < len; o += gpu::kGatherChunk)
+          gc[ng++] = {dv + o, st.d + off + o, u32(std::min<size_t>(gpu::kGatherChunk, len - o)), 0};
+        records_gathered_ += u64(len);
+        return;
+      }
       for (size_t o = 0; o < len; o += kPackChunk)
         tasks.push_back({static_cast<const u8*>(src) + o, st.h + off + o, std::min(kPackChunk, len - o)});
     };
@@ -1164,8 +1221,6 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     add(p.ctb_tile.data(), p.ctb_tile.size() * sizeof(u16), a.off_ctile);
   }
   std::vector<std::vector<const u8*>> seg_dev(static_cast<size_t>(n));
-  auto* gc = reinterpret_cast<gpu::GatherChunk*>(st.h + off_gather);
-  size_t ng = 0;
   for (int i = 0; i < n; ++i) {
     const auto& segs = jobs[size_t(i)].upd.segs;
     for (size_t g = 0; g < segs.size(); ++g) {
@@ -1359,6 +1414,25 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       VEP_CHECK(c->surface.slots > j.hevc_slots, "camera surfaces lack the SAO scratch slot");
       g.sao_y = c->surface.y + scratch * c->surface.slot_y();
       g.sao_uv = c->surface.uv + scratch * c->surface.slot_uv();
+      g.err = const_cast<u32*>(st.err_dev) + a.job;
+      {  // the camera's intra edge exchange (zeroed once: epochs start at 1)
+        Camera::Surface& sf = const_cast<Camera*>(c)->surface;
+        const size_t words = gpu::hevc_xg_words(g.stride, sf.hmbs * 16);
+        if (sf.hevc_xg_words < words) {
+          dev_.free(sf.hevc_xg);
+          sf.hevc_xg = static_cast<u64*>(dev_.alloc(words * sizeof(u64)));
+          VEP_HIP(hipMemset(sf.hevc_xg, 0, words * sizeof(u64)));
+          sf.hevc_xg_words = words;
+          sf.hevc_epoch = 0;
+        }
+        if (++sf.hevc_epoch == 0) {  // (after 2^32 rounds) never reuse a tag still in the words
+          VEP_HIP(hipMemset(sf.hevc_xg, 0, words * sizeof(u64)));
+          sf.hevc_epoch = 1;
+        }
+        g.xg = hevc_tu_levels_ ? nullptr : sf.hevc_xg;  // (per-level launches read the picture)
+        g.xg_h = sf.hmbs * 16;
+        g.epoch = sf.hevc_epoch;
+      }
       g.npu = int(p.pus.size());
       g.pu_begin = pus;
       g.blk_begin = blks;
@@ -1368,6 +1442,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     hround_work[size_t(r)] = {pus, blks};
     auto* hr = reinterpret_cast<gpu::HevcTuRange*>(st.h + off_hranges[size_t(r)]);
     for (size_t k = 0; k < hranges[size_t(r)].size(); ++k) hr[k] = hranges[size_t(r)][k];
+    std::memset(st.h + off_hctr[size_t(r)], 0, 4 * sizeof(u32));
   }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
@@ -1376,7 +1451,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   // on a queue another lane shares.
   if (ln.copy) {  // the stage's previous batch has completed (launch_on), so st.d is free
     VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, ln.copy));
-    if (!direct)
+    if (nchunks)
       gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
                          int(nchunks), ln.copy);
     VEP_HIP(hipEventRecord(st.copied, ln.copy));
@@ -1385,12 +1460,12 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   } else if (lanes_.size() > 1) {
     VEP_HIP(hipEventRecord(st.e0, cs));
     VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, cs));
-    if (!direct)
+    if (nchunks)
       gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
                          int(nchunks), cs);
   } else {
     VEP_HIP(hipMemcpyAsync(st.d, st.h, header_bytes, hipMemcpyHostToDevice, copy_stream_));
-    if (!direct)
+    if (nchunks)
       gpu::launch_gather(reinterpret_cast<const gpu::GatherChunk*>(st.d + off_gather),
                          int(nchunks), copy_stream_);
     VEP_HIP(hipEventRecord(st.copied, copy_stream_));
@@ -1426,7 +1501,14 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       sao |= hpics[size_t(k)].p->sao;
     }
     gpu::launch_hevc_mc(hd2, np, hround_work[size_t(r)][0], cs);
-    for (const auto& lv : hlevels[size_t(r)]) gpu::launch_hevc_tu(hd2, hr + lv[0], lv[1], lv[2], cs);
+    const auto& hw = hwork[size_t(r)];
+    gpu::launch_hevc_tu(hd2, hr, hw[0], 0, hw[1], cs);
+    if (hevc_tu_levels_) {  // one launch per intra level (kernel boundaries order the levels)
+      for (const auto& lv : hlevels[size_t(r)]) gpu::launch_hevc_tu(hd2, hr + hw[0], hw[2], lv[0], lv[1], cs);
+    } else {
+      gpu::launch_hevc_tu_queue(hd2, hr + hw[0], hw[2], hw[3], reinterpret_cast<u32*>(st.d + off_hctr[size_t(r)]),
+                                cs);
+    }
     if (dbk) {
       gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 0, cs);
       gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 1, cs);
@@ -1851,13 +1933,44 @@ void Worker::release_serve(ServeBuf* b) {
   serve_cv_.notify_one();
 }
 
-bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, size_t cap) {
+bool Worker::register_host(void* p, size_t n) {
+  if (!dev_.gpu() || !p || !n) return false;
+  dev_.bind();
+  if (hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return true;
+}
+
+void Worker::unregister_host(void* p) {
+  if (!dev_.gpu() || !p) return;
+  dev_.bind();
+  (void)hipHostUnregister(p);
+}
+
+bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, size_t cap, bool dst_pinned) {
   FrameRing* ring = &rg;
   for (int attempt = 0; attempt < 4; ++attempt) {
     int slot;
     if (!ring->latest(after, meta, &slot)) return false;
     const size_t n = ring->slot_bytes();
     VEP_CHECK(cap >= n, "read_latest destination too small");
+    if (dev_.gpu() && dst_pinned) {
+      dev_.bind();
+      ServeBuf* b = acquire_serve(0);  // only its completion event: the DMA lands in dst
+      try {
+        VEP_HIP(hipMemcpyAsync(dst, ring->slot_ptr(slot), n, hipMemcpyDeviceToHost, serve_stream_));
+        VEP_HIP(hipEventRecord(b->ev[0], serve_stream_));
+        VEP_HIP(hipEventSynchronize(b->ev[0]));
+      } catch (...) {
+        release_serve(b);
+        throw;
+      }
+      release_serve(b);
+      if (!ring->still_valid(slot, meta->seq)) continue;
+      return true;
+    }
     if (dev_.gpu()) {
       dev_.bind();
       ServeBuf* b = acquire_serve(n);

@@ -106,6 +106,7 @@ struct DecodeJob {
   PictureInfo pic;                     // the published frame's picture (sizes of the surfaces)
   FrameMeta meta;
   bool refresh = false;  // IDR: every MB is covered
+  bool keyframe_only = false;  // from a keyframe-only camera (one picture per GOP)
 
   // General path: DPB slot of the newest picture that left the reorder buffer in this job (it is
   // converted and published), -1 when every picture of the job is still waiting for output
@@ -187,6 +188,10 @@ class Camera {
     int slots = 1;                 // DPB surfaces (general H.264 path); slot k at y + k * bytes
     u8* y = nullptr;
     u8* uv = nullptr;
+    // H.265 intra edge exchange (gpu::hevc_xg_words of the coded picture) and its round epoch
+    u64* hevc_xg = nullptr;
+    size_t hevc_xg_words = 0;
+    u32 hevc_epoch = 0;
     size_t slot_y() const { return size_t(wmbs) * 16 * hmbs * 16; }
     size_t slot_uv() const { return slot_y() / 2; }
     std::vector<HostSurface> host;  // CPU backend: one per slot
@@ -243,6 +248,12 @@ struct WorkerOptions {
   // Decoder backend: kDecoderNative (CPU parse + gfx950 reconstruction), kDecoderVcn (rocDecode
   // on the video core; fails when librocdecode is missing) or kDecoderAuto (VCN when present).
   int decoder = 0;
+  // Keyframe-only coalescing: while every pending job is a keyframe-only camera's picture, the
+  // worker waits up to this long (from the first one) for more before launching, so one
+  // latency-bound intra + deblocking wavefront launch serves several pictures. Such cameras
+  // show one frame per GOP, so the wait is invisible to their clients. -1 = VEP_KF_WINDOW_US or
+  // the default; 0 = off.
+  int kf_window_us = -1;
 };
 enum DecoderBackend : int { kDecoderNative = 0, kDecoderVcn = 1, kDecoderAuto = 2 };
 
@@ -277,8 +288,13 @@ class Worker {
   void flush();
 
   // Serving: copy the newest frame with seq > after into dst (host). Returns false if none.
+  // dst_pinned: dst is page-locked (register_host) -> one DMA straight into it, no staging.
   bool read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap);
-  bool read_latest(FrameRing& ring, i64 after, FrameMeta* meta, u8* dst, size_t cap);
+  bool read_latest(FrameRing& ring, i64 after, FrameMeta* meta, u8* dst, size_t cap, bool dst_pinned = false);
+  // Page-lock caller memory (e.g. a shared-memory segment another process maps) for direct
+  // D2H. False on the CPU backend or when the driver refuses the range.
+  bool register_host(void* p, size_t n);
+  void unregister_host(void* p);
 
   // Consumer batch (letterbox): device pointers of [max_cameras, S, S, 3] u8 and CHW tensor.
   // Point the consumer batch at caller-owned device buffers (e.g. torch tensors that feed an
@@ -300,6 +316,8 @@ class Worker {
   u64 batches() const { return batches_.load(); }
   // slice bytes the GPU read in place from pinned AU blocks vs. staged by a host memcpy
   u64 bytes_inplace() const { return pinned_bytes_inplace_.load(); }
+  u64 records_gathered() const { return records_gathered_.load(); }  // record bytes the GPU pulled
+  int kf_window_us() const { return kf_window_us_; }
   u64 bytes_staged() const { return pinned_bytes_staged_.load(); }
   // frames committed to camera rings (what a client can read) / frames a batch produced but the
   // worker did not publish (GPU check failure, wavefront timeout, camera waiting for a keyframe
@@ -414,11 +432,13 @@ class Worker {
   std::mutex q_mu_;
   std::condition_variable q_cv_, idle_cv_;
   std::vector<DecodeJob> pending_;
+  int kf_window_us_ = 0;
+  bool hevc_tu_levels_ = false;
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;
   std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0};
-  std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0};
+  std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0}, records_gathered_{0};
   std::mutex timers_mu_;
   bool direct_reads_ = false;
   u64* avc_prof_ = nullptr;

@@ -135,3 +135,18 @@ def test_scaling_list_defaults_match_spec_table():
     assert f16[0, 0] == 16 and f16[15, 15] == 115 and f16[14, 15] == 115 and f16[0, 1] == 16
     f4 = np.array(v.hevc_scaling_factors(0, 0, None))
     assert (f4 == 16).all()
+
+
+@pytest.mark.parametrize("name", list(TOOLS) + ["coverage"])
+def test_intra_edge_exchange_is_consistent(name):
+    """The GPU queue kernel reconstructs every intra block of a picture in one launch; a block reads
+    the reference samples other intra blocks write from their published right column / bottom row
+    (GpuTu::pend). Checked on the records: every polled sample must be published by an intra block
+    of a lower dependency level (a violation would be a wavefront timeout on the GPU)."""
+    kw = dict(coverage=True, bframes=1, slices=2, width=200, height=120, seed=5) if name == "coverage" else TOOLS[name]
+    e, rec = encoder(**kw), v.HevcRecordsDecoder()
+    for _ in range(10):
+        rec.decode(e.next())
+    rec.flush()
+    st = rec.stats
+    assert st["intra_tus"] > 0 and st["exchange_violations"] == 0, st

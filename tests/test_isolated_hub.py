@@ -72,3 +72,142 @@ def test_isolated_hub_restarts_a_dead_worker_process(native, tmp_path):
     finally:
         hub.shutdown()
         srv.stop()
+
+
+def _settle(hub, names, n_frames=3, timeout=30.0):
+    """Query each camera until it has published n_frames, then stop querying: with a short
+    idle cutoff the cameras stop decoding, so the latest frames stay put."""
+    deadline = time.time() + timeout
+    seen = {}
+    while time.time() < deadline and len(seen) < len(names):
+        for n in names:
+            hub.touch(n)
+            r = None
+            try:
+                r = hub.latest_frame_bytes(n, 0, 100)
+            except RuntimeError:
+                pass
+            if r and r[0] >= n_frames:
+                seen[n] = r[0]
+        time.sleep(0.05)
+    assert len(seen) == len(names), seen
+    time.sleep(1.0)  # > idle cutoff: decoding pauses
+
+
+def _isolated_cfg(tmp_path, letterbox=32):
+    cfg = Config()
+    cfg.data_dir = str(tmp_path)
+    cfg.gpu.isolation = "process"
+    cfg.gpu.letterbox_size = letterbox
+    cfg.gpu.max_cameras_per_gpu = 4
+    cfg.gpu.idle_cutoff_ms = 300
+    return cfg
+
+
+def _check_rows(hub, batch, names, S):
+    import numpy as np
+    import torch
+
+    from video_edge_ai_proxy_amd.ops import letterbox_reference
+
+    assert tuple(batch.shape) == (len(names), S, S, 3) and batch.dtype == torch.uint8
+    for row, n in zip(batch, names):
+        meta, img = hub.latest_frame(n, 0)
+        ref, _ = letterbox_reference(torch.from_numpy(np.ascontiguousarray(img)), S)
+        assert (row.int() - ref.int()).abs().max().item() <= 1, n
+
+
+def test_isolated_frames_travel_through_shared_memory(native, tmp_path):
+    """VideoLatestImage bytes from a worker process arrive through its shared-memory segment and
+    are the same VideoFrame the in-process path builds (pixels equal the ring's latest frame)."""
+    import numpy as np
+
+    from video_edge_ai_proxy_amd.engine import shm
+    from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
+    from video_edge_ai_proxy_amd.proto import pb
+
+    srv = farm(native, 1)
+    hub = ProcessHub(_isolated_cfg(tmp_path, 0), devices=[-1], supervise_interval_s=0.2)
+    try:
+        hub.start_camera("c0", f"rtsp://127.0.0.1:{srv.port}/c0")
+        _settle(hub, ["c0"])
+        seq, frame, meta = hub.latest_frame_bytes("c0", 0, 0)
+        vf = pb.VideoFrame()
+        vf.ParseFromString(frame)
+        assert (vf.width, vf.height) == (160, 96) and vf.device_id == "c0"
+        m, img = hub.latest_frame("c0", 0)
+        assert m["seq"] == seq
+        assert np.array_equal(np.frombuffer(vf.data, np.uint8).reshape(96, 160, 3), img)
+        pid = hub.state("c0")["worker_pid"]
+        segs = [f for f in os.listdir(shm.SHM_DIR) if f.startswith(shm.segment_prefix(pid))]
+        assert segs, "the worker serves frames through shared-memory segments"
+        # nothing newer yet: None, and the cursor protocol is the in-process one
+        assert hub.latest_frame_bytes("c0", seq, 0) is None
+    finally:
+        hub.shutdown()
+        srv.stop()
+    assert not [f for f in os.listdir(shm.SHM_DIR) if f.startswith(shm.segment_prefix(pid))]
+
+
+def test_isolated_consumer_batch_gathers_across_worker_processes(native, tmp_path):
+    """consumer_batch() in process isolation: the worker processes form a torch.distributed
+    group (gloo here, RCCL on GPUs), all-gather their letterboxed rows and hand the node batch
+    back through shared memory, in the requested order; after a worker dies and is restarted,
+    the group is re-formed with a fresh rendezvous and the batch works again."""
+    from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
+
+    S = 32
+    srv = farm(native, 3)
+    hub = ProcessHub(_isolated_cfg(tmp_path, S), devices=[-1, -1], supervise_interval_s=0.2)
+    try:
+        for i in range(3):
+            hub.start_camera(f"c{i}", f"rtsp://127.0.0.1:{srv.port}/c{i}")
+        names = ["c2", "c0", "c1"]
+        _settle(hub, names)
+        batch, order = hub.consumer_batch(names=names)
+        assert order == names
+        _check_rows(hub, batch, names, S)
+        e1 = hub._group_epoch
+        info = [c.call("group_info") for c in hub._children]
+        assert [i["rank"] for i in info] == [0, 1] and all(i["world"] == 2 for i in info)
+        # the other rank holds the same node batch (all-gather), and a second gather reuses the group
+        b2, _ = hub.consumer_batch(device=-1, names=names)
+        assert hub._group_epoch == e1 and b2.shape == batch.shape
+        # kill one worker: restart, re-add, re-form, gather again
+        victim = hub.state("c0")["worker_pid"]
+        wi = hub.handle("c0").worker_index
+        os.kill(victim, signal.SIGKILL)
+        deadline = time.time() + 60
+        while time.time() < deadline and hub.child_restarts[wi] == 0:
+            time.sleep(0.1)
+        assert hub.child_restarts[wi] == 1
+        _settle(hub, names)
+        batch, order = hub.consumer_batch(names=names)
+        assert hub._group_epoch > e1
+        _check_rows(hub, batch, names, S)
+    finally:
+        hub.shutdown()
+        srv.stop()
+
+
+def test_isolated_hub_eight_worker_processes(native, tmp_path):
+    """World = 8 rehearsal of the process-isolated hub (gloo, CPU-backend workers): eight
+    supervised worker processes, one camera each, group formation and the node batch gather."""
+    from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
+
+    S = 16
+    srv = farm(native, 8)
+    hub = ProcessHub(_isolated_cfg(tmp_path, S), devices=[-1] * 8, supervise_interval_s=0.5)
+    try:
+        names = [f"c{i}" for i in range(8)]
+        for n in names:
+            hub.start_camera(n, f"rtsp://127.0.0.1:{srv.port}/{n}")
+        assert sorted(hub.handle(n).worker_index for n in names) == list(range(8))
+        _settle(hub, names, n_frames=2, timeout=60)
+        batch, order = hub.consumer_batch()
+        assert order == sorted(names)
+        _check_rows(hub, batch, order, S)
+        assert [c.call("group_info")["world"] for c in hub._children] == [8] * 8
+    finally:
+        hub.shutdown()
+        srv.stop()

@@ -67,6 +67,9 @@ class GpuConfig:
                                                  # worker process per GPU, engine/isolated.py)
     decoder: str = "native"                      # native (CPU parse + gfx950 reconstruction) |
                                                  # vcn (rocDecode on the video core) | auto
+    consumer_hook: str = ""                      # process isolation: "module:function" each
+                                                 # worker process calls with every gathered
+                                                 # node batch (fn(batch, names, rank), on its GPU)
 
 
 @dataclass

@@ -7,6 +7,15 @@ bitstream parse or a GPU error) ends this process only, and the parent starts a 
 re-adds its cameras — the reference's per-camera ``restart: always`` container
 (server/services/rtsp_process_manager.go:70-81) at per-GPU granularity.
 
+Frames leave through shared memory (engine/shm.py): each connection owns a page-locked segment
+the serialized ``VideoFrame`` is DMA'd into; only its name and length travel on the connection.
+
+The worker processes of one hub are the ranks of a ``torch.distributed`` group (RCCL over xGMI
+on GPUs, gloo on the CPU backend), formed by the parent on demand and re-formed with a fresh
+rendezvous after a restart. ``consumer_gather`` all-gathers every rank's letterboxed consumer
+rows, so every GPU holds the node-wide batch (handed to ``gpu.consumer_hook`` if configured); one
+rank also DMAs it into shared memory for the front-end's ``consumer_batch()``.
+
 Usage (by the parent only): ``python -m video_edge_ai_proxy_amd.engine.child --device D
 --config JSON`` with the connection key in ``VEP_CHILD_KEY``; prints ``{"port": P}`` once ready
 and exits when its stdin closes (the parent is gone).
@@ -14,45 +23,162 @@ and exits when its stdin closes (the parent is gone).
 from __future__ import annotations
 
 import argparse
+import importlib
 import json
 import logging
 import os
 import sys
 import threading
+from datetime import timedelta
 from multiprocessing.connection import Listener
+
+from .shm import ShmSlot, remove_segments
+
+log = logging.getLogger("vep.child")
 
 # methods of Hub a parent may call
 EXPORTED = {"start_camera", "stop_camera", "state", "logs", "touch", "set_proxy", "proxy",
             "latest_frame_bytes", "latest_frame", "wait_decoded", "has"}
 
 
-def _serve(hub, conn, lock_stop: threading.Event) -> None:
-    while not lock_stop.is_set():
-        try:
-            req = conn.recv()
-        except (EOFError, OSError):
-            return
-        method, args, kwargs = req
-        try:
-            if method == "ping":
-                res = os.getpid()
-            elif method == "worker_stats":
-                w = hub.workers[0]
-                res = {"batches": w.batches, "frames": w.frames, "gpu_ms_total": w.gpu_ms_total,
-                       "direct_reads": bool(w.direct_reads), "decoder": str(w.decoder)}
-            elif method == "start_camera":
-                h = hub.start_camera(*args, **kwargs)
-                res = {"cam": h.cam}
-            elif method in EXPORTED:
-                res = getattr(hub, method)(*args, **kwargs)
-            else:
-                raise AttributeError(f"no such method {method!r}")
-            conn.send(("ok", res))
-        except Exception as e:  # noqa: BLE001 — the error travels back to the caller
+def frame_into(hub, slot: ShmSlot, name: str, after: int = 0, wait_ms: int = 0):
+    """Hub.latest_frame_bytes, written into the connection's shared-memory slot:
+    (seq, segment name, length, meta) or None."""
+    w, cam = hub.worker_of(name)
+    pub = w.published(cam)
+    if pub < after:
+        after = 0  # the cursor belongs to an older ring (see Hub.latest_frame_bytes)
+    if wait_ms > 0 and pub <= after:
+        w.wait_frame(cam, after, wait_ms)
+    for _ in range(3):
+        if slot.cap == 0:
+            need = w.video_frame_bound(cam, name)
+            if need == 0:
+                return None
+            slot.ensure(need)
+        r = w.video_frame_into(cam, after, name, slot.addr, slot.cap, slot.pinned)
+        if isinstance(r, int):  # a larger ring appeared (resolution change): grow, retry
+            slot.ensure(r)
+            continue
+        if r is None:
+            return None
+        seq, length, meta = r
+        meta["shm_pinned"] = slot.pinned
+        return seq, slot.name, length, meta
+    return None
+
+
+class RankGroup:
+    """This process's membership in the hub's process group and the gathered node batch."""
+
+    def __init__(self, hub, device: int, hook: str = ""):
+        self.hub, self.device = hub, device
+        self.epoch, self.rank, self.world, self.backend = -1, 0, 1, ""
+        self.batch = None  # (tensor on this rank's device, names) of the last gather
+        self.hook = None
+        if hook:
+            mod, _, fn = hook.partition(":")
+            self.hook = getattr(importlib.import_module(mod), fn)
+        self.gathers = 0
+
+    def form(self, epoch: int, port: int, rank: int, world: int, timeout_s: float = 60.0) -> dict:
+        import torch
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+        backend = "nccl" if self.device >= 0 else "gloo"
+        if self.device >= 0:
+            torch.cuda.set_device(self.device)
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
+                                timeout=timedelta(seconds=timeout_s))
+        self.epoch, self.rank, self.world, self.backend = epoch, rank, world, backend
+        return {"rank": rank, "world": world, "backend": backend}
+
+    def gather(self, epoch: int, names: list, k: int, order: list, perm: list, slot=None) -> dict:
+        """All-gather ``k`` consumer rows per rank (this rank's ``names``, zero-padded); reorder
+        the node batch by ``perm`` into the caller's camera ``order``. Every rank enters the
+        collective, whatever went wrong before it (a missing camera reads as a zero row), so one
+        bad request cannot leave the other ranks waiting."""
+        import torch
+        import torch.distributed as dist
+
+        if epoch != self.epoch:
+            raise RuntimeError(f"gather for group epoch {epoch}, this rank is in {self.epoch}")
+        hub = self.hub
+        src = hub.consumer[0]
+        local = torch.zeros((k, *src.shape[1:]), dtype=src.dtype, device=src.device)
+        missing = []
+        rows, at = [], []
+        for j, n in enumerate(names):
             try:
-                conn.send(("err", type(e).__name__, str(e)))
-            except (OSError, EOFError):
+                rows.append(hub.handle(n).cam)
+                at.append(j)
+            except KeyError:
+                missing.append(n)
+        if src.is_cuda:
+            torch.cuda.synchronize(src.device)  # the letterbox kernels of published frames
+        if rows:
+            local[torch.tensor(at, device=src.device)] = src.index_select(0, torch.tensor(rows, device=src.device))
+        out = torch.empty((self.world * k, *src.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, local)
+        batch = out.index_select(0, torch.tensor(perm, dtype=torch.long, device=out.device))
+        self.batch = (batch, list(order))
+        self.gathers += 1
+        if self.hook is not None:
+            self.hook(batch, list(order), self.rank)
+        res = {"rank": self.rank, "missing": missing, "shape": list(batch.shape)}
+        if slot is not None:
+            nbytes = batch.numel() * batch.element_size()
+            slot.ensure(max(nbytes, 1))
+            host = torch.frombuffer(slot.view(nbytes), dtype=torch.uint8) if nbytes else None
+            if host is not None:
+                host.copy_(batch.reshape(-1).view(torch.uint8))  # one D2H into the (page-locked) segment
+            res.update(segment=slot.name, nbytes=nbytes)
+        return res
+
+
+def _serve(hub, group: RankGroup, conn, stop: threading.Event) -> None:
+    slot = ShmSlot(hub.workers[0])
+    try:
+        while not stop.is_set():
+            try:
+                req = conn.recv()
+            except (EOFError, OSError):
                 return
+            method, args, kwargs = req
+            try:
+                if method == "ping":
+                    res = os.getpid()
+                elif method == "worker_stats":
+                    w = hub.workers[0]
+                    res = {"batches": w.batches, "frames": w.frames, "gpu_ms_total": w.gpu_ms_total,
+                           "direct_reads": bool(w.direct_reads), "decoder": str(w.decoder)}
+                elif method == "start_camera":
+                    h = hub.start_camera(*args, **kwargs)
+                    res = {"cam": h.cam}
+                elif method == "latest_frame_shm":
+                    res = frame_into(hub, slot, *args, **kwargs)
+                elif method == "group_form":
+                    res = group.form(*args, **kwargs)
+                elif method == "consumer_gather":
+                    to_host = kwargs.pop("to_host", False)
+                    res = group.gather(*args, slot=slot if to_host else None, **kwargs)
+                elif method == "group_info":
+                    res = {"epoch": group.epoch, "rank": group.rank, "world": group.world, "gathers": group.gathers,
+                           "backend": group.backend}
+                elif method in EXPORTED:
+                    res = getattr(hub, method)(*args, **kwargs)
+                else:
+                    raise AttributeError(f"no such method {method!r}")
+                conn.send(("ok", res))
+            except Exception as e:  # noqa: BLE001 — the error travels back to the caller
+                try:
+                    conn.send(("err", type(e).__name__, str(e)))
+                except (OSError, EOFError):
+                    return
+    finally:
+        slot.close()
 
 
 def main(argv=None) -> int:
@@ -66,6 +192,7 @@ def main(argv=None) -> int:
 
     cfg = _merge(Config(), json.loads(a.config))
     hub = Hub(cfg, devices=[a.device])
+    group = RankGroup(hub, a.device, cfg.gpu.consumer_hook)
     key = bytes.fromhex(os.environ["VEP_CHILD_KEY"])
     listener = Listener(("127.0.0.1", 0), authkey=key)
     stop = threading.Event()
@@ -78,7 +205,7 @@ def main(argv=None) -> int:
                 if stop.is_set():
                     return
                 continue
-            threading.Thread(target=_serve, args=(hub, conn, stop), daemon=True).start()
+            threading.Thread(target=_serve, args=(hub, group, conn, stop), daemon=True).start()
 
     threading.Thread(target=accept_loop, daemon=True, name="vep-child-accept").start()
     print(json.dumps({"port": listener.address[1], "pid": os.getpid()}), flush=True)
@@ -92,6 +219,14 @@ def main(argv=None) -> int:
     except Exception:  # noqa: BLE001
         pass
     hub.shutdown()
+    remove_segments(os.getpid())  # (serving threads are daemons: they do not unwind)
+    try:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        pass
     return 0
 
 

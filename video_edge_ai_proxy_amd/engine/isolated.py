@@ -16,9 +16,16 @@ do not drive this class (their pytest process holds a context); tests/test_isola
 with CPU-backend children.
 
 Calls travel over authenticated local connections (a small pool per child, so a blocking
-``latest_frame_bytes`` does not hold the others up). The batched consumer tensor of the
-in-process hub is not offered here; the multi-process form of it is ``parallel.ConsumerBatch``
-(one RCCL all-gather across rank processes).
+``latest_frame_bytes`` does not hold the others up); frames come back through a shared-memory
+segment per connection (engine/shm.py: the child DMAs the serialized ``VideoFrame`` into it, the
+front-end copies it out once), not through the socket.
+
+The children are the ranks of one ``torch.distributed`` group (RCCL over xGMI between GPUs, gloo
+for CPU-backend children). The parent forms it on demand — a fresh TCP rendezvous on 127.0.0.1
+per epoch, re-formed after any child restart, since a collective group cannot re-admit a rank —
+and ``consumer_batch()`` drives one all-gather of the letterboxed consumer rows across all
+ranks: every GPU then holds the node-wide batch (for ``gpu.consumer_hook`` consumers in the
+children) and one rank DMAs it into shared memory for the caller here.
 """
 from __future__ import annotations
 
@@ -33,11 +40,14 @@ import subprocess
 import sys
 import threading
 import time
+import socket
+from concurrent.futures import ThreadPoolExecutor
 from multiprocessing.connection import Client
 from typing import Optional
 
 from ..config import Config
 from .hub import CameraExists, CameraHandle, CameraNotFound, place_camera
+from .shm import ShmReader, remove_segments
 
 log = logging.getLogger("vep.isolated")
 
@@ -81,8 +91,8 @@ class _Child:
         self.pid = int(hello["pid"])
         self.port = int(hello["port"])
         self.free: queue.Queue = queue.Queue()
-        for _ in range(nconn):
-            self.free.put(Client(("127.0.0.1", self.port), authkey=key))
+        for _ in range(nconn):  # (connection, reader of its shared-memory segment)
+            self.free.put((Client(("127.0.0.1", self.port), authkey=key), ShmReader()))
         threading.Thread(target=self._drain, daemon=True).start()  # stray stdout never blocks it
 
     def _drain(self) -> None:
@@ -95,21 +105,39 @@ class _Child:
     def alive(self) -> bool:
         return self.proc.poll() is None
 
-    def call(self, method: str, *args, **kwargs):
+    def call(self, method: str, *args, read=None, **kwargs):
+        """Run ``method`` in the child. ``read(result, shm_reader)`` post-processes the result
+        while this connection (and so its shared-memory segment) is still held."""
         if not self.alive():
             raise WorkerRestarting(f"worker process for device {self.device} is restarting")
-        conn = self.free.get(timeout=60)
+        conn, shm = self.free.get(timeout=60)
         try:
             conn.send((method, args, kwargs))
             r = conn.recv()
+            if r[0] == "ok" and read is not None:
+                r = ("ok", read(r[1], shm))
         except (EOFError, OSError) as e:
+            shm.close()
             raise WorkerRestarting(f"worker process for device {self.device} died: {e}") from e
-        self.free.put(conn)
+        except BaseException:
+            self.free.put((conn, shm))
+            raise
+        self.free.put((conn, shm))
         if r[0] == "ok":
             return r[1]
         raise _ERRORS.get(r[1], RuntimeError)(r[2])
 
     def close_pipes(self) -> None:
+        while True:  # unmap the shared-memory segments and drop the connections
+            try:
+                conn, shm = self.free.get_nowait()
+            except (queue.Empty, AttributeError):
+                break
+            shm.close()
+            try:
+                conn.close()
+            except Exception:  # noqa: BLE001
+                pass
         for f in (self.proc.stdin, self.proc.stdout):
             try:
                 if f is not None:
@@ -128,6 +156,7 @@ class _Child:
             self.proc.kill()
             self.proc.wait()
         self.close_pipes()
+        remove_segments(self.pid)
 
 
 class _WorkerView:
@@ -171,13 +200,28 @@ class ProcessHub:
             devices = list(cfg.gpu.devices) if cfg.gpu.devices else _count_gpus()
         self.devices = devices or [-1]
         self._cfg_json = json.dumps(dataclasses.asdict(cfg))
-        self._children = [_Child(d, self._cfg_json) for d in self.devices]
+        with ThreadPoolExecutor(max_workers=len(self.devices)) as ex:  # start them side by side
+            futs = [ex.submit(_Child, d, self._cfg_json) for d in self.devices]
+        errs = [f.exception() for f in futs]
+        started = [f.result() for f, e in zip(futs, errs) if e is None]
+        if any(e is not None for e in errs):
+            for c in started:
+                c.close(timeout_s=5.0)
+            raise next(e for e in errs if e is not None)
+        self._children = started
         self.workers = [_WorkerView(self, i) for i in range(len(self.devices))]
         self.cameras: dict[str, CameraHandle] = {}
         self._specs: dict[str, dict] = {}
         self._proxy: dict[str, bool] = {}
         self.child_restarts = [0] * len(self.devices)
         self._lock = threading.RLock()
+        # the children's torch.distributed group: formed on demand, re-formed after a restart
+        self._group_epoch = 0
+        self._group_ok = False
+        self._group_lock = threading.Lock()
+        self._gather_lock = threading.Lock()
+        self._pool = ThreadPoolExecutor(max_workers=max(2, len(self.devices)), thread_name_prefix="vep-group")
+        self.group_timeout_s = 60.0
         self._stop = threading.Event()
         self._sup = threading.Thread(target=self._supervise, args=(supervise_interval_s,), daemon=True,
                                      name="vep-supervisor")
@@ -202,7 +246,10 @@ class ProcessHub:
                     log.error("restart of device %s failed: %s", self.devices[i], e)
 
     def _restart(self, i: int) -> None:
-        self._children[i].close_pipes()  # the dead child's pipes
+        dead = self._children[i]
+        dead.close_pipes()  # the dead child's pipes and shared-memory mappings
+        remove_segments(dead.pid)  # and the segments it could not unlink itself
+        self._group_ok = False  # the survivors' group lost a rank: re-form before the next gather
         child = _Child(self.devices[i], self._cfg_json)
         try:
             with self._lock:
@@ -273,9 +320,98 @@ class ProcessHub:
         h = self.handle(name)
         return self._children[h.worker_index].call(method, name, *args, **kwargs)
 
-    def consumer_batch(self, device=None, names=None):
-        raise RuntimeError("the batched consumer tensor is in-process only; with gpu.isolation: process "
-                           "use parallel.ConsumerBatch (RCCL all-gather across rank processes)")
+    # ------------------------------------------------------------------ rank group / consumer batch
+    def _on_all(self, method: str, per_child_args: list, **kwargs) -> list:
+        """Call ``method`` on every child concurrently (collectives need all ranks at once)."""
+        futs = [self._pool.submit(self._children[i].call, method, *per_child_args[i], **kwargs)
+                for i in range(len(self._children))]
+        out, err = [], None
+        for f in futs:
+            try:
+                out.append(f.result(timeout=self.group_timeout_s + 30))
+            except Exception as e:  # noqa: BLE001 — first error wins, after every rank returned
+                out.append(None)
+                err = err or e
+        if err is not None:
+            raise err
+        return out
+
+    def form_group(self) -> int:
+        """(Re-)form the children's process group with a fresh rendezvous. Returns its epoch."""
+        with self._group_lock:
+            if not all(c.alive() for c in self._children):
+                raise WorkerRestarting("a worker process is restarting")
+            self._group_epoch += 1
+            port = _free_port()
+            world = len(self._children)
+            try:
+                self._on_all("group_form", [(self._group_epoch, port, r, world, self.group_timeout_s)
+                                            for r in range(world)])
+            except Exception:
+                self._group_ok = False
+                raise
+            self._group_ok = True
+            return self._group_epoch
+
+    def consumer_batch(self, device=None, names=None, copy: bool = True):
+        """Node-wide letterboxed batch of the newest frame of every running camera (or of
+        ``names``, in that order): ``(tensor [N, S, S, 3] uint8 (or NV12 rows), names)``.
+
+        One all-gather across the worker processes (RCCL over xGMI between GPUs) assembles it on
+        every rank's GPU — where ``gpu.consumer_hook`` consumers receive it — and the rank of
+        ``device`` (default: the first) DMAs it into shared memory, returned here as a CPU tensor
+        (``copy=False``: a view of the segment, valid until the next call; this process never
+        touches a GPU). Rows of cameras that have not published a frame yet are zero."""
+        if int(self.cfg.gpu.letterbox_size) <= 0:
+            raise RuntimeError("consumer batch disabled (gpu.letterbox_size is 0)")
+        with self._lock:
+            order = list(names) if names is not None else sorted(self.cameras)
+            hs = [self.handle(n) for n in order]
+        per = [[] for _ in range(len(self._children))]
+        pos = []
+        for h in hs:
+            pos.append((h.worker_index, len(per[h.worker_index])))
+            per[h.worker_index].append(h.name)
+        k = max(1, max(len(p) for p in per))
+        perm = [r * k + j for r, j in pos]
+        dst = 0 if device is None else self.devices.index(device)
+        with self._gather_lock:  # one collective at a time, in the same order on every rank
+            return self._gather(per, k, order, perm, dst, copy)
+
+    def _gather(self, per, k, order, perm, dst, copy):
+        import numpy as np
+        import torch
+
+        world = len(self._children)
+        if not self._group_ok:
+            self.form_group()
+        epoch = self._group_epoch
+
+        def read(res, shm):
+            if "segment" not in res:
+                return res
+            buf = shm.buffer(res["segment"], res["nbytes"])
+            arr = np.frombuffer(buf, dtype=np.uint8)
+            t = torch.from_numpy(arr.copy() if copy else arr)
+            res["tensor"] = t.view(*res["shape"])
+            return res
+
+        futs = []
+        for r in range(world):
+            kw = dict(to_host=(r == dst))
+            futs.append(self._pool.submit(self._children[r].call, "consumer_gather", epoch, per[r], k, order, perm,
+                                          read=read if r == dst else None, **kw))
+        results, err = [], None
+        for f in futs:
+            try:
+                results.append(f.result(timeout=self.group_timeout_s + 30))
+            except Exception as e:  # noqa: BLE001
+                results.append(None)
+                err = err or e
+        if err is not None:
+            self._group_ok = False  # a failed collective may have left the group unusable
+            raise err
+        return results[dst]["tensor"], order
 
     def shutdown(self) -> None:
         self._stop.set()
@@ -287,6 +423,7 @@ class ProcessHub:
                 pass
         for c in self._children:
             c.close()
+        self._pool.shutdown(wait=False)
 
     # ------------------------------------------------------------------ state / control / frames
     def state(self, name: str) -> dict:
@@ -319,13 +456,30 @@ class ProcessHub:
         return bool(self._call(name, "proxy"))
 
     def latest_frame_bytes(self, name: str, after: int = 0, wait_ms: int = 0):
-        return self._call(name, "latest_frame_bytes", after, wait_ms)
+        """(seq, serialized VideoFrame, meta) or None: the child writes the frame into this
+        connection's shared-memory segment, copied out here once (the bytes grpcio sends)."""
+        def read(res, shm):
+            if res is None:
+                return None
+            seq, segment, length, meta = res
+            return seq, shm.read(segment, length), meta
+
+        h = self.handle(name)
+        return self._children[h.worker_index].call("latest_frame_shm", name, after, wait_ms, read=read)
 
     def latest_frame(self, name: str, after: int = 0):
         return self._call(name, "latest_frame", after)
 
     def wait_decoded(self, name: str, n: int = 1, timeout_s: float = 10.0) -> bool:
         return bool(self._call(name, "wait_decoded", n, timeout_s))
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
 
 
 def _count_gpus() -> list[int]:
