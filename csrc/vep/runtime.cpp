@@ -409,6 +409,7 @@ constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
 constexpr int kDefaultKfWindowUs = 8000;  // keyframe-only coalescing window (see WorkerOptions)
+constexpr bool kDefaultTuQueue = false;    // H.265 intra TUs: queue launch (true) / per level
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (opt_.decoder == kDecoderVcn)
@@ -439,8 +440,9 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       kw = ke ? std::atoi(ke) : kDefaultKfWindowUs;
     }
     kf_window_us_ = std::clamp(kw, 0, 100000);
-    const char* tl = std::getenv("VEP_HEVC_TU_LEVELS");  // 1: one intra TU launch per level
-    hevc_tu_levels_ = tl && tl[0] == '1';
+    // H.265 intra transform blocks: one queue launch per round (1) or one launch per level (0)
+    const char* tq = std::getenv("VEP_HEVC_TU_QUEUE");
+    hevc_tu_levels_ = tq ? tq[0] != '1' : !kDefaultTuQueue;
     int ns = opt_.stages;
     if (ns <= 0) {
       const char* se = std::getenv("VEP_STAGES");

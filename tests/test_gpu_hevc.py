@@ -17,3 +17,12 @@ pytestmark = pytest.mark.gpu
 def test_hevc_gpu_bit_exact(native, w, h, n, kw):
     published = run_camera(native, 0, w, h, n, **kw)
     assert published >= n // 2
+
+
+@pytest.mark.parametrize("queue", ["1", "0"], ids=["tu-queue", "tu-levels"])
+def test_hevc_gpu_intra_tu_scheduling(native, monkeypatch, queue):
+    """Both schedules of the intra transform blocks are bit-exact: one queue launch per round
+    (edge-word exchange between blocks) and one launch per dependency level."""
+    monkeypatch.setenv("VEP_HEVC_TU_QUEUE", queue)
+    published = run_camera(native, 0, 200, 120, 14, coverage=True, bframes=1, slices=2)
+    assert published >= 7

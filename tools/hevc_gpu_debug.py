@@ -12,7 +12,7 @@ from test_hevc_camera import synth_hevc  # noqa: E402
 
 
 def run(mode, w=200, h=120, n=14, **kw):
-    os.environ["VEP_HEVC_TU_LEVELS"] = mode
+    os.environ["VEP_HEVC_TU_QUEUE"] = mode
     s = synth_hevc(native, w, h, **kw)
     wk = native.Worker(device=0)
     cam = wk.add_camera("hevc", 4)
@@ -34,5 +34,5 @@ def run(mode, w=200, h=120, n=14, **kw):
 
 
 if __name__ == "__main__":
-    for mode in ("1", "0"):
+    for mode in ("0", "1"):
         run(mode, coverage=True, bframes=1, slices=2)
