@@ -147,7 +147,8 @@ __device__ inline void xg_put(u64* p, u32 epoch, u32 v) {
 __device__ inline u64 xg_get(const u64* p) {
   return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr u32 kXgSpinLimit = 1u << 20;  // x s_sleep 1: well under a second per wait
+constexpr u32 kXgSpinLimit = 1u << 18;  // x s_sleep 4: well under a second per wait
+constexpr int kTuQueueWgs = 128;
 
 // Reference samples of an intra block with the 64 lanes of a wave (the parallel form of
 // hk_prepare_refs, same result): gather by availability, substitution as "nearest available
@@ -197,7 +198,7 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* p
         if (xq && u32(w >> 32) != d.epoch) atomicOr(d.err, 2u);  // (the frame is dropped)
         break;
       }
-      __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_s_sleep(4);
       if (xq && u32(w >> 32) != d.epoch) {
         w = xg_get(wp);
         if (wp2 && u32(w >> 32) != d.epoch) w = xg_get(wp2);
@@ -447,8 +448,9 @@ void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nr
 void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, u32* ctr,
                           hipStream_t s) {
   if (nranges <= 0 || total_tus <= 0) return;
-  // persistent waves: enough to fill the chip (4 per workgroup), never more than blocks
-  const int wgs = std::min((total_tus + 3) / 4, 1024);
+  // persistent waves: a fraction of the chip (4 per workgroup) — the other lanes' kernels run
+  // beside it, and waves that run far ahead of the wavefront only poll
+  const int wgs = std::min((total_tus + 3) / 4, kTuQueueWgs);
   hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, total_tus, ctr);
 }
 
