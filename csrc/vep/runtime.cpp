@@ -408,7 +408,7 @@ constexpr int kDefaultLanes = 3;
 constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
-constexpr int kDefaultKfWindowUs = 8000;  // keyframe-only coalescing window (see WorkerOptions)
+constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
 constexpr bool kDefaultTuQueue = false;    // H.265 intra TUs: queue launch (true) / per level
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
@@ -726,7 +726,7 @@ void Worker::loop() {
             if (!j.keyframe_only) return false;
           return true;
         };
-        const size_t enough = 4 * lanes_.size();
+        const size_t enough = 8 * lanes_.size();
         const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(kf_window_us_);
         while (!stop_ && pending_.size() < enough && all_kf())
           if (q_cv_.wait_until(g, deadline) == std::cv_status::timeout) break;
