@@ -20,13 +20,14 @@ void MbNeighbours::reset(int wmbs, int hmbs) {
   h_ = hmbs;
   cur_ = -1;
   const size_t n = size_t(wmbs) * hmbs;
-  if (st_.size() != n) {
-    st_.assign(n, MbState{});
-    return;
+  if (++epoch_ == 0) {  // (after 2^32 pictures) no stale stamp may equal the new epoch
+    epoch_ = 1;
+    stamp_.clear();
   }
-  // Only `kind` marks "not decoded in this picture": every other field is rewritten when the MB
-  // is decoded (MbState{} first), so one byte per MB is enough (a 1080p state array is 2 MB).
-  for (MbState& st : st_) st.kind = 0xFF;
+  // every field of an MB's state is rewritten when the MB is decoded (MbState{} first), and
+  // begin() stamps the MB with the epoch: nothing to clear here
+  if (st_.size() != n) st_.assign(n, MbState{});
+  if (stamp_.size() != n) stamp_.assign(n, 0u);
 }
 
 static int coded_count(const MbState& s, int blk) {
@@ -1019,6 +1020,8 @@ int dpb_slots_for(const Sps& sps) {
 
 }  // namespace
 
+static void validate_picture(const Picture& p);
+
 PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   auto pic = pic_pool_->acquire([](Picture& p) {  // default state, pool capacities kept
     auto mbs = std::move(p.mbs);
@@ -1044,6 +1047,12 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   const Pps* act_pps = nullptr;
   std::vector<u8> scratch;
   std::vector<std::array<std::vector<u32>, 2>> slice_uids;  // list uids per slice (colocated motion)
+  ColBuild colb;
+  std::shared_ptr<ColMotion> col_built;
+  struct ColbGuard {  // the picture never keeps a pointer to this frame's ColBuild
+    Picture* p;
+    ~ColbGuard() { p->colb = nullptr; }
+  } colb_guard{pic.get()};
   for (size_t i = 0; i < au.nals.size(); ++i) {
     const u8* p = au.nal(i);
     const size_t n = au.nal_size(i);
@@ -1137,6 +1146,15 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       pic->au.tag = tag;
       nb_.reset(W, H);
       pic->target = pick_slot();  // (pictures waiting for output keep their slots until bump)
+      if (sh.nal_ref_idc != 0 && sps.profile_idc != 66) {  // B slices may use this motion
+        col_built = col_pool_->acquire([](ColMotion&) {});  // (every entry is written below)
+        col_built->wmbs = W;
+        col_built->hmbs = H;
+        col_built->corners = sps.direct_8x8;
+        col_built->b.resize(size_t(W) * H * size_t(sps.direct_8x8 ? 4 : 16));
+        colb.col = col_built.get();
+        pic->colb = &colb;
+      }
       got = true;
     } else {
       VEP_CHECK(&sps == act_sps, "slices of one picture reference different SPSs");
@@ -1147,6 +1165,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
     for (int l = 0; l < 2; ++l)
       for (const auto& e : list_[l]) uids[size_t(l)].push_back(e.uid);
     slice_uids.push_back(std::move(uids));
+    colb.uids = &slice_uids.back();
     if (legacy_slice(sh, sps, pps)) {
       const size_t stop = BitReader(r + 1, rn - 1).stop_bit_pos();
       SliceCtx sc{sh, pps, slice_idx, sh.type() == h264::kP, sh.qp, list_[0]};
@@ -1194,8 +1213,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   int missing = 0;
   for (int mb = 0; mb < pic->nmbs(); ++mb) {
     MbRec& m = pic->mbs[size_t(mb)];
-    if (nb_.at(mb).kind != 0xFF) continue;
+    if (nb_.decoded(mb)) continue;
     ++missing;
+    if (pic->colb) colb.none(mb);
     m = MbRec{};
     m.res = kNoRes;
     m.dbk = 1;
@@ -1218,60 +1238,97 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   pic->info.coded_mbs = pic->nmbs() - missing;
   const u32 uid = next_uid_++;
   if (first.nal_ref_idc != 0) {
-    std::shared_ptr<ColMotion> col;
-    if (act_sps->profile_idc != 66)  // B slices possible: keep the motion for direct prediction
-      col = build_col_motion(nb_, pic->wmbs, pic->hmbs, slice_uids, act_sps->direct_8x8, col_pool_.get());
-    mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col));
+    // (B slices possible: the motion for direct prediction, built as the MBs were stored)
+    mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col_built));
   }
   const bool boundary = first.idr() || first.has_mmco5();
   bump(*pic, boundary, boundary && (hard_flush || reorder_cur_ == 0));
-  validate(*pic);
+  // (store_mb validated every record as it was written; concealed ones are built in range)
+  if (missing) validate(*pic);
+  else validate_picture(*pic);
   return pic;
 }
 
-void validate(const Picture& p) {
+// One record against the picture's pools (store_mb checks every record as it is written, so
+// the GPU never sees an out-of-range index from a malformed stream).
+static inline void validate_mb(const Picture& p, const MbRec& m) {
+  const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size();
+  VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
+  VEP_CHECK(m.qp <= 51 && m.qpc <= 51 && m.qpc2 <= 51, "macroblock QP out of range");
+  if (m.kind == kIPcm) {
+    VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 32 <= nblocks, "I_PCM samples outside the pool");
+    return;
+  }
+  const size_t nb = size_t(__builtin_popcount(m.luma_coded)) + size_t(__builtin_popcount(m.chroma_coded));
+  VEP_CHECK(size_t(m.coef) + nb <= nblocks, "coefficient blocks outside the pool");
+  VEP_CHECK(m.chroma_mode <= 3 && m.i16_mode <= 3, "intra prediction mode out of range");
+  if (m.flags & kMbT8x8)
+    for (int q = 0; q < 4; ++q) {
+      const u32 g = (u32(m.luma_coded) >> ((q & 1) * 2 + (q >> 1) * 8)) & 0x33u;
+      VEP_CHECK(g == 0 || g == 0x33u, "8x8 residual block partially coded");
+    }
+  if (m.kind == kSkip || m.kind == kInter) {
+    VEP_CHECK(size_t(m.mv) + size_t(mv_per_list(m.flags)) * ((m.flags & kMbL1) ? 2 : 1) <= nmv,
+              "motion vectors outside the pool");
+    for (int k = 0; k < 4; ++k) {
+      const int r0 = m.ref[k], r1 = m.ref1[k];
+      VEP_CHECK(r0 != 0xFF || r1 != 0xFF, "inter partition without a reference");
+      VEP_CHECK((r0 == 0xFF || r0 < p.dpb_slots) && (r1 == 0xFF || r1 < p.dpb_slots),
+                "reference slot outside the DPB");
+      VEP_CHECK(r1 == 0xFF || (m.flags & kMbL1), "list-1 reference without list-1 motion");
+    }
+    if (m.flags & kMbWp) VEP_CHECK(size_t(m.wp) + 4 <= p.wps.size(), "weights outside the pool");
+  } else if (m.kind == kI4x4) {
+    for (u8 b : m.i4) VEP_CHECK((b & 15) <= 8 && (b >> 4) <= 8, "Intra_4x4 mode out of range");
+  } else if (m.kind == kI8x8) {
+    VEP_CHECK((m.flags & kMbT8x8) && (m.i4[0] & 15) <= 8 && (m.i4[0] >> 4) <= 8 && (m.i4[1] & 15) <= 8 &&
+                  (m.i4[1] >> 4) <= 8,
+              "Intra_8x8 mode out of range");
+  }
+  VEP_CHECK(m.res == kNoRes || (is_intra(m.kind) && m.res < u32(p.intra_res)), "residual slot out of range");
+}
+
+static void validate_picture(const Picture& p) {
   VEP_CHECK(p.dpb_slots >= 1 && p.dpb_slots <= kMaxDpbSlots && p.target >= 0 && p.target < p.dpb_slots,
             "picture DPB slots out of range");
   VEP_CHECK(p.wmbs > 0 && p.hmbs > 0 && p.mbs.size() == size_t(p.nmbs()), "picture size mismatch");
-  const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size();
-  for (const MbRec& m : p.mbs) {
-    VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
-    VEP_CHECK(m.qp <= 51 && m.qpc <= 51 && m.qpc2 <= 51, "macroblock QP out of range");
-    if (m.kind == kIPcm) {
-      VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 32 <= nblocks, "I_PCM samples outside the pool");
-      continue;
-    }
-    const size_t nb = size_t(__builtin_popcount(m.luma_coded)) + size_t(__builtin_popcount(m.chroma_coded));
-    VEP_CHECK(size_t(m.coef) + nb <= nblocks, "coefficient blocks outside the pool");
-    VEP_CHECK(m.chroma_mode <= 3 && m.i16_mode <= 3, "intra prediction mode out of range");
-    if (m.flags & kMbT8x8)
-      for (int q = 0; q < 4; ++q) {
-        const u32 g = (u32(m.luma_coded) >> ((q & 1) * 2 + (q >> 1) * 8)) & 0x33u;
-        VEP_CHECK(g == 0 || g == 0x33u, "8x8 residual block partially coded");
-      }
-    if (m.kind == kSkip || m.kind == kInter) {
-      VEP_CHECK(size_t(m.mv) + size_t(mv_per_list(m.flags)) * ((m.flags & kMbL1) ? 2 : 1) <= nmv,
-                "motion vectors outside the pool");
-      for (int k = 0; k < 4; ++k) {
-        const int r0 = m.ref[k], r1 = m.ref1[k];
-        VEP_CHECK(r0 != 0xFF || r1 != 0xFF, "inter partition without a reference");
-        VEP_CHECK((r0 == 0xFF || r0 < p.dpb_slots) && (r1 == 0xFF || r1 < p.dpb_slots),
-                  "reference slot outside the DPB");
-        VEP_CHECK(r1 == 0xFF || (m.flags & kMbL1), "list-1 reference without list-1 motion");
-      }
-      if (m.flags & kMbWp) VEP_CHECK(size_t(m.wp) + 4 <= p.wps.size(), "weights outside the pool");
-    } else if (m.kind == kI4x4) {
-      for (u8 b : m.i4) VEP_CHECK((b & 15) <= 8 && (b >> 4) <= 8, "Intra_4x4 mode out of range");
-    } else if (m.kind == kI8x8) {
-      VEP_CHECK((m.flags & kMbT8x8) && (m.i4[0] & 15) <= 8 && (m.i4[0] >> 4) <= 8 && (m.i4[1] & 15) <= 8 &&
-                    (m.i4[1] >> 4) <= 8,
-                "Intra_8x8 mode out of range");
-    }
-    VEP_CHECK(m.res == kNoRes || (is_intra(m.kind) && m.res < u32(p.intra_res)), "residual slot out of range");
-  }
+}
+
+void validate(const Picture& p) {
+  validate_picture(p);
+  for (const MbRec& m : p.mbs) validate_mb(p, m);
 }
 
 // ------------------------------------------------------------------------- shared internals
+
+void ColBuild::none(int mb) {
+  const int per = col->corners ? 4 : 16;
+  ColMotion::Blk* out = &col->b[size_t(mb) * size_t(per)];
+  for (int k = 0; k < per; ++k) out[k] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
+}
+
+void ColBuild::store(int mb, const MbState& st) {
+  if (is_intra(st.kind) || !uids) {
+    none(mb);
+    return;
+  }
+  static constexpr u8 kCorner[4] = {0, 3, 12, 15};  // outer corner 4x4 block of each 8x8
+  const int per = col->corners ? 4 : 16;
+  ColMotion::Blk* out = &col->b[size_t(mb) * size_t(per)];
+  const auto& lu = *uids;
+  for (int k = 0; k < per; ++k) {
+    const int blk = col->corners ? kCorner[k] : k;
+    const int b8 = ((blk >> 3) << 1) | ((blk & 3) >> 1);
+    const int l = st.ref[0][b8] >= 0 ? 0 : 1;
+    const int ri = st.ref[l][b8];
+    if (ri < 0) {
+      out[k] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
+      continue;
+    }
+    out[k] = ColMotion::Blk{{st.mv[l][blk][0], st.mv[l][blk][1]},
+                            size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u, i8(ri)};
+  }
+}
 
 std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, int hmbs,
                                             const std::vector<std::array<std::vector<u32>, 2>>& slice_uids,
@@ -1287,7 +1344,7 @@ std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, in
   for (int mb = 0; mb < wmbs * hmbs; ++mb) {
     const MbState& st = nb.at(mb);
     ColMotion::Blk* out = &col->b[size_t(mb) * size_t(per)];
-    if (st.kind == 0xFF || is_intra(st.kind) || slice_uids.empty()) {
+    if (!nb.decoded(mb) || is_intra(st.kind) || slice_uids.empty()) {
       for (int k = 0; k < per; ++k) out[k] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
       continue;
     }
@@ -1488,7 +1545,9 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   }
   m.res = is_intra(m.kind) && m.kind != kIPcm && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
   if (!(m.dbk & 1)) pic.deblock = true;
+  validate_mb(pic, m);
   pic.mbs[size_t(mb)] = m;
+  if (pic.colb) pic.colb->store(mb, s);
 }
 
 // ------------------------------------------------------------------------- CPU reconstruction

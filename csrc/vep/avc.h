@@ -26,6 +26,7 @@
 // UnsupportedStream (the VCN backend's job).
 #pragma once
 
+#include <array>
 #include <map>
 #include <memory>
 
@@ -53,6 +54,8 @@ struct OutFrame {
   int poc = 0;
 };
 
+struct ColBuild;
+
 // One parsed picture, ready for reconstruction into DPB slot `target`.
 struct Picture {
   int wmbs = 0, hmbs = 0;
@@ -76,6 +79,9 @@ struct Picture {
   // Pictures that left the reorder buffer when this one was decoded, in output order (the last
   // one is the newest frame a client can be shown after this picture).
   std::vector<OutFrame> outputs;
+  // While the decoder parses a reference picture whose motion later B pictures may use: the
+  // colocated-motion table, filled as each MB is stored (no pass over the picture afterwards).
+  ColBuild* colb = nullptr;
 
   int nmbs() const { return wmbs * hmbs; }
   const i16* block(u32 b) const { return coefs.data() + size_t(b) * 16; }
@@ -163,8 +169,11 @@ class MbNeighbours {
   // available. For locations inside `mb` itself returns mb.
   int mb_at(int mb, int x, int y) const;
   bool mb_available(int mb, int nb) const {
-    return nb >= 0 && st_[size_t(nb)].kind != 0xFF && st_[size_t(nb)].slice == st_[size_t(mb)].slice;
+    return nb >= 0 && stamp_[size_t(nb)] == epoch_ && st_[size_t(nb)].kind != 0xFF &&
+           st_[size_t(nb)].slice == st_[size_t(mb)].slice;
   }
+  // decoded in the current picture (announced by begin() since the last reset())
+  bool decoded(int mb) const { return stamp_[size_t(mb)] == epoch_ && st_[size_t(mb)].kind != 0xFF; }
   // nC for luma block (raster) `blk` / chroma component c block `blk` (§9.2.1).
   int nc_luma(int mb, int blk) const;
   int nc_chroma(int mb, int c, int blk) const;
@@ -191,6 +200,7 @@ class MbNeighbours {
   std::vector<MbState> take_state() {
     std::vector<MbState> v;
     v.swap(st_);
+    stamp_.clear();
     return v;
   }
 
@@ -203,6 +213,11 @@ class MbNeighbours {
   Nb motion_at(int mb, int x, int y, u16 done, int list) const;  // x, y in luma samples rel. to mb
   int w_ = 0, h_ = 0;
   int cur_ = -1, cx_ = 0, cy_ = 0, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
+  // "decoded in this picture": begin() stamped the MB with the picture's epoch (and its kind is
+  // set). A new picture bumps the epoch instead of touching every MB's 256-byte state (a 1080p
+  // state array is 2 MB; the stamps are 32 KB).
+  u32 epoch_ = 0;
+  std::vector<u32> stamp_;
   std::vector<MbState> st_;
 };
 
@@ -226,6 +241,7 @@ inline void MbNeighbours::begin(int mb) {
   cur_ = mb;
   cx_ = mx;
   cy_ = my;
+  stamp_[size_t(mb)] = epoch_;
   auto nb = [&](int nx, int ny) {
     if (nx < 0 || nx >= w_ || ny < 0) return -1;
     const int n = ny * w_ + nx;
@@ -288,6 +304,15 @@ struct ColMotion {
   size_t index(int mb, int blk) const {
     return corners ? size_t(mb) * 4 + size_t(((blk >> 3) << 1) | ((blk & 3) >> 1)) : size_t(mb) * 16 + size_t(blk);
   }
+};
+
+// Colocated motion built as the MBs of a picture are stored (store_mb): the entries of one MB
+// from its final state, with the picture uids of the current slice's reference lists.
+struct ColBuild {
+  ColMotion* col = nullptr;
+  const std::array<std::vector<u32>, 2>* uids = nullptr;  // the current slice's list uids
+  void store(int mb, const MbState& st);
+  void none(int mb);  // intra / concealed: no motion
 };
 
 // Reference picture (DPB entry).
