@@ -19,6 +19,7 @@ void MbNeighbours::reset(int wmbs, int hmbs) {
   w_ = wmbs;
   h_ = hmbs;
   cur_ = -1;
+  announced_ = 0;
   const size_t n = size_t(wmbs) * hmbs;
   if (++epoch_ == 0) {  // (after 2^32 pictures) no stale stamp may equal the new epoch
     epoch_ = 1;
@@ -1210,10 +1211,11 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   VEP_CHECK(got, "access unit has no slice");
   (void)act_pps;
   // conceal macroblocks no slice covered (lost slices): copy from the first reference, or grey
+  // (an MB announced but not finished would have thrown: announced = decoded here)
   int missing = 0;
-  for (int mb = 0; mb < pic->nmbs(); ++mb) {
+  for (int mb = 0; nb_.announced_count() < pic->nmbs() && mb < pic->nmbs(); ++mb) {
     MbRec& m = pic->mbs[size_t(mb)];
-    if (nb_.decoded(mb)) continue;
+    if (nb_.announced(mb)) continue;
     ++missing;
     if (pic->colb) colb.none(mb);
     m = MbRec{};

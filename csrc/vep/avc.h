@@ -174,6 +174,8 @@ class MbNeighbours {
   }
   // decoded in the current picture (announced by begin() since the last reset())
   bool decoded(int mb) const { return stamp_[size_t(mb)] == epoch_ && st_[size_t(mb)].kind != 0xFF; }
+  bool announced(int mb) const { return stamp_[size_t(mb)] == epoch_; }
+  int announced_count() const { return announced_; }  // distinct MBs announced this picture
   // nC for luma block (raster) `blk` / chroma component c block `blk` (§9.2.1).
   int nc_luma(int mb, int blk) const;
   int nc_chroma(int mb, int c, int blk) const;
@@ -217,6 +219,7 @@ class MbNeighbours {
   // set). A new picture bumps the epoch instead of touching every MB's 256-byte state (a 1080p
   // state array is 2 MB; the stamps are 32 KB).
   u32 epoch_ = 0;
+  int announced_ = 0;
   std::vector<u32> stamp_;
   std::vector<MbState> st_;
 };
@@ -241,7 +244,10 @@ inline void MbNeighbours::begin(int mb) {
   cur_ = mb;
   cx_ = mx;
   cy_ = my;
-  stamp_[size_t(mb)] = epoch_;
+  if (stamp_[size_t(mb)] != epoch_) {
+    stamp_[size_t(mb)] = epoch_;
+    ++announced_;
+  }
   auto nb = [&](int nx, int ny) {
     if (nx < 0 || nx >= w_ || ny < 0) return -1;
     const int n = ny * w_ + nx;

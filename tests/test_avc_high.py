@@ -214,3 +214,33 @@ def test_high_stream_corruption_never_crashes(native):
                     if pts < 18 * 3000:  # (pts = (display + reorder depth 2) * 3000)
                         continue
                     assert np.array_equal(y, want[pts]), f"trial {trial} pts {pts}"
+
+
+def test_lost_slice_is_concealed(native):
+    """A picture that loses one of its slices still decodes: the MBs no slice covered are
+    concealed from the first reference (P_Skip-like records, every record in range), the other
+    slices' MBs decode normally, and the next IDR is bit-exact again."""
+    enc = high_encoder(native, 176, 144, bframes=0, gop=6, seed=11, slices=3)
+    dec = native.CpuDecoder()
+    recon, got = {}, {}
+    lost_pts = None
+    for i in range(12):
+        au = enc.next()
+        y, uv = enc.picture()
+        recon[enc.last_pts] = (y.copy(), uv.copy())
+        if i == 3:  # a P picture: drop its second slice NAL
+            nals = au.nals()
+            slices = [k for k, n in enumerate(nals) if (n[0] & 0x1F) in (1, 5)]
+            assert len(slices) == 3
+            del nals[slices[1]]
+            au = native.AccessUnit.from_nals(nals, au.pts, au.dts, au.keyframe)
+            lost_pts = enc.last_pts
+        dec.decode(au)
+        got.update(dict(dec.frames()))
+    got.update(dict(dec.flush_frames()))
+    assert lost_pts in got and len(got) == 12
+    ey, gy = recon[lost_pts][0], got[lost_pts][0]
+    assert not np.array_equal(gy, ey)  # the lost rows are concealed, not decoded
+    assert np.array_equal(gy[:16], ey[:16])  # the first slice's rows are untouched by the loss
+    last = max(got)  # the GOP after the loss starts with an IDR: bit-exact again
+    assert np.array_equal(got[last][0], recon[last][0])
