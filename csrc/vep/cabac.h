@@ -76,6 +76,17 @@ struct Ctx {
   }
 };
 
+// rangeTabLPS indexed by qRangeIdx * 128 + (pStateIdx << 1 | valMps) (the MPS bit duplicates
+// the entries), so the decoder indexes it with the context byte as stored.
+struct RangeLpsFlat {
+  u8 v[4 * 128];
+  constexpr RangeLpsFlat() : v() {
+    for (int q = 0; q < 4; ++q)
+      for (int s = 0; s < 128; ++s) v[q * 128 + s] = kRangeLps[s >> 1][q];
+  }
+};
+inline constexpr RangeLpsFlat kRangeLpsFlat{};
+
 // Arithmetic decoder over an RBSP (byte positions are RBSP offsets). Bits are pulled from a
 // 64-bit MSB-aligned cache (refilled a word at a time) and renormalisation is one clz + shift;
 // a context-coded bin is branch-free apart from the rare refill (an MPS / LPS outcome is close to
@@ -101,7 +112,8 @@ class Decoder {
   }
   VEP_CABAC_INLINE u32 decision(Ctx& c) {
     const u32 s = c.s;
-    const u32 lps = kRangeLps[s >> 1][(range_ >> 6) & 3];
+    // (range & 0xC0) * 2 + (state << 1 | mps): one mask on the range -> LPS dependency chain
+    const u32 lps = kRangeLpsFlat.v[((range_ & 0xC0u) << 1) + s];
     const u32 rmps = range_ - lps;
     const u32 is_lps = offset_ >= rmps ? 1u : 0u;
     offset_ -= rmps & (0u - is_lps);
