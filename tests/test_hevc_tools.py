@@ -150,3 +150,43 @@ def test_intra_edge_exchange_is_consistent(name):
     rec.flush()
     st = rec.stats
     assert st["intra_tus"] > 0 and st["exchange_violations"] == 0, st
+
+
+@pytest.mark.parametrize("name", ["everything", "tiles_explicit", "scaling_cov", "long_term_b"])
+def test_tool_streams_corruption_never_crashes(name):
+    """Bit flips in the slice data and the parameter sets of the tool streams (tile grids,
+    entry points, scaling lists, weights, long-term RPS): the reference decoder and the records
+    decoder (CPU mirror of the GPU kernels, which must never index out of range) raise or
+    decode; neither crashes, and a clean decoder afterwards still decodes the stream."""
+    import random
+
+    rnd = random.Random(hash(name) & 0xFFFF)
+    _, _, _, aus, _ = run(n=8, **TOOLS[name])
+    for trial in range(10):
+        d, rec = v.HevcDecoder(), v.HevcRecordsDecoder()
+        for i, au in enumerate(aus):
+            nals = [bytearray(x) for x in au.nals()]
+            if rnd.random() < 0.5:
+                k = rnd.randrange(len(nals))
+                for _ in range(rnd.randint(1, 4)):
+                    pos = rnd.randrange(2, len(nals[k]))
+                    nals[k][pos] ^= 1 << rnd.randrange(8)
+                if rnd.random() < 0.2:
+                    nals[k] = nals[k][: max(3, len(nals[k]) // 2)]
+            bad = v.AccessUnit.from_nals([bytes(x) for x in nals], pts=au.pts, codec=1)
+            for dec in (d, rec):
+                try:
+                    dec.decode(bad)
+                except Exception:  # noqa: BLE001 — a NativeError / UnsupportedStream is fine
+                    pass
+        for dec in (d, rec):
+            try:
+                dec.flush()
+            except Exception:  # noqa: BLE001
+                pass
+    clean = v.HevcDecoder()
+    outs = []
+    for au in aus:
+        outs += clean.decode(au)
+    outs += clean.flush()
+    assert len(outs) == len(aus)
