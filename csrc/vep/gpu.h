@@ -15,6 +15,17 @@
 
 namespace vep::gpu {
 
+// Device-side view of the descriptors' buffer pointers in the kernel sources (which define
+// VEP_KERNEL_SOURCE): the global address space. Kernels then issue global_load / global_store
+// (counted by vmcnt only) instead of flat accesses, which also count against lgkmcnt and so tie
+// every LDS or scalar-load wait to outstanding global traffic. Same size and layout as the
+// plain pointers the host code fills in.
+#if defined(__HIP_DEVICE_COMPILE__) && defined(VEP_KERNEL_SOURCE)
+#define VEP_DEV __attribute__((address_space(1)))
+#else
+#define VEP_DEV
+#endif
+
 #define VEP_HIP(expr)                                                                    \
   do {                                                                                   \
     hipError_t _e = (expr);                                                              \
@@ -28,17 +39,17 @@ bool rocdecode_available();  // VCN backend library present (backend.cpp)
 
 // One camera-frame of a batched decode_convert launch (lives in device memory).
 struct DecodeDesc {
-  u8* y;              // NV12 luma plane, pitch = wmbs*16
-  u8* uv;             // NV12 interleaved chroma plane, pitch = wmbs*16
-  u8* bgr;            // output slot: out_h x out_w x 3 (packed BGR24); may be null
+  VEP_DEV u8* y;              // NV12 luma plane, pitch = wmbs*16
+  VEP_DEV u8* uv;             // NV12 interleaved chroma plane, pitch = wmbs*16
+  VEP_DEV u8* bgr;            // output slot: out_h x out_w x 3 (packed BGR24); may be null
   // Coded-MB bitmask (bit mb of word mb/32) + exclusive per-word popcount prefix: the payload
   // slot of a coded MB is prefix[w] + popc(mask[w] & below(mb)), slots in raster order.
   // null mask = no update (pure conversion). 2 bits/MB of H2D instead of a 32-bit map.
-  const u32* mask;
-  const u32* prefix;
-  const u32* offsets;  // per coded MB (raster order): byte offset of its 384 samples in payload
-  const u8* payload;   // the slices' bytes as received (samples read in place, unaligned)
-  const u64* ptrs;     // direct mode (non-null): per coded MB, device address of its samples in
+  const VEP_DEV u32* mask;
+  const VEP_DEV u32* prefix;
+  const VEP_DEV u32* offsets;  // per coded MB (raster order): byte offset of its 384 samples in payload
+  const VEP_DEV u8* payload;   // the slices' bytes as received (samples read in place, unaligned)
+  const VEP_DEV u64* ptrs;     // direct mode (non-null): per coded MB, device address of its samples in
                        // pinned host memory — read over PCIe; offsets/payload unused
   i32 wmbs, hmbs;
   i32 out_w, out_h;
@@ -50,7 +61,7 @@ struct DecodeDesc {
   // host memory) and the worker drops the frame.
   i32 chk_lo, chk_hi;
   u32 chk_pat;
-  u32* err;
+  VEP_DEV u32* err;
 };
 constexpr int kTileMbW = 8, kTileMbH = 2;  // 256 threads: 32 pixel rows x 8 MB columns
 inline int tiles_for(int wmbs, int hmbs) {
@@ -65,8 +76,8 @@ void launch_decode_convert_one(const DecodeDesc& d, hipStream_t s);
 // memory over PCIe — one workgroup per chunk, 16-byte loads per lane. Replaces a host memcpy
 // into staging + SDMA copy when the slice bytes already live in the pinned ingest pool.
 struct GatherChunk {
-  const u8* src;  // device address of pinned host memory (any alignment)
-  u8* dst;        // device memory, 16-byte aligned
+  const VEP_DEV u8* src;  // device address of pinned host memory (any alignment)
+  VEP_DEV u8* dst;        // device memory, 16-byte aligned
   u32 len;
   u32 pad;
 };
@@ -77,8 +88,8 @@ void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s);
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera
 // lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = `stride`).
 struct HevcDesc {
-  u8* y;
-  u8* uv;
+  VEP_DEV u8* y;
+  VEP_DEV u8* uv;
   u64 slot_y, slot_uv;
   i32 stride, width, height;
   i32 log2ctb, wctb, hctb;
@@ -86,25 +97,25 @@ struct HevcDesc {
   i32 cb_qp_offset, cr_qp_offset;
   i32 flags;             // bit 0 deblock, bit 1 SAO, bit 2 samples not loop-filtered (pcm_map),
                          // bit 3 SAO does not cross tile boundaries
-  const void* pus;       // hevc::GpuPu[npu]
-  const void* tus;       // hevc::GpuTu (level-sorted)
-  const i16* coefs;
-  const u8* pcm;
-  const u8* bs_v;
-  const u8* bs_h;
-  const signed char* qp;
-  const u8* pcm_map;
-  const u16* ctb_slice;
-  const void* slices;    // hevc::GpuSlice
-  const void* sao;       // hevc::GpuSao per CTB
-  u8* sao_y;             // device scratch: the deblocked picture (SAO input)
-  u8* sao_uv;
-  const void* wp;        // hevc::GpuWp (explicit weighted prediction, GpuPu::wp - 1)
-  const u16* ctb_tile;   // tile id per CTB
-  u32* err;              // the job's error word (bit 1: a dependency wait timed out)
+  const VEP_DEV void* pus;       // hevc::GpuPu[npu]
+  const VEP_DEV void* tus;       // hevc::GpuTu (level-sorted)
+  const VEP_DEV i16* coefs;
+  const VEP_DEV u8* pcm;
+  const VEP_DEV u8* bs_v;
+  const VEP_DEV u8* bs_h;
+  const VEP_DEV signed char* qp;
+  const VEP_DEV u8* pcm_map;
+  const VEP_DEV u16* ctb_slice;
+  const VEP_DEV void* slices;    // hevc::GpuSlice
+  const VEP_DEV void* sao;       // hevc::GpuSao per CTB
+  VEP_DEV u8* sao_y;             // device scratch: the deblocked picture (SAO input)
+  VEP_DEV u8* sao_uv;
+  const VEP_DEV void* wp;        // hevc::GpuWp (explicit weighted prediction, GpuPu::wp - 1)
+  const VEP_DEV u16* ctb_tile;   // tile id per CTB
+  VEP_DEV u32* err;              // the job's error word (bit 1: a dependency wait timed out)
   // Intra edge exchange (hevc_tu_queue_kernel): the camera's words, tagged with this round's
   // epoch, holding the right column / bottom row samples of every intra transform block.
-  u64* xg;
+  VEP_DEV u64* xg;
   i32 xg_h;              // coded height of the exchange's luma plane (width = stride)
   u32 epoch;             // tag of this round's words (never 0)
   i32 npu, pu_begin;     // exclusive prefix of PUs over the round
@@ -124,12 +135,13 @@ void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s
 // at tickets base .. base + count of the queue's ranges), one wave per block.
 void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
                     hipStream_t s);
-// Every intra transform block of the round in ONE launch: persistent waves take tickets in
-// level order from ctr[0] (zero at launch); a block reads the reference samples other intra
-// blocks of the launch write (GpuTu::pend) from their epoch-tagged edge words (HevcDesc::xg),
-// polled until current, and publishes its own right column / bottom row the same way.
-void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, u32* ctr,
-                          hipStream_t s);
+// Intra transform blocks at tickets base .. base + count (every intra level of the round, or a
+// window of consecutive levels) in ONE launch: persistent waves take tickets in level order from
+// ctr[0] (zero at launch); a block reads the reference samples other intra blocks of the round
+// write (GpuTu::pend) from their epoch-tagged edge words (HevcDesc::xg), polled until current,
+// and publishes its own right column / bottom row the same way.
+void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
+                          u32* ctr, hipStream_t s);
 // Deblocking of every vertical (dir 0) or horizontal (dir 1) edge of the round, one thread per
 // 4-line edge segment; then SAO (copy of the deblocked picture, one thread per sample).
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s);
@@ -139,24 +151,24 @@ void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera
 // lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = wmbs * 16).
 struct AvcDesc {
-  const void* mbs;     // avc::MbRec[wmbs * hmbs]
-  const i16* coefs;    // dequantised 4x4 blocks (16 x i16) / I_PCM samples
-  const i16* mvs;      // 32 x i16 per list per inter MB
-  const void* wps;     // avc::WpEntry pool (weighted prediction)
-  u8* y;
-  u8* uv;
+  const VEP_DEV void* mbs;     // avc::MbRec[wmbs * hmbs]
+  const VEP_DEV i16* coefs;    // dequantised 4x4 blocks (16 x i16) / I_PCM samples
+  const VEP_DEV i16* mvs;      // 32 x i16 per list per inter MB
+  const VEP_DEV void* wps;     // avc::WpEntry pool (weighted prediction)
+  VEP_DEV u8* y;
+  VEP_DEV u8* uv;
   u64 slot_y, slot_uv;
   i32 wmbs, hmbs;
   i32 target;          // DPB slot reconstructed into
   i32 constrained;     // constrained_intra_pred_flag
   i32 mb_begin;        // exclusive prefix of MBs over the round (inter kernel block -> picture)
   i32 pad;
-  u32* err;            // pinned flag: wavefront timeout (frame dropped)
-  void* dbk;           // device scratch: AvcDbkInfo[wmbs * hmbs] (avc_bs_kernel -> deblock)
-  i16* res;            // device scratch: kAvcResSamples per intra MB with residual (MbRec::res
+  VEP_DEV u32* err;            // pinned flag: wavefront timeout (frame dropped)
+  VEP_DEV void* dbk;           // device scratch: AvcDbkInfo[wmbs * hmbs] (avc_bs_kernel -> deblock)
+  VEP_DEV i16* res;            // device scratch: kAvcResSamples per intra MB with residual (MbRec::res
                        // slot; avc_inter_kernel -> avc_intra_kernel)
-  u64* prof;           // optional (VEP_AVC_PROF=1): kAvcProfSlots clock64() phase accumulators
-  u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
+  VEP_DEV u64* prof;           // optional (VEP_AVC_PROF=1): kAvcProfSlots clock64() phase accumulators
+  VEP_DEV u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
                        // tagged words per MB of every workgroup's last row (intra wavefront:
                        // words 0..7, zeroed by avc_inter_kernel; deblocking: all, zeroed by
                        // avc_bs_kernel)
@@ -203,12 +215,12 @@ void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
 
 struct LetterboxDesc {
-  const u8* y;
-  const u8* uv;
+  const VEP_DEV u8* y;
+  const VEP_DEV u8* uv;
   i32 pitch;
   i32 src_w, src_h, crop_left, crop_top;
-  u8* out_hwc;      // S*S*3 BGR u8, or null
-  void* out_chw;    // 3*S*S RGB normalised, or null
+  VEP_DEV u8* out_hwc;      // S*S*3 BGR u8, or null
+  VEP_DEV void* out_chw;    // 3*S*S RGB normalised, or null
   i32 nw, nh, pad_x, pad_y;
   float rx, ry;     // src/dst scale per axis
 };

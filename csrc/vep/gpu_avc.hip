@@ -21,6 +21,7 @@
 //    carried in LDS (same-wave read-after-write never goes through global memory).
 //
 // All sample arithmetic comes from avc_recon.h, shared with the CPU reference decoder.
+#define VEP_KERNEL_SOURCE 1  // descriptors' pointers are global-address-space here (gpu.h)
 #include "avc_recon.h"
 #include "gpu.h"
 
@@ -55,6 +56,27 @@ __device__ inline void wave_sync() {
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+
+// Global-memory accesses through address-space-1 pointers: global_load/global_store count only
+// against vmcnt. Generic (flat) accesses also count against lgkmcnt, so every LDS wait would
+// stall on them too — prefetches and fire-and-forget stores would serialise with the LDS work.
+#define VEP_GLOBAL __attribute__((address_space(1)))
+#define VEP_LDS __attribute__((address_space(3)))
+__device__ inline u32 gld1(const void* p) { return *(const VEP_GLOBAL u8*)(p); }
+__device__ inline u32 gld4(const void* p) { return *(const VEP_GLOBAL u32*)(p); }
+// (uint2 / uint4 are classes: a copy goes through a generic reference, so the loads use the
+// native vector types)
+typedef u32 vu2 __attribute__((ext_vector_type(2)));
+typedef u32 vu4 __attribute__((ext_vector_type(4)));
+__device__ inline uint2 gld8(const void* p) {
+  const vu2 v = *(const VEP_GLOBAL vu2*)(p);
+  return make_uint2(v.x, v.y);
+}
+__device__ inline uint4 gld16(const void* p) {
+  const vu4 v = *(const VEP_GLOBAL vu4*)(p);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
 
 // --------------------------------------------------------------------------------- inter
 
@@ -270,9 +292,11 @@ __device__ inline bool intra_avail(const AvcDesc& d, const MbRec& m, int nx, int
 // Tagged exchange words between the workgroups of one picture's wavefront (AvcDesc::xg): device-scope relaxed atomics (global_{load,store}_dwordx2 sc1, past
 // the per-CU L1), single-copy atomic, so a reader sees a word's data and tag together.
 __device__ inline void xg_put(u64* p, u32 v, u32 tag) {
-  __hip_atomic_store(p, u64(tag) << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store((VEP_GLOBAL u64*)p, u64(tag) << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ inline u64 xg_get(u64* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ inline u64 xg_get(u64* p) {
+  return __hip_atomic_load((VEP_GLOBAL u64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // --------------------------------------------------------------------------------- intra
 
@@ -293,10 +317,11 @@ struct alignas(16) IntraWave {
   u8 up[68];          // row above, MBs base-1 .. base+64 of the chunk: intra (published in xg)?
 };
 
-__device__ inline bool avail_hdr(const AvcDesc& d, const uint4& h, bool in_pic, u16 slice) {
+// h0 / h3: words 0 and 3 of the neighbour's MbRec (kind in byte 0, slice in bytes 14..15)
+__device__ inline bool avail_hdr(const AvcDesc& d, u32 h0, u32 h3, bool in_pic, u16 slice) {
   if (!in_pic) return false;
-  const u8 kind = u8(h.x & 0xff);
-  if (u16(h.w >> 16) != slice) return false;  // MbRec.slice lives in bytes 14..15
+  const u8 kind = u8(h0 & 0xff);
+  if (u16(h3 >> 16) != slice) return false;
   return !(d.constrained && !avc::is_intra(kind));
 }
 
@@ -320,19 +345,26 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
   // ---- loads that do not depend on the row above, issued before waiting for it: residual
   // samples, the left column (a left MB that is not carried is inter / I_PCM, final since the
   // inter kernel), neighbour headers, and top samples of non-intra MBs above
-  // residual samples (768 B = 48 lanes x 16 B), computed by the parallel inter pass
-  uint4 cv = make_uint4(0, 0, 0, 0);
-  if (m.res != avc::kNoRes && lane < 48)
-    cv = reinterpret_cast<const uint4*>(d.res + size_t(m.res) * kAvcResSamples)[lane];
-  u32 a = 128, b = 128;
-  // where sample `a` of a top lane comes from once the row above is ready: 0 = already loaded
-  // (or none), 1 = previous workgroup's exchange word, 2 = this workgroup's LDS line of the row
-  // above, 3 = the picture (the row above's intra MBs, no LDS line)
+  // residual samples (768 B = 48 lanes x 16 B), computed by the parallel inter pass.
+  // Every load below is ONE full-wave instruction from an address valid in every lane (unused
+  // lanes read a dummy, selected away after the wait): a load issued under a lane branch shares
+  // its destination VGPR with the other lanes' default, so the default's write had to wait for
+  // the load (vmcnt(0)) and every later load was serialised behind it.
+  const bool has_res = m.res != avc::kNoRes;  // (wave-uniform)
+  uint4 cv;  // (undefined without residual: never read)
+  if (has_res)
+    cv = gld16(reinterpret_cast<const uint4*>(d.res + size_t(m.res) * kAvcResSamples) + (lane < 48 ? lane : 47));
+  // where sample `a` of a lane comes from: 0 = the early load below (ga_ok) or none, 1 = previous
+  // workgroup's exchange word, 2 = this workgroup's LDS line of the row above, 3 = the picture
+  // (the row above's intra MBs, no LDS line), read once the row above is ready
   int src = 0, xw = -1, xsh = 0, lo = 0;
-  const u8* gp = nullptr;
+  const u8* gp = Y;
+  const u8* ga = Y;  // early source of `a` (ga_ok), else a dummy
+  bool ga_ok = false;
   auto top = [&](int n, const u8* g, int word, int sh, int lo_off) {
     if (!up_intra || !up_intra[n]) {
-      a = *g;
+      ga = g;
+      ga_ok = true;
     } else if (xi_in) {
       src = 1;
       xw = n * kAvcXgWords + word;
@@ -350,7 +382,10 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     if (up && px >= 0 && px < pitch)
       top(px >> 4, &Y[size_t(y0 - 1) * pitch + px], (px & 15) >> 2, (px & 3) * 8, px & 15);
   } else if (lane < 41) {  // luma left column
-    if (lf && !carry) a = Y[size_t(y0 + lane - 25) * pitch + x0 - 1];
+    if (lf && !carry) {
+      ga = &Y[size_t(y0 + lane - 25) * pitch + x0 - 1];
+      ga_ok = true;
+    }
   } else if (lane < 59) {  // chroma row above: x*8-1 .. x*8+7 per component
     const int c = (lane - 41) / 9, k = (lane - 41) % 9, px = x * 8 - 1 + k;
     if (up && px >= 0) {
@@ -358,24 +393,27 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       top(px >> 3, &UV[size_t(row * 8 - 1) * pitch + px * 2 + c], 4 + (bo >> 2), (bo & 3) * 8, 16 + bo);
     }
   }
-  if (lane >= 48) {  // chroma left columns
-    const int c = (lane - 48) >> 3, k = (lane - 48) & 7;
-    if (lf && !carry) b = UV[size_t(row * 8 + k) * pitch + (x * 8 - 1) * 2 + c];
-  }
-  uint4 h = make_uint4(0, 0, 0, 0);  // neighbour record headers: B, C, D, A
+  const u32 ra = gld1(ga);
+  const u8* gb = UV;  // chroma left columns (lanes 48..63), else a dummy
+  const bool gb_ok = lane >= 48 && lf && !carry;
+  if (gb_ok) gb = &UV[size_t(row * 8 + ((lane - 48) & 7)) * pitch + (x * 8 - 1) * 2 + ((lane - 48) >> 3)];
+  const u32 rb = gld1(gb);
+  // neighbour record headers: B, C, D, A (lanes 56..59)
   bool in_pic = false;
   if (lane == 56) in_pic = up;
   else if (lane == 57) in_pic = up && x + 1 < W;
   else if (lane == 58) in_pic = up && lf;
   else if (lane == 59) in_pic = lf;
-  if (in_pic) {
-    const int nx = lane == 56 ? x : lane == 57 ? x + 1 : x - 1, ny = lane == 59 ? row : row - 1;
-    h = *reinterpret_cast<const uint4*>(&recs[ny * W + nx]);
-  }
+  const int hnx = lane == 56 ? x : lane == 57 ? x + 1 : x - 1, hny = lane == 59 ? row : row - 1;
+  // (words 0 and 3 only: a dead component of a wider load is a register the compiler reuses,
+  // which would wait for the load to land)
+  const u32* hp = reinterpret_cast<const u32*>(&recs[in_pic ? hny * W + hnx : 0]);  // (read only where in_pic)
+  const u32 h0 = gld4(hp), h3 = gld4(hp + 3);
   // ---- the row above: this workgroup's (LDS counter, then LDS line / picture) or the
   // previous workgroup's (exchange words, polled)
   const u64 t_wait = d.prof ? clock64() : 0;
   if (wait_need) wait_row(sync, wave - 1, wait_need, d.err);
+  u32 xv = 0;
   if (xi_in) {  // (wave-uniform) poll the published words until every one is final
     u64 v = src == 1 ? xg_get(xi_in + xw) : 0;
     u32 spins = 0;
@@ -389,19 +427,22 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       __builtin_amdgcn_s_sleep(1);
       if (src == 1) v = xg_get(xi_in + xw);
     }
-    if (src == 1) a = u32(v >> xsh) & 0xffu;
+    if (src == 1) xv = u32(v >> xsh) & 0xffu;
   }
-  if (src == 2) a = line_in[lo];
-  else if (src == 3) a = *gp;
+  u32 a = ga_ok ? ra : 128u;
+  if (src == 1) a = xv;
+  else if (src == 2) a = *(const VEP_LDS u8*)(line_in + lo);
+  else if (src == 3) a = gld1(gp);
+  const u32 b = gb_ok ? rb : 128u;
   const u64 waited = d.prof ? clock64() - t_wait : 0;
   acc[0] += waited;
   // ---- availability (B, C, D, A) and the LDS neighbour tiles
-  const bool av = avail_hdr(d, h, in_pic, m.slice);
+  const bool av = avail_hdr(d, h0, h3, in_pic, m.slice);
   const bool B = __builtin_amdgcn_readlane(int(av), 56) != 0;
   const bool C = __builtin_amdgcn_readlane(int(av), 57) != 0;
   const bool D = __builtin_amdgcn_readlane(int(av), 58) != 0;
   const bool A = __builtin_amdgcn_readlane(int(av), 59) != 0;
-  if (lane < 48) reinterpret_cast<uint4*>(L.res)[lane] = cv;  // zeros without residual
+  if (lane < 48) reinterpret_cast<uint4*>(L.res)[lane] = has_res ? cv : make_uint4(0, 0, 0, 0);
   if (lane < 25) {
     L.tile[lane] = u8((lane == 0 ? D : lane <= 16 ? B : C) ? a : 128u);
   } else if (lane < 41) {
@@ -567,17 +608,17 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     const int ry = lane >> 2, rx = (lane & 3) * 4;
     const u8* src = &L.tile[(ry + 1) * kTp + rx + 1];
     const u32 w = u32(src[0]) | u32(src[1]) << 8 | u32(src[2]) << 16 | u32(src[3]) << 24;
-    *reinterpret_cast<u32*>(Y + size_t(y0 + ry) * pitch + x0 + rx) = w;
+    gst4(Y + size_t(y0 + ry) * pitch + x0 + rx, w);
     if (xi_out && lane >= 60) xg_put(xi_out + size_t(x) * kAvcXgWords + (lane - 60), w, 1u);
-    if (line_out && lane >= 60) *reinterpret_cast<u32*>(line_out + x * kIntraLine + (lane - 60) * 4) = w;
+    if (line_out && lane >= 60) *(VEP_LDS u32*)(line_out + x * kIntraLine + (lane - 60) * 4) = w;
     if (lane < 32) {  // NV12: 8 rows x 16 bytes
       const int cyr = lane >> 2, cxb = (lane & 3) * 2;
       const u8* c0 = &L.ctile[0][(cyr + 1) * kCp + cxb + 1];
       const u8* c1 = &L.ctile[1][(cyr + 1) * kCp + cxb + 1];
       const u32 cw = u32(c0[0]) | u32(c1[0]) << 8 | u32(c0[1]) << 16 | u32(c1[1]) << 24;
-      *reinterpret_cast<u32*>(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cxb) * 2) = cw;
+      gst4(UV + size_t(row * 8 + cyr) * pitch + (x * 8 + cxb) * 2, cw);
       if (xi_out && lane >= 28) xg_put(xi_out + size_t(x) * kAvcXgWords + 4 + (lane - 28), cw, 1u);
-      if (line_out && lane >= 28) *reinterpret_cast<u32*>(line_out + x * kIntraLine + 16 + (lane - 28) * 4) = cw;
+      if (line_out && lane >= 28) *(VEP_LDS u32*)(line_out + x * kIntraLine + 16 + (lane - 28) * 4) = cw;
     }
     if (lane < 16) L.carry[lane] = L.tile[(lane + 1) * kTp + 16];
     if (lane < 16) L.ccarry[lane >> 3][lane & 7] = L.ctile[lane >> 3][((lane & 7) + 1) * kCp + 8];
@@ -639,7 +680,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
         const uint2* src = reinterpret_cast<const uint2*>(&recs[row * W + x]);
         uint2* dst = reinterpret_cast<uint2*>(&L.rec[lane]);
         uint2 q[kWords];
-        for (int k = 0; k < kWords; ++k) q[k] = src[k];
+        for (int k = 0; k < kWords; ++k) q[k] = gld8(src + k);
         for (int k = 0; k < kWords; ++k) dst[k] = q[k];
         intra = avc::is_wave_intra(u8(q[0].x & 0xff));
       }
@@ -648,7 +689,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
           const int ax = base - 1 + q;
           u8 v = 0;
           if (ax >= 0 && ax < W) {
-            v = avc::is_wave_intra(recs[(row - 1) * W + ax].kind);
+            v = avc::is_wave_intra(u8(gld1(&recs[(row - 1) * W + ax].kind)));
           }
           L.up[q] = v;
         }
@@ -786,12 +827,6 @@ struct DbkSync {
 
 __device__ inline void st4(u8* p, u32 v) { *reinterpret_cast<u32*>(p) = v; }
 __device__ inline u32 ld4(const u8* p) { return *reinterpret_cast<const u32*>(p); }
-// Global-memory accesses through address-space-1 pointers: global_load/global_store count only
-// against vmcnt. Generic (flat) accesses also count against lgkmcnt, so every LDS wait would
-// stall on them too — prefetches and fire-and-forget stores would serialise with the LDS work.
-#define VEP_GLOBAL __attribute__((address_space(1)))
-__device__ inline u32 gld4(const void* p) { return *(const VEP_GLOBAL u32*)(p); }
-__device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
 
 // LDS-only handshake: progress counters and the data they guard both live in LDS.
 __device__ inline void wait_row_lds(DbkSync& s, int r, u32 need, u32* err) {

@@ -22,6 +22,7 @@
 //
 // All sample arithmetic comes from hevc_kern.h, shared with the CPU mirror (hevc_gpu.cpp) that
 // is tested bit-exact against the reference decoder.
+#define VEP_KERNEL_SOURCE 1  // descriptors' pointers are global-address-space here (gpu.h)
 #include <algorithm>
 
 #include "gpu.h"
@@ -74,8 +75,8 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
   const int stride = d.stride, W = d.width, H = d.height;
   u8* y = d.y + size_t(d.target) * d.slot_y;
   u8* uv = d.uv + size_t(d.target) * d.slot_uv;
-  const u8* ry[2] = {nullptr, nullptr};
-  const u8* ruv[2] = {nullptr, nullptr};
+  const VEP_DEV u8* ry[2] = {nullptr, nullptr};  // (global: a null initialiser would make them flat)
+  const VEP_DEV u8* ruv[2] = {nullptr, nullptr};
   for (int l = 0; l < 2; ++l)
     if ((u.pred >> l) & 1) {
       ry[l] = d.y + size_t(u.slot[l]) * d.slot_y;
@@ -258,7 +259,10 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* p
 
 // One transform block with one wave: PCM copy, or (intra prediction +) inverse transform +
 // reconstruction into the picture.
-__device__ void tu_wave(const HevcDesc& d, const GpuTu& t, int lane, TuWave& L, bool publish) {
+// (inlined into both launch kernels: as a call its pointer arguments would be generic, i.e. flat
+// accesses)
+__device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d, const GpuTu& t, int lane, TuWave& L,
+                                                              bool publish) {
   const int stride = d.stride;
   u8* y = d.y + size_t(d.target) * d.slot_y;
   u8* uv = d.uv + size_t(d.target) * d.slot_uv;
@@ -327,17 +331,20 @@ __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict
 // which it polls from the producers' epoch-tagged edge words: the data is its own flag, so there
 // is no completion counter, no release fence and no L2 writeback. A wait that exceeds the spin
 // limit marks the picture's error word (the frame is dropped) and goes on, so the grid drains.
+// Tickets base .. end of the round's queue (a window of consecutive levels, or all of them);
+// producers in an earlier window of the round finished before this launch started (stream order)
+// and their edge words already carry this round's epoch.
 __global__ __launch_bounds__(256) void hevc_tu_queue_kernel(const HevcDesc* __restrict__ descs,
                                                            const HevcTuRange* __restrict__ ranges, int nranges,
-                                                           int total, u32* __restrict__ ctr) {
+                                                           int base, int end, u32* __restrict__ ctr) {
   __shared__ TuWave lds[4];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   TuWave& L = lds[wave];
   for (;;) {
     int t = 0;
-    if (lane == 0) t = int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (lane == 0) t = base + int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     t = __shfl(t, 0);
-    if (t >= total) break;
+    if (t >= end) break;
     const HevcTuRange& rg = ranges[pick_range(ranges, nranges, t)];
     const HevcDesc& d = descs[rg.desc];
     tu_wave(d, static_cast<const GpuTu*>(d.tus)[rg.first + (t - rg.begin)], lane, L, true);
@@ -445,13 +452,14 @@ void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nr
                      base + count);
 }
 
-void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int total_tus, u32* ctr,
-                          hipStream_t s) {
-  if (nranges <= 0 || total_tus <= 0) return;
+void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
+                          u32* ctr, hipStream_t s) {
+  if (nranges <= 0 || count <= 0) return;
   // persistent waves: a fraction of the chip (4 per workgroup) — the other lanes' kernels run
   // beside it, and waves that run far ahead of the wavefront only poll
-  const int wgs = std::min((total_tus + 3) / 4, kTuQueueWgs);
-  hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, total_tus, ctr);
+  const int wgs = std::min((count + 3) / 4, kTuQueueWgs);
+  hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, base, base + count,
+                     ctr);
 }
 
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s) {

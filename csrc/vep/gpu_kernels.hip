@@ -10,6 +10,7 @@
 //    BGR row, a wave covers 8 rows (no LDS needed — there is no intra-tile reuse).
 //  * PCM slots are 384 = 24 x 16 B, so every payload read is an aligned dwordx4 / dwordx2.
 //  * letterbox reads the NV12 surface (1.5 B/px) instead of the BGR slot (3 B/px).
+#define VEP_KERNEL_SOURCE 1  // descriptors' pointers are global-address-space here (gpu.h)
 #include <algorithm>
 #include <cmath>
 

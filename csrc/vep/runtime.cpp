@@ -409,7 +409,8 @@ constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
 constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
-constexpr bool kDefaultTuQueue = false;    // H.265 intra TUs: queue launch (true) / per level
+constexpr int kDefaultTuWindow = 0;        // H.265 intra TUs: 0 = per-level launches, k = queue windows
+constexpr int kAllLevels = 1 << 20;        // (a window holding every level of a round)
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (opt_.decoder == kDecoderVcn)
@@ -440,9 +441,11 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       kw = ke ? std::atoi(ke) : kDefaultKfWindowUs;
     }
     kf_window_us_ = std::clamp(kw, 0, 100000);
-    // H.265 intra transform blocks: one queue launch per round (1) or one launch per level (0)
-    const char* tq = std::getenv("VEP_HEVC_TU_QUEUE");
-    hevc_tu_levels_ = tq ? tq[0] != '1' : !kDefaultTuQueue;
+    // H.265 intra transform blocks: one launch per level (VEP_HEVC_TU_QUEUE=0), one queue launch
+    // per round (=1), or one queue launch per window of k levels (VEP_HEVC_TU_WINDOW=k)
+    hevc_tu_window_ = kDefaultTuWindow;
+    if (const char* tq = std::getenv("VEP_HEVC_TU_QUEUE")) hevc_tu_window_ = tq[0] == '1' ? kAllLevels : 0;
+    if (const char* tw = std::getenv("VEP_HEVC_TU_WINDOW")) hevc_tu_window_ = std::clamp(std::atoi(tw), 0, kAllLevels);
     int ns = opt_.stages;
     if (ns <= 0) {
       const char* se = std::getenv("VEP_STAGES");
@@ -1070,8 +1073,10 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   // per round: level-0 ranges, level-0 blocks, intra (queue) ranges, intra blocks
   std::vector<std::array<int, 4>> hwork(static_cast<size_t>(hrounds), std::array<int, 4>{0, 0, 0, 0});
   std::vector<size_t> off_hctr(static_cast<size_t>(hrounds));
-  // per round and intra level: first ticket, blocks (the one-launch-per-level mode)
+  // per round and intra level: first ticket, blocks (the one-launch-per-level mode); per round
+  // and queue window: first ticket, blocks (one ticket counter each)
   std::vector<std::vector<std::array<int, 2>>> hlevels(static_cast<size_t>(hrounds));
+  std::vector<std::vector<std::array<int, 2>>> hwindows(static_cast<size_t>(hrounds));
   for (int r = 0; r < hrounds; ++r) {
     int maxl = 0;
     for (int i = 0; i < n; ++i) {
@@ -1130,10 +1135,18 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       }
     }
     hwork[size_t(r)][3] = tickets;
+    if (hevc_tu_window_ > 0) {  // consecutive levels, hevc_tu_window_ per launch
+      const auto& lv = hlevels[size_t(r)];
+      for (size_t l = 0; l < lv.size(); l += size_t(hevc_tu_window_)) {
+        const size_t e = std::min(lv.size(), l + size_t(hevc_tu_window_));
+        const int first = lv[l][0], last = lv[e - 1][0] + lv[e - 1][1];
+        if (last > first) hwindows[size_t(r)].push_back({first, last - first});
+      }
+    }
     off_hranges[size_t(r)] = need;
     need += al(std::max<size_t>(hranges[size_t(r)].size(), 1) * sizeof(gpu::HevcTuRange));
-    off_hctr[size_t(r)] = need;  // the queue's ticket / done counters (zero in the upload)
-    need += al(4 * sizeof(u32));
+    off_hctr[size_t(r)] = need;  // the queue windows' ticket counters (zero in the upload)
+    need += al(std::max<size_t>(hwindows[size_t(r)].size(), 1) * sizeof(u32));
   }
   const size_t off_gather = need;  // gather chunks: pinned records (+ slices without direct reads)
   need += al(sizeof(gpu::GatherChunk) * std::max<size_t>(nchunks, 1));
@@ -1431,7 +1444,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
           VEP_HIP(hipMemset(sf.hevc_xg, 0, words * sizeof(u64)));
           sf.hevc_epoch = 1;
         }
-        g.xg = hevc_tu_levels_ ? nullptr : sf.hevc_xg;  // (per-level launches read the picture)
+        g.xg = hevc_tu_window_ == 0 ? nullptr : sf.hevc_xg;  // (per-level launches read the picture)
         g.xg_h = sf.hmbs * 16;
         g.epoch = sf.hevc_epoch;
       }
@@ -1444,7 +1457,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     hround_work[size_t(r)] = {pus, blks};
     auto* hr = reinterpret_cast<gpu::HevcTuRange*>(st.h + off_hranges[size_t(r)]);
     for (size_t k = 0; k < hranges[size_t(r)].size(); ++k) hr[k] = hranges[size_t(r)][k];
-    std::memset(st.h + off_hctr[size_t(r)], 0, 4 * sizeof(u32));
+    std::memset(st.h + off_hctr[size_t(r)], 0, std::max<size_t>(hwindows[size_t(r)].size(), 1) * sizeof(u32));
   }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
@@ -1505,11 +1518,13 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     gpu::launch_hevc_mc(hd2, np, hround_work[size_t(r)][0], cs);
     const auto& hw = hwork[size_t(r)];
     gpu::launch_hevc_tu(hd2, hr, hw[0], 0, hw[1], cs);
-    if (hevc_tu_levels_) {  // one launch per intra level (kernel boundaries order the levels)
+    if (hevc_tu_window_ == 0) {  // one launch per intra level (kernel boundaries order the levels)
       for (const auto& lv : hlevels[size_t(r)]) gpu::launch_hevc_tu(hd2, hr + hw[0], hw[2], lv[0], lv[1], cs);
-    } else {
-      gpu::launch_hevc_tu_queue(hd2, hr + hw[0], hw[2], hw[3], reinterpret_cast<u32*>(st.d + off_hctr[size_t(r)]),
-                                cs);
+    } else {  // one queue launch per window of levels, in level order on the stream
+      auto* ctr = reinterpret_cast<u32*>(st.d + off_hctr[size_t(r)]);
+      for (size_t k = 0; k < hwindows[size_t(r)].size(); ++k)
+        gpu::launch_hevc_tu_queue(hd2, hr + hw[0], hw[2], hwindows[size_t(r)][k][0], hwindows[size_t(r)][k][1],
+                                  ctr + k, cs);
     }
     if (dbk) {
       gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 0, cs);

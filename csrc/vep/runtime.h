@@ -433,7 +433,9 @@ class Worker {
   std::condition_variable q_cv_, idle_cv_;
   std::vector<DecodeJob> pending_;
   int kf_window_us_ = 0;
-  bool hevc_tu_levels_ = false;
+  // H.265 intra transform blocks: 0 = one launch per dependency level; k > 0 = one queue launch
+  // per window of k consecutive levels (kAllLevels: the whole round in one launch)
+  int hevc_tu_window_ = 0;
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;

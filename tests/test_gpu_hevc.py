@@ -19,10 +19,16 @@ def test_hevc_gpu_bit_exact(native, w, h, n, kw):
     assert published >= n // 2
 
 
-@pytest.mark.parametrize("queue", ["1", "0"], ids=["tu-queue", "tu-levels"])
-def test_hevc_gpu_intra_tu_scheduling(native, monkeypatch, queue):
-    """Both schedules of the intra transform blocks are bit-exact: one queue launch per round
-    (edge-word exchange between blocks) and one launch per dependency level."""
-    monkeypatch.setenv("VEP_HEVC_TU_QUEUE", queue)
+@pytest.mark.parametrize("env", [{"VEP_HEVC_TU_QUEUE": "1"}, {"VEP_HEVC_TU_QUEUE": "0"},
+                                 {"VEP_HEVC_TU_WINDOW": "3"}, {"VEP_HEVC_TU_WINDOW": "8"}],
+                         ids=["tu-queue", "tu-levels", "tu-window3", "tu-window8"])
+def test_hevc_gpu_intra_tu_scheduling(native, monkeypatch, env):
+    """Every schedule of the intra transform blocks is bit-exact: one queue launch per round
+    (edge-word exchange between blocks), one launch per dependency level, and one queue launch
+    per window of k levels (the exchange also spans windows)."""
+    monkeypatch.delenv("VEP_HEVC_TU_QUEUE", raising=False)
+    monkeypatch.delenv("VEP_HEVC_TU_WINDOW", raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
     published = run_camera(native, 0, 200, 120, 14, coverage=True, bframes=1, slices=2)
     assert published >= 7
