@@ -8,6 +8,7 @@
 
 #include "vep/hostprof.h"
 #include "vep/avc_cavlc.h"
+#include "vep/avc_recon.h"
 #include "vep/bench_driver.h"
 #include "vep/cabac.h"
 #include "vep/codec.h"
@@ -753,6 +754,45 @@ PYBIND11_MODULE(_vep, m) {
     d["dependent"] = sh.dependent;
     d["segment_address"] = sh.segment_address;
     return d;
+  });
+  // Intra_8x8 tap forms (intra8x8_pred_tap / intra8x8_filter_tap, the GPU kernel's branch-free
+  // form) against the direct formulas (intra8x8_pred_g / intra8x8_filter_at) on random samples:
+  // every mode but DC, every sample position, every availability combination. Returns the
+  // number of mismatching samples.
+  m.def("avc_intra8x8_tap_check", [](u64 seed, int trials) {
+    u64 st = seed * 0x9E3779B97F4A7C15ull + 7;
+    auto rnd = [&]() {
+      st ^= st << 13;
+      st ^= st >> 7;
+      st ^= st << 17;
+      return int(st & 255);
+    };
+    int bad = 0;
+    for (int t = 0; t < trials; ++t) {
+      int s[25];
+      for (int k = 0; k < 25; ++k) s[k] = (t & 3) == 0 ? (rnd() & 1) * 255 : rnd();  // extremes too
+      auto T = [&](int i) { return s[1 + i]; };
+      auto L = [&](int j) { return j < 0 ? s[0] : s[17 + j]; };
+      for (int mode = 0; mode < 9; ++mode) {
+        if (mode == 2) continue;
+        for (int y = 0; y < 8; ++y)
+          for (int x = 0; x < 8; ++x) {
+            const u32 tw = avc::intra8x8_pred_tap(mode, x, y);
+            const int got = avc::eval_tap8(tw, s[tw & 31], s[(tw >> 5) & 31], s[(tw >> 10) & 31]);
+            bad += got != avc::intra8x8_pred_g(T, L, true, true, mode, x, y);
+          }
+      }
+      for (int av = 0; av < 8; ++av) {
+        const bool top = av & 1, left = av & 2, tl = av & 4;
+        for (int k = 0; k < 25; ++k) {
+          const u32 tw = avc::intra8x8_filter_tap(top, left, tl, k);
+          const int got =
+              (tw & avc::kTap8Const) ? 128 : avc::eval_tap8(tw, s[tw & 31], s[(tw >> 5) & 31], s[(tw >> 10) & 31]);
+          bad += got != avc::intra8x8_filter_at(T, [&](int j) { return s[17 + j]; }, top, left, tl, k);
+        }
+      }
+    }
+    return bad;
   });
   // Random-bin CABAC engine round trip (context-coded with skewed and flipping statistics,
   // bypass, terminate-0 and a final terminate-1 flush). Returns (ok, coded_bytes).

@@ -385,6 +385,92 @@ VEP_HD int intra8x8_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, in
   }
 }
 
+// Intra_8x8 as taps, for the GPU's branch-free form (each lane: three loads + one multiply-add,
+// no lane-divergent path per mode): a sample is (w0 * s[i0] + w1 * s[i1] + w2 * s[i2] + add) >>
+// shift over 25 samples in the intra8x8_filter layout (0 = p[-1,-1], 1 + x = p[x,-1],
+// 17 + y = p[-1,y]). Packed: bits 0-4 i0, 5-9 i1, 10-14 i2, 15-16 w0, 17-18 w1, 19-20 w2,
+// 21-22 add, 23-24 shift; kTap8Const: the sample is 128 (side unavailable); kTap8Dc: DC mode.
+constexpr u32 kTap8Const = 1u << 30, kTap8Dc = 1u << 31;
+VEP_HD u32 pack_tap8(int i0, int i1, int i2, int w0, int w1, int w2, int add, int shift) {
+  return u32(i0) | u32(i1) << 5 | u32(i2) << 10 | u32(w0) << 15 | u32(w1) << 17 | u32(w2) << 19 |
+         u32(add) << 21 | u32(shift) << 23;
+}
+VEP_HD int eval_tap8(u32 t, int s0, int s1, int s2) {
+  return (int((t >> 15) & 3) * s0 + int((t >> 17) & 3) * s1 + int((t >> 19) & 3) * s2 + int((t >> 21) & 3)) >>
+         int((t >> 23) & 3);
+}
+// Prediction sample (x, y) of `mode` (intra8x8_pred_g) over the filtered references.
+VEP_HD u32 intra8x8_pred_tap(int mode, int x, int y) {
+  auto T = [](int i) { return 1 + i; };            // p'[i,-1], i = -1..15
+  auto L = [](int j) { return j < 0 ? 0 : 17 + j; };  // p'[-1,j], j = -1..7
+  auto t3 = [](int a, int b, int c) { return pack_tap8(a, b, c, 1, 2, 1, 2, 2); };
+  auto t2 = [](int a, int b) { return pack_tap8(a, b, 0, 1, 1, 0, 1, 1); };
+  auto cp = [](int a) { return pack_tap8(a, a, a, 1, 2, 1, 2, 2); };  // (4a + 2) >> 2 = a
+  switch (mode) {
+    case 0: return cp(T(x));
+    case 1: return cp(L(y));
+    case 2: return kTap8Dc;
+    case 3:
+      if (x == 7 && y == 7) return pack_tap8(T(14), T(15), 0, 1, 3, 0, 2, 2);
+      return t3(T(x + y), T(x + y + 1), T(x + y + 2));
+    case 4:
+      if (x > y) return t3(T(x - y - 2), T(x - y - 1), T(x - y));
+      if (x < y) return t3(L(y - x - 2), L(y - x - 1), L(y - x));
+      return t3(T(0), T(-1), L(0));
+    case 5: {
+      const int z = 2 * x - y;
+      if (z >= 0 && (z & 1) == 0) return t2(T(x - (y >> 1) - 1), T(x - (y >> 1)));
+      if (z >= 0) return t3(T(x - (y >> 1) - 2), T(x - (y >> 1) - 1), T(x - (y >> 1)));
+      if (z == -1) return t3(L(0), L(-1), T(0));
+      return t3(L(y - 2 * x - 1), L(y - 2 * x - 2), L(y - 2 * x - 3));
+    }
+    case 6: {
+      const int z = 2 * y - x;
+      if (z >= 0 && (z & 1) == 0) return t2(L(y - (x >> 1) - 1), L(y - (x >> 1)));
+      if (z >= 0) return t3(L(y - (x >> 1) - 2), L(y - (x >> 1) - 1), L(y - (x >> 1)));
+      if (z == -1) return t3(L(0), L(-1), T(0));
+      return t3(T(x - 2 * y - 1), T(x - 2 * y - 2), T(x - 2 * y - 3));
+    }
+    case 7:
+      if ((y & 1) == 0) return t2(T(x + (y >> 1)), T(x + (y >> 1) + 1));
+      return t3(T(x + (y >> 1)), T(x + (y >> 1) + 1), T(x + (y >> 1) + 2));
+    default: {  // 8
+      const int z = x + 2 * y;
+      if (z > 13) return cp(L(7));
+      if (z == 13) return pack_tap8(L(6), L(7), 0, 1, 3, 0, 2, 2);
+      if ((z & 1) == 0) return t2(L(y + (x >> 1)), L(y + (x >> 1) + 1));
+      return t3(L(y + (x >> 1)), L(y + (x >> 1) + 1), L(y + (x >> 1) + 2));
+    }
+  }
+}
+// Filtered reference k (intra8x8_filter_at) over the unfiltered samples in the same layout.
+VEP_HD u32 intra8x8_filter_tap(bool has_top, bool has_left, bool has_tl, int k) {
+  auto T = [](int i) { return 1 + i; };
+  auto L = [](int j) { return 17 + j; };
+  auto t3 = [](int a, int b, int c) { return pack_tap8(a, b, c, 1, 2, 1, 2, 2); };
+  auto w31 = [](int a, int b) { return pack_tap8(a, b, 0, 3, 1, 0, 2, 2); };  // (3a + b + 2) >> 2
+  auto w13 = [](int a, int b) { return pack_tap8(a, b, 0, 1, 3, 0, 2, 2); };  // (a + 3b + 2) >> 2
+  if (k == 0) {
+    if (!has_tl) return kTap8Const;
+    if (has_top && has_left) return t3(T(0), T(-1), L(0));
+    if (has_top) return w31(T(-1), T(0));
+    if (has_left) return w31(T(-1), L(0));
+    return t3(T(-1), T(-1), T(-1));
+  }
+  if (k <= 16) {
+    if (!has_top) return kTap8Const;
+    const int x = k - 1;
+    if (x == 0) return has_tl ? t3(T(-1), T(0), T(1)) : w31(T(0), T(1));
+    if (x == 15) return w13(T(14), T(15));
+    return t3(T(x - 1), T(x), T(x + 1));
+  }
+  if (!has_left) return kTap8Const;
+  const int y = k - 17;
+  if (y == 0) return has_tl ? t3(T(-1), L(0), L(1)) : w31(L(0), L(1));
+  if (y == 7) return w13(L(6), L(7));
+  return t3(L(y - 1), L(y), L(y + 1));
+}
+
 VEP_HD int intra8x8_pred(const int* f, bool has_top, bool has_left, int mode, int x, int y) {
   return intra8x8_pred_g([&](int xx) { return f[1 + xx]; }, [&](int yy) { return yy < 0 ? f[0] : f[17 + yy]; },
                          has_top, has_left, mode, x, y);

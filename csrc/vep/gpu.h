@@ -137,7 +137,8 @@ void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nr
                     hipStream_t s);
 // Intra transform blocks at tickets base .. base + count (every intra level of the round, or a
 // window of consecutive levels) in ONE launch: persistent waves take tickets in level order from
-// ctr[0] (zero at launch); a block reads the reference samples other intra blocks of the round
+// ctr[0] (zero at launch), or (ctr null) one wave per block in grid order; a block reads the
+// reference samples other intra blocks of the round
 // write (GpuTu::pend) from their epoch-tagged edge words (HevcDesc::xg), polled until current,
 // and publishes its own right column / bottom row the same way.
 void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,

@@ -333,7 +333,8 @@ __device__ inline bool avail_hdr(const AvcDesc& d, u32 h0, u32 h3, bool in_pic, 
 // `up_intra[n]` says whether MB n of the row above is such an MB. The last row of a workgroup
 // publishes its bottom lines to `xi_out`.
 __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, int row, bool carry,
-                         int lane, const u32* tap_lut, u64 t_start, u64* acc, Sync& sync, int wave,
+                         int lane, const u32* tap_lut, const u32* tap8_lut, u64 t_start, u64* acc, Sync& sync,
+                         int wave,
                          u32 wait_need, u64* xi_in, const u8* up_intra, const u8* line_in, u8* line_out,
                          u64* xi_out) {
   const int W = d.wmbs, pitch = W * 16;
@@ -429,10 +430,12 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
     }
     if (src == 1) xv = u32(v >> xsh) & 0xffu;
   }
-  u32 a = ga_ok ? ra : 128u;
-  if (src == 1) a = xv;
-  else if (src == 2) a = *(const VEP_LDS u8*)(line_in + lo);
-  else if (src == 3) a = gld1(gp);
+  // the other sources, again one full-wave load each (line_in / xi_in are wave-uniform; lanes
+  // that do not read one use a valid dummy address), then one select per lane
+  u32 lv = 0, gv = 0;
+  if (line_in) lv = *(const VEP_LDS u8*)(line_in + lo);
+  else if (!xi_in) gv = gld1(gp);
+  const u32 a = src == 1 ? xv : src == 2 ? lv : src == 3 ? gv : ga_ok ? ra : 128u;
   const u32 b = gb_ok ? rb : 128u;
   const u64 waited = d.prof ? clock64() - t_wait : 0;
   acc[0] += waited;
@@ -492,24 +495,41 @@ __device__ void intra_mb(const AvcDesc& d, IntraWave& L, const MbRec& m, int x, 
       L.tile[((p >> 4) + 1) * kTp + (p & 15) + 1] = out[k];
     }
   } else if (m.kind == avc::kI8x8) {
-    // Intra_8x8: four blocks in order; per block lanes 0-24 filter the 25 reference samples
-    // (§8.3.2.2.1) into LDS, then every lane predicts one sample and adds its residual.
+    // Intra_8x8 in tap form (avc::intra8x8_filter_tap / intra8x8_pred_tap): four blocks in
+    // order; per block lanes 0-24 filter the 25 reference samples (§8.3.2.2.1) into LDS, three
+    // loads and one multiply-add each, then every lane predicts its sample from its tap word
+    // (DC: a wave reduction) and adds its residual. No lane-divergent path per filter position
+    // or prediction mode, so each step is one round of LDS loads.
+    const int px = lane & 7, py = lane >> 3;
     for (int q = 0; q < 4; ++q) {
       const int bx = q & 1, by = q >> 1;
       const bool top = by > 0 || B, left = bx > 0 || A;
       const bool tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
       const bool tr = by == 0 ? (bx == 0 ? B : C) : (bx == 0);
       const u8* nb = &L.tile[(by * 8) * kTp + bx * 8];  // p[-1,-1] of the block
-      auto Tr = [&](int xx) -> int { return nb[1 + (xx >= 8 && !tr ? 7 : xx)]; };
-      auto Lr = [&](int yy) -> int { return nb[(yy + 1) * kTp]; };
-      if (lane < 25) L.pf[lane] = u8(avc::intra8x8_filter_at(Tr, Lr, top, left, tl, lane));
+      const int mode = avc::i4_mode(m, q);
+      const int rs = L.res[(by * 8 + py) * 16 + bx * 8 + px];
+      const u32 pw = tap8_lut[mode * 64 + lane];
+      if (lane < 25) {
+        const u32 fw = avc::intra8x8_filter_tap(top, left, tl, lane);
+        // sample u of the layout -> tile offset from p[-1,-1] (two selects: p[-1,-1] = 0,
+        // p[x,-1] = 1 + x with the top-right substitution, p[-1,y] = (y + 1) * kTp)
+        auto off = [&](u32 u) -> int { return u > 16 ? int(u - 16) * kTp : (u >= 9 && !tr) ? 8 : int(u); };
+        const int s0 = nb[off(fw & 31)], s1 = nb[off((fw >> 5) & 31)], s2 = nb[off((fw >> 10) & 31)];
+        const int fv = avc::eval_tap8(fw, s0, s1, s2);  // (kTap8Const: indices 0, value unused)
+        L.pf[lane] = u8((fw & avc::kTap8Const) ? 128 : fv);
+      }
       wave_sync();
-      const int px = lane & 7, py = lane >> 3;
-      auto Tf = [&](int xx) -> int { return L.pf[1 + xx]; };
-      auto Lf = [&](int yy) -> int { return yy < 0 ? L.pf[0] : L.pf[17 + yy]; };
-      const int v = avc::intra8x8_pred_g(Tf, Lf, top, left, avc::i4_mode(m, q), px, py) +
-                    L.res[(by * 8 + py) * 16 + bx * 8 + px];
-      L.tile[(by * 8 + py + 1) * kTp + bx * 8 + px + 1] = u8(avc::clip1(v));
+      int v;
+      if (mode == 2) {  // (wave-uniform)
+        int sv = lane < 8 ? (top ? int(L.pf[1 + lane]) : 0) : lane < 16 ? (left ? int(L.pf[9 + lane]) : 0) : 0;
+        for (int o = 8; o > 0; o >>= 1) sv += __shfl_xor(sv, o);
+        sv = __shfl(sv, 0);
+        v = top && left ? (sv + 8) >> 4 : (top || left) ? (sv + 4) >> 3 : 128;
+      } else {
+        v = avc::eval_tap8(pw, L.pf[pw & 31], L.pf[(pw >> 5) & 31], L.pf[(pw >> 10) & 31]);
+      }
+      L.tile[(by * 8 + py + 1) * kTp + bx * 8 + px + 1] = u8(avc::clip1(v + rs));
       wave_sync();
     }
   } else {
@@ -650,6 +670,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
   __shared__ Sync sync;
   __shared__ IntraWave lds[kIntraWaves];
   __shared__ u32 tap_lut[9 * 16];  // Intra_4x4 tap word per (mode, y, x) of a 4x4 block
+  __shared__ u32 tap8_lut[9 * 64];  // Intra_8x8 tap word per (mode, y, x) of an 8x8 block
   // bottom lines of the intra MBs of rows 0..6 for the row below (pictures up to kIntraLineCols
   // MBs wide; wider ones read the picture)
   __shared__ u8 lines[kIntraWaves - 1][kIntraLineCols * kIntraLine];
@@ -657,6 +678,8 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
     const int mode = t >> 4, y = (t >> 2) & 3, x = t & 3;
     tap_lut[t] = mode == 2 ? avc::kTapDc : avc::pack_taps(avc::intra4x4_taps(mode, x, y));
   }
+  for (int t = int(threadIdx.x); t < 9 * 64; t += int(blockDim.x))
+    tap8_lut[t] = avc::intra8x8_pred_tap(t >> 6, t & 7, (t >> 3) & 7);
   sync_init(sync, kIntraWaves);  // (its barrier also publishes the table)
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   IntraWave& L = lds[wave];
@@ -700,7 +723,7 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
         const u64 t0 = d.prof ? clock64() : 0;
         publish_row(sync, wave, u32(xx));  // every MB left of xx is final
         // (intra_mb waits for the row above itself, after issuing the loads that do not need it)
-        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, t0, acc, sync, wave,
+        intra_mb(d, L, L.rec[xx - base], xx, row, prev == xx - 1, lane, tap_lut, tap8_lut, t0, acc, sync, wave,
                  wave > 0 ? u32(xx + 2 < W ? xx + 2 : W) : 0u, xi_in, row > 0 ? &L.up[1] - base : nullptr,
                  line_in, line_out, xi_out);
         prev = xx;

@@ -340,10 +340,17 @@ __global__ __launch_bounds__(256) void hevc_tu_queue_kernel(const HevcDesc* __re
   __shared__ TuWave lds[4];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   TuWave& L = lds[wave];
-  for (;;) {
+  // ctr null: one block per wave in grid order (blocks dispatch in order, so every producer a
+  // block waits on was dispatched earlier and is resident); else persistent waves on tickets
+  for (int it = 0;; ++it) {
     int t = 0;
-    if (lane == 0) t = base + int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-    t = __shfl(t, 0);
+    if (!ctr) {
+      if (it > 0) break;
+      t = base + int(blockIdx.x) * 4 + wave;
+    } else {
+      if (lane == 0) t = base + int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      t = __shfl(t, 0);
+    }
     if (t >= end) break;
     const HevcTuRange& rg = ranges[pick_range(ranges, nranges, t)];
     const HevcDesc& d = descs[rg.desc];
@@ -457,7 +464,7 @@ void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, 
   if (nranges <= 0 || count <= 0) return;
   // persistent waves: a fraction of the chip (4 per workgroup) — the other lanes' kernels run
   // beside it, and waves that run far ahead of the wavefront only poll
-  const int wgs = std::min((count + 3) / 4, kTuQueueWgs);
+  const int wgs = ctr ? std::min((count + 3) / 4, kTuQueueWgs) : (count + 3) / 4;
   hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, base, base + count,
                      ctr);
 }

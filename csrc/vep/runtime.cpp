@@ -1522,9 +1522,12 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       for (const auto& lv : hlevels[size_t(r)]) gpu::launch_hevc_tu(hd2, hr + hw[0], hw[2], lv[0], lv[1], cs);
     } else {  // one queue launch per window of levels, in level order on the stream
       auto* ctr = reinterpret_cast<u32*>(st.d + off_hctr[size_t(r)]);
+      // (a window of bounded depth runs one wave per block in grid order; the whole round keeps
+      // the persistent ticket queue)
+      const bool persistent = hevc_tu_window_ >= kAllLevels;
       for (size_t k = 0; k < hwindows[size_t(r)].size(); ++k)
         gpu::launch_hevc_tu_queue(hd2, hr + hw[0], hw[2], hwindows[size_t(r)][k][0], hwindows[size_t(r)][k][1],
-                                  ctr + k, cs);
+                                  persistent ? ctr + k : nullptr, cs);
     }
     if (dbk) {
       gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 0, cs);

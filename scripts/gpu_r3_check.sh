@@ -38,10 +38,10 @@ if [ "${KF:-1}" = "1" ]; then
 fi
 if [ "${HEVC_AB:-1}" = "1" ]; then
   echo "[check] H.265 intra TU schedules (replay, decode path only)"
-  for w in 0 8 4 16; do
+  for w in ${W1080:-0 8 4 16}; do
     run h265_1080p_w$w VEP_HEVC_TU_WINDOW=$w --codec h265 --source replay --steps 60 --warmup 8 --latency-samples 0 --clients 0
   done
-  for w in 0 8; do
+  for w in ${W4K:-0 8}; do
     run h265_4k_w$w VEP_HEVC_TU_WINDOW=$w --codec h265 --source replay --width 3840 --height 2160 --cams-per-gpu 8 --steps 40 --warmup 6 --latency-samples 0 --clients 0
   done
 fi

@@ -143,3 +143,12 @@ def test_deblocking_edge_filters(rc):
 
 def clip(v):
     return max(0, min(255, v))
+
+
+def test_intra_8x8_tap_forms(native):
+    """The GPU kernel's branch-free Intra_8x8 form (one tap word per filtered reference and per
+    (mode, x, y) sample) equals the direct formulas (intra8x8_filter_at / intra8x8_pred_g, which
+    test_intra_8x8_all_modes_with_reference_filtering checks against the spec oracle) on random
+    and extreme samples, every mode but DC and every availability combination."""
+    assert native.avc_intra8x8_tap_check(1, 3000) == 0
+    assert native.avc_intra8x8_tap_check(12345, 3000) == 0
