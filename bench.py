@@ -373,6 +373,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         if world > 1:
             dist.barrier()
         elapsed = t1 - t0
+        rg1 = worker.records_gathered  # (sampled here: the farm keeps feeding after the timed loop)
         pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
         s1 = farm.stats()
         gpu_ms = worker.gpu_ms_total - g0
@@ -466,7 +467,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "decode_errors": errors,
             "concurrent_clients": a.clients,
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
-            "rank0_record_bytes_gathered_per_step": (worker.records_gathered - rg0) // max(1, a.steps),
+            "rank0_record_bytes_gathered_per_step": (rg1 - rg0) // max(1, a.steps),
             "keyframe_coalesce_window_us": worker.kf_window_us if a.keyframe_only else None,
             "parse_threads_per_rank": a.threads,
             "rocdecode_available": bool(vep.rocdecode_available()),
@@ -488,12 +489,14 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         sys.exit(3)
 
 
-def payload_path(a, compressed, worker, ip0, sg0, rg0=0):
-    """What reaches the GPU per picture, from the worker's own byte counters."""
-    inplace = (worker.bytes_inplace - ip0) // max(1, a.steps)
-    staged = (worker.bytes_staged - sg0) // max(1, a.steps)
+def payload_path(a, compressed, worker, ip0, sg0, rg0=0, end=None):
+    """What reaches the GPU per picture, from the worker's own byte counters (`end`: the
+    (in-place, staged, gathered) counters sampled when the timed region ended)."""
+    ip1, sg1, rg1 = end or (worker.bytes_inplace, worker.bytes_staged, worker.records_gathered)
+    inplace = (ip1 - ip0) // max(1, a.steps)
+    staged = (sg1 - sg0) // max(1, a.steps)
     if compressed:
-        gathered = (worker.records_gathered - rg0) // max(1, a.steps)
+        gathered = (rg1 - rg0) // max(1, a.steps)
         how = ("the H.264 records sit in pinned pool memory and a gather kernel pulls them over PCIe "
                "(no host copy); the H.265 records are copied into the pinned staging buffer and sent H2D"
                if gathered else "copied into the pinned staging buffer by the host and sent H2D per batch")
@@ -625,6 +628,7 @@ def main():
         step(a.warmup + i)
     drain()
     t1 = time.perf_counter()
+    end_bytes = (worker.bytes_inplace, worker.bytes_staged, worker.records_gathered)
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
@@ -710,7 +714,7 @@ def main():
             "parse_threads_per_rank": a.threads,
             "gpu_stages": worker.stages,
             "gpu_inflight_per_lane": worker.inflight,
-            "payload_path": payload_path(a, compressed, worker, ip0, sg0, rg0),
+            "payload_path": payload_path(a, compressed, worker, ip0, sg0, rg0, end_bytes),
             "rank0_launch_breakdown_ms_per_step": {
                 k: round((v - tm0[k]) / a.steps, 4) for k, v in tm1.items()},
         }

@@ -7,6 +7,7 @@
 #include <pybind11/stl.h>
 
 #include "vep/hostprof.h"
+#include "vep/avc.h"
 #include "vep/avc_cavlc.h"
 #include "vep/avc_recon.h"
 #include "vep/bench_driver.h"
@@ -753,6 +754,38 @@ PYBIND11_MODULE(_vep, m) {
     d["data_offset_ebsp"] = ebsp;
     d["dependent"] = sh.dependent;
     d["segment_address"] = sh.segment_address;
+    return d;
+  });
+  // Record-size statistics of H.264 access units parsed in records mode (the bytes the GPU pulls
+  // over PCIe per picture): macroblocks, coefficient-pool entries, non-zero coefficients,
+  // motion-vector entries.
+  m.def("avc_record_stats", [](const std::vector<std::shared_ptr<AccessUnit>>& aus) {
+    py::gil_scoped_release r;
+    avc::Decoder dec;
+    u64 mbs = 0, coefs = 0, nz = 0, mvs = 0, pics = 0;
+    for (const auto& au : aus) {
+      auto p = dec.parse(*au);
+      if (!p) continue;
+      ++pics;
+      mbs += p->mbs.size();
+      coefs += p->coefs.size();
+      mvs += p->mvs.size();
+      for (const avc::MbRec& m : p->mbs) {
+        if (m.kind == avc::kIPcm || !(m.luma_coded | m.chroma_coded)) continue;
+        const int nb = (m.flags & avc::kMbT8x8) ? 4 * __builtin_popcount(m.luma_coded & 0x0505u) +
+                                                      __builtin_popcount(m.chroma_coded)
+                                                : __builtin_popcount(m.luma_coded) + __builtin_popcount(m.chroma_coded);
+        const i16* b = p->coefs.data() + size_t(m.coef) * 16;
+        for (int k = 0; k < nb * 16; ++k) nz += b[k] != 0;
+      }
+    }
+    py::gil_scoped_acquire g;
+    py::dict d;
+    d["pictures"] = pics;
+    d["mbs"] = mbs;
+    d["coefs"] = coefs;
+    d["nonzero"] = nz;
+    d["mvs"] = mvs;
     return d;
   });
   // Intra_8x8 tap forms (intra8x8_pred_tap / intra8x8_filter_tap, the GPU kernel's branch-free

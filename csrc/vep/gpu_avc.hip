@@ -918,28 +918,34 @@ __device__ inline void filter_line_any(u8* s, int step, int bs, int alpha, int b
 
 // One direction of an MB's edges, whole wave (lanes of a half-wave: luma lines 0-15, chroma
 // lines 16-31, `any` = this half's MB has an edge to filter): 4 edges in order, each line by
-// filter_line_any on the LDS tile (chroma lines on the even edges only).
+// filter_line_any on the LDS tile (chroma lines on the even edges only). The four edges' bS and
+// thresholds are read up front (one round of LDS loads), so each edge step is only its samples'
+// round trip.
 __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
   const bool ch = l >= 16;
   const int c = (l - 16) >> 3, k = (l - 16) & 7;
+  int bs[4], al[4], be[4], tc[4];
+#pragma unroll
   for (int e = 0; e < 4; ++e) {
-    if (any && (!ch || !(e & 1))) {
-      const int bs = bs_of(L.info, dir, e, ch ? k >> 1 : l >> 2);
-      if (bs) {
-        const int pi = (e > 0 ? 2 : dir) + (ch ? 3 + 3 * c : 0);  // component, then left / top / internal
-        const int al = L.info.alpha[pi], be = L.info.beta[pi];
-        const int tc = bs < 4 ? L.info.tc0[pi][bs - 1] : 0;
-        u8* sp;
-        int step;
-        if (!ch) {
-          sp = dir == 0 ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.y[(4 + 4 * e) * 20 + 4 + l];
-          step = dir == 0 ? 1 : 20;
-        } else {
-          sp = dir == 0 ? &L.c[c][(2 + k) * 10 + 2 + 2 * e] : &L.c[c][(2 + 2 * e) * 10 + 2 + k];
-          step = dir == 0 ? 1 : 10;
-        }
-        filter_line_any(sp, step, bs, al, be, tc, ch);
+    bs[e] = any && (!ch || !(e & 1)) ? bs_of(L.info, dir, e, ch ? k >> 1 : l >> 2) : 0;
+    const int pi = (e > 0 ? 2 : dir) + (ch ? 3 + 3 * c : 0);  // component, then left / top / internal
+    al[e] = L.info.alpha[pi];
+    be[e] = L.info.beta[pi];
+    tc[e] = L.info.tc0[pi][bs[e] > 0 && bs[e] < 4 ? bs[e] - 1 : 0];
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (bs[e]) {
+      u8* sp;
+      int step;
+      if (!ch) {
+        sp = dir == 0 ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.y[(4 + 4 * e) * 20 + 4 + l];
+        step = dir == 0 ? 1 : 20;
+      } else {
+        sp = dir == 0 ? &L.c[c][(2 + k) * 10 + 2 + 2 * e] : &L.c[c][(2 + 2 * e) * 10 + 2 + k];
+        step = dir == 0 ? 1 : 10;
       }
+      filter_line_any(sp, step, bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0, ch);
     }
     wave_sync();
   }
