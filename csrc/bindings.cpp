@@ -757,8 +757,8 @@ PYBIND11_MODULE(_vep, m) {
     return d;
   });
   // Record-size statistics of H.264 access units parsed in records mode (the bytes the GPU pulls
-  // over PCIe per picture): macroblocks, coefficient-pool entries, non-zero coefficients,
-  // motion-vector entries.
+  // over PCIe per picture): macroblocks, coefficient-pool entries (sparse groups: mask words +
+  // values), non-zero coefficients, motion-vector entries.
   m.def("avc_record_stats", [](const std::vector<std::shared_ptr<AccessUnit>>& aus) {
     py::gil_scoped_release r;
     avc::Decoder dec;
@@ -770,14 +770,8 @@ PYBIND11_MODULE(_vep, m) {
       mbs += p->mbs.size();
       coefs += p->coefs.size();
       mvs += p->mvs.size();
-      for (const avc::MbRec& m : p->mbs) {
-        if (m.kind == avc::kIPcm || !(m.luma_coded | m.chroma_coded)) continue;
-        const int nb = (m.flags & avc::kMbT8x8) ? 4 * __builtin_popcount(m.luma_coded & 0x0505u) +
-                                                      __builtin_popcount(m.chroma_coded)
-                                                : __builtin_popcount(m.luma_coded) + __builtin_popcount(m.chroma_coded);
-        const i16* b = p->coefs.data() + size_t(m.coef) * 16;
-        for (int k = 0; k < nb * 16; ++k) nz += b[k] != 0;
-      }
+      for (const avc::MbRec& m : p->mbs)
+        if (m.kind != avc::kIPcm) nz += avc::coef_values(p->coefs.data(), m);
     }
     py::gil_scoped_acquire g;
     py::dict d;

@@ -2,6 +2,8 @@
 // DPB / reference lists and the CPU reference reconstruction. See avc.h for the CPU/GPU split.
 #include "avc.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <array>
 
@@ -1253,16 +1255,20 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
 
 // One record against the picture's pools (store_mb checks every record as it is written, so
 // the GPU never sees an out-of-range index from a malformed stream).
-static inline void validate_mb(const Picture& p, const MbRec& m) {
-  const size_t nblocks = p.coefs.size() / 16, nmv = p.mvs.size();
+// (`written`: store_mb has just appended this MB's groups, so they are inside the pool by
+// construction and their mask words need not be walked again.)
+static inline void validate_mb(const Picture& p, const MbRec& m, bool written = false) {
+  const size_t ncoef = p.coefs.size(), nmv = p.mvs.size();
   VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
   VEP_CHECK(m.qp <= 51 && m.qpc <= 51 && m.qpc2 <= 51, "macroblock QP out of range");
   if (m.kind == kIPcm) {
-    VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 32 <= nblocks, "I_PCM samples outside the pool");
+    VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 2 <= ncoef, "I_PCM samples outside the pool");
     return;
   }
-  const size_t nb = size_t(__builtin_popcount(m.luma_coded)) + size_t(__builtin_popcount(m.chroma_coded));
-  VEP_CHECK(size_t(m.coef) + nb <= nblocks, "coefficient blocks outside the pool");
+  // sparse groups: the mask words, then as many values as they announce, inside the pool
+  const size_t nw = size_t(coef_words(m));
+  VEP_CHECK(size_t(m.coef) + nw <= ncoef, "coefficient masks outside the pool");
+  VEP_CHECK(written || size_t(m.coef) + nw + coef_values(p.coefs.data(), m) <= ncoef, "coefficients outside the pool");
   VEP_CHECK(m.chroma_mode <= 3 && m.i16_mode <= 3, "intra prediction mode out of range");
   if (m.flags & kMbT8x8)
     for (int q = 0; q < 4; ++q) {
@@ -1473,9 +1479,65 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
   }
 }
 
+// Bit i set = p[i] != 0 (16 coefficients): one 256-bit compare, movemask, and a bit extract of
+// every second mask bit (the host build targets x86-64-v3: AVX2 + BMI2).
+static inline u16 nonzero_mask16(const i16* p) {
+#if defined(__AVX2__) && defined(__BMI2__)
+  const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p));
+  const u32 zero = u32(_mm256_movemask_epi8(_mm256_cmpeq_epi16(v, _mm256_setzero_si256())));
+  return u16(_pext_u32(~zero, 0x55555555u));
+#else
+  u32 m = 0;
+  for (int i = 0; i < 16; ++i) m |= u32(p[i] != 0) << i;
+  return u16(m);
+#endif
+}
+
+// pshufb control that moves the i16 lanes selected by an 8-bit mask to the front (branch-free
+// compaction of a group's non-zero values: the inner "for each set bit" loop mispredicted its
+// exit on most groups).
+struct Compact8 {
+  alignas(16) u8 c[256][16];
+  constexpr Compact8() : c() {
+    for (int m = 0; m < 256; ++m) {
+      int k = 0;
+      for (int i = 0; i < 8; ++i)
+        if ((m >> i) & 1) {
+          c[m][2 * k] = u8(2 * i);
+          c[m][2 * k + 1] = u8(2 * i + 1);
+          ++k;
+        }
+      for (int j = 2 * k; j < 16; ++j) c[m][j] = 0x80;  // (zeros; overwritten by the next group)
+    }
+  }
+};
+static constexpr Compact8 kCompact8{};
+
+// The non-zero values of 16 coefficients (mask = nonzero_mask16(p)) to out; writes up to 8
+// entries past the last value (the caller leaves that slack).
+static inline i16* compact16(const i16* p, u32 mask, i16* out) {
+#if defined(__SSSE3__)
+  const __m128i lo = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+  const __m128i hi = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 8));
+  const u32 m0 = mask & 0xFFu, m1 = mask >> 8;
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out),
+                   _mm_shuffle_epi8(lo, _mm_load_si128(reinterpret_cast<const __m128i*>(kCompact8.c[m0]))));
+  out += __builtin_popcount(m0);
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out),
+                   _mm_shuffle_epi8(hi, _mm_load_si128(reinterpret_cast<const __m128i*>(kCompact8.c[m1]))));
+  return out + __builtin_popcount(m1);
+#else
+  for (int i = 0; i < 16; ++i) {  // (branch-free: store every value, advance on non-zero)
+    *out = p[i];
+    out += (mask >> i) & 1;
+  }
+  return out;
+#endif
+}
+
 void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm,
               const WpEntry* wp) {
-  m.coef = u32(pic.coefs.size() / 16);
+  m.coef = u32(pic.coefs.size());
   m.luma_coded = 0;
   m.chroma_coded = 0;
   if (m.kind == kIPcm) {
@@ -1486,21 +1548,32 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   } else if (res && (res->luma | res->chroma)) {
     m.luma_coded = res->luma;
     m.chroma_coded = res->chroma;
-    // appended without a zero-filling resize (the pool is reserved per picture)
+    if (res->t8) m.flags |= kMbT8x8;
+    // sparse groups (avc_recon.h): the mask words, then the non-zero values
+    const i16* grp[24];
+    int ng = 0;
     if (res->t8) {
-      m.flags |= kMbT8x8;
       for (int q = 0; q < 4; ++q)
-        if ((res->luma >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) pic.coefs.insert(pic.coefs.end(), res->b8[q], res->b8[q] + 64);
+        if ((res->luma >> ((q & 1) * 2 + (q >> 1) * 8)) & 1)
+          for (int w = 0; w < 4; ++w) grp[ng++] = res->b8[q] + 16 * w;
     } else {
-      for (u32 w = res->luma; w; w &= w - 1) {
-        const i16* b = res->blk[__builtin_ctz(w)];
-        pic.coefs.insert(pic.coefs.end(), b, b + 16);
-      }
+      for (u32 w = res->luma; w; w &= w - 1) grp[ng++] = res->blk[__builtin_ctz(w)];
     }
-    for (u32 w = res->chroma; w; w &= w - 1) {
-      const i16* b = res->blk[16 + __builtin_ctz(w)];
-      pic.coefs.insert(pic.coefs.end(), b, b + 16);
+    for (u32 w = res->chroma; w; w &= w - 1) grp[ng++] = res->blk[16 + __builtin_ctz(w)];
+    u16 mask[24];
+    int nv = 0;
+    for (int g = 0; g < ng; ++g) {
+      mask[g] = nonzero_mask16(grp[g]);
+      nv += __builtin_popcount(mask[g]);
     }
+    // appended without zero-filling (the pool is reserved per picture), with 8 entries of slack
+    // for the last group's 16-byte stores, trimmed after
+    const size_t o = pic.coefs.size();
+    i16* out = pic.coefs.extend(size_t(ng + nv) + 8);
+    std::memcpy(out, mask, size_t(ng) * sizeof(u16));
+    i16* v = out + ng;
+    for (int g = 0; g < ng; ++g) v = compact16(grp[g], mask[g], v);
+    pic.coefs.resize(o + size_t(ng + nv));
   }
   m.mv = 0;
   m.wp = 0;
@@ -1547,7 +1620,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   }
   m.res = is_intra(m.kind) && m.kind != kIPcm && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
   if (!(m.dbk & 1)) pic.deblock = true;
-  validate_mb(pic, m);
+  validate_mb(pic, m, true);
   pic.mbs[size_t(mb)] = m;
   if (pic.colb) pic.colb->store(mb, s);
 }
@@ -1564,33 +1637,33 @@ bool intra_avail(const Picture& pic, const MbRec& m, int nx, int ny) {
   return !(pic.constrained_intra && !is_intra(n.kind));
 }
 
-const i16* luma_res(const Picture& pic, const MbRec& m, int r) {
+// `dense`: the MB's coefficients expanded (expand_coefs, avc_recon.h)
+const i16* luma_res(const i16* dense, const MbRec& m, int r) {
   if (!((m.luma_coded >> r) & 1)) return nullptr;
-  return pic.block(m.coef + u32(__builtin_popcount(m.luma_coded & ((1u << r) - 1))));
+  return dense + 16 * r;
 }
 
-const i16* chroma_res(const Picture& pic, const MbRec& m, int c, int b) {
+const i16* chroma_res(const i16* dense, const MbRec& m, int c, int b) {
   const int k = c * 4 + b;
   if (!((m.chroma_coded >> k) & 1)) return nullptr;
-  return pic.block(m.coef + u32(__builtin_popcount(m.luma_coded)) +
-                   u32(__builtin_popcount(m.chroma_coded & ((1u << k) - 1))));
+  return dense + 256 + 16 * k;
 }
 
 // Luma residual samples of the whole MB (raster 16x16), from 4x4 or 8x8 transform blocks.
-void luma_residual(const Picture& pic, const MbRec& m, int* out) {
+void luma_residual(const i16* dense, const MbRec& m, int* out) {
   std::memset(out, 0, 256 * sizeof(int));
   if (m.flags & kMbT8x8) {
     for (int q = 0; q < 4; ++q) {
       if (!((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1)) continue;
       int r[64];
-      idct8x8(pic.block(luma8_block_index(m, q)), r);
+      idct8x8(dense + 64 * q, r);
       for (int i = 0; i < 8; ++i)
         for (int j = 0; j < 8; ++j) out[((q >> 1) * 8 + i) * 16 + (q & 1) * 8 + j] = r[i * 8 + j];
     }
     return;
   }
   for (int blk = 0; blk < 16; ++blk) {
-    const i16* d = luma_res(pic, m, blk);
+    const i16* d = luma_res(dense, m, blk);
     if (!d) continue;
     int r[16];
     idct4x4(d, r);
@@ -1604,13 +1677,18 @@ struct Recon {
   std::vector<HostSurface>& slots;
   HostSurface& T;
   int pitch, wpx, hpx;
+  i16 dense[kDenseCoefs];  // the current MB's coefficients (load())
+
+  void load(const MbRec& m) {
+    if (m.kind != kIPcm) expand_coefs(pic.coefs.data(), m, dense);
+  }
 
   u8& Y(int x, int y) { return T.y[size_t(y) * pitch + x]; }
   u8& C(int x, int y, int c) { return T.uv[size_t(y) * pitch + 2 * x + c]; }
 
   void chroma_store(const MbRec& m, int mx, int my, int c, const int* pred /*8x8*/) {
     for (int b = 0; b < 4; ++b) {
-      const i16* d = chroma_res(pic, m, c, b);
+      const i16* d = chroma_res(dense, m, c, b);
       int res[16] = {};
       if (d) idct4x4(d, res);
       const int bx = (b & 1) * 4, by = (b >> 1) * 4;
@@ -1634,14 +1712,14 @@ struct Recon {
     const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
     int py[256], pc[2][64], res[256];
     predict_inter(slots, m, mv0, mv1, wp, mx, my, py, pc);
-    luma_residual(pic, m, res);
+    luma_residual(dense, m, res);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = u8(clip1(py[y * 16 + x] + res[y * 16 + x]));
     for (int c = 0; c < 2; ++c) chroma_store(m, mx, my, c, pc[c]);
   }
 
   void pcm(const MbRec& m, int mx, int my) {
-    const u8* s = reinterpret_cast<const u8*>(pic.block(m.coef));
+    const u8* s = reinterpret_cast<const u8*>(pic.coefs.data() + m.coef);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = s[y * 16 + x];
     for (int c = 0; c < 2; ++c)
@@ -1666,7 +1744,7 @@ struct Recon {
     intra16_neighbours(pic, mb, T, n);
     const PredConst k = intra16x16_const(n, m.i16_mode);
     int res[256];
-    luma_residual(pic, m, res);
+    luma_residual(dense, m, res);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x)
         Y(mx * 16 + x, my * 16 + y) = u8(clip1(intra16x16_pred(n, k, m.i16_mode, x, y) + res[y * 16 + x]));
@@ -1678,7 +1756,7 @@ struct Recon {
       Intra4Nb n;
       intra4x4_neighbours(pic, mb, idx, T, n);
       const int mode = i4_mode(m, r);
-      const i16* d = luma_res(pic, m, r);
+      const i16* d = luma_res(dense, m, r);
       int res[16] = {};
       if (d) idct4x4(d, res);
       for (int i = 0; i < 4; ++i)
@@ -1694,7 +1772,7 @@ struct Recon {
       intra8x8_neighbours(pic, mb, q, T, f, top, left);
       const int mode = i4_mode(m, q);
       int res[64] = {};
-      if ((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) idct8x8(pic.block(luma8_block_index(m, q)), res);
+      if ((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) idct8x8(dense + 64 * q, res);
       const int x0 = mx * 16 + (q & 1) * 8, y0 = my * 16 + (q >> 1) * 8;
       for (int i = 0; i < 8; ++i)
         for (int j = 0; j < 8; ++j) Y(x0 + j, y0 + i) = u8(clip1(intra8x8_pred(f, top, left, mode, j, i) + res[i * 8 + j]));
@@ -1781,8 +1859,9 @@ void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, 
 void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots) {
   HostSurface& T = slots[size_t(pic.target)];
   const int wpx = pic.wmbs * 16, hpx = pic.hmbs * 16;
-  Recon r{pic, slots, T, wpx, wpx, hpx};
+  Recon r{pic, slots, T, wpx, wpx, hpx, {}};
   const MbRec& m = pic.mbs[size_t(mb)];
+  r.load(m);
   const int mx = mb % pic.wmbs, my = mb / pic.wmbs;
   switch (m.kind) {
     case kSkip:

@@ -62,7 +62,7 @@ struct Picture {
   // Records in pinned pool memory once a GPU worker exists (hostmem::PinnedAllocator): the
   // worker's gather kernel pulls them over PCIe, no host copy into its staging buffer.
   hostmem::pinned_vector<MbRec> mbs;     // raster order
-  hostmem::pinned_vector<i16> coefs;     // 16-entry blocks (dequantised, row-major); I_PCM raw samples
+  hostmem::pinned_vector<i16> coefs;     // sparse dequantised coefficient groups per MB (avc_recon.h); I_PCM raw samples
   hostmem::pinned_vector<i16> mvs;       // 32 entries (16 x (mvx, mvy), quarter samples) per list per MB
   hostmem::pinned_vector<WpEntry> wps;   // weighted-prediction entries (4 per weighted MB)
   int target = 0;             // DPB slot this picture is reconstructed into
@@ -84,7 +84,6 @@ struct Picture {
   ColBuild* colb = nullptr;
 
   int nmbs() const { return wmbs * hmbs; }
-  const i16* block(u32 b) const { return coefs.data() + size_t(b) * 16; }
 };
 using PicturePtr = std::shared_ptr<const Picture>;
 

@@ -28,6 +28,7 @@
 namespace vep::gpu {
 
 using avc::MbRec;
+using avc::kDenseCoefs;
 
 namespace {
 
@@ -42,13 +43,6 @@ __device__ inline const MbRec& rec(const AvcDesc& d, int mb) {
   return static_cast<const MbRec*>(d.mbs)[mb];
 }
 
-__device__ inline const i16* luma_block(const AvcDesc& d, const MbRec& m, int r) {
-  return d.coefs + size_t(m.coef + u32(__popc(m.luma_coded & ((1u << r) - 1)))) * 16;
-}
-__device__ inline const i16* chroma_block(const AvcDesc& d, const MbRec& m, int k) {
-  return d.coefs + size_t(m.coef + u32(__popc(m.luma_coded)) +
-                          u32(__popc(m.chroma_coded & ((1u << k) - 1)))) * 16;
-}
 
 // wave-local barrier (one wave64 per "group" here: LDS ordering + compiler fence)
 __device__ inline void wave_sync() {
@@ -80,6 +74,34 @@ __device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
 
 // --------------------------------------------------------------------------------- inter
 
+// The MB's sparse coefficient groups (avc_recon.h) expanded into the wave's dense LDS buffer D
+// (kDenseCoefs entries, layout of avc::expand_coefs), whole wave: lanes 0..23 each take one mask
+// word, a wave prefix sum of their popcounts places their values, and each scatters its own.
+__device__ inline void expand_coefs_wave(const AvcDesc& d, const MbRec& m, int lane, i16* D) {
+  if (lane < kDenseCoefs / 8) reinterpret_cast<uint4*>(D)[lane] = make_uint4(0, 0, 0, 0);
+  const int nw = avc::coef_words(m);  // <= 24
+  const VEP_DEV i16* pool = d.coefs + m.coef;
+  u32 mask = 0;
+  int base = 0;
+  if (lane < nw) {
+    mask = u32(u16(pool[lane]));
+    base = avc::coef_word_base(m, lane);
+  }
+  const int cnt = __popc(mask);
+  int incl = cnt;
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    const int t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  wave_sync();  // the zeros land before the scatter
+  if (lane < nw) {
+    const VEP_DEV i16* v = pool + nw + (incl - cnt);
+    for (u32 b = mask; b; b &= b - 1) D[base + __ffs(int(b)) - 1] = *v++;
+  }
+  wave_sync();
+}
+
 // Luma residual of an 8x8-transform MB, whole wave: the four 8x8 inverse transforms as 32 row
 // butterflies then 32 column butterflies (lanes 0-31, one 8-point transform each) through the
 // wave's LDS buffer `T` (kT8Ints ints); afterwards T holds the MB's 16x16 residual (raster).
@@ -88,12 +110,12 @@ __device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
 // fall on 32 distinct banks, and the column reads stay conflict-free.
 constexpr int kT8Pitch = 9, kT8Block = 8 * kT8Pitch, kT8Ints = 4 * kT8Block;
 static_assert(kT8Ints >= 256, "the transpose buffer also holds the 16x16 raster result");
-__device__ inline void luma8_residual(const AvcDesc& d, const MbRec& m, int lane, int* T) {
+__device__ inline void luma8_residual(const i16* D, const MbRec& m, int lane, int* T) {
   if (lane < 32) {
     const int q = lane >> 3, i = lane & 7;
     int v[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if ((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) {
-      const uint4 w = *reinterpret_cast<const uint4*>(d.coefs + size_t(avc::luma8_block_index(m, q)) * 16 + i * 8);
+      const uint4 w = *reinterpret_cast<const uint4*>(D + q * 64 + i * 8);
       const u32 ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
@@ -129,6 +151,7 @@ __device__ inline void luma8_residual(const AvcDesc& d, const MbRec& m, int lane
 __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restrict__ descs, int n,
                                                          int total) {
   __shared__ int lres[4][kT8Ints];
+  __shared__ alignas(16) i16 lcoef[4][kDenseCoefs];  // the wave's MB coefficients, dense
   const int wv = int(threadIdx.x) >> 6;
   const int g = __builtin_amdgcn_readfirstlane(int(blockIdx.x) * 4 + wv);
   if (g >= total) return;  // (wave-uniform; the kernel has no workgroup barrier)
@@ -153,20 +176,22 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     // in parallel and the intra wavefront only adds them (same layout as IntraWave::res).
     if (m.res == avc::kNoRes) return;
     i16* r = d.res + size_t(m.res) * kAvcResSamples;
-    if (t8) luma8_residual(d, m, lane, T);
+    i16* D = lcoef[wv];
+    expand_coefs_wave(d, m, lane, D);
+    if (t8) luma8_residual(D, m, lane, T);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
       int v;
       if (t8) v = T[y * 16 + x];
-      else v = (m.luma_coded >> blk) & 1 ? avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3) : 0;
+      else v = (m.luma_coded >> blk) & 1 ? avc::idct4x4_at(D + 16 * blk, y & 3, x & 3) : 0;
       r[y * 16 + x] = i16(v);
     }
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
       const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
       const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
-      r[256 + t] = i16((m.chroma_coded >> kb) & 1 ? avc::idct4x4_at(chroma_block(d, m, kb), cy & 3, cx & 3) : 0);
+      r[256 + t] = i16((m.chroma_coded >> kb) & 1 ? avc::idct4x4_at(D + 256 + 16 * kb, cy & 3, cx & 3) : 0);
     }
     return;
   }
@@ -176,7 +201,7 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
   u8* ty = d.y + d.slot_y * u64(d.target);
   u8* tuv = d.uv + d.slot_uv * u64(d.target);
   if (m.kind == avc::kIPcm) {
-    const u8* s = reinterpret_cast<const u8*>(d.coefs + size_t(m.coef) * 16);
+    const VEP_DEV u8* s = reinterpret_cast<const VEP_DEV u8*>(d.coefs + m.coef);
 #pragma unroll
     for (int k = 0; k < 4; ++k) ty[size_t(my * 16 + y0 + 4 * k) * pitch + mx * 16 + x] = s[(y0 + 4 * k) * 16 + x];
 #pragma unroll
@@ -208,13 +233,15 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     }
     v[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 0);
   }
-  if (t8) luma8_residual(d, m, lane, T);
+  i16* D = lcoef[wv];
+  if (m.luma_coded | m.chroma_coded) expand_coefs_wave(d, m, lane, D);  // (wave-uniform)
+  if (t8) luma8_residual(D, m, lane, T);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
     int o = v[k];
     if (t8) o += T[y * 16 + x];
-    else if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(luma_block(d, m, blk), y & 3, x & 3);
+    else if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(D + 16 * blk, y & 3, x & 3);
     ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = u8(avc::clip1(o));
   }
   int u[2];
@@ -241,7 +268,7 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
     const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
     int o = u[k];
-    if ((m.chroma_coded >> kb) & 1) o += avc::idct4x4_at(chroma_block(d, m, kb), cy & 3, cx & 3);
+    if ((m.chroma_coded >> kb) & 1) o += avc::idct4x4_at(D + 256 + 16 * kb, cy & 3, cx & 3);
     tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = u8(avc::clip1(o));
   }
 }

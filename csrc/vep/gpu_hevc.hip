@@ -24,7 +24,6 @@
 // is tested bit-exact against the reference decoder.
 #define VEP_KERNEL_SOURCE 1  // descriptors' pointers are global-address-space here (gpu.h)
 #include <algorithm>
-#include <cstdlib>
 
 #include "gpu.h"
 #include "hevc_kern.h"
@@ -69,114 +68,11 @@ __device__ inline int pick_range(const HevcTuRange* r, int n, int b) {
 }
 
 // ------------------------------------------------------------------------------ MC
-// One prediction block per 256-lane workgroup, separable through LDS: per plane and list the
-// reference window ((h + taps - 1) x (w + taps - 1) samples, edge-clamped) is staged once, a
-// horizontal pass writes the fractional-x intermediates, and each output sample takes the
-// vertical taps from them — 8 + 8 LDS reads per luma sample instead of 64 clamped global loads.
-// The integer arithmetic is hk_luma_mc / hk_chroma_mc's, regrouped (bit-exact).
-constexpr int kMcWin = 71 * 72;  // (64 + 7) rows x (64 + 7 (+1)) samples
-struct McLds {
-  u8 win[kMcWin];
-  i16 hp[71 * 64];   // horizontal pass: (h + taps - 1) rows x w (16-bit for 8-bit video, §8.5.3.3.3)
-  int p0[64 * 64];   // first list's prediction of a bi-predicted block
-};
-
-// Prediction samples of one plane (luma: taps 8, step 1; chroma component c: taps 4, step 2,
-// offset c) of one list, block w x h at integer position (x0, y0) of a W x H plane, fraction
-// (fx, fy); `out(s, v)` receives sample s = j * w + i (14-bit intermediate).
-template <int kTaps, class Out>
-__device__ inline void mc_plane(McLds& L, const u8* ref, int stride, int step, int W, int H, int x0, int y0,
-                                int fx, int fy, int w, int h, const signed char (*filt)[kTaps], Out out) {
-  constexpr int half = kTaps / 2 - 1;
-  const int ww = w + kTaps - 1, wh = h + kTaps - 1, tid = int(threadIdx.x);
-  __syncthreads();  // the previous plane / list is done with the buffers
-  for (int t = tid; t < ww * wh; t += 256) {
-    const int r = t / ww, c = t - r * ww;
-    int xx = x0 - half + c, yy = y0 - half + r;
-    xx = xx < 0 ? 0 : (xx >= W ? W - 1 : xx);
-    yy = yy < 0 ? 0 : (yy >= H ? H - 1 : yy);
-    L.win[t] = ref[yy * stride + xx * step];
-  }
-  __syncthreads();
-  if (fx) {
-    const int r0 = fy ? 0 : half, r1 = fy ? wh : half + h;
-    for (int t = tid; t < (r1 - r0) * w; t += 256) {
-      const int r = r0 + t / w, c = t % w;
-      const u8* q = &L.win[r * ww + c];
-      int v = 0;
-#pragma unroll
-      for (int k = 0; k < kTaps; ++k) v += filt[fx][k] * int(q[k]);
-      L.hp[r * w + c] = i16(v);
-    }
-    __syncthreads();
-  }
-  for (int t = tid; t < w * h; t += 256) {
-    const int j = t / w, i = t - j * w;
-    int v;
-    if (!fx && !fy) {
-      v = int(L.win[(j + half) * ww + i + half]) << 6;
-    } else if (!fy) {
-      v = L.hp[(j + half) * w + i];
-    } else if (!fx) {
-      v = 0;
-#pragma unroll
-      for (int k = 0; k < kTaps; ++k) v += filt[fy][k] * int(L.win[(j + k) * ww + i + half]);
-    } else {
-      v = 0;
-#pragma unroll
-      for (int k = 0; k < kTaps; ++k) v += filt[fy][k] * int(L.hp[(j + k) * w + i]);
-      v >>= 6;
-    }
-    out(t, v);
-  }
-}
-
+// Each output sample's taps are read from the picture (edge-clamped) by its own thread. A
+// separable form staged through LDS (reference window, horizontal pass, vertical taps) was
+// measured 2.5-3x slower on the camera streams (profiles/r3/mcab/): most blocks are small and
+// their loads hit L1/L2, so the staging syncs and idle lanes cost more than the taps saved.
 __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict__ descs, int n) {
-  __shared__ McLds L;
-  const int b = int(blockIdx.x);
-  const HevcDesc& d = descs[pick_pu(descs, n, b)];
-  const GpuPu u = static_cast<const GpuPu*>(d.pus)[b - d.pu_begin];
-  const int stride = d.stride, W = d.width, H = d.height;
-  u8* y = d.y + size_t(d.target) * d.slot_y;
-  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
-  const bool bi = u.pred == 3;
-  // explicit weighted prediction: the PU's weights / offsets (uniform per workgroup)
-  const hevc::GpuWp* wp = u.wp ? static_cast<const hevc::GpuWp*>(d.wp) + (u.wp - 1) : nullptr;
-  const int ul = (u.pred & 1) ? 0 : 1;
-  // planes: luma, Cb, Cr; per plane the lists in order (list 0's samples wait in LDS when bi)
-  for (int c = 0; c < 3; ++c) {
-    const int sub = c ? 1 : 0, w = u.w >> sub, h = u.h >> sub;
-    u8* dst = c == 0 ? y + u.y * stride + u.x : uv + (u.y >> 1) * stride + u.x + (c - 1);
-    const int dstep = c == 0 ? 1 : 2;
-    bool first = true;
-    for (int l = 0; l < 2; ++l) {
-      if (!((u.pred >> l) & 1)) continue;
-      const VEP_DEV u8* ref = c == 0 ? d.y + size_t(u.slot[l]) * d.slot_y
-                                     : d.uv + size_t(u.slot[l]) * d.slot_uv + (c - 1);
-      const bool last = !bi || !first;
-      auto out = [&](int t, int v) {
-        if (!last) {
-          L.p0[t] = v;
-          return;
-        }
-        const int v0 = bi ? L.p0[t] : v, v1 = bi ? v : 0;
-        const int j = t / w, i = t - j * w;
-        dst[j * stride + i * dstep] = wp ? hevc::hk_weight_explicit(*wp, c, v0, v1, bi, ul) : hevc::hk_weight(v0, v1, bi);
-      };
-      if (c == 0)
-        mc_plane<8>(L, ref, stride, 1, W, H, u.x + (u.mv[l][0] >> 2), u.y + (u.mv[l][1] >> 2), u.mv[l][0] & 3,
-                    u.mv[l][1] & 3, w, h, hevc::kLumaFilter, out);
-      else
-        mc_plane<4>(L, ref, stride, 2, W >> 1, H >> 1, (u.x >> 1) + (u.mv[l][0] >> 3), (u.y >> 1) + (u.mv[l][1] >> 3),
-                    u.mv[l][0] & 7, u.mv[l][1] & 7, w, h, hevc::kChromaFilter, out);
-      first = false;
-    }
-  }
-}
-
-// The per-sample form (each output sample's taps read from the picture, edge-clamped): kept as
-// the A/B baseline of the staged kernel (VEP_HEVC_MC_DIRECT=1).
-__global__ __launch_bounds__(256) void hevc_mc_direct_kernel(const HevcDesc* __restrict__ descs, int n) {
   const int b = int(blockIdx.x);
   const HevcDesc& d = descs[pick_pu(descs, n, b)];
   const GpuPu u = static_cast<const GpuPu*>(d.pus)[b - d.pu_begin];
@@ -558,12 +454,7 @@ __global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restric
 
 void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s) {
   if (n <= 0 || total_pus <= 0) return;
-  static const bool direct = [] {
-    const char* e = std::getenv("VEP_HEVC_MC_DIRECT");
-    return e && e[0] == '1';
-  }();
-  if (direct) hipLaunchKernelGGL(hevc_mc_direct_kernel, dim3(total_pus), dim3(256), 0, s, d_descs, n);
-  else hipLaunchKernelGGL(hevc_mc_kernel, dim3(total_pus), dim3(256), 0, s, d_descs, n);
+  hipLaunchKernelGGL(hevc_mc_kernel, dim3(total_pus), dim3(256), 0, s, d_descs, n);
 }
 
 void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,

@@ -105,6 +105,13 @@ class PodVec {
     n_ += k;
   }
   void push_back(const T& v) { append(&v, 1); }
+  // k more entries, left uninitialised (the caller writes every one); returns the first
+  T* extend(size_t k) {
+    if (n_ + k > cap_) grow(std::max(n_ + k, 2 * cap_));
+    T* q = p_ + n_;
+    n_ += k;
+    return q;
+  }
   // (std::vector's range insert, at the end only)
   T* insert(T* pos, const T* first, const T* last) {
     const size_t at = size_t(pos - p_);
