@@ -1,6 +1,6 @@
 """Single-thread host parse throughput of the bench's H.264 High streams (replay, parse only),
 optionally with another build of the extension (A/B of parser changes on one machine):
-  python tools/parse_ab.py [--so path/to/_vep...so] [--reps 5] [--codec h265]
+  python tools/parse_ab.py [--so path/to/_vep...so] [--reps 5] [--codec h265] [--threads N --cams 32]
 Prints the best and median ms per tick over `reps` measurements of 60 ticks."""
 import argparse
 import importlib.machinery
@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--cams", type=int, default=4)
     ap.add_argument("--codec", default="h264")
+    ap.add_argument("--threads", type=int, default=1, help="parse pool threads (multi-thread throughput)")
     a, rest = ap.parse_known_args()
     if a.so:  # load the other build under the package's module name before anything imports it
         name = "video_edge_ai_proxy_amd._vep"
@@ -33,11 +34,12 @@ def main():
     b = bench.parse_args()
     w = vep.Worker(device=-1, letterbox_size=0, max_cameras=a.cams)
     cfg = bench.make_cfg(vep, b, 0, True)
-    rb = vep.ReplayBench(w, a.cams, cfg, cached_frames=b.gop * b.cache_gops, threads=1, prefix="p")
+    rb = vep.ReplayBench(w, a.cams, cfg, cached_frames=b.gop * b.cache_gops, threads=a.threads, prefix="p")
     rb.parse_only_ms(30)
     ms = [rb.parse_only_ms(60) for _ in range(a.reps)]
     print(f"{a.so or 'tree'}: best {min(ms):.3f} median {statistics.median(ms):.3f} ms/tick "
-          f"-> {a.cams / min(ms) * 1000:.1f} fps/thread (best)", flush=True)
+          f"-> {a.cams / min(ms) * 1000 / a.threads:.1f} fps/thread (best), {a.cams / min(ms) * 1000:.0f} fps "
+          f"with {a.threads} threads", flush=True)
 
 
 if __name__ == "__main__":
