@@ -202,9 +202,11 @@ def test_hostprof_samples_native_threads(native, tmp_path):
 def test_bench_config5_rtmp_annotation_cpu():
     """BASELINE config 5 shape on the CPU backend: H.265 cameras through the live ingest with RTMP
     pass-through to a loopback RTMP server and Annotate RPCs uploaded by the production queue +
-    batch consumer to a loopback cloud endpoint; the JSON reports all three."""
+    batch consumer to a loopback cloud endpoint; the JSON reports all three. (40 steps: the RTMP
+    counts cover the timed region only, and a few steps of these tiny pictures can be decoded
+    before the pass-through senders' first message lands.)"""
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--codec", "h265", "--rtmp", "--annotate",
-           "--annotate-rate", "20", "--steps", "6", "--warmup", "2", "--width", "128", "--height", "96",
+           "--annotate-rate", "20", "--steps", "40", "--warmup", "2", "--width", "128", "--height", "96",
            "--cams-per-gpu", "2", "--gop", "8", "--letterbox", "32", "--clients", "2", "--client-procs", "1",
            "--latency-seconds", "1", "--latency-samples", "5", "--threads", "2"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=400, cwd=ROOT)
