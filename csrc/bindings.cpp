@@ -17,6 +17,7 @@
 #include "vep/h264.h"
 #include "vep/hevc_ctu.h"
 #include "vep/hevc_dec.h"
+#include "vep/hevc_kern.h"
 #include "bind_ext.h"
 #include "vep/runtime.h"
 #include "vep/synth.h"
@@ -780,6 +781,33 @@ PYBIND11_MODULE(_vep, m) {
     d["coefs"] = coefs;
     d["nonzero"] = nz;
     d["mvs"] = mvs;
+    return d;
+  });
+  // Same for H.265 access units (records mode): pictures, transform blocks, coefficient-pool
+  // entries (sparse: mask words + stored values per coded block), non-zero entries, prediction
+  // blocks.
+  m.def("hevc_record_stats", [](const std::vector<std::shared_ptr<AccessUnit>>& aus) {
+    py::gil_scoped_release r;
+    hevc::Decoder dec;
+    dec.set_gpu_mode(true);
+    u64 pics = 0, tus = 0, coefs = 0, nz = 0, pus = 0;
+    for (const auto& au : aus) {
+      dec.decode(*au);
+      for (const auto& p : dec.take_gpu_pictures()) {
+        ++pics;
+        tus += p->tus.size();
+        pus += p->pus.size();
+        coefs += p->coefs.size();
+        for (i16 c : p->coefs) nz += c != 0;
+      }
+    }
+    py::gil_scoped_acquire g;
+    py::dict d;
+    d["pictures"] = pics;
+    d["tus"] = tus;
+    d["coefs"] = coefs;
+    d["nonzero"] = nz;
+    d["pus"] = pus;
     return d;
   });
   // Intra_8x8 tap forms (intra8x8_pred_tap / intra8x8_filter_tap, the GPU kernel's branch-free

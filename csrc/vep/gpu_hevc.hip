@@ -118,8 +118,9 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
 // ------------------------------------------------------------------------------ TUs
 // One wave per transform block: LDS of the wave (the block's column pass, references and their
 // substitution scratch). Blocks are at most 32x32 = 16 samples per lane.
-struct TuWave {
+struct alignas(16) TuWave {
   int g[32 * 32];
+  i16 dq[32 * 32];  // the block's coefficients, dense (expanded from the sparse records)
   int top[129];
   int left[128];
   int sbuf[129], sref[129];
@@ -290,7 +291,25 @@ __device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d,
   const bool tskip = t.flags & hevc::kTuSkip;
   const bool bypass = t.flags & hevc::kTuBypass;  // lossless CU: the coefficients are the residual
   const bool dst = t.flags & hevc::kTuDst;
-  const i16* dq = d.coefs + t.data;
+  if (coef) {  // (uniform per wave) sparse -> dense: lane w takes mask word w, a wave prefix sum
+               // of the popcounts places its values (hevc::hk_sparse_store's layout)
+    const int nn = n * n, nw = nn >> 4;
+    for (int k = lane * 8; k < nn; k += 64 * 8) *reinterpret_cast<uint4*>(&L.dq[k]) = make_uint4(0, 0, 0, 0);
+    const VEP_DEV i16* src = d.coefs + t.data;
+    const u32 mask = lane < nw ? u32(u16(src[lane])) : 0u;
+    const int cnt = __popc(mask);
+    int incl = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int u = __shfl_up(incl, o);
+      if (lane >= o) incl += u;
+    }
+    wave_sync();  // the zeros land before the scatter
+    const VEP_DEV i16* v = src + nw + (incl - cnt);
+    for (u32 b = mask; b; b &= b - 1) L.dq[16 * lane + __ffs(int(b)) - 1] = *v++;
+    wave_sync();
+  }
+  const i16* dq = L.dq;
   if (intra)  // (uniform per wave)
     prepare_refs_wave(d, t, plane, stride, step, lane, L);
   const int mx = t.ext_x, my = t.ext_y;

@@ -1030,17 +1030,17 @@ class CtuLayer {
       }
       if (tskip) t.flags |= kTuSkip;
       if (cu_.bypass) t.flags |= kTuBypass;
-      if (nz) {
+      if (nz) {  // sparse: mask words + the non-zero levels' dequantised values (hk_sparse_store)
         t.flags |= kTuCoef;
         t.data = u32(g->coefs.size());
         int ex = 0, ey = 0;
-        const size_t off = g->coefs.size();
-        g->coefs.resize(off + size_t(nn));
-        i16* dq = g->coefs.data() + off;
         const u8* m = scale_matrix(c, log2);
         const bool byp = cu_.bypass;
+        int np = 0;
         auto put = [&](int k) {
-          dq[k] = byp ? i16(std::clamp(lv[k], -32768, 32767)) : i16(dequant_level(lv[k], qp, log2, m ? m[k] : 16));
+          nzpos_[np] = u16(k);
+          nzval_[np++] =
+              byp ? i16(std::clamp(lv[k], -32768, 32767)) : i16(dequant_level(lv[k], qp, log2, m ? m[k] : 16));
           ex = std::max(ex, k & (n - 1));
           ey = std::max(ey, k >> log2);
         };
@@ -1050,6 +1050,9 @@ class CtuLayer {
         } else {
           for (int j = 0; j < nnz; ++j) put(nzbuf_[j]);
         }
+        const size_t off = g->coefs.size();
+        g->coefs.resize(off + size_t(hk_sparse_words(log2) + np));
+        hk_sparse_store(log2, nzpos_, nzval_, np, g->coefs.data() + off);
         t.ext_x = u8(ex);
         t.ext_y = u8(ey);
       }
@@ -1506,6 +1509,8 @@ class CtuLayer {
   int dry_qp_delta_ = 0;
   bool dry_tskip_ = false;
   u16 nzbuf_[1024];  // read mode: raster positions of a block's non-zero levels
+  u16 nzpos_[1024];  // the block's stored coefficients (raster positions, dequantised values)
+  i16 nzval_[1024];
   bool cbf_nonzero_ = false;
   int block_luma_mode_ = 1;
   u64 gpu_avail_ = 0;

@@ -71,7 +71,8 @@ namespace {
 // One transform block: residual into `res` (n x n raster).
 void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
   const int log2 = t.log2, n = 1 << log2;
-  const i16* d = p.coefs.data() + t.data;
+  i16 d[32 * 32];
+  hk_sparse_expand(p.coefs.data() + t.data, log2, d);
   if (t.flags & kTuBypass) {
     for (int k = 0; k < n * n; ++k) res[k] = d[k];
     return;

@@ -50,8 +50,8 @@ struct GpuTu {    // one transform block of one component (or one PCM coding blo
   u8 c;           // 0 Y, 1 Cb, 2 Cr (PCM: 0, covers all three)
   u8 flags;       // kTu*
   u8 mode;        // intra prediction mode (component's)
-  u32 data;       // kTuCoef: offset of the n x n dequantised coefficients (i16; kTuBypass: the
-                  // residual itself); kTuPcm: byte offset
+  u32 data;       // kTuCoef: i16 offset of the block's sparse coefficients (hk_sparse_*; kTuBypass:
+                  // the residual itself); kTuPcm: byte offset
   u16 level;      // intra dependency level (0: inter residual / PCM)
   u8 ext_x, ext_y;  // kTuCoef: last column / row holding a non-zero coefficient
   u64 avail;      // intra: reference availability, see hk_prepare_refs
@@ -73,6 +73,38 @@ struct GpuSao {  // per CTB (SaoParams)
 };
 
 // A picture's reconstruction work in decoding order, produced by hevc::Decoder in GPU mode.
+// Sparse transform-block coefficients (GpuTu::data): n*n/16 mask words (u16; word w covers
+// raster positions 16w .. 16w + 15, bit set = a stored coefficient), then the stored values in
+// raster order. 98% of the dense blocks' entries are zero on the camera streams, which made the
+// dense pool 4 MB per 1080p picture (16 MB at 4K) for the parse to zero-fill and the host to copy.
+VEP_HD int hk_sparse_words(int log2) { return (1 << (2 * log2)) >> 4; }
+// Positions in `pos` (any order, distinct) with their values -> out (words then values); returns
+// the entries written. (`pos` / `val` are the non-zero levels of the block.)
+inline int hk_sparse_store(int log2, const u16* pos, const i16* val, int n, i16* out) {
+  const int nw = hk_sparse_words(log2);
+  u16 m[64] = {};
+  for (int i = 0; i < n; ++i) m[pos[i] >> 4] |= u16(1u << (pos[i] & 15));
+  int before[64];
+  for (int w = 0, acc = 0; w < nw; ++w) {
+    before[w] = acc;
+    acc += __builtin_popcount(u32(m[w]));
+    out[w] = i16(m[w]);
+  }
+  for (int i = 0; i < n; ++i) {
+    const int k = pos[i];
+    out[nw + before[k >> 4] + __builtin_popcount(u32(m[k >> 4]) & ((1u << (k & 15)) - 1u))] = val[i];
+  }
+  return nw + n;
+}
+// The block's coefficients into dense[n * n] (CPU mirror; the GPU expands with the wave).
+inline void hk_sparse_expand(const i16* src, int log2, i16* dense) {
+  const int nn = 1 << (2 * log2), nw = nn >> 4;
+  for (int k = 0; k < nn; ++k) dense[k] = 0;
+  const i16* v = src + nw;
+  for (int w = 0; w < nw; ++w)
+    for (u32 b = u16(src[w]); b; b &= b - 1) dense[16 * w + __builtin_ctz(b)] = *v++;
+}
+
 struct GpuPicture {
   int width = 0, height = 0, log2ctb = 4, wctb = 0, hctb = 0;
   int target = 0;                     // DPB slot being reconstructed
