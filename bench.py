@@ -359,6 +359,9 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         rg0 = worker.records_gathered
         g0 = worker.gpu_ms_total
         handle = None
+        hostprof = os.environ.get("VEP_HOSTPROF")  # path: SIGPROF samples of every thread, timed region
+        if hostprof:
+            vep.hostprof_start(1000)
         t0 = time.perf_counter()
         for i in range(a.steps):
             farm.wait_pictures(p0 + cams * (i + 1))
@@ -374,6 +377,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             dist.barrier()
         elapsed = t1 - t0
         rg1 = worker.records_gathered  # (sampled here: the farm keeps feeding after the timed loop)
+        if hostprof:
+            vep.hostprof_stop(hostprof)
         pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
         s1 = farm.stats()
         gpu_ms = worker.gpu_ms_total - g0

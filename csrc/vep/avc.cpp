@@ -2,6 +2,8 @@
 // DPB / reference lists and the CPU reference reconstruction. See avc.h for the CPU/GPU split.
 #include "avc.h"
 
+#include <immintrin.h>
+
 #include <algorithm>
 #include <array>
 
@@ -1477,6 +1479,62 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
   }
 }
 
+// Bit i set = p[i] != 0 (16 coefficients): one 256-bit compare, movemask, and a bit extract of
+// every second mask bit (the host build targets x86-64-v3: AVX2 + BMI2).
+static inline u16 nonzero_mask16(const i16* p) {
+#if defined(__AVX2__) && defined(__BMI2__)
+  const __m256i v = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(p));
+  const u32 zero = u32(_mm256_movemask_epi8(_mm256_cmpeq_epi16(v, _mm256_setzero_si256())));
+  return u16(_pext_u32(~zero, 0x55555555u));
+#else
+  u32 m = 0;
+  for (int i = 0; i < 16; ++i) m |= u32(p[i] != 0) << i;
+  return u16(m);
+#endif
+}
+
+// pshufb control that moves the i16 lanes selected by an 8-bit mask to the front (branch-free
+// compaction of a group's non-zero values: the inner "for each set bit" loop mispredicted its
+// exit on most groups).
+struct Compact8 {
+  alignas(16) u8 c[256][16];
+  constexpr Compact8() : c() {
+    for (int m = 0; m < 256; ++m) {
+      int k = 0;
+      for (int i = 0; i < 8; ++i)
+        if ((m >> i) & 1) {
+          c[m][2 * k] = u8(2 * i);
+          c[m][2 * k + 1] = u8(2 * i + 1);
+          ++k;
+        }
+      for (int j = 2 * k; j < 16; ++j) c[m][j] = 0x80;  // (zeros; overwritten by the next group)
+    }
+  }
+};
+static constexpr Compact8 kCompact8{};
+
+// The non-zero values of 16 coefficients (mask = nonzero_mask16(p)) to out; writes up to 8
+// entries past the last value (the caller leaves that slack).
+static inline i16* compact16(const i16* p, u32 mask, i16* out) {
+#if defined(__SSSE3__)
+  const __m128i lo = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p));
+  const __m128i hi = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 8));
+  const u32 m0 = mask & 0xFFu, m1 = mask >> 8;
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out),
+                   _mm_shuffle_epi8(lo, _mm_load_si128(reinterpret_cast<const __m128i*>(kCompact8.c[m0]))));
+  out += __builtin_popcount(m0);
+  _mm_storeu_si128(reinterpret_cast<__m128i*>(out),
+                   _mm_shuffle_epi8(hi, _mm_load_si128(reinterpret_cast<const __m128i*>(kCompact8.c[m1]))));
+  return out + __builtin_popcount(m1);
+#else
+  for (int i = 0; i < 16; ++i) {  // (branch-free: store every value, advance on non-zero)
+    *out = p[i];
+    out += (mask >> i) & 1;
+  }
+  return out;
+#endif
+}
+
 void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm,
               const WpEntry* wp) {
   m.coef = u32(pic.coefs.size());
@@ -1491,35 +1549,31 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
     m.luma_coded = res->luma;
     m.chroma_coded = res->chroma;
     if (res->t8) m.flags |= kMbT8x8;
-    if (res->sparse) {  // the groups as the macroblock layer decoded them (avc_recon.h)
-      VEP_CHECK(res->nw == coef_words(m), "residual groups do not match the coded blocks");
-      i16* out = pic.coefs.extend(size_t(res->nw + res->nv));
-      std::memcpy(out, res->w, size_t(res->nw) * sizeof(u16));
-      std::memcpy(out + res->nw, res->v, size_t(res->nv) * sizeof(i16));
-    } else {  // dense blocks (the Baseline fast path, the encoders): the same groups from them
-      MbResidual g;
-      u8 gp[16];
-      int gv[16];
-      auto group = [&](const i16* d, const u8* zz, bool keep) {
-        for (int k = 0; k < 16; ++k) {
-          gp[k] = u8(k);
-          gv[k] = d[zz[k]];
-        }
-        g.add_group(gp, gv, 16, keep);
-      };
-      if (res->t8) {
-        for (int q = 0; q < 4; ++q)
-          if ((res->luma >> ((q & 1) * 2 + (q >> 1) * 8)) & 1)
-            for (int w = 0; w < 4; ++w) group(res->b8[q], kZigzag8x8 + 16 * w, true);
-      } else {
-        for (int idx = 0; idx < 16; ++idx)
-          if ((res->luma >> blk_to_raster(idx)) & 1) group(res->blk[blk_to_raster(idx)], kZigzag4x4, true);
-      }
-      for (u32 w = res->chroma; w; w &= w - 1) group(res->blk[16 + __builtin_ctz(w)], kZigzag4x4, true);
-      i16* out = pic.coefs.extend(size_t(g.nw + g.nv));
-      std::memcpy(out, g.w, size_t(g.nw) * sizeof(u16));
-      std::memcpy(out + g.nw, g.v, size_t(g.nv) * sizeof(i16));
+    // sparse groups (avc_recon.h): the mask words, then the non-zero values
+    const i16* grp[24];
+    int ng = 0;
+    if (res->t8) {
+      for (int q = 0; q < 4; ++q)
+        if ((res->luma >> ((q & 1) * 2 + (q >> 1) * 8)) & 1)
+          for (int w = 0; w < 4; ++w) grp[ng++] = res->b8[q] + 16 * w;
+    } else {
+      for (u32 w = res->luma; w; w &= w - 1) grp[ng++] = res->blk[__builtin_ctz(w)];
     }
+    for (u32 w = res->chroma; w; w &= w - 1) grp[ng++] = res->blk[16 + __builtin_ctz(w)];
+    u16 mask[24];
+    int nv = 0;
+    for (int g = 0; g < ng; ++g) {
+      mask[g] = nonzero_mask16(grp[g]);
+      nv += __builtin_popcount(mask[g]);
+    }
+    // appended without zero-filling (the pool is reserved per picture), with 8 entries of slack
+    // for the last group's 16-byte stores, trimmed after
+    const size_t o = pic.coefs.size();
+    i16* out = pic.coefs.extend(size_t(ng + nv) + 8);
+    std::memcpy(out, mask, size_t(ng) * sizeof(u16));
+    i16* v = out + ng;
+    for (int g = 0; g < ng; ++g) v = compact16(grp[g], mask[g], v);
+    pic.coefs.resize(o + size_t(ng + nv));
   }
   m.mv = 0;
   m.wp = 0;

@@ -435,32 +435,11 @@ struct MbLevels {
 };
 // Dequantised residual blocks of one MB (16 luma raster, 4 Cb, 4 Cr) and their coded masks.
 struct MbResidual {
-  // sparse (the macroblock layer's parse): the pool's groups as decoded (avc_recon.h), appended
-  // by add_group; dense (the other producers): blk / b8, converted by store_mb
-  bool sparse = false;
-  int nw = 0, nv = 0;
-  u16 w[24];
-  i16 v[kDenseCoefs];
   i16 blk[24][16];  // 16 luma 4x4 (raster), 4 Cb, 4 Cr
   i16 b8[4][64];    // 8x8-transform luma blocks (raster 8x8 in each; t8 MBs)
   u16 luma = 0;     // coded luma 4x4 blocks (t8: all four blocks of each coded 8x8)
   u8 chroma = 0;
   bool t8 = false;
-
-  // One group's (scan position, value) pairs, any order, zero values skipped (positions < 16,
-  // values already saturated to i16). An all-zero group is dropped unless `keep` (the four words
-  // of a coded 8x8 block). Returns whether any value is non-zero.
-  bool add_group(const u8* pos, const int* val, int n, bool keep = false) {
-    u32 mask = 0;
-    for (int i = 0; i < n; ++i) mask |= u32(val[i] != 0) << pos[i];
-    if (!mask && !keep) return false;
-    w[nw++] = u16(mask);
-    i16* out = v + nv;
-    for (int i = 0; i < n; ++i)
-      if (val[i]) out[__builtin_popcount(mask & ((1u << pos[i]) - 1u))] = i16(val[i]);
-    nv += __builtin_popcount(mask);
-    return mask != 0;
-  }
 };
 void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& out);
 // Append MB `mb` to `pic`: coefficient blocks (or I_PCM samples), motion vectors and the

@@ -795,18 +795,11 @@ class MbLayer {
     }
   }
 
-  // Residual of one MB, dequantised as each level is read, emitted straight into the sparse
-  // groups of the records (avc_recon.h; (scan position, value) pairs per 16-coefficient group,
-  // MbResidual::add_group): no dense block is cleared, filled or scanned.
   void residual(int mb, MbState& s, MbResidual& res, int cbp_luma, int cbp_chroma, int qp, bool intra) {
     const int ly = intra ? 0 : 3;
     const int q6 = qp / 6, qm = qp % 6;
     int lv[64];
     u8 nzp[64];
-    u8 gp[16];   // one 4x4 group: scan positions
-    int gv[16];  // and saturated values
-    res.sparse = true;
-    res.nw = res.nv = 0;
     if (s.kind == kI16x16) {
       const int inc = kCabac ? cbf_dc_inc(mb, 0, true) : 0;
       const int nc = kCabac ? 0 : nb_.nc_luma(mb, 0);
@@ -823,39 +816,39 @@ class MbLayer {
       }
       for (int idx = 0; idx < 16; ++idx) {
         const int r = blk_to_raster(idx);
-        int n = 0;
-        if (dcy[r]) {
-          gp[n] = 0;
-          gv[n++] = sat16(dcy[r]);
-        }
+        i16* d = res.blk[r];
+        bool nz = dcy[r] != 0;
+        std::memset(d, 0, 16 * sizeof(i16));
+        d[0] = sat16(dcy[r]);
         if (cbp_luma) {
           const int binc = kCabac ? cbf_luma_inc(mb, r, true) : 0;
           const int bnc = kCabac ? 0 : nb_.nc_luma(mb, r);
           const int tc = read_block(kCatLumaAc, binc, bnc, 15, lv, nzp, kWrite ? want->ac[r] : nullptr);
           for (int j = 0; j < tc; ++j) {
             const int k = nzp[j];
-            gp[n] = u8(k + 1);
-            gv[n++] = sat16(scale4(lv[k], dq_.ls4[ly][qm][kZigzag4x4[k + 1]], qp));
+            const int pos = kZigzag4x4[k + 1];
+            const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
+            d[pos] = sat16(v);
+            nz |= v != 0;
           }
           s.tc[r] = u8(tc);
           if (tc) s.cbf |= u16(1u << r);
         }
-        if (res.add_group(gp, gv, n)) res.luma |= u16(1u << r);
+        if (nz) res.luma |= u16(1u << r);
       }
     } else if (s.t8x8) {
       res.t8 = true;
       const int l8 = intra ? 0 : 1;
       for (int b8 = 0; b8 < 4; ++b8) {
         if (!((cbp_luma >> b8) & 1)) continue;
-        u8 p8[4][16];  // the block's four groups (scan positions 16w .. 16w + 15)
-        int v8[4][16], n8[4] = {0, 0, 0, 0};
+        i16* d = res.b8[b8];
+        std::memset(d, 0, 64 * sizeof(i16));
         bool nz = false;
         int total = 0;
         auto put = [&](int k, int level) {  // k: 8x8 scan position
-          const int v = sat16(scale8(level, dq_.ls8[l8][qm][kZigzag8x8[k]], qp));
-          const int w = k >> 4;
-          p8[w][n8[w]] = u8(k & 15);
-          v8[w][n8[w]++] = v;
+          const int pos = kZigzag8x8[k];
+          const int v = scale8(level, dq_.ls8[l8][qm][pos], qp);
+          d[pos] = sat16(v);
           nz |= v != 0;
         };
         if constexpr (kCabac) {
@@ -878,10 +871,7 @@ class MbLayer {
           s.cbf |= b8_blocks(b8);
           nz8_ |= b8_blocks(b8);
         }
-        if (nz) {
-          res.luma |= b8_blocks(b8);
-          for (int w = 0; w < 4; ++w) res.add_group(p8[w], v8[w], n8[w], true);
-        }
+        if (nz) res.luma |= b8_blocks(b8);
       }
     } else {
       for (int idx = 0; idx < 16; ++idx) {
@@ -893,12 +883,17 @@ class MbLayer {
         s.tc[r] = u8(tc);
         if (!tc) continue;
         s.cbf |= u16(1u << r);
+        i16* d = res.blk[r];
+        std::memset(d, 0, 16 * sizeof(i16));
+        bool nz = false;
         for (int j = 0; j < tc; ++j) {
           const int k = nzp[j];
-          gp[j] = u8(k);
-          gv[j] = sat16(scale4(lv[k], dq_.ls4[ly][qm][kZigzag4x4[k]], qp));
+          const int pos = kZigzag4x4[k];
+          const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
+          d[pos] = sat16(v);
+          nz |= v != 0;
         }
-        if (res.add_group(gp, gv, tc)) res.luma |= u16(1u << r);
+        if (nz) res.luma |= u16(1u << r);
       }
     }
     if (cbp_chroma) {
@@ -922,11 +917,10 @@ class MbLayer {
       for (int c = 0; c < 2; ++c) {
         const int lc = ly + 1 + c;
         for (int b = 0; b < 4; ++b) {
-          int n = 0;
-          if (dcv[c][b]) {
-            gp[n] = 0;
-            gv[n++] = sat16(dcv[c][b]);
-          }
+          i16* d = res.blk[16 + c * 4 + b];
+          bool nz = dcv[c][b] != 0;
+          std::memset(d, 0, 16 * sizeof(i16));
+          d[0] = sat16(dcv[c][b]);
           if (cbp_chroma & 2) {
             const int binc = kCabac ? cbf_cac_inc(mb, c, b, intra) : 0;
             const int bnc = kCabac ? 0 : nb_.nc_chroma(mb, c, b);
@@ -935,11 +929,13 @@ class MbLayer {
             if (tc) s.cbf_cac[c] |= u8(1u << b);
             for (int j = 0; j < tc; ++j) {
               const int k = nzp[j];
-              gp[n] = u8(k + 1);
-              gv[n++] = sat16(scale4(lv[k], dq_.ls4[lc][qpc[c] % 6][kZigzag4x4[k + 1]], qpc[c]));
+              const int pos = kZigzag4x4[k + 1];
+              const int v = scale4(lv[k], dq_.ls4[lc][qpc[c] % 6][pos], qpc[c]);
+              d[pos] = sat16(v);
+              nz |= v != 0;
             }
           }
-          if (res.add_group(gp, gv, n)) res.chroma |= u8(1u << (c * 4 + b));
+          if (nz) res.chroma |= u8(1u << (c * 4 + b));
         }
       }
     }

@@ -119,6 +119,61 @@ VEP_HD int wp_sample(int p0, int p1, bool has0, bool has1, const WpEntry* w, int
   return v < 0 ? 0 : (v > 255 ? 255 : v);
 }
 
+// ---- sparse coefficient records
+// An MB's dequantised coefficients in the picture's pool, from i16 offset MbRec::coef:
+//   * one mask word (u16) per coded 16-coefficient group: bit i set = coefficient i of the group
+//     (raster order) is non-zero. Groups, in order: the coded luma 4x4 blocks (raster order of
+//     luma_coded's bits) or, for 8x8-transform MBs, the coded 8x8 blocks in raster order with
+//     four words each (raster positions 16w .. 16w + 15 of the 8x8); then the coded chroma 4x4
+//     blocks (order of chroma_coded's bits, Cb then Cr). Either way the word count is
+//     popcount(luma_coded) + popcount(chroma_coded).
+//   * then the non-zero values, group by group, ascending bit order.
+// 93% of the dense blocks' entries are zero on the camera streams (89% on IDR pictures): this is
+// 5-7x fewer bytes for the parse to write and the GPU to pull over PCIe.
+// Dense layout (kDenseCoefs entries): luma 4x4 block r at 16 r, or 8x8 block q at 64 q (raster
+// 8x8); chroma block k (0-3 Cb, 4-7 Cr) at 256 + 16 k.
+// I_PCM: the 384 sample bytes from i16 offset MbRec::coef.
+constexpr int kDenseCoefs = 384;
+VEP_HD int coef_words(const MbRec& m) {
+  return __builtin_popcount(u32(m.luma_coded)) + __builtin_popcount(u32(m.chroma_coded));
+}
+// Dense offset of mask word j (j < coef_words(m)).
+VEP_HD int coef_word_base(const MbRec& m, int j) {
+  const u32 lc = m.luma_coded;
+  const int nl = __builtin_popcount(lc);
+  if (j >= nl) {  // chroma: the (j - nl)-th coded block
+    u32 cc = m.chroma_coded;
+    for (int k = j - nl; k > 0; --k) cc &= cc - 1;
+    return 256 + 16 * __builtin_ctz(cc);
+  }
+  if (m.flags & kMbT8x8) {  // the (j / 4)-th coded 8x8 block, word j % 4
+    const u32 qm = (lc & 1u) | ((lc >> 1) & 2u) | ((lc >> 6) & 4u) | ((lc >> 7) & 8u);
+    u32 q = qm;
+    for (int k = j >> 2; k > 0; --k) q &= q - 1;
+    return 64 * __builtin_ctz(q) + 16 * (j & 3);
+  }
+  u32 w = lc;
+  for (int k = j; k > 0; --k) w &= w - 1;
+  return 16 * __builtin_ctz(w);
+}
+// The MB's coefficients into dense[kDenseCoefs] (CPU reconstruction; the GPU expands in parallel).
+inline void expand_coefs(const i16* pool, const MbRec& m, i16* dense) {
+  for (int i = 0; i < kDenseCoefs; ++i) dense[i] = 0;
+  const int nw = coef_words(m);
+  const i16* v = pool + m.coef + nw;
+  for (int j = 0; j < nw; ++j) {
+    const u32 mask = u16(pool[m.coef + j]);
+    i16* d = dense + coef_word_base(m, j);
+    for (u32 b = mask; b; b &= b - 1) d[__builtin_ctz(b)] = *v++;
+  }
+}
+// Number of values the MB's mask words announce (validation).
+inline u32 coef_values(const i16* pool, const MbRec& m) {
+  u32 n = 0;
+  for (int j = 0, nw = coef_words(m); j < nw; ++j) n += u32(__builtin_popcount(u32(u16(pool[m.coef + j]))));
+  return n;
+}
+
 VEP_HD int i4_mode(const MbRec& m, int blk) { return (m.i4[blk >> 1] >> ((blk & 1) * 4)) & 15; }
 
 // Coding order of the 4x4 luma blocks (luma4x4BlkIdx) <-> raster position within the MB.
@@ -230,79 +285,6 @@ VEP_CONST static const u8 kZigzag8x8[64] = {
     0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18, 11, 4,  5,  12, 19, 26, 33, 40, 48,
     41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
     30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
-
-// ---- sparse coefficient records
-// An MB's dequantised coefficients in the picture's pool, from i16 offset MbRec::coef, in the
-// order the parser produces them (so it appends them as it decodes, with no dense block):
-//   * one mask word (u16) per coded 16-coefficient group: bit k set = scan position k of the
-//     group is non-zero (4x4: the zig-zag scan; an 8x8 block is four groups, word w covering
-//     8x8 scan positions 16w .. 16w + 15). Groups in decoding order: the coded luma 4x4 blocks
-//     in luma4x4BlkIdx order, or for 8x8-transform MBs the coded 8x8 blocks in order (four
-//     words each); then the coded chroma 4x4 blocks (Cb 0-3, then Cr 0-3). Either way the word
-//     count is popcount(luma_coded) + popcount(chroma_coded).
-//   * then the non-zero values, group by group, in ascending scan position.
-// 93% of the dense blocks' entries are zero on the camera streams (89% on IDR pictures): 5-7x
-// fewer bytes for the parse to write and the GPU to pull over PCIe.
-// Dense layout (kDenseCoefs entries, raster within each block): luma 4x4 block r (raster
-// index) at 16 r, or 8x8 block q at 64 q; chroma block k (0-3 Cb, 4-7 Cr) at 256 + 16 k.
-// I_PCM: the 384 sample bytes from i16 offset MbRec::coef.
-constexpr int kDenseCoefs = 384;
-VEP_HD int coef_words(const MbRec& m) {
-  return __builtin_popcount(u32(m.luma_coded)) + __builtin_popcount(u32(m.chroma_coded));
-}
-// Mask word j (j < coef_words(m)): dense offset of its block, and for 8x8 blocks the first scan
-// position it covers (-1: a 4x4 block). Sample k of the word lands at
-// base + (s8 < 0 ? kZigzag4x4[k] : kZigzag8x8[s8 + k]).
-VEP_HD void coef_word_at(const MbRec& m, int j, int& base, int& s8) {
-  const u32 lc = m.luma_coded;
-  const int nl = __builtin_popcount(lc);
-  s8 = -1;
-  if (j >= nl) {  // chroma: the (j - nl)-th coded block
-    u32 cc = m.chroma_coded;
-    for (int k = j - nl; k > 0; --k) cc &= cc - 1;
-    base = 256 + 16 * __builtin_ctz(cc);
-    return;
-  }
-  if (m.flags & kMbT8x8) {  // the (j / 4)-th coded 8x8 block, word j % 4
-    u32 q = (lc & 1u) | ((lc >> 1) & 2u) | ((lc >> 6) & 4u) | ((lc >> 7) & 8u);
-    for (int k = j >> 2; k > 0; --k) q &= q - 1;
-    base = 64 * __builtin_ctz(q);
-    s8 = 16 * (j & 3);
-    return;
-  }
-  int left = j;  // the j-th coded 4x4 block in luma4x4BlkIdx order
-  for (int idx = 0; idx < 16; ++idx) {
-    const int r = blk_to_raster(idx);
-    if ((lc >> r) & 1) {
-      if (left == 0) {
-        base = 16 * r;
-        return;
-      }
-      --left;
-    }
-  }
-  base = 0;  // (unreachable for j < coef_words)
-}
-// The MB's coefficients into dense[kDenseCoefs] (CPU reconstruction; the GPU expands in parallel).
-inline void expand_coefs(const i16* pool, const MbRec& m, i16* dense) {
-  for (int i = 0; i < kDenseCoefs; ++i) dense[i] = 0;
-  const int nw = coef_words(m);
-  const i16* v = pool + m.coef + nw;
-  for (int j = 0; j < nw; ++j) {
-    int base, s8;
-    coef_word_at(m, j, base, s8);
-    for (u32 b = u16(pool[m.coef + j]); b; b &= b - 1) {
-      const int k = __builtin_ctz(b);
-      dense[base + (s8 < 0 ? kZigzag4x4[k] : kZigzag8x8[s8 + k])] = *v++;
-    }
-  }
-}
-// Number of values the MB's mask words announce (validation).
-inline u32 coef_values(const i16* pool, const MbRec& m) {
-  u32 n = 0;
-  for (int j = 0, nw = coef_words(m); j < nw; ++j) n += u32(__builtin_popcount(u32(u16(pool[m.coef + j]))));
-  return n;
-}
 
 // normAdjust8x8 (§8.5.13.1): v[m][class] with the six position classes below.
 VEP_CONST static const u8 kNormAdjust8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26},

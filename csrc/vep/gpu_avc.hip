@@ -76,17 +76,16 @@ __device__ inline void gst4(void* p, u32 v) { *(VEP_GLOBAL u32*)(p) = v; }
 
 // The MB's sparse coefficient groups (avc_recon.h) expanded into the wave's dense LDS buffer D
 // (kDenseCoefs entries, layout of avc::expand_coefs), whole wave: lanes 0..23 each take one mask
-// word, a wave prefix sum of their popcounts places their values, and each scatters its own to
-// their raster positions (zig-zag scan -> raster).
+// word, a wave prefix sum of their popcounts places their values, and each scatters its own.
 __device__ inline void expand_coefs_wave(const AvcDesc& d, const MbRec& m, int lane, i16* D) {
   if (lane < kDenseCoefs / 8) reinterpret_cast<uint4*>(D)[lane] = make_uint4(0, 0, 0, 0);
   const int nw = avc::coef_words(m);  // <= 24
   const VEP_DEV i16* pool = d.coefs + m.coef;
   u32 mask = 0;
-  int base = 0, s8 = -1;
+  int base = 0;
   if (lane < nw) {
     mask = u32(u16(pool[lane]));
-    avc::coef_word_at(m, lane, base, s8);
+    base = avc::coef_word_base(m, lane);
   }
   const int cnt = __popc(mask);
   int incl = cnt;
@@ -98,10 +97,7 @@ __device__ inline void expand_coefs_wave(const AvcDesc& d, const MbRec& m, int l
   wave_sync();  // the zeros land before the scatter
   if (lane < nw) {
     const VEP_DEV i16* v = pool + nw + (incl - cnt);
-    for (u32 b = mask; b; b &= b - 1) {
-      const int k = __ffs(int(b)) - 1;
-      D[base + (s8 < 0 ? avc::kZigzag4x4[k] : avc::kZigzag8x8[s8 + k])] = *v++;
-    }
+    for (u32 b = mask; b; b &= b - 1) D[base + __ffs(int(b)) - 1] = *v++;
   }
   wave_sync();
 }

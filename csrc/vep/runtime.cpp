@@ -3,7 +3,9 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
 #include <cmath>
+#include <thread>
 
 #include "color.h"
 #include "trace.h"
@@ -443,6 +445,7 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     kf_window_us_ = std::clamp(kw, 0, 100000);
     // H.265 intra transform blocks: one launch per level (VEP_HEVC_TU_QUEUE=0), one queue launch
     // per round (=1), or one queue launch per window of k levels (VEP_HEVC_TU_WINDOW=k)
+    polite_wait_ = !(std::getenv("VEP_SPIN_WAIT") && std::getenv("VEP_SPIN_WAIT")[0] == '1');
     hevc_tu_window_ = kDefaultTuWindow;
     if (const char* tq = std::getenv("VEP_HEVC_TU_QUEUE")) hevc_tu_window_ = tq[0] == '1' ? kAllLevels : 0;
     if (const char* tw = std::getenv("VEP_HEVC_TU_WINDOW")) hevc_tu_window_ = std::clamp(std::atoi(tw), 0, kAllLevels);
@@ -1702,13 +1705,29 @@ void Worker::add_time(double Timers::*f, double us) {
   timers.*f += us;
 }
 
+// Wait for a batch's completion event without spinning a CPU core. hipEventSynchronize busy-polls
+// the HSA completion signal (rdtsc loop in libhsa-runtime64) even for hipEventBlockingSync events
+// for a while before it sleeps: in the host profile of the headline that spin was 17% of the
+// process's CPU samples, taken from the parse threads. A lane only needs to notice its stage is
+// free within a fraction of a batch (~5 ms), so it polls the event and sleeps between polls.
+static void wait_event_polite(hipEvent_t e) {
+  for (int i = 0;; ++i) {
+    const hipError_t r = hipEventQuery(e);
+    if (r == hipSuccess) return;
+    if (r != hipErrorNotReady) VEP_HIP(r);
+    if (i < 2) std::this_thread::yield();
+    else std::this_thread::sleep_for(std::chrono::microseconds(40));
+  }
+}
+
 void Worker::complete(Lane& ln, Stage& st) {
   if (!st.active) return;
   st.active = false;
   const i64 t0 = mono_us();
   {
     trace::Range tr("vep.wait_gpu");
-    VEP_HIP(hipEventSynchronize(st.e1));
+    if (polite_wait_) wait_event_polite(st.e1);
+    else VEP_HIP(hipEventSynchronize(st.e1));
   }
   add_time(&Timers::wait, double(mono_us() - t0));
   float ms = 0;

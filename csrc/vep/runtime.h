@@ -436,6 +436,9 @@ class Worker {
   // H.265 intra transform blocks: 0 = one launch per dependency level; k > 0 = one queue launch
   // per window of k consecutive levels (kAllLevels: the whole round in one launch)
   int hevc_tu_window_ = 0;
+  // lanes wait for a stage's batch by polling its event with sleeps (VEP_SPIN_WAIT=1:
+  // hipEventSynchronize, which spins a core in the HSA runtime)
+  bool polite_wait_ = true;
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;

@@ -17,3 +17,7 @@ for i in 1 2; do
   timeout -k 10 240 python tools/parse_ab.py --reps 3 --threads 15 --cams 32 2>&1 | tail -1 | tee -a "$O/parse_ab15.log" || exit 1
 done
 TAG=${TAG:-dsparse} bash scripts/gpu_e2e_ab.sh
+# host CPU profile of the headline's timed region (every thread: farm, ingest, parse, lanes)
+VEP_HOSTPROF="$R/$O/hostprof_headline.txt" timeout -k 10 300 python -u bench.py --steps 200 --warmup 10 --latency-samples 0 --clients 0 \
+  > "$O/hostprof_headline.json" 2> "$O/hostprof_headline.err" || { echo "hostprof bench failed"; tail -20 "$O/hostprof_headline.err"; exit 1; }
+echo "hostprof samples: $(wc -l < "$O/hostprof_headline.txt") lines"
