@@ -411,9 +411,10 @@ constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
 constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
-constexpr int kDefaultTuWindow = 8;        // H.265 intra TUs: 0 = per-level launches, k = queue windows
+constexpr int kDefaultTuWindow = 0;        // H.265 intra TUs: 0 = per-level launches, k = queue windows
                                            // of k levels (8: 8x fewer launches, same end-to-end rate,
-                                           // profiles/r3/hevc_window/)
+                                           // but edge-word waits time out under rocprofv3 --pmc
+                                           // serialisation: profiles/r3/hevc_window/)
 constexpr int kAllLevels = 1 << 20;        // (a window holding every level of a round)
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
