@@ -760,6 +760,78 @@ PYBIND11_MODULE(_vep, m) {
   // Record-size statistics of H.264 access units parsed in records mode (the bytes the GPU pulls
   // over PCIe per picture): macroblocks, coefficient-pool entries (sparse groups: mask words +
   // values), non-zero coefficients, motion-vector entries.
+  // Sparse coefficient records against the dense blocks they encode: random blocks (any density,
+  // int16 extremes, 4x4 and 8x8 transforms, any coded pattern) through store_mb -> expand_coefs
+  // (H.264, avc_recon.h) and through hk_sparse_store -> hk_sparse_expand for every H.265 TB size
+  // (hevc_kern.h). Returns (H.264 mismatches, H.265 mismatches).
+  m.def("sparse_coef_fuzz", [](u64 seed, int trials) {
+    u64 x = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() {
+      x ^= x << 13;
+      x ^= x >> 7;
+      x ^= x << 17;
+      return x;
+    };
+    auto val = [&](int density) -> i16 {  // non-zero with probability density / 16
+      if (int(rnd() & 15) >= density) return 0;
+      const int r = int(rnd() % 8);
+      if (r == 0) return i16(-32768);
+      if (r == 1) return i16(32767);
+      const int v = int(rnd() % 64) - 32;
+      return i16(v ? v : 1);
+    };
+    int bad_avc = 0, bad_hevc = 0;
+    for (int t = 0; t < trials; ++t) {
+      const int dens = int(rnd() % 17);
+      avc::MbResidual res;
+      res.t8 = rnd() & 1;
+      i16 want[avc::kDenseCoefs] = {};
+      if (res.t8) {
+        for (int q = 0; q < 4; ++q) {
+          const bool coded = rnd() & 1;
+          for (int i = 0; i < 64; ++i) want[64 * q + i] = res.b8[q][i] = coded ? val(dens) : 0;
+          if (coded) res.luma |= u16(0x33u << ((q & 1) * 2 + (q >> 1) * 8));
+        }
+      } else {
+        for (int b = 0; b < 16; ++b) {
+          const bool coded = rnd() & 1;
+          for (int i = 0; i < 16; ++i) want[16 * b + i] = res.blk[b][i] = coded ? val(dens) : 0;
+          if (coded) res.luma |= u16(1u << b);
+        }
+      }
+      for (int k = 0; k < 8; ++k) {
+        const bool coded = rnd() & 1;
+        for (int i = 0; i < 16; ++i) want[256 + 16 * k + i] = res.blk[16 + k][i] = coded ? val(dens) : 0;
+        if (coded) res.chroma |= u8(1u << k);
+      }
+      avc::Picture pic;
+      pic.wmbs = pic.hmbs = 1;
+      pic.mbs.resize(1);
+      avc::MbRec rec{};
+      rec.kind = res.t8 ? avc::kI8x8 : avc::kI16x16;
+      rec.flags = res.t8 ? u8(avc::kMbT8x8) : u8(0);
+      avc::MbState s;
+      avc::store_mb(pic, 0, rec, s, &res, nullptr);
+      i16 got[avc::kDenseCoefs];
+      avc::expand_coefs(pic.coefs.data(), pic.mbs[0], got);
+      bad_avc += std::memcmp(got, want, sizeof got) != 0 ||
+                 pic.coefs.size() != size_t(avc::coef_words(pic.mbs[0])) + avc::coef_values(pic.coefs.data(), pic.mbs[0]);
+      // H.265: one TB per size, positions listed in random order
+      for (int log2 = 2; log2 <= 5; ++log2) {
+        const int nn = 1 << (2 * log2);
+        std::vector<i16> dense(size_t(nn), 0), val_list, out(size_t(nn + nn / 16)), back(static_cast<size_t>(nn));
+        std::vector<u16> pos;
+        for (int k = 0; k < nn; ++k)
+          if ((dense[size_t(k)] = val(dens))) pos.push_back(u16(k));
+        for (size_t i = pos.size(); i > 1; --i) std::swap(pos[i - 1], pos[size_t(rnd() % i)]);
+        for (u16 k : pos) val_list.push_back(dense[k]);
+        const int n = hevc::hk_sparse_store(log2, pos.data(), val_list.data(), int(pos.size()), out.data());
+        hevc::hk_sparse_expand(out.data(), log2, back.data());
+        bad_hevc += back != dense || n != hevc::hk_sparse_words(log2) + int(pos.size());
+      }
+    }
+    return std::make_pair(bad_avc, bad_hevc);
+  });
   m.def("avc_record_stats", [](const std::vector<std::shared_ptr<AccessUnit>>& aus) {
     py::gil_scoped_release r;
     avc::Decoder dec;

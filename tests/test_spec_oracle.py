@@ -152,3 +152,14 @@ def test_intra_8x8_tap_forms(native):
     and extreme samples, every mode but DC and every availability combination."""
     assert native.avc_intra8x8_tap_check(1, 3000) == 0
     assert native.avc_intra8x8_tap_check(12345, 3000) == 0
+
+
+@pytest.mark.parametrize("seed", [1, 7, 2024])
+def test_sparse_coefficient_records(native, seed):
+    """Sparse coefficient records (mask word per 16 coefficients, then the non-zero values) give
+    back the dense blocks exactly: H.264 through store_mb -> expand_coefs (4x4 and 8x8
+    transforms, any coded pattern, int16 extremes, every density from empty to full) and H.265
+    through hk_sparse_store -> hk_sparse_expand for 4x4..32x32 TBs with unordered positions.
+    The GPU kernels expand the same words (expand_coefs_wave / tu_wave), and the bit-exact
+    decode tests cover them end to end."""
+    assert tuple(native.sparse_coef_fuzz(seed, 2000)) == (0, 0)
