@@ -50,10 +50,6 @@ static py::dict meta_dict(const FrameMeta& m) {
 
 // Worst case of a VideoFrame's trailer (everything after the pixel data): 7 varint fields
 // (<= 11 B each), 2 bools, frame_type, time_base, shape, device_id.
-static size_t video_frame_suffix_max(const std::string& device_id) {
-  return 7 * 11 + 2 * 2 + 3 + 9 + 48 + 12 + device_id.size();
-}
-
 static py::dict pic_dict(const PictureInfo& p) {
   py::dict d;
   d["width"] = p.width;
@@ -191,11 +187,13 @@ PYBIND11_MODULE(_vep, m) {
   // Frame servers and clients allocate a new multi-MB buffer per frame: glibc would mmap each
   // one and the first touch of its pages then costs more than the copy itself. Keep such blocks
   // in the (per-thread) heaps instead, so freed frame buffers are reused without page faults.
-  m.def("tune_malloc_for_frames", [](int mmap_threshold_mb) {
+  // The arenas are capped (M_ARENA_MAX): with hundreds of handler threads, per-thread arenas each
+  // keeping freed frames plus the trim threshold would grow the resident set without bound.
+  m.def("tune_malloc_for_frames", [](int mmap_threshold_mb, int arenas) {
     const int thr = std::max(1, mmap_threshold_mb) << 20;
     return mallopt(M_MMAP_THRESHOLD, thr) == 1 && mallopt(M_TRIM_THRESHOLD, 4 * thr) == 1 &&
-           mallopt(M_TOP_PAD, thr) == 1;
-  }, py::arg("mmap_threshold_mb") = 64);
+           mallopt(M_TOP_PAD, thr) == 1 && (arenas <= 0 || mallopt(M_ARENA_MAX, arenas) == 1);
+  }, py::arg("mmap_threshold_mb") = 64, py::arg("arenas") = 8);
 
   py::class_<SynthConfig>(m, "SynthConfig")
       .def(py::init<>())
@@ -1461,4 +1459,5 @@ PYBIND11_MODULE(_vep, m) {
   bind_net(m);
   bind_mux(m);
   bind_hevc(m);
+  bind_bus(m);
 }

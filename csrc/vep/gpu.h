@@ -136,13 +136,18 @@ void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s
 void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
                     hipStream_t s);
 // Intra transform blocks at tickets base .. base + count (every intra level of the round, or a
-// window of consecutive levels) in ONE launch: persistent waves take tickets in level order from
-// ctr[0] (zero at launch), or (ctr null) one wave per block in grid order; a block reads the
-// reference samples other intra blocks of the round
-// write (GpuTu::pend) from their epoch-tagged edge words (HevcDesc::xg), polled until current,
-// and publishes its own right column / bottom row the same way.
+// window of consecutive levels) in ONE launch: waves take tickets in level order from ctr[0]
+// (zero at launch) — persistent waves until the queue is empty, or (windows) one ticket per wave
+// — so every block a wave waits on was claimed by a running wave, whatever the dispatch order.
+// A block reads the reference samples other intra blocks of the round write (GpuTu::pend) from
+// their epoch-tagged edge words (HevcDesc::xg), polled until current, and publishes its own
+// right column / bottom row the same way.
 void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
-                          u32* ctr, hipStream_t s);
+                          u32* ctr, bool persistent, hipStream_t s);
+// Intra transform blocks, one workgroup per picture: d_pics[k] = {desc, first, count} names
+// picture k's intra blocks tus[first .. first + count) (level-major); the workgroup's waves take
+// them in order from an LDS counter, so every dependency wait stays inside one workgroup.
+void launch_hevc_tu_pics(const HevcDesc* d_descs, const HevcTuRange* d_pics, int npics, hipStream_t s);
 // Deblocking of every vertical (dir 0) or horizontal (dir 1) edge of the round, one thread per
 // 4-line edge segment; then SAO (copy of the deblocked picture, one thread per sample).
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s);

@@ -358,27 +358,52 @@ __global__ __launch_bounds__(256) void hevc_tu_kernel(const HevcDesc* __restrict
 // Tickets base .. end of the round's queue (a window of consecutive levels, or all of them);
 // producers in an earlier window of the round finished before this launch started (stream order)
 // and their edge words already carry this round's epoch.
+// Windows (persistent = 0): one wave per block, but the block is still taken from the ticket
+// counter, not from blockIdx: a wave only ever waits on blocks with lower tickets, which were
+// claimed by waves that are already running, so progress never depends on the order in which
+// the hardware dispatches workgroups (round 3's grid-order windows stalled when rocprofv3's
+// counter collection changed it).
 __global__ __launch_bounds__(256) void hevc_tu_queue_kernel(const HevcDesc* __restrict__ descs,
                                                            const HevcTuRange* __restrict__ ranges, int nranges,
-                                                           int base, int end, u32* __restrict__ ctr) {
+                                                           int base, int end, u32* __restrict__ ctr,
+                                                           int persistent) {
   __shared__ TuWave lds[4];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   TuWave& L = lds[wave];
-  // ctr null: one block per wave in grid order (blocks dispatch in order, so every producer a
-  // block waits on was dispatched earlier and is resident); else persistent waves on tickets
-  for (int it = 0;; ++it) {
+  for (int it = 0; persistent || it == 0; ++it) {
     int t = 0;
-    if (!ctr) {
-      if (it > 0) break;
-      t = base + int(blockIdx.x) * 4 + wave;
-    } else {
-      if (lane == 0) t = base + int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      t = __shfl(t, 0);
-    }
+    if (lane == 0) t = base + int(__hip_atomic_fetch_add(&ctr[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    t = __shfl(t, 0);
     if (t >= end) break;
     const HevcTuRange& rg = ranges[pick_range(ranges, nranges, t)];
     const HevcDesc& d = descs[rg.desc];
     tu_wave(d, static_cast<const GpuTu*>(d.tus)[rg.first + (t - rg.begin)], lane, L, true);
+  }
+}
+
+// One picture's intra blocks per workgroup (VEP_HEVC_TU_WINDOW=-1): pics[blockIdx.x] names the
+// picture and its intra blocks tus[first .. first + count), level-major. The workgroup's 16 waves
+// take them in that order from an LDS counter, so every block a wave waits on (a lower level of
+// the same picture) was claimed by a wave of the SAME workgroup: co-resident by construction, so
+// no wait depends on how or when the hardware dispatches other workgroups. The edge-word exchange
+// is the queue kernel's.
+constexpr int kTuPicWaves = 16;
+__global__ __launch_bounds__(64 * kTuPicWaves) void hevc_tu_pic_kernel(const HevcDesc* __restrict__ descs,
+                                                                       const HevcTuRange* __restrict__ pics) {
+  __shared__ TuWave lds[kTuPicWaves];
+  __shared__ u32 next;
+  const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
+  if (threadIdx.x == 0) next = 0;
+  __syncthreads();
+  const HevcTuRange pr = pics[blockIdx.x];
+  const HevcDesc& d = descs[pr.desc];
+  const GpuTu* tus = static_cast<const GpuTu*>(d.tus) + pr.first;
+  for (;;) {
+    int t = 0;
+    if (lane == 0) t = int(__hip_atomic_fetch_add(&next, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    t = __shfl(t, 0);
+    if (t >= pr.count) break;
+    tu_wave(d, tus[t], lane, lds[wave], true);
   }
 }
 
@@ -484,13 +509,18 @@ void launch_hevc_tu(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nr
 }
 
 void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, int nranges, int base, int count,
-                          u32* ctr, hipStream_t s) {
-  if (nranges <= 0 || count <= 0) return;
+                          u32* ctr, bool persistent, hipStream_t s) {
+  if (nranges <= 0 || count <= 0 || !ctr) return;
   // persistent waves: a fraction of the chip (4 per workgroup) — the other lanes' kernels run
-  // beside it, and waves that run far ahead of the wavefront only poll
-  const int wgs = ctr ? std::min((count + 3) / 4, kTuQueueWgs) : (count + 3) / 4;
+  // beside it, and waves that run far ahead of the wavefront only poll. Windows: a wave per block.
+  const int wgs = persistent ? std::min((count + 3) / 4, kTuQueueWgs) : (count + 3) / 4;
   hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, base, base + count,
-                     ctr);
+                     ctr, persistent ? 1 : 0);
+}
+
+void launch_hevc_tu_pics(const HevcDesc* d_descs, const HevcTuRange* d_pics, int npics, hipStream_t s) {
+  if (npics <= 0) return;
+  hipLaunchKernelGGL(hevc_tu_pic_kernel, dim3(npics), dim3(64 * kTuPicWaves), 0, s, d_descs, d_pics);
 }
 
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s) {

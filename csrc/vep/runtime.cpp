@@ -411,10 +411,9 @@ constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
 constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
-constexpr int kDefaultTuWindow = 0;        // H.265 intra TUs: 0 = per-level launches, k = queue windows
-                                           // of k levels (8: 8x fewer launches, same end-to-end rate,
-                                           // but edge-word waits time out under rocprofv3 --pmc
-                                           // serialisation: profiles/r3/hevc_window/)
+constexpr int kDefaultTuWindow = 8;        // H.265 intra TUs: 0 = per-level launches, k = queue windows
+                                           // of k levels, blocks taken by ticket (8x fewer launches;
+                                           // progress independent of dispatch order: profiles/r4/)
 constexpr int kAllLevels = 1 << 20;        // (a window holding every level of a round)
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
@@ -451,7 +450,7 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     polite_wait_ = !(std::getenv("VEP_SPIN_WAIT") && std::getenv("VEP_SPIN_WAIT")[0] == '1');
     hevc_tu_window_ = kDefaultTuWindow;
     if (const char* tq = std::getenv("VEP_HEVC_TU_QUEUE")) hevc_tu_window_ = tq[0] == '1' ? kAllLevels : 0;
-    if (const char* tw = std::getenv("VEP_HEVC_TU_WINDOW")) hevc_tu_window_ = std::clamp(std::atoi(tw), 0, kAllLevels);
+    if (const char* tw = std::getenv("VEP_HEVC_TU_WINDOW")) hevc_tu_window_ = std::clamp(std::atoi(tw), -1, kAllLevels);
     int ns = opt_.stages;
     if (ns <= 0) {
       const char* se = std::getenv("VEP_STAGES");
@@ -1078,7 +1077,9 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   std::vector<std::vector<gpu::HevcTuRange>> hranges(static_cast<size_t>(hrounds));
   // per round: level-0 ranges, level-0 blocks, intra (queue) ranges, intra blocks
   std::vector<std::array<int, 4>> hwork(static_cast<size_t>(hrounds), std::array<int, 4>{0, 0, 0, 0});
-  std::vector<size_t> off_hctr(static_cast<size_t>(hrounds));
+  std::vector<size_t> off_hctr(static_cast<size_t>(hrounds)), off_hpicq(static_cast<size_t>(hrounds));
+  // per round, picture mode (hevc_tu_window_ < 0): {desc, first intra block, intra blocks} per picture
+  std::vector<std::vector<gpu::HevcTuRange>> hpicq(static_cast<size_t>(hrounds));
   // per round and intra level: first ticket, blocks (the one-launch-per-level mode); per round
   // and queue window: first ticket, blocks (one ticket counter each)
   std::vector<std::vector<std::array<int, 2>>> hlevels(static_cast<size_t>(hrounds));
@@ -1141,6 +1142,14 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       }
     }
     hwork[size_t(r)][3] = tickets;
+    if (hevc_tu_window_ < 0) {  // one workgroup per picture with intra blocks
+      for (size_t k = 0; k < hround_pics[size_t(r)].size(); ++k) {
+        const hevc::GpuPicture& p = *hpics[size_t(hround_pics[size_t(r)][k])].p;
+        if (p.level_begin.size() < 3) continue;  // (levels 0 .. L-1 plus the end: intra needs L >= 2)
+        const int b = int(p.level_begin[1]), e = int(p.tus.size());
+        if (e > b) hpicq[size_t(r)].push_back({int(k), b, e - b, 0});
+      }
+    }
     if (hevc_tu_window_ > 0) {  // consecutive levels, hevc_tu_window_ per launch
       const auto& lv = hlevels[size_t(r)];
       for (size_t l = 0; l < lv.size(); l += size_t(hevc_tu_window_)) {
@@ -1153,6 +1162,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     need += al(std::max<size_t>(hranges[size_t(r)].size(), 1) * sizeof(gpu::HevcTuRange));
     off_hctr[size_t(r)] = need;  // the queue windows' ticket counters (zero in the upload)
     need += al(std::max<size_t>(hwindows[size_t(r)].size(), 1) * sizeof(u32));
+    off_hpicq[size_t(r)] = need;
+    need += al(std::max<size_t>(hpicq[size_t(r)].size(), 1) * sizeof(gpu::HevcTuRange));
   }
   const size_t off_gather = need;  // gather chunks: pinned records (+ slices without direct reads)
   need += al(sizeof(gpu::GatherChunk) * std::max<size_t>(nchunks, 1));
@@ -1464,6 +1475,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     auto* hr = reinterpret_cast<gpu::HevcTuRange*>(st.h + off_hranges[size_t(r)]);
     for (size_t k = 0; k < hranges[size_t(r)].size(); ++k) hr[k] = hranges[size_t(r)][k];
     std::memset(st.h + off_hctr[size_t(r)], 0, std::max<size_t>(hwindows[size_t(r)].size(), 1) * sizeof(u32));
+    if (!hpicq[size_t(r)].empty())
+      std::memcpy(st.h + off_hpicq[size_t(r)], hpicq[size_t(r)].data(), hpicq[size_t(r)].size() * sizeof(gpu::HevcTuRange));
   }
   // H2D on the copy stream overlaps the previous batch's kernels on the compute stream: the
   // small header region by SDMA, the slice payload by the gather kernel (PCIe reads)
@@ -1524,16 +1537,19 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     gpu::launch_hevc_mc(hd2, np, hround_work[size_t(r)][0], cs);
     const auto& hw = hwork[size_t(r)];
     gpu::launch_hevc_tu(hd2, hr, hw[0], 0, hw[1], cs);
-    if (hevc_tu_window_ == 0) {  // one launch per intra level (kernel boundaries order the levels)
+    if (hevc_tu_window_ < 0) {  // one workgroup per picture: every dependency wait inside it
+      gpu::launch_hevc_tu_pics(hd2, reinterpret_cast<const gpu::HevcTuRange*>(st.d + off_hpicq[size_t(r)]),
+                               int(hpicq[size_t(r)].size()), cs);
+    } else if (hevc_tu_window_ == 0) {  // one launch per intra level (kernel boundaries order the levels)
       for (const auto& lv : hlevels[size_t(r)]) gpu::launch_hevc_tu(hd2, hr + hw[0], hw[2], lv[0], lv[1], cs);
     } else {  // one queue launch per window of levels, in level order on the stream
       auto* ctr = reinterpret_cast<u32*>(st.d + off_hctr[size_t(r)]);
-      // (a window of bounded depth runs one wave per block in grid order; the whole round keeps
-      // the persistent ticket queue)
+      // (a window of bounded depth runs one wave per block, each taking its block from the
+      // window's ticket counter; the whole round keeps the persistent ticket queue)
       const bool persistent = hevc_tu_window_ >= kAllLevels;
       for (size_t k = 0; k < hwindows[size_t(r)].size(); ++k)
         gpu::launch_hevc_tu_queue(hd2, hr + hw[0], hw[2], hwindows[size_t(r)][k][0], hwindows[size_t(r)][k][1],
-                                  persistent ? ctr + k : nullptr, cs);
+                                  ctr + k, persistent, cs);
     }
     if (dbk) {
       gpu::launch_hevc_deblock(hd2, np, hround_work[size_t(r)][1], 0, cs);
@@ -1693,8 +1709,16 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
     cp->ring_->commit(slots[i], jobs[i].meta);
     cp->decoded.fetch_add(1, std::memory_order_relaxed);
     frames_.fetch_add(1, std::memory_order_relaxed);
+    if (auto hook = std::atomic_load(&publish_hook_)) (*hook)(jobs[i].cam, cp->ring_->published());
   }
   batches_.fetch_add(1);
+}
+
+void Worker::set_publish_hook(std::function<void(int, i64)> f) {
+  std::shared_ptr<std::function<void(int, i64)>> h;
+  if (f) h = std::make_shared<std::function<void(int, i64)>>(std::move(f));
+  std::lock_guard<std::mutex> g(cams_mu_);  // (publish holds it: no hook call is in flight after this)
+  std::atomic_store(&publish_hook_, h);
 }
 
 double Worker::gpu_ms_total() const {
@@ -2044,6 +2068,41 @@ bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, siz
     if (ring->still_valid(slot, meta->seq)) return true;
   }
   return false;
+}
+
+void Worker::read_latest_many(std::vector<ReadReq>& reqs) {
+  if (!dev_.gpu()) {
+    for (auto& r : reqs) r.ok = read_latest(*r.ring, r.after, &r.meta, r.dst, r.cap, r.pinned);
+    return;
+  }
+  dev_.bind();
+  std::vector<int> slot(reqs.size(), -1);
+  bool queued = false;
+  for (size_t k = 0; k < reqs.size(); ++k) {
+    ReadReq& r = reqs[k];
+    r.ok = false;
+    if (!r.pinned) {
+      r.ok = read_latest(*r.ring, r.after, &r.meta, r.dst, r.cap, false);
+      continue;
+    }
+    if (!r.ring->latest(r.after, &r.meta, &slot[k])) continue;
+    VEP_CHECK(r.cap >= r.ring->slot_bytes(), "read_latest_many destination too small");
+    VEP_HIP(hipMemcpyAsync(r.dst, r.ring->slot_ptr(slot[k]), r.ring->slot_bytes(), hipMemcpyDeviceToHost,
+                           serve_stream_));
+    queued = true;
+  }
+  if (!queued) return;
+  ServeBuf* b = acquire_serve(0);  // (its completion event)
+  try {
+    VEP_HIP(hipEventRecord(b->ev[0], serve_stream_));
+    VEP_HIP(hipEventSynchronize(b->ev[0]));
+  } catch (...) {
+    release_serve(b);
+    throw;
+  }
+  release_serve(b);
+  for (size_t k = 0; k < reqs.size(); ++k)  // a slot the writer reused meanwhile is not served
+    if (slot[k] >= 0) reqs[k].ok = reqs[k].ring->still_valid(slot[k], reqs[k].meta.seq);
 }
 
 // --------------------------------------------------------------------------- proto encoding

@@ -291,6 +291,21 @@ class Worker {
   // dst_pinned: dst is page-locked (register_host) -> one DMA straight into it, no staging.
   bool read_latest(int cam, i64 after, FrameMeta* meta, u8* dst, size_t cap);
   bool read_latest(FrameRing& ring, i64 after, FrameMeta* meta, u8* dst, size_t cap, bool dst_pinned = false);
+  // Several rings' newest frames at once (the frame bus pump): every copy into page-locked
+  // destinations is queued on the serving stream before one wait; others go one by one.
+  struct ReadReq {
+    FrameRing* ring = nullptr;
+    i64 after = 0;
+    u8* dst = nullptr;
+    size_t cap = 0;
+    bool pinned = false;
+    FrameMeta meta;  // out
+    bool ok = false; // out
+  };
+  void read_latest_many(std::vector<ReadReq>& reqs);
+  // Called after every frame a camera commits to its ring: (camera index, sequence). Runs on the
+  // publishing thread with the camera table locked: must be cheap and must not call back in.
+  void set_publish_hook(std::function<void(int, i64)> f);
   // Page-lock caller memory (e.g. a shared-memory segment another process maps) for direct
   // D2H. False on the CPU backend or when the driver refuses the range.
   bool register_host(void* p, size_t n);
@@ -442,6 +457,7 @@ class Worker {
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;
+  std::shared_ptr<std::function<void(int, i64)>> publish_hook_;  // (atomic_load / atomic_store)
   std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0};
   std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0}, records_gathered_{0};
   std::mutex timers_mu_;
@@ -462,5 +478,9 @@ class Worker {
 // the payload can be DMA'd straight into the output buffer: returns (prefix, suffix).
 std::pair<std::string, std::string> encode_video_frame(const FrameMeta& m, size_t data_len,
                                                        const std::string& device_id);
+// Upper bound of the suffix (fields after `data`) encode_video_frame produces for device_id.
+inline size_t video_frame_suffix_max(const std::string& device_id) {
+  return 7 * 11 + 2 * 2 + 3 + 9 + 48 + 12 + device_id.size();
+}
 
 }  // namespace vep

@@ -20,12 +20,14 @@ def test_hevc_gpu_bit_exact(native, w, h, n, kw):
 
 
 @pytest.mark.parametrize("env", [{"VEP_HEVC_TU_QUEUE": "1"}, {"VEP_HEVC_TU_QUEUE": "0"},
-                                 {"VEP_HEVC_TU_WINDOW": "3"}, {"VEP_HEVC_TU_WINDOW": "8"}],
-                         ids=["tu-queue", "tu-levels", "tu-window3", "tu-window8"])
+                                 {"VEP_HEVC_TU_WINDOW": "3"}, {"VEP_HEVC_TU_WINDOW": "8"},
+                                 {"VEP_HEVC_TU_WINDOW": "-1"}],
+                         ids=["tu-queue", "tu-levels", "tu-window3", "tu-window8", "tu-picture"])
 def test_hevc_gpu_intra_tu_scheduling(native, monkeypatch, env):
     """Every schedule of the intra transform blocks is bit-exact: one queue launch per round
     (edge-word exchange between blocks), one launch per dependency level, and one queue launch
-    per window of k levels (the exchange also spans windows)."""
+    per window of k levels (the exchange also spans windows), and one workgroup per picture
+    (every dependency wait inside the workgroup)."""
     monkeypatch.delenv("VEP_HEVC_TU_QUEUE", raising=False)
     monkeypatch.delenv("VEP_HEVC_TU_WINDOW", raising=False)
     for k, v in env.items():

@@ -117,12 +117,18 @@ def _check_rows(hub, batch, names, S):
         assert (row.int() - ref.int()).abs().max().item() <= 1, n
 
 
+def _bus_segments(pid):
+    from video_edge_ai_proxy_amd.engine import shm
+
+    return [f for f in os.listdir(shm.SHM_DIR) if f.startswith("vep-bus.") and f.split(".")[3:4] == [str(pid)]]
+
+
 def test_isolated_frames_travel_through_shared_memory(native, tmp_path):
-    """VideoLatestImage bytes from a worker process arrive through its shared-memory segment and
-    are the same VideoFrame the in-process path builds (pixels equal the ring's latest frame)."""
+    """VideoLatestImage bytes from a worker process arrive through the frame bus (the worker's
+    shared-memory segments, no call to the worker) and are the same VideoFrame the in-process path
+    builds (pixels equal the ring's latest frame)."""
     import numpy as np
 
-    from video_edge_ai_proxy_amd.engine import shm
     from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
     from video_edge_ai_proxy_amd.proto import pb
 
@@ -139,14 +145,13 @@ def test_isolated_frames_travel_through_shared_memory(native, tmp_path):
         assert m["seq"] == seq
         assert np.array_equal(np.frombuffer(vf.data, np.uint8).reshape(96, 160, 3), img)
         pid = hub.state("c0")["worker_pid"]
-        segs = [f for f in os.listdir(shm.SHM_DIR) if f.startswith(shm.segment_prefix(pid))]
-        assert segs, "the worker serves frames through shared-memory segments"
+        assert len(_bus_segments(pid)) >= 2, "the worker publishes frames on its bus segments (control + data)"
         # nothing newer yet: None, and the cursor protocol is the in-process one
         assert hub.latest_frame_bytes("c0", seq, 0) is None
     finally:
         hub.shutdown()
         srv.stop()
-    assert not [f for f in os.listdir(shm.SHM_DIR) if f.startswith(shm.segment_prefix(pid))]
+    assert not _bus_segments(pid)
 
 
 def test_isolated_consumer_batch_gathers_across_worker_processes(native, tmp_path):

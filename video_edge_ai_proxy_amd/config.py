@@ -73,6 +73,17 @@ class GpuConfig:
 
 
 @dataclass
+class ServingConfig:
+    """Frame serving. ``frontends`` > 0 runs that many gRPC serving processes, all bound to
+    ``grpc_port`` with SO_REUSEPORT (the kernel spreads client connections over them); they read
+    frames from the node's frame bus (shared memory, csrc/vep/bus.h) and forward the other RPCs to
+    the main process. -1 = one per GPU; 0 = serve from the main process."""
+    frontends: int = 0
+    threads: int = 256          # gRPC handler threads per serving process (each waits <= 3 x 1 s)
+    bus: bool = False           # main-process serving also reads the frame bus (shared DMA per frame)
+
+
+@dataclass
 class Config:
     version: str = "0.1.0"
     title: str = "vep MI355X video edge hub"
@@ -86,6 +97,9 @@ class Config:
     api: ApiConfig = field(default_factory=ApiConfig)
     buffer: BufferConfig = field(default_factory=BufferConfig)
     gpu: GpuConfig = field(default_factory=GpuConfig)
+    serving: ServingConfig = field(default_factory=ServingConfig)
+    # frame-bus tag of this hub instance (set at start-up when the bus is in use; not a YAML key)
+    bus_tag: str = ""
 
     @property
     def ring_slots(self) -> int:

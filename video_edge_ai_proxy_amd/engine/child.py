@@ -7,8 +7,10 @@ bitstream parse or a GPU error) ends this process only, and the parent starts a 
 re-adds its cameras — the reference's per-camera ``restart: always`` container
 (server/services/rtsp_process_manager.go:70-81) at per-GPU granularity.
 
-Frames leave through shared memory (engine/shm.py): each connection owns a page-locked segment
-the serialized ``VideoFrame`` is DMA'd into; only its name and length travel on the connection.
+Frames leave through the node's frame bus (csrc/vep/bus.h): the Hub of this process publishes
+its cameras under ``cfg.bus_tag`` with owner index ``--owner``, and readers (the parent, the serving
+processes) take frames from shared memory without calling this process. A gathered consumer batch
+still leaves through the connection's page-locked segment (engine/shm.py).
 
 The worker processes of one hub are the ranks of a ``torch.distributed`` group (RCCL over xGMI
 on GPUs, gloo on the CPU backend), formed by the parent on demand and re-formed with a fresh
@@ -39,33 +41,6 @@ log = logging.getLogger("vep.child")
 # methods of Hub a parent may call
 EXPORTED = {"start_camera", "stop_camera", "state", "logs", "touch", "set_proxy", "proxy",
             "latest_frame_bytes", "latest_frame", "wait_decoded", "has"}
-
-
-def frame_into(hub, slot: ShmSlot, name: str, after: int = 0, wait_ms: int = 0):
-    """Hub.latest_frame_bytes, written into the connection's shared-memory slot:
-    (seq, segment name, length, meta) or None."""
-    w, cam = hub.worker_of(name)
-    pub = w.published(cam)
-    if pub < after:
-        after = 0  # the cursor belongs to an older ring (see Hub.latest_frame_bytes)
-    if wait_ms > 0 and pub <= after:
-        w.wait_frame(cam, after, wait_ms)
-    for _ in range(3):
-        if slot.cap == 0:
-            need = w.video_frame_bound(cam, name)
-            if need == 0:
-                return None
-            slot.ensure(need)
-        r = w.video_frame_into(cam, after, name, slot.addr, slot.cap, slot.pinned)
-        if isinstance(r, int):  # a larger ring appeared (resolution change): grow, retry
-            slot.ensure(r)
-            continue
-        if r is None:
-            return None
-        seq, length, meta = r
-        meta["shm_pinned"] = slot.pinned
-        return seq, slot.name, length, meta
-    return None
 
 
 class RankGroup:
@@ -157,8 +132,6 @@ def _serve(hub, group: RankGroup, conn, stop: threading.Event) -> None:
                 elif method == "start_camera":
                     h = hub.start_camera(*args, **kwargs)
                     res = {"cam": h.cam}
-                elif method == "latest_frame_shm":
-                    res = frame_into(hub, slot, *args, **kwargs)
                 elif method == "group_form":
                     res = group.form(*args, **kwargs)
                 elif method == "consumer_gather":
@@ -185,13 +158,14 @@ def main(argv=None) -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--device", type=int, required=True)
     ap.add_argument("--config", required=True, help="Config as JSON")
+    ap.add_argument("--owner", type=int, default=0, help="frame-bus owner index of this worker")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format=f"%(asctime)s child[{a.device}] %(name)s: %(message)s")
     from ..config import Config, _merge
     from .hub import Hub
 
     cfg = _merge(Config(), json.loads(a.config))
-    hub = Hub(cfg, devices=[a.device])
+    hub = Hub(cfg, devices=[a.device], bus_owner=a.owner)
     group = RankGroup(hub, a.device, cfg.gpu.consumer_hook)
     key = bytes.fromhex(os.environ["VEP_CHILD_KEY"])
     listener = Listener(("127.0.0.1", 0), authkey=key)

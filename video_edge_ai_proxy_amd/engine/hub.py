@@ -56,7 +56,7 @@ def place_camera(name: str, loads: list[int], policy: str = "least_loaded") -> i
 
 
 class Hub:
-    def __init__(self, cfg: Config, devices: Optional[list[int]] = None):
+    def __init__(self, cfg: Config, devices: Optional[list[int]] = None, bus_owner: int = 0):
         self.cfg = cfg
         if devices is None:
             devices = list(cfg.gpu.devices) if cfg.gpu.devices else list(range(gpu_count()))
@@ -87,6 +87,14 @@ class Hub:
                 t = torch.zeros((int(g.max_cameras_per_gpu), *shape), dtype=torch.uint8, device=dev)
                 w.set_consumer_buffers(t.data_ptr(), 0, int(g.max_cameras_per_gpu))
                 self.consumer.append(t)
+        # Frame bus (cfg.bus_tag set: serving processes read frames from shared memory): one owner
+        # per worker, index bus_owner + k; the pump DMAs a camera's newest frame on demand.
+        self.bus = []
+        if cfg.bus_tag:
+            for k, w in enumerate(self.workers):
+                o = native.BusOwner(cfg.bus_tag, bus_owner + k, int(g.max_cameras_per_gpu))
+                o.attach(w)
+                self.bus.append(o)
         self.archiver = native.Archiver()
         self.cameras: dict[str, CameraHandle] = {}
         self._lock = threading.RLock()
@@ -119,6 +127,8 @@ class Hub:
                                              self.archiver, timeout_ms, reconnect_delay_ms, 30000)
             h.session.start()
             self.cameras[name] = h
+            if self.bus:
+                self.bus[wi].add(cam, name)
             log.info("camera %s -> worker %d (device %s) slot %d", name, wi, self.devices[wi], cam)
             return h
 
@@ -127,6 +137,8 @@ class Hub:
             h = self.cameras.pop(name, None)
         if h is None:
             raise CameraNotFound(name)
+        if self.bus:
+            self.bus[h.worker_index].remove(h.cam)
         h.session.stop()
         self.workers[h.worker_index].remove_camera(h.cam)
 
@@ -187,6 +199,8 @@ class Hub:
                 self.stop_camera(name)
             except CameraNotFound:
                 pass
+        for o in self.bus:
+            o.stop()
         for w in self.workers:
             w.stop()
         self.archiver.flush()

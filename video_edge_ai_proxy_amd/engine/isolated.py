@@ -15,10 +15,11 @@ context is what the children are for, not something the parent may do. The GPU t
 do not drive this class (their pytest process holds a context); tests/test_isolated_hub.py does,
 with CPU-backend children.
 
-Calls travel over authenticated local connections (a small pool per child, so a blocking
-``latest_frame_bytes`` does not hold the others up); frames come back through a shared-memory
-segment per connection (engine/shm.py: the child DMAs the serialized ``VideoFrame`` into it, the
-front-end copies it out once), not through the socket.
+Control calls travel over authenticated local connections (a small pool per child). Frames do
+not: every child publishes its cameras on the node's frame bus (csrc/vep/bus.h, tag
+``cfg.bus_tag``), and ``latest_frame_bytes`` / ``touch`` read and mark it directly — the child's
+pump DMAs a camera's newest frame into shared memory once for every reader (this process, the
+serving processes of ``serving.frontends``), with no call to the child on the frame path.
 
 The children are the ranks of one ``torch.distributed`` group (RCCL over xGMI between GPUs, gloo
 for CPU-backend children). The parent forms it on demand — a fresh TCP rendezvous on 127.0.0.1
@@ -63,14 +64,15 @@ _ERRORS = {"CameraNotFound": CameraNotFound, "CameraExists": CameraExists, "KeyE
 
 
 class _Child:
-    def __init__(self, device: int, cfg_json: str, nconn: int = 8, start_timeout_s: float = 180.0):
+    def __init__(self, device: int, cfg_json: str, nconn: int = 4, start_timeout_s: float = 180.0,
+                 owner: int = 0):
         self.device = device
         key = secrets.token_bytes(16)
         env = dict(os.environ, VEP_CHILD_KEY=key.hex())
         env["PYTHONPATH"] = _PKG_PARENT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "video_edge_ai_proxy_amd.engine.child", "--device", str(device),
-             "--config", cfg_json],
+             "--config", cfg_json, "--owner", str(owner)],
             stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env)
         line = b""
         deadline = time.time() + start_timeout_s
@@ -157,6 +159,13 @@ class _Child:
             self.proc.wait()
         self.close_pipes()
         remove_segments(self.pid)
+        _remove_bus_segments(self.pid)
+
+
+def _remove_bus_segments(pid: int) -> None:
+    from .._native import native
+
+    native.bus_remove_segments(pid)
 
 
 class _WorkerView:
@@ -199,9 +208,14 @@ class ProcessHub:
         if devices is None:
             devices = list(cfg.gpu.devices) if cfg.gpu.devices else _count_gpus()
         self.devices = devices or [-1]
+        if not cfg.bus_tag:  # the children publish their frames on the node's frame bus
+            cfg.bus_tag = f"n{os.getpid()}"
         self._cfg_json = json.dumps(dataclasses.asdict(cfg))
+        from .._native import native
+
+        self.bus = native.BusReader(cfg.bus_tag)
         with ThreadPoolExecutor(max_workers=len(self.devices)) as ex:  # start them side by side
-            futs = [ex.submit(_Child, d, self._cfg_json) for d in self.devices]
+            futs = [ex.submit(_Child, d, self._cfg_json, owner=i) for i, d in enumerate(self.devices)]
         errs = [f.exception() for f in futs]
         started = [f.result() for f, e in zip(futs, errs) if e is None]
         if any(e is not None for e in errs):
@@ -249,8 +263,9 @@ class ProcessHub:
         dead = self._children[i]
         dead.close_pipes()  # the dead child's pipes and shared-memory mappings
         remove_segments(dead.pid)  # and the segments it could not unlink itself
+        _remove_bus_segments(dead.pid)
         self._group_ok = False  # the survivors' group lost a rank: re-form before the next gather
-        child = _Child(self.devices[i], self._cfg_json)
+        child = _Child(self.devices[i], self._cfg_json, owner=i)
         try:
             with self._lock:
                 mine = [n for n, h in self.cameras.items() if h.worker_index == i]
@@ -446,7 +461,9 @@ class ProcessHub:
             return "", str(e)
 
     def touch(self, name: str, keyframe_only: Optional[bool] = None) -> None:
-        self._call(name, "touch", keyframe_only)
+        self.handle(name)
+        if not self.bus.touch(name, -1 if keyframe_only is None else int(bool(keyframe_only))):
+            raise WorkerRestarting(f"camera {name!r}: its worker process is restarting")
 
     def set_proxy(self, name: str, on: bool) -> None:
         self._proxy[name] = bool(on)
@@ -456,16 +473,13 @@ class ProcessHub:
         return bool(self._call(name, "proxy"))
 
     def latest_frame_bytes(self, name: str, after: int = 0, wait_ms: int = 0):
-        """(seq, serialized VideoFrame, meta) or None: the child writes the frame into this
-        connection's shared-memory segment, copied out here once (the bytes grpcio sends)."""
-        def read(res, shm):
-            if res is None:
-                return None
-            seq, segment, length, meta = res
-            return seq, shm.read(segment, length), meta
-
-        h = self.handle(name)
-        return self._children[h.worker_index].call("latest_frame_shm", name, after, wait_ms, read=read)
+        """(seq, serialized VideoFrame, meta) or None, from the frame bus: the child's pump DMAs
+        the frame into shared memory, copied out here once (the bytes grpcio sends)."""
+        self.handle(name)
+        r = self.bus.frame(name, after, wait_ms, -1)
+        if r is None:
+            return None
+        return r[0], r[1], {"seq": r[0]}
 
     def latest_frame(self, name: str, after: int = 0):
         return self._call(name, "latest_frame", after)

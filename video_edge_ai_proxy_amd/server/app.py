@@ -21,7 +21,7 @@ from ..services.edge import EdgeService
 from ..services.process_manager import ProcessManager
 from ..services.settings import SettingsManager
 from ..services.storage import Storage
-from .grpc_server import ImageService, serve
+from .grpc_server import BusFrames, ImageService, serve
 from .metrics import Metrics
 from .rest import create_app
 
@@ -44,10 +44,12 @@ class HubApp:
     rest_thread: Optional[threading.Thread]
     cron: list
     metrics: Metrics
+    frontends: Optional[object] = None  # server.frontend.FrontendPool (serving.frontends > 0)
+    public_grpc_port: int = 0
 
     @property
     def grpc_port(self) -> int:
-        return self.grpc_server.bound_port
+        return self.public_grpc_port or self.grpc_server.bound_port
 
     @property
     def rest_port(self) -> int:
@@ -55,6 +57,8 @@ class HubApp:
 
     def stop(self):
         log.info("shutting down")
+        if self.frontends is not None:
+            self.frontends.close()
         try:
             self.grpc_server.stop(grace=2).wait(5)
         except Exception:
@@ -74,6 +78,26 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
               grpc_port: Optional[int] = None, devices=None, start_rest: bool = True,
               restore: bool = True) -> HubApp:
     os.makedirs(cfg.data_dir, exist_ok=True)
+    gport = cfg.grpc_port if grpc_port is None else grpc_port
+    # Serving processes (serving.frontends): started first — this process may initialise a GPU
+    # below, and a process holding a GPU context must not start programs. They read frames from
+    # the frame bus, so every decoding process publishes one (cfg.bus_tag); the isolated hub's
+    # workers always do (the main process then serves from the bus too, without calling them).
+    nfront = int(cfg.serving.frontends)
+    if nfront < 0:
+        nfront = max(1, len(devices if devices is not None else (cfg.gpu.devices or _gpu_count())))
+    use_bus = nfront > 0 or cfg.gpu.isolation == "process" or cfg.serving.bus
+    if use_bus and not cfg.bus_tag:
+        cfg.bus_tag = f"n{os.getpid()}"
+    frontends, control = None, None
+    if nfront > 0:
+        from .frontend import FrontendPool
+
+        if not gport:
+            gport = _free_port(host)
+        control = f"127.0.0.1:{_free_port('127.0.0.1')}"
+        frontends = FrontendPool(nfront, cfg.bus_tag, f"{host}:{gport}", control, int(cfg.serving.threads),
+                                 stats_path=os.path.join(cfg.data_dir, f"serving-{cfg.bus_tag}"))
     storage = Storage(os.path.join(cfg.data_dir, "registry.db"))
     if cfg.gpu.isolation == "process":
         from ..engine.isolated import ProcessHub
@@ -88,11 +112,11 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
     consumer = AnnotationConsumer(settings, edge, cfg.annotation.endpoint)
     queue.start_consuming(consumer, cfg.annotation.unacked_limit, cfg.annotation.poll_duration_ms,
                           cfg.annotation.max_batch_size)
-    image = ImageService(pm, settings, edge, queue, cfg.api.endpoint)
-    gport = cfg.grpc_port if grpc_port is None else grpc_port
-    gsrv = serve(image, f"{host}:{gport}")
+    image = ImageService(pm, settings, edge, queue, cfg.api.endpoint, bus=BusFrames(cfg.bus_tag) if use_bus else None)
+    # with serving processes this server is their control port (non-frame RPCs); else public
+    gsrv = serve(image, control if frontends is not None else f"{host}:{gport}", workers=int(cfg.serving.threads))
     cron = start_cron_jobs(cfg)
-    metrics = Metrics(hub, image)
+    metrics = Metrics(hub, image, frontends)
     rest_server = rest_thread = None
     rport = cfg.port if rest_port is None else rest_port
     if start_rest:
@@ -111,14 +135,32 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
                                        daemon=True, name="vep-rest")
         rest_thread.start()
     happ = HubApp(cfg, storage, hub, pm, settings, edge, queue, consumer, image, gsrv,
-                  rest_server, rest_thread, cron, metrics)
+                  rest_server, rest_thread, cron, metrics, frontends, gport if frontends is not None else 0)
     happ._rest_port = rport  # type: ignore[attr-defined]
     if restore:
         restored = pm.restore()
         if restored:
             log.info("restored %d cameras from the registry", len(restored))
-    log.info("vep ready: REST :%s gRPC :%s devices=%s", rport, gsrv.bound_port, hub.devices)
+    log.info("vep ready: REST :%s gRPC :%s devices=%s serving processes=%d", rport, happ.grpc_port, hub.devices,
+             nfront)
     return happ
+
+
+def _free_port(host: str) -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind((host if host not in ("", "0.0.0.0") else "127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _gpu_count() -> list:
+    try:
+        import torch
+
+        return list(range(torch.cuda.device_count()))  # (does not initialise the GPU)
+    except Exception:  # noqa: BLE001
+        return []
 
 
 def run_forever(cfg: Config, **kw) -> None:

@@ -56,7 +56,7 @@ def serving(worker, cams, workers: int = 64):
     """gRPC server (this process) over the worker's cameras: yields (target, camera names, svc)."""
     hub = _WorkerHub(worker, cams)
     svc = ImageService(_PM(hub))
-    server = serve(svc, "127.0.0.1:0", workers=workers)
+    server = serve(svc, "127.0.0.1:0", workers=workers, tune_malloc=True)  # (a serving-only process)
     try:
         yield f"127.0.0.1:{server.bound_port}", list(hub.map), svc
     finally:

@@ -9,7 +9,9 @@ Reference parity (server/grpcapi/):
   * ``ListStreams`` (:100-131), ``Annotate`` (grpc_annotation_api.go), ``Proxy``
     (grpc_proxy_api.go), ``Storage`` (grpc_storage_api.go) with the same validation/status codes.
 Frames are served zero-copy from the camera's HBM ring: the native layer D2H-copies the slot into
-one pre-encoded protobuf buffer; the response serializer is the identity.
+one pre-encoded protobuf buffer; the response serializer is the identity. With a frame bus
+(``bus=BusFrames(tag)``: serving processes, isolated workers) the frame comes from the node's
+shared-memory bus instead (csrc/vep/bus.h): the owner's pump DMAs it once for every reader.
 """
 from __future__ import annotations
 
@@ -47,11 +49,39 @@ MAX_CURSORS = 65536  # (client, camera) cursors kept, least recently used evicte
 _EMPTY = b""  # serialized empty VideoFrame
 
 
+class BusFrames:
+    """Frames from the node's frame bus (any camera of any owner process, no GPU context here).
+    The newest frame's bytes are kept per camera, so the clients of one camera in this process
+    share one copy out of shared memory as well as the owner's one DMA."""
+
+    def __init__(self, tag: str):
+        from .._native import native
+
+        self.reader = native.BusReader(tag)
+        self._last: dict[str, tuple[int, bytes]] = {}
+
+    def has(self, dev: str) -> bool:
+        return self.reader.has(dev)
+
+    def frame(self, dev: str, after: int, wait_ms: int, key_frame_only: bool):
+        """(seq, serialized VideoFrame) of the newest frame with seq > after, or None."""
+        held = self._last.get(dev)
+        r = self.reader.frame(dev, after, wait_ms, 1 if key_frame_only else 0, held[0] if held else -1)
+        if r is None:
+            return None
+        seq, data = r
+        if data is None:  # the frame this process already copied out
+            return held
+        self._last[dev] = (seq, data)
+        return seq, data
+
+
 class ImageService:
-    def __init__(self, process_manager: ProcessManager, settings_manager=None, edge_service=None,
-                 annotation_queue=None, api_endpoint: str = ""):
+    def __init__(self, process_manager: Optional[ProcessManager], settings_manager=None, edge_service=None,
+                 annotation_queue=None, api_endpoint: str = "", bus: Optional[BusFrames] = None):
         self.pm = process_manager
-        self.hub = process_manager.hub
+        self.hub = process_manager.hub if process_manager is not None else None
+        self.bus = bus
         self.settings = settings_manager
         self.edge = edge_service
         self.queue = annotation_queue
@@ -77,8 +107,29 @@ class ImageService:
             while len(self._cursors) > MAX_CURSORS:
                 self._cursors.popitem(last=False)
 
+    def _served(self, peer: str, dev: str, seq: int, t0: float) -> None:
+        self._set_cursor(peer, dev, seq)
+        self.frames_served += 1
+        self.latencies_ms.append((time.perf_counter() - t0) * 1e3)
+        if len(self.latencies_ms) > 10000:
+            del self.latencies_ms[:5000]
+
+    def _bus_frame(self, dev: str, key_frame_only: bool, peer: str, t0: float) -> bytes:
+        after = self._cursor(peer, dev)
+        for _ in range(WAIT_ATTEMPTS):
+            r = self.bus.frame(dev, after, WAIT_BLOCK_MS, key_frame_only)  # (marks the demand too)
+            if r is not None:
+                self._served(peer, dev, r[0], t0)
+                return r[1]
+            if not self.bus.has(dev):
+                break  # unknown camera, or its owner is restarting: an empty frame
+            time.sleep(0.016)
+        return _EMPTY
+
     def frame_for(self, dev: str, key_frame_only: bool, peer: str = "") -> bytes:
         t0 = time.perf_counter()
+        if self.bus is not None:
+            return self._bus_frame(dev, key_frame_only, peer, t0)
         if not self.hub.has(dev):
             return _EMPTY
         try:
@@ -88,11 +139,7 @@ class ImageService:
                 r = self.hub.latest_frame_bytes(dev, after, WAIT_BLOCK_MS)
                 if r is not None:
                     seq, data, _meta = r
-                    self._set_cursor(peer, dev, seq)
-                    self.frames_served += 1
-                    self.latencies_ms.append((time.perf_counter() - t0) * 1e3)
-                    if len(self.latencies_ms) > 10000:
-                        del self.latencies_ms[:5000]
+                    self._served(peer, dev, seq, t0)
                     return data
                 time.sleep(0.016)
         except (CameraNotFound, WorkerRestarting):
@@ -223,14 +270,20 @@ def make_handler(svc: ImageService) -> grpc.GenericRpcHandler:
 
 
 def serve(svc: ImageService, address: str = "0.0.0.0:50001", workers: int = 64,
-          reuseport: bool = False) -> grpc.Server:
-    from .._native import native
+          reuseport: bool = False, handler: Optional[grpc.GenericRpcHandler] = None,
+          tune_malloc: bool = False) -> grpc.Server:
+    """Start the Image service on ``address``. ``workers`` handler threads (a VideoLatestImage
+    request holds one for up to 3 x 1 s of waiting). ``tune_malloc`` keeps frame-sized buffers in
+    the heap (native.tune_malloc_for_frames): worth it in a process that does nothing but serve
+    frames (the serving processes); off by default since it changes glibc's policy process-wide."""
+    if tune_malloc:
+        from .._native import native
 
-    native.tune_malloc_for_frames(64)  # every response allocates a frame-sized bytes object
+        native.tune_malloc_for_frames(64)
     opts = FRAME_CHANNEL_OPTS + [("grpc.so_reuseport", 1 if reuseport else 0)]
     server = grpc.server(futures.ThreadPoolExecutor(max_workers=workers), options=opts,
                          maximum_concurrent_rpcs=None)
-    server.add_generic_rpc_handlers((make_handler(svc),))
+    server.add_generic_rpc_handlers((handler or make_handler(svc),))
     port = server.add_insecure_port(address)
     if port == 0:
         raise RuntimeError(f"cannot bind gRPC server to {address}")

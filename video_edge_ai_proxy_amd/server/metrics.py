@@ -12,9 +12,10 @@ from prometheus_client.core import CounterMetricFamily, GaugeMetricFamily, Histo
 
 
 class HubCollector:
-    def __init__(self, hub, image_service=None):
+    def __init__(self, hub, image_service=None, frontends=None):
         self.hub = hub
         self.svc = image_service
+        self.frontends = frontends
 
     def collect(self):
         labels = ["camera", "device"]
@@ -64,8 +65,11 @@ class HubCollector:
         except Exception:  # noqa: BLE001 — metrics must never fail a scrape
             pass
         if self.svc is not None:
-            served = CounterMetricFamily("vep_grpc_frames_served", "VideoLatestImage frames sent")
-            served.add_metric([], self.svc.frames_served)
+            served = CounterMetricFamily("vep_grpc_frames_served", "VideoLatestImage frames sent",
+                                         labels=["process"])
+            served.add_metric(["main"], self.svc.frames_served)
+            if self.frontends is not None:
+                served.add_metric(["serving"], self.frontends.frames_served())
             yield served
             lat = list(self.svc.latencies_ms)
             if lat:
@@ -78,9 +82,9 @@ class HubCollector:
 
 
 class Metrics:
-    def __init__(self, hub, image_service=None):
+    def __init__(self, hub, image_service=None, frontends=None):
         self.registry = CollectorRegistry()
-        self.registry.register(HubCollector(hub, image_service))
+        self.registry.register(HubCollector(hub, image_service, frontends))
 
     def render(self):
         return generate_latest(self.registry), CONTENT_TYPE_LATEST
