@@ -292,6 +292,8 @@ class RtspFarm:
         """Switch the farm to real time and wait until the ingest backlog of the unthrottled run has
         drained (the decode rate has fallen to the cameras' frame rate)."""
         self.srv.set_pacing(1)
+        for sess in self.sessions:  # live cameras: the production (lossy) ingest
+            sess.set_lossless(False)
         deadline = time.perf_counter() + timeout_s
         target = self.cams * fps * 1.25
         while time.perf_counter() < deadline:
@@ -329,10 +331,15 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
     from video_edge_ai_proxy_amd.server.bench_latency import measure
 
     cams = a.cams_per_gpu
-    buf = torch.empty((cams, row), dtype=torch.uint8, device=dev)
+    # the worker letterboxes every published frame into the live rows; each step's all-gather
+    # reads a consistent snapshot of them (Worker.snapshot_consumer: ordered after the letterbox
+    # writes already enqueued, before any later one), double-buffered so the next snapshot never
+    # overwrites rows a gather in flight still reads
+    live = torch.zeros((cams, row), dtype=torch.uint8, device=dev)
     gather = world > 1 and not a.no_gather
-    gathered = torch.empty((world * cams, row), dtype=torch.uint8, device=dev) if gather else None
-    worker.set_consumer_buffers(buf.data_ptr(), 0, cams)
+    snaps = [torch.empty((cams, row), dtype=torch.uint8, device=dev) for _ in range(2)] if gather else None
+    gathered = [torch.empty((world * cams, row), dtype=torch.uint8, device=dev) for _ in range(2)] if gather else None
+    worker.set_consumer_buffers(live.data_ptr(), 0, cams)
 
     def sync():
         if use_gpu:
@@ -358,19 +365,23 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         p0, f0, d0, s0 = worker.pictures, worker.frames, worker.dropped, farm.stats()
         rg0 = worker.records_gathered
         g0 = worker.gpu_ms_total
-        handle = None
         hostprof = os.environ.get("VEP_HOSTPROF")  # path: SIGPROF samples of every thread, timed region
         if hostprof:
             vep.hostprof_start(1000)
+        handles = [None, None]
         t0 = time.perf_counter()
         for i in range(a.steps):
             farm.wait_pictures(p0 + cams * (i + 1))
             if gather:  # RCCL all-gather of the letterboxed consumer batch, overlapped with decode
-                if handle is not None:
-                    handle.wait()
-                handle = dist.all_gather_into_tensor(gathered, buf, async_op=True)
-        if handle is not None:
-            handle.wait()
+                b = i & 1
+                if handles[b] is not None:  # (a stream wait: the gather that last read snapshot b)
+                    handles[b].wait()
+                stream = torch.cuda.current_stream().cuda_stream if use_gpu else 0
+                worker.snapshot_consumer(snaps[b].data_ptr(), snaps[b].numel(), cams, stream)
+                handles[b] = dist.all_gather_into_tensor(gathered[b], snaps[b], async_op=True)
+        for h in handles:
+            if h is not None:
+                h.wait()
         sync()
         t1 = time.perf_counter()
         if world > 1:
@@ -407,9 +418,11 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                               device=dev)
             dist.all_reduce(fr, op=dist.ReduceOp.SUM)
             pictures, frames, dropped, errors, wire_bytes, aus, skipped = (int(v) for v in fr.tolist())
-        # latency: every rank's cameras go live (real-time farm), rank 0 measures
+        # latency: every rank's cameras go live (real-time farm) with the production ingest
+        # (lossy: a camera that outruns the decoder skips to its next keyframe), rank 0 measures
         if pool is not None or world > 1:
             settled = farm.go_live(a.fps)
+            ls0 = farm.stats()["skipped"]
             if world > 1:
                 dist.barrier()
             if pool is not None:
@@ -418,6 +431,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                               serve_samples=a.latency_samples)
                 live_fps = (worker.pictures - lp0) / (time.perf_counter() - lt0) / cams
                 lat["settled"] = settled
+                lat["live_skipped"] = farm.stats()["skipped"] - ls0
             if world > 1:
                 dist.barrier()
     finally:
@@ -468,6 +482,11 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "access_units_ingested": aus,
             "access_units_per_s": round(aus / elapsed, 1),
             "access_units_skipped": skipped,
+            "ingest_mode": {"timed_region": "lossless: a camera's socket is paused while its parse backlog is deep "
+                                            "(TCP back-pressure on the unthrottled farm), so no access unit is "
+                                            "skipped by construction",
+                            "latency_phase": "lossy (the production default): a camera that outruns its parse "
+                                             "drops to its next keyframe; live_phase_access_units_skipped counts them"},
             "frames_dropped": dropped,
             "decode_errors": errors,
             "concurrent_clients": a.clients,
@@ -484,6 +503,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         if lat is not None:
             res.update(latency_fields(a, lat, live_fps))
             res["latency_farm_settled"] = lat["settled"]
+            res["live_phase_access_units_skipped"] = lat["live_skipped"]
         res.update(side)  # (rank 0's side loads)
         print(json.dumps(res), flush=True)
     if world > 1:

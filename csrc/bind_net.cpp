@@ -217,5 +217,7 @@ void bind_net(py::module_& m) {
       .def("start", &IngestSession::start)
       .def("stop", &IngestSession::stop, py::call_guard<py::gil_scoped_release>())
       .def("state", [](IngestSession& s) { return state_dict(s.state()); })
+      .def("set_lossless", &IngestSession::set_lossless)
+      .def_property_readonly("lossless", &IngestSession::lossless)
       .def("log", &IngestSession::log);
 }

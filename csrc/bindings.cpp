@@ -1289,6 +1289,16 @@ PYBIND11_MODULE(_vep, m) {
            [](Worker& w, uintptr_t hwc, uintptr_t chw, int rows) {
              w.set_consumer_buffers(reinterpret_cast<u8*>(hwc), reinterpret_cast<void*>(chw), rows);
            })
+      .def("snapshot_consumer",
+           // Consistent copy of consumer rows [0, rows) into dst (device pointer on a GPU worker),
+           // enqueued on `stream` (a hipStream_t as int, e.g. torch.cuda.current_stream().cuda_stream;
+           // 0 = wait on the host): after every letterbox write already enqueued, before any later.
+           [](Worker& w, uintptr_t dst, size_t cap, int rows, uintptr_t stream) {
+             py::gil_scoped_release nogil;
+             return w.snapshot_consumer(reinterpret_cast<void*>(dst), cap, rows, reinterpret_cast<hipStream_t>(stream));
+           },
+           py::arg("dst"), py::arg("cap"), py::arg("rows"), py::arg("stream") = 0)
+      .def_property_readonly("snapshots", &Worker::snapshots)
       .def("wait_frame",
            // Block (GIL released) until the camera publishes a frame with seq > after.
            [](Worker& w, int i, i64 after, int timeout_ms) {

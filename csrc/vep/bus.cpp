@@ -67,6 +67,17 @@ void* map_file(const std::string& path, size_t bytes, bool create, bool writable
 
 bool pid_alive(int pid) { return pid > 0 && (::kill(pid, 0) == 0 || errno == EPERM); }
 
+u64 inode_of(const std::string& path) {
+  struct stat st;
+  return ::stat(path.c_str(), &st) == 0 ? u64(st.st_ino) : 0;
+}
+
+// unlink `path` only if it is still the file this process created (inode `ino`): another owner
+// with the same name may have replaced it since
+void unlink_own(const std::string& path, u64 ino) {
+  if (ino && inode_of(path) == ino) ::unlink(path.c_str());
+}
+
 }  // namespace
 
 size_t control_bytes(int max_cams) {
@@ -118,6 +129,7 @@ Owner::Owner(const std::string& tag, int owner, int max_cams) : tag_(clean_tag(t
   std::atomic_thread_fence(std::memory_order_release);
   hdr_->magic = kMagic;
   VEP_CHECK(::rename(tmp.c_str(), path_.c_str()) == 0, "bus: cannot publish " + path_);
+  ino_ = inode_of(path_);
   data_.resize(size_t(max_cams));
   synced_query_.assign(size_t(max_cams), 0);
   synced_kf_.assign(size_t(max_cams), kUnset);
@@ -129,7 +141,7 @@ Owner::~Owner() {
   for (size_t i = 0; i < data_.size(); ++i) release_data(int(i));
   if (hdr_) {
     ::munmap(hdr_, bytes_);
-    ::unlink(path_.c_str());
+    unlink_own(path_, ino_);
   }
 }
 
@@ -199,7 +211,7 @@ void Owner::release_data(int cam) {
   if (!d.base) return;
   if (d.pinned && w_) w_->unregister_host(d.base);
   ::munmap(d.base, d.bytes);
-  ::unlink(d.path.c_str());  // readers that still map it keep their mapping
+  unlink_own(d.path, d.ino);  // readers that still map it keep their mapping
   d = Data{};
 }
 
@@ -217,6 +229,7 @@ bool Owner::ensure_data(int cam, size_t slot_cap) {
   void* p = map_file(nd.path, nd.bytes, true, true);
   if (!p) return false;
   nd.base = static_cast<u8*>(p);
+  nd.ino = inode_of(nd.path);
   nd.pinned = w_ && w_->register_host(nd.base, nd.bytes);
   d = nd;
   for (auto& s : e.slots) {

@@ -107,6 +107,7 @@ class Owner {
     u8* base = nullptr;
     size_t bytes = 0;
     bool pinned = false;
+    u64 ino = 0;
   };
   void pump();
   void on_publish(int cam, i64 seq);
@@ -115,6 +116,7 @@ class Owner {
   std::string tag_;
   int owner_;
   std::string path_;
+  u64 ino_ = 0;
   Header* hdr_ = nullptr;
   size_t bytes_ = 0;
   Worker* w_ = nullptr;

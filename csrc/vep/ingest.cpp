@@ -89,7 +89,7 @@ constexpr size_t kHighWater = 32, kLowWater = 8;
 
 bool IngestSession::backlogged() const {
   const u64 key = parse_key_.load(std::memory_order_relaxed);
-  return cfg_.lossless && pooled_ && key && svc_->parse.depth(key) >= kHighWater;
+  return lossless_.load(std::memory_order_relaxed) && pooled_ && key && svc_->parse.depth(key) >= kHighWater;
 }
 
 bool IngestSession::drained() const {
@@ -99,7 +99,9 @@ bool IngestSession::drained() const {
 
 IngestSession::IngestSession(Worker& w, int cam, IngestConfig cfg,
                              std::shared_ptr<mux::Archiver> archiver)
-    : w_(w), cam_(cam), cfg_(std::move(cfg)), archiver_(std::move(archiver)) {}
+    : w_(w), cam_(cam), cfg_(std::move(cfg)), archiver_(std::move(archiver)) {
+  lossless_.store(cfg_.lossless);
+}
 
 IngestSession::~IngestSession() { stop(); }
 
@@ -276,7 +278,7 @@ void IngestSession::decode(const std::shared_ptr<Camera>& cam, const AuPtr& au) 
   }
   // parse off the socket thread, in order, on the camera's strand of the shared parse pool
   const u64 key = u64(reinterpret_cast<uintptr_t>(cam.get()));
-  if (cfg_.lossless) {
+  if (lossless_.load(std::memory_order_relaxed)) {
     // never drop: on_readable pauses the socket above the high-water mark
   } else if (drop_to_key_) {
     if (!au->keyframe) {
@@ -291,8 +293,8 @@ void IngestSession::decode(const std::shared_ptr<Camera>& cam, const AuPtr& au) 
     return;
   }
   parse_key_.store(key, std::memory_order_relaxed);
-  std::weak_ptr<Handler> wh;
-  if (cfg_.lossless) {
+  std::weak_ptr<Handler> wh;  // (always: a socket paused in lossless mode resumes even after
+  {                           // set_lossless(false))
     std::lock_guard<std::mutex> g(handler_mu_);
     wh = handler_;
   }

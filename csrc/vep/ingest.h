@@ -112,6 +112,9 @@ class IngestSession {
   void stop();
   SessionState state() const;
   const IngestConfig& config() const { return cfg_; }
+  // Switch lossless ingest (IngestConfig::lossless) on or off while running.
+  void set_lossless(bool on) { lossless_.store(on, std::memory_order_relaxed); }
+  bool lossless() const { return lossless_.load(std::memory_order_relaxed); }
   void log(bool err, const std::string& s);
   bool pooled() const { return pooled_; }
 
@@ -140,6 +143,7 @@ class IngestSession {
   // touches the camera) and the strand key they were posted under.
   std::shared_ptr<std::atomic<bool>> parse_live_;
   std::atomic<u64> parse_key_{0};
+  std::atomic<bool> lossless_{false};
   Worker& w_;
   int cam_;
   IngestConfig cfg_;

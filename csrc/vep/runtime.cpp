@@ -5,6 +5,8 @@
 #include <array>
 #include <chrono>
 #include <cmath>
+#include <csignal>
+#include <cstdio>
 #include <thread>
 
 #include "color.h"
@@ -148,7 +150,17 @@ std::string LogRing::dump(bool err, size_t last) const {
 // ------------------------------------------------------------------------------------ Camera
 
 Camera::Camera(Worker& w, int index, std::string name, int ring_slots)
-    : ring_slots_cfg(ring_slots), w_(w), index_(index), name_(std::move(name)), use_vcn_(w.vcn()) {}
+    : ring_slots_cfg(ring_slots), w_(w), index_(index), name_(std::move(name)), use_vcn_(w.vcn()) {
+  // Fault injection (tests of per-camera-group containment): VEP_FAULT_CAMERA=<name>[:<n>] makes
+  // this camera's n-th access unit (default 1) crash the process inside its parse, as a bug in
+  // the bitstream parser hit by a hostile stream would.
+  if (const char* f = std::getenv("VEP_FAULT_CAMERA")) {
+    const std::string spec(f);
+    const size_t colon = spec.rfind(':');
+    const std::string who = colon == std::string::npos ? spec : spec.substr(0, colon);
+    if (who == name_) fault_after_ = colon == std::string::npos ? 1 : std::max<u64>(1, std::strtoull(f + colon + 1, nullptr, 10));
+  }
+}
 
 std::vector<AuPtr> Camera::gop_snapshot() {
   std::lock_guard<std::mutex> g(mu_);
@@ -348,7 +360,13 @@ bool Camera::on_access_unit(const AuPtr& au) {
   DecodeJob job;
   {
     std::lock_guard<std::mutex> g(mu_);
-    packets.fetch_add(1, std::memory_order_relaxed);
+    const u64 np = packets.fetch_add(1, std::memory_order_relaxed) + 1;
+    if (fault_after_ && np >= fault_after_) {  // (VEP_FAULT_CAMERA, see the constructor)
+      std::fprintf(stderr, "vep: injected fault in camera %s's parse (access unit %llu)\n", name_.c_str(),
+                   static_cast<unsigned long long>(np));
+      std::fflush(stderr);
+      std::raise(SIGSEGV);
+    }
     bytes_in.fetch_add(au->bytes(), std::memory_order_relaxed);
     last_packet_ms.store(au->arrival_ms ? au->arrival_ms : now_ms());
     if (au->keyframe) {
@@ -574,7 +592,9 @@ Worker::~Worker() {
     }
     if (ln.stream && ln.stream != stream_) (void)hipStreamDestroy(ln.stream);
     if (ln.copy) (void)hipStreamDestroy(ln.copy);
+    if (ln.snap_mark) (void)hipEventDestroy(ln.snap_mark);
   }
+  if (snap_ev_) (void)hipEventDestroy(snap_ev_);
   for (auto& b : serve_all_) {
     dev_.free_pinned(b->h);
     for (hipEvent_t e : b->ev)
@@ -1780,6 +1800,12 @@ void Worker::launch_on(Lane& ln, Batch&& b) {
   st.cons_chw = b.cons_chw;
   st.cons_rows = b.cons_rows;
   try {
+    std::shared_lock<std::shared_mutex> gate(cons_gate_);
+    const u64 sg = snap_gen_.load();
+    if (ln.snap_seen != sg) {  // this batch's letterbox writes wait for the last snapshot's copy
+      VEP_HIP(hipStreamWaitEvent(ln.stream, snap_ev_, 0));
+      ln.snap_seen = sg;
+    }
     launch_gpu(ln, st);
   } catch (...) {
     // the batch is dropped: give its ring slots back and count it as published
@@ -2068,6 +2094,36 @@ bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, siz
     if (ring->still_valid(slot, meta->seq)) return true;
   }
   return false;
+}
+
+size_t Worker::snapshot_consumer(void* dst, size_t cap, int rows, hipStream_t stream) {
+  VEP_CHECK(opt_.letterbox_size > 0 && cons_hwc_, "consumer batch disabled (letterbox_size is 0)");
+  rows = std::clamp(rows, 0, cons_rows_);
+  const size_t n = size_t(rows) * gpu::letterbox_bytes(opt_.letterbox_size, opt_.letterbox_format);
+  VEP_CHECK(cap >= n, "snapshot_consumer destination too small");
+  if (!n) return 0;
+  if (!dev_.gpu()) {  // CPU backend: rows are written by launch_async (under launch_mu_)
+    std::lock_guard<std::mutex> g(launch_mu_);
+    std::memcpy(dst, cons_hwc_, n);
+    snap_gen_.fetch_add(1);
+    return n;
+  }
+  std::unique_lock<std::shared_mutex> gate(cons_gate_);  // no lane enqueues meanwhile
+  dev_.bind();
+  if (!snap_ev_) {
+    VEP_HIP(hipEventCreateWithFlags(&snap_ev_, hipEventDisableTiming));
+    for (auto& lp : lanes_) VEP_HIP(hipEventCreateWithFlags(&lp->snap_mark, hipEventDisableTiming));
+  }
+  const hipStream_t s = stream ? stream : serve_stream_;
+  for (auto& lp : lanes_) {  // after every letterbox write enqueued so far
+    VEP_HIP(hipEventRecord(lp->snap_mark, lp->stream));
+    VEP_HIP(hipStreamWaitEvent(s, lp->snap_mark, 0));
+  }
+  VEP_HIP(hipMemcpyAsync(dst, cons_hwc_, n, hipMemcpyDeviceToDevice, s));
+  VEP_HIP(hipEventRecord(snap_ev_, s));  // ... and before any later one (launch_on waits on it)
+  snap_gen_.fetch_add(1);
+  if (!stream) VEP_HIP(hipStreamSynchronize(s));
+  return n;
 }
 
 void Worker::read_latest_many(std::vector<ReadReq>& reqs) {

@@ -16,6 +16,7 @@
 #include <functional>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <thread>
 
 #include "avc.h"
@@ -221,6 +222,7 @@ class Camera {
   // VCN backend: one rocDecode session per camera, created on the first keyframe
   bool use_vcn_ = false;
   std::unique_ptr<vcn::Session> vcn_;
+  u64 fault_after_ = 0;  // VEP_FAULT_CAMERA: crash on this access unit (0 = never)
 };
 
 struct WorkerOptions {
@@ -316,6 +318,13 @@ class Worker {
   // RCCL all-gather); row r belongs to camera index r. Takes effect from the next batch.
   void set_consumer_buffers(u8* hwc, void* chw, int rows);
   u8* consumer_hwc() const { return cons_hwc_; }
+  // Consistent copy of consumer rows [0, rows) into dst (device memory on the GPU): ordered after
+  // every letterbox write already enqueued on any lane and before any later one, without a host
+  // wait. `stream` is the caller's (e.g. torch's current stream, so a collective enqueued next on
+  // it reads whole rows: no row is half one frame, half the next); 0 = wait on the host. Reading
+  // the live rows instead races the lanes' next letterbox writes. Returns the bytes copied.
+  size_t snapshot_consumer(void* dst, size_t cap, int rows, hipStream_t stream);
+  u64 snapshots() const { return snap_gen_.load(); }
   void* consumer_chw() const { return cons_chw_; }
   hipStream_t compute_stream() const { return stream_; }  // lane 0
   int lanes() const { return int(lanes_.size()); }
@@ -385,6 +394,8 @@ class Worker {
     std::deque<Batch> q;
     bool busy = false, drain = false, stop = false;
     std::deque<u64> unpublished;   // sequences given to this lane, not yet published (pub_mu_)
+    u64 snap_seen = 0;             // consumer snapshots this lane's stream already waits for
+    hipEvent_t snap_mark = nullptr;  // recorded by snapshot_consumer: the lane's enqueued work
   };
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
   void launch_gpu(Lane& ln, Stage& st);
@@ -441,6 +452,11 @@ class Worker {
   std::vector<ServeBuf*> serve_free_;
   u8* cons_hwc_ = nullptr;
   void* cons_chw_ = nullptr;
+  // consumer snapshots: exclusive while a snapshot is enqueued, shared while a lane enqueues a
+  // batch (its letterbox writes must come after the last snapshot's copy)
+  std::shared_mutex cons_gate_;
+  hipEvent_t snap_ev_ = nullptr;
+  std::atomic<u64> snap_gen_{0};
   bool owns_cons_ = true;
   int cons_rows_ = 0;
   // live queue

@@ -216,3 +216,105 @@ def test_isolated_hub_eight_worker_processes(native, tmp_path):
     finally:
         hub.shutdown()
         srv.stop()
+
+
+def test_camera_group_fault_containment(native, tmp_path, monkeypatch):
+    """gpu.workers_per_gpu = 2: two worker processes share the device, each owning a camera
+    group. A crash inside one camera's bitstream parse (VEP_FAULT_CAMERA, injected into the first
+    worker processes only) ends only its group's process: the other group's cameras keep serving
+    throughout, and the crashed group restarts and comes back (its cameras running and serving
+    again). Reference: one restart-always container per camera
+    (server/services/rtsp_process_manager.go:70-81)."""
+    from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
+
+    srv = farm(native, 4)
+    monkeypatch.setenv("VEP_FAULT_CAMERA", "c1:45")  # c1's 45th access unit (~1.5 s in)
+    cfg = _isolated_cfg(tmp_path, 0)
+    cfg.gpu.workers_per_gpu = 2
+    cfg.gpu.idle_cutoff_ms = 10000
+    hub = ProcessHub(cfg, devices=[-1], supervise_interval_s=0.2)
+    try:
+        assert len(hub._children) == 2
+        names = [f"c{i}" for i in range(4)]
+        for n in names:
+            hub.start_camera(n, f"rtsp://127.0.0.1:{srv.port}/{n}")
+        group = {n: hub.handle(n).worker_index for n in names}
+        bad = group["c1"]
+        others = [n for n in names if group[n] != bad]
+        assert others and len(others) < len(names)
+        victim = hub.state("c1")["worker_pid"]
+        seqs = {n: 0 for n in others}
+        deadline = time.time() + 60
+        while time.time() < deadline and hub.child_restarts[bad] == 0:
+            for n in others:  # the other group keeps serving while c1's group crashes
+                r = wait_frames(hub, n, timeout=5, after=seqs[n])
+                assert r is not None, f"{n} stopped serving"
+                seqs[n] = r[0]
+            time.sleep(0.05)
+        assert hub.child_restarts[bad] == 1, "the crashed camera group was not restarted"
+        assert hub.state("c1")["worker_pid"] != victim
+        assert all(hub.state(n)["worker_pid"] != victim for n in others)
+        assert hub.child_restarts[1 - bad] == 0
+        for n in names:  # every camera serves again, the crashed group's on its fresh process
+            assert wait_frames(hub, n, timeout=30) is not None, n
+            assert hub.state(n)["running"], n
+    finally:
+        hub.shutdown()
+        srv.stop()
+
+
+def test_rank_killed_during_gathers(native, tmp_path):
+    """A worker process killed while consumer gathers run: the gathers in flight fail (gloo fails
+    fast; RCCL survivors are aborted by the next group formation instead of waiting out the
+    collective timeout), the survivor keeps serving its camera throughout, and once the dead rank
+    is restarted the group is re-formed and the batch is whole again."""
+    import threading
+
+    from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
+
+    S = 16
+    srv = farm(native, 2)
+    hub = ProcessHub(_isolated_cfg(tmp_path, S), devices=[-1, -1], supervise_interval_s=0.2)
+    try:
+        for i in range(2):
+            hub.start_camera(f"c{i}", f"rtsp://127.0.0.1:{srv.port}/c{i}")
+        names = ["c0", "c1"]
+        _settle(hub, names)
+        hub.consumer_batch(names=names)
+        stop, outcomes = threading.Event(), []
+
+        def gathers():
+            while not stop.is_set():
+                try:
+                    hub.consumer_batch(names=names)
+                    outcomes.append("ok")
+                except Exception as e:  # noqa: BLE001
+                    outcomes.append(type(e).__name__)
+                    time.sleep(0.05)
+
+        th = threading.Thread(target=gathers, daemon=True)
+        th.start()
+        time.sleep(0.3)
+        victim_i = hub.handle("c1").worker_index
+        os.kill(hub.state("c1")["worker_pid"], signal.SIGKILL)
+        survivor = hub.handle("c0").worker_index
+        seq = 0
+        deadline = time.time() + 60
+        while time.time() < deadline and hub.child_restarts[victim_i] == 0:
+            r = wait_frames(hub, "c0", timeout=5, after=seq)  # the survivor keeps its camera
+            assert r is not None
+            seq = r[0]
+        assert hub.child_restarts[victim_i] == 1 and hub.child_restarts[survivor] == 0
+        _settle(hub, names)
+        n_ok = outcomes.count("ok")
+        deadline = time.time() + 60
+        while time.time() < deadline and outcomes.count("ok") <= n_ok:
+            time.sleep(0.1)
+        stop.set()
+        th.join(timeout=30)
+        assert outcomes.count("ok") > n_ok, outcomes[-10:]
+        batch, order = hub.consumer_batch(names=names)
+        _check_rows(hub, batch, names, S)
+    finally:
+        hub.shutdown()
+        srv.stop()

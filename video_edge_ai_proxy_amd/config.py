@@ -67,6 +67,11 @@ class GpuConfig:
                                                  # worker process per GPU, engine/isolated.py)
     decoder: str = "native"                      # native (CPU parse + gfx950 reconstruction) |
                                                  # vcn (rocDecode on the video core) | auto
+    workers_per_gpu: int = 1                     # process isolation: worker processes per GPU, each
+                                                 # owning a camera group (a crash costs 1/k of the
+                                                 # GPU's cameras)
+    consumer_rate_hz: float = 0.0                # >0: gather the node's consumer batch this often
+                                                 # and hand it to consumer_hook (engine/consumer.py)
     consumer_hook: str = ""                      # process isolation: "module:function" each
                                                  # worker process calls with every gathered
                                                  # node batch (fn(batch, names, rank), on its GPU)

@@ -55,14 +55,30 @@ class RankGroup:
             mod, _, fn = hook.partition(":")
             self.hook = getattr(importlib.import_module(mod), fn)
         self.gathers = 0
+        self.gather_ms: list[float] = []  # per gather, this rank: snapshot + collectives
 
-    def form(self, epoch: int, port: int, rank: int, world: int, timeout_s: float = 60.0) -> dict:
+    def abort(self) -> dict:
+        """Abort this rank's communicator (a collective pending on it fails at once): the parent
+        does this before re-forming the group, instead of waiting for the collective's timeout."""
+        import torch.distributed as dist
+        from torch.distributed import distributed_c10d as c10d
+
+        if dist.is_initialized():
+            try:
+                c10d._abort_process_group()
+            except Exception:  # noqa: BLE001 — fall back to a plain teardown
+                dist.destroy_process_group()
+        self.epoch = -1
+        return {"aborted": True}
+
+    def form(self, epoch: int, port: int, rank: int, world: int, timeout_s: float = 60.0,
+             backend: str = "") -> dict:
         import torch
         import torch.distributed as dist
 
         if dist.is_initialized():
-            dist.destroy_process_group()
-        backend = "nccl" if self.device >= 0 else "gloo"
+            self.abort()
+        backend = backend or ("nccl" if self.device >= 0 else "gloo")
         if self.device >= 0:
             torch.cuda.set_device(self.device)
         dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world,
@@ -70,39 +86,74 @@ class RankGroup:
         self.epoch, self.rank, self.world, self.backend = epoch, rank, world, backend
         return {"rank": rank, "world": world, "backend": backend}
 
-    def gather(self, epoch: int, names: list, k: int, order: list, perm: list, slot=None) -> dict:
-        """All-gather ``k`` consumer rows per rank (this rank's ``names``, zero-padded); reorder
-        the node batch by ``perm`` into the caller's camera ``order``. Every rank enters the
-        collective, whatever went wrong before it (a missing camera reads as a zero row), so one
-        bad request cannot leave the other ranks waiting."""
+    def _local_rows(self, names: list, k: int, src):
+        """This rank's k rows: a consistent snapshot of the worker's live consumer rows
+        (Worker.snapshot_consumer, ordered on the current stream), zero rows for cameras it no
+        longer has. Returns (rows, missing)."""
         import torch
-        import torch.distributed as dist
 
-        if epoch != self.epoch:
-            raise RuntimeError(f"gather for group epoch {epoch}, this rank is in {self.epoch}")
         hub = self.hub
-        src = hub.consumer[0]
         local = torch.zeros((k, *src.shape[1:]), dtype=src.dtype, device=src.device)
-        missing = []
-        rows, at = [], []
+        missing, rows, at = [], [], []
         for j, n in enumerate(names):
             try:
                 rows.append(hub.handle(n).cam)
                 at.append(j)
             except KeyError:
                 missing.append(n)
-        if src.is_cuda:
-            torch.cuda.synchronize(src.device)  # the letterbox kernels of published frames
         if rows:
-            local[torch.tensor(at, device=src.device)] = src.index_select(0, torch.tensor(rows, device=src.device))
-        out = torch.empty((self.world * k, *src.shape[1:]), dtype=src.dtype, device=src.device)
-        dist.all_gather_into_tensor(out, local)
+            snap = hub.snapshot(0, max(rows) + 1)
+            local[torch.tensor(at, device=src.device)] = snap.index_select(0, torch.tensor(rows, device=src.device))
+        return local, missing
+
+    def gather(self, epoch: int, names: list, k: int, order: list, perm: list, slot=None) -> dict:
+        """All-gather ``k`` consumer rows per rank (this rank's ``names``, zero-padded); reorder
+        the node batch by ``perm`` into the caller's camera ``order``.
+
+        Every rank of the group enters both collectives whatever went wrong locally (a missing
+        camera or a failed snapshot reads as zero rows and sets this rank's error flag), so one bad
+        request never leaves the other ranks waiting; a small header collective carries every
+        rank's (epoch, error) so all ranks agree on whether the batch is whole. A rank that is not
+        in group `epoch` at all (restarted meanwhile) cannot join it: it fails at once, and the
+        parent aborts the survivors' communicators before re-forming."""
+        import time
+
+        import torch
+        import torch.distributed as dist
+
+        if epoch != self.epoch:
+            raise RuntimeError(f"gather for group epoch {epoch}, this rank is in {self.epoch}")
+        t0 = time.perf_counter()
+        src = self.hub.consumer[0]
+        err = ""
+        try:
+            local, missing = self._local_rows(names, k, src)
+        except Exception as e:  # noqa: BLE001 — still join the collectives, with zero rows
+            err = f"{type(e).__name__}: {e}"
+            local = torch.zeros((k, *src.shape[1:]), dtype=src.dtype, device=src.device)
+            missing = list(names)
+        cdev = src.device if self.backend == "nccl" or not src.is_cuda else torch.device("cpu")
+        hdr = torch.tensor([epoch, 1 if err else 0], dtype=torch.int64, device=cdev)
+        hdrs = torch.empty((self.world * 2,), dtype=torch.int64, device=cdev)
+        dist.all_gather_into_tensor(hdrs, hdr)
+        out = torch.empty((self.world * k, *src.shape[1:]), dtype=src.dtype, device=cdev)
+        dist.all_gather_into_tensor(out, local.to(cdev))
         batch = out.index_select(0, torch.tensor(perm, dtype=torch.long, device=out.device))
-        self.batch = (batch, list(order))
+        hs = hdrs.view(self.world, 2).tolist()
+        if src.is_cuda:
+            torch.cuda.current_stream(src.device).synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+        self.gather_ms.append(ms)
+        if len(self.gather_ms) > 4096:
+            del self.gather_ms[:2048]
+        rank_errors = [r for r, (e, f) in enumerate(hs) if f or e != epoch]
         self.gathers += 1
-        if self.hook is not None:
-            self.hook(batch, list(order), self.rank)
-        res = {"rank": self.rank, "missing": missing, "shape": list(batch.shape)}
+        if not rank_errors:
+            self.batch = (batch, list(order))
+            if self.hook is not None:
+                self.hook(batch, list(order), self.rank)
+        res = {"rank": self.rank, "missing": missing, "shape": list(batch.shape), "error": err,
+               "rank_errors": rank_errors, "gather_ms": ms}
         if slot is not None:
             nbytes = batch.numel() * batch.element_size()
             slot.ensure(max(nbytes, 1))
@@ -134,12 +185,14 @@ def _serve(hub, group: RankGroup, conn, stop: threading.Event) -> None:
                     res = {"cam": h.cam}
                 elif method == "group_form":
                     res = group.form(*args, **kwargs)
+                elif method == "group_abort":
+                    res = group.abort()
                 elif method == "consumer_gather":
                     to_host = kwargs.pop("to_host", False)
                     res = group.gather(*args, slot=slot if to_host else None, **kwargs)
                 elif method == "group_info":
                     res = {"epoch": group.epoch, "rank": group.rank, "world": group.world, "gathers": group.gathers,
-                           "backend": group.backend}
+                           "backend": group.backend, "gather_ms": list(group.gather_ms[-256:])}
                 elif method in EXPORTED:
                     res = getattr(hub, method)(*args, **kwargs)
                 else:

@@ -26,6 +26,13 @@ log = logging.getLogger("vep.hub")
 _CHW = {"none": 0, "fp16": 1, "bf16": 2, "fp32": 3}
 
 
+def new_bus_tag() -> str:
+    """A frame-bus tag unique to one hub instance on this node (pid + random suffix)."""
+    import secrets
+
+    return f"n{os.getpid()}{secrets.token_hex(3)}"
+
+
 class CameraNotFound(KeyError):
     pass
 
@@ -87,6 +94,8 @@ class Hub:
                 t = torch.zeros((int(g.max_cameras_per_gpu), *shape), dtype=torch.uint8, device=dev)
                 w.set_consumer_buffers(t.data_ptr(), 0, int(g.max_cameras_per_gpu))
                 self.consumer.append(t)
+        self._snaps: list = [None] * len(self.consumer)
+        self._cons_lock = threading.Lock()  # one consumer batch at a time (shared snapshot tensors)
         # Frame bus (cfg.bus_tag set: serving processes read frames from shared memory): one owner
         # per worker, index bus_owner + k; the pump DMAs a camera's newest frame on demand.
         self.bus = []
@@ -163,8 +172,6 @@ class Hub:
         copies over xGMI (one process, many GPUs; the multi-process form is
         ``parallel.ConsumerBatch``, one RCCL all-gather). Rows of cameras that have not published
         a frame yet are zero."""
-        import torch
-
         from ..parallel import gather_to_device
 
         if not self.consumer:
@@ -174,17 +181,23 @@ class Hub:
             hs = [self.handle(n) for n in order]
         if device is None:
             device = self.consumer[0].device
-        # the letterbox kernels of every frame published so far have finished on each GPU
-        for t in self.consumer:
-            if t.is_cuda:
-                torch.cuda.synchronize(t.device)
+        with self._cons_lock:
+            return self._consumer_batch(hs, order, device, gather_to_device)
+
+    def _consumer_batch(self, hs, order, device, gather_to_device):
+        import torch
+
         parts, where = [], []
         for wi, t in enumerate(self.consumer):
             mine = [(k, h.cam) for k, h in enumerate(hs) if h.worker_index == wi]
             if not mine:
                 continue
+            # a consistent snapshot of the rows in use (the lanes keep letterboxing into the
+            # live rows; reading them directly could catch a row mid-rewrite), on the current
+            # stream: the row selection below is ordered after it without a host wait
+            snap = self.snapshot(wi, max(c for _, c in mine) + 1)
             idx = torch.tensor([c for _, c in mine], dtype=torch.long, device=t.device)
-            parts.append(t.index_select(0, idx))
+            parts.append(snap.index_select(0, idx))
             where += [k for k, _ in mine]
         if not parts:
             return torch.zeros((0, *self.consumer[0].shape[1:]), dtype=torch.uint8, device=device), []
@@ -192,6 +205,20 @@ class Hub:
         inv = torch.empty(len(where), dtype=torch.long)
         inv[torch.tensor(where, dtype=torch.long)] = torch.arange(len(where))
         return cat.index_select(0, inv.to(cat.device)), order
+
+    def snapshot(self, wi: int, rows: int):
+        """Consistent copy of worker wi's consumer rows [0, rows) (Worker.snapshot_consumer) into
+        a per-worker snapshot tensor, enqueued on the device's current stream."""
+        import torch
+
+        t = self.consumer[wi]
+        if self._snaps[wi] is None:
+            self._snaps[wi] = torch.empty_like(t)
+        snap = self._snaps[wi]
+        stream = torch.cuda.current_stream(t.device).cuda_stream if t.is_cuda else 0
+        n = snap[:rows].numel()
+        self.workers[wi].snapshot_consumer(snap.data_ptr(), n, rows, stream)
+        return snap[:rows]
 
     def shutdown(self) -> None:
         for name in list(self.cameras):
@@ -201,6 +228,7 @@ class Hub:
                 pass
         for o in self.bus:
             o.stop()
+        self.bus = []  # (unlinks the segments now, not at garbage collection)
         for w in self.workers:
             w.stop()
         self.archiver.flush()

@@ -47,7 +47,7 @@ from multiprocessing.connection import Client
 from typing import Optional
 
 from ..config import Config
-from .hub import CameraExists, CameraHandle, CameraNotFound, place_camera
+from .hub import CameraExists, CameraHandle, CameraNotFound, new_bus_tag, place_camera
 from .shm import ShmReader, remove_segments
 
 log = logging.getLogger("vep.isolated")
@@ -65,10 +65,12 @@ _ERRORS = {"CameraNotFound": CameraNotFound, "CameraExists": CameraExists, "KeyE
 
 class _Child:
     def __init__(self, device: int, cfg_json: str, nconn: int = 4, start_timeout_s: float = 180.0,
-                 owner: int = 0):
+                 owner: int = 0, first_start: bool = True):
         self.device = device
         key = secrets.token_bytes(16)
         env = dict(os.environ, VEP_CHILD_KEY=key.hex())
+        if not first_start:  # injected faults (VEP_FAULT_CAMERA) hit the first process only
+            env.pop("VEP_FAULT_CAMERA", None)
         env["PYTHONPATH"] = _PKG_PARENT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "video_edge_ai_proxy_amd.engine.child", "--device", str(device),
@@ -95,6 +97,11 @@ class _Child:
         self.free: queue.Queue = queue.Queue()
         for _ in range(nconn):  # (connection, reader of its shared-memory segment)
             self.free.put((Client(("127.0.0.1", self.port), authkey=key), ShmReader()))
+        # collectives (group_form / consumer_gather) travel on a connection of their own: a
+        # collective stuck on a dead peer holds only it, and the parent can still reach this
+        # child over the pool above to abort it (group_abort) before re-forming the group
+        self.gconn = (Client(("127.0.0.1", self.port), authkey=key), ShmReader())
+        self.glock = threading.Lock()
         threading.Thread(target=self._drain, daemon=True).start()  # stray stdout never blocks it
 
     def _drain(self) -> None:
@@ -129,6 +136,30 @@ class _Child:
             return r[1]
         raise _ERRORS.get(r[1], RuntimeError)(r[2])
 
+    def call_group(self, method: str, *args, read=None, **kwargs):
+        """A collective call on the dedicated connection. Fails at once (no queueing behind it)
+        when this child's previous collective has not returned."""
+        if not self.alive():
+            raise WorkerRestarting(f"worker process for device {self.device} is restarting")
+        if not self.glock.acquire(blocking=False):
+            raise RuntimeError(f"worker process for device {self.device}: previous collective still pending")
+        conn, shm = self.gconn
+        try:
+            conn.send((method, args, kwargs))
+            r = conn.recv()
+            if r[0] == "ok" and read is not None:
+                r = ("ok", read(r[1], shm))
+        except (EOFError, OSError) as e:
+            raise WorkerRestarting(f"worker process for device {self.device} died: {e}") from e
+        finally:
+            self.glock.release()
+        if r[0] == "ok":
+            return r[1]
+        raise _ERRORS.get(r[1], RuntimeError)(r[2])
+
+    def group_pending(self) -> bool:
+        return self.glock.locked()
+
     def close_pipes(self) -> None:
         while True:  # unmap the shared-memory segments and drop the connections
             try:
@@ -140,6 +171,11 @@ class _Child:
                 conn.close()
             except Exception:  # noqa: BLE001
                 pass
+        try:
+            self.gconn[1].close()
+            self.gconn[0].close()
+        except Exception:  # noqa: BLE001
+            pass
         for f in (self.proc.stdin, self.proc.stdout):
             try:
                 if f is not None:
@@ -207,9 +243,11 @@ class ProcessHub:
         self.cfg = cfg
         if devices is None:
             devices = list(cfg.gpu.devices) if cfg.gpu.devices else _count_gpus()
-        self.devices = devices or [-1]
+        # one child per (GPU, camera group): gpu.workers_per_gpu children share each device
+        k = max(1, int(getattr(cfg.gpu, "workers_per_gpu", 1)))
+        self.devices = [d for d in (devices or [-1]) for _ in range(k)]
         if not cfg.bus_tag:  # the children publish their frames on the node's frame bus
-            cfg.bus_tag = f"n{os.getpid()}"
+            cfg.bus_tag = new_bus_tag()
         self._cfg_json = json.dumps(dataclasses.asdict(cfg))
         from .._native import native
 
@@ -234,8 +272,11 @@ class ProcessHub:
         self._group_ok = False
         self._group_lock = threading.Lock()
         self._gather_lock = threading.Lock()
-        self._pool = ThreadPoolExecutor(max_workers=max(2, len(self.devices)), thread_name_prefix="vep-group")
+        # (2 x ranks: a gather's calls and the next form's can both be outstanding; a call into a
+        # child whose collective is still pending fails fast instead of waiting for a thread)
+        self._pool = ThreadPoolExecutor(max_workers=max(2, 2 * len(self.devices)), thread_name_prefix="vep-group")
         self.group_timeout_s = 60.0
+        self.gather_ms: list[float] = []  # steady-state gathers (max over ranks), no group formation
         self._stop = threading.Event()
         self._sup = threading.Thread(target=self._supervise, args=(supervise_interval_s,), daemon=True,
                                      name="vep-supervisor")
@@ -265,7 +306,7 @@ class ProcessHub:
         remove_segments(dead.pid)  # and the segments it could not unlink itself
         _remove_bus_segments(dead.pid)
         self._group_ok = False  # the survivors' group lost a rank: re-form before the next gather
-        child = _Child(self.devices[i], self._cfg_json, owner=i)
+        child = _Child(self.devices[i], self._cfg_json, owner=i, first_start=False)
         try:
             with self._lock:
                 mine = [n for n, h in self.cameras.items() if h.worker_index == i]
@@ -337,8 +378,9 @@ class ProcessHub:
 
     # ------------------------------------------------------------------ rank group / consumer batch
     def _on_all(self, method: str, per_child_args: list, **kwargs) -> list:
-        """Call ``method`` on every child concurrently (collectives need all ranks at once)."""
-        futs = [self._pool.submit(self._children[i].call, method, *per_child_args[i], **kwargs)
+        """Collective ``method`` on every child concurrently (all ranks must enter at once), each
+        on the child's collective connection."""
+        futs = [self._pool.submit(self._children[i].call_group, method, *per_child_args[i], **kwargs)
                 for i in range(len(self._children))]
         out, err = [], None
         for f in futs:
@@ -356,11 +398,28 @@ class ProcessHub:
         with self._group_lock:
             if not all(c.alive() for c in self._children):
                 raise WorkerRestarting("a worker process is restarting")
+            # survivors of a failed collective may still be blocked in it: abort their
+            # communicators (over the control pool) so the collective connections come free
+            for c in self._children:
+                if c.group_pending():
+                    try:
+                        c.call("group_abort")
+                    except Exception as e:  # noqa: BLE001
+                        log.warning("group abort on device %s failed: %s", c.device, e)
+            deadline = time.time() + self.group_timeout_s
+            while any(c.group_pending() for c in self._children):
+                if time.time() > deadline:
+                    raise RuntimeError("a worker's collective did not return after the abort")
+                time.sleep(0.05)
             self._group_epoch += 1
             port = _free_port()
             world = len(self._children)
+            # RCCL needs one rank per GPU: with several worker processes per GPU (or CPU
+            # workers) the group runs on gloo
+            gpus = [d for d in self.devices if d >= 0]
+            backend = "nccl" if gpus and len(set(gpus)) == len(self.devices) else "gloo"
             try:
-                self._on_all("group_form", [(self._group_epoch, port, r, world, self.group_timeout_s)
+                self._on_all("group_form", [(self._group_epoch, port, r, world, self.group_timeout_s, backend)
                                             for r in range(world)])
             except Exception:
                 self._group_ok = False
@@ -368,7 +427,7 @@ class ProcessHub:
             self._group_ok = True
             return self._group_epoch
 
-    def consumer_batch(self, device=None, names=None, copy: bool = True):
+    def consumer_batch(self, device=None, names=None, copy: bool = True, to_host: bool = True):
         """Node-wide letterboxed batch of the newest frame of every running camera (or of
         ``names``, in that order): ``(tensor [N, S, S, 3] uint8 (or NV12 rows), names)``.
 
@@ -376,7 +435,9 @@ class ProcessHub:
         every rank's GPU — where ``gpu.consumer_hook`` consumers receive it — and the rank of
         ``device`` (default: the first) DMAs it into shared memory, returned here as a CPU tensor
         (``copy=False``: a view of the segment, valid until the next call; this process never
-        touches a GPU). Rows of cameras that have not published a frame yet are zero."""
+        touches a GPU). Rows of cameras that have not published a frame yet are zero.
+        ``to_host=False``: gather on the ranks only (their consumer hooks get the batch), return
+        (None, names)."""
         if int(self.cfg.gpu.letterbox_size) <= 0:
             raise RuntimeError("consumer batch disabled (gpu.letterbox_size is 0)")
         with self._lock:
@@ -389,7 +450,7 @@ class ProcessHub:
             per[h.worker_index].append(h.name)
         k = max(1, max(len(p) for p in per))
         perm = [r * k + j for r, j in pos]
-        dst = 0 if device is None else self.devices.index(device)
+        dst = (0 if device is None else self.devices.index(device)) if to_host else -1
         with self._gather_lock:  # one collective at a time, in the same order on every rank
             return self._gather(per, k, order, perm, dst, copy)
 
@@ -414,8 +475,8 @@ class ProcessHub:
         futs = []
         for r in range(world):
             kw = dict(to_host=(r == dst))
-            futs.append(self._pool.submit(self._children[r].call, "consumer_gather", epoch, per[r], k, order, perm,
-                                          read=read if r == dst else None, **kw))
+            futs.append(self._pool.submit(self._children[r].call_group, "consumer_gather", epoch, per[r], k, order,
+                                          perm, read=read if r == dst else None, **kw))
         results, err = [], None
         for f in futs:
             try:
@@ -426,7 +487,14 @@ class ProcessHub:
         if err is not None:
             self._group_ok = False  # a failed collective may have left the group unusable
             raise err
-        return results[dst]["tensor"], order
+        bad = results[0].get("rank_errors") or []
+        if bad:  # every rank joined, but some sent zero rows: not a whole batch
+            raise RuntimeError(f"consumer gather: ranks {bad} failed locally: "
+                               f"{[results[r].get('error') for r in bad if results[r]]}")
+        self.gather_ms.append(max(r["gather_ms"] for r in results))
+        if len(self.gather_ms) > 4096:
+            del self.gather_ms[:2048]
+        return (results[dst]["tensor"] if dst >= 0 else None), order
 
     def shutdown(self) -> None:
         self._stop.set()

@@ -74,20 +74,31 @@ def init_distributed(backend: Optional[str] = None) -> tuple[int, int, int]:
 
 
 class ConsumerBatch:
-    """Double-buffered ``[cams, S, S, 3]`` uint8 letterboxed batch owned by torch, written by a
-    native Worker's letterbox kernel, gathered across ranks with one RCCL all-gather.
+    """``[cams, S, S, 3]`` uint8 letterboxed batch (or NV12 rows) gathered across ranks with one
+    RCCL all-gather.
 
-    Gathering the uint8 HWC tensor (1.2 MB per 640x640 camera) instead of the normalised
-    fp16/bf16 CHW tensor halves the xGMI bytes; consumers normalise after the gather (fused into
-    their first op, or via :func:`video_edge_ai_proxy_amd.ops.letterbox` style kernels)."""
+    The native Worker letterboxes every frame it publishes into its *live* rows (``self.live``)
+    on its lane streams, whenever that camera's batch runs. A gather therefore never reads the
+    live rows directly — a lane's next letterbox kernel could rewrite a row while the collective
+    reads it (a row half one frame, half the next). ``gather()`` first takes a snapshot
+    (``Worker.snapshot_consumer``: a device copy enqueued on the current stream after every
+    letterbox write already enqueued, and before any later one — the lanes wait on its event, the
+    host never does) into one of two snapshot buffers, then all-gathers that. The next gather uses
+    the other buffer after making the stream wait for the collective that last read it, so a
+    gather in flight is never overwritten.
+
+    Gathering the uint8 HWC tensor (1.2 MB per 640x640 camera; NV12 0.6 MB) instead of the
+    normalised fp16/bf16 CHW tensor halves the xGMI bytes; consumers normalise after the gather."""
 
     def __init__(self, worker, cams: int, size: int, device: torch.device, world: int = 1,
                  fmt: str = "bgr"):
         self.worker = worker
         self.cams, self.size, self.world, self.fmt = cams, size, world, fmt
+        self.device = device
         shape = (size * size * 3 // 2,) if fmt == "nv12" else (size, size, 3)
-        self.bufs = [torch.zeros((cams, *shape), dtype=torch.uint8, device=device)
-                     for _ in range(2)]
+        self.live = torch.zeros((cams, *shape), dtype=torch.uint8, device=device)
+        worker.set_consumer_buffers(self.live.data_ptr(), 0, cams)
+        self.bufs = [torch.zeros((cams, *shape), dtype=torch.uint8, device=device) for _ in range(2)]
         # a process group of any size (a 1-rank RCCL group included) gathers through the
         # collective; without one the local batch is the node batch
         self.collective = world > 1 or (dist.is_available() and dist.is_initialized())
@@ -97,25 +108,26 @@ class ConsumerBatch:
         self.tick = 0
 
     def prepare(self) -> torch.Tensor:
-        """Point the worker at the buffer for the next tick (waits if it still feeds a gather)."""
-        b = self.tick & 1
-        h = self.handles[b]
-        if h is not None:
-            h.wait()
-            self.handles[b] = None
-            if self.bufs[b].is_cuda:
-                torch.cuda.current_stream(self.bufs[b].device).synchronize()
-        self.worker.set_consumer_buffers(self.bufs[b].data_ptr(), 0, self.cams)
-        return self.bufs[b]
+        """The live rows the worker letterboxes into (kept for callers of the round-2 API; the
+        rows are written in place, nothing to switch)."""
+        return self.live
+
+    def _stream(self) -> int:
+        return torch.cuda.current_stream(self.device).cuda_stream if self.live.is_cuda else 0
 
     def gather(self, async_op: bool = True):
-        """All-gather the tick's batch. Returns (tensor, work)."""
-        self.worker.complete_all()  # the tick's letterbox kernels must have finished
+        """Snapshot the live rows and all-gather them. Returns (tensor, work)."""
         b = self.tick & 1
+        h = self.handles[b]
+        if h is not None:  # the collective that last read snapshot b (a stream wait on RCCL)
+            h.wait()
+            self.handles[b] = None
+        snap = self.bufs[b]
+        self.worker.snapshot_consumer(snap.data_ptr(), snap.numel(), self.cams, self._stream())
         self.tick += 1
         if not self.collective:
-            return self.bufs[b], None
-        w = dist.all_gather_into_tensor(self.out[b], self.bufs[b], async_op=async_op)
+            return snap, None
+        w = dist.all_gather_into_tensor(self.out[b], snap, async_op=async_op)
         self.handles[b] = w if async_op else None
         return self.out[b], w
 

@@ -14,7 +14,7 @@ from dataclasses import dataclass
 from typing import Optional
 
 from ..config import Config, load_config
-from ..engine.hub import Hub
+from ..engine.hub import Hub, new_bus_tag
 from ..services.annotation import AnnotationConsumer, AnnotationQueue
 from ..services.cron import start_cron_jobs
 from ..services.edge import EdgeService
@@ -46,6 +46,7 @@ class HubApp:
     metrics: Metrics
     frontends: Optional[object] = None  # server.frontend.FrontendPool (serving.frontends > 0)
     public_grpc_port: int = 0
+    consumer: Optional[object] = None   # engine.consumer.ConsumerLoop (gpu.consumer_rate_hz > 0)
 
     @property
     def grpc_port(self) -> int:
@@ -69,6 +70,8 @@ class HubApp:
                 self.rest_thread.join(timeout=5)
         for j in self.cron:
             j.stop()
+        if self.consumer is not None:
+            self.consumer.stop()
         self.queue.stop()
         self.hub.shutdown()
         self.storage.close()
@@ -88,7 +91,7 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
         nfront = max(1, len(devices if devices is not None else (cfg.gpu.devices or _gpu_count())))
     use_bus = nfront > 0 or cfg.gpu.isolation == "process" or cfg.serving.bus
     if use_bus and not cfg.bus_tag:
-        cfg.bus_tag = f"n{os.getpid()}"
+        cfg.bus_tag = new_bus_tag()
     frontends, control = None, None
     if nfront > 0:
         from .frontend import FrontendPool
@@ -137,6 +140,11 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
     happ = HubApp(cfg, storage, hub, pm, settings, edge, queue, consumer, image, gsrv,
                   rest_server, rest_thread, cron, metrics, frontends, gport if frontends is not None else 0)
     happ._rest_port = rport  # type: ignore[attr-defined]
+    if float(cfg.gpu.consumer_rate_hz) > 0 and int(cfg.gpu.letterbox_size) > 0:
+        from ..engine.consumer import ConsumerLoop
+
+        happ.consumer = ConsumerLoop(hub, float(cfg.gpu.consumer_rate_hz), cfg.gpu.consumer_hook).start()
+        metrics.consumer = happ.consumer
     if restore:
         restored = pm.restore()
         if restored:

@@ -16,6 +16,7 @@ class HubCollector:
         self.hub = hub
         self.svc = image_service
         self.frontends = frontends
+        self.consumer = None  # engine.consumer.ConsumerLoop
 
     def collect(self):
         labels = ["camera", "device"]
@@ -64,6 +65,19 @@ class HubCollector:
             yield pool
         except Exception:  # noqa: BLE001 — metrics must never fail a scrape
             pass
+        if self.consumer is not None:
+            st = self.consumer.stats()
+            cg = CounterMetricFamily("vep_consumer_gathers", "node consumer batches gathered")
+            cg.add_metric([], st["gathers"])
+            ce = CounterMetricFamily("vep_consumer_errors", "node consumer batches that failed")
+            ce.add_metric([], st["errors"])
+            yield from (cg, ce)
+            if st["gather_ms_p50"] is not None:
+                g = GaugeMetricFamily("vep_consumer_gather_ms", "steady-state gather time per batch",
+                                      labels=["quantile"])
+                g.add_metric(["0.5"], st["gather_ms_p50"])
+                g.add_metric(["0.99"], st["gather_ms_p99"])
+                yield g
         if self.svc is not None:
             served = CounterMetricFamily("vep_grpc_frames_served", "VideoLatestImage frames sent",
                                          labels=["process"])
@@ -84,7 +98,16 @@ class HubCollector:
 class Metrics:
     def __init__(self, hub, image_service=None, frontends=None):
         self.registry = CollectorRegistry()
-        self.registry.register(HubCollector(hub, image_service, frontends))
+        self.collector = HubCollector(hub, image_service, frontends)
+        self.registry.register(self.collector)
+
+    @property
+    def consumer(self):
+        return self.collector.consumer
+
+    @consumer.setter
+    def consumer(self, loop):
+        self.collector.consumer = loop
 
     def render(self):
         return generate_latest(self.registry), CONTENT_TYPE_LATEST

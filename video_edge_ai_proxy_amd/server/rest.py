@@ -128,10 +128,13 @@ def create_app(pm: ProcessManager, sm: SettingsManager, metrics=None) -> FastAPI
     def healthz():
         from .._native import native
 
-        return {"ok": True, "cameras": len(pm.hub.cameras), "devices": pm.hub.devices,
-                "decoder_backends": [w.decoder for w in pm.hub.workers],
-                "vcn_available": bool(native.rocdecode_available()),
-                "direct_host_reads": [bool(w.direct_reads) for w in pm.hub.workers]}
+        out = {"ok": True, "cameras": len(pm.hub.cameras), "devices": pm.hub.devices,
+               "decoder_backends": [w.decoder for w in pm.hub.workers],
+               "vcn_available": bool(native.rocdecode_available()),
+               "direct_host_reads": [bool(w.direct_reads) for w in pm.hub.workers]}
+        if metrics is not None and metrics.consumer is not None:
+            out["consumer"] = metrics.consumer.stats()
+        return out
 
     @app.get("/metrics")
     def prom():
