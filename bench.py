@@ -72,6 +72,9 @@ def parse_args():
                     help="per-frame sensor noise (default: 1.5 main/high -> ~3.9 Mbit/s at 1080p30, "
                          "1.0 baseline -> ~4.5 Mbit/s)")
     ap.add_argument("--refs", type=int, default=1, help="max_num_ref_frames of the compressed streams")
+    ap.add_argument("--slices", type=int, default=0,
+                    help="slices per picture of the synthetic streams (0: 8 for 4K H.265 — config 5 — else 1); "
+                         "the independent slices of an H.265 picture are parsed in parallel")
     ap.add_argument("--threads", type=int, default=0,
                     help="host parse threads per rank (0 = CPU budget / local ranks - 1, at most 15)")
     ap.add_argument("--parse-window", type=int, default=8,
@@ -120,6 +123,8 @@ def parse_args():
         ap.error("--rtmp / --annotate need --source rtsp")
     if a.qp is None:
         a.qp = 27 if a.profile == "baseline" else 25
+    if a.slices <= 0:
+        a.slices = 8 if a.codec == "h265" and a.width * a.height >= 3840 * 2160 else 1
     if a.temporal_noise is None:
         a.temporal_noise = 1.0 if a.profile == "baseline" else 1.5
     return a
@@ -127,7 +132,7 @@ def parse_args():
 
 def start_client_pool(a):
     """Latency clients in fresh processes, started before this process touches the GPU."""
-    from video_edge_ai_proxy_amd.server.latency_clients import ClientPool
+    from vep_bench.latency_clients import ClientPool
     from video_edge_ai_proxy_amd.utils import host_cpu_budget
 
     if a.clients <= 0 and a.latency_samples <= 0:
@@ -139,7 +144,7 @@ def start_client_pool(a):
 
 def latency_fields(a, lat, live_fps=None):
     """The JSON latency block of bench_latency.measure() results."""
-    from video_edge_ai_proxy_amd.server.bench_latency import summarize
+    from vep_bench.bench_latency import summarize
 
     def r3(x):
         return round(x, 3) if x is not None else None
@@ -188,7 +193,7 @@ def spawn_ranks(n: int) -> int:
 def describe_streams(a, compressed):
     if compressed and a.codec == "h265":
         return (f"HEVC Main CABAC I/P/B, {a.bframes} B per mini-GOP, CTB 32, merge/AMVP/TMVP, "
-                "deblocking")
+                f"deblocking, {a.slices} slice{'s' if a.slices > 1 else ''} per picture")
     if compressed and a.profile == "baseline":
         return "Baseline CAVLC I/P"
     if compressed:
@@ -203,6 +208,7 @@ def make_cfg(vep, a, rank, compressed):
     cfg.width, cfg.height, cfg.fps, cfg.gop, cfg.motion = a.width, a.height, a.fps, a.gop, a.motion
     cfg.codec = a.codec
     cfg.seed = 1 + rank * 100003
+    cfg.slices = a.slices
     if compressed:
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
@@ -328,7 +334,7 @@ def avc_cycles_per_mb(worker) -> dict:
 def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed, pool):
     """`--source rtsp`: the timed loop waits for the live pipeline (loopback RTSP farm ->
     IngestSession -> lazy decoder -> Worker batches) to decode `cams` more pictures per step."""
-    from video_edge_ai_proxy_amd.server.bench_latency import measure
+    from vep_bench.bench_latency import measure
 
     cams = a.cams_per_gpu
     # the worker letterboxes every published frame into the live rows; each step's all-gather
@@ -354,7 +360,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
     side = {}
     try:
         if a.annotate:  # (runs from the warmup on: the counts cover warmup + timed region)
-            from video_edge_ai_proxy_amd.server.bench_pipeline import AnnotationLoad
+            from vep_bench.bench_pipeline import AnnotationLoad
 
             annot = AnnotationLoad([f"r{rank}rtsp{i}" for i in range(cams)], rate=a.annotate_rate)
             annot.start()
@@ -675,7 +681,7 @@ def main():
 
     lat = None
     if pool is not None:
-        from video_edge_ai_proxy_amd.server.bench_latency import measure, ticking
+        from vep_bench.bench_latency import measure, ticking
 
         # cameras decode at their frame rate meanwhile; the single-process tick must not touch
         # the collective: decode-only ticks here

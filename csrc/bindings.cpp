@@ -426,7 +426,8 @@ PYBIND11_MODULE(_vep, m) {
     hevc::Decoder d;
     std::vector<HostSurface> slots;
     u64 pictures = 0, pus = 0, tus = 0, intra_tus = 0, max_level = 0, exchange_violations = 0;
-    HevcRecords() { d.set_gpu_mode(true); }
+    bool execute = true;  // false: parse only (records are counted, not executed: parse timing)
+    explicit HevcRecords(bool ex = true) : execute(ex) { d.set_gpu_mode(true); }
     py::list frames(const std::vector<hevc::FramePtr>& fs) {
       py::list l;
       for (const auto& f : fs) {
@@ -455,7 +456,7 @@ PYBIND11_MODULE(_vep, m) {
         if (slots.size() < size_t(d.gpu_slots())) slots.resize(size_t(d.gpu_slots()));
         for (auto& h : slots)
           if (h.coded_w != sw || h.coded_h != sh) h.alloc(sw, sh);
-        hevc::cpu_execute(*p, slots);
+        if (execute) hevc::cpu_execute(*p, slots);
         ++pictures;
         pus += p->pus.size();
         tus += p->tus.size();
@@ -467,7 +468,7 @@ PYBIND11_MODULE(_vep, m) {
     int coded_w_ = 0, coded_h_ = 0;
   };
   py::class_<HevcRecords>(m, "HevcRecordsDecoder")
-      .def(py::init<>())
+      .def(py::init<bool>(), py::arg("execute") = true)
       .def("decode",
            [](HevcRecords& r, const AccessUnit& au) {
              std::vector<hevc::FramePtr> fs;

@@ -24,6 +24,7 @@
 // is tested bit-exact against the reference decoder.
 #define VEP_KERNEL_SOURCE 1  // descriptors' pointers are global-address-space here (gpu.h)
 #include <algorithm>
+#include <cstdlib>
 
 #include "gpu.h"
 #include "hevc_kern.h"
@@ -513,7 +514,11 @@ void launch_hevc_tu_queue(const HevcDesc* d_descs, const HevcTuRange* d_ranges, 
   if (nranges <= 0 || count <= 0 || !ctr) return;
   // persistent waves: a fraction of the chip (4 per workgroup) — the other lanes' kernels run
   // beside it, and waves that run far ahead of the wavefront only poll. Windows: a wave per block.
-  const int wgs = persistent ? std::min((count + 3) / 4, kTuQueueWgs) : (count + 3) / 4;
+  static const int queue_wgs = [] {
+    const char* e = std::getenv("VEP_HEVC_TU_QUEUE_WGS");
+    return e ? std::clamp(std::atoi(e), 1, 65536) : kTuQueueWgs;
+  }();
+  const int wgs = persistent ? std::min((count + 3) / 4, queue_wgs) : (count + 3) / 4;
   hipLaunchKernelGGL(hevc_tu_queue_kernel, dim3(wgs), dim3(256), 0, s, d_descs, d_ranges, nranges, base, base + count,
                      ctr, persistent ? 1 : 0);
 }

@@ -95,10 +95,18 @@ class CtuLayer {
   static constexpr bool kWrite = E::kW;
 
   CtuLayer(PicCtx& pc, int si, E& e, CtuDecider* dec)
-      : pc_(pc), si_(si), sl_(pc.slices[size_t(si)]), sh_(sl_.sh), sps_(*pc.sps), pps_(*pc.pps), e_(e), dec_(dec) {
+      : pc_(pc), si_(si), sl_(pc.slices[size_t(si)]), sh_(sl_.sh), sps_(*pc.sps), pps_(*pc.pps), e_(e), dec_(dec),
+        g_(pc.gpu), st_(&pc.stats), bypass_(&pc.any_bypass) {
     slice_qp_ = sl_.qp;
     qp_last_ = slice_qp_;
     log2_min_qg_ = sps_.log2_ctb - (pps_.cu_qp_delta ? pps_.diff_cu_qp_delta_depth : 0);
+  }
+
+  // Outputs into a slice's own shard instead of the picture (parallel slices).
+  void use_shard(SliceShard& sh) {
+    g_ = pc_.gpu ? &sh.g : nullptr;
+    st_ = &sh.stats;
+    bypass_ = &sh.any_bypass;
   }
 
   cabac::Decoder* rd = nullptr;  // (read mode: PCM samples, re-initialisation)
@@ -110,8 +118,10 @@ class CtuLayer {
   void ctu(int addr, bool last) {
     const int rx = addr % pc_.wctb, ry = addr / pc_.wctb;
     const int x0 = rx << sps_.log2_ctb, y0 = ry << sps_.log2_ctb;
-    pc_.slice[size_t(addr)] = u16(si_);
-    pc_.sord[size_t(addr)] = u16(sl_.ord);
+    if (!pc_.prefilled) {
+      pc_.slice[size_t(addr)] = u16(si_);
+      pc_.sord[size_t(addr)] = u16(sl_.ord);
+    }
     if (sh_.sao_luma || sh_.sao_chroma) sao(rx, ry);
     quadtree(x0, y0, sps_.log2_ctb, 0);
     const u32 end = e_.term(last ? 1u : 0u);
@@ -291,7 +301,7 @@ class CtuLayer {
       u8* const m_byp = pc_.bypass.data();
       const u8 bv = u8(cu_.bypass);
       for4(x0, y0, n, n, [=](size_t k) { m_byp[k] = bv; });
-      if (cu_.bypass) pc_.any_bypass = true;
+      if (cu_.bypass) *bypass_ = true;
     }
     bool skip = false;
     if (sh_.slice_type != kI) {
@@ -309,7 +319,7 @@ class CtuLayer {
       u8* const m_intra = pc_.intra.data();
       for4(x0, y0, n, n, [=](size_t k) { m_intra[k] = 0; });
       prediction_unit(x0, y0, n, n, 0, 0, want.pu[0], true);
-      ++pc_.stats.skip;
+      ++st_->skip;
     } else {
       intra = sh_.slice_type == kI ? true : bin(kCtxPredMode, want.intra) != 0;
       cu_.intra = intra;
@@ -324,10 +334,10 @@ class CtuLayer {
           pcm = e_.term(want.pcm ? 1u : 0u) != 0;
         if (pcm) {
           pcm_sample(x0, y0, log2, want.pcm_samples);
-          ++pc_.stats.pcm;
+          ++st_->pcm;
         } else {
           intra_modes(x0, y0, log2, part, want);
-          ++pc_.stats.intra;
+          ++st_->intra;
         }
       } else {
         u8* const m_intra = pc_.intra.data();
@@ -335,8 +345,8 @@ class CtuLayer {
         int r[4][4];
         const int np = pu_rects(part, n, r);
         for (int k = 0; k < np; ++k) prediction_unit(x0 + r[k][0], y0 + r[k][1], r[k][2], r[k][3], k, part, want.pu[k], false);
-        ++pc_.stats.inter;
-        if (part >= 4) ++pc_.stats.amp;
+        ++st_->inter;
+        if (part >= 4) ++st_->amp;
       }
     }
     if (!cu_.intra) predict_inter_cu();
@@ -411,7 +421,7 @@ class CtuLayer {
       VEP_CHECK(pos + bytes <= data_n, "PCM samples past the end of the slice");
       src = data + pos;
       rd->start(pos + bytes);
-      if (GpuPicture* g = pc_.gpu) {  // records mode: the GPU copies the samples (level 0)
+      if (GpuPicture* g = g_) {  // records mode: the GPU copies the samples (level 0)
         GpuTu t{};
         t.x = u16(x0);
         t.y = u16(y0);
@@ -544,7 +554,7 @@ class CtuLayer {
         m.mv[l][0] = c[idx].mv[l][0];
         m.mv[l][1] = c[idx].mv[l][1];
       }
-      ++pc_.stats.merge;
+      ++st_->merge;
       if (partIdx == 0) cu_.merge0 = true;
     } else {
       int dir = 1;
@@ -599,7 +609,7 @@ class CtuLayer {
           m.mv[l][c] = i16(u >= 32768 ? u - 65536 : u);
         }
       }
-      if (dir == 3) ++pc_.stats.bi;
+      if (dir == 3) ++st_->bi;
     }
     {
       MvField* const m_mf = pc_.mf.data();
@@ -647,7 +657,7 @@ class CtuLayer {
           e.o[l][c] = i16(w.o[l][m.ref[l]][c]);
         }
     }
-    std::vector<GpuWp>& tab = pc_.gpu->wp;
+    std::vector<GpuWp>& tab = g_->wp;
     for (size_t i = 0; i < tab.size(); ++i)
       if (std::memcmp(&tab[i], &e, sizeof e) == 0) return u8(i + 1);
     VEP_CHECK(tab.size() < 255, "HEVC: more than 255 distinct prediction weights in one picture");
@@ -656,7 +666,7 @@ class CtuLayer {
   }
 
   void predict_inter_cu() {
-    if (GpuPicture* g = pc_.gpu) {  // records mode: one record per prediction block
+    if (GpuPicture* g = g_) {  // records mode: one record per prediction block
       for (int k = 0; k < cu_.npu; ++k) {
         const int x = cu_.pus[k][0], y = cu_.pus[k][1];
         const MvField& m = pc_.mf[pc_.i4(x, y)];
@@ -860,7 +870,7 @@ class CtuLayer {
   // -------------------------------------------------------------------- intra prediction
   void intra_pred_block(int c, int x0, int y0, int log2) {
     // x0, y0 in the component's samples
-    if (pc_.gpu) {
+    if (g_) {
       gpu_intra_refs(c, x0, y0, log2);
       return;
     }
@@ -998,7 +1008,7 @@ class CtuLayer {
       }
       if constexpr (kWrite) residual_coding(c, log2, lv, tskip);
       else nnz = residual_coding_rd(c, log2, lv, tskip, nzbuf_);
-      if (tskip) ++pc_.stats.tskip;
+      if (tskip) ++st_->tskip;
     }
     bool nz = false;
     if constexpr (kWrite) {
@@ -1007,7 +1017,7 @@ class CtuLayer {
     } else {
       nz = nnz > 0;
     }
-    if (GpuPicture* g = pc_.gpu) {  // records mode: the GPU predicts / transforms / adds
+    if (GpuPicture* g = g_) {  // records mode: the GPU predicts / transforms / adds
       if (nz) cbf_nonzero_ = true;
       if (!nz && !cu_.intra) return;
       GpuTu t{};
@@ -1518,6 +1528,9 @@ class CtuLayer {
   std::vector<int> lvbuf_;  // one transform block's levels
   int gpu_level_ = 1;
   std::map<TuKey, TuLevels> levels_;
+  GpuPicture* g_;         // records (the picture's, or the slice shard's)
+  Decoder::Stats* st_;
+  bool* bypass_;
 };
 
 void init_ctx(cabac::Ctx* ctx, const SliceHeader& sh, int qp) {
@@ -1576,22 +1589,27 @@ bool substream_boundary(const PicCtx& pc, int rs, int next_rs) {
 
 }  // namespace
 
-void decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos) {
+int decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos, SliceShard* shard) {
   SliceInfo& sl = pc.slices[size_t(slice_idx)];
   cabac::Ctx ctx[kCtxCount];
   cabac::Decoder dec(data, n, bytepos);
   RD e{dec, ctx};
   CtuLayer<RD> L(pc, slice_idx, e, nullptr);
+  if (shard) L.use_shard(*shard);
   L.rd = &dec;
   L.data = data;
   L.data_n = n;
   const int total = pc.wctb * pc.hctb;
   int ts = pc.rs2ts[size_t(sl.sh.segment_address)];
+  int ctus = 0;
   start_ctu_state(pc, sl, ctx, L, sl.sh.segment_address, true);
   for (;;) {
     const int rs = pc.ts2rs[size_t(ts)];
-    VEP_CHECK(pc.slice[size_t(rs)] == 0xFFFF, "HEVC: CTU decoded twice");
+    // (prefilled: the CTU must lie in this segment's range, filled in before the slices ran)
+    VEP_CHECK(pc.prefilled ? pc.slice[size_t(rs)] == u16(slice_idx) : pc.slice[size_t(rs)] == 0xFFFF,
+              "HEVC: CTU decoded twice");
     L.ctu(rs, false);
+    ++ctus;
     const bool end = L.end_of_slice();
     end_ctu_state(pc, ctx, L, rs, end);
     if (end) break;
@@ -1605,6 +1623,8 @@ void decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size
       start_ctu_state(pc, sl, ctx, L, next, false);
     }
   }
+  if (shard) shard->ctus = ctus;
+  return ctus;
 }
 
 void encode_slice_data(PicCtx& pc, int slice_idx, std::vector<u8>& out, CtuDecider& dec, int first_ts, int end_ts,

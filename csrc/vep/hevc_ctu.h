@@ -64,6 +64,10 @@ struct PicCtx {
   Decoder::Stats stats;
   // records mode (GPU reconstruction): the CTU layer emits work instead of samples
   GpuPicture* gpu = nullptr;
+  // Independent slices parsed in parallel (Decoder): `slice` / `sord` are filled for the whole
+  // picture before the slices run, so no CTU writes them and every availability test reads a
+  // value that does not change while other slices are being decoded.
+  bool prefilled = false;
   std::vector<u16> lvl_y, lvl_c;  // intra dependency level of each 4x4 block's samples
 
   void init(const Sps& sp, const Pps& pp, HostSurface* surf) {
@@ -129,11 +133,14 @@ struct PicCtx {
   // picture, same slice, already decoded.
   bool avail(int x, int y, int xn, int yn, const std::vector<u8>& flag) const {
     if (xn < 0 || yn < 0 || xn >= W || yn >= H) return false;
-    if (!flag[i4(xn, yn)]) return false;
-    // a decoded block of a single-slice, single-tile picture is in the current block's slice
-    if (!multi) return true;
-    const size_t a = size_t(ctb_of(xn, yn)), b = size_t(ctb_of(x, y));
-    return sord[a] == sord[b] && tile[a] == tile[b];
+    // a decoded block of a single-slice, single-tile picture is in the current block's slice;
+    // otherwise the slice / tile test comes first, so the decoded flag is only read for blocks of
+    // the current slice (another slice's may be written concurrently: parallel slices)
+    if (multi) {
+      const size_t a = size_t(ctb_of(xn, yn)), b = size_t(ctb_of(x, y));
+      if (sord[a] != sord[b] || tile[a] != tile[b]) return false;
+    }
+    return flag[i4(xn, yn)] != 0;
   }
 };
 
@@ -150,10 +157,21 @@ struct CtuDecider {
   ResidualFn residual;
 };
 
+// Outputs of one slice decoded in parallel with the picture's other slices (Decoder): merged
+// into the picture in slice order afterwards, so the records equal a sequential parse's.
+struct SliceShard {
+  GpuPicture g;               // records mode: the slice's tus / pus / coefs / pcm / wp
+  Decoder::Stats stats;
+  bool any_bypass = false;
+  int ctus = 0;               // CTUs the slice decoded
+};
+
 // Walk (decode or encode + reconstruct) the CTUs of one slice segment. `data` / `n`: the slice
 // NAL RBSP (read mode); `out`: the RBSP being written (write mode, slice header already in it,
-// byte aligned).
-void decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos);
+// byte aligned). `shard`: the slice's own outputs (parallel slices, see SliceShard). Returns the
+// number of CTUs decoded.
+int decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos,
+                      SliceShard* shard = nullptr);
 // Write mode: CTUs [first_ts, end_ts) in tile scan. `out` receives the slice segment data only;
 // `substreams` (when given) the byte offsets in `out` where each further WPP row / tile
 // substream starts (entry points, before emulation prevention).

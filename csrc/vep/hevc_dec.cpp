@@ -3,8 +3,10 @@
 // layer (hevc_ctu.cpp), the in-loop filters and output in POC order with the bumping process of
 // C.5.2. See hevc_dec.h for the supported feature set.
 #include <algorithm>
+#include <cstring>
 
 #include "bits.h"
+#include "fanout.h"
 #include "hevc_ctu.h"
 #include "hevc_recon.h"
 
@@ -32,7 +34,9 @@ void check_supported(const Sps& sps, const Pps& pps) {
 }
 }  // namespace
 
-Decoder::Decoder() : pc_(std::make_unique<PicCtx>()), gpu_pool_(Recycler<GpuPicture>::make(12)) {}
+Decoder::Decoder() : pc_(std::make_unique<PicCtx>()), gpu_pool_(Recycler<GpuPicture>::make(12)) {
+  if (const char* e = std::getenv("VEP_HEVC_SLICE_THREADS")) parallel_slices_ = e[0] != '0';
+}
 Decoder::~Decoder() = default;
 
 void Decoder::bump(std::vector<FramePtr>& out) {
@@ -172,6 +176,11 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   pps_act_ = &pps;
   pc_->init(sps, pps, &cur_->s);
   pc_->poc = poc;
+  pc_->prefilled = false;
+  deferred_.clear();
+  // independent slices in parallel: no WPP (rows share contexts) and no dependent segments
+  // (decode_slice switches deferral off when one arrives)
+  defer_ = parallel_slices_ && !pps.entropy_coding_sync && FanOut::shared().size() > 0;
   if (gpu_mode_) {
     cur_gpu_ = gpu_pool_->acquire([](GpuPicture& g) {  // default state, capacities kept
       GpuPicture fresh;
@@ -226,6 +235,8 @@ void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
       si.list_lt[l] = p.list_lt[l];
     }
     pc_->slices.push_back(std::move(si));
+    run_deferred(false);  // (a dependent segment continues the previous one's contexts: sequential)
+    defer_ = false;
     decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
     return;
   }
@@ -257,10 +268,104 @@ void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
     }
   }
   pc_->slices.push_back(std::move(si));
+  if (defer_) {  // kept until the picture's last slice: then every slice runs in parallel
+    const size_t k = deferred_.size();
+    if (slice_rbsp_.size() <= k) slice_rbsp_.resize(k + 1);
+    slice_rbsp_[k].assign(rbsp, rbsp + n);
+    deferred_.push_back({pc_->slices.size() - 1, n, sh.data_bytepos});
+    return;
+  }
   decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
 }
 
+void Decoder::run_deferred(bool parallel) {
+  if (deferred_.empty()) return;
+  std::vector<std::array<size_t, 3>> work;
+  work.swap(deferred_);
+  PicCtx& pc = *pc_;
+  if (work.size() == 1 || !parallel) {  // the sequential path, nothing to merge
+    for (size_t k = 0; k < work.size(); ++k)
+      decode_slice_data(pc, int(work[k][0]), slice_rbsp_[k].data(), work[k][1], work[k][2]);
+    return;
+  }
+  // The CTB -> slice maps for the whole picture first: slice k covers tile-scan addresses from its
+  // segment address up to the next slice's.
+  const int total = pc.wctb * pc.hctb;
+  for (size_t k = 0; k < work.size(); ++k) {
+    const SliceInfo& sl = pc.slices[work[k][0]];
+    const int b = pc.rs2ts[size_t(sl.sh.segment_address)];
+    const int e = k + 1 < work.size() ? pc.rs2ts[size_t(pc.slices[work[k + 1][0]].sh.segment_address)] : total;
+    VEP_CHECK(b < e, "HEVC: slice segment addresses out of order");
+    for (int ts = b; ts < e; ++ts) {
+      const int rs = pc.ts2rs[size_t(ts)];
+      pc.slice[size_t(rs)] = u16(work[k][0]);
+      pc.sord[size_t(rs)] = u16(sl.ord);
+    }
+  }
+  pc.prefilled = true;
+  pc.multi = true;
+  while (shards_.size() < work.size()) shards_.push_back(std::make_unique<SliceShard>());
+  for (size_t k = 0; k < work.size(); ++k) {  // (records buffers keep their capacity)
+    SliceShard& sh = *shards_[k];
+    sh.g.tus.clear();
+    sh.g.pus.clear();
+    sh.g.coefs.clear();
+    sh.g.pcm.clear();
+    sh.g.wp.clear();
+    sh.stats = {};
+    sh.any_bypass = false;
+    sh.ctus = 0;
+  }
+  FanOut::shared().run(int(work.size()), [&](int k) {
+    decode_slice_data(pc, int(work[size_t(k)][0]), slice_rbsp_[size_t(k)].data(), work[size_t(k)][1],
+                      work[size_t(k)][2], shards_[size_t(k)].get());
+  });
+  // merge in slice order: the records equal a sequential parse's
+  int ctus = 0;
+  for (size_t k = 0; k < work.size(); ++k) {
+    SliceShard& sh = *shards_[k];
+    ctus += sh.ctus;
+    pc.any_bypass |= sh.any_bypass;
+    Stats& st = pc.stats;
+    st.intra += sh.stats.intra, st.inter += sh.stats.inter, st.skip += sh.stats.skip, st.pcm += sh.stats.pcm;
+    st.merge += sh.stats.merge, st.bi += sh.stats.bi, st.tskip += sh.stats.tskip, st.amp += sh.stats.amp;
+    GpuPicture* g = pc.gpu;
+    if (!g) continue;
+    const u32 coef0 = u32(g->coefs.size()), pcm0 = u32(g->pcm.size());
+    g->coefs.insert(g->coefs.end(), sh.g.coefs.begin(), sh.g.coefs.end());
+    g->pcm.insert(g->pcm.end(), sh.g.pcm.begin(), sh.g.pcm.end());
+    for (GpuTu t : sh.g.tus) {
+      if (t.flags & kTuPcm) t.data += pcm0;
+      else if (t.flags & kTuCoef) t.data += coef0;
+      g->tus.push_back(t);
+    }
+    std::vector<u8> wmap(sh.g.wp.size() + 1, 0);  // shard weight index -> picture weight index
+    for (size_t i = 0; i < sh.g.wp.size(); ++i) {
+      size_t j = 0;
+      while (j < g->wp.size() && std::memcmp(&g->wp[j], &sh.g.wp[i], sizeof(GpuWp)) != 0) ++j;
+      if (j == g->wp.size()) {
+        VEP_CHECK(g->wp.size() < 255, "HEVC: more than 255 distinct prediction weights in one picture");
+        g->wp.push_back(sh.g.wp[i]);
+      }
+      wmap[i + 1] = u8(j + 1);
+    }
+    for (GpuPu u : sh.g.pus) {
+      u.wp = wmap[u.wp];
+      g->pus.push_back(u);
+    }
+  }
+  VEP_CHECK(ctus == total, "HEVC: picture has undecoded CTUs");
+}
+
 void Decoder::finish_picture(std::vector<FramePtr>& out) {
+  try {
+    run_deferred(true);
+  } catch (...) {  // the damaged picture is dropped
+    deferred_.clear();
+    cur_ = nullptr;
+    cur_gpu_ = nullptr;
+    throw;
+  }
   FramePtr f = cur_;
   cur_ = nullptr;
   for (int k = 0; k < pc_->wctb * pc_->hctb; ++k)

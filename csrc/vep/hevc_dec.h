@@ -21,6 +21,7 @@
 #pragma once
 
 #include <functional>
+#include <array>
 #include <map>
 #include <memory>
 
@@ -124,6 +125,8 @@ class Decoder {
   void finish_picture(std::vector<FramePtr>& out);
   void bump(std::vector<FramePtr>& out);
   void decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n);
+  // the picture's deferred slices: in parallel when the picture is complete, else in order
+  void run_deferred(bool parallel);
   std::map<int, Vps> vps_;
   std::map<int, Sps> sps_;
   std::map<int, Pps> pps_;
@@ -147,6 +150,15 @@ class Decoder {
   // records-mode pictures recycled per decoder (recycle.h: resident buffers, no page faults)
   std::shared_ptr<Recycler<struct GpuPicture>> gpu_pool_;
   std::vector<std::shared_ptr<struct GpuPicture>> gpu_out_;
+  // Independent slices of one picture are parsed in parallel on the shared fan-out pool
+  // (fanout.h): their slice data is kept (deferred_: slice index, RBSP bytes, data offset) until
+  // the picture's last slice arrived. Pictures with WPP or dependent slice segments (contexts
+  // carried between segments) are parsed slice by slice as before. VEP_HEVC_SLICE_THREADS=0: off.
+  bool parallel_slices_ = true;
+  bool defer_ = false;
+  std::vector<std::vector<u8>> slice_rbsp_;
+  std::vector<std::array<size_t, 3>> deferred_;
+  std::vector<std::unique_ptr<struct SliceShard>> shards_;
 };
 
 // CPU mirror of the GPU reconstruction of one picture (hevc_gpu.cpp): executes the records of a

@@ -363,7 +363,7 @@ IngestServices::IngestServices(int io_threads, int parse_threads, int connect_th
     : io(io_threads), parse(parse_threads), connect(connect_threads), timers(connect) {}
 
 // Host CPUs this process may use: its affinity mask, bounded by a cgroup v2 CPU quota.
-static int cpu_budget() {
+int cpu_budget() {
   int n = 1;
   cpu_set_t set;
   CPU_ZERO(&set);

@@ -22,6 +22,9 @@
 
 namespace vep {
 
+// Host CPUs this process may use: its affinity mask, bounded by a cgroup v2 CPU quota.
+int cpu_budget();
+
 // Fixed thread pool running posted tasks in FIFO order.
 class TaskQueue {
  public:

@@ -1,5 +1,5 @@
 """The process-isolated hub on the GPU (``gpu.isolation: process``): a front-end program that
-never touches the GPU supervises a worker process on device 0 (engine/isolated_check.py). Checks
+never touches the GPU supervises a worker process on device 0 (vep_bench/isolated_check.py). Checks
 frames served through page-locked shared memory against the ring, the RCCL-group consumer batch
 against the fp32 letterbox reference, and a SIGKILLed GPU worker's restart + group re-formation.
 Started as a child program with its own time limit (this pytest process holds a GPU context, so
@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_isolated_hub_on_gpu():
-    cmd = [sys.executable, "-m", "video_edge_ai_proxy_amd.engine.isolated_check", "--devices=0", "--cams", "2",
+    cmd = [sys.executable, "-m", "vep_bench.isolated_check", "--devices=0", "--cams", "2",
            "--width", "1920", "--height", "1080", "--letterbox", "640", "--samples", "30", "--kill"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=ROOT)
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]

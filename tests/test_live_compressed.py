@@ -120,6 +120,7 @@ def test_live_compressed_stream_bit_exact(native, profile):
         st = live.w.stats(live.cam)
     finally:
         live.close()
+    assert st["errors"] == 0 and st["skipped"] == 0, (st, live.w.logs(live.cam, True, 20))
     check_frames(got, ref, n, 90000 // FPS)
     assert len(got) >= 15 and st["decoder"] == "general" and st["errors"] == 0
     if profile == "high":
@@ -284,6 +285,8 @@ def test_rtmp_passthrough_never_stalls_ingest(native):
             time.sleep(0.01)
         time.sleep(0.2)  # (the last AUs' decode)
         d1, a1 = w.stats(cam)["decoded"], sess.state()["aus"]
+        diag = (w.stats(cam), w.logs(cam, True, 20), w.logs(cam, False, 20), native.ingest_pool_stats()
+                if hasattr(native, "ingest_pool_stats") else None)
     finally:
         sess.stop()
         srv.stop()
@@ -291,7 +294,7 @@ def test_rtmp_passthrough_never_stalls_ingest(native):
         hang.close()
     assert accepted, "the pass-through never tried to connect"
     assert a1 - a0 >= 60, f"ingest stalled behind RTMP: {a1 - a0} AUs"
-    assert d1 - d0 >= 0.8 * (a1 - a0), f"decoding stalled behind RTMP: {d1 - d0} frames for {a1 - a0} AUs"
+    assert d1 - d0 >= 0.8 * (a1 - a0), f"decoding stalled behind RTMP: {d1 - d0} frames for {a1 - a0} AUs: {diag}"
 
 
 def hevc_reference(native, cfg, n_cached, loops=4):
@@ -324,5 +327,6 @@ def test_live_hevc_stream_bit_exact(native):
         st = live.w.stats(live.cam)
     finally:
         live.close()
+    assert st["errors"] == 0 and st["skipped"] == 0, (st, live.w.logs(live.cam, True, 20))
     check_frames(got, ref, n, 90000 // FPS)
     assert len(got) >= 15 and st["decoder"] == "general" and st["errors"] == 0

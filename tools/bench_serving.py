@@ -79,7 +79,7 @@ def main() -> int:
     a = ap.parse_args()
 
     from video_edge_ai_proxy_amd.server.frontend import FrontendPool
-    from video_edge_ai_proxy_amd.server.latency_clients import ClientPool
+    from vep_bench.latency_clients import ClientPool
 
     clients, fronts = ints(a.clients), ints(a.frontends)
     tag = f"sb{os.getpid()}"
@@ -93,7 +93,7 @@ def main() -> int:
     import torch
 
     from video_edge_ai_proxy_amd import native as vep
-    from video_edge_ai_proxy_amd.server.bench_latency import serving, summarize
+    from vep_bench.bench_latency import serving, summarize
 
     use_gpu = (not a.cpu) and torch.cuda.is_available()
     dev = 0 if use_gpu else -1

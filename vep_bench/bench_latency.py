@@ -2,7 +2,7 @@
 (ImageService -> native ring D2H into the response bytes -> grpcio -> client decode).
 
 The server runs in the bench (GPU) process; the clients run in separate processes
-(:class:`~video_edge_ai_proxy_amd.server.latency_clients.ClientPool`, started before the bench
+(:class:`~vep_bench.latency_clients.ClientPool`, started before the bench
 touches the GPU), so their receive/parse work never holds the server's GIL. Definitions:
   * ``next`` (headline): N concurrent clients, one connected channel and camera each, issuing
     back-to-back requests while the cameras stream live at their frame rate: request sent -> the
@@ -16,8 +16,8 @@ import threading
 import time
 from contextlib import contextmanager
 
-from ..utils import now_ms
-from .grpc_server import ImageService, serve
+from video_edge_ai_proxy_amd.utils import now_ms
+from video_edge_ai_proxy_amd.server.grpc_server import ImageService, serve
 
 
 class _WorkerHub:

@@ -66,12 +66,12 @@ class AnnotationLoad:
     uploads the queued annotations in batches to the loopback cloud sink."""
 
     def __init__(self, cameras: list[str], rate: float = 5.0):
-        from ..models import Settings
-        from ..services.annotation import AnnotationConsumer, AnnotationQueue
-        from ..services.edge import EdgeService
-        from ..services.settings import SettingsManager
-        from ..services.storage import Storage
-        from .grpc_server import ImageClient, ImageService, serve
+        from video_edge_ai_proxy_amd.models import Settings
+        from video_edge_ai_proxy_amd.services.annotation import AnnotationConsumer, AnnotationQueue
+        from video_edge_ai_proxy_amd.services.edge import EdgeService
+        from video_edge_ai_proxy_amd.services.settings import SettingsManager
+        from video_edge_ai_proxy_amd.services.storage import Storage
+        from video_edge_ai_proxy_amd.server.grpc_server import ImageClient, ImageService, serve
 
         self.tmp = tempfile.TemporaryDirectory(prefix="vep-annot-")
         storage = Storage(os.path.join(self.tmp.name, "kv.sqlite"))
@@ -97,7 +97,7 @@ class AnnotationLoad:
         self._th = None
 
     def start(self):
-        from ..proto import pb
+        from video_edge_ai_proxy_amd.proto import pb
 
         def run():
             try:

@@ -1,6 +1,6 @@
 """End-to-end check of the process-isolated hub on real devices (``gpu.isolation: process``).
 
-Run it as its own program (``python -m video_edge_ai_proxy_amd.engine.isolated_check --devices 0``):
+Run it as its own program (``python -m vep_bench.isolated_check --devices 0``):
 this process is the front-end and never touches a GPU; the worker processes it supervises do.
 It starts a loopback RTSP farm, one supervised worker process per device, and checks:
 
@@ -44,7 +44,7 @@ def _rows_match(hub, batch, names, size) -> float:
     import numpy as np
     import torch
 
-    from ..ops import letterbox_reference
+    from video_edge_ai_proxy_amd.ops import letterbox_reference
 
     worst = 0.0
     for row, n in zip(batch, names):
@@ -65,9 +65,9 @@ def main(argv=None) -> int:
     ap.add_argument("--kill", action="store_true")
     a = ap.parse_args(argv)
 
-    from .._native import native
-    from ..config import Config
-    from .isolated import ProcessHub
+    from video_edge_ai_proxy_amd._native import native
+    from video_edge_ai_proxy_amd.config import Config
+    from video_edge_ai_proxy_amd.engine.isolated import ProcessHub
 
     devices = [int(x) for x in a.devices.split(",")]
     srv = native.RtspServer("127.0.0.1", 0)
@@ -113,7 +113,7 @@ def main(argv=None) -> int:
         # the same VideoFrame bytes as the ring's latest frame
         import numpy as np
 
-        from ..proto import pb
+        from video_edge_ai_proxy_amd.proto import pb
 
         time.sleep(1.0)  # > idle cutoff: decoding pauses, the latest frames stay put
         seq, frame, _ = hub.latest_frame_bytes(names[0], 0, 0)

@@ -3,7 +3,7 @@
 The clients of a frame server must not share its process: receiving and parsing a 6.2 MB 1080p
 ``VideoFrame`` costs the Python gRPC client ~10 ms of CPU, and in the server's process that work
 would hold the server's GIL. :class:`ClientPool` therefore runs the clients in fresh interpreter
-processes (``python -m video_edge_ai_proxy_amd.server.latency_clients``), started with
+processes (``python -m vep_bench.latency_clients``), started with
 ``subprocess`` *before* the parent initialises the GPU (a process that holds a GPU context must
 not be the one that starts other programs), each running several client threads.
 
@@ -27,7 +27,7 @@ import sys
 import threading
 import time
 
-_PKG_PARENT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+_PKG_PARENT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 # glibc would mmap (and page-fault) every freshly allocated multi-MB frame buffer; keep them in
 # the heap so they are reused (see native.tune_malloc_for_frames for the server side)
@@ -46,7 +46,7 @@ class ClientPool:
         # the clients never use the GPU: hide it so nothing in them can initialise it
         env["HIP_VISIBLE_DEVICES"] = ""
         env["CUDA_VISIBLE_DEVICES"] = ""
-        self._p = [subprocess.Popen([sys.executable, "-u", "-m", "video_edge_ai_proxy_amd.server.latency_clients",
+        self._p = [subprocess.Popen([sys.executable, "-u", "-m", "vep_bench.latency_clients",
                                      "--threads", str(threads)], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                     env=env, text=True) for _ in range(procs)]
         deadline = time.time() + start_timeout_s
@@ -111,7 +111,7 @@ class ClientPool:
 def _client_next(target, name, key_frame_only, start_at, duration, lat, errors):
     import grpc
 
-    from .grpc_server import ImageClient
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
 
     cli = ImageClient(target)
     try:
@@ -134,7 +134,7 @@ def _client_next(target, name, key_frame_only, start_at, duration, lat, errors):
 def _client_serve(target, names, key_frame_only, samples, lat, errors):
     import grpc
 
-    from .grpc_server import ImageClient
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
 
     clis = [ImageClient(target) for _ in range(samples)]
     try:
@@ -161,7 +161,7 @@ def main(argv=None) -> int:
     a = ap.parse_args(argv)
     import grpc  # noqa: F401 — imported once up front (the first import is slow on a fresh box)
 
-    from . import grpc_server  # noqa: F401
+    from video_edge_ai_proxy_amd.server import grpc_server  # noqa: F401
 
     print("ready", flush=True)
     for line in sys.stdin:
