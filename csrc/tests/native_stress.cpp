@@ -10,15 +10,23 @@
 //     producers and readers, with GOP catch-up merges and keyframe-only toggling;
 //   * the replay bench driver: parse pool threads + quiesce + step/drain (launch_async,
 //     wait_published, complete_all) against readers;
-//   * live ingest of a compressed High-profile camera with RTMP pass-through and the archiver.
+//   * live ingest of a compressed High-profile camera with RTMP pass-through and the archiver;
+//   * the frame bus: a pump serving readers in other threads while producers publish, cameras
+//     come and go and the serve-buffer pool (mock serve: the GPU path's pool and chunked
+//     copies, memcpy for the DMA) is hit by direct readers and consumer snapshots at once;
+//   * the fan-out pool: several H.265 decoders parsing multi-slice pictures in parallel at once.
 // Reference: SURVEY.md §5 "Race detection / sanitizers" (the reference had none and real races:
 // read_image.py:48,71-74 vs rtsp_to_rtmp.py:147-151; grpc_api.go:181-184).
+#include <unistd.h>
+
 #include <atomic>
 #include <cstdio>
 #include <thread>
 #include <vector>
 
 #include "../vep/bench_driver.h"
+#include "../vep/bus.h"
+#include "../vep/hevc_dec.h"
 #include "../vep/ingest.h"
 #include "../vep/runtime.h"
 #include "../vep/synth.h"
@@ -322,6 +330,122 @@ static void compressed_ingest_stress() {
   std::printf("compressed ingest: decoded %llu\n", (unsigned long long)w.camera(cam)->decoded.load());
 }
 
+static void bus_stress() {
+  WorkerOptions o;
+  o.device = -1;
+  o.letterbox_size = 32;
+  o.max_cameras = 8;
+  o.mock_serve = true;
+  Worker w(o);
+  w.start();
+  bus::Owner owner("stress" + std::to_string(::getpid()), 0, 8);
+  owner.attach(&w);
+  const int ncam = 3;
+  std::vector<int> cams;
+  for (int i = 0; i < ncam; ++i) {
+    cams.push_back(w.add_camera("b" + std::to_string(i), 3));
+    owner.add(cams.back(), "b" + std::to_string(i));
+  }
+  std::atomic<bool> stop{false};
+  std::atomic<u64> bus_frames{0}, direct{0}, snaps{0};
+  std::vector<std::thread> th;
+  for (int i = 0; i < ncam; ++i)
+    th.emplace_back([&, i] {
+      SynthConfig c;
+      c.width = 128;
+      c.height = 96;
+      c.gop = 6;
+      c.seed = u64(40 + i);
+      SynthH264 enc(c);
+      auto cam = w.camera(cams[size_t(i)]);
+      for (int f = 0; f < 90; ++f) {
+        cam->last_query_ms.store(now_ms());
+        cam->on_access_unit(enc.next());
+        std::this_thread::sleep_for(std::chrono::microseconds(300));
+      }
+    });
+  for (int r = 0; r < 4; ++r)  // bus readers (the serving processes' side)
+    th.emplace_back([&, r] {
+      bus::Reader rd("stress" + std::to_string(::getpid()));
+      std::vector<u8> buf;
+      i64 cursor[ncam] = {};
+      while (!stop.load()) {
+        const int i = (r + int(bus_frames.load())) % ncam;
+        bus::Reader::Ticket t;
+        if (!rd.wait("b" + std::to_string(i), cursor[i], 20, r & 1, &t)) continue;
+        buf.resize(t.cap);
+        i64 seq = 0;
+        const size_t len = rd.copy(t, buf.data(), buf.size(), &seq);
+        if (!len) continue;
+        CHECK(seq > cursor[size_t(i)] && len > size_t(128) * 96 * 3);
+        cursor[size_t(i)] = seq;
+        bus_frames.fetch_add(1);
+      }
+    });
+  th.emplace_back([&] {  // direct readers through the serve-buffer pool
+    std::vector<u8> buf(size_t(128) * 96 * 3);
+    while (!stop.load())
+      for (int i = 0; i < ncam; ++i) {
+        auto cam = w.camera(cams[size_t(i)]);
+        auto ring = cam ? cam->ring() : nullptr;
+        FrameMeta m;
+        if (ring && w.read_latest(*ring, 0, &m, buf.data(), buf.size())) direct.fetch_add(1);
+      }
+  });
+  th.emplace_back([&] {  // consumer snapshots against the letterbox writes
+    std::vector<u8> snap(size_t(ncam) * 32 * 32 * 3);
+    while (!stop.load()) {
+      w.snapshot_consumer(snap.data(), snap.size(), ncam, nullptr);
+      snaps.fetch_add(1);
+    }
+  });
+  for (int i = 0; i < ncam; ++i) th[size_t(i)].join();
+  w.flush();
+  owner.remove(cams[2]);  // a camera leaves while readers may wait on it
+  int extra = w.add_camera("b3", 2);
+  owner.add(extra, "b3");
+  std::this_thread::sleep_for(std::chrono::milliseconds(50));
+  stop.store(true);
+  for (size_t i = ncam; i < th.size(); ++i) th[i].join();
+  owner.stop();
+  w.stop();
+  CHECK(bus_frames.load() > 0 && direct.load() > 0 && snaps.load() > 0);
+  std::printf("frame bus: %llu bus frames, %llu direct reads, %llu snapshots\n",
+              (unsigned long long)bus_frames.load(), (unsigned long long)direct.load(),
+              (unsigned long long)snaps.load());
+}
+
+static void slice_fanout_stress() {
+  SynthConfig c;
+  c.width = 320;
+  c.height = 192;
+  c.gop = 8;
+  c.codec = Codec::kH265;
+  c.compressed = true;
+  c.slices = 4;
+  c.bframes = 1;
+  std::vector<AuPtr> aus;
+  {
+    SynthH264 enc(c);
+    for (int i = 0; i < 12; ++i) aus.push_back(enc.next());
+  }
+  std::atomic<u64> pictures{0};
+  std::vector<std::thread> th;
+  for (int d = 0; d < 3; ++d)
+    th.emplace_back([&, d] {
+      hevc::Decoder dec;
+      dec.set_gpu_mode(d != 0);  // records mode (shards merged) and CPU reconstruction
+      for (int loop = 0; loop < 3; ++loop) {
+        for (const auto& au : aus) dec.decode(*au, 0);
+        (void)dec.flush();
+        (void)dec.take_gpu_pictures();
+        pictures.fetch_add(aus.size());
+      }
+    });
+  for (auto& t : th) t.join();
+  std::printf("parallel slices: %llu pictures\n", (unsigned long long)pictures.load());
+}
+
 int main() {
   std::setvbuf(stdout, nullptr, _IONBF, 0);  // progress is visible even if a run is cut short
   live_worker_stress();
@@ -329,6 +453,8 @@ int main() {
   general_decoder_stress();
   replay_bench_stress();
   compressed_ingest_stress();
+  bus_stress();
+  slice_fanout_stress();
   std::printf("native_stress ok\n");
   return 0;
 }

@@ -429,12 +429,18 @@ constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
 constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
-constexpr int kDefaultTuWindow = 8;        // H.265 intra TUs: 0 = per-level launches, k = queue windows
-                                           // of k levels, blocks taken by ticket (8x fewer launches;
-                                           // progress independent of dispatch order: profiles/r4/)
 constexpr int kAllLevels = 1 << 20;        // (a window holding every level of a round)
+// H.265 intra transform blocks: one persistent ticket-queue launch per round (every intra level;
+// waves take blocks in level order, so a wait is only ever on a block a running wave claimed, and
+// no wait crosses a kernel boundary). 0 = one launch per level, k = windows of k levels (each
+// window polls the previous one's edge words across a launch boundary: under rocprofv3's SQ
+// counter pass that stalled and dropped pictures), -1 = one workgroup per picture. Measured on
+// one box: same end-to-end rate and GPU time as per-level launches with ~150x fewer launches, and
+// 0 pictures dropped under the SQ counter pass (profiles/r4/hevc_sched/).
+constexpr int kDefaultTuWindow = kAllLevels;
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
+  mock_serve_ = !dev_.gpu() && (opt_.mock_serve || (std::getenv("VEP_MOCK_SERVE") && std::getenv("VEP_MOCK_SERVE")[0] == '1'));
   if (opt_.decoder == kDecoderVcn)
     VEP_CHECK(vcn::available(), "decoder backend 'vcn' requested but rocDecode is unavailable: " + vcn::load_error());
   vcn_ = opt_.decoder == kDecoderVcn || (opt_.decoder == kDecoderAuto && vcn::available());
@@ -2011,7 +2017,7 @@ Worker::ServeBuf* Worker::acquire_serve(size_t n) {
     b->h = static_cast<u8*>(dev_.alloc_pinned(n));
     b->cap = n;
   }
-  if (!b->ev[0])
+  if (!b->ev[0] && dev_.gpu())
     for (hipEvent_t& e : b->ev)  // waiters sleep: several server threads wait at once
       VEP_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventBlockingSync));
   return b;
@@ -2063,8 +2069,9 @@ bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, siz
       if (!ring->still_valid(slot, meta->seq)) continue;
       return true;
     }
-    if (dev_.gpu()) {
-      dev_.bind();
+    if (dev_.gpu() || mock_serve_) {  // (mock: the same pool and chunking, memcpy for the DMA)
+      const bool gpu = dev_.gpu();
+      if (gpu) dev_.bind();
       ServeBuf* b = acquire_serve(n);
       const u8* src = ring->slot_ptr(slot);
       const size_t chunk = (n + kServeChunks - 1) / kServeChunks;
@@ -2072,6 +2079,10 @@ bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, siz
         for (int k = 0; k < kServeChunks; ++k) {
           const size_t off = size_t(k) * chunk;
           if (off >= n) break;
+          if (!gpu) {
+            std::memcpy(b->h + off, src + off, std::min(chunk, n - off));
+            continue;
+          }
           VEP_HIP(hipMemcpyAsync(b->h + off, src + off, std::min(chunk, n - off), hipMemcpyDeviceToHost,
                                  serve_stream_));
           VEP_HIP(hipEventRecord(b->ev[k], serve_stream_));
@@ -2079,7 +2090,7 @@ bool Worker::read_latest(FrameRing& rg, i64 after, FrameMeta* meta, u8* dst, siz
         for (int k = 0; k < kServeChunks; ++k) {
           const size_t off = size_t(k) * chunk;
           if (off >= n) break;
-          VEP_HIP(hipEventSynchronize(b->ev[k]));
+          if (gpu) VEP_HIP(hipEventSynchronize(b->ev[k]));
           std::memcpy(dst + off, b->h + off, std::min(chunk, n - off));
         }
       } catch (...) {

@@ -256,6 +256,10 @@ struct WorkerOptions {
   // show one frame per GOP, so the wait is invisible to their clients. -1 = VEP_KF_WINDOW_US or
   // the default; 0 = off.
   int kf_window_us = -1;
+  // CPU backend only (sanitizer runs): serve through the pinned serve-buffer pool with chunked
+  // copies, as the GPU path's D2H does, so its concurrency (acquire_serve / release_serve, chunk
+  // hand-off) runs under ThreadSanitizer without a GPU. Also VEP_MOCK_SERVE=1.
+  bool mock_serve = false;
 };
 enum DecoderBackend : int { kDecoderNative = 0, kDecoderVcn = 1, kDecoderAuto = 2 };
 
@@ -470,6 +474,7 @@ class Worker {
   // lanes wait for a stage's batch by polling its event with sleeps (VEP_SPIN_WAIT=1:
   // hipEventSynchronize, which spins a core in the HSA runtime)
   bool polite_wait_ = true;
+  bool mock_serve_ = false;  // WorkerOptions::mock_serve
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex launch_mu_;
