@@ -283,6 +283,20 @@ class RtspFarm:
                 raise RuntimeError(f"rtsp farm stalled at {self.worker.pictures}/{target} pictures")
             time.sleep(0.0002)
 
+    def settle(self, min_s=1.0, max_s=6.0, window_s=0.25):
+        """Before the warmup steps: let the unthrottled pipeline reach its steady state (the
+        sockets' start-up backlog drained: nearly every decoded picture is published again rather
+        than collapsed into a catch-up batch), so a short timed window measures the steady rate.
+        Returns the seconds it took."""
+        t0 = time.perf_counter()
+        while time.perf_counter() - t0 < max_s:
+            p0, f0 = self.worker.pictures, self.worker.frames
+            time.sleep(window_s)
+            dp, df = self.worker.pictures - p0, self.worker.frames - f0
+            if time.perf_counter() - t0 >= min_s and dp > 0 and df >= 0.9 * dp:
+                break
+        return round(time.perf_counter() - t0, 2)
+
     def stats(self):
         st = [self.worker.stats(c) for c in self.idx]
         out = {"packets": sum(x["packets"] for x in st), "bytes_in": sum(x["bytes_in"] for x in st),
@@ -364,7 +378,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
 
             annot = AnnotationLoad([f"r{rank}rtsp{i}" for i in range(cams)], rate=a.annotate_rate)
             annot.start()
-        farm.wait_pictures(cams * max(1, a.warmup), timeout_s=300.0)
+        settle_s = farm.settle()
+        farm.wait_pictures(farm.worker.pictures + cams * max(1, a.warmup), timeout_s=300.0)
         if world > 1:
             dist.barrier()
         sync()
@@ -489,6 +504,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "access_units_ingested": aus,
             "access_units_per_s": round(aus / elapsed, 1),
             "access_units_skipped": skipped,
+            "settle_s": settle_s,
             "ingest_mode": {"timed_region": "lossless: a camera's socket is paused while its parse backlog is deep "
                                             "(TCP back-pressure on the unthrottled farm), so no access unit is "
                                             "skipped by construction",

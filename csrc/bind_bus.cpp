@@ -28,17 +28,35 @@ void bind_bus(py::module_& m) {
       .def("touch", &bus::Reader::touch, py::arg("name"), py::arg("key_frame_only") = -1,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("rescans", &bus::Reader::rescans)
+      .def("info",
+           [](bus::Reader& r, const std::string& name) -> py::object {
+             bus::Reader::Info i;
+             bool ok;
+             {
+               py::gil_scoped_release nogil;
+               ok = r.info(name, &i);
+             }
+             if (!ok) return py::none();
+             py::dict d;
+             d["owner_pid"] = i.owner_pid;
+             d["pinned"] = i.pinned;
+             d["ring_seq"] = i.ring_seq;
+             d["bus_seq"] = i.bus_seq;
+             d["owner_published"] = i.published;
+             return d;
+           })
       .def("frame",
            // (seq, serialized VideoFrame bytes) of the newest bus frame with seq > after (waiting up
            // to wait_ms for it), (seq, None) when that frame's seq is `have` (the caller holds its
-           // bytes), None on timeout / unknown camera. key_frame_only < 0 leaves the mode as is.
+           // bytes), None on timeout / unknown camera. key_frame_only < 0 leaves the mode as is;
+           // touch = False reads without marking the camera's demand (last_query).
            [](bus::Reader& r, const std::string& name, i64 after, int wait_ms, int key_frame_only,
-              i64 have) -> py::object {
+              i64 have, bool touch) -> py::object {
              bus::Reader::Ticket t;
              bool ok;
              {
                py::gil_scoped_release nogil;
-               ok = r.wait(name, after, wait_ms, key_frame_only, &t);
+               ok = r.wait(name, after, wait_ms, key_frame_only, &t, touch);
              }
              if (!ok) return py::none();
              const i64 ns = r.newest_seq(t);
@@ -59,7 +77,7 @@ void bind_bus(py::module_& m) {
              return py::make_tuple(seq, py::reinterpret_steal<py::object>(b));
            },
            py::arg("name"), py::arg("after") = 0, py::arg("wait_ms") = 0, py::arg("key_frame_only") = -1,
-           py::arg("have") = -1);
+           py::arg("have") = -1, py::arg("touch") = true);
 
   m.def("bus_remove_segments", &bus::remove_segments_of, py::arg("pid"),
         "Unlink the frame-bus segments a (dead) process left in /dev/shm.");

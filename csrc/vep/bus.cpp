@@ -239,6 +239,7 @@ bool Owner::ensure_data(int cam, size_t slot_cap) {
   }
   e.bus_seq.store(0);
   e.slot_cap.store(cap);
+  e.pinned.store(nd.pinned ? 1u : 0u);
   e.data_gen.store(gen, std::memory_order_release);
   return true;
 }
@@ -457,6 +458,18 @@ std::vector<std::string> Reader::names() {
   return out;
 }
 
+bool Reader::info(const std::string& name, Info* out) {
+  Loc l;
+  if (!locate(name, &l)) return false;
+  const CamEntry& e = l.seg->hdr->cams[l.cam];
+  out->owner_pid = l.seg->pid;
+  out->pinned = e.pinned.load() != 0;
+  out->ring_seq = e.ring_seq.load();
+  out->bus_seq = e.bus_seq.load();
+  out->published = l.seg->hdr->published.load();
+  return true;
+}
+
 bool Reader::touch(const std::string& name, int key_frame_only) {
   Loc l;
   if (!locate(name, &l)) return false;
@@ -472,15 +485,17 @@ bool Reader::touch(const std::string& name, int key_frame_only) {
   return true;
 }
 
-bool Reader::wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t) {
+bool Reader::wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t, bool touch) {
   Loc l;
   if (!locate(name, &l)) return false;
   Header* h = l.seg->hdr;
   CamEntry& e = h->cams[l.cam];
-  if (key_frame_only >= 0) e.keyframe_only.store(key_frame_only ? 1u : 0u, std::memory_order_release);
-  const i64 now = wall_ms();
-  i64 cur = e.last_query_ms.load();
-  while (cur < now && !e.last_query_ms.compare_exchange_weak(cur, now)) {
+  if (touch) {
+    if (key_frame_only >= 0) e.keyframe_only.store(key_frame_only ? 1u : 0u, std::memory_order_release);
+    const i64 now = wall_ms();
+    i64 cur = e.last_query_ms.load();
+    while (cur < now && !e.last_query_ms.compare_exchange_weak(cur, now)) {
+    }
   }
   const i64 rs = e.ring_seq.load(std::memory_order_acquire);
   if (rs < after) after = 0;  // the cursor belongs to an older ring (restarted owner / new camera)

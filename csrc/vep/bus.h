@@ -66,6 +66,7 @@ struct alignas(64) CamEntry {
   std::atomic<u32> newest;         // slot holding bus_seq
   std::atomic<u32> data_gen;       // data segment generation (0: none yet)
   std::atomic<u64> slot_cap;       // bytes per slot of the data segment
+  std::atomic<u32> pinned;         // the data segment is page-locked (the DMA lands in it directly)
   SlotHdr slots[kSlots];
 };
 constexpr u32 kUnset = 2;
@@ -151,7 +152,8 @@ class Reader {
   // HSET last_access_time_<dev> / SET is_key_frame_only_<dev>, grpc_api.go:159-175), then waits
   // up to wait_ms for a bus frame with seq > after that is at least as new as the owner's ring
   // was at the call. False: unknown camera or timeout.
-  bool wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t);
+  // touch = false: read only (no demand marked; an internal reader, not a client request).
+  bool wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t, bool touch = true);
   // Copies the newest bus frame with seq > t.after into dst (cap >= t.cap): one seqlock-checked
   // memcpy. Returns its length and sequence, 0 if the camera went away meanwhile.
   size_t copy(const Ticket& t, u8* dst, size_t cap, i64* seq);
@@ -160,6 +162,13 @@ class Reader {
   i64 newest_seq(const Ticket& t) const;
   // Demand only.
   bool touch(const std::string& name, int key_frame_only);
+  struct Info {
+    int owner_pid = 0;
+    bool pinned = false;
+    i64 ring_seq = 0, bus_seq = 0;
+    u64 published = 0;  // the owner's bus publishes (all its cameras)
+  };
+  bool info(const std::string& name, Info* out);
   std::vector<std::string> names();
   u64 rescans() const { return rescans_.load(); }
 

@@ -4,10 +4,12 @@ Run it as its own program (``python -m vep_bench.isolated_check --devices 0``):
 this process is the front-end and never touches a GPU; the worker processes it supervises do.
 It starts a loopback RTSP farm, one supervised worker process per device, and checks:
 
-* frames served through shared memory (page-locked on GPUs: ``pinned``) equal the ring's
-  latest frame, with the serving latency of back-to-back ``latest_frame_bytes`` requests;
+* frames served through the frame bus (the worker's page-locked shared-memory segments on GPUs:
+  ``pinned``) equal the ring's latest frame, with the serving latency of back-to-back
+  ``latest_frame_bytes`` requests;
 * ``consumer_batch()`` — an all-gather across the worker processes' group (RCCL on GPUs) — matches
-  the fp32 letterbox reference of every camera's latest frame;
+  the fp32 letterbox reference of every camera's latest frame; then ``--gathers`` steady-state
+  gathers are timed (group formation excluded);
 * with ``--kill``: a SIGKILLed worker is restarted, its cameras re-added, the group re-formed and
   the gather works again.
 
@@ -63,6 +65,7 @@ def main(argv=None) -> int:
     ap.add_argument("--letterbox", type=int, default=640)
     ap.add_argument("--samples", type=int, default=60)
     ap.add_argument("--kill", action="store_true")
+    ap.add_argument("--gathers", type=int, default=20, help="steady-state consumer gathers to time")
     a = ap.parse_args(argv)
 
     from video_edge_ai_proxy_amd._native import native
@@ -123,7 +126,15 @@ def main(argv=None) -> int:
         out["frame_equal"] = bool(np.array_equal(np.frombuffer(vf.data, np.uint8).reshape(img.shape), img))
         t0 = time.perf_counter()
         batch, order = hub.consumer_batch(names=names)
-        out["gather_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+        out["first_gather_ms"] = round((time.perf_counter() - t0) * 1e3, 2)  # (includes group formation)
+        for _ in range(a.gathers):  # steady state: the group exists
+            hub.consumer_batch(names=names, to_host=False)
+        ms = sorted(hub.gather_ms[-a.gathers:]) if a.gathers else []
+        out["steady_gathers"] = len(ms)
+        out["steady_gather_ms_p50"] = round(ms[len(ms) // 2], 3) if ms else None
+        out["steady_gather_ms_max"] = round(ms[-1], 3) if ms else None
+        out["gather_definition"] = ("per call, max over ranks: snapshot of the consumer rows + the header and "
+                                    "row all-gathers (RCCL on GPUs) + stream sync; group formation excluded")
         out["batch_shape"] = list(batch.shape)
         out["batch_max_abs_err"] = _rows_match(hub, batch, order, a.letterbox)
         out["group"] = [c.call("group_info") for c in hub._children]

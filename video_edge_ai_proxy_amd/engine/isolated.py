@@ -544,10 +544,11 @@ class ProcessHub:
         """(seq, serialized VideoFrame, meta) or None, from the frame bus: the child's pump DMAs
         the frame into shared memory, copied out here once (the bytes grpcio sends)."""
         self.handle(name)
-        r = self.bus.frame(name, after, wait_ms, -1)
+        r = self.bus.frame(name, after, wait_ms, -1, -1, False)  # (a read: hub.touch marks demand)
         if r is None:
             return None
-        return r[0], r[1], {"seq": r[0]}
+        info = self.bus.info(name) or {}
+        return r[0], r[1], {"seq": r[0], "shm_pinned": bool(info.get("pinned"))}
 
     def latest_frame(self, name: str, after: int = 0):
         return self._call(name, "latest_frame", after)
