@@ -29,6 +29,22 @@ static py::bytes to_bytes(const u8* p, size_t n) {
   return py::bytes(reinterpret_cast<const char*>(p), n);
 }
 
+// (y, uv) coded NV12 planes of a surface: uint8, or uint16 for high bit depth (HEVC Main10)
+static py::tuple surface_planes(const HostSurface& p) {
+  if (p.wide()) {
+    py::array_t<uint16_t> y({p.coded_h, p.coded_w});
+    py::array_t<uint16_t> uv({p.coded_h / 2, p.coded_w});
+    std::memcpy(y.mutable_data(), p.y16.data(), p.y16.size() * 2);
+    std::memcpy(uv.mutable_data(), p.uv16.data(), p.uv16.size() * 2);
+    return py::make_tuple(y, uv);
+  }
+  py::array_t<uint8_t> y({p.coded_h, p.coded_w});
+  py::array_t<uint8_t> uv({p.coded_h / 2, p.coded_w});
+  std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
+  std::memcpy(uv.mutable_data(), p.uv.data(), p.uv.size());
+  return py::make_tuple(y, uv);
+}
+
 static py::dict meta_dict(const FrameMeta& m) {
   py::dict d;
   d["width"] = m.width;
@@ -228,6 +244,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("scaling_lists", &SynthConfig::scaling_lists)
       .def_readwrite("long_term", &SynthConfig::long_term)
       .def_readwrite("lossless", &SynthConfig::lossless)
+      .def_readwrite("bit_depth", &SynthConfig::bit_depth)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -283,15 +300,7 @@ PYBIND11_MODULE(_vep, m) {
       .def(py::init<const SynthConfig&>())
       .def("next", [](SynthH264& s) { return std::shared_ptr<AccessUnit>(s.next()); },
            py::call_guard<py::gil_scoped_release>())
-      .def("picture",
-           [](const SynthH264& s) {
-             const HostSurface& p = s.picture();
-             py::array_t<uint8_t> y({p.coded_h, p.coded_w});
-             py::array_t<uint8_t> uv({p.coded_h / 2, p.coded_w});
-             std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
-             std::memcpy(uv.mutable_data(), p.uv.data(), p.uv.size());
-             return py::make_tuple(y, uv);
-           })
+      .def("picture", [](const SynthH264& s) { return surface_planes(s.picture()); })
       .def_property_readonly("sps_nal", [](const SynthH264& s) { return to_bytes(s.sps_nal().data(), s.sps_nal().size()); })
       .def_property_readonly("pps_nal", [](const SynthH264& s) { return to_bytes(s.pps_nal().data(), s.pps_nal().size()); })
       .def_property_readonly("vps_nal", [](const SynthH264& s) { return to_bytes(s.vps_nal().data(), s.vps_nal().size()); })
@@ -299,13 +308,8 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("last_pts", &SynthH264::last_pts);
   m.attr("SynthEncoder") = m.attr("SynthH264");
 
-  auto surface_tuple = [](const HostSurface& p) {
-    py::array_t<uint8_t> y({p.coded_h, p.coded_w});
-    py::array_t<uint8_t> uv({p.coded_h / 2, p.coded_w});
-    std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
-    std::memcpy(uv.mutable_data(), p.uv.data(), p.uv.size());
-    return py::make_tuple(y, uv);
-  };
+  auto surface_tuple = [](const HostSurface& p) { return surface_planes(p); };
+
   py::class_<avc::AvcHighConfig>(m, "AvcHighConfig")
       .def(py::init<>())
       .def_readwrite("width", &avc::AvcHighConfig::width)
@@ -371,6 +375,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("weighted", &hevc::HevcEncConfig::weighted)
       .def_readwrite("long_term", &hevc::HevcEncConfig::long_term)
       .def_readwrite("lossless", &hevc::HevcEncConfig::lossless)
+      .def_readwrite("bit_depth", &hevc::HevcEncConfig::bit_depth)
       .def_readwrite("coverage", &hevc::HevcEncConfig::coverage)
       .def_readwrite("objects", &hevc::HevcEncConfig::objects)
       .def_readwrite("noise", &hevc::HevcEncConfig::noise)
@@ -439,12 +444,23 @@ PYBIND11_MODULE(_vep, m) {
         (void)ch;
         // the coded picture (the decoder's surfaces are coded_w x coded_h, slots are 16-aligned)
         const int pw = coded_w_, ph = coded_h_;
-        py::array_t<uint8_t> y({ph, pw});
-        py::array_t<uint8_t> uv({ph / 2, pw});
-        for (int r = 0; r < ph; ++r) std::memcpy(y.mutable_data() + size_t(r) * pw, &s.y[size_t(r) * cw], size_t(pw));
-        for (int r = 0; r < ph / 2; ++r)
-          std::memcpy(uv.mutable_data() + size_t(r) * pw, &s.uv[size_t(r) * cw], size_t(pw));
-        l.append(py::make_tuple(f->pts, f->poc, std::string(1, f->type), py::make_tuple(y, uv), f->slot));
+        py::tuple planes;
+        if (s.wide()) {  // Main10: uint16 planes
+          py::array_t<uint16_t> y({ph, pw});
+          py::array_t<uint16_t> uv({ph / 2, pw});
+          for (int r = 0; r < ph; ++r) std::memcpy(y.mutable_data() + size_t(r) * pw, &s.y16[size_t(r) * cw], size_t(pw) * 2);
+          for (int r = 0; r < ph / 2; ++r)
+            std::memcpy(uv.mutable_data() + size_t(r) * pw, &s.uv16[size_t(r) * cw], size_t(pw) * 2);
+          planes = py::make_tuple(y, uv);
+        } else {
+          py::array_t<uint8_t> y({ph, pw});
+          py::array_t<uint8_t> uv({ph / 2, pw});
+          for (int r = 0; r < ph; ++r) std::memcpy(y.mutable_data() + size_t(r) * pw, &s.y[size_t(r) * cw], size_t(pw));
+          for (int r = 0; r < ph / 2; ++r)
+            std::memcpy(uv.mutable_data() + size_t(r) * pw, &s.uv[size_t(r) * cw], size_t(pw));
+          planes = py::make_tuple(y, uv);
+        }
+        l.append(py::make_tuple(f->pts, f->poc, std::string(1, f->type), planes, f->slot));
       }
       return l;
     }
@@ -454,8 +470,9 @@ PYBIND11_MODULE(_vep, m) {
         coded_h_ = p->height;
         const int sw = (p->width + 15) & ~15, sh = (p->height + 15) & ~15;
         if (slots.size() < size_t(d.gpu_slots())) slots.resize(size_t(d.gpu_slots()));
+        const int bd = std::max(p->bd_y, p->bd_c);
         for (auto& h : slots)
-          if (h.coded_w != sw || h.coded_h != sh) h.alloc(sw, sh);
+          if (h.coded_w != sw || h.coded_h != sh || h.bd != bd) h.alloc(sw, sh, bd);
         if (execute) hevc::cpu_execute(*p, slots);
         ++pictures;
         pus += p->pus.size();

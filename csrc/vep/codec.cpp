@@ -1,5 +1,6 @@
 // Native H.264 macroblock-layer parser (CAVLC, I_PCM + P_Skip subset) and CPU reference
 // reconstruction. See codec.h for the CPU/GPU split.
+#include <algorithm>
 #include "codec.h"
 
 #include "cabac.h"
@@ -525,8 +526,29 @@ void cpu_apply_update(const MbUpdate& upd, HostSurface& s) {
   }
 }
 
-void cpu_nv12_to_bgr(const HostSurface& s, int crop_left, int crop_top, int width, int height,
+void narrow_surface(const HostSurface& s, HostSurface& out) {
+  if (!s.wide()) {
+    out = s;
+    return;
+  }
+  out.coded_w = s.coded_w;
+  out.coded_h = s.coded_h;
+  out.bd = 8;
+  out.y16.clear();
+  out.uv16.clear();
+  const int sh = s.bd - 8, rnd = (1 << sh) >> 1;
+  auto n8 = [&](u16 v) { return u8(std::min(255, (int(v) + rnd) >> sh)); };
+  out.y.resize(s.y16.size());
+  out.uv.resize(s.uv16.size());
+  for (size_t i = 0; i < s.y16.size(); ++i) out.y[i] = n8(s.y16[i]);
+  for (size_t i = 0; i < s.uv16.size(); ++i) out.uv[i] = n8(s.uv16[i]);
+}
+
+void cpu_nv12_to_bgr(const HostSurface& s8, int crop_left, int crop_top, int width, int height,
                      u8* out) {
+  HostSurface tmp;
+  if (s8.wide()) narrow_surface(s8, tmp);
+  const HostSurface& s = s8.wide() ? tmp : s8;
   for (int y = 0; y < height; ++y) {
     int sy = y + crop_top;
     const u8* yr = &s.y[size_t(sy) * s.coded_w];

@@ -283,13 +283,43 @@ class StreamParser {
 struct HostSurface {
   int coded_w = 0, coded_h = 0;
   std::vector<u8> y, uv;  // NV12
-  void alloc(int w, int h) {
+  // High bit depth (HEVC Main10): the same NV12 layout with one u16 per sample (LSB-aligned);
+  // y / uv stay empty. bd = the sample bit depth of the storage (8: u8 planes).
+  int bd = 8;
+  std::vector<u16> y16, uv16;
+  bool wide() const { return bd > 8; }
+  void alloc(int w, int h, int bit_depth = 8) {
     coded_w = w;
     coded_h = h;
-    y.assign(size_t(w) * h, 16);
-    uv.assign(size_t(w) * h / 2, 128);
+    bd = bit_depth;
+    if (bd > 8) {
+      y.clear();
+      uv.clear();
+      y16.assign(size_t(w) * h, u16(16 << (bd - 8)));
+      uv16.assign(size_t(w) * h / 2, u16(128 << (bd - 8)));
+    } else {
+      y16.clear();
+      uv16.clear();
+      y.assign(size_t(w) * h, 16);
+      uv.assign(size_t(w) * h / 2, 128);
+    }
+  }
+  // sample of component c (0 Y, 1 Cb, 2 Cr) at component coordinates (x, y)
+  int get(int c, int x, int yy) const {
+    const size_t i = c == 0 ? size_t(yy) * coded_w + size_t(x) : size_t(yy) * coded_w + size_t(2 * x + c - 1);
+    if (bd > 8) return c == 0 ? y16[i] : uv16[i];
+    return c == 0 ? y[i] : uv[i];
+  }
+  void set(int c, int x, int yy, int v) {
+    const size_t i = c == 0 ? size_t(yy) * coded_w + size_t(x) : size_t(yy) * coded_w + size_t(2 * x + c - 1);
+    if (bd > 8) (c == 0 ? y16 : uv16)[i] = u16(v);
+    else (c == 0 ? y : uv)[i] = u8(v);
   }
 };
+
+// 8-bit copy of a high bit depth surface (round to nearest, saturating): the form the BGR24
+// conversion and the letterbox read. An 8-bit surface is copied as is.
+void narrow_surface(const HostSurface& s, HostSurface& out);
 
 // CPU reference of the fused GPU kernel: apply MB update to the NV12 surface, then convert the
 // cropped picture to packed BGR24 (out must hold width*height*3 bytes).

@@ -86,7 +86,9 @@ void launch_gather(const GatherChunk* d_chunks, int n, hipStream_t s);
 
 // ---- general H.265 reconstruction (gpu_hevc.hip; records from hevc::Decoder, hevc_kern.h) ----
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera
-// lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = `stride`).
+// lives at y + k * slot_y / uv + k * slot_uv (NV12, pitch = `stride` samples; slot sizes in
+// bytes: Main10 pictures have u16 samples).
+constexpr int kHevcWide = 16;
 struct HevcDesc {
   VEP_DEV u8* y;
   VEP_DEV u8* uv;
@@ -96,7 +98,8 @@ struct HevcDesc {
   i32 target;
   i32 cb_qp_offset, cr_qp_offset;
   i32 flags;             // bit 0 deblock, bit 1 SAO, bit 2 samples not loop-filtered (pcm_map),
-                         // bit 3 SAO does not cross tile boundaries
+                         // bit 3 SAO does not cross tile boundaries, bit 4 (kHevcWide) u16 samples
+  i32 bd_y, bd_c;        // sample bit depths (8; Main10: up to 10, with kHevcWide)
   const VEP_DEV void* pus;       // hevc::GpuPu[npu]
   const VEP_DEV void* tus;       // hevc::GpuTu (level-sorted)
   const VEP_DEV i16* coefs;
@@ -152,6 +155,9 @@ void launch_hevc_tu_pics(const HevcDesc* d_descs, const HevcTuRange* d_pics, int
 // 4-line edge segment; then SAO (copy of the deblocked picture, one thread per sample).
 void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int dir, hipStream_t s);
 void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream_t s);
+// Main10 output: u16 NV12 planes (n luma samples, n / 2 chroma) -> 8-bit NV12 (round to nearest,
+// saturating), the form the BGR24 conversion and the letterbox read.
+void launch_narrow(const u16* y, const u16* uv, u8* y8, u8* uv8, size_t n, int bd, hipStream_t s);
 
 // ---- general H.264 reconstruction (gpu_avc.hip; records from avc::Decoder, avc.h) ----------
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera

@@ -68,24 +68,29 @@ __device__ inline int pick_range(const HevcTuRange* r, int n, int b) {
   return lo;
 }
 
+// Sample type of a picture: u8 planes (8-bit streams: the bit depth is the constant 8, so the
+// shifts of the shared math fold away) or u16 planes (Main10, HevcDesc::bd_y / bd_c).
+template <class P>
+__device__ inline int bd_of(int bd) {
+  return sizeof(P) == 1 ? 8 : bd;
+}
+
 // ------------------------------------------------------------------------------ MC
 // Each output sample's taps are read from the picture (edge-clamped) by its own thread. A
 // separable form staged through LDS (reference window, horizontal pass, vertical taps) was
 // measured 2.5-3x slower on the camera streams (profiles/r3/mcab/): most blocks are small and
 // their loads hit L1/L2, so the staging syncs and idle lanes cost more than the taps saved.
-__global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict__ descs, int n) {
-  const int b = int(blockIdx.x);
-  const HevcDesc& d = descs[pick_pu(descs, n, b)];
-  const GpuPu u = static_cast<const GpuPu*>(d.pus)[b - d.pu_begin];
-  const int stride = d.stride, W = d.width, H = d.height;
-  u8* y = d.y + size_t(d.target) * d.slot_y;
-  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
-  const VEP_DEV u8* ry[2] = {nullptr, nullptr};  // (global: a null initialiser would make them flat)
-  const VEP_DEV u8* ruv[2] = {nullptr, nullptr};
+template <class P>
+__device__ __attribute__((always_inline)) inline void mc_block(const HevcDesc& d, const GpuPu& u) {
+  const int stride = d.stride, W = d.width, H = d.height, bdy = bd_of<P>(d.bd_y), bdc = bd_of<P>(d.bd_c);
+  P* y = reinterpret_cast<P*>(d.y + size_t(d.target) * d.slot_y);
+  P* uv = reinterpret_cast<P*>(d.uv + size_t(d.target) * d.slot_uv);
+  const P* ry[2] = {nullptr, nullptr};
+  const P* ruv[2] = {nullptr, nullptr};
   for (int l = 0; l < 2; ++l)
     if ((u.pred >> l) & 1) {
-      ry[l] = d.y + size_t(u.slot[l]) * d.slot_y;
-      ruv[l] = d.uv + size_t(u.slot[l]) * d.slot_uv;
+      ry[l] = reinterpret_cast<const P*>(d.y + size_t(u.slot[l]) * d.slot_y);
+      ruv[l] = reinterpret_cast<const P*>(d.uv + size_t(u.slot[l]) * d.slot_uv);
     }
   const bool bi = u.pred == 3;
   // explicit weighted prediction: the PU's weights / offsets (uniform per workgroup)
@@ -98,9 +103,9 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
     for (int l = 0; l < 2; ++l)
       if (ry[l])
         v[k++] = hevc::hk_luma_mc(ry[l], stride, W, H, u.x + i + (u.mv[l][0] >> 2), u.y + j + (u.mv[l][1] >> 2),
-                                  u.mv[l][0] & 3, u.mv[l][1] & 3);
+                                  u.mv[l][0] & 3, u.mv[l][1] & 3, bdy);
     y[(u.y + j) * stride + u.x + i] =
-        wp ? hevc::hk_weight_explicit(*wp, 0, v[0], v[1], bi, ul) : hevc::hk_weight(v[0], v[1], bi);
+        P(wp ? hevc::hk_weight_explicit(*wp, 0, v[0], v[1], bi, ul, bdy) : hevc::hk_weight(v[0], v[1], bi, bdy));
   }
   const int wc = u.w >> 1, hc = u.h >> 1, nc = wc * hc;
   for (int s = int(threadIdx.x); s < 2 * nc; s += 256) {
@@ -109,10 +114,19 @@ __global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict
     for (int l = 0; l < 2; ++l)
       if (ruv[l])
         v[k++] = hevc::hk_chroma_mc(ruv[l], stride, W >> 1, H >> 1, c, (u.x >> 1) + i + (u.mv[l][0] >> 3),
-                                    (u.y >> 1) + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7);
+                                    (u.y >> 1) + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7, bdc);
     uv[((u.y >> 1) + j) * stride + u.x + 2 * i + c] =
-        wp ? hevc::hk_weight_explicit(*wp, 1 + c, v[0], v[1], bi, ul) : hevc::hk_weight(v[0], v[1], bi);
+        P(wp ? hevc::hk_weight_explicit(*wp, 1 + c, v[0], v[1], bi, ul, bdc) : hevc::hk_weight(v[0], v[1], bi, bdc));
   }
+}
+
+__global__ __launch_bounds__(256) void hevc_mc_kernel(const HevcDesc* __restrict__ descs, int n) {
+  const int b = int(blockIdx.x);
+  const HevcDesc& d = descs[pick_pu(descs, n, b)];
+  const GpuPu u = static_cast<const GpuPu*>(d.pus)[b - d.pu_begin];
+  // (8-bit pictures: bd = 8 folds into the same code as before; Main10 pictures: u16 samples)
+  if (d.flags & kHevcWide) mc_block<u16>(d, u);
+  else mc_block<u8>(d, u);
 }
 
 
@@ -162,8 +176,9 @@ constexpr int kTuQueueWgs = 128;
 // hk_prepare_refs, same result): gather by availability, substitution as "nearest available
 // sample before, else the first available one", then the [1 2 1] / strong filters. Units in
 // `pend` (queue kernel only) come from the epoch-tagged edge words, polled until current.
-__device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* plane, int stride, int step, int lane,
-                                  TuWave& L) {
+template <class P>
+__device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const P* plane, int stride, int step, int lane,
+                                  TuWave& L, int bd) {
   const int x0 = t.x, y0 = t.y, log2 = t.log2;
   const bool luma = t.c == 0;
   const u64 avail = t.avail, pend = d.xg ? t.pend : 0;
@@ -212,7 +227,7 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* p
         if (wp2 && u32(w >> 32) != d.epoch) w = xg_get(wp2);
       }
     }
-    if (xq) v = int(u32(w) & 0xffu);
+    if (xq) v = int(u32(w) & 0xffffu);
     L.sbuf[k] = v;
     L.sav[k] = a ? 1 : 0;
   }
@@ -223,7 +238,7 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* p
       if (L.sav[j]) src = j;
     for (int j = k + 1; j <= last && src < 0; ++j)
       if (L.sav[j]) src = j;
-    L.sref[k] = src >= 0 ? L.sbuf[src] : 128;
+    L.sref[k] = src >= 0 ? L.sbuf[src] : 1 << (bd - 1);
   }
   wave_sync();
   // filtering decision (luma): same rule as hk_prepare_refs
@@ -239,7 +254,7 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* p
       // tl = ref[2n], top[2n] = ref[4n], top[n] = ref[3n], left[2n-1] = ref[0], left[n-1] = ref[n]
       const int tl = L.sref[2 * n];
       const int a1 = tl + L.sref[4 * n] - 2 * L.sref[3 * n], a2 = tl + L.sref[0] - 2 * L.sref[n];
-      strong_f = (a1 < 0 ? -a1 : a1) < 8 && (a2 < 0 ? -a2 : a2) < 8;
+      strong_f = (a1 < 0 ? -a1 : a1) < (1 << (bd - 5)) && (a2 < 0 ? -a2 : a2) < (1 << (bd - 5));
     }
   }
   for (int k = lane; k <= last; k += 64) {
@@ -268,15 +283,16 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const u8* p
 // reconstruction into the picture.
 // (inlined into both launch kernels: as a call its pointer arguments would be generic, i.e. flat
 // accesses)
-__device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d, const GpuTu& t, int lane, TuWave& L,
-                                                              bool publish) {
+template <class P>
+__device__ __attribute__((always_inline)) inline void tu_wave_t(const HevcDesc& d, const GpuTu& t, int lane, TuWave& L,
+                                                                bool publish) {
   const int stride = d.stride;
-  u8* y = d.y + size_t(d.target) * d.slot_y;
-  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  P* y = reinterpret_cast<P*>(d.y + size_t(d.target) * d.slot_y);
+  P* uv = reinterpret_cast<P*>(d.uv + size_t(d.target) * d.slot_uv);
   wave_sync();  // the wave's previous block has finished reading its LDS
-  if (t.flags & hevc::kTuPcm) {
+  if (t.flags & hevc::kTuPcm) {  // (the records hold the samples at the picture's sample type)
     const int n = 1 << t.log2, nc = n >> 1;
-    const u8* src = d.pcm + t.data;
+    const P* src = reinterpret_cast<const P*>(d.pcm + t.data);
     for (int s = lane; s < n * n; s += 64) y[(t.y + s / n) * stride + t.x + s % n] = src[s];
     for (int s = lane; s < 2 * nc * nc; s += 64) {
       const int c = s / (nc * nc), r = s - c * nc * nc;
@@ -285,8 +301,9 @@ __device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d,
     return;
   }
   const int log2 = t.log2, n = 1 << log2;
-  u8* plane = t.c == 0 ? y : uv + (t.c - 1);
+  P* plane = t.c == 0 ? y : uv + (t.c - 1);
   const int step = t.c == 0 ? 1 : 2;
+  const int bd = bd_of<P>(t.c == 0 ? d.bd_y : d.bd_c);
   const bool intra = t.flags & hevc::kTuIntra;
   const bool coef = t.flags & hevc::kTuCoef;
   const bool tskip = t.flags & hevc::kTuSkip;
@@ -312,7 +329,7 @@ __device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d,
   }
   const i16* dq = L.dq;
   if (intra)  // (uniform per wave)
-    prepare_refs_wave(d, t, plane, stride, step, lane, L);
+    prepare_refs_wave(d, t, plane, stride, step, lane, L, bd);
   const int mx = t.ext_x, my = t.ext_y;
   if (coef && !tskip && !bypass) {
     for (int s = lane; s < n * (mx + 1); s += 64) {
@@ -323,16 +340,23 @@ __device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d,
   }
   for (int s = lane; s < n * n; s += 64) {
     const int yy = s >> log2, xx = s & (n - 1);
-    u8& q = plane[(t.y + yy) * stride + (t.x + xx) * step];
-    int v = intra ? int(hevc::hk_intra_sample(L.top, L.left, log2, t.mode, t.c == 0, xx, yy)) : int(q);
-    if (coef) v += bypass ? int(dq[s]) : (tskip ? hevc::hk_tskip(dq[s]) : hevc::hk_itx_row(&L.g[yy * n], log2, dst, xx, mx));
-    const u8 o = hevc::hk_clip8(v);
+    P& q = plane[(t.y + yy) * stride + (t.x + xx) * step];
+    int v = intra ? hevc::hk_intra_sample(L.top, L.left, log2, t.mode, t.c == 0, xx, yy, bd) : int(q);
+    if (coef)
+      v += bypass ? int(dq[s]) : (tskip ? hevc::hk_tskip(dq[s], bd) : hevc::hk_itx_row(&L.g[yy * n], log2, dst, xx, mx, bd));
+    const P o = P(hevc::hk_clip(v, bd));
     q = o;
     if (publish) {  // the right column / bottom row other intra blocks of the launch may read
       if (xx == n - 1) xg_put(xg_col(d, t.c, t.x + xx, t.y + yy), d.epoch, o);
       if (yy == n - 1) xg_put(xg_row(d, t.c, t.x + xx, t.y + yy), d.epoch, o);
     }
   }
+}
+
+__device__ __attribute__((always_inline)) inline void tu_wave(const HevcDesc& d, const GpuTu& t, int lane, TuWave& L,
+                                                              bool publish) {
+  if (d.flags & kHevcWide) tu_wave_t<u16>(d, t, lane, L, publish);
+  else tu_wave_t<u8>(d, t, lane, L, publish);
 }
 
 // Independent blocks (level 0, or one intra level when levels are launched one by one):
@@ -409,6 +433,29 @@ __global__ __launch_bounds__(64 * kTuPicWaves) void hevc_tu_pic_kernel(const Hev
 }
 
 // ------------------------------------------------------------------------------ deblocking
+template <class P>
+__device__ __attribute__((always_inline)) inline void deblock_edge(const HevcDesc& d, int k, int x, int yy, int bs,
+                                                                   int dir) {
+  const int w4 = d.width >> 2;
+  const int stride = d.stride, bdy = bd_of<P>(d.bd_y), bdc = bd_of<P>(d.bd_c);
+  P* y = reinterpret_cast<P*>(d.y + size_t(d.target) * d.slot_y);
+  P* uv = reinterpret_cast<P*>(d.uv + size_t(d.target) * d.slot_uv);
+  const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? yy : yy - 1;
+  const int kp = (yp >> 2) * w4 + (xp >> 2);
+  const GpuSlice& sl =
+      static_cast<const GpuSlice*>(d.slices)[d.ctb_slice[(yy >> d.log2ctb) * d.wctb + (x >> d.log2ctb)]];
+  const bool nof = d.flags & 4;
+  const bool nfp = nof && d.pcm_map[kp], nfq = nof && d.pcm_map[k];
+  // (bS is non-zero only on the 8x8 grid)
+  hevc::HkLumaEdgeT<P> e{y + yy * stride + x, dir == 0 ? stride : 1, dir == 0 ? 1 : stride};
+  hevc::hk_deblock_luma(e, bs, (d.qp[kp] + d.qp[k] + 1) >> 1, sl.beta_offset, sl.tc_offset, nfp, nfq, bdy);
+  if (bs == 2 && ((dir == 0 ? x : yy) & 15) == 0)
+    for (int c = 0; c < 2; ++c)
+      hevc::hk_deblock_chroma(uv + (yy >> 1) * stride + x + c, dir == 0 ? stride : 2, dir == 0 ? 2 : stride,
+                              d.qp[kp], d.qp[k], c == 0 ? d.cb_qp_offset : d.cr_qp_offset, sl.tc_offset, nfp,
+                              nfq, bdc);
+}
+
 __global__ __launch_bounds__(256) void hevc_deblock_kernel(const HevcDesc* __restrict__ descs, int n, int total,
                                                           int dir) {
   const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
@@ -420,26 +467,13 @@ __global__ __launch_bounds__(256) void hevc_deblock_kernel(const HevcDesc* __res
   const u8* bsm = dir == 0 ? d.bs_v : d.bs_h;
   const int bs = bsm[k];
   if (!bs) return;
-  const int stride = d.stride;
-  u8* y = d.y + size_t(d.target) * d.slot_y;
-  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
-  const int xp = dir == 0 ? x - 1 : x, yp = dir == 0 ? yy : yy - 1;
-  const int kp = (yp >> 2) * w4 + (xp >> 2);
-  const GpuSlice& sl =
-      static_cast<const GpuSlice*>(d.slices)[d.ctb_slice[(yy >> d.log2ctb) * d.wctb + (x >> d.log2ctb)]];
-  const bool nof = d.flags & 4;
-  const bool nfp = nof && d.pcm_map[kp], nfq = nof && d.pcm_map[k];
-  // (bS is non-zero only on the 8x8 grid)
-  hevc::HkLumaEdge e{y + yy * stride + x, dir == 0 ? stride : 1, dir == 0 ? 1 : stride};
-  hevc::hk_deblock_luma(e, bs, (d.qp[kp] + d.qp[k] + 1) >> 1, sl.beta_offset, sl.tc_offset, nfp, nfq);
-  if (bs == 2 && ((dir == 0 ? x : yy) & 15) == 0)
-    for (int c = 0; c < 2; ++c)
-      hevc::hk_deblock_chroma(uv + (yy >> 1) * stride + x + c, dir == 0 ? stride : 2, dir == 0 ? 2 : stride,
-                              d.qp[kp], d.qp[k], c == 0 ? d.cb_qp_offset : d.cr_qp_offset, sl.tc_offset, nfp,
-                              nfq);
+  if (d.flags & kHevcWide) deblock_edge<u16>(d, k, x, yy, bs, dir);
+  else deblock_edge<u8>(d, k, x, yy, bs, dir);
 }
 
 // ------------------------------------------------------------------------------ SAO
+// The deblocked picture into the SAO scratch surface: 4 samples per row of the lane's 4x4 block
+// (one u32, or one u64 for u16 samples).
 __global__ __launch_bounds__(256) void hevc_sao_copy_kernel(const HevcDesc* __restrict__ descs, int n, int total) {
   const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
   if (b >= total) return;
@@ -450,6 +484,15 @@ __global__ __launch_bounds__(256) void hevc_sao_copy_kernel(const HevcDesc* __re
   const int stride = d.stride;
   const u8* y = d.y + size_t(d.target) * d.slot_y;
   const u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  if (d.flags & kHevcWide) {  // byte offsets of u16 samples: 8-byte aligned rows of 4
+    for (int j = 0; j < 4; ++j)
+      *reinterpret_cast<u64*>(d.sao_y + 2 * ((yy + j) * stride + x)) =
+          *reinterpret_cast<const u64*>(y + 2 * ((yy + j) * stride + x));
+    for (int j = 0; j < 2; ++j)
+      *reinterpret_cast<u64*>(d.sao_uv + 2 * (((yy >> 1) + j) * stride + x)) =
+          *reinterpret_cast<const u64*>(uv + 2 * (((yy >> 1) + j) * stride + x));
+    return;
+  }
   for (int j = 0; j < 4; ++j)
     *reinterpret_cast<u32*>(d.sao_y + (yy + j) * stride + x) = *reinterpret_cast<const u32*>(y + (yy + j) * stride + x);
   for (int j = 0; j < 2; ++j)
@@ -457,27 +500,22 @@ __global__ __launch_bounds__(256) void hevc_sao_copy_kernel(const HevcDesc* __re
         *reinterpret_cast<const u32*>(uv + ((yy >> 1) + j) * stride + x);
 }
 
-__global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restrict__ descs, int n, int total) {
-  const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
-  if (b >= total) return;
-  const HevcDesc& d = descs[pick_blk(descs, n, b)];
-  if (!(d.flags & 2)) return;
-  const int w4 = d.width >> 2, k = b - d.blk_begin;
-  const int x4 = (k % w4) << 2, y4 = (k / w4) << 2;
-  if ((d.flags & 4) && d.pcm_map[k]) return;
+template <class P>
+__device__ __attribute__((always_inline)) inline void sao_block(const HevcDesc& d, int x4, int y4) {
   const int ci = (y4 >> d.log2ctb) * d.wctb + (x4 >> d.log2ctb);
   const GpuSao sp = static_cast<const GpuSao*>(d.sao)[ci];
   const int si = d.ctb_slice[ci];
   const GpuSlice* slices = static_cast<const GpuSlice*>(d.slices);
   const GpuSlice sl = slices[si];
   const int stride = d.stride;
-  u8* y = d.y + size_t(d.target) * d.slot_y;
-  u8* uv = d.uv + size_t(d.target) * d.slot_uv;
+  P* y = reinterpret_cast<P*>(d.y + size_t(d.target) * d.slot_y);
+  P* uv = reinterpret_cast<P*>(d.uv + size_t(d.target) * d.slot_uv);
   for (int c = 0; c < 3; ++c) {
     if (!sp.type[c] || (c == 0 ? !sl.sao_luma : !sl.sao_chroma)) continue;
     const int sub = c ? 1 : 0, step = c ? 2 : 1;
-    const u8* src = c == 0 ? d.sao_y : d.sao_uv + (c - 1);
-    u8* dst = c == 0 ? y : uv + (c - 1);
+    const int bd = bd_of<P>(c ? d.bd_c : d.bd_y);
+    const P* src = c == 0 ? reinterpret_cast<const P*>(d.sao_y) : reinterpret_cast<const P*>(d.sao_uv) + (c - 1);
+    P* dst = c == 0 ? y : uv + (c - 1);
     const int pw = d.width >> sub, ph = d.height >> sub;
     auto nb_ok = [&](int nx, int ny) {
       if (nx < 0 || ny < 0 || nx >= pw || ny >= ph) return false;
@@ -491,11 +529,48 @@ __global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restric
     for (int j = 0; j < sz; ++j)
       for (int i = 0; i < sz; ++i)
         dst[(y0 + j) * stride + (x0 + i) * step] =
-            u8(hevc::hk_sao_sample(src, stride, step, sp, c, x0 + i, y0 + j, nb_ok));
+            P(hevc::hk_sao_sample(src, stride, step, sp, c, x0 + i, y0 + j, nb_ok, bd));
   }
 }
 
+__global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restrict__ descs, int n, int total) {
+  const int b = int(blockIdx.x * blockDim.x + threadIdx.x);
+  if (b >= total) return;
+  const HevcDesc& d = descs[pick_blk(descs, n, b)];
+  if (!(d.flags & 2)) return;
+  const int w4 = d.width >> 2, k = b - d.blk_begin;
+  const int x4 = (k % w4) << 2, y4 = (k / w4) << 2;
+  if ((d.flags & 4) && d.pcm_map[k]) return;
+  if (d.flags & kHevcWide) sao_block<u16>(d, x4, y4);
+  else sao_block<u8>(d, x4, y4);
+}
+
+// 8 samples per lane: one 16-byte load, one 8-byte store.
+__global__ __launch_bounds__(256) void narrow_kernel(const u16* __restrict__ y, const u16* __restrict__ uv,
+                                                    u8* __restrict__ y8, u8* __restrict__ uv8, size_t ny, int bd) {
+  const size_t g = size_t(blockIdx.x) * 256 + threadIdx.x, groups = (ny + ny / 2) / 8;
+  if (g >= groups) return;
+  const bool luma = g < ny / 8;
+  const size_t o = luma ? g * 8 : (g - ny / 8) * 8;
+  const uint4 v = *reinterpret_cast<const uint4*>((luma ? y : uv) + o);
+  const int sh = bd - 8, rnd = (1 << sh) >> 1;
+  const u32 w[4] = {v.x, v.y, v.z, v.w};
+  u32 out[2] = {0, 0};
+  for (int k = 0; k < 8; ++k) {
+    const int s = int((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
+    const int n = (s + rnd) >> sh;
+    out[k >> 2] |= u32(n > 255 ? 255 : n) << (8 * (k & 3));
+  }
+  *reinterpret_cast<uint2*>((luma ? y8 : uv8) + o) = make_uint2(out[0], out[1]);
+}
+
 }  // namespace
+
+void launch_narrow(const u16* y, const u16* uv, u8* y8, u8* uv8, size_t n, int bd, hipStream_t s) {
+  if (!n) return;
+  const size_t groups = (n + n / 2) / 8;
+  hipLaunchKernelGGL(narrow_kernel, dim3(unsigned((groups + 255) / 256)), dim3(256), 0, s, y, uv, y8, uv8, n, bd);
+}
 
 void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s) {
   if (n <= 0 || total_pus <= 0) return;

@@ -191,10 +191,11 @@ class CtuLayer {
       }
       if (!p.type[c]) continue;
       int abs[4];
-      for (int i = 0; i < 4; ++i) {  // TR cMax 7, bypass
+      const int cmax = (1 << (std::min(c ? pc_.bd_c : pc_.bd_y, 10) - 5)) - 1;  // 7 at 8 bits, 31 at 10
+      for (int i = 0; i < 4; ++i) {  // TR cMax, bypass
         const int a = std::abs(int(want.off[c][i]));
         int v = 0;
-        while (v < 7 && byp(a > v)) ++v;
+        while (v < cmax && byp(a > v)) ++v;
         abs[i] = v;
       }
       if (p.type[c] == 1) {
@@ -255,7 +256,11 @@ class CtuLayer {
     };
     return (qp_at(qg_x_ - 1, qg_y_) + qp_at(qg_x_, qg_y_ - 1) + 1) >> 1;
   }
-  int qp_y() const { return ((qp_pred_ + cu_qp_delta_ + 52) % 52); }
+  // QpY (§8.6.1), in -QpBdOffsetY .. 51
+  int qp_y() const {
+    const int off = pc_.qp_off_y;
+    return ((qp_pred_ + cu_qp_delta_ + 52 + 2 * off) % (52 + off)) - off;
+  }
 
   // f(k) for every 4x4 block index of the rectangle clipped to the picture: row by row over
   // consecutive indices (the per-block bookkeeping of skip-heavy pictures is a large share of
@@ -404,43 +409,67 @@ class CtuLayer {
   }
 
   // -------------------------------------------------------------------- PCM
-  void pcm_sample(int x0, int y0, int log2, const u8* want) {
+  void pcm_sample(int x0, int y0, int log2, const u16* want) {
+    // pcm_sample_luma / chroma: u(PcmBitDepth) each, MSB first, byte aligned; the sample is the
+    // value << (BitDepth - PcmBitDepth) (§8.4.4.1)
     const int n = 1 << log2, nc = n / 2;
     HostSurface& s = *pc_.s;
-    const size_t bytes = size_t(n) * n + 2 * size_t(nc) * nc;
-    VEP_CHECK(sps_.pcm_bit_depth_luma == 8 && sps_.pcm_bit_depth_chroma == 8, "PCM sample bit depth != 8");
-    const u8* src;
-    std::vector<u8> tmp;
+    const int pby = sps_.pcm_bit_depth_luma, pbc = sps_.pcm_bit_depth_chroma;
+    VEP_CHECK(pby >= 1 && pbc >= 1 && pby <= pc_.bd_y && pbc <= pc_.bd_c, "PCM bit depth above the sample bit depth");
+    const size_t nl = size_t(n) * n, ns = nl + 2 * size_t(nc) * nc;
+    const size_t bytes = (nl * size_t(pby) + (ns - nl) * size_t(pbc)) / 8;  // (n >= 8: whole bytes)
+    u16 v[64 * 64 + 2 * 32 * 32];
     if constexpr (kWrite) {
+      std::vector<u8> packed(bytes, 0);
+      size_t bit = 0;
+      for (size_t k = 0; k < ns; ++k) {
+        const int nb = k < nl ? pby : pbc;
+        for (int b = nb - 1; b >= 0; --b, ++bit)
+          if ((want[k] >> b) & 1) packed[bit >> 3] |= u8(0x80u >> (bit & 7));
+      }
       wr->align_zero();
-      wr->raw_bytes(want, bytes);
+      wr->raw_bytes(packed.data(), bytes);
       wr->start();
-      src = want;
+      for (size_t k = 0; k < ns; ++k) v[k] = u16(want[k] << (k < nl ? pc_.bd_y - pby : pc_.bd_c - pbc));
     } else {
       const size_t pos = rd->aligned_bytepos();
       VEP_CHECK(pos + bytes <= data_n, "PCM samples past the end of the slice");
-      src = data + pos;
+      const u8* src = data + pos;
       rd->start(pos + bytes);
+      size_t bit = 0;
+      for (size_t k = 0; k < ns; ++k) {
+        const int nb = k < nl ? pby : pbc;
+        u32 x = 0;
+        for (int b = 0; b < nb; ++b, ++bit) x = (x << 1) | ((src[bit >> 3] >> (7 - (bit & 7))) & 1u);
+        v[k] = u16(x << (k < nl ? pc_.bd_y - pby : pc_.bd_c - pbc));
+      }
       if (GpuPicture* g = g_) {  // records mode: the GPU copies the samples (level 0)
         GpuTu t{};
         t.x = u16(x0);
         t.y = u16(y0);
         t.log2 = u8(log2);
         t.flags = kTuPcm;
-        t.data = u32(g->pcm.size());
-        g->pcm.insert(g->pcm.end(), src, src + bytes);
+        if (g->wide()) {  // u16 samples (2-byte aligned)
+          if (g->pcm.size() & 1) g->pcm.push_back(0);
+          t.data = u32(g->pcm.size());
+          const u8* b = reinterpret_cast<const u8*>(v);
+          g->pcm.insert(g->pcm.end(), b, b + 2 * ns);
+        } else {
+          t.data = u32(g->pcm.size());
+          for (size_t k = 0; k < ns; ++k) g->pcm.push_back(u8(v[k]));
+        }
         g->tus.push_back(t);
         return;
       }
     }
-    for (int y = 0; y < n; ++y) std::memcpy(&s.y[size_t(y0 + y) * s.coded_w + size_t(x0)], src + size_t(y) * n, size_t(n));
-    const u8* cb = src + size_t(n) * n;
-    const u8* cr = cb + size_t(nc) * nc;
+    for (int y = 0; y < n; ++y)
+      for (int x = 0; x < n; ++x) s.set(0, x0 + x, y0 + y, v[size_t(y) * n + x]);
+    const u16* cb = v + nl;
+    const u16* cr = cb + size_t(nc) * nc;
     for (int y = 0; y < nc; ++y)
       for (int x = 0; x < nc; ++x) {
-        u8* d = &s.uv[size_t(y0 / 2 + y) * s.coded_w + size_t(x0 + 2 * x)];
-        d[0] = cb[y * nc + x];
-        d[1] = cr[y * nc + x];
+        s.set(1, x0 / 2 + x, y0 / 2 + y, cb[y * nc + x]);
+        s.set(2, x0 / 2 + x, y0 / 2 + y, cr[y * nc + x]);
       }
   }
 
@@ -647,16 +676,7 @@ class CtuLayer {
   // Records mode: index + 1 of the explicit weighting of a PU in the picture's weight table
   // (entries are shared by every PU with the same weights / offsets / shifts).
   u8 gpu_wp_index(const MvField& m) {
-    GpuWp e{};
-    const PredWeights& w = sh_.pwt;
-    for (int c = 0; c < 3; ++c) {
-      e.shift[c] = u8(w.log2_denom(c) + 6);  // log2WD = denom + shift1 (14 - bitDepth)
-      for (int l = 0; l < 2; ++l)
-        if ((m.pred >> l) & 1) {
-          e.w[l][c] = i16(w.w[l][m.ref[l]][c]);
-          e.o[l][c] = i16(w.o[l][m.ref[l]][c]);
-        }
-    }
+    const GpuWp e = explicit_weights(sh_, m, pc_.bd_y, pc_.bd_c);
     std::vector<GpuWp>& tab = g_->wp;
     for (size_t i = 0; i < tab.size(); ++i)
       if (std::memcmp(&tab[i], &e, sizeof e) == 0) return u8(i + 1);
@@ -691,17 +711,16 @@ class CtuLayer {
       return;
     }
     HostSurface& s = *pc_.s;
-    const int st = s.coded_w;
     for (int k = 0; k < cu_.npu; ++k) {
       const int x = cu_.pus[k][0], y = cu_.pus[k][1], w = cu_.pus[k][2], h = cu_.pus[k][3];
-      std::vector<u8> py(size_t(w) * h), pcb(size_t(w / 2) * (h / 2)), pcr(pcb.size());
+      std::vector<u16> py(size_t(w) * h), pcb(size_t(w / 2) * (h / 2)), pcr(pcb.size());
       predict_pu(pc_, si_, x, y, w, h, pc_.mf[pc_.i4(x, y)], py.data(), w, pcb.data(), pcr.data(), w / 2);
-      for (int j = 0; j < h; ++j) std::memcpy(&s.y[size_t(y + j) * st + size_t(x)], &py[size_t(j) * w], size_t(w));
+      for (int j = 0; j < h; ++j)
+        for (int i = 0; i < w; ++i) s.set(0, x + i, y + j, py[size_t(j) * w + i]);
       for (int j = 0; j < h / 2; ++j)
         for (int i = 0; i < w / 2; ++i) {
-          u8* d = &s.uv[size_t(y / 2 + j) * st + size_t(x + 2 * i)];
-          d[0] = pcb[size_t(j) * (w / 2) + i];
-          d[1] = pcr[size_t(j) * (w / 2) + i];
+          s.set(1, x / 2 + i, y / 2 + j, pcb[size_t(j) * (w / 2) + i]);
+          s.set(2, x / 2 + i, y / 2 + j, pcr[size_t(j) * (w / 2) + i]);
         }
     }
   }
@@ -724,12 +743,15 @@ class CtuLayer {
   bool plan_residual(const CuDesc& want) {
     const int n = 1 << cu_.log2;
     HostSurface& s = *pc_.s;
-    const int st = s.coded_w;
     // save the CU's samples and availability (the dry run reconstructs into them)
-    std::vector<u8> sy(size_t(n) * n), suv(size_t(n) * n / 2);
-    for (int j = 0; j < n; ++j) std::memcpy(&sy[size_t(j) * n], &s.y[size_t(cu_.y0 + j) * st + size_t(cu_.x0)], size_t(n));
+    std::vector<u16> sy(size_t(n) * n), suv(size_t(n) * n / 2);
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) sy[size_t(j) * n + i] = u16(s.get(0, cu_.x0 + i, cu_.y0 + j));
     for (int j = 0; j < n / 2; ++j)
-      std::memcpy(&suv[size_t(j) * n], &s.uv[size_t(cu_.y0 / 2 + j) * st + size_t(cu_.x0)], size_t(n));
+      for (int i = 0; i < n / 2; ++i) {
+        suv[size_t(j) * n + 2 * i] = u16(s.get(1, cu_.x0 / 2 + i, cu_.y0 / 2 + j));
+        suv[size_t(j) * n + 2 * i + 1] = u16(s.get(2, cu_.x0 / 2 + i, cu_.y0 / 2 + j));
+      }
     std::vector<u8> srec;
     for4(cu_.x0, cu_.y0, n, n, [&](size_t k) { srec.push_back(pc_.rec[k]); });
     levels_.clear();
@@ -744,9 +766,13 @@ class CtuLayer {
     dry_ = false;
     cu_qp_delta_ = saved_delta;
     qg_coded_ = saved_coded;
-    for (int j = 0; j < n; ++j) std::memcpy(&s.y[size_t(cu_.y0 + j) * st + size_t(cu_.x0)], &sy[size_t(j) * n], size_t(n));
+    for (int j = 0; j < n; ++j)
+      for (int i = 0; i < n; ++i) s.set(0, cu_.x0 + i, cu_.y0 + j, sy[size_t(j) * n + i]);
     for (int j = 0; j < n / 2; ++j)
-      std::memcpy(&s.uv[size_t(cu_.y0 / 2 + j) * st + size_t(cu_.x0)], &suv[size_t(j) * n], size_t(n));
+      for (int i = 0; i < n / 2; ++i) {
+        s.set(1, cu_.x0 / 2 + i, cu_.y0 / 2 + j, suv[size_t(j) * n + 2 * i]);
+        s.set(2, cu_.x0 / 2 + i, cu_.y0 / 2 + j, suv[size_t(j) * n + 2 * i + 1]);
+      }
     size_t i = 0;
     for4(cu_.x0, cu_.y0, n, n, [&](size_t k) { pc_.rec[k] = srec[i++]; });
     bool any = false;
@@ -836,14 +862,14 @@ class CtuLayer {
       if (p == 5) abs += egk(0, a - 5);
       int d = abs;
       if (abs) d = byp(v < 0) ? -abs : abs;
-      VEP_CHECK(d >= -26 && d <= 25, "cu_qp_delta out of range");
+      VEP_CHECK(d >= -(26 + pc_.qp_off_y / 2) && d <= 25 + pc_.qp_off_y / 2, "cu_qp_delta out of range");
       cu_qp_delta_ = d;
       qg_coded_ = true;
     }
     const int qp = qp_y();
-    // luma
+    // luma (Qp'Y = QpY + QpBdOffsetY)
     if (cu_.intra) intra_pred_block(0, x0, y0, log2);
-    residual_block(0, x0, y0, log2, cl, qp);
+    residual_block(0, x0, y0, log2, cl, qp + pc_.qp_off_y);
     {
       u8* const m_cbf = pc_.cbf.data();
       u8* const m_rec = pc_.rec.data();
@@ -856,11 +882,13 @@ class CtuLayer {
     }
     // chroma
     if (chroma_here || chroma_at_parent) {
-      const int qpi_cb = std::clamp(qp + pps_.cb_qp_offset + sh_.cb_qp_offset, -0, 57);
-      const int qpi_cr = std::clamp(qp + pps_.cr_qp_offset + sh_.cr_qp_offset, -0, 57);
+      // qPiCb / Cr = Clip3(-QpBdOffsetC, 57, QpY + offsets); Qp'C = table(qPi) + QpBdOffsetC
+      const int oc = pc_.qp_off_c;
+      const int qpi_cb = std::clamp(qp + pps_.cb_qp_offset + sh_.cb_qp_offset, -oc, 57);
+      const int qpi_cr = std::clamp(qp + pps_.cr_qp_offset + sh_.cr_qp_offset, -oc, 57);
       for (int c = 1; c <= 2; ++c) {
         if (cu_.intra) intra_pred_block(c, xc / 2, yc / 2, log2c);
-        residual_block(c, xc / 2, yc / 2, log2c, c == 1 ? cb : cr, hevc_chroma_qp(c == 1 ? qpi_cb : qpi_cr));
+        residual_block(c, xc / 2, yc / 2, log2c, c == 1 ? cb : cr, hevc_chroma_qp(c == 1 ? qpi_cb : qpi_cr) + oc);
       }
     }
   }
@@ -875,8 +903,8 @@ class CtuLayer {
       return;
     }
     HostSurface& s = *pc_.s;
-    const int st = s.coded_w;
     const int n = 1 << log2, sub = c ? 1 : 0;
+    const int bd = c ? pc_.bd_c : pc_.bd_y;
     const int mode = c == 0 ? cu_.ipm[cu_.part == 3 ? ((y0 - cu_.y0 >= (1 << cu_.log2) / 2) ? 2 : 0) +
                                                           ((x0 - cu_.x0 >= (1 << cu_.log2) / 2) ? 1 : 0)
                                                     : 0]
@@ -884,9 +912,7 @@ class CtuLayer {
     int top[129], left[128];
     bool av_t[129], av_l[128];
     const int lx = x0 << sub, ly = y0 << sub;  // luma location of the block
-    auto sample = [&](int x, int y) -> int {
-      return c == 0 ? s.y[size_t(y) * st + size_t(x)] : s.uv[size_t(y) * st + size_t(2 * x + c - 1)];
-    };
+    auto sample = [&](int x, int y) -> int { return s.get(c, x, y); };
     auto avail = [&](int x, int y) {  // component location
       const int xl = x << sub, yl = y << sub;
       if (!pc_.avail(lx, ly, xl, yl, pc_.rec)) return false;
@@ -903,8 +929,8 @@ class CtuLayer {
       if (av_l[i]) left[i] = sample(x0 - 1, y0 + i), ++navail;
     }
     if (!navail) {
-      for (int i = 0; i <= 2 * n; ++i) top[i] = 128;
-      for (int i = 0; i < 2 * n; ++i) left[i] = 128;
+      for (int i = 0; i <= 2 * n; ++i) top[i] = 1 << (bd - 1);
+      for (int i = 0; i < 2 * n; ++i) left[i] = 1 << (bd - 1);
     } else {
       // substitution (§8.4.4.2.2): scan from p[-1][2n-1] up to p[-1][-1], then p[0..2n-1][-1]
       auto get = [&](int k) -> int& { return k < 2 * n ? left[2 * n - 1 - k] : top[k - 2 * n]; };
@@ -918,14 +944,11 @@ class CtuLayer {
       for (int k = 1; k < total; ++k)
         if (!av(k)) get(k) = get(k - 1);
     }
-    if (c == 0) filter_intra_refs(top, left, log2, mode, sps_.strong_intra_smoothing);
-    std::vector<u8> pred(size_t(n) * n);
-    intra_predict(top, left, log2, mode, c == 0, pred.data(), n);
+    if (c == 0) filter_intra_refs(top, left, log2, mode, sps_.strong_intra_smoothing, bd);
+    u16 pred[32 * 32];
+    intra_predict(top, left, log2, mode, c == 0, pred, n, true, bd);
     for (int j = 0; j < n; ++j)
-      for (int i = 0; i < n; ++i) {
-        if (c == 0) s.y[size_t(y0 + j) * st + size_t(x0 + i)] = pred[size_t(j) * n + i];
-        else s.uv[size_t(y0 + j) * st + size_t(2 * (x0 + i) + c - 1)] = pred[size_t(j) * n + i];
-      }
+      for (int i = 0; i < n; ++i) s.set(c, x0 + i, y0 + j, pred[j * n + i]);
   }
 
   // Records mode: which reference units of the block are available (hk_prepare_refs mask) and
@@ -974,10 +997,7 @@ class CtuLayer {
       block_luma_mode_ = cu_.ipm[cu_.part == 3 ? ((y0 - cu_.y0 >= half) ? 2 : 0) + ((x0 - cu_.x0 >= half) ? 1 : 0) : 0];
     }
     HostSurface& s = *pc_.s;
-    const int st = s.coded_w;
-    auto px = [&](int i, int j) -> u8& {
-      return c == 0 ? s.y[size_t(y0 + j) * st + size_t(x0 + i)] : s.uv[size_t(y0 + j) * st + size_t(2 * (x0 + i) + c - 1)];
-    };
+    const int bd = c ? pc_.bd_c : pc_.bd_y;
     if (lvbuf_.size() < 1024) lvbuf_.resize(1024);
     int* lv = lvbuf_.data();
     const int nn = n * n;
@@ -987,9 +1007,9 @@ class CtuLayer {
     const TuKey key{c, x0, y0};
     if (dry_) {
       if constexpr (kWrite) {
-        std::vector<u8> pred(size_t(n) * n);
+        std::vector<u16> pred(size_t(n) * n);
         for (int j = 0; j < n; ++j)
-          for (int i = 0; i < n; ++i) pred[size_t(j) * n + i] = px(i, j);
+          for (int i = 0; i < n; ++i) pred[size_t(j) * n + i] = u16(s.get(c, x0 + i, y0 + j));
         const bool ts_ok = pps_.transform_skip && log2 == 2 && !cu_.bypass;
         bool ts = dry_tskip_ && ts_ok;
         dec_->residual(c, x0, y0, log2, pred.data(), n, qp, ts_ok, cu_.intra, lv, ts);
@@ -1050,7 +1070,7 @@ class CtuLayer {
         auto put = [&](int k) {
           nzpos_[np] = u16(k);
           nzval_[np++] =
-              byp ? i16(std::clamp(lv[k], -32768, 32767)) : i16(dequant_level(lv[k], qp, log2, m ? m[k] : 16));
+              byp ? i16(std::clamp(lv[k], -32768, 32767)) : i16(dequant_level(lv[k], qp, log2, m ? m[k] : 16, bd));
           ex = std::max(ex, k & (n - 1));
           ey = std::max(ey, k >> log2);
         };
@@ -1076,14 +1096,12 @@ class CtuLayer {
       for (size_t k = 0; k < d.size(); ++k) r[k] = lv[k];
     } else {
       const u8* m = scale_matrix(c, log2);
-      for (size_t k = 0; k < d.size(); ++k) d[k] = lv[k] ? dequant_level(lv[k], qp, log2, m ? m[k] : 16) : 0;
-      inverse_transform(d.data(), log2, c == 0 && log2 == 2 && cu_.intra, tskip, r.data());
+      for (size_t k = 0; k < d.size(); ++k) d[k] = lv[k] ? dequant_level(lv[k], qp, log2, m ? m[k] : 16, bd) : 0;
+      inverse_transform(d.data(), log2, c == 0 && log2 == 2 && cu_.intra, tskip, r.data(), bd);
     }
+    const int hi = (1 << bd) - 1;
     for (int j = 0; j < n; ++j)
-      for (int i = 0; i < n; ++i) {
-        u8& p = px(i, j);
-        p = u8(std::clamp(int(p) + r[size_t(j) * n + i], 0, 255));
-      }
+      for (int i = 0; i < n; ++i) s.set(c, x0 + i, y0 + j, std::clamp(s.get(c, x0 + i, y0 + j) + r[size_t(j) * n + i], 0, hi));
   }
 
   // ScalingFactor of the block (raster n x n) or null when scaling lists are off (m = 16)

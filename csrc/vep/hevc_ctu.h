@@ -38,6 +38,8 @@ struct PicCtx {
   int log2ctb = 4, wctb = 0, hctb = 0;
   int poc = 0;
   HostSurface* s = nullptr;   // target surface (reconstruction, then loop filters)
+  // sample bit depths and QpBdOffsetY / C (Main10: 10 / 12)
+  int bd_y = 8, bd_c = 8, qp_off_y = 0, qp_off_c = 0;
   // per 4x4 block
   std::vector<u8> depth, skip, intra, ipm, done, rec, pcm, cbf, edge;
   std::vector<i8> qp;
@@ -81,6 +83,10 @@ struct PicCtx {
     wctb = sp.width_ctbs();
     hctb = sp.height_ctbs();
     s = surf;
+    bd_y = sp.bit_depth_luma;
+    bd_c = sp.bit_depth_chroma;
+    qp_off_y = 6 * (bd_y - 8);
+    qp_off_c = 6 * (bd_c - 8);
     const size_t n = size_t(w4) * h4;
     if (depth.size() != n) {  // (every other per-4x4 array is written by the CU covering it
       depth.assign(n, 0);     // before anything reads it: only the decoded flags are reset)
@@ -203,7 +209,9 @@ void amvp_candidates(const PicCtx& pc, int si, int xCb, int yCb, int nCbS, int x
 
 // Sample prediction of one PU into 16-bit intermediate arrays (before weighting) and final
 // samples (tests / encoder).
-void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const MvField& m, u8* y, int ys, u8* cb,
-                u8* cr, int cs);
+void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const MvField& m, u16* y, int ys, u16* cb,
+                u16* cr, int cs);
+// Explicit weighting record of one PU for the components' bit depths (log2WD and scaled offsets).
+GpuWp explicit_weights(const SliceHeader& sh, const MvField& m, int bd_y, int bd_c);
 
 }  // namespace vep::hevc

@@ -20,9 +20,12 @@ bool is_bla(int t) { return t >= 16 && t <= 18; }
 
 void check_supported(const Sps& sps, const Pps& pps) {
   if (sps.chroma_format_idc != 1 || sps.separate_colour_plane) throw UnsupportedStream("HEVC: only 4:2:0 is supported");
-  if (sps.bit_depth_luma != 8 || sps.bit_depth_chroma != 8) throw UnsupportedStream("HEVC: only 8-bit (Main) is supported");
-  if (sps.pcm && (sps.pcm_bit_depth_luma != 8 || sps.pcm_bit_depth_chroma != 8))
-    throw UnsupportedStream("HEVC: PCM bit depth below 8 is not supported");
+  if (sps.bit_depth_luma < 8 || sps.bit_depth_luma > 10 || sps.bit_depth_chroma < 8 || sps.bit_depth_chroma > 10)
+    throw UnsupportedStream("HEVC: bit depth above 10 (only Main / Main10) is not supported");
+  if (sps.bit_depth_luma != sps.bit_depth_chroma)
+    throw UnsupportedStream("HEVC: different luma and chroma bit depths are not supported");
+  if (sps.pcm && (sps.pcm_bit_depth_luma > sps.bit_depth_luma || sps.pcm_bit_depth_chroma > sps.bit_depth_chroma))
+    throw Error("HEVC: PCM bit depth above the sample bit depth");
   VEP_CHECK(sps.width > 0 && sps.height > 0 && sps.width % (1 << sps.log2_min_cb) == 0 &&
                 sps.height % (1 << sps.log2_min_cb) == 0,
             "HEVC: picture size must be a multiple of the minimum CU");
@@ -64,10 +67,11 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   }
   // only a picture that starts a new coded video sequence may change the picture size (a mid-GOP
   // SPS with another size would have the picture predict from surfaces of the old size)
-  if (!(irap && no_rasl_output_) && act_w_ && (sps.width != act_w_ || sps.height != act_h_))
-    throw Error("HEVC: picture size changed outside an IRAP picture");
+  if (!(irap && no_rasl_output_) && act_w_ && (sps.width != act_w_ || sps.height != act_h_ || sps.bit_depth_luma != act_bd_))
+    throw Error("HEVC: picture size or bit depth changed outside an IRAP picture");
   act_w_ = sps.width;  // (by value: a repeated SPS NAL replaces the map entry sps_act_ points at)
   act_h_ = sps.height;
+  act_bd_ = sps.bit_depth_luma;
   // picture order count (§8.3.1)
   const int max_lsb = 1 << sps.log2_max_poc_lsb;
   int msb = 0;
@@ -159,7 +163,7 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
     VEP_CHECK(slot < gpu_slots_, "HEVC: no free DPB surface");
     cur_->slot = slot;
   } else {
-    cur_->s.alloc(sps.width, sps.height);
+    cur_->s.alloc(sps.width, sps.height, sps.bit_depth_luma);
   }
   cur_->poc = poc;
   cur_->uid = next_uid_++;
@@ -207,6 +211,8 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
       g = std::move(fresh);
     });
     cur_gpu_->target = cur_->slot;
+    cur_gpu_->bd_y = sps.bit_depth_luma;
+    cur_gpu_->bd_c = sps.bit_depth_chroma;
     pc_->init_gpu(cur_gpu_.get());
   }
 }
@@ -240,8 +246,8 @@ void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
     decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
     return;
   }
-  si.qp = pps_act_->init_qp + sh.qp_delta;
-  VEP_CHECK(si.qp >= 0 && si.qp <= 51, "HEVC: slice QP out of range");
+  si.qp = pps_act_->init_qp + sh.qp_delta;  // SliceQpY, -QpBdOffsetY .. 51
+  VEP_CHECK(si.qp >= -pc_->qp_off_y && si.qp <= 51, "HEVC: slice QP out of range");
   si.ord = pc_->slices.empty() ? 0 : pc_->slices.back().ord + 1;
   si.addr_rs = sh.segment_address;
   if (si.ord > 0) pc_->multi = true;
@@ -312,6 +318,8 @@ void Decoder::run_deferred(bool parallel) {
     sh.g.coefs.clear();
     sh.g.pcm.clear();
     sh.g.wp.clear();
+    sh.g.bd_y = pc.bd_y;
+    sh.g.bd_c = pc.bd_c;
     sh.stats = {};
     sh.any_bypass = false;
     sh.ctus = 0;

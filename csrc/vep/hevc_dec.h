@@ -1,4 +1,4 @@
-// General H.265/HEVC Main-profile decoder (8-bit 4:2:0, progressive): I, P and B slices with
+// General H.265/HEVC Main / Main10 decoder (8..10-bit 4:2:0, progressive): I, P and B slices with
 // CABAC coding quadtrees (CTB 16..64, CU 8..64, all partition modes incl. AMP), intra prediction
 // (35 modes, reference substitution / smoothing, strong intra smoothing), PCM, transform trees
 // (4..32 DCT, 4x4 DST, transform skip, sign data hiding, cu_qp_delta), merge / AMVP with
@@ -12,8 +12,10 @@
 // over the finished picture. This is the CPU reference of the H.265 path (bit-exact oracle for
 // GPU reconstruction kernels). Also: tiles, wavefront (WPP) substreams, dependent slice
 // segments, long-term reference pictures, explicit weighted prediction, scaling lists and
-// transquant-bypass (lossless) CUs. Range extensions (non-4:2:0, > 8 bit) are reported as
-// UnsupportedStream.
+// transquant-bypass (lossless) CUs. Main10: 9..10-bit samples are kept in 16-bit surfaces
+// (HostSurface::y16 / uv16; QpBdOffset, bit-depth shifts of MC / transforms / loop filters,
+// 10-bit SAO offsets, PCM at any PCM bit depth). Range extensions (non-4:2:0, > 10 bit,
+// different luma / chroma bit depths) are reported as UnsupportedStream.
 //
 // Reference parity: libavcodec's hevc decoder behind PyAV (python/read_image.py:87
 // `p.decode()`), BASELINE config 5 (H.265 cameras). No third-party HEVC stream exists in this
@@ -73,7 +75,7 @@ struct CuDesc {
   bool bypass = false;        // cu_transquant_bypass_flag (lossless CU)
   int part = 0;               // PartMode: 0 2Nx2N 1 2NxN 2 Nx2N 3 NxN 4 2NxnU 5 2NxnD 6 nLx2N 7 nRx2N
   bool pcm = false;
-  const u8* pcm_samples = nullptr;  // (2N)^2 luma then 2 * N^2 chroma
+  const u16* pcm_samples = nullptr;  // (2N)^2 luma then 2 * N^2 chroma (at the PCM bit depths)
   int luma_mode[4] = {1, 1, 1, 1};  // IntraPredModeY per partition
   int chroma_mode = 4;              // intra_chroma_pred_mode (4 = DM)
   struct Pu {
@@ -92,7 +94,7 @@ struct CuDesc {
 // Supplies levels for one transform block in write mode: `pred` is the prediction (stride
 // `pstride`), `src` the source samples, the levels go to `lv` (raster n x n). Returns whether the
 // block is coded with transform skip (4x4 only).
-using ResidualFn = std::function<void(int c, int x0, int y0, int log2, const u8* pred, int pstride, int qp,
+using ResidualFn = std::function<void(int c, int x0, int y0, int log2, const u16* pred, int pstride, int qp,
                                       bool tskip_allowed, bool intra, int* lv, bool& tskip)>;
 
 struct PicCtx;
@@ -142,6 +144,7 @@ class Decoder {
   std::vector<u8> rbsp_;
   int prev_tid0_poc_ = 0;
   int act_w_ = 0, act_h_ = 0;  // picture size of the active coded video sequence
+  int act_bd_ = 8;             // and its bit depth
   bool first_ = true, no_rasl_output_ = true, skip_pic_ = false;
   u32 next_uid_ = 1;
   bool gpu_mode_ = false;
@@ -194,6 +197,7 @@ struct HevcEncConfig {
   bool weighted = false;             // explicit weighted prediction in P and B slices
   bool long_term = false;            // each GOP's IDR stays referenced as a long-term picture
   bool lossless = false;             // transquant bypass enabled (coverage: lossless CUs)
+  int bit_depth = 8;                 // 8 (Main) or 10 (Main10: 10-bit samples, 16-bit surfaces)
   bool coverage = false;
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;

@@ -112,7 +112,8 @@ struct HevcEncoder::Impl : CtuDecider {
   i64 last_pts = 0;
   char last_type = 'I';
   HostSurface recon_out, src_out;
-  std::vector<u8> pcm_buf;
+  std::vector<u16> pcm_buf;
+  int bd = 8;                // sample bit depth (Main10: 10)
   FramePtr lt_pic;         // long_term: the GOP's IDR, referenced as a long-term picture
   bool cur_bypass = false; // the CU being coded is lossless (transquant bypass)
 
@@ -121,6 +122,8 @@ struct HevcEncoder::Impl : CtuDecider {
               "encoder size must be even and >= 16");
     VEP_CHECK(c.log2_ctb >= 4 && c.log2_ctb <= 6 && c.log2_min_cb == 3, "log2_ctb 4..6, log2_min_cb 3");
     VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
+    VEP_CHECK(c.bit_depth >= 8 && c.bit_depth <= 10, "encoder bit depth 8..10");
+    bd = c.bit_depth;
     W = (c.width + 7) & ~7;
     H = (c.height + 7) & ~7;
     const bool cov = c.coverage;
@@ -141,6 +144,14 @@ struct HevcEncoder::Impl : CtuDecider {
     sps.log2_min_pcm = 3;
     sps.log2_max_pcm = std::min(5, c.log2_ctb);
     sps.pcm_loop_filter_disabled = cov ? rng.chance(50) : true;
+    sps.bit_depth_luma = sps.bit_depth_chroma = bd;
+    sps.pcm_bit_depth_luma = sps.pcm_bit_depth_chroma = 8;
+    if (bd > 8) {  // Main10 (general_profile_idc 2); PCM below the sample bit depth in coverage
+      sps.ptl.profile_idc = vps.ptl.profile_idc = 2;
+      sps.ptl.compat_flags = vps.ptl.compat_flags = 1u << 29;  // general_profile_compatibility_flag[2]
+      sps.pcm_bit_depth_luma = cov ? 6 + rng.uni(bd - 5) : bd;
+      sps.pcm_bit_depth_chroma = cov ? 6 + rng.uni(bd - 5) : bd;
+    }
     sps.temporal_mvp = c.tmvp;
     sps.strong_intra_smoothing = true;
     keep_refs = 2;
@@ -175,7 +186,7 @@ struct HevcEncoder::Impl : CtuDecider {
     nal(write_sps(sps), sps_nal);
     nal(write_pps(pps), pps_nal);
     scene.make(SceneConfig{c.width, c.height, W, H, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
-    residual = [this](int ci, int x0, int y0, int log2, const u8* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
+    residual = [this](int ci, int x0, int y0, int log2, const u16* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
                       bool& ts) { this->make_residual(ci, x0, y0, log2, pred, ps, qp, ts_ok, intra, lv, ts); };
   }
 
@@ -248,7 +259,16 @@ struct HevcEncoder::Impl : CtuDecider {
       if (rendered > 0) scene.advance();
       scene.render();
       scene.add_sensor_noise(rendered);
-      sources[rendered] = scene.src;
+      if (bd > 8) {  // 10-bit source: the 8-bit scene << 2 plus a position / time dither in the low bits
+        HostSurface& w = sources[rendered];
+        w.alloc(scene.src.coded_w, scene.src.coded_h, bd);
+        const int sh = bd - 8;
+        auto lo = [&](size_t i) { return u16((i * 2654435761u + u64(rendered) * 40503u) >> 29) & ((1u << sh) - 1); };
+        for (size_t i = 0; i < w.y16.size(); ++i) w.y16[i] = u16(scene.src.y[i] << sh | lo(i));
+        for (size_t i = 0; i < w.uv16.size(); ++i) w.uv16[i] = u16(scene.src.uv[i] << sh | lo(i + 7));
+      } else {
+        sources[rendered] = scene.src;
+      }
     }
     return sources.at(d);
   }
@@ -285,7 +305,7 @@ struct HevcEncoder::Impl : CtuDecider {
       p.band[c] = u8(rng.uni(32));
       p.eo[c] = u8(c == 2 ? p.eo[1] : rng.uni(4));
       for (int i = 0; i < 4; ++i) {
-        const int a = rng.uni(8);
+        const int a = rng.uni(bd > 8 ? 32 : 8);  // (SAO offsets up to 31 at 10 bits)
         p.off[c][i] = i8(p.type[c] == 1 && rng.chance(50) ? -a : a);
       }
     }
@@ -296,7 +316,7 @@ struct HevcEncoder::Impl : CtuDecider {
     for (int j = 0; j < n; ++j)
       for (int i = 0; i < n; ++i) {
         const int rx = std::clamp(x0 + i + mvx, 0, W - 1), ry = std::clamp(y0 + j + mvy, 0, H - 1);
-        s += std::abs(int(cur_src->y[size_t(y0 + j) * W + size_t(x0 + i)]) - int(ref.y[size_t(ry) * W + size_t(rx)]));
+        s += std::abs(cur_src->get(0, x0 + i, y0 + j) - ref.get(0, rx, ry));
       }
     return s;
   }
@@ -332,8 +352,8 @@ struct HevcEncoder::Impl : CtuDecider {
       s = sad_block(sl.list[l][size_t(mc[k].ref[l])]->s, x0, y0, n, mc[k].mv[l][0] >> 2, mc[k].mv[l][1] >> 2);
       if (s < best) best = s, best_m = k;
     }
-    const double qstep = std::pow(2.0, (cur_qp - 4) / 6.0);
-    if (best_m >= 0 && best < int(n * n * std::max(1.5, qstep * 0.15))) {
+    const double qstep = std::pow(2.0, (cur_qp + pc.qp_off_y - 4) / 6.0);  // (SADs at the bit depth)
+    if (best_m >= 0 && best < int(n * n * std::max(1.5 * (1 << (bd - 8)), qstep * 0.15))) {
       d.skip = true;
       d.pu[0].merge = true;
       d.pu[0].merge_idx = best_m;
@@ -359,7 +379,7 @@ struct HevcEncoder::Impl : CtuDecider {
       d.tu_log2 = std::min(log2, 4);
       return;
     }
-    if (bs > n * n * 40) {  // nothing matches: intra
+    if (bs > n * n * (40 << (bd - 8))) {  // nothing matches: intra
       d.intra = true;
       return;
     }
@@ -391,12 +411,12 @@ struct HevcEncoder::Impl : CtuDecider {
       if (d.part == 0 && sps.pcm && log2 >= sps.log2_min_pcm && log2 <= sps.log2_max_pcm && rng.chance(6)) {
         d.pcm = true;
         pcm_buf.clear();
+        const int shy = bd - sps.pcm_bit_depth_luma, shc = bd - sps.pcm_bit_depth_chroma;
         for (int j = 0; j < n; ++j)
-          for (int i = 0; i < n; ++i) pcm_buf.push_back(cur_src->y[size_t(y0 + j) * W + size_t(x0 + i)]);
+          for (int i = 0; i < n; ++i) pcm_buf.push_back(u16(cur_src->get(0, x0 + i, y0 + j) >> shy));
         for (int c = 0; c < 2; ++c)
           for (int j = 0; j < n / 2; ++j)
-            for (int i = 0; i < n / 2; ++i)
-              pcm_buf.push_back(cur_src->uv[size_t(y0 / 2 + j) * W + size_t(x0 + 2 * i + c)]);
+            for (int i = 0; i < n / 2; ++i) pcm_buf.push_back(u16(cur_src->get(1 + c, x0 / 2 + i, y0 / 2 + j) >> shc));
         d.pcm_samples = pcm_buf.data();
       }
       return;
@@ -435,16 +455,13 @@ struct HevcEncoder::Impl : CtuDecider {
     }
   }
 
-  void make_residual(int c, int x0, int y0, int log2, const u8* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
+  // qp: Qp' of the component (QpBdOffset included: the level scale is then bit-depth free)
+  void make_residual(int c, int x0, int y0, int log2, const u16* pred, int ps, int qp, bool ts_ok, bool intra, int* lv,
                      bool& ts) {
     const int n = 1 << log2;
     std::vector<int> res(size_t(n) * n);
     for (int j = 0; j < n; ++j)
-      for (int i = 0; i < n; ++i) {
-        const int s = c == 0 ? cur_src->y[size_t(y0 + j) * W + size_t(x0 + i)]
-                             : cur_src->uv[size_t(y0 + j) * W + size_t(2 * (x0 + i) + c - 1)];
-        res[size_t(j) * n + i] = s - int(pred[size_t(j) * ps + i]);
-      }
+      for (int i = 0; i < n; ++i) res[size_t(j) * n + i] = cur_src->get(c, x0 + i, y0 + j) - int(pred[size_t(j) * ps + i]);
     if (cur_bypass) {  // lossless CU: the levels are the residual
       ts = false;
       for (int k = 0; k < n * n; ++k) lv[k] = res[size_t(k)];
@@ -584,7 +601,7 @@ struct HevcEncoder::Impl : CtuDecider {
     cur_src = &source_of(job.disp);
     cur_type = job.type;
     cur = std::make_shared<HevcFrame>();
-    cur->s.alloc(W, H);
+    cur->s.alloc(W, H, bd);
     cur->poc = poc;
     cur->is_ref = job.ref;
     // reference picture set: every kept anchor; used = the ones this picture predicts from

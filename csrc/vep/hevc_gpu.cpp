@@ -69,7 +69,7 @@ void finish_gpu_picture(PicCtx& pc) {
 namespace {
 
 // One transform block: residual into `res` (n x n raster).
-void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
+void tu_residual(const GpuPicture& p, const GpuTu& t, int* res, int bd) {
   const int log2 = t.log2, n = 1 << log2;
   i16 d[32 * 32];
   hk_sparse_expand(p.coefs.data() + t.data, log2, d);
@@ -78,7 +78,7 @@ void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
     return;
   }
   if (t.flags & kTuSkip) {
-    for (int k = 0; k < n * n; ++k) res[k] = hk_tskip(d[k]);
+    for (int k = 0; k < n * n; ++k) res[k] = hk_tskip(d[k], bd);
     return;
   }
   const int mx = t.ext_x, my = t.ext_y;
@@ -87,8 +87,16 @@ void tu_residual(const GpuPicture& p, const GpuTu& t, int* res) {
   for (int y = 0; y < n; ++y)
     for (int x = 0; x <= mx; ++x) g[y * n + x] = hk_itx_col(d, log2, dst, y, x, my);
   for (int y = 0; y < n; ++y)
-    for (int x = 0; x < n; ++x) res[y * n + x] = hk_itx_row(g + y * n, log2, dst, x, mx);
+    for (int x = 0; x < n; ++x) res[y * n + x] = hk_itx_row(g + y * n, log2, dst, x, mx, bd);
 }
+
+// the planes of a surface as the sample type of the picture
+template <class P> P* yplane(HostSurface& s);
+template <class P> P* uvplane(HostSurface& s);
+template <> u8* yplane<u8>(HostSurface& s) { return s.y.data(); }
+template <> u8* uvplane<u8>(HostSurface& s) { return s.uv.data(); }
+template <> u16* yplane<u16>(HostSurface& s) { return s.y16.data(); }
+template <> u16* uvplane<u16>(HostSurface& s) { return s.uv16.data(); }
 
 }  // namespace
 
@@ -130,25 +138,32 @@ u64 exchange_violations(const GpuPicture& p) {
   return bad;
 }
 
-void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
+template <class P>
+static void execute_planes(const GpuPicture& p, std::vector<HostSurface>& slots) {
   HostSurface& s = slots[size_t(p.target)];
+  P* const SY = yplane<P>(s);
+  P* const SUV = uvplane<P>(s);
+  const int bdy = p.bd_y, bdc = p.bd_c;
   const int stride = s.coded_w, W = p.width, H = p.height;
   // pass 1: motion compensation
   for (const GpuPu& u : p.pus) {
     const bool bi = u.pred == 3;
     const GpuWp* wp = u.wp ? &p.wp[size_t(u.wp) - 1] : nullptr;
     const int ul = (u.pred & 1) ? 0 : 1;
-    auto fin = [&](int c, int p0, int p1) { return wp ? hk_weight_explicit(*wp, c, p0, p1, bi, ul) : hk_weight(p0, p1, bi); };
+    auto fin = [&](int c, int p0, int p1) {
+      const int bd = c ? bdc : bdy;
+      return P(wp ? hk_weight_explicit(*wp, c, p0, p1, bi, ul, bd) : hk_weight(p0, p1, bi, bd));
+    };
     for (int j = 0; j < u.h; ++j)
       for (int i = 0; i < u.w; ++i) {
         int v[2] = {0, 0}, nv = 0;
         for (int l = 0; l < 2; ++l) {
           if (!((u.pred >> l) & 1)) continue;
-          const HostSurface& r = slots[size_t(u.slot[l])];
-          v[nv++] = hk_luma_mc(r.y.data(), stride, W, H, u.x + i + (u.mv[l][0] >> 2), u.y + j + (u.mv[l][1] >> 2),
-                               u.mv[l][0] & 3, u.mv[l][1] & 3);
+          const P* r = yplane<P>(slots[size_t(u.slot[l])]);
+          v[nv++] = hk_luma_mc(r, stride, W, H, u.x + i + (u.mv[l][0] >> 2), u.y + j + (u.mv[l][1] >> 2),
+                               u.mv[l][0] & 3, u.mv[l][1] & 3, bdy);
         }
-        s.y[size_t(u.y + j) * stride + size_t(u.x + i)] = fin(0, v[0], v[1]);
+        SY[size_t(u.y + j) * stride + size_t(u.x + i)] = fin(0, v[0], v[1]);
       }
     for (int c = 0; c < 2; ++c)
       for (int j = 0; j < u.h / 2; ++j)
@@ -156,11 +171,11 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
           int v[2] = {0, 0}, nv = 0;
           for (int l = 0; l < 2; ++l) {
             if (!((u.pred >> l) & 1)) continue;
-            const HostSurface& r = slots[size_t(u.slot[l])];
-            v[nv++] = hk_chroma_mc(r.uv.data(), stride, W / 2, H / 2, c, u.x / 2 + i + (u.mv[l][0] >> 3),
-                                   u.y / 2 + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7);
+            const P* r = uvplane<P>(slots[size_t(u.slot[l])]);
+            v[nv++] = hk_chroma_mc(r, stride, W / 2, H / 2, c, u.x / 2 + i + (u.mv[l][0] >> 3),
+                                   u.y / 2 + j + (u.mv[l][1] >> 3), u.mv[l][0] & 7, u.mv[l][1] & 7, bdc);
           }
-          s.uv[size_t(u.y / 2 + j) * stride + size_t(u.x + 2 * i + c)] = fin(1 + c, v[0], v[1]);
+          SUV[size_t(u.y / 2 + j) * stride + size_t(u.x + 2 * i + c)] = fin(1 + c, v[0], v[1]);
         }
   }
   // pass 2+: transform blocks by level (0: inter residual and PCM; then intra levels)
@@ -168,33 +183,36 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
   for (const GpuTu& t : p.tus) {
     if (t.flags & kTuPcm) {
       const int n = 1 << t.log2, nc = n / 2;
-      const u8* src = p.pcm.data() + t.data;
-      for (int y = 0; y < n; ++y) std::memcpy(&s.y[size_t(t.y + y) * stride + t.x], src + y * n, size_t(n));
-      const u8* cb = src + n * n;
-      const u8* cr = cb + nc * nc;
+      const P* src = reinterpret_cast<const P*>(p.pcm.data() + t.data);
+      for (int y = 0; y < n; ++y)
+        for (int x = 0; x < n; ++x) SY[size_t(t.y + y) * stride + t.x + x] = src[y * n + x];
+      const P* cb = src + n * n;
+      const P* cr = cb + nc * nc;
       for (int y = 0; y < nc; ++y)
         for (int x = 0; x < nc; ++x) {
-          s.uv[size_t(t.y / 2 + y) * stride + size_t(t.x + 2 * x)] = cb[y * nc + x];
-          s.uv[size_t(t.y / 2 + y) * stride + size_t(t.x + 2 * x + 1)] = cr[y * nc + x];
+          SUV[size_t(t.y / 2 + y) * stride + size_t(t.x + 2 * x)] = cb[y * nc + x];
+          SUV[size_t(t.y / 2 + y) * stride + size_t(t.x + 2 * x + 1)] = cr[y * nc + x];
         }
       continue;
     }
     const int n = 1 << t.log2;
-    u8* plane = t.c == 0 ? s.y.data() : s.uv.data() + (t.c - 1);
+    P* plane = t.c == 0 ? SY : SUV + (t.c - 1);
     const int step = t.c == 0 ? 1 : 2;
+    const int bd = t.c == 0 ? bdy : bdc;
     if (t.flags & kTuIntra) {
       int top[129], left[128];
-      hk_prepare_refs(plane, stride, step, t.x, t.y, t.log2, t.c == 0, t.avail, t.mode, t.flags & kTuStrong, top, left);
+      hk_prepare_refs(plane, stride, step, t.x, t.y, t.log2, t.c == 0, t.avail, t.mode, t.flags & kTuStrong, top, left,
+                      bd);
       for (int y = 0; y < n; ++y)
         for (int x = 0; x < n; ++x)
-          plane[(t.y + y) * stride + (t.x + x) * step] = hk_intra_sample(top, left, t.log2, t.mode, t.c == 0, x, y);
+          plane[(t.y + y) * stride + (t.x + x) * step] = P(hk_intra_sample(top, left, t.log2, t.mode, t.c == 0, x, y, bd));
     }
     if (t.flags & kTuCoef) {
-      tu_residual(p, t, res);
+      tu_residual(p, t, res, bd);
       for (int y = 0; y < n; ++y)
         for (int x = 0; x < n; ++x) {
-          u8& q = plane[(t.y + y) * stride + (t.x + x) * step];
-          q = hk_clip8(int(q) + res[y * n + x]);
+          P& q = plane[(t.y + y) * stride + (t.x + x) * step];
+          q = P(hk_clip(int(q) + res[y * n + x], bd));
         }
     }
   }
@@ -212,8 +230,8 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
           const size_t kp = size_t(yp >> 2) * w4 + size_t(xp >> 2), kq = size_t(y >> 2) * w4 + size_t(x >> 2);
           const GpuSlice& sl = p.slices[p.ctb_slice[size_t(ctb(x, y))]];
           const bool nfp = p.pcm_nofilter && p.pcm_map[kp], nfq = p.pcm_nofilter && p.pcm_map[kq];
-          HkLumaEdge e{&s.y[size_t(y) * stride + size_t(x)], dir == 0 ? stride : 1, dir == 0 ? 1 : stride};
-          hk_deblock_luma(e, b, (p.qp[kp] + p.qp[kq] + 1) >> 1, sl.beta_offset, sl.tc_offset, nfp, nfq);
+          HkLumaEdgeT<P> e{&SY[size_t(y) * stride + size_t(x)], dir == 0 ? stride : 1, dir == 0 ? 1 : stride};
+          hk_deblock_luma(e, b, (p.qp[kp] + p.qp[kq] + 1) >> 1, sl.beta_offset, sl.tc_offset, nfp, nfq, bdy);
         }
       for (int y = 0; y < H; y += 4)
         for (int x = 0; x < W; x += 4) {
@@ -225,16 +243,16 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
           const GpuSlice& sl = p.slices[p.ctb_slice[size_t(ctb(x, y))]];
           const bool nfp = p.pcm_nofilter && p.pcm_map[kp], nfq = p.pcm_nofilter && p.pcm_map[kq];
           for (int c = 0; c < 2; ++c) {
-            u8* q = &s.uv[size_t(y / 2) * stride + size_t(x + c)];
+            P* q = &SUV[size_t(y / 2) * stride + size_t(x + c)];
             hk_deblock_chroma(q, dir == 0 ? stride : 2, dir == 0 ? 2 : stride, p.qp[kp], p.qp[kq],
-                              c == 0 ? p.cb_qp_offset : p.cr_qp_offset, sl.tc_offset, nfp, nfq);
+                              c == 0 ? p.cb_qp_offset : p.cr_qp_offset, sl.tc_offset, nfp, nfq, bdc);
           }
         }
     }
   }
   // SAO from a copy of the deblocked picture
   if (p.sao) {
-    const HostSurface src = s;
+    HostSurface src = s;
     const int ctbs = 1 << p.log2ctb;
     for (int ry = 0; ry < p.hctb; ++ry)
       for (int rx = 0; rx < p.wctb; ++rx) {
@@ -245,8 +263,9 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
         for (int c = 0; c < 3; ++c) {
           if (!sp.type[c] || (c == 0 ? !sl.sao_luma : !sl.sao_chroma)) continue;
           const int sub = c ? 1 : 0, step = c ? 2 : 1;
-          const u8* splane = c == 0 ? src.y.data() : src.uv.data() + (c - 1);
-          u8* dplane = c == 0 ? s.y.data() : s.uv.data() + (c - 1);
+          const P* splane = c == 0 ? yplane<P>(src) : uvplane<P>(src) + (c - 1);
+          P* dplane = c == 0 ? SY : SUV + (c - 1);
+          const int bd = c ? bdc : bdy;
           const int pw = W >> sub, ph = H >> sub;
           const int x0 = (rx * ctbs) >> sub, y0 = (ry * ctbs) >> sub;
           const int x1 = std::min(x0 + (ctbs >> sub), pw), y1 = std::min(y0 + (ctbs >> sub), ph);
@@ -261,11 +280,20 @@ void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
                 if (nsi == si) return true;
                 return nsi > si ? bool(p.slices[size_t(nsi)].across) : bool(sl.across);
               };
-              dplane[y * stride + x * step] = u8(hk_sao_sample(splane, stride, step, sp, c, x, y, nb_ok));
+              dplane[y * stride + x * step] = P(hk_sao_sample(splane, stride, step, sp, c, x, y, nb_ok, bd));
             }
         }
       }
   }
+}
+
+void cpu_execute(const GpuPicture& p, std::vector<HostSurface>& slots) {
+  HostSurface& s = slots[size_t(p.target)];
+  const int bd = std::max(p.bd_y, p.bd_c);
+  for (HostSurface& h : slots)  // (a CVS with another bit depth: the camera's surfaces follow it)
+    if (h.bd != bd) h.alloc(s.coded_w, s.coded_h, bd);
+  if (p.wide()) execute_planes<u16>(p, slots);
+  else execute_planes<u8>(p, slots);
 }
 
 }  // namespace vep::hevc

@@ -109,7 +109,11 @@ struct GpuPicture {
   int width = 0, height = 0, log2ctb = 4, wctb = 0, hctb = 0;
   int target = 0;                     // DPB slot being reconstructed
   int cb_qp_offset = 0, cr_qp_offset = 0;
+  // sample bit depths (Main10: up to 10; the surfaces then hold one u16 per sample and `pcm`
+  // holds the PCM samples as u16, already scaled to the bit depth)
+  int bd_y = 8, bd_c = 8;
   bool deblock = false, sao = false, pcm_nofilter = false, constrained_intra = false;
+  bool wide() const { return bd_y > 8 || bd_c > 8; }
   std::vector<GpuPu> pus;
   std::vector<GpuTu> tus;             // inter residual / PCM first (level 0), then intra by level
   std::vector<u32> level_begin;       // tus index where each level starts (size levels + 1)
@@ -134,75 +138,92 @@ struct GpuPicture {
 using GpuPicturePtr = std::shared_ptr<GpuPicture>;
 
 // ---------------------------------------------------------------------------- inter
+// Sample planes are u8 (8-bit streams) or u16 (Main10: one sample per u16, LSB-aligned); `bd` is
+// the component's bit depth (8..10). The 8-bit instantiations see bd = 8 as a constant.
 // 14-bit intermediate luma sample at integer (xi, yi) + fraction (fx, fy) from a plane with edge
-// clamping (§8.5.3.3.3.1).
-VEP_HD int hk_luma_at(const u8* p, int stride, int W, int H, int x, int y) {
+// clamping (§8.5.3.3.3.1): shift1 = bd - 8, shift2 = 6, full samples << (14 - bd).
+template <class P>
+VEP_HD int hk_luma_at(const P* p, int stride, int W, int H, int x, int y) {
   x = x < 0 ? 0 : (x >= W ? W - 1 : x);
   y = y < 0 ? 0 : (y >= H ? H - 1 : y);
   return p[y * stride + x];
 }
 
-VEP_HD int hk_luma_mc(const u8* p, int stride, int W, int H, int xi, int yi, int fx, int fy) {
-  if (!fx && !fy) return hk_luma_at(p, stride, W, H, xi, yi) << 6;
+template <class P>
+VEP_HD int hk_luma_mc(const P* p, int stride, int W, int H, int xi, int yi, int fx, int fy, int bd = 8) {
+  const int sh1 = bd - 8;
+  if (!fx && !fy) return hk_luma_at(p, stride, W, H, xi, yi) << (14 - bd);
   if (!fy) {
     int s = 0;
     for (int i = 0; i < 8; ++i) s += kLumaFilter[fx][i] * hk_luma_at(p, stride, W, H, xi + i - 3, yi);
-    return s;
+    return s >> sh1;
   }
   if (!fx) {
     int s = 0;
     for (int i = 0; i < 8; ++i) s += kLumaFilter[fy][i] * hk_luma_at(p, stride, W, H, xi, yi + i - 3);
-    return s;
+    return s >> sh1;
   }
   int s = 0;
   for (int k = 0; k < 8; ++k) {
     int h = 0;
     for (int i = 0; i < 8; ++i) h += kLumaFilter[fx][i] * hk_luma_at(p, stride, W, H, xi + i - 3, yi + k - 3);
-    s += kLumaFilter[fy][k] * h;
+    s += kLumaFilter[fy][k] * (h >> sh1);
   }
   return s >> 6;
 }
 
 // Chroma component c (0 Cb, 1 Cr) of an NV12 plane (stride = luma width), chroma size W x H.
-VEP_HD int hk_chroma_at(const u8* uv, int stride, int W, int H, int c, int x, int y) {
+template <class P>
+VEP_HD int hk_chroma_at(const P* uv, int stride, int W, int H, int c, int x, int y) {
   x = x < 0 ? 0 : (x >= W ? W - 1 : x);
   y = y < 0 ? 0 : (y >= H ? H - 1 : y);
   return uv[y * stride + 2 * x + c];
 }
 
-VEP_HD int hk_chroma_mc(const u8* uv, int stride, int W, int H, int c, int xi, int yi, int fx, int fy) {
-  if (!fx && !fy) return hk_chroma_at(uv, stride, W, H, c, xi, yi) << 6;
+template <class P>
+VEP_HD int hk_chroma_mc(const P* uv, int stride, int W, int H, int c, int xi, int yi, int fx, int fy, int bd = 8) {
+  const int sh1 = bd - 8;
+  if (!fx && !fy) return hk_chroma_at(uv, stride, W, H, c, xi, yi) << (14 - bd);
   if (!fy) {
     int s = 0;
     for (int i = 0; i < 4; ++i) s += kChromaFilter[fx][i] * hk_chroma_at(uv, stride, W, H, c, xi + i - 1, yi);
-    return s;
+    return s >> sh1;
   }
   if (!fx) {
     int s = 0;
     for (int i = 0; i < 4; ++i) s += kChromaFilter[fy][i] * hk_chroma_at(uv, stride, W, H, c, xi, yi + i - 1);
-    return s;
+    return s >> sh1;
   }
   int s = 0;
   for (int k = 0; k < 4; ++k) {
     int h = 0;
     for (int i = 0; i < 4; ++i) h += kChromaFilter[fx][i] * hk_chroma_at(uv, stride, W, H, c, xi + i - 1, yi + k - 1);
-    s += kChromaFilter[fy][k] * h;
+    s += kChromaFilter[fy][k] * (h >> sh1);
   }
   return s >> 6;
 }
 
 VEP_HD u8 hk_clip8(int v) { return u8(v < 0 ? 0 : (v > 255 ? 255 : v)); }
+VEP_HD int hk_clip(int v, int bd) {
+  const int hi = (1 << bd) - 1;
+  return v < 0 ? 0 : (v > hi ? hi : v);
+}
 
-// Final prediction sample from the 14-bit intermediates (uni: (p + 32) >> 6, bi: (p0 + p1 + 64) >> 7).
-VEP_HD u8 hk_weight(int p0, int p1, bool bi) { return hk_clip8(bi ? (p0 + p1 + 64) >> 7 : (p0 + 32) >> 6); }
+// Final prediction sample from the 14-bit intermediates (§8.5.3.3.4.2): uni (p + off) >> (14 -
+// bd), bi (p0 + p1 + off) >> (15 - bd).
+VEP_HD int hk_weight(int p0, int p1, bool bi, int bd = 8) {
+  const int sh = bi ? 15 - bd : 14 - bd;
+  return hk_clip(((bi ? p0 + p1 : p0) + (1 << (sh - 1))) >> sh, bd);
+}
 
-// Explicit weighting (§8.5.3.3.4.3, 8-bit) of component c; `l` is the list of a uni-predicted
-// sample (p0), ignored for bi-prediction (p0 list 0, p1 list 1).
-VEP_HD u8 hk_weight_explicit(const GpuWp& e, int c, int p0, int p1, bool bi, int l) {
+// Explicit weighting (§8.5.3.3.4.3) of component c; `l` is the list of a uni-predicted sample
+// (p0), ignored for bi-prediction (p0 list 0, p1 list 1). The record carries log2WD (= denom +
+// 14 - bd) and the offsets already scaled by 1 << (bd - 8).
+VEP_HD int hk_weight_explicit(const GpuWp& e, int c, int p0, int p1, bool bi, int l, int bd = 8) {
   const int sh = e.shift[c];
-  if (bi) return hk_clip8((p0 * e.w[0][c] + p1 * e.w[1][c] + ((e.o[0][c] + e.o[1][c] + 1) << sh)) >> (sh + 1));
+  if (bi) return hk_clip((p0 * e.w[0][c] + p1 * e.w[1][c] + ((e.o[0][c] + e.o[1][c] + 1) << sh)) >> (sh + 1), bd);
   const int v = sh >= 1 ? ((p0 * e.w[l][c] + (1 << (sh - 1))) >> sh) + e.o[l][c] : p0 * e.w[l][c] + e.o[l][c];
-  return hk_clip8(v);
+  return hk_clip(v, bd);
 }
 
 // ---------------------------------------------------------------------------- transform
@@ -220,34 +241,35 @@ VEP_HD int hk_itx_col(const i16* d, int log2, bool dst, int y, int x, int my) {
   return s < -32768 ? -32768 : (s > 32767 ? 32767 : s);
 }
 
-// Second stage (horizontal): residual r[y][x] from the first-stage row g (columns <= mx).
-VEP_HD int hk_itx_row(const int* grow, int log2, bool dst, int x, int mx) {
+// Second stage (horizontal): residual r[y][x] from the first-stage row g (columns <= mx);
+// bdShift = 20 - bd.
+VEP_HD int hk_itx_row(const int* grow, int log2, bool dst, int x, int mx, int bd = 8) {
   int s = 0;
   for (int j = 0; j <= mx; ++j) s += hk_basis(log2, dst, j, x) * grow[j];
-  return (s + (1 << 11)) >> 12;
+  return (s + (1 << (19 - bd))) >> (20 - bd);
 }
 
-VEP_HD int hk_tskip(int d) { return ((d << 7) + (1 << 11)) >> 12; }
+VEP_HD int hk_tskip(int d, int bd = 8) { return ((d << 7) + (1 << (19 - bd))) >> (20 - bd); }
 
 // ---------------------------------------------------------------------------- intra
 // One predicted sample at (x, y) of an n x n block (n = 1 << log2) from prepared (substituted,
 // filtered) references: top[k + 1] = p[k][-1] (k = -1 .. 2n-1), left[k] = p[-1][k] (k = 0 .. 2n-1).
-VEP_HD u8 hk_intra_sample(const int* top, const int* left, int log2, int mode, bool luma, int x, int y) {
+VEP_HD int hk_intra_sample(const int* top, const int* left, int log2, int mode, bool luma, int x, int y, int bd = 8) {
   const int n = 1 << log2;
   if (mode == 0) {  // planar
-    return u8(((n - 1 - x) * left[y] + (x + 1) * top[n + 1] + (n - 1 - y) * top[x + 1] + (y + 1) * left[n] + n) >>
-              (log2 + 1));
+    return ((n - 1 - x) * left[y] + (x + 1) * top[n + 1] + (n - 1 - y) * top[x + 1] + (y + 1) * left[n] + n) >>
+           (log2 + 1);
   }
   if (mode == 1) {  // DC (+ edge filter for luma blocks below 32)
     int sum = n;
     for (int k = 0; k < n; ++k) sum += top[k + 1] + left[k];
     const int dc = sum >> (log2 + 1);
     if (luma && n < 32) {
-      if (x == 0 && y == 0) return u8((left[0] + 2 * dc + top[1] + 2) >> 2);
-      if (y == 0) return u8((top[x + 1] + 3 * dc + 2) >> 2);
-      if (x == 0) return u8((left[y] + 3 * dc + 2) >> 2);
+      if (x == 0 && y == 0) return (left[0] + 2 * dc + top[1] + 2) >> 2;
+      if (y == 0) return (top[x + 1] + 3 * dc + 2) >> 2;
+      if (x == 0) return (left[y] + 3 * dc + 2) >> 2;
     }
-    return u8(dc);
+    return dc;
   }
   const int angle = kIntraAngle[mode - 2];
   // main direction: vertical modes read the top row (ref[k] = p[-1 + k][-1]); horizontal modes
@@ -266,7 +288,7 @@ VEP_HD u8 hk_intra_sample(const int* top, const int* left, int log2, int mode, b
     if (mode == 26 && x == 0) val = top[1] + ((left[y] - top[0]) >> 1);
     if (mode == 10 && y == 0) val = left[0] + ((top[x + 1] - top[0]) >> 1);
   }
-  return hk_clip8(val);
+  return hk_clip(val, bd);
 }
 
 // Reference samples of an intra block (§8.4.4.2.2-3) from the picture plane, the availability
@@ -275,8 +297,9 @@ VEP_HD u8 hk_intra_sample(const int* top, const int* left, int log2, int mode, b
 // of g samples (g = 4 luma, 2 chroma: one 4x4 luma block), nearest units first.
 // `plane` addresses sample (0, 0) of the component: luma plane, or the NV12 plane offset by c - 1
 // (then `step` = 2 between horizontal neighbours).
-VEP_HD void hk_prepare_refs(const u8* plane, int stride, int step, int x0, int y0, int log2, bool luma, u64 avail,
-                            int mode, bool strong, int* top, int* left) {
+template <class P>
+VEP_HD void hk_prepare_refs(const P* plane, int stride, int step, int x0, int y0, int log2, bool luma, u64 avail,
+                            int mode, bool strong, int* top, int* left, int bd = 8) {
   const int n = 1 << log2, g = luma ? 4 : 2;
   auto at = [&](int x, int y) { return int(plane[y * stride + x * step]); };
   // p[-1][2n-1] .. p[-1][-1] .. p[2n-1][-1] as one scan (k = 0 .. 4n)
@@ -303,7 +326,7 @@ VEP_HD void hk_prepare_refs(const u8* plane, int stride, int step, int x0, int y
     any |= a ? 1 : 0;
   }
   if (!any) {
-    for (int k = 0; k <= 4 * n; ++k) buf[k] = 128;
+    for (int k = 0; k <= 4 * n; ++k) buf[k] = 1 << (bd - 1);
   } else {
     if (!av[0]) {
       int k = 1;
@@ -324,7 +347,8 @@ VEP_HD void hk_prepare_refs(const u8* plane, int stride, int step, int x0, int y
   int t[65], l[64];
   const int tl = top[0];
   auto iabs = [](int v) { return v < 0 ? -v : v; };
-  if (strong && n == 32 && iabs(tl + top[2 * n] - 2 * top[n]) < 8 && iabs(tl + left[2 * n - 1] - 2 * left[n - 1]) < 8) {
+  const int lim = 1 << (bd - 5);
+  if (strong && n == 32 && iabs(tl + top[2 * n] - 2 * top[n]) < lim && iabs(tl + left[2 * n - 1] - 2 * left[n - 1]) < lim) {
     t[0] = tl;
     for (int y = 0; y < 63; ++y) l[y] = ((63 - y) * tl + (y + 1) * left[63] + 32) >> 6;
     l[63] = left[63];
@@ -343,54 +367,59 @@ VEP_HD void hk_prepare_refs(const u8* plane, int stride, int step, int x0, int y
 
 // ---------------------------------------------------------------------------- deblocking
 // Luma filtering of one 4-line segment of an edge (§8.7.2.5.3 / .6-.7). `at(k, i)` addresses line
-// k (0..3) at distance i from the edge (p side: i < 0, q side: i >= 0).
-struct HkLumaEdge {
-  u8* base;   // sample q0 of line 0
+// k (0..3) at distance i from the edge (p side: i < 0, q side: i >= 0). beta and tC scale by
+// 1 << (bd - 8).
+template <class P>
+struct HkLumaEdgeT {
+  P* base;    // sample q0 of line 0
   int along;  // step between lines
   int across; // step across the edge (q direction)
-  VEP_HD u8& at(int k, int i) const { return base[k * along + i * across]; }
+  VEP_HD P& at(int k, int i) const { return base[k * along + i * across]; }
 };
+using HkLumaEdge = HkLumaEdgeT<u8>;
 
-VEP_HD void hk_deblock_luma(const HkLumaEdge& e, int bs, int qpl, int beta_offset, int tc_offset, bool nfp, bool nfq) {
+template <class P>
+VEP_HD void hk_deblock_luma(const HkLumaEdgeT<P>& e, int bs, int qpl, int beta_offset, int tc_offset, bool nfp, bool nfq,
+                            int bd = 8) {
   const int bi = qpl + beta_offset, ti = qpl + 2 * (bs - 1) + tc_offset;
-  const int beta = kBetaTable[bi < 0 ? 0 : (bi > 51 ? 51 : bi)];
-  const int tc = kTcTable[ti < 0 ? 0 : (ti > 53 ? 53 : ti)];
-  auto P = [&](int k, int i) { return int(e.at(k, -1 - i)); };
+  const int beta = kBetaTable[bi < 0 ? 0 : (bi > 51 ? 51 : bi)] * (1 << (bd - 8));
+  const int tc = kTcTable[ti < 0 ? 0 : (ti > 53 ? 53 : ti)] * (1 << (bd - 8));
+  auto P_ = [&](int k, int i) { return int(e.at(k, -1 - i)); };
   auto Q = [&](int k, int i) { return int(e.at(k, i)); };
   auto iabs = [](int v) { return v < 0 ? -v : v; };
-  const int dp0 = iabs(P(0, 2) - 2 * P(0, 1) + P(0, 0)), dp3 = iabs(P(3, 2) - 2 * P(3, 1) + P(3, 0));
+  const int dp0 = iabs(P_(0, 2) - 2 * P_(0, 1) + P_(0, 0)), dp3 = iabs(P_(3, 2) - 2 * P_(3, 1) + P_(3, 0));
   const int dq0 = iabs(Q(0, 2) - 2 * Q(0, 1) + Q(0, 0)), dq3 = iabs(Q(3, 2) - 2 * Q(3, 1) + Q(3, 0));
   const int dpq0 = dp0 + dq0, dpq3 = dp3 + dq3, dp = dp0 + dp3, dq = dq0 + dq3, d = dpq0 + dpq3;
   if (d >= beta) return;
   auto dsam = [&](int k, int dpq) {
-    return 2 * dpq < (beta >> 2) && iabs(P(k, 3) - P(k, 0)) + iabs(Q(k, 0) - Q(k, 3)) < (beta >> 3) &&
-           iabs(P(k, 0) - Q(k, 0)) < ((5 * tc + 1) >> 1);
+    return 2 * dpq < (beta >> 2) && iabs(P_(k, 3) - P_(k, 0)) + iabs(Q(k, 0) - Q(k, 3)) < (beta >> 3) &&
+           iabs(P_(k, 0) - Q(k, 0)) < ((5 * tc + 1) >> 1);
   };
   const bool strong = dsam(0, dpq0) && dsam(3, dpq3);
   const bool dEp = dp < ((beta + (beta >> 1)) >> 3), dEq = dq < ((beta + (beta >> 1)) >> 3);
   auto clip3 = [](int lo, int hi, int v) { return v < lo ? lo : (v > hi ? hi : v); };
   for (int k = 0; k < 4; ++k) {
-    const int p0 = P(k, 0), p1 = P(k, 1), p2 = P(k, 2), p3 = P(k, 3);
+    const int p0 = P_(k, 0), p1 = P_(k, 1), p2 = P_(k, 2), p3 = P_(k, 3);
     const int q0 = Q(k, 0), q1 = Q(k, 1), q2 = Q(k, 2), q3 = Q(k, 3);
     if (strong) {
       if (!nfp) {
-        e.at(k, -1) = u8(clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3));
-        e.at(k, -2) = u8(clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2));
-        e.at(k, -3) = u8(clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3));
+        e.at(k, -1) = P(clip3(p0 - 2 * tc, p0 + 2 * tc, (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3));
+        e.at(k, -2) = P(clip3(p1 - 2 * tc, p1 + 2 * tc, (p2 + p1 + p0 + q0 + 2) >> 2));
+        e.at(k, -3) = P(clip3(p2 - 2 * tc, p2 + 2 * tc, (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3));
       }
       if (!nfq) {
-        e.at(k, 0) = u8(clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3));
-        e.at(k, 1) = u8(clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2));
-        e.at(k, 2) = u8(clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3));
+        e.at(k, 0) = P(clip3(q0 - 2 * tc, q0 + 2 * tc, (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3));
+        e.at(k, 1) = P(clip3(q1 - 2 * tc, q1 + 2 * tc, (p0 + q0 + q1 + q2 + 2) >> 2));
+        e.at(k, 2) = P(clip3(q2 - 2 * tc, q2 + 2 * tc, (p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3));
       }
     } else {
       int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
       if (iabs(delta) >= tc * 10) continue;
       delta = clip3(-tc, tc, delta);
-      if (!nfp) e.at(k, -1) = hk_clip8(p0 + delta);
-      if (!nfq) e.at(k, 0) = hk_clip8(q0 - delta);
-      if (dEp && !nfp) e.at(k, -2) = hk_clip8(p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1));
-      if (dEq && !nfq) e.at(k, 1) = hk_clip8(q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1));
+      if (!nfp) e.at(k, -1) = P(hk_clip(p0 + delta, bd));
+      if (!nfq) e.at(k, 0) = P(hk_clip(q0 - delta, bd));
+      if (dEp && !nfp) e.at(k, -2) = P(hk_clip(p1 + clip3(-(tc >> 1), tc >> 1, (((p2 + p0 + 1) >> 1) - p1 + delta) >> 1), bd));
+      if (dEq && !nfq) e.at(k, 1) = P(hk_clip(q1 + clip3(-(tc >> 1), tc >> 1, (((q2 + q0 + 1) >> 1) - q1 - delta) >> 1), bd));
     }
   }
 }
@@ -403,19 +432,20 @@ VEP_HD int hk_chroma_qp(int qpi) {
 }
 
 // Chroma filtering of the 2 chroma lines of one 4-luma-line segment (bS 2 edges only).
-VEP_HD void hk_deblock_chroma(u8* base, int along, int across, int qpP, int qpQ, int cqp_offset, int tc_offset,
-                              bool nfp, bool nfq) {
+template <class P>
+VEP_HD void hk_deblock_chroma(P* base, int along, int across, int qpP, int qpQ, int cqp_offset, int tc_offset,
+                              bool nfp, bool nfq, int bd = 8) {
   // §8.7.2.5.5: QpC from Table 8-10 of qPi (no clipping of qPi: that is the CU-level rule)
   const int qpi = ((qpP + qpQ + 1) >> 1) + cqp_offset;
   int ti = hk_chroma_qp(qpi) + 2 + tc_offset;
-  const int tc = kTcTable[ti < 0 ? 0 : (ti > 53 ? 53 : ti)];
+  const int tc = kTcTable[ti < 0 ? 0 : (ti > 53 ? 53 : ti)] * (1 << (bd - 8));
   for (int k = 0; k < 2; ++k) {
-    u8* q = base + k * along;
+    P* q = base + k * along;
     const int p0 = q[-across], p1 = q[-2 * across], q0 = q[0], q1 = q[across];
     int delta = (((q0 - p0) * 4) + p1 - q1 + 4) >> 3;
     delta = delta < -tc ? -tc : (delta > tc ? tc : delta);
-    if (!nfp) q[-across] = hk_clip8(p0 + delta);
-    if (!nfq) q[0] = hk_clip8(q0 - delta);
+    if (!nfp) q[-across] = P(hk_clip(p0 + delta, bd));
+    if (!nfq) q[0] = P(hk_clip(q0 - delta, bd));
   }
 }
 
@@ -423,14 +453,17 @@ VEP_HD void hk_deblock_chroma(u8* base, int along, int across, int qpP, int qpQ,
 // One SAO output sample of component c (0 luma) at (x, y) (component samples) of the CTB with
 // parameters sp, reading the deblocked picture `src` (plane pointer of the component as in
 // hk_prepare_refs). `nb_ok(nx, ny)` says whether the neighbour may be used (inside the picture,
-// slice-boundary rules). Returns the input sample when no offset applies.
-template <class NbOk>
-VEP_HD int hk_sao_sample(const u8* src, int stride, int step, const GpuSao& sp, int c, int x, int y, NbOk nb_ok) {
+// slice-boundary rules). Returns the input sample when no offset applies. Bands are
+// 1 << (bd - 5) wide; the offsets (SaoOffsetVal, << (bd - min(bd, 10)) = 0 for bd <= 10) are
+// the parsed ones.
+template <class P, class NbOk>
+VEP_HD int hk_sao_sample(const P* src, int stride, int step, const GpuSao& sp, int c, int x, int y, NbOk nb_ok,
+                         int bd = 8) {
   const int v = src[y * stride + x * step];
   const int type = sp.type[c];
   if (type == 1) {
-    const int k = ((v >> 3) - sp.band[c]) & 31;
-    return k < 4 ? hk_clip8(v + sp.off[c][k]) : v;
+    const int k = ((v >> (bd - 5)) - sp.band[c]) & 31;
+    return k < 4 ? hk_clip(v + sp.off[c][k], bd) : v;
   }
   const int hx[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
   const int vy[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
@@ -444,7 +477,7 @@ VEP_HD int hk_sao_sample(const u8* src, int stride, int step, const GpuSao& sp, 
   }
   int edge = 2 + sgn;
   if (edge <= 2) edge = edge == 2 ? 0 : edge + 1;
-  return edge ? hk_clip8(v + sp.off[c][edge - 1]) : v;
+  return edge ? hk_clip(v + sp.off[c][edge - 1], bd) : v;
 }
 
 }  // namespace vep::hevc

@@ -10,10 +10,11 @@
 namespace vep::hevc {
 
 // ------------------------------------------------------------------------------ transforms
-void inverse_transform(const i32* d, int log2, bool dst, bool tskip, i32* r) {
+void inverse_transform(const i32* d, int log2, bool dst, bool tskip, i32* r, int bd) {
   const int n = 1 << log2;
-  if (tskip) {  // §8.6.4.2: r = d << 7, then the final bdShift (20 - 8)
-    for (int k = 0; k < n * n; ++k) r[k] = ((d[k] << 7) + (1 << 11)) >> 12;
+  const int bsh = 20 - bd;  // the final bdShift
+  if (tskip) {  // §8.6.4.2: r = d << 7, then bdShift
+    for (int k = 0; k < n * n; ++k) r[k] = ((d[k] << 7) + (1 << (bsh - 1))) >> bsh;
     return;
   }
   // basis rows (frequency j, sample i): the n-point DCT is every (32 / n)-th row of the 32-point
@@ -40,34 +41,35 @@ void inverse_transform(const i32* d, int log2, bool dst, bool tskip, i32* r) {
       for (int j = 0; j <= my; ++j) s += basis[j][y] * d[j * n + x];
       g[y * n + x] = std::clamp((s + 64) >> 7, -32768, 32767);
     }
-  // second stage (horizontal): r[y][x] = (sum_j basis[j][x] * g[y][j] + 2^11) >> 12
+  // second stage (horizontal): r[y][x] = (sum_j basis[j][x] * g[y][j] + 2^(bsh - 1)) >> bsh
   for (int y = 0; y < n; ++y) {
     const i32* gr = g + y * n;
     for (int x = 0; x < n; ++x) {
       i32 s = 0;
       for (int j = 0; j <= mx; ++j) s += basis[j][x] * gr[j];
-      r[y * n + x] = (s + (1 << 11)) >> 12;
+      r[y * n + x] = (s + (1 << (bsh - 1))) >> bsh;
     }
   }
 }
 
-int dequant_level(int level, int qp, int log2, int m) {
+int dequant_level(int level, int qp, int log2, int m, int bit_depth) {
   static constexpr int kLevelScale[6] = {40, 45, 51, 57, 64, 72};
-  const int bd = 8 + log2 - 5;
+  const int bd = bit_depth + log2 - 5;  // bdShift
   const i64 v = ((i64(level) * m * kLevelScale[qp % 6]) << (qp / 6)) + (i64(1) << (bd - 1));
   return int(std::clamp<i64>(v >> bd, -32768, 32767));
 }
 
 // ------------------------------------------------------------------------------ intra
-void intra_predict(const int* top, const int* left, int log2, int mode, bool luma, u8* out, int stride,
-                   bool filter_edges) {
+void intra_predict(const int* top, const int* left, int log2, int mode, bool luma, u16* out, int stride,
+                   bool filter_edges, int bd) {
+  const int hi = (1 << bd) - 1;
   // top[x + 1] = p[x][-1] (x = -1 .. 2n-1), left[y] = p[-1][y] (y = 0 .. 2n-1)
   const int n = 1 << log2;
   auto P = [&](int x, int y) -> int { return y < 0 ? top[x + 1] : left[y]; };
   if (mode == 0) {  // planar
     for (int y = 0; y < n; ++y)
       for (int x = 0; x < n; ++x)
-        out[y * stride + x] = u8(((n - 1 - x) * P(-1, y) + (x + 1) * P(n, -1) + (n - 1 - y) * P(x, -1) +
+        out[y * stride + x] = u16(((n - 1 - x) * P(-1, y) + (x + 1) * P(n, -1) + (n - 1 - y) * P(x, -1) +
                                   (y + 1) * P(-1, n) + n) >> (log2 + 1));
     return;
   }
@@ -76,11 +78,11 @@ void intra_predict(const int* top, const int* left, int log2, int mode, bool lum
     for (int k = 0; k < n; ++k) sum += P(k, -1) + P(-1, k);
     const int dc = sum >> (log2 + 1);
     for (int y = 0; y < n; ++y)
-      for (int x = 0; x < n; ++x) out[y * stride + x] = u8(dc);
+      for (int x = 0; x < n; ++x) out[y * stride + x] = u16(dc);
     if (luma && n < 32 && filter_edges) {
-      out[0] = u8((P(-1, 0) + 2 * dc + P(0, -1) + 2) >> 2);
-      for (int x = 1; x < n; ++x) out[x] = u8((P(x, -1) + 3 * dc + 2) >> 2);
-      for (int y = 1; y < n; ++y) out[y * stride] = u8((P(-1, y) + 3 * dc + 2) >> 2);
+      out[0] = u16((P(-1, 0) + 2 * dc + P(0, -1) + 2) >> 2);
+      for (int x = 1; x < n; ++x) out[x] = u16((P(x, -1) + 3 * dc + 2) >> 2);
+      for (int y = 1; y < n; ++y) out[y * stride] = u16((P(-1, y) + 3 * dc + 2) >> 2);
     }
     return;
   }
@@ -99,11 +101,11 @@ void intra_predict(const int* top, const int* left, int log2, int mode, bool lum
     for (int y = 0; y < n; ++y) {
       const int idx = ((y + 1) * angle) >> 5, fact = ((y + 1) * angle) & 31;
       for (int x = 0; x < n; ++x)
-        out[y * stride + x] = u8(fact ? ((32 - fact) * ref[x + idx + 1] + fact * ref[x + idx + 2] + 16) >> 5
+        out[y * stride + x] = u16(fact ? ((32 - fact) * ref[x + idx + 1] + fact * ref[x + idx + 2] + 16) >> 5
                                       : ref[x + idx + 1]);
     }
     if (mode == 26 && luma && n < 32 && filter_edges)
-      for (int y = 0; y < n; ++y) out[y * stride] = u8(std::clamp(P(0, -1) + ((P(-1, y) - P(-1, -1)) >> 1), 0, 255));
+      for (int y = 0; y < n; ++y) out[y * stride] = u16(std::clamp(P(0, -1) + ((P(-1, y) - P(-1, -1)) >> 1), 0, hi));
   } else {
     for (int x = 0; x <= n; ++x) ref[x] = P(-1, -1 + x);
     if (angle < 0) {
@@ -116,15 +118,16 @@ void intra_predict(const int* top, const int* left, int log2, int mode, bool lum
     for (int x = 0; x < n; ++x) {
       const int idx = ((x + 1) * angle) >> 5, fact = ((x + 1) * angle) & 31;
       for (int y = 0; y < n; ++y)
-        out[y * stride + x] = u8(fact ? ((32 - fact) * ref[y + idx + 1] + fact * ref[y + idx + 2] + 16) >> 5
+        out[y * stride + x] = u16(fact ? ((32 - fact) * ref[y + idx + 1] + fact * ref[y + idx + 2] + 16) >> 5
                                       : ref[y + idx + 1]);
     }
     if (mode == 10 && luma && n < 32 && filter_edges)
-      for (int x = 0; x < n; ++x) out[x] = u8(std::clamp(P(-1, 0) + ((P(x, -1) - P(-1, -1)) >> 1), 0, 255));
+      for (int x = 0; x < n; ++x) out[x] = u16(std::clamp(P(-1, 0) + ((P(x, -1) - P(-1, -1)) >> 1), 0, hi));
   }
 }
 
-void filter_intra_refs(int* top, int* left, int log2, int mode, bool strong_enabled) {
+void filter_intra_refs(int* top, int* left, int log2, int mode, bool strong_enabled, int bd) {
+  const int lim = 1 << (bd - 5);
   const int n = 1 << log2;
   if (mode == 1 || n == 4) return;
   const int dist = std::min(std::abs(mode - 26), std::abs(mode - 10));
@@ -133,8 +136,8 @@ void filter_intra_refs(int* top, int* left, int log2, int mode, bool strong_enab
   // p[-1][-1] = top[0]; p[x][-1] = top[x + 1]; p[-1][y] = left[y]
   int t[65], l[64];
   const int tl = top[0];
-  if (strong_enabled && n == 32 && std::abs(tl + top[2 * n] - 2 * top[n]) < 8 &&
-      std::abs(tl + left[2 * n - 1] - 2 * left[n - 1]) < 8) {
+  if (strong_enabled && n == 32 && std::abs(tl + top[2 * n] - 2 * top[n]) < lim &&
+      std::abs(tl + left[2 * n - 1] - 2 * left[n - 1]) < lim) {
     t[0] = tl;
     for (int y = 0; y < 63; ++y) l[y] = ((63 - y) * tl + (y + 1) * left[63] + 32) >> 6;
     l[63] = left[63];
@@ -152,91 +155,48 @@ void filter_intra_refs(int* top, int* left, int log2, int mode, bool strong_enab
 }
 
 // ------------------------------------------------------------------------------ inter
-static inline int ref_luma(const HostSurface& r, int x, int y) {
-  x = std::clamp(x, 0, r.coded_w - 1);
-  y = std::clamp(y, 0, r.coded_h - 1);
-  return r.y[size_t(y) * r.coded_w + x];
-}
-static inline int ref_chroma(const HostSurface& r, int c, int x, int y) {
-  x = std::clamp(x, 0, r.coded_w / 2 - 1);
-  y = std::clamp(y, 0, r.coded_h / 2 - 1);
-  return r.uv[size_t(y) * r.coded_w + 2 * x + c];
-}
-
-// 14-bit intermediate luma prediction sample (§8.5.3.3.3.1).
+// 14-bit intermediate prediction samples of one reference sample position (spec form, tests).
 int luma_inter_sample(const HostSurface& r, int xi, int yi, int fx, int fy) {
-  if (!fx && !fy) return ref_luma(r, xi, yi) << 6;
-  if (!fy) {
-    int s = 0;
-    for (int i = 0; i < 8; ++i) s += kLumaFilter[fx][i] * ref_luma(r, xi + i - 3, yi);
-    return s;
-  }
-  if (!fx) {
-    int s = 0;
-    for (int i = 0; i < 8; ++i) s += kLumaFilter[fy][i] * ref_luma(r, xi, yi + i - 3);
-    return s;
-  }
-  int s = 0;
-  for (int k = 0; k < 8; ++k) {
-    int h = 0;
-    for (int i = 0; i < 8; ++i) h += kLumaFilter[fx][i] * ref_luma(r, xi + i - 3, yi + k - 3);
-    s += kLumaFilter[fy][k] * h;
-  }
-  return s >> 6;
+  if (r.wide()) return hk_luma_mc(r.y16.data(), r.coded_w, r.coded_w, r.coded_h, xi, yi, fx, fy, r.bd);
+  return hk_luma_mc(r.y.data(), r.coded_w, r.coded_w, r.coded_h, xi, yi, fx, fy);
 }
-
 int chroma_inter_sample(const HostSurface& r, int c, int xi, int yi, int fx, int fy) {
-  if (!fx && !fy) return ref_chroma(r, c, xi, yi) << 6;
-  if (!fy) {
-    int s = 0;
-    for (int i = 0; i < 4; ++i) s += kChromaFilter[fx][i] * ref_chroma(r, c, xi + i - 1, yi);
-    return s;
-  }
-  if (!fx) {
-    int s = 0;
-    for (int i = 0; i < 4; ++i) s += kChromaFilter[fy][i] * ref_chroma(r, c, xi, yi + i - 1);
-    return s;
-  }
-  int s = 0;
-  for (int k = 0; k < 4; ++k) {
-    int h = 0;
-    for (int i = 0; i < 4; ++i) h += kChromaFilter[fx][i] * ref_chroma(r, c, xi + i - 1, yi + k - 1);
-    s += kChromaFilter[fy][k] * h;
-  }
-  return s >> 6;
+  if (r.wide()) return hk_chroma_mc(r.uv16.data(), r.coded_w, r.coded_w / 2, r.coded_h / 2, c, xi, yi, fx, fy, r.bd);
+  return hk_chroma_mc(r.uv.data(), r.coded_w, r.coded_w / 2, r.coded_h / 2, c, xi, yi, fx, fy);
 }
 
 // 14-bit intermediate prediction of a w x h luma block at integer position (x0, y0) with
-// fraction (fx, fy), separable (§8.5.3.3.3.1): the (w + 7) x (h + 7) source window is read in
-// place when it lies inside the picture, else gathered with edge clamping.
-static void mc_luma(const HostSurface& r, int x0, int y0, int w, int h, int fx, int fy, i16* dst) {
-  const int W = r.coded_w, H = r.coded_h;
-  u8 win[71 * 71];
-  const u8* src;
+// fraction (fx, fy), separable (§8.5.3.3.3.1; shift1 = bd - 8): the (w + 7) x (h + 7) source
+// window is read in place when it lies inside the picture, else gathered with edge clamping.
+template <class P>
+static void mc_luma(const P* plane, int W, int H, int x0, int y0, int w, int h, int fx, int fy, i16* dst, int bd) {
+  P win[71 * 71];
+  const P* src;
   int ss;
   if (x0 - 3 >= 0 && y0 - 3 >= 0 && x0 + w + 4 <= W && y0 + h + 4 <= H) {
-    src = &r.y[size_t(y0 - 3) * W + size_t(x0 - 3)];
+    src = &plane[size_t(y0 - 3) * W + size_t(x0 - 3)];
     ss = W;
   } else {
     ss = w + 7;
     for (int j = 0; j < h + 7; ++j) {
       const size_t row = size_t(std::clamp(y0 - 3 + j, 0, H - 1)) * W;
-      for (int i = 0; i < w + 7; ++i) win[j * ss + i] = r.y[row + size_t(std::clamp(x0 - 3 + i, 0, W - 1))];
+      for (int i = 0; i < w + 7; ++i) win[j * ss + i] = plane[row + size_t(std::clamp(x0 - 3 + i, 0, W - 1))];
     }
     src = win;
   }
+  const int sh1 = bd - 8;
   const i8* fh = kLumaFilter[fx];
   const i8* fv = kLumaFilter[fy];
   if (!fx && !fy) {
     for (int j = 0; j < h; ++j)
-      for (int i = 0; i < w; ++i) dst[j * w + i] = i16(src[(j + 3) * ss + i + 3] << 6);
+      for (int i = 0; i < w; ++i) dst[j * w + i] = i16(src[(j + 3) * ss + i + 3] << (14 - bd));
   } else if (!fy) {
     for (int j = 0; j < h; ++j) {
-      const u8* p = src + (j + 3) * ss;
+      const P* p = src + (j + 3) * ss;
       for (int i = 0; i < w; ++i) {
         int s = 0;
         for (int k = 0; k < 8; ++k) s += fh[k] * p[i + k];
-        dst[j * w + i] = i16(s);
+        dst[j * w + i] = i16(s >> sh1);
       }
     }
   } else if (!fx) {
@@ -244,16 +204,16 @@ static void mc_luma(const HostSurface& r, int x0, int y0, int w, int h, int fx, 
       for (int i = 0; i < w; ++i) {
         int s = 0;
         for (int k = 0; k < 8; ++k) s += fv[k] * src[(j + k) * ss + i + 3];
-        dst[j * w + i] = i16(s);
+        dst[j * w + i] = i16(s >> sh1);
       }
   } else {
     i16 tmp[71 * 64];
     for (int j = 0; j < h + 7; ++j) {
-      const u8* p = src + j * ss;
+      const P* p = src + j * ss;
       for (int i = 0; i < w; ++i) {
         int s = 0;
         for (int k = 0; k < 8; ++k) s += fh[k] * p[i + k];
-        tmp[j * w + i] = i16(s);
+        tmp[j * w + i] = i16(s >> sh1);
       }
     }
     for (int j = 0; j < h; ++j)
@@ -265,43 +225,46 @@ static void mc_luma(const HostSurface& r, int x0, int y0, int w, int h, int fx, 
   }
 }
 
-// Same for one chroma component (4-tap, eighth-sample fraction) of the NV12 plane.
-static void mc_chroma(const HostSurface& r, int c, int x0, int y0, int w, int h, int fx, int fy, i16* dst) {
-  const int W = r.coded_w / 2, H = r.coded_h / 2, st = r.coded_w;
-  u8 win[35 * 35];
+// Same for one chroma component (4-tap, eighth-sample fraction) of the NV12 plane (`uv` of a
+// luma-wide stride).
+template <class P>
+static void mc_chroma(const P* uv, int st, int W, int H, int c, int x0, int y0, int w, int h, int fx, int fy, i16* dst,
+                      int bd) {
+  P win[35 * 35];
   const int ss = w + 3;
   for (int j = 0; j < h + 3; ++j) {
     const size_t row = size_t(std::clamp(y0 - 1 + j, 0, H - 1)) * st;
     if (x0 - 1 >= 0 && x0 + w + 2 <= W) {
-      const u8* p = &r.uv[row + 2 * size_t(x0 - 1) + size_t(c)];
+      const P* p = &uv[row + 2 * size_t(x0 - 1) + size_t(c)];
       for (int i = 0; i < w + 3; ++i) win[j * ss + i] = p[2 * i];
     } else {
-      for (int i = 0; i < w + 3; ++i) win[j * ss + i] = r.uv[row + 2 * size_t(std::clamp(x0 - 1 + i, 0, W - 1)) + size_t(c)];
+      for (int i = 0; i < w + 3; ++i) win[j * ss + i] = uv[row + 2 * size_t(std::clamp(x0 - 1 + i, 0, W - 1)) + size_t(c)];
     }
   }
+  const int sh1 = bd - 8;
   const i8* fh = kChromaFilter[fx];
   const i8* fv = kChromaFilter[fy];
   if (!fx && !fy) {
     for (int j = 0; j < h; ++j)
-      for (int i = 0; i < w; ++i) dst[j * w + i] = i16(win[(j + 1) * ss + i + 1] << 6);
+      for (int i = 0; i < w; ++i) dst[j * w + i] = i16(win[(j + 1) * ss + i + 1] << (14 - bd));
   } else if (!fy) {
     for (int j = 0; j < h; ++j)
       for (int i = 0; i < w; ++i) {
-        const u8* p = win + (j + 1) * ss + i;
-        dst[j * w + i] = i16(fh[0] * p[0] + fh[1] * p[1] + fh[2] * p[2] + fh[3] * p[3]);
+        const P* p = win + (j + 1) * ss + i;
+        dst[j * w + i] = i16((fh[0] * p[0] + fh[1] * p[1] + fh[2] * p[2] + fh[3] * p[3]) >> sh1);
       }
   } else if (!fx) {
     for (int j = 0; j < h; ++j)
       for (int i = 0; i < w; ++i) {
-        const u8* p = win + j * ss + i + 1;
-        dst[j * w + i] = i16(fv[0] * p[0] + fv[1] * p[ss] + fv[2] * p[2 * ss] + fv[3] * p[3 * ss]);
+        const P* p = win + j * ss + i + 1;
+        dst[j * w + i] = i16((fv[0] * p[0] + fv[1] * p[ss] + fv[2] * p[2 * ss] + fv[3] * p[3 * ss]) >> sh1);
       }
   } else {
     i16 tmp[35 * 32];
     for (int j = 0; j < h + 3; ++j)
       for (int i = 0; i < w; ++i) {
-        const u8* p = win + j * ss + i;
-        tmp[j * w + i] = i16(fh[0] * p[0] + fh[1] * p[1] + fh[2] * p[2] + fh[3] * p[3]);
+        const P* p = win + j * ss + i;
+        tmp[j * w + i] = i16((fh[0] * p[0] + fh[1] * p[1] + fh[2] * p[2] + fh[3] * p[3]) >> sh1);
       }
     for (int j = 0; j < h; ++j)
       for (int i = 0; i < w; ++i) {
@@ -311,8 +274,34 @@ static void mc_chroma(const HostSurface& r, int c, int x0, int y0, int w, int h,
   }
 }
 
-void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const MvField& m, u8* y, int ys, u8* cb,
-                u8* cr, int cs) {
+static void mc_luma(const HostSurface& r, int x0, int y0, int w, int h, int fx, int fy, i16* dst) {
+  if (r.wide()) mc_luma(r.y16.data(), r.coded_w, r.coded_h, x0, y0, w, h, fx, fy, dst, r.bd);
+  else mc_luma(r.y.data(), r.coded_w, r.coded_h, x0, y0, w, h, fx, fy, dst, 8);
+}
+static void mc_chroma(const HostSurface& r, int c, int x0, int y0, int w, int h, int fx, int fy, i16* dst) {
+  if (r.wide())
+    mc_chroma(r.uv16.data(), r.coded_w, r.coded_w / 2, r.coded_h / 2, c, x0, y0, w, h, fx, fy, dst, r.bd);
+  else mc_chroma(r.uv.data(), r.coded_w, r.coded_w / 2, r.coded_h / 2, c, x0, y0, w, h, fx, fy, dst, 8);
+}
+
+// Explicit weighting record of one PU (§8.5.3.3.4.3) for the components' bit depths: log2WD =
+// denom + 14 - bd, offsets << (bd - 8) (the GPU records carry the same, hevc_ctu.cpp).
+GpuWp explicit_weights(const SliceHeader& sh, const MvField& m, int bd_y, int bd_c) {
+  GpuWp e{};
+  for (int c = 0; c < 3; ++c) {
+    const int bd = c ? bd_c : bd_y;
+    e.shift[c] = u8(sh.pwt.log2_denom(c) + 14 - bd);
+    for (int l = 0; l < 2; ++l)
+      if ((m.pred >> l) & 1) {
+        e.w[l][c] = i16(sh.pwt.w[l][m.ref[l]][c]);
+        e.o[l][c] = i16(sh.pwt.o[l][m.ref[l]][c] * (1 << (bd - 8)));
+      }
+  }
+  return e;
+}
+
+void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const MvField& m, u16* y, int ys, u16* cb,
+                u16* cr, int cs) {
   const SliceInfo& sl = pc.slices[size_t(si)];
   const HostSurface* r[2] = {nullptr, nullptr};
   for (int l = 0; l < 2; ++l)
@@ -320,24 +309,16 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
       VEP_CHECK(m.ref[l] >= 0 && size_t(m.ref[l]) < sl.list[l].size() && sl.list[l][size_t(m.ref[l])],
                 "reference index outside the list");
       r[l] = &sl.list[l][size_t(m.ref[l])]->s;
+      VEP_CHECK(r[l]->bd == pc.s->bd, "reference picture of another bit depth");
     }
   const bool bi = r[0] && r[1];
   // explicit weighted prediction (§8.5.3.3.4.3): the slice's weights of the PU's references
   const bool wt = sl.sh.weighted;
-  GpuWp e{};
-  if (wt) {
-    for (int c = 0; c < 3; ++c) {
-      e.shift[c] = u8(sl.sh.pwt.log2_denom(c) + 6);
-      for (int l = 0; l < 2; ++l)
-        if (r[l]) {
-          e.w[l][c] = i16(sl.sh.pwt.w[l][m.ref[l]][c]);
-          e.o[l][c] = i16(sl.sh.pwt.o[l][m.ref[l]][c]);
-        }
-    }
-  }
+  const GpuWp e = wt ? explicit_weights(sl.sh, m, pc.bd_y, pc.bd_c) : GpuWp{};
   const int ul = r[0] ? 0 : 1;  // the list of a uni-predicted PU
-  auto fin = [&](int c, int p0, int p1) -> u8 {
-    return wt ? hk_weight_explicit(e, c, p0, p1, bi, ul) : hk_weight(p0, p1, bi);
+  auto fin = [&](int c, int p0, int p1) -> u16 {
+    const int bd = c ? pc.bd_c : pc.bd_y;
+    return u16(wt ? hk_weight_explicit(e, c, p0, p1, bi, ul, bd) : hk_weight(p0, p1, bi, bd));
   };
   if (!bi && !wt) {  // uni-prediction with a full-sample vector inside the picture: a plain copy
     const int l = r[0] ? 0 : 1;
@@ -345,15 +326,13 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
     const int mx = m.mv[l][0], my = m.mv[l][1];
     const int xi = xPb + (mx >> 2), yi = yPb + (my >> 2);
     if (!(mx & 7) && !(my & 7) && xi >= 0 && yi >= 0 && xi + w <= s.coded_w && yi + h <= s.coded_h) {
-      const int st = s.coded_w;
-      for (int j = 0; j < h; ++j) std::memcpy(y + j * ys, &s.y[size_t(yi + j) * st + size_t(xi)], size_t(w));
-      for (int j = 0; j < h / 2; ++j) {
-        const u8* src = &s.uv[size_t(yi / 2 + j) * st + size_t(xi)];
+      for (int j = 0; j < h; ++j)
+        for (int i = 0; i < w; ++i) y[j * ys + i] = u16(s.get(0, xi + i, yi + j));
+      for (int j = 0; j < h / 2; ++j)
         for (int i = 0; i < w / 2; ++i) {
-          cb[j * cs + i] = src[2 * i];
-          cr[j * cs + i] = src[2 * i + 1];
+          cb[j * cs + i] = u16(s.get(1, xi / 2 + i, yi / 2 + j));
+          cr[j * cs + i] = u16(s.get(2, xi / 2 + i, yi / 2 + j));
         }
-      }
       return;
     }
   }
@@ -370,7 +349,7 @@ void predict_pu(const PicCtx& pc, int si, int xPb, int yPb, int w, int h, const 
       if (r[l])
         mc_chroma(*r[l], c, xc + (m.mv[l][0] >> 3), yc + (m.mv[l][1] >> 3), wc, hc, m.mv[l][0] & 7, m.mv[l][1] & 7,
                   p[np++]);
-    u8* out = c == 0 ? cb : cr;
+    u16* out = c == 0 ? cb : cr;
     for (int j = 0; j < hc; ++j)
       for (int i = 0; i < wc; ++i) out[j * cs + i] = fin(1 + c, p[0][j * wc + i], bi ? p[1][j * wc + i] : 0);
   }
@@ -740,13 +719,11 @@ void deblock_strengths(const PicCtx& pc, std::vector<u8>& bsv, std::vector<u8>& 
   }
 }
 
-void deblock_picture(PicCtx& pc) {
-  HostSurface& s = *pc.s;
-  const int stride = s.coded_w;
+template <class T>
+static void deblock_planes(PicCtx& pc, T* Y, T* UV, const std::vector<u8>& bsv, const std::vector<u8>& bsh) {
+  const int stride = pc.s->coded_w;
   const int W = pc.W, H = pc.H;
-  // bS for every 4-sample edge segment on the 8x8 grid, both directions, before filtering
-  std::vector<u8> bsv, bsh;
-  deblock_strengths(pc, bsv, bsh);
+  const int bdy = pc.bd_y, bdc = pc.bd_c, hiy = (1 << bdy) - 1, hic = (1 << bdc) - 1;
   auto qpc = [&](int qpi, int c) {
     return hevc_chroma_qp(qpi + (c == 0 ? pc.pps->cb_qp_offset : pc.pps->cr_qp_offset));  // (no qPi clipping)
   };
@@ -761,13 +738,13 @@ void deblock_picture(PicCtx& pc) {
         const int qpP = pc.qp[pc.i4(xp, yp)], qpQ = pc.qp[pc.i4(x, y)];
         const SliceHeader& sh = pc.slices[pc.slice[size_t(pc.ctb_of(x, y))]].sh;
         const int qpl = (qpP + qpQ + 1) >> 1;
-        const int beta = kBetaTable[std::clamp(qpl + sh.beta_offset, 0, 51)];
-        const int tc = kTcTable[std::clamp(qpl + 2 * (b - 1) + sh.tc_offset, 0, 53)];
+        const int beta = kBetaTable[std::clamp(qpl + sh.beta_offset, 0, 51)] * (1 << (bdy - 8));
+        const int tc = kTcTable[std::clamp(qpl + 2 * (b - 1) + sh.tc_offset, 0, 53)] * (1 << (bdy - 8));
         const bool nfp = pc.nofilter(pc.i4(xp, yp));
         const bool nfq = pc.nofilter(pc.i4(x, y));
         // sample access: line k (0..3) along the edge, i = distance from the edge (p: -1-i, q: i)
-        auto at = [&](int k, int i) -> u8& {
-          return dir == 0 ? s.y[size_t(y + k) * stride + size_t(x + i)] : s.y[size_t(y + i) * stride + size_t(x + k)];
+        auto at = [&](int k, int i) -> T& {
+          return dir == 0 ? Y[size_t(y + k) * stride + size_t(x + i)] : Y[size_t(y + i) * stride + size_t(x + k)];
         };
         auto P = [&](int k, int i) { return int(at(k, -1 - i)); };
         auto Q = [&](int k, int i) { return int(at(k, i)); };
@@ -786,28 +763,28 @@ void deblock_picture(PicCtx& pc) {
           const int q0 = Q(k, 0), q1 = Q(k, 1), q2 = Q(k, 2), q3 = Q(k, 3);
           if (strong) {
             if (!nfp) {
-              at(k, -1) = u8(std::clamp((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, p0 - 2 * tc, p0 + 2 * tc));
-              at(k, -2) = u8(std::clamp((p2 + p1 + p0 + q0 + 2) >> 2, p1 - 2 * tc, p1 + 2 * tc));
-              at(k, -3) = u8(std::clamp((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, p2 - 2 * tc, p2 + 2 * tc));
+              at(k, -1) = T(std::clamp((p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3, p0 - 2 * tc, p0 + 2 * tc));
+              at(k, -2) = T(std::clamp((p2 + p1 + p0 + q0 + 2) >> 2, p1 - 2 * tc, p1 + 2 * tc));
+              at(k, -3) = T(std::clamp((2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3, p2 - 2 * tc, p2 + 2 * tc));
             }
             if (!nfq) {
-              at(k, 0) = u8(std::clamp((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, q0 - 2 * tc, q0 + 2 * tc));
-              at(k, 1) = u8(std::clamp((p0 + q0 + q1 + q2 + 2) >> 2, q1 - 2 * tc, q1 + 2 * tc));
-              at(k, 2) = u8(std::clamp((p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3, q2 - 2 * tc, q2 + 2 * tc));
+              at(k, 0) = T(std::clamp((p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3, q0 - 2 * tc, q0 + 2 * tc));
+              at(k, 1) = T(std::clamp((p0 + q0 + q1 + q2 + 2) >> 2, q1 - 2 * tc, q1 + 2 * tc));
+              at(k, 2) = T(std::clamp((p0 + q0 + q1 + 3 * q2 + 2 * q3 + 4) >> 3, q2 - 2 * tc, q2 + 2 * tc));
             }
           } else {
             int delta = (9 * (q0 - p0) - 3 * (q1 - p1) + 8) >> 4;
             if (std::abs(delta) >= tc * 10) continue;
             delta = std::clamp(delta, -tc, tc);
-            if (!nfp) at(k, -1) = u8(std::clamp(p0 + delta, 0, 255));
-            if (!nfq) at(k, 0) = u8(std::clamp(q0 - delta, 0, 255));
+            if (!nfp) at(k, -1) = T(std::clamp(p0 + delta, 0, hiy));
+            if (!nfq) at(k, 0) = T(std::clamp(q0 - delta, 0, hiy));
             if (dEp && !nfp) {
               const int dlt = std::clamp((((p2 + p0 + 1) >> 1) - p1 + delta) >> 1, -(tc >> 1), tc >> 1);
-              at(k, -2) = u8(std::clamp(p1 + dlt, 0, 255));
+              at(k, -2) = T(std::clamp(p1 + dlt, 0, hiy));
             }
             if (dEq && !nfq) {
               const int dlt = std::clamp((((q2 + q0 + 1) >> 1) - q1 - delta) >> 1, -(tc >> 1), tc >> 1);
-              at(k, 1) = u8(std::clamp(q1 + dlt, 0, 255));
+              at(k, 1) = T(std::clamp(q1 + dlt, 0, hiy));
             }
           }
         }
@@ -825,28 +802,36 @@ void deblock_picture(PicCtx& pc) {
         const bool nfq = pc.nofilter(pc.i4(x, y));
         for (int c = 0; c < 2; ++c) {
           const int qc = qpc((qpP + qpQ + 1) >> 1, c);
-          const int tc = kTcTable[std::clamp(qc + 2 + sh.tc_offset, 0, 53)];
+          const int tc = kTcTable[std::clamp(qc + 2 + sh.tc_offset, 0, 53)] * (1 << (bdc - 8));
           const int xc = x / 2, yc = y / 2;
           for (int k = 0; k < 2; ++k) {  // 4 luma lines = 2 chroma lines
-            auto at = [&](int i) -> u8& {
-              return dir == 0 ? s.uv[size_t(yc + k) * stride + size_t(2 * (xc + i) + c)]
-                              : s.uv[size_t(yc + i) * stride + size_t(2 * (xc + k) + c)];
+            auto at = [&](int i) -> T& {
+              return dir == 0 ? UV[size_t(yc + k) * stride + size_t(2 * (xc + i) + c)]
+                              : UV[size_t(yc + i) * stride + size_t(2 * (xc + k) + c)];
             };
             const int p0 = at(-1), p1 = at(-2), q0 = at(0), q1 = at(1);
             const int delta = std::clamp((((q0 - p0) * 4) + p1 - q1 + 4) >> 3, -tc, tc);
-            if (!nfp) at(-1) = u8(std::clamp(p0 + delta, 0, 255));
-            if (!nfq) at(0) = u8(std::clamp(q0 - delta, 0, 255));
+            if (!nfp) at(-1) = T(std::clamp(p0 + delta, 0, hic));
+            if (!nfq) at(0) = T(std::clamp(q0 - delta, 0, hic));
           }
         }
       }
   }
 }
 
-// ------------------------------------------------------------------------------ SAO
-void sao_picture(PicCtx& pc) {
+void deblock_picture(PicCtx& pc) {
+  // bS for every 4-sample edge segment on the 8x8 grid, both directions, before filtering
+  std::vector<u8> bsv, bsh;
+  deblock_strengths(pc, bsv, bsh);
   HostSurface& s = *pc.s;
-  const HostSurface src = s;  // deblocked picture: SAO reads it, writes s
-  const int stride = s.coded_w;
+  if (s.wide()) deblock_planes(pc, s.y16.data(), s.uv16.data(), bsv, bsh);
+  else deblock_planes(pc, s.y.data(), s.uv.data(), bsv, bsh);
+}
+
+// ------------------------------------------------------------------------------ SAO
+template <class P>
+static void sao_planes(PicCtx& pc, const P* SY, const P* SUV, P* DY, P* DUV) {
+  const int stride = pc.s->coded_w;
   const int ctb = 1 << pc.log2ctb;
   static constexpr int kHx[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
   static constexpr int kVy[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
@@ -865,21 +850,22 @@ void sao_picture(PicCtx& pc) {
         const int x0 = (rx * ctb) >> sub, y0 = (ry * ctb) >> sub;
         const int w = std::min(ctb >> sub, (pc.W >> sub) - x0), h = std::min(ctb >> sub, (pc.H >> sub) - y0);
         const int pw = pc.W >> sub, ph = pc.H >> sub;
-        auto get = [&](const HostSurface& sf, int x, int y) -> int {
-          return c == 0 ? sf.y[size_t(y) * stride + x] : sf.uv[size_t(y) * stride + 2 * x + (c - 1)];
+        const int bd = c ? pc.bd_c : pc.bd_y;
+        auto get = [&](int x, int y) -> int {
+          return c == 0 ? SY[size_t(y) * stride + x] : SUV[size_t(y) * stride + 2 * x + (c - 1)];
         };
         auto put = [&](int x, int y, int v) {
-          if (c == 0) s.y[size_t(y) * stride + x] = u8(v);
-          else s.uv[size_t(y) * stride + 2 * x + (c - 1)] = u8(v);
+          if (c == 0) DY[size_t(y) * stride + x] = P(v);
+          else DUV[size_t(y) * stride + 2 * x + (c - 1)] = P(v);
         };
         for (int y = y0; y < y0 + h; ++y)
           for (int x = x0; x < x0 + w; ++x) {
             const int lx = x << sub, ly = y << sub;  // luma location of the sample
             if (pc.nofilter(pc.i4(lx, ly))) continue;
-            const int v = get(src, x, y);
+            const int v = get(x, y);
             int off = 0;
             if (sp.type[c] == 1) {
-              const int band = v >> 3;
+              const int band = v >> (bd - 5);
               const int k = (band - sp.band[c]) & 31;
               if (k < 4) off = sp.off[c][k];
             } else {
@@ -908,7 +894,7 @@ void sao_picture(PicCtx& pc) {
                   ok = false;
                   break;
                 }
-                const int nv = get(src, nx, ny);
+                const int nv = get(nx, ny);
                 sgn += (v > nv) - (v < nv);
               }
               if (!ok) continue;
@@ -916,10 +902,17 @@ void sao_picture(PicCtx& pc) {
               if (edge <= 2) edge = edge == 2 ? 0 : edge + 1;
               if (edge) off = sp.off[c][edge - 1];
             }
-            if (off) put(x, y, std::clamp(v + off, 0, 255));
+            if (off) put(x, y, std::clamp(v + off, 0, (1 << bd) - 1));
           }
       }
     }
+}
+
+void sao_picture(PicCtx& pc) {
+  HostSurface& s = *pc.s;
+  const HostSurface src = s;  // deblocked picture: SAO reads it, writes s
+  if (s.wide()) sao_planes(pc, src.y16.data(), src.uv16.data(), s.y16.data(), s.uv16.data());
+  else sao_planes(pc, src.y.data(), src.uv.data(), s.y.data(), s.uv.data());
 }
 
 }  // namespace vep::hevc

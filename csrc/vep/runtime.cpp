@@ -569,6 +569,8 @@ Worker::~Worker() {
     if (!c) continue;
     dev_.free(c->surface.y);
     dev_.free(c->surface.uv);
+    dev_.free(c->surface.y8);
+    dev_.free(c->surface.uv8);
     dev_.free(c->surface.hevc_xg);
     c->set_ring(nullptr);
   }
@@ -640,6 +642,8 @@ void Worker::remove_camera(int idx) {
   auto& c = cams_[size_t(idx)];
   dev_.free(c->surface.y);
   dev_.free(c->surface.uv);
+  dev_.free(c->surface.y8);
+  dev_.free(c->surface.uv8);
   dev_.free(c->surface.hevc_xg);
   c.reset();
 }
@@ -798,29 +802,40 @@ void Worker::loop() {
   }
 }
 
-void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots) {
+void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps) {
   const int wmbs = pi.coded_width / 16, hmbs = pi.coded_height / 16;
   auto& s = c.surface;
-  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && c.ring_ &&
+  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && s.bps == bps && c.ring_ &&
       c.ring_->width() == pi.width && c.ring_->height() == pi.height)
     return;
   dev_.free(s.y);
   dev_.free(s.uv);
-  s.y = s.uv = nullptr;
+  dev_.free(s.y8);
+  dev_.free(s.uv8);
+  s.y = s.uv = s.y8 = s.uv8 = nullptr;
   s.wmbs = wmbs;
   s.hmbs = hmbs;
   s.slots = std::max(1, slots);
+  s.bps = bps;
   const size_t ysz = s.slot_y() * size_t(s.slots);
   if (dev_.gpu()) {
     s.y = static_cast<u8*>(dev_.alloc(ysz));
     s.uv = static_cast<u8*>(dev_.alloc(ysz / 2));
-    VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
-    VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
+    if (bps == 2) {  // Main10: u16 samples at 10-bit black / grey (a 10-bit CVS: HEVC only)
+      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.y), u16(16 << 2), ysz / 2, stream_));
+      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.uv), u16(128 << 2), ysz / 4, stream_));
+      const size_t y8 = size_t(wmbs) * 16 * hmbs * 16;
+      s.y8 = static_cast<u8*>(dev_.alloc(y8));
+      s.uv8 = static_cast<u8*>(dev_.alloc(y8 / 2));
+    } else {
+      VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
+      VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
+    }
     // the camera's lane may be another stream: the fill must land before its first kernel
     if (lanes_.size() > 1) VEP_HIP(hipStreamSynchronize(stream_));
   } else {
     s.host.assign(size_t(s.slots), HostSurface{});
-    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16);
+    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16, bps == 2 ? 10 : 8);
   }
   c.set_ring(std::make_shared<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height));
 }
@@ -939,7 +954,8 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       const bool have = c.ring_ != nullptr;
       if (have && (c.surface.wmbs * 16 != j.pic.coded_width ||
                    c.surface.hmbs * 16 != j.pic.coded_height || c.ring_->width() != j.pic.width ||
-                   c.ring_->height() != j.pic.height || c.surface.slots < j.dpb_slots()))
+                   c.ring_->height() != j.pic.height || c.surface.slots < j.dpb_slots() ||
+                   c.surface.bps != j.bytes_per_sample()))
         resize = true;
     }
   }
@@ -948,7 +964,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
   slots.resize(jobs.size());
   for (size_t i = 0; i < jobs.size(); ++i) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
-    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots());
+    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bytes_per_sample());
     slots[i] = jobs[i].has_output() ? c.ring_->begin_write() : -1;
   }
 }
@@ -1350,8 +1366,13 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const size_t words = size_t(j.upd.mbs() + 31) / 32;
     gpu::DecodeDesc& d = hd[k];
     const size_t tgt = size_t(j.target());
-    d.y = c->surface.y + tgt * c->surface.slot_y();
-    d.uv = c->surface.uv + tgt * c->surface.slot_uv();
+    if (c->surface.bps == 2) {  // Main10: convert / letterbox the 8-bit copy (launch_narrow below)
+      d.y = c->surface.y8;
+      d.uv = c->surface.uv8;
+    } else {
+      d.y = c->surface.y + tgt * c->surface.slot_y();
+      d.uv = c->surface.uv + tgt * c->surface.slot_uv();
+    }
     d.bgr = c->ring_->slot_ptr(st.slots[size_t(i)]);
     (void)words;
     d.mask = mask_ptr(st.d, i);
@@ -1454,7 +1475,11 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.target = p.target;
       g.cb_qp_offset = p.cb_qp_offset;
       g.cr_qp_offset = p.cr_qp_offset;
-      g.flags = (p.deblock ? 1 : 0) | (p.sao ? 2 : 0) | (p.pcm_nofilter ? 4 : 0) | (p.tiles_block_sao ? 8 : 0);
+      g.flags = (p.deblock ? 1 : 0) | (p.sao ? 2 : 0) | (p.pcm_nofilter ? 4 : 0) | (p.tiles_block_sao ? 8 : 0) |
+                (p.wide() ? gpu::kHevcWide : 0);
+      VEP_CHECK(c->surface.bps == (p.wide() ? 2 : 1), "HEVC: picture bit depth differs from the camera's surfaces");
+      g.bd_y = p.bd_y;
+      g.bd_c = p.bd_c;
       g.pus = st.d + a.off_pu;
       g.tus = st.d + a.off_tu;
       g.coefs = reinterpret_cast<const i16*>(st.d + a.off_coef);
@@ -1598,6 +1623,15 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     VEP_HIP(hipMemcpy2DAsync(c->surface.uv, pitch, f.uv, f.pitch_uv, size_t(f.width), size_t(f.height / 2),
                              hipMemcpyDefault, cs));
   }
+  for (int i : outs) {  // Main10 pictures: the published slot's 8-bit NV12 copy
+    const DecodeJob& j = jobs[size_t(i)];
+    const Camera::Surface& sf = cams_[size_t(j.cam)]->surface;
+    if (sf.bps != 2) continue;
+    const size_t tgt = size_t(j.target());
+    gpu::launch_narrow(reinterpret_cast<const u16*>(sf.y + tgt * sf.slot_y()),
+                       reinterpret_cast<const u16*>(sf.uv + tgt * sf.slot_uv()), sf.y8, sf.uv8,
+                       size_t(sf.wmbs) * 16 * sf.hmbs * 16, j.hevc.empty() ? 10 : j.hevc.back()->bd_y, cs);
+  }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), nout, tiles,
                              cs);
   if (opt_.letterbox_size > 0) {
@@ -1643,7 +1677,10 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
       cpu_apply_update(jobs[i].upd, c.surface.host[0]);
     }
     if (!jobs[i].has_output()) continue;
-    const HostSurface& src = c.surface.host[size_t(jobs[i].target())];
+    HostSurface narrow;  // Main10: the 8-bit copy the conversion and the letterbox read
+    const HostSurface& out = c.surface.host[size_t(jobs[i].target())];
+    if (out.wide()) narrow_surface(out, narrow);
+    const HostSurface& src = out.wide() ? narrow : out;
     cpu_nv12_to_bgr(src, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
                     jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
     if (opt_.letterbox_size > 0) {

@@ -120,6 +120,8 @@ struct DecodeJob {
   bool has_output() const { return !general() || out_slot >= 0; }
   // (H.265: the DPB slots plus one scratch surface, the SAO input copy)
   int dpb_slots() const { return !avc.empty() ? avc.back()->dpb_slots : (!hevc.empty() ? hevc_slots + 1 : 1); }
+  // bytes per sample of the camera's surfaces: 2 for Main10 pictures (u16 samples), else 1
+  int bytes_per_sample() const { return !hevc.empty() && hevc.back()->wide() ? 2 : 1; }
   int target() const { return general() ? out_slot : 0; }
 };
 
@@ -187,13 +189,18 @@ class Camera {
   struct Surface {
     int wmbs = 0, hmbs = 0;
     int slots = 1;                 // DPB surfaces (general H.264 path); slot k at y + k * bytes
+    int bps = 1;                   // bytes per sample: 2 = u16 samples (HEVC Main10)
     u8* y = nullptr;
     u8* uv = nullptr;
+    // bps 2: the 8-bit NV12 copy of the picture being published (what the BGR conversion and
+    // the letterbox read; written by gpu::launch_narrow)
+    u8* y8 = nullptr;
+    u8* uv8 = nullptr;
     // H.265 intra edge exchange (gpu::hevc_xg_words of the coded picture) and its round epoch
     u64* hevc_xg = nullptr;
     size_t hevc_xg_words = 0;
     u32 hevc_epoch = 0;
-    size_t slot_y() const { return size_t(wmbs) * 16 * hmbs * 16; }
+    size_t slot_y() const { return size_t(wmbs) * 16 * hmbs * 16 * size_t(bps); }
     size_t slot_uv() const { return slot_y() / 2; }
     std::vector<HostSurface> host;  // CPU backend: one per slot
   } surface;
@@ -376,7 +383,7 @@ class Worker {
     size_t err_cap = 0;
   };
   void loop();
-  void ensure_surface(Camera& c, const PictureInfo& pi, int slots);
+  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps = 1);
   struct Batch {
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;

@@ -96,6 +96,7 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
     hc.weighted = cfg.weighted_p || cfg.weighted_b;
     hc.long_term = cfg.long_term;
     hc.lossless = cfg.lossless;
+    hc.bit_depth = cfg.bit_depth;
     auto enc = std::make_unique<hevc::HevcEncoder>(hc);
     vps_nal_ = enc->vps_nal();
     avc_ = std::move(enc);

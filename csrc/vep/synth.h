@@ -51,6 +51,7 @@ struct SynthConfig {
   bool scaling_lists = false;
   bool long_term = false;
   bool lossless = false;
+  int bit_depth = 8;         // H.265: 10 = Main10 (10-bit samples)
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)

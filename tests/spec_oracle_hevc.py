@@ -3,7 +3,8 @@ the specification text in plain Python — not from csrc/vep/hevc_recon.* or hev
 the decoder, the gfx950 kernels and the closed-loop encoder share. tests/test_spec_oracle_hevc.py
 cross-checks both C++ implementations against it on randomised inputs.
 
-Conventions: 2-D arrays are indexed [y][x]; 8-bit video (BitDepth 8).
+Conventions: 2-D arrays are indexed [y][x]; BitDepth 8 unless set_bit_depth() chose 9..10
+(Main10).
 """
 from __future__ import annotations
 
@@ -11,6 +12,16 @@ import math
 
 BIT_DEPTH = 8
 MAX_VAL = (1 << BIT_DEPTH) - 1
+
+
+def set_bit_depth(bd):
+    """Switch the oracle to BitDepthY = BitDepthC = bd (8 .. 10: Main / Main10); returns the
+    previous value. Every formula reads the module-level values at call time."""
+    global BIT_DEPTH, MAX_VAL, SHIFT1, SHIFT3
+    prev = BIT_DEPTH
+    BIT_DEPTH, MAX_VAL = bd, (1 << bd) - 1
+    SHIFT1, SHIFT3 = min(4, bd - 8), max(2, 14 - bd)
+    return prev
 
 
 def clip3(lo, hi, v):
