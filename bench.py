@@ -75,6 +75,8 @@ def parse_args():
     ap.add_argument("--slices", type=int, default=0,
                     help="slices per picture of the synthetic streams (0: 8 for 4K H.265 — config 5 — else 1); "
                          "the independent slices of an H.265 picture are parsed in parallel")
+    ap.add_argument("--bit-depth", type=int, choices=[8, 10], default=8,
+                    help="h265: 10 = Main10 streams (u16 surfaces on the GPU, narrowed to 8 bits for BGR24)")
     ap.add_argument("--threads", type=int, default=0,
                     help="host parse threads per rank (0 = CPU budget / local ranks - 1, at most 15)")
     ap.add_argument("--parse-window", type=int, default=8,
@@ -192,7 +194,7 @@ def spawn_ranks(n: int) -> int:
 
 def describe_streams(a, compressed):
     if compressed and a.codec == "h265":
-        return (f"HEVC Main CABAC I/P/B, {a.bframes} B per mini-GOP, CTB 32, merge/AMVP/TMVP, "
+        return (f"HEVC {'Main10' if a.bit_depth == 10 else 'Main'} CABAC I/P/B, {a.bframes} B per mini-GOP, CTB 32, merge/AMVP/TMVP, "
                 f"deblocking, {a.slices} slice{'s' if a.slices > 1 else ''} per picture")
     if compressed and a.profile == "baseline":
         return "Baseline CAVLC I/P"
@@ -209,6 +211,7 @@ def make_cfg(vep, a, rank, compressed):
     cfg.codec = a.codec
     cfg.seed = 1 + rank * 100003
     cfg.slices = a.slices
+    cfg.bit_depth = a.bit_depth if a.codec == "h265" else 8
     if compressed:
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
