@@ -479,13 +479,30 @@ PYBIND11_MODULE(_vep, m) {
         tus += p->tus.size();
         for (const auto& t : p->tus) intra_tus += (t.flags & hevc::kTuIntra) ? 1 : 0;
         exchange_violations += hevc::exchange_violations(*p);
+        auto h = [](const void* d, size_t n) {  // FNV-1a of a record array (tests: records equality)
+          u64 x = 1469598103934665603ull;
+          for (size_t i = 0; i < n; ++i) x = (x ^ static_cast<const u8*>(d)[i]) * 1099511628211ull;
+          return x;
+        };
+        last_qp.assign(p->qp.begin(), p->qp.end());
+        last_digest = {h(p->pus.data(), p->pus.size() * sizeof(hevc::GpuPu)),
+                       h(p->tus.data(), p->tus.size() * sizeof(hevc::GpuTu)),
+                       h(p->coefs.data(), p->coefs.size() * 2), h(p->pcm.data(), p->pcm.size()),
+                       h(p->bs_v.data(), p->bs_v.size()), h(p->bs_h.data(), p->bs_h.size()),
+                       h(p->qp.data(), p->qp.size()), h(p->wp.data(), p->wp.size() * sizeof(hevc::GpuWp)),
+                       h(p->sao_params.data(), p->sao_params.size() * sizeof(hevc::GpuSao))};
         max_level = std::max<u64>(max_level, p->level_begin.empty() ? 0 : p->level_begin.size() - 1);
       }
     }
     int coded_w_ = 0, coded_h_ = 0;
+    std::vector<u64> last_digest;  // pus, tus, coefs, pcm, bs_v, bs_h, qp, wp, sao of the last picture
+    std::vector<signed char> last_qp;       // QpY per 4x4 block of the last picture
   };
   py::class_<HevcRecords>(m, "HevcRecordsDecoder")
       .def(py::init<bool>(), py::arg("execute") = true)
+      .def_property_readonly("parallel_units", [](const HevcRecords& r) { return r.d.parallel_units(); })
+      .def_property_readonly("last_digest", [](const HevcRecords& r) { return r.last_digest; })
+      .def_property_readonly("last_qp", [](const HevcRecords& r) { return std::vector<int>(r.last_qp.begin(), r.last_qp.end()); })
       .def("decode",
            [](HevcRecords& r, const AccessUnit& au) {
              std::vector<hevc::FramePtr> fs;

@@ -2,6 +2,7 @@
 // reconstruction it drives, written once for both directions: `CtuLayer<RD>` decodes, and
 // `CtuLayer<WR>` encodes the decisions of a CtuDecider through the same code (see hevc_ctu.h).
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <map>
 
@@ -233,8 +234,11 @@ class CtuLayer {
       qg_y_ = y0;
       qg_coded_ = false;
       cu_qp_delta_ = 0;
+      // qPY_PREV (§8.6.1): SliceQpY for the first quantization group of a slice, a tile or (WPP) a
+      // CTB row, else the QP of the previous QG's last CU. (The quadtree passes a QG start at
+      // every level down to Log2MinCuQpDeltaSize, several at the same position: the first-QG
+      // state ends with the first coded CU, not with the first of those passes.)
       qp_prev_ = first_qg_ ? slice_qp_ : qp_last_;
-      first_qg_ = false;
       qp_pred_ = predict_qp();
     }
     if (split) {
@@ -386,6 +390,7 @@ class CtuLayer {
       m_pcm[k] = u8(pcm);
     });
     qp_last_ = q;
+    first_qg_ = false;
   }
 
   int part_mode(bool intra, int log2, int want) {
@@ -1639,6 +1644,42 @@ int decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_
       VEP_CHECK(dec.terminate() == 1, "HEVC: end_of_subset_one_bit must be 1");
       dec.start(dec.aligned_bytepos());  // byte_alignment(), then a new arithmetic decoder
       start_ctu_state(pc, sl, ctx, L, next, false);
+    }
+  }
+  if (shard) shard->ctus = ctus;
+  return ctus;
+}
+
+int decode_substream(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos, int first_ts, int end_ts,
+                     bool last, SliceShard* shard) {
+  SliceInfo& sl = pc.slices[size_t(slice_idx)];
+  VEP_CHECK(pc.prefilled && first_ts < end_ts && bytepos < n, "HEVC: bad substream");
+  cabac::Ctx ctx[kCtxCount];
+  cabac::Decoder dec(data, n, bytepos);
+  RD e{dec, ctx};
+  CtuLayer<RD> L(pc, slice_idx, e, nullptr);
+  if (shard) L.use_shard(*shard);
+  L.rd = &dec;
+  L.data = data;
+  L.data_n = n;
+  const int first_rs = pc.ts2rs[size_t(first_ts)];
+  // the segment's first substream starts with the segment's state; a later one is a tile start
+  start_ctu_state(pc, sl, ctx, L, first_rs, first_rs == sl.sh.segment_address);
+  int ctus = 0;
+  for (int ts = first_ts; ts < end_ts; ++ts) {
+    const int rs = pc.ts2rs[size_t(ts)];
+    VEP_CHECK(pc.slice[size_t(rs)] == u16(slice_idx), "HEVC: CTU outside the substream's slice");
+    L.ctu(rs, false);
+    ++ctus;
+    const bool end = L.end_of_slice();
+    end_ctu_state(pc, ctx, L, rs, end);
+    VEP_CHECK(dec.bitpos() <= n * 8 + 16, "slice data overrun");
+    if (ts + 1 == end_ts) {
+      VEP_CHECK(end == last, last ? "HEVC: slice segment longer than its CTUs" : "HEVC: substream ends the slice early");
+      if (!last) VEP_CHECK(dec.terminate() == 1, "HEVC: end_of_subset_one_bit must be 1");
+    } else {
+      VEP_CHECK(!end, "HEVC: slice segment ends inside a substream");
+      VEP_CHECK(!substream_boundary(pc, rs, pc.ts2rs[size_t(ts) + 1]), "HEVC: substream spans a tile boundary");
     }
   }
   if (shard) shard->ctus = ctus;

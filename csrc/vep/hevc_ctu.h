@@ -178,6 +178,11 @@ struct SliceShard {
 // number of CTUs decoded.
 int decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos,
                       SliceShard* shard = nullptr);
+// One substream of a slice segment (a tile): CTUs [first_ts, end_ts) in tile scan, from RBSP
+// byte `bytepos` (its entry point); `last`: the segment's final substream (ends with
+// end_of_slice_segment_flag, the others with end_of_subset_one_bit). Returns the CTUs decoded.
+int decode_substream(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos, int first_ts, int end_ts,
+                     bool last, SliceShard* shard);
 // Write mode: CTUs [first_ts, end_ts) in tile scan. `out` receives the slice segment data only;
 // `substreams` (when given) the byte offsets in `out` where each further WPP row / tile
 // substream starts (entry points, before emulation prevention).

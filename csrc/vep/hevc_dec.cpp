@@ -3,6 +3,7 @@
 // layer (hevc_ctu.cpp), the in-loop filters and output in POC order with the bumping process of
 // C.5.2. See hevc_dec.h for the supported feature set.
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 
 #include "bits.h"
@@ -223,7 +224,36 @@ std::vector<std::shared_ptr<GpuPicture>> Decoder::take_gpu_pictures() {
   return v;
 }
 
-void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
+namespace {
+// RBSP offsets of the 2nd.. substreams of a slice segment: the entry point offsets count bytes of
+// the NAL as sent (emulation prevention bytes included, §7.4.7.1) from the first slice data byte.
+std::vector<size_t> substream_starts(const SliceHeader& sh, const u8* ebsp, size_t en) {
+  std::vector<size_t> ep;  // EBSP positions of the removed emulation prevention bytes
+  int zeros = 0;
+  for (size_t i = 0; i < en; ++i) {
+    if (zeros >= 2 && ebsp[i] == 3) {
+      ep.push_back(i);
+      zeros = 0;
+      continue;
+    }
+    zeros = ebsp[i] == 0 ? zeros + 1 : 0;
+  }
+  // EBSP position of the first slice data byte (RBSP data_bytepos)
+  size_t e0 = sh.data_bytepos, k = 0;
+  for (; k < ep.size() && ep[k] <= e0; ++k) ++e0;
+  std::vector<size_t> out;
+  size_t e = e0;
+  for (u32 off : sh.entry_points) {
+    e += off;
+    if (e >= en) return {};
+    const size_t removed = size_t(std::lower_bound(ep.begin(), ep.end(), e) - ep.begin());
+    out.push_back(e - removed);
+  }
+  return out;
+}
+}  // namespace
+
+void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n, const u8* ebsp, size_t en) {
   SliceInfo si;
   si.sh = sh;
   if (!sh.first_slice_in_pic) {
@@ -279,6 +309,9 @@ void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n) {
     if (slice_rbsp_.size() <= k) slice_rbsp_.resize(k + 1);
     slice_rbsp_[k].assign(rbsp, rbsp + n);
     deferred_.push_back({pc_->slices.size() - 1, n, sh.data_bytepos});
+    if (slice_subs_.size() <= k) slice_subs_.resize(k + 1);
+    slice_subs_[k].clear();
+    if (pps_act_->tiles && !sh.entry_points.empty()) slice_subs_[k] = substream_starts(sh, ebsp, en);
     return;
   }
   decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
@@ -289,7 +322,9 @@ void Decoder::run_deferred(bool parallel) {
   std::vector<std::array<size_t, 3>> work;
   work.swap(deferred_);
   PicCtx& pc = *pc_;
-  if (work.size() == 1 || !parallel) {  // the sequential path, nothing to merge
+  size_t subs = 0;
+  for (size_t k = 0; k < work.size(); ++k) subs += k < slice_subs_.size() ? slice_subs_[k].size() : 0;
+  if ((work.size() == 1 && subs == 0) || !parallel) {  // the sequential path, nothing to merge
     for (size_t k = 0; k < work.size(); ++k)
       decode_slice_data(pc, int(work[k][0]), slice_rbsp_[k].data(), work[k][1], work[k][2]);
     return;
@@ -310,8 +345,35 @@ void Decoder::run_deferred(bool parallel) {
   }
   pc.prefilled = true;
   pc.multi = true;
-  while (shards_.size() < work.size()) shards_.push_back(std::make_unique<SliceShard>());
-  for (size_t k = 0; k < work.size(); ++k) {  // (records buffers keep their capacity)
+  // units: whole slices, or (tiles with entry points) each substream of a slice: slice k,
+  // substream start (RBSP), tile-scan range, last substream of the slice
+  struct Unit {
+    size_t k, pos;
+    int first_ts, end_ts;
+    bool last;
+  };
+  std::vector<Unit> units;
+  for (size_t k = 0; k < work.size(); ++k) {
+    const int b = pc.rs2ts[size_t(pc.slices[work[k][0]].sh.segment_address)];
+    const int e = k + 1 < work.size() ? pc.rs2ts[size_t(pc.slices[work[k + 1][0]].sh.segment_address)] : total;
+    std::vector<int> cuts;  // tile starts inside the slice
+    for (int ts = b + 1; ts < e; ++ts)
+      if (pc.tile[size_t(pc.ts2rs[size_t(ts)])] != pc.tile[size_t(pc.ts2rs[size_t(ts - 1)])]) cuts.push_back(ts);
+    const std::vector<size_t>* sub = k < slice_subs_.size() ? &slice_subs_[k] : nullptr;
+    if (!sub || sub->empty() || sub->size() != cuts.size()) {
+      units.push_back({k, work[k][2], -1, -1, true});  // the whole slice (decode_slice_data)
+      continue;
+    }
+    int from = b;
+    size_t pos = work[k][2];
+    for (size_t j = 0; j <= cuts.size(); ++j) {
+      const int to = j < cuts.size() ? cuts[j] : e;
+      units.push_back({k, pos, from, to, j == cuts.size()});
+      if (j < cuts.size()) pos = (*sub)[j], from = to;
+    }
+  }
+  while (shards_.size() < units.size()) shards_.push_back(std::make_unique<SliceShard>());
+  for (size_t k = 0; k < units.size(); ++k) {  // (records buffers keep their capacity)
     SliceShard& sh = *shards_[k];
     sh.g.tus.clear();
     sh.g.pus.clear();
@@ -324,13 +386,20 @@ void Decoder::run_deferred(bool parallel) {
     sh.any_bypass = false;
     sh.ctus = 0;
   }
-  FanOut::shared().run(int(work.size()), [&](int k) {
-    decode_slice_data(pc, int(work[size_t(k)][0]), slice_rbsp_[size_t(k)].data(), work[size_t(k)][1],
-                      work[size_t(k)][2], shards_[size_t(k)].get());
+  parallel_units_ += units.size();
+
+  FanOut::shared().run(int(units.size()), [&](int u) {
+    const Unit& x = units[size_t(u)];
+    const auto& w = work[x.k];
+    if (x.first_ts < 0)
+      decode_slice_data(pc, int(w[0]), slice_rbsp_[x.k].data(), w[1], w[2], shards_[size_t(u)].get());
+    else
+      decode_substream(pc, int(w[0]), slice_rbsp_[x.k].data(), w[1], x.pos, x.first_ts, x.end_ts, x.last,
+                       shards_[size_t(u)].get());
   });
-  // merge in slice order: the records equal a sequential parse's
+  // merge in decoding order (slices, then their tiles): the records equal a sequential parse's
   int ctus = 0;
-  for (size_t k = 0; k < work.size(); ++k) {
+  for (size_t k = 0; k < units.size(); ++k) {
     SliceShard& sh = *shards_[k];
     ctus += sh.ctus;
     pc.any_bypass |= sh.any_bypass;
@@ -463,7 +532,7 @@ std::vector<FramePtr> Decoder::decode(const AccessUnit& au, i64 tag) {
         throw Error("HEVC: slice segment without the start of its picture");
       }
       if (skip_pic_) continue;
-      decode_slice(sh, rbsp_.data(), rn);
+      decode_slice(sh, rbsp_.data(), rn, p, n);
     } catch (...) {
       cur_ = nullptr;  // the damaged picture is dropped
       cur_gpu_ = nullptr;

@@ -116,6 +116,8 @@ class Decoder {
   std::vector<std::shared_ptr<struct GpuPicture>> take_gpu_pictures();
   int gpu_slots() const { return gpu_slots_; }  // surfaces a camera needs (max DPB + 2)
   FramePtr last_decoded() const { return last_; }
+  // slices / tile substreams parsed as parallel units so far (tests)
+  u64 parallel_units() const { return parallel_units_; }
   // statistics of the last picture (tests): CU counts by kind
   struct Stats {
     int intra = 0, inter = 0, skip = 0, pcm = 0, merge = 0, bi = 0, tskip = 0, amp = 0;
@@ -126,7 +128,8 @@ class Decoder {
                      std::vector<FramePtr>& out);
   void finish_picture(std::vector<FramePtr>& out);
   void bump(std::vector<FramePtr>& out);
-  void decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n);
+  // (ebsp / en: the NAL as received, for the RBSP positions of the entry points)
+  void decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n, const u8* ebsp, size_t en);
   // the picture's deferred slices: in parallel when the picture is complete, else in order
   void run_deferred(bool parallel);
   std::map<int, Vps> vps_;
@@ -153,7 +156,8 @@ class Decoder {
   // records-mode pictures recycled per decoder (recycle.h: resident buffers, no page faults)
   std::shared_ptr<Recycler<struct GpuPicture>> gpu_pool_;
   std::vector<std::shared_ptr<struct GpuPicture>> gpu_out_;
-  // Independent slices of one picture are parsed in parallel on the shared fan-out pool
+  // Independent slices (and the tiles inside them) of one picture are parsed in parallel on the
+  // shared fan-out pool
   // (fanout.h): their slice data is kept (deferred_: slice index, RBSP bytes, data offset) until
   // the picture's last slice arrived. Pictures with WPP or dependent slice segments (contexts
   // carried between segments) are parsed slice by slice as before. VEP_HEVC_SLICE_THREADS=0: off.
@@ -161,6 +165,10 @@ class Decoder {
   bool defer_ = false;
   std::vector<std::vector<u8>> slice_rbsp_;
   std::vector<std::array<size_t, 3>> deferred_;
+  // Tiles: the RBSP offsets of a deferred slice's 2nd.. substreams (its entry points), so each
+  // tile of the slice is parsed as a unit of its own (tiles share no CABAC state or prediction)
+  std::vector<std::vector<size_t>> slice_subs_;
+  u64 parallel_units_ = 0;
   std::vector<std::unique_ptr<struct SliceShard>> shards_;
 };
 

@@ -22,7 +22,7 @@ def _stream(native, w, h, n, **kw):
     return aus, rec
 
 
-def _decode(native, aus, monkeypatch, parallel):
+def _decode(native, aus, monkeypatch, parallel, units=None):
     monkeypatch.setenv("VEP_HEVC_SLICE_THREADS", "1" if parallel else "0")
     d = native.HevcRecordsDecoder()  # records mode + the CPU mirror of the GPU kernels
     out = {}
@@ -31,6 +31,8 @@ def _decode(native, aus, monkeypatch, parallel):
             out[pts] = (y.copy(), uv.copy())
     for pts, poc, t, (y, uv), slot in d.flush():
         out[pts] = (y.copy(), uv.copy())
+    if units is not None:
+        units.append(d.parallel_units)
     return out, d.stats
 
 
@@ -47,3 +49,23 @@ def test_parallel_slices_bit_exact(native, monkeypatch, kw):
         for a, b, r in zip(par[pts], seq[pts], rec[pts]):
             assert np.array_equal(a, b) and np.array_equal(a, r[: a.shape[0], : a.shape[1]]), pts
     assert st_par == st_seq  # identical records (counts of PUs / TUs / intra TUs / levels)
+
+
+@pytest.mark.parametrize("kw", [dict(tile_cols=3, tile_rows=2), dict(tile_cols=2, tile_rows=3, coverage=True, seed=5),
+                                dict(tile_cols=4, tile_rows=1, bit_depth=10)],
+                         ids=["1-slice-6-tiles", "coverage-tiles", "main10-tiles"])
+def test_parallel_tiles_of_one_slice_bit_exact(native, monkeypatch, kw):
+    """One slice, several tiles: each tile substream (found from the slice header's entry point
+    offsets, emulation prevention bytes counted) is parsed as a unit of its own."""
+    w, h = (352, 288) if kw.get("coverage") else (640, 360)
+    aus, rec = _stream(native, w, h, 8, **kw)
+    units = []
+    par, st_par = _decode(native, aus, monkeypatch, True, units)
+    seq, st_seq = _decode(native, aus, monkeypatch, False)
+    assert set(par) == set(seq) == set(rec)
+    for pts in rec:
+        for a, b, r in zip(par[pts], seq[pts], rec[pts]):
+            assert np.array_equal(a, b) and np.array_equal(a, r[: a.shape[0], : a.shape[1]]), pts
+    assert st_par == st_seq
+    tiles = kw["tile_cols"] * kw["tile_rows"]
+    assert units[0] >= tiles * len(aus) // 2  # the pictures ran tile by tile
