@@ -556,6 +556,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
       .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.coded; })
       .def_property_readonly("general", [](const CpuDecoder& d) { return d.general; })
+      .def_property_readonly("parallel_slices", [](const CpuDecoder& d) { return d.avc.parallel_slices_run(); })
       .def("surface", [](const CpuDecoder& d) {
         const HostSurface& s = d.out();
         py::array_t<uint8_t> y({s.coded_h, s.coded_w});

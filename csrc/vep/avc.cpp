@@ -9,6 +9,7 @@
 
 #include "avc_cavlc.h"
 #include "avc_internal.h"
+#include "fanout.h"
 
 namespace vep::avc {
 
@@ -1025,6 +1026,21 @@ int dpb_slots_for(const Sps& sps) {
 
 static void validate_picture(const Picture& p);
 
+// One slice kept for the parallel parse of its access unit (Decoder::parse).
+struct Decoder::SliceUnit {
+  MbNeighbours nb;        // this slice's neighbour state (own epoch: other slices' MBs unavailable)
+  Picture shard;          // this slice's records (full-size MB array, own pools)
+  ColBuild colb;          // colocated motion into the picture's table, with this slice's list uids
+  std::vector<u8> rbsp;   // slice RBSP after the NAL header byte
+  SliceHdr sh;
+  const Sps* sps = nullptr;
+  const Pps* pps = nullptr;
+  size_t bitpos = 0;      // first bit of slice_data()
+  int slice_idx = 0;
+  std::vector<ListEntry> list[2];
+  std::array<std::vector<u32>, 2> uids;
+};
+
 PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   auto pic = pic_pool_->acquire([](Picture& p) {  // default state, pool capacities kept
     auto mbs = std::move(p.mbs);
@@ -1056,6 +1072,14 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
     Picture* p;
     ~ColbGuard() { p->colb = nullptr; }
   } colb_guard{pic.get()};
+  int nslices = 0;  // slice NALs of the access unit: several -> parsed in parallel
+  for (size_t i = 0; i < au.nals.size(); ++i)
+    if (au.nal_size(i) >= 2) {
+      const int t = h264::nal_type(au.nal(i)[0]);
+      nslices += (t == h264::kNalSlice || t == h264::kNalIdr) ? 1 : 0;
+    }
+  const bool par = parallel_slices_ && nslices >= 2 && FanOut::shared().size() > 0;
+  int nunits = 0;
   for (size_t i = 0; i < au.nals.size(); ++i) {
     const u8* p = au.nal(i);
     const size_t n = au.nal_size(i);
@@ -1169,55 +1193,89 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       for (const auto& e : list_[l]) uids[size_t(l)].push_back(e.uid);
     slice_uids.push_back(std::move(uids));
     colb.uids = &slice_uids.back();
-    if (legacy_slice(sh, sps, pps)) {
-      const size_t stop = BitReader(r + 1, rn - 1).stop_bit_pos();
-      SliceCtx sc{sh, pps, slice_idx, sh.type() == h264::kP, sh.qp, list_[0]};
-      const int total = pic->nmbs();
-      int mb = sh.first_mb;
-      VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
-      bool more = true;
-      while (more) {
-        if (sc.is_p) {
-          const u32 run = br.ue();
-          VEP_CHECK(u32(total - mb) >= run, "mb_skip_run past end of picture");
-          MbDecoder d(nb_, *pic, sc);
-          for (u32 k = 0; k < run; ++k) d.skip(mb++);
-          if (run > 0) {
-            more = br.pos() < stop;
-            if (!more) break;
-          }
-        }
-        VEP_CHECK(mb < total, "macroblock address past end of picture");
-        MbDecoder d(nb_, *pic, sc);
-        d.macroblock(br, mb);
-        if (d.qp_out_ >= 0) sc.qp = d.qp_out_;
-        VEP_CHECK(!br.overrun(), "slice data overrun");
-        more = br.pos() < stop;
-        ++mb;
-      }
+    if (par) {  // kept until the access unit's last slice (parsed in parallel below)
+      if (units_.size() <= size_t(nunits)) units_.push_back(std::make_unique<SliceUnit>());
+      SliceUnit& u = *units_[size_t(nunits++)];
+      u.rbsp.assign(r + 1, r + rn);
+      u.sh = sh;
+      u.sps = &sps;
+      u.pps = &pps;
+      u.bitpos = br.pos();
+      u.slice_idx = slice_idx;
+      u.list[0] = list_[0];
+      u.list[1] = list_[1];
+      u.uids = slice_uids.back();
     } else {
-      SliceEnv env;
-      env.sh = &sh;
-      env.sps = &sps;
-      env.pps = &pps;
-      env.slice = slice_idx;
-      env.list[0] = &list_[0];
-      env.list[1] = &list_[1];
-      env.cur_poc = pic->poc;
-      env.scaling = h264::resolve_scaling(sps, pps);
-      decode_slice_generic(nb_, *pic, env, r + 1, rn - 1, br.pos());
+      parse_slice_data(nb_, *pic, sh, sps, pps, r + 1, rn - 1, br.pos(), slice_idx, list_);
     }
     ++slice_idx;
     VEP_CHECK(slice_idx < 65535, "too many slices");
   }
   VEP_CHECK(got, "access unit has no slice");
   (void)act_pps;
+  std::vector<u8> covered;  // parallel slices: MBs some slice decoded
+  if (par) {
+    const int W = pic->wmbs, H = pic->hmbs;
+    ColMotion* col_target = colb.col;
+    FanOut::shared().run(nunits, [&](int k) {
+      SliceUnit& u = *units_[size_t(k)];
+      u.nb.reset(W, H);
+      Picture& sh = u.shard;
+      sh.wmbs = W;
+      sh.hmbs = H;
+      if (sh.mbs.size() != size_t(W) * H) sh.mbs.assign(size_t(W) * H, MbRec{});
+      sh.coefs.clear();
+      sh.mvs.clear();
+      sh.wps.clear();
+      sh.intra_mbs = sh.intra_res = sh.inter_mbs = 0;
+      sh.deblock = false;
+      sh.target = pic->target;
+      sh.dpb_slots = pic->dpb_slots;
+      sh.constrained_intra = pic->constrained_intra;
+      sh.poc = pic->poc;
+      u.colb.col = col_target;
+      u.colb.uids = &u.uids;
+      sh.colb = col_target ? &u.colb : nullptr;
+      parse_slice_data(u.nb, sh, u.sh, *u.sps, *u.pps, u.rbsp.data(), u.rbsp.size(), u.bitpos, u.slice_idx, u.list);
+    });
+    parallel_slices_run_ += u64(nunits);
+    // merge in slice order: the MBs each slice decoded, pool offsets rebased
+    covered.assign(size_t(pic->nmbs()), 0);
+    for (int k = 0; k < nunits; ++k) {
+      SliceUnit& u = *units_[size_t(k)];
+      const Picture& sh = u.shard;
+      const u32 coef0 = u32(pic->coefs.size()), mv0 = u32(pic->mvs.size()), wp0 = u32(pic->wps.size());
+      const u32 res0 = u32(pic->intra_res);
+      pic->coefs.insert(pic->coefs.end(), sh.coefs.begin(), sh.coefs.end());
+      pic->mvs.insert(pic->mvs.end(), sh.mvs.begin(), sh.mvs.end());
+      pic->wps.insert(pic->wps.end(), sh.wps.begin(), sh.wps.end());
+      pic->intra_mbs += sh.intra_mbs;
+      pic->intra_res += sh.intra_res;
+      pic->inter_mbs += sh.inter_mbs;
+      pic->deblock |= sh.deblock;
+      for (int mb = u.sh.first_mb; mb < pic->nmbs(); ++mb) {
+        if (!u.nb.announced(mb)) continue;
+        VEP_CHECK(!covered[size_t(mb)], "H.264: slices overlap");
+        covered[size_t(mb)] = 1;
+        MbRec m = sh.mbs[size_t(mb)];
+        m.coef += coef0;
+        if (m.kind == kSkip || m.kind == kInter) m.mv += mv0;
+        if (m.flags & kMbWp) m.wp += wp0;
+        if (m.res != kNoRes) m.res += res0;
+        pic->mbs[size_t(mb)] = m;
+      }
+    }
+  }
+  int ncovered = 0;
+  if (par)
+    for (u8 c : covered) ncovered += c;
+  auto announced = [&](int mb) { return par ? covered[size_t(mb)] != 0 : nb_.announced(mb); };
   // conceal macroblocks no slice covered (lost slices): copy from the first reference, or grey
   // (an MB announced but not finished would have thrown: announced = decoded here)
   int missing = 0;
-  for (int mb = 0; nb_.announced_count() < pic->nmbs() && mb < pic->nmbs(); ++mb) {
+  for (int mb = 0; (par ? ncovered : nb_.announced_count()) < pic->nmbs() && mb < pic->nmbs(); ++mb) {
     MbRec& m = pic->mbs[size_t(mb)];
-    if (nb_.announced(mb)) continue;
+    if (announced(mb)) continue;
     ++missing;
     if (pic->colb) colb.none(mb);
     m = MbRec{};
@@ -1248,9 +1306,59 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   const bool boundary = first.idr() || first.has_mmco5();
   bump(*pic, boundary, boundary && (hard_flush || reorder_cur_ == 0));
   // (store_mb validated every record as it was written; concealed ones are built in range)
-  if (missing) validate(*pic);
+  if (missing || par) validate(*pic);
   else validate_picture(*pic);
   return pic;
+}
+
+Decoder::Decoder() {
+  if (const char* e = std::getenv("VEP_AVC_SLICE_THREADS")) parallel_slices_ = e[0] != '0';
+}
+Decoder::~Decoder() = default;
+
+// The slice data of one slice (either entropy layer) into `pic` through neighbour state `nb`.
+void Decoder::parse_slice_data(MbNeighbours& nb, Picture& pic, const SliceHdr& sh, const Sps& sps, const Pps& pps,
+                               const u8* data, size_t n, size_t bitpos, int slice_idx,
+                               const std::vector<ListEntry> (&lists)[2]) {
+  if (legacy_slice(sh, sps, pps)) {
+    Bits br(data, n, bitpos);
+    const size_t stop = BitReader(data, n).stop_bit_pos();
+    SliceCtx sc{sh, pps, slice_idx, sh.type() == h264::kP, sh.qp, lists[0]};
+    const int total = pic.nmbs();
+    int mb = sh.first_mb;
+    VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
+    bool more = true;
+    while (more) {
+      if (sc.is_p) {
+        const u32 run = br.ue();
+        VEP_CHECK(u32(total - mb) >= run, "mb_skip_run past end of picture");
+        MbDecoder d(nb, pic, sc);
+        for (u32 k = 0; k < run; ++k) d.skip(mb++);
+        if (run > 0) {
+          more = br.pos() < stop;
+          if (!more) break;
+        }
+      }
+      VEP_CHECK(mb < total, "macroblock address past end of picture");
+      MbDecoder d(nb, pic, sc);
+      d.macroblock(br, mb);
+      if (d.qp_out_ >= 0) sc.qp = d.qp_out_;
+      VEP_CHECK(!br.overrun(), "slice data overrun");
+      more = br.pos() < stop;
+      ++mb;
+    }
+    return;
+  }
+  SliceEnv env;
+  env.sh = &sh;
+  env.sps = &sps;
+  env.pps = &pps;
+  env.slice = slice_idx;
+  env.list[0] = &lists[0];
+  env.list[1] = &lists[1];
+  env.cur_poc = pic.poc;
+  env.scaling = h264::resolve_scaling(sps, pps);
+  decode_slice_generic(nb, pic, env, data, n, bitpos);
 }
 
 // One record against the picture's pools (store_mb checks every record as it is written, so

@@ -371,6 +371,9 @@ class Decoder {
   int compute_poc(const SliceHdr& sh, const h264::Sps& sps);
   void bump(Picture& pic, bool new_epoch, bool hard);
   int reorder_depth(const h264::Sps& sps) const;
+  void parse_slice_data(MbNeighbours& nb, Picture& pic, const SliceHdr& sh, const h264::Sps& sps,
+                        const h264::Pps& pps, const u8* data, size_t n, size_t bitpos, int slice_idx,
+                        const std::vector<ListEntry> (&lists)[2]);
 
   std::map<int, h264::Sps> sps_;
   std::map<int, h264::Pps> pps_;
@@ -399,6 +402,20 @@ class Decoder {
   int prev_frame_num_ = 0, prev_frame_num_offset_ = 0;
   bool prev_ref_mmco5_ = false;
   std::vector<std::vector<MbState>> spare_;  // recycled MbState arrays
+  // Slices of one picture are parsed in parallel on the shared fan-out pool (fanout.h) when the
+  // access unit holds several: each slice into its own neighbour state (other slices' MBs are
+  // unavailable to it by definition, §6.4.11) and its own records shard, merged into the
+  // picture in slice order (the records then equal a sequential parse's). VEP_AVC_SLICE_THREADS=0:
+  // off.
+  struct SliceUnit;
+  bool parallel_slices_ = true;
+  std::vector<std::unique_ptr<SliceUnit>> units_;
+  u64 parallel_slices_run_ = 0;
+
+ public:
+  Decoder();
+  ~Decoder();
+  u64 parallel_slices_run() const { return parallel_slices_run_; }  // (tests)
 };
 
 // CPU reference reconstruction of `pic` into DPB surfaces `slots` (coded size; references are
