@@ -415,35 +415,61 @@ static void bus_stress() {
               (unsigned long long)snaps.load());
 }
 
+// Parallel parse units of one picture on the shared fan-out pool, several decoders at once:
+// H.265 slices, the tiles of one slice, wavefront rows (per-CTB done flags + per-row contexts)
+// and H.264 slices (per-slice neighbour state and records shards).
 static void slice_fanout_stress() {
-  SynthConfig c;
-  c.width = 320;
-  c.height = 192;
-  c.gop = 8;
-  c.codec = Codec::kH265;
-  c.compressed = true;
-  c.slices = 4;
-  c.bframes = 1;
-  std::vector<AuPtr> aus;
-  {
-    SynthH264 enc(c);
-    for (int i = 0; i < 12; ++i) aus.push_back(enc.next());
-  }
+  struct Stream {
+    Codec codec;
+    int slices, tile_cols, tile_rows;
+    bool wpp;
+  };
+  const Stream streams[] = {{Codec::kH265, 4, 1, 1, false}, {Codec::kH265, 1, 3, 2, false},
+                            {Codec::kH265, 2, 1, 1, true}, {Codec::kH264, 4, 1, 1, false}};
   std::atomic<u64> pictures{0};
-  std::vector<std::thread> th;
-  for (int d = 0; d < 3; ++d)
-    th.emplace_back([&, d] {
-      hevc::Decoder dec;
-      dec.set_gpu_mode(d != 0);  // records mode (shards merged) and CPU reconstruction
-      for (int loop = 0; loop < 3; ++loop) {
-        for (const auto& au : aus) dec.decode(*au, 0);
-        (void)dec.flush();
-        (void)dec.take_gpu_pictures();
-        pictures.fetch_add(aus.size());
-      }
-    });
-  for (auto& t : th) t.join();
-  std::printf("parallel slices: %llu pictures\n", (unsigned long long)pictures.load());
+  for (const Stream& st : streams) {
+    SynthConfig c;
+    c.width = 320;
+    c.height = 192;
+    c.gop = 8;
+    c.codec = st.codec;
+    c.compressed = true;
+    c.profile = "high";
+    c.slices = st.slices;
+    c.tile_cols = st.tile_cols;
+    c.tile_rows = st.tile_rows;
+    c.wpp = st.wpp;
+    c.bframes = 1;
+    std::vector<AuPtr> aus;
+    {
+      SynthH264 enc(c);
+      for (int i = 0; i < 12; ++i) aus.push_back(enc.next());
+    }
+    std::vector<std::thread> th;
+    for (int d = 0; d < 3; ++d)
+      th.emplace_back([&, d] {
+        if (st.codec == Codec::kH264) {
+          avc::Decoder dec;
+          for (int loop = 0; loop < 3; ++loop) {
+            for (const auto& au : aus) (void)dec.parse(*au, 0);
+            (void)dec.flush_output();
+            dec.reset_references();
+            pictures.fetch_add(aus.size());
+          }
+          return;
+        }
+        hevc::Decoder dec;
+        dec.set_gpu_mode(d != 0);  // records mode (shards merged) and CPU reconstruction
+        for (int loop = 0; loop < 3; ++loop) {
+          for (const auto& au : aus) dec.decode(*au, 0);
+          (void)dec.flush();
+          (void)dec.take_gpu_pictures();
+          pictures.fetch_add(aus.size());
+        }
+      });
+    for (auto& t : th) t.join();
+  }
+  std::printf("parallel slices / tiles / wavefront rows: %llu pictures\n", (unsigned long long)pictures.load());
 }
 
 int main() {

@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstring>
 #include <map>
+#include <thread>
 
 #include "hevc_ctu.h"
 #include "hevc_recon.h"
@@ -1580,7 +1581,13 @@ void start_ctu_state(PicCtx& pc, const SliceInfo& sl, cabac::Ctx* ctx, L& layer,
     const int tr = rs - pc.wctb + 1;
     const bool avail = ry > 0 && rx + 1 < pc.wctb && pc.slice[size_t(tr)] != 0xFFFF &&
                        pc.sord[size_t(tr)] == sl.ord && pc.tile[size_t(tr)] == pc.tile[size_t(rs)];
-    if (avail) std::copy(pc.wpp_ctx, pc.wpp_ctx + kCtxCount, ctx);
+    if (avail && pc.wpp_sync) {  // rows in parallel: the row above's storage, once it exists
+      pc.wpp_sync->wait(tr);
+      const cabac::Ctx* src = pc.wpp_sync->rows.data() + size_t(ry - 1) * kCtxCount;
+      std::copy(src, src + kCtxCount, ctx);
+    } else if (avail) {
+      std::copy(pc.wpp_ctx, pc.wpp_ctx + kCtxCount, ctx);
+    }
     else init_ctx(ctx, sl.sh, sl.qp);
     layer.reset_qp_prediction();
     return;
@@ -1597,7 +1604,8 @@ void start_ctu_state(PicCtx& pc, const SliceInfo& sl, cabac::Ctx* ctx, L& layer,
 template <class L>
 void end_ctu_state(PicCtx& pc, const cabac::Ctx* ctx, const L& layer, int rs, bool segment_end) {
   if (pc.pps->entropy_coding_sync && rs % pc.wctb == pc.tile_col_start(rs % pc.wctb) + 1)
-    std::copy(ctx, ctx + kCtxCount, pc.wpp_ctx);
+    std::copy(ctx, ctx + kCtxCount,
+              pc.wpp_sync ? pc.wpp_sync->rows.data() + size_t(rs / pc.wctb) * kCtxCount : pc.wpp_ctx);
   if (segment_end && pc.pps->dependent_slice_segments) {
     std::copy(ctx, ctx + kCtxCount, pc.ds_ctx);
     pc.ds_qp = layer.qp_last();
@@ -1650,6 +1658,13 @@ int decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_
   return ctus;
 }
 
+void WppSync::wait(int rs) const {
+  for (u32 spin = 0; !done[size_t(rs)].load(std::memory_order_acquire); ++spin) {
+    if (abort.load(std::memory_order_relaxed)) throw Error("HEVC: a wavefront row failed");
+    if (spin > 64) std::this_thread::yield();
+  }
+}
+
 int decode_substream(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t bytepos, int first_ts, int end_ts,
                      bool last, SliceShard* shard) {
   SliceInfo& sl = pc.slices[size_t(slice_idx)];
@@ -1666,13 +1681,22 @@ int decode_substream(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t
   // the segment's first substream starts with the segment's state; a later one is a tile start
   start_ctu_state(pc, sl, ctx, L, first_rs, first_rs == sl.sh.segment_address);
   int ctus = 0;
+  WppSync* ws = pc.wpp_sync;
   for (int ts = first_ts; ts < end_ts; ++ts) {
     const int rs = pc.ts2rs[size_t(ts)];
     VEP_CHECK(pc.slice[size_t(rs)] == u16(slice_idx), "HEVC: CTU outside the substream's slice");
+    if (ws && rs >= pc.wctb) {  // wavefront: the CTBs above-left, above and above-right it may read
+      const int rx = rs % pc.wctb;
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int nx = rx + dx, nrs = rs - pc.wctb + dx;
+        if (nx >= 0 && nx < pc.wctb && pc.sord[size_t(nrs)] == pc.sord[size_t(rs)]) ws->wait(nrs);
+      }
+    }
     L.ctu(rs, false);
     ++ctus;
     const bool end = L.end_of_slice();
     end_ctu_state(pc, ctx, L, rs, end);
+    if (ws) ws->done[size_t(rs)].store(1, std::memory_order_release);
     VEP_CHECK(dec.bitpos() <= n * 8 + 16, "slice data overrun");
     if (ts + 1 == end_ts) {
       VEP_CHECK(end == last, last ? "HEVC: slice segment longer than its CTUs" : "HEVC: substream ends the slice early");

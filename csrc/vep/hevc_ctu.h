@@ -3,6 +3,8 @@
 #pragma once
 
 #include <array>
+#include <atomic>
+#include <memory>
 
 #include "cabac.h"
 #include "hevc_dec.h"
@@ -28,6 +30,25 @@ struct SliceInfo {
   std::vector<FramePtr> list[2];
   std::vector<int> list_poc[2];
   std::vector<u8> list_lt[2];  // the entry is a long-term reference picture
+};
+
+// Wavefront rows of one picture parsed in parallel (Decoder, WPP): per CTB a done flag
+// (release / acquire), per CTB row the contexts stored after its 2nd CTB, and an abort flag (a
+// row that fails releases the rows waiting on it).
+struct WppSync {
+  std::unique_ptr<std::atomic<u8>[]> done;
+  std::vector<cabac::Ctx> rows;  // hctb x kCtxCount
+  std::atomic<bool> abort{false};
+  int wctb = 0;
+  void reset(int w, int h) {
+    if (w * h != wctb * int(rows.size() / kCtxCount) || !done) done.reset(new std::atomic<u8>[size_t(w) * h]);
+    for (int k = 0; k < w * h; ++k) done[size_t(k)].store(0, std::memory_order_relaxed);
+    rows.resize(size_t(h) * kCtxCount);
+    wctb = w;
+    abort.store(false);
+  }
+  // until CTB rs is parsed (spin, then yield); throws when another row failed
+  void wait(int rs) const;
 };
 
 struct PicCtx {
@@ -61,6 +82,7 @@ struct PicCtx {
   // CABAC state carried across CTUs / segments: WPP storage (after the 2nd CTB of a row) and
   // the end of the previous slice segment (dependent slice segments)
   cabac::Ctx wpp_ctx[kCtxCount];
+  WppSync* wpp_sync = nullptr;  // rows in parallel: per-row storage + CTB done flags
   cabac::Ctx ds_ctx[kCtxCount];
   int ds_qp = 26;
   Decoder::Stats stats;

@@ -185,7 +185,8 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   deferred_.clear();
   // independent slices in parallel: no WPP (rows share contexts) and no dependent segments
   // (decode_slice switches deferral off when one arrives)
-  defer_ = parallel_slices_ && !pps.entropy_coding_sync && FanOut::shared().size() > 0;
+  // (tiles and wavefront rows together: parsed slice by slice)
+  defer_ = parallel_slices_ && !(pps.entropy_coding_sync && pps.tiles) && FanOut::shared().size() > 0;
   if (gpu_mode_) {
     cur_gpu_ = gpu_pool_->acquire([](GpuPicture& g) {  // default state, capacities kept
       GpuPicture fresh;
@@ -311,7 +312,8 @@ void Decoder::decode_slice(const SliceHeader& sh, const u8* rbsp, size_t n, cons
     deferred_.push_back({pc_->slices.size() - 1, n, sh.data_bytepos});
     if (slice_subs_.size() <= k) slice_subs_.resize(k + 1);
     slice_subs_[k].clear();
-    if (pps_act_->tiles && !sh.entry_points.empty()) slice_subs_[k] = substream_starts(sh, ebsp, en);
+    if ((pps_act_->tiles || pps_act_->entropy_coding_sync) && !sh.entry_points.empty())
+      slice_subs_[k] = substream_starts(sh, ebsp, en);
     return;
   }
   decode_slice_data(*pc_, int(pc_->slices.size()) - 1, rbsp, n, sh.data_bytepos);
@@ -356,9 +358,12 @@ void Decoder::run_deferred(bool parallel) {
   for (size_t k = 0; k < work.size(); ++k) {
     const int b = pc.rs2ts[size_t(pc.slices[work[k][0]].sh.segment_address)];
     const int e = k + 1 < work.size() ? pc.rs2ts[size_t(pc.slices[work[k + 1][0]].sh.segment_address)] : total;
-    std::vector<int> cuts;  // tile starts inside the slice
-    for (int ts = b + 1; ts < e; ++ts)
-      if (pc.tile[size_t(pc.ts2rs[size_t(ts)])] != pc.tile[size_t(pc.ts2rs[size_t(ts - 1)])]) cuts.push_back(ts);
+    std::vector<int> cuts;  // substream starts inside the slice: tiles, or CTB rows (WPP)
+    const bool wpp = pc.pps->entropy_coding_sync;
+    for (int ts = b + 1; ts < e; ++ts) {
+      const int rs = pc.ts2rs[size_t(ts)];
+      if (wpp ? pc.ctb_row_start(rs) : pc.tile[size_t(rs)] != pc.tile[size_t(pc.ts2rs[size_t(ts - 1)])]) cuts.push_back(ts);
+    }
     const std::vector<size_t>* sub = k < slice_subs_.size() ? &slice_subs_[k] : nullptr;
     if (!sub || sub->empty() || sub->size() != cuts.size()) {
       units.push_back({k, work[k][2], -1, -1, true});  // the whole slice (decode_slice_data)
@@ -388,14 +393,32 @@ void Decoder::run_deferred(bool parallel) {
   }
   parallel_units_ += units.size();
 
+  // wavefront rows: each waits for the CTBs above it (units are taken in order, so a waited-on
+  // row was claimed by a running thread: FanOut hands out indices in increasing order)
+  bool rows = false;
+  for (const Unit& x : units) rows |= x.first_ts >= 0 && pc.pps->entropy_coding_sync;
+  if (rows) {
+    if (!wpp_sync_) wpp_sync_ = std::make_unique<WppSync>();
+    wpp_sync_->reset(pc.wctb, pc.hctb);
+    pc.wpp_sync = wpp_sync_.get();
+  }
+  struct Clear {
+    PicCtx& pc;
+    ~Clear() { pc.wpp_sync = nullptr; }
+  } clear{pc};
   FanOut::shared().run(int(units.size()), [&](int u) {
     const Unit& x = units[size_t(u)];
     const auto& w = work[x.k];
-    if (x.first_ts < 0)
-      decode_slice_data(pc, int(w[0]), slice_rbsp_[x.k].data(), w[1], w[2], shards_[size_t(u)].get());
-    else
-      decode_substream(pc, int(w[0]), slice_rbsp_[x.k].data(), w[1], x.pos, x.first_ts, x.end_ts, x.last,
-                       shards_[size_t(u)].get());
+    try {
+      if (x.first_ts < 0)
+        decode_slice_data(pc, int(w[0]), slice_rbsp_[x.k].data(), w[1], w[2], shards_[size_t(u)].get());
+      else
+        decode_substream(pc, int(w[0]), slice_rbsp_[x.k].data(), w[1], x.pos, x.first_ts, x.end_ts, x.last,
+                         shards_[size_t(u)].get());
+    } catch (...) {
+      if (pc.wpp_sync) pc.wpp_sync->abort.store(true);
+      throw;
+    }
   });
   // merge in decoding order (slices, then their tiles): the records equal a sequential parse's
   int ctus = 0;

@@ -35,6 +35,8 @@
 
 namespace vep::hevc {
 
+struct WppSync;
+
 // Motion of one 4x4 block (also the TMVP store of a reference picture, at 16x16 granularity).
 struct MvField {
   i16 mv[2][2] = {{0, 0}, {0, 0}};
@@ -169,6 +171,7 @@ class Decoder {
   // tile of the slice is parsed as a unit of its own (tiles share no CABAC state or prediction)
   std::vector<std::vector<size_t>> slice_subs_;
   u64 parallel_units_ = 0;
+  std::unique_ptr<WppSync> wpp_sync_;  // wavefront rows in parallel (hevc_ctu.h)
   std::vector<std::unique_ptr<struct SliceShard>> shards_;
 };
 

@@ -69,3 +69,24 @@ def test_parallel_tiles_of_one_slice_bit_exact(native, monkeypatch, kw):
     assert st_par == st_seq
     tiles = kw["tile_cols"] * kw["tile_rows"]
     assert units[0] >= tiles * len(aus) // 2  # the pictures ran tile by tile
+
+
+@pytest.mark.parametrize("kw", [dict(wpp=True), dict(wpp=True, slices=3, coverage=True, seed=9),
+                                dict(wpp=True, bit_depth=10, bframes=1)],
+                         ids=["wpp-1-slice", "wpp-3-slices-coverage", "wpp-main10"])
+def test_parallel_wavefront_rows_bit_exact(native, monkeypatch, kw):
+    """WPP: each CTB row (a substream at its entry point) is a unit of its own; a row waits for
+    the CTBs above-left / above / above-right of each CTB it parses and takes its contexts from
+    the row above's storage after that row's 2nd CTB (the two-CTB lag)."""
+    w, h = (352, 288) if kw.get("coverage") else (640, 360)
+    aus, rec = _stream(native, w, h, 8, **kw)
+    units = []
+    par, st_par = _decode(native, aus, monkeypatch, True, units)
+    seq, st_seq = _decode(native, aus, monkeypatch, False)
+    assert set(par) == set(seq) == set(rec)
+    for pts in rec:
+        for a, b, r in zip(par[pts], seq[pts], rec[pts]):
+            assert np.array_equal(a, b) and np.array_equal(a, r[: a.shape[0], : a.shape[1]]), pts
+    assert st_par == st_seq
+    rows = (h + 31) // 32
+    assert units[0] >= rows * len(aus) // 2  # the pictures ran row by row
