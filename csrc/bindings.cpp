@@ -332,6 +332,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("chroma_qp_offset", &avc::AvcHighConfig::chroma_qp_offset)
       .def_readwrite("second_chroma_qp_offset", &avc::AvcHighConfig::second_chroma_qp_offset)
       .def_readwrite("coverage", &avc::AvcHighConfig::coverage)
+      .def_readwrite("interlaced", &avc::AvcHighConfig::interlaced)
       .def_readwrite("objects", &avc::AvcHighConfig::objects)
       .def_readwrite("noise", &avc::AvcHighConfig::noise)
       .def_readwrite("temporal_noise", &avc::AvcHighConfig::temporal_noise)

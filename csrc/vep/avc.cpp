@@ -182,7 +182,9 @@ namespace {
 void check_sps_supported(const Sps& s) {
   if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
     throw UnsupportedStream("only 8-bit 4:2:0 H.264 is supported");
-  if (!s.frame_mbs_only) throw UnsupportedStream("interlaced H.264 (field / MBAFF) is not supported");
+  // Interlaced SPS (frame_mbs_only_flag 0): frame pictures decode as progressive ones (frame
+  // macroblocks, frame POC = min(top, bottom)); field pictures and MBAFF frames are rejected.
+  if (!s.frame_mbs_only && s.mbaff) throw UnsupportedStream("interlaced H.264: MBAFF frames are not supported");
   if (s.transform_bypass) throw UnsupportedStream("lossless (transform bypass) H.264 is not supported");
 }
 
@@ -251,6 +253,8 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
   VEP_CHECK(sh.slice_type <= 9, "bad slice_type");
   sh.pps_id = int(br.ue());
   sh.frame_num = int(br.u(sps.log2_max_frame_num));
+  if (!sps.frame_mbs_only && br.u1())  // field_pic_flag
+    throw UnsupportedStream("interlaced H.264: field pictures (PAFF) are not supported");
   if (sh.idr()) sh.idr_pic_id = int(br.ue());
   if (sps.poc_type == 0) {
     sh.poc_lsb = int(br.u(sps.log2_max_poc_lsb));

@@ -21,7 +21,8 @@
 // Reference parity: this is the libavcodec h264 decoder the reference calls through PyAV
 // (python/read_image.py:87 `p.decode()`, :94 `to_ndarray('bgr24')`; SURVEY.md §2.2 N2 and
 // §2.3 K1), including its output order (frames leave in picture-order-count order). Interlaced
-// coding (field pictures / MBAFF), 4:2:2 / 4:4:4, high bit depth, lossless, data partitioning,
+// streams that code frame pictures decode like progressive ones; field pictures (PAFF) / MBAFF
+// frames, 4:2:2 / 4:4:4, high bit depth, lossless, data partitioning,
 // FMO/ASO, SP/SI slices and CABAC streams with cabac_init_idc 1 or 2 are reported as
 // UnsupportedStream (the VCN backend's job).
 #pragma once
@@ -558,6 +559,8 @@ struct AvcHighConfig {
   int deblock_idc = 0;
   int chroma_qp_offset = 0, second_chroma_qp_offset = 0;
   bool coverage = false;      // randomised decisions: every MB / sub-MB type, mode, transform
+  bool interlaced = false;    // interlaced SPS (frame_mbs_only 0) coding frame pictures, with
+                              // delta_pic_order_cnt_bottom (top field first)
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;
   u64 seed = 1;

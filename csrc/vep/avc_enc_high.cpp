@@ -137,6 +137,7 @@ struct AvcHighEncoder::Impl {
     VEP_CHECK(c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
     W = (c.width + 15) / 16;
     H = (c.height + 15) / 16;
+    if (c.interlaced) H = (H + 1) & ~1;  // (frame height in MB pairs: map units of 2 MB rows)
     wpx = W * 16;
     hpx = H * 16;
     sps.profile_idc = (c.t8x8 || c.scaling) ? 100 : 77;
@@ -148,7 +149,10 @@ struct AvcHighEncoder::Impl {
     const int pyr = c.pyramid && c.bframes >= 2 ? 1 : 0;
     sps.max_num_ref_frames = std::max(c.refs, c.bframes > 0 ? 2 : 1) + pyr;
     sps.width_mbs = W;
-    sps.height_map_units = H;
+    sps.frame_mbs_only = !c.interlaced;
+    sps.mbaff = false;
+    sps.direct_8x8 = true;
+    sps.height_map_units = c.interlaced ? H / 2 : H;
     sps.crop_right = wpx - c.width;
     sps.crop_bottom = hpx - c.height;
     sps.timing_info = true;
@@ -166,6 +170,7 @@ struct AvcHighEncoder::Impl {
       sps.scaling.flat();
     }
     pps.cabac = c.cabac;
+    pps.bottom_field_pic_order = c.interlaced;
     pps.weighted_pred = c.weighted_p;
     pps.weighted_bipred_idc = c.weighted_b;
     pps.chroma_qp_index_offset = c.chroma_qp_offset;
@@ -259,8 +264,10 @@ struct AvcHighEncoder::Impl {
     bw.ue(u32(sh.slice_type));
     bw.ue(0);
     bw.u(sps.log2_max_frame_num, u32(sh.frame_num));
+    if (!sps.frame_mbs_only) bw.u1(0);  // field_pic_flag: frame pictures
     if (sh.idr()) bw.ue(u32(sh.idr_pic_id));
     bw.u(sps.log2_max_poc_lsb, u32(sh.poc_lsb));
+    if (pps.bottom_field_pic_order) bw.se(1);  // delta_pic_order_cnt_bottom: top field first
     const int st = sh.type();
     if (st == h264::kB) bw.u1(sh.direct_spatial);
     if (st != h264::kI) {

@@ -206,31 +206,38 @@ void Owner::remove(int cam) {
   release_data(cam);
 }
 
+Owner::Mapping::~Mapping() {
+  if (!base) return;
+  if (pinned && w) w->unregister_host(base);
+  ::munmap(base, bytes);
+}
+
 void Owner::release_data(int cam) {
   Data& d = data_[size_t(cam)];
-  if (!d.base) return;
-  if (d.pinned && w_) w_->unregister_host(d.base);
-  ::munmap(d.base, d.bytes);
+  if (!d.map) return;
   unlink_own(d.path, d.ino);  // readers that still map it keep their mapping
-  d = Data{};
+  d = Data{};                 // (the pump's in-flight DMA may still hold the mapping)
 }
 
 bool Owner::ensure_data(int cam, size_t slot_cap) {
   CamEntry& e = hdr_->cams[cam];
   Data& d = data_[size_t(cam)];
-  if (d.base && e.slot_cap.load() >= slot_cap) return true;
+  if (d.map && e.slot_cap.load() >= slot_cap) return true;
   release_data(cam);
   const u32 gen = e.data_gen.load() + 1;
   const size_t cap = (slot_cap + 4095) & ~size_t(4095);
   Data nd;
   nd.path = path_ + ".c" + std::to_string(cam) + ".g" + std::to_string(gen);
-  nd.bytes = cap * kSlots;
+  auto m = std::make_shared<Mapping>();
+  m->bytes = cap * kSlots;
   ::unlink(nd.path.c_str());
-  void* p = map_file(nd.path, nd.bytes, true, true);
+  void* p = map_file(nd.path, m->bytes, true, true);
   if (!p) return false;
-  nd.base = static_cast<u8*>(p);
+  m->base = static_cast<u8*>(p);
+  m->w = w_;
   nd.ino = inode_of(nd.path);
-  nd.pinned = w_ && w_->register_host(nd.base, nd.bytes);
+  m->pinned = w_ && w_->register_host(m->base, m->bytes);
+  nd.map = std::move(m);
   d = nd;
   for (auto& s : e.slots) {
     s.version.fetch_add(2);  // (even: no reader may trust an old slot of the previous segment)
@@ -239,7 +246,7 @@ bool Owner::ensure_data(int cam, size_t slot_cap) {
   }
   e.bus_seq.store(0);
   e.slot_cap.store(cap);
-  e.pinned.store(nd.pinned ? 1u : 0u);
+  e.pinned.store(nd.pinned() ? 1u : 0u);
   e.data_gen.store(gen, std::memory_order_release);
   return true;
 }
@@ -262,6 +269,7 @@ void Owner::pump() {
     std::string name;
     std::shared_ptr<FrameRing> ring;
     std::shared_ptr<Camera> keep;
+    std::shared_ptr<Mapping> map;  // the segment the DMA writes into (kept mapped until it is done)
   };
   std::vector<Job> jobs;
   std::vector<Worker::ReadReq> reqs;
@@ -302,15 +310,15 @@ void Owner::pump() {
         const u64 cap = e.slot_cap.load();
         const int slot = e.bus_seq.load() == 0 ? 0 : int((e.newest.load() + 1) % kSlots);
         e.slots[slot].version.fetch_add(1, std::memory_order_acq_rel);  // odd: being written
-        u8* dst = data_[i].base + size_t(slot) * cap;
+        u8* dst = data_[i].base() + size_t(slot) * cap;
         std::memcpy(dst, pre.data(), pre.size());
-        jobs.push_back({int(i), slot, pre.size(), names_[i], ring, c});
+        jobs.push_back({int(i), slot, pre.size(), names_[i], ring, c, data_[i].map});
         Worker::ReadReq r;
         r.ring = ring.get();
         r.after = e.bus_seq.load();
         r.dst = dst + pre.size();
         r.cap = n;
-        r.pinned = data_[i].pinned;
+        r.pinned = data_[i].pinned();
         reqs.push_back(r);
       }
     }
@@ -328,10 +336,11 @@ void Owner::pump() {
       const Job& j = jobs[k];
       CamEntry& e = hdr_->cams[j.cam];
       SlotHdr& s = e.slots[j.slot];
-      if (reqs[k].ok && names_[size_t(j.cam)] == j.name && data_[size_t(j.cam)].base) {
+      // (the same segment as at the start: not replaced by a remove / add / regrow meanwhile)
+      if (reqs[k].ok && names_[size_t(j.cam)] == j.name && data_[size_t(j.cam)].map == j.map) {
         const size_t n = j.ring->slot_bytes();
         const std::string suf = encode_video_frame(reqs[k].meta, n, j.name).second;
-        u8* dst = data_[size_t(j.cam)].base + size_t(j.slot) * e.slot_cap.load();
+        u8* dst = j.map->base + size_t(j.slot) * e.slot_cap.load();
         std::memcpy(dst + j.pre + n, suf.data(), suf.size());
         s.len.store(j.pre + n + suf.size(), std::memory_order_relaxed);
         s.seq.store(reqs[k].meta.seq, std::memory_order_relaxed);

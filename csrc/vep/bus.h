@@ -103,12 +103,22 @@ class Owner {
   u64 dma_bytes() const { return dma_bytes_.load(); }
 
  private:
-  struct Data {  // one camera's data segment
-    std::string path;
+  // One camera's data segment. Reference-counted: the pump holds a reference while its DMA
+  // writes into the segment, so a camera removed / re-added meanwhile (remove(), add()) only
+  // unlinks the file; the mapping (and its page-locking) goes when the last holder drops it.
+  struct Mapping {
+    Worker* w = nullptr;
     u8* base = nullptr;
     size_t bytes = 0;
     bool pinned = false;
+    ~Mapping();
+  };
+  struct Data {
+    std::string path;
+    std::shared_ptr<Mapping> map;
     u64 ino = 0;
+    u8* base() const { return map ? map->base : nullptr; }
+    bool pinned() const { return map && map->pinned; }
   };
   void pump();
   void on_publish(int cam, i64 seq);

@@ -1,5 +1,6 @@
 // H.264 parameter-set / slice-header parsing and writing (ITU-T H.264 §7.3.2.1, §7.3.2.2, §7.3.3).
 #include "h264.h"
+#include "codec.h"
 
 #include <algorithm>
 
@@ -265,9 +266,7 @@ SliceHeader parse_slice_header(BitReader& br, u8 nal_hdr, const Sps& sps, const 
   sh.slice_type = br.ue();
   sh.pps_id = br.ue();
   sh.frame_num = br.u(sps.log2_max_frame_num);
-  if (!sps.frame_mbs_only) {
-    VEP_CHECK(br.u1() == 0, "field pictures are not supported");
-  }
+  if (!sps.frame_mbs_only && br.u1()) throw UnsupportedStream("interlaced H.264: field pictures (PAFF) are not supported");
   if (sh.idr()) sh.idr_pic_id = br.ue();
   if (sps.poc_type == 0) {
     sh.poc_lsb = br.u(sps.log2_max_poc_lsb);
@@ -391,15 +390,17 @@ std::vector<u8> write_sps(const Sps& s) {
   bw.u1(0);
   bw.ue(s.width_mbs - 1);
   bw.ue(s.height_map_units - 1);
-  bw.u1(1);  // frame_mbs_only
-  bw.u1(1);  // direct_8x8_inference
+  bw.u1(s.frame_mbs_only);
+  if (!s.frame_mbs_only) bw.u1(s.mbaff);  // mb_adaptive_frame_field_flag
+  bw.u1(s.direct_8x8 || !s.frame_mbs_only);  // direct_8x8_inference (1 for interlaced streams)
   bool crop = s.crop_left || s.crop_right || s.crop_top || s.crop_bottom;
   bw.u1(crop);
   if (crop) {
     bw.ue(s.crop_left / 2);
     bw.ue(s.crop_right / 2);
-    bw.ue(s.crop_top / 2);
-    bw.ue(s.crop_bottom / 2);
+    bw.ue(s.crop_top / (s.frame_mbs_only ? 2 : 4));
+    VEP_CHECK(s.frame_mbs_only || s.crop_bottom % 4 == 0, "interlaced crop must be a multiple of 4 rows");
+    bw.ue(s.crop_bottom / (s.frame_mbs_only ? 2 : 4));  // (CropUnitY)
   }
   bw.u1(1);  // vui
   bw.u1(0);  // aspect ratio
@@ -442,7 +443,7 @@ std::vector<u8> write_pps(const Pps& p) {
   bw.ue(p.pps_id);
   bw.ue(p.sps_id);
   bw.u1(p.cabac);
-  bw.u1(0);
+  bw.u1(p.bottom_field_pic_order);  // bottom_field_pic_order_in_frame_present_flag
   bw.ue(0);
   bw.ue(p.num_ref_idx_l0_default - 1);
   bw.ue(p.num_ref_idx_l1_default - 1);

@@ -98,7 +98,7 @@ def _sps_interlaced():
     u(1, 0)         # gaps
     ue(3), ue(1)    # 4 MBs wide, 2 map units (64x64 frame)
     u(1, 0)         # frame_mbs_only_flag = 0 -> interlaced
-    u(1, 0)         # mb_adaptive_frame_field_flag
+    u(1, 1)         # mb_adaptive_frame_field_flag = 1 -> MBAFF frames
     u(1, 1)         # direct_8x8_inference
     u(1, 0), u(1, 0)  # no crop, no VUI
     u(1, 1)
@@ -108,7 +108,9 @@ def _sps_interlaced():
 
 
 def test_unsupported_stream_is_reported(native):
-    # interlaced coding is outside the native decoder: it must refuse loudly (VCN backend's job)
+    # MBAFF (interlaced frames with field / frame MB pairs) is outside the native decoder: it must
+    # refuse loudly (VCN backend's job). (Interlaced streams of frame pictures decode:
+    # tests/test_avc_interlaced.py.)
     enc = synth(native, 64, 48)
     au = enc.next()
     nals = au.nals()

@@ -19,6 +19,9 @@ GPU_CONFIGS = {
                                                        weighted_p=True, weighted_b=1, deblock_idc=2,
                                                        chroma_qp_offset=-2, second_chroma_qp_offset=3)),
     "high-1080p-ibbp": (1920, 1080, 8, dict(bframes=2, qp=26, temporal_noise=2.0)),
+    # interlaced SPS coding frame pictures (1080i-style: 1088 coded rows in map units of 2 MB rows)
+    "interlaced-frames-cov": (176, 144, 12, dict(bframes=2, coverage=True, interlaced=True)),
+    "interlaced-1080-ibbp": (1920, 1080, 6, dict(bframes=2, qp=26, interlaced=True)),
 }
 
 

@@ -69,6 +69,7 @@ def main() -> int:
     ap.add_argument("--fps", type=int, default=30)
     ap.add_argument("--gop", type=int, default=30)
     ap.add_argument("--codec", choices=["h264", "h265"], default="h264")
+    ap.add_argument("--slices", type=int, default=1, help="slices per picture (H.265 4K: 8, parsed in parallel)")
     ap.add_argument("--clients", default="32,128")
     ap.add_argument("--frontends", default="0,1,4", help="serving processes per trial (0 = in-process server)")
     ap.add_argument("--client-threads", type=int, default=8, help="client threads per client process")
@@ -107,6 +108,7 @@ def main() -> int:
         c.compressed = True
         c.qp, c.noise, c.temporal_noise, c.profile, c.bframes = 25, 8.0, 1.5, "high", 2
         c.idr_phase = (i * a.gop) // a.cams
+        c.slices = a.slices
         srv.add_stream(f"/cam{i}", c, realtime=True, cached_frames=a.gop)
     srv.start()
     owner = vep.BusOwner(tag, 0, a.cams)
@@ -128,7 +130,7 @@ def main() -> int:
         time.sleep(0.1)
     names = [f"cam{i}" for i in range(a.cams)]
     out = []
-    base = {"cams": a.cams, "resolution": f"{a.width}x{a.height}", "codec": a.codec, "fps": a.fps,
+    base = {"cams": a.cams, "resolution": f"{a.width}x{a.height}", "codec": a.codec, "fps": a.fps, "slices": a.slices,
             "backend": "gfx950" if use_gpu else "cpu", "frame_bytes": a.width * a.height * 3,
             "cpus": psutil.cpu_count(), "client_threads_per_process": t}
     try:
