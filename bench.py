@@ -75,6 +75,9 @@ def parse_args():
     ap.add_argument("--slices", type=int, default=0,
                     help="slices per picture of the synthetic streams (0: 8 for 4K H.265 — config 5 — else 1); "
                          "the independent slices of an H.265 picture are parsed in parallel")
+    ap.add_argument("--interlaced", type=int, choices=[0, 1, 2], default=0,
+                    help="h264 main/high: 1 = interlaced SPS coding frame pictures, 2 = every frame a field "
+                         "pair (PAFF: CAVLC I/P fields, 4x4 transforms, no B pictures); fps counts frames")
     ap.add_argument("--bit-depth", type=int, choices=[8, 10], default=8,
                     help="h265: 10 = Main10 streams (u16 surfaces on the GPU, narrowed to 8 bits for BGR24)")
     ap.add_argument("--threads", type=int, default=0,
@@ -198,6 +201,8 @@ def describe_streams(a, compressed):
                 f"deblocking, {a.slices} slice{'s' if a.slices > 1 else ''} per picture")
     if compressed and a.profile == "baseline":
         return "Baseline CAVLC I/P"
+    if compressed and a.interlaced == 2:
+        return f"{a.profile.capitalize()} profile interlaced, every frame a field pair (PAFF), CAVLC I/P fields"
     if compressed:
         return (f"{a.profile.capitalize()} profile {'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
                 f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"
@@ -216,6 +221,8 @@ def make_cfg(vep, a, rank, compressed):
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
         cfg.profile, cfg.bframes, cfg.cabac = a.profile, a.bframes, not a.cavlc
+        if a.codec == "h264" and a.profile != "baseline":
+            cfg.interlaced = a.interlaced
     return cfg
 
 

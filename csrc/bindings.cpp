@@ -102,7 +102,16 @@ struct CpuDecoder {
   bool general = false;
   int target = 0;
   int coded = 0;
-  const HostSurface& out() const { return general ? slots[size_t(target)] : surf; }
+  bool fields_out = false;  // the newest output is a field pair (woven into `woven`)
+  HostSurface woven;
+  mutable HostSurface weave_tmp;
+  const HostSurface& out() const { return general ? (fields_out ? woven : slots[size_t(target)]) : surf; }
+  // samples of an output frame (a field pair: its two field slots woven)
+  const HostSurface& frame_of(const avc::OutFrame& f) const {
+    if (!f.fields) return slots[size_t(f.slot)];
+    avc::weave_fields(slots[2 * size_t(f.slot)], slots[2 * size_t(f.slot) + 1], weave_tmp);
+    return weave_tmp;
+  }
   py::object decode(const AccessUnit& au) {
     bool no_output = false;
     {
@@ -122,8 +131,11 @@ struct CpuDecoder {
           general = true;
         }
       }
-      if (!done) {
-        avc::PicturePtr pic = avc.parse(au);
+      std::vector<avc::OutFrame> outs;
+      size_t nal = 0;  // (a field pair may come as one access unit: one picture per field)
+      while (!done) {
+        avc::PicturePtr pic = avc.parse(au, 0, &nal);
+        done = nal >= au.nals.size();
         if (slots.size() < size_t(pic->dpb_slots)) slots.resize(size_t(pic->dpb_slots));
         for (auto& h : slots)
           if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16) h.alloc(pic->wmbs * 16, pic->hmbs * 16);
@@ -144,14 +156,18 @@ struct CpuDecoder {
             list1_only += l1only;
           }
         }
+        outs.insert(outs.end(), pic->outputs.begin(), pic->outputs.end());
+        if (!done) continue;
         // B-frame reordering: the newest frame that left the reorder buffer, if any
-        pending_outputs = pic->outputs;
-        no_output = pic->outputs.empty();
+        pending_outputs = outs;
+        no_output = outs.empty();
         if (!no_output) {
-          last = pic->outputs.back().info;
-          target = pic->outputs.back().slot;
-          last_poc = pic->outputs.back().poc;
-          last_pts = pic->outputs.back().au.pts;
+          last = outs.back().info;
+          target = outs.back().slot;
+          fields_out = outs.back().fields;
+          if (fields_out) woven = frame_of(outs.back());
+          last_poc = outs.back().poc;
+          last_pts = outs.back().au.pts;
         }
       }
     }
@@ -165,7 +181,7 @@ struct CpuDecoder {
   py::list frames_of(const std::vector<avc::OutFrame>& fs) const {
     py::list l;
     for (const auto& f : fs) {
-      const HostSurface& s = slots[size_t(f.slot)];
+      const HostSurface& s = frame_of(f);
       py::array_t<uint8_t> y({s.coded_h, s.coded_w});
       py::array_t<uint8_t> uv({s.coded_h / 2, s.coded_w});
       std::memcpy(y.mutable_data(), s.y.data(), s.y.size());
@@ -179,7 +195,7 @@ struct CpuDecoder {
     py::list out_list;
     for (const auto& f : avc.flush_output()) {
       py::array_t<uint8_t> o({f.info.height, f.info.width, 3});
-      cpu_nv12_to_bgr(slots[size_t(f.slot)], f.info.crop_left, f.info.crop_top, f.info.width, f.info.height,
+      cpu_nv12_to_bgr(frame_of(f), f.info.crop_left, f.info.crop_top, f.info.width, f.info.height,
                       o.mutable_data());
       out_list.append(o);
     }
@@ -245,6 +261,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("long_term", &SynthConfig::long_term)
       .def_readwrite("lossless", &SynthConfig::lossless)
       .def_readwrite("bit_depth", &SynthConfig::bit_depth)
+      .def_readwrite("interlaced", &SynthConfig::interlaced)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -333,6 +350,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("second_chroma_qp_offset", &avc::AvcHighConfig::second_chroma_qp_offset)
       .def_readwrite("coverage", &avc::AvcHighConfig::coverage)
       .def_readwrite("interlaced", &avc::AvcHighConfig::interlaced)
+      .def_readwrite("fields", &avc::AvcHighConfig::fields)
       .def_readwrite("objects", &avc::AvcHighConfig::objects)
       .def_readwrite("noise", &avc::AvcHighConfig::noise)
       .def_readwrite("temporal_noise", &avc::AvcHighConfig::temporal_noise)
@@ -556,6 +574,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("outputs_last", [](const CpuDecoder& d) { return int(d.pending_outputs.size()); })
       .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
       .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.coded; })
+      .def_property_readonly("pictures_decoded", [](const CpuDecoder& d) { return d.pictures.size(); })
       .def_property_readonly("general", [](const CpuDecoder& d) { return d.general; })
       .def_property_readonly("parallel_slices", [](const CpuDecoder& d) { return d.avc.parallel_slices_run(); })
       .def("surface", [](const CpuDecoder& d) {

@@ -183,7 +183,8 @@ void check_sps_supported(const Sps& s) {
   if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
     throw UnsupportedStream("only 8-bit 4:2:0 H.264 is supported");
   // Interlaced SPS (frame_mbs_only_flag 0): frame pictures decode as progressive ones (frame
-  // macroblocks, frame POC = min(top, bottom)); field pictures and MBAFF frames are rejected.
+  // macroblocks, frame POC = min(top, bottom)); field pictures as half-height pictures in field
+  // slots (CAVLC I / P, see Decoder::parse); MBAFF frames are rejected.
   if (!s.frame_mbs_only && s.mbaff) throw UnsupportedStream("interlaced H.264: MBAFF frames are not supported");
   if (s.transform_bypass) throw UnsupportedStream("lossless (transform bypass) H.264 is not supported");
 }
@@ -253,15 +254,14 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
   VEP_CHECK(sh.slice_type <= 9, "bad slice_type");
   sh.pps_id = int(br.ue());
   sh.frame_num = int(br.u(sps.log2_max_frame_num));
-  if (!sps.frame_mbs_only && br.u1())  // field_pic_flag
-    throw UnsupportedStream("interlaced H.264: field pictures (PAFF) are not supported");
+  if (!sps.frame_mbs_only && (sh.field_pic = br.u1())) sh.bottom_field = br.u1();
   if (sh.idr()) sh.idr_pic_id = int(br.ue());
   if (sps.poc_type == 0) {
     sh.poc_lsb = int(br.u(sps.log2_max_poc_lsb));
-    if (pps.bottom_field_pic_order) sh.delta_poc_bottom = br.se();
+    if (pps.bottom_field_pic_order && !sh.field_pic) sh.delta_poc_bottom = br.se();
   } else if (sps.poc_type == 1 && !sps.delta_pic_order_always_zero) {
     sh.delta_poc[0] = br.se();
-    if (pps.bottom_field_pic_order) sh.delta_poc[1] = br.se();
+    if (pps.bottom_field_pic_order && !sh.field_pic) sh.delta_poc[1] = br.se();
   }
   if (pps.redundant_pic_cnt_present) {
     if (br.ue() != 0) throw UnsupportedStream("redundant H.264 pictures are not supported");
@@ -343,12 +343,24 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
                 "deblocking offsets out of range");
     }
   }
+  if (sh.field_pic) {
+    // Field pictures: CAVLC I / P with 4x4 transforms and sliding-window marking. CABAC needs the
+    // field-coded context initialisation values (not in any source this build can pin), the 8x8
+    // transform the 8x8 field scan, B fields the field direct modes, and MMCOs / list
+    // modifications the field picture numbers: those stay with the VCN backend.
+    if (pps.cabac) throw UnsupportedStream("interlaced H.264: CABAC field pictures are not supported");
+    if (st == h264::kB) throw UnsupportedStream("interlaced H.264: B field pictures are not supported");
+    if (pps.transform_8x8_mode) throw UnsupportedStream("interlaced H.264: 8x8 transform in field pictures is not supported");
+    if (sh.adaptive_marking || sh.long_term_reference || !sh.ref_mods[0].empty())
+      throw UnsupportedStream("interlaced H.264: field MMCOs / long-term / list modifications are not supported");
+  }
   return sh;
 }
 
 // ------------------------------------------------------------------------- DPB
 
 void Decoder::reset_references() {
+  pair_ = OpenPair{};
   dpb_.clear();
   pending_.clear();
   have_idr_ = false;
@@ -358,7 +370,7 @@ void Decoder::reset_references() {
 
 int Decoder::pick_slot() const {
   for (int s = 0; s < dpb_slots_; ++s) {
-    bool used = s == pinned_slot_;
+    bool used = s == pinned_slot_ || (pair_.open && s == pair_.slot);
     for (const auto& r : dpb_) used |= r.slot == s;
     for (const auto& p : pending_) used |= p.f.slot == s;
     if (!used) return s;
@@ -375,7 +387,7 @@ int Decoder::compute_poc(const SliceHdr& sh, const Sps& sps) {
     int msb = prev_poc_msb_;
     if (sh.poc_lsb < prev_poc_lsb_ && prev_poc_lsb_ - sh.poc_lsb >= max_lsb / 2) msb = prev_poc_msb_ + max_lsb;
     else if (sh.poc_lsb > prev_poc_lsb_ && sh.poc_lsb - prev_poc_lsb_ > max_lsb / 2) msb = prev_poc_msb_ - max_lsb;
-    const int top = msb + sh.poc_lsb, bot = top + sh.delta_poc_bottom;
+    const int top = msb + sh.poc_lsb, bot = sh.field_pic ? top : top + sh.delta_poc_bottom;
     if (sh.nal_ref_idc != 0) {
       if (sh.has_mmco5()) {
         prev_poc_msb_ = 0;
@@ -408,7 +420,8 @@ int Decoder::compute_poc(const SliceHdr& sh, const Sps& sps) {
     if (sh.nal_ref_idc == 0) expected += sps.offset_for_non_ref_pic;
     const int top = expected + sh.delta_poc[0];
     const int bot = top + sps.offset_for_top_to_bottom_field + sh.delta_poc[1];
-    poc = std::min(top, bot);
+    // a field picture: its own field's count (bottom: expected + offset + delta_pic_order_cnt[0])
+    poc = !sh.field_pic ? std::min(top, bot) : sh.bottom_field ? top + sps.offset_for_top_to_bottom_field : top;
   } else {
     poc = sh.idr() ? 0 : (sh.nal_ref_idc == 0 ? 2 * (fno + sh.frame_num) - 1 : 2 * (fno + sh.frame_num));
   }
@@ -577,6 +590,88 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int 
   }
 }
 
+// §8.2.4.2.2 / §8.2.4.2.5: list 0 of a P field. The reference frames (short-term by
+// FrameNumWrap descending, then long-term by index) are taken apart into their fields, alternating
+// parities starting with the current field's; when one parity runs out the other's remaining
+// fields follow in order. The first field of the current frame is a reference frame entry too.
+void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps) {
+  const int max_fn = 1 << sps.log2_max_frame_num;
+  list_[0].clear();
+  list_[1].clear();
+  if (sh.type() == h264::kI) return;
+  std::vector<RefPic*> st, lt;
+  for (auto& r : dpb_) {
+    if (r.long_term) {
+      lt.push_back(&r);
+    } else {
+      r.frame_num_wrap = r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num;
+      st.push_back(&r);
+    }
+  }
+  std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
+  std::sort(lt.begin(), lt.end(), [](RefPic* a, RefPic* b) { return a->lt_idx < b->lt_idx; });
+  const int same = sh.bottom_field ? 1 : 0;
+  std::vector<ListEntry> all;
+  auto alternate = [&](const std::vector<RefPic*>& frames) {
+    std::vector<ListEntry> f[2];  // [0] same parity, [1] opposite
+    for (RefPic* r : frames)
+      for (int k = 0; k < 2; ++k) {
+        const int par = k == 0 ? same : 1 - same;
+        if ((r->fields >> par) & 1)
+          f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], r->long_term, r->uid_f[par], nullptr});
+      }
+    size_t i[2] = {0, 0};
+    for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
+      const int from = i[k] < f[k].size() ? k : k ^ 1;
+      all.push_back(f[from][i[from]++]);
+    }
+  };
+  alternate(st);
+  alternate(lt);
+  list_[0].assign(size_t(sh.num_ref_idx[0]), ListEntry{});
+  for (size_t i = 0; i < list_[0].size() && i < all.size(); ++i) list_[0][i] = all[i];
+}
+
+// Reference marking of a field (sliding window only, see read_slice_header): the first field of a
+// frame enters the DPB as a frame entry holding one field (after the sliding window makes room);
+// the second field joins its frame's entry.
+void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, u32 uid, bool second) {
+  const int par = sh.bottom_field ? 1 : 0;
+  if (second)
+    for (auto& r : dpb_)
+      if (r.slot == slot && !r.long_term && r.frame_num == sh.frame_num) {
+        r.fields |= u8(1 << par);
+        r.poc_f[par] = poc;
+        r.uid_f[par] = uid;
+        r.poc = std::min(r.poc, poc);
+        return;
+      }
+  const int max_fn = 1 << sps.log2_max_frame_num;
+  const int max_refs = std::max(1, sps.max_num_ref_frames);
+  if (sh.idr()) {
+    dpb_.clear();
+    max_lt_idx_ = -1;
+  } else {
+    auto wrap = [&](const RefPic& r) { return r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num; };
+    while (int(dpb_.size()) >= max_refs) {  // sliding window (frames)
+      auto it = std::min_element(dpb_.begin(), dpb_.end(), [&](const RefPic& a, const RefPic& b) {
+        if (a.long_term != b.long_term) return !a.long_term;
+        return wrap(a) < wrap(b);
+      });
+      dpb_.erase(it);
+    }
+  }
+  RefPic cur;
+  cur.slot = slot;
+  cur.frame_num = sh.frame_num;
+  cur.poc = poc;
+  cur.uid = uid;
+  cur.fields = u8(1 << par);
+  cur.poc_f[par] = poc;
+  cur.uid_f[par] = uid;
+  dpb_.push_back(cur);
+}
+
 int Decoder::reorder_depth(const Sps& sps) const {
   if (sps.max_num_reorder_frames >= 0) return sps.max_num_reorder_frames;
   if (sps.poc_type == 2 || sps.profile_idc == 66) return 0;  // output order = decoding order
@@ -594,7 +689,26 @@ int Decoder::reorder_depth(const Sps& sps) const {
 // steady state, so a stream with B pictures outputs one frame per access unit across GOPs
 // instead of a burst at every IDR. `hard` (new picture geometry, or no reordering) outputs every
 // waiting picture at once.
-void Decoder::bump(Picture& pic, bool new_epoch, bool hard) {
+OutFrame Decoder::out_of(const Picture& pic) const {
+  OutFrame f;
+  f.slot = pic.target;
+  f.info = pic.info;
+  f.au = pic.au;
+  f.poc = pic.poc;
+  return f;
+}
+
+// The open field pair's frame leaves for the reorder buffer (its second field was decoded, or
+// never came: then the missing field's rows are whatever the slot held).
+void Decoder::close_pair(Picture& pic) {
+  if (!pair_.open) return;
+  pair_.open = false;
+  OutFrame f = pair_.f;
+  f.poc = pair_.have == 3 ? std::min(pair_.poc[0], pair_.poc[1]) : pair_.poc[(pair_.have >> 1) & 1];
+  bump(pic, f, pair_.boundary, pair_.hard);
+}
+
+void Decoder::bump(Picture& pic, const OutFrame& f, bool new_epoch, bool hard) {
   auto before = [](const Pending& a, const Pending& b) {
     return a.epoch != b.epoch ? a.epoch < b.epoch : a.f.poc < b.f.poc;
   };
@@ -608,11 +722,6 @@ void Decoder::bump(Picture& pic, bool new_epoch, bool hard) {
   if (new_epoch) ++epoch_;
   if (hard)
     while (!pending_.empty()) take_min();
-  OutFrame f;
-  f.slot = pic.target;
-  f.info = pic.info;
-  f.au = pic.au;
-  f.poc = pic.poc;
   if (last_out_epoch_ == i64(epoch_) && f.poc < last_out_poc_) {
     if (adaptive_reorder_ < 16) ++adaptive_reorder_;  // late: dropped from output
   } else {
@@ -624,6 +733,7 @@ void Decoder::bump(Picture& pic, bool new_epoch, bool hard) {
 
 std::vector<OutFrame> Decoder::flush_output() {
   Picture tmp;
+  close_pair(tmp);  // (a lone first field: output as it is)
   while (!pending_.empty()) {
     auto it = std::min_element(pending_.begin(), pending_.end(), [](const Pending& a, const Pending& b) {
       return a.epoch != b.epoch ? a.epoch < b.epoch : a.f.poc < b.f.poc;
@@ -1011,7 +1121,7 @@ namespace {
 // The fast CAVLC MbDecoder above covers a slice when nothing beyond Baseline-style syntax is in
 // use (the default synthetic camera streams); everything else goes to decode_slice_generic.
 bool legacy_slice(const SliceHdr& sh, const Sps& sps, const Pps& pps) {
-  return !pps.cabac && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
+  return !pps.cabac && !sh.field_pic && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
          !sps.scaling_matrix_present && !pps.scaling_matrix_present && !sh.explicit_wp &&
          pps.chroma_qp_index_offset == pps.second_chroma_qp_index_offset;
 }
@@ -1045,7 +1155,7 @@ struct Decoder::SliceUnit {
   std::array<std::vector<u32>, 2> uids;
 };
 
-PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
+PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
   auto pic = pic_pool_->acquire([](Picture& p) {  // default state, pool capacities kept
     auto mbs = std::move(p.mbs);
     auto coefs = std::move(p.coefs), mvs = std::move(p.mvs);
@@ -1064,6 +1174,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   });
   bool got = false;
   bool hard_flush = false;  // IDR with a new picture geometry: waiting pictures leave at once
+  bool second_field = false;  // this picture completes the open field pair
   int slice_idx = 0;
   SliceHdr first;
   const Sps* act_sps = nullptr;
@@ -1084,7 +1195,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
     }
   const bool par = parallel_slices_ && nslices >= 2 && FanOut::shared().size() > 0;
   int nunits = 0;
-  for (size_t i = 0; i < au.nals.size(); ++i) {
+  const size_t start = next_nal ? *next_nal : 0;
+  if (next_nal) *next_nal = au.nals.size();
+  for (size_t i = start; i < au.nals.size(); ++i) {
     const u8* p = au.nal(i);
     const size_t n = au.nal_size(i);
     if (n < 2) continue;
@@ -1128,8 +1241,12 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       const int slots = dpb_slots_for(sps);
       VEP_CHECK(slots <= kMaxDpbSlots, "max_num_ref_frames out of range");
       const int W = sps.width_mbs, H = sps.height_mbs();
-      if (sh.idr()) {
-        hard_flush = slots != dpb_slots_ || W != wmbs_ || H != hmbs_;
+      second_field = sh.field_pic && pair_.open && pair_.bottom != int(sh.bottom_field) &&
+                     pair_.frame_num == sh.frame_num;
+      if (!second_field) close_pair(*pic);  // an unpaired field leaves before this picture
+      if (sh.idr() && !second_field) {
+        hard_flush = slots != dpb_slots_ || W != wmbs_ || H != hmbs_ || sh.field_pic != field_mode_;
+        field_mode_ = sh.field_pic;
         have_idr_ = true;
         dpb_slots_ = slots;
         wmbs_ = W;
@@ -1140,22 +1257,27 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
         // a non-IDR picture may not change the picture size or the DPB (a mid-GOP SPS that
         // does would make earlier pictures of a batch write outside the surfaces)
         VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_, "SPS changed without an IDR picture");
+        if (sh.field_pic != field_mode_)
+          throw UnsupportedStream("interlaced H.264: frame and field pictures mixed in one IDR period are not supported");
       }
-      if (sh.idr()) {
+      if (sh.idr() && !second_field) {
         // IDR: the DPB is emptied; pictures waiting for output stay (they leave before the
         // IDR's, bump(); no_output_of_prior_pics is not honoured: a viewer wants every frame)
         dpb_.clear();
         max_lt_idx_ = -1;
       }
       pic->poc = compute_poc(sh, sps);
+      const int Hp = sh.field_pic ? H / 2 : H;  // (a field: half the frame's MB rows)
       pic->wmbs = W;
-      pic->hmbs = H;
+      pic->hmbs = Hp;
       // every record is written by store_mb or by the concealment pass below: a recycled
       // picture of the same size needs no clearing
-      if (pic->mbs.size() != size_t(W) * H) pic->mbs.assign(size_t(W) * H, MbRec{});
-      pic->coefs.reserve(size_t(W) * H * 32);
-      pic->mvs.reserve(size_t(W) * H * 16);
-      pic->dpb_slots = dpb_slots_;
+      if (pic->mbs.size() != size_t(W) * Hp) pic->mbs.assign(size_t(W) * Hp, MbRec{});
+      pic->coefs.reserve(size_t(W) * Hp * 32);
+      pic->mvs.reserve(size_t(W) * Hp * 16);
+      pic->dpb_slots = field_mode_ ? 2 * dpb_slots_ : dpb_slots_;
+      pic->structure = sh.field_pic ? 1 + int(sh.bottom_field) : 0;
+      pic->second_field = second_field;
       pic->constrained_intra = pps.constrained_intra_pred;
       pic->idr = sh.idr();
       PictureInfo& pi = pic->info;
@@ -1175,9 +1297,30 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       pic->au.keyframe = au.keyframe;
       pic->au.corrupt = au.corrupt;
       pic->au.tag = tag;
-      nb_.reset(W, H);
-      pic->target = pick_slot();  // (pictures waiting for output keep their slots until bump)
-      if (sh.nal_ref_idc != 0 && sps.profile_idc != 66) {  // B slices may use this motion
+      nb_.reset(W, Hp);
+      if (sh.field_pic) {  // field slot 2 * frame slot + parity
+        const int fs = second_field ? pair_.slot : pick_slot();
+        pic->target = 2 * fs + int(sh.bottom_field);
+        if (!second_field) {
+          pair_ = OpenPair{};
+          pair_.open = true;
+          pair_.slot = fs;
+          pair_.frame_num = sh.frame_num;
+          pair_.bottom = int(sh.bottom_field);
+          pair_.ref = sh.nal_ref_idc != 0;
+          pair_.boundary = sh.idr();
+          pair_.hard = sh.idr() && (hard_flush || reorder_cur_ == 0);
+          pair_.f.slot = fs;
+          pair_.f.info = pic->info;
+          pair_.f.au = pic->au;
+          pair_.f.fields = true;
+        }
+        pair_.have |= u8(1 << int(sh.bottom_field));
+        pair_.poc[int(sh.bottom_field)] = pic->poc;
+      } else {
+        pic->target = pick_slot();  // (pictures waiting for output keep their slots until bump)
+      }
+      if (sh.nal_ref_idc != 0 && sps.profile_idc != 66 && !sh.field_pic) {  // B slices may use this motion
         col_built = col_pool_->acquire([](ColMotion&) {});  // (every entry is written below)
         col_built->wmbs = W;
         col_built->hmbs = H;
@@ -1189,9 +1332,16 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
       got = true;
     } else {
       VEP_CHECK(&sps == act_sps, "slices of one picture reference different SPSs");
+      if (sh.field_pic != first.field_pic || sh.bottom_field != first.bottom_field) {
+        // the next picture of the access unit (the pair's other field): the caller parses it next
+        VEP_CHECK(next_nal != nullptr, "H.264: one access unit holds several pictures");
+        *next_nal = i;
+        break;
+      }
       if (sh.type() == h264::kB || pic->info.pict_type == 'I') pic->info.pict_type = "PBISi"[sh.type()];
     }
-    build_lists(sh, sps, pic->poc);
+    if (sh.field_pic) build_field_lists(sh, sps);
+    else build_lists(sh, sps, pic->poc);
     std::array<std::vector<u32>, 2> uids;
     for (int l = 0; l < 2; ++l)
       for (const auto& e : list_[l]) uids[size_t(l)].push_back(e.uid);
@@ -1289,7 +1439,12 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
     std::fill(std::begin(m.ref1), std::end(m.ref1), u8(0xFF));
     if (!dpb_.empty()) {
       m.kind = kSkip;
-      for (auto& rf : m.ref) rf = u8(dpb_.front().slot);
+      int cs = dpb_.front().slot;
+      if (pic->structure) {  // a field of that frame, the current parity if it holds one
+        const int par = pic->structure - 1;
+        cs = 2 * cs + (((dpb_.front().fields >> par) & 1) ? par : 1 - par);
+      }
+      for (auto& rf : m.ref) rf = u8(cs);
       m.mv = u32(pic->mvs.size());
       m.flags |= kMbMv16;
       pic->mvs.resize(pic->mvs.size() + 2, 0);
@@ -1303,12 +1458,17 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag) {
   }
   pic->info.coded_mbs = pic->nmbs() - missing;
   const u32 uid = next_uid_++;
-  if (first.nal_ref_idc != 0) {
-    // (B slices possible: the motion for direct prediction, built as the MBs were stored)
-    mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col_built));
+  if (first.field_pic) {
+    if (first.nal_ref_idc != 0) mark_field(first, *act_sps, pic->target >> 1, pic->poc, uid, second_field && pair_.ref);
+    if (second_field) close_pair(*pic);  // the frame is complete
+  } else {
+    if (first.nal_ref_idc != 0) {
+      // (B slices possible: the motion for direct prediction, built as the MBs were stored)
+      mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col_built));
+    }
+    const bool boundary = first.idr() || first.has_mmco5();
+    bump(*pic, out_of(*pic), boundary, boundary && (hard_flush || reorder_cur_ == 0));
   }
-  const bool boundary = first.idr() || first.has_mmco5();
-  bump(*pic, boundary, boundary && (hard_flush || reorder_cur_ == 0));
   // (store_mb validated every record as it was written; concealed ones are built in range)
   if (missing || par) validate(*pic);
   else validate_picture(*pic);
@@ -1362,6 +1522,7 @@ void Decoder::parse_slice_data(MbNeighbours& nb, Picture& pic, const SliceHdr& s
   env.list[1] = &lists[1];
   env.cur_poc = pic.poc;
   env.scaling = h264::resolve_scaling(sps, pps);
+  env.field = sh.field_pic;
   decode_slice_generic(nb, pic, env, data, n, bitpos);
 }
 
@@ -1486,7 +1647,10 @@ std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, in
 }
 
 void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
-                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64]) {
+                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure) {
+  // field pictures: slot parity = field parity; a vector into the opposite-parity field is offset
+  // by a quarter chroma sample vertically (Table 8-10: 2 * (bottom_cur - bottom_ref) eighths)
+  auto cy_off = [&](int slot) { return structure ? 2 * ((structure == 2) - (slot & 1)) : 0; };
   const int pitch = slots[0].coded_w, wpx = pitch, hpx = slots[0].coded_h;
   for (int y = 0; y < 16; ++y)
     for (int x = 0; x < 16; ++x) {
@@ -1507,12 +1671,16 @@ void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const 
         const int r = (y >> 1) * 4 + (x >> 1), b8 = ((y >> 2) << 1) | (x >> 2);
         const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
         int p0 = 0, p1 = 0;
-        if (s0 != 0xFF)
+        if (s0 != 0xFF) {
+          const int vy = mv0[2 * r + 1] + cy_off(s0);
           p0 = chroma_epel(slots[size_t(s0)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
-                           my * 8 + y + (mv0[2 * r + 1] >> 3), mv0[2 * r] & 7, mv0[2 * r + 1] & 7);
-        if (s1 != 0xFF)
+                           my * 8 + y + (vy >> 3), mv0[2 * r] & 7, vy & 7);
+        }
+        if (s1 != 0xFF) {
+          const int vy = mv1[2 * r + 1] + cy_off(s1);
           p1 = chroma_epel(slots[size_t(s1)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
-                           my * 8 + y + (mv1[2 * r + 1] >> 3), mv1[2 * r] & 7, mv1[2 * r + 1] & 7);
+                           my * 8 + y + (vy >> 3), mv1[2 * r] & 7, vy & 7);
+        }
         pc[c][y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c);
       }
 }
@@ -1823,7 +1991,7 @@ struct Recon {
     const i16* mv1 = (m.flags & kMbL1) ? e[1] : nullptr;
     const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
     int py[256], pc[2][64], res[256];
-    predict_inter(slots, m, mv0, mv1, wp, mx, my, py, pc);
+    predict_inter(slots, m, mv0, mv1, wp, mx, my, py, pc, pic.structure);
     luma_residual(dense, m, res);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = u8(clip1(py[y * 16 + x] + res[y * 16 + x]));
@@ -2027,7 +2195,7 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
         for (int k = 0; k < 16; ++k) {
           const int bq = dir == 0 ? (k >> 2) * 4 + e : e * 4 + (k >> 2);
           const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
-          bs[k] = boundary_strength(p, bp, mp, q, bq, mq, e == 0);
+          bs[k] = boundary_strength(p, bp, mp, q, bq, mq, e == 0, pic.structure != 0, dir == 0);
         }
         for (int k = 0; k < 16; ++k) {
           if (!bs[k]) continue;
@@ -2048,6 +2216,16 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
       }
     }
   }
+}
+
+void weave_fields(const HostSurface& top, const HostSurface& bottom, HostSurface& frame) {
+  VEP_CHECK(top.coded_w == bottom.coded_w && top.coded_h == bottom.coded_h && !top.wide(), "weave: field sizes");
+  const int w = top.coded_w, fh = top.coded_h;
+  if (frame.coded_w != w || frame.coded_h != 2 * fh) frame.alloc(w, 2 * fh);
+  for (int r = 0; r < 2 * fh; ++r)
+    std::memcpy(&frame.y[size_t(r) * w], &(r & 1 ? bottom : top).y[size_t(r >> 1) * w], size_t(w));
+  for (int r = 0; r < fh; ++r)
+    std::memcpy(&frame.uv[size_t(r) * w], &(r & 1 ? bottom : top).uv[size_t(r >> 1) * w], size_t(w));
 }
 
 void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots) {

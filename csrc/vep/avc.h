@@ -53,6 +53,9 @@ struct OutFrame {
   PictureInfo info;  // size, crop, picture type
   AuMeta au;
   int poc = 0;
+  // A field pair: the frame slot holds the top field's rows then the bottom field's (field slots
+  // 2 * slot and 2 * slot + 1, each half a frame); the output weaves them.
+  bool fields = false;
 };
 
 struct ColBuild;
@@ -68,6 +71,10 @@ struct Picture {
   hostmem::pinned_vector<WpEntry> wps;   // weighted-prediction entries (4 per weighted MB)
   int target = 0;             // DPB slot this picture is reconstructed into
   int dpb_slots = 1;          // surfaces the camera needs for this stream
+  // 0 frame; 1 / 2 top / bottom field picture. Field pictures address field slots (half a frame
+  // each, parity = slot & 1: frame slot s = field slots 2s, 2s + 1), wmbs x hmbs is the field.
+  int structure = 0;
+  bool second_field = false;  // completes a field pair (frame counters count these, not first fields)
   bool constrained_intra = false;
   int intra_mbs = 0;          // I4x4 / I8x8 / I16x16 MBs (need the wavefront pass)
   int intra_res = 0;          // intra MBs with residual samples (MbRec::res slots)
@@ -98,6 +105,7 @@ void validate(const Picture& p);
 struct SliceHdr {
   int nal_type = 0, nal_ref_idc = 0;
   int first_mb = 0, slice_type = 0, pps_id = 0, frame_num = 0, idr_pic_id = 0;
+  bool field_pic = false, bottom_field = false;
   int poc_lsb = 0, delta_poc_bottom = 0, delta_poc[2] = {0, 0};
   bool direct_spatial = true;
   int num_ref_idx[2] = {1, 1};
@@ -331,6 +339,10 @@ struct RefPic {
   int poc = 0;
   u32 uid = 0;
   std::shared_ptr<const ColMotion> col;
+  // field decoding: reference fields of the frame (bit 0 top, bit 1 bottom), their POCs and uids
+  u8 fields = 3;
+  int poc_f[2] = {0, 0};
+  u32 uid_f[2] = {0, 0};
 };
 
 // Per-slice list entry (a RefPic snapshot).
@@ -348,7 +360,10 @@ class Decoder {
  public:
   // Parse one access unit into a Picture (decode order). Throws UnsupportedStream for syntax
   // outside the supported subset and Error for corrupt data. `tag` is carried to the output.
-  PicturePtr parse(const AccessUnit& au, i64 tag = 0);
+  // `next_nal` (optional): parse from that NAL on and stop before a second picture of the access
+  // unit (both fields of a pair in one access unit, as some packetizers deliver them), returning
+  // where it starts (au.nals.size(): none left). Without it a second picture is an error.
+  PicturePtr parse(const AccessUnit& au, i64 tag = 0, size_t* next_nal = nullptr);
   void absorb_parameter_sets(const AccessUnit& au);
   bool has_sps() const { return !sps_.empty(); }
   // Forget the DPB and the reorder buffer (e.g. after a failed picture): the next picture must
@@ -366,11 +381,14 @@ class Decoder {
     u32 epoch;  // IDR / MMCO5 period the picture belongs to (output order: epoch, then POC)
   };
   void build_lists(const SliceHdr& sh, const h264::Sps& sps, int cur_poc);
+  void build_field_lists(const SliceHdr& sh, const h264::Sps& sps);
+  void mark_field(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid, bool second);
   void mark_references(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid,
                        std::shared_ptr<const ColMotion> col);
   int pick_slot() const;
   int compute_poc(const SliceHdr& sh, const h264::Sps& sps);
-  void bump(Picture& pic, bool new_epoch, bool hard);
+  void bump(Picture& pic, const OutFrame& f, bool new_epoch, bool hard);
+  OutFrame out_of(const Picture& pic) const;
   int reorder_depth(const h264::Sps& sps) const;
   void parse_slice_data(MbNeighbours& nb, Picture& pic, const SliceHdr& sh, const h264::Sps& sps,
                         const h264::Pps& pps, const u8* data, size_t n, size_t bitpos, int slice_idx,
@@ -412,6 +430,19 @@ class Decoder {
   bool parallel_slices_ = true;
   std::vector<std::unique_ptr<SliceUnit>> units_;
   u64 parallel_slices_run_ = 0;
+  // Field pictures (PAFF): decided per IDR period (a stream mixing frame and field pictures in
+  // one period is UnsupportedStream). A field pair shares frame slot `slot`; the frame is output
+  // once its second field is decoded (or, unpaired, when the next frame starts).
+  bool field_mode_ = false;
+  struct OpenPair {
+    bool open = false;
+    int slot = -1, frame_num = 0, bottom = 0;
+    int poc[2] = {0, 0};
+    bool ref = false, boundary = false, hard = false;
+    u8 have = 0;       // fields decoded (bit 0 top, bit 1 bottom)
+    OutFrame f;        // the frame as output (info / au of the first field)
+  } pair_;
+  void close_pair(Picture& pic);  // output the open pair's frame through pic's outputs
 
  public:
   Decoder();
@@ -422,6 +453,8 @@ class Decoder {
 // CPU reference reconstruction of `pic` into DPB surfaces `slots` (coded size; references are
 // read from the slots named by the MbRecs). Bit-exact with the GPU kernels.
 void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots);
+// Field pair -> frame (frame row r = row r >> 1 of field r & 1), 8-bit NV12.
+void weave_fields(const HostSurface& top, const HostSurface& bottom, HostSurface& frame);
 
 // ---- internals shared by the decoder and the encoder -------------------------------------
 // Levels of one MB in scan order (luma per raster block; I16x16 AC at index 1..15 with the DC
@@ -561,6 +594,8 @@ struct AvcHighConfig {
   bool coverage = false;      // randomised decisions: every MB / sub-MB type, mode, transform
   bool interlaced = false;    // interlaced SPS (frame_mbs_only 0) coding frame pictures, with
                               // delta_pic_order_cnt_bottom (top field first)
+  bool fields = false;        // (interlaced) code every frame as a field pair (PAFF): top field
+                              // first, I / P or P / P, CAVLC, 4x4 transforms, no B pictures
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;
   u64 seed = 1;

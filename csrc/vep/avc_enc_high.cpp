@@ -110,6 +110,10 @@ struct AvcHighEncoder::Impl {
     int slot, frame_num, poc;
     u32 uid;
     std::shared_ptr<const ColMotion> col;
+    // field coding: the frame's reference fields (bit 0 top, bit 1 bottom), their POCs / uids
+    u8 fields = 3;
+    int poc_f[2] = {0, 0};
+    u32 uid_f[2] = {0, 0};
   };
   std::vector<Ref> dpb;
   struct Job {
@@ -117,6 +121,7 @@ struct AvcHighEncoder::Impl {
     int type;  // h264::kI / kP / kB
     bool ref;
     bool idr;
+    int parity = -1;  // field coding: 0 top / 1 bottom field of the frame (-1: frame picture)
   };
   std::deque<Job> plan;
   std::map<i64, HostSurface> sources;
@@ -129,12 +134,21 @@ struct AvcHighEncoder::Impl {
   i64 last_disp = 0, last_pts = 0;
   char last_type = 'I';
   const HostSurface* cur_src = nullptr;
+  // field coding (cfg.fields): slots are fields (2 per frame), ph = field height in pixels
+  bool fields = false;
+  int ph = 0;
+  HostSurface field_src;
+  int pair_slot = -1, pair_fn = 0;
+  const u8* scan4 = kZigzag4x4;  // 4x4 level scan of the current picture (field pictures: field scan)
 
   explicit Impl(const AvcHighConfig& c) : cfg(c), rng{c.seed * 0x9E3779B97F4A7C15ull + 777} {
     VEP_CHECK(c.width >= 16 && c.height >= 16 && c.width % 2 == 0 && c.height % 2 == 0,
               "encoder size must be even and >= 16");
     VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.refs >= 1 && c.refs <= 8, "bframes 0..4, refs 1..8");
     VEP_CHECK(c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
+    VEP_CHECK(!c.fields || (c.interlaced && !c.cabac && !c.t8x8 && c.bframes == 0 && c.weighted_b == 0),
+              "field coding: interlaced CAVLC I / P with 4x4 transforms only");
+    fields = c.fields;
     W = (c.width + 15) / 16;
     H = (c.height + 15) / 16;
     if (c.interlaced) H = (H + 1) & ~1;  // (frame height in MB pairs: map units of 2 MB rows)
@@ -181,8 +195,9 @@ struct AvcHighEncoder::Impl {
     auto nal = [](const std::vector<u8>& rbsp, std::vector<u8>& out) { rbsp_to_ebsp(rbsp.data(), rbsp.size(), out); };
     nal(h264::write_sps(sps), sps_nal);
     nal(h264::write_pps(pps), pps_nal);
-    slots.resize(size_t(sps.max_num_ref_frames) + 2);
-    for (auto& s : slots) s.alloc(wpx, hpx);
+    ph = fields ? hpx / 2 : hpx;
+    slots.resize((size_t(sps.max_num_ref_frames) + 2) * (fields ? 2 : 1));
+    for (auto& s : slots) s.alloc(wpx, ph);
     scene.make(SceneConfig{c.width, c.height, wpx, hpx, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
   }
 
@@ -200,6 +215,14 @@ struct AvcHighEncoder::Impl {
   }
 
   void plan_next() {
+    if (fields) {  // every frame a field pair: I / P (IDR frames) or P / P, both references
+      const bool idr = is_idr_pos(next_disp);
+      if (idr) gop_start = next_disp;
+      plan.push_back({next_disp, idr ? h264::kI : h264::kP, true, idr, 0});
+      plan.push_back({next_disp, h264::kP, true, false, 1});
+      ++next_disp;
+      return;
+    }
     if (is_idr_pos(next_disp)) {
       plan.push_back({next_disp, h264::kI, true, true});
       gop_start = next_disp;
@@ -248,7 +271,41 @@ struct AvcHighEncoder::Impl {
     }
   }
 
+  // List 0 of a P field: the decoder's field list initialisation (Decoder::build_field_lists):
+  // reference frames by FrameNumWrap descending, split into fields alternating from the current
+  // parity.
+  void build_field_lists(const SliceHdr& sh, std::vector<ListEntry>* lists) {
+    lists[0].clear();
+    lists[1].clear();
+    if (sh.type() == h264::kI) return;
+    std::vector<const Ref*> st;
+    for (const Ref& r : dpb) st.push_back(&r);
+    auto wrap = [&](const Ref* r) { return r->frame_num > sh.frame_num ? r->frame_num - max_fn : r->frame_num; };
+    std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap(a) > wrap(b); });
+    const int same = sh.bottom_field ? 1 : 0;
+    std::vector<ListEntry> f[2];
+    for (const Ref* r : st)
+      for (int k = 0; k < 2; ++k) {
+        const int par = k == 0 ? same : 1 - same;
+        if ((r->fields >> par) & 1) f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], false, r->uid_f[par], nullptr});
+      }
+    size_t i[2] = {0, 0};
+    for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
+      const int from = i[k] < f[k].size() ? k : k ^ 1;
+      if (int(lists[0].size()) < sh.num_ref_idx[0]) lists[0].push_back(f[from][i[from]]);
+      ++i[from];
+    }
+  }
+
   int pick_slot() const {
+    if (fields) {  // a frame slot (both of its field slots free)
+      for (int s = 0; 2 * s + 1 < int(slots.size()); ++s) {
+        bool used = false;
+        for (const Ref& r : dpb) used |= r.slot == s;
+        if (!used) return s;
+      }
+      throw Error("vep: encoder DPB overflow");
+    }
     for (int s = 0; s < int(slots.size()); ++s) {
       bool used = false;
       for (const Ref& r : dpb) used |= r.slot == s;
@@ -264,10 +321,14 @@ struct AvcHighEncoder::Impl {
     bw.ue(u32(sh.slice_type));
     bw.ue(0);
     bw.u(sps.log2_max_frame_num, u32(sh.frame_num));
-    if (!sps.frame_mbs_only) bw.u1(0);  // field_pic_flag: frame pictures
+    if (!sps.frame_mbs_only) {
+      bw.u1(sh.field_pic);
+      if (sh.field_pic) bw.u1(sh.bottom_field);
+    }
     if (sh.idr()) bw.ue(u32(sh.idr_pic_id));
     bw.u(sps.log2_max_poc_lsb, u32(sh.poc_lsb));
-    if (pps.bottom_field_pic_order) bw.se(1);  // delta_pic_order_cnt_bottom: top field first
+    // delta_pic_order_cnt_bottom (frame pictures): top field first
+    if (pps.bottom_field_pic_order && !sh.field_pic) bw.se(1);
     const int st = sh.type();
     if (st == h264::kB) bw.u1(sh.direct_spatial);
     if (st != h264::kI) {
@@ -355,7 +416,7 @@ struct AvcHighEncoder::Impl {
         fwd4x4(x, w);
         dcw[r] = w[0];
         for (int k = i16 ? 1 : 0; k < 16; ++k) {
-          const int pos = kZigzag4x4[k];
+          const int pos = scan4[k];
           const int l = quant(w[pos], qp, mf_class(pos), intra);
           d.ac[r][i16 ? k - 1 : k] = l;
           if (l) cl |= 1 << (raster_to_blk(r) >> 2);
@@ -377,7 +438,7 @@ struct AvcHighEncoder::Impl {
           g[8 + j] = a - b - c + e;
           g[12 + j] = a - b + c - e;
         }
-        for (int k = 0; k < 16; ++k) d.dc[k] = quant(g[kZigzag4x4[k]] / 2, qp, 0, true, 1);
+        for (int k = 0; k < 16; ++k) d.dc[k] = quant(g[scan4[k]] / 2, qp, 0, true, 1);
         cl = cl ? 15 : 0;
       }
     }
@@ -394,7 +455,7 @@ struct AvcHighEncoder::Impl {
         fwd4x4(x, w);
         cw[b] = w[0];
         for (int k = 1; k < 16; ++k) {
-          const int pos = kZigzag4x4[k];
+          const int pos = scan4[k];
           d.cac[c][b][k - 1] = quant(w[pos], qpc[c], mf_class(pos), intra);
           if (d.cac[c][b][k - 1]) cc = 2;
         }
@@ -448,14 +509,16 @@ struct AvcHighEncoder::Impl {
       for (int i = 0; i < 16; i += 2)
         for (int j = 0; j < 16; j += 2) {
           const int x = mx * 16 + j, y = my * 16 + i;
-          s += std::abs(S(x, y) - luma_qpel(R.y.data(), wpx, wpx, hpx, x + (vx >> 2), y + (vy >> 2), vx & 3, vy & 3));
+          s += std::abs(S(x, y) - luma_qpel(R.y.data(), wpx, wpx, ph, x + (vx >> 2), y + (vy >> 2), vx & 3, vy & 3));
         }
       return s * 4 + 4 * (std::abs(vx - pmv[0]) + std::abs(vy - pmv[1]));
     };
     std::vector<std::pair<int, int>> cand = {{0, 0}, {pmv[0], pmv[1]}};
+    const double ys = fields ? 0.5 : 1.0;  // (a field has half the frame's rows)
     for (const Scene::Obj& o : scene.objs) {
-      if (o.x > mx * 16 + 24 || o.x + o.w < mx * 16 - 8 || o.y > my * 16 + 24 || o.y + o.h < my * 16 - 8) continue;
-      cand.push_back({int(std::lround(o.vx * 4 * dist)), int(std::lround(o.vy * 4 * dist))});
+      if (o.x > mx * 16 + 24 || o.x + o.w < mx * 16 - 8 || o.y * ys > my * 16 + 24 || (o.y + o.h) * ys < my * 16 - 8)
+        continue;
+      cand.push_back({int(std::lround(o.vx * 4 * dist)), int(std::lround(o.vy * ys * 4 * dist))});
     }
     best_sad = 1 << 30;
     for (auto [vx, vy] : cand) {
@@ -680,6 +743,17 @@ struct AvcHighEncoder::Impl {
   // ---------------------------------------------------------------- picture
   std::shared_ptr<AccessUnit> encode(const Job& job) {
     cur_src = &source_of(job.disp);
+    const bool fld = job.parity >= 0;
+    if (fld) {  // the field's rows of the frame
+      const HostSurface& f = *cur_src;
+      if (field_src.coded_w != wpx || field_src.coded_h != ph) field_src.alloc(wpx, ph);
+      for (int r = 0; r < ph; ++r)
+        std::memcpy(&field_src.y[size_t(r) * wpx], &f.y[size_t(2 * r + job.parity) * wpx], size_t(wpx));
+      for (int r = 0; r < ph / 2; ++r)
+        std::memcpy(&field_src.uv[size_t(r) * wpx], &f.uv[size_t(2 * r + job.parity) * wpx], size_t(wpx));
+      cur_src = &field_src;
+    }
+    scan4 = fld ? kFieldScan4x4 : kZigzag4x4;
     const bool idr = job.idr;
     if (idr) {
       dpb.clear();
@@ -689,13 +763,20 @@ struct AvcHighEncoder::Impl {
     sh.nal_type = idr ? h264::kNalIdr : h264::kNalSlice;
     sh.nal_ref_idc = job.ref ? (job.type == h264::kB ? 2 : 3) : 0;
     sh.slice_type = job.type;
-    sh.frame_num = idr ? 0 : (prev_ref_fn + 1) % max_fn;
+    sh.frame_num = job.parity == 1 ? pair_fn : idr ? 0 : (prev_ref_fn + 1) % max_fn;
+    sh.field_pic = fld;
+    sh.bottom_field = job.parity == 1;
     sh.idr_pic_id = idr_id & 0xFFFF;
-    const int poc = int(2 * (job.disp - gop_start));
+    const int poc = int(2 * (job.disp - gop_start)) + (fld ? job.parity : 0);  // top 2k, bottom 2k + 1
     sh.poc_lsb = poc & ((1 << sps.log2_max_poc_lsb) - 1);
     sh.direct_spatial = cfg.direct_spatial;
     int n0 = 0, n1 = 0;
-    if (job.type == h264::kP) n0 = std::min<int>(cfg.refs, int(dpb.size()));
+    if (job.type == h264::kP && !fld) n0 = std::min<int>(cfg.refs, int(dpb.size()));
+    if (job.type == h264::kP && fld) {  // reference fields (the first field of this frame included)
+      int nf = 0;
+      for (const Ref& r : dpb) nf += (r.fields & 1) + (r.fields >> 1);
+      n0 = std::min(2 * cfg.refs, nf);
+    }
     if (job.type == h264::kB) {
       int before = 0, after = 0;
       for (const Ref& r : dpb) (r.poc < poc ? before : after) += 1;
@@ -727,17 +808,19 @@ struct AvcHighEncoder::Impl {
     sh.disable_deblocking = cfg.deblock_idc;
     const bool weighted = sh.explicit_wp || (job.type == h264::kB && cfg.weighted_b == 2);
 
+    const int Hp = fld ? H / 2 : H;  // MB rows of the picture
     pic = Picture{};
     pic.wmbs = W;
-    pic.hmbs = H;
-    pic.mbs.assign(size_t(W) * H, MbRec{});
-    pic.coefs.reserve(size_t(W) * H * 64);
-    pic.mvs.reserve(size_t(W) * H * 64);
+    pic.hmbs = Hp;
+    pic.mbs.assign(size_t(W) * Hp, MbRec{});
+    pic.coefs.reserve(size_t(W) * Hp * 64);
+    pic.mvs.reserve(size_t(W) * Hp * 64);
     pic.dpb_slots = int(slots.size());
-    pic.target = pick_slot();
+    pic.structure = fld ? 1 + job.parity : 0;
+    pic.target = fld ? 2 * (job.parity == 1 ? pair_slot : pick_slot()) + job.parity : pick_slot();
     pic.idr = idr;
     pic.poc = poc;
-    nb.reset(W, H);
+    nb.reset(W, Hp);
     std::vector<ListEntry> lists[2];
     auto au = std::make_shared<AccessUnit>();
     au->codec = Codec::kH264;
@@ -745,7 +828,7 @@ struct AvcHighEncoder::Impl {
     // decoding timestamps run `reorder depth` frames behind the display timestamps
     const i64 dur = 90000 / std::max(1, cfg.fps);
     au->pts = (job.disp + std::max(0, sps.max_num_reorder_frames)) * dur;
-    au->dts = coded * dur;
+    au->dts = fld ? coded * dur / 2 : coded * dur;
     au->duration = dur;
     au->seq = u64(coded);
     last_pts = au->pts;
@@ -755,11 +838,12 @@ struct AvcHighEncoder::Impl {
       au->add_nal(pps_nal.data(), pps_nal.size());
     }
     std::vector<std::array<std::vector<u32>, 2>> slice_uids;
-    const int nslices = std::max(1, std::min(cfg.slices, H));
+    const int nslices = std::max(1, std::min(cfg.slices, Hp));
     for (int si = 0; si < nslices; ++si) {
-      const int row0 = si * H / nslices, row1 = (si + 1) * H / nslices;
+      const int row0 = si * Hp / nslices, row1 = (si + 1) * Hp / nslices;
       sh.first_mb = row0 * W;
-      build_lists(sh, poc, lists);
+      if (fld) build_field_lists(sh, lists);
+      else build_lists(sh, poc, lists);
       std::array<std::vector<u32>, 2> uids;
       for (int l = 0; l < 2; ++l)
         for (const auto& e : lists[l]) uids[size_t(l)].push_back(e.uid);
@@ -773,6 +857,7 @@ struct AvcHighEncoder::Impl {
       env.list[1] = &lists[1];
       env.cur_poc = poc;
       env.scaling = h264::resolve_scaling(sps, pps);
+      env.field = fld;
       BitWriter bw;
       write_header(bw, sh);
       SliceWriter sw(nb, pic, env, bw);
@@ -790,7 +875,35 @@ struct AvcHighEncoder::Impl {
       au->add_nal(nal.data(), nal.size());
     }
     if (pic.deblock) cpu_deblock(pic, T());
-    if (job.ref) {
+    if (job.ref && fld) {  // a frame entry holding its reference fields (sliding window on frames)
+      const int fs = pic.target >> 1, par = job.parity;
+      bool joined = false;
+      if (par == 1)
+        for (Ref& r : dpb)
+          if (r.slot == fs && r.frame_num == sh.frame_num) {
+            r.fields |= 2;
+            r.poc_f[1] = poc;
+            r.uid_f[1] = next_uid;
+            joined = true;
+          }
+      if (!joined) {
+        if (int(dpb.size()) >= sps.max_num_ref_frames) {
+          auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
+            auto wrap = [&](const Ref& x) { return x.frame_num > sh.frame_num ? x.frame_num - max_fn : x.frame_num; };
+            return wrap(a) < wrap(b);
+          });
+          dpb.erase(it);
+        }
+        Ref r{fs, sh.frame_num, poc, next_uid, nullptr};
+        r.fields = u8(1 << par);
+        r.poc_f[par] = poc;
+        r.uid_f[par] = next_uid;
+        dpb.push_back(r);
+        prev_ref_fn = sh.frame_num;
+        pair_fn = sh.frame_num;
+        pair_slot = fs;
+      }
+    } else if (job.ref) {
       Ref r{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)};
       if (int(dpb.size()) >= sps.max_num_ref_frames) {  // sliding window (§8.2.5.3)
         auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
@@ -803,12 +916,17 @@ struct AvcHighEncoder::Impl {
       prev_ref_fn = sh.frame_num;
     }
     ++next_uid;
-    recon = T();
-    src_out = *cur_src;
+    if (!fld) {
+      recon = T();
+      src_out = *cur_src;
+    } else if (job.parity == 1) {  // the frame is complete: its two fields woven
+      weave_fields(slots[size_t(2 * pair_slot)], slots[size_t(2 * pair_slot + 1)], recon);
+      src_out = source_of(job.disp);
+    }
     last_disp = job.disp;
     ++coded;
     // sources of pictures coded and no longer needed
-    sources.erase(job.disp);
+    if (job.parity != 0) sources.erase(job.disp);
     return au;
   }
 

@@ -18,6 +18,7 @@ struct SliceEnv {
   const std::vector<ListEntry>* list[2] = {nullptr, nullptr};
   int cur_poc = 0;
   h264::ScalingLists scaling;                // in force for this slice (resolved)
+  bool field = false;                        // field picture: field scan of the 4x4 levels
 };
 
 // The macroblock layer of one slice (both entropy modes, I/P/B, 8x8 transform, direct and
@@ -39,8 +40,9 @@ std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, in
 
 // Inter prediction of one MB (list-0 / list-1 + weights), exactly the reconstruction's: py 16x16
 // luma, pc 2 x 8x8 chroma. mv0 / mv1: 16 (x, y) per list (mv1 may be null).
+// structure: Picture::structure (field pictures: slots are fields, slot parity = field parity).
 void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
-                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64]);
+                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure = 0);
 
 // Encoder side of the generic macroblock layer: the decisions of one macroblock. The layer turns
 // them into syntax (predicted intra modes -> prev/rem flags, motion -> mvd against the same

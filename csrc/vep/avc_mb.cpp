@@ -71,7 +71,8 @@ class MbLayer {
 
  public:
   MbLayer(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const Dequant& dq)
-      : nb_(nb), pic_(pic), env_(env), sh_(*env.sh), pps_(*env.pps), sps_(*env.sps), dq_(dq) {
+      : nb_(nb), pic_(pic), env_(env), sh_(*env.sh), pps_(*env.pps), sps_(*env.sps), dq_(dq),
+        scan4_(env.field ? kFieldScan4x4 : kZigzag4x4) {
     type_ = sh_.type();
     qp_ = sh_.qp;
     weighted_ = (type_ == h264::kP && pps_.weighted_pred) || (type_ == h264::kB && pps_.weighted_bipred_idc != 0);
@@ -808,7 +809,7 @@ class MbLayer {
       if (tdc > 0) {
         s.cbf_dc |= 1;
         int c[16] = {};
-        for (int j = 0; j < tdc; ++j) c[kZigzag4x4[nzp[j]]] = lv[nzp[j]];
+        for (int j = 0; j < tdc; ++j) c[scan4_[nzp[j]]] = lv[nzp[j]];
         hadamard4x4(c);
         const int ls = dq_.ls4[ly][qm][0];
         for (int k = 0; k < 16; ++k)
@@ -826,7 +827,7 @@ class MbLayer {
           const int tc = read_block(kCatLumaAc, binc, bnc, 15, lv, nzp, kWrite ? want->ac[r] : nullptr);
           for (int j = 0; j < tc; ++j) {
             const int k = nzp[j];
-            const int pos = kZigzag4x4[k + 1];
+            const int pos = scan4_[k + 1];
             const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
             d[pos] = sat16(v);
             nz |= v != 0;
@@ -888,7 +889,7 @@ class MbLayer {
         bool nz = false;
         for (int j = 0; j < tc; ++j) {
           const int k = nzp[j];
-          const int pos = kZigzag4x4[k];
+          const int pos = scan4_[k];
           const int v = scale4(lv[k], dq_.ls4[ly][qm][pos], qp);
           d[pos] = sat16(v);
           nz |= v != 0;
@@ -929,7 +930,7 @@ class MbLayer {
             if (tc) s.cbf_cac[c] |= u8(1u << b);
             for (int j = 0; j < tc; ++j) {
               const int k = nzp[j];
-              const int pos = kZigzag4x4[k + 1];
+              const int pos = scan4_[k + 1];
               const int v = scale4(lv[k], dq_.ls4[lc][qpc[c] % 6][pos], qpc[c]);
               d[pos] = sat16(v);
               nz |= v != 0;
@@ -1010,6 +1011,7 @@ class MbLayer {
   const h264::Pps& pps_;
   const h264::Sps& sps_;
   const Dequant& dq_;
+  const u8* scan4_;  // 4x4 scan: zig-zag (frame) or field
   int type_ = 0;
   int qp_ = 26;
   bool weighted_ = false, implicit_ = false;

@@ -209,6 +209,9 @@ VEP_HD int chroma_qp(int qpy, int offset) {
 
 // Zig-zag scan (frame macroblocks): scan index -> raster position in the 4x4 block.
 VEP_CONST static const u8 kZigzag4x4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
+// Field scan (field pictures, Table 8-13): mostly vertical, the field's rows being twice as far
+// apart as the frame's. (Scaling lists keep the zig-zag order in either case.)
+VEP_CONST static const u8 kFieldScan4x4[16] = {0, 4, 1, 8, 12, 5, 9, 13, 2, 6, 10, 14, 3, 7, 11, 15};
 
 // Deblocking thresholds (Table 8-16 / 8-17), indexed by indexA / indexB.
 VEP_CONST static const u8 kAlpha[52] = {
@@ -896,10 +899,14 @@ VEP_HD int chroma_epel(const u8* uv, int pitch, int w, int h, int c, int xi, int
 // mv pool (granularity by the MbRec flags, see mv_sub()); unused for intra MBs. Reference
 // pictures are compared by DPB slot (= picture identity within one picture's decode), so a
 // picture reached through list 0 and list 1 counts as the same picture.
-VEP_HD bool mv_far(const i16* a, const i16* b) { return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= 4; }
-VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
-                             const i16* mv_q, bool mb_edge) {
-  if (is_intra(mp.kind) || is_intra(mq.kind)) return mb_edge ? 4 : 3;
+// Field pictures (`field`): an intra horizontal MB edge gets bS 3, not 4, and vertical vectors
+// (quarter field samples) differ "by 4 quarter frame samples" at 2.
+VEP_HD bool mv_far(const i16* a, const i16* b, int ylim = 4) {
+  return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= ylim;
+}
+// (the non-intra part: coefficients, reference pictures, vectors)
+VEP_HD int boundary_strength_mv(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
+                                const i16* mv_q, int ylim) {
   if (((mp.nz >> bp) & 1) || ((mq.nz >> bq) & 1)) return 2;
   const int p8 = ((bp >> 3) << 1) | ((bp & 3) >> 1), q8 = ((bq >> 3) << 1) | ((bq & 3) >> 1);
   const int p0 = mp.ref[p8], p1 = (mp.flags & kMbL1) ? mp.ref1[p8] : 0xFF;
@@ -913,15 +920,22 @@ VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbR
   if (np == 1) {
     const int rp = p0 != 0xFF ? p0 : p1, rq = q0 != 0xFF ? q0 : q1;
     if (rp != rq) return 1;
-    return mv_far(p0 != 0xFF ? pa : pb, q0 != 0xFF ? qa : qb) ? 1 : 0;
+    return mv_far(p0 != 0xFF ? pa : pb, q0 != 0xFF ? qa : qb, ylim) ? 1 : 0;
   }
   if (!((p0 == q0 && p1 == q1) || (p0 == q1 && p1 == q0))) return 1;
   if (p0 != p1) {  // two different reference pictures: compare the vectors of the same picture
-    if (p0 == q0) return (mv_far(pa, qa) || mv_far(pb, qb)) ? 1 : 0;
-    return (mv_far(pa, qb) || mv_far(pb, qa)) ? 1 : 0;
+    if (p0 == q0) return (mv_far(pa, qa, ylim) || mv_far(pb, qb, ylim)) ? 1 : 0;
+    return (mv_far(pa, qb, ylim) || mv_far(pb, qa, ylim)) ? 1 : 0;
   }
   // both vectors of both blocks reference the same picture
-  return ((mv_far(pa, qa) || mv_far(pb, qb)) && (mv_far(pa, qb) || mv_far(pb, qa))) ? 1 : 0;
+  return ((mv_far(pa, qa, ylim) || mv_far(pb, qb, ylim)) && (mv_far(pa, qb, ylim) || mv_far(pb, qa, ylim))) ? 1 : 0;
+}
+
+VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
+                             const i16* mv_q, bool mb_edge, bool field = false, bool vertical = true) {
+  if (is_intra(mp.kind) || is_intra(mq.kind)) return (mb_edge && (vertical || !field)) ? 4 : 3;
+  if (field) return boundary_strength_mv(mp, bp, mv_p, mq, bq, mv_q, 2);
+  return boundary_strength_mv(mp, bp, mv_p, mq, bq, mv_q, 4);
 }
 
 struct EdgeParams {

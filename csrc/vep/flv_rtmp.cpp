@@ -330,11 +330,18 @@ RtmpPublisher::RtmpPublisher(std::string url, int timeout_ms)
 RtmpPublisher::~RtmpPublisher() { close(); }
 
 void RtmpPublisher::close() {
+  std::lock_guard<std::mutex> g(fd_mu_);
   if (fd_ >= 0) {
     ::shutdown(fd_, SHUT_RDWR);
     ::close(fd_);
     fd_ = -1;
   }
+}
+
+void RtmpPublisher::interrupt() {
+  std::lock_guard<std::mutex> g(fd_mu_);
+  interrupted_ = true;
+  if (fd_ >= 0) ::shutdown(fd_, SHUT_RDWR);
 }
 
 void RtmpPublisher::send_message(int csid, u8 type, u32 stream, u32 ts, const std::vector<u8>& body) {
@@ -349,7 +356,15 @@ void RtmpPublisher::send_message(int csid, u8 type, u32 stream, u32 ts, const st
 
 void RtmpPublisher::connect() {
   close();
-  fd_ = sock::connect_tcp(host_, port_, timeout_ms_);
+  int fd = sock::connect_tcp(host_, port_, timeout_ms_);
+  {
+    std::lock_guard<std::mutex> g(fd_mu_);
+    if (interrupted_) {
+      ::close(fd);
+      throw Error("RTMP publisher stopped");
+    }
+    fd_ = fd;
+  }
   VEP_CHECK(handshake_client(fd_, timeout_ms_), "RTMP handshake failed");
   ChunkReader rd;
   auto wait_for = [&](const std::string& name, double* stream_out) {

@@ -158,6 +158,9 @@ void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream
 // Main10 output: u16 NV12 planes (n luma samples, n / 2 chroma) -> 8-bit NV12 (round to nearest,
 // saturating), the form the BGR24 conversion and the letterbox read.
 void launch_narrow(const u16* y, const u16* uv, u8* y8, u8* uv8, size_t n, int bd, hipStream_t s);
+// H.264 field pair (frame slot in field-separated layout: top field rows, then bottom) -> the
+// interleaved 8-bit NV12 frame (pitch bytes per row, `height` luma rows).
+void launch_weave(const u8* y, const u8* uv, u8* y8, u8* uv8, int pitch, int height, hipStream_t s);
 
 // ---- general H.264 reconstruction (gpu_avc.hip; records from avc::Decoder, avc.h) ----------
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera
@@ -174,7 +177,7 @@ struct AvcDesc {
   i32 target;          // DPB slot reconstructed into
   i32 constrained;     // constrained_intra_pred_flag
   i32 mb_begin;        // exclusive prefix of MBs over the round (inter kernel block -> picture)
-  i32 pad;
+  i32 field;           // 0 frame; 1 / 2 top / bottom field picture (slots are fields, parity = slot & 1)
   VEP_DEV u32* err;            // pinned flag: wavefront timeout (frame dropped)
   VEP_DEV void* dbk;           // device scratch: AvcDbkInfo[wmbs * hmbs] (avc_bs_kernel -> deblock)
   VEP_DEV i16* res;            // device scratch: kAvcResSamples per intra MB with residual (MbRec::res

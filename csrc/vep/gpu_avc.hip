@@ -253,13 +253,15 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     int p0 = 0, p1 = 0;
     if (s0 != 0xFF) {
       const i16* v0 = mvb + avc::mv_sub(m.flags, 0, r);
+      const int vy = v0[1] + (d.field ? 2 * ((d.field == 2) - (s0 & 1)) : 0);  // opposite-parity field
       p0 = avc::chroma_epel(d.uv + d.slot_uv * u64(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v0[0] >> 3),
-                            my * 8 + cy + (v0[1] >> 3), v0[0] & 7, v0[1] & 7);
+                            my * 8 + cy + (vy >> 3), v0[0] & 7, vy & 7);
     }
     if (s1 != 0xFF) {
       const i16* v1 = mvb + avc::mv_sub(m.flags, 1, r);
+      const int vy = v1[1] + (d.field ? 2 * ((d.field == 2) - (s1 & 1)) : 0);
       p1 = avc::chroma_epel(d.uv + d.slot_uv * u64(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v1[0] >> 3),
-                            my * 8 + cy + (v1[1] >> 3), v1[0] & 7, v1[1] & 7);
+                            my * 8 + cy + (vy >> 3), v1[0] & 7, vy & 7);
     }
     u[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 1 + cc);
   }
@@ -803,7 +805,7 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
         for (int sg = 0; sg < 4; ++sg) {
           const int bq = dir == 0 ? sg * 4 + e : e * 4 + sg;
           const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
-          const int bs = avc::boundary_strength(p, bp, mp, q, bq, mq, e == 0);
+          const int bs = avc::boundary_strength(p, bp, mp, q, bq, mq, e == 0, d.field != 0, dir == 0);
           const int i = dir * 16 + e * 4 + sg;
           info.bs[i >> 3] |= u32(bs) << (4 * (i & 7));
         }
@@ -1226,7 +1228,31 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     for (int k = 0; k < 5; ++k) atomicAdd(&d.prof[6 + k], acc[k]);
 }
 
+// Field pair -> frame: the frame slot holds the top field's rows, then the bottom field's (luma
+// h / 2 rows each, chroma h / 4); frame row r is row r >> 1 of field r & 1. 16 bytes per lane.
+__global__ __launch_bounds__(256) void weave_kernel(const u8* __restrict__ y, const u8* __restrict__ uv,
+                                                    u8* __restrict__ y8, u8* __restrict__ uv8, int pitch, int h) {
+  const int per_row = pitch / 16;
+  const size_t g = size_t(blockIdx.x) * 256 + threadIdx.x, total = size_t(per_row) * size_t(h + h / 2);
+  if (g >= total) return;
+  const int row = int(g / size_t(per_row)), col = int(g % size_t(per_row)) * 16;
+  const bool luma = row < h;
+  const int r = luma ? row : row - h, fh = luma ? h / 2 : h / 4;  // rows per field
+  const u8* src = (luma ? y : uv) + (size_t(r & 1) * size_t(fh) + size_t(r >> 1)) * size_t(pitch) + size_t(col);
+  u8* dst = (luma ? y8 : uv8) + size_t(r) * size_t(pitch) + size_t(col);
+  *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+}
+
 }  // namespace
+
+void launch_weave(const u8* y, const u8* uv, u8* y8, u8* uv8, int pitch, int height, hipStream_t s) {
+  if (pitch <= 0 || height <= 0) return;
+  VEP_CHECK(pitch % 16 == 0 && height % 4 == 0, "weave: pitch / height alignment");
+  const size_t lanes = size_t(pitch / 16) * size_t(height + height / 2);
+  hipLaunchKernelGGL(weave_kernel, dim3(unsigned((lanes + 255) / 256)), dim3(256), 0, s, y, uv, y8, uv8, pitch,
+                     height);
+  VEP_HIP(hipGetLastError());
+}
 
 void launch_avc_inter(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s) {
   if (n <= 0 || total_mbs <= 0) return;

@@ -393,6 +393,7 @@ RtmpSender::~RtmpSender() {
   {
     std::lock_guard<std::mutex> g(mu_);
     stop_ = true;
+    if (cur_) cur_->interrupt();  // a handshake with a server that never answers ends now
   }
   cv_.notify_all();
   if (th_.joinable()) th_.join();
@@ -464,7 +465,9 @@ void RtmpSender::run() {
           dropped_.fetch_add(1);
           continue;
         }
-        pub = std::make_unique<mux::RtmpPublisher>(url_, timeout_ms_);
+        publish(pub, nullptr);
+        auto np = std::make_unique<mux::RtmpPublisher>(url_, timeout_ms_);
+        if (!publish(pub, std::move(np))) break;
         pub->connect();
         ts0_ = -1;
       }
@@ -478,7 +481,7 @@ void RtmpSender::run() {
       std::lock_guard<std::mutex> g(mu_);
       if (err_.rfind("rtmp send queue overflow", 0) != 0) err_.clear();
     } catch (const std::exception& e) {
-      pub.reset();
+      publish(pub, nullptr);
       retry_at = mono_us() / 1000 + 2000;
       std::lock_guard<std::mutex> g(mu_);
       err_ = e.what();
@@ -486,6 +489,17 @@ void RtmpSender::run() {
     }
   }
   if (pub) pub->close();
+  publish(pub, nullptr);
+}
+
+bool RtmpSender::publish(std::unique_ptr<mux::RtmpPublisher>& pub, std::unique_ptr<mux::RtmpPublisher> np) {
+  {
+    std::lock_guard<std::mutex> g(mu_);
+    if (np && stop_) return false;
+    cur_ = np.get();  // the destructor interrupts only a publisher that is still alive
+  }
+  pub = std::move(np);
+  return true;
 }
 
 void IngestSession::run() {

@@ -81,6 +81,8 @@ class RtmpSender {
   };
   void run();
   void drop_all_locked();
+  // Replaces the live publisher (registering it for interrupt()); false once stopping.
+  bool publish(std::unique_ptr<mux::RtmpPublisher>& pub, std::unique_ptr<mux::RtmpPublisher> np);
   const std::string url_;
   const int timeout_ms_;
   const size_t max_bytes_;
@@ -90,6 +92,7 @@ class RtmpSender {
   std::deque<Item> q_;
   size_t q_bytes_ = 0;
   bool stop_ = false;
+  mux::RtmpPublisher* cur_ = nullptr;  // the live publisher (under mu_), for interrupt()
   std::atomic<bool> need_key_{true};
   std::atomic<u64> msgs_{0}, dropped_{0};
   std::string err_;

@@ -42,6 +42,9 @@ class RtmpPublisher {
   void send_sequence_header(const ParamSets& ps);
   void send_au(const AccessUnit& au, u32 ts_ms);
   void close();
+  // From another thread: unblocks a connect / handshake / send in progress (shutdown of the
+  // socket) and makes later connects fail; the owning thread still closes.
+  void interrupt();
   u64 bytes_sent() const { return sent_; }
   u64 messages() const { return msgs_; }
 
@@ -51,6 +54,8 @@ class RtmpPublisher {
   std::string host_;
   int port_ = 1935, timeout_ms_;
   int fd_ = -1;
+  std::mutex fd_mu_;  // fd_ open/close vs interrupt()
+  bool interrupted_ = false;
   u32 out_chunk_ = 128;
   u32 stream_id_ = 1;
   u64 sent_ = 0, msgs_ = 0;

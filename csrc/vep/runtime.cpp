@@ -306,7 +306,9 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
     }
     if (full_) {
       for (size_t i = from; i < to; ++i) {
-        job.avc.push_back(avc_.parse(*gop_[i], i64(i)));
+        size_t nal = 0;  // (a field pair may come as one access unit: one picture per field)
+        do job.avc.push_back(avc_.parse(*gop_[i], i64(i), &nal));
+        while (nal < gop_[i]->nals.size());
         last = gop_[i].get();
       }
       job.pic = job.avc.back()->info;
@@ -315,6 +317,7 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
       for (const auto& p : job.avc)
         if (!p->outputs.empty()) of = &p->outputs.back();
       job.out_slot = of ? of->slot : -1;
+      job.out_fields = of && of->fields;
       if (of) {
         job.pic = of->info;
         FrameMeta& m = job.meta;
@@ -802,12 +805,21 @@ void Worker::loop() {
   }
 }
 
-void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps) {
+void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps, bool weave) {
   const int wmbs = pi.coded_width / 16, hmbs = pi.coded_height / 16;
   auto& s = c.surface;
+  // the 8-bit frame the conversion reads when the slot is not one (Main10; a woven field pair)
+  auto scratch8 = [&] {
+    if (!dev_.gpu() || s.y8) return;
+    const size_t y8 = size_t(s.wmbs) * 16 * s.hmbs * 16;
+    s.y8 = static_cast<u8*>(dev_.alloc(y8));
+    s.uv8 = static_cast<u8*>(dev_.alloc(y8 / 2));
+  };
   if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && s.bps == bps && c.ring_ &&
-      c.ring_->width() == pi.width && c.ring_->height() == pi.height)
+      c.ring_->width() == pi.width && c.ring_->height() == pi.height) {
+    if (weave) scratch8();  // (only ever added: no batch in flight reads a missing scratch)
     return;
+  }
   dev_.free(s.y);
   dev_.free(s.uv);
   dev_.free(s.y8);
@@ -824,10 +836,9 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps
     if (bps == 2) {  // Main10: u16 samples at 10-bit black / grey (a 10-bit CVS: HEVC only)
       VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.y), u16(16 << 2), ysz / 2, stream_));
       VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.uv), u16(128 << 2), ysz / 4, stream_));
-      const size_t y8 = size_t(wmbs) * 16 * hmbs * 16;
-      s.y8 = static_cast<u8*>(dev_.alloc(y8));
-      s.uv8 = static_cast<u8*>(dev_.alloc(y8 / 2));
+      scratch8();
     } else {
+      if (weave) scratch8();
       VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
       VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
     }
@@ -964,7 +975,9 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
   slots.resize(jobs.size());
   for (size_t i = 0; i < jobs.size(); ++i) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
-    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bytes_per_sample());
+    bool weave = jobs[i].out_fields;
+    for (const auto& p : jobs[i].avc) weave |= p->structure != 0;
+    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bytes_per_sample(), weave);
     slots[i] = jobs[i].has_output() ? c.ring_->begin_write() : -1;
   }
 }
@@ -1366,7 +1379,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const size_t words = size_t(j.upd.mbs() + 31) / 32;
     gpu::DecodeDesc& d = hd[k];
     const size_t tgt = size_t(j.target());
-    if (c->surface.bps == 2) {  // Main10: convert / letterbox the 8-bit copy (launch_narrow below)
+    if (c->surface.bps == 2 || j.out_fields) {  // Main10 / field pair: convert / letterbox the
+                                                // 8-bit frame (launch_narrow / launch_weave below)
       d.y = c->surface.y8;
       d.uv = c->surface.uv8;
     } else {
@@ -1434,14 +1448,16 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.wps = st.d + a.off_wp;
       g.y = c->surface.y;
       g.uv = c->surface.uv;
-      g.slot_y = c->surface.slot_y();
-      g.slot_uv = c->surface.slot_uv();
+      // field pictures address field slots: half a frame slot each (top field rows, then bottom)
+      const size_t per = a.p->structure ? 2 : 1;
+      g.slot_y = c->surface.slot_y() / per;
+      g.slot_uv = c->surface.slot_uv() / per;
       g.wmbs = a.p->wmbs;
       g.hmbs = a.p->hmbs;
       g.target = a.p->target;
       g.constrained = a.p->constrained_intra ? 1 : 0;
       g.mb_begin = mbs;
-      g.pad = 0;
+      g.field = a.p->structure;
       g.err = const_cast<u32*>(st.err_dev) + a.job;
       g.dbk = st.d + a.off_dbk;
       g.res = reinterpret_cast<i16*>(st.d + a.off_res);
@@ -1623,11 +1639,17 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     VEP_HIP(hipMemcpy2DAsync(c->surface.uv, pitch, f.uv, f.pitch_uv, size_t(f.width), size_t(f.height / 2),
                              hipMemcpyDefault, cs));
   }
-  for (int i : outs) {  // Main10 pictures: the published slot's 8-bit NV12 copy
+  for (int i : outs) {  // Main10 pictures / field pairs: the published slot's 8-bit NV12 frame
     const DecodeJob& j = jobs[size_t(i)];
     const Camera::Surface& sf = cams_[size_t(j.cam)]->surface;
-    if (sf.bps != 2) continue;
     const size_t tgt = size_t(j.target());
+    if (j.out_fields) {
+      VEP_CHECK(sf.y8 && sf.bps == 1, "field pair output without its weave scratch");
+      gpu::launch_weave(sf.y + tgt * sf.slot_y(), sf.uv + tgt * sf.slot_uv(), sf.y8, sf.uv8, sf.wmbs * 16,
+                        sf.hmbs * 16, cs);
+      continue;
+    }
+    if (sf.bps != 2) continue;
     gpu::launch_narrow(reinterpret_cast<const u16*>(sf.y + tgt * sf.slot_y()),
                        reinterpret_cast<const u16*>(sf.uv + tgt * sf.slot_uv()), sf.y8, sf.uv8,
                        size_t(sf.wmbs) * 16 * sf.hmbs * 16, j.hevc.empty() ? 10 : j.hevc.back()->bd_y, cs);
@@ -1671,14 +1693,30 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
       for (int r = 0; r < f.height / 2; ++r)
         std::memcpy(&hs.uv[size_t(r) * size_t(hs.coded_w)], f.uv + size_t(r) * f.pitch_uv, size_t(f.width));
     } else if (jobs[i].general()) {
-      for (const auto& pic : jobs[i].avc) avc::cpu_reconstruct(*pic, c.surface.host);
+      for (const auto& pic : jobs[i].avc) {
+        if (!pic->structure) {
+          avc::cpu_reconstruct(*pic, c.surface.host);
+          continue;
+        }
+        auto& F = c.surface.fields;  // field slots (half-height surfaces)
+        if (F.size() < size_t(pic->dpb_slots)) F.resize(size_t(pic->dpb_slots));
+        for (auto& h : F)
+          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16) h.alloc(pic->wmbs * 16, pic->hmbs * 16);
+        avc::cpu_reconstruct(*pic, F);
+      }
       for (const auto& pic : jobs[i].hevc) hevc::cpu_execute(*pic, c.surface.host);
     } else {
       cpu_apply_update(jobs[i].upd, c.surface.host[0]);
     }
     if (!jobs[i].has_output()) continue;
     HostSurface narrow;  // Main10: the 8-bit copy the conversion and the letterbox read
-    const HostSurface& out = c.surface.host[size_t(jobs[i].target())];
+    HostSurface woven;   // a field pair's frame
+    if (jobs[i].out_fields) {
+      const size_t t = size_t(jobs[i].target());
+      VEP_CHECK(2 * t + 1 < c.surface.fields.size(), "field pair output without its fields");
+      avc::weave_fields(c.surface.fields[2 * t], c.surface.fields[2 * t + 1], woven);
+    }
+    const HostSurface& out = jobs[i].out_fields ? woven : c.surface.host[size_t(jobs[i].target())];
     if (out.wide()) narrow_surface(out, narrow);
     const HostSurface& src = out.wide() ? narrow : out;
     cpu_nv12_to_bgr(src, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
@@ -1728,7 +1766,9 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       continue;
     }
     if (!(err && err[i]) && !cp->broken_) {
-      const u64 np = jobs[i].general() ? jobs[i].avc.size() + jobs[i].hevc.size() : 1;
+      // decoded frames (a field pair counts once: its second field)
+      u64 np = jobs[i].general() ? jobs[i].hevc.size() : 1;
+      for (const auto& p : jobs[i].avc) np += !p->structure || p->second_field;
       pictures_.fetch_add(np, std::memory_order_relaxed);
       cp->pictures.fetch_add(np, std::memory_order_relaxed);
     }

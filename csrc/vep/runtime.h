@@ -113,6 +113,7 @@ struct DecodeJob {
   // converted and published), -1 when every picture of the job is still waiting for output
   // (B-frame reordering): the job then only reconstructs.
   int out_slot = -1;
+  bool out_fields = false;  // H.264 field pair: out_slot holds two fields (avc::OutFrame::fields)
   // VCN backend (vcn.h): a picture decoded by the video core; the worker copies its planes into
   // the camera's surface, then converts / letterboxes / publishes it like any other frame.
   vcn::FramePtr ext;
@@ -203,6 +204,7 @@ class Camera {
     size_t slot_y() const { return size_t(wmbs) * 16 * hmbs * 16 * size_t(bps); }
     size_t slot_uv() const { return slot_y() / 2; }
     std::vector<HostSurface> host;  // CPU backend: one per slot
+    std::vector<HostSurface> fields;  // CPU backend, H.264 field pictures: one per field slot
   } surface;
   std::shared_ptr<FrameRing> ring_;  // written by the worker via set_ring(); read via ring()
   int ring_slots_cfg;
@@ -383,7 +385,7 @@ class Worker {
     size_t err_cap = 0;
   };
   void loop();
-  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps = 1);
+  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps = 1, bool weave = false);
   struct Batch {
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;

@@ -125,6 +125,12 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
       hc.coverage = cfg.coverage;
       hc.noise = cfg.noise;
       hc.temporal_noise = cfg.temporal_noise;
+      hc.interlaced = cfg.interlaced >= 1;
+      if (cfg.interlaced == 2) {
+        hc.fields = true;
+        hc.cabac = hc.t8x8 = false;
+        hc.bframes = hc.weighted_b = 0;
+      }
       avc_ = std::make_unique<avc::AvcHighEncoder>(hc);
     } else {
       VEP_CHECK(cfg.profile == "baseline", "profile must be baseline, main or high");

@@ -52,6 +52,9 @@ struct SynthConfig {
   bool long_term = false;
   bool lossless = false;
   int bit_depth = 8;         // H.265: 10 = Main10 (10-bit samples)
+  // main / high H.264: 1 = interlaced SPS coding frame pictures, 2 = every frame a field pair
+  // (PAFF: CAVLC, 4x4 transforms, no B pictures; overrides cabac / bframes / the 8x8 transform)
+  int interlaced = 0;
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)

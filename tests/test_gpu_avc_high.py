@@ -3,13 +3,15 @@ spatial / temporal direct), 8x8 transform + Intra_8x8, explicit / implicit weigh
 prediction, scaling matrices and multiple slices from the closed-loop High encoder. Every frame
 the GPU worker publishes equals the CPU reference decoder's output and the encoder's own
 reconstruction of that picture, bit-exact, at 176x144 (coverage streams: every MB / sub-MB
-type) and 1080p (realistic IBBP)."""
+type) and 1080p (realistic IBBP); interlaced streams of frame pictures and of field pairs."""
 import numpy as np
 import pytest
 
 from conftest import high_encoder
 
 pytestmark = pytest.mark.gpu
+
+PAFF = dict(interlaced=True, fields=True, cabac=False, t8x8=False, bframes=0)
 
 GPU_CONFIGS = {
     "cov-cabac-spatial": (176, 144, 16, dict(bframes=2, coverage=True)),
@@ -22,6 +24,9 @@ GPU_CONFIGS = {
     # interlaced SPS coding frame pictures (1080i-style: 1088 coded rows in map units of 2 MB rows)
     "interlaced-frames-cov": (176, 144, 12, dict(bframes=2, coverage=True, interlaced=True)),
     "interlaced-1080-ibbp": (1920, 1080, 6, dict(bframes=2, qp=26, interlaced=True)),
+    # field pairs (PAFF): half-height field pictures in field slots, the published frame woven
+    "paff-cov": (176, 144, 24, dict(coverage=True, **PAFF)),
+    "paff-1080-refs2": (1920, 1080, 12, dict(qp=26, refs=2, temporal_noise=2.0, **PAFF)),
 }
 
 
