@@ -21,8 +21,9 @@
 // Reference parity: this is the libavcodec h264 decoder the reference calls through PyAV
 // (python/read_image.py:87 `p.decode()`, :94 `to_ndarray('bgr24')`; SURVEY.md §2.2 N2 and
 // §2.3 K1), including its output order (frames leave in picture-order-count order). Interlaced
-// streams that code frame pictures decode like progressive ones; field pictures (PAFF) / MBAFF
-// frames, 4:2:2 / 4:4:4, high bit depth, lossless, data partitioning,
+// streams that code frame pictures decode like progressive ones; CAVLC I / P field pairs (PAFF)
+// decode as half-height pictures in field slots (Picture::structure). MBAFF frames, CABAC / B /
+// 8x8-transform field pictures, 4:2:2 / 4:4:4, high bit depth, lossless, data partitioning,
 // FMO/ASO, SP/SI slices and CABAC streams with cabac_init_idc 1 or 2 are reported as
 // UnsupportedStream (the VCN backend's job).
 #pragma once
