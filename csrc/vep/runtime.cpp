@@ -1097,7 +1097,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       const avc::Picture& p = *v[size_t(r)];
       VEP_CHECK(p.hmbs <= gpu::kAvcMaxRows && p.wmbs <= gpu::kAvcMaxCols,
                 "picture too large for the wavefront kernels");
-      VEP_CHECK(p.wmbs * 16 == jobs[size_t(i)].pic.coded_width && p.hmbs * 16 == jobs[size_t(i)].pic.coded_height,
+      VEP_CHECK(p.wmbs * 16 == jobs[size_t(i)].pic.coded_width &&
+                    p.hmbs * 16 * (p.structure ? 2 : 1) == jobs[size_t(i)].pic.coded_height,  // (a field: half)
                 "picture size differs from the camera's surfaces");
       AvcPic a{&p, i, 0, 0, 0, 0, 0, 0, 0};
       auto put = [&](const void* src, size_t bytes) {
