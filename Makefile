@@ -7,7 +7,7 @@ HIP_SRCS = $(wildcard csrc/vep/*.hip)
 TSAN_DIR = build/tsan
 ASAN_DIR = build/asan
 
-.PHONY: build test test-gpu bench bench-h265 smoke tsan asan link-check clean
+.PHONY: build test test-gpu bench bench-h265 smoke tsan asan link-check parse-prof clean
 
 build:                     ## compile the extension in-tree (video_edge_ai_proxy_amd/_vep*.so)
 	$(PY) csrc/build.py
@@ -56,6 +56,15 @@ tsan: $(TSAN_DIR)/native_stress
 
 asan: $(ASAN_DIR)/native_stress
 	cd /tmp && ASAN_OPTIONS="detect_leaks=1" $(CURDIR)/$(ASAN_DIR)/native_stress
+
+# Host parse profile (gprof): the general H.264 decoder over the headline bench's 1080p stream.
+build/prof/parse_prof: $(SRCS) $(HIP_SRCS) csrc/tests/parse_prof.cpp $(wildcard csrc/vep/*.h)
+	mkdir -p build/prof
+	$(HIPCC) --offload-arch=$(ARCH) -std=c++17 -O2 -g -Xarch_host -pg -Xarch_host -march=x86-64-v3 \
+	  -Icsrc $(SRCS) csrc/tests/parse_prof.cpp -x hip $(HIP_SRCS) -o $@ -lpthread
+
+parse-prof: build/prof/parse_prof
+	cd /tmp && $(CURDIR)/build/prof/parse_prof 10 && gprof -b -p $(CURDIR)/build/prof/parse_prof /tmp/gmon.out | head -40
 
 clean:
 	rm -rf build video_edge_ai_proxy_amd/_vep*.so

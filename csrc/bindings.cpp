@@ -886,6 +886,22 @@ PYBIND11_MODULE(_vep, m) {
     }
     return std::make_pair(bad_avc, bad_hevc);
   });
+  // Parse-only timing of an access-unit sequence (the host cost per picture; tools/bench).
+  m.def("avc_parse_seconds", [](const std::vector<std::shared_ptr<AccessUnit>>& aus, int reps) {
+    py::gil_scoped_release r;
+    double best = 1e30;
+    for (int k = 0; k < std::max(1, reps); ++k) {
+      avc::Decoder dec;
+      const i64 t0 = mono_us();
+      for (const auto& au : aus) {
+        size_t nal = 0;
+        do dec.parse(*au, 0, &nal);
+        while (nal < au->nals.size());
+      }
+      best = std::min(best, double(mono_us() - t0) * 1e-6);
+    }
+    return best;
+  }, py::arg("aus"), py::arg("reps") = 3);
   m.def("avc_record_stats", [](const std::vector<std::shared_ptr<AccessUnit>>& aus) {
     py::gil_scoped_release r;
     avc::Decoder dec;

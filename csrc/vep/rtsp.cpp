@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <cctype>
+#include <limits>
 #include <sstream>
 
 #include "md5.h"
@@ -628,6 +629,9 @@ void RtspServer::serve(int fd) {
     h.ssrc = 0x5ee0000u ^ u32(fd);
     h.seq = u16(fd * 7919);
     i64 frame = 0;
+    // capture instants: an access unit with the previous one's pts (the second field of a pair)
+    // shares its time slot and RTP timestamp
+    i64 tix = -1, prev_pts = std::numeric_limits<i64>::min();
     i64 pace_t0 = -1, pace_f0 = 0;
     std::vector<u8> out;
     std::vector<std::vector<u8>> pk;
@@ -665,19 +669,21 @@ void RtspServer::serve(int fd) {
         ++frame;
         continue;
       }
+      if (au->pts != prev_pts || tix < 0) ++tix;
+      prev_pts = au->pts;
       const int pace = pace_.load();
       if (pace == 1 || (pace < 0 && st->cfg.realtime)) {
         if (pace_t0 < 0) {  // (re)start pacing from this frame on
           pace_t0 = mono_us();
-          pace_f0 = frame;
+          pace_f0 = tix;
         }
-        i64 due = pace_t0 + (frame - pace_f0) * 1000000 / fps;
+        i64 due = pace_t0 + (tix - pace_f0) * 1000000 / fps;
         i64 now = mono_us();
         if (due > now) std::this_thread::sleep_for(std::chrono::microseconds(due - now));
       } else {
         pace_t0 = -1;
       }
-      h.ts = u32(frame * 90000 / fps);
+      h.ts = u32(tix * 90000 / fps);
       out.clear();
       const bool cached = !enc && fault != int(Fault::kCorruptNal);
       if (cached) {  // cached AU: payloads packetized once

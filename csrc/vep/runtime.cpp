@@ -717,6 +717,7 @@ void merge_job(DecodeJob& p, DecodeJob&& job) {
       p.pic = job.pic;
       p.meta = job.meta;
       p.out_slot = job.out_slot;
+      p.out_fields = job.out_fields;
     }
   } else if (job.refresh || job.general() != p.general() || p.upd.width_mbs != job.upd.width_mbs ||
              p.upd.height_mbs != job.upd.height_mbs) {

@@ -189,3 +189,47 @@ def test_frame_and_field_pictures_mixed_are_unsupported(native):
     p = frames.next()  # a P frame picture, same SPS / PPS ids and syntax
     with pytest.raises(native.UnsupportedStream, match="mixed"):
         dec.decode(p)
+
+
+def test_paff_live_rtsp_camera(native):
+    """A field-pair camera end to end (CPU backend): the loopback farm sends each field as its own
+    access unit, both with the frame's RTP timestamp (paced per frame, not per field); the RTP
+    depacketizer, the lazy decoder (catch-up batches merged into one job) and the runtime publish
+    one frame per pair, equal to the reference decoder's frame for that capture instant."""
+    live_paff_check(native, -1)
+
+
+@pytest.mark.gpu
+def test_paff_live_rtsp_camera_gpu(native):
+    """The same on gfx950 (field slots in the camera's DPB surfaces, launch_weave on output)."""
+    live_paff_check(native, 0)
+
+
+def live_paff_check(native, device):
+    from test_live_compressed import FPS, Live, ref_index
+
+    c = native.SynthConfig()
+    c.width, c.height, c.gop, c.fps, c.seed = 176, 144, 8, FPS, 5
+    c.compressed, c.profile, c.interlaced, c.objects = True, "high", 2, 3
+    n_aus = 16  # 8 frames = one GOP, looped by the farm
+    enc = native.SynthH264(c)
+    aus = [enc.next() for _ in range(n_aus)]
+    step = 90000 // FPS
+    dec, ref = native.CpuDecoder(), {}
+    for k in range(n_aus * 3):  # frame j = AUs 2j, 2j + 1 (RTP time j * step)
+        a = aus[k % n_aus]
+        img = dec.decode(native.AccessUnit.from_nals(a.nals(), pts=(k // 2) * step, dts=k * step, keyframe=a.keyframe))
+        if img is not None:
+            ref[dec.last_pts // step] = img
+    live = Live(native, c, n_aus, device=device)
+    try:
+        got = live.frames(60, max_frames=12)
+        st = live.w.stats(live.cam)
+    finally:
+        live.close()
+    assert st["errors"] == 0 and len(got) >= 12, st
+    for pts, img, meta in got:
+        j = pts // step
+        want = ref.get(ref_index(j, n_aus // 2))
+        assert want is not None and np.array_equal(img, want), f"frame {j}"
+    assert st["packets"] >= 2 * st["decoded"] - 2  # two access units (fields) per decoded frame
