@@ -344,12 +344,11 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
     }
   }
   if (sh.field_pic) {
-    // Field pictures: CAVLC I / P with 4x4 transforms and sliding-window marking. CABAC needs the
-    // field-coded context initialisation values (not in any source this build can pin), the 8x8
-    // transform the 8x8 field scan, B fields the field direct modes, and MMCOs / list
-    // modifications the field picture numbers: those stay with the VCN backend.
+    // Field pictures: CAVLC I / P / B with 4x4 transforms and sliding-window marking. CABAC needs
+    // the field-coded context initialisation values (not in any source this build can pin), the
+    // 8x8 transform the 8x8 field scan, MMCOs / list modifications the field picture numbers:
+    // those stay with the VCN backend.
     if (pps.cabac) throw UnsupportedStream("interlaced H.264: CABAC field pictures are not supported");
-    if (st == h264::kB) throw UnsupportedStream("interlaced H.264: B field pictures are not supported");
     if (pps.transform_8x8_mode) throw UnsupportedStream("interlaced H.264: 8x8 transform in field pictures is not supported");
     if (sh.adaptive_marking || sh.long_term_reference || !sh.ref_mods[0].empty())
       throw UnsupportedStream("interlaced H.264: field MMCOs / long-term / list modifications are not supported");
@@ -590,11 +589,13 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int 
   }
 }
 
-// §8.2.4.2.2 / §8.2.4.2.5: list 0 of a P field. The reference frames (short-term by
-// FrameNumWrap descending, then long-term by index) are taken apart into their fields, alternating
-// parities starting with the current field's; when one parity runs out the other's remaining
-// fields follow in order. The first field of the current frame is a reference frame entry too.
-void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps) {
+// §8.2.4.2.2 / §8.2.4.2.4 / §8.2.4.2.5: the lists of a P or B field. The reference frames
+// (P: short-term by FrameNumWrap descending; B: by POC around the current field's, list 0 the
+// earlier ones first, list 1 the later ones; then long-term by index) are taken apart into their
+// fields, alternating parities starting with the current field's; when one parity runs out the
+// other's remaining fields follow in order. A frame's POC here is the lowest of its reference
+// fields'; the first field of the current frame is a reference frame entry too.
+void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps, int cur_poc) {
   const int max_fn = 1 << sps.log2_max_frame_num;
   list_[0].clear();
   list_[1].clear();
@@ -608,17 +609,15 @@ void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps) {
       st.push_back(&r);
     }
   }
-  std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
   std::sort(lt.begin(), lt.end(), [](RefPic* a, RefPic* b) { return a->lt_idx < b->lt_idx; });
   const int same = sh.bottom_field ? 1 : 0;
-  std::vector<ListEntry> all;
-  auto alternate = [&](const std::vector<RefPic*>& frames) {
+  auto alternate = [&](const std::vector<RefPic*>& frames, std::vector<ListEntry>& all) {
     std::vector<ListEntry> f[2];  // [0] same parity, [1] opposite
     for (RefPic* r : frames)
       for (int k = 0; k < 2; ++k) {
         const int par = k == 0 ? same : 1 - same;
         if ((r->fields >> par) & 1)
-          f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], r->long_term, r->uid_f[par], nullptr});
+          f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], r->long_term, r->uid_f[par], r->col_f[par].get()});
       }
     size_t i[2] = {0, 0};
     for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
@@ -626,16 +625,44 @@ void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps) {
       all.push_back(f[from][i[from]++]);
     }
   };
-  alternate(st);
-  alternate(lt);
-  list_[0].assign(size_t(sh.num_ref_idx[0]), ListEntry{});
-  for (size_t i = 0; i < list_[0].size() && i < all.size(); ++i) list_[0][i] = all[i];
+  std::vector<RefPic*> init[2];
+  if (sh.type() == h264::kP) {
+    std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
+    init[0] = st;
+  } else {
+    std::vector<RefPic*> before, after;
+    for (RefPic* r : st) (r->poc <= cur_poc ? before : after).push_back(r);
+    std::sort(before.begin(), before.end(), [](RefPic* a, RefPic* b) { return a->poc > b->poc; });
+    std::sort(after.begin(), after.end(), [](RefPic* a, RefPic* b) { return a->poc < b->poc; });
+    init[0] = before;
+    init[0].insert(init[0].end(), after.begin(), after.end());
+    init[1] = after;
+    init[1].insert(init[1].end(), before.begin(), before.end());
+  }
+  std::vector<ListEntry> all[2];
+  const int nl = sh.type() == h264::kB ? 2 : 1;
+  for (int l = 0; l < nl; ++l) {
+    alternate(init[l], all[l]);
+    alternate(lt, all[l]);
+  }
+  auto same_entries = [](const std::vector<ListEntry>& a, const std::vector<ListEntry>& b) {
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); ++i)
+      if (a[i].slot != b[i].slot) return false;
+    return true;
+  };
+  if (nl == 2 && all[1].size() > 1 && same_entries(all[0], all[1])) std::swap(all[1][0], all[1][1]);
+  for (int l = 0; l < nl; ++l) {
+    list_[l].assign(size_t(sh.num_ref_idx[l]), ListEntry{});
+    for (size_t i = 0; i < list_[l].size() && i < all[l].size(); ++i) list_[l][i] = all[l][i];
+  }
 }
 
 // Reference marking of a field (sliding window only, see read_slice_header): the first field of a
 // frame enters the DPB as a frame entry holding one field (after the sliding window makes room);
 // the second field joins its frame's entry.
-void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, u32 uid, bool second) {
+void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, u32 uid, bool second,
+                         std::shared_ptr<const ColMotion> col) {
   const int par = sh.bottom_field ? 1 : 0;
   if (second)
     for (auto& r : dpb_)
@@ -643,6 +670,7 @@ void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, 
         r.fields |= u8(1 << par);
         r.poc_f[par] = poc;
         r.uid_f[par] = uid;
+        r.col_f[par] = std::move(col);
         r.poc = std::min(r.poc, poc);
         return;
       }
@@ -669,6 +697,7 @@ void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, 
   cur.fields = u8(1 << par);
   cur.poc_f[par] = poc;
   cur.uid_f[par] = uid;
+  cur.col_f[par] = std::move(col);
   dpb_.push_back(cur);
 }
 
@@ -1320,12 +1349,12 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       } else {
         pic->target = pick_slot();  // (pictures waiting for output keep their slots until bump)
       }
-      if (sh.nal_ref_idc != 0 && sps.profile_idc != 66 && !sh.field_pic) {  // B slices may use this motion
+      if (sh.nal_ref_idc != 0 && sps.profile_idc != 66) {  // B slices may use this motion
         col_built = col_pool_->acquire([](ColMotion&) {});  // (every entry is written below)
         col_built->wmbs = W;
-        col_built->hmbs = H;
+        col_built->hmbs = Hp;
         col_built->corners = sps.direct_8x8;
-        col_built->b.resize(size_t(W) * H * size_t(sps.direct_8x8 ? 4 : 16));
+        col_built->b.resize(size_t(W) * Hp * size_t(sps.direct_8x8 ? 4 : 16));
         colb.col = col_built.get();
         pic->colb = &colb;
       }
@@ -1340,7 +1369,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       }
       if (sh.type() == h264::kB || pic->info.pict_type == 'I') pic->info.pict_type = "PBISi"[sh.type()];
     }
-    if (sh.field_pic) build_field_lists(sh, sps);
+    if (sh.field_pic) build_field_lists(sh, sps, pic->poc);
     else build_lists(sh, sps, pic->poc);
     std::array<std::vector<u32>, 2> uids;
     for (int l = 0; l < 2; ++l)
@@ -1459,7 +1488,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
   pic->info.coded_mbs = pic->nmbs() - missing;
   const u32 uid = next_uid_++;
   if (first.field_pic) {
-    if (first.nal_ref_idc != 0) mark_field(first, *act_sps, pic->target >> 1, pic->poc, uid, second_field && pair_.ref);
+    if (first.nal_ref_idc != 0)
+      mark_field(first, *act_sps, pic->target >> 1, pic->poc, uid, second_field && pair_.ref, std::move(col_built));
     if (second_field) close_pair(*pic);  // the frame is complete
   } else {
     if (first.nal_ref_idc != 0) {

@@ -344,6 +344,7 @@ struct RefPic {
   u8 fields = 3;
   int poc_f[2] = {0, 0};
   u32 uid_f[2] = {0, 0};
+  std::shared_ptr<const ColMotion> col_f[2];  // each field's motion (B fields' direct prediction)
 };
 
 // Per-slice list entry (a RefPic snapshot).
@@ -382,8 +383,9 @@ class Decoder {
     u32 epoch;  // IDR / MMCO5 period the picture belongs to (output order: epoch, then POC)
   };
   void build_lists(const SliceHdr& sh, const h264::Sps& sps, int cur_poc);
-  void build_field_lists(const SliceHdr& sh, const h264::Sps& sps);
-  void mark_field(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid, bool second);
+  void build_field_lists(const SliceHdr& sh, const h264::Sps& sps, int cur_poc);
+  void mark_field(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid, bool second,
+                  std::shared_ptr<const ColMotion> col);
   void mark_references(const SliceHdr& sh, const h264::Sps& sps, int slot, int poc, u32 uid,
                        std::shared_ptr<const ColMotion> col);
   int pick_slot() const;
@@ -596,7 +598,8 @@ struct AvcHighConfig {
   bool interlaced = false;    // interlaced SPS (frame_mbs_only 0) coding frame pictures, with
                               // delta_pic_order_cnt_bottom (top field first)
   bool fields = false;        // (interlaced) code every frame as a field pair (PAFF): top field
-                              // first, I / P or P / P, CAVLC, 4x4 transforms, no B pictures
+                              // first; I / P, P / P anchors and non-reference B / B pairs; CAVLC,
+                              // 4x4 transforms
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;
   u64 seed = 1;

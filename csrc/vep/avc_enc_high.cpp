@@ -114,6 +114,7 @@ struct AvcHighEncoder::Impl {
     u8 fields = 3;
     int poc_f[2] = {0, 0};
     u32 uid_f[2] = {0, 0};
+    std::shared_ptr<const ColMotion> col_f[2];
   };
   std::vector<Ref> dpb;
   struct Job {
@@ -146,8 +147,8 @@ struct AvcHighEncoder::Impl {
               "encoder size must be even and >= 16");
     VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.refs >= 1 && c.refs <= 8, "bframes 0..4, refs 1..8");
     VEP_CHECK(c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
-    VEP_CHECK(!c.fields || (c.interlaced && !c.cabac && !c.t8x8 && c.bframes == 0 && c.weighted_b == 0),
-              "field coding: interlaced CAVLC I / P with 4x4 transforms only");
+    VEP_CHECK(!c.fields || (c.interlaced && !c.cabac && !c.t8x8),
+              "field coding: interlaced CAVLC with 4x4 transforms only");
     fields = c.fields;
     W = (c.width + 15) / 16;
     H = (c.height + 15) / 16;
@@ -160,7 +161,7 @@ struct AvcHighEncoder::Impl {
     sps.log2_max_frame_num = 16;
     sps.poc_type = 0;
     sps.log2_max_poc_lsb = 16;
-    const int pyr = c.pyramid && c.bframes >= 2 ? 1 : 0;
+    const int pyr = c.pyramid && c.bframes >= 2 && !c.fields ? 1 : 0;  // (field pairs: B non-reference)
     sps.max_num_ref_frames = std::max(c.refs, c.bframes > 0 ? 2 : 1) + pyr;
     sps.width_mbs = W;
     sps.frame_mbs_only = !c.interlaced;
@@ -215,12 +216,25 @@ struct AvcHighEncoder::Impl {
   }
 
   void plan_next() {
-    if (fields) {  // every frame a field pair: I / P (IDR frames) or P / P, both references
-      const bool idr = is_idr_pos(next_disp);
-      if (idr) gop_start = next_disp;
-      plan.push_back({next_disp, idr ? h264::kI : h264::kP, true, idr, 0});
-      plan.push_back({next_disp, h264::kP, true, false, 1});
-      ++next_disp;
+    if (fields) {  // every frame a field pair: I / P (IDR frames), P / P anchors, non-reference
+                   // B / B pairs between them (coding order: the anchor pair, then the B pairs)
+      if (is_idr_pos(next_disp)) {
+        gop_start = next_disp;
+        plan.push_back({next_disp, h264::kI, true, true, 0});
+        plan.push_back({next_disp, h264::kP, true, false, 1});
+        ++next_disp;
+        return;
+      }
+      i64 next_idr = next_disp + 1;
+      while (!is_idr_pos(next_idr)) ++next_idr;
+      const i64 anchor = std::min<i64>(next_disp + cfg.bframes, next_idr - 1);
+      plan.push_back({anchor, h264::kP, true, false, 0});
+      plan.push_back({anchor, h264::kP, true, false, 1});
+      for (i64 d = next_disp; d < anchor; ++d) {
+        plan.push_back({d, h264::kB, false, false, 0});
+        plan.push_back({d, h264::kB, false, false, 1});
+      }
+      next_disp = anchor + 1;
       return;
     }
     if (is_idr_pos(next_disp)) {
@@ -271,30 +285,55 @@ struct AvcHighEncoder::Impl {
     }
   }
 
-  // List 0 of a P field: the decoder's field list initialisation (Decoder::build_field_lists):
-  // reference frames by FrameNumWrap descending, split into fields alternating from the current
-  // parity.
-  void build_field_lists(const SliceHdr& sh, std::vector<ListEntry>* lists) {
+  // Lists of a P / B field: the decoder's field list initialisation (Decoder::build_field_lists):
+  // reference frames (P: FrameNumWrap descending; B: by POC around the current field's, a frame's
+  // POC the lowest of its fields'), split into fields alternating from the current parity.
+  void build_field_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* lists) {
     lists[0].clear();
     lists[1].clear();
     if (sh.type() == h264::kI) return;
     std::vector<const Ref*> st;
     for (const Ref& r : dpb) st.push_back(&r);
-    auto wrap = [&](const Ref* r) { return r->frame_num > sh.frame_num ? r->frame_num - max_fn : r->frame_num; };
-    std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap(a) > wrap(b); });
-    const int same = sh.bottom_field ? 1 : 0;
-    std::vector<ListEntry> f[2];
-    for (const Ref* r : st)
-      for (int k = 0; k < 2; ++k) {
-        const int par = k == 0 ? same : 1 - same;
-        if ((r->fields >> par) & 1) f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], false, r->uid_f[par], nullptr});
-      }
-    size_t i[2] = {0, 0};
-    for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
-      const int from = i[k] < f[k].size() ? k : k ^ 1;
-      if (int(lists[0].size()) < sh.num_ref_idx[0]) lists[0].push_back(f[from][i[from]]);
-      ++i[from];
+    auto fpoc = [](const Ref* r) { return (r->fields & 1) ? ((r->fields & 2) ? std::min(r->poc_f[0], r->poc_f[1]) : r->poc_f[0]) : r->poc_f[1]; };
+    std::vector<const Ref*> init[2];
+    if (sh.type() == h264::kP) {
+      auto wrap = [&](const Ref* r) { return r->frame_num > sh.frame_num ? r->frame_num - max_fn : r->frame_num; };
+      std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap(a) > wrap(b); });
+      init[0] = st;
+    } else {
+      std::vector<const Ref*> before, after;
+      for (const Ref* r : st) (fpoc(r) <= cur_poc ? before : after).push_back(r);
+      std::sort(before.begin(), before.end(), [&](const Ref* a, const Ref* b) { return fpoc(a) > fpoc(b); });
+      std::sort(after.begin(), after.end(), [&](const Ref* a, const Ref* b) { return fpoc(a) < fpoc(b); });
+      init[0] = before;
+      init[0].insert(init[0].end(), after.begin(), after.end());
+      init[1] = after;
+      init[1].insert(init[1].end(), before.begin(), before.end());
     }
+    const int same = sh.bottom_field ? 1 : 0;
+    std::vector<ListEntry> all[2];
+    const int nl = sh.type() == h264::kB ? 2 : 1;
+    for (int l = 0; l < nl; ++l) {
+      std::vector<ListEntry> f[2];
+      for (const Ref* r : init[l])
+        for (int k = 0; k < 2; ++k) {
+          const int par = k == 0 ? same : 1 - same;
+          if ((r->fields >> par) & 1)
+            f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], false, r->uid_f[par], r->col_f[par].get()});
+        }
+      size_t i[2] = {0, 0};
+      for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
+        const int from = i[k] < f[k].size() ? k : k ^ 1;
+        all[l].push_back(f[from][i[from]++]);
+      }
+    }
+    if (nl == 2 && all[1].size() > 1) {
+      bool same_lists = all[0].size() == all[1].size();
+      for (size_t k = 0; same_lists && k < all[0].size(); ++k) same_lists = all[0][k].slot == all[1][k].slot;
+      if (same_lists) std::swap(all[1][0], all[1][1]);
+    }
+    for (int l = 0; l < nl; ++l)
+      for (int k = 0; k < sh.num_ref_idx[l] && k < int(all[l].size()); ++k) lists[l].push_back(all[l][size_t(k)]);
   }
 
   int pick_slot() const {
@@ -494,7 +533,8 @@ struct AvcHighEncoder::Impl {
       l1 |= r1[k] >= 0;
       if (weighted) wp[k] = wp_entry(env, r0[k], r1[k]);
     }
-    predict_inter(slots, m, &mv[0][0][0], l1 ? &mv[1][0][0] : nullptr, weighted ? wp : nullptr, mb % W, mb / W, py, pc);
+    predict_inter(slots, m, &mv[0][0][0], l1 ? &mv[1][0][0] : nullptr, weighted ? wp : nullptr, mb % W, mb / W, py, pc,
+                  pic.structure);
   }
 
   // 16x16 motion search in one list for reference r: candidates (zero, predictor, the scene's
@@ -777,7 +817,19 @@ struct AvcHighEncoder::Impl {
       for (const Ref& r : dpb) nf += (r.fields & 1) + (r.fields >> 1);
       n0 = std::min(2 * cfg.refs, nf);
     }
-    if (job.type == h264::kB) {
+    if (job.type == h264::kB && fld) {  // reference fields on both sides (every one in list 0)
+      int before = 0, after = 0, nf = 0;
+      for (const Ref& r : dpb)
+        for (int par = 0; par < 2; ++par)
+          if ((r.fields >> par) & 1) {
+            ++nf;
+            (r.poc_f[par] < poc ? before : after) += 1;
+          }
+      n0 = nf;
+      n1 = std::min<int>(cfg.coverage ? 2 : 1, nf);
+      VEP_CHECK(before > 0 && after > 0, "B field without reference fields on both sides");
+    }
+    if (job.type == h264::kB && !fld) {
       int before = 0, after = 0;
       for (const Ref& r : dpb) (r.poc < poc ? before : after) += 1;
       // every reference in list 0: temporal direct needs the colocated picture's references
@@ -818,6 +870,10 @@ struct AvcHighEncoder::Impl {
     pic.dpb_slots = int(slots.size());
     pic.structure = fld ? 1 + job.parity : 0;
     pic.target = fld ? 2 * (job.parity == 1 ? pair_slot : pick_slot()) + job.parity : pick_slot();
+    if (job.parity == 0) {  // the pair's frame_num and frame slot, for its second field
+      pair_fn = sh.frame_num;
+      pair_slot = pic.target >> 1;
+    }
     pic.idr = idr;
     pic.poc = poc;
     nb.reset(W, Hp);
@@ -842,7 +898,7 @@ struct AvcHighEncoder::Impl {
     for (int si = 0; si < nslices; ++si) {
       const int row0 = si * Hp / nslices, row1 = (si + 1) * Hp / nslices;
       sh.first_mb = row0 * W;
-      if (fld) build_field_lists(sh, lists);
+      if (fld) build_field_lists(sh, poc, lists);
       else build_lists(sh, poc, lists);
       std::array<std::vector<u32>, 2> uids;
       for (int l = 0; l < 2; ++l)
@@ -884,6 +940,7 @@ struct AvcHighEncoder::Impl {
             r.fields |= 2;
             r.poc_f[1] = poc;
             r.uid_f[1] = next_uid;
+            r.col_f[1] = build_col_motion(nb, W, Hp, slice_uids, sps.direct_8x8);
             joined = true;
           }
       if (!joined) {
@@ -898,10 +955,9 @@ struct AvcHighEncoder::Impl {
         r.fields = u8(1 << par);
         r.poc_f[par] = poc;
         r.uid_f[par] = next_uid;
+        r.col_f[par] = build_col_motion(nb, W, Hp, slice_uids, sps.direct_8x8);
         dpb.push_back(r);
         prev_ref_fn = sh.frame_num;
-        pair_fn = sh.frame_num;
-        pair_slot = fs;
       }
     } else if (job.ref) {
       Ref r{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)};

@@ -129,7 +129,6 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
       if (cfg.interlaced == 2) {
         hc.fields = true;
         hc.cabac = hc.t8x8 = false;
-        hc.bframes = hc.weighted_b = 0;
       }
       avc_ = std::make_unique<avc::AvcHighEncoder>(hc);
     } else {

@@ -53,7 +53,7 @@ struct SynthConfig {
   bool lossless = false;
   int bit_depth = 8;         // H.265: 10 = Main10 (10-bit samples)
   // main / high H.264: 1 = interlaced SPS coding frame pictures, 2 = every frame a field pair
-  // (PAFF: CAVLC, 4x4 transforms, no B pictures; overrides cabac / bframes / the 8x8 transform)
+  // (PAFF: CAVLC, 4x4 transforms, B pairs non-reference; overrides cabac / the 8x8 transform)
   int interlaced = 0;
 };
 

@@ -10,9 +10,12 @@ picture, all exercised here by the closed-loop encoder (`AvcHighConfig.fields`):
   with the current one (§8.2.4.2.5), the first field of the current frame included;
 * chroma vectors into the opposite-parity field offset by a quarter sample (Table 8-10);
 * deblocking: horizontal intra MB edges get bS 3, vertical vector threshold 2 (§8.7.2.1);
-* sliding-window marking on frames (a field pair is one frame of the DPB).
+* sliding-window marking on frames (a field pair is one frame of the DPB);
+* B fields: lists by POC around the current field's (a frame's POC the lowest of its reference
+  fields'), alternated by parity (§8.2.4.2.4 / §8.2.4.2.5); spatial and temporal direct from the
+  colocated field (RefPicList1[0], its own motion table), implicit weights from field POCs.
 
-Coverage is CAVLC I / P fields with 4x4 transforms (the VCN backend's job otherwise): CABAC field
+Coverage is CAVLC I / P / B fields with 4x4 transforms (the VCN backend's job otherwise): CABAC field
 pictures need the field-coded context tables (ctxIdx 277..398 / 436..459), which no source in
 this image holds (parity unpinned), and are reported as UnsupportedStream, as are streams mixing
 frame and field pictures between IDRs. The encoder and decoder share the macroblock layer, so the
@@ -25,6 +28,7 @@ import pytest
 from conftest import high_encoder, roundtrip
 
 PAFF = dict(interlaced=True, fields=True, cabac=False, t8x8=False, bframes=0)
+PAFF_B = dict(PAFF, bframes=2)
 
 
 def paff_encoder(native, w=176, h=144, **kw):
@@ -45,6 +49,25 @@ def test_paff_closed_loop_bit_exact(native, kw):
         assert np.array_equal(rec[pts][0], got[pts][0]) and np.array_equal(rec[pts][1], got[pts][1]), pts
     assert dec.pictures_decoded == 24  # one decoded picture per field
     assert dec.info["coded_height"] == 160 and dec.info["height"] == 144
+
+
+@pytest.mark.parametrize("kw", [dict(bframes=1), dict(bframes=2, weighted_b=2), dict(bframes=2, direct_spatial=False),
+                                dict(bframes=3, coverage=True), dict(bframes=2, weighted_b=1, refs=2, coverage=True),
+                                dict(bframes=2, slices=2, direct_spatial=False, coverage=True)],
+                         ids=["ibp", "ibbp-implicit", "ibbp-temporal", "cov-b3", "cov-explicit-refs2",
+                              "cov-temporal-slices"])
+def test_paff_b_fields_closed_loop(native, kw):
+    """Non-reference B field pairs between I / P anchor pairs: the decoder's B-field lists, direct
+    modes and implicit weights against the encoder's (every MB / sub-MB type in coverage mode)."""
+    cfg = dict(PAFF)
+    cfg.update(kw)
+    enc = high_encoder(native, 176, 144, gop=9, seed=3, **cfg)
+    rec, got, dec, aus = roundtrip(native, enc, 36)
+    assert len(rec) == 18 and set(got) == set(rec)
+    for pts in rec:
+        assert np.array_equal(rec[pts][0], got[pts][0]) and np.array_equal(rec[pts][1], got[pts][1]), pts
+    st = dec.mb_stats
+    assert "B" in st["types"] and st["bipred"] > 0 and st["list1_only"] > 0
 
 
 def test_paff_output_per_pair_and_quality(native):
