@@ -202,7 +202,8 @@ def describe_streams(a, compressed):
     if compressed and a.profile == "baseline":
         return "Baseline CAVLC I/P"
     if compressed and a.interlaced == 2:
-        return f"{a.profile.capitalize()} profile interlaced, every frame a field pair (PAFF), CAVLC I/P fields"
+        return (f"{a.profile.capitalize()} profile interlaced, every frame a field pair (PAFF), CAVLC "
+                f"I/P{'/B' if a.bframes else ''} fields{f', {a.bframes} B pairs per mini-GOP' if a.bframes else ''}")
     if compressed:
         return (f"{a.profile.capitalize()} profile {'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
                 f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"

@@ -351,6 +351,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("coverage", &avc::AvcHighConfig::coverage)
       .def_readwrite("interlaced", &avc::AvcHighConfig::interlaced)
       .def_readwrite("fields", &avc::AvcHighConfig::fields)
+      .def_readwrite("marking", &avc::AvcHighConfig::marking)
       .def_readwrite("objects", &avc::AvcHighConfig::objects)
       .def_readwrite("noise", &avc::AvcHighConfig::noise)
       .def_readwrite("temporal_noise", &avc::AvcHighConfig::temporal_noise)
@@ -575,6 +576,13 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("info", [](const CpuDecoder& d) { return pic_dict(d.last); })
       .def_property_readonly("coded_mbs", [](const CpuDecoder& d) { return d.coded; })
       .def_property_readonly("pictures_decoded", [](const CpuDecoder& d) { return d.pictures.size(); })
+      .def_property_readonly("marking_stats", [](const CpuDecoder& d) {
+        py::dict s;
+        for (int k = 1; k <= 6; ++k) s[py::str("mmco" + std::to_string(k))] = d.avc.mmco_ops[k];
+        s["list_mods"] = d.avc.list_mods;
+        s["long_term_marked"] = d.avc.long_term_marked;
+        return s;
+      })
       .def_property_readonly("general", [](const CpuDecoder& d) { return d.general; })
       .def_property_readonly("parallel_slices", [](const CpuDecoder& d) { return d.avc.parallel_slices_run(); })
       .def("surface", [](const CpuDecoder& d) {

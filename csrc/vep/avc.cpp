@@ -484,6 +484,7 @@ void Decoder::build_lists(const SliceHdr& sh, const Sps& sps, int cur_poc) {
           if (r->lt_idx == m.val) pick = r;
       }
       if (!pick) throw Error("vep: reference list modification names a missing picture");
+      ++list_mods;
       list.insert(list.begin() + long(std::min(idx, list.size())), pick);
       for (size_t k = idx + 1; k < list.size(); ++k)
         if (list[k] == pick) {
@@ -516,6 +517,7 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int 
       cur.long_term = true;
       cur.lt_idx = 0;
       max_lt_idx_ = 0;
+      ++long_term_marked;
     } else {
       max_lt_idx_ = -1;
     }
@@ -528,6 +530,7 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int 
   int cur_lt = 0;
   if (sh.adaptive_marking) {
     for (const auto& m : sh.mmcos) {
+      ++mmco_ops[m.op];
       switch (m.op) {
         case 1: {
           const int pn = sh.frame_num - (m.a + 1);
@@ -578,6 +581,7 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int 
   cur.frame_num = mmco5 ? 0 : sh.frame_num;
   if (mmco5) cur.poc = 0;
   cur.long_term = cur_long;
+  long_term_marked += cur_long ? 1 : 0;
   cur.lt_idx = cur_lt;
   dpb_.push_back(cur);
   while (int(dpb_.size()) > max_refs) {  // non-conforming stream: drop the oldest short-term

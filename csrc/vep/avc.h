@@ -451,6 +451,10 @@ class Decoder {
   Decoder();
   ~Decoder();
   u64 parallel_slices_run() const { return parallel_slices_run_; }  // (tests)
+  // reference-marking coverage (tests): MMCOs executed by operation, list modification commands
+  // applied, pictures marked long-term
+  u64 mmco_ops[7] = {0, 0, 0, 0, 0, 0, 0};
+  u64 list_mods = 0, long_term_marked = 0;
 };
 
 // CPU reference reconstruction of `pic` into DPB surfaces `slots` (coded size; references are
@@ -597,6 +601,9 @@ struct AvcHighConfig {
   bool coverage = false;      // randomised decisions: every MB / sub-MB type, mode, transform
   bool interlaced = false;    // interlaced SPS (frame_mbs_only 0) coding frame pictures, with
                               // delta_pic_order_cnt_bottom (top field first)
+  // Reference marking coverage (frame pictures): random ref_pic_list_modification commands
+  // (short- and long-term), MMCO 1 / 2 / 3 / 4 / 6 and IDR long_term_reference_flag.
+  bool marking = false;
   bool fields = false;        // (interlaced) code every frame as a field pair (PAFF): top field
                               // first; I / P, P / P anchors and non-reference B / B pairs; CAVLC,
                               // 4x4 transforms

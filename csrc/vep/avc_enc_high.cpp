@@ -115,7 +115,10 @@ struct AvcHighEncoder::Impl {
     int poc_f[2] = {0, 0};
     u32 uid_f[2] = {0, 0};
     std::shared_ptr<const ColMotion> col_f[2];
+    bool long_term = false;  // (frame pictures, cfg.marking)
+    int lt_idx = 0;
   };
+  int max_lt_idx = -1;  // MaxLongTermFrameIdx (-1: no long-term frame indices)
   std::vector<Ref> dpb;
   struct Job {
     i64 disp;
@@ -257,14 +260,20 @@ struct AvcHighEncoder::Impl {
   }
 
   // ---------------------------------------------------------------- reference lists
-  void build_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* lists) {
-    std::vector<const Ref*> st;
-    for (const Ref& r : dpb) st.push_back(&r);
-    std::vector<const Ref*> init[2];
+  int wrap_of(const Ref& r, int frame_num) const { return r.frame_num > frame_num ? r.frame_num - max_fn : r.frame_num; }
+
+  // Initial lists of a frame picture (§8.2.4.2.1 / §8.2.4.2.3): short-term (P: FrameNumWrap
+  // descending; B: by POC around the current one), then long-term by LongTermFrameIdx.
+  void init_lists(const SliceHdr& sh, int cur_poc, std::vector<const Ref*>* init) const {
+    std::vector<const Ref*> st, lt;
+    for (const Ref& r : dpb) (r.long_term ? lt : st).push_back(&r);
+    std::sort(lt.begin(), lt.end(), [](const Ref* a, const Ref* b) { return a->lt_idx < b->lt_idx; });
+    init[0].clear();
+    init[1].clear();
     if (sh.type() == h264::kP) {
-      auto wrap = [&](const Ref* r) { return r->frame_num > sh.frame_num ? r->frame_num - max_fn : r->frame_num; };
-      std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap(a) > wrap(b); });
+      std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap_of(*a, sh.frame_num) > wrap_of(*b, sh.frame_num); });
       init[0] = st;
+      init[0].insert(init[0].end(), lt.begin(), lt.end());
     } else if (sh.type() == h264::kB) {
       std::vector<const Ref*> before, after;
       for (const Ref* r : st) (r->poc < cur_poc ? before : after).push_back(r);
@@ -272,17 +281,196 @@ struct AvcHighEncoder::Impl {
       std::sort(after.begin(), after.end(), [](const Ref* a, const Ref* b) { return a->poc < b->poc; });
       init[0] = before;
       init[0].insert(init[0].end(), after.begin(), after.end());
+      init[0].insert(init[0].end(), lt.begin(), lt.end());
       init[1] = after;
       init[1].insert(init[1].end(), before.begin(), before.end());
+      init[1].insert(init[1].end(), lt.begin(), lt.end());
       if (init[1].size() > 1 && init[1] == init[0]) std::swap(init[1][0], init[1][1]);
     }
+  }
+
+  // ref_pic_list_modification (cfg.marking): up to two random pictures of the initial list moved
+  // to the front, coded relative to picNumPred (short-term) or by LongTermPicNum.
+  void choose_mods(SliceHdr& sh, int cur_poc) {
+    std::vector<const Ref*> init[2];
+    init_lists(sh, cur_poc, init);
+    for (int l = 0; l < (sh.type() == h264::kB ? 2 : 1); ++l) {
+      sh.ref_mods[l].clear();
+      if (init[l].size() < 2 || rng.uni(100) >= 40) continue;
+      int pred = sh.frame_num;  // picNumLXPred (CurrPicNum)
+      const int n = 1 + rng.uni(2);
+      const Ref* last = nullptr;
+      for (int k = 0; k < n; ++k) {
+        const Ref* r = init[l][size_t(rng.uni(int(init[l].size())))];
+        if (r == last) continue;
+        last = r;
+        if (r->long_term) {
+          sh.ref_mods[l].push_back({2, r->lt_idx});
+          continue;
+        }
+        const int pic_num = wrap_of(*r, sh.frame_num);
+        const int nowrap = pic_num < 0 ? pic_num + max_fn : pic_num;
+        if (nowrap == pred) continue;  // (abs_diff_pic_num 0 is not codable)
+        sh.ref_mods[l].push_back({nowrap < pred ? 0 : 1, std::abs(nowrap - pred) - 1});
+        pred = nowrap;
+      }
+    }
+  }
+
+  // The modifications applied (§8.2.4.3): each named picture inserted at the next index, its
+  // later occurrence removed.
+  void apply_mods(const SliceHdr& sh, int l, std::vector<const Ref*>& list) const {
+    int pred = sh.frame_num;
+    size_t idx = 0;
+    for (const auto& m : sh.ref_mods[l]) {
+      const Ref* pick = nullptr;
+      if (m.idc < 2) {
+        int nw = m.idc == 0 ? pred - (m.val + 1) : pred + (m.val + 1);
+        if (nw < 0) nw += max_fn;
+        if (nw >= max_fn) nw -= max_fn;
+        pred = nw;
+        const int pic_num = nw > sh.frame_num ? nw - max_fn : nw;
+        for (const Ref& r : dpb)
+          if (!r.long_term && wrap_of(r, sh.frame_num) == pic_num) pick = &r;
+      } else {
+        for (const Ref& r : dpb)
+          if (r.long_term && r.lt_idx == m.val) pick = &r;
+      }
+      VEP_CHECK(pick != nullptr, "encoder: list modification names a missing picture");
+      list.insert(list.begin() + long(std::min(idx, list.size())), pick);
+      for (size_t k = idx + 1; k < list.size(); ++k)
+        if (list[k] == pick) {
+          list.erase(list.begin() + long(k));
+          break;
+        }
+      ++idx;
+    }
+  }
+
+  void build_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* lists) {
+    std::vector<const Ref*> init[2];
+    init_lists(sh, cur_poc, init);
     for (int l = 0; l < 2; ++l) {
+      apply_mods(sh, l, init[l]);
       lists[l].clear();
       for (int i = 0; i < sh.num_ref_idx[l] && i < int(init[l].size()); ++i) {
         const Ref& r = *init[l][size_t(i)];
-        lists[l].push_back(ListEntry{r.slot, r.poc, false, r.uid, r.col.get()});
+        lists[l].push_back(ListEntry{r.slot, r.poc, r.long_term, r.uid, r.col.get()});
       }
     }
+  }
+
+  // MMCOs of a reference frame picture (cfg.marking): a full DPB frees a frame (MMCO 1 or 2);
+  // then at random MMCO 4 (MaxLongTermFrameIdx), 6 (this picture long-term), 3 (a short-term
+  // picture long-term), 2 / 1 (a long-term / short-term picture unused). With B pictures the two
+  // newest pictures (the anchors the next B pictures predict from) are left as they are.
+  void choose_mmcos(SliceHdr& sh, bool anchor_with_bs) {
+    sh.mmcos.clear();
+    std::vector<const Ref*> all;
+    for (const Ref& r : dpb) all.push_back(&r);
+    std::sort(all.begin(), all.end(), [&](const Ref* a, const Ref* b) { return wrap_of(*a, sh.frame_num) < wrap_of(*b, sh.frame_num); });
+    const size_t keep = std::min(all.size(), size_t(cfg.bframes > 0 ? 2 : 0));  // newest pictures kept
+    int kept_lt = -1;  // highest LongTermFrameIdx among the kept pictures
+    u32 kept_mask = 0;  // their indices (not reassigned: MMCO 3 / 6 would drop the kept picture)
+    for (size_t k = all.size() - keep; k < all.size(); ++k)
+      if (all[k]->long_term) {
+        kept_lt = std::max(kept_lt, all[k]->lt_idx);
+        kept_mask |= 1u << all[k]->lt_idx;
+      }
+    auto free_idx = [&](int max_idx) {  // a random LongTermFrameIdx <= max_idx not kept, or -1
+      std::vector<int> c;
+      for (int i = 0; i <= max_idx; ++i)
+        if (!((kept_mask >> i) & 1)) c.push_back(i);
+      return c.empty() ? -1 : c[size_t(rng.uni(int(c.size())))];
+    };
+    std::vector<const Ref*> lt, free_st;
+    for (size_t k = 0; k + keep < all.size(); ++k) (all[k]->long_term ? lt : free_st).push_back(all[k]);
+    auto op1 = [&](const Ref* r) { sh.mmcos.push_back({1, sh.frame_num - wrap_of(*r, sh.frame_num) - 1, 0}); };
+    int n_frames = int(dpb.size());
+    if (n_frames >= std::max(1, sps.max_num_ref_frames)) {  // room for this picture
+      if (!free_st.empty()) {
+        op1(free_st.front());
+        free_st.erase(free_st.begin());
+      } else if (!lt.empty()) {
+        sh.mmcos.push_back({2, lt.front()->lt_idx, 0});
+        lt.erase(lt.begin());
+      } else {
+        return;  // (sliding window instead)
+      }
+      --n_frames;
+    }
+    const int r = rng.uni(100);
+    int max_lt = max_lt_idx;
+    if (r < 20) {
+      max_lt = std::max(kept_lt, rng.uni(3) - 1);  // max_long_term_frame_idx_plus1 0..2
+      sh.mmcos.push_back({4, max_lt + 1, 0});
+      std::vector<const Ref*> kept;
+      for (const Ref* x : lt)
+        if (x->lt_idx <= max_lt) kept.push_back(x);
+      lt = kept;
+    } else if (r < 40 && free_idx(max_lt) >= 0 && !anchor_with_bs) {
+      sh.mmcos.push_back({6, free_idx(max_lt), 0});
+    } else if (r < 60 && free_idx(max_lt) >= 0 && !free_st.empty()) {
+      const Ref* x = free_st[size_t(rng.uni(int(free_st.size())))];
+      sh.mmcos.push_back({3, sh.frame_num - wrap_of(*x, sh.frame_num) - 1, free_idx(max_lt)});
+    } else if (r < 75 && !lt.empty()) {
+      sh.mmcos.push_back({2, lt[size_t(rng.uni(int(lt.size())))]->lt_idx, 0});
+    } else if (r < 90 && !free_st.empty()) {
+      op1(free_st[size_t(rng.uni(int(free_st.size())))]);
+    }
+    if (!sh.mmcos.empty()) sh.adaptive_marking = true;
+  }
+
+  // Marking of the current reference frame picture (the decoder's mark_references): MMCOs in
+  // order, else the sliding window; returns the entry's long-term state.
+  void mark_frame(const SliceHdr& sh, Ref cur) {
+    auto erase_if = [&](auto pred) { dpb.erase(std::remove_if(dpb.begin(), dpb.end(), pred), dpb.end()); };
+    if (sh.idr()) {
+      dpb.clear();
+      max_lt_idx = sh.long_term_reference ? 0 : -1;
+      cur.long_term = sh.long_term_reference;
+      cur.lt_idx = 0;
+      dpb.push_back(cur);
+      return;
+    }
+    if (sh.adaptive_marking) {
+      for (const auto& m : sh.mmcos) {
+        switch (m.op) {
+          case 1: erase_if([&](const Ref& r) { return !r.long_term && wrap_of(r, sh.frame_num) == sh.frame_num - (m.a + 1); }); break;
+          case 2: erase_if([&](const Ref& r) { return r.long_term && r.lt_idx == m.a; }); break;
+          case 3:
+            erase_if([&](const Ref& r) { return r.long_term && r.lt_idx == m.b; });
+            for (Ref& r : dpb)
+              if (!r.long_term && wrap_of(r, sh.frame_num) == sh.frame_num - (m.a + 1)) {
+                r.long_term = true;
+                r.lt_idx = m.b;
+              }
+            break;
+          case 4:
+            max_lt_idx = m.a - 1;
+            erase_if([&](const Ref& r) { return r.long_term && r.lt_idx > max_lt_idx; });
+            break;
+          case 6:
+            erase_if([&](const Ref& r) { return r.long_term && r.lt_idx == m.a; });
+            cur.long_term = true;
+            cur.lt_idx = m.a;
+            break;
+          default: break;
+        }
+      }
+    } else if (int(dpb.size()) >= std::max(1, sps.max_num_ref_frames)) {  // sliding window (§8.2.5.3)
+      int n_short = 0;
+      for (const Ref& r : dpb) n_short += !r.long_term;
+      if (n_short > 0) {
+        auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
+          if (a.long_term != b.long_term) return !a.long_term;
+          return wrap_of(a, sh.frame_num) < wrap_of(b, sh.frame_num);
+        });
+        dpb.erase(it);
+      }
+    }
+    dpb.push_back(cur);
+    VEP_CHECK(int(dpb.size()) <= std::max(1, sps.max_num_ref_frames), "encoder: DPB overflow after marking");
   }
 
   // Lists of a P / B field: the decoder's field list initialisation (Decoder::build_field_lists):
@@ -374,8 +562,15 @@ struct AvcHighEncoder::Impl {
       bw.u1(1);  // num_ref_idx_active_override_flag
       bw.ue(u32(sh.num_ref_idx[0] - 1));
       if (st == h264::kB) bw.ue(u32(sh.num_ref_idx[1] - 1));
-      bw.u1(0);  // ref_pic_list_modification_flag_l0
-      if (st == h264::kB) bw.u1(0);
+      for (int l = 0; l < (st == h264::kB ? 2 : 1); ++l) {  // ref_pic_list_modification()
+        bw.u1(!sh.ref_mods[l].empty());
+        if (sh.ref_mods[l].empty()) continue;
+        for (const auto& m : sh.ref_mods[l]) {
+          bw.ue(u32(m.idc));
+          bw.ue(u32(m.val));
+        }
+        bw.ue(3);
+      }
     }
     if (sh.explicit_wp) {
       bw.ue(u32(sh.luma_lwd));
@@ -397,12 +592,23 @@ struct AvcHighEncoder::Impl {
             }
         }
     }
-    if (sh.nal_ref_idc != 0) {
+    if (sh.nal_ref_idc != 0) {  // dec_ref_pic_marking()
       if (sh.idr()) {
         bw.u1(0);
-        bw.u1(0);
+        bw.u1(sh.long_term_reference);
       } else {
-        bw.u1(0);  // sliding window
+        bw.u1(sh.adaptive_marking);
+        if (sh.adaptive_marking) {
+          for (const auto& m : sh.mmcos) {
+            bw.ue(u32(m.op));
+            if (m.op == 1 || m.op == 3) bw.ue(u32(m.a));
+            if (m.op == 2) bw.ue(u32(m.a));
+            if (m.op == 3) bw.ue(u32(m.b));
+            if (m.op == 6) bw.ue(u32(m.a));
+            if (m.op == 4) bw.ue(u32(m.a));
+          }
+          bw.ue(0);
+        }
       }
     }
     if (pps.cabac && st != h264::kI) bw.ue(0);  // cabac_init_idc
@@ -855,6 +1061,14 @@ struct AvcHighEncoder::Impl {
         }
       }
     }
+    if (cfg.marking && !fld) {  // reference marking / list modification coverage
+      if (idr) {
+        sh.long_term_reference = rng.uni(100) < 30;
+      } else {
+        if (job.type != h264::kI) choose_mods(sh, poc);
+        if (job.ref) choose_mmcos(sh, job.type == h264::kP && cfg.bframes > 0);
+      }
+    }
     sh.cabac_init_idc = 0;
     sh.qp = std::clamp(cfg.qp + (job.type == h264::kB ? (job.ref ? 1 : 2) : 0), 0, 51);
     sh.disable_deblocking = cfg.deblock_idc;
@@ -960,15 +1174,7 @@ struct AvcHighEncoder::Impl {
         prev_ref_fn = sh.frame_num;
       }
     } else if (job.ref) {
-      Ref r{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)};
-      if (int(dpb.size()) >= sps.max_num_ref_frames) {  // sliding window (§8.2.5.3)
-        auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
-          auto wrap = [&](const Ref& x) { return x.frame_num > sh.frame_num ? x.frame_num - max_fn : x.frame_num; };
-          return wrap(a) < wrap(b);
-        });
-        dpb.erase(it);
-      }
-      dpb.push_back(r);
+      mark_frame(sh, Ref{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)});
       prev_ref_fn = sh.frame_num;
     }
     ++next_uid;

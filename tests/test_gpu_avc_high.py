@@ -24,6 +24,9 @@ GPU_CONFIGS = {
     # interlaced SPS coding frame pictures (1080i-style: 1088 coded rows in map units of 2 MB rows)
     "interlaced-frames-cov": (176, 144, 12, dict(bframes=2, coverage=True, interlaced=True)),
     "interlaced-1080-ibbp": (1920, 1080, 6, dict(bframes=2, qp=26, interlaced=True)),
+    # long-term references, MMCO 1-4 / 6 and list modifications (marking coverage)
+    "marking-cov-ibbp": (176, 144, 30, dict(bframes=2, refs=3, coverage=True, marking=True)),
+    "marking-1080-p": (1920, 1080, 12, dict(bframes=0, refs=4, qp=26, marking=True)),
     # field pairs (PAFF): half-height field pictures in field slots, the published frame woven
     "paff-cov": (176, 144, 24, dict(coverage=True, **PAFF)),
     "paff-1080-refs2": (1920, 1080, 12, dict(qp=26, refs=2, temporal_noise=2.0, **PAFF)),
