@@ -344,14 +344,12 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
     }
   }
   if (sh.field_pic) {
-    // Field pictures: CAVLC I / P / B with 4x4 transforms and sliding-window marking. CABAC needs
-    // the field-coded context initialisation values (not in any source this build can pin), the
-    // 8x8 transform the 8x8 field scan, MMCOs / list modifications the field picture numbers:
-    // those stay with the VCN backend.
+    // Field pictures: CAVLC I / P / B with 4x4 transforms. CABAC needs the field-coded context
+    // initialisation values (not in any source this build can pin) and the 8x8 transform the 8x8
+    // field scan: those stay with the VCN backend, as does MMCO 5 in a field.
     if (pps.cabac) throw UnsupportedStream("interlaced H.264: CABAC field pictures are not supported");
     if (pps.transform_8x8_mode) throw UnsupportedStream("interlaced H.264: 8x8 transform in field pictures is not supported");
-    if (sh.adaptive_marking || sh.long_term_reference || !sh.ref_mods[0].empty())
-      throw UnsupportedStream("interlaced H.264: field MMCOs / long-term / list modifications are not supported");
+    if (sh.has_mmco5()) throw UnsupportedStream("interlaced H.264: MMCO 5 in field pictures is not supported");
   }
   return sh;
 }
@@ -593,12 +591,24 @@ void Decoder::mark_references(const SliceHdr& sh, const Sps& sps, int slot, int 
   }
 }
 
+// Field picture numbers (§8.2.4.1): a field of the current parity counts 2 * FrameNumWrap + 1
+// (long-term: 2 * LongTermFrameIdx + 1), one of the other parity the even number below.
+static int field_pic_num(const RefPic& r, int par, int cur_par, int frame_num, int max_fn) {
+  const int wrap = r.frame_num > frame_num ? r.frame_num - max_fn : r.frame_num;
+  return 2 * wrap + (par == cur_par ? 1 : 0);
+}
+static int field_lt_pic_num(const RefPic& r, int par, int cur_par) { return 2 * r.lt_idx + (par == cur_par ? 1 : 0); }
+static ListEntry field_entry(const RefPic& r, int par, bool lt) {
+  return ListEntry{2 * r.slot + par, r.poc_f[par], lt, r.uid_f[par], r.col_f[par].get()};
+}
+
 // §8.2.4.2.2 / §8.2.4.2.4 / §8.2.4.2.5: the lists of a P or B field. The reference frames
 // (P: short-term by FrameNumWrap descending; B: by POC around the current field's, list 0 the
 // earlier ones first, list 1 the later ones; then long-term by index) are taken apart into their
 // fields, alternating parities starting with the current field's; when one parity runs out the
-// other's remaining fields follow in order. A frame's POC here is the lowest of its reference
-// fields'; the first field of the current frame is a reference frame entry too.
+// other's remaining fields follow in order. A frame's POC here is the lowest of its short-term
+// fields'; the first field of the current frame is a reference frame entry too. Then the slice's
+// modifications (§8.2.4.3 with field picture numbers).
 void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps, int cur_poc) {
   const int max_fn = 1 << sps.log2_max_frame_num;
   list_[0].clear();
@@ -606,22 +616,20 @@ void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps, int cur_poc)
   if (sh.type() == h264::kI) return;
   std::vector<RefPic*> st, lt;
   for (auto& r : dpb_) {
-    if (r.long_term) {
-      lt.push_back(&r);
-    } else {
+    if (r.fields & 3) {
       r.frame_num_wrap = r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num;
       st.push_back(&r);
     }
+    if (r.lt_fields & 3) lt.push_back(&r);
   }
   std::sort(lt.begin(), lt.end(), [](RefPic* a, RefPic* b) { return a->lt_idx < b->lt_idx; });
   const int same = sh.bottom_field ? 1 : 0;
-  auto alternate = [&](const std::vector<RefPic*>& frames, std::vector<ListEntry>& all) {
+  auto alternate = [&](const std::vector<RefPic*>& frames, bool long_term, std::vector<ListEntry>& all) {
     std::vector<ListEntry> f[2];  // [0] same parity, [1] opposite
     for (RefPic* r : frames)
       for (int k = 0; k < 2; ++k) {
         const int par = k == 0 ? same : 1 - same;
-        if ((r->fields >> par) & 1)
-          f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], r->long_term, r->uid_f[par], r->col_f[par].get()});
+        if (((long_term ? r->lt_fields : r->fields) >> par) & 1) f[k].push_back(field_entry(*r, par, long_term));
       }
     size_t i[2] = {0, 0};
     for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
@@ -629,15 +637,18 @@ void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps, int cur_poc)
       all.push_back(f[from][i[from]++]);
     }
   };
+  auto st_poc = [](const RefPic* r) {
+    return (r->fields & 1) ? ((r->fields & 2) ? std::min(r->poc_f[0], r->poc_f[1]) : r->poc_f[0]) : r->poc_f[1];
+  };
   std::vector<RefPic*> init[2];
   if (sh.type() == h264::kP) {
     std::sort(st.begin(), st.end(), [](RefPic* a, RefPic* b) { return a->frame_num_wrap > b->frame_num_wrap; });
     init[0] = st;
   } else {
     std::vector<RefPic*> before, after;
-    for (RefPic* r : st) (r->poc <= cur_poc ? before : after).push_back(r);
-    std::sort(before.begin(), before.end(), [](RefPic* a, RefPic* b) { return a->poc > b->poc; });
-    std::sort(after.begin(), after.end(), [](RefPic* a, RefPic* b) { return a->poc < b->poc; });
+    for (RefPic* r : st) (st_poc(r) <= cur_poc ? before : after).push_back(r);
+    std::sort(before.begin(), before.end(), [&](RefPic* a, RefPic* b) { return st_poc(a) > st_poc(b); });
+    std::sort(after.begin(), after.end(), [&](RefPic* a, RefPic* b) { return st_poc(a) < st_poc(b); });
     init[0] = before;
     init[0].insert(init[0].end(), after.begin(), after.end());
     init[1] = after;
@@ -646,63 +657,182 @@ void Decoder::build_field_lists(const SliceHdr& sh, const Sps& sps, int cur_poc)
   std::vector<ListEntry> all[2];
   const int nl = sh.type() == h264::kB ? 2 : 1;
   for (int l = 0; l < nl; ++l) {
-    alternate(init[l], all[l]);
-    alternate(lt, all[l]);
+    alternate(init[l], false, all[l]);
+    alternate(lt, true, all[l]);
   }
   auto same_entries = [](const std::vector<ListEntry>& a, const std::vector<ListEntry>& b) {
     if (a.size() != b.size()) return false;
     for (size_t i = 0; i < a.size(); ++i)
-      if (a[i].slot != b[i].slot) return false;
+      if (a[i].slot != b[i].slot || a[i].long_term != b[i].long_term) return false;
     return true;
   };
   if (nl == 2 && all[1].size() > 1 && same_entries(all[0], all[1])) std::swap(all[1][0], all[1][1]);
+  const int cur_pic_num = 2 * sh.frame_num + 1, max_pic = 2 * max_fn;
   for (int l = 0; l < nl; ++l) {
+    std::vector<ListEntry>& list = all[l];
+    int pred = cur_pic_num;
+    size_t idx = 0;
+    for (const auto& m : sh.ref_mods[l]) {
+      bool found = false;
+      ListEntry pick{};
+      if (m.idc < 2) {
+        int nw = m.idc == 0 ? pred - (m.val + 1) : pred + (m.val + 1);
+        if (nw < 0) nw += max_pic;
+        if (nw >= max_pic) nw -= max_pic;
+        pred = nw;
+        const int pic_num = nw > cur_pic_num ? nw - max_pic : nw;
+        for (const auto& r : dpb_)
+          for (int par = 0; par < 2; ++par)
+            if (((r.fields >> par) & 1) && field_pic_num(r, par, same, sh.frame_num, max_fn) == pic_num) {
+              pick = field_entry(r, par, false);
+              found = true;
+            }
+      } else {
+        for (const auto& r : dpb_)
+          for (int par = 0; par < 2; ++par)
+            if (((r.lt_fields >> par) & 1) && field_lt_pic_num(r, par, same) == m.val) {
+              pick = field_entry(r, par, true);
+              found = true;
+            }
+      }
+      if (!found) throw Error("vep: reference list modification names a missing field");
+      ++list_mods;
+      list.insert(list.begin() + long(std::min(idx, list.size())), pick);
+      for (size_t k = idx + 1; k < list.size(); ++k)
+        if (list[k].slot == pick.slot && list[k].long_term == pick.long_term) {
+          list.erase(list.begin() + long(k));
+          break;
+        }
+      ++idx;
+    }
     list_[l].assign(size_t(sh.num_ref_idx[l]), ListEntry{});
-    for (size_t i = 0; i < list_[l].size() && i < all[l].size(); ++i) list_[l][i] = all[l][i];
+    for (size_t i = 0; i < list_[l].size() && i < list.size(); ++i) list_[l][i] = list[i];
   }
 }
 
-// Reference marking of a field (sliding window only, see read_slice_header): the first field of a
-// frame enters the DPB as a frame entry holding one field (after the sliding window makes room);
-// the second field joins its frame's entry.
+// Reference marking of a field (§8.2.5 with field picture numbers). The first field of a frame
+// enters the DPB as a frame entry holding one field (after the sliding window, which works on
+// frames, makes room), the second field joins its frame's entry; MMCOs mark single fields
+// (1 / 2), move a field to long-term (3; a long-term frame index held by another frame frees
+// it), cap the long-term indices (4) or make the current field long-term (6). The second field
+// of a pair whose first field is long-term is long-term with the same index.
 void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, u32 uid, bool second,
                          std::shared_ptr<const ColMotion> col) {
   const int par = sh.bottom_field ? 1 : 0;
-  if (second)
-    for (auto& r : dpb_)
-      if (r.slot == slot && !r.long_term && r.frame_num == sh.frame_num) {
-        r.fields |= u8(1 << par);
-        r.poc_f[par] = poc;
-        r.uid_f[par] = uid;
-        r.col_f[par] = std::move(col);
-        r.poc = std::min(r.poc, poc);
-        return;
-      }
   const int max_fn = 1 << sps.log2_max_frame_num;
   const int max_refs = std::max(1, sps.max_num_ref_frames);
-  if (sh.idr()) {
+  const int cur_pic_num = 2 * sh.frame_num + 1;
+  auto cur_entry = [&]() -> RefPic* {
+    if (!second) return nullptr;
+    for (auto& r : dpb_)
+      if (r.slot == slot && r.frame_num == sh.frame_num && ((r.fields | r.lt_fields) & 3)) return &r;
+    return nullptr;
+  };
+  bool cur_long = false;
+  int cur_lt = 0;
+  if (sh.idr() && !second) {
     dpb_.clear();
-    max_lt_idx_ = -1;
-  } else {
-    auto wrap = [&](const RefPic& r) { return r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num; };
-    while (int(dpb_.size()) >= max_refs) {  // sliding window (frames)
-      auto it = std::min_element(dpb_.begin(), dpb_.end(), [&](const RefPic& a, const RefPic& b) {
-        if (a.long_term != b.long_term) return !a.long_term;
-        return wrap(a) < wrap(b);
-      });
-      dpb_.erase(it);
+    max_lt_idx_ = sh.long_term_reference ? 0 : -1;
+    cur_long = sh.long_term_reference;
+    long_term_marked += cur_long ? 1 : 0;
+  } else if (sh.adaptive_marking) {
+    const RefPic* self = cur_entry();
+    for (const auto& m : sh.mmcos) {
+      ++mmco_ops[m.op];
+      switch (m.op) {
+        case 1:
+          for (auto& r : dpb_)
+            for (int p = 0; p < 2; ++p)
+              if (((r.fields >> p) & 1) && field_pic_num(r, p, par, sh.frame_num, max_fn) == cur_pic_num - (m.a + 1))
+                r.fields &= u8(~(1 << p));
+          break;
+        case 2:
+          for (auto& r : dpb_)
+            for (int p = 0; p < 2; ++p)
+              if (((r.lt_fields >> p) & 1) && field_lt_pic_num(r, p, par) == m.a) r.lt_fields &= u8(~(1 << p));
+          break;
+        case 3: {
+          RefPic* f = nullptr;
+          int fp = 0;
+          for (auto& r : dpb_)
+            for (int p = 0; p < 2; ++p)
+              if (((r.fields >> p) & 1) && field_pic_num(r, p, par, sh.frame_num, max_fn) == cur_pic_num - (m.a + 1)) {
+                f = &r;
+                fp = p;
+              }
+          if (!f) break;
+          for (auto& r : dpb_)
+            if (&r != f && (r.lt_fields & 3) && r.lt_idx == m.b) r.lt_fields = 0;
+          f->fields &= u8(~(1 << fp));
+          f->lt_fields |= u8(1 << fp);
+          f->lt_idx = m.b;
+          ++long_term_marked;
+          break;
+        }
+        case 4:
+          max_lt_idx_ = m.a - 1;
+          for (auto& r : dpb_)
+            if ((r.lt_fields & 3) && r.lt_idx > max_lt_idx_) r.lt_fields = 0;
+          break;
+        case 6:
+          for (auto& r : dpb_)
+            if (&r != self && (r.lt_fields & 3) && r.lt_idx == m.a) r.lt_fields = 0;
+          cur_long = true;
+          cur_lt = m.a;
+          ++long_term_marked;
+          break;
+        default:  // (5 is rejected with the slice header)
+          break;
+      }
+    }
+  } else if (!second) {  // sliding window (§8.2.5.3) on frames, for the first field of a frame
+    int frames = 0, n_short = 0;
+    for (const auto& r : dpb_) {
+      frames += ((r.fields | r.lt_fields) & 3) ? 1 : 0;
+      n_short += (r.fields & 3) ? 1 : 0;
+    }
+    if (frames >= max_refs && n_short > 0) {
+      RefPic* oldest = nullptr;
+      int ow = 0;
+      for (auto& r : dpb_) {
+        if (!(r.fields & 3)) continue;
+        const int w = r.frame_num > sh.frame_num ? r.frame_num - max_fn : r.frame_num;
+        if (!oldest || w < ow) {
+          oldest = &r;
+          ow = w;
+        }
+      }
+      oldest->fields = 0;
     }
   }
-  RefPic cur;
-  cur.slot = slot;
-  cur.frame_num = sh.frame_num;
-  cur.poc = poc;
-  cur.uid = uid;
-  cur.fields = u8(1 << par);
-  cur.poc_f[par] = poc;
-  cur.uid_f[par] = uid;
-  cur.col_f[par] = std::move(col);
-  dpb_.push_back(cur);
+  if (!cur_long && second)  // the pair's first field is long-term: so is this one
+    if (const RefPic* f = cur_entry(); f && (f->lt_fields & 3)) {
+      cur_long = true;
+      cur_lt = f->lt_idx;
+    }
+  dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const RefPic& r) { return !((r.fields | r.lt_fields) & 3); }),
+             dpb_.end());
+  RefPic* e = cur_entry();
+  if (!e) {
+    dpb_.push_back(RefPic{});
+    e = &dpb_.back();
+    e->slot = slot;
+    e->frame_num = sh.frame_num;
+    e->poc = poc;
+    e->uid = uid;
+    e->fields = 0;
+  }
+  e->poc_f[par] = poc;
+  e->uid_f[par] = uid;
+  e->col_f[par] = std::move(col);
+  e->poc = std::min(e->poc, poc);
+  if (cur_long) {
+    e->lt_fields |= u8(1 << par);
+    e->lt_idx = cur_lt;
+  } else {
+    e->fields |= u8(1 << par);
+  }
+  e->long_term = (e->lt_fields & 3) && !(e->fields & 3);
 }
 
 int Decoder::reorder_depth(const Sps& sps) const {
@@ -1475,7 +1605,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       int cs = dpb_.front().slot;
       if (pic->structure) {  // a field of that frame, the current parity if it holds one
         const int par = pic->structure - 1;
-        cs = 2 * cs + (((dpb_.front().fields >> par) & 1) ? par : 1 - par);
+        cs = 2 * cs + ((((dpb_.front().fields | dpb_.front().lt_fields) >> par) & 1) ? par : 1 - par);
       }
       for (auto& rf : m.ref) rf = u8(cs);
       m.mv = u32(pic->mvs.size());

@@ -340,8 +340,10 @@ struct RefPic {
   int poc = 0;
   u32 uid = 0;
   std::shared_ptr<const ColMotion> col;
-  // field decoding: reference fields of the frame (bit 0 top, bit 1 bottom), their POCs and uids
+  // field decoding: short-term / long-term reference fields of the frame (bit 0 top, bit 1
+  // bottom; frame decoding uses `long_term` instead), their POCs and uids
   u8 fields = 3;
+  u8 lt_fields = 0;
   int poc_f[2] = {0, 0};
   u32 uid_f[2] = {0, 0};
   std::shared_ptr<const ColMotion> col_f[2];  // each field's motion (B fields' direct prediction)

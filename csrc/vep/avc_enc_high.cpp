@@ -117,6 +117,7 @@ struct AvcHighEncoder::Impl {
     std::shared_ptr<const ColMotion> col_f[2];
     bool long_term = false;  // (frame pictures, cfg.marking)
     int lt_idx = 0;
+    u8 lt_fields = 0;        // (field pictures: long-term fields; `fields` are the short-term ones)
   };
   int max_lt_idx = -1;  // MaxLongTermFrameIdx (-1: no long-term frame indices)
   std::vector<Ref> dpb;
@@ -473,55 +474,316 @@ struct AvcHighEncoder::Impl {
     VEP_CHECK(int(dpb.size()) <= std::max(1, sps.max_num_ref_frames), "encoder: DPB overflow after marking");
   }
 
-  // Lists of a P / B field: the decoder's field list initialisation (Decoder::build_field_lists):
-  // reference frames (P: FrameNumWrap descending; B: by POC around the current field's, a frame's
-  // POC the lowest of its fields'), split into fields alternating from the current parity.
-  void build_field_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* lists) {
-    lists[0].clear();
-    lists[1].clear();
+  // Field picture numbers (the decoder's field_pic_num / field_lt_pic_num, §8.2.4.1).
+  int fpic_num(const Ref& r, int par, int cur_par, int fn) const { return 2 * wrap_of(r, fn) + (par == cur_par ? 1 : 0); }
+  static int flt_pic_num(const Ref& r, int par, int cur_par) { return 2 * r.lt_idx + (par == cur_par ? 1 : 0); }
+  static ListEntry fentry(const Ref& r, int par, bool lt) {
+    return ListEntry{2 * r.slot + par, r.poc_f[par], lt, r.uid_f[par], r.col_f[par].get()};
+  }
+
+  // Initial lists of a P / B field: the decoder's field list initialisation
+  // (Decoder::build_field_lists): reference frames (P: FrameNumWrap descending; B: by POC around
+  // the current field's, a frame's POC the lowest of its short-term fields'), then long-term by
+  // index, split into fields alternating from the current parity.
+  void init_field_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* all) const {
+    all[0].clear();
+    all[1].clear();
     if (sh.type() == h264::kI) return;
-    std::vector<const Ref*> st;
-    for (const Ref& r : dpb) st.push_back(&r);
-    auto fpoc = [](const Ref* r) { return (r->fields & 1) ? ((r->fields & 2) ? std::min(r->poc_f[0], r->poc_f[1]) : r->poc_f[0]) : r->poc_f[1]; };
+    std::vector<const Ref*> st, lt;
+    for (const Ref& r : dpb) {
+      if (r.fields & 3) st.push_back(&r);
+      if (r.lt_fields & 3) lt.push_back(&r);
+    }
+    std::sort(lt.begin(), lt.end(), [](const Ref* a, const Ref* b) { return a->lt_idx < b->lt_idx; });
+    auto st_poc = [](const Ref* r) {
+      return (r->fields & 1) ? ((r->fields & 2) ? std::min(r->poc_f[0], r->poc_f[1]) : r->poc_f[0]) : r->poc_f[1];
+    };
     std::vector<const Ref*> init[2];
     if (sh.type() == h264::kP) {
-      auto wrap = [&](const Ref* r) { return r->frame_num > sh.frame_num ? r->frame_num - max_fn : r->frame_num; };
-      std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap(a) > wrap(b); });
+      std::sort(st.begin(), st.end(), [&](const Ref* a, const Ref* b) { return wrap_of(*a, sh.frame_num) > wrap_of(*b, sh.frame_num); });
       init[0] = st;
     } else {
       std::vector<const Ref*> before, after;
-      for (const Ref* r : st) (fpoc(r) <= cur_poc ? before : after).push_back(r);
-      std::sort(before.begin(), before.end(), [&](const Ref* a, const Ref* b) { return fpoc(a) > fpoc(b); });
-      std::sort(after.begin(), after.end(), [&](const Ref* a, const Ref* b) { return fpoc(a) < fpoc(b); });
+      for (const Ref* r : st) (st_poc(r) <= cur_poc ? before : after).push_back(r);
+      std::sort(before.begin(), before.end(), [&](const Ref* a, const Ref* b) { return st_poc(a) > st_poc(b); });
+      std::sort(after.begin(), after.end(), [&](const Ref* a, const Ref* b) { return st_poc(a) < st_poc(b); });
       init[0] = before;
       init[0].insert(init[0].end(), after.begin(), after.end());
       init[1] = after;
       init[1].insert(init[1].end(), before.begin(), before.end());
     }
     const int same = sh.bottom_field ? 1 : 0;
-    std::vector<ListEntry> all[2];
     const int nl = sh.type() == h264::kB ? 2 : 1;
-    for (int l = 0; l < nl; ++l) {
-      std::vector<ListEntry> f[2];
-      for (const Ref* r : init[l])
-        for (int k = 0; k < 2; ++k) {
-          const int par = k == 0 ? same : 1 - same;
-          if ((r->fields >> par) & 1)
-            f[k].push_back(ListEntry{2 * r->slot + par, r->poc_f[par], false, r->uid_f[par], r->col_f[par].get()});
+    for (int l = 0; l < nl; ++l)
+      for (int part = 0; part < 2; ++part) {  // short-term frames, then long-term
+        std::vector<ListEntry> f[2];
+        for (const Ref* r : part == 0 ? init[l] : lt)
+          for (int k = 0; k < 2; ++k) {
+            const int par = k == 0 ? same : 1 - same;
+            if (((part == 0 ? r->fields : r->lt_fields) >> par) & 1) f[k].push_back(fentry(*r, par, part == 1));
+          }
+        size_t i[2] = {0, 0};
+        for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
+          const int from = i[k] < f[k].size() ? k : k ^ 1;
+          all[l].push_back(f[from][i[from]++]);
         }
-      size_t i[2] = {0, 0};
-      for (int k = 0; i[0] < f[0].size() || i[1] < f[1].size(); k ^= 1) {
-        const int from = i[k] < f[k].size() ? k : k ^ 1;
-        all[l].push_back(f[from][i[from]++]);
       }
-    }
     if (nl == 2 && all[1].size() > 1) {
       bool same_lists = all[0].size() == all[1].size();
-      for (size_t k = 0; same_lists && k < all[0].size(); ++k) same_lists = all[0][k].slot == all[1][k].slot;
+      for (size_t k = 0; same_lists && k < all[0].size(); ++k)
+        same_lists = all[0][k].slot == all[1][k].slot && all[0][k].long_term == all[1][k].long_term;
       if (same_lists) std::swap(all[1][0], all[1][1]);
     }
-    for (int l = 0; l < nl; ++l)
-      for (int k = 0; k < sh.num_ref_idx[l] && k < int(all[l].size()); ++k) lists[l].push_back(all[l][size_t(k)]);
+  }
+
+  // Field list modifications (cfg.marking): up to two random fields moved to the front.
+  void choose_field_mods(SliceHdr& sh, int cur_poc) {
+    std::vector<ListEntry> all[2];
+    init_field_lists(sh, cur_poc, all);
+    const int cur = sh.bottom_field ? 1 : 0, max_pic = 2 * max_fn;
+    for (int l = 0; l < (sh.type() == h264::kB ? 2 : 1); ++l) {
+      sh.ref_mods[l].clear();
+      if (all[l].size() < 2 || rng.uni(100) >= 40) continue;
+      int pred = 2 * sh.frame_num + 1;  // CurrPicNum
+      const int n = 1 + rng.uni(2);
+      for (int k = 0; k < n; ++k) {
+        const ListEntry& e = all[l][size_t(rng.uni(int(all[l].size())))];
+        const Ref* r = nullptr;
+        for (const Ref& x : dpb)
+          if (x.slot == e.slot >> 1) r = &x;
+        const int par = e.slot & 1;
+        if (e.long_term) {
+          sh.ref_mods[l].push_back({2, flt_pic_num(*r, par, cur)});
+          continue;
+        }
+        const int pn = fpic_num(*r, par, cur, sh.frame_num);
+        const int nowrap = pn < 0 ? pn + max_pic : pn;
+        if (nowrap == pred) continue;
+        sh.ref_mods[l].push_back({nowrap < pred ? 0 : 1, std::abs(nowrap - pred) - 1});
+        pred = nowrap;
+      }
+    }
+  }
+
+  void build_field_lists(const SliceHdr& sh, int cur_poc, std::vector<ListEntry>* lists) {
+    std::vector<ListEntry> all[2];
+    init_field_lists(sh, cur_poc, all);
+    const int cur = sh.bottom_field ? 1 : 0, cur_pic_num = 2 * sh.frame_num + 1, max_pic = 2 * max_fn;
+    for (int l = 0; l < 2; ++l) {
+      std::vector<ListEntry>& list = all[l];
+      int pred = cur_pic_num;
+      size_t idx = 0;
+      for (const auto& m : sh.ref_mods[l]) {
+        bool found = false;
+        ListEntry pick{};
+        if (m.idc < 2) {
+          int nw = m.idc == 0 ? pred - (m.val + 1) : pred + (m.val + 1);
+          if (nw < 0) nw += max_pic;
+          if (nw >= max_pic) nw -= max_pic;
+          pred = nw;
+          const int pic_num = nw > cur_pic_num ? nw - max_pic : nw;
+          for (const Ref& r : dpb)
+            for (int par = 0; par < 2; ++par)
+              if (((r.fields >> par) & 1) && fpic_num(r, par, cur, sh.frame_num) == pic_num) {
+                pick = fentry(r, par, false);
+                found = true;
+              }
+        } else {
+          for (const Ref& r : dpb)
+            for (int par = 0; par < 2; ++par)
+              if (((r.lt_fields >> par) & 1) && flt_pic_num(r, par, cur) == m.val) {
+                pick = fentry(r, par, true);
+                found = true;
+              }
+        }
+        VEP_CHECK(found, "encoder: field list modification names a missing field");
+        list.insert(list.begin() + long(std::min(idx, list.size())), pick);
+        for (size_t k = idx + 1; k < list.size(); ++k)
+          if (list[k].slot == pick.slot && list[k].long_term == pick.long_term) {
+            list.erase(list.begin() + long(k));
+            break;
+          }
+        ++idx;
+      }
+      lists[l].clear();
+      for (int k = 0; k < sh.num_ref_idx[l] && k < int(list.size()); ++k) lists[l].push_back(list[size_t(k)]);
+    }
+  }
+
+  // MMCOs of a reference field (cfg.marking): room for a new frame (its first field) frees the
+  // oldest unprotected frame's fields (MMCO 1 / 2); then at random MMCO 4, 6 (a first field
+  // long-term: its second field follows), 3 (a short-term field of an all-short-term frame
+  // long-term), 2 / 1 (a long-term / short-term field unused). The current frame and, with B
+  // pictures, the two newest frames are left as they are.
+  void choose_field_mmcos(SliceHdr& sh, int parity, bool anchor_with_bs) {
+    sh.mmcos.clear();
+    const int cur = parity;
+    std::vector<const Ref*> all;
+    for (const Ref& r : dpb) all.push_back(&r);
+    std::sort(all.begin(), all.end(), [&](const Ref* a, const Ref* b) { return wrap_of(*a, sh.frame_num) < wrap_of(*b, sh.frame_num); });
+    std::vector<const Ref*> prot;  // frames left alone
+    const size_t keep = cfg.bframes > 0 ? 2 : 0;
+    for (size_t k = all.size() >= keep ? all.size() - keep : 0; k < all.size(); ++k) prot.push_back(all[k]);
+    if (parity == 1)
+      for (const Ref* r : all)
+        if (r->slot == pair_slot && r->frame_num == sh.frame_num) prot.push_back(r);
+    auto is_prot = [&](const Ref* r) { return std::find(prot.begin(), prot.end(), r) != prot.end(); };
+    u32 kept_mask = 0;
+    int kept_lt = -1;
+    for (const Ref* r : prot)
+      if (r->lt_fields & 3) {
+        kept_mask |= 1u << r->lt_idx;
+        kept_lt = std::max(kept_lt, r->lt_idx);
+      }
+    auto free_idx = [&](int max_idx) {
+      std::vector<int> c;
+      for (int i = 0; i <= max_idx; ++i)
+        if (!((kept_mask >> i) & 1)) c.push_back(i);
+      return c.empty() ? -1 : c[size_t(rng.uni(int(c.size())))];
+    };
+    auto op1 = [&](const Ref* r, int par) { sh.mmcos.push_back({1, 2 * sh.frame_num + 1 - fpic_num(*r, par, cur, sh.frame_num) - 1, 0}); };
+    auto op2 = [&](const Ref* r, int par) { sh.mmcos.push_back({2, flt_pic_num(*r, par, cur), 0}); };
+    std::vector<const Ref*> freed;
+    if (parity == 0 && int(dpb.size()) >= std::max(1, sps.max_num_ref_frames)) {  // room for this frame
+      const Ref* victim = nullptr;
+      for (const Ref* r : all)
+        if (!is_prot(r)) {
+          victim = r;
+          break;
+        }
+      if (!victim) return;  // (sliding window instead)
+      for (int par = 0; par < 2; ++par) {
+        if ((victim->fields >> par) & 1) op1(victim, par);
+        if ((victim->lt_fields >> par) & 1) op2(victim, par);
+      }
+      freed.push_back(victim);
+    }
+    std::vector<std::pair<const Ref*, int>> st_f, lt_f;  // unprotected fields
+    for (const Ref* r : all) {
+      if (is_prot(r) || std::find(freed.begin(), freed.end(), r) != freed.end()) continue;
+      for (int par = 0; par < 2; ++par) {
+        if (((r->fields >> par) & 1) && !(r->lt_fields & 3)) st_f.push_back({r, par});
+        if ((r->lt_fields >> par) & 1) lt_f.push_back({r, par});
+      }
+    }
+    const int rr = rng.uni(100);
+    int max_lt = max_lt_idx;
+    if (rr < 15) {
+      max_lt = std::max(kept_lt, rng.uni(3) - 1);
+      sh.mmcos.push_back({4, max_lt + 1, 0});
+    } else if (rr < 30 && parity == 0 && !anchor_with_bs && free_idx(max_lt) >= 0) {
+      sh.mmcos.push_back({6, free_idx(max_lt), 0});
+    } else if (rr < 45 && free_idx(max_lt) >= 0 && !st_f.empty()) {
+      const auto [r, par] = st_f[size_t(rng.uni(int(st_f.size())))];
+      sh.mmcos.push_back({3, 2 * sh.frame_num + 1 - fpic_num(*r, par, cur, sh.frame_num) - 1, free_idx(max_lt)});
+    } else if (rr < 55 && !lt_f.empty()) {
+      const auto [r, par] = lt_f[size_t(rng.uni(int(lt_f.size())))];
+      op2(r, par);
+    } else if (rr < 70 && !st_f.empty()) {
+      const auto [r, par] = st_f[size_t(rng.uni(int(st_f.size())))];
+      op1(r, par);
+    }
+    if (!sh.mmcos.empty()) sh.adaptive_marking = true;
+  }
+
+  // Marking of the current reference field: Decoder::mark_field, mirrored.
+  void mark_field_enc(const SliceHdr& sh, int slot, int poc, u32 uid, bool second, std::shared_ptr<const ColMotion> col) {
+    const int par = sh.bottom_field ? 1 : 0;
+    const int max_refs = std::max(1, sps.max_num_ref_frames);
+    const int cur_pic_num = 2 * sh.frame_num + 1;
+    auto cur_entry = [&]() -> Ref* {
+      if (!second) return nullptr;
+      for (Ref& r : dpb)
+        if (r.slot == slot && r.frame_num == sh.frame_num && ((r.fields | r.lt_fields) & 3)) return &r;
+      return nullptr;
+    };
+    bool cur_long = false;
+    int cur_lt = 0;
+    if (sh.idr() && !second) {
+      dpb.clear();
+      max_lt_idx = sh.long_term_reference ? 0 : -1;
+      cur_long = sh.long_term_reference;
+    } else if (sh.adaptive_marking) {
+      const Ref* self = cur_entry();
+      for (const auto& m : sh.mmcos) {
+        switch (m.op) {
+          case 1:
+            for (Ref& r : dpb)
+              for (int p = 0; p < 2; ++p)
+                if (((r.fields >> p) & 1) && fpic_num(r, p, par, sh.frame_num) == cur_pic_num - (m.a + 1)) r.fields &= u8(~(1 << p));
+            break;
+          case 2:
+            for (Ref& r : dpb)
+              for (int p = 0; p < 2; ++p)
+                if (((r.lt_fields >> p) & 1) && flt_pic_num(r, p, par) == m.a) r.lt_fields &= u8(~(1 << p));
+            break;
+          case 3: {
+            Ref* f = nullptr;
+            int fp = 0;
+            for (Ref& r : dpb)
+              for (int p = 0; p < 2; ++p)
+                if (((r.fields >> p) & 1) && fpic_num(r, p, par, sh.frame_num) == cur_pic_num - (m.a + 1)) {
+                  f = &r;
+                  fp = p;
+                }
+            if (!f) break;
+            for (Ref& r : dpb)
+              if (&r != f && (r.lt_fields & 3) && r.lt_idx == m.b) r.lt_fields = 0;
+            f->fields &= u8(~(1 << fp));
+            f->lt_fields |= u8(1 << fp);
+            f->lt_idx = m.b;
+            break;
+          }
+          case 4:
+            max_lt_idx = m.a - 1;
+            for (Ref& r : dpb)
+              if ((r.lt_fields & 3) && r.lt_idx > max_lt_idx) r.lt_fields = 0;
+            break;
+          case 6:
+            for (Ref& r : dpb)
+              if (&r != self && (r.lt_fields & 3) && r.lt_idx == m.a) r.lt_fields = 0;
+            cur_long = true;
+            cur_lt = m.a;
+            break;
+          default: break;
+        }
+      }
+    } else if (!second) {  // sliding window on frames
+      int frames = 0, n_short = 0;
+      for (const Ref& r : dpb) {
+        frames += ((r.fields | r.lt_fields) & 3) ? 1 : 0;
+        n_short += (r.fields & 3) ? 1 : 0;
+      }
+      if (frames >= max_refs && n_short > 0) {
+        Ref* oldest = nullptr;
+        for (Ref& r : dpb)
+          if ((r.fields & 3) && (!oldest || wrap_of(r, sh.frame_num) < wrap_of(*oldest, sh.frame_num))) oldest = &r;
+        oldest->fields = 0;
+      }
+    }
+    if (!cur_long && second)
+      if (const Ref* f = cur_entry(); f && (f->lt_fields & 3)) {
+        cur_long = true;
+        cur_lt = f->lt_idx;
+      }
+    dpb.erase(std::remove_if(dpb.begin(), dpb.end(), [](const Ref& r) { return !((r.fields | r.lt_fields) & 3); }), dpb.end());
+    Ref* e = cur_entry();
+    if (!e) {
+      dpb.push_back(Ref{slot, sh.frame_num, poc, uid, nullptr});
+      e = &dpb.back();
+      e->fields = 0;
+    }
+    e->poc_f[par] = poc;
+    e->uid_f[par] = uid;
+    e->col_f[par] = std::move(col);
+    e->poc = std::min(e->poc, poc);
+    if (cur_long) {
+      e->lt_fields |= u8(1 << par);
+      e->lt_idx = cur_lt;
+    } else {
+      e->fields |= u8(1 << par);
+    }
+    VEP_CHECK(int(dpb.size()) <= max_refs, "encoder: DPB overflow after field marking");
   }
 
   int pick_slot() const {
@@ -1020,14 +1282,14 @@ struct AvcHighEncoder::Impl {
     if (job.type == h264::kP && !fld) n0 = std::min<int>(cfg.refs, int(dpb.size()));
     if (job.type == h264::kP && fld) {  // reference fields (the first field of this frame included)
       int nf = 0;
-      for (const Ref& r : dpb) nf += (r.fields & 1) + (r.fields >> 1);
+      for (const Ref& r : dpb) nf += (r.fields & 1) + ((r.fields >> 1) & 1) + (r.lt_fields & 1) + ((r.lt_fields >> 1) & 1);
       n0 = std::min(2 * cfg.refs, nf);
     }
     if (job.type == h264::kB && fld) {  // reference fields on both sides (every one in list 0)
       int before = 0, after = 0, nf = 0;
       for (const Ref& r : dpb)
         for (int par = 0; par < 2; ++par)
-          if ((r.fields >> par) & 1) {
+          if (((r.fields | r.lt_fields) >> par) & 1) {
             ++nf;
             (r.poc_f[par] < poc ? before : after) += 1;
           }
@@ -1067,6 +1329,14 @@ struct AvcHighEncoder::Impl {
       } else {
         if (job.type != h264::kI) choose_mods(sh, poc);
         if (job.ref) choose_mmcos(sh, job.type == h264::kP && cfg.bframes > 0);
+      }
+    }
+    if (cfg.marking && fld) {
+      if (idr) {
+        sh.long_term_reference = rng.uni(100) < 30;
+      } else {
+        if (job.type != h264::kI) choose_field_mods(sh, poc);
+        if (job.ref) choose_field_mmcos(sh, job.parity, job.type == h264::kP && cfg.bframes > 0);
       }
     }
     sh.cabac_init_idc = 0;
@@ -1145,34 +1415,10 @@ struct AvcHighEncoder::Impl {
       au->add_nal(nal.data(), nal.size());
     }
     if (pic.deblock) cpu_deblock(pic, T());
-    if (job.ref && fld) {  // a frame entry holding its reference fields (sliding window on frames)
-      const int fs = pic.target >> 1, par = job.parity;
-      bool joined = false;
-      if (par == 1)
-        for (Ref& r : dpb)
-          if (r.slot == fs && r.frame_num == sh.frame_num) {
-            r.fields |= 2;
-            r.poc_f[1] = poc;
-            r.uid_f[1] = next_uid;
-            r.col_f[1] = build_col_motion(nb, W, Hp, slice_uids, sps.direct_8x8);
-            joined = true;
-          }
-      if (!joined) {
-        if (int(dpb.size()) >= sps.max_num_ref_frames) {
-          auto it = std::min_element(dpb.begin(), dpb.end(), [&](const Ref& a, const Ref& b) {
-            auto wrap = [&](const Ref& x) { return x.frame_num > sh.frame_num ? x.frame_num - max_fn : x.frame_num; };
-            return wrap(a) < wrap(b);
-          });
-          dpb.erase(it);
-        }
-        Ref r{fs, sh.frame_num, poc, next_uid, nullptr};
-        r.fields = u8(1 << par);
-        r.poc_f[par] = poc;
-        r.uid_f[par] = next_uid;
-        r.col_f[par] = build_col_motion(nb, W, Hp, slice_uids, sps.direct_8x8);
-        dpb.push_back(r);
-        prev_ref_fn = sh.frame_num;
-      }
+    if (job.ref && fld) {  // a frame entry holding its reference fields
+      mark_field_enc(sh, pic.target >> 1, poc, next_uid, job.parity == 1,
+                     build_col_motion(nb, W, Hp, slice_uids, sps.direct_8x8));
+      prev_ref_fn = sh.frame_num;
     } else if (job.ref) {
       mark_frame(sh, Ref{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)});
       prev_ref_fn = sh.frame_num;

@@ -48,3 +48,37 @@ def test_marking_covers_every_operation(native):
             total[k] = total.get(k, 0) + v
     for k in ("mmco1", "mmco2", "mmco3", "mmco4", "mmco6", "list_mods", "long_term_marked"):
         assert total[k] > 0, (k, total)
+
+
+FIELD = dict(interlaced=True, fields=True, cabac=False, t8x8=False)
+FIELD_CONFIGS = {
+    "fields-p-refs4": dict(bframes=0, refs=4),
+    "fields-p-refs4-cov": dict(bframes=0, refs=4, coverage=True),
+    "fields-ibbp": dict(bframes=2, refs=3),
+    "fields-ibbp-temporal-cov": dict(bframes=2, refs=3, coverage=True, direct_spatial=False),
+    "fields-ibp-implicit": dict(bframes=1, refs=2, weighted_b=2),
+}
+
+
+@pytest.mark.parametrize("name", sorted(FIELD_CONFIGS))
+@pytest.mark.parametrize("seed", [3, 5])
+def test_field_marking_and_list_modification_bit_exact(native, name, seed):
+    """The same in field pictures (§8.2.4.1 field picture numbers: 2 * FrameNumWrap + 1 for the
+    current parity; MMCOs mark single fields; the sliding window works on frames; the second
+    field of a pair whose first field is long-term is long-term too)."""
+    enc = high_encoder(native, 176, 144, gop=15, seed=seed, marking=True, **FIELD, **FIELD_CONFIGS[name])
+    rec, got, dec, aus = roundtrip(native, enc, 60)
+    assert set(got) == set(rec) and len(rec) == 30
+    for pts in rec:
+        assert np.array_equal(rec[pts][0], got[pts][0]) and np.array_equal(rec[pts][1], got[pts][1]), pts
+
+
+def test_field_marking_covers_every_operation(native):
+    total = {}
+    for name, seed in [("fields-p-refs4", 3), ("fields-ibbp", 4), ("fields-p-refs4-cov", 5), ("fields-ibbp", 3)]:
+        enc = high_encoder(native, 176, 144, gop=15, seed=seed, marking=True, **FIELD, **FIELD_CONFIGS[name])
+        _, _, dec, _ = roundtrip(native, enc, 60)
+        for k, v in dec.marking_stats.items():
+            total[k] = total.get(k, 0) + v
+    for k in ("mmco1", "mmco2", "mmco3", "mmco4", "mmco6", "list_mods", "long_term_marked"):
+        assert total[k] > 0, (k, total)

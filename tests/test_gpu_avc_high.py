@@ -32,6 +32,7 @@ GPU_CONFIGS = {
     "paff-1080-refs2": (1920, 1080, 12, dict(qp=26, refs=2, temporal_noise=2.0, **PAFF)),
     "paff-b-cov-temporal": (176, 144, 36, dict(PAFF, bframes=2, coverage=True, direct_spatial=False, weighted_b=2)),
     "paff-b-1080-ibbp": (1920, 1080, 18, dict(PAFF, bframes=2, qp=26, temporal_noise=2.0)),
+    "paff-marking-cov": (176, 144, 40, dict(PAFF, bframes=2, refs=3, coverage=True, marking=True)),
 }
 
 
