@@ -344,11 +344,10 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
     }
   }
   if (sh.field_pic) {
-    // Field pictures: CAVLC I / P / B with 4x4 transforms. CABAC needs the field-coded context
-    // initialisation values (not in any source this build can pin) and the 8x8 transform the 8x8
-    // field scan: those stay with the VCN backend, as does MMCO 5 in a field.
+    // Field pictures: CAVLC I / P / B. CABAC needs the field-coded context initialisation values
+    // (not in any source this build can pin): it stays with the VCN backend, as does MMCO 5 in a
+    // field.
     if (pps.cabac) throw UnsupportedStream("interlaced H.264: CABAC field pictures are not supported");
-    if (pps.transform_8x8_mode) throw UnsupportedStream("interlaced H.264: 8x8 transform in field pictures is not supported");
     if (sh.has_mmco5()) throw UnsupportedStream("interlaced H.264: MMCO 5 in field pictures is not supported");
   }
   return sh;

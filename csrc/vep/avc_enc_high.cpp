@@ -58,7 +58,7 @@ struct Idct8Inverse {
 const Idct8Inverse kInv8;
 
 // Levels (8x8 scan order) of residual x (raster 8x8) at qp with flat matrices.
-void quant8x8(const int* x, int qp, bool intra, int* lv) {
+void quant8x8(const int* x, int qp, bool intra, int* lv, const u8* scan = kZigzag8x8) {
   double t[64], d[64];
   for (int i = 0; i < 8; ++i)
     for (int j = 0; j < 8; ++j) {
@@ -74,7 +74,7 @@ void quant8x8(const int* x, int qp, bool intra, int* lv) {
     }
   const double f = intra ? 1.0 / 3 : 1.0 / 6;
   for (int k = 0; k < 64; ++k) {
-    const int pos = kZigzag8x8[k], i = pos >> 3, j = pos & 7;
+    const int pos = scan[k], i = pos >> 3, j = pos & 7;
     const double step = 16.0 * norm_adjust8(qp % 6, i, j) * std::ldexp(1.0, qp / 6) / 64.0;
     const double v = d[pos] / step;
     const int a = int(std::fabs(v) + f);
@@ -83,11 +83,11 @@ void quant8x8(const int* x, int qp, bool intra, int* lv) {
 }
 
 // Decoder-exact 8x8 dequantisation + inverse transform (flat matrices): residual samples.
-void recon8x8(const int* lv, int qp, int* r) {
+void recon8x8(const int* lv, int qp, int* r, const u8* scan = kZigzag8x8) {
   i16 d[64] = {};
   for (int k = 0; k < 64; ++k) {
     if (!lv[k]) continue;
-    const int pos = kZigzag8x8[k];
+    const int pos = scan[k];
     const int ls = 16 * norm_adjust8(qp % 6, pos >> 3, pos & 7);
     const int v = qp >= 36 ? (lv[k] * ls) * (1 << (qp / 6 - 6)) : (lv[k] * ls + (1 << (5 - qp / 6))) >> (6 - qp / 6);
     d[pos] = sat16(v);
@@ -145,14 +145,14 @@ struct AvcHighEncoder::Impl {
   HostSurface field_src;
   int pair_slot = -1, pair_fn = 0;
   const u8* scan4 = kZigzag4x4;  // 4x4 level scan of the current picture (field pictures: field scan)
+  const u8* scan8 = kZigzag8x8;
 
   explicit Impl(const AvcHighConfig& c) : cfg(c), rng{c.seed * 0x9E3779B97F4A7C15ull + 777} {
     VEP_CHECK(c.width >= 16 && c.height >= 16 && c.width % 2 == 0 && c.height % 2 == 0,
               "encoder size must be even and >= 16");
     VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.refs >= 1 && c.refs <= 8, "bframes 0..4, refs 1..8");
     VEP_CHECK(c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
-    VEP_CHECK(!c.fields || (c.interlaced && !c.cabac && !c.t8x8),
-              "field coding: interlaced CAVLC with 4x4 transforms only");
+    VEP_CHECK(!c.fields || (c.interlaced && !c.cabac), "field coding: interlaced CAVLC only");
     fields = c.fields;
     W = (c.width + 15) / 16;
     H = (c.height + 15) / 16;
@@ -908,7 +908,7 @@ struct AvcHighEncoder::Impl {
             const int yy = (q >> 1) * 8 + i, xx = (q & 1) * 8 + j;
             x[i * 8 + j] = S(mx * 16 + xx, my * 16 + yy) - py[yy * 16 + xx];
           }
-        quant8x8(x, qp, intra, d.l8[q]);
+        quant8x8(x, qp, intra, d.l8[q], scan8);
         for (int k = 0; k < 64; ++k)
           if (d.l8[q][k]) cl |= 1 << q;
       }
@@ -1108,9 +1108,9 @@ struct AvcHighEncoder::Impl {
             py[(by * 8 + i) * 16 + bx * 8 + j] = pb[i * 8 + j];
             x[i * 8 + j] = S(mx * 16 + bx * 8 + j, my * 16 + by * 8 + i) - pb[i * 8 + j];
           }
-        quant8x8(x, qp, true, d.l8[q]);
+        quant8x8(x, qp, true, d.l8[q], scan8);
         int r[64];
-        recon8x8(d.l8[q], qp, r);
+        recon8x8(d.l8[q], qp, r, scan8);
         for (int i = 0; i < 8; ++i)
           for (int j = 0; j < 8; ++j)
             t.y[size_t(my * 16 + by * 8 + i) * wpx + mx * 16 + bx * 8 + j] = u8(clip1(pb[i * 8 + j] + r[i * 8 + j]));
@@ -1262,6 +1262,7 @@ struct AvcHighEncoder::Impl {
       cur_src = &field_src;
     }
     scan4 = fld ? kFieldScan4x4 : kZigzag4x4;
+    scan8 = fld ? kFieldScan8x8 : kZigzag8x8;
     const bool idr = job.idr;
     if (idr) {
       dpb.clear();

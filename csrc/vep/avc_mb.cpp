@@ -72,7 +72,7 @@ class MbLayer {
  public:
   MbLayer(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const Dequant& dq)
       : nb_(nb), pic_(pic), env_(env), sh_(*env.sh), pps_(*env.pps), sps_(*env.sps), dq_(dq),
-        scan4_(env.field ? kFieldScan4x4 : kZigzag4x4) {
+        scan4_(env.field ? kFieldScan4x4 : kZigzag4x4), scan8_(env.field ? kFieldScan8x8 : kZigzag8x8) {
     type_ = sh_.type();
     qp_ = sh_.qp;
     weighted_ = (type_ == h264::kP && pps_.weighted_pred) || (type_ == h264::kB && pps_.weighted_bipred_idc != 0);
@@ -847,7 +847,7 @@ class MbLayer {
         bool nz = false;
         int total = 0;
         auto put = [&](int k, int level) {  // k: 8x8 scan position
-          const int pos = kZigzag8x8[k];
+          const int pos = scan8_[k];
           const int v = scale8(level, dq_.ls8[l8][qm][pos], qp);
           d[pos] = sat16(v);
           nz |= v != 0;
@@ -1012,6 +1012,7 @@ class MbLayer {
   const h264::Sps& sps_;
   const Dequant& dq_;
   const u8* scan4_;  // 4x4 scan: zig-zag (frame) or field
+  const u8* scan8_;  // 8x8 scan
   int type_ = 0;
   int qp_ = 26;
   bool weighted_ = false, implicit_ = false;

@@ -289,6 +289,14 @@ VEP_CONST static const u8 kZigzag8x8[64] = {
     41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
     30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+// 8x8 field scan (field pictures, Table 8-13): down the first columns first. Written from the
+// standard's table; no source in this image holds it to check against (the closed loop pins
+// encoder / decoder agreement only): parity unpinned.
+VEP_CONST static const u8 kFieldScan8x8[64] = {
+    0,  8,  16, 1,  9,  24, 32, 17, 2,  25, 40, 48, 56, 33, 10, 3,  18, 41, 49, 57, 26, 11,
+    4,  19, 34, 42, 50, 58, 27, 12, 5,  20, 35, 43, 51, 59, 28, 13, 6,  21, 36, 44, 52, 60,
+    29, 14, 22, 37, 45, 53, 61, 30, 7,  15, 38, 46, 54, 62, 23, 31, 39, 47, 55, 63};
+
 // normAdjust8x8 (§8.5.13.1): v[m][class] with the six position classes below.
 VEP_CONST static const u8 kNormAdjust8[6][6] = {{20, 18, 32, 19, 25, 24}, {22, 19, 35, 21, 28, 26},
                                                 {26, 23, 42, 24, 33, 31}, {28, 25, 45, 26, 35, 33},

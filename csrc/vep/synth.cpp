@@ -128,7 +128,7 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
       hc.interlaced = cfg.interlaced >= 1;
       if (cfg.interlaced == 2) {
         hc.fields = true;
-        hc.cabac = hc.t8x8 = false;
+        hc.cabac = false;
       }
       avc_ = std::make_unique<avc::AvcHighEncoder>(hc);
     } else {

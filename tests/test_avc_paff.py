@@ -15,10 +15,12 @@ picture, all exercised here by the closed-loop encoder (`AvcHighConfig.fields`):
   fields'), alternated by parity (§8.2.4.2.4 / §8.2.4.2.5); spatial and temporal direct from the
   colocated field (RefPicList1[0], its own motion table), implicit weights from field POCs.
 
-Coverage is CAVLC I / P / B fields with 4x4 transforms (the VCN backend's job otherwise): CABAC field
-pictures need the field-coded context tables (ctxIdx 277..398 / 436..459), which no source in
-this image holds (parity unpinned), and are reported as UnsupportedStream, as are streams mixing
-frame and field pictures between IDRs. The encoder and decoder share the macroblock layer, so the
+Coverage is CAVLC I / P / B fields, 4x4 and 8x8 transforms (the 8x8 field scan is written from
+the standard's table, which no source here holds to check against: the closed loop pins only the
+encoder / decoder agreement, parity unpinned). CABAC field pictures need the field-coded context
+tables (ctxIdx 277..398 / 436..459), which no source in this image holds (parity unpinned), and
+are reported as UnsupportedStream (the VCN backend's job), as are streams mixing frame and field
+pictures between IDRs. The encoder and decoder share the macroblock layer, so the
 closed loop pins their agreement; the field-specific rules above are each written from the spec
 tables (field scan, chroma offset, bS), and PSNR to the source checks the fields are the source's
 rows."""
@@ -53,9 +55,10 @@ def test_paff_closed_loop_bit_exact(native, kw):
 
 @pytest.mark.parametrize("kw", [dict(bframes=1), dict(bframes=2, weighted_b=2), dict(bframes=2, direct_spatial=False),
                                 dict(bframes=3, coverage=True), dict(bframes=2, weighted_b=1, refs=2, coverage=True),
-                                dict(bframes=2, slices=2, direct_spatial=False, coverage=True)],
+                                dict(bframes=2, slices=2, direct_spatial=False, coverage=True),
+                                dict(bframes=2, t8x8=True), dict(bframes=2, t8x8=True, coverage=True, scaling=True)],
                          ids=["ibp", "ibbp-implicit", "ibbp-temporal", "cov-b3", "cov-explicit-refs2",
-                              "cov-temporal-slices"])
+                              "cov-temporal-slices", "high-8x8", "high-8x8-cov-scaling"])
 def test_paff_b_fields_closed_loop(native, kw):
     """Non-reference B field pairs between I / P anchor pairs: the decoder's B-field lists, direct
     modes and implicit weights against the encoder's (every MB / sub-MB type in coverage mode)."""
@@ -68,6 +71,8 @@ def test_paff_b_fields_closed_loop(native, kw):
         assert np.array_equal(rec[pts][0], got[pts][0]) and np.array_equal(rec[pts][1], got[pts][1]), pts
     st = dec.mb_stats
     assert "B" in st["types"] and st["bipred"] > 0 and st["list1_only"] > 0
+    if kw.get("t8x8"):  # 8x8 transform with the 8x8 field scan, Intra_8x8
+        assert st["t8x8"] > 0 and st["i8x8"] > 0
 
 
 def test_paff_output_per_pair_and_quality(native):

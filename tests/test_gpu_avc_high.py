@@ -33,6 +33,7 @@ GPU_CONFIGS = {
     "paff-b-cov-temporal": (176, 144, 36, dict(PAFF, bframes=2, coverage=True, direct_spatial=False, weighted_b=2)),
     "paff-b-1080-ibbp": (1920, 1080, 18, dict(PAFF, bframes=2, qp=26, temporal_noise=2.0)),
     "paff-marking-cov": (176, 144, 40, dict(PAFF, bframes=2, refs=3, coverage=True, marking=True)),
+    "paff-high-8x8-cov": (176, 144, 36, dict(PAFF, bframes=2, t8x8=True, coverage=True)),
 }
 
 
