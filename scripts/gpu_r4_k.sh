@@ -25,4 +25,12 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$O/prof_paff" -o paff --o
   || { echo "rocprof failed"; tail -30 "$O/prof_paff.log"; exit 1; }
 cd "$R"
 ls "$O/prof_paff" | head
+echo "[k] serving with publish-latency percentiles"
+timeout -k 10 400 python -u tools/bench_serving.py --codec h265 --width 3840 --height 2160 --cams 8 --slices 8 \
+  --clients 8 --frontends 0,2 --duration 6 --out "$O/s4k_pub.jsonl" > "$O/s4k.log" 2>&1 \
+  || { echo "serving 4k failed"; tail -30 "$O/s4k.log"; exit 1; }
+cut -c1-900 "$O/s4k_pub.jsonl"
+timeout -k 10 400 python -u tools/bench_serving.py --cams 32 --clients 128 --frontends 2 --duration 6 \
+  --out "$O/s1080_pub.jsonl" > "$O/s1080.log" 2>&1 || { echo "serving 1080p failed"; tail -30 "$O/s1080.log"; exit 1; }
+cut -c1-900 "$O/s1080_pub.jsonl"
 echo "[k] done"

@@ -61,6 +61,32 @@ def cpu_of(pids) -> float:
     return t
 
 
+def hist_sum(w, cams):
+    tot, bounds = None, None
+    for c in cams:
+        st = w.stats(c)
+        h = st["latency_hist"]
+        bounds = st["latency_bounds_ms"]
+        tot = list(h) if tot is None else [a + b for a, b in zip(tot, h)]
+    return tot, bounds
+
+
+def hist_pct(h0, h1, q):
+    """Upper bound (ms) of the histogram bucket holding quantile q of the samples between two
+    snapshots (None: no samples; inf: the overflow bucket)."""
+    (a, bounds), (b, _) = h0, h1
+    d = [y - x for x, y in zip(a, b)]
+    n = sum(d)
+    if n <= 0:
+        return None
+    acc = 0
+    for i, v in enumerate(d):
+        acc += v
+        if acc >= q * n:
+            return bounds[i] if i < len(bounds) else float("inf")
+    return None
+
+
 def main() -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--cams", type=int, default=32)
@@ -152,6 +178,7 @@ def main() -> int:
                     s0 = cpu_of(srv_pids)
                     k0 = cpu_of([p.pid for p in pool._p[:procs]])
                     f0 = sum(w.published(c) for c in cams)
+                    h0 = hist_sum(w, cams)
                     t0 = time.perf_counter()
                     lat = pool.run(target, names, mode="next", duration_s=a.duration, procs=procs)
                     el = time.perf_counter() - t0
@@ -159,6 +186,7 @@ def main() -> int:
                     s1 = cpu_of(srv_pids)
                     k1 = cpu_of([p.pid for p in pool._p[:procs]])
                     f1 = sum(w.published(c) for c in cams)
+                    h1 = hist_sum(w, cams)
                 finally:
                     if ctx is not None:
                         ctx.__exit__(None, None, None)
@@ -170,6 +198,8 @@ def main() -> int:
                          samples=len(lat), frames_served_per_s=round(served, 1),
                          served_gbytes_per_s=round(served * a.width * a.height * 3 / 1e9, 2),
                          decoded_frames_per_s=round((f1 - f0) / el, 1),
+                         # packet arrival -> frame published (the worker's per-camera histogram)
+                         publish_latency_ms_p50=hist_pct(h0, h1, 0.5), publish_latency_ms_p99=hist_pct(h0, h1, 0.99),
                          bus_dma_frames=(owner.published - pub0) if k > 0 else None,
                          bus_dma_gbytes_per_s=round((owner.dma_bytes - dma0) / el / 1e9, 2) if k > 0 else None,
                          machine_cpu_busy=round(busy / el, 2),
