@@ -581,6 +581,7 @@ PYBIND11_MODULE(_vep, m) {
         for (int k = 1; k <= 6; ++k) s[py::str("mmco" + std::to_string(k))] = d.avc.mmco_ops[k];
         s["list_mods"] = d.avc.list_mods;
         s["long_term_marked"] = d.avc.long_term_marked;
+        s["redundant_slices_skipped"] = d.avc.redundant_slices_skipped;
         return s;
       })
       .def_property_readonly("general", [](const CpuDecoder& d) { return d.general; })

@@ -263,9 +263,8 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
     sh.delta_poc[0] = br.se();
     if (pps.bottom_field_pic_order && !sh.field_pic) sh.delta_poc[1] = br.se();
   }
-  if (pps.redundant_pic_cnt_present) {
-    if (br.ue() != 0) throw UnsupportedStream("redundant H.264 pictures are not supported");
-  }
+  if (pps.redundant_pic_cnt_present && (sh.redundant_pic_cnt = int(br.ue())) != 0)
+    return sh;  // a redundant coded picture's slice: ignored (the primary picture is decoded)
   const int st = sh.type();
   if (st == h264::kSP || st == h264::kSI) throw UnsupportedStream("H.264 SP / SI slices are not supported");
   if (st == h264::kB) sh.direct_spatial = br.u1();
@@ -1396,6 +1395,10 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
     check_sps_supported(sps);
     Bits br(r + 1, rn - 1);
     const SliceHdr sh = read_slice_header(br, p[0], sps, pps);
+    if (sh.redundant_pic_cnt > 0) {  // §7.4.3: a decoder may ignore redundant coded pictures
+      ++redundant_slices_skipped;
+      continue;
+    }
     if (!got) {
       first = sh;
       act_sps = &sps;

@@ -107,6 +107,7 @@ struct SliceHdr {
   int nal_type = 0, nal_ref_idc = 0;
   int first_mb = 0, slice_type = 0, pps_id = 0, frame_num = 0, idr_pic_id = 0;
   bool field_pic = false, bottom_field = false;
+  int redundant_pic_cnt = 0;  // > 0: a slice of a redundant coded picture (skipped)
   int poc_lsb = 0, delta_poc_bottom = 0, delta_poc[2] = {0, 0};
   bool direct_spatial = true;
   int num_ref_idx[2] = {1, 1};
@@ -457,6 +458,7 @@ class Decoder {
   // applied, pictures marked long-term
   u64 mmco_ops[7] = {0, 0, 0, 0, 0, 0, 0};
   u64 list_mods = 0, long_term_marked = 0;
+  u64 redundant_slices_skipped = 0;
 };
 
 // CPU reference reconstruction of `pic` into DPB surfaces `slots` (coded size; references are
