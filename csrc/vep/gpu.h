@@ -158,9 +158,17 @@ void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream
 // Main10 output: u16 NV12 planes (n luma samples, n / 2 chroma) -> 8-bit NV12 (round to nearest,
 // saturating), the form the BGR24 conversion and the letterbox read.
 void launch_narrow(const u16* y, const u16* uv, u8* y8, u8* uv8, size_t n, int bd, hipStream_t s);
-// H.264 field pair (frame slot in field-separated layout: top field rows, then bottom) -> the
-// interleaved 8-bit NV12 frame (pitch bytes per row, `height` luma rows).
-void launch_weave(const u8* y, const u8* uv, u8* y8, u8* uv8, int pitch, int height, hipStream_t s);
+// H.264 field pairs (frame slot in field-separated layout: top field rows, then bottom) -> the
+// interleaved 8-bit NV12 frames (pitch bytes per row, `height` luma rows), one launch for the
+// `n` descriptors of a batch (grid y = descriptor).
+struct WeaveDesc {
+  const VEP_DEV u8* y;
+  const VEP_DEV u8* uv;
+  VEP_DEV u8* y8;
+  VEP_DEV u8* uv8;
+  i32 pitch, height;
+};
+void launch_weave(const WeaveDesc* d_descs, int n, int max_pitch, int max_height, hipStream_t s);
 
 // ---- general H.264 reconstruction (gpu_avc.hip; records from avc::Decoder, avc.h) ----------
 // One picture of a batched reconstruction round (device memory). DPB slot k of the camera

@@ -1230,8 +1230,13 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
 
 // Field pair -> frame: the frame slot holds the top field's rows, then the bottom field's (luma
 // h / 2 rows each, chroma h / 4); frame row r is row r >> 1 of field r & 1. 16 bytes per lane.
-__global__ __launch_bounds__(256) void weave_kernel(const u8* __restrict__ y, const u8* __restrict__ uv,
-                                                    u8* __restrict__ y8, u8* __restrict__ uv8, int pitch, int h) {
+__global__ __launch_bounds__(256) void weave_kernel(const WeaveDesc* __restrict__ descs) {
+  const WeaveDesc d = descs[blockIdx.y];
+  const u8* __restrict__ y = d.y;
+  const u8* __restrict__ uv = d.uv;
+  u8* __restrict__ y8 = d.y8;
+  u8* __restrict__ uv8 = d.uv8;
+  const int pitch = d.pitch, h = d.height;
   const int per_row = pitch / 16;
   const size_t g = size_t(blockIdx.x) * 256 + threadIdx.x, total = size_t(per_row) * size_t(h + h / 2);
   if (g >= total) return;
@@ -1245,12 +1250,10 @@ __global__ __launch_bounds__(256) void weave_kernel(const u8* __restrict__ y, co
 
 }  // namespace
 
-void launch_weave(const u8* y, const u8* uv, u8* y8, u8* uv8, int pitch, int height, hipStream_t s) {
-  if (pitch <= 0 || height <= 0) return;
-  VEP_CHECK(pitch % 16 == 0 && height % 4 == 0, "weave: pitch / height alignment");
-  const size_t lanes = size_t(pitch / 16) * size_t(height + height / 2);
-  hipLaunchKernelGGL(weave_kernel, dim3(unsigned((lanes + 255) / 256)), dim3(256), 0, s, y, uv, y8, uv8, pitch,
-                     height);
+void launch_weave(const WeaveDesc* d_descs, int n, int max_pitch, int max_height, hipStream_t s) {
+  if (n <= 0 || max_pitch <= 0 || max_height <= 0) return;
+  const size_t lanes = size_t(max_pitch / 16) * size_t(max_height + max_height / 2);
+  hipLaunchKernelGGL(weave_kernel, dim3(unsigned((lanes + 255) / 256), unsigned(n)), dim3(256), 0, s, d_descs);
   VEP_HIP(hipGetLastError());
 }
 

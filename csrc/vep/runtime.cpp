@@ -1069,7 +1069,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   auto pinned = [](const void* p, size_t len) {
     return len > 0 && hostmem::device_address(static_cast<const u8*>(p), len) != nullptr;
   };
-  size_t need = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));
+  const size_t off_wv = off_lb + al(sizeof(gpu::LetterboxDesc) * size_t(n));  // field-pair weaves
+  size_t need = off_wv + al(sizeof(gpu::WeaveDesc) * size_t(n));
   std::vector<size_t> mask_off(static_cast<size_t>(n)), pay_off(static_cast<size_t>(n));
   std::vector<std::vector<size_t>> seg_off(static_cast<size_t>(n));
   auto words_of = [&](int i) { return size_t(jobs[size_t(i)].upd.mbs() + 31) / 32; };
@@ -1367,6 +1368,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
   std::memset(st.err, 0, size_t(n) * sizeof(u32));
   auto* hd = reinterpret_cast<gpu::DecodeDesc*>(st.h + off_desc);
   auto* hl = reinterpret_cast<gpu::LetterboxDesc*>(st.h + off_lb);
+  auto* hw = reinterpret_cast<gpu::WeaveDesc*>(st.h + off_wv);
+  int nweave = 0, weave_pitch = 0, weave_h = 0;
   int tiles = 0;
   // conversion / letterbox descriptors only for jobs that publish a frame (a general-path job
   // whose pictures all wait in the reorder buffer only reconstructs)
@@ -1381,6 +1384,20 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const size_t words = size_t(j.upd.mbs() + 31) / 32;
     gpu::DecodeDesc& d = hd[k];
     const size_t tgt = size_t(j.target());
+    if (j.out_fields) {  // field pair: woven into the 8-bit scratch first (launch_weave below)
+      const Camera::Surface& sf = c->surface;
+      VEP_CHECK(sf.y8 && sf.bps == 1 && sf.hmbs % 2 == 0,
+                "field pair output without its weave scratch");
+      gpu::WeaveDesc& w = hw[nweave++];
+      w.y = sf.y + tgt * sf.slot_y();
+      w.uv = sf.uv + tgt * sf.slot_uv();
+      w.y8 = sf.y8;
+      w.uv8 = sf.uv8;
+      w.pitch = sf.wmbs * 16;
+      w.height = sf.hmbs * 16;
+      weave_pitch = std::max(weave_pitch, w.pitch);
+      weave_h = std::max(weave_h, w.height);
+    }
     if (c->surface.bps == 2 || j.out_fields) {  // Main10 / field pair: convert / letterbox the
                                                 // 8-bit frame (launch_narrow / launch_weave below)
       d.y = c->surface.y8;
@@ -1641,16 +1658,11 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     VEP_HIP(hipMemcpy2DAsync(c->surface.uv, pitch, f.uv, f.pitch_uv, size_t(f.width), size_t(f.height / 2),
                              hipMemcpyDefault, cs));
   }
-  for (int i : outs) {  // Main10 pictures / field pairs: the published slot's 8-bit NV12 frame
+  gpu::launch_weave(reinterpret_cast<const gpu::WeaveDesc*>(st.d + off_wv), nweave, weave_pitch, weave_h, cs);
+  for (int i : outs) {  // Main10 pictures: the published slot's 8-bit NV12 copy
     const DecodeJob& j = jobs[size_t(i)];
     const Camera::Surface& sf = cams_[size_t(j.cam)]->surface;
     const size_t tgt = size_t(j.target());
-    if (j.out_fields) {
-      VEP_CHECK(sf.y8 && sf.bps == 1, "field pair output without its weave scratch");
-      gpu::launch_weave(sf.y + tgt * sf.slot_y(), sf.uv + tgt * sf.slot_uv(), sf.y8, sf.uv8, sf.wmbs * 16,
-                        sf.hmbs * 16, cs);
-      continue;
-    }
     if (sf.bps != 2) continue;
     gpu::launch_narrow(reinterpret_cast<const u16*>(sf.y + tgt * sf.slot_y()),
                        reinterpret_cast<const u16*>(sf.uv + tgt * sf.slot_uv()), sf.y8, sf.uv8,
