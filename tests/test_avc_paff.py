@@ -261,3 +261,39 @@ def live_paff_check(native, device):
         want = ref.get(ref_index(j, n_aus // 2))
         assert want is not None and np.array_equal(img, want), f"frame {j}"
     assert st["packets"] >= 2 * st["decoded"] - 2  # two access units (fields) per decoded frame
+
+
+def test_paff_corruption_never_crashes(native):
+    """Bit flips anywhere in field slices (headers included: parity, frame_num, POC, lists):
+    every access unit decodes or raises, nothing crashes, and the stream is bit-exact again from
+    the next IDR field pair on."""
+    import random
+
+    rnd = random.Random(7)
+    enc = paff_encoder(native, seed=9, gop=6, bframes=2, refs=2, coverage=True, marking=True)
+    aus = [enc.next() for _ in range(36)]  # 3 GOPs of 6 frames = 12 field AUs each
+    clean = native.CpuDecoder()
+    want = {}
+    for a in aus:
+        clean.decode(a)
+        for pts, (y, uv) in clean.frames():
+            want[pts] = y
+    for trial in range(16):
+        dec = native.CpuDecoder()
+        bad = rnd.randrange(1, 12)
+        for i, a in enumerate(aus):
+            if i == bad:
+                nals = [bytearray(n) for n in a.nals()]
+                k = [j for j, x in enumerate(nals) if (x[0] & 0x1F) in (1, 5)][0]
+                for _ in range(rnd.randint(1, 4)):
+                    pos = rnd.randrange(1, min(len(nals[k]), 12 if trial % 2 else len(nals[k])))
+                    nals[k][pos] ^= 1 << rnd.randrange(8)
+                a = native.AccessUnit.from_nals([bytes(x) for x in nals], a.pts, a.dts, a.keyframe)
+            try:
+                dec.decode(a)
+                frames = dec.frames()
+            except (native.NativeError, native.UnsupportedStream):
+                continue
+            if i >= 24:  # the third GOP: bit-exact again
+                for pts, (y, uv) in frames:
+                    assert np.array_equal(y, want[pts]), f"trial {trial}: AU {i}"
