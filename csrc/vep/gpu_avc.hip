@@ -904,6 +904,69 @@ __device__ inline int bs_of(const AvcDbkInfo& in, int dir, int e, int sg) {
 // luma lanes (0-15) and chroma lanes (16-31) of a half-wave run one filter body together instead
 // of the two type-specialised copies back to back. p2/p3/q2/q3 are read for chroma lines too
 // (in-bounds LDS of the DbkWave tile, values unused) and only p0/q0 are stored for them.
+// The filter on values (p0..p3, q0..q3 across the edge): false when the line is left as it is,
+// else the new p0..p2 / q0..q2 (chroma: p0 / q0 only).
+__device__ inline bool filter_vals(int p0, int p1, int p2, int p3, int q0, int q1, int q2, int q3, int bs, int alpha,
+                                   int beta, int tc0, bool chroma, int& np0, int& np1, int& np2, int& nq0, int& nq1,
+                                   int& nq2) {
+  if (!(avc::iabs(p0 - q0) < alpha && avc::iabs(p1 - p0) < beta && avc::iabs(q1 - q0) < beta)) return false;
+  const int ap = avc::iabs(p2 - p0), aq = avc::iabs(q2 - q0);
+  const bool lp = !chroma && ap < beta, lq = !chroma && aq < beta;
+  np1 = p1;
+  nq1 = q1;
+  np2 = p2;
+  nq2 = q2;
+  if (bs < 4) {
+    const int tc = chroma ? tc0 + 1 : tc0 + int(lp) + int(lq);
+    const int dl = avc::clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+    np0 = avc::clip1(p0 + dl);
+    nq0 = avc::clip1(q0 - dl);
+    if (lp) np1 = p1 + avc::clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
+    if (lq) nq1 = q1 + avc::clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
+  } else {
+    const bool strong = !chroma && avc::iabs(p0 - q0) < ((alpha >> 2) + 2);
+    if (lp && strong) {
+      np0 = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+      np1 = (p2 + p1 + p0 + q0 + 2) >> 2;
+      np2 = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+    } else {
+      np0 = (2 * p1 + p0 + q1 + 2) >> 2;
+    }
+    if (lq && strong) {
+      nq0 = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+      nq1 = (p0 + q0 + q1 + q2 + 2) >> 2;
+      nq2 = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+    } else {
+      nq0 = (2 * q1 + q0 + p1 + 2) >> 2;
+    }
+  }
+  return true;
+}
+
+// A vertical edge's line is contiguous in the LDS tile: luma p3..p0 / q0..q3 are two aligned
+// words (rows of 20 bytes, the edge 4 bytes from a word boundary), chroma p1 p0 / q0 q1 two
+// half-words; one load and one store each instead of a byte per sample.
+__device__ inline void filter_vert_luma(u8* row, int bs, int alpha, int beta, int tc0) {  // row: p3
+  u32* w = reinterpret_cast<u32*>(row);
+  const u32 P = w[0], Q = w[1];
+  int np0, np1, np2, nq0, nq1, nq2;
+  if (!filter_vals(int(P >> 24), int((P >> 16) & 255), int((P >> 8) & 255), int(P & 255), int(Q & 255),
+                   int((Q >> 8) & 255), int((Q >> 16) & 255), int(Q >> 24), bs, alpha, beta, tc0, false, np0, np1, np2,
+                   nq0, nq1, nq2))
+    return;
+  w[0] = (P & 255u) | u32(np2) << 8 | u32(np1) << 16 | u32(np0) << 24;
+  w[1] = u32(nq0) | u32(nq1) << 8 | u32(nq2) << 16 | (Q & 0xFF000000u);
+}
+__device__ inline void filter_vert_chroma(u8* pp, int bs, int alpha, int beta, int tc0) {  // pp: p1
+  u16* h = reinterpret_cast<u16*>(pp);
+  const u32 P = h[0], Q = h[1];
+  const int p1 = int(P & 255), p0 = int(P >> 8), q0 = int(Q & 255), q1 = int(Q >> 8);
+  int np0, np1, np2, nq0, nq1, nq2;
+  if (!filter_vals(p0, p1, p1, p1, q0, q1, q1, q1, bs, alpha, beta, tc0, true, np0, np1, np2, nq0, nq1, nq2)) return;
+  h[0] = u16(p1 | np0 << 8);
+  h[1] = u16(nq0 | q1 << 8);
+}
+
 __device__ inline void filter_line_any(u8* s, int step, int bs, int alpha, int beta, int tc0, bool chroma) {
   const int p0 = s[-step], p1 = s[-2 * step], q0 = s[0], q1 = s[step];
   const int p2 = s[-3 * step], p3 = s[-4 * step], q2 = s[2 * step], q3 = s[3 * step];
@@ -964,7 +1027,10 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    if (bs[e]) {
+    if (bs[e] && dir == 0) {  // vertical edge: packed LDS accesses
+      if (!ch) filter_vert_luma(&L.y[(4 + l) * 20 + 4 * e], bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0);
+      else filter_vert_chroma(&L.c[c][(2 + k) * 10 + 2 * e], bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0);
+    } else if (bs[e]) {
       u8* sp;
       int step;
       if (!ch) {
