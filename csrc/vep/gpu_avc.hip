@@ -945,26 +945,44 @@ __device__ inline bool filter_vals(int p0, int p1, int p2, int p3, int q0, int q
 
 // A vertical edge's line is contiguous in the LDS tile: luma p3..p0 / q0..q3 are two aligned
 // words (rows of 20 bytes, the edge 4 bytes from a word boundary), chroma p1 p0 / q0 q1 two
-// half-words; one load and one store each instead of a byte per sample.
-__device__ inline void filter_vert_luma(u8* row, int bs, int alpha, int beta, int tc0) {  // row: p3
-  u32* w = reinterpret_cast<u32*>(row);
-  const u32 P = w[0], Q = w[1];
+// half-words; one load and one store each instead of a byte per sample. The loads and stores
+// differ between luma and chroma lanes, the filter body between them is one (filter_vals) for
+// the whole half-wave, as in filter_line_any.
+__device__ inline void filter_vert_any(u8* q0p, int bs, int alpha, int beta, int tc0, bool chroma) {
+  int p0, p1, p2, p3, q0, q1, q2, q3;
+  u32 P = 0, Q = 0;
+  if (!chroma) {
+    const u32* w = reinterpret_cast<const u32*>(q0p - 4);
+    P = w[0];
+    Q = w[1];
+    p3 = int(P & 255);
+    p2 = int((P >> 8) & 255);
+    p1 = int((P >> 16) & 255);
+    p0 = int(P >> 24);
+    q0 = int(Q & 255);
+    q1 = int((Q >> 8) & 255);
+    q2 = int((Q >> 16) & 255);
+    q3 = int(Q >> 24);
+  } else {
+    const u16* h = reinterpret_cast<const u16*>(q0p - 2);
+    P = h[0];
+    Q = h[1];
+    p1 = p2 = p3 = int(P & 255);
+    p0 = int(P >> 8);
+    q0 = int(Q & 255);
+    q1 = q2 = q3 = int(Q >> 8);
+  }
   int np0, np1, np2, nq0, nq1, nq2;
-  if (!filter_vals(int(P >> 24), int((P >> 16) & 255), int((P >> 8) & 255), int(P & 255), int(Q & 255),
-                   int((Q >> 8) & 255), int((Q >> 16) & 255), int(Q >> 24), bs, alpha, beta, tc0, false, np0, np1, np2,
-                   nq0, nq1, nq2))
-    return;
-  w[0] = (P & 255u) | u32(np2) << 8 | u32(np1) << 16 | u32(np0) << 24;
-  w[1] = u32(nq0) | u32(nq1) << 8 | u32(nq2) << 16 | (Q & 0xFF000000u);
-}
-__device__ inline void filter_vert_chroma(u8* pp, int bs, int alpha, int beta, int tc0) {  // pp: p1
-  u16* h = reinterpret_cast<u16*>(pp);
-  const u32 P = h[0], Q = h[1];
-  const int p1 = int(P & 255), p0 = int(P >> 8), q0 = int(Q & 255), q1 = int(Q >> 8);
-  int np0, np1, np2, nq0, nq1, nq2;
-  if (!filter_vals(p0, p1, p1, p1, q0, q1, q1, q1, bs, alpha, beta, tc0, true, np0, np1, np2, nq0, nq1, nq2)) return;
-  h[0] = u16(p1 | np0 << 8);
-  h[1] = u16(nq0 | q1 << 8);
+  if (!filter_vals(p0, p1, p2, p3, q0, q1, q2, q3, bs, alpha, beta, tc0, chroma, np0, np1, np2, nq0, nq1, nq2)) return;
+  if (!chroma) {
+    u32* w = reinterpret_cast<u32*>(q0p - 4);
+    w[0] = (P & 255u) | u32(np2) << 8 | u32(np1) << 16 | u32(np0) << 24;
+    w[1] = u32(nq0) | u32(nq1) << 8 | u32(nq2) << 16 | (Q & 0xFF000000u);
+  } else {
+    u16* h = reinterpret_cast<u16*>(q0p - 2);
+    h[0] = u16((P & 255u) | u32(np0) << 8);
+    h[1] = u16(u32(nq0) | (Q & 0xFF00u));
+  }
 }
 
 __device__ inline void filter_line_any(u8* s, int step, int bs, int alpha, int beta, int tc0, bool chroma) {
@@ -1013,7 +1031,7 @@ __device__ inline void filter_line_any(u8* s, int step, int bs, int alpha, int b
 // filter_line_any on the LDS tile (chroma lines on the even edges only). The four edges' bS and
 // thresholds are read up front (one round of LDS loads), so each edge step is only its samples'
 // round trip.
-__device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
+__device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed) {
   const bool ch = l >= 16;
   const int c = (l - 16) >> 3, k = (l - 16) & 7;
   int bs[4], al[4], be[4], tc[4];
@@ -1027,9 +1045,9 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir) {
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    if (bs[e] && dir == 0) {  // vertical edge: packed LDS accesses
-      if (!ch) filter_vert_luma(&L.y[(4 + l) * 20 + 4 * e], bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0);
-      else filter_vert_chroma(&L.c[c][(2 + k) * 10 + 2 * e], bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0);
+    if (bs[e] && dir == 0 && packed) {  // vertical edge: packed LDS accesses
+      u8* q0p = !ch ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.c[c][(2 + k) * 10 + 2 + 2 * e];
+      filter_vert_any(q0p, bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0, ch);
     } else if (bs[e]) {
       u8* sp;
       int step;
@@ -1051,7 +1069,7 @@ struct DbkRegs {  // one MB's inputs as loaded from global memory (per lane of a
 };
 
 __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDesc* __restrict__ descs,
-                                                                      int n, int groups) {
+                                                                      int n, int groups, int packed) {
   // grid order: workgroup b runs on XCD b % 8; picture p's group k is b = ((p / 8) * groups +
   // k) * 8 + p % 8, so a picture stays on one XCD and its groups dispatch in order
   const int b = int(blockIdx.x), j = b >> 3;
@@ -1143,7 +1161,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     const bool wany = __ballot(any) != 0;
     // ---- vertical edges (per half: luma lanes 0-15, chroma 16-31): they touch only this MB's
     // rows, so they need nothing from the row above
-    if (wany) dbk_dir(L, any, l, 0);
+    if (wany) dbk_dir(L, any, l, 0, packed != 0);
     // ---- the previous MB's right columns are final now (this MB's left edge was the last
     // filter to touch them): complete its exchange entry for the row below, then publish
     // "vertical edges of MB x done" (the row below may filter MB x - 1's top edge)
@@ -1207,7 +1225,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     wave_sync();
     const u64 t5 = d.prof ? clock64() : 0;
     // ---- horizontal edges
-    if (wany) dbk_dir(L, any, l, 1);
+    if (wany) dbk_dir(L, any, l, 1, false);
     const u64 t6 = d.prof ? clock64() : 0;
     if (act) {
       // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left
@@ -1345,11 +1363,11 @@ void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s) 
   VEP_HIP(hipGetLastError());
 }
 
-void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s) {
+void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s, int packed) {
   if (n <= 0 || max_hmbs <= 0) return;
   const int groups = avc_dbk_groups(max_hmbs);
   const unsigned blocks = unsigned((n + 7) / 8) * unsigned(groups) * 8u;
-  hipLaunchKernelGGL(avc_deblock_kernel, dim3(blocks), dim3(64 * kDbkWaves), 0, s, d_descs, n, groups);
+  hipLaunchKernelGGL(avc_deblock_kernel, dim3(blocks), dim3(64 * kDbkWaves), 0, s, d_descs, n, groups, packed);
   VEP_HIP(hipGetLastError());
 }
 

@@ -522,6 +522,8 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       avc_prof_ = static_cast<u64*>(dev_.alloc(gpu::kAvcProfSlots * sizeof(u64)));
       VEP_HIP(hipMemset(avc_prof_, 0, gpu::kAvcProfSlots * sizeof(u64)));
     }
+    const char* dp = std::getenv("VEP_DBK_PACKED");
+    dbk_packed_ = (dp && dp[0] == '0') ? 0 : 1;
     const char* dr = std::getenv("VEP_DIRECT_READS");
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
@@ -1608,7 +1610,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     if (intra) gpu::launch_avc_intra(ad, np, max_h, cs);
     if (dbk) {
       gpu::launch_avc_bs(ad, np, mbs, cs);
-      gpu::launch_avc_deblock(ad, np, max_h, cs);
+      gpu::launch_avc_deblock(ad, np, max_h, cs, dbk_packed_);
     }
   }
   for (int r = 0; r < hrounds; ++r) {

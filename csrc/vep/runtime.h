@@ -493,6 +493,7 @@ class Worker {
   std::mutex timers_mu_;
   bool direct_reads_ = false;
   u64* avc_prof_ = nullptr;
+  int dbk_packed_ = 1;  // VEP_DBK_PACKED=0: the deblocking filter's byte-wise vertical edges (A/B)
 
  public:
   bool direct_reads() const { return direct_reads_; }
