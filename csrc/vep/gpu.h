@@ -233,7 +233,8 @@ void launch_avc_intra(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s
 // deblocking wavefront over them: avc_dbk_groups(hmbs) workgroups of kAvcDbkWgRows / 2 wave64s
 // per picture, spread over the XCDs picture-wise (a picture's workgroups share one L2).
 void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
-// packed: vertical edges with word / half-word LDS accesses (VEP_DBK_PACKED=0: a byte per sample)
+// packed: bit 0 vertical edges with word / half-word LDS accesses (VEP_DBK_PACKED=0: a byte per
+// sample); bit 1 a wave sync after every edge instead of one per direction (VEP_DBK_SYNC=1)
 void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s, int packed = 1);
 
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };

@@ -1031,7 +1031,7 @@ __device__ inline void filter_line_any(u8* s, int step, int bs, int alpha, int b
 // filter_line_any on the LDS tile (chroma lines on the even edges only). The four edges' bS and
 // thresholds are read up front (one round of LDS loads), so each edge step is only its samples'
 // round trip.
-__device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed) {
+__device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed, bool sync_each) {
   const bool ch = l >= 16;
   const int c = (l - 16) >> 3, k = (l - 16) & 7;
   int bs[4], al[4], be[4], tc[4];
@@ -1060,8 +1060,14 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed
       }
       filter_line_any(sp, step, bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0, ch);
     }
-    wave_sync();
+    // Within one direction every lane filters its own line (a row for vertical edges, a column
+    // for horizontal ones) through all four edges: edge e + 1 reads only what this lane wrote at
+    // edge e, which a wave's in-order LDS accesses already order. Other lanes read it only in
+    // the other direction, so one sync per direction, after its last edge (VEP_DBK_SYNC=0 keeps
+    // one per edge, for A/B).
+    if (sync_each) wave_sync();
   }
+  if (!sync_each) wave_sync();
 }
 
 struct DbkRegs {  // one MB's inputs as loaded from global memory (per lane of a half-wave)
@@ -1161,7 +1167,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     const bool wany = __ballot(any) != 0;
     // ---- vertical edges (per half: luma lanes 0-15, chroma 16-31): they touch only this MB's
     // rows, so they need nothing from the row above
-    if (wany) dbk_dir(L, any, l, 0, packed != 0);
+    if (wany) dbk_dir(L, any, l, 0, (packed & 1) != 0, (packed & 2) != 0);
     // ---- the previous MB's right columns are final now (this MB's left edge was the last
     // filter to touch them): complete its exchange entry for the row below, then publish
     // "vertical edges of MB x done" (the row below may filter MB x - 1's top edge)
@@ -1225,7 +1231,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     wave_sync();
     const u64 t5 = d.prof ? clock64() : 0;
     // ---- horizontal edges
-    if (wany) dbk_dir(L, any, l, 1, false);
+    if (wany) dbk_dir(L, any, l, 1, false, (packed & 2) != 0);
     const u64 t6 = d.prof ? clock64() : 0;
     if (act) {
       // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left

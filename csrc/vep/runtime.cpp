@@ -523,7 +523,8 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       VEP_HIP(hipMemset(avc_prof_, 0, gpu::kAvcProfSlots * sizeof(u64)));
     }
     const char* dp = std::getenv("VEP_DBK_PACKED");
-    dbk_packed_ = (dp && dp[0] == '0') ? 0 : 1;
+    const char* ds = std::getenv("VEP_DBK_SYNC");  // 1: a wave sync after every edge (A/B)
+    dbk_packed_ = ((dp && dp[0] == '0') ? 0 : 1) | ((ds && ds[0] == '1') ? 2 : 0);
     const char* dr = std::getenv("VEP_DIRECT_READS");
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
