@@ -416,14 +416,16 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                 h.wait()
         sync()
         t1 = time.perf_counter()
+        # every counter is sampled at the end of this rank's timed region, before the barrier: the
+        # unthrottled farm keeps feeding (and the worker decoding) while a rank waits for the others
+        rg1 = worker.records_gathered
+        pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
+        s1 = farm.stats()
         if world > 1:
             dist.barrier()
         elapsed = t1 - t0
-        rg1 = worker.records_gathered  # (sampled here: the farm keeps feeding after the timed loop)
         if hostprof:
             vep.hostprof_stop(hostprof)
-        pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
-        s1 = farm.stats()
         gpu_ms = worker.gpu_ms_total - g0
         wire_bytes = s1["bytes_in"] - s0["bytes_in"]
         errors = s1["errors"] - s0["errors"]
@@ -688,16 +690,17 @@ def main():
     drain()
     t1 = time.perf_counter()
     end_bytes = (worker.bytes_inplace, worker.bytes_staged, worker.records_gathered)
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    # frames committed to the camera rings (readable by clients), not jobs launched
+    # frames committed to the camera rings (readable by clients), not jobs launched; sampled at the
+    # end of this rank's timed region, before the barrier
     frames = worker.frames - f0
     launched = rb.frames - l0
     dropped = (worker.dropped - d0) + (rb.parse_failures - pf0)
     parse_ms, batch_ms, gpu_ms = rb.parse_ms - p0, rb.batch_ms - b0, worker.gpu_ms_total - g0
     parse_wait_ms = rb.parse_wait_ms - pw0
     tm1 = worker.timings()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
