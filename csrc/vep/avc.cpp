@@ -1633,6 +1633,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       mark_references(first, *act_sps, pic->target, pic->poc, uid, std::move(col_built));
     }
     const bool boundary = first.idr() || first.has_mmco5();
+    // MMCO 5: the picture's POC becomes 0 (tempPicOrderCnt subtracted, §8.2.1), for output order
+    // too: it starts the new period the later pictures' POCs count from
+    if (first.has_mmco5()) pic->poc = 0;
     bump(*pic, out_of(*pic), boundary, boundary && (hard_flush || reorder_cur_ == 0));
   }
   // (store_mb validated every record as it was written; concealed ones are built in range)

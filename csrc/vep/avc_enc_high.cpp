@@ -402,6 +402,11 @@ struct AvcHighEncoder::Impl {
     }
     const int r = rng.uni(100);
     int max_lt = max_lt_idx;
+    if (cfg.bframes == 0 && r >= 93) {  // MMCO 5 alone (POC and frame_num restart; no B pictures
+      sh.mmcos.assign(1, {5, 0, 0});   // to reorder around it)
+      sh.adaptive_marking = true;
+      return;
+    }
     if (r < 20) {
       max_lt = std::max(kept_lt, rng.uni(3) - 1);  // max_long_term_frame_idx_plus1 0..2
       sh.mmcos.push_back({4, max_lt + 1, 0});
@@ -450,6 +455,12 @@ struct AvcHighEncoder::Impl {
           case 4:
             max_lt_idx = m.a - 1;
             erase_if([&](const Ref& r) { return r.long_term && r.lt_idx > max_lt_idx; });
+            break;
+          case 5:  // every reference unused; this picture becomes frame_num 0, POC 0
+            dpb.clear();
+            max_lt_idx = -1;
+            cur.frame_num = 0;
+            cur.poc = 0;
             break;
           case 6:
             erase_if([&](const Ref& r) { return r.long_term && r.lt_idx == m.a; });
@@ -1423,6 +1434,10 @@ struct AvcHighEncoder::Impl {
     } else if (job.ref) {
       mark_frame(sh, Ref{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)});
       prev_ref_fn = sh.frame_num;
+      if (sh.has_mmco5()) {  // the picture now counts as frame_num 0, POC 0 (§8.2.1)
+        prev_ref_fn = 0;
+        gop_start = job.disp;
+      }
     }
     ++next_uid;
     if (!fld) {

@@ -3,7 +3,8 @@
 The Main / High encoder's `marking` mode writes, at random, ref_pic_list_modification commands
 (short-term pictures coded relative to picNumPred with wrap-around, long-term pictures by
 LongTermPicNum), adaptive marking with MMCO 1 (short-term unused), 2 (long-term unused),
-3 (short-term -> long-term), 4 (MaxLongTermFrameIdx) and 6 (current picture long-term), and IDR
+3 (short-term -> long-term), 4 (MaxLongTermFrameIdx), 5 (everything unused, POC / frame_num
+restart; streams without B pictures) and 6 (current picture long-term), and IDR
 pictures marked long-term (long_term_reference_flag). The decoder's lists (long-term pictures
 after the short-term ones, by LongTermFrameIdx), its marking, temporal direct with long-term
 references (mvL0 = mvCol, mvL1 = 0) and implicit weights (default weights when a long-term
@@ -46,8 +47,23 @@ def test_marking_covers_every_operation(native):
         _, _, dec, _ = roundtrip(native, enc, 45)
         for k, v in dec.marking_stats.items():
             total[k] = total.get(k, 0) + v
-    for k in ("mmco1", "mmco2", "mmco3", "mmco4", "mmco6", "list_mods", "long_term_marked"):
+    for k in ("mmco1", "mmco2", "mmco3", "mmco4", "mmco5", "mmco6", "list_mods", "long_term_marked"):
         assert total[k] > 0, (k, total)
+
+
+def test_mmco5_restarts_poc_and_frame_num(native):
+    """MMCO 5 (P streams): every reference goes, the picture counts as frame_num 0 and POC 0
+    from then on — for output order too (§8.2.1: the picture's POC minus tempPicOrderCnt). A
+    decoder that kept its old POC would drop the following pictures as late."""
+    seen = 0
+    for seed in (3, 4, 5):
+        enc = high_encoder(native, 176, 144, gop=30, seed=seed, marking=True, bframes=0, refs=4)
+        rec, got, dec, _ = roundtrip(native, enc, 60)
+        assert set(got) == set(rec) and len(rec) == 60
+        for pts in rec:
+            assert np.array_equal(rec[pts][0], got[pts][0]), pts
+        seen += dec.marking_stats["mmco5"]
+    assert seen > 0
 
 
 FIELD = dict(interlaced=True, fields=True, cabac=False, t8x8=False)
