@@ -347,7 +347,10 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
     // (not in any source this build can pin): it stays with the VCN backend, as does MMCO 5 in a
     // field.
     if (pps.cabac) throw UnsupportedStream("interlaced H.264: CABAC field pictures are not supported");
-    if (sh.has_mmco5()) throw UnsupportedStream("interlaced H.264: MMCO 5 in field pictures is not supported");
+    // MMCO 5 in the first field of a pair (the second field then carries frame_num 0); in a
+    // second field it would also drop the pair's first field: not supported
+    if (sh.has_mmco5() && sh.adaptive_marking && sh.mmcos.size() != 1)
+      throw UnsupportedStream("interlaced H.264: MMCO 5 with other MMCOs in a field is not supported");
   }
   return sh;
 }
@@ -726,7 +729,7 @@ void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, 
       if (r.slot == slot && r.frame_num == sh.frame_num && ((r.fields | r.lt_fields) & 3)) return &r;
     return nullptr;
   };
-  bool cur_long = false;
+  bool cur_long = false, mmco5 = false;
   int cur_lt = 0;
   if (sh.idr() && !second) {
     dpb_.clear();
@@ -779,7 +782,13 @@ void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, 
           cur_lt = m.a;
           ++long_term_marked;
           break;
-        default:  // (5 is rejected with the slice header)
+        case 5:  // every reference unused; this field counts as frame_num 0, POC 0 (first field only)
+          if (second) throw UnsupportedStream("interlaced H.264: MMCO 5 in a second field is not supported");
+          for (auto& r : dpb_) r.fields = r.lt_fields = 0;
+          max_lt_idx_ = -1;
+          mmco5 = true;
+          break;
+        default:
           break;
       }
     }
@@ -810,12 +819,13 @@ void Decoder::mark_field(const SliceHdr& sh, const Sps& sps, int slot, int poc, 
     }
   dpb_.erase(std::remove_if(dpb_.begin(), dpb_.end(), [](const RefPic& r) { return !((r.fields | r.lt_fields) & 3); }),
              dpb_.end());
+  if (mmco5) poc = 0;
   RefPic* e = cur_entry();
   if (!e) {
     dpb_.push_back(RefPic{});
     e = &dpb_.back();
     e->slot = slot;
-    e->frame_num = sh.frame_num;
+    e->frame_num = mmco5 ? 0 : sh.frame_num;
     e->poc = poc;
     e->uid = uid;
     e->fields = 0;
@@ -1626,6 +1636,13 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
   if (first.field_pic) {
     if (first.nal_ref_idc != 0)
       mark_field(first, *act_sps, pic->target >> 1, pic->poc, uid, second_field && pair_.ref, std::move(col_built));
+    if (first.has_mmco5() && !second_field) {  // POC / frame_num restart (§8.2.1): the pair
+      pic->poc = 0;                            // continues with frame_num 0 and a new period
+      pair_.frame_num = 0;
+      pair_.poc[int(first.bottom_field)] = 0;
+      pair_.boundary = true;
+      pair_.hard = reorder_cur_ == 0;
+    }
     if (second_field) close_pair(*pic);  // the frame is complete
   } else {
     if (first.nal_ref_idc != 0) {

@@ -679,6 +679,11 @@ struct AvcHighEncoder::Impl {
     }
     const int rr = rng.uni(100);
     int max_lt = max_lt_idx;
+    if (parity == 0 && cfg.bframes == 0 && rr >= 94) {  // MMCO 5 alone, in a first field
+      sh.mmcos.assign(1, {5, 0, 0});
+      sh.adaptive_marking = true;
+      return;
+    }
     if (rr < 15) {
       max_lt = std::max(kept_lt, rng.uni(3) - 1);
       sh.mmcos.push_back({4, max_lt + 1, 0});
@@ -708,7 +713,7 @@ struct AvcHighEncoder::Impl {
         if (r.slot == slot && r.frame_num == sh.frame_num && ((r.fields | r.lt_fields) & 3)) return &r;
       return nullptr;
     };
-    bool cur_long = false;
+    bool cur_long = false, mmco5 = false;
     int cur_lt = 0;
     if (sh.idr() && !second) {
       dpb.clear();
@@ -750,6 +755,11 @@ struct AvcHighEncoder::Impl {
             for (Ref& r : dpb)
               if ((r.lt_fields & 3) && r.lt_idx > max_lt_idx) r.lt_fields = 0;
             break;
+          case 5:  // (first fields only, see choose_field_mmcos)
+            for (Ref& r : dpb) r.fields = r.lt_fields = 0;
+            max_lt_idx = -1;
+            mmco5 = true;
+            break;
           case 6:
             for (Ref& r : dpb)
               if (&r != self && (r.lt_fields & 3) && r.lt_idx == m.a) r.lt_fields = 0;
@@ -778,9 +788,10 @@ struct AvcHighEncoder::Impl {
         cur_lt = f->lt_idx;
       }
     dpb.erase(std::remove_if(dpb.begin(), dpb.end(), [](const Ref& r) { return !((r.fields | r.lt_fields) & 3); }), dpb.end());
+    if (mmco5) poc = 0;
     Ref* e = cur_entry();
     if (!e) {
-      dpb.push_back(Ref{slot, sh.frame_num, poc, uid, nullptr});
+      dpb.push_back(Ref{slot, mmco5 ? 0 : sh.frame_num, poc, uid, nullptr});
       e = &dpb.back();
       e->fields = 0;
     }
@@ -1431,6 +1442,10 @@ struct AvcHighEncoder::Impl {
       mark_field_enc(sh, pic.target >> 1, poc, next_uid, job.parity == 1,
                      build_col_motion(nb, W, Hp, slice_uids, sps.direct_8x8));
       prev_ref_fn = sh.frame_num;
+      if (sh.has_mmco5()) {  // the pair continues with frame_num 0; POCs count from this frame
+        prev_ref_fn = pair_fn = 0;
+        gop_start = job.disp;
+      }
     } else if (job.ref) {
       mark_frame(sh, Ref{pic.target, sh.frame_num, poc, next_uid, build_col_motion(nb, W, H, slice_uids, sps.direct_8x8)});
       prev_ref_fn = sh.frame_num;

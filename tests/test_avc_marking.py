@@ -98,3 +98,17 @@ def test_field_marking_covers_every_operation(native):
             total[k] = total.get(k, 0) + v
     for k in ("mmco1", "mmco2", "mmco3", "mmco4", "mmco6", "list_mods", "long_term_marked"):
         assert total[k] > 0, (k, total)
+
+
+def test_field_mmco5_restarts_the_pair(native):
+    """MMCO 5 in the first field of a pair: every reference goes, the field counts as frame_num 0
+    and POC 0, and its pair's second field follows with frame_num 0 (P field streams)."""
+    seen = 0
+    for seed in (4, 5):
+        enc = high_encoder(native, 176, 144, gop=30, seed=seed, marking=True, **FIELD, bframes=0, refs=4)
+        rec, got, dec, _ = roundtrip(native, enc, 80)
+        assert set(got) == set(rec) and len(rec) == 40
+        for pts in rec:
+            assert np.array_equal(rec[pts][0], got[pts][0]), pts
+        seen += dec.marking_stats["mmco5"]
+    assert seen > 0
