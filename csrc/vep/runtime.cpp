@@ -708,11 +708,30 @@ static void fold_update(MbUpdate& into, const MbUpdate& from) {
   into.frames += from.frames;
 }
 
+// Whether one of the job's own pictures reconstructs its output slot.
+static bool reconstructs_output(const DecodeJob& j) {
+  for (const auto& p : j.avc)
+    if ((p->structure ? p->target / 2 : p->target) == j.out_slot) return true;
+  for (const auto& p : j.hevc)
+    if (p->target == j.out_slot) return true;
+  return false;
+}
+
 void merge_job(DecodeJob& p, DecodeJob&& job) {
   VEP_CHECK(p.cam == job.cam, "merge_job: different cameras");
   // collapse into the not-yet-launched job: latest writer wins per macroblock (fast path);
   // general-path pictures are appended (each references the previous ones)
-  if (job.general() && p.general() && !job.refresh) {
+  if (job.general() && p.general() && job.refresh) {
+    // A backlog that reaches a keyframe restarts from it (load shedding: the queued pictures are
+    // dropped). The keyframe bumps the previous GOP's pictures out of the reorder buffer; when the
+    // frame it would publish is one of those, its reconstruction was in the dropped job, so the
+    // merged job only reconstructs (the keyframe's picture is published by a later job).
+    p = std::move(job);
+    if (p.out_slot >= 0 && !reconstructs_output(p)) {
+      p.out_slot = -1;
+      p.out_fields = false;
+    }
+  } else if (job.general() && p.general()) {
     p.avc.insert(p.avc.end(), job.avc.begin(), job.avc.end());
     p.hevc.insert(p.hevc.end(), job.hevc.begin(), job.hevc.end());
     p.hevc_slots = std::max(p.hevc_slots, job.hevc_slots);
@@ -1794,6 +1813,8 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
         cp->errors.fetch_add(1, std::memory_order_relaxed);
         cp->logs.add(true, "GPU reconstruction wavefront timed out; waiting for the next keyframe");
         cp->broken_ = true;
+      } else if (jobs[i].refresh) {
+        cp->broken_ = false;  // a keyframe reconstructed (its picture is published later)
       }
       continue;
     }

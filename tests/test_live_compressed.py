@@ -127,6 +127,38 @@ def test_live_compressed_stream_bit_exact(native, profile):
         assert {m["frame_type"] for _, _, m in got} >= {"B", "P"}
 
 
+@pytest.mark.parametrize("device", [-1, pytest.param(0, marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("chunk", [2, 3, 4, 7])
+def test_backlog_across_idr_publishes_the_output_picture(native, chunk, device):
+    """A worker that falls behind merges a camera's queued jobs into one (GOP catch-up collapse);
+    a backlog that reaches an IDR restarts from it (the queued pictures are dropped). The IDR
+    bumps the previous GOP's pictures out of the reorder buffer: a frame whose reconstruction was
+    dropped must not be published (it would be a stale surface). Deterministic twin of a live-farm
+    flake ("AU 27 (P) differs") that showed up only on a loaded host."""
+    n = 20
+    cfg = stream_cfg(native, "high")
+    ref, aus = reference(native, cfg, n, loops=2)
+    step = 90000 // cfg.fps
+    wk = native.Worker(device=device)
+    cam = wk.add_camera("backlog", 4)
+    seq, checked = 0, 0
+    for k0 in range(0, 2 * n, chunk):
+        batch = []
+        for k in range(k0, min(k0 + chunk, 2 * n)):
+            a = aus[k % n]
+            batch.append(native.AccessUnit.from_nals(a.nals(), pts=k * step, dts=k * step, keyframe=a.keyframe))
+        wk.decode_many([(cam, batch)])  # one merged job per chunk
+        r = wk.read_latest(cam, seq)
+        if r is None:
+            continue
+        meta, img = r
+        seq = meta["seq"]
+        k = meta["pts"] // step
+        assert np.array_equal(img, ref[k]), f"chunk ending at AU {k0 + chunk - 1}: AU {k} ({meta['frame_type']}) stale"
+        checked += 1
+    assert checked >= 2 * n // chunk - 5  # (a chunk that crosses an IDR may publish nothing)
+
+
 def test_live_gop_catch_up_after_late_query(native):
     """No client for the first half second (nothing decoded), then a query mid-GOP: the lazy
     decoder catches up from the GOP's keyframe and the first frame it publishes is already the
