@@ -344,6 +344,31 @@ class RtspFarm:
         self.worker.stop()
 
 
+def thread_cpu() -> dict:
+    """CPU seconds of this process's threads by name (/proc/self/task/*/comm; the native threads
+    name themselves by role: vep-parse, vep-io, vep-worker, vep-farm, ...)."""
+    tick = os.sysconf("SC_CLK_TCK")
+    out = {}
+    for tid in os.listdir("/proc/self/task"):
+        try:
+            with open(f"/proc/self/task/{tid}/comm") as f:
+                name = f.read().strip()
+            with open(f"/proc/self/task/{tid}/stat") as f:
+                st = f.read().rsplit(")", 1)[1].split()
+        except OSError:  # (a thread that ended meanwhile)
+            continue
+        name = name if name.startswith("vep-") else "other (python / grpc / hip)"
+        out[name] = out.get(name, 0.0) + (int(st[11]) + int(st[12])) / tick  # utime + stime
+    return out
+
+
+def cpu_cores_by_thread(c0: dict, c1: dict, elapsed: float) -> dict:
+    d = {k: round((c1.get(k, 0.0) - c0.get(k, 0.0)) / elapsed, 2) for k in set(c0) | set(c1)}
+    d = {k: v for k, v in sorted(d.items(), key=lambda kv: -kv[1]) if v > 0}
+    d["total"] = round(sum(d.values()), 2)
+    return d
+
+
 def avc_cycles_per_mb(worker) -> dict:
     """VEP_AVC_PROF=1: the H.264 wavefront kernels' per-phase clocks, per macroblock."""
     pr = worker.avc_profile()
@@ -401,6 +426,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         if hostprof:
             vep.hostprof_start(1000)
         handles = [None, None]
+        cpu0 = thread_cpu()
         t0 = time.perf_counter()
         for i in range(a.steps):
             farm.wait_pictures(p0 + cams * (i + 1))
@@ -421,12 +447,16 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         rg1 = worker.records_gathered
         pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
         s1 = farm.stats()
+        cpu1 = thread_cpu()
         if world > 1:
             dist.barrier()
         elapsed = t1 - t0
         if hostprof:
             vep.hostprof_stop(hostprof)
         gpu_ms = worker.gpu_ms_total - g0
+        # where the host's CPU went in the timed region (the in-process farm included): cores busy
+        # per thread role, this rank's process
+        side["rank0_host_cpu_cores_by_thread"] = cpu_cores_by_thread(cpu0, cpu1, t1 - t0)
         wire_bytes = s1["bytes_in"] - s0["bytes_in"]
         errors = s1["errors"] - s0["errors"]
         aus = s1["packets"] - s0["packets"]  # access units through Camera::on_access_unit

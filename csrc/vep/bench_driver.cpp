@@ -44,7 +44,10 @@ ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cach
   cam_tick_.assign(size_t(ncams), 0);
   cam_busy_.assign(size_t(ncams), 0);
   cam_thread_.assign(size_t(ncams), -1);
-  for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this, i] { parse_loop(i); });
+  for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this, i] {
+    name_thread("vep-bparse");
+    parse_loop(i);
+  });
 }
 
 ReplayBench::~ReplayBench() {

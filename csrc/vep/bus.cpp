@@ -149,7 +149,10 @@ void Owner::attach(Worker* w) {
   VEP_CHECK(!w_, "bus owner already attached");
   w_ = w;
   w_->set_publish_hook([this](int cam, i64 seq) { on_publish(cam, seq); });
-  th_ = std::thread([this] { pump(); });
+  th_ = std::thread([this] {
+    name_thread("vep-pump");
+    pump();
+  });
 }
 
 void Owner::stop() {

@@ -1,6 +1,8 @@
 // vep — MI355X-native multi-camera video edge hub: shared native utilities.
 #pragma once
 
+#include <pthread.h>
+
 #include <atomic>
 #include <chrono>
 #include <cstddef>
@@ -33,6 +35,10 @@ inline i64 now_ms() {
   using namespace std::chrono;
   return duration_cast<milliseconds>(system_clock::now().time_since_epoch()).count();
 }
+
+// Names the calling thread (at most 15 characters; /proc/<pid>/task/<tid>/comm): the bench's
+// per-role CPU accounting and `top -H` tell the parse pool from the I/O loops and the GPU feeder.
+inline void name_thread(const char* name) { ::pthread_setname_np(::pthread_self(), name); }
 
 inline i64 mono_us() {
   using namespace std::chrono;

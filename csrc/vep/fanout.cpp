@@ -9,7 +9,10 @@
 namespace vep {
 
 FanOut::FanOut(int threads) {
-  for (int i = 0; i < threads; ++i) th_.emplace_back([this] { loop(); });
+  for (int i = 0; i < threads; ++i) th_.emplace_back([this] {
+    name_thread("vep-fanout");
+    loop();
+  });
 }
 
 FanOut::~FanOut() {

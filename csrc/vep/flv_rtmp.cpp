@@ -452,13 +452,17 @@ void RtmpSink::start() {
   lfd_ = sock::listen_tcp(bind_, port_);
   stop_ = false;
   acc_ = std::thread([this] {
+    name_thread("vep-rtmpsink");
     while (!stop_.load()) {
       pollfd p{lfd_, POLLIN, 0};
       if (::poll(&p, 1, 100) <= 0) continue;
       int fd = ::accept4(lfd_, nullptr, nullptr, SOCK_CLOEXEC);
       if (fd < 0) continue;
       live_.fetch_add(1);
-      std::thread([this, fd] { serve(fd); }).detach();
+      std::thread([this, fd] {
+        name_thread("vep-rtmpsink");
+        serve(fd);
+      }).detach();
     }
   });
 }

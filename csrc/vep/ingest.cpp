@@ -114,7 +114,10 @@ void IngestSession::start() {
   const char* th = std::getenv("VEP_INGEST_THREADS");
   pooled_ = !(th && th[0] == '1');
   if (!pooled_) {
-    th_ = std::thread([this] { run(); });
+    th_ = std::thread([this] {
+      name_thread("vep-ingest");
+      run();
+    });
     return;
   }
   svc_ = IngestServices::acquire();
@@ -386,7 +389,10 @@ void IngestSession::on_au(const AuPtr& au) {
 
 RtmpSender::RtmpSender(std::string url, int timeout_ms, size_t max_bytes)
     : url_(std::move(url)), timeout_ms_(timeout_ms), max_bytes_(max_bytes) {
-  th_ = std::thread([this] { run(); });
+  th_ = std::thread([this] {
+    name_thread("vep-rtmp");
+    run();
+  });
 }
 
 RtmpSender::~RtmpSender() {

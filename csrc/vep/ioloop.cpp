@@ -17,7 +17,10 @@ namespace vep {
 // ------------------------------------------------------------------------------ TaskQueue
 
 TaskQueue::TaskQueue(int threads) {
-  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this] { run(); });
+  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this] {
+    name_thread("vep-task");
+    run();
+  });
 }
 
 TaskQueue::~TaskQueue() {
@@ -58,7 +61,10 @@ void TaskQueue::run() {
 // ------------------------------------------------------------------------------ StrandPool
 
 StrandPool::StrandPool(int threads) {
-  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this, i] { run(i); });
+  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this, i] {
+    name_thread("vep-parse");
+    run(i);
+  });
 }
 
 StrandPool::~StrandPool() {
@@ -144,7 +150,11 @@ void StrandPool::run(int me) {
 
 // ------------------------------------------------------------------------------ TimerQueue
 
-TimerQueue::TimerQueue(TaskQueue& exec) : exec_(exec) { th_ = std::thread([this] { run(); }); }
+TimerQueue::TimerQueue(TaskQueue& exec) : exec_(exec) { th_ = std::thread([this] {
+    name_thread("vep-timer");
+    run();
+  });
+}
 
 TimerQueue::~TimerQueue() {
   {
@@ -198,7 +208,10 @@ IoLoop::IoLoop(int threads) {
   }
   for (auto& l : loops_) {
     Loop* lp = l.get();
-    l->th = std::thread([this, lp] { run(*lp); });
+    l->th = std::thread([this, lp] {
+      name_thread("vep-io");
+      run(*lp);
+    });
   }
 }
 

@@ -7,12 +7,17 @@
 #include <thread>
 #include <vector>
 
+#include "common.h"
+
 namespace vep {
 
 class ThreadPool {
  public:
   explicit ThreadPool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] { run(); });
+    for (int i = 0; i < n; ++i) th_.emplace_back([this] {
+      name_thread("vep-pool");
+      run();
+    });
   }
   ~ThreadPool() {
     {

@@ -483,7 +483,10 @@ void RtspServer::start() {
   getsockname(lfd_, reinterpret_cast<sockaddr*>(&a), &sl);
   port_ = ntohs(a.sin_port);
   stop_ = false;
-  acc_ = std::thread([this] { accept_loop(); });
+  acc_ = std::thread([this] {
+    name_thread("vep-farm");
+    accept_loop();
+  });
 }
 
 void RtspServer::stop() {
@@ -516,7 +519,10 @@ void RtspServer::accept_loop() {
     std::lock_guard<std::mutex> g(mu_);
     conn_fds_.push_back(fd);
     live_.fetch_add(1);
-    std::thread([this, fd] { serve(fd); }).detach();
+    std::thread([this, fd] {
+      name_thread("vep-farm");
+      serve(fd);
+    }).detach();
   }
 }
 

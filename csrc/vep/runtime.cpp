@@ -532,7 +532,10 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   if (threaded_)
     for (auto& lp : lanes_) {
       Lane* ln = lp.get();
-      ln->th = std::thread([this, ln] { lane_loop(*ln); });
+      ln->th = std::thread([this, ln] {
+        name_thread("vep-lane");
+        lane_loop(*ln);
+      });
     }
   cams_.reserve(size_t(opt_.max_cameras));
   if (opt_.letterbox_size > 0) {
@@ -679,7 +682,10 @@ void Worker::start() {
   if (running_) return;
   running_ = true;
   stop_ = false;
-  th_ = std::thread([this] { loop(); });
+  th_ = std::thread([this] {
+    name_thread("vep-worker");
+    loop();
+  });
 }
 
 void Worker::stop() {
