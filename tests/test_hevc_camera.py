@@ -72,3 +72,32 @@ def test_hevc_camera_keyframe_only(native):
     assert wk.decode_now(cam, au)
     meta, got = wk.read_latest(cam, 0)
     assert np.array_equal(got, native.nv12_to_bgr_cpu(y, uv, 0, 0, 160, 96))
+
+
+@pytest.mark.parametrize("device", [-1, pytest.param(0, marks=pytest.mark.gpu)])
+@pytest.mark.parametrize("chunk", [3, 5])
+def test_hevc_backlog_across_irap(native, chunk, device):
+    """The H.265 twin of test_live_compressed.py::test_backlog_across_idr_publishes_the_output_picture:
+    backlogs merged into one job per chunk (a chunk that reaches an IRAP restarts from it) publish
+    only frames whose reconstruction they hold, each equal to the encoder's picture."""
+    w, h = 200, 120
+    s = synth_hevc(native, w, h, bframes=2)
+    aus, want = [], {}
+    for _ in range(24):
+        aus.append(s.next())
+        y, uv = s.picture()
+        want[s.last_pts] = native.nv12_to_bgr_cpu(y, uv, 0, 0, w, h)
+    wk = native.Worker(device=device)
+    cam = wk.add_camera("hevc-backlog", 4)
+    seq, checked = 0, 0
+    for k0 in range(0, len(aus), chunk):
+        wk.decode_many([(cam, aus[k0:k0 + chunk])])
+        r = wk.read_latest(cam, seq)
+        if r is None:
+            continue
+        meta, got = r
+        seq = meta["seq"]
+        ref = want[meta["pts"]]
+        assert np.array_equal(got, ref), f"chunk at AU {k0}: pts {meta['pts']} stale ({int((got != ref).sum())} samples)"
+        checked += 1
+    assert checked >= len(aus) // chunk - 4
