@@ -7,7 +7,7 @@ cd "$R"
 O=$R/gpurun_out/${TAG:-r4q}
 mkdir -p "$O"
 echo "[q] backlog across IDR (gpu)"
-timeout -k 10 200 python -u -m pytest tests/test_live_compressed.py -m gpu -x -q --timeout 120 \
+timeout -k 10 200 python -u -m pytest tests/test_live_compressed.py tests/test_hevc_camera.py -m gpu -x -q --timeout 120 \
   --timeout-method thread -k backlog > "$O/pytest_backlog.log" 2>&1 || { echo "backlog failed"; tail -40 "$O/pytest_backlog.log"; exit 1; }
 tail -1 "$O/pytest_backlog.log"
 echo "[q] gpu suite"
