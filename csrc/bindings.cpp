@@ -262,6 +262,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("lossless", &SynthConfig::lossless)
       .def_readwrite("bit_depth", &SynthConfig::bit_depth)
       .def_readwrite("interlaced", &SynthConfig::interlaced)
+      .def_readwrite("mono", &SynthConfig::mono)
       .def_property(
           "codec", [](const SynthConfig& c) { return c.codec == Codec::kH265 ? "h265" : "h264"; },
           [](SynthConfig& c, const std::string& v) {
@@ -350,6 +351,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("second_chroma_qp_offset", &avc::AvcHighConfig::second_chroma_qp_offset)
       .def_readwrite("coverage", &avc::AvcHighConfig::coverage)
       .def_readwrite("interlaced", &avc::AvcHighConfig::interlaced)
+      .def_readwrite("mono", &avc::AvcHighConfig::mono)
       .def_readwrite("fields", &avc::AvcHighConfig::fields)
       .def_readwrite("marking", &avc::AvcHighConfig::marking)
       .def_readwrite("objects", &avc::AvcHighConfig::objects)

@@ -180,8 +180,8 @@ namespace {
 
 // Stream features outside the supported subset (progressive 8-bit 4:2:0, no lossless).
 void check_sps_supported(const Sps& s) {
-  if (s.chroma_format_idc != 1 || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
-    throw UnsupportedStream("only 8-bit 4:2:0 H.264 is supported");
+  if ((s.chroma_format_idc != 1 && s.chroma_format_idc != 0) || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
+    throw UnsupportedStream("only 8-bit 4:2:0 / 4:0:0 H.264 is supported");
   // Interlaced SPS (frame_mbs_only_flag 0): frame pictures decode as progressive ones (frame
   // macroblocks, frame POC = min(top, bottom)); field pictures as half-height pictures in field
   // slots (CAVLC I / P, see Decoder::parse); MBAFF frames are rejected.
@@ -1292,7 +1292,7 @@ namespace {
 // The fast CAVLC MbDecoder above covers a slice when nothing beyond Baseline-style syntax is in
 // use (the default synthetic camera streams); everything else goes to decode_slice_generic.
 bool legacy_slice(const SliceHdr& sh, const Sps& sps, const Pps& pps) {
-  return !pps.cabac && !sh.field_pic && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
+  return !pps.cabac && !sh.field_pic && sps.chroma_format_idc == 1 && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
          !sps.scaling_matrix_present && !pps.scaling_matrix_present && !sh.explicit_wp &&
          pps.chroma_qp_index_offset == pps.second_chroma_qp_index_offset;
 }

@@ -611,6 +611,7 @@ struct AvcHighConfig {
   bool fields = false;        // (interlaced) code every frame as a field pair (PAFF): top field
                               // first; I / P, P / P anchors and non-reference B / B pairs; CAVLC,
                               // 4x4 transforms
+  bool mono = false;          // 4:0:0 (monochrome, High profile): luma only, chroma decodes grey
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;
   u64 seed = 1;

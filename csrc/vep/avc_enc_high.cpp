@@ -159,7 +159,9 @@ struct AvcHighEncoder::Impl {
     if (c.interlaced) H = (H + 1) & ~1;  // (frame height in MB pairs: map units of 2 MB rows)
     wpx = W * 16;
     hpx = H * 16;
-    sps.profile_idc = (c.t8x8 || c.scaling) ? 100 : 77;
+    sps.profile_idc = (c.t8x8 || c.scaling || c.mono) ? 100 : 77;
+    sps.chroma_format_idc = c.mono ? 0 : 1;
+    VEP_CHECK(!c.mono || (!c.weighted_p && c.weighted_b != 1), "4:0:0 encoder: explicit weighted prediction is not emitted");
     sps.constraint_flags = 0;
     sps.level_idc = W * H > 8192 ? 51 : 40;
     sps.log2_max_frame_num = 16;
@@ -973,7 +975,7 @@ struct AvcHighEncoder::Impl {
     }
     int cc = 0;
     const int qpc[2] = {chroma_qp(qp, pps.chroma_qp_index_offset), chroma_qp(qp, pps.second_chroma_qp_index_offset)};
-    for (int c = 0; c < 2; ++c) {
+    for (int c = 0; c < (cfg.mono ? 0 : 2); ++c) {  // (4:0:0: no chroma residual)
       int cw[4];
       for (int b = 0; b < 4; ++b) {
         const int bx = (b & 1) * 4, by = (b >> 1) * 4;
@@ -1214,17 +1216,18 @@ struct AvcHighEncoder::Impl {
     if (islice_pcm_ok && r < 5) {
       static thread_local u8 pcm[kPcmMbBytes];
       for (auto& p : pcm) p = u8(16 + rng.uni(220));
+      if (cfg.mono) std::memset(pcm + 256, 128, kPcmMbBytes - 256);  // (the grey the decoder fills)
       d.pcm = pcm;
       base_type = 25;
       return;
     }
-    d.chroma_mode = chroma();
+    d.chroma_mode = cfg.mono ? 0 : chroma();
     if (r < 40) {  // Intra_16x16
       int m;
       do m = rng.uni(4);
       while ((m == 0 && !B) || (m == 1 && !A) || (m == 3 && !(A && B && D)));
       random_levels(d, false, true);
-      const int cl = rng.chance(50) ? 15 : 0, cc = rng.uni(3);
+      const int cl = rng.chance(50) ? 15 : 0, cc = cfg.mono ? 0 : rng.uni(3);
       if (!cl)
         for (auto& b : d.ac)
           for (int& v : b) v = 0;
@@ -1267,7 +1270,7 @@ struct AvcHighEncoder::Impl {
       }
     }
     random_levels(d, d.t8x8, false);
-    d.cbp = rng.uni(16) | rng.uni(3) << 4;
+    d.cbp = rng.uni(16) | (cfg.mono ? 0 : rng.uni(3) << 4);
   }
 
   // ---------------------------------------------------------------- picture
@@ -1665,7 +1668,7 @@ struct AvcHighEncoder::Impl {
     const bool t8_ok = cfg.t8x8 && !small && (!direct16 || sps.direct_8x8);
     d.t8x8 = t8_ok && rng.chance(50);
     random_levels(d, d.t8x8, false);
-    d.cbp = rng.uni(16) | rng.uni(3) << 4;
+    d.cbp = rng.uni(16) | (cfg.mono ? 0 : rng.uni(3) << 4);
     d.qp_delta = rng.chance(20) ? rng.uni(9) - 4 : 0;
   }
 

@@ -197,6 +197,7 @@ class MbLayer {
       cbp = (((itype - 1) / 4) % 3) << 4 | (itype >= 13 ? 15 : 0);
       std::fill(std::begin(s.i4), std::end(s.i4), u8(2));
       s.chroma_mode = u8(read_chroma_mode(mb, kWrite ? want->chroma_mode : 0));
+      VEP_CHECK(!mono() || (cbp >> 4) == 0, "4:0:0: Intra_16x16 type with chroma coefficients");
     } else {
       s.kind = kInter;
       no_small = inter_pred(mb, s, mbt);
@@ -279,6 +280,7 @@ class MbLayer {
     }
   }
   int read_chroma_mode(int mb, int v) {
+    if (mono()) return 0;  // 4:0:0: no intra_chroma_pred_mode (the grey planes stay 128)
     if constexpr (kCabac) {
       auto cond = [&](int m) {
         if (m < 0) return 0;
@@ -361,7 +363,7 @@ class MbLayer {
       auto cc = [&](int m, int thr) { return m >= 0 && (nb_.at(m).cbp >> 4) >= thr ? 1 : 0; };
       const int vc = v >> 4;
       int chroma = 0;
-      if (bins->cbp_chroma_bin(cc(am, 1) + 2 * cc(bm, 1), vc != 0))
+      if (!mono() && bins->cbp_chroma_bin(cc(am, 1) + 2 * cc(bm, 1), vc != 0))
         chroma = 1 + int(bins->cbp_chroma_bin(4 + cc(am, 2) + 2 * cc(bm, 2), vc == 2));
       (void)s;
       (void)intra;
@@ -369,12 +371,16 @@ class MbLayer {
     } else {
       (void)mb;
       (void)s;
-      const u8* tab = intra ? kCbpIntra : kCbpInter;
+      // (4:0:0: the 16-entry luma-only mapping of Table 9-4)
+      static constexpr u8 kIntraMono[16] = {15, 0, 7, 11, 13, 14, 3, 5, 10, 12, 1, 2, 4, 8, 6, 9};
+      static constexpr u8 kInterMono[16] = {0, 1, 2, 4, 8, 3, 5, 10, 12, 15, 7, 11, 13, 14, 6, 9};
+      const u32 n = mono() ? 16 : 48;
+      const u8* tab = mono() ? (intra ? kIntraMono : kInterMono) : (intra ? kCbpIntra : kCbpInter);
       u32 code = 0;
       if constexpr (kWrite)
-        while (code < 48 && tab[code] != v) ++code;
+        while (code < n && tab[code] != v) ++code;
       const u32 me = u32(ue(code));
-      VEP_CHECK(me < 48, "bad coded_block_pattern");
+      VEP_CHECK(me < n, "bad coded_block_pattern");
       return tab[me];
     }
   }
@@ -394,32 +400,41 @@ class MbLayer {
     for (auto& c : s.tcc) std::fill(std::begin(c), std::end(c), u8(16));
     s.qp = u8(qp_);
     const u8* pcm;
+    const size_t nb = mono() ? 256 : kPcmMbBytes;  // (4:0:0: luma samples only)
     if constexpr (kWrite) {
       pcm = want->pcm;
       VEP_CHECK(pcm, "I_PCM macroblock without samples");
       if constexpr (kCabac) {
         cenc->align_zero();  // pcm_alignment_zero_bit (the terminate bin flushed the engine)
-        cenc->raw_bytes(pcm, kPcmMbBytes);
+        cenc->raw_bytes(pcm, nb);
         cenc->start();
       } else {
         bw->align_zero();
-        bw->bytes(pcm, kPcmMbBytes);
+        bw->bytes(pcm, nb);
       }
     } else if constexpr (kCabac) {
       const size_t off = cabac->aligned_bytepos();
-      VEP_CHECK(off + kPcmMbBytes <= data_n, "truncated I_PCM macroblock");
+      VEP_CHECK(off + nb <= data_n, "truncated I_PCM macroblock");
       pcm = data + off;
-      cabac->start(off + kPcmMbBytes);
+      cabac->start(off + nb);
     } else {
       br->align();
       const size_t off = br->pos() >> 3;
-      VEP_CHECK(off + kPcmMbBytes <= br->size(), "truncated I_PCM macroblock");
+      VEP_CHECK(off + nb <= br->size(), "truncated I_PCM macroblock");
       pcm = br->data() + off;
-      br->skip(kPcmMbBytes * 8);
+      br->skip(nb * 8);
+    }
+    if (mono()) {  // the record's chroma samples: grey
+      std::memcpy(pcm_mono_, pcm, 256);
+      std::memset(pcm_mono_ + 256, 128, kPcmMbBytes - 256);
+      pcm = pcm_mono_;
     }
     prev_qpd_nz = 0;
     emit(mb, s, res, 0, 0, pcm);
   }
+
+  bool mono() const { return sps_.chroma_format_idc == 0; }
+  u8 pcm_mono_[kPcmMbBytes];
 
  public:
   const u8* data = nullptr;  // CABAC: slice RBSP (I_PCM samples are read in place)

@@ -363,7 +363,7 @@ std::vector<u8> write_sps(const Sps& s) {
   bw.u(8, s.level_idc);
   bw.ue(s.sps_id);
   if (s.profile_idc >= 100) {
-    bw.ue(1);   // chroma_format_idc 4:2:0
+    bw.ue(s.chroma_format_idc);  // 4:2:0, or 4:0:0 (monochrome)
     bw.ue(0);   // bit_depth_luma_minus8
     bw.ue(0);   // bit_depth_chroma_minus8
     bw.u1(0);   // qpprime_y_zero_transform_bypass_flag
@@ -396,11 +396,13 @@ std::vector<u8> write_sps(const Sps& s) {
   bool crop = s.crop_left || s.crop_right || s.crop_top || s.crop_bottom;
   bw.u1(crop);
   if (crop) {
-    bw.ue(s.crop_left / 2);
-    bw.ue(s.crop_right / 2);
-    bw.ue(s.crop_top / (s.frame_mbs_only ? 2 : 4));
-    VEP_CHECK(s.frame_mbs_only || s.crop_bottom % 4 == 0, "interlaced crop must be a multiple of 4 rows");
-    bw.ue(s.crop_bottom / (s.frame_mbs_only ? 2 : 4));  // (CropUnitY)
+    const int cx = s.chroma_format_idc == 0 ? 1 : 2;  // CropUnitX / Y (§7.4.2.1.1)
+    const int cy = (s.chroma_format_idc == 0 ? 1 : 2) * (s.frame_mbs_only ? 1 : 2);
+    bw.ue(s.crop_left / cx);
+    bw.ue(s.crop_right / cx);
+    bw.ue(s.crop_top / cy);
+    VEP_CHECK(s.crop_bottom % cy == 0, "crop must be a multiple of CropUnitY rows");
+    bw.ue(s.crop_bottom / cy);
   }
   bw.u1(1);  // vui
   bw.u1(0);  // aspect ratio

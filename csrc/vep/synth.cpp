@@ -126,6 +126,7 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
       hc.noise = cfg.noise;
       hc.temporal_noise = cfg.temporal_noise;
       hc.interlaced = cfg.interlaced >= 1;
+      hc.mono = cfg.mono;
       if (cfg.interlaced == 2) {
         hc.fields = true;
         hc.cabac = false;

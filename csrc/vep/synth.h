@@ -55,6 +55,7 @@ struct SynthConfig {
   // main / high H.264: 1 = interlaced SPS coding frame pictures, 2 = every frame a field pair
   // (PAFF: CAVLC, 4x4 transforms, B pairs non-reference; overrides cabac / the 8x8 transform)
   int interlaced = 0;
+  bool mono = false;  // High profile: 4:0:0 (monochrome) stream
 };
 
 class SynthH264 {  // (both codecs; the name predates H.265 support)
