@@ -7,8 +7,8 @@ cd "$R"
 O=$R/gpurun_out/${TAG:-r4q}
 mkdir -p "$O"
 echo "[q] backlog across IDR (gpu)"
-timeout -k 10 200 python -u -m pytest tests/test_live_compressed.py tests/test_hevc_camera.py -m gpu -x -q --timeout 120 \
-  --timeout-method thread -k backlog > "$O/pytest_backlog.log" 2>&1 || { echo "backlog failed"; tail -40 "$O/pytest_backlog.log"; exit 1; }
+timeout -k 10 200 python -u -m pytest tests/test_live_compressed.py tests/test_hevc_camera.py tests/test_avc_mono.py -m gpu -x -q --timeout 120 \
+  --timeout-method thread -k "backlog or mono" > "$O/pytest_backlog.log" 2>&1 || { echo "backlog failed"; tail -40 "$O/pytest_backlog.log"; exit 1; }
 tail -1 "$O/pytest_backlog.log"
 echo "[q] gpu suite"
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$O/pytest_gpu.log" 2>&1 \
