@@ -732,7 +732,10 @@ void merge_job(DecodeJob& p, DecodeJob&& job) {
     // dropped). The keyframe bumps the previous GOP's pictures out of the reorder buffer; when the
     // frame it would publish is one of those, its reconstruction was in the dropped job, so the
     // merged job only reconstructs (the keyframe's picture is published by a later job).
+    std::vector<std::pair<int, i64>> dropped = std::move(p.dropped);
+    for (const auto& pic : p.avc) dropped.emplace_back(pic->structure ? pic->target / 2 : pic->target, pic->au.pts);
     p = std::move(job);
+    p.dropped = std::move(dropped);
     if (p.out_slot >= 0 && !reconstructs_output(p)) {
       p.out_slot = -1;
       p.out_fields = false;
@@ -1813,6 +1816,17 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       for (const auto& p : jobs[i].avc) np += !p->structure || p->second_field;
       pictures_.fetch_add(np, std::memory_order_relaxed);
       cp->pictures.fetch_add(np, std::memory_order_relaxed);
+    }
+    if (!jobs[i].dropped.empty()) {  // (bounded: a few reorder depths of pictures)
+      auto& st = cp->stale_;
+      st.insert(st.end(), jobs[i].dropped.begin(), jobs[i].dropped.end());
+      if (st.size() > 64) st.erase(st.begin(), st.end() - 64);
+    }
+    if (out && jobs[i].general() && !cp->stale_.empty() &&
+        std::find(cp->stale_.begin(), cp->stale_.end(), std::make_pair(jobs[i].out_slot, jobs[i].meta.pts)) !=
+            cp->stale_.end()) {
+      cp->ring_->abort(slots[i]);  // its reconstruction was dropped with a backlog: a stale surface
+      continue;
     }
     if (!out) {  // reconstruction only (its pictures wait in the reorder buffer)
       if (err && err[i]) {

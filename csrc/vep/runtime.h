@@ -114,6 +114,9 @@ struct DecodeJob {
   // (B-frame reordering): the job then only reconstructs.
   int out_slot = -1;
   bool out_fields = false;  // H.264 field pair: out_slot holds two fields (avc::OutFrame::fields)
+  // (slot, pts) of H.264 pictures a keyframe's job dropped from the backlog it replaced
+  // (merge_job): the reorder buffer may still output them from later jobs; they are not published
+  std::vector<std::pair<int, i64>> dropped;
   // VCN backend (vcn.h): a picture decoded by the video core; the worker copies its planes into
   // the camera's surface, then converts / letterboxes / publishes it like any other frame.
   vcn::FramePtr ext;
@@ -220,6 +223,7 @@ class Camera {
   std::vector<AuPtr> gop_;
   size_t decoded_upto_ = 0;  // gop_[0, decoded_upto_) are reconstructed on the surface
   bool broken_ = false;      // worker thread: a published frame failed its check; drop until IDR
+  std::vector<std::pair<int, i64>> stale_;  // worker thread: DecodeJob::dropped of recent jobs
   i64 keyframes_ = 0;
   StreamParser parser_;
   avc::Decoder avc_;

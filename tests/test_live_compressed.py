@@ -128,7 +128,7 @@ def test_live_compressed_stream_bit_exact(native, profile):
 
 
 @pytest.mark.parametrize("device", [-1, pytest.param(0, marks=pytest.mark.gpu)])
-@pytest.mark.parametrize("chunk", [2, 3, 4, 7])
+@pytest.mark.parametrize("chunk", [2, 3, 4, 5, 6, 7, 9, 11])
 def test_backlog_across_idr_publishes_the_output_picture(native, chunk, device):
     """A worker that falls behind merges a camera's queued jobs into one (GOP catch-up collapse);
     a backlog that reaches an IDR restarts from it (the queued pictures are dropped). The IDR
