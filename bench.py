@@ -11,7 +11,15 @@ strands, the GPU worker's batched gfx950 reconstruction + NV12->BGR24 into each 
 + letterbox into the consumer batch — decodes them. One *step* is ``cams-per-gpu`` decoded
 pictures; the farm is unthrottled during the timed region, so ``value`` is the node's decode
 capacity (decoded pictures / s summed over ranks, time = max over ranks). With N > 1 the
-letterboxed consumer batch is all-gathered over RCCL once per step, overlapped with decode.
+letterboxed consumer batch is all-gathered over RCCL once per frame interval, overlapped with
+decode, and every rank checks what it received: per-row checksums of each rank's snapshot are
+all-gathered next to the rows and compared with the checksums of the gathered rows
+(``gather_verified``).
+
+One *step* is ``--frames-per-step`` frame intervals of every camera (default: one GOP, 30 frames):
+``cams-per-gpu x frames-per-step`` decoded pictures per rank, so ``--steps 20`` times ~3 s of
+decoding at the headline rate and every step covers whole GOPs (IDR, P and B pictures in the
+stream's own proportions) rather than a transient.
 
 Latency (headline ``p50_latency_ms`` / ``p99_latency_ms``): after the timed loop the farm switches
 to real time (``--fps``), and ``--clients`` concurrent gRPC clients running in separate processes
@@ -47,9 +55,11 @@ ENTROPY = {"h264": "CAVLC macroblock-layer", "h265": "CABAC coding-tree"}
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    # a tick takes ~4-5 ms: 300 timed ticks (10 GOPs of every camera) keep the number steady
-    ap.add_argument("--steps", type=int, default=300)
-    ap.add_argument("--warmup", type=int, default=30)
+    # a step is --frames-per-step frame intervals of every camera (~155 ms at the headline rate)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--frames-per-step", type=int, default=0,
+                    help="frame intervals of every camera per step (0 = one GOP, --gop; keyframe-only: 1)")
     ap.add_argument("--cams-per-gpu", type=int, default=32)
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
@@ -132,7 +142,57 @@ def parse_args():
         a.slices = 8 if a.codec == "h265" and a.width * a.height >= 3840 * 2160 else 1
     if a.temporal_noise is None:
         a.temporal_noise = 1.0 if a.profile == "baseline" else 1.5
+    if a.frames_per_step <= 0:  # (keyframe-only cameras decode one picture per GOP: a step is a GOP)
+        a.frames_per_step = 1 if a.keyframe_only else a.gop
     return a
+
+
+class GatherCheck:
+    """Correctness of the consumer-batch all-gather: every checked gather also all-gathers the
+    per-row checksums of each rank's snapshot (computed on the stream that took the snapshot), and
+    once the rows have arrived each rank compares the checksums of the rows it received with the
+    ones their owners sent. Mismatches are counted on the device (no host sync in the loop)."""
+
+    def __init__(self, torch, dist, world, cams, row, dev, nbuf, every=4):
+        self.torch, self.dist, self.every = torch, dist, every
+        words = row // 4 if row % 4 == 0 else row
+        self.view = torch.int32 if row % 4 == 0 else torch.uint8
+        self.w = torch.arange(words, dtype=torch.int64, device=dev) % 65521 + 1
+        self.local = [torch.empty(cams, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+        self.remote = [torch.empty(world * cams, dtype=torch.int64, device=dev) for _ in range(nbuf)]
+        self.handles = [None] * nbuf
+        self.bad = torch.zeros((), dtype=torch.int64, device=dev)
+        self.checks = self.rows = 0
+        self.n = 0
+
+    def sums(self, rows):
+        return (rows.view(self.view).to(self.torch.int64) * self.w).sum(dim=1)
+
+    def issue(self, b, snap):
+        """After the snapshot of buffer b was enqueued: its checksums, gathered (every `every`-th)."""
+        self.n += 1
+        if (self.n - 1) % self.every:
+            self.handles[b] = None
+            return
+        self.local[b].copy_(self.sums(snap))
+        self.handles[b] = self.dist.all_gather_into_tensor(self.remote[b], self.local[b], async_op=True)
+
+    def verify(self, b, gathered):
+        """After the rows' gather of buffer b was waited on."""
+        h, self.handles[b] = self.handles[b], None
+        if h is None:
+            return
+        h.wait()
+        self.bad += (self.sums(gathered) != self.remote[b]).sum()
+        self.checks += 1
+        self.rows += gathered.shape[0]
+
+    def result(self, dev):
+        """(verified, checks, rows checked, mismatching rows), summed over ranks."""
+        t = self.torch.tensor([int(self.bad.item()), self.checks, self.rows], dtype=self.torch.float64, device=dev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.SUM)
+        bad, checks, rows = (int(v) for v in t.tolist())
+        return checks > 0 and bad == 0, checks, rows, bad
 
 
 def start_client_pool(a):
@@ -395,6 +455,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
     gather = world > 1 and not a.no_gather
     snaps = [torch.empty((cams, row), dtype=torch.uint8, device=dev) for _ in range(2)] if gather else None
     gathered = [torch.empty((world * cams, row), dtype=torch.uint8, device=dev) for _ in range(2)] if gather else None
+    check = GatherCheck(torch, dist, world, cams, row, dev, 2) if gather else None
+    F = a.frames_per_step
     worker.set_consumer_buffers(live.data_ptr(), 0, cams)
 
     def sync():
@@ -415,11 +477,12 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             annot = AnnotationLoad([f"r{rank}rtsp{i}" for i in range(cams)], rate=a.annotate_rate)
             annot.start()
         settle_s = farm.settle()
-        farm.wait_pictures(farm.worker.pictures + cams * max(1, a.warmup), timeout_s=300.0)
+        farm.wait_pictures(farm.worker.pictures + cams * max(1, a.warmup * a.frames_per_step), timeout_s=300.0)
         if world > 1:
             dist.barrier()
         sync()
         p0, f0, d0, s0 = worker.pictures, worker.frames, worker.dropped, farm.stats()
+        sh0 = worker.shed
         rg0 = worker.records_gathered
         g0 = worker.gpu_ms_total
         hostprof = os.environ.get("VEP_HOSTPROF")  # path: SIGPROF samples of every thread, timed region
@@ -428,24 +491,28 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         handles = [None, None]
         cpu0 = thread_cpu()
         t0 = time.perf_counter()
-        for i in range(a.steps):
+        for i in range(a.steps * F):  # (a step: F frame intervals of every camera)
             farm.wait_pictures(p0 + cams * (i + 1))
             if gather:  # RCCL all-gather of the letterboxed consumer batch, overlapped with decode
                 b = i & 1
                 if handles[b] is not None:  # (a stream wait: the gather that last read snapshot b)
                     handles[b].wait()
+                    check.verify(b, gathered[b])
                 stream = torch.cuda.current_stream().cuda_stream if use_gpu else 0
                 worker.snapshot_consumer(snaps[b].data_ptr(), snaps[b].numel(), cams, stream)
                 handles[b] = dist.all_gather_into_tensor(gathered[b], snaps[b], async_op=True)
-        for h in handles:
+                check.issue(b, snaps[b])
+        for b, h in enumerate(handles):
             if h is not None:
                 h.wait()
+                check.verify(b, gathered[b])
         sync()
         t1 = time.perf_counter()
         # every counter is sampled at the end of this rank's timed region, before the barrier: the
         # unthrottled farm keeps feeding (and the worker decoding) while a rank waits for the others
         rg1 = worker.records_gathered
         pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
+        shed = worker.shed - sh0
         s1 = farm.stats()
         cpu1 = thread_cpu()
         if world > 1:
@@ -475,14 +542,21 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             side["annotation"]["rate_per_camera_per_s"] = a.annotate_rate
             annot.close()
             annot = None
+        if gather:
+            verified, checks, rows_checked, bad_rows = check.result(dev)
+            side["gather_check"] = {"gather_verified": verified, "checked_gathers": checks, "rows_checked": rows_checked,
+                                    "mismatching_rows": bad_rows,
+                                    "definition": "every 4th all-gather of the consumer batch also all-gathers each rank's "
+                                                  "per-row checksums (int32 words x position weights); every rank compares "
+                                                  "them with the checksums of the rows it received (summed over ranks)"}
         if world > 1:
             t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes, aus, skipped], dtype=torch.float64,
+            fr = torch.tensor([pictures, frames, dropped, errors, wire_bytes, aus, skipped, shed], dtype=torch.float64,
                               device=dev)
             dist.all_reduce(fr, op=dist.ReduceOp.SUM)
-            pictures, frames, dropped, errors, wire_bytes, aus, skipped = (int(v) for v in fr.tolist())
+            pictures, frames, dropped, errors, wire_bytes, aus, skipped, shed = (int(v) for v in fr.tolist())
         # latency: every rank's cameras go live (real-time farm) with the production ingest
         # (lossy: a camera that outruns the decoder skips to its next keyframe), rank 0 measures
         if pool is not None or world > 1:
@@ -515,7 +589,13 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "n_ranks": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "frames_per_step": a.frames_per_step,
+            "step_definition": f"{a.frames_per_step} frame intervals of every camera: {cams} x {a.frames_per_step} "
+                               "decoded pictures per rank",
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "rccl_world": world if (use_gpu and world > 1) else 0,
+            "collective_backend": (dist.get_backend() if world > 1 else None),
+            "gather_verified": side.get("gather_check", {}).get("gather_verified") if world > 1 else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -554,6 +634,10 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                             "latency_phase": "lossy (the production default): a camera that outruns its parse "
                                              "drops to its next keyframe; live_phase_access_units_skipped counts them"},
             "frames_dropped": dropped,
+            "frames_shed": shed,
+            "frames_shed_definition": "outputs not published because the worker shed their reconstruction: a camera "
+                                      "whose queued job reached a keyframe restarted from it (GOP catch-up collapse "
+                                      "under load); frames_decoded counts only reconstructed pictures",
             "decode_errors": errors,
             "concurrent_clients": a.clients,
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
@@ -663,6 +747,9 @@ def main():
     gathered = [torch.empty((world * cams, row), dtype=torch.uint8, device=dev)
                 for _ in range(NB)] if gather else None
     handles = [None] * NB
+    check = GatherCheck(torch, dist, world, cams, row, dev, NB) if gather else None
+    side = {}
+    F = a.frames_per_step
     pending = []  # ticks launched whose consumer batch has not been handed to the gather yet
     seq_of = {}   # tick -> the worker's launch sequence (lane threads publish asynchronously)
 
@@ -676,12 +763,14 @@ def main():
         if gather:
             worker.wait_published(seq)  # every lane has written tick t's letterbox rows
             handles[k] = dist.all_gather_into_tensor(gathered[k], bufs[k], async_op=True)
+            check.issue(k, bufs[k])
 
     def step(i):
         b = i % NB
         if handles[b] is not None:  # buffer b may still feed the all-gather of tick i - NB
             handles[b].wait()
             handles[b] = None
+            check.verify(b, gathered[b])
             sync()
         worker.set_consumer_buffers(bufs[b].data_ptr(), 0, cams)
         rb.step()  # enqueues tick i
@@ -698,9 +787,10 @@ def main():
             if handles[k] is not None:
                 handles[k].wait()
                 handles[k] = None
+                check.verify(k, gathered[k])
         sync()
 
-    for i in range(a.warmup):
+    for i in range(a.warmup * F):
         step(i)
     # the parse pipeline runs ahead of the launched tick: launch what it has already parsed and
     # stop it, so every tick of the timed region is parsed inside the timed region
@@ -715,8 +805,8 @@ def main():
     ip0, sg0, rg0 = worker.bytes_inplace, worker.bytes_staged, worker.records_gathered
     tm0 = worker.timings()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        step(a.warmup + i)
+    for i in range(a.steps * F):  # (a step: F ticks, one frame interval of every camera each)
+        step(a.warmup * F + i)
     drain()
     t1 = time.perf_counter()
     end_bytes = (worker.bytes_inplace, worker.bytes_staged, worker.records_gathered)
@@ -731,6 +821,10 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = t1 - t0
+    if gather:
+        verified, checks, rows_checked, bad_rows = check.result(dev)
+        side["gather_check"] = {"gather_verified": verified, "checked_gathers": checks, "rows_checked": rows_checked,
+                                "mismatching_rows": bad_rows}
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -765,7 +859,13 @@ def main():
             "n_ranks": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "frames_per_step": a.frames_per_step,
+            "step_definition": f"{a.frames_per_step} frame intervals of every camera: {cams} x {a.frames_per_step} "
+                               "decoded pictures per rank",
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
+            "rccl_world": world if (use_gpu and world > 1) else 0,
+            "collective_backend": (dist.get_backend() if world > 1 else None),
+            "gather_verified": side.get("gather_check", {}).get("gather_verified") if world > 1 else None,
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
@@ -814,6 +914,7 @@ def main():
             res.update(avc_cycles_per_mb(worker))
         if lat is not None:
             res.update(latency_fields(a, lat))
+        res.update(side)
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

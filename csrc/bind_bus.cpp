@@ -28,6 +28,7 @@ void bind_bus(py::module_& m) {
       .def("touch", &bus::Reader::touch, py::arg("name"), py::arg("key_frame_only") = -1,
            py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("rescans", &bus::Reader::rescans)
+      .def("mapped_data_segments", &bus::Reader::mapped_data_segments, py::call_guard<py::gil_scoped_release>())
       .def("info",
            [](bus::Reader& r, const std::string& name) -> py::object {
              bus::Reader::Info i;

@@ -259,6 +259,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("segments", &SynthConfig::segments)
       .def_readwrite("scaling_lists", &SynthConfig::scaling_lists)
       .def_readwrite("long_term", &SynthConfig::long_term)
+      .def_readwrite("open_gop", &SynthConfig::open_gop)
       .def_readwrite("lossless", &SynthConfig::lossless)
       .def_readwrite("bit_depth", &SynthConfig::bit_depth)
       .def_readwrite("interlaced", &SynthConfig::interlaced)
@@ -396,6 +397,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("scaling_lists", &hevc::HevcEncConfig::scaling_lists)
       .def_readwrite("weighted", &hevc::HevcEncConfig::weighted)
       .def_readwrite("long_term", &hevc::HevcEncConfig::long_term)
+      .def_readwrite("open_gop", &hevc::HevcEncConfig::open_gop)
       .def_readwrite("lossless", &hevc::HevcEncConfig::lossless)
       .def_readwrite("bit_depth", &hevc::HevcEncConfig::bit_depth)
       .def_readwrite("coverage", &hevc::HevcEncConfig::coverage)
@@ -1237,6 +1239,7 @@ PYBIND11_MODULE(_vep, m) {
              d["packets"] = c.packets.load();
              d["decoded"] = c.decoded.load();
              d["skipped"] = c.skipped.load();
+             d["shed"] = c.shed.load();
              d["errors"] = c.errors.load();
              d["bytes_in"] = c.bytes_in.load();
              d["last_packet_ms"] = c.last_packet_ms.load();
@@ -1429,6 +1432,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("batches", &Worker::batches)
       .def_property_readonly("frames", &Worker::frames)
       .def_property_readonly("dropped", &Worker::dropped)
+      .def_property_readonly("shed", &Worker::shed)
       .def_property_readonly("pictures", &Worker::pictures)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
       .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)

@@ -425,6 +425,7 @@ void Reader::rescan_locked() {
   ::closedir(d);
   segs_.swap(keep);
   where_.clear();
+  prune_data_locked();
   for (auto& s : segs_)
     for (u32 i = 0; i < s->hdr->max_cams; ++i) {
       const CamEntry& e = s->hdr->cams[i];
@@ -436,8 +437,31 @@ void Reader::rescan_locked() {
     }
 }
 
+void Reader::prune_data_locked() {
+  for (auto it = data_.begin(); it != data_.end();) {
+    const Seg* seg = nullptr;
+    for (const auto& sp : segs_)
+      if (sp->path == it->second.seg_path) seg = sp.get();
+    bool keep = seg != nullptr && it->second.cam >= 0 && u32(it->second.cam) < seg->hdr->max_cams;
+    if (keep) {
+      const CamEntry& e = seg->hdr->cams[it->second.cam];
+      keep = e.live.load(std::memory_order_acquire) && e.gen.load(std::memory_order_acquire) == it->second.cam_gen &&
+             e.data_gen.load(std::memory_order_acquire) == it->second.data_gen;
+    }
+    it = keep ? std::next(it) : data_.erase(it);  // (a copy in flight holds its own reference)
+  }
+}
+
+size_t Reader::mapped_data_segments() {
+  std::lock_guard<std::mutex> g(mu_);
+  rescan_locked();
+  return data_.size();
+}
+
 bool Reader::locate(const std::string& name, Loc* loc) {
   std::lock_guard<std::mutex> g(mu_);
+  // (a periodic rescan also unmaps the data segments of cameras and owners that went away)
+  if (mono_ms() - last_scan_ms_ >= 5000) rescan_locked();
   for (int pass = 0; pass < 2; ++pass) {
     auto it = where_.find(name);
     if (it != where_.end()) {
@@ -565,15 +589,16 @@ size_t Reader::copy(const Ticket& t, u8* dst, size_t cap, i64* seq) {
       std::lock_guard<std::mutex> g(mu_);
       const std::string key = seg->path + "/" + std::to_string(t.cam);
       auto it = data_.find(key);
-      if (it == data_.end() || it->second.first != dg) {
+      if (it == data_.end() || it->second.data_gen != dg || it->second.cam_gen != t.gen) {
+        if (it != data_.end()) data_.erase(it);  // the camera's older segment: unmapped
         const std::string path = seg->path + ".c" + std::to_string(t.cam) + ".g" + std::to_string(dg);
         auto m = std::make_shared<DataSeg>();
         m->bytes = size_t(scap) * kSlots;
         m->base = static_cast<const u8*>(map_file(path, m->bytes, false, false));
         if (!m->base) continue;  // (replaced meanwhile)
-        data_[key] = {dg, m};
+        data_[key] = DataMap{seg->path, t.cam, dg, t.gen, m};
       }
-      ds = std::static_pointer_cast<DataSeg>(data_[key].second);
+      ds = std::static_pointer_cast<DataSeg>(data_[key].map);
     }
     const u32 k = e.newest.load(std::memory_order_acquire);
     const SlotHdr& s = e.slots[k % kSlots];

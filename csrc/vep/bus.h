@@ -181,6 +181,8 @@ class Reader {
   bool info(const std::string& name, Info* out);
   std::vector<std::string> names();
   u64 rescans() const { return rescans_.load(); }
+  // data segments this reader keeps mapped (tests: none outlives its camera or owner)
+  size_t mapped_data_segments();
 
  private:
   struct Seg;
@@ -195,8 +197,17 @@ class Reader {
   std::mutex mu_;
   std::vector<std::shared_ptr<Seg>> segs_;
   std::unordered_map<std::string, Loc> where_;
-  // mapped data segments, key: control segment path + '/' + cam -> (generation, mapping)
-  std::unordered_map<std::string, std::pair<u32, std::shared_ptr<void>>> data_;
+  // Mapped data segments, key: control segment path + '/' + cam. An entry is unmapped when its
+  // camera is re-registered or removed (gen / live), or its owner's control segment disappears:
+  // an unlinked tmpfs file keeps its pages while any process maps it.
+  struct DataMap {
+    std::string seg_path;
+    int cam = -1;
+    u32 data_gen = 0, cam_gen = 0;
+    std::shared_ptr<void> map;
+  };
+  std::unordered_map<std::string, DataMap> data_;
+  void prune_data_locked();
   i64 last_scan_ms_ = 0;
   std::atomic<u64> rescans_{0};
 };

@@ -19,6 +19,8 @@ namespace vep::hevc {
 enum NalType : int {
   kTrailN = 0,
   kTrailR = 1,
+  kRaslN = 8,
+  kRaslR = 9,
   kBlaWLp = 16,
   kIdrWRadl = 19,
   kIdrNLp = 20,

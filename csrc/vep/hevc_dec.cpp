@@ -60,7 +60,10 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   check_supported(sps, pps);
   const int t = sh.nal_type;
   const bool irap = is_irap(t);
-  if (irap) no_rasl_output_ = is_idr(t) || is_bla(t) || first_;
+  if (irap) {
+    no_rasl_output_ = is_idr(t) || is_bla(t) || first_;
+    irap_tag_ = tag;
+  }
   skip_pic_ = false;
   if (is_rasl(t) && no_rasl_output_) {  // leading pictures of a CRA we started at: not decodable
     skip_pic_ = true;
@@ -172,6 +175,7 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
   cur_->dts = au.dts;
   cur_->tag = tag;
   cur_->keyframe = irap;
+  cur_->rasl_of = is_rasl(t) ? irap_tag_ : -1;
   cur_->type = sh.pict_char();
   cur_->width = sps.out_width();
   cur_->height = sps.out_height();
@@ -213,6 +217,9 @@ void Decoder::start_picture(const SliceHeader& sh, int tid, const Sps& sps, cons
       g = std::move(fresh);
     });
     cur_gpu_->target = cur_->slot;
+    cur_gpu_->pts = au.pts;
+    cur_gpu_->tag = tag;
+    cur_gpu_->cra = irap && !no_rasl_output_;
     cur_gpu_->bd_y = sps.bit_depth_luma;
     cur_gpu_->bd_c = sps.bit_depth_chroma;
     pc_->init_gpu(cur_gpu_.get());

@@ -66,6 +66,7 @@ struct HevcFrame {
   int width = 0, height = 0, crop_left = 0, crop_top = 0;  // conformance window (output size)
   int slot = 0;                                             // DPB surface slot (GPU mode)
   int latency = 0;                                          // (output bumping, C.5.2.3)
+  i64 rasl_of = -1;  // RASL picture: decode tag of its associated CRA (-1: not a RASL picture)
 };
 using FramePtr = std::shared_ptr<HevcFrame>;
 
@@ -151,6 +152,7 @@ class Decoder {
   int act_w_ = 0, act_h_ = 0;  // picture size of the active coded video sequence
   int act_bd_ = 8;             // and its bit depth
   bool first_ = true, no_rasl_output_ = true, skip_pic_ = false;
+  i64 irap_tag_ = -1;  // decode tag of the last IRAP picture (RASL pictures' association)
   u32 next_uid_ = 1;
   bool gpu_mode_ = false;
   int gpu_slots_ = 0, last_out_slot_ = -1;
@@ -207,6 +209,9 @@ struct HevcEncConfig {
   bool scaling_lists = false;        // scaling lists (coverage: custom SPS / PPS lists)
   bool weighted = false;             // explicit weighted prediction in P and B slices
   bool long_term = false;            // each GOP's IDR stays referenced as a long-term picture
+  // open GOPs: every IRAP after the first is a CRA, coded before the B pictures that precede it in
+  // display order (RASL pictures: they predict from the previous GOP's anchor and the CRA)
+  bool open_gop = false;
   bool lossless = false;             // transquant bypass enabled (coverage: lossless CUs)
   int bit_depth = 8;                 // 8 (Main) or 10 (Main10: 10-bit samples, 16-bit surfaces)
   bool coverage = false;

@@ -99,10 +99,12 @@ struct HevcEncoder::Impl : CtuDecider {
     i64 disp;
     int type;
     bool ref, idr;
+    bool cra = false, rasl = false;  // (open GOPs)
   };
   std::deque<Job> plan;
   std::map<i64, HostSurface> sources;
   i64 next_disp = 0, rendered = -1, coded = 0, idr_disp = 0;
+  int cra_poc = -1;  // open GOP: POC of the last CRA until its first trailing picture drops the older anchors
   std::vector<FramePtr> anchors;  // kept reference pictures (coding order)
   int keep_refs = 2;
   PicCtx pc;
@@ -123,6 +125,7 @@ struct HevcEncoder::Impl : CtuDecider {
     VEP_CHECK(c.log2_ctb >= 4 && c.log2_ctb <= 6 && c.log2_min_cb == 3, "log2_ctb 4..6, log2_min_cb 3");
     VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
     VEP_CHECK(c.bit_depth >= 8 && c.bit_depth <= 10, "encoder bit depth 8..10");
+    VEP_CHECK(!(c.open_gop && c.long_term), "open_gop: the long-term IDR would precede every CRA");
     bd = c.bit_depth;
     W = (c.width + 7) & ~7;
     H = (c.height + 7) & ~7;
@@ -274,13 +277,22 @@ struct HevcEncoder::Impl : CtuDecider {
   }
 
   void plan_next() {
-    if (is_idr_pos(next_disp)) {
-      plan.push_back({next_disp, kI, true, true});
+    if (is_idr_pos(next_disp)) {  // (open GOPs: only the stream's first IRAP is an IDR)
+      const bool cra = cfg.open_gop && next_disp > 0;
+      plan.push_back({next_disp, kI, true, !cra, cra, false});
       ++next_disp;
       return;
     }
     i64 next_idr = next_disp + 1;
     while (!is_idr_pos(next_idr)) ++next_idr;
+    if (cfg.open_gop && next_idr - next_disp <= cfg.bframes) {
+      // the mini-GOP ends at the next IRAP: a CRA anchors it, and the B pictures before it in
+      // display order follow it in decoding order (RASL)
+      plan.push_back({next_idr, kI, true, false, true, false});
+      for (i64 d = next_disp; d < next_idr; ++d) plan.push_back({d, kB, false, false, false, true});
+      next_disp = next_idr + 1;
+      return;
+    }
     const i64 anchor = std::min<i64>(next_disp + cfg.bframes, next_idr - 1);
     plan.push_back({anchor, kP, true, false});
     for (i64 d = next_disp; d < anchor; ++d) plan.push_back({d, kB, false, false});
@@ -598,6 +610,12 @@ struct HevcEncoder::Impl : CtuDecider {
       lt_pic = nullptr;
     }
     const int poc = int(job.disp - idr_disp);
+    if (job.cra) cra_poc = poc;
+    if (cra_poc >= 0 && !job.cra && !job.rasl) {  // a trailing picture references nothing before its CRA
+      anchors.erase(std::remove_if(anchors.begin(), anchors.end(), [&](const FramePtr& f) { return f->poc < cra_poc; }),
+                    anchors.end());
+      cra_poc = -1;
+    }
     cur_src = &source_of(job.disp);
     cur_type = job.type;
     cur = std::make_shared<HevcFrame>();
@@ -615,6 +633,8 @@ struct HevcEncoder::Impl : CtuDecider {
     for (size_t i = 0; i < before.size(); ++i) rps.delta_poc[i] = before[i]->poc - poc, rps.used[i] = true;
     for (size_t i = 0; i < after.size(); ++i)
       rps.delta_poc[before.size() + i] = after[i]->poc - poc, rps.used[before.size() + i] = true;
+    if (job.cra)  // an IRAP predicts from nothing: its RPS only keeps the anchors its RASL pictures use
+      for (int i = 0; i < rps.num_delta(); ++i) rps.used[i] = false;
     const bool cov = cfg.coverage;
     // the GOP's long-term picture (used unless coverage leaves it in LtFoll for a while)
     std::vector<FramePtr> lt;
@@ -640,7 +660,7 @@ struct HevcEncoder::Impl : CtuDecider {
     pc.poc = poc;
     auto au = std::make_shared<AccessUnit>();
     au->codec = Codec::kH265;
-    if (job.idr) {
+    if (job.idr || job.cra) {
       au->add_nal(vps_nal.data(), vps_nal.size());
       au->add_nal(sps_nal.data(), sps_nal.size());
       au->add_nal(pps_nal.data(), pps_nal.size());
@@ -652,7 +672,7 @@ struct HevcEncoder::Impl : CtuDecider {
     for (size_t s = 0; s < slice_ranges.size(); ++s) {
       const auto [first_ts, end_ts] = slice_ranges[s];
       SliceHeader sh = lth;
-      sh.nal_type = job.idr ? kIdrWRadl : (job.ref ? kTrailR : kTrailN);
+      sh.nal_type = job.idr ? kIdrWRadl : job.cra ? kCra : job.rasl ? kRaslN : (job.ref ? kTrailR : kTrailN);
       sh.first_slice_in_pic = s == 0;
       sh.segment_address = pc.ts2rs[size_t(first_ts)];
       sh.slice_type = job.type;
@@ -728,7 +748,7 @@ struct HevcEncoder::Impl : CtuDecider {
     au->pts = job.disp * dur;
     au->dts = coded * dur - (cfg.bframes > 0 ? dur : 0);
     au->duration = dur;
-    au->keyframe = job.idr;
+    au->keyframe = job.idr || job.cra;
     ++coded;
     last_pts = au->pts;
     last_type = job.type == kI ? 'I' : job.type == kP ? 'P' : 'B';

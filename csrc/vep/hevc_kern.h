@@ -108,6 +108,8 @@ inline void hk_sparse_expand(const i16* src, int log2, i16* dense) {
 struct GpuPicture {
   int width = 0, height = 0, log2ctb = 4, wctb = 0, hctb = 0;
   int target = 0;                     // DPB slot being reconstructed
+  i64 pts = 0, tag = -1;              // of the access unit (output bookkeeping of merged backlogs)
+  bool cra = false;                   // a CRA whose RASL pictures predict from earlier pictures
   int cb_qp_offset = 0, cr_qp_offset = 0;
   // sample bit depths (Main10: up to 10; the surfaces then hold one u16 per sample and `pcm`
   // holds the PCM samples as u16, already scaled to the bit depth)

@@ -285,6 +285,7 @@ bool Camera::build_job(DecodeJob& job, size_t from, size_t to, bool refresh) {
       pi.width = of ? of->width : gp.width;
       pi.height = of ? of->height : gp.height;
       job.out_slot = of ? of->slot : -1;
+      job.out_rasl_of = of ? of->rasl_of : -1;
       if (!of) return true;  // reordering: reconstruct only, nothing leaves the DPB yet
       pi.crop_left = of->crop_left;
       pi.crop_top = of->crop_top;
@@ -732,10 +733,19 @@ void merge_job(DecodeJob& p, DecodeJob&& job) {
     // dropped). The keyframe bumps the previous GOP's pictures out of the reorder buffer; when the
     // frame it would publish is one of those, its reconstruction was in the dropped job, so the
     // merged job only reconstructs (the keyframe's picture is published by a later job).
+    // (H.265 open GOPs: the RASL pictures of a CRA predict from the previous GOP, whose dropped
+    // pictures are never reconstructed; they are not published either)
     std::vector<std::pair<int, i64>> dropped = std::move(p.dropped);
+    std::vector<i64> poisoned = std::move(p.poisoned_cra);
     for (const auto& pic : p.avc) dropped.emplace_back(pic->structure ? pic->target / 2 : pic->target, pic->au.pts);
+    for (const auto& pic : p.hevc) dropped.emplace_back(pic->target, pic->pts);
+    const bool lost = !p.hevc.empty();
     p = std::move(job);
-    p.dropped = std::move(dropped);
+    if (lost)
+      for (const auto& pic : p.hevc)
+        if (pic->cra) poisoned.push_back(pic->tag);
+    p.dropped.insert(p.dropped.begin(), dropped.begin(), dropped.end());
+    p.poisoned_cra.insert(p.poisoned_cra.begin(), poisoned.begin(), poisoned.end());
     if (p.out_slot >= 0 && !reconstructs_output(p)) {
       p.out_slot = -1;
       p.out_fields = false;
@@ -749,7 +759,10 @@ void merge_job(DecodeJob& p, DecodeJob&& job) {
       p.meta = job.meta;
       p.out_slot = job.out_slot;
       p.out_fields = job.out_fields;
+      p.out_rasl_of = job.out_rasl_of;
     }
+    p.dropped.insert(p.dropped.end(), job.dropped.begin(), job.dropped.end());
+    p.poisoned_cra.insert(p.poisoned_cra.end(), job.poisoned_cra.begin(), job.poisoned_cra.end());
   } else if (job.refresh || job.general() != p.general() || p.upd.width_mbs != job.upd.width_mbs ||
              p.upd.height_mbs != job.upd.height_mbs) {
     p = std::move(job);
@@ -1798,6 +1811,30 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
   }
 }
 
+// Worker thread, per finished job of a camera: records the job's dropped pictures / poisoned
+// CRAs and tells whether its output is one of the recorded stale pictures (each is output once:
+// the entry is erased) or a RASL picture of a poisoned CRA.
+bool stale_output(Camera& c, const DecodeJob& j, bool check) {
+  const u64 now = ++c.jobs_seen_;
+  for (const auto& d : j.dropped) c.stale_.push_back({d.first, d.second, now + Camera::kStaleJobs});
+  for (i64 tag : j.poisoned_cra) c.bad_cra_.emplace_back(tag, now + Camera::kStaleJobs);
+  c.stale_.erase(std::remove_if(c.stale_.begin(), c.stale_.end(), [&](const Camera::StaleOut& s) { return s.until < now; }),
+                 c.stale_.end());
+  c.bad_cra_.erase(std::remove_if(c.bad_cra_.begin(), c.bad_cra_.end(), [&](const auto& b) { return b.second < now; }),
+                   c.bad_cra_.end());
+  if (c.stale_.size() > 64) c.stale_.erase(c.stale_.begin(), c.stale_.end() - 64);
+  if (!check) return false;
+  for (auto it = c.stale_.begin(); it != c.stale_.end(); ++it)
+    if (it->slot == j.out_slot && it->pts == j.meta.pts) {
+      c.stale_.erase(it);
+      return true;
+    }
+  if (j.out_rasl_of >= 0)
+    for (const auto& b : c.bad_cra_)
+      if (b.first == j.out_rasl_of) return true;
+  return false;
+}
+
 void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, const u32* err) {
   trace::Range tr("vep.publish");
   const i64 t = mono_us();
@@ -1817,17 +1854,7 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       pictures_.fetch_add(np, std::memory_order_relaxed);
       cp->pictures.fetch_add(np, std::memory_order_relaxed);
     }
-    if (!jobs[i].dropped.empty()) {  // (bounded: a few reorder depths of pictures)
-      auto& st = cp->stale_;
-      st.insert(st.end(), jobs[i].dropped.begin(), jobs[i].dropped.end());
-      if (st.size() > 64) st.erase(st.begin(), st.end() - 64);
-    }
-    if (out && jobs[i].general() && !cp->stale_.empty() &&
-        std::find(cp->stale_.begin(), cp->stale_.end(), std::make_pair(jobs[i].out_slot, jobs[i].meta.pts)) !=
-            cp->stale_.end()) {
-      cp->ring_->abort(slots[i]);  // its reconstruction was dropped with a backlog: a stale surface
-      continue;
-    }
+    const bool stale = stale_output(*cp, jobs[i], out && jobs[i].general());
     if (!out) {  // reconstruction only (its pictures wait in the reorder buffer)
       if (err && err[i]) {
         cp->errors.fetch_add(1, std::memory_order_relaxed);
@@ -1858,6 +1885,12 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
         continue;
       }
       cp->broken_ = false;
+    }
+    if (stale) {  // its reconstruction was dropped with a backlog (or predicts from one): a stale surface
+      cp->ring_->abort(slots[i]);
+      shed_.fetch_add(1, std::memory_order_relaxed);
+      cp->shed.fetch_add(1, std::memory_order_relaxed);
+      continue;
     }
     jobs[i].meta.decoded_us = t;
     if (jobs[i].meta.arrival_ms > 0) {

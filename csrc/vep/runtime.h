@@ -114,9 +114,13 @@ struct DecodeJob {
   // (B-frame reordering): the job then only reconstructs.
   int out_slot = -1;
   bool out_fields = false;  // H.264 field pair: out_slot holds two fields (avc::OutFrame::fields)
-  // (slot, pts) of H.264 pictures a keyframe's job dropped from the backlog it replaced
+  // (slot, pts) of the pictures a keyframe's job dropped from the backlog it replaced
   // (merge_job): the reorder buffer may still output them from later jobs; they are not published
   std::vector<std::pair<int, i64>> dropped;
+  // H.265: decode tags of CRA pictures such a job restarted from. Their RASL pictures predict from
+  // pictures before the CRA, possibly dropped ones: they are not published either.
+  std::vector<i64> poisoned_cra;
+  i64 out_rasl_of = -1;  // H.265: the output picture is a RASL picture of the CRA with this tag
   // VCN backend (vcn.h): a picture decoded by the video core; the worker copies its planes into
   // the camera's surface, then converts / letterboxes / publishes it like any other frame.
   vcn::FramePtr ext;
@@ -169,7 +173,7 @@ class Camera {
   // --- stats ---
   // decoded = frames published to the ring; pictures = pictures reconstructed (general path: a
   // picture can be reconstructed in one job and output by a later one)
-  std::atomic<u64> packets{0}, decoded{0}, skipped{0}, errors{0}, bytes_in{0}, pictures{0};
+  std::atomic<u64> packets{0}, decoded{0}, skipped{0}, errors{0}, bytes_in{0}, pictures{0}, shed{0};
   // packet arrival -> frame published (ms) histogram, upper bounds kLatBucketsMs (+inf last)
   static constexpr int kLatBuckets = 12;
   static constexpr double kLatBucketsMs[kLatBuckets - 1] = {1, 2, 5, 10, 20, 35, 50, 100, 250, 500, 1000};
@@ -214,6 +218,7 @@ class Camera {
 
  private:
   friend class Worker;
+  friend bool stale_output(Camera& c, const DecodeJob& j, bool check);
   bool build_job(DecodeJob& job, size_t from, size_t to, bool refresh);
   bool build_vcn_job(DecodeJob& job, size_t from, size_t to);
   Worker& w_;
@@ -223,7 +228,19 @@ class Camera {
   std::vector<AuPtr> gop_;
   size_t decoded_upto_ = 0;  // gop_[0, decoded_upto_) are reconstructed on the surface
   bool broken_ = false;      // worker thread: a published frame failed its check; drop until IDR
-  std::vector<std::pair<int, i64>> stale_;  // worker thread: DecodeJob::dropped of recent jobs
+  // Worker thread: DecodeJob::dropped / poisoned_cra of recent jobs. A dropped picture leaves the
+  // reorder buffer at most once (its entry is erased when it does); entries also expire after
+  // kStaleJobs of the camera's jobs, so a pts that repeats later (looped source, reconnect, wrap)
+  // is not suppressed for good.
+  static constexpr u64 kStaleJobs = 64;
+  struct StaleOut {
+    int slot;
+    i64 pts;
+    u64 until;
+  };
+  std::vector<StaleOut> stale_;
+  std::vector<std::pair<i64, u64>> bad_cra_;  // (CRA tag, expiry)
+  u64 jobs_seen_ = 0;
   i64 keyframes_ = 0;
   StreamParser parser_;
   avc::Decoder avc_;
@@ -365,6 +382,9 @@ class Worker {
   // after an error, camera removed)
   u64 frames() const { return frames_.load(); }
   u64 dropped() const { return dropped_.load(); }
+  // outputs not published because their reconstruction was shed with a merged backlog (load
+  // shedding at a keyframe, merge_job) or predicts from such a picture (RASL of a shed CRA)
+  u64 shed() const { return shed_.load(); }
   u64 pictures() const { return pictures_.load(); }  // pictures reconstructed
   // GPU time of the batches (first event to last, per lane; the busiest lane's total)
   double gpu_ms_total() const;
@@ -492,7 +512,7 @@ class Worker {
   std::thread th_;
   std::mutex launch_mu_;
   std::shared_ptr<std::function<void(int, i64)>> publish_hook_;  // (atomic_load / atomic_store)
-  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0};
+  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0}, shed_{0};
   std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0}, records_gathered_{0};
   std::mutex timers_mu_;
   bool direct_reads_ = false;

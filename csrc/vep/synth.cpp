@@ -95,6 +95,7 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
     hc.scaling_lists = cfg.scaling_lists;
     hc.weighted = cfg.weighted_p || cfg.weighted_b;
     hc.long_term = cfg.long_term;
+    hc.open_gop = cfg.open_gop;
     hc.lossless = cfg.lossless;
     hc.bit_depth = cfg.bit_depth;
     auto enc = std::make_unique<hevc::HevcEncoder>(hc);

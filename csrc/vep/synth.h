@@ -50,6 +50,7 @@ struct SynthConfig {
   int segments = 1;
   bool scaling_lists = false;
   bool long_term = false;
+  bool open_gop = false;  // H.265: CRA + RASL pictures at every IRAP after the first
   bool lossless = false;
   int bit_depth = 8;         // H.265: 10 = Main10 (10-bit samples)
   // main / high H.264: 1 = interlaced SPS coding frame pictures, 2 = every frame a field pair

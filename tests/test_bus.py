@@ -239,3 +239,54 @@ def test_serving_process_restart(native, tmp_path):
     finally:
         app.stop()
         srv.stop()
+
+
+def test_bus_reader_unmaps_data_of_removed_cameras_and_dead_owners(native):
+    """A reader's data-segment mappings do not outlive the camera (removed / re-registered) or
+    its owner process (killed): an unlinked /dev/shm file keeps its pages while mapped."""
+    tag = f"t{os.getpid()}m"
+    w, o = _owner(native, tag)
+    r = native.BusReader(tag)
+    try:
+        cam = w.add_camera("camM", 3)
+        o.add(cam, "camM")
+        w.decode_now(cam, synth(native, 160, 96, gop=4).next())
+        assert r.frame("camM", 0, 3000, 0) is not None
+        assert r.mapped_data_segments() == 1
+        o.remove(cam)
+        assert r.mapped_data_segments() == 0
+    finally:
+        o.stop()
+        w.stop()
+    # an owner in another process, killed while the reader holds its camera's data mapped
+    tag2 = f"t{os.getpid()}n"
+    code = f"""
+import sys, time
+sys.path.insert(0, {ROOT!r})
+sys.path.insert(0, {os.path.join(ROOT, 'tests')!r})
+from video_edge_ai_proxy_amd import native
+from conftest import synth
+w = native.Worker(device=-1)
+w.start()
+o = native.BusOwner({tag2!r}, 0, 4)
+o.attach(w)
+cam = w.add_camera("camK", 3)
+o.add(cam, "camK")
+w.decode_now(cam, synth(native, 160, 96, gop=4).next())
+print("ready", flush=True)
+time.sleep(60)
+"""
+    p = subprocess.Popen([sys.executable, "-c", code], stdout=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().strip() == "ready"
+        r2 = native.BusReader(tag2)
+        assert r2.frame("camK", 0, 5000, 0) is not None
+        assert r2.mapped_data_segments() == 1
+        p.kill()
+        p.wait(timeout=30)
+        assert r2.mapped_data_segments() == 0
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait()
+        native.bus_remove_segments(p.pid)

@@ -87,13 +87,15 @@ def test_bench_two_ranks_gloo():
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
            "--gpus", "2", "--steps", "3", "--warmup", "1", "--cpu", "--width", "96", "--height", "64",
-           "--cams-per-gpu", "2", "--letterbox", "32", "--latency-samples", "3", "--threads", "1"]
+           "--cams-per-gpu", "2", "--letterbox", "32", "--latency-samples", "3", "--threads", "1",
+           "--frames-per-step", "2"]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     d = json.loads(line)
     assert d["n_ranks"] == 2 and d["n_gpus"] == 0 and d["config"]["global_batch"] == 4 and d["config"]["all_gather"]
     assert d["value"] > 0 and d["config"]["parallelism"] == "camera-dp2"
+    assert d["gather_verified"] is True and d["frames_per_step"] == 2
 
 
 def test_parse_threads_split_cpu_budget(monkeypatch):
@@ -237,3 +239,7 @@ def test_bench_eight_ranks_gloo():
     d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert d["n_ranks"] == 8 and d["config"]["global_batch"] == 8 and d["config"]["all_gather"]
     assert d["config"]["parallelism"] == "camera-dp8" and d["frames_dropped"] == 0 and d["value"] > 0
+    # every rank checked the rows it received against their owners' checksums
+    assert d["gather_verified"] is True and d["gather_check"]["mismatching_rows"] == 0
+    assert d["gather_check"]["checked_gathers"] >= 8 and d["collective_backend"] == "gloo"
+    assert d["frames_per_step"] == 6 and d["rccl_world"] == 0
