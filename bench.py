@@ -91,7 +91,8 @@ def parse_args():
     ap.add_argument("--bit-depth", type=int, choices=[8, 10], default=8,
                     help="h265: 10 = Main10 streams (u16 surfaces on the GPU, narrowed to 8 bits for BGR24)")
     ap.add_argument("--threads", type=int, default=0,
-                    help="host parse threads per rank (0 = CPU budget / local ranks - 1, at most 15)")
+                    help="host parse threads per rank (0 = the rank's host domain: its part of the CPU "
+                         "budget - 1, pinned to its GPU's NUMA-local CPUs)")
     ap.add_argument("--parse-window", type=int, default=8,
                     help="ticks a camera's parse may run ahead of the tick being launched")
     ap.add_argument("--pack-threads", type=int, default=4, help="host index/staging threads per rank")
@@ -463,8 +464,6 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         if use_gpu:
             torch.cuda.synchronize()
 
-    # the live ingest's parse strands get the rank's parse-thread budget (as the replay pool does)
-    os.environ.setdefault("VEP_INGEST_PARSE_THREADS", str(a.threads))
     farm = RtspFarm(vep, worker, a, rank, compressed)
     lat = None
     live_fps = None
@@ -644,6 +643,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "rank0_record_bytes_gathered_per_step": (rg1 - rg0) // max(1, a.steps),
             "keyframe_coalesce_window_us": worker.kf_window_us if a.keyframe_only else None,
             "parse_threads_per_rank": a.threads,
+            "rank0_host_domain": a.host_domain,
             "rocdecode_available": bool(vep.rocdecode_available()),
             "decoder_backend": decoder_backend(a, compressed),
             "per_gpu_fps": round(fps / max(world, 1), 2),
@@ -719,16 +719,23 @@ def main():
         torch.cuda.set_device(local)
 
     from video_edge_ai_proxy_amd import native as vep
-    from video_edge_ai_proxy_amd.utils import parse_threads_per_rank
 
-    if a.threads <= 0:
-        a.threads = parse_threads_per_rank(int(os.environ.get("LOCAL_WORLD_SIZE", str(world))))
+    # this rank's host domain (hostplan.h): the node's ranks split the CPUs, each rank's share
+    # pinned to its GPU's NUMA-local CPUs and sized from the CPU budget (no constant cap)
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    plan_devs = list(range(local_world)) if use_gpu else [-1] * local_world
+    dom = vep.plan_host_domains(plan_devs)[local]
+    if a.threads > 0:
+        dom["parse_threads"] = a.threads
+    a.threads = dom["parse_threads"]
+    a.host_domain = {k: dom[k] for k in ("cpulist", "numa_node", "pci_bus_id", "cpu_share", "parse_threads",
+                                         "io_threads", "source")}
     cams = a.cams_per_gpu
     S = a.letterbox
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
                         max_cameras=cams, pack_threads=a.pack_threads,
                         letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes,
-                        stages=a.stages, queue=a.lane_queue)
+                        stages=a.stages, queue=a.lane_queue, host_domain=dom)
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     compressed = a.content == "avc"  # (h265: general HEVC Main streams, CPU reconstruction)
     cfg = make_cfg(vep, a, rank, compressed)
@@ -904,6 +911,7 @@ def main():
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
             "gpu_lanes": worker.lanes,
             "parse_threads_per_rank": a.threads,
+            "rank0_host_domain": a.host_domain,
             "gpu_stages": worker.stages,
             "gpu_inflight_per_lane": worker.inflight,
             "payload_path": payload_path(a, compressed, worker, ip0, sg0, rg0, end_bytes),

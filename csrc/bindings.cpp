@@ -82,6 +82,36 @@ static py::dict pic_dict(const PictureInfo& p) {
 
 // Callers bind the result to a local (`auto cp = cam_ref(w, i)`) when the camera must outlive
 // a GIL-released section; short accessors use cam_of.
+static py::dict domain_dict(const HostDomain& d) {
+  py::dict o;
+  o["device"] = d.device;
+  o["index"] = d.index;
+  o["numa_node"] = d.numa_node;
+  o["pci_bus_id"] = d.pci_bus_id;
+  o["cpus"] = d.cpus;
+  o["cpulist"] = format_cpulist(d.cpus);
+  o["cpu_share"] = d.cpu_share;
+  o["parse_threads"] = d.parse_threads;
+  o["io_threads"] = d.io_threads;
+  o["source"] = d.source;
+  return o;
+}
+
+static HostDomain domain_from(const py::dict& o) {
+  HostDomain d;
+  auto get_i = [&](const char* k, int dflt) { return o.contains(k) ? o[k].cast<int>() : dflt; };
+  d.device = get_i("device", -1);
+  d.index = get_i("index", 0);
+  d.numa_node = get_i("numa_node", -1);
+  if (o.contains("pci_bus_id")) d.pci_bus_id = o["pci_bus_id"].cast<std::string>();
+  if (o.contains("cpus")) d.cpus = o["cpus"].cast<std::vector<int>>();
+  d.cpu_share = get_i("cpu_share", int(d.cpus.size()));
+  d.parse_threads = get_i("parse_threads", 0);
+  d.io_threads = get_i("io_threads", 1);
+  if (o.contains("source")) d.source = o["source"].cast<std::string>();
+  return d;
+}
+
 static std::shared_ptr<Camera> cam_ref(Worker& w, int idx) {
   std::shared_ptr<Camera> c = w.camera(idx);
   if (!c) throw py::index_error("no camera with index " + std::to_string(idx));
@@ -1123,13 +1153,30 @@ PYBIND11_MODULE(_vep, m) {
     return py::make_tuple(u, s, at_stop);
   });
 
+  m.def(
+      "plan_host_domains",
+      [](const std::vector<int>& devices, const std::vector<std::string>& explicit_cpus, int reserve) {
+        py::list out;
+        for (const HostDomain& d : plan_host_domains(devices, explicit_cpus, reserve)) out.append(domain_dict(d));
+        return out;
+      },
+      py::arg("devices"), py::arg("explicit_cpus") = std::vector<std::string>{}, py::arg("reserve") = 1,
+      "Per-worker host domains (hostplan.h): CPUs, NUMA node, parse / io thread counts");
+  m.def("affinity_cpus", &affinity_cpus);
+  m.def("parse_cpulist", &parse_cpulist);
+  m.def("format_cpulist", &format_cpulist);
+  m.def("cpu_budget", &cpu_budget);
   py::class_<Worker>(m, "Worker")
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
                        std::vector<float> stdv, int max_cameras, int pack_threads,
                        int letterbox_format, int lanes, int stages, int queue, bool lane_threads,
-                       const std::string& decoder, int kf_window_us) {
+                       const std::string& decoder, int kf_window_us, py::object host_domain) {
              WorkerOptions o;
              o.device = device;
+             if (!host_domain.is_none()) {
+               o.domain = domain_from(host_domain.cast<py::dict>());
+               VEP_CHECK(o.domain.device == device, "host_domain belongs to another device");
+             }
              if (decoder == "native") o.decoder = kDecoderNative;
              else if (decoder == "vcn") o.decoder = kDecoderVcn;
              else if (decoder == "auto") o.decoder = kDecoderAuto;
@@ -1155,8 +1202,10 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
            py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0,
            py::arg("queue") = 0, py::arg("lane_threads") = false, py::arg("decoder") = "native",
-           py::arg("kf_window_us") = -1)
+           py::arg("kf_window_us") = -1, py::arg("host_domain") = py::none())
       .def_property_readonly("kf_window_us", &Worker::kf_window_us)
+      .def_property_readonly("host_domain", [](Worker& w) { return domain_dict(w.host_domain()); })
+      .def_property_readonly("ingest_parse_threads", &Worker::ingest_parse_threads)
       .def_property_readonly("device", [](Worker& w) { return w.device().id(); })
       .def_property_readonly("decoder", [](Worker& w) { return std::string(w.vcn() ? "vcn" : "native"); })
       .def_property_readonly("lanes", &Worker::lanes)

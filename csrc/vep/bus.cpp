@@ -151,6 +151,7 @@ void Owner::attach(Worker* w) {
   w_->set_publish_hook([this](int cam, i64 seq) { on_publish(cam, seq); });
   th_ = std::thread([this] {
     name_thread("vep-pump");
+    pin_current_thread(w_->host_domain().cpus);  // (the worker's host domain)
     pump();
   });
 }

@@ -8,9 +8,16 @@
 
 namespace vep {
 
-FanOut::FanOut(int threads) {
-  for (int i = 0; i < threads; ++i) th_.emplace_back([this] {
+namespace {
+thread_local FanOut* tls_pool = nullptr;
+}
+
+void FanOut::bind_thread(FanOut* pool) { tls_pool = pool; }
+
+FanOut::FanOut(int threads, std::function<void()> init) {
+  for (int i = 0; i < threads; ++i) th_.emplace_back([this, init] {
     name_thread("vep-fanout");
+    if (init) init();
     loop();
   });
 }
@@ -25,6 +32,7 @@ FanOut::~FanOut() {
 }
 
 FanOut& FanOut::shared() {
+  if (tls_pool) return *tls_pool;
   // the same CPU share as the parse strands (VEP_INGEST_PARSE_THREADS, else the process's CPU
   // budget minus the socket loops and the GPU launcher): a picture's slices run on the cores its
   // camera's strand would otherwise leave idle, not beyond the process's share

@@ -20,12 +20,15 @@ namespace vep {
 
 class FanOut {
  public:
-  explicit FanOut(int threads);
+  // init runs first on every pool thread (host domain pinning, hostplan.h)
+  explicit FanOut(int threads, std::function<void()> init = {});
   ~FanOut();
   FanOut(const FanOut&) = delete;
   FanOut& operator=(const FanOut&) = delete;
-  // Process-wide pool: VEP_FANOUT_THREADS, else the CPUs this process may use minus one.
+  // The calling thread's pool: the host domain's (bind_thread, set on the parse strands of a GPU
+  // worker's domain), else the process-wide pool (VEP_FANOUT_THREADS, else the CPU budget - 3).
   static FanOut& shared();
+  static void bind_thread(FanOut* pool);
   int size() const { return int(th_.size()); }
   // fn(i) for i in [0, n); returns when every call has returned (rethrows the first exception).
   void run(int n, const std::function<void(int)>& fn);

@@ -6,6 +6,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <new>
+#include <array>
 #include <map>
 #include <shared_mutex>
 
@@ -25,7 +26,9 @@ struct Pool {
   std::shared_mutex reg_mu;
   std::map<const u8*, Region> regions;  // host base -> (len, device base)
   std::mutex mu;
-  std::vector<u8*> free_[kMaxShift + 1];
+  // free blocks per (device the allocating thread was bound to, size class): a domain reuses
+  // blocks on its own NUMA node
+  std::map<int, std::array<std::vector<u8*>, kMaxShift + 1>> free_;
   bool enabled = false;
   size_t max_bytes = 0;
   PoolStats st;
@@ -51,7 +54,11 @@ u8* new_chunk(size_t bytes) {
   return static_cast<u8*>(h);
 }
 
+thread_local int tls_device = -1;
+
 }  // namespace
+
+void bind_thread_device(int device) { tls_device = device; }
 
 void enable_pool(size_t max_bytes) {
   Pool& p = pool();
@@ -69,13 +76,15 @@ bool pool_enabled() {
 std::shared_ptr<u8> pinned_block(size_t n) {
   Pool& p = pool();
   const int cls = class_of(n);
+  const int dev = tls_device;
   u8* blk = nullptr;
   {
     std::lock_guard<std::mutex> g(p.mu);
     if (!p.enabled) return nullptr;
-    if (cls >= 0 && !p.free_[cls].empty()) {
-      blk = p.free_[cls].back();
-      p.free_[cls].pop_back();
+    auto& fl = p.free_[dev];
+    if (cls >= 0 && !fl[size_t(cls)].empty()) {
+      blk = fl[size_t(cls)].back();
+      fl[size_t(cls)].pop_back();
       ++p.st.blocks_reused;
       ++p.st.blocks_live;
     }
@@ -100,13 +109,13 @@ std::shared_ptr<u8> pinned_block(size_t n) {
     ++p.st.chunks;
     ++p.st.blocks_live;
   }
-  return std::shared_ptr<u8>(blk, [cls](u8* b) {
+  return std::shared_ptr<u8>(blk, [cls, dev](u8* b) {
     Pool& q = pool();
     std::lock_guard<std::mutex> g(q.mu);
     --q.st.blocks_live;
     // pooled, never returned to the driver; a dedicated (> 64 MiB) chunk is recycled as a
     // top-class block (it is at least that large)
-    q.free_[cls >= 0 ? cls : kMaxShift].push_back(b);
+    q.free_[dev][size_t(cls >= 0 ? cls : kMaxShift)].push_back(b);
   });
 }
 

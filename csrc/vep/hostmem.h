@@ -26,6 +26,10 @@ namespace vep::hostmem {
 void enable_pool(size_t max_bytes = size_t(8) << 30);
 bool pool_enabled();
 
+// The GPU whose NUMA node the calling thread's new pinned blocks should sit on (a host domain's
+// threads bind their worker's device, hostplan.h; -1: unbound). Blocks are pooled per device.
+void bind_thread_device(int device);
+
 // A block of at least n bytes from the pool (nullptr if disabled or over budget). The memory is
 // returned to the pool when the last reference drops.
 std::shared_ptr<u8> pinned_block(size_t n);

@@ -120,7 +120,7 @@ void IngestSession::start() {
     });
     return;
   }
-  svc_ = IngestServices::acquire();
+  svc_ = w_.ingest_services();  // (the worker's host domain: its GPU's CPUs)
   guard_ = std::make_shared<Guard>();
   parse_live_ = std::make_shared<std::atomic<bool>>(true);
   drop_to_key_ = false;

@@ -1,6 +1,9 @@
 // Shared ingest machinery. See ioloop.h.
 #include "ioloop.h"
 
+#include "fanout.h"
+#include "hostplan.h"
+
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
@@ -16,9 +19,10 @@ namespace vep {
 
 // ------------------------------------------------------------------------------ TaskQueue
 
-TaskQueue::TaskQueue(int threads) {
-  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this] {
+TaskQueue::TaskQueue(int threads, std::function<void()> init) {
+  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this, init] {
     name_thread("vep-task");
+    if (init) init();
     run();
   });
 }
@@ -60,9 +64,10 @@ void TaskQueue::run() {
 
 // ------------------------------------------------------------------------------ StrandPool
 
-StrandPool::StrandPool(int threads) {
-  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this, i] {
+StrandPool::StrandPool(int threads, std::function<void()> init) {
+  for (int i = 0; i < std::max(1, threads); ++i) th_.emplace_back([this, i, init] {
     name_thread("vep-parse");
+    if (init) init();
     run(i);
   });
 }
@@ -150,8 +155,9 @@ void StrandPool::run(int me) {
 
 // ------------------------------------------------------------------------------ TimerQueue
 
-TimerQueue::TimerQueue(TaskQueue& exec) : exec_(exec) { th_ = std::thread([this] {
+TimerQueue::TimerQueue(TaskQueue& exec, std::function<void()> init) : exec_(exec) { th_ = std::thread([this, init] {
     name_thread("vep-timer");
+    if (init) init();
     run();
   });
 }
@@ -194,7 +200,7 @@ void TimerQueue::run() {
 
 // ------------------------------------------------------------------------------ IoLoop
 
-IoLoop::IoLoop(int threads) {
+IoLoop::IoLoop(int threads, std::function<void()> init) {
   for (int i = 0; i < std::max(1, threads); ++i) {
     auto l = std::make_unique<Loop>();
     l->ep = ::epoll_create1(EPOLL_CLOEXEC);
@@ -208,8 +214,9 @@ IoLoop::IoLoop(int threads) {
   }
   for (auto& l : loops_) {
     Loop* lp = l.get();
-    l->th = std::thread([this, lp] {
+    l->th = std::thread([this, lp, init] {
       name_thread("vep-io");
+      if (init) init();
       run(*lp);
     });
   }
@@ -373,7 +380,21 @@ static int env_int(const char* name, int dflt) {
 }
 
 IngestServices::IngestServices(int io_threads, int parse_threads, int connect_threads)
-    : io(io_threads), parse(parse_threads), connect(connect_threads), timers(connect) {}
+    : io(io_threads), parse(parse_threads), connect(connect_threads), timers(connect),
+      parse_threads(std::max(1, parse_threads)), io_threads(std::max(1, io_threads)) {}
+
+// (the fan-out pool helps the parse strands with a picture's slices / tiles / WPP rows: the same
+// CPUs, one thread fewer so a strand's own share of the work is not displaced)
+IngestServices::IngestServices(const HostDomain& d)
+    : fan(std::make_unique<FanOut>(std::max(0, d.parse_threads - 1), domain_thread_init(d, nullptr))),
+      io(d.io_threads, domain_thread_init(d, nullptr)),
+      parse(d.parse_threads, domain_thread_init(d, fan.get())),
+      connect(env_int("VEP_CONNECT_THREADS", 4), domain_thread_init(d, nullptr)),
+      timers(connect, domain_thread_init(d, nullptr)),
+      parse_threads(std::max(1, d.parse_threads)),
+      io_threads(std::max(1, d.io_threads)) {}
+
+IngestServices::~IngestServices() = default;
 
 // Host CPUs this process may use: its affinity mask, bounded by a cgroup v2 CPU quota.
 int cpu_budget() {
@@ -396,8 +417,9 @@ std::shared_ptr<IngestServices> IngestServices::acquire() {
   static std::weak_ptr<IngestServices> cur;
   std::lock_guard<std::mutex> g(mu);
   if (auto s = cur.lock()) return s;
-  // parse strands: the process's CPU budget minus the socket loops and the GPU launcher
-  const int parse_default = std::max(2, std::min(32, cpu_budget() - 2));
+  // parse strands: the process's CPU budget minus the socket loops and the GPU launcher (no
+  // constant cap: a GPU worker with a host domain sizes its own pool, hostplan.h)
+  const int parse_default = std::max(2, cpu_budget() - 2);
   auto s = std::make_shared<IngestServices>(env_int("VEP_IO_THREADS", 2),
                                             env_int("VEP_INGEST_PARSE_THREADS", parse_default),
                                             env_int("VEP_CONNECT_THREADS", 4));

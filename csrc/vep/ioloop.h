@@ -28,7 +28,8 @@ int cpu_budget();
 // Fixed thread pool running posted tasks in FIFO order.
 class TaskQueue {
  public:
-  explicit TaskQueue(int threads);
+  // init (optional) runs first on every pool thread (host domain pinning, hostplan.h)
+  explicit TaskQueue(int threads, std::function<void()> init = {});
   ~TaskQueue();
   void post(std::function<void()> fn);
 
@@ -46,7 +47,7 @@ class TaskQueue {
 // camera's decoder state is still in that core's caches) among the oldest few ready keys.
 class StrandPool {
  public:
-  explicit StrandPool(int threads);
+  explicit StrandPool(int threads, std::function<void()> init = {});
   ~StrandPool();
   // Returns the number of tasks of `key` queued or running after this post.
   size_t post(u64 key, std::function<void()> fn);
@@ -73,7 +74,7 @@ class StrandPool {
 // One-shot timers executed on a TaskQueue.
 class TimerQueue {
  public:
-  explicit TimerQueue(TaskQueue& exec);
+  explicit TimerQueue(TaskQueue& exec, std::function<void()> init = {});
   ~TimerQueue();
   void at(i64 due_ms, std::function<void()> fn);  // mono_us() / 1000 clock
 
@@ -109,7 +110,7 @@ class IoHandler {
 
 class IoLoop {
  public:
-  explicit IoLoop(int threads);
+  explicit IoLoop(int threads, std::function<void()> init = {});
   ~IoLoop();
   // The fd must stay open until remove() / on_closed(). on_readable() runs once right away
   // (bytes may already be buffered by a handshake).
@@ -139,15 +140,21 @@ class IoLoop {
   std::atomic<u32> next_{0};
 };
 
-// Process-wide ingest services shared by every IngestSession (created with the first session,
-// destroyed with the last). Sizes: VEP_IO_THREADS (default 2), VEP_INGEST_PARSE_THREADS
-// (default 4), VEP_CONNECT_THREADS (default 4).
+// Ingest services of one host domain (hostplan.h): the GPU worker's socket loops, parse strands,
+// intra-picture fan-out pool and connector, every thread pinned to the domain's CPUs. A Worker
+// with a host domain owns its services (Worker::ingest_services); acquire() is the process-wide
+// default for workers without one (created with the first session, destroyed with the last;
+// sizes VEP_IO_THREADS (2), VEP_INGEST_PARSE_THREADS (CPU budget - 2), VEP_CONNECT_THREADS (4)).
 struct IngestServices {
+  std::unique_ptr<class FanOut> fan;  // the domain's fan-out pool (null: the process-wide one)
   IoLoop io;
   StrandPool parse;
   TaskQueue connect;
   TimerQueue timers;
+  int parse_threads = 0, io_threads = 0;
   IngestServices(int io_threads, int parse_threads, int connect_threads);
+  explicit IngestServices(const struct HostDomain& d);
+  ~IngestServices();
   static std::shared_ptr<IngestServices> acquire();
 };
 

@@ -13,9 +13,10 @@ namespace vep {
 
 class ThreadPool {
  public:
-  explicit ThreadPool(int n) {
-    for (int i = 0; i < n; ++i) th_.emplace_back([this] {
+  explicit ThreadPool(int n, std::function<void()> init = {}) {
+    for (int i = 0; i < n; ++i) th_.emplace_back([this, init] {
       name_thread("vep-pool");
+      if (init) init();
       run();
     });
   }

@@ -529,12 +529,13 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     const char* dr = std::getenv("VEP_DIRECT_READS");
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
-  if (opt_.pack_threads > 0 && !threaded_) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads);
+  if (opt_.pack_threads > 0 && !threaded_) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads, domain_thread_init(opt_.domain, nullptr));
   if (threaded_)
     for (auto& lp : lanes_) {
       Lane* ln = lp.get();
       ln->th = std::thread([this, ln] {
         name_thread("vep-lane");
+        pin_current_thread(opt_.domain.cpus);
         lane_loop(*ln);
       });
     }
@@ -658,6 +659,20 @@ void Worker::remove_camera(int idx) {
   c.reset();
 }
 
+std::shared_ptr<IngestServices> Worker::ingest_services() {
+  std::lock_guard<std::mutex> g(svc_mu_);
+  if (auto s = svc_.lock()) return s;
+  auto s = opt_.domain.parse_threads > 0 ? std::make_shared<IngestServices>(opt_.domain) : IngestServices::acquire();
+  svc_ = s;
+  return s;
+}
+
+int Worker::ingest_parse_threads() {
+  std::lock_guard<std::mutex> g(svc_mu_);
+  auto s = svc_.lock();
+  return s ? s->parse_threads : 0;
+}
+
 std::shared_ptr<Camera> Worker::camera(int idx) {
   std::lock_guard<std::mutex> g(cams_mu_);
   if (idx < 0 || idx >= int(cams_.size())) return nullptr;
@@ -685,6 +700,7 @@ void Worker::start() {
   stop_ = false;
   th_ = std::thread([this] {
     name_thread("vep-worker");
+    pin_current_thread(opt_.domain.cpus);
     loop();
   });
 }

@@ -23,6 +23,8 @@
 #include "codec.h"
 #include "hevc_dec.h"
 #include "hevc_kern.h"
+#include "hostplan.h"
+#include "ioloop.h"
 #include "gpu.h"
 #include "pool.h"
 #include "vcn.h"
@@ -290,6 +292,10 @@ struct WorkerOptions {
   // copies, as the GPU path's D2H does, so its concurrency (acquire_serve / release_serve, chunk
   // hand-off) runs under ThreadSanitizer without a GPU. Also VEP_MOCK_SERVE=1.
   bool mock_serve = false;
+  // Host domain (hostplan.h): the CPUs this worker's host threads run on and its ingest pool
+  // sizes. parse_threads 0 = none: the worker's threads are not pinned and its cameras share the
+  // process-wide ingest services.
+  HostDomain domain;
 };
 enum DecoderBackend : int { kDecoderNative = 0, kDecoderVcn = 1, kDecoderAuto = 2 };
 
@@ -299,6 +305,13 @@ class Worker {
   ~Worker();
   Device& device() { return dev_; }
   const WorkerOptions& options() const { return opt_; }
+  const HostDomain& host_domain() const { return opt_.domain; }
+  // Ingest services (socket loops, parse strands, fan-out) of this worker's host domain, created
+  // with its first IngestSession and released with the last; the process-wide services when the
+  // worker has no host domain.
+  std::shared_ptr<IngestServices> ingest_services();
+  // Parse strands of the live ingest services (0 when none are running).
+  int ingest_parse_threads();
 
   int add_camera(const std::string& name, int ring_slots);
   void remove_camera(int idx);
@@ -510,6 +523,8 @@ class Worker {
   bool mock_serve_ = false;  // WorkerOptions::mock_serve
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
+  std::mutex svc_mu_;
+  std::weak_ptr<IngestServices> svc_;  // ingest_services()
   std::mutex launch_mu_;
   std::shared_ptr<std::function<void(int, i64)>> publish_hook_;  // (atomic_load / atomic_store)
   std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0}, shed_{0};

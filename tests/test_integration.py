@@ -146,6 +146,9 @@ def test_end_to_end_serving(native, farm, hubapp):
     assert "vep_decode_latency_seconds_bucket" in m and "vep_pinned_pool_bytes" in m
     h = rest.get("/healthz").json()
     assert h["decoder_backends"] == ["native"]
+    hp = h["host_plane"]  # the worker's host domain: its CPUs and its live parse strands
+    assert len(hp) == 1 and hp[0]["cpulist"] and hp[0]["parse_threads"] >= 1
+    assert hp[0]["ingest_parse_threads"] == hp[0]["parse_threads"] and hp[0]["cameras"] == 1
 
     # per-GOP archive on disk: <dir>/<device>/<start_ms>_<dur_ms>.mp4
     t0 = time.time()

@@ -105,6 +105,8 @@ def test_parse_threads_split_cpu_budget(monkeypatch):
     assert utils.parse_threads_per_rank(1) == 15      # single-GPU share: the measured optimum
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 128)
     assert utils.parse_threads_per_rank(8) == 15      # 16 CPUs per rank
+    monkeypatch.setattr(utils, "host_cpu_budget", lambda: 256)
+    assert utils.parse_threads_per_rank(8) == 31      # no constant cap: 32 CPUs per rank
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 64)
     assert utils.parse_threads_per_rank(8) == 7       # 8 per rank, 1 left for launch/lanes
     monkeypatch.setattr(utils, "host_cpu_budget", lambda: 4)

@@ -72,6 +72,10 @@ class GpuConfig:
                                                  # GPU's cameras)
     consumer_rate_hz: float = 0.0                # >0: gather the node's consumer batch this often
                                                  # and hand it to consumer_hook (engine/consumer.py)
+    host_cpus: list = field(default_factory=list)  # per-worker CPU lists ("0-15", ...) overriding the
+                                                 # GPU-local (NUMA) split of the host data plane;
+                                                 # [] = detect (hostplan.h); env VEP_HOST_CPUS
+                                                 # "0-15;16-31;..." also sets it
     consumer_hook: str = ""                      # process isolation: "module:function" each
                                                  # worker process calls with every gathered
                                                  # node batch (fn(batch, names, rank), on its GPU)
@@ -142,6 +146,8 @@ def load_config(path: str | os.PathLike | None = None, data_dir: str | None = No
         _merge(cfg, data)
         if data_dir:
             cfg.data_dir = str(data_dir)
+    if os.environ.get("VEP_HOST_CPUS"):
+        cfg.gpu.host_cpus = [s.strip() for s in os.environ["VEP_HOST_CPUS"].split(";")]
     return cfg
 
 

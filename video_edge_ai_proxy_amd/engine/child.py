@@ -39,7 +39,7 @@ from .shm import ShmSlot, remove_segments
 log = logging.getLogger("vep.child")
 
 # methods of Hub a parent may call
-EXPORTED = {"start_camera", "stop_camera", "state", "logs", "touch", "set_proxy", "proxy",
+EXPORTED = {"start_camera", "stop_camera", "state", "logs", "touch", "set_proxy", "proxy", "host_plane",
             "latest_frame_bytes", "latest_frame", "wait_decoded", "has"}
 
 
@@ -212,13 +212,30 @@ def main(argv=None) -> int:
     ap.add_argument("--device", type=int, required=True)
     ap.add_argument("--config", required=True, help="Config as JSON")
     ap.add_argument("--owner", type=int, default=0, help="frame-bus owner index of this worker")
+    ap.add_argument("--plan-devices", default="",
+                    help="devices of every worker process of the node, comma-separated (this one is "
+                         "entry --owner): each child takes its part of the node's host data plane")
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format=f"%(asctime)s child[{a.device}] %(name)s: %(message)s")
     from ..config import Config, _merge
     from .hub import Hub
 
     cfg = _merge(Config(), json.loads(a.config))
-    hub = Hub(cfg, devices=[a.device], bus_owner=a.owner)
+    from .._native import native
+
+    # this child's host domain: the plan over every worker process of the node (deterministic,
+    # so the children agree without talking), the whole process pinned to its CPUs
+    plan_devices = [int(x) for x in a.plan_devices.split(",") if x != ""] or [a.device]
+    idx = a.owner if a.owner < len(plan_devices) else 0
+    explicit = [str(c) for c in (cfg.gpu.host_cpus or [])]
+    dom = native.plan_host_domains(plan_devices, explicit)[idx]
+    dom["device"] = a.device
+    if dom["cpus"]:
+        try:
+            os.sched_setaffinity(0, dom["cpus"])
+        except OSError:
+            pass
+    hub = Hub(cfg, devices=[a.device], bus_owner=a.owner, host_domains=[dom])
     group = RankGroup(hub, a.device, cfg.gpu.consumer_hook)
     key = bytes.fromhex(os.environ["VEP_CHILD_KEY"])
     listener = Listener(("127.0.0.1", 0), authkey=key)

@@ -63,7 +63,8 @@ def place_camera(name: str, loads: list[int], policy: str = "least_loaded") -> i
 
 
 class Hub:
-    def __init__(self, cfg: Config, devices: Optional[list[int]] = None, bus_owner: int = 0):
+    def __init__(self, cfg: Config, devices: Optional[list[int]] = None, bus_owner: int = 0,
+                 host_domains: Optional[list[dict]] = None):
         self.cfg = cfg
         if devices is None:
             devices = list(cfg.gpu.devices) if cfg.gpu.devices else list(range(gpu_count()))
@@ -71,13 +72,19 @@ class Hub:
             devices = [-1]  # CPU backend (no GPU visible)
         self.devices = devices
         g = cfg.gpu
+        # per-GPU host data plane (hostplan.h): each worker's ingest sockets, parse strands and
+        # GPU feeder threads run on its own CPU set (the GPU's NUMA-local CPUs, split among the
+        # workers sharing them), sized from the process's CPU budget / workers
+        if host_domains is None:
+            host_domains = native.plan_host_domains(list(devices), [str(c) for c in (g.host_cpus or [])])
+        self.host_domains = host_domains
         self.workers = []
-        for d in devices:
+        for d, dom in zip(devices, host_domains):
             w = native.Worker(device=d, letterbox_size=int(g.letterbox_size),
                               chw_dtype=_CHW.get(g.letterbox_dtype, 0), mean=list(g.mean),
                               std=list(g.std), max_cameras=int(g.max_cameras_per_gpu),
                               letterbox_format=1 if g.letterbox_format == "nv12" else 0,
-                              decoder=str(getattr(g, "decoder", "native")))
+                              decoder=str(getattr(g, "decoder", "native")), host_domain=dom)
             w.start()
             self.workers.append(w)
         # Consumer batch: with letterbox_size > 0 every worker letterboxes each frame it publishes
@@ -234,6 +241,20 @@ class Hub:
         self.archiver.flush()
 
     # ------------------------------------------------------------------ state
+    def host_plane(self) -> list[dict]:
+        """Each worker's host domain: device, NUMA node, CPU list, parse / io threads planned and
+        the parse strands its live ingest services run (0 until its first camera)."""
+        out = []
+        loads = self._loads()
+        for i, w in enumerate(self.workers):
+            d = dict(w.host_domain)
+            d.pop("cpus", None)  # (cpulist says it compactly)
+            d["ingest_parse_threads"] = w.ingest_parse_threads
+            d["cameras"] = loads[i]
+            d["pid"] = os.getpid()
+            out.append(d)
+        return out
+
     def state(self, name: str) -> dict:
         h = self.handle(name)
         w = self.workers[h.worker_index]

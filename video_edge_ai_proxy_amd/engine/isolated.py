@@ -65,7 +65,7 @@ _ERRORS = {"CameraNotFound": CameraNotFound, "CameraExists": CameraExists, "KeyE
 
 class _Child:
     def __init__(self, device: int, cfg_json: str, nconn: int = 4, start_timeout_s: float = 180.0,
-                 owner: int = 0, first_start: bool = True):
+                 owner: int = 0, first_start: bool = True, plan_devices: Optional[list[int]] = None):
         self.device = device
         key = secrets.token_bytes(16)
         env = dict(os.environ, VEP_CHILD_KEY=key.hex())
@@ -74,7 +74,8 @@ class _Child:
         env["PYTHONPATH"] = _PKG_PARENT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
         self.proc = subprocess.Popen(
             [sys.executable, "-m", "video_edge_ai_proxy_amd.engine.child", "--device", str(device),
-             "--config", cfg_json, "--owner", str(owner)],
+             "--config", cfg_json, "--owner", str(owner),
+             "--plan-devices=" + ",".join(str(d) for d in (plan_devices or [device]))],
             stdin=subprocess.PIPE, stdout=subprocess.PIPE, env=env)
         line = b""
         deadline = time.time() + start_timeout_s
@@ -253,7 +254,8 @@ class ProcessHub:
 
         self.bus = native.BusReader(cfg.bus_tag)
         with ThreadPoolExecutor(max_workers=len(self.devices)) as ex:  # start them side by side
-            futs = [ex.submit(_Child, d, self._cfg_json, owner=i) for i, d in enumerate(self.devices)]
+            futs = [ex.submit(_Child, d, self._cfg_json, owner=i, plan_devices=self.devices)
+                    for i, d in enumerate(self.devices)]
         errs = [f.exception() for f in futs]
         started = [f.result() for f, e in zip(futs, errs) if e is None]
         if any(e is not None for e in errs):
@@ -306,7 +308,7 @@ class ProcessHub:
         remove_segments(dead.pid)  # and the segments it could not unlink itself
         _remove_bus_segments(dead.pid)
         self._group_ok = False  # the survivors' group lost a rank: re-form before the next gather
-        child = _Child(self.devices[i], self._cfg_json, owner=i, first_start=False)
+        child = _Child(self.devices[i], self._cfg_json, owner=i, first_start=False, plan_devices=self.devices)
         try:
             with self._lock:
                 mine = [n for n, h in self.cameras.items() if h.worker_index == i]
@@ -509,6 +511,16 @@ class ProcessHub:
         self._pool.shutdown(wait=False)
 
     # ------------------------------------------------------------------ state / control / frames
+    def host_plane(self) -> list[dict]:
+        """Each worker process's host domain (Hub.host_plane of every child)."""
+        out = []
+        for i in range(len(self._children)):
+            try:
+                out += self._child(i).call("host_plane")
+            except Exception:  # noqa: BLE001 — a restarting child
+                out.append({"device": self.devices[i], "index": i, "restarting": True})
+        return out
+
     def state(self, name: str) -> dict:
         h = self.handle(name)
         child = self._children[h.worker_index]

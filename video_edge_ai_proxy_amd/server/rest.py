@@ -131,7 +131,9 @@ def create_app(pm: ProcessManager, sm: SettingsManager, metrics=None) -> FastAPI
         out = {"ok": True, "cameras": len(pm.hub.cameras), "devices": pm.hub.devices,
                "decoder_backends": [w.decoder for w in pm.hub.workers],
                "vcn_available": bool(native.rocdecode_available()),
-               "direct_host_reads": [bool(w.direct_reads) for w in pm.hub.workers]}
+               "direct_host_reads": [bool(w.direct_reads) for w in pm.hub.workers],
+               # per-GPU host data plane: each worker's CPU list, NUMA node and parse threads
+               "host_plane": pm.hub.host_plane() if hasattr(pm.hub, "host_plane") else []}
         if metrics is not None and metrics.consumer is not None:
             out["consumer"] = metrics.consumer.stats()
         return out

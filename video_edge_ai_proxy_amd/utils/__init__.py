@@ -79,10 +79,11 @@ def host_cpu_budget() -> int:
     return max(1, n)
 
 
-def parse_threads_per_rank(local_world: int, cap: int = 15, reserve: int = 1) -> int:
+def parse_threads_per_rank(local_world: int, reserve: int = 1) -> int:
     """Host parse threads for one rank: the node's CPU budget split over the ranks that share
-    it, minus ``reserve`` for the rank's launcher / lane / gRPC threads, capped at ``cap``
-    (15 on a 16-CPU single-GPU share: the measured optimum with cache-affine parse pools,
-    profiles/r2/sweep_threads_s2.txt; 14 before them, profiles/r1_sweep_threads_v17.txt)."""
+    it, minus ``reserve`` for the rank's launcher / lane / gRPC threads, with no constant cap
+    (15 on a 16-CPU single-GPU share, the measured optimum: profiles/r2/sweep_threads_s2.txt).
+    The GPU ranks' own plan is the native ``plan_host_domains`` (hostplan.h: the same split,
+    pinned to each GPU's NUMA-local CPUs); this is the fallback without the extension."""
     share = host_cpu_budget() // max(1, local_world)
-    return max(2, min(cap, share - reserve))
+    return max(2, share - reserve)
