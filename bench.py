@@ -130,6 +130,9 @@ def parse_args():
                     help="concurrent gRPC clients for the latency run (one camera each)")
     ap.add_argument("--client-procs", type=int, default=0,
                     help="processes the latency clients run in (0 = half the rank's CPU budget)")
+    ap.add_argument("--serving", choices=["native", "grpcio"], default="native",
+                    help="latency run's gRPC endpoint: the native HTTP/2 server on the worker's frame bus "
+                         "(vep serve's default) or the grpcio ImageService")
     ap.add_argument("--latency-seconds", type=float, default=4.0,
                     help="duration of the concurrent-client latency run")
     a = ap.parse_args()
@@ -226,10 +229,12 @@ def latency_fields(a, lat, live_fps=None):
                                f"it, up to one frame interval); {len(lat['next'])} samples over "
                                f"{a.latency_seconds:g} s"),
         "latency_frames_served_per_s": round(lat["frames_served"] / a.latency_seconds, 1),
+        "serving_endpoint": ("native HTTP/2 gRPC endpoint (csrc/vep/rpcsrv.h) on the worker's frame bus"
+                             if a.serving == "native" else "grpcio ImageService"),
         "server_p50_ms": r3(srv[0]),
         "server_p99_ms": r3(srv[1]),
-        "server_latency_definition": "server side: request received -> serialized frame handed to grpcio "
-                                     "(includes waiting for the next frame)",
+        "server_latency_definition": "server side: request received -> serialized frame queued for the "
+                                     "connection (includes waiting for the next frame)",
         "serve_p50_latency_ms": r3(sv[0]),
         "serve_p99_latency_ms": r3(sv[1]),
         "serve_latency_definition": "one request per fresh connected channel, no concurrent clients: the "
@@ -566,7 +571,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             if pool is not None:
                 lp0, lt0 = worker.pictures, time.perf_counter()
                 lat = measure(pool, worker, farm.idx, duration_s=a.latency_seconds,
-                              serve_samples=a.latency_samples)
+                              serve_samples=a.latency_samples, native=a.serving == "native")
                 live_fps = (worker.pictures - lp0) / (time.perf_counter() - lt0) / cams
                 lat["settled"] = settled
                 lat["live_skipped"] = farm.stats()["skipped"] - ls0
@@ -850,7 +855,7 @@ def main():
         with ticking(lambda: (rb.step(), rb.drain()), float(a.fps)):
             time.sleep(0.5)
             lat = measure(pool, worker, list(rb.cameras), duration_s=a.latency_seconds,
-                          serve_samples=a.latency_samples)
+                          serve_samples=a.latency_samples, native=a.serving == "native")
         pool.close()
     if world > 1:
         dist.barrier()

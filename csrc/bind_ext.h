@@ -6,3 +6,4 @@ void bind_net(pybind11::module_& m);
 void bind_mux(pybind11::module_& m);
 void bind_hevc(pybind11::module_& m);
 void bind_bus(pybind11::module_& m);
+void bind_rpc(pybind11::module_& m);

@@ -1606,4 +1606,5 @@ PYBIND11_MODULE(_vep, m) {
   bind_mux(m);
   bind_hevc(m);
   bind_bus(m);
+  bind_rpc(m);
 }

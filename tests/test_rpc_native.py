@@ -1,0 +1,187 @@
+"""Native gRPC endpoint (csrc/vep/rpcsrv.h): HTTP/2 + HPACK in C++, VideoLatestImage served from
+the frame bus without Python, the other Image methods through a callback. Checked against the
+RFC 7541 Appendix C examples and, end to end, with the unchanged grpcio client (ImageClient, what
+examples/basic_usage.py uses). Reference: server/grpcapi/grpc_api.go:133-235."""
+import os
+import random
+import threading
+import time
+
+import grpc
+import numpy as np
+import pytest
+
+from conftest import synth
+
+
+# RFC 7541 Appendix C.4 / C.6 Huffman-coded strings
+RFC_HUFFMAN = [("www.example.com", "f1e3c2e5f23a6ba0ab90f4ff"), ("no-cache", "a8eb10649cbf"),
+               ("custom-key", "25a849e95ba97d7f"), ("custom-value", "25a849e95bb8e8b4bf"), ("302", "6402"),
+               ("private", "aec3771a4b"),
+               ("Mon, 21 Oct 2013 20:13:21 GMT", "d07abe941054d444a8200595040b8166e082a62d1bff"),
+               ("https://www.example.com", "9d29ad171863c78f0b97c8e9ae82ae43d3")]
+
+
+def test_huffman_matches_rfc7541(native):
+    for text, hx in RFC_HUFFMAN:
+        assert native.hpack_huffman_encode(text.encode()).hex() == hx
+        assert native.hpack_huffman_decode(bytes.fromhex(hx)) == text.encode()
+    rng = random.Random(7)
+    for _ in range(300):  # every byte value round-trips
+        s = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 40)))
+        assert native.hpack_huffman_decode(native.hpack_huffman_encode(s)) == s
+    assert native.hpack_huffman_decode(b"\x00\x00\x00\x00\xff") is None or True  # (no crash on junk)
+    assert native.hpack_huffman_decode(bytes.fromhex("f1e3c2e5f23a6ba0ab90f4") + b"\x00") is None  # bad padding
+
+
+@pytest.mark.parametrize("huff", [False, True])
+def test_hpack_decoder_rfc7541_request_sequences(native, huff):
+    """Appendix C.3 (no Huffman) / C.4 (Huffman): three requests on one connection, the dynamic
+    table carried between them."""
+    blocks = ["828684410f7777772e6578616d706c652e636f6d", "828684be58086e6f2d6361636865",
+              "828785bf400a637573746f6d2d6b65790c637573746f6d2d76616c7565"]
+    if huff:
+        blocks = ["828684418cf1e3c2e5f23a6ba0ab90f4ff", "828684be5886a8eb10649cbf",
+                  "828785bf408825a849e95ba97d7f8925a849e95bb8e8b4bf"]
+    want = [[(":method", "GET"), (":scheme", "http"), (":path", "/"), (":authority", "www.example.com")],
+            [(":method", "GET"), (":scheme", "http"), (":path", "/"), (":authority", "www.example.com"),
+             ("cache-control", "no-cache")],
+            [(":method", "GET"), (":scheme", "https"), (":path", "/index.html"), (":authority", "www.example.com"),
+             ("custom-key", "custom-value")]]
+    d = native.HpackDecoder()
+    for blk, w, size in zip(blocks, want, [57, 110, 164]):
+        assert d.decode(bytes.fromhex(blk)) == w
+        assert d.table_size == size
+    assert d.decode(b"\xff") is None  # index out of range
+
+
+def _owner(native, tag, n=4):
+    w = native.Worker(device=-1)
+    w.start()
+    o = native.BusOwner(tag, 0, n)
+    o.attach(w)
+    return w, o
+
+
+def _handler(calls):
+    from video_edge_ai_proxy_amd.proto import pb
+
+    def h(method, req, peer):
+        calls.append((method, peer))
+        if method == "ListStreams":
+            return 0, "", [pb.ListStream(name=n, running=True).SerializeToString() for n in ("a", "b")]
+        if method == "Annotate":
+            return 3, "device_name required (é)", []  # INVALID_ARGUMENT, non-ASCII message
+        return 0, "", [pb.ProxyResponse(device_id="x", passthrough=True).SerializeToString()]
+    return h
+
+
+def test_native_endpoint_serves_bus_frames_to_grpcio_clients(native):
+    from video_edge_ai_proxy_amd.proto import pb
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
+    tag = f"t{os.getpid()}r"
+    w, o = _owner(native, tag)
+    calls = []
+    srv = native.RpcServer("127.0.0.1", 0, tag, io_threads=2, wait_threads=16, slow_threads=2,
+                           handler=_handler(calls), reuseport=False)
+    cli = ImageClient(f"127.0.0.1:{srv.port}")
+    try:
+        cam = w.add_camera("camR", 3)
+        o.add(cam, "camR")
+        enc, ref = synth(native, 320, 240, gop=5), native.CpuDecoder()
+        want = []
+        for _ in range(3):
+            au = enc.next()
+            want.append(ref.decode(au))
+            w.decode_now(cam, au)
+        # a waiting client gets the newest frame: the bytes the in-process encoder produces
+        vf = cli.latest_frame("camR")
+        seq, same, _ = w.video_frame(cam, 0, "camR")
+        assert vf.SerializeToString() == same
+        assert (vf.width, vf.height, vf.device_id) == (320, 240, "camR")
+        assert np.array_equal(np.frombuffer(vf.data, np.uint8).reshape(240, 320, 3), want[-1])
+        # the next request on a fresh stream waits for a newer frame (per-connection cursor)
+        got = {}
+        th = threading.Thread(target=lambda: got.setdefault("vf", cli.latest_frame("camR")))
+        th.start()
+        time.sleep(0.2)
+        au = enc.next()
+        want.append(ref.decode(au))
+        w.decode_now(cam, au)
+        th.join(timeout=10)
+        assert np.array_equal(np.frombuffer(got["vf"].data, np.uint8).reshape(240, 320, 3), want[-1])
+        assert got["vf"].pts != vf.pts
+        # several requests on one bidirectional stream: one response each
+        reqs = [pb.VideoFrameRequest(device_id="camR", key_frame_only=True) for _ in range(2)]
+        it = cli.VideoLatestImage(iter(reqs), timeout=20)
+        t0 = time.time()
+        res = list(it)
+        assert len(res) == 2 and time.time() - t0 < 10  # (the second: empty after 3 x 1 s at most)
+        assert w.keyframe_only(cam)  # the request marked keyframe-only mode on the camera
+        # unknown device -> an empty VideoFrame (reference behaviour)
+        assert cli.latest_frame("nope").width == 0
+        # the other methods through the callback
+        ls = list(cli.ListStreams(pb.ListStreamRequest()))
+        assert [s.name for s in ls] == ["a", "b"]
+        with pytest.raises(grpc.RpcError) as e:
+            cli.Annotate(pb.AnnotateRequest())
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT and e.value.details() == "device_name required (é)"
+        assert cli.Proxy(pb.ProxyRequest(device_id="x", passthrough=True)).passthrough
+        assert {m for m, _ in calls} == {"ListStreams", "Annotate", "Proxy"}
+        assert all(p.startswith("ipv4:127.0.0.1:") for _, p in calls)
+        # a method the service does not have
+        un = cli.channel.unary_unary("/chrys.cloud.videostreaming.v1beta1.Image/Nope")
+        with pytest.raises(grpc.RpcError) as e:
+            un(b"")
+        assert e.value.code() == grpc.StatusCode.UNIMPLEMENTED
+        st = srv.stats()
+        # (the bidi stream's two requests found no frame newer than the connection's cursor)
+        assert st["frames_served"] == 2 and st["empty_frames"] == 3
+        assert st["protocol_errors"] == 0 and st["slow_calls"] == 3
+    finally:
+        cli.close()
+        srv.stop()
+        o.stop()
+        w.stop()
+
+
+def test_native_endpoint_many_clients_share_one_copy(native):
+    """32 clients (own connections) of one 1080p camera: every one gets each new frame, and the
+    serving process copies each frame out of the bus once, not once per client."""
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
+    tag = f"t{os.getpid()}s"
+    w, o = _owner(native, tag)
+    srv = native.RpcServer("127.0.0.1", 0, tag, io_threads=2, wait_threads=64, reuseport=False)
+    clients = [ImageClient(f"127.0.0.1:{srv.port}", own_connection=True) for _ in range(32)]
+    try:
+        cam = w.add_camera("big", 3)
+        o.add(cam, "big")
+        enc = synth(native, 1920, 1080, gop=10)
+        w.decode_now(cam, enc.next())
+        for c in clients:  # every connection's cursor at the current frame
+            assert c.latest_frame("big").width == 1920
+        for rnd in range(3):
+            out = [None] * len(clients)
+
+            def get(i):
+                out[i] = clients[i].latest_frame("big")
+
+            ths = [threading.Thread(target=get, args=(i,)) for i in range(len(clients))]
+            for t in ths:
+                t.start()
+            time.sleep(0.3)
+            w.decode_now(cam, enc.next())
+            for t in ths:
+                t.join(timeout=30)
+            assert all(v is not None and v.width == 1920 and len(v.data) == 1920 * 1080 * 3 for v in out)
+            assert len({v.pts for v in out}) == 1  # everyone got the same (newest) frame
+        st = srv.stats()
+        assert st["connections"] == 32 and st["frames_served"] >= 128 and st["frame_copies"] <= 8
+    finally:
+        for c in clients:
+            c.close()
+        srv.stop()
+        o.stop()
+        w.stop()

@@ -10,13 +10,17 @@ from out-of-process clients (ClientPool: several clients per camera when clients
     D2H-copies its frame through the worker's pinned serve pool);
   * ``frontends=K``: K serving processes bound to one port with SO_REUSEPORT, reading the frame bus
     (server/frontend.py): one DMA per frame for all of a camera's clients, no GPU context and no
-    connection to the decoding process.
+    connection to the decoding process;
+  * ``native:K`` (--modes): the same with the native HTTP/2 endpoint (csrc/vep/rpcsrv.h) in the
+    serving processes instead of grpcio; ``native:0`` runs it inside the decoding process (the
+    default ``vep serve`` path on one GPU), reading that process's own frame bus.
 
 Reported per pair: p50 / p99 client latency (request sent -> next frame received and parsed),
 aggregate frames/s served, and the CPU the machine, the serving processes and the clients used.
 Every process is started before this one touches the GPU.
 
     python tools/bench_serving.py --cams 32 --clients 32,128,256 --frontends 0,1,2,4
+    python tools/bench_serving.py --cams 32 --clients 128,256 --modes native:0,native:2,grpcio:2
     python tools/bench_serving.py --codec h265 --width 3840 --height 2160 --cams 8 --clients 8,32
     python tools/bench_serving.py --cpu --width 320 --height 240 ...   (CPU backend rehearsal)
 
@@ -98,6 +102,7 @@ def main() -> int:
     ap.add_argument("--slices", type=int, default=1, help="slices per picture (H.265 4K: 8, parsed in parallel)")
     ap.add_argument("--clients", default="32,128")
     ap.add_argument("--frontends", default="0,1,4", help="serving processes per trial (0 = in-process server)")
+    ap.add_argument("--modes", default="", help="serving modes 'kind:K' (kind grpcio | native); overrides --frontends")
     ap.add_argument("--client-threads", type=int, default=8, help="client threads per client process")
     ap.add_argument("--serve-threads", type=int, default=256)
     ap.add_argument("--duration", type=float, default=4.0)
@@ -108,13 +113,16 @@ def main() -> int:
     from video_edge_ai_proxy_amd.server.frontend import FrontendPool
     from vep_bench.latency_clients import ClientPool
 
-    clients, fronts = ints(a.clients), ints(a.frontends)
+    clients = ints(a.clients)
+    modes = ([(m.split(":")[0], int(m.split(":")[1])) for m in a.modes.split(",") if m.strip()] if a.modes
+             else [("grpcio", k) for k in ints(a.frontends)])
     tag = f"sb{os.getpid()}"
     # every process first: this one initialises the GPU below
     t = a.client_threads
     pool = ClientPool(max(1, -(-max(clients) // t)), t)
-    fpools = {k: FrontendPool(k, tag, f"127.0.0.1:{free_port()}", f"127.0.0.1:{free_port()}", a.serve_threads)
-              for k in fronts if k > 0}
+    fpools = {(kind, k): FrontendPool(k, tag, f"127.0.0.1:{free_port()}", f"127.0.0.1:{free_port()}", a.serve_threads,
+                                      native=kind == "native")
+              for kind, k in modes if k > 0}
 
     import psutil
     import torch
@@ -159,18 +167,25 @@ def main() -> int:
     base = {"cams": a.cams, "resolution": f"{a.width}x{a.height}", "codec": a.codec, "fps": a.fps, "slices": a.slices,
             "backend": "gfx950" if use_gpu else "cpu", "frame_bytes": a.width * a.height * 3,
             "cpus": psutil.cpu_count(), "client_threads_per_process": t}
+    nsrv = None
     try:
-        for k in fronts:
+        for kind, k in modes:
             for m in clients:
                 procs = max(1, -(-m // t))
-                if k == 0:
+                if k == 0 and kind == "native":
+                    ctx, svc = None, None
+                    if nsrv is None:
+                        nsrv = vep.RpcServer("127.0.0.1", 0, tag, wait_threads=max(64, 2 * m), reuseport=False)
+                    target = f"127.0.0.1:{nsrv.port}"
+                    srv_pids = [os.getpid()]
+                elif k == 0:
                     ctx = serving(w, cams, workers=max(64, 2 * m))
                     target, _, svc = ctx.__enter__()
                     srv_pids = [os.getpid()]
                 else:
                     ctx, svc = None, None
-                    target = f"127.0.0.1:{fpools[k].port}"
-                    srv_pids = [fpools[k].p.pid]
+                    target = f"127.0.0.1:{fpools[(kind, k)].port}"
+                    srv_pids = [fpools[(kind, k)].p.pid]
                 try:
                     pool.run(target, names, mode="next", duration_s=1.0, procs=procs)  # connect + warm
                     pub0, dma0 = owner.published, owner.dma_bytes
@@ -193,23 +208,31 @@ def main() -> int:
                 busy = (c1.user + c1.system) - (c0.user + c0.system)
                 p50, p99 = summarize(lat)
                 served = len(lat) / a.duration
-                r = dict(base, frontends=k, clients=m, client_procs=procs,
+                r = dict(base, serving=kind, frontends=k, clients=m, client_procs=procs,
                          p50_ms=round(p50, 2) if p50 else None, p99_ms=round(p99, 2) if p99 else None,
                          samples=len(lat), frames_served_per_s=round(served, 1),
                          served_gbytes_per_s=round(served * a.width * a.height * 3 / 1e9, 2),
                          decoded_frames_per_s=round((f1 - f0) / el, 1),
                          # packet arrival -> frame published (the worker's per-camera histogram)
                          publish_latency_ms_p50=hist_pct(h0, h1, 0.5), publish_latency_ms_p99=hist_pct(h0, h1, 0.99),
-                         bus_dma_frames=(owner.published - pub0) if k > 0 else None,
-                         bus_dma_gbytes_per_s=round((owner.dma_bytes - dma0) / el / 1e9, 2) if k > 0 else None,
+                         bus_dma_frames=(owner.published - pub0) if (k > 0 or kind == "native") else None,
+                         bus_dma_gbytes_per_s=(round((owner.dma_bytes - dma0) / el / 1e9, 2)
+                                               if (k > 0 or kind == "native") else None),
                          machine_cpu_busy=round(busy / el, 2),
                          serving_cpu=round((s1 - s0) / el, 2), client_cpu=round((k1 - k0) / el, 2),
+                         # serving CPU seconds per GB served (k > 0: the serving processes alone)
+                         serving_cpu_s_per_gb=(round((s1 - s0) / el / (served * a.width * a.height * 3 / 1e9), 3)
+                                               if k > 0 and served > 0 else None),
                          latency_definition="client-side: request sent -> the camera's next VideoFrame "
                                             "received and parsed (back-to-back requests, includes waiting "
                                             "for the frame, up to one frame interval)")
+                if nsrv is not None and k == 0 and kind == "native":
+                    r["native_stats"] = nsrv.stats()
                 print(json.dumps(r), flush=True)
                 out.append(r)
     finally:
+        if nsrv is not None:
+            nsrv.stop()
         for s in sess:
             s.stop()
         owner.stop()

@@ -1,5 +1,7 @@
-"""Client-observed ``VideoLatestImage`` latency for bench.py, through the production gRPC path
-(ImageService -> native ring D2H into the response bytes -> grpcio -> client decode).
+"""Client-observed ``VideoLatestImage`` latency for bench.py, through the production gRPC path:
+by default the native HTTP/2 endpoint ``vep serve`` runs (csrc/vep/rpcsrv.h: the worker's frame
+bus -> one shared copy per frame -> writev), or (``native=False``) the grpcio ImageService
+(native ring D2H into the response bytes -> grpcio). Client decode in separate processes.
 
 The server runs in the bench (GPU) process; the clients run in separate processes
 (:class:`~vep_bench.latency_clients.ClientPool`, started before the bench
@@ -51,10 +53,53 @@ class _PM:
         self.hub = hub
 
 
+class _NativeSvc:
+    """The counters measure() reads, from the native endpoint."""
+
+    def __init__(self, srv):
+        self.srv = srv
+        self.latencies_ms = _Lat(srv)
+
+    @property
+    def frames_served(self):
+        return self.srv.stats()["frames_served"]
+
+
+class _Lat(list):
+    def __init__(self, srv):
+        super().__init__()
+        self.srv = srv
+
+    def clear(self):
+        self.srv.take_latencies()
+
+    def __iter__(self):
+        return iter(self.srv.take_latencies())
+
+
 @contextmanager
-def serving(worker, cams, workers: int = 64):
-    """gRPC server (this process) over the worker's cameras: yields (target, camera names, svc)."""
+def serving(worker, cams, workers: int = 64, native: bool = True):
+    """gRPC server (this process) over the worker's cameras: yields (target, camera names, svc).
+    native: the worker's cameras go on a frame bus and the native endpoint serves them (the
+    production default); else the grpcio ImageService reads the worker's rings."""
     hub = _WorkerHub(worker, cams)
+    if native:
+        import os
+
+        from video_edge_ai_proxy_amd import native as vep
+
+        tag = f"bl{os.getpid()}"
+        owner = vep.BusOwner(tag, 0, max(cams) + 1)
+        owner.attach(worker)
+        for name, c in hub.map.items():
+            owner.add(c, name)
+        srv = vep.RpcServer("127.0.0.1", 0, tag, wait_threads=workers, reuseport=False)
+        try:
+            yield f"127.0.0.1:{srv.port}", list(hub.map), _NativeSvc(srv)
+        finally:
+            srv.stop()
+            owner.stop()
+        return
     svc = ImageService(_PM(hub))
     server = serve(svc, "127.0.0.1:0", workers=workers, tune_malloc=True)  # (a serving-only process)
     try:
@@ -87,10 +132,10 @@ def ticking(tick, fps: float):
             th.join(timeout=10)
 
 
-def measure(pool, worker, cams, duration_s: float = 3.0, serve_samples: int = 100):
+def measure(pool, worker, cams, duration_s: float = 3.0, serve_samples: int = 100, native: bool = True):
     """Runs the ``serve`` then the ``next`` measurement on the out-of-process ``pool``.
     Returns {"serve": [ms...], "next": [ms...], "frames_served": n, "server_ms": [...]}."""
-    with serving(worker, cams, workers=max(16, 2 * pool.clients)) as (target, names, svc):
+    with serving(worker, cams, workers=max(16, 2 * pool.clients), native=native) as (target, names, svc):
         serve_ms = pool.run(target, names, mode="serve", samples=serve_samples, procs=1) if serve_samples else []
         svc.latencies_ms.clear()
         n0 = svc.frames_served

@@ -9,6 +9,8 @@ not be the one that starts other programs), each running several client threads.
 
 A job is one JSON line on a worker's stdin; the worker answers with one JSON line of latencies.
 Two modes, both measured client-side (request sent -> ``VideoFrame`` received and parsed):
+Every client has its own TCP connection (grpc-core would otherwise share one connection among
+the channels of a process, and the server's per-connection cursors and HTTP/2 streams with it).
   * ``next``: each client owns one connected channel and camera and issues back-to-back
     ``VideoLatestImage`` requests (the reference example clients' pattern,
     examples/opencv_display.py:43-45); every answer is a frame newer than the client's previous
@@ -113,7 +115,7 @@ def _client_next(target, name, key_frame_only, start_at, duration, lat, errors):
 
     from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
 
-    cli = ImageClient(target)
+    cli = ImageClient(target, own_connection=True)  # (a camera viewer: its own TCP connection)
     try:
         grpc.channel_ready_future(cli.channel).result(timeout=20)
         cli.latest_frame(name, key_frame_only)  # the server-side cursor sits at the current frame
@@ -136,7 +138,7 @@ def _client_serve(target, names, key_frame_only, samples, lat, errors):
 
     from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
 
-    clis = [ImageClient(target) for _ in range(samples)]
+    clis = [ImageClient(target, own_connection=True) for _ in range(samples)]
     try:
         for c in clis:
             grpc.channel_ready_future(c.channel).result(timeout=20)

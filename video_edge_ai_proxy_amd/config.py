@@ -83,13 +83,21 @@ class GpuConfig:
 
 @dataclass
 class ServingConfig:
-    """Frame serving. ``frontends`` > 0 runs that many gRPC serving processes, all bound to
+    """Frame serving. ``frontends`` > 0 runs that many serving processes, all bound to
     ``grpc_port`` with SO_REUSEPORT (the kernel spreads client connections over them); they read
     frames from the node's frame bus (shared memory, csrc/vep/bus.h) and forward the other RPCs to
-    the main process. -1 = one per GPU; 0 = serve from the main process."""
-    frontends: int = 0
-    threads: int = 256          # gRPC handler threads per serving process (each waits <= 3 x 1 s)
+    the main process. -1 = one per GPU; 0 = serve from the main process; -2 (default) = auto: one
+    per GPU when the node has more than one GPU, else the main process.
+
+    ``native`` (default): VideoLatestImage is answered by the native HTTP/2 gRPC endpoint
+    (csrc/vep/rpcsrv.h: C++, no interpreter lock, straight from the frame bus); the other methods
+    go to the grpcio server, which then listens on an internal loopback port. ``native: false``
+    serves every method with grpcio (round 4's path)."""
+    frontends: int = -2
+    threads: int = 256          # handler threads per serving process (each request waits <= 3 x 1 s)
     bus: bool = False           # main-process serving also reads the frame bus (shared DMA per frame)
+    native: bool = True
+    io_threads: int = 2         # native endpoint: epoll threads per serving process
 
 
 @dataclass

@@ -46,6 +46,7 @@ class HubApp:
     metrics: Metrics
     frontends: Optional[object] = None  # server.frontend.FrontendPool (serving.frontends > 0)
     public_grpc_port: int = 0
+    native_server: Optional[object] = None  # native.RpcServer (serving.native, main-process serving)
     consumer_loop: Optional[object] = None  # engine.consumer.ConsumerLoop (gpu.consumer_rate_hz > 0)
 
     @property
@@ -60,6 +61,8 @@ class HubApp:
         log.info("shutting down")
         if self.frontends is not None:
             self.frontends.close()
+        if self.native_server is not None:
+            self.native_server.stop()
         try:
             self.grpc_server.stop(grace=2).wait(5)
         except Exception:
@@ -87,9 +90,14 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
     # the frame bus, so every decoding process publishes one (cfg.bus_tag); the isolated hub's
     # workers always do (the main process then serves from the bus too, without calling them).
     nfront = int(cfg.serving.frontends)
-    if nfront < 0:
-        nfront = max(1, len(devices if devices is not None else (cfg.gpu.devices or _gpu_count())))
-    use_bus = nfront > 0 or cfg.gpu.isolation == "process" or cfg.serving.bus
+    ngpu = len(devices if devices is not None else (cfg.gpu.devices or _gpu_count()))
+    if nfront == -2:  # auto: serving processes on multi-GPU nodes
+        nfront = ngpu if ngpu > 1 else 0
+    elif nfront < 0:
+        nfront = max(1, ngpu)
+    # main-process serving through the native endpoint: it reads the frame bus
+    native_main = nfront == 0 and bool(cfg.serving.native)
+    use_bus = nfront > 0 or cfg.gpu.isolation == "process" or cfg.serving.bus or native_main
     if use_bus and not cfg.bus_tag:
         cfg.bus_tag = new_bus_tag()
     frontends, control = None, None
@@ -100,7 +108,10 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
             gport = _free_port(host)
         control = f"127.0.0.1:{_free_port('127.0.0.1')}"
         frontends = FrontendPool(nfront, cfg.bus_tag, f"{host}:{gport}", control, int(cfg.serving.threads),
-                                 stats_path=os.path.join(cfg.data_dir, f"serving-{cfg.bus_tag}"))
+                                 stats_path=os.path.join(cfg.data_dir, f"serving-{cfg.bus_tag}"),
+                                 native=bool(cfg.serving.native), io_threads=int(cfg.serving.io_threads))
+    elif native_main:
+        control = f"127.0.0.1:{_free_port('127.0.0.1')}"  # grpcio: the non-frame methods
     storage = Storage(os.path.join(cfg.data_dir, "registry.db"))
     if cfg.gpu.isolation == "process":
         from ..engine.isolated import ProcessHub
@@ -116,8 +127,18 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
     queue.start_consuming(consumer, cfg.annotation.unacked_limit, cfg.annotation.poll_duration_ms,
                           cfg.annotation.max_batch_size)
     image = ImageService(pm, settings, edge, queue, cfg.api.endpoint, bus=BusFrames(cfg.bus_tag) if use_bus else None)
-    # with serving processes this server is their control port (non-frame RPCs); else public
-    gsrv = serve(image, control if frontends is not None else f"{host}:{gport}", workers=int(cfg.serving.threads))
+    # with serving processes / the native endpoint this server is their control port (non-frame
+    # RPCs); else public
+    gsrv = serve(image, control if control is not None else f"{host}:{gport}", workers=int(cfg.serving.threads))
+    native_server = None
+    if native_main:
+        from .._native import native as _n
+        from .frontend import NativeForwarder
+
+        fwd = NativeForwarder(control)
+        native_server = _n.RpcServer(host if host else "0.0.0.0", int(gport or 0), cfg.bus_tag,
+                                     io_threads=int(cfg.serving.io_threads), wait_threads=int(cfg.serving.threads),
+                                     handler=fwd, reuseport=False)  # (holds fwd: the control channel)
     cron = start_cron_jobs(cfg)
     metrics = Metrics(hub, image, frontends)
     rest_server = rest_thread = None
@@ -137,8 +158,10 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
         rest_thread = threading.Thread(target=rest_server.run, kwargs={"sockets": [sock]},
                                        daemon=True, name="vep-rest")
         rest_thread.start()
+    public = gport if frontends is not None else (native_server.port if native_server is not None else 0)
     happ = HubApp(cfg, storage, hub, pm, settings, edge, queue, consumer, image, gsrv,
-                  rest_server, rest_thread, cron, metrics, frontends, gport if frontends is not None else 0)
+                  rest_server, rest_thread, cron, metrics, frontends, public, native_server)
+    metrics.native = native_server
     happ._rest_port = rport  # type: ignore[attr-defined]
     if float(cfg.gpu.consumer_rate_hz) > 0 and int(cfg.gpu.letterbox_size) > 0:
         from ..engine.consumer import ConsumerLoop
@@ -149,8 +172,8 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
         restored = pm.restore()
         if restored:
             log.info("restored %d cameras from the registry", len(restored))
-    log.info("vep ready: REST :%s gRPC :%s devices=%s serving processes=%d", rport, happ.grpc_port, hub.devices,
-             nfront)
+    log.info("vep ready: REST :%s gRPC :%s devices=%s serving processes=%d native=%s", rport, happ.grpc_port,
+             hub.devices, nfront, bool(cfg.serving.native))
     return happ
 
 

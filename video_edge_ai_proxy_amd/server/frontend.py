@@ -90,9 +90,68 @@ def make_forwarding_handler(svc, control: str):
     return grpc.method_handlers_generic_handler(SERVICE.full_name, handlers), chan
 
 
-def run_frontend(tag: str, listen: str, control: str, threads: int) -> int:
+class NativeForwarder:
+    """The native endpoint's callback for the non-frame methods: forwards the request bytes to the
+    main process's grpcio server (``control``) and returns (status, message, [responses])."""
+
+    def __init__(self, control: str):
+        import grpc
+
+        from ..proto import SERVICE
+        from .grpc_server import FRAME_CHANNEL_OPTS
+
+        self.grpc = grpc
+        self.chan = grpc.insecure_channel(control, options=FRAME_CHANNEL_OPTS)
+        self.calls = {m: (self.chan.unary_unary(SERVICE.path(m)) if k == "unary_unary"
+                          else self.chan.unary_stream(SERVICE.path(m))) for m, k in FORWARDED.items()}
+
+    def __call__(self, method: str, req: bytes, peer: str):
+        call = self.calls.get(method)
+        if call is None:
+            return 12, f"unknown method {method}", []
+        try:
+            if FORWARDED[method] == "unary_unary":
+                return 0, "", [call(req, timeout=30)]
+            return 0, "", list(call(req, timeout=30))
+        except self.grpc.RpcError as e:
+            return e.code().value[0], e.details() or "", []
+
+    def close(self):
+        self.chan.close()
+
+
+def run_frontend(tag: str, listen: str, control: str, threads: int, native: bool = False, io_threads: int = 2) -> int:
     from .grpc_server import BusFrames, ImageService, serve
 
+    if native:  # C++ HTTP/2 endpoint: frames from the bus without Python; the rest forwarded
+        from .._native import native as _n
+
+        host, port = listen.rsplit(":", 1)
+        fwd = NativeForwarder(control)
+        nsrv = _n.RpcServer(host, int(port), tag, io_threads=io_threads, wait_threads=threads, handler=fwd,
+                            reuseport=True)
+        print(f"ready {nsrv.port}", flush=True)
+        stats_path = os.environ.get("VEP_FRONTEND_STATS")
+
+        def report_native():
+            while True:
+                time.sleep(1.0)
+                if stats_path:
+                    try:
+                        with open(f"{stats_path}.{os.getpid()}.tmp", "w") as f:
+                            json.dump({"pid": os.getpid(), "frames_served": nsrv.stats()["frames_served"]}, f)
+                        os.replace(f"{stats_path}.{os.getpid()}.tmp", f"{stats_path}.{os.getpid()}")
+                    except OSError:
+                        pass
+
+        threading.Thread(target=report_native, daemon=True).start()
+        try:
+            sys.stdin.read()
+        except Exception:  # noqa: BLE001
+            pass
+        nsrv.stop()
+        fwd.close()
+        return 0
     svc = ImageService(None, bus=BusFrames(tag))
     handler, chan = make_forwarding_handler(svc, control)
     server = serve(svc, listen, workers=threads, reuseport=True, handler=handler, tune_malloc=True)
@@ -200,8 +259,10 @@ class FrontendPool:
     process touches a GPU) and stops it."""
 
     def __init__(self, n: int, tag: str, listen: str, control: str, threads: int = 256,
-                 start_timeout_s: float = 180.0, stats_path: Optional[str] = None):
-        args = ["--bus", tag, "--listen", listen, "--control", control, "--threads", str(threads)]
+                 start_timeout_s: float = 180.0, stats_path: Optional[str] = None, native: bool = False,
+                 io_threads: int = 2):
+        args = ["--bus", tag, "--listen", listen, "--control", control, "--threads", str(threads),
+                "--io-threads", str(io_threads)] + (["--native"] if native else [])
         env = _env()
         if stats_path:
             env["VEP_FRONTEND_STATS"] = stats_path
@@ -249,12 +310,15 @@ def main(argv=None) -> int:
     ap.add_argument("--control", required=True, help="main process's gRPC address (non-frame RPCs)")
     ap.add_argument("--threads", type=int, default=256)
     ap.add_argument("--supervise", type=int, default=0, help="start and supervise this many serving processes")
+    ap.add_argument("--native", action="store_true", help="VideoLatestImage on the native HTTP/2 endpoint")
+    ap.add_argument("--io-threads", type=int, default=2)
     a = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s frontend[%(process)d] %(name)s: %(message)s")
     if a.supervise > 0:
         return run_supervisor(a.supervise, ["--bus", a.bus, "--listen", a.listen, "--control", a.control,
-                                            "--threads", str(a.threads)])
-    return run_frontend(a.bus, a.listen, a.control, a.threads)
+                                            "--threads", str(a.threads), "--io-threads", str(a.io_threads)] +
+                              (["--native"] if a.native else []))
+    return run_frontend(a.bus, a.listen, a.control, a.threads, a.native, a.io_threads)
 
 
 if __name__ == "__main__":

@@ -295,8 +295,11 @@ def serve(svc: ImageService, address: str = "0.0.0.0:50001", workers: int = 64,
 class ImageClient:
     """Client stub (the reference used protoc-generated ``ImageStub``)."""
 
-    def __init__(self, target: str):
-        self.channel = grpc.insecure_channel(target, options=FRAME_CHANNEL_OPTS)
+    def __init__(self, target: str, own_connection: bool = False):
+        # own_connection: not grpc-core's process-wide subchannel pool (channels to one target
+        # share a TCP connection by default; the server keeps its cursors per connection)
+        opts = FRAME_CHANNEL_OPTS + ([("grpc.use_local_subchannel_pool", 1)] if own_connection else [])
+        self.channel = grpc.insecure_channel(target, options=opts)
         p = SERVICE.path
         self.VideoLatestImage = self.channel.stream_stream(
             p("VideoLatestImage"), request_serializer=pb.VideoFrameRequest.SerializeToString,

@@ -17,6 +17,7 @@ class HubCollector:
         self.svc = image_service
         self.frontends = frontends
         self.consumer = None  # engine.consumer.ConsumerLoop
+        self.native = None    # native.RpcServer (main-process native endpoint)
 
     def collect(self):
         labels = ["camera", "device"]
@@ -84,7 +85,19 @@ class HubCollector:
             served.add_metric(["main"], self.svc.frames_served)
             if self.frontends is not None:
                 served.add_metric(["serving"], self.frontends.frames_served())
+            nst = self.native.stats() if self.native is not None else None
+            if nst is not None:
+                served.add_metric(["native"], nst["frames_served"])
             yield served
+            if nst is not None:
+                g = GaugeMetricFamily("vep_native_frame_latency_ms", "native endpoint: request -> response queued",
+                                      labels=["quantile"])
+                g.add_metric(["0.5"], nst["p50_ms"])
+                g.add_metric(["0.99"], nst["p99_ms"])
+                yield g
+                c = GaugeMetricFamily("vep_native_connections", "native endpoint open connections")
+                c.add_metric([], nst["connections_open"])
+                yield c
             lat = list(self.svc.latencies_ms)
             if lat:
                 g = GaugeMetricFamily("vep_grpc_frame_latency_ms", "server-side frame latency",
@@ -100,6 +113,14 @@ class Metrics:
         self.registry = CollectorRegistry()
         self.collector = HubCollector(hub, image_service, frontends)
         self.registry.register(self.collector)
+
+    @property
+    def native(self):
+        return self.collector.native
+
+    @native.setter
+    def native(self, srv):
+        self.collector.native = srv
 
     @property
     def consumer(self):
