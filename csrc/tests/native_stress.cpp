@@ -41,6 +41,27 @@ using namespace vep;
     }                                                                         \
   } while (0)
 
+// Waits until done(); gives up only when progress() has not changed for stall_ms. A sanitizer
+// build runs many times slower than a release one, so no wall-clock budget: a live pipeline that
+// keeps making progress is waited for, a stuck one fails.
+template <class Done, class Progress, class Tick>
+static bool wait_progress(Done done, Progress progress, Tick tick, int stall_ms = 60000) {
+  unsigned long long last = progress();
+  auto since = std::chrono::steady_clock::now();
+  while (!done()) {
+    tick();
+    std::this_thread::sleep_for(std::chrono::milliseconds(20));
+    const unsigned long long p = progress();
+    if (p != last) {
+      last = p;
+      since = std::chrono::steady_clock::now();
+    } else if (std::chrono::steady_clock::now() - since > std::chrono::milliseconds(stall_ms)) {
+      return false;
+    }
+  }
+  return true;
+}
+
 static void live_worker_stress() {
   WorkerOptions o;
   o.device = -1;
@@ -162,10 +183,10 @@ static void rtsp_stress() {
   IngestSession sess(w, cam, ic, arch);
   sess.start();
   // the RTMP sender connects and sends on its own thread: also wait for its first messages
-  for (int i = 0; i < 500 && (w.camera(cam)->decoded.load() < 5 || sess.state().rtmp_messages < 3); ++i) {
-    w.camera(cam)->last_query_ms.store(now_ms());
-    std::this_thread::sleep_for(std::chrono::milliseconds(20));
-  }
+  CHECK(wait_progress(
+      [&] { return w.camera(cam)->decoded.load() >= 5 && sess.state().rtmp_messages >= 3; },
+      [&] { return w.camera(cam)->packets.load() + w.camera(cam)->decoded.load() + sess.state().rtmp_messages; },
+      [&] { w.camera(cam)->last_query_ms.store(now_ms()); }));
   sess.stop();
   w.flush();
   CHECK(w.camera(cam)->decoded.load() >= 5);
@@ -315,10 +336,10 @@ static void compressed_ingest_stress() {
   auto arch = std::make_shared<mux::Archiver>();
   IngestSession sess(w, cam, ic, arch);
   sess.start();
-  for (int i = 0; i < 500 && (w.camera(cam)->decoded.load() < 20 || sess.state().rtmp_messages < 3); ++i) {
-    w.camera(cam)->last_query_ms.store(now_ms());
-    std::this_thread::sleep_for(std::chrono::milliseconds(20));
-  }
+  CHECK(wait_progress(
+      [&] { return w.camera(cam)->decoded.load() >= 20 && sess.state().rtmp_messages >= 3; },
+      [&] { return w.camera(cam)->packets.load() + w.camera(cam)->decoded.load() + sess.state().rtmp_messages; },
+      [&] { w.camera(cam)->last_query_ms.store(now_ms()); }));
   sess.stop();
   w.flush();
   CHECK(w.camera(cam)->decoded.load() >= 20 && w.camera(cam)->errors.load() == 0);

@@ -181,9 +181,10 @@ def letterbox(y: torch.Tensor, uv: torch.Tensor, size: int = 640, width: int | N
 
 def nv12_to_bgr_reference(y: torch.Tensor, uv: torch.Tensor, width=None, height=None,
                           crop_left=0, crop_top=0) -> torch.Tensor:
-    """fp32 BT.601 limited-range conversion with nearest chroma (reference oracle).
-
-    Mirrors the fixed-point kernel exactly: each channel = floor((c + k*d + 2^15) / 2^16)."""
+    """Bit-exact oracle of the conversion kernel's integer arithmetic (BT.601 limited range,
+    nearest chroma): each channel = floor((c + k*d + 2^15) / 2^16) with the kernel's 16.16
+    coefficients. It shares the kernel's constants, so it pins the implementation, not the colour
+    science: ``nv12_to_bgr_bt601_float`` is the independent check (±1 LSB)."""
     H, W = y.shape
     width = W - crop_left if width is None else width
     height = H - crop_top if height is None else height
@@ -198,6 +199,30 @@ def nv12_to_bgr_reference(y: torch.Tensor, uv: torch.Tensor, width=None, height=
     g = torch.div(c - 25675 * d - 53279 * e, 65536, rounding_mode="floor")
     b = torch.div(c + 132201 * d, 65536, rounding_mode="floor")
     return torch.stack([b, g, r], dim=-1).clamp(0, 255).to(torch.uint8)
+
+
+def nv12_to_bgr_bt601_float(y: torch.Tensor, uv: torch.Tensor, width=None, height=None,
+                            crop_left=0, crop_top=0) -> torch.Tensor:
+    """Independent float64 BT.601 limited-range YCbCr -> BGR (what swscale's default converts,
+    read_image.py:94 ``to_ndarray('bgr24')``), derived from the standard's definitions rather than
+    from any fixed-point constants: Kr = 0.299, Kb = 0.114, luma scaled by 255/219 from
+    [16, 235], chroma by 255/224 around 128; round to nearest, clip to [0, 255]. Nearest chroma
+    sample (4:2:0, the sample at or left of / above the luma position)."""
+    H, W = y.shape
+    width = W - crop_left if width is None else width
+    height = H - crop_top if height is None else height
+    kr, kb = 0.299, 0.114
+    kg = 1.0 - kr - kb
+    Y = (y[crop_top:crop_top + height, crop_left:crop_left + width].to(torch.float64) - 16.0) * (255.0 / 219.0)
+    xs = torch.arange(crop_left, crop_left + width, device=y.device) // 2 * 2
+    ys = torch.arange(crop_top, crop_top + height, device=y.device) // 2
+    pb = (uv[ys][:, xs].to(torch.float64) - 128.0) * (255.0 / 224.0)
+    pr = (uv[ys][:, xs + 1].to(torch.float64) - 128.0) * (255.0 / 224.0)
+    r = Y + 2.0 * (1.0 - kr) * pr
+    b = Y + 2.0 * (1.0 - kb) * pb
+    g = Y - (2.0 * (1.0 - kb) * kb / kg) * pb - (2.0 * (1.0 - kr) * kr / kg) * pr
+    bgr = torch.stack([b, g, r], dim=-1)
+    return torch.floor(bgr + 0.5).clamp(0, 255).to(torch.uint8)
 
 
 def letterbox_reference(bgr: torch.Tensor, size: int = 640, pad_value: int = 114,
