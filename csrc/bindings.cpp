@@ -1095,6 +1095,9 @@ PYBIND11_MODULE(_vep, m) {
     return std::make_pair(parse_us, scan_us);
   }, py::arg("au"), py::arg("iters") = 100, py::arg("prime") = nullptr);
   m.def("rocdecode_available", [] { return gpu::rocdecode_available(); });
+  m.def("cabac_bins_decoded", [] { return cabac::bins_decoded().load(); },
+        "CABAC bins decoded by this process so far (H.264 and H.265 slices, counted as each ends)");
+  m.def("tsc_now", [] { return u64(__builtin_ia32_rdtsc()); }, "the x86 time-stamp counter");
   m.def("hostprof_start", &hostprof::start, py::arg("interval_us") = 1000,
         "start sampling host CPU time (SIGPROF, every thread of the process)");
   m.def("hostprof_stop", &hostprof::stop, py::arg("path"), "stop sampling; write 'count object offset symbol' lines");

@@ -1117,7 +1117,10 @@ void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, c
       if (sh.type() != h264::kI && L.read_skip_flag(mb)) L.skip_mb(mb, false);
       else L.coded_mb(mb, sh.type() == h264::kI);
       ++mb;
-      if (bins.end_of_slice(false)) break;
+      if (bins.end_of_slice(false)) {
+        cabac::bins_decoded().fetch_add(dec.bins(), std::memory_order_relaxed);
+        break;
+      }
       VEP_CHECK(dec.bitpos() <= n * 8 + 16, "slice data overrun");
     }
     return;

@@ -8,6 +8,7 @@
 // (python/read_image.py:87 `p.decode()`).
 #pragma once
 
+#include <atomic>
 #include <cstring>
 
 #include "common.h"
@@ -111,6 +112,7 @@ class Decoder {
     offset_ = bits(9);
   }
   VEP_CABAC_INLINE u32 decision(Ctx& c) {
+    ++nbins_;
     const u32 s = c.s;
     // (range & 0xC0) * 2 + (state << 1 | mps): one mask on the range -> LPS dependency chain
     const u32 lps = kRangeLpsFlat.v[((range_ & 0xC0u) << 1) + s];
@@ -125,12 +127,14 @@ class Decoder {
   // §9.3.3.2.2.3. After a 1 (pcm_flag / end_of_slice_flag) the bit position is exactly the end
   // of the encoder's flush (the flush's final 1 bit included).
   u32 terminate() {
+    ++nbins_;
     range_ -= 2;
     if (offset_ >= range_) return 1;
     renorm();
     return 0;
   }
   VEP_CABAC_INLINE u32 bypass() {
+    ++nbins_;
     offset_ = (offset_ << 1) | bits(1);
     if (offset_ >= range_) {
       offset_ -= range_;
@@ -139,6 +143,7 @@ class Decoder {
     return 0;
   }
   size_t bitpos() const { return byte_ * 8 - size_t(cbits_); }
+  u64 bins() const { return nbins_; }  // bins decoded (decision + bypass + terminate)
   size_t aligned_bytepos() const { return (bitpos() + 7) >> 3; }
  private:
   VEP_CABAC_INLINE void renorm() {  // range_ in [2, 510]: shift it back to >= 256 (0 when it already is)
@@ -186,7 +191,15 @@ class Decoder {
   u64 cache_ = 0;
   int cbits_ = 0;
   u32 range_ = 510, offset_ = 0;
+  u64 nbins_ = 0;  // (a register in the hot loops' local copies: off the range / offset chain)
 };
+
+// Process-wide count of bins decoded (slices add their decoder's count when they end): the parse
+// benchmarks' bins per picture and cycles per bin.
+inline std::atomic<u64>& bins_decoded() {
+  static std::atomic<u64> n{0};
+  return n;
+}
 
 // Arithmetic encoder appending to a byte-aligned RBSP buffer (§9.3.5).
 class Encoder {

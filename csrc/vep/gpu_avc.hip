@@ -831,7 +831,9 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
 struct DbkWave {
   AvcDbkInfo info;
   u8 y[20 * 20];      // rows -4..15, cols -4..15 of the MB (top-left corner unused)
-  u8 c[2][10 * 10];   // rows -2..7, cols -2..7 per chroma component
+  // rows -2..7 per chroma component, kDbkCs bytes each: 2 pad bytes, then cols -2..7, so that a
+  // row's words hold (pad, pad, -2, -1) (0..3) (4..7) like a luma row's edges' p / q words
+  u8 c[2][10 * 12];
   u8 carry[16 * 4];   // previous MB's filtered luma columns 12..15
   u8 ccarry[2][8 * 2];
 };
@@ -1046,7 +1048,7 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     if (bs[e] && dir == 0 && packed) {  // vertical edge: packed LDS accesses
-      u8* q0p = !ch ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.c[c][(2 + k) * 10 + 2 + 2 * e];
+      u8* q0p = !ch ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.c[c][(2 + k) * 12 + 4 + 2 * e];
       filter_vert_any(q0p, bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0, ch);
     } else if (bs[e]) {
       u8* sp;
@@ -1055,8 +1057,8 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed
         sp = dir == 0 ? &L.y[(4 + l) * 20 + 4 + 4 * e] : &L.y[(4 + 4 * e) * 20 + 4 + l];
         step = dir == 0 ? 1 : 20;
       } else {
-        sp = dir == 0 ? &L.c[c][(2 + k) * 10 + 2 + 2 * e] : &L.c[c][(2 + 2 * e) * 10 + 2 + k];
-        step = dir == 0 ? 1 : 10;
+        sp = dir == 0 ? &L.c[c][(2 + k) * 12 + 4 + 2 * e] : &L.c[c][(2 + 2 * e) * 12 + 4 + k];
+        step = dir == 0 ? 1 : 12;
       }
       filter_line_any(sp, step, bs[e], al[e], be[e], bs[e] < 4 ? tc[e] : 0, ch);
     }
@@ -1068,6 +1070,67 @@ __device__ inline void dbk_dir(DbkWave& L, bool any, int l, int dir, bool packed
     if (sync_each) wave_sync();
   }
   if (!sync_each) wave_sync();
+}
+
+// One direction of an MB's edges with each lane's line in VGPRs (VEP_DBK_REGS, the default): a
+// luma lane (0-15) holds its row (vertical edges) / column (horizontal edges) as 20 samples, 4 of
+// the neighbour then the MB's 16, in five words; a chroma lane (16-31) holds 10 samples of its
+// component (2 + 8) in the same five-word shape (pad, pad, -2, -1 | 0..3 | 4..7), so chroma edges
+// 0 / 2 fall on the word boundaries 0 / 1 exactly like luma edges 0 / 1 and one filter body serves
+// every lane. The line comes in with one LDS round trip (words for rows, bytes for columns), the
+// four (chroma: two) dependent edge filters run in registers, and it goes back in one: round 4's
+// form did an LDS round trip per edge (the wavefront's per-MB critical path).
+__device__ inline void dbk_dir_regs(DbkWave& L, bool any, int l, int dir) {
+  const bool ch = l >= 16;
+  const int c = (l - 16) >> 3, k = (l - 16) & 7;
+  int bs[4], al[4], be[4], tc[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ee = ch ? 2 * e : e;  // the MB edge register edge e stands for
+    bs[e] = any && (!ch || e < 2) ? bs_of(L.info, dir, ee, ch ? k >> 1 : l >> 2) : 0;
+    const int pi = (ee > 0 ? 2 : dir) + (ch ? 3 + 3 * c : 0);
+    al[e] = L.info.alpha[pi];
+    be[e] = L.info.beta[pi];
+    tc[e] = L.info.tc0[pi][bs[e] > 0 && bs[e] < 4 ? bs[e] - 1 : 0];
+  }
+  u32 w[5] = {0, 0, 0, 0, 0};
+  // rows: the line's words are the tile row's words; columns: sample i of the line is tile row
+  // i - 4 (luma rows -4..15, chroma rows -2..7 at line positions 2..11)
+  u8* row = !ch ? &L.y[(4 + l) * 20] : &L.c[c][(2 + k) * 12];
+  u8* col = !ch ? &L.y[4 * 20 + 4 + l] : &L.c[c][2 * 12 + 4 + k];  // (row 0 of the column)
+  const int stride = ch ? 12 : 20, lo = ch ? 2 : 0, hi = ch ? 12 : 20, nw = ch ? 3 : 5;
+  if (dir == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (i < nw) w[i] = ld4(row + 4 * i);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 20; ++i)
+      if (i >= lo && i < hi) w[i >> 2] |= u32(col[(i - 4) * stride]) << (8 * (i & 3));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (!bs[e]) continue;
+    const u32 P = w[e], Q = w[e + 1];
+    int np0, np1, np2, nq0, nq1, nq2;
+    if (!filter_vals(int(P >> 24), int((P >> 16) & 255), int((P >> 8) & 255), int(P & 255), int(Q & 255),
+                     int((Q >> 8) & 255), int((Q >> 16) & 255), int(Q >> 24), bs[e], al[e], be[e],
+                     bs[e] < 4 ? tc[e] : 0, ch, np0, np1, np2, nq0, nq1, nq2))
+      continue;
+    w[e] = (P & 255u) | u32(np2) << 8 | u32(np1) << 16 | u32(np0) << 24;
+    w[e + 1] = u32(nq0) | u32(nq1) << 8 | u32(nq2) << 16 | (Q & 0xFF000000u);
+  }
+  // (chroma: filter_vals leaves p1 / q1 / p2 / q2 as they were, so the repacked words are exact)
+  if (dir == 0) {
+#pragma unroll
+    for (int i = 0; i < 5; ++i)
+      if (i < nw) st4(row + 4 * i, w[i]);
+  } else {
+#pragma unroll
+    for (int i = 1; i < 20; ++i)  // (sample 0, luma row -4, is never written by a filter)
+      if (i >= lo && i < hi) col[(i - 4) * stride] = u8(w[i >> 2] >> (8 * (i & 3)));
+  }
+  wave_sync();
 }
 
 struct DbkRegs {  // one MB's inputs as loaded from global memory (per lane of a half-wave)
@@ -1150,15 +1213,15 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
       {
         const int cyr = l >> 2, cb = (l & 3) * 2;
         for (int q = 0; q < 2; ++q) {
-          L.c[0][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q));
-          L.c[1][(cyr + 2) * 10 + 2 + cb + q] = u8(cur.c >> (16 * q + 8));
+          L.c[0][(cyr + 2) * 12 + 4 + cb + q] = u8(cur.c >> (16 * q));
+          L.c[1][(cyr + 2) * 12 + 4 + cb + q] = u8(cur.c >> (16 * q + 8));
         }
       }
       if (l < 8 && x > 0) {
-        L.c[0][(l + 2) * 10 + 0] = L.ccarry[0][l * 2];
-        L.c[1][(l + 2) * 10 + 0] = L.ccarry[1][l * 2];
-        L.c[0][(l + 2) * 10 + 1] = L.ccarry[0][l * 2 + 1];
-        L.c[1][(l + 2) * 10 + 1] = L.ccarry[1][l * 2 + 1];
+        L.c[0][(l + 2) * 12 + 2] = L.ccarry[0][l * 2];
+        L.c[1][(l + 2) * 12 + 2] = L.ccarry[1][l * 2];
+        L.c[0][(l + 2) * 12 + 3] = L.ccarry[0][l * 2 + 1];
+        L.c[1][(l + 2) * 12 + 3] = L.ccarry[1][l * 2 + 1];
       }
     }
     wave_sync();
@@ -1167,7 +1230,10 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     const bool wany = __ballot(any) != 0;
     // ---- vertical edges (per half: luma lanes 0-15, chroma 16-31): they touch only this MB's
     // rows, so they need nothing from the row above
-    if (wany) dbk_dir(L, any, l, 0, (packed & 1) != 0, (packed & 2) != 0);
+    if (wany) {
+      if (packed & 4) dbk_dir_regs(L, any, l, 0);
+      else dbk_dir(L, any, l, 0, (packed & 1) != 0, (packed & 2) != 0);
+    }
     // ---- the previous MB's right columns are final now (this MB's left edge was the last
     // filter to touch them): complete its exchange entry for the row below, then publish
     // "vertical edges of MB x done" (the row below may filter MB x - 1's top edge)
@@ -1180,8 +1246,8 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
         fi = k * 4 + 3;
       } else if (l >= 28 && l < 30) {
         const int k = l - 28, cr = 8 + k;
-        fw = u32(L.c[0][cr * 10]) | u32(L.c[1][cr * 10]) << 8 | u32(L.c[0][cr * 10 + 1]) << 16 |
-             u32(L.c[1][cr * 10 + 1]) << 24;
+        fw = u32(L.c[0][cr * 12 + 2]) | u32(L.c[1][cr * 12 + 2]) << 8 | u32(L.c[0][cr * 12 + 3]) << 16 |
+             u32(L.c[1][cr * 12 + 3]) << 24;
         fi = 16 + k * 4 + 3;
       }
       if (fi >= 0) {
@@ -1223,15 +1289,18 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
         const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
         const u32 v = top_g ? gv : ld4(&xch(row - 1, x).c[k * 4]);
         for (int q = 0; q < 2; ++q) {
-          L.c[0][tr * 10 + 2 + cb + q] = u8(v >> (16 * q));
-          L.c[1][tr * 10 + 2 + cb + q] = u8(v >> (16 * q + 8));
+          L.c[0][tr * 12 + 4 + cb + q] = u8(v >> (16 * q));
+          L.c[1][tr * 12 + 4 + cb + q] = u8(v >> (16 * q + 8));
         }
       }
     }
     wave_sync();
     const u64 t5 = d.prof ? clock64() : 0;
     // ---- horizontal edges
-    if (wany) dbk_dir(L, any, l, 1, false, (packed & 2) != 0);
+    if (wany) {
+      if (packed & 4) dbk_dir_regs(L, any, l, 1);
+      else dbk_dir(L, any, l, 1, false, (packed & 2) != 0);
+    }
     const u64 t6 = d.prof ? clock64() : 0;
     if (act) {
       // ---- write back: MB rows 0..11 (0..15 for the last row) if filtered, the left
@@ -1247,7 +1316,7 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
         if (cyr < 6 || last) {
           u32 cw = 0;
           for (int q = 0; q < 2; ++q)
-            cw |= (u32(L.c[0][(cyr + 2) * 10 + 2 + cb + q]) | u32(L.c[1][(cyr + 2) * 10 + 2 + cb + q]) << 8)
+            cw |= (u32(L.c[0][(cyr + 2) * 12 + 4 + cb + q]) | u32(L.c[1][(cyr + 2) * 12 + 4 + cb + q]) << 8)
                   << (16 * q);
           gst4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
         }
@@ -1261,15 +1330,15 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
       }
       if (l < 8) {
         if (left && (l < 6 || last)) {
-          const u32 cw = u32(L.c[0][(l + 2) * 10]) | u32(L.c[1][(l + 2) * 10]) << 8 |
-                         u32(L.c[0][(l + 2) * 10 + 1]) << 16 | u32(L.c[1][(l + 2) * 10 + 1]) << 24;
+          const u32 cw = u32(L.c[0][(l + 2) * 12 + 2]) | u32(L.c[1][(l + 2) * 12 + 2]) << 8 |
+                         u32(L.c[0][(l + 2) * 12 + 3]) << 16 | u32(L.c[1][(l + 2) * 12 + 3]) << 24;
           gst4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
         }
       } else if (l < 16 && row > 0) {
         const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
         u32 cw = 0;
         for (int q = 0; q < 2; ++q)
-          cw |= (u32(L.c[0][tr * 10 + 2 + cb + q]) | u32(L.c[1][tr * 10 + 2 + cb + q]) << 8) << (16 * q);
+          cw |= (u32(L.c[0][tr * 12 + 4 + cb + q]) | u32(L.c[1][tr * 12 + 4 + cb + q]) << 8) << (16 * q);
         gst4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
       }
       // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (the last
@@ -1281,8 +1350,8 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
           w = ld4(&L.y[(16 + (l >> 2)) * 20 + 4 + (l & 3) * 4]);
         } else {
           const int k = l - 16, cr = 8 + (k >> 2), cb = (k & 3) * 2;
-          w = u32(L.c[0][cr * 10 + 2 + cb]) | u32(L.c[1][cr * 10 + 2 + cb]) << 8 |
-              u32(L.c[0][cr * 10 + 3 + cb]) << 16 | u32(L.c[1][cr * 10 + 3 + cb]) << 24;
+          w = u32(L.c[0][cr * 12 + 4 + cb]) | u32(L.c[1][cr * 12 + 4 + cb]) << 8 |
+              u32(L.c[0][cr * 12 + 5 + cb]) << 16 | u32(L.c[1][cr * 12 + 5 + cb]) << 24;
         }
         if (xout)
           xg_put(xg_out + size_t(x) * kAvcXgWords + l, w, (l & 3) == 3 && x + 1 < W ? kXgPartial : kXgFinal);
@@ -1294,8 +1363,8 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
         st4(&L.carry[l * 4], ld4(&L.y[(l + 4) * 20 + 16]));
       } else {
         const int c = (l - 16) >> 3, k = (l - 16) & 7;
-        L.ccarry[c][k * 2] = L.c[c][(k + 2) * 10 + 8];
-        L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 10 + 9];
+        L.ccarry[c][k * 2] = L.c[c][(k + 2) * 12 + 10];
+        L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 12 + 11];
       }
     }
     if (x == W - 1) {  // the row's exchange is complete (no MB to its right)

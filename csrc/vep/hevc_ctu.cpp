@@ -1655,6 +1655,7 @@ int decode_slice_data(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_
     }
   }
   if (shard) shard->ctus = ctus;
+  cabac::bins_decoded().fetch_add(dec.bins(), std::memory_order_relaxed);
   return ctus;
 }
 
@@ -1707,6 +1708,7 @@ int decode_substream(PicCtx& pc, int slice_idx, const u8* data, size_t n, size_t
     }
   }
   if (shard) shard->ctus = ctus;
+  cabac::bins_decoded().fetch_add(dec.bins(), std::memory_order_relaxed);
   return ctus;
 }
 

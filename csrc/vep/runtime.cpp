@@ -525,7 +525,8 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     }
     const char* dp = std::getenv("VEP_DBK_PACKED");
     const char* ds = std::getenv("VEP_DBK_SYNC");  // 1: a wave sync after every edge (A/B)
-    dbk_packed_ = ((dp && dp[0] == '0') ? 0 : 1) | ((ds && ds[0] == '1') ? 2 : 0);
+    const char* dg = std::getenv("VEP_DBK_REGS");  // 0: round 4's per-edge LDS lines (A/B)
+    dbk_packed_ = ((dp && dp[0] == '0') ? 0 : 1) | ((ds && ds[0] == '1') ? 2 : 0) | ((dg && dg[0] == '0') ? 0 : 4);
     const char* dr = std::getenv("VEP_DIRECT_READS");
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
