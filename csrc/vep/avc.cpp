@@ -1832,8 +1832,32 @@ std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, in
   return col;
 }
 
-void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
-                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure) {
+namespace {
+template <class P>
+const P* yplane(const HostSurface& s) {
+  if constexpr (sizeof(P) == 1) return s.y.data();
+  else return s.y16.data();
+}
+template <class P>
+const P* uvplane(const HostSurface& s) {
+  if constexpr (sizeof(P) == 1) return s.uv.data();
+  else return s.uv16.data();
+}
+template <class P>
+P* yplane(HostSurface& s) {
+  if constexpr (sizeof(P) == 1) return s.y.data();
+  else return s.y16.data();
+}
+template <class P>
+P* uvplane(HostSurface& s) {
+  if constexpr (sizeof(P) == 1) return s.uv.data();
+  else return s.uv16.data();
+}
+
+// (P: u8 surfaces, or u16 at bit depth bd, High 10)
+template <class P>
+void predict_inter_t(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
+                     const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure, int bd) {
   // field pictures: slot parity = field parity; a vector into the opposite-parity field is offset
   // by a quarter chroma sample vertically (Table 8-10: 2 * (bottom_cur - bottom_ref) eighths)
   auto cy_off = [&](int slot) { return structure ? 2 * ((structure == 2) - (slot & 1)) : 0; };
@@ -1844,12 +1868,12 @@ void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const 
       const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
       int p0 = 0, p1 = 0;
       if (s0 != 0xFF)
-        p0 = luma_qpel(slots[size_t(s0)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * r] >> 2),
-                       my * 16 + y + (mv0[2 * r + 1] >> 2), mv0[2 * r] & 3, mv0[2 * r + 1] & 3);
+        p0 = luma_qpel(yplane<P>(slots[size_t(s0)]), pitch, wpx, hpx, mx * 16 + x + (mv0[2 * r] >> 2),
+                       my * 16 + y + (mv0[2 * r + 1] >> 2), mv0[2 * r] & 3, mv0[2 * r + 1] & 3, bd);
       if (s1 != 0xFF)
-        p1 = luma_qpel(slots[size_t(s1)].y.data(), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * r] >> 2),
-                       my * 16 + y + (mv1[2 * r + 1] >> 2), mv1[2 * r] & 3, mv1[2 * r + 1] & 3);
-      py[y * 16 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 0);
+        p1 = luma_qpel(yplane<P>(slots[size_t(s1)]), pitch, wpx, hpx, mx * 16 + x + (mv1[2 * r] >> 2),
+                       my * 16 + y + (mv1[2 * r + 1] >> 2), mv1[2 * r] & 3, mv1[2 * r + 1] & 3, bd);
+      py[y * 16 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 0, bd);
     }
   for (int c = 0; c < 2; ++c)
     for (int y = 0; y < 8; ++y)
@@ -1859,16 +1883,23 @@ void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const 
         int p0 = 0, p1 = 0;
         if (s0 != 0xFF) {
           const int vy = mv0[2 * r + 1] + cy_off(s0);
-          p0 = chroma_epel(slots[size_t(s0)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
+          p0 = chroma_epel(uvplane<P>(slots[size_t(s0)]), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
                            my * 8 + y + (vy >> 3), mv0[2 * r] & 7, vy & 7);
         }
         if (s1 != 0xFF) {
           const int vy = mv1[2 * r + 1] + cy_off(s1);
-          p1 = chroma_epel(slots[size_t(s1)].uv.data(), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
+          p1 = chroma_epel(uvplane<P>(slots[size_t(s1)]), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
                            my * 8 + y + (vy >> 3), mv1[2 * r] & 7, vy & 7);
         }
-        pc[c][y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c);
+        pc[c][y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c, bd);
       }
+}
+}  // namespace
+
+void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
+                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure) {
+  if (slots[0].wide()) predict_inter_t<u16>(slots, m, mv0, mv1, wp, mx, my, py, pc, structure, slots[0].bd);
+  else predict_inter_t<u8>(slots, m, mv0, mv1, wp, mx, my, py, pc, structure, 8);
 }
 
 void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& res) {
@@ -2138,19 +2169,21 @@ void luma_residual(const i16* dense, const MbRec& m, int* out) {
   }
 }
 
+template <class P>
 struct Recon {
   const Picture& pic;
   std::vector<HostSurface>& slots;
   HostSurface& T;
-  int pitch, wpx, hpx;
+  int pitch, wpx, hpx, bd;
   i16 dense[kDenseCoefs];  // the current MB's coefficients (load())
 
   void load(const MbRec& m) {
     if (m.kind != kIPcm) expand_coefs(pic.coefs.data(), m, dense);
   }
 
-  u8& Y(int x, int y) { return T.y[size_t(y) * pitch + x]; }
-  u8& C(int x, int y, int c) { return T.uv[size_t(y) * pitch + 2 * x + c]; }
+  P& Y(int x, int y) { return yplane<P>(T)[size_t(y) * pitch + x]; }
+  P& C(int x, int y, int c) { return uvplane<P>(T)[size_t(y) * pitch + 2 * x + c]; }
+  P px(int v) const { return P(clip1(v, bd)); }
 
   void chroma_store(const MbRec& m, int mx, int my, int c, const int* pred /*8x8*/) {
     for (int b = 0; b < 4; ++b) {
@@ -2160,7 +2193,7 @@ struct Recon {
       const int bx = (b & 1) * 4, by = (b >> 1) * 4;
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j)
-          C(mx * 8 + bx + j, my * 8 + by + i, c) = u8(clip1(pred[(by + i) * 8 + bx + j] + res[i * 4 + j]));
+          C(mx * 8 + bx + j, my * 8 + by + i, c) = px(pred[(by + i) * 8 + bx + j] + res[i * 4 + j]);
     }
   }
 
@@ -2177,15 +2210,15 @@ struct Recon {
     const i16* mv1 = (m.flags & kMbL1) ? e[1] : nullptr;
     const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
     int py[256], pc[2][64], res[256];
-    predict_inter(slots, m, mv0, mv1, wp, mx, my, py, pc, pic.structure);
+    predict_inter_t<P>(slots, m, mv0, mv1, wp, mx, my, py, pc, pic.structure, bd);
     luma_residual(dense, m, res);
     for (int y = 0; y < 16; ++y)
-      for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = u8(clip1(py[y * 16 + x] + res[y * 16 + x]));
+      for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = px(py[y * 16 + x] + res[y * 16 + x]);
     for (int c = 0; c < 2; ++c) chroma_store(m, mx, my, c, pc[c]);
   }
 
-  void pcm(const MbRec& m, int mx, int my) {
-    const u8* s = reinterpret_cast<const u8*>(pic.coefs.data() + m.coef);
+  void pcm(const MbRec& m, int mx, int my) {  // (u8 surfaces: 384 sample bytes; u16: 384 samples)
+    const P* s = reinterpret_cast<const P*>(pic.coefs.data() + m.coef);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = s[y * 16 + x];
     for (int c = 0; c < 2; ++c)
@@ -2200,7 +2233,7 @@ struct Recon {
       const PredConst k = m.chroma_mode == 3 ? chroma_plane_const(n) : PredConst{0, 0, 0, 0};
       int cp[64];
       for (int y = 0; y < 8; ++y)
-        for (int x = 0; x < 8; ++x) cp[y * 8 + x] = chroma_pred(n, k, m.chroma_mode, x, y);
+        for (int x = 0; x < 8; ++x) cp[y * 8 + x] = chroma_pred(n, k, m.chroma_mode, x, y, bd);
       chroma_store(m, mx, my, c, cp);
     }
   }
@@ -2208,12 +2241,12 @@ struct Recon {
   void intra16(const MbRec& m, int mb, int mx, int my) {
     Intra16Nb n;
     intra16_neighbours(pic, mb, T, n);
-    const PredConst k = intra16x16_const(n, m.i16_mode);
+    const PredConst k = intra16x16_const(n, m.i16_mode, bd);
     int res[256];
     luma_residual(dense, m, res);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x)
-        Y(mx * 16 + x, my * 16 + y) = u8(clip1(intra16x16_pred(n, k, m.i16_mode, x, y) + res[y * 16 + x]));
+        Y(mx * 16 + x, my * 16 + y) = px(intra16x16_pred(n, k, m.i16_mode, x, y, bd) + res[y * 16 + x]);
   }
 
   void intra4(const MbRec& m, int mb, int mx, int my) {
@@ -2227,7 +2260,7 @@ struct Recon {
       if (d) idct4x4(d, res);
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j)
-          Y(mx * 16 + bx * 4 + j, my * 16 + by * 4 + i) = u8(clip1(intra4x4_pred(n, mode, j, i) + res[i * 4 + j]));
+          Y(mx * 16 + bx * 4 + j, my * 16 + by * 4 + i) = px(intra4x4_pred(n, mode, j, i, bd) + res[i * 4 + j]);
     }
   }
 
@@ -2241,7 +2274,7 @@ struct Recon {
       if ((m.luma_coded >> ((q & 1) * 2 + (q >> 1) * 8)) & 1) idct8x8(dense + 64 * q, res);
       const int x0 = mx * 16 + (q & 1) * 8, y0 = my * 16 + (q >> 1) * 8;
       for (int i = 0; i < 8; ++i)
-        for (int j = 0; j < 8; ++j) Y(x0 + j, y0 + i) = u8(clip1(intra8x8_pred(f, top, left, mode, j, i) + res[i * 8 + j]));
+        for (int j = 0; j < 8; ++j) Y(x0 + j, y0 + i) = px(intra8x8_pred(f, top, left, mode, j, i, bd) + res[i * 8 + j]);
     }
   }
 };
@@ -2262,7 +2295,7 @@ void intra8x8_neighbours(const Picture& pic, int mb, int q, const HostSurface& T
   has_left = bx > 0 || A;
   const bool has_tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
   const bool has_tr = by == 0 ? (bx == 0 ? B : Cm) : (bx == 0);  // block 2's top-right is block 1
-  auto P = [&](int x, int y) { return int(T.y[size_t(y) * pitch + x]); };
+  auto P = [&](int x, int y) { return T.wide() ? int(T.y16[size_t(y) * pitch + x]) : int(T.y[size_t(y) * pitch + x]); };
   int t[17], l[8];  // t[0] = p[-1,-1], t[1 + x] = p[x,-1]
   t[0] = has_tl ? P(x0 - 1, y0 - 1) : 128;
   for (int k = 0; k < 8; ++k) {
@@ -2281,7 +2314,7 @@ void intra4x4_neighbours(const Picture& pic, int mb, int idx, const HostSurface&
              Cm = intra_avail(pic, m, mx + 1, my - 1), D = intra_avail(pic, m, mx - 1, my - 1);
   const int r = blk_to_raster(idx), bx = r & 3, by = r >> 2;
   const int x0 = mx * 16 + bx * 4, y0 = my * 16 + by * 4;
-  auto P = [&](int x, int y) { return int(T.y[size_t(y) * pitch + x]); };
+  auto P = [&](int x, int y) { return T.wide() ? int(T.y16[size_t(y) * pitch + x]) : int(T.y[size_t(y) * pitch + x]); };
   n.has_top = by > 0 || B;
   n.has_left = bx > 0 || A;
   n.has_tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
@@ -2297,7 +2330,7 @@ void intra4x4_neighbours(const Picture& pic, int mb, int idx, const HostSurface&
 void intra16_neighbours(const Picture& pic, int mb, const HostSurface& T, Intra16Nb& n) {
   const MbRec& m = pic.mbs[size_t(mb)];
   const int mx = mb % pic.wmbs, my = mb / pic.wmbs, pitch = T.coded_w;
-  auto P = [&](int x, int y) { return int(T.y[size_t(y) * pitch + x]); };
+  auto P = [&](int x, int y) { return T.wide() ? int(T.y16[size_t(y) * pitch + x]) : int(T.y[size_t(y) * pitch + x]); };
   n.has_left = intra_avail(pic, m, mx - 1, my);
   n.has_top = intra_avail(pic, m, mx, my - 1);
   n.has_tl = intra_avail(pic, m, mx - 1, my - 1);
@@ -2311,7 +2344,9 @@ void intra16_neighbours(const Picture& pic, int mb, const HostSurface& T, Intra1
 void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, IntraChromaNb& n) {
   const MbRec& m = pic.mbs[size_t(mb)];
   const int mx = mb % pic.wmbs, my = mb / pic.wmbs, pitch = T.coded_w;
-  auto P = [&](int x, int y) { return int(T.uv[size_t(y) * pitch + 2 * x + c]); };
+  auto P = [&](int x, int y) {
+    return T.wide() ? int(T.uv16[size_t(y) * pitch + 2 * x + c]) : int(T.uv[size_t(y) * pitch + 2 * x + c]);
+  };
   n.has_left = intra_avail(pic, m, mx - 1, my);
   n.has_top = intra_avail(pic, m, mx, my - 1);
   n.has_tl = intra_avail(pic, m, mx - 1, my - 1);
@@ -2322,10 +2357,12 @@ void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, 
   }
 }
 
-void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots) {
+namespace {
+template <class P>
+void reconstruct_mb_t(const Picture& pic, int mb, std::vector<HostSurface>& slots) {
   HostSurface& T = slots[size_t(pic.target)];
   const int wpx = pic.wmbs * 16, hpx = pic.hmbs * 16;
-  Recon r{pic, slots, T, wpx, wpx, hpx, {}};
+  Recon<P> r{pic, slots, T, wpx, wpx, hpx, T.wide() ? T.bd : 8, {}};
   const MbRec& m = pic.mbs[size_t(mb)];
   r.load(m);
   const int mx = mb % pic.wmbs, my = mb / pic.wmbs;
@@ -2355,11 +2392,13 @@ void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& sl
   }
 }
 
-void cpu_deblock(const Picture& pic, HostSurface& T) {
+template <class P>
+void deblock_t(const Picture& pic, HostSurface& T) {
   static const i16 kZeroMv[64] = {};
-  const int W = pic.wmbs, pitch = T.coded_w;
-  u8* Yp = T.y.data();
-  u8* UV = T.uv.data();
+  const int W = pic.wmbs, pitch = T.coded_w, bd = T.wide() ? T.bd : 8;
+  const int qb = pic.qp_bias, qcb = pic.qpc_bias;
+  P* Yp = yplane<P>(T);
+  P* UV = uvplane<P>(T);
   auto mvs = [&](const MbRec& r) { return is_intra(r.kind) ? kZeroMv : &pic.mvs[size_t(r.mv)]; };
   for (int mb = 0; mb < pic.nmbs(); ++mb) {
     const MbRec& q = pic.mbs[size_t(mb)];
@@ -2374,9 +2413,9 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
         const MbRec& p = e > 0 ? q : pic.mbs[size_t(dir == 0 ? mb - 1 : mb - W)];
         const i16* mp = mvs(p);
         if ((e & 1) && (q.flags & kMbT8x8)) continue;  // no 4x4 edges inside 8x8 transform blocks
-        const EdgeParams ep = edge_params(p.qp, q.qp, q.alpha_off, q.beta_off);
-        const EdgeParams epcs[2] = {edge_params(p.qpc, q.qpc, q.alpha_off, q.beta_off),
-                                    edge_params(p.qpc2, q.qpc2, q.alpha_off, q.beta_off)};
+        const EdgeParams ep = edge_params(p.qp - qb, q.qp - qb, q.alpha_off, q.beta_off, bd);
+        const EdgeParams epcs[2] = {edge_params(p.qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off, bd),
+                                    edge_params(p.qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off, bd)};
         int bs[16];
         for (int k = 0; k < 16; ++k) {
           const int bq = dir == 0 ? (k >> 2) * 4 + e : e * 4 + (k >> 2);
@@ -2385,8 +2424,8 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
         }
         for (int k = 0; k < 16; ++k) {
           if (!bs[k]) continue;
-          if (dir == 0) filter_line(Yp + size_t(my * 16 + k) * pitch + mx * 16 + 4 * e, 1, bs[k], ep, false);
-          else filter_line(Yp + size_t(my * 16 + 4 * e) * pitch + mx * 16 + k, long(pitch), bs[k], ep, false);
+          if (dir == 0) filter_line(Yp + size_t(my * 16 + k) * pitch + mx * 16 + 4 * e, 1, bs[k], ep, false, bd);
+          else filter_line(Yp + size_t(my * 16 + 4 * e) * pitch + mx * 16 + k, long(pitch), bs[k], ep, false, bd);
         }
         if (e & 1) continue;  // chroma edges at chroma sample 0 and 4 (luma edges 0 and 2)
         for (int c = 0; c < 2; ++c)
@@ -2395,13 +2434,24 @@ void cpu_deblock(const Picture& pic, HostSurface& T) {
             const int b = bs[2 * k];
             if (!b) continue;
             if (dir == 0)
-              filter_line(UV + size_t(my * 8 + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, b, epc, true);
+              filter_line(UV + size_t(my * 8 + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, b, epc, true, bd);
             else
-              filter_line(UV + size_t(my * 8 + 2 * e) * pitch + (mx * 8 + k) * 2 + c, long(pitch), b, epc, true);
+              filter_line(UV + size_t(my * 8 + 2 * e) * pitch + (mx * 8 + k) * 2 + c, long(pitch), b, epc, true, bd);
           }
       }
     }
   }
+}
+}  // namespace
+
+void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots) {
+  if (slots[size_t(pic.target)].wide()) reconstruct_mb_t<u16>(pic, mb, slots);
+  else reconstruct_mb_t<u8>(pic, mb, slots);
+}
+
+void cpu_deblock(const Picture& pic, HostSurface& T) {
+  if (T.wide()) deblock_t<u16>(pic, T);
+  else deblock_t<u8>(pic, T);
 }
 
 void weave_fields(const HostSurface& top, const HostSurface& bottom, HostSurface& frame) {

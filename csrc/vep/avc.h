@@ -75,6 +75,10 @@ struct Picture {
   // 0 frame; 1 / 2 top / bottom field picture. Field pictures address field slots (half a frame
   // each, parity = slot & 1: frame slot s = field slots 2s, 2s + 1), wmbs x hmbs is the field.
   int structure = 0;
+  // Sample bit depth (High 10: 9 / 10; the surfaces then hold u16 samples) and the QP bias of the
+  // records: MbRec::qp = QPY + QpBdOffsetY, MbRec::qpc / qpc2 = QPC + QpBdOffsetC (QPY / QPC may
+  // be negative above 8 bits); the loop filter subtracts them.
+  int bd = 8, qp_bias = 0, qpc_bias = 0;
   bool second_field = false;  // completes a field pair (frame counters count these, not first fields)
   bool constrained_intra = false;
   int intra_mbs = 0;          // I4x4 / I8x8 / I16x16 MBs (need the wavefront pass)

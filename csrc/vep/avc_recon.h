@@ -107,16 +107,17 @@ static_assert(sizeof(WpEntry) == 32, "WpEntry layout");
 
 // Final prediction sample from the list-0 / list-1 predictions (§8.4.2.3.1 default, §8.4.2.3.2
 // weighted); c = component.
-VEP_HD int wp_sample(int p0, int p1, bool has0, bool has1, const WpEntry* w, int c) {
+// bd: sample bit depth (High 10: the offsets in WpEntry are already scaled by 1 << (bd - 8)).
+VEP_HD int wp_sample(int p0, int p1, bool has0, bool has1, const WpEntry* w, int c, int bd = 8) {
   if (!w) return has0 && has1 ? (p0 + p1 + 1) >> 1 : (has0 ? p0 : p1);
-  const int lwd = w->lwd[c];
+  const int lwd = w->lwd[c], mx = (1 << bd) - 1;
   if (has0 && has1) {
     const int v = ((p0 * w->w0[c] + p1 * w->w1[c] + (1 << lwd)) >> (lwd + 1)) + w->o[c];
-    return v < 0 ? 0 : (v > 255 ? 255 : v);
+    return v < 0 ? 0 : (v > mx ? mx : v);
   }
   const int p = has0 ? p0 : p1, ww = has0 ? w->w0[c] : w->w1[c];
   const int v = lwd >= 1 ? ((p * ww + (1 << (lwd - 1))) >> lwd) + w->o[c] : p * ww + w->o[c];
-  return v < 0 ? 0 : (v > 255 ? 255 : v);
+  return v < 0 ? 0 : (v > mx ? mx : v);
 }
 
 // ---- sparse coefficient records
@@ -206,6 +207,13 @@ VEP_HD int chroma_qp(int qpy, int offset) {
   q = q < 0 ? 0 : q > 51 ? 51 : q;
   return kChromaQp[q];
 }
+// High bit depth (§8.5.8): qPI = Clip3(-QpBdOffsetC, 51, QPY + offset); QPC = qPI below 30 (so
+// it may be negative), the table above it. (QP'C = QPC + QpBdOffsetC is the dequantisation QP.)
+VEP_HD int chroma_qp_bd(int qpy, int offset, int qpbd_c) {
+  int q = qpy + offset;
+  q = q < -qpbd_c ? -qpbd_c : q > 51 ? 51 : q;
+  return q < 0 ? q : kChromaQp[q];
+}
 
 // Zig-zag scan (frame macroblocks): scan index -> raster position in the 4x4 block.
 VEP_CONST static const u8 kZigzag4x4[16] = {0, 1, 4, 8, 5, 2, 3, 6, 9, 12, 13, 10, 7, 11, 14, 15};
@@ -232,7 +240,7 @@ VEP_CONST static const u8 kTc0[52][3] = {
     {10, 13, 20}, {11, 15, 23}, {13, 17, 25}};
 
 // ------------------------------------------------------------------------------ helpers
-VEP_HD int clip1(int x) { return x < 0 ? 0 : (x > 255 ? 255 : x); }
+VEP_HD int clip1(int x, int bd = 8) { return x < 0 ? 0 : (x > (1 << bd) - 1 ? (1 << bd) - 1 : x); }
 VEP_HD int clip3(int lo, int hi, int x) { return x < lo ? lo : (x > hi ? hi : x); }
 VEP_HD int iabs(int x) { return x < 0 ? -x : x; }
 VEP_HD int imin(int a, int b) { return a < b ? a : b; }
@@ -389,7 +397,7 @@ VEP_HD void intra8x8_filter(TF T, LF L, bool has_top, bool has_left, bool has_tl
 // Intra_8x8 sample prediction (§8.3.2.2.2 - 8.3.2.2.10) from the filtered references.
 // Generic: T(x) = p'[x,-1] for x in -1..15, L(y) = p'[-1,y] for y in -1..7 (L(-1) = T(-1)).
 template <class TF, class LF>
-VEP_HD int intra8x8_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, int x, int y) {
+VEP_HD int intra8x8_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, int x, int y, int bd = 8) {
   switch (mode) {
     case 0: return T(x);
     case 1: return L(y);
@@ -407,7 +415,7 @@ VEP_HD int intra8x8_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, in
         for (int k = 0; k < 8; ++k) s += T(k);
         return (s + 4) >> 3;
       }
-      return 128;
+      return 1 << (bd - 1);
     }
     case 3:
       if (x == 7 && y == 7) return (T(14) + 3 * T(15) + 2) >> 2;
@@ -529,9 +537,9 @@ VEP_HD u32 intra8x8_filter_tap(bool has_top, bool has_left, bool has_tl, int k) 
   return t3(L(y - 1), L(y), L(y + 1));
 }
 
-VEP_HD int intra8x8_pred(const int* f, bool has_top, bool has_left, int mode, int x, int y) {
+VEP_HD int intra8x8_pred(const int* f, bool has_top, bool has_left, int mode, int x, int y, int bd = 8) {
   return intra8x8_pred_g([&](int xx) { return f[1 + xx]; }, [&](int yy) { return yy < 0 ? f[0] : f[17 + yy]; },
-                         has_top, has_left, mode, x, y);
+                         has_top, has_left, mode, x, y, bd);
 }
 
 // ------------------------------------------------------------------------------ intra 4x4
@@ -547,7 +555,7 @@ struct Intra4Nb {
 // p[-1, yy] for yy in -1..3. The GPU passes LDS accessors, the CPU the Intra4Nb arrays; the
 // arithmetic is shared.
 template <class TF, class LF>
-VEP_HD int intra4x4_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, int x, int y) {
+VEP_HD int intra4x4_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, int x, int y, int bd = 8) {
   switch (mode) {
     case 0: return T(x);
     case 1: return L(y);
@@ -565,7 +573,7 @@ VEP_HD int intra4x4_pred_g(TF T, LF L, bool has_top, bool has_left, int mode, in
         for (int k = 0; k < 4; ++k) s += T(k);
         return (s + 2) >> 2;
       }
-      return 128;
+      return 1 << (bd - 1);
     }
     case 3:
       if (x == 3 && y == 3) return (T(6) + 3 * T(7) + 2) >> 2;
@@ -697,10 +705,10 @@ VEP_HD u32 pack_taps(const Taps4& t) {
          u32(t.w[1]) << 14 | u32(t.w[2]) << 16 | u32(t.add) << 18 | u32(t.shift) << 20;
 }
 
-VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y) {
+VEP_HD int intra4x4_pred(const Intra4Nb& n, int mode, int x, int y, int bd = 8) {
   return intra4x4_pred_g([&](int xx) { return n.t[xx + 1]; },
                          [&](int yy) { return yy < 0 ? n.t[0] : n.l[yy]; }, n.has_top, n.has_left,
-                         mode, x, y);
+                         mode, x, y, bd);
 }
 
 // ------------------------------------------------------------------------------ intra 16x16
@@ -720,8 +728,8 @@ struct PredConst {
 // Final step of the 16x16 constants from the neighbour sums (the GPU computes the sums with a
 // wave reduction): st / sl = sum of the 16 top / left samples, H / V the plane gradients.
 VEP_HD PredConst intra16x16_const_from_sums(int mode, bool has_top, bool has_left, int st, int sl,
-                                            int H, int V, int top15, int left15) {
-  PredConst k{128, 0, 0, 0};
+                                            int H, int V, int top15, int left15, int bd = 8) {
+  PredConst k{1 << (bd - 1), 0, 0, 0};
   if (mode == 2) {
     if (has_top && has_left) k.dc = (st + sl + 16) >> 5;
     else if (has_left) k.dc = (sl + 8) >> 4;
@@ -736,7 +744,7 @@ VEP_HD PredConst intra16x16_const_from_sums(int mode, bool has_top, bool has_lef
 
 // Generic forms: T(x) = p[x, -1] for x in -1..15, L(y) = p[-1, y] for y in 0..15.
 template <class TF, class LF>
-VEP_HD PredConst intra16x16_const_g(TF T, LF L, bool has_top, bool has_left, int mode) {
+VEP_HD PredConst intra16x16_const_g(TF T, LF L, bool has_top, bool has_left, int mode, int bd = 8) {
   int st = 0, sl = 0, H = 0, V = 0;
   for (int i = 0; i < 16; ++i) {
     st += T(i);
@@ -746,27 +754,27 @@ VEP_HD PredConst intra16x16_const_g(TF T, LF L, bool has_top, bool has_left, int
     H += (i + 1) * (T(8 + i) - T(6 - i));
     V += (i + 1) * (L(8 + i) - (6 - i >= 0 ? L(6 - i) : T(-1)));
   }
-  return intra16x16_const_from_sums(mode, has_top, has_left, st, sl, H, V, T(15), L(15));
+  return intra16x16_const_from_sums(mode, has_top, has_left, st, sl, H, V, T(15), L(15), bd);
 }
 
 template <class TF, class LF>
-VEP_HD int intra16x16_pred_g(TF T, LF L, const PredConst& k, int mode, int x, int y) {
+VEP_HD int intra16x16_pred_g(TF T, LF L, const PredConst& k, int mode, int x, int y, int bd = 8) {
   switch (mode) {
     case 0: return T(x);
     case 1: return L(y);
     case 2: return k.dc;
-    default: return clip1((k.a + k.b * (x - 7) + k.c * (y - 7) + 16) >> 5);
+    default: return clip1((k.a + k.b * (x - 7) + k.c * (y - 7) + 16) >> 5, bd);
   }
 }
 
-VEP_HD PredConst intra16x16_const(const Intra16Nb& n, int mode) {
+VEP_HD PredConst intra16x16_const(const Intra16Nb& n, int mode, int bd = 8) {
   return intra16x16_const_g([&](int x) { return n.top[x + 1]; }, [&](int y) { return n.left[y]; },
-                            n.has_top, n.has_left, mode);
+                            n.has_top, n.has_left, mode, bd);
 }
 
-VEP_HD int intra16x16_pred(const Intra16Nb& n, const PredConst& k, int mode, int x, int y) {
+VEP_HD int intra16x16_pred(const Intra16Nb& n, const PredConst& k, int mode, int x, int y, int bd = 8) {
   return intra16x16_pred_g([&](int xx) { return n.top[xx + 1]; }, [&](int yy) { return n.left[yy]; },
-                           k, mode, x, y);
+                           k, mode, x, y, bd);
 }
 
 // Chroma (4:2:0, 8x8 per component): top[0] = p[-1,-1], top[1..8]; left[0..7].
@@ -779,7 +787,7 @@ struct IntraChromaNb {
 // DC of chroma 4x4 block (bx, by) (§8.3.4.1-3). Generic: T(x) = p[x, -1] (x in -1..7),
 // L(y) = p[-1, y] (y in 0..7).
 template <class TF, class LF>
-VEP_HD int chroma_dc_g(TF T, LF L, bool has_top, bool has_left, int bx, int by) {
+VEP_HD int chroma_dc_g(TF T, LF L, bool has_top, bool has_left, int bx, int by, int bd = 8) {
   int st = 0, sl = 0;
   for (int i = 0; i < 4; ++i) {
     st += T(bx * 4 + i);
@@ -790,16 +798,16 @@ VEP_HD int chroma_dc_g(TF T, LF L, bool has_top, bool has_left, int bx, int by) 
     if (has_top && has_left) return (st + sl + 4) >> 3;
     if (has_left) return (sl + 2) >> 2;
     if (has_top) return (st + 2) >> 2;
-    return 128;
+    return 1 << (bd - 1);
   }
   if (bx > 0) {  // top-right block: top first
     if (has_top) return (st + 2) >> 2;
     if (has_left) return (sl + 2) >> 2;
-    return 128;
+    return 1 << (bd - 1);
   }
   if (has_left) return (sl + 2) >> 2;  // bottom-left block: left first
   if (has_top) return (st + 2) >> 2;
-  return 128;
+  return 1 << (bd - 1);
 }
 
 template <class TF, class LF>
@@ -816,12 +824,12 @@ VEP_HD PredConst chroma_plane_const_g(TF T, LF L) {
 // mode: 0 DC, 1 horizontal, 2 vertical, 3 plane
 template <class TF, class LF>
 VEP_HD int chroma_pred_g(TF T, LF L, bool has_top, bool has_left, const PredConst& k, int mode, int x,
-                         int y) {
+                         int y, int bd = 8) {
   switch (mode) {
-    case 0: return chroma_dc_g(T, L, has_top, has_left, x >> 2, y >> 2);
+    case 0: return chroma_dc_g(T, L, has_top, has_left, x >> 2, y >> 2, bd);
     case 1: return L(y);
     case 2: return T(x);
-    default: return clip1((k.a + k.b * (x - 3) + k.c * (y - 3) + 16) >> 5);
+    default: return clip1((k.a + k.b * (x - 3) + k.c * (y - 3) + 16) >> 5, bd);
   }
 }
 
@@ -829,14 +837,15 @@ VEP_HD PredConst chroma_plane_const(const IntraChromaNb& n) {
   return chroma_plane_const_g([&](int x) { return n.top[x + 1]; }, [&](int y) { return n.left[y]; });
 }
 
-VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y) {
+VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y, int bd = 8) {
   return chroma_pred_g([&](int xx) { return n.top[xx + 1]; }, [&](int yy) { return n.left[yy]; },
-                       n.has_top, n.has_left, k, mode, x, y);
+                       n.has_top, n.has_left, k, mode, x, y, bd);
 }
 
 // ------------------------------------------------------------------------------ inter
 // Reference sample fetch with edge clamping (§8.4.2.2.1 Clip3 on xInt/yInt).
-VEP_HD int ref_px(const u8* p, int pitch, int w, int h, int x, int y) {
+template <class P>
+VEP_HD int ref_px(const P* p, int pitch, int w, int h, int x, int y) {
   x = clip3(0, w - 1, x);
   y = clip3(0, h - 1, y);
   return p[size_t(y) * pitch + x];
@@ -848,7 +857,9 @@ VEP_HD int tap6(int a, int b, int c, int d, int e, int f) {
 
 // Luma sample prediction at integer (xi, yi) with fractional offset (fx, fy) in quarter samples
 // (Table 8-12).
-VEP_HD int luma_qpel(const u8* p, int pitch, int w, int h, int xi, int yi, int fx, int fy) {
+// (P: u8 planes, or u16 at bit depth bd: High 10)
+template <class P>
+VEP_HD int luma_qpel(const P* p, int pitch, int w, int h, int xi, int yi, int fx, int fy, int bd = 8) {
   auto G = [&](int dx, int dy) { return ref_px(p, pitch, w, h, xi + dx, yi + dy); };
   // unrounded half-sample intermediates
   auto b1 = [&](int dy) {  // horizontal half sample between (0,dy) and (1,dy)
@@ -857,7 +868,7 @@ VEP_HD int luma_qpel(const u8* p, int pitch, int w, int h, int xi, int yi, int f
   auto h1 = [&](int dx) {  // vertical half sample between (dx,0) and (dx,1)
     return tap6(G(dx, -2), G(dx, -1), G(dx, 0), G(dx, 1), G(dx, 2), G(dx, 3));
   };
-  auto rb = [&](int v) { return clip1((v + 16) >> 5); };
+  auto rb = [&](int v) { return clip1((v + 16) >> 5, bd); };
   if (fx == 0 && fy == 0) return G(0, 0);
   if (fy == 0) {
     const int b = rb(b1(0));
@@ -872,7 +883,7 @@ VEP_HD int luma_qpel(const u8* p, int pitch, int w, int h, int xi, int yi, int f
   if (fx == 2 || fy == 2) {
     // j from the vertical 6-tap over horizontal intermediates
     const int j1 = tap6(b1(-2), b1(-1), b1(0), b1(1), b1(2), b1(3));
-    const int j = clip1((j1 + 512) >> 10);
+    const int j = clip1((j1 + 512) >> 10, bd);
     if (fx == 2 && fy == 2) return j;
     if (fx == 2) {  // f (fy 1) / q (fy 3): with b (row 0) or s (row 1)
       const int o = rb(b1(fy == 1 ? 0 : 1));
@@ -890,7 +901,8 @@ VEP_HD int luma_qpel(const u8* p, int pitch, int w, int h, int xi, int yi, int f
 
 // Chroma sample prediction (§8.4.2.2.2) at integer (xi, yi) with eighth-sample (fx, fy) in one
 // component of an interleaved NV12 plane (component c in {0, 1}); w, h in chroma samples.
-VEP_HD int chroma_epel(const u8* uv, int pitch, int w, int h, int c, int xi, int yi, int fx,
+template <class P>
+VEP_HD int chroma_epel(const P* uv, int pitch, int w, int h, int c, int xi, int yi, int fx,
                        int fy) {
   auto S = [&](int x, int y) {
     x = clip3(0, w - 1, x);
@@ -951,10 +963,13 @@ struct EdgeParams {
   int tc0[3];  // tC0 for bS 1..3 (Table 8-17), resolved once per edge, not per sample line
 };
 
-VEP_HD EdgeParams edge_params(int qp_p, int qp_q, int off_a, int off_b) {
+// (qp_p / qp_q: QPY of the two MBs, or their QPC for chroma edges; negative at high bit depth.
+// bd > 8: alpha / beta / tC0 scaled by 1 << (bd - 8), §8.7.2.2)
+VEP_HD EdgeParams edge_params(int qp_p, int qp_q, int off_a, int off_b, int bd = 8) {
   const int qav = (qp_p + qp_q + 1) >> 1;
   const int ia = clip3(0, 51, qav + off_a), ib = clip3(0, 51, qav + off_b);
-  return EdgeParams{kAlpha[ia], kBeta[ib], {kTc0[ia][0], kTc0[ia][1], kTc0[ia][2]}};
+  const int s = bd - 8;
+  return EdgeParams{kAlpha[ia] << s, kBeta[ib] << s, {kTc0[ia][0] << s, kTc0[ia][1] << s, kTc0[ia][2] << s}};
 }
 
 // Filter one line of samples across an edge: s points at q0, `step` is the distance between
@@ -963,15 +978,15 @@ VEP_HD EdgeParams edge_params(int qp_p, int qp_q, int off_a, int off_b) {
 // Filter one sample line in registers: p[k] = p_k, q[k] = q_k (k = 0..3; chroma uses k < 2).
 // Returns false (nothing changed) when the edge is not filtered at this line. tc0 = tC0 of
 // the line's bS (ignored for bS 4).
-VEP_HD bool filter_samples(int* p, int* q, int bs, int alpha, int beta, int tc0, bool chroma) {
+VEP_HD bool filter_samples(int* p, int* q, int bs, int alpha, int beta, int tc0, bool chroma, int bd = 8) {
   const int p0 = p[0], p1 = p[1], q0 = q[0], q1 = q[1];
   if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return false;
   if (chroma) {
     if (bs < 4) {
       const int tc = tc0 + 1;
       const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-      p[0] = clip1(p0 + d);
-      q[0] = clip1(q0 - d);
+      p[0] = clip1(p0 + d, bd);
+      q[0] = clip1(q0 - d, bd);
     } else {
       p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
       q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
@@ -983,8 +998,8 @@ VEP_HD bool filter_samples(int* p, int* q, int bs, int alpha, int beta, int tc0,
   if (bs < 4) {
     const int tc = tc0 + (ap < beta) + (aq < beta);
     const int d = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
-    p[0] = clip1(p0 + d);
-    q[0] = clip1(q0 - d);
+    p[0] = clip1(p0 + d, bd);
+    q[0] = clip1(q0 - d, bd);
     if (ap < beta) p[1] = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
     if (aq < beta) q[1] = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
     return true;
@@ -1010,14 +1025,14 @@ VEP_HD bool filter_samples(int* p, int* q, int bs, int alpha, int beta, int tc0,
 
 // filter_samples on samples in memory (stride `step` across the edge; s = q0).
 template <typename Px>
-VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0, bool chroma) {
+VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0, bool chroma, int bd = 8) {
   const int n = chroma ? 2 : 4;
   int p[4] = {0, 0, 0, 0}, q[4] = {0, 0, 0, 0};
   for (int k = 0; k < n; ++k) {
     p[k] = s[-(k + 1) * step];
     q[k] = s[k * step];
   }
-  if (!filter_samples(p, q, bs, alpha, beta, tc0, chroma)) return;
+  if (!filter_samples(p, q, bs, alpha, beta, tc0, chroma, bd)) return;
   const int m = chroma ? 1 : 3;
   for (int k = 0; k < m; ++k) {
     s[-(k + 1) * step] = Px(p[k]);
@@ -1026,8 +1041,8 @@ VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0
 }
 
 template <typename Px>
-VEP_HD void filter_line(Px* s, long step, int bs, const EdgeParams& e, bool chroma) {
-  filter_line_t(s, step, bs, e.alpha, e.beta, bs < 4 ? e.tc0[bs - 1] : 0, chroma);
+VEP_HD void filter_line(Px* s, long step, int bs, const EdgeParams& e, bool chroma, int bd = 8) {
+  filter_line_t(s, step, bs, e.alpha, e.beta, bs < 4 ? e.tc0[bs - 1] : 0, chroma, bd);
 }
 
 }  // namespace vep::avc
