@@ -168,7 +168,8 @@ struct CpuDecoder {
         done = nal >= au.nals.size();
         if (slots.size() < size_t(pic->dpb_slots)) slots.resize(size_t(pic->dpb_slots));
         for (auto& h : slots)
-          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16) h.alloc(pic->wmbs * 16, pic->hmbs * 16);
+          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16 || h.bd != pic->bd)
+            h.alloc(pic->wmbs * 16, pic->hmbs * 16, pic->bd);
         avc::cpu_reconstruct(*pic, slots);
         coded = pic->info.coded_mbs;
         pictures.push_back(pic->info);
@@ -212,6 +213,14 @@ struct CpuDecoder {
     py::list l;
     for (const auto& f : fs) {
       const HostSurface& s = frame_of(f);
+      if (s.wide()) {  // High 10: u16 planes
+        py::array_t<uint16_t> y({s.coded_h, s.coded_w});
+        py::array_t<uint16_t> uv({s.coded_h / 2, s.coded_w});
+        std::memcpy(y.mutable_data(), s.y16.data(), s.y16.size() * 2);
+        std::memcpy(uv.mutable_data(), s.uv16.data(), s.uv16.size() * 2);
+        l.append(py::make_tuple(f.au.pts, py::make_tuple(y, uv)));
+        continue;
+      }
       py::array_t<uint8_t> y({s.coded_h, s.coded_w});
       py::array_t<uint8_t> uv({s.coded_h / 2, s.coded_w});
       std::memcpy(y.mutable_data(), s.y.data(), s.y.size());
@@ -370,6 +379,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("pyramid", &avc::AvcHighConfig::pyramid)
       .def_readwrite("refs", &avc::AvcHighConfig::refs)
       .def_readwrite("qp", &avc::AvcHighConfig::qp)
+      .def_readwrite("bit_depth", &avc::AvcHighConfig::bit_depth)
       .def_readwrite("cabac", &avc::AvcHighConfig::cabac)
       .def_readwrite("t8x8", &avc::AvcHighConfig::t8x8)
       .def_readwrite("weighted_p", &avc::AvcHighConfig::weighted_p)
@@ -716,17 +726,20 @@ PYBIND11_MODULE(_vep, m) {
     const int h = int(uv.shape(0)), pitch = int(uv.shape(1));
     return avc::chroma_epel(uv.data(), pitch, pitch / 2, h, c, xi, yi, fx, fy);
   });
-  rc.def("edge_params", [](int qp_p, int qp_q, int off_a, int off_b) {
-    const avc::EdgeParams e = avc::edge_params(qp_p, qp_q, off_a, off_b);
+  rc.def("edge_params", [](int qp_p, int qp_q, int off_a, int off_b, int bd) {
+    const avc::EdgeParams e = avc::edge_params(qp_p, qp_q, off_a, off_b, bd);
     return py::make_tuple(e.alpha, e.beta, std::vector<int>{e.tc0[0], e.tc0[1], e.tc0[2]});
-  });
+  }, py::arg("qp_p"), py::arg("qp_q"), py::arg("off_a"), py::arg("off_b"), py::arg("bd") = 8);
+  // QPC of Table 8-15 from QPY (QpBdOffsetC: High 10 QPs below 0)
+  rc.def("chroma_qp_bd", [](int qpy, int offset, int qpbd_c) { return avc::chroma_qp_bd(qpy, offset, qpbd_c); });
   // one sample line across an edge: p = p0..p3, q = q0..q3 -> filtered (p, q)
   rc.def("filter_line", [](std::vector<int> p, std::vector<int> q, int bs, int alpha, int beta, int tc0,
-                           bool chroma) {
+                           bool chroma, int bd) {
     VEP_CHECK(p.size() == 4 && q.size() == 4, "4 + 4 samples");
-    avc::filter_samples(p.data(), q.data(), bs, alpha, beta, tc0, chroma);
+    avc::filter_samples(p.data(), q.data(), bs, alpha, beta, tc0, chroma, bd);
     return py::make_tuple(p, q);
-  });
+  }, py::arg("p"), py::arg("q"), py::arg("bs"), py::arg("alpha"), py::arg("beta"), py::arg("tc0"),
+     py::arg("chroma"), py::arg("bd") = 8);
 
   m.def("cavlc_roundtrip", [](int nc, int max_coeff, const std::vector<int>& c) {
     // write_residual_block -> read_residual_block (table self-consistency, tests only)
@@ -761,6 +774,9 @@ PYBIND11_MODULE(_vep, m) {
     d["fps"] = s.fps();
     d["poc_type"] = s.poc_type;
     d["max_num_ref_frames"] = s.max_num_ref_frames;
+    d["chroma_format_idc"] = s.chroma_format_idc;
+    d["bit_depth_luma"] = s.bit_depth_luma;
+    d["bit_depth_chroma"] = s.bit_depth_chroma;
     return d;
   });
   m.def("parse_hevc_sps", [](const std::string& nal) {

@@ -180,7 +180,9 @@ namespace {
 
 // Stream features outside the supported subset (progressive 8-bit 4:2:0, no lossless).
 void check_sps_supported(const Sps& s) {
-  if ((s.chroma_format_idc != 1 && s.chroma_format_idc != 0) || s.bit_depth_luma != 8 || s.bit_depth_chroma != 8)
+  // (High 10: 9 / 10-bit samples, one depth for luma and chroma: the surfaces hold one)
+  if ((s.chroma_format_idc != 1 && s.chroma_format_idc != 0) || s.bit_depth_luma > 10 ||
+      s.bit_depth_chroma != s.bit_depth_luma)
     throw UnsupportedStream("only 8-bit 4:2:0 / 4:0:0 H.264 is supported");
   // Interlaced SPS (frame_mbs_only_flag 0): frame pictures decode as progressive ones (frame
   // macroblocks, frame POC = min(top, bottom)); field pictures as half-height pictures in field
@@ -331,7 +333,7 @@ static SliceHdr read_slice_header(Bits& br, u8 nal_hdr, const Sps& sps, const Pp
     VEP_CHECK(sh.cabac_init_idc <= 2, "bad cabac_init_idc");
   }
   sh.qp = pps.pic_init_qp + br.se();
-  VEP_CHECK(sh.qp >= 0 && sh.qp <= 51, "slice QP out of range");
+  VEP_CHECK(sh.qp >= -6 * (sps.bit_depth_luma - 8) && sh.qp <= 51, "slice QP out of range");
   if (pps.deblocking_filter_control) {
     sh.disable_deblocking = int(br.ue());
     VEP_CHECK(sh.disable_deblocking <= 2, "bad disable_deblocking_filter_idc");
@@ -1292,7 +1294,7 @@ namespace {
 // The fast CAVLC MbDecoder above covers a slice when nothing beyond Baseline-style syntax is in
 // use (the default synthetic camera streams); everything else goes to decode_slice_generic.
 bool legacy_slice(const SliceHdr& sh, const Sps& sps, const Pps& pps) {
-  return !pps.cabac && !sh.field_pic && sps.chroma_format_idc == 1 && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
+  return !pps.cabac && !sh.field_pic && sps.chroma_format_idc == 1 && sps.bit_depth_luma == 8 && (sh.type() == h264::kP || sh.type() == h264::kI) && !pps.transform_8x8_mode &&
          !sps.scaling_matrix_present && !pps.scaling_matrix_present && !sh.explicit_wp &&
          pps.chroma_qp_index_offset == pps.second_chroma_qp_index_offset;
 }
@@ -1409,6 +1411,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       ++redundant_slices_skipped;
       continue;
     }
+    if (sh.field_pic && sps.bit_depth_luma > 8)
+      throw UnsupportedStream("H.264 High 10 field pictures are not supported (progressive only)");
     if (!got) {
       first = sh;
       act_sps = &sps;
@@ -1420,7 +1424,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
                      pair_.frame_num == sh.frame_num;
       if (!second_field) close_pair(*pic);  // an unpaired field leaves before this picture
       if (sh.idr() && !second_field) {
-        hard_flush = slots != dpb_slots_ || W != wmbs_ || H != hmbs_ || sh.field_pic != field_mode_;
+        hard_flush = slots != dpb_slots_ || W != wmbs_ || H != hmbs_ || sh.field_pic != field_mode_ ||
+                     sps.bit_depth_luma != bd_;
+        bd_ = sps.bit_depth_luma;
         field_mode_ = sh.field_pic;
         have_idr_ = true;
         dpb_slots_ = slots;
@@ -1431,7 +1437,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
         if (!have_idr_) throw Error("vep: H.264 stream does not start with an IDR picture");
         // a non-IDR picture may not change the picture size or the DPB (a mid-GOP SPS that
         // does would make earlier pictures of a batch write outside the surfaces)
-        VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_, "SPS changed without an IDR picture");
+        VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_ && sps.bit_depth_luma == bd_,
+                  "SPS changed without an IDR picture");
         if (sh.field_pic != field_mode_)
           throw UnsupportedStream("interlaced H.264: frame and field pictures mixed in one IDR period are not supported");
       }
@@ -1452,6 +1459,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       pic->mvs.reserve(size_t(W) * Hp * 16);
       pic->dpb_slots = field_mode_ ? 2 * dpb_slots_ : dpb_slots_;
       pic->structure = sh.field_pic ? 1 + int(sh.bottom_field) : 0;
+      pic->bd = sps.bit_depth_luma;
+      pic->qp_bias = 6 * (sps.bit_depth_luma - 8);
+      pic->qpc_bias = 6 * (sps.bit_depth_chroma - 8);
       pic->second_field = second_field;
       pic->constrained_intra = pps.constrained_intra_pred;
       pic->idr = sh.idr();
@@ -1562,6 +1572,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       sh.dpb_slots = pic->dpb_slots;
       sh.constrained_intra = pic->constrained_intra;
       sh.poc = pic->poc;
+      sh.bd = pic->bd;
+      sh.qp_bias = pic->qp_bias;
+      sh.qpc_bias = pic->qpc_bias;
       u.colb.col = col_target;
       u.colb.uids = &u.uids;
       sh.colb = col_target ? &u.colb : nullptr;
@@ -1719,9 +1732,10 @@ void Decoder::parse_slice_data(MbNeighbours& nb, Picture& pic, const SliceHdr& s
 static inline void validate_mb(const Picture& p, const MbRec& m, bool written = false) {
   const size_t ncoef = p.coefs.size(), nmv = p.mvs.size();
   VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
-  VEP_CHECK(m.qp <= 51 && m.qpc <= 51 && m.qpc2 <= 51, "macroblock QP out of range");
+  VEP_CHECK(m.qp <= 51 + p.qp_bias && m.qpc <= 51 + p.qpc_bias && m.qpc2 <= 51 + p.qpc_bias,
+            "macroblock QP out of range");
   if (m.kind == kIPcm) {
-    VEP_CHECK(size_t(m.coef) + kPcmMbBytes / 2 <= ncoef, "I_PCM samples outside the pool");
+    VEP_CHECK(size_t(m.coef) + (p.bd > 8 ? kPcmMbBytes : kPcmMbBytes / 2) <= ncoef, "I_PCM samples outside the pool");
     return;
   }
   // sparse groups: the mask words, then as many values as they announce, inside the pool
@@ -2039,9 +2053,10 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   m.chroma_coded = 0;
   if (m.kind == kIPcm) {
     VEP_CHECK(pcm, "I_PCM macroblock without samples");
-    const size_t o = pic.coefs.size();
-    pic.coefs.resize(o + kPcmMbBytes / 2);
-    std::memcpy(pic.coefs.data() + o, pcm, kPcmMbBytes);
+    // (8-bit: 384 sample bytes; High 10: `pcm` holds 384 u16 samples)
+    const size_t o = pic.coefs.size(), nb = pic.bd > 8 ? 2 * kPcmMbBytes : kPcmMbBytes;
+    pic.coefs.resize(o + nb / 2);
+    std::memcpy(pic.coefs.data() + o, pcm, nb);
   } else if (res && (res->luma | res->chroma)) {
     m.luma_coded = res->luma;
     m.chroma_coded = res->chroma;
@@ -2467,7 +2482,7 @@ void weave_fields(const HostSurface& top, const HostSurface& bottom, HostSurface
 void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots) {
   VEP_CHECK(pic.target >= 0 && pic.target < int(slots.size()), "target slot out of range");
   HostSurface& T = slots[size_t(pic.target)];
-  VEP_CHECK(T.coded_w == pic.wmbs * 16 && T.coded_h == pic.hmbs * 16, "surface size mismatch");
+  VEP_CHECK(T.coded_w == pic.wmbs * 16 && T.coded_h == pic.hmbs * 16 && T.bd == pic.bd, "surface size mismatch");
   for (int mb = 0; mb < pic.nmbs(); ++mb) cpu_reconstruct_mb(pic, mb, slots);
   if (pic.deblock) cpu_deblock(pic, T);
 }

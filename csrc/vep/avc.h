@@ -418,6 +418,7 @@ class Decoder {
   int max_lt_idx_ = -1;     // MaxLongTermFrameIdx ("no long-term frame indices" = -1)
   int dpb_slots_ = 2;
   int wmbs_ = 0, hmbs_ = 0;  // active picture size (changes only at an IDR)
+  int bd_ = 8;               // active sample bit depth (changes only at an IDR)
   bool have_idr_ = false;
   int pinned_slot_ = -1;    // newest output: kept until a newer one leaves the reorder buffer
   int last_out_poc_ = 0;
@@ -616,6 +617,8 @@ struct AvcHighConfig {
                               // first; I / P, P / P anchors and non-reference B / B pairs; CAVLC,
                               // 4x4 transforms
   bool mono = false;          // 4:0:0 (monochrome, High profile): luma only, chroma decodes grey
+  int bit_depth = 8;          // 9 / 10: High 10 profile (u16 samples; frame pictures only); qp may
+                              // then go down to -6 * (bit_depth - 8)
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;
   u64 seed = 1;

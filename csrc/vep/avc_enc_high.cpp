@@ -144,6 +144,7 @@ struct AvcHighEncoder::Impl {
   int ph = 0;
   HostSurface field_src;
   int pair_slot = -1, pair_fn = 0;
+  int bd = 8, qpbd = 0;  // sample bit depth, QpBdOffset (High 10)
   const u8* scan4 = kZigzag4x4;  // 4x4 level scan of the current picture (field pictures: field scan)
   const u8* scan8 = kZigzag8x8;
 
@@ -151,7 +152,11 @@ struct AvcHighEncoder::Impl {
     VEP_CHECK(c.width >= 16 && c.height >= 16 && c.width % 2 == 0 && c.height % 2 == 0,
               "encoder size must be even and >= 16");
     VEP_CHECK(c.bframes >= 0 && c.bframes <= 4 && c.refs >= 1 && c.refs <= 8, "bframes 0..4, refs 1..8");
-    VEP_CHECK(c.qp >= 0 && c.qp <= 51 && c.gop >= 1, "bad encoder config");
+    VEP_CHECK(c.bit_depth >= 8 && c.bit_depth <= 10 && (c.bit_depth == 8 || !c.fields),
+              "bit_depth 8..10 (High 10: frame pictures)");
+    bd = c.bit_depth;
+    qpbd = 6 * (bd - 8);
+    VEP_CHECK(c.qp >= -qpbd && c.qp <= 51 && c.gop >= 1, "bad encoder config");
     VEP_CHECK(!c.fields || (c.interlaced && !c.cabac), "field coding: interlaced CAVLC only");
     fields = c.fields;
     W = (c.width + 15) / 16;
@@ -159,8 +164,9 @@ struct AvcHighEncoder::Impl {
     if (c.interlaced) H = (H + 1) & ~1;  // (frame height in MB pairs: map units of 2 MB rows)
     wpx = W * 16;
     hpx = H * 16;
-    sps.profile_idc = (c.t8x8 || c.scaling || c.mono) ? 100 : 77;
+    sps.profile_idc = bd > 8 ? 110 : (c.t8x8 || c.scaling || c.mono) ? 100 : 77;
     sps.chroma_format_idc = c.mono ? 0 : 1;
+    sps.bit_depth_luma = sps.bit_depth_chroma = bd;
     VEP_CHECK(!c.mono || (!c.weighted_p && c.weighted_b != 1), "4:0:0 encoder: explicit weighted prediction is not emitted");
     sps.constraint_flags = 0;
     sps.level_idc = W * H > 8192 ? 51 : 40;
@@ -204,7 +210,7 @@ struct AvcHighEncoder::Impl {
     nal(h264::write_pps(pps), pps_nal);
     ph = fields ? hpx / 2 : hpx;
     slots.resize((size_t(sps.max_num_ref_frames) + 2) * (fields ? 2 : 1));
-    for (auto& s : slots) s.alloc(wpx, ph);
+    for (auto& s : slots) s.alloc(wpx, ph, bd);
     scene.make(SceneConfig{c.width, c.height, wpx, hpx, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
   }
 
@@ -216,7 +222,16 @@ struct AvcHighEncoder::Impl {
       if (rendered > 0) scene.advance();
       scene.render();
       scene.add_sensor_noise(rendered);
-      sources[rendered] = scene.src;
+      if (bd > 8) {  // High 10 source: the 8-bit scene << 2 plus a position / time dither in the low bits
+        HostSurface& w = sources[rendered];
+        w.alloc(scene.src.coded_w, scene.src.coded_h, bd);
+        const int sh = bd - 8;
+        auto lo = [&](size_t i) { return u16(u16((i * 2654435761u + u64(rendered) * 40503u) >> 29) & ((1u << sh) - 1)); };
+        for (size_t i = 0; i < w.y16.size(); ++i) w.y16[i] = u16(scene.src.y[i] << sh | lo(i));
+        for (size_t i = 0; i < w.uv16.size(); ++i) w.uv16[i] = u16(scene.src.uv[i] << sh | lo(i + 7));
+      } else {
+        sources[rendered] = scene.src;
+      }
     }
     return sources.at(d);
   }
@@ -907,8 +922,11 @@ struct AvcHighEncoder::Impl {
   }
 
   // ---------------------------------------------------------------- helpers
-  int S(int x, int y) const { return cur_src->y[size_t(y) * wpx + x]; }
-  int SC(int x, int y, int c) const { return cur_src->uv[size_t(y) * wpx + 2 * x + c]; }
+  int S(int x, int y) const { return cur_src->get(0, x, y); }
+  int SC(int x, int y, int c) const { return cur_src->get(1 + c, x, y); }
+  // reconstructed luma sample of the current picture (u8 or u16 surface)
+  int ty(int x, int y) { return T().get(0, x, y); }
+  void set_ty(int x, int y, int v) { T().set(0, x, y, v); }
   HostSurface& T() { return slots[size_t(pic.target)]; }
 
   // Neighbour MB (dx, dy) of `mb` coded in the current slice (intra availability).
@@ -921,6 +939,7 @@ struct AvcHighEncoder::Impl {
   int cur_slice = 0;
 
   // Luma / chroma residual levels of a prediction into `d` (t8: 8x8 transform), cbp returned.
+  // (qp = QP'Y = QPY + QpBdOffsetY)
   int code_residual(int mb, const int* py, const int (*pc)[64], bool intra, bool t8, bool i16, int qp, MbDesc& d) {
     const int mx = mb % W, my = mb / W;
     int cl = 0;
@@ -974,7 +993,8 @@ struct AvcHighEncoder::Impl {
       }
     }
     int cc = 0;
-    const int qpc[2] = {chroma_qp(qp, pps.chroma_qp_index_offset), chroma_qp(qp, pps.second_chroma_qp_index_offset)};
+    const int qpc[2] = {chroma_qp_bd(qp - qpbd, pps.chroma_qp_index_offset, qpbd) + qpbd,
+                        chroma_qp_bd(qp - qpbd, pps.second_chroma_qp_index_offset, qpbd) + qpbd};
     for (int c = 0; c < (cfg.mono ? 0 : 2); ++c) {  // (4:0:0: no chroma residual)
       int cw[4];
       for (int b = 0; b < 4; ++b) {
@@ -1041,7 +1061,9 @@ struct AvcHighEncoder::Impl {
       for (int i = 0; i < 16; i += 2)
         for (int j = 0; j < 16; j += 2) {
           const int x = mx * 16 + j, y = my * 16 + i;
-          s += std::abs(S(x, y) - luma_qpel(R.y.data(), wpx, wpx, ph, x + (vx >> 2), y + (vy >> 2), vx & 3, vy & 3));
+          const int p = bd > 8 ? luma_qpel(R.y16.data(), wpx, wpx, ph, x + (vx >> 2), y + (vy >> 2), vx & 3, vy & 3, bd)
+                               : luma_qpel(R.y.data(), wpx, wpx, ph, x + (vx >> 2), y + (vy >> 2), vx & 3, vy & 3);
+          s += std::abs(S(x, y) - p);
         }
       return s * 4 + 4 * (std::abs(vx - pmv[0]) + std::abs(vy - pmv[1]));
     };
@@ -1095,7 +1117,7 @@ struct AvcHighEncoder::Impl {
         IntraChromaNb n;
         chroma_neighbours(pic, mb, c, T(), n);
         for (int y = 0; y < 8; ++y)
-          for (int x = 0; x < 8; ++x) cp[c][y * 8 + x] = chroma_pred(n, PredConst{0, 0, 0, 0}, 0, x, y);
+          for (int x = 0; x < 8; ++x) cp[c][y * 8 + x] = chroma_pred(n, PredConst{0, 0, 0, 0}, 0, x, y, bd);
       }
       d.chroma_mode = 0;
     }
@@ -1118,7 +1140,7 @@ struct AvcHighEncoder::Impl {
           int s = 0;
           for (int i = 0; i < 8; ++i)
             for (int j = 0; j < 8; ++j)
-              s += std::abs(S(mx * 16 + bx * 8 + j, my * 16 + by * 8 + i) - intra8x8_pred(f, top, left, mode, j, i));
+              s += std::abs(S(mx * 16 + bx * 8 + j, my * 16 + by * 8 + i) - intra8x8_pred(f, top, left, mode, j, i, bd));
           if (s < best_s) {
             best_s = s;
             best = mode;
@@ -1128,7 +1150,7 @@ struct AvcHighEncoder::Impl {
         int x[64], pb[64];
         for (int i = 0; i < 8; ++i)
           for (int j = 0; j < 8; ++j) {
-            pb[i * 8 + j] = intra8x8_pred(f, top, left, best, j, i);
+            pb[i * 8 + j] = intra8x8_pred(f, top, left, best, j, i, bd);
             py[(by * 8 + i) * 16 + bx * 8 + j] = pb[i * 8 + j];
             x[i * 8 + j] = S(mx * 16 + bx * 8 + j, my * 16 + by * 8 + i) - pb[i * 8 + j];
           }
@@ -1137,7 +1159,7 @@ struct AvcHighEncoder::Impl {
         recon8x8(d.l8[q], qp, r, scan8);
         for (int i = 0; i < 8; ++i)
           for (int j = 0; j < 8; ++j)
-            t.y[size_t(my * 16 + by * 8 + i) * wpx + mx * 16 + bx * 8 + j] = u8(clip1(pb[i * 8 + j] + r[i * 8 + j]));
+            t.set(0, mx * 16 + bx * 8 + j, my * 16 + by * 8 + i, clip1(pb[i * 8 + j] + r[i * 8 + j], bd));
         sad += best_s;
       }
       MbDesc tmp;
@@ -1161,18 +1183,18 @@ struct AvcHighEncoder::Impl {
     int py[256];
     for (int mode = 0; mode < 4; ++mode) {
       if ((mode == 0 && !B) || (mode == 1 && !A) || (mode == 3 && !(A && B && D))) continue;
-      const PredConst k = intra16x16_const(n, mode);
+      const PredConst k = intra16x16_const(n, mode, bd);
       int s = 0;
       for (int y = 0; y < 16; ++y)
-        for (int x = 0; x < 16; ++x) s += std::abs(S(mx * 16 + x, my * 16 + y) - intra16x16_pred(n, k, mode, x, y));
+        for (int x = 0; x < 16; ++x) s += std::abs(S(mx * 16 + x, my * 16 + y) - intra16x16_pred(n, k, mode, x, y, bd));
       if (s < best_s) {
         best_s = s;
         best = mode;
       }
     }
-    const PredConst k = intra16x16_const(n, best);
+    const PredConst k = intra16x16_const(n, best, bd);
     for (int y = 0; y < 16; ++y)
-      for (int x = 0; x < 16; ++x) py[y * 16 + x] = intra16x16_pred(n, k, best, x, y);
+      for (int x = 0; x < 16; ++x) py[y * 16 + x] = intra16x16_pred(n, k, best, x, y, bd);
     const int cbp = code_residual(mb, py, cp, true, false, true, qp, d);
     d.mb_type = 1 + best + 4 * (cbp >> 4) + 12 * ((cbp & 15) ? 1 : 0);
     if (!(cbp & 15))
@@ -1213,6 +1235,15 @@ struct AvcHighEncoder::Impl {
       while ((m == 1 && !A) || (m == 2 && !B) || (m == 3 && !(A && B && D)));
       return m;
     };
+    if (islice_pcm_ok && r < 5 && bd > 8) {  // (High 10: u16 samples of bd bits)
+      static thread_local u16 pcm16[kPcmMbBytes];
+      for (auto& p : pcm16) p = u16(rng.uni(1 << bd));
+      if (cfg.mono)
+        for (size_t i = 256; i < kPcmMbBytes; ++i) pcm16[i] = u16(1 << (bd - 1));
+      d.pcm = reinterpret_cast<const u8*>(pcm16);
+      base_type = 25;
+      return;
+    }
     if (islice_pcm_ok && r < 5) {
       static thread_local u8 pcm[kPcmMbBytes];
       for (auto& p : pcm) p = u8(16 + rng.uni(220));
@@ -1366,7 +1397,7 @@ struct AvcHighEncoder::Impl {
       }
     }
     sh.cabac_init_idc = 0;
-    sh.qp = std::clamp(cfg.qp + (job.type == h264::kB ? (job.ref ? 1 : 2) : 0), 0, 51);
+    sh.qp = std::clamp(cfg.qp + (job.type == h264::kB ? (job.ref ? 1 : 2) : 0), -qpbd, 51);
     sh.disable_deblocking = cfg.deblock_idc;
     const bool weighted = sh.explicit_wp || (job.type == h264::kB && cfg.weighted_b == 2);
 
@@ -1379,6 +1410,8 @@ struct AvcHighEncoder::Impl {
     pic.mvs.reserve(size_t(W) * Hp * 64);
     pic.dpb_slots = int(slots.size());
     pic.structure = fld ? 1 + job.parity : 0;
+    pic.bd = bd;
+    pic.qp_bias = pic.qpc_bias = qpbd;
     pic.target = fld ? 2 * (job.parity == 1 ? pair_slot : pick_slot()) + job.parity : pick_slot();
     if (job.parity == 0) {  // the pair's frame_num and frame slot, for its second field
       pair_fn = sh.frame_num;
@@ -1474,7 +1507,7 @@ struct AvcHighEncoder::Impl {
 
   void decide(const SliceEnv& env, SliceWriter& sw, int mb, const Job& job, const SliceHdr& sh, bool weighted,
               MbDesc& d) {
-    const int qp = sh.qp;
+    const int qp = sh.qp + qpbd;  // QP'Y
     const int t = job.type;
     if (cfg.coverage) {
       decide_random(env, sw, mb, t, d);
@@ -1548,10 +1581,12 @@ struct AvcHighEncoder::Impl {
       MbDesc id;
       int isad;
       HostSurface& T0 = T();
-      std::vector<u8> save;
+      std::vector<int> save;
+      (void)T0;
       if (cfg.t8x8) {  // decide_intra's closed loop writes samples: keep them to undo
         save.resize(16 * 16);
-        for (int y = 0; y < 16; ++y) std::memcpy(&save[size_t(y) * 16], &T0.y[size_t(mb / W * 16 + y) * wpx + mb % W * 16], 16);
+        for (int y = 0; y < 16; ++y)
+          for (int x = 0; x < 16; ++x) save[size_t(y) * 16 + x] = ty(mb % W * 16 + x, mb / W * 16 + y);
       }
       decide_intra(mb, qp, id, isad);
       if (isad + 256 * 4 < best_cost) {
@@ -1560,7 +1595,8 @@ struct AvcHighEncoder::Impl {
         return;
       }
       if (cfg.t8x8)
-        for (int y = 0; y < 16; ++y) std::memcpy(&T0.y[size_t(mb / W * 16 + y) * wpx + mb % W * 16], &save[size_t(y) * 16], 16);
+        for (int y = 0; y < 16; ++y)
+          for (int x = 0; x < 16; ++x) set_ty(mb % W * 16 + x, mb / W * 16 + y, save[size_t(y) * 16 + x]);
     }
     if (best_c < 0) {  // the skip / direct motion with residual
       if (t == h264::kP) {

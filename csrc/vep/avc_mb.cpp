@@ -75,6 +75,9 @@ class MbLayer {
         scan4_(env.field ? kFieldScan4x4 : kZigzag4x4), scan8_(env.field ? kFieldScan8x8 : kZigzag8x8) {
     type_ = sh_.type();
     qp_ = sh_.qp;
+    bd_ = sps_.bit_depth_luma;
+    qpbd_ = 6 * (sps_.bit_depth_luma - 8);
+    qpbdc_ = 6 * (sps_.bit_depth_chroma - 8);
     weighted_ = (type_ == h264::kP && pps_.weighted_pred) || (type_ == h264::kB && pps_.weighted_bipred_idc != 0);
     implicit_ = type_ == h264::kB && pps_.weighted_bipred_idc == 2;
   }
@@ -135,7 +138,7 @@ class MbLayer {
     }
     s.kind = kSkip;
     s.skip = 1;
-    s.qp = u8(qp_);
+    s.qp = u8(qp_ + qpbd_);
     MbResidual res;
     res.luma = 0;
     res.chroma = 0;
@@ -211,15 +214,15 @@ class MbLayer {
     int qp = qp_;
     if ((cbp & 15) || (cbp >> 4) || s.kind == kI16x16) {
       const int dqp = read_qp_delta(kWrite ? want->qp_delta : 0);
-      VEP_CHECK(dqp >= -26 && dqp <= 25, "mb_qp_delta out of range");
-      qp = (qp + dqp + 52) % 52;
+      VEP_CHECK(dqp >= -(26 + qpbd_ / 2) && dqp <= 25 + qpbd_ / 2, "mb_qp_delta out of range");
+      qp = (qp + dqp + 52 + 2 * qpbd_) % (52 + qpbd_) - qpbd_;  // (7-37: QPY in -QpBdOffsetY..51)
       prev_qpd_nz = dqp != 0;
     } else {
       prev_qpd_nz = 0;
     }
     qp_ = qp;
-    s.qp = u8(qp);
-    residual(mb, s, res, cbp & 15, cbp >> 4, qp, intra);
+    s.qp = u8(qp + qpbd_);
+    residual(mb, s, res, cbp & 15, cbp >> 4, qp + qpbd_, intra);
     emit(mb, s, res, i16_mode, s.chroma_mode, nullptr);
   }
 
@@ -398,9 +401,13 @@ class MbLayer {
     s.cbf_cac[0] = s.cbf_cac[1] = 0xF;
     std::fill(std::begin(s.tc), std::end(s.tc), u8(16));
     for (auto& c : s.tcc) std::fill(std::begin(c), std::end(c), u8(16));
-    s.qp = u8(qp_);
+    s.qp = u8(qp_ + qpbd_);
     const u8* pcm;
     const size_t nb = mono() ? 256 : kPcmMbBytes;  // (4:0:0: luma samples only)
+    if (bd_ > 8) {  // High 10: bd-bit samples (u(v)), kept as u16 in the record
+      pcm_wide(mb, s, res, nb);
+      return;
+    }
     if constexpr (kWrite) {
       pcm = want->pcm;
       VEP_CHECK(pcm, "I_PCM macroblock without samples");
@@ -433,8 +440,50 @@ class MbLayer {
     emit(mb, s, res, 0, 0, pcm);
   }
 
+  // I_PCM above 8 bits: ns samples of bd_ bits (luma, then Cb, then Cr), byte-aligned at both
+  // ends (the sample block is bd_ * 48 bytes for 4:2:0, a whole number). want->pcm: u16 samples.
+  void pcm_wide(int mb, MbState& s, MbResidual& res, size_t ns) {
+    const size_t nbytes = ns * size_t(bd_) / 8;
+    if constexpr (kWrite) {
+      const u16* src = reinterpret_cast<const u16*>(want->pcm);
+      VEP_CHECK(src, "I_PCM macroblock without samples");
+      for (size_t i = 0; i < kPcmMbBytes; ++i) pcm16_[i] = i < ns ? src[i] : u16(1 << (bd_ - 1));
+      BitWriter w;
+      for (size_t i = 0; i < ns; ++i) w.u(bd_, pcm16_[i]);
+      VEP_CHECK(w.buf().size() == nbytes, "I_PCM sample block size");
+      if constexpr (kCabac) {
+        cenc->align_zero();
+        cenc->raw_bytes(w.buf().data(), nbytes);
+        cenc->start();
+      } else {
+        bw->align_zero();
+        bw->bytes(w.buf().data(), nbytes);
+      }
+    } else {
+      const u8* p;
+      if constexpr (kCabac) {
+        const size_t off = cabac->aligned_bytepos();
+        VEP_CHECK(off + nbytes <= data_n, "truncated I_PCM macroblock");
+        p = data + off;
+        cabac->start(off + nbytes);
+      } else {
+        br->align();
+        const size_t off = br->pos() >> 3;
+        VEP_CHECK(off + nbytes <= br->size(), "truncated I_PCM macroblock");
+        p = br->data() + off;
+        br->skip(nbytes * 8);
+      }
+      BitReader r(p, nbytes);
+      for (size_t i = 0; i < kPcmMbBytes; ++i) pcm16_[i] = i < ns ? u16(r.u(bd_)) : u16(1 << (bd_ - 1));
+    }
+    prev_qpd_nz = 0;
+    emit(mb, s, res, 0, 0, reinterpret_cast<const u8*>(pcm16_));
+  }
+
   bool mono() const { return sps_.chroma_format_idc == 0; }
   u8 pcm_mono_[kPcmMbBytes];
+  u16 pcm16_[kPcmMbBytes];
+  int bd_ = 8, qpbd_ = 0, qpbdc_ = 0;  // bit depth, QpBdOffsetY / C (High 10)
 
  public:
   const u8* data = nullptr;  // CABAC: slice RBSP (I_PCM samples are read in place)
@@ -913,8 +962,9 @@ class MbLayer {
       }
     }
     if (cbp_chroma) {
-      const int qpc[2] = {chroma_qp(qp, pps_.chroma_qp_index_offset),
-                          chroma_qp(qp, pps_.second_chroma_qp_index_offset)};
+      // (qp = QP'Y; QP'C = QPC + QpBdOffsetC, QPC from QPY, Table 8-15)
+      const int qpc[2] = {chroma_qp_bd(qp - qpbd_, pps_.chroma_qp_index_offset, qpbdc_) + qpbdc_,
+                          chroma_qp_bd(qp - qpbd_, pps_.second_chroma_qp_index_offset, qpbdc_) + qpbdc_};
       int dcv[2][4] = {};
       for (int c = 0; c < 2; ++c) {
         const int inc = kCabac ? cbf_dc_inc(mb, 1 + c, intra) : 0;
@@ -962,9 +1012,10 @@ class MbLayer {
   void emit(int mb, const MbState& s, const MbResidual& res, int i16_mode, int chroma_mode, const u8* pcm) {
     MbRec m{};
     m.kind = s.kind;
-    m.qp = s.kind == kIPcm ? 0 : s.qp;
-    m.qpc = u8(chroma_qp(m.qp, pps_.chroma_qp_index_offset));
-    m.qpc2 = u8(chroma_qp(m.qp, pps_.second_chroma_qp_index_offset));
+    // (biased by QpBdOffset: Picture::qp_bias / qpc_bias; I_PCM: QPY 0)
+    m.qp = u8(s.kind == kIPcm ? qpbd_ : s.qp);
+    m.qpc = u8(chroma_qp_bd(m.qp - qpbd_, pps_.chroma_qp_index_offset, qpbdc_) + qpbdc_);
+    m.qpc2 = u8(chroma_qp_bd(m.qp - qpbd_, pps_.second_chroma_qp_index_offset, qpbdc_) + qpbdc_);
     m.i16_mode = u8(i16_mode);
     m.chroma_mode = u8(chroma_mode);
     m.dbk = u8((sh_.disable_deblocking == 1 ? 1 : 0) | (sh_.disable_deblocking == 2 ? 2 : 0));
@@ -1085,8 +1136,13 @@ WpEntry wp_entry(const SliceEnv& env, int r0, int r1) {
       o1[c] = w.o[c];
     }
   }
-  for (int c = 0; c < 3; ++c)
+  // (offsets scaled to the sample depth, 8-301 / 8-304, before the bi-prediction average)
+  for (int c = 0; c < 3; ++c) {
+    const int sc = 1 << ((c == 0 ? env.sps->bit_depth_luma : env.sps->bit_depth_chroma) - 8);
+    o0[c] *= sc;
+    o1[c] *= sc;
     e.o[c] = i16(r0 >= 0 && r1 >= 0 ? (o0[c] + o1[c] + 1) >> 1 : (r0 >= 0 ? o0[c] : o1[c]));
+  }
   return e;
 }
 
@@ -1103,7 +1159,7 @@ void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, c
     const size_t start = (bitpos + 7) >> 3;  // cabac_alignment_one_bit
     VEP_CHECK(start <= n, "slice data overrun");
     cabac::Ctx ctx[kCabacCtx];
-    cabac_init_contexts(ctx, sh.type() == h264::kI ? -1 : 0, sh.qp);
+    cabac_init_contexts(ctx, sh.type() == h264::kI ? -1 : 0, std::max(0, sh.qp));  // (9-5: Clip3(0, 51, SliceQPY))
     cabac::Decoder dec(data, n, start);
     BinDecoder bd{dec, ctx};
     AvcBins<BinDecoder> bins{bd};
@@ -1168,7 +1224,7 @@ struct SliceWriter::Impl {
       : env(e), bw(w), dq(e.scaling), cabac(e.pps->cabac), is_i(e.sh->type() == h264::kI) {
     if (cabac) {
       while (!bw.byte_aligned()) bw.u1(1);  // cabac_alignment_one_bit
-      cabac_init_contexts(ctx, is_i ? -1 : 0, e.sh->qp);
+      cabac_init_contexts(ctx, is_i ? -1 : 0, std::max(0, e.sh->qp));
       enc = std::make_unique<cabac::Encoder>(bw.buf());
       be = std::make_unique<BinEncoder>(BinEncoder{*enc, ctx});
       bins = std::make_unique<AvcBins<BinEncoder>>(AvcBins<BinEncoder>{*be});

@@ -191,6 +191,10 @@ struct AvcDesc {
   VEP_DEV i16* res;            // device scratch: kAvcResSamples per intra MB with residual (MbRec::res
                        // slot; avc_inter_kernel -> avc_intra_kernel)
   VEP_DEV u64* prof;           // optional (VEP_AVC_PROF=1): kAvcProfSlots clock64() phase accumulators
+  i32 bd;              // sample bit depth: 8 (u8 surfaces), 9 / 10 (High 10: u16 surfaces,
+                       // slot_y / slot_uv in bytes; intra + deblocking in avc_hbd_kernel)
+  i32 qp_bias, qpc_bias;  // MbRec::qp / qpc bias (QpBdOffsetY / C)
+  i32 pad_;
   VEP_DEV u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
                        // tagged words per MB of every workgroup's last row (intra wavefront:
                        // words 0..7, zeroed by avc_inter_kernel; deblocking: all, zeroed by
@@ -236,6 +240,9 @@ void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
 // packed: bit 0 vertical edges with word / half-word LDS accesses (VEP_DBK_PACKED=0: a byte per
 // sample); bit 1 a wave sync after every edge instead of one per direction (VEP_DBK_SYNC=1)
 void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s, int packed = 1);
+// High 10 pictures of the round (AvcDesc::bd > 8; the 8-bit wavefronts skip them): intra
+// prediction, then (dbk: after launch_avc_bs) the loop filter. gpu_avc_hbd.hip
+void launch_avc_hbd(const AvcDesc* d_descs, int n, bool intra, bool dbk, hipStream_t s);
 
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
 

@@ -143,6 +143,92 @@ __device__ inline void luma8_residual(const i16* D, const MbRec& m, int lane, in
   wave_sync();
 }
 
+// Skip / inter / I_PCM MB of the inter kernel, whole wave, on u8 (8-bit) or u16 (High 10)
+// surfaces. D: the wave's dense coefficient buffer, T: its 8x8-transform buffer.
+template <class P>
+__device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int lane, int* T, i16* D, bool t8) {
+  const int x = lane & 15, y0 = lane >> 4;  // luma sample (x, y0 + 4k), block row k
+  const int W = d.wmbs, wpx = W * 16, hpx = d.hmbs * 16, pitch = wpx;
+  const int mx = mb % W, my = mb / W;
+  const int bd = sizeof(P) == 1 ? 8 : d.bd;
+  VEP_DEV P* ty = reinterpret_cast<VEP_DEV P*>(d.y + d.slot_y * u64(d.target));
+  VEP_DEV P* tuv = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
+  auto yref = [&](int s) { return reinterpret_cast<const VEP_DEV P*>(d.y + d.slot_y * u64(s)); };
+  auto uvref = [&](int s) { return reinterpret_cast<const VEP_DEV P*>(d.uv + d.slot_uv * u64(s)); };
+  if (m.kind == avc::kIPcm) {
+    const VEP_DEV P* s = reinterpret_cast<const VEP_DEV P*>(d.coefs + m.coef);  // (u16: 384 samples)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) ty[size_t(my * 16 + y0 + 4 * k) * pitch + mx * 16 + x] = s[(y0 + 4 * k) * 16 + x];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
+      tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = s[256 + t];
+    }
+    return;
+  }
+  const i16* mvb = d.mvs + size_t(m.mv);  // the MB's vectors (granularity: m.flags)
+  const bool l1 = (m.flags & avc::kMbL1) != 0;
+  const avc::WpEntry* wpp =
+      (m.flags & avc::kMbWp) ? static_cast<const avc::WpEntry*>(d.wps) + m.wp : nullptr;
+  int v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
+    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
+    int p0 = 0, p1 = 0;
+    if (s0 != 0xFF) {
+      const i16* v0 = mvb + avc::mv_sub(m.flags, 0, blk);
+      p0 = avc::luma_qpel(yref(s0), pitch, wpx, hpx, mx * 16 + x + (v0[0] >> 2),
+                          my * 16 + y + (v0[1] >> 2), v0[0] & 3, v0[1] & 3, bd);
+    }
+    if (s1 != 0xFF) {
+      const i16* v1 = mvb + avc::mv_sub(m.flags, 1, blk);
+      p1 = avc::luma_qpel(yref(s1), pitch, wpx, hpx, mx * 16 + x + (v1[0] >> 2),
+                          my * 16 + y + (v1[1] >> 2), v1[0] & 3, v1[1] & 3, bd);
+    }
+    v[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 0, bd);
+  }
+  if (m.luma_coded | m.chroma_coded) expand_coefs_wave(d, m, lane, D);  // (wave-uniform)
+  if (t8) luma8_residual(D, m, lane, T);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
+    int o = v[k];
+    if (t8) o += T[y * 16 + x];
+    else if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(D + 16 * blk, y & 3, x & 3);
+    ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = P(avc::clip1(o, bd));
+  }
+  int u[2];
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
+    const int r = (cy >> 1) * 4 + (cx >> 1), b8 = ((cy >> 2) << 1) | (cx >> 2);
+    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
+    int p0 = 0, p1 = 0;
+    if (s0 != 0xFF) {
+      const i16* v0 = mvb + avc::mv_sub(m.flags, 0, r);
+      const int vy = v0[1] + (d.field ? 2 * ((d.field == 2) - (s0 & 1)) : 0);  // opposite-parity field
+      p0 = avc::chroma_epel(uvref(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v0[0] >> 3),
+                            my * 8 + cy + (vy >> 3), v0[0] & 7, vy & 7);
+    }
+    if (s1 != 0xFF) {
+      const i16* v1 = mvb + avc::mv_sub(m.flags, 1, r);
+      const int vy = v1[1] + (d.field ? 2 * ((d.field == 2) - (s1 & 1)) : 0);
+      p1 = avc::chroma_epel(uvref(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v1[0] >> 3),
+                            my * 8 + cy + (vy >> 3), v1[0] & 7, vy & 7);
+    }
+    u[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 1 + cc, bd);
+  }
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
+    const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
+    int o = u[k];
+    if ((m.chroma_coded >> kb) & 1) o += avc::idct4x4_at(D + 256 + 16 * kb, cy & 3, cx & 3);
+    tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = P(avc::clip1(o, bd));
+  }
+}
+
 // One wave64 per MB, four MBs per workgroup: each lane reconstructs 4 luma samples (one per
 // 4x4-block row) and 2 chroma samples, so a lane has all of its reference loads in flight at
 // once and the picture lookup / record / MV loads are paid once per wave instead of per
@@ -196,83 +282,8 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     return;
   }
   if (m.kind != avc::kSkip && m.kind != avc::kInter && m.kind != avc::kIPcm) return;
-  const int W = d.wmbs, wpx = W * 16, hpx = d.hmbs * 16, pitch = wpx;
-  const int mx = mb % W, my = mb / W;
-  u8* ty = d.y + d.slot_y * u64(d.target);
-  u8* tuv = d.uv + d.slot_uv * u64(d.target);
-  if (m.kind == avc::kIPcm) {
-    const VEP_DEV u8* s = reinterpret_cast<const VEP_DEV u8*>(d.coefs + m.coef);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) ty[size_t(my * 16 + y0 + 4 * k) * pitch + mx * 16 + x] = s[(y0 + 4 * k) * 16 + x];
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-      tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = s[256 + t];
-    }
-    return;
-  }
-  const i16* mvb = d.mvs + size_t(m.mv);  // the MB's vectors (granularity: m.flags)
-  const bool l1 = (m.flags & avc::kMbL1) != 0;
-  const avc::WpEntry* wpp =
-      (m.flags & avc::kMbWp) ? static_cast<const avc::WpEntry*>(d.wps) + m.wp : nullptr;
-  int v[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
-    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
-    int p0 = 0, p1 = 0;
-    if (s0 != 0xFF) {
-      const i16* v0 = mvb + avc::mv_sub(m.flags, 0, blk);
-      p0 = avc::luma_qpel(d.y + d.slot_y * u64(s0), pitch, wpx, hpx, mx * 16 + x + (v0[0] >> 2),
-                          my * 16 + y + (v0[1] >> 2), v0[0] & 3, v0[1] & 3);
-    }
-    if (s1 != 0xFF) {
-      const i16* v1 = mvb + avc::mv_sub(m.flags, 1, blk);
-      p1 = avc::luma_qpel(d.y + d.slot_y * u64(s1), pitch, wpx, hpx, mx * 16 + x + (v1[0] >> 2),
-                          my * 16 + y + (v1[1] >> 2), v1[0] & 3, v1[1] & 3);
-    }
-    v[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 0);
-  }
-  i16* D = lcoef[wv];
-  if (m.luma_coded | m.chroma_coded) expand_coefs_wave(d, m, lane, D);  // (wave-uniform)
-  if (t8) luma8_residual(D, m, lane, T);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    const int y = y0 + 4 * k, blk = k * 4 + (x >> 2);
-    int o = v[k];
-    if (t8) o += T[y * 16 + x];
-    else if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(D + 16 * blk, y & 3, x & 3);
-    ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = u8(avc::clip1(o));
-  }
-  int u[2];
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-    const int r = (cy >> 1) * 4 + (cx >> 1), b8 = ((cy >> 2) << 1) | (cx >> 2);
-    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
-    int p0 = 0, p1 = 0;
-    if (s0 != 0xFF) {
-      const i16* v0 = mvb + avc::mv_sub(m.flags, 0, r);
-      const int vy = v0[1] + (d.field ? 2 * ((d.field == 2) - (s0 & 1)) : 0);  // opposite-parity field
-      p0 = avc::chroma_epel(d.uv + d.slot_uv * u64(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v0[0] >> 3),
-                            my * 8 + cy + (vy >> 3), v0[0] & 7, vy & 7);
-    }
-    if (s1 != 0xFF) {
-      const i16* v1 = mvb + avc::mv_sub(m.flags, 1, r);
-      const int vy = v1[1] + (d.field ? 2 * ((d.field == 2) - (s1 & 1)) : 0);
-      p1 = avc::chroma_epel(d.uv + d.slot_uv * u64(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v1[0] >> 3),
-                            my * 8 + cy + (vy >> 3), v1[0] & 7, vy & 7);
-    }
-    u[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 1 + cc);
-  }
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-    const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
-    int o = u[k];
-    if ((m.chroma_coded >> kb) & 1) o += avc::idct4x4_at(D + 256 + 16 * kb, cy & 3, cx & 3);
-    tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = u8(avc::clip1(o));
-  }
+  if (d.bd > 8) inter_mb<u16>(d, m, mb, lane, T, lcoef[wv], t8);
+  else inter_mb<u8>(d, m, mb, lane, T, lcoef[wv], t8);
 }
 
 // ---------------------------------------------------------------------- wavefront helpers
@@ -695,7 +706,8 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
   if (pic >= n) return;
   const AvcDesc d = descs[pic];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, g0 = grp * kIntraWaves;
-  if (g0 >= H) return;  // (uniform over the workgroup, before any barrier)
+  if (g0 >= H || d.bd > 8) return;  // (uniform over the workgroup, before any barrier; High 10:
+                                    // avc_hbd_kernel)
   __shared__ Sync sync;
   __shared__ IntraWave lds[kIntraWaves];
   __shared__ u32 tap_lut[9 * 16];  // Intra_4x4 tap word per (mode, y, x) of a 4x4 block
@@ -1147,7 +1159,8 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
   const AvcDesc d = descs[pic];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, pitch = W * 16;
   const int g0 = grp * kDbkRows;  // first row of this workgroup
-  if (g0 >= H) return;            // (uniform over the workgroup, before any barrier)
+  if (g0 >= H || d.bd > 8) return;  // (uniform over the workgroup, before any barrier; High 10:
+                                    // avc_hbd_kernel)
   __shared__ DbkSync sync;
   __shared__ DbkWave lds[kDbkWaves][2];
   __shared__ DbkXch xring[kDbkRows - 1][kDbkDepth];

@@ -364,8 +364,8 @@ std::vector<u8> write_sps(const Sps& s) {
   bw.ue(s.sps_id);
   if (s.profile_idc >= 100) {
     bw.ue(s.chroma_format_idc);  // 4:2:0, or 4:0:0 (monochrome)
-    bw.ue(0);   // bit_depth_luma_minus8
-    bw.ue(0);   // bit_depth_chroma_minus8
+    bw.ue(u32(s.bit_depth_luma - 8));    // (High 10: 2)
+    bw.ue(u32(s.bit_depth_chroma - 8));
     bw.u1(0);   // qpprime_y_zero_transform_bypass_flag
     bw.u1(s.scaling_matrix_present);
     if (s.scaling_matrix_present) {  // all eight lists explicit (delta-coded, §7.3.2.1.1.1)

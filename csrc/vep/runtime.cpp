@@ -867,7 +867,8 @@ void Worker::loop() {
   }
 }
 
-void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps, bool weave) {
+void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd, bool weave) {
+  const int bps = bd > 8 ? 2 : 1;
   const int wmbs = pi.coded_width / 16, hmbs = pi.coded_height / 16;
   auto& s = c.surface;
   // the 8-bit frame the conversion reads when the slot is not one (Main10; a woven field pair)
@@ -877,7 +878,7 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps
     s.y8 = static_cast<u8*>(dev_.alloc(y8));
     s.uv8 = static_cast<u8*>(dev_.alloc(y8 / 2));
   };
-  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && s.bps == bps && c.ring_ &&
+  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && s.bd == bd && c.ring_ &&
       c.ring_->width() == pi.width && c.ring_->height() == pi.height) {
     if (weave) scratch8();  // (only ever added: no batch in flight reads a missing scratch)
     return;
@@ -891,13 +892,14 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps
   s.hmbs = hmbs;
   s.slots = std::max(1, slots);
   s.bps = bps;
+  s.bd = bd;
   const size_t ysz = s.slot_y() * size_t(s.slots);
   if (dev_.gpu()) {
     s.y = static_cast<u8*>(dev_.alloc(ysz));
     s.uv = static_cast<u8*>(dev_.alloc(ysz / 2));
-    if (bps == 2) {  // Main10: u16 samples at 10-bit black / grey (a 10-bit CVS: HEVC only)
-      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.y), u16(16 << 2), ysz / 2, stream_));
-      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.uv), u16(128 << 2), ysz / 4, stream_));
+    if (bps == 2) {  // Main10 / High 10: u16 samples at the depth's black / grey
+      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.y), u16(16 << (bd - 8)), ysz / 2, stream_));
+      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.uv), u16(128 << (bd - 8)), ysz / 4, stream_));
       scratch8();
     } else {
       if (weave) scratch8();
@@ -908,7 +910,7 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps
     if (lanes_.size() > 1) VEP_HIP(hipStreamSynchronize(stream_));
   } else {
     s.host.assign(size_t(s.slots), HostSurface{});
-    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16, bps == 2 ? 10 : 8);
+    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16, bd);
   }
   c.set_ring(std::make_shared<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height));
 }
@@ -1028,7 +1030,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       if (have && (c.surface.wmbs * 16 != j.pic.coded_width ||
                    c.surface.hmbs * 16 != j.pic.coded_height || c.ring_->width() != j.pic.width ||
                    c.ring_->height() != j.pic.height || c.surface.slots < j.dpb_slots() ||
-                   c.surface.bps != j.bytes_per_sample()))
+                   c.surface.bd != j.bit_depth()))
         resize = true;
     }
   }
@@ -1039,7 +1041,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
     bool weave = jobs[i].out_fields;
     for (const auto& p : jobs[i].avc) weave |= p->structure != 0;
-    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bytes_per_sample(), weave);
+    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bit_depth(), weave);
     slots[i] = jobs[i].has_output() ? c.ring_->begin_write() : -1;
   }
 }
@@ -1543,6 +1545,10 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.res = reinterpret_cast<i16*>(st.d + a.off_res);
       g.xg = reinterpret_cast<u64*>(st.d + a.off_xg);
       g.prof = avc_prof_;
+      g.bd = a.p->bd;
+      g.qp_bias = a.p->qp_bias;
+      g.qpc_bias = a.p->qpc_bias;
+      VEP_CHECK(c->surface.bd == a.p->bd, "H.264: picture bit depth differs from the camera's surfaces");
       mbs += a.p->nmbs();
     }
   }
@@ -1657,20 +1663,22 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const auto* ad = reinterpret_cast<const gpu::AvcDesc*>(st.d + off_round[size_t(r)]);
     const int np = int(round_pics[size_t(r)].size());
     int mbs = 0;
-    bool intra = false, dbk = false;
+    bool intra = false, dbk = false, wide = false, narrow = false;
     int max_h = 0;
     for (int k : round_pics[size_t(r)]) {
       mbs += apics[size_t(k)].p->nmbs();
       max_h = std::max(max_h, apics[size_t(k)].p->hmbs);
       intra |= apics[size_t(k)].p->intra_mbs > 0;
       dbk |= apics[size_t(k)].p->deblock;
+      (apics[size_t(k)].p->bd > 8 ? wide : narrow) = true;
     }
     gpu::launch_avc_inter(ad, np, mbs, cs);
-    if (intra) gpu::launch_avc_intra(ad, np, max_h, cs);
+    if (intra && narrow) gpu::launch_avc_intra(ad, np, max_h, cs);
     if (dbk) {
       gpu::launch_avc_bs(ad, np, mbs, cs);
-      gpu::launch_avc_deblock(ad, np, max_h, cs, dbk_packed_);
+      if (narrow) gpu::launch_avc_deblock(ad, np, max_h, cs, dbk_packed_);
     }
+    if (wide) gpu::launch_avc_hbd(ad, np, intra, dbk, cs);  // (High 10 pictures)
   }
   for (int r = 0; r < hrounds; ++r) {
     const auto* hd2 = reinterpret_cast<const gpu::HevcDesc*>(st.d + off_hround[size_t(r)]);
@@ -1727,7 +1735,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     if (sf.bps != 2) continue;
     gpu::launch_narrow(reinterpret_cast<const u16*>(sf.y + tgt * sf.slot_y()),
                        reinterpret_cast<const u16*>(sf.uv + tgt * sf.slot_uv()), sf.y8, sf.uv8,
-                       size_t(sf.wmbs) * 16 * sf.hmbs * 16, j.hevc.empty() ? 10 : j.hevc.back()->bd_y, cs);
+                       size_t(sf.wmbs) * 16 * sf.hmbs * 16, sf.bd, cs);
   }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), nout, tiles,
                              cs);
@@ -1776,7 +1784,8 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
         auto& F = c.surface.fields;  // field slots (half-height surfaces)
         if (F.size() < size_t(pic->dpb_slots)) F.resize(size_t(pic->dpb_slots));
         for (auto& h : F)
-          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16) h.alloc(pic->wmbs * 16, pic->hmbs * 16);
+          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16 || h.bd != pic->bd)
+            h.alloc(pic->wmbs * 16, pic->hmbs * 16, pic->bd);
         avc::cpu_reconstruct(*pic, F);
       }
       for (const auto& pic : jobs[i].hevc) hevc::cpu_execute(*pic, c.surface.host);

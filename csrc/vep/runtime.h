@@ -131,7 +131,13 @@ struct DecodeJob {
   // (H.265: the DPB slots plus one scratch surface, the SAO input copy)
   int dpb_slots() const { return !avc.empty() ? avc.back()->dpb_slots : (!hevc.empty() ? hevc_slots + 1 : 1); }
   // bytes per sample of the camera's surfaces: 2 for Main10 pictures (u16 samples), else 1
-  int bytes_per_sample() const { return !hevc.empty() && hevc.back()->wide() ? 2 : 1; }
+  // (High 10 H.264 / Main10 H.265: u16 samples at the stream's bit depth)
+  int bit_depth() const {
+    if (!avc.empty()) return avc.back()->bd;
+    if (!hevc.empty()) return std::max(hevc.back()->bd_y, hevc.back()->bd_c);
+    return 8;
+  }
+  int bytes_per_sample() const { return bit_depth() > 8 ? 2 : 1; }
   int target() const { return general() ? out_slot : 0; }
 };
 
@@ -199,7 +205,8 @@ class Camera {
   struct Surface {
     int wmbs = 0, hmbs = 0;
     int slots = 1;                 // DPB surfaces (general H.264 path); slot k at y + k * bytes
-    int bps = 1;                   // bytes per sample: 2 = u16 samples (HEVC Main10)
+    int bps = 1;                   // bytes per sample: 2 = u16 samples (HEVC Main10, H.264 High 10)
+    int bd = 8;                    // sample bit depth
     u8* y = nullptr;
     u8* uv = nullptr;
     // bps 2: the 8-bit NV12 copy of the picture being published (what the BGR conversion and
@@ -422,7 +429,7 @@ class Worker {
     size_t err_cap = 0;
   };
   void loop();
-  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bps = 1, bool weave = false);
+  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd = 8, bool weave = false);
   struct Batch {
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;

@@ -128,6 +128,7 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
       hc.temporal_noise = cfg.temporal_noise;
       hc.interlaced = cfg.interlaced >= 1;
       hc.mono = cfg.mono;
+      hc.bit_depth = cfg.bit_depth;
       if (cfg.interlaced == 2) {
         hc.fields = true;
         hc.cabac = false;
