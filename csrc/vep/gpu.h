@@ -123,6 +123,11 @@ struct HevcDesc {
   u32 epoch;             // tag of this round's words (never 0)
   i32 npu, pu_begin;     // exclusive prefix of PUs over the round
   i32 blk_begin;         // exclusive prefix of 4x4 blocks over the round
+  // Polling backoff of a wave waiting on an edge word: it sleeps 256 cycles, then twice as long
+  // after every miss, up to nap_max x 256 cycles (1: a fixed 256-cycle poll). Waves far ahead of
+  // the wavefront then stop loading L2 with polls the producers' stores compete with.
+  u32 nap_max;
+  u32 pad_;
 };
 // Exchange words of a stride x h picture: luma columns (x % 4 == 3) and rows (y % 4 == 3), then
 // the same for Cb and Cr. 3/4 word per luma sample.

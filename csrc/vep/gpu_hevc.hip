@@ -169,7 +169,7 @@ __device__ inline void xg_put(u64* p, u32 epoch, u32 v) {
 __device__ inline u64 xg_get(const u64* p) {
   return __hip_atomic_load(const_cast<u64*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr u32 kXgSpinLimit = 1u << 18;  // x s_sleep 4: well under a second per wait
+constexpr u32 kXgSpinLimit = 1u << 18;  // polls (x at most nap_max x 256 cycles): a few seconds at most
 constexpr int kTuQueueWgs = 128;
 
 // Reference samples of an intra block with the 64 lanes of a wave (the parallel form of
@@ -215,13 +215,14 @@ __device__ void prepare_refs_wave(const HevcDesc& d, const GpuTu& t, const P* pl
       w = xg_get(wp);
       if (wp2 && u32(w >> 32) != d.epoch) w = xg_get(wp2);
     }
-    u32 spins = 0;
+    u32 spins = 0, nap = 1;
     while (__ballot(xq && u32(w >> 32) != d.epoch)) {
       if (++spins > kXgSpinLimit) {
         if (xq && u32(w >> 32) != d.epoch) atomicOr(d.err, 2u);  // (the frame is dropped)
         break;
       }
-      __builtin_amdgcn_s_sleep(4);
+      for (u32 z = 0; z < nap; ++z) __builtin_amdgcn_s_sleep(4);
+      nap = nap < d.nap_max ? 2 * nap : nap;  // (HevcDesc::nap_max: exponential backoff)
       if (xq && u32(w >> 32) != d.epoch) {
         w = xg_get(wp);
         if (wp2 && u32(w >> 32) != d.epoch) w = xg_get(wp2);

@@ -479,6 +479,8 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     hevc_tu_window_ = kDefaultTuWindow;
     if (const char* tq = std::getenv("VEP_HEVC_TU_QUEUE")) hevc_tu_window_ = tq[0] == '1' ? kAllLevels : 0;
     if (const char* tw = std::getenv("VEP_HEVC_TU_WINDOW")) hevc_tu_window_ = std::clamp(std::atoi(tw), -1, kAllLevels);
+    // (queue waits: longest polling nap, x 256 cycles; 1 = round 4's fixed poll)
+    if (const char* tn = std::getenv("VEP_HEVC_TU_NAP")) hevc_tu_nap_ = u32(std::clamp(std::atoi(tn), 1, 256));
     int ns = opt_.stages;
     if (ns <= 0) {
       const char* se = std::getenv("VEP_STAGES");
@@ -1617,6 +1619,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
         g.xg = hevc_tu_window_ == 0 ? nullptr : sf.hevc_xg;  // (per-level launches read the picture)
         g.xg_h = sf.hmbs * 16;
         g.epoch = sf.hevc_epoch;
+        g.nap_max = hevc_tu_nap_;
       }
       g.npu = int(p.pus.size());
       g.pu_begin = pus;

@@ -524,6 +524,7 @@ class Worker {
   // H.265 intra transform blocks: 0 = one launch per dependency level; k > 0 = one queue launch
   // per window of k consecutive levels (kAllLevels: the whole round in one launch)
   int hevc_tu_window_ = 0;
+  u32 hevc_tu_nap_ = 16;  // HevcDesc::nap_max (VEP_HEVC_TU_NAP)
   // lanes wait for a stage's batch by polling its event with sleeps (VEP_SPIN_WAIT=1:
   // hipEventSynchronize, which spins a core in the HSA runtime)
   bool polite_wait_ = true;
