@@ -661,7 +661,7 @@ PYBIND11_MODULE(_vep, m) {
   });
   rc.def("dequant4", [](int c, int qp, int i, int j) { return avc::dequant4x4(c, qp, i, j); });
   // top = p[-1..7, -1] (9, top-right already substituted), left = p[-1, 0..3]
-  rc.def("intra4x4", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode) {
+  rc.def("intra4x4", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode, int bd) {
     VEP_CHECK(top.size() == 9 && left.size() == 4, "9 top + 4 left samples");
     avc::Intra4Nb n{};
     for (int k = 0; k < 9; ++k) n.t[k] = top[size_t(k)];
@@ -670,23 +670,24 @@ PYBIND11_MODULE(_vep, m) {
     n.has_left = has_left;
     std::vector<int> r(16);
     for (int y = 0; y < 4; ++y)
-      for (int x = 0; x < 4; ++x) r[size_t(y * 4 + x)] = avc::intra4x4_pred(n, mode, x, y);
+      for (int x = 0; x < 4; ++x) r[size_t(y * 4 + x)] = avc::intra4x4_pred(n, mode, x, y, bd);
     return r;
-  });
+  }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("mode"), py::arg("bd") = 8);
   // top = p[-1..15, -1] (17, top-right substituted), left = p[-1, 0..7]: reference filtering +
   // prediction
   rc.def("intra8x8", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, bool has_tl,
-                        int mode) {
+                        int mode, int bd) {
     VEP_CHECK(top.size() == 17 && left.size() == 8, "17 top + 8 left samples");
     int f[25];
     avc::intra8x8_filter([&](int x) { return top[size_t(x + 1)]; }, [&](int y) { return left[size_t(y)]; },
                          has_top, has_left, has_tl, f);
     std::vector<int> r(64);
     for (int y = 0; y < 8; ++y)
-      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::intra8x8_pred(f, has_top, has_left, mode, x, y);
+      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::intra8x8_pred(f, has_top, has_left, mode, x, y, bd);
     return r;
-  });
-  rc.def("intra16x16", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode) {
+  }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("has_tl"), py::arg("mode"),
+     py::arg("bd") = 8);
+  rc.def("intra16x16", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode, int bd) {
     VEP_CHECK(top.size() == 17 && left.size() == 16, "17 top + 16 left samples");
     avc::Intra16Nb n{};
     for (int k = 0; k < 17; ++k) n.top[k] = top[size_t(k)];
@@ -694,13 +695,13 @@ PYBIND11_MODULE(_vep, m) {
     n.has_top = has_top;
     n.has_left = has_left;
     n.has_tl = has_top && has_left;
-    const avc::PredConst k = avc::intra16x16_const(n, mode);
+    const avc::PredConst k = avc::intra16x16_const(n, mode, bd);
     std::vector<int> r(256);
     for (int y = 0; y < 16; ++y)
-      for (int x = 0; x < 16; ++x) r[size_t(y * 16 + x)] = avc::intra16x16_pred(n, k, mode, x, y);
+      for (int x = 0; x < 16; ++x) r[size_t(y * 16 + x)] = avc::intra16x16_pred(n, k, mode, x, y, bd);
     return r;
-  });
-  rc.def("intra_chroma", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode) {
+  }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("mode"), py::arg("bd") = 8);
+  rc.def("intra_chroma", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode, int bd) {
     VEP_CHECK(top.size() == 9 && left.size() == 8, "9 top + 8 left samples");
     avc::IntraChromaNb n{};
     for (int k = 0; k < 9; ++k) n.top[k] = top[size_t(k)];
@@ -711,9 +712,9 @@ PYBIND11_MODULE(_vep, m) {
     const avc::PredConst k = mode == 3 ? avc::chroma_plane_const(n) : avc::PredConst{0, 0, 0, 0};
     std::vector<int> r(64);
     for (int y = 0; y < 8; ++y)
-      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::chroma_pred(n, k, mode, x, y);
+      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::chroma_pred(n, k, mode, x, y, bd);
     return r;
-  });
+  }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("mode"), py::arg("bd") = 8);
   rc.def("luma_qpel", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> plane, int xi, int yi,
                          int fx, int fy) {
     VEP_CHECK(plane.ndim() == 2, "2-D plane");
@@ -722,6 +723,19 @@ PYBIND11_MODULE(_vep, m) {
   });
   rc.def("chroma_epel", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> uv, int c, int xi,
                            int yi, int fx, int fy) {
+    VEP_CHECK(uv.ndim() == 2 && uv.shape(1) % 2 == 0, "interleaved UV plane");
+    const int h = int(uv.shape(0)), pitch = int(uv.shape(1));
+    return avc::chroma_epel(uv.data(), pitch, pitch / 2, h, c, xi, yi, fx, fy);
+  });
+  // High 10 planes: u16 samples at bit depth bd
+  rc.def("luma_qpel16", [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> plane, int xi, int yi,
+                           int fx, int fy, int bd) {
+    VEP_CHECK(plane.ndim() == 2, "2-D plane");
+    const int h = int(plane.shape(0)), w = int(plane.shape(1));
+    return avc::luma_qpel(plane.data(), w, w, h, xi, yi, fx, fy, bd);
+  });
+  rc.def("chroma_epel16", [](py::array_t<uint16_t, py::array::c_style | py::array::forcecast> uv, int c, int xi,
+                             int yi, int fx, int fy) {
     VEP_CHECK(uv.ndim() == 2 && uv.shape(1) % 2 == 0, "interleaved UV plane");
     const int h = int(uv.shape(0)), pitch = int(uv.shape(1));
     return avc::chroma_epel(uv.data(), pitch, pitch / 2, h, c, xi, yi, fx, fy);

@@ -13,8 +13,9 @@ def clip3(lo, hi, v):
     return lo if v < lo else hi if v > hi else v
 
 
-def clip1(v):
-    return clip3(0, 255, v)
+def clip1(v, bd=8):
+    """Clip1Y / Clip1C (5-3 / 5-4) at sample bit depth bd (High 10: 9 or 10)."""
+    return clip3(0, (1 << bd) - 1, v)
 
 
 # ------------------------------------------------------------------ 8.5.12.2 / 8.5.13.2
@@ -81,7 +82,7 @@ def dequant_4x4(c, qp, i, j):
 
 
 # ------------------------------------------------------------------ 8.3.1.2 Intra_4x4
-def intra_4x4(top, left, has_top, has_left, mode):
+def intra_4x4(top, left, has_top, has_left, mode, bd=8):
     """top = p[-1..7, -1] (top-right substituted), left = p[-1, 0..3]."""
     def P(x, y):
         return top[x + 1] if y == -1 else left[y]
@@ -103,7 +104,7 @@ def intra_4x4(top, left, has_top, has_left, mode):
                 elif has_top:
                     v = (st + 2) >> 2
                 else:
-                    v = 128
+                    v = 1 << (bd - 1)  # (8-51 etc.: 1 << (BitDepth - 1))
             elif mode == 3:
                 if x == 3 and y == 3:
                     v = (P(6, -1) + 3 * P(7, -1) + 2) >> 2
@@ -190,7 +191,7 @@ def filter_8x8_refs(top, left, has_top, has_left, has_tl):
     return t, lf
 
 
-def intra_8x8(top, left, has_top, has_left, has_tl, mode):
+def intra_8x8(top, left, has_top, has_left, has_tl, mode, bd=8):
     t, lf = filter_8x8_refs(top, left, has_top, has_left, has_tl)
 
     def P(x, y):
@@ -211,7 +212,7 @@ def intra_8x8(top, left, has_top, has_left, has_tl, mode):
                 elif has_top:
                     v = (sum(P(k, -1) for k in range(8)) + 4) >> 3
                 else:
-                    v = 128
+                    v = 1 << (bd - 1)  # (8-51 etc.: 1 << (BitDepth - 1))
             elif mode == 3:
                 if x == 7 and y == 7:
                     v = (P(14, -1) + 3 * P(15, -1) + 2) >> 2
@@ -264,7 +265,7 @@ def intra_8x8(top, left, has_top, has_left, has_tl, mode):
 
 
 # ------------------------------------------------------------------ 8.3.3 Intra_16x16
-def intra_16x16(top, left, has_top, has_left, mode):
+def intra_16x16(top, left, has_top, has_left, mode, bd=8):
     """top = p[-1..15, -1], left = p[-1, 0..15]."""
     def P(x, y):
         return top[x + 1] if y == -1 else left[y]
@@ -292,15 +293,15 @@ def intra_16x16(top, left, has_top, has_left, mode):
                 elif has_top:
                     v = (st + 8) >> 4
                 else:
-                    v = 128
+                    v = 1 << (bd - 1)  # (8-51 etc.: 1 << (BitDepth - 1))
             else:
-                v = clip1((a + b * (x - 7) + c * (y - 7) + 16) >> 5)
+                v = clip1((a + b * (x - 7) + c * (y - 7) + 16) >> 5, bd)
             out[y][x] = v
     return out
 
 
 # ------------------------------------------------------------------ 8.3.4 chroma (4:2:0)
-def intra_chroma(top, left, has_top, has_left, mode):
+def intra_chroma(top, left, has_top, has_left, mode, bd=8):
     """top = p[-1..7, -1], left = p[-1, 0..7]; mode: 0 DC, 1 horizontal, 2 vertical, 3 plane."""
     def P(x, y):
         return top[x + 1] if y == -1 else left[y]
@@ -320,23 +321,23 @@ def intra_chroma(top, left, has_top, has_left, mode):
                 sl = sum(P(-1, yo + k) for k in range(4))
                 if (xo, yo) in ((0, 0), (4, 4)):
                     v = (st + sl + 4) >> 3 if has_top and has_left else (sl + 2) >> 2 if has_left else \
-                        (st + 2) >> 2 if has_top else 128
+                        (st + 2) >> 2 if has_top else 1 << (bd - 1)
                 elif xo > 0:
-                    v = (st + 2) >> 2 if has_top else (sl + 2) >> 2 if has_left else 128
+                    v = (st + 2) >> 2 if has_top else (sl + 2) >> 2 if has_left else 1 << (bd - 1)
                 else:
-                    v = (sl + 2) >> 2 if has_left else (st + 2) >> 2 if has_top else 128
+                    v = (sl + 2) >> 2 if has_left else (st + 2) >> 2 if has_top else 1 << (bd - 1)
             elif mode == 1:
                 v = P(-1, y)
             elif mode == 2:
                 v = P(x, -1)
             else:
-                v = clip1((a + b * (x - 3) + c * (y - 3) + 16) >> 5)
+                v = clip1((a + b * (x - 3) + c * (y - 3) + 16) >> 5, bd)
             out[y][x] = v
     return out
 
 
 # ------------------------------------------------------------------ 8.4.2.2 interpolation
-def luma_sample(plane, xi, yi, fx, fy):
+def luma_sample(plane, xi, yi, fx, fy, bd=8):
     """8.4.2.2.1: plane = 2-D list/array of rows; (xi, yi) integer luma position, (fx, fy)
     quarter-sample fraction; reference positions are clamped into the picture."""
     h, w = len(plane), len(plane[0])
@@ -355,12 +356,12 @@ def luma_sample(plane, xi, yi, fx, fy):
 
     x, y = xi, yi
     Gs = G(x, y)
-    b = clip1((b1(x, y) + 16) >> 5)
-    hh = clip1((h1(x, y) + 16) >> 5)
-    s = clip1((b1(x, y + 1) + 16) >> 5)
-    m = clip1((h1(x + 1, y) + 16) >> 5)
+    b = clip1((b1(x, y) + 16) >> 5, bd)
+    hh = clip1((h1(x, y) + 16) >> 5, bd)
+    s = clip1((b1(x, y + 1) + 16) >> 5, bd)
+    m = clip1((h1(x + 1, y) + 16) >> 5, bd)
     j1 = tap(b1(x, y - 2), b1(x, y - 1), b1(x, y), b1(x, y + 1), b1(x, y + 2), b1(x, y + 3))
-    j = clip1((j1 + 512) >> 10)
+    j = clip1((j1 + 512) >> 10, bd)
     table = {
         (0, 0): Gs,
         (0, 1): (Gs + hh + 1) >> 1,             # d
@@ -405,14 +406,17 @@ TC0 = [[0, 0, 0]] * 17 + [
     [6, 8, 11], [6, 8, 13], [7, 10, 14], [8, 11, 16], [9, 12, 18], [10, 13, 20], [11, 15, 23], [13, 17, 25]]
 
 
-def edge_thresholds(qp_p, qp_q, off_a, off_b):
+def edge_thresholds(qp_p, qp_q, off_a, off_b, bd=8):
+    """8-324..8-328: alpha = alpha' * (1 << (BitDepth - 8)), beta and tC0 likewise; qp_p / qp_q
+    are QPY / QPC (negative above 8 bits), indexA / indexB clipped to 0..51."""
     qav = (qp_p + qp_q + 1) >> 1
     ia = clip3(0, 51, qav + off_a)
     ib = clip3(0, 51, qav + off_b)
-    return ALPHA[ia], BETA[ib], TC0[ia]
+    sc = 1 << (bd - 8)
+    return ALPHA[ia] * sc, BETA[ib] * sc, [t * sc for t in TC0[ia]]
 
 
-def filter_line(p, q, bs, alpha, beta, tc0, chroma):
+def filter_line(p, q, bs, alpha, beta, tc0, chroma, bd=8):
     """8.7.2.3 (bS < 4) / 8.7.2.4 (bS = 4) on one line: p = [p0..p3], q = [q0..q3]."""
     p, q = list(p), list(q)
     p0, p1, p2, p3 = p
@@ -424,8 +428,8 @@ def filter_line(p, q, bs, alpha, beta, tc0, chroma):
     if bs < 4:
         tc = tc0 + 1 if chroma else tc0 + (1 if ap < beta else 0) + (1 if aq < beta else 0)
         delta = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3)
-        p[0] = clip1(p0 + delta)
-        q[0] = clip1(q0 - delta)
+        p[0] = clip1(p0 + delta, bd)
+        q[0] = clip1(q0 - delta, bd)
         if not chroma:
             if ap < beta:
                 p[1] = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1)
@@ -446,3 +450,21 @@ def filter_line(p, q, bs, alpha, beta, tc0, chroma):
     else:
         q[0] = (2 * q1 + q0 + p1 + 2) >> 2
     return p, q
+
+
+# ------------------------------------------------------------------ 8.5.8 / Table 8-15
+QPC_TABLE = {30: 29, 31: 30, 32: 31, 33: 32, 34: 32, 35: 33, 36: 34, 37: 34, 38: 35, 39: 35, 40: 36, 41: 36,
+             42: 37, 43: 37, 44: 37, 45: 38, 46: 38, 47: 38, 48: 39, 49: 39, 50: 39, 51: 39}
+
+
+def chroma_qp(qpy, offset, bd_c=8):
+    """QPC from QPY: qPI = Clip3(-QpBdOffsetC, 51, QPY + qPOffset) (8-313), Table 8-15."""
+    qpi = clip3(-6 * (bd_c - 8), 51, qpy + offset)
+    return qpi if qpi < 30 else QPC_TABLE[qpi]
+
+
+def mb_qp(prev_qpy, mb_qp_delta, bd=8):
+    """QPY of a macroblock (7-37): ((QPY,PRED + mb_qp_delta + 52 + 2 * QpBdOffsetY) %
+    (52 + QpBdOffsetY)) - QpBdOffsetY."""
+    off = 6 * (bd - 8)
+    return ((prev_qpy + mb_qp_delta + 52 + 2 * off) % (52 + off)) - off
