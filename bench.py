@@ -89,7 +89,8 @@ def parse_args():
                     help="h264 main/high: 1 = interlaced SPS coding frame pictures, 2 = every frame a field "
                          "pair (PAFF: CAVLC I/P fields, 4x4 transforms, no B pictures); fps counts frames")
     ap.add_argument("--bit-depth", type=int, choices=[8, 10], default=8,
-                    help="h265: 10 = Main10 streams (u16 surfaces on the GPU, narrowed to 8 bits for BGR24)")
+                    help="10: H.265 Main10 / H.264 High 10 (main / high profiles, progressive) streams (u16 "
+                         "surfaces on the GPU, narrowed to 8 bits for BGR24)")
     ap.add_argument("--threads", type=int, default=0,
                     help="host parse threads per rank (0 = the rank's host domain: its part of the CPU "
                          "budget - 1, pinned to its GPU's NUMA-local CPUs)")
@@ -271,7 +272,8 @@ def describe_streams(a, compressed):
         return (f"{a.profile.capitalize()} profile interlaced, every frame a field pair (PAFF), CAVLC "
                 f"I/P{'/B' if a.bframes else ''} fields{f', {a.bframes} B pairs per mini-GOP' if a.bframes else ''}")
     if compressed:
-        return (f"{a.profile.capitalize()} profile {'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
+        return (f"{'High 10' if a.bit_depth == 10 and a.profile != 'baseline' else a.profile.capitalize()} profile "
+                f"{'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
                 f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"
                 f"{', 8x8 transform + Intra_8x8' if a.profile == 'high' else ''}")
     return "I_PCM/P_Skip fast path"
@@ -283,7 +285,7 @@ def make_cfg(vep, a, rank, compressed):
     cfg.codec = a.codec
     cfg.seed = 1 + rank * 100003
     cfg.slices = a.slices
-    cfg.bit_depth = a.bit_depth if a.codec == "h265" else 8
+    cfg.bit_depth = a.bit_depth if (a.codec == "h265" or (a.profile != "baseline" and a.interlaced == 0)) else 8
     if compressed:
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
