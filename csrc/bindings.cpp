@@ -29,17 +29,18 @@ static py::bytes to_bytes(const u8* p, size_t n) {
   return py::bytes(reinterpret_cast<const char*>(p), n);
 }
 
-// (y, uv) coded NV12 planes of a surface: uint8, or uint16 for high bit depth (HEVC Main10)
+// (y, uv) coded NV12 planes of a surface: uint8, or uint16 for high bit depth (HEVC Main10,
+// H.264 High 10); 4:2:2 (NV16): the uv plane has coded_h rows
 static py::tuple surface_planes(const HostSurface& p) {
   if (p.wide()) {
     py::array_t<uint16_t> y({p.coded_h, p.coded_w});
-    py::array_t<uint16_t> uv({p.coded_h / 2, p.coded_w});
+    py::array_t<uint16_t> uv({p.chroma_rows(), p.coded_w});
     std::memcpy(y.mutable_data(), p.y16.data(), p.y16.size() * 2);
     std::memcpy(uv.mutable_data(), p.uv16.data(), p.uv16.size() * 2);
     return py::make_tuple(y, uv);
   }
   py::array_t<uint8_t> y({p.coded_h, p.coded_w});
-  py::array_t<uint8_t> uv({p.coded_h / 2, p.coded_w});
+  py::array_t<uint8_t> uv({p.chroma_rows(), p.coded_w});
   std::memcpy(y.mutable_data(), p.y.data(), p.y.size());
   std::memcpy(uv.mutable_data(), p.uv.data(), p.uv.size());
   return py::make_tuple(y, uv);
@@ -168,8 +169,8 @@ struct CpuDecoder {
         done = nal >= au.nals.size();
         if (slots.size() < size_t(pic->dpb_slots)) slots.resize(size_t(pic->dpb_slots));
         for (auto& h : slots)
-          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16 || h.bd != pic->bd)
-            h.alloc(pic->wmbs * 16, pic->hmbs * 16, pic->bd);
+          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16 || h.bd != pic->bd || h.cf != pic->cf)
+            h.alloc(pic->wmbs * 16, pic->hmbs * 16, pic->bd, pic->cf);
         avc::cpu_reconstruct(*pic, slots);
         coded = pic->info.coded_mbs;
         pictures.push_back(pic->info);
@@ -213,19 +214,7 @@ struct CpuDecoder {
     py::list l;
     for (const auto& f : fs) {
       const HostSurface& s = frame_of(f);
-      if (s.wide()) {  // High 10: u16 planes
-        py::array_t<uint16_t> y({s.coded_h, s.coded_w});
-        py::array_t<uint16_t> uv({s.coded_h / 2, s.coded_w});
-        std::memcpy(y.mutable_data(), s.y16.data(), s.y16.size() * 2);
-        std::memcpy(uv.mutable_data(), s.uv16.data(), s.uv16.size() * 2);
-        l.append(py::make_tuple(f.au.pts, py::make_tuple(y, uv)));
-        continue;
-      }
-      py::array_t<uint8_t> y({s.coded_h, s.coded_w});
-      py::array_t<uint8_t> uv({s.coded_h / 2, s.coded_w});
-      std::memcpy(y.mutable_data(), s.y.data(), s.y.size());
-      std::memcpy(uv.mutable_data(), s.uv.data(), s.uv.size());
-      l.append(py::make_tuple(f.au.pts, py::make_tuple(y, uv)));
+      l.append(py::make_tuple(f.au.pts, surface_planes(s)));
     }
     return l;
   }
@@ -380,6 +369,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("refs", &avc::AvcHighConfig::refs)
       .def_readwrite("qp", &avc::AvcHighConfig::qp)
       .def_readwrite("bit_depth", &avc::AvcHighConfig::bit_depth)
+      .def_readwrite("chroma_format", &avc::AvcHighConfig::chroma_format)
       .def_readwrite("cabac", &avc::AvcHighConfig::cabac)
       .def_readwrite("t8x8", &avc::AvcHighConfig::t8x8)
       .def_readwrite("weighted_p", &avc::AvcHighConfig::weighted_p)

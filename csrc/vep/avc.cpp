@@ -53,7 +53,7 @@ int MbNeighbours::nc_luma(int mb, int blk) const {
   return 0;
 }
 
-int MbNeighbours::nc_chroma(int mb, int c, int blk) const {
+int MbNeighbours::nc_chroma(int mb, int c, int blk, int nbc) const {
   const int bx = blk & 1, by = blk >> 1;
   auto count = [&](int m, int b) {
     const MbState& s = st_[size_t(m)];
@@ -65,7 +65,7 @@ int MbNeighbours::nc_chroma(int mb, int c, int blk) const {
   const int am = bx > 0 ? mb : mb_at(mb, -1, 0);
   if (am >= 0) na = count(am, bx > 0 ? blk - 1 : blk + 1);
   const int bm = by > 0 ? mb : mb_at(mb, 0, -1);
-  if (bm >= 0) nb = count(bm, by > 0 ? blk - 2 : blk + 2);
+  if (bm >= 0) nb = count(bm, by > 0 ? blk - 2 : blk + nbc - 2);  // (above MB: its bottom row of blocks)
   if (na >= 0 && nb >= 0) return (na + nb + 1) >> 1;
   if (na >= 0) return na;
   if (nb >= 0) return nb;
@@ -181,8 +181,8 @@ namespace {
 // Stream features outside the supported subset (progressive 8-bit 4:2:0, no lossless).
 void check_sps_supported(const Sps& s) {
   // (High 10: 9 / 10-bit samples, one depth for luma and chroma: the surfaces hold one)
-  if ((s.chroma_format_idc != 1 && s.chroma_format_idc != 0) || s.bit_depth_luma > 10 ||
-      s.bit_depth_chroma != s.bit_depth_luma)
+  // (4:2:2: High 4:2:2, 8..10 bits, progressive)
+  if (s.chroma_format_idc > 2 || s.bit_depth_luma > 10 || s.bit_depth_chroma != s.bit_depth_luma)
     throw UnsupportedStream("only 8-bit 4:2:0 / 4:0:0 H.264 is supported");
   // Interlaced SPS (frame_mbs_only_flag 0): frame pictures decode as progressive ones (frame
   // macroblocks, frame POC = min(top, bottom)); field pictures as half-height pictures in field
@@ -1411,8 +1411,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       ++redundant_slices_skipped;
       continue;
     }
-    if (sh.field_pic && sps.bit_depth_luma > 8)
-      throw UnsupportedStream("H.264 High 10 field pictures are not supported (progressive only)");
+    if (sh.field_pic && (sps.bit_depth_luma > 8 || sps.chroma_format_idc == 2))
+      throw UnsupportedStream("H.264 High 10 / 4:2:2 field pictures are not supported (progressive only)");
     if (!got) {
       first = sh;
       act_sps = &sps;
@@ -1425,8 +1425,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       if (!second_field) close_pair(*pic);  // an unpaired field leaves before this picture
       if (sh.idr() && !second_field) {
         hard_flush = slots != dpb_slots_ || W != wmbs_ || H != hmbs_ || sh.field_pic != field_mode_ ||
-                     sps.bit_depth_luma != bd_;
+                     sps.bit_depth_luma != bd_ || (sps.chroma_format_idc == 2) != (cf_ == 2);
         bd_ = sps.bit_depth_luma;
+        cf_ = sps.chroma_format_idc == 2 ? 2 : 1;
         field_mode_ = sh.field_pic;
         have_idr_ = true;
         dpb_slots_ = slots;
@@ -1437,7 +1438,8 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
         if (!have_idr_) throw Error("vep: H.264 stream does not start with an IDR picture");
         // a non-IDR picture may not change the picture size or the DPB (a mid-GOP SPS that
         // does would make earlier pictures of a batch write outside the surfaces)
-        VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_ && sps.bit_depth_luma == bd_,
+        VEP_CHECK(slots == dpb_slots_ && W == wmbs_ && H == hmbs_ && sps.bit_depth_luma == bd_ &&
+                      (sps.chroma_format_idc == 2) == (cf_ == 2),
                   "SPS changed without an IDR picture");
         if (sh.field_pic != field_mode_)
           throw UnsupportedStream("interlaced H.264: frame and field pictures mixed in one IDR period are not supported");
@@ -1460,6 +1462,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       pic->dpb_slots = field_mode_ ? 2 * dpb_slots_ : dpb_slots_;
       pic->structure = sh.field_pic ? 1 + int(sh.bottom_field) : 0;
       pic->bd = sps.bit_depth_luma;
+      pic->cf = sps.chroma_format_idc == 2 ? 2 : 1;
       pic->qp_bias = 6 * (sps.bit_depth_luma - 8);
       pic->qpc_bias = 6 * (sps.bit_depth_chroma - 8);
       pic->second_field = second_field;
@@ -1573,6 +1576,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       sh.constrained_intra = pic->constrained_intra;
       sh.poc = pic->poc;
       sh.bd = pic->bd;
+      sh.cf = pic->cf;
       sh.qp_bias = pic->qp_bias;
       sh.qpc_bias = pic->qpc_bias;
       u.colb.col = col_target;
@@ -1732,10 +1736,12 @@ void Decoder::parse_slice_data(MbNeighbours& nb, Picture& pic, const SliceHdr& s
 static inline void validate_mb(const Picture& p, const MbRec& m, bool written = false) {
   const size_t ncoef = p.coefs.size(), nmv = p.mvs.size();
   VEP_CHECK(m.kind <= kI8x8, "macroblock kind out of range");
+  VEP_CHECK(p.cf == 2 || m.chroma_coded < 0x100, "chroma block mask out of range");
   VEP_CHECK(m.qp <= 51 + p.qp_bias && m.qpc <= 51 + p.qpc_bias && m.qpc2 <= 51 + p.qpc_bias,
             "macroblock QP out of range");
   if (m.kind == kIPcm) {
-    VEP_CHECK(size_t(m.coef) + (p.bd > 8 ? kPcmMbBytes : kPcmMbBytes / 2) <= ncoef, "I_PCM samples outside the pool");
+    const size_t ns = p.cf == 2 ? size_t(kPcmMaxSamples) : size_t(kPcmMbBytes);
+    VEP_CHECK(size_t(m.coef) + (p.bd > 8 ? ns : ns / 2) <= ncoef, "I_PCM samples outside the pool");
     return;
   }
   // sparse groups: the mask words, then as many values as they announce, inside the pool
@@ -1871,7 +1877,7 @@ P* uvplane(HostSurface& s) {
 // (P: u8 surfaces, or u16 at bit depth bd, High 10)
 template <class P>
 void predict_inter_t(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
-                     const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure, int bd) {
+                     const WpEntry* wp, int mx, int my, int* py, int (*pc)[128], int structure, int bd) {
   // field pictures: slot parity = field parity; a vector into the opposite-parity field is offset
   // by a quarter chroma sample vertically (Table 8-10: 2 * (bottom_cur - bottom_ref) eighths)
   auto cy_off = [&](int slot) { return structure ? 2 * ((structure == 2) - (slot & 1)) : 0; };
@@ -1889,21 +1895,22 @@ void predict_inter_t(const std::vector<HostSurface>& slots, const MbRec& m, cons
                        my * 16 + y + (mv1[2 * r + 1] >> 2), mv1[2 * r] & 3, mv1[2 * r + 1] & 3, bd);
       py[y * 16 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 0, bd);
     }
+  // chroma: 8x8 (4:2:0) or 8x16 (4:2:2, full-height chroma: chroma row y is luma row y)
+  const int cf = slots[0].cf, ch = cf == 2 ? 16 : 8, chp = cf == 2 ? hpx : hpx / 2;
   for (int c = 0; c < 2; ++c)
-    for (int y = 0; y < 8; ++y)
+    for (int y = 0; y < ch; ++y)
       for (int x = 0; x < 8; ++x) {
-        const int r = (y >> 1) * 4 + (x >> 1), b8 = ((y >> 2) << 1) | (x >> 2);
+        const int ly = cf == 2 ? y : 2 * y;  // luma row of the sample
+        const int r = (ly >> 2) * 4 + (x >> 1), b8 = ((ly >> 3) << 1) | (x >> 2);
         const int s0 = m.ref[b8], s1 = mv1 ? m.ref1[b8] : 0xFF;
-        int p0 = 0, p1 = 0;
+        int p0 = 0, p1 = 0, ix, fx, iy, fy;
         if (s0 != 0xFF) {
-          const int vy = mv0[2 * r + 1] + cy_off(s0);
-          p0 = chroma_epel(uvplane<P>(slots[size_t(s0)]), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv0[2 * r] >> 3),
-                           my * 8 + y + (vy >> 3), mv0[2 * r] & 7, vy & 7);
+          chroma_mv(mv0[2 * r], mv0[2 * r + 1] + cy_off(s0), cf, ix, fx, iy, fy);
+          p0 = chroma_epel(uvplane<P>(slots[size_t(s0)]), pitch, wpx / 2, chp, c, mx * 8 + x + ix, my * ch + y + iy, fx, fy);
         }
         if (s1 != 0xFF) {
-          const int vy = mv1[2 * r + 1] + cy_off(s1);
-          p1 = chroma_epel(uvplane<P>(slots[size_t(s1)]), pitch, wpx / 2, hpx / 2, c, mx * 8 + x + (mv1[2 * r] >> 3),
-                           my * 8 + y + (vy >> 3), mv1[2 * r] & 7, vy & 7);
+          chroma_mv(mv1[2 * r], mv1[2 * r + 1] + cy_off(s1), cf, ix, fx, iy, fy);
+          p1 = chroma_epel(uvplane<P>(slots[size_t(s1)]), pitch, wpx / 2, chp, c, mx * 8 + x + ix, my * ch + y + iy, fx, fy);
         }
         pc[c][y * 8 + x] = wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wp ? wp + b8 : nullptr, 1 + c, bd);
       }
@@ -1911,7 +1918,7 @@ void predict_inter_t(const std::vector<HostSurface>& slots, const MbRec& m, cons
 }  // namespace
 
 void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
-                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure) {
+                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[128], int structure) {
   if (slots[0].wide()) predict_inter_t<u16>(slots, m, mv0, mv1, wp, mx, my, py, pc, structure, slots[0].bd);
   else predict_inter_t<u8>(slots, m, mv0, mv1, wp, mx, my, py, pc, structure, 8);
 }
@@ -2053,8 +2060,9 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   m.chroma_coded = 0;
   if (m.kind == kIPcm) {
     VEP_CHECK(pcm, "I_PCM macroblock without samples");
-    // (8-bit: 384 sample bytes; High 10: `pcm` holds 384 u16 samples)
-    const size_t o = pic.coefs.size(), nb = pic.bd > 8 ? 2 * kPcmMbBytes : kPcmMbBytes;
+    // (8-bit: sample bytes; High 10: u16 samples; 384 samples, 4:2:2 512)
+    const size_t ns = pic.cf == 2 ? size_t(kPcmMaxSamples) : size_t(kPcmMbBytes);
+    const size_t o = pic.coefs.size(), nb = pic.bd > 8 ? 2 * ns : ns;
     pic.coefs.resize(o + nb / 2);
     std::memcpy(pic.coefs.data() + o, pcm, nb);
   } else if (res && (res->luma | res->chroma)) {
@@ -2062,7 +2070,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
     m.chroma_coded = res->chroma;
     if (res->t8) m.flags |= kMbT8x8;
     // sparse groups (avc_recon.h): the mask words, then the non-zero values
-    const i16* grp[24];
+    const i16* grp[32];  // (16 luma + 16 chroma groups in 4:2:2)
     int ng = 0;
     if (res->t8) {
       for (int q = 0; q < 4; ++q)
@@ -2072,7 +2080,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
       for (u32 w = res->luma; w; w &= w - 1) grp[ng++] = res->blk[__builtin_ctz(w)];
     }
     for (u32 w = res->chroma; w; w &= w - 1) grp[ng++] = res->blk[16 + __builtin_ctz(w)];
-    u16 mask[24];
+    u16 mask[32];
     int nv = 0;
     for (int g = 0; g < ng; ++g) {
       mask[g] = nonzero_mask16(grp[g]);
@@ -2155,8 +2163,8 @@ const i16* luma_res(const i16* dense, const MbRec& m, int r) {
   return dense + 16 * r;
 }
 
-const i16* chroma_res(const i16* dense, const MbRec& m, int c, int b) {
-  const int k = c * 4 + b;
+const i16* chroma_res(const i16* dense, const MbRec& m, int c, int b, int nbc) {
+  const int k = c * nbc + b;
   if (!((m.chroma_coded >> k) & 1)) return nullptr;
   return dense + 256 + 16 * k;
 }
@@ -2190,6 +2198,7 @@ struct Recon {
   std::vector<HostSurface>& slots;
   HostSurface& T;
   int pitch, wpx, hpx, bd;
+  int cf, ch, nbc;  // chroma format, chroma MB height (8 / 16), chroma 4x4 blocks per component
   i16 dense[kDenseCoefs];  // the current MB's coefficients (load())
 
   void load(const MbRec& m) {
@@ -2200,15 +2209,15 @@ struct Recon {
   P& C(int x, int y, int c) { return uvplane<P>(T)[size_t(y) * pitch + 2 * x + c]; }
   P px(int v) const { return P(clip1(v, bd)); }
 
-  void chroma_store(const MbRec& m, int mx, int my, int c, const int* pred /*8x8*/) {
-    for (int b = 0; b < 4; ++b) {
-      const i16* d = chroma_res(dense, m, c, b);
+  void chroma_store(const MbRec& m, int mx, int my, int c, const int* pred /*8 x ch*/) {
+    for (int b = 0; b < nbc; ++b) {
+      const i16* d = chroma_res(dense, m, c, b, nbc);
       int res[16] = {};
       if (d) idct4x4(d, res);
       const int bx = (b & 1) * 4, by = (b >> 1) * 4;
       for (int i = 0; i < 4; ++i)
         for (int j = 0; j < 4; ++j)
-          C(mx * 8 + bx + j, my * 8 + by + i, c) = px(pred[(by + i) * 8 + bx + j] + res[i * 4 + j]);
+          C(mx * 8 + bx + j, my * ch + by + i, c) = px(pred[(by + i) * 8 + bx + j] + res[i * 4 + j]);
     }
   }
 
@@ -2224,7 +2233,7 @@ struct Recon {
     const i16* mv0 = e[0];
     const i16* mv1 = (m.flags & kMbL1) ? e[1] : nullptr;
     const WpEntry* wp = (m.flags & kMbWp) ? &pic.wps[m.wp] : nullptr;
-    int py[256], pc[2][64], res[256];
+    int py[256], pc[2][128], res[256];
     predict_inter_t<P>(slots, m, mv0, mv1, wp, mx, my, py, pc, pic.structure, bd);
     luma_residual(dense, m, res);
     for (int y = 0; y < 16; ++y)
@@ -2232,23 +2241,23 @@ struct Recon {
     for (int c = 0; c < 2; ++c) chroma_store(m, mx, my, c, pc[c]);
   }
 
-  void pcm(const MbRec& m, int mx, int my) {  // (u8 surfaces: 384 sample bytes; u16: 384 samples)
+  void pcm(const MbRec& m, int mx, int my) {  // (u8 surfaces: sample bytes; u16: samples; 384 / 4:2:2 512)
     const P* s = reinterpret_cast<const P*>(pic.coefs.data() + m.coef);
     for (int y = 0; y < 16; ++y)
       for (int x = 0; x < 16; ++x) Y(mx * 16 + x, my * 16 + y) = s[y * 16 + x];
     for (int c = 0; c < 2; ++c)
-      for (int y = 0; y < 8; ++y)
-        for (int x = 0; x < 8; ++x) C(mx * 8 + x, my * 8 + y, c) = s[256 + c * 64 + y * 8 + x];
+      for (int y = 0; y < ch; ++y)
+        for (int x = 0; x < 8; ++x) C(mx * 8 + x, my * ch + y, c) = s[256 + c * 8 * ch + y * 8 + x];
   }
 
   void intra_chroma(const MbRec& m, int mb, int mx, int my) {
     for (int c = 0; c < 2; ++c) {
       IntraChromaNb n;
       chroma_neighbours(pic, mb, c, T, n);
-      const PredConst k = m.chroma_mode == 3 ? chroma_plane_const(n) : PredConst{0, 0, 0, 0};
-      int cp[64];
-      for (int y = 0; y < 8; ++y)
-        for (int x = 0; x < 8; ++x) cp[y * 8 + x] = chroma_pred(n, k, m.chroma_mode, x, y, bd);
+      const PredConst k = m.chroma_mode == 3 ? chroma_plane_const(n, cf) : PredConst{0, 0, 0, 0};
+      int cp[128];
+      for (int y = 0; y < ch; ++y)
+        for (int x = 0; x < 8; ++x) cp[y * 8 + x] = chroma_pred(n, k, m.chroma_mode, x, y, bd, cf);
       chroma_store(m, mx, my, c, cp);
     }
   }
@@ -2365,11 +2374,10 @@ void chroma_neighbours(const Picture& pic, int mb, int c, const HostSurface& T, 
   n.has_left = intra_avail(pic, m, mx - 1, my);
   n.has_top = intra_avail(pic, m, mx, my - 1);
   n.has_tl = intra_avail(pic, m, mx - 1, my - 1);
-  n.top[0] = n.has_tl ? P(mx * 8 - 1, my * 8 - 1) : 128;
-  for (int k = 0; k < 8; ++k) {
-    n.top[k + 1] = n.has_top ? P(mx * 8 + k, my * 8 - 1) : 128;
-    n.left[k] = n.has_left ? P(mx * 8 - 1, my * 8 + k) : 128;
-  }
+  const int ch = T.cf == 2 ? 16 : 8;  // chroma MB height (4:2:2: 16 rows)
+  n.top[0] = n.has_tl ? P(mx * 8 - 1, my * ch - 1) : 128;
+  for (int k = 0; k < 8; ++k) n.top[k + 1] = n.has_top ? P(mx * 8 + k, my * ch - 1) : 128;
+  for (int k = 0; k < ch; ++k) n.left[k] = n.has_left ? P(mx * 8 - 1, my * ch + k) : 128;
 }
 
 namespace {
@@ -2377,7 +2385,7 @@ template <class P>
 void reconstruct_mb_t(const Picture& pic, int mb, std::vector<HostSurface>& slots) {
   HostSurface& T = slots[size_t(pic.target)];
   const int wpx = pic.wmbs * 16, hpx = pic.hmbs * 16;
-  Recon<P> r{pic, slots, T, wpx, wpx, hpx, T.wide() ? T.bd : 8, {}};
+  Recon<P> r{pic, slots, T, wpx, wpx, hpx, T.wide() ? T.bd : 8, T.cf, T.cf == 2 ? 16 : 8, T.cf == 2 ? 8 : 4, {}};
   const MbRec& m = pic.mbs[size_t(mb)];
   r.load(m);
   const int mx = mb % pic.wmbs, my = mb / pic.wmbs;
@@ -2412,6 +2420,7 @@ void deblock_t(const Picture& pic, HostSurface& T) {
   static const i16 kZeroMv[64] = {};
   const int W = pic.wmbs, pitch = T.coded_w, bd = T.wide() ? T.bd : 8;
   const int qb = pic.qp_bias, qcb = pic.qpc_bias;
+  const bool cf2 = T.cf == 2;
   P* Yp = yplane<P>(T);
   P* UV = uvplane<P>(T);
   auto mvs = [&](const MbRec& r) { return is_intra(r.kind) ? kZeroMv : &pic.mvs[size_t(r.mv)]; };
@@ -2427,7 +2436,12 @@ void deblock_t(const Picture& pic, HostSurface& T) {
         if (e == 0 && !(dir == 0 ? left : top)) continue;
         const MbRec& p = e > 0 ? q : pic.mbs[size_t(dir == 0 ? mb - 1 : mb - W)];
         const i16* mp = mvs(p);
-        if ((e & 1) && (q.flags & kMbT8x8)) continue;  // no 4x4 edges inside 8x8 transform blocks
+        // luma: no 4x4 edges inside 8x8 transform blocks; chroma (4x4 transforms): the edges at
+        // chroma samples 0 and 4 (luma edges 0 and 2), and in 4:2:2 every horizontal edge (chroma
+        // rows 0, 4, 8, 12 = luma rows: the odd ones also inside luma 8x8 transform blocks)
+        const bool luma_edge = !((e & 1) && (q.flags & kMbT8x8));
+        const bool chroma_edge = cf2 ? (dir == 1 || !(e & 1)) : !(e & 1);
+        if (!luma_edge && !chroma_edge) continue;
         const EdgeParams ep = edge_params(p.qp - qb, q.qp - qb, q.alpha_off, q.beta_off, bd);
         const EdgeParams epcs[2] = {edge_params(p.qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off, bd),
                                     edge_params(p.qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off, bd)};
@@ -2437,21 +2451,25 @@ void deblock_t(const Picture& pic, HostSurface& T) {
           const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
           bs[k] = boundary_strength(p, bp, mp, q, bq, mq, e == 0, pic.structure != 0, dir == 0);
         }
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < 16 && luma_edge; ++k) {
           if (!bs[k]) continue;
           if (dir == 0) filter_line(Yp + size_t(my * 16 + k) * pitch + mx * 16 + 4 * e, 1, bs[k], ep, false, bd);
           else filter_line(Yp + size_t(my * 16 + 4 * e) * pitch + mx * 16 + k, long(pitch), bs[k], ep, false, bd);
         }
-        if (e & 1) continue;  // chroma edges at chroma sample 0 and 4 (luma edges 0 and 2)
+        if (!chroma_edge) continue;
+        const int ch = cf2 ? 16 : 8;  // chroma MB height
         for (int c = 0; c < 2; ++c)
-          for (int k = 0; k < 8; ++k) {
+          for (int k = 0; k < (dir == 0 ? ch : 8); ++k) {
             const EdgeParams& epc = epcs[c];
-            const int b = bs[2 * k];
+            // bS of the luma line through the chroma line: vertical edges row k (4:2:0: 2k),
+            // horizontal edges column 2k
+            const int b = bs[dir == 0 && cf2 ? k : 2 * k];
             if (!b) continue;
             if (dir == 0)
-              filter_line(UV + size_t(my * 8 + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, b, epc, true, bd);
-            else
-              filter_line(UV + size_t(my * 8 + 2 * e) * pitch + (mx * 8 + k) * 2 + c, long(pitch), b, epc, true, bd);
+              filter_line(UV + size_t(my * ch + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, b, epc, true, bd);
+            else  // (chroma row of edge e: 4:2:0 2e, 4:2:2 4e)
+              filter_line(UV + size_t(my * ch + (cf2 ? 4 : 2) * e) * pitch + (mx * 8 + k) * 2 + c, long(pitch), b,
+                          epc, true, bd);
           }
       }
     }
@@ -2482,7 +2500,8 @@ void weave_fields(const HostSurface& top, const HostSurface& bottom, HostSurface
 void cpu_reconstruct(const Picture& pic, std::vector<HostSurface>& slots) {
   VEP_CHECK(pic.target >= 0 && pic.target < int(slots.size()), "target slot out of range");
   HostSurface& T = slots[size_t(pic.target)];
-  VEP_CHECK(T.coded_w == pic.wmbs * 16 && T.coded_h == pic.hmbs * 16 && T.bd == pic.bd, "surface size mismatch");
+  VEP_CHECK(T.coded_w == pic.wmbs * 16 && T.coded_h == pic.hmbs * 16 && T.bd == pic.bd && T.cf == pic.cf,
+            "surface size mismatch");
   for (int mb = 0; mb < pic.nmbs(); ++mb) cpu_reconstruct_mb(pic, mb, slots);
   if (pic.deblock) cpu_deblock(pic, T);
 }

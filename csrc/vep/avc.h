@@ -79,6 +79,7 @@ struct Picture {
   // records: MbRec::qp = QPY + QpBdOffsetY, MbRec::qpc / qpc2 = QPC + QpBdOffsetC (QPY / QPC may
   // be negative above 8 bits); the loop filter subtracts them.
   int bd = 8, qp_bias = 0, qpc_bias = 0;
+  int cf = 1;  // chroma_format_idc: 0 / 1 NV12 surfaces, 2 (4:2:2) NV16 (full-height chroma plane)
   bool second_field = false;  // completes a field pair (frame counters count these, not first fields)
   bool constrained_intra = false;
   int intra_mbs = 0;          // I4x4 / I8x8 / I16x16 MBs (need the wavefront pass)
@@ -158,12 +159,12 @@ struct MbState {
   u16 slice = 0;
   u16 cbf = 0;       // coded_block_flag of the luma 4x4 blocks (raster)
   u8 cbf_dc = 0;     // bit 0 luma DC (Intra16x16), bits 1-2 Cb / Cr DC
-  u8 cbf_cac[2] = {0, 0};  // chroma AC blocks (raster 2x2) per component
+  u8 cbf_cac[2] = {0, 0};  // chroma AC blocks (raster, 2 wide: 2x2 in 4:2:0, 2x4 in 4:2:2) per component
   i8 ref[2][4] = {{-1, -1, -1, -1}, {-1, -1, -1, -1}};  // refIdx per list per 8x8 (-1: unused)
   i16 mv[2][16][2] = {};
   u8 mvd[2][16][2] = {};  // min(|mvd|, 127) per 4x4 (CABAC mvd context)
   u8 tc[16] = {};     // CAVLC luma total_coeff (raster)
-  u8 tcc[2][4] = {};  // CAVLC chroma AC total_coeff per component (raster 2x2)
+  u8 tcc[2][8] = {};  // CAVLC chroma AC total_coeff per component (raster, 2 wide)
   u8 i4[16] = {};     // Intra4x4PredMode (raster; Intra8x8PredMode replicated over its 4 blocks)
 };
 
@@ -192,7 +193,7 @@ class MbNeighbours {
   int announced_count() const { return announced_; }  // distinct MBs announced this picture
   // nC for luma block (raster) `blk` / chroma component c block `blk` (§9.2.1).
   int nc_luma(int mb, int blk) const;
-  int nc_chroma(int mb, int c, int blk) const;
+  int nc_chroma(int mb, int c, int blk, int nbc = 4) const;  // nbc: chroma 4x4 blocks per component
   // predIntra4x4PredMode for raster block `blk` (also predIntra8x8PredMode with blk = the
   // 8x8's top-left 4x4 block and n8 = true: §8.3.2.1's neighbour block choice).
   int pred_intra4x4(int mb, int blk, bool constrained_intra) const;
@@ -419,6 +420,7 @@ class Decoder {
   int dpb_slots_ = 2;
   int wmbs_ = 0, hmbs_ = 0;  // active picture size (changes only at an IDR)
   int bd_ = 8;               // active sample bit depth (changes only at an IDR)
+  int cf_ = 1;               // active chroma format (2: 4:2:2; changes only at an IDR)
   bool have_idr_ = false;
   int pinned_slot_ = -1;    // newest output: kept until a newer one leaves the reorder buffer
   int last_out_poc_ = 0;
@@ -502,10 +504,10 @@ struct MbLevels {
 };
 // Dequantised residual blocks of one MB (16 luma raster, 4 Cb, 4 Cr) and their coded masks.
 struct MbResidual {
-  i16 blk[24][16];  // 16 luma 4x4 (raster), 4 Cb, 4 Cr
+  i16 blk[32][16];  // 16 luma 4x4 (raster), then chroma block k at 16 + k (MbRec::chroma_coded order)
   i16 b8[4][64];    // 8x8-transform luma blocks (raster 8x8 in each; t8 MBs)
   u16 luma = 0;     // coded luma 4x4 blocks (t8: all four blocks of each coded 8x8)
-  u8 chroma = 0;
+  u16 chroma = 0;
   bool t8 = false;
 };
 void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual& out);
@@ -619,6 +621,7 @@ struct AvcHighConfig {
   bool mono = false;          // 4:0:0 (monochrome, High profile): luma only, chroma decodes grey
   int bit_depth = 8;          // 9 / 10: High 10 profile (u16 samples; frame pictures only); qp may
                               // then go down to -6 * (bit_depth - 8)
+  int chroma_format = 1;      // 2: 4:2:2 (High 4:2:2 profile; frame pictures, 8..10 bits)
   int objects = 3;
   double noise = 3.0, temporal_noise = 0.0;
   u64 seed = 1;

@@ -226,8 +226,9 @@ struct AvcBins {
     } else {
       const int sig_base = 105 + kSigCatOff[cat], last_base = 166 + kSigCatOff[cat];
       const bool cdc = cat == kCatChromaDc;
+      const int dsh = n == 8 ? 1 : 0;  // chroma DC: ctxIdxInc = Min(i / NumC8x8, 2) (4:2:2: NumC8x8 2)
       for (; i < n - 1; ++i) {
-        const int si = cdc ? (i < 2 ? i : 2) : i;
+        const int si = cdc ? ((i >> dsh) < 2 ? (i >> dsh) : 2) : i;
         if (bin(sig_base + si, E::kWrite && coef[i] != 0)) {
           nzpos[num++] = u8(i);
           if (bin(last_base + si, i == last_nz)) break;
@@ -284,8 +285,9 @@ inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef,
     cabac::Ctx* const sig = ctx + 105 + kSigCatOff[cat];
     cabac::Ctx* const last = ctx + 166 + kSigCatOff[cat];
     if (cat == kCatChromaDc) {
+      const int dsh = n == 8 ? 1 : 0;  // Min(i / NumC8x8, 2): 4:2:2 has NumC8x8 = 2
       for (; i < n - 1; ++i) {
-        const int si = i < 2 ? i : 2;
+        const int si = (i >> dsh) < 2 ? (i >> dsh) : 2;
         if (d.decision(sig[si])) {
           nzpos[num++] = u8(i);
           if (d.decision(last[si])) break;

@@ -36,6 +36,12 @@ const u8 kCtBits[4][4 * 17] = {
 const u8 kCdcLen[4 * 5] = {2, 0, 0, 0, 6, 1, 0, 0, 6, 6, 3, 0, 6, 7, 7, 6, 6, 8, 8, 7};
 const u8 kCdcBits[4 * 5] = {1, 0, 0, 0, 7, 1, 0, 0, 4, 6, 1, 0, 3, 3, 2, 5, 2, 3, 2, 0};
 
+// nC == -2 (chroma DC, 4:2:2: up to 8 coefficients), index total_coeff * 4 + trailing_ones.
+const u8 kCdc422Len[4 * 9] = {1, 0, 0, 0, 7, 2, 0, 0, 7, 7, 3, 0, 9, 7, 7, 5, 9, 9, 7, 6,
+                              10, 10, 9, 7, 11, 11, 10, 7, 12, 12, 11, 10, 13, 12, 12, 11};
+const u8 kCdc422Bits[4 * 9] = {1, 0, 0, 0, 15, 1, 0, 0, 14, 13, 1, 0, 7, 12, 11, 1, 6, 5, 10, 1,
+                               7, 6, 4, 9, 7, 6, 5, 8, 7, 6, 5, 4, 7, 5, 4, 4};
+
 // Tables 9-7 / 9-8: total_zeros for 4x4 blocks, [total_coeff - 1][total_zeros].
 const u8 kTzLen[15][16] = {{1, 3, 3, 4, 4, 5, 5, 6, 6, 7, 7, 8, 8, 9, 9, 9},
                            {3, 3, 3, 3, 3, 4, 4, 4, 4, 5, 5, 6, 6, 6, 6},
@@ -70,6 +76,11 @@ const u8 kTzBits[15][16] = {{1, 3, 2, 3, 2, 3, 2, 3, 2, 3, 2, 3, 2, 3, 2, 1},
 // Table 9-9a: total_zeros for chroma DC 2x2, [total_coeff - 1][total_zeros].
 const u8 kTzDcLen[3][4] = {{1, 2, 3, 3}, {1, 2, 2, 0}, {1, 1, 0, 0}};
 const u8 kTzDcBits[3][4] = {{1, 1, 1, 0}, {1, 1, 0, 0}, {1, 0, 0, 0}};
+// Table 9-9b: total_zeros for chroma DC 2x4 (4:2:2), [total_coeff - 1][total_zeros].
+const u8 kTzDc422Len[7][8] = {{1, 3, 3, 4, 4, 4, 5, 5}, {3, 2, 3, 3, 3, 3, 3}, {3, 3, 2, 2, 3, 3},
+                              {3, 2, 2, 2, 3}, {2, 2, 2, 2}, {2, 2, 1}, {1, 1}};
+const u8 kTzDc422Bits[7][8] = {{1, 2, 3, 2, 3, 1, 1, 0}, {0, 1, 1, 4, 5, 6, 7}, {0, 1, 1, 2, 6, 7},
+                               {6, 0, 1, 2, 7}, {0, 1, 2, 3}, {0, 1, 1}, {0, 1}};
 // Table 9-10: run_before, [min(zeros_left, 7) - 1][run_before].
 const u8 kRunLen[7][16] = {{1, 1},          {1, 2, 2},       {2, 2, 2, 2},
                            {2, 2, 2, 3, 3}, {2, 2, 3, 3, 3, 3}, {2, 3, 3, 3, 3, 3, 3},
@@ -101,8 +112,8 @@ struct Lut {
 };
 
 struct Tables {
-  Lut ct[5];     // coeff_token classes 0-2 and 4 (class 3 is a 6-bit FLC)
-  Lut tz[15], tzdc[3], run[7];
+  Lut ct[6];     // coeff_token classes 0-2, 4 and 5 (class 3 is a 6-bit FLC)
+  Lut tz[15], tzdc[3], tzdc422[7], run[7];
   Tables() {
     const int maxlen[3] = {16, 14, 10};
     for (int c = 0; c < 3; ++c) {
@@ -111,6 +122,12 @@ struct Tables {
     }
     ct[4].init(8);
     for (int i = 0; i < 4 * 5; ++i) ct[4].add(kCdcLen[i], kCdcBits[i], i);
+    ct[5].init(13);
+    for (int i = 0; i < 4 * 9; ++i) ct[5].add(kCdc422Len[i], kCdc422Bits[i], i);
+    for (int t = 0; t < 7; ++t) {
+      tzdc422[t].init(5);
+      for (int z = 0; z < 8 - t; ++z) tzdc422[t].add(kTzDc422Len[t][z], kTzDc422Bits[t][z], z);
+    }
     for (int t = 0; t < 15; ++t) {
       tz[t].init(9);
       for (int z = 0; z < 16 - t; ++z) tz[t].add(kTzLen[t][z], kTzBits[t][z], z);
@@ -144,8 +161,10 @@ CoeffToken read_coeff_token(Bits& br, int cls) {
   return {v >> 2, v & 3};
 }
 
-int read_total_zeros(Bits& br, int tc, bool chroma_dc) {
-  return chroma_dc ? tables().tzdc[tc - 1].read(br) : tables().tz[tc - 1].read(br);
+int read_total_zeros(Bits& br, int tc, int max_coeff) {
+  if (max_coeff == 4) return tables().tzdc[tc - 1].read(br);
+  if (max_coeff == 8) return tables().tzdc422[tc - 1].read(br);
+  return tables().tz[tc - 1].read(br);
 }
 
 int read_run_before(Bits& br, int zeros_left) {
@@ -169,6 +188,8 @@ int write_residual_block(BitWriter& bw, int nc, int max_coeff, const int* coeff)
     bw.u(6, total == 0 ? 3u : u32(((total - 1) << 2) | t1));
   } else if (cls == 4) {
     bw.u(kCdcLen[total * 4 + t1], kCdcBits[total * 4 + t1]);
+  } else if (cls == 5) {
+    bw.u(kCdc422Len[total * 4 + t1], kCdc422Bits[total * 4 + t1]);
   } else {
     bw.u(kCtLen[cls][total * 4 + t1], kCtBits[cls][total * 4 + t1]);
   }
@@ -206,6 +227,7 @@ int write_residual_block(BitWriter& bw, int nc, int max_coeff, const int* coeff)
   const int zeros = pos[0] + 1 - total;
   if (total < max_coeff) {
     if (max_coeff == 4) bw.u(kTzDcLen[total - 1][zeros], kTzDcBits[total - 1][zeros]);
+    else if (max_coeff == 8) bw.u(kTzDc422Len[total - 1][zeros], kTzDc422Bits[total - 1][zeros]);
     else bw.u(kTzLen[total - 1][zeros], kTzBits[total - 1][zeros]);
   }
   int left = zeros;

@@ -69,9 +69,10 @@ inline constexpr u8 kCbpInter[48] = {0,  16, 1,  2,  4,  8,  32, 3,  5,  10, 12,
                                      14, 6,  9,  31, 35, 37, 42, 44, 33, 34, 36, 40, 39, 43, 45, 46,
                                      17, 18, 20, 24, 19, 21, 26, 28, 23, 27, 29, 30, 22, 25, 38, 41};
 
-// coeff_token class: 0..3 for nC ranges [0,2) [2,4) [4,8) [8,inf), 4 for chroma DC (nC = -1).
+// coeff_token class: 0..3 for nC ranges [0,2) [2,4) [4,8) [8,inf), 4 for chroma DC 4:2:0
+// (nC = -1), 5 for chroma DC 4:2:2 (nC = -2).
 inline int coeff_token_class(int nc) {
-  return nc < 0 ? 4 : nc < 2 ? 0 : nc < 4 ? 1 : nc < 8 ? 2 : 3;
+  return nc == -2 ? 5 : nc < 0 ? 4 : nc < 2 ? 0 : nc < 4 ? 1 : nc < 8 ? 2 : 3;
 }
 
 struct CoeffToken {
@@ -79,7 +80,8 @@ struct CoeffToken {
 };
 
 CoeffToken read_coeff_token(Bits& br, int cls);
-int read_total_zeros(Bits& br, int total_coeff, bool chroma_dc);
+// max_coeff 4 / 8: the chroma DC tables of 4:2:0 (Table 9-9a) / 4:2:2 (Table 9-9b)
+int read_total_zeros(Bits& br, int total_coeff, int max_coeff);
 int read_run_before(Bits& br, int zeros_left);
 
 // Parse one residual_block_cavlc (§7.3.5.3.3), handing every nonzero coefficient to
@@ -112,7 +114,7 @@ inline int read_residual_block_cb(Bits& br, int nc, int max_coeff, Put&& put) {
     if (a > (3 << (suffix_len - 1)) && suffix_len < 6) ++suffix_len;
   }
   int left = 0;
-  if (t.total < max_coeff) left = read_total_zeros(br, t.total, max_coeff == 4);
+  if (t.total < max_coeff) left = read_total_zeros(br, t.total, max_coeff);
   VEP_CHECK(t.total + left <= max_coeff, "total_zeros out of range");
   // levels arrive highest frequency first: walk scan positions downwards from the last one
   int pos = t.total + left - 1;

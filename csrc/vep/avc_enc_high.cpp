@@ -145,6 +145,7 @@ struct AvcHighEncoder::Impl {
   HostSurface field_src;
   int pair_slot = -1, pair_fn = 0;
   int bd = 8, qpbd = 0;  // sample bit depth, QpBdOffset (High 10)
+  int cf = 1;            // chroma format (2: 4:2:2)
   const u8* scan4 = kZigzag4x4;  // 4x4 level scan of the current picture (field pictures: field scan)
   const u8* scan8 = kZigzag8x8;
 
@@ -156,6 +157,9 @@ struct AvcHighEncoder::Impl {
               "bit_depth 8..10 (High 10: frame pictures)");
     bd = c.bit_depth;
     qpbd = 6 * (bd - 8);
+    VEP_CHECK(c.chroma_format == 1 || (c.chroma_format == 2 && !c.fields && !c.mono),
+              "chroma_format 1 or 2 (4:2:2: frame pictures, not 4:0:0)");
+    cf = c.chroma_format;
     VEP_CHECK(c.qp >= -qpbd && c.qp <= 51 && c.gop >= 1, "bad encoder config");
     VEP_CHECK(!c.fields || (c.interlaced && !c.cabac), "field coding: interlaced CAVLC only");
     fields = c.fields;
@@ -164,8 +168,8 @@ struct AvcHighEncoder::Impl {
     if (c.interlaced) H = (H + 1) & ~1;  // (frame height in MB pairs: map units of 2 MB rows)
     wpx = W * 16;
     hpx = H * 16;
-    sps.profile_idc = bd > 8 ? 110 : (c.t8x8 || c.scaling || c.mono) ? 100 : 77;
-    sps.chroma_format_idc = c.mono ? 0 : 1;
+    sps.profile_idc = cf == 2 ? 122 : bd > 8 ? 110 : (c.t8x8 || c.scaling || c.mono) ? 100 : 77;
+    sps.chroma_format_idc = c.mono ? 0 : cf;
     sps.bit_depth_luma = sps.bit_depth_chroma = bd;
     VEP_CHECK(!c.mono || (!c.weighted_p && c.weighted_b != 1), "4:0:0 encoder: explicit weighted prediction is not emitted");
     sps.constraint_flags = 0;
@@ -210,7 +214,7 @@ struct AvcHighEncoder::Impl {
     nal(h264::write_pps(pps), pps_nal);
     ph = fields ? hpx / 2 : hpx;
     slots.resize((size_t(sps.max_num_ref_frames) + 2) * (fields ? 2 : 1));
-    for (auto& s : slots) s.alloc(wpx, ph, bd);
+    for (auto& s : slots) s.alloc(wpx, ph, bd, cf);
     scene.make(SceneConfig{c.width, c.height, wpx, hpx, c.objects, c.noise, c.temporal_noise, c.seed}, rng);
   }
 
@@ -222,13 +226,29 @@ struct AvcHighEncoder::Impl {
       if (rendered > 0) scene.advance();
       scene.render();
       scene.add_sensor_noise(rendered);
-      if (bd > 8) {  // High 10 source: the 8-bit scene << 2 plus a position / time dither in the low bits
+      if (bd > 8 || cf == 2) {
+        // High 10 source: the 8-bit scene << 2 plus a position / time dither in the low bits;
+        // 4:2:2: the scene's chroma rows interpolated to full height
         HostSurface& w = sources[rendered];
-        w.alloc(scene.src.coded_w, scene.src.coded_h, bd);
+        const HostSurface& s8 = scene.src;
+        w.alloc(s8.coded_w, s8.coded_h, bd, cf);
         const int sh = bd - 8;
-        auto lo = [&](size_t i) { return u16(u16((i * 2654435761u + u64(rendered) * 40503u) >> 29) & ((1u << sh) - 1)); };
-        for (size_t i = 0; i < w.y16.size(); ++i) w.y16[i] = u16(scene.src.y[i] << sh | lo(i));
-        for (size_t i = 0; i < w.uv16.size(); ++i) w.uv16[i] = u16(scene.src.uv[i] << sh | lo(i + 7));
+        auto lo = [&](size_t i) {
+          return sh ? int(u16((i * 2654435761u + u64(rendered) * 40503u) >> 29) & ((1u << sh) - 1)) : 0;
+        };
+        const size_t cw = size_t(s8.coded_w), crows = size_t(s8.coded_h / 2);
+        for (size_t i = 0; i < size_t(s8.coded_w) * size_t(s8.coded_h); ++i) w.set(0, int(i % cw), int(i / cw), s8.y[i] << sh | lo(i));
+        for (size_t r = 0; r < size_t(w.chroma_rows()); ++r)
+          for (size_t x = 0; x < cw; ++x) {
+            int v;
+            if (cf == 2) {
+              const size_t r0 = r >> 1, r1 = std::min(crows - 1, r0 + (r & 1));
+              v = (s8.uv[r0 * cw + x] + s8.uv[r1 * cw + x] + 1) >> 1;
+            } else {
+              v = s8.uv[r * cw + x];
+            }
+            w.set(1 + int(x & 1), int(x >> 1), int(r), v << sh | lo(r * cw + x + 7));
+          }
       } else {
         sources[rendered] = scene.src;
       }
@@ -940,7 +960,7 @@ struct AvcHighEncoder::Impl {
 
   // Luma / chroma residual levels of a prediction into `d` (t8: 8x8 transform), cbp returned.
   // (qp = QP'Y = QPY + QpBdOffsetY)
-  int code_residual(int mb, const int* py, const int (*pc)[64], bool intra, bool t8, bool i16, int qp, MbDesc& d) {
+  int code_residual(int mb, const int* py, const int (*pc)[128], bool intra, bool t8, bool i16, int qp, MbDesc& d) {
     const int mx = mb % W, my = mb / W;
     int cl = 0;
     if (t8) {
@@ -995,14 +1015,15 @@ struct AvcHighEncoder::Impl {
     int cc = 0;
     const int qpc[2] = {chroma_qp_bd(qp - qpbd, pps.chroma_qp_index_offset, qpbd) + qpbd,
                         chroma_qp_bd(qp - qpbd, pps.second_chroma_qp_index_offset, qpbd) + qpbd};
+    const int nbc = cf == 2 ? 8 : 4, ch = cf == 2 ? 16 : 8;  // chroma 4x4 blocks / MB height
     for (int c = 0; c < (cfg.mono ? 0 : 2); ++c) {  // (4:0:0: no chroma residual)
-      int cw[4];
-      for (int b = 0; b < 4; ++b) {
+      int cw[8];
+      for (int b = 0; b < nbc; ++b) {
         const int bx = (b & 1) * 4, by = (b >> 1) * 4;
         int x[16], w[16];
         for (int i = 0; i < 4; ++i)
           for (int j = 0; j < 4; ++j)
-            x[i * 4 + j] = SC(mx * 8 + bx + j, my * 8 + by + i, c) - pc[c][(by + i) * 8 + bx + j];
+            x[i * 4 + j] = SC(mx * 8 + bx + j, my * ch + by + i, c) - pc[c][(by + i) * 8 + bx + j];
         fwd4x4(x, w);
         cw[b] = w[0];
         for (int k = 1; k < 16; ++k) {
@@ -1010,6 +1031,27 @@ struct AvcHighEncoder::Impl {
           d.cac[c][b][k - 1] = quant(w[pos], qpc[c], mf_class(pos), intra);
           if (d.cac[c][b][k - 1]) cc = 2;
         }
+      }
+      if (cf == 2) {  // 2x4 DC: the decoder's transform (self-inverse up to scale), levels at QP'C + 3,
+                      // in the 4:2:2 chroma DC scan order
+        int f[8];
+        for (int x = 0; x < 2; ++x) {
+          const int c0 = cw[x], c1 = cw[2 + x], c2 = cw[4 + x], c3 = cw[6 + x];
+          f[x] = c0 + c1 + c2 + c3;
+          f[2 + x] = c0 + c1 - c2 - c3;
+          f[4 + x] = c0 - c1 - c2 + c3;
+          f[6 + x] = c0 - c1 + c2 - c3;
+        }
+        for (int y = 0; y < 4; ++y) {
+          const int a = f[2 * y], b = f[2 * y + 1];
+          f[2 * y] = a + b;
+          f[2 * y + 1] = a - b;
+        }
+        for (int k = 0; k < 8; ++k) {
+          d.cdc[c][k] = quant(f[kChroma422DcScan[k]], qpc[c] + 3, 0, intra, 1);
+          if (d.cdc[c][k]) cc = std::max(cc, 1);
+        }
+        continue;
       }
       const int f[4] = {cw[0] + cw[1] + cw[2] + cw[3], cw[0] - cw[1] + cw[2] - cw[3],
                         cw[0] + cw[1] - cw[2] - cw[3], cw[0] - cw[1] - cw[2] + cw[3]};
@@ -1035,7 +1077,7 @@ struct AvcHighEncoder::Impl {
 
   // Inter prediction of a whole MB from per-8x8 list entries and per-4x4 motion.
   void predict(const SliceEnv& env, int mb, const int r0[4], const int r1[4], const i16 (*mv)[16][2], int* py,
-               int (*pc)[64], bool weighted) {
+               int (*pc)[128], bool weighted) {
     MbRec m{};
     bool l1 = false;
     WpEntry wp[4];
@@ -1111,13 +1153,13 @@ struct AvcHighEncoder::Impl {
     const bool A = avail(mb, -1, 0), B = avail(mb, 0, -1), D = avail(mb, -1, -1);
     const int itype_base = 0;
     (void)itype_base;
-    int cp[2][64];
+    int cp[2][128];
     {  // chroma: DC
       for (int c = 0; c < 2; ++c) {
         IntraChromaNb n;
         chroma_neighbours(pic, mb, c, T(), n);
-        for (int y = 0; y < 8; ++y)
-          for (int x = 0; x < 8; ++x) cp[c][y * 8 + x] = chroma_pred(n, PredConst{0, 0, 0, 0}, 0, x, y, bd);
+        for (int y = 0; y < (cf == 2 ? 16 : 8); ++y)
+          for (int x = 0; x < 8; ++x) cp[c][y * 8 + x] = chroma_pred(n, PredConst{0, 0, 0, 0}, 0, x, y, bd, cf);
       }
       d.chroma_mode = 0;
     }
@@ -1236,7 +1278,7 @@ struct AvcHighEncoder::Impl {
       return m;
     };
     if (islice_pcm_ok && r < 5 && bd > 8) {  // (High 10: u16 samples of bd bits)
-      static thread_local u16 pcm16[kPcmMbBytes];
+      static thread_local u16 pcm16[kPcmMaxSamples];
       for (auto& p : pcm16) p = u16(rng.uni(1 << bd));
       if (cfg.mono)
         for (size_t i = 256; i < kPcmMbBytes; ++i) pcm16[i] = u16(1 << (bd - 1));
@@ -1245,7 +1287,7 @@ struct AvcHighEncoder::Impl {
       return;
     }
     if (islice_pcm_ok && r < 5) {
-      static thread_local u8 pcm[kPcmMbBytes];
+      static thread_local u8 pcm[kPcmMaxSamples];  // (4:2:2: 512 samples)
       for (auto& p : pcm) p = u8(16 + rng.uni(220));
       if (cfg.mono) std::memset(pcm + 256, 128, kPcmMbBytes - 256);  // (the grey the decoder fills)
       d.pcm = pcm;
@@ -1412,6 +1454,7 @@ struct AvcHighEncoder::Impl {
     pic.structure = fld ? 1 + job.parity : 0;
     pic.bd = bd;
     pic.qp_bias = pic.qpc_bias = qpbd;
+    pic.cf = cf;
     pic.target = fld ? 2 * (job.parity == 1 ? pair_slot : pick_slot()) + job.parity : pick_slot();
     if (job.parity == 0) {  // the pair's frame_num and frame slot, for its second field
       pair_fn = sh.frame_num;
@@ -1528,7 +1571,7 @@ struct AvcHighEncoder::Impl {
       r0[k] = skip.ref[0][k];
       r1[k] = skip.ref[1][k];
     }
-    int py[256], pc[2][64];
+    int py[256], pc[2][128];
     predict(env, mb, r0, r1, skip.mv, py, pc, weighted);
     const int skip_sad = sad_pred(mb, py);
     MbDesc sd;
@@ -1556,7 +1599,7 @@ struct AvcHighEncoder::Impl {
     // candidate predictions: 0 L0, 1 L1, 2 Bi (B) ; direct (with residual)
     int cands = t == h264::kB ? 3 : 1;
     int best_c = -1, best_cost = skip_sad + 256 * 2;  // direct / skip-motion with residual
-    int cpy[3][256], cpc[3][2][64];
+    int cpy[3][256], cpc[3][2][128];
     for (int c = 0; c < cands; ++c) {
       int a0[4], a1[4];
       i16 mv[2][16][2];

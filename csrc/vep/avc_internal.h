@@ -42,7 +42,7 @@ std::shared_ptr<ColMotion> build_col_motion(const MbNeighbours& nb, int wmbs, in
 // luma, pc 2 x 8x8 chroma. mv0 / mv1: 16 (x, y) per list (mv1 may be null).
 // structure: Picture::structure (field pictures: slots are fields, slot parity = field parity).
 void predict_inter(const std::vector<HostSurface>& slots, const MbRec& m, const i16* mv0, const i16* mv1,
-                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[64], int structure = 0);
+                   const WpEntry* wp, int mx, int my, int* py, int (*pc)[128], int structure = 0);
 
 // Encoder side of the generic macroblock layer: the decisions of one macroblock. The layer turns
 // them into syntax (predicted intra modes -> prev/rem flags, motion -> mvd against the same
@@ -65,9 +65,9 @@ struct MbDesc {
   int dc[16] = {};          // Intra16x16 DC
   int ac[16][16] = {};      // per raster 4x4 block; Intra16x16 AC in [0..14] (scan 1..15)
   int l8[4][64] = {};       // 8x8 transform blocks
-  int cdc[2][4] = {};
-  int cac[2][4][15] = {};   // chroma AC, scan 1..15
-  const u8* pcm = nullptr;  // I_PCM samples (384 bytes)
+  int cdc[2][8] = {};       // chroma DC (4:2:2: 8 per component, parsing order)
+  int cac[2][8][15] = {};   // chroma AC per raster block (4:2:2: 8 per component), scan 1..15
+  const u8* pcm = nullptr;  // I_PCM samples (384 bytes; 4:2:2 512; above 8 bits u16 samples)
 };
 
 // Writes the macroblocks of one slice (slice header already in `bw`).

@@ -78,6 +78,8 @@ class MbLayer {
     bd_ = sps_.bit_depth_luma;
     qpbd_ = 6 * (sps_.bit_depth_luma - 8);
     qpbdc_ = 6 * (sps_.bit_depth_chroma - 8);
+    cf_ = sps_.chroma_format_idc;
+    nbc_ = cf_ == 2 ? 8 : 4;
     weighted_ = (type_ == h264::kP && pps_.weighted_pred) || (type_ == h264::kB && pps_.weighted_bipred_idc != 0);
     implicit_ = type_ == h264::kB && pps_.weighted_bipred_idc == 2;
   }
@@ -398,13 +400,13 @@ class MbLayer {
     s.cbp = 0x2F;
     s.cbf = 0xFFFF;
     s.cbf_dc = 7;
-    s.cbf_cac[0] = s.cbf_cac[1] = 0xF;
+    s.cbf_cac[0] = s.cbf_cac[1] = u8((1u << nbc_) - 1);
     std::fill(std::begin(s.tc), std::end(s.tc), u8(16));
     for (auto& c : s.tcc) std::fill(std::begin(c), std::end(c), u8(16));
     s.qp = u8(qp_ + qpbd_);
     const u8* pcm;
-    const size_t nb = mono() ? 256 : kPcmMbBytes;  // (4:0:0: luma samples only)
-    if (bd_ > 8) {  // High 10: bd-bit samples (u(v)), kept as u16 in the record
+    const size_t nb = mono() ? 256 : pcm_samples();  // (4:0:0: luma samples only)
+    if (bd_ > 8 || cf_ == 2) {  // High 10 / 4:2:2: bd-bit samples (u(v)), kept as u16 / u8 in the record
       pcm_wide(mb, s, res, nb);
       return;
     }
@@ -440,14 +442,18 @@ class MbLayer {
     emit(mb, s, res, 0, 0, pcm);
   }
 
-  // I_PCM above 8 bits: ns samples of bd_ bits (luma, then Cb, then Cr), byte-aligned at both
-  // ends (the sample block is bd_ * 48 bytes for 4:2:0, a whole number). want->pcm: u16 samples.
+  // Samples of an I_PCM MB in the record: 384 (4:2:0 / 4:0:0), 512 (4:2:2).
+  size_t pcm_samples() const { return cf_ == 2 ? size_t(kPcmMaxSamples) : size_t(kPcmMbBytes); }
+  // I_PCM above 8 bits or in 4:2:2: ns samples of bd_ bits (luma, then Cb, then Cr), byte-aligned
+  // at both ends (ns * bd_ is a multiple of 8). want->pcm: u16 samples above 8 bits, else bytes.
+  // The record holds u16 samples above 8 bits, bytes at 8 bits.
   void pcm_wide(int mb, MbState& s, MbResidual& res, size_t ns) {
-    const size_t nbytes = ns * size_t(bd_) / 8;
+    const size_t nbytes = ns * size_t(bd_) / 8, total = pcm_samples();
     if constexpr (kWrite) {
-      const u16* src = reinterpret_cast<const u16*>(want->pcm);
-      VEP_CHECK(src, "I_PCM macroblock without samples");
-      for (size_t i = 0; i < kPcmMbBytes; ++i) pcm16_[i] = i < ns ? src[i] : u16(1 << (bd_ - 1));
+      VEP_CHECK(want->pcm, "I_PCM macroblock without samples");
+      const u16* src16 = reinterpret_cast<const u16*>(want->pcm);
+      for (size_t i = 0; i < total; ++i)
+        pcm16_[i] = i < ns ? (bd_ > 8 ? src16[i] : u16(want->pcm[i])) : u16(1 << (bd_ - 1));
       BitWriter w;
       for (size_t i = 0; i < ns; ++i) w.u(bd_, pcm16_[i]);
       VEP_CHECK(w.buf().size() == nbytes, "I_PCM sample block size");
@@ -474,16 +480,23 @@ class MbLayer {
         br->skip(nbytes * 8);
       }
       BitReader r(p, nbytes);
-      for (size_t i = 0; i < kPcmMbBytes; ++i) pcm16_[i] = i < ns ? u16(r.u(bd_)) : u16(1 << (bd_ - 1));
+      for (size_t i = 0; i < total; ++i) pcm16_[i] = i < ns ? u16(r.u(bd_)) : u16(1 << (bd_ - 1));
     }
     prev_qpd_nz = 0;
-    emit(mb, s, res, 0, 0, reinterpret_cast<const u8*>(pcm16_));
+    if (bd_ > 8) {
+      emit(mb, s, res, 0, 0, reinterpret_cast<const u8*>(pcm16_));
+    } else {
+      for (size_t i = 0; i < total; ++i) pcm8_[i] = u8(pcm16_[i]);
+      emit(mb, s, res, 0, 0, pcm8_);
+    }
   }
 
   bool mono() const { return sps_.chroma_format_idc == 0; }
   u8 pcm_mono_[kPcmMbBytes];
-  u16 pcm16_[kPcmMbBytes];
+  u16 pcm16_[kPcmMaxSamples];
+  u8 pcm8_[kPcmMaxSamples];
   int bd_ = 8, qpbd_ = 0, qpbdc_ = 0;  // bit depth, QpBdOffsetY / C (High 10)
+  int cf_ = 1, nbc_ = 4;               // chroma_format_idc, chroma 4x4 blocks per component
 
  public:
   const u8* data = nullptr;  // CABAC: slice RBSP (I_PCM samples are read in place)
@@ -828,7 +841,7 @@ class MbLayer {
     };
     const int bx = b & 1, by = b >> 1;
     const int a = bx ? cond(mb, b - 1, true) : cond(nb_.mb_at(mb, -1, 0), b + 1, false);
-    const int bb = by ? cond(mb, b - 2, true) : cond(nb_.mb_at(mb, 0, -1), b + 2, false);
+    const int bb = by ? cond(mb, b - 2, true) : cond(nb_.mb_at(mb, 0, -1), b + nbc_ - 2, false);
     return a + 2 * bb;
   }
 
@@ -965,31 +978,38 @@ class MbLayer {
       // (qp = QP'Y; QP'C = QPC + QpBdOffsetC, QPC from QPY, Table 8-15)
       const int qpc[2] = {chroma_qp_bd(qp - qpbd_, pps_.chroma_qp_index_offset, qpbdc_) + qpbdc_,
                           chroma_qp_bd(qp - qpbd_, pps_.second_chroma_qp_index_offset, qpbdc_) + qpbdc_};
-      int dcv[2][4] = {};
+      const int nbc = nbc_;  // chroma 4x4 blocks per component (4:2:2: 8, 2 wide x 4 tall)
+      int dcv[2][8] = {};
       for (int c = 0; c < 2; ++c) {
         const int inc = kCabac ? cbf_dc_inc(mb, 1 + c, intra) : 0;
-        int v4[4];
-        const int t = read_block(kCatChromaDc, inc, -1, 4, v4, nzp, kWrite ? want->cdc[c] : nullptr);
+        int v8[8];
+        // (CAVLC nC -1 / -2: the 4:2:0 / 4:2:2 chroma DC coeff_token tables)
+        const int t = read_block(kCatChromaDc, inc, cf_ == 2 ? -2 : -1, nbc, v8, nzp, kWrite ? want->cdc[c] : nullptr);
         if (t > 0) {
           s.cbf_dc |= u8(2 << c);
-          int u[4] = {0, 0, 0, 0};
-          for (int j = 0; j < t; ++j) u[nzp[j]] = v4[nzp[j]];
-          const int f[4] = {u[0] + u[1] + u[2] + u[3], u[0] - u[1] + u[2] - u[3], u[0] + u[1] - u[2] - u[3],
-                            u[0] - u[1] - u[2] + u[3]};
-          const int ls = dq_.ls4[ly + 1 + c][qpc[c] % 6][0];
-          for (int b = 0; b < 4; ++b) dcv[c][b] = ((f[b] * ls) * (1 << (qpc[c] / 6))) >> 5;
+          int u[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+          for (int j = 0; j < t; ++j) u[nzp[j]] = v8[nzp[j]];
+          if (cf_ == 2) {  // 2x4 DC at qP,DC = QP'C + 3 (§8.5.11.2)
+            const int qpdc = qpc[c] + 3;
+            chroma422_dc(u, qpdc, dq_.ls4[ly + 1 + c][qpdc % 6][0], dcv[c]);
+          } else {
+            const int f[4] = {u[0] + u[1] + u[2] + u[3], u[0] - u[1] + u[2] - u[3], u[0] + u[1] - u[2] - u[3],
+                              u[0] - u[1] - u[2] + u[3]};
+            const int ls = dq_.ls4[ly + 1 + c][qpc[c] % 6][0];
+            for (int b = 0; b < 4; ++b) dcv[c][b] = ((f[b] * ls) * (1 << (qpc[c] / 6))) >> 5;
+          }
         }
       }
       for (int c = 0; c < 2; ++c) {
         const int lc = ly + 1 + c;
-        for (int b = 0; b < 4; ++b) {
-          i16* d = res.blk[16 + c * 4 + b];
+        for (int b = 0; b < nbc; ++b) {  // (4:2:2: the two 8x8s top to bottom, raster 2x2 in each)
+          i16* d = res.blk[16 + c * nbc + b];
           bool nz = dcv[c][b] != 0;
           std::memset(d, 0, 16 * sizeof(i16));
           d[0] = sat16(dcv[c][b]);
           if (cbp_chroma & 2) {
             const int binc = kCabac ? cbf_cac_inc(mb, c, b, intra) : 0;
-            const int bnc = kCabac ? 0 : nb_.nc_chroma(mb, c, b);
+            const int bnc = kCabac ? 0 : nb_.nc_chroma(mb, c, b, nbc);
             const int tc = read_block(kCatChromaAc, binc, bnc, 15, lv, nzp, kWrite ? want->cac[c][b] : nullptr);
             s.tcc[c][b] = u8(tc);
             if (tc) s.cbf_cac[c] |= u8(1u << b);
@@ -1001,7 +1021,7 @@ class MbLayer {
               nz |= v != 0;
             }
           }
-          if (nz) res.chroma |= u8(1u << (c * 4 + b));
+          if (nz) res.chroma |= u16(1u << (c * nbc + b));
         }
       }
     }

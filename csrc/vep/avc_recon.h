@@ -67,8 +67,8 @@ struct MbRec {
   i8 alpha_off;     // FilterOffsetA
   i8 beta_off;      // FilterOffsetB
   u16 slice;        // slice index within the picture (neighbour availability); bytes 14..15
-  u8 chroma_coded;  // bits 0-3 Cb, 4-7 Cr 4x4 blocks (raster) with residual
-  u8 pad0;
+  u16 chroma_coded;  // chroma 4x4 blocks (raster per component) with residual: 4:2:0 bits 0-3 Cb,
+                     // 4-7 Cr; 4:2:2 (8 blocks per component, 2 wide x 4 tall) bits 0-7 Cb, 8-15 Cr
   u16 pad1;
   u8 ref[4];        // per 8x8 (raster): DPB slot of the list-0 reference picture (0xFF = none)
   u8 ref1[4];       // per 8x8: DPB slot of the list-1 reference picture (0xFF = none)
@@ -132,9 +132,10 @@ VEP_HD int wp_sample(int p0, int p1, bool has0, bool has1, const WpEntry* w, int
 // 93% of the dense blocks' entries are zero on the camera streams (89% on IDR pictures): this is
 // 5-7x fewer bytes for the parse to write and the GPU to pull over PCIe.
 // Dense layout (kDenseCoefs entries): luma 4x4 block r at 16 r, or 8x8 block q at 64 q (raster
-// 8x8); chroma block k (0-3 Cb, 4-7 Cr) at 256 + 16 k.
-// I_PCM: the 384 sample bytes from i16 offset MbRec::coef.
-constexpr int kDenseCoefs = 384;
+// 8x8); chroma block k (bit k of chroma_coded: 4:2:0 0-3 Cb, 4-7 Cr; 4:2:2 0-7 Cb, 8-15 Cr) at
+// 256 + 16 k.
+// I_PCM: the 384 (4:2:2: 512) samples from i16 offset MbRec::coef (bytes, or u16 above 8 bits).
+constexpr int kDenseCoefs = 512;
 VEP_HD int coef_words(const MbRec& m) {
   return __builtin_popcount(u32(m.luma_coded)) + __builtin_popcount(u32(m.chroma_coded));
 }
@@ -777,10 +778,11 @@ VEP_HD int intra16x16_pred(const Intra16Nb& n, const PredConst& k, int mode, int
                            k, mode, x, y, bd);
 }
 
-// Chroma (4:2:0, 8x8 per component): top[0] = p[-1,-1], top[1..8]; left[0..7].
+// Chroma (8x8 per component in 4:2:0, 8x16 in 4:2:2): top[0] = p[-1,-1], top[1..8]; left[0..7]
+// (4:2:2: left[0..15]).
 struct IntraChromaNb {
   int top[9];
-  int left[8];
+  int left[16];
   bool has_top, has_left, has_tl;
 };
 
@@ -810,36 +812,80 @@ VEP_HD int chroma_dc_g(TF T, LF L, bool has_top, bool has_left, int bx, int by, 
   return 1 << (bd - 1);
 }
 
+// Plane prediction constants (§8.3.4.4) with xCF = 0 and yCF = 4 * (chroma_format_idc == 2): the
+// 8x16 4:2:2 block sums 8 vertical gradient terms and weighs them by 5 instead of 34.
 template <class TF, class LF>
-VEP_HD PredConst chroma_plane_const_g(TF T, LF L) {
+VEP_HD PredConst chroma_plane_const_g(TF T, LF L, int cf = 1) {
   int H = 0, V = 0;
-  for (int i = 0; i < 4; ++i) {
-    H += (i + 1) * (T(4 + i) - T(2 - i));
-    V += (i + 1) * (L(4 + i) - (2 - i >= 0 ? L(2 - i) : T(-1)));
+  for (int i = 0; i < 4; ++i) H += (i + 1) * (T(4 + i) - T(2 - i));
+  if (cf == 2) {
+    for (int i = 0; i < 8; ++i) V += (i + 1) * (L(8 + i) - (6 - i >= 0 ? L(6 - i) : T(-1)));
+    return PredConst{0, 16 * (L(15) + T(7)), (34 * H + 32) >> 6, (5 * V + 32) >> 6};
   }
-  PredConst k{0, 16 * (L(7) + T(7)), (34 * H + 32) >> 6, (34 * V + 32) >> 6};
-  return k;
+  for (int i = 0; i < 4; ++i) V += (i + 1) * (L(4 + i) - (2 - i >= 0 ? L(2 - i) : T(-1)));
+  return PredConst{0, 16 * (L(7) + T(7)), (34 * H + 32) >> 6, (34 * V + 32) >> 6};
 }
 
-// mode: 0 DC, 1 horizontal, 2 vertical, 3 plane
+// mode: 0 DC, 1 horizontal, 2 vertical, 3 plane. (x, y) in the 8x8 (4:2:2: 8x16) block; the DC
+// rule of 4x4 block (x >> 2, y >> 2) covers the 4:2:2 blocks below the first row as well.
 template <class TF, class LF>
 VEP_HD int chroma_pred_g(TF T, LF L, bool has_top, bool has_left, const PredConst& k, int mode, int x,
-                         int y, int bd = 8) {
+                         int y, int bd = 8, int cf = 1) {
   switch (mode) {
     case 0: return chroma_dc_g(T, L, has_top, has_left, x >> 2, y >> 2, bd);
     case 1: return L(y);
     case 2: return T(x);
-    default: return clip1((k.a + k.b * (x - 3) + k.c * (y - 3) + 16) >> 5, bd);
+    default: return clip1((k.a + k.b * (x - 3) + k.c * (y - (cf == 2 ? 7 : 3)) + 16) >> 5, bd);
   }
 }
 
-VEP_HD PredConst chroma_plane_const(const IntraChromaNb& n) {
-  return chroma_plane_const_g([&](int x) { return n.top[x + 1]; }, [&](int y) { return n.left[y]; });
+VEP_HD PredConst chroma_plane_const(const IntraChromaNb& n, int cf = 1) {
+  return chroma_plane_const_g([&](int x) { return n.top[x + 1]; }, [&](int y) { return n.left[y]; }, cf);
 }
 
-VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y, int bd = 8) {
+VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int x, int y, int bd = 8, int cf = 1) {
   return chroma_pred_g([&](int xx) { return n.top[xx + 1]; }, [&](int yy) { return n.left[yy]; },
-                       n.has_top, n.has_left, k, mode, x, y, bd);
+                       n.has_top, n.has_left, k, mode, x, y, bd, cf);
+}
+
+// ---- 4:2:2 chroma DC (§8.5.11): 8 levels in parsing order -> c[4][2] (chroma DC scan of 4:2:2),
+// the 4x4 x 2x2 Hadamard-type transform f = A c B, then the scaling at qP,DC = QP'C + 3.
+// dcv[blk] for chroma block blk (raster, 2 wide x 4 tall). ls = LevelScale4x4(qP,DC % 6, 0, 0).
+VEP_CONST static const u8 kChroma422DcScan[8] = {0, 2, 1, 5, 3, 6, 4, 7};  // scan -> raster (x + 2 y)
+VEP_HD void chroma422_dc(const int* lv_scan, int qpdc, int ls, int* dcv) {
+  int c[8];
+  for (int k = 0; k < 8; ++k) c[kChroma422DcScan[k]] = lv_scan[k];
+  int f[8];
+  for (int x = 0; x < 2; ++x) {  // A (4 x 4) on the columns
+    const int c0 = c[x], c1 = c[2 + x], c2 = c[4 + x], c3 = c[6 + x];
+    f[x] = c0 + c1 + c2 + c3;
+    f[2 + x] = c0 + c1 - c2 - c3;
+    f[4 + x] = c0 - c1 - c2 + c3;
+    f[6 + x] = c0 - c1 + c2 - c3;
+  }
+  for (int y = 0; y < 4; ++y) {  // B (2 x 2) on the rows
+    const int a = f[2 * y], b = f[2 * y + 1];
+    f[2 * y] = a + b;
+    f[2 * y + 1] = a - b;
+  }
+  for (int k = 0; k < 8; ++k)
+    dcv[k] = qpdc >= 36 ? (f[k] * ls) * (1 << (qpdc / 6 - 6))
+                        : (f[k] * ls + (1 << (5 - qpdc / 6))) >> (6 - qpdc / 6);
+}
+
+// Chroma vector of a luma vector (§8.4.1.4 / §8.4.2.2.2) as integer + eighth-sample fraction per
+// axis: horizontally 1/8 chroma sample in both formats; vertically 1/8 in 4:2:0 and, in 4:2:2
+// (full-height chroma), the quarter-sample luma position scaled to eighths.
+VEP_HD void chroma_mv(int mvx, int mvy, int cf, int& ix, int& fx, int& iy, int& fy) {
+  ix = mvx >> 3;
+  fx = mvx & 7;
+  if (cf == 2) {
+    iy = mvy >> 2;
+    fy = (mvy & 3) << 1;
+  } else {
+    iy = mvy >> 3;
+    fy = mvy & 7;
+  }
 }
 
 // ------------------------------------------------------------------------------ inter

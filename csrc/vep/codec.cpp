@@ -527,28 +527,34 @@ void cpu_apply_update(const MbUpdate& upd, HostSurface& s) {
 }
 
 void narrow_surface(const HostSurface& s, HostSurface& out) {
-  if (!s.wide()) {
+  if (!s.wide() && s.cf != 2) {
     out = s;
     return;
   }
   out.coded_w = s.coded_w;
   out.coded_h = s.coded_h;
   out.bd = 8;
+  out.cf = 1;
   out.y16.clear();
   out.uv16.clear();
   const int sh = s.bd - 8, rnd = (1 << sh) >> 1;
-  auto n8 = [&](u16 v) { return u8(std::min(255, (int(v) + rnd) >> sh)); };
-  out.y.resize(s.y16.size());
-  out.uv.resize(s.uv16.size());
-  for (size_t i = 0; i < s.y16.size(); ++i) out.y[i] = n8(s.y16[i]);
-  for (size_t i = 0; i < s.uv16.size(); ++i) out.uv[i] = n8(s.uv16[i]);
+  auto n8 = [&](int v) { return u8(std::min(255, (v + rnd) >> sh)); };
+  const size_t w = size_t(s.coded_w), ny = w * size_t(s.coded_h);
+  out.y.resize(ny);
+  out.uv.resize(ny / 2);
+  for (size_t i = 0; i < ny; ++i) out.y[i] = n8(s.wide() ? int(s.y16[i]) : int(s.y[i]));
+  auto c = [&](size_t i) { return s.wide() ? int(s.uv16[i]) : int(s.uv[i]); };
+  for (size_t r = 0; r < size_t(s.coded_h / 2); ++r)
+    for (size_t x = 0; x < w; ++x)
+      out.uv[r * w + x] = n8(s.cf == 2 ? (c(2 * r * w + x) + c((2 * r + 1) * w + x) + 1) >> 1 : c(r * w + x));
 }
 
 void cpu_nv12_to_bgr(const HostSurface& s8, int crop_left, int crop_top, int width, int height,
                      u8* out) {
   HostSurface tmp;
-  if (s8.wide()) narrow_surface(s8, tmp);
-  const HostSurface& s = s8.wide() ? tmp : s8;
+  const bool conv = s8.wide() || s8.cf == 2;
+  if (conv) narrow_surface(s8, tmp);
+  const HostSurface& s = conv ? tmp : s8;
   for (int y = 0; y < height; ++y) {
     int sy = y + crop_top;
     const u8* yr = &s.y[size_t(sy) * s.coded_w];

@@ -287,21 +287,27 @@ struct HostSurface {
   // y / uv stay empty. bd = the sample bit depth of the storage (8: u8 planes).
   int bd = 8;
   std::vector<u16> y16, uv16;
+  // chroma format: 1 (and 0, grey chroma) NV12; 2 = 4:2:2 (H.264 High 4:2:2): NV16, the
+  // interleaved chroma plane has coded_h rows
+  int cf = 1;
   bool wide() const { return bd > 8; }
-  void alloc(int w, int h, int bit_depth = 8) {
+  int chroma_rows() const { return cf == 2 ? coded_h : coded_h / 2; }
+  void alloc(int w, int h, int bit_depth = 8, int chroma_format = 1) {
     coded_w = w;
     coded_h = h;
     bd = bit_depth;
+    cf = chroma_format == 2 ? 2 : 1;
+    const size_t nc = size_t(w) * size_t(chroma_rows());
     if (bd > 8) {
       y.clear();
       uv.clear();
       y16.assign(size_t(w) * h, u16(16 << (bd - 8)));
-      uv16.assign(size_t(w) * h / 2, u16(128 << (bd - 8)));
+      uv16.assign(nc, u16(128 << (bd - 8)));
     } else {
       y16.clear();
       uv16.clear();
       y.assign(size_t(w) * h, 16);
-      uv.assign(size_t(w) * h / 2, 128);
+      uv.assign(nc, 128);
     }
   }
   // sample of component c (0 Y, 1 Cb, 2 Cr) at component coordinates (x, y)
@@ -317,8 +323,10 @@ struct HostSurface {
   }
 };
 
-// 8-bit copy of a high bit depth surface (round to nearest, saturating): the form the BGR24
-// conversion and the letterbox read. An 8-bit surface is copied as is.
+// 8-bit NV12 copy of a high bit depth and / or 4:2:2 surface: the form the BGR24 conversion and
+// the letterbox read. 4:2:2 chroma rows are averaged in pairs, (a + b + 1) >> 1 at the source
+// depth; then samples above 8 bits are rounded to nearest, saturating. An 8-bit 4:2:0 surface is
+// copied as is.
 void narrow_surface(const HostSurface& s, HostSurface& out);
 
 // CPU reference of the fused GPU kernel: apply MB update to the NV12 surface, then convert the

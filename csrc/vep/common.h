@@ -50,6 +50,7 @@ constexpr int kMbSize = 16;
 constexpr int kPcmLumaBytes = 256;
 constexpr int kPcmChromaBytes = 64;  // per plane
 constexpr int kPcmMbBytes = kPcmLumaBytes + 2 * kPcmChromaBytes;  // 384 = 24 x 16 B
+constexpr int kPcmMaxSamples = 512;  // (H.264 4:2:2 I_PCM: 256 + 2 x 128 samples)
 
 // 64-byte aligned growable byte buffer (host, pageable).
 class AlignedBuf {
