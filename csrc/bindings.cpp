@@ -290,6 +290,7 @@ PYBIND11_MODULE(_vep, m) {
       .def_readwrite("open_gop", &SynthConfig::open_gop)
       .def_readwrite("lossless", &SynthConfig::lossless)
       .def_readwrite("bit_depth", &SynthConfig::bit_depth)
+      .def_readwrite("chroma_format", &SynthConfig::chroma_format)
       .def_readwrite("interlaced", &SynthConfig::interlaced)
       .def_readwrite("mono", &SynthConfig::mono)
       .def_property(
@@ -691,20 +692,31 @@ PYBIND11_MODULE(_vep, m) {
       for (int x = 0; x < 16; ++x) r[size_t(y * 16 + x)] = avc::intra16x16_pred(n, k, mode, x, y, bd);
     return r;
   }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("mode"), py::arg("bd") = 8);
-  rc.def("intra_chroma", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode, int bd) {
-    VEP_CHECK(top.size() == 9 && left.size() == 8, "9 top + 8 left samples");
+  // (cf 2: 4:2:2, 16 left samples, 8x16 prediction)
+  rc.def("intra_chroma", [](std::vector<int> top, std::vector<int> left, bool has_top, bool has_left, int mode, int bd,
+                            int cf) {
+    const int ch = cf == 2 ? 16 : 8;
+    VEP_CHECK(top.size() == 9 && left.size() == size_t(ch), "9 top + 8 (4:2:2: 16) left samples");
     avc::IntraChromaNb n{};
     for (int k = 0; k < 9; ++k) n.top[k] = top[size_t(k)];
-    for (int k = 0; k < 8; ++k) n.left[k] = left[size_t(k)];
+    for (int k = 0; k < ch; ++k) n.left[k] = left[size_t(k)];
     n.has_top = has_top;
     n.has_left = has_left;
     n.has_tl = has_top && has_left;
-    const avc::PredConst k = mode == 3 ? avc::chroma_plane_const(n) : avc::PredConst{0, 0, 0, 0};
-    std::vector<int> r(64);
-    for (int y = 0; y < 8; ++y)
-      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::chroma_pred(n, k, mode, x, y, bd);
+    const avc::PredConst k = mode == 3 ? avc::chroma_plane_const(n, cf) : avc::PredConst{0, 0, 0, 0};
+    std::vector<int> r(size_t(8 * ch));
+    for (int y = 0; y < ch; ++y)
+      for (int x = 0; x < 8; ++x) r[size_t(y * 8 + x)] = avc::chroma_pred(n, k, mode, x, y, bd, cf);
     return r;
-  }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("mode"), py::arg("bd") = 8);
+  }, py::arg("top"), py::arg("left"), py::arg("has_top"), py::arg("has_left"), py::arg("mode"), py::arg("bd") = 8,
+     py::arg("cf") = 1);
+  // 4:2:2 chroma DC: 8 levels (parsing order) -> dcC per chroma block (raster, 2 wide)
+  rc.def("chroma422_dc", [](std::vector<int> lv, int qpdc, int ls) {
+    VEP_CHECK(lv.size() == 8, "8 levels");
+    std::vector<int> r(8);
+    avc::chroma422_dc(lv.data(), qpdc, ls, r.data());
+    return r;
+  });
   rc.def("luma_qpel", [](py::array_t<uint8_t, py::array::c_style | py::array::forcecast> plane, int xi, int yi,
                          int fx, int fy) {
     VEP_CHECK(plane.ndim() == 2, "2-D plane");

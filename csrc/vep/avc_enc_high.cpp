@@ -1048,7 +1048,7 @@ struct AvcHighEncoder::Impl {
           f[2 * y + 1] = a - b;
         }
         for (int k = 0; k < 8; ++k) {
-          d.cdc[c][k] = quant(f[kChroma422DcScan[k]], qpc[c] + 3, 0, intra, 1);
+          d.cdc[c][k] = quant(f[kChroma422DcScanToRaster[k]], qpc[c] + 3, 0, intra, 1);
           if (d.cdc[c][k]) cc = std::max(cc, 1);
         }
         continue;

@@ -851,10 +851,13 @@ VEP_HD int chroma_pred(const IntraChromaNb& n, const PredConst& k, int mode, int
 // ---- 4:2:2 chroma DC (§8.5.11): 8 levels in parsing order -> c[4][2] (chroma DC scan of 4:2:2),
 // the 4x4 x 2x2 Hadamard-type transform f = A c B, then the scaling at qP,DC = QP'C + 3.
 // dcv[blk] for chroma block blk (raster, 2 wide x 4 tall). ls = LevelScale4x4(qP,DC % 6, 0, 0).
-VEP_CONST static const u8 kChroma422DcScan[8] = {0, 2, 1, 5, 3, 6, 4, 7};  // scan -> raster (x + 2 y)
+// c[4][2] = [[c0, c2], [c1, c5], [c3, c6], [c4, c7]] (8-330): raster (x + 2 y) -> parsing index,
+// and its inverse
+VEP_CONST static const u8 kChroma422DcRasterToScan[8] = {0, 2, 1, 5, 3, 6, 4, 7};
+VEP_CONST static const u8 kChroma422DcScanToRaster[8] = {0, 2, 1, 4, 6, 3, 5, 7};
 VEP_HD void chroma422_dc(const int* lv_scan, int qpdc, int ls, int* dcv) {
   int c[8];
-  for (int k = 0; k < 8; ++k) c[kChroma422DcScan[k]] = lv_scan[k];
+  for (int r = 0; r < 8; ++r) c[r] = lv_scan[kChroma422DcRasterToScan[r]];
   int f[8];
   for (int x = 0; x < 2; ++x) {  // A (4 x 4) on the columns
     const int c0 = c[x], c1 = c[2 + x], c2 = c[4 + x], c3 = c[6 + x];

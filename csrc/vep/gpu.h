@@ -162,7 +162,10 @@ void launch_hevc_deblock(const HevcDesc* d_descs, int n, int total_blocks, int d
 void launch_hevc_sao(const HevcDesc* d_descs, int n, int total_blocks, hipStream_t s);
 // Main10 output: u16 NV12 planes (n luma samples, n / 2 chroma) -> 8-bit NV12 (round to nearest,
 // saturating), the form the BGR24 conversion and the letterbox read.
-void launch_narrow(const u16* y, const u16* uv, u8* y8, u8* uv8, size_t n, int bd, hipStream_t s);
+// 8-bit NV12 copy of a published slot (w x h luma): samples above 8 bits rounded to nearest
+// (bd > 8: u16 planes), 4:2:2 chroma rows averaged in pairs (cf 2: an NV16 chroma plane of h rows)
+// — the same result as narrow_surface (codec.h).
+void launch_narrow(const void* y, const void* uv, u8* y8, u8* uv8, int w, int h, int bd, int cf, hipStream_t s);
 // H.264 field pairs (frame slot in field-separated layout: top field rows, then bottom) -> the
 // interleaved 8-bit NV12 frames (pitch bytes per row, `height` luma rows), one launch for the
 // `n` descriptors of a batch (grid y = descriptor).
@@ -199,7 +202,8 @@ struct AvcDesc {
   i32 bd;              // sample bit depth: 8 (u8 surfaces), 9 / 10 (High 10: u16 surfaces,
                        // slot_y / slot_uv in bytes; intra + deblocking in avc_hbd_kernel)
   i32 qp_bias, qpc_bias;  // MbRec::qp / qpc bias (QpBdOffsetY / C)
-  i32 pad_;
+  i32 cf;              // chroma format: 1 (or 0: grey chroma) 4:2:0, 2 = 4:2:2 (NV16 slots; intra +
+                       // deblocking in avc_hbd_kernel)
   VEP_DEV u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
                        // tagged words per MB of every workgroup's last row (intra wavefront:
                        // words 0..7, zeroed by avc_inter_kernel; deblocking: all, zeroed by
@@ -209,7 +213,7 @@ struct AvcDesc {
 // chroma / store+publish / MBs, deblock wait / load / filter / store+publish / MBs.
 constexpr int kAvcProfSlots = 12;  // + [11] intra residual pass
 // Residual samples of one intra MB: 256 luma (raster) + 2 x 64 chroma, as i16.
-constexpr int kAvcResSamples = 384;
+constexpr int kAvcResSamples = 512;  // slot stride: 256 luma + 2 x 64 chroma (4:2:2: 2 x 128)
 // Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.
 struct AvcDbkInfo {
   u32 bs[4];      // 32 x 4-bit bS: nibble dir * 16 + edge * 4 + segment (0 = edge not filtered)

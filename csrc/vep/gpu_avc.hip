@@ -144,9 +144,15 @@ __device__ inline void luma8_residual(const i16* D, const MbRec& m, int lane, in
 }
 
 // Skip / inter / I_PCM MB of the inter kernel, whole wave, on u8 (8-bit) or u16 (High 10)
-// surfaces. D: the wave's dense coefficient buffer, T: its 8x8-transform buffer.
-template <class P>
+// surfaces, chroma format CF (1: 8x8 chroma per component, 2 lanes' worth of samples each;
+// 2 = 4:2:2: 8x16, 4 per lane). D: the wave's dense coefficient buffer, T: its 8x8-transform
+// buffer.
+template <class P, int CF>
 __device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int lane, int* T, i16* D, bool t8) {
+  constexpr int CH = CF == 2 ? 16 : 8;  // chroma MB height
+  constexpr int CS = 8 * CH;            // chroma samples per component
+  constexpr int NCL = 2 * CS / 64;      // chroma samples per lane
+  constexpr int NB = CF == 2 ? 8 : 4;   // chroma 4x4 blocks per component
   const int x = lane & 15, y0 = lane >> 4;  // luma sample (x, y0 + 4k), block row k
   const int W = d.wmbs, wpx = W * 16, hpx = d.hmbs * 16, pitch = wpx;
   const int mx = mb % W, my = mb / W;
@@ -160,9 +166,9 @@ __device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int la
 #pragma unroll
     for (int k = 0; k < 4; ++k) ty[size_t(my * 16 + y0 + 4 * k) * pitch + mx * 16 + x] = s[(y0 + 4 * k) * 16 + x];
 #pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-      tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = s[256 + t];
+    for (int k = 0; k < NCL; ++k) {
+      const int t = lane + 64 * k, cc = t / CS, cq = t % CS, cx = cq & 7, cy = cq >> 3;
+      tuv[size_t(my * CH + cy) * pitch + (mx * 8 + cx) * 2 + cc] = s[256 + t];
     }
     return;
   }
@@ -198,34 +204,36 @@ __device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int la
     else if ((m.luma_coded >> blk) & 1) o += avc::idct4x4_at(D + 16 * blk, y & 3, x & 3);
     ty[size_t(my * 16 + y) * pitch + mx * 16 + x] = P(avc::clip1(o, bd));
   }
-  int u[2];
+  int u[NCL];
+  const int chp = CF == 2 ? hpx : hpx / 2;  // chroma plane height
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-    const int r = (cy >> 1) * 4 + (cx >> 1), b8 = ((cy >> 2) << 1) | (cx >> 2);
+  for (int k = 0; k < NCL; ++k) {
+    const int t = lane + 64 * k, cc = t / CS, cq = t % CS, cx = cq & 7, cy = cq >> 3;
+    const int ly = CF == 2 ? cy : 2 * cy;  // luma row of the sample
+    const int r = (ly >> 2) * 4 + (cx >> 1), b8 = ((ly >> 3) << 1) | (cx >> 2);
     const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
-    int p0 = 0, p1 = 0;
+    int p0 = 0, p1 = 0, ix, fx, iy, fy;
     if (s0 != 0xFF) {
       const i16* v0 = mvb + avc::mv_sub(m.flags, 0, r);
       const int vy = v0[1] + (d.field ? 2 * ((d.field == 2) - (s0 & 1)) : 0);  // opposite-parity field
-      p0 = avc::chroma_epel(uvref(s0), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v0[0] >> 3),
-                            my * 8 + cy + (vy >> 3), v0[0] & 7, vy & 7);
+      avc::chroma_mv(v0[0], vy, CF, ix, fx, iy, fy);
+      p0 = avc::chroma_epel(uvref(s0), pitch, wpx / 2, chp, cc, mx * 8 + cx + ix, my * CH + cy + iy, fx, fy);
     }
     if (s1 != 0xFF) {
       const i16* v1 = mvb + avc::mv_sub(m.flags, 1, r);
       const int vy = v1[1] + (d.field ? 2 * ((d.field == 2) - (s1 & 1)) : 0);
-      p1 = avc::chroma_epel(uvref(s1), pitch, wpx / 2, hpx / 2, cc, mx * 8 + cx + (v1[0] >> 3),
-                            my * 8 + cy + (vy >> 3), v1[0] & 7, vy & 7);
+      avc::chroma_mv(v1[0], vy, CF, ix, fx, iy, fy);
+      p1 = avc::chroma_epel(uvref(s1), pitch, wpx / 2, chp, cc, mx * 8 + cx + ix, my * CH + cy + iy, fx, fy);
     }
     u[k] = avc::wp_sample(p0, p1, s0 != 0xFF, s1 != 0xFF, wpp ? wpp + b8 : nullptr, 1 + cc, bd);
   }
 #pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-    const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
+  for (int k = 0; k < NCL; ++k) {
+    const int t = lane + 64 * k, cc = t / CS, cq = t % CS, cx = cq & 7, cy = cq >> 3;
+    const int kb = cc * NB + (cy >> 2) * 2 + (cx >> 2);
     int o = u[k];
     if ((m.chroma_coded >> kb) & 1) o += avc::idct4x4_at(D + 256 + 16 * kb, cy & 3, cx & 3);
-    tuv[size_t(my * 8 + cy) * pitch + (mx * 8 + cx) * 2 + cc] = P(avc::clip1(o, bd));
+    tuv[size_t(my * CH + cy) * pitch + (mx * 8 + cx) * 2 + cc] = P(avc::clip1(o, bd));
   }
 }
 
@@ -273,17 +281,23 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
       else v = (m.luma_coded >> blk) & 1 ? avc::idct4x4_at(D + 16 * blk, y & 3, x & 3) : 0;
       r[y * 16 + x] = i16(v);
     }
-#pragma unroll
-    for (int k = 0; k < 2; ++k) {
-      const int t = lane + 64 * k, cc = t >> 6, cq = t & 63, cx = cq & 7, cy = cq >> 3;
-      const int kb = cc * 4 + (cy >> 2) * 2 + (cx >> 2);
+    const int ncs = d.cf == 2 ? 128 : 64, nb = d.cf == 2 ? 8 : 4;  // (4:2:2: 8x16 chroma)
+    for (int k = 0; k < 2 * ncs / 64; ++k) {
+      const int t = lane + 64 * k, cc = t / ncs, cq = t % ncs, cx = cq & 7, cy = cq >> 3;
+      const int kb = cc * nb + (cy >> 2) * 2 + (cx >> 2);
       r[256 + t] = i16((m.chroma_coded >> kb) & 1 ? avc::idct4x4_at(D + 256 + 16 * kb, cy & 3, cx & 3) : 0);
     }
     return;
   }
   if (m.kind != avc::kSkip && m.kind != avc::kInter && m.kind != avc::kIPcm) return;
-  if (d.bd > 8) inter_mb<u16>(d, m, mb, lane, T, lcoef[wv], t8);
-  else inter_mb<u8>(d, m, mb, lane, T, lcoef[wv], t8);
+  if (d.cf == 2) {
+    if (d.bd > 8) inter_mb<u16, 2>(d, m, mb, lane, T, lcoef[wv], t8);
+    else inter_mb<u8, 2>(d, m, mb, lane, T, lcoef[wv], t8);
+  } else if (d.bd > 8) {
+    inter_mb<u16, 1>(d, m, mb, lane, T, lcoef[wv], t8);
+  } else {
+    inter_mb<u8, 1>(d, m, mb, lane, T, lcoef[wv], t8);
+  }
 }
 
 // ---------------------------------------------------------------------- wavefront helpers
@@ -706,8 +720,8 @@ __global__ __launch_bounds__(64 * kIntraWaves) void avc_intra_kernel(const AvcDe
   if (pic >= n) return;
   const AvcDesc d = descs[pic];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, g0 = grp * kIntraWaves;
-  if (g0 >= H || d.bd > 8) return;  // (uniform over the workgroup, before any barrier; High 10:
-                                    // avc_hbd_kernel)
+  if (g0 >= H || d.bd > 8 || d.cf == 2) return;  // (uniform over the workgroup, before any barrier;
+                                                  // High 10 / 4:2:2: avc_hbd_kernel)
   __shared__ Sync sync;
   __shared__ IntraWave lds[kIntraWaves];
   __shared__ u32 tap_lut[9 * 16];  // Intra_4x4 tap word per (mode, y, x) of a 4x4 block
@@ -811,7 +825,9 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
     for (int dir = 0; dir < 2; ++dir)
       for (int e = 0; e < 4; ++e) {
         if (e == 0 && !(dir == 0 ? left : top)) continue;
-        if ((e & 1) && t8) continue;  // no 4x4 edges inside 8x8 transform blocks
+        // no 4x4 edges inside 8x8 transform blocks — except, in 4:2:2, the horizontal ones the
+        // chroma filters (avc_hbd_kernel skips them for luma)
+        if ((e & 1) && t8 && !(d.cf == 2 && dir == 1)) continue;
         const MbRec& p = e > 0 ? q : (dir == 0 ? lm : tm);
         const i16* mp = e > 0 ? mq : (dir == 0 ? ml : mt);
         for (int sg = 0; sg < 4; ++sg) {
@@ -1159,8 +1175,8 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
   const AvcDesc d = descs[pic];  // by value: SGPRs, no reloads after stores
   const int W = d.wmbs, H = d.hmbs, pitch = W * 16;
   const int g0 = grp * kDbkRows;  // first row of this workgroup
-  if (g0 >= H || d.bd > 8) return;  // (uniform over the workgroup, before any barrier; High 10:
-                                    // avc_hbd_kernel)
+  if (g0 >= H || d.bd > 8 || d.cf == 2) return;  // (uniform over the workgroup, before any barrier;
+                                                  // High 10 / 4:2:2: avc_hbd_kernel)
   __shared__ DbkSync sync;
   __shared__ DbkWave lds[kDbkWaves][2];
   __shared__ DbkXch xring[kDbkRows - 1][kDbkDepth];

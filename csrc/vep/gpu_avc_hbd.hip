@@ -1,8 +1,9 @@
-// gfx950 intra prediction + loop filter of H.264 High 10 pictures (9 / 10-bit samples, u16
-// surfaces). The 8-bit wavefront kernels (gpu_avc.hip) keep their byte-packed LDS tiles and
-// word-wide filters and skip such pictures; avc_inter_kernel handles both depths (motion
-// compensation, I_PCM and the intra residuals), and this kernel then runs the two ordered passes
-// of every High 10 picture of the round:
+// gfx950 intra prediction + loop filter of H.264 High 10 (9 / 10-bit samples, u16 surfaces) and
+// 4:2:2 (High 4:2:2, 8..10 bits, NV16 surfaces) pictures. The 8-bit 4:2:0 wavefront kernels
+// (gpu_avc.hip) keep their byte-packed LDS tiles and word-wide filters and skip such pictures;
+// avc_inter_kernel handles every depth and chroma format (motion compensation, I_PCM and the intra
+// residuals), and this kernel then runs the two ordered passes of every such picture of the
+// round:
 //
 //  * one 512-lane workgroup per picture; both passes walk the MBs in 2-skewed diagonals
 //    (step t = x + 2y): every intra neighbour of an MB (left, top-left, top, top-right) and every
@@ -11,12 +12,15 @@
 //    MBs are spread over the 8 waves (one MB per wave at a time, its 64 lanes on the MB's
 //    samples); a workgroup barrier separates the steps.
 //  * intra: the MB and its neighbours (p[-1..23, -1], p[-1, 0..15]; chroma p[-1..7, -1],
-//    p[-1, 0..7]) in a per-wave LDS tile of ints; Intra_4x4 / Intra_8x8 blocks in decoding order
-//    (16 / 64 lanes each), Intra_16x16 and chroma 4 / 2 samples per lane, then one store.
+//    p[-1, 0..7], 4:2:2 p[-1, 0..15]) in a per-wave LDS tile of ints; Intra_4x4 / Intra_8x8 blocks
+//    in decoding order (16 / 64 lanes each), Intra_16x16 and chroma 4 / 2 (4:2:2: 4) samples per
+//    lane, then one store.
 //  * loop filter: per edge (vertical edges first, left to right, then horizontal ones), lanes
-//    0-15 the luma lines and 16-31 the two chroma components' lines, read-modify-write in place;
+//    0-15 the luma lines and 16-47 the two chroma components' lines, read-modify-write in place;
 //    bS from avc_bs_kernel's AvcDbkInfo, thresholds from the records at the picture's depth
-//    (alpha / beta / tC0 << (bd - 8), QPs less the QpBdOffset bias).
+//    (alpha / beta / tC0 << (bd - 8), QPs less the QpBdOffset bias). 4:2:2 chroma: 16-row
+//    vertical edges at chroma x 0 / 4, horizontal edges at chroma rows 0, 4, 8, 12 (the odd ones
+//    inside luma 8x8 transform blocks too: luma skips them, chroma filters them).
 //
 // All sample arithmetic comes from avc_recon.h (the CPU reconstruction's, avc.cpp cpu_deblock /
 // Recon), at the picture's bit depth. High 10 is a coverage feature, not the 8-bit headline's
@@ -40,7 +44,7 @@ constexpr int kCw = 9;   // chroma tile row: x = -1..7
 
 struct HbdWave {
   int t[17 * kTw];      // luma: row 0 = p[-1..23, -1], row 1 + y = p[-1..23, y] (x > 15 unused)
-  int c[2][9 * kCw];    // chroma per component: row 0 = p[-1..7, -1], row 1 + y = p[-1..7, y]
+  int c[2][17 * kCw];   // chroma per component: row 0 = p[-1..7, -1], row 1 + y = p[-1..7, y]
 };
 
 __device__ inline void wsync() {
@@ -62,12 +66,14 @@ __device__ inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
 __device__ inline int& T(HbdWave& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
 __device__ inline int& Cc(HbdWave& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
 
+template <class P, int CF>
 __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
+  constexpr int CH = CF == 2 ? 16 : 8;  // chroma MB height
   const MbRec m = recd(d, mb);
   if (!avc::is_wave_intra(m.kind)) return;  // (skip / inter / I_PCM: written by the inter kernel)
-  const int W = d.wmbs, pitch = W * 16, mx = mb % W, my = mb / W, bd = d.bd;
-  VEP_DEV u16* Y = reinterpret_cast<VEP_DEV u16*>(d.y + d.slot_y * u64(d.target));
-  VEP_DEV u16* UV = reinterpret_cast<VEP_DEV u16*>(d.uv + d.slot_uv * u64(d.target));
+  const int W = d.wmbs, pitch = W * 16, mx = mb % W, my = mb / W, bd = sizeof(P) == 1 ? 8 : d.bd;
+  VEP_DEV P* Y = reinterpret_cast<VEP_DEV P*>(d.y + d.slot_y * u64(d.target));
+  VEP_DEV P* UV = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
   const bool A = avail(d, m, mx - 1, my), B = avail(d, m, mx, my - 1), C = avail(d, m, mx + 1, my - 1),
              D = avail(d, m, mx - 1, my - 1);
   const VEP_DEV i16* res = m.res == avc::kNoRes ? nullptr : d.res + size_t(m.res) * kAvcResSamples;
@@ -82,11 +88,11 @@ __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
   } else if (lane < 59) {  // chroma: row -1 x = -1..7 (9 per component), then the left column
     const int k = lane - 41, c = k / 9, x = k % 9 - 1;
     const bool ok = x < 0 ? D : B;
-    Cc(L, c, x, -1) = ok ? int(UV[size_t(my * 8 - 1) * pitch + (mx * 8 + x) * 2 + c]) : 128;
+    Cc(L, c, x, -1) = ok ? int(UV[size_t(my * CH - 1) * pitch + (mx * 8 + x) * 2 + c]) : 128;
   }
-  if (lane < 16) {
-    const int c = lane >> 3, y = lane & 7;
-    Cc(L, c, -1, y) = A ? int(UV[size_t(my * 8 + y) * pitch + (mx * 8 - 1) * 2 + c]) : 128;
+  if (lane < 2 * CH) {
+    const int c = lane / CH, y = lane % CH;
+    Cc(L, c, -1, y) = A ? int(UV[size_t(my * CH + y) * pitch + (mx * 8 - 1) * 2 + c]) : 128;
   }
   wsync();
   // ---- luma
@@ -152,7 +158,7 @@ __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
       wsync();
     }
   }
-  // ---- chroma (the whole 8x8 predicted from the neighbours: straight to the picture)
+  // ---- chroma (the whole 8x8 / 8x16 predicted from the neighbours: straight to the picture)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     avc::IntraChromaNb n;
@@ -160,34 +166,39 @@ __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
     n.has_top = B;
     n.has_tl = D;
     n.top[0] = Cc(L, c, -1, -1);
-    for (int k = 0; k < 8; ++k) {
-      n.top[k + 1] = Cc(L, c, k, -1);
-      n.left[k] = Cc(L, c, -1, k);
+    for (int k = 0; k < 8; ++k) n.top[k + 1] = Cc(L, c, k, -1);
+    for (int k = 0; k < CH; ++k) n.left[k] = Cc(L, c, -1, k);
+    const avc::PredConst k = m.chroma_mode == 3 ? avc::chroma_plane_const(n, CF) : avc::PredConst{0, 0, 0, 0};
+#pragma unroll
+    for (int h = 0; h < CH / 8; ++h) {
+      const int x = lane & 7, y = (lane >> 3) + 8 * h;
+      const int v = avc::chroma_pred(n, k, m.chroma_mode, x, y, bd, CF) +
+                    (res ? int(res[256 + c * 8 * CH + y * 8 + x]) : 0);
+      UV[size_t(my * CH + y) * pitch + (mx * 8 + x) * 2 + c] = P(avc::clip1(v, bd));
     }
-    const avc::PredConst k = m.chroma_mode == 3 ? avc::chroma_plane_const(n) : avc::PredConst{0, 0, 0, 0};
-    const int x = lane & 7, y = lane >> 3;
-    const int v = avc::chroma_pred(n, k, m.chroma_mode, x, y, bd) + (res ? int(res[256 + c * 64 + y * 8 + x]) : 0);
-    UV[size_t(my * 8 + y) * pitch + (mx * 8 + x) * 2 + c] = u16(avc::clip1(v, bd));
   }
   wsync();
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int x = lane & 15, y = (lane >> 4) + 4 * s;
-    Y[size_t(my * 16 + y) * pitch + mx * 16 + x] = u16(T(L, x, y));
+    Y[size_t(my * 16 + y) * pitch + mx * 16 + x] = P(T(L, x, y));
   }
 }
 
 // avc.cpp deblock_t for one MB (bS per 4-line segment from avc_bs_kernel)
+template <class P, int CF>
 __device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
+  constexpr int CH = CF == 2 ? 16 : 8;
   const MbRec q = recd(d, mb);
   if (q.dbk & 1) return;
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
   const AvcDbkInfo& info = infos[mb];
   if (!info.any) return;
-  const int W = d.wmbs, pitch = W * 16, mx = mb % W, my = mb / W, bd = d.bd;
+  const int W = d.wmbs, pitch = W * 16, mx = mb % W, my = mb / W, bd = sizeof(P) == 1 ? 8 : d.bd;
   const int qb = d.qp_bias, qcb = d.qpc_bias;
-  VEP_DEV u16* Y = reinterpret_cast<VEP_DEV u16*>(d.y + d.slot_y * u64(d.target));
-  VEP_DEV u16* UV = reinterpret_cast<VEP_DEV u16*>(d.uv + d.slot_uv * u64(d.target));
+  const bool t8 = (q.flags & avc::kMbT8x8) != 0;
+  VEP_DEV P* Y = reinterpret_cast<VEP_DEV P*>(d.y + d.slot_y * u64(d.target));
+  VEP_DEV P* UV = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
   const MbRec lm = mx > 0 ? recd(d, mb - 1) : q;
   const MbRec tm = my > 0 ? recd(d, mb - W) : q;
   auto bs_of = [&](int i) { return int((info.bs[i >> 3] >> (4 * (i & 7))) & 15u); };
@@ -195,21 +206,27 @@ __device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
     for (int e = 0; e < 4; ++e) {
       const MbRec& p = e > 0 ? q : (dir == 0 ? lm : tm);
       if (lane < 16) {
-        const int k = lane, bs = bs_of(dir * 16 + e * 4 + (k >> 2));
+        const int k = lane, bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
         if (bs) {
           const avc::EdgeParams ep = avc::edge_params(p.qp - qb, q.qp - qb, q.alpha_off, q.beta_off, bd);
           if (dir == 0) avc::filter_line(Y + size_t(my * 16 + k) * pitch + mx * 16 + 4 * e, 1, bs, ep, false, bd);
           else avc::filter_line(Y + size_t(my * 16 + 4 * e) * pitch + mx * 16 + k, long(pitch), bs, ep, false, bd);
         }
-      } else if (lane < 32 && !(e & 1)) {  // chroma edges at chroma samples 0 and 4 (luma edges 0, 2)
-        const int c = (lane - 16) >> 3, k = (lane - 16) & 7, bs = bs_of(dir * 16 + e * 4 + (k >> 1));
+      } else if (lane >= 16 && !(e & 1) || (CF == 2 && dir == 1 && lane >= 16)) {
+        // chroma edges at chroma samples 0 and 4 (luma edges 0, 2); 4:2:2: every horizontal edge
+        // (chroma rows 4e). Lines: vertical edges CH rows, horizontal edges 8 columns, per component.
+        const int nl = dir == 0 ? CH : 8, c = (lane - 16) / nl, k = (lane - 16) % nl;
+        // bS of the luma line through the chroma line: vertical edges luma row k (4:2:0: 2k),
+        // horizontal edges luma column 2k
+        const int bs = c < 2 ? bs_of(dir * 16 + e * 4 + (dir == 0 && CF == 2 ? k >> 2 : k >> 1)) : 0;
         if (bs) {
           const avc::EdgeParams ep = c == 0 ? avc::edge_params(p.qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off, bd)
                                             : avc::edge_params(p.qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off, bd);
           if (dir == 0)
-            avc::filter_line(UV + size_t(my * 8 + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, bs, ep, true, bd);
+            avc::filter_line(UV + size_t(my * CH + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, bs, ep, true, bd);
           else
-            avc::filter_line(UV + size_t(my * 8 + 2 * e) * pitch + (mx * 8 + k) * 2 + c, long(pitch), bs, ep, true, bd);
+            avc::filter_line(UV + size_t(my * CH + (CF == 2 ? 4 : 2) * e) * pitch + (mx * 8 + k) * 2 + c,
+                             long(pitch), bs, ep, true, bd);
         }
       }
       wsync();
@@ -221,18 +238,26 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   const int pic = int(blockIdx.x);
   if (pic >= n) return;
   const AvcDesc d = descs[pic];
-  if (d.bd <= 8) return;  // (uniform over the workgroup, before any barrier)
+  if (d.bd <= 8 && d.cf != 2) return;  // (uniform over the workgroup, before any barrier)
   __shared__ HbdWave lds[kHbdWaves];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int W = d.wmbs, H = d.hmbs, steps = W + 2 * (H - 1);
+  const int variant = (d.bd > 8 ? 1 : 0) | (d.cf == 2 ? 2 : 0);  // (uniform)
   for (int pass = 0; pass < 2; ++pass) {
     if (!(pass == 0 ? intra : dbk)) continue;
     for (int t = 0; t < steps; ++t) {
       const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
       for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
         const int mb = y * W + t - 2 * y;
-        if (pass == 0) intra_mb(d, lds[wave], mb, lane);
-        else deblock_mb(d, mb, lane);
+        if (pass == 0) {
+          if (variant == 1) intra_mb<u16, 1>(d, lds[wave], mb, lane);
+          else if (variant == 2) intra_mb<u8, 2>(d, lds[wave], mb, lane);
+          else intra_mb<u16, 2>(d, lds[wave], mb, lane);
+        } else {
+          if (variant == 1) deblock_mb<u16, 1>(d, mb, lane);
+          else if (variant == 2) deblock_mb<u8, 2>(d, mb, lane);
+          else deblock_mb<u16, 2>(d, mb, lane);
+        }
       }
       __syncthreads();
     }

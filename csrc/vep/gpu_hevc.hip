@@ -547,19 +547,39 @@ __global__ __launch_bounds__(256) void hevc_sao_kernel(const HevcDesc* __restric
 }
 
 // 8 samples per lane: one 16-byte load, one 8-byte store.
-__global__ __launch_bounds__(256) void narrow_kernel(const u16* __restrict__ y, const u16* __restrict__ uv,
-                                                    u8* __restrict__ y8, u8* __restrict__ uv8, size_t ny, int bd) {
+// 8-bit NV12 copy of a published slot: one thread per 8 output bytes (w is a multiple of 16, so
+// a group never straddles a row). Luma: rounded to 8 bits; chroma: NV12 row r from row r of the
+// source (4:2:0) or the average of rows 2r and 2r + 1 (4:2:2, NV16), then rounded.
+template <class P>
+__global__ __launch_bounds__(256) void narrow_kernel(const P* __restrict__ y, const P* __restrict__ uv,
+                                                    u8* __restrict__ y8, u8* __restrict__ uv8, int w, int h, int bd,
+                                                    int cf) {
+  const size_t ny = size_t(w) * size_t(h);
   const size_t g = size_t(blockIdx.x) * 256 + threadIdx.x, groups = (ny + ny / 2) / 8;
   if (g >= groups) return;
   const bool luma = g < ny / 8;
   const size_t o = luma ? g * 8 : (g - ny / 8) * 8;
-  const uint4 v = *reinterpret_cast<const uint4*>((luma ? y : uv) + o);
+  int v[8];
+  if (luma) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = int(y[o + size_t(k)]);
+  } else {
+    const size_t r = o / size_t(w), x = o % size_t(w);
+    if (cf == 2) {
+      const P* a = uv + 2 * r * size_t(w) + x;
+      const P* b = a + w;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = (int(a[k]) + int(b[k]) + 1) >> 1;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = int(uv[o + size_t(k)]);
+    }
+  }
   const int sh = bd - 8, rnd = (1 << sh) >> 1;
-  const u32 w[4] = {v.x, v.y, v.z, v.w};
   u32 out[2] = {0, 0};
+#pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const int s = int((w[k >> 1] >> (16 * (k & 1))) & 0xffffu);
-    const int n = (s + rnd) >> sh;
+    const int n = (v[k] + rnd) >> sh;
     out[k >> 2] |= u32(n > 255 ? 255 : n) << (8 * (k & 3));
   }
   *reinterpret_cast<uint2*>((luma ? y8 : uv8) + o) = make_uint2(out[0], out[1]);
@@ -567,10 +587,17 @@ __global__ __launch_bounds__(256) void narrow_kernel(const u16* __restrict__ y, 
 
 }  // namespace
 
-void launch_narrow(const u16* y, const u16* uv, u8* y8, u8* uv8, size_t n, int bd, hipStream_t s) {
+void launch_narrow(const void* y, const void* uv, u8* y8, u8* uv8, int w, int h, int bd, int cf, hipStream_t s) {
+  const size_t n = size_t(w) * size_t(h);
   if (!n) return;
   const size_t groups = (n + n / 2) / 8;
-  hipLaunchKernelGGL(narrow_kernel, dim3(unsigned((groups + 255) / 256)), dim3(256), 0, s, y, uv, y8, uv8, n, bd);
+  const dim3 grid(unsigned((groups + 255) / 256));
+  if (bd > 8)
+    hipLaunchKernelGGL(narrow_kernel<u16>, grid, dim3(256), 0, s, static_cast<const u16*>(y),
+                       static_cast<const u16*>(uv), y8, uv8, w, h, bd, cf);
+  else
+    hipLaunchKernelGGL(narrow_kernel<u8>, grid, dim3(256), 0, s, static_cast<const u8*>(y),
+                       static_cast<const u8*>(uv), y8, uv8, w, h, 8, cf);
 }
 
 void launch_hevc_mc(const HevcDesc* d_descs, int n, int total_pus, hipStream_t s) {

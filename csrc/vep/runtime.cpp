@@ -869,7 +869,7 @@ void Worker::loop() {
   }
 }
 
-void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd, bool weave) {
+void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd, bool weave, int cf) {
   const int bps = bd > 8 ? 2 : 1;
   const int wmbs = pi.coded_width / 16, hmbs = pi.coded_height / 16;
   auto& s = c.surface;
@@ -880,7 +880,7 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd,
     s.y8 = static_cast<u8*>(dev_.alloc(y8));
     s.uv8 = static_cast<u8*>(dev_.alloc(y8 / 2));
   };
-  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && s.bd == bd && c.ring_ &&
+  if (s.wmbs == wmbs && s.hmbs == hmbs && s.slots >= slots && s.bd == bd && s.cf == cf && c.ring_ &&
       c.ring_->width() == pi.width && c.ring_->height() == pi.height) {
     if (weave) scratch8();  // (only ever added: no batch in flight reads a missing scratch)
     return;
@@ -895,24 +895,26 @@ void Worker::ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd,
   s.slots = std::max(1, slots);
   s.bps = bps;
   s.bd = bd;
+  s.cf = cf;
   const size_t ysz = s.slot_y() * size_t(s.slots);
   if (dev_.gpu()) {
     s.y = static_cast<u8*>(dev_.alloc(ysz));
-    s.uv = static_cast<u8*>(dev_.alloc(ysz / 2));
+    const size_t uvsz = s.slot_uv() * size_t(s.slots);
+    s.uv = static_cast<u8*>(dev_.alloc(uvsz));
     if (bps == 2) {  // Main10 / High 10: u16 samples at the depth's black / grey
       VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.y), u16(16 << (bd - 8)), ysz / 2, stream_));
-      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.uv), u16(128 << (bd - 8)), ysz / 4, stream_));
+      VEP_HIP(hipMemsetD16Async(reinterpret_cast<hipDeviceptr_t>(s.uv), u16(128 << (bd - 8)), uvsz / 2, stream_));
       scratch8();
     } else {
-      if (weave) scratch8();
+      if (weave || cf == 2) scratch8();
       VEP_HIP(hipMemsetAsync(s.y, 16, ysz, stream_));
-      VEP_HIP(hipMemsetAsync(s.uv, 128, ysz / 2, stream_));
+      VEP_HIP(hipMemsetAsync(s.uv, 128, uvsz, stream_));
     }
     // the camera's lane may be another stream: the fill must land before its first kernel
     if (lanes_.size() > 1) VEP_HIP(hipStreamSynchronize(stream_));
   } else {
     s.host.assign(size_t(s.slots), HostSurface{});
-    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16, bd);
+    for (auto& h : s.host) h.alloc(wmbs * 16, hmbs * 16, bd, cf);
   }
   c.set_ring(std::make_shared<FrameRing>(dev_, c.ring_slots_cfg, pi.width, pi.height));
 }
@@ -1032,7 +1034,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
       if (have && (c.surface.wmbs * 16 != j.pic.coded_width ||
                    c.surface.hmbs * 16 != j.pic.coded_height || c.ring_->width() != j.pic.width ||
                    c.ring_->height() != j.pic.height || c.surface.slots < j.dpb_slots() ||
-                   c.surface.bd != j.bit_depth()))
+                   c.surface.bd != j.bit_depth() || c.surface.cf != j.chroma_format()))
         resize = true;
     }
   }
@@ -1043,7 +1045,7 @@ void Worker::prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots) {
     Camera& c = *cams_[size_t(jobs[i].cam)];
     bool weave = jobs[i].out_fields;
     for (const auto& p : jobs[i].avc) weave |= p->structure != 0;
-    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bit_depth(), weave);
+    ensure_surface(c, jobs[i].pic, jobs[i].dpb_slots(), jobs[i].bit_depth(), weave, jobs[i].chroma_format());
     slots[i] = jobs[i].has_output() ? c.ring_->begin_write() : -1;
   }
 }
@@ -1463,7 +1465,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       weave_pitch = std::max(weave_pitch, w.pitch);
       weave_h = std::max(weave_h, w.height);
     }
-    if (c->surface.bps == 2 || j.out_fields) {  // Main10 / field pair: convert / letterbox the
+    if (c->surface.narrowed() || j.out_fields) {  // Main10 / 4:2:2 / field pair: convert / letterbox the
                                                 // 8-bit frame (launch_narrow / launch_weave below)
       d.y = c->surface.y8;
       d.uv = c->surface.uv8;
@@ -1550,7 +1552,9 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.bd = a.p->bd;
       g.qp_bias = a.p->qp_bias;
       g.qpc_bias = a.p->qpc_bias;
-      VEP_CHECK(c->surface.bd == a.p->bd, "H.264: picture bit depth differs from the camera's surfaces");
+      g.cf = a.p->cf;
+      VEP_CHECK(c->surface.bd == a.p->bd && c->surface.cf == a.p->cf,
+                "H.264: picture bit depth / chroma format differs from the camera's surfaces");
       mbs += a.p->nmbs();
     }
   }
@@ -1673,7 +1677,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       max_h = std::max(max_h, apics[size_t(k)].p->hmbs);
       intra |= apics[size_t(k)].p->intra_mbs > 0;
       dbk |= apics[size_t(k)].p->deblock;
-      (apics[size_t(k)].p->bd > 8 ? wide : narrow) = true;
+      (apics[size_t(k)].p->bd > 8 || apics[size_t(k)].p->cf == 2 ? wide : narrow) = true;
     }
     gpu::launch_avc_inter(ad, np, mbs, cs);
     if (intra && narrow) gpu::launch_avc_intra(ad, np, max_h, cs);
@@ -1681,7 +1685,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       gpu::launch_avc_bs(ad, np, mbs, cs);
       if (narrow) gpu::launch_avc_deblock(ad, np, max_h, cs, dbk_packed_);
     }
-    if (wide) gpu::launch_avc_hbd(ad, np, intra, dbk, cs);  // (High 10 pictures)
+    if (wide) gpu::launch_avc_hbd(ad, np, intra, dbk, cs);  // (High 10 / 4:2:2 pictures)
   }
   for (int r = 0; r < hrounds; ++r) {
     const auto* hd2 = reinterpret_cast<const gpu::HevcDesc*>(st.d + off_hround[size_t(r)]);
@@ -1735,10 +1739,9 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const DecodeJob& j = jobs[size_t(i)];
     const Camera::Surface& sf = cams_[size_t(j.cam)]->surface;
     const size_t tgt = size_t(j.target());
-    if (sf.bps != 2) continue;
-    gpu::launch_narrow(reinterpret_cast<const u16*>(sf.y + tgt * sf.slot_y()),
-                       reinterpret_cast<const u16*>(sf.uv + tgt * sf.slot_uv()), sf.y8, sf.uv8,
-                       size_t(sf.wmbs) * 16 * sf.hmbs * 16, sf.bd, cs);
+    if (!sf.narrowed()) continue;
+    gpu::launch_narrow(sf.y + tgt * sf.slot_y(), sf.uv + tgt * sf.slot_uv(), sf.y8, sf.uv8, sf.wmbs * 16,
+                       sf.hmbs * 16, sf.bd, sf.cf, cs);
   }
   gpu::launch_decode_convert(reinterpret_cast<const gpu::DecodeDesc*>(st.d + off_desc), nout, tiles,
                              cs);
@@ -1787,8 +1790,8 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
         auto& F = c.surface.fields;  // field slots (half-height surfaces)
         if (F.size() < size_t(pic->dpb_slots)) F.resize(size_t(pic->dpb_slots));
         for (auto& h : F)
-          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16 || h.bd != pic->bd)
-            h.alloc(pic->wmbs * 16, pic->hmbs * 16, pic->bd);
+          if (h.coded_w != pic->wmbs * 16 || h.coded_h != pic->hmbs * 16 || h.bd != pic->bd || h.cf != pic->cf)
+            h.alloc(pic->wmbs * 16, pic->hmbs * 16, pic->bd, pic->cf);
         avc::cpu_reconstruct(*pic, F);
       }
       for (const auto& pic : jobs[i].hevc) hevc::cpu_execute(*pic, c.surface.host);
@@ -1804,8 +1807,9 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
       avc::weave_fields(c.surface.fields[2 * t], c.surface.fields[2 * t + 1], woven);
     }
     const HostSurface& out = jobs[i].out_fields ? woven : c.surface.host[size_t(jobs[i].target())];
-    if (out.wide()) narrow_surface(out, narrow);
-    const HostSurface& src = out.wide() ? narrow : out;
+    const bool conv = out.wide() || out.cf == 2;
+    if (conv) narrow_surface(out, narrow);
+    const HostSurface& src = conv ? narrow : out;
     cpu_nv12_to_bgr(src, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
                     jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
     if (opt_.letterbox_size > 0) {

@@ -138,6 +138,7 @@ struct DecodeJob {
     return 8;
   }
   int bytes_per_sample() const { return bit_depth() > 8 ? 2 : 1; }
+  int chroma_format() const { return !avc.empty() && avc.back()->cf == 2 ? 2 : 1; }
   int target() const { return general() ? out_slot : 0; }
 };
 
@@ -207,10 +208,11 @@ class Camera {
     int slots = 1;                 // DPB surfaces (general H.264 path); slot k at y + k * bytes
     int bps = 1;                   // bytes per sample: 2 = u16 samples (HEVC Main10, H.264 High 10)
     int bd = 8;                    // sample bit depth
+    int cf = 1;                    // chroma format: 2 = 4:2:2 (NV16: full-height chroma plane)
     u8* y = nullptr;
     u8* uv = nullptr;
-    // bps 2: the 8-bit NV12 copy of the picture being published (what the BGR conversion and
-    // the letterbox read; written by gpu::launch_narrow)
+    // bps 2 or 4:2:2: the 8-bit NV12 copy of the picture being published (what the BGR
+    // conversion and the letterbox read; written by gpu::launch_narrow)
     u8* y8 = nullptr;
     u8* uv8 = nullptr;
     // H.265 intra edge exchange (gpu::hevc_xg_words of the coded picture) and its round epoch
@@ -218,7 +220,8 @@ class Camera {
     size_t hevc_xg_words = 0;
     u32 hevc_epoch = 0;
     size_t slot_y() const { return size_t(wmbs) * 16 * hmbs * 16 * size_t(bps); }
-    size_t slot_uv() const { return slot_y() / 2; }
+    size_t slot_uv() const { return cf == 2 ? slot_y() : slot_y() / 2; }
+    bool narrowed() const { return bps == 2 || cf == 2; }  // published through y8 / uv8
     std::vector<HostSurface> host;  // CPU backend: one per slot
     std::vector<HostSurface> fields;  // CPU backend, H.264 field pictures: one per field slot
   } surface;
@@ -429,7 +432,7 @@ class Worker {
     size_t err_cap = 0;
   };
   void loop();
-  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd = 8, bool weave = false);
+  void ensure_surface(Camera& c, const PictureInfo& pi, int slots, int bd = 8, bool weave = false, int cf = 1);
   struct Batch {
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;

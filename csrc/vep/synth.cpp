@@ -129,6 +129,7 @@ SynthH264::SynthH264(const SynthConfig& cfg) : cfg_(cfg) {
       hc.interlaced = cfg.interlaced >= 1;
       hc.mono = cfg.mono;
       hc.bit_depth = cfg.bit_depth;
+      hc.chroma_format = cfg.chroma_format;
       if (cfg.interlaced == 2) {
         hc.fields = true;
         hc.cabac = false;

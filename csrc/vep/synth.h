@@ -53,6 +53,7 @@ struct SynthConfig {
   bool open_gop = false;  // H.265: CRA + RASL pictures at every IRAP after the first
   bool lossless = false;
   int bit_depth = 8;         // 10: H.265 Main10 / H.264 High 10 (main / high profiles; 10-bit samples)
+  int chroma_format = 1;     // 2: H.264 4:2:2 (High 4:2:2; main / high profiles, progressive)
   // main / high H.264: 1 = interlaced SPS coding frame pictures, 2 = every frame a field pair
   // (PAFF: CAVLC, 4x4 transforms, B pairs non-reference; overrides cabac / the 8x8 transform)
   int interlaced = 0;

@@ -301,25 +301,28 @@ def intra_16x16(top, left, has_top, has_left, mode, bd=8):
 
 
 # ------------------------------------------------------------------ 8.3.4 chroma (4:2:0)
-def intra_chroma(top, left, has_top, has_left, mode, bd=8):
-    """top = p[-1..7, -1], left = p[-1, 0..7]; mode: 0 DC, 1 horizontal, 2 vertical, 3 plane."""
+def intra_chroma(top, left, has_top, has_left, mode, bd=8, cf=1):
+    """top = p[-1..7, -1], left = p[-1, 0..MbHeightC-1]; mode: 0 DC, 1 horizontal, 2 vertical,
+    3 plane. cf = chroma_format_idc (2: 4:2:2, MbHeightC 16; 8.3.4 with xCF = 0, yCF = 4)."""
     def P(x, y):
         return top[x + 1] if y == -1 else left[y]
 
-    out = [[0] * 8 for _ in range(8)]
+    hc = 16 if cf == 2 else 8
+    ycf = 4 if cf == 2 else 0
+    out = [[0] * 8 for _ in range(hc)]
     if mode == 3:
         H = sum((k + 1) * (P(4 + k, -1) - P(2 - k, -1)) for k in range(4))
-        V = sum((k + 1) * (P(-1, 4 + k) - (P(-1, 2 - k) if 2 - k >= 0 else top[0])) for k in range(4))
-        a = 16 * (P(-1, 7) + P(7, -1))
+        V = sum((k + 1) * (P(-1, 4 + ycf + k) - P(-1, 2 + ycf - k)) for k in range(4 + ycf))  # P(-1,-1) = top[0]
+        a = 16 * (P(-1, hc - 1) + P(7, -1))
         b = (34 * H + 32) >> 6
-        c = (34 * V + 32) >> 6
-    for y in range(8):
+        c = ((34 - 29 * (cf != 1)) * V + 32) >> 6
+    for y in range(hc):
         for x in range(8):
             if mode == 0:
                 xo, yo = (x // 4) * 4, (y // 4) * 4
                 st = sum(P(xo + k, -1) for k in range(4))
                 sl = sum(P(-1, yo + k) for k in range(4))
-                if (xo, yo) in ((0, 0), (4, 4)):
+                if (xo == 0 and yo == 0) or (xo > 0 and yo > 0):  # (8.3.4.1-3: chroma4x4BlkIdx rules)
                     v = (st + sl + 4) >> 3 if has_top and has_left else (sl + 2) >> 2 if has_left else \
                         (st + 2) >> 2 if has_top else 1 << (bd - 1)
                 elif xo > 0:
@@ -331,9 +334,26 @@ def intra_chroma(top, left, has_top, has_left, mode, bd=8):
             elif mode == 2:
                 v = P(x, -1)
             else:
-                v = clip1((a + b * (x - 3) + c * (y - 3) + 16) >> 5, bd)
+                v = clip1((a + b * (x - 3) + c * (y - 3 - ycf) + 16) >> 5, bd)
             out[y][x] = v
     return out
+
+
+# ------------------------------------------------------------------ 8.5.11 4:2:2 chroma DC
+CHROMA422_DC_C = [[0, 2], [1, 5], [3, 6], [4, 7]]  # c[i][j] = chromaList[CHROMA422_DC_C[i][j]] (8-330)
+
+
+def chroma422_dc(levels, qpdc, ls):
+    """levels: the 8 chroma DC levels in parsing order; qpdc = QP'C + 3; ls = LevelScale4x4(qpdc %
+    6, 0, 0). Returns dcC[i][j] (4 rows x 2 columns of 4x4 chroma blocks)."""
+    c = [[levels[CHROMA422_DC_C[i][j]] for j in range(2)] for i in range(4)]
+    A = [[1, 1, 1, 1], [1, 1, -1, -1], [1, -1, -1, 1], [1, -1, 1, -1]]
+    B = [[1, 1], [1, -1]]
+    ac = [[sum(A[i][k] * c[k][j] for k in range(4)) for j in range(2)] for i in range(4)]
+    f = [[sum(ac[i][k] * B[k][j] for k in range(2)) for j in range(2)] for i in range(4)]
+    if qpdc >= 36:
+        return [[(f[i][j] * ls) << (qpdc // 6 - 6) for j in range(2)] for i in range(4)]
+    return [[(f[i][j] * ls + 2 ** (5 - qpdc // 6)) >> (6 - qpdc // 6) for j in range(2)] for i in range(4)]
 
 
 # ------------------------------------------------------------------ 8.4.2.2 interpolation
