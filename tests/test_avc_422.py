@@ -140,3 +140,41 @@ def test_422_camera_cpu_backend(native, kw):
 def test_422_gpu_bit_exact(native, w, h, n, kw):
     """gfx950: NV16 surfaces, avc_inter_kernel<P, 2> + avc_hbd_kernel<P, 2>, narrow + convert."""
     assert run_camera(native, 0, w, h, n, **kw) >= n // 2
+
+
+@pytest.mark.parametrize("kw", [dict(chroma_format=2), dict(chroma_format=2, bit_depth=10, cabac=False),
+                                dict(bit_depth=10)], ids=["422", "422-10bit-cavlc", "high10"])
+def test_422_and_high10_corruption_never_crashes(native, kw):
+    """Bit flips in 4:2:2 / High 10 slices: the decoder raises or decodes (never crashes, never
+    writes outside its pools: every record is validated), and recovers at the next IDR."""
+    import random
+
+    rnd = random.Random(11)
+    enc = high_encoder(native, 176, 144, bframes=2, gop=8, seed=4, coverage=True, **kw)
+    aus = [enc.next() for _ in range(24)]
+    clean = native.CpuDecoder()
+    want = {}
+    for a in aus:
+        clean.decode(a)
+        for pts, (y, uv) in clean.frames():
+            want[pts] = (y, uv)
+    for trial in range(10):
+        dec = native.CpuDecoder()
+        bad = rnd.randrange(1, 14)
+        for i, a in enumerate(aus):
+            if i == bad:
+                nals = [bytearray(n) for n in a.nals()]
+                sl = [k for k, x in enumerate(nals) if (x[0] & 0x1F) in (1, 5)][0]
+                for _ in range(rnd.randint(1, 5)):
+                    pos = rnd.randrange(3, len(nals[sl]))
+                    nals[sl][pos] ^= 1 << rnd.randrange(8)
+                a = native.AccessUnit.from_nals([bytes(x) for x in nals], pts=a.pts, dts=a.dts, keyframe=a.keyframe)
+            try:
+                dec.decode(a)
+            except (native.NativeError, native.UnsupportedStream):
+                continue
+            if i >= 16:
+                for pts, (y, uv) in dec.frames():
+                    if pts < 18 * 3000:
+                        continue
+                    assert np.array_equal(y, want[pts][0]) and np.array_equal(uv, want[pts][1]), f"trial {trial}"
