@@ -204,6 +204,10 @@ struct AvcDesc {
   i32 qp_bias, qpc_bias;  // MbRec::qp / qpc bias (QpBdOffsetY / C)
   i32 cf;              // chroma format: 1 (or 0: grey chroma) 4:2:0, 2 = 4:2:2 (NV16 slots; intra +
                        // deblocking in avc_hbd_kernel)
+  // pool sizes (i16 coefficients, intra residual slots): the High 10 / 4:2:2 paths bound-check
+  // every picture / pool access against them and report a violation in *err (bits 8..15)
+  // instead of touching memory outside
+  u32 ncoef, nres;
   VEP_DEV u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
                        // tagged words per MB of every workgroup's last row (intra wavefront:
                        // words 0..7, zeroed by avc_inter_kernel; deblocking: all, zeroed by

@@ -161,6 +161,15 @@ __device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int la
   VEP_DEV P* tuv = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
   auto yref = [&](int s) { return reinterpret_cast<const VEP_DEV P*>(d.y + d.slot_y * u64(s)); };
   auto uvref = [&](int s) { return reinterpret_cast<const VEP_DEV P*>(d.uv + d.slot_uv * u64(s)); };
+  // High 10 / 4:2:2 (not the 8-bit 4:2:0 hot path): bound checks of the pools, reported in *err
+  constexpr bool kCheck = sizeof(P) == 2 || CF == 2;
+  if (kCheck) {
+    const u32 need = m.kind == avc::kIPcm ? u32((256 + 2 * CS) * sizeof(P) / 2) : 0u;
+    if (u64(m.coef) + need > u64(d.ncoef)) {
+      atomicOr(d.err, 0x4000u);
+      return;
+    }
+  }
   if (m.kind == avc::kIPcm) {
     const VEP_DEV P* s = reinterpret_cast<const VEP_DEV P*>(d.coefs + m.coef);  // (u16: 384 samples)
 #pragma unroll
@@ -269,6 +278,10 @@ __global__ __launch_bounds__(256) void avc_inter_kernel(const AvcDesc* __restric
     // Intra MB: its residual samples do not depend on the prediction, so they are computed here
     // in parallel and the intra wavefront only adds them (same layout as IntraWave::res).
     if (m.res == avc::kNoRes) return;
+    if ((d.bd > 8 || d.cf == 2) && m.res >= d.nres) {  // (High 10 / 4:2:2: bound check)
+      atomicOr(d.err, 0x8000u);
+      return;
+    }
     i16* r = d.res + size_t(m.res) * kAvcResSamples;
     i16* D = lcoef[wv];
     expand_coefs_wave(d, m, lane, D);

@@ -63,6 +63,16 @@ __device__ inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
   return !(d.constrained && !avc::is_intra(n.kind));
 }
 
+// Bound check of a picture index (luma: wpx * hpx samples; chroma plane: wpx * chroma rows): a
+// violation is reported in *err (bits 8..15, AvcDesc) and the access skipped, never performed.
+__device__ inline bool oob(const AvcDesc& d, long i, long n, u32 bit) {
+  if (i >= 0 && i < n) return false;
+  atomicOr(d.err, bit);
+  return true;
+}
+constexpr u32 kOobLumaLoad = 0x100, kOobChromaLoad = 0x200, kOobRes = 0x400, kOobStore = 0x800,
+              kOobDbkLuma = 0x1000, kOobDbkChroma = 0x2000;
+
 __device__ inline int& T(HbdWave& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
 __device__ inline int& Cc(HbdWave& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
 
@@ -76,23 +86,29 @@ __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
   VEP_DEV P* UV = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
   const bool A = avail(d, m, mx - 1, my), B = avail(d, m, mx, my - 1), C = avail(d, m, mx + 1, my - 1),
              D = avail(d, m, mx - 1, my - 1);
+  const long ny = long(pitch) * d.hmbs * 16, nuv = long(pitch) * d.hmbs * CH;
+  if (m.res != avc::kNoRes && oob(d, long(m.res), long(d.nres), kOobRes)) return;
   const VEP_DEV i16* res = m.res == avc::kNoRes ? nullptr : d.res + size_t(m.res) * kAvcResSamples;
   // ---- neighbours into the tile (128: an unavailable side, as the CPU's neighbour arrays)
   if (lane < 25) {  // top row x = -1..23
     const int x = lane - 1;
     const bool ok = x < 0 ? D : (x < 16 ? B : C);
-    T(L, x, -1) = ok ? int(Y[size_t(my * 16 - 1) * pitch + mx * 16 + x]) : 128;
+    const long i = long(my * 16 - 1) * pitch + mx * 16 + x;
+    T(L, x, -1) = ok && !oob(d, i, ny, kOobLumaLoad) ? int(Y[i]) : 128;
   } else if (lane < 41) {  // left column
     const int y = lane - 25;
-    T(L, -1, y) = A ? int(Y[size_t(my * 16 + y) * pitch + mx * 16 - 1]) : 128;
+    const long i = long(my * 16 + y) * pitch + mx * 16 - 1;
+    T(L, -1, y) = A && !oob(d, i, ny, kOobLumaLoad) ? int(Y[i]) : 128;
   } else if (lane < 59) {  // chroma: row -1 x = -1..7 (9 per component), then the left column
     const int k = lane - 41, c = k / 9, x = k % 9 - 1;
     const bool ok = x < 0 ? D : B;
-    Cc(L, c, x, -1) = ok ? int(UV[size_t(my * CH - 1) * pitch + (mx * 8 + x) * 2 + c]) : 128;
+    const long i = long(my * CH - 1) * pitch + (mx * 8 + x) * 2 + c;
+    Cc(L, c, x, -1) = ok && !oob(d, i, nuv, kOobChromaLoad) ? int(UV[i]) : 128;
   }
   if (lane < 2 * CH) {
     const int c = lane / CH, y = lane % CH;
-    Cc(L, c, -1, y) = A ? int(UV[size_t(my * CH + y) * pitch + (mx * 8 - 1) * 2 + c]) : 128;
+    const long i = long(my * CH + y) * pitch + (mx * 8 - 1) * 2 + c;
+    Cc(L, c, -1, y) = A && !oob(d, i, nuv, kOobChromaLoad) ? int(UV[i]) : 128;
   }
   wsync();
   // ---- luma
@@ -174,14 +190,16 @@ __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
       const int x = lane & 7, y = (lane >> 3) + 8 * h;
       const int v = avc::chroma_pred(n, k, m.chroma_mode, x, y, bd, CF) +
                     (res ? int(res[256 + c * 8 * CH + y * 8 + x]) : 0);
-      UV[size_t(my * CH + y) * pitch + (mx * 8 + x) * 2 + c] = P(avc::clip1(v, bd));
+      const long i = long(my * CH + y) * pitch + (mx * 8 + x) * 2 + c;
+      if (!oob(d, i, nuv, kOobStore)) UV[i] = P(avc::clip1(v, bd));
     }
   }
   wsync();
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     const int x = lane & 15, y = (lane >> 4) + 4 * s;
-    Y[size_t(my * 16 + y) * pitch + mx * 16 + x] = P(T(L, x, y));
+    const long i = long(my * 16 + y) * pitch + mx * 16 + x;
+    if (!oob(d, i, ny, kOobStore)) Y[i] = P(T(L, x, y));
   }
 }
 
@@ -201,6 +219,11 @@ __device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
   VEP_DEV P* UV = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
   const MbRec lm = mx > 0 ? recd(d, mb - 1) : q;
   const MbRec tm = my > 0 ? recd(d, mb - W) : q;
+  const long ny = long(pitch) * d.hmbs * 16, nuv = long(pitch) * d.hmbs * CH;
+  // (a line at index i across an edge with stride st touches i - n * st .. i + (n - 1) * st)
+  auto line_ok = [&](long i, long st, int n, long lim, u32 bit) {
+    return !oob(d, i - n * st, lim, bit) && !oob(d, i + (n - 1) * st, lim, bit);
+  };
   auto bs_of = [&](int i) { return int((info.bs[i >> 3] >> (4 * (i & 7))) & 15u); };
   for (int dir = 0; dir < 2; ++dir)
     for (int e = 0; e < 4; ++e) {
@@ -209,8 +232,9 @@ __device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
         const int k = lane, bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
         if (bs) {
           const avc::EdgeParams ep = avc::edge_params(p.qp - qb, q.qp - qb, q.alpha_off, q.beta_off, bd);
-          if (dir == 0) avc::filter_line(Y + size_t(my * 16 + k) * pitch + mx * 16 + 4 * e, 1, bs, ep, false, bd);
-          else avc::filter_line(Y + size_t(my * 16 + 4 * e) * pitch + mx * 16 + k, long(pitch), bs, ep, false, bd);
+          const long i = dir == 0 ? long(my * 16 + k) * pitch + mx * 16 + 4 * e : long(my * 16 + 4 * e) * pitch + mx * 16 + k;
+          const long st = dir == 0 ? 1 : long(pitch);
+          if (line_ok(i, st, 4, ny, kOobDbkLuma)) avc::filter_line(Y + i, st, bs, ep, false, bd);
         }
       } else if (lane >= 16 && !(e & 1) || (CF == 2 && dir == 1 && lane >= 16)) {
         // chroma edges at chroma samples 0 and 4 (luma edges 0, 2); 4:2:2: every horizontal edge
@@ -222,11 +246,10 @@ __device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
         if (bs) {
           const avc::EdgeParams ep = c == 0 ? avc::edge_params(p.qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off, bd)
                                             : avc::edge_params(p.qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off, bd);
-          if (dir == 0)
-            avc::filter_line(UV + size_t(my * CH + k) * pitch + (mx * 8 + 2 * e) * 2 + c, 2, bs, ep, true, bd);
-          else
-            avc::filter_line(UV + size_t(my * CH + (CF == 2 ? 4 : 2) * e) * pitch + (mx * 8 + k) * 2 + c,
-                             long(pitch), bs, ep, true, bd);
+          const long i = dir == 0 ? long(my * CH + k) * pitch + (mx * 8 + 2 * e) * 2 + c
+                                  : long(my * CH + (CF == 2 ? 4 : 2) * e) * pitch + (mx * 8 + k) * 2 + c;
+          const long st = dir == 0 ? 2 : long(pitch);
+          if (line_ok(i, st, 2, nuv, kOobDbkChroma)) avc::filter_line(UV + i, st, bs, ep, true, bd);
         }
       }
       wsync();

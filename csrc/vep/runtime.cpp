@@ -1553,6 +1553,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.qp_bias = a.p->qp_bias;
       g.qpc_bias = a.p->qpc_bias;
       g.cf = a.p->cf;
+      g.ncoef = u32(a.p->coefs.size());
+      g.nres = u32(a.p->intra_res);
       VEP_CHECK(c->surface.bd == a.p->bd && c->surface.cf == a.p->cf,
                 "H.264: picture bit depth / chroma format differs from the camera's surfaces");
       mbs += a.p->nmbs();
@@ -1905,8 +1907,14 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       // bit 1: a reconstruction wavefront timed out waiting for a neighbour (gpu_avc.hip)
       if (err[i] & 2u)
         cp->logs.add(true, "GPU reconstruction wavefront timed out; frame dropped, waiting for the next keyframe");
-      if (err[i] & ~2u)
+      if (err[i] & 0xFF00u) {  // (gpu_avc.hip / gpu_avc_hbd.hip bound checks)
+        char b[96];
+        std::snprintf(b, sizeof b, "GPU reconstruction bound check failed (0x%x); frame dropped", err[i]);
+        cp->logs.add(true, b);
+        std::fprintf(stderr, "vep: camera %s: %s\n", cp->name().c_str(), b);
+      } else if (err[i] & ~2u) {
         cp->logs.add(true, "corrupt keyframe: I_PCM header check failed; waiting for the next keyframe");
+      }
       cp->broken_ = true;
       cp->ring_->abort(slots[i]);
       continue;
