@@ -255,7 +255,8 @@ void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s);
 void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s, int packed = 1);
 // High 10 pictures of the round (AvcDesc::bd > 8; the 8-bit wavefronts skip them): intra
 // prediction, then (dbk: after launch_avc_bs) the loop filter. gpu_avc_hbd.hip
-void launch_avc_hbd(const AvcDesc* d_descs, int n, bool intra, bool dbk, hipStream_t s);
+// variants: bit 0 High 10 4:2:0, bit 1 8-bit 4:2:2, bit 2 High 10 4:2:2 pictures present
+void launch_avc_hbd(const AvcDesc* d_descs, int n, bool intra, bool dbk, int variants, hipStream_t s);
 
 enum ChwDtype : int { kChwNone = 0, kChwF16 = 1, kChwBF16 = 2, kChwF32 = 3 };
 

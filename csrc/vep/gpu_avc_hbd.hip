@@ -47,16 +47,21 @@ struct HbdWave {
   int c[2][17 * kCw];   // chroma per component: row 0 = p[-1..7, -1], row 1 + y = p[-1..7, y]
 };
 
-__device__ inline void wsync() {
+// (The per-MB functions are host-callable too: csrc/tests/hbd_emu.cpp runs them lane by lane on
+// the CPU under AddressSanitizer.)
+#define VEP_HBD_FN __host__ __device__
+VEP_HBD_FN inline void wsync() {
+#if defined(__HIP_DEVICE_COMPILE__)
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (global RMW of the filter steps too)
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#endif
 }
 
-__device__ inline const MbRec& recd(const AvcDesc& d, int mb) { return static_cast<const MbRec*>(d.mbs)[mb]; }
+VEP_HBD_FN inline const MbRec& recd(const AvcDesc& d, int mb) { return static_cast<const MbRec*>(d.mbs)[mb]; }
 
 // avc.cpp intra_avail
-__device__ inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
+VEP_HBD_FN inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
   if (nx < 0 || ny < 0 || nx >= d.wmbs) return false;
   const MbRec& n = recd(d, ny * d.wmbs + nx);
   if (n.slice != m.slice) return false;
@@ -65,19 +70,23 @@ __device__ inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
 
 // Bound check of a picture index (luma: wpx * hpx samples; chroma plane: wpx * chroma rows): a
 // violation is reported in *err (bits 8..15, AvcDesc) and the access skipped, never performed.
-__device__ inline bool oob(const AvcDesc& d, long i, long n, u32 bit) {
+VEP_HBD_FN inline bool oob(const AvcDesc& d, long i, long n, u32 bit) {
   if (i >= 0 && i < n) return false;
+#if defined(__HIP_DEVICE_COMPILE__)
   atomicOr(d.err, bit);
+#else
+  *d.err |= bit;
+#endif
   return true;
 }
 constexpr u32 kOobLumaLoad = 0x100, kOobChromaLoad = 0x200, kOobRes = 0x400, kOobStore = 0x800,
               kOobDbkLuma = 0x1000, kOobDbkChroma = 0x2000;
 
-__device__ inline int& T(HbdWave& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
-__device__ inline int& Cc(HbdWave& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
+VEP_HBD_FN inline int& T(HbdWave& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
+VEP_HBD_FN inline int& Cc(HbdWave& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
 
 template <class P, int CF>
-__device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
+VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
   constexpr int CH = CF == 2 ? 16 : 8;  // chroma MB height
   const MbRec m = recd(d, mb);
   if (!avc::is_wave_intra(m.kind)) return;  // (skip / inter / I_PCM: written by the inter kernel)
@@ -205,7 +214,7 @@ __device__ void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
 
 // avc.cpp deblock_t for one MB (bS per 4-line segment from avc_bs_kernel)
 template <class P, int CF>
-__device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
+VEP_HBD_FN void deblock_mb(const AvcDesc& d, int mb, int lane) {
   constexpr int CH = CF == 2 ? 16 : 8;
   const MbRec q = recd(d, mb);
   if (q.dbk & 1) return;
@@ -256,44 +265,48 @@ __device__ void deblock_mb(const AvcDesc& d, int mb, int lane) {
     }
 }
 
+#ifndef VEP_HBD_EMU  // (csrc/tests/hbd_emu.cpp: the per-MB functions only)
+// One instantiation per (sample type, chroma format): each workgroup takes one picture of the
+// round and returns at once unless the picture is of its variant.
+template <class P, int CF>
 __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* __restrict__ descs, int n,
                                                                   int intra, int dbk) {
   const int pic = int(blockIdx.x);
   if (pic >= n) return;
   const AvcDesc d = descs[pic];
-  if (d.bd <= 8 && d.cf != 2) return;  // (uniform over the workgroup, before any barrier)
+  // (uniform over the workgroup, before any barrier)
+  if ((d.bd > 8) != (sizeof(P) == 2) || (d.cf == 2) != (CF == 2)) return;
   __shared__ HbdWave lds[kHbdWaves];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int W = d.wmbs, H = d.hmbs, steps = W + 2 * (H - 1);
-  const int variant = (d.bd > 8 ? 1 : 0) | (d.cf == 2 ? 2 : 0);  // (uniform)
   for (int pass = 0; pass < 2; ++pass) {
     if (!(pass == 0 ? intra : dbk)) continue;
     for (int t = 0; t < steps; ++t) {
       const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
       for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
         const int mb = y * W + t - 2 * y;
-        if (pass == 0) {
-          if (variant == 1) intra_mb<u16, 1>(d, lds[wave], mb, lane);
-          else if (variant == 2) intra_mb<u8, 2>(d, lds[wave], mb, lane);
-          else intra_mb<u16, 2>(d, lds[wave], mb, lane);
-        } else {
-          if (variant == 1) deblock_mb<u16, 1>(d, mb, lane);
-          else if (variant == 2) deblock_mb<u8, 2>(d, mb, lane);
-          else deblock_mb<u16, 2>(d, mb, lane);
-        }
+        if (pass == 0) intra_mb<P, CF>(d, lds[wave], mb, lane);
+        else deblock_mb<P, CF>(d, mb, lane);
       }
       __syncthreads();
     }
   }
 }
 
+#endif  // VEP_HBD_EMU
+
 }  // namespace
 
-void launch_avc_hbd(const AvcDesc* d_descs, int n, bool intra, bool dbk, hipStream_t s) {
+#ifndef VEP_HBD_EMU
+void launch_avc_hbd(const AvcDesc* d_descs, int n, bool intra, bool dbk, int variants, hipStream_t s) {
   if (n <= 0 || !(intra || dbk)) return;
-  hipLaunchKernelGGL(avc_hbd_kernel, dim3(unsigned(n)), dim3(64 * kHbdWaves), 0, s, d_descs, n, intra ? 1 : 0,
-                     dbk ? 1 : 0);
+  const dim3 grid{unsigned(n)}, block{64 * kHbdWaves};
+  const int in = intra ? 1 : 0, db = dbk ? 1 : 0;
+  if (variants & 1) hipLaunchKernelGGL((avc_hbd_kernel<u16, 1>), grid, block, 0, s, d_descs, n, in, db);
+  if (variants & 2) hipLaunchKernelGGL((avc_hbd_kernel<u8, 2>), grid, block, 0, s, d_descs, n, in, db);
+  if (variants & 4) hipLaunchKernelGGL((avc_hbd_kernel<u16, 2>), grid, block, 0, s, d_descs, n, in, db);
   VEP_HIP(hipGetLastError());
 }
+#endif  // VEP_HBD_EMU
 
 }  // namespace vep::gpu

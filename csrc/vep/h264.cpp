@@ -145,9 +145,8 @@ Sps parse_sps(const u8* rbsp, size_t n) {
   if (!s.frame_mbs_only) s.mbaff = br.u1();
   s.direct_8x8 = br.u1();
   if (br.u1()) {  // frame_cropping_flag
-    int cx = (s.chroma_format_idc == 0 || s.chroma_format_idc == 3) ? 1 : 2;
-    int cy = ((s.chroma_format_idc == 1) ? 2 : 1) * (s.frame_mbs_only ? 1 : 2);
-    if (s.chroma_format_idc == 0) cy = s.frame_mbs_only ? 1 : 2;
+    const int cx = (s.chroma_format_idc == 0 || s.chroma_format_idc == 3) ? 1 : 2;
+    const int cy = ((s.chroma_format_idc == 1) ? 2 : 1) * (s.frame_mbs_only ? 1 : 2);
     s.crop_left = br.ue() * cx;
     s.crop_right = br.ue() * cx;
     s.crop_top = br.ue() * cy;
@@ -396,8 +395,9 @@ std::vector<u8> write_sps(const Sps& s) {
   bool crop = s.crop_left || s.crop_right || s.crop_top || s.crop_bottom;
   bw.u1(crop);
   if (crop) {
-    const int cx = s.chroma_format_idc == 0 ? 1 : 2;  // CropUnitX / Y (§7.4.2.1.1)
-    const int cy = (s.chroma_format_idc == 0 ? 1 : 2) * (s.frame_mbs_only ? 1 : 2);
+    // CropUnitX / Y (§7.4.2.1.1): SubWidthC / SubHeightC (4:2:2: 2 / 1; 4:0:0 and 4:4:4: 1 / 1)
+    const int cx = s.chroma_format_idc == 0 || s.chroma_format_idc == 3 ? 1 : 2;
+    const int cy = (s.chroma_format_idc == 1 ? 2 : 1) * (s.frame_mbs_only ? 1 : 2);
     bw.ue(s.crop_left / cx);
     bw.ue(s.crop_right / cx);
     bw.ue(s.crop_top / cy);

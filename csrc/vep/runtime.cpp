@@ -1672,14 +1672,17 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
     const auto* ad = reinterpret_cast<const gpu::AvcDesc*>(st.d + off_round[size_t(r)]);
     const int np = int(round_pics[size_t(r)].size());
     int mbs = 0;
-    bool intra = false, dbk = false, wide = false, narrow = false;
+    bool intra = false, dbk = false, narrow = false;
+    int variants = 0;  // High 10 / 4:2:2 pictures by kind (launch_avc_hbd)
     int max_h = 0;
     for (int k : round_pics[size_t(r)]) {
       mbs += apics[size_t(k)].p->nmbs();
       max_h = std::max(max_h, apics[size_t(k)].p->hmbs);
       intra |= apics[size_t(k)].p->intra_mbs > 0;
       dbk |= apics[size_t(k)].p->deblock;
-      (apics[size_t(k)].p->bd > 8 || apics[size_t(k)].p->cf == 2 ? wide : narrow) = true;
+      const avc::Picture& ap = *apics[size_t(k)].p;
+      if (ap.bd > 8 || ap.cf == 2) variants |= ap.cf != 2 ? 1 : (ap.bd > 8 ? 4 : 2);
+      else narrow = true;
     }
     gpu::launch_avc_inter(ad, np, mbs, cs);
     if (intra && narrow) gpu::launch_avc_intra(ad, np, max_h, cs);
@@ -1687,7 +1690,7 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       gpu::launch_avc_bs(ad, np, mbs, cs);
       if (narrow) gpu::launch_avc_deblock(ad, np, max_h, cs, dbk_packed_);
     }
-    if (wide) gpu::launch_avc_hbd(ad, np, intra, dbk, cs);  // (High 10 / 4:2:2 pictures)
+    if (variants) gpu::launch_avc_hbd(ad, np, intra, dbk, variants, cs);  // (High 10 / 4:2:2 pictures)
   }
   for (int r = 0; r < hrounds; ++r) {
     const auto* hd2 = reinterpret_cast<const gpu::HevcDesc*>(st.d + off_hround[size_t(r)]);

@@ -130,6 +130,12 @@ def test_422_camera_cpu_backend(native, kw):
     assert run_camera(native, -1, 176, 144, 12, **kw) >= 8
 
 
+def test_422_cropping_cpu_backend(native):
+    """A height that is not a multiple of 16: 4:2:2's CropUnitY is 1 (SubHeightC), not 4:2:0's 2,
+    so 1088 -> 1080 is frame_crop_bottom_offset 8 (writer and parser, §7.4.2.1.1)."""
+    assert run_camera(native, -1, 176, 136, 8, bframes=1) >= 4
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("w,h,n,kw", [
     (176, 144, 14, dict(coverage=True, bframes=2, slices=2)),
