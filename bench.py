@@ -91,6 +91,9 @@ def parse_args():
     ap.add_argument("--bit-depth", type=int, choices=[8, 10], default=8,
                     help="10: H.265 Main10 / H.264 High 10 (main / high profiles, progressive) streams (u16 "
                          "surfaces on the GPU, narrowed to 8 bits for BGR24)")
+    ap.add_argument("--chroma-format", type=int, choices=[1, 2], default=1,
+                    help="h264 main/high, progressive: 2 = High 4:2:2 streams (NV16 surfaces, 4:2:0 display "
+                         "conversion for BGR24)")
     ap.add_argument("--threads", type=int, default=0,
                     help="host parse threads per rank (0 = the rank's host domain: its part of the CPU "
                          "budget - 1, pinned to its GPU's NUMA-local CPUs)")
@@ -272,7 +275,9 @@ def describe_streams(a, compressed):
         return (f"{a.profile.capitalize()} profile interlaced, every frame a field pair (PAFF), CAVLC "
                 f"I/P{'/B' if a.bframes else ''} fields{f', {a.bframes} B pairs per mini-GOP' if a.bframes else ''}")
     if compressed:
-        return (f"{'High 10' if a.bit_depth == 10 and a.profile != 'baseline' else a.profile.capitalize()} profile "
+        hp = ("High 4:2:2" if a.chroma_format == 2 else "High 10" if a.bit_depth == 10 else a.profile.capitalize()) \
+            if a.profile != "baseline" else a.profile.capitalize()
+        return (f"{hp} profile{' 10-bit' if a.chroma_format == 2 and a.bit_depth == 10 else ''} "
                 f"{'CAVLC' if a.cavlc else 'CABAC'} I/P/B, "
                 f"{a.bframes} B per mini-GOP{' (pyramid)' if a.bframes >= 2 else ''}"
                 f"{', 8x8 transform + Intra_8x8' if a.profile == 'high' else ''}")
@@ -286,6 +291,7 @@ def make_cfg(vep, a, rank, compressed):
     cfg.seed = 1 + rank * 100003
     cfg.slices = a.slices
     cfg.bit_depth = a.bit_depth if (a.codec == "h265" or (a.profile != "baseline" and a.interlaced == 0)) else 8
+    cfg.chroma_format = a.chroma_format if (a.codec == "h264" and a.profile != "baseline" and a.interlaced == 0) else 1
     if compressed:
         cfg.compressed = True
         cfg.qp, cfg.noise, cfg.temporal_noise, cfg.refs = a.qp, a.noise, a.temporal_noise, a.refs
@@ -491,6 +497,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         sh0 = worker.shed
         rg0 = worker.records_gathered
         g0 = worker.gpu_ms_total
+        bt0, mg0 = worker.batches, worker.merged
         hostprof = os.environ.get("VEP_HOSTPROF")  # path: SIGPROF samples of every thread, timed region
         if hostprof:
             vep.hostprof_start(1000)
@@ -519,6 +526,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         rg1 = worker.records_gathered
         pictures, frames, dropped = worker.pictures - p0, worker.frames - f0, worker.dropped - d0
         shed = worker.shed - sh0
+        batches, merged = worker.batches - bt0, worker.merged - mg0
         s1 = farm.stats()
         cpu1 = thread_cpu()
         if world > 1:
@@ -647,6 +655,8 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             "decode_errors": errors,
             "concurrent_clients": a.clients,
             "rank0_gpu_kernel_ms_per_step": round(gpu_ms / a.steps, 4),
+            "rank0_pictures_per_launch": round(pictures / max(1, batches), 3),
+            "rank0_launches_merged": merged,
             "rank0_record_bytes_gathered_per_step": (rg1 - rg0) // max(1, a.steps),
             "keyframe_coalesce_window_us": worker.kf_window_us if a.keyframe_only else None,
             "parse_threads_per_rank": a.threads,

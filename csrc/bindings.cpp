@@ -1310,7 +1310,8 @@ PYBIND11_MODULE(_vep, m) {
       .def("avc_profile", [](Worker& w) {
         static const char* kNames[gpu::kAvcProfSlots] = {
             "intra_wait", "intra_load", "intra_luma", "intra_chroma", "intra_store", "intra_mbs",
-            "dbk_wait", "dbk_load", "dbk_filter", "dbk_store", "dbk_mbs", "intra_residual"};
+            "dbk_wait", "dbk_load", "dbk_filter", "dbk_store", "dbk_mbs", "intra_residual",
+            "hbd_intra", "hbd_dbk", "hbd_barrier", "hbd_pictures"};
         const std::vector<u64> v = w.avc_profile();
         py::dict d;
         for (int i = 0; i < gpu::kAvcProfSlots; ++i) d[kNames[i]] = v[size_t(i)];
@@ -1517,6 +1518,8 @@ PYBIND11_MODULE(_vep, m) {
       .def_property_readonly("frames", &Worker::frames)
       .def_property_readonly("dropped", &Worker::dropped)
       .def_property_readonly("shed", &Worker::shed)
+      .def_property_readonly("merged", &Worker::merged)
+      .def("hold_lanes", &Worker::hold_lanes, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("pictures", &Worker::pictures)
       .def_property_readonly("gpu_ms_total", &Worker::gpu_ms_total)
       .def_property_readonly("bytes_inplace", &Worker::bytes_inplace)

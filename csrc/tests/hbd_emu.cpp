@@ -51,6 +51,18 @@ static void bs_info(const avc::Picture& pic, int cf, std::vector<AvcDbkInfo>& ou
           }
         }
       info.any = (info.bs[0] | info.bs[1] | info.bs[2] | info.bs[3]) ? 1 : 0;
+      const avc::MbRec* ps[3] = {&lm, &tm, &q};
+      for (int k = 0; k < 3; ++k) {
+        const avc::EdgeParams ep[3] = {
+            avc::edge_params(ps[k]->qp - pic.qp_bias, q.qp - pic.qp_bias, q.alpha_off, q.beta_off),
+            avc::edge_params(ps[k]->qpc - pic.qpc_bias, q.qpc - pic.qpc_bias, q.alpha_off, q.beta_off),
+            avc::edge_params(ps[k]->qpc2 - pic.qpc_bias, q.qpc2 - pic.qpc_bias, q.alpha_off, q.beta_off)};
+        for (int c = 0; c < 3; ++c) {
+          info.alpha[c * 3 + k] = u8(ep[c].alpha);
+          info.beta[c * 3 + k] = u8(ep[c].beta);
+          for (int j = 0; j < 3; ++j) info.tc0[c * 3 + k][j] = u8(ep[c].tc0[j]);
+        }
+      }
     }
     out[size_t(mb)] = info;
   }
@@ -87,6 +99,8 @@ static int run_picture(const avc::Picture& pic) {
   d.cf = pic.cf;
   d.ncoef = u32(pic.coefs.size());
   d.nres = u32(pic.intra_res);
+  d.intra_mbs = pic.intra_mbs;
+  d.deblock = pic.deblock ? 1 : 0;
   gpu::HbdWave L{};
   const int steps = W + 2 * (H - 1);
   for (int pass = 0; pass < 2; ++pass)
@@ -96,7 +110,7 @@ static int run_picture(const avc::Picture& pic) {
         const int mb = yy * W + t - 2 * yy;
         for (int lane = 0; lane < 64; ++lane) {
           if (pass == 0) gpu::intra_mb<P, CF>(d, L, mb, lane);
-          else gpu::deblock_mb<P, CF>(d, mb, lane);
+          else gpu::deblock_mb<P, CF>(d, L, mb, lane);
         }
       }
     }

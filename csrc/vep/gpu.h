@@ -208,6 +208,8 @@ struct AvcDesc {
   // every picture / pool access against them and report a violation in *err (bits 8..15)
   // instead of touching memory outside
   u32 ncoef, nres;
+  i32 intra_mbs;       // intra MBs of the picture (avc_hbd_kernel skips its intra pass without)
+  i32 deblock;         // any MB filtered (avc_hbd_kernel skips its loop-filter pass without)
   VEP_DEV u64* xg;             // device scratch: exchange between the wavefront workgroups, kAvcXgWords
                        // tagged words per MB of every workgroup's last row (intra wavefront:
                        // words 0..7, zeroed by avc_inter_kernel; deblocking: all, zeroed by
@@ -215,7 +217,9 @@ struct AvcDesc {
 };
 // Phase accumulators of the wavefront kernels (summed over waves): intra wait / load / luma /
 // chroma / store+publish / MBs, deblock wait / load / filter / store+publish / MBs.
-constexpr int kAvcProfSlots = 12;  // + [11] intra residual pass
+constexpr int kAvcProfSlots = 16;  // + [11] intra residual pass, [12..15] avc_hbd_kernel: intra
+                                   // pass / loop-filter pass / barrier cycles (per workgroup),
+                                   // pictures
 // Residual samples of one intra MB: 256 luma (raster) + 2 x 64 chroma, as i16.
 constexpr int kAvcResSamples = 512;  // slot stride: 256 luma + 2 x 64 chroma (4:2:2: 2 x 128)
 // Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.

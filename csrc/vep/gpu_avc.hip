@@ -852,11 +852,14 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
         }
       }
     info.any = (info.bs[0] | info.bs[1] | info.bs[2] | info.bs[3]) ? 1 : 0;
+    // thresholds at 8-bit scale (QPs less the QpBdOffset bias; avc_hbd_kernel shifts them by
+    // bd - 8)
     const MbRec* ps[3] = {&lm, &tm, &q};
+    const int qb = d.qp_bias, qcb = d.qpc_bias;
     for (int k = 0; k < 3; ++k) {
-      const avc::EdgeParams ep[3] = {avc::edge_params(ps[k]->qp, q.qp, q.alpha_off, q.beta_off),
-                                     avc::edge_params(ps[k]->qpc, q.qpc, q.alpha_off, q.beta_off),
-                                     avc::edge_params(ps[k]->qpc2, q.qpc2, q.alpha_off, q.beta_off)};
+      const avc::EdgeParams ep[3] = {avc::edge_params(ps[k]->qp - qb, q.qp - qb, q.alpha_off, q.beta_off),
+                                     avc::edge_params(ps[k]->qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off),
+                                     avc::edge_params(ps[k]->qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off)};
       for (int c = 0; c < 3; ++c) {
         info.alpha[c * 3 + k] = u8(ep[c].alpha);
         info.beta[c * 3 + k] = u8(ep[c].beta);

@@ -42,19 +42,35 @@ constexpr int kHbdWaves = 8;
 constexpr int kTw = 25;  // luma tile row: x = -1..23
 constexpr int kCw = 9;   // chroma tile row: x = -1..7
 
-struct HbdWave {
+struct HbdIntra {
   int t[17 * kTw];      // luma: row 0 = p[-1..23, -1], row 1 + y = p[-1..23, y] (x > 15 unused)
   int c[2][17 * kCw];   // chroma per component: row 0 = p[-1..7, -1], row 1 + y = p[-1..7, y]
+  int f[25];            // Intra_8x8 filtered references of the current 8x8 block
+};
+constexpr int kDw = 20;   // loop-filter luma tile row: x = -4..15 (rows y = -4..15)
+constexpr int kDcw = 10;  // chroma tile row: x = -2..7 (rows y = -2..CH-1)
+struct HbdDbk {
+  int y[20 * kDw];
+  int c[2][18 * kDcw];
+  AvcDbkInfo info;  // the MB's bS / thresholds (lane-indexed reads: LDS, not scratch)
+};
+// A wave's LDS: the intra tile in the first pass, the loop-filter tile in the second (a
+// workgroup barrier separates them).
+union HbdWave {
+  HbdIntra in;
+  HbdDbk db;
 };
 
 // (The per-MB functions are host-callable too: csrc/tests/hbd_emu.cpp runs them lane by lane on
 // the CPU under AddressSanitizer.)
 #define VEP_HBD_FN __host__ __device__
+// Wave-level sync of the LDS tile (both passes keep every dependency inside the wave's tile; the
+// picture in global memory is read once per MB before and written once after).
 VEP_HBD_FN inline void wsync() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // (global RMW of the filter steps too)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 #endif
 }
 
@@ -82,11 +98,12 @@ VEP_HBD_FN inline bool oob(const AvcDesc& d, long i, long n, u32 bit) {
 constexpr u32 kOobLumaLoad = 0x100, kOobChromaLoad = 0x200, kOobRes = 0x400, kOobStore = 0x800,
               kOobDbkLuma = 0x1000, kOobDbkChroma = 0x2000;
 
-VEP_HBD_FN inline int& T(HbdWave& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
-VEP_HBD_FN inline int& Cc(HbdWave& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
+VEP_HBD_FN inline int& T(HbdIntra& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
+VEP_HBD_FN inline int& Cc(HbdIntra& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
 
 template <class P, int CF>
-VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
+VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
+  HbdIntra& L = LW.in;
   constexpr int CH = CF == 2 ? 16 : 8;  // chroma MB height
   const MbRec m = recd(d, mb);
   if (!avc::is_wave_intra(m.kind)) return;  // (skip / inter / I_PCM: written by the inter kernel)
@@ -120,64 +137,51 @@ VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
     Cc(L, c, -1, y) = A && !oob(d, i, nuv, kOobChromaLoad) ? int(UV[i]) : 128;
   }
   wsync();
-  // ---- luma
+  // ---- luma (the predictors read their neighbours straight from the LDS tile, which already
+  // holds 128 for an unavailable side: no per-lane neighbour arrays, which would live in
+  // scratch when indexed by lane)
   if (m.kind == avc::kI16x16) {
-    avc::Intra16Nb n;
-    n.has_left = A;
-    n.has_top = B;
-    n.has_tl = D;
-    n.top[0] = T(L, -1, -1);
-    for (int k = 0; k < 16; ++k) {
-      n.top[k + 1] = T(L, k, -1);
-      n.left[k] = T(L, -1, k);
-    }
-    const avc::PredConst k = avc::intra16x16_const(n, m.i16_mode, bd);
+    auto tf = [&](int x) { return T(L, x, -1); };
+    auto lf = [&](int y) { return T(L, -1, y); };
+    const avc::PredConst k = avc::intra16x16_const_g(tf, lf, B, A, m.i16_mode, bd);
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int x = lane & 15, y = (lane >> 4) + 4 * s;
-      T(L, x, y) = avc::clip1(avc::intra16x16_pred(n, k, m.i16_mode, x, y, bd) + (res ? int(res[y * 16 + x]) : 0), bd);
+      T(L, x, y) = avc::clip1(avc::intra16x16_pred_g(tf, lf, k, m.i16_mode, x, y, bd) + (res ? int(res[y * 16 + x]) : 0), bd);
     }
   } else if (m.kind == avc::kI4x4) {
     for (int idx = 0; idx < 16; ++idx) {
       const int r = avc::blk_to_raster(idx), bx = r & 3, by = r >> 2;
       if (lane < 16) {
         const int x0 = bx * 4, y0 = by * 4;
-        avc::Intra4Nb n;
-        n.has_top = by > 0 || B;
-        n.has_left = bx > 0 || A;
-        n.has_tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
+        const bool has_top = by > 0 || B, has_left = bx > 0 || A;
         const bool tr = by == 0 ? (bx < 3 ? B : C) : (bx < 3 && avc::raster_to_blk((by - 1) * 4 + bx + 1) < idx);
-        n.t[0] = n.has_tl ? T(L, x0 - 1, y0 - 1) : 128;
-        for (int k = 0; k < 4; ++k) {
-          n.t[1 + k] = n.has_top ? T(L, x0 + k, y0 - 1) : 128;
-          n.l[k] = n.has_left ? T(L, x0 - 1, y0 + k) : 128;
-        }
-        for (int k = 0; k < 4; ++k) n.t[5 + k] = tr ? T(L, x0 + 4 + k, y0 - 1) : n.t[4];
+        // (top-right unavailable: p[3, -1] repeated)
+        auto tf = [&](int x) { return T(L, x0 + (x >= 4 && !tr ? 3 : x), y0 - 1); };
+        auto lf = [&](int y) { return T(L, x0 - 1, y0 + y); };  // (y = -1: the corner)
         const int j = lane & 3, i = lane >> 2;
-        const int v = avc::intra4x4_pred(n, avc::i4_mode(m, r), j, i, bd) +
+        const int v = avc::intra4x4_pred_g(tf, lf, has_top, has_left, avc::i4_mode(m, r), j, i, bd) +
                       (res ? int(res[(y0 + i) * 16 + x0 + j]) : 0);
         T(L, x0 + j, y0 + i) = avc::clip1(v, bd);
       }
       wsync();
     }
-  } else {  // Intra_8x8
+  } else {  // Intra_8x8: the 25 filtered references into LDS (a lane each), then the prediction
     for (int q = 0; q < 4; ++q) {
       const int bx = q & 1, by = q >> 1, x0 = bx * 8, y0 = by * 8;
       const bool has_top = by > 0 || B, has_left = bx > 0 || A;
       const bool has_tl = (bx > 0 && by > 0) || (bx == 0 && by == 0 ? D : bx == 0 ? A : B);
       const bool has_tr = by == 0 ? (bx == 0 ? B : C) : (bx == 0);
-      int t[17], l[8];
-      t[0] = has_tl ? T(L, x0 - 1, y0 - 1) : 128;
-      for (int k = 0; k < 8; ++k) {
-        t[1 + k] = has_top ? T(L, x0 + k, y0 - 1) : 128;
-        l[k] = has_left ? T(L, x0 - 1, y0 + k) : 128;
+      if (lane < 25) {
+        auto tf = [&](int x) { return T(L, x0 + (x >= 8 && !has_tr ? 7 : x), y0 - 1); };
+        auto lf = [&](int y) { return T(L, x0 - 1, y0 + y); };
+        L.f[lane] = avc::intra8x8_filter_at(tf, lf, has_top, has_left, has_tl, lane);
       }
-      for (int k = 8; k < 16; ++k) t[1 + k] = has_tr ? T(L, x0 + k, y0 - 1) : t[8];
-      int f[25];
-      avc::intra8x8_filter([&](int x) { return t[1 + x]; }, [&](int y) { return l[y]; }, has_top, has_left,
-                           has_tl, f);
+      wsync();
       const int j = lane & 7, i = lane >> 3;
-      const int v = avc::intra8x8_pred(f, has_top, has_left, avc::i4_mode(m, q), j, i, bd) +
+      const int v = avc::intra8x8_pred_g([&](int x) { return L.f[1 + x]; },
+                                         [&](int y) { return y < 0 ? L.f[0] : L.f[17 + y]; }, has_top, has_left,
+                                         avc::i4_mode(m, q), j, i, bd) +
                     (res ? int(res[(y0 + i) * 16 + x0 + j]) : 0);
       T(L, x0 + j, y0 + i) = avc::clip1(v, bd);  // (no sample of the block is its own neighbour)
       wsync();
@@ -186,18 +190,13 @@ VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
   // ---- chroma (the whole 8x8 / 8x16 predicted from the neighbours: straight to the picture)
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
-    avc::IntraChromaNb n;
-    n.has_left = A;
-    n.has_top = B;
-    n.has_tl = D;
-    n.top[0] = Cc(L, c, -1, -1);
-    for (int k = 0; k < 8; ++k) n.top[k + 1] = Cc(L, c, k, -1);
-    for (int k = 0; k < CH; ++k) n.left[k] = Cc(L, c, -1, k);
-    const avc::PredConst k = m.chroma_mode == 3 ? avc::chroma_plane_const(n, CF) : avc::PredConst{0, 0, 0, 0};
+    auto tf = [&](int x) { return Cc(L, c, x, -1); };
+    auto lf = [&](int y) { return Cc(L, c, -1, y); };
+    const avc::PredConst k = m.chroma_mode == 3 ? avc::chroma_plane_const_g(tf, lf, CF) : avc::PredConst{0, 0, 0, 0};
 #pragma unroll
     for (int h = 0; h < CH / 8; ++h) {
       const int x = lane & 7, y = (lane >> 3) + 8 * h;
-      const int v = avc::chroma_pred(n, k, m.chroma_mode, x, y, bd, CF) +
+      const int v = avc::chroma_pred_g(tf, lf, B, A, k, m.chroma_mode, x, y, bd, CF) +
                     (res ? int(res[256 + c * 8 * CH + y * 8 + x]) : 0);
       const long i = long(my * CH + y) * pitch + (mx * 8 + x) * 2 + c;
       if (!oob(d, i, nuv, kOobStore)) UV[i] = P(avc::clip1(v, bd));
@@ -212,57 +211,98 @@ VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& L, int mb, int lane) {
   }
 }
 
-// avc.cpp deblock_t for one MB (bS per 4-line segment from avc_bs_kernel)
+// avc.cpp deblock_t for one MB (bS per 4-line segment from avc_bs_kernel), on the wave's LDS
+// tile: the MB and the samples its edges reach (luma rows / columns -4..15, chroma -2..) are
+// loaded once, the edges run in order in LDS, and the tile goes back once. (The MBs of a step
+// touch disjoint samples, and every earlier step is complete, so the tile is exact and writing
+// all of it back is safe.)
 template <class P, int CF>
-VEP_HBD_FN void deblock_mb(const AvcDesc& d, int mb, int lane) {
+VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
   constexpr int CH = CF == 2 ? 16 : 8;
+  constexpr int NL = 20 * kDw, NC = 2 * (CH + 2) * kDcw;  // tile samples
+  HbdDbk& L = LW.db;
   const MbRec q = recd(d, mb);
   if (q.dbk & 1) return;
+  // bS and the thresholds (avc_bs_kernel, 8-bit scale) into the wave's LDS once per MB: no table
+  // lookup on the filters' dependency chain, and the lane-indexed reads stay out of scratch
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
-  const AvcDbkInfo& info = infos[mb];
-  if (!info.any) return;
+  if (!infos[mb].any) return;
+  const AvcDbkInfo& info = L.info;
+  if (lane < 16) reinterpret_cast<u32*>(&L.info)[lane] = reinterpret_cast<const u32*>(&infos[mb])[lane];
   const int W = d.wmbs, pitch = W * 16, mx = mb % W, my = mb / W, bd = sizeof(P) == 1 ? 8 : d.bd;
-  const int qb = d.qp_bias, qcb = d.qpc_bias;
+  const int sh = bd - 8;
   const bool t8 = (q.flags & avc::kMbT8x8) != 0;
   VEP_DEV P* Y = reinterpret_cast<VEP_DEV P*>(d.y + d.slot_y * u64(d.target));
   VEP_DEV P* UV = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
-  const MbRec lm = mx > 0 ? recd(d, mb - 1) : q;
-  const MbRec tm = my > 0 ? recd(d, mb - W) : q;
+  // edge class k (0: left MB edge, 1: top MB edge, 2: internal) of component c
   const long ny = long(pitch) * d.hmbs * 16, nuv = long(pitch) * d.hmbs * CH;
-  // (a line at index i across an edge with stride st touches i - n * st .. i + (n - 1) * st)
-  auto line_ok = [&](long i, long st, int n, long lim, u32 bit) {
-    return !oob(d, i - n * st, lim, bit) && !oob(d, i + (n - 1) * st, lim, bit);
+  // tile sample t -> picture index (-1: outside the picture, left / above the MB's neighbours)
+  auto luma_at = [&](int t) -> long {
+    const int y = t / kDw - 4, x = t % kDw - 4;
+    if (my * 16 + y < 0 || mx * 16 + x < 0) return -1;
+    return long(my * 16 + y) * pitch + mx * 16 + x;
   };
+  // chroma tile sample t: component t / ((CH + 2) * kDcw), then its entry r = y * kDcw + x
+  auto chroma_at = [&](int t, int& c, int& r) -> long {
+    c = t / ((CH + 2) * kDcw);
+    r = t % ((CH + 2) * kDcw);
+    const int y = r / kDcw - 2, x = r % kDcw - 2;
+    if (my * CH + y < 0 || mx * 8 + x < 0) return -1;
+    return long(my * CH + y) * pitch + (mx * 8 + x) * 2 + c;
+  };
+  for (int t = lane; t < NL; t += 64) {
+    const long i = luma_at(t);
+    L.y[t] = i >= 0 && !oob(d, i, ny, kOobDbkLuma) ? int(Y[i]) : 0;
+  }
+  for (int t = lane; t < NC; t += 64) {
+    int c, r;
+    const long i = chroma_at(t, c, r);
+    L.c[c][r] = i >= 0 && !oob(d, i, nuv, kOobDbkChroma) ? int(UV[i]) : 0;
+  }
+  wsync();
   auto bs_of = [&](int i) { return int((info.bs[i >> 3] >> (4 * (i & 7))) & 15u); };
+  // Per edge, one filter body for the whole wave: lanes 0-15 the luma lines, 16.. the chroma
+  // lines (each lane its own pointer, stride, bS and thresholds), as one instruction stream.
   for (int dir = 0; dir < 2; ++dir)
     for (int e = 0; e < 4; ++e) {
-      const MbRec& p = e > 0 ? q : (dir == 0 ? lm : tm);
+      const int ek = e > 0 ? 2 : dir;
+      int bs = 0, comp = 0, step = 1;
+      int* s0 = L.y;
       if (lane < 16) {
-        const int k = lane, bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
-        if (bs) {
-          const avc::EdgeParams ep = avc::edge_params(p.qp - qb, q.qp - qb, q.alpha_off, q.beta_off, bd);
-          const long i = dir == 0 ? long(my * 16 + k) * pitch + mx * 16 + 4 * e : long(my * 16 + 4 * e) * pitch + mx * 16 + k;
-          const long st = dir == 0 ? 1 : long(pitch);
-          if (line_ok(i, st, 4, ny, kOobDbkLuma)) avc::filter_line(Y + i, st, bs, ep, false, bd);
-        }
-      } else if (lane >= 16 && !(e & 1) || (CF == 2 && dir == 1 && lane >= 16)) {
+        const int k = lane;
+        bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
+        s0 = dir == 0 ? &L.y[(k + 4) * kDw + 4 * e + 4] : &L.y[(4 * e + 4) * kDw + k + 4];
+        step = dir == 0 ? 1 : kDw;
+      } else if (!(e & 1) || (CF == 2 && dir == 1)) {
         // chroma edges at chroma samples 0 and 4 (luma edges 0, 2); 4:2:2: every horizontal edge
         // (chroma rows 4e). Lines: vertical edges CH rows, horizontal edges 8 columns, per component.
         const int nl = dir == 0 ? CH : 8, c = (lane - 16) / nl, k = (lane - 16) % nl;
         // bS of the luma line through the chroma line: vertical edges luma row k (4:2:0: 2k),
         // horizontal edges luma column 2k
-        const int bs = c < 2 ? bs_of(dir * 16 + e * 4 + (dir == 0 && CF == 2 ? k >> 2 : k >> 1)) : 0;
-        if (bs) {
-          const avc::EdgeParams ep = c == 0 ? avc::edge_params(p.qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off, bd)
-                                            : avc::edge_params(p.qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off, bd);
-          const long i = dir == 0 ? long(my * CH + k) * pitch + (mx * 8 + 2 * e) * 2 + c
-                                  : long(my * CH + (CF == 2 ? 4 : 2) * e) * pitch + (mx * 8 + k) * 2 + c;
-          const long st = dir == 0 ? 2 : long(pitch);
-          if (line_ok(i, st, 2, nuv, kOobDbkChroma)) avc::filter_line(UV + i, st, bs, ep, true, bd);
+        if (c < 2) {
+          bs = bs_of(dir * 16 + e * 4 + (dir == 0 && CF == 2 ? k >> 2 : k >> 1));
+          comp = 1 + c;
+          s0 = dir == 0 ? &L.c[c][(k + 2) * kDcw + 2 * e + 2] : &L.c[c][((CF == 2 ? 4 : 2) * e + 2) * kDcw + k + 2];
+          step = dir == 0 ? 1 : kDcw;
         }
+      }
+      if (bs) {  // (thresholds straight from the LDS copy: no EdgeParams array indexed by bS)
+        const int pi = comp * 3 + ek;
+        avc::filter_line_t(s0, step, bs, int(info.alpha[pi]) << sh, int(info.beta[pi]) << sh,
+                           bs < 4 ? int(info.tc0[pi][bs - 1]) << sh : 0, comp > 0, bd);
       }
       wsync();
     }
+  for (int t = lane; t < NL; t += 64) {
+    const long i = luma_at(t);
+    if (i >= 0 && !oob(d, i, ny, kOobStore)) Y[i] = P(L.y[t]);
+  }
+  for (int t = lane; t < NC; t += 64) {
+    int c, r;
+    const long i = chroma_at(t, c, r);
+    if (i >= 0 && !oob(d, i, nuv, kOobStore)) UV[i] = P(L.c[c][r]);
+  }
+  wsync();  // (the tile is reused by the wave's next MB)
 }
 
 #ifndef VEP_HBD_EMU  // (csrc/tests/hbd_emu.cpp: the per-MB functions only)
@@ -279,17 +319,29 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   __shared__ HbdWave lds[kHbdWaves];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int W = d.wmbs, H = d.hmbs, steps = W + 2 * (H - 1);
+  const bool prof = d.prof && threadIdx.x == 0;  // (VEP_AVC_PROF=1: workgroup phase clocks)
+  u64 tb = 0;
   for (int pass = 0; pass < 2; ++pass) {
-    if (!(pass == 0 ? intra : dbk)) continue;
+    if (!(pass == 0 ? intra && d.intra_mbs > 0 : dbk && d.deblock)) continue;  // (uniform)
+    const u64 tp = prof ? clock64() : 0;
     for (int t = 0; t < steps; ++t) {
       const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
       for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
         const int mb = y * W + t - 2 * y;
-        if (pass == 0) intra_mb<P, CF>(d, lds[wave], mb, lane);
-        else deblock_mb<P, CF>(d, mb, lane);
+        // (the descriptor by reference into global memory: a local copy passed by reference
+        // would live in scratch)
+        if (pass == 0) intra_mb<P, CF>(descs[pic], lds[wave], mb, lane);
+        else deblock_mb<P, CF>(descs[pic], lds[wave], mb, lane);
       }
+      const u64 ts = prof ? clock64() : 0;
       __syncthreads();
+      if (prof) tb += clock64() - ts;
     }
+    if (prof) atomicAdd(&d.prof[12 + pass], clock64() - tp);
+  }
+  if (prof) {
+    atomicAdd(&d.prof[14], tb);
+    atomicAdd(&d.prof[15], u64(1));
   }
 }
 

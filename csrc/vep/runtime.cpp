@@ -432,6 +432,7 @@ constexpr int kDefaultLanes = 3;
 constexpr int kDefaultStages = 3;
 // Batches queued per lane launcher thread behind the in-flight ones.
 constexpr int kDefaultLaneQueue = 2;
+constexpr int kDefaultLaneMergeJobs = 64;  // jobs per merged lane launch (lane launcher threads)
 constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
 constexpr int kAllLevels = 1 << 20;        // (a window holding every level of a round)
 // H.265 intra transform blocks: one persistent ticket-queue launch per round (every intra level;
@@ -467,6 +468,9 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
       nq = qe ? std::atoi(qe) : kDefaultLaneQueue;
     }
     queue_ = std::clamp(nq, 1, 16);
+    // lane launchers merge queued batches (merge_queued); VEP_LANE_MERGE = job cap, 0 = off
+    const char* me = std::getenv("VEP_LANE_MERGE");
+    merge_jobs_ = std::clamp(me ? std::atoi(me) : kDefaultLaneMergeJobs, 0, 4096);
     int kw = opt_.kf_window_us;
     if (kw < 0) {
       const char* ke = std::getenv("VEP_KF_WINDOW_US");
@@ -1555,6 +1559,8 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
       g.cf = a.p->cf;
       g.ncoef = u32(a.p->coefs.size());
       g.nres = u32(a.p->intra_res);
+      g.intra_mbs = a.p->intra_mbs;
+      g.deblock = a.p->deblock ? 1 : 0;
       VEP_CHECK(c->surface.bd == a.p->bd && c->surface.cf == a.p->cf,
                 "H.264: picture bit depth / chroma format differs from the camera's surfaces");
       mbs += a.p->nmbs();
@@ -2002,7 +2008,8 @@ void Worker::complete(Lane& ln, Stage& st) {
   st.slots.clear();
   {
     std::lock_guard<std::mutex> g(pub_mu_);
-    if (!ln.unpublished.empty() && ln.unpublished.front() == st.seq) ln.unpublished.pop_front();
+    while (!ln.unpublished.empty() && ln.unpublished.front() >= st.seq && ln.unpublished.front() <= st.seq_last)
+      ln.unpublished.pop_front();
   }
   pub_cv_.notify_all();
 }
@@ -2014,6 +2021,7 @@ void Worker::launch_on(Lane& ln, Batch&& b) {
   st.jobs.swap(b.jobs);
   st.slots.swap(b.slots);
   st.seq = b.seq;
+  st.seq_last = std::max(b.seq, b.seq_last);
   st.cons_hwc = b.cons_hwc;
   st.cons_chw = b.cons_chw;
   st.cons_rows = b.cons_rows;
@@ -2039,12 +2047,48 @@ void Worker::launch_on(Lane& ln, Batch&& b) {
     st.slots.clear();
     {
       std::lock_guard<std::mutex> g(pub_mu_);
-      if (!ln.unpublished.empty() && ln.unpublished.front() == st.seq) ln.unpublished.pop_front();
+      while (!ln.unpublished.empty() && ln.unpublished.front() >= st.seq && ln.unpublished.front() <= st.seq_last)
+        ln.unpublished.pop_front();
     }
     pub_cv_.notify_all();
     throw;
   }
   st.active = true;
+}
+
+// Batches that queued behind this lane's in-flight ones (ln.mu held) join `b`: one launch per
+// kernel for all of them. The wavefront kernels (intra, deblock) take about the same time for
+// one picture as for many (a picture's latency is its MB-row chain, and a launch of one picture
+// fills a few CUs of 256), and the batches would run back to back on the lane's stream anyway,
+// so merging turns queueing into parallel work without holding anything back: nothing waits
+// for a merge, only what is already waiting is merged. A camera appears at most once per launch
+// (its pictures inside one job are rounds; two jobs of one camera in one launch would put
+// dependent pictures in the same round), so the merge stops at a batch that repeats a camera,
+// at a different consumer batch, or at merge_jobs_ jobs.
+void Worker::merge_queued(Lane& ln, Batch& b) {
+  if (merge_jobs_ <= 0) return;
+  while (!ln.q.empty()) {
+    Batch& n = ln.q.front();
+    if (n.cons_hwc != b.cons_hwc || n.cons_chw != b.cons_chw || n.cons_rows != b.cons_rows) break;
+    if (int(b.jobs.size() + n.jobs.size()) > merge_jobs_) break;
+    bool repeat = false;
+    for (const DecodeJob& j : n.jobs) {
+      for (const DecodeJob& k : b.jobs)
+        if (k.cam == j.cam) {
+          repeat = true;
+          break;
+        }
+      if (repeat) break;
+    }
+    if (repeat) break;
+    for (size_t i = 0; i < n.jobs.size(); ++i) {
+      b.jobs.push_back(std::move(n.jobs[i]));
+      b.slots.push_back(n.slots[i]);
+    }
+    b.seq_last = std::max(n.seq, n.seq_last);
+    ln.q.pop_front();
+    merged_.fetch_add(1, std::memory_order_relaxed);
+  }
 }
 
 // Launcher thread of one lane: launches the batches handed over by launch_async, each after
@@ -2058,10 +2102,11 @@ void Worker::lane_loop(Lane& ln) {
   };
   std::unique_lock<std::mutex> lk(ln.mu);
   for (;;) {
-    ln.cv.wait(lk, [&] { return ln.stop || ln.drain || !ln.q.empty(); });
-    if (!ln.q.empty()) {
+    ln.cv.wait(lk, [&] { return ln.stop || ln.drain || (!ln.q.empty() && !hold_.load()); });
+    if (!ln.q.empty() && (!hold_.load() || ln.drain || ln.stop)) {
       Batch b = std::move(ln.q.front());
       ln.q.pop_front();
+      merge_queued(ln, b);
       ln.busy = true;
       lk.unlock();
       ln.cv.notify_all();  // room for the next batch
@@ -2090,6 +2135,14 @@ void Worker::lane_loop(Lane& ln) {
     }
     if (ln.stop) return;
   }
+}
+
+void Worker::hold_lanes(bool hold) {
+  hold_.store(hold);
+  for (auto& lp : lanes_) {
+    std::lock_guard<std::mutex> g(lp->mu);  // (a launcher between its predicate check and its wait)
+  }
+  for (auto& lp : lanes_) lp->cv.notify_all();
 }
 
 void Worker::drain_lanes() {
@@ -2171,7 +2224,7 @@ void Worker::launch_async(std::vector<DecodeJob>& jobs) {
       std::lock_guard<std::mutex> pg(pub_mu_);
       ln.unpublished.push_back(seq);
     }
-    Batch b{std::move(lj[g]), std::move(ls[g]), seq, cons_hwc_, cons_chw_, cons_rows_};
+    Batch b{std::move(lj[g]), std::move(ls[g]), seq, seq, cons_hwc_, cons_chw_, cons_rows_};
     if (!threaded_) {
       launch_on(ln, std::move(b));
       continue;

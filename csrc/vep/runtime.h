@@ -408,6 +408,10 @@ class Worker {
   // outputs not published because their reconstruction was shed with a merged backlog (load
   // shedding at a keyframe, merge_job) or predicts from such a picture (RASL of a shed CRA)
   u64 shed() const { return shed_.load(); }
+  u64 merged() const { return merged_.load(); }  // batches merged into an earlier one (lane launchers)
+  // Lane launcher threads leave queued batches queued while held (tests: a deterministic queue
+  // for merge_queued; a drain still launches them).
+  void hold_lanes(bool hold);
   u64 pictures() const { return pictures_.load(); }  // pictures reconstructed
   // GPU time of the batches (first event to last, per lane; the busiest lane's total)
   double gpu_ms_total() const;
@@ -422,7 +426,8 @@ class Worker {
     hipEvent_t copied = nullptr, e0 = nullptr, e1 = nullptr;
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;
-    u64 seq = 0;               // launch sequence of the batch
+    u64 seq = 0;               // launch sequence of the batch (merged batches: the first ...
+    u64 seq_last = 0;          // ... to the last, consecutive in the lane's `unpublished`)
     u8* cons_hwc = nullptr;    // consumer batch at launch time (set_consumer_buffers may move on)
     void* cons_chw = nullptr;
     int cons_rows = 0;
@@ -436,7 +441,7 @@ class Worker {
   struct Batch {
     std::vector<DecodeJob> jobs;
     std::vector<int> slots;
-    u64 seq = 0;
+    u64 seq = 0, seq_last = 0;
     u8* cons_hwc = nullptr;
     void* cons_chw = nullptr;
     int cons_rows = 0;
@@ -460,6 +465,7 @@ class Worker {
   void prepare(std::vector<DecodeJob>& jobs, std::vector<int>& slots);
   void launch_gpu(Lane& ln, Stage& st);
   void lane_loop(Lane& ln);
+  void merge_queued(Lane& ln, Batch& b);
   void launch_on(Lane& ln, Batch&& b);  // reuse the lane's oldest stage for batch b
   void drain_lanes();
   void run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err);
@@ -477,6 +483,8 @@ class Worker {
   int stages_ = 2;
   bool threaded_ = false;        // one launcher thread per lane
   int queue_ = 0;                // lane queue depth (threaded)
+  std::atomic<bool> hold_{false};
+  int merge_jobs_ = 0;           // lane launcher: merge queued batches up to this many jobs (0: off)
   std::atomic<u64> launch_seq_{0};
   std::mutex pub_mu_;
   std::condition_variable pub_cv_;
@@ -538,7 +546,7 @@ class Worker {
   std::weak_ptr<IngestServices> svc_;  // ingest_services()
   std::mutex launch_mu_;
   std::shared_ptr<std::function<void(int, i64)>> publish_hook_;  // (atomic_load / atomic_store)
-  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0}, shed_{0};
+  std::atomic<u64> batches_{0}, frames_{0}, dropped_{0}, pictures_{0}, shed_{0}, merged_{0};
   std::atomic<u64> pinned_bytes_inplace_{0}, pinned_bytes_staged_{0}, records_gathered_{0};
   std::mutex timers_mu_;
   bool direct_reads_ = false;

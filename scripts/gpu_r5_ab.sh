@@ -20,7 +20,8 @@ run() {  # name, env assignments..., --, bench args...
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 keys = ("value", "ms_per_step", "rank0_gpu_kernel_ms_per_step", "frames_dropped", "dbk_cycles_per_mb",
-        "intra_cycles_per_mb")
+        "intra_cycles_per_mb", "rank0_pictures_per_launch", "rank0_launches_merged", "p50_latency_ms",
+        "p99_latency_ms")
 print(sys.argv[2], {k: d.get(k) for k in keys if k in d})
 PY
 }
@@ -30,6 +31,14 @@ if [ "${PART:-dbk}" = dbk ]; then
       run dbk_regs${g}_$i VEP_DBK_REGS=$g -- --gpus 1 --steps 20 --warmup 5
       run dbk_regs${g}_prof_$i VEP_DBK_REGS=$g VEP_AVC_PROF=1 -- --gpus 1 --steps 10 --warmup 3 --clients 0 \
         --latency-samples 0
+    done
+  done
+fi
+if [ "${PART:-dbk}" = lanes ]; then  # lane launchers merging queued batches vs not vs round 4's launcher
+  for i in 1 2; do
+    for v in single:VEP_LANE_THREADS=0 merge:VEP_LANE_THREADS=1 nomerge:VEP_LANE_MERGE=0:VEP_LANE_THREADS=1; do
+      IFS=: read -r nm e1 e2 <<< "$v"
+      run lanes_${nm}_$i $e1 ${e2:-VEP_NOP=1} -- --gpus 1 --steps 20 --warmup 5 ${BENCH_ARGS:-}
     done
   done
 fi

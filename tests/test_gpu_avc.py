@@ -101,6 +101,34 @@ def test_lanes_pipeline_bit_exact(native, lane_threads):
         assert np.array_equal(got, want[k][-1]), f"camera {k}"
 
 
+def test_lane_merge_bit_exact(native):
+    """Lane launcher threads merge the batches queued behind their in-flight ones into one launch
+    (Worker::merge_queued): many one-camera batches submitted without waiting queue up and merge,
+    a merge never holds two jobs of one camera, and every frame stays bit-exact (a merge that put
+    dependent pictures in one round would corrupt every later picture of that camera)."""
+    ncam = 6
+    encs = [synth(native, 320, 240, gop=8, seed=70 + k, compressed=True, coverage=k % 2 == 1)
+            for k in range(ncam)]
+    refs = [native.CpuDecoder() for _ in encs]
+    wk = native.Worker(device=0, lanes=2, stages=2, queue=16, lane_threads=True)
+    cams = [wk.add_camera(f"m{k}", 2) for k in range(ncam)]
+    want = [None] * ncam
+    for rnd in range(4):
+        wk.hold_lanes(True)  # the launchers leave the batches queued: 12 per lane (queue 16)
+        for step in range(4):
+            for k in range(ncam):  # one batch per camera: consecutive batches repeat every camera
+                au = encs[k].next()
+                want[k] = refs[k].decode(au)
+                wk.decode_many([(cams[k], [au])], sync=False)
+        wk.hold_lanes(False)
+        wk.complete_all()
+    assert wk.merged > 0
+    assert wk.frames == 16 * ncam
+    for k in range(ncam):
+        _, got = wk.read_latest(cams[k], 0)
+        assert np.array_equal(got, want[k]), f"camera {k}"
+
+
 def test_corrupt_slices_on_gpu_recover_at_idr(native):
     """Bit errors in slice data through the GPU worker: a rejected picture is dropped (the
     camera waits for the next keyframe); whatever the kernels are given has passed
