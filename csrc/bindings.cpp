@@ -1311,7 +1311,8 @@ PYBIND11_MODULE(_vep, m) {
         static const char* kNames[gpu::kAvcProfSlots] = {
             "intra_wait", "intra_load", "intra_luma", "intra_chroma", "intra_store", "intra_mbs",
             "dbk_wait", "dbk_load", "dbk_filter", "dbk_store", "dbk_mbs", "intra_residual",
-            "hbd_intra", "hbd_dbk", "hbd_barrier", "hbd_pictures"};
+            "hbd_intra", "hbd_dbk", "hbd_barrier", "hbd_pictures", "hbd_dbk_load", "hbd_dbk_edges",
+            "hbd_dbk_store", "hbd_dbk_mbs"};
         const std::vector<u64> v = w.avc_profile();
         py::dict d;
         for (int i = 0; i < gpu::kAvcProfSlots; ++i) d[kNames[i]] = v[size_t(i)];

@@ -217,9 +217,10 @@ struct AvcDesc {
 };
 // Phase accumulators of the wavefront kernels (summed over waves): intra wait / load / luma /
 // chroma / store+publish / MBs, deblock wait / load / filter / store+publish / MBs.
-constexpr int kAvcProfSlots = 16;  // + [11] intra residual pass, [12..15] avc_hbd_kernel: intra
+constexpr int kAvcProfSlots = 20;  // + [11] intra residual pass, [12..15] avc_hbd_kernel: intra
                                    // pass / loop-filter pass / barrier cycles (per workgroup),
-                                   // pictures
+                                   // pictures; [16..19] its loop filter per MB (wave 0): tile
+                                   // load / edges / store cycles, MBs
 // Residual samples of one intra MB: 256 luma (raster) + 2 x 64 chroma, as i16.
 constexpr int kAvcResSamples = 512;  // slot stride: 256 luma + 2 x 64 chroma (4:2:2: 2 x 128)
 // Per-MB loop-filter inputs, computed in parallel ahead of the deblocking wavefront.

@@ -63,10 +63,10 @@ union HbdWave {
 
 // (The per-MB functions are host-callable too: csrc/tests/hbd_emu.cpp runs them lane by lane on
 // the CPU under AddressSanitizer.)
-#define VEP_HBD_FN __host__ __device__
+#define VEP_HBD_FN __host__ __device__ inline __attribute__((always_inline))
 // Wave-level sync of the LDS tile (both passes keep every dependency inside the wave's tile; the
 // picture in global memory is read once per MB before and written once after).
-VEP_HBD_FN inline void wsync() {
+VEP_HBD_FN void wsync() {
 #if defined(__HIP_DEVICE_COMPILE__)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_wave_barrier();
@@ -74,10 +74,26 @@ VEP_HBD_FN inline void wsync() {
 #endif
 }
 
-VEP_HBD_FN inline const MbRec& recd(const AvcDesc& d, int mb) { return static_cast<const MbRec*>(d.mbs)[mb]; }
+// clock64() / "thread 0 of the workgroup" for the phase clocks (0 / false in the host emulation)
+VEP_HBD_FN u64 hbd_clock() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return clock64();
+#else
+  return 0;
+#endif
+}
+VEP_HBD_FN bool hbd_thread0() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return threadIdx.x == 0;
+#else
+  return false;
+#endif
+}
+
+VEP_HBD_FN const MbRec& recd(const AvcDesc& d, int mb) { return static_cast<const MbRec*>(d.mbs)[mb]; }
 
 // avc.cpp intra_avail
-VEP_HBD_FN inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
+VEP_HBD_FN bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
   if (nx < 0 || ny < 0 || nx >= d.wmbs) return false;
   const MbRec& n = recd(d, ny * d.wmbs + nx);
   if (n.slice != m.slice) return false;
@@ -86,7 +102,7 @@ VEP_HBD_FN inline bool avail(const AvcDesc& d, const MbRec& m, int nx, int ny) {
 
 // Bound check of a picture index (luma: wpx * hpx samples; chroma plane: wpx * chroma rows): a
 // violation is reported in *err (bits 8..15, AvcDesc) and the access skipped, never performed.
-VEP_HBD_FN inline bool oob(const AvcDesc& d, long i, long n, u32 bit) {
+VEP_HBD_FN bool oob(const AvcDesc& d, long i, long n, u32 bit) {
   if (i >= 0 && i < n) return false;
 #if defined(__HIP_DEVICE_COMPILE__)
   atomicOr(d.err, bit);
@@ -98,8 +114,8 @@ VEP_HBD_FN inline bool oob(const AvcDesc& d, long i, long n, u32 bit) {
 constexpr u32 kOobLumaLoad = 0x100, kOobChromaLoad = 0x200, kOobRes = 0x400, kOobStore = 0x800,
               kOobDbkLuma = 0x1000, kOobDbkChroma = 0x2000;
 
-VEP_HBD_FN inline int& T(HbdIntra& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
-VEP_HBD_FN inline int& Cc(HbdIntra& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
+VEP_HBD_FN int& T(HbdIntra& L, int x, int y) { return L.t[(y + 1) * kTw + x + 1]; }
+VEP_HBD_FN int& Cc(HbdIntra& L, int c, int x, int y) { return L.c[c][(y + 1) * kCw + x + 1]; }
 
 template <class P, int CF>
 VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
@@ -250,98 +266,176 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
     if (my * CH + y < 0 || mx * 8 + x < 0) return -1;
     return long(my * CH + y) * pitch + (mx * 8 + x) * 2 + c;
   };
-  for (int t = lane; t < NL; t += 64) {
-    const long i = luma_at(t);
-    L.y[t] = i >= 0 && !oob(d, i, ny, kOobDbkLuma) ? int(Y[i]) : 0;
+  const bool pf = d.prof && hbd_thread0();  // (VEP_AVC_PROF: wave 0's MB phases)
+  const u64 c0 = pf ? hbd_clock() : 0;
+  // every load of the tile in flight at once: unconditional loads at clamped indices (a
+  // conditional load would wait at its join), then the LDS stores
+  constexpr int KL = (NL + 63) / 64, KC = (NC + 63) / 64;
+  int lv[KL], cv[KC];
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    const int t = lane + 64 * j;
+    const long i = t < NL ? luma_at(t) : -1;
+    const bool ok = i >= 0 && i < ny;
+    if (i >= 0 && !ok) oob(d, i, ny, kOobDbkLuma);
+    lv[j] = int(Y[ok ? i : 0]);
   }
-  for (int t = lane; t < NC; t += 64) {
-    int c, r;
-    const long i = chroma_at(t, c, r);
-    L.c[c][r] = i >= 0 && !oob(d, i, nuv, kOobDbkChroma) ? int(UV[i]) : 0;
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int t = lane + 64 * j;
+    int c = 0, r = 0;
+    const long i = t < NC ? chroma_at(t, c, r) : -1;
+    const bool ok = i >= 0 && i < nuv;
+    if (i >= 0 && !ok) oob(d, i, nuv, kOobDbkChroma);
+    cv[j] = int(UV[ok ? i : 0]);
+  }
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    const int t = lane + 64 * j;
+    if (t < NL) L.y[t] = lv[j];
+  }
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int t = lane + 64 * j;
+    if (t < NC) L.c[t / ((CH + 2) * kDcw)][t % ((CH + 2) * kDcw)] = cv[j];
   }
   wsync();
+  const u64 c1 = pf ? hbd_clock() : 0;
   auto bs_of = [&](int i) { return int((info.bs[i >> 3] >> (4 * (i & 7))) & 15u); };
-  // Per edge, one filter body for the whole wave: lanes 0-15 the luma lines, 16.. the chroma
-  // lines (each lane its own pointer, stride, bS and thresholds), as one instruction stream.
-  for (int dir = 0; dir < 2; ++dir)
-    for (int e = 0; e < 4; ++e) {
-      const int ek = e > 0 ? 2 : dir;
-      int bs = 0, comp = 0, step = 1;
-      int* s0 = L.y;
-      if (lane < 16) {
-        const int k = lane;
-        bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
-        s0 = dir == 0 ? &L.y[(k + 4) * kDw + 4 * e + 4] : &L.y[(4 * e + 4) * kDw + k + 4];
-        step = dir == 0 ? 1 : kDw;
-      } else if (!(e & 1) || (CF == 2 && dir == 1)) {
-        // chroma edges at chroma samples 0 and 4 (luma edges 0, 2); 4:2:2: every horizontal edge
-        // (chroma rows 4e). Lines: vertical edges CH rows, horizontal edges 8 columns, per component.
-        const int nl = dir == 0 ? CH : 8, c = (lane - 16) / nl, k = (lane - 16) % nl;
-        // bS of the luma line through the chroma line: vertical edges luma row k (4:2:0: 2k),
-        // horizontal edges luma column 2k
-        if (c < 2) {
-          bs = bs_of(dir * 16 + e * 4 + (dir == 0 && CF == 2 ? k >> 2 : k >> 1));
-          comp = 1 + c;
-          s0 = dir == 0 ? &L.c[c][(k + 2) * kDcw + 2 * e + 2] : &L.c[c][((CF == 2 ? 4 : 2) * e + 2) * kDcw + k + 2];
-          step = dir == 0 ? 1 : kDcw;
-        }
+  // Per direction, each lane holds one line in registers — lanes 0-15 a luma row (vertical
+  // edges) / column (horizontal edges) as 20 samples (positions -4..15), lanes 16.. a chroma row /
+  // column of one component at positions -2.. from register 2 — so its register edge r (between
+  // registers 4r + 3 and 4r + 4) is luma MB edge r, and chroma edge r is chroma sample 4r (MB edges
+  // 0 and 2; 4:2:2 horizontal: all four). The line's four edges then run in order in registers,
+  // with one LDS round trip per direction instead of one per edge.
+  const bool luma = lane < 16;
+#pragma unroll
+  for (int dir = 0; dir < 2; ++dir) {
+    const int nlc = dir == 0 ? CH : 8;  // chroma lines per component
+    const int cl = lane - 16, c = luma ? 0 : cl / nlc, k = luma ? lane : cl % nlc;
+    const bool act = luma || c < 2;
+    const bool all4 = luma || (CF == 2 && dir == 1);
+    const int comp = luma ? 0 : 1 + c;
+    int bsr[4], al[4], be[4], tc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int e = all4 ? r : 2 * r;
+      int bs = 0;
+      if (act && e < 4) {
+        if (luma) bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
+        // chroma: bS of the luma line through it (vertical: luma row k, 4:2:0 2k; horizontal: column 2k)
+        else bs = bs_of(dir * 16 + e * 4 + (dir == 0 && CF == 2 ? k >> 2 : k >> 1));
       }
-      if (bs) {  // (thresholds straight from the LDS copy: no EdgeParams array indexed by bS)
-        const int pi = comp * 3 + ek;
-        avc::filter_line_t(s0, step, bs, int(info.alpha[pi]) << sh, int(info.beta[pi]) << sh,
-                           bs < 4 ? int(info.tc0[pi][bs - 1]) << sh : 0, comp > 0, bd);
-      }
-      wsync();
+      const int pi = (act ? comp : 0) * 3 + (e > 0 ? 2 : dir);
+      bsr[r] = bs;
+      al[r] = int(info.alpha[pi]) << sh;
+      be[r] = int(info.beta[pi]) << sh;
+      tc[r] = bs > 0 && bs < 4 ? int(info.tc0[pi][bs - 1]) << sh : 0;
     }
-  for (int t = lane; t < NL; t += 64) {
-    const long i = luma_at(t);
-    if (i >= 0 && !oob(d, i, ny, kOobStore)) Y[i] = P(L.y[t]);
+    int* base;
+    int stride, off, n;
+    if (luma) {
+      base = dir == 0 ? &L.y[(k + 4) * kDw] : &L.y[k + 4];
+      stride = dir == 0 ? 1 : kDw;
+      off = 0;
+      n = 20;
+    } else {
+      base = dir == 0 ? &L.c[act ? c : 0][(k + 2) * kDcw] : &L.c[act ? c : 0][k + 2];
+      stride = dir == 0 ? 1 : kDcw;
+      off = 2;
+      n = act ? (dir == 0 ? kDcw : CH + 2) : 0;
+    }
+    int v[20];
+#pragma unroll
+    for (int i = 0; i < 20; ++i) v[i] = i >= off && i - off < n ? base[(i - off) * stride] : 0;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (!bsr[r]) continue;
+      int pp[4] = {v[4 * r + 3], v[4 * r + 2], v[4 * r + 1], v[4 * r]};
+      int qq[4] = {v[4 * r + 4], v[4 * r + 5], v[4 * r + 6], v[4 * r + 7]};
+      avc::filter_samples(pp, qq, bsr[r], al[r], be[r], tc[r], !luma, bd);  // (in place; chroma: p0 / q0)
+      v[4 * r + 3] = pp[0];
+      v[4 * r + 2] = pp[1];
+      v[4 * r + 1] = pp[2];
+      v[4 * r + 4] = qq[0];
+      v[4 * r + 5] = qq[1];
+      v[4 * r + 6] = qq[2];
+    }
+#pragma unroll
+    for (int i = 0; i < 20; ++i)
+      if (i >= off && i - off < n) base[(i - off) * stride] = v[i];
+    wsync();
   }
-  for (int t = lane; t < NC; t += 64) {
-    int c, r;
-    const long i = chroma_at(t, c, r);
-    if (i >= 0 && !oob(d, i, nuv, kOobStore)) UV[i] = P(L.c[c][r]);
+  const u64 c2 = pf ? hbd_clock() : 0;
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    const int t = lane + 64 * j;
+    lv[j] = t < NL ? L.y[t] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int t = lane + 64 * j;
+    cv[j] = t < NC ? L.c[t / ((CH + 2) * kDcw)][t % ((CH + 2) * kDcw)] : 0;
+  }
+#pragma unroll
+  for (int j = 0; j < KL; ++j) {
+    const int t = lane + 64 * j;
+    const long i = t < NL ? luma_at(t) : -1;
+    if (i >= 0 && !oob(d, i, ny, kOobStore)) Y[i] = P(lv[j]);
+  }
+#pragma unroll
+  for (int j = 0; j < KC; ++j) {
+    const int t = lane + 64 * j;
+    int c = 0, r = 0;
+    const long i = t < NC ? chroma_at(t, c, r) : -1;
+    if (i >= 0 && !oob(d, i, nuv, kOobStore)) UV[i] = P(cv[j]);
   }
   wsync();  // (the tile is reused by the wave's next MB)
+#if defined(__HIP_DEVICE_COMPILE__)
+  if (pf) {
+    atomicAdd(&d.prof[16], c1 - c0);
+    atomicAdd(&d.prof[17], c2 - c1);
+    atomicAdd(&d.prof[18], clock64() - c2);
+    atomicAdd(&d.prof[19], u64(1));
+  }
+#endif
 }
 
 #ifndef VEP_HBD_EMU  // (csrc/tests/hbd_emu.cpp: the per-MB functions only)
-// One instantiation per (sample type, chroma format): each workgroup takes one picture of the
-// round and returns at once unless the picture is of its variant.
-template <class P, int CF>
-__global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* __restrict__ descs, int n,
-                                                                  int intra, int dbk) {
+// One instantiation per (sample type, chroma format, pass): each workgroup takes one picture of
+// the round and returns at once unless the picture is of its variant. The two passes are
+// separate kernels (intra, then the loop filter) so each gets the whole register file.
+template <class P, int CF, int PASS>
+__global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* __restrict__ descs, int n) {
   const int pic = int(blockIdx.x);
   if (pic >= n) return;
   const AvcDesc d = descs[pic];
   // (uniform over the workgroup, before any barrier)
   if ((d.bd > 8) != (sizeof(P) == 2) || (d.cf == 2) != (CF == 2)) return;
+  if (!(PASS == 0 ? d.intra_mbs > 0 : d.deblock != 0)) return;
   __shared__ HbdWave lds[kHbdWaves];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int W = d.wmbs, H = d.hmbs, steps = W + 2 * (H - 1);
   const bool prof = d.prof && threadIdx.x == 0;  // (VEP_AVC_PROF=1: workgroup phase clocks)
   u64 tb = 0;
-  for (int pass = 0; pass < 2; ++pass) {
-    if (!(pass == 0 ? intra && d.intra_mbs > 0 : dbk && d.deblock)) continue;  // (uniform)
-    const u64 tp = prof ? clock64() : 0;
-    for (int t = 0; t < steps; ++t) {
-      const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
-      for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
-        const int mb = y * W + t - 2 * y;
-        // (the descriptor by reference into global memory: a local copy passed by reference
-        // would live in scratch)
-        if (pass == 0) intra_mb<P, CF>(descs[pic], lds[wave], mb, lane);
-        else deblock_mb<P, CF>(descs[pic], lds[wave], mb, lane);
-      }
-      const u64 ts = prof ? clock64() : 0;
-      __syncthreads();
-      if (prof) tb += clock64() - ts;
+  const u64 tp = prof ? clock64() : 0;
+  for (int t = 0; t < steps; ++t) {
+    const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
+    for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
+      const int mb = y * W + t - 2 * y;
+      // (the descriptor by reference into global memory: a local copy passed by reference
+      // would live in scratch)
+      if (PASS == 0) intra_mb<P, CF>(descs[pic], lds[wave], mb, lane);
+      else deblock_mb<P, CF>(descs[pic], lds[wave], mb, lane);
     }
-    if (prof) atomicAdd(&d.prof[12 + pass], clock64() - tp);
+    const u64 ts = prof ? clock64() : 0;
+    __syncthreads();
+    if (prof) tb += clock64() - ts;
   }
   if (prof) {
+    atomicAdd(&d.prof[12 + PASS], clock64() - tp);
     atomicAdd(&d.prof[14], tb);
-    atomicAdd(&d.prof[15], u64(1));
+    if (PASS == 1) atomicAdd(&d.prof[15], u64(1));
   }
 }
 
@@ -353,10 +447,16 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
 void launch_avc_hbd(const AvcDesc* d_descs, int n, bool intra, bool dbk, int variants, hipStream_t s) {
   if (n <= 0 || !(intra || dbk)) return;
   const dim3 grid{unsigned(n)}, block{64 * kHbdWaves};
-  const int in = intra ? 1 : 0, db = dbk ? 1 : 0;
-  if (variants & 1) hipLaunchKernelGGL((avc_hbd_kernel<u16, 1>), grid, block, 0, s, d_descs, n, in, db);
-  if (variants & 2) hipLaunchKernelGGL((avc_hbd_kernel<u8, 2>), grid, block, 0, s, d_descs, n, in, db);
-  if (variants & 4) hipLaunchKernelGGL((avc_hbd_kernel<u16, 2>), grid, block, 0, s, d_descs, n, in, db);
+  if (intra) {
+    if (variants & 1) hipLaunchKernelGGL((avc_hbd_kernel<u16, 1, 0>), grid, block, 0, s, d_descs, n);
+    if (variants & 2) hipLaunchKernelGGL((avc_hbd_kernel<u8, 2, 0>), grid, block, 0, s, d_descs, n);
+    if (variants & 4) hipLaunchKernelGGL((avc_hbd_kernel<u16, 2, 0>), grid, block, 0, s, d_descs, n);
+  }
+  if (dbk) {
+    if (variants & 1) hipLaunchKernelGGL((avc_hbd_kernel<u16, 1, 1>), grid, block, 0, s, d_descs, n);
+    if (variants & 2) hipLaunchKernelGGL((avc_hbd_kernel<u8, 2, 1>), grid, block, 0, s, d_descs, n);
+    if (variants & 4) hipLaunchKernelGGL((avc_hbd_kernel<u16, 2, 1>), grid, block, 0, s, d_descs, n);
+  }
   VEP_HIP(hipGetLastError());
 }
 #endif  // VEP_HBD_EMU

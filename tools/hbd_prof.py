@@ -24,8 +24,10 @@ def main():
     dt = time.perf_counter() - t0
     pr = wk.avc_profile()
     pics = max(1, pr["hbd_pictures"])
+    mbs = max(1, pr["hbd_dbk_mbs"])
     print({"pictures": pr["hbd_pictures"], "ms_per_picture_wall": round(dt * 1e3 / n, 3),
-           **{k: round(pr[k] / pics) for k in ("hbd_intra", "hbd_dbk", "hbd_barrier")}})
+           **{k: round(pr[k] / pics) for k in ("hbd_intra", "hbd_dbk", "hbd_barrier")},
+           "dbk_cycles_per_mb": {k[8:]: round(pr[k] / mbs) for k in ("hbd_dbk_load", "hbd_dbk_edges", "hbd_dbk_store")}})
 
 
 if __name__ == "__main__":
