@@ -69,7 +69,7 @@ static void bs_info(const avc::Picture& pic, int cf, std::vector<AvcDbkInfo>& ou
 }
 
 template <class P, int CF>
-static int run_picture(const avc::Picture& pic) {
+static int run_picture(const avc::Picture& pic, bool half = false) {
   const int W = pic.wmbs, H = pic.hmbs, ch = CF == 2 ? 16 : 8;
   const size_t ny = size_t(W) * 16 * H * 16, nuv = size_t(W) * 16 * H * ch;
   const int slots = pic.dpb_slots;
@@ -110,7 +110,8 @@ static int run_picture(const avc::Picture& pic) {
         const int mb = yy * W + t - 2 * yy;
         for (int lane = 0; lane < 64; ++lane) {
           if (pass == 0) gpu::intra_mb<P, CF>(d, L, mb, lane);
-          else gpu::deblock_mb<P, CF>(d, L, mb, lane);
+          else if (CF == 1 && half) gpu::deblock_mb<P, 1, 32>(d, L.db, mb, lane & 31, true);
+          else gpu::deblock_mb<P, CF>(d, L.db, mb, lane);
         }
       }
     }
@@ -138,7 +139,7 @@ int main() {
         auto au = enc.next();
         auto pic = dec.parse(*au, 0, nullptr);
         int e;
-        if (variant == 0) e = run_picture<u16, 1>(*pic);
+        if (variant == 0) e = run_picture<u16, 1>(*pic) | run_picture<u16, 1>(*pic, true);
         else if (variant == 1) e = run_picture<u8, 2>(*pic);
         else e = run_picture<u16, 2>(*pic);
         ++pics;
@@ -175,7 +176,7 @@ int main() {
         auto pic = dec.parse(*au, 0, nullptr);
         if (!pic) continue;
         int e;
-        if (k.cf != 2) e = run_picture<u16, 1>(*pic);
+        if (k.cf != 2) e = run_picture<u16, 1>(*pic) | run_picture<u16, 1>(*pic, true);
         else if (k.bd == 8) e = run_picture<u8, 2>(*pic);
         else e = run_picture<u16, 2>(*pic);
         ++pics;

@@ -32,6 +32,8 @@
 #include "avc_recon.h"
 #include "gpu.h"
 
+#include <type_traits>
+
 namespace vep::gpu {
 
 using avc::MbRec;
@@ -227,24 +229,25 @@ VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
   }
 }
 
-// avc.cpp deblock_t for one MB (bS per 4-line segment from avc_bs_kernel), on the wave's LDS
-// tile: the MB and the samples its edges reach (luma rows / columns -4..15, chroma -2..) are
-// loaded once, the edges run in order in LDS, and the tile goes back once. (The MBs of a step
-// touch disjoint samples, and every earlier step is complete, so the tile is exact and writing
-// all of it back is safe.)
-template <class P, int CF>
-VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
+// avc.cpp deblock_t for one MB (bS per 4-line segment from avc_bs_kernel), on an LDS tile: the
+// MB and the samples its edges reach (luma rows / columns -4..15, chroma -2..) are loaded once,
+// the edges run in order, and the tile goes back once. (The MBs of a step touch disjoint
+// samples, and every earlier step is complete, so the tile is exact and writing all of it back
+// is safe.) NT lanes per MB: a whole wave (64), or half a wave (32: 4:2:0, whose 16 luma + 2 x 8
+// chroma lines fit, so a wave filters two MBs at once); `valid` false: this half has no MB.
+template <class P, int CF, int NT = 64>
+VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdDbk& L, int mb, int lane, bool valid = true) {
+  static_assert(NT == 64 || CF == 1, "half-wave MBs: 4:2:0 only");
   constexpr int CH = CF == 2 ? 16 : 8;
-  constexpr int NL = 20 * kDw, NC = 2 * (CH + 2) * kDcw;  // tile samples
-  HbdDbk& L = LW.db;
+  if (!valid) mb = 0;
   const MbRec q = recd(d, mb);
-  if (q.dbk & 1) return;
-  // bS and the thresholds (avc_bs_kernel, 8-bit scale) into the wave's LDS once per MB: no table
-  // lookup on the filters' dependency chain, and the lane-indexed reads stay out of scratch
+  // bS and the thresholds (avc_bs_kernel, 8-bit scale) into LDS once per MB: no table lookup on
+  // the filters' dependency chain, and the lane-indexed reads stay out of scratch
   const AvcDbkInfo* infos = static_cast<const AvcDbkInfo*>(d.dbk);
-  if (!infos[mb].any) return;
+  const bool on = valid && !(q.dbk & 1) && infos[mb].any;
+  if (NT == 64 && !on) return;  // (whole-wave MB: uniform)
   const AvcDbkInfo& info = L.info;
-  if (lane < 16) reinterpret_cast<u32*>(&L.info)[lane] = reinterpret_cast<const u32*>(&infos[mb])[lane];
+  if (on && lane < 16) reinterpret_cast<u32*>(&L.info)[lane] = reinterpret_cast<const u32*>(&infos[mb])[lane];
   const int W = d.wmbs, pitch = W * 16, mx = mb % W, my = mb / W, bd = sizeof(P) == 1 ? 8 : d.bd;
   const int sh = bd - 8;
   const bool t8 = (q.flags & avc::kMbT8x8) != 0;
@@ -252,52 +255,63 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
   VEP_DEV P* UV = reinterpret_cast<VEP_DEV P*>(d.uv + d.slot_uv * u64(d.target));
   // edge class k (0: left MB edge, 1: top MB edge, 2: internal) of component c
   const long ny = long(pitch) * d.hmbs * 16, nuv = long(pitch) * d.hmbs * CH;
-  // tile sample t -> picture index (-1: outside the picture, left / above the MB's neighbours)
-  auto luma_at = [&](int t) -> long {
-    const int y = t / kDw - 4, x = t % kDw - 4;
+  // The tile moves in groups of 4 consecutive picture samples (one 4- or 8-byte access): luma
+  // tile row y (-4..15) is 5 groups, columns 4g - 4 .. 4g - 1; a chroma tile row (-2..CH-1) is
+  // the 20 interleaved Cb / Cr samples of columns -2..7, 5 groups of 2 columns x 2 components.
+  // Group index -> picture index of its first sample (-1: left of / above the picture).
+  constexpr int NLG = 20 * 5, NCG = (CH + 2) * 5;
+  auto luma_grp = [&](int g) -> long {
+    const int y = g / 5 - 4, x = 4 * (g % 5) - 4;
     if (my * 16 + y < 0 || mx * 16 + x < 0) return -1;
     return long(my * 16 + y) * pitch + mx * 16 + x;
   };
-  // chroma tile sample t: component t / ((CH + 2) * kDcw), then its entry r = y * kDcw + x
-  auto chroma_at = [&](int t, int& c, int& r) -> long {
-    c = t / ((CH + 2) * kDcw);
-    r = t % ((CH + 2) * kDcw);
-    const int y = r / kDcw - 2, x = r % kDcw - 2;
+  auto chroma_grp = [&](int g) -> long {
+    const int y = g / 5 - 2, x = 2 * (g % 5) - 2;
     if (my * CH + y < 0 || mx * 8 + x < 0) return -1;
-    return long(my * CH + y) * pitch + (mx * 8 + x) * 2 + c;
+    return long(my * CH + y) * pitch + (mx * 8 + x) * 2;
   };
-  const bool pf = d.prof && hbd_thread0();  // (VEP_AVC_PROF: wave 0's MB phases)
+  using V4 = typename std::conditional<sizeof(P) == 1, u32, u64>::type;  // 4 samples
+  auto get4 = [](V4 v, int k) { return int((v >> (8 * sizeof(P) * k)) & ((V4(1) << (8 * sizeof(P))) - 1)); };
+  const bool pf = on && d.prof && hbd_thread0();  // (VEP_AVC_PROF: wave 0's MB phases)
   const u64 c0 = pf ? hbd_clock() : 0;
   // every load of the tile in flight at once: unconditional loads at clamped indices (a
   // conditional load would wait at its join), then the LDS stores
-  constexpr int KL = (NL + 63) / 64, KC = (NC + 63) / 64;
-  int lv[KL], cv[KC];
+  constexpr int KL = (NLG + NT - 1) / NT, KC = (NCG + NT - 1) / NT;
+  V4 lv[KL], cv[KC];
 #pragma unroll
   for (int j = 0; j < KL; ++j) {
-    const int t = lane + 64 * j;
-    const long i = t < NL ? luma_at(t) : -1;
-    const bool ok = i >= 0 && i < ny;
+    const int g = lane + NT * j;
+    const long i = on && g < NLG ? luma_grp(g) : -1;
+    const bool ok = i >= 0 && i + 3 < ny;
     if (i >= 0 && !ok) oob(d, i, ny, kOobDbkLuma);
-    lv[j] = int(Y[ok ? i : 0]);
+    lv[j] = *reinterpret_cast<const VEP_DEV V4*>(Y + (ok ? i : 0));
   }
 #pragma unroll
   for (int j = 0; j < KC; ++j) {
-    const int t = lane + 64 * j;
-    int c = 0, r = 0;
-    const long i = t < NC ? chroma_at(t, c, r) : -1;
-    const bool ok = i >= 0 && i < nuv;
+    const int g = lane + NT * j;
+    const long i = on && g < NCG ? chroma_grp(g) : -1;
+    const bool ok = i >= 0 && i + 3 < nuv;
     if (i >= 0 && !ok) oob(d, i, nuv, kOobDbkChroma);
-    cv[j] = int(UV[ok ? i : 0]);
+    cv[j] = *reinterpret_cast<const VEP_DEV V4*>(UV + (ok ? i : 0));
   }
 #pragma unroll
   for (int j = 0; j < KL; ++j) {
-    const int t = lane + 64 * j;
-    if (t < NL) L.y[t] = lv[j];
+    const int g = lane + NT * j;
+    if (g < NLG) {
+      int* o = &L.y[(g / 5) * kDw + 4 * (g % 5)];
+      for (int k = 0; k < 4; ++k) o[k] = get4(lv[j], k);
+    }
   }
 #pragma unroll
   for (int j = 0; j < KC; ++j) {
-    const int t = lane + 64 * j;
-    if (t < NC) L.c[t / ((CH + 2) * kDcw)][t % ((CH + 2) * kDcw)] = cv[j];
+    const int g = lane + NT * j;
+    if (g < NCG) {
+      const int r = (g / 5) * kDcw + 2 * (g % 5);
+      L.c[0][r] = get4(cv[j], 0);
+      L.c[1][r] = get4(cv[j], 1);
+      L.c[0][r + 1] = get4(cv[j], 2);
+      L.c[1][r + 1] = get4(cv[j], 3);
+    }
   }
   wsync();
   const u64 c1 = pf ? hbd_clock() : 0;
@@ -321,7 +335,7 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
     for (int r = 0; r < 4; ++r) {
       const int e = all4 ? r : 2 * r;
       int bs = 0;
-      if (act && e < 4) {
+      if (on && act && e < 4) {
         if (luma) bs = (e & 1) && t8 ? 0 : bs_of(dir * 16 + e * 4 + (k >> 2));  // (4:2:2 t8: chroma only)
         // chroma: bS of the luma line through it (vertical: luma row k, 4:2:0 2k; horizontal: column 2k)
         else bs = bs_of(dir * 16 + e * 4 + (dir == 0 && CF == 2 ? k >> 2 : k >> 1));
@@ -367,28 +381,37 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
     wsync();
   }
   const u64 c2 = pf ? hbd_clock() : 0;
+  auto put4 = [](int a, int b, int c, int e) {
+    constexpr int B = 8 * sizeof(P);
+    return V4(u32(a)) | V4(u32(b)) << B | V4(u32(c)) << (2 * B) | V4(u32(e)) << (3 * B);
+  };
 #pragma unroll
   for (int j = 0; j < KL; ++j) {
-    const int t = lane + 64 * j;
-    lv[j] = t < NL ? L.y[t] : 0;
+    const int g = lane + NT * j;
+    if (g < NLG) {
+      const int* o = &L.y[(g / 5) * kDw + 4 * (g % 5)];
+      lv[j] = put4(o[0], o[1], o[2], o[3]);
+    }
   }
 #pragma unroll
   for (int j = 0; j < KC; ++j) {
-    const int t = lane + 64 * j;
-    cv[j] = t < NC ? L.c[t / ((CH + 2) * kDcw)][t % ((CH + 2) * kDcw)] : 0;
+    const int g = lane + NT * j;
+    if (g < NCG) {
+      const int r = (g / 5) * kDcw + 2 * (g % 5);
+      cv[j] = put4(L.c[0][r], L.c[1][r], L.c[0][r + 1], L.c[1][r + 1]);
+    }
   }
 #pragma unroll
   for (int j = 0; j < KL; ++j) {
-    const int t = lane + 64 * j;
-    const long i = t < NL ? luma_at(t) : -1;
-    if (i >= 0 && !oob(d, i, ny, kOobStore)) Y[i] = P(lv[j]);
+    const int g = lane + NT * j;
+    const long i = on && g < NLG ? luma_grp(g) : -1;
+    if (i >= 0 && !oob(d, i + 3, ny, kOobStore)) *reinterpret_cast<VEP_DEV V4*>(Y + i) = lv[j];
   }
 #pragma unroll
   for (int j = 0; j < KC; ++j) {
-    const int t = lane + 64 * j;
-    int c = 0, r = 0;
-    const long i = t < NC ? chroma_at(t, c, r) : -1;
-    if (i >= 0 && !oob(d, i, nuv, kOobStore)) UV[i] = P(cv[j]);
+    const int g = lane + NT * j;
+    const long i = on && g < NCG ? chroma_grp(g) : -1;
+    if (i >= 0 && !oob(d, i + 3, nuv, kOobStore)) *reinterpret_cast<VEP_DEV V4*>(UV + i) = cv[j];
   }
   wsync();  // (the tile is reused by the wave's next MB)
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -413,7 +436,10 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   // (uniform over the workgroup, before any barrier)
   if ((d.bd > 8) != (sizeof(P) == 2) || (d.cf == 2) != (CF == 2)) return;
   if (!(PASS == 0 ? d.intra_mbs > 0 : d.deblock != 0)) return;
-  __shared__ HbdWave lds[kHbdWaves];
+  // 4:2:0 loop filter: two MBs per wave (half a wave each, a tile each)
+  constexpr bool kHalf = PASS == 1 && CF == 1;
+  constexpr int kTiles = kHalf ? 2 : 1;
+  __shared__ HbdWave lds[kHbdWaves][kTiles];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int W = d.wmbs, H = d.hmbs, steps = W + 2 * (H - 1);
   const bool prof = d.prof && threadIdx.x == 0;  // (VEP_AVC_PROF=1: workgroup phase clocks)
@@ -421,12 +447,21 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   const u64 tp = prof ? clock64() : 0;
   for (int t = 0; t < steps; ++t) {
     const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
-    for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
-      const int mb = y * W + t - 2 * y;
-      // (the descriptor by reference into global memory: a local copy passed by reference
-      // would live in scratch)
-      if (PASS == 0) intra_mb<P, CF>(descs[pic], lds[wave], mb, lane);
-      else deblock_mb<P, CF>(descs[pic], lds[wave], mb, lane);
+    // (the descriptor by reference into global memory: a local copy passed by reference would
+    // live in scratch)
+    if constexpr (kHalf) {
+      const int hh = lane >> 5;
+      for (int y0 = ylo + 2 * wave; y0 <= yhi; y0 += 2 * kHbdWaves) {  // (wave-uniform)
+        const int y = y0 + hh;
+        deblock_mb<P, CF, 32>(descs[pic], lds[wave][hh].db, y * W + t - 2 * y, lane & 31,
+                              y <= yhi);
+      }
+    } else {
+      for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
+        const int mb = y * W + t - 2 * y;
+        if (PASS == 0) intra_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
+        else deblock_mb<P, CF>(descs[pic], lds[wave][0].db, mb, lane);
+      }
     }
     const u64 ts = prof ? clock64() : 0;
     __syncthreads();
