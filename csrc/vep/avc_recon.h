@@ -90,6 +90,14 @@ constexpr u32 kNoRes = 0xFFFFFFFFu;
 VEP_HD int mv_per_list(u8 flags) { return (flags & kMbMv16) ? 2 : ((flags & kMbMv8x8) ? 8 : 32); }
 // Offset (i16 units, from the MB's pool base) of the (x, y) vector of raster 4x4 block `blk` in
 // list `list`.
+// Byte i of a 4-byte array (MbRec::ref / ref1) as one word and a shift: an index into the
+// array itself, when it varies per GPU lane, puts the whole record in scratch memory.
+VEP_HD int byte_at(const u8* a, int i) {
+  u32 w;
+  __builtin_memcpy(&w, a, 4);
+  return int((w >> (8 * i)) & 0xFFu);
+}
+
 VEP_HD int mv_sub(u8 flags, int list, int blk) {
   const int k = (flags & kMbMv16) ? 0 : ((flags & kMbMv8x8) ? 2 * (((blk >> 3) << 1) | ((blk & 3) >> 1)) : 2 * blk);
   return list * mv_per_list(flags) + k;
@@ -978,8 +986,8 @@ VEP_HD int boundary_strength_mv(const MbRec& mp, int bp, const i16* mv_p, const 
                                 const i16* mv_q, int ylim) {
   if (((mp.nz >> bp) & 1) || ((mq.nz >> bq) & 1)) return 2;
   const int p8 = ((bp >> 3) << 1) | ((bp & 3) >> 1), q8 = ((bq >> 3) << 1) | ((bq & 3) >> 1);
-  const int p0 = mp.ref[p8], p1 = (mp.flags & kMbL1) ? mp.ref1[p8] : 0xFF;
-  const int q0 = mq.ref[q8], q1 = (mq.flags & kMbL1) ? mq.ref1[q8] : 0xFF;
+  const int p0 = byte_at(mp.ref, p8), p1 = (mp.flags & kMbL1) ? byte_at(mp.ref1, p8) : 0xFF;
+  const int q0 = byte_at(mq.ref, q8), q1 = (mq.flags & kMbL1) ? byte_at(mq.ref1, q8) : 0xFF;
   const int np = (p0 != 0xFF) + (p1 != 0xFF), nq = (q0 != 0xFF) + (q1 != 0xFF);
   if (np != nq) return 1;
   const i16* pa = mv_p + mv_sub(mp.flags, 0, bp);  // list 0 of P

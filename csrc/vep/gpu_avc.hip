@@ -189,7 +189,7 @@ __device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int la
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     const int y = y0 + 4 * k, blk = k * 4 + (x >> 2), b8 = ((y >> 3) << 1) | (x >> 3);
-    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
+    const int s0 = avc::byte_at(m.ref, b8), s1 = l1 ? avc::byte_at(m.ref1, b8) : 0xFF;
     int p0 = 0, p1 = 0;
     if (s0 != 0xFF) {
       const i16* v0 = mvb + avc::mv_sub(m.flags, 0, blk);
@@ -220,7 +220,7 @@ __device__ inline void inter_mb(const AvcDesc& d, const MbRec& m, int mb, int la
     const int t = lane + 64 * k, cc = t / CS, cq = t % CS, cx = cq & 7, cy = cq >> 3;
     const int ly = CF == 2 ? cy : 2 * cy;  // luma row of the sample
     const int r = (ly >> 2) * 4 + (cx >> 1), b8 = ((ly >> 3) << 1) | (cx >> 2);
-    const int s0 = m.ref[b8], s1 = l1 ? m.ref1[b8] : 0xFF;
+    const int s0 = avc::byte_at(m.ref, b8), s1 = l1 ? avc::byte_at(m.ref1, b8) : 0xFF;
     int p0 = 0, p1 = 0, ix, fx, iy, fy;
     if (s0 != 0xFF) {
       const i16* v0 = mvb + avc::mv_sub(m.flags, 0, r);
@@ -854,12 +854,15 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
     info.any = (info.bs[0] | info.bs[1] | info.bs[2] | info.bs[3]) ? 1 : 0;
     // thresholds at 8-bit scale (QPs less the QpBdOffset bias; avc_hbd_kernel shifts them by
     // bd - 8)
-    const MbRec* ps[3] = {&lm, &tm, &q};
+    // (the P-side record by value select, not through an array of pointers to the locals, which
+    // would put the records in scratch)
     const int qb = d.qp_bias, qcb = d.qpc_bias;
+#pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const avc::EdgeParams ep[3] = {avc::edge_params(ps[k]->qp - qb, q.qp - qb, q.alpha_off, q.beta_off),
-                                     avc::edge_params(ps[k]->qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off),
-                                     avc::edge_params(ps[k]->qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off)};
+      const MbRec& pk = k == 0 ? lm : (k == 1 ? tm : q);
+      const avc::EdgeParams ep[3] = {avc::edge_params(pk.qp - qb, q.qp - qb, q.alpha_off, q.beta_off),
+                                     avc::edge_params(pk.qpc - qcb, q.qpc - qcb, q.alpha_off, q.beta_off),
+                                     avc::edge_params(pk.qpc2 - qcb, q.qpc2 - qcb, q.alpha_off, q.beta_off)};
       for (int c = 0; c < 3; ++c) {
         info.alpha[c * 3 + k] = u8(ep[c].alpha);
         info.beta[c * 3 + k] = u8(ep[c].beta);
