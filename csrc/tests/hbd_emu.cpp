@@ -110,7 +110,7 @@ static int run_picture(const avc::Picture& pic, bool half = false) {
         const int mb = yy * W + t - 2 * yy;
         for (int lane = 0; lane < 64; ++lane) {
           if (pass == 0) gpu::intra_mb<P, CF>(d, L, mb, lane);
-          else if (CF == 1 && half) gpu::deblock_mb<P, 1, 32>(d, L.db, mb, lane & 31, true);
+          else if (half) gpu::deblock_mb<P, CF, 32>(d, L.db, mb, lane & 31, true);
           else gpu::deblock_mb<P, CF>(d, L.db, mb, lane);
         }
       }
@@ -140,8 +140,8 @@ int main() {
         auto pic = dec.parse(*au, 0, nullptr);
         int e;
         if (variant == 0) e = run_picture<u16, 1>(*pic) | run_picture<u16, 1>(*pic, true);
-        else if (variant == 1) e = run_picture<u8, 2>(*pic);
-        else e = run_picture<u16, 2>(*pic);
+        else if (variant == 1) e = run_picture<u8, 2>(*pic) | run_picture<u8, 2>(*pic, true);
+        else e = run_picture<u16, 2>(*pic) | run_picture<u16, 2>(*pic, true);
         ++pics;
         if (e) std::printf("variant %d seed %d picture %d: bound-check bits 0x%x\n", variant, seed, i, e);
         worst |= e;
@@ -177,8 +177,8 @@ int main() {
         if (!pic) continue;
         int e;
         if (k.cf != 2) e = run_picture<u16, 1>(*pic) | run_picture<u16, 1>(*pic, true);
-        else if (k.bd == 8) e = run_picture<u8, 2>(*pic);
-        else e = run_picture<u16, 2>(*pic);
+        else if (k.bd == 8) e = run_picture<u8, 2>(*pic) | run_picture<u8, 2>(*pic, true);
+        else e = run_picture<u16, 2>(*pic) | run_picture<u16, 2>(*pic, true);
         ++pics;
         if (e) std::printf("camera bd %d cf %d picture %d: bound-check bits 0x%x\n", k.bd, k.cf, i, e);
         worst |= e;

@@ -233,11 +233,11 @@ VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
 // MB and the samples its edges reach (luma rows / columns -4..15, chroma -2..) are loaded once,
 // the edges run in order, and the tile goes back once. (The MBs of a step touch disjoint
 // samples, and every earlier step is complete, so the tile is exact and writing all of it back
-// is safe.) NT lanes per MB: a whole wave (64), or half a wave (32: 4:2:0, whose 16 luma + 2 x 8
-// chroma lines fit, so a wave filters two MBs at once); `valid` false: this half has no MB.
+// is safe.) NT lanes per MB: a whole wave (64), or half a wave (32, so a wave filters two MBs at
+// once; the 48 lines of a 4:2:2 MB's vertical edges take two rounds); `valid` false: this half
+// has no MB.
 template <class P, int CF, int NT = 64>
 VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdDbk& L, int mb, int lane, bool valid = true) {
-  static_assert(NT == 64 || CF == 1, "half-wave MBs: 4:2:0 only");
   constexpr int CH = CF == 2 ? 16 : 8;
   if (!valid) mb = 0;
   const MbRec q = recd(d, mb);
@@ -322,11 +322,18 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdDbk& L, int mb, int lane, bool v
   // registers 4r + 3 and 4r + 4) is luma MB edge r, and chroma edge r is chroma sample 4r (MB edges
   // 0 and 2; 4:2:2 horizontal: all four). The line's four edges then run in order in registers,
   // with one LDS round trip per direction instead of one per edge.
-  const bool luma = lane < 16;
 #pragma unroll
   for (int dir = 0; dir < 2; ++dir) {
     const int nlc = dir == 0 ? CH : 8;  // chroma lines per component
-    const int cl = lane - 16, c = luma ? 0 : cl / nlc, k = luma ? lane : cl % nlc;
+    // line slots: 16 luma lines, then 2 x nlc chroma lines, NT at a time (4:2:2 vertical edges
+    // with half a wave per MB: two rounds)
+    constexpr int kRounds = (16 + 2 * CH + NT - 1) / NT;
+#pragma unroll
+    for (int rho = 0; rho < kRounds; ++rho) {
+    const int slot = lane + NT * rho;
+    if (rho > 0 && 16 + 2 * nlc <= NT * rho) break;  // (uniform)
+    const bool luma = slot < 16;
+    const int cl = slot - 16, c = luma ? 0 : cl / nlc, k = luma ? slot : cl % nlc;
     const bool act = luma || c < 2;
     const bool all4 = luma || (CF == 2 && dir == 1);
     const int comp = luma ? 0 : 1 + c;
@@ -378,6 +385,7 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdDbk& L, int mb, int lane, bool v
 #pragma unroll
     for (int i = 0; i < 20; ++i)
       if (i >= off && i - off < n) base[(i - off) * stride] = v[i];
+    }  // rounds (each lane's lines are its own: no sync between them)
     wsync();
   }
   const u64 c2 = pf ? hbd_clock() : 0;
@@ -436,8 +444,8 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   // (uniform over the workgroup, before any barrier)
   if ((d.bd > 8) != (sizeof(P) == 2) || (d.cf == 2) != (CF == 2)) return;
   if (!(PASS == 0 ? d.intra_mbs > 0 : d.deblock != 0)) return;
-  // 4:2:0 loop filter: two MBs per wave (half a wave each, a tile each)
-  constexpr bool kHalf = PASS == 1 && CF == 1;
+  // loop filter: two MBs per wave (half a wave each, a tile each)
+  constexpr bool kHalf = PASS == 1;
   constexpr int kTiles = kHalf ? 2 : 1;
   __shared__ HbdWave lds[kHbdWaves][kTiles];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
