@@ -463,23 +463,29 @@ VEP_HD int hk_sao_sample(const P* src, int stride, int step, const GpuSao& sp, i
                          int bd = 8) {
   const int v = src[y * stride + x * step];
   const int type = sp.type[c];
+  // offset k of component c: a shift out of the component's four offsets as one word (an index
+  // into the arrays, varying per GPU lane, would put the parameters in scratch memory)
+  u32 ow;
+  __builtin_memcpy(&ow, sp.off[c], 4);
+  auto off = [&](int k) { return int(i8(u8(ow >> (8 * k)))); };
   if (type == 1) {
     const int k = ((v >> (bd - 5)) - sp.band[c]) & 31;
-    return k < 4 ? hk_clip(v + sp.off[c][k], bd) : v;
+    return k < 4 ? hk_clip(v + off(k), bd) : v;
   }
-  const int hx[4][2] = {{-1, 1}, {0, 0}, {-1, 1}, {1, -1}};
-  const int vy[4][2] = {{0, 0}, {-1, 1}, {-1, 1}, {-1, 1}};
+  // edge class: 0 horizontal (-1, 0) / (1, 0), 1 vertical (0, -1) / (0, 1), 2 135 degrees
+  // (-1, -1) / (1, 1), 3 45 degrees (1, -1) / (-1, 1)
   const int e = sp.eo[c];
+  const int dx = e == 1 ? 0 : (e == 3 ? 1 : -1), dy = e == 0 ? 0 : -1;
   int sgn = 0;
   for (int t = 0; t < 2; ++t) {
-    const int nx = x + hx[e][t], ny = y + vy[e][t];
+    const int nx = x + (t ? -dx : dx), ny = y + (t ? -dy : dy);
     if (!nb_ok(nx, ny)) return v;
     const int nv = src[ny * stride + nx * step];
     sgn += (v > nv) - (v < nv);
   }
   int edge = 2 + sgn;
   if (edge <= 2) edge = edge == 2 ? 0 : edge + 1;
-  return edge ? hk_clip(v + sp.off[c][edge - 1], bd) : v;
+  return edge ? hk_clip(v + off(edge - 1), bd) : v;
 }
 
 }  // namespace vep::hevc
