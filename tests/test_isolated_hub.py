@@ -257,7 +257,8 @@ def test_camera_group_fault_containment(native, tmp_path, monkeypatch):
         deadline = time.time() + 60
         while time.time() < deadline and hub.child_restarts[bad] == 0:
             for n in others:  # the other group keeps serving while c1's group crashes
-                r = wait_frames(hub, n, timeout=5, after=seqs[n])
+                # (15 s: a loaded CI host can hold a CPU worker's next picture for seconds)
+                r = wait_frames(hub, n, timeout=15, after=seqs[n])
                 assert r is not None, f"{n} stopped serving"
                 seqs[n] = r[0]
             time.sleep(0.05)
