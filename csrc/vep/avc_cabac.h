@@ -262,18 +262,23 @@ struct AvcBins {
 // Decoder direction of residual_block_cabac, the parse hot loop (most bins of a High-profile
 // picture): same bins, same context selection as the generic body above, with the arithmetic
 // decoder held in a local copy so range/offset/bit cache stay in registers across the context
-// byte updates (see cabac.h).
-template <>
-inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef, u8* nzpos) {
-  cabac::Ctx* const ctx = e.ctx;
-  cabac::Decoder d = e.d;
-  if (cbf_inc >= 0 && !d.decision(ctx[85 + kCbfCatOff[cat] + cbf_inc])) {
-    e.d = d;
+// byte updates (see cabac.h). One instantiation per block category: the context bases, the
+// scan length and the 8x8 / chroma DC special cases are constants of the loop.
+template <int CAT>
+inline int residual_dec(cabac::Ctx* const ctx, cabac::Decoder& engine, int cbf_inc, int n_dc, int* coef,
+                        u8* nzpos) {
+  constexpr bool b8 = CAT == kCatLuma8x8, cdc = CAT == kCatChromaDc;
+  // (chroma DC: 4 or, in 4:2:2, 8 coefficients; the others are fixed)
+  constexpr int kN = CAT == kCatLumaAc || CAT == kCatChromaAc ? 15 : (b8 ? 64 : 16);
+  const int n = cdc ? n_dc : kN;
+  cabac::Decoder d = engine;
+  // (cbf_inc < 0: no coded_block_flag — the 8x8 blocks of 4:2:0)
+  if (!b8 && cbf_inc >= 0 && !d.decision(ctx[85 + kCbfCatOff[b8 ? 0 : CAT] + cbf_inc])) {
+    engine = d;
     return 0;
   }
   int num = 0, i = 0;
-  const bool b8 = cat == kCatLuma8x8;
-  if (b8) {
+  if constexpr (b8) {
     cabac::Ctx* const sig = ctx + 402;
     cabac::Ctx* const last = ctx + 417;
     for (; i < 63; ++i)
@@ -282,9 +287,9 @@ inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef,
         if (d.decision(last[kLast8x8[i]])) break;
       }
   } else {
-    cabac::Ctx* const sig = ctx + 105 + kSigCatOff[cat];
-    cabac::Ctx* const last = ctx + 166 + kSigCatOff[cat];
-    if (cat == kCatChromaDc) {
+    cabac::Ctx* const sig = ctx + 105 + kSigCatOff[CAT];
+    cabac::Ctx* const last = ctx + 166 + kSigCatOff[CAT];
+    if constexpr (cdc) {
       const int dsh = n == 8 ? 1 : 0;  // Min(i / NumC8x8, 2): 4:2:2 has NumC8x8 = 2
       for (; i < n - 1; ++i) {
         const int si = (i >> dsh) < 2 ? (i >> dsh) : 2;
@@ -294,7 +299,7 @@ inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef,
         }
       }
     } else {
-      for (; i < n - 1; ++i)
+      for (; i < kN - 1; ++i)
         if (d.decision(sig[i])) {
           nzpos[num++] = u8(i);
           if (d.decision(last[i])) break;
@@ -302,8 +307,8 @@ inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef,
     }
   }
   if (i == n - 1) nzpos[num++] = u8(n - 1);
-  cabac::Ctx* const absc = ctx + (b8 ? 426 : 227 + kAbsCatOff[cat]);
-  const int gt1_max = cat == kCatChromaDc ? 3 : 4;
+  cabac::Ctx* const absc = ctx + (b8 ? 426 : 227 + kAbsCatOff[b8 ? 0 : CAT]);
+  constexpr int gt1_max = cdc ? 3 : 4;
   int gt1 = 0, eq1 = 0;
   for (int k = num - 1; k >= 0; --k) {
     int level = 1;
@@ -327,8 +332,20 @@ inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef,
     }
     coef[nzpos[k]] = d.bypass() ? -level : level;
   }
-  e.d = d;
+  engine = d;
   return num;
+}
+
+template <>
+inline int AvcBins<BinDecoder>::residual(int cat, int cbf_inc, int n, int* coef, u8* nzpos) {
+  switch (cat) {
+    case kCatLumaDc: return residual_dec<kCatLumaDc>(e.ctx, e.d, cbf_inc, n, coef, nzpos);
+    case kCatLumaAc: return residual_dec<kCatLumaAc>(e.ctx, e.d, cbf_inc, n, coef, nzpos);
+    case kCatLuma4x4: return residual_dec<kCatLuma4x4>(e.ctx, e.d, cbf_inc, n, coef, nzpos);
+    case kCatChromaDc: return residual_dec<kCatChromaDc>(e.ctx, e.d, cbf_inc, n, coef, nzpos);
+    case kCatChromaAc: return residual_dec<kCatChromaAc>(e.ctx, e.d, cbf_inc, n, coef, nzpos);
+    default: return residual_dec<kCatLuma8x8>(e.ctx, e.d, cbf_inc, n, coef, nzpos);
+  }
 }
 
 // Decoder direction of mvd_lX (UEG3, signed, uCoff 9), the second-largest bin consumer of P/B
