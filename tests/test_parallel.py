@@ -182,6 +182,21 @@ def test_bench_keyframe_only_rtsp_cpu():
     assert 0 < d["frames_decoded"] < d["access_units_ingested"]
 
 
+@pytest.mark.parametrize("fmt", [["--bit-depth", "10"], ["--chroma-format", "2"]], ids=["high10", "422"])
+def test_bench_high_formats_rtsp_cpu(fmt):
+    """The headline bench with H.264 High 10 / High 4:2:2 streams (CPU backend): every picture
+    decodes and publishes, the JSON names the profile and reports the launch statistics."""
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--cpu", "--source", "rtsp", "--steps", "1",
+           "--warmup", "1", "--width", "96", "--height", "64", "--cams-per-gpu", "2", "--gop", "6",
+           "--letterbox", "32", "--latency-samples", "0", "--threads", "1"] + fmt
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert d["frames_dropped"] == 0 and d["frames_decoded"] >= 12
+    assert ("High 10" if fmt[0] == "--bit-depth" else "High 4:2:2") in d["data"]
+    assert d["rank0_pictures_per_launch"] > 0
+
+
 def test_hostprof_samples_native_threads(native, tmp_path):
     """The extension's SIGPROF sampler records where host CPU time goes (parse hot spots)."""
     import time
