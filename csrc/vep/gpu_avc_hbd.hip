@@ -453,11 +453,37 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   const bool prof = d.prof && threadIdx.x == 0;  // (VEP_AVC_PROF=1: workgroup phase clocks)
   u64 tb = 0;
   const u64 tp = prof ? clock64() : 0;
+  // Intra pass: the intra MBs and the diagonal steps that hold any, listed in LDS up front (one
+  // parallel scan of the records), so a P / B picture's few intra MBs cost a few steps instead of
+  // a record load per MB and a barrier per step of the whole picture.
+  constexpr int kMaxMbs = PASS == 0 ? 16384 : 1, kMaxSteps = PASS == 0 ? 1024 : 1;
+  __shared__ u8 intra_at[kMaxMbs];
+  __shared__ u8 step_has[kMaxSteps];
+  const bool listed = PASS == 0 && W * H <= kMaxMbs && steps <= kMaxSteps;
+  if (listed) {
+    for (int i = int(threadIdx.x); i < steps; i += 64 * kHbdWaves) step_has[i] = 0;
+    __syncthreads();
+    const MbRec* recs = static_cast<const MbRec*>(d.mbs);
+    for (int i = int(threadIdx.x); i < W * H; i += 64 * kHbdWaves) {
+      const bool in = avc::is_wave_intra(recs[i].kind);
+      intra_at[i] = in ? 1 : 0;
+      if (in) step_has[i % W + 2 * (i / W)] = 1;  // (benign race: every writer stores 1)
+    }
+    __syncthreads();
+  }
   for (int t = 0; t < steps; ++t) {
+    if (listed && !step_has[t]) continue;  // (uniform: nothing of this step to predict)
     const int ylo = max(0, (t - W + 2) >> 1), yhi = min(H - 1, t >> 1);
     // (the descriptor by reference into global memory: a local copy passed by reference would
     // live in scratch)
-    if constexpr (kHalf) {
+    if (listed) {  // this step's intra MBs, dealt round-robin over the waves
+      int k = 0;
+      for (int y = ylo; y <= yhi; ++y) {
+        const int mb = y * W + t - 2 * y;
+        if (!intra_at[mb]) continue;
+        if (k++ % kHbdWaves == wave) intra_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
+      }
+    } else if constexpr (kHalf) {
       const int hh = lane >> 5;
       for (int y0 = ylo + 2 * wave; y0 <= yhi; y0 += 2 * kHbdWaves) {  // (wave-uniform)
         const int y = y0 + hh;
