@@ -177,7 +177,9 @@ def test_high10_camera_cpu_backend(native, kw):
     (176, 144, 12, dict(coverage=True, bframes=1, cabac=False, weighted_p=True, weighted_b=1, bit_depth=10)),
     (352, 288, 12, dict(coverage=True, bframes=2, bit_depth=9, deblock_idc=2, slices=3)),
     (1920, 1080, 6, dict(bframes=2, qp=24, temporal_noise=2.0, bit_depth=10)),
-], ids=["cov-cabac", "cov-cavlc-wp", "cov-9bit-dbk2", "1080p-ibbp"])
+    # 256 x 68 MBs: past the intra pass's LDS MB list (16384 MBs), which then walks every MB
+    (4096, 1088, 3, dict(bframes=0, qp=26, coverage=True, bit_depth=10)),
+], ids=["cov-cabac", "cov-cavlc-wp", "cov-9bit-dbk2", "1080p-ibbp", "4096x1088-unlisted"])
 def test_high10_gpu_bit_exact(native, w, h, n, kw):
     """gfx950: u16 surfaces, avc_inter_kernel<u16> + avc_hbd_kernel, narrow + convert."""
     assert run_camera(native, 0, w, h, n, **kw) >= n // 2
