@@ -9,6 +9,7 @@
 //   hipcc -std=c++17 -O1 -g -Xarch_host -fsanitize=address -fno-gpu-sanitize --offload-host-only -Icsrc \
 //     csrc/tests/hbd_emu.cpp csrc/vep/{avc_enc_high,avc_mb,avc_cabac,avc_cavlc,avc,h264,codec,
 //     fanout,hostmem,hostplan,hevc,ioloop}.cpp -o build/hbd_emu -lpthread
+#include <algorithm>
 #include <cstdio>
 #include <vector>
 
@@ -118,8 +119,36 @@ static int run_picture(const avc::Picture& pic, bool half = false) {
   return int(err);
 }
 
+// filter_samples_u (the GPU loop filter's one-stream form) against filter_samples, random lines
+static int check_filter_u() {
+  u64 st = 88172645463325252ull;
+  auto rnd = [&](int n) {
+    st ^= st << 13, st ^= st >> 7, st ^= st << 17;
+    return int(st % u64(n));
+  };
+  int bad = 0;
+  for (int it = 0; it < 2000000; ++it) {
+    const int bd = 8 + rnd(3), maxv = (1 << bd) - 1, bs = 1 + rnd(4), chroma = rnd(2);
+    const int base = rnd(maxv + 1), spread = 1 + rnd(40 << (bd - 8));
+    int p[4], q[4], p2[4], q2[4];
+    for (int k = 0; k < 4; ++k) {
+      p[k] = p2[k] = std::min(maxv, std::max(0, base + rnd(2 * spread + 1) - spread));
+      q[k] = q2[k] = std::min(maxv, std::max(0, base + rnd(2 * spread + 1) - spread));
+    }
+    const int ia = rnd(52), sh = bd - 8;
+    const int alpha = avc::kAlpha[ia] << sh, beta = avc::kBeta[rnd(52)] << sh, tc0 = avc::kTc0[ia][rnd(3)] << sh;
+    const bool a = avc::filter_samples(p, q, bs, alpha, beta, tc0, chroma, bd);
+    const bool b = avc::filter_samples_u(p2, q2, bs, alpha, beta, tc0, chroma, bd);
+    for (int k = 0; k < 4; ++k) bad += a != b || p[k] != p2[k] || q[k] != q2[k];
+  }
+  return bad;
+}
+
 int main() {
   int worst = 0, pics = 0;
+  const int fbad = check_filter_u();
+  std::printf("filter_samples_u vs filter_samples: %d mismatches\n", fbad);
+  if (fbad) return 1;
   for (int variant = 0; variant < 3; ++variant)
     for (int seed = 1; seed <= 3; ++seed) {
       avc::AvcHighConfig c;

@@ -1081,6 +1081,40 @@ VEP_HD bool filter_samples(int* p, int* q, int bs, int alpha, int beta, int tc0,
 }
 
 // filter_samples on samples in memory (stride `step` across the edge; s = q0).
+// filter_samples with one instruction stream for luma and chroma lines (GPU lanes of both kinds in
+// one wave): a chroma line is a luma line whose ap / aq tests fail (no p1 / q1 / strong update)
+// and whose tC is tC0 + 1. Same results as filter_samples for every input (hbd_emu checks it).
+VEP_HD bool filter_samples_u(int* p, int* q, int bs, int alpha, int beta, int tc0, bool chroma, int bd = 8) {
+  const int p0 = p[0], p1 = p[1], p2 = p[2], p3 = p[3], q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+  if (!(iabs(p0 - q0) < alpha && iabs(p1 - p0) < beta && iabs(q1 - q0) < beta)) return false;
+  const bool lp = !chroma && iabs(p2 - p0) < beta, lq = !chroma && iabs(q2 - q0) < beta;
+  if (bs < 4) {
+    const int tc = chroma ? tc0 + 1 : tc0 + int(lp) + int(lq);
+    const int dl = clip3(-tc, tc, (((q0 - p0) << 2) + (p1 - q1) + 4) >> 3);
+    p[0] = clip1(p0 + dl, bd);
+    q[0] = clip1(q0 - dl, bd);
+    if (lp) p[1] = p1 + clip3(-tc0, tc0, (p2 + ((p0 + q0 + 1) >> 1) - (p1 << 1)) >> 1);
+    if (lq) q[1] = q1 + clip3(-tc0, tc0, (q2 + ((p0 + q0 + 1) >> 1) - (q1 << 1)) >> 1);
+    return true;
+  }
+  const bool strong = iabs(p0 - q0) < ((alpha >> 2) + 2);
+  if (lp && strong) {
+    p[0] = (p2 + 2 * p1 + 2 * p0 + 2 * q0 + q1 + 4) >> 3;
+    p[1] = (p2 + p1 + p0 + q0 + 2) >> 2;
+    p[2] = (2 * p3 + 3 * p2 + p1 + p0 + q0 + 4) >> 3;
+  } else {
+    p[0] = (2 * p1 + p0 + q1 + 2) >> 2;
+  }
+  if (lq && strong) {
+    q[0] = (p1 + 2 * p0 + 2 * q0 + 2 * q1 + q2 + 4) >> 3;
+    q[1] = (p0 + q0 + q1 + q2 + 2) >> 2;
+    q[2] = (2 * q3 + 3 * q2 + q1 + q0 + p0 + 4) >> 3;
+  } else {
+    q[0] = (2 * q1 + q0 + p1 + 2) >> 2;
+  }
+  return true;
+}
+
 template <typename Px>
 VEP_HD void filter_line_t(Px* s, long step, int bs, int alpha, int beta, int tc0, bool chroma, int bd = 8) {
   const int n = chroma ? 2 : 4;

@@ -374,7 +374,7 @@ VEP_HBD_FN void deblock_mb(const AvcDesc& d, HbdDbk& L, int mb, int lane, bool v
       if (!bsr[r]) continue;
       int pp[4] = {v[4 * r + 3], v[4 * r + 2], v[4 * r + 1], v[4 * r]};
       int qq[4] = {v[4 * r + 4], v[4 * r + 5], v[4 * r + 6], v[4 * r + 7]};
-      avc::filter_samples(pp, qq, bsr[r], al[r], be[r], tc[r], !luma, bd);  // (in place; chroma: p0 / q0)
+      avc::filter_samples_u(pp, qq, bsr[r], al[r], be[r], tc[r], !luma, bd);  // (in place; chroma: p0 / q0)
       v[4 * r + 3] = pp[0];
       v[4 * r + 2] = pp[1];
       v[4 * r + 1] = pp[2];
