@@ -48,6 +48,7 @@ struct HbdIntra {
   int t[17 * kTw];      // luma: row 0 = p[-1..23, -1], row 1 + y = p[-1..23, y] (x > 15 unused)
   int c[2][17 * kCw];   // chroma per component: row 0 = p[-1..7, -1], row 1 + y = p[-1..7, y]
   int f[25];            // Intra_8x8 filtered references of the current 8x8 block
+  i16 r[kAvcResSamples];  // the MB's residual (avc_inter_kernel's slot), loaded once
 };
 constexpr int kDw = 20;   // loop-filter luma tile row: x = -4..15 (rows y = -4..15)
 constexpr int kDcw = 10;  // chroma tile row: x = -2..7 (rows y = -2..CH-1)
@@ -132,7 +133,15 @@ VEP_HBD_FN void intra_mb(const AvcDesc& d, HbdWave& LW, int mb, int lane) {
              D = avail(d, m, mx - 1, my - 1);
   const long ny = long(pitch) * d.hmbs * 16, nuv = long(pitch) * d.hmbs * CH;
   if (m.res != avc::kNoRes && oob(d, long(m.res), long(d.nres), kOobRes)) return;
-  const VEP_DEV i16* res = m.res == avc::kNoRes ? nullptr : d.res + size_t(m.res) * kAvcResSamples;
+  const bool has_res = m.res != avc::kNoRes;
+  // the residual into LDS in one round trip (8 samples a lane): a global load per 4x4 block
+  // would sit on the Intra_4x4 chain sixteen times
+  if (has_res) {
+    static_assert(kAvcResSamples == 64 * 8, "one 16-byte load per lane");
+    const VEP_DEV uint4* src = reinterpret_cast<const VEP_DEV uint4*>(d.res + size_t(m.res) * kAvcResSamples);
+    reinterpret_cast<uint4*>(L.r)[lane] = src[lane];
+  }
+  const i16* res = has_res ? L.r : nullptr;
   // ---- neighbours into the tile (128: an unavailable side, as the CPU's neighbour arrays)
   if (lane < 25) {  // top row x = -1..23
     const int x = lane - 1;
@@ -447,7 +456,8 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
   // loop filter: two MBs per wave (half a wave each, a tile each)
   constexpr bool kHalf = PASS == 1;
   constexpr int kTiles = kHalf ? 2 : 1;
-  __shared__ HbdWave lds[kHbdWaves][kTiles];
+  // (per pass its own tile type: the intra tile with the residual is the larger)
+  __shared__ typename std::conditional<PASS == 0, HbdWave, HbdDbk>::type lds[kHbdWaves][kTiles];
   const int wave = int(threadIdx.x) >> 6, lane = int(threadIdx.x) & 63;
   const int W = d.wmbs, H = d.hmbs, steps = W + 2 * (H - 1);
   const bool prof = d.prof && threadIdx.x == 0;  // (VEP_AVC_PROF=1: workgroup phase clocks)
@@ -481,20 +491,21 @@ __global__ __launch_bounds__(64 * kHbdWaves) void avc_hbd_kernel(const AvcDesc* 
       for (int y = ylo; y <= yhi; ++y) {
         const int mb = y * W + t - 2 * y;
         if (!intra_at[mb]) continue;
-        if (k++ % kHbdWaves == wave) intra_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
+        if constexpr (PASS == 0)
+          if (k++ % kHbdWaves == wave) intra_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
       }
     } else if constexpr (kHalf) {
       const int hh = lane >> 5;
       for (int y0 = ylo + 2 * wave; y0 <= yhi; y0 += 2 * kHbdWaves) {  // (wave-uniform)
         const int y = y0 + hh;
-        deblock_mb<P, CF, 32>(descs[pic], lds[wave][hh].db, y * W + t - 2 * y, lane & 31,
+        deblock_mb<P, CF, 32>(descs[pic], lds[wave][hh], y * W + t - 2 * y, lane & 31,
                               y <= yhi);
       }
     } else {
       for (int y = ylo + wave; y <= yhi; y += kHbdWaves) {
         const int mb = y * W + t - 2 * y;
-        if (PASS == 0) intra_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
-        else deblock_mb<P, CF>(descs[pic], lds[wave][0].db, mb, lane);
+        if constexpr (PASS == 0) intra_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
+        else deblock_mb<P, CF>(descs[pic], lds[wave][0], mb, lane);
       }
     }
     const u64 ts = prof ? clock64() : 0;
