@@ -749,13 +749,15 @@ PYBIND11_MODULE(_vep, m) {
   // QPC of Table 8-15 from QPY (QpBdOffsetC: High 10 QPs below 0)
   rc.def("chroma_qp_bd", [](int qpy, int offset, int qpbd_c) { return avc::chroma_qp_bd(qpy, offset, qpbd_c); });
   // one sample line across an edge: p = p0..p3, q = q0..q3 -> filtered (p, q)
+  // (unified: filter_samples_u, the one-stream luma / chroma form of the GPU High 10 / 4:2:2 filter)
   rc.def("filter_line", [](std::vector<int> p, std::vector<int> q, int bs, int alpha, int beta, int tc0,
-                           bool chroma, int bd) {
+                           bool chroma, int bd, bool unified) {
     VEP_CHECK(p.size() == 4 && q.size() == 4, "4 + 4 samples");
-    avc::filter_samples(p.data(), q.data(), bs, alpha, beta, tc0, chroma, bd);
+    if (unified) avc::filter_samples_u(p.data(), q.data(), bs, alpha, beta, tc0, chroma, bd);
+    else avc::filter_samples(p.data(), q.data(), bs, alpha, beta, tc0, chroma, bd);
     return py::make_tuple(p, q);
   }, py::arg("p"), py::arg("q"), py::arg("bs"), py::arg("alpha"), py::arg("beta"), py::arg("tc0"),
-     py::arg("chroma"), py::arg("bd") = 8);
+     py::arg("chroma"), py::arg("bd") = 8, py::arg("unified") = false);
 
   m.def("cavlc_roundtrip", [](int nc, int max_coeff, const std::vector<int>& c) {
     // write_residual_block -> read_residual_block (table self-consistency, tests only)

@@ -115,8 +115,12 @@ def test_deblocking_at_depth(rc, bd):
         bs = rnd.randint(1, 4)
         tc0 = tc0s[bs - 1] if bs < 4 else 0
         chroma = rnd.random() < 0.3
+        want = so.filter_line(p, q, bs, alpha, beta, tc0, chroma, bd)
         got = rc.filter_line(p, q, bs, alpha, beta, tc0, chroma, bd)
-        assert (list(got[0]), list(got[1])) == so.filter_line(p, q, bs, alpha, beta, tc0, chroma, bd)
+        assert (list(got[0]), list(got[1])) == want
+        # the GPU High 10 / 4:2:2 loop filter's one-stream luma / chroma form
+        got = rc.filter_line(p, q, bs, alpha, beta, tc0, chroma, bd, True)
+        assert (list(got[0]), list(got[1])) == want
 
 
 def test_chroma_qp_and_qp_wrap(rc):
