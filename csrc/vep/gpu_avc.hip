@@ -1355,64 +1355,59 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
       // neighbour's columns 12..15 if the left edge was filtered, and always the MB above's
       // final rows 12..15 (this wave is their only writer)
       const bool left = any && (L.info.bs[0] & 0xFFFFu) != 0;  // dir 0, edge 0 nibbles
+      // Every LDS read of the write-back first (in-range addresses for every lane, the values
+      // unused where a store below does not happen), so they are in flight together and the
+      // wave waits once, not once per store.
+      auto cbyte = [&](int c, int i) { return u32(L.c[c][i]); };
+      auto cword = [&](int base) {  // 2 columns x 2 components from chroma tile entry base
+        return cbyte(0, base) | cbyte(1, base) << 8 | cbyte(0, base + 1) << 16 | cbyte(1, base + 1) << 24;
+      };
+      const int q4 = l >> 2, r4 = (l & 3) * 4, cb = (l & 3) * 2, k16 = (l - 16) & 15;
+      const u32 w_top = ld4(&L.y[(q4 + 4) * 20 + 4 + r4]);                 // MB rows 0..7
+      const u32 w_bot = ld4(&L.y[(q4 + 12) * 20 + 4 + r4]);                // MB rows 8..15
+      const u32 w_c = cword((q4 + 2) * 12 + 4 + cb);                        // chroma rows 0..7
+      const u32 w_side = ld4(l < 16 ? &L.y[(l + 4) * 20]                    // left columns 12..15
+                                    : &L.y[(k16 >> 2) * 20 + 4 + (k16 & 3) * 4]);  // MB above, rows 12..15
+      const int l8 = l & 7, k8 = (l - 8) & 7;
+      const u32 w_cside = l < 8 ? cword((l8 + 2) * 12 + 2)                 // left chroma columns 6..7
+                                : cword((k8 >> 2) * 12 + 4 + (k8 & 3) * 2);  // above: chroma rows 6..7
+      const int kx = (l - 16) & 7;
+      const u32 w_x = l < 16 ? ld4(&L.y[(16 + q4) * 20 + 4 + r4])          // exchange: rows 12..15
+                             : cword((8 + (kx >> 2)) * 12 + 4 + (kx & 3) * 2);  // chroma rows 6..7
+      const u32 w_carry = ld4(&L.y[((l & 15) + 4) * 20 + 16]);
+      const int cc = ((l - 16) >> 3) & 1, ck = (l - 16) & 7;
+      const u8 cr0 = L.c[cc][(ck + 2) * 12 + 10], cr1 = L.c[cc][(ck + 2) * 12 + 11];
       if (any) {
-        u8* ym = Y + size_t(y0 + (l >> 2)) * pitch + x0 + (l & 3) * 4;
-        gst4(ym, ld4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4]));
-        if ((l >> 2) < 4 || last)
-          gst4(ym + size_t(8) * pitch, ld4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4]));
-        const int cyr = l >> 2, cb = (l & 3) * 2;
-        if (cyr < 6 || last) {
-          u32 cw = 0;
-          for (int q = 0; q < 2; ++q)
-            cw |= (u32(L.c[0][(cyr + 2) * 12 + 4 + cb + q]) | u32(L.c[1][(cyr + 2) * 12 + 4 + cb + q]) << 8)
-                  << (16 * q);
-          gst4(UV + size_t(row * 8 + cyr) * pitch + x0 + cb * 2, cw);
-        }
+        u8* ym = Y + size_t(y0 + q4) * pitch + x0 + r4;
+        gst4(ym, w_top);
+        if (q4 < 4 || last) gst4(ym + size_t(8) * pitch, w_bot);
+        if (q4 < 6 || last) gst4(UV + size_t(row * 8 + q4) * pitch + x0 + cb * 2, w_c);
       }
       if (l < 16) {
-        if (left && (l < 12 || last)) gst4(Y + size_t(y0 + l) * pitch + x0 - 4, ld4(&L.y[(l + 4) * 20]));
+        if (left && (l < 12 || last)) gst4(Y + size_t(y0 + l) * pitch + x0 - 4, w_side);
       } else if (row > 0) {
-        const int k = l - 16;
-        gst4(Y + size_t(y0 - 4 + (k >> 2)) * pitch + x0 + (k & 3) * 4,
-             ld4(&L.y[(k >> 2) * 20 + 4 + (k & 3) * 4]));
+        gst4(Y + size_t(y0 - 4 + (k16 >> 2)) * pitch + x0 + (k16 & 3) * 4, w_side);
       }
       if (l < 8) {
-        if (left && (l < 6 || last)) {
-          const u32 cw = u32(L.c[0][(l + 2) * 12 + 2]) | u32(L.c[1][(l + 2) * 12 + 2]) << 8 |
-                         u32(L.c[0][(l + 2) * 12 + 3]) << 16 | u32(L.c[1][(l + 2) * 12 + 3]) << 24;
-          gst4(UV + size_t(row * 8 + l) * pitch + x0 - 4, cw);
-        }
+        if (left && (l < 6 || last)) gst4(UV + size_t(row * 8 + l) * pitch + x0 - 4, w_cside);
       } else if (l < 16 && row > 0) {
-        const int k = l - 8, tr = k >> 2, cb = (k & 3) * 2;
-        u32 cw = 0;
-        for (int q = 0; q < 2; ++q)
-          cw |= (u32(L.c[0][tr * 12 + 4 + cb + q]) | u32(L.c[1][tr * 12 + 4 + cb + q]) << 8) << (16 * q);
-        gst4(UV + size_t(row * 8 - 2 + tr) * pitch + x0 + cb * 2, cw);
+        gst4(UV + size_t(row * 8 - 2 + (k8 >> 2)) * pitch + x0 + (k8 & 3) * 4, w_cside);
       }
       // ---- exchange for the row below: this MB's rows 12..15 / chroma rows 6..7 (the last
       // word of each 4-word row, columns 12..15 / 6..7, is completed by the next MB's vertical
       // edges above)
       if (prod && l < 24) {
-        u32 w;
-        if (l < 16) {
-          w = ld4(&L.y[(16 + (l >> 2)) * 20 + 4 + (l & 3) * 4]);
-        } else {
-          const int k = l - 16, cr = 8 + (k >> 2), cb = (k & 3) * 2;
-          w = u32(L.c[0][cr * 12 + 4 + cb]) | u32(L.c[1][cr * 12 + 4 + cb]) << 8 |
-              u32(L.c[0][cr * 12 + 5 + cb]) << 16 | u32(L.c[1][cr * 12 + 5 + cb]) << 24;
-        }
         if (xout)
-          xg_put(xg_out + size_t(x) * kAvcXgWords + l, w, (l & 3) == 3 && x + 1 < W ? kXgPartial : kXgFinal);
+          xg_put(xg_out + size_t(x) * kAvcXgWords + l, w_x, (l & 3) == 3 && x + 1 < W ? kXgPartial : kXgFinal);
         else
-          st4(l < 16 ? &xch(row, x).y[l * 4] : &xch(row, x).c[(l - 16) * 4], w);
+          st4(l < 16 ? &xch(row, x).y[l * 4] : &xch(row, x).c[(l - 16) * 4], w_x);
       }
       // ---- carry columns 12..15 (luma) / 6..7 (chroma) of this MB to the next one of the row
       if (l < 16) {
-        st4(&L.carry[l * 4], ld4(&L.y[(l + 4) * 20 + 16]));
+        st4(&L.carry[l * 4], w_carry);
       } else {
-        const int c = (l - 16) >> 3, k = (l - 16) & 7;
-        L.ccarry[c][k * 2] = L.c[c][(k + 2) * 12 + 10];
-        L.ccarry[c][k * 2 + 1] = L.c[c][(k + 2) * 12 + 11];
+        L.ccarry[cc][ck * 2] = cr0;
+        L.ccarry[cc][ck * 2 + 1] = cr1;
       }
     }
     if (x == W - 1) {  // the row's exchange is complete (no MB to its right)
