@@ -1252,12 +1252,15 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
     const int x0 = x * 16, y0 = row * 16;
     // ---- LDS: MB samples and left columns (carried)
     if (act) {
+      // (the carried columns read first, in range for every lane: one wait for all the reads)
+      const u32 carry = ld4(&L.carry[(l & 15) * 4]);
+      const int l7 = l & 7;
+      const u8 cc0 = L.ccarry[0][l7 * 2], cc1 = L.ccarry[1][l7 * 2], cc2 = L.ccarry[0][l7 * 2 + 1],
+               cc3 = L.ccarry[1][l7 * 2 + 1];
       if (l < 16) reinterpret_cast<u32*>(&L.info)[l] = cur.info;
       st4(&L.y[((l >> 2) + 4) * 20 + 4 + (l & 3) * 4], cur.m0);
       st4(&L.y[((l >> 2) + 12) * 20 + 4 + (l & 3) * 4], cur.m1);
-      if (l < 16) {
-        if (x > 0) st4(&L.y[(l + 4) * 20], ld4(&L.carry[l * 4]));
-      }
+      if (l < 16 && x > 0) st4(&L.y[(l + 4) * 20], carry);
       {
         const int cyr = l >> 2, cb = (l & 3) * 2;
         for (int q = 0; q < 2; ++q) {
@@ -1266,10 +1269,10 @@ __global__ __launch_bounds__(64 * kDbkWaves) void avc_deblock_kernel(const AvcDe
         }
       }
       if (l < 8 && x > 0) {
-        L.c[0][(l + 2) * 12 + 2] = L.ccarry[0][l * 2];
-        L.c[1][(l + 2) * 12 + 2] = L.ccarry[1][l * 2];
-        L.c[0][(l + 2) * 12 + 3] = L.ccarry[0][l * 2 + 1];
-        L.c[1][(l + 2) * 12 + 3] = L.ccarry[1][l * 2 + 1];
+        L.c[0][(l + 2) * 12 + 2] = cc0;
+        L.c[1][(l + 2) * 12 + 2] = cc1;
+        L.c[0][(l + 2) * 12 + 3] = cc2;
+        L.c[1][(l + 2) * 12 + 3] = cc3;
       }
     }
     wave_sync();
