@@ -14,13 +14,15 @@
 //   * the frame bus: a pump serving readers in other threads while producers publish, cameras
 //     come and go and the serve-buffer pool (mock serve: the GPU path's pool and chunked
 //     copies, memcpy for the DMA) is hit by direct readers and consumer snapshots at once;
-//   * the fan-out pool: several H.265 decoders parsing multi-slice pictures in parallel at once.
+//   * the fan-out pool: several H.265 decoders parsing multi-slice pictures in parallel at once;
+//   * the native gRPC endpoint under hostile HTTP/2 clients (csrc/tests/rpc_stress.cpp).
 // Reference: SURVEY.md §5 "Race detection / sanitizers" (the reference had none and real races:
 // read_image.py:48,71-74 vs rtsp_to_rtmp.py:147-151; grpc_api.go:181-184).
 #include <unistd.h>
 
 #include <atomic>
 #include <cstdio>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -493,8 +495,15 @@ static void slice_fanout_stress() {
   std::printf("parallel slices / tiles / wavefront rows: %llu pictures\n", (unsigned long long)pictures.load());
 }
 
-int main() {
+void rpc_hostile_stress();  // rpc_stress.cpp
+
+int main(int argc, char** argv) {
   std::setvbuf(stdout, nullptr, _IONBF, 0);  // progress is visible even if a run is cut short
+  if (argc > 1 && std::string(argv[1]) == "rpc") {  // the endpoint part alone
+    rpc_hostile_stress();
+    std::printf("native_stress ok\n");
+    return 0;
+  }
   live_worker_stress();
   rtsp_stress();
   general_decoder_stress();
@@ -502,6 +511,7 @@ int main() {
   compressed_ingest_stress();
   bus_stress();
   slice_fanout_stress();
+  rpc_hostile_stress();
   std::printf("native_stress ok\n");
   return 0;
 }

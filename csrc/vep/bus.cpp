@@ -522,7 +522,8 @@ bool Reader::touch(const std::string& name, int key_frame_only) {
   return true;
 }
 
-bool Reader::wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t, bool touch) {
+bool Reader::wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t, bool touch,
+                  const std::atomic<bool>* cancel) {
   Loc l;
   if (!locate(name, &l)) return false;
   Header* h = l.seg->hdr;
@@ -554,6 +555,7 @@ bool Reader::wait(const std::string& name, i64 after, int wait_ms, int key_frame
       if ((ok = ready())) break;
       const i64 left = deadline - mono_ms();
       if (left <= 0 || !pid_alive(l.seg->pid)) break;
+      if (cancel && cancel->load(std::memory_order_acquire)) break;
       futex_wait(&e.pub, p, int(std::min<i64>(left, 100)));
     }
     e.waiters.fetch_sub(1, std::memory_order_acq_rel);

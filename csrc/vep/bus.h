@@ -163,7 +163,9 @@ class Reader {
   // up to wait_ms for a bus frame with seq > after that is at least as new as the owner's ring
   // was at the call. False: unknown camera or timeout.
   // touch = false: read only (no demand marked; an internal reader, not a client request).
-  bool wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t, bool touch = true);
+  // cancel: when set (e.g. the client reset its stream), the wait ends within ~100 ms.
+  bool wait(const std::string& name, i64 after, int wait_ms, int key_frame_only, Ticket* t, bool touch = true,
+            const std::atomic<bool>* cancel = nullptr);
   // Copies the newest bus frame with seq > t.after into dst (cap >= t.cap): one seqlock-checked
   // memcpy. Returns its length and sequence, 0 if the camera went away meanwhile.
   size_t copy(const Ticket& t, u8* dst, size_t cap, i64* seq);

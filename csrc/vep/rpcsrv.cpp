@@ -3,6 +3,7 @@
 
 #include <arpa/inet.h>
 #include <fcntl.h>
+#include <netdb.h>
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/epoll.h>
@@ -253,12 +254,23 @@ void HpackDecoder::add(const std::string& name, const std::string& value) {
 bool HpackDecoder::decode(const u8* p, size_t n, std::vector<std::pair<std::string, std::string>>& out) {
   const u8* end = p + n;
   std::string name, value;
+  size_t list = 0;
+  over_ = false;
+  auto emit = [&]() {
+    list += name.size() + value.size() + 32;
+    if (list > max_list_) {
+      over_ = true;
+      return false;
+    }
+    out.emplace_back(name, value);
+    return true;
+  };
   while (p < end) {
     const u8 b = *p;
     u64 idx;
     if (b & 0x80) {  // indexed (§6.1)
       if (!read_int(p, end, 7, idx) || !entry(size_t(idx), name, value)) return false;
-      out.emplace_back(name, value);
+      if (!emit()) return false;
     } else if ((b & 0xC0) == 0x40) {  // literal with incremental indexing (§6.2.1)
       if (!read_int(p, end, 6, idx)) return false;
       if (idx) {
@@ -269,7 +281,7 @@ bool HpackDecoder::decode(const u8* p, size_t n, std::vector<std::pair<std::stri
       }
       if (!read_str(p, end, value)) return false;
       add(name, value);
-      out.emplace_back(name, value);
+      if (!emit()) return false;
     } else if ((b & 0xE0) == 0x20) {  // dynamic table size update (§6.3)
       if (!read_int(p, end, 5, idx) || idx > limit_) return false;
       max_ = size_t(idx);
@@ -283,7 +295,7 @@ bool HpackDecoder::decode(const u8* p, size_t n, std::vector<std::pair<std::stri
         return false;
       }
       if (!read_str(p, end, value)) return false;
-      out.emplace_back(name, value);
+      if (!emit()) return false;
     }
   }
   return true;
@@ -296,6 +308,11 @@ namespace {
 enum : u8 { kData = 0, kHeaders = 1, kPriority = 2, kRst = 3, kSettings = 4, kPush = 5, kPing = 6, kGoaway = 7,
             kWindowUpdate = 8, kContinuation = 9 };
 enum : u8 { kEndStream = 1, kAck = 1, kEndHeaders = 4, kPadded = 8, kPriorityFlag = 0x20 };
+// error codes (RFC 7540 7)
+enum : u32 { kNoError = 0, kProtocolError = 1, kFlowControlError = 3, kFrameSizeError = 6, kRefusedStream = 7,
+             kCancel = 8, kCompressionError = 9, kEnhanceYourCalm = 11 };
+constexpr u32 kMaxFrame = 16384;  // SETTINGS_MAX_FRAME_SIZE: never raised by this server
+constexpr size_t kMaxGrpcMessage = 1024;  // grpc-message bytes before percent-encoding
 constexpr char kPreface[] = "PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n";
 constexpr size_t kPrefaceLen = 24;
 constexpr i64 kRecvStreamWindow = 1 << 20;     // advertised per stream (requests are tiny)
@@ -381,8 +398,11 @@ struct Stream {
   std::deque<std::string> requests;  // complete request messages
   bool remote_closed = false, headers_sent = false, trailers_queued = false, trailers_sent = false;
   bool inflight = false;             // a frame / slow job runs for this stream
+  std::shared_ptr<std::atomic<bool>> cancel;  // set when the client resets the stream mid-job
   i64 t0_ms = 0;
   i64 send_win = 65535;
+  i64 recv_win = 0;                  // what the client may still send on this stream
+  size_t held = 0;                   // received DATA payload bytes not yet credited back
   std::deque<Chunk> pending;         // response messages (5-byte prefix included)
   int status = 0;
   std::string message;
@@ -405,6 +425,11 @@ struct Conn {
   std::map<u32, Stream> streams;
   std::deque<Chunk> out;
   size_t out_bytes = 0;
+  bool read_paused = false;      // input paused while the client does not read its output
+  i64 recv_win = 0;              // connection receive window left to the client
+  u64 credit = 0;                // consumed bytes not yet returned by a connection WINDOW_UPDATE
+  i64 rst_window_ms = 0;         // rapid-reset accounting: resets of unanswered streams per second
+  u32 rst_count = 0;
 };
 
 }  // namespace
@@ -425,6 +450,7 @@ struct Server::Impl {
     std::vector<std::function<void()>> tasks;
     std::unordered_map<int, std::shared_ptr<Conn>> conns;  // by fd (loop thread only)
     std::unordered_map<u64, int> fd_of;                    // conn id -> fd (loop thread only)
+    i64 last_sweep_ms = 0;
   };
   std::vector<std::unique_ptr<Loop>> loops;
   std::atomic<u32> rr{0};
@@ -456,7 +482,7 @@ struct Server::Impl {
 
   // stats
   std::atomic<u64> n_conn{0}, n_open{0}, n_streams{0}, n_frames{0}, n_empty{0}, n_bytes{0}, n_slow{0}, n_copies{0},
-      n_proto{0};
+      n_proto{0}, n_goaway{0}, n_refused{0}, n_cancelled{0}, n_deadline{0};
   mutable std::mutex lat_mu;
   std::vector<float> lat;
   size_t lat_next = 0;
@@ -512,22 +538,43 @@ struct Server::Impl {
 
   static constexpr u64 kWakeTag = ~0ull, kListenTag = ~1ull;
 
-  void start() {
-    listen_fd = ::socket(AF_INET, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
-    VEP_CHECK(listen_fd >= 0, "rpc: socket() failed");
-    int on = 1;
-    ::setsockopt(listen_fd, SOL_SOCKET, SO_REUSEADDR, &on, sizeof on);
-    if (opt.reuseport) ::setsockopt(listen_fd, SOL_SOCKET, SO_REUSEPORT, &on, sizeof on);
-    sockaddr_in a{};
-    a.sin_family = AF_INET;
-    a.sin_port = htons(u16(opt.port));
-    VEP_CHECK(::inet_pton(AF_INET, opt.host.c_str(), &a.sin_addr) == 1, "rpc: bad listen host " + opt.host);
-    VEP_CHECK(::bind(listen_fd, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0,
-              "rpc: bind to " + opt.host + ":" + std::to_string(opt.port) + " failed: " + std::strerror(errno));
-    VEP_CHECK(::listen(listen_fd, 1024) == 0, "rpc: listen failed");
+  // The listen address: an IPv4 / IPv6 literal or a host name ("localhost", "::", "" = any),
+  // resolved with getaddrinfo like grpc's ":port" / "[::]:port" listeners.
+  void listen_on() {
+    addrinfo hints{};
+    hints.ai_family = AF_UNSPEC;
+    hints.ai_socktype = SOCK_STREAM;
+    hints.ai_flags = AI_PASSIVE | AI_NUMERICSERV;
+    addrinfo* res = nullptr;
+    const std::string svc = std::to_string(opt.port);
+    const int rc = ::getaddrinfo(opt.host.empty() ? nullptr : opt.host.c_str(), svc.c_str(), &hints, &res);
+    VEP_CHECK(rc == 0 && res, "rpc: cannot resolve listen host '" + opt.host + "': " + ::gai_strerror(rc));
+    std::string err;
+    for (addrinfo* ai = res; ai; ai = ai->ai_next) {
+      const int fd = ::socket(ai->ai_family, SOCK_STREAM | SOCK_NONBLOCK | SOCK_CLOEXEC, 0);
+      if (fd < 0) continue;
+      int on = 1, off = 0;
+      ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &on, sizeof on);
+      if (opt.reuseport) ::setsockopt(fd, SOL_SOCKET, SO_REUSEPORT, &on, sizeof on);
+      if (ai->ai_family == AF_INET6) ::setsockopt(fd, IPPROTO_IPV6, IPV6_V6ONLY, &off, sizeof off);  // dual stack
+      if (::bind(fd, ai->ai_addr, ai->ai_addrlen) == 0 && ::listen(fd, 1024) == 0) {
+        listen_fd = fd;
+        break;
+      }
+      err = std::strerror(errno);
+      ::close(fd);
+    }
+    ::freeaddrinfo(res);
+    VEP_CHECK(listen_fd >= 0, "rpc: bind to " + opt.host + ":" + std::to_string(opt.port) + " failed: " + err);
+    sockaddr_storage a{};
     socklen_t sl = sizeof a;
     ::getsockname(listen_fd, reinterpret_cast<sockaddr*>(&a), &sl);
-    port = ntohs(a.sin_port);
+    port = a.ss_family == AF_INET6 ? ntohs(reinterpret_cast<sockaddr_in6*>(&a)->sin6_port)
+                                   : ntohs(reinterpret_cast<sockaddr_in*>(&a)->sin_port);
+  }
+
+  void start() {
+    listen_on();
     pool_start(waiters, opt.wait_threads, "vep-rpc-wait");
     pool_start(slows, opt.slow_threads, "vep-rpc-slow");
     for (int i = 0; i < std::max(1, opt.io_threads); ++i) {
@@ -600,12 +647,35 @@ struct Server::Impl {
         t.swap(L.tasks);
       }
       for (auto& f : t) f();
+      const i64 now = now_ms_mono();
+      if (now - L.last_sweep_ms >= 500) {
+        L.last_sweep_ms = now;
+        sweep(L);
+      }
     }
+  }
+
+  // grpc's peer strings: "ipv4:1.2.3.4:port", "ipv6:[::1]:port" (a v4-mapped v6 peer as ipv4)
+  static std::string peer_name(const sockaddr_storage& a) {
+    char ip[INET6_ADDRSTRLEN] = {0};
+    if (a.ss_family == AF_INET6) {
+      const auto* v6 = reinterpret_cast<const sockaddr_in6*>(&a);
+      const int p = ntohs(v6->sin6_port);
+      if (IN6_IS_ADDR_V4MAPPED(&v6->sin6_addr)) {
+        ::inet_ntop(AF_INET, &v6->sin6_addr.s6_addr[12], ip, sizeof ip);
+        return std::string("ipv4:") + ip + ":" + std::to_string(p);
+      }
+      ::inet_ntop(AF_INET6, &v6->sin6_addr, ip, sizeof ip);
+      return std::string("ipv6:[") + ip + "]:" + std::to_string(p);
+    }
+    const auto* v4 = reinterpret_cast<const sockaddr_in*>(&a);
+    ::inet_ntop(AF_INET, &v4->sin_addr, ip, sizeof ip);
+    return std::string("ipv4:") + ip + ":" + std::to_string(ntohs(v4->sin_port));
   }
 
   void accept_all() {
     for (;;) {
-      sockaddr_in a{};
+      sockaddr_storage a{};
       socklen_t sl = sizeof a;
       const int fd = ::accept4(listen_fd, reinterpret_cast<sockaddr*>(&a), &sl, SOCK_NONBLOCK | SOCK_CLOEXEC);
       if (fd < 0) return;
@@ -613,12 +683,11 @@ struct Server::Impl {
       ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &on, sizeof on);
       int sndbuf = 8 << 20;
       ::setsockopt(fd, SOL_SOCKET, SO_SNDBUF, &sndbuf, sizeof sndbuf);
-      char ip[64] = {0};
-      ::inet_ntop(AF_INET, &a.sin_addr, ip, sizeof ip);
       auto c = std::make_shared<Conn>();
       c->fd = fd;
       c->id = next_conn.fetch_add(1);
-      c->peer = std::string("ipv4:") + ip + ":" + std::to_string(ntohs(a.sin_port));
+      c->peer = peer_name(a);
+      c->hp.set_max_list(opt.max_header_list);
       n_conn.fetch_add(1);
       n_open.fetch_add(1);
       Loop& L = *loops[rr.fetch_add(1) % loops.size()];
@@ -633,18 +702,19 @@ struct Server::Impl {
     ev.events = EPOLLIN | EPOLLRDHUP;
     ev.data.u64 = u64(c->fd);
     ::epoll_ctl(L.ep, EPOLL_CTL_ADD, c->fd, &ev);
-    // server preface: SETTINGS (max concurrent streams, per-stream receive window), then a
-    // connection window update
+    // server preface: SETTINGS (max concurrent streams, per-stream receive window, max header
+    // list size), then a connection window update
     std::string s;
-    frame_hdr(s, 12, kSettings, 0, 0);
-    const u16 ids[2] = {3, 4};
-    const u32 vals[2] = {1000u, u32(kRecvStreamWindow)};
-    for (int k = 0; k < 2; ++k) {
+    frame_hdr(s, 18, kSettings, 0, 0);
+    const u16 ids[3] = {3, 4, 6};
+    const u32 vals[3] = {opt.max_streams, u32(kRecvStreamWindow), opt.max_header_list};
+    for (int k = 0; k < 3; ++k) {
       const char e[6] = {char(ids[k] >> 8), char(ids[k]), char(vals[k] >> 24), char(vals[k] >> 16),
                          char(vals[k] >> 8), char(vals[k])};
       s.append(e, 6);
     }
     window_update(s, 0, u32(kRecvConnBoost));
+    c->recv_win = 65535 + kRecvConnBoost;
     queue(*c, std::move(s));
     on_readable(L, *c);  // (bytes may already be waiting)
   }
@@ -709,14 +779,41 @@ struct Server::Impl {
     }
     if (c.fd < 0) return;
     const bool want = !c.out.empty();
-    if (want != c.epollout) {
-      epoll_event ev{};
-      ev.events = EPOLLIN | EPOLLRDHUP | (want ? EPOLLOUT : 0u);
-      ev.data.u64 = u64(c.fd);
-      ::epoll_ctl(L.ep, EPOLL_CTL_MOD, c.fd, &ev);
+    bool resume = false;
+    if (c.read_paused && c.out_bytes <= opt.out_high_water / 2) {
+      c.read_paused = false;
+      resume = true;
+    }
+    if (want != c.epollout || resume) {
+      set_events(L, c, want);
       c.epollout = want;
     }
     if (c.closing && c.out.empty() && c.streams.empty()) close_conn(L, c);
+    if (resume && c.fd >= 0) on_readable(L, c);  // (level-triggered: bytes may be waiting)
+  }
+
+  void set_events(Loop& L, Conn& c, bool out) {
+    epoll_event ev{};
+    ev.events = (c.read_paused ? 0u : u32(EPOLLIN | EPOLLRDHUP)) | (out ? u32(EPOLLOUT) : 0u);
+    ev.data.u64 = u64(c.fd);
+    ::epoll_ctl(L.ep, EPOLL_CTL_MOD, c.fd, &ev);
+  }
+
+  // A header block as HEADERS + CONTINUATION frames no larger than the peer's max frame size.
+  void queue_block(Conn& c, const std::string& blk, u32 sid, bool end_stream) {
+    const size_t mf = std::max<size_t>(c.peer_max_frame, 16384);
+    std::string f;
+    size_t off = 0;
+    do {
+      const size_t n = std::min(mf, blk.size() - off);
+      const bool last = off + n == blk.size();
+      const u8 type = off == 0 ? kHeaders : kContinuation;
+      const u8 flags = u8((last ? kEndHeaders : 0) | (off == 0 && end_stream ? kEndStream : 0));
+      frame_hdr(f, u32(n), type, flags, sid);
+      f.append(blk, off, n);
+      off += n;
+    } while (off < blk.size());
+    queue(c, std::move(f));
   }
 
   void send_headers(Conn& c, Stream& s) {
@@ -740,10 +837,8 @@ struct Server::Impl {
       blk += "application/grpc";
     }
     put_literal(blk, "grpc-status", std::to_string(s.status));
-    if (!s.message.empty()) put_literal(blk, "grpc-message", pct_encode(s.message));
-    std::string f;
-    frame_hdr(f, u32(blk.size()), kHeaders, kEndHeaders | kEndStream, s.id);
-    queue(c, f + blk);
+    if (!s.message.empty()) put_literal(blk, "grpc-message", pct_encode(s.message.substr(0, kMaxGrpcMessage)));
+    queue_block(c, blk, s.id, true);
     s.trailers_sent = true;
   }
 
@@ -775,7 +870,7 @@ struct Server::Impl {
           progress = true;
         }
         if (s.trailers_sent) {
-          it = c.streams.erase(it);
+          it = erase_stream(c, it);
           continue;
         }
         ++it;
@@ -805,6 +900,7 @@ struct Server::Impl {
   }
 
   void goaway(Conn& c, u32 code) {
+    if (code != kNoError) n_goaway.fetch_add(1);
     std::string f;
     frame_hdr(f, 8, kGoaway, 0, 0);
     const u32 ls = c.last_sid;
@@ -816,12 +912,56 @@ struct Server::Impl {
   }
 
   // ------------------------------------------------------------------ input
+  // Received DATA bytes of a stream consumed (a request taken, failed or dropped): the client may
+  // send that much again. Connection credit goes back in batches; stream credit only to open
+  // streams that can still send.
+  void release(Conn& c, Stream* s, size_t n) {
+    if (n == 0) return;
+    if (s) {
+      n = std::min(n, s->held);
+      s->held -= n;
+      if (!s->remote_closed && !s->trailers_queued) {
+        std::string w;
+        window_update(w, s->id, u32(n));
+        s->recv_win += i64(n);
+        queue(c, std::move(w));
+      }
+    }
+    c.credit += n;
+    if (c.credit >= 16384) {
+      std::string w;
+      window_update(w, 0, u32(c.credit));
+      c.recv_win += i64(c.credit);
+      c.credit = 0;
+      queue(c, std::move(w));
+    }
+  }
+
+  std::map<u32, Stream>::iterator erase_stream(Conn& c, std::map<u32, Stream>::iterator it) {
+    Stream& s = it->second;
+    if (s.cancel) s.cancel->store(true, std::memory_order_release);
+    const size_t h = s.held;
+    s.held = 0;
+    c.credit += h;
+    return c.streams.erase(it);
+  }
+
   void on_readable(Loop& L, Conn& c) {
+    if (c.out_bytes > opt.out_high_water) {  // the client does not read what it asks for: pause its input
+      if (!c.read_paused) {
+        c.read_paused = true;
+        set_events(L, c, true);
+        c.epollout = true;
+      }
+      return;
+    }
     char buf[1 << 16];
-    for (;;) {
+    size_t got = 0;
+    while (got < opt.read_budget) {  // (level-triggered: what is left comes with the next event)
       const ssize_t r = ::read(c.fd, buf, sizeof buf);
       if (r > 0) {
         c.in.append(buf, size_t(r));
+        got += size_t(r);
         if (size_t(r) < sizeof buf) break;
         continue;
       }
@@ -834,11 +974,13 @@ struct Server::Impl {
       close_conn(L, c);
       return;
     }
-    if (!parse(L, c)) {
+    const u32 err = parse(L, c);
+    if (err != kNoError) {
       n_proto.fetch_add(1);
-      goaway(c, 1);  // PROTOCOL_ERROR
+      goaway(c, err);
       c.in.clear();
       c.in_off = 0;
+      for (auto it = c.streams.begin(); it != c.streams.end();) it = erase_stream(c, it);
       flush(L, c);
       if (c.fd >= 0) close_conn(L, c);
       return;
@@ -846,10 +988,11 @@ struct Server::Impl {
     pump(L, c);
   }
 
-  bool parse(Loop& L, Conn& c) {
+  u32 parse(Loop& L, Conn& c) {
     if (!c.preface) {
-      if (c.in.size() < kPrefaceLen) return std::string(kPreface).compare(0, c.in.size(), c.in) == 0;
-      if (c.in.compare(0, kPrefaceLen, kPreface) != 0) return false;
+      if (c.in.size() < kPrefaceLen)
+        return std::string(kPreface).compare(0, c.in.size(), c.in) == 0 ? kNoError : kProtocolError;
+      if (c.in.compare(0, kPrefaceLen, kPreface) != 0) return kProtocolError;
       c.preface = true;
       c.in_off = kPrefaceLen;
     }
@@ -858,145 +1001,201 @@ struct Server::Impl {
       if (avail < 9) break;
       const u8* h = reinterpret_cast<const u8*>(c.in.data() + c.in_off);
       const u32 len = u32(h[0]) << 16 | u32(h[1]) << 8 | u32(h[2]);
-      if (len > (1u << 24)) return false;
+      if (len > kMaxFrame) return kFrameSizeError;  // (checked before buffering the payload)
       if (avail < 9 + size_t(len)) break;
       const u8 type = h[3], flags = h[4];
       const u32 sid = be32(h + 5) & 0x7FFFFFFFu;
-      if (!frame(L, c, type, flags, sid, h + 9, len)) return false;
+      const u32 err = frame(L, c, type, flags, sid, h + 9, len);
+      if (err != kNoError) return err;
       c.in_off += 9 + len;
-      if (c.fd < 0) return true;
+      if (c.fd < 0) return kNoError;
     }
     if (c.in_off > 0 && c.in_off == c.in.size()) {
       c.in.clear();
       c.in_off = 0;
-    } else if (c.in_off > (1u << 20)) {
-      c.in.erase(0, c.in_off);
+    } else if (c.in_off > 0) {
+      c.in.erase(0, c.in_off);  // (at most one partial frame is left: <= 9 + 16384 bytes)
       c.in_off = 0;
     }
-    return true;
+    return kNoError;
   }
 
-  bool frame(Loop& L, Conn& c, u8 type, u8 flags, u32 sid, const u8* p, u32 len) {
-    if (c.hdr_sid && type != kContinuation) return false;  // a header block must be contiguous
+  // One inbound frame; a non-zero result is a connection error (GOAWAY with that code).
+  u32 frame(Loop& L, Conn& c, u8 type, u8 flags, u32 sid, const u8* p, u32 len) {
+    if (c.hdr_sid && type != kContinuation) return kProtocolError;  // a header block must be contiguous
     switch (type) {
       case kSettings: {
-        if (sid != 0 || (len % 6) != 0) return false;
-        if (flags & kAck) return true;
+        if (sid != 0) return kProtocolError;
+        if (len % 6) return kFrameSizeError;
+        if (flags & kAck) return len ? kFrameSizeError : kNoError;
         for (u32 k = 0; k < len; k += 6) {
           const u16 id = u16(p[k] << 8 | p[k + 1]);
           const u32 v = be32(p + k + 2);
+          if (id == 2 && v > 1) return kProtocolError;  // ENABLE_PUSH
           if (id == 4) {  // INITIAL_WINDOW_SIZE: the delta applies to every open stream
-            if (v > 0x7FFFFFFFu) return false;
+            if (v > 0x7FFFFFFFu) return kFlowControlError;
             const i64 d = i64(v) - c.peer_init_win;
             c.peer_init_win = i64(v);
             for (auto& [i, s] : c.streams) s.send_win += d;
           } else if (id == 5) {
-            if (v < 16384 || v > 16777215) return false;
+            if (v < 16384 || v > 16777215) return kProtocolError;
             c.peer_max_frame = v;
           }
         }
         std::string a;
         frame_hdr(a, 0, kSettings, kAck, 0);
         queue(c, std::move(a));
-        return true;
+        return kNoError;
       }
       case kPing: {
-        if (len != 8 || sid != 0) return false;
-        if (flags & kAck) return true;
+        if (sid != 0) return kProtocolError;
+        if (len != 8) return kFrameSizeError;
+        if (flags & kAck) return kNoError;
         std::string a;
         frame_hdr(a, 8, kPing, kAck, 0);
         a.append(reinterpret_cast<const char*>(p), 8);
         queue(c, std::move(a));
-        return true;
+        return kNoError;
       }
       case kWindowUpdate: {
-        if (len != 4) return false;
+        if (len != 4) return kFrameSizeError;
         const u32 inc = be32(p) & 0x7FFFFFFFu;
         if (sid == 0) {
+          if (inc == 0) return kProtocolError;
           c.conn_send_win += inc;
+          if (c.conn_send_win > 0x7FFFFFFF) return kFlowControlError;
         } else {
           auto it = c.streams.find(sid);
-          if (it != c.streams.end()) it->second.send_win += inc;
+          if (it != c.streams.end()) {
+            if (inc == 0 || it->second.send_win + i64(inc) > 0x7FFFFFFF) {
+              rst(c, sid, inc == 0 ? kProtocolError : kFlowControlError);
+              erase_stream(c, it);
+            } else {
+              it->second.send_win += inc;
+            }
+          }
         }
-        return true;
+        return kNoError;
       }
       case kGoaway:
+        if (sid != 0) return kProtocolError;
         c.closing = true;
-        return true;
+        return kNoError;
       case kRst: {
+        if (sid == 0) return kProtocolError;
+        if (len != 4) return kFrameSizeError;
         auto it = c.streams.find(sid);
-        if (it != c.streams.end()) c.streams.erase(it);  // (a job in flight finds no stream)
-        return true;
+        if (it == c.streams.end()) return kNoError;
+        // a reset of a stream that had not been answered: its waiter is released (cancel flag)
+        // and the reset counts against the connection (rapid-reset defence)
+        if (!it->second.trailers_queued) {
+          if (it->second.inflight) n_cancelled.fetch_add(1);
+          const i64 now = now_ms_mono();
+          if (now - c.rst_window_ms >= 1000) {
+            c.rst_window_ms = now;
+            c.rst_count = 0;
+          }
+          if (++c.rst_count > opt.max_resets_per_s) {
+            erase_stream(c, it);
+            return kEnhanceYourCalm;
+          }
+        }
+        erase_stream(c, it);  // (a job in flight finds no stream)
+        return kNoError;
       }
+      case kPriority:
+        if (sid == 0) return kProtocolError;
+        return len == 5 ? kNoError : kFrameSizeError;
       case kHeaders: {
-        if (sid == 0 || (sid & 1) == 0) return false;
+        if (sid == 0 || (sid & 1) == 0) return kProtocolError;
         size_t off = 0, pad = 0;
         if (flags & kPadded) {
-          if (len < 1) return false;
+          if (len < 1) return kFrameSizeError;
           pad = p[0];
           off = 1;
         }
         if (flags & kPriorityFlag) off += 5;
-        if (off + pad > len) return false;
+        if (off + pad > len) return kProtocolError;
         c.hdr_block.assign(reinterpret_cast<const char*>(p + off), len - off - pad);
         c.hdr_sid = sid;
         c.hdr_end_stream = (flags & kEndStream) != 0;
         if (flags & kEndHeaders) return headers_done(L, c);
-        return true;
+        return kNoError;
       }
       case kContinuation: {
-        if (!c.hdr_sid || sid != c.hdr_sid) return false;
+        if (!c.hdr_sid || sid != c.hdr_sid) return kProtocolError;
+        if (c.hdr_block.size() + len > opt.max_header_block) return kEnhanceYourCalm;  // CONTINUATION flood
         c.hdr_block.append(reinterpret_cast<const char*>(p), len);
         if (flags & kEndHeaders) return headers_done(L, c);
-        return true;
+        return kNoError;
       }
       case kData: {
-        if (sid == 0) return false;
+        if (sid == 0) return kProtocolError;
         size_t off = 0, pad = 0;
         if (flags & kPadded) {
-          if (len < 1) return false;
+          if (len < 1) return kFrameSizeError;
           pad = p[0];
           off = 1;
         }
-        if (off + pad > len) return false;
-        if (len > 0) {  // flow control: give the bytes back at once (requests are consumed here)
-          std::string w;
-          window_update(w, 0, len);
-          if (!(flags & kEndStream) && c.streams.count(sid)) window_update(w, sid, len);
-          queue(c, std::move(w));
-        }
+        if (off + pad > len) return kProtocolError;
+        // flow control (RFC 7540 6.9): what the client sends counts against the windows this
+        // server advertised; the payload is credited back only as its requests are consumed, so
+        // a client cannot make the server buffer more than those windows
+        c.recv_win -= i64(len);
+        if (c.recv_win < 0) return kFlowControlError;
         auto it = c.streams.find(sid);
-        if (it == c.streams.end()) return true;  // (reset / finished stream)
+        const size_t payload = len - off - pad;
+        if (it == c.streams.end() || it->second.remote_closed || it->second.trailers_queued) {
+          release(c, nullptr, len);  // (reset / finished / half-closed stream: dropped)
+          return kNoError;
+        }
         Stream& s = it->second;
-        s.rbuf.append(reinterpret_cast<const char*>(p + off), len - off - pad);
-        if (!messages(c, s)) return true;
+        s.recv_win -= i64(len);
+        if (s.recv_win < 0) {
+          rst(c, sid, kFlowControlError);
+          erase_stream(c, it);
+          release(c, nullptr, len);
+          return kNoError;
+        }
+        if (len > payload) release(c, nullptr, len - payload);  // padding
+        s.held += payload;
+        s.rbuf.append(reinterpret_cast<const char*>(p + off), payload);
+        if (!messages(c, s)) return kNoError;
         if (flags & kEndStream) s.remote_closed = true;
         advance(L, c, s);
-        return true;
+        return kNoError;
       }
       default:
-        return true;  // PRIORITY, PUSH_PROMISE (never from a client), unknown types: ignored
+        return kNoError;  // PUSH_PROMISE (never from a client), unknown types: ignored
     }
   }
 
-  bool headers_done(Loop& L, Conn& c) {
+  u32 headers_done(Loop& L, Conn& c) {
     const u32 sid = c.hdr_sid;
     c.hdr_sid = 0;
     std::vector<std::pair<std::string, std::string>> hs;
-    if (!c.hp.decode(reinterpret_cast<const u8*>(c.hdr_block.data()), c.hdr_block.size(), hs)) return false;
+    const bool ok = c.hp.decode(reinterpret_cast<const u8*>(c.hdr_block.data()), c.hdr_block.size(), hs);
     c.hdr_block.clear();
+    c.hdr_block.shrink_to_fit();
+    if (!ok) return c.hp.list_too_large() ? kEnhanceYourCalm : kCompressionError;
     auto it = c.streams.find(sid);
     if (it != c.streams.end()) {  // trailers from the client: end of its messages
       if (c.hdr_end_stream) it->second.remote_closed = true;
       advance(L, c, it->second);
-      return true;
+      return kNoError;
     }
-    if (sid <= c.last_sid) return true;  // (a stream already closed)
+    if (sid <= c.last_sid) return kNoError;  // (a stream already closed)
     c.last_sid = sid;
+    if (c.streams.size() >= opt.max_streams) {  // over SETTINGS_MAX_CONCURRENT_STREAMS
+      n_refused.fetch_add(1);
+      rst(c, sid, kRefusedStream);
+      return kNoError;
+    }
     Stream& s = c.streams[sid];
     s.id = sid;
     s.t0_ms = now_ms_mono();
     s.send_win = c.peer_init_win;
+    s.recv_win = kRecvStreamWindow;
     n_streams.fetch_add(1);
     std::string path, ctype;
     for (auto& [k, v] : hs) {
@@ -1009,12 +1208,20 @@ struct Server::Impl {
     else if (s.method == "ListStreams" || s.method == "Annotate" || s.method == "Proxy" || s.method == "Storage")
       s.kind = Kind::kSlow;
     if (s.kind == Kind::kUnknown || ctype.compare(0, 16, "application/grpc") != 0) {
-      finish(c, s, 12, "unknown method " + path);  // UNIMPLEMENTED
-      return true;
+      finish(c, s, 12, "unknown method " + path.substr(0, 256));  // UNIMPLEMENTED
+      return kNoError;
     }
     if (c.hdr_end_stream) s.remote_closed = true;
     advance(L, c, s);
-    return true;
+    return kNoError;
+  }
+
+  // fail a stream's request side: its buffered requests are dropped (and credited back)
+  void fail(Conn& c, Stream& s, int status, const std::string& msg) {
+    finish(c, s, status, msg);
+    s.rbuf.clear();
+    s.requests.clear();
+    release(c, &s, s.held);
   }
 
   // complete gRPC messages of the request bytes; false if the stream was failed
@@ -1024,16 +1231,18 @@ struct Server::Impl {
       const u8* b = reinterpret_cast<const u8*>(s.rbuf.data());
       const u32 n = be32(b + 1);
       if (b[0] != 0) {  // compressed: no grpc-encoding is negotiated
-        finish(c, s, 12, "compressed requests are not supported");
-        s.rbuf.clear();
+        fail(c, s, 12, "compressed requests are not supported");
         return false;
       }
       if (n > (4u << 20)) {
-        finish(c, s, 8, "request too large");  // RESOURCE_EXHAUSTED
-        s.rbuf.clear();
+        fail(c, s, 8, "request too large");  // RESOURCE_EXHAUSTED
         return false;
       }
       if (s.rbuf.size() < 5 + size_t(n)) return true;
+      if (s.requests.size() >= opt.max_queued_requests) {  // requests faster than they are answered
+        fail(c, s, 8, "too many queued requests");
+        return false;
+      }
       s.requests.push_back(s.rbuf.substr(5, n));
       s.rbuf.erase(0, 5 + size_t(n));
     }
@@ -1047,6 +1256,7 @@ struct Server::Impl {
       if (!s.remote_closed) return;
       std::string req = s.requests.empty() ? std::string() : s.requests.front();
       s.requests.clear();
+      release(c, &s, s.held);
       s.inflight = true;
       n_slow.fetch_add(1);
       const u64 cid = c.id;
@@ -1088,26 +1298,31 @@ struct Server::Impl {
       return;
     }
     if (now_ms_mono() - s.t0_ms > opt.stream_deadline_ms) {
-      s.requests.clear();
-      finish(c, s, 4, "stream deadline exceeded");  // DEADLINE_EXCEEDED
+      n_deadline.fetch_add(1);
+      fail(c, s, 4, "stream deadline exceeded");  // DEADLINE_EXCEEDED
       return;
     }
     std::string dev;
     bool kfo = false;
     const std::string req = std::move(s.requests.front());
     s.requests.pop_front();
+    release(c, &s, req.size() + 5);
     if (!parse_frame_request(req, dev, kfo)) {
-      s.requests.clear();
-      finish(c, s, 13, "bad VideoFrameRequest");
+      fail(c, s, 13, "bad VideoFrameRequest");
       return;
     }
     s.inflight = true;
+    if (!s.cancel) s.cancel = std::make_shared<std::atomic<bool>>(false);
     const u64 cid = c.id;
     const u32 sid = s.id;
     const std::string key = c.peer + '\n' + dev;
     const i64 t0 = now_ms_mono();
-    pool_post(waiters, [this, &L, cid, sid, dev, kfo, key, t0] {
-      Buf msg = frame_for(dev, kfo, key);
+    const i64 deadline = s.t0_ms + opt.stream_deadline_ms;
+    std::shared_ptr<std::atomic<bool>> cancel = s.cancel;
+    pool_post(waiters, [this, &L, cid, sid, dev, kfo, key, t0, deadline, cancel] {
+      if (cancel->load(std::memory_order_acquire)) return;  // reset while queued: nothing to answer
+      Buf msg = frame_for(dev, kfo, key, deadline, cancel.get());
+      if (cancel->load(std::memory_order_acquire)) return;
       record_latency(float(now_ms_mono() - t0));
       post(L, [this, &L, cid, sid, msg] {
         Conn* cc = find(L, cid);
@@ -1121,6 +1336,27 @@ struct Server::Impl {
         pump(L, *cc);
       });
     });
+  }
+
+  // Streams past their deadline with no job running end with DEADLINE_EXCEEDED (the reference's
+  // 15 s context on the whole stream, grpc_api.go:135-137), whether or not requests arrive.
+  void sweep(Loop& L) {
+    const i64 now = now_ms_mono();
+    std::vector<std::shared_ptr<Conn>> cs;
+    cs.reserve(L.conns.size());
+    for (auto& [fd, cp] : L.conns) cs.push_back(cp);
+    for (auto& cp : cs) {
+      Conn& c = *cp;
+      if (c.fd < 0) continue;
+      bool any = false;
+      for (auto& [sid, s] : c.streams)
+        if (!s.inflight && !s.trailers_queued && now - s.t0_ms > opt.stream_deadline_ms) {
+          n_deadline.fetch_add(1);
+          fail(c, s, 4, "stream deadline exceeded");
+          any = true;
+        }
+      if (any) pump(L, c);
+    }
   }
 
   // ------------------------------------------------------------------ frames
@@ -1148,11 +1384,15 @@ struct Server::Impl {
   // The newest bus frame of `dev` with seq > the caller's cursor (waiting up to 3 x 1 s), as one
   // gRPC message (5-byte prefix + serialized VideoFrame) shared by every client of the camera;
   // the empty message when none arrives.
-  Buf frame_for(const std::string& dev, bool kfo, const std::string& key) {
+  // Ends early (the empty message) when `cancel` is set: the client reset the stream.
+  Buf frame_for(const std::string& dev, bool kfo, const std::string& key, i64 deadline_ms,
+                const std::atomic<bool>* cancel) {
     const i64 after = cursor(key);
     for (int attempt = 0; attempt < opt.wait_attempts && !stop_.load(); ++attempt) {
+      if (cancel->load(std::memory_order_acquire) || now_ms_mono() >= deadline_ms) break;
       bus::Reader::Ticket t;
-      if (reader.wait(dev, after, opt.wait_block_ms, kfo ? 1 : 0, &t, true)) {
+      const int block = int(std::max<i64>(0, std::min<i64>(opt.wait_block_ms, deadline_ms - now_ms_mono())));
+      if (reader.wait(dev, after, block, kfo ? 1 : 0, &t, true, cancel)) {
         const i64 ns = reader.newest_seq(t);
         {
           std::unique_lock<std::mutex> g(cache_mu);
@@ -1243,6 +1483,10 @@ ServerStats Server::stats() const {
   s.slow_calls = p_->n_slow.load();
   s.frame_copies = p_->n_copies.load();
   s.protocol_errors = p_->n_proto.load();
+  s.goaways = p_->n_goaway.load();
+  s.refused_streams = p_->n_refused.load();
+  s.cancelled_waits = p_->n_cancelled.load();
+  s.deadline_streams = p_->n_deadline.load();
   std::vector<float> v;
   {
     std::lock_guard<std::mutex> g(p_->lat_mu);

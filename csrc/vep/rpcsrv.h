@@ -50,11 +50,28 @@ struct ServerOptions {
   int wait_attempts = 3;           // grpc_api.go:187 (XREAD BLOCK 1 s, 3 attempts)
   int wait_block_ms = 1000;
   size_t max_cursors = 65536;
+  // Protocol limits (what grpc-go's server bounds for the reference, server/main.go:142-153).
+  // Violations end the connection with GOAWAY (or refuse / fail the one stream) before any
+  // unbounded buffering happens.
+  u32 max_streams = 1000;            // SETTINGS_MAX_CONCURRENT_STREAMS; more: RST_STREAM REFUSED_STREAM
+  u32 max_header_list = 16384;       // SETTINGS_MAX_HEADER_LIST_SIZE (decoded, RFC 7540 6.5.2 accounting)
+  u32 max_header_block = 65536;      // encoded header block incl. CONTINUATION; more: ENHANCE_YOUR_CALM
+  u32 max_queued_requests = 16;      // per stream, not yet answered; more: RESOURCE_EXHAUSTED on the stream
+  size_t max_request_bytes = 8u << 20;   // buffered request bytes per connection; more: ENHANCE_YOUR_CALM
+  u32 max_resets_per_s = 200;        // client resets of unanswered streams (rapid-reset defence)
+  size_t read_budget = 256u << 10;   // bytes read from one connection per readiness event
+  size_t out_high_water = 64u << 20; // queued output above which the connection's input is paused
+  // HTTP/2 inbound frame payloads above 16384 bytes (the SETTINGS_MAX_FRAME_SIZE this server
+  // never raises) are FRAME_SIZE_ERROR.
 };
 
 struct ServerStats {
   u64 connections = 0, connections_open = 0, streams = 0, frames_served = 0, empty_frames = 0;
   u64 bytes_sent = 0, slow_calls = 0, frame_copies = 0, protocol_errors = 0;
+  u64 goaways = 0;           // connections ended by the server for a protocol or limit violation
+  u64 refused_streams = 0;   // RST_STREAM REFUSED_STREAM (over max_streams)
+  u64 cancelled_waits = 0;   // frame waits ended early because the client reset the stream
+  u64 deadline_streams = 0;  // streams ended with DEADLINE_EXCEEDED
   double p50_ms = 0, p99_ms = 0;  // request received -> response queued (recent requests)
 };
 
@@ -83,8 +100,12 @@ std::string huffman_encode(const std::string& s);
 
 class HpackDecoder {
  public:
-  // Decodes one header block; false on a malformed block (a connection error).
+  // Decodes one header block; false on a malformed block (a connection error) or when the decoded
+  // header list exceeds max_list (sum of name + value + 32 per field, RFC 7540 6.5.2): indexed
+  // fields can expand a small block, so the bound applies to the output, not the input.
   bool decode(const u8* p, size_t n, std::vector<std::pair<std::string, std::string>>& out);
+  void set_max_list(size_t n) { max_list_ = n; }
+  bool list_too_large() const { return over_; }
   size_t table_size() const { return size_; }
   size_t table_entries() const { return dyn_.size(); }
 
@@ -94,6 +115,8 @@ class HpackDecoder {
   void evict();
   std::vector<std::pair<std::string, std::string>> dyn_;  // newest first
   size_t size_ = 0, max_ = 4096, limit_ = 4096;
+  size_t max_list_ = size_t(-1);
+  bool over_ = false;
 };
 
 }  // namespace vep::rpc

@@ -1,0 +1,429 @@
+"""Hostile and edge-case HTTP/2 traffic against the native gRPC endpoint (csrc/vep/rpcsrv.cpp).
+
+The reference serves VideoLatestImage with grpc-go's stock server (server/main.go:142-153), which
+bounds header lists, frame sizes, concurrent streams and buffered input. These tests drive the
+native replacement with a raw-socket HTTP/2 client and check the same protections:
+
+* CONTINUATION flood / HPACK expansion -> GOAWAY ENHANCE_YOUR_CALM before any large buffering;
+* frames above the 16,384-byte SETTINGS_MAX_FRAME_SIZE -> GOAWAY FRAME_SIZE_ERROR;
+* streams above SETTINGS_MAX_CONCURRENT_STREAMS -> RST_STREAM REFUSED_STREAM;
+* HEADERS + DATA + RST_STREAM loops: the reset cancels the waiting job (the waiter pool is not
+  held), and a connection resetting faster than the limit gets GOAWAY (rapid-reset defence);
+* per-stream queued requests are bounded (RESOURCE_EXHAUSTED), streams past the deadline end with
+  DEADLINE_EXCEEDED even when idle, flow control in both directions;
+* long grpc-message trailers stay within a frame; IPv6 / host-name listen addresses;
+* a byte-level mutation fuzz of valid connections: the server stays up and keeps serving.
+"""
+import os
+import random
+import socket
+import struct
+import threading
+import time
+
+import pytest
+
+from conftest import synth
+
+SERVICE = "/chrys.cloud.videostreaming.v1beta1.Image/"
+DATA, HEADERS, PRIORITY, RST, SETTINGS, PUSH, PING, GOAWAY, WINUPD, CONT = range(10)
+END_STREAM, END_HEADERS, PADDED = 1, 4, 8
+
+
+def frame(ftype, flags, sid, payload=b""):
+    n = len(payload)
+    return struct.pack(">BHBBI", n >> 16, n & 0xFFFF, ftype, flags, sid & 0x7FFFFFFF) + payload
+
+
+def hp_int(v, prefix, first=0):
+    mask = (1 << prefix) - 1
+    if v < mask:
+        return bytes([first | v])
+    out = [first | mask]
+    v -= mask
+    while v >= 128:
+        out.append(0x80 | (v & 0x7F))
+        v >>= 7
+    out.append(v)
+    return bytes(out)
+
+
+def hp_lit(name, value, index=False):
+    """literal header field, new name, raw strings (with incremental indexing if index)"""
+    name, value = name.encode(), value.encode() if isinstance(value, str) else value
+    return (b"\x40" if index else b"\x00") + hp_int(len(name), 7) + name + hp_int(len(value), 7) + value
+
+
+def request_block(method="VideoLatestImage"):
+    return (hp_lit(":method", "POST") + hp_lit(":scheme", "http") + hp_lit(":path", SERVICE + method)
+            + hp_lit(":authority", "x") + hp_lit("content-type", "application/grpc") + hp_lit("te", "trailers"))
+
+
+def grpc_msg(b):
+    return b"\x00" + struct.pack(">I", len(b)) + b
+
+
+def frame_request(dev, kfo=False):
+    d = dev.encode()
+    body = (b"\x08\x01" if kfo else b"") + b"\x12" + bytes([len(d)]) + d
+    return grpc_msg(body)
+
+
+class H2:
+    """Minimal HTTP/2 client: writes raw frames, reads and classifies the server's frames."""
+
+    def __init__(self, port, host="127.0.0.1", window=None):
+        self.s = socket.create_connection((host, port), timeout=10)
+        self.buf = b""
+        settings = b"" if window is None else struct.pack(">HI", 4, window)
+        self.s.sendall(b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n" + frame(SETTINGS, 0, 0, settings))
+
+    def send(self, data):
+        self.s.sendall(data)
+
+    def try_send(self, data):
+        try:
+            self.s.sendall(data)
+            return True
+        except OSError:
+            return False
+
+    def read_frame(self, timeout=5.0):
+        self.s.settimeout(timeout)
+        while len(self.buf) < 9 or len(self.buf) < 9 + int.from_bytes(self.buf[:3], "big"):
+            try:
+                d = self.s.recv(1 << 20)
+            except (socket.timeout, ConnectionResetError):
+                return None
+            if not d:
+                return None
+            self.buf += d
+        n = int.from_bytes(self.buf[:3], "big")
+        t, fl, sid = self.buf[3], self.buf[4], struct.unpack(">I", self.buf[5:9])[0] & 0x7FFFFFFF
+        p = self.buf[9:9 + n]
+        self.buf = self.buf[9 + n:]
+        return t, fl, sid, p
+
+    def frames(self, timeout=5.0, until=None):
+        """frames until the connection closes, `timeout` passes without one, or until(frame)"""
+        out = []
+        end = time.time() + timeout
+        while time.time() < end:
+            f = self.read_frame(max(0.05, end - time.time()))
+            if f is None:
+                break
+            out.append(f)
+            if until and until(f):
+                break
+        return out
+
+    def goaway_code(self, timeout=5.0):
+        for t, fl, sid, p in self.frames(timeout, until=lambda f: f[0] == GOAWAY):
+            if t == GOAWAY:
+                return struct.unpack(">I", p[4:8])[0]
+        return None
+
+    def close(self):
+        try:
+            self.s.close()
+        except OSError:
+            pass
+
+
+def trailers_status(block):
+    """grpc-status of a trailers block the server wrote (literal without indexing, raw strings)"""
+    i = block.find(b"grpc-status")
+    if i < 0:
+        return None
+    ln = block[i + 11]
+    return int(block[i + 12:i + 12 + ln])
+
+
+def _owner(native, tag, n=4):
+    w = native.Worker(device=-1)
+    w.start()
+    o = native.BusOwner(tag, 0, n)
+    o.attach(w)
+    return w, o
+
+
+@pytest.fixture()
+def server(native):
+    made = []
+
+    def make(**kw):
+        tag = f"h{os.getpid()}{len(made)}{random.randrange(1 << 30)}"
+        w, o = _owner(native, tag)
+        args = dict(io_threads=2, wait_threads=8, slow_threads=2, reuseport=False)
+        args.update(kw)
+        srv = native.RpcServer(args.pop("host", "127.0.0.1"), 0, tag, **args)
+        made.append((srv, o, w))
+        return srv, w, o
+
+    yield make
+    for srv, o, w in made:
+        srv.stop()
+        o.stop()
+        w.stop()
+
+
+def _rss_mb():
+    with open("/proc/self/statm") as f:
+        return int(f.read().split()[1]) * os.sysconf("SC_PAGE_SIZE") / 2**20
+
+
+def test_continuation_flood_gets_goaway_and_memory_stays_flat(server):
+    srv, _, _ = server()
+    rss0 = _rss_mb()
+    c = H2(srv.port)
+    c.send(frame(HEADERS, 0, 1, request_block()))  # no END_HEADERS: CONTINUATION expected
+    sent = 0
+    chunk = frame(CONT, 0, 1, b"\x00" * 16384)
+    while sent < (256 << 20) and c.try_send(chunk * 16):
+        sent += 16 * 16384
+    assert sent < (64 << 20)  # the server closed the connection long before 256 MiB
+    code = c.goaway_code()
+    c.close()
+    assert code in (11, None)  # ENHANCE_YOUR_CALM (None: the RST raced the GOAWAY read)
+    st = srv.stats()
+    assert st["goaways"] >= 1 and st["protocol_errors"] >= 1
+    assert _rss_mb() - rss0 < 64
+
+
+def test_hpack_expansion_bomb_is_bounded(server):
+    """A 4 KB indexed value referenced 4,000 times (one byte each) would decode to 16 MB: the
+    decoded header list is bounded by the advertised SETTINGS_MAX_HEADER_LIST_SIZE (16 KiB)."""
+    srv, _, _ = server()
+    c = H2(srv.port)
+    blk = request_block() + hp_lit("x-big", "v" * 4000, index=True) + bytes([0x80 | 62]) * 4000
+    assert len(blk) < 16384
+    c.send(frame(HEADERS, END_HEADERS, 1, blk))
+    assert c.goaway_code() == 11
+    c.close()
+
+
+def test_oversized_frame_is_frame_size_error(server):
+    srv, _, _ = server()
+    c = H2(srv.port)
+    c.send(frame(PING, 0, 0, b"\x00" * 20000))
+    assert c.goaway_code() == 6  # FRAME_SIZE_ERROR
+    c.close()
+    c = H2(srv.port)  # a bad frame length is an error before its payload arrives
+    c.send(struct.pack(">BHBBI", 0xFF, 0xFFFF, DATA, 0, 1))
+    assert c.goaway_code() == 6
+    c.close()
+    c = H2(srv.port)  # malformed control frames
+    c.send(frame(SETTINGS, 0, 0, b"\x00" * 5))
+    assert c.goaway_code() == 6
+    c.close()
+    c = H2(srv.port)
+    c.send(frame(WINUPD, 0, 0, b"\x00\x00\x00\x00"))  # zero increment on the connection
+    assert c.goaway_code() == 1
+    c.close()
+
+
+def test_stream_limit_refuses_streams(server):
+    srv, _, _ = server(max_streams=50)
+    c = H2(srv.port)
+    blk = request_block()
+    c.send(b"".join(frame(HEADERS, END_HEADERS, 1 + 2 * i, blk) for i in range(80)))
+    refused = set()
+    for t, fl, sid, p in c.frames(3.0):
+        if t == RST and struct.unpack(">I", p)[0] == 7:
+            refused.add(sid)
+    assert refused == {1 + 2 * i for i in range(50, 80)}
+    assert srv.stats()["refused_streams"] == 30
+    c.close()
+
+
+def test_reset_cancels_waiters_and_rapid_reset_gets_goaway(server, native):
+    """HEADERS + DATA + RST loops: each reset releases its waiter (4 waiter threads serve 400
+    reset requests at once and then a legitimate client); past max_resets_per_s the connection
+    gets GOAWAY ENHANCE_YOUR_CALM."""
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
+    srv, w, o = server(wait_threads=4, max_resets_per_s=100000)
+    cam = w.add_camera("camH", 3)
+    o.add(cam, "camH")
+    c = H2(srv.port)
+    req = frame_request("camH")
+    batch = []
+    for i in range(400):
+        sid = 1 + 2 * i
+        batch.append(frame(HEADERS, END_HEADERS, sid, request_block()) + frame(DATA, 0, sid, req)
+                     + frame(RST, 0, sid, struct.pack(">I", 8)))
+    t0 = time.time()
+    c.send(b"".join(batch))
+    time.sleep(0.5)
+    enc = synth(native, 160, 128, gop=5)
+    w.decode_now(cam, enc.next())
+    cli = ImageClient(f"127.0.0.1:{srv.port}")
+    try:
+        vf = cli.latest_frame("camH", timeout=10)
+        assert vf.width == 160 and time.time() - t0 < 6  # 400 x 3 s of held waiters would take minutes
+    finally:
+        cli.close()
+    st = srv.stats()
+    assert st["cancelled_waits"] >= 1 and st["protocol_errors"] == 0
+    c.close()
+    # rapid reset over the limit
+    srv2, w2, o2 = server(max_resets_per_s=50)
+    c = H2(srv2.port)
+    c.send(b"".join(frame(HEADERS, END_HEADERS, 1 + 2 * i, request_block())
+                    + frame(RST, 0, 1 + 2 * i, struct.pack(">I", 8)) for i in range(200)))
+    assert c.goaway_code() == 11
+    c.close()
+
+
+def test_queued_requests_are_bounded(server):
+    srv, _, _ = server(max_queued_requests=4)
+    c = H2(srv.port)
+    c.send(frame(HEADERS, END_HEADERS, 1, request_block()))
+    c.send(frame(DATA, 0, 1, frame_request("nope") * 20))
+    status = None
+    for t, fl, sid, p in c.frames(8.0, until=lambda f: f[0] == HEADERS and f[1] & END_STREAM):
+        if t == HEADERS and fl & END_STREAM:
+            status = trailers_status(p)
+    assert status == 8  # RESOURCE_EXHAUSTED
+    c.close()
+
+
+def test_idle_stream_hits_deadline(server):
+    srv, _, _ = server(stream_deadline_ms=400)
+    c = H2(srv.port)
+    c.send(frame(HEADERS, END_HEADERS, 1, request_block()))  # never sends a request
+    t0 = time.time()
+    got = [f for f in c.frames(5.0, until=lambda f: f[0] == HEADERS and f[1] & END_STREAM)
+           if f[0] == HEADERS and f[1] & END_STREAM]
+    assert got and trailers_status(got[0][3]) == 4 and time.time() - t0 < 3
+    assert srv.stats()["deadline_streams"] >= 1
+    c.close()
+
+
+def test_small_window_stops_and_resumes_data(server, native):
+    srv, w, o = server()
+    cam = w.add_camera("camW", 3)
+    o.add(cam, "camW")
+    enc = synth(native, 320, 240, gop=5)
+    w.decode_now(cam, enc.next())
+    c = H2(srv.port, window=1000)
+    c.send(frame(HEADERS, END_HEADERS, 1, request_block()) + frame(DATA, END_STREAM, 1, frame_request("camW")))
+    got = sum(len(p) for t, fl, sid, p in c.frames(2.0) if t == DATA)
+    assert got == 1000  # the stream window (the connection window is 64 KiB)
+    c.send(frame(WINUPD, 0, 1, struct.pack(">I", 1 << 24)) + frame(WINUPD, 0, 0, struct.pack(">I", 1 << 24)))
+    fs = c.frames(5.0, until=lambda f: f[0] == HEADERS and f[1] & END_STREAM)
+    got += sum(len(p) for t, fl, sid, p in fs if t == DATA)
+    assert got > 320 * 240 * 3 and trailers_status(fs[-1][3]) == 0
+    c.close()
+
+
+def test_handler_errors_and_long_messages(server):
+    import grpc
+
+    from video_edge_ai_proxy_amd.proto import pb
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
+    def h(method, req, peer):
+        if method == "Annotate":
+            raise RuntimeError("boom")
+        return 3, "x" * 100000, []  # a 100 kB message: truncated to fit one trailers frame
+
+    srv, _, _ = server(handler=h)
+    cli = ImageClient(f"127.0.0.1:{srv.port}")
+    try:
+        with pytest.raises(grpc.RpcError) as e:
+            cli.Annotate(pb.AnnotateRequest())
+        assert e.value.code() == grpc.StatusCode.INTERNAL
+        with pytest.raises(grpc.RpcError) as e:
+            cli.Proxy(pb.ProxyRequest(device_id="x"))
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT and 0 < len(e.value.details()) <= 1024
+        # the connection survived both
+        with pytest.raises(grpc.RpcError) as e:
+            cli.Proxy(pb.ProxyRequest(device_id="x"))
+        assert e.value.code() == grpc.StatusCode.INVALID_ARGUMENT
+    finally:
+        cli.close()
+    assert srv.stats()["protocol_errors"] == 0
+
+
+@pytest.mark.parametrize("host", ["localhost", "::", "0.0.0.0"])
+def test_listen_host_names(server, host):
+    try:
+        srv, _, _ = server(host=host)
+    except RuntimeError as e:
+        if host == "::" and "bind" in str(e):
+            pytest.skip("no IPv6 in this container")
+        raise
+    c = H2(srv.port)
+    c.send(frame(PING, 0, 0, b"12345678"))
+    fs = c.frames(3.0, until=lambda f: f[0] == PING)
+    assert any(t == PING and fl & 1 and p == b"12345678" for t, fl, sid, p in fs)
+    c.close()
+
+
+def _valid_session(dev):
+    req = frame_request(dev)
+    out = [frame(SETTINGS, 0, 0, struct.pack(">HI", 4, 1 << 20)), frame(PING, 0, 0, b"abcdefgh"),
+           frame(WINUPD, 0, 0, struct.pack(">I", 1 << 20))]
+    for i in range(3):
+        sid = 1 + 2 * i
+        blk = request_block("VideoLatestImage" if i != 1 else "ListStreams")
+        out.append(frame(HEADERS, 0, sid, blk[:20]) + frame(CONT, END_HEADERS, sid, blk[20:]))
+        out.append(frame(DATA, PADDED, sid, bytes([3]) + req + b"\x00\x00\x00"))
+        out.append(frame(PRIORITY, 0, sid, b"\x00\x00\x00\x00\x10"))
+        out.append(frame(DATA, END_STREAM, sid, b""))
+    out.append(frame(RST, 0, 5, struct.pack(">I", 8)))
+    out.append(frame(GOAWAY, 0, 0, struct.pack(">II", 0, 0)))
+    return b"PRI * HTTP/2.0\r\n\r\nSM\r\n\r\n" + b"".join(out)
+
+
+def test_mutation_fuzz_keeps_server_alive(server, native):
+    """300 connections of a valid session (SETTINGS, PING, CONTINUATION, padded DATA, PRIORITY,
+    RST, GOAWAY) with random byte flips, insertions, deletions and truncations; afterwards a
+    legitimate client is still served. (The same mutator runs under ASan in
+    csrc/tests/rpc_stress.cpp.)"""
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
+    srv, w, o = server(wait_threads=16, stream_deadline_ms=2000,
+                       handler=lambda m, r, p: (0, "", []))
+    cam = w.add_camera("camF", 3)
+    o.add(cam, "camF")
+    enc = synth(native, 160, 128, gop=5)
+    w.decode_now(cam, enc.next())
+    base = _valid_session("camF")
+    rng = random.Random(1234)
+    socks = []
+    for it in range(300):
+        b = bytearray(base)
+        for _ in range(rng.randrange(1, 8)):
+            op = rng.randrange(4)
+            i = rng.randrange(len(b))
+            if op == 0:
+                b[i] = rng.randrange(256)
+            elif op == 1:
+                b[i:i] = bytes(rng.randrange(256) for _ in range(rng.randrange(1, 16)))
+            elif op == 2:
+                del b[i:i + rng.randrange(1, 16)]
+            else:
+                b[i] ^= 1 << rng.randrange(8)
+        if rng.random() < 0.2:
+            b = b[:rng.randrange(len(b))]
+        try:
+            s = socket.create_connection(("127.0.0.1", srv.port), timeout=5)
+            s.sendall(bytes(b))
+            socks.append(s)
+        except OSError:
+            pass
+        if len(socks) > 32:
+            for s in socks:
+                s.close()
+            socks.clear()
+    for s in socks:
+        s.close()
+    cli = ImageClient(f"127.0.0.1:{srv.port}")
+    try:
+        assert cli.latest_frame("camF", timeout=10).width == 160
+    finally:
+        cli.close()
+    st = srv.stats()
+    assert st["protocol_errors"] > 0 and st["connections"] >= 300
