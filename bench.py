@@ -115,6 +115,13 @@ def parse_args():
     ap.add_argument("--ring-slots", type=int, default=2)
     ap.add_argument("--latency-samples", type=int, default=100)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (plumbing check, no GPU)")
+    ap.add_argument("--ref-equivalent", action="store_true",
+                    help="with --cpu: the reference-equivalent CPU path (CPU parse + CPU reconstruction + CPU "
+                         "BGR24, the tobytes + SerializeToString copy chain per frame; read_image.py:87-121)")
+    ap.add_argument("--ref-cpu", choices=["on", "off"], default="on",
+                    help="GPU runs: after the measurement, rank 0 runs the same cameras / steps / clients "
+                         "through the reference-equivalent CPU path on its host domain's CPUs and reports "
+                         "reference_equivalent_cpu_fps and vs_baseline = value / (that x ranks)")
     ap.add_argument("--source", choices=["replay", "rtsp"], default="rtsp",
                     help="replay = pre-encoded AUs fed to the decode pipeline (decode-only); rtsp = an "
                          "in-process loopback RTSP camera farm, unthrottled, with the production "
@@ -247,6 +254,15 @@ def latency_fields(a, lat, live_fps=None):
     if live_fps is not None:
         out["latency_live_fps_per_camera"] = round(live_fps, 2)
     return out
+
+
+def n_gpus_scope(res):
+    """The headline names a whole node (8 GPUs, 256 cameras); a run on fewer GPUs is that share."""
+    n = res.get("n_gpus") or 0
+    if 0 < n < 8:
+        cams = res["config"]["cams_per_gpu"] * n
+        return f"per-GPU share: {n} of the node's 8 GPUs ({cams} of 256 cameras); not a whole-node number"
+    return None
 
 
 def spawn_ranks(n: int) -> int:
@@ -672,6 +688,13 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             res["latency_farm_settled"] = lat["settled"]
             res["live_phase_access_units_skipped"] = lat["live_skipped"]
         res.update(side)  # (rank 0's side loads)
+        if n_gpus_scope(res):
+            res["scope"] = n_gpus_scope(res)
+        if use_gpu and not a.cpu and a.ref_cpu == "on":
+            res.update(reference_fields(a, res, world))
+        elif a.cpu and a.ref_equivalent:
+            res["source_definition"] = REF_CPU_DEFINITION
+            res["ref_copy_bytes"] = worker.ref_copy_bytes
         print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -699,6 +722,70 @@ def payload_path(a, compressed, worker, ip0, sg0, rg0=0, end=None):
     return {"gpu_input": "I_PCM slice bytes: the decode kernel reads them from pinned host memory over PCIe"
                          if worker.direct_reads else "I_PCM slice bytes gathered into HBM, decode reads HBM",
             "slice_bytes_read_in_place_per_step": inplace, "slice_bytes_staged_per_step": staged}
+
+
+REF_CPU_DEFINITION = (
+    "reference-equivalent CPU path (SURVEY.md §6 / BASELINE.md: FFmpeg, Redis and the Go server cannot run "
+    "here): the same cameras, streams, RTSP farm, steps and latency clients, decoded by this repo's CPU backend "
+    "on rank 0's host-domain CPUs (its CPU share) - CPU CABAC parse, CPU reconstruction (the portable scalar "
+    "bit-exact reference, no SIMD: libavcodec's SIMD decoder is faster, so vs_baseline is an upper bound), CPU "
+    "NV12->BGR24 and the read_image.py:97/:119 tobytes + SerializeToString copy chain per published frame; "
+    "whole-node value = per-share rate x ranks (each GPU has its own CPU share)")
+
+
+def reference_equivalent(a):
+    """Rank 0, after the GPU measurement: the same command on the CPU backend in a fresh process
+    (bench.py --cpu --ref-equivalent) on this rank's host-domain CPUs; its JSON line."""
+    import subprocess
+
+    args = [a for a in sys.argv[1:]]
+    drop = {"--gpus", "--ref-cpu", "--warmup"}
+    out, skip = [], False
+    for x in args:
+        if skip:
+            skip = False
+            continue
+        key = x.split("=")[0]
+        if key in drop:
+            skip = "=" not in x
+            continue
+        out.append(x)
+    cmd = [sys.executable, os.path.abspath(__file__), *out, "--cpu", "--ref-equivalent", "--ref-cpu", "off",
+           "--warmup", "1"]
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT") and not k.startswith("TORCHELASTIC")}
+    env["VEP_HOST_CPUS"] = a.host_domain["cpulist"]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=420)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"error": f"reference-equivalent run failed (rc {r.returncode}): {r.stderr[-400:]}"}
+    d = json.loads(lines[-1])
+    d["wall_s"] = round(time.perf_counter() - t0, 1)
+    return d
+
+
+def reference_fields(a, res, world):
+    """reference_equivalent_cpu_fps and vs_baseline for the GPU run's JSON (rank 0)."""
+    ref = reference_equivalent(a)
+    if "value" not in ref:
+        return {"reference_equivalent": ref}
+    per_share = ref["value"]
+    node = per_share * max(1, world)
+    keep = ("value", "frames_decoded", "frames_published", "decode_errors", "access_units_ingested", "ms_per_step",
+            "p50_latency_ms", "p99_latency_ms", "latency_frames_served_per_s", "rank0_host_cpu_cores_by_thread",
+            "rank0_host_domain", "steps", "warmup", "wall_s")
+    return {
+        "reference_equivalent_cpu_fps": round(node, 2),
+        "reference_equivalent_cpu_fps_per_share": per_share,
+        "reference_equivalent_p50_latency_ms": ref.get("p50_latency_ms"),
+        "reference_equivalent_definition": REF_CPU_DEFINITION,
+        "reference_equivalent_run": {k: ref.get(k) for k in keep},
+        "vs_baseline": round(res["value"] / node, 3) if node > 0 else None,
+        "vs_baseline_definition": "value / reference_equivalent_cpu_fps (BASELINE.json publishes no number; "
+                                  "this ratio is against the labelled reference-equivalent CPU path above)",
+    }
 
 
 def decoder_backend(a, compressed):
@@ -741,7 +828,9 @@ def main():
     # pinned to its GPU's NUMA-local CPUs and sized from the CPU budget (no constant cap)
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     plan_devs = list(range(local_world)) if use_gpu else [-1] * local_world
-    dom = vep.plan_host_domains(plan_devs)[local]
+    # VEP_HOST_CPUS "a-b;c-d;..." (one CPU list per local rank) overrides the NUMA-local plan
+    explicit = [x.strip() for x in os.environ["VEP_HOST_CPUS"].split(";")] if os.environ.get("VEP_HOST_CPUS") else []
+    dom = vep.plan_host_domains(plan_devs, explicit)[local]
     if a.threads > 0:
         dom["parse_threads"] = a.threads
     a.threads = dom["parse_threads"]
@@ -752,7 +841,8 @@ def main():
     worker = vep.Worker(device=local if use_gpu else -1, letterbox_size=S, chw_dtype=0,
                         max_cameras=cams, pack_threads=a.pack_threads,
                         letterbox_format=1 if a.consumer_format == "nv12" else 0, lanes=a.lanes,
-                        stages=a.stages, queue=a.lane_queue, host_domain=dom)
+                        stages=a.stages, queue=a.lane_queue, host_domain=dom,
+                        ref_copies=bool(a.cpu and a.ref_equivalent), backpressure=bool(a.cpu and a.ref_equivalent))
     row = S * S * 3 // 2 if a.consumer_format == "nv12" else S * S * 3
     compressed = a.content == "avc"  # (h265: general HEVC Main streams, CPU reconstruction)
     cfg = make_cfg(vep, a, rank, compressed)

@@ -1207,7 +1207,8 @@ PYBIND11_MODULE(_vep, m) {
       .def(py::init([](int device, int letterbox_size, int chw_dtype, std::vector<float> mean,
                        std::vector<float> stdv, int max_cameras, int pack_threads,
                        int letterbox_format, int lanes, int stages, int queue, bool lane_threads,
-                       const std::string& decoder, int kf_window_us, py::object host_domain) {
+                       const std::string& decoder, int kf_window_us, py::object host_domain,
+                       bool ref_copies, bool backpressure) {
              WorkerOptions o;
              o.device = device;
              if (!host_domain.is_none()) {
@@ -1223,6 +1224,8 @@ PYBIND11_MODULE(_vep, m) {
              o.queue = queue;
              o.lane_threads = lane_threads;
              o.kf_window_us = kf_window_us;
+             o.ref_copies = ref_copies;
+             o.backpressure = backpressure;
              o.pack_threads = pack_threads;
              o.letterbox_format = letterbox_format;
              o.letterbox_size = letterbox_size;
@@ -1239,7 +1242,9 @@ PYBIND11_MODULE(_vep, m) {
            py::arg("max_cameras") = 256, py::arg("pack_threads") = 4,
            py::arg("letterbox_format") = 0, py::arg("lanes") = 0, py::arg("stages") = 0,
            py::arg("queue") = 0, py::arg("lane_threads") = false, py::arg("decoder") = "native",
-           py::arg("kf_window_us") = -1, py::arg("host_domain") = py::none())
+           py::arg("kf_window_us") = -1, py::arg("host_domain") = py::none(), py::arg("ref_copies") = false,
+           py::arg("backpressure") = false)
+      .def_property_readonly("ref_copy_bytes", &Worker::ref_copy_bytes)
       .def_property_readonly("kf_window_us", &Worker::kf_window_us)
       .def_property_readonly("host_domain", [](Worker& w) { return domain_dict(w.host_domain()); })
       .def_property_readonly("ingest_parse_threads", &Worker::ingest_parse_threads)
@@ -1272,6 +1277,21 @@ PYBIND11_MODULE(_vep, m) {
              py::gil_scoped_release r;
              return c.on_access_unit(au);
            })
+      .def("read_surface",
+           [](Worker& w, int i) -> py::object {
+             HostSurface s;
+             i64 pts = 0;
+             bool ok;
+             {
+               py::gil_scoped_release r;
+               ok = w.read_surface(i, s, &pts);
+             }
+             if (!ok) return py::none();
+             return py::make_tuple(pts, surface_planes(s));
+           },
+           py::arg("cam"),
+           "(pts, (y, uv)) of the DPB surface holding the camera's newest published picture at full "
+           "sample depth (uint16 above 8 bits), coded size; None when none. Call with the camera idle.")
       .def("decode_now",
            [](Worker& w, int i, std::shared_ptr<AccessUnit> au) {
              Camera& c = cam_of(w, i);

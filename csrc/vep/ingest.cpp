@@ -305,6 +305,7 @@ void IngestSession::decode(const std::shared_ptr<Camera>& cam, const AuPtr& au) 
     if (!live->load(std::memory_order_acquire)) return;  // session stopped: cancelled
     try {
       cam->on_access_unit(au);
+      cam->wait_reconstruction();  // (WorkerOptions::backpressure only)
     } catch (const std::exception& e) {
       cam->errors.fetch_add(1);
       cam->logs.add(true, std::string("failed to decode packet: ") + e.what());

@@ -733,7 +733,8 @@ void RtspServer::serve(int fd) {
           ++h.seq;
         }
       }
-      if (!send_all(fd, out.data(), out.size(), 5000)) break;
+      // (a lossless reader pauses its socket for seconds while a slow backend drains its backlog)
+      if (!send_all(fd, out.data(), out.size(), 30000)) break;
       aus_sent_.fetch_add(1);
       ++frame;
     }

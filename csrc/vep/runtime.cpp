@@ -7,6 +7,7 @@
 #include <cmath>
 #include <csignal>
 #include <cstdio>
+#include <map>
 #include <thread>
 
 #include "color.h"
@@ -537,6 +538,10 @@ Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
     direct_reads_ = opt_.direct_reads && !(dr && dr[0] == '0');
   }
   if (opt_.pack_threads > 0 && !threaded_) pack_pool_ = std::make_unique<ThreadPool>(opt_.pack_threads, domain_thread_init(opt_.domain, nullptr));
+  if (!dev_.gpu()) {
+    const int n = opt_.domain.cpu_share > 0 ? opt_.domain.cpu_share : std::max(1, int(std::thread::hardware_concurrency()) / 2);
+    if (n > 1) cpu_pool_ = std::make_unique<ThreadPool>(n, domain_thread_init(opt_.domain, nullptr));
+  }
   if (threaded_)
     for (auto& lp : lanes_) {
       Lane* ln = lp.get();
@@ -719,6 +724,7 @@ void Worker::stop() {
     stop_ = true;
   }
   q_cv_.notify_all();
+  taken_cv_.notify_all();
   if (th_.joinable()) th_.join();
   std::lock_guard<std::mutex> g(q_mu_);
   running_ = false;
@@ -810,6 +816,49 @@ void Worker::submit(DecodeJob&& job) {
   q_cv_.notify_one();
 }
 
+void Worker::wait_camera_taken(int cam, int timeout_ms) {
+  std::unique_lock<std::mutex> g(q_mu_);
+  taken_cv_.wait_for(g, std::chrono::milliseconds(timeout_ms), [&] {
+    if (stop_) return true;
+    for (const DecodeJob& p : pending_)
+      if (p.cam == cam) return false;
+    return true;
+  });
+}
+
+bool Worker::read_surface(int cam, HostSurface& out, i64* pts) {
+  std::shared_ptr<Camera> c;
+  int slot;
+  {
+    std::lock_guard<std::mutex> g(cams_mu_);
+    if (cam < 0 || size_t(cam) >= cams_.size() || !cams_[size_t(cam)]) return false;
+    c = cams_[size_t(cam)];
+    slot = c->out_surface_slot;
+    if (pts) *pts = c->out_surface_pts;
+  }
+  if (slot < 0) return false;
+  const Camera::Surface& sf = c->surface;
+  if (!dev_.gpu()) {
+    if (size_t(slot) >= sf.host.size()) return false;
+    out = sf.host[size_t(slot)];
+    return true;
+  }
+  if (!sf.y || slot >= sf.slots) return false;
+  out.alloc(sf.wmbs * 16, sf.hmbs * 16, sf.bd, sf.cf);
+  void* dy = out.wide() ? static_cast<void*>(out.y16.data()) : static_cast<void*>(out.y.data());
+  void* duv = out.wide() ? static_cast<void*>(out.uv16.data()) : static_cast<void*>(out.uv.data());
+  VEP_CHECK(sf.slot_y() == size_t(out.coded_w) * size_t(out.coded_h) * size_t(sf.bps), "surface size mismatch");
+  dev_.bind();
+  VEP_HIP(hipDeviceSynchronize());  // (the picture's reconstruction ran on a lane stream)
+  VEP_HIP(hipMemcpy(dy, sf.y + size_t(slot) * sf.slot_y(), sf.slot_y(), hipMemcpyDeviceToHost));
+  VEP_HIP(hipMemcpy(duv, sf.uv + size_t(slot) * sf.slot_uv(), sf.slot_uv(), hipMemcpyDeviceToHost));
+  return true;
+}
+
+void Camera::wait_reconstruction() {
+  if (w_.options().backpressure) w_.wait_camera_taken(index_, 2000);
+}
+
 void Worker::flush() {
   {
     std::unique_lock<std::mutex> g(q_mu_);
@@ -843,6 +892,7 @@ void Worker::loop() {
       batch.swap(pending_);
       busy_ = true;
     }
+    taken_cv_.notify_all();
     try {
       launch_async(batch);
     } catch (const std::exception& e) {
@@ -1776,14 +1826,35 @@ void Worker::launch_gpu(Lane& ln, Stage& st) {
 void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
                      std::vector<u32>& err) {
   err.assign(jobs.size(), 0);
+  // one task per camera (a camera's jobs stay in order: they share its surfaces)
+  std::vector<std::vector<size_t>> groups;
+  std::map<int, size_t> of;
   for (size_t i = 0; i < jobs.size(); ++i) {
+    auto it = of.find(jobs[i].cam);
+    if (it == of.end()) {
+      of[jobs[i].cam] = groups.size();
+      groups.push_back({i});
+    } else {
+      groups[it->second].push_back(i);
+    }
+  }
+  auto run = [&](int g) {
+    for (size_t i : groups[size_t(g)]) run_cpu_job(jobs, slots, err, i);
+  };
+  if (cpu_pool_ && groups.size() > 1) cpu_pool_->parallel_for(int(groups.size()), run);
+  else
+    for (int g = 0; g < int(groups.size()); ++g) run(g);
+}
+
+void Worker::run_cpu_job(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err, size_t i) {
+  {
     Camera& c = *cams_[size_t(jobs[i].cam)];
     const PictureInfo& pi = jobs[i].pic;
     for (int sl = pi.spec_lo; sl < pi.spec_hi && !err[i]; ++sl) {  // speculative headers
       const u8* b = jobs[i].upd.block(sl);
       err[i] = (b[-2] != 0x0D || b[-1] != 0x00) ? 1u : 0u;
     }
-    if (err[i]) continue;
+    if (err[i]) return;
     if (jobs[i].ext) {  // VCN picture (host-visible planes on the CPU backend)
       const vcn::Frame& f = *jobs[i].ext;
       HostSurface& hs = c.surface.host[0];
@@ -1809,7 +1880,7 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
     } else {
       cpu_apply_update(jobs[i].upd, c.surface.host[0]);
     }
-    if (!jobs[i].has_output()) continue;
+    if (!jobs[i].has_output()) return;
     HostSurface narrow;  // Main10: the 8-bit copy the conversion and the letterbox read
     HostSurface woven;   // a field pair's frame
     if (jobs[i].out_fields) {
@@ -1823,6 +1894,21 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
     const HostSurface& src = conv ? narrow : out;
     cpu_nv12_to_bgr(src, jobs[i].pic.crop_left, jobs[i].pic.crop_top,
                     jobs[i].pic.width, jobs[i].pic.height, c.ring_->slot_ptr(slots[i]));
+    if (opt_.ref_copies) {  // read_image.py:97 tobytes() + :119 SerializeToString()
+      const size_t n = size_t(jobs[i].pic.width) * size_t(jobs[i].pic.height) * 3;
+      std::vector<u8> bytes(c.ring_->slot_ptr(slots[i]), c.ring_->slot_ptr(slots[i]) + n);
+      FrameMeta m{};
+      m.width = jobs[i].pic.width;
+      m.height = jobs[i].pic.height;
+      m.pts = jobs[i].meta.pts;
+      const auto pre_suf = encode_video_frame(m, n, c.name());
+      std::string msg;
+      msg.reserve(pre_suf.first.size() + n + pre_suf.second.size());
+      msg += pre_suf.first;
+      msg.append(reinterpret_cast<const char*>(bytes.data()), n);
+      msg += pre_suf.second;
+      ref_copy_bytes_.fetch_add(msg.size(), std::memory_order_relaxed);
+    }
     if (opt_.letterbox_size > 0) {
       gpu::LetterboxDesc l{};
       const size_t S = size_t(opt_.letterbox_size);
@@ -1840,7 +1926,7 @@ void Worker::run_cpu(std::vector<DecodeJob>& jobs, std::vector<int>& slots,
       gpu::fill_letterbox_geometry(l, opt_.letterbox_size, nv12);
       if (nv12) {
         cpu_letterbox_nv12(src, l, opt_.letterbox_size, 114);
-        continue;
+        return;
       }
       gpu::LetterboxParams p{};
       p.size = opt_.letterbox_size;
@@ -1951,6 +2037,8 @@ void Worker::publish(std::vector<DecodeJob>& jobs, std::vector<int>& slots, cons
       cp->lat_sum_ms.fetch_add(u64(lat), std::memory_order_relaxed);
     }
     cp->ring_->commit(slots[i], jobs[i].meta);
+    cp->out_surface_slot = jobs[i].general() && !jobs[i].out_fields ? jobs[i].target() : -1;
+    cp->out_surface_pts = jobs[i].meta.pts;
     cp->decoded.fetch_add(1, std::memory_order_relaxed);
     frames_.fetch_add(1, std::memory_order_relaxed);
     if (auto hook = std::atomic_load(&publish_hook_)) (*hook)(jobs[i].cam, cp->ring_->published());

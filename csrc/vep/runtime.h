@@ -164,6 +164,8 @@ class Camera {
   Camera(Worker& w, int index, std::string name, int ring_slots);
   const std::string& name() const { return name_; }
   int index() const { return index_; }
+  // WorkerOptions::backpressure: wait (bounded) until the worker took this camera's queued job
+  void wait_reconstruction();
 
   // --- control (atomics; replaces Redis control keys) ---
   std::atomic<i64> last_query_ms{0};   // 0 = never queried ("no last_query" in the hash)
@@ -226,6 +228,10 @@ class Camera {
     std::vector<HostSurface> fields;  // CPU backend, H.264 field pictures: one per field slot
   } surface;
   std::shared_ptr<FrameRing> ring_;  // written by the worker via set_ring(); read via ring()
+  // DPB slot and pts of the newest published picture (Worker::read_surface; -1: none / a field
+  // pair). Worker thread, under the worker's camera lock.
+  int out_surface_slot = -1;
+  i64 out_surface_pts = 0;
   int ring_slots_cfg;
 
  private:
@@ -302,6 +308,17 @@ struct WorkerOptions {
   // copies, as the GPU path's D2H does, so its concurrency (acquire_serve / release_serve, chunk
   // hand-off) runs under ThreadSanitizer without a GPU. Also VEP_MOCK_SERVE=1.
   bool mock_serve = false;
+  // CPU backend: the reference's per-frame copy chain after the BGR24 conversion
+  // (read_image.py:97 `img.tobytes()` + :119 `SerializeToString()`): each published frame is
+  // copied into a bytes buffer and then into a serialized VideoFrame message. Used by the bench's
+  // reference-equivalent CPU run (bench.py), off otherwise.
+  bool ref_copies = false;
+  // Lossless ingest also waits for reconstruction: a camera's parse strand waits (up to 2 s)
+  // until the worker has taken the camera's queued job before parsing its next access unit, so a
+  // reconstruction-bound backend back-pressures the socket instead of parsing pictures a GOP
+  // catch-up later drops (the reference decodes only what it shows). Used by the bench's
+  // reference-equivalent CPU run.
+  bool backpressure = false;
   // Host domain (hostplan.h): the CPUs this worker's host threads run on and its ingest pool
   // sizes. parse_threads 0 = none: the worker's threads are not pinned and its cameras share the
   // process-wide ingest services.
@@ -490,6 +507,10 @@ class Worker {
   std::condition_variable pub_cv_;
   std::exception_ptr lane_err_;  // first error of a lane thread, rethrown to the launcher
   std::unique_ptr<ThreadPool> pack_pool_;
+  // CPU backend: reconstruction + conversion of a batch's cameras in parallel (the reference runs
+  // one decoder per camera container); the host domain's CPU share threads
+  std::unique_ptr<ThreadPool> cpu_pool_;
+  void run_cpu_job(std::vector<DecodeJob>& jobs, std::vector<int>& slots, std::vector<u32>& err, size_t i);
 
  public:
   // host-side launch path timers (µs, cumulative): where a batch's CPU time goes (summed over
@@ -529,7 +550,7 @@ class Worker {
   int cons_rows_ = 0;
   // live queue
   std::mutex q_mu_;
-  std::condition_variable q_cv_, idle_cv_;
+  std::condition_variable q_cv_, idle_cv_, taken_cv_;
   std::vector<DecodeJob> pending_;
   int kf_window_us_ = 0;
   // H.265 intra transform blocks: 0 = one launch per dependency level; k > 0 = one queue launch
@@ -540,6 +561,19 @@ class Worker {
   // hipEventSynchronize, which spins a core in the HSA runtime)
   bool polite_wait_ = true;
   bool mock_serve_ = false;  // WorkerOptions::mock_serve
+
+ public:
+  u64 ref_copy_bytes() const { return ref_copy_bytes_.load(); }  // WorkerOptions::ref_copies output
+  // until no queued (not yet taken) job of camera `cam` or timeout_ms passed
+  void wait_camera_taken(int cam, int timeout_ms);
+  // Debug / test readback of the DPB surface holding camera `cam`'s newest published picture, at
+  // its full sample depth (u16 planes above 8 bits; NV16 chroma for 4:2:2) and coded size: what
+  // the reconstruction wrote before the 8-bit narrowing for BGR24. False when none (or a field
+  // pair). Call with the camera idle (after decode_now / flush): later jobs reuse the slot.
+  bool read_surface(int cam, HostSurface& out, i64* pts);
+
+ private:
+  std::atomic<u64> ref_copy_bytes_{0};
   bool running_ = false, stop_ = false, busy_ = false;
   std::thread th_;
   std::mutex svc_mu_;

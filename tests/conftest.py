@@ -51,6 +51,27 @@ def synth(native, w=640, h=480, gop=10, motion=0.05, seed=1, slices=1, zero=Fals
     return native.SynthH264(c)
 
 
+def check_surface(wk, cam, pts, full, w, h, cf=1):
+    """The DPB surface behind camera `cam`'s newest published frame (Worker.read_surface: full
+    sample depth, before the 8-bit narrowing for BGR24) equals the encoder's reconstruction of that
+    picture, `full[pts]` = (y, uv) coded planes (uint16 above 8 bits; 4:2:2 chroma has h rows).
+    Returns the luma plane read back."""
+    import numpy as np
+
+    r = wk.read_surface(cam)
+    assert r is not None, "no surface for the published frame"
+    spts, (y, uv) = r
+    assert spts == pts, (spts, pts)
+    wy, wuv = full[pts]
+    assert y.dtype == wy.dtype, (y.dtype, wy.dtype)
+    ch = h if cf == 2 else h // 2
+    dy = y[:h, :w] != wy[:h, :w]
+    assert not dy.any(), f"pts {pts}: {int(dy.sum())} luma samples differ at full depth"
+    duv = uv[:ch, :w] != wuv[:ch, :w]
+    assert not duv.any(), f"pts {pts}: {int(duv.sum())} chroma samples differ at full depth"
+    return y[:h, :w]
+
+
 def high_encoder(native, w=176, h=144, **kw):
     """Main / High-profile synthetic encoder (avc::AvcHighEncoder); kw = AvcHighConfig fields."""
     c = native.AvcHighConfig()

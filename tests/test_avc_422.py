@@ -16,7 +16,7 @@ macroblock layer and reconstruction, so the closed loop pins that both direction
 import numpy as np
 import pytest
 
-from conftest import high_encoder, roundtrip
+from conftest import check_surface, high_encoder, roundtrip
 
 CONFIGS = {
     "cabac-ibbp": dict(bframes=2),
@@ -101,10 +101,11 @@ def run_camera(native, device, w, h, n, **kw):
     s = synth_422(native, w, h, **kw)
     wk = native.Worker(device=device)
     cam = wk.add_camera("c422", 4)
-    want, published, seq = {}, 0, 0
+    want, full, published, seq, low_bits = {}, {}, 0, 0, False
     for _ in range(n):
         au = s.next()
         y, uv = s.picture()
+        full[s.last_pts] = (y.copy(), uv.copy())
         uv = (uv[0::2].astype(np.int32) + uv[1::2] + 1) >> 1  # 4:2:0 display conversion
         y = y.astype(np.int32)
         if bd > 8:
@@ -119,8 +120,13 @@ def run_camera(native, device, w, h, n, **kw):
         seq = meta["seq"]
         ref = want[meta["pts"]]
         assert np.array_equal(got, ref), f"pts {meta['pts']}: {int((got != ref).sum())} samples differ"
+        # the NV16 reconstruction itself at full depth (before the 4:2:0 display conversion and
+        # the 8-bit narrowing)
+        ys = check_surface(wk, cam, meta["pts"], full, w, h, cf=2)
+        low_bits |= bd > 8 and bool(((ys & ((1 << (bd - 8)) - 1)) != 0).any())
         published += 1
     assert wk.stats(cam)["decoder"] == "general"
+    assert bd == 8 or published == 0 or low_bits, "no sample below the 8-bit grid: the check would be vacuous"
     return published
 
 

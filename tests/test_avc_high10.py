@@ -18,7 +18,7 @@ avc_inter_kernel<u16> + avc_hbd_kernel, launch_narrow, decode_convert)."""
 import numpy as np
 import pytest
 
-from conftest import high_encoder, roundtrip
+from conftest import check_surface, high_encoder, roundtrip
 
 CONFIGS = {
     "cabac-ibbp": dict(bframes=2),
@@ -145,10 +145,11 @@ def run_camera(native, device, w, h, n, **kw):
     s = synth_avc(native, w, h, **kw)
     wk = native.Worker(device=device)
     cam = wk.add_camera("h10", 4)
-    want, published, seq = {}, 0, 0
+    want, full, published, seq, low_bits = {}, {}, 0, 0, False
     for _ in range(n):
         au = s.next()
         y, uv = s.picture()
+        full[s.last_pts] = (y.copy(), uv.copy())
         if bd > 8:  # the worker publishes the surface rounded to 8 bits
             y, uv = narrow(y, bd), narrow(uv, bd)
         want[s.last_pts] = native.nv12_to_bgr_cpu(y, uv, 0, 0, w, h)
@@ -160,8 +161,12 @@ def run_camera(native, device, w, h, n, **kw):
         seq = meta["seq"]
         ref = want[meta["pts"]]
         assert np.array_equal(got, ref), f"pts {meta['pts']}: {int((got != ref).sum())} samples differ"
+        # and the reconstruction itself at full depth (the low bits the narrowing rounds away)
+        ys = check_surface(wk, cam, meta["pts"], full, w, h)
+        low_bits |= bd > 8 and bool(((ys & ((1 << (bd - 8)) - 1)) != 0).any())
         published += 1
     assert wk.stats(cam)["decoder"] == "general"
+    assert bd == 8 or published == 0 or low_bits, "no sample below the 8-bit grid: the check would be vacuous"
     return published
 
 

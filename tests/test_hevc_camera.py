@@ -7,6 +7,8 @@ and on gfx950 in the GPU variant."""
 import numpy as np
 import pytest
 
+from conftest import check_surface
+
 
 def synth_hevc(native, w, h, **kw):
     c = native.SynthConfig()
@@ -21,12 +23,14 @@ def run_camera(native, device, w, h, n, **kw):
     s = synth_hevc(native, w, h, **kw)
     wk = native.Worker(device=device)
     cam = wk.add_camera("hevc", 4)
-    want = {}
+    want, full = {}, {}
     published = 0
     seq = 0
+    low_bits = False
     for _ in range(n):
         au = s.next()
         y, uv = s.picture()
+        full[s.last_pts] = (y.copy(), uv.copy())
         if y.dtype == np.uint16:  # Main10: the worker publishes the surface rounded to 8 bits
             y, uv = (np.minimum((p.astype(np.int32) + 2) >> 2, 255).astype(np.uint8) for p in (y, uv))
         want[s.last_pts] = native.nv12_to_bgr_cpu(y, uv, 0, 0, w, h)
@@ -39,9 +43,13 @@ def run_camera(native, device, w, h, n, **kw):
         assert got.shape == (h, w, 3)
         ref = want[meta["pts"]]
         assert np.array_equal(got, ref), f"pts {meta['pts']}: {int((got != ref).sum())} samples differ"
+        # the reconstruction itself at full depth (Main10: before the 8-bit narrowing)
+        ys = check_surface(wk, cam, meta["pts"], full, w, h)
+        low_bits |= ys.dtype == np.uint16 and bool((ys & 3).any())
         published += 1
     st = wk.stats(cam)
     assert st["decoder"] == "general"
+    assert kw.get("bit_depth", 8) == 8 or published == 0 or low_bits, "no sample below the 8-bit grid"
     return published
 
 
