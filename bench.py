@@ -122,10 +122,12 @@ def parse_args():
                     help="GPU runs: after the measurement, rank 0 runs the same cameras / steps / clients "
                          "through the reference-equivalent CPU path on its host domain's CPUs and reports "
                          "reference_equivalent_cpu_fps and vs_baseline = value / (that x ranks)")
-    ap.add_argument("--source", choices=["replay", "rtsp"], default="rtsp",
+    ap.add_argument("--source", choices=["replay", "rtsp", "records"], default="rtsp",
                     help="replay = pre-encoded AUs fed to the decode pipeline (decode-only); rtsp = an "
                          "in-process loopback RTSP camera farm, unthrottled, with the production "
-                         "ingest (RtspClient + RTP depacketizer + lazy decoder) inside the timed loop")
+                         "ingest (RtspClient + RTP depacketizer + lazy decoder) inside the timed loop; "
+                         "records = the GPU-side ceiling: every camera's GOPs parsed once up front and the "
+                         "reconstruction jobs (records) replayed into the GPU lanes, no host parse in the loop")
     ap.add_argument("--rtmp", action="store_true",
                     help="BASELINE config 5: every camera's RTMP pass-through on, to a loopback RTMP server "
                          "(rtsp source)")
@@ -850,7 +852,8 @@ def main():
     if a.source == "rtsp":
         return run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compressed, pool)
     rb = vep.ReplayBench(worker, cams, cfg, cached_frames=a.gop * a.cache_gops, threads=a.threads,
-                         ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window)
+                         ring_slots=a.ring_slots, prefix=f"r{rank}cam", window=a.parse_window,
+                         records=a.source == "records")
 
     # The native worker keeps up to `worker.inflight` ticks per lane launched but unpublished,
     # and one all-gather may still be reading an older tick: inflight + 2 consumer buffers.
@@ -1003,8 +1006,12 @@ def main():
             },
             "rocdecode_available": bool(vep.rocdecode_available()),
             "decoder_backend": decoder_backend(a, compressed),
-            "source": "replay (decode-only: pre-encoded access units fed to the parse pool; no RTSP "
-                      "receive / depacketization in the timed region)",
+            "source": ("records (GPU-side ceiling: each camera's looped GOPs parsed once before the timed "
+                       "region; the timed loop replays the parsed reconstruction jobs - records gathered over "
+                       "PCIe, GPU reconstruction, BGR24, ring publish, letterbox - with no host parse)"
+                       if a.source == "records" else
+                       "replay (decode-only: pre-encoded access units fed to the parse pool; no RTSP "
+                       "receive / depacketization in the timed region)"),
             "per_gpu_fps": round(fps / max(world, 1), 2),
             "frames_published": frames,
             "frames_launched": launched,

@@ -1553,14 +1553,14 @@ PYBIND11_MODULE(_vep, m) {
 
   py::class_<ReplayBench>(m, "ReplayBench")
       .def(py::init([](Worker& w, int ncams, const SynthConfig& cfg, int cached, int threads,
-                       int ring_slots, const std::string& prefix, int window) {
+                       int ring_slots, const std::string& prefix, int window, bool records) {
              py::gil_scoped_release r;
              return std::make_unique<ReplayBench>(w, ncams, cfg, cached, threads, ring_slots, prefix,
-                                                  window);
+                                                  window, records);
            }),
            py::arg("worker"), py::arg("ncams"), py::arg("cfg"), py::arg("cached_frames") = 30,
            py::arg("threads") = 8, py::arg("ring_slots") = 2, py::arg("prefix") = "cam",
-           py::arg("window") = 2, py::keep_alive<1, 2>())
+           py::arg("window") = 2, py::arg("records") = false, py::keep_alive<1, 2>())
       .def("step", &ReplayBench::step, py::call_guard<py::gil_scoped_release>())
       .def("parse_only_ms", &ReplayBench::parse_only_ms, py::call_guard<py::gil_scoped_release>())
       .def("drain", &ReplayBench::drain, py::call_guard<py::gil_scoped_release>())

@@ -9,8 +9,8 @@
 namespace vep {
 
 ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cached_frames,
-                         int threads, int ring_slots, const std::string& prefix, int window)
-    : w_(w), window_(std::max(1, window)) {
+                         int threads, int ring_slots, const std::string& prefix, int window, bool records)
+    : w_(w), window_(std::max(1, window)), records_(records) {
   VEP_CHECK(ncams > 0, "bench needs at least one camera");
   const int gop = std::max(1, base.gop);
   const int nframes = std::max(gop, (cached_frames + gop - 1) / gop * gop);
@@ -44,6 +44,36 @@ ReplayBench::ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cach
   cam_tick_.assign(size_t(ncams), 0);
   cam_busy_.assign(size_t(ncams), 0);
   cam_thread_.assign(size_t(ncams), -1);
+  if (records_) {  // parse everything now (two cycles, keep the second): no parse threads
+    rec_.resize(size_t(ncams));
+    rec_pos_.assign(size_t(ncams), 0);
+    ThreadPool parse_pool(std::max(1, threads));
+    parse_pool.parallel_for(ncams, [&](int i) {
+      auto cam = w_.camera(cams_[size_t(i)]);
+      const auto& v = aus_[size_t(i)];
+      for (int cycle = 0; cycle < 2; ++cycle)
+        for (const AuPtr& au : v) {
+          DecodeJob job;
+          bool ok = false;
+          try {
+            ok = cam && cam->make_job(au, job);
+          } catch (const std::exception&) {
+            ok = false;
+          }
+          if (cycle == 1 && ok) rec_[size_t(i)].push_back(std::move(job));
+        }
+      VEP_CHECK(!rec_[size_t(i)].empty(), "records replay: no job parsed");
+    });
+    // one untimed cycle: the IDR of the first replayed cycle outputs the previous cycle's last
+    // pictures from the reorder buffer, so those must have been reconstructed once
+    size_t longest = 0;
+    for (const auto& r : rec_) longest = std::max(longest, r.size());
+    for (size_t k = 0; k < longest; ++k) step();
+    w_.complete_all();
+    frames_ = bytes_ = 0;
+    batch_us_ = 0;
+    return;
+  }
   for (int i = 0; i < std::max(1, threads); ++i) workers_.emplace_back([this, i] {
     name_thread("vep-bparse");
     parse_loop(i);
@@ -143,6 +173,7 @@ std::vector<DecodeJob> ReplayBench::take(bool timed) {
 }
 
 double ReplayBench::parse_only_ms(int ticks) {
+  VEP_CHECK(!records_, "parse_only_ms: records mode has no parse");
   drain();
   const i64 t0 = mono_us();
   for (int t = 0; t < ticks; ++t) (void)take(false);
@@ -150,6 +181,10 @@ double ReplayBench::parse_only_ms(int ticks) {
 }
 
 void ReplayBench::quiesce() {
+  if (records_) {
+    w_.complete_all();
+    return;
+  }
   i64 upto;
   {
     std::unique_lock<std::mutex> g(mu_);
@@ -178,6 +213,22 @@ void ReplayBench::quiesce() {
 }
 
 void ReplayBench::step() {
+  if (records_) {  // the next recorded job of every camera (a copy: the records are shared)
+    std::vector<DecodeJob> jobs;
+    jobs.reserve(rec_.size());
+    for (size_t c = 0; c < rec_.size(); ++c) {
+      jobs.push_back(rec_[c][rec_pos_[c]]);
+      rec_pos_[c] = (rec_pos_[c] + 1) % rec_[c].size();
+    }
+    for (auto& j : jobs)
+      for (const auto& p : j.avc) bytes_ += u64(p->coefs.size()) * 2 + p->mbs.size() * sizeof(avc::MbRec);
+    const i64 t0 = mono_us();
+    const size_t n = jobs.size();
+    w_.launch_async(jobs);
+    batch_us_ += double(mono_us() - t0);
+    frames_ += n;
+    return;
+  }
   {
     std::lock_guard<std::mutex> g(mu_);
     if (gate_ != INT64_MAX) gate_ = INT64_MAX;  // re-open parsing (after quiesce)

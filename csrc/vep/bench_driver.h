@@ -20,8 +20,13 @@ namespace vep {
 
 class ReplayBench {
  public:
+  // records = true: the GPU-side ceiling (bench.py --source records). Every camera's cached
+  // access units are parsed up front — two passes over the GOPs, the second one kept, so its
+  // jobs carry the steady-state DPB / output bookkeeping of a looped stream — and step()
+  // replays those reconstruction jobs (records in pinned memory, gathered over PCIe by the GPU
+  // as in the live path) with no host parse in the loop.
   ReplayBench(Worker& w, int ncams, const SynthConfig& base, int cached_frames, int threads,
-              int ring_slots, const std::string& prefix, int window = 2);
+              int ring_slots, const std::string& prefix, int window = 2, bool records = false);
   ~ReplayBench();
   void step();      // takes the next parsed tick and launches it (publishes tick t - stages)
   void drain();     // publish every launched tick
@@ -72,6 +77,10 @@ class ReplayBench {
   std::vector<std::thread> workers_;
   u64 frames_ = 0, bytes_ = 0, parse_fail_ = 0;
   std::atomic<u64> stream_bytes_{0}, stream_frames_{0}, parse_ns_{0};
+  // records mode: per camera the parsed jobs of one cycle of its GOPs, replayed in order
+  bool records_ = false;
+  std::vector<std::vector<DecodeJob>> rec_;
+  std::vector<size_t> rec_pos_;
   double wait_us_ = 0, batch_us_ = 0;
 };
 
