@@ -25,7 +25,7 @@ void bind_rpc(py::module_& m) {
       .def(py::init([](const std::string& host, int port, const std::string& bus_tag, int io_threads,
                        int wait_threads, int slow_threads, py::object handler, bool reuseport,
                        int stream_deadline_ms, u32 max_streams, u32 max_queued_requests,
-                       u32 max_resets_per_s) {
+                       u32 max_resets_per_s, bool zero_copy) {
              rpc::ServerOptions o;
              o.host = host;
              o.port = port;
@@ -38,6 +38,7 @@ void bind_rpc(py::module_& m) {
              o.max_streams = max_streams;
              o.max_queued_requests = max_queued_requests;
              o.max_resets_per_s = max_resets_per_s;
+             o.zero_copy = zero_copy;
              rpc::SlowHandler h;
              if (!handler.is_none()) {
                // (the callable is released with the GIL held, whichever thread drops it last)
@@ -61,7 +62,7 @@ void bind_rpc(py::module_& m) {
            py::arg("host") = "0.0.0.0", py::arg("port") = 0, py::arg("bus_tag") = "", py::arg("io_threads") = 2,
            py::arg("wait_threads") = 256, py::arg("slow_threads") = 8, py::arg("handler") = py::none(),
            py::arg("reuseport") = true, py::arg("stream_deadline_ms") = 15000, py::arg("max_streams") = 1000,
-           py::arg("max_queued_requests") = 16, py::arg("max_resets_per_s") = 200,
+           py::arg("max_queued_requests") = 16, py::arg("max_resets_per_s") = 200, py::arg("zero_copy") = true,
            "Native gRPC endpoint: VideoLatestImage from the frame bus `bus_tag`; the other Image methods "
            "call handler(method, request_bytes, peer) -> (status, message, [response_bytes, ...])")
       .def_property_readonly("port", &rpc::Server::port)
@@ -83,6 +84,8 @@ void bind_rpc(py::module_& m) {
         d["refused_streams"] = st.refused_streams;
         d["cancelled_waits"] = st.cancelled_waits;
         d["deadline_streams"] = st.deadline_streams;
+        d["zero_copy_frames"] = st.zero_copy_frames;
+        d["slow_readers"] = st.slow_readers;
         d["p50_ms"] = st.p50_ms;
         d["p99_ms"] = st.p99_ms;
         return d;

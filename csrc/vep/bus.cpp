@@ -312,8 +312,25 @@ void Owner::pump() {
         const std::string pre = encode_video_frame(probe, n, names_[i]).first;
         if (!ensure_data(int(i), pre.size() + n + video_frame_suffix_max(names_[i]))) continue;
         const u64 cap = e.slot_cap.load();
-        const int slot = e.bus_seq.load() == 0 ? 0 : int((e.newest.load() + 1) % kSlots);
-        e.slots[slot].version.fetch_add(1, std::memory_order_acq_rel);  // odd: being written
+        // the next slot after the newest that no reader holds a lease on (marked odd first,
+        // then the leases checked: see SlotHdr)
+        int slot = -1;
+        const bool none = e.bus_seq.load() == 0;
+        const int newest = int(e.newest.load() % kSlots);
+        for (int d = none ? 0 : 1; d < kSlots && slot < 0; ++d) {
+          const int k = (newest + d) % kSlots;
+          SlotHdr& s = e.slots[k];
+          s.version.fetch_add(1, std::memory_order_seq_cst);  // odd: being written
+          if (s.leases.load(std::memory_order_seq_cst) > 0 && mono_ms() < s.lease_until.load(std::memory_order_acquire)) {
+            s.version.fetch_add(1, std::memory_order_acq_rel);  // (even again: untouched)
+            continue;
+          }
+          slot = k;
+        }
+        if (slot < 0) {  // every other slot is being sent by some reader: the next pass retries
+          lease_skips_.fetch_add(1);
+          continue;
+        }
         u8* dst = data_[i].base() + size_t(slot) * cap;
         std::memcpy(dst, pre.data(), pre.size());
         jobs.push_back({int(i), slot, pre.size(), names_[i], ring, c, data_[i].map});
@@ -579,6 +596,70 @@ i64 Reader::newest_seq(const Ticket& t) const {
   return e.bus_seq.load(std::memory_order_acquire);
 }
 
+// The camera's data segment of generation dg, mapped once per reader (null: replaced meanwhile).
+std::shared_ptr<void> Reader::data_map(const std::shared_ptr<Seg>& seg, int cam, u32 gen, u32 dg, u64 scap) {
+  std::lock_guard<std::mutex> g(mu_);
+  const std::string key = seg->path + "/" + std::to_string(cam);
+  auto it = data_.find(key);
+  if (it == data_.end() || it->second.data_gen != dg || it->second.cam_gen != gen) {
+    if (it != data_.end()) data_.erase(it);  // the camera's older segment: unmapped
+    const std::string path = seg->path + ".c" + std::to_string(cam) + ".g" + std::to_string(dg);
+    auto m = std::make_shared<DataSeg>();
+    m->bytes = size_t(scap) * kSlots;
+    m->base = static_cast<const u8*>(map_file(path, m->bytes, false, false));
+    if (!m->base) return nullptr;
+    data_[key] = DataMap{seg->path, cam, dg, gen, m};
+  }
+  return data_[key].map;
+}
+
+std::shared_ptr<const Reader::Lease> Reader::lease(const Ticket& t) {
+  auto seg = std::static_pointer_cast<Seg>(t.seg);
+  CamEntry& e = seg->hdr->cams[t.cam];
+  for (int attempt = 0; attempt < 8; ++attempt) {
+    if (!e.live.load(std::memory_order_acquire) || e.gen.load(std::memory_order_acquire) != t.gen) return nullptr;
+    const u32 dg = e.data_gen.load(std::memory_order_acquire);
+    const u64 scap = e.slot_cap.load(std::memory_order_acquire);
+    if (dg == 0 || scap == 0) return nullptr;
+    std::shared_ptr<DataSeg> ds = std::static_pointer_cast<DataSeg>(data_map(seg, t.cam, t.gen, dg, scap));
+    if (!ds) continue;
+    const u32 k = e.newest.load(std::memory_order_acquire) % kSlots;
+    SlotHdr& s = e.slots[k];
+    s.leases.fetch_add(1, std::memory_order_seq_cst);
+    const i64 now = mono_ms();
+    i64 until = s.lease_until.load(std::memory_order_relaxed);
+    while (until < now + kLeaseMs && !s.lease_until.compare_exchange_weak(until, now + kLeaseMs)) {
+    }
+    const u64 v = s.version.load(std::memory_order_seq_cst);
+    const i64 sq = s.seq.load(std::memory_order_acquire);
+    const u64 len = s.len.load(std::memory_order_acquire);
+    if ((v & 1) || sq <= t.after || len == 0 || len > scap || e.data_gen.load(std::memory_order_acquire) != dg) {
+      s.leases.fetch_sub(1, std::memory_order_acq_rel);
+      if (!(v & 1) && sq <= t.after) return nullptr;
+      continue;
+    }
+    // the lease object keeps both segments mapped and gives the slot back when dropped
+    struct Held {
+      Lease l;
+      std::shared_ptr<Seg> seg;
+      std::shared_ptr<DataSeg> ds;
+      SlotHdr* s;
+      ~Held() { s->leases.fetch_sub(1, std::memory_order_acq_rel); }
+    };
+    auto h = std::make_shared<Held>();
+    h->l.data = ds->base + size_t(k) * scap;
+    h->l.len = size_t(len);
+    h->l.seq = sq;
+    h->l.taken_ms = now;
+    h->seg = seg;
+    h->ds = ds;
+    h->s = &s;
+    leases_taken_.fetch_add(1);
+    return std::shared_ptr<const Lease>(h, &h->l);
+  }
+  return nullptr;
+}
+
 size_t Reader::copy(const Ticket& t, u8* dst, size_t cap, i64* seq) {
   auto seg = std::static_pointer_cast<Seg>(t.seg);
   CamEntry& e = seg->hdr->cams[t.cam];
@@ -587,22 +668,8 @@ size_t Reader::copy(const Ticket& t, u8* dst, size_t cap, i64* seq) {
     const u32 dg = e.data_gen.load(std::memory_order_acquire);
     const u64 scap = e.slot_cap.load(std::memory_order_acquire);
     if (dg == 0 || scap == 0) return 0;
-    std::shared_ptr<DataSeg> ds;
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      const std::string key = seg->path + "/" + std::to_string(t.cam);
-      auto it = data_.find(key);
-      if (it == data_.end() || it->second.data_gen != dg || it->second.cam_gen != t.gen) {
-        if (it != data_.end()) data_.erase(it);  // the camera's older segment: unmapped
-        const std::string path = seg->path + ".c" + std::to_string(t.cam) + ".g" + std::to_string(dg);
-        auto m = std::make_shared<DataSeg>();
-        m->bytes = size_t(scap) * kSlots;
-        m->base = static_cast<const u8*>(map_file(path, m->bytes, false, false));
-        if (!m->base) continue;  // (replaced meanwhile)
-        data_[key] = DataMap{seg->path, t.cam, dg, t.gen, m};
-      }
-      ds = std::static_pointer_cast<DataSeg>(data_[key].map);
-    }
+    std::shared_ptr<DataSeg> ds = std::static_pointer_cast<DataSeg>(data_map(seg, t.cam, t.gen, dg, scap));
+    if (!ds) continue;  // (replaced meanwhile)
     const u32 k = e.newest.load(std::memory_order_acquire);
     const SlotHdr& s = e.slots[k % kSlots];
     const u64 v1 = s.version.load(std::memory_order_acquire);

@@ -18,8 +18,10 @@
 //  * Reader (a serving process; no GPU context): maps every owner's control segment of the tag,
 //    finds a camera by name, writes its demand (last_query / keyframe-only: the reference's
 //    HSET last_access_time_<dev> / SET is_key_frame_only_<dev>, grpc_api.go:159-175), and copies
-//    the newest bus slot out (one copy, into the bytes object grpcio sends). Every client of a
-//    camera, in every serving process, shares the one DMA of a frame.
+//    the newest bus slot out (one copy, into the bytes object grpcio sends), or takes a *lease*
+//    on it (the native endpoint, rpcsrv.h): the owner does not rewrite a leased slot, so the
+//    server writev()s the frame straight from shared memory with no copy at all. Every client of
+//    a camera, in every serving process, shares the one DMA of a frame.
 //
 // Futexes on MAP_SHARED memory wake across processes; all shared words are lock-free atomics.
 #pragma once
@@ -41,14 +43,22 @@ class Camera;
 
 namespace bus {
 
-constexpr u64 kMagic = 0x31737562706576ull;  // "vepbus1"
+constexpr u64 kMagic = 0x32737562706576ull;  // "vepbus2"
 constexpr int kNameLen = 96;
-constexpr int kSlots = 3;
+constexpr int kSlots = 4;  // newest + slots readers may still hold leases on + the one being written
+// A lease pins a slot for at most this long (a reader that died holding one frees it then); the
+// native endpoint closes a connection whose leased bytes are still unsent after kLeaseSendMs.
+constexpr i64 kLeaseMs = 30000, kLeaseSendMs = 20000;
 
 struct alignas(64) SlotHdr {
   std::atomic<u64> version;  // odd while the owner writes the slot
   std::atomic<i64> seq;      // ring sequence of the frame in it
   std::atomic<u64> len;      // serialized VideoFrame bytes
+  // Readers sending straight from the slot (Reader::lease). The owner marks a slot odd, then
+  // checks `leases` (seq_cst); a reader increments `leases`, then checks `version` (seq_cst): one
+  // of the two always sees the other, so a leased slot is never rewritten.
+  std::atomic<u32> leases;
+  std::atomic<i64> lease_until;  // monotonic ms after which the leases are stale (dead reader)
 };
 
 struct alignas(64) CamEntry {
@@ -101,6 +111,7 @@ class Owner {
   const std::string& path() const { return path_; }
   u64 published() const { return hdr_->published.load(); }
   u64 dma_bytes() const { return dma_bytes_.load(); }
+  u64 lease_skips() const { return lease_skips_.load(); }  // publishes deferred: every other slot leased
 
  private:
   // One camera's data segment. Reference-counted: the pump holds a reference while its DMA
@@ -138,7 +149,7 @@ class Owner {
   std::mutex mu_;  // names_ / data_ against add / remove
   std::thread th_;
   std::atomic<bool> stop_{false};
-  std::atomic<u64> dma_bytes_{0};
+  std::atomic<u64> dma_bytes_{0}, lease_skips_{0};
 };
 
 // ---------------------------------------------------------------------------- reader side
@@ -172,6 +183,17 @@ class Reader {
   // Sequence of the newest bus frame of the ticket's camera (a caller that already holds that
   // frame's bytes skips the copy).
   i64 newest_seq(const Ticket& t) const;
+  // A lease on the newest bus frame with seq > t.after: its bytes in shared memory, not
+  // rewritten while the lease lives (up to kLeaseMs), so a server sends them with no copy.
+  // Null when there is none (or the camera went away). The lease keeps the segments mapped.
+  struct Lease {
+    const u8* data = nullptr;
+    size_t len = 0;
+    i64 seq = 0;
+    i64 taken_ms = 0;  // monotonic ms
+  };
+  std::shared_ptr<const Lease> lease(const Ticket& t);
+  u64 leases_taken() const { return leases_taken_.load(); }
   // Demand only.
   bool touch(const std::string& name, int key_frame_only);
   struct Info {
@@ -211,7 +233,8 @@ class Reader {
   std::unordered_map<std::string, DataMap> data_;
   void prune_data_locked();
   i64 last_scan_ms_ = 0;
-  std::atomic<u64> rescans_{0};
+  std::atomic<u64> rescans_{0}, leases_taken_{0};
+  std::shared_ptr<void> data_map(const std::shared_ptr<Seg>& seg, int cam, u32 gen, u32 dg, u64 scap);
 };
 
 // Removes the bus segments a (dead) process left in /dev/shm. Returns how many.

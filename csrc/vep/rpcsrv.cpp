@@ -381,12 +381,29 @@ bool parse_frame_request(const std::string& m, std::string& dev, bool& kfo) {
   return true;
 }
 
-using Buf = std::shared_ptr<const std::string>;
-
+// A byte range kept alive by `keep`: an output string, or a leased bus slot (lease_ms > 0: the
+// bytes live in the frame bus's shared memory, taken then; see bus::Reader::lease).
 struct Chunk {
-  Buf owner;
-  size_t off = 0, len = 0;
+  std::shared_ptr<const void> keep;
+  const char* p = nullptr;
+  size_t len = 0;
+  i64 lease_ms = 0;
 };
+// One gRPC message (5-byte prefix included) as one or more ranges.
+struct Msg {
+  std::vector<Chunk> parts;
+  size_t size = 0;
+  i64 lease_ms = 0;
+};
+using Buf = std::shared_ptr<const Msg>;
+
+Buf make_msg(std::string s) {
+  auto str = std::make_shared<const std::string>(std::move(s));
+  auto m = std::make_shared<Msg>();
+  m->parts.push_back(Chunk{str, str->data(), str->size(), 0});
+  m->size = str->size();
+  return m;
+}
 
 enum class Kind { kFrame, kSlow, kUnknown };
 
@@ -478,11 +495,11 @@ struct Server::Impl {
   std::mutex cache_mu;
   std::condition_variable cache_cv;
   std::unordered_map<std::string, Cached> cache;
-  Buf empty_msg = std::make_shared<const std::string>(std::string(5, '\0'));
+  Buf empty_msg = make_msg(std::string(5, '\0'));
 
   // stats
   std::atomic<u64> n_conn{0}, n_open{0}, n_streams{0}, n_frames{0}, n_empty{0}, n_bytes{0}, n_slow{0}, n_copies{0},
-      n_proto{0}, n_goaway{0}, n_refused{0}, n_cancelled{0}, n_deadline{0};
+      n_proto{0}, n_goaway{0}, n_refused{0}, n_cancelled{0}, n_deadline{0}, n_leased{0}, n_slow_readers{0};
   mutable std::mutex lat_mu;
   std::vector<float> lat;
   size_t lat_next = 0;
@@ -747,7 +764,7 @@ struct Server::Impl {
   void queue(Conn& c, std::string s) {
     auto b = std::make_shared<const std::string>(std::move(s));
     c.out_bytes += b->size();
-    c.out.push_back(Chunk{b, 0, b->size()});
+    c.out.push_back(Chunk{b, b->data(), b->size(), 0});
   }
 
   void flush(Loop& L, Conn& c) {
@@ -755,7 +772,7 @@ struct Server::Impl {
       iovec iov[256];
       int k = 0;
       for (auto it = c.out.begin(); it != c.out.end() && k < 256; ++it, ++k) {
-        iov[k].iov_base = const_cast<char*>(it->owner->data() + it->off);
+        iov[k].iov_base = const_cast<char*>(it->p);
         iov[k].iov_len = it->len;
       }
       const ssize_t w = ::writev(c.fd, iov, k);
@@ -771,7 +788,7 @@ struct Server::Impl {
       while (left > 0) {
         Chunk& f = c.out.front();
         const size_t t = std::min(left, f.len);
-        f.off += t;
+        f.p += t;
         f.len -= t;
         left -= t;
         if (f.len == 0) c.out.pop_front();
@@ -856,9 +873,9 @@ struct Server::Impl {
           std::string h;
           frame_hdr(h, u32(n), kData, 0, s.id);
           queue(c, std::move(h));
-          c.out.push_back(Chunk{m.owner, m.off, n});
+          c.out.push_back(Chunk{m.keep, m.p, n, m.lease_ms});
           c.out_bytes += n;
-          m.off += n;
+          m.p += n;
           m.len -= n;
           c.conn_send_win -= i64(n);
           s.send_win -= i64(n);
@@ -881,7 +898,7 @@ struct Server::Impl {
 
   void respond(Conn& c, Stream& s, const Buf& msg) {
     if (!s.headers_sent) send_headers(c, s);
-    s.pending.push_back(Chunk{msg, 0, msg->size()});
+    for (const Chunk& part : msg->parts) s.pending.push_back(part);
   }
 
   void finish(Conn& c, Stream& s, int status, const std::string& message) {
@@ -1284,7 +1301,7 @@ struct Server::Impl {
               std::string w(5, '\0');
               const u32 n = u32(m.size());
               w[1] = char(n >> 24), w[2] = char(n >> 16), w[3] = char(n >> 8), w[4] = char(n);
-              respond(*cc, st, std::make_shared<const std::string>(w + m));
+              respond(*cc, st, make_msg(w + m));
             }
           finish(*cc, st, rp->status, rp->message);
           pump(L, *cc);
@@ -1338,6 +1355,18 @@ struct Server::Impl {
     });
   }
 
+  // Output still pointing into a bus slot whose lease is about to lapse (the owner may then rewrite
+  // it): the oldest chunks of the connection and of every stream.
+  static bool stale_lease(const Conn& c, i64 now) {
+    auto old = [&](const Chunk& k) { return k.lease_ms > 0 && now - k.lease_ms > bus::kLeaseSendMs; };
+    int n = 0;
+    for (auto it = c.out.begin(); it != c.out.end() && n < 8; ++it, ++n)
+      if (old(*it)) return true;
+    for (const auto& [sid, s] : c.streams)
+      if (!s.pending.empty() && old(s.pending.front())) return true;
+    return false;
+  }
+
   // Streams past their deadline with no job running end with DEADLINE_EXCEEDED (the reference's
   // 15 s context on the whole stream, grpc_api.go:135-137), whether or not requests arrive.
   void sweep(Loop& L) {
@@ -1348,6 +1377,11 @@ struct Server::Impl {
     for (auto& cp : cs) {
       Conn& c = *cp;
       if (c.fd < 0) continue;
+      if (stale_lease(c, now)) {  // leased bytes unsent for kLeaseSendMs: a client that does not read
+        n_slow_readers.fetch_add(1);
+        close_conn(L, c);
+        continue;
+      }
       bool any = false;
       for (auto& [sid, s] : c.streams)
         if (!s.inflight && !s.trailers_queued && now - s.t0_ms > opt.stream_deadline_ms) {
@@ -1399,7 +1433,9 @@ struct Server::Impl {
           Cached& e = cache[dev];
           // another waiter is copying this frame: take its copy (bounded: a copy is a memcpy)
           cache_cv.wait_for(g, std::chrono::milliseconds(200), [&] { return e.copying != ns || e.seq >= ns; });
-          if (e.seq >= ns && e.seq > after && e.msg) {
+          // (a cached leased frame is reused only well inside its lease)
+          const bool fresh = !e.msg || !e.msg->lease_ms || now_ms_mono() - e.msg->lease_ms < bus::kLeaseSendMs / 2;
+          if (e.seq >= ns && e.seq > after && e.msg && fresh) {
             const i64 s = e.seq;
             Buf b = e.msg;
             g.unlock();
@@ -1409,15 +1445,31 @@ struct Server::Impl {
           }
           e.copying = ns;
         }
-        auto m = std::make_shared<std::string>(t.cap + 5, '\0');
         i64 seq = 0;
-        const size_t n = reader.copy(t, reinterpret_cast<u8*>(&(*m)[5]), t.cap, &seq);
         Buf b;
-        if (n > 0) {
-          m->resize(n + 5);
-          (*m)[1] = char(n >> 24), (*m)[2] = char(n >> 16), (*m)[3] = char(n >> 8), (*m)[4] = char(n);
-          b = m;
-          n_copies.fetch_add(1);
+        if (opt.zero_copy) {  // a lease: DATA frames point into the bus slot, no copy
+          if (auto l = reader.lease(t)) {
+            const size_t n = l->len;
+            auto pre = std::make_shared<const std::string>(
+                std::string{'\0', char(n >> 24), char(n >> 16), char(n >> 8), char(n)});
+            auto m = std::make_shared<Msg>();
+            m->parts.push_back(Chunk{pre, pre->data(), 5, 0});
+            m->parts.push_back(Chunk{l, reinterpret_cast<const char*>(l->data), n, l->taken_ms});
+            m->size = 5 + n;
+            m->lease_ms = l->taken_ms;
+            seq = l->seq;
+            b = m;
+            n_leased.fetch_add(1);
+          }
+        } else {
+          auto m = std::make_shared<std::string>(t.cap + 5, '\0');
+          const size_t n = reader.copy(t, reinterpret_cast<u8*>(&(*m)[5]), t.cap, &seq);
+          if (n > 0) {
+            m->resize(n + 5);
+            (*m)[1] = char(n >> 24), (*m)[2] = char(n >> 16), (*m)[3] = char(n >> 8), (*m)[4] = char(n);
+            b = make_msg(std::move(*m));
+            n_copies.fetch_add(1);
+          }
         }
         {
           std::lock_guard<std::mutex> g(cache_mu);
@@ -1487,6 +1539,8 @@ ServerStats Server::stats() const {
   s.refused_streams = p_->n_refused.load();
   s.cancelled_waits = p_->n_cancelled.load();
   s.deadline_streams = p_->n_deadline.load();
+  s.zero_copy_frames = p_->n_leased.load();
+  s.slow_readers = p_->n_slow_readers.load();
   std::vector<float> v;
   {
     std::lock_guard<std::mutex> g(p_->lat_mu);

@@ -50,6 +50,9 @@ struct ServerOptions {
   int wait_attempts = 3;           // grpc_api.go:187 (XREAD BLOCK 1 s, 3 attempts)
   int wait_block_ms = 1000;
   size_t max_cursors = 65536;
+  // Send frames straight from the frame bus's shared memory under a slot lease (bus.h) instead of
+  // copying each new frame once per serving process.
+  bool zero_copy = true;
   // Protocol limits (what grpc-go's server bounds for the reference, server/main.go:142-153).
   // Violations end the connection with GOAWAY (or refuse / fail the one stream) before any
   // unbounded buffering happens.
@@ -72,6 +75,8 @@ struct ServerStats {
   u64 refused_streams = 0;   // RST_STREAM REFUSED_STREAM (over max_streams)
   u64 cancelled_waits = 0;   // frame waits ended early because the client reset the stream
   u64 deadline_streams = 0;  // streams ended with DEADLINE_EXCEEDED
+  u64 zero_copy_frames = 0;  // frames sent straight from a leased bus slot (no copy)
+  u64 slow_readers = 0;      // connections closed with leased bytes unsent for bus::kLeaseSendMs
   double p50_ms = 0, p99_ms = 0;  // request received -> response queued (recent requests)
 };
 

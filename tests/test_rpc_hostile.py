@@ -21,6 +21,7 @@ import struct
 import threading
 import time
 
+import numpy as np
 import pytest
 
 from conftest import synth
@@ -165,6 +166,10 @@ def server(native):
         srv.stop()
         o.stop()
         w.stop()
+    made.clear()  # (the owners' destructors unlink their bus segments)
+    import gc
+
+    gc.collect()
 
 
 def _rss_mb():
@@ -301,19 +306,53 @@ def test_idle_stream_hits_deadline(server):
 
 
 def test_small_window_stops_and_resumes_data(server, native):
+    """A client with a 1000-byte window holds its (zero-copy, leased) frame half-sent while other
+    clients pull five newer frames through the same bus: the owner writes them around the leased
+    slot, and the stalled frame, once the window opens, arrives intact (the bytes of its pts)."""
+    from video_edge_ai_proxy_amd.proto import pb
+    from video_edge_ai_proxy_amd.server.grpc_server import ImageClient
+
     srv, w, o = server()
     cam = w.add_camera("camW", 3)
     o.add(cam, "camW")
-    enc = synth(native, 320, 240, gop=5)
-    w.decode_now(cam, enc.next())
+    enc, ref = synth(native, 320, 240, gop=5), native.CpuDecoder()
+    want = {}
+
+    def decode():  # (the synthetic camera stamps AU k with pts k * 3000: 90 kHz at 30 fps)
+        au = enc.next()
+        img = ref.decode(au)
+        w.decode_now(cam, au)
+        want[len(want) * 3000] = img
+
+    decode()
     c = H2(srv.port, window=1000)
     c.send(frame(HEADERS, END_HEADERS, 1, request_block()) + frame(DATA, END_STREAM, 1, frame_request("camW")))
-    got = sum(len(p) for t, fl, sid, p in c.frames(2.0) if t == DATA)
-    assert got == 1000  # the stream window (the connection window is 64 KiB)
+    data = b"".join(p for t, fl, sid, p in c.frames(2.0) if t == DATA)
+    assert len(data) == 1000  # the stream window (the connection window is 64 KiB)
+    cli = ImageClient(f"127.0.0.1:{srv.port}")
+    try:
+        for _ in range(5):  # newer frames through the bus while the lease is held
+            th_frame = {}
+            import threading
+
+            th = threading.Thread(target=lambda: th_frame.setdefault("vf", cli.latest_frame("camW", timeout=10)))
+            th.start()
+            time.sleep(0.15)
+            decode()
+            th.join(timeout=10)
+            assert th_frame["vf"].width == 320
+    finally:
+        cli.close()
     c.send(frame(WINUPD, 0, 1, struct.pack(">I", 1 << 24)) + frame(WINUPD, 0, 0, struct.pack(">I", 1 << 24)))
     fs = c.frames(5.0, until=lambda f: f[0] == HEADERS and f[1] & END_STREAM)
-    got += sum(len(p) for t, fl, sid, p in fs if t == DATA)
-    assert got > 320 * 240 * 3 and trailers_status(fs[-1][3]) == 0
+    data += b"".join(p for t, fl, sid, p in fs if t == DATA)
+    assert trailers_status(fs[-1][3]) == 0
+    n = struct.unpack(">I", data[1:5])[0]
+    vf = pb.VideoFrame.FromString(data[5:5 + n])
+    img = np.frombuffer(vf.data, np.uint8).reshape(240, 320, 3)
+    assert np.array_equal(img, want[vf.pts])  # not torn by the owner's newer writes
+    st = srv.stats()
+    assert st["zero_copy_frames"] >= 4 and st["frame_copies"] == 0
     c.close()
 
 
