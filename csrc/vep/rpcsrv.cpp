@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <list>
@@ -504,7 +505,10 @@ struct Server::Impl {
   std::vector<float> lat;
   size_t lat_next = 0;
 
-  Impl(const ServerOptions& o, SlowHandler s) : opt(o), slow(std::move(s)), reader(o.bus_tag) {}
+  Impl(const ServerOptions& o, SlowHandler s) : opt(o), slow(std::move(s)), reader(o.bus_tag) {
+    const char* z = std::getenv("VEP_RPC_ZERO_COPY");  // 0: copy each new frame (A/B)
+    if (z && z[0] == '0') opt.zero_copy = false;
+  }
 
   // ------------------------------------------------------------------ pools
   void pool_start(Pool& p, int n, const char* name) {

@@ -265,3 +265,13 @@ def test_cron_schedule_and_cleanup(tmp_path):
     time.sleep(0.6)
     job.stop()
     assert not new.exists() and job.runs >= 1
+
+
+def test_auto_serving_processes():
+    """serving.frontends -2: one serving process per GPU on multi-GPU nodes; on one GPU two when
+    8 CPUs remain beyond the GPU's 16-CPU decode share, else the main process serves."""
+    from video_edge_ai_proxy_amd.server.app import auto_frontends
+
+    assert auto_frontends(8, 256) == 8 and auto_frontends(2, 8) == 2
+    assert auto_frontends(1, 16) == 0 and auto_frontends(1, 23) == 0
+    assert auto_frontends(1, 24) == 2 and auto_frontends(1, 64) == 2

@@ -87,7 +87,8 @@ class ServingConfig:
     ``grpc_port`` with SO_REUSEPORT (the kernel spreads client connections over them); they read
     frames from the node's frame bus (shared memory, csrc/vep/bus.h) and forward the other RPCs to
     the main process. -1 = one per GPU; 0 = serve from the main process; -2 (default) = auto: one
-    per GPU when the node has more than one GPU, else the main process.
+    per GPU when the node has more than one GPU; on one GPU, two when the CPU budget has 8 CPUs
+    beyond the GPU's 16-CPU decode share (server/app.py auto_frontends), else the main process.
 
     ``native`` (default): VideoLatestImage is answered by the native HTTP/2 gRPC endpoint
     (csrc/vep/rpcsrv.h: C++, no interpreter lock, straight from the frame bus); the other methods

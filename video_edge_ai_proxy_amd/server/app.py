@@ -21,6 +21,7 @@ from ..services.edge import EdgeService
 from ..services.process_manager import ProcessManager
 from ..services.settings import SettingsManager
 from ..services.storage import Storage
+from ..utils import host_cpu_budget
 from .grpc_server import BusFrames, ImageService, serve
 from .metrics import Metrics
 from .rest import create_app
@@ -80,6 +81,22 @@ class HubApp:
         self.storage.close()
 
 
+# One GPU saturates its host parse on ~16 CPUs (the headline's host domain); CPUs beyond that
+# are spare, and 8 of them pay for two serving processes (their writev / TCP work then runs off the
+# decoding process's CPUs; docs/ROUND6.md).
+SERVING_SPARE_CPUS = 8
+DECODE_CPUS_PER_GPU = 16
+
+
+def auto_frontends(ngpu: int, budget: int) -> int:
+    """serving.frontends -2: one serving process per GPU on a multi-GPU node; on one GPU, two when
+    the CPU budget leaves SERVING_SPARE_CPUS beyond the GPU's decode share, else none (the main
+    process serves)."""
+    if ngpu > 1:
+        return ngpu
+    return 2 if budget - DECODE_CPUS_PER_GPU >= SERVING_SPARE_CPUS else 0
+
+
 def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = None,
               grpc_port: Optional[int] = None, devices=None, start_rest: bool = True,
               restore: bool = True) -> HubApp:
@@ -91,8 +108,8 @@ def build_app(cfg: Config, host: str = "0.0.0.0", rest_port: Optional[int] = Non
     # workers always do (the main process then serves from the bus too, without calling them).
     nfront = int(cfg.serving.frontends)
     ngpu = len(devices if devices is not None else (cfg.gpu.devices or _gpu_count()))
-    if nfront == -2:  # auto: serving processes on multi-GPU nodes
-        nfront = ngpu if ngpu > 1 else 0
+    if nfront == -2:  # auto: serving processes on multi-GPU nodes, and on one GPU with CPUs to spare
+        nfront = auto_frontends(ngpu, host_cpu_budget())
     elif nfront < 0:
         nfront = max(1, ngpu)
     # main-process serving through the native endpoint: it reads the frame bus
