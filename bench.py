@@ -611,6 +611,9 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
         farm.close()
         if pool is not None:
             pool.close()
+    backend = dist.get_backend() if world > 1 else None
+    if world > 1:  # (every collective is done; rank 0's reference-equivalent run needs none)
+        dist.destroy_process_group()
     if rank == 0:
         fps = pictures / elapsed
         res = {
@@ -626,7 +629,7 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
                                "decoded pictures per rank",
             "ms_per_step": round(elapsed / a.steps * 1e3, 4),
             "rccl_world": world if (use_gpu and world > 1) else 0,
-            "collective_backend": (dist.get_backend() if world > 1 else None),
+            "collective_backend": backend,
             "gather_verified": side.get("gather_check", {}).get("gather_verified") if world > 1 else None,
             "higher_is_better": True,
             "scaling": "weak",
@@ -698,8 +701,6 @@ def run_rtsp(a, vep, torch, dist, worker, world, rank, use_gpu, dev, row, compre
             res["source_definition"] = REF_CPU_DEFINITION
             res["ref_copy_bytes"] = worker.ref_copy_bytes
         print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
     if dropped or errors:
         print(f"bench: {dropped} frames dropped, {errors} decode errors in the timed region", file=sys.stderr,
               flush=True)
