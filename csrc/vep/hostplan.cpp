@@ -178,7 +178,8 @@ std::vector<HostDomain> plan_host_domains(const std::vector<int>& devices, const
       share = int((i64(d.cpus.size()) * budget + sum / 2) / std::max<i64>(1, sum));
     }
     d.cpu_share = std::max(1, share);
-    d.parse_threads = parse_env ? parse_env : std::max(1, d.cpu_share - (d.cpu_share >= 4 ? reserve : 0));
+    d.parse_threads = parse_env ? parse_env
+                                : std::max(1, d.cpu_share - (d.cpu_share >= 4 && d.cpu_share < 16 ? reserve : 0));
     d.io_threads = io_env ? io_env : (d.cpu_share >= 16 ? 2 : 1);
   }
   return out;

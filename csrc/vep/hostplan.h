@@ -49,7 +49,9 @@ std::vector<int> gpu_local_cpus(int device, int* numa_node = nullptr);
 //  * else (CPU backend, no sysfs) the affinity CPUs not claimed above, split evenly.
 // cpu_share is the set's size, or its proportional part of a cgroup quota smaller than the CPUs the
 // sets cover (a 16-CPU quota on a 256-CPU mask: one domain gets 16, eight get 2 each); parse threads =
-// cpu_share - reserve (at least 1; reserve only when the share is >= 4), io threads 1 (2 from 16).
+// cpu_share - reserve (at least 1; reserve only when the share is 4..15: from 16 CPUs the ingest /
+// worker / lane threads take ~0.2 cores of the timed region, and a parse thread on every CPU of
+// the share measured +3-4% decoded pictures/s, profiles/r6/threads/), io threads 1 (2 from 16).
 // VEP_INGEST_PARSE_THREADS / VEP_IO_THREADS override the sizes.
 std::vector<HostDomain> plan_host_domains(const std::vector<int>& devices,
                                           const std::vector<std::string>& explicit_cpus = {}, int reserve = 1);

@@ -436,14 +436,15 @@ constexpr int kDefaultLaneQueue = 2;
 constexpr int kDefaultLaneMergeJobs = 64;  // jobs per merged lane launch (lane launcher threads)
 constexpr int kDefaultKfWindowUs = 16000;  // keyframe-only coalescing window (see WorkerOptions)
 constexpr int kAllLevels = 1 << 20;        // (a window holding every level of a round)
-// H.265 intra transform blocks: one persistent ticket-queue launch per round (every intra level;
-// waves take blocks in level order, so a wait is only ever on a block a running wave claimed, and
-// no wait crosses a kernel boundary). 0 = one launch per level, k = windows of k levels (each
-// window polls the previous one's edge words across a launch boundary: under rocprofv3's SQ
-// counter pass that stalled and dropped pictures), -1 = one workgroup per picture. Measured on
-// one box: same end-to-end rate and GPU time as per-level launches with ~150x fewer launches, and
-// 0 pictures dropped under the SQ counter pass (profiles/r4/hevc_sched/).
-constexpr int kDefaultTuWindow = kAllLevels;
+// H.265 intra transform blocks: one launch per intra level (kernel boundaries order the levels;
+// no wave ever polls). kAllLevels (VEP_HEVC_TU_QUEUE=1) = one persistent ticket-queue launch per
+// round (waves take blocks in level order and poll their neighbours' edge words), k = windows of
+// k levels, -1 = one workgroup per picture. Round 6, GPU-side ceiling of 8 x 4K H.265 (--source
+// records, three alternated runs, profiles/r6/hevc_tu/): per-level 2,199 / 2,183 / 2,187
+// pictures/s, GPU 91-93 ms per step; queue 2,087 / 2,068 / 2,052, 94-99 ms; per-picture 353-362.
+// The queue's ~150x fewer launches do not pay for its polling (84% of its wave-cycles waiting,
+// round 5 counters), so per-level launches are the default again.
+constexpr int kDefaultTuWindow = 0;
 
 Worker::Worker(const WorkerOptions& o) : opt_(o), dev_(o.device) {
   mock_serve_ = !dev_.gpu() && (opt_.mock_serve || (std::getenv("VEP_MOCK_SERVE") && std::getenv("VEP_MOCK_SERVE")[0] == '1'));

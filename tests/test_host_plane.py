@@ -24,7 +24,8 @@ def test_plan_splits_the_budget_without_a_cap(native):
     budget = native.cpu_budget()
     one = native.plan_host_domains([-1])
     assert one[0]["cpus"] == aff and one[0]["cpu_share"] == min(budget, len(aff))
-    assert one[0]["parse_threads"] == max(1, one[0]["cpu_share"] - (1 if one[0]["cpu_share"] >= 4 else 0))
+    share = one[0]["cpu_share"]
+    assert one[0]["parse_threads"] == max(1, share - (1 if 4 <= share < 16 else 0))
     if len(aff) >= 2:
         two = native.plan_host_domains([-1, -1])
         assert not set(two[0]["cpus"]) & set(two[1]["cpus"])  # disjoint halves
