@@ -18,8 +18,10 @@ namespace sampler {
 constexpr int kMaxSamples = 1 << 20;
 inline uintptr_t g_samples[kMaxSamples];
 inline std::atomic<int> g_nsamples{0};
+inline volatile bool g_on = true;  // samples are recorded only while set (a body may gate phases)
 
 inline void on_prof(int, siginfo_t*, void* uc) {
+  if (!g_on) return;
   const int i = g_nsamples.fetch_add(1, std::memory_order_relaxed);
   if (i < kMaxSamples) g_samples[i] = uintptr_t(static_cast<ucontext_t*>(uc)->uc_mcontext.gregs[REG_RIP]);
 }

@@ -213,6 +213,9 @@ class MbNeighbours {
   // Spatial direct (§8.4.1.2.2) for list `list`: refIdx = MinPositive over A, B, C and the
   // 16x16 motion-vector predictor for it (mv = 0 when ref < 0), from one neighbour fetch.
   void direct_spatial_pred(int mb, int list, int& ref, int mv[2]) const;
+  // The same for both lists at once, for the MB announced by begin() (B_Skip / B_Direct_16x16:
+  // one fetch of the A / B / C(D) neighbours' motion instead of four motion_at() per list).
+  void direct_spatial_both(int ref[2], int mv[2][2]) const;
   // Swap the state array out (kept as the colocated picture's motion) and start a fresh one.
   std::vector<MbState> take_state() {
     std::vector<MbState> v;
@@ -305,6 +308,59 @@ inline MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done, 
   r.mv[0] = s.mv[list][blk][0];
   r.mv[1] = s.mv[list][blk][1];
   return r;
+}
+
+inline void MbNeighbours::direct_spatial_both(int ref[2], int mv[2][2]) const {
+  // A: the left MB's block 3, B: the above MB's block 12, C: the above-right MB's block 12, or
+  // D (the above-left MB's block 15) when C is unavailable (§8.4.1.3.2 for the whole MB)
+  const int nm[3] = {a_, b_, c_ >= 0 ? c_ : d_};
+  const int nblk[3] = {3, 12, c_ >= 0 ? 12 : 15};
+  bool avail[3];
+  int r[2][3];
+  int v[2][3][2];
+  for (int k = 0; k < 3; ++k) {
+    avail[k] = nm[k] >= 0;
+    for (int l = 0; l < 2; ++l) {
+      r[l][k] = -1;
+      v[l][k][0] = v[l][k][1] = 0;
+    }
+    if (!avail[k]) continue;
+    const MbState& s = st_[size_t(nm[k])];
+    if (is_intra(s.kind)) continue;
+    const int b8 = ((nblk[k] >> 3) << 1) | ((nblk[k] & 3) >> 1);
+    for (int l = 0; l < 2; ++l) {
+      r[l][k] = s.ref[l][b8];
+      if (r[l][k] < 0) continue;
+      v[l][k][0] = s.mv[l][nblk[k]][0];
+      v[l][k][1] = s.mv[l][nblk[k]][1];
+    }
+  }
+  auto minpos = [](int a, int b) { return (a >= 0 && b >= 0) ? (a < b ? a : b) : (a > b ? a : b); };
+  // B and C unavailable, A available: B = C = A for the predictor (after refIdx is chosen)
+  const bool only_a = !avail[1] && !avail[2] && avail[0];
+  for (int l = 0; l < 2; ++l) {
+    const int rf = minpos(r[l][0], minpos(r[l][1], r[l][2]));
+    ref[l] = rf;
+    mv[l][0] = mv[l][1] = 0;
+    if (rf < 0) continue;
+    if (only_a) {
+      mv[l][0] = v[l][0][0];
+      mv[l][1] = v[l][0][1];
+      continue;
+    }
+    const int match = (r[l][0] == rf) + (r[l][1] == rf) + (r[l][2] == rf);
+    if (match == 1) {
+      const int k = r[l][0] == rf ? 0 : (r[l][1] == rf ? 1 : 2);
+      mv[l][0] = v[l][k][0];
+      mv[l][1] = v[l][k][1];
+      continue;
+    }
+    for (int c = 0; c < 2; ++c) {
+      const int a = v[l][0][c], b = v[l][1][c], d = v[l][2][c];
+      const int lo = a < b ? a : b, hi = a < b ? b : a;
+      mv[l][c] = d < lo ? lo : (d > hi ? hi : d);  // median
+    }
+  }
 }
 
 // Motion of a reference picture as the colocated picture of direct prediction (§8.4.1.2.1):

@@ -82,6 +82,20 @@ class MbLayer {
     nbc_ = cf_ == 2 ? 8 : 4;
     weighted_ = (type_ == h264::kP && pps_.weighted_pred) || (type_ == h264::kB && pps_.weighted_bipred_idc != 0);
     implicit_ = type_ == h264::kB && pps_.weighted_bipred_idc == 2;
+    // per-slice lookup tables of emit(): DPB slot by (refIdx + 1) per list (0xFF: refIdx -1 or
+    // no such list entry), QP'C of both chroma components by QP'Y
+    for (int l = 0; l < 2; ++l) {
+      std::fill(std::begin(slot_[l]), std::end(slot_[l]), u8(0xFF));
+      if (const auto* lst = env_.list[l])
+        for (size_t k = 0; k < lst->size() && k + 1 < std::size(slot_[l]); ++k)
+          if ((*lst)[k].slot >= 0) slot_[l][k + 1] = u8((*lst)[k].slot);
+    }
+    for (int q = 0; q < 52 + qpbd_ && q < int(std::size(qpc_tab_[0])); ++q) {
+      qpc_tab_[0][q] = u8(chroma_qp_bd(q - qpbd_, pps_.chroma_qp_index_offset, qpbdc_) + qpbdc_);
+      qpc_tab_[1][q] = u8(chroma_qp_bd(q - qpbd_, pps_.second_chroma_qp_index_offset, qpbdc_) + qpbdc_);
+    }
+    // B_Skip / B_Direct_16x16 take direct16_spatial() (no weights, spatial, 8x8 inference)
+    fast_direct_ = !kWrite && type_ == h264::kB && sh_.direct_spatial && sps_.direct_8x8 && !weighted_;
   }
 
   // entropy sources / sinks (the ones of the mode are used)
@@ -156,7 +170,8 @@ class MbLayer {
     } else {
       s.direct16 = 1;
       s.direct8 = 0xF;
-      direct(mb, s, 0xF);
+      if (fast_direct_) direct16_spatial(mb, s);
+      else direct(mb, s, 0xF);
     }
     prev_qpd_nz = 0;
     emit(mb, s, res, 0, 0, nullptr);
@@ -554,7 +569,8 @@ class MbLayer {
     if (b && mbt == 0) {  // B_Direct_16x16
       s.direct16 = 1;
       s.direct8 = 0xF;
-      direct(mb, s, 0xF);
+      if (fast_direct_) direct16_spatial(mb, s);
+      else direct(mb, s, 0xF);
       return true;
     }
     if ((!b && mbt <= 2) || (b && mbt <= 21)) {
@@ -799,6 +815,49 @@ class MbLayer {
     }
   }
 
+  // direct() for the whole MB (mask 0xF) in the slices fast_direct_ names: spatial mode with
+  // direct_8x8_inference, so each 8x8 takes its outer corner's colocated block and the four 4x4
+  // blocks of an 8x8 share one vector. Same derivation as direct(); both lists' neighbour motion
+  // in one fetch, the colocated picture checked once per slice, vectors written as words.
+  void direct16_spatial(int mb, MbState& s) {
+    if (!dcol_) {  // (the checks of direct(), on the slice's first direct MB)
+      VEP_CHECK(env_.list[1] && !env_.list[1]->empty() && (*env_.list[1])[0].slot >= 0,
+                "direct prediction without a list-1 reference");
+      const ListEntry& c1 = (*env_.list[1])[0];
+      VEP_CHECK(c1.col && c1.col->wmbs == nb_.wmbs() && c1.col->hmbs == nb_.hmbs() && c1.col->corners,
+                "colocated picture motion missing");
+      dcol_ = c1.col;
+      dcol_long_ = c1.long_term;
+    }
+    int ref[2], mvp[2][2];
+    nb_.direct_spatial_both(ref, mvp);
+    const bool zero = ref[0] < 0 && ref[1] < 0;
+    if (zero) ref[0] = ref[1] = 0;
+    u32 pv[2];
+    for (int l = 0; l < 2; ++l) {
+      if (ref[l] >= 0) need_ref(l, ref[l]);
+      const bool use = ref[l] >= 0 && !zero;
+      pv[l] = use ? (u32(u16(mvp[l][0])) | u32(u16(mvp[l][1])) << 16) : 0u;
+      std::memset(s.ref[l], ref[l], 4);
+    }
+    const ColMotion::Blk* cb = &dcol_->b[size_t(mb) * 4];
+    u32 v8[2][4];
+    for (int b8 = 0; b8 < 4; ++b8) {
+      const bool col_zero = !dcol_long_ && cb[b8].ref == 0 && cb[b8].mv[0] >= -1 && cb[b8].mv[0] <= 1 &&
+                            cb[b8].mv[1] >= -1 && cb[b8].mv[1] <= 1;
+      for (int l = 0; l < 2; ++l) v8[l][b8] = (ref[l] == 0 && col_zero) ? 0u : pv[l];
+    }
+    for (int l = 0; l < 2; ++l) {
+      u32 row[2][4];  // the two rows of 4x4 blocks an 8x8 row spans: (b8 0, 0, 1, 1)
+      for (int h = 0; h < 2; ++h) {
+        row[h][0] = row[h][1] = v8[l][2 * h];
+        row[h][2] = row[h][3] = v8[l][2 * h + 1];
+      }
+      u8* mv = reinterpret_cast<u8*>(&s.mv[l][0][0]);
+      for (int y = 0; y < 4; ++y) std::memcpy(mv + 16 * y, row[y >> 1], 16);
+    }
+  }
+
   // ------------------------------------------------------------------ weighted prediction
   WpEntry weights(int r0, int r1) { return wp_entry(env_, r0, r1); }
 
@@ -1034,8 +1093,9 @@ class MbLayer {
     m.kind = s.kind;
     // (biased by QpBdOffset: Picture::qp_bias / qpc_bias; I_PCM: QPY 0)
     m.qp = u8(s.kind == kIPcm ? qpbd_ : s.qp);
-    m.qpc = u8(chroma_qp_bd(m.qp - qpbd_, pps_.chroma_qp_index_offset, qpbdc_) + qpbdc_);
-    m.qpc2 = u8(chroma_qp_bd(m.qp - qpbd_, pps_.second_chroma_qp_index_offset, qpbdc_) + qpbdc_);
+    VEP_CHECK(m.qp < std::size(qpc_tab_[0]), "macroblock QP out of range");
+    m.qpc = qpc_tab_[0][m.qp];
+    m.qpc2 = qpc_tab_[1][m.qp];
     m.i16_mode = u8(i16_mode);
     m.chroma_mode = u8(chroma_mode);
     m.dbk = u8((sh_.disable_deblocking == 1 ? 1 : 0) | (sh_.disable_deblocking == 2 ? 2 : 0));
@@ -1045,15 +1105,12 @@ class MbLayer {
     m.flags = s.t8x8 && s.kind != kI8x8 ? kMbT8x8 : 0;
     if (s.kind == kI8x8) m.flags = kMbT8x8;
     bool l1 = false;
+    const bool intra = is_intra(s.kind);
     for (int k = 0; k < 4; ++k) {
-      m.ref[k] = u8(0xFF);
-      m.ref1[k] = u8(0xFF);
-      if (is_intra(s.kind)) continue;
-      if (s.ref[0][k] >= 0) m.ref[k] = u8((*env_.list[0])[size_t(s.ref[0][k])].slot);
-      if (s.ref[1][k] >= 0) {
-        m.ref1[k] = u8((*env_.list[1])[size_t(s.ref[1][k])].slot);
-        l1 = true;
-      }
+      // (refIdx -1..31 by construction: read_ref() / direct() checked the entry exists)
+      m.ref[k] = intra ? u8(0xFF) : slot_[0][s.ref[0][k] + 1];
+      m.ref1[k] = intra ? u8(0xFF) : slot_[1][s.ref[1][k] + 1];
+      l1 |= !intra && s.ref[1][k] >= 0;
     }
     if (l1) m.flags |= kMbL1;
     // deblocking bS 2: 4x4 blocks with coefficients (8x8 transform: all blocks of the 8x8)
@@ -1103,6 +1160,11 @@ class MbLayer {
   int qp_ = 26;
   bool weighted_ = false, implicit_ = false;
   u16 nz8_ = 0;  // CABAC 8x8 blocks with coefficients (current MB)
+  u8 slot_[2][33];     // DPB slot by refIdx + 1 per list (0xFF: none)
+  u8 qpc_tab_[2][96];  // QP'C (Cb, Cr) by QP'Y
+  bool fast_direct_ = false;
+  const ColMotion* dcol_ = nullptr;  // direct16_spatial(): the checked colocated motion
+  bool dcol_long_ = false;
 };
 
 }  // namespace
