@@ -2053,6 +2053,75 @@ static inline i16* compact16(const i16* p, u32 mask, i16* out) {
 #endif
 }
 
+// Granularity of one list's motion (16 raster 4x4 vectors as words): bit 0 every vector equals
+// block 0's (kMbMv16), bit 1 every vector equals its 8x8's top-left block's (kMbMv8x8).
+static inline u32 motion_uniformity(const i16* mv) {
+#if defined(__AVX2__)
+  const __m256i a = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(mv));       // blocks 0..7
+  const __m256i b = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(mv + 16));  // blocks 8..15
+  const __m256i v0 = _mm256_broadcastd_epi32(_mm256_castsi256_si128(a));
+  const __m256i tl = _mm256_setr_epi32(0, 0, 2, 2, 0, 0, 2, 2);  // top-left block of each 8x8
+  const u32 all = u32(_mm256_movemask_epi8(_mm256_and_si256(_mm256_cmpeq_epi32(a, v0), _mm256_cmpeq_epi32(b, v0))));
+  const u32 q8 = u32(_mm256_movemask_epi8(_mm256_and_si256(_mm256_cmpeq_epi32(a, _mm256_permutevar8x32_epi32(a, tl)),
+                                                           _mm256_cmpeq_epi32(b, _mm256_permutevar8x32_epi32(b, tl)))));
+  return (all == 0xFFFFFFFFu ? 1u : 0u) | (q8 == 0xFFFFFFFFu ? 2u : 0u);
+#else
+  u32 v[16];
+  std::memcpy(v, mv, sizeof v);
+  bool u16 = true, u8x8 = true;
+  for (int b = 1; b < 16; ++b) u16 &= v[b] == v[0];
+  for (int b = 0; b < 16; ++b) u8x8 &= v[b] == v[((b >> 3) << 3) | (b & 2)];
+  return (u16 ? 1u : 0u) | (u8x8 ? 2u : 0u);
+#endif
+}
+
+// The MB's motion into the picture's vector pool at the coarsest granularity that represents
+// every list used exactly (sets m.mv and the kMbMv16 / kMbMv8x8 flag).
+static inline void store_motion(Picture& pic, MbRec& m, const MbState& s) {
+  const int nl = (m.flags & kMbL1) ? 2 : 1;
+  u32 u = 3;
+  for (int l = 0; l < nl; ++l) u &= motion_uniformity(&s.mv[l][0][0]);
+  m.flags |= (u & 1) ? kMbMv16 : ((u & 2) ? kMbMv8x8 : 0);
+  m.mv = u32(pic.mvs.size());
+  const int per = (u & 1) ? 2 : ((u & 2) ? 8 : 32);
+  i16* out = pic.mvs.extend(size_t(per * nl));
+  for (int l = 0; l < nl; ++l, out += per) {
+    const i16* v = &s.mv[l][0][0];
+    if (per == 2) {
+      std::memcpy(out, v, 4);
+    } else if (per == 8) {  // blocks 0, 2, 8, 10
+      std::memcpy(out, v, 4);
+      std::memcpy(out + 2, v + 4, 4);
+      std::memcpy(out + 4, v + 16, 4);
+      std::memcpy(out + 6, v + 20, 4);
+    } else {
+      std::memcpy(out, v, 64);
+    }
+  }
+}
+
+void store_skip_mb(Picture& pic, int mb, MbRec& m, const MbState& s) {
+  m.coef = u32(pic.coefs.size());
+  m.luma_coded = 0;
+  m.chroma_coded = 0;
+  m.wp = 0;
+  m.res = kNoRes;
+  store_motion(pic, m, s);
+  ++pic.inter_mbs;
+  if (!(m.dbk & 1)) pic.deblock = true;
+  // (validate_mb's checks that can fail for a skipped MB: the reference slots)
+  for (int k = 0; k < 4; ++k) {
+    const int r0 = m.ref[k], r1 = m.ref1[k];
+    VEP_CHECK((r0 != 0xFF || r1 != 0xFF) && (r0 == 0xFF || r0 < pic.dpb_slots) && (r1 == 0xFF || r1 < pic.dpb_slots) &&
+                  (r1 == 0xFF || (m.flags & kMbL1)),
+              "skipped macroblock reference slot outside the DPB");
+  }
+  VEP_CHECK(m.qp <= 51 + pic.qp_bias && m.qpc <= 51 + pic.qpc_bias && m.qpc2 <= 51 + pic.qpc_bias,
+            "macroblock QP out of range");
+  pic.mbs[size_t(mb)] = m;
+  if (pic.colb) pic.colb->store(mb, s);
+}
+
 void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm,
               const WpEntry* wp) {
   m.coef = u32(pic.coefs.size());
@@ -2099,33 +2168,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   m.wp = 0;
   m.flags &= u8(~(kMbMv8x8 | kMbMv16));
   if (m.kind == kSkip || m.kind == kInter) {
-    // the coarsest granularity that represents the motion of every list used exactly
-    const int nl = (m.flags & kMbL1) ? 2 : 1;
-    bool u16 = true, u8x8 = true;
-    for (int l = 0; l < nl; ++l) {
-      u32 v[16];
-      std::memcpy(v, &s.mv[l][0][0], sizeof v);
-      for (int b = 1; b < 16; ++b) u16 &= v[b] == v[0];
-      for (int b = 0; b < 16; ++b) {
-        const int c = ((b >> 3) << 3) | (b & 2);  // top-left block of b's 8x8
-        u8x8 &= v[b] == v[c];
-      }
-    }
-    m.flags |= u16 ? kMbMv16 : (u8x8 ? kMbMv8x8 : 0);
-    m.mv = u32(pic.mvs.size());
-    for (int l = 0; l < nl; ++l) {
-      const i16* v = &s.mv[l][0][0];
-      if (u16) {
-        pic.mvs.insert(pic.mvs.end(), v, v + 2);
-      } else if (u8x8) {
-        for (int q = 0; q < 4; ++q) {
-          const int b = (q & 1) * 2 + (q >> 1) * 8;
-          pic.mvs.insert(pic.mvs.end(), v + 2 * b, v + 2 * b + 2);
-        }
-      } else {
-        pic.mvs.insert(pic.mvs.end(), v, v + 32);
-      }
-    }
+    store_motion(pic, m, s);
     if (wp && (m.flags & kMbWp)) {
       m.wp = u32(pic.wps.size());
       pic.wps.insert(pic.wps.end(), wp, wp + 4);

@@ -572,6 +572,9 @@ void dequantize_mb(const MbLevels& lv, bool i16x16, int qp, int qpc, MbResidual&
 // (m.nz is the caller's; wp = 4 WpEntry when m.flags has kMbWp)
 void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual* res, const u8* pcm,
               const WpEntry* wp = nullptr);
+// store_mb() of a skipped MB without weights (P_Skip, B_Skip): `m` holds the header fields
+// (kind, QPs, deblocking, slice, reference slots, kMbL1); no residual.
+void store_skip_mb(Picture& pic, int mb, MbRec& m, const MbState& s);
 void cpu_reconstruct_mb(const Picture& pic, int mb, std::vector<HostSurface>& slots);
 void cpu_deblock(const Picture& pic, HostSurface& target);
 // Neighbour samples for intra prediction from the surface being reconstructed.

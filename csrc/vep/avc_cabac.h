@@ -330,7 +330,8 @@ inline int residual_dec(cabac::Ctx* const ctx, cabac::Decoder& engine, int cbf_i
     } else {
       ++eq1;
     }
-    coef[nzpos[k]] = d.bypass() ? -level : level;
+    const int neg = -int(d.bypass());  // coeff_sign_flag: 0 / -1
+    coef[nzpos[k]] = (level ^ neg) - neg;
   }
   engine = d;
   return num;

@@ -174,7 +174,8 @@ class MbLayer {
       else direct(mb, s, 0xF);
     }
     prev_qpd_nz = 0;
-    emit(mb, s, res, 0, 0, nullptr);
+    if (!weighted_ && !kWrite) emit_skip(mb, s);
+    else emit(mb, s, res, 0, 0, nullptr);
   }
 
   void coded_mb(int mb, bool fresh) {
@@ -541,10 +542,8 @@ class MbLayer {
     int x4, y4, w4, h4, shape;
   };
   static u16 part_mask(const Part& p) {
-    u16 m = 0;
-    for (int y = p.y4; y < p.y4 + p.h4; ++y)
-      for (int x = p.x4; x < p.x4 + p.w4; ++x) m |= u16(1u << (y * 4 + x));
-    return m;
+    static constexpr u16 kRows[5] = {0, 0x1, 0x11, 0x111, 0x1111};  // bit 0 of h4 rows
+    return u16((((1u << p.w4) - 1u) << p.x4) * kRows[p.h4] << (4 * p.y4));
   }
   static void set_mvd(MbState& s, int list, const Part& p, int dx, int dy) {
     const u8 ax = u8(std::min(dx < 0 ? -dx : dx, 127)), ay = u8(std::min(dy < 0 ? -dy : dy, 127));
@@ -1145,6 +1144,29 @@ class MbLayer {
       if (use_wp) m.flags |= kMbWp;
     }
     store_mb(pic_, mb, m, s, &res, pcm, use_wp ? wp : nullptr);
+  }
+
+  // emit() of a skipped MB without weights: the record's header straight from the slice tables
+  void emit_skip(int mb, const MbState& s) {
+    MbRec m{};
+    m.kind = kSkip;
+    m.qp = s.qp;
+    VEP_CHECK(m.qp < std::size(qpc_tab_[0]), "macroblock QP out of range");
+    m.qpc = qpc_tab_[0][m.qp];
+    m.qpc2 = qpc_tab_[1][m.qp];
+    m.dbk = u8((sh_.disable_deblocking == 1 ? 1 : 0) | (sh_.disable_deblocking == 2 ? 2 : 0));
+    m.alpha_off = i8(sh_.alpha_off);
+    m.beta_off = i8(sh_.beta_off);
+    m.slice = s.slice;
+    bool l1 = false;
+    for (int k = 0; k < 4; ++k) {
+      m.ref[k] = slot_[0][s.ref[0][k] + 1];
+      m.ref1[k] = slot_[1][s.ref[1][k] + 1];
+      l1 |= s.ref[1][k] >= 0;
+    }
+    m.flags = l1 ? kMbL1 : 0;
+    nz8_ = 0;
+    store_skip_mb(pic_, mb, m, s);
   }
 
   MbNeighbours& nb_;

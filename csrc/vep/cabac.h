@@ -15,6 +15,8 @@
 
 namespace vep::cabac {
 
+#define VEP_CABAC_INLINE inline __attribute__((always_inline))
+
 // rangeTabLPS[pStateIdx][qRangeIdx] (H.265 Table 9-52 / H.264 Table 9-44).
 inline constexpr u8 kRangeLps[64][4] = {
     {128, 176, 208, 240}, {128, 167, 197, 227}, {128, 158, 187, 216}, {123, 150, 178, 205},
@@ -41,11 +43,8 @@ inline constexpr u8 kNextLps[64] = {
     18, 18, 19, 19, 21, 21, 22, 22, 23, 24, 24, 25, 26, 26, 27, 27, 28, 29, 29, 30, 30, 30,
     31, 32, 32, 33, 33, 33, 34, 34, 35, 35, 35, 36, 36, 36, 37, 37, 37, 38, 38, 63,
 };
-// A context is one u16: pStateIdx << 1 | valMps. (Not a pair of u8: u8 stores may alias any
-// object, so every context update would force the arithmetic decoder's range / offset / bit
-// cache back to memory when the decoder is reached through a pointer.)
-// Both transitions of the packed value in one table for the branch-free decoder:
-// kTrans[is_lps][s] = the next packed value (an LPS in state 0 flips valMps).
+// Packed state s = pStateIdx << 1 | valMps. Both transitions in one table:
+// kTrans[is_lps][s] = the next packed state (an LPS in state 0 flips valMps).
 struct StateTrans {
   u16 t[2][128];
   constexpr StateTrans() : t{} {
@@ -59,12 +58,36 @@ struct StateTrans {
 };
 inline constexpr StateTrans kTrans{};
 
-struct Ctx {
-  u16 s = 0;  // pStateIdx << 1 | valMps
+// A context is one u64 carrying everything a bin needs from it:
+//   bits  0..31  rangeTabLPS[pStateIdx][qRangeIdx 0..3], a byte each
+//   bits 32..38  packed state s (bit 32 = valMps)
+//   bits 40..46  packed state after an LPS, bits 48..54 after an MPS.
+// The LPS range is then a shift of the context word by the range's two quantisation bits (no
+// table load on the range -> range dependency chain), and both successor words are loaded from
+// the context alone while that chain runs, so the outcome only selects one (a cmov): the next
+// bin of the same context waits on a select and a store-forward, not on a load indexed by the
+// outcome. (Not a smaller type: u8/u16 stores may alias any object, and every context update
+// would force the arithmetic decoder's registers back to memory when reached through a pointer.)
+struct CtxWords {
+  u64 e[128];
+  constexpr CtxWords() : e() {
+    for (int s = 0; s < 128; ++s) {
+      const int st = s >> 1;
+      u64 w = 0;
+      for (int q = 0; q < 4; ++q) w |= u64(kRangeLps[st][q]) << (8 * q);
+      w |= u64(s) << 32 | u64(kTrans.t[1][s]) << 40 | u64(kTrans.t[0][s]) << 48;
+      e[s] = w;
+    }
+  }
+};
+inline constexpr CtxWords kCtxWords{};
 
-  int state() const { return s >> 1; }
-  int mps() const { return s & 1; }
-  void set(int state, int mps) { s = u16(state << 1 | mps); }
+struct Ctx {
+  u64 e = kCtxWords.e[0];
+
+  int state() const { return int((e >> 33) & 63); }
+  int mps() const { return int((e >> 32) & 1); }
+  void set(int state, int mps) { e = kCtxWords.e[(state << 1 | mps) & 127]; }
   // §9.3.2.2: initValue -> (pStateIdx, valMps) for SliceQpY.
   void init(int init_value, int qp) {
     const int slope = init_value >> 4, offset = init_value & 15;
@@ -75,18 +98,13 @@ struct Ctx {
     const int mp = pre <= 63 ? 0 : 1;
     set(mp ? pre - 64 : 63 - pre, mp);
   }
-};
-
-// rangeTabLPS indexed by qRangeIdx * 128 + (pStateIdx << 1 | valMps) (the MPS bit duplicates
-// the entries), so the decoder indexes it with the context byte as stored.
-struct RangeLpsFlat {
-  u8 v[4 * 128];
-  constexpr RangeLpsFlat() : v() {
-    for (int q = 0; q < 4; ++q)
-      for (int s = 0; s < 128; ++s) v[q * 128 + s] = kRangeLps[s >> 1][q];
+  // rangeTabLPS[pStateIdx][qRangeIdx] for a range in [256, 510]
+  static VEP_CABAC_INLINE u32 lps_of(u64 e, u32 range) { return u32(e >> ((range >> 3) & 24u)) & 0xFFu; }
+  static VEP_CABAC_INLINE u64 after(u64 e, u32 is_lps) {
+    const u64 el = kCtxWords.e[(e >> 40) & 127], em = kCtxWords.e[(e >> 48) & 127];
+    return is_lps ? el : em;
   }
 };
-inline constexpr RangeLpsFlat kRangeLpsFlat{};
 
 // Arithmetic decoder over an RBSP (byte positions are RBSP offsets). Bits are pulled from a
 // 64-bit MSB-aligned cache (refilled a word at a time) and renormalisation is one clz + shift;
@@ -98,7 +116,6 @@ inline constexpr RangeLpsFlat kRangeLpsFlat{};
 // Hot loops (residual blocks) also work on a local copy of the decoder (`Decoder d = engine;
 // ...; engine = d;`): a copy whose address never escapes (every member is force-inlined) stays
 // in registers for the whole block.
-#define VEP_CABAC_INLINE inline __attribute__((always_inline))
 class Decoder {
  public:
   Decoder(const u8* p, size_t n, size_t bytepos) : p_(p), n_(n) { start(bytepos); }
@@ -113,16 +130,16 @@ class Decoder {
   }
   VEP_CABAC_INLINE u32 decision(Ctx& c) {
     ++nbins_;
-    const u32 s = c.s;
-    // (range & 0xC0) * 2 + (state << 1 | mps): one mask on the range -> LPS dependency chain
-    const u32 lps = kRangeLpsFlat.v[((range_ & 0xC0u) << 1) + s];
+    const u64 e = c.e;
+    const u32 lps = Ctx::lps_of(e, range_);
+    const u64 e_lps = kCtxWords.e[(e >> 40) & 127], e_mps = kCtxWords.e[(e >> 48) & 127];
     const u32 rmps = range_ - lps;
     const u32 is_lps = offset_ >= rmps ? 1u : 0u;
     offset_ -= rmps & (0u - is_lps);
     range_ = is_lps ? lps : rmps;
-    c.s = kTrans.t[is_lps][s];
+    c.e = is_lps ? e_lps : e_mps;
     renorm();
-    return (s & 1u) ^ is_lps;
+    return (u32(e >> 32) & 1u) ^ is_lps;
   }
   // §9.3.3.2.2.3. After a 1 (pcm_flag / end_of_slice_flag) the bit position is exactly the end
   // of the encoder's flush (the flush's final 1 bit included).
@@ -136,11 +153,9 @@ class Decoder {
   VEP_CABAC_INLINE u32 bypass() {
     ++nbins_;
     offset_ = (offset_ << 1) | bits(1);
-    if (offset_ >= range_) {
-      offset_ -= range_;
-      return 1;
-    }
-    return 0;
+    const u32 b = offset_ >= range_ ? 1u : 0u;  // (branch-free: signs are close to random)
+    offset_ -= range_ & (0u - b);
+    return b;
   }
   size_t bitpos() const { return byte_ * 8 - size_t(cbits_); }
   u64 bins() const { return nbins_; }  // bins decoded (decision + bypass + terminate)
@@ -214,14 +229,14 @@ class Encoder {
     outstanding_ = 0;
   }
   void decision(Ctx& c, u32 bin) {
-    const u32 lps = kRangeLps[c.s >> 1][(range_ >> 6) & 3];
+    const u32 lps = Ctx::lps_of(c.e, range_);
     range_ -= lps;
-    const u32 is_lps = bin != u32(c.s & 1) ? 1u : 0u;
+    const u32 is_lps = bin != u32(c.mps()) ? 1u : 0u;
     if (is_lps) {
       low_ += range_;
       range_ = lps;
     }
-    c.s = kTrans.t[is_lps][c.s];
+    c.e = Ctx::after(c.e, is_lps);
     renorm();
   }
   void terminate(u32 bin) {
