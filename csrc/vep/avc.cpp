@@ -18,7 +18,7 @@ using h264::Sps;
 
 // ------------------------------------------------------------------------- MbNeighbours
 
-void MbNeighbours::reset(int wmbs, int hmbs) {
+void MbNeighbours::reset(int wmbs, int hmbs, bool ring) {
   w_ = wmbs;
   h_ = hmbs;
   cur_ = -1;
@@ -29,8 +29,19 @@ void MbNeighbours::reset(int wmbs, int hmbs) {
     stamp_.clear();
   }
   // every field of an MB's state is rewritten when the MB is decoded (MbState{} first), and
-  // begin() stamps the MB with the epoch: nothing to clear here
-  if (st_.size() != n) st_.assign(n, MbState{});
+  // begin() stamps the MB with the epoch and tags its state entry: nothing to clear here
+  size_t ns = n;
+  mask_ = ~size_t(0);
+  if (ring) {  // a power of two >= 2 * (row + 2): the A / B / C / D neighbours are <= row + 1 back
+    size_t r = 1;
+    while (r < 2 * (size_t(wmbs) + 2)) r <<= 1;
+    if (r < n) {
+      ns = r;
+      mask_ = r - 1;
+    }
+  }
+  if (st_.size() != ns) st_.assign(ns, MbState{});
+  if (tag_.size() != ns) tag_.assign(ns, ~0u);
   if (stamp_.size() != n) stamp_.assign(n, 0u);
 }
 
@@ -44,9 +55,9 @@ int MbNeighbours::nc_luma(int mb, int blk) const {
   const int bx = blk & 3, by = blk >> 2;
   int na = -1, nb = -1;
   const int am = mb_at(mb, bx * 4 - 1, by * 4);
-  if (am >= 0) na = coded_count(st_[size_t(am)], bx > 0 ? blk - 1 : blk + 3);
+  if (am >= 0) na = coded_count(st_[size_t(am) & mask_], bx > 0 ? blk - 1 : blk + 3);
   const int bm = mb_at(mb, bx * 4, by * 4 - 1);
-  if (bm >= 0) nb = coded_count(st_[size_t(bm)], by > 0 ? blk - 4 : blk + 12);
+  if (bm >= 0) nb = coded_count(st_[size_t(bm) & mask_], by > 0 ? blk - 4 : blk + 12);
   if (na >= 0 && nb >= 0) return (na + nb + 1) >> 1;
   if (na >= 0) return na;
   if (nb >= 0) return nb;
@@ -56,7 +67,7 @@ int MbNeighbours::nc_luma(int mb, int blk) const {
 int MbNeighbours::nc_chroma(int mb, int c, int blk, int nbc) const {
   const int bx = blk & 1, by = blk >> 1;
   auto count = [&](int m, int b) {
-    const MbState& s = st_[size_t(m)];
+    const MbState& s = st_[size_t(m) & mask_];
     if (s.kind == kSkip) return 0;
     if (s.kind == kIPcm) return 16;
     return int(s.tcc[c][b]);
@@ -76,8 +87,8 @@ int MbNeighbours::pred_intra4x4(int mb, int blk, bool constrained) const {
   const int bx = blk & 3, by = blk >> 2;
   const int am = mb_at(mb, bx * 4 - 1, by * 4), bm = mb_at(mb, bx * 4, by * 4 - 1);
   if (am < 0 || bm < 0) return 2;
-  const MbState& a = st_[size_t(am)];
-  const MbState& b = st_[size_t(bm)];
+  const MbState& a = st_[size_t(am) & mask_];
+  const MbState& b = st_[size_t(bm) & mask_];
   if (constrained && (!is_intra(a.kind) || !is_intra(b.kind))) return 2;
   const int ma = a.kind == kI4x4 ? a.i4[bx > 0 ? blk - 1 : blk + 3] : 2;
   const int mbm = b.kind == kI4x4 ? b.i4[by > 0 ? blk - 4 : blk + 12] : 2;
@@ -92,8 +103,8 @@ int MbNeighbours::pred_intra8x8(int mb, int b8, bool constrained) const {
   const int bx = blk & 3, by = blk >> 2;
   const int am = mb_at(mb, bx * 4 - 1, by * 4), bm = mb_at(mb, bx * 4, by * 4 - 1);
   if (am < 0 || bm < 0) return 2;
-  const MbState& a = st_[size_t(am)];
-  const MbState& b = st_[size_t(bm)];
+  const MbState& a = st_[size_t(am) & mask_];
+  const MbState& b = st_[size_t(bm) & mask_];
   if (constrained && (!is_intra(a.kind) || !is_intra(b.kind))) return 2;
   auto mode = [](const MbState& n, int r, int b8n) -> int {
     if (n.kind == kI8x8) return n.i4[(b8n & 1) * 2 + (b8n >> 1) * 8];
@@ -112,6 +123,7 @@ static int median3(int a, int b, int c) { return a + b + c - std::min({a, b, c})
 void MbNeighbours::pred_mv(int mb, int x4, int y4, int w4, int h4, int list, int ref, u16 done, int shape,
                            int out[2]) const {
   (void)h4;
+  if (mb == cur_ && w4 == 4 && h4 == 4 && shape == 0) return pred_mv16(list, ref, out);  // (x4 = y4 = 0)
   const int x = x4 * 4, y = y4 * 4, w = w4 * 4;
   Nb A = motion_at(mb, x - 1, y, done, list);
   Nb B = motion_at(mb, x, y - 1, done, list);
@@ -137,6 +149,15 @@ void MbNeighbours::pred_mv(int mb, int x4, int y4, int w4, int h4, int list, int
 
 void MbNeighbours::pskip_mv(int mb, int out[2]) const {
   out[0] = out[1] = 0;
+  if (mb == cur_) {  // the announced MB: one neighbour fetch for the checks and the predictor
+    if (a_ < 0 || b_ < 0) return;
+    Nb n[3];
+    nb16(0, n);
+    if ((n[0].ref == 0 && n[0].mv[0] == 0 && n[0].mv[1] == 0) || (n[1].ref == 0 && n[1].mv[0] == 0 && n[1].mv[1] == 0))
+      return;
+    pred_mv16(0, 0, out);
+    return;
+  }
   if (mb_at(mb, -1, 0) < 0 || mb_at(mb, 0, -1) < 0) return;
   const Nb A = motion_at(mb, -1, 0, 0, 0), B = motion_at(mb, 0, -1, 0, 0);
   if ((A.ref == 0 && A.mv[0] == 0 && A.mv[1] == 0) || (B.ref == 0 && B.mv[0] == 0 && B.mv[1] == 0))
@@ -1485,7 +1506,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       pic->au.keyframe = au.keyframe;
       pic->au.corrupt = au.corrupt;
       pic->au.tag = tag;
-      nb_.reset(W, Hp);
+      nb_.reset(W, Hp, true);
       if (sh.field_pic) {  // field slot 2 * frame slot + parity
         const int fs = second_field ? pair_.slot : pick_slot();
         pic->target = 2 * fs + int(sh.bottom_field);
@@ -1561,7 +1582,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
     ColMotion* col_target = colb.col;
     FanOut::shared().run(nunits, [&](int k) {
       SliceUnit& u = *units_[size_t(k)];
-      u.nb.reset(W, H);
+      u.nb.reset(W, H, true);
       Picture& sh = u.shard;
       sh.wmbs = W;
       sh.hmbs = H;

@@ -172,23 +172,32 @@ struct MbState {
 // §9.2.1): availability is "same slice and already decoded".
 class MbNeighbours {
  public:
-  void reset(int wmbs, int hmbs);
+  // ring: keep only the state of the most recent MBs (a power-of-two ring of at least two MB
+  // rows + 2) instead of the whole picture's — every derivation of the decoder reads the current
+  // MB and its A / B / C / D neighbours (at most one row + 1 back), and the colocated motion of
+  // later B pictures is copied out as each MB is stored (ColBuild). The ring (~64 KB at 1080p)
+  // stays cache resident, where the whole picture's state (2 MB) was written and read back through
+  // the cache hierarchy for every picture. The encoders keep the whole picture (build_col_motion).
+  void reset(int wmbs, int hmbs, bool ring = false);
   // Announce the MB being decoded (after its kind and slice are set): caches the A/B/C/D
   // neighbour availability so the per-block derivations below need no division or lookup.
   void begin(int mb);
-  MbState& at(int mb) { return st_[size_t(mb)]; }
-  const MbState& at(int mb) const { return st_[size_t(mb)]; }
+  MbState& at(int mb) { return st_[size_t(mb) & mask_]; }
+  const MbState& at(int mb) const { return st_[size_t(mb) & mask_]; }
   int wmbs() const { return w_; }
   int hmbs() const { return h_; }
   // MB containing luma location (x, y) relative to MB `mb` (x, y may be -1 or >= 16); -1 if not
   // available. For locations inside `mb` itself returns mb.
   int mb_at(int mb, int x, int y) const;
   bool mb_available(int mb, int nb) const {
-    return nb >= 0 && stamp_[size_t(nb)] == epoch_ && st_[size_t(nb)].kind != 0xFF &&
-           st_[size_t(nb)].slice == st_[size_t(mb)].slice;
+    const size_t i = size_t(nb) & mask_;
+    return nb >= 0 && stamp_[size_t(nb)] == epoch_ && tag_[i] == u32(nb) && st_[i].kind != 0xFF &&
+           st_[i].slice == st_[size_t(mb) & mask_].slice;
   }
   // decoded in the current picture (announced by begin() since the last reset())
-  bool decoded(int mb) const { return stamp_[size_t(mb)] == epoch_ && st_[size_t(mb)].kind != 0xFF; }
+  bool decoded(int mb) const {
+    return stamp_[size_t(mb)] == epoch_ && tag_[size_t(mb) & mask_] == u32(mb) && st_[size_t(mb) & mask_].kind != 0xFF;
+  }
   bool announced(int mb) const { return stamp_[size_t(mb)] == epoch_; }
   int announced_count() const { return announced_; }  // distinct MBs announced this picture
   // nC for luma block (raster) `blk` / chroma component c block `blk` (§9.2.1).
@@ -216,13 +225,6 @@ class MbNeighbours {
   // The same for both lists at once, for the MB announced by begin() (B_Skip / B_Direct_16x16:
   // one fetch of the A / B / C(D) neighbours' motion instead of four motion_at() per list).
   void direct_spatial_both(int ref[2], int mv[2][2]) const;
-  // Swap the state array out (kept as the colocated picture's motion) and start a fresh one.
-  std::vector<MbState> take_state() {
-    std::vector<MbState> v;
-    v.swap(st_);
-    stamp_.clear();
-    return v;
-  }
 
  private:
   struct Nb {
@@ -231,6 +233,10 @@ class MbNeighbours {
     int mv[2];
   };
   Nb motion_at(int mb, int x, int y, u16 done, int list) const;  // x, y in luma samples rel. to mb
+  // A, B and C (D when C is unavailable) of the whole announced MB for one list: the
+  // motion_at() results of (-1, 0), (0, -1), (16, -1) / (-1, -1) without the coordinate walk
+  void nb16(int list, Nb n[3]) const;
+  void pred_mv16(int list, int ref, int out[2]) const;  // pred_mv() of the 16x16 partition
   int w_ = 0, h_ = 0;
   int cur_ = -1, cx_ = 0, cy_ = 0, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
   // "decoded in this picture": begin() stamped the MB with the picture's epoch (and its kind is
@@ -238,7 +244,9 @@ class MbNeighbours {
   // state array is 2 MB; the stamps are 32 KB).
   u32 epoch_ = 0;
   int announced_ = 0;
-  std::vector<u32> stamp_;
+  size_t mask_ = ~size_t(0);  // state index = mb & mask_ (all ones: the whole picture)
+  std::vector<u32> stamp_;    // per MB of the picture
+  std::vector<u32> tag_;      // per state entry: the MB whose state it holds (ring)
   std::vector<MbState> st_;
 };
 
@@ -266,6 +274,7 @@ inline void MbNeighbours::begin(int mb) {
     stamp_[size_t(mb)] = epoch_;
     ++announced_;
   }
+  tag_[size_t(mb) & mask_] = u32(mb);
   auto nb = [&](int nx, int ny) {
     if (nx < 0 || nx >= w_ || ny < 0) return -1;
     const int n = ny * w_ + nx;
@@ -301,13 +310,47 @@ inline MbNeighbours::Nb MbNeighbours::motion_at(int mb, int x, int y, u16 done, 
   const int blk = ((y & 15) >> 2) * 4 + ((x & 15) >> 2);
   if (m == mb && !((done >> blk) & 1)) return r;  // partition not yet decoded
   r.avail = true;
-  const MbState& s = st_[size_t(m)];
+  const MbState& s = st_[size_t(m) & mask_];
   if (is_intra(s.kind)) return r;
   r.ref = s.ref[list][((blk >> 3) << 1) | ((blk & 3) >> 1)];
   if (r.ref < 0) return r;  // list unused: refIdx -1, mv 0
   r.mv[0] = s.mv[list][blk][0];
   r.mv[1] = s.mv[list][blk][1];
   return r;
+}
+
+inline void MbNeighbours::nb16(int list, Nb n[3]) const {
+  const int nm[3] = {a_, b_, c_ >= 0 ? c_ : d_};
+  const int nblk[3] = {3, 12, c_ >= 0 ? 12 : 15};
+  for (int k = 0; k < 3; ++k) {
+    n[k] = Nb{nm[k] >= 0, -1, {0, 0}};
+    if (nm[k] < 0) continue;
+    const MbState& s = st_[size_t(nm[k]) & mask_];
+    if (is_intra(s.kind)) continue;
+    const int b8 = ((nblk[k] >> 3) << 1) | ((nblk[k] & 3) >> 1);
+    n[k].ref = s.ref[list][b8];
+    if (n[k].ref < 0) continue;
+    n[k].mv[0] = s.mv[list][nblk[k]][0];
+    n[k].mv[1] = s.mv[list][nblk[k]][1];
+  }
+}
+
+inline void MbNeighbours::pred_mv16(int list, int ref, int out[2]) const {
+  Nb n[3];
+  nb16(list, n);
+  if (!n[1].avail && !n[2].avail && n[0].avail) n[1] = n[2] = n[0];
+  const int match = (n[0].ref == ref) + (n[1].ref == ref) + (n[2].ref == ref);
+  if (match == 1) {
+    const Nb& t = n[0].ref == ref ? n[0] : (n[1].ref == ref ? n[1] : n[2]);
+    out[0] = t.mv[0];
+    out[1] = t.mv[1];
+    return;
+  }
+  for (int c = 0; c < 2; ++c) {
+    const int a = n[0].mv[c], b = n[1].mv[c], d = n[2].mv[c];
+    const int lo = a < b ? a : b, hi = a < b ? b : a;
+    out[c] = d < lo ? lo : (d > hi ? hi : d);  // median
+  }
 }
 
 inline void MbNeighbours::direct_spatial_both(int ref[2], int mv[2][2]) const {
@@ -325,7 +368,7 @@ inline void MbNeighbours::direct_spatial_both(int ref[2], int mv[2][2]) const {
       v[l][k][0] = v[l][k][1] = 0;
     }
     if (!avail[k]) continue;
-    const MbState& s = st_[size_t(nm[k])];
+    const MbState& s = st_[size_t(nm[k]) & mask_];
     if (is_intra(s.kind)) continue;
     const int b8 = ((nblk[k] >> 3) << 1) | ((nblk[k] & 3) >> 1);
     for (int l = 0; l < 2; ++l) {
