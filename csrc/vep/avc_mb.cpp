@@ -12,6 +12,8 @@
 // Reference parity: libavcodec's h264 macroblock decoding behind PyAV `packet.decode()`
 // (python/read_image.py:87).
 #include <algorithm>
+#include <cstddef>
+#include <cstring>
 
 #include "avc_cabac.h"
 #include "avc_cavlc.h"
@@ -135,9 +137,19 @@ class MbLayer {
     }
   }
 
+  // MbState{} except the motion vectors (a skipped MB writes every vector a reader can look at:
+  // list 0 for P_Skip — list 1 of a P slice is never read — and both lists for B_Skip; a coded
+  // MB clears them in coded_mb())
+  static void clear_but_mv(MbState& s) {
+    static const MbState z{};
+    std::memcpy(static_cast<void*>(&s), &z, offsetof(MbState, mv));
+    std::memcpy(static_cast<void*>(&s.mvd), &z.mvd, sizeof(MbState) - offsetof(MbState, mvd));
+  }
+
   bool read_skip_flag(int mb, bool v = false) {
     MbState& s = nb_.at(mb);
-    s = MbState{};
+    if constexpr (kWrite) s = MbState{};
+    else clear_but_mv(s);
     s.slice = u16(env_.slice);
     nb_.begin(mb);
     auto cond = [&](int m) { return m >= 0 && !nb_.at(m).skip ? 1 : 0; };
@@ -184,6 +196,8 @@ class MbLayer {
       s = MbState{};
       s.slice = u16(env_.slice);
       nb_.begin(mb);
+    } else if constexpr (!kWrite) {
+      std::memset(static_cast<void*>(s.mv), 0, sizeof s.mv);  // (read_skip_flag() left them)
     }
     int mbt = read_mb_type(mb, kWrite ? want->mb_type : 0);
     int itype = -1;
@@ -267,10 +281,8 @@ class MbLayer {
   }
 
   // Pictures the slice's MBs reference (list entries that must exist).
-  void need_ref(int list, int idx) {
-    const auto* l = env_.list[list];
-    VEP_CHECK(l && idx >= 0 && idx < int(l->size()) && (*l)[size_t(idx)].slot >= 0,
-              "ref_idx names a missing reference picture");
+  void need_ref(int list, int idx) {  // (slot_: the list's entries with a picture)
+    VEP_CHECK(idx >= 0 && idx < 32 && slot_[list][idx + 1] != 0xFF, "ref_idx names a missing reference picture");
   }
 
  private:
