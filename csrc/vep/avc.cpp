@@ -1350,6 +1350,13 @@ struct Decoder::SliceUnit {
 };
 
 PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
+  struct FenceOnExit {  // the records' non-temporal stores (store_rec) are ordered before the return
+    ~FenceOnExit() {
+#if defined(__x86_64__)
+      _mm_sfence();
+#endif
+    }
+  } fence;
   auto pic = pic_pool_->acquire([](Picture& p) {  // default state, pool capacities kept
     auto mbs = std::move(p.mbs);
     auto coefs = std::move(p.coefs), mvs = std::move(p.mvs);
@@ -1604,6 +1611,9 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       u.colb.uids = &u.uids;
       sh.colb = col_target ? &u.colb : nullptr;
       parse_slice_data(u.nb, sh, u.sh, *u.sps, *u.pps, u.rbsp.data(), u.rbsp.size(), u.bitpos, u.slice_idx, u.list);
+#if defined(__x86_64__)
+      _mm_sfence();  // (the shard's non-temporal record stores, before the join)
+#endif
     });
     parallel_slices_run_ += u64(nunits);
     // merge in slice order: the MBs each slice decoded, pool offsets rebased
@@ -1809,6 +1819,24 @@ void validate(const Picture& p) {
 
 // ------------------------------------------------------------------------- shared internals
 
+// Non-temporal stores of `bytes` (a multiple of 8) from `src` to the 8-byte aligned `dst`: for
+// the parser's write-once outputs (records, colocated motion) that are read next by the GPU or
+// by another picture's parse on another thread — write-allocating them only pulled their lines
+// in for ownership and evicted the parser's working set. Decoder::parse ends with an sfence.
+static inline void stream_words(void* dst, const void* src, size_t bytes) {
+#if defined(__x86_64__)
+  long long w[16];
+  for (size_t o = 0; o < bytes; o += sizeof w) {
+    const size_t n = bytes - o < sizeof w ? bytes - o : sizeof w;
+    std::memcpy(w, static_cast<const char*>(src) + o, n);
+    long long* d = reinterpret_cast<long long*>(static_cast<char*>(dst) + o);
+    for (size_t k = 0; k < n / 8; ++k) _mm_stream_si64(d + k, w[k]);
+  }
+#else
+  std::memcpy(dst, src, bytes);
+#endif
+}
+
 void ColBuild::none(int mb) {
   const int per = col->corners ? 4 : 16;
   ColMotion::Blk* out = &col->b[size_t(mb) * size_t(per)];
@@ -1821,20 +1849,30 @@ void ColBuild::store(int mb, const MbState& st) {
     return;
   }
   static constexpr u8 kCorner[4] = {0, 3, 12, 15};  // outer corner 4x4 block of each 8x8
-  const int per = col->corners ? 4 : 16;
-  ColMotion::Blk* out = &col->b[size_t(mb) * size_t(per)];
   const auto& lu = *uids;
-  for (int k = 0; k < per; ++k) {
-    const int blk = col->corners ? kCorner[k] : k;
+  if (col->corners) {  // 48 bytes per MB, streamed (read next by a later B picture's parse)
+    ColMotion::Blk out[4];
+    for (int k = 0; k < 4; ++k) {
+      const int l = st.ref[0][k] >= 0 ? 0 : 1;
+      const int ri = st.ref[l][k];
+      out[k] = ri < 0 ? ColMotion::Blk{{0, 0}, 0u, i8(-1)}
+                      : ColMotion::Blk{{st.mv[l][kCorner[k]][0], st.mv[l][kCorner[k]][1]},
+                                       size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u, i8(ri)};
+    }
+    stream_words(&col->b[size_t(mb) * 4], out, sizeof out);
+    return;
+  }
+  ColMotion::Blk* out = &col->b[size_t(mb) * 16];
+  for (int blk = 0; blk < 16; ++blk) {
     const int b8 = ((blk >> 3) << 1) | ((blk & 3) >> 1);
     const int l = st.ref[0][b8] >= 0 ? 0 : 1;
     const int ri = st.ref[l][b8];
     if (ri < 0) {
-      out[k] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
+      out[blk] = ColMotion::Blk{{0, 0}, 0u, i8(-1)};
       continue;
     }
-    out[k] = ColMotion::Blk{{st.mv[l][blk][0], st.mv[l][blk][1]},
-                            size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u, i8(ri)};
+    out[blk] = ColMotion::Blk{{st.mv[l][blk][0], st.mv[l][blk][1]},
+                              size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u, i8(ri)};
   }
 }
 
@@ -2121,6 +2159,14 @@ static inline void store_motion(Picture& pic, MbRec& m, const MbState& s) {
   }
 }
 
+// Records leave the parser with non-temporal stores (stream_words): pic.mbs (56 bytes per MB,
+// 457 KB per 1080p picture) is written once and read next by the GPU's record gather over PCIe
+// (or, on the CPU backend, by the reconstruction much later).
+static inline void store_rec(MbRec* dst, const MbRec& m) {
+  static_assert(sizeof(MbRec) % 8 == 0 && sizeof(ColMotion::Blk) * 4 % 8 == 0, "8-byte words");
+  stream_words(dst, &m, sizeof(MbRec));
+}
+
 void store_skip_mb(Picture& pic, int mb, MbRec& m, const MbState& s) {
   m.coef = u32(pic.coefs.size());
   m.luma_coded = 0;
@@ -2139,7 +2185,7 @@ void store_skip_mb(Picture& pic, int mb, MbRec& m, const MbState& s) {
   }
   VEP_CHECK(m.qp <= 51 + pic.qp_bias && m.qpc <= 51 + pic.qpc_bias && m.qpc2 <= 51 + pic.qpc_bias,
             "macroblock QP out of range");
-  pic.mbs[size_t(mb)] = m;
+  store_rec(&pic.mbs[size_t(mb)], m);
   if (pic.colb) pic.colb->store(mb, s);
 }
 
@@ -2205,7 +2251,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   m.res = is_intra(m.kind) && m.kind != kIPcm && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
   if (!(m.dbk & 1)) pic.deblock = true;
   validate_mb(pic, m, true);
-  pic.mbs[size_t(mb)] = m;
+  store_rec(&pic.mbs[size_t(mb)], m);
   if (pic.colb) pic.colb->store(mb, s);
 }
 
