@@ -945,9 +945,8 @@ PYBIND11_MODULE(_vep, m) {
       avc::store_mb(pic, 0, rec, s, &res, nullptr);
       i16 got[avc::kDenseCoefs];
       avc::expand_coefs(pic.coefs.data(), pic.mbs[0], got);
-      // (the MB's words + values, padded to 8-byte words: store_mb keeps the pool's end aligned)
-      const size_t used = size_t(avc::coef_words(pic.mbs[0])) + avc::coef_values(pic.coefs.data(), pic.mbs[0]);
-      bad_avc += std::memcmp(got, want, sizeof got) != 0 || pic.coefs.size() != ((used + 3) & ~size_t(3));
+      bad_avc += std::memcmp(got, want, sizeof got) != 0 ||
+                 pic.coefs.size() != size_t(avc::coef_words(pic.mbs[0])) + avc::coef_values(pic.coefs.data(), pic.mbs[0]);
       // H.265: one TB per size, positions listed in random order
       for (int log2 = 2; log2 <= 5; ++log2) {
         const int nn = 1 << (2 * log2);

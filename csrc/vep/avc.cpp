@@ -1670,7 +1670,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       for (auto& rf : m.ref) rf = u8(cs);
       m.mv = u32(pic->mvs.size());
       m.flags |= kMbMv16;
-      pic->mvs.resize(pic->mvs.size() + 4, 0);  // (one vector, padded: the pool stays 8-byte aligned)
+      pic->mvs.resize(pic->mvs.size() + 2, 0);
       ++pic->inter_mbs;
     } else {
       m.kind = kI16x16;
@@ -2143,8 +2143,7 @@ static inline void store_motion(Picture& pic, MbRec& m, const MbState& s) {
   m.flags |= (u & 1) ? kMbMv16 : ((u & 2) ? kMbMv8x8 : 0);
   m.mv = u32(pic.mvs.size());
   const int per = (u & 1) ? 2 : ((u & 2) ? 8 : 32);
-  alignas(16) i16 buf[64];
-  i16* out = buf;
+  i16* out = pic.mvs.extend(size_t(per * nl));
   for (int l = 0; l < nl; ++l, out += per) {
     const i16* v = &s.mv[l][0][0];
     if (per == 2) {
@@ -2158,11 +2157,6 @@ static inline void store_motion(Picture& pic, MbRec& m, const MbState& s) {
       std::memcpy(out, v, 64);
     }
   }
-  // (padded to 8-byte words: every append to the pool keeps its end 8-byte aligned for the
-  // non-temporal stores; the pad entries are never read)
-  const size_t n = (size_t(per * nl) + 3) & ~size_t(3);
-  if (n > size_t(per * nl)) std::memset(buf + per * nl, 0, (n - size_t(per * nl)) * sizeof(i16));
-  stream_words(pic.mvs.extend(n), buf, n * sizeof(i16));
 }
 
 // Records leave the parser with non-temporal stores (stream_words): pic.mbs (56 bytes per MB,
@@ -2228,15 +2222,14 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
       mask[g] = nonzero_mask16(grp[g]);
       nv += __builtin_popcount(mask[g]);
     }
-    // staged (compact16 writes up to 8 entries of slack past the last value), then streamed to
-    // the pool padded to 8-byte words, so the pool's end stays 8-byte aligned (pad never read)
-    alignas(16) i16 buf[32 + 32 * 16 + 8];
-    std::memcpy(buf, mask, size_t(ng) * sizeof(u16));
-    i16* v = buf + ng;
+    // appended without zero-filling (the pool is reserved per picture), with 8 entries of slack
+    // for the last group's 16-byte stores, trimmed after
+    const size_t o = pic.coefs.size();
+    i16* out = pic.coefs.extend(size_t(ng + nv) + 8);
+    std::memcpy(out, mask, size_t(ng) * sizeof(u16));
+    i16* v = out + ng;
     for (int g = 0; g < ng; ++g) v = compact16(grp[g], mask[g], v);
-    const size_t n = (size_t(ng + nv) + 3) & ~size_t(3);
-    for (size_t k = size_t(ng + nv); k < n; ++k) buf[k] = 0;
-    stream_words(pic.coefs.extend(n), buf, n * sizeof(i16));
+    pic.coefs.resize(o + size_t(ng + nv));
   }
   m.mv = 0;
   m.wp = 0;
