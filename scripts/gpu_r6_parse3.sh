@@ -1,6 +1,6 @@
 #!/bin/bash
-# Round 6 parse A/B #3 on the box CPU: the last commit (ab_so/head.so) vs the tree (ring-buffer
-# MB state, 16x16 MV predictor fast path), alternated at 1 thread x 4 cameras and 16 threads x 32
+# Round 6 parse A/B #3 on the box CPU: commit fe522e0 (ab_so/head.so) vs the tree (ring-buffer
+# MB state, 16x16 MV predictor fast path, skipped MBs without the vector clear), alternated at 1 thread x 4 cameras and 16 threads x 32
 # cameras; then the driver's command on the tree. Output: gpurun_out/$TAG/.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
