@@ -22,6 +22,8 @@ void MbNeighbours::reset(int wmbs, int hmbs, bool ring) {
   w_ = wmbs;
   h_ = hmbs;
   cur_ = -1;
+  run_slice_ = ~0u;
+  run_start_ = 0;
   announced_ = 0;
   const size_t n = size_t(wmbs) * hmbs;
   if (++epoch_ == 0) {  // (after 2^32 pictures) no stale stamp may equal the new epoch

@@ -239,6 +239,8 @@ class MbNeighbours {
   void pred_mv16(int list, int ref, int out[2]) const;  // pred_mv() of the 16x16 partition
   int w_ = 0, h_ = 0;
   int cur_ = -1, cx_ = 0, cy_ = 0, a_ = -1, b_ = -1, c_ = -1, d_ = -1;
+  u32 run_slice_ = ~0u;  // begin(): the slice of the run of consecutively announced MBs
+  int run_start_ = 0;    // ... and its first MB
   // "decoded in this picture": begin() stamped the MB with the picture's epoch (and its kind is
   // set). A new picture bumps the epoch instead of touching every MB's 256-byte state (a 1080p
   // state array is 2 MB; the stamps are 32 KB).
@@ -253,10 +255,12 @@ class MbNeighbours {
 // Hot neighbour derivations, inline (called several times per macroblock).
 inline void MbNeighbours::begin(int mb) {
   int mx, my;
-  if (mb == cur_) {
+  const int prev = cur_;
+  const bool next = mb == prev + 1 && prev >= 0;
+  if (mb == prev) {
     mx = cx_;
     my = cy_;
-  } else if (mb == cur_ + 1 && cur_ >= 0) {  // raster order: no division
+  } else if (next) {  // raster order: no division
     mx = cx_ + 1;
     my = cy_;
     if (mx == w_) {
@@ -275,6 +279,23 @@ inline void MbNeighbours::begin(int mb) {
     ++announced_;
   }
   tag_[size_t(mb) & mask_] = u32(mb);
+  const u32 sl = st_[size_t(mb) & mask_].slice;
+  if (next && sl == run_slice_) {
+    // the next MB of a run announced consecutively in one slice since run_start_ (this
+    // picture): a neighbour is available exactly when it lies in the picture at or after the
+    // run's first MB — every MB from there to mb - 1 is of this slice and decoded, every earlier
+    // one of another slice. The generic test below gives the same answer with four state lookups.
+    const int f = run_start_;
+    a_ = mx > 0 && mb - 1 >= f ? mb - 1 : -1;
+    b_ = my > 0 && mb - w_ >= f ? mb - w_ : -1;
+    c_ = my > 0 && mx + 1 < w_ && mb - w_ + 1 >= f ? mb - w_ + 1 : -1;
+    d_ = my > 0 && mx > 0 && mb - w_ - 1 >= f ? mb - w_ - 1 : -1;
+    return;
+  }
+  if (!(mb == prev && sl == run_slice_)) {  // (the same MB announced again keeps its run)
+    run_slice_ = sl;
+    run_start_ = mb;
+  }
   auto nb = [&](int nx, int ny) {
     if (nx < 0 || nx >= w_ || ny < 0) return -1;
     const int n = ny * w_ + nx;
