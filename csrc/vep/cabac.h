@@ -132,7 +132,10 @@ class Decoder {
     ++nbins_;
     const u64 e = c.e;
     const u32 lps = Ctx::lps_of(e, range_);
-    const u64 e_lps = kCtxWords.e[(e >> 40) & 127], e_mps = kCtxWords.e[(e >> 48) & 127];
+    u64 e_lps = kCtxWords.e[(e >> 40) & 127], e_mps = kCtxWords.e[(e >> 48) & 127];
+    // (both words loaded here, off the bin's chain: without this the compiler selects the
+    // address by the outcome and loads after it, putting the load back on the same-context chain)
+    asm("" : "+r"(e_lps), "+r"(e_mps));
     const u32 rmps = range_ - lps;
     const u32 is_lps = offset_ >= rmps ? 1u : 0u;
     offset_ -= rmps & (0u - is_lps);
@@ -167,21 +170,21 @@ class Decoder {
     offset_ = (offset_ << sh) | bits0(sh);
   }
   VEP_CABAC_INLINE u32 bits(int k) {  // 1 <= k <= 9
-    if (cbits_ < k) refill();
+    if (__builtin_expect(cbits_ < k, 0)) refill();
     const u32 v = u32(cache_ >> (64 - k));
     cache_ <<= k;
     cbits_ -= k;
     return v;
   }
   VEP_CABAC_INLINE u32 bits0(int k) {  // 0 <= k <= 8 (k = 0 reads nothing)
-    if (cbits_ < k) refill();
+    if (__builtin_expect(cbits_ < k, 0)) refill();
     const u32 v = u32((cache_ >> 1) >> (63 - k));
     cache_ <<= k;
     cbits_ -= k;
     return v;
   }
   VEP_CABAC_INLINE void refill() {
-    if (byte_ + 8 <= n_) {  // whole bytes that fit behind the cached bits, one load
+    if (__builtin_expect(byte_ + 8 <= n_, 1)) {  // whole bytes that fit behind the cached bits, one load
       u64 w;
       std::memcpy(&w, p_ + byte_, 8);
       w = __builtin_bswap64(w);
@@ -192,13 +195,27 @@ class Decoder {
       byte_ += size_t(take);
       return;
     }
-    // reading past the end yields zeros (the trailing bits); the caller bounds the walk
-    while (cbits_ <= 56) {
-      const u64 b = byte_ < n_ ? p_[byte_] : 0;
-      ++byte_;
-      cache_ |= b << (56 - cbits_);
-      cbits_ += 8;
+    const Tail t = refill_tail(p_, n_, byte_, cache_, cbits_);
+    byte_ = t.byte;
+    cache_ = t.cache;
+    cbits_ = t.cbits;
+  }
+  // The last bytes of the buffer, out of line (values in and out: the hot loops' register copies
+  // of the decoder never have their address taken). Reading past the end yields zeros (the
+  // trailing bits); the caller bounds the walk.
+  struct Tail {
+    size_t byte;
+    u64 cache;
+    int cbits;
+  };
+  __attribute__((noinline)) static Tail refill_tail(const u8* p, size_t n, size_t byte, u64 cache, int cbits) {
+    while (cbits <= 56) {
+      const u64 b = byte < n ? p[byte] : 0;
+      ++byte;
+      cache |= b << (56 - cbits);
+      cbits += 8;
     }
+    return Tail{byte, cache, cbits};
   }
   const u8* p_;
   size_t n_;
