@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round 6 driver A/B on one box: an earlier build
 # (ab_so/head.so, in a copy of the tree) vs the tree, as the driver's command (without the
-# reference-equivalent run) alternated 3 times each, then parse_ab at 16 threads x 32 cameras.
+# reference-equivalent run) alternated 3 times each, then parse_ab at 1 thread x 4 cameras and 16 threads x 32 cameras.
 # Output: gpurun_out/$TAG/.
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -18,6 +18,10 @@ drv() {  # label dir
 for i in 1 2 3; do
   drv head_$i "$ALT" || exit 1
   drv tree_$i "$R" || exit 1
+done
+for i in 1 2; do
+  timeout -k 10 300 python -u tools/parse_ab.py --so ab_so/head.so --reps 4 2>&1 | tail -1 | sed "s/^/head 1t: /" | tee -a "$O/parse_ab.log" || exit 1
+  timeout -k 10 300 python -u tools/parse_ab.py --reps 4 2>&1 | tail -1 | sed "s/^/tree 1t: /" | tee -a "$O/parse_ab.log" || exit 1
 done
 for i in 1 2; do
   timeout -k 10 300 python -u tools/parse_ab.py --so ab_so/head.so --reps 3 --threads 16 --cams 32 2>&1 | tail -1 | sed "s/^/head 16t: /" | tee -a "$O/parse_ab.log" || exit 1
