@@ -557,21 +557,21 @@ class MbLayer {
     static constexpr u16 kRows[5] = {0, 0x1, 0x11, 0x111, 0x1111};  // bit 0 of h4 rows
     return u16((((1u << p.w4) - 1u) << p.x4) * kRows[p.h4] << (4 * p.y4));
   }
-  // (rows of the partition written as whole words: a byte store may alias anything, so the
-  // per-byte loops reloaded the partition bounds after every store)
   static void set_mvd(MbState& s, int list, const Part& p, int dx, int dy) {
-    const u32 ax = u32(std::min(dx < 0 ? -dx : dx, 127)), ay = u32(std::min(dy < 0 ? -dy : dy, 127));
-    const u16 w = u16(ax | ay << 8);
-    const u16 row[4] = {w, w, w, w};
-    const int x4 = p.x4, w4 = p.w4;
-    for (int y = p.y4, ye = p.y4 + p.h4; y < ye; ++y) std::memcpy(&s.mvd[list][y * 4 + x4][0], row, size_t(w4) * 2);
+    const u8 ax = u8(std::min(dx < 0 ? -dx : dx, 127)), ay = u8(std::min(dy < 0 ? -dy : dy, 127));
+    for (int y = p.y4; y < p.y4 + p.h4; ++y)
+      for (int x = p.x4; x < p.x4 + p.w4; ++x) {
+        s.mvd[list][y * 4 + x][0] = ax;
+        s.mvd[list][y * 4 + x][1] = ay;
+      }
   }
   static void set_mv(MbState& s, int list, const Part& p, int mx, int my) {
     VEP_CHECK(mx >= -32768 && mx <= 32767 && my >= -32768 && my <= 32767, "motion vector out of range");
-    const u32 w = u32(u16(mx)) | u32(u16(my)) << 16;
-    const u32 row[4] = {w, w, w, w};
-    const int x4 = p.x4, w4 = p.w4;
-    for (int y = p.y4, ye = p.y4 + p.h4; y < ye; ++y) std::memcpy(&s.mv[list][y * 4 + x4][0], row, size_t(w4) * 4);
+    for (int y = p.y4; y < p.y4 + p.h4; ++y)
+      for (int x = p.x4; x < p.x4 + p.w4; ++x) {
+        s.mv[list][y * 4 + x][0] = i16(mx);
+        s.mv[list][y * 4 + x][1] = i16(my);
+      }
   }
 
   // Returns noSubMbPartSizeLessThan8x8Flag.
@@ -608,10 +608,9 @@ class MbLayer {
         for (int i = 0; i < np; ++i) {
           if (!((pred[i] >> l) & 1)) continue;
           refs[l][i] = read_ref(mb, l, parts[i].x4, parts[i].y4, kWrite ? want->ref[l][i] : 0);
-          const Part p = parts[i];  // (a copy: the i8 stores below may alias anything)
-          const i8 r = i8(refs[l][i]);
-          for (int y = p.y4 / 2, ye = (p.y4 + p.h4) / 2; y < ye; ++y)
-            for (int x = p.x4 / 2, xe = (p.x4 + p.w4) / 2; x < xe; ++x) s.ref[l][y * 2 + x] = r;
+          const Part& p = parts[i];
+          for (int y = p.y4 / 2; y < (p.y4 + p.h4) / 2; ++y)
+            for (int x = p.x4 / 2; x < (p.x4 + p.w4) / 2; ++x) s.ref[l][y * 2 + x] = i8(refs[l][i]);
         }
       int mvd[2][2][2] = {};
       if constexpr (kWrite) {  // the decoder's predictors in decoding order give the mvds to code
