@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "bind_ext.h"
+#include "vep/h2load.h"
 #include "vep/rpcsrv.h"
 
 namespace py = pybind11;
@@ -91,6 +92,37 @@ void bind_rpc(py::module_& m) {
         return d;
       });
 
+  // Native load generator (csrc/vep/h2load.h): back-to-back VideoLatestImage clients, one TCP
+  // connection each, on `threads` epoll threads; latencies of the measured window in ms.
+  m.def(
+      "h2_load",
+      [](const std::string& host, int port, const std::vector<std::string>& names, int clients, int threads,
+         double start_at, double duration_s, bool key_frame_only) {
+        h2load::Options o;
+        o.host = host;
+        o.port = port;
+        o.names = names;
+        o.clients = clients;
+        o.threads = threads;
+        o.start_at = start_at;
+        o.duration_s = duration_s;
+        o.key_frame_only = key_frame_only;
+        h2load::Result r;
+        {
+          py::gil_scoped_release g;
+          r = h2load::run(o);
+        }
+        py::dict d;
+        d["lat_ms"] = r.lat_ms;
+        d["ok"] = r.ok;
+        d["errors"] = r.errors;
+        d["bytes"] = r.bytes;
+        d["cpu_s"] = r.cpu_s;
+        d["first_error"] = r.first_error;
+        return d;
+      },
+      py::arg("host"), py::arg("port"), py::arg("names"), py::arg("clients"), py::arg("threads") = 2,
+      py::arg("start_at") = 0.0, py::arg("duration_s") = 3.0, py::arg("key_frame_only") = false);
   m.def("hpack_huffman_encode", [](const py::bytes& b) { return py::bytes(rpc::huffman_encode(std::string(b))); });
   m.def("hpack_huffman_decode", [](const py::bytes& b) -> py::object {
     const std::string s = b;

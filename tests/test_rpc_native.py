@@ -187,3 +187,43 @@ def test_native_endpoint_many_clients_share_one_copy(native):
         srv.stop()
         o.stop()
         w.stop()
+
+
+def test_native_load_generator_against_native_endpoint(native):
+    """native.h2_load (csrc/vep/h2load.h): back-to-back VideoLatestImage clients on epoll threads,
+    one connection each, against the native endpoint while a camera publishes ~30 frames/s: every
+    measured request is answered with a frame (no errors), each client gets a newer frame per
+    request (so roughly one per published frame), and the DATA bytes match the frames served."""
+    import time as _time
+
+    tag = f"t{os.getpid()}L"
+    w, o = _owner(native, tag)
+    srv = native.RpcServer("127.0.0.1", 0, tag, io_threads=2, wait_threads=16, slow_threads=2,
+                           handler=_handler([]), reuseport=False)
+    stop = threading.Event()
+    try:
+        cam = w.add_camera("camL", 3)
+        o.add(cam, "camL")
+        enc = synth(native, 320, 240, gop=10)
+        w.decode_now(cam, enc.next())
+
+        def feed():
+            while not stop.is_set():
+                w.decode_now(cam, enc.next())
+                _time.sleep(1 / 30)
+
+        th = threading.Thread(target=feed, daemon=True)
+        th.start()
+        dur = 1.5
+        r = native.h2_load("127.0.0.1", srv.port, ["camL"], clients=6, threads=2,
+                           start_at=_time.time() + 0.5, duration_s=dur)
+        assert r["errors"] == 0, r["first_error"]
+        assert r["ok"] >= 6 * dur * 30 * 0.5, r["ok"]  # each client: about one per published frame
+        assert r["ok"] <= 6 * (dur * 30 + 4)           # never the same frame twice to one client
+        lat = sorted(r["lat_ms"])
+        assert len(lat) == r["ok"] and 0 < lat[len(lat) // 2] < 200
+        assert r["bytes"] >= r["ok"] * 320 * 240 * 3   # BGR24 payloads in the DATA frames
+    finally:
+        stop.set()
+        del srv
+        w.stop()

@@ -108,6 +108,9 @@ def main() -> int:
     ap.add_argument("--duration", type=float, default=4.0)
     ap.add_argument("--cpu", action="store_true", help="CPU backend (no GPU)")
     ap.add_argument("--out", default="", help="also append the JSON lines to this file")
+    ap.add_argument("--client", choices=["grpcio", "native"], default="grpcio",
+                    help="load generator: grpcio clients (Python, parse every VideoFrame) or the native "
+                         "HTTP/2 clients (csrc/vep/h2load.h: count and discard the frame bytes)")
     a = ap.parse_args()
 
     from video_edge_ai_proxy_amd.server.frontend import FrontendPool
@@ -187,7 +190,8 @@ def main() -> int:
                     target = f"127.0.0.1:{fpools[(kind, k)].port}"
                     srv_pids = [fpools[(kind, k)].p.pid]
                 try:
-                    pool.run(target, names, mode="next", duration_s=1.0, procs=procs)  # connect + warm
+                    cmode = "native" if a.client == "native" else "next"
+                    pool.run(target, names, mode=cmode, duration_s=1.0, procs=procs)  # connect + warm
                     pub0, dma0 = owner.published, owner.dma_bytes
                     c0 = psutil.cpu_times()
                     s0 = cpu_of(srv_pids)
@@ -195,7 +199,7 @@ def main() -> int:
                     f0 = sum(w.published(c) for c in cams)
                     h0 = hist_sum(w, cams)
                     t0 = time.perf_counter()
-                    lat = pool.run(target, names, mode="next", duration_s=a.duration, procs=procs)
+                    lat = pool.run(target, names, mode=cmode, duration_s=a.duration, procs=procs)
                     el = time.perf_counter() - t0
                     c1 = psutil.cpu_times()
                     s1 = cpu_of(srv_pids)
@@ -208,7 +212,7 @@ def main() -> int:
                 busy = (c1.user + c1.system) - (c0.user + c0.system)
                 p50, p99 = summarize(lat)
                 served = len(lat) / a.duration
-                r = dict(base, serving=kind, frontends=k, clients=m, client_procs=procs,
+                r = dict(base, serving=kind, frontends=k, clients=m, client_procs=procs, client_impl=a.client,
                          p50_ms=round(p50, 2) if p50 else None, p99_ms=round(p99, 2) if p99 else None,
                          samples=len(lat), frames_served_per_s=round(served, 1),
                          served_gbytes_per_s=round(served * a.width * a.height * 3 / 1e9, 2),
@@ -223,9 +227,12 @@ def main() -> int:
                          # serving CPU seconds per GB served (k > 0: the serving processes alone)
                          serving_cpu_s_per_gb=(round((s1 - s0) / el / (served * a.width * a.height * 3 / 1e9), 3)
                                                if k > 0 and served > 0 else None),
-                         latency_definition="client-side: request sent -> the camera's next VideoFrame "
-                                            "received and parsed (back-to-back requests, includes waiting "
-                                            "for the frame, up to one frame interval)")
+                         latency_definition=("client-side: request sent -> the camera's next VideoFrame "
+                                             + ("received and parsed" if a.client == "grpcio" else
+                                                "received (all DATA bytes, then the trailers; native HTTP/2 "
+                                                "client, bytes counted and discarded)")
+                                             + " (back-to-back requests, includes waiting for the frame, up "
+                                               "to one frame interval)"))
                 if nsrv is not None and k == 0 and kind == "native":
                     r["native_stats"] = nsrv.stats()
                 print(json.dumps(r), flush=True)

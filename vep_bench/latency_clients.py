@@ -68,7 +68,10 @@ class ClientPool:
     def run(self, target: str, names: list[str], mode: str = "next", duration_s: float = 3.0,
             samples: int = 0, key_frame_only: bool = False, procs: int = 0) -> list[float]:
         """Run one job on every process (or the first ``procs``): client k (of procs x threads)
-        asks for camera ``names[k % len(names)]``. Returns every latency sample (ms)."""
+        asks for camera ``names[k % len(names)]``. Returns every latency sample (ms).
+        ``mode="native"``: the ``next`` pattern with the native load generator (``native.h2_load``,
+        csrc/vep/h2load.h) instead of grpcio clients: each process runs its clients as raw HTTP/2
+        connections on two epoll threads, counting and discarding the frame bytes."""
         use = self._p[:procs] if procs > 0 else self._p
         start_at = time.time() + 1.0 + 0.05 * len(use)  # all processes connect first
         for i, p in enumerate(use):
@@ -172,6 +175,17 @@ def main(argv=None) -> int:
         errors: list[str] = []
         if job["mode"] == "serve":
             _client_serve(job["target"], job["names"], job["key_frame_only"], max(1, job["samples"]), lat, errors)
+        elif job["mode"] == "native":
+            from video_edge_ai_proxy_amd import native
+
+            host, port = job["target"].rsplit(":", 1)
+            names = job["names"][:a.threads]
+            r = native.h2_load(host, int(port), names, clients=len(names), threads=min(2, len(names)),
+                               start_at=job["start_at"], duration_s=job["duration"],
+                               key_frame_only=job["key_frame_only"])
+            lat = list(r["lat_ms"])
+            if r["errors"]:
+                errors.append(f"h2_load: {r['errors']} errors ({r['first_error']})")
         else:
             ths = [threading.Thread(target=_client_next, args=(job["target"], n, job["key_frame_only"],
                                                                job["start_at"], job["duration"], lat, errors),
