@@ -57,12 +57,17 @@ int main(int argc, char** argv) {
       avc::Decoder d;
       for (auto& a : aus) types.push_back(d.parse(*a)->info.pict_type);
     }
+    // PROF_CAMS=n: n decoders parse the stream interleaved (cold per-camera state, as the bench's
+    // parse pool sees it)
+    const int pc = std::getenv("PROF_CAMS") ? std::atoi(std::getenv("PROF_CAMS")) : 1;
     sampler::run(std::atof(p), [&] {
-      avc::Decoder d;
-      for (size_t i = 0; i < aus.size(); ++i) {
-        sampler::g_on = !pt || types[i] == pt[0];
-        (void)d.parse(*aus[i]);
-      }
+      std::vector<avc::Decoder> ds(static_cast<size_t>(std::max(1, pc)));
+      std::vector<avc::PicturePtr> keep(ds.size() * 3);
+      for (size_t i = 0; i < aus.size(); ++i)
+        for (size_t c = 0; c < ds.size(); ++c) {
+          sampler::g_on = !pt || types[i] == pt[0];
+          keep[c * 3 + i % 3] = ds[c].parse(*aus[i]);
+        }
       sampler::g_on = true;
     });
     return 0;
