@@ -916,10 +916,17 @@ struct alignas(16) DbkXch {
 constexpr int kDbkLag = 1;  // the second row filters MB x's top edge after the first row's
                             // vertical edges of MB x + 1, in the same step
 constexpr int kDbkDepth = 8;
-constexpr int kDbkRows = kAvcDbkWgRows;
+// (rows per deblocking workgroup: VEP_DBK_WG_ROWS at build time, default kAvcDbkWgRows; the
+// exchange slots between its workgroups are a subset of the kAvcDbkWgRows-row slots that
+// avc_bs_kernel clears for every launch)
+#ifndef VEP_DBK_WG_ROWS
+#define VEP_DBK_WG_ROWS kAvcDbkWgRows
+#endif
+constexpr int kDbkRows = VEP_DBK_WG_ROWS;
 constexpr int kDbkWaves = kDbkRows / 2;
 constexpr u32 kXgFinal = 2u, kXgPartial = 1u;
-static_assert(kDbkRows % 2 == 0 && kDbkDepth > kDbkLag, "deblock wavefront geometry");
+static_assert(kDbkRows % 2 == 0 && kDbkDepth > kDbkLag && kDbkRows % kAvcDbkWgRows == 0 && kDbkRows <= 32,
+              "deblock wavefront geometry");
 
 struct DbkSync {
   u32 progress[kDbkRows];  // MBs finished per row of the workgroup
@@ -1486,7 +1493,7 @@ void launch_avc_bs(const AvcDesc* d_descs, int n, int total_mbs, hipStream_t s) 
 
 void launch_avc_deblock(const AvcDesc* d_descs, int n, int max_hmbs, hipStream_t s, int packed) {
   if (n <= 0 || max_hmbs <= 0) return;
-  const int groups = avc_dbk_groups(max_hmbs);
+  const int groups = (max_hmbs + kDbkRows - 1) / kDbkRows;
   const unsigned blocks = unsigned((n + 7) / 8) * unsigned(groups) * 8u;
   hipLaunchKernelGGL(avc_deblock_kernel, dim3(blocks), dim3(64 * kDbkWaves), 0, s, d_descs, n, groups, packed);
   VEP_HIP(hipGetLastError());
