@@ -20,6 +20,14 @@ int main(int argc, char** argv) {
   c.qp = argc > 5 ? std::atoi(argv[5]) : 27;
   c.gop = 32;
   c.temporal_noise = 2.0;
+  // BENCH=1: the bench's camera streams (bench.py --codec h265: QP 25, texture noise 8, sensor
+  // noise 1.5, 8 slices per picture at 4K)
+  if (std::getenv("BENCH")) {
+    c.qp = argc > 5 ? std::atoi(argv[5]) : 25;
+    c.noise = 8.0;
+    c.temporal_noise = 1.5;
+    c.slices = c.width * c.height >= 3840 * 2160 ? 8 : 1;
+  }
   hevc::HevcEncoder enc(c);
   std::vector<std::shared_ptr<AccessUnit>> aus;
   size_t bytes = 0;

@@ -281,6 +281,15 @@ class CtuLayer {
     }
   }
 
+  // for4() storing one constant byte into a per-4x4 map: a memset per row of 4x4 blocks
+  void fill4(void* map, int x0, int y0, int w, int h, u8 v) {
+    u8* const m = static_cast<u8*>(map);
+    const int xe = std::min(x0 + w, pc_.W), ye = std::min(y0 + h, pc_.H);
+    if (xe <= x0) return;
+    const size_t cnt = size_t((xe - x0 + 3) >> 2);
+    for (int y = y0; y < ye; y += 4) std::memset(m + pc_.i4(x0, y), v, cnt);
+  }
+
   // -------------------------------------------------------------------- coding unit
   void coding_unit(int x0, int y0, int log2, int depth) {
     const int n = 1 << log2;
@@ -296,12 +305,10 @@ class CtuLayer {
     u8* const m_edge = pc_.edge.data();
     u8* const m_cbf = pc_.cbf.data();
     u8* const m_pcm = pc_.pcm.data();
-    for4(x0, y0, n, n, [=](size_t k) {
-      m_depth[k] = u8(depth);
-      m_edge[k] = 0;
-      m_cbf[k] = 0;
-      m_pcm[k] = 0;
-    });
+    fill4(m_depth, x0, y0, n, n, u8(depth));
+    fill4(m_edge, x0, y0, n, n, 0);
+    fill4(m_cbf, x0, y0, n, n, 0);
+    fill4(m_pcm, x0, y0, n, n, 0);
     // CU boundaries are transform and prediction block edges
     for4(x0, y0, 4, n, [=](size_t k) { m_edge[k] |= kEdgeTuV | kEdgePuV; });
     for4(x0, y0, n, 4, [=](size_t k) { m_edge[k] |= kEdgeTuH | kEdgePuH; });
@@ -310,7 +317,7 @@ class CtuLayer {
       cu_.bypass = bin(kCtxTransquantBypass, want.bypass) != 0;
       u8* const m_byp = pc_.bypass.data();
       const u8 bv = u8(cu_.bypass);
-      for4(x0, y0, n, n, [=](size_t k) { m_byp[k] = bv; });
+      fill4(m_byp, x0, y0, n, n, bv);
       if (cu_.bypass) *bypass_ = true;
     }
     bool skip = false;
@@ -321,13 +328,13 @@ class CtuLayer {
       skip = bin(kCtxSkip + inc, want.skip);
     }
     u8* const m_skip = pc_.skip.data();
-    for4(x0, y0, n, n, [=](size_t k) { m_skip[k] = u8(skip); });
+    fill4(m_skip, x0, y0, n, n, u8(skip));
     bool intra = false, pcm = false;
     int part = 0;
     if (skip) {
       cu_.intra = false;
       u8* const m_intra = pc_.intra.data();
-      for4(x0, y0, n, n, [=](size_t k) { m_intra[k] = 0; });
+      fill4(m_intra, x0, y0, n, n, 0);
       prediction_unit(x0, y0, n, n, 0, 0, want.pu[0], true);
       ++st_->skip;
     } else {
@@ -351,7 +358,7 @@ class CtuLayer {
         }
       } else {
         u8* const m_intra = pc_.intra.data();
-        for4(x0, y0, n, n, [=](size_t k) { m_intra[k] = 0; });
+        fill4(m_intra, x0, y0, n, n, 0);
         int r[4][4];
         const int np = pu_rects(part, n, r);
         for (int k = 0; k < np; ++k) prediction_unit(x0 + r[k][0], y0 + r[k][1], r[k][2], r[k][3], k, part, want.pu[k], false);
@@ -384,12 +391,10 @@ class CtuLayer {
     i8* const m_qp = pc_.qp.data();
     u8* const m_done = pc_.done.data();
     u8* const m_rec = pc_.rec.data();
-    for4(x0, y0, n, n, [=](size_t k) {
-      m_qp[k] = i8(q);
-      m_done[k] = 1;
-      m_rec[k] = 1;
-      m_pcm[k] = u8(pcm);
-    });
+    fill4(m_qp, x0, y0, n, n, u8(i8(q)));
+    fill4(m_done, x0, y0, n, n, 1);
+    fill4(m_rec, x0, y0, n, n, 1);
+    fill4(m_pcm, x0, y0, n, n, u8(pcm));
     qp_last_ = q;
     first_qg_ = false;
   }
@@ -1004,7 +1009,7 @@ class CtuLayer {
     }
     HostSurface& s = *pc_.s;
     const int bd = c ? pc_.bd_c : pc_.bd_y;
-    if (lvbuf_.size() < 1024) lvbuf_.resize(1024);
+    if (lvbuf_.size() < 1024) lvbuf_.assign(1024, 0);
     int* lv = lvbuf_.data();
     const int nn = n * n;
     if (kWrite) std::fill(lv, lv + nn, 0);  // (read mode: residual_coding clears what it reads)
@@ -1032,10 +1037,29 @@ class CtuLayer {
         std::copy(t.lv.begin(), t.lv.end(), lv);
         tskip = t.tskip;
       }
-      if constexpr (kWrite) residual_coding(c, log2, lv, tskip);
-      else nnz = residual_coding_rd(c, log2, lv, tskip, nzbuf_);
+      if constexpr (kWrite) {
+        residual_coding(c, log2, lv, tskip);
+      } else {
+        // lv is all zeros between TUs (the read levels are cleared again by position when this
+        // TU is done, below); a decode that threw leaves it dirty and the next one clears it all
+        if (lv_dirty_) std::fill(lv, lv + lvbuf_.size(), 0);
+        lv_dirty_ = true;
+        nnz = residual_coding_rd(c, log2, lv, tskip, nzbuf_);
+      }
       if (tskip) ++st_->tskip;
     }
+    struct LvClear {  // (read mode) the levels of this TU back to zero on every way out
+      int* lv;
+      const u16* pos;
+      const int& n;
+      bool& dirty;
+      bool armed;
+      ~LvClear() {
+        if (!armed) return;
+        for (int j = 0; j < n; ++j) lv[pos[j]] = 0;
+        dirty = false;
+      }
+    } lv_clear{lv, nzbuf_, nnz, lv_dirty_, !kWrite && coded && !dry_};
     bool nz = false;
     if constexpr (kWrite) {
       if (coded || dry_)
@@ -1355,22 +1379,11 @@ class CtuLayer {
     if (scan == 2) std::swap(pos[0], pos[1]);
     const int lx = pos[0], ly = pos[1];
     VEP_CHECK(lx < n && ly < n, "last significant coefficient outside the block");
-    int last_sb = 0, last_pos = 0;
-    {
-      bool ok = false;
-      for (int i = (1 << (2 * nsb)) - 1; i >= 0 && !ok; --i) {
-        int xs, ys;
-        scan_pos(scan, nsb, i, xs, ys);
-        if (xs != (lx >> 2) || ys != (ly >> 2)) continue;
-        const int want = (lx & 3) | ((ly & 3) << 2);
-        for (int k = 15; k >= 0; --k)
-          if (kScan4.s[scan][k] == want) {
-            last_sb = i, last_pos = k, ok = true;
-            break;
-          }
-      }
-    }
-    std::fill(lv, lv + n * n, 0);
+    // the sub-block and position of the last coefficient, by the inverse scans
+    const int xs0 = lx >> 2, ys0 = ly >> 2;
+    const int last_sb = scan == 0 ? kScanDiagInv.s[nsb][xs0 | ys0 << 3] : (scan == 1 ? (ys0 << nsb | xs0) : (xs0 << nsb | ys0));
+    const int last_pos = kScan4Inv.s[scan][(lx & 3) | ((ly & 3) << 2)];
+    // (lv arrives all zeros: the caller's invariant; only the non-zero levels are written)
     const u8* const sc4 = kScan4.s[scan];
     const int cofs = c ? 27 : 0;
     u8 csbf[8][8] = {};
@@ -1550,6 +1563,7 @@ class CtuLayer {
   u64 gpu_avail_ = 0;
   u64 gpu_pend_ = 0;  // reference units the GPU reads from the intra blocks' edge exchange
   std::vector<int> lvbuf_;  // one transform block's levels
+  bool lv_dirty_ = true;    // (read mode) lvbuf_ may hold non-zero levels
   int gpu_level_ = 1;
   std::map<TuKey, TuLevels> levels_;
   GpuPicture* g_;         // records (the picture's, or the slice shard's)

@@ -157,6 +157,24 @@ struct ScanDiag8 {
 };
 inline constexpr ScanDiag8 kScanDiag{};
 
+// Inverse scans: kScan4Inv[scanIdx][x | y << 2] = k, kScanDiagInv[log2 n][x | y << 3] = k.
+struct Scan4Inv {
+  u8 s[3][16];
+  constexpr Scan4Inv() : s{} {
+    for (int t = 0; t < 3; ++t)
+      for (int k = 0; k < 16; ++k) s[t][kScan4.s[t][k]] = u8(k);
+  }
+};
+inline constexpr Scan4Inv kScan4Inv{};
+struct ScanDiag8Inv {
+  u8 s[4][64];
+  constexpr ScanDiag8Inv() : s{} {
+    for (int l = 0; l < 4; ++l)
+      for (int k = 0; k < (1 << (2 * l)); ++k) s[l][kScanDiag.s[l][k]] = u8(k);
+  }
+};
+inline constexpr ScanDiag8Inv kScanDiagInv{};
+
 // ---------------------------------------------------------------------------- intra
 // intraPredAngle for modes 2..34 (index mode - 2) and invAngle for modes 11..25.
 HK_TABLE i8 kIntraAngle[33] = {32,  26,  21,  17,  13,  9,  5,  2,  0,  -2, -5, -9, -13, -17, -21, -26, -32,
