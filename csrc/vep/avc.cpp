@@ -1564,7 +1564,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
     for (int l = 0; l < 2; ++l)
       for (const auto& e : list_[l]) uids[size_t(l)].push_back(e.uid);
     slice_uids.push_back(std::move(uids));
-    colb.uids = &slice_uids.back();
+    colb.set_uids(&slice_uids.back());
     if (par) {  // kept until the access unit's last slice (parsed in parallel below)
       if (units_.size() <= size_t(nunits)) units_.push_back(std::make_unique<SliceUnit>());
       SliceUnit& u = *units_[size_t(nunits++)];
@@ -1610,7 +1610,7 @@ PicturePtr Decoder::parse(const AccessUnit& au, i64 tag, size_t* next_nal) {
       sh.qp_bias = pic->qp_bias;
       sh.qpc_bias = pic->qpc_bias;
       u.colb.col = col_target;
-      u.colb.uids = &u.uids;
+      u.colb.set_uids(&u.uids);
       sh.colb = col_target ? &u.colb : nullptr;
       parse_slice_data(u.nb, sh, u.sh, *u.sps, *u.pps, u.rbsp.data(), u.rbsp.size(), u.bitpos, u.slice_idx, u.list);
 #if defined(__x86_64__)
@@ -1858,8 +1858,7 @@ void ColBuild::store(int mb, const MbState& st) {
       const int l = st.ref[0][k] >= 0 ? 0 : 1;
       const int ri = st.ref[l][k];
       out[k] = ri < 0 ? ColMotion::Blk{{0, 0}, 0u, i8(-1)}
-                      : ColMotion::Blk{{st.mv[l][kCorner[k]][0], st.mv[l][kCorner[k]][1]},
-                                       size_t(ri) < lu[size_t(l)].size() ? lu[size_t(l)][size_t(ri)] : 0u, i8(ri)};
+                      : ColMotion::Blk{{st.mv[l][kCorner[k]][0], st.mv[l][kCorner[k]][1]}, uid_tab[l][ri & 31], i8(ri)};
     }
     stream_words(&col->b[size_t(mb) * 4], out, sizeof out);
     return;

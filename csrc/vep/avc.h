@@ -452,6 +452,12 @@ struct ColMotion {
 struct ColBuild {
   ColMotion* col = nullptr;
   const std::array<std::vector<u32>, 2>* uids = nullptr;  // the current slice's list uids
+  u32 uid_tab[2][32] = {};  // uids by refIdx (0 past the list), filled by set_uids
+  void set_uids(const std::array<std::vector<u32>, 2>* u) {
+    uids = u;
+    for (int l = 0; l < 2; ++l)
+      for (size_t k = 0; k < 32; ++k) uid_tab[l][k] = u && k < (*u)[size_t(l)].size() ? (*u)[size_t(l)][k] : 0u;
+  }
   void store(int mb, const MbState& st);
   void none(int mb);  // intra / concealed: no motion
 };

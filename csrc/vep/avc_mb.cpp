@@ -12,6 +12,7 @@
 // Reference parity: libavcodec's h264 macroblock decoding behind PyAV `packet.decode()`
 // (python/read_image.py:87).
 #include <algorithm>
+#include <memory>
 #include <cstddef>
 #include <cstring>
 
@@ -43,6 +44,18 @@ struct Dequant {
         }
   }
 };
+
+// The LevelScale tables of the slice's scaling lists, rebuilt only when they change (per parse
+// thread: nearly every stream keeps one set of lists).
+const Dequant& dequant_for(const h264::ScalingLists& sl) {
+  thread_local h264::ScalingLists last;
+  thread_local std::unique_ptr<Dequant> dq;
+  if (!dq || std::memcmp(&last, &sl, sizeof sl) != 0) {
+    dq = std::make_unique<Dequant>(sl);
+    last = sl;
+  }
+  return *dq;
+}
 
 inline int scale4(int c, int ls, int qp) {
   return qp >= 24 ? (c * ls) * (1 << (qp / 6 - 4)) : (c * ls + (1 << (3 - qp / 6))) >> (4 - qp / 6);
@@ -1135,7 +1148,8 @@ class MbLayer {
           if (any) nz |= b8_blocks(b8);
         }
     } else {
-      for (int r = 0; r < 16; ++r) nz |= u16(s.tc[r] ? 1u << r : 0u);
+      nz = s.cbf;  // (4x4 transforms: the coded_block_flag bits are exactly the blocks with levels;
+                   // I_PCM: all set, as its total_coeff 16)
     }
     nz8_ = 0;
     m.nz = nz;
@@ -1265,7 +1279,7 @@ WpEntry wp_entry(const SliceEnv& env, int r0, int r1) {
 void decode_slice_generic(MbNeighbours& nb, Picture& pic, const SliceEnv& env, const u8* data, size_t n,
                           size_t bitpos) {
   const SliceHdr& sh = *env.sh;
-  const Dequant dq(env.scaling);
+  const Dequant& dq = dequant_for(env.scaling);
   const int total = pic.nmbs();
   int mb = sh.first_mb;
   VEP_CHECK(mb < total, "first_mb_in_slice past end of picture");
