@@ -315,17 +315,7 @@ inline int residual_dec(cabac::Ctx* const ctx, cabac::Decoder& engine, int cbf_i
     if (d.decision(absc[gt1 != 0 ? 0 : (eq1 < 3 ? eq1 + 1 : 4)])) {
       cabac::Ctx& cx = absc[5 + (gt1 < gt1_max ? gt1 : gt1_max)];
       int v = 1;
-      // (the prefix's bins all use one context: its word stays in a register across them
-      // instead of a store and a store-forwarded reload per bin)
-      u64 ce = cx.e;
-      while (v < 14) {
-        u64 nx;
-        const u32 b = d.decision_word(ce, nx);
-        ce = nx;
-        if (!b) break;
-        ++v;
-      }
-      cx.e = ce;
+      while (v < 14 && d.decision(cx)) ++v;
       if (v >= 14) {  // UEG0 suffix
         int kk = 0;
         while (d.bypass()) {

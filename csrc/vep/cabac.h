@@ -129,15 +129,8 @@ class Decoder {
     offset_ = bits(9);
   }
   VEP_CABAC_INLINE u32 decision(Ctx& c) {
-    u64 next;
-    const u32 b = decision_word(c.e, next);
-    c.e = next;
-    return b;
-  }
-  // decision() on a context word held by the caller: returns the bin, the updated word in `next`
-  // (a run of bins of one context keeps its word in a register)
-  VEP_CABAC_INLINE u32 decision_word(u64 e, u64& next) {
     ++nbins_;
+    const u64 e = c.e;
     const u32 lps = Ctx::lps_of(e, range_);
     u64 e_lps = kCtxWords.e[(e >> 40) & 127], e_mps = kCtxWords.e[(e >> 48) & 127];
     // (both words loaded here, off the bin's chain: without this the compiler selects the
@@ -147,7 +140,7 @@ class Decoder {
     const u32 is_lps = offset_ >= rmps ? 1u : 0u;
     offset_ -= rmps & (0u - is_lps);
     range_ = is_lps ? lps : rmps;
-    next = is_lps ? e_lps : e_mps;
+    c.e = is_lps ? e_lps : e_mps;
     renorm();
     return (u32(e >> 32) & 1u) ^ is_lps;
   }
