@@ -1808,6 +1808,42 @@ static inline void validate_mb(const Picture& p, const MbRec& m, bool written = 
   VEP_CHECK(m.res == kNoRes || (is_intra(m.kind) && m.res < u32(p.intra_res)), "residual slot out of range");
 }
 
+// validate_mb(p, m, true) as one branch-free verdict (store_mb's per-MB check): every condition
+// folded into one flag, the detailed check (and its message) only when something fails.
+static inline void validate_written_mb(const Picture& p, const MbRec& m) {
+  const size_t ncoef = p.coefs.size(), nmv = p.mvs.size();
+  bool ok = (m.kind <= kI8x8) & (p.cf == 2 || m.chroma_coded < 0x100) & (m.qp <= 51 + p.qp_bias) &
+            (m.qpc <= 51 + p.qpc_bias) & (m.qpc2 <= 51 + p.qpc_bias);
+  if (m.kind != kIPcm) {
+    ok &= size_t(m.coef) + size_t(coef_words(m)) <= ncoef;
+    ok &= (m.chroma_mode <= 3) & (m.i16_mode <= 3);
+    if (m.flags & kMbT8x8)
+      for (int q = 0; q < 4; ++q) {
+        const u32 g = (u32(m.luma_coded) >> ((q & 1) * 2 + (q >> 1) * 8)) & 0x33u;
+        ok &= (g == 0) | (g == 0x33u);
+      }
+    if (m.kind == kSkip || m.kind == kInter) {
+      ok &= size_t(m.mv) + size_t(mv_per_list(m.flags)) * ((m.flags & kMbL1) ? 2 : 1) <= nmv;
+      u32 r0w, r1w;
+      std::memcpy(&r0w, m.ref, 4);
+      std::memcpy(&r1w, m.ref1, 4);
+      for (int k = 0; k < 4; ++k) {
+        const u32 r0 = (r0w >> (8 * k)) & 0xFFu, r1 = (r1w >> (8 * k)) & 0xFFu;
+        ok &= (r0 != 0xFF) | (r1 != 0xFF);
+        ok &= (r0 == 0xFF) | (r0 < u32(p.dpb_slots));
+        ok &= (r1 == 0xFF) | (r1 < u32(p.dpb_slots));
+        ok &= (r1 == 0xFF) | ((m.flags & kMbL1) != 0);
+      }
+      if (m.flags & kMbWp) ok &= size_t(m.wp) + 4 <= p.wps.size();
+    } else if (m.kind == kI4x4 || m.kind == kI8x8) {
+      for (u8 b : m.i4) ok &= ((b & 15) <= 8) & ((b >> 4) <= 8);
+      if (m.kind == kI8x8) ok &= (m.flags & kMbT8x8) != 0;
+    }
+    ok &= m.res == kNoRes || (is_intra(m.kind) && m.res < u32(p.intra_res));
+  }
+  if (!ok) validate_mb(p, m, true);  // (throws, naming the failed check)
+}
+
 static void validate_picture(const Picture& p) {
   VEP_CHECK(p.dpb_slots >= 1 && p.dpb_slots <= kMaxDpbSlots && p.target >= 0 && p.target < p.dpb_slots,
             "picture DPB slots out of range");
@@ -2251,7 +2287,7 @@ void store_mb(Picture& pic, int mb, MbRec m, const MbState& s, const MbResidual*
   }
   m.res = is_intra(m.kind) && m.kind != kIPcm && (m.luma_coded | m.chroma_coded) ? u32(pic.intra_res++) : kNoRes;
   if (!(m.dbk & 1)) pic.deblock = true;
-  validate_mb(pic, m, true);
+  validate_written_mb(pic, m);
   store_rec(&pic.mbs[size_t(mb)], m);
   if (pic.colb) pic.colb->store(mb, s);
 }

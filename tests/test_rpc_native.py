@@ -215,11 +215,13 @@ def test_native_load_generator_against_native_endpoint(native):
         th = threading.Thread(target=feed, daemon=True)
         th.start()
         dur = 1.5
+        p0 = w.published(cam)
         r = native.h2_load("127.0.0.1", srv.port, ["camL"], clients=6, threads=2,
                            start_at=_time.time() + 0.5, duration_s=dur)
-        assert r["errors"] == 0, r["first_error"]
-        assert r["ok"] >= 6 * dur * 30 * 0.5, r["ok"]  # each client: about one per published frame
-        assert r["ok"] <= 6 * (dur * 30 + 4)           # never the same frame twice to one client
+        pub = w.published(cam) - p0  # frames published from the warm-up to the end (the window and
+        assert r["errors"] == 0, r["first_error"]  # its 0.5 s lead-in; fewer on a loaded machine)
+        assert pub > 4 and r["ok"] >= 6 * (pub * dur / (dur + 0.5) - 4) * 0.5, (r["ok"], pub)
+        assert r["ok"] <= 6 * (pub + 2)  # never the same frame twice to one client
         lat = sorted(r["lat_ms"])
         assert len(lat) == r["ok"] and 0 < lat[len(lat) // 2] < 200
         assert r["bytes"] >= r["ok"] * 320 * 240 * 3   # BGR24 payloads in the DATA frames
