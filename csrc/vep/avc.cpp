@@ -2213,18 +2213,15 @@ void store_skip_mb(Picture& pic, int mb, MbRec& m, const MbState& s) {
   store_motion(pic, m, s);
   ++pic.inter_mbs;
   if (!(m.dbk & 1)) pic.deblock = true;
-  // (validate_mb's checks that can fail for a skipped MB: the reference slots and QPs, as one
-  // branch-free verdict)
-  u32 r0w, r1w;
-  std::memcpy(&r0w, m.ref, 4);
-  std::memcpy(&r1w, m.ref1, 4);
-  bool ok = (m.qp <= 51 + pic.qp_bias) & (m.qpc <= 51 + pic.qpc_bias) & (m.qpc2 <= 51 + pic.qpc_bias);
+  // (validate_mb's checks that can fail for a skipped MB: the reference slots)
   for (int k = 0; k < 4; ++k) {
-    const u32 r0 = (r0w >> (8 * k)) & 0xFFu, r1 = (r1w >> (8 * k)) & 0xFFu;
-    ok &= ((r0 != 0xFF) | (r1 != 0xFF)) & ((r0 == 0xFF) | (r0 < u32(pic.dpb_slots))) &
-          ((r1 == 0xFF) | (r1 < u32(pic.dpb_slots))) & ((r1 == 0xFF) | ((m.flags & kMbL1) != 0));
+    const int r0 = m.ref[k], r1 = m.ref1[k];
+    VEP_CHECK((r0 != 0xFF || r1 != 0xFF) && (r0 == 0xFF || r0 < pic.dpb_slots) && (r1 == 0xFF || r1 < pic.dpb_slots) &&
+                  (r1 == 0xFF || (m.flags & kMbL1)),
+              "skipped macroblock reference slot outside the DPB");
   }
-  VEP_CHECK(ok, "skipped macroblock reference slot outside the DPB or QP out of range");
+  VEP_CHECK(m.qp <= 51 + pic.qp_bias && m.qpc <= 51 + pic.qpc_bias && m.qpc2 <= 51 + pic.qpc_bias,
+            "macroblock QP out of range");
   store_rec(&pic.mbs[size_t(mb)], m);
   if (pic.colb) pic.colb->store(mb, s);
 }

@@ -295,8 +295,7 @@ class MbLayer {
 
   // Pictures the slice's MBs reference (list entries that must exist).
   void need_ref(int list, int idx) {  // (slot_: the list's entries with a picture)
-    const u32 i = u32(idx);  // (one branch: -1 and >= 32 fail the range half, the table read stays in bounds)
-    VEP_CHECK((i < 32u) & (slot_[list][(i & 31u) + 1] != 0xFF), "ref_idx names a missing reference picture");
+    VEP_CHECK(idx >= 0 && idx < 32 && slot_[list][idx + 1] != 0xFF, "ref_idx names a missing reference picture");
   }
 
  private:
@@ -580,7 +579,7 @@ class MbLayer {
       }
   }
   static void set_mv(MbState& s, int list, const Part& p, int mx, int my) {
-    VEP_CHECK(((u32(mx + 32768) | u32(my + 32768)) >> 16) == 0, "motion vector out of range");
+    VEP_CHECK(mx >= -32768 && mx <= 32767 && my >= -32768 && my <= 32767, "motion vector out of range");
     for (int y = p.y4; y < p.y4 + p.h4; ++y)
       for (int x = p.x4; x < p.x4 + p.w4; ++x) {
         s.mv[list][y * 4 + x][0] = i16(mx);
