@@ -2196,19 +2196,11 @@ static inline void store_motion(Picture& pic, MbRec& m, const MbState& s) {
   }
 }
 
-// Records leave the parser with non-temporal stores (stream_words): pic.mbs (64 bytes per MB,
+// Records leave the parser with non-temporal stores (stream_words): pic.mbs (56 bytes per MB,
 // 457 KB per 1080p picture) is written once and read next by the GPU's record gather over PCIe
 // (or, on the CPU backend, by the reconstruction much later).
 static inline void store_rec(MbRec* dst, const MbRec& m) {
-  static_assert(sizeof(MbRec) == 64 && sizeof(ColMotion::Blk) * 4 % 8 == 0, "record stores");
-#if defined(__SSE2__)
-  if ((reinterpret_cast<uintptr_t>(dst) & 15) == 0) {  // a whole line in four 16-byte stores
-    const __m128i* s = reinterpret_cast<const __m128i*>(&m);
-    __m128i* d = reinterpret_cast<__m128i*>(dst);
-    for (int k = 0; k < 4; ++k) _mm_stream_si128(d + k, _mm_loadu_si128(s + k));
-    return;
-  }
-#endif
+  static_assert(sizeof(MbRec) % 8 == 0 && sizeof(ColMotion::Blk) * 4 % 8 == 0, "8-byte words");
   stream_words(dst, &m, sizeof(MbRec));
 }
 

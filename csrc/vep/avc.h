@@ -8,7 +8,7 @@
 // Split of work (MI355X-first):
 //  * CPU (`Decoder::parse`): the inherently serial entropy layer — slice headers, mb_type,
 //    prediction modes, motion-vector prediction (incl. direct modes), residual levels and
-//    dequantisation — into a compact per-picture record array (`Picture`: 64-byte MbRec per MB
+//    dequantisation — into a compact per-picture record array (`Picture`: 56-byte MbRec per MB
 //    + a pool of dequantised coefficient blocks + a motion-vector pool + a weight pool), and the
 //    DPB / reference-list / output-order bookkeeping (which GPU surface holds which picture).
 //  * GPU (gpu_avc.hip): everything that touches samples — motion compensation (bi-predictive and

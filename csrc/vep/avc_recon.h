@@ -34,7 +34,7 @@ using i16 = int16_t;
 using i8 = int8_t;
 
 // ------------------------------------------------------------------------------ MB records
-// One macroblock of a parsed picture, as shipped to the GPU (64 bytes, one cache line).
+// One macroblock of a parsed picture, as shipped to the GPU (56 bytes).
 enum MbKind : u8 { kSkip = 0, kInter = 1, kI4x4 = 2, kI16x16 = 3, kIPcm = 4, kI8x8 = 5 };
 VEP_HD bool is_intra(u8 k) { return k >= kI4x4; }
 // intra MBs reconstructed by the wavefront (prediction from reconstructed neighbours)
@@ -81,10 +81,9 @@ struct MbRec {
   u32 res;          // intra MBs with residual: slot of their 384 residual samples (GPU scratch,
                     // filled by the parallel pass); kNoRes otherwise
   u32 wp;           // kMbWp: first of 4 WpEntry in the picture's weight pool
-  u32 pad2, pad3, pad4;  // (one record per 64-byte line: whole-line non-temporal stores on the
-                         // host, line-aligned loads in the kernels)
+  u32 pad2;
 };
-static_assert(sizeof(MbRec) == 64, "MbRec layout");
+static_assert(sizeof(MbRec) == 56, "MbRec layout");
 constexpr u32 kNoRes = 0xFFFFFFFFu;
 
 // i16 entries per list of an MB's motion (2, 8 or 32).
