@@ -981,13 +981,32 @@ VEP_HD int chroma_epel(const P* uv, int pitch, int w, int h, int c, int xi, int 
 VEP_HD bool mv_far(const i16* a, const i16* b, int ylim = 4) {
   return iabs(a[0] - b[0]) >= 4 || iabs(a[1] - b[1]) >= ylim;
 }
+// The fields of one MB record the bS decision reads, as scalars: the reference-slot arrays
+// become words (their bytes read by a shift), so a GPU lane keeps the side in registers
+// rather than taking the address of a local record.
+struct BsSide {
+  u32 ref, ref1;
+  u16 nz;
+  u8 kind, flags;
+};
+VEP_HD BsSide bs_side(const MbRec& m) {
+  BsSide s;
+  __builtin_memcpy(&s.ref, m.ref, 4);
+  __builtin_memcpy(&s.ref1, m.ref1, 4);
+  s.nz = m.nz;
+  s.kind = m.kind;
+  s.flags = m.flags;
+  return s;
+}
+VEP_HD int word_byte(u32 w, int i) { return int((w >> (8 * i)) & 0xFFu); }
+
 // (the non-intra part: coefficients, reference pictures, vectors)
-VEP_HD int boundary_strength_mv(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
+VEP_HD int boundary_strength_mv(BsSide mp, int bp, const i16* mv_p, BsSide mq, int bq,
                                 const i16* mv_q, int ylim) {
   if (((mp.nz >> bp) & 1) || ((mq.nz >> bq) & 1)) return 2;
   const int p8 = ((bp >> 3) << 1) | ((bp & 3) >> 1), q8 = ((bq >> 3) << 1) | ((bq & 3) >> 1);
-  const int p0 = byte_at(mp.ref, p8), p1 = (mp.flags & kMbL1) ? byte_at(mp.ref1, p8) : 0xFF;
-  const int q0 = byte_at(mq.ref, q8), q1 = (mq.flags & kMbL1) ? byte_at(mq.ref1, q8) : 0xFF;
+  const int p0 = word_byte(mp.ref, p8), p1 = (mp.flags & kMbL1) ? word_byte(mp.ref1, p8) : 0xFF;
+  const int q0 = word_byte(mq.ref, q8), q1 = (mq.flags & kMbL1) ? word_byte(mq.ref1, q8) : 0xFF;
   const int np = (p0 != 0xFF) + (p1 != 0xFF), nq = (q0 != 0xFF) + (q1 != 0xFF);
   if (np != nq) return 1;
   const i16* pa = mv_p + mv_sub(mp.flags, 0, bp);  // list 0 of P
@@ -1008,11 +1027,16 @@ VEP_HD int boundary_strength_mv(const MbRec& mp, int bp, const i16* mv_p, const 
   return ((mv_far(pa, qa, ylim) || mv_far(pb, qb, ylim)) && (mv_far(pa, qb, ylim) || mv_far(pb, qa, ylim))) ? 1 : 0;
 }
 
-VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
+VEP_HD int boundary_strength(BsSide mp, int bp, const i16* mv_p, BsSide mq, int bq,
                              const i16* mv_q, bool mb_edge, bool field = false, bool vertical = true) {
   if (is_intra(mp.kind) || is_intra(mq.kind)) return (mb_edge && (vertical || !field)) ? 4 : 3;
   if (field) return boundary_strength_mv(mp, bp, mv_p, mq, bq, mv_q, 2);
   return boundary_strength_mv(mp, bp, mv_p, mq, bq, mv_q, 4);
+}
+
+VEP_HD int boundary_strength(const MbRec& mp, int bp, const i16* mv_p, const MbRec& mq, int bq,
+                             const i16* mv_q, bool mb_edge, bool field = false, bool vertical = true) {
+  return boundary_strength(bs_side(mp), bp, mv_p, bs_side(mq), bq, mv_q, mb_edge, field, vertical);
 }
 
 struct EdgeParams {

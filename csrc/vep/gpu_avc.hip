@@ -827,31 +827,44 @@ __global__ __launch_bounds__(256) void avc_bs_kernel(const AvcDesc* __restrict__
   const MbRec q = rec(d, mb);
   AvcDbkInfo info{};
   if (!(q.dbk & 1)) {
-    const MbRec lm = x > 0 ? rec(d, mb - 1) : q;
-    const MbRec tm = row > 0 ? rec(d, mb - W) : q;
+    // (absent neighbours read as the MB itself, by index: a select between a loaded record and
+    // the local q takes q's address and puts it in scratch)
+    const MbRec lm = rec(d, x > 0 ? mb - 1 : mb);
+    const MbRec tm = rec(d, row > 0 ? mb - W : mb);
     const bool left = x > 0 && !((q.dbk & 2) && lm.slice != q.slice);
     const bool top = row > 0 && !((q.dbk & 2) && tm.slice != q.slice);
     const i16* mq = avc::is_intra(q.kind) ? nullptr : d.mvs + size_t(q.mv);
     const i16* ml = avc::is_intra(lm.kind) ? nullptr : d.mvs + size_t(lm.mv);
     const i16* mt = avc::is_intra(tm.kind) ? nullptr : d.mvs + size_t(tm.mv);
     const bool t8 = (q.flags & avc::kMbT8x8) != 0;
+    const avc::BsSide sq = avc::bs_side(q), sl = avc::bs_side(lm), st = avc::bs_side(tm);
+    // (the 32 nibbles gathered in two 64-bit registers, one per direction: an index into
+    // info.bs that varies with the loop counters put the whole struct in scratch memory)
+    u64 bsw[2] = {0, 0};
     for (int dir = 0; dir < 2; ++dir)
       for (int e = 0; e < 4; ++e) {
         if (e == 0 && !(dir == 0 ? left : top)) continue;
         // no 4x4 edges inside 8x8 transform blocks — except, in 4:2:2, the horizontal ones the
         // chroma filters (avc_hbd_kernel skips them for luma)
         if ((e & 1) && t8 && !(d.cf == 2 && dir == 1)) continue;
-        const MbRec& p = e > 0 ? q : (dir == 0 ? lm : tm);
+        // (the sides as scalar words, selected by value: a record chosen at run time among
+        // locals, or a pointer into one, needs their addresses and puts them in scratch)
+        const avc::BsSide p = e > 0 ? sq : (dir == 0 ? sl : st);
         const i16* mp = e > 0 ? mq : (dir == 0 ? ml : mt);
         for (int sg = 0; sg < 4; ++sg) {
           const int bq = dir == 0 ? sg * 4 + e : e * 4 + sg;
           const int bp = e > 0 ? (dir == 0 ? bq - 1 : bq - 4) : (dir == 0 ? bq + 3 : bq + 12);
-          const int bs = avc::boundary_strength(p, bp, mp, q, bq, mq, e == 0, d.field != 0, dir == 0);
-          const int i = dir * 16 + e * 4 + sg;
-          info.bs[i >> 3] |= u32(bs) << (4 * (i & 7));
+          const int bs = avc::boundary_strength(p, bp, mp, sq, bq, mq, e == 0, d.field != 0, dir == 0);
+          const u64 v = u64(bs) << (4 * (e * 4 + sg));
+          if (dir == 0) bsw[0] |= v;
+          else bsw[1] |= v;
         }
       }
-    info.any = (info.bs[0] | info.bs[1] | info.bs[2] | info.bs[3]) ? 1 : 0;
+    info.bs[0] = u32(bsw[0]);
+    info.bs[1] = u32(bsw[0] >> 32);
+    info.bs[2] = u32(bsw[1]);
+    info.bs[3] = u32(bsw[1] >> 32);
+    info.any = (bsw[0] | bsw[1]) ? 1 : 0;
     // thresholds at 8-bit scale (QPs less the QpBdOffset bias; avc_hbd_kernel shifts them by
     // bd - 8)
     // (the P-side record by value select, not through an array of pointers to the locals, which
